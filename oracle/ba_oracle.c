@@ -1,0 +1,287 @@
+/*
+ * oracle/ba_oracle.c -- TEST INFRASTRUCTURE ONLY (see orb_oracle.h).
+ *
+ * Double-precision restatement of the per-edge arithmetic g2o performs inside
+ * Optimizer::LocalBundleAdjustment (src/Optimizer.cc:633-979):
+ *   EdgeSE3ProjectXYZ::computeError / cam_project     types_six_dof_expmap.h:90-95, .cpp:141-147
+ *   EdgeStereoSE3ProjectXYZ::computeError / cam_project  .h:122-127, .cpp:150-157 (float invz, float bf)
+ *   linearizeOplus (mono, stereo)                     .cpp:103-139, 188-234
+ *   SE3Quat::map (Eigen quaternion * vector)          se3quat.h:217-220
+ *   chi2 / robustInformation                          core/base_edge.h:58-61, 96-102
+ *   RobustKernelHuber::robustify (float dsqr)         core/robust_kernel_impl.cpp:65-91
+ *   BaseBinaryEdge::constructQuadraticForm            core/base_binary_edge.hpp:55-120
+ *   numeric linearizeOplus (central diff, 1e-9)       core/base_binary_edge.hpp:131-205
+ *   SE3Quat::exp (oplus of VertexSE3Expmap)           se3quat.h:223-257, types_six_dof_expmap.h:73-76
+ */
+#include "orb_oracle.h"
+
+#include <math.h>
+#include <string.h>
+
+static void quat_rotate(const double q[4], const double v[3], double out[3])
+{
+    /* Eigen _transformVector: uv = 2 (q.vec x v); v + w uv + q.vec x uv */
+    double uv[3] = {q[1] * v[2] - q[2] * v[1], q[2] * v[0] - q[0] * v[2],
+                    q[0] * v[1] - q[1] * v[0]};
+    uv[0] += uv[0];
+    uv[1] += uv[1];
+    uv[2] += uv[2];
+    const double c[3] = {q[1] * uv[2] - q[2] * uv[1], q[2] * uv[0] - q[0] * uv[2],
+                         q[0] * uv[1] - q[1] * uv[0]};
+    out[0] = v[0] + q[3] * uv[0] + c[0];
+    out[1] = v[1] + q[3] * uv[1] + c[1];
+    out[2] = v[2] + q[3] * uv[2] + c[2];
+}
+
+static void quat_to_rot(const double q[4], double R[3][3])
+{
+    /* Eigen QuaternionBase::toRotationMatrix */
+    const double tx = 2 * q[0], ty = 2 * q[1], tz = 2 * q[2];
+    const double twx = tx * q[3], twy = ty * q[3], twz = tz * q[3];
+    const double txx = tx * q[0], txy = ty * q[0], txz = tz * q[0];
+    const double tyy = ty * q[1], tyz = tz * q[1], tzz = tz * q[2];
+    R[0][0] = 1 - (tyy + tzz);
+    R[0][1] = txy - twz;
+    R[0][2] = txz + twy;
+    R[1][0] = txy + twz;
+    R[1][1] = 1 - (txx + tzz);
+    R[1][2] = tyz - twx;
+    R[2][0] = txz - twy;
+    R[2][1] = tyz + twx;
+    R[2][2] = 1 - (txx + tyy);
+}
+
+/* computeError with the pose given as (R, t) matrices (used by the numeric Jacobian) */
+static void edge_error_rt(const double R[3][3], const double t[3], const double X[3],
+                          const orc_edge *e, double err[3])
+{
+    double xc[3];
+    for (int i = 0; i < 3; i++)
+        xc[i] = R[i][0] * X[0] + R[i][1] * X[1] + R[i][2] * X[2] + t[i];
+    if (!e->stereo) {
+        err[0] = e->obs[0] - ((xc[0] / xc[2]) * e->fx + e->cx);
+        err[1] = e->obs[1] - ((xc[1] / xc[2]) * e->fy + e->cy);
+        err[2] = 0;
+    } else {
+        const float invz = (float)(1.0f / xc[2]);
+        const float bf = (float)e->bf;
+        const double u = xc[0] * invz * e->fx + e->cx;
+        const double v = xc[1] * invz * e->fy + e->cy;
+        err[0] = e->obs[0] - u;
+        err[1] = e->obs[1] - v;
+        err[2] = e->obs[2] - (u - (double)(bf * invz));
+    }
+}
+
+static void edge_error(const orc_pose *P, const double X[3], const orc_edge *e, double err[3],
+                       double xc[3])
+{
+    quat_rotate(P->q, X, xc);
+    xc[0] += P->t[0];
+    xc[1] += P->t[1];
+    xc[2] += P->t[2];
+    if (!e->stereo) {
+        /* project2d then *f + c */
+        const double px = xc[0] / xc[2], py = xc[1] / xc[2];
+        err[0] = e->obs[0] - (px * e->fx + e->cx);
+        err[1] = e->obs[1] - (py * e->fy + e->cy);
+        err[2] = 0;
+    } else {
+        const float invz = (float)(1.0f / xc[2]);
+        const float bf = (float)e->bf; /* cam_project(const Vector3d&, const float &bf) */
+        const double u = xc[0] * invz * e->fx + e->cx;
+        const double v = xc[1] * invz * e->fy + e->cy;
+        err[0] = e->obs[0] - u;
+        err[1] = e->obs[1] - v;
+        err[2] = e->obs[2] - (u - (double)(bf * invz));
+    }
+}
+
+static void edge_jacobians(const orc_pose *P, const double xc[3], const orc_edge *e,
+                           double jp[3][3], double jt[3][6])
+{
+    double R[3][3];
+    quat_to_rot(P->q, R);
+    const double x = xc[0], y = xc[1], z = xc[2], z_2 = z * z;
+    const double fx = e->fx, fy = e->fy;
+    memset(jp, 0, sizeof(double) * 9);
+    memset(jt, 0, sizeof(double) * 18);
+    if (!e->stereo) {
+        const double tmp[2][3] = {{fx, 0, -x / z * fx}, {0, fy, -y / z * fy}};
+        for (int r = 0; r < 2; r++)
+            for (int c = 0; c < 3; c++) {
+                double acc = 0;
+                for (int k = 0; k < 3; k++)
+                    acc += tmp[r][k] * R[k][c];
+                jp[r][c] = -1. / z * acc;
+            }
+    } else {
+        for (int c = 0; c < 3; c++) {
+            jp[0][c] = -fx * R[0][c] / z + fx * x * R[2][c] / z_2;
+            jp[1][c] = -fy * R[1][c] / z + fy * y * R[2][c] / z_2;
+            jp[2][c] = jp[0][c] - e->bf * R[2][c] / z_2;
+        }
+    }
+    jt[0][0] = x * y / z_2 * fx;
+    jt[0][1] = -(1 + (x * x / z_2)) * fx;
+    jt[0][2] = y / z * fx;
+    jt[0][3] = -1. / z * fx;
+    jt[0][4] = 0;
+    jt[0][5] = x / z_2 * fx;
+    jt[1][0] = (1 + y * y / z_2) * fy;
+    jt[1][1] = -x * y / z_2 * fy;
+    jt[1][2] = -x / z * fy;
+    jt[1][3] = 0;
+    jt[1][4] = -1. / z * fy;
+    jt[1][5] = y / z_2 * fy;
+    if (e->stereo) {
+        jt[2][0] = jt[0][0] - e->bf * y / z_2;
+        jt[2][1] = jt[0][1] + e->bf * x / z_2;
+        jt[2][2] = jt[0][2];
+        jt[2][3] = jt[0][3];
+        jt[2][4] = 0;
+        jt[2][5] = jt[0][5] - e->bf / z_2;
+    }
+}
+
+void orc_ba_linearize(const orc_pose *poses, int npose, const double *points, int npoint,
+                      const orc_edge *edges, int nedge, orc_edge_out *eout, double *hpose,
+                      double *bpose, double *hpoint, double *bpoint)
+{
+    memset(hpose, 0, sizeof(double) * 36 * (size_t)npose);
+    memset(bpose, 0, sizeof(double) * 6 * (size_t)npose);
+    memset(hpoint, 0, sizeof(double) * 9 * (size_t)npoint);
+    memset(bpoint, 0, sizeof(double) * 3 * (size_t)npoint);
+    for (int i = 0; i < nedge; i++) {
+        const orc_edge *e = &edges[i];
+        orc_edge_out *o = &eout[i];
+        memset(o, 0, sizeof(*o));
+        if (!e->active)
+            continue;
+        const orc_pose *P = &poses[e->pose];
+        const double *X = points + 3 * (size_t)e->point;
+        double xc[3];
+        edge_error(P, X, e, o->err, xc);
+        edge_jacobians(P, xc, e, o->jp, o->jt);
+        const int D = e->stereo ? 3 : 2;
+        const double info = e->inv_sigma2;
+        double chi2 = 0;
+        for (int k = 0; k < D; k++)
+            chi2 += o->err[k] * (info * o->err[k]);
+        o->chi2 = chi2;
+        double rho1 = 1.0;
+        if (e->robust) {
+            const float dsqr = (float)(e->huber_delta * e->huber_delta);
+            if (!(chi2 <= dsqr))
+                rho1 = e->huber_delta / sqrt(chi2);
+        }
+        o->rho1 = rho1;
+        const double w = rho1 * info; /* weighted Omega = rho' * Omega (diagonal) */
+        double wr[3];
+        for (int k = 0; k < D; k++)
+            wr[k] = -info * o->err[k] * rho1;
+        /* from = point (never fixed in LBA), to = pose */
+        double *hp = hpoint + 9 * (size_t)e->point, *bp = bpoint + 3 * (size_t)e->point;
+        for (int r = 0; r < 3; r++) {
+            double acc = 0;
+            for (int k = 0; k < D; k++)
+                acc += o->jp[k][r] * wr[k];
+            bp[r] += acc;
+            for (int c = 0; c < 3; c++) {
+                double a2 = 0;
+                for (int k = 0; k < D; k++)
+                    a2 += o->jp[k][r] * w * o->jp[k][c];
+                hp[r * 3 + c] += a2;
+            }
+        }
+        if (!P->fixed) {
+            for (int r = 0; r < 3; r++)
+                for (int c = 0; c < 6; c++) {
+                    double a2 = 0;
+                    for (int k = 0; k < D; k++)
+                        a2 += o->jp[k][r] * w * o->jt[k][c];
+                    o->hpl[r][c] = a2;
+                }
+            double *ht = hpose + 36 * (size_t)e->pose, *bt = bpose + 6 * (size_t)e->pose;
+            for (int r = 0; r < 6; r++) {
+                double acc = 0;
+                for (int k = 0; k < D; k++)
+                    acc += o->jt[k][r] * wr[k];
+                bt[r] += acc;
+                for (int c = 0; c < 6; c++) {
+                    double a2 = 0;
+                    for (int k = 0; k < D; k++)
+                        a2 += o->jt[k][r] * w * o->jt[k][c];
+                    ht[r * 6 + c] += a2;
+                }
+            }
+        }
+    }
+}
+
+/* SE3Quat::exp(update) * T applied in rotation-matrix form (se3quat.h:223-257) */
+static void oplus_pose(const double R[3][3], const double t[3], const double upd[6],
+                       double R2[3][3], double t2[3])
+{
+    const double w[3] = {upd[0], upd[1], upd[2]}, u[3] = {upd[3], upd[4], upd[5]};
+    const double theta = sqrt(w[0] * w[0] + w[1] * w[1] + w[2] * w[2]);
+    const double O[3][3] = {{0, -w[2], w[1]}, {w[2], 0, -w[0]}, {-w[1], w[0], 0}};
+    double O2[3][3], Re[3][3], V[3][3];
+    for (int i = 0; i < 3; i++)
+        for (int j = 0; j < 3; j++) {
+            O2[i][j] = 0;
+            for (int k = 0; k < 3; k++)
+                O2[i][j] += O[i][k] * O[k][j];
+        }
+    for (int i = 0; i < 3; i++)
+        for (int j = 0; j < 3; j++) {
+            const double I = (i == j) ? 1.0 : 0.0;
+            if (theta < 0.00001) {
+                Re[i][j] = I + O[i][j] + O2[i][j];
+                V[i][j] = Re[i][j];
+            } else {
+                Re[i][j] = I + sin(theta) / theta * O[i][j] +
+                           (1 - cos(theta)) / (theta * theta) * O2[i][j];
+                V[i][j] = I + (1 - cos(theta)) / (theta * theta) * O[i][j] +
+                          (theta - sin(theta)) / pow(theta, 3) * O2[i][j];
+            }
+        }
+    double te[3];
+    for (int i = 0; i < 3; i++)
+        te[i] = V[i][0] * u[0] + V[i][1] * u[1] + V[i][2] * u[2];
+    for (int i = 0; i < 3; i++) {
+        for (int j = 0; j < 3; j++)
+            R2[i][j] = Re[i][0] * R[0][j] + Re[i][1] * R[1][j] + Re[i][2] * R[2][j];
+        t2[i] = Re[i][0] * t[0] + Re[i][1] * t[1] + Re[i][2] * t[2] + te[i];
+    }
+}
+
+void orc_ba_numeric_jacobian(const orc_pose *pose, const double *xyz, const orc_edge *e,
+                             double jp[3][3], double jt[3][6])
+{
+    const double delta = 1e-9, scalar = 1.0 / (2 * delta);
+    double R[3][3];
+    quat_to_rot(pose->q, R);
+    double ep[3], em[3];
+    for (int d = 0; d < 3; d++) {
+        double Xp[3] = {xyz[0], xyz[1], xyz[2]}, Xm[3] = {xyz[0], xyz[1], xyz[2]};
+        Xp[d] += delta;
+        Xm[d] -= delta;
+        edge_error_rt(R, pose->t, Xp, e, ep);
+        edge_error_rt(R, pose->t, Xm, e, em);
+        for (int k = 0; k < 3; k++)
+            jp[k][d] = scalar * (ep[k] - em[k]);
+    }
+    for (int d = 0; d < 6; d++) {
+        double up[6] = {0, 0, 0, 0, 0, 0}, um[6] = {0, 0, 0, 0, 0, 0};
+        up[d] = delta;
+        um[d] = -delta;
+        double R2[3][3], t2[3];
+        oplus_pose(R, pose->t, up, R2, t2);
+        edge_error_rt(R2, t2, xyz, e, ep);
+        oplus_pose(R, pose->t, um, R2, t2);
+        edge_error_rt(R2, t2, xyz, e, em);
+        for (int k = 0; k < 3; k++)
+            jt[k][d] = scalar * (ep[k] - em[k]);
+    }
+}

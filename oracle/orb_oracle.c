@@ -1,0 +1,1093 @@
+/*
+ * oracle/orb_oracle.c -- TEST INFRASTRUCTURE ONLY (see orb_oracle.h).
+ *
+ * Plain-C restatement of ORBextractor (src/ORBextractor.cc) and the OpenCV 3.4
+ * primitives it calls.  Written for clarity, literally following the sequential
+ * semantics of the reference (std::list order, FAST row buffers, ...), so that it
+ * is an independent check of the data-parallel HIP formulation in
+ * orb_slam2_test_amd/csrc/.  Compile with -ffp-contract=off (no FMA contraction;
+ * see SURVEY.md 8a "OpenCV pins").
+ */
+#include "orb_oracle.h"
+
+#include <math.h>
+#include <pthread.h>
+#include <stdlib.h>
+#include <string.h>
+
+#define PATCH_SIZE 31
+#define HALF_PATCH_SIZE 15
+#define EDGE_THRESHOLD 19
+
+/* ------------------------------------------------------------------ */
+/* OpenCV scalar helpers (cvRound = round-half-even via cvtss2si)       */
+/* ------------------------------------------------------------------ */
+static int cv_round_f(float v) { return (int)lrintf(v); }
+static int cv_round_d(double v) { return (int)lrint(v); }
+static int cv_floor_f(float v) { int i = (int)v; return i - (i > v); }
+static short sat_short_f(float v)
+{
+    int i = cv_round_f(v);
+    return (short)(i < -32768 ? -32768 : (i > 32767 ? 32767 : i));
+}
+static uint8_t sat_u8(int v) { return (uint8_t)(v < 0 ? 0 : (v > 255 ? 255 : v)); }
+
+static const signed char orc_pattern[256][4] = {
+#define ORBG_PAIR(a, b, c, d) {a, b, c, d},
+#include "orb_pattern.inc"
+#undef ORBG_PAIR
+};
+
+/* ------------------------------------------------------------------ */
+/* ORBextractor::ORBextractor tables, ORBextractor.cc:432-521            */
+/* ------------------------------------------------------------------ */
+int orc_init_params(orc_params *p, int nfeatures, float scale_factor, int nlevels,
+                    int ini_th_fast, int min_th_fast)
+{
+    if (nlevels < 1 || nlevels > ORC_MAX_LEVELS || nfeatures < 0 || !(scale_factor > 1.0f))
+        return -22;
+    memset(p, 0, sizeof(*p));
+    p->nfeatures = nfeatures;
+    p->scale_factor = scale_factor;
+    p->nlevels = nlevels;
+    p->ini_th_fast = ini_th_fast;
+    p->min_th_fast = min_th_fast;
+
+    /* the scaleFactor MEMBER is double (ORBextractor.h:128): float*double products */
+    const double sf = (double)scale_factor;
+    p->scale[0] = 1.0f;
+    p->sigma2[0] = 1.0f;
+    for (int i = 1; i < nlevels; i++) {
+        p->scale[i] = (float)((double)p->scale[i - 1] * sf);
+        p->sigma2[i] = p->scale[i] * p->scale[i];
+    }
+    for (int i = 0; i < nlevels; i++) {
+        p->inv_scale[i] = 1.0f / p->scale[i];
+        p->inv_sigma2[i] = 1.0f / p->sigma2[i];
+    }
+
+    /* mnFeaturesPerLevel, :465-476 */
+    const float factor = (float)(1.0f / sf);
+    float desired = (float)nfeatures * (1 - factor) /
+                    (1 - (float)pow((double)factor, (double)nlevels));
+    int sum = 0;
+    for (int l = 0; l < nlevels - 1; l++) {
+        p->features_per_level[l] = cv_round_f(desired);
+        sum += p->features_per_level[l];
+        desired *= factor;
+    }
+    p->features_per_level[nlevels - 1] = nfeatures - sum > 0 ? nfeatures - sum : 0;
+
+    /* umax, :504-520 */
+    const int vmax = cv_floor_f(HALF_PATCH_SIZE * sqrtf(2.f) / 2 + 1);
+    const int vmin = (int)ceilf(HALF_PATCH_SIZE * sqrtf(2.f) / 2);
+    const double hp2 = HALF_PATCH_SIZE * HALF_PATCH_SIZE;
+    int v, v0;
+    for (v = 0; v <= vmax; ++v)
+        p->umax[v] = cv_round_d(sqrt(hp2 - v * v));
+    for (v = HALF_PATCH_SIZE, v0 = 0; v >= vmin; --v) {
+        while (p->umax[v0] == p->umax[v0 + 1])
+            ++v0;
+        p->umax[v] = v0;
+        ++v0;
+    }
+
+    p->resize_mode = ORC_RESIZE_SIMD_16_8;
+    /* GaussianBlur 7x7 sigma 2, OpenCV >= 3.4.9 bit-exact kernel (error-diffusion table) */
+    static const int32_t k_ed[7] = {18, 34, 48, 56, 48, 34, 18};
+    memcpy(p->gauss_k, k_ed, sizeof(k_ed));
+    p->brief_fma = 0;
+    return 0;
+}
+
+void orc_level_size(const orc_params *p, int w, int h, int level, int *lw, int *lh)
+{
+    /* ComputePyramid, ORBextractor.cc:1405-1406 */
+    const float s = p->inv_scale[level];
+    *lw = cv_round_f((float)w * s);
+    *lh = cv_round_f((float)h * s);
+}
+
+/* ------------------------------------------------------------------ */
+/* cv::resize(src, dst, dsize, 0, 0, INTER_LINEAR) for 8UC1              */
+/* (imgproc/resize.cpp, OpenCV 3.4: coefficient set-up in resize(),     */
+/*  HResizeLinear + VResizeLinear<.., FixedPtCast<int,uchar,22>, VecOp>) */
+/* ------------------------------------------------------------------ */
+static int resize_bulk_end(int width, int mode)
+{
+    if (mode == ORC_RESIZE_SCALAR)
+        return 0;
+    int x = 0;
+    for (; x <= width - 16; x += 16) {
+    }
+    for (; x < width - mode; x += mode) {
+    }
+    return x;
+}
+
+void orc_resize_linear_u8(const uint8_t *src, int sw, int sh, int sstep, uint8_t *dst, int dw,
+                          int dh, int dstep, int mode)
+{
+    const double inv_sx = (double)dw / sw, inv_sy = (double)dh / sh;
+    const double scale_x = 1. / inv_sx, scale_y = 1. / inv_sy;
+    int *xofs = (int *)malloc(sizeof(int) * dw);
+    short *alpha = (short *)malloc(sizeof(short) * 2 * dw);
+    int *row0 = (int *)malloc(sizeof(int) * dw);
+    int *row1 = (int *)malloc(sizeof(int) * dw);
+    int xmax = dw;
+
+    for (int dx = 0; dx < dw; dx++) {
+        float fx = (float)((dx + 0.5) * scale_x - 0.5);
+        int sx = cv_floor_f(fx);
+        fx -= sx;
+        if (sx < 0) {
+            fx = 0;
+            sx = 0;
+        }
+        if (sx + 1 >= sw) {
+            if (xmax > dx)
+                xmax = dx;
+            if (sx >= sw - 1) {
+                fx = 0;
+                sx = sw - 1;
+            }
+        }
+        xofs[dx] = sx;
+        alpha[2 * dx] = sat_short_f((1.f - fx) * 2048);
+        alpha[2 * dx + 1] = sat_short_f(fx * 2048);
+    }
+
+    const int bulk = resize_bulk_end(dw, mode);
+    for (int dy = 0; dy < dh; dy++) {
+        float fy = (float)((dy + 0.5) * scale_y - 0.5);
+        int sy = cv_floor_f(fy);
+        fy -= sy;
+        const short b0 = sat_short_f((1.f - fy) * 2048);
+        const short b1 = sat_short_f(fy * 2048);
+        int sy0 = sy < 0 ? 0 : (sy < sh ? sy : sh - 1);
+        int sy1 = sy + 1 < 0 ? 0 : (sy + 1 < sh ? sy + 1 : sh - 1);
+        const uint8_t *s0 = src + (size_t)sy0 * sstep;
+        const uint8_t *s1 = src + (size_t)sy1 * sstep;
+        for (int dx = 0; dx < dw; dx++) {
+            const int sx = xofs[dx];
+            if (dx < xmax) {
+                row0[dx] = s0[sx] * alpha[2 * dx] + s0[sx + 1] * alpha[2 * dx + 1];
+                row1[dx] = s1[sx] * alpha[2 * dx] + s1[sx + 1] * alpha[2 * dx + 1];
+            } else {
+                row0[dx] = s0[sx] * 2048;
+                row1[dx] = s1[sx] * 2048;
+            }
+        }
+        uint8_t *d = dst + (size_t)dy * dstep;
+        for (int x = 0; x < dw; x++) {
+            if (x < bulk) {
+                /* v_mul_hi(v_pack(S >> 4), beta) + ..., then rshr_pack_u<2> */
+                int a = ((row0[x] >> 4) * b0) >> 16;
+                int b = ((row1[x] >> 4) * b1) >> 16;
+                d[x] = sat_u8((a + b + 2) >> 2);
+            } else {
+                d[x] = sat_u8((row0[x] * b0 + row1[x] * b1 + (1 << 21)) >> 22);
+            }
+        }
+    }
+    free(xofs);
+    free(alpha);
+    free(row0);
+    free(row1);
+}
+
+/* ------------------------------------------------------------------ */
+/* cv::GaussianBlur(7x7, sigma 2, BORDER_REFLECT_101) on a whole image   */
+/* bit-exact fixed point: out = sat((sum_v k_v sum_h k_h p + 2^15) >> 16) */
+/* ------------------------------------------------------------------ */
+static int reflect101(int i, int n)
+{
+    if (n == 1)
+        return 0;
+    while (i < 0 || i >= n) {
+        if (i < 0)
+            i = -i;
+        if (i >= n)
+            i = 2 * n - 2 - i;
+    }
+    return i;
+}
+
+void orc_gauss7_u8(const uint8_t *src, int w, int h, int sstep, uint8_t *dst, int dstep,
+                   const int32_t k[7])
+{
+    int *rows = (int *)malloc(sizeof(int) * (size_t)w * h);
+    for (int y = 0; y < h; y++)
+        for (int x = 0; x < w; x++) {
+            int acc = 0;
+            for (int t = -3; t <= 3; t++)
+                acc += k[t + 3] * src[(size_t)y * sstep + reflect101(x + t, w)];
+            rows[(size_t)y * w + x] = acc;
+        }
+    for (int y = 0; y < h; y++)
+        for (int x = 0; x < w; x++) {
+            int acc = 0;
+            for (int t = -3; t <= 3; t++)
+                acc += k[t + 3] * rows[(size_t)reflect101(y + t, h) * w + x];
+            dst[(size_t)y * dstep + x] = sat_u8((acc + (1 << 15)) >> 16);
+        }
+    free(rows);
+}
+
+/* ------------------------------------------------------------------ */
+/* cv::FAST(roi, kps, th, nonmax=true), TYPE_9_16 (features2d/fast.cpp)  */
+/* ------------------------------------------------------------------ */
+static const int fast_off[16][2] = {{0, 3},  {1, 3},   {2, 2},   {3, 1},   {3, 0},   {3, -1},
+                                    {2, -2}, {1, -3},  {0, -3},  {-1, -3}, {-2, -2}, {-3, -1},
+                                    {-3, 0}, {-3, 1},  {-2, 2},  {-1, 3}};
+
+static void fast_offsets(int step, int pixel[25])
+{
+    for (int k = 0; k < 16; k++)
+        pixel[k] = fast_off[k][0] + fast_off[k][1] * step;
+    for (int k = 16; k < 25; k++)
+        pixel[k] = pixel[k - 16];
+}
+
+/* cornerScore<16>: max(threshold, best 9-arc) - 1 */
+static int corner_score16(const uint8_t *ptr, const int pixel[25], int threshold)
+{
+    int d[25];
+    const int v = ptr[0];
+    for (int k = 0; k < 25; k++)
+        d[k] = v - ptr[pixel[k]];
+    int a0 = threshold;
+    for (int k = 0; k < 16; k += 2) {
+        int a = d[k + 1] < d[k + 2] ? d[k + 1] : d[k + 2];
+        if (d[k + 3] < a) a = d[k + 3];
+        if (a <= a0)
+            continue;
+        for (int m = 4; m <= 8; m++)
+            if (d[k + m] < a) a = d[k + m];
+        int t = a < d[k] ? a : d[k];
+        if (t > a0) a0 = t;
+        t = a < d[k + 9] ? a : d[k + 9];
+        if (t > a0) a0 = t;
+    }
+    int b0 = -a0;
+    for (int k = 0; k < 16; k += 2) {
+        int b = d[k + 1] > d[k + 2] ? d[k + 1] : d[k + 2];
+        for (int m = 3; m <= 5; m++)
+            if (d[k + m] > b) b = d[k + m];
+        if (b >= b0)
+            continue;
+        for (int m = 6; m <= 8; m++)
+            if (d[k + m] > b) b = d[k + m];
+        int t = b > d[k] ? b : d[k];
+        if (t < b0) b0 = t;
+        t = b > d[k + 9] ? b : d[k + 9];
+        if (t < b0) b0 = t;
+    }
+    return -b0 - 1;
+}
+
+/* corner test at threshold th, following FAST_t's tab / contiguous-count logic */
+static int fast_is_corner(const uint8_t *ptr, const int pixel[25], int th)
+{
+    const int v = ptr[0];
+    int dk[16];
+    for (int k = 0; k < 16; k++) {
+        int x = ptr[pixel[k]];
+        dk[k] = (x - v) < -th ? 1 : ((x - v) > th ? 2 : 0);
+    }
+    int d = dk[0] | dk[8];
+    if (d == 0)
+        return 0;
+    d &= dk[2] | dk[10];
+    d &= dk[4] | dk[12];
+    d &= dk[6] | dk[14];
+    if (d == 0)
+        return 0;
+    d &= dk[1] | dk[9];
+    d &= dk[3] | dk[11];
+    d &= dk[5] | dk[13];
+    d &= dk[7] | dk[15];
+    if (d & 1) {
+        int vt = v - th, count = 0;
+        for (int k = 0; k < 25; k++) {
+            if (ptr[pixel[k]] < vt) {
+                if (++count > 8)
+                    return 1;
+            } else
+                count = 0;
+        }
+    }
+    if (d & 2) {
+        int vt = v + th, count = 0;
+        for (int k = 0; k < 25; k++) {
+            if (ptr[pixel[k]] > vt) {
+                if (++count > 8)
+                    return 1;
+            } else
+                count = 0;
+        }
+    }
+    return 0;
+}
+
+int orc_fast_score(const uint8_t *p, int step)
+{
+    int pixel[25];
+    fast_offsets(step, pixel);
+    /* score independent of th when corner; -1 if not a corner even at th = 0 */
+    if (!fast_is_corner(p, pixel, 0))
+        return -1;
+    return corner_score16(p, pixel, 0);
+}
+
+int orc_fast_window(const uint8_t *img, int step, int w, int h, int th, orc_keypoint *out,
+                    int cap)
+{
+    int pixel[25];
+    fast_offsets(step, pixel);
+    th = th < 0 ? 0 : (th > 255 ? 255 : th);
+    int n = 0;
+    if (w <= 0 || h <= 0)
+        return 0;
+    uint8_t *buf = (uint8_t *)calloc((size_t)3 * w, 1);
+    int *cpos = (int *)malloc(sizeof(int) * 3 * (w + 1));
+    int ncp[3] = {0, 0, 0};
+    for (int i = 3; i < h - 2; i++) {
+        uint8_t *curr = buf + (size_t)((i - 3) % 3) * w;
+        int *cornerpos = cpos + ((i - 3) % 3) * (w + 1);
+        memset(curr, 0, w);
+        int ncorners = 0;
+        if (i < h - 3) {
+            for (int j = 3; j < w - 3; j++) {
+                const uint8_t *ptr = img + (size_t)i * step + j;
+                if (fast_is_corner(ptr, pixel, th)) {
+                    cornerpos[ncorners++] = j;
+                    curr[j] = (uint8_t)corner_score16(ptr, pixel, th);
+                }
+            }
+        }
+        ncp[(i - 3) % 3] = ncorners;
+        if (i == 3)
+            continue;
+        const uint8_t *prev = buf + (size_t)((i - 4 + 3) % 3) * w;
+        const uint8_t *pprev = buf + (size_t)((i - 5 + 3) % 3) * w;
+        const int *cp = cpos + ((i - 4 + 3) % 3) * (w + 1);
+        const int nc = ncp[(i - 4 + 3) % 3];
+        for (int k = 0; k < nc; k++) {
+            const int j = cp[k];
+            const int s = prev[j];
+            if (s > prev[j + 1] && s > prev[j - 1] && s > pprev[j - 1] && s > pprev[j] &&
+                s > pprev[j + 1] && s > curr[j - 1] && s > curr[j] && s > curr[j + 1]) {
+                if (n < cap) {
+                    orc_keypoint *kp = &out[n];
+                    kp->x = (float)j;
+                    kp->y = (float)(i - 1);
+                    kp->size = 7.f;
+                    kp->angle = -1.f;
+                    kp->response = (float)s;
+                    kp->octave = 0;
+                    kp->class_id = -1;
+                }
+                n++;
+            }
+        }
+    }
+    free(buf);
+    free(cpos);
+    return n;
+}
+
+/* ------------------------------------------------------------------ */
+/* DistributeOctTree, ORBextractor.cc:668-951 (+ DivideNode :537-614)    */
+/* std::list emulated with an index-linked pool.  The (size, pointer)   */
+/* sort at :869 tie-breaks on heap address; pinned here to creation     */
+/* order ("monotonic allocation"): among equal sizes the most recently  */
+/* created node is split first.                                          */
+/* ------------------------------------------------------------------ */
+typedef struct {
+    int x0, y0, x1, y1;   /* UL=(x0,y0) UR=(x1,y0) BL=(x0,y1) BR=(x1,y1) */
+    int *keys;
+    int nkeys;
+    int no_more;
+    int prev, next;
+    long seq;
+} onode;
+
+typedef struct {
+    onode *v;
+    int n, cap;
+    int head, tail, size;
+    long seq;
+} olist;
+
+static int ol_new(olist *L, int x0, int y0, int x1, int y1, int cap_keys)
+{
+    if (L->n == L->cap) {
+        L->cap = L->cap ? 2 * L->cap : 64;
+        L->v = (onode *)realloc(L->v, sizeof(onode) * L->cap);
+    }
+    onode *nd = &L->v[L->n];
+    memset(nd, 0, sizeof(*nd));
+    nd->x0 = x0;
+    nd->y0 = y0;
+    nd->x1 = x1;
+    nd->y1 = y1;
+    nd->keys = (int *)malloc(sizeof(int) * (cap_keys > 0 ? cap_keys : 1));
+    nd->prev = nd->next = -1;
+    nd->seq = L->seq++;
+    return L->n++;
+}
+static void ol_link_front(olist *L, int id)
+{
+    L->v[id].prev = -1;
+    L->v[id].next = L->head;
+    if (L->head >= 0)
+        L->v[L->head].prev = id;
+    L->head = id;
+    if (L->tail < 0)
+        L->tail = id;
+    L->size++;
+}
+static void ol_link_back(olist *L, int id)
+{
+    L->v[id].next = -1;
+    L->v[id].prev = L->tail;
+    if (L->tail >= 0)
+        L->v[L->tail].next = id;
+    L->tail = id;
+    if (L->head < 0)
+        L->head = id;
+    L->size++;
+}
+static int ol_erase(olist *L, int id) /* returns next */
+{
+    onode *nd = &L->v[id];
+    int nx = nd->next;
+    if (nd->prev >= 0)
+        L->v[nd->prev].next = nd->next;
+    else
+        L->head = nd->next;
+    if (nd->next >= 0)
+        L->v[nd->next].prev = nd->prev;
+    else
+        L->tail = nd->prev;
+    L->size--;
+    return nx;
+}
+
+/* DivideNode; children created (not linked) in n1..n4 order; returns ids in c[4] */
+static void divide_node(olist *L, int id, const orc_keypoint *keys, int c[4])
+{
+    const int x0 = L->v[id].x0, y0 = L->v[id].y0, x1 = L->v[id].x1, y1 = L->v[id].y1;
+    const int halfX = (int)ceilf((float)(x1 - x0) / 2);
+    const int halfY = (int)ceilf((float)(y1 - y0) / 2);
+    const int nk = L->v[id].nkeys;
+    c[0] = ol_new(L, x0, y0, x0 + halfX, y0 + halfY, nk);
+    c[1] = ol_new(L, x0 + halfX, y0, x1, y0 + halfY, nk);
+    c[2] = ol_new(L, x0, y0 + halfY, x0 + halfX, y1, nk);
+    c[3] = ol_new(L, x0 + halfX, y0 + halfY, x1, y1, nk);
+    const onode *par = &L->v[id];
+    const float bx = (float)(x0 + halfX), by = (float)(y0 + halfY);
+    for (int i = 0; i < nk; i++) {
+        const int k = par->keys[i];
+        const orc_keypoint *kp = &keys[k];
+        int q;
+        if (kp->x < bx)
+            q = kp->y < by ? 0 : 2;
+        else
+            q = kp->y < by ? 1 : 3;
+        onode *ch = &L->v[c[q]];
+        ch->keys[ch->nkeys++] = k;
+        par = &L->v[id];
+    }
+    for (int q = 0; q < 4; q++)
+        if (L->v[c[q]].nkeys == 1)
+            L->v[c[q]].no_more = 1;
+}
+
+typedef struct {
+    int size;
+    long seq;
+    int id;
+} size_ptr;
+
+static int cmp_size_ptr(const void *a, const void *b)
+{
+    const size_ptr *x = (const size_ptr *)a, *y = (const size_ptr *)b;
+    if (x->size != y->size)
+        return x->size < y->size ? -1 : 1;
+    return x->seq < y->seq ? -1 : (x->seq > y->seq);
+}
+
+int orc_distribute_octree(const orc_keypoint *keys, int n, int minX, int maxX, int minY,
+                          int maxY, int N, orc_keypoint *out, int cap)
+{
+    const int nIni = (int)roundf((float)(maxX - minX) / (maxY - minY));
+    if (nIni <= 0)
+        return -22; /* the reference divides by zero here */
+    const float hX = (float)(maxX - minX) / nIni;
+
+    olist L;
+    memset(&L, 0, sizeof(L));
+    L.head = L.tail = -1;
+    int *ini = (int *)malloc(sizeof(int) * nIni);
+    for (int i = 0; i < nIni; i++) {
+        ini[i] = ol_new(&L, (int)(hX * (float)i), 0, (int)(hX * (float)(i + 1)), maxY - minY, n);
+        ol_link_back(&L, ini[i]);
+    }
+    for (int i = 0; i < n; i++) {
+        const size_t r = (size_t)(keys[i].x / hX);
+        onode *nd = &L.v[ini[r]];
+        nd->keys[nd->nkeys++] = i;
+    }
+    for (int it = L.head; it >= 0;) {
+        if (L.v[it].nkeys == 1) {
+            L.v[it].no_more = 1;
+            it = L.v[it].next;
+        } else if (L.v[it].nkeys == 0)
+            it = ol_erase(&L, it);
+        else
+            it = L.v[it].next;
+    }
+
+    int finish = 0;
+    size_t vcap = 64;
+    size_t vn = 0;
+    size_ptr *vsp = (size_ptr *)malloc(sizeof(size_ptr) * vcap);
+    size_ptr *vprev = NULL;
+#define PUSH_SP(idv)                                                                       \
+    do {                                                                                   \
+        if (vn == vcap) {                                                                  \
+            vcap *= 2;                                                                     \
+            vsp = (size_ptr *)realloc(vsp, sizeof(size_ptr) * vcap);                       \
+        }                                                                                  \
+        vsp[vn].size = L.v[idv].nkeys;                                                     \
+        vsp[vn].seq = L.v[idv].seq;                                                        \
+        vsp[vn].id = idv;                                                                  \
+        vn++;                                                                              \
+    } while (0)
+
+    while (!finish) {
+        int prevSize = L.size;
+        int nToExpand = 0;
+        vn = 0;
+        for (int it = L.head; it >= 0;) {
+            if (L.v[it].no_more) {
+                it = L.v[it].next;
+                continue;
+            }
+            int c[4];
+            divide_node(&L, it, keys, c);
+            for (int q = 0; q < 4; q++) {
+                if (L.v[c[q]].nkeys > 0) {
+                    ol_link_front(&L, c[q]);
+                    if (L.v[c[q]].nkeys > 1) {
+                        nToExpand++;
+                        PUSH_SP(c[q]);
+                    }
+                }
+            }
+            it = ol_erase(&L, it);
+        }
+        if (L.size >= N || L.size == prevSize) {
+            finish = 1;
+        } else if (L.size + nToExpand * 3 > N) {
+            while (!finish) {
+                prevSize = L.size;
+                size_t np = vn;
+                vprev = (size_ptr *)realloc(vprev, sizeof(size_ptr) * (np ? np : 1));
+                memcpy(vprev, vsp, sizeof(size_ptr) * np);
+                vn = 0;
+                qsort(vprev, np, sizeof(size_ptr), cmp_size_ptr);
+                for (long j = (long)np - 1; j >= 0; j--) {
+                    int c[4];
+                    const int pid = vprev[j].id;
+                    divide_node(&L, pid, keys, c);
+                    for (int q = 0; q < 4; q++) {
+                        if (L.v[c[q]].nkeys > 0) {
+                            ol_link_front(&L, c[q]);
+                            if (L.v[c[q]].nkeys > 1)
+                                PUSH_SP(c[q]);
+                        }
+                    }
+                    ol_erase(&L, pid);
+                    if (L.size >= N)
+                        break;
+                }
+                if (L.size >= N || L.size == prevSize)
+                    finish = 1;
+            }
+        }
+    }
+#undef PUSH_SP
+
+    int nout = 0;
+    for (int it = L.head; it >= 0; it = L.v[it].next) {
+        const onode *nd = &L.v[it];
+        int best = nd->keys[0];
+        float maxr = keys[best].response;
+        for (int k = 1; k < nd->nkeys; k++) {
+            if (keys[nd->keys[k]].response > maxr) {
+                best = nd->keys[k];
+                maxr = keys[best].response;
+            }
+        }
+        if (nout < cap)
+            out[nout] = keys[best];
+        nout++;
+    }
+    for (int i = 0; i < L.n; i++)
+        free(L.v[i].keys);
+    free(L.v);
+    free(ini);
+    free(vsp);
+    free(vprev);
+    return nout;
+}
+
+/* ------------------------------------------------------------------ */
+/* cv::fastAtan2 (core/mathfuncs_core, OpenCV 3.4) -- no FMA             */
+/* ------------------------------------------------------------------ */
+float orc_fast_atan2(float y, float x)
+{
+    static const float r2d = (float)(180 / 3.14159265358979323846);
+    const float p1 = 0.9997878412794807f * r2d;
+    const float p3 = -0.3258083974640975f * r2d;
+    const float p5 = 0.1555786518463281f * r2d;
+    const float p7 = -0.04432655554792128f * r2d;
+    const float eps = (float)2.2204460492503131e-16; /* (float)DBL_EPSILON */
+    float ax = fabsf(x), ay = fabsf(y), a, c, c2;
+    if (ax >= ay) {
+        c = ay / (ax + eps);
+        c2 = c * c;
+        a = (((p7 * c2 + p5) * c2 + p3) * c2 + p1) * c;
+    } else {
+        c = ax / (ay + eps);
+        c2 = c * c;
+        a = 90.f - (((p7 * c2 + p5) * c2 + p3) * c2 + p1) * c;
+    }
+    if (x < 0)
+        a = 180.f - a;
+    if (y < 0)
+        a = 360.f - a;
+    return a;
+}
+
+/* IC_Angle, ORBextractor.cc:83-111 */
+float orc_ic_angle(const uint8_t *img, int step, float px, float py, const int32_t umax[16])
+{
+    int m_01 = 0, m_10 = 0;
+    const uint8_t *center = img + (size_t)cv_round_f(py) * step + cv_round_f(px);
+    for (int u = -HALF_PATCH_SIZE; u <= HALF_PATCH_SIZE; ++u)
+        m_10 += u * center[u];
+    for (int v = 1; v <= HALF_PATCH_SIZE; ++v) {
+        int v_sum = 0;
+        const int d = umax[v];
+        for (int u = -d; u <= d; ++u) {
+            const int val_plus = center[u + v * step], val_minus = center[u - v * step];
+            v_sum += (val_plus - val_minus);
+            m_10 += u * (val_plus + val_minus);
+        }
+        m_01 += v * v_sum;
+    }
+    return orc_fast_atan2((float)m_01, (float)m_10);
+}
+
+/* ------------------------------------------------------------------ */
+/* Pinned cosf/sinf (ORBextractor.cc:121-122).  glibc's cosf is not      */
+/* specified bit-for-bit; both the oracle and the HIP kernel use this    */
+/* double-precision evaluation (Cody-Waite reduction + Taylor to x^19),  */
+/* rounded once to float.                                                */
+/* ------------------------------------------------------------------ */
+static void pinned_sincos(double x, double *s, double *c)
+{
+    const double two_over_pi = 6.36619772367581382433e-01;
+    const double pio2_1 = 1.57079632673412561417e+00;  /* first 33 bits of pi/2 */
+    const double pio2_1t = 6.07710050650619224932e-11; /* pi/2 - pio2_1 */
+    const double kd = rint(x * two_over_pi);
+    const int k = (int)kd;
+    const double r = (x - kd * pio2_1) - kd * pio2_1t;
+    const double r2 = r * r;
+    const double sp =
+        r + r * r2 *
+                (-1.0 / 6.0 +
+                 r2 * (1.0 / 120.0 +
+                       r2 * (-1.0 / 5040.0 +
+                             r2 * (1.0 / 362880.0 +
+                                   r2 * (-1.0 / 39916800.0 +
+                                         r2 * (1.0 / 6227020800.0 +
+                                               r2 * (-1.0 / 1307674368000.0 +
+                                                     r2 * (1.0 / 355687428096000.0 +
+                                                           r2 * (-1.0 / 121645100408832000.0)))))))));
+    const double cp =
+        1.0 + r2 * (-0.5 +
+                    r2 * (1.0 / 24.0 +
+                          r2 * (-1.0 / 720.0 +
+                                r2 * (1.0 / 40320.0 +
+                                      r2 * (-1.0 / 3628800.0 +
+                                            r2 * (1.0 / 479001600.0 +
+                                                  r2 * (-1.0 / 87178291200.0 +
+                                                        r2 * (1.0 / 20922789888000.0 +
+                                                              r2 * (-1.0 / 6402373705728000.0)))))))));
+    switch (k & 3) {
+    case 0: *s = sp; *c = cp; break;
+    case 1: *s = cp; *c = -sp; break;
+    case 2: *s = -sp; *c = -cp; break;
+    default: *s = -cp; *c = sp; break;
+    }
+}
+
+void orc_pinned_sincos_deg(float angle_deg, float *c, float *s)
+{
+    const float factorPI = (float)(3.14159265358979323846 / 180.f);
+    const float angle = angle_deg * factorPI;
+    double sd, cd;
+    pinned_sincos((double)angle, &sd, &cd);
+    *c = (float)cd;
+    *s = (float)sd;
+}
+
+/* computeOrbDescriptor, ORBextractor.cc:117-157 */
+void orc_orb_descriptor(const orc_keypoint *kp, const uint8_t *img, int step, int brief_fma,
+                        uint8_t desc[32])
+{
+    float a, b;
+    orc_pinned_sincos_deg(kp->angle, &a, &b);
+    const uint8_t *center = img + (size_t)cv_round_f(kp->y) * step + cv_round_f(kp->x);
+    for (int i = 0; i < 32; ++i) {
+        int val = 0;
+        for (int bit = 0; bit < 8; bit++) {
+            const signed char *pp = orc_pattern[i * 8 + bit];
+            int t[2];
+            for (int s = 0; s < 2; s++) {
+                const float px = (float)pp[2 * s], py = (float)pp[2 * s + 1];
+                float ry, rx;
+                if (brief_fma) {
+                    ry = fmaf(px, b, py * a);
+                    rx = fmaf(px, a, -(py * b));
+                } else {
+                    const float t0 = px * b, t1 = py * a, t2 = px * a, t3 = py * b;
+                    ry = t0 + t1;
+                    rx = t2 - t3;
+                }
+                t[s] = center[cv_round_f(ry) * step + cv_round_f(rx)];
+            }
+            val |= (t[0] < t[1]) << bit;
+        }
+        desc[i] = (uint8_t)val;
+    }
+}
+
+/* ------------------------------------------------------------------ */
+/* ComputeKeyPointsOctTree's FAST part for one level, :970-1094          */
+/* ------------------------------------------------------------------ */
+int orc_level_candidates(const orc_params *p, const uint8_t *lvl, int lw, int lh, int step,
+                         int level, orc_keypoint *out, int cap)
+{
+    (void)level;
+    const float W = 30;
+    const int minBorderX = EDGE_THRESHOLD - 3, minBorderY = minBorderX;
+    const int maxBorderX = lw - EDGE_THRESHOLD + 3, maxBorderY = lh - EDGE_THRESHOLD + 3;
+    const float width = (float)(maxBorderX - minBorderX);
+    const float height = (float)(maxBorderY - minBorderY);
+    const int nCols = (int)(width / W), nRows = (int)(height / W);
+    if (nCols <= 0 || nRows <= 0)
+        return -22; /* reference divides by zero */
+    const int wCell = (int)ceilf(width / nCols), hCell = (int)ceilf(height / nRows);
+    int n = 0;
+    orc_keypoint *cell = (orc_keypoint *)malloc(sizeof(orc_keypoint) * (size_t)(wCell + 6) *
+                                                (hCell + 6));
+    const int cell_cap = (wCell + 6) * (hCell + 6);
+    for (int i = 0; i < nRows; i++) {
+        const float iniY = (float)(minBorderY + i * hCell);
+        float maxY = iniY + hCell + 6;
+        if (iniY >= maxBorderY - 3)
+            continue;
+        if (maxY > maxBorderY)
+            maxY = (float)maxBorderY;
+        for (int j = 0; j < nCols; j++) {
+            const float iniX = (float)(minBorderX + j * wCell);
+            float maxX = iniX + wCell + 6;
+            if (iniX >= maxBorderX - 6)
+                continue;
+            if (maxX > maxBorderX)
+                maxX = (float)maxBorderX;
+            const int y0 = (int)iniY, y1 = (int)maxY, x0 = (int)iniX, x1 = (int)maxX;
+            const uint8_t *roi = lvl + (size_t)y0 * step + x0;
+            int nc = orc_fast_window(roi, step, x1 - x0, y1 - y0, p->ini_th_fast, cell, cell_cap);
+            if (nc == 0)
+                nc = orc_fast_window(roi, step, x1 - x0, y1 - y0, p->min_th_fast, cell, cell_cap);
+            for (int k = 0; k < nc; k++) {
+                cell[k].x += j * wCell;
+                cell[k].y += i * hCell;
+                if (n < cap)
+                    out[n] = cell[k];
+                n++;
+            }
+        }
+    }
+    free(cell);
+    return n;
+}
+
+/* ------------------------------------------------------------------ */
+/* ORBextractor::operator(), :1330-1397                                 */
+/* ------------------------------------------------------------------ */
+int orc_extract(const orc_params *p, const uint8_t *img, int w, int h, int step,
+                orc_keypoint *kps, uint8_t *desc, int cap, int32_t *level_counts, uint8_t *pyr,
+                int32_t *cand_counts)
+{
+    if (w <= 0 || h <= 0 || img == NULL)
+        return 0; /* empty image: return, outputs untouched (:1333-1334) */
+    const int L = p->nlevels;
+    int lw[ORC_MAX_LEVELS], lh[ORC_MAX_LEVELS];
+    size_t off[ORC_MAX_LEVELS + 1];
+    off[0] = 0;
+    for (int l = 0; l < L; l++) {
+        orc_level_size(p, w, h, l, &lw[l], &lh[l]);
+        off[l + 1] = off[l] + (size_t)lw[l] * lh[l];
+        if (l > 0 && lw[l - 1] == 2 * lw[l] && lh[l - 1] == 2 * lh[l])
+            return -95; /* cv::resize switches to INTER_AREA for exact 2x: not restated */
+    }
+    uint8_t *levels = (uint8_t *)malloc(off[L]);
+    for (int y = 0; y < h; y++)
+        memcpy(levels + (size_t)y * w, img + (size_t)y * step, w);
+    for (int l = 1; l < L; l++)
+        orc_resize_linear_u8(levels + off[l - 1], lw[l - 1], lh[l - 1], lw[l - 1], levels + off[l],
+                             lw[l], lh[l], lw[l], p->resize_mode);
+    if (pyr)
+        memcpy(pyr, levels, off[L]);
+
+    orc_keypoint *lk[ORC_MAX_LEVELS];
+    int nk[ORC_MAX_LEVELS];
+    int total = 0, err = 0;
+    for (int l = 0; l < L; l++) {
+        const int lcap = (lw[l] * lh[l]) / 2 + 16;
+        orc_keypoint *cand = (orc_keypoint *)malloc(sizeof(orc_keypoint) * lcap);
+        int nc = orc_level_candidates(p, levels + off[l], lw[l], lh[l], lw[l], l, cand, lcap);
+        if (nc < 0) {
+            err = nc;
+            free(cand);
+            lk[l] = NULL;
+            nk[l] = 0;
+            continue;
+        }
+        if (cand_counts)
+            cand_counts[l] = nc;
+        const int minB = EDGE_THRESHOLD - 3;
+        const int maxBX = lw[l] - EDGE_THRESHOLD + 3, maxBY = lh[l] - EDGE_THRESHOLD + 3;
+        const int ocap = p->features_per_level[l] + 8 + 64;
+        lk[l] = (orc_keypoint *)malloc(sizeof(orc_keypoint) * ocap);
+        int no = orc_distribute_octree(cand, nc, minB, maxBX, minB, maxBY,
+                                       p->features_per_level[l], lk[l], ocap);
+        free(cand);
+        if (no < 0) {
+            err = no;
+            nk[l] = 0;
+            continue;
+        }
+        if (no > ocap)
+            no = ocap;
+        const int scaledPatchSize = (int)(PATCH_SIZE * p->scale[l]);
+        for (int i = 0; i < no; i++) {
+            lk[l][i].x += minB;
+            lk[l][i].y += minB;
+            lk[l][i].octave = l;
+            lk[l][i].size = (float)scaledPatchSize;
+        }
+        nk[l] = no;
+        total += no;
+    }
+    if (err) {
+        for (int l = 0; l < L; l++)
+            free(lk[l]);
+        free(levels);
+        return err;
+    }
+    for (int l = 0; l < L; l++)
+        for (int i = 0; i < nk[l]; i++)
+            lk[l][i].angle =
+                orc_ic_angle(levels + off[l], lw[l], lk[l][i].x, lk[l][i].y, p->umax);
+
+    int o = 0;
+    for (int l = 0; l < L; l++) {
+        if (level_counts)
+            level_counts[l] = nk[l];
+        if (nk[l] == 0)
+            continue;
+        uint8_t *blur = NULL;
+        if (desc) {
+            blur = (uint8_t *)malloc((size_t)lw[l] * lh[l]);
+            orc_gauss7_u8(levels + off[l], lw[l], lh[l], lw[l], blur, lw[l], p->gauss_k);
+        }
+        for (int i = 0; i < nk[l]; i++, o++) {
+            if (o >= cap)
+                continue;
+            if (desc)
+                orc_orb_descriptor(&lk[l][i], blur, lw[l], p->brief_fma, desc + (size_t)o * 32);
+            orc_keypoint k = lk[l][i];
+            if (l != 0) {
+                const float s = p->scale[l];
+                k.x *= s;
+                k.y *= s;
+            }
+            if (kps)
+                kps[o] = k;
+        }
+        free(blur);
+    }
+    for (int l = 0; l < L; l++)
+        free(lk[l]);
+    free(levels);
+    return total;
+}
+
+/* ------------------------------------------------------------------ */
+/* CPU baseline: independent frames on pthreads                          */
+/* ------------------------------------------------------------------ */
+typedef struct {
+    const orc_params *p;
+    const uint8_t *imgs;
+    int w, h, f0, f1;
+    int32_t *counts;
+    long total;
+} batch_job;
+
+static void *batch_worker(void *arg)
+{
+    batch_job *j = (batch_job *)arg;
+    const int cap = j->p->nfeatures * 2 + 256;
+    orc_keypoint *k = (orc_keypoint *)malloc(sizeof(orc_keypoint) * cap);
+    uint8_t *d = (uint8_t *)malloc((size_t)cap * 32);
+    for (int f = j->f0; f < j->f1; f++) {
+        int n = orc_extract(j->p, j->imgs + (size_t)f * j->w * j->h, j->w, j->h, j->w, k, d, cap,
+                            NULL, NULL, NULL);
+        if (j->counts)
+            j->counts[f] = n;
+        j->total += n;
+    }
+    free(k);
+    free(d);
+    return NULL;
+}
+
+long orc_extract_batch(const orc_params *p, const uint8_t *imgs, int nframes, int w, int h,
+                       int nthreads, int32_t *counts_out)
+{
+    if (nthreads < 1)
+        nthreads = 1;
+    if (nthreads > nframes)
+        nthreads = nframes > 0 ? nframes : 1;
+    pthread_t th[256];
+    batch_job jobs[256];
+    if (nthreads > 256)
+        nthreads = 256;
+    for (int t = 0; t < nthreads; t++) {
+        jobs[t].p = p;
+        jobs[t].imgs = imgs;
+        jobs[t].w = w;
+        jobs[t].h = h;
+        jobs[t].f0 = (int)((long)nframes * t / nthreads);
+        jobs[t].f1 = (int)((long)nframes * (t + 1) / nthreads);
+        jobs[t].counts = counts_out;
+        jobs[t].total = 0;
+        pthread_create(&th[t], NULL, batch_worker, &jobs[t]);
+    }
+    long total = 0;
+    for (int t = 0; t < nthreads; t++) {
+        pthread_join(th[t], NULL);
+        total += jobs[t].total;
+    }
+    return total;
+}
+
+/* ------------------------------------------------------------------ */
+/* CPU baseline for the bench unit "frame" = extract(t) + match(t-1,t):  */
+/* all-pairs knn2 + SearchForInitialization(window, nnratio, checkOri). */
+/* Each thread takes a contiguous block of frames and re-extracts the   */
+/* block's predecessor (1-frame halo), like the GPU sharding.           */
+/* ------------------------------------------------------------------ */
+typedef struct {
+    const orc_params *p;
+    const uint8_t *imgs;
+    int w, h, f0, f1, nframes, window;
+    float nnratio;
+    int32_t *nkp, *nmatch;
+} frames_job;
+
+static void *frames_worker(void *arg)
+{
+    frames_job *j = (frames_job *)arg;
+    const int cap = j->p->nfeatures * 2 + 256;
+    orc_keypoint *k[2];
+    uint8_t *d[2];
+    int n[2];
+    for (int s = 0; s < 2; s++) {
+        k[s] = (orc_keypoint *)malloc(sizeof(orc_keypoint) * cap);
+        d[s] = (uint8_t *)malloc((size_t)cap * 32);
+    }
+    int32_t *bi = (int32_t *)malloc(sizeof(int32_t) * cap * 4);
+    float *prev = (float *)malloc(sizeof(float) * 2 * cap);
+    const orc_bounds b = {0.f, (float)j->w, 0.f, (float)j->h};
+    const size_t fsz = (size_t)j->w * j->h;
+    int cur = 0;
+    const int fprev = (j->f0 + j->nframes - 1) % j->nframes;
+    n[1] = orc_extract(j->p, j->imgs + fprev * fsz, j->w, j->h, j->w, k[1], d[1], cap, NULL, NULL,
+                       NULL);
+    for (int f = j->f0; f < j->f1; f++) {
+        const int pv = cur ^ 1;
+        n[cur] = orc_extract(j->p, j->imgs + f * fsz, j->w, j->h, j->w, k[cur], d[cur], cap, NULL,
+                             NULL, NULL);
+        orc_knn2(d[cur], n[cur], d[pv], n[pv], bi, bi + cap, bi + 2 * cap);
+        for (int i = 0; i < n[pv]; i++) {
+            prev[2 * i] = k[pv][i].x;
+            prev[2 * i + 1] = k[pv][i].y;
+        }
+        int nm = orc_search_for_initialization(k[pv], d[pv], n[pv], k[cur], d[cur], n[cur], &b,
+                                               prev, bi + 3 * cap, j->window, j->nnratio, 1);
+        if (j->nkp)
+            j->nkp[f] = n[cur];
+        if (j->nmatch)
+            j->nmatch[f] = nm;
+        cur ^= 1;
+    }
+    for (int s = 0; s < 2; s++) {
+        free(k[s]);
+        free(d[s]);
+    }
+    free(bi);
+    free(prev);
+    return NULL;
+}
+
+int orc_frames_batch(const orc_params *p, const uint8_t *imgs, int nframes, int w, int h,
+                     int nthreads, int window, float nnratio, int32_t *nkp, int32_t *nmatch)
+{
+    if (nframes <= 0)
+        return 0;
+    if (nthreads < 1)
+        nthreads = 1;
+    if (nthreads > nframes)
+        nthreads = nframes;
+    if (nthreads > 256)
+        nthreads = 256;
+    pthread_t th[256];
+    frames_job jobs[256];
+    for (int t = 0; t < nthreads; t++) {
+        jobs[t].p = p;
+        jobs[t].imgs = imgs;
+        jobs[t].w = w;
+        jobs[t].h = h;
+        jobs[t].nframes = nframes;
+        jobs[t].f0 = (int)((long)nframes * t / nthreads);
+        jobs[t].f1 = (int)((long)nframes * (t + 1) / nthreads);
+        jobs[t].window = window;
+        jobs[t].nnratio = nnratio;
+        jobs[t].nkp = nkp;
+        jobs[t].nmatch = nmatch;
+        pthread_create(&th[t], NULL, frames_worker, &jobs[t]);
+    }
+    for (int t = 0; t < nthreads; t++)
+        pthread_join(th[t], NULL);
+    return nframes;
+}

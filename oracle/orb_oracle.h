@@ -1,0 +1,176 @@
+/*
+ * oracle/orb_oracle.h -- TEST INFRASTRUCTURE ONLY.
+ *
+ * A plain-C CPU restatement of the ORB-SLAM2 per-frame hot path, used as the
+ * parity CHECKER by tests/, __graft_entry__.smoke() and bench.py's
+ * cpu_baseline leg.  It is never linked into, loaded by, or called from the
+ * product library (liborbg.so); the product fails loudly without its HIP code.
+ *
+ * What it restates (reference = /root/reference, read as text only):
+ *   ORBextractor ctor tables ........ src/ORBextractor.cc:432-521
+ *   ComputePyramid .................. src/ORBextractor.cc:1400-1443 (+ cv::resize pin)
+ *   ComputeKeyPointsOctTree (FAST) .. src/ORBextractor.cc:966-1128  (+ cv::FAST pin)
+ *   DistributeOctTree / DivideNode .. src/ORBextractor.cc:668-951, 537-614
+ *   IC_Angle / computeOrientation ... src/ORBextractor.cc:83-111, 523-530 (+ fastAtan2 pin)
+ *   GaussianBlur + computeOrbDesc ... src/ORBextractor.cc:1366-1396, 117-157, 1310-1317
+ *   ORBmatcher::DescriptorDistance .. src/ORBmatcher.cc:1846-1862
+ *   ORBmatcher::SearchForInit ....... src/ORBmatcher.cc:487-631, 1800-1841
+ *   Frame grid / GetFeaturesInArea .. src/Frame.cc:292-307, 421-520
+ *   g2o edge arithmetic (double) .... Thirdparty/g2o/g2o/types/types_six_dof_expmap.{h,cpp},
+ *                                     core/base_binary_edge.hpp:55-120, core/base_edge.h:58-102,
+ *                                     core/robust_kernel_impl.cpp:65-91
+ *
+ * Parity pinning status (see DESIGN.md "Oracle"):
+ *   - PINNED by the reference text: the rBRIEF pattern, umax, per-level feature
+ *     counts / level sizes, matcher constants (tests/golden/ref_tables.json), and
+ *     g2o's own central-difference Jacobian (base_binary_edge.hpp:131-205).
+ *   - UNPINNED: whole keypoint/descriptor outputs.  The reference ships no tests,
+ *     fixtures or golden vectors, and cannot be compiled here (it needs OpenCV,
+ *     Eigen and Pangolin, none present).  The OpenCV primitives it calls are
+ *     restated from OpenCV 3.4 semantics and are switchable (ORC_RESIZE_*, Gaussian
+ *     weights) -- "parity unpinned" for those outputs.
+ */
+#ifndef ORB_ORACLE_H
+#define ORB_ORACLE_H
+
+#include <stdint.h>
+#include <stddef.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define ORC_MAX_LEVELS 16
+
+/* cv::KeyPoint field order (pt.x, pt.y, size, angle, response, octave, class_id): 28 bytes */
+typedef struct {
+    float x, y, size, angle, response;
+    int32_t octave, class_id;
+} orc_keypoint;
+
+/* cv::resize INTER_LINEAR 8UC1 vertical-pass variants (see orb_oracle.c, orc_resize_linear_u8) */
+enum {
+    ORC_RESIZE_SCALAR = 0,     /* FixedPtCast<int,uchar,22> everywhere                   */
+    ORC_RESIZE_SSE2_16_4 = 4,  /* OpenCV 2.4-3.3 SSE2 VResizeLinearVec_32s8u (16 then 4)  */
+    ORC_RESIZE_SIMD_16_8 = 8   /* OpenCV 3.4 universal intrinsics (16 then 8)  [default] */
+};
+
+typedef struct {
+    /* ctor arguments, ORBextractor.h:64-65 */
+    int32_t nfeatures;
+    float scale_factor;
+    int32_t nlevels;
+    int32_t ini_th_fast;
+    int32_t min_th_fast;
+    /* derived tables, ORBextractor.cc:437-476 */
+    float scale[ORC_MAX_LEVELS];
+    float inv_scale[ORC_MAX_LEVELS];
+    float sigma2[ORC_MAX_LEVELS];
+    float inv_sigma2[ORC_MAX_LEVELS];
+    int32_t features_per_level[ORC_MAX_LEVELS];
+    int32_t umax[16];
+    /* OpenCV-primitive pins */
+    int32_t resize_mode;       /* ORC_RESIZE_* */
+    int32_t gauss_k[7];        /* 7-tap weights (sum 256 for the bit-exact 3.4.9+ table) */
+    int32_t brief_fma;         /* 0: x*b + y*a rounded twice (default); 1: fused */
+} orc_params;
+
+/* ---- extractor ---- */
+int orc_init_params(orc_params *p, int nfeatures, float scale_factor, int nlevels,
+                    int ini_th_fast, int min_th_fast);
+void orc_level_size(const orc_params *p, int w, int h, int level, int *lw, int *lh);
+
+void orc_resize_linear_u8(const uint8_t *src, int sw, int sh, int sstep,
+                          uint8_t *dst, int dw, int dh, int dstep, int mode);
+void orc_gauss7_u8(const uint8_t *src, int w, int h, int sstep, uint8_t *dst, int dstep,
+                   const int32_t k[7]);
+int orc_fast_score(const uint8_t *p, int step);              /* cornerScore<16> + corner test */
+int orc_fast_window(const uint8_t *img, int step, int w, int h, int th,
+                    orc_keypoint *out, int cap);             /* cv::FAST(roi, kps, th, true) */
+int orc_distribute_octree(const orc_keypoint *keys, int n, int minX, int maxX, int minY,
+                          int maxY, int N, orc_keypoint *out, int cap);
+float orc_fast_atan2(float y, float x);
+float orc_ic_angle(const uint8_t *img, int step, float px, float py, const int32_t umax[16]);
+void orc_pinned_sincos_deg(float angle_deg, float *c, float *s);
+void orc_orb_descriptor(const orc_keypoint *kp, const uint8_t *img, int step, int brief_fma,
+                        uint8_t desc[32]);
+
+/* Full ORBextractor::operator() for one 8-bit image.
+ * Returns the number of keypoints (>=0) or a negative error.  kps/desc may be NULL
+ * to query the count.  If level_counts != NULL it receives per-level counts.
+ * If pyr != NULL it must hold sum_l(lw*lh) bytes; receives the levels packed (pitch = lw).
+ * If cand_counts != NULL it receives per-level FAST candidate counts. */
+int orc_extract(const orc_params *p, const uint8_t *img, int w, int h, int step,
+                orc_keypoint *kps, uint8_t *desc, int cap, int32_t *level_counts,
+                uint8_t *pyr, int32_t *cand_counts);
+/* Per-level candidate list (vToDistributeKeys, coordinates relative to minBorder) */
+int orc_level_candidates(const orc_params *p, const uint8_t *lvl, int lw, int lh, int step,
+                         int level, orc_keypoint *out, int cap);
+/* Batch of frames on nthreads pthreads (cpu baseline); returns total keypoints */
+long orc_extract_batch(const orc_params *p, const uint8_t *imgs, int nframes, int w, int h,
+                       int nthreads, int32_t *counts_out);
+
+/* frames = extract(t) + knn2(t, t-1) + SearchForInitialization(t-1 -> t); pthreads */
+int orc_frames_batch(const orc_params *p, const uint8_t *imgs, int nframes, int w, int h,
+                     int nthreads, int window, float nnratio, int32_t *nkp, int32_t *nmatch);
+
+/* ---- matcher ---- */
+int orc_descriptor_distance(const uint8_t *a, const uint8_t *b);
+void orc_knn2(const uint8_t *qdesc, int nq, const uint8_t *tdesc, int nt, int32_t *best_idx,
+              int32_t *best_dist, int32_t *second_dist);
+
+typedef struct {
+    float min_x, max_x, min_y, max_y;   /* Frame::mnMinX.. (ComputeImageBounds) */
+} orc_bounds;
+
+/* ORBmatcher(nnratio, checkOri).SearchForInitialization(F1, F2, prev, matches12, window).
+ * kps1/kps2 are mvKeysUn (x, y, angle, octave used).  prev_xy (2*n1 floats) is updated
+ * in place.  Returns nmatches. */
+int orc_search_for_initialization(const orc_keypoint *kps1, const uint8_t *desc1, int n1,
+                                  const orc_keypoint *kps2, const uint8_t *desc2, int n2,
+                                  const orc_bounds *b2, float *prev_xy, int32_t *matches12,
+                                  int window, float nnratio, int check_ori);
+
+/* ---- local BA edge linearisation (double) ---- */
+typedef struct {
+    double q[4];   /* x, y, z, w (Eigen coeffs order) */
+    double t[3];
+    int32_t fixed;
+    int32_t pad;
+} orc_pose;
+
+typedef struct {
+    int32_t point;     /* vertex 0 (VertexSBAPointXYZ) */
+    int32_t pose;      /* vertex 1 (VertexSE3Expmap)  */
+    int32_t stereo;    /* 0: EdgeSE3ProjectXYZ, 1: EdgeStereoSE3ProjectXYZ */
+    int32_t robust;    /* 1: Huber attached (first optimize), 0: removed */
+    int32_t active;    /* level 0 edge (1) or setLevel(1) edge (0) */
+    int32_t pad;
+    double obs[3];
+    double inv_sigma2;
+    double fx, fy, cx, cy, bf;
+    double huber_delta;   /* (double)(float)sqrt(5.991) / sqrt(7.815) */
+} orc_edge;
+
+typedef struct {
+    double err[3];
+    double chi2;
+    double rho1;       /* Huber weight */
+    double jp[3][3];   /* _jacobianOplusXi (point) */
+    double jt[3][6];   /* _jacobianOplusXj (pose)  */
+    double hpl[3][6];  /* per-edge off-diagonal block A^T W B */
+} orc_edge_out;
+
+/* computeError + linearizeOplus + constructQuadraticForm for every active edge.
+ * hpose: npose*36 + bpose: npose*6, hpoint: npoint*9 + bpoint: npoint*3 (zeroed here). */
+void orc_ba_linearize(const orc_pose *poses, int npose, const double *points, int npoint,
+                      const orc_edge *edges, int nedge, orc_edge_out *eout, double *hpose,
+                      double *bpose, double *hpoint, double *bpoint);
+/* central-difference Jacobian of computeError (base_binary_edge.hpp:131-205, delta 1e-9) */
+void orc_ba_numeric_jacobian(const orc_pose *pose, const double *xyz, const orc_edge *e,
+                             double jp[3][3], double jt[3][6]);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

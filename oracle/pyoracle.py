@@ -1,0 +1,258 @@
+"""ctypes front-end of the CPU oracle -- TEST INFRASTRUCTURE ONLY.
+
+Only tests/, ``__graft_entry__.smoke()`` and bench.py's ``cpu_baseline`` leg may
+import this module.  The product (``orb_slam2_test_amd``) never does.
+
+The oracle restates the reference algorithms (see oracle/orb_oracle.h for the
+file:line map) in plain C; this module builds ``oracle/_build/liborbg_oracle.so``
+on demand (gcc) and exposes numpy-friendly wrappers.
+"""
+import ctypes as C
+import os
+import subprocess
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "_build", "liborbg_oracle.so")
+
+MAX_LEVELS = 16
+
+KP_DTYPE = np.dtype([("x", "<f4"), ("y", "<f4"), ("size", "<f4"), ("angle", "<f4"),
+                     ("response", "<f4"), ("octave", "<i4"), ("class_id", "<i4")])
+POSE_DTYPE = np.dtype([("q", "<f8", 4), ("t", "<f8", 3), ("fixed", "<i4"), ("pad", "<i4")])
+EDGE_DTYPE = np.dtype([("point", "<i4"), ("pose", "<i4"), ("stereo", "<i4"), ("robust", "<i4"),
+                       ("active", "<i4"), ("pad", "<i4"), ("obs", "<f8", 3),
+                       ("inv_sigma2", "<f8"), ("fx", "<f8"), ("fy", "<f8"), ("cx", "<f8"),
+                       ("cy", "<f8"), ("bf", "<f8"), ("huber_delta", "<f8")])
+EDGE_OUT_DTYPE = np.dtype([("err", "<f8", 3), ("chi2", "<f8"), ("rho1", "<f8"),
+                           ("jp", "<f8", (3, 3)), ("jt", "<f8", (3, 6)), ("hpl", "<f8", (3, 6))])
+
+RESIZE_SCALAR, RESIZE_SSE2_16_4, RESIZE_SIMD_16_8 = 0, 4, 8
+
+
+class Params(C.Structure):
+    _fields_ = [("nfeatures", C.c_int32), ("scale_factor", C.c_float), ("nlevels", C.c_int32),
+                ("ini_th_fast", C.c_int32), ("min_th_fast", C.c_int32),
+                ("scale", C.c_float * MAX_LEVELS), ("inv_scale", C.c_float * MAX_LEVELS),
+                ("sigma2", C.c_float * MAX_LEVELS), ("inv_sigma2", C.c_float * MAX_LEVELS),
+                ("features_per_level", C.c_int32 * MAX_LEVELS), ("umax", C.c_int32 * 16),
+                ("resize_mode", C.c_int32), ("gauss_k", C.c_int32 * 7), ("brief_fma", C.c_int32)]
+
+
+class Bounds(C.Structure):
+    _fields_ = [("min_x", C.c_float), ("max_x", C.c_float), ("min_y", C.c_float),
+                ("max_y", C.c_float)]
+
+
+_lib = None
+
+
+def build(force=False):
+    """Compile the oracle with its Makefile (gcc).  Returns the .so path."""
+    srcs = [os.path.join(HERE, f) for f in ("orb_oracle.c", "match_oracle.c", "ba_oracle.c",
+                                            "orb_oracle.h", "orb_pattern.inc")]
+    if force or not os.path.exists(LIB_PATH) or any(
+            os.path.getmtime(s) > os.path.getmtime(LIB_PATH) for s in srcs if os.path.exists(s)):
+        subprocess.check_call(["make", "-s", "-C", HERE])
+    return LIB_PATH
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            build()
+        L = C.CDLL(LIB_PATH)
+        P = C.POINTER
+        vp = C.c_void_p
+        L.orc_init_params.argtypes = [P(Params), C.c_int, C.c_float, C.c_int, C.c_int, C.c_int]
+        L.orc_extract.argtypes = [P(Params), vp, C.c_int, C.c_int, C.c_int, vp, vp, C.c_int, vp,
+                                  vp, vp]
+        L.orc_level_candidates.argtypes = [P(Params), vp, C.c_int, C.c_int, C.c_int, C.c_int, vp,
+                                           C.c_int]
+        L.orc_distribute_octree.argtypes = [vp, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int,
+                                            C.c_int, vp, C.c_int]
+        L.orc_resize_linear_u8.argtypes = [vp, C.c_int, C.c_int, C.c_int, vp, C.c_int, C.c_int,
+                                           C.c_int, C.c_int]
+        L.orc_gauss7_u8.argtypes = [vp, C.c_int, C.c_int, C.c_int, vp, C.c_int, vp]
+        L.orc_fast_score.argtypes = [vp, C.c_int]
+        L.orc_fast_window.argtypes = [vp, C.c_int, C.c_int, C.c_int, C.c_int, vp, C.c_int]
+        L.orc_fast_atan2.argtypes = [C.c_float, C.c_float]
+        L.orc_fast_atan2.restype = C.c_float
+        L.orc_ic_angle.argtypes = [vp, C.c_int, C.c_float, C.c_float, vp]
+        L.orc_ic_angle.restype = C.c_float
+        L.orc_pinned_sincos_deg.argtypes = [C.c_float, P(C.c_float), P(C.c_float)]
+        L.orc_descriptor_distance.argtypes = [vp, vp]
+        L.orc_knn2.argtypes = [vp, C.c_int, vp, C.c_int, vp, vp, vp]
+        L.orc_search_for_initialization.argtypes = [vp, vp, C.c_int, vp, vp, C.c_int,
+                                                    P(Bounds), vp, vp, C.c_int, C.c_float,
+                                                    C.c_int]
+        L.orc_frames_batch.argtypes = [P(Params), vp, C.c_int, C.c_int, C.c_int, C.c_int,
+                                       C.c_int, C.c_float, vp, vp]
+        L.orc_extract_batch.argtypes = [P(Params), vp, C.c_int, C.c_int, C.c_int, C.c_int, vp]
+        L.orc_extract_batch.restype = C.c_long
+        L.orc_ba_linearize.argtypes = [vp, C.c_int, vp, C.c_int, vp, C.c_int, vp, vp, vp, vp, vp]
+        L.orc_ba_numeric_jacobian.argtypes = [vp, vp, vp, vp, vp]
+        _lib = L
+    return _lib
+
+
+def _p(a):
+    return a.ctypes.data_as(C.c_void_p) if a is not None else None
+
+
+def params(nfeatures=2000, scale_factor=1.2, nlevels=8, ini_th_fast=20, min_th_fast=7,
+           resize_mode=RESIZE_SIMD_16_8, gauss_k=None, brief_fma=0):
+    p = Params()
+    rc = lib().orc_init_params(C.byref(p), nfeatures, scale_factor, nlevels, ini_th_fast,
+                               min_th_fast)
+    if rc != 0:
+        raise ValueError("orc_init_params: %d" % rc)
+    p.resize_mode = resize_mode
+    if gauss_k is not None:
+        for i in range(7):
+            p.gauss_k[i] = int(gauss_k[i])
+    p.brief_fma = brief_fma
+    return p
+
+
+def level_sizes(p, w, h):
+    out = []
+    for l in range(p.nlevels):
+        s = np.float32(p.inv_scale[l])
+        out.append((int(np.rint(np.float32(w) * s)), int(np.rint(np.float32(h) * s))))
+    return out
+
+
+def extract(p, img, with_pyramid=False, with_desc=True):
+    """ORBextractor::operator() restated.  Returns dict(kps, desc, level_counts[, pyramid])."""
+    img = np.ascontiguousarray(img, dtype=np.uint8)
+    h, w = img.shape
+    cap = p.nfeatures * 2 + 8 * 70
+    kps = np.zeros(cap, KP_DTYPE)
+    desc = np.zeros((cap, 32), np.uint8) if with_desc else None
+    lc = np.zeros(MAX_LEVELS, np.int32)
+    cc = np.zeros(MAX_LEVELS, np.int32)
+    sizes = level_sizes(p, w, h)
+    pyr = np.zeros(sum(a * b for a, b in sizes), np.uint8) if with_pyramid else None
+    n = lib().orc_extract(C.byref(p), _p(img), w, h, w, _p(kps), _p(desc), cap, _p(lc), _p(pyr),
+                          _p(cc))
+    if n < 0:
+        raise RuntimeError("orc_extract failed: %d" % n)
+    out = {"kps": kps[:n].copy(), "level_counts": lc[:p.nlevels].copy(),
+           "cand_counts": cc[:p.nlevels].copy()}
+    if with_desc:
+        out["desc"] = desc[:n].copy()
+    if with_pyramid:
+        levels, o = [], 0
+        for (lw, lh) in sizes:
+            levels.append(pyr[o:o + lw * lh].reshape(lh, lw).copy())
+            o += lw * lh
+        out["pyramid"] = levels
+    return out
+
+
+def level_candidates(p, lvl, level):
+    lvl = np.ascontiguousarray(lvl, dtype=np.uint8)
+    lh, lw = lvl.shape
+    cap = lw * lh // 2 + 16
+    out = np.zeros(cap, KP_DTYPE)
+    n = lib().orc_level_candidates(C.byref(p), _p(lvl), lw, lh, lw, level, _p(out), cap)
+    if n < 0:
+        raise RuntimeError("orc_level_candidates failed: %d" % n)
+    return out[:n].copy()
+
+
+def resize_linear(src, dw, dh, mode=RESIZE_SIMD_16_8):
+    src = np.ascontiguousarray(src, dtype=np.uint8)
+    sh, sw = src.shape
+    dst = np.zeros((dh, dw), np.uint8)
+    lib().orc_resize_linear_u8(_p(src), sw, sh, sw, _p(dst), dw, dh, dw, mode)
+    return dst
+
+
+def gauss7(src, k=(18, 34, 48, 56, 48, 34, 18)):
+    src = np.ascontiguousarray(src, dtype=np.uint8)
+    h, w = src.shape
+    dst = np.zeros_like(src)
+    kk = np.asarray(k, np.int32)
+    lib().orc_gauss7_u8(_p(src), w, h, w, _p(dst), w, _p(kk))
+    return dst
+
+
+def fast_atan2(y, x):
+    return lib().orc_fast_atan2(float(y), float(x))
+
+
+def sincos_deg(a):
+    c, s = C.c_float(), C.c_float()
+    lib().orc_pinned_sincos_deg(float(a), C.byref(c), C.byref(s))
+    return c.value, s.value
+
+
+def descriptor_distance(a, b):
+    a = np.ascontiguousarray(a, np.uint8)
+    b = np.ascontiguousarray(b, np.uint8)
+    return lib().orc_descriptor_distance(_p(a), _p(b))
+
+
+def knn2(qdesc, tdesc):
+    qdesc = np.ascontiguousarray(qdesc, np.uint8)
+    tdesc = np.ascontiguousarray(tdesc, np.uint8)
+    nq, nt = len(qdesc), len(tdesc)
+    bi = np.zeros(nq, np.int32)
+    bd = np.zeros(nq, np.int32)
+    sd = np.zeros(nq, np.int32)
+    lib().orc_knn2(_p(qdesc), nq, _p(tdesc), nt, _p(bi), _p(bd), _p(sd))
+    return bi, bd, sd
+
+
+def search_for_initialization(kps1, desc1, kps2, desc2, prev_xy, bounds, window=100,
+                              nnratio=0.9, check_ori=True):
+    kps1 = np.ascontiguousarray(kps1, KP_DTYPE)
+    kps2 = np.ascontiguousarray(kps2, KP_DTYPE)
+    desc1 = np.ascontiguousarray(desc1, np.uint8)
+    desc2 = np.ascontiguousarray(desc2, np.uint8)
+    prev = np.ascontiguousarray(prev_xy, np.float32).copy()
+    m12 = np.zeros(len(kps1), np.int32)
+    b = Bounds(*[float(v) for v in bounds])
+    n = lib().orc_search_for_initialization(_p(kps1), _p(desc1), len(kps1), _p(kps2), _p(desc2),
+                                            len(kps2), C.byref(b), _p(prev), _p(m12), window,
+                                            nnratio, 1 if check_ori else 0)
+    return n, m12, prev
+
+
+def frames_batch(p, imgs, nthreads=1, window=100, nnratio=0.9):
+    imgs = np.ascontiguousarray(imgs, np.uint8)
+    nf, h, w = imgs.shape
+    nkp = np.zeros(nf, np.int32)
+    nm = np.zeros(nf, np.int32)
+    lib().orc_frames_batch(C.byref(p), _p(imgs), nf, w, h, nthreads, window, nnratio, _p(nkp),
+                           _p(nm))
+    return nkp, nm
+
+
+def ba_linearize(poses, points, edges):
+    poses = np.ascontiguousarray(poses, POSE_DTYPE)
+    points = np.ascontiguousarray(points, np.float64)
+    edges = np.ascontiguousarray(edges, EDGE_DTYPE)
+    npose, npoint, nedge = len(poses), len(points), len(edges)
+    eout = np.zeros(nedge, EDGE_OUT_DTYPE)
+    hpose = np.zeros((npose, 6, 6))
+    bpose = np.zeros((npose, 6))
+    hpoint = np.zeros((npoint, 3, 3))
+    bpoint = np.zeros((npoint, 3))
+    lib().orc_ba_linearize(_p(poses), npose, _p(points), npoint, _p(edges), nedge, _p(eout),
+                           _p(hpose), _p(bpose), _p(hpoint), _p(bpoint))
+    return eout, hpose, bpose, hpoint, bpoint
+
+
+def ba_numeric_jacobian(pose, xyz, edge):
+    pose = np.ascontiguousarray(np.asarray(pose, POSE_DTYPE).reshape(1))
+    xyz = np.ascontiguousarray(xyz, np.float64)
+    edge = np.ascontiguousarray(np.asarray(edge, EDGE_DTYPE).reshape(1))
+    jp = np.zeros((3, 3))
+    jt = np.zeros((3, 6))
+    lib().orc_ba_numeric_jacobian(_p(pose), _p(xyz), _p(edge), _p(jp), _p(jt))
+    return jp, jt
