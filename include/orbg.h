@@ -1,0 +1,209 @@
+/*
+ * orbg.h -- C ABI of the MI355X-native ORB-SLAM2 hot path (liborbg.so).
+ *
+ * Plain pointers and sizes only; no C++ or torch types cross this boundary.
+ * Each entry point replaces one reference interface (/root/reference):
+ *
+ *   orbg_create / orbg_params ....... ORBextractor::ORBextractor(nfeatures, scaleFactor,
+ *                                     nlevels, iniThFAST, minThFAST)   include/ORBextractor.h:64-65
+ *                                                                      src/ORBextractor.cc:432-521
+ *   orbg_get_scale_tables ........... GetLevels/GetScaleFactor(s)/GetInverseScaleFactors/
+ *                                     GetScaleSigmaSquares/GetInverseScaleSigmaSquares
+ *                                                                      include/ORBextractor.h:78-98
+ *   orbg_extract .................... ORBextractor::operator()(image, mask, keypoints, descriptors)
+ *                                                                      include/ORBextractor.h:74-76
+ *                                                                      src/ORBextractor.cc:1330-1397
+ *   orbg_get_level .................. public std::vector<cv::Mat> mvImagePyramid
+ *                                                                      include/ORBextractor.h:101
+ *   orbg_descriptor_distance ........ static ORBmatcher::DescriptorDistance
+ *                                                                      src/ORBmatcher.cc:1846-1862
+ *   orbg_hamming_knn2 ............... brute-force 2-NN over DescriptorDistance (the matcher
+ *                                     loops' strict-< best/second rule, ORBmatcher.cc:541-556)
+ *   orbg_search_for_initialization .. ORBmatcher(nnratio,checkOri).SearchForInitialization(
+ *                                     F1, F2, vbPrevMatched, vnMatches12, windowSize)
+ *                                                                      src/ORBmatcher.cc:487-631
+ *   orbg_ba_linearize ............... g2o computeActiveErrors + BlockSolver::buildSystem arithmetic
+ *                                     for EdgeSE3ProjectXYZ / EdgeStereoSE3ProjectXYZ inside
+ *                                     Optimizer::LocalBundleAdjustment  src/Optimizer.cc:633-979
+ *
+ * Batched, device-resident entry points (orbg_*_device) run the same kernels over many
+ * frames at once; they exist for the batched-sequence mode and the bench.
+ *
+ * Conventions: every int-returning function returns ORBG_OK (0) or a negative errno-style
+ * code; orbg_last_error() gives a message for the calling thread.  No C++ exception crosses
+ * the ABI.  The caller owns all output buffers.  A context owns its device buffers and one
+ * HIP stream; a context is not thread-safe, distinct contexts may run concurrently (the two
+ * stereo extractors of Frame.cc:110-113).
+ */
+#ifndef ORBG_H
+#define ORBG_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define ORBG_ABI_VERSION 1
+#define ORBG_MAX_LEVELS 16
+
+#define ORBG_OK 0
+#define ORBG_EIO -5       /* HIP runtime / device error */
+#define ORBG_ENOMEM -12
+#define ORBG_EINVAL -22
+#define ORBG_ERANGE -34   /* caller capacity too small; *n_out holds the needed count */
+#define ORBG_ENOTSUP -95  /* configuration outside what the reference defines */
+
+/* cv::resize INTER_LINEAR 8UC1 vertical-pass variant (OpenCV build pin) */
+#define ORBG_RESIZE_SCALAR 0
+#define ORBG_RESIZE_SSE2_16_4 4
+#define ORBG_RESIZE_SIMD_16_8 8
+
+typedef struct orbg_ctx orbg_ctx;
+
+typedef struct {
+    /* ORBextractor ctor arguments */
+    int32_t nfeatures;
+    float scale_factor;
+    int32_t nlevels;
+    int32_t ini_th_fast;
+    int32_t min_th_fast;
+    /* OpenCV primitive pins (orbg_params_default sets the OpenCV 3.4 values) */
+    int32_t resize_mode;   /* ORBG_RESIZE_* */
+    int32_t gauss_k[7];    /* GaussianBlur 7x7 sigma=2 fixed-point weights */
+    int32_t brief_fma;     /* 1: fuse x*b + y*a in rBRIEF sampling (reference built -ffp-contract=fast) */
+    /* batch capacity (frames per orbg_extract_batch_device call); 0 -> 1 */
+    int32_t max_batch;
+} orbg_params;
+
+/* cv::KeyPoint layout: pt.x, pt.y, size, angle, response, octave, class_id (28 bytes) */
+typedef struct {
+    float x, y, size, angle, response;
+    int32_t octave, class_id;
+} orbg_keypoint;
+
+/* ---------------- context / extractor ---------------- */
+void orbg_params_default(orbg_params *p);
+int orbg_create(int device, const orbg_params *p, orbg_ctx **out);
+void orbg_destroy(orbg_ctx *ctx);
+const char *orbg_last_error(void);
+int orbg_abi_version(void);
+
+/* GetLevels / GetScaleFactor(s) / inverse / sigma^2 tables; any pointer may be NULL.
+ * Arrays must hold nlevels entries.  features_per_level = mnFeaturesPerLevel, umax[16]. */
+int orbg_get_scale_tables(const orbg_ctx *ctx, int32_t *nlevels, float *scale_factor,
+                          float *scale, float *inv_scale, float *sigma2, float *inv_sigma2,
+                          int32_t *features_per_level, int32_t *umax);
+/* the 256 rBRIEF test pairs (x0,y0,x1,y1) the kernels use (bit_pattern_31_) */
+int orbg_get_pattern(int32_t out[1024]);
+
+/* ORBextractor::operator() on one host image (CV_8UC1, row pitch `step`).
+ * w == 0 or h == 0: returns ORBG_OK with *n_out = -1 and outputs untouched (:1333-1334).
+ * Otherwise kps[0..n) in level order, desc n x 32 bytes row-major.  If cap < n, returns
+ * ORBG_ERANGE with *n_out = n and nothing written. */
+int orbg_extract(orbg_ctx *ctx, const uint8_t *img, int w, int h, size_t step,
+                 orbg_keypoint *kps, uint8_t *desc, int cap, int *n_out);
+
+/* mvImagePyramid[level] of frame `frame` of the last extraction (host copy). */
+int orbg_get_level(orbg_ctx *ctx, int frame, int level, uint8_t *dst, size_t dst_step, int *lw,
+                   int *lh);
+
+/* ---------------- batched, device-resident ---------------- */
+/* d_imgs: device pointer, nframes images of w x h, row pitch `step`, frame pitch
+ * `frame_stride` bytes.  Enqueued on the context stream; the caller keeps d_imgs alive
+ * until the next call (level 0 of the pyramid IS the input). */
+int orbg_extract_batch_device(orbg_ctx *ctx, const uint8_t *d_imgs, int nframes, int w, int h,
+                              size_t step, size_t frame_stride);
+/* device pointers to the last batch's outputs: frame f keypoints at d_kps + f*frame_cap,
+ * descriptors at d_desc + f*frame_cap*32, count d_counts[f]. */
+int orbg_batch_outputs(orbg_ctx *ctx, orbg_keypoint **d_kps, uint8_t **d_desc,
+                       int32_t **d_counts, int32_t *frame_cap);
+/* copy frame `frame` of the last batch to the host (synchronises) */
+int orbg_download_frame(orbg_ctx *ctx, int frame, orbg_keypoint *kps, uint8_t *desc, int cap,
+                        int *n_out);
+
+/* Match pairs of frames of the last batch on the device: for pair i, F1 = frame f1[i]
+ * (reference / previous), F2 = frame f2[i] (current).
+ *  - knn2: for every F2 keypoint, best/second distance and best index over all F1
+ *    descriptors (all-pairs Hamming).
+ *  - SearchForInitialization(F1, F2, vbPrevMatched = F1 keypoint positions, window)
+ *    with image bounds (0, w, 0, h) (undistorted KITTI-style frames, Frame.cc:603-609).
+ * Results stay on the device (orbg_match_outputs). */
+int orbg_match_batch_device(orbg_ctx *ctx, const int32_t *f1, const int32_t *f2, int npairs,
+                            int window, float nnratio, int check_ori);
+int orbg_match_outputs(orbg_ctx *ctx, int32_t **d_knn /* [npairs][frame_cap][3] */,
+                       int32_t **d_matches12 /* [npairs][frame_cap] */,
+                       int32_t **d_nmatches /* [npairs] */, int32_t *frame_cap);
+int orbg_download_matches(orbg_ctx *ctx, int pair, int32_t *knn, int32_t *matches12,
+                          int cap, int32_t *nmatches);
+
+int orbg_sync(orbg_ctx *ctx);
+void *orbg_stream(orbg_ctx *ctx); /* the hipStream_t the context launches on */
+
+/* per-kernel timing with HIP events on the context stream (for bench roofline) */
+int orbg_profile_enable(orbg_ctx *ctx, int enable);
+/* returns number of kernel kinds; fills name/total_ms/launches for index i */
+int orbg_profile_read(orbg_ctx *ctx, int i, const char **name, double *total_ms,
+                      int64_t *launches);
+int orbg_profile_reset(orbg_ctx *ctx);
+
+/* ---------------- matcher (host data) ---------------- */
+int orbg_descriptor_distance(const uint8_t *a, const uint8_t *b);
+
+/* best/second over all train descriptors for every query (strict <, lowest index on ties) */
+int orbg_hamming_knn2(orbg_ctx *ctx, const uint8_t *qdesc, int nq, const uint8_t *tdesc, int nt,
+                      int32_t *best_idx, int32_t *best_dist, int32_t *second_dist);
+
+typedef struct {
+    float min_x, max_x, min_y, max_y; /* Frame::mnMinX, mnMaxX, mnMinY, mnMaxY */
+} orbg_bounds;
+
+/* kps1/kps2 are mvKeysUn (x, y, angle, octave used); prev_xy (2*n1 floats) is
+ * vbPrevMatched, updated in place; matches12[n1] = vnMatches12. */
+int orbg_search_for_initialization(orbg_ctx *ctx, const orbg_keypoint *kps1,
+                                   const uint8_t *desc1, int n1, const orbg_keypoint *kps2,
+                                   const uint8_t *desc2, int n2, const orbg_bounds *bounds2,
+                                   float *prev_xy, int32_t *matches12, int window,
+                                   float nnratio, int check_ori, int *nmatches);
+
+/* ---------------- local BA linearisation ---------------- */
+typedef struct {
+    double q[4]; /* SE3Quat rotation, Eigen coeffs order (x, y, z, w), normalised */
+    double t[3];
+    int32_t fixed;
+    int32_t pad;
+} orbg_pose;
+
+typedef struct {
+    int32_t point;   /* vertex 0: VertexSBAPointXYZ */
+    int32_t pose;    /* vertex 1: VertexSE3Expmap */
+    int32_t stereo;  /* 0 EdgeSE3ProjectXYZ, 1 EdgeStereoSE3ProjectXYZ */
+    int32_t robust;  /* Huber kernel attached */
+    int32_t active;  /* level-0 edge */
+    int32_t pad;
+    double obs[3];
+    double inv_sigma2;
+    double fx, fy, cx, cy, bf;
+    double huber_delta;
+} orbg_edge;
+
+typedef struct {
+    double err[3];
+    double chi2;
+    double rho1;
+    double jp[3][3];
+    double jt[3][6];
+    double hpl[3][6];
+} orbg_edge_out;
+
+/* Host arrays in, host arrays out (uploads, runs the device kernels, downloads).
+ * eout may be NULL.  hpose npose*36, bpose npose*6, hpoint npoint*9, bpoint npoint*3. */
+int orbg_ba_linearize(orbg_ctx *ctx, const orbg_pose *poses, int npose, const double *points,
+                      int npoint, const orbg_edge *edges, int nedge, orbg_edge_out *eout,
+                      double *hpose, double *bpose, double *hpoint, double *bpoint);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* ORBG_H */

@@ -52,8 +52,12 @@ static void quat_to_rot(const double q[4], double R[3][3])
 }
 
 /* computeError with the pose given as (R, t) matrices (used by the numeric Jacobian) */
+/* exact_invz: evaluate the stereo projection with a double 1/z.  The reference's
+ * float invz (types_six_dof_expmap.cpp:151) makes the residual piecewise constant at
+ * ~1e-7 relative, so a 1e-9 central difference of it is noise; the analytic stereo
+ * Jacobian (:188-234) is the derivative of the double-precision model. */
 static void edge_error_rt(const double R[3][3], const double t[3], const double X[3],
-                          const orc_edge *e, double err[3])
+                          const orc_edge *e, double err[3], int exact_invz)
 {
     double xc[3];
     for (int i = 0; i < 3; i++)
@@ -62,6 +66,13 @@ static void edge_error_rt(const double R[3][3], const double t[3], const double 
         err[0] = e->obs[0] - ((xc[0] / xc[2]) * e->fx + e->cx);
         err[1] = e->obs[1] - ((xc[1] / xc[2]) * e->fy + e->cy);
         err[2] = 0;
+    } else if (exact_invz) {
+        const double invz = 1.0 / xc[2];
+        const double u = xc[0] * invz * e->fx + e->cx;
+        const double v = xc[1] * invz * e->fy + e->cy;
+        err[0] = e->obs[0] - u;
+        err[1] = e->obs[1] - v;
+        err[2] = e->obs[2] - (u - e->bf * invz);
     } else {
         const float invz = (float)(1.0f / xc[2]);
         const float bf = (float)e->bf;
@@ -267,8 +278,8 @@ void orc_ba_numeric_jacobian(const orc_pose *pose, const double *xyz, const orc_
         double Xp[3] = {xyz[0], xyz[1], xyz[2]}, Xm[3] = {xyz[0], xyz[1], xyz[2]};
         Xp[d] += delta;
         Xm[d] -= delta;
-        edge_error_rt(R, pose->t, Xp, e, ep);
-        edge_error_rt(R, pose->t, Xm, e, em);
+        edge_error_rt(R, pose->t, Xp, e, ep, 1);
+        edge_error_rt(R, pose->t, Xm, e, em, 1);
         for (int k = 0; k < 3; k++)
             jp[k][d] = scalar * (ep[k] - em[k]);
     }
@@ -278,9 +289,9 @@ void orc_ba_numeric_jacobian(const orc_pose *pose, const double *xyz, const orc_
         um[d] = -delta;
         double R2[3][3], t2[3];
         oplus_pose(R, pose->t, up, R2, t2);
-        edge_error_rt(R2, t2, xyz, e, ep);
+        edge_error_rt(R2, t2, xyz, e, ep, 1);
         oplus_pose(R, pose->t, um, R2, t2);
-        edge_error_rt(R2, t2, xyz, e, em);
+        edge_error_rt(R2, t2, xyz, e, em, 1);
         for (int k = 0; k < 3; k++)
             jt[k][d] = scalar * (ep[k] - em[k]);
     }

@@ -1,0 +1,183 @@
+"""ctypes binding of liborbg.so (include/orbg.h).
+
+The product path has no CPU fallback: if the HIP library is missing or no GPU is
+visible, the calls below raise.  ``lib()`` loads ``orb_slam2_test_amd/lib/liborbg.so``
+(built in-tree by ``csrc/Makefile`` / ``__graft_entry__.build()``).
+"""
+import ctypes as C
+import os
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "lib", "liborbg.so")
+MAX_LEVELS = 16
+
+ORBG_OK = 0
+ORBG_EIO = -5
+ORBG_ENOMEM = -12
+ORBG_EINVAL = -22
+ORBG_ERANGE = -34
+ORBG_ENOTSUP = -95
+
+RESIZE_SCALAR, RESIZE_SSE2_16_4, RESIZE_SIMD_16_8 = 0, 4, 8
+
+# cv::KeyPoint layout (orbg_keypoint)
+KP_DTYPE = np.dtype([("x", "<f4"), ("y", "<f4"), ("size", "<f4"), ("angle", "<f4"),
+                     ("response", "<f4"), ("octave", "<i4"), ("class_id", "<i4")])
+POSE_DTYPE = np.dtype([("q", "<f8", 4), ("t", "<f8", 3), ("fixed", "<i4"), ("pad", "<i4")])
+EDGE_DTYPE = np.dtype([("point", "<i4"), ("pose", "<i4"), ("stereo", "<i4"), ("robust", "<i4"),
+                       ("active", "<i4"), ("pad", "<i4"), ("obs", "<f8", 3),
+                       ("inv_sigma2", "<f8"), ("fx", "<f8"), ("fy", "<f8"), ("cx", "<f8"),
+                       ("cy", "<f8"), ("bf", "<f8"), ("huber_delta", "<f8")])
+EDGE_OUT_DTYPE = np.dtype([("err", "<f8", 3), ("chi2", "<f8"), ("rho1", "<f8"),
+                           ("jp", "<f8", (3, 3)), ("jt", "<f8", (3, 6)), ("hpl", "<f8", (3, 6))])
+
+
+class Params(C.Structure):
+    _fields_ = [("nfeatures", C.c_int32), ("scale_factor", C.c_float), ("nlevels", C.c_int32),
+                ("ini_th_fast", C.c_int32), ("min_th_fast", C.c_int32),
+                ("resize_mode", C.c_int32), ("gauss_k", C.c_int32 * 7),
+                ("brief_fma", C.c_int32), ("max_batch", C.c_int32)]
+
+
+class Bounds(C.Structure):
+    _fields_ = [("min_x", C.c_float), ("max_x", C.c_float), ("min_y", C.c_float),
+                ("max_y", C.c_float)]
+
+
+class OrbgError(RuntimeError):
+    def __init__(self, code, what):
+        super().__init__("%s failed (%d): %s" % (what, code, last_error()))
+        self.code = code
+
+
+_lib = None
+
+
+def lib():
+    """Load liborbg.so; raises if it is absent (no silent fallback)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise RuntimeError("liborbg.so not built at %s: run __graft_entry__.build() "
+                           "(the product has no CPU fallback)" % LIB_PATH)
+    # One HIP runtime per process: torch ships libamdhip64 / libhsa-runtime64 with the
+    # same SONAMEs as /opt/rocm (libamdhip64.so.7, libhsa-runtime64.so.1).  Importing
+    # torch first makes liborbg's DT_NEEDED entries bind to the copies torch loaded, so
+    # torch (RCCL, tensors) and liborbg share one runtime and one device context.
+    try:
+        import torch  # noqa: F401
+    except ImportError:
+        pass
+    L = C.CDLL(LIB_PATH)
+    vp, P, i32, f32 = C.c_void_p, C.POINTER, C.c_int, C.c_float
+    sz = C.c_size_t
+    sig = {
+        "orbg_params_default": (None, [P(Params)]),
+        "orbg_create": (i32, [i32, P(Params), P(vp)]),
+        "orbg_destroy": (None, [vp]),
+        "orbg_last_error": (C.c_char_p, []),
+        "orbg_abi_version": (i32, []),
+        "orbg_get_scale_tables": (i32, [vp, vp, vp, vp, vp, vp, vp, vp, vp]),
+        "orbg_get_pattern": (i32, [vp]),
+        "orbg_extract": (i32, [vp, vp, i32, i32, sz, vp, vp, i32, P(i32)]),
+        "orbg_get_level": (i32, [vp, i32, i32, vp, sz, P(i32), P(i32)]),
+        "orbg_extract_batch_device": (i32, [vp, vp, i32, i32, i32, sz, sz]),
+        "orbg_batch_outputs": (i32, [vp, P(vp), P(vp), P(vp), P(C.c_int32)]),
+        "orbg_download_frame": (i32, [vp, i32, vp, vp, i32, P(i32)]),
+        "orbg_match_batch_device": (i32, [vp, vp, vp, i32, i32, f32, i32]),
+        "orbg_match_outputs": (i32, [vp, P(vp), P(vp), P(vp), P(C.c_int32)]),
+        "orbg_download_matches": (i32, [vp, i32, vp, vp, i32, vp]),
+        "orbg_sync": (i32, [vp]),
+        "orbg_stream": (vp, [vp]),
+        "orbg_profile_enable": (i32, [vp, i32]),
+        "orbg_profile_read": (i32, [vp, i32, P(C.c_char_p), P(C.c_double), P(C.c_int64)]),
+        "orbg_profile_reset": (i32, [vp]),
+        "orbg_descriptor_distance": (i32, [vp, vp]),
+        "orbg_hamming_knn2": (i32, [vp, vp, i32, vp, i32, vp, vp, vp]),
+        "orbg_search_for_initialization": (i32, [vp, vp, vp, i32, vp, vp, i32, P(Bounds), vp, vp,
+                                                 i32, f32, i32, P(i32)]),
+        "orbg_ba_linearize": (i32, [vp, vp, i32, vp, i32, vp, i32, vp, vp, vp, vp, vp]),
+    }
+    for name, (res, args) in sig.items():
+        fn = getattr(L, name)
+        fn.restype = res
+        fn.argtypes = args
+    _lib = L
+    return L
+
+
+def last_error():
+    if _lib is None:
+        return ""
+    m = _lib.orbg_last_error()
+    return m.decode() if m else ""
+
+
+def check(rc, what):
+    if rc != ORBG_OK:
+        raise OrbgError(rc, what)
+    return rc
+
+
+def ptr(a):
+    """data pointer of a numpy array (or None)."""
+    if a is None:
+        return None
+    return C.c_void_p(a.ctypes.data)
+
+
+def default_params(**kw):
+    p = Params()
+    lib().orbg_params_default(C.byref(p))
+    for k, v in kw.items():
+        if k == "gauss_k":
+            for i in range(7):
+                p.gauss_k[i] = int(v[i])
+        else:
+            setattr(p, k, v)
+    return p
+
+
+class Context:
+    """Owns one orbg_ctx (device buffers + one HIP stream)."""
+
+    def __init__(self, device=0, params=None):
+        self._L = lib()
+        self.params = params if params is not None else default_params()
+        h = C.c_void_p()
+        check(self._L.orbg_create(int(device), C.byref(self.params), C.byref(h)), "orbg_create")
+        self.handle = h
+        self.device = device
+
+    def close(self):
+        if getattr(self, "handle", None):
+            self._L.orbg_destroy(self.handle)
+            self.handle = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    # profiling (HIP events on the context stream)
+    def profile(self, enable=True):
+        check(self._L.orbg_profile_enable(self.handle, 1 if enable else 0), "profile_enable")
+
+    def profile_reset(self):
+        check(self._L.orbg_profile_reset(self.handle), "profile_reset")
+
+    def profile_read(self):
+        n = self._L.orbg_profile_read(self.handle, -1, None, None, None)
+        out = {}
+        for i in range(n):
+            name, ms, cnt = C.c_char_p(), C.c_double(), C.c_int64()
+            self._L.orbg_profile_read(self.handle, i, C.byref(name), C.byref(ms), C.byref(cnt))
+            out[name.value.decode()] = (ms.value, cnt.value)
+        return out
+
+    def sync(self):
+        check(self._L.orbg_sync(self.handle), "orbg_sync")

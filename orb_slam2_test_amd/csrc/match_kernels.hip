@@ -1,0 +1,573 @@
+// match_kernels.hip -- ORBmatcher hot loops for gfx950.
+//
+//   k_knn2_*          brute-force 2-NN over ORBmatcher::DescriptorDistance
+//                     (ORBmatcher.cc:1846-1862; best/second update rule :541-556): one
+//                     query per lane, train descriptors staged through LDS and read as
+//                     broadcasts, 8 x v_bcnt_u32_b32 per pair.
+//   k_init_cands      SearchForInitialization's data-parallel part (ORBmatcher.cc:508-545):
+//                     per level-0 query, the window candidates of F2.GetFeaturesInArea
+//                     (Frame.cc:421-504) with their distances, kept as the K smallest
+//                     (dist, grid-enumeration order) keys.  One wave per query.
+//   k_init_resolve    the order-dependent part (:536-631): vMatchedDistance filter,
+//                     best/second, TH_LOW, ratio, conflict stealing, rotation histogram,
+//                     ComputeThreeMaxima (:1800-1841).  One wave per frame pair walks the
+//                     queries in index order; an exact wave-parallel rescan covers the
+//                     rare query whose K-list is exhausted by the filter.
+#include <hip/hip_runtime.h>
+
+#include <climits>
+
+#include "../../include/orbg.h"
+#include "orbg_internal.h"
+
+#pragma clang fp contract(off)
+
+namespace orbg {
+
+void prof_begin(void *prof, hipStream_t s, const char *n, hipEvent_t *a);
+void prof_end(void *prof, hipStream_t s, const char *n, hipEvent_t a);
+
+#define TH_LOW 50
+#define HISTO_LENGTH 30
+#define KNN_TILE 256
+
+__device__ __forceinline__ int wave_isum(int x)
+{
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) x += __shfl_xor(x, o, 64);
+    return x;
+}
+
+__device__ __forceinline__ int hamming8(const uint32_t a[8], const uint32_t *b)
+{
+    int d = 0;
+#pragma unroll
+    for (int i = 0; i < 8; i++) d += __popc(a[i] ^ b[i]);
+    return d;
+}
+
+// one 256-thread block: queries q[qbase + tid], all nt train descriptors
+__device__ void knn2_block(const uint8_t *__restrict__ q, int nq, const uint8_t *__restrict__ t,
+                           int nt, int32_t *__restrict__ out, int qbase)
+{
+    __shared__ uint32_t tile[KNN_TILE * 8];
+    const int tid = threadIdx.x;
+    const int qi = qbase + tid;
+    uint32_t qd[8];
+    const bool valid = qi < nq;
+    if (valid) {
+        const uint4 *p = (const uint4 *)(q + (size_t)qi * 32);
+        const uint4 a = p[0], b = p[1];
+        qd[0] = a.x; qd[1] = a.y; qd[2] = a.z; qd[3] = a.w;
+        qd[4] = b.x; qd[5] = b.y; qd[6] = b.z; qd[7] = b.w;
+    }
+    int best = INT_MAX, second = INT_MAX, bi = -1;
+    for (int t0 = 0; t0 < nt; t0 += KNN_TILE) {
+        const int nn = min(KNN_TILE, nt - t0);
+        __syncthreads();
+        const uint4 *src = (const uint4 *)(t + (size_t)t0 * 32);
+        for (int i = tid; i < nn * 2; i += 256) ((uint4 *)tile)[i] = src[i];
+        __syncthreads();
+        if (valid) {
+            for (int j = 0; j < nn; j++) {
+                const int d = hamming8(qd, &tile[j * 8]);
+                if (d < best) {
+                    second = best;
+                    best = d;
+                    bi = t0 + j;
+                } else if (d < second) {
+                    second = d;
+                }
+            }
+        }
+    }
+    if (valid) {
+        out[(size_t)qi * 3 + 0] = bi;
+        out[(size_t)qi * 3 + 1] = best;
+        out[(size_t)qi * 3 + 2] = second;
+    }
+}
+
+__global__ __launch_bounds__(256) void k_knn2_single(const uint8_t *q, int nq, const uint8_t *t,
+                                                     int nt, int32_t *out)
+{
+    knn2_block(q, nq, t, nt, out, blockIdx.x * 256);
+}
+
+// batch: queries = F2 (current) keypoints of pair p, train = F1 (previous)
+__global__ __launch_bounds__(256) void k_knn2_pairs(const uint8_t *desc, const int32_t *counts,
+                                                    int fc, const int32_t *f1, const int32_t *f2,
+                                                    int32_t *out)
+{
+    const int p = blockIdx.y;
+    const int a = f1[p], b = f2[p];
+    const int nq = counts[b], nt = counts[a];
+    if ((int)blockIdx.x * 256 >= nq) return;
+    knn2_block(desc + (size_t)b * fc * 32, nq, desc + (size_t)a * fc * 32, nt,
+               out + (size_t)p * fc * 3, blockIdx.x * 256);
+}
+
+// ---------------------------------------------------------------------------
+// SearchForInitialization
+// ---------------------------------------------------------------------------
+struct GridPrm {
+    float min_x, min_y, inv_w, inv_h;
+};
+
+__device__ __forceinline__ GridPrm grid_prm(orbg_bounds b)
+{
+    GridPrm g;
+    g.min_x = b.min_x;
+    g.min_y = b.min_y;
+    // Frame.cc:273-274
+    g.inv_w = (float)ORBG_GRID_COLS / (float)(b.max_x - b.min_x);
+    g.inv_h = (float)ORBG_GRID_ROWS / (float)(b.max_y - b.min_y);
+    return g;
+}
+
+struct Window {
+    int cx0, cx1, cy0, cy1;
+    float x, y, r;
+    bool empty;
+};
+
+// GetFeaturesInArea's cell range (Frame.cc:446-460)
+__device__ __forceinline__ Window make_window(const GridPrm &g, float x, float y, float r)
+{
+    Window w;
+    w.x = x;
+    w.y = y;
+    w.r = r;
+    w.cx0 = max(0, (int)floorf((x - g.min_x - r) * g.inv_w));
+    w.cx1 = min(ORBG_GRID_COLS - 1, (int)ceilf((x - g.min_x + r) * g.inv_w));
+    w.cy0 = max(0, (int)floorf((y - g.min_y - r) * g.inv_h));
+    w.cy1 = min(ORBG_GRID_ROWS - 1, (int)ceilf((y - g.min_y + r) * g.inv_h));
+    w.empty = w.cx0 >= ORBG_GRID_COLS || w.cx1 < 0 || w.cy0 >= ORBG_GRID_ROWS || w.cy1 < 0;
+    return w;
+}
+
+// candidate test for key (kx, ky, octave 0) with grid position (PosInGrid, round()).
+// returns the grid-enumeration order key (cell major: ix, iy) or -1
+__device__ __forceinline__ int cand_order(const GridPrm &g, const Window &w, float kx, float ky)
+{
+    const int px = (int)roundf((kx - g.min_x) * g.inv_w);
+    const int py = (int)roundf((ky - g.min_y) * g.inv_h);
+    if (px < 0 || px >= ORBG_GRID_COLS || py < 0 || py >= ORBG_GRID_ROWS) return -1;
+    if (px < w.cx0 || px > w.cx1 || py < w.cy0 || py > w.cy1) return -1;
+    const float dx = kx - w.x, dy = ky - w.y;
+    if (!(fabsf(dx) < w.r && fabsf(dy) < w.r)) return -1;
+    return px * ORBG_GRID_ROWS + py;
+}
+
+__device__ __forceinline__ unsigned long long wave_min_u64(unsigned long long v)
+{
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+        const unsigned long long u = __shfl_xor(v, o, 64);
+        v = u < v ? u : v;
+    }
+    return v;
+}
+
+// LDS image of F2's level-0 keypoints: x, y, index
+struct F2Key {
+    float x, y;
+    int idx;
+};
+
+#define INIT_QPW 8   // queries per wave in k_init_cands
+#define INIT_F2_CAP 4096
+
+// one 256-thread block: load F2 level-0 keys to LDS, then each wave handles INIT_QPW queries
+__device__ void init_cands_block(const orbg_keypoint *__restrict__ k1,
+                                 const uint8_t *__restrict__ d1, int n1,
+                                 const orbg_keypoint *__restrict__ k2,
+                                 const uint8_t *__restrict__ d2, int n2, orbg_bounds b,
+                                 const float *__restrict__ prev, int prev_stride, int window,
+                                 unsigned long long *__restrict__ topk, int32_t *__restrict__ topn,
+                                 int qbase)
+{
+    __shared__ F2Key f2[INIT_F2_CAP];
+    __shared__ int nf2;
+    const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+    if (tid == 0) nf2 = 0;
+    __syncthreads();
+    for (int i = tid; i < n2; i += 256) {
+        const orbg_keypoint kp = k2[i];
+        if (kp.octave == 0) {
+            const int s = atomicAdd(&nf2, 1);
+            if (s < INIT_F2_CAP) f2[s] = F2Key{kp.x, kp.y, i};
+        }
+    }
+    __syncthreads();
+    const int m = min(nf2, INIT_F2_CAP);
+    const GridPrm g = grid_prm(b);
+    const float r = (float)window;
+    for (int qq = 0; qq < INIT_QPW; qq++) {
+        const int i1 = qbase + wv * INIT_QPW + qq;
+        if (i1 >= n1) break;
+        if (k1[i1].octave > 0) {
+            if (lane == 0) topn[i1] = -1;  // not a query
+            continue;
+        }
+        const Window w = make_window(g, prev[(size_t)i1 * prev_stride],
+                                     prev[(size_t)i1 * prev_stride + 1], r);
+        uint32_t qd[8];
+        {
+            const uint4 *p = (const uint4 *)(d1 + (size_t)i1 * 32);
+            const uint4 a = p[0], c = p[1];
+            qd[0] = a.x; qd[1] = a.y; qd[2] = a.z; qd[3] = a.w;
+            qd[4] = c.x; qd[5] = c.y; qd[6] = c.z; qd[7] = c.w;
+        }
+        unsigned long long loc[ORBG_MATCH_TOPK];
+#pragma unroll
+        for (int k = 0; k < ORBG_MATCH_TOPK; k++) loc[k] = ~0ull;
+        int cnt = 0;
+        if (!w.empty) {
+            for (int j = lane; j < m; j += 64) {
+                const F2Key fk = f2[j];
+                const int ord = cand_order(g, w, fk.x, fk.y);
+                if (ord < 0) continue;
+                const int d = hamming8(qd, (const uint32_t *)(d2 + (size_t)fk.idx * 32));
+                unsigned long long key = ((unsigned long long)d << 32) |
+                                         ((unsigned long long)ord << 20) | (unsigned)fk.idx;
+                cnt++;
+#pragma unroll
+                for (int k = 0; k < ORBG_MATCH_TOPK; k++) {
+                    const unsigned long long lo = key < loc[k] ? key : loc[k];
+                    const unsigned long long hi = key < loc[k] ? loc[k] : key;
+                    loc[k] = lo;
+                    key = hi;
+                }
+            }
+        }
+        cnt = wave_isum(cnt);
+        // merge: K rounds of wave-min over the lanes' sorted heads
+        int head = 0;
+        for (int k = 0; k < ORBG_MATCH_TOPK; k++) {
+            unsigned long long mine = ~0ull;
+#pragma unroll
+            for (int h = 0; h < ORBG_MATCH_TOPK; h++)
+                if (h == head) mine = loc[h];
+            const unsigned long long mn = wave_min_u64(mine);
+            if (mn == ~0ull) {
+                if (lane == 0) topk[(size_t)i1 * ORBG_MATCH_TOPK + k] = ~0ull;
+                continue;
+            }
+            if (mine == mn) head++;  // keys are unique (index in low bits)
+            if (lane == 0) topk[(size_t)i1 * ORBG_MATCH_TOPK + k] = mn;
+        }
+        if (lane == 0) topn[i1] = cnt;
+    }
+}
+
+__global__ __launch_bounds__(256) void k_init_cands_single(
+    const orbg_keypoint *k1, const uint8_t *d1, int n1, const orbg_keypoint *k2,
+    const uint8_t *d2, int n2, orbg_bounds b, const float *prev, int window,
+    unsigned long long *topk, int32_t *topn)
+{
+    init_cands_block(k1, d1, n1, k2, d2, n2, b, prev, 2, window, topk, topn,
+                     blockIdx.x * 4 * INIT_QPW);
+}
+
+// batch: F1 = frame f1[p] (its keypoints are vbPrevMatched), F2 = frame f2[p]
+__global__ __launch_bounds__(256) void k_init_cands_pairs(
+    const orbg_keypoint *kps, const uint8_t *desc, const int32_t *counts, int fc,
+    const int32_t *f1, const int32_t *f2, int w, int h, int window, unsigned long long *topk,
+    int32_t *topn)
+{
+    const int p = blockIdx.y;
+    const int a = f1[p], c = f2[p];
+    const int n1 = counts[a], n2 = counts[c];
+    if ((int)blockIdx.x * 4 * INIT_QPW >= n1) return;
+    const orbg_keypoint *k1 = kps + (size_t)a * fc;
+    orbg_bounds b{0.f, (float)w, 0.f, (float)h};
+    // vbPrevMatched = F1.mvKeysUn[i].pt: read x, y straight out of the keypoint records
+    init_cands_block(k1, desc + (size_t)a * fc * 32, n1, kps + (size_t)c * fc,
+                     desc + (size_t)c * fc * 32, n2, b, (const float *)k1,
+                     (int)(sizeof(orbg_keypoint) / sizeof(float)), window,
+                     topk + (size_t)p * fc * ORBG_MATCH_TOPK, topn + (size_t)p * fc,
+                     blockIdx.x * 4 * INIT_QPW);
+}
+
+// prev stride: the batch path reads x,y out of orbg_keypoint records (stride 7 floats)
+#define RESOLVE_CHUNK 64
+#define RESOLVE_N2_CAP 4608
+
+struct ResolveShared {
+    int mdist[RESOLVE_N2_CAP];
+    int m21[RESOLVE_N2_CAP];
+    int8_t hbin[RESOLVE_N2_CAP];
+    unsigned long long chunk[RESOLVE_CHUNK * ORBG_MATCH_TOPK];
+    int chunkn[RESOLVE_CHUNK];
+    int hsize[HISTO_LENGTH];
+    int nm;
+};
+
+// exact fallback: sequential-scan semantics, wave-parallel
+__device__ void rescan(const orbg_keypoint *k2, const uint8_t *d2, int n2, const GridPrm &g,
+                       const Window &w, const uint32_t qd[8], const int *mdist, int *best,
+                       int *best2, int *bidx)
+{
+    const int lane = threadIdx.x & 63;
+    unsigned long long m1 = ~0ull, m2 = ~0ull;
+    for (int j = lane; j < n2; j += 64) {
+        const orbg_keypoint kp = k2[j];
+        if (kp.octave != 0) continue;
+        const int ord = cand_order(g, w, kp.x, kp.y);
+        if (ord < 0) continue;
+        const int d = hamming8(qd, (const uint32_t *)(d2 + (size_t)j * 32));
+        if (mdist[j] <= d) continue;
+        const unsigned long long key =
+            ((unsigned long long)d << 32) | ((unsigned long long)ord << 20) | (unsigned)j;
+        if (key < m1) {
+            m2 = m1;
+            m1 = key;
+        } else if (key < m2) {
+            m2 = key;
+        }
+    }
+    const unsigned long long a = wave_min_u64(m1);
+    unsigned long long rest = (m1 == a) ? m2 : m1;
+    const unsigned long long b = wave_min_u64(rest);
+    *best = a == ~0ull ? INT_MAX : (int)(a >> 32);
+    *bidx = a == ~0ull ? -1 : (int)(a & 0xFFFFF);
+    *best2 = b == ~0ull ? INT_MAX : (int)(b >> 32);
+}
+
+// one wave (64 threads) per pair
+__device__ void init_resolve_wave(ResolveShared &S, const orbg_keypoint *__restrict__ k1,
+                                  const uint8_t *__restrict__ d1, int n1,
+                                  const orbg_keypoint *__restrict__ k2,
+                                  const uint8_t *__restrict__ d2, int n2, orbg_bounds b,
+                                  const float *prev, int prev_stride, int window, float nnratio,
+                                  int check_ori, const unsigned long long *__restrict__ topk,
+                                  const int32_t *__restrict__ topn, int32_t *__restrict__ m12,
+                                  int32_t *__restrict__ nm_out, float *prev_out)
+{
+    const int lane = threadIdx.x & 63;
+    for (int i = lane; i < n2; i += 64) {
+        S.mdist[i] = INT_MAX;
+        S.m21[i] = -1;
+    }
+    for (int i = lane; i < n1; i += 64) {
+        S.hbin[i] = -1;
+        m12[i] = -1;
+    }
+    if (lane < HISTO_LENGTH) S.hsize[lane] = 0;
+    if (lane == 0) S.nm = 0;
+    __syncthreads();
+    const GridPrm g = grid_prm(b);
+    const float factor = 1.0f / HISTO_LENGTH;
+    int nmatches = 0;
+    for (int c0 = 0; c0 < n1; c0 += RESOLVE_CHUNK) {
+        const int cn = min(RESOLVE_CHUNK, n1 - c0);
+        // prefetch the chunk's K-lists (independent of the sequential state)
+        for (int i = lane; i < cn * ORBG_MATCH_TOPK; i += 64)
+            S.chunk[i] = topk[(size_t)c0 * ORBG_MATCH_TOPK + i];
+        if (lane < cn) S.chunkn[lane] = topn[c0 + lane];
+        __syncthreads();
+        for (int qi = 0; qi < cn; qi++) {
+            const int i1 = c0 + qi;
+            const int total = S.chunkn[qi];
+            if (total <= 0) continue;  // octave > 0 (-1) or empty window (0)
+            // walk the sorted K-list: first two entries that pass the vMatchedDistance filter
+            const int kk = min(total, ORBG_MATCH_TOPK);
+            bool ok = false;
+            unsigned long long e = ~0ull;
+            if (lane < kk) {
+                e = S.chunk[qi * ORBG_MATCH_TOPK + lane];
+                const int d = (int)(e >> 32), i2 = (int)(e & 0xFFFFF);
+                ok = !(S.mdist[i2] <= d);
+            }
+            const unsigned long long bal = __ballot(ok);
+            int bestDist, bestDist2, bestIdx2;
+            const int nvalid = __popcll(bal);
+            if (nvalid >= 2 || total <= ORBG_MATCH_TOPK) {
+                const int l1 = nvalid >= 1 ? __ffsll((long long)bal) - 1 : -1;
+                const unsigned long long rest = nvalid >= 1 ? (bal & (bal - 1)) : 0ull;
+                const int l2 = nvalid >= 2 ? __ffsll((long long)rest) - 1 : -1;
+                const unsigned long long e1 = l1 >= 0 ? __shfl(e, l1, 64) : ~0ull;
+                const unsigned long long e2 = l2 >= 0 ? __shfl(e, l2, 64) : ~0ull;
+                bestDist = l1 >= 0 ? (int)(e1 >> 32) : INT_MAX;
+                bestIdx2 = l1 >= 0 ? (int)(e1 & 0xFFFFF) : -1;
+                bestDist2 = l2 >= 0 ? (int)(e2 >> 32) : INT_MAX;
+            } else {
+                const float px = prev[(size_t)i1 * prev_stride], py = prev[(size_t)i1 * prev_stride + 1];
+                const Window w = make_window(g, px, py, (float)window);
+                uint32_t qd[8];
+                const uint32_t *qp = (const uint32_t *)(d1 + (size_t)i1 * 32);
+#pragma unroll
+                for (int k = 0; k < 8; k++) qd[k] = qp[k];
+                rescan(k2, d2, n2, g, w, qd, S.mdist, &bestDist, &bestDist2, &bestIdx2);
+            }
+            if (bestDist <= TH_LOW && bestDist < (float)bestDist2 * nnratio) {
+                // all lanes hold identical values; lane 0 updates the sequential state
+                if (lane == 0) {
+                    const int old = S.m21[bestIdx2];
+                    if (old >= 0) {
+                        m12[old] = -1;
+                        nmatches--;
+                    }
+                    m12[i1] = bestIdx2;
+                    S.m21[bestIdx2] = i1;
+                    S.mdist[bestIdx2] = bestDist;
+                    nmatches++;
+                    if (check_ori) {
+                        float rot = k1[i1].angle - k2[bestIdx2].angle;
+                        if (rot < 0.0f) rot += 360.0f;
+                        int bin = (int)roundf(rot * factor);
+                        if (bin == HISTO_LENGTH) bin = 0;
+                        S.hbin[i1] = (int8_t)bin;
+                        S.hsize[bin]++;
+                    }
+                }
+                __syncthreads();
+            }
+        }
+        __syncthreads();
+    }
+    nmatches = __shfl(nmatches, 0, 64);
+    if (check_ori) {
+        __syncthreads();
+        __shared__ int ind[3];
+        if (lane == 0) {
+            // ComputeThreeMaxima (:1800-1841)
+            int max1 = 0, max2 = 0, max3 = 0, ind1 = -1, ind2 = -1, ind3 = -1;
+            for (int i = 0; i < HISTO_LENGTH; i++) {
+                const int s = S.hsize[i];
+                if (s > max1) {
+                    max3 = max2; max2 = max1; max1 = s;
+                    ind3 = ind2; ind2 = ind1; ind1 = i;
+                } else if (s > max2) {
+                    max3 = max2; max2 = s;
+                    ind3 = ind2; ind2 = i;
+                } else if (s > max3) {
+                    max3 = s;
+                    ind3 = i;
+                }
+            }
+            if (max2 < 0.1f * (float)max1) {
+                ind2 = -1;
+                ind3 = -1;
+            } else if (max3 < 0.1f * (float)max1) {
+                ind3 = -1;
+            }
+            ind[0] = ind1;
+            ind[1] = ind2;
+            ind[2] = ind3;
+        }
+        __syncthreads();
+        int removed = 0;
+        for (int i = lane; i < n1; i += 64) {
+            const int bn = S.hbin[i];
+            if (bn < 0 || bn == ind[0] || bn == ind[1] || bn == ind[2]) continue;
+            if (m12[i] >= 0) {
+                m12[i] = -1;
+                removed++;
+            }
+        }
+        removed = wave_isum(removed);
+        nmatches -= removed;
+    }
+    __syncthreads();
+    if (prev_out) {
+        for (int i = lane; i < n1; i += 64) {
+            const int j = m12[i];
+            if (j >= 0) {
+                prev_out[2 * i] = k2[j].x;
+                prev_out[2 * i + 1] = k2[j].y;
+            }
+        }
+    }
+    if (lane == 0) *nm_out = nmatches;
+}
+
+__global__ __launch_bounds__(64) void k_init_resolve_single(
+    const orbg_keypoint *k1, const uint8_t *d1, int n1, const orbg_keypoint *k2,
+    const uint8_t *d2, int n2, orbg_bounds b, float *prev, int window, float nnratio,
+    int check_ori, const unsigned long long *topk, const int32_t *topn, int32_t *m12,
+    int32_t *nm)
+{
+    __shared__ ResolveShared S;
+    init_resolve_wave(S, k1, d1, n1, k2, d2, n2, b, prev, 2, window, nnratio, check_ori, topk,
+                      topn, m12, nm, prev);
+}
+
+__global__ __launch_bounds__(64) void k_init_resolve_pairs(
+    const orbg_keypoint *kps, const uint8_t *desc, const int32_t *counts, int fc,
+    const int32_t *f1, const int32_t *f2, int w, int h, int window, float nnratio,
+    int check_ori, const unsigned long long *topk, const int32_t *topn, int32_t *m12,
+    int32_t *nm)
+{
+    __shared__ ResolveShared S;
+    const int p = blockIdx.x;
+    const int a = f1[p], c = f2[p];
+    const orbg_keypoint *k1 = kps + (size_t)a * fc;
+    orbg_bounds b{0.f, (float)w, 0.f, (float)h};
+    init_resolve_wave(S, k1, desc + (size_t)a * fc * 32, counts[a], kps + (size_t)c * fc,
+                      desc + (size_t)c * fc * 32, counts[c], b, (const float *)k1,
+                      (int)(sizeof(orbg_keypoint) / sizeof(float)), window, nnratio, check_ori,
+                      topk + (size_t)p * fc * ORBG_MATCH_TOPK, topn + (size_t)p * fc,
+                      m12 + (size_t)p * fc, nm + p, nullptr);
+}
+
+// ---------------------------------------------------------------------------
+// launchers
+// ---------------------------------------------------------------------------
+#define PL(prof, st, name, ...)                                                            \
+    do {                                                                                   \
+        hipEvent_t a_ = nullptr;                                                           \
+        prof_begin(prof, st, name, &a_);                                                   \
+        __VA_ARGS__;                                                                       \
+        prof_end(prof, st, name, a_);                                                      \
+    } while (0)
+
+int launch_knn2(hipStream_t st, const uint8_t *q, int nq, const uint8_t *t, int nt, int32_t *out,
+                void *prof)
+{
+    PL(prof, st, "knn2",
+       hipLaunchKernelGGL(k_knn2_single, dim3((nq + 255) / 256), dim3(256), 0, st, q, nq, t, nt,
+                          out));
+    return hipGetLastError() == hipSuccess ? ORBG_OK : ORBG_EIO;
+}
+
+int launch_match_pairs(hipStream_t st, const uint8_t *desc, const orbg_keypoint *kps,
+                       const int32_t *counts, int fc, const int32_t *d_f1, const int32_t *d_f2,
+                       int npairs, int w, int h, int window, float nnratio, int check_ori,
+                       int32_t *knn, int32_t *m12, int32_t *nm, uint32_t *topk, int32_t *topk_n,
+                       void *prof)
+{
+    if (fc > RESOLVE_N2_CAP || fc > (1 << 20)) return ORBG_ENOTSUP;
+    PL(prof, st, "knn2",
+       hipLaunchKernelGGL(k_knn2_pairs, dim3((fc + 255) / 256, npairs), dim3(256), 0, st, desc,
+                          counts, fc, d_f1, d_f2, knn));
+    PL(prof, st, "init_cands",
+       hipLaunchKernelGGL(k_init_cands_pairs, dim3((fc + 4 * INIT_QPW - 1) / (4 * INIT_QPW), npairs),
+                          dim3(256), 0, st, kps, desc, counts, fc, d_f1, d_f2, w, h, window,
+                          (unsigned long long *)topk, topk_n));
+    PL(prof, st, "init_resolve",
+       hipLaunchKernelGGL(k_init_resolve_pairs, dim3(npairs), dim3(64), 0, st, kps, desc, counts,
+                          fc, d_f1, d_f2, w, h, window, nnratio, check_ori,
+                          (const unsigned long long *)topk, topk_n, m12, nm));
+    return hipGetLastError() == hipSuccess ? ORBG_OK : ORBG_EIO;
+}
+
+int launch_init_match_single(hipStream_t st, const orbg_keypoint *k1, const uint8_t *d1, int n1,
+                             const orbg_keypoint *k2, const uint8_t *d2, int n2, orbg_bounds b,
+                             float *prev, int32_t *m12, int32_t *nm, int window, float nnratio,
+                             int check_ori, uint32_t *topk, int32_t *topk_n, void *prof)
+{
+    if (n1 > RESOLVE_N2_CAP || n2 > RESOLVE_N2_CAP || n2 > INIT_F2_CAP) return ORBG_ENOTSUP;
+    PL(prof, st, "init_cands",
+       hipLaunchKernelGGL(k_init_cands_single, dim3((n1 + 4 * INIT_QPW - 1) / (4 * INIT_QPW)),
+                          dim3(256), 0, st, k1, d1, n1, k2, d2, n2, b, prev, window,
+                          (unsigned long long *)topk, topk_n));
+    PL(prof, st, "init_resolve",
+       hipLaunchKernelGGL(k_init_resolve_single, dim3(1), dim3(64), 0, st, k1, d1, n1, k2, d2, n2,
+                          b, prev, window, nnratio, check_ori, (const unsigned long long *)topk,
+                          topk_n, m12, nm));
+    return hipGetLastError() == hipSuccess ? ORBG_OK : ORBG_EIO;
+}
+
+}  // namespace orbg

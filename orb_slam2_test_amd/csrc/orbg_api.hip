@@ -1,0 +1,1009 @@
+// orbg_api.hip -- host side of liborbg: the C ABI (include/orbg.h), context, HBM plan
+// and kernel launches.  All reference tables are computed here exactly as the
+// ORBextractor ctor does (ORBextractor.cc:432-521); geometry (levels, cells, quadtree
+// roots) as ComputePyramid / ComputeKeyPointsOctTree / DistributeOctTree do.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstdarg>
+#include <cstdio>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "../../include/orbg.h"
+#include "orbg_internal.h"
+
+#pragma clang fp contract(off)
+
+namespace orbg {
+__global__ void k_resize(const uint8_t *, int64_t, int, int, uint8_t *, int64_t, int, int, int,
+                         const int2 *, const int2 *, int);
+__global__ void k_fast_cells(const OrbgGeom *, const OrbgCell *, const uint8_t *, int64_t, int,
+                             const uint8_t *, int32_t *, uint32_t *);
+__global__ void k_blur(const OrbgGeom *, const int32_t *, const uint8_t *, int64_t, int,
+                       const uint8_t *, uint8_t *);
+__global__ void k_octree(const OrbgGeom *, const int32_t *, const uint32_t *, uint32_t *,
+                         uint32_t *, uint32_t *, uint8_t *, int4 *, uint32_t *, int32_t *,
+                         int32_t *);
+struct OrbgKeypointDev;
+__global__ void k_orient_desc(const OrbgGeom *, const uint8_t *, int64_t, int, const uint8_t *,
+                              const uint8_t *, const uint32_t *, const int32_t *,
+                              OrbgKeypointDev *, uint8_t *, int32_t *);
+// match_kernels.hip
+int launch_match_pairs(hipStream_t st, const uint8_t *desc, const orbg_keypoint *kps,
+                       const int32_t *counts, int frame_cap, const int32_t *d_f1,
+                       const int32_t *d_f2, int npairs, int w, int h, int window, float nnratio,
+                       int check_ori, int32_t *knn, int32_t *m12, int32_t *nm, uint32_t *topk,
+                       int32_t *topk_n, void *prof);
+int launch_knn2(hipStream_t st, const uint8_t *q, int nq, const uint8_t *t, int nt, int32_t *out,
+                void *prof);
+int launch_init_match_single(hipStream_t st, const orbg_keypoint *k1, const uint8_t *d1, int n1,
+                             const orbg_keypoint *k2, const uint8_t *d2, int n2,
+                             orbg_bounds b, float *prev, int32_t *m12, int32_t *nm, int window,
+                             float nnratio, int check_ori, uint32_t *topk, int32_t *topk_n,
+                             void *prof);
+// ba_kernels.hip
+int launch_ba(hipStream_t st, const orbg_pose *poses, int npose, const double *points,
+              int npoint, const orbg_edge *edges, int nedge, orbg_edge_out *eout,
+              double *hpose, double *bpose, double *hpoint, double *bpoint, void *scratch,
+              void *prof);
+size_t ba_scratch_bytes(int npose, int npoint, int nedge);
+}  // namespace orbg
+
+using namespace orbg;
+
+// ---------------------------------------------------------------------------
+// errors
+// ---------------------------------------------------------------------------
+static thread_local std::string g_err;
+static int set_err(int code, const char *fmt, ...)
+{
+    char buf[512];
+    va_list ap;
+    va_start(ap, fmt);
+    vsnprintf(buf, sizeof(buf), fmt, ap);
+    va_end(ap);
+    g_err = buf;
+    return code;
+}
+#define HIPCHK(x)                                                                          \
+    do {                                                                                   \
+        hipError_t e_ = (x);                                                               \
+        if (e_ != hipSuccess)                                                              \
+            return set_err(ORBG_EIO, "%s failed: %s (%s:%d)", #x, hipGetErrorString(e_),   \
+                           __FILE__, __LINE__);                                            \
+    } while (0)
+
+extern "C" const char *orbg_last_error(void) { return g_err.c_str(); }
+extern "C" int orbg_abi_version(void) { return ORBG_ABI_VERSION; }
+
+// ---------------------------------------------------------------------------
+// profiling: HIP events around every launch on the context stream
+// ---------------------------------------------------------------------------
+namespace orbg {
+struct ProfKind {
+    const char *name;
+    double total_ms = 0;
+    int64_t launches = 0;
+};
+struct Prof {
+    bool on = false;
+    std::vector<ProfKind> kinds;
+    struct Pending {
+        int kind;
+        hipEvent_t a, b;
+    };
+    std::vector<Pending> pending;
+    std::vector<hipEvent_t> pool;
+    hipEvent_t get()
+    {
+        if (!pool.empty()) {
+            hipEvent_t e = pool.back();
+            pool.pop_back();
+            return e;
+        }
+        hipEvent_t e;
+        hipEventCreate(&e);
+        return e;
+    }
+    int kind(const char *n)
+    {
+        for (size_t i = 0; i < kinds.size(); i++)
+            if (!strcmp(kinds[i].name, n)) return (int)i;
+        kinds.push_back(ProfKind{n});
+        return (int)kinds.size() - 1;
+    }
+    void begin(hipStream_t s, const char *n, hipEvent_t *a)
+    {
+        if (!on) return;
+        *a = get();
+        hipEventRecord(*a, s);
+        (void)n;
+    }
+    void end(hipStream_t s, const char *n, hipEvent_t a)
+    {
+        if (!on) return;
+        hipEvent_t b = get();
+        hipEventRecord(b, s);
+        pending.push_back(Pending{kind(n), a, b});
+    }
+    void collect()
+    {
+        for (auto &p : pending) {
+            hipEventSynchronize(p.b);
+            float ms = 0;
+            hipEventElapsedTime(&ms, p.a, p.b);
+            kinds[p.kind].total_ms += ms;
+            kinds[p.kind].launches++;
+            pool.push_back(p.a);
+            pool.push_back(p.b);
+        }
+        pending.clear();
+    }
+};
+}  // namespace orbg
+
+#define PROF_LAUNCH(ctxp, name, ...)                                                       \
+    do {                                                                                   \
+        hipEvent_t ev_a_ = nullptr;                                                        \
+        (ctxp)->prof.begin((ctxp)->stream, name, &ev_a_);                                  \
+        __VA_ARGS__;                                                                       \
+        (ctxp)->prof.end((ctxp)->stream, name, ev_a_);                                     \
+    } while (0)
+
+// ---------------------------------------------------------------------------
+// context
+// ---------------------------------------------------------------------------
+struct orbg_ctx {
+    int device = 0;
+    orbg_params p{};
+    hipStream_t stream = nullptr;
+    float scale[16], inv_scale[16], sigma2[16], inv_sigma2[16];
+    int32_t fpl[16], umax[16];
+    // plan
+    int gw = 0, gh = 0, gbatch = 0;
+    OrbgGeom geom{};
+    std::vector<OrbgCell> cells;
+    std::vector<int32_t> tile_base;
+    int total_tiles = 0;
+    // device
+    OrbgGeom *d_geom = nullptr;
+    OrbgCell *d_cells = nullptr;
+    int32_t *d_tile_base = nullptr;
+    int2 *d_rtab = nullptr;
+    uint8_t *d_img = nullptr;
+    size_t img_bytes = 0;
+    uint8_t *d_pyr = nullptr, *d_blur = nullptr;
+    int32_t *d_cell_cnt = nullptr;
+    uint32_t *d_cell_kp = nullptr;
+    uint32_t *d_keys = nullptr, *d_knode = nullptr, *d_act = nullptr;
+    uint8_t *d_qk = nullptr;
+    int4 *d_nodes = nullptr;
+    uint32_t *d_lvl_kp = nullptr;
+    int32_t *d_lvl_cnt = nullptr;
+    orbg_keypoint *d_kps = nullptr;
+    uint8_t *d_desc = nullptr;
+    int32_t *d_counts = nullptr;
+    int32_t *d_err = nullptr;
+    // last batch
+    const uint8_t *last_img = nullptr;
+    int64_t last_fs = 0;
+    int last_pitch = 0;
+    int last_n = 0;
+    // matching (batch)
+    int32_t *d_pairs = nullptr;
+    int pair_cap = 0;
+    int32_t *d_knn = nullptr, *d_m12 = nullptr, *d_nm = nullptr;
+    uint32_t *d_topk = nullptr;
+    int32_t *d_topk_n = nullptr;
+    int last_npairs = 0;
+    // single-pair / host-data scratch
+    void *d_scr = nullptr;
+    size_t scr_bytes = 0;
+    Prof prof;
+};
+
+extern "C" void orbg_params_default(orbg_params *p)
+{
+    memset(p, 0, sizeof(*p));
+    p->nfeatures = 2000;
+    p->scale_factor = 1.2f;
+    p->nlevels = 8;
+    p->ini_th_fast = 20;
+    p->min_th_fast = 7;
+    p->resize_mode = ORBG_RESIZE_SIMD_16_8;
+    const int32_t k[7] = {18, 34, 48, 56, 48, 34, 18};
+    memcpy(p->gauss_k, k, sizeof(k));
+    p->brief_fma = 0;
+    p->max_batch = 1;
+}
+
+static int cv_round_f(float v) { return (int)lrintf(v); }
+static int cv_floor_f(float v)
+{
+    int i = (int)v;
+    return i - (i > v);
+}
+
+// ORBextractor ctor tables, ORBextractor.cc:437-520
+static void make_tables(orbg_ctx *c)
+{
+    const orbg_params &p = c->p;
+    const double sf = (double)p.scale_factor;
+    c->scale[0] = 1.0f;
+    c->sigma2[0] = 1.0f;
+    for (int i = 1; i < p.nlevels; i++) {
+        c->scale[i] = (float)((double)c->scale[i - 1] * sf);
+        c->sigma2[i] = c->scale[i] * c->scale[i];
+    }
+    for (int i = 0; i < p.nlevels; i++) {
+        c->inv_scale[i] = 1.0f / c->scale[i];
+        c->inv_sigma2[i] = 1.0f / c->sigma2[i];
+    }
+    const float factor = (float)(1.0f / sf);
+    float desired = (float)p.nfeatures * (1 - factor) /
+                    (1 - (float)pow((double)factor, (double)p.nlevels));
+    int sum = 0;
+    for (int l = 0; l < p.nlevels - 1; l++) {
+        c->fpl[l] = cv_round_f(desired);
+        sum += c->fpl[l];
+        desired *= factor;
+    }
+    c->fpl[p.nlevels - 1] = std::max(p.nfeatures - sum, 0);
+    const int vmax = cv_floor_f(ORBG_HALF_PATCH * sqrtf(2.f) / 2 + 1);
+    const int vmin = (int)ceilf(ORBG_HALF_PATCH * sqrtf(2.f) / 2);
+    const double hp2 = ORBG_HALF_PATCH * ORBG_HALF_PATCH;
+    int v, v0;
+    for (v = 0; v <= vmax; ++v) c->umax[v] = (int)lrint(sqrt(hp2 - v * v));
+    for (v = ORBG_HALF_PATCH, v0 = 0; v >= vmin; --v) {
+        while (c->umax[v0] == c->umax[v0 + 1]) ++v0;
+        c->umax[v] = v0;
+        ++v0;
+    }
+}
+
+static void free_plan(orbg_ctx *c)
+{
+    void *ptrs[] = {c->d_geom, c->d_cells, c->d_tile_base, c->d_rtab, c->d_pyr, c->d_blur,
+                    c->d_cell_cnt, c->d_cell_kp, c->d_keys, c->d_knode, c->d_act, c->d_qk,
+                    c->d_nodes, c->d_lvl_kp, c->d_lvl_cnt, c->d_kps, c->d_desc, c->d_counts,
+                    c->d_err, c->d_knn, c->d_m12, c->d_nm, c->d_topk, c->d_topk_n, c->d_pairs};
+    for (void *q : ptrs)
+        if (q) hipFree(q);
+    c->d_geom = nullptr;
+    c->d_cells = nullptr;
+    c->d_tile_base = nullptr;
+    c->d_rtab = nullptr;
+    c->d_pyr = c->d_blur = nullptr;
+    c->d_cell_cnt = nullptr;
+    c->d_cell_kp = nullptr;
+    c->d_keys = c->d_knode = c->d_act = nullptr;
+    c->d_qk = nullptr;
+    c->d_nodes = nullptr;
+    c->d_lvl_kp = nullptr;
+    c->d_lvl_cnt = nullptr;
+    c->d_kps = nullptr;
+    c->d_desc = nullptr;
+    c->d_counts = nullptr;
+    c->d_err = nullptr;
+    c->d_knn = c->d_m12 = c->d_nm = nullptr;
+    c->d_topk = nullptr;
+    c->d_topk_n = nullptr;
+    c->d_pairs = nullptr;
+    c->pair_cap = 0;
+    c->gw = c->gh = c->gbatch = 0;
+}
+
+template <typename T>
+static int dalloc(T **p, size_t n)
+{
+    if (n == 0) n = 1;
+    hipError_t e = hipMalloc((void **)p, n * sizeof(T));
+    if (e != hipSuccess)
+        return set_err(ORBG_ENOMEM, "hipMalloc(%zu bytes): %s", n * sizeof(T),
+                       hipGetErrorString(e));
+    return ORBG_OK;
+}
+
+// Build the geometry for an image size and allocate HBM for `batch` frames.
+static int plan(orbg_ctx *c, int w, int h, int batch)
+{
+    if (c->gw == w && c->gh == h && c->gbatch >= batch) return ORBG_OK;
+    const int want_batch = std::max(batch, c->gbatch);
+    free_plan(c);
+    const orbg_params &p = c->p;
+    OrbgGeom G{};
+    G.L = p.nlevels;
+    G.w = w;
+    G.h = h;
+    G.ini_th = std::min(std::max(p.ini_th_fast, 0), 255);
+    G.min_th = std::min(std::max(p.min_th_fast, 0), 255);
+    G.brief_fma = p.brief_fma;
+    for (int i = 0; i < 7; i++) G.gk[i] = p.gauss_k[i];
+    for (int i = 0; i < 16; i++) G.umax[i] = c->umax[i];
+    std::vector<OrbgCell> cells;
+    std::vector<int2> rtab;
+    int cell_cap = 1;
+    int lw[16], lh[16];
+    for (int l = 0; l < G.L; l++) {
+        lw[l] = cv_round_f((float)w * c->inv_scale[l]);
+        lh[l] = cv_round_f((float)h * c->inv_scale[l]);
+        if (l > 0 && lw[l - 1] == 2 * lw[l] && lh[l - 1] == 2 * lh[l])
+            return set_err(ORBG_ENOTSUP, "level %d is an exact 2x downscale: cv::resize would "
+                                         "switch to INTER_AREA (not restated)", l);
+        if (lw[l] - 2 * ORBG_MIN_BORDER >= 4096 || lh[l] - 2 * ORBG_MIN_BORDER >= 4096)
+            return set_err(ORBG_ENOTSUP, "level %d too large (%dx%d)", l, lw[l], lh[l]);
+    }
+    int64_t pyr_off = 0, blur_off = 0;
+    int key_off = 0, node_off = 0, out_off = 0, tiles = 0;
+    std::vector<int32_t> tile_base;
+    for (int l = 0; l < G.L; l++) {
+        OrbgLevel &L = G.lv[l];
+        L.w = lw[l];
+        L.h = lh[l];
+        L.pitch = (lw[l] + 63) & ~63;
+        L.max_bx = lw[l] - ORBG_EDGE_THRESHOLD + 3;
+        L.max_by = lh[l] - ORBG_EDGE_THRESHOLD + 3;
+        const float width = (float)(L.max_bx - ORBG_MIN_BORDER);
+        const float height = (float)(L.max_by - ORBG_MIN_BORDER);
+        L.ncols = (int)(width / ORBG_CELL_W);
+        L.nrows = (int)(height / ORBG_CELL_W);
+        if (L.ncols <= 0 || L.nrows <= 0)
+            return set_err(ORBG_ENOTSUP, "level %d (%dx%d) smaller than one 30-px cell: the "
+                                         "reference divides by zero", l, lw[l], lh[l]);
+        L.wcell = (int)ceilf(width / L.ncols);
+        L.hcell = (int)ceilf(height / L.nrows);
+        L.cell_base = (int)cells.size();
+        for (int i = 0; i < L.nrows; i++) {
+            const float iniY = (float)(ORBG_MIN_BORDER + i * L.hcell);
+            float maxY = iniY + L.hcell + 6;
+            if (iniY >= L.max_by - 3) continue;
+            if (maxY > L.max_by) maxY = (float)L.max_by;
+            for (int j = 0; j < L.ncols; j++) {
+                const float iniX = (float)(ORBG_MIN_BORDER + j * L.wcell);
+                float maxX = iniX + L.wcell + 6;
+                if (iniX >= L.max_bx - 6) continue;
+                if (maxX > L.max_bx) maxX = (float)L.max_bx;
+                OrbgCell cl{};
+                cl.level = (int16_t)l;
+                cl.x0 = (int16_t)(int)iniX;
+                cl.y0 = (int16_t)(int)iniY;
+                cl.w = (int16_t)((int)maxX - (int)iniX);
+                cl.h = (int16_t)((int)maxY - (int)iniY);
+                cl.ci = (int16_t)i;
+                cl.cj = (int16_t)j;
+                if (cl.w > ORBG_MAX_WIN || cl.h > ORBG_MAX_WIN)
+                    return set_err(ORBG_ENOTSUP, "FAST window %dx%d exceeds %d", cl.w, cl.h,
+                                   ORBG_MAX_WIN);
+                const int rw = std::max(cl.w - 6, 0), rh = std::max(cl.h - 6, 0);
+                cell_cap = std::max(cell_cap, ((rw + 1) / 2) * ((rh + 1) / 2));
+                cells.push_back(cl);
+            }
+        }
+        L.ncells = (int)cells.size() - L.cell_base;
+        L.nfeat = c->fpl[l];
+        const int nini = (int)roundf((float)(L.max_bx - ORBG_MIN_BORDER) /
+                                     (L.max_by - ORBG_MIN_BORDER));
+        if (nini <= 0 || nini > 64)
+            return set_err(ORBG_ENOTSUP, "level %d aspect gives %d quadtree roots", l, nini);
+        L.nini = nini;
+        L.hx = (float)(L.max_bx - ORBG_MIN_BORDER) / nini;
+        L.out_cap = std::max(L.nfeat + 3, 4 * nini + 1);
+        if (L.out_cap > ORBG_OCT_ALIVE)
+            return set_err(ORBG_ENOTSUP, "level %d wants %d features (> %d)", l, L.nfeat,
+                           ORBG_OCT_ALIVE - 3);
+        L.out_off = out_off;
+        out_off += L.out_cap;
+        L.node_cap = 20 * (L.nfeat + 3) + 20 * nini + 64;
+        if (L.node_cap > 65535) L.node_cap = 65535;
+        L.node_off = node_off;
+        node_off += L.node_cap;
+        L.scale = c->scale[l];
+        L.patch_size = (int)(ORBG_PATCH * c->scale[l]);
+        if (l > 0) {
+            L.pyr_off = pyr_off;
+            pyr_off += (int64_t)L.pitch * L.h;
+        }
+        L.blur_off = blur_off;
+        blur_off += (int64_t)L.pitch * L.h;
+        tile_base.push_back(tiles);
+        tiles += ((L.w + 63) / 64) * ((L.h + 15) / 16);
+        // resize coefficient tables (cv::resize, INTER_LINEAR)
+        if (l > 0) {
+            const int sw = lw[l - 1], sh = lh[l - 1], dw = lw[l], dh = lh[l];
+            const double inv_sx = (double)dw / sw, inv_sy = (double)dh / sh;
+            const double scale_x = 1. / inv_sx, scale_y = 1. / inv_sy;
+            L.xtab_off = (int)rtab.size();
+            for (int dx = 0; dx < dw; dx++) {
+                float fx = (float)((dx + 0.5) * scale_x - 0.5);
+                int sx = cv_floor_f(fx);
+                fx -= sx;
+                if (sx < 0) {
+                    fx = 0;
+                    sx = 0;
+                }
+                if (sx + 1 >= sw && sx >= sw - 1) {
+                    fx = 0;
+                    sx = sw - 1;
+                }
+                const int a0 = std::min(std::max(cv_round_f((1.f - fx) * 2048), -32768), 32767);
+                const int a1 = std::min(std::max(cv_round_f(fx * 2048), -32768), 32767);
+                rtab.push_back(make_int2(sx, (a0 & 0xFFFF) | (a1 << 16)));
+            }
+            L.ytab_off = (int)rtab.size();
+            for (int dy = 0; dy < dh; dy++) {
+                float fy = (float)((dy + 0.5) * scale_y - 0.5);
+                int sy = cv_floor_f(fy);
+                fy -= sy;
+                const int b0 = std::min(std::max(cv_round_f((1.f - fy) * 2048), -32768), 32767);
+                const int b1 = std::min(std::max(cv_round_f(fy * 2048), -32768), 32767);
+                const int sy0 = sy < 0 ? 0 : (sy < sh ? sy : sh - 1);
+                const int sy1 = sy + 1 < 0 ? 0 : (sy + 1 < sh ? sy + 1 : sh - 1);
+                rtab.push_back(make_int2(sy0 | (sy1 << 16), (b0 & 0xFFFF) | (b1 << 16)));
+            }
+            int be = 0;
+            if (p.resize_mode != ORBG_RESIZE_SCALAR) {
+                const int step = p.resize_mode;
+                int x = 0;
+                for (; x <= dw - 16; x += 16) {
+                }
+                for (; x < dw - step; x += step) {
+                }
+                be = x;
+            }
+            L.bulk_end = be;
+        }
+    }
+    tile_base.push_back(tiles);
+    G.ncells = (int)cells.size();
+    G.cell_cap = cell_cap;
+    for (int l = 0; l < G.L; l++) {
+        G.lv[l].key_off = key_off;
+        G.lv[l].key_cap = G.lv[l].ncells * cell_cap;
+        key_off += G.lv[l].key_cap;
+    }
+    if ((int64_t)key_off * 1 >= (1 << 24))
+        return set_err(ORBG_ENOTSUP, "candidate capacity %d exceeds 2^24", key_off);
+    G.keys_frame = key_off;
+    G.nodes_frame = node_off;
+    G.out_frame = out_off;
+    G.frame_cap = out_off;
+    G.pyr_frame = (pyr_off + 255) & ~(int64_t)255;
+    G.blur_frame = (blur_off + 255) & ~(int64_t)255;
+
+    const size_t B = (size_t)want_batch;
+    int rc;
+    if ((rc = dalloc(&c->d_geom, 1)) || (rc = dalloc(&c->d_cells, cells.size())) ||
+        (rc = dalloc(&c->d_tile_base, tile_base.size())) || (rc = dalloc(&c->d_rtab, rtab.size())) ||
+        (rc = dalloc(&c->d_pyr, B * G.pyr_frame)) || (rc = dalloc(&c->d_blur, B * G.blur_frame)) ||
+        (rc = dalloc(&c->d_cell_cnt, B * G.ncells)) ||
+        (rc = dalloc(&c->d_cell_kp, B * G.ncells * (size_t)cell_cap)) ||
+        (rc = dalloc(&c->d_keys, B * G.keys_frame)) || (rc = dalloc(&c->d_knode, B * G.keys_frame)) ||
+        (rc = dalloc(&c->d_act, 2 * B * G.keys_frame)) || (rc = dalloc(&c->d_qk, B * G.keys_frame)) ||
+        (rc = dalloc(&c->d_nodes, B * G.nodes_frame)) || (rc = dalloc(&c->d_lvl_kp, B * G.out_frame)) ||
+        (rc = dalloc(&c->d_lvl_cnt, B * G.L)) || (rc = dalloc(&c->d_kps, B * G.frame_cap)) ||
+        (rc = dalloc(&c->d_desc, B * G.frame_cap * 32)) || (rc = dalloc(&c->d_counts, B)) ||
+        (rc = dalloc(&c->d_err, 1))) {
+        free_plan(c);
+        return rc;
+    }
+    // resize tables are referenced by offset: fix up pointers through offsets at launch
+    HIPCHK(hipMemcpy(c->d_geom, &G, sizeof(G), hipMemcpyHostToDevice));
+    HIPCHK(hipMemcpy(c->d_cells, cells.data(), cells.size() * sizeof(OrbgCell),
+                     hipMemcpyHostToDevice));
+    HIPCHK(hipMemcpy(c->d_tile_base, tile_base.data(), tile_base.size() * sizeof(int32_t),
+                     hipMemcpyHostToDevice));
+    if (!rtab.empty())
+        HIPCHK(hipMemcpy(c->d_rtab, rtab.data(), rtab.size() * sizeof(int2),
+                         hipMemcpyHostToDevice));
+    HIPCHK(hipMemset(c->d_counts, 0, B * sizeof(int32_t)));
+    c->geom = G;
+    c->cells = cells;
+    c->tile_base = tile_base;
+    c->total_tiles = tiles;
+    c->gw = w;
+    c->gh = h;
+    c->gbatch = want_batch;
+    return ORBG_OK;
+}
+
+extern "C" int orbg_create(int device, const orbg_params *p, orbg_ctx **out)
+{
+    if (!out) return set_err(ORBG_EINVAL, "out is NULL");
+    *out = nullptr;
+    orbg_params prm;
+    if (p)
+        prm = *p;
+    else
+        orbg_params_default(&prm);
+    if (prm.nlevels < 1 || prm.nlevels > ORBG_MAX_LEVELS)
+        return set_err(ORBG_EINVAL, "nlevels %d out of [1, %d]", prm.nlevels, ORBG_MAX_LEVELS);
+    if (!(prm.scale_factor > 1.0f))
+        return set_err(ORBG_EINVAL, "scale_factor must be > 1");
+    if (prm.nfeatures < 0) return set_err(ORBG_EINVAL, "nfeatures < 0");
+    if (prm.resize_mode != ORBG_RESIZE_SCALAR && prm.resize_mode != ORBG_RESIZE_SSE2_16_4 &&
+        prm.resize_mode != ORBG_RESIZE_SIMD_16_8)
+        return set_err(ORBG_EINVAL, "resize_mode %d", prm.resize_mode);
+    int ksum = 0;
+    for (int i = 0; i < 7; i++) ksum += prm.gauss_k[i];
+    if (ksum == 0) {
+        const int32_t k[7] = {18, 34, 48, 56, 48, 34, 18};
+        memcpy(prm.gauss_k, k, sizeof(k));
+    }
+    if (prm.max_batch < 1) prm.max_batch = 1;
+    int ndev = 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0)
+        return set_err(ORBG_EIO, "no HIP device visible (liborbg has no CPU fallback)");
+    if (device < 0 || device >= ndev) return set_err(ORBG_EINVAL, "device %d of %d", device, ndev);
+    HIPCHK(hipSetDevice(device));
+    orbg_ctx *c = new orbg_ctx();
+    c->device = device;
+    c->p = prm;
+    make_tables(c);
+    if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) {
+        delete c;
+        return set_err(ORBG_EIO, "hipStreamCreate failed");
+    }
+    *out = c;
+    return ORBG_OK;
+}
+
+extern "C" void orbg_destroy(orbg_ctx *c)
+{
+    if (!c) return;
+    hipSetDevice(c->device);
+    if (c->stream) hipStreamSynchronize(c->stream);
+    c->prof.collect();
+    for (hipEvent_t e : c->prof.pool) hipEventDestroy(e);
+    free_plan(c);
+    if (c->d_img) hipFree(c->d_img);
+    if (c->d_scr) hipFree(c->d_scr);
+    if (c->stream) hipStreamDestroy(c->stream);
+    delete c;
+}
+
+extern "C" int orbg_get_scale_tables(const orbg_ctx *c, int32_t *nlevels, float *scale_factor,
+                                     float *scale, float *inv_scale, float *sigma2,
+                                     float *inv_sigma2, int32_t *fpl, int32_t *umax)
+{
+    if (!c) return set_err(ORBG_EINVAL, "ctx is NULL");
+    const int L = c->p.nlevels;
+    if (nlevels) *nlevels = L;
+    if (scale_factor) *scale_factor = c->p.scale_factor;
+    for (int i = 0; i < L; i++) {
+        if (scale) scale[i] = c->scale[i];
+        if (inv_scale) inv_scale[i] = c->inv_scale[i];
+        if (sigma2) sigma2[i] = c->sigma2[i];
+        if (inv_sigma2) inv_sigma2[i] = c->inv_sigma2[i];
+        if (fpl) fpl[i] = c->fpl[i];
+    }
+    if (umax)
+        for (int i = 0; i < 16; i++) umax[i] = c->umax[i];
+    return ORBG_OK;
+}
+
+extern "C" int orbg_get_pattern(int32_t out[1024])
+{
+    static const int8_t pat[1024] = {
+#define ORBG_PAIR(a, b, c, d) a, b, c, d,
+#include "orb_pattern.inc"
+#undef ORBG_PAIR
+    };
+    for (int i = 0; i < 1024; i++) out[i] = pat[i];
+    return ORBG_OK;
+}
+
+// ---------------------------------------------------------------------------
+// extraction
+// ---------------------------------------------------------------------------
+static int launch_extract(orbg_ctx *c, const uint8_t *d_imgs, int B, int pitch, int64_t fs)
+{
+    const OrbgGeom &G = c->geom;
+    hipStream_t st = c->stream;
+    HIPCHK(hipMemsetAsync(c->d_err, 0, sizeof(int32_t), st));
+    for (int l = 1; l < G.L; l++) {
+        const OrbgLevel &L = G.lv[l], &P = G.lv[l - 1];
+        const uint8_t *src = (l == 1) ? d_imgs : c->d_pyr + P.pyr_off;
+        const int64_t sfs = (l == 1) ? fs : G.pyr_frame;
+        const int spitch = (l == 1) ? pitch : P.pitch;
+        dim3 grid((L.w + 63) / 64, (L.h + 3) / 4, B);
+        PROF_LAUNCH(c, "resize",
+                    hipLaunchKernelGGL(k_resize, grid, dim3(256), 0, st, src, sfs, spitch, P.w,
+                                       c->d_pyr + L.pyr_off, G.pyr_frame, L.pitch, L.w, L.h,
+                                       c->d_rtab + L.xtab_off, c->d_rtab + L.ytab_off,
+                                       L.bulk_end));
+    }
+    PROF_LAUNCH(c, "fast_cells",
+                hipLaunchKernelGGL(k_fast_cells, dim3(G.ncells, B), dim3(256), 0, st, c->d_geom,
+                                   c->d_cells, d_imgs, fs, pitch, c->d_pyr, c->d_cell_cnt,
+                                   c->d_cell_kp));
+    PROF_LAUNCH(c, "blur",
+                hipLaunchKernelGGL(k_blur, dim3(c->total_tiles, B), dim3(256), 0, st, c->d_geom,
+                                   c->d_tile_base, d_imgs, fs, pitch, c->d_pyr, c->d_blur));
+    PROF_LAUNCH(c, "octree",
+                hipLaunchKernelGGL(k_octree, dim3(G.L, B), dim3(ORBG_OCT_THREADS), 0, st,
+                                   c->d_geom, c->d_cell_cnt, c->d_cell_kp, c->d_keys, c->d_knode,
+                                   c->d_act, c->d_qk, c->d_nodes, c->d_lvl_kp, c->d_lvl_cnt,
+                                   c->d_err));
+    PROF_LAUNCH(c, "orient_desc",
+                hipLaunchKernelGGL(k_orient_desc, dim3((G.frame_cap + 3) / 4, B), dim3(256), 0, st,
+                                   c->d_geom, d_imgs, fs, pitch, c->d_pyr, c->d_blur,
+                                   c->d_lvl_kp, c->d_lvl_cnt, (OrbgKeypointDev *)c->d_kps,
+                                   c->d_desc, c->d_counts));
+    HIPCHK(hipGetLastError());
+    c->last_img = d_imgs;
+    c->last_fs = fs;
+    c->last_pitch = pitch;
+    c->last_n = B;
+    return ORBG_OK;
+}
+
+static int check_err(orbg_ctx *c)
+{
+    int32_t e = 0;
+    HIPCHK(hipMemcpyAsync(&e, c->d_err, sizeof(e), hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(hipStreamSynchronize(c->stream));
+    c->prof.collect();
+    if (e) return set_err(ORBG_ENOTSUP, "quadtree capacity exceeded (flags 0x%x)", e);
+    return ORBG_OK;
+}
+
+extern "C" int orbg_extract_batch_device(orbg_ctx *c, const uint8_t *d_imgs, int nframes, int w,
+                                         int h, size_t step, size_t frame_stride)
+{
+    if (!c || !d_imgs) return set_err(ORBG_EINVAL, "NULL argument");
+    if (nframes <= 0 || w <= 0 || h <= 0 || step < (size_t)w)
+        return set_err(ORBG_EINVAL, "bad batch shape");
+    HIPCHK(hipSetDevice(c->device));
+    int rc = plan(c, w, h, std::max(nframes, c->p.max_batch));
+    if (rc) return rc;
+    return launch_extract(c, d_imgs, nframes, (int)step, (int64_t)frame_stride);
+}
+
+extern "C" int orbg_batch_outputs(orbg_ctx *c, orbg_keypoint **d_kps, uint8_t **d_desc,
+                                  int32_t **d_counts, int32_t *frame_cap)
+{
+    if (!c || !c->gw) return set_err(ORBG_EINVAL, "no batch extracted yet");
+    if (d_kps) *d_kps = c->d_kps;
+    if (d_desc) *d_desc = c->d_desc;
+    if (d_counts) *d_counts = c->d_counts;
+    if (frame_cap) *frame_cap = c->geom.frame_cap;
+    return ORBG_OK;
+}
+
+extern "C" int orbg_download_frame(orbg_ctx *c, int frame, orbg_keypoint *kps, uint8_t *desc,
+                                   int cap, int *n_out)
+{
+    if (!c || !c->gw || frame < 0 || frame >= c->last_n)
+        return set_err(ORBG_EINVAL, "bad frame index");
+    int rc = check_err(c);
+    if (rc) return rc;
+    int32_t n = 0;
+    HIPCHK(hipMemcpy(&n, c->d_counts + frame, sizeof(n), hipMemcpyDeviceToHost));
+    if (n_out) *n_out = n;
+    if (n > cap) return set_err(ORBG_ERANGE, "capacity %d < %d keypoints", cap, n);
+    const size_t fc = (size_t)c->geom.frame_cap;
+    if (kps && n)
+        HIPCHK(hipMemcpy(kps, c->d_kps + frame * fc, n * sizeof(orbg_keypoint),
+                         hipMemcpyDeviceToHost));
+    if (desc && n)
+        HIPCHK(hipMemcpy(desc, c->d_desc + frame * fc * 32, (size_t)n * 32,
+                         hipMemcpyDeviceToHost));
+    return ORBG_OK;
+}
+
+extern "C" int orbg_extract(orbg_ctx *c, const uint8_t *img, int w, int h, size_t step,
+                            orbg_keypoint *kps, uint8_t *desc, int cap, int *n_out)
+{
+    if (!c) return set_err(ORBG_EINVAL, "ctx is NULL");
+    if (w == 0 || h == 0 || img == nullptr) {  // _image.empty(): return (:1333-1334)
+        if (n_out) *n_out = -1;
+        return ORBG_OK;
+    }
+    if (w < 0 || h < 0 || step < (size_t)w) return set_err(ORBG_EINVAL, "bad image shape");
+    HIPCHK(hipSetDevice(c->device));
+    int rc = plan(c, w, h, c->p.max_batch);
+    if (rc) return rc;
+    const size_t bytes = (size_t)w * h;
+    if (c->img_bytes < bytes) {
+        if (c->d_img) hipFree(c->d_img);
+        c->d_img = nullptr;
+        c->img_bytes = 0;
+        if ((rc = dalloc(&c->d_img, bytes))) return rc;
+        c->img_bytes = bytes;
+    }
+    HIPCHK(hipMemcpy2DAsync(c->d_img, w, img, step, w, h, hipMemcpyHostToDevice, c->stream));
+    if ((rc = launch_extract(c, c->d_img, 1, w, (int64_t)bytes))) return rc;
+    return orbg_download_frame(c, 0, kps, desc, cap, n_out);
+}
+
+extern "C" int orbg_get_level(orbg_ctx *c, int frame, int level, uint8_t *dst, size_t dst_step,
+                              int *lw, int *lh)
+{
+    if (!c || !c->gw) return set_err(ORBG_EINVAL, "nothing extracted yet");
+    if (level < 0 || level >= c->geom.L || frame < 0 || frame >= c->last_n)
+        return set_err(ORBG_EINVAL, "bad level/frame");
+    const OrbgLevel &L = c->geom.lv[level];
+    if (lw) *lw = L.w;
+    if (lh) *lh = L.h;
+    if (!dst) return ORBG_OK;
+    if (dst_step < (size_t)L.w) return set_err(ORBG_EINVAL, "dst_step too small");
+    HIPCHK(hipStreamSynchronize(c->stream));
+    if (level == 0)
+        HIPCHK(hipMemcpy2D(dst, dst_step, c->last_img + frame * c->last_fs, c->last_pitch, L.w,
+                           L.h, hipMemcpyDeviceToHost));
+    else
+        HIPCHK(hipMemcpy2D(dst, dst_step, c->d_pyr + frame * c->geom.pyr_frame + L.pyr_off,
+                           L.pitch, L.w, L.h, hipMemcpyDeviceToHost));
+    return ORBG_OK;
+}
+
+extern "C" int orbg_sync(orbg_ctx *c)
+{
+    if (!c) return set_err(ORBG_EINVAL, "ctx is NULL");
+    HIPCHK(hipStreamSynchronize(c->stream));
+    c->prof.collect();
+    return ORBG_OK;
+}
+
+extern "C" void *orbg_stream(orbg_ctx *c) { return c ? (void *)c->stream : nullptr; }
+
+extern "C" int orbg_profile_enable(orbg_ctx *c, int enable)
+{
+    if (!c) return set_err(ORBG_EINVAL, "ctx is NULL");
+    c->prof.on = enable != 0;
+    return ORBG_OK;
+}
+
+extern "C" int orbg_profile_read(orbg_ctx *c, int i, const char **name, double *total_ms,
+                                 int64_t *launches)
+{
+    if (!c) return set_err(ORBG_EINVAL, "ctx is NULL");
+    c->prof.collect();
+    const int n = (int)c->prof.kinds.size();
+    if (i >= 0 && i < n) {
+        if (name) *name = c->prof.kinds[i].name;
+        if (total_ms) *total_ms = c->prof.kinds[i].total_ms;
+        if (launches) *launches = c->prof.kinds[i].launches;
+    }
+    return n;
+}
+
+extern "C" int orbg_profile_reset(orbg_ctx *c)
+{
+    if (!c) return set_err(ORBG_EINVAL, "ctx is NULL");
+    c->prof.collect();
+    for (auto &k : c->prof.kinds) {
+        k.total_ms = 0;
+        k.launches = 0;
+    }
+    return ORBG_OK;
+}
+
+// ---------------------------------------------------------------------------
+// matcher
+// ---------------------------------------------------------------------------
+extern "C" int orbg_descriptor_distance(const uint8_t *a, const uint8_t *b)
+{
+    int d = 0;
+    for (int i = 0; i < 8; i++) {
+        uint32_t x, y;
+        memcpy(&x, a + 4 * i, 4);
+        memcpy(&y, b + 4 * i, 4);
+        d += __builtin_popcount(x ^ y);
+    }
+    return d;
+}
+
+static int scratch(orbg_ctx *c, size_t bytes, void **p)
+{
+    if (c->scr_bytes < bytes) {
+        if (c->d_scr) hipFree(c->d_scr);
+        c->d_scr = nullptr;
+        c->scr_bytes = 0;
+        hipError_t e = hipMalloc(&c->d_scr, bytes);
+        if (e != hipSuccess) return set_err(ORBG_ENOMEM, "scratch %zu bytes", bytes);
+        c->scr_bytes = bytes;
+    }
+    *p = c->d_scr;
+    return ORBG_OK;
+}
+
+static size_t al256(size_t x) { return (x + 255) & ~(size_t)255; }
+
+extern "C" int orbg_match_batch_device(orbg_ctx *c, const int32_t *f1, const int32_t *f2,
+                                       int npairs, int window, float nnratio, int check_ori)
+{
+    if (!c || !c->gw || c->last_n <= 0) return set_err(ORBG_EINVAL, "no batch extracted");
+    if (npairs <= 0 || !f1 || !f2) return set_err(ORBG_EINVAL, "no pairs");
+    for (int i = 0; i < npairs; i++)
+        if (f1[i] < 0 || f1[i] >= c->last_n || f2[i] < 0 || f2[i] >= c->last_n)
+            return set_err(ORBG_EINVAL, "pair %d references a frame outside the batch", i);
+    HIPCHK(hipSetDevice(c->device));
+    const size_t fc = (size_t)c->geom.frame_cap;
+    if (c->pair_cap < npairs) {
+        hipFree(c->d_pairs);
+        hipFree(c->d_knn);
+        hipFree(c->d_m12);
+        hipFree(c->d_nm);
+        hipFree(c->d_topk);
+        hipFree(c->d_topk_n);
+        c->d_pairs = nullptr;
+        c->d_knn = c->d_m12 = c->d_nm = nullptr;
+        c->d_topk = nullptr;
+        c->d_topk_n = nullptr;
+        c->pair_cap = 0;
+        int rc;
+        const size_t P = (size_t)std::max(npairs, c->gbatch);
+        if ((rc = dalloc(&c->d_pairs, 2 * P)) || (rc = dalloc(&c->d_knn, P * fc * 3)) ||
+            (rc = dalloc(&c->d_m12, P * fc)) || (rc = dalloc(&c->d_nm, P)) ||
+            (rc = dalloc(&c->d_topk, P * fc * ORBG_MATCH_TOPK * 2)) ||
+            (rc = dalloc(&c->d_topk_n, P * fc)))
+            return rc;
+        c->pair_cap = (int)P;
+    }
+    HIPCHK(hipMemcpyAsync(c->d_pairs, f1, npairs * sizeof(int32_t), hipMemcpyHostToDevice,
+                          c->stream));
+    HIPCHK(hipMemcpyAsync(c->d_pairs + c->pair_cap, f2, npairs * sizeof(int32_t),
+                          hipMemcpyHostToDevice, c->stream));
+    int rc = launch_match_pairs(c->stream, c->d_desc, c->d_kps, c->d_counts, (int)fc, c->d_pairs,
+                                c->d_pairs + c->pair_cap, npairs, c->geom.w, c->geom.h, window,
+                                nnratio, check_ori, c->d_knn, c->d_m12, c->d_nm, c->d_topk,
+                                c->d_topk_n, &c->prof);
+    if (rc) return rc;
+    c->last_npairs = npairs;
+    return ORBG_OK;
+}
+
+extern "C" int orbg_match_outputs(orbg_ctx *c, int32_t **d_knn, int32_t **d_m12, int32_t **d_nm,
+                                  int32_t *frame_cap)
+{
+    if (!c || !c->last_npairs) return set_err(ORBG_EINVAL, "no match batch yet");
+    if (d_knn) *d_knn = c->d_knn;
+    if (d_m12) *d_m12 = c->d_m12;
+    if (d_nm) *d_nm = c->d_nm;
+    if (frame_cap) *frame_cap = c->geom.frame_cap;
+    return ORBG_OK;
+}
+
+extern "C" int orbg_download_matches(orbg_ctx *c, int pair, int32_t *knn, int32_t *m12, int cap,
+                                     int32_t *nmatches)
+{
+    if (!c || pair < 0 || pair >= c->last_npairs) return set_err(ORBG_EINVAL, "bad pair");
+    HIPCHK(hipStreamSynchronize(c->stream));
+    c->prof.collect();
+    const size_t fc = (size_t)c->geom.frame_cap;
+    const int n = std::min(cap, (int)fc);
+    if (knn) HIPCHK(hipMemcpy(knn, c->d_knn + pair * fc * 3, (size_t)n * 3 * 4, hipMemcpyDeviceToHost));
+    if (m12) HIPCHK(hipMemcpy(m12, c->d_m12 + pair * fc, (size_t)n * 4, hipMemcpyDeviceToHost));
+    if (nmatches) HIPCHK(hipMemcpy(nmatches, c->d_nm + pair, 4, hipMemcpyDeviceToHost));
+    return ORBG_OK;
+}
+
+extern "C" int orbg_hamming_knn2(orbg_ctx *c, const uint8_t *qdesc, int nq, const uint8_t *tdesc,
+                                 int nt, int32_t *best_idx, int32_t *best_dist,
+                                 int32_t *second_dist)
+{
+    if (!c) return set_err(ORBG_EINVAL, "ctx is NULL");
+    if (nq < 0 || nt < 0) return set_err(ORBG_EINVAL, "negative size");
+    if (nq == 0) return ORBG_OK;
+    HIPCHK(hipSetDevice(c->device));
+    const size_t oq = 0, ot = al256((size_t)nq * 32), oo = ot + al256((size_t)std::max(nt, 1) * 32);
+    const size_t bytes = oo + al256((size_t)nq * 12);
+    void *s;
+    int rc = scratch(c, bytes, &s);
+    if (rc) return rc;
+    uint8_t *b = (uint8_t *)s;
+    HIPCHK(hipMemcpyAsync(b + oq, qdesc, (size_t)nq * 32, hipMemcpyHostToDevice, c->stream));
+    if (nt) HIPCHK(hipMemcpyAsync(b + ot, tdesc, (size_t)nt * 32, hipMemcpyHostToDevice, c->stream));
+    if ((rc = launch_knn2(c->stream, b + oq, nq, b + ot, nt, (int32_t *)(b + oo), &c->prof)))
+        return rc;
+    std::vector<int32_t> out((size_t)nq * 3);
+    HIPCHK(hipMemcpyAsync(out.data(), b + oo, (size_t)nq * 12, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(hipStreamSynchronize(c->stream));
+    c->prof.collect();
+    for (int i = 0; i < nq; i++) {
+        if (best_idx) best_idx[i] = out[3 * i];
+        if (best_dist) best_dist[i] = out[3 * i + 1];
+        if (second_dist) second_dist[i] = out[3 * i + 2];
+    }
+    return ORBG_OK;
+}
+
+extern "C" int orbg_search_for_initialization(orbg_ctx *c, const orbg_keypoint *kps1,
+                                              const uint8_t *desc1, int n1,
+                                              const orbg_keypoint *kps2, const uint8_t *desc2,
+                                              int n2, const orbg_bounds *bounds2,
+                                              float *prev_xy, int32_t *matches12, int window,
+                                              float nnratio, int check_ori, int *nmatches)
+{
+    if (!c || !bounds2) return set_err(ORBG_EINVAL, "NULL argument");
+    if (n1 < 0 || n2 < 0) return set_err(ORBG_EINVAL, "negative size");
+    if (nmatches) *nmatches = 0;
+    if (n1 == 0) return ORBG_OK;
+    HIPCHK(hipSetDevice(c->device));
+    const size_t m1 = (size_t)n1, m2 = (size_t)std::max(n2, 1);
+    size_t o = 0;
+    const size_t ok1 = o;
+    o += al256(m1 * sizeof(orbg_keypoint));
+    const size_t od1 = o;
+    o += al256(m1 * 32);
+    const size_t ok2 = o;
+    o += al256(m2 * sizeof(orbg_keypoint));
+    const size_t od2 = o;
+    o += al256(m2 * 32);
+    const size_t opv = o;
+    o += al256(m1 * 8);
+    const size_t om = o;
+    o += al256(m1 * 4 + 4);
+    const size_t otk = o;
+    o += al256(m1 * 8 * ORBG_MATCH_TOPK);
+    const size_t otn = o;
+    o += al256(m1 * 4);
+    void *s;
+    int rc = scratch(c, o, &s);
+    if (rc) return rc;
+    uint8_t *b = (uint8_t *)s;
+    HIPCHK(hipMemcpyAsync(b + ok1, kps1, m1 * sizeof(orbg_keypoint), hipMemcpyHostToDevice, c->stream));
+    HIPCHK(hipMemcpyAsync(b + od1, desc1, m1 * 32, hipMemcpyHostToDevice, c->stream));
+    if (n2) {
+        HIPCHK(hipMemcpyAsync(b + ok2, kps2, (size_t)n2 * sizeof(orbg_keypoint), hipMemcpyHostToDevice, c->stream));
+        HIPCHK(hipMemcpyAsync(b + od2, desc2, (size_t)n2 * 32, hipMemcpyHostToDevice, c->stream));
+    }
+    HIPCHK(hipMemcpyAsync(b + opv, prev_xy, m1 * 8, hipMemcpyHostToDevice, c->stream));
+    rc = launch_init_match_single(c->stream, (const orbg_keypoint *)(b + ok1), b + od1, n1,
+                                  (const orbg_keypoint *)(b + ok2), b + od2, n2, *bounds2,
+                                  (float *)(b + opv), (int32_t *)(b + om),
+                                  (int32_t *)(b + om + m1 * 4), window, nnratio, check_ori,
+                                  (uint32_t *)(b + otk), (int32_t *)(b + otn), &c->prof);
+    if (rc) return rc;
+    int32_t nm = 0;
+    HIPCHK(hipMemcpyAsync(matches12, b + om, m1 * 4, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(hipMemcpyAsync(&nm, b + om + m1 * 4, 4, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(hipMemcpyAsync(prev_xy, b + opv, m1 * 8, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(hipStreamSynchronize(c->stream));
+    c->prof.collect();
+    if (nmatches) *nmatches = nm;
+    return ORBG_OK;
+}
+
+// ---------------------------------------------------------------------------
+// local BA
+// ---------------------------------------------------------------------------
+extern "C" int orbg_ba_linearize(orbg_ctx *c, const orbg_pose *poses, int npose,
+                                 const double *points, int npoint, const orbg_edge *edges,
+                                 int nedge, orbg_edge_out *eout, double *hpose, double *bpose,
+                                 double *hpoint, double *bpoint)
+{
+    if (!c) return set_err(ORBG_EINVAL, "ctx is NULL");
+    if (npose < 0 || npoint < 0 || nedge < 0) return set_err(ORBG_EINVAL, "negative size");
+    for (int i = 0; i < nedge; i++)
+        if (edges[i].pose < 0 || edges[i].pose >= npose || edges[i].point < 0 ||
+            edges[i].point >= npoint)
+            return set_err(ORBG_EINVAL, "edge %d references a missing vertex", i);
+    HIPCHK(hipSetDevice(c->device));
+    const size_t sb = ba_scratch_bytes(npose, npoint, nedge);
+    void *s;
+    int rc = scratch(c, sb, &s);
+    if (rc) return rc;
+    rc = launch_ba(c->stream, poses, npose, points, npoint, edges, nedge, eout, hpose, bpose,
+                   hpoint, bpoint, s, &c->prof);
+    if (rc) return rc;
+    HIPCHK(hipStreamSynchronize(c->stream));
+    c->prof.collect();
+    return ORBG_OK;
+}
+
+// profiling hook used by the other translation units
+namespace orbg {
+void prof_begin(void *prof, hipStream_t s, const char *n, hipEvent_t *a)
+{
+    ((Prof *)prof)->begin(s, n, a);
+}
+void prof_end(void *prof, hipStream_t s, const char *n, hipEvent_t a)
+{
+    ((Prof *)prof)->end(s, n, a);
+}
+}  // namespace orbg

@@ -1,0 +1,81 @@
+// orbg_internal.h -- shared host/device definitions of liborbg (MI355X, gfx950).
+//
+// HBM layout for a batch of B frames (all per-frame regions contiguous, frame-major):
+//   input images ........ caller's buffer (level 0 of the pyramid, pitch = caller's step)
+//   pyramid levels 1..L-1  d_pyr   [B][pyr_frame_bytes], level l at lv[l].off, pitch lv[l].pitch
+//   blurred levels 0..L-1  d_blur  [B][blur_frame_bytes]
+//   FAST cell slots ...... d_cell_cnt [B][ncells], d_cell_kp [B][ncells][cell_cap] (packed u32)
+//   octree scratch ....... d_keys/d_keynode [B][keys_frame]; d_nodes [B][nodes_frame] (int4)
+//   octree output ........ d_lvl_kp [B][out_frame] (packed u32), d_lvl_cnt [B][L]
+//   final outputs ........ d_kps [B][frame_cap] orbg_keypoint, d_desc [B][frame_cap][32],
+//                          d_counts [B]
+// Packed candidate/keypoint word: x | y << 12 | score << 24 (coordinates relative to
+// minBorder = EDGE_THRESHOLD-3 = 16, exactly the vToDistributeKeys coordinates).
+#pragma once
+
+#include <stdint.h>
+
+#define ORBG_EDGE_THRESHOLD 19
+#define ORBG_MIN_BORDER 16
+#define ORBG_HALF_PATCH 15
+#define ORBG_PATCH 31
+#define ORBG_CELL_W 30.0f
+#define ORBG_MAX_WIN 72          // largest FAST window edge (wCell+6 < 66)
+#define ORBG_OCT_ALIVE 2048      // max live quadtree nodes per (frame, level)
+#define ORBG_OCT_THREADS 256
+#define ORBG_GRID_COLS 64        // Frame.h:38
+#define ORBG_GRID_ROWS 48        // Frame.h:37
+#define ORBG_MATCH_TOPK 8
+
+struct OrbgLevel {
+    int32_t w, h, pitch;
+    int32_t max_bx, max_by;       // maxBorderX/Y = w-16 / h-16
+    int32_t ncols, nrows, wcell, hcell;
+    int32_t cell_base, ncells;
+    int32_t nfeat;                // mnFeaturesPerLevel
+    int32_t nini;                 // quadtree roots
+    float hx;                     // root width (float, DistributeOctTree :680)
+    int32_t key_off, key_cap;     // candidate scratch (u32 words) within a frame
+    int32_t node_off, node_cap;   // int4 node records within a frame
+    int32_t out_off, out_cap;     // octree output words within a frame
+    int32_t bulk_end;             // resize: first column using the scalar vertical pass
+    int32_t xtab_off, ytab_off;   // resize coefficient tables (int2 per column / row)
+    int64_t pyr_off;              // byte offset of the level in a frame's pyramid (l >= 1)
+    int64_t blur_off;             // byte offset in a frame's blurred pyramid
+    float scale;                  // mvScaleFactor[l]
+    int32_t patch_size;           // int(PATCH_SIZE * scale)
+};
+
+struct OrbgGeom {
+    int32_t L;
+    int32_t w, h;
+    int32_t ncells;               // all levels
+    int32_t cell_cap;             // max packed candidates per cell
+    int32_t keys_frame;           // u32 words per frame of candidate scratch
+    int32_t nodes_frame;          // int4 per frame
+    int32_t out_frame;            // octree output words per frame
+    int32_t frame_cap;            // max keypoints per frame (final)
+    int32_t ini_th, min_th;
+    int32_t brief_fma;
+    int32_t gk[7];
+    int64_t pyr_frame;            // bytes per frame of d_pyr
+    int64_t blur_frame;
+    int32_t umax[16];
+    OrbgLevel lv[16];
+};
+
+// cell table entry
+struct OrbgCell {
+    int16_t level, pad;
+    int16_t x0, y0;   // window top-left (level coords)
+    int16_t w, h;     // window size
+    int16_t ci, cj;   // cell row / col (for pt += j*wCell, i*hCell)
+};
+
+static inline __host__ __device__ uint32_t orbg_pack(int x, int y, int s)
+{
+    return (uint32_t)x | ((uint32_t)y << 12) | ((uint32_t)s << 24);
+}
+static inline __host__ __device__ int orbg_px(uint32_t v) { return (int)(v & 0xFFFu); }
+static inline __host__ __device__ int orbg_py(uint32_t v) { return (int)((v >> 12) & 0xFFFu); }
+static inline __host__ __device__ int orbg_ps(uint32_t v) { return (int)(v >> 24); }

@@ -85,3 +85,97 @@ def constant(h, w, value=128):
 def pure_noise(h, w, seed=DEFAULT_SEED):
     rng = np.random.Generator(np.random.PCG64(seed + 7))
     return rng.integers(0, 256, size=(h, w), dtype=np.uint8)
+
+
+# ---------------------------------------------------------------------------
+# Local-BA windows (SURVEY.md 8d "BA"): KITTI00 intrinsics (Stereo/KITTI00-02.yaml)
+# ---------------------------------------------------------------------------
+KITTI_FX = 718.856
+KITTI_FY = 718.856
+KITTI_CX = 607.1928
+KITTI_CY = 185.2157
+KITTI_BF = 386.1448
+
+
+def _quat_from_axis_angle(axis, ang):
+    axis = axis / np.linalg.norm(axis)
+    s = np.sin(ang / 2)
+    q = np.array([axis[0] * s, axis[1] * s, axis[2] * s, np.cos(ang / 2)])
+    if q[3] < 0:
+        q = -q
+    return q
+
+
+def _rot(q):
+    x, y, z, w = q
+    return np.array([[1 - 2 * (y * y + z * z), 2 * (x * y - z * w), 2 * (x * z + y * w)],
+                     [2 * (x * y + z * w), 1 - 2 * (x * x + z * z), 2 * (y * z - x * w)],
+                     [2 * (x * z - y * w), 2 * (y * z + x * w), 1 - 2 * (x * x + y * y)]])
+
+
+def ba_window(n_local=10, n_fixed=10, n_points=6000, obs_per_point=4.5, stereo_frac=0.6,
+              outlier_frac=0.1, seed=DEFAULT_SEED, world_offset=500.0, robust=True,
+              scale_factor=1.2, nlevels=8):
+    """A synthetic LocalBundleAdjustment window.  Returns (poses, points, edges) as
+    structured arrays with the dtypes of orb_slam2_test_amd._lib (pose/edge records)."""
+    from ._lib import EDGE_DTYPE, POSE_DTYPE
+    rng = np.random.Generator(np.random.PCG64(seed + 99))
+    npose = n_local + n_fixed
+    origin = rng.uniform(-world_offset, world_offset, size=3)
+    poses = np.zeros(npose, POSE_DTYPE)
+    cams = []
+    for i in range(npose):
+        # cameras driving forward along +z in world, small rotations
+        q = _quat_from_axis_angle(rng.normal(size=3), rng.uniform(0, 0.15))
+        Rcw = _rot(q)
+        center = origin + np.array([rng.normal(0, 1.0), rng.normal(0, 0.2), 1.5 * i])
+        t = -Rcw @ center
+        poses[i]["q"] = q
+        poses[i]["t"] = t
+        poses[i]["fixed"] = 1 if i >= n_local else 0
+        cams.append((Rcw, t))
+    # points in front of the cameras at depth 5-60 m
+    pts = np.zeros((n_points, 3))
+    for j in range(n_points):
+        Rcw, t = cams[rng.integers(0, npose)]
+        depth = rng.uniform(5, 60)
+        u = rng.uniform(0, 1241)
+        v = rng.uniform(0, 376)
+        xc = np.array([(u - KITTI_CX) / KITTI_FX * depth, (v - KITTI_CY) / KITTI_FY * depth, depth])
+        pts[j] = Rcw.T @ (xc - t)
+    inv_sigma2 = [1.0 / float(np.float32(np.float32(scale_factor) ** (2 * l))) for l in range(nlevels)]
+    edges = []
+    for j in range(n_points):
+        k = max(1, int(rng.poisson(obs_per_point - 1)) + 1)
+        kfs = rng.choice(npose, size=min(k, npose), replace=False)
+        for i in kfs:
+            Rcw, t = cams[i]
+            xc = Rcw @ pts[j] + t
+            if xc[2] <= 0.1:
+                continue
+            e = np.zeros((), EDGE_DTYPE)
+            e["point"] = j
+            e["pose"] = i
+            octave = int(rng.integers(0, nlevels))
+            e["inv_sigma2"] = float(np.float32(inv_sigma2[octave]))
+            e["fx"], e["fy"], e["cx"], e["cy"], e["bf"] = (KITTI_FX, KITTI_FY, KITTI_CX, KITTI_CY,
+                                                           KITTI_BF)
+            u = KITTI_FX * xc[0] / xc[2] + KITTI_CX
+            v = KITTI_FY * xc[1] / xc[2] + KITTI_CY
+            noise = rng.normal(0, 1.0, size=3)
+            if rng.random() < outlier_frac:
+                noise *= 25
+            stereo = rng.random() < stereo_frac
+            # observations are float keypoint coordinates (cv::KeyPoint pt, f32 -> double)
+            e["obs"][0] = float(np.float32(u + noise[0]))
+            e["obs"][1] = float(np.float32(v + noise[1]))
+            if stereo:
+                e["stereo"] = 1
+                e["obs"][2] = float(np.float32(u - KITTI_BF / xc[2] + noise[2]))
+                e["huber_delta"] = float(np.float32(np.sqrt(7.815)))
+            else:
+                e["huber_delta"] = float(np.float32(np.sqrt(5.991)))
+            e["robust"] = 1 if robust else 0
+            e["active"] = 1
+            edges.append(e)
+    return poses, pts, np.array(edges, dtype=EDGE_DTYPE)

@@ -1,0 +1,173 @@
+#!/usr/bin/env python3
+"""Stage-by-stage GPU-vs-oracle diagnostic (developer tool, run under gpurun).
+
+Prints mismatch statistics for the pyramid, keypoints, descriptors, matcher and BA
+and a quick per-kernel timing of the batched path.  Uses the oracle only as checker.
+"""
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+from oracle import pyoracle as O  # noqa: E402
+from orb_slam2_test_amd import synthetic as S  # noqa: E402
+from orb_slam2_test_amd import ORBextractor, ORBmatcher, Frame, linearize_local_ba  # noqa: E402
+
+
+def cmp_kps(a, b, tag):
+    if len(a) != len(b):
+        print(f"  [{tag}] COUNT MISMATCH gpu={len(a)} oracle={len(b)}")
+    n = min(len(a), len(b))
+    bad = 0
+    for f in ("x", "y", "size", "angle", "response", "octave", "class_id"):
+        d = np.nonzero(a[f][:n] != b[f][:n])[0]
+        if len(d):
+            bad += 1
+            i = d[0]
+            print(f"  [{tag}] field {f}: {len(d)} mismatches, first at {i}: gpu={a[f][i]} or={b[f][i]}")
+    return bad == 0 and len(a) == len(b)
+
+
+def check_extract(w, h, nfeat, nlevels, img, tag):
+    print(f"== extract {tag} {w}x{h} nfeat={nfeat} L={nlevels}")
+    p = O.params(nfeatures=nfeat, nlevels=nlevels)
+    ref = O.extract(p, img, with_pyramid=True)
+    ext = ORBextractor(nfeat, 1.2, nlevels, 20, 7)
+    t = time.time()
+    kps, desc = ext(img)
+    print(f"  gpu single-frame call {1e3*(time.time()-t):.1f} ms (includes first-call plan)")
+    ok = True
+    for l in range(nlevels):
+        g = ext.mvImagePyramid[l]
+        r = ref["pyramid"][l]
+        if g.shape != r.shape or not np.array_equal(g, r):
+            nd = (g != r).sum() if g.shape == r.shape else -1
+            print(f"  level {l} pyramid mismatch: {nd} px")
+            if nd > 0:
+                ys, xs = np.nonzero(g != r)
+                print(f"    first ({ys[0]},{xs[0]}) gpu={g[ys[0],xs[0]]} or={r[ys[0],xs[0]]}")
+            ok = False
+    lc_g = np.bincount(kps["octave"], minlength=nlevels) if len(kps) else np.zeros(nlevels, int)
+    print(f"  per-level gpu={list(lc_g)} oracle={list(ref['level_counts'])}")
+    ok &= cmp_kps(kps, ref["kps"], "kps")
+    if len(desc) == len(ref["desc"]):
+        nd = (desc != ref["desc"]).any(axis=1).sum()
+        if nd:
+            print(f"  descriptors: {nd} rows differ")
+            ok = False
+    print("  PASS" if ok else "  FAIL")
+    return ok, ext, kps, desc, ref
+
+
+def main():
+    allok = True
+    seq = S.sequence(4, 376, 1241)
+    ok, ext, kps, desc, ref = check_extract(1241, 376, 2000, 8, seq[0], "C2")
+    allok &= ok
+    tum = S.frame(480, 640, seed=5)
+    allok &= check_extract(640, 480, 1000, 8, tum, "TUM")[0]
+    allok &= check_extract(1241, 376, 4000, 8, seq[1], "ini4000")[0]
+    allok &= check_extract(1241, 376, 2000, 8, S.pure_noise(376, 1241), "noise")[0]
+    allok &= check_extract(1241, 376, 2000, 8, S.constant(376, 1241), "const")[0]
+
+    # matcher, host-data API
+    print("== matcher")
+    p = O.params()
+    a = O.extract(p, seq[0])
+    b = O.extract(p, seq[1])
+    m = ORBmatcher(0.9, True)
+    bi, bd, sd = m.hamming_knn2(b["desc"], a["desc"])
+    rbi, rbd, rsd = O.knn2(b["desc"], a["desc"])
+    kok = np.array_equal(bi, rbi) and np.array_equal(bd, rbd) and np.array_equal(sd, rsd)
+    print("  knn2", "PASS" if kok else f"FAIL {(bi != rbi).sum()} {(bd != rbd).sum()} {(sd != rsd).sum()}")
+    allok &= kok
+    prev = np.ascontiguousarray(np.stack([a["kps"]["x"], a["kps"]["y"]], 1).astype(np.float32))
+    F1 = Frame.from_extraction(a["kps"], a["desc"], 1241, 376)
+    F2 = Frame.from_extraction(b["kps"], b["desc"], 1241, 376)
+    gp = prev.copy()
+    nm, m12 = m.SearchForInitialization(F1, F2, gp, 100)
+    rn, rm12, rprev = O.search_for_initialization(a["kps"], a["desc"], b["kps"], b["desc"], prev,
+                                                  (0, 1241, 0, 376), 100, 0.9, True)
+    sok = nm == rn and np.array_equal(m12, rm12) and np.array_equal(gp, rprev)
+    print(f"  SearchForInitialization gpu={nm} oracle={rn}", "PASS" if sok else
+          f"FAIL m12 diff {(m12 != rm12).sum()}")
+    allok &= sok
+
+    # BA
+    print("== BA")
+    poses, pts, edges = S.ba_window(n_points=2000)
+    eo, hp, bp, hq, bq = linearize_local_ba(poses, pts, edges)
+    reo, rhp, rbp, rhq, rbq = O.ba_linearize(poses, pts, edges)
+
+    def rel(a, b):
+        return np.abs(a - b).max() / max(np.abs(b).max(), 1e-300)
+    errs = {"err": rel(eo["err"], reo["err"]), "jp": rel(eo["jp"], reo["jp"]),
+            "jt": rel(eo["jt"], reo["jt"]), "hpose": rel(hp, rhp), "bpose": rel(bp, rbp),
+            "hpoint": rel(hq, rhq), "bpoint": rel(bq, rbq), "hpl": rel(eo["hpl"], reo["hpl"])}
+    rerr = np.abs(eo["err"] - reo["err"]) / np.maximum(np.abs(reo["err"]), 1e-3)
+    print("  max rel:", {k: f"{v:.2e}" for k, v in errs.items()}, f"per-residual {rerr.max():.2e}")
+    bok = all(v < 1e-5 for v in errs.values())
+    print("  PASS" if bok else "  FAIL")
+    allok &= bok
+
+    # batched device path
+    print("== batch")
+    import torch
+    B = 64
+    frames = S.sequence(B, 376, 1241, seed=11)
+    d = torch.from_numpy(frames).cuda()
+    bext = ORBextractor(2000, 1.2, 8, 20, 7, max_batch=B)
+    bext.extract_batch_device(d.data_ptr(), B, 1241, 376)
+    f1 = np.arange(B) - 1
+    f1[0] = B - 1
+    f2 = np.arange(B)
+    bext.match_batch_device(f1, f2, 100, 0.9, True)
+    bext.ctx.sync()
+    bad = 0
+    for f in (0, 1, 17, B - 1):
+        k, dsc = bext.download_frame(f)
+        r = O.extract(p, frames[f])
+        same = len(k) == len(r["kps"]) and np.array_equal(k, r["kps"]) and np.array_equal(dsc, r["desc"])
+        bad += not same
+    print("  batch extract parity on 4 frames:", "PASS" if bad == 0 else f"FAIL ({bad})")
+    allok &= bad == 0
+    # batch match parity on pair 1 (frames 0 -> 1)
+    k0, d0 = bext.download_frame(0)
+    k1, d1 = bext.download_frame(1)
+    knn, m12b, nmb = bext.download_matches(1, len(k1))
+    rbi, rbd, rsd = O.knn2(d1, d0)
+    prev0 = np.ascontiguousarray(np.stack([k0["x"], k0["y"]], 1).astype(np.float32))
+    rn, rm12, _ = O.search_for_initialization(k0, d0, k1, d1, prev0, (0, 1241, 0, 376), 100, 0.9, True)
+    mok = np.array_equal(knn[:, 0], rbi) and np.array_equal(knn[:, 1], rbd) and nmb == rn and \
+        np.array_equal(m12b[:len(k0)], rm12) if len(k0) <= len(k1) else nmb == rn
+    print(f"  batch match parity pair 1: nm gpu={nmb} oracle={rn}", "PASS" if mok else "FAIL")
+    allok &= bool(mok)
+
+    # timing
+    bext.ctx.profile(True)
+    torch.cuda.synchronize()
+    for it in range(3):
+        bext.extract_batch_device(d.data_ptr(), B, 1241, 376)
+        bext.match_batch_device(f1, f2, 100, 0.9, True)
+    bext.ctx.sync()
+    bext.ctx.profile_reset()
+    t = time.time()
+    iters = 5
+    for it in range(iters):
+        bext.extract_batch_device(d.data_ptr(), B, 1241, 376)
+        bext.match_batch_device(f1, f2, 100, 0.9, True)
+    bext.ctx.sync()
+    dt = time.time() - t
+    print(f"  {B} frames x {iters}: {dt/iters*1e3:.2f} ms/step  {B*iters/dt:.0f} frames/s (profiled)")
+    for k, (ms, n) in bext.ctx.profile_read().items():
+        print(f"    {k:14s} {ms/iters:8.3f} ms/step  ({n} launches)")
+    print("ALL PASS" if allok else "SOME FAILED")
+    return 0 if allok else 1
+
+
+if __name__ == "__main__":
+    sys.exit(main())
