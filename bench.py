@@ -1,0 +1,214 @@
+#!/usr/bin/env python3
+"""bench.py -- frames/s of ORB extract + match at 1241x376, 2000 features, 8 levels.
+
+A step = one pass of the hot path over one batch of B synthetic frames per GPU, resident
+in HBM before the timed region:
+  ORBextractor::operator() on every frame (pyramid, FAST cells, quadtree, blur,
+  IC_Angle + rBRIEF) and, for every frame t, the matcher between t-1 and t
+  (all-pairs Hamming knn2 + SearchForInitialization(window 100, nnratio 0.9, checkOri)).
+Multi-GPU (torch.distributed.run, one process per GPU): frames are sharded (each rank
+owns its own block of the sequence, weak scaling); the only collective is an RCCL
+all_gather of the per-frame trajectory summary (keypoint and match counts) per step.
+
+Prints ONE JSON line on rank 0 (contract in the task statement):
+  value = all ranks' frames / max-over-ranks wall time of K steps,
+  roofline = dominant kernel, algorithmic bytes / HIP-event duration (on the stream the
+             kernels run on) vs 8 TB/s HBM,
+  cpu_baseline = the oracle (C restatement, "port") on a bounded sample on host cores.
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+METRIC = "frames/sec ORB extract+match, 1241×376 2000feat 8lvl, 1/2/4/8 GPU"
+W, H, NFEAT, NLEV = 1241, 376, 2000, 8
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
+# SURVEY.md 8d algorithmic bytes per unit
+PYR_BYTES = 1444097          # all 8 levels at 1241x376
+FRAME_ALGO_BYTES = 2701578   # extract 2,533,578 + match 168,000
+
+
+def kernel_algo_bytes(name, B, npairs, ncand, nkp, launches_per_step):
+    """Algorithmic bytes of one launch of `name` (see DESIGN.md 'Kernels')."""
+    lv = level_sizes()
+    if name == "resize":
+        tot = B * sum(lv[l - 1][0] * lv[l - 1][1] + lv[l][0] * lv[l][1] for l in range(1, NLEV))
+    elif name == "fast_cells":
+        tot = B * PYR_BYTES + 4 * ncand
+    elif name == "blur":
+        tot = 2 * B * PYR_BYTES
+    elif name == "octree":
+        tot = 4 * ncand + 4 * nkp
+    elif name == "orient_desc":
+        tot = nkp * (749 + 512 + 4 + 28 + 32)
+    elif name == "knn2":
+        kp = nkp / max(B, 1)
+        tot = npairs * (2 * kp * 32 + kp * 12)
+    elif name == "init_cands":
+        kp = nkp / max(B, 1)
+        tot = npairs * (kp * 28 + kp * 32 + kp * 64)
+    elif name == "init_resolve":
+        kp = nkp / max(B, 1)
+        tot = npairs * (kp * 64 + kp * 4)
+    else:
+        return None
+    return tot / max(launches_per_step, 1)
+
+
+def level_sizes():
+    sizes, s = [], np.float32(1.0)
+    for l in range(NLEV):
+        inv = np.float32(1.0) / s
+        sizes.append((int(np.rint(np.float32(W) * inv)), int(np.rint(np.float32(H) * inv))))
+        s = np.float32(np.float64(s) * np.float64(np.float32(1.2)))
+    return sizes
+
+
+def cpu_baseline(frames, threads, nframes):
+    from oracle import pyoracle as O
+    p = O.params(nfeatures=NFEAT, nlevels=NLEV)
+    idx = np.arange(nframes) % len(frames)
+    sample = np.ascontiguousarray(frames[idx])
+    t0 = time.perf_counter()
+    O.frames_batch(p, sample, nthreads=threads, window=100, nnratio=0.9)
+    dt = time.perf_counter() - t0
+    return {"value": round(nframes / dt, 3), "unit": "frames/s", "cores": threads,
+            "kind": "port",
+            "sample": ("%d synthetic 1241x376 frames (extract 2000 feat/8 lvl + knn2 + "
+                       "SearchForInitialization vs t-1), oracle/ C restatement -O3, %d pthreads, "
+                       "%.1f s wall" % (nframes, threads, dt))}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--batch", type=int, default=256, help="frames per GPU per step")
+    ap.add_argument("--cpu-threads", type=int, default=int(os.environ.get("OMP_NUM_THREADS", "16")))
+    ap.add_argument("--cpu-frames", type=int, default=0, help="0: 24 x threads")
+    ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--no-kernel-timing", action="store_true")
+    args = ap.parse_args()
+
+    import torch
+    import torch.distributed as dist
+    from orb_slam2_test_amd import ORBextractor, synthetic
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+
+    B = args.batch
+    frames = synthetic.sequence(B, H, W, seed=synthetic.DEFAULT_SEED + 1000 * rank)
+    d_frames = torch.from_numpy(frames).to("cuda")
+    ext = ORBextractor(NFEAT, 1.2, NLEV, 20, 7, device=local, max_batch=B)
+    stream = torch.cuda.current_stream()
+    ext.ctx.set_stream(stream.cuda_stream)
+    f1 = ((np.arange(B) - 1) % B).astype(np.int32)
+    f2 = np.arange(B, dtype=np.int32)
+    summary = torch.zeros(2 * B, dtype=torch.int32, device="cuda")
+    gathered = [torch.zeros_like(summary) for _ in range(world)]
+
+    def step():
+        ext.extract_batch_device(d_frames.data_ptr(), B, W, H)
+        ext.match_batch_device(f1, f2, 100, 0.9, True)
+        ext.ctx.batch_summary(summary.data_ptr())
+        if world > 1:
+            dist.all_gather(gathered, summary)
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+    ncand, nkp = ext.ctx.batch_stats()
+    if not args.no_kernel_timing:
+        ext.ctx.profile(True)
+        ext.ctx.profile_reset()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    t1 = time.perf_counter()
+    elapsed = t1 - t0
+    if world > 1:
+        e = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
+        dist.all_reduce(e, op=dist.ReduceOp.MAX)
+        elapsed = float(e.item())
+    kern = ext.ctx.profile_read() if not args.no_kernel_timing else {}
+    ext.ctx.profile(False)
+
+    frames_total = B * args.steps * world
+    value = frames_total / elapsed
+    out = None
+    if rank == 0:
+        kstats = {}
+        for name, (ms, n) in kern.items():
+            lps = n / max(args.steps, 1)
+            avg = ms / max(n, 1)
+            ab = kernel_algo_bytes(name, B, B, ncand, nkp, lps)
+            kstats[name] = {"ms_per_step": round(ms / args.steps, 4), "launches_per_step": lps,
+                            "avg_launch_ms": round(avg, 5),
+                            "algo_bytes_per_launch": None if ab is None else int(ab),
+                            "achieved_GBps": None if ab is None else round(ab / (avg * 1e-3) / 1e9, 1)}
+        roof = None
+        if kstats:
+            dom = max(kstats, key=lambda k: kstats[k]["ms_per_step"])
+            ks = kstats[dom]
+            ach = ks["achieved_GBps"]
+            traffic = None
+            pmc = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+            if os.path.exists(pmc):
+                with open(pmc) as f:
+                    traffic = json.load(f).get(dom, {}).get("hbm_bytes_per_launch")
+            roof = {"kernel": dom, "bound": "hbm", "achieved": ach, "peak": HBM_PEAK_GBS,
+                    "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBS, 4) if ach else None,
+                    "traffic": traffic,
+                    "algo_bytes_per_launch": ks["algo_bytes_per_launch"],
+                    "avg_launch_ms": ks["avg_launch_ms"]}
+        out = {
+            "metric": METRIC, "value": round(value, 2), "unit": "frames/s", "n_gpus": world,
+            "steps": args.steps, "warmup": args.warmup,
+            "ms_per_step": round(elapsed / args.steps * 1e3, 4), "higher_is_better": True,
+            "scaling": "weak", "vs_baseline": None, "dtype": "u8", "data": "synthetic",
+            "config": {
+                "workload": "C3 KITTI03-shaped mono 1241x376, 2000 feat, 8 lvl: ORBextractor + "
+                            "Hamming knn2 (t vs t-1) + SearchForInitialization(w=100, 0.9, checkOri)",
+                "frames_per_gpu_per_step": B, "global_batch": B * world, "width": W,
+                "height": H, "nfeatures": NFEAT, "nlevels": NLEV,
+                "parallelism": "frames sharded over %d GPU(s), RCCL all_gather of per-frame "
+                               "summary" % world},
+            "roofline": roof,
+            "pipeline_roofline": {"algo_bytes_per_frame": FRAME_ALGO_BYTES,
+                                  "achieved_GBps": round(value * FRAME_ALGO_BYTES / 1e9, 1),
+                                  "frac": round(value * FRAME_ALGO_BYTES / 1e9 / HBM_PEAK_GBS, 4)},
+            "kernels": kstats,
+            "candidates_per_frame": round(ncand / B, 1), "keypoints_per_frame": round(nkp / B, 1),
+        }
+        if world == 1 and not args.no_cpu:
+            n = args.cpu_frames or 24 * args.cpu_threads
+            out["cpu_baseline"] = cpu_baseline(frames, args.cpu_threads, n)
+        else:
+            out["cpu_baseline"] = None
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -140,6 +140,17 @@ int orbg_download_matches(orbg_ctx *ctx, int pair, int32_t *knn, int32_t *matche
 
 int orbg_sync(orbg_ctx *ctx);
 void *orbg_stream(orbg_ctx *ctx); /* the hipStream_t the context launches on */
+/* launch on a caller-owned hipStream_t (e.g. torch's current stream) instead of the
+ * context's own; NULL restores the context stream */
+int orbg_set_stream(orbg_ctx *ctx, void *stream);
+/* per-frame trajectory summary of the last batch, written on the context stream into a
+ * device buffer: d_out[f] = keypoints of frame f (f < nframes), then
+ * d_out[nframes + p] = SearchForInitialization matches of pair p (p < npairs of the last
+ * orbg_match_batch_device, 0 if none) */
+int orbg_batch_summary(orbg_ctx *ctx, int32_t *d_out);
+/* host-side statistics of the last batch (synchronises): FAST candidates over all
+ * cells/levels/frames and output keypoints over all frames (for bandwidth accounting) */
+int orbg_batch_stats(orbg_ctx *ctx, int64_t *ncandidates, int64_t *nkeypoints);
 
 /* per-kernel timing with HIP events on the context stream (for bench roofline) */
 int orbg_profile_enable(orbg_ctx *ctx, int enable);

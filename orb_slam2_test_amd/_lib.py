@@ -92,6 +92,9 @@ def lib():
         "orbg_download_matches": (i32, [vp, i32, vp, vp, i32, vp]),
         "orbg_sync": (i32, [vp]),
         "orbg_stream": (vp, [vp]),
+        "orbg_set_stream": (i32, [vp, vp]),
+        "orbg_batch_summary": (i32, [vp, vp]),
+        "orbg_batch_stats": (i32, [vp, P(C.c_int64), P(C.c_int64)]),
         "orbg_profile_enable": (i32, [vp, i32]),
         "orbg_profile_read": (i32, [vp, i32, P(C.c_char_p), P(C.c_double), P(C.c_int64)]),
         "orbg_profile_reset": (i32, [vp]),
@@ -181,3 +184,16 @@ class Context:
 
     def sync(self):
         check(self._L.orbg_sync(self.handle), "orbg_sync")
+
+    def set_stream(self, stream_ptr):
+        """Launch on a caller-owned hipStream_t (int pointer) or the own stream (None)."""
+        check(self._L.orbg_set_stream(self.handle, C.c_void_p(stream_ptr) if stream_ptr else None),
+              "orbg_set_stream")
+
+    def batch_stats(self):
+        a, b = C.c_int64(), C.c_int64()
+        check(self._L.orbg_batch_stats(self.handle, C.byref(a), C.byref(b)), "orbg_batch_stats")
+        return a.value, b.value
+
+    def batch_summary(self, d_out_ptr):
+        check(self._L.orbg_batch_summary(self.handle, C.c_void_p(d_out_ptr)), "orbg_batch_summary")

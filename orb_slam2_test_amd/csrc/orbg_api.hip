@@ -160,6 +160,7 @@ struct orbg_ctx {
     int device = 0;
     orbg_params p{};
     hipStream_t stream = nullptr;
+    hipStream_t own_stream = nullptr;
     float scale[16], inv_scale[16], sigma2[16], inv_sigma2[16];
     int32_t fpl[16], umax[16];
     // plan
@@ -195,6 +196,7 @@ struct orbg_ctx {
     // matching (batch)
     int32_t *d_pairs = nullptr;
     int pair_cap = 0;
+    std::vector<int32_t> h_pairs;  // last uploaded (f1, f2) lists
     int32_t *d_knn = nullptr, *d_m12 = nullptr, *d_nm = nullptr;
     uint32_t *d_topk = nullptr;
     int32_t *d_topk_n = nullptr;
@@ -293,6 +295,7 @@ static void free_plan(orbg_ctx *c)
     c->d_topk_n = nullptr;
     c->d_pairs = nullptr;
     c->pair_cap = 0;
+    c->h_pairs.clear();
     c->gw = c->gh = c->gbatch = 0;
 }
 
@@ -542,10 +545,11 @@ extern "C" int orbg_create(int device, const orbg_params *p, orbg_ctx **out)
     c->device = device;
     c->p = prm;
     make_tables(c);
-    if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) {
+    if (hipStreamCreateWithFlags(&c->own_stream, hipStreamNonBlocking) != hipSuccess) {
         delete c;
         return set_err(ORBG_EIO, "hipStreamCreate failed");
     }
+    c->stream = c->own_stream;
     *out = c;
     return ORBG_OK;
 }
@@ -560,7 +564,7 @@ extern "C" void orbg_destroy(orbg_ctx *c)
     free_plan(c);
     if (c->d_img) hipFree(c->d_img);
     if (c->d_scr) hipFree(c->d_scr);
-    if (c->stream) hipStreamDestroy(c->stream);
+    if (c->own_stream) hipStreamDestroy(c->own_stream);
     delete c;
 }
 
@@ -750,6 +754,41 @@ extern "C" int orbg_sync(orbg_ctx *c)
 
 extern "C" void *orbg_stream(orbg_ctx *c) { return c ? (void *)c->stream : nullptr; }
 
+extern "C" int orbg_set_stream(orbg_ctx *c, void *stream)
+{
+    if (!c) return set_err(ORBG_EINVAL, "ctx is NULL");
+    HIPCHK(hipStreamSynchronize(c->stream));
+    c->prof.collect();
+    c->stream = stream ? (hipStream_t)stream : c->own_stream;
+    return ORBG_OK;
+}
+
+extern "C" int orbg_batch_stats(orbg_ctx *c, int64_t *ncand, int64_t *nkp)
+{
+    if (!c || !c->gw || c->last_n <= 0) return set_err(ORBG_EINVAL, "no batch");
+    HIPCHK(hipStreamSynchronize(c->stream));
+    std::vector<int32_t> cc((size_t)c->last_n * c->geom.ncells), kc(c->last_n);
+    HIPCHK(hipMemcpy(cc.data(), c->d_cell_cnt, cc.size() * 4, hipMemcpyDeviceToHost));
+    HIPCHK(hipMemcpy(kc.data(), c->d_counts, kc.size() * 4, hipMemcpyDeviceToHost));
+    int64_t a = 0, b = 0;
+    for (int32_t v : cc) a += v;
+    for (int32_t v : kc) b += v;
+    if (ncand) *ncand = a;
+    if (nkp) *nkp = b;
+    return ORBG_OK;
+}
+
+extern "C" int orbg_batch_summary(orbg_ctx *c, int32_t *d_out)
+{
+    if (!c || !c->gw || c->last_n <= 0 || !d_out) return set_err(ORBG_EINVAL, "no batch");
+    HIPCHK(hipMemcpyAsync(d_out, c->d_counts, c->last_n * sizeof(int32_t),
+                          hipMemcpyDeviceToDevice, c->stream));
+    if (c->last_npairs > 0)
+        HIPCHK(hipMemcpyAsync(d_out + c->last_n, c->d_nm, c->last_npairs * sizeof(int32_t),
+                              hipMemcpyDeviceToDevice, c->stream));
+    return ORBG_OK;
+}
+
 extern "C" int orbg_profile_enable(orbg_ctx *c, int enable)
 {
     if (!c) return set_err(ORBG_EINVAL, "ctx is NULL");
@@ -824,6 +863,7 @@ extern "C" int orbg_match_batch_device(orbg_ctx *c, const int32_t *f1, const int
     HIPCHK(hipSetDevice(c->device));
     const size_t fc = (size_t)c->geom.frame_cap;
     if (c->pair_cap < npairs) {
+        c->h_pairs.clear();
         hipFree(c->d_pairs);
         hipFree(c->d_knn);
         hipFree(c->d_m12);
@@ -844,10 +884,15 @@ extern "C" int orbg_match_batch_device(orbg_ctx *c, const int32_t *f1, const int
             return rc;
         c->pair_cap = (int)P;
     }
-    HIPCHK(hipMemcpyAsync(c->d_pairs, f1, npairs * sizeof(int32_t), hipMemcpyHostToDevice,
-                          c->stream));
-    HIPCHK(hipMemcpyAsync(c->d_pairs + c->pair_cap, f2, npairs * sizeof(int32_t),
-                          hipMemcpyHostToDevice, c->stream));
+    // upload the pair lists only when they change (the bench reuses them every step)
+    std::vector<int32_t> hp(f1, f1 + npairs);
+    hp.insert(hp.end(), f2, f2 + npairs);
+    if (hp != c->h_pairs) {
+        HIPCHK(hipMemcpy(c->d_pairs, f1, npairs * sizeof(int32_t), hipMemcpyHostToDevice));
+        HIPCHK(hipMemcpy(c->d_pairs + c->pair_cap, f2, npairs * sizeof(int32_t),
+                         hipMemcpyHostToDevice));
+        c->h_pairs.swap(hp);
+    }
     int rc = launch_match_pairs(c->stream, c->d_desc, c->d_kps, c->d_counts, (int)fc, c->d_pairs,
                                 c->d_pairs + c->pair_cap, npairs, c->geom.w, c->geom.h, window,
                                 nnratio, check_ori, c->d_knn, c->d_m12, c->d_nm, c->d_topk,

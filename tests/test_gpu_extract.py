@@ -1,0 +1,161 @@
+"""GPU: ORBextractor (HIP, through the C ABI) vs the CPU oracle -- bit-exact.
+
+Keypoints are compared field by field (x, y, size, angle, response, octave, class_id),
+descriptors byte by byte, pyramid levels pixel by pixel.  Tolerance: none (integer and
+pinned-float arithmetic).
+"""
+import numpy as np
+import pytest
+
+from orb_slam2_test_amd import ORBextractor, synthetic as S
+from orb_slam2_test_amd import _lib
+
+pytestmark = pytest.mark.gpu
+
+_EXT = {}
+
+
+def ext_for(nfeat=2000, nlevels=8, ini=20, mn=7, **pins):
+    key = (nfeat, nlevels, ini, mn, tuple(sorted(pins.items())))
+    if key not in _EXT:
+        _EXT[key] = ORBextractor(nfeat, 1.2, nlevels, ini, mn, **pins)
+    return _EXT[key]
+
+
+def assert_same(oracle, img, nfeat=2000, nlevels=8, ini=20, mn=7, check_pyr=True,
+                opins=None, **pins):
+    opins = opins or {}
+    p = oracle.params(nfeatures=nfeat, nlevels=nlevels, ini_th_fast=ini, min_th_fast=mn, **opins)
+    ref = oracle.extract(p, img, with_pyramid=True)
+    ext = ext_for(nfeat, nlevels, ini, mn, **pins)
+    kps, desc = ext(img)
+    if check_pyr:
+        for l in range(nlevels):
+            assert np.array_equal(ext.mvImagePyramid[l], ref["pyramid"][l]), f"level {l}"
+    assert len(kps) == len(ref["kps"])
+    for f in _lib.KP_DTYPE.names:
+        assert np.array_equal(kps[f], ref["kps"][f]), f
+    assert np.array_equal(desc, ref["desc"])
+    return kps, desc
+
+
+def test_c2_kitti_frames(oracle, kitti_seq):
+    for t in range(3):
+        kps, desc = assert_same(oracle, kitti_seq[t])
+        assert 2000 <= len(kps) <= 2000 + 3 * 8
+
+
+def test_tum_640x480_1000(oracle):
+    assert_same(oracle, S.frame(480, 640, seed=31), nfeat=1000)
+
+
+def test_mono_init_4000(oracle, kitti_seq):
+    assert_same(oracle, kitti_seq[3], nfeat=4000)
+
+
+def test_pure_noise_many_candidates(oracle):
+    assert_same(oracle, S.pure_noise(376, 1241))
+
+
+def test_constant_image_has_no_keypoints(oracle):
+    kps, desc = assert_same(oracle, S.constant(376, 1241))
+    assert len(kps) == 0 and desc.shape == (0, 32)
+
+
+def test_threshold_fallback_cells(oracle):
+    # low-contrast texture: most cells find nothing at 20 and fall back to 7
+    img = (S.frame(376, 1241, seed=9).astype(np.float32) * 0.15 + 100).astype(np.uint8)
+    assert_same(oracle, img)
+
+
+@pytest.mark.parametrize("w,h,L", [(1226, 370, 8), (752, 480, 8), (500, 300, 5), (333, 250, 3)])
+def test_odd_sizes(oracle, w, h, L):
+    assert_same(oracle, S.frame(h, w, seed=w + h), nlevels=L)
+
+
+def test_small_golden_fixture():
+    g = np.load(__import__("os").path.join(__import__("os").path.dirname(__file__), "golden",
+                                           "small_320x240.npz"), allow_pickle=False)
+    nf, nl, ini, mn = [int(v) for v in g["params"]]
+    ext = ORBextractor(nf, 1.2, nl, ini, mn)
+    kps, desc = ext(g["image"])
+    assert np.array_equal(np.ascontiguousarray(kps).view(np.uint8).reshape(-1, 28), g["kps"])
+    assert np.array_equal(desc, g["desc"])
+
+
+@pytest.mark.parametrize("mode", [_lib.RESIZE_SCALAR, _lib.RESIZE_SSE2_16_4])
+def test_resize_pins(oracle, kitti_seq, mode):
+    assert_same(oracle, kitti_seq[1], resize_mode=mode, opins={"resize_mode": mode})
+
+
+def test_gauss_legacy_table_and_fma_pin(oracle, kitti_seq):
+    k = (18, 34, 49, 55, 49, 34, 18)  # OpenCV 3.2 / 3.4.0-3.4.8 rounding table
+    assert_same(oracle, kitti_seq[2], gauss_k=k, opins={"gauss_k": k}, check_pyr=False)
+    assert_same(oracle, kitti_seq[2], brief_fma=1, opins={"brief_fma": 1}, check_pyr=False)
+
+
+def test_strided_input_and_empty(oracle, kitti_seq):
+    big = np.zeros((376, 1300), np.uint8)
+    big[:, :1241] = kitti_seq[4]
+    view = big[:, :1241]  # row pitch 1300
+    ext = ext_for()
+    k1, d1 = ext(np.ascontiguousarray(view))
+    ref = oracle.extract(oracle.params(), kitti_seq[4])
+    assert np.array_equal(d1, ref["desc"])
+    assert ext(np.zeros((0, 0), np.uint8)) == (None, None)
+
+
+def test_getters_match_oracle_tables(oracle):
+    ext = ext_for()
+    p = oracle.params()
+    assert ext.GetLevels() == 8
+    assert np.float32(ext.GetScaleFactor()) == np.float32(1.2)
+    assert np.array_equal(np.array(ext.GetScaleFactors(), np.float32), np.array(p.scale[:8], np.float32))
+    assert np.array_equal(np.array(ext.GetInverseScaleSigmaSquares(), np.float32),
+                          np.array(p.inv_sigma2[:8], np.float32))
+    assert list(ext.mnFeaturesPerLevel) == list(p.features_per_level[:8])
+
+
+def test_batch_equals_single_and_oracle(oracle):
+    import torch
+    B = 48
+    frames = S.sequence(B, 376, 1241, seed=77)
+    d = torch.from_numpy(frames).cuda()
+    ext = ORBextractor(2000, 1.2, 8, 20, 7, max_batch=B)
+    ext.extract_batch_device(d.data_ptr(), B, 1241, 376)
+    ext.ctx.sync()
+    p = oracle.params()
+    for f in (0, 1, 13, 29, B - 1):
+        k, desc = ext.download_frame(f)
+        r = oracle.extract(p, frames[f])
+        assert np.array_equal(k, r["kps"]) and np.array_equal(desc, r["desc"]), f
+    # full-size properties for every frame of the batch: determinism + bounds
+    outs = [ext.download_frame(f) for f in range(B)]
+    ext.extract_batch_device(d.data_ptr(), B, 1241, 376)
+    ext.ctx.sync()
+    for f in range(B):
+        k2, d2 = ext.download_frame(f)
+        assert np.array_equal(outs[f][0], k2) and np.array_equal(outs[f][1], d2)
+        k = outs[f][0]
+        assert np.all((k["x"] >= 16) & (k["x"] < 1241 - 16) & (k["y"] >= 16) & (k["y"] < 376 - 16))
+        cnt = np.bincount(k["octave"], minlength=8)
+        assert np.all(cnt <= np.array(ext.mnFeaturesPerLevel) + 3)
+        assert np.all(np.diff(k["octave"]) >= 0)
+
+
+def test_batch_padded_pitch(oracle):
+    import torch
+    B, W, H, P = 4, 1241, 376, 1280
+    frames = S.sequence(B, H, W, seed=78)
+    buf = np.zeros((B, H, P), np.uint8)
+    buf[:, :, :W] = frames
+    d = torch.from_numpy(buf).cuda()
+    ext = ORBextractor(2000, 1.2, 8, 20, 7, max_batch=B)
+    ext.extract_batch_device(d.data_ptr(), B, W, H, step=P, frame_stride=P * H)
+    ext.ctx.sync()
+    p = oracle.params()
+    for f in range(B):
+        k, desc = ext.download_frame(f)
+        r = oracle.extract(p, frames[f])
+        assert np.array_equal(k, r["kps"]) and np.array_equal(desc, r["desc"])
+        assert np.array_equal(ext.get_level(f, 0), frames[f])

@@ -1,0 +1,194 @@
+"""CPU: pin the oracle against the known answers the reference text itself holds.
+
+SURVEY.md 8c "Golden vectors / KATs pinned by the reference text": bit_pattern_31_,
+umax, mnFeaturesPerLevel / level sizes, matcher constants, Huber thresholds, and g2o's
+own central-difference Jacobian as the check of the analytic edge Jacobians.
+"""
+import math
+import os
+import re
+
+import numpy as np
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _inc_pattern(path):
+    vals = []
+    with open(path) as f:
+        for line in f:
+            m = re.match(r"ORBG_PAIR\(\s*(-?\d+),\s*(-?\d+),\s*(-?\d+),\s*(-?\d+)\)", line)
+            if m:
+                vals.extend(int(g) for g in m.groups())
+    return vals
+
+
+def test_pattern_tables_match_reference_text(ref_tables):
+    assert len(ref_tables["bit_pattern_31"]) == 1024
+    for p in ("oracle/orb_pattern.inc", "orb_slam2_test_amd/csrc/orb_pattern.inc"):
+        assert _inc_pattern(os.path.join(ROOT, p)) == ref_tables["bit_pattern_31"], p
+
+
+@pytest.mark.skipif(not os.path.isdir("/root/reference/src"), reason="reference text absent")
+def test_ref_tables_current():
+    """ref_tables.json is what tools/make_ref_tables.py extracts from the reference text."""
+    import importlib.util
+    spec = importlib.util.spec_from_file_location(
+        "mrt", os.path.join(ROOT, "tools", "make_ref_tables.py"))
+    mrt = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(mrt)
+    with open("/root/reference/src/ORBextractor.cc", errors="replace") as f:
+        pat = mrt.parse_pattern(f.read())
+    import json
+    with open(os.path.join(ROOT, "tests/golden/ref_tables.json")) as f:
+        assert json.load(f)["bit_pattern_31"] == pat
+
+
+def test_umax_kat(oracle, ref_tables):
+    p = oracle.params()
+    assert list(p.umax) == ref_tables["umax"]
+
+
+@pytest.mark.parametrize("nfeat,expect", [
+    (2000, [434, 362, 302, 251, 209, 175, 145, 122]),
+    (1000, [217, 181, 151, 126, 105, 87, 73, 60]),         # TUM1
+    (4000, [869, 724, 603, 503, 419, 349, 291, 242]),      # mono init 2 x nFeatures
+])
+def test_features_per_level_kat(oracle, nfeat, expect):
+    p = oracle.params(nfeatures=nfeat)
+    got = list(p.features_per_level)[:8]
+    assert got[:7] == expect[:7]
+    assert sum(got) == nfeat
+
+
+def test_level_sizes_kat(oracle):
+    p = oracle.params()
+    assert oracle.level_sizes(p, 1241, 376) == [
+        (1241, 376), (1034, 313), (862, 261), (718, 218), (598, 181), (499, 151), (416, 126),
+        (346, 105)]
+    assert oracle.level_sizes(p, 640, 480) == [
+        (640, 480), (533, 400), (444, 333), (370, 278), (309, 231), (257, 193), (214, 161),
+        (179, 134)]
+    # pyramid totals quoted in SURVEY.md 8
+    assert sum(a * b for a, b in oracle.level_sizes(p, 1241, 376)) == 1444097
+    assert sum(a * b for a, b in oracle.level_sizes(p, 640, 480)) == 950532
+
+
+def test_scale_tables_float_semantics(oracle):
+    p = oracle.params()
+    # mvScaleFactor[i] = float(float(prev) * double(1.2f)), ORBextractor.cc:445 + .h:128
+    s = np.float32(1.0)
+    for i in range(8):
+        assert np.float32(p.scale[i]) == s
+        s = np.float32(np.float64(s) * np.float64(np.float32(1.2)))
+
+
+def test_matcher_constants(ref_tables):
+    from orb_slam2_test_amd import ORBmatcher
+    c = ref_tables["matcher_consts"]
+    assert (ORBmatcher.TH_HIGH, ORBmatcher.TH_LOW, ORBmatcher.HISTO_LENGTH) == (
+        c["TH_HIGH"], c["TH_LOW"], c["HISTO_LENGTH"])
+
+
+def test_descriptor_distance_is_popcount(oracle):
+    rng = np.random.default_rng(0)
+    for _ in range(200):
+        a = rng.integers(0, 256, 32, dtype=np.uint8)
+        b = rng.integers(0, 256, 32, dtype=np.uint8)
+        ref = int(np.unpackbits(a ^ b).sum())
+        assert oracle.descriptor_distance(a, b) == ref
+    z = np.zeros(32, np.uint8)
+    assert oracle.descriptor_distance(z, np.full(32, 255, np.uint8)) == 256
+
+
+def test_fast_atan2_accuracy_and_range(oracle):
+    rng = np.random.default_rng(1)
+    for _ in range(500):
+        y, x = rng.normal(size=2) * 1000
+        a = oracle.fast_atan2(y, x)
+        ref = math.degrees(math.atan2(y, x)) % 360
+        d = abs(a - ref)
+        assert min(d, 360 - d) < 0.02  # fastAtan2 is accurate to ~0.01 deg
+        assert 0 <= a <= 360
+    assert oracle.fast_atan2(0, 0) == 0
+
+
+def test_pinned_sincos_is_correctly_rounded(oracle):
+    rng = np.random.default_rng(2)
+    for a in list(rng.uniform(0, 360, 2000)) + [0, 90, 180, 270, 359.999, 45]:
+        c, s = oracle.sincos_deg(a)
+        ang = np.float32(np.float32(a) * np.float32(math.pi / 180.0))
+        assert c == np.float32(math.cos(float(ang)))
+        assert s == np.float32(math.sin(float(ang)))
+
+
+def test_fast_score_equals_threshold_test(oracle):
+    """cornerScore<16> == max threshold at which the pixel is a corner (score >= th <=> corner)."""
+    rng = np.random.default_rng(3)
+    for _ in range(300):
+        patch = rng.integers(0, 256, (7, 7), dtype=np.uint8)
+        if rng.random() < 0.5:  # plant a corner
+            patch[:, :] = rng.integers(0, 60)
+            patch[3, 3] = 200
+        s = oracle.lib().orc_fast_score(patch.ctypes.data + 3 * 7 + 3, 7)
+        for th in (0, 7, 20, 40):
+            kp = np.zeros(4, oracle.KP_DTYPE)
+            # a 7x7 window has exactly one detectable pixel (3,3), NMS has no neighbours
+            n = oracle.lib().orc_fast_window(patch.ctypes.data, 7, 7, 7, th, kp.ctypes.data, 4)
+            # NMS compares against 0-filled neighbours: a score-0 corner never survives
+            assert n == (1 if (s >= th and s > 0) else 0), (s, th)
+
+
+def test_octree_returns_one_key_per_node(oracle):
+    rng = np.random.default_rng(4)
+    n = 3000
+    keys = np.zeros(n, oracle.KP_DTYPE)
+    pts = rng.choice(1209 * 344, size=n, replace=False)
+    keys["x"] = (pts % 1209).astype(np.float32)
+    keys["y"] = (pts // 1209).astype(np.float32)
+    keys["response"] = rng.integers(7, 100, n).astype(np.float32)
+    out = np.zeros(600, oracle.KP_DTYPE)
+    for N in (1, 50, 434):
+        k = oracle.lib().orc_distribute_octree(keys.ctypes.data, n, 16, 1225, 16, 360, N,
+                                               out.ctypes.data, 600)
+        assert N <= k <= N + 3 or (N < 16 and k <= 16)
+        sel = out[:k]
+        # every selected key is a candidate, no duplicates
+        assert len(set(zip(sel["x"], sel["y"]))) == k
+
+
+def test_ba_analytic_vs_numeric_jacobian(oracle):
+    """g2o's generic BaseBinaryEdge::linearizeOplus (central differences, delta 1e-9,
+    base_binary_edge.hpp:131-205) is the in-tree check of the analytic Jacobians."""
+    from orb_slam2_test_amd import synthetic as S
+    poses, pts, edges = S.ba_window(n_points=150, seed=7)
+    eo, *_ = oracle.ba_linearize(poses, pts, edges)
+    for i in range(0, len(edges), 7):
+        e = edges[i]
+        jp, jt = oracle.ba_numeric_jacobian(poses[e["pose"]], pts[e["point"]], e)
+        D = 3 if e["stereo"] else 2
+        sj = np.abs(eo[i]["jp"][:D]).max()
+        st = np.abs(eo[i]["jt"][:D]).max()
+        assert np.abs(jp[:D] - eo[i]["jp"][:D]).max() / sj < 2e-4
+        assert np.abs(jt[:D] - eo[i]["jt"][:D]).max() / st < 2e-5
+
+
+def test_ba_huber_and_quadratic_form(oracle):
+    """chi2 = e^T Omega e, rho' = 1 inside delta^2 (float dsqr) else delta/sqrt(chi2);
+    H blocks symmetric PSD; b = -J^T W e summed per vertex."""
+    from orb_slam2_test_amd import synthetic as S
+    poses, pts, edges = S.ba_window(n_points=300, seed=8)
+    eo, hp, bp, hq, bq = oracle.ba_linearize(poses, pts, edges)
+    for i in range(len(edges)):
+        e, o = edges[i], eo[i]
+        D = 3 if e["stereo"] else 2
+        chi2 = float(np.sum(o["err"][:D] ** 2) * e["inv_sigma2"])
+        assert abs(o["chi2"] - chi2) <= 1e-12 * max(1.0, chi2)
+        dsqr = np.float32(e["huber_delta"] * e["huber_delta"])
+        want = 1.0 if o["chi2"] <= dsqr else e["huber_delta"] / math.sqrt(o["chi2"])
+        assert o["rho1"] == pytest.approx(want, rel=1e-15)
+    for H in list(hp) + list(hq):
+        assert np.allclose(H, H.T, rtol=1e-12, atol=1e-9 * np.abs(H).max())
+        assert np.linalg.eigvalsh((H + H.T) / 2).min() >= -1e-6 * np.abs(H).max()
+    assert np.all(hp[poses["fixed"] == 1] == 0)
