@@ -15,6 +15,7 @@
 #include <hip/hip_runtime.h>
 
 #include "orbg_internal.h"
+#include "orbg_device.h"
 
 #pragma clang fp contract(off)
 
@@ -31,24 +32,6 @@ __device__ __forceinline__ int cv_round(float v) { return __float2int_rn(v); }
 // ---------------------------------------------------------------------------
 // block-wide helpers (blockDim.x == 256)
 // ---------------------------------------------------------------------------
-__device__ __forceinline__ int wave_incl_scan(int x)
-{
-    const int lane = threadIdx.x & 63;
-#pragma unroll
-    for (int o = 1; o < 64; o <<= 1) {
-        int y = __shfl_up(x, o, 64);
-        if (lane >= o) x += y;
-    }
-    return x;
-}
-
-__device__ __forceinline__ int wave_sum(int x)
-{
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) x += __shfl_xor(x, o, 64);
-    return x;
-}
-
 // exclusive scan of one value per thread over the 256-thread block; *total = block sum.
 // `sh` is an 8-int LDS scratch.  Contains two barriers.
 __device__ int block_excl_scan(int v, int *total, int *sh)
@@ -88,97 +71,159 @@ __global__ __launch_bounds__(256) void k_resize(const uint8_t *__restrict__ src,
                                                 const int2 *__restrict__ xtab,
                                                 const int2 *__restrict__ ytab, int bulk_end)
 {
-    const int dx = blockIdx.x * 64 + (threadIdx.x & 63);
+    // thread = 4 consecutive output pixels of one row (dword store: dpitch % 64 == 0)
+    const int dx0 = 4 * (blockIdx.x * 64 + (threadIdx.x & 63));
     const int dy = blockIdx.y * 4 + (threadIdx.x >> 6);
     const int f = blockIdx.z;
-    if (dx >= dw || dy >= dh) return;
-    const int2 xt = xtab[dx];
+    if (dx0 >= dw || dy >= dh) return;
     const int2 yt = ytab[dy];
-    const int sx = xt.x, sx1 = min(sx + 1, sw - 1);
-    const int a0 = (int)(short)(xt.y & 0xFFFF), a1 = (int)(short)(xt.y >> 16);
     const int sy0 = yt.x & 0xFFFF, sy1 = yt.x >> 16;
     const int b0 = (int)(short)(yt.y & 0xFFFF), b1 = (int)(short)(yt.y >> 16);
     const uint8_t *s0 = src + f * sfs + (int64_t)sy0 * spitch;
     const uint8_t *s1 = src + f * sfs + (int64_t)sy1 * spitch;
-    const int r0 = s0[sx] * a0 + s0[sx1] * a1;
-    const int r1 = s1[sx] * a0 + s1[sx1] * a1;
-    int v;
-    if (dx < bulk_end) {
-        const int a = ((r0 >> 4) * b0) >> 16;
-        const int b = ((r1 >> 4) * b1) >> 16;
-        v = (a + b + 2) >> 2;
+    uint32_t word = 0;
+#pragma unroll
+    for (int i = 0; i < 4; i++) {
+        const int dx = dx0 + i;
+        if (dx < dw) {
+            const int2 xt = xtab[dx];
+            const int sx = xt.x, sx1 = min(sx + 1, sw - 1);
+            const int a0 = (int)(short)(xt.y & 0xFFFF), a1 = (int)(short)(xt.y >> 16);
+            const int r0 = s0[sx] * a0 + s0[sx1] * a1;
+            const int r1 = s1[sx] * a0 + s1[sx1] * a1;
+            int v;
+            if (dx < bulk_end) {
+                const int a = ((r0 >> 4) * b0) >> 16;
+                const int b = ((r1 >> 4) * b1) >> 16;
+                v = (a + b + 2) >> 2;
+            } else {
+                v = (r0 * b0 + r1 * b1 + (1 << 21)) >> 22;
+            }
+            word |= (uint32_t)min(max(v, 0), 255) << (8 * i);
+        }
+    }
+    uint8_t *d = dst + f * dfs + (int64_t)dy * dpitch + dx0;
+    if (dx0 + 4 <= dw) {
+        *(uint32_t *)d = word;
     } else {
-        v = (r0 * b0 + r1 * b1 + (1 << 21)) >> 22;
+        for (int i = 0; dx0 + i < dw; i++) d[i] = (uint8_t)(word >> (8 * i));
     }
-    dst[f * dfs + (int64_t)dy * dpitch + dx] = (uint8_t)min(max(v, 0), 255);
 }
 
 // ---------------------------------------------------------------------------
-// FAST-9 score: max(M) - 1 where M = max over the 16 contiguous 9-arcs of
-// max(min d, min -d), d = centre - circle.  Equals cornerScore<16> for every
-// corner and "corner at threshold th" <=> score >= th.  -1: not a corner.
-// Circle offsets (x, y) of makeOffsets(16).
+// FAST-9 score (cornerScore<16> semantics): s = M - 1, M = max over the 16 contiguous
+// 9-arcs of the circle of max(min d, min -d), d = centre - circle pixel.  "Corner at
+// threshold th" <=> s >= th; the score is stored as u8 max(s, 0) (0 = no corner or score
+// 0, which FAST's NMS treats identically: it keeps a pixel only if score > 0-filled
+// neighbours).  Two pixels per register: u8 -> u16 lanes with v_perm_b32, then
+// v_pk_sub/min/max_i16.  Arc minima use OpenCV's structure: for even k the 8-run
+// d[k+1..k+8] extended by d[k] or d[k+9] (all 16 starts).
 // ---------------------------------------------------------------------------
-__device__ __forceinline__ int fast_score_lds(const uint8_t *t, int stride)
+typedef short v2s __attribute__((ext_vector_type(2)));
+
+__device__ __forceinline__ v2s pmin(v2s a, v2s b) { return __builtin_elementwise_min(a, b); }
+__device__ __forceinline__ v2s pmax(v2s a, v2s b) { return __builtin_elementwise_max(a, b); }
+
+// bytes OFF and OFF+1 of the 12-byte window {w0, w1, w2} as two zero-extended u16 lanes
+template <int OFF>
+__device__ __forceinline__ v2s gather2(uint32_t w0, uint32_t w1, uint32_t w2)
 {
-    const int v = t[0];
-    int d[16];
-    d[0] = v - t[3 * stride];
-    d[1] = v - t[3 * stride + 1];
-    d[2] = v - t[2 * stride + 2];
-    d[3] = v - t[stride + 3];
-    d[4] = v - t[3];
-    d[5] = v - t[-stride + 3];
-    d[6] = v - t[-2 * stride + 2];
-    d[7] = v - t[-3 * stride + 1];
-    d[8] = v - t[-3 * stride];
-    d[9] = v - t[-3 * stride - 1];
-    d[10] = v - t[-2 * stride - 2];
-    d[11] = v - t[-stride - 3];
-    d[12] = v - t[-3];
-    d[13] = v - t[stride - 3];
-    d[14] = v - t[2 * stride - 2];
-    d[15] = v - t[3 * stride - 1];
-    // sliding 9-window min / max over the circular sequence
-    int mn2[16], mx2[16];
-#pragma unroll
-    for (int k = 0; k < 16; k++) {
-        mn2[k] = min(d[k], d[(k + 1) & 15]);
-        mx2[k] = max(d[k], d[(k + 1) & 15]);
+    static_assert(OFF >= 0 && OFF + 1 < 12, "window");
+    uint32_t r;
+    if (OFF + 1 < 4) {
+        r = __builtin_amdgcn_perm(w1, w0, 0x0c000c00u | (OFF + 1) << 16 | OFF);
+    } else if (OFF >= 4 && OFF + 1 < 8) {
+        r = __builtin_amdgcn_perm(w2, w1, 0x0c000c00u | (OFF - 3) << 16 | (OFF - 4));
+    } else if (OFF >= 8) {
+        r = __builtin_amdgcn_perm(w2, w2, 0x0c000c00u | (OFF - 7) << 16 | (OFF - 8));
+    } else if (OFF == 3) {  // straddles w0 / w1
+        r = __builtin_amdgcn_perm(w1, w0, 0x0c040c03u);
+    } else {  // OFF == 7: straddles w1 / w2
+        r = __builtin_amdgcn_perm(w2, w1, 0x0c040c03u);
     }
-    int mn4[16], mx4[16];
+    return __builtin_bit_cast(v2s, r);
+}
+
+struct Rows7 {
+    uint32_t w[7][3];
+};
+
+// circle (dx, dy) of makeOffsets(16); row index = 3 + dy, byte offset = 4 + dx (+ pixel i)
+template <int I>
+__device__ __forceinline__ v2s fast_score_pair(const Rows7 &R)
+{
+#define GB(row, dx) gather2<4 + (dx) + I>(R.w[row][0], R.w[row][1], R.w[row][2])
+    const v2s v = GB(3, 0);
+    v2s d[16];
+    d[0] = v - GB(6, 0);
+    d[1] = v - GB(6, 1);
+    d[2] = v - GB(5, 2);
+    d[3] = v - GB(4, 3);
+    d[4] = v - GB(3, 3);
+    d[5] = v - GB(2, 3);
+    d[6] = v - GB(1, 2);
+    d[7] = v - GB(0, 1);
+    d[8] = v - GB(0, 0);
+    d[9] = v - GB(0, -1);
+    d[10] = v - GB(1, -2);
+    d[11] = v - GB(2, -3);
+    d[12] = v - GB(3, -3);
+    d[13] = v - GB(4, -3);
+    d[14] = v - GB(5, -2);
+    d[15] = v - GB(6, -1);
+#undef GB
+    v2s lo2[8], hi2[8], lo4[8], hi4[8], lo8[8], hi8[8];
 #pragma unroll
-    for (int k = 0; k < 16; k++) {
-        mn4[k] = min(mn2[k], mn2[(k + 2) & 15]);
-        mx4[k] = max(mx2[k], mx2[(k + 2) & 15]);
+    for (int j = 0; j < 8; j++) {  // odd start s = 2j+1
+        const int s = 2 * j + 1;
+        lo2[j] = pmin(d[s], d[(s + 1) & 15]);
+        hi2[j] = pmax(d[s], d[(s + 1) & 15]);
     }
-    int best_pos = -1000, best_neg = 1000;
 #pragma unroll
-    for (int k = 0; k < 16; k++) {
-        const int mn9 = min(min(mn4[k], mn4[(k + 4) & 15]), d[(k + 8) & 15]);
-        const int mx9 = max(max(mx4[k], mx4[(k + 4) & 15]), d[(k + 8) & 15]);
-        best_pos = max(best_pos, mn9);
-        best_neg = min(best_neg, mx9);
+    for (int j = 0; j < 8; j++) {
+        lo4[j] = pmin(lo2[j], lo2[(j + 1) & 7]);
+        hi4[j] = pmax(hi2[j], hi2[(j + 1) & 7]);
     }
-    const int M = max(best_pos, -best_neg);
-    return M >= 1 ? M - 1 : -1;
+#pragma unroll
+    for (int j = 0; j < 8; j++) {
+        lo8[j] = pmin(lo4[j], lo4[(j + 2) & 7]);  // d[s .. s+7]
+        hi8[j] = pmax(hi4[j], hi4[(j + 2) & 7]);
+    }
+    v2s bp = (v2s){-1000, -1000}, bn = (v2s){1000, 1000};
+#pragma unroll
+    for (int j = 0; j < 8; j++) {  // even k = 2j: run d[k+1..k+8] = lo8[j]
+        const int k = 2 * j;
+        bp = pmax(bp, pmax(pmin(lo8[j], d[k]), pmin(lo8[j], d[(k + 9) & 15])));
+        bn = pmin(bn, pmin(pmax(hi8[j], d[k]), pmax(hi8[j], d[(k + 9) & 15])));
+    }
+    const v2s zero = (v2s){0, 0}, one = (v2s){1, 1};
+    const v2s M = pmax(bp, zero - bn);
+    return pmax(M - one, zero);  // u8 score, 0 = none
 }
 
 // ---------------------------------------------------------------------------
-// k_fast_cells: one workgroup per (cell, frame)
+// k_fast_cells: one 256-thread workgroup per (cell, frame).
+// LDS tile: window row r at tile[r][1 + x] (x window-local) so that a group of 4
+// detection pixels (window x = 3+4g .. 6+4g) and its +-3 neighbours are the 12 bytes of
+// dwords g..g+2.  Scores: sc[ry+1][rx+4] with a zero border (NMS neighbours outside the
+// cell's detection region count as 0 -- cv::FAST runs on the cell ROI alone).
+// Unit = (region row ry, 4-pixel group g), u = ry*RG + g, handled in raster order so
+// compaction preserves FAST's row-major output order.
 // ---------------------------------------------------------------------------
-#define FAST_MAXPIX (ORBG_MAX_WIN * ORBG_MAX_WIN)
+#define FC_P 72               // LDS row pitch (bytes)
+#define FC_MAXU 4             // units per thread (<= 60x60 region / 4 / 256)
 
 __global__ __launch_bounds__(256) void k_fast_cells(const OrbgGeom *__restrict__ g,
                                                     const OrbgCell *__restrict__ cells,
                                                     const uint8_t *__restrict__ img0,
                                                     int64_t img_fs, int img_pitch,
                                                     const uint8_t *__restrict__ pyr,
+                                                    const uint32_t *__restrict__ ctab,
                                                     int32_t *__restrict__ cell_cnt,
-                                                    uint32_t *__restrict__ cell_kp)
+                                                    uint2 *__restrict__ cell_kp)
 {
-    __shared__ uint8_t tile[FAST_MAXPIX];
-    __shared__ int16_t sc[FAST_MAXPIX];
+    __shared__ __attribute__((aligned(16))) uint8_t tile[ORBG_MAX_WIN][FC_P];
+    __shared__ __attribute__((aligned(16))) uint8_t sc[ORBG_MAX_WIN][FC_P];
     __shared__ int red[8];
     const int c = blockIdx.x, f = blockIdx.y, tid = threadIdx.x;
     const OrbgCell cl = cells[c];
@@ -194,49 +239,89 @@ __global__ __launch_bounds__(256) void k_fast_cells(const OrbgGeom *__restrict__
         pitch = g->lv[l].pitch;
     }
     base += (int64_t)cl.y0 * pitch + cl.x0;
-    for (int i = tid; i < W * H; i += 256) {
-        const int y = i / W, x = i - y * W;
-        tile[i] = base[(int64_t)y * pitch + x];
+    {
+        const int cx = tid & 63;
+        for (int r = tid >> 6; r < H; r += 4) {
+            const uint8_t *row = base + (int64_t)r * pitch;
+            if (cx < W) tile[r][1 + cx] = row[cx];
+            if (cx + 64 < W) tile[r][65 + cx] = row[cx + 64];
+        }
+    }
+    const int RW = W - 6, RH = H - 6;
+    const int RG = RW > 0 ? (RW + 3) >> 2 : 0;
+    const int nunits = RH > 0 ? RH * RG : 0;
+    {
+        uint32_t *z = (uint32_t *)&sc[0][0];
+        const int nz = (RH + 2) * (FC_P / 4);
+        for (int i = tid; i < nz; i += 256) z[i] = 0;
     }
     __syncthreads();
 
-    const int RW = W - 6, RH = H - 6;  // detection region [3, W-3) x [3, H-3)
-    const int npix = (RW > 0 && RH > 0) ? RW * RH : 0;
-    const int chunk = (npix + 255) / 256;
-    const int p0 = min(tid * chunk, npix), p1 = min(p0 + chunk, npix);
-    for (int p = p0; p < p1; p++) {
-        const int ry = p / RW, rx = p - ry * RW;
-        const int idx = (ry + 3) * W + rx + 3;
-        sc[idx] = (int16_t)fast_score_lds(&tile[idx], W);
+    // ---- scores ----
+    for (int k = 0; k < FC_MAXU; k++) {
+        const int u = tid + 256 * k;
+        if (u >= nunits) break;
+        const int ry = u / RG, gg = u - ry * RG;
+        Rows7 R;
+#pragma unroll
+        for (int r = 0; r < 7; r++) {
+            const uint32_t *p = (const uint32_t *)&tile[ry + r][4 * gg];
+            R.w[r][0] = p[0];
+            R.w[r][1] = p[1];
+            R.w[r][2] = p[2];
+        }
+        const v2s sa = fast_score_pair<0>(R);
+        const v2s sb = fast_score_pair<2>(R);
+        uint32_t word = (uint32_t)(uint16_t)sa.x | ((uint32_t)(uint16_t)sa.y << 8) |
+                        ((uint32_t)(uint16_t)sb.x << 16) | ((uint32_t)(uint16_t)sb.y << 24);
+        const int valid = min(RW - 4 * gg, 4);
+        if (valid < 4) word &= (1u << (8 * valid)) - 1u;
+        *(uint32_t *)&sc[ry + 1][4 * gg + 4] = word;
     }
     __syncthreads();
 
-    // NMS at threshold th over this thread's raster chunk; bitmask of survivors
+    // ---- NMS (cell-local) at threshold th: 4-bit survivor mask per unit ----
+    uint32_t centre[FC_MAXU];
     auto nms = [&](int th, uint32_t &mask) -> int {
         int cnt = 0;
         mask = 0;
-        for (int p = p0; p < p1; p++) {
-            const int ry = p / RW, rx = p - ry * RW;
-            const int idx = (ry + 3) * W + rx + 3;
-            const int s = sc[idx];
-            if (s < th) continue;
-            bool keep = true;
 #pragma unroll
-            for (int dy = -1; dy <= 1; dy++)
+        for (int k = 0; k < FC_MAXU; k++) {
+            const int u = tid + 256 * k;
+            centre[k] = 0;
+            if (u >= nunits) continue;
+            const int ry = u / RG, gg = u - ry * RG;
+            const uint32_t *m0 = (const uint32_t *)&sc[ry + 1][4 * gg];
+            const uint32_t c1 = m0[1];
+            centre[k] = c1;
+            // quick reject: no byte >= max(th, 1)
+            const int t1 = max(th, 1);
+            const int mx = max(max((int)(c1 & 0xFF), (int)((c1 >> 8) & 0xFF)),
+                               max((int)((c1 >> 16) & 0xFF), (int)(c1 >> 24)));
+            if (mx < t1) continue;
+            const uint32_t *mu = (const uint32_t *)&sc[ry][4 * gg];
+            const uint32_t *md = (const uint32_t *)&sc[ry + 2][4 * gg];
+            const uint32_t row[3][3] = {{mu[0], mu[1], mu[2]}, {m0[0], c1, m0[2]},
+                                        {md[0], md[1], md[2]}};
 #pragma unroll
-                for (int dx = -1; dx <= 1; dx++) {
-                    if (dx == 0 && dy == 0) continue;
-                    const int qy = ry + dy, qx = rx + dx;
-                    int q = 0;
-                    if (qy >= 0 && qy < RH && qx >= 0 && qx < RW) {
-                        const int sq = sc[(qy + 3) * W + qx + 3];
-                        q = sq >= th ? sq : 0;
+            for (int i = 0; i < 4; i++) {
+                const int s = (c1 >> (8 * i)) & 0xFF;
+                if (s < t1) continue;
+                bool keep = true;
+#pragma unroll
+                for (int rr = 0; rr < 3; rr++)
+#pragma unroll
+                    for (int dx = -1; dx <= 1; dx++) {
+                        if (rr == 1 && dx == 0) continue;
+                        const int off = 4 + i + dx;  // byte offset in the 12-byte window
+                        const int q = (row[rr][off >> 2] >> (8 * (off & 3))) & 0xFF;
+                        const int qe = q >= th ? q : 0;
+                        keep = keep && (s > qe);
                     }
-                    keep = keep && (s > q);
+                if (keep) {
+                    mask |= 1u << (4 * k + i);
+                    cnt++;
                 }
-            if (keep) {
-                mask |= 1u << (p - p0);
-                cnt++;
             }
         }
         return cnt;
@@ -245,33 +330,53 @@ __global__ __launch_bounds__(256) void k_fast_cells(const OrbgGeom *__restrict__
     int cnt = nms(g->ini_th, mask);
     const int tot_ini = block_sum(cnt, red);
     if (tot_ini == 0) cnt = nms(g->min_th, mask);
-    int total;
-    int off = block_excl_scan(cnt, &total, red);
+
+    // ---- raster-order compaction ----
     const int64_t slot = (int64_t)f * g->ncells + c;
-    uint32_t *out = cell_kp + slot * g->cell_cap;
-    const int xo = cl.x0 - ORBG_MIN_BORDER, yo = cl.y0 - ORBG_MIN_BORDER;
-    for (int p = p0; p < p1; p++) {
-        if (!(mask & (1u << (p - p0)))) continue;
-        const int ry = p / RW, rx = p - ry * RW;
-        const int s = sc[(ry + 3) * W + rx + 3];
-        out[off++] = orbg_pack(xo + rx + 3, yo + ry + 3, s);
+    uint2 *out = cell_kp + slot * g->cell_cap;
+    const int xo = cl.x0 - ORBG_MIN_BORDER + 3, yo = cl.y0 - ORBG_MIN_BORDER + 3;
+    const uint32_t *xs = ctab + g->lv[l].xs_off, *ys = ctab + g->lv[l].ys_off;
+    int run = 0;
+    for (int k = 0; k < FC_MAXU; k++) {
+        if (256 * k >= nunits) break;  // uniform
+        const uint32_t mk = (mask >> (4 * k)) & 0xFu;
+        int tot;
+        int off = block_excl_scan(__popc(mk), &tot, red) + run;
+        const int u = tid + 256 * k;
+        if (mk) {
+            const int ry = u / RG, gg = u - ry * RG;
+#pragma unroll
+            for (int i = 0; i < 4; i++)
+                if (mk & (1u << i)) {
+                    const int x = xo + 4 * gg + i, y = yo + ry;
+                    out[off++] = make_uint2(orbg_pack(x, y, (centre[k] >> (8 * i)) & 0xFF),
+                                            xs[x] | ys[y]);
+                }
+        }
+        run += tot;
     }
-    if (tid == 0) cell_cnt[slot] = total;
+    if (tid == 0) cell_cnt[slot] = run;
 }
 
 // ---------------------------------------------------------------------------
 // k_blur: GaussianBlur(7x7, sigma 2, BORDER_REFLECT_101), bit-exact fixed point
-// out = sat((sum_v k_v * sum_h k_h * p + 2^15) >> 16).  64x16 output tile.
-// blockIdx.x enumerates tiles of all levels (tile_base per level in g).
+// out = sat((sum_v k_v * sum_h k_h * p + 2^15) >> 16).
+// 128x32 output tile per 256-thread workgroup.  The (128+8)x38 input tile (x origin
+// aligned at tile_x0 - 4) is filled with coalesced byte loads and a branch-free
+// reflection; the row pass keeps u16 sums (<= 256*255) in LDS; the column pass reads
+// 4 sums per ds_read_b64 and stores 4 output pixels per dword.
+// blockIdx.x enumerates tiles of all levels (tile_base per level).
 // ---------------------------------------------------------------------------
+#define BLUR_TW 128
+#define BLUR_TH 32
+#define BLUR_IW (BLUR_TW + 8)
+#define BLUR_IH (BLUR_TH + 6)
+
 __device__ __forceinline__ int reflect101(int i, int n)
 {
-    if (n == 1) return 0;
-    while (i < 0 || i >= n) {
-        if (i < 0) i = -i;
-        if (i >= n) i = 2 * n - 2 - i;
-    }
-    return i;
+    // single reflection suffices for the 3-pixel halo (n >= 4 for every level)
+    i = i < 0 ? -i : i;
+    return i >= n ? 2 * n - 2 - i : i;
 }
 
 __global__ __launch_bounds__(256) void k_blur(const OrbgGeom *__restrict__ g,
@@ -280,15 +385,17 @@ __global__ __launch_bounds__(256) void k_blur(const OrbgGeom *__restrict__ g,
                                               int img_pitch, const uint8_t *__restrict__ pyr,
                                               uint8_t *__restrict__ blur)
 {
-    __shared__ uint8_t in[22][72];
-    __shared__ int rows[22][64];
+    __shared__ __attribute__((aligned(16))) uint8_t in[BLUR_IH][BLUR_IW];
+    __shared__ __attribute__((aligned(16))) uint16_t rows[BLUR_IH][BLUR_TW];
     const int f = blockIdx.y, tid = threadIdx.x;
     int l = 0;
     while (l + 1 < g->L && (int)blockIdx.x >= tile_base[l + 1]) l++;
     const int t = blockIdx.x - tile_base[l];
     const OrbgLevel &lv = g->lv[l];
-    const int ntx = (lv.w + 63) / 64;
-    const int tx0 = (t % ntx) * 64, ty0 = (t / ntx) * 16;
+    const int W = lv.w, H = lv.h;
+    const int ntx = (W + BLUR_TW - 1) / BLUR_TW;
+    const int ty = t / ntx;
+    const int tx0 = (t - ty * ntx) * BLUR_TW, ty0 = ty * BLUR_TH;
     const uint8_t *src;
     int pitch;
     if (l == 0) {
@@ -298,30 +405,77 @@ __global__ __launch_bounds__(256) void k_blur(const OrbgGeom *__restrict__ g,
         src = pyr + f * g->pyr_frame + lv.pyr_off;
         pitch = lv.pitch;
     }
-    for (int i = tid; i < 22 * 70; i += 256) {
-        const int yy = i / 70, xx = i - yy * 70;
-        const int sy = reflect101(ty0 + yy - 3, lv.h), sx = reflect101(tx0 + xx - 3, lv.w);
-        in[yy][xx] = src[(int64_t)sy * pitch + sx];
+    // fill: column c of the tile is image x = tx0 - 4 + c, row r is y = ty0 - 3 + r
+    for (int i = tid; i < BLUR_IH * BLUR_IW; i += 256) {
+        const int r = i / BLUR_IW, c = i - r * BLUR_IW;
+        const int y = reflect101(min(ty0 - 3 + r, H + 2), H);
+        const int x = reflect101(min(tx0 - 4 + c, W + 2), W);
+        in[r][c] = src[(int64_t)y * pitch + x];
     }
     __syncthreads();
     const int k0 = g->gk[0], k1 = g->gk[1], k2 = g->gk[2], k3 = g->gk[3], k4 = g->gk[4],
               k5 = g->gk[5], k6 = g->gk[6];
-    for (int i = tid; i < 22 * 64; i += 256) {
-        const int yy = i >> 6, xx = i & 63;
-        const uint8_t *r = &in[yy][xx];
-        rows[yy][xx] = k0 * r[0] + k1 * r[1] + k2 * r[2] + k3 * r[3] + k4 * r[4] + k5 * r[5] +
-                       k6 * r[6];
+    // row pass: unit = (row r, 4-column group j); outputs x = 4j..4j+3 need tile bytes 4j+1..4j+10
+    for (int u = tid; u < BLUR_IH * (BLUR_TW / 4); u += 256) {
+        const int r = u >> 5, j = u & 31;
+        const uint32_t *w = (const uint32_t *)&in[r][4 * j];
+        const uint32_t w0 = w[0], w1 = w[1], w2 = w[2];
+        int p[12];
+#pragma unroll
+        for (int b = 0; b < 4; b++) {
+            p[b] = (w0 >> (8 * b)) & 0xFF;
+            p[4 + b] = (w1 >> (8 * b)) & 0xFF;
+            p[8 + b] = (w2 >> (8 * b)) & 0xFF;
+        }
+        uint32_t s[4];
+#pragma unroll
+        for (int o = 0; o < 4; o++) {
+            const int* q = &p[o + 1];
+            s[o] = (uint32_t)(k0 * q[0] + k1 * q[1] + k2 * q[2] + k3 * q[3] + k4 * q[4] +
+                              k5 * q[5] + k6 * q[6]);
+        }
+        uint2 pk;
+        pk.x = s[0] | (s[1] << 16);
+        pk.y = s[2] | (s[3] << 16);
+        *(uint2 *)&rows[r][4 * j] = pk;
     }
     __syncthreads();
+    // column pass: thread = (4-column group j, 4-row group rg)
+    const int j = tid & 31, rg = tid >> 5;  // rg in [0, 8): rows 4rg .. 4rg+3
+    uint32_t acc[4][4];
+#pragma unroll
+    for (int o = 0; o < 4; o++)
+#pragma unroll
+        for (int b = 0; b < 4; b++) acc[o][b] = 0;
+    const int kk[7] = {k0, k1, k2, k3, k4, k5, k6};
+#pragma unroll
+    for (int rr = 0; rr < 10; rr++) {
+        const uint2 pk = *(const uint2 *)&rows[4 * rg + rr][4 * j];
+        const uint32_t v[4] = {pk.x & 0xFFFF, pk.x >> 16, pk.y & 0xFFFF, pk.y >> 16};
+#pragma unroll
+        for (int o = 0; o < 4; o++) {
+            const int tap = rr - o;
+            if (tap >= 0 && tap < 7) {
+#pragma unroll
+                for (int b = 0; b < 4; b++) acc[o][b] += (uint32_t)kk[tap] * v[b];
+            }
+        }
+    }
     uint8_t *dst = blur + f * g->blur_frame + lv.blur_off;
-    for (int i = tid; i < 16 * 64; i += 256) {
-        const int yy = i >> 6, xx = i & 63;
-        const int gy = ty0 + yy, gx = tx0 + xx;
-        if (gy >= lv.h || gx >= lv.w) continue;
-        const int acc = k0 * rows[yy][xx] + k1 * rows[yy + 1][xx] + k2 * rows[yy + 2][xx] +
-                        k3 * rows[yy + 3][xx] + k4 * rows[yy + 4][xx] + k5 * rows[yy + 5][xx] +
-                        k6 * rows[yy + 6][xx];
-        dst[(int64_t)gy * lv.pitch + gx] = (uint8_t)min(max((acc + (1 << 15)) >> 16, 0), 255);
+    const int gx = tx0 + 4 * j;
+#pragma unroll
+    for (int o = 0; o < 4; o++) {
+        const int gy = ty0 + 4 * rg + o;
+        if (gy >= H || gx >= W) continue;
+        uint32_t word = 0;
+#pragma unroll
+        for (int b = 0; b < 4; b++) word |= min((acc[o][b] + (1u << 15)) >> 16, 255u) << (8 * b);
+        uint8_t *d = dst + (int64_t)gy * lv.pitch + gx;
+        if (gx + 4 <= W) {
+            *(uint32_t *)d = word;  // pitch is a multiple of 64, gx of 4: aligned
+        } else {
+            for (int b = 0; b < 4 && gx + b < W; b++) d[b] = (uint8_t)(word >> (8 * b));
+        }
     }
 }
 
@@ -337,6 +491,7 @@ __global__ __launch_bounds__(256) void k_blur(const OrbgGeom *__restrict__ g,
 //   untouched nodes in their previous order.
 // Keys carry their node id (knode); only keys of multi-key nodes ("active") are touched.
 // ---------------------------------------------------------------------------
+
 struct OctShared {
     uint16_t ord[2][ORBG_OCT_ALIVE];
     uint16_t aux[ORBG_OCT_ALIVE];          // split-before counts / processing list
@@ -387,7 +542,7 @@ __device__ __forceinline__ int4 child_rect(int4 n, int q, int cnt)
 
 __global__ __launch_bounds__(ORBG_OCT_THREADS) void k_octree(
     const OrbgGeom *__restrict__ g, const int32_t *__restrict__ cell_cnt,
-    const uint32_t *__restrict__ cell_kp, uint32_t *__restrict__ keys_all,
+    const uint2 *__restrict__ cell_kp, uint32_t *__restrict__ keys_all,
     uint32_t *__restrict__ knode_all, uint32_t *__restrict__ act_all,
     uint8_t *__restrict__ qk_all, int4 *__restrict__ nodes_all, uint32_t *__restrict__ lvl_kp,
     int32_t *__restrict__ lvl_cnt, int32_t *__restrict__ err_flag)
@@ -410,16 +565,24 @@ __global__ __launch_bounds__(ORBG_OCT_THREADS) void k_octree(
 
     // ---- gather candidates of this level's cells in cell order (vToDistributeKeys) ----
     const int32_t *ccount = cell_cnt + (int64_t)f * g->ncells + lv.cell_base;
-    const uint32_t *ckp = cell_kp + ((int64_t)f * g->ncells + lv.cell_base) * g->cell_cap;
+    const uint2 *ckp = cell_kp + ((int64_t)f * g->ncells + lv.cell_base) * g->cell_cap;
     int n = 0;
     {
         int run = 0;
         for (int c0 = 0; c0 < lv.ncells; c0 += nthr) {
             const int c = c0 + tid;
+            int tot;
+            block_excl_scan(c < lv.ncells ? ccount[c] : 0, &tot, S.red);
+            run += tot;
+        }
+        if (run <= OCT_KEY_CAP && lv.ncells + 1 <= ORBG_OCT_ALIVE) return;  // k_octree_lds
+        run = 0;
+        for (int c0 = 0; c0 < lv.ncells; c0 += nthr) {
+            const int c = c0 + tid;
             const int cn = c < lv.ncells ? ccount[c] : 0;
             int tot;
             const int off = block_excl_scan(cn, &tot, S.red) + run;
-            for (int i = 0; i < cn; i++) keys[off + i] = ckp[(int64_t)c * g->cell_cap + i];
+            for (int i = 0; i < cn; i++) keys[off + i] = ckp[(int64_t)c * g->cell_cap + i].x;
             run += tot;
         }
         n = run;

@@ -292,14 +292,17 @@ __global__ __launch_bounds__(256) void k_init_cands_pairs(
 
 // prev stride: the batch path reads x,y out of orbg_keypoint records (stride 7 floats)
 #define RESOLVE_CHUNK 64
-#define RESOLVE_N2_CAP 4608
+#define RESOLVE_N2_CAP 4608  // n1, n2 <= frame capacity (4000 features + 8 x 3)
 
 struct ResolveShared {
     int mdist[RESOLVE_N2_CAP];
     int m21[RESOLVE_N2_CAP];
+    int m12[RESOLVE_N2_CAP];
+    float ang1[RESOLVE_N2_CAP];
+    float ang2[RESOLVE_N2_CAP];
     int8_t hbin[RESOLVE_N2_CAP];
-    unsigned long long chunk[RESOLVE_CHUNK * ORBG_MATCH_TOPK];
-    int chunkn[RESOLVE_CHUNK];
+    unsigned long long chunk[2][RESOLVE_CHUNK * ORBG_MATCH_TOPK];
+    int chunkn[2][RESOLVE_CHUNK];
     int hsize[HISTO_LENGTH];
     int nm;
 };
@@ -335,103 +338,195 @@ __device__ void rescan(const orbg_keypoint *k2, const uint8_t *d2, int n2, const
     *best2 = b == ~0ull ? INT_MAX : (int)(b >> 32);
 }
 
-// one wave (64 threads) per pair
-__device__ void init_resolve_wave(ResolveShared &S, const orbg_keypoint *__restrict__ k1,
-                                  const uint8_t *__restrict__ d1, int n1,
-                                  const orbg_keypoint *__restrict__ k2,
-                                  const uint8_t *__restrict__ d2, int n2, orbg_bounds b,
-                                  const float *prev, int prev_stride, int window, float nnratio,
-                                  int check_ori, const unsigned long long *__restrict__ topk,
-                                  const int32_t *__restrict__ topn, int32_t *__restrict__ m12,
-                                  int32_t *__restrict__ nm_out, float *prev_out)
+// Two waves per pair.  Wave 0's lane 0 walks the queries in index order (the
+// reference's sequential semantics) over candidate lists in LDS while wave 1 prefetches
+// the next chunk of lists (double buffer); wave 0 runs the exact rescan for a query
+// whose K-list the vMatchedDistance filter exhausted.
+#define RESOLVE_T 128
+
+__device__ __forceinline__ void wave_sync_lds()
 {
-    const int lane = threadIdx.x & 63;
-    for (int i = lane; i < n2; i += 64) {
-        S.mdist[i] = INT_MAX;
-        S.m21[i] = -1;
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+}
+
+__device__ void init_resolve_block(ResolveShared &S, const orbg_keypoint *__restrict__ k1,
+                                   const uint8_t *__restrict__ d1, int n1,
+                                   const orbg_keypoint *__restrict__ k2,
+                                   const uint8_t *__restrict__ d2, int n2, orbg_bounds b,
+                                   const float *prev, int prev_stride, int window, float nnratio,
+                                   int check_ori, const unsigned long long *__restrict__ topk,
+                                   const int32_t *__restrict__ topn, int32_t *__restrict__ m12,
+                                   int32_t *__restrict__ nm_out, float *prev_out)
+{
+    const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+    for (int i0 = 0; i0 < n2; i0 += 4 * RESOLVE_T) {
+        float a[4];
+#pragma unroll
+        for (int u = 0; u < 4; u++) {
+            const int i = i0 + u * RESOLVE_T + tid;
+            a[u] = i < n2 ? k2[i].angle : 0.f;
+        }
+#pragma unroll
+        for (int u = 0; u < 4; u++) {
+            const int i = i0 + u * RESOLVE_T + tid;
+            if (i < n2) {
+                S.mdist[i] = INT_MAX;
+                S.m21[i] = -1;
+                S.ang2[i] = a[u];
+            }
+        }
     }
-    for (int i = lane; i < n1; i += 64) {
-        S.hbin[i] = -1;
-        m12[i] = -1;
+    for (int i0 = 0; i0 < n1; i0 += 4 * RESOLVE_T) {
+        float a[4];
+#pragma unroll
+        for (int u = 0; u < 4; u++) {
+            const int i = i0 + u * RESOLVE_T + tid;
+            a[u] = i < n1 ? k1[i].angle : 0.f;
+        }
+#pragma unroll
+        for (int u = 0; u < 4; u++) {
+            const int i = i0 + u * RESOLVE_T + tid;
+            if (i < n1) {
+                S.hbin[i] = -1;
+                S.m12[i] = -1;
+                S.ang1[i] = a[u];
+            }
+        }
     }
-    if (lane < HISTO_LENGTH) S.hsize[lane] = 0;
-    if (lane == 0) S.nm = 0;
-    __syncthreads();
+    if (tid < HISTO_LENGTH) S.hsize[tid] = 0;
+    if (tid == 0) S.nm = 0;
     const GridPrm g = grid_prm(b);
     const float factor = 1.0f / HISTO_LENGTH;
-    int nmatches = 0;
-    for (int c0 = 0; c0 < n1; c0 += RESOLVE_CHUNK) {
+    // lane 0 of wave 0: sequential state update for query i1
+    auto apply = [&](int i1, int bestDist, int bestDist2, int bestIdx2) {
+        if (bestDist <= TH_LOW && bestDist < (float)bestDist2 * nnratio) {
+            const int old = S.m21[bestIdx2];
+            const float rot0 = S.ang1[i1] - S.ang2[bestIdx2];
+            if (old >= 0) {
+                S.m12[old] = -1;
+                S.nm--;
+            }
+            S.m12[i1] = bestIdx2;
+            S.m21[bestIdx2] = i1;
+            S.mdist[bestIdx2] = bestDist;
+            S.nm++;
+            if (check_ori) {
+                float rot = rot0;
+                if (rot < 0.0f) rot += 360.0f;
+                int bin = (int)roundf(rot * factor);
+                if (bin == HISTO_LENGTH) bin = 0;
+                S.hbin[i1] = (int8_t)bin;
+                S.hsize[bin]++;
+            }
+        }
+    };
+    // wave 1: load chunk c into buffer c & 1 (lists only when the chunk has a live query)
+    auto prefetch = [&](int c) {
+        const int c0 = c * RESOLVE_CHUNK;
+        if (c0 >= n1) return;
         const int cn = min(RESOLVE_CHUNK, n1 - c0);
-        // prefetch the chunk's K-lists (independent of the sequential state)
-        for (int i = lane; i < cn * ORBG_MATCH_TOPK; i += 64)
-            S.chunk[i] = topk[(size_t)c0 * ORBG_MATCH_TOPK + i];
-        if (lane < cn) S.chunkn[lane] = topn[c0 + lane];
-        __syncthreads();
-        for (int qi = 0; qi < cn; qi++) {
-            const int i1 = c0 + qi;
-            const int total = S.chunkn[qi];
-            if (total <= 0) continue;  // octave > 0 (-1) or empty window (0)
-            // walk the sorted K-list: first two entries that pass the vMatchedDistance filter
-            const int kk = min(total, ORBG_MATCH_TOPK);
-            bool ok = false;
-            unsigned long long e = ~0ull;
-            if (lane < kk) {
-                e = S.chunk[qi * ORBG_MATCH_TOPK + lane];
-                const int d = (int)(e >> 32), i2 = (int)(e & 0xFFFFF);
-                ok = !(S.mdist[i2] <= d);
-            }
-            const unsigned long long bal = __ballot(ok);
-            int bestDist, bestDist2, bestIdx2;
-            const int nvalid = __popcll(bal);
-            if (nvalid >= 2 || total <= ORBG_MATCH_TOPK) {
-                const int l1 = nvalid >= 1 ? __ffsll((long long)bal) - 1 : -1;
-                const unsigned long long rest = nvalid >= 1 ? (bal & (bal - 1)) : 0ull;
-                const int l2 = nvalid >= 2 ? __ffsll((long long)rest) - 1 : -1;
-                const unsigned long long e1 = l1 >= 0 ? __shfl(e, l1, 64) : ~0ull;
-                const unsigned long long e2 = l2 >= 0 ? __shfl(e, l2, 64) : ~0ull;
-                bestDist = l1 >= 0 ? (int)(e1 >> 32) : INT_MAX;
-                bestIdx2 = l1 >= 0 ? (int)(e1 & 0xFFFFF) : -1;
-                bestDist2 = l2 >= 0 ? (int)(e2 >> 32) : INT_MAX;
-            } else {
-                const float px = prev[(size_t)i1 * prev_stride], py = prev[(size_t)i1 * prev_stride + 1];
-                const Window w = make_window(g, px, py, (float)window);
-                uint32_t qd[8];
-                const uint32_t *qp = (const uint32_t *)(d1 + (size_t)i1 * 32);
+        const int t = lane < cn ? topn[c0 + lane] : -1;
+        S.chunkn[c & 1][lane] = t;
+        if (__ballot(t > 0) == 0ull) return;
+        unsigned long long e[ORBG_MATCH_TOPK];
 #pragma unroll
-                for (int k = 0; k < 8; k++) qd[k] = qp[k];
-                rescan(k2, d2, n2, g, w, qd, S.mdist, &bestDist, &bestDist2, &bestIdx2);
-            }
-            if (bestDist <= TH_LOW && bestDist < (float)bestDist2 * nnratio) {
-                // all lanes hold identical values; lane 0 updates the sequential state
+        for (int u = 0; u < ORBG_MATCH_TOPK; u++) {
+            const int i = u * 64 + lane;
+            e[u] = i < cn * ORBG_MATCH_TOPK ? topk[(size_t)c0 * ORBG_MATCH_TOPK + i] : ~0ull;
+        }
+#pragma unroll
+        for (int u = 0; u < ORBG_MATCH_TOPK; u++) S.chunk[c & 1][u * 64 + lane] = e[u];
+    };
+    if (wv == 1) prefetch(0);
+    __syncthreads();
+    const int nchunks = (n1 + RESOLVE_CHUNK - 1) / RESOLVE_CHUNK;
+    for (int c = 0; c < nchunks; c++) {
+        if (wv == 1) {
+            prefetch(c + 1);
+        } else {
+            const int c0 = c * RESOLVE_CHUNK, cn = min(RESOLVE_CHUNK, n1 - c0);
+            const int *cnt = S.chunkn[c & 1];
+            const unsigned long long *lists = S.chunk[c & 1];
+            int qi = 0;
+            while (qi < cn) {
+                int q = qi, fb = 0;
                 if (lane == 0) {
-                    const int old = S.m21[bestIdx2];
-                    if (old >= 0) {
-                        m12[old] = -1;
-                        nmatches--;
-                    }
-                    m12[i1] = bestIdx2;
-                    S.m21[bestIdx2] = i1;
-                    S.mdist[bestIdx2] = bestDist;
-                    nmatches++;
-                    if (check_ori) {
-                        float rot = k1[i1].angle - k2[bestIdx2].angle;
-                        if (rot < 0.0f) rot += 360.0f;
-                        int bin = (int)roundf(rot * factor);
-                        if (bin == HISTO_LENGTH) bin = 0;
-                        S.hbin[i1] = (int8_t)bin;
-                        S.hsize[bin]++;
+                    for (; q < cn; q++) {
+                        const int total = cnt[q];
+                        if (total <= 0) continue;  // octave > 0 (-1) or empty window (0)
+                        const int kk = min(total, ORBG_MATCH_TOPK);
+                        const unsigned long long *lst = &lists[q * ORBG_MATCH_TOPK];
+                        // first three entries and their filter state in flight together
+                        const unsigned long long e0 = lst[0], e1 = lst[1], e2 = lst[2];
+                        const int md0 = S.mdist[(int)(e0 & 0xFFFFF)];
+                        const int md1 = S.mdist[(int)(e1 & 0xFFFFF)];
+                        const int md2 = S.mdist[(int)(e2 & 0xFFFFF)];
+                        int found = 0, bd = INT_MAX, bd2 = INT_MAX, bi = -1;
+                        const unsigned long long ev[3] = {e0, e1, e2};
+                        const int mv[3] = {md0, md1, md2};
+#pragma unroll
+                        for (int k = 0; k < 3; k++) {
+                            if (k < kk && found < 2) {
+                                const int d = (int)(ev[k] >> 32);
+                                if (!(mv[k] <= d)) {
+                                    if (found == 0) {
+                                        bd = d;
+                                        bi = (int)(ev[k] & 0xFFFFF);
+                                    } else {
+                                        bd2 = d;
+                                    }
+                                    found++;
+                                }
+                            }
+                        }
+                        for (int k = 3; k < kk && found < 2; k++) {
+                            const unsigned long long e = lst[k];
+                            const int d = (int)(e >> 32), i2 = (int)(e & 0xFFFFF);
+                            if (!(S.mdist[i2] <= d)) {
+                                if (found == 0) {
+                                    bd = d;
+                                    bi = i2;
+                                } else {
+                                    bd2 = d;
+                                }
+                                found++;
+                            }
+                        }
+                        if (found < 2 && total > ORBG_MATCH_TOPK) {
+                            fb = 1;  // the sorted K-list cannot decide: exact rescan
+                            break;
+                        }
+                        apply(c0 + q, bd, bd2, bi);
                     }
                 }
-                __syncthreads();
+                q = __shfl(q, 0, 64);
+                fb = __shfl(fb, 0, 64);
+                wave_sync_lds();
+                qi = q;
+                if (fb) {
+                    const int i1 = c0 + qi;
+                    const float px = prev[(size_t)i1 * prev_stride];
+                    const float py = prev[(size_t)i1 * prev_stride + 1];
+                    const Window w = make_window(g, px, py, (float)window);
+                    uint32_t qd[8];
+                    const uint32_t *qp = (const uint32_t *)(d1 + (size_t)i1 * 32);
+#pragma unroll
+                    for (int k = 0; k < 8; k++) qd[k] = qp[k];
+                    int bestDist, bestDist2, bestIdx2;
+                    rescan(k2, d2, n2, g, w, qd, S.mdist, &bestDist, &bestDist2, &bestIdx2);
+                    if (lane == 0) apply(i1, bestDist, bestDist2, bestIdx2);
+                    wave_sync_lds();
+                    qi++;
+                }
             }
         }
         __syncthreads();
     }
-    nmatches = __shfl(nmatches, 0, 64);
+    int nmatches = S.nm;
     if (check_ori) {
-        __syncthreads();
         __shared__ int ind[3];
-        if (lane == 0) {
+        if (tid == 0) {
             // ComputeThreeMaxima (:1800-1841)
             int max1 = 0, max2 = 0, max3 = 0, ind1 = -1, ind2 = -1, ind3 = -1;
             for (int i = 0; i < HISTO_LENGTH; i++) {
@@ -459,42 +554,46 @@ __device__ void init_resolve_wave(ResolveShared &S, const orbg_keypoint *__restr
         }
         __syncthreads();
         int removed = 0;
-        for (int i = lane; i < n1; i += 64) {
+        for (int i = tid; i < n1; i += RESOLVE_T) {
             const int bn = S.hbin[i];
             if (bn < 0 || bn == ind[0] || bn == ind[1] || bn == ind[2]) continue;
-            if (m12[i] >= 0) {
-                m12[i] = -1;
+            if (S.m12[i] >= 0) {
+                S.m12[i] = -1;
                 removed++;
             }
         }
         removed = wave_isum(removed);
-        nmatches -= removed;
+        __shared__ int rem2[2];
+        if (lane == 0) rem2[wv] = removed;
+        __syncthreads();
+        nmatches -= rem2[0] + rem2[1];
     }
     __syncthreads();
+    for (int i = tid; i < n1; i += RESOLVE_T) m12[i] = S.m12[i];
     if (prev_out) {
-        for (int i = lane; i < n1; i += 64) {
-            const int j = m12[i];
+        for (int i = tid; i < n1; i += RESOLVE_T) {
+            const int j = S.m12[i];
             if (j >= 0) {
                 prev_out[2 * i] = k2[j].x;
                 prev_out[2 * i + 1] = k2[j].y;
             }
         }
     }
-    if (lane == 0) *nm_out = nmatches;
+    if (tid == 0) *nm_out = nmatches;
 }
 
-__global__ __launch_bounds__(64) void k_init_resolve_single(
+__global__ __launch_bounds__(RESOLVE_T) void k_init_resolve_single(
     const orbg_keypoint *k1, const uint8_t *d1, int n1, const orbg_keypoint *k2,
     const uint8_t *d2, int n2, orbg_bounds b, float *prev, int window, float nnratio,
     int check_ori, const unsigned long long *topk, const int32_t *topn, int32_t *m12,
     int32_t *nm)
 {
     __shared__ ResolveShared S;
-    init_resolve_wave(S, k1, d1, n1, k2, d2, n2, b, prev, 2, window, nnratio, check_ori, topk,
-                      topn, m12, nm, prev);
+    init_resolve_block(S, k1, d1, n1, k2, d2, n2, b, prev, 2, window, nnratio, check_ori, topk,
+                       topn, m12, nm, prev);
 }
 
-__global__ __launch_bounds__(64) void k_init_resolve_pairs(
+__global__ __launch_bounds__(RESOLVE_T) void k_init_resolve_pairs(
     const orbg_keypoint *kps, const uint8_t *desc, const int32_t *counts, int fc,
     const int32_t *f1, const int32_t *f2, int w, int h, int window, float nnratio,
     int check_ori, const unsigned long long *topk, const int32_t *topn, int32_t *m12,
@@ -505,7 +604,7 @@ __global__ __launch_bounds__(64) void k_init_resolve_pairs(
     const int a = f1[p], c = f2[p];
     const orbg_keypoint *k1 = kps + (size_t)a * fc;
     orbg_bounds b{0.f, (float)w, 0.f, (float)h};
-    init_resolve_wave(S, k1, desc + (size_t)a * fc * 32, counts[a], kps + (size_t)c * fc,
+    init_resolve_block(S, k1, desc + (size_t)a * fc * 32, counts[a], kps + (size_t)c * fc,
                       desc + (size_t)c * fc * 32, counts[c], b, (const float *)k1,
                       (int)(sizeof(orbg_keypoint) / sizeof(float)), window, nnratio, check_ori,
                       topk + (size_t)p * fc * ORBG_MATCH_TOPK, topn + (size_t)p * fc,
@@ -547,7 +646,7 @@ int launch_match_pairs(hipStream_t st, const uint8_t *desc, const orbg_keypoint 
                           dim3(256), 0, st, kps, desc, counts, fc, d_f1, d_f2, w, h, window,
                           (unsigned long long *)topk, topk_n));
     PL(prof, st, "init_resolve",
-       hipLaunchKernelGGL(k_init_resolve_pairs, dim3(npairs), dim3(64), 0, st, kps, desc, counts,
+       hipLaunchKernelGGL(k_init_resolve_pairs, dim3(npairs), dim3(RESOLVE_T), 0, st, kps, desc, counts,
                           fc, d_f1, d_f2, w, h, window, nnratio, check_ori,
                           (const unsigned long long *)topk, topk_n, m12, nm));
     return hipGetLastError() == hipSuccess ? ORBG_OK : ORBG_EIO;
@@ -564,7 +663,7 @@ int launch_init_match_single(hipStream_t st, const orbg_keypoint *k1, const uint
                           dim3(256), 0, st, k1, d1, n1, k2, d2, n2, b, prev, window,
                           (unsigned long long *)topk, topk_n));
     PL(prof, st, "init_resolve",
-       hipLaunchKernelGGL(k_init_resolve_single, dim3(1), dim3(64), 0, st, k1, d1, n1, k2, d2, n2,
+       hipLaunchKernelGGL(k_init_resolve_single, dim3(1), dim3(RESOLVE_T), 0, st, k1, d1, n1, k2, d2, n2,
                           b, prev, window, nnratio, check_ori, (const unsigned long long *)topk,
                           topk_n, m12, nm));
     return hipGetLastError() == hipSuccess ? ORBG_OK : ORBG_EIO;

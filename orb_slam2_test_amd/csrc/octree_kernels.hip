@@ -1,0 +1,581 @@
+// octree_kernels.hip -- DistributeOctTree (ORBextractor.cc:668-951) on gfx950, LDS version.
+//
+// k_octree_lds handles every (frame, level) with <= OCT_KEY_CAP FAST candidates; levels
+// with more fall back to k_octree (extract_kernels.hip, global-memory key scans).
+//
+// Every candidate's quadtree path is a 32-bit code: root index (4 bits, :705-724) then 14
+// quadrant digits (n1=0, n2=1, n3=2, n4=3) computed with DivideNode's boundaries
+// (:539-594).  (code, candidate index) pairs are sorted in LDS, so a node of depth d is a
+// contiguous range whose children split at digit d: a split is three binary searches
+// and no pass touches individual keys.  The std::list is an array of u64 node records
+// {lo:16 | cnt:16 | seq:16 | depth:8} rebuilt every pass with the reference's
+// push_front/erase order; seq = creation order = the pinned pointer tie-break of the
+// sort at :869.  The best key of a node (:932-948) is the max of (response << 24 |
+// ~index) over its range: max response, then lowest candidate index.
+#include <hip/hip_runtime.h>
+
+#include "orbg_device.h"
+#include "orbg_internal.h"
+
+#pragma clang fp contract(off)
+
+namespace orbg {
+
+#define OCT_T 512
+#define OCT_CODE_DEPTH 14
+
+#define OCT_NBUCKET 16384  // counting-sort buckets: root (4 bits) + first 5 quadtree digits
+#define OCT_BSHIFT 18
+
+struct OctLdsShared {
+    uint32_t codes[OCT_KEY_CAP];
+    uint16_t sidx[OCT_KEY_CAP];
+    union {
+        uint32_t bcnt[OCT_NBUCKET / 2];  // two u16 bucket counters per word
+        struct {
+            unsigned long long list[2][ORBG_OCT_ALIVE];
+            unsigned long long sortv[ORBG_OCT_ALIVE];
+        } q;
+    } u;
+    uint16_t aux[ORBG_OCT_ALIVE];
+    int red[16];
+    int rootlo[20];
+    int s_alive, s_cur, s_seq, s_vbase, s_vend, s_err, s_nproc, s_phase2;
+};
+
+__device__ __forceinline__ unsigned long long rec_make(int lo, int cnt, int seq, int depth)
+{
+    return (unsigned long long)(uint32_t)lo | ((unsigned long long)(uint32_t)cnt << 16) |
+           ((unsigned long long)(uint32_t)seq << 32) | ((unsigned long long)(uint32_t)depth << 48);
+}
+__device__ __forceinline__ int rec_lo(unsigned long long r) { return (int)(r & 0xFFFF); }
+__device__ __forceinline__ int rec_cnt(unsigned long long r) { return (int)((r >> 16) & 0xFFFF); }
+__device__ __forceinline__ int rec_seq(unsigned long long r) { return (int)((r >> 32) & 0xFFFF); }
+__device__ __forceinline__ int rec_depth(unsigned long long r) { return (int)((r >> 48) & 0xFF); }
+
+// exclusive block scan for OCT_T threads (8 waves); sh: 16 ints; two barriers
+__device__ int oct_scan(int v, int *total, int *sh)
+{
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    int x = wave_incl_scan(v);
+    if (lane == 63) sh[wid] = x;
+    __syncthreads();
+    int before = 0, tot = 0;
+#pragma unroll
+    for (int i = 0; i < OCT_T / 64; i++) {
+        const int s = sh[i];
+        before += (i < wid) ? s : 0;
+        tot += s;
+    }
+    __syncthreads();
+    *total = tot;
+    return before + x - v;
+}
+
+// In-place ascending sort of u64 v[0..n) without padding (flip bitonic; virtual +inf
+// entries at [n, pw) never move, so comparators touching them are skipped).
+__device__ void flip_bitonic_u64(unsigned long long *v, int n)
+{
+    int pw = 1;
+    while (pw < n) pw <<= 1;
+    const int half = pw >> 1;
+    for (int k = 2; k <= pw; k <<= 1) {
+        const int lhk = __builtin_ctz(k) - 1;
+        for (int i = threadIdx.x; i < half; i += OCT_T) {
+            const int blk = i >> lhk, r = i & ((k >> 1) - 1);
+            const int a = blk * k + r, b = blk * k + k - 1 - r;
+            if (b < n) {
+                const unsigned long long x = v[a], y = v[b];
+                if (x > y) {
+                    v[a] = y;
+                    v[b] = x;
+                }
+            }
+        }
+        __syncthreads();
+        for (int j = k >> 2; j > 0; j >>= 1) {
+            const int lj = __builtin_ctz(j);
+            for (int i = threadIdx.x; i < half; i += OCT_T) {
+                const int a = ((i >> lj) << (lj + 1)) + (i & (j - 1)), b = a + j;
+                if (b < n) {
+                    const unsigned long long x = v[a], y = v[b];
+                    if (x > y) {
+                        v[a] = y;
+                        v[b] = x;
+                    }
+                }
+            }
+            __syncthreads();
+        }
+    }
+}
+
+// children of the node record r: child start offsets b[0..4] (b[0] = lo, b[4] = lo + cnt)
+__device__ __forceinline__ void oct_children(const uint32_t *codes, unsigned long long r,
+                                             int b[5])
+{
+    const int lo = rec_lo(r), hi = lo + rec_cnt(r), d = rec_depth(r);
+    const int shift = 26 - 2 * d;
+    b[0] = lo;
+    b[4] = hi;
+#pragma unroll
+    for (int q = 1; q < 4; q++) {
+        int a = b[q - 1], z = hi;  // first index in [a, z) with digit >= q
+        while (a < z) {
+            const int m = (a + z) >> 1;
+            if ((int)((codes[m] >> shift) & 3) < q)
+                a = m + 1;
+            else
+                z = m;
+        }
+        b[q] = a;
+    }
+}
+
+__global__ __launch_bounds__(OCT_T) void k_octree_lds(
+    const OrbgGeom *__restrict__ g, const int32_t *__restrict__ cell_cnt,
+    const uint2 *__restrict__ cell_kp, uint32_t *__restrict__ keys_all,
+    uint32_t *__restrict__ scratch_all, uint32_t *__restrict__ lvl_kp,
+    int32_t *__restrict__ lvl_cnt, int32_t *__restrict__ err_flag)
+{
+    __shared__ OctLdsShared S;
+    const int l = blockIdx.x, f = blockIdx.y, tid = threadIdx.x;
+    const OrbgLevel &lv = g->lv[l];
+    const int64_t kbase = (int64_t)f * g->keys_frame + lv.key_off;
+    uint32_t *kglob = keys_all + kbase;
+    uint2 *pairs = (uint2 *)(scratch_all + 2 * kbase);  // 2 words per candidate
+    const int N = lv.nfeat, nIni = lv.nini;
+
+    // ---- candidate count; larger levels (or > ALIVE-1 cells) belong to k_octree ----
+    const int32_t *ccount = cell_cnt + (int64_t)f * g->ncells + lv.cell_base;
+    const uint2 *ckp = cell_kp + ((int64_t)f * g->ncells + lv.cell_base) * g->cell_cap;
+    const int ncells = lv.ncells;
+    if (ncells + 1 > ORBG_OCT_ALIVE) return;
+    int n = 0;
+    for (int c0 = 0; c0 < ncells; c0 += OCT_T) {
+        const int c = c0 + tid;
+        int tot;
+        const int off = oct_scan(c < ncells ? ccount[c] : 0, &tot, S.red) + n;
+        if (c < ncells) S.aux[c] = (uint16_t)min(off, 65535);
+        n += tot;
+    }
+    if (n > OCT_KEY_CAP) return;
+    if (tid == 0) S.aux[ncells] = (uint16_t)n;
+    for (int i = tid; i < OCT_NBUCKET / 2; i += OCT_T) S.u.bcnt[i] = 0;
+    __syncthreads();
+
+    // flattened candidate k -> (cell, slot): largest c with cell_offset[c] <= k
+    auto cell_of = [&](int k) -> int {
+        int lo = 0, hi = ncells - 1;
+        while (lo < hi) {
+            const int mid = (lo + hi + 1) >> 1;
+            if ((int)S.aux[mid] <= k)
+                lo = mid;
+            else
+                hi = mid - 1;
+        }
+        return lo;
+    };
+    // ---- gather (vToDistributeKeys order) + bucket histogram ----
+    for (int k0 = tid; k0 < n; k0 += 4 * OCT_T) {
+        uint2 e[4];
+        int cc[4];
+#pragma unroll
+        for (int u = 0; u < 4; u++) {
+            const int k = k0 + u * OCT_T;
+            cc[u] = k < n ? cell_of(k) : 0;
+        }
+#pragma unroll
+        for (int u = 0; u < 4; u++) {
+            const int k = k0 + u * OCT_T;
+            e[u] = k < n ? ckp[(int64_t)cc[u] * g->cell_cap + (k - S.aux[cc[u]])] : make_uint2(0, 0);
+        }
+#pragma unroll
+        for (int u = 0; u < 4; u++) {
+            const int k = k0 + u * OCT_T;
+            if (k < n) {
+                kglob[k] = e[u].x;
+                const uint32_t b = e[u].y >> OCT_BSHIFT;
+                atomicAdd(&S.u.bcnt[b >> 1], 1u << (16 * (b & 1)));
+            }
+        }
+    }
+    __syncthreads();
+    if (g->dbg == 1) return;
+    // ---- exclusive scan of the 16384 u16 bucket counters (32 per thread) ----
+    {
+        constexpr int PER = OCT_NBUCKET / 2 / OCT_T;  // words per thread
+        uint32_t w[PER];
+        int sum = 0;
+#pragma unroll
+        for (int i = 0; i < PER; i++) {
+            w[i] = S.u.bcnt[tid * PER + i];
+            sum += (int)(w[i] & 0xFFFF) + (int)(w[i] >> 16);
+        }
+        int tot;
+        int run = oct_scan(sum, &tot, S.red);
+#pragma unroll
+        for (int i = 0; i < PER; i++) {
+            const int a = (int)(w[i] & 0xFFFF), b = (int)(w[i] >> 16);
+            S.u.bcnt[tid * PER + i] = (uint32_t)run | ((uint32_t)(run + a) << 16);
+            run += a + b;
+        }
+    }
+    __syncthreads();
+    // ---- scatter into bucket order (unordered inside a bucket) ----
+    for (int k0 = tid; k0 < n; k0 += 4 * OCT_T) {
+        uint2 e[4];
+        int cc[4];
+#pragma unroll
+        for (int u = 0; u < 4; u++) {
+            const int k = k0 + u * OCT_T;
+            cc[u] = k < n ? cell_of(k) : 0;
+        }
+#pragma unroll
+        for (int u = 0; u < 4; u++) {
+            const int k = k0 + u * OCT_T;
+            e[u] = k < n ? ckp[(int64_t)cc[u] * g->cell_cap + (k - S.aux[cc[u]])] : make_uint2(0, 0);
+        }
+#pragma unroll
+        for (int u = 0; u < 4; u++) {
+            const int k = k0 + u * OCT_T;
+            if (k < n) {
+                const uint32_t b = e[u].y >> OCT_BSHIFT;
+                const uint32_t old = atomicAdd(&S.u.bcnt[b >> 1], 1u << (16 * (b & 1)));
+                const int slot = (int)((old >> (16 * (b & 1))) & 0xFFFF);
+                S.codes[slot] = e[u].y;
+                S.sidx[slot] = (uint16_t)k;
+            }
+        }
+    }
+    __syncthreads();
+    // ---- order inside each bucket: rank of every key among its bucket (a bucket spans
+    //      ~1/32 x 1/32 of a root, so it holds few keys), written through global scratch ----
+    auto bucket_end = [&](int b) -> int {
+        return b < 0 ? 0 : (int)((S.u.bcnt[b >> 1] >> (16 * (b & 1))) & 0xFFFF);
+    };
+    for (int p0 = tid; p0 < n; p0 += 4 * OCT_T) {
+        uint32_t c[4], v[4];
+        int lo[4], hi[4];
+#pragma unroll
+        for (int u = 0; u < 4; u++) {
+            const int p = p0 + u * OCT_T;
+            c[u] = p < n ? S.codes[p] : 0;
+            v[u] = p < n ? S.sidx[p] : 0;
+            const int b = (int)(c[u] >> OCT_BSHIFT);
+            lo[u] = p < n ? bucket_end(b - 1) : 0;
+            hi[u] = p < n ? bucket_end(b) : 0;
+        }
+#pragma unroll
+        for (int u = 0; u < 4; u++) {
+            int rank = 0;
+            for (int q = lo[u]; q < hi[u]; q++) rank += S.codes[q] < c[u];
+            if (p0 + u * OCT_T < n) pairs[lo[u] + rank] = make_uint2(c[u], v[u]);
+        }
+    }
+    __syncthreads();
+    for (int p0 = tid; p0 < n; p0 += 4 * OCT_T) {
+        uint2 e[4];
+#pragma unroll
+        for (int u = 0; u < 4; u++) e[u] = p0 + u * OCT_T < n ? pairs[p0 + u * OCT_T] : make_uint2(0, 0);
+#pragma unroll
+        for (int u = 0; u < 4; u++)
+            if (p0 + u * OCT_T < n) {
+                S.codes[p0 + u * OCT_T] = e[u].x;
+                S.sidx[p0 + u * OCT_T] = (uint16_t)e[u].y;
+            }
+    }
+    __syncthreads();
+    if (g->dbg == 2) return;
+
+    // ---- roots (:705-739): contiguous by the top 4 code bits ----
+    if (tid <= nIni) S.rootlo[tid] = 0;
+    __syncthreads();
+    for (int i = tid; i < n; i += OCT_T) {
+        const int r = (int)(S.codes[i] >> 28);
+        const int rp = i > 0 ? (int)(S.codes[i - 1] >> 28) : -1;
+        if (r != rp)
+            for (int q = rp + 1; q <= r; q++) S.rootlo[q] = i;
+    }
+    if (tid == 0) {
+        const int rl = n > 0 ? (int)(S.codes[n - 1] >> 28) : -1;
+        for (int q = rl + 1; q <= nIni; q++) S.rootlo[q] = n;
+    }
+    __syncthreads();
+    if (tid == 0) {
+        int a = 0;
+        for (int r = 0; r < nIni; r++) {
+            const int cnt = S.rootlo[r + 1] - S.rootlo[r];
+            if (cnt > 0) S.u.q.list[0][a++] = rec_make(S.rootlo[r], cnt, 0, 0);
+        }
+        S.s_alive = a;
+        S.s_cur = 0;
+        S.s_seq = 1;  // roots never enter vSizeAndPointerToNode
+        S.s_err = 0;
+        S.s_phase2 = 0;
+    }
+    __syncthreads();
+
+    // ================= phase 1 passes (:751-852) =================
+    while (true) {
+        const int alive = S.s_alive, cur = S.s_cur, nxt = cur ^ 1, seq0 = S.s_seq;
+        // sweep 1: children of every splitting node (kept in registers for sweep 2)
+        constexpr int MAXCH = ORBG_OCT_ALIVE / OCT_T;
+        int bb[MAXCH][5];
+        int ee[MAXCH], spp[MAXCH];
+        int tot_e = 0, nexp = 0;
+#pragma unroll
+        for (int ch = 0; ch < MAXCH; ch++) {
+            const int i = ch * OCT_T + tid;
+            int e = 0, m = 0, sp = 0;
+#pragma unroll
+            for (int q = 0; q < 5; q++) bb[ch][q] = 0;
+            if (ch * OCT_T < alive) {
+                if (i < alive) {
+                    const unsigned long long r = S.u.q.list[cur][i];
+                    if (rec_cnt(r) > 1) {
+                        if (rec_depth(r) >= OCT_CODE_DEPTH) {
+                            S.s_err = 4;
+                        } else {
+                            sp = 1;
+                            oct_children(S.codes, r, bb[ch]);
+#pragma unroll
+                            for (int q = 0; q < 4; q++) {
+                                e += bb[ch][q + 1] > bb[ch][q];
+                                m += bb[ch][q + 1] - bb[ch][q] > 1;
+                            }
+                        }
+                    }
+                }
+                int t1, t2;
+                oct_scan(e, &t1, S.red);
+                oct_scan(m, &t2, S.red);
+                tot_e += t1;
+                nexp += t2;
+            }
+            ee[ch] = e;
+            spp[ch] = sp;
+        }
+        int nsplit_total = 0;
+        // sweep 2: place children (reverse parent order, n4..n1) and the untouched nodes
+        {
+            int run = 0;
+#pragma unroll
+            for (int ch = 0; ch < MAXCH; ch++) {
+                if (ch * OCT_T >= alive) break;
+                const int i = ch * OCT_T + tid;
+                const int e = ee[ch], sp = spp[ch];
+                int tot;
+                const int pre = oct_scan(e | (sp << 16), &tot, S.red) + run;
+                const int E = pre & 0xFFFF, splits_before = pre >> 16;
+                if (i < alive) {
+                    const unsigned long long r = S.u.q.list[cur][i];
+                    if (sp) {
+                        const int blk = tot_e - E - e;
+                        int k = 0;
+#pragma unroll
+                        for (int q = 0; q < 4; q++) {
+                            const int cnt = bb[ch][q + 1] - bb[ch][q];
+                            if (cnt == 0) continue;
+                            S.u.q.list[nxt][blk + (e - 1 - k)] =
+                                rec_make(bb[ch][q], cnt, seq0 + E + k, rec_depth(r) + 1);
+                            k++;
+                        }
+                    } else {
+                        S.u.q.list[nxt][tot_e + i - splits_before] = r;
+                    }
+                }
+                run += tot;
+            }
+            nsplit_total = run >> 16;
+        }
+        const int na = tot_e + alive - nsplit_total;
+        __syncthreads();
+        if (tid == 0) {
+            S.s_alive = na;
+            S.s_cur = nxt;
+            S.s_seq = seq0 + tot_e;
+            S.s_vbase = seq0;
+            S.s_vend = seq0 + tot_e;
+            if (na > ORBG_OCT_ALIVE || seq0 + tot_e > 65535) S.s_err = 5;
+        }
+        __syncthreads();
+        if (S.s_err) break;
+        if (na >= N || na == alive) break;   // :849-852
+        if (na + nexp * 3 > N) {              // :856
+            if (tid == 0) S.s_phase2 = 1;
+            __syncthreads();
+            break;
+        }
+    }
+
+    // ================= phase 2 rounds (:859-924) =================
+    if (S.s_phase2 && !S.s_err) {
+        while (true) {
+            const int alive = S.s_alive, cur = S.s_cur, nxt = cur ^ 1, seq0 = S.s_seq;
+            const int vbase = S.s_vbase, vend = S.s_vend;
+            // vPrevSizeAndPointerToNode: multi-key nodes created last round -> (cnt, seq, pos)
+            int np = 0;
+            for (int i0 = 0; i0 < alive; i0 += OCT_T) {
+                const int i = i0 + tid;
+                int fl = 0;
+                unsigned long long r = 0;
+                if (i < alive) {
+                    r = S.u.q.list[cur][i];
+                    const int sq = rec_seq(r);
+                    fl = rec_cnt(r) > 1 && sq >= vbase && sq < vend;
+                }
+                int tot;
+                const int o = oct_scan(fl, &tot, S.red) + np;
+                if (fl)
+                    S.u.q.sortv[o] = ((unsigned long long)rec_cnt(r) << 32) |
+                                 ((unsigned long long)rec_seq(r) << 16) | (unsigned)i;
+                np += tot;
+            }
+            for (int i = tid; i < alive; i += OCT_T) S.aux[i] = 0;
+            __syncthreads();
+            flip_bitonic_u64(S.u.q.sortv, np);
+            // processing order p = largest (cnt, seq) first (:872); cut at the first p with
+            // alive + sum_{p' <= p} (children - 1) >= N (:917-918)
+            if (tid == 0) S.s_nproc = np;
+            __syncthreads();
+            {
+                int run = 0;
+                for (int p0 = 0; p0 < np; p0 += OCT_T) {
+                    const int p = p0 + tid;
+                    int dl = 0;
+                    if (p < np) {
+                        const int pos = (int)(S.u.q.sortv[np - 1 - p] & 0xFFFF);
+                        const unsigned long long r = S.u.q.list[cur][pos];
+                        if (rec_depth(r) >= OCT_CODE_DEPTH) S.s_err = 6;
+                        int b[5];
+                        oct_children(S.codes, r, b);
+                        int e = 0;
+#pragma unroll
+                        for (int q = 0; q < 4; q++) e += b[q + 1] > b[q];
+                        dl = e - 1;
+                    }
+                    int tot;
+                    const int incl = oct_scan(dl, &tot, S.red) + run + dl;
+                    if (p < np && alive + incl >= N) atomicMin(&S.s_nproc, p + 1);
+                    run += tot;
+                }
+            }
+            __syncthreads();
+            const int nproc = S.s_nproc;
+            // children of processed parents (creation order = processing order)
+            int tot_e = 0;
+            for (int p0 = 0; p0 < nproc; p0 += OCT_T) {
+                const int p = p0 + tid;
+                int e = 0;
+                if (p < nproc) {
+                    const int pos = (int)(S.u.q.sortv[np - 1 - p] & 0xFFFF);
+                    int b[5];
+                    oct_children(S.codes, S.u.q.list[cur][pos], b);
+#pragma unroll
+                    for (int q = 0; q < 4; q++) e += b[q + 1] > b[q];
+                    S.aux[pos] = 1;  // processed parent
+                }
+                int t;
+                oct_scan(e, &t, S.red);
+                tot_e += t;
+            }
+            {
+                int run = 0;
+                for (int p0 = 0; p0 < nproc; p0 += OCT_T) {
+                    const int p = p0 + tid;
+                    int e = 0, b[5] = {0, 0, 0, 0, 0};
+                    unsigned long long r = 0;
+                    if (p < nproc) {
+                        const int pos = (int)(S.u.q.sortv[np - 1 - p] & 0xFFFF);
+                        r = S.u.q.list[cur][pos];
+                        oct_children(S.codes, r, b);
+#pragma unroll
+                        for (int q = 0; q < 4; q++) e += b[q + 1] > b[q];
+                    }
+                    int tot;
+                    const int E = oct_scan(e, &tot, S.red) + run;
+                    if (p < nproc) {
+                        const int blk = tot_e - E - e;
+                        int k = 0;
+#pragma unroll
+                        for (int q = 0; q < 4; q++) {
+                            const int cnt = b[q + 1] - b[q];
+                            if (cnt == 0) continue;
+                            S.u.q.list[nxt][blk + (e - 1 - k)] =
+                                rec_make(b[q], cnt, seq0 + E + k, rec_depth(r) + 1);
+                            k++;
+                        }
+                    }
+                    run += tot;
+                }
+                int runp = 0;
+                for (int i0 = 0; i0 < alive; i0 += OCT_T) {
+                    const int i = i0 + tid;
+                    const int fl = (i < alive) ? (int)S.aux[i] : 0;
+                    int tot;
+                    const int before = oct_scan(fl, &tot, S.red) + runp;
+                    if (i < alive && !fl) S.u.q.list[nxt][tot_e + i - before] = S.u.q.list[cur][i];
+                    runp += tot;
+                }
+            }
+            const int na = tot_e + alive - nproc;
+            __syncthreads();
+            if (tid == 0) {
+                S.s_alive = na;
+                S.s_cur = nxt;
+                S.s_seq = seq0 + tot_e;
+                S.s_vbase = seq0;
+                S.s_vend = seq0 + tot_e;
+                if (na > ORBG_OCT_ALIVE || seq0 + tot_e > 65535) S.s_err = 7;
+            }
+            __syncthreads();
+            if (S.s_err) break;
+            if (na >= N || na == alive) break;  // :921-922
+        }
+    }
+
+    // ================= best key per node, list order (:932-948) =================
+    const int alive = S.s_alive, cur = S.s_cur;
+    if (S.s_err) {
+        if (tid == 0) {
+            atomicOr(err_flag, 1 << S.s_err);
+            lvl_cnt[(int64_t)f * g->L + l] = 0;
+        }
+        return;
+    }
+    // label every sorted position with its node's list position, then one flat pass
+    uint32_t *best = (uint32_t *)S.u.q.sortv;
+    for (int i = tid; i < alive; i += OCT_T) {
+        const unsigned long long r = S.u.q.list[cur][i];
+        const int lo = rec_lo(r), cnt = rec_cnt(r);
+        for (int p = lo; p < lo + cnt; p++) S.codes[p] = (uint32_t)i;
+        best[i] = 0;
+    }
+    __syncthreads();
+    for (int p0 = tid; p0 < n; p0 += 4 * OCT_T) {
+        uint32_t key[4], pos[4], idx[4];
+#pragma unroll
+        for (int u = 0; u < 4; u++) {
+            const int p = p0 + u * OCT_T;
+            idx[u] = p < n ? S.sidx[p] : 0;
+            pos[u] = p < n ? S.codes[p] : 0;
+        }
+#pragma unroll
+        for (int u = 0; u < 4; u++) key[u] = kglob[idx[u]];
+#pragma unroll
+        for (int u = 0; u < 4; u++)
+            if (p0 + u * OCT_T < n)
+                atomicMax(&best[pos[u]], ((uint32_t)orbg_ps(key[u]) << 24) | (0xFFFFFFu - idx[u]));
+    }
+    __syncthreads();
+    uint32_t *out = lvl_kp + (int64_t)f * g->out_frame + lv.out_off;
+    const int nout = min(alive, lv.out_cap);
+    for (int i = tid; i < nout; i += OCT_T) out[i] = kglob[0xFFFFFFu - (best[i] & 0xFFFFFFu)];
+    if (tid == 0) {
+        lvl_cnt[(int64_t)f * g->L + l] = nout;
+        if (alive > lv.out_cap) atomicOr(err_flag, 1 << 8);
+    }
+}
+
+}  // namespace orbg

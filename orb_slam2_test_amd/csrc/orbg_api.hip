@@ -8,6 +8,7 @@
 #include <cmath>
 #include <cstdarg>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <string>
 #include <vector>
@@ -21,12 +22,14 @@ namespace orbg {
 __global__ void k_resize(const uint8_t *, int64_t, int, int, uint8_t *, int64_t, int, int, int,
                          const int2 *, const int2 *, int);
 __global__ void k_fast_cells(const OrbgGeom *, const OrbgCell *, const uint8_t *, int64_t, int,
-                             const uint8_t *, int32_t *, uint32_t *);
+                             const uint8_t *, const uint32_t *, int32_t *, uint2 *);
 __global__ void k_blur(const OrbgGeom *, const int32_t *, const uint8_t *, int64_t, int,
                        const uint8_t *, uint8_t *);
-__global__ void k_octree(const OrbgGeom *, const int32_t *, const uint32_t *, uint32_t *,
+__global__ void k_octree(const OrbgGeom *, const int32_t *, const uint2 *, uint32_t *,
                          uint32_t *, uint32_t *, uint8_t *, int4 *, uint32_t *, int32_t *,
                          int32_t *);
+__global__ void k_octree_lds(const OrbgGeom *, const int32_t *, const uint2 *, uint32_t *,
+                             uint32_t *, uint32_t *, int32_t *, int32_t *);
 struct OrbgKeypointDev;
 __global__ void k_orient_desc(const OrbgGeom *, const uint8_t *, int64_t, int, const uint8_t *,
                               const uint8_t *, const uint32_t *, const int32_t *,
@@ -174,11 +177,12 @@ struct orbg_ctx {
     OrbgCell *d_cells = nullptr;
     int32_t *d_tile_base = nullptr;
     int2 *d_rtab = nullptr;
+    uint32_t *d_ctab = nullptr;  // quadtree path-code tables (xs | ys per level)
     uint8_t *d_img = nullptr;
     size_t img_bytes = 0;
     uint8_t *d_pyr = nullptr, *d_blur = nullptr;
     int32_t *d_cell_cnt = nullptr;
-    uint32_t *d_cell_kp = nullptr;
+    uint2 *d_cell_kp = nullptr;
     uint32_t *d_keys = nullptr, *d_knode = nullptr, *d_act = nullptr;
     uint8_t *d_qk = nullptr;
     int4 *d_nodes = nullptr;
@@ -268,7 +272,7 @@ static void make_tables(orbg_ctx *c)
 
 static void free_plan(orbg_ctx *c)
 {
-    void *ptrs[] = {c->d_geom, c->d_cells, c->d_tile_base, c->d_rtab, c->d_pyr, c->d_blur,
+    void *ptrs[] = {c->d_geom, c->d_cells, c->d_tile_base, c->d_rtab, c->d_ctab, c->d_pyr, c->d_blur,
                     c->d_cell_cnt, c->d_cell_kp, c->d_keys, c->d_knode, c->d_act, c->d_qk,
                     c->d_nodes, c->d_lvl_kp, c->d_lvl_cnt, c->d_kps, c->d_desc, c->d_counts,
                     c->d_err, c->d_knn, c->d_m12, c->d_nm, c->d_topk, c->d_topk_n, c->d_pairs};
@@ -278,6 +282,7 @@ static void free_plan(orbg_ctx *c)
     c->d_cells = nullptr;
     c->d_tile_base = nullptr;
     c->d_rtab = nullptr;
+    c->d_ctab = nullptr;
     c->d_pyr = c->d_blur = nullptr;
     c->d_cell_cnt = nullptr;
     c->d_cell_kp = nullptr;
@@ -324,10 +329,12 @@ static int plan(orbg_ctx *c, int w, int h, int batch)
     G.ini_th = std::min(std::max(p.ini_th_fast, 0), 255);
     G.min_th = std::min(std::max(p.min_th_fast, 0), 255);
     G.brief_fma = p.brief_fma;
+    G.dbg = getenv("ORBG_DBG") ? atoi(getenv("ORBG_DBG")) : 0;
     for (int i = 0; i < 7; i++) G.gk[i] = p.gauss_k[i];
     for (int i = 0; i < 16; i++) G.umax[i] = c->umax[i];
     std::vector<OrbgCell> cells;
     std::vector<int2> rtab;
+    std::vector<uint32_t> ctab;
     int cell_cap = 1;
     int lw[16], lh[16];
     for (int l = 0; l < G.L; l++) {
@@ -389,10 +396,48 @@ static int plan(orbg_ctx *c, int w, int h, int batch)
         L.nfeat = c->fpl[l];
         const int nini = (int)roundf((float)(L.max_bx - ORBG_MIN_BORDER) /
                                      (L.max_by - ORBG_MIN_BORDER));
-        if (nini <= 0 || nini > 64)
+        if (nini <= 0 || nini > 15)  // 4-bit root index of the quadtree path code
             return set_err(ORBG_ENOTSUP, "level %d aspect gives %d quadtree roots", l, nini);
         L.nini = nini;
         L.hx = (float)(L.max_bx - ORBG_MIN_BORDER) / nini;
+        // Quadtree path codes (DistributeOctTree :705-724 roots, DivideNode :539-594).
+        // A candidate's child at every depth depends on x and y separately: x decides
+        // left/right along the halving of its root's [x0, x1), y top/bottom along
+        // [0, rootH).  code = root << 28 | digit_d << (26 - 2d), digit = right | bottom << 1.
+        {
+            const int wrel = L.max_bx - ORBG_MIN_BORDER, hrel = L.max_by - ORBG_MIN_BORDER;
+            L.xs_off = (int)ctab.size();
+            for (int x = 0; x <= wrel; x++) {
+                const int r = std::min((int)((float)x / L.hx), nini - 1);
+                int x0 = (int)(L.hx * (float)r), x1 = (int)(L.hx * (float)(r + 1));
+                uint32_t code = (uint32_t)r << 28;
+                for (int d = 0; d < 14; d++) {
+                    const int xm = x0 + (int)ceilf((float)(x1 - x0) / 2);
+                    if (x >= xm) {
+                        code |= 1u << (26 - 2 * d);
+                        x0 = xm;
+                    } else {
+                        x1 = xm;
+                    }
+                }
+                ctab.push_back(code);
+            }
+            L.ys_off = (int)ctab.size();
+            for (int y = 0; y <= hrel; y++) {
+                int y0 = 0, y1 = hrel;
+                uint32_t code = 0;
+                for (int d = 0; d < 14; d++) {
+                    const int ym = y0 + (int)ceilf((float)(y1 - y0) / 2);
+                    if (y >= ym) {
+                        code |= 2u << (26 - 2 * d);
+                        y0 = ym;
+                    } else {
+                        y1 = ym;
+                    }
+                }
+                ctab.push_back(code);
+            }
+        }
         L.out_cap = std::max(L.nfeat + 3, 4 * nini + 1);
         if (L.out_cap > ORBG_OCT_ALIVE)
             return set_err(ORBG_ENOTSUP, "level %d wants %d features (> %d)", l, L.nfeat,
@@ -412,7 +457,7 @@ static int plan(orbg_ctx *c, int w, int h, int batch)
         L.blur_off = blur_off;
         blur_off += (int64_t)L.pitch * L.h;
         tile_base.push_back(tiles);
-        tiles += ((L.w + 63) / 64) * ((L.h + 15) / 16);
+        tiles += ((L.w + 127) / 128) * ((L.h + 31) / 32);  // k_blur 128x32 tiles
         // resize coefficient tables (cv::resize, INTER_LINEAR)
         if (l > 0) {
             const int sw = lw[l - 1], sh = lh[l - 1], dw = lw[l], dh = lh[l];
@@ -479,6 +524,7 @@ static int plan(orbg_ctx *c, int w, int h, int batch)
     const size_t B = (size_t)want_batch;
     int rc;
     if ((rc = dalloc(&c->d_geom, 1)) || (rc = dalloc(&c->d_cells, cells.size())) ||
+        (rc = dalloc(&c->d_ctab, ctab.size())) ||
         (rc = dalloc(&c->d_tile_base, tile_base.size())) || (rc = dalloc(&c->d_rtab, rtab.size())) ||
         (rc = dalloc(&c->d_pyr, B * G.pyr_frame)) || (rc = dalloc(&c->d_blur, B * G.blur_frame)) ||
         (rc = dalloc(&c->d_cell_cnt, B * G.ncells)) ||
@@ -501,6 +547,8 @@ static int plan(orbg_ctx *c, int w, int h, int batch)
     if (!rtab.empty())
         HIPCHK(hipMemcpy(c->d_rtab, rtab.data(), rtab.size() * sizeof(int2),
                          hipMemcpyHostToDevice));
+    HIPCHK(hipMemcpy(c->d_ctab, ctab.data(), ctab.size() * sizeof(uint32_t),
+                     hipMemcpyHostToDevice));
     HIPCHK(hipMemset(c->d_counts, 0, B * sizeof(int32_t)));
     c->geom = G;
     c->cells = cells;
@@ -612,7 +660,7 @@ static int launch_extract(orbg_ctx *c, const uint8_t *d_imgs, int B, int pitch, 
         const uint8_t *src = (l == 1) ? d_imgs : c->d_pyr + P.pyr_off;
         const int64_t sfs = (l == 1) ? fs : G.pyr_frame;
         const int spitch = (l == 1) ? pitch : P.pitch;
-        dim3 grid((L.w + 63) / 64, (L.h + 3) / 4, B);
+        dim3 grid((L.w + 255) / 256, (L.h + 3) / 4, B);
         PROF_LAUNCH(c, "resize",
                     hipLaunchKernelGGL(k_resize, grid, dim3(256), 0, st, src, sfs, spitch, P.w,
                                        c->d_pyr + L.pyr_off, G.pyr_frame, L.pitch, L.w, L.h,
@@ -621,12 +669,16 @@ static int launch_extract(orbg_ctx *c, const uint8_t *d_imgs, int B, int pitch, 
     }
     PROF_LAUNCH(c, "fast_cells",
                 hipLaunchKernelGGL(k_fast_cells, dim3(G.ncells, B), dim3(256), 0, st, c->d_geom,
-                                   c->d_cells, d_imgs, fs, pitch, c->d_pyr, c->d_cell_cnt,
-                                   c->d_cell_kp));
+                                   c->d_cells, d_imgs, fs, pitch, c->d_pyr, c->d_ctab,
+                                   c->d_cell_cnt, c->d_cell_kp));
     PROF_LAUNCH(c, "blur",
                 hipLaunchKernelGGL(k_blur, dim3(c->total_tiles, B), dim3(256), 0, st, c->d_geom,
                                    c->d_tile_base, d_imgs, fs, pitch, c->d_pyr, c->d_blur));
     PROF_LAUNCH(c, "octree",
+                hipLaunchKernelGGL(k_octree_lds, dim3(G.L, B), dim3(512), 0, st, c->d_geom,
+                                   c->d_cell_cnt, c->d_cell_kp, c->d_keys, c->d_act,
+                                   c->d_lvl_kp, c->d_lvl_cnt, c->d_err));
+    PROF_LAUNCH(c, "octree_big",
                 hipLaunchKernelGGL(k_octree, dim3(G.L, B), dim3(ORBG_OCT_THREADS), 0, st,
                                    c->d_geom, c->d_cell_cnt, c->d_cell_kp, c->d_keys, c->d_knode,
                                    c->d_act, c->d_qk, c->d_nodes, c->d_lvl_kp, c->d_lvl_cnt,

@@ -26,6 +26,7 @@
 #define ORBG_GRID_COLS 64        // Frame.h:38
 #define ORBG_GRID_ROWS 48        // Frame.h:37
 #define ORBG_MATCH_TOPK 8
+#define OCT_KEY_CAP 16384        // k_octree_lds handles levels with <= this many candidates
 
 struct OrbgLevel {
     int32_t w, h, pitch;
@@ -40,6 +41,7 @@ struct OrbgLevel {
     int32_t out_off, out_cap;     // octree output words within a frame
     int32_t bulk_end;             // resize: first column using the scalar vertical pass
     int32_t xtab_off, ytab_off;   // resize coefficient tables (int2 per column / row)
+    int32_t xs_off, ys_off;       // quadtree path-code tables (u32 per rel. column / row)
     int64_t pyr_off;              // byte offset of the level in a frame's pyramid (l >= 1)
     int64_t blur_off;             // byte offset in a frame's blurred pyramid
     float scale;                  // mvScaleFactor[l]
@@ -57,6 +59,7 @@ struct OrbgGeom {
     int32_t frame_cap;            // max keypoints per frame (final)
     int32_t ini_th, min_th;
     int32_t brief_fma;
+    int32_t dbg;                  // developer timing knob (ORBG_DBG env), 0 in production
     int32_t gk[7];
     int64_t pyr_frame;            // bytes per frame of d_pyr
     int64_t blur_frame;
