@@ -64,49 +64,97 @@ __device__ int block_sum(int v, int *sh)
 // xtab[dx] = {sx, a0 | a1 << 16}; ytab[dy] = {sy0 | sy1 << 16, b0 | b1 << 16}
 // columns dx < bulk_end use the SIMD vertical pass (mulhi of S>>4), the rest the
 // scalar FixedPtCast<int,uchar,22>.
+// One workgroup per RZ_TW x RZ_TH output tile: the source rows/columns the tile touches
+// are staged in LDS with dword loads (each row keeps its source address alignment, so a
+// caller image with an odd pitch works), then each thread owns 4 output columns (their
+// coefficients stay in registers) and walks RZ_TH/4 rows, storing one dword per row.
 // ---------------------------------------------------------------------------
+#define RZ_TW 256
+#define RZ_TH 16
+
 __global__ __launch_bounds__(256) void k_resize(const uint8_t *__restrict__ src, int64_t sfs,
                                                 int spitch, int sw, uint8_t *__restrict__ dst,
                                                 int64_t dfs, int dpitch, int dw, int dh,
                                                 const int2 *__restrict__ xtab,
-                                                const int2 *__restrict__ ytab, int bulk_end)
+                                                const int2 *__restrict__ ytab, int bulk_end,
+                                                int lds_pitch)
 {
-    // thread = 4 consecutive output pixels of one row (dword store: dpitch % 64 == 0)
-    const int dx0 = 4 * (blockIdx.x * 64 + (threadIdx.x & 63));
-    const int dy = blockIdx.y * 4 + (threadIdx.x >> 6);
-    const int f = blockIdx.z;
-    if (dx0 >= dw || dy >= dh) return;
-    const int2 yt = ytab[dy];
-    const int sy0 = yt.x & 0xFFFF, sy1 = yt.x >> 16;
-    const int b0 = (int)(short)(yt.y & 0xFFFF), b1 = (int)(short)(yt.y >> 16);
-    const uint8_t *s0 = src + f * sfs + (int64_t)sy0 * spitch;
-    const uint8_t *s1 = src + f * sfs + (int64_t)sy1 * spitch;
-    uint32_t word = 0;
+    extern __shared__ __attribute__((aligned(16))) uint32_t rz_lds[];
+    uint8_t *lds = (uint8_t *)rz_lds;
+    const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+    const int c0 = blockIdx.x * RZ_TW, r0 = blockIdx.y * RZ_TH, f = blockIdx.z;
+    const int c1 = min(c0 + RZ_TW, dw) - 1, r1 = min(r0 + RZ_TH, dh) - 1;
+    const int sx_lo = xtab[c0].x;
+    const int sx_hi = min(xtab[c1].x + 1, sw - 1);
+    const int sy_lo = ytab[r0].x & 0xFFFF;
+    const int sy_hi = ytab[r1].x >> 16;
+    const uint8_t *fb = src + f * sfs;
+    // ---- stage rows sy_lo..sy_hi, columns sx_lo..sx_hi ----
+    for (int r = wv; r <= sy_hi - sy_lo; r += 4) {
+        const uint8_t *row = fb + (int64_t)(sy_lo + r) * spitch;
+        const uint8_t *start = row + sx_lo;
+        const int sh = (int)((uintptr_t)start & 3);
+        const uint32_t *aw = (const uint32_t *)(start - sh);
+        const int nw = (sh + sx_hi - sx_lo + 1 + 3) >> 2;
+        uint32_t *dw32 = (uint32_t *)(lds + r * lds_pitch);
+        for (int k = lane; k < nw; k += 64) {
+            const uint8_t *wp = (const uint8_t *)(aw + k);
+            uint32_t v;
+            if (wp >= row && wp + 3 < row + sw) {
+                v = aw[k];
+            } else {  // first / last word of the row: only bytes inside [row, row + sw)
+                v = 0;
+#pragma unroll
+                for (int b = 0; b < 4; b++)
+                    if (wp + b >= row && wp + b < row + sw) v |= (uint32_t)wp[b] << (8 * b);
+            }
+            dw32[k] = v;
+        }
+    }
+    // ---- per-thread column coefficients ----
+    const int dx0 = c0 + 4 * lane;
+    int ox0[4], ox1[4], ca0[4], ca1[4];
 #pragma unroll
     for (int i = 0; i < 4; i++) {
-        const int dx = dx0 + i;
-        if (dx < dw) {
-            const int2 xt = xtab[dx];
-            const int sx = xt.x, sx1 = min(sx + 1, sw - 1);
-            const int a0 = (int)(short)(xt.y & 0xFFFF), a1 = (int)(short)(xt.y >> 16);
-            const int r0 = s0[sx] * a0 + s0[sx1] * a1;
-            const int r1 = s1[sx] * a0 + s1[sx1] * a1;
+        const int dx = min(dx0 + i, c1);
+        const int2 xt = xtab[dx];
+        ox0[i] = xt.x - sx_lo;
+        ox1[i] = min(xt.x + 1, sw - 1) - sx_lo;
+        ca0[i] = (int)(short)(xt.y & 0xFFFF);
+        ca1[i] = (int)(short)(xt.y >> 16);
+    }
+    __syncthreads();
+    if (dx0 > c1) return;
+    const int nvalid = min(4, c1 - dx0 + 1);
+    for (int dy = r0 + wv; dy <= r1; dy += 4) {
+        const int2 yt = ytab[dy];
+        const int sy0 = yt.x & 0xFFFF, sy1 = yt.x >> 16;
+        const int b0 = (int)(short)(yt.y & 0xFFFF), b1 = (int)(short)(yt.y >> 16);
+        const int sh0 = (int)((uintptr_t)(fb + (int64_t)sy0 * spitch + sx_lo) & 3);
+        const int sh1 = (int)((uintptr_t)(fb + (int64_t)sy1 * spitch + sx_lo) & 3);
+        const uint8_t *l0 = lds + (sy0 - sy_lo) * lds_pitch + sh0;
+        const uint8_t *l1 = lds + (sy1 - sy_lo) * lds_pitch + sh1;
+        uint32_t word = 0;
+#pragma unroll
+        for (int i = 0; i < 4; i++) {
+            const int rr0 = l0[ox0[i]] * ca0[i] + l0[ox1[i]] * ca1[i];
+            const int rr1 = l1[ox0[i]] * ca0[i] + l1[ox1[i]] * ca1[i];
             int v;
-            if (dx < bulk_end) {
-                const int a = ((r0 >> 4) * b0) >> 16;
-                const int b = ((r1 >> 4) * b1) >> 16;
+            if (dx0 + i < bulk_end) {
+                const int a = ((rr0 >> 4) * b0) >> 16;
+                const int b = ((rr1 >> 4) * b1) >> 16;
                 v = (a + b + 2) >> 2;
             } else {
-                v = (r0 * b0 + r1 * b1 + (1 << 21)) >> 22;
+                v = (rr0 * b0 + rr1 * b1 + (1 << 21)) >> 22;
             }
             word |= (uint32_t)min(max(v, 0), 255) << (8 * i);
         }
-    }
-    uint8_t *d = dst + f * dfs + (int64_t)dy * dpitch + dx0;
-    if (dx0 + 4 <= dw) {
-        *(uint32_t *)d = word;
-    } else {
-        for (int i = 0; dx0 + i < dw; i++) d[i] = (uint8_t)(word >> (8 * i));
+        uint8_t *d = dst + f * dfs + (int64_t)dy * dpitch + dx0;
+        if (nvalid == 4) {
+            *(uint32_t *)d = word;  // dpitch % 64 == 0 and dx0 % 4 == 0
+        } else {
+            for (int i = 0; i < nvalid; i++) d[i] = (uint8_t)(word >> (8 * i));
+        }
     }
 }
 
@@ -193,8 +241,9 @@ __device__ __forceinline__ v2s fast_score_pair(const Rows7 &R)
 #pragma unroll
     for (int j = 0; j < 8; j++) {  // even k = 2j: run d[k+1..k+8] = lo8[j]
         const int k = 2 * j;
-        bp = pmax(bp, pmax(pmin(lo8[j], d[k]), pmin(lo8[j], d[(k + 9) & 15])));
-        bn = pmin(bn, pmin(pmax(hi8[j], d[k]), pmax(hi8[j], d[(k + 9) & 15])));
+        // max(min(a,b), min(a,c)) = min(a, max(b,c)) (and dual): exact on integers
+        bp = pmax(bp, pmin(lo8[j], pmax(d[k], d[(k + 9) & 15])));
+        bn = pmin(bn, pmax(hi8[j], pmin(d[k], d[(k + 9) & 15])));
     }
     const v2s zero = (v2s){0, 0}, one = (v2s){1, 1};
     const v2s M = pmax(bp, zero - bn);
@@ -202,30 +251,35 @@ __device__ __forceinline__ v2s fast_score_pair(const Rows7 &R)
 }
 
 // ---------------------------------------------------------------------------
-// k_fast_cells: one 256-thread workgroup per (cell, frame).
-// LDS tile: window row r at tile[r][1 + x] (x window-local) so that a group of 4
-// detection pixels (window x = 3+4g .. 6+4g) and its +-3 neighbours are the 12 bytes of
-// dwords g..g+2.  Scores: sc[ry+1][rx+4] with a zero border (NMS neighbours outside the
-// cell's detection region count as 0 -- cv::FAST runs on the cell ROI alone).
-// Unit = (region row ry, 4-pixel group g), u = ry*RG + g, handled in raster order so
-// compaction preserves FAST's row-major output order.
+// k_fast_cells: one wave per (cell, frame), four cells per 256-thread workgroup; the
+// 1-D grid of ceil(ncells * B / 4) workgroups is frame-major after the XCD remap, so a
+// workgroup's cells are neighbours sharing halo rows in L1/L2.  Everything inside a cell
+// is wave-synchronous (no workgroup barrier).
+// LDS per wave: tile (window) + sc (scores), both fc_pitch bytes per row.  Window row r at
+// tile[r][1 + x] (x window-local) so that a group of 4 detection pixels (window
+// x = 3+4g .. 6+4g) and its +-3 neighbours are the 12 bytes of dwords g..g+2; the window
+// is copied with aligned dword loads + v_alignbyte.  Scores: sc[ry+1][rx+4] with a zero
+// border (NMS neighbours outside the cell's detection region count as 0 -- cv::FAST runs
+// on the cell ROI alone).  Unit = (region row ry, 4-pixel group g), u = ry*RG + g, walked in
+// raster order so the compaction preserves FAST's row-major output order.
 // ---------------------------------------------------------------------------
-#define FC_P 72               // LDS row pitch (bytes)
-#define FC_MAXU 4             // units per thread (<= 60x60 region / 4 / 256)
-
-__global__ __launch_bounds__(256) void k_fast_cells(const OrbgGeom *__restrict__ g,
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(6, 8))) void k_fast_cells(const OrbgGeom *__restrict__ g,
                                                     const OrbgCell *__restrict__ cells,
                                                     const uint8_t *__restrict__ img0,
                                                     int64_t img_fs, int img_pitch,
                                                     const uint8_t *__restrict__ pyr,
                                                     const uint32_t *__restrict__ ctab,
                                                     int32_t *__restrict__ cell_cnt,
-                                                    uint2 *__restrict__ cell_kp)
+                                                    uint2 *__restrict__ cell_kp, int nframes)
 {
-    __shared__ __attribute__((aligned(16))) uint8_t tile[ORBG_MAX_WIN][FC_P];
-    __shared__ __attribute__((aligned(16))) uint8_t sc[ORBG_MAX_WIN][FC_P];
-    __shared__ int red[8];
-    const int c = blockIdx.x, f = blockIdx.y, tid = threadIdx.x;
+    extern __shared__ __attribute__((aligned(16))) uint32_t fc_lds[];
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    const int P = g->fc_pitch;
+    uint8_t *tile = (uint8_t *)fc_lds + wv * g->fc_wave_bytes;
+    uint8_t *sc = tile + g->fc_tile_rows * P;
+    const int cid = xcd_remap(blockIdx.x, gridDim.x) * 4 + wv;
+    if (cid >= g->ncells * nframes) return;  // wave-uniform; no workgroup barrier below
+    const int f = cid / g->ncells, c = cid - f * g->ncells;
     const OrbgCell cl = cells[c];
     const int l = cl.level;
     const int W = cl.w, H = cl.h;
@@ -239,33 +293,34 @@ __global__ __launch_bounds__(256) void k_fast_cells(const OrbgGeom *__restrict__
         pitch = g->lv[l].pitch;
     }
     base += (int64_t)cl.y0 * pitch + cl.x0;
-    {
-        const int cx = tid & 63;
-        for (int r = tid >> 6; r < H; r += 4) {
-            const uint8_t *row = base + (int64_t)r * pitch;
-            if (cx < W) tile[r][1 + cx] = row[cx];
-            if (cx + 64 < W) tile[r][65 + cx] = row[cx + 64];
-        }
-    }
     const int RW = W - 6, RH = H - 6;
     const int RG = RW > 0 ? (RW + 3) >> 2 : 0;
     const int nunits = RH > 0 ? RH * RG : 0;
     {
-        uint32_t *z = (uint32_t *)&sc[0][0];
-        const int nz = (RH + 2) * (FC_P / 4);
-        for (int i = tid; i < nz; i += 256) z[i] = 0;
+        // dword j of tile row r = window bytes 4j-1 .. 4j+2 (the window sits >= 13 px inside
+        // the level on every side, so the aligned over-read stays in the image)
+        const int NWR = RG + 2;
+        const int nw = H * NWR;
+        for (int i = lane; i < nw; i += 64) {
+            const int r = i / NWR, j = i - r * NWR;
+            const uintptr_t a = (uintptr_t)(base + (int64_t)r * pitch + 4 * j - 1);
+            const uint32_t *aw = (const uint32_t *)(a & ~(uintptr_t)3);
+            const uint32_t v = __builtin_amdgcn_alignbyte(aw[1], aw[0], (uint32_t)(a & 3));
+            *(uint32_t *)(tile + r * P + 4 * j) = v;
+        }
+        uint32_t *z = (uint32_t *)sc;
+        const int nz = (RH + 2) * (P >> 2);
+        for (int i = lane; i < nz; i += 64) z[i] = 0;
     }
-    __syncthreads();
+    wave_sync_lds();
 
     // ---- scores ----
-    for (int k = 0; k < FC_MAXU; k++) {
-        const int u = tid + 256 * k;
-        if (u >= nunits) break;
+    for (int u = lane; u < nunits; u += 64) {
         const int ry = u / RG, gg = u - ry * RG;
         Rows7 R;
 #pragma unroll
         for (int r = 0; r < 7; r++) {
-            const uint32_t *p = (const uint32_t *)&tile[ry + r][4 * gg];
+            const uint32_t *p = (const uint32_t *)(tile + (ry + r) * P + 4 * gg);
             R.w[r][0] = p[0];
             R.w[r][1] = p[1];
             R.w[r][2] = p[2];
@@ -276,86 +331,73 @@ __global__ __launch_bounds__(256) void k_fast_cells(const OrbgGeom *__restrict__
                         ((uint32_t)(uint16_t)sb.x << 16) | ((uint32_t)(uint16_t)sb.y << 24);
         const int valid = min(RW - 4 * gg, 4);
         if (valid < 4) word &= (1u << (8 * valid)) - 1u;
-        *(uint32_t *)&sc[ry + 1][4 * gg + 4] = word;
+        *(uint32_t *)(sc + (ry + 1) * P + 4 * gg + 4) = word;
     }
-    __syncthreads();
+    wave_sync_lds();
 
-    // ---- NMS (cell-local) at threshold th: 4-bit survivor mask per unit ----
-    uint32_t centre[FC_MAXU];
-    auto nms = [&](int th, uint32_t &mask) -> int {
-        int cnt = 0;
-        mask = 0;
-#pragma unroll
-        for (int k = 0; k < FC_MAXU; k++) {
-            const int u = tid + 256 * k;
-            centre[k] = 0;
-            if (u >= nunits) continue;
-            const int ry = u / RG, gg = u - ry * RG;
-            const uint32_t *m0 = (const uint32_t *)&sc[ry + 1][4 * gg];
-            const uint32_t c1 = m0[1];
-            centre[k] = c1;
-            // quick reject: no byte >= max(th, 1)
-            const int t1 = max(th, 1);
-            const int mx = max(max((int)(c1 & 0xFF), (int)((c1 >> 8) & 0xFF)),
-                               max((int)((c1 >> 16) & 0xFF), (int)(c1 >> 24)));
-            if (mx < t1) continue;
-            const uint32_t *mu = (const uint32_t *)&sc[ry][4 * gg];
-            const uint32_t *md = (const uint32_t *)&sc[ry + 2][4 * gg];
-            const uint32_t row[3][3] = {{mu[0], mu[1], mu[2]}, {m0[0], c1, m0[2]},
-                                        {md[0], md[1], md[2]}};
-#pragma unroll
-            for (int i = 0; i < 4; i++) {
-                const int s = (c1 >> (8 * i)) & 0xFF;
-                if (s < t1) continue;
-                bool keep = true;
-#pragma unroll
-                for (int rr = 0; rr < 3; rr++)
-#pragma unroll
-                    for (int dx = -1; dx <= 1; dx++) {
-                        if (rr == 1 && dx == 0) continue;
-                        const int off = 4 + i + dx;  // byte offset in the 12-byte window
-                        const int q = (row[rr][off >> 2] >> (8 * (off & 3))) & 0xFF;
-                        const int qe = q >= th ? q : 0;
-                        keep = keep && (s > qe);
-                    }
-                if (keep) {
-                    mask |= 1u << (4 * k + i);
-                    cnt++;
-                }
-            }
-        }
-        return cnt;
-    };
-    uint32_t mask;
-    int cnt = nms(g->ini_th, mask);
-    const int tot_ini = block_sum(cnt, red);
-    if (tot_ini == 0) cnt = nms(g->min_th, mask);
-
-    // ---- raster-order compaction ----
+    // ---- NMS (cell-local) at threshold th + raster-order compaction ----
     const int64_t slot = (int64_t)f * g->ncells + c;
     uint2 *out = cell_kp + slot * g->cell_cap;
     const int xo = cl.x0 - ORBG_MIN_BORDER + 3, yo = cl.y0 - ORBG_MIN_BORDER + 3;
     const uint32_t *xs = ctab + g->lv[l].xs_off, *ys = ctab + g->lv[l].ys_off;
-    int run = 0;
-    for (int k = 0; k < FC_MAXU; k++) {
-        if (256 * k >= nunits) break;  // uniform
-        const uint32_t mk = (mask >> (4 * k)) & 0xFu;
-        int tot;
-        int off = block_excl_scan(__popc(mk), &tot, red) + run;
-        const int u = tid + 256 * k;
-        if (mk) {
-            const int ry = u / RG, gg = u - ry * RG;
+    auto nms_compact = [&](int th) -> int {
+        const int t1 = max(th, 1);
+        int run = 0;
+        for (int u0 = 0; u0 < nunits; u0 += 64) {
+            const int u = u0 + lane;
+            uint32_t mask = 0, c1 = 0;
+            int ry = 0, gg = 0;
+            if (u < nunits) {
+                ry = u / RG;
+                gg = u - ry * RG;
+                const uint32_t *m0 = (const uint32_t *)(sc + (ry + 1) * P + 4 * gg);
+                c1 = m0[1];
+                // quick reject: no byte >= max(th, 1)
+                const int mx = max(max((int)(c1 & 0xFF), (int)((c1 >> 8) & 0xFF)),
+                                   max((int)((c1 >> 16) & 0xFF), (int)(c1 >> 24)));
+                if (mx >= t1) {
+                    const uint32_t *mu = (const uint32_t *)(sc + ry * P + 4 * gg);
+                    const uint32_t *md = (const uint32_t *)(sc + (ry + 2) * P + 4 * gg);
+                    const uint32_t row[3][3] = {{mu[0], mu[1], mu[2]}, {m0[0], c1, m0[2]},
+                                                {md[0], md[1], md[2]}};
+#pragma unroll
+                    for (int i = 0; i < 4; i++) {
+                        const int s = (c1 >> (8 * i)) & 0xFF;
+                        if (s < t1) continue;
+                        bool keep = true;
+#pragma unroll
+                        for (int rr = 0; rr < 3; rr++)
+#pragma unroll
+                            for (int dx = -1; dx <= 1; dx++) {
+                                if (rr == 1 && dx == 0) continue;
+                                const int off = 4 + i + dx;  // byte in the 12-byte window
+                                const int q = (row[rr][off >> 2] >> (8 * (off & 3))) & 0xFF;
+                                const int qe = q >= th ? q : 0;
+                                keep = keep && (s > qe);
+                            }
+                        if (keep) mask |= 1u << i;
+                    }
+                }
+            }
+            const int n = __popc(mask);
+            const int incl = wave_incl_scan(n);
+            int off = run + incl - n;
 #pragma unroll
             for (int i = 0; i < 4; i++)
-                if (mk & (1u << i)) {
+                if (mask & (1u << i)) {
                     const int x = xo + 4 * gg + i, y = yo + ry;
-                    out[off++] = make_uint2(orbg_pack(x, y, (centre[k] >> (8 * i)) & 0xFF),
+                    out[off++] = make_uint2(orbg_pack(x, y, (c1 >> (8 * i)) & 0xFF),
                                             xs[x] | ys[y]);
                 }
+            run += __shfl(incl, 63, 64);
         }
-        run += tot;
-    }
-    if (tid == 0) cell_cnt[slot] = run;
+        return run;
+    };
+    // FAST at iniThFAST; an empty cell retries at minThFAST (ORBextractor.cc:1069-1075).
+    // A pass that keeps nothing wrote nothing, so the retry simply overwrites from 0.
+    int run = nms_compact(g->ini_th);
+    if (run == 0) run = nms_compact(g->min_th);
+    if (lane == 0) cell_cnt[slot] = run;
 }
 
 // ---------------------------------------------------------------------------
@@ -387,10 +429,12 @@ __global__ __launch_bounds__(256) void k_blur(const OrbgGeom *__restrict__ g,
 {
     __shared__ __attribute__((aligned(16))) uint8_t in[BLUR_IH][BLUR_IW];
     __shared__ __attribute__((aligned(16))) uint16_t rows[BLUR_IH][BLUR_TW];
-    const int f = blockIdx.y, tid = threadIdx.x;
+    const int ntiles = tile_base[g->L];
+    const int id = xcd_remap(blockIdx.x, gridDim.x);
+    const int f = id / ntiles, bt = id - f * ntiles, tid = threadIdx.x;
     int l = 0;
-    while (l + 1 < g->L && (int)blockIdx.x >= tile_base[l + 1]) l++;
-    const int t = blockIdx.x - tile_base[l];
+    while (l + 1 < g->L && bt >= tile_base[l + 1]) l++;
+    const int t = bt - tile_base[l];
     const OrbgLevel &lv = g->lv[l];
     const int W = lv.w, H = lv.h;
     const int ntx = (W + BLUR_TW - 1) / BLUR_TW;
@@ -405,12 +449,26 @@ __global__ __launch_bounds__(256) void k_blur(const OrbgGeom *__restrict__ g,
         src = pyr + f * g->pyr_frame + lv.pyr_off;
         pitch = lv.pitch;
     }
-    // fill: column c of the tile is image x = tx0 - 4 + c, row r is y = ty0 - 3 + r
-    for (int i = tid; i < BLUR_IH * BLUR_IW; i += 256) {
-        const int r = i / BLUR_IW, c = i - r * BLUR_IW;
+    // fill: column c of the tile is image x = tx0 - 4 + c, row r is y = ty0 - 3 + r.
+    // Word j of a row = x0 .. x0+3 (x0 = tx0 - 4 + 4j): aligned dword pair + v_alignbyte
+    // when x0 .. x0+7 lies inside the row, else bytes with REFLECT_101.
+    for (int i = tid; i < BLUR_IH * (BLUR_IW / 4); i += 256) {
+        const int r = i / (BLUR_IW / 4), j = i - r * (BLUR_IW / 4);
         const int y = reflect101(min(ty0 - 3 + r, H + 2), H);
-        const int x = reflect101(min(tx0 - 4 + c, W + 2), W);
-        in[r][c] = src[(int64_t)y * pitch + x];
+        const uint8_t *row = src + (int64_t)y * pitch;
+        const int x0 = tx0 - 4 + 4 * j;
+        uint32_t v;
+        if (x0 >= 0 && x0 + 7 < W) {
+            const uintptr_t a = (uintptr_t)(row + x0);
+            const uint32_t *aw = (const uint32_t *)(a & ~(uintptr_t)3);
+            v = __builtin_amdgcn_alignbyte(aw[1], aw[0], (uint32_t)(a & 3));
+        } else {
+            v = 0;
+#pragma unroll
+            for (int b = 0; b < 4; b++)
+                v |= (uint32_t)row[reflect101(min(x0 + b, W + 2), W)] << (8 * b);
+        }
+        *(uint32_t *)&in[r][4 * j] = v;
     }
     __syncthreads();
     const int k0 = g->gk[0], k1 = g->gk[1], k2 = g->gk[2], k3 = g->gk[3], k4 = g->gk[4],
@@ -1077,9 +1135,11 @@ __global__ __launch_bounds__(256) void k_orient_desc(
     const uint32_t *__restrict__ lvl_kp, const int32_t *__restrict__ lvl_cnt,
     OrbgKeypointDev *__restrict__ kps, uint8_t *__restrict__ desc, int32_t *__restrict__ counts)
 {
-    const int f = blockIdx.y;
+    const int nb = (g->frame_cap + 3) >> 2;  // blocks per frame
+    const int id = xcd_remap(blockIdx.x, gridDim.x);
+    const int f = id / nb, bx = id - f * nb;
     const int lane = threadIdx.x & 63;
-    const int i = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
+    const int i = bx * (blockDim.x >> 6) + (threadIdx.x >> 6);
     const int L = g->L;
     const int32_t *lc = lvl_cnt + (int64_t)f * L;
     int total = 0, level = -1, idx = 0;
@@ -1091,7 +1151,7 @@ __global__ __launch_bounds__(256) void k_orient_desc(
         }
         total += c;
     }
-    if (blockIdx.x == 0 && threadIdx.x == 0) counts[f] = total;
+    if (bx == 0 && threadIdx.x == 0) counts[f] = total;
     if (level < 0 || i >= g->frame_cap) return;
     const OrbgLevel &lv = g->lv[level];
     const uint32_t key = lvl_kp[(int64_t)f * g->out_frame + lv.out_off + idx];
@@ -1105,18 +1165,41 @@ __global__ __launch_bounds__(256) void k_orient_desc(
         im = pyr + f * g->pyr_frame + lv.pyr_off;
         pitch = lv.pitch;
     }
-    // ---- IC_Angle: lanes 0..30 own column u = lane - 15 ----
+    // ---- IC_Angle (ORBextractor.cc:83-111): the 31 x 31 patch as 31 rows x 9 aligned
+    // dwords, all loads issued up front (5 per lane); each byte is weighted by (u, v) and
+    // masked to the circle |u| <= umax[|v|], then two wave reductions ----
     int m01 = 0, m10 = 0;
-    if (lane < 31) {
-        const int u = lane - ORBG_HALF_PATCH;
+    {
         const uint8_t *ctr = im + (int64_t)y * pitch + x;
-        m10 = u * ctr[u];
-        const int au = u < 0 ? -u : u;
-        for (int v = 1; v <= ORBG_HALF_PATCH; v++) {
-            if (au <= g->umax[v]) {
-                const int vp = ctr[u + v * pitch], vm = ctr[u - v * pitch];
-                m10 += u * (vp + vm);
-                m01 += v * (vp - vm);
+        uint32_t wd[5];
+        int shv[5];  // byte alignment of the row start (per row: the pitch may be odd)
+#pragma unroll
+        for (int k = 0; k < 5; k++) {
+            const int w = lane + 64 * k;  // row v = w / 9 - 15, word c = w % 9
+            wd[k] = 0;
+            shv[k] = 0;
+            if (w < 31 * 9) {
+                const int v = w / 9 - ORBG_HALF_PATCH, cw = w - (w / 9) * 9;
+                const uintptr_t a = (uintptr_t)(ctr + (int64_t)v * pitch - ORBG_HALF_PATCH);
+                wd[k] = ((const uint32_t *)(a & ~(uintptr_t)3))[cw];
+                shv[k] = (int)(a & 3);
+            }
+        }
+#pragma unroll
+        for (int k = 0; k < 5; k++) {
+            const int w = lane + 64 * k;
+            if (w < 31 * 9) {
+                const int v = w / 9 - ORBG_HALF_PATCH, cw = w - (w / 9) * 9;
+                const int um = g->umax[v < 0 ? -v : v];
+#pragma unroll
+                for (int b = 0; b < 4; b++) {
+                    const int u = 4 * cw + b - shv[k] - ORBG_HALF_PATCH;
+                    const int val = (wd[k] >> (8 * b)) & 0xFF;
+                    if (u >= -um && u <= um) {
+                        m10 += u * val;
+                        m01 += v * val;
+                    }
+                }
             }
         }
     }

@@ -19,6 +19,7 @@
 
 #include "../../include/orbg.h"
 #include "orbg_internal.h"
+#include "orbg_device.h"
 
 #pragma clang fp contract(off)
 
@@ -99,12 +100,16 @@ __global__ __launch_bounds__(256) void k_knn2_pairs(const uint8_t *desc, const i
                                                     int fc, const int32_t *f1, const int32_t *f2,
                                                     int32_t *out)
 {
-    const int p = blockIdx.y;
+    // 1-D grid of nbx blocks per pair, remapped so one pair's blocks share an XCD (and
+    // the L2 copy of the train descriptors they all stream)
+    const int nbx = (fc + 255) >> 8;
+    const int id = xcd_remap(blockIdx.x, gridDim.x);
+    const int p = id / nbx, bx = id - p * nbx;
     const int a = f1[p], b = f2[p];
     const int nq = counts[b], nt = counts[a];
-    if ((int)blockIdx.x * 256 >= nq) return;
+    if (bx * 256 >= nq) return;
     knn2_block(desc + (size_t)b * fc * 32, nq, desc + (size_t)a * fc * 32, nt,
-               out + (size_t)p * fc * 3, blockIdx.x * 256);
+               out + (size_t)p * fc * 3, bx * 256);
 }
 
 // ---------------------------------------------------------------------------
@@ -276,18 +281,27 @@ __global__ __launch_bounds__(256) void k_init_cands_pairs(
     const int32_t *f1, const int32_t *f2, int w, int h, int window, unsigned long long *topk,
     int32_t *topn)
 {
-    const int p = blockIdx.y;
+    const int nbx = (fc + 4 * INIT_QPW - 1) / (4 * INIT_QPW);
+    const int id = xcd_remap(blockIdx.x, gridDim.x);
+    const int p = id / nbx, bx = id - p * nbx;
     const int a = f1[p], c = f2[p];
     const int n1 = counts[a], n2 = counts[c];
-    if ((int)blockIdx.x * 4 * INIT_QPW >= n1) return;
+    const int qbase = bx * 4 * INIT_QPW;
+    if (qbase >= n1) return;
     const orbg_keypoint *k1 = kps + (size_t)a * fc;
+    // extractor output is level-major: a block whose first query is above level 0 has no
+    // SearchForInitialization query (octave > 0 only, ORBmatcher.cc:500-502)
+    if (k1[qbase].octave > 0) {
+        for (int i = qbase + threadIdx.x; i < min(n1, qbase + 4 * INIT_QPW); i += 256)
+            topn[(size_t)p * fc + i] = -1;
+        return;
+    }
     orbg_bounds b{0.f, (float)w, 0.f, (float)h};
     // vbPrevMatched = F1.mvKeysUn[i].pt: read x, y straight out of the keypoint records
     init_cands_block(k1, desc + (size_t)a * fc * 32, n1, kps + (size_t)c * fc,
                      desc + (size_t)c * fc * 32, n2, b, (const float *)k1,
                      (int)(sizeof(orbg_keypoint) / sizeof(float)), window,
-                     topk + (size_t)p * fc * ORBG_MATCH_TOPK, topn + (size_t)p * fc,
-                     blockIdx.x * 4 * INIT_QPW);
+                     topk + (size_t)p * fc * ORBG_MATCH_TOPK, topn + (size_t)p * fc, qbase);
 }
 
 // prev stride: the batch path reads x,y out of orbg_keypoint records (stride 7 floats)
@@ -343,12 +357,6 @@ __device__ void rescan(const orbg_keypoint *k2, const uint8_t *d2, int n2, const
 // the next chunk of lists (double buffer); wave 0 runs the exact rescan for a query
 // whose K-list the vMatchedDistance filter exhausted.
 #define RESOLVE_T 128
-
-__device__ __forceinline__ void wave_sync_lds()
-{
-    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-}
 
 __device__ void init_resolve_block(ResolveShared &S, const orbg_keypoint *__restrict__ k1,
                                    const uint8_t *__restrict__ d1, int n1,
@@ -639,10 +647,10 @@ int launch_match_pairs(hipStream_t st, const uint8_t *desc, const orbg_keypoint 
 {
     if (fc > RESOLVE_N2_CAP || fc > (1 << 20)) return ORBG_ENOTSUP;
     PL(prof, st, "knn2",
-       hipLaunchKernelGGL(k_knn2_pairs, dim3((fc + 255) / 256, npairs), dim3(256), 0, st, desc,
+       hipLaunchKernelGGL(k_knn2_pairs, dim3((fc + 255) / 256 * npairs), dim3(256), 0, st, desc,
                           counts, fc, d_f1, d_f2, knn));
     PL(prof, st, "init_cands",
-       hipLaunchKernelGGL(k_init_cands_pairs, dim3((fc + 4 * INIT_QPW - 1) / (4 * INIT_QPW), npairs),
+       hipLaunchKernelGGL(k_init_cands_pairs, dim3((fc + 4 * INIT_QPW - 1) / (4 * INIT_QPW) * npairs),
                           dim3(256), 0, st, kps, desc, counts, fc, d_f1, d_f2, w, h, window,
                           (unsigned long long *)topk, topk_n));
     PL(prof, st, "init_resolve",

@@ -20,9 +20,9 @@
 
 namespace orbg {
 __global__ void k_resize(const uint8_t *, int64_t, int, int, uint8_t *, int64_t, int, int, int,
-                         const int2 *, const int2 *, int);
+                         const int2 *, const int2 *, int, int);
 __global__ void k_fast_cells(const OrbgGeom *, const OrbgCell *, const uint8_t *, int64_t, int,
-                             const uint8_t *, const uint32_t *, int32_t *, uint2 *);
+                             const uint8_t *, const uint32_t *, int32_t *, uint2 *, int);
 __global__ void k_blur(const OrbgGeom *, const int32_t *, const uint8_t *, int64_t, int,
                        const uint8_t *, uint8_t *);
 __global__ void k_octree(const OrbgGeom *, const int32_t *, const uint2 *, uint32_t *,
@@ -502,11 +502,43 @@ static int plan(orbg_ctx *c, int w, int h, int batch)
                 be = x;
             }
             L.bulk_end = be;
+            // k_resize LDS staging extent (RZ_TW x RZ_TH output tiles)
+            int span = 0, rows = 0;
+            for (int c0 = 0; c0 < dw; c0 += 256) {
+                const int c1 = std::min(c0 + 256, dw) - 1;
+                const int lo = rtab[L.xtab_off + c0].x;
+                const int hi = std::min(rtab[L.xtab_off + c1].x + 1, sw - 1);
+                span = std::max(span, hi - lo + 1);
+            }
+            for (int r0 = 0; r0 < dh; r0 += 16) {
+                const int r1 = std::min(r0 + 16, dh) - 1;
+                rows = std::max(rows, (rtab[L.ytab_off + r1].x >> 16) -
+                                          (rtab[L.ytab_off + r0].x & 0xFFFF) + 1);
+            }
+            L.rz_pitch = ((span + 3 + 3) / 4) * 4 + 4;
+            L.rz_rows = rows;
+            if ((int64_t)L.rz_pitch * rows > 64 * 1024)
+                return set_err(ORBG_ENOTSUP, "level %d resize tile needs %d x %d LDS bytes", l,
+                               rows, L.rz_pitch);
         }
     }
     tile_base.push_back(tiles);
     G.ncells = (int)cells.size();
     G.cell_cap = cell_cap;
+    {
+        int wmax = 0, hmax = 0;
+        for (const OrbgCell &cl : cells) {
+            wmax = std::max(wmax, (int)cl.w);
+            hmax = std::max(hmax, (int)cl.h);
+        }
+        const int rg = std::max(wmax - 6 + 3, 0) / 4;
+        G.fc_pitch = 4 * rg + 12;  // dwords 0..RG+1 of the window / score rows, + slack
+        G.fc_tile_rows = hmax;
+        G.fc_wave_bytes = ((hmax + std::max(hmax - 6, 0) + 2) * G.fc_pitch + 15) & ~15;
+        if (4 * G.fc_wave_bytes > 64 * 1024)
+            return set_err(ORBG_ENOTSUP, "FAST cell %dx%d needs %d LDS bytes per wave", wmax,
+                           hmax, G.fc_wave_bytes);
+    }
     for (int l = 0; l < G.L; l++) {
         G.lv[l].key_off = key_off;
         G.lv[l].key_cap = G.lv[l].ncells * cell_cap;
@@ -660,19 +692,19 @@ static int launch_extract(orbg_ctx *c, const uint8_t *d_imgs, int B, int pitch, 
         const uint8_t *src = (l == 1) ? d_imgs : c->d_pyr + P.pyr_off;
         const int64_t sfs = (l == 1) ? fs : G.pyr_frame;
         const int spitch = (l == 1) ? pitch : P.pitch;
-        dim3 grid((L.w + 255) / 256, (L.h + 3) / 4, B);
+        dim3 grid((L.w + 255) / 256, (L.h + 15) / 16, B);
         PROF_LAUNCH(c, "resize",
-                    hipLaunchKernelGGL(k_resize, grid, dim3(256), 0, st, src, sfs, spitch, P.w,
-                                       c->d_pyr + L.pyr_off, G.pyr_frame, L.pitch, L.w, L.h,
-                                       c->d_rtab + L.xtab_off, c->d_rtab + L.ytab_off,
-                                       L.bulk_end));
+                    hipLaunchKernelGGL(k_resize, grid, dim3(256), L.rz_pitch * L.rz_rows, st,
+                                       src, sfs, spitch, P.w, c->d_pyr + L.pyr_off, G.pyr_frame,
+                                       L.pitch, L.w, L.h, c->d_rtab + L.xtab_off,
+                                       c->d_rtab + L.ytab_off, L.bulk_end, L.rz_pitch));
     }
     PROF_LAUNCH(c, "fast_cells",
-                hipLaunchKernelGGL(k_fast_cells, dim3(G.ncells, B), dim3(256), 0, st, c->d_geom,
-                                   c->d_cells, d_imgs, fs, pitch, c->d_pyr, c->d_ctab,
-                                   c->d_cell_cnt, c->d_cell_kp));
+                hipLaunchKernelGGL(k_fast_cells, dim3((G.ncells * B + 3) / 4), dim3(256),
+                                   4 * G.fc_wave_bytes, st, c->d_geom, c->d_cells, d_imgs, fs,
+                                   pitch, c->d_pyr, c->d_ctab, c->d_cell_cnt, c->d_cell_kp, B));
     PROF_LAUNCH(c, "blur",
-                hipLaunchKernelGGL(k_blur, dim3(c->total_tiles, B), dim3(256), 0, st, c->d_geom,
+                hipLaunchKernelGGL(k_blur, dim3(c->total_tiles * B), dim3(256), 0, st, c->d_geom,
                                    c->d_tile_base, d_imgs, fs, pitch, c->d_pyr, c->d_blur));
     PROF_LAUNCH(c, "octree",
                 hipLaunchKernelGGL(k_octree_lds, dim3(G.L, B), dim3(512), 0, st, c->d_geom,
@@ -684,7 +716,7 @@ static int launch_extract(orbg_ctx *c, const uint8_t *d_imgs, int B, int pitch, 
                                    c->d_act, c->d_qk, c->d_nodes, c->d_lvl_kp, c->d_lvl_cnt,
                                    c->d_err));
     PROF_LAUNCH(c, "orient_desc",
-                hipLaunchKernelGGL(k_orient_desc, dim3((G.frame_cap + 3) / 4, B), dim3(256), 0, st,
+                hipLaunchKernelGGL(k_orient_desc, dim3((G.frame_cap + 3) / 4 * B), dim3(256), 0, st,
                                    c->d_geom, d_imgs, fs, pitch, c->d_pyr, c->d_blur,
                                    c->d_lvl_kp, c->d_lvl_cnt, (OrbgKeypointDev *)c->d_kps,
                                    c->d_desc, c->d_counts));

@@ -23,4 +23,23 @@ __device__ __forceinline__ int wave_sum(int x)
     return x;
 }
 
+// LDS written by some lanes of a wave, then read by others: keep the compiler from
+// reordering (the hardware keeps one wave's LDS ops in order).
+__device__ __forceinline__ void wave_sync_lds()
+{
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+}
+
+// XCD-aware block remap (cdna_hip_programming.md T1, bijective for nwg % 8 != 0).
+// The dispatcher deals workgroups round-robin over the 8 XCDs (orig % 8 shares an L2);
+// the remap hands each XCD a contiguous run of logical blocks, so neighbouring cells /
+// tiles / keypoints of one frame (which share halo lines and pyramid levels) hit in the
+// same 4 MiB L2 instead of being fetched once per XCD.  Speed only, never correctness.
+__device__ __forceinline__ int xcd_remap(int orig, int nwg)
+{
+    const int xcd = orig & 7, q = nwg >> 3, r = nwg & 7;
+    return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (orig >> 3);
+}
+
 }  // namespace orbg

@@ -42,6 +42,7 @@ struct OrbgLevel {
     int32_t bulk_end;             // resize: first column using the scalar vertical pass
     int32_t xtab_off, ytab_off;   // resize coefficient tables (int2 per column / row)
     int32_t xs_off, ys_off;       // quadtree path-code tables (u32 per rel. column / row)
+    int32_t rz_pitch, rz_rows;    // k_resize LDS staging: bytes per source row, rows per tile
     int64_t pyr_off;              // byte offset of the level in a frame's pyramid (l >= 1)
     int64_t blur_off;             // byte offset in a frame's blurred pyramid
     float scale;                  // mvScaleFactor[l]
@@ -60,6 +61,9 @@ struct OrbgGeom {
     int32_t ini_th, min_th;
     int32_t brief_fma;
     int32_t dbg;                  // developer timing knob (ORBG_DBG env), 0 in production
+    int32_t fc_pitch;             // k_fast_cells LDS row pitch (bytes)
+    int32_t fc_tile_rows;         // max FAST window height
+    int32_t fc_wave_bytes;        // LDS bytes per wave (window + score tiles)
     int32_t gk[7];
     int64_t pyr_frame;            // bytes per frame of d_pyr
     int64_t blur_frame;
