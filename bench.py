@@ -41,11 +41,11 @@ def kernel_algo_bytes(name, B, npairs, ncand, nkp, launches_per_step):
     if name == "resize":
         tot = B * sum(lv[l - 1][0] * lv[l - 1][1] + lv[l][0] * lv[l][1] for l in range(1, NLEV))
     elif name == "fast_cells":
-        tot = B * PYR_BYTES + 4 * ncand
+        tot = B * PYR_BYTES + 8 * ncand
     elif name == "blur":
         tot = 2 * B * PYR_BYTES
     elif name == "octree":
-        tot = 4 * ncand + 4 * nkp
+        tot = 8 * ncand + 4 * nkp
     elif name == "orient_desc":
         tot = nkp * (749 + 512 + 4 + 28 + 32)
     elif name == "knn2":
@@ -93,14 +93,14 @@ def main():
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--batch", type=int, default=256, help="frames per GPU per step")
     ap.add_argument("--cpu-threads", type=int, default=int(os.environ.get("OMP_NUM_THREADS", "16")))
-    ap.add_argument("--cpu-frames", type=int, default=0, help="0: 24 x threads")
+    ap.add_argument("--cpu-frames", type=int, default=0, help="0: 256 x threads (~10-20 s)")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-kernel-timing", action="store_true")
     args = ap.parse_args()
 
     import torch
     import torch.distributed as dist
-    from orb_slam2_test_amd import ORBextractor, synthetic
+    from orb_slam2_test_amd import ORBextractor, sequence, synthetic
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -112,20 +112,23 @@ def main():
     B = args.batch
     frames = synthetic.sequence(B, H, W, seed=synthetic.DEFAULT_SEED + 1000 * rank)
     d_frames = torch.from_numpy(frames).to("cuda")
+    torch.cuda.synchronize()
     ext = ORBextractor(NFEAT, 1.2, NLEV, 20, 7, device=local, max_batch=B)
-    stream = torch.cuda.current_stream()
+    # one non-null torch stream for everything: liborbg's kernels, the summary and RCCL
+    # (the null stream's handle is 0, which orbg_set_stream reads as "own stream")
+    stream = torch.cuda.Stream()
+    torch.cuda.set_stream(stream)
     ext.ctx.set_stream(stream.cuda_stream)
     f1 = ((np.arange(B) - 1) % B).astype(np.int32)
     f2 = np.arange(B, dtype=np.int32)
     summary = torch.zeros(2 * B, dtype=torch.int32, device="cuda")
-    gathered = [torch.zeros_like(summary) for _ in range(world)]
 
     def step():
         ext.extract_batch_device(d_frames.data_ptr(), B, W, H)
         ext.match_batch_device(f1, f2, 100, 0.9, True)
         ext.ctx.batch_summary(summary.data_ptr())
-        if world > 1:
-            dist.all_gather(gathered, summary)
+        if world > 1:  # trajectory summary of every rank's frames (RCCL all_gather)
+            sequence.gather_summary(summary.view(2, B), world, sizes=[B] * world)
 
     for _ in range(args.warmup):
         step()
@@ -200,7 +203,7 @@ def main():
             "candidates_per_frame": round(ncand / B, 1), "keypoints_per_frame": round(nkp / B, 1),
         }
         if world == 1 and not args.no_cpu:
-            n = args.cpu_frames or 24 * args.cpu_threads
+            n = args.cpu_frames or 256 * args.cpu_threads
             out["cpu_baseline"] = cpu_baseline(frames, args.cpu_threads, n)
         else:
             out["cpu_baseline"] = None

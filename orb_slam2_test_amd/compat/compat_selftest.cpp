@@ -1,0 +1,101 @@
+// compat_selftest.cpp -- drives the C++ compat layer the way Tracking.cc drives the
+// reference (extract two frames, SearchForInitialization, brute-force knn2) and dumps the
+// results as raw files for tests/test_gpu_compat.py to compare against the oracle.
+//
+//   compat_selftest nogpu
+//       expects the Extractor constructor to throw (no HIP device: no CPU fallback)
+//   compat_selftest run <w> <h> <frame0.raw> <frame1.raw> <outdir> <nfeatures>
+//       writes kps0/kps1 (28-B cv::KeyPoint records), desc0/desc1 (N x 32),
+//       m12 (int32 per F1 keypoint), knn (int32 triples per F2 keypoint), nm.txt
+#include <cstdio>
+#include <cstdlib>
+#include <fstream>
+#include <iostream>
+#include <string>
+#include <vector>
+
+#include "orbg_compat.hpp"
+
+static std::vector<uint8_t> read_file(const std::string &p, size_t n)
+{
+    std::vector<uint8_t> b(n);
+    std::ifstream f(p, std::ios::binary);
+    f.read((char *)b.data(), (std::streamsize)n);
+    if ((size_t)f.gcount() != n) throw std::runtime_error("short read: " + p);
+    return b;
+}
+
+template <class T>
+static void write_file(const std::string &p, const std::vector<T> &v)
+{
+    std::ofstream f(p, std::ios::binary);
+    f.write((const char *)v.data(), (std::streamsize)(v.size() * sizeof(T)));
+}
+
+int main(int argc, char **argv)
+{
+    if (argc >= 2 && std::string(argv[1]) == "nogpu") {
+        try {
+            orbg_compat::Extractor e(2000, 1.2f, 8, 20, 7);
+            std::cerr << "constructor succeeded without a GPU\n";
+            return 1;
+        } catch (const orbg_compat::Error &err) {
+            std::cout << "no-gpu ok (" << err.code << "): " << err.what() << "\n";
+            return err.code == ORBG_EIO ? 0 : 2;
+        }
+    }
+    if (argc < 8 || std::string(argv[1]) != "run") {
+        std::cerr << "usage: compat_selftest nogpu | run w h f0 f1 outdir nfeatures\n";
+        return 2;
+    }
+    const int w = std::atoi(argv[2]), h = std::atoi(argv[3]);
+    const std::string out = argv[6];
+    const int nfeat = std::atoi(argv[7]);
+    std::vector<uint8_t> im0 = read_file(argv[4], (size_t)w * h);
+    std::vector<uint8_t> im1 = read_file(argv[5], (size_t)w * h);
+
+    // Tracking.cc:127 / Frame.cc:310-316: one extractor per role, reused every frame
+    orbg_compat::Extractor ext(nfeat, 1.2f, 8, 20, 7);
+    std::vector<orbg_keypoint> k0, k1;
+    std::vector<uint8_t> d0, d1;
+    // empty image: outputs untouched (ORBextractor.cc:1333-1334)
+    k0.resize(3);
+    if (ext(nullptr, 0, 0, 0, k0, d0) != 0 || k0.size() != 3) return 3;
+    const int n0 = ext(im0.data(), w, h, (size_t)w, k0, d0);
+    const int n1 = ext(im1.data(), w, h, (size_t)w, k1, d1);
+    int lw = 0, lh = 0;
+    std::vector<uint8_t> top = ext.ImagePyramidLevel(ext.GetLevels() - 1, &lw, &lh);
+    if ((int)top.size() != lw * lh || lw <= 0) return 4;
+
+    // Tracking::MonocularInitialization (Tracking.cc:781-782): ORBmatcher(0.9, true),
+    // vbPrevMatched = F1 keypoint positions, window 100
+    orbg_compat::Matcher matcher(0.9f, true, ext.context());
+    orbg_compat::FrameView F1{k0.data(), d0.data(), n0, {0.f, (float)w, 0.f, (float)h}};
+    orbg_compat::FrameView F2{k1.data(), d1.data(), n1, {0.f, (float)w, 0.f, (float)h}};
+    std::vector<float> prev(2 * (size_t)n0);
+    for (int i = 0; i < n0; i++) {
+        prev[2 * i] = k0[i].x;
+        prev[2 * i + 1] = k0[i].y;
+    }
+    std::vector<int> m12;
+    const int nm = matcher.SearchForInitialization(F1, F2, prev, m12, 100);
+    std::vector<int32_t> bi, bd, sd;
+    matcher.HammingKnn2(d1.data(), n1, d0.data(), n0, bi, bd, sd);
+    std::vector<int32_t> knn(3 * (size_t)n1);
+    for (int i = 0; i < n1; i++) {
+        knn[3 * i] = bi[i];
+        knn[3 * i + 1] = bd[i];
+        knn[3 * i + 2] = sd[i];
+    }
+    if (n0 > 1 && orbg_compat::Matcher::DescriptorDistance(d0.data(), d0.data()) != 0) return 5;
+
+    write_file(out + "/kps0", k0);
+    write_file(out + "/kps1", k1);
+    write_file(out + "/desc0", d0);
+    write_file(out + "/desc1", d1);
+    write_file(out + "/m12", std::vector<int32_t>(m12.begin(), m12.end()));
+    write_file(out + "/knn", knn);
+    std::ofstream(out + "/nm.txt") << nm << "\n";
+    std::cout << "compat ok: " << n0 << " + " << n1 << " keypoints, " << nm << " matches\n";
+    return 0;
+}

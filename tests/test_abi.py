@@ -92,11 +92,18 @@ def test_invalid_arguments_rejected(liborbg):
 
 
 def test_cpp_compat_header_compiles():
-    """The C++ drop-in classes (compat/) compile against the C ABI with g++."""
-    src = os.path.join(ROOT, "orb_slam2_test_amd", "compat", "compat_selftest.cpp")
-    if not os.path.exists(src):
-        pytest.skip("compat layer not present")
-    out = "/tmp/orbg_compat_selftest"
-    subprocess.check_call(["g++", "-std=c++17", "-fsyntax-only", "-I", os.path.join(ROOT, "include"),
-                           "-I", os.path.join(ROOT, "orb_slam2_test_amd", "compat"), src])
-    assert out
+    """The C++ drop-in classes (compat/) compile against the C ABI with g++, and without a
+    GPU the Extractor constructor throws (ORBG_EIO): no CPU fallback behind them either."""
+    comp = os.path.join(ROOT, "orb_slam2_test_amd", "compat")
+    src = os.path.join(comp, "compat_selftest.cpp")
+    subprocess.check_call(["g++", "-std=c++17", "-Wall", "-Werror", "-fsyntax-only", "-I",
+                           os.path.join(ROOT, "include"), "-I", comp, src])
+    exe = os.path.join(ROOT, "orb_slam2_test_amd", "lib", "compat_selftest")
+    if not os.path.exists(exe):
+        subprocess.check_call(["make", "-s", "-C", os.path.join(ROOT, "orb_slam2_test_amd", "csrc")])
+    import torch
+    if torch.cuda.is_available():
+        pytest.skip("a GPU is visible (tests/test_gpu_compat.py runs the selftest)")
+    r = subprocess.run([exe, "nogpu"], capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert "no HIP device" in r.stdout

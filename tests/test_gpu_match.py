@@ -166,3 +166,23 @@ def test_batch_match_device(oracle):
     ext.ctx.sync()
     s = out.cpu().numpy()
     assert s[0] == len(ext.download_frame(0)[0])
+
+
+def test_sharded_sequence_gpu(oracle):
+    """Batched-sequence mode on the GPU: each shard (block + 1-frame halo, as a rank would
+    run it) through liborbg's batch entry points; the concatenated per-frame summary equals
+    the oracle's single-process run of the whole cyclic sequence."""
+    from orb_slam2_test_amd import ORBextractor, sequence, synthetic
+    frames = synthetic.sequence(7, 376, 1241, seed=synthetic.DEFAULT_SEED + 9)
+    p = oracle.params(nfeatures=2000)
+    ref_nkp, ref_nm = oracle.frames_batch(p, frames, nthreads=4, window=100, nnratio=0.9)
+    be = sequence.GpuBackend(ORBextractor(2000, 1.2, 8, 20, 7, max_batch=8))
+    for world in (1, 2, 3):
+        nkp, nm = [], []
+        for r in range(world):
+            lo, hi = sequence.shard(len(frames), world, r)
+            k, m = be(frames[sequence.local_indices(len(frames), lo, hi)])
+            nkp.append(k[1:])
+            nm.append(m[1:])
+        assert np.array_equal(np.concatenate(nkp), ref_nkp), world
+        assert np.array_equal(np.concatenate(nm), ref_nm), world
