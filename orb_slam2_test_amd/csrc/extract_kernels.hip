@@ -196,57 +196,68 @@ struct Rows7 {
     uint32_t w[7][3];
 };
 
+// Score of two pixels from the 16 circle pixels x[k] alone (no per-pixel differences):
+// with d = v - x,  max_arc min d = v - min_k A_k  and  min_arc max d = v - max_k a_k,
+// A_k / a_k = max / min of x over the 9-arc starting at k, so
+//   M = max(v - min_k A_k, max_k a_k - v),   score = max(M - 1, 0).
+// Arc extrema use gfx950's 3-input packed v_pk_maximum3_f16 / v_pk_minimum3_f16: the u16
+// lanes (values 0..255) are read as f16 bit patterns, i.e. +0 and positive denormals,
+// whose IEEE order is the integer order (f16 denormals are preserved; nothing is
+// computed in f16, only ordered).  3-arcs t_k = ext(x[k..k+2]), 9-arcs ext(t_k, t_k+3, t_k+6).
+typedef _Float16 h2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ h2 hmax3(h2 a, h2 b, h2 c)
+{
+    return __builtin_elementwise_maximum(__builtin_elementwise_maximum(a, b), c);
+}
+__device__ __forceinline__ h2 hmin3(h2 a, h2 b, h2 c)
+{
+    return __builtin_elementwise_minimum(__builtin_elementwise_minimum(a, b), c);
+}
+__device__ __forceinline__ h2 as_h2(v2s v) { return __builtin_bit_cast(h2, v); }
+__device__ __forceinline__ v2s as_v2s(h2 v) { return __builtin_bit_cast(v2s, v); }
+
 // circle (dx, dy) of makeOffsets(16); row index = 3 + dy, byte offset = 4 + dx (+ pixel i)
 template <int I>
 __device__ __forceinline__ v2s fast_score_pair(const Rows7 &R)
 {
-#define GB(row, dx) gather2<4 + (dx) + I>(R.w[row][0], R.w[row][1], R.w[row][2])
-    const v2s v = GB(3, 0);
-    v2s d[16];
-    d[0] = v - GB(6, 0);
-    d[1] = v - GB(6, 1);
-    d[2] = v - GB(5, 2);
-    d[3] = v - GB(4, 3);
-    d[4] = v - GB(3, 3);
-    d[5] = v - GB(2, 3);
-    d[6] = v - GB(1, 2);
-    d[7] = v - GB(0, 1);
-    d[8] = v - GB(0, 0);
-    d[9] = v - GB(0, -1);
-    d[10] = v - GB(1, -2);
-    d[11] = v - GB(2, -3);
-    d[12] = v - GB(3, -3);
-    d[13] = v - GB(4, -3);
-    d[14] = v - GB(5, -2);
-    d[15] = v - GB(6, -1);
+#define GB(row, dx) as_h2(gather2<4 + (dx) + I>(R.w[row][0], R.w[row][1], R.w[row][2]))
+    const v2s v = gather2<4 + I>(R.w[3][0], R.w[3][1], R.w[3][2]);
+    h2 x[16];
+    x[0] = GB(6, 0);
+    x[1] = GB(6, 1);
+    x[2] = GB(5, 2);
+    x[3] = GB(4, 3);
+    x[4] = GB(3, 3);
+    x[5] = GB(2, 3);
+    x[6] = GB(1, 2);
+    x[7] = GB(0, 1);
+    x[8] = GB(0, 0);
+    x[9] = GB(0, -1);
+    x[10] = GB(1, -2);
+    x[11] = GB(2, -3);
+    x[12] = GB(3, -3);
+    x[13] = GB(4, -3);
+    x[14] = GB(5, -2);
+    x[15] = GB(6, -1);
 #undef GB
-    v2s lo2[8], hi2[8], lo4[8], hi4[8], lo8[8], hi8[8];
+    // one side at a time keeps x[16] + 16 temporaries live, not 48
+    h2 t[16], A[16];
 #pragma unroll
-    for (int j = 0; j < 8; j++) {  // odd start s = 2j+1
-        const int s = 2 * j + 1;
-        lo2[j] = pmin(d[s], d[(s + 1) & 15]);
-        hi2[j] = pmax(d[s], d[(s + 1) & 15]);
-    }
+    for (int k = 0; k < 16; k++) t[k] = hmax3(x[k], x[(k + 1) & 15], x[(k + 2) & 15]);
 #pragma unroll
-    for (int j = 0; j < 8; j++) {
-        lo4[j] = pmin(lo2[j], lo2[(j + 1) & 7]);
-        hi4[j] = pmax(hi2[j], hi2[(j + 1) & 7]);
-    }
+    for (int k = 0; k < 16; k++) A[k] = hmax3(t[k], t[(k + 3) & 15], t[(k + 6) & 15]);
+    const h2 Amin = __builtin_elementwise_minimum(
+        hmin3(hmin3(A[0], A[1], A[2]), hmin3(A[3], A[4], A[5]), hmin3(A[6], A[7], A[8])),
+        hmin3(hmin3(A[9], A[10], A[11]), hmin3(A[12], A[13], A[14]), A[15]));
 #pragma unroll
-    for (int j = 0; j < 8; j++) {
-        lo8[j] = pmin(lo4[j], lo4[(j + 2) & 7]);  // d[s .. s+7]
-        hi8[j] = pmax(hi4[j], hi4[(j + 2) & 7]);
-    }
-    v2s bp = (v2s){-1000, -1000}, bn = (v2s){1000, 1000};
+    for (int k = 0; k < 16; k++) t[k] = hmin3(x[k], x[(k + 1) & 15], x[(k + 2) & 15]);
 #pragma unroll
-    for (int j = 0; j < 8; j++) {  // even k = 2j: run d[k+1..k+8] = lo8[j]
-        const int k = 2 * j;
-        // max(min(a,b), min(a,c)) = min(a, max(b,c)) (and dual): exact on integers
-        bp = pmax(bp, pmin(lo8[j], pmax(d[k], d[(k + 9) & 15])));
-        bn = pmin(bn, pmax(hi8[j], pmin(d[k], d[(k + 9) & 15])));
-    }
+    for (int k = 0; k < 16; k++) A[k] = hmin3(t[k], t[(k + 3) & 15], t[(k + 6) & 15]);
+    const h2 amax = __builtin_elementwise_maximum(
+        hmax3(hmax3(A[0], A[1], A[2]), hmax3(A[3], A[4], A[5]), hmax3(A[6], A[7], A[8])),
+        hmax3(hmax3(A[9], A[10], A[11]), hmax3(A[12], A[13], A[14]), A[15]));
     const v2s zero = (v2s){0, 0}, one = (v2s){1, 1};
-    const v2s M = pmax(bp, zero - bn);
+    const v2s M = pmax(v - as_v2s(Amin), as_v2s(amax) - v);
     return pmax(M - one, zero);  // u8 score, 0 = none
 }
 
@@ -296,27 +307,53 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(6, 8))) voi
     const int RW = W - 6, RH = H - 6;
     const int RG = RW > 0 ? (RW + 3) >> 2 : 0;
     const int nunits = RH > 0 ? RH * RG : 0;
+    // quadtree path codes of this cell's columns / rows (RW, RH <= 60 < 64), one per lane,
+    // issued now so their latency hides behind the window loads
+    const int xo = cl.x0 - ORBG_MIN_BORDER + 3, yo = cl.y0 - ORBG_MIN_BORDER + 3;
+    const uint32_t xs_l = lane < RW ? ctab[g->lv[l].xs_off + xo + lane] : 0u;
+    const uint32_t ys_l = lane < RH ? ctab[g->lv[l].ys_off + yo + lane] : 0u;
     {
         // dword j of tile row r = window bytes 4j-1 .. 4j+2 (the window sits >= 13 px inside
         // the level on every side, so the aligned over-read stays in the image)
+        // all loads of a 512-word chunk are issued before the first LDS store (one memory
+        // latency per chunk instead of one per 64 words)
         const int NWR = RG + 2;
         const int nw = H * NWR;
-        for (int i = lane; i < nw; i += 64) {
-            const int r = i / NWR, j = i - r * NWR;
-            const uintptr_t a = (uintptr_t)(base + (int64_t)r * pitch + 4 * j - 1);
-            const uint32_t *aw = (const uint32_t *)(a & ~(uintptr_t)3);
-            const uint32_t v = __builtin_amdgcn_alignbyte(aw[1], aw[0], (uint32_t)(a & 3));
-            *(uint32_t *)(tile + r * P + 4 * j) = v;
+        for (int i0 = 0; i0 < nw; i0 += 8 * 64) {
+            uint32_t lo[8], hi[8], sh[8];
+            int dst[8];
+#pragma unroll
+            for (int k = 0; k < 8; k++) {
+                const int i = i0 + 64 * k + lane;
+                lo[k] = hi[k] = sh[k] = 0;
+                dst[k] = -1;
+                if (i < nw) {
+                    const int r = i / NWR, j = i - r * NWR;
+                    const uintptr_t a = (uintptr_t)(base + (int64_t)r * pitch + 4 * j - 1);
+                    const uint32_t *aw = (const uint32_t *)(a & ~(uintptr_t)3);
+                    lo[k] = aw[0];
+                    hi[k] = aw[1];
+                    sh[k] = (uint32_t)(a & 3);
+                    dst[k] = r * P + 4 * j;
+                }
+            }
+#pragma unroll
+            for (int k = 0; k < 8; k++)
+                if (dst[k] >= 0)
+                    *(uint32_t *)(tile + dst[k]) = __builtin_amdgcn_alignbyte(hi[k], lo[k], sh[k]);
         }
         uint32_t *z = (uint32_t *)sc;
         const int nz = (RH + 2) * (P >> 2);
         for (int i = lane; i < nz; i += 64) z[i] = 0;
     }
     wave_sync_lds();
+    if (g->dbg == 11) return;
 
+    // unit u = ry * RG + gg walked as u = lane + 64 k: (ry, gg) advance by (64 / RG, 64 % RG)
+    const int rstep = RG > 0 ? 64 / RG : 0, gstep = RG > 0 ? 64 - rstep * RG : 0;
+    const int ry0 = RG > 0 ? lane / RG : 0, gg0 = lane - ry0 * RG;
     // ---- scores ----
-    for (int u = lane; u < nunits; u += 64) {
-        const int ry = u / RG, gg = u - ry * RG;
+    for (int u = lane, ry = ry0, gg = gg0; u < nunits; u += 64) {
         Rows7 R;
 #pragma unroll
         for (int r = 0; r < 7; r++) {
@@ -332,82 +369,132 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(6, 8))) voi
         const int valid = min(RW - 4 * gg, 4);
         if (valid < 4) word &= (1u << (8 * valid)) - 1u;
         *(uint32_t *)(sc + (ry + 1) * P + 4 * gg + 4) = word;
+        ry += rstep;
+        gg += gstep;
+        if (gg >= RG) {
+            gg -= RG;
+            ry++;
+        }
     }
     wave_sync_lds();
+    if (g->dbg == 12) return;
 
-    // ---- NMS (cell-local) at threshold th + raster-order compaction ----
+    // ---- NMS (cell-local), both thresholds in one pass ----
+    // cv::FAST keeps p iff s_p > every neighbour's score, a neighbour that is not a corner
+    // at the cell threshold th counting as 0.  With s_p >= max(th, 1) that is exactly
+    //   max(raw 8-neighbour scores) < max(th, s_p)
+    // (a neighbour q < th is always below max(th, s_p); one with q >= th must be < s_p).
+    // Pixel pairs in packed u16 lanes; the mask byte of unit u (low nibble at iniThFAST,
+    // high nibble at minThFAST) goes to the window tile, which is free by now.
+    uint8_t *mk = tile;
+    const int thi = g->ini_th, tlo = g->min_th;
+    const v2s vt1h = (v2s){(short)max(thi, 1), (short)max(thi, 1)};
+    const v2s vt1l = (v2s){(short)max(tlo, 1), (short)max(tlo, 1)};
+    const v2s vthh = (v2s){(short)thi, (short)thi}, vthl = (v2s){(short)tlo, (short)tlo};
+    const v2s one = (v2s){1, 1};
+    int cnt_hi = 0;
+    for (int u = lane, ry = ry0, gg = gg0; u < nunits; u += 64) {
+        const uint32_t *mu = (const uint32_t *)(sc + ry * P + 4 * gg);
+        const uint32_t *m0 = (const uint32_t *)(sc + (ry + 1) * P + 4 * gg);
+        const uint32_t *md = (const uint32_t *)(sc + (ry + 2) * P + 4 * gg);
+        const uint32_t c1 = m0[1];
+        uint32_t mbyte = 0;
+        if (c1 != 0) {  // a unit with no scored pixel keeps nothing at any threshold
+            const uint32_t u0 = mu[0], u1 = mu[1], u2 = mu[2];
+            const uint32_t c0 = m0[0], c2 = m0[2];
+            const uint32_t d0 = md[0], d1 = md[1], d2 = md[2];
+            // pixels 0,1 (bytes 4,5): neighbours at bytes 3..6
+            v2s mA = pmax(pmax(gather2<3>(u0, u1, u2), gather2<4>(u0, u1, u2)),
+                          gather2<5>(u0, u1, u2));
+            mA = pmax(mA, pmax(pmax(gather2<3>(d0, d1, d2), gather2<4>(d0, d1, d2)),
+                               gather2<5>(d0, d1, d2)));
+            mA = pmax(mA, pmax(gather2<3>(c0, c1, c2), gather2<5>(c0, c1, c2)));
+            // pixels 2,3 (bytes 6,7): neighbours at bytes 5..8
+            v2s mB = pmax(pmax(gather2<5>(u0, u1, u2), gather2<6>(u0, u1, u2)),
+                          gather2<7>(u0, u1, u2));
+            mB = pmax(mB, pmax(pmax(gather2<5>(d0, d1, d2), gather2<6>(d0, d1, d2)),
+                               gather2<7>(d0, d1, d2)));
+            mB = pmax(mB, pmax(gather2<5>(c0, c1, c2), gather2<7>(c0, c1, c2)));
+            const v2s sA = gather2<4>(c0, c1, c2), sB = gather2<6>(c0, c1, c2);
+            // keep <=> min(s - t1, max(th, s) - M - 1) >= 0: sign bit of each u16 lane
+            auto keep = [&](v2s sv, v2s m, v2s t1v, v2s thv) -> uint32_t {
+                const v2s k = pmin(sv - t1v, pmax(thv, sv) - m - one);
+                const uint32_t w = __builtin_bit_cast(uint32_t, k);
+                return (~w >> 15 & 1u) | (~w >> 30 & 2u);
+            };
+            const uint32_t kh = keep(sA, mA, vt1h, vthh) | keep(sB, mB, vt1h, vthh) << 2;
+            const uint32_t kl = keep(sA, mA, vt1l, vthl) | keep(sB, mB, vt1l, vthl) << 2;
+            const int valid = min(RW - 4 * gg, 4);
+            const uint32_t vm = valid < 4 ? (1u << valid) - 1u : 0xFu;
+            mbyte = (kh & vm) | (kl & vm) << 4;
+            cnt_hi += __popc(kh & vm);
+        }
+        mk[u] = (uint8_t)mbyte;
+        ry += rstep;
+        gg += gstep;
+        if (gg >= RG) {
+            gg -= RG;
+            ry++;
+        }
+    }
+    // FAST at iniThFAST; an empty cell retries at minThFAST (ORBextractor.cc:1069-1075)
+    const int nib = wave_sum(cnt_hi) > 0 ? 0 : 4;
+    wave_sync_lds();
+    if (g->dbg == 13) return;
+
+    // ---- raster-order compaction ----
     const int64_t slot = (int64_t)f * g->ncells + c;
     uint2 *out = cell_kp + slot * g->cell_cap;
-    const int xo = cl.x0 - ORBG_MIN_BORDER + 3, yo = cl.y0 - ORBG_MIN_BORDER + 3;
-    const uint32_t *xs = ctab + g->lv[l].xs_off, *ys = ctab + g->lv[l].ys_off;
-    auto nms_compact = [&](int th) -> int {
-        const int t1 = max(th, 1);
-        int run = 0;
-        for (int u0 = 0; u0 < nunits; u0 += 64) {
-            const int u = u0 + lane;
-            uint32_t mask = 0, c1 = 0;
-            int ry = 0, gg = 0;
-            if (u < nunits) {
-                ry = u / RG;
-                gg = u - ry * RG;
-                const uint32_t *m0 = (const uint32_t *)(sc + (ry + 1) * P + 4 * gg);
-                c1 = m0[1];
-                // quick reject: no byte >= max(th, 1)
-                const int mx = max(max((int)(c1 & 0xFF), (int)((c1 >> 8) & 0xFF)),
-                                   max((int)((c1 >> 16) & 0xFF), (int)(c1 >> 24)));
-                if (mx >= t1) {
-                    const uint32_t *mu = (const uint32_t *)(sc + ry * P + 4 * gg);
-                    const uint32_t *md = (const uint32_t *)(sc + (ry + 2) * P + 4 * gg);
-                    const uint32_t row[3][3] = {{mu[0], mu[1], mu[2]}, {m0[0], c1, m0[2]},
-                                                {md[0], md[1], md[2]}};
-#pragma unroll
-                    for (int i = 0; i < 4; i++) {
-                        const int s = (c1 >> (8 * i)) & 0xFF;
-                        if (s < t1) continue;
-                        bool keep = true;
-#pragma unroll
-                        for (int rr = 0; rr < 3; rr++)
-#pragma unroll
-                            for (int dx = -1; dx <= 1; dx++) {
-                                if (rr == 1 && dx == 0) continue;
-                                const int off = 4 + i + dx;  // byte in the 12-byte window
-                                const int q = (row[rr][off >> 2] >> (8 * (off & 3))) & 0xFF;
-                                const int qe = q >= th ? q : 0;
-                                keep = keep && (s > qe);
-                            }
-                        if (keep) mask |= 1u << i;
-                    }
-                }
+    int run = 0;
+    for (int u0 = 0, ry = ry0, gg = gg0; u0 < nunits; u0 += 64) {
+        const int u = u0 + lane;
+        const uint32_t mask = u < nunits ? (mk[u] >> nib) & 0xFu : 0u;
+        const int n = __popc(mask);
+        int tot;
+        const int incl = wave_incl_scan_small(n, &tot);
+        if (tot == 0) {  // wave-uniform
+            ry += rstep;
+            gg += gstep;
+            if (gg >= RG) {
+                gg -= RG;
+                ry++;
             }
-            const int n = __popc(mask);
-            const int incl = wave_incl_scan(n);
+            continue;
+        }
+        // path codes by shuffle, all lanes active (a lane past the region reads lane 0)
+        const uint32_t cy = (uint32_t)__shfl((int)ys_l, ry & 63, 64);
+        uint32_t cx[4];
+#pragma unroll
+        for (int i = 0; i < 4; i++) cx[i] = (uint32_t)__shfl((int)xs_l, (4 * gg + i) & 63, 64);
+        if (mask) {
             int off = run + incl - n;
+            const uint32_t c1 = *(const uint32_t *)(sc + (ry + 1) * P + 4 * gg + 4);
+            const int x0 = xo + 4 * gg, y = yo + ry;
 #pragma unroll
             for (int i = 0; i < 4; i++)
-                if (mask & (1u << i)) {
-                    const int x = xo + 4 * gg + i, y = yo + ry;
-                    out[off++] = make_uint2(orbg_pack(x, y, (c1 >> (8 * i)) & 0xFF),
-                                            xs[x] | ys[y]);
-                }
-            run += __shfl(incl, 63, 64);
+                if (mask & (1u << i))
+                    out[off++] = make_uint2(orbg_pack(x0 + i, y, (c1 >> (8 * i)) & 0xFF),
+                                            cx[i] | cy);
         }
-        return run;
-    };
-    // FAST at iniThFAST; an empty cell retries at minThFAST (ORBextractor.cc:1069-1075).
-    // A pass that keeps nothing wrote nothing, so the retry simply overwrites from 0.
-    int run = nms_compact(g->ini_th);
-    if (run == 0) run = nms_compact(g->min_th);
+        run += tot;
+        ry += rstep;
+        gg += gstep;
+        if (gg >= RG) {
+            gg -= RG;
+            ry++;
+        }
+    }
     if (lane == 0) cell_cnt[slot] = run;
 }
 
 // ---------------------------------------------------------------------------
 // k_blur: GaussianBlur(7x7, sigma 2, BORDER_REFLECT_101), bit-exact fixed point
 // out = sat((sum_v k_v * sum_h k_h * p + 2^15) >> 16).
-// 128x32 output tile per 256-thread workgroup.  The (128+8)x38 input tile (x origin
-// aligned at tile_x0 - 4) is filled with coalesced byte loads and a branch-free
-// reflection; the row pass keeps u16 sums (<= 256*255) in LDS; the column pass reads
-// 4 sums per ds_read_b64 and stores 4 output pixels per dword.
-// blockIdx.x enumerates tiles of all levels (tile_base per level).
+// 128x32 output tile per 256-thread workgroup.  The (128+8)x38 input tile (x origin at
+// tile_x0 - 4) is filled with aligned dword pairs + v_alignbyte (REFLECT_101 bytes at the
+// image edges), all loads issued before the LDS stores; the row pass keeps u16 sums
+// (<= 256*255) in LDS; the column pass reads 4 sums per ds_read_b64 and stores 4 output
+// pixels per dword.  The 1-D grid enumerates (frame, tile of any level), XCD-remapped.
 // ---------------------------------------------------------------------------
 #define BLUR_TW 128
 #define BLUR_TH 32
@@ -452,23 +539,39 @@ __global__ __launch_bounds__(256) void k_blur(const OrbgGeom *__restrict__ g,
     // fill: column c of the tile is image x = tx0 - 4 + c, row r is y = ty0 - 3 + r.
     // Word j of a row = x0 .. x0+3 (x0 = tx0 - 4 + 4j): aligned dword pair + v_alignbyte
     // when x0 .. x0+7 lies inside the row, else bytes with REFLECT_101.
-    for (int i = tid; i < BLUR_IH * (BLUR_IW / 4); i += 256) {
-        const int r = i / (BLUR_IW / 4), j = i - r * (BLUR_IW / 4);
-        const int y = reflect101(min(ty0 - 3 + r, H + 2), H);
-        const uint8_t *row = src + (int64_t)y * pitch;
-        const int x0 = tx0 - 4 + 4 * j;
-        uint32_t v;
-        if (x0 >= 0 && x0 + 7 < W) {
-            const uintptr_t a = (uintptr_t)(row + x0);
-            const uint32_t *aw = (const uint32_t *)(a & ~(uintptr_t)3);
-            v = __builtin_amdgcn_alignbyte(aw[1], aw[0], (uint32_t)(a & 3));
-        } else {
-            v = 0;
+    constexpr int NFILL = (BLUR_IH * (BLUR_IW / 4) + 255) / 256;  // words per thread
+    {
+        uint32_t lo[NFILL], hi[NFILL], sh[NFILL];
 #pragma unroll
-            for (int b = 0; b < 4; b++)
-                v |= (uint32_t)row[reflect101(min(x0 + b, W + 2), W)] << (8 * b);
+        for (int k = 0; k < NFILL; k++) {  // issue every load first
+            const int i = tid + 256 * k;
+            lo[k] = hi[k] = sh[k] = 0;
+            if (i < BLUR_IH * (BLUR_IW / 4)) {
+                const int r = i / (BLUR_IW / 4), j = i - r * (BLUR_IW / 4);
+                const int y = reflect101(min(ty0 - 3 + r, H + 2), H);
+                const uint8_t *row = src + (int64_t)y * pitch;
+                const int x0 = tx0 - 4 + 4 * j;
+                if (x0 >= 0 && x0 + 7 < W) {
+                    const uintptr_t a = (uintptr_t)(row + x0);
+                    const uint32_t *aw = (const uint32_t *)(a & ~(uintptr_t)3);
+                    lo[k] = aw[0];
+                    hi[k] = aw[1];
+                    sh[k] = (uint32_t)(a & 3);
+                } else {
+#pragma unroll
+                    for (int b = 0; b < 4; b++)
+                        lo[k] |= (uint32_t)row[reflect101(min(x0 + b, W + 2), W)] << (8 * b);
+                }
+            }
         }
-        *(uint32_t *)&in[r][4 * j] = v;
+#pragma unroll
+        for (int k = 0; k < NFILL; k++) {
+            const int i = tid + 256 * k;
+            if (i < BLUR_IH * (BLUR_IW / 4)) {
+                const int r = i / (BLUR_IW / 4), j = i - r * (BLUR_IW / 4);
+                *(uint32_t *)&in[r][4 * j] = __builtin_amdgcn_alignbyte(hi[k], lo[k], sh[k]);
+            }
+        }
     }
     __syncthreads();
     const int k0 = g->gk[0], k1 = g->gk[1], k2 = g->gk[2], k3 = g->gk[3], k4 = g->gk[4],

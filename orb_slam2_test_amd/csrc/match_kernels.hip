@@ -639,24 +639,30 @@ int launch_knn2(hipStream_t st, const uint8_t *q, int nq, const uint8_t *t, int 
     return hipGetLastError() == hipSuccess ? ORBG_OK : ORBG_EIO;
 }
 
-int launch_match_pairs(hipStream_t st, const uint8_t *desc, const orbg_keypoint *kps,
+int launch_match_pairs(hipStream_t st, hipStream_t aux, hipEvent_t evf, hipEvent_t evj,
+                       const uint8_t *desc, const orbg_keypoint *kps,
                        const int32_t *counts, int fc, const int32_t *d_f1, const int32_t *d_f2,
                        int npairs, int w, int h, int window, float nnratio, int check_ori,
                        int32_t *knn, int32_t *m12, int32_t *nm, uint32_t *topk, int32_t *topk_n,
                        void *prof)
 {
     if (fc > RESOLVE_N2_CAP || fc > (1 << 20)) return ORBG_ENOTSUP;
-    PL(prof, st, "knn2",
-       hipLaunchKernelGGL(k_knn2_pairs, dim3((fc + 255) / 256 * npairs), dim3(256), 0, st, desc,
-                          counts, fc, d_f1, d_f2, knn));
     PL(prof, st, "init_cands",
        hipLaunchKernelGGL(k_init_cands_pairs, dim3((fc + 4 * INIT_QPW - 1) / (4 * INIT_QPW) * npairs),
                           dim3(256), 0, st, kps, desc, counts, fc, d_f1, d_f2, w, h, window,
                           (unsigned long long *)topk, topk_n));
+    // knn2 (VALU bound) on `aux` beside init_resolve (one sequential workgroup per pair)
+    if (hipEventRecord(evf, st) != hipSuccess || hipStreamWaitEvent(aux, evf, 0) != hipSuccess)
+        return ORBG_EIO;
+    PL(prof, aux, "knn2",
+       hipLaunchKernelGGL(k_knn2_pairs, dim3((fc + 255) / 256 * npairs), dim3(256), 0, aux, desc,
+                          counts, fc, d_f1, d_f2, knn));
+    if (hipEventRecord(evj, aux) != hipSuccess) return ORBG_EIO;
     PL(prof, st, "init_resolve",
        hipLaunchKernelGGL(k_init_resolve_pairs, dim3(npairs), dim3(RESOLVE_T), 0, st, kps, desc, counts,
                           fc, d_f1, d_f2, w, h, window, nnratio, check_ori,
                           (const unsigned long long *)topk, topk_n, m12, nm));
+    if (hipStreamWaitEvent(st, evj, 0) != hipSuccess) return ORBG_EIO;
     return hipGetLastError() == hipSuccess ? ORBG_OK : ORBG_EIO;
 }
 

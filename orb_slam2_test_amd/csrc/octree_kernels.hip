@@ -25,7 +25,7 @@ namespace orbg {
 #define OCT_CODE_DEPTH 14
 
 #define OCT_NBUCKET 16384  // counting-sort buckets: root (4 bits) + first 5 quadtree digits
-#define OCT_BSHIFT 18
+#define OCT_BSHIFT 18      // code >> 18 = root (4 bits) + digits 0..4
 
 struct OctLdsShared {
     uint32_t codes[OCT_KEY_CAP];
@@ -110,11 +110,36 @@ __device__ void flip_bitonic_u64(unsigned long long *v, int n)
     }
 }
 
+// Candidates sit in counting-sort bucket order (root + first OCT_BDEPTH digits), unordered
+// inside a bucket.  A node shallower than OCT_BDEPTH is a run of whole buckets, so its next
+// digit is already monotone; a node of depth OCT_BDEPTH is exactly one bucket and is put in
+// full-code order (insertion sort, buckets hold a handful of keys) by the one thread that
+// splits it -- every deeper node is a sub-range of it.  Idempotent.
+#define OCT_BDEPTH 5
+
+__device__ __forceinline__ void oct_sort_bucket(uint32_t *codes, uint16_t *sidx, int lo, int hi)
+{
+    for (int i = lo + 1; i < hi; i++) {
+        const uint32_t c = codes[i];
+        if (codes[i - 1] <= c) continue;
+        const uint16_t v = sidx[i];
+        int j = i - 1;
+        while (j >= lo && codes[j] > c) {
+            codes[j + 1] = codes[j];
+            sidx[j + 1] = sidx[j];
+            j--;
+        }
+        codes[j + 1] = c;
+        sidx[j + 1] = v;
+    }
+}
+
 // children of the node record r: child start offsets b[0..4] (b[0] = lo, b[4] = lo + cnt)
-__device__ __forceinline__ void oct_children(const uint32_t *codes, unsigned long long r,
-                                             int b[5])
+__device__ __forceinline__ void oct_children(uint32_t *codes, uint16_t *sidx,
+                                             unsigned long long r, int b[5])
 {
     const int lo = rec_lo(r), hi = lo + rec_cnt(r), d = rec_depth(r);
+    if (d == OCT_BDEPTH) oct_sort_bucket(codes, sidx, lo, hi);
     const int shift = 26 - 2 * d;
     b[0] = lo;
     b[4] = hi;
@@ -143,7 +168,7 @@ __global__ __launch_bounds__(OCT_T) void k_octree_lds(
     const OrbgLevel &lv = g->lv[l];
     const int64_t kbase = (int64_t)f * g->keys_frame + lv.key_off;
     uint32_t *kglob = keys_all + kbase;
-    uint2 *pairs = (uint2 *)(scratch_all + 2 * kbase);  // 2 words per candidate
+    (void)scratch_all;
     const int N = lv.nfeat, nIni = lv.nini;
 
     // ---- candidate count; larger levels (or > ALIVE-1 cells) belong to k_octree ----
@@ -249,43 +274,6 @@ __global__ __launch_bounds__(OCT_T) void k_octree_lds(
         }
     }
     __syncthreads();
-    // ---- order inside each bucket: rank of every key among its bucket (a bucket spans
-    //      ~1/32 x 1/32 of a root, so it holds few keys), written through global scratch ----
-    auto bucket_end = [&](int b) -> int {
-        return b < 0 ? 0 : (int)((S.u.bcnt[b >> 1] >> (16 * (b & 1))) & 0xFFFF);
-    };
-    for (int p0 = tid; p0 < n; p0 += 4 * OCT_T) {
-        uint32_t c[4], v[4];
-        int lo[4], hi[4];
-#pragma unroll
-        for (int u = 0; u < 4; u++) {
-            const int p = p0 + u * OCT_T;
-            c[u] = p < n ? S.codes[p] : 0;
-            v[u] = p < n ? S.sidx[p] : 0;
-            const int b = (int)(c[u] >> OCT_BSHIFT);
-            lo[u] = p < n ? bucket_end(b - 1) : 0;
-            hi[u] = p < n ? bucket_end(b) : 0;
-        }
-#pragma unroll
-        for (int u = 0; u < 4; u++) {
-            int rank = 0;
-            for (int q = lo[u]; q < hi[u]; q++) rank += S.codes[q] < c[u];
-            if (p0 + u * OCT_T < n) pairs[lo[u] + rank] = make_uint2(c[u], v[u]);
-        }
-    }
-    __syncthreads();
-    for (int p0 = tid; p0 < n; p0 += 4 * OCT_T) {
-        uint2 e[4];
-#pragma unroll
-        for (int u = 0; u < 4; u++) e[u] = p0 + u * OCT_T < n ? pairs[p0 + u * OCT_T] : make_uint2(0, 0);
-#pragma unroll
-        for (int u = 0; u < 4; u++)
-            if (p0 + u * OCT_T < n) {
-                S.codes[p0 + u * OCT_T] = e[u].x;
-                S.sidx[p0 + u * OCT_T] = (uint16_t)e[u].y;
-            }
-    }
-    __syncthreads();
     if (g->dbg == 2) return;
 
     // ---- roots (:705-739): contiguous by the top 4 code bits ----
@@ -338,7 +326,7 @@ __global__ __launch_bounds__(OCT_T) void k_octree_lds(
                             S.s_err = 4;
                         } else {
                             sp = 1;
-                            oct_children(S.codes, r, bb[ch]);
+                            oct_children(S.codes, S.sidx, r, bb[ch]);
 #pragma unroll
                             for (int q = 0; q < 4; q++) {
                                 e += bb[ch][q + 1] > bb[ch][q];
@@ -449,7 +437,7 @@ __global__ __launch_bounds__(OCT_T) void k_octree_lds(
                         const unsigned long long r = S.u.q.list[cur][pos];
                         if (rec_depth(r) >= OCT_CODE_DEPTH) S.s_err = 6;
                         int b[5];
-                        oct_children(S.codes, r, b);
+                        oct_children(S.codes, S.sidx, r, b);
                         int e = 0;
 #pragma unroll
                         for (int q = 0; q < 4; q++) e += b[q + 1] > b[q];
@@ -471,7 +459,7 @@ __global__ __launch_bounds__(OCT_T) void k_octree_lds(
                 if (p < nproc) {
                     const int pos = (int)(S.u.q.sortv[np - 1 - p] & 0xFFFF);
                     int b[5];
-                    oct_children(S.codes, S.u.q.list[cur][pos], b);
+                    oct_children(S.codes, S.sidx, S.u.q.list[cur][pos], b);
 #pragma unroll
                     for (int q = 0; q < 4; q++) e += b[q + 1] > b[q];
                     S.aux[pos] = 1;  // processed parent
@@ -489,7 +477,7 @@ __global__ __launch_bounds__(OCT_T) void k_octree_lds(
                     if (p < nproc) {
                         const int pos = (int)(S.u.q.sortv[np - 1 - p] & 0xFFFF);
                         r = S.u.q.list[cur][pos];
-                        oct_children(S.codes, r, b);
+                        oct_children(S.codes, S.sidx, r, b);
 #pragma unroll
                         for (int q = 0; q < 4; q++) e += b[q + 1] > b[q];
                     }

@@ -35,7 +35,8 @@ __global__ void k_orient_desc(const OrbgGeom *, const uint8_t *, int64_t, int, c
                               const uint8_t *, const uint32_t *, const int32_t *,
                               OrbgKeypointDev *, uint8_t *, int32_t *);
 // match_kernels.hip
-int launch_match_pairs(hipStream_t st, const uint8_t *desc, const orbg_keypoint *kps,
+int launch_match_pairs(hipStream_t st, hipStream_t aux, hipEvent_t evf, hipEvent_t evj,
+                       const uint8_t *desc, const orbg_keypoint *kps,
                        const int32_t *counts, int frame_cap, const int32_t *d_f1,
                        const int32_t *d_f2, int npairs, int w, int h, int window, float nnratio,
                        int check_ori, int32_t *knn, int32_t *m12, int32_t *nm, uint32_t *topk,
@@ -148,12 +149,13 @@ struct Prof {
 };
 }  // namespace orbg
 
+// events on `st`, the stream the kernel is launched on (a local in every caller)
 #define PROF_LAUNCH(ctxp, name, ...)                                                       \
     do {                                                                                   \
         hipEvent_t ev_a_ = nullptr;                                                        \
-        (ctxp)->prof.begin((ctxp)->stream, name, &ev_a_);                                  \
+        (ctxp)->prof.begin(st, name, &ev_a_);                                              \
         __VA_ARGS__;                                                                       \
-        (ctxp)->prof.end((ctxp)->stream, name, ev_a_);                                     \
+        (ctxp)->prof.end(st, name, ev_a_);                                                 \
     } while (0)
 
 // ---------------------------------------------------------------------------
@@ -164,6 +166,10 @@ struct orbg_ctx {
     orbg_params p{};
     hipStream_t stream = nullptr;
     hipStream_t own_stream = nullptr;
+    // second stream for independent work inside one call (blur beside FAST+quadtree, knn2
+    // beside SearchForInitialization); forked from / joined into `stream` with events
+    hipStream_t aux_stream = nullptr;
+    hipEvent_t ev_fork[2] = {nullptr, nullptr}, ev_join[2] = {nullptr, nullptr};
     float scale[16], inv_scale[16], sigma2[16], inv_sigma2[16];
     int32_t fpl[16], umax[16];
     // plan
@@ -532,7 +538,34 @@ static int plan(orbg_ctx *c, int w, int h, int batch)
             hmax = std::max(hmax, (int)cl.h);
         }
         const int rg = std::max(wmax - 6 + 3, 0) / 4;
-        G.fc_pitch = 4 * rg + 12;  // dwords 0..RG+1 of the window / score rows, + slack
+        // LDS row pitch (dwords) >= RG + 3; pick the one whose raster unit -> (row, group)
+        // mapping spreads a wave's 64 dword reads best over the 64 LDS banks, summed over
+        // the cells' distinct group counts (ds_read cost ~ worst bank multiplicity)
+        std::vector<int> rgs;
+        for (const OrbgCell &cl : cells) {
+            const int r = std::max((int)cl.w - 6 + 3, 0) / 4;
+            if (r > 0 && std::find(rgs.begin(), rgs.end(), r) == rgs.end()) rgs.push_back(r);
+        }
+        int best_w = rg + 3, best_cost = 1 << 30;
+        const int rows_per_wave = hmax + std::max(hmax - 6, 0) + 2;
+        for (int wd = rg + 3; wd <= rg + 3 + 64; wd++) {
+            if (wd > rg + 3 && rows_per_wave * 4 * wd > 16 * 1024) break;  // 4 waves <= 64 KB
+            int cost = 0;
+            for (int r : rgs)
+                for (int k = 0; k < 3; k++) {
+                    int hist[64] = {0}, mx = 0;
+                    for (int lane = 0; lane < 64; lane++) {
+                        const int b = ((lane / r) * wd + lane % r + k) & 63;
+                        mx = std::max(mx, ++hist[b]);
+                    }
+                    cost += mx;
+                }
+            if (cost < best_cost) {
+                best_cost = cost;
+                best_w = wd;
+            }
+        }
+        G.fc_pitch = 4 * best_w;  // dwords 0..RG+1 of the window / score rows, + slack
         G.fc_tile_rows = hmax;
         G.fc_wave_bytes = ((hmax + std::max(hmax - 6, 0) + 2) * G.fc_pitch + 15) & ~15;
         if (4 * G.fc_wave_bytes > 64 * 1024)
@@ -630,6 +663,15 @@ extern "C" int orbg_create(int device, const orbg_params *p, orbg_ctx **out)
         return set_err(ORBG_EIO, "hipStreamCreate failed");
     }
     c->stream = c->own_stream;
+    if (hipStreamCreateWithFlags(&c->aux_stream, hipStreamNonBlocking) != hipSuccess) {
+        hipStreamDestroy(c->own_stream);
+        delete c;
+        return set_err(ORBG_EIO, "hipStreamCreate failed");
+    }
+    for (int i = 0; i < 2; i++) {
+        hipEventCreateWithFlags(&c->ev_fork[i], hipEventDisableTiming);
+        hipEventCreateWithFlags(&c->ev_join[i], hipEventDisableTiming);
+    }
     *out = c;
     return ORBG_OK;
 }
@@ -644,6 +686,12 @@ extern "C" void orbg_destroy(orbg_ctx *c)
     free_plan(c);
     if (c->d_img) hipFree(c->d_img);
     if (c->d_scr) hipFree(c->d_scr);
+    if (c->aux_stream) hipStreamSynchronize(c->aux_stream);
+    for (int i = 0; i < 2; i++) {
+        if (c->ev_fork[i]) hipEventDestroy(c->ev_fork[i]);
+        if (c->ev_join[i]) hipEventDestroy(c->ev_join[i]);
+    }
+    if (c->aux_stream) hipStreamDestroy(c->aux_stream);
     if (c->own_stream) hipStreamDestroy(c->own_stream);
     delete c;
 }
@@ -977,7 +1025,8 @@ extern "C" int orbg_match_batch_device(orbg_ctx *c, const int32_t *f1, const int
                          hipMemcpyHostToDevice));
         c->h_pairs.swap(hp);
     }
-    int rc = launch_match_pairs(c->stream, c->d_desc, c->d_kps, c->d_counts, (int)fc, c->d_pairs,
+    int rc = launch_match_pairs(c->stream, c->aux_stream, c->ev_fork[1], c->ev_join[1],
+                                c->d_desc, c->d_kps, c->d_counts, (int)fc, c->d_pairs,
                                 c->d_pairs + c->pair_cap, npairs, c->geom.w, c->geom.h, window,
                                 nnratio, check_ori, c->d_knn, c->d_m12, c->d_nm, c->d_topk,
                                 c->d_topk_n, &c->prof);

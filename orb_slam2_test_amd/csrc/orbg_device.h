@@ -16,6 +16,23 @@ __device__ __forceinline__ int wave_incl_scan(int x)
     return x;
 }
 
+// inclusive wave prefix of small counts 0 <= x < 8 from three ballots (no shuffles);
+// *total = wave total
+__device__ __forceinline__ int wave_incl_scan_small(int x, int *total)
+{
+    int incl = 0, tot = 0;
+#pragma unroll
+    for (int b = 0; b < 3; b++) {
+        const unsigned long long m = __ballot((x >> b) & 1);
+        const int below = __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32),
+                                                    __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0));
+        incl += (below + ((x >> b) & 1)) << b;
+        tot += __popcll(m) << b;
+    }
+    *total = tot;
+    return incl;
+}
+
 __device__ __forceinline__ int wave_sum(int x)
 {
 #pragma unroll
