@@ -21,7 +21,7 @@
 
 namespace orbg {
 
-__constant__ int8_t c_pattern[1024] = {
+__device__ __attribute__((aligned(16))) int8_t pattern_i8[1024] = {
 #define ORBG_PAIR(a, b, c, d) a, b, c, d,
 #include "orb_pattern.inc"
 #undef ORBG_PAIR
@@ -1225,12 +1225,21 @@ __device__ float fast_atan2(float y, float x)
 }
 
 // ---------------------------------------------------------------------------
-// k_orient_desc: one wave per output keypoint (level-major, octree list order)
+// k_orient_desc: one wave per quadtree output slot (frame, level, list position); the
+// wave of a filled slot writes keypoint i = (keypoints of lower levels) + position, the
+// level-major order of ORBextractor.cc:1381.  Memory round trips per wave: the slot's key
+// word (issued together with the level counts), then the 31x31 unblurred patch (IC_Angle)
+// and the 37x37 blurred neighbourhood (every rotated rBRIEF sample lies within +-18 px)
+// together; the 512 samples are then read from LDS.
 // ---------------------------------------------------------------------------
 struct OrbgKeypointDev {
     float x, y, size, angle, response;
     int32_t octave, class_id;
 };
+
+#define OD_R 18                 // rBRIEF sample radius bound: 13 * sqrt(2) rounded
+#define OD_SPAN (2 * OD_R + 1)  // 37 rows
+#define OD_ROWB 48              // staged row: 3 x 16 bytes (37 bytes + up to 3 of alignment)
 
 __global__ __launch_bounds__(256) void k_orient_desc(
     const OrbgGeom *__restrict__ g, const uint8_t *__restrict__ img0, int64_t img_fs,
@@ -1238,26 +1247,34 @@ __global__ __launch_bounds__(256) void k_orient_desc(
     const uint32_t *__restrict__ lvl_kp, const int32_t *__restrict__ lvl_cnt,
     OrbgKeypointDev *__restrict__ kps, uint8_t *__restrict__ desc, int32_t *__restrict__ counts)
 {
-    const int nb = (g->frame_cap + 3) >> 2;  // blocks per frame
+    __shared__ uint4 bpatch[4][OD_SPAN * OD_ROWB / 16];
+    const int nb = (g->out_frame + 3) >> 2;  // blocks per frame
     const int id = xcd_remap(blockIdx.x, gridDim.x);
     const int f = id / nb, bx = id - f * nb;
-    const int lane = threadIdx.x & 63;
-    const int i = bx * (blockDim.x >> 6) + (threadIdx.x >> 6);
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    const int slot = bx * 4 + wv;
     const int L = g->L;
+    if (slot >= g->out_frame) return;
+    int level = 0;
+    while (level + 1 < L && slot >= g->lv[level + 1].out_off) level++;
+    const OrbgLevel &lv = g->lv[level];
+    const uint32_t key = lvl_kp[(int64_t)f * g->out_frame + slot];
     const int32_t *lc = lvl_cnt + (int64_t)f * L;
-    int total = 0, level = -1, idx = 0;
+    int before = 0, total = 0, cnt = 0;
     for (int l = 0; l < L; l++) {
         const int c = lc[l];
-        if (level < 0 && i < total + c) {
-            level = l;
-            idx = i - total;
-        }
+        before += l < level ? c : 0;
+        cnt = l == level ? c : cnt;
         total += c;
     }
-    if (bx == 0 && threadIdx.x == 0) counts[f] = total;
-    if (level < 0 || i >= g->frame_cap) return;
-    const OrbgLevel &lv = g->lv[level];
-    const uint32_t key = lvl_kp[(int64_t)f * g->out_frame + lv.out_off + idx];
+    if (slot == 0 && lane == 0) counts[f] = total;
+    const int pos = slot - lv.out_off;
+    if (pos >= cnt) return;
+    if (g->dbg == 31) {  // developer timing: key only
+        if (lane == 0) desc[((int64_t)f * g->frame_cap + before + pos) * 32] = (uint8_t)key;
+        return;
+    }
+    const int i = before + pos;
     const int x = orbg_px(key) + ORBG_MIN_BORDER, y = orbg_py(key) + ORBG_MIN_BORDER;
     const uint8_t *im;
     int pitch;
@@ -1268,64 +1285,104 @@ __global__ __launch_bounds__(256) void k_orient_desc(
         im = pyr + f * g->pyr_frame + lv.pyr_off;
         pitch = lv.pitch;
     }
-    // ---- IC_Angle (ORBextractor.cc:83-111): the 31 x 31 patch as 31 rows x 9 aligned
-    // dwords, all loads issued up front (5 per lane); each byte is weighted by (u, v) and
-    // masked to the circle |u| <= umax[|v|], then two wave reductions ----
+    // ---- issue every load up front, 16 bytes per lane: the unblurred 31-row patch and the
+    // blurred 37-row neighbourhood as 48-byte row chunks from the 4-byte-aligned row start
+    // (3 x dwordx4 per row; the level-0 pitch may be odd, so alignment is per row), and this
+    // lane's 4 rBRIEF tests (16 pattern bytes) ----
+    const int4 pat = ((const int4 *)pattern_i8)[lane];
+    const uint8_t *ctr = im + (int64_t)y * pitch + x;
+    uint4 wd[2];
+    int shv[2];
+#pragma unroll
+    for (int k = 0; k < 2; k++) {
+        const int w = lane + 64 * k;  // row v = w / 3 - 15, chunk c = w % 3
+        wd[k] = make_uint4(0, 0, 0, 0);
+        shv[k] = 0;
+        if (w < 31 * 3) {
+            const int r = w / 3, cw = w - r * 3;
+            const uintptr_t a = (uintptr_t)(ctr + (int64_t)(r - ORBG_HALF_PATCH) * pitch -
+                                            ORBG_HALF_PATCH);
+            wd[k] = *(const uint4 *)((a & ~(uintptr_t)3) + 16 * cw);
+            shv[k] = (int)(a & 3);
+        }
+    }
+    const int bpitch = lv.pitch;
+    const uint8_t *bl0 = blur + f * g->blur_frame + lv.blur_off + (int64_t)(y - OD_R) * bpitch +
+                         (x - OD_R);
+    const int bsh = (int)((uintptr_t)bl0 & 3);
+    const uint8_t *bw = bl0 - bsh;
+    uint4 bv[2];
+#pragma unroll
+    for (int k = 0; k < 2; k++) {
+        const int w = lane + 64 * k;
+        bv[k] = make_uint4(0, 0, 0, 0);
+        if (w < OD_SPAN * 3) {
+            const int r = w / 3, cw = w - r * 3;
+            bv[k] = *(const uint4 *)(bw + (int64_t)r * bpitch + 16 * cw);
+        }
+    }
+    // ---- IC_Angle (ORBextractor.cc:83-111): bytes weighted by (u, v), masked to the
+    // circle |u| <= umax[|v|], two wave reductions ----
     int m01 = 0, m10 = 0;
-    {
-        const uint8_t *ctr = im + (int64_t)y * pitch + x;
-        uint32_t wd[5];
-        int shv[5];  // byte alignment of the row start (per row: the pitch may be odd)
 #pragma unroll
-        for (int k = 0; k < 5; k++) {
-            const int w = lane + 64 * k;  // row v = w / 9 - 15, word c = w % 9
-            wd[k] = 0;
-            shv[k] = 0;
-            if (w < 31 * 9) {
-                const int v = w / 9 - ORBG_HALF_PATCH, cw = w - (w / 9) * 9;
-                const uintptr_t a = (uintptr_t)(ctr + (int64_t)v * pitch - ORBG_HALF_PATCH);
-                wd[k] = ((const uint32_t *)(a & ~(uintptr_t)3))[cw];
-                shv[k] = (int)(a & 3);
+    for (int k = 0; k < 2; k++) {
+        const int w = lane + 64 * k;
+        if (w < 31 * 3) {
+            const int r = w / 3, cw = w - r * 3;
+            const int v = r - ORBG_HALF_PATCH;
+            const int um = g->umax[v < 0 ? -v : v];
+            const uint32_t q[4] = {wd[k].x, wd[k].y, wd[k].z, wd[k].w};
+            int su = 0, sv = 0;
+#pragma unroll
+            for (int b = 0; b < 16; b++) {
+                const int u = 16 * cw + b - shv[k] - ORBG_HALF_PATCH;
+                const int val = (q[b >> 2] >> (8 * (b & 3))) & 0xFF;
+                const int in = (u >= -um && u <= um) ? val : 0;
+                su += u * in;
+                sv += in;
             }
+            m10 += su;
+            m01 += v * sv;
         }
+    }
+    uint8_t *bp = (uint8_t *)bpatch[wv];
 #pragma unroll
-        for (int k = 0; k < 5; k++) {
-            const int w = lane + 64 * k;
-            if (w < 31 * 9) {
-                const int v = w / 9 - ORBG_HALF_PATCH, cw = w - (w / 9) * 9;
-                const int um = g->umax[v < 0 ? -v : v];
-#pragma unroll
-                for (int b = 0; b < 4; b++) {
-                    const int u = 4 * cw + b - shv[k] - ORBG_HALF_PATCH;
-                    const int val = (wd[k] >> (8 * b)) & 0xFF;
-                    if (u >= -um && u <= um) {
-                        m10 += u * val;
-                        m01 += v * val;
-                    }
-                }
-            }
+    for (int k = 0; k < 2; k++) {
+        const int w = lane + 64 * k;
+        if (w < OD_SPAN * 3) {
+            const int r = w / 3, cw = w - r * 3;
+            *(uint4 *)(bp + r * OD_ROWB + 16 * cw) = bv[k];
         }
+    }
+    wave_sync_lds();
+    if (g->dbg == 32) {  // developer timing: patches loaded and staged
+        if (lane == 0) desc[((int64_t)f * g->frame_cap + i) * 32] = (uint8_t)(m01 + m10 + bp[5]);
+        return;
     }
     m01 = wave_sum(m01);
     m10 = wave_sum(m10);
     const float angle = fast_atan2((float)m01, (float)m10);
+    if (g->dbg == 33) {  // developer timing: angle
+        if (lane == 0) desc[((int64_t)f * g->frame_cap + i) * 32] = (uint8_t)angle;
+        return;
+    }
 
-    // ---- rBRIEF on the blurred level: lane owns tests 4*lane .. 4*lane+3 ----
+    // ---- rBRIEF (ORBextractor.cc:117-157) from the staged blurred neighbourhood: lane
+    // owns tests 4*lane .. 4*lane+3 ----
     const float factorPI = (float)(3.14159265358979323846 / 180.f);
     double sd, cd;
     pinned_sincos((double)(angle * factorPI), &sd, &cd);
     const float a = (float)cd, b = (float)sd;
-    const uint8_t *bl = blur + f * g->blur_frame + lv.blur_off + (int64_t)y * lv.pitch + x;
-    const int bpitch = lv.pitch;
+    const uint8_t *bl = bp + OD_R * OD_ROWB + bsh + OD_R;  // centre
     int nib = 0;
 #pragma unroll
     for (int j = 0; j < 4; j++) {
-        const int t = 4 * lane + j;
         int val[2];
 #pragma unroll
         for (int s = 0; s < 2; s++) {
-            const float px = (float)c_pattern[4 * t + 2 * s];
-            const float py = (float)c_pattern[4 * t + 2 * s + 1];
+            const int pw = j == 0 ? pat.x : j == 1 ? pat.y : j == 2 ? pat.z : pat.w;
+            const float px = (float)(int8_t)(pw >> (16 * s));
+            const float py = (float)(int8_t)(pw >> (16 * s + 8));
             float ry, rx;
             if (g->brief_fma) {
                 ry = fmaf(px, b, py * a);
@@ -1335,7 +1392,7 @@ __global__ __launch_bounds__(256) void k_orient_desc(
                 ry = t0 + t1;
                 rx = t2 - t3;
             }
-            val[s] = bl[cv_round(ry) * bpitch + cv_round(rx)];
+            val[s] = bl[cv_round(ry) * OD_ROWB + cv_round(rx)];
         }
         nib |= (val[0] < val[1]) << j;
     }
