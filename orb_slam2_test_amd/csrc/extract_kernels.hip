@@ -89,26 +89,41 @@ __global__ __launch_bounds__(256) void k_resize(const uint8_t *__restrict__ src,
     const int sy_lo = ytab[r0].x & 0xFFFF;
     const int sy_hi = ytab[r1].x >> 16;
     const uint8_t *fb = src + f * sfs;
-    // ---- stage rows sy_lo..sy_hi, columns sx_lo..sx_hi ----
-    for (int r = wv; r <= sy_hi - sy_lo; r += 4) {
-        const uint8_t *row = fb + (int64_t)(sy_lo + r) * spitch;
-        const uint8_t *start = row + sx_lo;
-        const int sh = (int)((uintptr_t)start & 3);
-        const uint32_t *aw = (const uint32_t *)(start - sh);
-        const int nw = (sh + sx_hi - sx_lo + 1 + 3) >> 2;
-        uint32_t *dw32 = (uint32_t *)(lds + r * lds_pitch);
-        for (int k = lane; k < nw; k += 64) {
-            const uint8_t *wp = (const uint8_t *)(aw + k);
-            uint32_t v;
-            if (wp >= row && wp + 3 < row + sw) {
-                v = aw[k];
-            } else {  // first / last word of the row: only bytes inside [row, row + sw)
-                v = 0;
+    // ---- stage rows sy_lo..sy_hi, columns sx_lo..sx_hi: 16-byte chunks from each row's
+    // 4-byte-aligned start, every load issued before the LDS stores; a chunk reaching
+    // outside [row, row + sw) is assembled from its in-row bytes ----
+    {
+        const int nrow = sy_hi - sy_lo + 1;
+        const int nch = (3 + sx_hi - sx_lo + 1 + 15) >> 4;  // chunks per row (upper bound)
+        const int total = nrow * nch;
+        for (int i0 = 0; i0 < total; i0 += 4 * 256) {
+            uint4 q[4];
+            int dst[4];
 #pragma unroll
-                for (int b = 0; b < 4; b++)
-                    if (wp + b >= row && wp + b < row + sw) v |= (uint32_t)wp[b] << (8 * b);
+            for (int k = 0; k < 4; k++) {
+                const int i = i0 + 256 * k + tid;
+                q[k] = make_uint4(0, 0, 0, 0);
+                dst[k] = -1;
+                if (i < total) {
+                    const int r = i / nch, c = i - r * nch;
+                    const uint8_t *row = fb + (int64_t)(sy_lo + r) * spitch;
+                    const uint8_t *start = row + sx_lo;
+                    const uint8_t *cp = start - ((uintptr_t)start & 3) + 16 * c;
+                    if (cp >= row && cp + 16 <= row + sw) {
+                        q[k] = *(const uint4 *)cp;
+                    } else {
+                        uint32_t w4[4] = {0, 0, 0, 0};
+                        for (int b = 0; b < 16; b++)
+                            if (cp + b >= row && cp + b < row + sw)
+                                w4[b >> 2] |= (uint32_t)cp[b] << (8 * (b & 3));
+                        q[k] = make_uint4(w4[0], w4[1], w4[2], w4[3]);
+                    }
+                    dst[k] = r * lds_pitch + 16 * c;
+                }
             }
-            dw32[k] = v;
+#pragma unroll
+            for (int k = 0; k < 4; k++)
+                if (dst[k] >= 0) *(uint4 *)(lds + dst[k]) = q[k];
         }
     }
     // ---- per-thread column coefficients ----
@@ -498,7 +513,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(6, 8))) voi
 // ---------------------------------------------------------------------------
 #define BLUR_TW 128
 #define BLUR_TH 32
-#define BLUR_IW (BLUR_TW + 8)
+#define BLUR_IW (BLUR_TW + 16)  // 9 x 16-byte chunks from x = tile_x0 - 4 (135 bytes read)
 #define BLUR_IH (BLUR_TH + 6)
 
 __device__ __forceinline__ int reflect101(int i, int n)
@@ -539,66 +554,96 @@ __global__ __launch_bounds__(256) void k_blur(const OrbgGeom *__restrict__ g,
     // fill: column c of the tile is image x = tx0 - 4 + c, row r is y = ty0 - 3 + r.
     // Word j of a row = x0 .. x0+3 (x0 = tx0 - 4 + 4j): aligned dword pair + v_alignbyte
     // when x0 .. x0+7 lies inside the row, else bytes with REFLECT_101.
-    constexpr int NFILL = (BLUR_IH * (BLUR_IW / 4) + 255) / 256;  // words per thread
+    // 16-byte chunk c of a row = x0 .. x0+15 (x0 = tx0 - 4 + 16c): one dwordx4 from the
+    // aligned address + one dword for the v_alignbyte shift when x0 .. x0+19 lies inside
+    // the row, else bytes with REFLECT_101 (image edges only).  All loads first.
+    constexpr int NCH = BLUR_IW / 16;                      // chunks per row
+    constexpr int NFILL = (BLUR_IH * NCH + 255) / 256;     // chunks per thread
     {
-        uint32_t lo[NFILL], hi[NFILL], sh[NFILL];
+        uint4 q[NFILL];
+        uint32_t q4[NFILL], sh[NFILL];
 #pragma unroll
-        for (int k = 0; k < NFILL; k++) {  // issue every load first
+        for (int k = 0; k < NFILL; k++) {
             const int i = tid + 256 * k;
-            lo[k] = hi[k] = sh[k] = 0;
-            if (i < BLUR_IH * (BLUR_IW / 4)) {
-                const int r = i / (BLUR_IW / 4), j = i - r * (BLUR_IW / 4);
+            q[k] = make_uint4(0, 0, 0, 0);
+            q4[k] = sh[k] = 0;
+            if (i < BLUR_IH * NCH) {
+                const int r = i / NCH, c = i - r * NCH;
                 const int y = reflect101(min(ty0 - 3 + r, H + 2), H);
                 const uint8_t *row = src + (int64_t)y * pitch;
-                const int x0 = tx0 - 4 + 4 * j;
-                if (x0 >= 0 && x0 + 7 < W) {
+                const int x0 = tx0 - 4 + 16 * c;
+                if (x0 >= 0 && x0 + 20 <= W) {
                     const uintptr_t a = (uintptr_t)(row + x0);
                     const uint32_t *aw = (const uint32_t *)(a & ~(uintptr_t)3);
-                    lo[k] = aw[0];
-                    hi[k] = aw[1];
+                    q[k] = *(const uint4 *)aw;
                     sh[k] = (uint32_t)(a & 3);
+                    if (sh[k]) q4[k] = aw[4];
                 } else {
+                    uint32_t w4[4] = {0, 0, 0, 0};
 #pragma unroll
-                    for (int b = 0; b < 4; b++)
-                        lo[k] |= (uint32_t)row[reflect101(min(x0 + b, W + 2), W)] << (8 * b);
+                    for (int bb = 0; bb < 16; bb++)
+                        w4[bb >> 2] |= (uint32_t)row[reflect101(min(x0 + bb, W + 2), W)]
+                                       << (8 * (bb & 3));
+                    q[k] = make_uint4(w4[0], w4[1], w4[2], w4[3]);
                 }
             }
         }
 #pragma unroll
         for (int k = 0; k < NFILL; k++) {
             const int i = tid + 256 * k;
-            if (i < BLUR_IH * (BLUR_IW / 4)) {
-                const int r = i / (BLUR_IW / 4), j = i - r * (BLUR_IW / 4);
-                *(uint32_t *)&in[r][4 * j] = __builtin_amdgcn_alignbyte(hi[k], lo[k], sh[k]);
+            if (i < BLUR_IH * NCH) {
+                const int r = i / NCH, c = i - r * NCH;
+                const uint32_t t = sh[k];
+                uint4 o;
+                o.x = __builtin_amdgcn_alignbyte(q[k].y, q[k].x, t);
+                o.y = __builtin_amdgcn_alignbyte(q[k].z, q[k].y, t);
+                o.z = __builtin_amdgcn_alignbyte(q[k].w, q[k].z, t);
+                o.w = __builtin_amdgcn_alignbyte(q4[k], q[k].w, t);
+                *(uint4 *)&in[r][16 * c] = o;
             }
         }
     }
     __syncthreads();
     const int k0 = g->gk[0], k1 = g->gk[1], k2 = g->gk[2], k3 = g->gk[3], k4 = g->gk[4],
               k5 = g->gk[5], k6 = g->gk[6];
-    // row pass: unit = (row r, 4-column group j); outputs x = 4j..4j+3 need tile bytes 4j+1..4j+10
-    for (int u = tid; u < BLUR_IH * (BLUR_TW / 4); u += 256) {
-        const int r = u >> 5, j = u & 31;
-        const uint32_t *w = (const uint32_t *)&in[r][4 * j];
-        const uint32_t w0 = w[0], w1 = w[1], w2 = w[2];
-        int p[12];
-#pragma unroll
-        for (int b = 0; b < 4; b++) {
-            p[b] = (w0 >> (8 * b)) & 0xFF;
-            p[4 + b] = (w1 >> (8 * b)) & 0xFF;
-            p[8 + b] = (w2 >> (8 * b)) & 0xFF;
+    // row pass: unit = (row r, 4-column group j); outputs x = 4j..4j+3 need tile bytes
+    // 4j+1..4j+10.  Two outputs per packed u16 multiply-add: a row sum is at most
+    // sum(k) * 255 <= 257 * 255 = 65535 (orbg_create enforces sum(k) <= 257), so every
+    // partial sum is exact in 16 bits.
+    {
+        typedef unsigned short v2u __attribute__((ext_vector_type(2)));
+        const v2u kv[7] = {(v2u){(unsigned short)k0, (unsigned short)k0},
+                           (v2u){(unsigned short)k1, (unsigned short)k1},
+                           (v2u){(unsigned short)k2, (unsigned short)k2},
+                           (v2u){(unsigned short)k3, (unsigned short)k3},
+                           (v2u){(unsigned short)k4, (unsigned short)k4},
+                           (v2u){(unsigned short)k5, (unsigned short)k5},
+                           (v2u){(unsigned short)k6, (unsigned short)k6}};
+#define BG(off) __builtin_bit_cast(v2u, gather2<off>(w0, w1, w2))
+        for (int u = tid; u < BLUR_IH * (BLUR_TW / 4); u += 256) {
+            const int r = u >> 5, j = u & 31;
+            const uint32_t *w = (const uint32_t *)&in[r][4 * j];
+            const uint32_t w0 = w[0], w1 = w[1], w2 = w[2];
+            // outputs (4j, 4j+1): bytes (1+t, 2+t); outputs (4j+2, 4j+3): bytes (3+t, 4+t)
+            v2u a = kv[0] * BG(1), b = kv[0] * BG(3);
+            a += kv[1] * BG(2);
+            b += kv[1] * BG(4);
+            a += kv[2] * BG(3);
+            b += kv[2] * BG(5);
+            a += kv[3] * BG(4);
+            b += kv[3] * BG(6);
+            a += kv[4] * BG(5);
+            b += kv[4] * BG(7);
+            a += kv[5] * BG(6);
+            b += kv[5] * BG(8);
+            a += kv[6] * BG(7);
+            b += kv[6] * BG(9);
+            uint2 pk;
+            pk.x = __builtin_bit_cast(uint32_t, a);
+            pk.y = __builtin_bit_cast(uint32_t, b);
+            *(uint2 *)&rows[r][4 * j] = pk;
         }
-        uint32_t s[4];
-#pragma unroll
-        for (int o = 0; o < 4; o++) {
-            const int* q = &p[o + 1];
-            s[o] = (uint32_t)(k0 * q[0] + k1 * q[1] + k2 * q[2] + k3 * q[3] + k4 * q[4] +
-                              k5 * q[5] + k6 * q[6]);
-        }
-        uint2 pk;
-        pk.x = s[0] | (s[1] << 16);
-        pk.y = s[2] | (s[3] << 16);
-        *(uint2 *)&rows[r][4 * j] = pk;
+#undef BG
     }
     __syncthreads();
     // column pass: thread = (4-column group j, 4-row group rg)
@@ -618,7 +663,8 @@ __global__ __launch_bounds__(256) void k_blur(const OrbgGeom *__restrict__ g,
             const int tap = rr - o;
             if (tap >= 0 && tap < 7) {
 #pragma unroll
-                for (int b = 0; b < 4; b++) acc[o][b] += (uint32_t)kk[tap] * v[b];
+                for (int b = 0; b < 4; b++)  // 16-bit sum x weight <= 257: 24-bit multiply
+                    acc[o][b] = __umul24((uint32_t)kk[tap], v[b]) + acc[o][b];
             }
         }
     }

@@ -521,7 +521,7 @@ static int plan(orbg_ctx *c, int w, int h, int batch)
                 rows = std::max(rows, (rtab[L.ytab_off + r1].x >> 16) -
                                           (rtab[L.ytab_off + r0].x & 0xFFFF) + 1);
             }
-            L.rz_pitch = ((span + 3 + 3) / 4) * 4 + 4;
+            L.rz_pitch = ((span + 3 + 15) / 16) * 16;  // whole 16-byte chunks per row
             L.rz_rows = rows;
             if ((int64_t)L.rz_pitch * rows > 64 * 1024)
                 return set_err(ORBG_ENOTSUP, "level %d resize tile needs %d x %d LDS bytes", l,
@@ -643,7 +643,12 @@ extern "C" int orbg_create(int device, const orbg_params *p, orbg_ctx **out)
         prm.resize_mode != ORBG_RESIZE_SIMD_16_8)
         return set_err(ORBG_EINVAL, "resize_mode %d", prm.resize_mode);
     int ksum = 0;
-    for (int i = 0; i < 7; i++) ksum += prm.gauss_k[i];
+    for (int i = 0; i < 7; i++) {
+        if (prm.gauss_k[i] < 0) return set_err(ORBG_EINVAL, "gauss_k[%d] < 0", i);
+        ksum += prm.gauss_k[i];
+    }
+    // 16-bit row sums in k_blur: sum(k) * 255 must fit (both OpenCV tables: 256, 257)
+    if (ksum > 257) return set_err(ORBG_EINVAL, "gauss_k sums to %d (> 257)", ksum);
     if (ksum == 0) {
         const int32_t k[7] = {18, 34, 48, 56, 48, 34, 18};
         memcpy(prm.gauss_k, k, sizeof(k));
