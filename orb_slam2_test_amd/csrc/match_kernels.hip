@@ -644,14 +644,16 @@ int launch_match_pairs(hipStream_t st, hipStream_t aux, hipEvent_t evf, hipEvent
                        const int32_t *counts, int fc, const int32_t *d_f1, const int32_t *d_f2,
                        int npairs, int w, int h, int window, float nnratio, int check_ori,
                        int32_t *knn, int32_t *m12, int32_t *nm, uint32_t *topk, int32_t *topk_n,
-                       void *prof)
+                       void *prof, int serial)
 {
     if (fc > RESOLVE_N2_CAP || fc > (1 << 20)) return ORBG_ENOTSUP;
     PL(prof, st, "init_cands",
        hipLaunchKernelGGL(k_init_cands_pairs, dim3((fc + 4 * INIT_QPW - 1) / (4 * INIT_QPW) * npairs),
                           dim3(256), 0, st, kps, desc, counts, fc, d_f1, d_f2, w, h, window,
                           (unsigned long long *)topk, topk_n));
-    // knn2 (VALU bound) on `aux` beside init_resolve (one sequential workgroup per pair)
+    // knn2 (VALU bound) on `aux` beside init_resolve (one sequential workgroup per pair);
+    // serial == 1 (developer timing, ORBG_DBG=40) keeps it on `st`
+    if (serial) aux = st;
     if (hipEventRecord(evf, st) != hipSuccess || hipStreamWaitEvent(aux, evf, 0) != hipSuccess)
         return ORBG_EIO;
     PL(prof, aux, "knn2",

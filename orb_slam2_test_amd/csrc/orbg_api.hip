@@ -40,7 +40,7 @@ int launch_match_pairs(hipStream_t st, hipStream_t aux, hipEvent_t evf, hipEvent
                        const int32_t *counts, int frame_cap, const int32_t *d_f1,
                        const int32_t *d_f2, int npairs, int w, int h, int window, float nnratio,
                        int check_ori, int32_t *knn, int32_t *m12, int32_t *nm, uint32_t *topk,
-                       int32_t *topk_n, void *prof);
+                       int32_t *topk_n, void *prof, int serial);
 int launch_knn2(hipStream_t st, const uint8_t *q, int nq, const uint8_t *t, int nt, int32_t *out,
                 void *prof);
 int launch_init_match_single(hipStream_t st, const orbg_keypoint *k1, const uint8_t *d1, int n1,
@@ -1034,7 +1034,7 @@ extern "C" int orbg_match_batch_device(orbg_ctx *c, const int32_t *f1, const int
                                 c->d_desc, c->d_kps, c->d_counts, (int)fc, c->d_pairs,
                                 c->d_pairs + c->pair_cap, npairs, c->geom.w, c->geom.h, window,
                                 nnratio, check_ori, c->d_knn, c->d_m12, c->d_nm, c->d_topk,
-                                c->d_topk_n, &c->prof);
+                                c->d_topk_n, &c->prof, c->geom.dbg == 40);
     if (rc) return rc;
     c->last_npairs = npairs;
     return ORBG_OK;
