@@ -168,7 +168,6 @@ __global__ __launch_bounds__(OCT_T) void k_octree_lds(
     const OrbgLevel &lv = g->lv[l];
     const int64_t kbase = (int64_t)f * g->keys_frame + lv.key_off;
     uint32_t *kglob = keys_all + kbase;
-    (void)scratch_all;
     const int N = lv.nfeat, nIni = lv.nini;
 
     // ---- candidate count; larger levels (or > ALIVE-1 cells) belong to k_octree ----
@@ -189,39 +188,45 @@ __global__ __launch_bounds__(OCT_T) void k_octree_lds(
     for (int i = tid; i < OCT_NBUCKET / 2; i += OCT_T) S.u.bcnt[i] = 0;
     __syncthreads();
 
-    // flattened candidate k -> (cell, slot): largest c with cell_offset[c] <= k
-    auto cell_of = [&](int k) -> int {
-        int lo = 0, hi = ncells - 1;
-        while (lo < hi) {
-            const int mid = (lo + hi + 1) >> 1;
-            if ((int)S.aux[mid] <= k)
-                lo = mid;
-            else
-                hi = mid - 1;
-        }
-        return lo;
-    };
-    // ---- gather (vToDistributeKeys order) + bucket histogram ----
-    for (int k0 = tid; k0 < n; k0 += 4 * OCT_T) {
-        uint2 e[4];
-        int cc[4];
+    // ---- gather (vToDistributeKeys order: cell-major, FAST order inside a cell) +
+    //      bucket histogram: one wave per cell (lane = slot), four cells' loads in flight;
+    //      each candidate's path code also goes to global scratch for the scatter ----
+    uint32_t *cscr = scratch_all + 2 * kbase;  // flattened path codes
+    {
+        const int lane = tid & 63, wv = tid >> 6;
+        constexpr int NW = OCT_T / 64;
+        for (int c0 = wv; c0 < ncells; c0 += 4 * NW) {
+            uint2 e[4];
+            int k[4], cnt[4];
 #pragma unroll
-        for (int u = 0; u < 4; u++) {
-            const int k = k0 + u * OCT_T;
-            cc[u] = k < n ? cell_of(k) : 0;
-        }
+            for (int u = 0; u < 4; u++) {
+                const int c = c0 + u * NW;
+                cnt[u] = 0;
+                k[u] = 0;
+                e[u] = make_uint2(0, 0);
+                if (c < ncells) {
+                    const int lo = S.aux[c];
+                    cnt[u] = (int)S.aux[c + 1] - lo;
+                    k[u] = lo + lane;
+                    if (lane < cnt[u]) e[u] = ckp[(int64_t)c * g->cell_cap + lane];
+                }
+            }
 #pragma unroll
-        for (int u = 0; u < 4; u++) {
-            const int k = k0 + u * OCT_T;
-            e[u] = k < n ? ckp[(int64_t)cc[u] * g->cell_cap + (k - S.aux[cc[u]])] : make_uint2(0, 0);
-        }
-#pragma unroll
-        for (int u = 0; u < 4; u++) {
-            const int k = k0 + u * OCT_T;
-            if (k < n) {
-                kglob[k] = e[u].x;
-                const uint32_t b = e[u].y >> OCT_BSHIFT;
-                atomicAdd(&S.u.bcnt[b >> 1], 1u << (16 * (b & 1)));
+            for (int u = 0; u < 4; u++) {
+                if (lane < cnt[u]) {
+                    kglob[k[u]] = e[u].x;
+                    cscr[k[u]] = e[u].y;
+                    const uint32_t b = e[u].y >> OCT_BSHIFT;
+                    atomicAdd(&S.u.bcnt[b >> 1], 1u << (16 * (b & 1)));
+                }
+                for (int kl = lane + 64; kl < cnt[u]; kl += 64) {  // cells with > 64 corners
+                    const int c = c0 + u * NW;
+                    const uint2 x = ckp[(int64_t)c * g->cell_cap + kl];
+                    kglob[k[u] - lane + kl] = x.x;
+                    cscr[k[u] - lane + kl] = x.y;
+                    const uint32_t b = x.y >> OCT_BSHIFT;
+                    atomicAdd(&S.u.bcnt[b >> 1], 1u << (16 * (b & 1)));
+                }
             }
         }
     }
@@ -247,28 +252,22 @@ __global__ __launch_bounds__(OCT_T) void k_octree_lds(
         }
     }
     __syncthreads();
-    // ---- scatter into bucket order (unordered inside a bucket) ----
+    // ---- scatter into bucket order (unordered inside a bucket), codes read back flat ----
     for (int k0 = tid; k0 < n; k0 += 4 * OCT_T) {
-        uint2 e[4];
-        int cc[4];
+        uint32_t code[4];
 #pragma unroll
         for (int u = 0; u < 4; u++) {
             const int k = k0 + u * OCT_T;
-            cc[u] = k < n ? cell_of(k) : 0;
-        }
-#pragma unroll
-        for (int u = 0; u < 4; u++) {
-            const int k = k0 + u * OCT_T;
-            e[u] = k < n ? ckp[(int64_t)cc[u] * g->cell_cap + (k - S.aux[cc[u]])] : make_uint2(0, 0);
+            code[u] = k < n ? cscr[k] : 0u;
         }
 #pragma unroll
         for (int u = 0; u < 4; u++) {
             const int k = k0 + u * OCT_T;
             if (k < n) {
-                const uint32_t b = e[u].y >> OCT_BSHIFT;
+                const uint32_t b = code[u] >> OCT_BSHIFT;
                 const uint32_t old = atomicAdd(&S.u.bcnt[b >> 1], 1u << (16 * (b & 1)));
                 const int slot = (int)((old >> (16 * (b & 1))) & 0xFFFF);
-                S.codes[slot] = e[u].y;
+                S.codes[slot] = code[u];
                 S.sidx[slot] = (uint16_t)k;
             }
         }
