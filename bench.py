@@ -122,13 +122,18 @@ def main():
     f1 = ((np.arange(B) - 1) % B).astype(np.int32)
     f2 = np.arange(B, dtype=np.int32)
     summary = torch.zeros(2 * B, dtype=torch.int32, device="cuda")
+    # matching of step k (and its summary + gather) runs on liborbg's match stream while the
+    # extraction of step k+1 runs on `stream` (two output slots inside liborbg)
+    mstream = torch.cuda.ExternalStream(ext.ctx.match_stream())
+    torch.cuda.synchronize()
 
     def step():
         ext.extract_batch_device(d_frames.data_ptr(), B, W, H)
         ext.match_batch_device(f1, f2, 100, 0.9, True)
         ext.ctx.batch_summary(summary.data_ptr())
         if world > 1:  # trajectory summary of every rank's frames (RCCL all_gather)
-            sequence.gather_summary(summary.view(2, B), world, sizes=[B] * world)
+            with torch.cuda.stream(mstream):
+                sequence.gather_summary(summary.view(2, B), world, sizes=[B] * world)
 
     for _ in range(args.warmup):
         step()

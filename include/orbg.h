@@ -138,13 +138,19 @@ int orbg_match_outputs(orbg_ctx *ctx, int32_t **d_knn /* [npairs][frame_cap][3] 
 int orbg_download_matches(orbg_ctx *ctx, int pair, int32_t *knn, int32_t *matches12,
                           int cap, int32_t *nmatches);
 
+/* Extraction runs on the context stream; batch matching and the summary run on a second
+ * (match) stream so the matching of batch k overlaps the extraction of batch k+1.  The
+ * per-frame outputs alternate between two buffers (orbg_batch_outputs returns the ones of
+ * the last extraction); every host-side read (download, get_level, stats, sync) drains
+ * both streams. */
 int orbg_sync(orbg_ctx *ctx);
-void *orbg_stream(orbg_ctx *ctx); /* the hipStream_t the context launches on */
+void *orbg_stream(orbg_ctx *ctx);       /* hipStream_t of extraction (and host-data calls) */
+void *orbg_match_stream(orbg_ctx *ctx); /* hipStream_t of batch matching and the summary */
 /* launch on a caller-owned hipStream_t (e.g. torch's current stream) instead of the
  * context's own; NULL restores the context stream */
 int orbg_set_stream(orbg_ctx *ctx, void *stream);
-/* per-frame trajectory summary of the last batch, written on the context stream into a
- * device buffer: d_out[f] = keypoints of frame f (f < nframes), then
+/* per-frame trajectory summary of the last batch, written on the match stream into a
+ * device buffer (order readers after orbg_match_stream, or orbg_sync): d_out[f] = keypoints of frame f (f < nframes), then
  * d_out[nframes + p] = SearchForInitialization matches of pair p (p < npairs of the last
  * orbg_match_batch_device, 0 if none) */
 int orbg_batch_summary(orbg_ctx *ctx, int32_t *d_out);

@@ -94,6 +94,7 @@ def lib():
         "orbg_stream": (vp, [vp]),
         "orbg_set_stream": (i32, [vp, vp]),
         "orbg_batch_summary": (i32, [vp, vp]),
+        "orbg_match_stream": (vp, [vp]),
         "orbg_batch_stats": (i32, [vp, P(C.c_int64), P(C.c_int64)]),
         "orbg_profile_enable": (i32, [vp, i32]),
         "orbg_profile_read": (i32, [vp, i32, P(C.c_char_p), P(C.c_double), P(C.c_int64)]),
@@ -194,6 +195,10 @@ class Context:
         a, b = C.c_int64(), C.c_int64()
         check(self._L.orbg_batch_stats(self.handle, C.byref(a), C.byref(b)), "orbg_batch_stats")
         return a.value, b.value
+
+    def match_stream(self):
+        """hipStream_t (int) of batch matching and the summary."""
+        return self._L.orbg_match_stream(self.handle)
 
     def batch_summary(self, d_out_ptr):
         check(self._L.orbg_batch_summary(self.handle, C.c_void_p(d_out_ptr)), "orbg_batch_summary")

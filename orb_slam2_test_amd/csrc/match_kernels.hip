@@ -15,6 +15,7 @@
 //                     rare query whose K-list is exhausted by the filter.
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <climits>
 
 #include "../../include/orbg.h"
@@ -181,7 +182,7 @@ struct F2Key {
 };
 
 #define INIT_QPW 8   // queries per wave in k_init_cands
-#define INIT_F2_CAP 4096
+#define INIT_F2_CAP 4608  // host-data path bound (frame capacity at 4000 features)
 
 // one 256-thread block: load F2 level-0 keys to LDS, then each wave handles INIT_QPW queries
 __device__ void init_cands_block(const orbg_keypoint *__restrict__ k1,
@@ -190,9 +191,11 @@ __device__ void init_cands_block(const orbg_keypoint *__restrict__ k1,
                                  const uint8_t *__restrict__ d2, int n2, orbg_bounds b,
                                  const float *__restrict__ prev, int prev_stride, int window,
                                  unsigned long long *__restrict__ topk, int32_t *__restrict__ topn,
-                                 int qbase)
+                                 int qbase, int f2cap)
 {
-    __shared__ F2Key f2[INIT_F2_CAP];
+    // F2's level-0 keys, dynamic LDS of f2cap entries (batch: level-0 capacity; host-data
+    // path: n2)
+    extern __shared__ __attribute__((aligned(16))) F2Key f2[];
     __shared__ int nf2;
     const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
     if (tid == 0) nf2 = 0;
@@ -201,11 +204,11 @@ __device__ void init_cands_block(const orbg_keypoint *__restrict__ k1,
         const orbg_keypoint kp = k2[i];
         if (kp.octave == 0) {
             const int s = atomicAdd(&nf2, 1);
-            if (s < INIT_F2_CAP) f2[s] = F2Key{kp.x, kp.y, i};
+            if (s < f2cap) f2[s] = F2Key{kp.x, kp.y, i};
         }
     }
     __syncthreads();
-    const int m = min(nf2, INIT_F2_CAP);
+    const int m = min(nf2, f2cap);
     const GridPrm g = grid_prm(b);
     const float r = (float)window;
     for (int qq = 0; qq < INIT_QPW; qq++) {
@@ -272,14 +275,14 @@ __global__ __launch_bounds__(256) void k_init_cands_single(
     unsigned long long *topk, int32_t *topn)
 {
     init_cands_block(k1, d1, n1, k2, d2, n2, b, prev, 2, window, topk, topn,
-                     blockIdx.x * 4 * INIT_QPW);
+                     blockIdx.x * 4 * INIT_QPW, n2);
 }
 
 // batch: F1 = frame f1[p] (its keypoints are vbPrevMatched), F2 = frame f2[p]
 __global__ __launch_bounds__(256) void k_init_cands_pairs(
     const orbg_keypoint *kps, const uint8_t *desc, const int32_t *counts, int fc,
     const int32_t *f1, const int32_t *f2, int w, int h, int window, unsigned long long *topk,
-    int32_t *topn)
+    int32_t *topn, int cap)
 {
     const int nbx = (fc + 4 * INIT_QPW - 1) / (4 * INIT_QPW);
     const int id = xcd_remap(blockIdx.x, gridDim.x);
@@ -301,29 +304,61 @@ __global__ __launch_bounds__(256) void k_init_cands_pairs(
     init_cands_block(k1, desc + (size_t)a * fc * 32, n1, kps + (size_t)c * fc,
                      desc + (size_t)c * fc * 32, n2, b, (const float *)k1,
                      (int)(sizeof(orbg_keypoint) / sizeof(float)), window,
-                     topk + (size_t)p * fc * ORBG_MATCH_TOPK, topn + (size_t)p * fc, qbase);
+                     topk + (size_t)p * fc * ORBG_MATCH_TOPK, topn + (size_t)p * fc, qbase, cap);
 }
 
 // prev stride: the batch path reads x,y out of orbg_keypoint records (stride 7 floats)
 #define RESOLVE_CHUNK 64
 #define RESOLVE_N2_CAP 4608  // n1, n2 <= frame capacity (4000 features + 8 x 3)
 
+// LDS of one resolver, dynamic: only keypoint indices < cap are held.  SearchForInit-
+// ialization reads level-0 keypoints only (queries: octave 0; candidates:
+// GetFeaturesInArea(.., 0, 0)), and the batch extractor's output is level-major, so the
+// batch path uses cap = level-0 capacity (~440 at 2000 features) instead of the frame
+// capacity; the host-data path uses cap = max(n1, n2).  vMatchedDistance is u16 (sentinel
+// 0xFFFF > any distance), match indices i16.
 struct ResolveShared {
-    int mdist[RESOLVE_N2_CAP];
-    int m21[RESOLVE_N2_CAP];
-    int m12[RESOLVE_N2_CAP];
-    float ang1[RESOLVE_N2_CAP];
-    float ang2[RESOLVE_N2_CAP];
-    int8_t hbin[RESOLVE_N2_CAP];
-    unsigned long long chunk[2][RESOLVE_CHUNK * ORBG_MATCH_TOPK];
-    int chunkn[2][RESOLVE_CHUNK];
-    int hsize[HISTO_LENGTH];
-    int nm;
+    unsigned long long (*chunk)[RESOLVE_CHUNK * ORBG_MATCH_TOPK];
+    int (*chunkn)[RESOLVE_CHUNK];
+    int *hsize;
+    int *nmp;
+    float *ang1, *ang2;
+    uint16_t *mdist;
+    int16_t *m21, *m12;
+    int8_t *hbin;
 };
+
+#define RESOLVE_FIXED_BYTES (2 * RESOLVE_CHUNK * ORBG_MATCH_TOPK * 8 + 2 * RESOLVE_CHUNK * 4 + 32 * 4 + 16)
+
+__host__ __device__ constexpr size_t resolve_lds_bytes(int cap)
+{
+    return RESOLVE_FIXED_BYTES + (size_t)cap * 8 + (((size_t)cap * 7 + 15) & ~(size_t)15);
+}
+
+__device__ __forceinline__ ResolveShared resolve_layout(uint8_t *base, int cap)
+{
+    ResolveShared S;
+    S.chunk = (unsigned long long(*)[RESOLVE_CHUNK * ORBG_MATCH_TOPK])base;
+    base += 2 * RESOLVE_CHUNK * ORBG_MATCH_TOPK * 8;
+    S.chunkn = (int(*)[RESOLVE_CHUNK])base;
+    base += 2 * RESOLVE_CHUNK * 4;
+    S.hsize = (int *)base;
+    base += 32 * 4;
+    S.nmp = (int *)base;
+    base += 16;
+    S.ang1 = (float *)base;
+    S.ang2 = S.ang1 + cap;
+    base += (size_t)cap * 8;
+    S.mdist = (uint16_t *)base;
+    S.m21 = (int16_t *)(S.mdist + cap);
+    S.m12 = S.m21 + cap;
+    S.hbin = (int8_t *)(S.m12 + cap);
+    return S;
+}
 
 // exact fallback: sequential-scan semantics, wave-parallel
 __device__ void rescan(const orbg_keypoint *k2, const uint8_t *d2, int n2, const GridPrm &g,
-                       const Window &w, const uint32_t qd[8], const int *mdist, int *best,
+                       const Window &w, const uint32_t qd[8], const uint16_t *mdist, int *best,
                        int *best2, int *bidx)
 {
     const int lane = threadIdx.x & 63;
@@ -334,7 +369,7 @@ __device__ void rescan(const orbg_keypoint *k2, const uint8_t *d2, int n2, const
         const int ord = cand_order(g, w, kp.x, kp.y);
         if (ord < 0) continue;
         const int d = hamming8(qd, (const uint32_t *)(d2 + (size_t)j * 32));
-        if (mdist[j] <= d) continue;
+        if ((int)mdist[j] <= d) continue;
         const unsigned long long key =
             ((unsigned long long)d << 32) | ((unsigned long long)ord << 20) | (unsigned)j;
         if (key < m1) {
@@ -358,7 +393,7 @@ __device__ void rescan(const orbg_keypoint *k2, const uint8_t *d2, int n2, const
 // whose K-list the vMatchedDistance filter exhausted.
 #define RESOLVE_T 128
 
-__device__ void init_resolve_block(ResolveShared &S, const orbg_keypoint *__restrict__ k1,
+__device__ void init_resolve_block(ResolveShared &S, int cap, const orbg_keypoint *__restrict__ k1,
                                    const uint8_t *__restrict__ d1, int n1,
                                    const orbg_keypoint *__restrict__ k2,
                                    const uint8_t *__restrict__ d2, int n2, orbg_bounds b,
@@ -368,34 +403,35 @@ __device__ void init_resolve_block(ResolveShared &S, const orbg_keypoint *__rest
                                    int32_t *__restrict__ nm_out, float *prev_out)
 {
     const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
-    for (int i0 = 0; i0 < n2; i0 += 4 * RESOLVE_T) {
+    const int n1c = min(n1, cap), n2c = min(n2, cap);  // indices any query / candidate can have
+    for (int i0 = 0; i0 < n2c; i0 += 4 * RESOLVE_T) {
         float a[4];
 #pragma unroll
         for (int u = 0; u < 4; u++) {
             const int i = i0 + u * RESOLVE_T + tid;
-            a[u] = i < n2 ? k2[i].angle : 0.f;
+            a[u] = i < n2c ? k2[i].angle : 0.f;
         }
 #pragma unroll
         for (int u = 0; u < 4; u++) {
             const int i = i0 + u * RESOLVE_T + tid;
-            if (i < n2) {
-                S.mdist[i] = INT_MAX;
+            if (i < n2c) {
+                S.mdist[i] = 0xFFFF;
                 S.m21[i] = -1;
                 S.ang2[i] = a[u];
             }
         }
     }
-    for (int i0 = 0; i0 < n1; i0 += 4 * RESOLVE_T) {
+    for (int i0 = 0; i0 < n1c; i0 += 4 * RESOLVE_T) {
         float a[4];
 #pragma unroll
         for (int u = 0; u < 4; u++) {
             const int i = i0 + u * RESOLVE_T + tid;
-            a[u] = i < n1 ? k1[i].angle : 0.f;
+            a[u] = i < n1c ? k1[i].angle : 0.f;
         }
 #pragma unroll
         for (int u = 0; u < 4; u++) {
             const int i = i0 + u * RESOLVE_T + tid;
-            if (i < n1) {
+            if (i < n1c) {
                 S.hbin[i] = -1;
                 S.m12[i] = -1;
                 S.ang1[i] = a[u];
@@ -403,7 +439,7 @@ __device__ void init_resolve_block(ResolveShared &S, const orbg_keypoint *__rest
         }
     }
     if (tid < HISTO_LENGTH) S.hsize[tid] = 0;
-    if (tid == 0) S.nm = 0;
+    if (tid == 0) *S.nmp = 0;
     const GridPrm g = grid_prm(b);
     const float factor = 1.0f / HISTO_LENGTH;
     // lane 0 of wave 0: sequential state update for query i1
@@ -413,12 +449,12 @@ __device__ void init_resolve_block(ResolveShared &S, const orbg_keypoint *__rest
             const float rot0 = S.ang1[i1] - S.ang2[bestIdx2];
             if (old >= 0) {
                 S.m12[old] = -1;
-                S.nm--;
+                (*S.nmp)--;
             }
-            S.m12[i1] = bestIdx2;
-            S.m21[bestIdx2] = i1;
-            S.mdist[bestIdx2] = bestDist;
-            S.nm++;
+            S.m12[i1] = (int16_t)bestIdx2;
+            S.m21[bestIdx2] = (int16_t)i1;
+            S.mdist[bestIdx2] = (uint16_t)bestDist;
+            (*S.nmp)++;
             if (check_ori) {
                 float rot = rot0;
                 if (rot < 0.0f) rot += 360.0f;
@@ -432,8 +468,8 @@ __device__ void init_resolve_block(ResolveShared &S, const orbg_keypoint *__rest
     // wave 1: load chunk c into buffer c & 1 (lists only when the chunk has a live query)
     auto prefetch = [&](int c) {
         const int c0 = c * RESOLVE_CHUNK;
-        if (c0 >= n1) return;
-        const int cn = min(RESOLVE_CHUNK, n1 - c0);
+        if (c0 >= n1c) return;
+        const int cn = min(RESOLVE_CHUNK, n1c - c0);
         const int t = lane < cn ? topn[c0 + lane] : -1;
         S.chunkn[c & 1][lane] = t;
         if (__ballot(t > 0) == 0ull) return;
@@ -448,12 +484,12 @@ __device__ void init_resolve_block(ResolveShared &S, const orbg_keypoint *__rest
     };
     if (wv == 1) prefetch(0);
     __syncthreads();
-    const int nchunks = (n1 + RESOLVE_CHUNK - 1) / RESOLVE_CHUNK;
+    const int nchunks = (n1c + RESOLVE_CHUNK - 1) / RESOLVE_CHUNK;
     for (int c = 0; c < nchunks; c++) {
         if (wv == 1) {
             prefetch(c + 1);
         } else {
-            const int c0 = c * RESOLVE_CHUNK, cn = min(RESOLVE_CHUNK, n1 - c0);
+            const int c0 = c * RESOLVE_CHUNK, cn = min(RESOLVE_CHUNK, n1c - c0);
             const int *cnt = S.chunkn[c & 1];
             const unsigned long long *lists = S.chunk[c & 1];
             int qi = 0;
@@ -467,9 +503,9 @@ __device__ void init_resolve_block(ResolveShared &S, const orbg_keypoint *__rest
                         const unsigned long long *lst = &lists[q * ORBG_MATCH_TOPK];
                         // first three entries and their filter state in flight together
                         const unsigned long long e0 = lst[0], e1 = lst[1], e2 = lst[2];
-                        const int md0 = S.mdist[(int)(e0 & 0xFFFFF)];
-                        const int md1 = S.mdist[(int)(e1 & 0xFFFFF)];
-                        const int md2 = S.mdist[(int)(e2 & 0xFFFFF)];
+                        const int md0 = S.mdist[kk > 0 ? (int)(e0 & 0xFFFFF) : 0];
+                        const int md1 = S.mdist[kk > 1 ? (int)(e1 & 0xFFFFF) : 0];
+                        const int md2 = S.mdist[kk > 2 ? (int)(e2 & 0xFFFFF) : 0];
                         int found = 0, bd = INT_MAX, bd2 = INT_MAX, bi = -1;
                         const unsigned long long ev[3] = {e0, e1, e2};
                         const int mv[3] = {md0, md1, md2};
@@ -491,7 +527,7 @@ __device__ void init_resolve_block(ResolveShared &S, const orbg_keypoint *__rest
                         for (int k = 3; k < kk && found < 2; k++) {
                             const unsigned long long e = lst[k];
                             const int d = (int)(e >> 32), i2 = (int)(e & 0xFFFFF);
-                            if (!(S.mdist[i2] <= d)) {
+                            if (!((int)S.mdist[i2] <= d)) {
                                 if (found == 0) {
                                     bd = d;
                                     bi = i2;
@@ -522,7 +558,7 @@ __device__ void init_resolve_block(ResolveShared &S, const orbg_keypoint *__rest
 #pragma unroll
                     for (int k = 0; k < 8; k++) qd[k] = qp[k];
                     int bestDist, bestDist2, bestIdx2;
-                    rescan(k2, d2, n2, g, w, qd, S.mdist, &bestDist, &bestDist2, &bestIdx2);
+                    rescan(k2, d2, n2c, g, w, qd, S.mdist, &bestDist, &bestDist2, &bestIdx2);
                     if (lane == 0) apply(i1, bestDist, bestDist2, bestIdx2);
                     wave_sync_lds();
                     qi++;
@@ -531,7 +567,7 @@ __device__ void init_resolve_block(ResolveShared &S, const orbg_keypoint *__rest
         }
         __syncthreads();
     }
-    int nmatches = S.nm;
+    int nmatches = *S.nmp;
     if (check_ori) {
         __shared__ int ind[3];
         if (tid == 0) {
@@ -562,7 +598,7 @@ __device__ void init_resolve_block(ResolveShared &S, const orbg_keypoint *__rest
         }
         __syncthreads();
         int removed = 0;
-        for (int i = tid; i < n1; i += RESOLVE_T) {
+        for (int i = tid; i < n1c; i += RESOLVE_T) {
             const int bn = S.hbin[i];
             if (bn < 0 || bn == ind[0] || bn == ind[1] || bn == ind[2]) continue;
             if (S.m12[i] >= 0) {
@@ -577,9 +613,9 @@ __device__ void init_resolve_block(ResolveShared &S, const orbg_keypoint *__rest
         nmatches -= rem2[0] + rem2[1];
     }
     __syncthreads();
-    for (int i = tid; i < n1; i += RESOLVE_T) m12[i] = S.m12[i];
+    for (int i = tid; i < n1; i += RESOLVE_T) m12[i] = i < n1c ? S.m12[i] : -1;
     if (prev_out) {
-        for (int i = tid; i < n1; i += RESOLVE_T) {
+        for (int i = tid; i < n1c; i += RESOLVE_T) {
             const int j = S.m12[i];
             if (j >= 0) {
                 prev_out[2 * i] = k2[j].x;
@@ -596,8 +632,10 @@ __global__ __launch_bounds__(RESOLVE_T) void k_init_resolve_single(
     int check_ori, const unsigned long long *topk, const int32_t *topn, int32_t *m12,
     int32_t *nm)
 {
-    __shared__ ResolveShared S;
-    init_resolve_block(S, k1, d1, n1, k2, d2, n2, b, prev, 2, window, nnratio, check_ori, topk,
+    extern __shared__ __attribute__((aligned(16))) uint8_t rs_lds[];
+    const int cap = max(n1, n2);
+    ResolveShared S = resolve_layout(rs_lds, cap);
+    init_resolve_block(S, cap, k1, d1, n1, k2, d2, n2, b, prev, 2, window, nnratio, check_ori, topk,
                        topn, m12, nm, prev);
 }
 
@@ -605,14 +643,15 @@ __global__ __launch_bounds__(RESOLVE_T) void k_init_resolve_pairs(
     const orbg_keypoint *kps, const uint8_t *desc, const int32_t *counts, int fc,
     const int32_t *f1, const int32_t *f2, int w, int h, int window, float nnratio,
     int check_ori, const unsigned long long *topk, const int32_t *topn, int32_t *m12,
-    int32_t *nm)
+    int32_t *nm, int cap)
 {
-    __shared__ ResolveShared S;
+    extern __shared__ __attribute__((aligned(16))) uint8_t rs_lds[];
+    ResolveShared S = resolve_layout(rs_lds, cap);
     const int p = blockIdx.x;
     const int a = f1[p], c = f2[p];
     const orbg_keypoint *k1 = kps + (size_t)a * fc;
     orbg_bounds b{0.f, (float)w, 0.f, (float)h};
-    init_resolve_block(S, k1, desc + (size_t)a * fc * 32, counts[a], kps + (size_t)c * fc,
+    init_resolve_block(S, cap, k1, desc + (size_t)a * fc * 32, counts[a], kps + (size_t)c * fc,
                       desc + (size_t)c * fc * 32, counts[c], b, (const float *)k1,
                       (int)(sizeof(orbg_keypoint) / sizeof(float)), window, nnratio, check_ori,
                       topk + (size_t)p * fc * ORBG_MATCH_TOPK, topn + (size_t)p * fc,
@@ -644,13 +683,14 @@ int launch_match_pairs(hipStream_t st, hipStream_t aux, hipEvent_t evf, hipEvent
                        const int32_t *counts, int fc, const int32_t *d_f1, const int32_t *d_f2,
                        int npairs, int w, int h, int window, float nnratio, int check_ori,
                        int32_t *knn, int32_t *m12, int32_t *nm, uint32_t *topk, int32_t *topk_n,
-                       void *prof, int serial)
+                       void *prof, int serial, int cap0)
 {
-    if (fc > RESOLVE_N2_CAP || fc > (1 << 20)) return ORBG_ENOTSUP;
+    // cap0 = level-0 capacity: every index SearchForInitialization touches is below it
+    if (fc > RESOLVE_N2_CAP || fc > (1 << 20) || cap0 > fc) return ORBG_ENOTSUP;
     PL(prof, st, "init_cands",
        hipLaunchKernelGGL(k_init_cands_pairs, dim3((fc + 4 * INIT_QPW - 1) / (4 * INIT_QPW) * npairs),
-                          dim3(256), 0, st, kps, desc, counts, fc, d_f1, d_f2, w, h, window,
-                          (unsigned long long *)topk, topk_n));
+                          dim3(256), cap0 * sizeof(F2Key), st, kps, desc, counts, fc, d_f1, d_f2,
+                          w, h, window, (unsigned long long *)topk, topk_n, cap0));
     // knn2 (VALU bound) on `aux` beside init_resolve (one sequential workgroup per pair);
     // serial == 1 (developer timing, ORBG_DBG=40) keeps it on `st`
     if (serial) aux = st;
@@ -661,9 +701,10 @@ int launch_match_pairs(hipStream_t st, hipStream_t aux, hipEvent_t evf, hipEvent
                           counts, fc, d_f1, d_f2, knn));
     if (hipEventRecord(evj, aux) != hipSuccess) return ORBG_EIO;
     PL(prof, st, "init_resolve",
-       hipLaunchKernelGGL(k_init_resolve_pairs, dim3(npairs), dim3(RESOLVE_T), 0, st, kps, desc, counts,
-                          fc, d_f1, d_f2, w, h, window, nnratio, check_ori,
-                          (const unsigned long long *)topk, topk_n, m12, nm));
+       hipLaunchKernelGGL(k_init_resolve_pairs, dim3(npairs), dim3(RESOLVE_T),
+                          resolve_lds_bytes(cap0), st, kps, desc, counts, fc, d_f1, d_f2, w, h,
+                          window, nnratio, check_ori, (const unsigned long long *)topk, topk_n,
+                          m12, nm, cap0));
     if (hipStreamWaitEvent(st, evj, 0) != hipSuccess) return ORBG_EIO;
     return hipGetLastError() == hipSuccess ? ORBG_OK : ORBG_EIO;
 }
@@ -674,12 +715,21 @@ int launch_init_match_single(hipStream_t st, const orbg_keypoint *k1, const uint
                              int check_ori, uint32_t *topk, int32_t *topk_n, void *prof)
 {
     if (n1 > RESOLVE_N2_CAP || n2 > RESOLVE_N2_CAP || n2 > INIT_F2_CAP) return ORBG_ENOTSUP;
+    static bool attr = false;  // > 64 KB of dynamic LDS at the 4608-keypoint bound
+    if (!attr) {
+        if (hipFuncSetAttribute((const void *)k_init_resolve_single,
+                                hipFuncAttributeMaxDynamicSharedMemorySize,
+                                (int)resolve_lds_bytes(RESOLVE_N2_CAP)) != hipSuccess)
+            return ORBG_EIO;
+        attr = true;
+    }
     PL(prof, st, "init_cands",
        hipLaunchKernelGGL(k_init_cands_single, dim3((n1 + 4 * INIT_QPW - 1) / (4 * INIT_QPW)),
-                          dim3(256), 0, st, k1, d1, n1, k2, d2, n2, b, prev, window,
-                          (unsigned long long *)topk, topk_n));
+                          dim3(256), (size_t)std::max(n2, 1) * sizeof(F2Key), st, k1, d1, n1, k2,
+                          d2, n2, b, prev, window, (unsigned long long *)topk, topk_n));
     PL(prof, st, "init_resolve",
-       hipLaunchKernelGGL(k_init_resolve_single, dim3(1), dim3(RESOLVE_T), 0, st, k1, d1, n1, k2, d2, n2,
+       hipLaunchKernelGGL(k_init_resolve_single, dim3(1), dim3(RESOLVE_T),
+                          resolve_lds_bytes(std::max(std::max(n1, n2), 1)), st, k1, d1, n1, k2, d2, n2,
                           b, prev, window, nnratio, check_ori, (const unsigned long long *)topk,
                           topk_n, m12, nm));
     return hipGetLastError() == hipSuccess ? ORBG_OK : ORBG_EIO;

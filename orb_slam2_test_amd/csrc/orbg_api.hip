@@ -40,7 +40,7 @@ int launch_match_pairs(hipStream_t st, hipStream_t aux, hipEvent_t evf, hipEvent
                        const int32_t *counts, int frame_cap, const int32_t *d_f1,
                        const int32_t *d_f2, int npairs, int w, int h, int window, float nnratio,
                        int check_ori, int32_t *knn, int32_t *m12, int32_t *nm, uint32_t *topk,
-                       int32_t *topk_n, void *prof, int serial);
+                       int32_t *topk_n, void *prof, int serial, int cap0);
 int launch_knn2(hipStream_t st, const uint8_t *q, int nq, const uint8_t *t, int nt, int32_t *out,
                 void *prof);
 int launch_init_match_single(hipStream_t st, const orbg_keypoint *k1, const uint8_t *d1, int n1,
@@ -170,6 +170,15 @@ struct orbg_ctx {
     // beside SearchForInitialization); forked from / joined into `stream` with events
     hipStream_t aux_stream = nullptr;
     hipEvent_t ev_fork[2] = {nullptr, nullptr}, ev_join[2] = {nullptr, nullptr};
+    // Batch matching and the trajectory summary run on `mstream`, so the matching of batch k
+    // overlaps the extraction of batch k+1 on `stream`.  The per-frame outputs (kps, desc,
+    // counts) alternate between two slots: ev_ext[s] = slot s written (on `stream`),
+    // ev_mat[s] = slot s no longer read (on `mstream`); extraction into slot s waits for
+    // ev_mat[s], matching of slot s waits for ev_ext[s].
+    hipStream_t mstream = nullptr;
+    hipEvent_t ev_ext[2] = {nullptr, nullptr}, ev_mat[2] = {nullptr, nullptr};
+    bool mat_pending[2] = {false, false};
+    int slot = 0;  // slot of the last extraction
     float scale[16], inv_scale[16], sigma2[16], inv_sigma2[16];
     int32_t fpl[16], umax[16];
     // plan
@@ -194,9 +203,12 @@ struct orbg_ctx {
     int4 *d_nodes = nullptr;
     uint32_t *d_lvl_kp = nullptr;
     int32_t *d_lvl_cnt = nullptr;
-    orbg_keypoint *d_kps = nullptr;
-    uint8_t *d_desc = nullptr;
-    int32_t *d_counts = nullptr;
+    orbg_keypoint *d_kps = nullptr;  // = kps_slot[slot]
+    uint8_t *d_desc = nullptr;        // = desc_slot[slot]
+    int32_t *d_counts = nullptr;      // = counts_slot[slot]
+    orbg_keypoint *kps_slot[2] = {nullptr, nullptr};
+    uint8_t *desc_slot[2] = {nullptr, nullptr};
+    int32_t *counts_slot[2] = {nullptr, nullptr};
     int32_t *d_err = nullptr;
     // last batch
     const uint8_t *last_img = nullptr;
@@ -278,9 +290,13 @@ static void make_tables(orbg_ctx *c)
 
 static void free_plan(orbg_ctx *c)
 {
+    if (c->stream) hipStreamSynchronize(c->stream);
+    if (c->mstream) hipStreamSynchronize(c->mstream);
+    c->mat_pending[0] = c->mat_pending[1] = false;
     void *ptrs[] = {c->d_geom, c->d_cells, c->d_tile_base, c->d_rtab, c->d_ctab, c->d_pyr, c->d_blur,
                     c->d_cell_cnt, c->d_cell_kp, c->d_keys, c->d_knode, c->d_act, c->d_qk,
-                    c->d_nodes, c->d_lvl_kp, c->d_lvl_cnt, c->d_kps, c->d_desc, c->d_counts,
+                    c->d_nodes, c->d_lvl_kp, c->d_lvl_cnt, c->kps_slot[0], c->kps_slot[1],
+                    c->desc_slot[0], c->desc_slot[1], c->counts_slot[0], c->counts_slot[1],
                     c->d_err, c->d_knn, c->d_m12, c->d_nm, c->d_topk, c->d_topk_n, c->d_pairs};
     for (void *q : ptrs)
         if (q) hipFree(q);
@@ -300,6 +316,11 @@ static void free_plan(orbg_ctx *c)
     c->d_kps = nullptr;
     c->d_desc = nullptr;
     c->d_counts = nullptr;
+    for (int i = 0; i < 2; i++) {
+        c->kps_slot[i] = nullptr;
+        c->desc_slot[i] = nullptr;
+        c->counts_slot[i] = nullptr;
+    }
     c->d_err = nullptr;
     c->d_knn = c->d_m12 = c->d_nm = nullptr;
     c->d_topk = nullptr;
@@ -597,8 +618,12 @@ static int plan(orbg_ctx *c, int w, int h, int batch)
         (rc = dalloc(&c->d_keys, B * G.keys_frame)) || (rc = dalloc(&c->d_knode, B * G.keys_frame)) ||
         (rc = dalloc(&c->d_act, 2 * B * G.keys_frame)) || (rc = dalloc(&c->d_qk, B * G.keys_frame)) ||
         (rc = dalloc(&c->d_nodes, B * G.nodes_frame)) || (rc = dalloc(&c->d_lvl_kp, B * G.out_frame)) ||
-        (rc = dalloc(&c->d_lvl_cnt, B * G.L)) || (rc = dalloc(&c->d_kps, B * G.frame_cap)) ||
-        (rc = dalloc(&c->d_desc, B * G.frame_cap * 32)) || (rc = dalloc(&c->d_counts, B)) ||
+        (rc = dalloc(&c->d_lvl_cnt, B * G.L)) ||
+        (rc = dalloc(&c->kps_slot[0], B * G.frame_cap)) ||
+        (rc = dalloc(&c->kps_slot[1], B * G.frame_cap)) ||
+        (rc = dalloc(&c->desc_slot[0], B * G.frame_cap * 32)) ||
+        (rc = dalloc(&c->desc_slot[1], B * G.frame_cap * 32)) ||
+        (rc = dalloc(&c->counts_slot[0], B)) || (rc = dalloc(&c->counts_slot[1], B)) ||
         (rc = dalloc(&c->d_err, 1))) {
         free_plan(c);
         return rc;
@@ -614,7 +639,12 @@ static int plan(orbg_ctx *c, int w, int h, int batch)
                          hipMemcpyHostToDevice));
     HIPCHK(hipMemcpy(c->d_ctab, ctab.data(), ctab.size() * sizeof(uint32_t),
                      hipMemcpyHostToDevice));
-    HIPCHK(hipMemset(c->d_counts, 0, B * sizeof(int32_t)));
+    HIPCHK(hipMemset(c->counts_slot[0], 0, B * sizeof(int32_t)));
+    HIPCHK(hipMemset(c->counts_slot[1], 0, B * sizeof(int32_t)));
+    c->slot = 0;
+    c->d_kps = c->kps_slot[0];
+    c->d_desc = c->desc_slot[0];
+    c->d_counts = c->counts_slot[0];
     c->geom = G;
     c->cells = cells;
     c->tile_base = tile_base;
@@ -673,9 +703,17 @@ extern "C" int orbg_create(int device, const orbg_params *p, orbg_ctx **out)
         delete c;
         return set_err(ORBG_EIO, "hipStreamCreate failed");
     }
+    if (hipStreamCreateWithFlags(&c->mstream, hipStreamNonBlocking) != hipSuccess) {
+        hipStreamDestroy(c->aux_stream);
+        hipStreamDestroy(c->own_stream);
+        delete c;
+        return set_err(ORBG_EIO, "hipStreamCreate failed");
+    }
     for (int i = 0; i < 2; i++) {
         hipEventCreateWithFlags(&c->ev_fork[i], hipEventDisableTiming);
         hipEventCreateWithFlags(&c->ev_join[i], hipEventDisableTiming);
+        hipEventCreateWithFlags(&c->ev_ext[i], hipEventDisableTiming);
+        hipEventCreateWithFlags(&c->ev_mat[i], hipEventDisableTiming);
     }
     *out = c;
     return ORBG_OK;
@@ -692,11 +730,15 @@ extern "C" void orbg_destroy(orbg_ctx *c)
     if (c->d_img) hipFree(c->d_img);
     if (c->d_scr) hipFree(c->d_scr);
     if (c->aux_stream) hipStreamSynchronize(c->aux_stream);
+    if (c->mstream) hipStreamSynchronize(c->mstream);
     for (int i = 0; i < 2; i++) {
         if (c->ev_fork[i]) hipEventDestroy(c->ev_fork[i]);
         if (c->ev_join[i]) hipEventDestroy(c->ev_join[i]);
+        if (c->ev_ext[i]) hipEventDestroy(c->ev_ext[i]);
+        if (c->ev_mat[i]) hipEventDestroy(c->ev_mat[i]);
     }
     if (c->aux_stream) hipStreamDestroy(c->aux_stream);
+    if (c->mstream) hipStreamDestroy(c->mstream);
     if (c->own_stream) hipStreamDestroy(c->own_stream);
     delete c;
 }
@@ -768,11 +810,23 @@ static int launch_extract(orbg_ctx *c, const uint8_t *d_imgs, int B, int pitch, 
                                    c->d_geom, c->d_cell_cnt, c->d_cell_kp, c->d_keys, c->d_knode,
                                    c->d_act, c->d_qk, c->d_nodes, c->d_lvl_kp, c->d_lvl_cnt,
                                    c->d_err));
+    // per-frame outputs go to the other slot; wait until its last reader (matching of the
+    // batch before last) is done
+    const int s = c->slot ^ 1;
+    if (c->mat_pending[s]) {
+        HIPCHK(hipStreamWaitEvent(st, c->ev_mat[s], 0));
+        c->mat_pending[s] = false;
+    }
+    c->slot = s;
+    c->d_kps = c->kps_slot[s];
+    c->d_desc = c->desc_slot[s];
+    c->d_counts = c->counts_slot[s];
     PROF_LAUNCH(c, "orient_desc",
                 hipLaunchKernelGGL(k_orient_desc, dim3((G.frame_cap + 3) / 4 * B), dim3(256), 0, st,
                                    c->d_geom, d_imgs, fs, pitch, c->d_pyr, c->d_blur,
                                    c->d_lvl_kp, c->d_lvl_cnt, (OrbgKeypointDev *)c->d_kps,
                                    c->d_desc, c->d_counts));
+    HIPCHK(hipEventRecord(c->ev_ext[s], st));
     HIPCHK(hipGetLastError());
     c->last_img = d_imgs;
     c->last_fs = fs;
@@ -781,11 +835,21 @@ static int launch_extract(orbg_ctx *c, const uint8_t *d_imgs, int B, int pitch, 
     return ORBG_OK;
 }
 
+// both streams drained (host reads of any output)
+static int sync_all(orbg_ctx *c)
+{
+    HIPCHK(hipStreamSynchronize(c->stream));
+    HIPCHK(hipStreamSynchronize(c->mstream));
+    c->mat_pending[0] = c->mat_pending[1] = false;
+    return ORBG_OK;
+}
+
 static int check_err(orbg_ctx *c)
 {
     int32_t e = 0;
     HIPCHK(hipMemcpyAsync(&e, c->d_err, sizeof(e), hipMemcpyDeviceToHost, c->stream));
-    HIPCHK(hipStreamSynchronize(c->stream));
+    int rc = sync_all(c);
+    if (rc) return rc;
     c->prof.collect();
     if (e) return set_err(ORBG_ENOTSUP, "quadtree capacity exceeded (flags 0x%x)", e);
     return ORBG_OK;
@@ -871,7 +935,8 @@ extern "C" int orbg_get_level(orbg_ctx *c, int frame, int level, uint8_t *dst, s
     if (lh) *lh = L.h;
     if (!dst) return ORBG_OK;
     if (dst_step < (size_t)L.w) return set_err(ORBG_EINVAL, "dst_step too small");
-    HIPCHK(hipStreamSynchronize(c->stream));
+    int rc = sync_all(c);
+    if (rc) return rc;
     if (level == 0)
         HIPCHK(hipMemcpy2D(dst, dst_step, c->last_img + frame * c->last_fs, c->last_pitch, L.w,
                            L.h, hipMemcpyDeviceToHost));
@@ -884,17 +949,21 @@ extern "C" int orbg_get_level(orbg_ctx *c, int frame, int level, uint8_t *dst, s
 extern "C" int orbg_sync(orbg_ctx *c)
 {
     if (!c) return set_err(ORBG_EINVAL, "ctx is NULL");
-    HIPCHK(hipStreamSynchronize(c->stream));
+    int rc = sync_all(c);
+    if (rc) return rc;
     c->prof.collect();
     return ORBG_OK;
 }
 
 extern "C" void *orbg_stream(orbg_ctx *c) { return c ? (void *)c->stream : nullptr; }
 
+extern "C" void *orbg_match_stream(orbg_ctx *c) { return c ? (void *)c->mstream : nullptr; }
+
 extern "C" int orbg_set_stream(orbg_ctx *c, void *stream)
 {
     if (!c) return set_err(ORBG_EINVAL, "ctx is NULL");
-    HIPCHK(hipStreamSynchronize(c->stream));
+    int rc = sync_all(c);
+    if (rc) return rc;
     c->prof.collect();
     c->stream = stream ? (hipStream_t)stream : c->own_stream;
     return ORBG_OK;
@@ -903,7 +972,8 @@ extern "C" int orbg_set_stream(orbg_ctx *c, void *stream)
 extern "C" int orbg_batch_stats(orbg_ctx *c, int64_t *ncand, int64_t *nkp)
 {
     if (!c || !c->gw || c->last_n <= 0) return set_err(ORBG_EINVAL, "no batch");
-    HIPCHK(hipStreamSynchronize(c->stream));
+    int rc = sync_all(c);
+    if (rc) return rc;
     std::vector<int32_t> cc((size_t)c->last_n * c->geom.ncells), kc(c->last_n);
     HIPCHK(hipMemcpy(cc.data(), c->d_cell_cnt, cc.size() * 4, hipMemcpyDeviceToHost));
     HIPCHK(hipMemcpy(kc.data(), c->d_counts, kc.size() * 4, hipMemcpyDeviceToHost));
@@ -918,11 +988,15 @@ extern "C" int orbg_batch_stats(orbg_ctx *c, int64_t *ncand, int64_t *nkp)
 extern "C" int orbg_batch_summary(orbg_ctx *c, int32_t *d_out)
 {
     if (!c || !c->gw || c->last_n <= 0 || !d_out) return set_err(ORBG_EINVAL, "no batch");
+    const int s = c->slot;
+    HIPCHK(hipStreamWaitEvent(c->mstream, c->ev_ext[s], 0));
     HIPCHK(hipMemcpyAsync(d_out, c->d_counts, c->last_n * sizeof(int32_t),
-                          hipMemcpyDeviceToDevice, c->stream));
+                          hipMemcpyDeviceToDevice, c->mstream));
     if (c->last_npairs > 0)
         HIPCHK(hipMemcpyAsync(d_out + c->last_n, c->d_nm, c->last_npairs * sizeof(int32_t),
-                              hipMemcpyDeviceToDevice, c->stream));
+                              hipMemcpyDeviceToDevice, c->mstream));
+    HIPCHK(hipEventRecord(c->ev_mat[s], c->mstream));
+    c->mat_pending[s] = true;
     return ORBG_OK;
 }
 
@@ -1000,6 +1074,8 @@ extern "C" int orbg_match_batch_device(orbg_ctx *c, const int32_t *f1, const int
     HIPCHK(hipSetDevice(c->device));
     const size_t fc = (size_t)c->geom.frame_cap;
     if (c->pair_cap < npairs) {
+        int rs = sync_all(c);  // an earlier match may still read the buffers
+        if (rs) return rs;
         c->h_pairs.clear();
         hipFree(c->d_pairs);
         hipFree(c->d_knn);
@@ -1025,17 +1101,22 @@ extern "C" int orbg_match_batch_device(orbg_ctx *c, const int32_t *f1, const int
     std::vector<int32_t> hp(f1, f1 + npairs);
     hp.insert(hp.end(), f2, f2 + npairs);
     if (hp != c->h_pairs) {
+        HIPCHK(hipStreamSynchronize(c->mstream));  // the previous match reads d_pairs
         HIPCHK(hipMemcpy(c->d_pairs, f1, npairs * sizeof(int32_t), hipMemcpyHostToDevice));
         HIPCHK(hipMemcpy(c->d_pairs + c->pair_cap, f2, npairs * sizeof(int32_t),
                          hipMemcpyHostToDevice));
         c->h_pairs.swap(hp);
     }
-    int rc = launch_match_pairs(c->stream, c->aux_stream, c->ev_fork[1], c->ev_join[1],
+    const int s = c->slot;
+    HIPCHK(hipStreamWaitEvent(c->mstream, c->ev_ext[s], 0));
+    int rc = launch_match_pairs(c->mstream, c->aux_stream, c->ev_fork[1], c->ev_join[1],
                                 c->d_desc, c->d_kps, c->d_counts, (int)fc, c->d_pairs,
                                 c->d_pairs + c->pair_cap, npairs, c->geom.w, c->geom.h, window,
                                 nnratio, check_ori, c->d_knn, c->d_m12, c->d_nm, c->d_topk,
-                                c->d_topk_n, &c->prof, c->geom.dbg == 40);
+                                c->d_topk_n, &c->prof, c->geom.dbg == 40, c->geom.lv[0].out_cap);
     if (rc) return rc;
+    HIPCHK(hipEventRecord(c->ev_mat[s], c->mstream));
+    c->mat_pending[s] = true;
     c->last_npairs = npairs;
     return ORBG_OK;
 }
@@ -1055,7 +1136,8 @@ extern "C" int orbg_download_matches(orbg_ctx *c, int pair, int32_t *knn, int32_
                                      int32_t *nmatches)
 {
     if (!c || pair < 0 || pair >= c->last_npairs) return set_err(ORBG_EINVAL, "bad pair");
-    HIPCHK(hipStreamSynchronize(c->stream));
+    int rc0 = sync_all(c);
+    if (rc0) return rc0;
     c->prof.collect();
     const size_t fc = (size_t)c->geom.frame_cap;
     const int n = std::min(cap, (int)fc);

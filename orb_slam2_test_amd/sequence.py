@@ -101,6 +101,7 @@ class GpuBackend:
             self.ext.match_batch_device(np.arange(n - 1), np.arange(1, n), self.window,
                                         self.nnratio, self.check_ori)
         self.ext.ctx.batch_summary(summary.data_ptr())
+        self.ext.ctx.sync()  # the summary is written on liborbg's match stream
         s = summary.cpu().numpy()
         nkp = s[:n].copy()
         if n > 1:
