@@ -220,6 +220,16 @@ int orbg_ba_linearize(orbg_ctx *ctx, const orbg_pose *poses, int npose, const do
                       int npoint, const orbg_edge *edges, int nedge, orbg_edge_out *eout,
                       double *hpose, double *bpose, double *hpoint, double *bpoint);
 
+/* Device-resident variant (batched LBA windows): every pointer is device memory, enqueued
+ * on the context stream.  pose_off[npose+1] / pose_edges[nedge] list each pose's edges
+ * (CSR); d_eout is required (the pose blocks are reduced from it); outputs are
+ * overwritten.  Pose blocks H_pp | b_p are accumulated with MFMA f64. */
+int orbg_ba_linearize_device(orbg_ctx *ctx, const orbg_pose *d_poses, int npose,
+                             const double *d_points, int npoint, const orbg_edge *d_edges,
+                             int nedge, const int32_t *d_pose_off, const int32_t *d_pose_edges,
+                             orbg_edge_out *d_eout, double *d_hpose, double *d_bpose,
+                             double *d_hpoint, double *d_bpoint);
+
 #ifdef __cplusplus
 }
 #endif

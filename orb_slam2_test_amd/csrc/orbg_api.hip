@@ -50,9 +50,14 @@ int launch_init_match_single(hipStream_t st, const orbg_keypoint *k1, const uint
                              void *prof);
 // ba_kernels.hip
 int launch_ba(hipStream_t st, const orbg_pose *poses, int npose, const double *points,
-              int npoint, const orbg_edge *edges, int nedge, orbg_edge_out *eout,
-              double *hpose, double *bpose, double *hpoint, double *bpoint, void *scratch,
-              void *prof);
+              int npoint, const orbg_edge *edges, int nedge, const int32_t *pose_off,
+              const int32_t *pose_edges, orbg_edge_out *eout, double *hpose, double *bpose,
+              double *hpoint, double *bpoint, void *scratch, void *prof);
+int launch_ba_device(hipStream_t st, const orbg_pose *poses, int npose, const double *points,
+                     int npoint, const orbg_edge *edges, int nedge, const int32_t *pose_off,
+                     const int32_t *pose_edges, orbg_edge_out *eout, double *hpose, double *bpose,
+                     double *hpoint, double *bpoint, double *rows, void *prof);
+size_t ba_rows_bytes(int nedge);
 size_t ba_scratch_bytes(int npose, int npoint, int nedge);
 }  // namespace orbg
 
@@ -1249,15 +1254,47 @@ extern "C" int orbg_ba_linearize(orbg_ctx *c, const orbg_pose *poses, int npose,
             edges[i].point >= npoint)
             return set_err(ORBG_EINVAL, "edge %d references a missing vertex", i);
     HIPCHK(hipSetDevice(c->device));
+    // edge lists per pose (CSR) for the MFMA pose-block reduction
+    std::vector<int32_t> off(npose + 1, 0), pe(nedge > 0 ? nedge : 1);
+    for (int i = 0; i < nedge; i++) off[edges[i].pose + 1]++;
+    for (int p = 0; p < npose; p++) off[p + 1] += off[p];
+    {
+        std::vector<int32_t> fill(off.begin(), off.end() - 1);
+        for (int i = 0; i < nedge; i++) pe[fill[edges[i].pose]++] = i;
+    }
     const size_t sb = ba_scratch_bytes(npose, npoint, nedge);
     void *s;
     int rc = scratch(c, sb, &s);
     if (rc) return rc;
-    rc = launch_ba(c->stream, poses, npose, points, npoint, edges, nedge, eout, hpose, bpose,
-                   hpoint, bpoint, s, &c->prof);
+    rc = launch_ba(c->stream, poses, npose, points, npoint, edges, nedge, off.data(), pe.data(),
+                   eout, hpose, bpose, hpoint, bpoint, s, &c->prof);
     if (rc) return rc;
     HIPCHK(hipStreamSynchronize(c->stream));
     c->prof.collect();
+    return ORBG_OK;
+}
+
+extern "C" int orbg_ba_linearize_device(orbg_ctx *c, const orbg_pose *d_poses, int npose,
+                                        const double *d_points, int npoint,
+                                        const orbg_edge *d_edges, int nedge,
+                                        const int32_t *d_pose_off, const int32_t *d_pose_edges,
+                                        orbg_edge_out *d_eout, double *d_hpose, double *d_bpose,
+                                        double *d_hpoint, double *d_bpoint)
+{
+    if (!c) return set_err(ORBG_EINVAL, "ctx is NULL");
+    if (npose < 0 || npoint < 0 || nedge < 0) return set_err(ORBG_EINVAL, "negative size");
+    if ((nedge && (!d_edges || !d_eout)) || (npose && (!d_poses || !d_pose_off || !d_pose_edges ||
+                                                       !d_hpose || !d_bpose)) ||
+        (npoint && (!d_points || !d_hpoint || !d_bpoint)))
+        return set_err(ORBG_EINVAL, "NULL device array");
+    HIPCHK(hipSetDevice(c->device));
+    void *s;
+    int rc = scratch(c, ba_rows_bytes(nedge), &s);
+    if (rc) return rc;
+    rc = launch_ba_device(c->stream, d_poses, npose, d_points, npoint, d_edges, nedge, d_pose_off,
+                          d_pose_edges, d_eout, d_hpose, d_bpose, d_hpoint, d_bpoint,
+                          (double *)s, &c->prof);
+    if (rc) return set_err(ORBG_EIO, "BA kernel launch failed");
     return ORBG_OK;
 }
 

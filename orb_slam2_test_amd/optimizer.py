@@ -38,3 +38,54 @@ def linearize_local_ba(poses, points, edges, device=0, with_edges=True):
                                       L.ptr(bpose), L.ptr(hpoint), L.ptr(bpoint)),
             "orbg_ba_linearize")
     return eout, hpose, bpose, hpoint, bpoint
+
+
+def pose_csr(edges, npose):
+    """Edge lists per pose (CSR): (pose_off[npose+1], pose_edges[nedge]) int32, the
+    layout orbg_ba_linearize_device reduces the MFMA pose blocks over."""
+    pose = np.asarray(edges["pose"], np.int64)
+    order = np.argsort(pose, kind="stable").astype(np.int32)
+    off = np.zeros(npose + 1, np.int32)
+    np.add.at(off, pose + 1, 1)
+    return np.cumsum(off).astype(np.int32), order
+
+
+class DeviceLBA:
+    """Device-resident batch of LBA windows (one graph; windows are independent blocks of
+    it): uploads once, then linearize() runs orbg_ba_linearize_device on the context stream
+    with every array in HBM -- the per-iteration work of g2o's computeActiveErrors +
+    buildSystem."""
+
+    def __init__(self, poses, points, edges, device=0):
+        import torch
+        self.ctx = _ctx(device)
+        self.np, self.nq, self.ne = len(poses), len(points), len(edges)
+        off, pe = pose_csr(edges, self.np)
+        dev = torch.device("cuda", device)
+
+        def up(a):
+            return torch.from_numpy(np.ascontiguousarray(a).view(np.uint8)).to(dev)
+
+        self.d_poses = up(np.ascontiguousarray(poses, L.POSE_DTYPE))
+        self.d_points = up(np.ascontiguousarray(points, np.float64))
+        self.d_edges = up(np.ascontiguousarray(edges, L.EDGE_DTYPE))
+        self.d_off, self.d_pe = up(off), up(pe)
+        self.d_eout = torch.zeros(self.ne * L.EDGE_OUT_DTYPE.itemsize, dtype=torch.uint8, device=dev)
+        self.d_hpose = torch.zeros((self.np, 6, 6), dtype=torch.float64, device=dev)
+        self.d_bpose = torch.zeros((self.np, 6), dtype=torch.float64, device=dev)
+        self.d_hpoint = torch.zeros((self.nq, 3, 3), dtype=torch.float64, device=dev)
+        self.d_bpoint = torch.zeros((self.nq, 3), dtype=torch.float64, device=dev)
+        torch.cuda.synchronize(dev)
+
+    def linearize(self):
+        p = lambda t: L.C.c_void_p(t.data_ptr())  # noqa: E731
+        L.check(L.lib().orbg_ba_linearize_device(
+            self.ctx.handle, p(self.d_poses), self.np, p(self.d_points), self.nq, p(self.d_edges),
+            self.ne, p(self.d_off), p(self.d_pe), p(self.d_eout), p(self.d_hpose),
+            p(self.d_bpose), p(self.d_hpoint), p(self.d_bpoint)), "orbg_ba_linearize_device")
+
+    def download(self):
+        self.ctx.sync()
+        eo = np.frombuffer(self.d_eout.cpu().numpy().tobytes(), L.EDGE_OUT_DTYPE)
+        return (eo, self.d_hpose.cpu().numpy(), self.d_bpose.cpu().numpy(),
+                self.d_hpoint.cpu().numpy(), self.d_bpoint.cpu().numpy())

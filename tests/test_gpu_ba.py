@@ -54,3 +54,37 @@ def test_empty_problem(oracle):
     poses, pts, edges = S.ba_window(n_points=10, seed=26)
     eo, hp, bp, hq, bq = linearize_local_ba(poses, pts, edges[:0])
     assert np.all(hp == 0) and np.all(hq == 0) and len(eo) == 0
+
+
+def concat_windows(ws):
+    """Independent LBA windows as one graph (vertex indices offset per window)."""
+    poses, pts, edges = [], [], []
+    po = qo = 0
+    for p, q, e in ws:
+        e = e.copy()
+        e["pose"] += po
+        e["point"] += qo
+        poses.append(p)
+        pts.append(q)
+        edges.append(e)
+        po += len(p)
+        qo += len(q)
+    return np.concatenate(poses), np.concatenate(pts), np.concatenate(edges)
+
+
+def test_device_resident_batched_windows(oracle):
+    """orbg_ba_linearize_device (HBM-resident, MFMA f64 pose blocks) on three windows at
+    once equals the oracle on the concatenated graph, and repeated calls are idempotent."""
+    from orb_slam2_test_amd.optimizer import DeviceLBA
+    poses, pts, edges = concat_windows([S.ba_window(n_points=600, seed=40 + i) for i in range(3)])
+    lba = DeviceLBA(poses, pts, edges)
+    lba.linearize()
+    lba.linearize()
+    eo, hp, bp, hq, bq = lba.download()
+    reo, rhp, rbp, rhq, rbq = oracle.ba_linearize(poses, pts, edges)
+    for name, g, r in (("err", eo["err"], reo["err"]), ("jt", eo["jt"], reo["jt"]),
+                       ("hpl", eo["hpl"], reo["hpl"]), ("hpose", hp, rhp), ("bpose", bp, rbp),
+                       ("hpoint", hq, rhq), ("bpoint", bq, rbq)):
+        assert rel(g, r) < RTOL, name
+    fixed = poses["fixed"] != 0
+    assert fixed.any() and not np.any(hp[fixed]) and not np.any(bp[fixed])
