@@ -221,12 +221,14 @@ int orbg_ba_linearize(orbg_ctx *ctx, const orbg_pose *poses, int npose, const do
                       double *hpose, double *bpose, double *hpoint, double *bpoint);
 
 /* Device-resident variant (batched LBA windows): every pointer is device memory, enqueued
- * on the context stream.  pose_off[npose+1] / pose_edges[nedge] list each pose's edges
- * (CSR); d_eout is required (the pose blocks are reduced from it); outputs are
- * overwritten.  Pose blocks H_pp | b_p are accumulated with MFMA f64. */
+ * on the context stream.  pose_off[npose+1] / pose_edges[nedge] and point_off[npoint+1] /
+ * point_edges[nedge] list each vertex's edges (CSR, built once per window: the graph does
+ * not change across LM iterations).  d_eout is required; outputs are overwritten.  Pose
+ * blocks H_pp | b_p are accumulated with MFMA f64, point blocks summed per point. */
 int orbg_ba_linearize_device(orbg_ctx *ctx, const orbg_pose *d_poses, int npose,
                              const double *d_points, int npoint, const orbg_edge *d_edges,
                              int nedge, const int32_t *d_pose_off, const int32_t *d_pose_edges,
+                             const int32_t *d_point_off, const int32_t *d_point_edges,
                              orbg_edge_out *d_eout, double *d_hpose, double *d_bpose,
                              double *d_hpoint, double *d_bpoint);
 

@@ -105,7 +105,7 @@ def lib():
                                                  i32, f32, i32, P(i32)]),
         "orbg_ba_linearize": (i32, [vp, vp, i32, vp, i32, vp, i32, vp, vp, vp, vp, vp]),
         "orbg_ba_linearize_device": (i32, [vp, vp, i32, vp, i32, vp, i32, vp, vp, vp, vp, vp, vp,
-                                           vp]),
+                                           vp, vp, vp]),
     }
     for name, (res, args) in sig.items():
         fn = getattr(L, name)

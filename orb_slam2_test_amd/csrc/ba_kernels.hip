@@ -8,8 +8,8 @@
 //   chi2, Huber rho' (float dsqr)                              base_edge.h:58-61, robust_kernel_impl.cpp:65-91
 //   constructQuadraticForm: H_pp += A^T W A, b_p += A^T w_r,   base_binary_edge.hpp:55-120
 //       H_ll += B^T W B, b_l += B^T w_r, H_pl = A^T W B
-// Point blocks are accumulated with fp64 global atomics (no-return global_atomic_add_f64);
-// pose blocks by k_ba_pose_mfma (MFMA f64 over each pose's edge rows).
+// Point blocks are summed per point over its edge list (k_ba_point_blocks, no atomics);
+// pose blocks by k_ba_pose_mfma (MFMA f64 over slices of each pose's edge rows).
 #include <hip/hip_runtime.h>
 
 #include <cstring>
@@ -40,24 +40,26 @@ __device__ __forceinline__ void quat_rotate(const double q[4], const double v[3]
 // edge: rows[e][k] = {J_pose[k][0..5], -e[k], w} (w = rho' * invSigma2; mono edges have a
 // zero third row, inactive edges zero rows).
 // ---------------------------------------------------------------------------
-#define BA_ROW 8  // doubles per pose row
+#define BA_ROW 8    // doubles per pose row
+#define BA_PROW 12  // doubles per edge share of its point block
 
 __global__ __launch_bounds__(256) void k_ba_edges(const orbg_pose *__restrict__ poses,
                                                   const double *__restrict__ points,
                                                   const orbg_edge *__restrict__ edges, int nedge,
                                                   orbg_edge_out *__restrict__ eout,
                                                   double *__restrict__ rows,
-                                                  double *__restrict__ hpoint,
-                                                  double *__restrict__ bpoint)
+                                                  double *__restrict__ prow)
 {
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= nedge) return;
     const orbg_edge e = edges[i];
     orbg_edge_out *o = eout + i;
     double *row = rows + (size_t)i * 3 * BA_ROW;
+    double *pr = prow + (size_t)i * BA_PROW;
     if (!e.active) {
         memset(o, 0, sizeof(*o));
         for (int k = 0; k < 3 * BA_ROW; k++) row[k] = 0;
+        for (int k = 0; k < BA_PROW; k++) pr[k] = 0;
         return;
     }
     const orbg_pose P = poses[e.pose];
@@ -152,19 +154,20 @@ __global__ __launch_bounds__(256) void k_ba_edges(const orbg_pose *__restrict__ 
     double wr[3];
 #pragma unroll
     for (int k = 0; k < 3; k++) wr[k] = -info * err[k] * rho1;
-    double *hp = hpoint + 9 * (size_t)e.point, *bp = bpoint + 3 * (size_t)e.point;
+    // this edge's share of the point block (k_ba_point_blocks adds a point's edges in list
+    // order: no atomics, deterministic): pr = {H_ll row-major (9), b_l (3)}
 #pragma unroll
     for (int r = 0; r < 3; r++) {
         double acc = 0;
 #pragma unroll
         for (int k = 0; k < 3; k++) acc += jp[k][r] * wr[k];
-        atomicAdd(&bp[r], acc);
+        pr[9 + r] = acc;
 #pragma unroll
         for (int c = 0; c < 3; c++) {
             double a2 = 0;
 #pragma unroll
             for (int k = 0; k < 3; k++) a2 += jp[k][r] * w * jp[k][c];
-            atomicAdd(&hp[r * 3 + c], a2);
+            pr[r * 3 + c] = a2;
         }
     }
     // H_pl = J_point^T W J_pose (stored per edge, base_binary_edge.hpp:105-117)
@@ -198,24 +201,31 @@ __global__ __launch_bounds__(256) void k_ba_edges(const orbg_pose *__restrict__ 
 // ---------------------------------------------------------------------------
 typedef double v4d __attribute__((ext_vector_type(4)));
 
+#define BA_SLICE 64  // edges per wave: a pose's rows are split over waves, blocks add up
+
 __global__ __launch_bounds__(256) void k_ba_pose_mfma(const orbg_pose *__restrict__ poses,
                                                       int npose,
                                                       const int32_t *__restrict__ pose_off,
                                                       const int32_t *__restrict__ pose_edges,
+                                                      const int32_t *__restrict__ slice_off,
+                                                      const int32_t *__restrict__ slice_pose,
+                                                      int nslice,
                                                       const double *__restrict__ rows,
                                                       double *__restrict__ hpose,
                                                       double *__restrict__ bpose)
 {
     const int lane = threadIdx.x & 63;
-    const int p = blockIdx.x * 4 + (threadIdx.x >> 6);
-    if (p >= npose) return;
+    const int sl = blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (sl >= nslice) return;
+    const int p = slice_pose[sl];
+    if (p < 0) return;           // past the last slice (table filled with -1)
+    if (poses[p].fixed) return;  // stays zero (memset): g2o builds no block for it
     double *H = hpose + 36 * (size_t)p, *bv = bpose + 6 * (size_t)p;
-    if (poses[p].fixed) {
-        if (lane < 36) H[lane] = 0;
-        if (lane < 6) bv[lane] = 0;
-        return;
-    }
-    const int e0 = pose_off[p], ne = pose_off[p + 1] - e0;
+    // this wave = slice (sl - slice_off[p]) of pose p: edges [e0, e0 + ne) of its list
+    const int e0p = pose_off[p], nep = pose_off[p + 1] - e0p;
+    const int ks = sl - slice_off[p];
+    const int e0 = e0p + ks * BA_SLICE;
+    const int ne = min(BA_SLICE, nep - ks * BA_SLICE);
     const int nrow = 3 * ne;
     const int i = lane & 15, k = lane >> 4;  // A: (row i of the 16x4 tile, k); B: (k, column i)
     const int col = i < 7 ? i : 7;           // padded columns read the weight and are zeroed
@@ -243,12 +253,83 @@ __global__ __launch_bounds__(256) void k_ba_pose_mfma(const orbg_pose *__restric
 #pragma unroll
     for (int v = 0; v < 4; v++) {
         const int row = (lane >> 4) + 4 * v;
-        if (row < 6 && j < 6) H[row * 6 + j] = C[v];
-        if (row < 6 && j == 6) bv[row] = C[v];
+        if (row < 6 && j < 6) atomicAdd(&H[row * 6 + j], C[v]);
+        if (row < 6 && j == 6) atomicAdd(&bv[row], C[v]);
     }
 }
 
+// k_ba_point_blocks: thread per point, sums its edges' shares in list order
+__global__ __launch_bounds__(256) void k_ba_point_blocks(int npoint,
+                                                         const int32_t *__restrict__ point_off,
+                                                         const int32_t *__restrict__ point_edges,
+                                                         const double *__restrict__ prow,
+                                                         double *__restrict__ hpoint,
+                                                         double *__restrict__ bpoint)
+{
+    const int q = blockIdx.x * blockDim.x + threadIdx.x;
+    if (q >= npoint) return;
+    double acc[BA_PROW];
+#pragma unroll
+    for (int k = 0; k < BA_PROW; k++) acc[k] = 0;
+    for (int a = point_off[q]; a < point_off[q + 1]; a++) {
+        const double2 *pr = (const double2 *)(prow + (size_t)point_edges[a] * BA_PROW);
+#pragma unroll
+        for (int k = 0; k < BA_PROW / 2; k++) {
+            const double2 v = pr[k];
+            acc[2 * k] += v.x;
+            acc[2 * k + 1] += v.y;
+        }
+    }
+#pragma unroll
+    for (int k = 0; k < 9; k++) hpoint[9 * (size_t)q + k] = acc[k];
+#pragma unroll
+    for (int k = 0; k < 3; k++) bpoint[3 * (size_t)q + k] = acc[9 + k];
+}
+
+// slice -> pose table: pose p owns ceil(edges_p / BA_SLICE) consecutive slices
+__global__ __launch_bounds__(256) void k_ba_slices(const int32_t *__restrict__ pose_off,
+                                                   int npose, int32_t *__restrict__ slice_off,
+                                                   int32_t *__restrict__ slice_pose, int *nslice)
+{
+    // single workgroup: exclusive scan of per-pose slice counts, then fill
+    __shared__ int run;
+    if (threadIdx.x == 0) run = 0;
+    __syncthreads();
+    for (int p0 = 0; p0 < npose; p0 += 256) {
+        const int p = p0 + threadIdx.x;
+        const int n = p < npose ? (pose_off[p + 1] - pose_off[p] + BA_SLICE - 1) / BA_SLICE : 0;
+        int x = n;  // inclusive block scan (simple, npose is small)
+        __shared__ int sc[256];
+        sc[threadIdx.x] = x;
+        __syncthreads();
+        for (int o = 1; o < 256; o <<= 1) {
+            const int y = threadIdx.x >= o ? sc[threadIdx.x - o] : 0;
+            __syncthreads();
+            sc[threadIdx.x] += y;
+            __syncthreads();
+        }
+        const int excl = run + sc[threadIdx.x] - n;
+        if (p < npose) {
+            slice_off[p] = excl;
+            for (int q = 0; q < n; q++) slice_pose[excl + q] = p;
+        }
+        __syncthreads();
+        if (threadIdx.x == 255) run += sc[255];
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) *nslice = run;
+}
+
 static size_t al(size_t x) { return (x + 255) & ~(size_t)255; }
+
+// rows + slice tables (upper bound: one slice per pose plus one per BA_SLICE edges)
+size_t ba_rows_bytes(int nedge, int npose)
+{
+    const size_t ns = (size_t)(npose > 0 ? npose : 1) + (size_t)(nedge > 0 ? nedge : 1) / BA_SLICE;
+    return al((size_t)(nedge > 0 ? nedge : 1) * 3 * BA_ROW * 8) +
+           al((size_t)(nedge > 0 ? nedge : 1) * BA_PROW * 8) + al((npose + 1) * 4) +
+           al(ns * 4) + 256;
+}
 
 size_t ba_scratch_bytes(int npose, int npoint, int nedge)
 {
@@ -256,32 +337,54 @@ size_t ba_scratch_bytes(int npose, int npoint, int nedge)
                  ne = (size_t)(nedge > 0 ? nedge : 1);
     return al(np * sizeof(orbg_pose)) + al(nq * 24) + al(ne * sizeof(orbg_edge)) +
            al(ne * sizeof(orbg_edge_out)) + al(np * 36 * 8) + al(np * 6 * 8) + al(nq * 9 * 8) +
-           al(nq * 3 * 8) + al((np + 1) * 4) + al(ne * 4) + al(ne * 3 * BA_ROW * 8);
+           al(nq * 3 * 8) + al((np + 1) * 4) + 2 * al(ne * 4) + al((nq + 1) * 4) +
+           ba_rows_bytes(nedge, npose);
 }
 
-size_t ba_rows_bytes(int nedge) { return (size_t)(nedge > 0 ? nedge : 1) * 3 * BA_ROW * 8; }
 
 // device-resident linearisation: every pointer is device memory; rows = ba_rows_bytes(nedge)
 int launch_ba_device(hipStream_t st, const orbg_pose *poses, int npose, const double *points,
                      int npoint, const orbg_edge *edges, int nedge, const int32_t *pose_off,
-                     const int32_t *pose_edges, orbg_edge_out *eout, double *hpose, double *bpose,
-                     double *hpoint, double *bpoint, double *rows, void *prof)
+                     const int32_t *pose_edges, const int32_t *point_off,
+                     const int32_t *point_edges, orbg_edge_out *eout, double *hpose,
+                     double *bpose, double *hpoint, double *bpoint, double *rows, void *prof)
 {
-    if (npoint && (hipMemsetAsync(hpoint, 0, (size_t)npoint * 9 * 8, st) != hipSuccess ||
-                   hipMemsetAsync(bpoint, 0, (size_t)npoint * 3 * 8, st) != hipSuccess))
-        return -5;
+    double *prow = (double *)((uint8_t *)rows + al((size_t)(nedge > 0 ? nedge : 1) * 3 * BA_ROW * 8));
     if (nedge) {
         hipEvent_t a = nullptr;
         prof_begin(prof, st, "ba_edges", &a);
         hipLaunchKernelGGL(k_ba_edges, dim3((nedge + 255) / 256), dim3(256), 0, st, poses, points,
-                           edges, nedge, eout, rows, hpoint, bpoint);
+                           edges, nedge, eout, rows, prow);
         prof_end(prof, st, "ba_edges", a);
     }
+    if (npoint) {
+        hipEvent_t a = nullptr;
+        prof_begin(prof, st, "ba_point_blocks", &a);
+        hipLaunchKernelGGL(k_ba_point_blocks, dim3((npoint + 255) / 256), dim3(256), 0, st,
+                           npoint, point_off, point_edges, prow, hpoint, bpoint);
+        prof_end(prof, st, "ba_point_blocks", a);
+    }
     if (npose) {
+        // scratch after rows and point shares: slice_off[npose+1], slice_pose[max], nslice
+        uint8_t *t = (uint8_t *)prow + al((size_t)(nedge > 0 ? nedge : 1) * BA_PROW * 8);
+        int32_t *slice_off = (int32_t *)t;
+        t += al((npose + 1) * 4);
+        int32_t *slice_pose = (int32_t *)t;
+        const int max_slices = npose + (nedge > 0 ? nedge : 1) / BA_SLICE;
+        t += al((size_t)max_slices * 4);
+        int *d_nslice = (int *)t;
+        if (hipMemsetAsync(hpose, 0, (size_t)npose * 36 * 8, st) != hipSuccess ||
+            hipMemsetAsync(bpose, 0, (size_t)npose * 6 * 8, st) != hipSuccess)
+            return -5;
+        if (hipMemsetAsync(slice_pose, 0xFF, (size_t)max_slices * 4, st) != hipSuccess) return -5;
+        hipLaunchKernelGGL(k_ba_slices, dim3(1), dim3(256), 0, st, pose_off, npose, slice_off,
+                           slice_pose, d_nslice);
         hipEvent_t a = nullptr;
         prof_begin(prof, st, "ba_pose_mfma", &a);
-        hipLaunchKernelGGL(k_ba_pose_mfma, dim3((npose + 3) / 4), dim3(256), 0, st, poses, npose,
-                           pose_off, pose_edges, rows, hpose, bpose);
+        // the grid covers the bound; waves past the actual slice count exit at once
+        hipLaunchKernelGGL(k_ba_pose_mfma, dim3((max_slices + 3) / 4), dim3(256), 0, st, poses,
+                           npose, pose_off, pose_edges, slice_off, slice_pose, max_slices, rows,
+                           hpose, bpose);
         prof_end(prof, st, "ba_pose_mfma", a);
     }
     return hipGetLastError() == hipSuccess ? 0 : -5;
@@ -290,8 +393,9 @@ int launch_ba_device(hipStream_t st, const orbg_pose *poses, int npose, const do
 // host arrays in/out: upload, build nothing on the device but the blocks, download
 int launch_ba(hipStream_t st, const orbg_pose *poses, int npose, const double *points,
               int npoint, const orbg_edge *edges, int nedge, const int32_t *pose_off,
-              const int32_t *pose_edges, orbg_edge_out *eout, double *hpose, double *bpose,
-              double *hpoint, double *bpoint, void *scratch, void *prof)
+              const int32_t *pose_edges, const int32_t *point_off, const int32_t *point_edges,
+              orbg_edge_out *eout, double *hpose, double *bpose, double *hpoint, double *bpoint,
+              void *scratch, void *prof)
 {
     uint8_t *s = (uint8_t *)scratch;
     const size_t np = (size_t)(npose > 0 ? npose : 1), nq = (size_t)(npoint > 0 ? npoint : 1),
@@ -316,6 +420,10 @@ int launch_ba(hipStream_t st, const orbg_pose *poses, int npose, const double *p
     s += al((np + 1) * 4);
     int32_t *d_pe = (int32_t *)s;
     s += al(ne * 4);
+    int32_t *d_qoff = (int32_t *)s;
+    s += al((nq + 1) * 4);
+    int32_t *d_qe = (int32_t *)s;
+    s += al(ne * 4);
     double *d_rows = (double *)s;
 #define CK(x)                                                                              \
     if ((x) != hipSuccess) return -5
@@ -324,8 +432,11 @@ int launch_ba(hipStream_t st, const orbg_pose *poses, int npose, const double *p
     if (nedge) CK(hipMemcpyAsync(d_edges, edges, nedge * sizeof(orbg_edge), hipMemcpyHostToDevice, st));
     if (npose) CK(hipMemcpyAsync(d_off, pose_off, (npose + 1) * 4, hipMemcpyHostToDevice, st));
     if (nedge) CK(hipMemcpyAsync(d_pe, pose_edges, nedge * 4, hipMemcpyHostToDevice, st));
+    if (npoint) CK(hipMemcpyAsync(d_qoff, point_off, (npoint + 1) * 4, hipMemcpyHostToDevice, st));
+    if (nedge) CK(hipMemcpyAsync(d_qe, point_edges, nedge * 4, hipMemcpyHostToDevice, st));
     const int rc = launch_ba_device(st, d_pose, npose, d_pts, npoint, d_edges, nedge, d_off, d_pe,
-                                    d_eout, d_hpose, d_bpose, d_hpt, d_bpt, d_rows, prof);
+                                    d_qoff, d_qe, d_eout, d_hpose, d_bpose, d_hpt, d_bpt, d_rows,
+                                    prof);
     if (rc) return rc;
     if (eout && nedge)
         CK(hipMemcpyAsync(eout, d_eout, nedge * sizeof(orbg_edge_out), hipMemcpyDeviceToHost, st));

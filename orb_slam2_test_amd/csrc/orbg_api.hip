@@ -51,13 +51,15 @@ int launch_init_match_single(hipStream_t st, const orbg_keypoint *k1, const uint
 // ba_kernels.hip
 int launch_ba(hipStream_t st, const orbg_pose *poses, int npose, const double *points,
               int npoint, const orbg_edge *edges, int nedge, const int32_t *pose_off,
-              const int32_t *pose_edges, orbg_edge_out *eout, double *hpose, double *bpose,
-              double *hpoint, double *bpoint, void *scratch, void *prof);
+              const int32_t *pose_edges, const int32_t *point_off, const int32_t *point_edges,
+              orbg_edge_out *eout, double *hpose, double *bpose, double *hpoint, double *bpoint,
+              void *scratch, void *prof);
 int launch_ba_device(hipStream_t st, const orbg_pose *poses, int npose, const double *points,
                      int npoint, const orbg_edge *edges, int nedge, const int32_t *pose_off,
-                     const int32_t *pose_edges, orbg_edge_out *eout, double *hpose, double *bpose,
-                     double *hpoint, double *bpoint, double *rows, void *prof);
-size_t ba_rows_bytes(int nedge);
+                     const int32_t *pose_edges, const int32_t *point_off,
+                     const int32_t *point_edges, orbg_edge_out *eout, double *hpose,
+                     double *bpose, double *hpoint, double *bpoint, double *rows, void *prof);
+size_t ba_rows_bytes(int nedge, int npose);
 size_t ba_scratch_bytes(int npose, int npoint, int nedge);
 }  // namespace orbg
 
@@ -1254,20 +1256,28 @@ extern "C" int orbg_ba_linearize(orbg_ctx *c, const orbg_pose *poses, int npose,
             edges[i].point >= npoint)
             return set_err(ORBG_EINVAL, "edge %d references a missing vertex", i);
     HIPCHK(hipSetDevice(c->device));
-    // edge lists per pose (CSR) for the MFMA pose-block reduction
+    // edge lists per pose and per point (CSR): MFMA pose blocks, summed point blocks
     std::vector<int32_t> off(npose + 1, 0), pe(nedge > 0 ? nedge : 1);
-    for (int i = 0; i < nedge; i++) off[edges[i].pose + 1]++;
+    std::vector<int32_t> qoff(npoint + 1, 0), qe(nedge > 0 ? nedge : 1);
+    for (int i = 0; i < nedge; i++) {
+        off[edges[i].pose + 1]++;
+        qoff[edges[i].point + 1]++;
+    }
     for (int p = 0; p < npose; p++) off[p + 1] += off[p];
+    for (int q = 0; q < npoint; q++) qoff[q + 1] += qoff[q];
     {
-        std::vector<int32_t> fill(off.begin(), off.end() - 1);
-        for (int i = 0; i < nedge; i++) pe[fill[edges[i].pose]++] = i;
+        std::vector<int32_t> fill(off.begin(), off.end() - 1), qfill(qoff.begin(), qoff.end() - 1);
+        for (int i = 0; i < nedge; i++) {
+            pe[fill[edges[i].pose]++] = i;
+            qe[qfill[edges[i].point]++] = i;
+        }
     }
     const size_t sb = ba_scratch_bytes(npose, npoint, nedge);
     void *s;
     int rc = scratch(c, sb, &s);
     if (rc) return rc;
     rc = launch_ba(c->stream, poses, npose, points, npoint, edges, nedge, off.data(), pe.data(),
-                   eout, hpose, bpose, hpoint, bpoint, s, &c->prof);
+                   qoff.data(), qe.data(), eout, hpose, bpose, hpoint, bpoint, s, &c->prof);
     if (rc) return rc;
     HIPCHK(hipStreamSynchronize(c->stream));
     c->prof.collect();
@@ -1278,22 +1288,24 @@ extern "C" int orbg_ba_linearize_device(orbg_ctx *c, const orbg_pose *d_poses, i
                                         const double *d_points, int npoint,
                                         const orbg_edge *d_edges, int nedge,
                                         const int32_t *d_pose_off, const int32_t *d_pose_edges,
-                                        orbg_edge_out *d_eout, double *d_hpose, double *d_bpose,
-                                        double *d_hpoint, double *d_bpoint)
+                                        const int32_t *d_point_off,
+                                        const int32_t *d_point_edges, orbg_edge_out *d_eout,
+                                        double *d_hpose, double *d_bpose, double *d_hpoint,
+                                        double *d_bpoint)
 {
     if (!c) return set_err(ORBG_EINVAL, "ctx is NULL");
     if (npose < 0 || npoint < 0 || nedge < 0) return set_err(ORBG_EINVAL, "negative size");
     if ((nedge && (!d_edges || !d_eout)) || (npose && (!d_poses || !d_pose_off || !d_pose_edges ||
                                                        !d_hpose || !d_bpose)) ||
-        (npoint && (!d_points || !d_hpoint || !d_bpoint)))
+        (npoint && (!d_points || !d_hpoint || !d_bpoint || !d_point_off || !d_point_edges)))
         return set_err(ORBG_EINVAL, "NULL device array");
     HIPCHK(hipSetDevice(c->device));
     void *s;
-    int rc = scratch(c, ba_rows_bytes(nedge), &s);
+    int rc = scratch(c, ba_rows_bytes(nedge, npose), &s);
     if (rc) return rc;
     rc = launch_ba_device(c->stream, d_poses, npose, d_points, npoint, d_edges, nedge, d_pose_off,
-                          d_pose_edges, d_eout, d_hpose, d_bpose, d_hpoint, d_bpoint,
-                          (double *)s, &c->prof);
+                          d_pose_edges, d_point_off, d_point_edges, d_eout, d_hpose, d_bpose,
+                          d_hpoint, d_bpoint, (double *)s, &c->prof);
     if (rc) return set_err(ORBG_EIO, "BA kernel launch failed");
     return ORBG_OK;
 }

@@ -40,13 +40,13 @@ def linearize_local_ba(poses, points, edges, device=0, with_edges=True):
     return eout, hpose, bpose, hpoint, bpoint
 
 
-def pose_csr(edges, npose):
-    """Edge lists per pose (CSR): (pose_off[npose+1], pose_edges[nedge]) int32, the
-    layout orbg_ba_linearize_device reduces the MFMA pose blocks over."""
-    pose = np.asarray(edges["pose"], np.int64)
-    order = np.argsort(pose, kind="stable").astype(np.int32)
-    off = np.zeros(npose + 1, np.int32)
-    np.add.at(off, pose + 1, 1)
+def vertex_csr(edges, field, nvert):
+    """Edge lists per vertex (CSR): (off[nvert+1], edge ids[nedge]) int32, edges in input
+    order within a vertex -- the layout orbg_ba_linearize_device reduces blocks over."""
+    v = np.asarray(edges[field], np.int64)
+    order = np.argsort(v, kind="stable").astype(np.int32)
+    off = np.zeros(nvert + 1, np.int64)
+    np.add.at(off, v + 1, 1)
     return np.cumsum(off).astype(np.int32), order
 
 
@@ -60,7 +60,8 @@ class DeviceLBA:
         import torch
         self.ctx = _ctx(device)
         self.np, self.nq, self.ne = len(poses), len(points), len(edges)
-        off, pe = pose_csr(edges, self.np)
+        off, pe = vertex_csr(edges, "pose", self.np)
+        qoff, qe = vertex_csr(edges, "point", self.nq)
         dev = torch.device("cuda", device)
 
         def up(a):
@@ -70,6 +71,7 @@ class DeviceLBA:
         self.d_points = up(np.ascontiguousarray(points, np.float64))
         self.d_edges = up(np.ascontiguousarray(edges, L.EDGE_DTYPE))
         self.d_off, self.d_pe = up(off), up(pe)
+        self.d_qoff, self.d_qe = up(qoff), up(qe)
         self.d_eout = torch.zeros(self.ne * L.EDGE_OUT_DTYPE.itemsize, dtype=torch.uint8, device=dev)
         self.d_hpose = torch.zeros((self.np, 6, 6), dtype=torch.float64, device=dev)
         self.d_bpose = torch.zeros((self.np, 6), dtype=torch.float64, device=dev)
@@ -81,7 +83,8 @@ class DeviceLBA:
         p = lambda t: L.C.c_void_p(t.data_ptr())  # noqa: E731
         L.check(L.lib().orbg_ba_linearize_device(
             self.ctx.handle, p(self.d_poses), self.np, p(self.d_points), self.nq, p(self.d_edges),
-            self.ne, p(self.d_off), p(self.d_pe), p(self.d_eout), p(self.d_hpose),
+            self.ne, p(self.d_off), p(self.d_pe), p(self.d_qoff), p(self.d_qe), p(self.d_eout),
+            p(self.d_hpose),
             p(self.d_bpose), p(self.d_hpoint), p(self.d_bpoint)), "orbg_ba_linearize_device")
 
     def download(self):

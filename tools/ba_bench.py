@@ -1,0 +1,97 @@
+#!/usr/bin/env python3
+"""LocalBundleAdjustment linearisation throughput (configs[4]: KITTI00-like windows).
+
+One "iteration" = g2o's computeActiveErrors + buildSystem arithmetic for every edge of W
+independent LBA windows (10 local + 10 fixed KFs, 6000 points, ~27k edges, 60% stereo,
+KITTI intrinsics), HBM-resident, through orbg_ba_linearize_device: k_ba_edges (thread per
+edge, fp64) + k_ba_pose_mfma (MFMA f64 pose blocks).  Prints one JSON line with edges/s,
+per-kernel HIP-event times, the HBM roofline of k_ba_edges (108 algorithmic
+bytes per edge) and the oracle (fp64 C restatement) on one window on one host core.
+
+    python tools/ba_bench.py [--windows 64] [--iters 20] [--warmup 3]
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+HBM_PEAK_GBS = 8000.0
+EDGE_ALGO_BYTES = 108  # per-edge algorithmic bytes
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--windows", type=int, default=64)
+    ap.add_argument("--distinct", type=int, default=4, help="distinct synthetic windows, tiled")
+    ap.add_argument("--iters", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--no-cpu", action="store_true")
+    args = ap.parse_args()
+
+    import torch
+    from orb_slam2_test_amd import synthetic as S
+    from orb_slam2_test_amd.optimizer import DeviceLBA
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    from test_gpu_ba import concat_windows
+
+    base = [S.ba_window(seed=500 + i) for i in range(args.distinct)]
+    poses, pts, edges = concat_windows([base[i % args.distinct] for i in range(args.windows)])
+    lba = DeviceLBA(poses, pts, edges)
+    for _ in range(args.warmup):
+        lba.linearize()
+    lba.ctx.sync()
+    lba.ctx.profile(True)
+    lba.ctx.profile_reset()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.iters):
+        lba.linearize()
+    lba.ctx.sync()
+    torch.cuda.synchronize()
+    dt = time.perf_counter() - t0
+    kern = lba.ctx.profile_read()
+    lba.ctx.profile(False)
+    ne = len(edges)
+    out = {
+        "metric": "LBA linearisation edges/s (computeActiveErrors + buildSystem arithmetic)",
+        "value": round(ne * args.iters / dt, 1), "unit": "edges/s", "higher_is_better": True,
+        "dtype": "f64", "data": "synthetic",
+        "config": {"workload": "configs[4]: %d KITTI00-like LBA windows (20 KFs, 6000 points)"
+                               % args.windows, "edges": ne, "poses": len(poses),
+                   "points": len(pts), "stereo_frac": round(float(np.mean(edges["stereo"])), 3)},
+        "ms_per_iter": round(dt / args.iters * 1e3, 4),
+        "kernels": {k: {"ms_per_iter": round(v[0] / args.iters, 4),
+                        "avg_launch_ms": round(v[0] / max(v[1], 1), 5)} for k, v in kern.items()},
+    }
+    if "ba_edges" in kern:
+        ms = kern["ba_edges"][0] / max(kern["ba_edges"][1], 1)
+        ach = ne * EDGE_ALGO_BYTES / (ms * 1e-3) / 1e9
+        out["roofline"] = {"kernel": "ba_edges", "bound": "hbm", "achieved": round(ach, 1),
+                           "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                           "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": None,
+                           "algo_bytes_per_launch": ne * EDGE_ALGO_BYTES,
+                           "avg_launch_ms": round(ms, 5)}
+    if not args.no_cpu:
+        from oracle import pyoracle as O
+        p, q, e = base[0]
+        t0 = time.perf_counter()
+        reps = 0
+        while time.perf_counter() - t0 < 5.0:
+            O.ba_linearize(p, q, e)
+            reps += 1
+        cdt = time.perf_counter() - t0
+        out["cpu_baseline"] = {"value": round(len(e) * reps / cdt, 1), "unit": "edges/s",
+                               "cores": 1, "kind": "port",
+                               "sample": "%d x one window (%d edges), oracle/ba_oracle.c -O3, "
+                                         "1 thread, %.1f s" % (reps, len(e), cdt)}
+    print(json.dumps(out), flush=True)
+
+
+if __name__ == "__main__":
+    main()
