@@ -22,6 +22,7 @@
  *   orbg_search_for_initialization .. ORBmatcher(nnratio,checkOri).SearchForInitialization(
  *                                     F1, F2, vbPrevMatched, vnMatches12, windowSize)
  *                                                                      src/ORBmatcher.cc:487-631
+ *   orbg_stereo_batch_device ........ Frame::ComputeStereoMatches  src/Frame.cc:619-834
  *   orbg_ba_linearize ............... g2o computeActiveErrors + BlockSolver::buildSystem arithmetic
  *                                     for EdgeSE3ProjectXYZ / EdgeStereoSE3ProjectXYZ inside
  *                                     Optimizer::LocalBundleAdjustment  src/Optimizer.cc:633-979
@@ -143,6 +144,22 @@ int orbg_download_matches(orbg_ctx *ctx, int pair, int32_t *knn, int32_t *matche
  * per-frame outputs alternate between two buffers (orbg_batch_outputs returns the ones of
  * the last extraction); every host-side read (download, get_level, stats, sync) drains
  * both streams. */
+/* Frame::ComputeStereoMatches (src/Frame.cc:619-834) for npairs (left, right) frames of the
+ * last batch: row-band descriptor match, 11x11 SAD refinement at the keypoint's level,
+ * parabola, median cut.  bf = Frame::mbf; min_z = Frame::mb, which the reference reads before
+ * assigning it (Frame.cc:661 vs :148) -- pass bf / fx, the value assigned right after
+ * (min_z <= 0: no maximum disparity).  Runs on the context stream (it reads this batch's
+ * pyramid).  Results per pair over the left frame's keypoints: mvuRight, mvDepth (-1 where
+ * unmatched) and the number of depths. */
+int orbg_stereo_batch_device(orbg_ctx *ctx, const int32_t *left, const int32_t *right,
+                             int npairs, float bf, float min_z);
+int orbg_stereo_outputs(orbg_ctx *ctx, float **d_uright /* [npairs][frame_cap] */,
+                        float **d_depth /* [npairs][frame_cap] */,
+                        int32_t **d_nvalid /* [npairs] */, int32_t *frame_cap);
+/* copies cap entries of pair `pair` (synchronises) */
+int orbg_download_stereo(orbg_ctx *ctx, int pair, float *uright, float *depth, int cap,
+                         int32_t *nvalid);
+
 int orbg_sync(orbg_ctx *ctx);
 void *orbg_stream(orbg_ctx *ctx);       /* hipStream_t of extraction (and host-data calls) */
 void *orbg_match_stream(orbg_ctx *ctx); /* hipStream_t of batch matching and the summary */

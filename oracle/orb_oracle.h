@@ -16,6 +16,7 @@
  *   ORBmatcher::DescriptorDistance .. src/ORBmatcher.cc:1846-1862
  *   ORBmatcher::SearchForInit ....... src/ORBmatcher.cc:487-631, 1800-1841
  *   Frame grid / GetFeaturesInArea .. src/Frame.cc:292-307, 421-520
+ *   Frame::ComputeStereoMatches ..... src/Frame.cc:619-834 (stereo_oracle.c)
  *   g2o edge arithmetic (double) .... Thirdparty/g2o/g2o/types/types_six_dof_expmap.{h,cpp},
  *                                     core/base_binary_edge.hpp:55-120, core/base_edge.h:58-102,
  *                                     core/robust_kernel_impl.cpp:65-91
@@ -130,6 +131,16 @@ int orc_search_for_initialization(const orc_keypoint *kps1, const uint8_t *desc1
                                   const orc_keypoint *kps2, const uint8_t *desc2, int n2,
                                   const orc_bounds *b2, float *prev_xy, int32_t *matches12,
                                   int window, float nnratio, int check_ori);
+
+/* ---- Frame::ComputeStereoMatches (stereo_oracle.c) ----
+ * kl/dl: left keypoints (mvKeys) + descriptors, kr/dr: right.  pyr_l / pyr_r: the two
+ * pyramids packed as orc_extract writes them.  min_z: Frame::mb (see stereo_oracle.c).
+ * uright/depth[nl] receive mvuRight / mvDepth (-1 where unmatched).  Returns the number of
+ * keypoints with a depth. */
+int orc_stereo_matches(const orc_params *p, const orc_keypoint *kl, const uint8_t *dl, int nl,
+                       const orc_keypoint *kr, const uint8_t *dr, int nr, const uint8_t *pyr_l,
+                       const uint8_t *pyr_r, int w, int h, float bf, float min_z,
+                       float *uright, float *depth);
 
 /* ---- local BA edge linearisation (double) ---- */
 typedef struct {

@@ -94,6 +94,8 @@ def lib():
         L.orc_extract_batch.restype = C.c_long
         L.orc_ba_linearize.argtypes = [vp, C.c_int, vp, C.c_int, vp, C.c_int, vp, vp, vp, vp, vp]
         L.orc_ba_numeric_jacobian.argtypes = [vp, vp, vp, vp, vp]
+        L.orc_stereo_matches.argtypes = [P(Params), vp, vp, C.c_int, vp, vp, C.c_int, vp, vp,
+                                         C.c_int, C.c_int, C.c_float, C.c_float, vp, vp]
         _lib = L
     return _lib
 
@@ -221,6 +223,24 @@ def search_for_initialization(kps1, desc1, kps2, desc2, prev_xy, bounds, window=
                                             len(kps2), C.byref(b), _p(prev), _p(m12), window,
                                             nnratio, 1 if check_ori else 0)
     return n, m12, prev
+
+
+def stereo_matches(p, left, right, w, h, bf, min_z):
+    """Frame::ComputeStereoMatches restated (oracle/stereo_oracle.c).  left / right are
+    extract(..., with_pyramid=True) results of the two images.  Returns (uRight, depth)
+    float32 arrays over the left keypoints (-1 where unmatched)."""
+    def packed(r):
+        return np.ascontiguousarray(np.concatenate([lv.reshape(-1) for lv in r["pyramid"]]))
+    kl = np.ascontiguousarray(left["kps"], KP_DTYPE)
+    kr = np.ascontiguousarray(right["kps"], KP_DTYPE)
+    dl = np.ascontiguousarray(left["desc"], np.uint8)
+    dr = np.ascontiguousarray(right["desc"], np.uint8)
+    ur = np.zeros(max(len(kl), 1), np.float32)
+    dp = np.zeros(max(len(kl), 1), np.float32)
+    pl, pr = packed(left), packed(right)
+    lib().orc_stereo_matches(C.byref(p), _p(kl), _p(dl), len(kl), _p(kr), _p(dr), len(kr),
+                             _p(pl), _p(pr), w, h, float(bf), float(min_z), _p(ur), _p(dp))
+    return ur[:len(kl)].copy(), dp[:len(kl)].copy()
 
 
 def frames_batch(p, imgs, nthreads=1, window=100, nnratio=0.9):

@@ -60,6 +60,13 @@ int launch_ba_device(hipStream_t st, const orbg_pose *poses, int npose, const do
                      const int32_t *point_edges, orbg_edge_out *eout, double *hpose,
                      double *bpose, double *hpoint, double *bpoint, double *rows, void *prof);
 size_t ba_rows_bytes(int nedge, int npose);
+// stereo_kernels.hip
+size_t stereo_scratch_bytes(int npairs, int frame_cap);
+int launch_stereo(hipStream_t st, const OrbgGeom &g, const orbg_keypoint *kps,
+                  const uint8_t *desc, const int32_t *counts, const int32_t *d_left,
+                  const int32_t *d_right, int npairs, const uint8_t *img0, int64_t img_fs,
+                  int img_pitch, const uint8_t *pyr, float bf, float min_z, void *scratch,
+                  float *uright, float *depth, int32_t *nvalid, void *prof);
 size_t ba_scratch_bytes(int npose, int npoint, int nedge);
 }  // namespace orbg
 
@@ -230,6 +237,12 @@ struct orbg_ctx {
     uint32_t *d_topk = nullptr;
     int32_t *d_topk_n = nullptr;
     int last_npairs = 0;
+    // stereo (ComputeStereoMatches) of the last batch
+    int32_t *d_spairs = nullptr;
+    float *d_uright = nullptr, *d_depth = nullptr;
+    int32_t *d_snvalid = nullptr;
+    void *d_sscr = nullptr;
+    int stereo_cap = 0, last_nstereo = 0;
     // single-pair / host-data scratch
     void *d_scr = nullptr;
     size_t scr_bytes = 0;
@@ -304,7 +317,8 @@ static void free_plan(orbg_ctx *c)
                     c->d_cell_cnt, c->d_cell_kp, c->d_keys, c->d_knode, c->d_act, c->d_qk,
                     c->d_nodes, c->d_lvl_kp, c->d_lvl_cnt, c->kps_slot[0], c->kps_slot[1],
                     c->desc_slot[0], c->desc_slot[1], c->counts_slot[0], c->counts_slot[1],
-                    c->d_err, c->d_knn, c->d_m12, c->d_nm, c->d_topk, c->d_topk_n, c->d_pairs};
+                    c->d_err, c->d_knn, c->d_m12, c->d_nm, c->d_topk, c->d_topk_n, c->d_pairs,
+                    c->d_spairs, c->d_uright, c->d_depth, c->d_snvalid, c->d_sscr};
     for (void *q : ptrs)
         if (q) hipFree(q);
     c->d_geom = nullptr;
@@ -334,6 +348,11 @@ static void free_plan(orbg_ctx *c)
     c->d_topk_n = nullptr;
     c->d_pairs = nullptr;
     c->pair_cap = 0;
+    c->d_spairs = nullptr;
+    c->d_uright = c->d_depth = nullptr;
+    c->d_snvalid = nullptr;
+    c->d_sscr = nullptr;
+    c->stereo_cap = c->last_nstereo = 0;
     c->h_pairs.clear();
     c->gw = c->gh = c->gbatch = 0;
 }
@@ -1125,6 +1144,83 @@ extern "C" int orbg_match_batch_device(orbg_ctx *c, const int32_t *f1, const int
     HIPCHK(hipEventRecord(c->ev_mat[s], c->mstream));
     c->mat_pending[s] = true;
     c->last_npairs = npairs;
+    return ORBG_OK;
+}
+
+extern "C" int orbg_stereo_batch_device(orbg_ctx *c, const int32_t *left, const int32_t *right,
+                                        int npairs, float bf, float min_z)
+{
+    if (!c || !c->gw || c->last_n <= 0) return set_err(ORBG_EINVAL, "no batch extracted");
+    if (npairs <= 0 || !left || !right) return set_err(ORBG_EINVAL, "no pairs");
+    if (!(bf > 0)) return set_err(ORBG_EINVAL, "bf must be > 0");
+    for (int i = 0; i < npairs; i++)
+        if (left[i] < 0 || left[i] >= c->last_n || right[i] < 0 || right[i] >= c->last_n)
+            return set_err(ORBG_EINVAL, "stereo pair %d references a frame outside the batch", i);
+    HIPCHK(hipSetDevice(c->device));
+    const size_t fc = (size_t)c->geom.frame_cap;
+    if (c->stereo_cap < npairs) {
+        int rs = sync_all(c);
+        if (rs) return rs;
+        hipFree(c->d_spairs);
+        hipFree(c->d_uright);
+        hipFree(c->d_depth);
+        hipFree(c->d_snvalid);
+        hipFree(c->d_sscr);
+        c->d_spairs = nullptr;
+        c->d_uright = c->d_depth = nullptr;
+        c->d_snvalid = nullptr;
+        c->d_sscr = nullptr;
+        c->stereo_cap = 0;
+        const size_t P = (size_t)npairs;
+        int rc;
+        if ((rc = dalloc(&c->d_spairs, 2 * P)) || (rc = dalloc(&c->d_uright, P * fc)) ||
+            (rc = dalloc(&c->d_depth, P * fc)) || (rc = dalloc(&c->d_snvalid, P)) ||
+            (rc = dalloc((uint8_t **)&c->d_sscr, stereo_scratch_bytes(npairs, (int)fc))))
+            return rc;
+        c->stereo_cap = npairs;
+    }
+    // the kernels run on the extraction stream (they read this batch's pyramid, which the
+    // next extraction overwrites); the pair lists are uploaded in order on it
+    HIPCHK(hipMemcpyAsync(c->d_spairs, left, npairs * sizeof(int32_t), hipMemcpyHostToDevice,
+                          c->stream));
+    HIPCHK(hipMemcpyAsync(c->d_spairs + c->stereo_cap, right, npairs * sizeof(int32_t),
+                          hipMemcpyHostToDevice, c->stream));
+    HIPCHK(hipStreamSynchronize(c->stream));  // host lists are the caller's
+    int rc = launch_stereo(c->stream, c->geom, c->d_kps, c->d_desc, c->d_counts, c->d_spairs,
+                           c->d_spairs + c->stereo_cap, npairs, c->last_img, c->last_fs,
+                           c->last_pitch, c->d_pyr, bf, min_z, c->d_sscr, c->d_uright,
+                           c->d_depth, c->d_snvalid, &c->prof);
+    if (rc) return set_err(rc, "stereo launch failed (level-0 height > 4096?)");
+    c->last_nstereo = npairs;
+    return ORBG_OK;
+}
+
+extern "C" int orbg_stereo_outputs(orbg_ctx *c, float **d_uright, float **d_depth,
+                                   int32_t **d_nvalid, int32_t *frame_cap)
+{
+    if (!c || !c->last_nstereo) return set_err(ORBG_EINVAL, "no stereo batch yet");
+    if (d_uright) *d_uright = c->d_uright;
+    if (d_depth) *d_depth = c->d_depth;
+    if (d_nvalid) *d_nvalid = c->d_snvalid;
+    if (frame_cap) *frame_cap = c->geom.frame_cap;
+    return ORBG_OK;
+}
+
+extern "C" int orbg_download_stereo(orbg_ctx *c, int pair, float *uright, float *depth, int cap,
+                                    int32_t *nvalid)
+{
+    if (!c || pair < 0 || pair >= c->last_nstereo) return set_err(ORBG_EINVAL, "bad pair");
+    int rc = sync_all(c);
+    if (rc) return rc;
+    const size_t fc = (size_t)c->geom.frame_cap;
+    if (uright)
+        HIPCHK(hipMemcpy(uright, c->d_uright + pair * fc, (size_t)cap * sizeof(float),
+                         hipMemcpyDeviceToHost));
+    if (depth)
+        HIPCHK(hipMemcpy(depth, c->d_depth + pair * fc, (size_t)cap * sizeof(float),
+                         hipMemcpyDeviceToHost));
+    if (nvalid)
+        HIPCHK(hipMemcpy(nvalid, c->d_snvalid + pair, sizeof(int32_t), hipMemcpyDeviceToHost));
     return ORBG_OK;
 }
 

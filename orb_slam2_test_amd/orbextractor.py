@@ -164,5 +164,24 @@ class ORBextractor:
                                               L.ptr(nm)), "orbg_download_matches")
         return knn[:n], m12[:n], int(nm[0])
 
+    # --- Frame::ComputeStereoMatches on frame pairs of the last batch (Frame.cc:619-834) ---
+    def stereo_batch_device(self, left, right, bf, min_z):
+        """Enqueue ComputeStereoMatches for (left[i], right[i]) frames of the last batch.
+        min_z is Frame::mb (the reference reads it uninitialised; pass bf / fx)."""
+        a = np.ascontiguousarray(left, np.int32)
+        b = np.ascontiguousarray(right, np.int32)
+        L.check(L.lib().orbg_stereo_batch_device(self.ctx.handle, L.ptr(a), L.ptr(b), len(a),
+                                                 float(bf), float(min_z)),
+                "orbg_stereo_batch_device")
+
+    def download_stereo(self, pair, n):
+        """(mvuRight[n], mvDepth[n], number of depths) of stereo pair `pair`."""
+        ur = np.zeros(max(n, 1), np.float32)
+        dp = np.zeros(max(n, 1), np.float32)
+        nv = np.zeros(1, np.int32)
+        L.check(L.lib().orbg_download_stereo(self.ctx.handle, pair, L.ptr(ur), L.ptr(dp), n,
+                                             L.ptr(nv)), "orbg_download_stereo")
+        return ur[:n], dp[:n], int(nv[0])
+
     def close(self):
         self.ctx.close()

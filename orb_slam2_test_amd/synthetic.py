@@ -78,6 +78,38 @@ def sequence(n, h, w, seed=DEFAULT_SEED, max_step=8, noise=2):
     return out
 
 
+def stereo_pair(h, w, seed=DEFAULT_SEED, noise=2, d_min=4.0, d_max=60.0, n_objects=6):
+    """A rectified synthetic stereo pair (left, right) u8 and the true disparity map.
+
+    Disparity d(x, y) is a road-like plane growing from d_min at the top row to ~d_max/2 at
+    the bottom, with n_objects nearer fronto-parallel boxes up to d_max.  The right image
+    samples the left canvas at x + d (linear interpolation): a left pixel at column x sees
+    the same scene point at x - d in the right image, as for KITTI's rectified cameras.
+    Occlusions are ignored.  Noise is +-noise independently per image."""
+    rng = np.random.Generator(np.random.PCG64(seed + 31))
+    pad = int(np.ceil(d_max)) + 2
+    base = canvas(h, w + pad, seed)
+    ys = np.arange(h, dtype=np.float32)[:, None]
+    disp = np.broadcast_to(d_min + (d_max / 2 - d_min) * ys / max(h - 1, 1), (h, w)).copy()
+    for _ in range(n_objects):
+        oh, ow = rng.integers(h // 8, h // 3), rng.integers(w // 16, w // 5)
+        oy, ox = rng.integers(0, h - oh), rng.integers(0, w - ow)
+        disp[oy:oy + oh, ox:ox + ow] = rng.uniform(d_max / 3, d_max)
+    left = base[:, :w]
+    xs = np.arange(w, dtype=np.float32)[None, :]
+    # right(x) = scene point whose left column is x + d: sample the left canvas at x + d
+    src = np.clip(xs + disp, 0, w + pad - 2)
+    x0 = np.floor(src).astype(np.int64)
+    fx = src - x0
+    rows = np.arange(h)[:, None]
+    right = base[rows, x0] * (1 - fx) + base[rows, x0 + 1] * fx
+    jl = rng.integers(-noise, noise + 1, size=(h, w)).astype(np.float32)
+    jr = rng.integers(-noise, noise + 1, size=(h, w)).astype(np.float32)
+    L = np.clip(np.rint(left + jl), 0, 255).astype(np.uint8)
+    R = np.clip(np.rint(right + jr), 0, 255).astype(np.uint8)
+    return L, R, disp
+
+
 def constant(h, w, value=128):
     return np.full((h, w), value, np.uint8)
 

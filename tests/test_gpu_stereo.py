@@ -1,0 +1,64 @@
+"""GPU: Frame::ComputeStereoMatches (HIP, through the C ABI) vs the CPU oracle.
+
+mvuRight and mvDepth are compared bit for bit: the SAD is integer-exact and the parabola,
+sub-pixel and depth arithmetic is the reference's float sequence, without FMA contraction.
+Pairs are synthetic rectified stereo images (synthetic.stereo_pair), several per batch.
+"""
+import numpy as np
+import pytest
+
+from orb_slam2_test_amd import ORBextractor, synthetic as S
+
+pytestmark = pytest.mark.gpu
+
+BF, FX = S.KITTI_BF, S.KITTI_FX
+
+
+def run_pairs(oracle, pairs, nfeat=2000, min_z=BF / FX, bf=BF):
+    h, w = pairs[0][0].shape
+    frames = np.stack([im for pr in pairs for im in pr[:2]])
+    ext = ORBextractor(nfeat, 1.2, 8, 20, 7, max_batch=len(frames))
+    import torch
+    d = torch.from_numpy(frames).cuda()
+    ext.extract_batch_device(d.data_ptr(), len(frames), w, h)
+    n = len(pairs)
+    ext.stereo_batch_device(np.arange(n) * 2, np.arange(n) * 2 + 1, bf, min_z)
+    p = oracle.params(nfeatures=nfeat)
+    out = []
+    for i, pr in enumerate(pairs):
+        kl, dl = ext.download_frame(2 * i)
+        ur, dp, nv = ext.download_stereo(i, len(kl))
+        rl = oracle.extract(p, pr[0], with_pyramid=True)
+        rr = oracle.extract(p, pr[1], with_pyramid=True)
+        assert np.array_equal(kl, rl["kps"])
+        rur, rdp = oracle.stereo_matches(p, rl, rr, w, h, bf, min_z)
+        assert np.array_equal(ur, rur), "mvuRight pair %d" % i
+        assert np.array_equal(dp, rdp), "mvDepth pair %d" % i
+        assert nv == int((rdp > 0).sum())
+        out.append((kl, ur, dp))
+    return out
+
+
+def test_kitti_stereo_pairs(oracle):
+    pairs = [S.stereo_pair(376, 1241, seed=100 + i) for i in range(3)]
+    res = run_pairs(oracle, pairs)
+    for (kl, ur, dp), (_, _, disp) in zip(res, pairs):
+        ok = dp > 0
+        assert ok.sum() > 300
+        # and they are right: disparity close to the generator's truth for most matches
+        y = np.clip(np.rint(kl["y"][ok]).astype(int), 0, disp.shape[0] - 1)
+        x = np.clip(np.rint(kl["x"][ok]).astype(int), 0, disp.shape[1] - 1)
+        err = np.abs((kl["x"][ok] - ur[ok]) - disp[y, x])
+        assert np.median(err) < 1.0
+
+
+def test_no_disparity_limit_and_other_size(oracle):
+    # min_z <= 0: maxD = +inf; EuRoC-sized 752x480 with 1200 features
+    run_pairs(oracle, [S.stereo_pair(480, 752, seed=7, d_max=40.0)], nfeat=1200, min_z=0.0)
+
+
+def test_degenerate_pairs(oracle):
+    L, R, _ = S.stereo_pair(376, 1241, seed=9)
+    # identical images: disparity 0 everywhere (the reference's 0 -> 0.01 branch)
+    # and a featureless right image: no candidates, empty median step
+    run_pairs(oracle, [(L, L.copy()), (L, S.constant(376, 1241, 90))])
