@@ -28,11 +28,14 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 METRIC = "frames/sec ORB extract+match, 1241×376 2000feat 8lvl, 1/2/4/8 GPU"
+METRIC_STEREO = ("stereo frames/sec ORB extract L+R + ComputeStereoMatches, 1241×376 "
+                 "2000feat/eye 8lvl")
 W, H, NFEAT, NLEV = 1241, 376, 2000, 8
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
 # SURVEY.md 8d algorithmic bytes per unit
 PYR_BYTES = 1444097          # all 8 levels at 1241x376
 FRAME_ALGO_BYTES = 2701578   # extract 2,533,578 + match 168,000
+STEREO_FRAME_ALGO_BYTES = 5235156  # 2 x extract + match
 
 
 def kernel_algo_bytes(name, B, npairs, ncand, nkp, launches_per_step):
@@ -57,6 +60,9 @@ def kernel_algo_bytes(name, B, npairs, ncand, nkp, launches_per_step):
     elif name == "init_resolve":
         kp = nkp / max(B, 1)
         tot = npairs * (kp * 64 + kp * 4)
+    elif name == "stereo":
+        kp = nkp / max(B, 1)
+        tot = npairs * (2 * kp * (32 + 28) + kp * 8)  # both frames' kps + desc, uR + depth
     else:
         return None
     return tot / max(launches_per_step, 1)
@@ -69,6 +75,27 @@ def level_sizes():
         sizes.append((int(np.rint(np.float32(W) * inv)), int(np.rint(np.float32(H) * inv))))
         s = np.float32(np.float64(s) * np.float64(np.float32(1.2)))
     return sizes
+
+
+def cpu_baseline_stereo(lefts, rights, seconds=10.0):
+    """oracle/ (C restatement, one thread): extract L + R + ComputeStereoMatches per stereo
+    frame, as many frames as fit in `seconds`."""
+    from oracle import pyoracle as O
+    from orb_slam2_test_amd import synthetic as S
+    p = O.params(nfeatures=NFEAT, nlevels=NLEV)
+    t0 = time.perf_counter()
+    n = 0
+    while time.perf_counter() - t0 < seconds:
+        i = n % len(lefts)
+        lft = O.extract(p, lefts[i], with_pyramid=True)
+        rgt = O.extract(p, rights[i], with_pyramid=True)
+        O.stereo_matches(p, lft, rgt, W, H, S.KITTI_BF, S.KITTI_BF / S.KITTI_FX)
+        n += 1
+    dt = time.perf_counter() - t0
+    return {"value": round(n / dt, 3), "unit": "stereo frames/s", "cores": 1, "kind": "port",
+            "sample": ("%d synthetic 1241x376 stereo frames (extract L+R 2000 feat/8 lvl + "
+                       "ComputeStereoMatches), oracle/ C restatement -O3, 1 thread, %.1f s wall"
+                       % (n, dt))}
 
 
 def cpu_baseline(frames, threads, nframes):
@@ -96,6 +123,8 @@ def main():
     ap.add_argument("--cpu-frames", type=int, default=0, help="0: 256 x threads (~10-20 s)")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-kernel-timing", action="store_true")
+    ap.add_argument("--stereo", action="store_true",
+                    help="configs[3]: stereo frames (extract L+R + ComputeStereoMatches)")
     args = ap.parse_args()
 
     import torch
@@ -110,10 +139,16 @@ def main():
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
 
     B = args.batch
-    frames = synthetic.sequence(B, H, W, seed=synthetic.DEFAULT_SEED + 1000 * rank)
+    if args.stereo:
+        lefts, rights, _ = synthetic.stereo_sequence(B, H, W, seed=synthetic.DEFAULT_SEED + 1000 * rank)
+        frames = np.empty((2 * B, H, W), np.uint8)
+        frames[0::2], frames[1::2] = lefts, rights
+    else:
+        frames = synthetic.sequence(B, H, W, seed=synthetic.DEFAULT_SEED + 1000 * rank)
+    nimg = len(frames)
     d_frames = torch.from_numpy(frames).to("cuda")
     torch.cuda.synchronize()
-    ext = ORBextractor(NFEAT, 1.2, NLEV, 20, 7, device=local, max_batch=B)
+    ext = ORBextractor(NFEAT, 1.2, NLEV, 20, 7, device=local, max_batch=nimg)
     # one non-null torch stream for everything: liborbg's kernels, the summary and RCCL
     # (the null stream's handle is 0, which orbg_set_stream reads as "own stream")
     stream = torch.cuda.Stream()
@@ -127,7 +162,18 @@ def main():
     mstream = torch.cuda.ExternalStream(ext.ctx.match_stream())
     torch.cuda.synchronize()
 
+    sl, sr = np.arange(B) * 2, np.arange(B) * 2 + 1
+    ssum = torch.zeros(2 * B, dtype=torch.int32, device="cuda")
+
     def step():
+        if args.stereo:
+            ext.extract_batch_device(d_frames.data_ptr(), nimg, W, H)
+            ext.stereo_batch_device(sl, sr, synthetic.KITTI_BF,
+                                    synthetic.KITTI_BF / synthetic.KITTI_FX)
+            ext.ctx.stereo_summary(ssum.data_ptr())
+            if world > 1:  # per-frame (keypoints, depths) of every rank (RCCL all_gather)
+                sequence.gather_summary(ssum.view(2, B), world, sizes=[B] * world)
+            return
         ext.extract_batch_device(d_frames.data_ptr(), B, W, H)
         ext.match_batch_device(f1, f2, 100, 0.9, True)
         ext.ctx.batch_summary(summary.data_ptr())
@@ -168,7 +214,7 @@ def main():
         for name, (ms, n) in kern.items():
             lps = n / max(args.steps, 1)
             avg = ms / max(n, 1)
-            ab = kernel_algo_bytes(name, B, B, ncand, nkp, lps)
+            ab = kernel_algo_bytes(name, nimg, B, ncand, nkp, lps)
             kstats[name] = {"ms_per_step": round(ms / args.steps, 4), "launches_per_step": lps,
                             "avg_launch_ms": round(avg, 5),
                             "algo_bytes_per_launch": None if ab is None else int(ab),
@@ -188,26 +234,37 @@ def main():
                     "traffic": traffic,
                     "algo_bytes_per_launch": ks["algo_bytes_per_launch"],
                     "avg_launch_ms": ks["avg_launch_ms"]}
+        fab = STEREO_FRAME_ALGO_BYTES if args.stereo else FRAME_ALGO_BYTES
+        if args.stereo:
+            workload = ("configs[3] KITTI00-shaped stereo 1241x376 L+R, 2000 feat/eye, 8 lvl: "
+                        "ORBextractor x2 + Frame::ComputeStereoMatches (bf=386.1448, "
+                        "mb=bf/fx)")
+        else:
+            workload = ("C3 KITTI03-shaped mono 1241x376, 2000 feat, 8 lvl: ORBextractor + "
+                        "Hamming knn2 (t vs t-1) + SearchForInitialization(w=100, 0.9, checkOri)")
         out = {
-            "metric": METRIC, "value": round(value, 2), "unit": "frames/s", "n_gpus": world,
+            "metric": METRIC_STEREO if args.stereo else METRIC, "value": round(value, 2),
+            "unit": "stereo frames/s" if args.stereo else "frames/s", "n_gpus": world,
             "steps": args.steps, "warmup": args.warmup,
             "ms_per_step": round(elapsed / args.steps * 1e3, 4), "higher_is_better": True,
             "scaling": "weak", "vs_baseline": None, "dtype": "u8", "data": "synthetic",
             "config": {
-                "workload": "C3 KITTI03-shaped mono 1241x376, 2000 feat, 8 lvl: ORBextractor + "
-                            "Hamming knn2 (t vs t-1) + SearchForInitialization(w=100, 0.9, checkOri)",
+                "workload": workload,
                 "frames_per_gpu_per_step": B, "global_batch": B * world, "width": W,
                 "height": H, "nfeatures": NFEAT, "nlevels": NLEV,
                 "parallelism": "frames sharded over %d GPU(s), RCCL all_gather of per-frame "
                                "summary" % world},
             "roofline": roof,
-            "pipeline_roofline": {"algo_bytes_per_frame": FRAME_ALGO_BYTES,
-                                  "achieved_GBps": round(value * FRAME_ALGO_BYTES / 1e9, 1),
-                                  "frac": round(value * FRAME_ALGO_BYTES / 1e9 / HBM_PEAK_GBS, 4)},
+            "pipeline_roofline": {"algo_bytes_per_frame": fab,
+                                  "achieved_GBps": round(value * fab / 1e9, 1),
+                                  "frac": round(value * fab / 1e9 / HBM_PEAK_GBS, 4)},
             "kernels": kstats,
-            "candidates_per_frame": round(ncand / B, 1), "keypoints_per_frame": round(nkp / B, 1),
+            "candidates_per_image": round(ncand / nimg, 1),
+            "keypoints_per_image": round(nkp / nimg, 1),
         }
-        if world == 1 and not args.no_cpu:
+        if world == 1 and not args.no_cpu and args.stereo:
+            out["cpu_baseline"] = cpu_baseline_stereo(lefts, rights)
+        elif world == 1 and not args.no_cpu:
             n = args.cpu_frames or 256 * args.cpu_threads
             out["cpu_baseline"] = cpu_baseline(frames, args.cpu_threads, n)
         else:

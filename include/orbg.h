@@ -156,6 +156,9 @@ int orbg_stereo_batch_device(orbg_ctx *ctx, const int32_t *left, const int32_t *
 int orbg_stereo_outputs(orbg_ctx *ctx, float **d_uright /* [npairs][frame_cap] */,
                         float **d_depth /* [npairs][frame_cap] */,
                         int32_t **d_nvalid /* [npairs] */, int32_t *frame_cap);
+/* per-pair summary on the context stream into a device buffer: d_out[p] = keypoints of the
+ * left frame of pair p, d_out[npairs + p] = keypoints with a depth */
+int orbg_stereo_summary(orbg_ctx *ctx, int32_t *d_out);
 /* copies cap entries of pair `pair` (synchronises) */
 int orbg_download_stereo(orbg_ctx *ctx, int pair, float *uright, float *depth, int cap,
                          int32_t *nvalid);

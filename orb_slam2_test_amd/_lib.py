@@ -96,6 +96,7 @@ def lib():
         "orbg_batch_summary": (i32, [vp, vp]),
         "orbg_stereo_batch_device": (i32, [vp, vp, vp, i32, f32, f32]),
         "orbg_stereo_outputs": (i32, [vp, vp, vp, vp, vp]),
+        "orbg_stereo_summary": (i32, [vp, vp]),
         "orbg_download_stereo": (i32, [vp, i32, vp, vp, i32, vp]),
         "orbg_match_stream": (vp, [vp]),
         "orbg_batch_stats": (i32, [vp, P(C.c_int64), P(C.c_int64)]),
@@ -200,6 +201,10 @@ class Context:
         a, b = C.c_int64(), C.c_int64()
         check(self._L.orbg_batch_stats(self.handle, C.byref(a), C.byref(b)), "orbg_batch_stats")
         return a.value, b.value
+
+    def stereo_summary(self, d_out_ptr):
+        check(self._L.orbg_stereo_summary(self.handle, C.c_void_p(d_out_ptr)),
+              "orbg_stereo_summary")
 
     def match_stream(self):
         """hipStream_t (int) of batch matching and the summary."""

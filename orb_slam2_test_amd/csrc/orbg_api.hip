@@ -239,6 +239,7 @@ struct orbg_ctx {
     int last_npairs = 0;
     // stereo (ComputeStereoMatches) of the last batch
     int32_t *d_spairs = nullptr;
+    std::vector<int32_t> h_spairs;  // last uploaded (left, right) lists
     float *d_uright = nullptr, *d_depth = nullptr;
     int32_t *d_snvalid = nullptr;
     void *d_sscr = nullptr;
@@ -349,6 +350,7 @@ static void free_plan(orbg_ctx *c)
     c->d_pairs = nullptr;
     c->pair_cap = 0;
     c->d_spairs = nullptr;
+    c->h_spairs.clear();
     c->d_uright = c->d_depth = nullptr;
     c->d_snvalid = nullptr;
     c->d_sscr = nullptr;
@@ -1166,6 +1168,7 @@ extern "C" int orbg_stereo_batch_device(orbg_ctx *c, const int32_t *left, const 
         hipFree(c->d_depth);
         hipFree(c->d_snvalid);
         hipFree(c->d_sscr);
+        c->h_spairs.clear();
         c->d_spairs = nullptr;
         c->d_uright = c->d_depth = nullptr;
         c->d_snvalid = nullptr;
@@ -1180,18 +1183,43 @@ extern "C" int orbg_stereo_batch_device(orbg_ctx *c, const int32_t *left, const 
         c->stereo_cap = npairs;
     }
     // the kernels run on the extraction stream (they read this batch's pyramid, which the
-    // next extraction overwrites); the pair lists are uploaded in order on it
-    HIPCHK(hipMemcpyAsync(c->d_spairs, left, npairs * sizeof(int32_t), hipMemcpyHostToDevice,
-                          c->stream));
-    HIPCHK(hipMemcpyAsync(c->d_spairs + c->stereo_cap, right, npairs * sizeof(int32_t),
-                          hipMemcpyHostToDevice, c->stream));
-    HIPCHK(hipStreamSynchronize(c->stream));  // host lists are the caller's
+    // next extraction overwrites); the pair lists are uploaded only when they change
+    std::vector<int32_t> hp(left, left + npairs);
+    hp.insert(hp.end(), right, right + npairs);
+    if (hp != c->h_spairs) {
+        HIPCHK(hipStreamSynchronize(c->stream));  // a previous stereo pass may read them
+        HIPCHK(hipMemcpy(c->d_spairs, left, npairs * sizeof(int32_t), hipMemcpyHostToDevice));
+        HIPCHK(hipMemcpy(c->d_spairs + c->stereo_cap, right, npairs * sizeof(int32_t),
+                         hipMemcpyHostToDevice));
+        c->h_spairs.swap(hp);
+    }
     int rc = launch_stereo(c->stream, c->geom, c->d_kps, c->d_desc, c->d_counts, c->d_spairs,
                            c->d_spairs + c->stereo_cap, npairs, c->last_img, c->last_fs,
                            c->last_pitch, c->d_pyr, bf, min_z, c->d_sscr, c->d_uright,
                            c->d_depth, c->d_snvalid, &c->prof);
     if (rc) return set_err(rc, "stereo launch failed (level-0 height > 4096?)");
     c->last_nstereo = npairs;
+    return ORBG_OK;
+}
+
+__global__ void k_stereo_summary(const int32_t *__restrict__ counts,
+                                 const int32_t *__restrict__ left,
+                                 const int32_t *__restrict__ nvalid, int npairs,
+                                 int32_t *__restrict__ out)
+{
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < npairs) {
+        out[i] = counts[left[i]];
+        out[npairs + i] = nvalid[i];
+    }
+}
+
+extern "C" int orbg_stereo_summary(orbg_ctx *c, int32_t *d_out)
+{
+    if (!c || !c->last_nstereo || !d_out) return set_err(ORBG_EINVAL, "no stereo batch yet");
+    hipLaunchKernelGGL(k_stereo_summary, dim3((c->last_nstereo + 255) / 256), dim3(256), 0,
+                       c->stream, c->d_counts, c->d_spairs, c->d_snvalid, c->last_nstereo, d_out);
+    HIPCHK(hipGetLastError());
     return ORBG_OK;
 }
 

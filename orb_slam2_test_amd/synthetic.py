@@ -110,6 +110,27 @@ def stereo_pair(h, w, seed=DEFAULT_SEED, noise=2, d_min=4.0, d_max=60.0, n_objec
     return L, R, disp
 
 
+def stereo_sequence(n, h, w, seed=DEFAULT_SEED, noise=2, d_min=4.0, d_max=60.0):
+    """n rectified stereo frames: left = sequence(n, h, w, seed), right[t](x) = left[t](x + d)
+    (linear interpolation, clamped at the right edge) with one disparity map d(x, y) of the
+    stereo_pair kind, plus +-noise.  Returns (lefts, rights, disparity)."""
+    lefts = sequence(n, h, w, seed=seed)
+    _, _, disp = stereo_pair(h, w, seed=seed, noise=0, d_min=d_min, d_max=d_max)
+    rng = np.random.Generator(np.random.PCG64(seed + 57))
+    xs = np.arange(w, dtype=np.float32)[None, :]
+    src = np.clip(xs + disp, 0, w - 1.001)
+    x0 = np.floor(src).astype(np.int64)
+    fx = (src - x0).astype(np.float32)
+    rows = np.arange(h)[:, None]
+    rights = np.empty_like(lefts)
+    for t in range(n):
+        a = lefts[t].astype(np.float32)
+        r = a[rows, x0] * (1 - fx) + a[rows, x0 + 1] * fx
+        r += rng.integers(-noise, noise + 1, size=(h, w)).astype(np.float32)
+        rights[t] = np.clip(np.rint(r), 0, 255).astype(np.uint8)
+    return lefts, rights, disp
+
+
 def constant(h, w, value=128):
     return np.full((h, w), value, np.uint8)
 
