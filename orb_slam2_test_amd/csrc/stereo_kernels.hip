@@ -5,7 +5,7 @@
 //                              floor(y - r) .. ceil(y + r), r = 2 * scale[octave]; one
 //                              workgroup per pair, counts / scan / fill in LDS, the lists go
 //                              to global scratch (order inside a row is free: see below)
-//   k_stereo_match   :676-738  thread per left keypoint: candidates of row (int)vL, octave
+//   k_stereo_match   :676-738  wave per left keypoint: candidates of row (int)vL, octave
 //                              within +-1, uL - maxD <= uR <= uL; best = minimum of
 //                              (Hamming distance, iR) below TH_HIGH -- the reference walks
 //                              each row in increasing iR with a strict <, so its winner is
@@ -113,6 +113,54 @@ __global__ __launch_bounds__(ST_ROWS_T) void k_stereo_rows(StereoGeom G,
 }
 
 // ---- descriptor match ---------------------------------------------------------------
+// one wave per left keypoint at a time, lanes over the row's candidates (all loads in
+// flight), then a wave minimum of (dist << 16 | iR) -- the lexicographic (distance, index)
+// minimum.  ST_WAVES waves per pair walk the left keypoints.
+#define ST_WAVES 512
+
+__device__ __forceinline__ void stereo_match_one(const StereoGeom &G,
+                                                 const orbg_keypoint *__restrict__ kps,
+                                                 const uint8_t *__restrict__ desc, int fl,
+                                                 int fr, int iL, int lane, int p,
+                                                 const int32_t *__restrict__ row_off,
+                                                 const int16_t *__restrict__ row_list,
+                                                 int32_t *__restrict__ out)
+{
+    const orbg_keypoint kl = kps[(size_t)fl * G.fc + iL];
+    const int row = (int)kl.y;
+    const float minU = kl.x - G.max_d, maxU = kl.x - 0.0f;
+    int c0 = 0, c1 = 0;
+    if (row >= 0 && row < G.h && !(maxU < 0)) {
+        const int32_t *off = row_off + (size_t)p * (ST_MAX_ROWS + 1);
+        c0 = off[row];
+        c1 = min(off[row + 1], G.list_cap);
+    }
+    const uint4 *q = (const uint4 *)(desc + ((size_t)fl * G.fc + iL) * 32);
+    const orbg_keypoint *kr = kps + (size_t)fr * G.fc;
+    const uint8_t *dr = desc + (size_t)fr * G.fc * 32;
+    const int16_t *list = row_list + (size_t)p * G.list_cap;
+    uint32_t best = 0xFFFFFFFFu;
+    for (int c = c0 + lane; c < c1; c += 64) {
+        const int iR = list[c];
+        const orbg_keypoint k = kr[iR];
+        if (k.octave < kl.octave - 1 || k.octave > kl.octave + 1) continue;
+        if (!(k.x >= minU && k.x <= maxU)) continue;
+        const uint4 *d = (const uint4 *)(dr + (size_t)iR * 32);
+        const uint4 d0 = d[0], d1 = d[1], q0 = q[0], q1 = q[1];
+        const uint32_t dist = __popc(q0.x ^ d0.x) + __popc(q0.y ^ d0.y) + __popc(q0.z ^ d0.z) +
+                              __popc(q0.w ^ d0.w) + __popc(q1.x ^ d1.x) + __popc(q1.y ^ d1.y) +
+                              __popc(q1.z ^ d1.z) + __popc(q1.w ^ d1.w);
+        best = min(best, (dist << 16) | (uint32_t)iR);
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) best = min(best, (uint32_t)__shfl_xor((int)best, o, 64));
+    if (lane == 0) {
+        const int bestDist = best == 0xFFFFFFFFu ? ST_TH_HIGH : (int)(best >> 16);
+        // the reference keeps a candidate only below TH_HIGH, then needs < (TH_HIGH+TH_LOW)/2
+        out[iL] = (bestDist < ST_TH_HIGH && bestDist < ST_TH_ORB) ? (int)(best & 0xFFFF) : -1;
+    }
+}
+
 __global__ __launch_bounds__(256) void k_stereo_match(StereoGeom G,
                                                      const orbg_keypoint *__restrict__ kps,
                                                      const uint8_t *__restrict__ desc,
@@ -124,43 +172,12 @@ __global__ __launch_bounds__(256) void k_stereo_match(StereoGeom G,
                                                      int32_t *__restrict__ best_r)
 {
     const int p = blockIdx.y;
-    const int iL = blockIdx.x * 256 + threadIdx.x;
+    const int lane = threadIdx.x & 63;
     const int fl = left[p], fr = right[p];
     const int nl = counts[fl];
-    if (iL >= nl) return;
-    int32_t *out = best_r + (size_t)p * G.fc;
-    const orbg_keypoint kl = kps[(size_t)fl * G.fc + iL];
-    out[iL] = -1;
-    const int row = (int)kl.y;
-    if (row < 0 || row >= G.h) return;
-    const int32_t *off = row_off + (size_t)p * (ST_MAX_ROWS + 1);
-    const int c0 = off[row], c1 = min(off[row + 1], G.list_cap);
-    if (c0 >= c1) return;
-    const float minU = kl.x - G.max_d, maxU = kl.x - 0.0f;
-    if (maxU < 0) return;
-    const uint32_t *ql = (const uint32_t *)(desc + ((size_t)fl * G.fc + iL) * 32);
-    uint32_t qd[8];
-#pragma unroll
-    for (int i = 0; i < 8; i++) qd[i] = ql[i];
-    const orbg_keypoint *kr = kps + (size_t)fr * G.fc;
-    const uint8_t *dr = desc + (size_t)fr * G.fc * 32;
-    const int16_t *list = row_list + (size_t)p * G.list_cap;
-    int bestDist = ST_TH_HIGH, bestIdx = INT_MAX;
-    for (int c = c0; c < c1; c++) {
-        const int iR = list[c];
-        const orbg_keypoint k = kr[iR];
-        if (k.octave < kl.octave - 1 || k.octave > kl.octave + 1) continue;
-        if (!(k.x >= minU && k.x <= maxU)) continue;
-        const uint32_t *d = (const uint32_t *)(dr + (size_t)iR * 32);
-        int dist = 0;
-#pragma unroll
-        for (int i = 0; i < 8; i++) dist += __popc(qd[i] ^ d[i]);
-        if (dist < bestDist || (dist == bestDist && iR < bestIdx && dist < ST_TH_HIGH)) {
-            bestDist = dist;
-            bestIdx = iR;
-        }
-    }
-    if (bestDist < ST_TH_ORB) out[iL] = bestIdx;
+    for (int iL = blockIdx.x * 4 + (threadIdx.x >> 6); iL < nl; iL += ST_WAVES)
+        stereo_match_one(G, kps, desc, fl, fr, iL, lane, p, row_off, row_list,
+                         best_r + (size_t)p * G.fc);
 }
 
 // ---- SAD refinement -----------------------------------------------------------------
@@ -177,26 +194,17 @@ __device__ __forceinline__ const uint8_t *st_level(const StereoGeom &G, const ui
     return pyr + f * pyr_frame + G.pyr_off[l];
 }
 
-__global__ __launch_bounds__(256) void k_stereo_sad(StereoGeom G,
-                                                   const orbg_keypoint *__restrict__ kps,
-                                                   const int32_t *__restrict__ counts,
-                                                   const int32_t *__restrict__ left,
-                                                   const int32_t *__restrict__ right,
-                                                   const int32_t *__restrict__ best_r,
-                                                   const uint8_t *__restrict__ img0,
-                                                   int64_t img_fs, int img_pitch,
-                                                   const uint8_t *__restrict__ pyr,
-                                                   int64_t pyr_frame, float *__restrict__ uright,
-                                                   float *__restrict__ depth,
-                                                   int32_t *__restrict__ sad_out)
+__device__ __forceinline__ void stereo_sad_one(const StereoGeom &G,
+                                               const orbg_keypoint *__restrict__ kps,
+                                               const int32_t *__restrict__ best_r,
+                                               const uint8_t *__restrict__ img0, int64_t img_fs,
+                                               int img_pitch, const uint8_t *__restrict__ pyr,
+                                               int64_t pyr_frame, float *__restrict__ uright,
+                                               float *__restrict__ depth,
+                                               int32_t *__restrict__ sad_out, int p, int fl,
+                                               int fr, int iL, int lane, int *sadw,
+                                               uint32_t *stagew, int *shlw, int *shrw)
 {
-    __shared__ int sad[4][2 * ST_L + 1];
-    const int p = blockIdx.y;
-    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-    const int iL = blockIdx.x * 4 + wv;
-    const int fl = left[p], fr = right[p];
-    const int nl = counts[fl];
-    if (iL >= nl) return;  // wave-uniform
     float *ur = uright + (size_t)p * G.fc, *dp = depth + (size_t)p * G.fc;
     int32_t *so = sad_out + (size_t)p * G.fc;
     const int iR = best_r[(size_t)p * G.fc + iL];
@@ -220,34 +228,52 @@ __global__ __launch_bounds__(256) void k_stereo_sad(StereoGeom G,
     const uint8_t *IL = st_level(G, img0, img_fs, img_pitch, pyr, pyr_frame, fl, lev, &lp);
     const uint8_t *IR = st_level(G, img0, img_fs, img_pitch, pyr, pyr_frame, fr, lev, &rp);
     const int yl = (int)scaledvL, xl = (int)scaleduL, xr = (int)scaleduR0;
-    const int cl = IL[(int64_t)yl * lp + xl];
-    if (lane < 2 * ST_L + 1) sad[wv][lane] = 0;
+    // stage the 11x11 left patch (columns xl-5..xl+5) and the 11x21 right strip (xr-10..xr+10)
+    // as 4 / 7 aligned dwords per row (per-row alignment: the level-0 pitch may be odd)
+    uint32_t *stL = stagew, *stR = stagew + 11 * 4;
+    for (int t = lane; t < 11 * 11; t += 64) {
+        const int r = t / 11, c = t - r * 11;  // c < 4: left dword, else right dword c - 4
+        const int y = yl - ST_W + r;
+        const uint8_t *src = c < 4 ? IL + (int64_t)y * lp + xl - ST_W
+                                   : IR + (int64_t)y * rp + xr - 2 * ST_W;
+        const uintptr_t a = (uintptr_t)src & ~(uintptr_t)3;
+        const uint32_t v = ((const uint32_t *)a)[c < 4 ? c : c - 4];
+        if (c < 4)
+            stL[r * 4 + c] = v;
+        else
+            stR[r * 7 + c - 4] = v;
+        if (c == 0) shlw[r] = (int)((uintptr_t)src & 3);
+        if (c == 4) shrw[r] = (int)((uintptr_t)src & 3);
+    }
+    if (lane < 2 * ST_L + 1) sadw[lane] = 0;
     wave_sync_lds();
+    const uint8_t *bL = (const uint8_t *)stL, *bR = (const uint8_t *)stR;
+    const int cl = bL[ST_W * 16 + shlw[ST_W] + ST_W];
     // items t = (shift, row): 11 x 11, two per lane
     for (int t = lane; t < (2 * ST_L + 1) * (2 * ST_W + 1); t += 64) {
-        const int inc = t / (2 * ST_W + 1) - ST_L, dy = t % (2 * ST_W + 1) - ST_W;
-        const int cr = IR[(int64_t)yl * rp + xr + inc];
-        const uint8_t *a = IL + (int64_t)(yl + dy) * lp + xl - ST_W;
-        const uint8_t *b = IR + (int64_t)(yl + dy) * rp + xr + inc - ST_W;
+        const int inc = t / (2 * ST_W + 1) - ST_L, dy = t % (2 * ST_W + 1);
+        const int cr = bR[ST_W * 28 + shrw[ST_W] + 2 * ST_W + inc];
+        const uint8_t *a = bL + dy * 16 + shlw[dy];
+        const uint8_t *b = bR + dy * 28 + shrw[dy] + ST_L + inc;
         int s = 0;
 #pragma unroll
         for (int dx = 0; dx < 2 * ST_W + 1; dx++) s += abs((a[dx] - cl) - (b[dx] - cr));
-        atomicAdd(&sad[wv][inc + ST_L], s);
+        atomicAdd(&sadw[inc + ST_L], s);
     }
     wave_sync_lds();
     if (lane != 0) return;
     int best = INT_MAX, bestinc = 0;
     for (int inc = -ST_L; inc <= ST_L; inc++) {
-        const int s = sad[wv][inc + ST_L];
+        const int s = sadw[inc + ST_L];
         if (s < best) {
             best = s;
             bestinc = inc;
         }
     }
     if (bestinc == -ST_L || bestinc == ST_L) return;
-    const float dist1 = (float)sad[wv][ST_L + bestinc - 1];
-    const float dist2 = (float)sad[wv][ST_L + bestinc];
-    const float dist3 = (float)sad[wv][ST_L + bestinc + 1];
+    const float dist1 = (float)sadw[ST_L + bestinc - 1];
+    const float dist2 = (float)sadw[ST_L + bestinc];
+    const float dist3 = (float)sadw[ST_L + bestinc + 1];
     const float deltaR = (dist1 - dist3) / (2.0f * (dist1 + dist3 - 2.0f * dist2));
     if (deltaR < -1 || deltaR > 1) return;
     float bestuR = G.scale[lev] * ((float)scaleduR0 + (float)bestinc + deltaR);
@@ -260,6 +286,33 @@ __global__ __launch_bounds__(256) void k_stereo_sad(StereoGeom G,
         dp[iL] = G.bf / disparity;
         ur[iL] = bestuR;
         so[iL] = best;
+    }
+}
+
+__global__ __launch_bounds__(256) void k_stereo_sad(StereoGeom G,
+                                                   const orbg_keypoint *__restrict__ kps,
+                                                   const int32_t *__restrict__ counts,
+                                                   const int32_t *__restrict__ left,
+                                                   const int32_t *__restrict__ right,
+                                                   const int32_t *__restrict__ best_r,
+                                                   const uint8_t *__restrict__ img0,
+                                                   int64_t img_fs, int img_pitch,
+                                                   const uint8_t *__restrict__ pyr,
+                                                   int64_t pyr_frame, float *__restrict__ uright,
+                                                   float *__restrict__ depth,
+                                                   int32_t *__restrict__ sad_out)
+{
+    __shared__ int sad[4][2 * ST_L + 1];
+    __shared__ uint32_t stage[4][11 * 4 + 11 * 7];
+    __shared__ int shl[4][11], shr[4][11];
+    const int p = blockIdx.y;
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    const int fl = left[p], fr = right[p];
+    const int nl = counts[fl];
+    for (int iL = blockIdx.x * 4 + wv; iL < nl; iL += ST_WAVES) {
+        stereo_sad_one(G, kps, best_r, img0, img_fs, img_pitch, pyr, pyr_frame, uright, depth,
+                       sad_out, p, fl, fr, iL, lane, sad[wv], stage[wv], shl[wv], shr[wv]);
+        wave_sync_lds();  // the next keypoint reuses this wave's LDS
     }
 }
 
@@ -380,17 +433,23 @@ int launch_stereo(hipStream_t st, const OrbgGeom &g, const orbg_keypoint *kps,
     s += (size_t)npairs * G.fc * 4;
     int32_t *sad = (int32_t *)s;
     hipEvent_t a = nullptr;
-    prof_begin(prof, st, "stereo", &a);
+    prof_begin(prof, st, "stereo_rows", &a);
     hipLaunchKernelGGL(k_stereo_rows, dim3(npairs), dim3(ST_ROWS_T), 0, st, G, kps, counts,
                        d_right, row_off, row_list);
-    hipLaunchKernelGGL(k_stereo_match, dim3((G.fc + 255) / 256, npairs), dim3(256), 0, st, G, kps,
+    prof_end(prof, st, "stereo_rows", a);
+    prof_begin(prof, st, "stereo_match", &a);
+    hipLaunchKernelGGL(k_stereo_match, dim3(ST_WAVES / 4, npairs), dim3(256), 0, st, G, kps,
                        desc, counts, d_left, d_right, row_off, row_list, best_r);
-    hipLaunchKernelGGL(k_stereo_sad, dim3((G.fc + 3) / 4, npairs), dim3(256), 0, st, G, kps,
+    prof_end(prof, st, "stereo_match", a);
+    prof_begin(prof, st, "stereo_sad", &a);
+    hipLaunchKernelGGL(k_stereo_sad, dim3(ST_WAVES / 4, npairs), dim3(256), 0, st, G, kps,
                        counts, d_left, d_right, best_r, img0, img_fs, img_pitch, pyr,
                        g.pyr_frame, uright, depth, sad);
+    prof_end(prof, st, "stereo_sad", a);
+    prof_begin(prof, st, "stereo_median", &a);
     hipLaunchKernelGGL(k_stereo_median, dim3(npairs), dim3(256), 0, st, G, counts, d_left, sad,
                        uright, depth, nvalid);
-    prof_end(prof, st, "stereo", a);
+    prof_end(prof, st, "stereo_median", a);
     return hipGetLastError() == hipSuccess ? ORBG_OK : ORBG_EIO;
 }
 
