@@ -156,6 +156,14 @@ int orbg_stereo_batch_device(orbg_ctx *ctx, const int32_t *left, const int32_t *
 int orbg_stereo_outputs(orbg_ctx *ctx, float **d_uright /* [npairs][frame_cap] */,
                         float **d_depth /* [npairs][frame_cap] */,
                         int32_t **d_nvalid /* [npairs] */, int32_t *frame_cap);
+/* The stereo Frame constructor on host images (Frame.cc:86-161): ORBextractor on the left
+ * and right image (both CV_8UC1, same size and row pitch) + ComputeStereoMatches.  Outputs
+ * as orbg_extract for each image (ORBG_ERANGE with *n_l / *n_r set if a capacity is short);
+ * uright / depth receive *n_l entries (mvuRight, mvDepth). */
+int orbg_stereo_frame(orbg_ctx *ctx, const uint8_t *left, const uint8_t *right, int w, int h,
+                      size_t step, float bf, float min_z, orbg_keypoint *kps_l, uint8_t *desc_l,
+                      int cap_l, int *n_l, orbg_keypoint *kps_r, uint8_t *desc_r, int cap_r,
+                      int *n_r, float *uright, float *depth);
 /* per-pair summary on the context stream into a device buffer: d_out[p] = keypoints of the
  * left frame of pair p, d_out[npairs + p] = keypoints with a depth */
 int orbg_stereo_summary(orbg_ctx *ctx, int32_t *d_out);

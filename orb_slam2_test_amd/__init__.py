@@ -1,7 +1,8 @@
 """orb_slam2_test_amd: MI355X-native (gfx950) ORB-SLAM2 per-frame hot path.
 
 ORBextractor (pyramid, FAST-9 + quadtree distribution, IC_Angle, rBRIEF), ORBmatcher's
-Hamming matching (DescriptorDistance, brute-force 2-NN, SearchForInitialization) and
+Hamming matching (DescriptorDistance, brute-force 2-NN, SearchForInitialization),
+Frame::ComputeStereoMatches and
 the per-edge arithmetic of Optimizer::LocalBundleAdjustment, as hand-written HIP
 kernels behind the C ABI in include/orbg.h (lib/liborbg.so).  The Python classes mirror
 the reference's C++ interfaces; see DESIGN.md.
@@ -9,7 +10,8 @@ the reference's C++ interfaces; see DESIGN.md.
 from ._lib import KP_DTYPE, EDGE_DTYPE, EDGE_OUT_DTYPE, POSE_DTYPE, LIB_PATH  # noqa: F401
 from .orbextractor import ORBextractor  # noqa: F401
 from .orbmatcher import Frame, ORBmatcher  # noqa: F401
+from .frame import StereoFrame  # noqa: F401
 from .optimizer import linearize_local_ba  # noqa: F401
 
-__all__ = ["ORBextractor", "ORBmatcher", "Frame", "linearize_local_ba", "KP_DTYPE",
+__all__ = ["ORBextractor", "ORBmatcher", "Frame", "StereoFrame", "linearize_local_ba", "KP_DTYPE",
            "EDGE_DTYPE", "EDGE_OUT_DTYPE", "POSE_DTYPE"]

@@ -97,6 +97,8 @@ def lib():
         "orbg_stereo_batch_device": (i32, [vp, vp, vp, i32, f32, f32]),
         "orbg_stereo_outputs": (i32, [vp, vp, vp, vp, vp]),
         "orbg_stereo_summary": (i32, [vp, vp]),
+        "orbg_stereo_frame": (i32, [vp, vp, vp, i32, i32, C.c_size_t, f32, f32, vp, vp, i32, vp,
+                                    vp, vp, i32, vp, vp, vp]),
         "orbg_download_stereo": (i32, [vp, i32, vp, vp, i32, vp]),
         "orbg_match_stream": (vp, [vp]),
         "orbg_batch_stats": (i32, [vp, P(C.c_int64), P(C.c_int64)]),

@@ -6,7 +6,8 @@
 //       expects the Extractor constructor to throw (no HIP device: no CPU fallback)
 //   compat_selftest run <w> <h> <frame0.raw> <frame1.raw> <outdir> <nfeatures>
 //       writes kps0/kps1 (28-B cv::KeyPoint records), desc0/desc1 (N x 32),
-//       m12 (int32 per F1 keypoint), knn (int32 triples per F2 keypoint), nm.txt
+//       m12 (int32 per F1 keypoint), knn (int32 triples per F2 keypoint), nm.txt,
+//       stereo_ur / stereo_depth (StereoFrame of frame0 as left, frame1 as right)
 #include <cstdio>
 #include <cstdlib>
 #include <fstream>
@@ -88,6 +89,13 @@ int main(int argc, char **argv)
         knn[3 * i + 2] = sd[i];
     }
     if (n0 > 1 && orbg_compat::Matcher::DescriptorDistance(d0.data(), d0.data()) != 0) return 5;
+
+    // stereo Frame constructor on (frame0, frame1) as (left, right), KITTI00 bf / fx
+    const float bf = 386.1448f, fx = 718.856f;
+    orbg_compat::StereoFrame SF(ext, im0.data(), im1.data(), w, h, (size_t)w, bf, bf / fx);
+    if (SF.N != n0 || (int)SF.mvDepth.size() != n0) return 6;
+    write_file(out + "/stereo_ur", SF.mvuRight);
+    write_file(out + "/stereo_depth", SF.mvDepth);
 
     write_file(out + "/kps0", k0);
     write_file(out + "/kps1", k1);

@@ -14,6 +14,8 @@
 //         mvImagePyramid (downloaded on demand) ............ include/ORBextractor.h:101
 //         ORBmatcher(nnratio, checkOri), DescriptorDistance, SearchForInitialization
 //                                           include/ORBmatcher.h:47,51,128
+//         StereoFrame: the stereo Frame constructor (two extractions + ComputeStereoMatches)
+//                                           src/Frame.cc:86-161, 619-834
 //   ORB_SLAM2::ORBextractor (only when OpenCV headers are present)
 //       the reference's exact cv::InputArray / std::vector<cv::KeyPoint> / cv::OutputArray
 //       signatures, so Tracking.cc and Frame.cc compile unchanged.  This
@@ -203,6 +205,48 @@ private:
     float nnratio_;
     bool check_ori_;
     orbg_ctx *ctx_;
+};
+
+// The stereo Frame constructor (Frame.cc:86-161): both extractions + ComputeStereoMatches.
+// mb is Frame::mb, read uninitialised by the reference (Frame.cc:661 vs :148); pass bf / fx.
+struct StereoFrame {
+    std::vector<orbg_keypoint> mvKeys, mvKeysRight;
+    std::vector<uint8_t> mDescriptors, mDescriptorsRight;  // N x 32, Nr x 32
+    std::vector<float> mvuRight, mvDepth;                  // -1 where unmatched
+    int N = 0;
+    float mbf = 0.f, mb = 0.f;
+
+    StereoFrame(Extractor &ext, const uint8_t *imLeft, const uint8_t *imRight, int w, int h,
+                size_t step, float bf, float mb_)
+        : mbf(bf), mb(mb_)
+    {
+        int cap = 4096, nl = 0, nr = 0;
+        for (;;) {
+            mvKeys.resize(cap);
+            mvKeysRight.resize(cap);
+            mDescriptors.resize((size_t)cap * 32);
+            mDescriptorsRight.resize((size_t)cap * 32);
+            mvuRight.resize(cap);
+            mvDepth.resize(cap);
+            const int rc = orbg_stereo_frame(ext.context(), imLeft, imRight, w, h, step, bf, mb_,
+                                             mvKeys.data(), mDescriptors.data(), cap, &nl,
+                                             mvKeysRight.data(), mDescriptorsRight.data(), cap,
+                                             &nr, mvuRight.data(), mvDepth.data());
+            if (rc == ORBG_ERANGE) {
+                cap = nl > nr ? nl : nr;
+                continue;
+            }
+            check(rc, "orbg_stereo_frame");
+            break;
+        }
+        N = nl;
+        mvKeys.resize(nl);
+        mDescriptors.resize((size_t)nl * 32);
+        mvKeysRight.resize(nr);
+        mDescriptorsRight.resize((size_t)nr * 32);
+        mvuRight.resize(nl);
+        mvDepth.resize(nl);
+    }
 };
 
 // Optimizer::LocalBundleAdjustment's per-edge arithmetic (computeActiveErrors +

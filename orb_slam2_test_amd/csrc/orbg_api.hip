@@ -1223,6 +1223,43 @@ extern "C" int orbg_stereo_summary(orbg_ctx *c, int32_t *d_out)
     return ORBG_OK;
 }
 
+extern "C" int orbg_stereo_frame(orbg_ctx *c, const uint8_t *left, const uint8_t *right, int w,
+                                 int h, size_t step, float bf, float min_z, orbg_keypoint *kps_l,
+                                 uint8_t *desc_l, int cap_l, int *n_l, orbg_keypoint *kps_r,
+                                 uint8_t *desc_r, int cap_r, int *n_r, float *uright,
+                                 float *depth)
+{
+    if (!c) return set_err(ORBG_EINVAL, "ctx is NULL");
+    if (!left || !right || w <= 0 || h <= 0 || step < (size_t)w)
+        return set_err(ORBG_EINVAL, "bad stereo images");
+    HIPCHK(hipSetDevice(c->device));
+    int rc = plan(c, w, h, std::max(2, c->p.max_batch));
+    if (rc) return rc;
+    const size_t bytes = (size_t)w * h;
+    if (c->img_bytes < 2 * bytes) {
+        if (c->d_img) hipFree(c->d_img);
+        c->d_img = nullptr;
+        c->img_bytes = 0;
+        if ((rc = dalloc(&c->d_img, 2 * bytes))) return rc;
+        c->img_bytes = 2 * bytes;
+    }
+    // Frame.cc:110-113 extracts both images (two threads), then ComputeStereoMatches
+    HIPCHK(hipMemcpy2DAsync(c->d_img, w, left, step, w, h, hipMemcpyHostToDevice, c->stream));
+    HIPCHK(hipMemcpy2DAsync(c->d_img + bytes, w, right, step, w, h, hipMemcpyHostToDevice,
+                            c->stream));
+    if ((rc = launch_extract(c, c->d_img, 2, w, (int64_t)bytes))) return rc;
+    const int32_t l0 = 0, r1 = 1;
+    if ((rc = orbg_stereo_batch_device(c, &l0, &r1, 1, bf, min_z))) return rc;
+    int nl = 0, nr = 0;
+    rc = orbg_download_frame(c, 0, kps_l, desc_l, cap_l, &nl);
+    if (n_l) *n_l = nl;
+    if (rc) return rc;
+    rc = orbg_download_frame(c, 1, kps_r, desc_r, cap_r, &nr);
+    if (n_r) *n_r = nr;
+    if (rc) return rc;
+    return orbg_download_stereo(c, 0, uright, depth, nl, nullptr);
+}
+
 extern "C" int orbg_stereo_outputs(orbg_ctx *c, float **d_uright, float **d_depth,
                                    int32_t **d_nvalid, int32_t *frame_cap)
 {

@@ -1,6 +1,6 @@
 """GPU: the C++ host layer (compat/orbg_compat.hpp) driven like Tracking.cc -- two KITTI-
-shaped frames through ORBextractor, SearchForInitialization(0.9, checkOri, window 100) and
-brute-force knn2 -- bit-exact against the oracle.
+shaped frames through ORBextractor, SearchForInitialization(0.9, checkOri, window 100),
+brute-force knn2 and a StereoFrame -- bit-exact against the oracle.
 
 The selftest binary is started as a child process from this module, which sorts first among
 the GPU tests, before this pytest process has initialised the GPU (device_count() does not).
@@ -49,6 +49,13 @@ def test_cpp_compat_layer_matches_oracle(oracle, tmp_path):
     m12 = np.fromfile(tmp_path / "m12", dtype=np.int32)
     assert int(open(tmp_path / "nm.txt").read()) == rn
     assert np.array_equal(m12, rm12)
+    # StereoFrame (frame0 left, frame1 right)
+    pl = oracle.extract(p, seq[0], with_pyramid=True)
+    pr = oracle.extract(p, seq[1], with_pyramid=True)
+    bf = np.float32(386.1448)
+    rur, rdp = oracle.stereo_matches(p, pl, pr, w, h, float(bf), float(bf / np.float32(718.856)))
+    assert np.array_equal(np.fromfile(tmp_path / "stereo_ur", dtype=np.float32), rur)
+    assert np.array_equal(np.fromfile(tmp_path / "stereo_depth", dtype=np.float32), rdp)
     knn = np.fromfile(tmp_path / "knn", dtype=np.int32).reshape(-1, 3)
     rbi, rbd, rsd = oracle.knn2(ref[1]["desc"], ref[0]["desc"])
     assert np.array_equal(knn[:, 0], rbi)

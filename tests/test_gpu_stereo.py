@@ -62,3 +62,21 @@ def test_degenerate_pairs(oracle):
     # identical images: disparity 0 everywhere (the reference's 0 -> 0.01 branch)
     # and a featureless right image: no candidates, empty median step
     run_pairs(oracle, [(L, L.copy()), (L, S.constant(376, 1241, 90))])
+
+
+def test_stereo_frame_host_entry(oracle):
+    """StereoFrame (orbg_stereo_frame: the stereo Frame constructor on host images) equals
+    the oracle's two extractions + ComputeStereoMatches."""
+    from orb_slam2_test_amd import StereoFrame
+    L, R, _ = S.stereo_pair(376, 1241, seed=77)
+    ext = ORBextractor(2000, 1.2, 8, 20, 7)
+    F = StereoFrame(L, R, ext, BF, fx=FX)
+    p = oracle.params(nfeatures=2000)
+    rl = oracle.extract(p, L, with_pyramid=True)
+    rr = oracle.extract(p, R, with_pyramid=True)
+    assert np.array_equal(F.mvKeys, rl["kps"]) and np.array_equal(F.mDescriptors, rl["desc"])
+    assert np.array_equal(F.mvKeysRight, rr["kps"])
+    assert np.array_equal(F.mDescriptorsRight, rr["desc"])
+    rur, rdp = oracle.stereo_matches(p, rl, rr, 1241, 376, BF, float(np.float32(BF) / np.float32(FX)))
+    assert np.array_equal(F.mvuRight, rur) and np.array_equal(F.mvDepth, rdp)
+    assert F.N == len(rl["kps"])
