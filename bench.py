@@ -60,7 +60,7 @@ def kernel_algo_bytes(name, B, npairs, ncand, nkp, launches_per_step):
     elif name == "init_resolve":
         kp = nkp / max(B, 1)
         tot = npairs * (kp * 64 + kp * 4)
-    elif name == "stereo":
+    elif name == "stereo_match":
         kp = nkp / max(B, 1)
         tot = npairs * (2 * kp * (32 + 28) + kp * 8)  # both frames' kps + desc, uR + depth
     else:
