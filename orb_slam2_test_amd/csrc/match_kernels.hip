@@ -193,79 +193,116 @@ __device__ void init_cands_block(const orbg_keypoint *__restrict__ k1,
                                  unsigned long long *__restrict__ topk, int32_t *__restrict__ topn,
                                  int qbase, int f2cap)
 {
-    // F2's level-0 keys, dynamic LDS of f2cap entries (batch: level-0 capacity; host-data
-    // path: n2)
-    extern __shared__ __attribute__((aligned(16))) F2Key f2[];
+    // F2's level-0 keys (dynamic LDS, 2 x f2cap entries: batch: level-0 capacity; host-data
+    // path: n2), counting-sorted by grid column PosInGrid-x (Frame.cc:292-307): a query's
+    // window spans columns cx0..cx1 only, so it scans just those keys (the K-list order is
+    // (distance, grid order, index), independent of the scan order)
+    extern __shared__ __attribute__((aligned(16))) F2Key f2mem[];
+    F2Key *f2raw = f2mem, *f2 = f2mem + f2cap;
     __shared__ int nf2;
+    __shared__ int colstart[ORBG_GRID_COLS + 1];
     const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+    const GridPrm g = grid_prm(b);
     if (tid == 0) nf2 = 0;
+    if (tid <= ORBG_GRID_COLS) colstart[tid] = 0;
     __syncthreads();
-    for (int i = tid; i < n2; i += 256) {
+    // batch: level-major output, every level-0 key sits below f2cap = level-0 capacity
+    const int n2s = min(n2, f2cap);
+    for (int i = tid; i < n2s; i += 256) {
         const orbg_keypoint kp = k2[i];
         if (kp.octave == 0) {
+            const int px = (int)roundf((kp.x - g.min_x) * g.inv_w);
+            if (px < 0 || px >= ORBG_GRID_COLS) continue;  // outside the grid: never a candidate
             const int s = atomicAdd(&nf2, 1);
-            if (s < f2cap) f2[s] = F2Key{kp.x, kp.y, i};
+            if (s < f2cap) {
+                f2raw[s] = F2Key{kp.x, kp.y, i};
+                atomicAdd(&colstart[px + 1], 1);
+            }
         }
     }
     __syncthreads();
     const int m = min(nf2, f2cap);
-    const GridPrm g = grid_prm(b);
+    if (wv == 0) {  // 64 columns: one wave's inclusive scan
+        const int c = colstart[lane + 1];
+        const int incl = wave_incl_scan(c);
+        colstart[lane + 1] = incl;
+    }
+    __syncthreads();
+    __shared__ int cursor[ORBG_GRID_COLS];
+    if (tid < ORBG_GRID_COLS) cursor[tid] = colstart[tid];
+    __syncthreads();
+    for (int j = tid; j < m; j += 256) {
+        const F2Key fk = f2raw[j];
+        const int px = (int)roundf((fk.x - g.min_x) * g.inv_w);
+        f2[atomicAdd(&cursor[px], 1)] = fk;
+    }
+    __syncthreads();
+    // queries: 16-lane groups, 4 queries per wave at a time (~50 candidates per query: a
+    // 16-way split keeps every lane busy and the K-round merge is 4 shuffle steps deep)
     const float r = (float)window;
-    for (int qq = 0; qq < INIT_QPW; qq++) {
-        const int i1 = qbase + wv * INIT_QPW + qq;
-        if (i1 >= n1) break;
-        if (k1[i1].octave > 0) {
-            if (lane == 0) topn[i1] = -1;  // not a query
-            continue;
+    const int grp = lane >> 4, sub = lane & 15;
+    for (int qq = 0; qq < INIT_QPW; qq += 4) {
+        const int i1 = qbase + wv * INIT_QPW + qq + grp;
+        bool act = i1 < n1;
+        if (act && k1[i1].octave > 0) {
+            if (sub == 0) topn[i1] = -1;  // not a query
+            act = false;
         }
-        const Window w = make_window(g, prev[(size_t)i1 * prev_stride],
-                                     prev[(size_t)i1 * prev_stride + 1], r);
-        uint32_t qd[8];
-        {
-            const uint4 *p = (const uint4 *)(d1 + (size_t)i1 * 32);
-            const uint4 a = p[0], c = p[1];
-            qd[0] = a.x; qd[1] = a.y; qd[2] = a.z; qd[3] = a.w;
-            qd[4] = c.x; qd[5] = c.y; qd[6] = c.z; qd[7] = c.w;
-        }
+        if (!__any(act)) continue;
         unsigned long long loc[ORBG_MATCH_TOPK];
 #pragma unroll
         for (int k = 0; k < ORBG_MATCH_TOPK; k++) loc[k] = ~0ull;
         int cnt = 0;
-        if (!w.empty) {
-            for (int j = lane; j < m; j += 64) {
-                const F2Key fk = f2[j];
-                const int ord = cand_order(g, w, fk.x, fk.y);
-                if (ord < 0) continue;
-                const int d = hamming8(qd, (const uint32_t *)(d2 + (size_t)fk.idx * 32));
-                unsigned long long key = ((unsigned long long)d << 32) |
-                                         ((unsigned long long)ord << 20) | (unsigned)fk.idx;
-                cnt++;
+        if (act) {
+            const Window w = make_window(g, prev[(size_t)i1 * prev_stride],
+                                         prev[(size_t)i1 * prev_stride + 1], r);
+            uint32_t qd[8];
+            {
+                const uint4 *p = (const uint4 *)(d1 + (size_t)i1 * 32);
+                const uint4 a = p[0], c = p[1];
+                qd[0] = a.x; qd[1] = a.y; qd[2] = a.z; qd[3] = a.w;
+                qd[4] = c.x; qd[5] = c.y; qd[6] = c.z; qd[7] = c.w;
+            }
+            if (!w.empty) {
+                const int j0 = colstart[w.cx0], j1 = colstart[w.cx1 + 1];
+                for (int j = j0 + sub; j < j1; j += 16) {
+                    const F2Key fk = f2[j];
+                    const int ord = cand_order(g, w, fk.x, fk.y);
+                    if (ord < 0) continue;
+                    const int d = hamming8(qd, (const uint32_t *)(d2 + (size_t)fk.idx * 32));
+                    unsigned long long key = ((unsigned long long)d << 32) |
+                                             ((unsigned long long)ord << 20) | (unsigned)fk.idx;
+                    cnt++;
 #pragma unroll
-                for (int k = 0; k < ORBG_MATCH_TOPK; k++) {
-                    const unsigned long long lo = key < loc[k] ? key : loc[k];
-                    const unsigned long long hi = key < loc[k] ? loc[k] : key;
-                    loc[k] = lo;
-                    key = hi;
+                    for (int k = 0; k < ORBG_MATCH_TOPK; k++) {
+                        const unsigned long long lo = key < loc[k] ? key : loc[k];
+                        const unsigned long long hi = key < loc[k] ? loc[k] : key;
+                        loc[k] = lo;
+                        key = hi;
+                    }
                 }
             }
         }
-        cnt = wave_isum(cnt);
-        // merge: K rounds of wave-min over the lanes' sorted heads
+#pragma unroll
+        for (int o = 8; o > 0; o >>= 1) cnt += __shfl_xor(cnt, o, 16);
+        // merge: K rounds of group-min over the lanes' sorted heads
         int head = 0;
+        unsigned long long *out = topk + (size_t)i1 * ORBG_MATCH_TOPK;
         for (int k = 0; k < ORBG_MATCH_TOPK; k++) {
             unsigned long long mine = ~0ull;
 #pragma unroll
             for (int h = 0; h < ORBG_MATCH_TOPK; h++)
                 if (h == head) mine = loc[h];
-            const unsigned long long mn = wave_min_u64(mine);
-            if (mn == ~0ull) {
-                if (lane == 0) topk[(size_t)i1 * ORBG_MATCH_TOPK + k] = ~0ull;
-                continue;
+            unsigned long long mn = mine;
+#pragma unroll
+            for (int o = 8; o > 0; o >>= 1) {
+                const unsigned long long u = __shfl_xor(mn, o, 16);
+                mn = u < mn ? u : mn;
             }
-            if (mine == mn) head++;  // keys are unique (index in low bits)
-            if (lane == 0) topk[(size_t)i1 * ORBG_MATCH_TOPK + k] = mn;
+            if (mn != ~0ull && mine == mn) head++;  // keys are unique (index in low bits)
+            if (act && sub == 0) out[k] = mn;
         }
-        if (lane == 0) topn[i1] = cnt;
+        if (act && sub == 0) topn[i1] = cnt;
     }
 }
 
@@ -284,7 +321,8 @@ __global__ __launch_bounds__(256) void k_init_cands_pairs(
     const int32_t *f1, const int32_t *f2, int w, int h, int window, unsigned long long *topk,
     int32_t *topn, int cap)
 {
-    const int nbx = (fc + 4 * INIT_QPW - 1) / (4 * INIT_QPW);
+    // queries are level-0 keypoints: indices below the level-0 capacity
+    const int nbx = (cap + 4 * INIT_QPW - 1) / (4 * INIT_QPW);
     const int id = xcd_remap(blockIdx.x, gridDim.x);
     const int p = id / nbx, bx = id - p * nbx;
     const int a = f1[p], c = f2[p];
@@ -688,8 +726,8 @@ int launch_match_pairs(hipStream_t st, hipStream_t aux, hipEvent_t evf, hipEvent
     // cap0 = level-0 capacity: every index SearchForInitialization touches is below it
     if (fc > RESOLVE_N2_CAP || fc > (1 << 20) || cap0 > fc) return ORBG_ENOTSUP;
     PL(prof, st, "init_cands",
-       hipLaunchKernelGGL(k_init_cands_pairs, dim3((fc + 4 * INIT_QPW - 1) / (4 * INIT_QPW) * npairs),
-                          dim3(256), cap0 * sizeof(F2Key), st, kps, desc, counts, fc, d_f1, d_f2,
+       hipLaunchKernelGGL(k_init_cands_pairs, dim3((cap0 + 4 * INIT_QPW - 1) / (4 * INIT_QPW) * npairs),
+                          dim3(256), 2 * cap0 * sizeof(F2Key), st, kps, desc, counts, fc, d_f1, d_f2,
                           w, h, window, (unsigned long long *)topk, topk_n, cap0));
     // knn2 (VALU bound) on `aux` beside init_resolve (one sequential workgroup per pair);
     // serial == 1 (developer timing, ORBG_DBG=40) keeps it on `st`
@@ -725,7 +763,7 @@ int launch_init_match_single(hipStream_t st, const orbg_keypoint *k1, const uint
     }
     PL(prof, st, "init_cands",
        hipLaunchKernelGGL(k_init_cands_single, dim3((n1 + 4 * INIT_QPW - 1) / (4 * INIT_QPW)),
-                          dim3(256), (size_t)std::max(n2, 1) * sizeof(F2Key), st, k1, d1, n1, k2,
+                          dim3(256), 2 * (size_t)std::max(n2, 1) * sizeof(F2Key), st, k1, d1, n1, k2,
                           d2, n2, b, prev, window, (unsigned long long *)topk, topk_n));
     PL(prof, st, "init_resolve",
        hipLaunchKernelGGL(k_init_resolve_single, dim3(1), dim3(RESOLVE_T),
