@@ -1323,24 +1323,43 @@ extern "C" int orbg_hamming_knn2(orbg_ctx *c, const uint8_t *qdesc, int nq, cons
     if (nq < 0 || nt < 0) return set_err(ORBG_EINVAL, "negative size");
     if (nq == 0) return ORBG_OK;
     HIPCHK(hipSetDevice(c->device));
+    // the MFMA kernel keys train indices in 13 bits: train sets past that run in chunks of
+    // KNN_CHUNK, merged here in chunk order (lowest index wins ties, as in the in-order scan)
+    const int KNN_CHUNK = 8191;
+    const int nch = std::max(1, (nt + KNN_CHUNK - 1) / KNN_CHUNK);
     const size_t oq = 0, ot = al256((size_t)nq * 32), oo = ot + al256((size_t)std::max(nt, 1) * 32);
-    const size_t bytes = oo + al256((size_t)nq * 12);
+    const size_t bytes = oo + al256((size_t)nq * 12 * nch);
     void *s;
     int rc = scratch(c, bytes, &s);
     if (rc) return rc;
     uint8_t *b = (uint8_t *)s;
     HIPCHK(hipMemcpyAsync(b + oq, qdesc, (size_t)nq * 32, hipMemcpyHostToDevice, c->stream));
     if (nt) HIPCHK(hipMemcpyAsync(b + ot, tdesc, (size_t)nt * 32, hipMemcpyHostToDevice, c->stream));
-    if ((rc = launch_knn2(c->stream, b + oq, nq, b + ot, nt, (int32_t *)(b + oo), &c->prof)))
-        return rc;
-    std::vector<int32_t> out((size_t)nq * 3);
-    HIPCHK(hipMemcpyAsync(out.data(), b + oo, (size_t)nq * 12, hipMemcpyDeviceToHost, c->stream));
+    for (int k = 0; k < nch; k++) {
+        const int t0 = k * KNN_CHUNK, tn = std::min(KNN_CHUNK, nt - t0);
+        if ((rc = launch_knn2(c->stream, b + oq, nq, b + ot + (size_t)t0 * 32, std::max(tn, 0),
+                              (int32_t *)(b + oo) + (size_t)k * nq * 3, &c->prof)))
+            return rc;
+    }
+    std::vector<int32_t> out((size_t)nq * 3 * nch);
+    HIPCHK(hipMemcpyAsync(out.data(), b + oo, out.size() * 4, hipMemcpyDeviceToHost, c->stream));
     HIPCHK(hipStreamSynchronize(c->stream));
     c->prof.collect();
     for (int i = 0; i < nq; i++) {
-        if (best_idx) best_idx[i] = out[3 * i];
-        if (best_dist) best_dist[i] = out[3 * i + 1];
-        if (second_dist) second_dist[i] = out[3 * i + 2];
+        int bi = out[3 * i], bd = out[3 * i + 1], sd = out[3 * i + 2];
+        for (int k = 1; k < nch; k++) {
+            const int32_t *o = &out[((size_t)k * nq + i) * 3];
+            if (o[1] < bd) {  // a later chunk's best is strictly better
+                sd = std::min(bd, o[2]);
+                bd = o[1];
+                bi = o[0] + k * KNN_CHUNK;
+            } else {
+                sd = std::min(sd, o[1]);
+            }
+        }
+        if (best_idx) best_idx[i] = bi;
+        if (best_dist) best_dist[i] = bd;
+        if (second_dist) second_dist[i] = sd;
     }
     return ORBG_OK;
 }

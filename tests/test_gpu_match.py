@@ -67,6 +67,28 @@ def test_knn2_ties_and_edges(oracle):
     assert np.all(bi == -1) and np.all(bd == 2**31 - 1)
 
 
+def test_knn2_distance_extremes_and_train_chunks(oracle):
+    """d = 0 and d = 256 (bitwise complements), and a train set past the MFMA kernel's 13-bit
+    index (8191 rows per launch): duplicates straddling the chunk boundary keep the lowest
+    index."""
+    rng = np.random.default_rng(12)
+    t = rng.integers(0, 256, (9000, 32), dtype=np.uint8)
+    q = rng.integers(0, 256, (200, 32), dtype=np.uint8)
+    t[8500] = q[0]                  # only exact match, in the second chunk
+    t[40] = q[1]; t[8191] = q[1]    # exact match in both chunks: index 40
+    t[8192] = q[2]                  # first row of the second chunk
+    t[7] = ~q[3]                    # complement only (d = 256 is the farthest)
+    m = ORBmatcher()
+    for tt in (t, t[:8191], t[:8192]):
+        got = m.hamming_knn2(q, tt)
+        ref = oracle.knn2(q, tt)
+        for g, r in zip(got, ref):
+            assert np.array_equal(g, r)
+    qq = np.stack([~t[0], t[0]])
+    bi, bd, sd = m.hamming_knn2(qq, t[:1])
+    assert bd.tolist() == [256, 0] and bi.tolist() == [0, 0] and np.all(sd == 2**31 - 1)
+
+
 @pytest.mark.parametrize("window,nnratio,ori", [(100, 0.9, True), (10, 0.9, True),
                                                 (50, 0.6, True), (200, 0.9, False)])
 def test_search_for_initialization(oracle, pairs, window, nnratio, ori):
