@@ -23,6 +23,11 @@
  *                                     F1, F2, vbPrevMatched, vnMatches12, windowSize)
  *                                                                      src/ORBmatcher.cc:487-631
  *   orbg_stereo_batch_device ........ Frame::ComputeStereoMatches  src/Frame.cc:619-834
+ *   orbg_search_by_projection_lastframe
+ *                                     ORBmatcher(0.9,true).SearchByProjection(CurrentFrame,
+ *                                     LastFrame, th, bMono)         src/ORBmatcher.cc:1503-1667
+ *   orbg_search_by_projection_local . ORBmatcher(nnratio).SearchByProjection(F, vpMapPoints, th)
+ *                                                                      src/ORBmatcher.cc:59-154
  *   orbg_ba_linearize ............... g2o computeActiveErrors + BlockSolver::buildSystem arithmetic
  *                                     for EdgeSE3ProjectXYZ / EdgeStereoSE3ProjectXYZ inside
  *                                     Optimizer::LocalBundleAdjustment  src/Optimizer.cc:633-979
@@ -211,6 +216,80 @@ int orbg_search_for_initialization(orbg_ctx *ctx, const orbg_keypoint *kps1,
                                    const uint8_t *desc2, int n2, const orbg_bounds *bounds2,
                                    float *prev_xy, int32_t *matches12, int window,
                                    float nnratio, int check_ori, int *nmatches);
+
+/* ---------------- tracking matchers ----------------
+ * The MapPoint / Frame state the two SearchByProjection loops read enters as flat records;
+ * their writes come back as match[N] (CurrentFrame.mvpMapPoints as a query index, -1 =
+ * NULL / untouched) and nmatches.  The frame side is CurrentFrame (F): kps = mvKeysUn,
+ * desc = mDescriptors, uright = mvuRight (NULL for monocular), taken0 (NULL = none) =
+ * "mvpMapPoints[i] && mvpMapPoints[i]->Observations() > 0" on entry, bounds = mnMinX...
+ * Scale factors are the context's (ORBextractor GetScaleFactors). */
+#define ORBG_MP_VALID 1    /* lastframe: pMP && !LastFrame.mvbOutlier[i]; local: mbTrackInView && !isBad() */
+#define ORBG_MP_HAS_OBS 2  /* pMP->Observations() > 0 */
+
+typedef struct {
+    float x, y, z;     /* pMP->GetWorldPos() */
+    int32_t octave;    /* LastFrame.mvKeys[i].octave */
+    float angle;       /* LastFrame.mvKeysUn[i].angle */
+    int32_t flags;     /* ORBG_MP_* */
+} orbg_lastframe_point;
+
+typedef struct {
+    float u, v, ur;    /* mTrackProjX, mTrackProjY, mTrackProjXR (Frame::isInFrustum) */
+    int32_t level;     /* mnTrackScaleLevel */
+    float view_cos;    /* mTrackViewCos */
+    int32_t flags;     /* ORBG_MP_* */
+} orbg_map_projection;
+
+typedef struct {
+    float Tcw[12];     /* CurrentFrame.mTcw rows 0..2 (row-major 3x4) */
+    float Tlw[12];     /* LastFrame.mTcw rows 0..2 */
+    float fx, fy, cx, cy, bf, b;  /* Frame::fx.., mbf, mb */
+    int32_t mono;      /* bMono */
+    int32_t pad;
+} orbg_track_camera;
+
+/* ORBmatcher(nnratio, checkOri).SearchByProjection(CurrentFrame, LastFrame, th, bMono):
+ * pts[np] / pdesc = LastFrame.mvpMapPoints[i] (one record per LastFrame keypoint). */
+int orbg_search_by_projection_lastframe(orbg_ctx *ctx, const orbg_keypoint *kps,
+                                        const uint8_t *desc, const float *uright, int n,
+                                        const uint8_t *taken0, const orbg_bounds *bounds,
+                                        const orbg_lastframe_point *pts, const uint8_t *pdesc,
+                                        int np, const orbg_track_camera *cam, float th,
+                                        int check_ori, int32_t *match, int *nmatches);
+
+/* ORBmatcher(nnratio).SearchByProjection(F, vpMapPoints, th): mps[nm] / mdesc. */
+int orbg_search_by_projection_local(orbg_ctx *ctx, const orbg_keypoint *kps,
+                                    const uint8_t *desc, const float *uright, int n,
+                                    const uint8_t *taken0, const orbg_bounds *bounds,
+                                    const orbg_map_projection *mps, const uint8_t *mdesc, int nm,
+                                    float th, float nnratio, int32_t *match, int *nmatches);
+
+/* Batched, device-resident form of both (mode ORBG_TRACK_LASTFRAME / ORBG_TRACK_LOCAL):
+ * every pointer is device memory, frame f's arrays at f * frame_cap (keypoint side) and
+ * f * query_cap (query side); enqueued on the context stream. */
+#define ORBG_TRACK_LASTFRAME 0
+#define ORBG_TRACK_LOCAL 1
+typedef struct {
+    const orbg_keypoint *kps;    /* [B][frame_cap] */
+    const uint8_t *desc;         /* [B][frame_cap][32] */
+    const float *uright;         /* [B][frame_cap] or NULL */
+    const uint8_t *taken0;       /* [B][frame_cap] or NULL */
+    const int32_t *counts;       /* [B] */
+    const orbg_bounds *bounds;   /* [B] */
+    int32_t frame_cap;
+    const void *queries;         /* [B][query_cap] orbg_lastframe_point / orbg_map_projection */
+    const uint8_t *qdesc;        /* [B][query_cap][32] */
+    const int32_t *qcounts;      /* [B] */
+    int32_t query_cap;
+    const orbg_track_camera *cams;  /* [B], last-frame mode */
+    float th, nnratio;
+    int32_t check_ori;
+    int32_t *match;              /* [B][frame_cap] out */
+    int32_t *nmatches;           /* [B] out */
+} orbg_track_batch;
+int orbg_search_by_projection_batch_device(orbg_ctx *ctx, int mode, const orbg_track_batch *tb,
+                                           int nframes);
 
 /* ---------------- local BA linearisation ---------------- */
 typedef struct {

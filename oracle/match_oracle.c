@@ -13,10 +13,7 @@
 #include <stdlib.h>
 #include <string.h>
 
-#define GRID_ROWS 48 /* Frame.h:37 */
-#define GRID_COLS 64 /* Frame.h:38 */
 #define TH_LOW 50    /* ORBmatcher.cc:38 */
-#define HISTO_LENGTH 30
 
 /* bit-parallel popcount over 8 x int32, ORBmatcher.cc:1846-1862 */
 int orc_descriptor_distance(const uint8_t *a, const uint8_t *b)
@@ -56,13 +53,7 @@ void orc_knn2(const uint8_t *qdesc, int nq, const uint8_t *tdesc, int nt, int32_
     }
 }
 
-/* Frame grid: mGrid[ix][iy] = indices in increasing order */
-typedef struct {
-    int *start; /* GRID_COLS*GRID_ROWS + 1 */
-    int *idx;
-    float inv_w, inv_h;
-    orc_bounds b;
-} ogrid;
+#include "orc_grid.h"
 
 static int pos_in_grid(const ogrid *g, const orc_keypoint *kp, int *px, int *py)
 {
@@ -72,7 +63,7 @@ static int pos_in_grid(const ogrid *g, const orc_keypoint *kp, int *px, int *py)
     return !(*px < 0 || *px >= GRID_COLS || *py < 0 || *py >= GRID_ROWS);
 }
 
-static void build_grid(ogrid *g, const orc_keypoint *kps, int n, const orc_bounds *b)
+void orc_grid_build(ogrid *g, const orc_keypoint *kps, int n, const orc_bounds *b)
 {
     g->b = *b;
     /* Frame.cc:273-274 */
@@ -99,14 +90,14 @@ static void build_grid(ogrid *g, const orc_keypoint *kps, int n, const orc_bound
     free(cell);
 }
 
-static void free_grid(ogrid *g)
+void orc_grid_free(ogrid *g)
 {
     free(g->start);
     free(g->idx);
 }
 
 /* Frame::GetFeaturesInArea, Frame.cc:421-504 */
-static int features_in_area(const ogrid *g, const orc_keypoint *kps, float x, float y, float r,
+int orc_features_in_area(const ogrid *g, const orc_keypoint *kps, float x, float y, float r,
                             int minLevel, int maxLevel, int *out)
 {
     int n = 0;
@@ -151,7 +142,7 @@ static int features_in_area(const ogrid *g, const orc_keypoint *kps, float x, fl
 }
 
 /* ORBmatcher::ComputeThreeMaxima, :1800-1841 */
-static void three_maxima(const int *hsize, int *ind1, int *ind2, int *ind3)
+void orc_three_maxima(const int *hsize, int *ind1, int *ind2, int *ind3)
 {
     int max1 = 0, max2 = 0, max3 = 0;
     for (int i = 0; i < HISTO_LENGTH; i++) {
@@ -188,7 +179,7 @@ int orc_search_for_initialization(const orc_keypoint *kps1, const uint8_t *desc1
 {
     int nmatches = 0;
     ogrid g;
-    build_grid(&g, kps2, n2, b2);
+    orc_grid_build(&g, kps2, n2, b2);
     for (int i = 0; i < n1; i++)
         matches12[i] = -1;
     int *hist = (int *)malloc(sizeof(int) * HISTO_LENGTH * (n1 > 0 ? n1 : 1));
@@ -207,7 +198,7 @@ int orc_search_for_initialization(const orc_keypoint *kps1, const uint8_t *desc1
         const int level1 = kps1[i1].octave;
         if (level1 > 0)
             continue;
-        const int nc = features_in_area(&g, kps2, prev_xy[2 * i1], prev_xy[2 * i1 + 1],
+        const int nc = orc_features_in_area(&g, kps2, prev_xy[2 * i1], prev_xy[2 * i1 + 1],
                                         (float)window, level1, level1, cand);
         if (nc == 0)
             continue;
@@ -250,7 +241,7 @@ int orc_search_for_initialization(const orc_keypoint *kps1, const uint8_t *desc1
     }
     if (check_ori) {
         int ind1 = -1, ind2 = -1, ind3 = -1;
-        three_maxima(hsize, &ind1, &ind2, &ind3);
+        orc_three_maxima(hsize, &ind1, &ind2, &ind3);
         for (int i = 0; i < HISTO_LENGTH; i++) {
             if (i == ind1 || i == ind2 || i == ind3)
                 continue;
@@ -272,6 +263,6 @@ int orc_search_for_initialization(const orc_keypoint *kps1, const uint8_t *desc1
     free(matched_dist);
     free(matches21);
     free(cand);
-    free_grid(&g);
+    orc_grid_free(&g);
     return nmatches;
 }

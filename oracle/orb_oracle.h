@@ -17,6 +17,7 @@
  *   ORBmatcher::SearchForInit ....... src/ORBmatcher.cc:487-631, 1800-1841
  *   Frame grid / GetFeaturesInArea .. src/Frame.cc:292-307, 421-520
  *   Frame::ComputeStereoMatches ..... src/Frame.cc:619-834 (stereo_oracle.c)
+ *   ORBmatcher::SearchByProjection .. src/ORBmatcher.cc:1503-1667, 59-154 (track_oracle.c)
  *   g2o edge arithmetic (double) .... Thirdparty/g2o/g2o/types/types_six_dof_expmap.{h,cpp},
  *                                     core/base_binary_edge.hpp:55-120, core/base_edge.h:58-102,
  *                                     core/robust_kernel_impl.cpp:65-91
@@ -131,6 +132,54 @@ int orc_search_for_initialization(const orc_keypoint *kps1, const uint8_t *desc1
                                   const orc_keypoint *kps2, const uint8_t *desc2, int n2,
                                   const orc_bounds *b2, float *prev_xy, int32_t *matches12,
                                   int window, float nnratio, int check_ori);
+
+/* ---- tracking matchers (track_oracle.c) ---- */
+#define ORC_MP_VALID 1    /* lastframe: pMP && !mvbOutlier[i]; local: mbTrackInView && !isBad() */
+#define ORC_MP_HAS_OBS 2  /* pMP->Observations() > 0 */
+
+/* LastFrame.mvpMapPoints[i] as SearchByProjection(CurrentFrame, LastFrame) reads it */
+typedef struct {
+    float x, y, z;      /* pMP->GetWorldPos() */
+    int32_t octave;     /* LastFrame.mvKeys[i].octave */
+    float angle;        /* LastFrame.mvKeysUn[i].angle */
+    int32_t flags;
+} orc_lf_point;
+
+/* a local map point after Frame::isInFrustum (MapPoint mTrack* members) */
+typedef struct {
+    float u, v, ur;     /* mTrackProjX, mTrackProjY, mTrackProjXR */
+    int32_t level;      /* mnTrackScaleLevel */
+    float view_cos;     /* mTrackViewCos */
+    int32_t flags;
+} orc_map_proj;
+
+/* CurrentFrame / LastFrame camera state: 3x4 row-major mTcw, intrinsics, mbf, mb */
+typedef struct {
+    float Tcw[12], Tlw[12];
+    float fx, fy, cx, cy, bf, b;
+    int32_t mono, pad;
+} orc_track_cam;
+
+/* cv::gemm small-matrix pin: out = (float)(alpha * op(R) x + c), double work type.  R is
+ * the 3x3 block of a 3x4 row-major matrix. */
+void orc_gemm3(const float *R, int transR, const float *x, float alpha, const float *c,
+               float *out);
+/* bForward / bBackward of ORBmatcher.cc:1521-1522 */
+void orc_track_direction(const orc_track_cam *cam, int *forward, int *backward);
+/* match[n]: CurrentFrame.mvpMapPoints as a LastFrame point index (-1 = NULL); taken0 (may
+ * be NULL): initial mvpMapPoints[i] && Observations() > 0.  Returns nmatches. */
+int orc_search_by_projection_lastframe(const orc_keypoint *kps, const uint8_t *desc,
+                                       const float *uright, int n, const uint8_t *taken0,
+                                       const orc_bounds *b, const float *scale_factors,
+                                       const orc_lf_point *pts, const uint8_t *pdesc, int np,
+                                       const orc_track_cam *cam, float th, int check_ori,
+                                       int32_t *match);
+/* match[n]: map point index written by this call (-1 = untouched).  Returns nmatches. */
+int orc_search_by_projection_local(const orc_keypoint *kps, const uint8_t *desc,
+                                   const float *uright, int n, const uint8_t *taken0,
+                                   const orc_bounds *b, const float *scale_factors,
+                                   const orc_map_proj *mps, const uint8_t *mdesc, int nm,
+                                   float th, float nnratio, int32_t *match);
 
 /* ---- Frame::ComputeStereoMatches (stereo_oracle.c) ----
  * kl/dl: left keypoints (mvKeys) + descriptors, kr/dr: right.  pyr_l / pyr_r: the two

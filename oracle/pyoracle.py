@@ -30,6 +30,13 @@ EDGE_OUT_DTYPE = np.dtype([("err", "<f8", 3), ("chi2", "<f8"), ("rho1", "<f8"),
 
 RESIZE_SCALAR, RESIZE_SSE2_16_4, RESIZE_SIMD_16_8 = 0, 4, 8
 
+# tracking matcher records (orb_oracle.h: orc_lf_point, orc_map_proj)
+MP_VALID, MP_HAS_OBS = 1, 2
+LF_DTYPE = np.dtype([("x", "<f4"), ("y", "<f4"), ("z", "<f4"), ("octave", "<i4"),
+                     ("angle", "<f4"), ("flags", "<i4")])
+MP_DTYPE = np.dtype([("u", "<f4"), ("v", "<f4"), ("ur", "<f4"), ("level", "<i4"),
+                     ("view_cos", "<f4"), ("flags", "<i4")])
+
 
 class Params(C.Structure):
     _fields_ = [("nfeatures", C.c_int32), ("scale_factor", C.c_float), ("nlevels", C.c_int32),
@@ -38,6 +45,23 @@ class Params(C.Structure):
                 ("sigma2", C.c_float * MAX_LEVELS), ("inv_sigma2", C.c_float * MAX_LEVELS),
                 ("features_per_level", C.c_int32 * MAX_LEVELS), ("umax", C.c_int32 * 16),
                 ("resize_mode", C.c_int32), ("gauss_k", C.c_int32 * 7), ("brief_fma", C.c_int32)]
+
+
+class TrackCam(C.Structure):
+    _fields_ = [("Tcw", C.c_float * 12), ("Tlw", C.c_float * 12), ("fx", C.c_float),
+                ("fy", C.c_float), ("cx", C.c_float), ("cy", C.c_float), ("bf", C.c_float),
+                ("b", C.c_float), ("mono", C.c_int32), ("pad", C.c_int32)]
+
+
+def track_cam(Tcw, Tlw, fx, fy, cx, cy, bf, b, mono):
+    c = TrackCam()
+    for i, v in enumerate(np.asarray(Tcw, np.float32).reshape(12)):
+        c.Tcw[i] = float(v)
+    for i, v in enumerate(np.asarray(Tlw, np.float32).reshape(12)):
+        c.Tlw[i] = float(v)
+    c.fx, c.fy, c.cx, c.cy, c.bf, c.b = (float(np.float32(v)) for v in (fx, fy, cx, cy, bf, b))
+    c.mono = 1 if mono else 0
+    return c
 
 
 class Bounds(C.Structure):
@@ -50,8 +74,8 @@ _lib = None
 
 def build(force=False):
     """Compile the oracle with its Makefile (gcc).  Returns the .so path."""
-    srcs = [os.path.join(HERE, f) for f in ("orb_oracle.c", "match_oracle.c", "ba_oracle.c",
-                                            "orb_oracle.h", "orb_pattern.inc")]
+    srcs = [os.path.join(HERE, f) for f in os.listdir(HERE)
+            if f.endswith((".c", ".h", ".inc")) or f == "Makefile"]
     if force or not os.path.exists(LIB_PATH) or any(
             os.path.getmtime(s) > os.path.getmtime(LIB_PATH) for s in srcs if os.path.exists(s)):
         subprocess.check_call(["make", "-s", "-C", HERE])
@@ -96,6 +120,12 @@ def lib():
         L.orc_ba_numeric_jacobian.argtypes = [vp, vp, vp, vp, vp]
         L.orc_stereo_matches.argtypes = [P(Params), vp, vp, C.c_int, vp, vp, C.c_int, vp, vp,
                                          C.c_int, C.c_int, C.c_float, C.c_float, vp, vp]
+        L.orc_track_direction.argtypes = [vp, vp, vp]
+        L.orc_search_by_projection_lastframe.argtypes = [vp, vp, vp, C.c_int, vp, vp, vp, vp,
+                                                         vp, C.c_int, vp, C.c_float, C.c_int,
+                                                         vp]
+        L.orc_search_by_projection_local.argtypes = [vp, vp, vp, C.c_int, vp, vp, vp, vp, vp,
+                                                     C.c_int, C.c_float, C.c_float, vp]
         _lib = L
     return _lib
 
@@ -241,6 +271,53 @@ def stereo_matches(p, left, right, w, h, bf, min_z):
     lib().orc_stereo_matches(C.byref(p), _p(kl), _p(dl), len(kl), _p(kr), _p(dr), len(kr),
                              _p(pl), _p(pr), w, h, float(bf), float(min_z), _p(ur), _p(dp))
     return ur[:len(kl)].copy(), dp[:len(kl)].copy()
+
+
+def _frame_args(kps, desc, uright, taken0):
+    kps = np.ascontiguousarray(kps, KP_DTYPE)
+    desc = np.ascontiguousarray(desc, np.uint8)
+    ur = None if uright is None else np.ascontiguousarray(uright, np.float32)
+    tk = None if taken0 is None else np.ascontiguousarray(taken0, np.uint8)
+    return kps, desc, ur, tk
+
+
+def track_direction(cam):
+    f, b = C.c_int(), C.c_int()
+    lib().orc_track_direction(C.byref(cam), C.byref(f), C.byref(b))
+    return f.value, b.value
+
+
+def search_by_projection_lastframe(kps, desc, uright, taken0, bounds, scale_factors, pts, pdesc,
+                                   cam, th, check_ori=True):
+    """ORBmatcher::SearchByProjection(CurrentFrame, LastFrame, th, bMono) restated
+    (oracle/track_oracle.c).  Returns (nmatches, match[n]: LastFrame point index or -1)."""
+    kps, desc, ur, tk = _frame_args(kps, desc, uright, taken0)
+    pts = np.ascontiguousarray(pts, LF_DTYPE)
+    pdesc = np.ascontiguousarray(pdesc, np.uint8)
+    sf = np.ascontiguousarray(scale_factors, np.float32)
+    match = np.zeros(max(len(kps), 1), np.int32)
+    b = Bounds(*[float(v) for v in bounds])
+    n = lib().orc_search_by_projection_lastframe(_p(kps), _p(desc), _p(ur), len(kps), _p(tk),
+                                                 C.byref(b), _p(sf), _p(pts), _p(pdesc),
+                                                 len(pts), C.byref(cam), float(th),
+                                                 1 if check_ori else 0, _p(match))
+    return n, match[:len(kps)].copy()
+
+
+def search_by_projection_local(kps, desc, uright, taken0, bounds, scale_factors, mps, mdesc,
+                               th=1.0, nnratio=0.8):
+    """ORBmatcher(nnratio).SearchByProjection(F, vpMapPoints, th) restated.  Returns
+    (nmatches, match[n]: map point index written by the call or -1)."""
+    kps, desc, ur, tk = _frame_args(kps, desc, uright, taken0)
+    mps = np.ascontiguousarray(mps, MP_DTYPE)
+    mdesc = np.ascontiguousarray(mdesc, np.uint8)
+    sf = np.ascontiguousarray(scale_factors, np.float32)
+    match = np.zeros(max(len(kps), 1), np.int32)
+    b = Bounds(*[float(v) for v in bounds])
+    n = lib().orc_search_by_projection_local(_p(kps), _p(desc), _p(ur), len(kps), _p(tk),
+                                             C.byref(b), _p(sf), _p(mps), _p(mdesc), len(mps),
+                                             float(th), float(nnratio), _p(match))
+    return n, match[:len(kps)].copy()
 
 
 def frames_batch(p, imgs, nthreads=1, window=100, nnratio=0.9):

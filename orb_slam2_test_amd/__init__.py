@@ -9,9 +9,9 @@ the reference's C++ interfaces; see DESIGN.md.
 """
 from ._lib import KP_DTYPE, EDGE_DTYPE, EDGE_OUT_DTYPE, POSE_DTYPE, LIB_PATH  # noqa: F401
 from .orbextractor import ORBextractor  # noqa: F401
-from .orbmatcher import Frame, ORBmatcher  # noqa: F401
+from .orbmatcher import Frame, MapPointProjections, ORBmatcher  # noqa: F401
 from .frame import StereoFrame  # noqa: F401
 from .optimizer import linearize_local_ba  # noqa: F401
 
-__all__ = ["ORBextractor", "ORBmatcher", "Frame", "StereoFrame", "linearize_local_ba", "KP_DTYPE",
+__all__ = ["ORBextractor", "ORBmatcher", "Frame", "MapPointProjections", "StereoFrame", "linearize_local_ba", "KP_DTYPE",
            "EDGE_DTYPE", "EDGE_OUT_DTYPE", "POSE_DTYPE"]

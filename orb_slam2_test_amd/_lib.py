@@ -34,6 +34,41 @@ EDGE_OUT_DTYPE = np.dtype([("err", "<f8", 3), ("chi2", "<f8"), ("rho1", "<f8"),
                            ("jp", "<f8", (3, 3)), ("jt", "<f8", (3, 6)), ("hpl", "<f8", (3, 6))])
 
 
+# tracking matcher records (orbg_lastframe_point, orbg_map_projection)
+MP_VALID, MP_HAS_OBS = 1, 2
+TRACK_LASTFRAME, TRACK_LOCAL = 0, 1
+LF_DTYPE = np.dtype([("x", "<f4"), ("y", "<f4"), ("z", "<f4"), ("octave", "<i4"),
+                     ("angle", "<f4"), ("flags", "<i4")])
+MP_DTYPE = np.dtype([("u", "<f4"), ("v", "<f4"), ("ur", "<f4"), ("level", "<i4"),
+                     ("view_cos", "<f4"), ("flags", "<i4")])
+
+
+class TrackCamera(C.Structure):
+    _fields_ = [("Tcw", C.c_float * 12), ("Tlw", C.c_float * 12), ("fx", C.c_float),
+                ("fy", C.c_float), ("cx", C.c_float), ("cy", C.c_float), ("bf", C.c_float),
+                ("b", C.c_float), ("mono", C.c_int32), ("pad", C.c_int32)]
+
+
+class TrackBatch(C.Structure):
+    _fields_ = [("kps", C.c_void_p), ("desc", C.c_void_p), ("uright", C.c_void_p),
+                ("taken0", C.c_void_p), ("counts", C.c_void_p), ("bounds", C.c_void_p),
+                ("frame_cap", C.c_int32), ("queries", C.c_void_p), ("qdesc", C.c_void_p),
+                ("qcounts", C.c_void_p), ("query_cap", C.c_int32), ("cams", C.c_void_p),
+                ("th", C.c_float), ("nnratio", C.c_float), ("check_ori", C.c_int32),
+                ("match", C.c_void_p), ("nmatches", C.c_void_p)]
+
+
+def track_camera(Tcw, Tlw, fx, fy, cx, cy, bf, b, mono):
+    c = TrackCamera()
+    for i, v in enumerate(np.asarray(Tcw, np.float32).reshape(12)):
+        c.Tcw[i] = float(v)
+    for i, v in enumerate(np.asarray(Tlw, np.float32).reshape(12)):
+        c.Tlw[i] = float(v)
+    c.fx, c.fy, c.cx, c.cy, c.bf, c.b = (float(np.float32(v)) for v in (fx, fy, cx, cy, bf, b))
+    c.mono = 1 if mono else 0
+    return c
+
+
 class Params(C.Structure):
     _fields_ = [("nfeatures", C.c_int32), ("scale_factor", C.c_float), ("nlevels", C.c_int32),
                 ("ini_th_fast", C.c_int32), ("min_th_fast", C.c_int32),
@@ -109,6 +144,11 @@ def lib():
         "orbg_hamming_knn2": (i32, [vp, vp, i32, vp, i32, vp, vp, vp]),
         "orbg_search_for_initialization": (i32, [vp, vp, vp, i32, vp, vp, i32, P(Bounds), vp, vp,
                                                  i32, f32, i32, P(i32)]),
+        "orbg_search_by_projection_lastframe": (i32, [vp, vp, vp, vp, i32, vp, P(Bounds), vp, vp,
+                                                      i32, P(TrackCamera), f32, i32, vp, P(i32)]),
+        "orbg_search_by_projection_local": (i32, [vp, vp, vp, vp, i32, vp, P(Bounds), vp, vp, i32,
+                                                  f32, f32, vp, P(i32)]),
+        "orbg_search_by_projection_batch_device": (i32, [vp, i32, P(TrackBatch), i32]),
         "orbg_ba_linearize": (i32, [vp, vp, i32, vp, i32, vp, i32, vp, vp, vp, vp, vp]),
         "orbg_ba_linearize_device": (i32, [vp, vp, i32, vp, i32, vp, i32, vp, vp, vp, vp, vp, vp,
                                            vp, vp, vp]),

@@ -15,6 +15,7 @@
 
 #include "../../include/orbg.h"
 #include "orbg_internal.h"
+#include "track_args.h"
 
 #pragma clang fp contract(off)
 
@@ -247,6 +248,9 @@ struct orbg_ctx {
     // single-pair / host-data scratch
     void *d_scr = nullptr;
     size_t scr_bytes = 0;
+    // tracking matchers: K-lists of the queries
+    void *d_trk = nullptr;
+    size_t trk_bytes = 0;
     Prof prof;
 };
 
@@ -757,6 +761,7 @@ extern "C" void orbg_destroy(orbg_ctx *c)
     free_plan(c);
     if (c->d_img) hipFree(c->d_img);
     if (c->d_scr) hipFree(c->d_scr);
+    if (c->d_trk) hipFree(c->d_trk);
     if (c->aux_stream) hipStreamSynchronize(c->aux_stream);
     if (c->mstream) hipStreamSynchronize(c->mstream);
     for (int i = 0; i < 2; i++) {
@@ -1501,3 +1506,162 @@ void prof_end(void *prof, hipStream_t s, const char *n, hipEvent_t a)
     ((Prof *)prof)->end(s, n, a);
 }
 }  // namespace orbg
+
+// ---------------------------------------------------------------------------
+// tracking matchers (ORBmatcher::SearchByProjection x 2)
+// ---------------------------------------------------------------------------
+static int track_run(orbg_ctx *c, int mode, const orbg_track_batch *tb, int nframes)
+{
+    if (tb->frame_cap <= 0 || tb->query_cap <= 0 || tb->frame_cap > (1 << 20))
+        return set_err(ORBG_EINVAL, "frame_cap / query_cap out of range");
+    if (!tb->kps || !tb->desc || !tb->counts || !tb->bounds || !tb->queries || !tb->qdesc ||
+        !tb->qcounts || !tb->match || !tb->nmatches)
+        return set_err(ORBG_EINVAL, "NULL device array");
+    if (mode == ORBG_TRACK_LASTFRAME && !tb->cams) return set_err(ORBG_EINVAL, "cams is NULL");
+    const size_t tk = al256((size_t)nframes * tb->query_cap * ORBG_MATCH_TOPK * 8);
+    const size_t need = tk + al256((size_t)nframes * tb->query_cap * 4);
+    if (c->trk_bytes < need) {
+        HIPCHK(hipStreamSynchronize(c->stream));
+        if (c->d_trk) hipFree(c->d_trk);
+        c->d_trk = nullptr;
+        c->trk_bytes = 0;
+        if (hipMalloc(&c->d_trk, need) != hipSuccess)
+            return set_err(ORBG_ENOMEM, "track scratch %zu bytes", need);
+        c->trk_bytes = need;
+    }
+    TrackArgs A{};
+    A.kps = tb->kps;
+    A.desc = tb->desc;
+    A.uright = tb->uright;
+    A.taken0 = tb->taken0;
+    A.counts = tb->counts;
+    A.bounds = tb->bounds;
+    A.fc = tb->frame_cap;
+    A.q = tb->queries;
+    A.qdesc = tb->qdesc;
+    A.qcounts = tb->qcounts;
+    A.qc = tb->query_cap;
+    A.cams = tb->cams;
+    for (int l = 0; l < ORBG_MAX_LEVELS; l++)
+        A.scale[l] = l < c->p.nlevels ? c->scale[l] : 1.f;
+    A.th = tb->th;
+    A.nnratio = tb->nnratio;
+    A.check_ori = tb->check_ori;
+    A.topk = (unsigned long long *)c->d_trk;
+    A.topn = (int32_t *)((uint8_t *)c->d_trk + tk);
+    A.match = tb->match;
+    A.nmatches = tb->nmatches;
+    const int rc = launch_track(c->stream, mode, A, nframes, &c->prof);
+    if (rc == ORBG_ENOTSUP)
+        return set_err(rc, "frame_cap %d / query_cap %d exceed the LDS budget", tb->frame_cap,
+                       tb->query_cap);
+    if (rc) return set_err(rc, "track launch failed");
+    return ORBG_OK;
+}
+
+extern "C" int orbg_search_by_projection_batch_device(orbg_ctx *c, int mode,
+                                                      const orbg_track_batch *tb, int nframes)
+{
+    if (!c || !tb) return set_err(ORBG_EINVAL, "NULL argument");
+    if (mode != ORBG_TRACK_LASTFRAME && mode != ORBG_TRACK_LOCAL)
+        return set_err(ORBG_EINVAL, "mode %d", mode);
+    if (nframes <= 0) return ORBG_OK;
+    HIPCHK(hipSetDevice(c->device));
+    return track_run(c, mode, tb, nframes);
+}
+
+// one frame from host arrays: upload, run, download
+static int track_host(orbg_ctx *c, int mode, const orbg_keypoint *kps, const uint8_t *desc,
+                      const float *uright, int n, const uint8_t *taken0, const orbg_bounds *bounds,
+                      const void *q, size_t qrec, const uint8_t *qdesc, int nq,
+                      const orbg_track_camera *cam, float th, float nnratio, int check_ori,
+                      int32_t *match, int *nmatches)
+{
+    if (!c || !bounds || !match || (n > 0 && (!kps || !desc)) || (nq > 0 && (!q || !qdesc)))
+        return set_err(ORBG_EINVAL, "NULL argument");
+    if (n < 0 || nq < 0) return set_err(ORBG_EINVAL, "negative size");
+    if (mode == ORBG_TRACK_LASTFRAME && !cam) return set_err(ORBG_EINVAL, "cam is NULL");
+    for (int i = 0; i < n; i++) match[i] = -1;
+    if (nmatches) *nmatches = 0;
+    if (n == 0 || nq == 0) return ORBG_OK;
+    HIPCHK(hipSetDevice(c->device));
+    const size_t fc = (size_t)n, qc = (size_t)nq;
+    size_t off = 0;
+    auto take = [&](size_t bytes) {
+        const size_t o = off;
+        off += al256(bytes);
+        return o;
+    };
+    const size_t o_kps = take(fc * sizeof(orbg_keypoint)), o_desc = take(fc * 32);
+    const size_t o_ur = uright ? take(fc * 4) : 0, o_tk = taken0 ? take(fc) : 0;
+    const size_t o_cnt = take(8), o_b = take(sizeof(orbg_bounds)), o_q = take(qc * qrec);
+    const size_t o_qd = take(qc * 32), o_cam = take(sizeof(orbg_track_camera));
+    const size_t o_match = take(fc * 4), o_nm = take(4);
+    void *s;
+    int rc = scratch(c, off, &s);
+    if (rc) return rc;
+    uint8_t *b = (uint8_t *)s;
+    const int32_t cnts[2] = {n, nq};
+    HIPCHK(hipMemcpyAsync(b + o_kps, kps, fc * sizeof(orbg_keypoint), hipMemcpyHostToDevice, c->stream));
+    HIPCHK(hipMemcpyAsync(b + o_desc, desc, fc * 32, hipMemcpyHostToDevice, c->stream));
+    if (uright) HIPCHK(hipMemcpyAsync(b + o_ur, uright, fc * 4, hipMemcpyHostToDevice, c->stream));
+    if (taken0) HIPCHK(hipMemcpyAsync(b + o_tk, taken0, fc, hipMemcpyHostToDevice, c->stream));
+    HIPCHK(hipMemcpyAsync(b + o_cnt, cnts, 8, hipMemcpyHostToDevice, c->stream));
+    HIPCHK(hipMemcpyAsync(b + o_b, bounds, sizeof(orbg_bounds), hipMemcpyHostToDevice, c->stream));
+    HIPCHK(hipMemcpyAsync(b + o_q, q, qc * qrec, hipMemcpyHostToDevice, c->stream));
+    HIPCHK(hipMemcpyAsync(b + o_qd, qdesc, qc * 32, hipMemcpyHostToDevice, c->stream));
+    if (cam)
+        HIPCHK(hipMemcpyAsync(b + o_cam, cam, sizeof(*cam), hipMemcpyHostToDevice, c->stream));
+    orbg_track_batch tb{};
+    tb.kps = (const orbg_keypoint *)(b + o_kps);
+    tb.desc = b + o_desc;
+    tb.uright = uright ? (const float *)(b + o_ur) : nullptr;
+    tb.taken0 = taken0 ? b + o_tk : nullptr;
+    tb.counts = (const int32_t *)(b + o_cnt);
+    tb.bounds = (const orbg_bounds *)(b + o_b);
+    tb.frame_cap = n;
+    tb.queries = b + o_q;
+    tb.qdesc = b + o_qd;
+    tb.qcounts = (const int32_t *)(b + o_cnt) + 1;
+    tb.query_cap = nq;
+    tb.cams = cam ? (const orbg_track_camera *)(b + o_cam) : nullptr;
+    tb.th = th;
+    tb.nnratio = nnratio;
+    tb.check_ori = check_ori;
+    tb.match = (int32_t *)(b + o_match);
+    tb.nmatches = (int32_t *)(b + o_nm);
+    if ((rc = track_run(c, mode, &tb, 1))) return rc;
+    int32_t nm = 0;
+    HIPCHK(hipMemcpyAsync(match, b + o_match, fc * 4, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(hipMemcpyAsync(&nm, b + o_nm, 4, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(hipStreamSynchronize(c->stream));
+    c->prof.collect();
+    if (nmatches) *nmatches = nm;
+    return ORBG_OK;
+}
+
+extern "C" int orbg_search_by_projection_lastframe(orbg_ctx *c, const orbg_keypoint *kps,
+                                                   const uint8_t *desc, const float *uright,
+                                                   int n, const uint8_t *taken0,
+                                                   const orbg_bounds *bounds,
+                                                   const orbg_lastframe_point *pts,
+                                                   const uint8_t *pdesc, int np,
+                                                   const orbg_track_camera *cam, float th,
+                                                   int check_ori, int32_t *match, int *nmatches)
+{
+    return track_host(c, ORBG_TRACK_LASTFRAME, kps, desc, uright, n, taken0, bounds, pts,
+                      sizeof(orbg_lastframe_point), pdesc, np, cam, th, 0.f, check_ori, match,
+                      nmatches);
+}
+
+extern "C" int orbg_search_by_projection_local(orbg_ctx *c, const orbg_keypoint *kps,
+                                               const uint8_t *desc, const float *uright, int n,
+                                               const uint8_t *taken0, const orbg_bounds *bounds,
+                                               const orbg_map_projection *mps,
+                                               const uint8_t *mdesc, int nm, float th,
+                                               float nnratio, int32_t *match, int *nmatches)
+{
+    return track_host(c, ORBG_TRACK_LOCAL, kps, desc, uright, n, taken0, bounds, mps,
+                      sizeof(orbg_map_projection), mdesc, nm, nullptr, th, nnratio, 0, match,
+                      nmatches);
+}

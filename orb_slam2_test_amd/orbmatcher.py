@@ -5,6 +5,8 @@ Reference: include/ORBmatcher.h:40-193, src/ORBmatcher.cc.
     m = ORBmatcher(nnratio=0.9, checkOri=True)
     nmatches, vnMatches12 = m.SearchForInitialization(F1, F2, vbPrevMatched, windowSize=100)
     d = ORBmatcher.DescriptorDistance(a, b)
+    n, match = m.SearchByProjection(CurrentFrame, LastFrame, th, bMono)   # motion model
+    n, match = m.SearchByProjection(F, vpMapPoints, th)                   # local map
 
 ``Frame`` here carries just what the matcher reads from ORB_SLAM2::Frame
 (mvKeysUn, mDescriptors and the image bounds mnMinX/mnMaxX/mnMinY/mnMaxY that define
@@ -31,13 +33,27 @@ def _ctx(device=0):
 
 @dataclass
 class Frame:
-    """The subset of ORB_SLAM2::Frame the matcher reads."""
+    """The subset of ORB_SLAM2::Frame the matchers read."""
     mvKeysUn: np.ndarray          # KP_DTYPE structured array
     mDescriptors: np.ndarray      # (N, 32) uint8
     mnMinX: float = 0.0
     mnMaxX: float = 0.0
     mnMinY: float = 0.0
     mnMaxY: float = 0.0
+    # tracking state (SearchByProjection)
+    mvuRight: np.ndarray = None   # (N,) float32, None = monocular
+    mTcw: np.ndarray = None       # (3, 4) float32 rows of the pose
+    fx: float = 0.0
+    fy: float = 0.0
+    cx: float = 0.0
+    cy: float = 0.0
+    mbf: float = 0.0
+    mb: float = 0.0
+    # mvpMapPoints[i] && mvpMapPoints[i]->Observations() > 0 on entry, (N,) uint8 or None
+    taken: np.ndarray = None
+    # LastFrame.mvpMapPoints as LF_DTYPE records (+ their descriptors), one per keypoint
+    points: np.ndarray = None
+    point_desc: np.ndarray = None
 
     @classmethod
     def from_extraction(cls, keypoints, descriptors, width, height):
@@ -49,6 +65,14 @@ class Frame:
     @property
     def N(self):
         return len(self.mvKeysUn)
+
+
+@dataclass
+class MapPointProjections:
+    """vpMapPoints after Frame::isInFrustum: MP_DTYPE records (mTrackProjX/Y/XR,
+    mnTrackScaleLevel, mTrackViewCos, flags) and pMP->GetDescriptor() rows."""
+    records: np.ndarray
+    descriptors: np.ndarray
 
 
 class ORBmatcher:
@@ -95,3 +119,35 @@ class ORBmatcher:
                                           len(t), L.ptr(bi), L.ptr(bd), L.ptr(sd)),
                 "orbg_hamming_knn2")
         return bi, bd, sd
+
+    def SearchByProjection(self, F, second, th, bMono=True):
+        """SearchByProjection(CurrentFrame, LastFrame, th, bMono) (ORBmatcher.cc:1503-1667)
+        when `second` is a Frame carrying `points`, SearchByProjection(F, vpMapPoints, th)
+        (:59-146) when it is a MapPointProjections.  Returns (nmatches, match): match[i] is
+        the LastFrame keypoint / map point index written to F.mvpMapPoints[i], -1 for
+        NULL / untouched."""
+        kps = np.ascontiguousarray(F.mvKeysUn, L.KP_DTYPE)
+        desc = np.ascontiguousarray(F.mDescriptors, np.uint8)
+        ur = None if F.mvuRight is None else np.ascontiguousarray(F.mvuRight, np.float32)
+        tk = None if F.taken is None else np.ascontiguousarray(F.taken, np.uint8)
+        b = L.Bounds(F.mnMinX, F.mnMaxX, F.mnMinY, F.mnMaxY)
+        match = np.full(len(kps), -1, np.int32)
+        nm = C.c_int()
+        h = _ctx(self.device).handle
+        if isinstance(second, MapPointProjections):
+            rec = np.ascontiguousarray(second.records, L.MP_DTYPE)
+            md = np.ascontiguousarray(second.descriptors, np.uint8)
+            L.check(L.lib().orbg_search_by_projection_local(
+                h, L.ptr(kps), L.ptr(desc), L.ptr(ur), len(kps), L.ptr(tk), C.byref(b),
+                L.ptr(rec), L.ptr(md), len(rec), float(th), self.mfNNratio, L.ptr(match),
+                C.byref(nm)), "orbg_search_by_projection_local")
+        else:
+            pts = np.ascontiguousarray(second.points, L.LF_DTYPE)
+            pd = np.ascontiguousarray(second.point_desc, np.uint8)
+            cam = L.track_camera(F.mTcw, second.mTcw, F.fx, F.fy, F.cx, F.cy, F.mbf, F.mb, bMono)
+            L.check(L.lib().orbg_search_by_projection_lastframe(
+                h, L.ptr(kps), L.ptr(desc), L.ptr(ur), len(kps), L.ptr(tk), C.byref(b),
+                L.ptr(pts), L.ptr(pd), len(pts), C.byref(cam), float(th),
+                1 if self.mbCheckOrientation else 0, L.ptr(match), C.byref(nm)),
+                "orbg_search_by_projection_lastframe")
+        return nm.value, match

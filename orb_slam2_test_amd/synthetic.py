@@ -131,6 +131,16 @@ def stereo_sequence(n, h, w, seed=DEFAULT_SEED, noise=2, d_min=4.0, d_max=60.0):
     return lefts, rights, disp
 
 
+def sequence_positions(n, seed=DEFAULT_SEED, max_step=8):
+    """(n, 2) canvas offsets (y, x) of sequence(n, ..., seed, max_step): frame t's pixel
+    (x, y) is canvas (x + pos[t, 1], y + pos[t, 0])."""
+    rng = np.random.Generator(np.random.PCG64(seed + 1))
+    steps = rng.integers(-max_step, max_step + 1, size=(n, 2))
+    steps[0] = 0
+    pos = np.cumsum(steps, axis=0)
+    return pos - pos.min(axis=0)
+
+
 def constant(h, w, value=128):
     return np.full((h, w), value, np.uint8)
 
@@ -232,3 +242,62 @@ def ba_window(n_local=10, n_fixed=10, n_points=6000, obs_per_point=4.5, stereo_f
             e["active"] = 1
             edges.append(e)
     return poses, pts, np.array(edges, dtype=EDGE_DTYPE)
+
+
+# ---------------------------------------------------------------------------
+# Tracking-matcher scenes (ORBmatcher::SearchByProjection): map points back-projected
+# from frame t-1's keypoints at a common depth, so a pure camera translation reproduces
+# the sequence's pan (u' = u + fx tx / z) and the matches have a ground truth.
+# ---------------------------------------------------------------------------
+MP_VALID, MP_HAS_OBS = 1, 2
+LF_DTYPE = np.dtype([("x", "<f4"), ("y", "<f4"), ("z", "<f4"), ("octave", "<i4"),
+                     ("angle", "<f4"), ("flags", "<i4")])
+MP_DTYPE = np.dtype([("u", "<f4"), ("v", "<f4"), ("ur", "<f4"), ("level", "<i4"),
+                     ("view_cos", "<f4"), ("flags", "<i4")])
+
+
+def tracking_scene(kps_last, shift_xy, seed=DEFAULT_SEED, depth=10.0, fx=KITTI_FX, fy=KITTI_FY,
+                   cx=KITTI_CX, cy=KITTI_CY, bf=KITTI_BF, tz=0.0, valid_frac=0.9,
+                   obs_frac=0.8):
+    """LastFrame points and camera poses for SearchByProjection(CurrentFrame, LastFrame).
+
+    kps_last: frame t-1 keypoints (KP_DTYPE); shift_xy: image motion (dx, dy) of the scene
+    from t-1 to t.  World = camera t-1 (Tlw = [I | 0]); Tcw = [I | t] with
+    t = (dx z / fx, dy z / fy, tz).  Returns (points LF_DTYPE, Tcw (3, 4), Tlw (3, 4))."""
+    rng = np.random.Generator(np.random.PCG64(seed + 31))
+    n = len(kps_last)
+    z = np.float32(depth)
+    pts = np.zeros(n, LF_DTYPE)
+    pts["x"] = (kps_last["x"] - np.float32(cx)) * z / np.float32(fx)
+    pts["y"] = (kps_last["y"] - np.float32(cy)) * z / np.float32(fy)
+    pts["z"] = z
+    pts["octave"] = kps_last["octave"]
+    pts["angle"] = kps_last["angle"]
+    fl = np.where(rng.random(n) < valid_frac, MP_VALID, 0)
+    fl |= np.where(rng.random(n) < obs_frac, MP_HAS_OBS, 0)
+    pts["flags"] = fl
+    Tlw = np.zeros((3, 4), np.float32)
+    Tlw[:, :3] = np.eye(3)
+    Tcw = Tlw.copy()
+    Tcw[0, 3] = shift_xy[0] * depth / fx
+    Tcw[1, 3] = shift_xy[1] * depth / fy
+    Tcw[2, 3] = tz
+    return pts, Tcw, Tlw
+
+
+def map_projections(kps_src, shift_xy, seed=DEFAULT_SEED, depth=10.0, bf=KITTI_BF, jitter=0.7,
+                    valid_frac=0.9, obs_frac=0.9):
+    """Local-map projections (Frame::isInFrustum outputs) of map points seen at kps_src,
+    moved by shift_xy plus up to +-jitter px: MP_DTYPE records."""
+    rng = np.random.Generator(np.random.PCG64(seed + 37))
+    n = len(kps_src)
+    mp = np.zeros(n, MP_DTYPE)
+    mp["u"] = kps_src["x"] + np.float32(shift_xy[0]) + rng.uniform(-jitter, jitter, n).astype(np.float32)
+    mp["v"] = kps_src["y"] + np.float32(shift_xy[1]) + rng.uniform(-jitter, jitter, n).astype(np.float32)
+    mp["ur"] = mp["u"] - np.float32(bf / depth)
+    mp["level"] = kps_src["octave"]
+    mp["view_cos"] = np.where(rng.random(n) < 0.5, 0.9995, 0.99).astype(np.float32)
+    fl = np.where(rng.random(n) < valid_frac, MP_VALID, 0)
+    fl |= np.where(rng.random(n) < obs_frac, MP_HAS_OBS, 0)
+    mp["flags"] = fl
+    return mp
