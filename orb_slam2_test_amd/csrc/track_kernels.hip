@@ -14,7 +14,8 @@
 //                    the K smallest (distance, grid order, index) keys.  The frame's
 //                    keypoints are counting-sorted by grid column in LDS once per
 //                    workgroup; 16-lane groups, 4 queries per wave at a time.
-//   k_track_resolve  one wave per frame walks the queries in index order over the K-lists
+//   k_track_resolve  one workgroup per frame: wave 0 walks the queries in index order over
+//                    the K-lists in LDS while wave 1 prefetches the next chunk
 //                    (the first two keys whose keypoint is not taken are best / second),
 //                    with an exact wave-parallel rescan when a K-list runs out; then the
 //                    rotation-consistency pass (ComputeThreeMaxima) for the last-frame
@@ -328,132 +329,227 @@ __device__ void track_rescan(const TrackArgs &A, int f, int i, const TrackQuery 
 }
 
 #define TRK_CHUNK 64
+#define TRK_RT 128  // resolver threads: wave 0 resolves, wave 1 prefetches the next chunk
 
-// LDS: chunk lists (u64), chunk counts, misc, match[fc] i32, pushes[qc] i32
-// (index << 8 | bin), taken[fc] u8
+// Resolver LDS (all of the sequential walk's reads are LDS reads):
+//   lists[2][64 * K] u64, cnts[2][64], qinfo[2][64] (angle bits | flags), misc[64],
+//   match[fc] i32, push[qc] i32 (index << 8 | bin), kang[fc] f32 (keypoint angles),
+//   taken[fc] u8, koct[fc] i8, owner[fc] i32 (lowest taking lane of a speculative round)
 __host__ __device__ constexpr size_t track_resolve_lds(int fc, int qc)
 {
-    return (size_t)TRK_CHUNK * ORBG_MATCH_TOPK * 8 + TRK_CHUNK * 4 + 64 * 4 + (size_t)fc * 4 +
-           (size_t)qc * 4 + (size_t)fc;
+    return (size_t)2 * TRK_CHUNK * ORBG_MATCH_TOPK * 8 + 2 * TRK_CHUNK * 4 +
+           2 * TRK_CHUNK * 8 + 64 * 4 + (size_t)fc * 4 + (size_t)qc * 4 + (size_t)fc * 4 +
+           (size_t)fc + (size_t)fc + 4 + (size_t)fc * 4;
 }
 
-// one wave per frame
+// one workgroup (two waves) per frame
 template <int MODE>
-__global__ __launch_bounds__(64) void k_track_resolve(TrackArgs A)
+__global__ __launch_bounds__(TRK_RT) void k_track_resolve(TrackArgs A)
 {
     extern __shared__ __attribute__((aligned(16))) uint8_t trs[];
-    const int f = blockIdx.x, lane = threadIdx.x;
+    const int f = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
     const int n = A.counts[f], nq = A.qcounts[f];
-    unsigned long long *lists = (unsigned long long *)trs;
-    int32_t *cnts = (int32_t *)(lists + TRK_CHUNK * ORBG_MATCH_TOPK);
-    int32_t *misc = cnts + TRK_CHUNK;  // [0] npush, [1] nmatches, [2..31] histogram sizes
+    unsigned long long *lists = (unsigned long long *)trs;          // [2][64 K]
+    int2 *qinfo = (int2 *)(lists + 2 * TRK_CHUNK * ORBG_MATCH_TOPK);  // [2][64]
+    int32_t *cnts = (int32_t *)(qinfo + 2 * TRK_CHUNK);             // [2][64]
+    int32_t *misc = cnts + 2 * TRK_CHUNK;  // [0] npush, [1] nmatches, [2..31] histogram
     int32_t *match = misc + 64;
     int32_t *push = match + A.fc;
-    uint8_t *taken = (uint8_t *)(push + A.qc);
+    float *kang = (float *)(push + A.qc);
+    uint8_t *taken = (uint8_t *)(kang + A.fc);
+    int8_t *koct = (int8_t *)(taken + A.fc);
+    int32_t *owner = (int32_t *)(((uintptr_t)(koct + A.fc) + 3) & ~(uintptr_t)3);
     const uint8_t *t0 = A.taken0 ? A.taken0 + (size_t)f * A.fc : nullptr;
-    for (int i = lane; i < n; i += 64) {
+    const orbg_keypoint *kps = A.kps + (size_t)f * A.fc;
+    for (int i = tid; i < n; i += TRK_RT) {
+        const orbg_keypoint kp = kps[i];
         taken[i] = t0 ? t0[i] : 0;
         match[i] = -1;
+        kang[i] = kp.angle;
+        koct[i] = (int8_t)kp.octave;
+        owner[i] = 64;
     }
-    misc[lane] = 0;
-    wave_sync_lds();
+    if (tid < 64) misc[tid] = 0;
     bool fwd = false, bwd = false;
     if (MODE == TRK_LASTFRAME) track_direction(A.cams[f], &fwd, &bwd);
-    const orbg_keypoint *kps = A.kps + (size_t)f * A.fc;
     const orbg_bounds b = A.bounds[f];
     const float factor = 1.0f / HISTO_LENGTH;
 
-    // lane 0: the loop body's state update once best / second are known
-    auto apply = [&](int i, unsigned long long k1, unsigned long long k2) {
-        if (k1 == ~0ull) return;
-        const int bestDist = (int)(k1 >> 32), bestIdx = (int)(k1 & 0xFFFFF);
-        if (bestDist > TH_HIGH) return;
-        bool has_obs;
-        if (MODE == TRK_LOCAL) {
-            // ORBmatcher.cc:131-139: ratio only between matches of the same level
-            const int bestLevel = kps[bestIdx].octave;
-            const int bestDist2 = k2 == ~0ull ? 256 : (int)(k2 >> 32);
-            const int bestLevel2 = k2 == ~0ull ? -1 : kps[(int)(k2 & 0xFFFFF)].octave;
-            if (bestLevel == bestLevel2 && bestDist > A.nnratio * bestDist2) return;
-            has_obs = (((const orbg_map_projection *)A.q)[(size_t)f * A.qc + i].flags &
-                       ORBG_MP_HAS_OBS) != 0;
-        } else {
-            const orbg_lastframe_point P =
-                ((const orbg_lastframe_point *)A.q)[(size_t)f * A.qc + i];
-            has_obs = (P.flags & ORBG_MP_HAS_OBS) != 0;
-            if (A.check_ori) {
-                // ORBmatcher.cc:1633-1642
-                float rot = P.angle - kps[bestIdx].angle;
-                if (rot < 0.0) rot += 360.0f;
-                int bin = (int)roundf(rot * factor);
-                if (bin == HISTO_LENGTH) bin = 0;
-                push[misc[0]++] = bestIdx << 8 | bin;
-                misc[2 + bin]++;
+    // wave 1: chunk c's counts, K-lists and query info into buffer c & 1
+    auto prefetch = [&](int c) {
+        const int c0 = c * TRK_CHUNK;
+        if (c0 >= nq) return;
+        const int cn = min(TRK_CHUNK, nq - c0);
+        const int bf = c & 1;
+        const int t = lane < cn ? A.topn[(size_t)f * A.qc + c0 + lane] : -1;
+        cnts[bf * TRK_CHUNK + lane] = t;
+        if (__ballot(t > 0) == 0ull) return;
+        int2 qi = make_int2(0, 0);
+        if (lane < cn) {
+            if (MODE == TRK_LASTFRAME) {
+                const orbg_lastframe_point P =
+                    ((const orbg_lastframe_point *)A.q)[(size_t)f * A.qc + c0 + lane];
+                qi = make_int2(__float_as_int(P.angle), P.flags);
+            } else {
+                qi.y = ((const orbg_map_projection *)A.q)[(size_t)f * A.qc + c0 + lane].flags;
             }
         }
-        match[bestIdx] = i;
-        taken[bestIdx] = has_obs ? 1 : 0;
-        misc[1]++;
-    };
-
-    for (int c0 = 0; c0 < nq; c0 += TRK_CHUNK) {
-        const int cn = min(TRK_CHUNK, nq - c0);
-        const int t = lane < cn ? A.topn[(size_t)f * A.qc + c0 + lane] : -1;
-        cnts[lane] = t;
-        if (__ballot(t > 0) == 0ull) continue;
+        qinfo[bf * TRK_CHUNK + lane] = qi;
+        unsigned long long e[ORBG_MATCH_TOPK];
 #pragma unroll
         for (int u = 0; u < ORBG_MATCH_TOPK; u++) {
-            const int e = u * 64 + lane;
-            lists[e] = e < cn * ORBG_MATCH_TOPK
-                           ? A.topk[((size_t)f * A.qc + c0) * ORBG_MATCH_TOPK + e]
-                           : ~0ull;
+            const int k = u * 64 + lane;
+            e[u] = k < cn * ORBG_MATCH_TOPK
+                       ? A.topk[((size_t)f * A.qc + c0) * ORBG_MATCH_TOPK + k]
+                       : ~0ull;
         }
-        wave_sync_lds();
-        int qi = 0;
-        while (qi < cn) {
-            int q = qi, fb = 0;
-            if (lane == 0) {
-                for (; q < cn; q++) {
-                    const int total = cnts[q];
-                    if (total <= 0) continue;
-                    const int kk = min(total, ORBG_MATCH_TOPK);
-                    const unsigned long long *lst = &lists[q * ORBG_MATCH_TOPK];
-                    unsigned long long k1 = ~0ull, k2 = ~0ull;
-                    int found = 0;
-                    for (int k = 0; k < kk && found < 2; k++) {
-                        const unsigned long long e = lst[k];
-                        if (taken[(int)(e & 0xFFFFF)]) continue;
-                        if (found == 0) k1 = e; else k2 = e;
-                        found++;
+#pragma unroll
+        for (int u = 0; u < ORBG_MATCH_TOPK; u++)
+            lists[bf * TRK_CHUNK * ORBG_MATCH_TOPK + u * 64 + lane] = e[u];
+    };
+
+    // wave 0's running counts (the rotation histogram is built from the push list)
+    int npush = 0, nmatch = 0;
+
+    if (wv == 1) prefetch(0);
+    __syncthreads();
+    const int nchunks = (nq + TRK_CHUNK - 1) / TRK_CHUNK;
+    for (int c = 0; c < nchunks; c++) {
+        if (wv == 1) {
+            prefetch(c + 1);
+        } else {
+            const int c0 = c * TRK_CHUNK, cn = min(TRK_CHUNK, nq - c0), bf = c & 1;
+            const int *cnt = cnts + bf * TRK_CHUNK;
+            const unsigned long long *lst0 = lists + bf * TRK_CHUNK * ORBG_MATCH_TOPK;
+            const int2 *qin = qinfo + bf * TRK_CHUNK;
+            // Speculative parallel walk, one query per lane.  Every pending lane picks
+            // best / second from its K-list against the current taken state; a lane's
+            // picks are exact unless an earlier pending lane takes (has_obs) a keypoint at
+            // or before its last consulted list position.  owner[idx] = lowest taking lane
+            // finds the first such lane l*; lanes below l* (and below the first lane whose
+            // K-list ran out) commit in lane order, the rest go again.  Same result as the
+            // in-order loop, typically in one or two rounds per chunk.
+            const int need = MODE == TRK_LOCAL ? 2 : 1;
+            const int qidx = c0 + lane;
+            const int total = lane < cn ? cnt[lane] : 0;
+            const int2 qv = qin[lane];
+            unsigned long long e[ORBG_MATCH_TOPK];
+#pragma unroll
+            for (int k = 0; k < ORBG_MATCH_TOPK; k++) e[k] = lst0[lane * ORBG_MATCH_TOPK + k];
+            const int kk = min(total, ORBG_MATCH_TOPK);
+            unsigned long long pending = __ballot(total > 0);
+            while (pending) {
+                const bool pend = (pending >> lane) & 1ull;
+                unsigned long long k1 = ~0ull, k2 = ~0ull;
+                int found = 0, lastpos = kk - 1;
+#pragma unroll
+                for (int k = 0; k < ORBG_MATCH_TOPK; k++) {
+                    if (!pend || k >= kk || found >= need) continue;
+                    if (taken[(int)(e[k] & 0xFFFFF)]) continue;
+                    if (found == 0) k1 = e[k]; else k2 = e[k];
+                    if (++found == need) lastpos = k;
+                }
+                const bool resc = pend && found < need && total > ORBG_MATCH_TOPK;
+                // the loop body's decision (ORBmatcher.cc:1623-1625 / 129-139)
+                bool app = false;
+                int bestIdx = 0, bin = 0;
+                if (pend && !resc && k1 != ~0ull && (int)(k1 >> 32) <= TH_HIGH) {
+                    bestIdx = (int)(k1 & 0xFFFFF);
+                    app = true;
+                    if (MODE == TRK_LOCAL) {
+                        const int bestDist2 = k2 == ~0ull ? 256 : (int)(k2 >> 32);
+                        const int o2 = k2 == ~0ull ? -1 : koct[(int)(k2 & 0xFFFFF)];
+                        if (koct[bestIdx] == o2 && (int)(k1 >> 32) > A.nnratio * bestDist2)
+                            app = false;
+                    } else if (A.check_ori) {
+                        float rot = __int_as_float(qv.x) - kang[bestIdx];
+                        if (rot < 0.0) rot += 360.0f;
+                        bin = (int)roundf(rot * factor);
+                        if (bin == HISTO_LENGTH) bin = 0;
                     }
-                    // the last-frame search needs only the best
-                    const int need = MODE == TRK_LOCAL ? 2 : 1;
-                    if (found < need && total > ORBG_MATCH_TOPK) {
-                        fb = 1;
-                        break;
+                }
+                const bool takes = app && (qv.y & ORBG_MP_HAS_OBS);
+                if (takes) atomicMin(&owner[bestIdx], lane);
+                wave_sync_lds();
+                bool conf = false;
+#pragma unroll
+                for (int k = 0; k < ORBG_MATCH_TOPK; k++)
+                    if (pend && k < kk && k <= lastpos && owner[(int)(e[k] & 0xFFFFF)] < lane)
+                        conf = true;
+                const unsigned long long cm = __ballot(conf), rm = __ballot(resc);
+                const int lc = cm ? __builtin_ctzll(cm) : 64, lr = rm ? __builtin_ctzll(rm) : 64;
+                const int lstar = min(lc, lr);
+                const unsigned long long below = lstar >= 64 ? ~0ull : ((1ull << lstar) - 1ull);
+                const bool commit = pend && lane < lstar;
+                if (takes) owner[bestIdx] = 64;
+                if (commit && app) {
+                    atomicMax(&match[bestIdx], qidx);  // later query overwrites: larger index
+                    if (takes) taken[bestIdx] = 1;
+                }
+                const unsigned long long am = __ballot(commit && app);
+                if (MODE == TRK_LASTFRAME && A.check_ori && commit && app) {
+                    const int pos = __builtin_amdgcn_mbcnt_hi(
+                        (uint32_t)(am >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)am, 0));
+                    push[npush + pos] = bestIdx << 8 | bin;
+                }
+                npush += (MODE == TRK_LASTFRAME && A.check_ori) ? __popcll(am) : 0;
+                nmatch += __popcll(am);
+                pending &= ~below;
+                wave_sync_lds();
+                if (lr < 64 && lr == lstar) {
+                    // K-list exhausted: exact rescan of query lr against the committed state
+                    const TrackQuery Q = track_query<MODE>(A, f, c0 + lr, fwd, bwd, b);
+                    unsigned long long r1, r2;
+                    track_rescan<MODE>(A, f, c0 + lr, Q, taken, &r1, &r2);
+                    const int qy = __shfl(qv.y, lr, 64), qx = __shfl(qv.x, lr, 64);
+                    if (lane == 0 && r1 != ~0ull && (int)(r1 >> 32) <= TH_HIGH) {
+                        const int bi = (int)(r1 & 0xFFFFF);
+                        bool ok = true;
+                        int bn = 0;
+                        if (MODE == TRK_LOCAL) {
+                            const int bestDist2 = r2 == ~0ull ? 256 : (int)(r2 >> 32);
+                            const int o2 = r2 == ~0ull ? -1 : koct[(int)(r2 & 0xFFFFF)];
+                            if (koct[bi] == o2 && (int)(r1 >> 32) > A.nnratio * bestDist2) ok = false;
+                        } else if (A.check_ori) {
+                            float rot = __int_as_float(qx) - kang[bi];
+                            if (rot < 0.0) rot += 360.0f;
+                            bn = (int)roundf(rot * factor);
+                            if (bn == HISTO_LENGTH) bn = 0;
+                        }
+                        if (ok) {
+                            match[bi] = max(match[bi], c0 + lr);
+                            if (qy & ORBG_MP_HAS_OBS) taken[bi] = 1;
+                            if (MODE == TRK_LASTFRAME && A.check_ori) push[npush] = bi << 8 | bn;
+                            misc[63] = 1;
+                        } else {
+                            misc[63] = 0;
+                        }
+                    } else if (lane == 0) {
+                        misc[63] = 0;
                     }
-                    apply(c0 + q, k1, k2);
+                    wave_sync_lds();
+                    const int ap = misc[63];
+                    npush += (MODE == TRK_LASTFRAME && A.check_ori) ? ap : 0;
+                    nmatch += ap;
+                    pending &= ~(1ull << lr);
+                    wave_sync_lds();
                 }
             }
-            q = __shfl(q, 0, 64);
-            fb = __shfl(fb, 0, 64);
-            wave_sync_lds();
-            qi = q;
-            if (fb) {
-                const int i = c0 + qi;
-                const TrackQuery Q = track_query<MODE>(A, f, i, fwd, bwd, b);
-                unsigned long long k1, k2;
-                track_rescan<MODE>(A, f, i, Q, taken, &k1, &k2);
-                if (lane == 0) apply(i, k1, k2);
-                wave_sync_lds();
-                qi++;
-            }
         }
+        __syncthreads();
     }
+    if (tid == 0) {
+        misc[0] = npush;
+        misc[1] = nmatch;
+    }
+    __syncthreads();
     int nm = misc[1];
     if (MODE == TRK_LASTFRAME && A.check_ori) {
-        // ComputeThreeMaxima (:1800-1841), then every push in a dropped bin NULLs its slot
-        // and decrements nmatches (:1651-1663)
+        // rotation histogram of the pushes, ComputeThreeMaxima (:1800-1841), then every
+        // push in a dropped bin NULLs its slot and decrements nmatches (:1651-1663)
+        const int np = misc[0];
+        for (int k = tid; k < np; k += TRK_RT) atomicAdd(&misc[2 + (push[k] & 0xFF)], 1);
+        __syncthreads();
         int ind1 = -1, ind2 = -1, ind3 = -1;
         {
             int max1 = 0, max2 = 0, max3 = 0;
@@ -477,21 +573,23 @@ __global__ __launch_bounds__(64) void k_track_resolve(TrackArgs A)
                 ind3 = -1;
             }
         }
-        const int np = misc[0];
         int removed = 0;
-        for (int k = lane; k < np; k += 64) {
+        for (int k = tid; k < np; k += TRK_RT) {
             const int e = push[k], bn = e & 0xFF;
             if (bn != ind1 && bn != ind2 && bn != ind3) {
                 match[e >> 8] = -1;  // same value from every writer: no ordering needed
                 removed++;
             }
         }
-        nm -= wave_isum(removed);
-        wave_sync_lds();
+        removed = wave_isum(removed);
+        __shared__ int rem[2];
+        if (lane == 0) rem[wv] = removed;
+        __syncthreads();
+        nm -= rem[0] + rem[1];
     }
     int32_t *mo = A.match + (size_t)f * A.fc;
-    for (int i = lane; i < n; i += 64) mo[i] = match[i];
-    if (lane == 0) A.nmatches[f] = nm;
+    for (int i = tid; i < n; i += TRK_RT) mo[i] = match[i];
+    if (tid == 0) A.nmatches[f] = nm;
 }
 
 #define PL(prof, st, name, launch)                                    \
@@ -521,7 +619,7 @@ int launch_track(hipStream_t st, int mode, const TrackArgs &A, int nframes, void
            hipLaunchKernelGGL(k_track_cands<TRK_LASTFRAME>, dim3(nbx * nframes), dim3(256), l1,
                               st, A));
         PL(prof, st, "track_resolve",
-           hipLaunchKernelGGL(k_track_resolve<TRK_LASTFRAME>, dim3(nframes), dim3(64), l2, st,
+           hipLaunchKernelGGL(k_track_resolve<TRK_LASTFRAME>, dim3(nframes), dim3(TRK_RT), l2, st,
                               A));
     } else {
         hipFuncSetAttribute((const void *)k_track_cands<TRK_LOCAL>,
@@ -532,7 +630,7 @@ int launch_track(hipStream_t st, int mode, const TrackArgs &A, int nframes, void
            hipLaunchKernelGGL(k_track_cands<TRK_LOCAL>, dim3(nbx * nframes), dim3(256), l1, st,
                               A));
         PL(prof, st, "track_resolve",
-           hipLaunchKernelGGL(k_track_resolve<TRK_LOCAL>, dim3(nframes), dim3(64), l2, st, A));
+           hipLaunchKernelGGL(k_track_resolve<TRK_LOCAL>, dim3(nframes), dim3(TRK_RT), l2, st, A));
     }
     return hipGetLastError() == hipSuccess ? ORBG_OK : ORBG_EIO;
 }
