@@ -42,7 +42,8 @@ void prof_end(void *prof, hipStream_t s, const char *n, hipEvent_t a);
 
 #define TH_HIGH 100
 #define HISTO_LENGTH 30
-#define TRK_QPW 16  // queries per wave in k_track_cands (4 x 4 in 16-lane groups)
+#define TRK_QPW 32  // queries per wave in k_track_cands (8 x 4 in 16-lane groups)
+#define TRK_NB (ORBG_MAX_LEVELS * ORBG_GRID_COLS)  // (octave, column) buckets
 
 // cv::gemm small-matrix pin (see oracle/track_oracle.c orc_gemm3): double work type, one
 // rounding per element.  R = 3x3 block of a 3x4 row-major matrix.
@@ -167,8 +168,10 @@ template <int MODE>
 __global__ __launch_bounds__(256) void k_track_cands(TrackArgs A)
 {
     extern __shared__ __attribute__((aligned(16))) TKey fk[];
-    __shared__ int colstart[ORBG_GRID_COLS + 1];
-    __shared__ int cursor[ORBG_GRID_COLS];
+    // bucket = octave * 64 + grid column: a query scans only its level range's columns
+    __shared__ int colstart[TRK_NB + 1];
+    __shared__ int cursor[TRK_NB];
+    __shared__ int wsum[4];
     const int nbx = (A.qc + 4 * TRK_QPW - 1) / (4 * TRK_QPW);
     const int id = xcd_remap(blockIdx.x, gridDim.x);
     const int f = id / nbx, bx = id - f * nbx;
@@ -180,31 +183,45 @@ __global__ __launch_bounds__(256) void k_track_cands(TrackArgs A)
     const GridPrm g = grid_prm(b);
     const orbg_keypoint *kps = A.kps + (size_t)f * A.fc;
     const float *urf = A.uright ? A.uright + (size_t)f * A.fc : nullptr;
-    // counting sort by PosInGrid column (Frame.cc:510-520); keypoints outside the grid are
-    // in no cell and never candidates
-    if (tid <= ORBG_GRID_COLS) colstart[tid] = 0;
+    // counting sort by (octave, PosInGrid column) (Frame.cc:510-520); keypoints outside
+    // the grid are in no cell and never candidates
+    for (int i = tid; i <= TRK_NB; i += 256) colstart[i] = 0;
+    __syncthreads();
+    auto bucket = [&](const orbg_keypoint &kp) -> int {
+        const int px = (int)roundf((kp.x - g.min_x) * g.inv_w);
+        const int py = (int)roundf((kp.y - g.min_y) * g.inv_h);
+        if (px < 0 || px >= ORBG_GRID_COLS || py < 0 || py >= ORBG_GRID_ROWS) return -1;
+        return min(max(kp.octave, 0), ORBG_MAX_LEVELS - 1) * ORBG_GRID_COLS + px;
+    };
+    for (int i = tid; i < n; i += 256) {
+        const int bk = bucket(kps[i]);
+        if (bk >= 0) atomicAdd(&colstart[bk + 1], 1);
+    }
+    __syncthreads();
+    {
+        // inclusive scan of colstart[1..TRK_NB]: 4 consecutive buckets per thread
+        int v[4], run = 0;
+#pragma unroll
+        for (int k = 0; k < 4; k++) {
+            run += colstart[1 + 4 * tid + k];
+            v[k] = run;
+        }
+        const int incl = wave_incl_scan(run);
+        if (lane == 63) wsum[wv] = incl;
+        __syncthreads();
+        int base = incl - run;
+        for (int w2 = 0; w2 < wv; w2++) base += wsum[w2];
+#pragma unroll
+        for (int k = 0; k < 4; k++) colstart[1 + 4 * tid + k] = base + v[k];
+    }
+    __syncthreads();
+    for (int i = tid; i < TRK_NB; i += 256) cursor[i] = colstart[i];
     __syncthreads();
     for (int i = tid; i < n; i += 256) {
         const orbg_keypoint kp = kps[i];
-        const int px = (int)roundf((kp.x - g.min_x) * g.inv_w);
-        const int py = (int)roundf((kp.y - g.min_y) * g.inv_h);
-        if (px >= 0 && px < ORBG_GRID_COLS && py >= 0 && py < ORBG_GRID_ROWS)
-            atomicAdd(&colstart[px + 1], 1);
-    }
-    __syncthreads();
-    if (wv == 0) {
-        const int c = colstart[lane + 1];
-        colstart[lane + 1] = wave_incl_scan(c);
-    }
-    __syncthreads();
-    if (tid < ORBG_GRID_COLS) cursor[tid] = colstart[tid];
-    __syncthreads();
-    for (int i = tid; i < n; i += 256) {
-        const orbg_keypoint kp = kps[i];
-        const int px = (int)roundf((kp.x - g.min_x) * g.inv_w);
-        const int py = (int)roundf((kp.y - g.min_y) * g.inv_h);
-        if (px >= 0 && px < ORBG_GRID_COLS && py >= 0 && py < ORBG_GRID_ROWS)
-            fk[atomicAdd(&cursor[px], 1)] =
+        const int bk = bucket(kp);
+        if (bk >= 0)
+            fk[atomicAdd(&cursor[bk], 1)] =
                 TKey{kp.x, kp.y, (uint32_t)i | (uint32_t)kp.octave << 24, urf ? urf[i] : 0.f};
     }
     __syncthreads();
@@ -239,8 +256,13 @@ __global__ __launch_bounds__(256) void k_track_cands(TrackArgs A)
                 qd[0] = a.x; qd[1] = a.y; qd[2] = a.z; qd[3] = a.w;
                 qd[4] = c.x; qd[5] = c.y; qd[6] = c.z; qd[7] = c.w;
             }
-            if (!w.empty) {
-                const int j0 = colstart[w.cx0], j1 = colstart[w.cx1 + 1];
+            // levels GetFeaturesInArea can return (bCheckLevels, :475-482)
+            const bool chk = Q.minL > 0 || Q.maxL >= 0;
+            const int lv0 = chk ? max(Q.minL, 0) : 0;
+            const int lv1 = (chk && Q.maxL >= 0) ? min(Q.maxL, ORBG_MAX_LEVELS - 1) : ORBG_MAX_LEVELS - 1;
+            for (int lv = lv0; !w.empty && lv <= lv1; lv++) {
+                const int j0 = colstart[lv * ORBG_GRID_COLS + w.cx0];
+                const int j1 = colstart[lv * ORBG_GRID_COLS + w.cx1 + 1];
                 for (int j = j0 + sub; j < j1; j += 16) {
                     const TKey k = fk[j];
                     const int ord = cand_order(g, w, k.x, k.y);
