@@ -411,13 +411,15 @@ struct ResolveShared {
     uint16_t *mdist;
     int16_t *m21, *m12;
     int8_t *hbin;
+    int32_t *owner;  // lowest applying lane of a speculative round (64 = none)
 };
 
 #define RESOLVE_FIXED_BYTES (2 * RESOLVE_CHUNK * ORBG_MATCH_TOPK * 8 + 2 * RESOLVE_CHUNK * 4 + 32 * 4 + 16)
 
 __host__ __device__ constexpr size_t resolve_lds_bytes(int cap)
 {
-    return RESOLVE_FIXED_BYTES + (size_t)cap * 8 + (((size_t)cap * 7 + 15) & ~(size_t)15);
+    return RESOLVE_FIXED_BYTES + (size_t)cap * 8 + (((size_t)cap * 7 + 15) & ~(size_t)15) +
+           (size_t)cap * 4;
 }
 
 __device__ __forceinline__ ResolveShared resolve_layout(uint8_t *base, int cap)
@@ -438,6 +440,7 @@ __device__ __forceinline__ ResolveShared resolve_layout(uint8_t *base, int cap)
     S.m21 = (int16_t *)(S.mdist + cap);
     S.m12 = S.m21 + cap;
     S.hbin = (int8_t *)(S.m12 + cap);
+    S.owner = (int32_t *)(base + (((size_t)cap * 7 + 15) & ~(size_t)15));
     return S;
 }
 
@@ -503,6 +506,7 @@ __device__ void init_resolve_block(ResolveShared &S, int cap, const orbg_keypoin
                 S.mdist[i] = 0xFFFF;
                 S.m21[i] = -1;
                 S.ang2[i] = a[u];
+                S.owner[i] = 64;
             }
         }
     }
@@ -574,79 +578,93 @@ __device__ void init_resolve_block(ResolveShared &S, int cap, const orbg_keypoin
         if (wv == 1) {
             prefetch(c + 1);
         } else {
+            // Speculative parallel walk, one query per lane (see track_kernels.hip): each
+            // pending lane picks best / second from its K-list against the current
+            // vMatchedDistance; a pick is exact unless an earlier pending lane that applies
+            // rewrites vMatchedDistance of a keypoint at or before the lane's last consulted
+            // list position.  owner[i2] (lowest applying lane) finds the first such lane l*;
+            // lanes below l* and below the first exhausted K-list commit (their best
+            // keypoints are distinct, so their steals and writes are independent), the rest
+            // go again.
             const int c0 = c * RESOLVE_CHUNK, cn = min(RESOLVE_CHUNK, n1c - c0);
             const int *cnt = S.chunkn[c & 1];
             const unsigned long long *lists = S.chunk[c & 1];
-            int qi = 0;
-            while (qi < cn) {
-                int q = qi, fb = 0;
-                if (lane == 0) {
-                    for (; q < cn; q++) {
-                        const int total = cnt[q];
-                        if (total <= 0) continue;  // octave > 0 (-1) or empty window (0)
-                        const int kk = min(total, ORBG_MATCH_TOPK);
-                        const unsigned long long *lst = &lists[q * ORBG_MATCH_TOPK];
-                        // first three entries and their filter state in flight together
-                        const unsigned long long e0 = lst[0], e1 = lst[1], e2 = lst[2];
-                        const int md0 = S.mdist[kk > 0 ? (int)(e0 & 0xFFFFF) : 0];
-                        const int md1 = S.mdist[kk > 1 ? (int)(e1 & 0xFFFFF) : 0];
-                        const int md2 = S.mdist[kk > 2 ? (int)(e2 & 0xFFFFF) : 0];
-                        int found = 0, bd = INT_MAX, bd2 = INT_MAX, bi = -1;
-                        const unsigned long long ev[3] = {e0, e1, e2};
-                        const int mv[3] = {md0, md1, md2};
+            const int total = lane < cn ? cnt[lane] : 0;
+            unsigned long long e[ORBG_MATCH_TOPK];
 #pragma unroll
-                        for (int k = 0; k < 3; k++) {
-                            if (k < kk && found < 2) {
-                                const int d = (int)(ev[k] >> 32);
-                                if (!(mv[k] <= d)) {
-                                    if (found == 0) {
-                                        bd = d;
-                                        bi = (int)(ev[k] & 0xFFFFF);
-                                    } else {
-                                        bd2 = d;
-                                    }
-                                    found++;
-                                }
-                            }
-                        }
-                        for (int k = 3; k < kk && found < 2; k++) {
-                            const unsigned long long e = lst[k];
-                            const int d = (int)(e >> 32), i2 = (int)(e & 0xFFFFF);
-                            if (!((int)S.mdist[i2] <= d)) {
-                                if (found == 0) {
-                                    bd = d;
-                                    bi = i2;
-                                } else {
-                                    bd2 = d;
-                                }
-                                found++;
-                            }
-                        }
-                        if (found < 2 && total > ORBG_MATCH_TOPK) {
-                            fb = 1;  // the sorted K-list cannot decide: exact rescan
-                            break;
-                        }
-                        apply(c0 + q, bd, bd2, bi);
+            for (int k = 0; k < ORBG_MATCH_TOPK; k++) e[k] = lists[lane * ORBG_MATCH_TOPK + k];
+            const int kk = min(total, ORBG_MATCH_TOPK);
+            const int i1 = c0 + lane;
+            unsigned long long pending = __ballot(total > 0);
+            while (pending) {
+                const bool pend = (pending >> lane) & 1ull;
+                int found = 0, bd = INT_MAX, bd2 = INT_MAX, bi = -1, lastpos = kk - 1;
+#pragma unroll
+                for (int k = 0; k < ORBG_MATCH_TOPK; k++) {
+                    if (!pend || k >= kk || found >= 2) continue;
+                    const int d = (int)(e[k] >> 32), i2 = (int)(e[k] & 0xFFFFF);
+                    if ((int)S.mdist[i2] <= d) continue;
+                    if (found == 0) {
+                        bd = d;
+                        bi = i2;
+                    } else {
+                        bd2 = d;
+                    }
+                    if (++found == 2) lastpos = k;
+                }
+                const bool resc = pend && found < 2 && total > ORBG_MATCH_TOPK;
+                const bool app = pend && !resc && bd <= TH_LOW && bd < (float)bd2 * nnratio;
+                if (app) atomicMin(&S.owner[bi], lane);
+                wave_sync_lds();
+                bool conf = false;
+#pragma unroll
+                for (int k = 0; k < ORBG_MATCH_TOPK; k++)
+                    if (pend && k < kk && k <= lastpos && S.owner[(int)(e[k] & 0xFFFFF)] < lane)
+                        conf = true;
+                const unsigned long long cm = __ballot(conf), rm = __ballot(resc);
+                const int lc = cm ? __builtin_ctzll(cm) : 64, lr = rm ? __builtin_ctzll(rm) : 64;
+                const int lstar = min(lc, lr);
+                const unsigned long long below = lstar >= 64 ? ~0ull : ((1ull << lstar) - 1ull);
+                const bool commit = app && lane < lstar;
+                if (app) S.owner[bi] = 64;
+                bool stole = false;
+                if (commit) {
+                    const int old = S.m21[bi];
+                    if (old >= 0) {
+                        S.m12[old] = -1;
+                        stole = true;
+                    }
+                    S.m12[i1] = (int16_t)bi;
+                    S.m21[bi] = (int16_t)i1;
+                    S.mdist[bi] = (uint16_t)bd;
+                    if (check_ori) {
+                        float rot = S.ang1[i1] - S.ang2[bi];
+                        if (rot < 0.0f) rot += 360.0f;
+                        int bin = (int)roundf(rot * factor);
+                        if (bin == HISTO_LENGTH) bin = 0;
+                        S.hbin[i1] = (int8_t)bin;
+                        atomicAdd(&S.hsize[bin], 1);
                     }
                 }
-                q = __shfl(q, 0, 64);
-                fb = __shfl(fb, 0, 64);
+                const int delta = __popcll(__ballot(commit)) - __popcll(__ballot(stole));
+                if (lane == 0) *S.nmp += delta;
+                pending &= ~below;
                 wave_sync_lds();
-                qi = q;
-                if (fb) {
-                    const int i1 = c0 + qi;
-                    const float px = prev[(size_t)i1 * prev_stride];
-                    const float py = prev[(size_t)i1 * prev_stride + 1];
+                if (lr < 64 && lr == lstar) {
+                    // K-list exhausted: exact rescan of query c0 + lr against the committed state
+                    const int q1 = c0 + lr;
+                    const float px = prev[(size_t)q1 * prev_stride];
+                    const float py = prev[(size_t)q1 * prev_stride + 1];
                     const Window w = make_window(g, px, py, (float)window);
                     uint32_t qd[8];
-                    const uint32_t *qp = (const uint32_t *)(d1 + (size_t)i1 * 32);
+                    const uint32_t *qp = (const uint32_t *)(d1 + (size_t)q1 * 32);
 #pragma unroll
                     for (int k = 0; k < 8; k++) qd[k] = qp[k];
                     int bestDist, bestDist2, bestIdx2;
                     rescan(k2, d2, n2c, g, w, qd, S.mdist, &bestDist, &bestDist2, &bestIdx2);
-                    if (lane == 0) apply(i1, bestDist, bestDist2, bestIdx2);
+                    if (lane == 0) apply(q1, bestDist, bestDist2, bestIdx2);
+                    pending &= ~(1ull << lr);
                     wave_sync_lds();
-                    qi++;
                 }
             }
         }
