@@ -737,6 +737,8 @@ static void pinned_sincos(double x, double *s, double *c)
     }
 }
 
+void orc_pinned_sincos_d(double x, double *s, double *c) { pinned_sincos(x, s, c); }
+
 void orc_pinned_sincos_deg(float angle_deg, float *c, float *s)
 {
     const float factorPI = (float)(3.14159265358979323846 / 180.f);

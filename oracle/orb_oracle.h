@@ -18,6 +18,7 @@
  *   Frame grid / GetFeaturesInArea .. src/Frame.cc:292-307, 421-520
  *   Frame::ComputeStereoMatches ..... src/Frame.cc:619-834 (stereo_oracle.c)
  *   ORBmatcher::SearchByProjection .. src/ORBmatcher.cc:1503-1667, 59-154 (track_oracle.c)
+ *   Optimizer::PoseOptimization ..... src/Optimizer.cc:356-631 + g2o LM / LDLT (pose_oracle.c)
  *   g2o edge arithmetic (double) .... Thirdparty/g2o/g2o/types/types_six_dof_expmap.{h,cpp},
  *                                     core/base_binary_edge.hpp:55-120, core/base_edge.h:58-102,
  *                                     core/robust_kernel_impl.cpp:65-91
@@ -180,6 +181,31 @@ int orc_search_by_projection_local(const orc_keypoint *kps, const uint8_t *desc,
                                    const orc_bounds *b, const float *scale_factors,
                                    const orc_map_proj *mps, const uint8_t *mdesc, int nm,
                                    float th, float nnratio, int32_t *match);
+
+/* ---- Optimizer::PoseOptimization (pose_oracle.c) ---- */
+/* one EdgeSE3ProjectXYZOnlyPose (stereo = 0) / EdgeStereoSE3ProjectXYZOnlyPose (1) */
+typedef struct {
+    float obs[3];       /* kpUn.pt.x, kpUn.pt.y, mvuRight[i] */
+    float xw[3];        /* pMP->GetWorldPos() */
+    float inv_sigma2;   /* mvInvLevelSigma2[kpUn.octave] */
+    int32_t stereo;     /* mvuRight[i] >= 0 */
+} orc_pose_edge;
+
+typedef struct {
+    float fx, fy, cx, cy, bf;  /* Frame::fx .. mbf */
+    float pad;
+} orc_pose_cam;
+
+/* edges: the frame's keypoints with a MapPoint, in index order.  Tcw_in: pFrame->mTcw
+ * (3x4 row-major float).  Outputs: the optimised SE3Quat (q x,y,z,w; t), its cv::Mat form
+ * (Converter::toCvMat) and mvbOutlier per edge.  Returns nInitialCorrespondences - nBad. */
+int orc_pose_optimization(const orc_pose_edge *edges, int n, const orc_pose_cam *cam,
+                          const float Tcw_in[12], double q_out[4], double t_out[3],
+                          float Tcw_out[12], uint8_t *outlier);
+void orc_se3_from_tcw(const float Tcw[12], double q[4], double t[3]);
+void orc_se3_to_tcw(const double q[4], const double t[3], float Tcw[12]);
+void orc_se3_oplus(double q[4], double t[3], const double upd[6]);
+int orc_ldlt_solve6(const double H[6][6], const double b[6], double x[6]);
 
 /* ---- Frame::ComputeStereoMatches (stereo_oracle.c) ----
  * kl/dl: left keypoints (mvKeys) + descriptors, kr/dr: right.  pyr_l / pyr_r: the two

@@ -47,6 +47,15 @@ class Params(C.Structure):
                 ("resize_mode", C.c_int32), ("gauss_k", C.c_int32 * 7), ("brief_fma", C.c_int32)]
 
 
+PEDGE_DTYPE = np.dtype([("obs", "<f4", 3), ("xw", "<f4", 3), ("inv_sigma2", "<f4"),
+                        ("stereo", "<i4")])
+
+
+class PoseCam(C.Structure):
+    _fields_ = [("fx", C.c_float), ("fy", C.c_float), ("cx", C.c_float), ("cy", C.c_float),
+                ("bf", C.c_float), ("pad", C.c_float)]
+
+
 class TrackCam(C.Structure):
     _fields_ = [("Tcw", C.c_float * 12), ("Tlw", C.c_float * 12), ("fx", C.c_float),
                 ("fy", C.c_float), ("cx", C.c_float), ("cy", C.c_float), ("bf", C.c_float),
@@ -121,6 +130,8 @@ def lib():
         L.orc_stereo_matches.argtypes = [P(Params), vp, vp, C.c_int, vp, vp, C.c_int, vp, vp,
                                          C.c_int, C.c_int, C.c_float, C.c_float, vp, vp]
         L.orc_track_direction.argtypes = [vp, vp, vp]
+        L.orc_pose_optimization.argtypes = [vp, C.c_int, vp, vp, vp, vp, vp, vp]
+        L.orc_se3_from_tcw.argtypes = [vp, vp, vp]
         L.orc_search_by_projection_lastframe.argtypes = [vp, vp, vp, C.c_int, vp, vp, vp, vp,
                                                          vp, C.c_int, vp, C.c_float, C.c_int,
                                                          vp]
@@ -353,3 +364,19 @@ def ba_numeric_jacobian(pose, xyz, edge):
     jt = np.zeros((3, 6))
     lib().orc_ba_numeric_jacobian(_p(pose), _p(xyz), _p(edge), _p(jp), _p(jt))
     return jp, jt
+
+
+def pose_optimization(edges, cam, Tcw):
+    """Optimizer::PoseOptimization restated (oracle/pose_oracle.c).  edges: PEDGE_DTYPE,
+    cam: (fx, fy, cx, cy, bf), Tcw: (3, 4) float32.  Returns (ninliers, q (x,y,z,w),
+    t, Tcw_out (3, 4) float32, outlier (n,) bool)."""
+    e = np.ascontiguousarray(edges, PEDGE_DTYPE)
+    c = PoseCam(*[float(np.float32(v)) for v in cam], 0.0)
+    T = np.ascontiguousarray(np.asarray(Tcw, np.float32).reshape(12))
+    q = np.zeros(4)
+    t = np.zeros(3)
+    To = np.zeros(12, np.float32)
+    out = np.zeros(max(len(e), 1), np.uint8)
+    n = lib().orc_pose_optimization(_p(e), len(e), C.byref(c), _p(T), _p(q), _p(t), _p(To),
+                                    _p(out))
+    return n, q, t, To.reshape(3, 4), out[:len(e)].astype(bool)

@@ -301,3 +301,54 @@ def map_projections(kps_src, shift_xy, seed=DEFAULT_SEED, depth=10.0, bf=KITTI_B
     fl |= np.where(rng.random(n) < obs_frac, MP_HAS_OBS, 0)
     mp["flags"] = fl
     return mp
+
+
+# ---------------------------------------------------------------------------
+# PoseOptimization frames: map points seen by one frame with a perturbed initial pose
+# ---------------------------------------------------------------------------
+PEDGE_DTYPE = np.dtype([("obs", "<f4", 3), ("xw", "<f4", 3), ("inv_sigma2", "<f4"),
+                        ("stereo", "<i4")])
+
+
+def pose_frame(n=1500, stereo_frac=0.5, outlier_frac=0.1, seed=DEFAULT_SEED, noise=1.0,
+               rot_err=0.01, trans_err=0.1, world_offset=50.0):
+    """One Tracking frame for Optimizer::PoseOptimization: n map points at 4-60 m with their
+    keypoint observations (pixel noise `noise` scaled per octave, stereo u_r for
+    stereo_frac, outlier_frac replaced by random pixels), the true pose Tcw and a perturbed
+    initial pose (the motion-model prediction).  Returns (edges, Tcw_true (3, 4),
+    Tcw_init (3, 4)), float32 poses."""
+    rng = np.random.Generator(np.random.PCG64(seed + 41))
+    q = _quat_from_axis_angle(rng.normal(size=3), rng.uniform(0, 0.3))
+    R = _rot(q)
+    t = rng.uniform(-world_offset, world_offset, 3)
+    Tcw = np.zeros((3, 4))
+    Tcw[:, :3] = R
+    Tcw[:, 3] = t
+    # points in front of the camera, then to world
+    depth = rng.uniform(4, 60, n)
+    u = rng.uniform(0, 1241, n)
+    v = rng.uniform(0, 376, n)
+    xc = np.stack([(u - KITTI_CX) * depth / KITTI_FX, (v - KITTI_CY) * depth / KITTI_FY, depth], 1)
+    xw = (xc - t) @ R  # R^T (xc - t)
+    octave = rng.integers(0, 8, n)
+    scale = 1.2 ** octave
+    e = np.zeros(n, PEDGE_DTYPE)
+    obs_u = u + rng.normal(0, noise, n) * scale
+    obs_v = v + rng.normal(0, noise, n) * scale
+    ur = obs_u - KITTI_BF / depth + rng.normal(0, noise, n) * scale
+    out = rng.random(n) < outlier_frac
+    obs_u[out] = rng.uniform(0, 1241, out.sum())
+    obs_v[out] = rng.uniform(0, 376, out.sum())
+    e["obs"][:, 0] = obs_u
+    e["obs"][:, 1] = obs_v
+    st = rng.random(n) < stereo_frac
+    e["obs"][:, 2] = np.where(st, ur, -1.0)
+    e["stereo"] = st
+    e["xw"] = xw
+    e["inv_sigma2"] = (1.0 / (scale * scale)).astype(np.float32)
+    dq = _quat_from_axis_angle(rng.normal(size=3), rot_err)
+    R0 = _rot(dq) @ R
+    T0 = np.zeros((3, 4))
+    T0[:, :3] = R0
+    T0[:, 3] = t + rng.normal(0, trans_err, 3)
+    return e, Tcw.astype(np.float32), T0.astype(np.float32)
