@@ -28,6 +28,7 @@
  *                                     LastFrame, th, bMono)         src/ORBmatcher.cc:1503-1667
  *   orbg_search_by_projection_local . ORBmatcher(nnratio).SearchByProjection(F, vpMapPoints, th)
  *                                                                      src/ORBmatcher.cc:59-154
+ *   orbg_pose_optimization .......... Optimizer::PoseOptimization(Frame*)  src/Optimizer.cc:356-631
  *   orbg_ba_linearize ............... g2o computeActiveErrors + BlockSolver::buildSystem arithmetic
  *                                     for EdgeSE3ProjectXYZ / EdgeStereoSE3ProjectXYZ inside
  *                                     Optimizer::LocalBundleAdjustment  src/Optimizer.cc:633-979
@@ -290,6 +291,38 @@ typedef struct {
 } orbg_track_batch;
 int orbg_search_by_projection_batch_device(orbg_ctx *ctx, int mode, const orbg_track_batch *tb,
                                            int nframes);
+
+/* ---------------- Optimizer::PoseOptimization ----------------
+ * One edge per Frame keypoint with a MapPoint (index order): EdgeSE3ProjectXYZOnlyPose when
+ * mvuRight[i] < 0, else EdgeStereoSE3ProjectXYZOnlyPose (Optimizer.cc:381-460). */
+typedef struct {
+    float obs[3];      /* kpUn.pt.x, kpUn.pt.y, mvuRight[i] */
+    float xw[3];       /* pMP->GetWorldPos() */
+    float inv_sigma2;  /* mvInvLevelSigma2[kpUn.octave] */
+    int32_t stereo;    /* mvuRight[i] >= 0 */
+} orbg_pose_edge;
+
+typedef struct {
+    float fx, fy, cx, cy, bf; /* Frame::fx, fy, cx, cy, mbf */
+    float pad;
+} orbg_pose_camera;
+
+/* Optimizer::PoseOptimization(pFrame): tcw_in = pFrame->mTcw rows 0..2 (row-major 3x4).
+ * Outputs the optimised SE3Quat (q x,y,z,w; t), its cv::Mat form tcw_out (SetPose), the
+ * mvbOutlier flag per edge and the return value (nInitialCorrespondences - nBad) in
+ * *ninliers.  Fewer than 3 edges: pose unchanged, 0. */
+int orbg_pose_optimization(orbg_ctx *ctx, const orbg_pose_edge *edges, int n,
+                           const orbg_pose_camera *cam, const float tcw_in[12], double q_out[4],
+                           double t_out[3], float tcw_out[12], uint8_t *outlier, int *ninliers);
+
+/* Batched, device-resident: frame f's edges at edges + f * edge_cap, counts[f] of them;
+ * cams[f], tcw_in[f * 12]; outputs q_out[f * 4], t_out[f * 3], tcw_out[f * 12],
+ * outlier[f * edge_cap], ninliers[f].  One workgroup per frame, on the context stream. */
+int orbg_pose_optimization_batch_device(orbg_ctx *ctx, const orbg_pose_edge *edges,
+                                        const int32_t *counts, int edge_cap,
+                                        const orbg_pose_camera *cams, const float *tcw_in,
+                                        double *q_out, double *t_out, float *tcw_out,
+                                        uint8_t *outlier, int32_t *ninliers, int nframes);
 
 /* ---------------- local BA linearisation ---------------- */
 typedef struct {

@@ -243,11 +243,13 @@ static void po_reduce(const double *part, int nv, double *out)
 /* one pass over the active edges at (q, t): robust chi2 and, when want_sys, H (lower
  * triangle, 21 entries row-major r >= c) and b */
 #define PO_NV 28 /* chi2 + 21 H + 6 b */
+int orc_pose_passes; /* edge passes of the last orc_pose_optimization (diagnostics) */
 static double po_pass(const double q[4], const double t[3], const orc_pose_edge *edges, int n,
                       const uint8_t *active, int robust, const orc_pose_cam *cam, double H[6][6],
                       double b[6], double *part)
 {
     memset(part, 0, sizeof(double) * PO_T * PO_NV);
+    orc_pose_passes++;
     for (int e = 0; e < n; e++) {
         if (!active[e])
             continue;
@@ -517,6 +519,7 @@ int orc_pose_optimization(const orc_pose_edge *edges, int n, const orc_pose_cam 
                           float Tcw_out[12], uint8_t *outlier)
 {
     double q0[4], t0[3];
+    orc_pose_passes = 0;
     orc_se3_from_tcw(Tcw_in, q0, t0);
     for (int i = 0; i < n; i++)
         outlier[i] = 0;

@@ -11,7 +11,7 @@ from ._lib import KP_DTYPE, EDGE_DTYPE, EDGE_OUT_DTYPE, POSE_DTYPE, LIB_PATH  # 
 from .orbextractor import ORBextractor  # noqa: F401
 from .orbmatcher import Frame, MapPointProjections, ORBmatcher  # noqa: F401
 from .frame import StereoFrame  # noqa: F401
-from .optimizer import linearize_local_ba  # noqa: F401
+from .optimizer import PoseOptimization, linearize_local_ba  # noqa: F401
 
-__all__ = ["ORBextractor", "ORBmatcher", "Frame", "MapPointProjections", "StereoFrame", "linearize_local_ba", "KP_DTYPE",
+__all__ = ["ORBextractor", "ORBmatcher", "Frame", "MapPointProjections", "StereoFrame", "PoseOptimization", "linearize_local_ba", "KP_DTYPE",
            "EDGE_DTYPE", "EDGE_OUT_DTYPE", "POSE_DTYPE"]

@@ -43,6 +43,15 @@ MP_DTYPE = np.dtype([("u", "<f4"), ("v", "<f4"), ("ur", "<f4"), ("level", "<i4")
                      ("view_cos", "<f4"), ("flags", "<i4")])
 
 
+PEDGE_DTYPE = np.dtype([("obs", "<f4", 3), ("xw", "<f4", 3), ("inv_sigma2", "<f4"),
+                        ("stereo", "<i4")])
+
+
+class PoseCamera(C.Structure):
+    _fields_ = [("fx", C.c_float), ("fy", C.c_float), ("cx", C.c_float), ("cy", C.c_float),
+                ("bf", C.c_float), ("pad", C.c_float)]
+
+
 class TrackCamera(C.Structure):
     _fields_ = [("Tcw", C.c_float * 12), ("Tlw", C.c_float * 12), ("fx", C.c_float),
                 ("fy", C.c_float), ("cx", C.c_float), ("cy", C.c_float), ("bf", C.c_float),
@@ -149,6 +158,9 @@ def lib():
         "orbg_search_by_projection_local": (i32, [vp, vp, vp, vp, i32, vp, P(Bounds), vp, vp, i32,
                                                   f32, f32, vp, P(i32)]),
         "orbg_search_by_projection_batch_device": (i32, [vp, i32, P(TrackBatch), i32]),
+        "orbg_pose_optimization": (i32, [vp, vp, i32, P(PoseCamera), vp, vp, vp, vp, vp, P(i32)]),
+        "orbg_pose_optimization_batch_device": (i32, [vp, vp, vp, i32, vp, vp, vp, vp, vp, vp, vp,
+                                                      i32]),
         "orbg_ba_linearize": (i32, [vp, vp, i32, vp, i32, vp, i32, vp, vp, vp, vp, vp]),
         "orbg_ba_linearize_device": (i32, [vp, vp, i32, vp, i32, vp, i32, vp, vp, vp, vp, vp, vp,
                                            vp, vp, vp]),

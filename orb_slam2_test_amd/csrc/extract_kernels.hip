@@ -1207,43 +1207,6 @@ __global__ __launch_bounds__(ORBG_OCT_THREADS) void k_octree(
 // ---------------------------------------------------------------------------
 // pinned sincos (double Cody-Waite + Taylor, identical to oracle/orb_oracle.c)
 // ---------------------------------------------------------------------------
-__device__ void pinned_sincos(double x, double *s, double *c)
-{
-    const double two_over_pi = 6.36619772367581382433e-01;
-    const double pio2_1 = 1.57079632673412561417e+00;
-    const double pio2_1t = 6.07710050650619224932e-11;
-    const double kd = rint(x * two_over_pi);
-    const int k = (int)kd;
-    const double r = (x - kd * pio2_1) - kd * pio2_1t;
-    const double r2 = r * r;
-    const double sp =
-        r + r * r2 *
-                (-1.0 / 6.0 +
-                 r2 * (1.0 / 120.0 +
-                       r2 * (-1.0 / 5040.0 +
-                             r2 * (1.0 / 362880.0 +
-                                   r2 * (-1.0 / 39916800.0 +
-                                         r2 * (1.0 / 6227020800.0 +
-                                               r2 * (-1.0 / 1307674368000.0 +
-                                                     r2 * (1.0 / 355687428096000.0 +
-                                                           r2 * (-1.0 / 121645100408832000.0)))))))));
-    const double cp =
-        1.0 + r2 * (-0.5 +
-                    r2 * (1.0 / 24.0 +
-                          r2 * (-1.0 / 720.0 +
-                                r2 * (1.0 / 40320.0 +
-                                      r2 * (-1.0 / 3628800.0 +
-                                            r2 * (1.0 / 479001600.0 +
-                                                  r2 * (-1.0 / 87178291200.0 +
-                                                        r2 * (1.0 / 20922789888000.0 +
-                                                              r2 * (-1.0 / 6402373705728000.0)))))))));
-    switch (k & 3) {
-    case 0: *s = sp; *c = cp; break;
-    case 1: *s = cp; *c = -sp; break;
-    case 2: *s = -sp; *c = -cp; break;
-    default: *s = -cp; *c = sp; break;
-    }
-}
 
 // cv::fastAtan2 (OpenCV 3.4 atan_f32), degrees in [0, 360]
 __device__ float fast_atan2(float y, float x)

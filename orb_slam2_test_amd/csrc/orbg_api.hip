@@ -42,6 +42,10 @@ int launch_match_pairs(hipStream_t st, hipStream_t aux, hipEvent_t evf, hipEvent
                        const int32_t *d_f2, int npairs, int w, int h, int window, float nnratio,
                        int check_ori, int32_t *knn, int32_t *m12, int32_t *nm, uint32_t *topk,
                        int32_t *topk_n, void *prof, int serial, int cap0);
+int launch_pose_opt(hipStream_t st, const orbg_pose_edge *edges, const int32_t *counts, int cap,
+                    const orbg_pose_camera *cams, const float *tcw_in, double *q_out,
+                    double *t_out, float *tcw_out, uint8_t *outlier, int32_t *ninliers,
+                    int nframes, void *prof);
 int launch_knn2(hipStream_t st, const uint8_t *q, int nq, const uint8_t *t, int nt, int32_t *out,
                 void *prof);
 int launch_init_match_single(hipStream_t st, const orbg_keypoint *k1, const uint8_t *d1, int n1,
@@ -1664,4 +1668,72 @@ extern "C" int orbg_search_by_projection_local(orbg_ctx *c, const orbg_keypoint 
     return track_host(c, ORBG_TRACK_LOCAL, kps, desc, uright, n, taken0, bounds, mps,
                       sizeof(orbg_map_projection), mdesc, nm, nullptr, th, nnratio, 0, match,
                       nmatches);
+}
+
+// ---------------------------------------------------------------------------
+// Optimizer::PoseOptimization
+// ---------------------------------------------------------------------------
+extern "C" int orbg_pose_optimization_batch_device(orbg_ctx *c, const orbg_pose_edge *edges,
+                                                   const int32_t *counts, int edge_cap,
+                                                   const orbg_pose_camera *cams,
+                                                   const float *tcw_in, double *q_out,
+                                                   double *t_out, float *tcw_out,
+                                                   uint8_t *outlier, int32_t *ninliers,
+                                                   int nframes)
+{
+    if (!c) return set_err(ORBG_EINVAL, "ctx is NULL");
+    if (nframes <= 0) return ORBG_OK;
+    if (edge_cap < 0 || !edges || !counts || !cams || !tcw_in || !q_out || !t_out || !tcw_out ||
+        !outlier || !ninliers)
+        return set_err(ORBG_EINVAL, "NULL device array");
+    HIPCHK(hipSetDevice(c->device));
+    const int rc = launch_pose_opt(c->stream, edges, counts, edge_cap, cams, tcw_in, q_out,
+                                   t_out, tcw_out, outlier, ninliers, nframes, &c->prof);
+    return rc ? set_err(rc, "pose optimisation launch failed") : ORBG_OK;
+}
+
+extern "C" int orbg_pose_optimization(orbg_ctx *c, const orbg_pose_edge *edges, int n,
+                                      const orbg_pose_camera *cam, const float tcw_in[12],
+                                      double q_out[4], double t_out[3], float tcw_out[12],
+                                      uint8_t *outlier, int *ninliers)
+{
+    if (!c || !cam || !tcw_in || !q_out || !t_out || !tcw_out || (n > 0 && (!edges || !outlier)))
+        return set_err(ORBG_EINVAL, "NULL argument");
+    if (n < 0) return set_err(ORBG_EINVAL, "negative size");
+    HIPCHK(hipSetDevice(c->device));
+    size_t off = 0;
+    auto take = [&](size_t bytes) {
+        const size_t o = off;
+        off += al256(bytes);
+        return o;
+    };
+    const size_t o_e = take((size_t)std::max(n, 1) * sizeof(orbg_pose_edge)), o_n = take(4);
+    const size_t o_cam = take(sizeof(orbg_pose_camera)), o_tin = take(48), o_q = take(32);
+    const size_t o_t = take(24), o_tout = take(48), o_out = take((size_t)std::max(n, 1));
+    const size_t o_ni = take(4);
+    void *s;
+    int rc = scratch(c, off, &s);
+    if (rc) return rc;
+    uint8_t *b = (uint8_t *)s;
+    const int32_t cnt = n;
+    if (n) HIPCHK(hipMemcpyAsync(b + o_e, edges, (size_t)n * sizeof(orbg_pose_edge), hipMemcpyHostToDevice, c->stream));
+    HIPCHK(hipMemcpyAsync(b + o_n, &cnt, 4, hipMemcpyHostToDevice, c->stream));
+    HIPCHK(hipMemcpyAsync(b + o_cam, cam, sizeof(*cam), hipMemcpyHostToDevice, c->stream));
+    HIPCHK(hipMemcpyAsync(b + o_tin, tcw_in, 48, hipMemcpyHostToDevice, c->stream));
+    if ((rc = launch_pose_opt(c->stream, (const orbg_pose_edge *)(b + o_e), (const int32_t *)(b + o_n),
+                              std::max(n, 1), (const orbg_pose_camera *)(b + o_cam),
+                              (const float *)(b + o_tin), (double *)(b + o_q), (double *)(b + o_t),
+                              (float *)(b + o_tout), b + o_out, (int32_t *)(b + o_ni), 1,
+                              &c->prof)))
+        return set_err(rc, "pose optimisation launch failed");
+    int32_t ni = 0;
+    HIPCHK(hipMemcpyAsync(q_out, b + o_q, 32, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(hipMemcpyAsync(t_out, b + o_t, 24, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(hipMemcpyAsync(tcw_out, b + o_tout, 48, hipMemcpyDeviceToHost, c->stream));
+    if (n) HIPCHK(hipMemcpyAsync(outlier, b + o_out, (size_t)n, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(hipMemcpyAsync(&ni, b + o_ni, 4, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(hipStreamSynchronize(c->stream));
+    c->prof.collect();
+    if (ninliers) *ninliers = ni;
+    return ORBG_OK;
 }

@@ -1,6 +1,8 @@
 // orbg_device.h -- small wave64 helpers shared by the kernel translation units.
 #pragma once
 
+#pragma clang fp contract(off)
+
 #include <hip/hip_runtime.h>
 
 namespace orbg {
@@ -57,6 +59,45 @@ __device__ __forceinline__ int xcd_remap(int orig, int nwg)
 {
     const int xcd = orig & 7, q = nwg >> 3, r = nwg & 7;
     return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (orig >> 3);
+}
+
+// double sin/cos pinned to one polynomial so the oracle (orb_oracle.c) matches bit for bit
+__device__ __forceinline__ void pinned_sincos(double x, double *s, double *c)
+{
+    const double two_over_pi = 6.36619772367581382433e-01;
+    const double pio2_1 = 1.57079632673412561417e+00;
+    const double pio2_1t = 6.07710050650619224932e-11;
+    const double kd = rint(x * two_over_pi);
+    const int k = (int)kd;
+    const double r = (x - kd * pio2_1) - kd * pio2_1t;
+    const double r2 = r * r;
+    const double sp =
+        r + r * r2 *
+                (-1.0 / 6.0 +
+                 r2 * (1.0 / 120.0 +
+                       r2 * (-1.0 / 5040.0 +
+                             r2 * (1.0 / 362880.0 +
+                                   r2 * (-1.0 / 39916800.0 +
+                                         r2 * (1.0 / 6227020800.0 +
+                                               r2 * (-1.0 / 1307674368000.0 +
+                                                     r2 * (1.0 / 355687428096000.0 +
+                                                           r2 * (-1.0 / 121645100408832000.0)))))))));
+    const double cp =
+        1.0 + r2 * (-0.5 +
+                    r2 * (1.0 / 24.0 +
+                          r2 * (-1.0 / 720.0 +
+                                r2 * (1.0 / 40320.0 +
+                                      r2 * (-1.0 / 3628800.0 +
+                                            r2 * (1.0 / 479001600.0 +
+                                                  r2 * (-1.0 / 87178291200.0 +
+                                                        r2 * (1.0 / 20922789888000.0 +
+                                                              r2 * (-1.0 / 6402373705728000.0)))))))));
+    switch (k & 3) {
+    case 0: *s = sp; *c = cp; break;
+    case 1: *s = cp; *c = -sp; break;
+    case 2: *s = -sp; *c = -cp; break;
+    default: *s = -cp; *c = sp; break;
+    }
 }
 
 }  // namespace orbg

@@ -1,0 +1,595 @@
+// pose_kernels.hip -- Optimizer::PoseOptimization (src/Optimizer.cc:356-631) for gfx950.
+//
+// One 256-thread workgroup per frame runs the whole motion-only BA: four rounds of
+// g2o's Levenberg-Marquardt optimize(10) on one VertexSE3Expmap with unary
+// EdgeSE3ProjectXYZOnlyPose / EdgeStereoSE3ProjectXYZOnlyPose edges (Huber in rounds 0-2),
+// re-classifying outliers after each round.  Every LM trial is one pass over the frame's
+// edges: thread t takes edges t, t+256, ... and accumulates the robust chi2, the lower
+// triangle of H = J^T W J and b = -rho' J^T Omega e in registers (28 doubles), then the
+// workgroup reduces them in the pinned order of oracle/pose_oracle.c (butterfly within a
+// wave, (w0 + w1) + (w2 + w3) across waves), so the result is bit-identical to the oracle.
+// The 6x6 LDLT solve, the SE3 exp update and the step control run on lane 0 (state in LDS).  A trial's
+// pass also yields the system at the trial pose, which the next iteration reuses when the
+// step is accepted (g2o rebuilds it at the same pose: same values).
+//
+// fp64 throughout; no FMA contraction; sin/cos of the exp map pinned (orbg_device.h).
+#include <hip/hip_runtime.h>
+
+#include <cfloat>
+#include <climits>
+
+#include "../../include/orbg.h"
+#include "orbg_internal.h"
+#include "orbg_device.h"
+#include "match_device.h"
+
+#pragma clang fp contract(off)
+
+namespace orbg {
+
+void prof_begin(void *prof, hipStream_t s, const char *n, hipEvent_t *a);
+void prof_end(void *prof, hipStream_t s, const char *n, hipEvent_t a);
+
+#define PO_T 256
+#define PO_NV 28  // robust chi2, 21 lower-triangle H entries, 6 b entries
+
+// ---- SE3Quat (q = x, y, z, w), Eigen's formulas (see oracle/pose_oracle.c) ----
+__device__ __forceinline__ void q_rotate(const double q[4], const double v[3], double out[3])
+{
+    double uv[3] = {q[1] * v[2] - q[2] * v[1], q[2] * v[0] - q[0] * v[2],
+                    q[0] * v[1] - q[1] * v[0]};
+    uv[0] += uv[0];
+    uv[1] += uv[1];
+    uv[2] += uv[2];
+    const double c[3] = {q[1] * uv[2] - q[2] * uv[1], q[2] * uv[0] - q[0] * uv[2],
+                         q[0] * uv[1] - q[1] * uv[0]};
+    out[0] = v[0] + q[3] * uv[0] + c[0];
+    out[1] = v[1] + q[3] * uv[1] + c[1];
+    out[2] = v[2] + q[3] * uv[2] + c[2];
+}
+
+__device__ __forceinline__ void q_mul(const double a[4], const double b[4], double o[4])
+{
+    o[3] = a[3] * b[3] - a[0] * b[0] - a[1] * b[1] - a[2] * b[2];
+    o[0] = a[3] * b[0] + a[0] * b[3] + a[1] * b[2] - a[2] * b[1];
+    o[1] = a[3] * b[1] + a[1] * b[3] + a[2] * b[0] - a[0] * b[2];
+    o[2] = a[3] * b[2] + a[2] * b[3] + a[0] * b[1] - a[1] * b[0];
+}
+
+__device__ __forceinline__ void q_normalize(double q[4])
+{
+    if (q[3] < 0) {
+        q[0] = -q[0];
+        q[1] = -q[1];
+        q[2] = -q[2];
+        q[3] = -q[3];
+    }
+    const double n = sqrt(q[0] * q[0] + q[1] * q[1] + q[2] * q[2] + q[3] * q[3]);
+    q[0] /= n;
+    q[1] /= n;
+    q[2] /= n;
+    q[3] /= n;
+}
+
+__device__ void q_from_rot(const double R[3][3], double q[4])
+{
+    const double t = R[0][0] + R[1][1] + R[2][2];
+    if (t > 0) {
+        double s = sqrt(t + 1.0);
+        q[3] = 0.5 * s;
+        s = 0.5 / s;
+        q[0] = (R[2][1] - R[1][2]) * s;
+        q[1] = (R[0][2] - R[2][0]) * s;
+        q[2] = (R[1][0] - R[0][1]) * s;
+    } else {
+        int i = 0;
+        if (R[1][1] > R[0][0]) i = 1;
+        if (R[2][2] > R[i][i]) i = 2;
+        const int j = (i + 1) % 3, k = (j + 1) % 3;
+        double s = sqrt(R[i][i] - R[j][j] - R[k][k] + 1.0);
+        q[i] = 0.5 * s;
+        s = 0.5 / s;
+        q[3] = (R[k][j] - R[j][k]) * s;
+        q[j] = (R[j][i] + R[i][j]) * s;
+        q[k] = (R[k][i] + R[i][k]) * s;
+    }
+}
+
+// VertexSE3Expmap::oplusImpl: estimate = SE3Quat::exp(update) * estimate
+__device__ void se3_oplus(double q[4], double t[3], const double upd[6])
+{
+    const double w[3] = {upd[0], upd[1], upd[2]}, u[3] = {upd[3], upd[4], upd[5]};
+    const double theta = sqrt(w[0] * w[0] + w[1] * w[1] + w[2] * w[2]);
+    const double O[3][3] = {{0, -w[2], w[1]}, {w[2], 0, -w[0]}, {-w[1], w[0], 0}};
+    double O2[3][3], R[3][3], V[3][3];
+    for (int i = 0; i < 3; i++)
+        for (int j = 0; j < 3; j++)
+            O2[i][j] = O[i][0] * O[0][j] + O[i][1] * O[1][j] + O[i][2] * O[2][j];
+    if (theta < 0.00001) {
+        for (int i = 0; i < 3; i++)
+            for (int j = 0; j < 3; j++) {
+                R[i][j] = ((i == j ? 1.0 : 0.0) + O[i][j]) + O2[i][j];
+                V[i][j] = R[i][j];
+            }
+    } else {
+        double s, c;
+        pinned_sincos(theta, &s, &c);
+        const double a = s / theta, b = (1 - c) / (theta * theta);
+        const double cc = (theta - s) / (theta * theta * theta);
+        for (int i = 0; i < 3; i++)
+            for (int j = 0; j < 3; j++) {
+                const double I = i == j ? 1.0 : 0.0;
+                R[i][j] = (I + a * O[i][j]) + b * O2[i][j];
+                V[i][j] = (I + b * O[i][j]) + cc * O2[i][j];
+            }
+    }
+    double dq[4], dt[3];
+    q_from_rot(R, dq);
+    for (int i = 0; i < 3; i++) dt[i] = V[i][0] * u[0] + V[i][1] * u[1] + V[i][2] * u[2];
+    q_normalize(dq);
+    double rt[3], nq[4];
+    q_rotate(dq, t, rt);
+    for (int i = 0; i < 3; i++) t[i] = dt[i] + rt[i];
+    q_mul(dq, q, nq);
+    q_normalize(nq);
+    for (int i = 0; i < 4; i++) q[i] = nq[i];
+}
+
+// Eigen LDLT (lower, diagonal pivoting) + solve; returns isPositive()
+__device__ bool ldlt_solve6(double m[6][6], const double b[6], double x[6])
+{
+    int tr[6];
+    int sign = 0;  // 0 zero, 1 positive semidef, 2 negative semidef, 3 indefinite
+    double temp[6];
+    for (int k = 0; k < 6; k++) {
+        int big = k;
+        double bv = fabs(m[k][k]);
+        for (int i = k + 1; i < 6; i++)
+            if (fabs(m[i][i]) > bv) {
+                bv = fabs(m[i][i]);
+                big = i;
+            }
+        tr[k] = big;
+        if (k != big) {
+            for (int j = 0; j < k; j++) {
+                const double s = m[k][j];
+                m[k][j] = m[big][j];
+                m[big][j] = s;
+            }
+            for (int i = big + 1; i < 6; i++) {
+                const double s = m[i][k];
+                m[i][k] = m[i][big];
+                m[i][big] = s;
+            }
+            {
+                const double s = m[k][k];
+                m[k][k] = m[big][big];
+                m[big][big] = s;
+            }
+            for (int i = k + 1; i < big; i++) {
+                const double s = m[i][k];
+                m[i][k] = m[big][i];
+                m[big][i] = s;
+            }
+        }
+        if (k > 0) {
+            for (int j = 0; j < k; j++) temp[j] = m[j][j] * m[k][j];
+            double dot = 0;
+            for (int j = 0; j < k; j++) dot += m[k][j] * temp[j];
+            m[k][k] -= dot;
+            for (int i = k + 1; i < 6; i++) {
+                double s = 0;
+                for (int j = 0; j < k; j++) s += m[i][j] * temp[j];
+                m[i][k] -= s;
+            }
+        }
+        const double akk = m[k][k];
+        const bool valid = fabs(akk) > 0.0;
+        if (k == 0 && !valid) {
+            sign = 0;
+            for (int j = 0; j < 6; j++) tr[j] = j;
+            break;
+        }
+        if (k < 5 && valid)
+            for (int i = k + 1; i < 6; i++) m[i][k] /= akk;
+        if (sign == 0 || sign == 1) {
+            if (akk > 0) sign = 1;
+            else if (akk < 0) sign = sign == 0 ? 2 : 3;
+        } else if (sign == 2 && akk > 0) {
+            sign = 3;
+        }
+    }
+    if (!(sign == 1 || sign == 0)) return false;
+    double d[6];
+    for (int i = 0; i < 6; i++) d[i] = b[i];
+    for (int k = 0; k < 6; k++) {
+        const double s = d[k];
+        d[k] = d[tr[k]];
+        d[tr[k]] = s;
+    }
+    for (int i = 0; i < 6; i++) {
+        double s = 0;
+        for (int j = 0; j < i; j++) s += m[i][j] * d[j];
+        d[i] -= s;
+    }
+    for (int i = 0; i < 6; i++) d[i] = fabs(m[i][i]) > DBL_MIN ? d[i] / m[i][i] : 0.0;
+    for (int i = 5; i >= 0; i--) {
+        double s = 0;
+        for (int j = i + 1; j < 6; j++) s += m[j][i] * d[j];
+        d[i] -= s;
+    }
+    for (int k = 5; k >= 0; k--) {
+        const double s = d[k];
+        d[k] = d[tr[k]];
+        d[tr[k]] = s;
+    }
+    for (int i = 0; i < 6; i++) x[i] = d[i];
+    return true;
+}
+
+// ---- the unary edges ----
+__device__ __forceinline__ int pedge_error(const double q[4], const double t[3],
+                                           const orbg_pose_edge &e, const orbg_pose_camera &cam,
+                                           double err[3], double xc[3])
+{
+    const double X[3] = {e.xw[0], e.xw[1], e.xw[2]};
+    q_rotate(q, X, xc);
+    xc[0] += t[0];
+    xc[1] += t[1];
+    xc[2] += t[2];
+    const double fx = cam.fx, fy = cam.fy, cx = cam.cx, cy = cam.cy;
+    if (!e.stereo) {
+        const double px = xc[0] / xc[2], py = xc[1] / xc[2];
+        err[0] = (double)e.obs[0] - (px * fx + cx);
+        err[1] = (double)e.obs[1] - (py * fy + cy);
+        err[2] = 0;
+        return 2;
+    }
+    const float invz = (float)(1.0f / xc[2]);
+    const double u = xc[0] * invz * fx + cx;
+    const double v = xc[1] * invz * fy + cy;
+    err[0] = (double)e.obs[0] - u;
+    err[1] = (double)e.obs[1] - v;
+    err[2] = (double)e.obs[2] - (u - (double)cam.bf * invz);
+    return 3;
+}
+
+__device__ __forceinline__ double pedge_chi2(const double err[3], int D, double info)
+{
+    // err[2] = 0 for a mono edge: the third term adds +0 (see po_partial)
+    (void)D;
+    double chi2 = 0;
+#pragma unroll
+    for (int k = 0; k < 3; k++) chi2 += err[k] * (info * err[k]);
+    return chi2;
+}
+
+// per-thread partial sums of one pass at (q, t) over the active edges
+__device__ void po_partial(const double q[4], const double t[3], const orbg_pose_edge *edges,
+                           int n, const uint8_t *outlier, bool robust,
+                           const orbg_pose_camera &cam, double p[PO_NV])
+{
+    for (int j = 0; j < PO_NV; j++) p[j] = 0;
+    const double dmono = (double)(float)sqrt(5.991), dstereo = (double)(float)sqrt(7.815);
+    for (int e = threadIdx.x; e < n; e += PO_T) {
+        if (outlier[e]) continue;
+        const orbg_pose_edge E = edges[e];
+        double err[3], xc[3];
+        const int D = pedge_error(q, t, E, cam, err, xc);
+        const double info = E.inv_sigma2;
+        const double chi2 = pedge_chi2(err, D, info);
+        double rho1 = 1.0, rho0 = chi2;
+        if (robust) {
+            const double delta = E.stereo ? dstereo : dmono;
+            const float dsqr = (float)(delta * delta);
+            if (!(chi2 <= dsqr)) {
+                const double sq = sqrt(chi2);
+                rho1 = delta / sq;
+                rho0 = 2 * sq * delta - dsqr;
+            }
+        }
+        p[0] += rho0;
+        // linearizeOplus (types_six_dof_expmap.cpp:266-288, 335-364)
+        double J[3][6];
+        {
+            const double x = xc[0], y = xc[1];
+            const double invz = 1.0 / xc[2], invz_2 = invz * invz;
+            const double fx = cam.fx, fy = cam.fy, bf = cam.bf;
+            J[0][0] = x * y * invz_2 * fx;
+            J[0][1] = -(1 + (x * x * invz_2)) * fx;
+            J[0][2] = y * invz * fx;
+            J[0][3] = -invz * fx;
+            J[0][4] = 0;
+            J[0][5] = x * invz_2 * fx;
+            J[1][0] = (1 + y * y * invz_2) * fy;
+            J[1][1] = -x * y * invz_2 * fy;
+            J[1][2] = -x * invz * fy;
+            J[1][3] = 0;
+            J[1][4] = -invz * fy;
+            J[1][5] = y * invz_2 * fy;
+            if (D == 3) {
+                J[2][0] = J[0][0] - bf * y * invz_2;
+                J[2][1] = J[0][1] + bf * x * invz_2;
+                J[2][2] = J[0][2];
+                J[2][3] = J[0][3];
+                J[2][4] = 0;
+                J[2][5] = J[0][5] - bf * invz_2;
+            } else {
+#pragma unroll
+                for (int c = 0; c < 6; c++) J[2][c] = 0;
+            }
+        }
+        // fixed three rows: a mono edge's third row is +0 (J) / -0 (wr), and adding those
+        // to sums that start at +0 leaves every bit as the oracle's two-row loop does
+        const double w = rho1 * info;
+        double wr[3];
+#pragma unroll
+        for (int k = 0; k < 3; k++) wr[k] = -info * err[k] * rho1;
+        int hi = 1;
+#pragma unroll
+        for (int r = 0; r < 6; r++)
+#pragma unroll
+            for (int c = 0; c <= r; c++) {
+                double a2 = 0;
+#pragma unroll
+                for (int k = 0; k < 3; k++) a2 += J[k][r] * w * J[k][c];
+                p[hi++] += a2;
+            }
+#pragma unroll
+        for (int r = 0; r < 6; r++) {
+            double acc = 0;
+#pragma unroll
+            for (int k = 0; k < 3; k++) acc += J[k][r] * wr[k];
+            p[22 + r] += acc;
+        }
+    }
+}
+
+// pinned reduction: butterfly within each wave, (w0 + w1) + (w2 + w3); result in red[0..27]
+__device__ void po_reduce(double p[PO_NV], double *wred /* [4][PO_NV] */, double *red)
+{
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+#pragma unroll
+    for (int j = 0; j < PO_NV; j++) {
+        double v = p[j];
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) v = v + __shfl_xor(v, o, 64);
+        if (lane == 0) wred[wv * PO_NV + j] = v;
+    }
+    __syncthreads();
+    if (threadIdx.x < PO_NV) {
+        const int j = threadIdx.x;
+        red[j] = (wred[j] + wred[PO_NV + j]) + (wred[2 * PO_NV + j] + wred[3 * PO_NV + j]);
+    }
+    __syncthreads();
+}
+
+__device__ __forceinline__ void unpack_sys(const double *red, double *H, double *b)
+{
+    int hi = 1;
+    for (int r = 0; r < 6; r++)
+        for (int c = 0; c <= r; c++) {
+            H[r * 6 + c] = red[hi];
+            H[c * 6 + r] = red[hi];
+            hi++;
+        }
+    for (int r = 0; r < 6; r++) b[r] = red[22 + r];
+}
+
+struct PoShared {
+    double red[PO_NV];
+    double wred[4 * PO_NV];
+    double q[4], t[3];     // current estimate
+    double tq[4], tt[3];   // trial estimate
+    double lq[4], lt[3];   // where computeActiveErrors last ran
+    double H[36], b[6], x[6];
+    int go;                // lane 0's loop decisions: bit 0 continue trials, bit 1 stop LM
+};
+
+// Lane 0 owns all of the LM scalar state (lambda, ni, chi values, the 6x6 system and its
+// solve); the workgroup only runs the edge passes.  Barriers hand the trial pose out and
+// the reduced sums back.
+__global__ __launch_bounds__(PO_T) void k_pose_opt(const orbg_pose_edge *__restrict__ edges_all,
+                                                    const int32_t *__restrict__ counts, int cap,
+                                                    const orbg_pose_camera *__restrict__ cams,
+                                                    const float *__restrict__ tcw_in,
+                                                    double *__restrict__ q_out,
+                                                    double *__restrict__ t_out,
+                                                    float *__restrict__ tcw_out,
+                                                    uint8_t *__restrict__ outlier_all,
+                                                    int32_t *__restrict__ ninliers)
+{
+    __shared__ PoShared S;
+    const int f = blockIdx.x, tid = threadIdx.x;
+    const int n = counts[f];
+    const orbg_pose_edge *edges = edges_all + (size_t)f * cap;
+    uint8_t *outlier = outlier_all + (size_t)f * cap;
+    const orbg_pose_camera cam = cams[f];
+    const float *Tin = tcw_in + (size_t)f * 12;
+    for (int i = tid; i < n; i += PO_T) outlier[i] = 0;
+    if (tid == 0) {
+        // Converter::toSE3Quat
+        double R[3][3];
+        for (int i = 0; i < 3; i++) {
+            for (int j = 0; j < 3; j++) R[i][j] = Tin[4 * i + j];
+            S.tt[i] = Tin[4 * i + 3];
+        }
+        q_from_rot(R, S.tq);
+        q_normalize(S.tq);
+    }
+    __syncthreads();
+    double q0[4], t0[3];
+    for (int i = 0; i < 4; i++) q0[i] = S.tq[i];
+    for (int i = 0; i < 3; i++) t0[i] = S.tt[i];
+    if (n < 3) {
+        if (tid == 0) {
+            for (int i = 0; i < 4; i++) q_out[f * 4 + i] = q0[i];
+            for (int i = 0; i < 3; i++) t_out[f * 3 + i] = t0[i];
+            for (int i = 0; i < 12; i++) tcw_out[f * 12 + i] = Tin[i];
+            ninliers[f] = 0;
+        }
+        return;
+    }
+    bool robust = true;
+    int nBad = 0;
+    double p[PO_NV];
+    // lane-0 state
+    double lambda = 0, ni = 2, currentChi = 0, iniChi = 0;
+    int nBadLM = 0, qmax = 0;
+    bool have_sys = false;
+    for (int round = 0; round < 4; round++) {
+        if (tid == 0) {
+            for (int i = 0; i < 4; i++) S.q[i] = q0[i];
+            for (int i = 0; i < 3; i++) S.t[i] = t0[i];
+        }
+        int act = 0;
+        for (int i = tid; i < n; i += PO_T) act += !outlier[i];
+        act = __syncthreads_or(act);
+        if (act) {
+            // ---- optimize(10): OptimizationAlgorithmLevenberg::solve per iteration ----
+            have_sys = false;
+            for (int it = 0; it < 10; it++) {
+                if (!__syncthreads_or(have_sys)) {
+                    // computeActiveErrors + buildSystem at the current estimate
+                    po_partial(S.q, S.t, edges, n, outlier, robust, cam, p);
+                    po_reduce(p, S.wred, S.red);
+                    if (tid == 0) {
+                        for (int i = 0; i < 4; i++) S.lq[i] = S.q[i];
+                        for (int i = 0; i < 3; i++) S.lt[i] = S.t[i];
+                        currentChi = S.red[0];
+                        unpack_sys(S.red, S.H, S.b);
+                    }
+                }
+                if (tid == 0) {
+                    have_sys = false;
+                    iniChi = currentChi;
+                    if (it == 0) {
+                        double maxd = 0;
+                        for (int j = 0; j < 6; j++) maxd = fmax(fabs(S.H[j * 7]), maxd);
+                        lambda = 1e-5 * maxd;
+                        ni = 2;
+                        nBadLM = 0;
+                    }
+                    qmax = 0;
+                }
+                for (;;) {
+                    bool ok2 = false;
+                    if (tid == 0) {
+                        // setLambda, LDLT solve, oplus (trial), restoreDiagonal
+                        double Hd[6][6];
+                        for (int r = 0; r < 6; r++)
+                            for (int c = 0; c < 6; c++) Hd[r][c] = S.H[r * 6 + c];
+                        for (int j = 0; j < 6; j++) Hd[j][j] += lambda;
+                        ok2 = ldlt_solve6(Hd, S.b, S.x);
+                        for (int i = 0; i < 4; i++) S.tq[i] = S.q[i];
+                        for (int i = 0; i < 3; i++) S.tt[i] = S.t[i];
+                        se3_oplus(S.tq, S.tt, S.x);
+                        for (int i = 0; i < 4; i++) S.lq[i] = S.tq[i];
+                        for (int i = 0; i < 3; i++) S.lt[i] = S.tt[i];
+                    }
+                    __syncthreads();
+                    po_partial(S.tq, S.tt, edges, n, outlier, robust, cam, p);
+                    po_reduce(p, S.wred, S.red);
+                    if (tid == 0) {
+                        double tempChi = S.red[0];
+                        if (!ok2) tempChi = DBL_MAX;
+                        double rho = currentChi - tempChi;
+                        double scale = 0;
+                        for (int j = 0; j < 6; j++) scale += S.x[j] * (lambda * S.x[j] + S.b[j]);
+                        scale += 1e-3;
+                        rho /= scale;
+                        if (rho > 0 && isfinite(tempChi)) {
+                            const double t3 = 2 * rho - 1;
+                            double alpha = 1. - t3 * t3 * t3;
+                            alpha = fmin(alpha, 2. / 3.);
+                            const double sf = fmax(1. / 3., alpha);
+                            lambda *= sf;
+                            ni = 2;
+                            currentChi = tempChi;
+                            for (int i = 0; i < 4; i++) S.q[i] = S.tq[i];
+                            for (int i = 0; i < 3; i++) S.t[i] = S.tt[i];
+                            // the system at the accepted pose is the next buildSystem's
+                            unpack_sys(S.red, S.H, S.b);
+                            have_sys = true;
+                        } else {
+                            lambda *= ni;
+                            ni *= 2;
+                        }
+                        qmax++;
+                        int go = 0;
+                        if (rho < 0 && qmax < 10) {
+                            go = 1;  // another trial
+                        } else if (qmax == 10 || rho == 0) {
+                            go = 2;  // Terminate
+                        } else {
+                            if ((iniChi - currentChi) * 1e3 < iniChi)
+                                nBadLM++;
+                            else
+                                nBadLM = 0;
+                            if (nBadLM >= 3) go = 2;
+                        }
+                        S.go = go;
+                    }
+                    __syncthreads();
+                    if (S.go != 1) break;
+                }
+                if (S.go == 2) break;
+            }
+        }
+        __syncthreads();
+        // ---- classification (Optimizer.cc:518-580) ----
+        int bad = 0;
+        for (int i = tid; i < n; i += PO_T) {
+            const orbg_pose_edge E = edges[i];
+            double err[3], xc[3];
+            const bool was_active = !outlier[i];
+            const int D = was_active ? pedge_error(S.lq, S.lt, E, cam, err, xc)
+                                     : pedge_error(S.q, S.t, E, cam, err, xc);
+            const float chi2 = (float)pedge_chi2(err, D, E.inv_sigma2);
+            const bool o = chi2 > (E.stereo ? 7.815f : 5.991f);
+            outlier[i] = o;
+            bad += o;
+        }
+        bad = wave_isum(bad);
+        if ((tid & 63) == 0) S.wred[tid >> 6] = bad;
+        __syncthreads();
+        nBad = (int)(S.wred[0] + S.wred[1] + S.wred[2] + S.wred[3]);
+        __syncthreads();
+        if (round == 2) robust = false;
+        if (n < 10) break;
+    }
+    if (tid == 0) {
+        for (int i = 0; i < 4; i++) q_out[f * 4 + i] = S.q[i];
+        for (int i = 0; i < 3; i++) t_out[f * 3 + i] = S.t[i];
+        // Converter::toCvMat(SE3Quat)
+        const double *q = S.q;
+        const double tx = 2 * q[0], ty = 2 * q[1], tz = 2 * q[2];
+        const double twx = tx * q[3], twy = ty * q[3], twz = tz * q[3];
+        const double txx = tx * q[0], txy = ty * q[0], txz = tz * q[0];
+        const double tyy = ty * q[1], tyz = tz * q[1], tzz = tz * q[2];
+        const double R[3][3] = {{1 - (tyy + tzz), txy - twz, txz + twy},
+                                {txy + twz, 1 - (txx + tzz), tyz - twx},
+                                {txz - twy, tyz + twx, 1 - (txx + tyy)}};
+        for (int i = 0; i < 3; i++) {
+            for (int j = 0; j < 3; j++) tcw_out[f * 12 + 4 * i + j] = (float)R[i][j];
+            tcw_out[f * 12 + 4 * i + 3] = (float)S.t[i];
+        }
+        ninliers[f] = n - nBad;
+    }
+}
+
+int launch_pose_opt(hipStream_t st, const orbg_pose_edge *edges, const int32_t *counts, int cap,
+                    const orbg_pose_camera *cams, const float *tcw_in, double *q_out,
+                    double *t_out, float *tcw_out, uint8_t *outlier, int32_t *ninliers,
+                    int nframes, void *prof)
+{
+    if (nframes <= 0) return ORBG_OK;
+    hipEvent_t ev = nullptr;
+    prof_begin(prof, st, "pose_opt", &ev);
+    hipLaunchKernelGGL(k_pose_opt, dim3(nframes), dim3(PO_T), 0, st, edges, counts, cap, cams,
+                       tcw_in, q_out, t_out, tcw_out, outlier, ninliers);
+    prof_end(prof, st, "pose_opt", ev);
+    return hipGetLastError() == hipSuccess ? ORBG_OK : ORBG_EIO;
+}
+
+}  // namespace orbg

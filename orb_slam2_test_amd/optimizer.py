@@ -9,6 +9,7 @@ residual, analytic Jacobians, chi2, Huber weight and the J^T W J / J^T W r block
 
 Arrays use the dtypes of ``_lib`` (POSE_DTYPE, EDGE_DTYPE, EDGE_OUT_DTYPE).
 """
+import ctypes
 import math
 
 import numpy as np
@@ -38,6 +39,27 @@ def linearize_local_ba(poses, points, edges, device=0, with_edges=True):
                                       L.ptr(bpose), L.ptr(hpoint), L.ptr(bpoint)),
             "orbg_ba_linearize")
     return eout, hpose, bpose, hpoint, bpoint
+
+
+def PoseOptimization(edges, Tcw, fx, fy, cx, cy, bf, device=0):
+    """Optimizer::PoseOptimization (Optimizer.cc:356-631) on one frame.
+
+    edges: PEDGE_DTYPE records, one per keypoint with a MapPoint in index order (obs =
+    kpUn.pt.x, kpUn.pt.y, mvuRight; xw = world position; inv_sigma2 = mvInvLevelSigma2
+    [octave]; stereo = mvuRight >= 0).  Tcw: pFrame->mTcw (3x4 or 4x4).  Returns
+    (nInliers, Tcw_out (3, 4) float32 = SetPose's matrix, q (x, y, z, w), t, mvbOutlier)."""
+    e = np.ascontiguousarray(edges, L.PEDGE_DTYPE)
+    T = np.ascontiguousarray(np.asarray(Tcw, np.float32)[:3, :4].reshape(12))
+    cam = L.PoseCamera(*[float(np.float32(v)) for v in (fx, fy, cx, cy, bf)], 0.0)
+    q = np.zeros(4)
+    t = np.zeros(3)
+    To = np.zeros(12, np.float32)
+    out = np.zeros(max(len(e), 1), np.uint8)
+    ni = ctypes.c_int()
+    L.check(L.lib().orbg_pose_optimization(_ctx(device).handle, L.ptr(e), len(e), ctypes.byref(cam),
+                                           L.ptr(T), L.ptr(q), L.ptr(t), L.ptr(To), L.ptr(out),
+                                           ctypes.byref(ni)), "orbg_pose_optimization")
+    return ni.value, To.reshape(3, 4), q, t, out[:len(e)].astype(bool)
 
 
 def vertex_csr(edges, field, nvert):
