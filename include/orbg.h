@@ -220,8 +220,8 @@ int orbg_search_for_initialization(orbg_ctx *ctx, const orbg_keypoint *kps1,
 
 /* ---------------- tracking matchers ----------------
  * The MapPoint / Frame state the two SearchByProjection loops read enters as flat records;
- * their writes come back as match[N] (CurrentFrame.mvpMapPoints as a query index, -1 =
- * NULL / untouched) and nmatches.  The frame side is CurrentFrame (F): kps = mvKeysUn,
+ * their writes come back as match[N] (CurrentFrame.mvpMapPoints as a query index; -1 = not
+ * written; -2 = set to NULL by the rotation-consistency filter) and nmatches.  The frame side is CurrentFrame (F): kps = mvKeysUn,
  * desc = mDescriptors, uright = mvuRight (NULL for monocular), taken0 (NULL = none) =
  * "mvpMapPoints[i] && mvpMapPoints[i]->Observations() > 0" on entry, bounds = mnMinX...
  * Scale factors are the context's (ORBextractor GetScaleFactors). */

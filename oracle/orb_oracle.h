@@ -167,7 +167,8 @@ void orc_gemm3(const float *R, int transR, const float *x, float alpha, const fl
                float *out);
 /* bForward / bBackward of ORBmatcher.cc:1521-1522 */
 void orc_track_direction(const orc_track_cam *cam, int *forward, int *backward);
-/* match[n]: CurrentFrame.mvpMapPoints as a LastFrame point index (-1 = NULL); taken0 (may
+/* match[n]: CurrentFrame.mvpMapPoints as a LastFrame point index (-1 = not written, -2 =
+ * NULLed by the rotation filter); taken0 (may
  * be NULL): initial mvpMapPoints[i] && Observations() > 0.  Returns nmatches. */
 int orc_search_by_projection_lastframe(const orc_keypoint *kps, const uint8_t *desc,
                                        const float *uright, int n, const uint8_t *taken0,

@@ -160,7 +160,7 @@ int orc_search_by_projection_lastframe(const orc_keypoint *kps, const uint8_t *d
         for (int k = 0; k < npush; k++) {
             const int bn = push_bin[k];
             if (bn != ind1 && bn != ind2 && bn != ind3) {
-                match[push_idx[k]] = -1;
+                match[push_idx[k]] = -2; /* NULLed by the rotation filter */
                 nmatches--;
             }
         }

@@ -599,7 +599,7 @@ __global__ __launch_bounds__(TRK_RT) void k_track_resolve(TrackArgs A)
         for (int k = tid; k < np; k += TRK_RT) {
             const int e = push[k], bn = e & 0xFF;
             if (bn != ind1 && bn != ind2 && bn != ind3) {
-                match[e >> 8] = -1;  // same value from every writer: no ordering needed
+                match[e >> 8] = -2;  // NULLed by the rotation filter (same value from every writer)
                 removed++;
             }
         }

@@ -124,8 +124,8 @@ class ORBmatcher:
         """SearchByProjection(CurrentFrame, LastFrame, th, bMono) (ORBmatcher.cc:1503-1667)
         when `second` is a Frame carrying `points`, SearchByProjection(F, vpMapPoints, th)
         (:59-146) when it is a MapPointProjections.  Returns (nmatches, match): match[i] is
-        the LastFrame keypoint / map point index written to F.mvpMapPoints[i], -1 for
-        NULL / untouched."""
+        the LastFrame keypoint / map point index written to F.mvpMapPoints[i], -1 where the
+        call wrote nothing, -2 where the rotation filter set the slot to NULL."""
         kps = np.ascontiguousarray(F.mvKeysUn, L.KP_DTYPE)
         desc = np.ascontiguousarray(F.mDescriptors, np.uint8)
         ur = None if F.mvuRight is None else np.ascontiguousarray(F.mvuRight, np.float32)
