@@ -367,8 +367,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(6, 8))) voi
     // unit u = ry * RG + gg walked as u = lane + 64 k: (ry, gg) advance by (64 / RG, 64 % RG)
     const int rstep = RG > 0 ? 64 / RG : 0, gstep = RG > 0 ? 64 - rstep * RG : 0;
     const int ry0 = RG > 0 ? lane / RG : 0, gg0 = lane - ry0 * RG;
-    // ---- scores ----
-    for (int u = lane, ry = ry0, gg = gg0; u < nunits; u += 64) {
+    // unit (ry, gg): its 7 window rows x 3 dwords, both pixel pairs scored, word -> sc
+    auto score_unit = [&](int ry, int gg) {
         Rows7 R;
 #pragma unroll
         for (int r = 0; r < 7; r++) {
@@ -384,76 +384,150 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(6, 8))) voi
         const int valid = min(RW - 4 * gg, 4);
         if (valid < 4) word &= (1u << (8 * valid)) - 1u;
         *(uint32_t *)(sc + (ry + 1) * P + 4 * gg + 4) = word;
-        ry += rstep;
-        gg += gstep;
-        if (gg >= RG) {
-            gg -= RG;
-            ry++;
+    };
+    const int thi = g->ini_th, tlo = g->min_th;
+    // ---- compass pretest at iniThFAST + compaction ----
+    // A corner at th has 9 contiguous circle pixels all brighter than v + th or all darker
+    // than v - th; any 9-arc holds two adjacent compass points (circle 0/4, 4/8, 8/12,
+    // 12/0), so "both brighter" or "both darker" for some adjacent pair is necessary.  Only
+    // units with a pixel passing it are scored; the others keep score 0, which the NMS at
+    // iniThFAST treats exactly like any score below th (a neighbour < th never blocks).
+    // Pixel pairs in packed i16 lanes: mb = max over pairs of min(ca, cb) (> v + th <=>
+    // some pair brighter), md = min over pairs of max(ca, cb) (< v - th <=> darker).
+    uint16_t *plist = (uint16_t *)(tile + g->fc_list_off);
+    int npass = 0;
+    {
+        const v2s vth1 = (v2s){(short)(thi + 1), (short)(thi + 1)};
+        // uniform trip count: the scan below is wave-wide
+        for (int u0 = 0, ry = ry0, gg = gg0; u0 < nunits; u0 += 64) {
+            const int u = u0 + lane;
+            uint32_t pm = 0;
+            if (u < nunits) {
+                uint32_t r0[3], r3[3], r6[3];
+                const uint32_t *p0 = (const uint32_t *)(tile + ry * P + 4 * gg);
+                const uint32_t *p3 = (const uint32_t *)(tile + (ry + 3) * P + 4 * gg);
+                const uint32_t *p6 = (const uint32_t *)(tile + (ry + 6) * P + 4 * gg);
+#pragma unroll
+                for (int k = 0; k < 3; k++) {
+                    r0[k] = p0[k];
+                    r3[k] = p3[k];
+                    r6[k] = p6[k];
+                }
+                auto pretest = [&](auto I) -> uint32_t {
+                    constexpr int i = decltype(I)::value;
+                    const v2s v = gather2<4 + i>(r3[0], r3[1], r3[2]);
+                    const v2s c0 = gather2<4 + i>(r6[0], r6[1], r6[2]);
+                    const v2s c4 = gather2<7 + i>(r3[0], r3[1], r3[2]);
+                    const v2s c8 = gather2<4 + i>(r0[0], r0[1], r0[2]);
+                    const v2s c12 = gather2<1 + i>(r3[0], r3[1], r3[2]);
+                    const v2s mb = pmax(pmax(pmin(c0, c4), pmin(c4, c8)),
+                                        pmax(pmin(c8, c12), pmin(c12, c0)));
+                    const v2s md = pmin(pmin(pmax(c0, c4), pmax(c4, c8)),
+                                        pmin(pmax(c8, c12), pmax(c12, c0)));
+                    const v2s k = pmax(mb - v, v - md) - vth1;  // >= 0 <=> pass
+                    const uint32_t w = __builtin_bit_cast(uint32_t, k);
+                    return (~w >> 15 & 1u) | (~w >> 30 & 2u);
+                };
+                pm = pretest(std::integral_constant<int, 0>{}) |
+                     pretest(std::integral_constant<int, 2>{}) << 2;
+                const int valid = min(RW - 4 * gg, 4);
+                if (valid < 4) pm &= (1u << valid) - 1u;
+            }
+            int tot;
+            const int incl = wave_incl_scan_small(pm ? 1 : 0, &tot);
+            if (pm) plist[npass + incl - 1] = (uint16_t)(ry << 8 | gg);
+            npass += tot;
+            ry += rstep;
+            gg += gstep;
+            if (gg >= RG) {
+                gg -= RG;
+                ry++;
+            }
         }
+    }
+    wave_sync_lds();
+    // ---- scores of the pretest survivors (dense over lanes) ----
+    for (int j = lane; j < npass; j += 64) {
+        const int e = plist[j];
+        score_unit(e >> 8, e & 0xFF);
     }
     wave_sync_lds();
     if (g->dbg == 12) return;
 
-    // ---- NMS (cell-local), both thresholds in one pass ----
+    // ---- NMS (cell-local) ----
     // cv::FAST keeps p iff s_p > every neighbour's score, a neighbour that is not a corner
     // at the cell threshold th counting as 0.  With s_p >= max(th, 1) that is exactly
     //   max(raw 8-neighbour scores) < max(th, s_p)
     // (a neighbour q < th is always below max(th, s_p); one with q >= th must be < s_p).
-    // Pixel pairs in packed u16 lanes; the mask byte of unit u (low nibble at iniThFAST,
-    // high nibble at minThFAST) goes to the window tile, which is free by now.
-    uint8_t *mk = tile;
-    const int thi = g->ini_th, tlo = g->min_th;
-    const v2s vt1h = (v2s){(short)max(thi, 1), (short)max(thi, 1)};
-    const v2s vt1l = (v2s){(short)max(tlo, 1), (short)max(tlo, 1)};
-    const v2s vthh = (v2s){(short)thi, (short)thi}, vthl = (v2s){(short)tlo, (short)tlo};
+    // Pixel pairs in packed u16 lanes; the keep bits of unit u go to mk[u] (the pretest
+    // list's LDS, free by now).
+    uint8_t *mk = (uint8_t *)plist;
     const v2s one = (v2s){1, 1};
-    int cnt_hi = 0;
-    for (int u = lane, ry = ry0, gg = gg0; u < nunits; u += 64) {
-        const uint32_t *mu = (const uint32_t *)(sc + ry * P + 4 * gg);
-        const uint32_t *m0 = (const uint32_t *)(sc + (ry + 1) * P + 4 * gg);
-        const uint32_t *md = (const uint32_t *)(sc + (ry + 2) * P + 4 * gg);
-        const uint32_t c1 = m0[1];
-        uint32_t mbyte = 0;
-        if (c1 != 0) {  // a unit with no scored pixel keeps nothing at any threshold
-            const uint32_t u0 = mu[0], u1 = mu[1], u2 = mu[2];
-            const uint32_t c0 = m0[0], c2 = m0[2];
-            const uint32_t d0 = md[0], d1 = md[1], d2 = md[2];
-            // pixels 0,1 (bytes 4,5): neighbours at bytes 3..6
-            v2s mA = pmax(pmax(gather2<3>(u0, u1, u2), gather2<4>(u0, u1, u2)),
-                          gather2<5>(u0, u1, u2));
-            mA = pmax(mA, pmax(pmax(gather2<3>(d0, d1, d2), gather2<4>(d0, d1, d2)),
-                               gather2<5>(d0, d1, d2)));
-            mA = pmax(mA, pmax(gather2<3>(c0, c1, c2), gather2<5>(c0, c1, c2)));
-            // pixels 2,3 (bytes 6,7): neighbours at bytes 5..8
-            v2s mB = pmax(pmax(gather2<5>(u0, u1, u2), gather2<6>(u0, u1, u2)),
-                          gather2<7>(u0, u1, u2));
-            mB = pmax(mB, pmax(pmax(gather2<5>(d0, d1, d2), gather2<6>(d0, d1, d2)),
-                               gather2<7>(d0, d1, d2)));
-            mB = pmax(mB, pmax(gather2<5>(c0, c1, c2), gather2<7>(c0, c1, c2)));
-            const v2s sA = gather2<4>(c0, c1, c2), sB = gather2<6>(c0, c1, c2);
-            // keep <=> min(s - t1, max(th, s) - M - 1) >= 0: sign bit of each u16 lane
-            auto keep = [&](v2s sv, v2s m, v2s t1v, v2s thv) -> uint32_t {
-                const v2s k = pmin(sv - t1v, pmax(thv, sv) - m - one);
-                const uint32_t w = __builtin_bit_cast(uint32_t, k);
-                return (~w >> 15 & 1u) | (~w >> 30 & 2u);
-            };
-            const uint32_t kh = keep(sA, mA, vt1h, vthh) | keep(sB, mB, vt1h, vthh) << 2;
-            const uint32_t kl = keep(sA, mA, vt1l, vthl) | keep(sB, mB, vt1l, vthl) << 2;
-            const int valid = min(RW - 4 * gg, 4);
-            const uint32_t vm = valid < 4 ? (1u << valid) - 1u : 0xFu;
-            mbyte = (kh & vm) | (kl & vm) << 4;
-            cnt_hi += __popc(kh & vm);
+    auto nms = [&](int th) -> int {
+        const v2s t1v = (v2s){(short)max(th, 1), (short)max(th, 1)};
+        const v2s thv = (v2s){(short)th, (short)th};
+        int cnt = 0;
+        for (int u = lane, ry = ry0, gg = gg0; u < nunits; u += 64) {
+            const uint32_t *mu = (const uint32_t *)(sc + ry * P + 4 * gg);
+            const uint32_t *m0 = (const uint32_t *)(sc + (ry + 1) * P + 4 * gg);
+            const uint32_t *md = (const uint32_t *)(sc + (ry + 2) * P + 4 * gg);
+            const uint32_t c1 = m0[1];
+            uint32_t kb = 0;
+            if (c1 != 0) {  // a unit with no scored pixel keeps nothing
+                const uint32_t u0 = mu[0], u1 = mu[1], u2 = mu[2];
+                const uint32_t c0 = m0[0], c2 = m0[2];
+                const uint32_t d0 = md[0], d1 = md[1], d2 = md[2];
+                // pixels 0,1 (bytes 4,5): neighbours at bytes 3..6
+                v2s mA = pmax(pmax(gather2<3>(u0, u1, u2), gather2<4>(u0, u1, u2)),
+                              gather2<5>(u0, u1, u2));
+                mA = pmax(mA, pmax(pmax(gather2<3>(d0, d1, d2), gather2<4>(d0, d1, d2)),
+                                   gather2<5>(d0, d1, d2)));
+                mA = pmax(mA, pmax(gather2<3>(c0, c1, c2), gather2<5>(c0, c1, c2)));
+                // pixels 2,3 (bytes 6,7): neighbours at bytes 5..8
+                v2s mB = pmax(pmax(gather2<5>(u0, u1, u2), gather2<6>(u0, u1, u2)),
+                              gather2<7>(u0, u1, u2));
+                mB = pmax(mB, pmax(pmax(gather2<5>(d0, d1, d2), gather2<6>(d0, d1, d2)),
+                                   gather2<7>(d0, d1, d2)));
+                mB = pmax(mB, pmax(gather2<5>(c0, c1, c2), gather2<7>(c0, c1, c2)));
+                const v2s sA = gather2<4>(c0, c1, c2), sB = gather2<6>(c0, c1, c2);
+                // keep <=> min(s - t1, max(th, s) - M - 1) >= 0: sign bit of each u16 lane
+                auto keep = [&](v2s sv, v2s m) -> uint32_t {
+                    const v2s k = pmin(sv - t1v, pmax(thv, sv) - m - one);
+                    const uint32_t w = __builtin_bit_cast(uint32_t, k);
+                    return (~w >> 15 & 1u) | (~w >> 30 & 2u);
+                };
+                kb = keep(sA, mA) | keep(sB, mB) << 2;
+                const int valid = min(RW - 4 * gg, 4);
+                if (valid < 4) kb &= (1u << valid) - 1u;
+                cnt += __popc(kb);
+            }
+            mk[u] = (uint8_t)kb;
+            ry += rstep;
+            gg += gstep;
+            if (gg >= RG) {
+                gg -= RG;
+                ry++;
+            }
         }
-        mk[u] = (uint8_t)mbyte;
-        ry += rstep;
-        gg += gstep;
-        if (gg >= RG) {
-            gg -= RG;
-            ry++;
-        }
-    }
+        return wave_sum(cnt);
+    };
     // FAST at iniThFAST; an empty cell retries at minThFAST (ORBextractor.cc:1069-1075)
-    const int nib = wave_sum(cnt_hi) > 0 ? 0 : 4;
+    // with every unit scored (the window tile is still intact)
+    if (nms(thi) == 0) {
+        wave_sync_lds();
+        for (int u = lane, ry = ry0, gg = gg0; u < nunits; u += 64) {
+            score_unit(ry, gg);
+            ry += rstep;
+            gg += gstep;
+            if (gg >= RG) {
+                gg -= RG;
+                ry++;
+            }
+        }
+        wave_sync_lds();
+        nms(tlo);
+    }
+    const int nib = 0;
     wave_sync_lds();
     if (g->dbg == 13) return;
 

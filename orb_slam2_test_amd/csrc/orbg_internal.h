@@ -63,7 +63,8 @@ struct OrbgGeom {
     int32_t dbg;                  // developer timing knob (ORBG_DBG env), 0 in production
     int32_t fc_pitch;             // k_fast_cells LDS row pitch (bytes)
     int32_t fc_tile_rows;         // max FAST window height
-    int32_t fc_wave_bytes;        // LDS bytes per wave (window + score tiles)
+    int32_t fc_wave_bytes;        // LDS bytes per wave (window + score tiles + unit list)
+    int32_t fc_list_off;          // byte offset of the pretest unit list in a wave's LDS
     int32_t gk[7];
     int64_t pyr_frame;            // bytes per frame of d_pyr
     int64_t blur_frame;
