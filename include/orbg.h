@@ -29,6 +29,8 @@
  *   orbg_search_by_projection_local . ORBmatcher(nnratio).SearchByProjection(F, vpMapPoints, th)
  *                                                                      src/ORBmatcher.cc:59-154
  *   orbg_pose_optimization .......... Optimizer::PoseOptimization(Frame*)  src/Optimizer.cc:356-631
+ *   orbg_ba_schur_solve ............. g2o BlockSolver<6,3>::solve (Schur complement + pose solve)
+ *                                     Thirdparty/g2o/g2o/core/block_solver.hpp:354-486
  *   orbg_ba_linearize ............... g2o computeActiveErrors + BlockSolver::buildSystem arithmetic
  *                                     for EdgeSE3ProjectXYZ / EdgeStereoSE3ProjectXYZ inside
  *                                     Optimizer::LocalBundleAdjustment  src/Optimizer.cc:633-979
@@ -371,6 +373,18 @@ int orbg_ba_linearize_device(orbg_ctx *ctx, const orbg_pose *d_poses, int npose,
                              const int32_t *d_point_off, const int32_t *d_point_edges,
                              orbg_edge_out *d_eout, double *d_hpose, double *d_bpose,
                              double *d_hpoint, double *d_bpoint);
+
+/* g2o BlockSolver<6,3>::solve with the Schur complement (Thirdparty/g2o/g2o/core/
+ * block_solver.hpp:354-486) for one LocalBundleAdjustment window, after setLambda(lambda):
+ * inputs are orbg_ba_linearize's outputs (eout[e].hpl = H_pl^T of edge e) for the same
+ * poses / edges; only active edges and non-fixed poses take part.  dx_pose[npose*6] (0 for
+ * fixed poses), dx_point[npoint*3] (0 for points without an active edge); *ok = the linear
+ * solver's success (0: increments are zero). */
+int orbg_ba_schur_solve(orbg_ctx *ctx, const orbg_pose *poses, int npose, int npoint,
+                        const orbg_edge *edges, int nedge, const orbg_edge_out *eout,
+                        const double *hpose, const double *bpose, const double *hpoint,
+                        const double *bpoint, double lambda, double *dx_pose, double *dx_point,
+                        int *ok);
 
 #ifdef __cplusplus
 }

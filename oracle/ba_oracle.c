@@ -16,6 +16,7 @@
 #include "orb_oracle.h"
 
 #include <math.h>
+#include <stdlib.h>
 #include <string.h>
 
 static void quat_rotate(const double q[4], const double v[3], double out[3])
@@ -295,4 +296,198 @@ void orc_ba_numeric_jacobian(const orc_pose *pose, const double *xyz, const orc_
         for (int k = 0; k < 3; k++)
             jt[k][d] = scalar * (ep[k] - em[k]);
     }
+}
+
+/* ---- BlockSolver<6,3>::solve with Schur complement (block_solver.hpp:354-486) ----
+ * Pinned orders (see orb_oracle.h): landmarks in index order, a landmark's blocks in
+ * ascending pose order, every small product summed in index order, Hschur blocks updated
+ * landmark by landmark ("S -= BDinv Bj^T").  Eigen's 3x3 inverse (cofactors / det).  The
+ * pose system is solved by a dense LDLT without pivoting in natural order (g2o's
+ * LinearSolverEigen runs Eigen's SimplicialLDLT with an AMD ordering: unpinned). */
+static void inv3_eigen(const double m[9], double r[9])
+{
+#define M(i, j) m[(i) * 3 + (j)]
+#define COF(i, j) (M(((i) + 1) % 3, ((j) + 1) % 3) * M(((i) + 2) % 3, ((j) + 2) % 3) - \
+                   M(((i) + 1) % 3, ((j) + 2) % 3) * M(((i) + 2) % 3, ((j) + 1) % 3))
+    const double c0 = COF(0, 0), c1 = COF(1, 0), c2 = COF(2, 0);
+    const double det = (c0 * M(0, 0) + c1 * M(1, 0)) + c2 * M(2, 0);
+    const double invdet = 1.0 / det;
+    r[0] = c0 * invdet;
+    r[1] = c1 * invdet;
+    r[2] = c2 * invdet;
+    r[3] = COF(0, 1) * invdet;
+    r[4] = COF(1, 1) * invdet;
+    r[5] = COF(2, 1) * invdet;
+    r[6] = COF(0, 2) * invdet;
+    r[7] = COF(1, 2) * invdet;
+    r[8] = COF(2, 2) * invdet;
+#undef COF
+#undef M
+}
+
+/* dense LDLT (no pivoting), A n x n row-major (lower triangle read), solve in place */
+int orc_ldlt_dense_solve(double *A, int n, double *x)
+{
+    for (int j = 0; j < n; j++) {
+        double d = A[j * n + j];
+        for (int k = 0; k < j; k++)
+            d -= A[j * n + k] * A[j * n + k] * A[k * n + k];
+        A[j * n + j] = d;
+        if (d == 0.0 || !isfinite(d))
+            return 0;
+        for (int i = j + 1; i < n; i++) {
+            double s = A[i * n + j];
+            for (int k = 0; k < j; k++)
+                s -= A[i * n + k] * A[j * n + k] * A[k * n + k];
+            A[i * n + j] = s / d;
+        }
+    }
+    for (int i = 0; i < n; i++) { /* L y = b */
+        double s = x[i];
+        for (int k = 0; k < i; k++)
+            s -= A[i * n + k] * x[k];
+        x[i] = s;
+    }
+    for (int i = 0; i < n; i++)
+        x[i] /= A[i * n + i];
+    for (int i = n - 1; i >= 0; i--) { /* L^T x = y */
+        double s = x[i];
+        for (int k = i + 1; k < n; k++)
+            s -= A[k * n + i] * x[k];
+        x[i] = s;
+    }
+    return 1;
+}
+
+int orc_ba_schur_solve(const orc_pose *poses, int npose, int npoint, const orc_edge *edges,
+                       int nedge, const orc_edge_out *eout, const double *hpose,
+                       const double *bpose, const double *hpoint, const double *bpoint,
+                       double lambda, double *dx_pose, double *dx_point)
+{
+    /* free poses -> Schur index; points with an active edge to a free or fixed pose */
+    int *pidx = (int *)malloc(sizeof(int) * (npose > 0 ? npose : 1));
+    int nfree = 0;
+    for (int i = 0; i < npose; i++)
+        pidx[i] = poses[i].fixed ? -1 : nfree++;
+    /* active edges per point, ascending pose (at most one edge per (pose, point)) */
+    int *cnt = (int *)calloc((size_t)npoint + 1, sizeof(int));
+    for (int e = 0; e < nedge; e++)
+        if (edges[e].active)
+            cnt[edges[e].point + 1]++;
+    for (int i = 0; i < npoint; i++)
+        cnt[i + 1] += cnt[i];
+    int *lst = (int *)malloc(sizeof(int) * (nedge > 0 ? nedge : 1));
+    int *fill = (int *)malloc(sizeof(int) * (npoint > 0 ? npoint : 1));
+    memcpy(fill, cnt, sizeof(int) * (npoint > 0 ? npoint : 1));
+    for (int e = 0; e < nedge; e++)
+        if (edges[e].active)
+            lst[fill[edges[e].point]++] = e;
+    for (int p = 0; p < npoint; p++) /* insertion sort by pose */
+        for (int a = cnt[p] + 1; a < cnt[p + 1]; a++) {
+            const int v = lst[a];
+            int b = a - 1;
+            while (b >= cnt[p] && edges[lst[b]].pose > edges[v].pose) {
+                lst[b + 1] = lst[b];
+                b--;
+            }
+            lst[b + 1] = v;
+        }
+    const int n = 6 * nfree;
+    double *S = (double *)calloc((size_t)n * n + 1, sizeof(double));
+    double *coef = (double *)calloc((size_t)n + 1, sizeof(double));
+    double *Dinv = (double *)malloc(sizeof(double) * 9 * (npoint > 0 ? npoint : 1));
+    /* Hschur = Hpp + lambda (diagonal blocks) */
+    for (int i = 0; i < npose; i++) {
+        if (pidx[i] < 0)
+            continue;
+        const int o = 6 * pidx[i];
+        for (int r = 0; r < 6; r++)
+            for (int c = 0; c < 6; c++)
+                S[(o + r) * n + o + c] = hpose[36 * (size_t)i + r * 6 + c] + (r == c ? lambda : 0.0);
+    }
+    for (int p = 0; p < npoint; p++) {
+        double D[9];
+        for (int k = 0; k < 9; k++)
+            D[k] = hpoint[9 * (size_t)p + k];
+        D[0] += lambda;
+        D[4] += lambda;
+        D[8] += lambda;
+        double *Di = Dinv + 9 * (size_t)p;
+        if (cnt[p + 1] == cnt[p]) { /* no active edge: not in the optimisation */
+            memset(Di, 0, sizeof(double) * 9);
+            continue;
+        }
+        inv3_eigen(D, Di);
+        const double *bl = bpoint + 3 * (size_t)p;
+        double db[3];
+        for (int r = 0; r < 3; r++)
+            db[r] = (Di[r * 3] * bl[0] + Di[r * 3 + 1] * bl[1]) + Di[r * 3 + 2] * bl[2];
+        for (int a = cnt[p]; a < cnt[p + 1]; a++) {
+            const int e1 = lst[a], i1 = pidx[edges[e1].pose];
+            if (i1 < 0)
+                continue;
+            const double (*h1)[6] = eout[e1].hpl; /* Bi = h1^T (6 x 3) */
+            double BD[6][3];
+            for (int r = 0; r < 6; r++)
+                for (int c = 0; c < 3; c++)
+                    BD[r][c] = (h1[0][r] * Di[c] + h1[1][r] * Di[3 + c]) + h1[2][r] * Di[6 + c];
+            for (int r = 0; r < 6; r++)
+                coef[6 * i1 + r] += (h1[0][r] * db[0] + h1[1][r] * db[1]) + h1[2][r] * db[2];
+            for (int b2 = a; b2 < cnt[p + 1]; b2++) {
+                const int e2 = lst[b2], i2 = pidx[edges[e2].pose];
+                if (i2 < 0)
+                    continue;
+                const double (*h2)[6] = eout[e2].hpl;
+                for (int r = 0; r < 6; r++)
+                    for (int c = 0; c < 6; c++)
+                        S[(6 * i1 + r) * n + 6 * i2 + c] -=
+                            (BD[r][0] * h2[0][c] + BD[r][1] * h2[1][c]) + BD[r][2] * h2[2][c];
+            }
+        }
+    }
+    /* symmetric: lower blocks mirror the upper ones */
+    for (int r = 0; r < n; r++)
+        for (int c = 0; c < r; c++)
+            S[r * n + c] = S[c * n + r];
+    double *xp = (double *)calloc((size_t)n + 1, sizeof(double));
+    for (int i = 0; i < npose; i++)
+        if (pidx[i] >= 0)
+            for (int r = 0; r < 6; r++)
+                xp[6 * pidx[i] + r] = bpose[6 * (size_t)i + r] - coef[6 * pidx[i] + r];
+    const int ok = n == 0 ? 1 : orc_ldlt_dense_solve(S, n, xp);
+    for (int i = 0; i < npose; i++)
+        for (int r = 0; r < 6; r++)
+            dx_pose[6 * (size_t)i + r] = (ok && pidx[i] >= 0) ? xp[6 * pidx[i] + r] : 0.0;
+    for (int p = 0; p < npoint; p++) {
+        double *xl = dx_point + 3 * (size_t)p;
+        xl[0] = xl[1] = xl[2] = 0.0;
+        if (!ok || cnt[p + 1] == cnt[p])
+            continue;
+        const double *bl = bpoint + 3 * (size_t)p;
+        double cl[3] = {bl[0], bl[1], bl[2]};
+        for (int a = cnt[p]; a < cnt[p + 1]; a++) {
+            const int e1 = lst[a], i1 = pidx[edges[e1].pose];
+            if (i1 < 0)
+                continue;
+            const double (*h1)[6] = eout[e1].hpl;
+            for (int k = 0; k < 3; k++) {
+                double s = 0;
+                for (int r = 0; r < 6; r++)
+                    s += h1[k][r] * -xp[6 * i1 + r];
+                cl[k] += s;
+            }
+        }
+        const double *Di = Dinv + 9 * (size_t)p;
+        for (int r = 0; r < 3; r++)
+            xl[r] = (Di[r * 3] * cl[0] + Di[r * 3 + 1] * cl[1]) + Di[r * 3 + 2] * cl[2];
+    }
+    free(pidx);
+    free(cnt);
+    free(lst);
+    free(fill);
+    free(S);
+    free(coef);
+    free(Dinv);
+    free(xp);
+    return ok;
 }

@@ -253,6 +253,15 @@ typedef struct {
 void orc_ba_linearize(const orc_pose *poses, int npose, const double *points, int npoint,
                       const orc_edge *edges, int nedge, orc_edge_out *eout, double *hpose,
                       double *bpose, double *hpoint, double *bpoint);
+/* BlockSolver_6_3::solve with the Schur complement (block_solver.hpp:354-486) after
+ * setLambda(lambda): inputs are orc_ba_linearize's outputs (hpl = A^T W B per edge).
+ * dx_pose[npose*6] (0 for fixed poses), dx_point[npoint*3] (0 for points without an
+ * active edge).  Returns the linear solver's success. */
+int orc_ba_schur_solve(const orc_pose *poses, int npose, int npoint, const orc_edge *edges,
+                       int nedge, const orc_edge_out *eout, const double *hpose,
+                       const double *bpose, const double *hpoint, const double *bpoint,
+                       double lambda, double *dx_pose, double *dx_point);
+int orc_ldlt_dense_solve(double *A, int n, double *x);
 /* central-difference Jacobian of computeError (base_binary_edge.hpp:131-205, delta 1e-9) */
 void orc_ba_numeric_jacobian(const orc_pose *pose, const double *xyz, const orc_edge *e,
                              double jp[3][3], double jt[3][6]);

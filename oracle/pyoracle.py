@@ -127,6 +127,8 @@ def lib():
         L.orc_extract_batch.restype = C.c_long
         L.orc_ba_linearize.argtypes = [vp, C.c_int, vp, C.c_int, vp, C.c_int, vp, vp, vp, vp, vp]
         L.orc_ba_numeric_jacobian.argtypes = [vp, vp, vp, vp, vp]
+        L.orc_ba_schur_solve.argtypes = [vp, C.c_int, C.c_int, vp, C.c_int, vp, vp, vp, vp, vp,
+                                         C.c_double, vp, vp]
         L.orc_stereo_matches.argtypes = [P(Params), vp, vp, C.c_int, vp, vp, C.c_int, vp, vp,
                                          C.c_int, C.c_int, C.c_float, C.c_float, vp, vp]
         L.orc_track_direction.argtypes = [vp, vp, vp]
@@ -380,3 +382,18 @@ def pose_optimization(edges, cam, Tcw):
     n = lib().orc_pose_optimization(_p(e), len(e), C.byref(c), _p(T), _p(q), _p(t), _p(To),
                                     _p(out))
     return n, q, t, To.reshape(3, 4), out[:len(e)].astype(bool)
+
+
+def ba_schur_solve(poses, npoint, edges, eout, hpose, bpose, hpoint, bpoint, lam):
+    """g2o BlockSolver_6_3::solve (Schur) after setLambda(lam) on ba_linearize's outputs.
+    Returns (ok, dx_pose (npose, 6), dx_point (npoint, 3))."""
+    poses = np.ascontiguousarray(poses, POSE_DTYPE)
+    edges = np.ascontiguousarray(edges, EDGE_DTYPE)
+    eout = np.ascontiguousarray(eout, EDGE_OUT_DTYPE)
+    hp, bp = np.ascontiguousarray(hpose, np.float64), np.ascontiguousarray(bpose, np.float64)
+    hq, bq = np.ascontiguousarray(hpoint, np.float64), np.ascontiguousarray(bpoint, np.float64)
+    dp = np.zeros((max(len(poses), 1), 6))
+    dq = np.zeros((max(npoint, 1), 3))
+    ok = lib().orc_ba_schur_solve(_p(poses), len(poses), npoint, _p(edges), len(edges), _p(eout),
+                                  _p(hp), _p(bp), _p(hq), _p(bq), float(lam), _p(dp), _p(dq))
+    return bool(ok), dp[:len(poses)], dq[:npoint]

@@ -161,6 +161,8 @@ def lib():
         "orbg_pose_optimization": (i32, [vp, vp, i32, P(PoseCamera), vp, vp, vp, vp, vp, P(i32)]),
         "orbg_pose_optimization_batch_device": (i32, [vp, vp, vp, i32, vp, vp, vp, vp, vp, vp, vp,
                                                       i32]),
+        "orbg_ba_schur_solve": (i32, [vp, vp, i32, i32, vp, i32, vp, vp, vp, vp, vp, C.c_double, vp,
+                                      vp, P(i32)]),
         "orbg_ba_linearize": (i32, [vp, vp, i32, vp, i32, vp, i32, vp, vp, vp, vp, vp]),
         "orbg_ba_linearize_device": (i32, [vp, vp, i32, vp, i32, vp, i32, vp, vp, vp, vp, vp, vp,
                                            vp, vp, vp]),

@@ -16,6 +16,7 @@
 #include "../../include/orbg.h"
 #include "orbg_internal.h"
 #include "track_args.h"
+#include "schur_args.h"
 
 #pragma clang fp contract(off)
 
@@ -1741,5 +1742,157 @@ extern "C" int orbg_pose_optimization(orbg_ctx *c, const orbg_pose_edge *edges, 
     HIPCHK(hipStreamSynchronize(c->stream));
     c->prof.collect();
     if (ninliers) *ninliers = ni;
+    return ORBG_OK;
+}
+
+// ---------------------------------------------------------------------------
+// LocalBundleAdjustment: BlockSolver<6,3>::solve (Schur complement)
+// ---------------------------------------------------------------------------
+extern "C" int orbg_ba_schur_solve(orbg_ctx *c, const orbg_pose *poses, int npose, int npoint,
+                                   const orbg_edge *edges, int nedge, const orbg_edge_out *eout,
+                                   const double *hpose, const double *bpose,
+                                   const double *hpoint, const double *bpoint, double lambda,
+                                   double *dx_pose, double *dx_point, int *ok)
+{
+    if (!c || !ok || npose < 0 || npoint < 0 || nedge < 0)
+        return set_err(ORBG_EINVAL, "NULL argument or negative size");
+    if ((npose && (!poses || !hpose || !bpose || !dx_pose)) ||
+        (npoint && (!hpoint || !bpoint || !dx_point)) || (nedge && (!edges || !eout)))
+        return set_err(ORBG_EINVAL, "NULL array");
+    for (int e = 0; e < nedge; e++)
+        if (edges[e].pose < 0 || edges[e].pose >= npose || edges[e].point < 0 ||
+            edges[e].point >= npoint)
+            return set_err(ORBG_EINVAL, "edge %d references a missing vertex", e);
+    HIPCHK(hipSetDevice(c->device));
+    // ---- host structure (the graph is fixed across LM iterations) ----
+    std::vector<int32_t> pidx(std::max(npose, 1));
+    int nfree = 0;
+    for (int i = 0; i < npose; i++) pidx[i] = poses[i].fixed ? -1 : nfree++;
+    std::vector<int32_t> pt_off(npoint + 1, 0), pt_edges, edge_pose(std::max(nedge, 1));
+    for (int e = 0; e < nedge; e++) {
+        edge_pose[e] = edges[e].pose;
+        if (edges[e].active) pt_off[edges[e].point + 1]++;
+    }
+    for (int i = 0; i < npoint; i++) pt_off[i + 1] += pt_off[i];
+    pt_edges.resize(std::max(pt_off[npoint], 1));
+    {
+        std::vector<int32_t> fill(pt_off.begin(), pt_off.end() - 1);
+        for (int e = 0; e < nedge; e++)
+            if (edges[e].active) pt_edges[fill[edges[e].point]++] = e;
+        for (int p = 0; p < npoint; p++)
+            std::stable_sort(pt_edges.begin() + pt_off[p], pt_edges.begin() + pt_off[p + 1],
+                             [&](int a, int b) { return edges[a].pose < edges[b].pose; });
+    }
+    // upper Schur blocks: all diagonal blocks + every pose pair sharing a landmark; pairs
+    // listed in landmark order
+    std::vector<std::vector<int2>> blists((size_t)nfree * nfree);
+    std::vector<std::vector<int32_t>> pose_lists(nfree);
+    for (int p = 0; p < npoint; p++)
+        for (int a = pt_off[p]; a < pt_off[p + 1]; a++) {
+            const int e1 = pt_edges[a], i1 = pidx[edges[e1].pose];
+            if (i1 < 0) continue;
+            pose_lists[i1].push_back(e1);
+            for (int b = a; b < pt_off[p + 1]; b++) {
+                const int e2 = pt_edges[b], i2 = pidx[edges[e2].pose];
+                if (i2 < 0) continue;
+                blists[(size_t)i1 * nfree + i2].push_back(make_int2(e1, e2));
+            }
+        }
+    std::vector<int32_t> blk_off(1, 0), blk_i1, blk_i2;
+    std::vector<int2> blk_pairs;
+    for (int i1 = 0; i1 < nfree; i1++)
+        for (int i2 = i1; i2 < nfree; i2++) {
+            const auto &l = blists[(size_t)i1 * nfree + i2];
+            if (i1 != i2 && l.empty()) continue;
+            blk_i1.push_back(i1);
+            blk_i2.push_back(i2);
+            blk_pairs.insert(blk_pairs.end(), l.begin(), l.end());
+            blk_off.push_back((int32_t)blk_pairs.size());
+        }
+    std::vector<int32_t> pose_off(nfree + 1, 0), pose_edges;
+    for (int i = 0; i < nfree; i++) {
+        pose_edges.insert(pose_edges.end(), pose_lists[i].begin(), pose_lists[i].end());
+        pose_off[i + 1] = (int32_t)pose_edges.size();
+    }
+    const int nblk = (int)blk_i1.size(), n = 6 * nfree;
+    // ---- device buffers (scratch) ----
+    size_t off = 0;
+    auto take = [&](size_t bytes) {
+        const size_t o = off;
+        off += al256(std::max(bytes, (size_t)1));
+        return o;
+    };
+    const size_t o_pidx = take(pidx.size() * 4), o_ptoff = take(pt_off.size() * 4);
+    const size_t o_pte = take(pt_edges.size() * 4), o_ep = take(edge_pose.size() * 4);
+    const size_t o_boff = take(blk_off.size() * 4), o_bp = take(blk_pairs.size() * 8);
+    const size_t o_bi1 = take(blk_i1.size() * 4), o_bi2 = take(blk_i2.size() * 4);
+    const size_t o_poff = take(pose_off.size() * 4), o_pe = take(pose_edges.size() * 4);
+    const size_t o_eout = take((size_t)nedge * sizeof(orbg_edge_out));
+    const size_t o_hp = take((size_t)npose * 36 * 8), o_bpz = take((size_t)npose * 6 * 8);
+    const size_t o_hq = take((size_t)npoint * 9 * 8), o_bq = take((size_t)npoint * 3 * 8);
+    const size_t o_dinv = take((size_t)npoint * 9 * 8), o_bd = take((size_t)nedge * 18 * 8);
+    const size_t o_cf = take((size_t)nedge * 6 * 8), o_S = take((size_t)n * n * 8);
+    const size_t o_x = take((size_t)n * 8), o_ok = take(4);
+    const size_t o_dp = take((size_t)npose * 6 * 8), o_dq = take((size_t)npoint * 3 * 8);
+    void *sp;
+    int rc = scratch(c, off, &sp);
+    if (rc) return rc;
+    uint8_t *B = (uint8_t *)sp;
+    auto up = [&](size_t o, const void *src, size_t bytes) -> int {
+        if (bytes) HIPCHK(hipMemcpyAsync(B + o, src, bytes, hipMemcpyHostToDevice, c->stream));
+        return ORBG_OK;
+    };
+    if ((rc = up(o_pidx, pidx.data(), pidx.size() * 4)) || (rc = up(o_ptoff, pt_off.data(), pt_off.size() * 4)) ||
+        (rc = up(o_pte, pt_edges.data(), pt_edges.size() * 4)) ||
+        (rc = up(o_ep, edge_pose.data(), (size_t)nedge * 4)) ||
+        (rc = up(o_boff, blk_off.data(), blk_off.size() * 4)) ||
+        (rc = up(o_bp, blk_pairs.data(), blk_pairs.size() * 8)) ||
+        (rc = up(o_bi1, blk_i1.data(), blk_i1.size() * 4)) ||
+        (rc = up(o_bi2, blk_i2.data(), blk_i2.size() * 4)) ||
+        (rc = up(o_poff, pose_off.data(), pose_off.size() * 4)) ||
+        (rc = up(o_pe, pose_edges.data(), pose_edges.size() * 4)) ||
+        (rc = up(o_eout, eout, (size_t)nedge * sizeof(orbg_edge_out))) ||
+        (rc = up(o_hp, hpose, (size_t)npose * 36 * 8)) || (rc = up(o_bpz, bpose, (size_t)npose * 6 * 8)) ||
+        (rc = up(o_hq, hpoint, (size_t)npoint * 9 * 8)) || (rc = up(o_bq, bpoint, (size_t)npoint * 3 * 8)))
+        return rc;
+    if (n) HIPCHK(hipMemsetAsync(B + o_S, 0, (size_t)n * n * 8, c->stream));
+    SchurArgs A{};
+    A.npose = npose;
+    A.npoint = npoint;
+    A.nfree = nfree;
+    A.n = n;
+    A.pidx = (const int32_t *)(B + o_pidx);
+    A.pt_off = (const int32_t *)(B + o_ptoff);
+    A.pt_edges = (const int32_t *)(B + o_pte);
+    A.edge_pose = (const int32_t *)(B + o_ep);
+    A.blk_off = (const int32_t *)(B + o_boff);
+    A.blk_pairs = (const int2 *)(B + o_bp);
+    A.blk_i1 = (const int32_t *)(B + o_bi1);
+    A.blk_i2 = (const int32_t *)(B + o_bi2);
+    A.nblk = nblk;
+    A.pose_off = (const int32_t *)(B + o_poff);
+    A.pose_edges = (const int32_t *)(B + o_pe);
+    A.eout = (const orbg_edge_out *)(B + o_eout);
+    A.hpose = (const double *)(B + o_hp);
+    A.bpose = (const double *)(B + o_bpz);
+    A.hpoint = (const double *)(B + o_hq);
+    A.bpoint = (const double *)(B + o_bq);
+    A.lambda = lambda;
+    A.dinv = (double *)(B + o_dinv);
+    A.bd = (double *)(B + o_bd);
+    A.cf = (double *)(B + o_cf);
+    A.S = (double *)(B + o_S);
+    A.x = (double *)(B + o_x);
+    A.ok = (int32_t *)(B + o_ok);
+    A.dx_pose = (double *)(B + o_dp);
+    A.dx_point = (double *)(B + o_dq);
+    if ((rc = launch_schur(c->stream, A, &c->prof))) return set_err(rc, "schur launch failed");
+    int32_t okv = 0;
+    if (npose) HIPCHK(hipMemcpyAsync(dx_pose, B + o_dp, (size_t)npose * 6 * 8, hipMemcpyDeviceToHost, c->stream));
+    if (npoint) HIPCHK(hipMemcpyAsync(dx_point, B + o_dq, (size_t)npoint * 3 * 8, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(hipMemcpyAsync(&okv, B + o_ok, 4, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(hipStreamSynchronize(c->stream));
+    c->prof.collect();
+    *ok = okv;
     return ORBG_OK;
 }

@@ -41,6 +41,23 @@ def linearize_local_ba(poses, points, edges, device=0, with_edges=True):
     return eout, hpose, bpose, hpoint, bpoint
 
 
+def ba_schur_solve(poses, npoint, edges, eout, hpose, bpose, hpoint, bpoint, lam, device=0):
+    """g2o BlockSolver<6,3>::solve (block_solver.hpp:354-486) after setLambda(lam), on
+    linearize_local_ba's outputs.  Returns (ok, dx_pose (npose, 6), dx_point (npoint, 3))."""
+    poses = np.ascontiguousarray(poses, L.POSE_DTYPE)
+    edges = np.ascontiguousarray(edges, L.EDGE_DTYPE)
+    eout = np.ascontiguousarray(eout, L.EDGE_OUT_DTYPE)
+    arrs = [np.ascontiguousarray(a, np.float64) for a in (hpose, bpose, hpoint, bpoint)]
+    dp = np.zeros((max(len(poses), 1), 6))
+    dq = np.zeros((max(npoint, 1), 3))
+    ok = ctypes.c_int()
+    L.check(L.lib().orbg_ba_schur_solve(_ctx(device).handle, L.ptr(poses), len(poses), npoint,
+                                        L.ptr(edges), len(edges), L.ptr(eout), *[L.ptr(a) for a in arrs],
+                                        float(lam), L.ptr(dp), L.ptr(dq), ctypes.byref(ok)),
+            "orbg_ba_schur_solve")
+    return bool(ok.value), dp[:len(poses)], dq[:npoint]
+
+
 def PoseOptimization(edges, Tcw, fx, fy, cx, cy, bf, device=0):
     """Optimizer::PoseOptimization (Optimizer.cc:356-631) on one frame.
 

@@ -218,3 +218,45 @@ def test_stereo_oracle_recovers_synthetic_disparity(oracle):
     c = oracle.extract(p, S.constant(240, 752, 90), with_pyramid=True)
     ur2, dp2 = oracle.stereo_matches(p, l, c, 752, 240, bf, bf / S.KITTI_FX)
     assert np.all(dp2 == -1)
+
+
+def test_schur_solve_equals_dense_solve(oracle):
+    """orc_ba_schur_solve (g2o's Schur complement + pose solve + back-substitution) equals a
+    dense solve of the full damped system [H_pp H_pl; H_lp H_ll] + lambda I."""
+    import numpy as np
+    from orb_slam2_test_amd import synthetic as S
+    poses, pts, edges = S.ba_window(seed=3, n_points=400)
+    eo, hp, bp, hq, bq = oracle.ba_linearize(poses, pts, edges)
+    lam = 1e-3 * np.abs(hp.reshape(len(poses), 36)[:, ::7]).max()
+    ok, dxp, dxq = oracle.ba_schur_solve(poses, len(pts), edges, eo, hp, bp, hq, bq, lam)
+    assert ok
+    free = [i for i in range(len(poses)) if not poses[i]["fixed"]]
+    act = edges["active"] != 0
+    has = np.zeros(len(pts), bool)
+    np.logical_or.at(has, edges["point"][act], True)
+    pi = {p: k for k, p in enumerate(free)}
+    qi = {q: k for k, q in enumerate(np.nonzero(has)[0])}
+    n = 6 * len(free) + 3 * len(qi)
+    H = np.zeros((n, n))
+    b = np.zeros(n)
+    hp3, hq3 = hp.reshape(len(poses), 6, 6), hq.reshape(len(pts), 3, 3)
+    for p in free:
+        o = 6 * pi[p]
+        H[o:o + 6, o:o + 6] = hp3[p] + lam * np.eye(6)
+        b[o:o + 6] = bp.reshape(-1, 6)[p]
+    for q in qi:
+        o = 6 * len(free) + 3 * qi[q]
+        H[o:o + 3, o:o + 3] = hq3[q] + lam * np.eye(3)
+        b[o:o + 3] = bq.reshape(-1, 3)[q]
+    for e, ed in enumerate(edges):
+        if not ed["active"] or ed["pose"] not in pi:
+            continue
+        o1, o2 = 6 * pi[ed["pose"]], 6 * len(free) + 3 * qi[ed["point"]]
+        H[o1:o1 + 6, o2:o2 + 3] = eo["hpl"][e].T
+        H[o2:o2 + 3, o1:o1 + 6] = eo["hpl"][e]
+    x = np.linalg.solve(H, b)
+    for p in free:
+        assert np.allclose(dxp[p], x[6 * pi[p]:6 * pi[p] + 6], rtol=1e-9, atol=1e-12 * np.abs(x).max())
+    for q in qi:
+        o = 6 * len(free) + 3 * qi[q]
+        assert np.allclose(dxq[q], x[o:o + 3], rtol=1e-9, atol=1e-12 * np.abs(x).max())
