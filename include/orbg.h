@@ -31,6 +31,11 @@
  *   orbg_pose_optimization .......... Optimizer::PoseOptimization(Frame*)  src/Optimizer.cc:356-631
  *   orbg_ba_schur_solve ............. g2o BlockSolver<6,3>::solve (Schur complement + pose solve)
  *                                     Thirdparty/g2o/g2o/core/block_solver.hpp:354-486
+ *   orbg_vocab_load_text ............ TemplatedVocabulary::loadFromTextFile
+ *                                     Thirdparty/DBoW2/DBoW2/TemplatedVocabulary.h:1337-1420
+ *   orbg_bow_transform .............. TemplatedVocabulary::transform(features, BowVector,
+ *                                     FeatureVector, levelsup) as Frame::ComputeBoW calls it
+ *                                     TemplatedVocabulary.h:1126-1189, 1220-1259; Frame.cc:532-539
  *   orbg_ba_linearize ............... g2o computeActiveErrors + BlockSolver::buildSystem arithmetic
  *                                     for EdgeSE3ProjectXYZ / EdgeStereoSE3ProjectXYZ inside
  *                                     Optimizer::LocalBundleAdjustment  src/Optimizer.cc:633-979
@@ -385,6 +390,58 @@ int orbg_ba_schur_solve(orbg_ctx *ctx, const orbg_pose *poses, int npose, int np
                         const double *hpose, const double *bpose, const double *hpoint,
                         const double *bpoint, double lambda, double *dx_pose, double *dx_point,
                         int *ok);
+
+/* ---------------- DBoW2 vocabulary + transform (Frame::ComputeBoW) ---------------- */
+/* WeightingType / ScoringType of Thirdparty/DBoW2/DBoW2/BowVector.h:36-53 */
+#define ORBG_TF_IDF 0
+#define ORBG_TF 1
+#define ORBG_IDF 2
+#define ORBG_BINARY 3
+#define ORBG_L1_NORM 0
+#define ORBG_L2_NORM 1
+#define ORBG_CHI_SQUARE 2
+#define ORBG_KL 3
+#define ORBG_BHATTACHARYYA 4
+#define ORBG_DOT_PRODUCT 5
+
+typedef struct orbg_vocab orbg_vocab;   /* device-resident vocabulary tree (one GPU) */
+
+/* The tree exactly as loadFromTextFile builds it: node 0 is the root, nodes 1..nnodes-1 in
+ * file order with parent[i] < i; children of a node in node order; is_leaf[i] > 0 gives the
+ * node the next word id (leaves numbered in node order).  desc[nnodes][32], weight[nnodes]
+ * (the idf of a word; ignored for the root).  k, L, scoring, weighting as in the header line
+ * (0 <= k <= 20, 1 <= L <= 10, scoring 0..5, weighting 0..3).  Uploads to ctx's device. */
+int orbg_vocab_create(orbg_ctx *ctx, int k, int L, int scoring, int weighting, int nnodes,
+                      const int32_t *parent, const uint8_t *is_leaf, const uint8_t *desc,
+                      const double *weight, orbg_vocab **out);
+/* Parses the ORBvoc.txt text format ("k L scoring weighting", then one "parent isLeaf d0..d31
+ * weight" line per node).  Blank lines are skipped (the reference appends an uninitialised
+ * stopped node under the root for a trailing newline).  ORBG_EINVAL on a
+ * malformed file. */
+int orbg_vocab_load_text(orbg_ctx *ctx, const char *path, orbg_vocab **out);
+void orbg_vocab_destroy(orbg_vocab *v);
+/* k, L, scoring, weighting, nnodes, nwords (any pointer may be NULL) */
+int orbg_vocab_info(const orbg_vocab *v, int32_t *k, int32_t *L, int32_t *scoring,
+                    int32_t *weighting, int32_t *nnodes, int32_t *nwords);
+
+/* transform(descriptors, mBowVec, mFeatVec, levelsup) for n descriptors (n x 32 bytes, host):
+ *   BowVector: bow_words[*nbow] ascending word ids, bow_weights[*nbow] (normalised per the
+ *   scoring), FeatureVector: fv_nodes[*nfv] ascending node ids, feature indices
+ *   fv_feats[fv_off[j] .. fv_off[j+1]) ascending.  Capacities: n for bow_*, fv_nodes, fv_feats;
+ *   n + 1 for fv_off.  Bit-identical to the reference (doubles included). */
+int orbg_bow_transform(orbg_ctx *ctx, const orbg_vocab *v, const uint8_t *desc, int n,
+                       int levelsup, int32_t *bow_words, double *bow_weights, int *nbow,
+                       int32_t *fv_nodes, int32_t *fv_off, int32_t *fv_feats, int *nfv);
+
+/* Batched, device-resident: frame f's descriptors at desc + f * cap * 32, counts[f] of them
+ * (cap <= 8192); outputs per frame at bow_words / bow_weights / fv_nodes / fv_feats + f * cap,
+ * fv_off + f * (cap + 1), nbow[f], nfv[f].  Also word_of[f * cap + i] (word id of feature i,
+ * -1 if stopped) and node_of[...] (its levelsup node) when non-NULL. */
+int orbg_bow_transform_batch_device(orbg_ctx *ctx, const orbg_vocab *v, const uint8_t *desc,
+                                    const int32_t *counts, int cap, int nframes, int levelsup,
+                                    int32_t *bow_words, double *bow_weights, int32_t *nbow,
+                                    int32_t *fv_nodes, int32_t *fv_off, int32_t *fv_feats,
+                                    int32_t *nfv, int32_t *word_of, int32_t *node_of);
 
 #ifdef __cplusplus
 }

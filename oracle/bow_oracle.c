@@ -1,0 +1,146 @@
+/*
+ * oracle/bow_oracle.c -- TEST INFRASTRUCTURE ONLY (see orb_oracle.h).
+ *
+ * Restatement of DBoW2's TemplatedVocabulary<FORB::TDescriptor, FORB>::transform(features,
+ * BowVector, FeatureVector, levelsup) (Thirdparty/DBoW2/DBoW2/TemplatedVocabulary.h:
+ * 1127-1189, 1220-1259) for the ORB vocabulary's settings (TF_IDF weighting, L1 scoring:
+ * mustNormalize -> L1), as Frame::ComputeBoW calls it (src/Frame.cc:532-539, levelsup 4):
+ *   - per feature: descend from the root choosing the child with the smallest
+ *     FORB::distance (strict <, first child wins ties) until a leaf; the node reached at
+ *     level L - levelsup is the FeatureVector key (root if <= 0; the leaf if the descent
+ *     ends above that level, where the reference reads an uninitialised NodeId);
+ *   - TF / TF_IDF: BowVector::addWeight (BowVector.cpp:34-46), per word the weights of its
+ *     features summed in feature order; IDF / BINARY: addIfNotExist (:50-58), the first
+ *     feature's weight; stopped words (weight <= 0, or NaN) are skipped;
+ *   - mustNormalize (ScoringObject.h:73-88): BowVector::normalize (BowVector.cpp:62-84) by
+ *     the sum of |w| (L1) or sqrt of the sum of w^2 (L2_NORM) in word-id order; DOT_PRODUCT
+ *     does not normalise, and TF weights are then divided by the word count;
+ *   - FeatureVector::addFeature (FeatureVector.cpp:31-45): feature indices per node, in
+ *     feature order.
+ * The vocabulary is a flat node array (what loadFromTextFile builds, :1338-1420): node
+ * descriptors, idf weights, word ids (-1 for inner nodes) and children as CSR.
+ */
+#include "orb_oracle.h"
+
+#include <math.h>
+#include <stdlib.h>
+#include <string.h>
+
+void orc_bow_word(const orc_vocab *v, const uint8_t *feat, int levelsup, int32_t *word,
+                  double *weight, int32_t *nid)
+{
+    const int nid_level = v->L - levelsup;
+    if (nid_level <= 0)
+        *nid = 0;
+    int final_id = 0, level = 0;
+    do {
+        ++level;
+        const int c0 = v->child_off[final_id], c1 = v->child_off[final_id + 1];
+        final_id = v->child_idx[c0];
+        int best_d = orc_descriptor_distance(feat, v->desc + (size_t)final_id * 32);
+        for (int c = c0 + 1; c < c1; c++) {
+            const int id = v->child_idx[c];
+            const int d = orc_descriptor_distance(feat, v->desc + (size_t)id * 32);
+            if (d < best_d) {
+                best_d = d;
+                final_id = id;
+            }
+        }
+        if (level == nid_level)
+            *nid = final_id;
+    } while (v->child_off[final_id + 1] > v->child_off[final_id]);
+    /* A leaf above nid_level leaves *nid unwritten in the reference (the caller's
+     * uninitialised NodeId: undefined, never reached with ORBvoc.txt's full tree); pinned
+     * here to the leaf itself. */
+    if (level < nid_level)
+        *nid = final_id;
+    *word = v->word_id[final_id];
+    *weight = v->weight[final_id];
+}
+
+static int cmp_pair(const void *a, const void *b)
+{
+    const int64_t x = *(const int64_t *)a, y = *(const int64_t *)b;
+    return x < y ? -1 : x > y;
+}
+
+int orc_bow_transform(const orc_vocab *v, const uint8_t *desc, int n, int levelsup,
+                      int32_t *bow_words, double *bow_weights, int *nbow, int32_t *fv_nodes,
+                      int32_t *fv_off, int32_t *fv_feats, int *nfv)
+{
+    *nbow = 0;
+    *nfv = 0;
+    fv_off[0] = 0;
+    if (v->nwords == 0 || n <= 0)  /* TemplatedVocabulary::empty() */
+        return 0;
+    const int nn = n;
+    int32_t *w = (int32_t *)malloc(sizeof(int32_t) * nn);
+    int32_t *nd = (int32_t *)malloc(sizeof(int32_t) * nn);
+    double *wt = (double *)malloc(sizeof(double) * nn);
+    int64_t *pw = (int64_t *)malloc(sizeof(int64_t) * nn);
+    int64_t *pn = (int64_t *)malloc(sizeof(int64_t) * nn);
+    int m = 0;
+    for (int i = 0; i < n; i++) {
+        orc_bow_word(v, desc + (size_t)i * 32, levelsup, &w[i], &wt[i], &nd[i]);
+        if (wt[i] > 0) {  /* not stopped */
+            pw[m] = ((int64_t)(uint32_t)w[i] << 32) | i;
+            pn[m] = ((int64_t)(uint32_t)nd[i] << 32) | i;
+            m++;
+        }
+    }
+    /* std::map<WordId, ...> / std::map<NodeId, ...>: ascending unsigned ids */
+    qsort(pw, m, sizeof(int64_t), cmp_pair);
+    qsort(pn, m, sizeof(int64_t), cmp_pair);
+    const int tf = v->weighting == ORC_TF_IDF || v->weighting == ORC_TF;
+    int nb = 0;
+    for (int k = 0; k < m; k++) {
+        const int32_t word = (int32_t)(pw[k] >> 32), f = (int32_t)(pw[k] & 0xFFFFFFFF);
+        if (nb > 0 && bow_words[nb - 1] == word) {
+            if (tf)  /* addWeight; IDF / BINARY: addIfNotExist keeps the first */
+                bow_weights[nb - 1] += wt[f];
+        } else {
+            bow_words[nb] = word;
+            bow_weights[nb] = wt[f];
+            nb++;
+        }
+    }
+    /* mustNormalize: every scoring but DOT_PRODUCT; L2 for L2_NORM, L1 otherwise */
+    const int must = v->scoring != ORC_DOT_PRODUCT;
+    if (tf && nb > 0 && !must) {
+        const double cnt = nb;
+        for (int k = 0; k < nb; k++)
+            bow_weights[k] /= cnt;
+    }
+    if (must) {
+        double norm = 0.0;
+        if (v->scoring == ORC_L2_NORM) {
+            for (int k = 0; k < nb; k++)
+                norm += bow_weights[k] * bow_weights[k];
+            norm = sqrt(norm);
+        } else {
+            for (int k = 0; k < nb; k++)
+                norm += fabs(bow_weights[k]);
+        }
+        if (norm > 0.0)
+            for (int k = 0; k < nb; k++)
+                bow_weights[k] /= norm;
+    }
+    int nf = 0;
+    for (int k = 0; k < m; k++) {
+        const int32_t node = (int32_t)(pn[k] >> 32);
+        if (!(nf > 0 && fv_nodes[nf - 1] == node)) {
+            fv_nodes[nf] = node;
+            fv_off[nf + 1] = fv_off[nf];
+            nf++;
+        }
+        fv_feats[fv_off[nf]++] = (int32_t)(pn[k] & 0xFFFFFFFF);
+    }
+    *nbow = nb;
+    *nfv = nf;
+    free(w);
+    free(nd);
+    free(wt);
+    free(pw);
+    free(pn);
+    return m;
+}

@@ -19,6 +19,7 @@
  *   Frame::ComputeStereoMatches ..... src/Frame.cc:619-834 (stereo_oracle.c)
  *   ORBmatcher::SearchByProjection .. src/ORBmatcher.cc:1503-1667, 59-154 (track_oracle.c)
  *   Optimizer::PoseOptimization ..... src/Optimizer.cc:356-631 + g2o LM / LDLT (pose_oracle.c)
+ *   DBoW2 transform (Frame::ComputeBoW) Thirdparty/DBoW2/DBoW2/TemplatedVocabulary.h (bow_oracle.c)
  *   g2o edge arithmetic (double) .... Thirdparty/g2o/g2o/types/types_six_dof_expmap.{h,cpp},
  *                                     core/base_binary_edge.hpp:55-120, core/base_edge.h:58-102,
  *                                     core/robust_kernel_impl.cpp:65-91
@@ -207,6 +208,26 @@ void orc_se3_from_tcw(const float Tcw[12], double q[4], double t[3]);
 void orc_se3_to_tcw(const double q[4], const double t[3], float Tcw[12]);
 void orc_se3_oplus(double q[4], double t[3], const double upd[6]);
 int orc_ldlt_solve6(const double H[6][6], const double b[6], double x[6]);
+
+/* ---- DBoW2 TemplatedVocabulary::transform (bow_oracle.c) ---- */
+enum { ORC_TF_IDF = 0, ORC_TF = 1, ORC_IDF = 2, ORC_BINARY = 3 };           /* WeightingType */
+enum { ORC_L1_NORM = 0, ORC_L2_NORM = 1, ORC_DOT_PRODUCT = 5 };            /* ScoringType */
+typedef struct {
+    int32_t k, L, scoring, weighting, nnodes, nwords;
+    const uint8_t *desc;        /* [nnodes][32] node descriptors */
+    const double *weight;       /* [nnodes] idf weight (words) */
+    const int32_t *word_id;     /* [nnodes] word id (leaves, file order); 0 otherwise (Node()) */
+    const int32_t *child_off;   /* [nnodes + 1] children CSR */
+    const int32_t *child_idx;
+} orc_vocab;
+
+void orc_bow_word(const orc_vocab *v, const uint8_t *feat, int levelsup, int32_t *word,
+                  double *weight, int32_t *nid);
+/* BowVector (ascending word ids + L1-normalised weights) and FeatureVector (ascending node
+ * ids, CSR of feature indices).  Returns the number of features not stopped. */
+int orc_bow_transform(const orc_vocab *v, const uint8_t *desc, int n, int levelsup,
+                      int32_t *bow_words, double *bow_weights, int *nbow, int32_t *fv_nodes,
+                      int32_t *fv_off, int32_t *fv_feats, int *nfv);
 
 /* ---- Frame::ComputeStereoMatches (stereo_oracle.c) ----
  * kl/dl: left keypoints (mvKeys) + descriptors, kr/dr: right.  pyr_l / pyr_r: the two

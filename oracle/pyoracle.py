@@ -73,6 +73,13 @@ def track_cam(Tcw, Tlw, fx, fy, cx, cy, bf, b, mono):
     return c
 
 
+class OrcVocab(C.Structure):
+    _fields_ = [("k", C.c_int32), ("L", C.c_int32), ("scoring", C.c_int32),
+                ("weighting", C.c_int32), ("nnodes", C.c_int32), ("nwords", C.c_int32),
+                ("desc", C.c_void_p), ("weight", C.c_void_p), ("word_id", C.c_void_p),
+                ("child_off", C.c_void_p), ("child_idx", C.c_void_p)]
+
+
 class Bounds(C.Structure):
     _fields_ = [("min_x", C.c_float), ("max_x", C.c_float), ("min_y", C.c_float),
                 ("max_y", C.c_float)]
@@ -139,6 +146,10 @@ def lib():
                                                          vp]
         L.orc_search_by_projection_local.argtypes = [vp, vp, vp, C.c_int, vp, vp, vp, vp, vp,
                                                      C.c_int, C.c_float, C.c_float, vp]
+        L.orc_bow_transform.argtypes = [P(OrcVocab), vp, C.c_int, C.c_int, vp, vp, P(C.c_int), vp,
+                                        vp, vp, P(C.c_int)]
+        L.orc_bow_word.argtypes = [P(OrcVocab), vp, C.c_int, P(C.c_int32), P(C.c_double),
+                                   P(C.c_int32)]
         _lib = L
     return _lib
 
@@ -397,3 +408,49 @@ def ba_schur_solve(poses, npoint, edges, eout, hpose, bpose, hpoint, bpoint, lam
     ok = lib().orc_ba_schur_solve(_p(poses), len(poses), npoint, _p(edges), len(edges), _p(eout),
                                   _p(hp), _p(bp), _p(hq), _p(bq), float(lam), _p(dp), _p(dq))
     return bool(ok), dp[:len(poses)], dq[:npoint]
+
+
+class Vocab:
+    """Flat vocabulary for oracle/bow_oracle.c, built from the loadFromTextFile node list
+    (TemplatedVocabulary.h:1376-1417): children in node order, leaves numbered in order."""
+
+    def __init__(self, k, L, scoring, weighting, parent, is_leaf, desc, weight):
+        parent = np.asarray(parent, np.int64)
+        n = len(parent)
+        is_leaf = np.asarray(is_leaf).astype(bool)
+        is_leaf[0] = False
+        self.desc = np.ascontiguousarray(np.asarray(desc, np.uint8).reshape(n, 32))
+        self.weight = np.ascontiguousarray(weight, np.float64)
+        self.word_id = np.zeros(n, np.int32)
+        self.word_id[is_leaf] = np.arange(int(is_leaf.sum()), dtype=np.int32)
+        cnt = np.bincount(parent[1:], minlength=n) if n > 1 else np.zeros(n, np.int64)
+        self.child_off = np.zeros(n + 1, np.int32)
+        self.child_off[1:] = np.cumsum(cnt)
+        order = np.argsort(parent[1:], kind="stable") + 1
+        self.child_idx = np.ascontiguousarray(order, np.int32) if n > 1 else np.zeros(1, np.int32)
+        self.s = OrcVocab(k, L, scoring, weighting, n, int(is_leaf.sum()), _p(self.desc),
+                          _p(self.weight), _p(self.word_id), _p(self.child_off),
+                          _p(self.child_idx))
+
+
+def bow_word(voc, feat, levelsup):
+    """single-feature transform (TemplatedVocabulary.h:1220-1259): (word, weight, nid)"""
+    w, x, nid = C.c_int32(), C.c_double(), C.c_int32(-7)
+    f = np.ascontiguousarray(feat, np.uint8)
+    lib().orc_bow_word(C.byref(voc.s), _p(f), levelsup, C.byref(w), C.byref(x), C.byref(nid))
+    return w.value, x.value, nid.value
+
+
+def bow_transform(voc, desc, levelsup):
+    """transform(features, BowVector, FeatureVector, levelsup) -> (bow_words, bow_weights,
+    fv_nodes, fv_off, fv_feats)."""
+    d = np.ascontiguousarray(desc, np.uint8).reshape(-1, 32)
+    n = len(d)
+    cap = max(n, 1)
+    bw, bx = np.zeros(cap, np.int32), np.zeros(cap)
+    vn, vo, vf = np.zeros(cap, np.int32), np.zeros(cap + 1, np.int32), np.zeros(cap, np.int32)
+    nb, nf = C.c_int(), C.c_int()
+    lib().orc_bow_transform(C.byref(voc.s), _p(d), n, levelsup, _p(bw), _p(bx), C.byref(nb),
+                            _p(vn), _p(vo), _p(vf), C.byref(nf))
+    nb, nf = nb.value, nf.value
+    return bw[:nb], bx[:nb], vn[:nf], vo[:nf + 1], vf[:vo[nf]]

@@ -163,6 +163,13 @@ def lib():
                                                       i32]),
         "orbg_ba_schur_solve": (i32, [vp, vp, i32, i32, vp, i32, vp, vp, vp, vp, vp, C.c_double, vp,
                                       vp, P(i32)]),
+        "orbg_vocab_create": (i32, [vp, i32, i32, i32, i32, i32, vp, vp, vp, vp, P(vp)]),
+        "orbg_vocab_load_text": (i32, [vp, C.c_char_p, P(vp)]),
+        "orbg_vocab_destroy": (None, [vp]),
+        "orbg_vocab_info": (i32, [vp, P(i32), P(i32), P(i32), P(i32), P(i32), P(i32)]),
+        "orbg_bow_transform": (i32, [vp, vp, vp, i32, i32, vp, vp, P(i32), vp, vp, vp, P(i32)]),
+        "orbg_bow_transform_batch_device": (i32, [vp, vp, vp, vp, i32, i32, i32, vp, vp, vp, vp,
+                                                  vp, vp, vp, vp, vp]),
         "orbg_ba_linearize": (i32, [vp, vp, i32, vp, i32, vp, i32, vp, vp, vp, vp, vp]),
         "orbg_ba_linearize_device": (i32, [vp, vp, i32, vp, i32, vp, i32, vp, vp, vp, vp, vp, vp,
                                            vp, vp, vp]),

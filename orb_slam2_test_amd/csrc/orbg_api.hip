@@ -17,6 +17,7 @@
 #include "orbg_internal.h"
 #include "track_args.h"
 #include "schur_args.h"
+#include "bow_args.h"
 
 #pragma clang fp contract(off)
 
@@ -1894,5 +1895,272 @@ extern "C" int orbg_ba_schur_solve(orbg_ctx *c, const orbg_pose *poses, int npos
     HIPCHK(hipStreamSynchronize(c->stream));
     c->prof.collect();
     *ok = okv;
+    return ORBG_OK;
+}
+
+// ---------------------------------------------------------------------------
+// DBoW2 vocabulary (TemplatedVocabulary::loadFromTextFile) + transform (Frame::ComputeBoW)
+// ---------------------------------------------------------------------------
+struct orbg_vocab {
+    int device = 0;
+    int k = 0, L = 0, scoring = 0, weighting = 0, nnodes = 0, nwords = 0;
+    int group = 16, root_c0 = 0, root_c1 = 0;
+    BowSlot *d_slots = nullptr;
+};
+
+extern "C" int orbg_vocab_create(orbg_ctx *c, int k, int L, int scoring, int weighting,
+                                 int nnodes, const int32_t *parent, const uint8_t *is_leaf,
+                                 const uint8_t *desc, const double *weight, orbg_vocab **out)
+{
+    if (!c || !out) return set_err(ORBG_EINVAL, "NULL argument");
+    *out = nullptr;
+    // header checks of loadFromTextFile (TemplatedVocabulary.h:1359-1363)
+    if (k < 0 || k > 20 || L < 1 || L > 10 || scoring < 0 || scoring > 5 || weighting < 0 ||
+        weighting > 3)
+        return set_err(ORBG_EINVAL, "k %d L %d scoring %d weighting %d outside the text format",
+                       k, L, scoring, weighting);
+    if (nnodes < 1) return set_err(ORBG_EINVAL, "a vocabulary has at least the root node");
+    if (nnodes > 1 && (!parent || !is_leaf || !desc || !weight))
+        return set_err(ORBG_EINVAL, "NULL node array");
+    std::vector<int32_t> off(nnodes + 1, 0), word(nnodes, 0);
+    int nwords = 0;
+    for (int i = 1; i < nnodes; i++) {
+        if (parent[i] < 0 || parent[i] >= i)
+            return set_err(ORBG_EINVAL, "node %d: parent %d is not an earlier node", i, parent[i]);
+        off[parent[i] + 1]++;
+        if (is_leaf[i]) word[i] = nwords++;
+    }
+    int maxc = 0;
+    for (int i = 0; i < nnodes; i++) {
+        maxc = std::max(maxc, off[i + 1]);
+        off[i + 1] += off[i];
+    }
+    if (maxc > 64) return set_err(ORBG_ENOTSUP, "a node with %d children (> 64)", maxc);
+    std::vector<BowSlot> slots(std::max(nnodes - 1, 1));
+    std::vector<int32_t> fill(off.begin(), off.end() - 1);
+    for (int i = 1; i < nnodes; i++) {  // children in node (file) order
+        BowSlot &s = slots[fill[parent[i]]++];
+        memset(&s, 0, sizeof(s));
+        memcpy(s.d, desc + (size_t)i * 32, 32);
+        s.c0 = off[i];
+        s.c1 = off[i + 1];
+        s.node = i;
+        s.word = word[i];
+        s.weight = weight[i];
+    }
+    auto *v = new orbg_vocab();
+    v->device = c->device;
+    v->k = k;
+    v->L = L;
+    v->scoring = scoring;
+    v->weighting = weighting;
+    v->nnodes = nnodes;
+    v->nwords = nwords;
+    v->group = maxc <= 16 ? 16 : maxc <= 32 ? 32 : 64;
+    v->root_c0 = off[0];
+    v->root_c1 = off[1];
+    hipError_t e = hipSetDevice(c->device);
+    if (e == hipSuccess) e = hipMalloc(&v->d_slots, slots.size() * sizeof(BowSlot));
+    if (e == hipSuccess)
+        e = hipMemcpy(v->d_slots, slots.data(), slots.size() * sizeof(BowSlot), hipMemcpyHostToDevice);
+    if (e != hipSuccess) {
+        if (v->d_slots) hipFree(v->d_slots);
+        delete v;
+        return set_err(ORBG_ENOMEM, "vocabulary upload: %s", hipGetErrorString(e));
+    }
+    *out = v;
+    return ORBG_OK;
+}
+
+extern "C" int orbg_vocab_load_text(orbg_ctx *c, const char *path, orbg_vocab **out)
+{
+    if (!c || !path || !out) return set_err(ORBG_EINVAL, "NULL argument");
+    FILE *fp = fopen(path, "r");
+    if (!fp) return set_err(ORBG_EINVAL, "cannot open %s", path);
+    char *line = nullptr;
+    size_t cap = 0;
+    int k = 0, L = 0, n1 = 0, n2 = 0, rc = ORBG_OK;
+    std::vector<int32_t> parent(1, 0);
+    std::vector<uint8_t> leaf(1, 0), desc(32, 0);
+    std::vector<double> weight(1, 0.0);
+    if (getline(&line, &cap, fp) < 0 || sscanf(line, "%d %d %d %d", &k, &L, &n1, &n2) != 4) {
+        rc = set_err(ORBG_EINVAL, "%s: missing header line", path);
+    } else {
+        long lineno = 1;
+        while (getline(&line, &cap, fp) >= 0) {
+            lineno++;
+            char *p = line, *e;
+            while (*p == ' ' || *p == '\t' || *p == '\r' || *p == '\n') p++;
+            if (!*p) continue;  // blank line
+            long vals[34];
+            int nv = 0;
+            for (; nv < 34; nv++) {
+                vals[nv] = strtol(p, &e, 10);
+                if (e == p) break;
+                p = e;
+            }
+            const double w = strtod(p, &e);
+            if (nv < 34 || e == p) {
+                rc = set_err(ORBG_EINVAL, "%s:%ld: expected parent isLeaf 32 bytes weight", path,
+                             lineno);
+                break;
+            }
+            parent.push_back((int32_t)vals[0]);
+            leaf.push_back(vals[1] > 0);
+            for (int j = 0; j < 32; j++) desc.push_back((uint8_t)vals[2 + j]);
+            weight.push_back(w);
+        }
+    }
+    free(line);
+    fclose(fp);
+    if (rc) return rc;
+    return orbg_vocab_create(c, k, L, n1, n2, (int)parent.size(), parent.data(), leaf.data(),
+                             desc.data(), weight.data(), out);
+}
+
+extern "C" void orbg_vocab_destroy(orbg_vocab *v)
+{
+    if (!v) return;
+    if (v->d_slots) {
+        hipSetDevice(v->device);
+        hipFree(v->d_slots);
+    }
+    delete v;
+}
+
+extern "C" int orbg_vocab_info(const orbg_vocab *v, int32_t *k, int32_t *L, int32_t *scoring,
+                               int32_t *weighting, int32_t *nnodes, int32_t *nwords)
+{
+    if (!v) return set_err(ORBG_EINVAL, "vocabulary is NULL");
+    if (k) *k = v->k;
+    if (L) *L = v->L;
+    if (scoring) *scoring = v->scoring;
+    if (weighting) *weighting = v->weighting;
+    if (nnodes) *nnodes = v->nnodes;
+    if (nwords) *nwords = v->nwords;
+    return ORBG_OK;
+}
+
+#define ORBG_BOW_MAX_CAP 8192   // k_bow_vectors sorts a frame's keys in LDS
+
+static BowArgs bow_args(const orbg_vocab *v, int levelsup)
+{
+    BowArgs A{};
+    A.slots = v->d_slots;
+    A.root_c0 = v->root_c0;
+    A.root_c1 = v->root_c1;
+    A.group = v->group;
+    A.nid_level = v->L - levelsup;
+    A.scoring = v->scoring;
+    A.weighting = v->weighting;
+    A.empty = v->nwords == 0;
+    return A;
+}
+
+extern "C" int orbg_bow_transform_batch_device(orbg_ctx *c, const orbg_vocab *v,
+                                               const uint8_t *desc, const int32_t *counts,
+                                               int cap, int nframes, int levelsup,
+                                               int32_t *bow_words, double *bow_weights,
+                                               int32_t *nbow, int32_t *fv_nodes,
+                                               int32_t *fv_off, int32_t *fv_feats, int32_t *nfv,
+                                               int32_t *word_of, int32_t *node_of)
+{
+    if (!c || !v) return set_err(ORBG_EINVAL, "NULL context or vocabulary");
+    if (v->device != c->device) return set_err(ORBG_EINVAL, "vocabulary lives on another device");
+    if (nframes <= 0) return ORBG_OK;
+    if (cap < 1 || cap > ORBG_BOW_MAX_CAP)
+        return set_err(ORBG_ENOTSUP, "cap %d outside 1..%d", cap, ORBG_BOW_MAX_CAP);
+    if (!desc || !counts || !bow_words || !bow_weights || !nbow || !fv_nodes || !fv_off ||
+        !fv_feats || !nfv)
+        return set_err(ORBG_EINVAL, "NULL device array");
+    HIPCHK(hipSetDevice(c->device));
+    const size_t per = (size_t)nframes * cap;
+    const size_t o_w = 0, o_n = al256(per * 4), o_x = o_n + al256(per * 4);
+    void *s;
+    int rc = scratch(c, o_x + al256(per * 8), &s);
+    if (rc) return rc;
+    BowArgs A = bow_args(v, levelsup);
+    A.desc = desc;
+    A.counts = counts;
+    A.cap = cap;
+    A.nframes = nframes;
+    A.fword = word_of ? word_of : (int32_t *)((uint8_t *)s + o_w);
+    A.fnode = node_of ? node_of : (int32_t *)((uint8_t *)s + o_n);
+    A.fweight = (double *)((uint8_t *)s + o_x);
+    A.bow_words = bow_words;
+    A.bow_weights = bow_weights;
+    A.nbow = nbow;
+    A.fv_nodes = fv_nodes;
+    A.fv_off = fv_off;
+    A.fv_feats = fv_feats;
+    A.nfv = nfv;
+    if ((rc = launch_bow(c->stream, A, &c->prof))) return set_err(rc, "bow launch failed");
+    return ORBG_OK;
+}
+
+extern "C" int orbg_bow_transform(orbg_ctx *c, const orbg_vocab *v, const uint8_t *desc, int n,
+                                  int levelsup, int32_t *bow_words, double *bow_weights,
+                                  int *nbow, int32_t *fv_nodes, int32_t *fv_off,
+                                  int32_t *fv_feats, int *nfv)
+{
+    if (!c || !v || !nbow || !nfv || !fv_off) return set_err(ORBG_EINVAL, "NULL argument");
+    if (n < 0) return set_err(ORBG_EINVAL, "negative size");
+    if (n > ORBG_BOW_MAX_CAP) return set_err(ORBG_ENOTSUP, "%d descriptors (> %d)", n, ORBG_BOW_MAX_CAP);
+    if (n > 0 && (!desc || !bow_words || !bow_weights || !fv_nodes || !fv_feats))
+        return set_err(ORBG_EINVAL, "NULL array");
+    *nbow = *nfv = 0;
+    fv_off[0] = 0;
+    if (n == 0) return ORBG_OK;
+    HIPCHK(hipSetDevice(c->device));
+    size_t off = 0;
+    auto take = [&](size_t bytes) {
+        const size_t o = off;
+        off += al256(bytes);
+        return o;
+    };
+    const size_t o_d = take((size_t)n * 32), o_c = take(4), o_fw = take((size_t)n * 4);
+    const size_t o_fn = take((size_t)n * 4), o_fx = take((size_t)n * 8);
+    const size_t o_bw = take((size_t)n * 4), o_bx = take((size_t)n * 8), o_nb = take(4);
+    const size_t o_vn = take((size_t)n * 4), o_vo = take((size_t)(n + 1) * 4);
+    const size_t o_vf = take((size_t)n * 4), o_nf = take(4);
+    void *s;
+    int rc = scratch(c, off, &s);
+    if (rc) return rc;
+    uint8_t *b = (uint8_t *)s;
+    const int32_t cnt = n;
+    HIPCHK(hipMemcpyAsync(b + o_d, desc, (size_t)n * 32, hipMemcpyHostToDevice, c->stream));
+    HIPCHK(hipMemcpyAsync(b + o_c, &cnt, 4, hipMemcpyHostToDevice, c->stream));
+    BowArgs A = bow_args(v, levelsup);
+    A.desc = b + o_d;
+    A.counts = (const int32_t *)(b + o_c);
+    A.cap = n;
+    A.nframes = 1;
+    A.fword = (int32_t *)(b + o_fw);
+    A.fnode = (int32_t *)(b + o_fn);
+    A.fweight = (double *)(b + o_fx);
+    A.bow_words = (int32_t *)(b + o_bw);
+    A.bow_weights = (double *)(b + o_bx);
+    A.nbow = (int32_t *)(b + o_nb);
+    A.fv_nodes = (int32_t *)(b + o_vn);
+    A.fv_off = (int32_t *)(b + o_vo);
+    A.fv_feats = (int32_t *)(b + o_vf);
+    A.nfv = (int32_t *)(b + o_nf);
+    if ((rc = launch_bow(c->stream, A, &c->prof))) return set_err(rc, "bow launch failed");
+    int32_t nb = 0, nf = 0;
+    HIPCHK(hipMemcpyAsync(&nb, b + o_nb, 4, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(hipMemcpyAsync(&nf, b + o_nf, 4, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(hipStreamSynchronize(c->stream));
+    // outputs are at most n long; copy what was produced
+    HIPCHK(hipMemcpyAsync(bow_words, b + o_bw, (size_t)nb * 4, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(hipMemcpyAsync(bow_weights, b + o_bx, (size_t)nb * 8, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(hipMemcpyAsync(fv_nodes, b + o_vn, (size_t)nf * 4, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(hipMemcpyAsync(fv_off, b + o_vo, (size_t)(nf + 1) * 4, hipMemcpyDeviceToHost, c->stream));
+    int32_t m = 0;
+    HIPCHK(hipMemcpyAsync(&m, b + o_vo + (size_t)nf * 4, 4, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(hipStreamSynchronize(c->stream));
+    if (m) HIPCHK(hipMemcpy(fv_feats, b + o_vf, (size_t)m * 4, hipMemcpyDeviceToHost));
+    c->prof.collect();
+    *nbow = nb;
+    *nfv = nf;
     return ORBG_OK;
 }

@@ -352,3 +352,103 @@ def pose_frame(n=1500, stereo_frac=0.5, outlier_frac=0.1, seed=DEFAULT_SEED, noi
     T0[:, :3] = R0
     T0[:, 3] = t + rng.normal(0, trans_err, 3)
     return e, Tcw.astype(np.float32), T0.astype(np.float32)
+
+
+# ---------------------------------------------------------------------------
+# DBoW2 vocabularies (ORBvoc.txt is not shipped with the reference checkout; these stand in
+# for it with the same text format, sizes and weighting)
+# ---------------------------------------------------------------------------
+def _flip_mask(rng, n, depth):
+    """random 32-byte masks whose bits are set with probability 2^-depth"""
+    m = rng.integers(0, 256, (n, 32), dtype=np.uint8)
+    for _ in range(depth - 1):
+        m &= rng.integers(0, 256, (n, 32), dtype=np.uint8)
+    return m
+
+
+def vocabulary(k=10, L=6, seed=DEFAULT_SEED, stop_frac=0.01, scoring=0, weighting=0):
+    """A full k-ary tree of depth L in breadth-first node order (node 0 the root, parent
+    (i - 1) // k), the node list loadFromTextFile builds (TemplatedVocabulary.h:1376-1417).
+    Children descend from their parent's descriptor with 2^-level bit flips (level 1 fully
+    random), so a descriptor's path is decided by real distance gaps and ties as in a
+    k-means tree.  Leaves carry idf weights in (0.5, 10), stop_frac of them 0 (stopped);
+    ORBvoc.txt's header is "10 6 0 0" (TF_IDF, L1_NORM)."""
+    rng = np.random.default_rng(seed)
+    n = (k ** (L + 1) - 1) // (k - 1)
+    parent = np.zeros(n, np.int32)
+    parent[1:] = (np.arange(1, n) - 1) // k
+    desc = np.zeros((n, 32), np.uint8)
+    lo = 1
+    for lvl in range(1, L + 1):
+        hi = lo + k ** lvl
+        if lvl == 1:
+            desc[lo:hi] = rng.integers(0, 256, (hi - lo, 32), dtype=np.uint8)
+        else:
+            desc[lo:hi] = desc[parent[lo:hi]] ^ _flip_mask(rng, hi - lo, min(lvl, 4))
+        lo = hi
+    is_leaf = np.zeros(n, np.uint8)
+    first_leaf = (k ** L - 1) // (k - 1)
+    is_leaf[first_leaf:] = 1
+    weight = np.zeros(n)
+    nl = n - first_leaf
+    w = rng.uniform(0.5, 10.0, nl)
+    w[rng.random(nl) < stop_frac] = 0.0
+    weight[first_leaf:] = w
+    return dict(k=k, L=L, scoring=scoring, weighting=weighting, parent=parent,
+                is_leaf=is_leaf, desc=desc, weight=weight)
+
+
+def ragged_vocabulary(k=10, L=5, seed=DEFAULT_SEED, leaf_prob=0.25, stop_frac=0.05,
+                      scoring=0, weighting=0, max_nodes=60000):
+    """A ragged tree in DBoW2's creation order (each node's children appended together,
+    then each child expanded -- HKmeansStep): k root children, 1..k per inner node, leaves at
+    depths 2..L (a node below L becomes a leaf with probability leaf_prob), duplicate sibling
+    descriptors (exact distance ties) and some stopped words."""
+    rng = np.random.default_rng(seed)
+    parent, leaf, desc, depth = [0], [0], [np.zeros(32, np.uint8)], [0]
+    stack = [0]
+    while stack:
+        p = stack.pop(0)
+        if len(parent) + k > max_nodes:
+            break
+        nc = int(rng.integers(1, k + 1)) if p else k
+        kids = []
+        for j in range(nc):
+            d = (desc[p] ^ _flip_mask(rng, 1, min(depth[p] + 1, 4))[0]) if p else \
+                rng.integers(0, 256, 32, dtype=np.uint8)
+            if j > 0 and rng.random() < 0.1:
+                d = desc[kids[-1]].copy()         # sibling duplicate: exact tie
+            nid = len(parent)
+            parent.append(p)
+            desc.append(d)
+            depth.append(depth[p] + 1)
+            is_leaf = depth[p] + 1 >= L or (depth[p] >= 1 and rng.random() < leaf_prob)
+            leaf.append(1 if is_leaf else 0)
+            kids.append(nid)
+            if not is_leaf:
+                stack.append(nid)
+    # inner nodes left unexpanded by max_nodes become leaves (isLeaf() = no children)
+    has_child = np.zeros(len(parent), bool)
+    has_child[np.asarray(parent[1:], np.int64)] = True
+    leaf = np.where(has_child, 0, 1).astype(np.uint8)
+    leaf[0] = 0
+    n = len(parent)
+    weight = np.where(leaf > 0, rng.uniform(0.5, 10.0, n), 0.0)
+    weight[(leaf > 0) & (rng.random(n) < stop_frac)] = 0.0
+    return dict(k=k, L=L, scoring=scoring, weighting=weighting,
+                parent=np.asarray(parent, np.int32), is_leaf=leaf, desc=np.asarray(desc),
+                weight=weight)
+
+
+def write_vocabulary_text(path, voc, weight_fmt="%.17g"):
+    """TemplatedVocabulary::saveToTextFile's format (TemplatedVocabulary.h:1429-1447):
+    "k L scoring weighting", then "parent isLeaf d0 .. d31 weight" per node 1..n-1
+    (saveToTextFile streams the weight with the default 6 significant digits; pass
+    weight_fmt="%g" for that)."""
+    n = len(voc["parent"])
+    with open(path, "w") as f:
+        f.write("%d %d %d %d\n" % (voc["k"], voc["L"], voc["scoring"], voc["weighting"]))
+        for i in range(1, n):
+            f.write("%d %d %s %s\n" % (voc["parent"][i], voc["is_leaf"][i],
+                                       " ".join(str(int(b)) for b in voc["desc"][i]),
+                                       weight_fmt % voc["weight"][i]))
