@@ -35,7 +35,7 @@ __global__ void k_octree_lds(const OrbgGeom *, const int32_t *, const uint2 *, u
                              uint32_t *, uint32_t *, int32_t *, int32_t *);
 struct OrbgKeypointDev;
 __global__ void k_orient_desc(const OrbgGeom *, const uint8_t *, int64_t, int, const uint8_t *,
-                              const uint8_t *, const uint32_t *, const int32_t *,
+                              const uint8_t *, const uint4 *, const uint32_t *, const int32_t *,
                               OrbgKeypointDev *, uint8_t *, int32_t *);
 // match_kernels.hip
 int launch_match_pairs(hipStream_t st, hipStream_t aux, hipEvent_t evf, hipEvent_t evj,
@@ -214,6 +214,7 @@ struct orbg_ctx {
     int32_t *d_tile_base = nullptr;
     int2 *d_rtab = nullptr;
     uint32_t *d_ctab = nullptr;  // quadtree path-code tables (xs | ys per level)
+    uint4 *d_odtab = nullptr;    // k_orient_desc IC_Angle byte tables (make_od_tab)
     uint8_t *d_img = nullptr;
     size_t img_bytes = 0;
     uint8_t *d_pyr = nullptr, *d_blur = nullptr;
@@ -324,7 +325,8 @@ static void free_plan(orbg_ctx *c)
     if (c->stream) hipStreamSynchronize(c->stream);
     if (c->mstream) hipStreamSynchronize(c->mstream);
     c->mat_pending[0] = c->mat_pending[1] = false;
-    void *ptrs[] = {c->d_geom, c->d_cells, c->d_tile_base, c->d_rtab, c->d_ctab, c->d_pyr, c->d_blur,
+    void *ptrs[] = {c->d_geom, c->d_cells, c->d_tile_base, c->d_rtab, c->d_ctab, c->d_odtab,
+                    c->d_pyr, c->d_blur,
                     c->d_cell_cnt, c->d_cell_kp, c->d_keys, c->d_knode, c->d_act, c->d_qk,
                     c->d_nodes, c->d_lvl_kp, c->d_lvl_cnt, c->kps_slot[0], c->kps_slot[1],
                     c->desc_slot[0], c->desc_slot[1], c->counts_slot[0], c->counts_slot[1],
@@ -337,6 +339,7 @@ static void free_plan(orbg_ctx *c)
     c->d_tile_base = nullptr;
     c->d_rtab = nullptr;
     c->d_ctab = nullptr;
+    c->d_odtab = nullptr;
     c->d_pyr = c->d_blur = nullptr;
     c->d_cell_cnt = nullptr;
     c->d_cell_kp = nullptr;
@@ -367,6 +370,31 @@ static void free_plan(orbg_ctx *c)
     c->stereo_cap = c->last_nstereo = 0;
     c->h_pairs.clear();
     c->gw = c->gh = c->gbatch = 0;
+}
+
+// k_orient_desc's IC_Angle byte tables, [sh 0..3][w 0..92][weights, ones]: lane w holds
+// bytes 16c .. 16c+15 (c = w % 3) of patch row r = w / 3 read from sh bytes before the row
+// start, i.e. column u = 16c + b - sh - 15; inside the circle (|u| <= umax[|r - 15|],
+// ORBextractor.cc:92-104) the weight byte is u + 15 and the one byte 1, else both 0.
+static std::vector<uint4> make_od_tab(const int32_t *umax)
+{
+    std::vector<uint4> t(4 * ORBG_OD_TABW * 2);
+    for (int sh = 0; sh < 4; sh++)
+        for (int w = 0; w < ORBG_OD_TABW; w++) {
+            const int r = w / 3, cw = w % 3, v = r - ORBG_HALF_PATCH;
+            const int um = umax[v < 0 ? -v : v];
+            uint32_t wt[4] = {0, 0, 0, 0}, on[4] = {0, 0, 0, 0};
+            for (int b = 0; b < 16; b++) {
+                const int u = 16 * cw + b - sh - ORBG_HALF_PATCH;
+                if (u >= -um && u <= um) {
+                    wt[b >> 2] |= (uint32_t)(u + ORBG_HALF_PATCH) << (8 * (b & 3));
+                    on[b >> 2] |= 1u << (8 * (b & 3));
+                }
+            }
+            t[(sh * ORBG_OD_TABW + w) * 2] = make_uint4(wt[0], wt[1], wt[2], wt[3]);
+            t[(sh * ORBG_OD_TABW + w) * 2 + 1] = make_uint4(on[0], on[1], on[2], on[3]);
+        }
+    return t;
 }
 
 template <typename T>
@@ -651,10 +679,11 @@ static int plan(orbg_ctx *c, int w, int h, int batch)
     G.pyr_frame = (pyr_off + 255) & ~(int64_t)255;
     G.blur_frame = (blur_off + 255) & ~(int64_t)255;
 
+    const std::vector<uint4> odtab = make_od_tab(G.umax);
     const size_t B = (size_t)want_batch;
     int rc;
     if ((rc = dalloc(&c->d_geom, 1)) || (rc = dalloc(&c->d_cells, cells.size())) ||
-        (rc = dalloc(&c->d_ctab, ctab.size())) ||
+        (rc = dalloc(&c->d_ctab, ctab.size())) || (rc = dalloc(&c->d_odtab, odtab.size())) ||
         (rc = dalloc(&c->d_tile_base, tile_base.size())) || (rc = dalloc(&c->d_rtab, rtab.size())) ||
         (rc = dalloc(&c->d_pyr, B * G.pyr_frame)) || (rc = dalloc(&c->d_blur, B * G.blur_frame)) ||
         (rc = dalloc(&c->d_cell_cnt, B * G.ncells)) ||
@@ -682,6 +711,8 @@ static int plan(orbg_ctx *c, int w, int h, int batch)
         HIPCHK(hipMemcpy(c->d_rtab, rtab.data(), rtab.size() * sizeof(int2),
                          hipMemcpyHostToDevice));
     HIPCHK(hipMemcpy(c->d_ctab, ctab.data(), ctab.size() * sizeof(uint32_t),
+                     hipMemcpyHostToDevice));
+    HIPCHK(hipMemcpy(c->d_odtab, odtab.data(), odtab.size() * sizeof(uint4),
                      hipMemcpyHostToDevice));
     HIPCHK(hipMemset(c->counts_slot[0], 0, B * sizeof(int32_t)));
     HIPCHK(hipMemset(c->counts_slot[1], 0, B * sizeof(int32_t)));
@@ -867,9 +898,10 @@ static int launch_extract(orbg_ctx *c, const uint8_t *d_imgs, int B, int pitch, 
     c->d_desc = c->desc_slot[s];
     c->d_counts = c->counts_slot[s];
     PROF_LAUNCH(c, "orient_desc",
-                hipLaunchKernelGGL(k_orient_desc, dim3((G.frame_cap + 3) / 4 * B), dim3(256), 0, st,
-                                   c->d_geom, d_imgs, fs, pitch, c->d_pyr, c->d_blur,
-                                   c->d_lvl_kp, c->d_lvl_cnt, (OrbgKeypointDev *)c->d_kps,
+                hipLaunchKernelGGL(k_orient_desc,
+                                   dim3((G.out_frame + 4 * ORBG_OD_KPW - 1) / (4 * ORBG_OD_KPW) * B),
+                                   dim3(256), 0, st, c->d_geom, d_imgs, fs, pitch, c->d_pyr,
+                                   c->d_blur, c->d_odtab, c->d_lvl_kp, c->d_lvl_cnt, (OrbgKeypointDev *)c->d_kps,
                                    c->d_desc, c->d_counts));
     HIPCHK(hipEventRecord(c->ev_ext[s], st));
     HIPCHK(hipGetLastError());

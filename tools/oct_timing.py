@@ -7,6 +7,10 @@ import sys
 CODE = r'''
 import sys, time, numpy as np, torch
 sys.path.insert(0, ".")
+import os
+import orb_slam2_test_amd._lib as _L
+if os.environ.get("ORBG_VARIANT"):  # developer A/B: a liborbg.so built into lib/<variant>/
+    _L.LIB_PATH = os.path.join(os.path.dirname(_L.LIB_PATH), os.environ["ORBG_VARIANT"], "liborbg.so")
 from orb_slam2_test_amd import ORBextractor, synthetic as S
 B = int(sys.argv[1])
 fr = S.sequence(B, 376, 1241, seed=11)
@@ -23,6 +27,8 @@ print(" ".join("%s=%.3f" % (k, v[0] / 5) for k, v in e.ctx.profile_read().items(
 '''
 B = sys.argv[1] if len(sys.argv) > 1 else "256"
 for dbg in sys.argv[2:] or ["0"]:
-    env = dict(os.environ, ORBG_DBG=dbg)
+    # "<dbg>" or "<dbg>@<variant>" (variant = subdirectory of orb_slam2_test_amd/lib)
+    d, _, var = dbg.partition("@")
+    env = dict(os.environ, ORBG_DBG=d, ORBG_VARIANT=var)
     out = subprocess.run([sys.executable, "-c", CODE, B], env=env, capture_output=True, text=True)
     print("ORBG_DBG=%s B=%s: %s %s" % (dbg, B, out.stdout.strip(), out.stderr.strip()[-300:] if out.returncode else ""))
