@@ -856,7 +856,7 @@ __global__ __launch_bounds__(ORBG_OCT_THREADS) void k_octree(
             block_excl_scan(c < lv.ncells ? ccount[c] : 0, &tot, S.red);
             run += tot;
         }
-        if (run <= OCT_KEY_CAP && lv.ncells + 1 <= ORBG_OCT_ALIVE) return;  // k_octree_lds
+        if (run <= lv.oct_kcap && lv.ncells + 1 <= lv.oct_acap2) return;  // k_octree_lds
         run = 0;
         for (int c0 = 0; c0 < lv.ncells; c0 += nthr) {
             const int c = c0 + tid;

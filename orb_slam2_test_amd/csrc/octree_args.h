@@ -1,0 +1,27 @@
+// octree_args.h -- launch dimensions of k_octree_lds (host + device).
+#pragma once
+
+#include <stdint.h>
+
+// One k_octree_lds launch covers levels level0 .. level0 + gridDim.x - 1.  Dynamic LDS =
+// kcap * 6 + uni_bytes + acap2 * 2 (octree_kernels.hip OctLdsView).
+struct OctLdsDims {
+    int32_t level0;
+    int32_t kcap;       // candidates per level this launch can hold (multiple of 64)
+    int32_t acap;       // quadtree list capacity: max over its levels of out_cap
+    int32_t acap2;      // aux entries: max(acap, cells + 1)
+    int32_t nbw;        // bucket counter words: 512 * max roots (two u16 counters per word)
+    int32_t uni_bytes;  // max(nbw * 4, 3 * acap * 8)
+};
+
+// static LDS header of k_octree_lds
+struct OctLdsHdr {
+    int red[16];
+    int rootlo[20];
+    int s_alive, s_cur, s_seq, s_vbase, s_vend, s_err, s_nproc, s_phase2;
+};
+
+static inline size_t oct_lds_bytes(const OctLdsDims &d)
+{
+    return (size_t)d.kcap * 6 + (size_t)d.uni_bytes + (size_t)d.acap2 * 2;
+}

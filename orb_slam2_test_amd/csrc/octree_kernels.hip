@@ -16,6 +16,7 @@
 
 #include "orbg_device.h"
 #include "orbg_internal.h"
+#include "octree_args.h"
 
 #pragma clang fp contract(off)
 
@@ -27,20 +28,19 @@ namespace orbg {
 #define OCT_NBUCKET 16384  // counting-sort buckets: root (4 bits) + first 5 quadtree digits
 #define OCT_BSHIFT 18      // code >> 18 = root (4 bits) + digits 0..4
 
-struct OctLdsShared {
-    uint32_t codes[OCT_KEY_CAP];
-    uint16_t sidx[OCT_KEY_CAP];
-    union {
-        uint32_t bcnt[OCT_NBUCKET / 2];  // two u16 bucket counters per word
-        struct {
-            unsigned long long list[2][ORBG_OCT_ALIVE];
-            unsigned long long sortv[ORBG_OCT_ALIVE];
-        } q;
-    } u;
-    uint16_t aux[ORBG_OCT_ALIVE];
-    int red[16];
-    int rootlo[20];
-    int s_alive, s_cur, s_seq, s_vbase, s_vend, s_err, s_nproc, s_phase2;
+// LDS: a static header plus a dynamic area sized per launch (OctLdsDims, host
+// octree_lds_bytes): codes[kcap] u32 | sidx[kcap] u16 | uni | aux[acap2] u16, where uni is
+// the bucket counters (nbw u32, two u16 counters each) during the sort and afterwards the
+// two list buffers + the phase-2 sort keys (3 x acap u64).  A launch whose levels need
+// little LDS runs several workgroups per CU.
+struct OctLdsView {
+    uint32_t *codes;
+    uint16_t *sidx;
+    uint32_t *bcnt;
+    unsigned long long *list0, *list1;
+    __device__ unsigned long long *list(int k) const { return k ? list1 : list0; }
+    unsigned long long *sortv;
+    uint16_t *aux;
 };
 
 __device__ __forceinline__ unsigned long long rec_make(int lo, int cnt, int seq, int depth)
@@ -157,14 +157,31 @@ __device__ __forceinline__ void oct_children(uint32_t *codes, uint16_t *sidx,
     }
 }
 
+// level = level0 + blockIdx.x, frame = blockIdx.y; handles a level iff its candidate count
+// n <= D.kcap (k_octree takes the rest, same threshold)
 __global__ __launch_bounds__(OCT_T) void k_octree_lds(
     const OrbgGeom *__restrict__ g, const int32_t *__restrict__ cell_cnt,
     const uint2 *__restrict__ cell_kp, uint32_t *__restrict__ keys_all,
     uint32_t *__restrict__ scratch_all, uint32_t *__restrict__ lvl_kp,
-    int32_t *__restrict__ lvl_cnt, int32_t *__restrict__ err_flag)
+    int32_t *__restrict__ lvl_cnt, int32_t *__restrict__ err_flag, OctLdsDims D)
 {
-    __shared__ OctLdsShared S;
-    const int l = blockIdx.x, f = blockIdx.y, tid = threadIdx.x;
+    __shared__ OctLdsHdr S;
+    extern __shared__ __attribute__((aligned(16))) uint8_t oct_dyn[];
+    OctLdsView V;
+    {
+        uint8_t *p = oct_dyn;
+        V.codes = (uint32_t *)p;
+        p += (size_t)D.kcap * 4;
+        V.sidx = (uint16_t *)p;
+        p += (size_t)D.kcap * 2;
+        V.bcnt = (uint32_t *)p;
+        V.list0 = (unsigned long long *)p;
+        V.list1 = V.list0 + D.acap;
+        V.sortv = V.list1 + D.acap;
+        p += D.uni_bytes;
+        V.aux = (uint16_t *)p;
+    }
+    const int l = D.level0 + blockIdx.x, f = blockIdx.y, tid = threadIdx.x;
     const OrbgLevel &lv = g->lv[l];
     const int64_t kbase = (int64_t)f * g->keys_frame + lv.key_off;
     uint32_t *kglob = keys_all + kbase;
@@ -174,18 +191,18 @@ __global__ __launch_bounds__(OCT_T) void k_octree_lds(
     const int32_t *ccount = cell_cnt + (int64_t)f * g->ncells + lv.cell_base;
     const uint2 *ckp = cell_kp + ((int64_t)f * g->ncells + lv.cell_base) * g->cell_cap;
     const int ncells = lv.ncells;
-    if (ncells + 1 > ORBG_OCT_ALIVE) return;
+    if (ncells + 1 > D.acap2) return;
     int n = 0;
     for (int c0 = 0; c0 < ncells; c0 += OCT_T) {
         const int c = c0 + tid;
         int tot;
         const int off = oct_scan(c < ncells ? ccount[c] : 0, &tot, S.red) + n;
-        if (c < ncells) S.aux[c] = (uint16_t)min(off, 65535);
+        if (c < ncells) V.aux[c] = (uint16_t)min(off, 65535);
         n += tot;
     }
-    if (n > OCT_KEY_CAP) return;
-    if (tid == 0) S.aux[ncells] = (uint16_t)n;
-    for (int i = tid; i < OCT_NBUCKET / 2; i += OCT_T) S.u.bcnt[i] = 0;
+    if (n > D.kcap) return;
+    if (tid == 0) V.aux[ncells] = (uint16_t)n;
+    for (int i = tid; i < D.nbw; i += OCT_T) V.bcnt[i] = 0;
     __syncthreads();
 
     // ---- gather (vToDistributeKeys order: cell-major, FAST order inside a cell) +
@@ -205,8 +222,8 @@ __global__ __launch_bounds__(OCT_T) void k_octree_lds(
                 k[u] = 0;
                 e[u] = make_uint2(0, 0);
                 if (c < ncells) {
-                    const int lo = S.aux[c];
-                    cnt[u] = (int)S.aux[c + 1] - lo;
+                    const int lo = V.aux[c];
+                    cnt[u] = (int)V.aux[c + 1] - lo;
                     k[u] = lo + lane;
                     if (lane < cnt[u]) e[u] = ckp[(int64_t)c * g->cell_cap + lane];
                 }
@@ -217,7 +234,7 @@ __global__ __launch_bounds__(OCT_T) void k_octree_lds(
                     kglob[k[u]] = e[u].x;
                     cscr[k[u]] = e[u].y;
                     const uint32_t b = e[u].y >> OCT_BSHIFT;
-                    atomicAdd(&S.u.bcnt[b >> 1], 1u << (16 * (b & 1)));
+                    atomicAdd(&V.bcnt[b >> 1], 1u << (16 * (b & 1)));
                 }
                 for (int kl = lane + 64; kl < cnt[u]; kl += 64) {  // cells with > 64 corners
                     const int c = c0 + u * NW;
@@ -225,29 +242,25 @@ __global__ __launch_bounds__(OCT_T) void k_octree_lds(
                     kglob[k[u] - lane + kl] = x.x;
                     cscr[k[u] - lane + kl] = x.y;
                     const uint32_t b = x.y >> OCT_BSHIFT;
-                    atomicAdd(&S.u.bcnt[b >> 1], 1u << (16 * (b & 1)));
+                    atomicAdd(&V.bcnt[b >> 1], 1u << (16 * (b & 1)));
                 }
             }
         }
     }
     __syncthreads();
     if (g->dbg == 1) return;
-    // ---- exclusive scan of the 16384 u16 bucket counters (32 per thread) ----
+    // ---- exclusive scan of the nini * 1024 u16 bucket counters (2 * nini per thread) ----
     {
-        constexpr int PER = OCT_NBUCKET / 2 / OCT_T;  // words per thread
-        uint32_t w[PER];
+        const int PER = D.nbw / OCT_T;  // words per thread (= roots)
+        uint32_t *wb = V.bcnt + tid * PER;
         int sum = 0;
-#pragma unroll
-        for (int i = 0; i < PER; i++) {
-            w[i] = S.u.bcnt[tid * PER + i];
-            sum += (int)(w[i] & 0xFFFF) + (int)(w[i] >> 16);
-        }
+        for (int i = 0; i < PER; i++) sum += (int)(wb[i] & 0xFFFF) + (int)(wb[i] >> 16);
         int tot;
         int run = oct_scan(sum, &tot, S.red);
-#pragma unroll
         for (int i = 0; i < PER; i++) {
-            const int a = (int)(w[i] & 0xFFFF), b = (int)(w[i] >> 16);
-            S.u.bcnt[tid * PER + i] = (uint32_t)run | ((uint32_t)(run + a) << 16);
+            const uint32_t w = wb[i];
+            const int a = (int)(w & 0xFFFF), b = (int)(w >> 16);
+            wb[i] = (uint32_t)run | ((uint32_t)(run + a) << 16);
             run += a + b;
         }
     }
@@ -265,10 +278,10 @@ __global__ __launch_bounds__(OCT_T) void k_octree_lds(
             const int k = k0 + u * OCT_T;
             if (k < n) {
                 const uint32_t b = code[u] >> OCT_BSHIFT;
-                const uint32_t old = atomicAdd(&S.u.bcnt[b >> 1], 1u << (16 * (b & 1)));
+                const uint32_t old = atomicAdd(&V.bcnt[b >> 1], 1u << (16 * (b & 1)));
                 const int slot = (int)((old >> (16 * (b & 1))) & 0xFFFF);
-                S.codes[slot] = code[u];
-                S.sidx[slot] = (uint16_t)k;
+                V.codes[slot] = code[u];
+                V.sidx[slot] = (uint16_t)k;
             }
         }
     }
@@ -279,13 +292,13 @@ __global__ __launch_bounds__(OCT_T) void k_octree_lds(
     if (tid <= nIni) S.rootlo[tid] = 0;
     __syncthreads();
     for (int i = tid; i < n; i += OCT_T) {
-        const int r = (int)(S.codes[i] >> 28);
-        const int rp = i > 0 ? (int)(S.codes[i - 1] >> 28) : -1;
+        const int r = (int)(V.codes[i] >> 28);
+        const int rp = i > 0 ? (int)(V.codes[i - 1] >> 28) : -1;
         if (r != rp)
             for (int q = rp + 1; q <= r; q++) S.rootlo[q] = i;
     }
     if (tid == 0) {
-        const int rl = n > 0 ? (int)(S.codes[n - 1] >> 28) : -1;
+        const int rl = n > 0 ? (int)(V.codes[n - 1] >> 28) : -1;
         for (int q = rl + 1; q <= nIni; q++) S.rootlo[q] = n;
     }
     __syncthreads();
@@ -293,7 +306,7 @@ __global__ __launch_bounds__(OCT_T) void k_octree_lds(
         int a = 0;
         for (int r = 0; r < nIni; r++) {
             const int cnt = S.rootlo[r + 1] - S.rootlo[r];
-            if (cnt > 0) S.u.q.list[0][a++] = rec_make(S.rootlo[r], cnt, 0, 0);
+            if (cnt > 0) V.list(0)[a++] = rec_make(S.rootlo[r], cnt, 0, 0);
         }
         S.s_alive = a;
         S.s_cur = 0;
@@ -319,13 +332,13 @@ __global__ __launch_bounds__(OCT_T) void k_octree_lds(
             for (int q = 0; q < 5; q++) bb[ch][q] = 0;
             if (ch * OCT_T < alive) {
                 if (i < alive) {
-                    const unsigned long long r = S.u.q.list[cur][i];
+                    const unsigned long long r = V.list(cur)[i];
                     if (rec_cnt(r) > 1) {
                         if (rec_depth(r) >= OCT_CODE_DEPTH) {
                             S.s_err = 4;
                         } else {
                             sp = 1;
-                            oct_children(S.codes, S.sidx, r, bb[ch]);
+                            oct_children(V.codes, V.sidx, r, bb[ch]);
 #pragma unroll
                             for (int q = 0; q < 4; q++) {
                                 e += bb[ch][q + 1] > bb[ch][q];
@@ -356,7 +369,7 @@ __global__ __launch_bounds__(OCT_T) void k_octree_lds(
                 const int pre = oct_scan(e | (sp << 16), &tot, S.red) + run;
                 const int E = pre & 0xFFFF, splits_before = pre >> 16;
                 if (i < alive) {
-                    const unsigned long long r = S.u.q.list[cur][i];
+                    const unsigned long long r = V.list(cur)[i];
                     if (sp) {
                         const int blk = tot_e - E - e;
                         int k = 0;
@@ -364,12 +377,12 @@ __global__ __launch_bounds__(OCT_T) void k_octree_lds(
                         for (int q = 0; q < 4; q++) {
                             const int cnt = bb[ch][q + 1] - bb[ch][q];
                             if (cnt == 0) continue;
-                            S.u.q.list[nxt][blk + (e - 1 - k)] =
+                            V.list(nxt)[blk + (e - 1 - k)] =
                                 rec_make(bb[ch][q], cnt, seq0 + E + k, rec_depth(r) + 1);
                             k++;
                         }
                     } else {
-                        S.u.q.list[nxt][tot_e + i - splits_before] = r;
+                        V.list(nxt)[tot_e + i - splits_before] = r;
                     }
                 }
                 run += tot;
@@ -384,7 +397,7 @@ __global__ __launch_bounds__(OCT_T) void k_octree_lds(
             S.s_seq = seq0 + tot_e;
             S.s_vbase = seq0;
             S.s_vend = seq0 + tot_e;
-            if (na > ORBG_OCT_ALIVE || seq0 + tot_e > 65535) S.s_err = 5;
+            if (na > D.acap || seq0 + tot_e > 65535) S.s_err = 5;
         }
         __syncthreads();
         if (S.s_err) break;
@@ -408,20 +421,20 @@ __global__ __launch_bounds__(OCT_T) void k_octree_lds(
                 int fl = 0;
                 unsigned long long r = 0;
                 if (i < alive) {
-                    r = S.u.q.list[cur][i];
+                    r = V.list(cur)[i];
                     const int sq = rec_seq(r);
                     fl = rec_cnt(r) > 1 && sq >= vbase && sq < vend;
                 }
                 int tot;
                 const int o = oct_scan(fl, &tot, S.red) + np;
                 if (fl)
-                    S.u.q.sortv[o] = ((unsigned long long)rec_cnt(r) << 32) |
+                    V.sortv[o] = ((unsigned long long)rec_cnt(r) << 32) |
                                  ((unsigned long long)rec_seq(r) << 16) | (unsigned)i;
                 np += tot;
             }
-            for (int i = tid; i < alive; i += OCT_T) S.aux[i] = 0;
+            for (int i = tid; i < alive; i += OCT_T) V.aux[i] = 0;
             __syncthreads();
-            flip_bitonic_u64(S.u.q.sortv, np);
+            flip_bitonic_u64(V.sortv, np);
             // processing order p = largest (cnt, seq) first (:872); cut at the first p with
             // alive + sum_{p' <= p} (children - 1) >= N (:917-918)
             if (tid == 0) S.s_nproc = np;
@@ -432,11 +445,11 @@ __global__ __launch_bounds__(OCT_T) void k_octree_lds(
                     const int p = p0 + tid;
                     int dl = 0;
                     if (p < np) {
-                        const int pos = (int)(S.u.q.sortv[np - 1 - p] & 0xFFFF);
-                        const unsigned long long r = S.u.q.list[cur][pos];
+                        const int pos = (int)(V.sortv[np - 1 - p] & 0xFFFF);
+                        const unsigned long long r = V.list(cur)[pos];
                         if (rec_depth(r) >= OCT_CODE_DEPTH) S.s_err = 6;
                         int b[5];
-                        oct_children(S.codes, S.sidx, r, b);
+                        oct_children(V.codes, V.sidx, r, b);
                         int e = 0;
 #pragma unroll
                         for (int q = 0; q < 4; q++) e += b[q + 1] > b[q];
@@ -456,12 +469,12 @@ __global__ __launch_bounds__(OCT_T) void k_octree_lds(
                 const int p = p0 + tid;
                 int e = 0;
                 if (p < nproc) {
-                    const int pos = (int)(S.u.q.sortv[np - 1 - p] & 0xFFFF);
+                    const int pos = (int)(V.sortv[np - 1 - p] & 0xFFFF);
                     int b[5];
-                    oct_children(S.codes, S.sidx, S.u.q.list[cur][pos], b);
+                    oct_children(V.codes, V.sidx, V.list(cur)[pos], b);
 #pragma unroll
                     for (int q = 0; q < 4; q++) e += b[q + 1] > b[q];
-                    S.aux[pos] = 1;  // processed parent
+                    V.aux[pos] = 1;  // processed parent
                 }
                 int t;
                 oct_scan(e, &t, S.red);
@@ -474,9 +487,9 @@ __global__ __launch_bounds__(OCT_T) void k_octree_lds(
                     int e = 0, b[5] = {0, 0, 0, 0, 0};
                     unsigned long long r = 0;
                     if (p < nproc) {
-                        const int pos = (int)(S.u.q.sortv[np - 1 - p] & 0xFFFF);
-                        r = S.u.q.list[cur][pos];
-                        oct_children(S.codes, S.sidx, r, b);
+                        const int pos = (int)(V.sortv[np - 1 - p] & 0xFFFF);
+                        r = V.list(cur)[pos];
+                        oct_children(V.codes, V.sidx, r, b);
 #pragma unroll
                         for (int q = 0; q < 4; q++) e += b[q + 1] > b[q];
                     }
@@ -489,7 +502,7 @@ __global__ __launch_bounds__(OCT_T) void k_octree_lds(
                         for (int q = 0; q < 4; q++) {
                             const int cnt = b[q + 1] - b[q];
                             if (cnt == 0) continue;
-                            S.u.q.list[nxt][blk + (e - 1 - k)] =
+                            V.list(nxt)[blk + (e - 1 - k)] =
                                 rec_make(b[q], cnt, seq0 + E + k, rec_depth(r) + 1);
                             k++;
                         }
@@ -499,10 +512,10 @@ __global__ __launch_bounds__(OCT_T) void k_octree_lds(
                 int runp = 0;
                 for (int i0 = 0; i0 < alive; i0 += OCT_T) {
                     const int i = i0 + tid;
-                    const int fl = (i < alive) ? (int)S.aux[i] : 0;
+                    const int fl = (i < alive) ? (int)V.aux[i] : 0;
                     int tot;
                     const int before = oct_scan(fl, &tot, S.red) + runp;
-                    if (i < alive && !fl) S.u.q.list[nxt][tot_e + i - before] = S.u.q.list[cur][i];
+                    if (i < alive && !fl) V.list(nxt)[tot_e + i - before] = V.list(cur)[i];
                     runp += tot;
                 }
             }
@@ -514,7 +527,7 @@ __global__ __launch_bounds__(OCT_T) void k_octree_lds(
                 S.s_seq = seq0 + tot_e;
                 S.s_vbase = seq0;
                 S.s_vend = seq0 + tot_e;
-                if (na > ORBG_OCT_ALIVE || seq0 + tot_e > 65535) S.s_err = 7;
+                if (na > D.acap || seq0 + tot_e > 65535) S.s_err = 7;
             }
             __syncthreads();
             if (S.s_err) break;
@@ -532,11 +545,11 @@ __global__ __launch_bounds__(OCT_T) void k_octree_lds(
         return;
     }
     // label every sorted position with its node's list position, then one flat pass
-    uint32_t *best = (uint32_t *)S.u.q.sortv;
+    uint32_t *best = (uint32_t *)V.sortv;
     for (int i = tid; i < alive; i += OCT_T) {
-        const unsigned long long r = S.u.q.list[cur][i];
+        const unsigned long long r = V.list(cur)[i];
         const int lo = rec_lo(r), cnt = rec_cnt(r);
-        for (int p = lo; p < lo + cnt; p++) S.codes[p] = (uint32_t)i;
+        for (int p = lo; p < lo + cnt; p++) V.codes[p] = (uint32_t)i;
         best[i] = 0;
     }
     __syncthreads();
@@ -545,8 +558,8 @@ __global__ __launch_bounds__(OCT_T) void k_octree_lds(
 #pragma unroll
         for (int u = 0; u < 4; u++) {
             const int p = p0 + u * OCT_T;
-            idx[u] = p < n ? S.sidx[p] : 0;
-            pos[u] = p < n ? S.codes[p] : 0;
+            idx[u] = p < n ? V.sidx[p] : 0;
+            pos[u] = p < n ? V.codes[p] : 0;
         }
 #pragma unroll
         for (int u = 0; u < 4; u++) key[u] = kglob[idx[u]];

@@ -15,6 +15,7 @@
 
 #include "../../include/orbg.h"
 #include "orbg_internal.h"
+#include "octree_args.h"
 #include "track_args.h"
 #include "schur_args.h"
 #include "bow_args.h"
@@ -32,7 +33,7 @@ __global__ void k_octree(const OrbgGeom *, const int32_t *, const uint2 *, uint3
                          uint32_t *, uint32_t *, uint8_t *, int4 *, uint32_t *, int32_t *,
                          int32_t *);
 __global__ void k_octree_lds(const OrbgGeom *, const int32_t *, const uint2 *, uint32_t *,
-                             uint32_t *, uint32_t *, int32_t *, int32_t *);
+                             uint32_t *, uint32_t *, int32_t *, int32_t *, OctLdsDims);
 struct OrbgKeypointDev;
 __global__ void k_orient_desc(const OrbgGeom *, const uint8_t *, int64_t, int, const uint8_t *,
                               const uint8_t *, const uint4 *, const uint32_t *, const int32_t *,
@@ -208,6 +209,7 @@ struct orbg_ctx {
     std::vector<OrbgCell> cells;
     std::vector<int32_t> tile_base;
     int total_tiles = 0;
+    OctLdsDims oct_dims[2] = {};
     // device
     OrbgGeom *d_geom = nullptr;
     OrbgCell *d_cells = nullptr;
@@ -672,6 +674,48 @@ static int plan(orbg_ctx *c, int w, int h, int batch)
     }
     if ((int64_t)key_off * 1 >= (1 << 24))
         return set_err(ORBG_ENOTSUP, "candidate capacity %d exceeds 2^24", key_off);
+    // k_octree_lds launches: level 0 alone with room for OCT_KEY_CAP candidates (one
+    // workgroup per CU, one round at B <= 256 frames); levels 1.. sized for three
+    // workgroups per CU.  A level whose candidates exceed its launch's kcap goes to k_octree.
+    {
+        auto dims = [&](int l0, int l1, int kcap_or_budget, bool budget) {
+            OctLdsDims d{};
+            d.level0 = l0;
+            int acap = 0, cells = 0, roots = 0;
+            for (int l = l0; l < l1; l++) {
+                acap = std::max(acap, G.lv[l].out_cap);
+                cells = std::max(cells, G.lv[l].ncells + 1);
+                roots = std::max(roots, G.lv[l].nini);
+            }
+            d.acap = (acap + 63) & ~63;
+            d.acap2 = (std::max(d.acap, cells) + 7) & ~7;
+            d.nbw = 512 * roots;
+            d.uni_bytes = std::max(d.nbw * 4, 3 * d.acap * 8);
+            if (budget) {
+                const int room = kcap_or_budget - d.uni_bytes - 2 * d.acap2;
+                d.kcap = std::min(OCT_KEY_CAP, std::max(0, room / 6) & ~63);
+            } else {
+                d.kcap = kcap_or_budget;
+            }
+            if (d.acap > ORBG_OCT_ALIVE) d.kcap = 0;  // k_octree only
+            for (int l = l0; l < l1; l++) {
+                G.lv[l].oct_kcap = d.kcap;
+                G.lv[l].oct_acap2 = d.acap2;
+            }
+            return d;
+        };
+        c->oct_dims[0] = dims(0, 1, OCT_KEY_CAP, false);
+        // 3 workgroups per CU: 160 KB / 3 minus the static header
+        c->oct_dims[1] = dims(1, G.L, 163840 / 3 - (int)sizeof(OctLdsHdr) - 64, true);
+        for (int k = 0; k < 2; k++) {
+            const size_t b = oct_lds_bytes(c->oct_dims[k]);
+            if (b + sizeof(OctLdsHdr) > 160 * 1024)
+                return set_err(ORBG_ENOTSUP, "k_octree_lds needs %zu LDS bytes", b);
+            if (b > 64 * 1024)
+                HIPCHK(hipFuncSetAttribute((const void *)k_octree_lds,
+                                           hipFuncAttributeMaxDynamicSharedMemorySize, (int)b));
+        }
+    }
     G.keys_frame = key_off;
     G.nodes_frame = node_off;
     G.out_frame = out_off;
@@ -878,9 +922,16 @@ static int launch_extract(orbg_ctx *c, const uint8_t *d_imgs, int B, int pitch, 
                 hipLaunchKernelGGL(k_blur, dim3(c->total_tiles * B), dim3(256), 0, st, c->d_geom,
                                    c->d_tile_base, d_imgs, fs, pitch, c->d_pyr, c->d_blur));
     PROF_LAUNCH(c, "octree",
-                hipLaunchKernelGGL(k_octree_lds, dim3(G.L, B), dim3(512), 0, st, c->d_geom,
-                                   c->d_cell_cnt, c->d_cell_kp, c->d_keys, c->d_act,
-                                   c->d_lvl_kp, c->d_lvl_cnt, c->d_err));
+                hipLaunchKernelGGL(k_octree_lds, dim3(1, B), dim3(512),
+                                   oct_lds_bytes(c->oct_dims[0]), st, c->d_geom, c->d_cell_cnt,
+                                   c->d_cell_kp, c->d_keys, c->d_act, c->d_lvl_kp, c->d_lvl_cnt,
+                                   c->d_err, c->oct_dims[0]));
+    if (G.L > 1)
+        PROF_LAUNCH(c, "octree",
+                    hipLaunchKernelGGL(k_octree_lds, dim3(G.L - 1, B), dim3(512),
+                                       oct_lds_bytes(c->oct_dims[1]), st, c->d_geom,
+                                       c->d_cell_cnt, c->d_cell_kp, c->d_keys, c->d_act,
+                                       c->d_lvl_kp, c->d_lvl_cnt, c->d_err, c->oct_dims[1]));
     PROF_LAUNCH(c, "octree_big",
                 hipLaunchKernelGGL(k_octree, dim3(G.L, B), dim3(ORBG_OCT_THREADS), 0, st,
                                    c->d_geom, c->d_cell_cnt, c->d_cell_kp, c->d_keys, c->d_knode,

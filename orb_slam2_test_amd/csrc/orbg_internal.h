@@ -51,6 +51,7 @@ struct OrbgLevel {
     int64_t blur_off;             // byte offset in a frame's blurred pyramid
     float scale;                  // mvScaleFactor[l]
     int32_t patch_size;           // int(PATCH_SIZE * scale)
+    int32_t oct_kcap, oct_acap2;  // this level's k_octree_lds launch: candidate / cell caps
 };
 
 struct OrbgGeom {
