@@ -334,22 +334,36 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(6, 8))) voi
         // latency per chunk instead of one per 64 words)
         const int NWR = RG + 2;
         const int nw = H * NWR;
+        // word i = lane + 64 k of the window as (row r, word j), advanced by (64 / NWR,
+        // 64 % NWR) per k (no division in the loop); its byte offset r * pitch + 4 j - 1
+        // and tile offset r * P + 4 j advance with it
+        const int dr = 64 / NWR, dj = 64 - dr * NWR;
+        int r = lane / NWR, j = lane - r * NWR;
+        int goff = r * pitch + 4 * j - 1, toff = r * P + 4 * j;
+        const int gstep_r = dr * pitch + 4 * dj, tstep_r = dr * P + 4 * dj;
+        const int gwrap = pitch - 4 * NWR, twrap = P - 4 * NWR;
         for (int i0 = 0; i0 < nw; i0 += 8 * 64) {
             uint32_t lo[8], hi[8], sh[8];
             int dst[8];
 #pragma unroll
             for (int k = 0; k < 8; k++) {
-                const int i = i0 + 64 * k + lane;
-                lo[k] = hi[k] = sh[k] = 0;
-                dst[k] = -1;
-                if (i < nw) {
-                    const int r = i / NWR, j = i - r * NWR;
-                    const uintptr_t a = (uintptr_t)(base + (int64_t)r * pitch + 4 * j - 1);
-                    const uint32_t *aw = (const uint32_t *)(a & ~(uintptr_t)3);
-                    lo[k] = aw[0];
-                    hi[k] = aw[1];
-                    sh[k] = (uint32_t)(a & 3);
-                    dst[k] = r * P + 4 * j;
+                // unconditional loads (a lane past the window reads word 0 again): no
+                // branch, so all 16 loads are in flight before the first wait
+                const bool ok = i0 + 64 * k + lane < nw;
+                const int go = ok ? goff : -1;
+                const int mis = (int)(((uint32_t)(uintptr_t)base + (uint32_t)go) & 3u);
+                const uint32_t *aw = (const uint32_t *)(base + (go - mis));
+                lo[k] = aw[0];
+                hi[k] = aw[1];
+                sh[k] = (uint32_t)mis;
+                dst[k] = ok ? toff : -1;
+                goff += gstep_r;
+                toff += tstep_r;
+                j += dj;
+                if (j >= NWR) {
+                    j -= NWR;
+                    goff += gwrap;
+                    toff += twrap;
                 }
             }
 #pragma unroll
@@ -459,61 +473,85 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(6, 8))) voi
     // at the cell threshold th counting as 0.  With s_p >= max(th, 1) that is exactly
     //   max(raw 8-neighbour scores) < max(th, s_p)
     // (a neighbour q < th is always below max(th, s_p); one with q >= th must be < s_p).
-    // Pixel pairs in packed u16 lanes; the keep bits of unit u go to mk[u] (the pretest
-    // list's LDS, free by now).
-    uint8_t *mk = (uint8_t *)plist;
+    // Pixel pairs in packed u16 lanes; keep bits (4 per unit) of unit (ry, gg).
     const v2s one = (v2s){1, 1};
-    auto nms = [&](int th) -> int {
+    auto keep_bits = [&](int ry, int gg, int th) -> uint32_t {
         const v2s t1v = (v2s){(short)max(th, 1), (short)max(th, 1)};
         const v2s thv = (v2s){(short)th, (short)th};
-        int cnt = 0;
-        for (int u = lane, ry = ry0, gg = gg0; u < nunits; u += 64) {
-            const uint32_t *mu = (const uint32_t *)(sc + ry * P + 4 * gg);
-            const uint32_t *m0 = (const uint32_t *)(sc + (ry + 1) * P + 4 * gg);
-            const uint32_t *md = (const uint32_t *)(sc + (ry + 2) * P + 4 * gg);
-            const uint32_t c1 = m0[1];
-            uint32_t kb = 0;
-            if (c1 != 0) {  // a unit with no scored pixel keeps nothing
-                const uint32_t u0 = mu[0], u1 = mu[1], u2 = mu[2];
-                const uint32_t c0 = m0[0], c2 = m0[2];
-                const uint32_t d0 = md[0], d1 = md[1], d2 = md[2];
-                // pixels 0,1 (bytes 4,5): neighbours at bytes 3..6
-                v2s mA = pmax(pmax(gather2<3>(u0, u1, u2), gather2<4>(u0, u1, u2)),
-                              gather2<5>(u0, u1, u2));
-                mA = pmax(mA, pmax(pmax(gather2<3>(d0, d1, d2), gather2<4>(d0, d1, d2)),
-                                   gather2<5>(d0, d1, d2)));
-                mA = pmax(mA, pmax(gather2<3>(c0, c1, c2), gather2<5>(c0, c1, c2)));
-                // pixels 2,3 (bytes 6,7): neighbours at bytes 5..8
-                v2s mB = pmax(pmax(gather2<5>(u0, u1, u2), gather2<6>(u0, u1, u2)),
-                              gather2<7>(u0, u1, u2));
-                mB = pmax(mB, pmax(pmax(gather2<5>(d0, d1, d2), gather2<6>(d0, d1, d2)),
-                                   gather2<7>(d0, d1, d2)));
-                mB = pmax(mB, pmax(gather2<5>(c0, c1, c2), gather2<7>(c0, c1, c2)));
-                const v2s sA = gather2<4>(c0, c1, c2), sB = gather2<6>(c0, c1, c2);
-                // keep <=> min(s - t1, max(th, s) - M - 1) >= 0: sign bit of each u16 lane
-                auto keep = [&](v2s sv, v2s m) -> uint32_t {
-                    const v2s k = pmin(sv - t1v, pmax(thv, sv) - m - one);
-                    const uint32_t w = __builtin_bit_cast(uint32_t, k);
-                    return (~w >> 15 & 1u) | (~w >> 30 & 2u);
-                };
-                kb = keep(sA, mA) | keep(sB, mB) << 2;
-                const int valid = min(RW - 4 * gg, 4);
-                if (valid < 4) kb &= (1u << valid) - 1u;
-                cnt += __popc(kb);
-            }
-            mk[u] = (uint8_t)kb;
-            ry += rstep;
-            gg += gstep;
-            if (gg >= RG) {
-                gg -= RG;
-                ry++;
-            }
-        }
-        return wave_sum(cnt);
+        const uint32_t *mu = (const uint32_t *)(sc + ry * P + 4 * gg);
+        const uint32_t *m0 = (const uint32_t *)(sc + (ry + 1) * P + 4 * gg);
+        const uint32_t *md = (const uint32_t *)(sc + (ry + 2) * P + 4 * gg);
+        const uint32_t c1 = m0[1];
+        if (c1 == 0) return 0u;  // a unit with no scored pixel keeps nothing
+        const uint32_t u0 = mu[0], u1 = mu[1], u2 = mu[2];
+        const uint32_t c0 = m0[0], c2 = m0[2];
+        const uint32_t d0 = md[0], d1 = md[1], d2 = md[2];
+        // pixels 0,1 (bytes 4,5): neighbours at bytes 3..6
+        v2s mA = pmax(pmax(gather2<3>(u0, u1, u2), gather2<4>(u0, u1, u2)), gather2<5>(u0, u1, u2));
+        mA = pmax(mA, pmax(pmax(gather2<3>(d0, d1, d2), gather2<4>(d0, d1, d2)),
+                           gather2<5>(d0, d1, d2)));
+        mA = pmax(mA, pmax(gather2<3>(c0, c1, c2), gather2<5>(c0, c1, c2)));
+        // pixels 2,3 (bytes 6,7): neighbours at bytes 5..8
+        v2s mB = pmax(pmax(gather2<5>(u0, u1, u2), gather2<6>(u0, u1, u2)), gather2<7>(u0, u1, u2));
+        mB = pmax(mB, pmax(pmax(gather2<5>(d0, d1, d2), gather2<6>(d0, d1, d2)),
+                           gather2<7>(d0, d1, d2)));
+        mB = pmax(mB, pmax(gather2<5>(c0, c1, c2), gather2<7>(c0, c1, c2)));
+        const v2s sA = gather2<4>(c0, c1, c2), sB = gather2<6>(c0, c1, c2);
+        // keep <=> min(s - t1, max(th, s) - M - 1) >= 0: sign bit of each u16 lane
+        auto keep = [&](v2s sv, v2s m) -> uint32_t {
+            const v2s k = pmin(sv - t1v, pmax(thv, sv) - m - one);
+            const uint32_t w = __builtin_bit_cast(uint32_t, k);
+            return (~w >> 15 & 1u) | (~w >> 30 & 2u);
+        };
+        uint32_t kb = keep(sA, mA) | keep(sB, mB) << 2;
+        const int valid = min(RW - 4 * gg, 4);
+        if (valid < 4) kb &= (1u << valid) - 1u;
+        return kb;
     };
-    // FAST at iniThFAST; an empty cell retries at minThFAST (ORBextractor.cc:1069-1075)
-    // with every unit scored (the window tile is still intact)
-    if (nms(thi) == 0) {
+    // ---- raster-order compaction of one 64-unit chunk: lane's unit (ry, gg) keeps kb ----
+    const int64_t slot = (int64_t)f * g->ncells + c;
+    uint2 *out = cell_kp + slot * g->cell_cap;
+    int run = 0;
+    auto emit = [&](uint32_t kb, int ry, int gg) {
+        const int n = __popc(kb);
+        int tot;
+        const int incl = wave_incl_scan_small(n, &tot);
+        if (tot == 0) return;  // wave-uniform
+        // path codes by shuffle, all lanes active (a lane past the region reads lane 0)
+        const uint32_t cy = (uint32_t)__shfl((int)ys_l, ry & 63, 64);
+        uint32_t cx[4];
+#pragma unroll
+        for (int i = 0; i < 4; i++) cx[i] = (uint32_t)__shfl((int)xs_l, (4 * gg + i) & 63, 64);
+        if (kb) {
+            int off = run + incl - n;
+            const uint32_t c1 = *(const uint32_t *)(sc + (ry + 1) * P + 4 * gg + 4);
+            const int x0 = xo + 4 * gg, y = yo + ry;
+#pragma unroll
+            for (int i = 0; i < 4; i++)
+                if (kb & (1u << i))
+                    out[off++] = make_uint2(orbg_pack(x0 + i, y, (c1 >> (8 * i)) & 0xFF),
+                                            cx[i] | cy);
+        }
+        run += tot;
+    };
+    // FAST at iniThFAST: only pretest survivors can hold a corner, and their list is in
+    // raster order, so NMS + compaction walk the list densely
+    for (int j0 = 0; j0 < npass; j0 += 64) {
+        const int j = j0 + lane;
+        int ry = 0, gg = 0;
+        uint32_t kb = 0;
+        if (j < npass) {
+            const int e = plist[j];
+            ry = e >> 8;
+            gg = e & 0xFF;
+            kb = keep_bits(ry, gg, thi);
+        }
+        emit(kb, ry, gg);
+    }
+    if (g->dbg == 13) return;
+    if (run == 0) {
+        // an empty cell retries at minThFAST (ORBextractor.cc:1069-1075) with every unit
+        // scored (the window tile is still intact)
         wave_sync_lds();
         for (int u = lane, ry = ry0, gg = gg0; u < nunits; u += 64) {
             score_unit(ry, gg);
@@ -525,52 +563,15 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(6, 8))) voi
             }
         }
         wave_sync_lds();
-        nms(tlo);
-    }
-    const int nib = 0;
-    wave_sync_lds();
-    if (g->dbg == 13) return;
-
-    // ---- raster-order compaction ----
-    const int64_t slot = (int64_t)f * g->ncells + c;
-    uint2 *out = cell_kp + slot * g->cell_cap;
-    int run = 0;
-    for (int u0 = 0, ry = ry0, gg = gg0; u0 < nunits; u0 += 64) {
-        const int u = u0 + lane;
-        const uint32_t mask = u < nunits ? (mk[u] >> nib) & 0xFu : 0u;
-        const int n = __popc(mask);
-        int tot;
-        const int incl = wave_incl_scan_small(n, &tot);
-        if (tot == 0) {  // wave-uniform
+        for (int u0 = 0, ry = ry0, gg = gg0; u0 < nunits; u0 += 64) {
+            const uint32_t kb = u0 + lane < nunits ? keep_bits(ry, gg, tlo) : 0u;
+            emit(kb, ry, gg);
             ry += rstep;
             gg += gstep;
             if (gg >= RG) {
                 gg -= RG;
                 ry++;
             }
-            continue;
-        }
-        // path codes by shuffle, all lanes active (a lane past the region reads lane 0)
-        const uint32_t cy = (uint32_t)__shfl((int)ys_l, ry & 63, 64);
-        uint32_t cx[4];
-#pragma unroll
-        for (int i = 0; i < 4; i++) cx[i] = (uint32_t)__shfl((int)xs_l, (4 * gg + i) & 63, 64);
-        if (mask) {
-            int off = run + incl - n;
-            const uint32_t c1 = *(const uint32_t *)(sc + (ry + 1) * P + 4 * gg + 4);
-            const int x0 = xo + 4 * gg, y = yo + ry;
-#pragma unroll
-            for (int i = 0; i < 4; i++)
-                if (mask & (1u << i))
-                    out[off++] = make_uint2(orbg_pack(x0 + i, y, (c1 >> (8 * i)) & 0xFF),
-                                            cx[i] | cy);
-        }
-        run += tot;
-        ry += rstep;
-        gg += gstep;
-        if (gg >= RG) {
-            gg -= RG;
-            ry++;
         }
     }
     if (lane == 0) cell_cnt[slot] = run;
