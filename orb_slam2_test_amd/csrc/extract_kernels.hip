@@ -303,12 +303,20 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(6, 8))) voi
     const int P = g->fc_pitch;
     uint8_t *tile = (uint8_t *)fc_lds + wv * g->fc_wave_bytes;
     uint8_t *sc = tile + g->fc_tile_rows * P;
-    const int cid = xcd_remap(blockIdx.x, gridDim.x) * 4 + wv;
+    // wave-uniform: the cell record and level parameters come through the scalar cache
+    const int cid = __builtin_amdgcn_readfirstlane(xcd_remap(blockIdx.x, gridDim.x) * 4 + wv);
     if (cid >= g->ncells * nframes) return;  // wave-uniform; no workgroup barrier below
     const int f = cid / g->ncells, c = cid - f * g->ncells;
-    const OrbgCell cl = cells[c];
-    const int l = cl.level;
-    const int W = cl.w, H = cl.h;
+    // one dwordx4 (scalar load: sub-dword loads would go through the vector path)
+    const uint4 cw4 = ((const uint4 *)cells)[c];
+    const uint32_t cw0 = __builtin_amdgcn_readfirstlane(cw4.x);  // level | pad
+    const uint32_t cw1 = __builtin_amdgcn_readfirstlane(cw4.y);  // x0 | y0
+    const uint32_t cw2 = __builtin_amdgcn_readfirstlane(cw4.z);  // w | h
+    struct {
+        int x0, y0;
+    } cl = {(int)(int16_t)(cw1 & 0xFFFF), (int)(int16_t)(cw1 >> 16)};
+    const int l = (int)(int16_t)(cw0 & 0xFFFF);
+    const int W = (int)(int16_t)(cw2 & 0xFFFF), H = (int)(int16_t)(cw2 >> 16);
     const uint8_t *base;
     int pitch;
     if (l == 0) {
@@ -406,8 +414,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(6, 8))) voi
     // 12/0), so "both brighter" or "both darker" for some adjacent pair is necessary.  Only
     // units with a pixel passing it are scored; the others keep score 0, which the NMS at
     // iniThFAST treats exactly like any score below th (a neighbour < th never blocks).
-    // Pixel pairs in packed i16 lanes: mb = max over pairs of min(ca, cb) (> v + th <=>
-    // some pair brighter), md = min over pairs of max(ca, cb) (< v - th <=> darker).
+    // Pixel pairs in packed i16 lanes.  "Some adjacent pair both brighter" is
+    // (b0 & b4) | (b4 & b8) | (b8 & b12) | (b12 & b0) = (b0 | b8) & (b4 | b12), i.e.
+    // mb = min(max(c0, c8), max(c4, c12)) > v + th; darker: md = max(min(c0, c8),
+    // min(c4, c12)) < v - th.
     uint16_t *plist = (uint16_t *)(tile + g->fc_list_off);
     int npass = 0;
     {
@@ -434,10 +444,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(6, 8))) voi
                     const v2s c4 = gather2<7 + i>(r3[0], r3[1], r3[2]);
                     const v2s c8 = gather2<4 + i>(r0[0], r0[1], r0[2]);
                     const v2s c12 = gather2<1 + i>(r3[0], r3[1], r3[2]);
-                    const v2s mb = pmax(pmax(pmin(c0, c4), pmin(c4, c8)),
-                                        pmax(pmin(c8, c12), pmin(c12, c0)));
-                    const v2s md = pmin(pmin(pmax(c0, c4), pmax(c4, c8)),
-                                        pmin(pmax(c8, c12), pmax(c12, c0)));
+                    // "some adjacent compass pair both brighter" = (b0|b8) & (b4|b12)
+                    const v2s mb = pmin(pmax(c0, c8), pmax(c4, c12));
+                    const v2s md = pmax(pmin(c0, c8), pmin(c4, c12));
                     const v2s k = pmax(mb - v, v - md) - vth1;  // >= 0 <=> pass
                     const uint32_t w = __builtin_bit_cast(uint32_t, k);
                     return (~w >> 15 & 1u) | (~w >> 30 & 2u);
@@ -1367,7 +1376,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(ORBG_OD_WPE
     const int nb = (g->out_frame + 4 * OD_KPW - 1) / (4 * OD_KPW);  // blocks per frame
     const int id = xcd_remap(blockIdx.x, gridDim.x);
     const int f = id / nb, bx = id - f * nb;
-    const int s0 = (bx * 4 + wv) * OD_KPW;
+    const int s0 = __builtin_amdgcn_readfirstlane((bx * 4 + wv) * OD_KPW);  // wave-uniform
     const int L = g->L, OF = g->out_frame;
     if (s0 >= OF) return;
     const uint32_t kl = (lane < OD_KPW && s0 + lane < OF) ? lvl_kp[(int64_t)f * OF + s0 + lane] : 0u;
