@@ -600,6 +600,14 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(6, 8))) voi
 #define BLUR_IW (BLUR_TW + 16)  // 9 x 16-byte chunks from x = tile_x0 - 4 (135 bytes read)
 #define BLUR_IH (BLUR_TH + 6)
 
+// v_dot2_u32_u16 on u16 pairs held in u32 words
+__device__ __forceinline__ uint32_t udot2_u32(uint32_t a, uint32_t b, uint32_t c)
+{
+    typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));
+    return __builtin_amdgcn_udot2(__builtin_bit_cast(u16x2, a), __builtin_bit_cast(u16x2, b), c,
+                                  false);
+}
+
 __device__ __forceinline__ int reflect101(int i, int n)
 {
     // single reflection suffices for the 3-pixel halo (n >= 4 for every level)
@@ -614,7 +622,7 @@ __global__ __launch_bounds__(256) void k_blur(const OrbgGeom *__restrict__ g,
                                               uint8_t *__restrict__ blur)
 {
     __shared__ __attribute__((aligned(16))) uint8_t in[BLUR_IH][BLUR_IW];
-    __shared__ __attribute__((aligned(16))) uint16_t rows[BLUR_IH][BLUR_TW];
+    __shared__ __attribute__((aligned(16))) uint32_t rows[BLUR_IH / 2][BLUR_TW];  // row-pair sums
     const int ntiles = tile_base[g->L];
     const int id = xcd_remap(blockIdx.x, gridDim.x);
     const int f = id / ntiles, bt = id - f * ntiles, tid = threadIdx.x;
@@ -688,67 +696,72 @@ __global__ __launch_bounds__(256) void k_blur(const OrbgGeom *__restrict__ g,
         }
     }
     __syncthreads();
-    const int k0 = g->gk[0], k1 = g->gk[1], k2 = g->gk[2], k3 = g->gk[3], k4 = g->gk[4],
-              k5 = g->gk[5], k6 = g->gk[6];
-    // row pass: unit = (row r, 4-column group j); outputs x = 4j..4j+3 need tile bytes
-    // 4j+1..4j+10.  Two outputs per packed u16 multiply-add: a row sum is at most
-    // sum(k) * 255 <= 257 * 255 = 65535 (orbg_create enforces sum(k) <= 257), so every
-    // partial sum is exact in 16 bits.
+    const uint32_t k0 = g->gk[0], k1 = g->gk[1], k2 = g->gk[2], k3 = g->gk[3], k4 = g->gk[4],
+                   k5 = g->gk[5], k6 = g->gk[6];
+    // row pass: unit = (row pair rp, 4-column group j).  Output x = 4j+i of a row needs tile
+    // bytes 4j+1+i .. 4j+7+i, i.e. the aligned dwords W0..W2 = bytes 4j .. 4j+11 against
+    // the 7 weights placed at byte 1+i: ten v_dot4_u32_u8 per 4 outputs (row sums <=
+    // 257 * 255, exact).  The two rows' sums of a column are stored as one u16 pair,
+    // rows[rp][x] = sum(2rp, x) | sum(2rp+1, x) << 16, for the column pass's v_dot2.
     {
-        typedef unsigned short v2u __attribute__((ext_vector_type(2)));
-        const v2u kv[7] = {(v2u){(unsigned short)k0, (unsigned short)k0},
-                           (v2u){(unsigned short)k1, (unsigned short)k1},
-                           (v2u){(unsigned short)k2, (unsigned short)k2},
-                           (v2u){(unsigned short)k3, (unsigned short)k3},
-                           (v2u){(unsigned short)k4, (unsigned short)k4},
-                           (v2u){(unsigned short)k5, (unsigned short)k5},
-                           (v2u){(unsigned short)k6, (unsigned short)k6}};
-#define BG(off) __builtin_bit_cast(v2u, gather2<off>(w0, w1, w2))
-        for (int u = tid; u < BLUR_IH * (BLUR_TW / 4); u += 256) {
-            const int r = u >> 5, j = u & 31;
-            const uint32_t *w = (const uint32_t *)&in[r][4 * j];
-            const uint32_t w0 = w[0], w1 = w[1], w2 = w[2];
-            // outputs (4j, 4j+1): bytes (1+t, 2+t); outputs (4j+2, 4j+3): bytes (3+t, 4+t)
-            v2u a = kv[0] * BG(1), b = kv[0] * BG(3);
-            a += kv[1] * BG(2);
-            b += kv[1] * BG(4);
-            a += kv[2] * BG(3);
-            b += kv[2] * BG(5);
-            a += kv[3] * BG(4);
-            b += kv[3] * BG(6);
-            a += kv[4] * BG(5);
-            b += kv[4] * BG(7);
-            a += kv[5] * BG(6);
-            b += kv[5] * BG(8);
-            a += kv[6] * BG(7);
-            b += kv[6] * BG(9);
-            uint2 pk;
-            pk.x = __builtin_bit_cast(uint32_t, a);
-            pk.y = __builtin_bit_cast(uint32_t, b);
-            *(uint2 *)&rows[r][4 * j] = pk;
+        const uint32_t K00 = k0 << 8 | k1 << 16 | k2 << 24, K01 = k3 | k4 << 8 | k5 << 16 | k6 << 24;
+        const uint32_t K10 = k0 << 16 | k1 << 24, K11 = k2 | k3 << 8 | k4 << 16 | k5 << 24, K12 = k6;
+        const uint32_t K20 = k0 << 24, K21 = k1 | k2 << 8 | k3 << 16 | k4 << 24, K22 = k5 | k6 << 8;
+        const uint32_t K31 = k0 | k1 << 8 | k2 << 16 | k3 << 24, K32 = k4 | k5 << 8 | k6 << 16;
+        for (int u = tid; u < (BLUR_IH / 2) * (BLUR_TW / 4); u += 256) {
+            const int rp = u >> 5, j = u & 31;
+            uint32_t sm[2][4];
+#pragma unroll
+            for (int h = 0; h < 2; h++) {
+                const uint32_t *w = (const uint32_t *)&in[2 * rp + h][4 * j];
+                const uint32_t w0 = w[0], w1 = w[1], w2 = w[2];
+                sm[h][0] = __builtin_amdgcn_udot4(w1, K01, __builtin_amdgcn_udot4(w0, K00, 0u, false), false);
+                sm[h][1] = __builtin_amdgcn_udot4(w2, K12, __builtin_amdgcn_udot4(w1, K11, __builtin_amdgcn_udot4(w0, K10, 0u, false), false), false);
+                sm[h][2] = __builtin_amdgcn_udot4(w2, K22, __builtin_amdgcn_udot4(w1, K21, __builtin_amdgcn_udot4(w0, K20, 0u, false), false), false);
+                sm[h][3] = __builtin_amdgcn_udot4(w2, K32, __builtin_amdgcn_udot4(w1, K31, 0u, false), false);
+            }
+            uint4 pk;
+            pk.x = sm[0][0] | sm[1][0] << 16;
+            pk.y = sm[0][1] | sm[1][1] << 16;
+            pk.z = sm[0][2] | sm[1][2] << 16;
+            pk.w = sm[0][3] | sm[1][3] << 16;
+            *(uint4 *)&rows[rp][4 * j] = pk;
         }
-#undef BG
     }
     __syncthreads();
-    // column pass: thread = (4-column group j, 4-row group rg)
-    const int j = tid & 31, rg = tid >> 5;  // rg in [0, 8): rows 4rg .. 4rg+3
+    // column pass: thread = (4-column group j, 4-row group rg), outputs o = 4rg .. 4rg+3 from
+    // tile rows o .. o+6, i.e. row pairs 2rg .. 2rg+4; four v_dot2_u32_u16 per output with
+    // the weights aligned to the output's parity (even o: (k0,k1)(k2,k3)(k4,k5)(k6,0);
+    // odd o: (0,k0)(k1,k2)(k3,k4)(k5,k6)).  Sums <= 257 * 65535 fit in 32 bits.
+    const int j = tid & 31, rg = tid >> 5;  // rg in [0, 8)
     uint32_t acc[4][4];
+    {
+        const uint32_t E0 = k0 | k1 << 16, E1 = k2 | k3 << 16, E2 = k4 | k5 << 16, E3 = k6;
+        const uint32_t O0 = k0 << 16, O1 = k1 | k2 << 16, O2 = k3 | k4 << 16, O3 = k5 | k6 << 16;
+        uint4 P[5];
 #pragma unroll
-    for (int o = 0; o < 4; o++)
+        for (int q = 0; q < 5; q++) P[q] = *(const uint4 *)&rows[2 * rg + q][4 * j];
 #pragma unroll
-        for (int b = 0; b < 4; b++) acc[o][b] = 0;
-    const int kk[7] = {k0, k1, k2, k3, k4, k5, k6};
+        for (int b = 0; b < 4; b++) {
+            auto col = [&](int q) -> uint32_t {
+                return b == 0 ? P[q].x : b == 1 ? P[q].y : b == 2 ? P[q].z : P[q].w;
+            };
 #pragma unroll
-    for (int rr = 0; rr < 10; rr++) {
-        const uint2 pk = *(const uint2 *)&rows[4 * rg + rr][4 * j];
-        const uint32_t v[4] = {pk.x & 0xFFFF, pk.x >> 16, pk.y & 0xFFFF, pk.y >> 16};
-#pragma unroll
-        for (int o = 0; o < 4; o++) {
-            const int tap = rr - o;
-            if (tap >= 0 && tap < 7) {
-#pragma unroll
-                for (int b = 0; b < 4; b++)  // 16-bit sum x weight <= 257: 24-bit multiply
-                    acc[o][b] = __umul24((uint32_t)kk[tap], v[b]) + acc[o][b];
+            for (int o = 0; o < 4; o++) {
+                const int m = o >> 1;  // first pair of output 4rg+o: 2rg + m
+                uint32_t a2;
+                if ((o & 1) == 0) {
+                    a2 = udot2_u32(col(m), E0, 0u);
+                    a2 = udot2_u32(col(m + 1), E1, a2);
+                    a2 = udot2_u32(col(m + 2), E2, a2);
+                    a2 = udot2_u32(col(m + 3), E3, a2);
+                } else {
+                    a2 = udot2_u32(col(m), O0, 0u);
+                    a2 = udot2_u32(col(m + 1), O1, a2);
+                    a2 = udot2_u32(col(m + 2), O2, a2);
+                    a2 = udot2_u32(col(m + 3), O3, a2);
+                }
+                acc[o][b] = a2;
             }
         }
     }
