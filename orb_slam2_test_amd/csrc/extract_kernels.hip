@@ -21,14 +21,6 @@
 
 namespace orbg {
 
-__device__ __attribute__((aligned(16))) int8_t pattern_i8[1024] = {
-#define ORBG_PAIR(a, b, c, d) a, b, c, d,
-#include "orb_pattern.inc"
-#undef ORBG_PAIR
-};
-
-__device__ __forceinline__ int cv_round(float v) { return __float2int_rn(v); }
-
 // ---------------------------------------------------------------------------
 // block-wide helpers (blockDim.x == 256)
 // ---------------------------------------------------------------------------
@@ -1298,290 +1290,6 @@ __global__ __launch_bounds__(ORBG_OCT_THREADS) void k_octree(
     if (tid == 0) {
         lvl_cnt[(int64_t)f * g->L + l] = nout;
         if (alive > lv.out_cap) atomicOr(err_flag, 1 << 8);
-    }
-}
-
-// ---------------------------------------------------------------------------
-// pinned sincos (double Cody-Waite + Taylor, identical to oracle/orb_oracle.c)
-// ---------------------------------------------------------------------------
-
-// cv::fastAtan2 (OpenCV 3.4 atan_f32), degrees in [0, 360]
-__device__ float fast_atan2(float y, float x)
-{
-    const float r2d = (float)(180 / 3.14159265358979323846);
-    const float p1 = 0.9997878412794807f * r2d;
-    const float p3 = -0.3258083974640975f * r2d;
-    const float p5 = 0.1555786518463281f * r2d;
-    const float p7 = -0.04432655554792128f * r2d;
-    const float eps = (float)2.2204460492503131e-16;
-    const float ax = fabsf(x), ay = fabsf(y);
-    float a, c, c2;
-    if (ax >= ay) {
-        c = ay / (ax + eps);
-        c2 = c * c;
-        a = (((p7 * c2 + p5) * c2 + p3) * c2 + p1) * c;
-    } else {
-        c = ax / (ay + eps);
-        c2 = c * c;
-        a = 90.f - (((p7 * c2 + p5) * c2 + p3) * c2 + p1) * c;
-    }
-    if (x < 0) a = 180.f - a;
-    if (y < 0) a = 360.f - a;
-    return a;
-}
-
-// ---------------------------------------------------------------------------
-// k_orient_desc: each wave walks OD_KPW consecutive quadtree output slots of one frame
-// (frame, level, list position); the keypoint of a filled slot is written at
-// i = (keypoints of lower levels) + position, the level-major order of ORBextractor.cc:1381.
-// The wave's slot keys come in one load; the 31x31 unblurred patch (IC_Angle) and the 37x37
-// blurred neighbourhood (every rotated rBRIEF sample lies within +-18 px) of slot j+1 are in
-// flight while slot j is computed.  IC_Angle's circle-masked moments are v_dot4_u32_u8
-// products of the patch words with per-(alignment, lane) byte tables staged in LDS:
-// weights u+15 (0 outside the circle) and ones (0 outside), so per 16 patch bytes
-// m_10 += dot(w) - 15 dot(1) and m_01 += v dot(1).  The 512 samples are read from LDS.
-// ---------------------------------------------------------------------------
-struct OrbgKeypointDev {
-    float x, y, size, angle, response;
-    int32_t octave, class_id;
-};
-
-#define OD_R 18                 // rBRIEF sample radius bound: 13 * sqrt(2) rounded
-#define OD_SPAN (2 * OD_R + 1)  // 37 rows
-#define OD_ROWB 48              // staged row: 3 x 16 bytes (37 bytes + up to 3 of alignment)
-#define OD_KPW ORBG_OD_KPW      // slots per wave
-#ifndef ORBG_OD_PREFETCH
-#define ORBG_OD_PREFETCH 0
-#endif
-#ifndef ORBG_OD_LDSTAB
-#define ORBG_OD_LDSTAB 1
-#endif
-#ifndef ORBG_OD_WPE
-#define ORBG_OD_WPE 8  // min waves per SIMD (VGPR budget)
-#endif
-#define OD_TABW ORBG_OD_TABW    // IC_Angle lanes: 31 patch rows x 3 16-byte chunks
-
-// IC_Angle byte tables (host-built, orbg_api.hip make_od_tab): entry (sh, w) for the patch
-// row r = w / 3, chunk c = w % 3 loaded from the 4-byte-aligned address sh bytes before the
-// row start: byte b is column u = 16c + b - sh - 15, weight u + 15 and one when
-// |u| <= umax[|r - 15|], else 0.  [sh][w][0] = weights, [sh][w][1] = ones.
-struct OdPatch {
-    uint4 wd[2], bv[2];
-    int sh[2], bsh;
-};
-
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(ORBG_OD_WPE, 8))) void k_orient_desc(
-    const OrbgGeom *__restrict__ g, const uint8_t *__restrict__ img0, int64_t img_fs,
-    int img_pitch, const uint8_t *__restrict__ pyr, const uint8_t *__restrict__ blur,
-    const uint4 *__restrict__ odtab, const uint32_t *__restrict__ lvl_kp,
-    const int32_t *__restrict__ lvl_cnt, OrbgKeypointDev *__restrict__ kps,
-    uint8_t *__restrict__ desc, int32_t *__restrict__ counts)
-{
-    __shared__ uint4 bpatch[4][OD_SPAN * OD_ROWB / 16];
-    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-#if ORBG_OD_LDSTAB
-    __shared__ uint4 tab[4 * OD_TABW * 2];
-    for (int i = threadIdx.x; i < 4 * OD_TABW * 2; i += 256) tab[i] = odtab[i];
-    __syncthreads();
-#else
-    const uint4 *tab = odtab;  // 11.9 KB, L1/L2-resident
-#endif
-    const int nb = (g->out_frame + 4 * OD_KPW - 1) / (4 * OD_KPW);  // blocks per frame
-    const int id = xcd_remap(blockIdx.x, gridDim.x);
-    const int f = id / nb, bx = id - f * nb;
-    const int s0 = __builtin_amdgcn_readfirstlane((bx * 4 + wv) * OD_KPW);  // wave-uniform
-    const int L = g->L, OF = g->out_frame;
-    if (s0 >= OF) return;
-    const uint32_t kl = (lane < OD_KPW && s0 + lane < OF) ? lvl_kp[(int64_t)f * OF + s0 + lane] : 0u;
-    const int32_t *lc = lvl_cnt + (int64_t)f * L;
-    if (s0 == 0 && lane == 0) {
-        int total = 0;
-        for (int l = 0; l < L; l++) total += lc[l];
-        counts[f] = total;
-    }
-    const int4 pat = ((const int4 *)pattern_i8)[lane];
-    // slot -> (level, keypoint index, x, y); false for an empty slot (wave-uniform)
-    auto locate = [&](int j, int &level, int &i, int &x, int &y, uint32_t &key) -> bool {
-        const int slot = s0 + j;
-        if (slot >= OF) return false;
-        level = 0;
-        while (level + 1 < L && slot >= g->lv[level + 1].out_off) level++;
-        int before = 0;
-        for (int l = 0; l < level; l++) before += lc[l];
-        const int pos = slot - g->lv[level].out_off;
-        if (pos >= lc[level]) return false;
-        i = before + pos;
-        key = (uint32_t)__builtin_amdgcn_readlane((int)kl, j);
-        x = orbg_px(key) + ORBG_MIN_BORDER;
-        y = orbg_py(key) + ORBG_MIN_BORDER;
-        return true;
-    };
-    // every load of one slot, 16 bytes per lane: the unblurred 31-row patch and the blurred
-    // 37-row neighbourhood as 48-byte row chunks from the 4-byte-aligned row start (3 x
-    // dwordx4 per row; the level-0 pitch may be odd, so alignment is per row)
-    auto issue = [&](int level, int x, int y, OdPatch &P) {
-        const OrbgLevel &lv = g->lv[level];
-        const uint8_t *im;
-        int pitch;
-        if (level == 0) {
-            im = img0 + f * img_fs;
-            pitch = img_pitch;
-        } else {
-            im = pyr + f * g->pyr_frame + lv.pyr_off;
-            pitch = lv.pitch;
-        }
-        const uint8_t *ctr = im + (int64_t)y * pitch + x;
-#pragma unroll
-        for (int k = 0; k < 2; k++) {
-            const int w = lane + 64 * k;  // row v = w / 3 - 15, chunk c = w % 3
-            P.wd[k] = make_uint4(0, 0, 0, 0);
-            P.sh[k] = 0;
-            if (w < OD_TABW) {
-                const int r = w / 3, cw = w - r * 3;
-                const uintptr_t a = (uintptr_t)(ctr + (int64_t)(r - ORBG_HALF_PATCH) * pitch -
-                                                ORBG_HALF_PATCH);
-                P.wd[k] = *(const uint4 *)((a & ~(uintptr_t)3) + 16 * cw);
-                P.sh[k] = (int)(a & 3);
-            }
-        }
-        const int bpitch = lv.pitch;
-        const uint8_t *bl0 = blur + f * g->blur_frame + lv.blur_off +
-                             (int64_t)(y - OD_R) * bpitch + (x - OD_R);
-        P.bsh = (int)((uintptr_t)bl0 & 3);
-        const uint8_t *bw = bl0 - P.bsh;
-#pragma unroll
-        for (int k = 0; k < 2; k++) {
-            const int w = lane + 64 * k;
-            P.bv[k] = make_uint4(0, 0, 0, 0);
-            if (w < OD_SPAN * 3) {
-                const int r = w / 3, cw = w - r * 3;
-                P.bv[k] = *(const uint4 *)(bw + (int64_t)r * bpitch + 16 * cw);
-            }
-        }
-    };
-    uint8_t *bp = (uint8_t *)bpatch[wv];
-    const float factorPI = (float)(3.14159265358979323846 / 180.f);
-#if ORBG_OD_PREFETCH
-    // slot j+1's loads are issued before slot j is computed (two register sets)
-    OdPatch cur, nxt;
-    int lev_c = 0, i_c = 0, x_c = 0, y_c = 0;
-    uint32_t key_c = 0;
-    bool v_c = locate(0, lev_c, i_c, x_c, y_c, key_c);
-    if (v_c) issue(lev_c, x_c, y_c, cur);
-#pragma unroll 1
-    for (int j = 0; j < OD_KPW; j++) {
-        int lev_n = 0, i_n = 0, x_n = 0, y_n = 0;
-        uint32_t key_n = 0;
-        const bool v_n = j + 1 < OD_KPW && locate(j + 1, lev_n, i_n, x_n, y_n, key_n);
-        if (v_n) issue(lev_n, x_n, y_n, nxt);
-        if (v_c) {
-#else
-#pragma unroll 1
-    for (int j = 0; j < OD_KPW; j++) {
-        OdPatch cur;
-        int lev_c = 0, i_c = 0, x_c = 0, y_c = 0;
-        uint32_t key_c = 0;
-        if (locate(j, lev_c, i_c, x_c, y_c, key_c)) {
-            issue(lev_c, x_c, y_c, cur);
-#endif
-            // ---- IC_Angle (ORBextractor.cc:83-111) ----
-            int m01 = 0, m10 = 0;
-#pragma unroll
-            for (int k = 0; k < 2; k++) {
-                const int w = lane + 64 * k;
-                if (w < OD_TABW) {
-                    const int v = w / 3 - ORBG_HALF_PATCH;
-                    const uint4 tw = tab[(cur.sh[k] * OD_TABW + w) * 2];
-                    const uint4 to = tab[(cur.sh[k] * OD_TABW + w) * 2 + 1];
-                    uint32_t su = 0, sv = 0;
-                    su = __builtin_amdgcn_udot4(cur.wd[k].x, tw.x, su, false);
-                    su = __builtin_amdgcn_udot4(cur.wd[k].y, tw.y, su, false);
-                    su = __builtin_amdgcn_udot4(cur.wd[k].z, tw.z, su, false);
-                    su = __builtin_amdgcn_udot4(cur.wd[k].w, tw.w, su, false);
-                    sv = __builtin_amdgcn_udot4(cur.wd[k].x, to.x, sv, false);
-                    sv = __builtin_amdgcn_udot4(cur.wd[k].y, to.y, sv, false);
-                    sv = __builtin_amdgcn_udot4(cur.wd[k].z, to.z, sv, false);
-                    sv = __builtin_amdgcn_udot4(cur.wd[k].w, to.w, sv, false);
-                    m10 += (int)su - ORBG_HALF_PATCH * (int)sv;
-                    m01 += v * (int)sv;
-                }
-            }
-            wave_sync_lds();  // the previous slot's rBRIEF reads are done
-#pragma unroll
-            for (int k = 0; k < 2; k++) {
-                const int w = lane + 64 * k;
-                if (w < OD_SPAN * 3) {
-                    const int r = w / 3, cw = w - r * 3;
-                    *(uint4 *)(bp + r * OD_ROWB + 16 * cw) = cur.bv[k];
-                }
-            }
-            wave_sync_lds();
-            m01 = wave_sum(m01);
-            m10 = wave_sum(m10);
-            const float angle = fast_atan2((float)m01, (float)m10);
-
-            // ---- rBRIEF (ORBextractor.cc:117-157) from the staged blurred neighbourhood:
-            // lane owns tests 4*lane .. 4*lane+3 ----
-            double sd, cd;
-            pinned_sincos((double)(angle * factorPI), &sd, &cd);
-            const float a = (float)cd, b = (float)sd;
-            const uint8_t *bl = bp + OD_R * OD_ROWB + cur.bsh + OD_R;  // centre
-            // opaque per slot: keeps the pattern decode inside the loop (hoisted, it holds
-            // 16 more VGPRs across the whole slot)
-            int4 pt = pat;
-            asm volatile("" : "+v"(pt.x), "+v"(pt.y), "+v"(pt.z), "+v"(pt.w));
-            int nib = 0;
-#pragma unroll
-            for (int t = 0; t < 4; t++) {
-                int val[2];
-#pragma unroll
-                for (int s = 0; s < 2; s++) {
-                    const int pw = t == 0 ? pt.x : t == 1 ? pt.y : t == 2 ? pt.z : pt.w;
-                    const float px = (float)(int8_t)(pw >> (16 * s));
-                    const float py = (float)(int8_t)(pw >> (16 * s + 8));
-                    float ry, rx;
-                    if (g->brief_fma) {
-                        ry = fmaf(px, b, py * a);
-                        rx = fmaf(px, a, -(py * b));
-                    } else {
-                        const float t0 = px * b, t1 = py * a, t2 = px * a, t3 = py * b;
-                        ry = t0 + t1;
-                        rx = t2 - t3;
-                    }
-                    val[s] = bl[cv_round(ry) * OD_ROWB + cv_round(rx)];
-                }
-                nib |= (val[0] < val[1]) << t;
-            }
-            const int hi = __shfl_down(nib, 1, 64);
-            const int64_t o = (int64_t)f * g->frame_cap + i_c;
-            if ((lane & 1) == 0) desc[o * 32 + (lane >> 1)] = (uint8_t)(nib | (hi << 4));
-            if (lane == 0) {
-                const OrbgLevel &lv = g->lv[lev_c];
-                OrbgKeypointDev kp;
-                float fx = (float)x_c, fy = (float)y_c;
-                if (lev_c != 0) {
-                    fx *= lv.scale;
-                    fy *= lv.scale;
-                }
-                kp.x = fx;
-                kp.y = fy;
-                kp.size = (float)lv.patch_size;
-                kp.angle = angle;
-                kp.response = (float)orbg_ps(key_c);
-                kp.octave = lev_c;
-                kp.class_id = -1;
-                kps[o] = kp;
-            }
-        }
-#if ORBG_OD_PREFETCH
-        cur = nxt;
-        v_c = v_n;
-        lev_c = lev_n;
-        i_c = i_n;
-        x_c = x_n;
-        y_c = y_n;
-        key_c = key_n;
-#endif
     }
 }
 

@@ -35,11 +35,18 @@ __device__ __forceinline__ int wave_incl_scan_small(int x, int *total)
     return incl;
 }
 
+// wave64 sum, uniform result: every lane gets its 16-lane row's sum by DPP quad_perm /
+// row_ror adds, row_bcast:15 / row_bcast:31 fold the four rows into lane 63 (gfx9 DPP: no
+// LDS round trips, unlike __shfl_xor's ds_bpermute).  Integer adds, exact in any order.
 __device__ __forceinline__ int wave_sum(int x)
 {
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) x += __shfl_xor(x, o, 64);
-    return x;
+    x += __builtin_amdgcn_update_dpp(0, x, 0xb1, 0xf, 0xf, false);   // quad_perm [1,0,3,2]
+    x += __builtin_amdgcn_update_dpp(0, x, 0x4e, 0xf, 0xf, false);   // quad_perm [2,3,0,1]
+    x += __builtin_amdgcn_update_dpp(0, x, 0x124, 0xf, 0xf, false);  // row_ror:4
+    x += __builtin_amdgcn_update_dpp(0, x, 0x128, 0xf, 0xf, false);  // row_ror:8
+    x += __builtin_amdgcn_update_dpp(0, x, 0x142, 0xf, 0xf, false);  // row_bcast:15 (row r += r-1)
+    x += __builtin_amdgcn_update_dpp(0, x, 0x143, 0xf, 0xf, false);  // row_bcast:31 (rows 2, 3)
+    return __builtin_amdgcn_readlane(x, 63);
 }
 
 // LDS written by some lanes of a wave, then read by others: keep the compiler from

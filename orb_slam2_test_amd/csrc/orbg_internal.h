@@ -27,7 +27,7 @@
 #define ORBG_GRID_ROWS 48        // Frame.h:37
 #define ORBG_MATCH_TOPK 8
 #ifndef ORBG_OD_KPW
-#define ORBG_OD_KPW 2            // k_orient_desc: quadtree output slots per wave
+#define ORBG_OD_KPW 8            // k_orient_desc: quadtree output slots per wave
 #endif
 #define ORBG_OD_TABW 93          // k_orient_desc: IC_Angle lanes (31 rows x 3 chunks)
 #define OCT_KEY_CAP 16384        // k_octree_lds handles levels with <= this many candidates

@@ -1,0 +1,299 @@
+// orient_kernels.hip -- IC_Angle (ORBextractor.cc:83-111, computeOrientation :523-530),
+// computeOrbDescriptor (:117-157) and the output assembly of ORBextractor::operator()
+// (:1381-1395) as one batched HIP kernel for gfx950.
+// Bit-exactness pins: no FMA contraction (-ffp-contract=off + pragma),
+// cvRound = round-half-even, fastAtan2 polynomial, pinned double sincos.
+#include <hip/hip_runtime.h>
+
+#include "orbg_internal.h"
+#include "orbg_device.h"
+
+#pragma clang fp contract(off)
+
+namespace orbg {
+
+// bit_pattern_31_ (ORBextractor.cc:160-418): test t = bytes 4t .. 4t+3 = (x0, y0, x1, y1)
+__device__ __attribute__((aligned(16))) int8_t od_pattern_i8[1024] = {
+#define ORBG_PAIR(a, b, c, d) a, b, c, d,
+#include "orb_pattern.inc"
+#undef ORBG_PAIR
+};
+
+__device__ __forceinline__ int cv_round(float v) { return __float2int_rn(v); }
+
+// cv::fastAtan2 (OpenCV 3.4 atan_f32), degrees in [0, 360]
+__device__ __forceinline__ float fast_atan2(float y, float x)
+{
+    const float r2d = (float)(180 / 3.14159265358979323846);
+    const float p1 = 0.9997878412794807f * r2d;
+    const float p3 = -0.3258083974640975f * r2d;
+    const float p5 = 0.1555786518463281f * r2d;
+    const float p7 = -0.04432655554792128f * r2d;
+    const float eps = (float)2.2204460492503131e-16;
+    const float ax = fabsf(x), ay = fabsf(y);
+    float a, c, c2;
+    if (ax >= ay) {
+        c = ay / (ax + eps);
+        c2 = c * c;
+        a = (((p7 * c2 + p5) * c2 + p3) * c2 + p1) * c;
+    } else {
+        c = ax / (ay + eps);
+        c2 = c * c;
+        a = 90.f - (((p7 * c2 + p5) * c2 + p3) * c2 + p1) * c;
+    }
+    if (x < 0) a = 180.f - a;
+    if (y < 0) a = 360.f - a;
+    return a;
+}
+
+// ---------------------------------------------------------------------------
+// k_orient_desc: each wave owns OD_KPW consecutive quadtree output slots of one frame
+// (frame, level, list position); the keypoint of a filled slot is written at
+// i = (keypoints of lower levels) + position, the level-major order of ORBextractor.cc:1381.
+// Lane j < OD_KPW locates slot j once; the wave then runs three phases, so the wave-uniform
+// scalar math (fastAtan2, the double sincos, the keypoint record) runs once per wave with
+// one slot per lane instead of once per slot on all 64 lanes:
+//   A  per slot: the 31x31 unblurred patch as 93 aligned 16-byte row chunks; circle-masked
+//      moments are v_dot4_u32_u8 products with per-(alignment, lane) byte tables staged in
+//      LDS (weights u+15 and ones, 0 outside the circle), so per 16 patch bytes
+//      m_10 += dot(w) - 15 dot(1) and m_01 += v dot(1); DPP wave sums; lane j keeps slot j's;
+//   B  all lanes at once: angle, cos, sin; lanes j write their keypoint records;
+//   C  per slot: the 37x37 blurred neighbourhood (every rotated rBRIEF sample lies within
+//      +-18 px) staged in LDS; lane L runs tests L, L+64, L+128, L+192, so ballot t is
+//      descriptor bits 64t .. 64t+63 and lanes 0..7 store the 32 bytes as dwords.
+// ---------------------------------------------------------------------------
+struct OrbgKeypointDev {
+    float x, y, size, angle, response;
+    int32_t octave, class_id;
+};
+
+#define OD_R 18                 // rBRIEF sample radius bound: 13 * sqrt(2) rounded
+#define OD_SPAN (2 * OD_R + 1)  // 37 rows
+#define OD_ROWB 48              // staged row: 3 x 16 bytes (37 bytes + up to 3 of alignment)
+#define OD_KPW ORBG_OD_KPW      // slots per wave
+#ifndef ORBG_OD_LDSTAB
+#define ORBG_OD_LDSTAB 1
+#endif
+#ifndef ORBG_OD_WPE
+#define ORBG_OD_WPE 8  // min waves per SIMD (VGPR budget)
+#endif
+#define OD_TABW ORBG_OD_TABW    // IC_Angle lanes: 31 patch rows x 3 16-byte chunks
+static_assert(OD_KPW >= 1 && OD_KPW <= 32, "one slot per lane, okmask is 32 bits");
+
+// IC_Angle byte tables (host-built, orbg_api.hip make_od_tab): entry (sh, w) for the patch
+// row r = w / 3, chunk c = w % 3 loaded from the 4-byte-aligned address sh bytes before the
+// row start: byte b is column u = 16c + b - sh - 15, weight u + 15 and one when
+// |u| <= umax[|r - 15|], else 0.  [sh][w][0] = weights, [sh][w][1] = ones.
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(ORBG_OD_WPE, 8))) void k_orient_desc(
+    const OrbgGeom *__restrict__ g, const uint8_t *__restrict__ img0, int64_t img_fs,
+    int img_pitch, const uint8_t *__restrict__ pyr, const uint8_t *__restrict__ blur,
+    const uint4 *__restrict__ odtab, const uint32_t *__restrict__ lvl_kp,
+    const int32_t *__restrict__ lvl_cnt, OrbgKeypointDev *__restrict__ kps,
+    uint8_t *__restrict__ desc, int32_t *__restrict__ counts)
+{
+    __shared__ uint4 bpatch[4][OD_SPAN * OD_ROWB / 16];
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+#if ORBG_OD_LDSTAB
+    __shared__ uint4 tab[4 * OD_TABW * 2];
+    for (int i = threadIdx.x; i < 4 * OD_TABW * 2; i += 256) tab[i] = odtab[i];
+    __syncthreads();
+#else
+    const uint4 *tab = odtab;  // 11.9 KB, L1/L2-resident
+#endif
+    const int nb = (g->out_frame + 4 * OD_KPW - 1) / (4 * OD_KPW);  // blocks per frame
+    const int id = xcd_remap(blockIdx.x, gridDim.x);
+    const int f = id / nb, bx = id - f * nb;
+    const int s0 = __builtin_amdgcn_readfirstlane((bx * 4 + wv) * OD_KPW);  // wave-uniform
+    const int L = g->L, OF = g->out_frame;
+    if (s0 >= OF) return;
+    const int32_t *lc = lvl_cnt + (int64_t)f * L;
+    if (s0 == 0 && lane == 0) {
+        int total = 0;
+        for (int l = 0; l < L; l++) total += lc[l];
+        counts[f] = total;
+    }
+    // lane j < OD_KPW: slot s0 + j -> quadtree key, level, output row; okmask bit j
+    // (wave-uniform) = the slot holds a keypoint
+    uint32_t kl = 0u;
+    int my_lev = 0, my_i = 0, my_ok = 0;
+    {
+        const int slot = s0 + lane;
+        if (lane < OD_KPW && slot < OF) {
+            int level = 0;
+            while (level + 1 < L && slot >= g->lv[level + 1].out_off) level++;
+            int before = 0;
+            for (int l = 0; l < level; l++) before += lc[l];
+            const int pos = slot - g->lv[level].out_off;
+            if (pos < lc[level]) {
+                kl = lvl_kp[(int64_t)f * OF + slot];
+                my_ok = 1;
+                my_lev = level;
+                my_i = before + pos;
+            }
+        }
+    }
+    const uint32_t okmask = (uint32_t)__ballot(my_ok);
+    // lane-constant (row, 16-byte chunk) of the patch / neighbourhood words this lane loads
+    int pr[2], pc[2];
+#pragma unroll
+    for (int k = 0; k < 2; k++) {
+        const int w = lane + 64 * k;
+        pr[k] = w / 3;
+        pc[k] = w - pr[k] * 3;
+    }
+
+    // ---- A: IC_Angle moments (ORBextractor.cc:83-111), slot j's sums kept by lane j ----
+    int M01 = 0, M10 = 0;
+#pragma unroll 1
+    for (int j = 0; j < OD_KPW; j++) {
+        if (!((okmask >> j) & 1u)) continue;  // wave-uniform
+        const int lev = __builtin_amdgcn_readlane(my_lev, j);
+        const uint32_t key = (uint32_t)__builtin_amdgcn_readlane((int)kl, j);
+        const int x = orbg_px(key) + ORBG_MIN_BORDER, y = orbg_py(key) + ORBG_MIN_BORDER;
+        const uint8_t *im;
+        int pitch;
+        if (lev == 0) {
+            im = img0 + f * img_fs;
+            pitch = img_pitch;
+        } else {
+            im = pyr + f * g->pyr_frame + g->lv[lev].pyr_off;
+            pitch = g->lv[lev].pitch;
+        }
+        const uint8_t *ctr = im + (int64_t)y * pitch + x;
+        // 16 bytes per lane from each row's 4-byte-aligned start (the level-0 pitch may be
+        // odd, so the alignment is per row)
+        uint4 wd[2];
+        int sh[2];
+#pragma unroll
+        for (int k = 0; k < 2; k++) {
+            wd[k] = make_uint4(0, 0, 0, 0);
+            sh[k] = 0;
+            if (lane + 64 * k < OD_TABW) {
+                const uintptr_t a = (uintptr_t)(ctr + (int64_t)(pr[k] - ORBG_HALF_PATCH) * pitch -
+                                                ORBG_HALF_PATCH);
+                wd[k] = *(const uint4 *)((a & ~(uintptr_t)3) + 16 * pc[k]);
+                sh[k] = (int)(a & 3);
+            }
+        }
+        int m01 = 0, m10 = 0;
+#pragma unroll
+        for (int k = 0; k < 2; k++) {
+            const int w = lane + 64 * k;
+            if (w < OD_TABW) {
+                const int v = pr[k] - ORBG_HALF_PATCH;
+                const uint4 tw = tab[(sh[k] * OD_TABW + w) * 2];
+                const uint4 to = tab[(sh[k] * OD_TABW + w) * 2 + 1];
+                uint32_t su = 0, sv = 0;
+                su = __builtin_amdgcn_udot4(wd[k].x, tw.x, su, false);
+                su = __builtin_amdgcn_udot4(wd[k].y, tw.y, su, false);
+                su = __builtin_amdgcn_udot4(wd[k].z, tw.z, su, false);
+                su = __builtin_amdgcn_udot4(wd[k].w, tw.w, su, false);
+                sv = __builtin_amdgcn_udot4(wd[k].x, to.x, sv, false);
+                sv = __builtin_amdgcn_udot4(wd[k].y, to.y, sv, false);
+                sv = __builtin_amdgcn_udot4(wd[k].z, to.z, sv, false);
+                sv = __builtin_amdgcn_udot4(wd[k].w, to.w, sv, false);
+                m10 += (int)su - ORBG_HALF_PATCH * (int)sv;
+                m01 += v * (int)sv;
+            }
+        }
+        m01 = wave_sum(m01);
+        m10 = wave_sum(m10);
+        if (lane == j) {
+            M01 = m01;
+            M10 = m10;
+        }
+    }
+
+    // ---- B: angle = fastAtan2(m_01, m_10) (:110), cos / sin of it (:121-122), and the
+    // keypoint record (:1115-1122, :1387-1393), lane j for slot j ----
+    const float factorPI = (float)(3.14159265358979323846 / 180.f);
+    const float angle_l = fast_atan2((float)M01, (float)M10);
+    double sd, cd;
+    pinned_sincos((double)(angle_l * factorPI), &sd, &cd);
+    const float a_l = (float)cd, b_l = (float)sd;
+    if (my_ok) {
+        const OrbgLevel &lv = g->lv[my_lev];
+        OrbgKeypointDev kp;
+        float fx = (float)(orbg_px(kl) + ORBG_MIN_BORDER), fy = (float)(orbg_py(kl) + ORBG_MIN_BORDER);
+        if (my_lev != 0) {
+            fx *= lv.scale;
+            fy *= lv.scale;
+        }
+        kp.x = fx;
+        kp.y = fy;
+        kp.size = (float)lv.patch_size;
+        kp.angle = angle_l;
+        kp.response = (float)orbg_ps(kl);
+        kp.octave = my_lev;
+        kp.class_id = -1;
+        kps[(int64_t)f * g->frame_cap + my_i] = kp;
+    }
+
+    // ---- C: rBRIEF (ORBextractor.cc:117-157) on the blurred level ----
+    // lane L owns tests L + 64t (t = 0..3), one pattern word (x0, y0, x1, y1) each
+    int pat[4];
+#pragma unroll
+    for (int t = 0; t < 4; t++) pat[t] = ((const int *)od_pattern_i8)[lane + 64 * t];
+    const bool bfma = g->brief_fma != 0;
+    uint8_t *bp = (uint8_t *)bpatch[wv];
+#pragma unroll 1
+    for (int j = 0; j < OD_KPW; j++) {
+        if (!((okmask >> j) & 1u)) continue;  // wave-uniform
+        const int lev = __builtin_amdgcn_readlane(my_lev, j);
+        const uint32_t key = (uint32_t)__builtin_amdgcn_readlane((int)kl, j);
+        const int x = orbg_px(key) + ORBG_MIN_BORDER, y = orbg_py(key) + ORBG_MIN_BORDER;
+        const OrbgLevel &lv = g->lv[lev];
+        const int bpitch = lv.pitch;
+        const uint8_t *bl0 = blur + f * g->blur_frame + lv.blur_off +
+                             (int64_t)(y - OD_R) * bpitch + (x - OD_R);
+        const int bsh = (int)((uintptr_t)bl0 & 3);
+        const uint8_t *bw = bl0 - bsh;
+        uint4 bv[2];
+#pragma unroll
+        for (int k = 0; k < 2; k++) {
+            bv[k] = make_uint4(0, 0, 0, 0);
+            if (lane + 64 * k < OD_SPAN * 3)
+                bv[k] = *(const uint4 *)(bw + (int64_t)pr[k] * bpitch + 16 * pc[k]);
+        }
+        wave_sync_lds();  // the previous slot's sample reads are done
+#pragma unroll
+        for (int k = 0; k < 2; k++)
+            if (lane + 64 * k < OD_SPAN * 3) *(uint4 *)(bp + pr[k] * OD_ROWB + 16 * pc[k]) = bv[k];
+        wave_sync_lds();
+        const float a = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, a_l), j));
+        const float b = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, b_l), j));
+        const uint8_t *bl = bp + OD_R * OD_ROWB + bsh + OD_R;  // centre
+        // opaque per slot: keeps the offset decode inside the loop (hoisted, the 16 floats
+        // stay live through phase C and push the kernel past 64 VGPRs)
+        int pt[4] = {pat[0], pat[1], pat[2], pat[3]};
+        asm volatile("" : "+v"(pt[0]), "+v"(pt[1]), "+v"(pt[2]), "+v"(pt[3]));
+        uint32_t word = 0;
+#pragma unroll
+        for (int t = 0; t < 4; t++) {
+            int val[2];
+#pragma unroll
+            for (int s = 0; s < 2; s++) {
+                const float px = (float)(int8_t)(pt[t] >> (16 * s));
+                const float py = (float)(int8_t)(pt[t] >> (16 * s + 8));
+                float ry, rx;
+                if (bfma) {
+                    ry = fmaf(px, b, py * a);
+                    rx = fmaf(px, a, -(py * b));
+                } else {
+                    const float t0 = px * b, t1 = py * a, t2 = px * a, t3 = py * b;
+                    ry = t0 + t1;
+                    rx = t2 - t3;
+                }
+                val[s] = bl[cv_round(ry) * OD_ROWB + cv_round(rx)];
+            }
+            // bit L of ballot t = test 64t + L = descriptor bit 64t + L; dword d of the
+            // descriptor is half (d & 1) of ballot d >> 1
+            const unsigned long long m = __ballot(val[0] < val[1]);
+            if ((lane >> 1) == t) word = (uint32_t)(m >> (32 * (lane & 1)));
+        }
+        const int i = __builtin_amdgcn_readlane(my_i, j);
+        if (lane < 8) ((uint32_t *)(desc + ((int64_t)f * g->frame_cap + i) * 32))[lane] = word;
+    }
+}
+
+}  // namespace orbg
