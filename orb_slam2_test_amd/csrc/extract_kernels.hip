@@ -581,7 +581,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(6, 8))) voi
 // ---------------------------------------------------------------------------
 // k_blur: GaussianBlur(7x7, sigma 2, BORDER_REFLECT_101), bit-exact fixed point
 // out = sat((sum_v k_v * sum_h k_h * p + 2^15) >> 16).
-// 128x32 output tile per 256-thread workgroup.  The (128+8)x38 input tile (x origin at
+// A 256-thread workgroup walks BLUR_NB vertical 128x32 output bands; the loads of band b+1
+// are in flight while band b is computed.  The (128+8)x38 input tile (x origin at
 // tile_x0 - 4) is filled with aligned dword pairs + v_alignbyte (REFLECT_101 bytes at the
 // image edges), all loads issued before the LDS stores; the row pass keeps u16 sums
 // (<= 256*255) in LDS; the column pass reads 4 sums per ds_read_b64 and stores 4 output
@@ -591,6 +592,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(6, 8))) voi
 #define BLUR_TH 32
 #define BLUR_IW (BLUR_TW + 16)  // 9 x 16-byte chunks from x = tile_x0 - 4 (135 bytes read)
 #define BLUR_IH (BLUR_TH + 6)
+#define BLUR_NB ORBG_BLUR_NB  // bands per workgroup
 
 // v_dot2_u32_u16 on u16 pairs held in u32 words
 __device__ __forceinline__ uint32_t udot2_u32(uint32_t a, uint32_t b, uint32_t c)
@@ -625,7 +627,8 @@ __global__ __launch_bounds__(256) void k_blur(const OrbgGeom *__restrict__ g,
     const int W = lv.w, H = lv.h;
     const int ntx = (W + BLUR_TW - 1) / BLUR_TW;
     const int ty = t / ntx;
-    const int tx0 = (t - ty * ntx) * BLUR_TW, ty0 = ty * BLUR_TH;
+    const int tx0 = (t - ty * ntx) * BLUR_TW, yr0 = ty * (BLUR_TH * BLUR_NB);
+    const int nband = min(BLUR_NB, (H - yr0 + BLUR_TH - 1) / BLUR_TH);  // >= 1
     const uint8_t *src;
     int pitch;
     if (l == 0) {
@@ -635,17 +638,16 @@ __global__ __launch_bounds__(256) void k_blur(const OrbgGeom *__restrict__ g,
         src = pyr + f * g->pyr_frame + lv.pyr_off;
         pitch = lv.pitch;
     }
-    // fill: column c of the tile is image x = tx0 - 4 + c, row r is y = ty0 - 3 + r.
-    // Word j of a row = x0 .. x0+3 (x0 = tx0 - 4 + 4j): aligned dword pair + v_alignbyte
-    // when x0 .. x0+7 lies inside the row, else bytes with REFLECT_101.
-    // 16-byte chunk c of a row = x0 .. x0+15 (x0 = tx0 - 4 + 16c): one dwordx4 from the
-    // aligned address + one dword for the v_alignbyte shift when x0 .. x0+19 lies inside
-    // the row, else bytes with REFLECT_101 (image edges only).  All loads first.
+    // fill of the band starting at output row ty0: column c of the tile is image
+    // x = tx0 - 4 + c, row r is y = ty0 - 3 + r.  16-byte chunk c of a row = x0 .. x0+15
+    // (x0 = tx0 - 4 + 16c): one dwordx4 from the aligned address + one dword for the
+    // v_alignbyte shift when x0 .. x0+19 lies inside the row, else bytes with REFLECT_101
+    // (image edges only).  The loads of band b+1 are issued before band b is computed.
     constexpr int NCH = BLUR_IW / 16;                      // chunks per row
     constexpr int NFILL = (BLUR_IH * NCH + 255) / 256;     // chunks per thread
-    {
-        uint4 q[NFILL];
-        uint32_t q4[NFILL], sh[NFILL];
+    uint4 q[NFILL];
+    uint32_t q4[NFILL], sh[NFILL];
+    auto load_band = [&](int ty0) {
 #pragma unroll
         for (int k = 0; k < NFILL; k++) {
             const int i = tid + 256 * k;
@@ -663,49 +665,74 @@ __global__ __launch_bounds__(256) void k_blur(const OrbgGeom *__restrict__ g,
                     sh[k] = (uint32_t)(a & 3);
                     if (sh[k]) q4[k] = aw[4];
                 } else {
-                    uint32_t w4[4] = {0, 0, 0, 0};
-#pragma unroll
-                    for (int bb = 0; bb < 16; bb++)
-                        w4[bb >> 2] |= (uint32_t)row[reflect101(min(x0 + bb, W + 2), W)]
-                                       << (8 * (bb & 3));
-                    q[k] = make_uint4(w4[0], w4[1], w4[2], w4[3]);
+                    sh[k] = 4u;  // image-edge chunk: gathered byte-wise in store_band
                 }
             }
         }
+    };
+    auto store_band = [&](int ty0) {
 #pragma unroll
         for (int k = 0; k < NFILL; k++) {
             const int i = tid + 256 * k;
             if (i < BLUR_IH * NCH) {
                 const int r = i / NCH, c = i - r * NCH;
-                const uint32_t t = sh[k];
+                const uint32_t s = sh[k];
                 uint4 o;
-                o.x = __builtin_amdgcn_alignbyte(q[k].y, q[k].x, t);
-                o.y = __builtin_amdgcn_alignbyte(q[k].z, q[k].y, t);
-                o.z = __builtin_amdgcn_alignbyte(q[k].w, q[k].z, t);
-                o.w = __builtin_amdgcn_alignbyte(q4[k], q[k].w, t);
+                if (s < 4u) {
+                    o.x = __builtin_amdgcn_alignbyte(q[k].y, q[k].x, s);
+                    o.y = __builtin_amdgcn_alignbyte(q[k].z, q[k].y, s);
+                    o.z = __builtin_amdgcn_alignbyte(q[k].w, q[k].z, s);
+                    o.w = __builtin_amdgcn_alignbyte(q4[k], q[k].w, s);
+                } else {
+                    const int y = reflect101(min(ty0 - 3 + r, H + 2), H);
+                    const uint8_t *row = src + (int64_t)y * pitch;
+                    int x0 = tx0 - 4 + 16 * c;
+                    // opaque: keeps the 16 reflected column indices from being hoisted out
+                    // of the band loop (32 VGPRs held across it)
+                    asm volatile("" : "+v"(x0));
+                    uint32_t w4[4] = {0, 0, 0, 0};
+#pragma unroll
+                    for (int bb = 0; bb < 16; bb++)
+                        w4[bb >> 2] |= (uint32_t)row[reflect101(min(x0 + bb, W + 2), W)]
+                                       << (8 * (bb & 3));
+                    o = make_uint4(w4[0], w4[1], w4[2], w4[3]);
+                }
                 *(uint4 *)&in[r][16 * c] = o;
             }
         }
-    }
-    __syncthreads();
+    };
     const uint32_t k0 = g->gk[0], k1 = g->gk[1], k2 = g->gk[2], k3 = g->gk[3], k4 = g->gk[4],
                    k5 = g->gk[5], k6 = g->gk[6];
-    // row pass: unit = (row pair rp, 4-column group j).  Output x = 4j+i of a row needs tile
-    // bytes 4j+1+i .. 4j+7+i, i.e. the aligned dwords W0..W2 = bytes 4j .. 4j+11 against
-    // the 7 weights placed at byte 1+i: ten v_dot4_u32_u8 per 4 outputs (row sums <=
-    // 257 * 255, exact).  The two rows' sums of a column are stored as one u16 pair,
-    // rows[rp][x] = sum(2rp, x) | sum(2rp+1, x) << 16, for the column pass's v_dot2.
-    {
-        const uint32_t K00 = k0 << 8 | k1 << 16 | k2 << 24, K01 = k3 | k4 << 8 | k5 << 16 | k6 << 24;
-        const uint32_t K10 = k0 << 16 | k1 << 24, K11 = k2 | k3 << 8 | k4 << 16 | k5 << 24, K12 = k6;
-        const uint32_t K20 = k0 << 24, K21 = k1 | k2 << 8 | k3 << 16 | k4 << 24, K22 = k5 | k6 << 8;
-        const uint32_t K31 = k0 | k1 << 8 | k2 << 16 | k3 << 24, K32 = k4 | k5 << 8 | k6 << 16;
+    // row pass weights: output x = 4j+i of a row needs tile bytes 4j+1+i .. 4j+7+i, i.e. the
+    // aligned dwords W0..W2 = bytes 4j .. 4j+11 against the 7 weights placed at byte 1+i
+    const uint32_t K00 = k0 << 8 | k1 << 16 | k2 << 24, K01 = k3 | k4 << 8 | k5 << 16 | k6 << 24;
+    const uint32_t K10 = k0 << 16 | k1 << 24, K11 = k2 | k3 << 8 | k4 << 16 | k5 << 24, K12 = k6;
+    const uint32_t K20 = k0 << 24, K21 = k1 | k2 << 8 | k3 << 16 | k4 << 24, K22 = k5 | k6 << 8;
+    const uint32_t K31 = k0 | k1 << 8 | k2 << 16 | k3 << 24, K32 = k4 | k5 << 8 | k6 << 16;
+    // column pass weights aligned to the output's parity (even o: (k0,k1)(k2,k3)(k4,k5)(k6,0);
+    // odd o: (0,k0)(k1,k2)(k3,k4)(k5,k6))
+    const uint32_t E0 = k0 | k1 << 16, E1 = k2 | k3 << 16, E2 = k4 | k5 << 16, E3 = k6;
+    const uint32_t O0 = k0 << 16, O1 = k1 | k2 << 16, O2 = k3 | k4 << 16, O3 = k5 | k6 << 16;
+    uint8_t *dst = blur + f * g->blur_frame + lv.blur_off;
+    const int j = tid & 31, rg = tid >> 5;  // column pass: 4-column group j, 4-row group rg
+    const int gx = tx0 + 4 * j;
+    load_band(yr0);
+#pragma unroll 1
+    for (int b = 0; b < nband; b++) {  // workgroup-uniform trip count
+        const int ty0 = yr0 + b * BLUR_TH;
+        // every thread is past the previous band's row pass (barrier below), so in[] is free
+        store_band(ty0);
+        __syncthreads();  // in[] complete; every thread's previous column pass is done
+        if (b + 1 < nband) load_band(ty0 + BLUR_TH);
+        // row pass: unit = (row pair rp, 4-column group jj): ten v_dot4_u32_u8 per 4 outputs
+        // (row sums <= 257 * 255, exact); the two rows' sums of a column are stored as one
+        // u16 pair, rows[rp][x] = sum(2rp, x) | sum(2rp+1, x) << 16, for the column pass
         for (int u = tid; u < (BLUR_IH / 2) * (BLUR_TW / 4); u += 256) {
-            const int rp = u >> 5, j = u & 31;
+            const int rp = u >> 5, jj = u & 31;
             uint32_t sm[2][4];
 #pragma unroll
             for (int h = 0; h < 2; h++) {
-                const uint32_t *w = (const uint32_t *)&in[2 * rp + h][4 * j];
+                const uint32_t *w = (const uint32_t *)&in[2 * rp + h][4 * jj];
                 const uint32_t w0 = w[0], w1 = w[1], w2 = w[2];
                 sm[h][0] = __builtin_amdgcn_udot4(w1, K01, __builtin_amdgcn_udot4(w0, K00, 0u, false), false);
                 sm[h][1] = __builtin_amdgcn_udot4(w2, K12, __builtin_amdgcn_udot4(w1, K11, __builtin_amdgcn_udot4(w0, K10, 0u, false), false), false);
@@ -717,60 +744,53 @@ __global__ __launch_bounds__(256) void k_blur(const OrbgGeom *__restrict__ g,
             pk.y = sm[0][1] | sm[1][1] << 16;
             pk.z = sm[0][2] | sm[1][2] << 16;
             pk.w = sm[0][3] | sm[1][3] << 16;
-            *(uint4 *)&rows[rp][4 * j] = pk;
+            *(uint4 *)&rows[rp][4 * jj] = pk;
         }
-    }
-    __syncthreads();
-    // column pass: thread = (4-column group j, 4-row group rg), outputs o = 4rg .. 4rg+3 from
-    // tile rows o .. o+6, i.e. row pairs 2rg .. 2rg+4; four v_dot2_u32_u16 per output with
-    // the weights aligned to the output's parity (even o: (k0,k1)(k2,k3)(k4,k5)(k6,0);
-    // odd o: (0,k0)(k1,k2)(k3,k4)(k5,k6)).  Sums <= 257 * 65535 fit in 32 bits.
-    const int j = tid & 31, rg = tid >> 5;  // rg in [0, 8)
-    uint32_t acc[4][4];
-    {
-        const uint32_t E0 = k0 | k1 << 16, E1 = k2 | k3 << 16, E2 = k4 | k5 << 16, E3 = k6;
-        const uint32_t O0 = k0 << 16, O1 = k1 | k2 << 16, O2 = k3 | k4 << 16, O3 = k5 | k6 << 16;
-        uint4 P[5];
+        __syncthreads();
+        // column pass: outputs o = 4rg .. 4rg+3 from tile rows o .. o+6, i.e. row pairs
+        // 2rg .. 2rg+4; four v_dot2_u32_u16 per output (sums <= 257 * 65535 fit 32 bits)
+        uint32_t acc[4][4];
+        {
+            uint4 P[5];
 #pragma unroll
-        for (int q = 0; q < 5; q++) P[q] = *(const uint4 *)&rows[2 * rg + q][4 * j];
+            for (int qq = 0; qq < 5; qq++) P[qq] = *(const uint4 *)&rows[2 * rg + qq][4 * j];
 #pragma unroll
-        for (int b = 0; b < 4; b++) {
-            auto col = [&](int q) -> uint32_t {
-                return b == 0 ? P[q].x : b == 1 ? P[q].y : b == 2 ? P[q].z : P[q].w;
-            };
+            for (int bc = 0; bc < 4; bc++) {
+                auto col = [&](int qq) -> uint32_t {
+                    return bc == 0 ? P[qq].x : bc == 1 ? P[qq].y : bc == 2 ? P[qq].z : P[qq].w;
+                };
 #pragma unroll
-            for (int o = 0; o < 4; o++) {
-                const int m = o >> 1;  // first pair of output 4rg+o: 2rg + m
-                uint32_t a2;
-                if ((o & 1) == 0) {
-                    a2 = udot2_u32(col(m), E0, 0u);
-                    a2 = udot2_u32(col(m + 1), E1, a2);
-                    a2 = udot2_u32(col(m + 2), E2, a2);
-                    a2 = udot2_u32(col(m + 3), E3, a2);
-                } else {
-                    a2 = udot2_u32(col(m), O0, 0u);
-                    a2 = udot2_u32(col(m + 1), O1, a2);
-                    a2 = udot2_u32(col(m + 2), O2, a2);
-                    a2 = udot2_u32(col(m + 3), O3, a2);
+                for (int o = 0; o < 4; o++) {
+                    const int m = o >> 1;  // first pair of output 4rg+o: 2rg + m
+                    uint32_t a2;
+                    if ((o & 1) == 0) {
+                        a2 = udot2_u32(col(m), E0, 0u);
+                        a2 = udot2_u32(col(m + 1), E1, a2);
+                        a2 = udot2_u32(col(m + 2), E2, a2);
+                        a2 = udot2_u32(col(m + 3), E3, a2);
+                    } else {
+                        a2 = udot2_u32(col(m), O0, 0u);
+                        a2 = udot2_u32(col(m + 1), O1, a2);
+                        a2 = udot2_u32(col(m + 2), O2, a2);
+                        a2 = udot2_u32(col(m + 3), O3, a2);
+                    }
+                    acc[o][bc] = a2;
                 }
-                acc[o][b] = a2;
             }
         }
-    }
-    uint8_t *dst = blur + f * g->blur_frame + lv.blur_off;
-    const int gx = tx0 + 4 * j;
 #pragma unroll
-    for (int o = 0; o < 4; o++) {
-        const int gy = ty0 + 4 * rg + o;
-        if (gy >= H || gx >= W) continue;
-        uint32_t word = 0;
+        for (int o = 0; o < 4; o++) {
+            const int gy = ty0 + 4 * rg + o;
+            if (gy >= H || gx >= W) continue;
+            uint32_t word = 0;
 #pragma unroll
-        for (int b = 0; b < 4; b++) word |= min((acc[o][b] + (1u << 15)) >> 16, 255u) << (8 * b);
-        uint8_t *d = dst + (int64_t)gy * lv.pitch + gx;
-        if (gx + 4 <= W) {
-            *(uint32_t *)d = word;  // pitch is a multiple of 64, gx of 4: aligned
-        } else {
-            for (int b = 0; b < 4 && gx + b < W; b++) d[b] = (uint8_t)(word >> (8 * b));
+            for (int bc = 0; bc < 4; bc++) word |= min((acc[o][bc] + (1u << 15)) >> 16, 255u) << (8 * bc);
+            uint8_t *d = dst + (int64_t)gy * lv.pitch + gx;
+            if (gx + 4 <= W) {
+                *(uint32_t *)d = word;  // pitch is a multiple of 64, gx of 4: aligned
+            } else {
+                for (int bc = 0; bc < 4 && gx + bc < W; bc++) d[bc] = (uint8_t)(word >> (8 * bc));
+            }
         }
     }
 }

@@ -552,7 +552,7 @@ static int plan(orbg_ctx *c, int w, int h, int batch)
         L.blur_off = blur_off;
         blur_off += (int64_t)L.pitch * L.h;
         tile_base.push_back(tiles);
-        tiles += ((L.w + 127) / 128) * ((L.h + 31) / 32);  // k_blur 128x32 tiles
+        tiles += ((L.w + 127) / 128) * ((L.h + 32 * ORBG_BLUR_NB - 1) / (32 * ORBG_BLUR_NB));  // k_blur regions
         // resize coefficient tables (cv::resize, INTER_LINEAR)
         if (l > 0) {
             const int sw = lw[l - 1], sh = lh[l - 1], dw = lw[l], dh = lh[l];

@@ -26,6 +26,7 @@
 #define ORBG_GRID_COLS 64        // Frame.h:38
 #define ORBG_GRID_ROWS 48        // Frame.h:37
 #define ORBG_MATCH_TOPK 8
+#define ORBG_BLUR_NB 4           // k_blur: 32-row output bands per workgroup
 #ifndef ORBG_OD_KPW
 #define ORBG_OD_KPW 8            // k_orient_desc: quadtree output slots per wave
 #endif
