@@ -56,15 +56,23 @@ __device__ int block_sum(int v, int *sh)
 // xtab[dx] = {sx, a0 | a1 << 16}; ytab[dy] = {sy0 | sy1 << 16, b0 | b1 << 16}
 // columns dx < bulk_end use the SIMD vertical pass (mulhi of S>>4), the rest the
 // scalar FixedPtCast<int,uchar,22>.
-// One workgroup per RZ_TW x RZ_TH output tile: the source rows/columns the tile touches
-// are staged in LDS with dword loads (each row keeps its source address alignment, so a
-// caller image with an odd pitch works), then each thread owns 4 output columns (their
-// coefficients stay in registers) and walks RZ_TH/4 rows, storing one dword per row.
+// A workgroup walks RZ_NT vertical RZ_TW x RZ_TH output tiles.  The source rows/columns a
+// tile touches are staged in LDS from 16-byte chunks (each row keeps its source address
+// alignment, so a caller image with an odd pitch works); the next tile's chunks are in
+// flight while the current one is computed.  Each thread owns 4 output columns (their
+// coefficients stay in registers) and wave w walks the tile's rows 4w .. 4w+3 in order, so
+// a source row's horizontal sums are computed once and reused by the next output row
+// (1.2 source rows per output row instead of 2).  One dword store per output row.
 // ---------------------------------------------------------------------------
 #define RZ_TW 256
 #define RZ_TH 16
+#define RZ_NT ORBG_RZ_NT      // tiles per workgroup
+#define RZ_FILL ORBG_RZ_FILL  // staged chunks per thread (host: rows x chunks <= 256 x RZ_FILL)
+#ifndef RZ_WPE
+#define RZ_WPE 1  // min waves per SIMD (no cap: the prefetch chunks need ~90 VGPRs)
+#endif
 
-__global__ __launch_bounds__(256) void k_resize(const uint8_t *__restrict__ src, int64_t sfs,
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RZ_WPE, 8))) void k_resize(const uint8_t *__restrict__ src, int64_t sfs,
                                                 int spitch, int sw, uint8_t *__restrict__ dst,
                                                 int64_t dfs, int dpitch, int dw, int dh,
                                                 const int2 *__restrict__ xtab,
@@ -74,50 +82,62 @@ __global__ __launch_bounds__(256) void k_resize(const uint8_t *__restrict__ src,
     extern __shared__ __attribute__((aligned(16))) uint32_t rz_lds[];
     uint8_t *lds = (uint8_t *)rz_lds;
     const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
-    const int c0 = blockIdx.x * RZ_TW, r0 = blockIdx.y * RZ_TH, f = blockIdx.z;
-    const int c1 = min(c0 + RZ_TW, dw) - 1, r1 = min(r0 + RZ_TH, dh) - 1;
+    const int c0 = blockIdx.x * RZ_TW, rb0 = blockIdx.y * (RZ_TH * RZ_NT), f = blockIdx.z;
+    const int ntile = min(RZ_NT, (dh - rb0 + RZ_TH - 1) / RZ_TH);  // >= 1
+    const int c1 = min(c0 + RZ_TW, dw) - 1;
     const int sx_lo = xtab[c0].x;
     const int sx_hi = min(xtab[c1].x + 1, sw - 1);
-    const int sy_lo = ytab[r0].x & 0xFFFF;
-    const int sy_hi = ytab[r1].x >> 16;
     const uint8_t *fb = src + f * sfs;
-    // ---- stage rows sy_lo..sy_hi, columns sx_lo..sx_hi: 16-byte chunks from each row's
-    // 4-byte-aligned start, every load issued before the LDS stores; a chunk reaching
-    // outside [row, row + sw) is assembled from its in-row bytes ----
-    {
-        const int nrow = sy_hi - sy_lo + 1;
-        const int nch = (3 + sx_hi - sx_lo + 1 + 15) >> 4;  // chunks per row (upper bound)
-        const int total = nrow * nch;
-        for (int i0 = 0; i0 < total; i0 += 4 * 256) {
-            uint4 q[4];
-            int dst[4];
+    const int nch = (3 + sx_hi - sx_lo + 1 + 15) >> 4;  // chunks per row (upper bound)
+    // ---- staging: chunk i = (row r, chunk c) of the tile's source rows, 16 bytes from the
+    // row's 4-byte-aligned start; a chunk reaching outside [row, row + sw) (image edges) is
+    // assembled byte-wise at store time ----
+    uint4 q[RZ_FILL];
+    int dsto[RZ_FILL];  // LDS offset, bit 30 = edge chunk, -1 = none
+    auto load_tile = [&](int r0) {
+        const int r1 = min(r0 + RZ_TH, dh) - 1;
+        const int sy_lo = ytab[r0].x & 0xFFFF, sy_hi = ytab[r1].x >> 16;
+        const int total = (sy_hi - sy_lo + 1) * nch;
 #pragma unroll
-            for (int k = 0; k < 4; k++) {
-                const int i = i0 + 256 * k + tid;
-                q[k] = make_uint4(0, 0, 0, 0);
-                dst[k] = -1;
-                if (i < total) {
-                    const int r = i / nch, c = i - r * nch;
-                    const uint8_t *row = fb + (int64_t)(sy_lo + r) * spitch;
-                    const uint8_t *start = row + sx_lo;
-                    const uint8_t *cp = start - ((uintptr_t)start & 3) + 16 * c;
-                    if (cp >= row && cp + 16 <= row + sw) {
-                        q[k] = *(const uint4 *)cp;
-                    } else {
-                        uint32_t w4[4] = {0, 0, 0, 0};
-                        for (int b = 0; b < 16; b++)
-                            if (cp + b >= row && cp + b < row + sw)
-                                w4[b >> 2] |= (uint32_t)cp[b] << (8 * (b & 3));
-                        q[k] = make_uint4(w4[0], w4[1], w4[2], w4[3]);
-                    }
-                    dst[k] = r * lds_pitch + 16 * c;
-                }
+        for (int k = 0; k < RZ_FILL; k++) {
+            const int i = 256 * k + tid;
+            q[k] = make_uint4(0, 0, 0, 0);
+            dsto[k] = -1;
+            if (i < total) {
+                const int r = i / nch, c = i - r * nch;
+                const uint8_t *row = fb + (int64_t)(sy_lo + r) * spitch;
+                const uint8_t *start = row + sx_lo;
+                const uint8_t *cp = start - ((uintptr_t)start & 3) + 16 * c;
+                const bool in_row = cp >= row && cp + 16 <= row + sw;
+                if (in_row) q[k] = *(const uint4 *)cp;
+                dsto[k] = (r * lds_pitch + 16 * c) | (in_row ? 0 : 1 << 30);
             }
-#pragma unroll
-            for (int k = 0; k < 4; k++)
-                if (dst[k] >= 0) *(uint4 *)(lds + dst[k]) = q[k];
         }
-    }
+        return sy_lo;
+    };
+    auto store_tile = [&](int sy_lo) {
+#pragma unroll
+        for (int k = 0; k < RZ_FILL; k++) {
+            if (dsto[k] < 0) continue;
+            int o = dsto[k];
+            if (o & (1 << 30)) {
+                o &= ~(1 << 30);
+                int r = o / lds_pitch;
+                // opaque: keeps the edge path's address math out of the tile loop
+                asm volatile("" : "+v"(r));
+                const int c = (o - r * lds_pitch) >> 4;
+                const uint8_t *row = fb + (int64_t)(sy_lo + r) * spitch;
+                const uint8_t *start = row + sx_lo;
+                const uint8_t *cp = start - ((uintptr_t)start & 3) + 16 * c;
+                uint32_t w4[4] = {0, 0, 0, 0};
+                for (int b = 0; b < 16; b++)
+                    if (cp + b >= row && cp + b < row + sw)
+                        w4[b >> 2] |= (uint32_t)cp[b] << (8 * (b & 3));
+                q[k] = make_uint4(w4[0], w4[1], w4[2], w4[3]);
+            }
+            *(uint4 *)(lds + o) = q[k];
+        }
+    };
     // ---- per-thread column coefficients ----
     const int dx0 = c0 + 4 * lane;
     int ox0[4], ox1[4], ca0[4], ca1[4];
@@ -130,37 +150,67 @@ __global__ __launch_bounds__(256) void k_resize(const uint8_t *__restrict__ src,
         ca0[i] = (int)(short)(xt.y & 0xFFFF);
         ca1[i] = (int)(short)(xt.y >> 16);
     }
-    __syncthreads();
-    if (dx0 > c1) return;
-    const int nvalid = min(4, c1 - dx0 + 1);
-    for (int dy = r0 + wv; dy <= r1; dy += 4) {
-        const int2 yt = ytab[dy];
-        const int sy0 = yt.x & 0xFFFF, sy1 = yt.x >> 16;
-        const int b0 = (int)(short)(yt.y & 0xFFFF), b1 = (int)(short)(yt.y >> 16);
-        const int sh0 = (int)((uintptr_t)(fb + (int64_t)sy0 * spitch + sx_lo) & 3);
-        const int sh1 = (int)((uintptr_t)(fb + (int64_t)sy1 * spitch + sx_lo) & 3);
-        const uint8_t *l0 = lds + (sy0 - sy_lo) * lds_pitch + sh0;
-        const uint8_t *l1 = lds + (sy1 - sy_lo) * lds_pitch + sh1;
-        uint32_t word = 0;
+    const int nvalid = min(4, c1 - dx0 + 1);  // <= 0: this thread has no columns
+    int sy_lo = load_tile(rb0);
+#pragma unroll 1
+    for (int t = 0; t < ntile; t++) {  // workgroup-uniform trip count
+        const int r0 = rb0 + t * RZ_TH, r1 = min(r0 + RZ_TH, dh) - 1;
+        __syncthreads();  // the previous tile's LDS reads are done
+        store_tile(sy_lo);
+        __syncthreads();
+        const int cur_lo = sy_lo;
+        if (t + 1 < ntile) sy_lo = load_tile(r0 + RZ_TH);
+        if (nvalid <= 0) continue;
+        // horizontal sums of source row sy for this thread's 4 columns
+        auto hrow = [&](int sy, int h[4]) {
+            const int sh = (int)((uintptr_t)(fb + (int64_t)sy * spitch + sx_lo) & 3);
+            const uint8_t *lr = lds + (sy - cur_lo) * lds_pitch + sh;
 #pragma unroll
-        for (int i = 0; i < 4; i++) {
-            const int rr0 = l0[ox0[i]] * ca0[i] + l0[ox1[i]] * ca1[i];
-            const int rr1 = l1[ox0[i]] * ca0[i] + l1[ox1[i]] * ca1[i];
-            int v;
-            if (dx0 + i < bulk_end) {
-                const int a = ((rr0 >> 4) * b0) >> 16;
-                const int b = ((rr1 >> 4) * b1) >> 16;
-                v = (a + b + 2) >> 2;
+            for (int i = 0; i < 4; i++) h[i] = lr[ox0[i]] * ca0[i] + lr[ox1[i]] * ca1[i];
+        };
+        int psy = -1, ph[4] = {0, 0, 0, 0};
+#pragma unroll 1
+        for (int k = 0; k < RZ_TH / 4; k++) {
+            const int dy = r0 + 4 * wv + k;  // wave-uniform
+            if (dy > r1) break;
+            const int2 yt = ytab[dy];
+            const int sy0 = yt.x & 0xFFFF, sy1 = yt.x >> 16;
+            const int b0 = (int)(short)(yt.y & 0xFFFF), b1 = (int)(short)(yt.y >> 16);
+            int h0[4], h1[4];
+            if (sy0 == psy) {
+#pragma unroll
+                for (int i = 0; i < 4; i++) h0[i] = ph[i];
             } else {
-                v = (rr0 * b0 + rr1 * b1 + (1 << 21)) >> 22;
+                hrow(sy0, h0);
             }
-            word |= (uint32_t)min(max(v, 0), 255) << (8 * i);
-        }
-        uint8_t *d = dst + f * dfs + (int64_t)dy * dpitch + dx0;
-        if (nvalid == 4) {
-            *(uint32_t *)d = word;  // dpitch % 64 == 0 and dx0 % 4 == 0
-        } else {
-            for (int i = 0; i < nvalid; i++) d[i] = (uint8_t)(word >> (8 * i));
+            if (sy1 == sy0) {
+#pragma unroll
+                for (int i = 0; i < 4; i++) h1[i] = h0[i];
+            } else {
+                hrow(sy1, h1);
+            }
+            psy = sy1;
+#pragma unroll
+            for (int i = 0; i < 4; i++) ph[i] = h1[i];
+            uint32_t word = 0;
+#pragma unroll
+            for (int i = 0; i < 4; i++) {
+                int v;
+                if (dx0 + i < bulk_end) {
+                    const int a = ((h0[i] >> 4) * b0) >> 16;
+                    const int b = ((h1[i] >> 4) * b1) >> 16;
+                    v = (a + b + 2) >> 2;
+                } else {
+                    v = (h0[i] * b0 + h1[i] * b1 + (1 << 21)) >> 22;
+                }
+                word |= (uint32_t)min(max(v, 0), 255) << (8 * i);
+            }
+            uint8_t *d = dst + f * dfs + (int64_t)dy * dpitch + dx0;
+            if (nvalid == 4) {
+                *(uint32_t *)d = word;  // dpitch % 64 == 0 and dx0 % 4 == 0
+            } else {
+                for (int i = 0; i < nvalid; i++) d[i] = (uint8_t)(word >> (8 * i));
+            }
         }
     }
 }

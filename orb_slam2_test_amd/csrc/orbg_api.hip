@@ -612,8 +612,8 @@ static int plan(orbg_ctx *c, int w, int h, int batch)
             }
             L.rz_pitch = ((span + 3 + 15) / 16) * 16;  // whole 16-byte chunks per row
             L.rz_rows = rows;
-            if ((int64_t)L.rz_pitch * rows > 64 * 1024)
-                return set_err(ORBG_ENOTSUP, "level %d resize tile needs %d x %d LDS bytes", l,
+            if ((int64_t)L.rz_pitch * rows > 64 * 1024 || rows * (L.rz_pitch / 16) > 256 * ORBG_RZ_FILL)
+                return set_err(ORBG_ENOTSUP, "level %d resize tile needs %d x %d staged bytes", l,
                                rows, L.rz_pitch);
         }
     }
@@ -907,7 +907,7 @@ static int launch_extract(orbg_ctx *c, const uint8_t *d_imgs, int B, int pitch, 
         const uint8_t *src = (l == 1) ? d_imgs : c->d_pyr + P.pyr_off;
         const int64_t sfs = (l == 1) ? fs : G.pyr_frame;
         const int spitch = (l == 1) ? pitch : P.pitch;
-        dim3 grid((L.w + 255) / 256, (L.h + 15) / 16, B);
+        dim3 grid((L.w + 255) / 256, (L.h + 16 * ORBG_RZ_NT - 1) / (16 * ORBG_RZ_NT), B);
         PROF_LAUNCH(c, "resize",
                     hipLaunchKernelGGL(k_resize, grid, dim3(256), L.rz_pitch * L.rz_rows, st,
                                        src, sfs, spitch, P.w, c->d_pyr + L.pyr_off, G.pyr_frame,

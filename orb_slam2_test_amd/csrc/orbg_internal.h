@@ -26,6 +26,12 @@
 #define ORBG_GRID_COLS 64        // Frame.h:38
 #define ORBG_GRID_ROWS 48        // Frame.h:37
 #define ORBG_MATCH_TOPK 8
+#ifndef ORBG_RZ_NT
+#define ORBG_RZ_NT 1             // k_resize: 16-row output tiles per workgroup (more: the prefetched chunks cost occupancy, measured slower)
+#endif
+#ifndef ORBG_RZ_FILL
+#define ORBG_RZ_FILL 5           // k_resize: staged 16-byte chunks per thread
+#endif
 #define ORBG_BLUR_NB 4           // k_blur: 32-row output bands per workgroup
 #ifndef ORBG_OD_KPW
 #define ORBG_OD_KPW 8            // k_orient_desc: quadtree output slots per wave
