@@ -817,12 +817,24 @@ extern "C" int orbg_create(int device, const orbg_params *p, orbg_ctx **out)
         return set_err(ORBG_EIO, "hipStreamCreate failed");
     }
     c->stream = c->own_stream;
-    if (hipStreamCreateWithFlags(&c->aux_stream, hipStreamNonBlocking) != hipSuccess) {
+    // The matching streams run at low priority: a stream of another priority gets its own
+    // hardware queue (at normal priority it can share one with the caller's stream and then
+    // runs strictly after it), and the dispatcher hands the matching kernels the slots the
+    // extraction leaves free (quadtree, kernel tails).  Measured: extract + match per 256
+    // frames 2.24 -> 2.13 ms.  Developer A/B: ORBG_MATCH_PRIO=normal|high.
+    int prio_lo = 0, prio_hi = 0;
+    hipDeviceGetStreamPriorityRange(&prio_lo, &prio_hi);
+    int mprio = prio_lo;
+    if (const char *e = getenv("ORBG_MATCH_PRIO")) {
+        if (!strcmp(e, "normal")) mprio = 0;
+        if (!strcmp(e, "high")) mprio = prio_hi;
+    }
+    if (hipStreamCreateWithPriority(&c->aux_stream, hipStreamNonBlocking, mprio) != hipSuccess) {
         hipStreamDestroy(c->own_stream);
         delete c;
         return set_err(ORBG_EIO, "hipStreamCreate failed");
     }
-    if (hipStreamCreateWithFlags(&c->mstream, hipStreamNonBlocking) != hipSuccess) {
+    if (hipStreamCreateWithPriority(&c->mstream, hipStreamNonBlocking, mprio) != hipSuccess) {
         hipStreamDestroy(c->aux_stream);
         hipStreamDestroy(c->own_stream);
         delete c;
