@@ -157,7 +157,9 @@ __device__ __forceinline__ void oct_children(uint32_t *codes, uint16_t *sidx,
     }
 }
 
-// level = level0 + blockIdx.x, frame = blockIdx.y; handles a level iff its candidate count
+// frame = blockIdx.x, level = level0 + blockIdx.y (the dispatcher walks x fastest, so every
+// frame's largest level starts first and the small levels fill the tail); handles a level iff
+// its candidate count
 // n <= D.kcap (k_octree takes the rest, same threshold)
 __global__ __launch_bounds__(OCT_T) void k_octree_lds(
     const OrbgGeom *__restrict__ g, const int32_t *__restrict__ cell_cnt,
@@ -181,7 +183,7 @@ __global__ __launch_bounds__(OCT_T) void k_octree_lds(
         p += D.uni_bytes;
         V.aux = (uint16_t *)p;
     }
-    const int l = D.level0 + blockIdx.x, f = blockIdx.y, tid = threadIdx.x;
+    const int l = D.level0 + blockIdx.y, f = blockIdx.x, tid = threadIdx.x;
     const OrbgLevel &lv = g->lv[l];
     const int64_t kbase = (int64_t)f * g->keys_frame + lv.key_off;
     uint32_t *kglob = keys_all + kbase;

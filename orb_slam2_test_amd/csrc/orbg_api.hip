@@ -934,13 +934,13 @@ static int launch_extract(orbg_ctx *c, const uint8_t *d_imgs, int B, int pitch, 
                 hipLaunchKernelGGL(k_blur, dim3(c->total_tiles * B), dim3(256), 0, st, c->d_geom,
                                    c->d_tile_base, d_imgs, fs, pitch, c->d_pyr, c->d_blur));
     PROF_LAUNCH(c, "octree",
-                hipLaunchKernelGGL(k_octree_lds, dim3(1, B), dim3(512),
+                hipLaunchKernelGGL(k_octree_lds, dim3(B, 1), dim3(512),
                                    oct_lds_bytes(c->oct_dims[0]), st, c->d_geom, c->d_cell_cnt,
                                    c->d_cell_kp, c->d_keys, c->d_act, c->d_lvl_kp, c->d_lvl_cnt,
                                    c->d_err, c->oct_dims[0]));
     if (G.L > 1)
         PROF_LAUNCH(c, "octree",
-                    hipLaunchKernelGGL(k_octree_lds, dim3(G.L - 1, B), dim3(512),
+                    hipLaunchKernelGGL(k_octree_lds, dim3(B, G.L - 1), dim3(512),
                                        oct_lds_bytes(c->oct_dims[1]), st, c->d_geom,
                                        c->d_cell_cnt, c->d_cell_kp, c->d_keys, c->d_act,
                                        c->d_lvl_kp, c->d_lvl_cnt, c->d_err, c->oct_dims[1]));
