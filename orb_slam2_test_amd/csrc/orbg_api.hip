@@ -191,6 +191,12 @@ struct orbg_ctx {
     // second stream for independent work inside one call (blur beside FAST+quadtree, knn2
     // beside SearchForInitialization); forked from / joined into `stream` with events
     hipStream_t aux_stream = nullptr;
+    // quadtree stream (high priority, its own hardware queue): the quadtree runs beside the
+    // GaussianBlur, fork after the FAST cells (ev_fast), join before k_octree (ev_oct).
+    // oct_mode 0: everything on the extraction stream, 1: level 0 only, 2: all levels.
+    hipStream_t ostream = nullptr;
+    hipEvent_t ev_fast = nullptr, ev_oct = nullptr;
+    int oct_mode = 0;
     hipEvent_t ev_fork[2] = {nullptr, nullptr}, ev_join[2] = {nullptr, nullptr};
     // Batch matching and the trajectory summary run on `mstream`, so the matching of batch k
     // overlaps the extraction of batch k+1 on `stream`.  The per-frame outputs (kps, desc,
@@ -704,9 +710,12 @@ static int plan(orbg_ctx *c, int w, int h, int batch)
             }
             return d;
         };
-        c->oct_dims[0] = dims(0, 1, OCT_KEY_CAP, false);
-        // 3 workgroups per CU: 160 KB / 3 minus the static header
+        // levels 1..: 3 workgroups per CU (160 KB / 3 minus the static header); level 0: the
+        // rest of a CU beside one of them (it runs concurrently on the quadtree stream), at
+        // most OCT_KEY_CAP candidates
         c->oct_dims[1] = dims(1, G.L, 163840 / 3 - (int)sizeof(OctLdsHdr) - 64, true);
+        c->oct_dims[0] = dims(0, 1, 163840 - (int)oct_lds_bytes(c->oct_dims[1]) -
+                                        2 * (int)sizeof(OctLdsHdr) - 128, true);
         for (int k = 0; k < 2; k++) {
             const size_t b = oct_lds_bytes(c->oct_dims[k]);
             if (b + sizeof(OctLdsHdr) > 160 * 1024)
@@ -834,6 +843,18 @@ extern "C" int orbg_create(int device, const orbg_params *p, orbg_ctx **out)
         delete c;
         return set_err(ORBG_EIO, "hipStreamCreate failed");
     }
+    {
+        const char *e = getenv("ORBG_OCT_STREAM");
+        c->oct_mode = e ? atoi(e) : 1;
+        if (c->oct_mode &&
+            hipStreamCreateWithPriority(&c->ostream, hipStreamNonBlocking, prio_hi) == hipSuccess) {
+            hipEventCreateWithFlags(&c->ev_fast, hipEventDisableTiming);
+            hipEventCreateWithFlags(&c->ev_oct, hipEventDisableTiming);
+        } else {
+            c->ostream = nullptr;
+            c->oct_mode = 0;
+        }
+    }
     if (hipStreamCreateWithPriority(&c->mstream, hipStreamNonBlocking, mprio) != hipSuccess) {
         hipStreamDestroy(c->aux_stream);
         hipStreamDestroy(c->own_stream);
@@ -862,6 +883,7 @@ extern "C" void orbg_destroy(orbg_ctx *c)
     if (c->d_scr) hipFree(c->d_scr);
     if (c->d_trk) hipFree(c->d_trk);
     if (c->aux_stream) hipStreamSynchronize(c->aux_stream);
+    if (c->ostream) hipStreamSynchronize(c->ostream);
     if (c->mstream) hipStreamSynchronize(c->mstream);
     for (int i = 0; i < 2; i++) {
         if (c->ev_fork[i]) hipEventDestroy(c->ev_fork[i]);
@@ -870,6 +892,9 @@ extern "C" void orbg_destroy(orbg_ctx *c)
         if (c->ev_mat[i]) hipEventDestroy(c->ev_mat[i]);
     }
     if (c->aux_stream) hipStreamDestroy(c->aux_stream);
+    if (c->ostream) hipStreamDestroy(c->ostream);
+    if (c->ev_fast) hipEventDestroy(c->ev_fast);
+    if (c->ev_oct) hipEventDestroy(c->ev_oct);
     if (c->mstream) hipStreamDestroy(c->mstream);
     if (c->own_stream) hipStreamDestroy(c->own_stream);
     delete c;
@@ -930,20 +955,36 @@ static int launch_extract(orbg_ctx *c, const uint8_t *d_imgs, int B, int pitch, 
                 hipLaunchKernelGGL(k_fast_cells, dim3((G.ncells * B + 3) / 4), dim3(256),
                                    4 * G.fc_wave_bytes, st, c->d_geom, c->d_cells, d_imgs, fs,
                                    pitch, c->d_pyr, c->d_ctab, c->d_cell_cnt, c->d_cell_kp, B));
+    if (c->oct_mode) {
+        HIPCHK(hipEventRecord(c->ev_fast, st));
+        HIPCHK(hipStreamWaitEvent(c->ostream, c->ev_fast, 0));
+    }
+    {
+        // PROF_LAUNCH records on `st`
+        hipStream_t st = c->oct_mode ? c->ostream : c->stream;
+        PROF_LAUNCH(c, "octree",
+                    hipLaunchKernelGGL(k_octree_lds, dim3(B, 1), dim3(512),
+                                       oct_lds_bytes(c->oct_dims[0]), st, c->d_geom,
+                                       c->d_cell_cnt, c->d_cell_kp, c->d_keys, c->d_act,
+                                       c->d_lvl_kp, c->d_lvl_cnt, c->d_err, c->oct_dims[0]));
+        if (c->oct_mode == 2 && G.L > 1)
+            PROF_LAUNCH(c, "octree",
+                        hipLaunchKernelGGL(k_octree_lds, dim3(B, G.L - 1), dim3(512),
+                                           oct_lds_bytes(c->oct_dims[1]), st, c->d_geom,
+                                           c->d_cell_cnt, c->d_cell_kp, c->d_keys, c->d_act,
+                                           c->d_lvl_kp, c->d_lvl_cnt, c->d_err, c->oct_dims[1]));
+        if (c->oct_mode) HIPCHK(hipEventRecord(c->ev_oct, st));
+    }
     PROF_LAUNCH(c, "blur",
                 hipLaunchKernelGGL(k_blur, dim3(c->total_tiles * B), dim3(256), 0, st, c->d_geom,
                                    c->d_tile_base, d_imgs, fs, pitch, c->d_pyr, c->d_blur));
-    PROF_LAUNCH(c, "octree",
-                hipLaunchKernelGGL(k_octree_lds, dim3(B, 1), dim3(512),
-                                   oct_lds_bytes(c->oct_dims[0]), st, c->d_geom, c->d_cell_cnt,
-                                   c->d_cell_kp, c->d_keys, c->d_act, c->d_lvl_kp, c->d_lvl_cnt,
-                                   c->d_err, c->oct_dims[0]));
-    if (G.L > 1)
+    if (c->oct_mode != 2 && G.L > 1)
         PROF_LAUNCH(c, "octree",
                     hipLaunchKernelGGL(k_octree_lds, dim3(B, G.L - 1), dim3(512),
                                        oct_lds_bytes(c->oct_dims[1]), st, c->d_geom,
                                        c->d_cell_cnt, c->d_cell_kp, c->d_keys, c->d_act,
                                        c->d_lvl_kp, c->d_lvl_cnt, c->d_err, c->oct_dims[1]));
+    if (c->oct_mode) HIPCHK(hipStreamWaitEvent(st, c->ev_oct, 0));
     PROF_LAUNCH(c, "octree_big",
                 hipLaunchKernelGGL(k_octree, dim3(G.L, B), dim3(ORBG_OCT_THREADS), 0, st,
                                    c->d_geom, c->d_cell_cnt, c->d_cell_kp, c->d_keys, c->d_knode,
@@ -980,6 +1021,7 @@ static int sync_all(orbg_ctx *c)
 {
     HIPCHK(hipStreamSynchronize(c->stream));
     HIPCHK(hipStreamSynchronize(c->mstream));
+    if (c->ostream) HIPCHK(hipStreamSynchronize(c->ostream));
     c->mat_pending[0] = c->mat_pending[1] = false;
     return ORBG_OK;
 }
