@@ -166,7 +166,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RZ_WPE, 8))
             const int sh = (int)((uintptr_t)(fb + (int64_t)sy * spitch + sx_lo) & 3);
             const uint8_t *lr = lds + (sy - cur_lo) * lds_pitch + sh;
 #pragma unroll
-            for (int i = 0; i < 4; i++) h[i] = lr[ox0[i]] * ca0[i] + lr[ox1[i]] * ca1[i];
+            for (int i = 0; i < 4; i++)
+                h[i] = __mul24((int)lr[ox0[i]], ca0[i]) + __mul24((int)lr[ox1[i]], ca1[i]);
         };
         int psy = -1, ph[4] = {0, 0, 0, 0};
 #pragma unroll 1
@@ -196,12 +197,13 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RZ_WPE, 8))
 #pragma unroll
             for (int i = 0; i < 4; i++) {
                 int v;
+                // 24-bit multiplies (full rate): |h| <= 255 * 2 * 2048 < 2^23, |b| <= 2048
                 if (dx0 + i < bulk_end) {
-                    const int a = ((h0[i] >> 4) * b0) >> 16;
-                    const int b = ((h1[i] >> 4) * b1) >> 16;
+                    const int a = __mul24(h0[i] >> 4, b0) >> 16;
+                    const int b = __mul24(h1[i] >> 4, b1) >> 16;
                     v = (a + b + 2) >> 2;
                 } else {
-                    v = (h0[i] * b0 + h1[i] * b1 + (1 << 21)) >> 22;
+                    v = (__mul24(h0[i], b0) + __mul24(h1[i], b1) + (1 << 21)) >> 22;
                 }
                 word |= (uint32_t)min(max(v, 0), 255) << (8 * i);
             }
