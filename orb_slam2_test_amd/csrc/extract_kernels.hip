@@ -462,8 +462,13 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(6, 8))) voi
     // (b0 & b4) | (b4 & b8) | (b8 & b12) | (b12 & b0) = (b0 | b8) & (b4 | b12), i.e.
     // mb = min(max(c0, c8), max(c4, c12)) > v + th; darker: md = max(min(c0, c8),
     // min(c4, c12)) < v - th.
+    // Three survivor lists (u16 row << 8 | group, raster order): units with any passing
+    // pixel (walked by the NMS) and, per pixel pair, pairs A (pixels 0,1) and B (2,3).  The
+    // scores are computed per pair: 31% of the pairs pass where 46% of the units do.
+    const int lcap = (g->fc_wave_bytes - g->fc_list_off) / 6;
     uint16_t *plist = (uint16_t *)(tile + g->fc_list_off);
-    int npass = 0;
+    uint16_t *alist = plist + lcap, *blist = alist + lcap;
+    int npass = 0, na = 0, nb = 0;
     {
         const v2s vth1 = (v2s){(short)(thi + 1), (short)(thi + 1)};
         // uniform trip count: the scan below is wave-wide
@@ -500,10 +505,18 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(6, 8))) voi
                 const int valid = min(RW - 4 * gg, 4);
                 if (valid < 4) pm &= (1u << valid) - 1u;
             }
-            int tot;
-            const int incl = wave_incl_scan_small(pm ? 1 : 0, &tot);
-            if (pm) plist[npass + incl - 1] = (uint16_t)(ry << 8 | gg);
-            npass += tot;
+            // ballot + mbcnt compaction of the three lists
+            const uint16_t e = (uint16_t)(ry << 8 | gg);
+            auto append = [&](bool flag, uint16_t *list, int &n) {
+                const unsigned long long m = __ballot(flag);
+                const int below = __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32),
+                                                            __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0));
+                if (flag) list[n + below] = e;
+                n += __popcll(m);
+            };
+            append(pm != 0, plist, npass);
+            append((pm & 3u) != 0, alist, na);
+            append((pm & 12u) != 0, blist, nb);
             ry += rstep;
             gg += gstep;
             if (gg >= RG) {
@@ -513,11 +526,27 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(6, 8))) voi
         }
     }
     wave_sync_lds();
-    // ---- scores of the pretest survivors (dense over lanes) ----
-    for (int j = lane; j < npass; j += 64) {
-        const int e = plist[j];
-        score_unit(e >> 8, e & 0xFF);
-    }
+    // ---- scores of the pretest survivors, per pixel pair (dense over lanes) ----
+    // a pair's two scores go to bytes 0,1 (A) or 2,3 (B) of the unit's score word; the
+    // pair not listed keeps the zeros of the cleared score tile
+    auto score_pair = [&](auto I, int e) {
+        constexpr int i = decltype(I)::value;
+        const int ry = e >> 8, gg = e & 0xFF;
+        Rows7 R;
+#pragma unroll
+        for (int r = 0; r < 7; r++) {
+            const uint32_t *p = (const uint32_t *)(tile + (ry + r) * P + 4 * gg);
+            R.w[r][0] = p[0];
+            R.w[r][1] = p[1];
+            R.w[r][2] = p[2];
+        }
+        const v2s s = fast_score_pair<i>(R);
+        uint32_t h = (uint32_t)(uint16_t)s.x | ((uint32_t)(uint16_t)s.y << 8);
+        if (RW - 4 * gg < i + 2) h &= 0xFFu;  // pixel i + 1 past the region
+        *(uint16_t *)(sc + (ry + 1) * P + 4 * gg + 4 + i) = (uint16_t)h;
+    };
+    for (int j = lane; j < na; j += 64) score_pair(std::integral_constant<int, 0>{}, alist[j]);
+    for (int j = lane; j < nb; j += 64) score_pair(std::integral_constant<int, 2>{}, blist[j]);
     wave_sync_lds();
     if (g->dbg == 12) return;
 
