@@ -340,7 +340,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(6, 8))) voi
                                                     const uint8_t *__restrict__ pyr,
                                                     const uint32_t *__restrict__ ctab,
                                                     int32_t *__restrict__ cell_cnt,
-                                                    uint2 *__restrict__ cell_kp, int nframes)
+                                                    uint2 *__restrict__ cell_kp, int nframes,
+                                                    int c_begin, int c_count)
 {
     extern __shared__ __attribute__((aligned(16))) uint32_t fc_lds[];
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
@@ -349,8 +350,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(6, 8))) voi
     uint8_t *sc = tile + g->fc_tile_rows * P;
     // wave-uniform: the cell record and level parameters come through the scalar cache
     const int cid = __builtin_amdgcn_readfirstlane(xcd_remap(blockIdx.x, gridDim.x) * 4 + wv);
-    if (cid >= g->ncells * nframes) return;  // wave-uniform; no workgroup barrier below
-    const int f = cid / g->ncells, c = cid - f * g->ncells;
+    // cells [c_begin, c_begin + c_count) of every frame (level 0 alone or levels 1.. alone
+    // when the level-0 cells run beside the pyramid)
+    if (cid >= c_count * nframes) return;  // wave-uniform; no workgroup barrier below
+    const int f = cid / c_count, c = c_begin + cid - f * c_count;
     // one dwordx4 (scalar load: sub-dword loads would go through the vector path)
     const uint4 cw4 = ((const uint4 *)cells)[c];
     const uint32_t cw0 = __builtin_amdgcn_readfirstlane(cw4.x);  // level | pad

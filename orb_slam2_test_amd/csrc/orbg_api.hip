@@ -26,7 +26,7 @@ namespace orbg {
 __global__ void k_resize(const uint8_t *, int64_t, int, int, uint8_t *, int64_t, int, int, int,
                          const int2 *, const int2 *, int, int);
 __global__ void k_fast_cells(const OrbgGeom *, const OrbgCell *, const uint8_t *, int64_t, int,
-                             const uint8_t *, const uint32_t *, int32_t *, uint2 *, int);
+                             const uint8_t *, const uint32_t *, int32_t *, uint2 *, int, int, int);
 __global__ void k_blur(const OrbgGeom *, const int32_t *, const uint8_t *, int64_t, int,
                        const uint8_t *, uint8_t *);
 __global__ void k_octree(const OrbgGeom *, const int32_t *, const uint2 *, uint32_t *,
@@ -197,6 +197,7 @@ struct orbg_ctx {
     hipStream_t ostream = nullptr;
     hipEvent_t ev_fast = nullptr, ev_oct = nullptr;
     int oct_mode = 0;
+    int fast0_mode = 1;  // level-0 FAST cells on `ostream` beside the resize chain (ORBG_FAST0)
     hipEvent_t ev_fork[2] = {nullptr, nullptr}, ev_join[2] = {nullptr, nullptr};
     // Batch matching and the trajectory summary run on `mstream`, so the matching of batch k
     // overlaps the extraction of batch k+1 on `stream`.  The per-frame outputs (kps, desc,
@@ -846,6 +847,8 @@ extern "C" int orbg_create(int device, const orbg_params *p, orbg_ctx **out)
     {
         const char *e = getenv("ORBG_OCT_STREAM");
         c->oct_mode = e ? atoi(e) : 1;
+        const char *f0 = getenv("ORBG_FAST0");
+        c->fast0_mode = f0 ? atoi(f0) : 1;
         if (c->oct_mode &&
             hipStreamCreateWithPriority(&c->ostream, hipStreamNonBlocking, prio_hi) == hipSuccess) {
             hipEventCreateWithFlags(&c->ev_fast, hipEventDisableTiming);
@@ -939,6 +942,23 @@ static int launch_extract(orbg_ctx *c, const uint8_t *d_imgs, int B, int pitch, 
     const OrbgGeom &G = c->geom;
     hipStream_t st = c->stream;
     HIPCHK(hipMemsetAsync(c->d_err, 0, sizeof(int32_t), st));
+    // fast0: the level-0 FAST cells and quadtree need only the input images, so they run on
+    // the quadtree stream beside the resize chain (latency-bound small launches)
+    const bool fast0 = c->fast0_mode && c->oct_mode && G.L > 1;
+    const int n0 = G.L > 1 ? G.lv[1].cell_base : G.ncells;
+    auto launch_fast = [&](hipStream_t st, int cb, int cn) {
+        PROF_LAUNCH(c, "fast_cells",
+                    hipLaunchKernelGGL(k_fast_cells, dim3((cn * B + 3) / 4), dim3(256),
+                                       4 * G.fc_wave_bytes, st, c->d_geom, c->d_cells, d_imgs,
+                                       fs, pitch, c->d_pyr, c->d_ctab, c->d_cell_cnt,
+                                       c->d_cell_kp, B, cb, cn));
+        return hipSuccess;
+    };
+    if (fast0) {
+        HIPCHK(hipEventRecord(c->ev_fast, st));
+        HIPCHK(hipStreamWaitEvent(c->ostream, c->ev_fast, 0));
+        HIPCHK(launch_fast(c->ostream, 0, n0));
+    }
     for (int l = 1; l < G.L; l++) {
         const OrbgLevel &L = G.lv[l], &P = G.lv[l - 1];
         const uint8_t *src = (l == 1) ? d_imgs : c->d_pyr + P.pyr_off;
@@ -951,13 +971,14 @@ static int launch_extract(orbg_ctx *c, const uint8_t *d_imgs, int B, int pitch, 
                                        L.pitch, L.w, L.h, c->d_rtab + L.xtab_off,
                                        c->d_rtab + L.ytab_off, L.bulk_end, L.rz_pitch));
     }
-    PROF_LAUNCH(c, "fast_cells",
-                hipLaunchKernelGGL(k_fast_cells, dim3((G.ncells * B + 3) / 4), dim3(256),
-                                   4 * G.fc_wave_bytes, st, c->d_geom, c->d_cells, d_imgs, fs,
-                                   pitch, c->d_pyr, c->d_ctab, c->d_cell_cnt, c->d_cell_kp, B));
-    if (c->oct_mode) {
-        HIPCHK(hipEventRecord(c->ev_fast, st));
-        HIPCHK(hipStreamWaitEvent(c->ostream, c->ev_fast, 0));
+    if (fast0) {
+        HIPCHK(launch_fast(st, n0, G.ncells - n0));
+    } else {
+        HIPCHK(launch_fast(st, 0, G.ncells));
+        if (c->oct_mode) {
+            HIPCHK(hipEventRecord(c->ev_fast, st));
+            HIPCHK(hipStreamWaitEvent(c->ostream, c->ev_fast, 0));
+        }
     }
     {
         // PROF_LAUNCH records on `st`
@@ -967,12 +988,18 @@ static int launch_extract(orbg_ctx *c, const uint8_t *d_imgs, int B, int pitch, 
                                        oct_lds_bytes(c->oct_dims[0]), st, c->d_geom,
                                        c->d_cell_cnt, c->d_cell_kp, c->d_keys, c->d_act,
                                        c->d_lvl_kp, c->d_lvl_cnt, c->d_err, c->oct_dims[0]));
-        if (c->oct_mode == 2 && G.L > 1)
+        if (c->oct_mode == 2 && G.L > 1) {
+            // levels 1.. need their FAST cells (launched on the extraction stream under fast0)
+            if (fast0) {
+                HIPCHK(hipEventRecord(c->ev_fast, c->stream));
+                HIPCHK(hipStreamWaitEvent(st, c->ev_fast, 0));
+            }
             PROF_LAUNCH(c, "octree",
                         hipLaunchKernelGGL(k_octree_lds, dim3(B, G.L - 1), dim3(512),
                                            oct_lds_bytes(c->oct_dims[1]), st, c->d_geom,
                                            c->d_cell_cnt, c->d_cell_kp, c->d_keys, c->d_act,
                                            c->d_lvl_kp, c->d_lvl_cnt, c->d_err, c->oct_dims[1]));
+        }
         if (c->oct_mode) HIPCHK(hipEventRecord(c->ev_oct, st));
     }
     PROF_LAUNCH(c, "blur",
