@@ -697,13 +697,15 @@ __global__ __launch_bounds__(256) void k_blur(const OrbgGeom *__restrict__ g,
                                               const int32_t *__restrict__ tile_base,
                                               const uint8_t *__restrict__ img0, int64_t img_fs,
                                               int img_pitch, const uint8_t *__restrict__ pyr,
-                                              uint8_t *__restrict__ blur)
+                                              uint8_t *__restrict__ blur, int tb_begin,
+                                              int tb_count)
 {
     __shared__ __attribute__((aligned(16))) uint8_t in[BLUR_IH][BLUR_IW];
     __shared__ __attribute__((aligned(16))) uint32_t rows[BLUR_IH / 2][BLUR_TW];  // row-pair sums
-    const int ntiles = tile_base[g->L];
+    // tiles [tb_begin, tb_begin + tb_count) of every frame (level 0 alone or levels 1..
+    // alone when level 0 runs on the quadtree stream)
     const int id = xcd_remap(blockIdx.x, gridDim.x);
-    const int f = id / ntiles, bt = id - f * ntiles, tid = threadIdx.x;
+    const int f = id / tb_count, bt = tb_begin + id - f * tb_count, tid = threadIdx.x;
     int l = 0;
     while (l + 1 < g->L && bt >= tile_base[l + 1]) l++;
     const int t = bt - tile_base[l];
