@@ -529,6 +529,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(6, 8))) voi
         }
     }
     wave_sync_lds();
+    if (g->dbg == 14) return;
     // ---- scores of the pretest survivors, per pixel pair (dense over lanes) ----
     // a pair's two scores go to bytes 0,1 (A) or 2,3 (B) of the unit's score word; the
     // pair not listed keeps the zeros of the cleared score tile
