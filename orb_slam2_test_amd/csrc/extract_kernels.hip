@@ -545,7 +545,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(6, 8))) voi
             R.w[r][2] = p[2];
         }
         const v2s s = fast_score_pair<i>(R);
-        uint32_t h = (uint32_t)(uint16_t)s.x | ((uint32_t)(uint16_t)s.y << 8);
+        // a score below iniThFAST is stored as 0: the NMS treats both alike (a neighbour
+        // < th never blocks), and a unit with no corner then has a zero score word
+        const uint32_t s0 = (uint16_t)s.x >= (uint32_t)thi ? (uint16_t)s.x : 0u;
+        const uint32_t s1 = (uint16_t)s.y >= (uint32_t)thi ? (uint16_t)s.y : 0u;
+        uint32_t h = s0 | (s1 << 8);
         if (RW - 4 * gg < i + 2) h &= 0xFFu;  // pixel i + 1 past the region
         *(uint16_t *)(sc + (ry + 1) * P + 4 * gg + 4 + i) = (uint16_t)h;
     };
@@ -620,8 +624,28 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(6, 8))) voi
         }
         run += tot;
     };
-    // FAST at iniThFAST: only pretest survivors can hold a corner, and their list is in
-    // raster order, so NMS + compaction walk the list densely
+    // FAST at iniThFAST: only units with a corner (nonzero score word) can keep a pixel;
+    // the unit list is compacted to them in place (raster order kept; a write never passes
+    // the chunk being read), then NMS + compaction walk it densely
+    {
+        int nc = 0;
+        for (int j0 = 0; j0 < npass; j0 += 64) {
+            const int j = j0 + lane;
+            int e = 0;
+            bool corner = false;
+            if (j < npass) {
+                e = plist[j];
+                corner = *(const uint32_t *)(sc + ((e >> 8) + 1) * P + 4 * (e & 0xFF) + 4) != 0;
+            }
+            const unsigned long long m = __ballot(corner);
+            const int below = __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32),
+                                                        __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0));
+            if (corner) plist[nc + below] = (uint16_t)e;
+            nc += __popcll(m);
+        }
+        npass = nc;
+    }
+    wave_sync_lds();
     for (int j0 = 0; j0 < npass; j0 += 64) {
         const int j = j0 + lane;
         int ry = 0, gg = 0;
