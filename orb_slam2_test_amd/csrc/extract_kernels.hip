@@ -465,12 +465,13 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(6, 8))) voi
     // (b0 & b4) | (b4 & b8) | (b8 & b12) | (b12 & b0) = (b0 | b8) & (b4 | b12), i.e.
     // mb = min(max(c0, c8), max(c4, c12)) > v + th; darker: md = max(min(c0, c8),
     // min(c4, c12)) < v - th.
-    // Three survivor lists (u16 row << 8 | group, raster order): units with any passing
-    // pixel (walked by the NMS) and, per pixel pair, pairs A (pixels 0,1) and B (2,3).  The
-    // scores are computed per pair: 31% of the pairs pass where 46% of the units do.
-    const int lcap = (g->fc_wave_bytes - g->fc_list_off) / 6;
-    uint16_t *plist = (uint16_t *)(tile + g->fc_list_off);
-    uint16_t *alist = plist + lcap, *blist = alist + lcap;
+    // Two survivor lists (u16 row << 8 | group, raster order) of the pixel pairs A (pixels
+    // 0,1) and B (2,3) with a pixel passing; the scores are computed per pair: 31% of the
+    // pairs pass where 46% of the units do.
+    const int lcap = (g->fc_wave_bytes - g->fc_list_off) / 4;
+    uint16_t *alist = (uint16_t *)(tile + g->fc_list_off), *blist = alist + lcap;
+    // the corner-unit list of the NMS is built after the scoring, over the pair lists
+    uint16_t *plist = alist;
     int npass = 0, na = 0, nb = 0;
     {
         const v2s vth1 = (v2s){(short)(thi + 1), (short)(thi + 1)};
@@ -517,7 +518,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(6, 8))) voi
                 if (flag) list[n + below] = e;
                 n += __popcll(m);
             };
-            append(pm != 0, plist, npass);
             append((pm & 3u) != 0, alist, na);
             append((pm & 12u) != 0, blist, nb);
             ry += rstep;
@@ -625,23 +625,24 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(6, 8))) voi
         run += tot;
     };
     // FAST at iniThFAST: only units with a corner (nonzero score word) can keep a pixel;
-    // the unit list is compacted to them in place (raster order kept; a write never passes
-    // the chunk being read), then NMS + compaction walk it densely
+    // they are listed in raster order (over the dead pair lists), then NMS + compaction walk
+    // the list densely
     {
         int nc = 0;
-        for (int j0 = 0; j0 < npass; j0 += 64) {
-            const int j = j0 + lane;
-            int e = 0;
-            bool corner = false;
-            if (j < npass) {
-                e = plist[j];
-                corner = *(const uint32_t *)(sc + ((e >> 8) + 1) * P + 4 * (e & 0xFF) + 4) != 0;
-            }
+        for (int u0 = 0, ry = ry0, gg = gg0; u0 < nunits; u0 += 64) {
+            const bool corner =
+                u0 + lane < nunits && *(const uint32_t *)(sc + (ry + 1) * P + 4 * gg + 4) != 0;
             const unsigned long long m = __ballot(corner);
             const int below = __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32),
                                                         __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0));
-            if (corner) plist[nc + below] = (uint16_t)e;
+            if (corner) plist[nc + below] = (uint16_t)(ry << 8 | gg);
             nc += __popcll(m);
+            ry += rstep;
+            gg += gstep;
+            if (gg >= RG) {
+                gg -= RG;
+                ry++;
+            }
         }
         npass = nc;
     }

@@ -664,13 +664,13 @@ static int plan(orbg_ctx *c, int w, int h, int batch)
         }
         G.fc_pitch = 4 * best_w;  // dwords 0..RG+1 of the window / score rows, + slack
         G.fc_tile_rows = hmax;
-        // pretest survivor lists: three of one u16 (row << 8 | group) per unit of the largest cell
+        // pretest survivor lists: two of one u16 (row << 8 | group) per unit of the largest cell
         int max_units = 0;
         for (const OrbgCell &cl : cells)
             max_units = std::max(max_units, std::max((int)cl.h - 6, 0) *
                                                 ((std::max((int)cl.w - 6, 0) + 3) / 4));
         G.fc_list_off = (hmax + std::max(hmax - 6, 0) + 2) * G.fc_pitch;
-        G.fc_wave_bytes = (G.fc_list_off + 6 * max_units + 15) & ~15;
+        G.fc_wave_bytes = (G.fc_list_off + 4 * max_units + 15) & ~15;
         if (4 * G.fc_wave_bytes > 64 * 1024)
             return set_err(ORBG_ENOTSUP, "FAST cell %dx%d needs %d LDS bytes per wave", wmax,
                            hmax, G.fc_wave_bytes);
