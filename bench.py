@@ -196,6 +196,9 @@ def main():
         dist.barrier()
     t1 = time.perf_counter()
     elapsed = t1 - t0
+    # sticky device error flags (quadtree capacity overflows) of every timed batch: a step
+    # that lost keypoints would make `value` invalid, so fail instead of reporting it
+    ext.ctx.check_errors()
     if world > 1:
         e = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
         dist.all_reduce(e, op=dist.ReduceOp.MAX)

@@ -89,7 +89,14 @@ typedef struct {
     int32_t brief_fma;     /* 1: fuse x*b + y*a in rBRIEF sampling (reference built -ffp-contract=fast) */
     /* batch capacity (frames per orbg_extract_batch_device call); 0 -> 1 */
     int32_t max_batch;
+    /* cos/sin of the rBRIEF rotation (ORBextractor.cc:122, (float)cos(float) = glibc cosf):
+     * ORBG_SINCOS_GLIBC restates glibc 2.35's sinf/cosf (bit-equal to the host libm on every
+     * float in [0, 7)); ORBG_SINCOS_PINNED is round 1's correctly rounded evaluation */
+    int32_t sincos_mode;
 } orbg_params;
+
+#define ORBG_SINCOS_GLIBC 0
+#define ORBG_SINCOS_PINNED 1
 
 /* cv::KeyPoint layout: pt.x, pt.y, size, angle, response, octave, class_id (28 bytes) */
 typedef struct {
@@ -184,7 +191,13 @@ int orbg_stereo_summary(orbg_ctx *ctx, int32_t *d_out);
 int orbg_download_stereo(orbg_ctx *ctx, int pair, float *uright, float *depth, int cap,
                          int32_t *nvalid);
 
+/* Device error flags are sticky: a frame whose quadtree level overflowed a capacity (its
+ * keypoints would be incomplete) sets a flag that stays set until read.  orbg_sync,
+ * orbg_check_errors, orbg_batch_stats and orbg_download_frame drain the streams, read and
+ * clear it, and return ORBG_ENOTSUP (orbg_last_error names the flags and the first frame)
+ * if any batch since the last read raised one. */
 int orbg_sync(orbg_ctx *ctx);
+int orbg_check_errors(orbg_ctx *ctx);
 void *orbg_stream(orbg_ctx *ctx);       /* hipStream_t of extraction (and host-data calls) */
 void *orbg_match_stream(orbg_ctx *ctx); /* hipStream_t of batch matching and the summary */
 /* launch on a caller-owned hipStream_t (e.g. torch's current stream) instead of the

@@ -749,12 +749,128 @@ void orc_pinned_sincos_deg(float angle_deg, float *c, float *s)
     *s = (float)sd;
 }
 
+/* ------------------------------------------------------------------ */
+/* glibc 2.35 sinf / cosf (sysdeps/ieee754/flt-32/s_sinf.c, s_cosf.c,    */
+/* sincosf.h; the ARM optimized-routines algorithm), restated for the   */
+/* range the rBRIEF rotation uses (|y| < 120; larger inputs never occur: */
+/* the angle is fastAtan2's [0, 360] degrees times pi/180).  Double     */
+/* arithmetic, one rounding to float.  The coefficient table is         */
+/* glibc's __sincosf_table (sincosf_data.c), layout {sign[4], hpi_inv   */
+/* (2/pi * 2^24), hpi, c0, c1, s1, c2, s2, c3, s3, c4}; the second entry */
+/* negates the cosine polynomial for quadrants 2-3.  glibc's x86_64 FMA */
+/* build (s_sinf-fma.c) contracts the a + b*c steps; on [0, 7) the fused */
+/* and unfused forms round to the same float for every input, and both  */
+/* equal the host libm (tools/sincosf_sweep.c, exhaustive).             */
+/* ------------------------------------------------------------------ */
+static const double sincosf_tab[2][14] = {
+    {1.0, -1.0, -1.0, 1.0, 0x1.45f306dc9c883p+23, 0x1.921fb54442d18p+0, 1.0,
+     -0x1.ffffffd0c621cp-2, -0x1.555545995a603p-3, 0x1.55553e1068f19p-5, 0x1.1107605230bc4p-7,
+     -0x1.6c087e89a359dp-10, -0x1.994eb3774cf24p-13, 0x1.99343027bf8c3p-16},
+    {1.0, -1.0, -1.0, 1.0, 0x1.45f306dc9c883p+23, 0x1.921fb54442d18p+0, -1.0,
+     0x1.ffffffd0c621cp-2, -0x1.555545995a603p-3, -0x1.55553e1068f19p-5, 0x1.1107605230bc4p-7,
+     0x1.6c087e89a359dp-10, -0x1.994eb3774cf24p-13, -0x1.99343027bf8c3p-16}};
+enum { SC_HPI_INV = 4, SC_HPI, SC_C0, SC_C1, SC_S1, SC_C2, SC_S2, SC_C3, SC_S3, SC_C4 };
+
+static uint32_t sc_top12(float f)
+{
+    uint32_t u;
+    memcpy(&u, &f, 4);
+    return (u >> 20) & 0x7ff;
+}
+
+/* sinf_poly (sincosf.h): sine polynomial for even n, cosine for odd n */
+static float sc_poly(double x, double x2, const double *p, int n)
+{
+    if ((n & 1) == 0) {
+        const double x3 = x * x2;
+        const double s1 = p[SC_S2] + x2 * p[SC_S3];
+        const double x7 = x3 * x2;
+        const double s = x + x3 * p[SC_S1];
+        return (float)(s + x7 * s1);
+    }
+    const double x4 = x2 * x2;
+    const double c2 = p[SC_C3] + x2 * p[SC_C4];
+    const double c1 = p[SC_C0] + x2 * p[SC_C1];
+    const double x6 = x4 * x2;
+    const double c = c1 + x4 * p[SC_C2];
+    return (float)(c + x6 * c2);
+}
+
+/* reduce_fast without TOINT_INTRINSICS (x86_64): quadrant n from the 2^24-scaled product */
+static double sc_reduce(double x, const double *p, int *np)
+{
+    const double r = x * p[SC_HPI_INV];
+    const int n = ((int32_t)r + 0x800000) >> 24;
+    *np = n;
+    return x - n * p[SC_HPI];
+}
+
+float orc_glibc_sinf(float y)
+{
+    double x = y;
+    const double *p = sincosf_tab[0];
+    int n;
+    if (sc_top12(y) < sc_top12(0x1.921FB6p-1f)) {  /* |y| < pi/4 by the top 12 bits */
+        if (sc_top12(y) < sc_top12(0x1p-12f)) return y;
+        return sc_poly(x, x * x, p, 0);
+    }
+    x = sc_reduce(x, p, &n);
+    const double s = p[n & 3];
+    if (n & 2) p = sincosf_tab[1];
+    return sc_poly(x * s, x * x, p, n);
+}
+
+float orc_glibc_cosf(float y)
+{
+    double x = y;
+    const double *p = sincosf_tab[0];
+    int n;
+    if (sc_top12(y) < sc_top12(0x1.921FB6p-1f)) {
+        if (sc_top12(y) < sc_top12(0x1p-12f)) return 1.0f;
+        return sc_poly(x, x * x, p, 1);
+    }
+    x = sc_reduce(x, p, &n);
+    const double s = p[n & 3];
+    if (n & 2) p = sincosf_tab[1];
+    return sc_poly(x * s, x * x, p, n ^ 1);
+}
+
+long orc_sincosf_check(uint32_t lo, uint32_t hi, uint32_t stride)
+{
+    long bad = 0;
+    if (!stride) stride = 1;
+    for (uint64_t u = lo; u < hi; u += stride) {
+        const uint32_t w = (uint32_t)u;
+        float y;
+        memcpy(&y, &w, 4);
+        const float a = sinf(y), b = orc_glibc_sinf(y), c = cosf(y), d = orc_glibc_cosf(y);
+        bad += memcmp(&a, &b, 4) != 0;
+        bad += memcmp(&c, &d, 4) != 0;
+    }
+    return bad;
+}
+
+void orc_brief_sincos_deg(float angle_deg, int sincos_mode, float *a, float *b)
+{
+    const float factorPI = (float)(3.14159265358979323846 / 180.f);
+    const float angle = angle_deg * factorPI;  /* ORBextractor.cc:121 */
+    if (sincos_mode == ORC_SINCOS_PINNED) {
+        orc_pinned_sincos_deg(angle_deg, a, b);
+    } else if (sincos_mode == ORC_SINCOS_HOST) {
+        *a = cosf(angle);
+        *b = sinf(angle);
+    } else {
+        *a = orc_glibc_cosf(angle);
+        *b = orc_glibc_sinf(angle);
+    }
+}
+
 /* computeOrbDescriptor, ORBextractor.cc:117-157 */
 void orc_orb_descriptor(const orc_keypoint *kp, const uint8_t *img, int step, int brief_fma,
-                        uint8_t desc[32])
+                        int sincos_mode, uint8_t desc[32])
 {
     float a, b;
-    orc_pinned_sincos_deg(kp->angle, &a, &b);
+    orc_brief_sincos_deg(kp->angle, sincos_mode, &a, &b);
     const uint8_t *center = img + (size_t)cv_round_f(kp->y) * step + cv_round_f(kp->x);
     for (int i = 0; i < 32; ++i) {
         int val = 0;
@@ -926,7 +1042,8 @@ int orc_extract(const orc_params *p, const uint8_t *img, int w, int h, int step,
             if (o >= cap)
                 continue;
             if (desc)
-                orc_orb_descriptor(&lk[l][i], blur, lw[l], p->brief_fma, desc + (size_t)o * 32);
+                orc_orb_descriptor(&lk[l][i], blur, lw[l], p->brief_fma, p->sincos_mode,
+                                   desc + (size_t)o * 32);
             orc_keypoint k = lk[l][i];
             if (l != 0) {
                 const float s = p->scale[l];

@@ -77,7 +77,20 @@ typedef struct {
     int32_t resize_mode;       /* ORC_RESIZE_* */
     int32_t gauss_k[7];        /* 7-tap weights (sum 256 for the bit-exact 3.4.9+ table) */
     int32_t brief_fma;         /* 0: x*b + y*a rounded twice (default); 1: fused */
+    int32_t sincos_mode;       /* ORC_SINCOS_*: the cosf/sinf of ORBextractor.cc:122 */
 } orc_params;
+
+/* cos/sin of the rBRIEF rotation (ORBextractor.cc:121-122: (float)cos(float), i.e. glibc's
+ * cosf/sinf).  GLIBC restates glibc 2.35's flt-32 sinf/cosf (sysdeps/ieee754/flt-32/
+ * s_sinf.c, s_cosf.c, sincosf.h, its __sincosf_table) and equals the host libm for every
+ * float in [0, 7) (tools/sincosf_sweep.c); HOST calls the machine's libm (validation only);
+ * PINNED is round 1's double Cody-Waite + Taylor evaluation. */
+enum { ORC_SINCOS_GLIBC = 0, ORC_SINCOS_PINNED = 1, ORC_SINCOS_HOST = 2 };
+float orc_glibc_sinf(float y);
+float orc_glibc_cosf(float y);
+/* mismatches of orc_glibc_sinf/cosf against the linked libm over every `stride`-th float bit
+ * pattern in [lo, hi) */
+long orc_sincosf_check(uint32_t lo, uint32_t hi, uint32_t stride);
 
 /* ---- extractor ---- */
 int orc_init_params(orc_params *p, int nfeatures, float scale_factor, int nlevels,
@@ -96,8 +109,10 @@ int orc_distribute_octree(const orc_keypoint *keys, int n, int minX, int maxX, i
 float orc_fast_atan2(float y, float x);
 float orc_ic_angle(const uint8_t *img, int step, float px, float py, const int32_t umax[16]);
 void orc_pinned_sincos_deg(float angle_deg, float *c, float *s);
+/* a = cos, b = sin of angle_deg * factorPI (ORBextractor.cc:120-122) by sincos_mode */
+void orc_brief_sincos_deg(float angle_deg, int sincos_mode, float *a, float *b);
 void orc_orb_descriptor(const orc_keypoint *kp, const uint8_t *img, int step, int brief_fma,
-                        uint8_t desc[32]);
+                        int sincos_mode, uint8_t desc[32]);
 
 /* Full ORBextractor::operator() for one 8-bit image.
  * Returns the number of keypoints (>=0) or a negative error.  kps/desc may be NULL

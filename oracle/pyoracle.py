@@ -29,6 +29,8 @@ EDGE_OUT_DTYPE = np.dtype([("err", "<f8", 3), ("chi2", "<f8"), ("rho1", "<f8"),
                            ("jp", "<f8", (3, 3)), ("jt", "<f8", (3, 6)), ("hpl", "<f8", (3, 6))])
 
 RESIZE_SCALAR, RESIZE_SSE2_16_4, RESIZE_SIMD_16_8 = 0, 4, 8
+# cosf/sinf of the rBRIEF rotation (orb_oracle.h ORC_SINCOS_*)
+SINCOS_GLIBC, SINCOS_PINNED, SINCOS_HOST = 0, 1, 2
 
 # tracking matcher records (orb_oracle.h: orc_lf_point, orc_map_proj)
 MP_VALID, MP_HAS_OBS = 1, 2
@@ -44,7 +46,8 @@ class Params(C.Structure):
                 ("scale", C.c_float * MAX_LEVELS), ("inv_scale", C.c_float * MAX_LEVELS),
                 ("sigma2", C.c_float * MAX_LEVELS), ("inv_sigma2", C.c_float * MAX_LEVELS),
                 ("features_per_level", C.c_int32 * MAX_LEVELS), ("umax", C.c_int32 * 16),
-                ("resize_mode", C.c_int32), ("gauss_k", C.c_int32 * 7), ("brief_fma", C.c_int32)]
+                ("resize_mode", C.c_int32), ("gauss_k", C.c_int32 * 7), ("brief_fma", C.c_int32),
+                ("sincos_mode", C.c_int32)]
 
 
 PEDGE_DTYPE = np.dtype([("obs", "<f4", 3), ("xw", "<f4", 3), ("inv_sigma2", "<f4"),
@@ -123,6 +126,13 @@ def lib():
         L.orc_ic_angle.argtypes = [vp, C.c_int, C.c_float, C.c_float, vp]
         L.orc_ic_angle.restype = C.c_float
         L.orc_pinned_sincos_deg.argtypes = [C.c_float, P(C.c_float), P(C.c_float)]
+        L.orc_brief_sincos_deg.argtypes = [C.c_float, C.c_int, P(C.c_float), P(C.c_float)]
+        L.orc_glibc_sinf.argtypes = [C.c_float]
+        L.orc_glibc_sinf.restype = C.c_float
+        L.orc_glibc_cosf.argtypes = [C.c_float]
+        L.orc_glibc_cosf.restype = C.c_float
+        L.orc_sincosf_check.argtypes = [C.c_uint32, C.c_uint32, C.c_uint32]
+        L.orc_sincosf_check.restype = C.c_long
         L.orc_descriptor_distance.argtypes = [vp, vp]
         L.orc_knn2.argtypes = [vp, C.c_int, vp, C.c_int, vp, vp, vp]
         L.orc_search_for_initialization.argtypes = [vp, vp, C.c_int, vp, vp, C.c_int,
@@ -159,7 +169,7 @@ def _p(a):
 
 
 def params(nfeatures=2000, scale_factor=1.2, nlevels=8, ini_th_fast=20, min_th_fast=7,
-           resize_mode=RESIZE_SIMD_16_8, gauss_k=None, brief_fma=0):
+           resize_mode=RESIZE_SIMD_16_8, gauss_k=None, brief_fma=0, sincos_mode=SINCOS_GLIBC):
     p = Params()
     rc = lib().orc_init_params(C.byref(p), nfeatures, scale_factor, nlevels, ini_th_fast,
                                min_th_fast)
@@ -170,6 +180,7 @@ def params(nfeatures=2000, scale_factor=1.2, nlevels=8, ini_th_fast=20, min_th_f
         for i in range(7):
             p.gauss_k[i] = int(gauss_k[i])
     p.brief_fma = brief_fma
+    p.sincos_mode = sincos_mode
     return p
 
 
@@ -241,10 +252,25 @@ def fast_atan2(y, x):
     return lib().orc_fast_atan2(float(y), float(x))
 
 
-def sincos_deg(a):
+def sincos_deg(a, mode=SINCOS_PINNED):
+    """(cos, sin) of the rBRIEF rotation for an angle in degrees (ORBextractor.cc:120-122)."""
     c, s = C.c_float(), C.c_float()
-    lib().orc_pinned_sincos_deg(float(a), C.byref(c), C.byref(s))
+    lib().orc_brief_sincos_deg(float(a), int(mode), C.byref(c), C.byref(s))
     return c.value, s.value
+
+
+def glibc_sinf(y):
+    return lib().orc_glibc_sinf(float(y))
+
+
+def glibc_cosf(y):
+    return lib().orc_glibc_cosf(float(y))
+
+
+def sincosf_check(lo, hi, stride):
+    """Mismatches of the glibc sinf/cosf restatement against the linked libm over every
+    `stride`-th float bit pattern in [lo, hi)."""
+    return int(lib().orc_sincosf_check(int(lo), int(hi), int(stride)))
 
 
 def descriptor_distance(a, b):

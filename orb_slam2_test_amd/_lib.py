@@ -21,6 +21,7 @@ ORBG_ERANGE = -34
 ORBG_ENOTSUP = -95
 
 RESIZE_SCALAR, RESIZE_SSE2_16_4, RESIZE_SIMD_16_8 = 0, 4, 8
+SINCOS_GLIBC, SINCOS_PINNED = 0, 1
 
 # cv::KeyPoint layout (orbg_keypoint)
 KP_DTYPE = np.dtype([("x", "<f4"), ("y", "<f4"), ("size", "<f4"), ("angle", "<f4"),
@@ -82,7 +83,7 @@ class Params(C.Structure):
     _fields_ = [("nfeatures", C.c_int32), ("scale_factor", C.c_float), ("nlevels", C.c_int32),
                 ("ini_th_fast", C.c_int32), ("min_th_fast", C.c_int32),
                 ("resize_mode", C.c_int32), ("gauss_k", C.c_int32 * 7),
-                ("brief_fma", C.c_int32), ("max_batch", C.c_int32)]
+                ("brief_fma", C.c_int32), ("max_batch", C.c_int32), ("sincos_mode", C.c_int32)]
 
 
 class Bounds(C.Structure):
@@ -135,6 +136,7 @@ def lib():
         "orbg_match_outputs": (i32, [vp, P(vp), P(vp), P(vp), P(C.c_int32)]),
         "orbg_download_matches": (i32, [vp, i32, vp, vp, i32, vp]),
         "orbg_sync": (i32, [vp]),
+        "orbg_check_errors": (i32, [vp]),
         "orbg_stream": (vp, [vp]),
         "orbg_set_stream": (i32, [vp, vp]),
         "orbg_batch_summary": (i32, [vp, vp]),
@@ -253,7 +255,13 @@ class Context:
         return out
 
     def sync(self):
+        """Drain the context's streams; raises OrbgError(ORBG_ENOTSUP) if a batch since the
+        last check overflowed a quadtree capacity (sticky device flag)."""
         check(self._L.orbg_sync(self.handle), "orbg_sync")
+
+    def check_errors(self):
+        """Same check as sync(): read and clear the sticky device error flag."""
+        check(self._L.orbg_check_errors(self.handle), "orbg_check_errors")
 
     def set_stream(self, stream_ptr):
         """Launch on a caller-owned hipStream_t (int pointer) or the own stream (None)."""

@@ -542,6 +542,7 @@ __global__ __launch_bounds__(OCT_T) void k_octree_lds(
     if (S.s_err) {
         if (tid == 0) {
             atomicOr(err_flag, 1 << S.s_err);
+            atomicMin(err_flag + 1, f);
             lvl_cnt[(int64_t)f * g->L + l] = 0;
         }
         return;
@@ -576,7 +577,10 @@ __global__ __launch_bounds__(OCT_T) void k_octree_lds(
     for (int i = tid; i < nout; i += OCT_T) out[i] = kglob[0xFFFFFFu - (best[i] & 0xFFFFFFu)];
     if (tid == 0) {
         lvl_cnt[(int64_t)f * g->L + l] = nout;
-        if (alive > lv.out_cap) atomicOr(err_flag, 1 << 8);
+        if (alive > lv.out_cap) {
+            atomicOr(err_flag, 1 << 8);
+            atomicMin(err_flag + 1, f);
+        }
     }
 }
 

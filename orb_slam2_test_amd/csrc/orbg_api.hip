@@ -34,6 +34,13 @@ __global__ void k_octree(const OrbgGeom *, const int32_t *, const uint2 *, uint3
                          int32_t *);
 __global__ void k_octree_lds(const OrbgGeom *, const int32_t *, const uint2 *, uint32_t *,
                              uint32_t *, uint32_t *, int32_t *, int32_t *, OctLdsDims);
+// fast_kernels.hip
+bool fast2_pitch_ok(int p4);
+hipError_t launch_fast2(int p4, dim3 grid, size_t lds, hipStream_t st, const OrbgGeom *g,
+                        const OrbgCell *cells, const uint8_t *img0, int64_t img_fs,
+                        int img_pitch, const uint8_t *pyr, const uint32_t *ctab,
+                        int32_t *cell_cnt, uint2 *cell_kp, int nframes, int c_begin,
+                        int c_count);
 struct OrbgKeypointDev;
 __global__ void k_orient_desc(const OrbgGeom *, const uint8_t *, int64_t, int, const uint8_t *,
                               const uint8_t *, const uint4 *, const uint32_t *, const int32_t *,
@@ -199,6 +206,7 @@ struct orbg_ctx {
     int oct_mode = 0;
     int blur0_mode = 0;  // measured: 2.013 vs 2.025 ms per 256 frames with it on
     int fast0_mode = 1;  // level-0 FAST cells on `ostream` beside the resize chain (ORBG_FAST0)
+    int fast_v2 = 1;     // k_fast2 (fast_kernels.hip) where its pitch fits, else k_fast_cells (ORBG_FAST_V=1)
     hipEvent_t ev_fork[2] = {nullptr, nullptr}, ev_join[2] = {nullptr, nullptr};
     // Batch matching and the trajectory summary run on `mstream`, so the matching of batch k
     // overlaps the extraction of batch k+1 on `stream`.  The per-frame outputs (kps, desc,
@@ -284,6 +292,7 @@ extern "C" void orbg_params_default(orbg_params *p)
     memcpy(p->gauss_k, k, sizeof(k));
     p->brief_fma = 0;
     p->max_batch = 1;
+    p->sincos_mode = ORBG_SINCOS_GLIBC;
 }
 
 static int cv_round_f(float v) { return (int)lrintf(v); }
@@ -378,6 +387,8 @@ static void free_plan(orbg_ctx *c)
     c->d_snvalid = nullptr;
     c->d_sscr = nullptr;
     c->stereo_cap = c->last_nstereo = 0;
+    c->last_npairs = 0;
+    c->last_n = 0;
     c->h_pairs.clear();
     c->gw = c->gh = c->gbatch = 0;
 }
@@ -432,6 +443,7 @@ static int plan(orbg_ctx *c, int w, int h, int batch)
     G.ini_th = std::min(std::max(p.ini_th_fast, 0), 255);
     G.min_th = std::min(std::max(p.min_th_fast, 0), 255);
     G.brief_fma = p.brief_fma;
+    G.sincos_mode = p.sincos_mode;
     G.dbg = getenv("ORBG_DBG") ? atoi(getenv("ORBG_DBG")) : 0;
     for (int i = 0; i < 7; i++) G.gk[i] = p.gauss_k[i];
     for (int i = 0; i < 16; i++) G.umax[i] = c->umax[i];
@@ -674,6 +686,40 @@ static int plan(orbg_ctx *c, int w, int h, int batch)
         if (4 * G.fc_wave_bytes > 64 * 1024)
             return set_err(ORBG_ENOTSUP, "FAST cell %dx%d needs %d LDS bytes per wave", wmax,
                            hmax, G.fc_wave_bytes);
+        // k_fast2 (fast_kernels.hip): compile-time pitch P4 >= 4 * ceil((RG + 3) / 4) (its
+        // 16-byte window chunks), picked among the instantiated ones by the same bank-spread
+        // cost; layout tA | tB (hmax rows each) | scores (hmax - 4 rows) | list (4 entries per
+        // unit: two pixel pairs x two sides)
+        G.fc2_p4 = 0;
+        if (c->fast_v2) {
+            const int need = 4 * ((rg + 3 + 3) / 4);
+            int best_c = 1 << 30;
+            for (int wd = need; wd <= 32; wd++) {
+                if (!fast2_pitch_ok(wd)) continue;
+                int cost = 0;
+                for (int r : rgs)
+                    for (int k = 0; k < 3; k++) {
+                        int hist[64] = {0}, mx = 0;
+                        for (int lane = 0; lane < 64; lane++) {
+                            const int b = ((lane / r) * wd + lane % r + k) & 63;
+                            mx = std::max(mx, ++hist[b]);
+                        }
+                        cost += mx;
+                    }
+                if (cost < best_c) {
+                    best_c = cost;
+                    G.fc2_p4 = wd;
+                }
+            }
+            if (G.fc2_p4) {
+                const int P2 = 4 * G.fc2_p4;
+                G.fc2_tileb_off = hmax * P2;
+                G.fc2_sc_off = 2 * hmax * P2;
+                G.fc2_list_off = G.fc2_sc_off + (std::max(hmax - 6, 0) + 2) * P2;
+                G.fc2_wave_bytes = (G.fc2_list_off + 8 * max_units + 15) & ~15;
+                if (4 * G.fc2_wave_bytes > 160 * 1024) G.fc2_p4 = 0;
+            }
+        }
     }
     for (int l = 0; l < G.L; l++) {
         G.lv[l].key_off = key_off;
@@ -752,9 +798,15 @@ static int plan(orbg_ctx *c, int w, int h, int batch)
         (rc = dalloc(&c->desc_slot[0], B * G.frame_cap * 32)) ||
         (rc = dalloc(&c->desc_slot[1], B * G.frame_cap * 32)) ||
         (rc = dalloc(&c->counts_slot[0], B)) || (rc = dalloc(&c->counts_slot[1], B)) ||
-        (rc = dalloc(&c->d_err, 1))) {
+        (rc = dalloc(&c->d_err, 2))) {
         free_plan(c);
         return rc;
+    }
+    {
+        // sticky device error word {flags, first failing frame}: OR of every batch since it
+        // was last read (check_err), so a pipelined caller cannot lose an overflow
+        const int32_t e0[2] = {0, INT32_MAX};
+        HIPCHK(hipMemcpy(c->d_err, e0, sizeof(e0), hipMemcpyHostToDevice));
     }
     // resize tables are referenced by offset: fix up pointers through offsets at launch
     HIPCHK(hipMemcpy(c->d_geom, &G, sizeof(G), hipMemcpyHostToDevice));
@@ -814,6 +866,8 @@ extern "C" int orbg_create(int device, const orbg_params *p, orbg_ctx **out)
         memcpy(prm.gauss_k, k, sizeof(k));
     }
     if (prm.max_batch < 1) prm.max_batch = 1;
+    if (prm.sincos_mode != ORBG_SINCOS_GLIBC && prm.sincos_mode != ORBG_SINCOS_PINNED)
+        return set_err(ORBG_EINVAL, "sincos_mode %d", prm.sincos_mode);
     int ndev = 0;
     if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0)
         return set_err(ORBG_EIO, "no HIP device visible (liborbg has no CPU fallback)");
@@ -850,6 +904,8 @@ extern "C" int orbg_create(int device, const orbg_params *p, orbg_ctx **out)
         c->oct_mode = e ? atoi(e) : 1;
         const char *f0 = getenv("ORBG_FAST0");
         c->fast0_mode = f0 ? atoi(f0) : 1;
+        const char *fv = getenv("ORBG_FAST_V");
+        c->fast_v2 = fv ? (atoi(fv) >= 2) : 1;
         const char *b0 = getenv("ORBG_BLUR0");
         c->blur0_mode = b0 ? atoi(b0) : 0;
         if (c->oct_mode &&
@@ -944,7 +1000,10 @@ static int launch_extract(orbg_ctx *c, const uint8_t *d_imgs, int B, int pitch, 
 {
     const OrbgGeom &G = c->geom;
     hipStream_t st = c->stream;
-    HIPCHK(hipMemsetAsync(c->d_err, 0, sizeof(int32_t), st));
+    // the match / stereo outputs of the previous batch are stale from here on
+    c->last_npairs = 0;
+    c->last_nstereo = 0;
+    // d_err is not cleared here: it is sticky until check_err reads it
     // fast0: the level-0 FAST cells and quadtree need only the input images, so they run on
     // the quadtree stream beside the resize chain (latency-bound small launches)
     const bool fast0 = c->fast0_mode && c->oct_mode && G.L > 1;
@@ -953,6 +1012,14 @@ static int launch_extract(orbg_ctx *c, const uint8_t *d_imgs, int B, int pitch, 
     const bool blur0 = fast0 && c->blur0_mode;
     const int tb1 = c->tile_base[1], tb0 = blur0 ? tb1 : 0;
     auto launch_fast = [&](hipStream_t st, int cb, int cn) {
+        if (G.fc2_p4) {
+            hipError_t e = hipSuccess;
+            PROF_LAUNCH(c, "fast_cells",
+                        e = launch_fast2(G.fc2_p4, dim3((cn * B + 3) / 4), 4 * G.fc2_wave_bytes, st,
+                                         c->d_geom, c->d_cells, d_imgs, fs, pitch, c->d_pyr,
+                                         c->d_ctab, c->d_cell_cnt, c->d_cell_kp, B, cb, cn));
+            return e;
+        }
         PROF_LAUNCH(c, "fast_cells",
                     hipLaunchKernelGGL(k_fast_cells, dim3((cn * B + 3) / 4), dim3(256),
                                        4 * G.fc_wave_bytes, st, c->d_geom, c->d_cells, d_imgs,
@@ -1065,15 +1132,30 @@ static int sync_all(orbg_ctx *c)
     return ORBG_OK;
 }
 
+// Drains every stream, then reads and clears the sticky device error word: a non-zero flag
+// means some frame since the last read lost a level (quadtree capacity exceeded) and its
+// keypoints are incomplete, so the caller gets ORBG_ENOTSUP instead of short outputs.
 static int check_err(orbg_ctx *c)
 {
-    int32_t e = 0;
-    HIPCHK(hipMemcpyAsync(&e, c->d_err, sizeof(e), hipMemcpyDeviceToHost, c->stream));
     int rc = sync_all(c);
     if (rc) return rc;
     c->prof.collect();
-    if (e) return set_err(ORBG_ENOTSUP, "quadtree capacity exceeded (flags 0x%x)", e);
+    if (!c->d_err) return ORBG_OK;
+    int32_t e[2] = {0, 0};
+    HIPCHK(hipMemcpy(e, c->d_err, sizeof(e), hipMemcpyDeviceToHost));
+    if (e[0]) {
+        const int32_t e0[2] = {0, INT32_MAX};
+        HIPCHK(hipMemcpy(c->d_err, e0, sizeof(e0), hipMemcpyHostToDevice));
+        return set_err(ORBG_ENOTSUP, "quadtree capacity exceeded (flags 0x%x, first frame %d of "
+                                     "a batch since the last check)", e[0], e[1]);
+    }
     return ORBG_OK;
+}
+
+extern "C" int orbg_check_errors(orbg_ctx *c)
+{
+    if (!c) return set_err(ORBG_EINVAL, "ctx is NULL");
+    return check_err(c);
 }
 
 extern "C" int orbg_extract_batch_device(orbg_ctx *c, const uint8_t *d_imgs, int nframes, int w,
@@ -1170,10 +1252,7 @@ extern "C" int orbg_get_level(orbg_ctx *c, int frame, int level, uint8_t *dst, s
 extern "C" int orbg_sync(orbg_ctx *c)
 {
     if (!c) return set_err(ORBG_EINVAL, "ctx is NULL");
-    int rc = sync_all(c);
-    if (rc) return rc;
-    c->prof.collect();
-    return ORBG_OK;
+    return check_err(c);  // drains the streams and surfaces any device error flag
 }
 
 extern "C" void *orbg_stream(orbg_ctx *c) { return c ? (void *)c->stream : nullptr; }
@@ -1193,7 +1272,7 @@ extern "C" int orbg_set_stream(orbg_ctx *c, void *stream)
 extern "C" int orbg_batch_stats(orbg_ctx *c, int64_t *ncand, int64_t *nkp)
 {
     if (!c || !c->gw || c->last_n <= 0) return set_err(ORBG_EINVAL, "no batch");
-    int rc = sync_all(c);
+    int rc = check_err(c);
     if (rc) return rc;
     std::vector<int32_t> cc((size_t)c->last_n * c->geom.ncells), kc(c->last_n);
     HIPCHK(hipMemcpy(cc.data(), c->d_cell_cnt, cc.size() * 4, hipMemcpyDeviceToHost));

@@ -107,4 +107,63 @@ __device__ __forceinline__ void pinned_sincos(double x, double *s, double *c)
     }
 }
 
+// glibc 2.35 sinf / cosf (sysdeps/ieee754/flt-32/s_sinf.c, s_cosf.c, sincosf.h and its
+// __sincosf_table) for |y| < 120 -- the rBRIEF rotation's (float)cos(angle) /
+// (float)sin(angle) (ORBextractor.cc:122) resolve to these.  Same restatement as
+// oracle/orb_oracle.c orc_glibc_sinf/cosf; both equal the host libm for every float in
+// [0, 7) (tools/sincosf_sweep.c).  Double arithmetic, unfused (-ffp-contract=off; the
+// fused x86_64 build rounds to the same floats on that range), one rounding to float.
+static __constant__ const double orbg_sincosf_tab[2][14] = {
+    {1.0, -1.0, -1.0, 1.0, 0x1.45f306dc9c883p+23, 0x1.921fb54442d18p+0, 1.0,
+     -0x1.ffffffd0c621cp-2, -0x1.555545995a603p-3, 0x1.55553e1068f19p-5, 0x1.1107605230bc4p-7,
+     -0x1.6c087e89a359dp-10, -0x1.994eb3774cf24p-13, 0x1.99343027bf8c3p-16},
+    {1.0, -1.0, -1.0, 1.0, 0x1.45f306dc9c883p+23, 0x1.921fb54442d18p+0, -1.0,
+     0x1.ffffffd0c621cp-2, -0x1.555545995a603p-3, -0x1.55553e1068f19p-5, 0x1.1107605230bc4p-7,
+     0x1.6c087e89a359dp-10, -0x1.994eb3774cf24p-13, -0x1.99343027bf8c3p-16}};
+
+// sinf_poly: sine polynomial for even n, cosine for odd n
+__device__ __forceinline__ float glibc_sincosf_poly(double x, double x2, const double *p, int n)
+{
+    if ((n & 1) == 0) {
+        const double x3 = x * x2;
+        const double s1 = p[10] + x2 * p[12];  // s2 + x2 * s3
+        const double x7 = x3 * x2;
+        const double s = x + x3 * p[8];        // x + x3 * s1
+        return (float)(s + x7 * s1);
+    }
+    const double x4 = x2 * x2;
+    const double c2 = p[11] + x2 * p[13];      // c3 + x2 * c4
+    const double c1 = p[6] + x2 * p[7];        // c0 + x2 * c1
+    const double x6 = x4 * x2;
+    const double c = c1 + x4 * p[9];           // c1 + x4 * c2
+    return (float)(c + x6 * c2);
+}
+
+// *c = cosf(y), *s = sinf(y) as glibc computes them (quadrant reduction shared)
+__device__ __forceinline__ void glibc_sincosf(float y, float *s, float *c)
+{
+    const uint32_t top = (__float_as_uint(y) >> 20) & 0x7ff;
+    double x = y;
+    if (top < 0x3f4) {            // abstop12(y) < abstop12(pio4)
+        if (top < 0x398) {        // < abstop12(0x1p-12f)
+            *s = y;
+            *c = 1.0f;
+            return;
+        }
+        const double x2 = x * x;
+        *s = glibc_sincosf_poly(x, x2, orbg_sincosf_tab[0], 0);
+        *c = glibc_sincosf_poly(x, x2, orbg_sincosf_tab[0], 1);
+        return;
+    }
+    // reduce_fast without TOINT_INTRINSICS: quadrant from the 2^24-scaled product
+    const double r = x * orbg_sincosf_tab[0][4];
+    const int n = ((int32_t)r + 0x800000) >> 24;
+    x = x - n * orbg_sincosf_tab[0][5];
+    const double sg = orbg_sincosf_tab[0][n & 3];
+    const double *p = orbg_sincosf_tab[(n & 2) ? 1 : 0];
+    const double xs = x * sg, x2 = x * x;
+    *s = glibc_sincosf_poly(xs, x2, p, n);
+    *c = glibc_sincosf_poly(xs, x2, p, n ^ 1);
+}
+
 }  // namespace orbg

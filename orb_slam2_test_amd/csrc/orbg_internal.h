@@ -72,11 +72,15 @@ struct OrbgGeom {
     int32_t frame_cap;            // max keypoints per frame (final)
     int32_t ini_th, min_th;
     int32_t brief_fma;
+    int32_t sincos_mode;          // rBRIEF cos/sin: 0 glibc cosf/sinf restated, 1 pinned double
     int32_t dbg;                  // developer timing knob (ORBG_DBG env), 0 in production
     int32_t fc_pitch;             // k_fast_cells LDS row pitch (bytes)
     int32_t fc_tile_rows;         // max FAST window height
     int32_t fc_wave_bytes;        // LDS bytes per wave (window + score tiles + unit list)
     int32_t fc_list_off;          // byte offset of the pretest unit list in a wave's LDS
+    int32_t fc2_p4;               // k_fast2 LDS row pitch (dwords, a template instance; 0: k_fast_cells)
+    int32_t fc2_wave_bytes;       // k_fast2 LDS bytes per wave
+    int32_t fc2_tileb_off, fc2_sc_off, fc2_list_off;  // k_fast2 regions within a wave's LDS
     int32_t gk[7];
     int64_t pyr_frame;            // bytes per frame of d_pyr
     int64_t blur_frame;

@@ -2,7 +2,7 @@
 // computeOrbDescriptor (:117-157) and the output assembly of ORBextractor::operator()
 // (:1381-1395) as one batched HIP kernel for gfx950.
 // Bit-exactness pins: no FMA contraction (-ffp-contract=off + pragma),
-// cvRound = round-half-even, fastAtan2 polynomial, pinned double sincos.
+// cvRound = round-half-even, fastAtan2 polynomial, glibc cosf/sinf restated (orbg_device.h).
 #include <hip/hip_runtime.h>
 
 #include "orbg_internal.h"
@@ -208,9 +208,15 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(ORBG_OD_WPE
     // keypoint record (:1115-1122, :1387-1393), lane j for slot j ----
     const float factorPI = (float)(3.14159265358979323846 / 180.f);
     const float angle_l = fast_atan2((float)M01, (float)M10);
-    double sd, cd;
-    pinned_sincos((double)(angle_l * factorPI), &sd, &cd);
-    const float a_l = (float)cd, b_l = (float)sd;
+    float a_l, b_l;
+    if (g->sincos_mode == 0) {  // glibc cosf / sinf (the reference's libm), default
+        glibc_sincosf(angle_l * factorPI, &b_l, &a_l);
+    } else {                    // round 1's correctly rounded double evaluation
+        double sd, cd;
+        pinned_sincos((double)(angle_l * factorPI), &sd, &cd);
+        a_l = (float)cd;
+        b_l = (float)sd;
+    }
     if (my_ok) {
         const OrbgLevel &lv = g->lv[my_lev];
         OrbgKeypointDev kp;

