@@ -123,6 +123,9 @@ def main():
     ap.add_argument("--cpu-frames", type=int, default=0, help="0: 256 x threads (~10-20 s)")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-kernel-timing", action="store_true")
+    ap.add_argument("--pipeline", type=int, default=int(os.environ.get("ORBG_PIPELINE", "1")),
+                    help="1: pipelined batches (image half of step k+1 beside the keypoint half "
+                         "of step k, orbg_set_pipeline); 0: one batch after the other")
     ap.add_argument("--stereo", action="store_true",
                     help="configs[3]: stereo frames (extract L+R + ComputeStereoMatches)")
     args = ap.parse_args()
@@ -154,6 +157,7 @@ def main():
     stream = torch.cuda.Stream()
     torch.cuda.set_stream(stream)
     ext.ctx.set_stream(stream.cuda_stream)
+    ext.ctx.set_pipeline(bool(args.pipeline))
     f1 = ((np.arange(B) - 1) % B).astype(np.int32)
     f2 = np.arange(B, dtype=np.int32)
     summary = torch.zeros(2 * B, dtype=torch.int32, device="cuda")
@@ -262,6 +266,7 @@ def main():
             "config": {
                 "workload": workload,
                 "frames_per_gpu_per_step": B, "global_batch": B * world, "width": W,
+                "pipelined_batches": bool(args.pipeline),
                 "height": H, "nfeatures": NFEAT, "nlevels": NLEV,
                 "parallelism": "frames sharded over %d GPU(s), RCCL all_gather of per-frame "
                                "summary" % world},

@@ -203,6 +203,18 @@ void *orbg_match_stream(orbg_ctx *ctx); /* hipStream_t of batch matching and the
 /* launch on a caller-owned hipStream_t (e.g. torch's current stream) instead of the
  * context's own; NULL restores the context stream */
 int orbg_set_stream(orbg_ctx *ctx, void *stream);
+/* Pipelined batches (batched-sequence mode; no reference counterpart -- the reference
+ * extracts one frame per Tracking call): with enable != 0 the image half of a batch
+ * (pyramid, FAST cells, GaussianBlur) runs on the context stream and its keypoint half
+ * (quadtree, orientation + rBRIEF, stereo) on an internal high-priority stream, so the image
+ * half of batch k+1 overlaps the keypoint half of batch k.  Outputs, the batch's errors and
+ * the summary are unchanged; the per-frame outputs of a batch are complete when the match
+ * stream's work on them is (orbg_match_batch_device / orbg_batch_summary order themselves
+ * after it) or after orbg_sync.  The batch's input images must stay unchanged until then.
+ * Also selected with the environment variable ORBG_PIPELINE=1 at orbg_create.
+ * Synchronises.  ORBG_ENOTSUP without the internal stream. */
+int orbg_set_pipeline(orbg_ctx *ctx, int enable);
+int orbg_get_pipeline(const orbg_ctx *ctx);
 /* per-frame trajectory summary of the last batch, written on the match stream into a
  * device buffer (order readers after orbg_match_stream, or orbg_sync): d_out[f] = keypoints of frame f (f < nframes), then
  * d_out[nframes + p] = SearchForInitialization matches of pair p (p < npairs of the last

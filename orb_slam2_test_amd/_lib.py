@@ -139,6 +139,8 @@ def lib():
         "orbg_check_errors": (i32, [vp]),
         "orbg_stream": (vp, [vp]),
         "orbg_set_stream": (i32, [vp, vp]),
+        "orbg_set_pipeline": (i32, [vp, i32]),
+        "orbg_get_pipeline": (i32, [vp]),
         "orbg_batch_summary": (i32, [vp, vp]),
         "orbg_stereo_batch_device": (i32, [vp, vp, vp, i32, f32, f32]),
         "orbg_stereo_outputs": (i32, [vp, vp, vp, vp, vp]),
@@ -267,6 +269,15 @@ class Context:
         """Launch on a caller-owned hipStream_t (int pointer) or the own stream (None)."""
         check(self._L.orbg_set_stream(self.handle, C.c_void_p(stream_ptr) if stream_ptr else None),
               "orbg_set_stream")
+
+    def set_pipeline(self, enable=True):
+        """Pipelined batches: the image half of batch k+1 beside the keypoint half of batch k
+        (orbg_set_pipeline; the batch's input images must stay unchanged until its outputs
+        are complete)."""
+        check(self._L.orbg_set_pipeline(self.handle, 1 if enable else 0), "orbg_set_pipeline")
+
+    def pipelined(self):
+        return bool(self._L.orbg_get_pipeline(self.handle))
 
     def batch_stats(self):
         a, b = C.c_int64(), C.c_int64()

@@ -669,10 +669,11 @@ __global__ __launch_bounds__(256) void k_blur(const OrbgGeom *__restrict__ g,
                 const uint8_t *row = src + (int64_t)y * pitch;
                 const int x0 = tx0 - 4 + 16 * c;
                 if (x0 >= 0 && x0 + 20 <= W) {
-                    const uintptr_t a = (uintptr_t)(row + x0);
-                    const uint32_t *aw = (const uint32_t *)(a & ~(uintptr_t)3);
+                    // pointer arithmetic (not an integer round trip): global_, not flat_, loads
+                    const uint8_t *pa = row + x0;
+                    sh[k] = (uint32_t)((uintptr_t)pa & 3);
+                    const uint32_t *aw = (const uint32_t *)(pa - sh[k]);
                     q[k] = *(const uint4 *)aw;
-                    sh[k] = (uint32_t)(a & 3);
                     if (sh[k]) q4[k] = aw[4];
                 } else {
                     sh[k] = 4u;  // image-edge chunk: gathered byte-wise in store_band

@@ -37,6 +37,14 @@ namespace orbg {
 //                 sit where pixels 0-1 sit in tA
 //   sc [RH+2][P]  u8 scores at sc[ry + 1][4 + 4gg + i], zero border
 //   list u16      pretest survivors: ry << 8 | gg << 2 | half << 1 | dark
+#define FC2_CPW 2  // consecutive cells per wave (shared halo lines in L1, fewer workgroups)
+
+// one cell, wave-uniform (scalar registers)
+struct Fc2Cell {
+    const uint8_t *base;  // window top-left
+    int pitch, f, c, W, H, RW, RH, RG, nunits, xo, yo, NC, nch, xs, ys;
+};
+
 template <int P4>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4, 8))) void k_fast2(
     const OrbgGeom *__restrict__ g, const OrbgCell *__restrict__ cells,
@@ -52,74 +60,101 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4, 8))) voi
     uint8_t *tB = tA + g->fc2_tileb_off;
     uint8_t *sc = tA + g->fc2_sc_off;
     uint16_t *list = (uint16_t *)(tA + g->fc2_list_off);
-    // wave-uniform cell record through the scalar cache (as k_fast_cells)
-    const int cid = __builtin_amdgcn_readfirstlane(xcd_remap(blockIdx.x, gridDim.x) * 4 + wv);
-    if (cid >= c_count * nframes) return;  // wave-uniform; no workgroup barrier below
-    const int f = cid / c_count, c = c_begin + cid - f * c_count;
-    const uint4 cw4 = ((const uint4 *)cells)[c];
-    const uint32_t cw0 = __builtin_amdgcn_readfirstlane(cw4.x);
-    const uint32_t cw1 = __builtin_amdgcn_readfirstlane(cw4.y);
-    const uint32_t cw2 = __builtin_amdgcn_readfirstlane(cw4.z);
-    const int x0 = (int)(int16_t)(cw1 & 0xFFFF), y0 = (int)(int16_t)(cw1 >> 16);
-    const int l = (int)(int16_t)(cw0 & 0xFFFF);
-    const int W = (int)(int16_t)(cw2 & 0xFFFF), H = (int)(int16_t)(cw2 >> 16);
-    const uint8_t *base;
-    int pitch;
-    if (l == 0) {
-        base = img0 + f * img_fs;
-        pitch = img_pitch;
-    } else {
-        base = pyr + f * g->pyr_frame + g->lv[l].pyr_off;
-        pitch = g->lv[l].pitch;
-    }
-    base += (int64_t)y0 * pitch + x0;
-    const int RW = W - 6, RH = H - 6;
-    const int RG = RW > 0 ? (RW + 3) >> 2 : 0;
-    const int nunits = RH > 0 ? RH * RG : 0;
-    // quadtree path codes of this cell's columns / rows (one per lane), issued early
-    const int xo = x0 - ORBG_MIN_BORDER + 3, yo = y0 - ORBG_MIN_BORDER + 3;
-    const uint32_t xs_l = lane < RW ? ctab[g->lv[l].xs_off + xo + lane] : 0u;
-    const uint32_t ys_l = lane < RH ? ctab[g->lv[l].ys_off + yo + lane] : 0u;
+    const int total = c_count * nframes;
+    // FC2_CPW consecutive cells per wave (neighbours: shared halo lines in L1 / L2)
+    const int cid0 =
+        __builtin_amdgcn_readfirstlane((xcd_remap(blockIdx.x, gridDim.x) * 4 + wv) * FC2_CPW);
+    if (cid0 >= total) return;  // wave-uniform; no workgroup barrier below
 
-    // ---- window -> tA / tB: lane = (row, 16-byte chunk); chunk cc is tile dwords 4cc ..
-    // 4cc+3, window bytes 16cc-1 .. 16cc+14, loaded as 6 aligned dwords + v_alignbyte (the
-    // window sits >= 13 px inside the level, every row has >= 16 rows below it, so the
-    // aligned over-read stays inside the image) ----
+    // cell record + level geometry through the scalar cache
+    auto decode = [&](int cid) {
+        Fc2Cell k;
+        k.f = cid / c_count;
+        k.c = c_begin + cid - k.f * c_count;
+        const uint4 cw4 = ((const uint4 *)cells)[k.c];
+        const uint32_t cw0 = __builtin_amdgcn_readfirstlane(cw4.x);
+        const uint32_t cw1 = __builtin_amdgcn_readfirstlane(cw4.y);
+        const uint32_t cw2 = __builtin_amdgcn_readfirstlane(cw4.z);
+        const int x0 = (int)(int16_t)(cw1 & 0xFFFF), y0 = (int)(int16_t)(cw1 >> 16);
+        const int l = (int)(int16_t)(cw0 & 0xFFFF);
+        k.W = (int)(int16_t)(cw2 & 0xFFFF);
+        k.H = (int)(int16_t)(cw2 >> 16);
+        if (l == 0) {
+            k.base = img0 + k.f * img_fs;
+            k.pitch = img_pitch;
+        } else {
+            k.base = pyr + k.f * g->pyr_frame + g->lv[l].pyr_off;
+            k.pitch = g->lv[l].pitch;
+        }
+        k.base += (int64_t)y0 * k.pitch + x0;
+        k.RW = k.W - 6;
+        k.RH = k.H - 6;
+        k.RG = k.RW > 0 ? (k.RW + 3) >> 2 : 0;
+        k.nunits = k.RH > 0 ? k.RH * k.RG : 0;
+        k.xo = x0 - ORBG_MIN_BORDER + 3;
+        k.yo = y0 - ORBG_MIN_BORDER + 3;
+        k.xs = g->lv[l].xs_off + k.xo;
+        k.ys = g->lv[l].ys_off + k.yo;
+        k.NC = (k.RG + 3 + 3) >> 2;  // tile dwords 0 .. RG+2 (tB needs tA dword RG+2)
+        k.nch = k.H * k.NC;
+        return k;
+    };
+    // Window chunk i = (row r, chunk cc): tile dwords 4cc .. 4cc+3 = window bytes 16cc-1 ..
+    // 16cc+14, from 6 aligned dwords + v_alignbyte.  The window sits >= 13 px inside the level
+    // and every row has >= 16 rows below it, so the aligned over-read stays in the image.
+    auto chunk_src = [&](const Fc2Cell &k, int i, uint32_t &sh) {
+        const int mdiv = (65536 + k.NC - 1) / k.NC;  // i / NC == (i * mdiv) >> 16, i < 1024
+        const int r = (i * mdiv) >> 16, cc = i - r * k.NC;
+        // pointer arithmetic (no integer round trip): global_, not flat_, loads
+        const uint8_t *src = k.base + (int64_t)r * k.pitch + 16 * cc - 1;
+        sh = (uint32_t)((uintptr_t)src & 3u);
+        return (const uint32_t *)(src - sh);
+    };
+    auto put = [&](const Fc2Cell &k, int i, uint4 q, uint2 q2, uint32_t sh) {
+        const int mdiv = (65536 + k.NC - 1) / k.NC;
+        const int r = (i * mdiv) >> 16, cc = i - r * k.NC;
+        const int to = r * P + 16 * cc;
+        const uint32_t d[6] = {q.x, q.y, q.z, q.w, q2.x, q2.y};
+        uint32_t A[5], Bw[4];
+#pragma unroll
+        for (int j = 0; j < 5; j++) A[j] = __builtin_amdgcn_alignbyte(d[j + 1], d[j], sh);
+#pragma unroll
+        for (int j = 0; j < 4; j++) Bw[j] = __builtin_amdgcn_alignbyte(A[j + 1], A[j], 2);
+        *(uint2 *)(tA + to) = make_uint2(A[0], A[1]);
+        *(uint2 *)(tA + to + 8) = make_uint2(A[2], A[3]);
+        *(uint2 *)(tB + to) = make_uint2(Bw[0], Bw[1]);
+        *(uint2 *)(tB + to + 8) = make_uint2(Bw[2], Bw[3]);
+    };
+
+#pragma unroll 1
+    for (int kc = 0; kc < FC2_CPW; kc++) {
+    const int cid = cid0 + kc;
+    if (cid >= total) break;  // wave-uniform
+    const Fc2Cell cur = decode(cid);
+    const int f = cur.f, c = cur.c, RW = cur.RW, RH = cur.RH, RG = cur.RG, nunits = cur.nunits;
+    const int xo = cur.xo, yo = cur.yo;
+    // quadtree path codes of the cell's columns / rows (one per lane), issued early
+    const uint32_t xs_l = lane < RW ? ctab[cur.xs + lane] : 0u;
+    const uint32_t ys_l = lane < RH ? ctab[cur.ys + lane] : 0u;
+    // ---- window -> tA / tB: all of a lane's chunk loads in flight before the first store
+    // (the previous cell's reads of the tiles are done: a wave's LDS ops complete in order) ----
+    wave_sync_lds();
     {
-        const int NC = (RG + 3 + 3) >> 2;     // tile dwords 0 .. RG+2 (tB needs tA dword RG+2)
-        const int nch = H * NC;
-        const int mdiv = (65536 + NC - 1) / NC;  // i / NC == (i * mdiv) >> 16 for i < 1024
-        for (int i0 = 0; i0 < nch; i0 += 128) {
+        for (int i0 = 0; i0 < cur.nch; i0 += 2 * 64) {
             uint4 q[2];
             uint2 q2[2];
             uint32_t sh[2];
-            int to[2];
 #pragma unroll
-            for (int k = 0; k < 2; k++) {
-                const int i = i0 + 64 * k + lane;
-                const bool ok = i < nch;
-                const int ii = ok ? i : 0;  // unconditional loads: all four in flight
-                const int r = (ii * mdiv) >> 16, cc = ii - r * NC;
-                const uintptr_t a = (uintptr_t)(base + (int64_t)r * pitch + 16 * cc - 1);
-                sh[k] = (uint32_t)(a & 3u);
-                const uint32_t *aw = (const uint32_t *)(a - sh[k]);
-                q[k] = *(const uint4 *)aw;
-                q2[k] = *(const uint2 *)(aw + 4);
-                to[k] = ok ? r * P + 16 * cc : -1;
+            for (int u = 0; u < 2; u++) {
+                const int i = i0 + 64 * u + lane;
+                const uint32_t *aw = chunk_src(cur, i < cur.nch ? i : 0, sh[u]);
+                q[u] = *(const uint4 *)aw;  // unconditional: both in flight
+                q2[u] = *(const uint2 *)(aw + 4);
             }
 #pragma unroll
-            for (int k = 0; k < 2; k++) {
-                if (to[k] < 0) continue;
-                const uint32_t d[6] = {q[k].x, q[k].y, q[k].z, q[k].w, q2[k].x, q2[k].y};
-                uint32_t A[5], Bw[4];
-#pragma unroll
-                for (int j = 0; j < 5; j++) A[j] = __builtin_amdgcn_alignbyte(d[j + 1], d[j], sh[k]);
-#pragma unroll
-                for (int j = 0; j < 4; j++) Bw[j] = __builtin_amdgcn_alignbyte(A[j + 1], A[j], 2);
-                *(uint2 *)(tA + to[k]) = make_uint2(A[0], A[1]);
-                *(uint2 *)(tA + to[k] + 8) = make_uint2(A[2], A[3]);
-                *(uint2 *)(tB + to[k]) = make_uint2(Bw[0], Bw[1]);
-                *(uint2 *)(tB + to[k] + 8) = make_uint2(Bw[2], Bw[3]);
+            for (int u = 0; u < 2; u++) {
+                const int i = i0 + 64 * u + lane;
+                if (i < cur.nch) put(cur, i, q[u], q2[u], sh[u]);
             }
         }
         uint2 *z = (uint2 *)sc;
@@ -127,7 +162,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4, 8))) voi
         for (int i = lane; i < nz; i += 64) z[i] = make_uint2(0, 0);
     }
     wave_sync_lds();
-    if (g->dbg == 11) return;
+    if (g->dbg == 11) continue;
 
     // unit u = ry * RG + gg walked as u = lane + 64 k: (ry, gg) advance by (64 / RG, 64 % RG)
     const int rstep = RG > 0 ? 64 / RG : 0, gstep = RG > 0 ? 64 - rstep * RG : 0;
@@ -139,14 +174,20 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4, 8))) voi
     //   bright: min(max(c0, c8), max(c4, c12)) > v + th,  dark: max(min(c0, c8), min(c4, c12)) < v - th
     // Survivors (pair, side) are ballot-compacted into one list; order is irrelevant (the
     // scores go to their place in sc) ----
-    int nlist = 0;
+    int nlist = 0, nboth = 0;
+    const int lcap = g->fc2_list_cap;  // entries (2 per unit of the largest cell)
     {
         const v2s vth1 = (v2s){(short)(thi + 1), (short)(thi + 1)};
+        // tile offset of unit (ry, gg) kept incrementally (no per-iteration multiply)
+        int toff = ry0 * P + 4 * gg0;
+        const int tstep = rstep * P + 4 * gstep, twrap = P - 4 * RG;
         for (int u0 = 0, ry = ry0, gg = gg0; u0 < nunits; u0 += 64) {
             const int u = u0 + lane;
-            uint32_t pa = 0, pb = 0;
+            // per pair: bright / dark survivors as the sign bits (15, 31) of a packed word,
+            // 0 = none; pixels outside the region are forced to fail
+            uint32_t ab = 0, ad = 0, bb = 0, bd = 0;
             if (u < nunits) {
-                const uint32_t *p = (const uint32_t *)(tA + ry * P + 4 * gg);
+                const uint32_t *p = (const uint32_t *)(tA + toff);
                 uint32_t r0[3], r3[3], r6[3];
 #pragma unroll
                 for (int k = 0; k < 3; k++) {
@@ -154,8 +195,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4, 8))) voi
                     r3[k] = p[3 * P4 + k];
                     r6[k] = p[6 * P4 + k];
                 }
-                // bits: 0/1 bright pixel i/i+1, 2/3 dark pixel i/i+1
-                auto pretest = [&](auto I) -> uint32_t {
+                const int valid = RW - 4 * gg;  // pixels of the unit inside the region (>= 1)
+                const uint32_t invA = valid > 1 ? 0u : 0x80000000u;
+                const uint32_t invB = valid > 3 ? 0u : (valid > 2 ? 0x80000000u : 0x80008000u);
+                auto pretest = [&](auto I, uint32_t inv, uint32_t &pb_, uint32_t &pd_) {
                     constexpr int i = decltype(I)::value;
                     const v2s v = gather2<4 + i>(r3[0], r3[1], r3[2]);
                     const v2s c0 = gather2<4 + i>(r6[0], r6[1], r6[2]);
@@ -164,43 +207,56 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4, 8))) voi
                     const v2s c12 = gather2<1 + i>(r3[0], r3[1], r3[2]);
                     const v2s mb = pmin(pmax(c0, c8), pmax(c4, c12));
                     const v2s md = pmax(pmin(c0, c8), pmin(c4, c12));
-                    const uint32_t wb = __builtin_bit_cast(uint32_t, (v2s)(mb - v - vth1));
-                    const uint32_t wd = __builtin_bit_cast(uint32_t, (v2s)(v - md - vth1));
-                    return (~wb >> 15 & 1u) | (~wb >> 30 & 2u) | (~wd >> 13 & 4u) |
-                           (~wd >> 28 & 8u);
+                    // lane >= 0 <=> pass: mb - (v + th + 1) and (v - th - 1) - md
+                    const uint32_t wb = __builtin_bit_cast(uint32_t, (v2s)(mb - (v + vth1)));
+                    const uint32_t wd = __builtin_bit_cast(uint32_t, (v2s)((v - vth1) - md));
+                    pb_ = ~(wb | inv) & 0x80008000u;
+                    pd_ = ~(wd | inv) & 0x80008000u;
                 };
-                pa = pretest(std::integral_constant<int, 0>{});
-                pb = pretest(std::integral_constant<int, 2>{});
-                const int valid = min(RW - 4 * gg, 4);  // pixels of the unit inside the region
-                pa &= valid > 1 ? 15u : 5u;
-                pb &= valid > 3 ? 15u : (valid > 2 ? 5u : 0u);
+                pretest(std::integral_constant<int, 0>{}, invA, ab, ad);
+                pretest(std::integral_constant<int, 2>{}, invB, bb, bd);
             }
             const uint16_t e = (uint16_t)(ry << 8 | gg << 2);
-            auto append = [&](bool flag, uint16_t tag) {
+            // one entry per pair with a survivor, from the bottom of the list (side: bright
+            // unless only dark passed); pairs passing both sides (rare) from the top, expanded
+            // into two lane tasks by the scoring loop -- 2 entries per unit at most
+            auto append = [&](bool flag, bool top, uint16_t tag) {
                 const unsigned long long m = __ballot(flag);
                 const int below = __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32),
                                                             __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0));
-                if (flag) list[nlist + below] = (uint16_t)(e | tag);
-                nlist += __popcll(m);
+                if (flag) list[top ? lcap - 1 - (nboth + below) : nlist + below] = (uint16_t)(e | tag);
+                (top ? nboth : nlist) += __popcll(m);
             };
-            append((pa & 3u) != 0, 0);   // pixels 0-1, bright
-            append((pa & 12u) != 0, 1);  // pixels 0-1, dark
-            append((pb & 3u) != 0, 2);   // pixels 2-3, bright
-            append((pb & 12u) != 0, 3);  // pixels 2-3, dark
+            const bool bothA = ab && ad, bothB = bb && bd;
+            append((ab | ad) && !bothA, false, ab ? 0 : 1);  // pixels 0-1
+            append((bb | bd) && !bothB, false, bb ? 2 : 3);  // pixels 2-3
+            if (__ballot(bothA || bothB)) {
+                append(bothA, true, 0);
+                append(bothB, true, 2);
+            }
             ry += rstep;
             gg += gstep;
+            toff += tstep;
             if (gg >= RG) {
                 gg -= RG;
                 ry++;
+                toff += twrap;
             }
         }
     }
     wave_sync_lds();
-    if (g->dbg == 14) return;
+    if (g->dbg == 14) continue;
 
-    // ---- one side of one pixel pair per listed entry ----
-    for (int j = lane; j < nlist; j += 64) {
-        const int e = list[j];
+    // ---- one side of one pixel pair per lane task: tasks [0, nlist) are the bottom entries,
+    // then two per top entry (bright, dark) ----
+    for (int j = lane; j < nlist + 2 * nboth; j += 64) {
+        int e;
+        if (j < nlist) {
+            e = list[j];
+        } else {
+            const int t = j - nlist;
+            e = list[lcap - 1 - (t >> 1)] | (t & 1);
+        }
         const int ry = e >> 8, gg = (e >> 2) & 63, half = (e >> 1) & 1;
         const uint32_t flip = (e & 1) ? 0xFFFFFFFFu : 0u;  // dark: complemented bytes
         const uint32_t *p = (const uint32_t *)((half ? tB : tA) + ry * P + 4 * gg);
@@ -220,7 +276,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4, 8))) voi
                               __HIP_MEMORY_SCOPE_WAVEFRONT);
     }
     wave_sync_lds();
-    if (g->dbg == 12) return;
+    if (g->dbg == 12) continue;
 
     // ---- NMS (cell-local) + raster-order compaction, as k_fast_cells ----
     // cv::FAST keeps p iff s_p > every neighbour's score, a neighbour that is not a corner
@@ -309,7 +365,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4, 8))) voi
         }
         emit(kb, ry, gg);
     }
-    if (g->dbg == 13) return;
+    if (g->dbg == 13) continue;
     if (run == 0) {
         // an empty cell retries at minThFAST (ORBextractor.cc:1069-1075): every unit scored
         // on both sides (the window tiles are intact), then NMS at minThFAST
@@ -350,6 +406,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4, 8))) voi
         }
     }
     if (lane == 0) cell_cnt[slot] = run;
+    }  // cells of this wave
 }
 
 // instantiated LDS pitches (dwords); the host plan picks one, else k_fast_cells
@@ -367,12 +424,13 @@ bool fast2_pitch_ok(int p4)
     }
 }
 
-hipError_t launch_fast2(int p4, dim3 grid, size_t lds, hipStream_t st, const OrbgGeom *g,
+hipError_t launch_fast2(int p4, size_t lds, hipStream_t st, const OrbgGeom *g,
                         const OrbgCell *cells, const uint8_t *img0, int64_t img_fs,
                         int img_pitch, const uint8_t *pyr, const uint32_t *ctab,
                         int32_t *cell_cnt, uint2 *cell_kp, int nframes, int c_begin,
                         int c_count)
 {
+    const dim3 grid((c_count * nframes + 4 * FC2_CPW - 1) / (4 * FC2_CPW));
     switch (p4) {
 #define X(n)                                                                                  \
     case n:                                                                                   \

@@ -232,7 +232,9 @@ struct F2Key {
 #define INIT_F2_CAP 4608  // host-data path bound (frame capacity at 4000 features)
 
 // one 256-thread block: load F2 level-0 keys to LDS, then each wave handles INIT_QPW queries
-__device__ void init_cands_block(const orbg_keypoint *__restrict__ k1,
+// force-inlined: as a called function its pointer arguments would be generic (flat_ loads
+// and stores, which also count in lgkmcnt)
+__device__ __forceinline__ void init_cands_block(const orbg_keypoint *__restrict__ k1,
                                  const uint8_t *__restrict__ d1, int n1,
                                  const orbg_keypoint *__restrict__ k2,
                                  const uint8_t *__restrict__ d2, int n2, orbg_bounds b,

@@ -36,7 +36,7 @@ __global__ void k_octree_lds(const OrbgGeom *, const int32_t *, const uint2 *, u
                              uint32_t *, uint32_t *, int32_t *, int32_t *, OctLdsDims);
 // fast_kernels.hip
 bool fast2_pitch_ok(int p4);
-hipError_t launch_fast2(int p4, dim3 grid, size_t lds, hipStream_t st, const OrbgGeom *g,
+hipError_t launch_fast2(int p4, size_t lds, hipStream_t st, const OrbgGeom *g,
                         const OrbgCell *cells, const uint8_t *img0, int64_t img_fs,
                         int img_pitch, const uint8_t *pyr, const uint32_t *ctab,
                         int32_t *cell_cnt, uint2 *cell_kp, int nframes, int c_begin,
@@ -207,6 +207,17 @@ struct orbg_ctx {
     int blur0_mode = 0;  // measured: 2.013 vs 2.025 ms per 256 frames with it on
     int fast0_mode = 1;  // level-0 FAST cells on `ostream` beside the resize chain (ORBG_FAST0)
     int fast_v2 = 1;     // k_fast2 (fast_kernels.hip) where its pitch fits, else k_fast_cells (ORBG_FAST_V=1)
+    // Pipelined batches (orbg_set_pipeline): the front of a batch (pyramid, FAST cells,
+    // GaussianBlur: image work) runs on `stream`, its back (quadtree, orientation +
+    // descriptors, stereo: keypoint work) on `ostream`, so the front of batch k+1 overlaps
+    // the back of batch k.  The per-batch intermediates (pyramid, blur, FAST cells) alternate
+    // between two slots with the outputs: ev_cells[s] / ev_front[s] = slot s's FAST cells /
+    // whole front written (on `stream`), ev_back[s] = slot s's last back reader done (on
+    // `ostream`); the front into slot s waits for ev_back[s].
+    int pipelined = 0;
+    hipEvent_t ev_cells[2] = {nullptr, nullptr}, ev_front[2] = {nullptr, nullptr};
+    hipEvent_t ev_back[2] = {nullptr, nullptr};
+    bool back_pending[2] = {false, false};
     hipEvent_t ev_fork[2] = {nullptr, nullptr}, ev_join[2] = {nullptr, nullptr};
     // Batch matching and the trajectory summary run on `mstream`, so the matching of batch k
     // overlaps the extraction of batch k+1 on `stream`.  The per-frame outputs (kps, desc,
@@ -235,9 +246,12 @@ struct orbg_ctx {
     uint4 *d_odtab = nullptr;    // k_orient_desc IC_Angle byte tables (make_od_tab)
     uint8_t *d_img = nullptr;
     size_t img_bytes = 0;
-    uint8_t *d_pyr = nullptr, *d_blur = nullptr;
-    int32_t *d_cell_cnt = nullptr;
-    uint2 *d_cell_kp = nullptr;
+    uint8_t *d_pyr = nullptr, *d_blur = nullptr;  // = pyr_slot[slot], blur_slot[slot]
+    int32_t *d_cell_cnt = nullptr;                 // = cnt_slot[slot]
+    uint2 *d_cell_kp = nullptr;                    // = ckp_slot[slot]
+    uint8_t *pyr_slot[2] = {nullptr, nullptr}, *blur_slot[2] = {nullptr, nullptr};
+    int32_t *cnt_slot[2] = {nullptr, nullptr};
+    uint2 *ckp_slot[2] = {nullptr, nullptr};
     uint32_t *d_keys = nullptr, *d_knode = nullptr, *d_act = nullptr;
     uint8_t *d_qk = nullptr;
     int4 *d_nodes = nullptr;
@@ -341,12 +355,13 @@ static void make_tables(orbg_ctx *c)
 
 static void free_plan(orbg_ctx *c)
 {
-    if (c->stream) hipStreamSynchronize(c->stream);
-    if (c->mstream) hipStreamSynchronize(c->mstream);
+    for (hipStream_t q : {c->stream, c->mstream, c->ostream, c->aux_stream})
+        if (q) hipStreamSynchronize(q);
     c->mat_pending[0] = c->mat_pending[1] = false;
+    c->back_pending[0] = c->back_pending[1] = false;
     void *ptrs[] = {c->d_geom, c->d_cells, c->d_tile_base, c->d_rtab, c->d_ctab, c->d_odtab,
-                    c->d_pyr, c->d_blur,
-                    c->d_cell_cnt, c->d_cell_kp, c->d_keys, c->d_knode, c->d_act, c->d_qk,
+                    c->pyr_slot[0], c->pyr_slot[1], c->blur_slot[0], c->blur_slot[1],
+                    c->cnt_slot[0], c->cnt_slot[1], c->ckp_slot[0], c->ckp_slot[1], c->d_keys, c->d_knode, c->d_act, c->d_qk,
                     c->d_nodes, c->d_lvl_kp, c->d_lvl_cnt, c->kps_slot[0], c->kps_slot[1],
                     c->desc_slot[0], c->desc_slot[1], c->counts_slot[0], c->counts_slot[1],
                     c->d_err, c->d_knn, c->d_m12, c->d_nm, c->d_topk, c->d_topk_n, c->d_pairs,
@@ -362,6 +377,11 @@ static void free_plan(orbg_ctx *c)
     c->d_pyr = c->d_blur = nullptr;
     c->d_cell_cnt = nullptr;
     c->d_cell_kp = nullptr;
+    for (int i = 0; i < 2; i++) {
+        c->pyr_slot[i] = c->blur_slot[i] = nullptr;
+        c->cnt_slot[i] = nullptr;
+        c->ckp_slot[i] = nullptr;
+    }
     c->d_keys = c->d_knode = c->d_act = nullptr;
     c->d_qk = nullptr;
     c->d_nodes = nullptr;
@@ -687,15 +707,19 @@ static int plan(orbg_ctx *c, int w, int h, int batch)
             return set_err(ORBG_ENOTSUP, "FAST cell %dx%d needs %d LDS bytes per wave", wmax,
                            hmax, G.fc_wave_bytes);
         // k_fast2 (fast_kernels.hip): compile-time pitch P4 >= 4 * ceil((RG + 3) / 4) (its
-        // 16-byte window chunks), picked among the instantiated ones by the same bank-spread
-        // cost; layout tA | tB (hmax rows each) | scores (hmax - 4 rows) | list (4 entries per
-        // unit: two pixel pairs x two sides)
+        // 16-byte window chunks) among the instantiated ones; layout tA | tB (hmax rows each)
+        // | scores (hmax - 4 rows) | list (2 entries per unit).  Preferred: the most
+        // workgroups per CU by LDS (capped at 6: the VGPR bound), then the bank-spread cost.
         G.fc2_p4 = 0;
         if (c->fast_v2) {
             const int need = 4 * ((rg + 3 + 3) / 4);
-            int best_c = 1 << 30;
+            int best_c = 1 << 30, best_wg = 0;
             for (int wd = need; wd <= 32; wd++) {
                 if (!fast2_pitch_ok(wd)) continue;
+                const int P2 = 4 * wd;
+                const int wb = (2 * hmax * P2 + (std::max(hmax - 6, 0) + 2) * P2 +
+                                4 * max_units + 15) & ~15;
+                const int wgs = std::min(6, 163840 / (4 * wb));
                 int cost = 0;
                 for (int r : rgs)
                     for (int k = 0; k < 3; k++) {
@@ -706,7 +730,8 @@ static int plan(orbg_ctx *c, int w, int h, int batch)
                         }
                         cost += mx;
                     }
-                if (cost < best_c) {
+                if (wgs > best_wg || (wgs == best_wg && cost < best_c)) {
+                    best_wg = wgs;
                     best_c = cost;
                     G.fc2_p4 = wd;
                 }
@@ -716,7 +741,8 @@ static int plan(orbg_ctx *c, int w, int h, int batch)
                 G.fc2_tileb_off = hmax * P2;
                 G.fc2_sc_off = 2 * hmax * P2;
                 G.fc2_list_off = G.fc2_sc_off + (std::max(hmax - 6, 0) + 2) * P2;
-                G.fc2_wave_bytes = (G.fc2_list_off + 8 * max_units + 15) & ~15;
+                G.fc2_list_cap = 2 * max_units;
+                G.fc2_wave_bytes = (G.fc2_list_off + 2 * G.fc2_list_cap + 15) & ~15;
                 if (4 * G.fc2_wave_bytes > 160 * 1024) G.fc2_p4 = 0;
             }
         }
@@ -786,9 +812,13 @@ static int plan(orbg_ctx *c, int w, int h, int batch)
     if ((rc = dalloc(&c->d_geom, 1)) || (rc = dalloc(&c->d_cells, cells.size())) ||
         (rc = dalloc(&c->d_ctab, ctab.size())) || (rc = dalloc(&c->d_odtab, odtab.size())) ||
         (rc = dalloc(&c->d_tile_base, tile_base.size())) || (rc = dalloc(&c->d_rtab, rtab.size())) ||
-        (rc = dalloc(&c->d_pyr, B * G.pyr_frame)) || (rc = dalloc(&c->d_blur, B * G.blur_frame)) ||
-        (rc = dalloc(&c->d_cell_cnt, B * G.ncells)) ||
-        (rc = dalloc(&c->d_cell_kp, B * G.ncells * (size_t)cell_cap)) ||
+        (rc = dalloc(&c->pyr_slot[0], B * G.pyr_frame)) ||
+        (rc = dalloc(&c->pyr_slot[1], B * G.pyr_frame)) ||
+        (rc = dalloc(&c->blur_slot[0], B * G.blur_frame)) ||
+        (rc = dalloc(&c->blur_slot[1], B * G.blur_frame)) ||
+        (rc = dalloc(&c->cnt_slot[0], B * G.ncells)) || (rc = dalloc(&c->cnt_slot[1], B * G.ncells)) ||
+        (rc = dalloc(&c->ckp_slot[0], B * G.ncells * (size_t)cell_cap)) ||
+        (rc = dalloc(&c->ckp_slot[1], B * G.ncells * (size_t)cell_cap)) ||
         (rc = dalloc(&c->d_keys, B * G.keys_frame)) || (rc = dalloc(&c->d_knode, B * G.keys_frame)) ||
         (rc = dalloc(&c->d_act, 2 * B * G.keys_frame)) || (rc = dalloc(&c->d_qk, B * G.keys_frame)) ||
         (rc = dalloc(&c->d_nodes, B * G.nodes_frame)) || (rc = dalloc(&c->d_lvl_kp, B * G.out_frame)) ||
@@ -827,6 +857,10 @@ static int plan(orbg_ctx *c, int w, int h, int batch)
     c->d_kps = c->kps_slot[0];
     c->d_desc = c->desc_slot[0];
     c->d_counts = c->counts_slot[0];
+    c->d_pyr = c->pyr_slot[0];
+    c->d_blur = c->blur_slot[0];
+    c->d_cell_cnt = c->cnt_slot[0];
+    c->d_cell_kp = c->ckp_slot[0];
     c->geom = G;
     c->cells = cells;
     c->tile_base = tile_base;
@@ -928,7 +962,11 @@ extern "C" int orbg_create(int device, const orbg_params *p, orbg_ctx **out)
         hipEventCreateWithFlags(&c->ev_join[i], hipEventDisableTiming);
         hipEventCreateWithFlags(&c->ev_ext[i], hipEventDisableTiming);
         hipEventCreateWithFlags(&c->ev_mat[i], hipEventDisableTiming);
+        hipEventCreateWithFlags(&c->ev_cells[i], hipEventDisableTiming);
+        hipEventCreateWithFlags(&c->ev_front[i], hipEventDisableTiming);
+        hipEventCreateWithFlags(&c->ev_back[i], hipEventDisableTiming);
     }
+    if (const char *e = getenv("ORBG_PIPELINE")) c->pipelined = atoi(e) && c->ostream;
     *out = c;
     return ORBG_OK;
 }
@@ -952,6 +990,9 @@ extern "C" void orbg_destroy(orbg_ctx *c)
         if (c->ev_join[i]) hipEventDestroy(c->ev_join[i]);
         if (c->ev_ext[i]) hipEventDestroy(c->ev_ext[i]);
         if (c->ev_mat[i]) hipEventDestroy(c->ev_mat[i]);
+        if (c->ev_cells[i]) hipEventDestroy(c->ev_cells[i]);
+        if (c->ev_front[i]) hipEventDestroy(c->ev_front[i]);
+        if (c->ev_back[i]) hipEventDestroy(c->ev_back[i]);
     }
     if (c->aux_stream) hipStreamDestroy(c->aux_stream);
     if (c->ostream) hipStreamDestroy(c->ostream);
@@ -996,6 +1037,113 @@ extern "C" int orbg_get_pattern(int32_t out[1024])
 // ---------------------------------------------------------------------------
 // extraction
 // ---------------------------------------------------------------------------
+// FAST cells [cb, cb + cn) of every frame on `st` (k_fast2 where the plan picked a pitch)
+static hipError_t launch_fast_cells(orbg_ctx *c, hipStream_t st, const uint8_t *d_imgs, int B,
+                                    int pitch, int64_t fs, int cb, int cn)
+{
+    const OrbgGeom &G = c->geom;
+    if (G.fc2_p4) {
+        hipError_t e = hipSuccess;
+        PROF_LAUNCH(c, "fast_cells",
+                    e = launch_fast2(G.fc2_p4, 4 * G.fc2_wave_bytes, st, c->d_geom, c->d_cells,
+                                     d_imgs, fs, pitch, c->d_pyr, c->d_ctab, c->d_cell_cnt,
+                                     c->d_cell_kp, B, cb, cn));
+        return e;
+    }
+    PROF_LAUNCH(c, "fast_cells",
+                hipLaunchKernelGGL(k_fast_cells, dim3((cn * B + 3) / 4), dim3(256),
+                                   4 * G.fc_wave_bytes, st, c->d_geom, c->d_cells, d_imgs, fs,
+                                   pitch, c->d_pyr, c->d_ctab, c->d_cell_cnt, c->d_cell_kp, B,
+                                   cb, cn));
+    return hipGetLastError();
+}
+
+// Pipelined batch into slot s (orbg_set_pipeline).  Front on `stream`: resize chain, FAST
+// cells of every level (one launch), GaussianBlur.  Back on `ostream` (high priority):
+// quadtree levels once the cells are written, k_octree, then orientation + descriptors once
+// the blur is written.  The front of the next batch goes to the other slot, so it runs
+// beside this back; the front into slot s waits until slot s's previous back is done.
+// The back is in stream order on `ostream`, so the quadtree scratch (keys, lists, per-level
+// outputs) is reused by consecutive batches without further events.  The input images
+// must stay unchanged until the batch's outputs are complete (the back reads level 0).
+static int launch_extract_pipe(orbg_ctx *c, const uint8_t *d_imgs, int B, int pitch, int64_t fs,
+                               int s)
+{
+    const OrbgGeom &G = c->geom;
+    {
+        hipStream_t st = c->stream;
+        if (c->back_pending[s]) {
+            HIPCHK(hipStreamWaitEvent(st, c->ev_back[s], 0));
+            c->back_pending[s] = false;
+        }
+        for (int l = 1; l < G.L; l++) {
+            const OrbgLevel &L = G.lv[l], &P = G.lv[l - 1];
+            const uint8_t *src = (l == 1) ? d_imgs : c->d_pyr + P.pyr_off;
+            const int64_t sfs = (l == 1) ? fs : G.pyr_frame;
+            const int spitch = (l == 1) ? pitch : P.pitch;
+            dim3 grid((L.w + 255) / 256, (L.h + 16 * ORBG_RZ_NT - 1) / (16 * ORBG_RZ_NT), B);
+            PROF_LAUNCH(c, "resize",
+                        hipLaunchKernelGGL(k_resize, grid, dim3(256), L.rz_pitch * L.rz_rows, st,
+                                           src, sfs, spitch, P.w, c->d_pyr + L.pyr_off,
+                                           G.pyr_frame, L.pitch, L.w, L.h,
+                                           c->d_rtab + L.xtab_off, c->d_rtab + L.ytab_off,
+                                           L.bulk_end, L.rz_pitch));
+        }
+        HIPCHK(launch_fast_cells(c, st, d_imgs, B, pitch, fs, 0, G.ncells));
+        HIPCHK(hipEventRecord(c->ev_cells[s], st));
+        PROF_LAUNCH(c, "blur",
+                    hipLaunchKernelGGL(k_blur, dim3(c->total_tiles * B), dim3(256), 0, st,
+                                       c->d_geom, c->d_tile_base, d_imgs, fs, pitch, c->d_pyr,
+                                       c->d_blur, 0, c->total_tiles));
+        HIPCHK(hipEventRecord(c->ev_front[s], st));
+    }
+    hipStream_t st = c->ostream;  // the back (PROF_LAUNCH records on `st`)
+    HIPCHK(hipStreamWaitEvent(st, c->ev_cells[s], 0));
+    PROF_LAUNCH(c, "octree",
+                hipLaunchKernelGGL(k_octree_lds, dim3(B, 1), dim3(512),
+                                   oct_lds_bytes(c->oct_dims[0]), st, c->d_geom, c->d_cell_cnt,
+                                   c->d_cell_kp, c->d_keys, c->d_act, c->d_lvl_kp, c->d_lvl_cnt,
+                                   c->d_err, c->oct_dims[0]));
+    if (G.L > 1)
+        PROF_LAUNCH(c, "octree",
+                    hipLaunchKernelGGL(k_octree_lds, dim3(B, G.L - 1), dim3(512),
+                                       oct_lds_bytes(c->oct_dims[1]), st, c->d_geom,
+                                       c->d_cell_cnt, c->d_cell_kp, c->d_keys, c->d_act,
+                                       c->d_lvl_kp, c->d_lvl_cnt, c->d_err, c->oct_dims[1]));
+    PROF_LAUNCH(c, "octree_big",
+                hipLaunchKernelGGL(k_octree, dim3(G.L, B), dim3(ORBG_OCT_THREADS), 0, st,
+                                   c->d_geom, c->d_cell_cnt, c->d_cell_kp, c->d_keys, c->d_knode,
+                                   c->d_act, c->d_qk, c->d_nodes, c->d_lvl_kp, c->d_lvl_cnt,
+                                   c->d_err));
+    HIPCHK(hipStreamWaitEvent(st, c->ev_front[s], 0));
+    if (c->mat_pending[s]) {  // the matching of the batch before last reads output slot s
+        HIPCHK(hipStreamWaitEvent(st, c->ev_mat[s], 0));
+        c->mat_pending[s] = false;
+    }
+    c->slot = s;
+    c->d_kps = c->kps_slot[s];
+    c->d_desc = c->desc_slot[s];
+    c->d_counts = c->counts_slot[s];
+    PROF_LAUNCH(c, "orient_desc",
+                hipLaunchKernelGGL(k_orient_desc,
+                                   dim3((G.out_frame + 4 * ORBG_OD_KPW - 1) / (4 * ORBG_OD_KPW) * B),
+                                   dim3(256), 0, st, c->d_geom, d_imgs, fs, pitch, c->d_pyr,
+                                   c->d_blur, c->d_odtab, c->d_lvl_kp, c->d_lvl_cnt,
+                                   (OrbgKeypointDev *)c->d_kps, c->d_desc, c->d_counts));
+    HIPCHK(hipEventRecord(c->ev_ext[s], st));
+    HIPCHK(hipEventRecord(c->ev_back[s], st));
+    c->back_pending[s] = true;
+    HIPCHK(hipGetLastError());
+    c->last_img = d_imgs;
+    c->last_fs = fs;
+    c->last_pitch = pitch;
+    c->last_n = B;
+    return ORBG_OK;
+}
+
+// stream the last batch's per-frame outputs are written on (and stereo runs on)
+static hipStream_t back_stream(orbg_ctx *c) { return c->pipelined ? c->ostream : c->stream; }
+
 static int launch_extract(orbg_ctx *c, const uint8_t *d_imgs, int B, int pitch, int64_t fs)
 {
     const OrbgGeom &G = c->geom;
@@ -1004,6 +1152,13 @@ static int launch_extract(orbg_ctx *c, const uint8_t *d_imgs, int B, int pitch, 
     c->last_npairs = 0;
     c->last_nstereo = 0;
     // d_err is not cleared here: it is sticky until check_err reads it
+    // this batch's slot: intermediates (pyramid, blur, FAST cells) and per-frame outputs
+    const int s = c->slot ^ 1;
+    c->d_pyr = c->pyr_slot[s];
+    c->d_blur = c->blur_slot[s];
+    c->d_cell_cnt = c->cnt_slot[s];
+    c->d_cell_kp = c->ckp_slot[s];
+    if (c->pipelined) return launch_extract_pipe(c, d_imgs, B, pitch, fs, s);
     // fast0: the level-0 FAST cells and quadtree need only the input images, so they run on
     // the quadtree stream beside the resize chain (latency-bound small launches)
     const bool fast0 = c->fast0_mode && c->oct_mode && G.L > 1;
@@ -1011,21 +1166,8 @@ static int launch_extract(orbg_ctx *c, const uint8_t *d_imgs, int B, int pitch, 
     // blur0: the level-0 GaussianBlur follows them there (ORBG_BLUR0)
     const bool blur0 = fast0 && c->blur0_mode;
     const int tb1 = c->tile_base[1], tb0 = blur0 ? tb1 : 0;
-    auto launch_fast = [&](hipStream_t st, int cb, int cn) {
-        if (G.fc2_p4) {
-            hipError_t e = hipSuccess;
-            PROF_LAUNCH(c, "fast_cells",
-                        e = launch_fast2(G.fc2_p4, dim3((cn * B + 3) / 4), 4 * G.fc2_wave_bytes, st,
-                                         c->d_geom, c->d_cells, d_imgs, fs, pitch, c->d_pyr,
-                                         c->d_ctab, c->d_cell_cnt, c->d_cell_kp, B, cb, cn));
-            return e;
-        }
-        PROF_LAUNCH(c, "fast_cells",
-                    hipLaunchKernelGGL(k_fast_cells, dim3((cn * B + 3) / 4), dim3(256),
-                                       4 * G.fc_wave_bytes, st, c->d_geom, c->d_cells, d_imgs,
-                                       fs, pitch, c->d_pyr, c->d_ctab, c->d_cell_cnt,
-                                       c->d_cell_kp, B, cb, cn));
-        return hipSuccess;
+    auto launch_fast = [&](hipStream_t q, int cb, int cn) {
+        return launch_fast_cells(c, q, d_imgs, B, pitch, fs, cb, cn);
     };
     if (fast0) {
         HIPCHK(hipEventRecord(c->ev_fast, st));
@@ -1098,7 +1240,6 @@ static int launch_extract(orbg_ctx *c, const uint8_t *d_imgs, int B, int pitch, 
                                    c->d_err));
     // per-frame outputs go to the other slot; wait until its last reader (matching of the
     // batch before last) is done
-    const int s = c->slot ^ 1;
     if (c->mat_pending[s]) {
         HIPCHK(hipStreamWaitEvent(st, c->ev_mat[s], 0));
         c->mat_pending[s] = false;
@@ -1268,6 +1409,20 @@ extern "C" int orbg_set_stream(orbg_ctx *c, void *stream)
     c->stream = stream ? (hipStream_t)stream : c->own_stream;
     return ORBG_OK;
 }
+
+extern "C" int orbg_set_pipeline(orbg_ctx *c, int enable)
+{
+    if (!c) return set_err(ORBG_EINVAL, "ctx is NULL");
+    if (enable && !c->ostream)
+        return set_err(ORBG_ENOTSUP, "pipelined batches need the quadtree stream (ORBG_OCT_STREAM=0)");
+    int rc = sync_all(c);
+    if (rc) return rc;
+    c->pipelined = enable ? 1 : 0;
+    c->back_pending[0] = c->back_pending[1] = false;
+    return ORBG_OK;
+}
+
+extern "C" int orbg_get_pipeline(const orbg_ctx *c) { return c ? c->pipelined : 0; }
 
 extern "C" int orbg_batch_stats(orbg_ctx *c, int64_t *ncand, int64_t *nkp)
 {
@@ -1459,17 +1614,20 @@ extern "C" int orbg_stereo_batch_device(orbg_ctx *c, const int32_t *left, const 
     std::vector<int32_t> hp(left, left + npairs);
     hp.insert(hp.end(), right, right + npairs);
     if (hp != c->h_spairs) {
-        HIPCHK(hipStreamSynchronize(c->stream));  // a previous stereo pass may read them
+        HIPCHK(hipStreamSynchronize(back_stream(c)));  // a previous stereo pass may read them
         HIPCHK(hipMemcpy(c->d_spairs, left, npairs * sizeof(int32_t), hipMemcpyHostToDevice));
         HIPCHK(hipMemcpy(c->d_spairs + c->stereo_cap, right, npairs * sizeof(int32_t),
                          hipMemcpyHostToDevice));
         c->h_spairs.swap(hp);
     }
-    int rc = launch_stereo(c->stream, c->geom, c->d_kps, c->d_desc, c->d_counts, c->d_spairs,
+    // pipelined: on the back stream after the batch's descriptors; the slot's next front
+    // waits for it (ev_back)
+    int rc = launch_stereo(back_stream(c), c->geom, c->d_kps, c->d_desc, c->d_counts, c->d_spairs,
                            c->d_spairs + c->stereo_cap, npairs, c->last_img, c->last_fs,
                            c->last_pitch, c->d_pyr, bf, min_z, c->d_sscr, c->d_uright,
                            c->d_depth, c->d_snvalid, &c->prof);
     if (rc) return set_err(rc, "stereo launch failed (level-0 height > 4096?)");
+    if (c->pipelined) HIPCHK(hipEventRecord(c->ev_back[c->slot], c->ostream));
     c->last_nstereo = npairs;
     return ORBG_OK;
 }
@@ -1490,7 +1648,8 @@ extern "C" int orbg_stereo_summary(orbg_ctx *c, int32_t *d_out)
 {
     if (!c || !c->last_nstereo || !d_out) return set_err(ORBG_EINVAL, "no stereo batch yet");
     hipLaunchKernelGGL(k_stereo_summary, dim3((c->last_nstereo + 255) / 256), dim3(256), 0,
-                       c->stream, c->d_counts, c->d_spairs, c->d_snvalid, c->last_nstereo, d_out);
+                       back_stream(c), c->d_counts, c->d_spairs, c->d_snvalid, c->last_nstereo,
+                       d_out);
     HIPCHK(hipGetLastError());
     return ORBG_OK;
 }

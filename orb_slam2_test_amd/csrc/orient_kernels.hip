@@ -169,10 +169,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(ORBG_OD_WPE
             wd[k] = make_uint4(0, 0, 0, 0);
             sh[k] = 0;
             if (lane + 64 * k < OD_TABW) {
-                const uintptr_t a = (uintptr_t)(ctr + (int64_t)(pr[k] - ORBG_HALF_PATCH) * pitch -
-                                                ORBG_HALF_PATCH);
-                wd[k] = *(const uint4 *)((a & ~(uintptr_t)3) + 16 * pc[k]);
-                sh[k] = (int)(a & 3);
+                // pointer arithmetic (not an integer round trip): global_, not flat_, loads
+                const uint8_t *pa = ctr + (int64_t)(pr[k] - ORBG_HALF_PATCH) * pitch - ORBG_HALF_PATCH;
+                sh[k] = (int)((uintptr_t)pa & 3);
+                wd[k] = *(const uint4 *)(pa - sh[k] + 16 * pc[k]);
             }
         }
         int m01 = 0, m10 = 0;

@@ -309,7 +309,7 @@ __global__ __launch_bounds__(256) void k_track_cands(TrackArgs A)
 // exact rescan of one query against the current taken state: best and second keys over
 // all keypoints of the frame, wave-parallel (the rare query whose K-list ran out)
 template <int MODE>
-__device__ void track_rescan(const TrackArgs &A, int f, int i, const TrackQuery &Q,
+__device__ __forceinline__ void track_rescan(const TrackArgs &A, int f, int i, const TrackQuery &Q,
                              const uint8_t *taken, unsigned long long *k1o,
                              unsigned long long *k2o)
 {
