@@ -19,6 +19,7 @@
 #include "track_args.h"
 #include "schur_args.h"
 #include "bow_args.h"
+#include "pyramid_args.h"
 
 #pragma clang fp contract(off)
 
@@ -36,6 +37,8 @@ __global__ void k_octree_lds(const OrbgGeom *, const int32_t *, const uint2 *, u
                              uint32_t *, uint32_t *, int32_t *, int32_t *, OctLdsDims);
 // fast_kernels.hip
 bool fast2_pitch_ok(int p4);
+__global__ void k_pyramid(PyrArgs, const uint4 *, const int4 *, const int2 *, const uint8_t *,
+                          int64_t, int, const uint8_t *, uint8_t *, int);
 hipError_t launch_fast2(int p4, size_t lds, hipStream_t st, const OrbgGeom *g,
                         const OrbgCell *cells, const uint8_t *img0, int64_t img_fs,
                         int img_pitch, const uint8_t *pyr, const uint32_t *ctab,
@@ -242,6 +245,14 @@ struct orbg_ctx {
     OrbgCell *d_cells = nullptr;
     int32_t *d_tile_base = nullptr;
     int2 *d_rtab = nullptr;
+    // k_pyramid (all levels in one launch): octet / row records and band closures; pyr_ok
+    // = the plan passed k_pyramid's checks (else the k_resize chain)
+    uint4 *d_ptab = nullptr;
+    int4 *d_ytab4 = nullptr;
+    int2 *d_bands = nullptr;
+    PyrArgs pyr_args{};
+    bool pyr_ok = false;
+    int pyr_wg = 512;  // k_pyramid workgroup size (ORBG_PYR_WG)
     uint32_t *d_ctab = nullptr;  // quadtree path-code tables (xs | ys per level)
     uint4 *d_odtab = nullptr;    // k_orient_desc IC_Angle byte tables (make_od_tab)
     uint8_t *d_img = nullptr;
@@ -365,13 +376,18 @@ static void free_plan(orbg_ctx *c)
                     c->d_nodes, c->d_lvl_kp, c->d_lvl_cnt, c->kps_slot[0], c->kps_slot[1],
                     c->desc_slot[0], c->desc_slot[1], c->counts_slot[0], c->counts_slot[1],
                     c->d_err, c->d_knn, c->d_m12, c->d_nm, c->d_topk, c->d_topk_n, c->d_pairs,
-                    c->d_spairs, c->d_uright, c->d_depth, c->d_snvalid, c->d_sscr};
+                    c->d_spairs, c->d_uright, c->d_depth, c->d_snvalid, c->d_sscr,
+                    c->d_ptab, c->d_ytab4, c->d_bands};
     for (void *q : ptrs)
         if (q) hipFree(q);
     c->d_geom = nullptr;
     c->d_cells = nullptr;
     c->d_tile_base = nullptr;
     c->d_rtab = nullptr;
+    c->d_ptab = nullptr;
+    c->d_ytab4 = nullptr;
+    c->d_bands = nullptr;
+    c->pyr_ok = false;
     c->d_ctab = nullptr;
     c->d_odtab = nullptr;
     c->d_pyr = c->d_blur = nullptr;
@@ -447,6 +463,107 @@ static int dalloc(T **p, size_t n)
         return set_err(ORBG_ENOMEM, "hipMalloc(%zu bytes): %s", n * sizeof(T),
                        hipGetErrorString(e));
     return ORBG_OK;
+}
+
+// k_pyramid tables (pyramid_args.h) from the cv::resize coefficient tables of every level.
+// Returns false when a level falls outside what the kernel assumes (scale factors near 1.2:
+// an octet's source bytes within 12, one output row completing per source row, at most
+// PYR_NS source rows per 8 output rows); the k_resize chain then builds the pyramid.
+static bool make_pyr_tables(const OrbgGeom &G, const std::vector<int2> &rtab, int nband,
+                            std::vector<uint4> &ptab, std::vector<int4> &ytab,
+                            std::vector<int2> &bands, PyrArgs &A)
+{
+    if (G.L < 2 || G.L > 16 || nband < 1) return false;
+    A = PyrArgs{};
+    A.L = G.L;
+    A.nband = nband;
+    A.pyr_frame = G.pyr_frame;
+    for (int l = 1; l < G.L; l++) {
+        const OrbgLevel &L = G.lv[l], &S = G.lv[l - 1];
+        PyrLevelArgs &P = A.lv[l];
+        P.sw = S.w;
+        P.sh = S.h;
+        P.dw = L.w;
+        P.dh = L.h;
+        P.spitch = S.pitch;
+        P.dpitch = L.pitch;
+        P.src_off = l >= 2 ? S.pyr_off : 0;
+        P.dst_off = L.pyr_off;
+        P.noct = (L.w + PYR_COLS - 1) / PYR_COLS;
+        P.ptab_off = (int)ptab.size();
+        P.ytab_off = (int)ytab.size();
+        if (L.pitch % 64 || S.w < 2 || S.h < 2) return false;
+        const int2 *xt = rtab.data() + L.xtab_off, *yt = rtab.data() + L.ytab_off;
+        P.fix_oct = P.noct;
+        P.clamp_row = L.h;
+        P.guard_row = L.h;
+        for (int dy = L.h - 1; dy >= 0; dy--) {
+            if ((yt[dy].x & 0xFFFF) == (yt[dy].x >> 16)) P.clamp_row = dy;
+            if ((yt[dy].x >> 16) == S.h - 1) P.guard_row = dy;
+        }
+        for (int q = 0; q < P.noct; q++) {
+            const int dx0 = q * PYR_COLS, sx0 = xt[dx0].x;
+            uint32_t sel[PYR_COLS], cf[PYR_COLS], smask = 0;
+            for (int i = 0; i < PYR_COLS; i++) {
+                const int dx = dx0 + i;
+                sel[i] = 0x0c0c0c0cu;  // past the level's width: zeros, never stored
+                cf[i] = 0;
+                if (dx >= L.w) continue;
+                const int sx = xt[dx].x, sx1 = std::min(sx + 1, S.w - 1);
+                const int a0 = (int)(short)(xt[dx].y & 0xFFFF), a1 = (int)(short)(xt[dx].y >> 16);
+                if (a0 < 0 || a1 < 0 || a0 > 4095 || a1 > 4095) return false;
+                int r0 = sx - sx0, r1 = sx1 - sx0;
+                if (i >= 4) {
+                    r0 -= 4;
+                    r1 -= 4;
+                }
+                if (r0 < 0 || r1 < 0 || r0 > 7 || r1 > 7) return false;
+                sel[i] = (uint32_t)r0 | 0x0cu << 8 | (uint32_t)r1 << 16 | 0x0cu << 24;
+                cf[i] = (uint32_t)(a0 << 4) | (uint32_t)(a1 << 4) << 16;
+                if (dx >= L.bulk_end) smask |= 1u << i;
+            }
+            if ((smask || dx0 + PYR_COLS > L.w) && P.fix_oct == P.noct) P.fix_oct = q;
+            ptab.push_back(make_uint4((uint32_t)sx0, smask, 0, 0));
+            ptab.push_back(make_uint4(sel[0], sel[1], sel[2], sel[3]));
+            ptab.push_back(make_uint4(sel[4], sel[5], sel[6], sel[7]));
+            ptab.push_back(make_uint4(cf[0], cf[1], cf[2], cf[3]));
+            ptab.push_back(make_uint4(cf[4], cf[5], cf[6], cf[7]));
+        }
+        for (int dy = 0; dy < L.h; dy++) {
+            const int sy0 = yt[dy].x & 0xFFFF, sy1 = yt[dy].x >> 16;
+            const int b0 = (int)(short)(yt[dy].y & 0xFFFF), b1 = (int)(short)(yt[dy].y >> 16);
+            if (b0 < 0 || b1 < 0 || b0 > 4095 || b1 > 4095) return false;
+            if (!(sy1 == sy0 + 1 || sy1 == sy0)) return false;
+            if (dy > 0 && sy1 <= (yt[dy - 1].x >> 16)) return false;  // one row per source row
+            if ((yt[std::min(dy + PYR_ROWS - 1, L.h - 1)].x >> 16) - sy0 + 1 > PYR_NS) return false;
+            ytab.push_back(make_int4(sy0 | sy1 << 16, b0 << 8, b1 << 8, b0 | b1 << 16));
+        }
+    }
+    // bands: own rows split evenly per level; the rows a band computes are its own rows plus
+    // the source rows of what it computes one level up (top-down closure)
+    bands.assign((size_t)nband * G.L, make_int2(0, 0));
+    for (int b = 0; b < nband; b++) {
+        int lo = 0, hi = 0;  // computed rows of level l + 1
+        for (int l = G.L - 1; l >= 1; l--) {
+            const OrbgLevel &L = G.lv[l];
+            int olo = (int)((int64_t)L.h * b / nband), ohi = (int)((int64_t)L.h * (b + 1) / nband);
+            if (l < G.L - 1 && hi > lo) {
+                const int2 *yt = rtab.data() + G.lv[l + 1].ytab_off;
+                const int slo = yt[lo].x & 0xFFFF, shi = (yt[hi - 1].x >> 16) + 1;
+                if (ohi > olo) {
+                    olo = std::min(olo, slo);
+                    ohi = std::max(ohi, shi);
+                } else {
+                    olo = slo;
+                    ohi = shi;
+                }
+            }
+            bands[(size_t)b * G.L + l] = make_int2(olo, ohi);
+            lo = olo;
+            hi = ohi;
+        }
+    }
+    return true;
 }
 
 // Build the geometry for an image size and allocate HBM for `batch` frames.
@@ -851,6 +968,28 @@ static int plan(orbg_ctx *c, int w, int h, int batch)
                      hipMemcpyHostToDevice));
     HIPCHK(hipMemcpy(c->d_odtab, odtab.data(), odtab.size() * sizeof(uint4),
                      hipMemcpyHostToDevice));
+    {
+        // k_pyramid (ORBG_PYR=0: the k_resize chain, developer A/B; ORBG_PYR_NB: bands)
+        const char *e = getenv("ORBG_PYR"), *nb = getenv("ORBG_PYR_NB");
+        std::vector<uint4> pt;
+        std::vector<int4> yt4;
+        std::vector<int2> bd;
+        PyrArgs A{};
+        c->pyr_ok = (!e || atoi(e)) && make_pyr_tables(G, rtab, nb ? atoi(nb) : 4, pt, yt4, bd, A);
+        if (c->pyr_ok) {
+            if ((rc = dalloc(&c->d_ptab, pt.size())) || (rc = dalloc(&c->d_ytab4, yt4.size())) ||
+                (rc = dalloc(&c->d_bands, bd.size()))) {
+                free_plan(c);
+                return rc;
+            }
+            HIPCHK(hipMemcpy(c->d_ptab, pt.data(), pt.size() * sizeof(uint4), hipMemcpyHostToDevice));
+            HIPCHK(hipMemcpy(c->d_ytab4, yt4.data(), yt4.size() * sizeof(int4), hipMemcpyHostToDevice));
+            HIPCHK(hipMemcpy(c->d_bands, bd.data(), bd.size() * sizeof(int2), hipMemcpyHostToDevice));
+            c->pyr_args = A;
+            const char *wg = getenv("ORBG_PYR_WG");
+            c->pyr_wg = wg ? std::min(std::max(atoi(wg) / 64 * 64, 64), 1024) : 512;
+        }
+    }
     HIPCHK(hipMemset(c->counts_slot[0], 0, B * sizeof(int32_t)));
     HIPCHK(hipMemset(c->counts_slot[1], 0, B * sizeof(int32_t)));
     c->slot = 0;
@@ -1037,6 +1176,37 @@ extern "C" int orbg_get_pattern(int32_t out[1024])
 // ---------------------------------------------------------------------------
 // extraction
 // ---------------------------------------------------------------------------
+// ComputePyramid for B frames on `st`: k_pyramid (one launch, every level) when the plan
+// passed its checks, else the k_resize chain (one launch per level)
+static hipError_t launch_pyramid(orbg_ctx *c, hipStream_t st, const uint8_t *d_imgs, int B,
+                                 int pitch, int64_t fs)
+{
+    const OrbgGeom &G = c->geom;
+    if (G.L < 2) return hipSuccess;
+    if (c->pyr_ok) {
+        const OrbgLevel &L0 = G.lv[0];
+        const uint8_t *img_end = d_imgs + (int64_t)(B - 1) * fs + (int64_t)(L0.h - 1) * pitch + L0.w;
+        PROF_LAUNCH(c, "resize",
+                    hipLaunchKernelGGL(k_pyramid, dim3(c->pyr_args.nband * B), dim3(c->pyr_wg), 0, st,
+                                       c->pyr_args, c->d_ptab, c->d_ytab4, c->d_bands, d_imgs, fs,
+                                       pitch, img_end, c->d_pyr, B));
+        return hipGetLastError();
+    }
+    for (int l = 1; l < G.L; l++) {
+        const OrbgLevel &L = G.lv[l], &P = G.lv[l - 1];
+        const uint8_t *src = (l == 1) ? d_imgs : c->d_pyr + P.pyr_off;
+        const int64_t sfs = (l == 1) ? fs : G.pyr_frame;
+        const int spitch = (l == 1) ? pitch : P.pitch;
+        dim3 grid((L.w + 255) / 256, (L.h + 16 * ORBG_RZ_NT - 1) / (16 * ORBG_RZ_NT), B);
+        PROF_LAUNCH(c, "resize",
+                    hipLaunchKernelGGL(k_resize, grid, dim3(256), L.rz_pitch * L.rz_rows, st,
+                                       src, sfs, spitch, P.w, c->d_pyr + L.pyr_off, G.pyr_frame,
+                                       L.pitch, L.w, L.h, c->d_rtab + L.xtab_off,
+                                       c->d_rtab + L.ytab_off, L.bulk_end, L.rz_pitch));
+    }
+    return hipGetLastError();
+}
+
 // FAST cells [cb, cb + cn) of every frame on `st` (k_fast2 where the plan picked a pitch)
 static hipError_t launch_fast_cells(orbg_ctx *c, hipStream_t st, const uint8_t *d_imgs, int B,
                                     int pitch, int64_t fs, int cb, int cn)
@@ -1076,19 +1246,7 @@ static int launch_extract_pipe(orbg_ctx *c, const uint8_t *d_imgs, int B, int pi
             HIPCHK(hipStreamWaitEvent(st, c->ev_back[s], 0));
             c->back_pending[s] = false;
         }
-        for (int l = 1; l < G.L; l++) {
-            const OrbgLevel &L = G.lv[l], &P = G.lv[l - 1];
-            const uint8_t *src = (l == 1) ? d_imgs : c->d_pyr + P.pyr_off;
-            const int64_t sfs = (l == 1) ? fs : G.pyr_frame;
-            const int spitch = (l == 1) ? pitch : P.pitch;
-            dim3 grid((L.w + 255) / 256, (L.h + 16 * ORBG_RZ_NT - 1) / (16 * ORBG_RZ_NT), B);
-            PROF_LAUNCH(c, "resize",
-                        hipLaunchKernelGGL(k_resize, grid, dim3(256), L.rz_pitch * L.rz_rows, st,
-                                           src, sfs, spitch, P.w, c->d_pyr + L.pyr_off,
-                                           G.pyr_frame, L.pitch, L.w, L.h,
-                                           c->d_rtab + L.xtab_off, c->d_rtab + L.ytab_off,
-                                           L.bulk_end, L.rz_pitch));
-        }
+        HIPCHK(launch_pyramid(c, st, d_imgs, B, pitch, fs));
         HIPCHK(launch_fast_cells(c, st, d_imgs, B, pitch, fs, 0, G.ncells));
         HIPCHK(hipEventRecord(c->ev_cells[s], st));
         PROF_LAUNCH(c, "blur",
@@ -1174,18 +1332,7 @@ static int launch_extract(orbg_ctx *c, const uint8_t *d_imgs, int B, int pitch, 
         HIPCHK(hipStreamWaitEvent(c->ostream, c->ev_fast, 0));
         HIPCHK(launch_fast(c->ostream, 0, n0));
     }
-    for (int l = 1; l < G.L; l++) {
-        const OrbgLevel &L = G.lv[l], &P = G.lv[l - 1];
-        const uint8_t *src = (l == 1) ? d_imgs : c->d_pyr + P.pyr_off;
-        const int64_t sfs = (l == 1) ? fs : G.pyr_frame;
-        const int spitch = (l == 1) ? pitch : P.pitch;
-        dim3 grid((L.w + 255) / 256, (L.h + 16 * ORBG_RZ_NT - 1) / (16 * ORBG_RZ_NT), B);
-        PROF_LAUNCH(c, "resize",
-                    hipLaunchKernelGGL(k_resize, grid, dim3(256), L.rz_pitch * L.rz_rows, st,
-                                       src, sfs, spitch, P.w, c->d_pyr + L.pyr_off, G.pyr_frame,
-                                       L.pitch, L.w, L.h, c->d_rtab + L.xtab_off,
-                                       c->d_rtab + L.ytab_off, L.bulk_end, L.rz_pitch));
-    }
+    HIPCHK(launch_pyramid(c, st, d_imgs, B, pitch, fs));
     if (fast0) {
         HIPCHK(launch_fast(st, n0, G.ncells - n0));
     } else {

@@ -8,7 +8,7 @@ from collections import defaultdict
 acc = defaultdict(lambda: defaultdict(list))
 for path in glob.glob(sys.argv[1] + "/*/run_counter_collection.csv"):
     for r in csv.DictReader(open(path)):
-        name = r["Kernel_Name"].split("(")[0].replace("orbg::", "").strip()
+        name = r["Kernel_Name"].split("(")[0].replace("void ", "").replace("orbg::", "").strip()
         if not name.startswith("k_"):
             continue
         acc[name][r["Counter_Name"]].append(float(r["Counter_Value"]))
