@@ -29,6 +29,7 @@ namespace orbg {
 
 void prof_begin(void *prof, hipStream_t s, const char *n, hipEvent_t *a);
 void prof_end(void *prof, hipStream_t s, const char *n, hipEvent_t a);
+bool prof_skip_name(const char *n);
 
 #define TH_LOW 50
 #define HISTO_LENGTH 30
@@ -768,6 +769,7 @@ __global__ __launch_bounds__(RESOLVE_T) void k_init_resolve_pairs(
 // ---------------------------------------------------------------------------
 #define PL(prof, st, name, ...)                                                            \
     do {                                                                                   \
+        if (prof_skip_name(name)) break;                                                   \
         hipEvent_t a_ = nullptr;                                                           \
         prof_begin(prof, st, name, &a_);                                                   \
         __VA_ARGS__;                                                                       \

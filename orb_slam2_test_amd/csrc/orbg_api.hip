@@ -182,8 +182,17 @@ struct Prof {
 }  // namespace orbg
 
 // events on `st`, the stream the kernel is launched on (a local in every caller)
+// Developer what-if knob ORBG_SKIP=<names>: launches whose profile name is listed are not
+// issued (their consumers read the previous batch's buffers), so a bench run shows what a
+// kernel costs inside the overlapped pipeline.  Wrong results; never set in production.
+static bool prof_skip(const char *name)
+{
+    static const char *skip = getenv("ORBG_SKIP");
+    return skip && strstr(skip, name);
+}
 #define PROF_LAUNCH(ctxp, name, ...)                                                       \
     do {                                                                                   \
+        if (prof_skip(name)) break;                                                        \
         hipEvent_t ev_a_ = nullptr;                                                        \
         (ctxp)->prof.begin(st, name, &ev_a_);                                              \
         __VA_ARGS__;                                                                       \
@@ -206,6 +215,12 @@ struct orbg_ctx {
     // oct_mode 0: everything on the extraction stream, 1: level 0 only, 2: all levels.
     hipStream_t ostream = nullptr;
     hipEvent_t ev_fast = nullptr, ev_oct = nullptr;
+    // pipelined front, level 0 (FAST cells + GaussianBlur need only the input images) on
+    // `fstream` beside the pyramid (ORBG_SIDE: 0 off, 1 normal priority, 2 high)
+    hipStream_t fstream = nullptr;
+    int side_mode = 2;
+    hipEvent_t ev_f0[2] = {nullptr, nullptr}, ev_b0[2] = {nullptr, nullptr},
+               ev_pfork[2] = {nullptr, nullptr};
     int oct_mode = 0;
     int blur0_mode = 0;  // measured: 2.013 vs 2.025 ms per 256 frames with it on
     int fast0_mode = 1;  // level-0 FAST cells on `ostream` beside the resize chain (ORBG_FAST0)
@@ -366,7 +381,7 @@ static void make_tables(orbg_ctx *c)
 
 static void free_plan(orbg_ctx *c)
 {
-    for (hipStream_t q : {c->stream, c->mstream, c->ostream, c->aux_stream})
+    for (hipStream_t q : {c->stream, c->mstream, c->ostream, c->aux_stream, c->fstream})
         if (q) hipStreamSynchronize(q);
     c->mat_pending[0] = c->mat_pending[1] = false;
     c->back_pending[0] = c->back_pending[1] = false;
@@ -1081,13 +1096,29 @@ extern "C" int orbg_create(int device, const orbg_params *p, orbg_ctx **out)
         c->fast_v2 = fv ? (atoi(fv) >= 2) : 1;
         const char *b0 = getenv("ORBG_BLUR0");
         c->blur0_mode = b0 ? atoi(b0) : 0;
+        const char *bp = getenv("ORBG_BACK_PRIO");  // developer A/B: normal | high (default)
+        const int oprio = (bp && !strcmp(bp, "normal")) ? 0 : prio_hi;
         if (c->oct_mode &&
-            hipStreamCreateWithPriority(&c->ostream, hipStreamNonBlocking, prio_hi) == hipSuccess) {
+            hipStreamCreateWithPriority(&c->ostream, hipStreamNonBlocking, oprio) == hipSuccess) {
             hipEventCreateWithFlags(&c->ev_fast, hipEventDisableTiming);
             hipEventCreateWithFlags(&c->ev_oct, hipEventDisableTiming);
         } else {
             c->ostream = nullptr;
             c->oct_mode = 0;
+        }
+    }
+    {
+        const char *e = getenv("ORBG_SIDE");
+        c->side_mode = e ? atoi(e) : 2;
+        if (c->side_mode && hipStreamCreateWithPriority(&c->fstream, hipStreamNonBlocking,
+                                                        c->side_mode >= 2 ? prio_hi : 0) != hipSuccess) {
+            c->fstream = nullptr;
+            c->side_mode = 0;
+        }
+        for (int i = 0; i < 2; i++) {
+            hipEventCreateWithFlags(&c->ev_f0[i], hipEventDisableTiming);
+            hipEventCreateWithFlags(&c->ev_b0[i], hipEventDisableTiming);
+            hipEventCreateWithFlags(&c->ev_pfork[i], hipEventDisableTiming);
         }
     }
     if (hipStreamCreateWithPriority(&c->mstream, hipStreamNonBlocking, mprio) != hipSuccess) {
@@ -1135,6 +1166,10 @@ extern "C" void orbg_destroy(orbg_ctx *c)
     }
     if (c->aux_stream) hipStreamDestroy(c->aux_stream);
     if (c->ostream) hipStreamDestroy(c->ostream);
+    for (int i = 0; i < 2; i++)
+        for (hipEvent_t e : {c->ev_f0[i], c->ev_b0[i], c->ev_pfork[i]})
+            if (e) hipEventDestroy(e);
+    if (c->fstream) hipStreamDestroy(c->fstream);
     if (c->ev_fast) hipEventDestroy(c->ev_fast);
     if (c->ev_oct) hipEventDestroy(c->ev_oct);
     if (c->mstream) hipStreamDestroy(c->mstream);
@@ -1246,13 +1281,32 @@ static int launch_extract_pipe(orbg_ctx *c, const uint8_t *d_imgs, int B, int pi
             HIPCHK(hipStreamWaitEvent(st, c->ev_back[s], 0));
             c->back_pending[s] = false;
         }
+        const bool side = c->fstream && G.L > 1;
+        const int n0 = side ? G.lv[1].cell_base : 0, tb1 = side ? c->tile_base[1] : 0;
+        if (side) {
+            // level 0 beside the pyramid: FAST cells, then its GaussianBlur
+            HIPCHK(hipEventRecord(c->ev_pfork[s], st));
+            HIPCHK(hipStreamWaitEvent(c->fstream, c->ev_pfork[s], 0));
+            {
+                hipStream_t st = c->fstream;  // PROF_LAUNCH records on `st`
+                HIPCHK(launch_fast_cells(c, st, d_imgs, B, pitch, fs, 0, n0));
+                HIPCHK(hipEventRecord(c->ev_f0[s], st));
+                PROF_LAUNCH(c, "blur",
+                            hipLaunchKernelGGL(k_blur, dim3(tb1 * B), dim3(256), 0, st, c->d_geom,
+                                               c->d_tile_base, d_imgs, fs, pitch, c->d_pyr,
+                                               c->d_blur, 0, tb1));
+                HIPCHK(hipEventRecord(c->ev_b0[s], st));
+            }
+        }
         HIPCHK(launch_pyramid(c, st, d_imgs, B, pitch, fs));
-        HIPCHK(launch_fast_cells(c, st, d_imgs, B, pitch, fs, 0, G.ncells));
+        HIPCHK(launch_fast_cells(c, st, d_imgs, B, pitch, fs, n0, G.ncells - n0));
+        if (side) HIPCHK(hipStreamWaitEvent(st, c->ev_f0[s], 0));
         HIPCHK(hipEventRecord(c->ev_cells[s], st));
         PROF_LAUNCH(c, "blur",
-                    hipLaunchKernelGGL(k_blur, dim3(c->total_tiles * B), dim3(256), 0, st,
+                    hipLaunchKernelGGL(k_blur, dim3((c->total_tiles - tb1) * B), dim3(256), 0, st,
                                        c->d_geom, c->d_tile_base, d_imgs, fs, pitch, c->d_pyr,
-                                       c->d_blur, 0, c->total_tiles));
+                                       c->d_blur, tb1, c->total_tiles - tb1));
+        if (side) HIPCHK(hipStreamWaitEvent(st, c->ev_b0[s], 0));
         HIPCHK(hipEventRecord(c->ev_front[s], st));
     }
     hipStream_t st = c->ostream;  // the back (PROF_LAUNCH records on `st`)
@@ -2078,6 +2132,7 @@ void prof_end(void *prof, hipStream_t s, const char *n, hipEvent_t a)
 {
     ((Prof *)prof)->end(s, n, a);
 }
+bool prof_skip_name(const char *n) { return prof_skip(n); }
 }  // namespace orbg
 
 // ---------------------------------------------------------------------------
