@@ -11,6 +11,8 @@ import numpy as np
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(HERE, "lib", "liborbg.so")
+if os.environ.get("ORBG_LIB_VARIANT"):  # developer A/B: a build in lib/<variant>/ (csrc make OUT=)
+    LIB_PATH = os.path.join(HERE, "lib", os.environ["ORBG_LIB_VARIANT"], "liborbg.so")
 MAX_LEVELS = 16
 
 ORBG_OK = 0

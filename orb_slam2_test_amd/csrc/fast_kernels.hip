@@ -37,7 +37,9 @@ namespace orbg {
 //                 sit where pixels 0-1 sit in tA
 //   sc [RH+2][P]  u8 scores at sc[ry + 1][4 + 4gg + i], zero border
 //   list u16      pretest survivors: ry << 8 | gg << 2 | half << 1 | dark
+#ifndef FC2_CPW
 #define FC2_CPW 2  // consecutive cells per wave (shared halo lines in L1, fewer workgroups)
+#endif
 
 // one cell, wave-uniform (scalar registers)
 struct Fc2Cell {
