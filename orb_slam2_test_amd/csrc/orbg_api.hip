@@ -185,10 +185,12 @@ struct Prof {
 // Developer what-if knob ORBG_SKIP=<names>: launches whose profile name is listed are not
 // issued (their consumers read the previous batch's buffers), so a bench run shows what a
 // kernel costs inside the overlapped pipeline.  Wrong results; never set in production.
+static int g_extract_batches = 0;  // batches issued (ORBG_SKIP_AFTER)
 static bool prof_skip(const char *name)
 {
     static const char *skip = getenv("ORBG_SKIP");
-    return skip && strstr(skip, name);
+    static const int after = getenv("ORBG_SKIP_AFTER") ? atoi(getenv("ORBG_SKIP_AFTER")) : 0;
+    return skip && strstr(skip, name) && g_extract_batches > after;
 }
 #define PROF_LAUNCH(ctxp, name, ...)                                                       \
     do {                                                                                   \
@@ -220,7 +222,8 @@ struct orbg_ctx {
     hipStream_t fstream = nullptr;
     int side_mode = 2;
     hipEvent_t ev_f0[2] = {nullptr, nullptr}, ev_b0[2] = {nullptr, nullptr},
-               ev_pfork[2] = {nullptr, nullptr};
+               ev_pfork[2] = {nullptr, nullptr}, ev_pyr[2] = {nullptr, nullptr};
+    bool blur_side = false;  // ORBG_BLUR_SIDE
     int oct_mode = 0;
     int blur0_mode = 0;  // measured: 2.013 vs 2.025 ms per 256 frames with it on
     int fast0_mode = 1;  // level-0 FAST cells on `ostream` beside the resize chain (ORBG_FAST0)
@@ -1119,7 +1122,10 @@ extern "C" int orbg_create(int device, const orbg_params *p, orbg_ctx **out)
             hipEventCreateWithFlags(&c->ev_f0[i], hipEventDisableTiming);
             hipEventCreateWithFlags(&c->ev_b0[i], hipEventDisableTiming);
             hipEventCreateWithFlags(&c->ev_pfork[i], hipEventDisableTiming);
+            hipEventCreateWithFlags(&c->ev_pyr[i], hipEventDisableTiming);
         }
+        const char *bs = getenv("ORBG_BLUR_SIDE");
+        c->blur_side = bs ? atoi(bs) != 0 : false;
     }
     if (hipStreamCreateWithPriority(&c->mstream, hipStreamNonBlocking, mprio) != hipSuccess) {
         hipStreamDestroy(c->aux_stream);
@@ -1167,7 +1173,7 @@ extern "C" void orbg_destroy(orbg_ctx *c)
     if (c->aux_stream) hipStreamDestroy(c->aux_stream);
     if (c->ostream) hipStreamDestroy(c->ostream);
     for (int i = 0; i < 2; i++)
-        for (hipEvent_t e : {c->ev_f0[i], c->ev_b0[i], c->ev_pfork[i]})
+        for (hipEvent_t e : {c->ev_f0[i], c->ev_b0[i], c->ev_pfork[i], c->ev_pyr[i]})
             if (e) hipEventDestroy(e);
     if (c->fstream) hipStreamDestroy(c->fstream);
     if (c->ev_fast) hipEventDestroy(c->ev_fast);
@@ -1299,13 +1305,27 @@ static int launch_extract_pipe(orbg_ctx *c, const uint8_t *d_imgs, int B, int pi
             }
         }
         HIPCHK(launch_pyramid(c, st, d_imgs, B, pitch, fs));
+        // blur_side: levels 1.. of the GaussianBlur on the side stream too, beside the FAST
+        // cells of levels 1.. (both need only the pyramid)
+        const bool bside = side && c->blur_side;
+        if (bside) {
+            HIPCHK(hipEventRecord(c->ev_pyr[s], st));
+            HIPCHK(hipStreamWaitEvent(c->fstream, c->ev_pyr[s], 0));
+            hipStream_t st = c->fstream;  // PROF_LAUNCH records on `st`
+            PROF_LAUNCH(c, "blur",
+                        hipLaunchKernelGGL(k_blur, dim3((c->total_tiles - tb1) * B), dim3(256), 0,
+                                           st, c->d_geom, c->d_tile_base, d_imgs, fs, pitch,
+                                           c->d_pyr, c->d_blur, tb1, c->total_tiles - tb1));
+            HIPCHK(hipEventRecord(c->ev_b0[s], st));
+        }
         HIPCHK(launch_fast_cells(c, st, d_imgs, B, pitch, fs, n0, G.ncells - n0));
         if (side) HIPCHK(hipStreamWaitEvent(st, c->ev_f0[s], 0));
         HIPCHK(hipEventRecord(c->ev_cells[s], st));
-        PROF_LAUNCH(c, "blur",
-                    hipLaunchKernelGGL(k_blur, dim3((c->total_tiles - tb1) * B), dim3(256), 0, st,
-                                       c->d_geom, c->d_tile_base, d_imgs, fs, pitch, c->d_pyr,
-                                       c->d_blur, tb1, c->total_tiles - tb1));
+        if (!bside)
+            PROF_LAUNCH(c, "blur",
+                        hipLaunchKernelGGL(k_blur, dim3((c->total_tiles - tb1) * B), dim3(256), 0,
+                                           st, c->d_geom, c->d_tile_base, d_imgs, fs, pitch,
+                                           c->d_pyr, c->d_blur, tb1, c->total_tiles - tb1));
         if (side) HIPCHK(hipStreamWaitEvent(st, c->ev_b0[s], 0));
         HIPCHK(hipEventRecord(c->ev_front[s], st));
     }
@@ -1363,6 +1383,7 @@ static int launch_extract(orbg_ctx *c, const uint8_t *d_imgs, int B, int pitch, 
     // the match / stereo outputs of the previous batch are stale from here on
     c->last_npairs = 0;
     c->last_nstereo = 0;
+    g_extract_batches++;
     // d_err is not cleared here: it is sticky until check_err reads it
     // this batch's slot: intermediates (pyramid, blur, FAST cells) and per-frame outputs
     const int s = c->slot ^ 1;
