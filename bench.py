@@ -38,6 +38,10 @@ FRAME_ALGO_BYTES = 2701578   # extract 2,533,578 + match 168,000
 STEREO_FRAME_ALGO_BYTES = 5235156  # 2 x extract + match
 
 
+PMC_MONO = "r02_pmc_kernels.json"       # tools/r02_profile.sh r02 (bench.py)
+PMC_STEREO = "r02_stereo_pmc_kernels.json"  # tools/r02_profile.sh r02s --stereo
+
+
 def kernel_algo_bytes(name, B, npairs, ncand, nkp, launches_per_step):
     """Algorithmic bytes of one launch of `name` (see DESIGN.md 'Kernels')."""
     lv = level_sizes()
@@ -208,16 +212,35 @@ def main():
         dist.all_reduce(e, op=dist.ReduceOp.MAX)
         elapsed = float(e.item())
     # per-kernel HIP event times (roofline): a second pass of the same K steps, so that the
-    # events recorded around every launch (~5% of a step) stay out of `value`
+    # events recorded around every launch (~5% of a step) stay out of `value`.  It runs
+    # serially (orbg_set_serial, the matching after the extraction): in the timed pass the
+    # kernels of two batches and three streams overlap, and an event pair around a kernel
+    # would time its neighbours too.
     kern = {}
     if not args.no_kernel_timing:
+        ext.ctx.set_serial(True)
+
+        def step_serial():
+            if args.stereo:
+                ext.extract_batch_device(d_frames.data_ptr(), nimg, W, H)
+                ext.ctx.sync()
+                ext.stereo_batch_device(sl, sr, synthetic.KITTI_BF,
+                                        synthetic.KITTI_BF / synthetic.KITTI_FX)
+            else:
+                ext.extract_batch_device(d_frames.data_ptr(), B, W, H)
+                ext.ctx.sync()
+                ext.match_batch_device(f1, f2, 100, 0.9, True)
+            ext.ctx.sync()
+
+        step_serial()
         ext.ctx.profile(True)
         ext.ctx.profile_reset()
         for _ in range(args.steps):
-            step()
+            step_serial()
         torch.cuda.synchronize()
         kern = ext.ctx.profile_read()
         ext.ctx.profile(False)
+        ext.ctx.set_serial(False)
         if world > 1:
             dist.barrier()
 
@@ -239,16 +262,22 @@ def main():
             dom = max(kstats, key=lambda k: kstats[k]["ms_per_step"])
             ks = kstats[dom]
             ach = ks["achieved_GBps"]
-            traffic = None
-            pmc = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+            # PMC figures of the same kernel from the committed profile of this workload
+            # (tools/r02_profile.sh -> tools/pmc_kernels.py): HBM bytes per launch and the
+            # fractions of the chip's VALU issue / LDS cycles it used
+            pk = {}
+            pmc = os.path.join(ROOT, "profiles", PMC_STEREO if args.stereo else PMC_MONO)
             if os.path.exists(pmc):
                 with open(pmc) as f:
-                    traffic = json.load(f).get(dom, {}).get("hbm_bytes_per_launch")
+                    pk = json.load(f).get(dom, {})
             roof = {"kernel": dom, "bound": "hbm", "achieved": ach, "peak": HBM_PEAK_GBS,
                     "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBS, 4) if ach else None,
-                    "traffic": traffic,
+                    "traffic": pk.get("hbm_bytes_per_launch"),
+                    "valu_frac": pk.get("valu_frac"), "lds_frac": pk.get("lds_frac"),
+                    "pmc_source": os.path.relpath(pmc, ROOT) if pk else None,
                     "algo_bytes_per_launch": ks["algo_bytes_per_launch"],
-                    "avg_launch_ms": ks["avg_launch_ms"]}
+                    "avg_launch_ms": ks["avg_launch_ms"],
+                    "timing": "serial pass (orbg_set_serial), HIP events on the launch stream"}
         fab = STEREO_FRAME_ALGO_BYTES if args.stereo else FRAME_ALGO_BYTES
         if args.stereo:
             workload = ("configs[3] KITTI00-shaped stereo 1241x376 L+R, 2000 feat/eye, 8 lvl: "

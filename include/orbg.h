@@ -215,6 +215,11 @@ int orbg_set_stream(orbg_ctx *ctx, void *stream);
  * Synchronises.  ORBG_ENOTSUP without the internal stream. */
 int orbg_set_pipeline(orbg_ctx *ctx, int enable);
 int orbg_get_pipeline(const orbg_ctx *ctx);
+/* Serial execution (measurement; no reference counterpart): with enable != 0 every
+ * extraction kernel runs on the context stream, one after the other (no pipelining, no
+ * internal streams), so per-kernel event times are the kernels' own.  Outputs unchanged.
+ * Synchronises. */
+int orbg_set_serial(orbg_ctx *ctx, int enable);
 /* per-frame trajectory summary of the last batch, written on the match stream into a
  * device buffer (order readers after orbg_match_stream, or orbg_sync): d_out[f] = keypoints of frame f (f < nframes), then
  * d_out[nframes + p] = SearchForInitialization matches of pair p (p < npairs of the last

@@ -142,6 +142,7 @@ def lib():
         "orbg_stream": (vp, [vp]),
         "orbg_set_stream": (i32, [vp, vp]),
         "orbg_set_pipeline": (i32, [vp, i32]),
+        "orbg_set_serial": (i32, [vp, i32]),
         "orbg_get_pipeline": (i32, [vp]),
         "orbg_batch_summary": (i32, [vp, vp]),
         "orbg_stereo_batch_device": (i32, [vp, vp, vp, i32, f32, f32]),
@@ -277,6 +278,11 @@ class Context:
         (orbg_set_pipeline; the batch's input images must stay unchanged until its outputs
         are complete)."""
         check(self._L.orbg_set_pipeline(self.handle, 1 if enable else 0), "orbg_set_pipeline")
+
+    def set_serial(self, enable=True):
+        """Every extraction kernel on the context stream, one after the other
+        (orbg_set_serial): per-kernel event times without overlap."""
+        check(self._L.orbg_set_serial(self.handle, 1 if enable else 0), "orbg_set_serial")
 
     def pipelined(self):
         return bool(self._L.orbg_get_pipeline(self.handle))

@@ -224,6 +224,7 @@ struct orbg_ctx {
     hipEvent_t ev_f0[2] = {nullptr, nullptr}, ev_b0[2] = {nullptr, nullptr},
                ev_pfork[2] = {nullptr, nullptr}, ev_pyr[2] = {nullptr, nullptr};
     bool blur_side = false;  // ORBG_BLUR_SIDE
+    bool serial = false;     // orbg_set_serial: no stream overlap (isolated kernel timing)
     int oct_mode = 0;
     int blur0_mode = 0;  // measured: 2.013 vs 2.025 ms per 256 frames with it on
     int fast0_mode = 1;  // level-0 FAST cells on `ostream` beside the resize chain (ORBG_FAST0)
@@ -1391,10 +1392,12 @@ static int launch_extract(orbg_ctx *c, const uint8_t *d_imgs, int B, int pitch, 
     c->d_blur = c->blur_slot[s];
     c->d_cell_cnt = c->cnt_slot[s];
     c->d_cell_kp = c->ckp_slot[s];
-    if (c->pipelined) return launch_extract_pipe(c, d_imgs, B, pitch, fs, s);
+    if (c->pipelined && !c->serial) return launch_extract_pipe(c, d_imgs, B, pitch, fs, s);
+    // serial (orbg_set_serial): every kernel on the caller's stream, one after the other
+    const int oct_mode = c->serial ? 0 : c->oct_mode;
     // fast0: the level-0 FAST cells and quadtree need only the input images, so they run on
     // the quadtree stream beside the resize chain (latency-bound small launches)
-    const bool fast0 = c->fast0_mode && c->oct_mode && G.L > 1;
+    const bool fast0 = c->fast0_mode && oct_mode && G.L > 1;
     const int n0 = G.L > 1 ? G.lv[1].cell_base : G.ncells;
     // blur0: the level-0 GaussianBlur follows them there (ORBG_BLUR0)
     const bool blur0 = fast0 && c->blur0_mode;
@@ -1412,20 +1415,20 @@ static int launch_extract(orbg_ctx *c, const uint8_t *d_imgs, int B, int pitch, 
         HIPCHK(launch_fast(st, n0, G.ncells - n0));
     } else {
         HIPCHK(launch_fast(st, 0, G.ncells));
-        if (c->oct_mode) {
+        if (oct_mode) {
             HIPCHK(hipEventRecord(c->ev_fast, st));
             HIPCHK(hipStreamWaitEvent(c->ostream, c->ev_fast, 0));
         }
     }
     {
         // PROF_LAUNCH records on `st`
-        hipStream_t st = c->oct_mode ? c->ostream : c->stream;
+        hipStream_t st = oct_mode ? c->ostream : c->stream;
         PROF_LAUNCH(c, "octree",
                     hipLaunchKernelGGL(k_octree_lds, dim3(B, 1), dim3(512),
                                        oct_lds_bytes(c->oct_dims[0]), st, c->d_geom,
                                        c->d_cell_cnt, c->d_cell_kp, c->d_keys, c->d_act,
                                        c->d_lvl_kp, c->d_lvl_cnt, c->d_err, c->oct_dims[0]));
-        if (c->oct_mode == 2 && G.L > 1) {
+        if (oct_mode == 2 && G.L > 1) {
             // levels 1.. need their FAST cells (launched on the extraction stream under fast0)
             if (fast0) {
                 HIPCHK(hipEventRecord(c->ev_fast, c->stream));
@@ -1442,19 +1445,19 @@ static int launch_extract(orbg_ctx *c, const uint8_t *d_imgs, int B, int pitch, 
                         hipLaunchKernelGGL(k_blur, dim3(tb1 * B), dim3(256), 0, st, c->d_geom,
                                            c->d_tile_base, d_imgs, fs, pitch, c->d_pyr,
                                            c->d_blur, 0, tb1));
-        if (c->oct_mode) HIPCHK(hipEventRecord(c->ev_oct, st));
+        if (oct_mode) HIPCHK(hipEventRecord(c->ev_oct, st));
     }
     PROF_LAUNCH(c, "blur",
                 hipLaunchKernelGGL(k_blur, dim3((c->total_tiles - tb0) * B), dim3(256), 0, st,
                                    c->d_geom, c->d_tile_base, d_imgs, fs, pitch, c->d_pyr,
                                    c->d_blur, tb0, c->total_tiles - tb0));
-    if (c->oct_mode != 2 && G.L > 1)
+    if (oct_mode != 2 && G.L > 1)
         PROF_LAUNCH(c, "octree",
                     hipLaunchKernelGGL(k_octree_lds, dim3(B, G.L - 1), dim3(512),
                                        oct_lds_bytes(c->oct_dims[1]), st, c->d_geom,
                                        c->d_cell_cnt, c->d_cell_kp, c->d_keys, c->d_act,
                                        c->d_lvl_kp, c->d_lvl_cnt, c->d_err, c->oct_dims[1]));
-    if (c->oct_mode) HIPCHK(hipStreamWaitEvent(st, c->ev_oct, 0));
+    if (oct_mode) HIPCHK(hipStreamWaitEvent(st, c->ev_oct, 0));
     PROF_LAUNCH(c, "octree_big",
                 hipLaunchKernelGGL(k_octree, dim3(G.L, B), dim3(ORBG_OCT_THREADS), 0, st,
                                    c->d_geom, c->d_cell_cnt, c->d_cell_kp, c->d_keys, c->d_knode,
@@ -1645,6 +1648,16 @@ extern "C" int orbg_set_pipeline(orbg_ctx *c, int enable)
 }
 
 extern "C" int orbg_get_pipeline(const orbg_ctx *c) { return c ? c->pipelined : 0; }
+
+extern "C" int orbg_set_serial(orbg_ctx *c, int enable)
+{
+    if (!c) return set_err(ORBG_EINVAL, "ctx is NULL");
+    int rc = sync_all(c);
+    if (rc) return rc;
+    c->serial = enable != 0;
+    c->back_pending[0] = c->back_pending[1] = false;
+    return ORBG_OK;
+}
 
 extern "C" int orbg_batch_stats(orbg_ctx *c, int64_t *ncand, int64_t *nkp)
 {
