@@ -81,40 +81,78 @@ def level_sizes():
     return sizes
 
 
-def cpu_baseline_stereo(lefts, rights, seconds=10.0):
-    """oracle/ (C restatement, one thread): extract L + R + ComputeStereoMatches per stereo
-    frame, as many frames as fit in `seconds`."""
+def cpu_baseline_stereo(lefts, rights, threads, nframes, nframes_1core=8):
+    """oracle/ (C restatement) on host threads, as the mono baseline: extract L + R +
+    ComputeStereoMatches per stereo frame, `nframes` frames over `threads` threads (ctypes
+    calls release the GIL), and `nframes_1core` frames on one thread."""
+    from concurrent.futures import ThreadPoolExecutor
     from oracle import pyoracle as O
     from orb_slam2_test_amd import synthetic as S
     p = O.params(nfeatures=NFEAT, nlevels=NLEV)
-    t0 = time.perf_counter()
-    n = 0
-    while time.perf_counter() - t0 < seconds:
-        i = n % len(lefts)
+
+    def one(i):
+        i %= len(lefts)
         lft = O.extract(p, lefts[i], with_pyramid=True)
         rgt = O.extract(p, rights[i], with_pyramid=True)
         O.stereo_matches(p, lft, rgt, W, H, S.KITTI_BF, S.KITTI_BF / S.KITTI_FX)
-        n += 1
-    dt = time.perf_counter() - t0
-    return {"value": round(n / dt, 3), "unit": "stereo frames/s", "cores": 1, "kind": "port",
+
+    def run(n, th):
+        t0 = time.perf_counter()
+        with ThreadPoolExecutor(th) as pool:
+            list(pool.map(one, range(n)))
+        return time.perf_counter() - t0
+
+    dt = run(nframes, threads)
+    dt1 = run(nframes_1core, 1)
+    ncpu, model = host_cpu()
+    return {"value": round(nframes / dt, 3), "unit": "stereo frames/s", "cores": threads,
+            "kind": "port", "value_1core": round(nframes_1core / dt1, 3),
+            "host_logical_cpus": ncpu, "host_cpu_model": model,
             "sample": ("%d synthetic 1241x376 stereo frames (extract L+R 2000 feat/8 lvl + "
-                       "ComputeStereoMatches), oracle/ C restatement -O3, 1 thread, %.1f s wall"
-                       % (n, dt))}
+                       "ComputeStereoMatches), oracle/ C restatement -O3, %d threads, %.1f s "
+                       "wall; 1 thread: %d frames, %.1f s" % (nframes, threads, dt,
+                                                             nframes_1core, dt1))}
 
 
-def cpu_baseline(frames, threads, nframes):
+def host_cpu():
+    """The GPU box's host: logical CPUs (std::thread::hardware_concurrency) and the model
+    name lscpu prints (/proc/cpuinfo)."""
+    model = None
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    model = line.split(":", 1)[1].strip()
+                    break
+    except OSError:
+        pass
+    return os.cpu_count(), model
+
+
+def cpu_baseline(frames, threads, nframes, nframes_1core=32):
+    """oracle/ (C restatement) on host pthreads: `threads` threads over `nframes` frames,
+    and one thread over `nframes_1core` frames (the reference's own single-threaded
+    Tracking loop, mono_kitti.cc:78-90, extracts one frame per call)."""
     from oracle import pyoracle as O
     p = O.params(nfeatures=NFEAT, nlevels=NLEV)
-    idx = np.arange(nframes) % len(frames)
-    sample = np.ascontiguousarray(frames[idx])
-    t0 = time.perf_counter()
-    O.frames_batch(p, sample, nthreads=threads, window=100, nnratio=0.9)
-    dt = time.perf_counter() - t0
+
+    def run(n, th):
+        idx = np.arange(n) % len(frames)
+        sample = np.ascontiguousarray(frames[idx])
+        t0 = time.perf_counter()
+        O.frames_batch(p, sample, nthreads=th, window=100, nnratio=0.9)
+        return time.perf_counter() - t0
+
+    dt = run(nframes, threads)
+    dt1 = run(nframes_1core, 1)
+    ncpu, model = host_cpu()
     return {"value": round(nframes / dt, 3), "unit": "frames/s", "cores": threads,
-            "kind": "port",
+            "kind": "port", "value_1core": round(nframes_1core / dt1, 3),
+            "host_logical_cpus": ncpu, "host_cpu_model": model,
             "sample": ("%d synthetic 1241x376 frames (extract 2000 feat/8 lvl + knn2 + "
                        "SearchForInitialization vs t-1), oracle/ C restatement -O3, %d pthreads, "
-                       "%.1f s wall" % (nframes, threads, dt))}
+                       "%.1f s wall; 1 thread: %d frames, %.1f s"
+                       % (nframes, threads, dt, nframes_1core, dt1))}
 
 
 def main():
@@ -151,7 +189,10 @@ def main():
         frames = np.empty((2 * B, H, W), np.uint8)
         frames[0::2], frames[1::2] = lefts, rights
     else:
-        frames = synthetic.sequence(B, H, W, seed=synthetic.DEFAULT_SEED + 1000 * rank)
+        # batched-sequence partition (sequence.run_sharded): rank r owns frames
+        # [r*B, (r+1)*B) of one cyclic B*world-frame sequence and extracts them plus the frame
+        # before the block (1-frame halo), so its B pairs (t-1, t) match with no exchange
+        frames = synthetic.sequence_block(B * world, rank * B, (rank + 1) * B, H, W)
     nimg = len(frames)
     d_frames = torch.from_numpy(frames).to("cuda")
     torch.cuda.synchronize()
@@ -162,9 +203,10 @@ def main():
     torch.cuda.set_stream(stream)
     ext.ctx.set_stream(stream.cuda_stream)
     ext.ctx.set_pipeline(bool(args.pipeline))
-    f1 = ((np.arange(B) - 1) % B).astype(np.int32)
-    f2 = np.arange(B, dtype=np.int32)
-    summary = torch.zeros(2 * B, dtype=torch.int32, device="cuda")
+    f1 = np.arange(B, dtype=np.int32)        # local frame i (0 = the halo) ...
+    f2 = np.arange(1, B + 1, dtype=np.int32)  # ... matched to frame i + 1
+    summary = torch.zeros(2 * B + 1, dtype=torch.int32, device="cuda")
+    m12 = None
     # matching of step k (and its summary + gather) runs on liborbg's match stream while the
     # extraction of step k+1 runs on `stream` (two output slots inside liborbg)
     mstream = torch.cuda.ExternalStream(ext.ctx.match_stream())
@@ -182,12 +224,18 @@ def main():
             if world > 1:  # per-frame (keypoints, depths) of every rank (RCCL all_gather)
                 sequence.gather_summary(ssum.view(2, B), world, sizes=[B] * world)
             return
-        ext.extract_batch_device(d_frames.data_ptr(), B, W, H)
+        nonlocal m12
+        ext.extract_batch_device(d_frames.data_ptr(), nimg, W, H)
         ext.match_batch_device(f1, f2, 100, 0.9, True)
         ext.ctx.batch_summary(summary.data_ptr())
-        if world > 1:  # trajectory summary of every rank's frames (RCCL all_gather)
+        if m12 is None:
+            m12 = torch.empty((B, ext.ctx.batch_matches(None)), dtype=torch.int32, device="cuda")
+        ext.ctx.batch_matches(m12.data_ptr())  # vnMatches12 rows of the B pairs
+        if world > 1:  # per-frame outputs of every rank (RCCL all_gather)
             with torch.cuda.stream(mstream):
-                sequence.gather_summary(summary.view(2, B), world, sizes=[B] * world)
+                local = torch.stack([summary[1:B + 1], summary[B + 1:]])
+                sequence.gather_summary(local, world, sizes=[B] * world)
+                sequence.gather_rows(m12, world, sizes=[B] * world)
 
     for _ in range(args.warmup):
         step()
@@ -227,7 +275,7 @@ def main():
                 ext.stereo_batch_device(sl, sr, synthetic.KITTI_BF,
                                         synthetic.KITTI_BF / synthetic.KITTI_FX)
             else:
-                ext.extract_batch_device(d_frames.data_ptr(), B, W, H)
+                ext.extract_batch_device(d_frames.data_ptr(), nimg, W, H)
                 ext.ctx.sync()
                 ext.match_batch_device(f1, f2, 100, 0.9, True)
             ext.ctx.sync()
@@ -308,7 +356,8 @@ def main():
             "keypoints_per_image": round(nkp / nimg, 1),
         }
         if world == 1 and not args.no_cpu and args.stereo:
-            out["cpu_baseline"] = cpu_baseline_stereo(lefts, rights)
+            out["cpu_baseline"] = cpu_baseline_stereo(lefts, rights, args.cpu_threads,
+                                                      args.cpu_frames or 32 * args.cpu_threads)
         elif world == 1 and not args.no_cpu:
             n = args.cpu_frames or 256 * args.cpu_threads
             out["cpu_baseline"] = cpu_baseline(frames, args.cpu_threads, n)

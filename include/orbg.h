@@ -225,6 +225,12 @@ int orbg_set_serial(orbg_ctx *ctx, int enable);
  * d_out[nframes + p] = SearchForInitialization matches of pair p (p < npairs of the last
  * orbg_match_batch_device, 0 if none) */
 int orbg_batch_summary(orbg_ctx *ctx, int32_t *d_out);
+/* vnMatches12 of every pair of the last orbg_match_batch_device (ORBmatcher.cc:487-631's
+ * output; the batched-sequence gather of SURVEY 8e), written on the match stream into a
+ * device buffer: d_out[p * frame_cap + i] = index in frame f2[p] matched to keypoint i of
+ * frame f1[p], -1 if none or i >= keypoints of f1[p].  *frame_cap (if non-NULL) receives the
+ * row length; d_out == NULL only queries it.  ORBG_EINVAL without a match batch. */
+int orbg_batch_matches(orbg_ctx *ctx, int32_t *d_out, int32_t *frame_cap);
 /* host-side statistics of the last batch (synchronises): FAST candidates over all
  * cells/levels/frames and output keypoints over all frames (for bandwidth accounting) */
 int orbg_batch_stats(orbg_ctx *ctx, int64_t *ncandidates, int64_t *nkeypoints);

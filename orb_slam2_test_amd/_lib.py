@@ -145,6 +145,7 @@ def lib():
         "orbg_set_serial": (i32, [vp, i32]),
         "orbg_get_pipeline": (i32, [vp]),
         "orbg_batch_summary": (i32, [vp, vp]),
+        "orbg_batch_matches": (i32, [vp, vp, vp]),
         "orbg_stereo_batch_device": (i32, [vp, vp, vp, i32, f32, f32]),
         "orbg_stereo_outputs": (i32, [vp, vp, vp, vp, vp]),
         "orbg_stereo_summary": (i32, [vp, vp]),
@@ -299,6 +300,14 @@ class Context:
     def match_stream(self):
         """hipStream_t (int) of batch matching and the summary."""
         return self._L.orbg_match_stream(self.handle)
+
+    def batch_matches(self, d_out_ptr=None):
+        """vnMatches12 of every pair of the last match batch into a device buffer of
+        npairs x frame_cap int32 (orbg_batch_matches); returns frame_cap."""
+        fc = C.c_int32()
+        check(self._L.orbg_batch_matches(self.handle, C.c_void_p(d_out_ptr) if d_out_ptr else None,
+                                         C.byref(fc)), "orbg_batch_matches")
+        return fc.value
 
     def batch_summary(self, d_out_ptr):
         check(self._L.orbg_batch_summary(self.handle, C.c_void_p(d_out_ptr)), "orbg_batch_summary")

@@ -776,6 +776,30 @@ __global__ __launch_bounds__(RESOLVE_T) void k_init_resolve_pairs(
         prof_end(prof, st, name, a_);                                                      \
     } while (0)
 
+// vnMatches12 of every pair into a caller buffer [npairs][frame_cap]: entries past the
+// pair's first-frame keypoint count are -1 (the match kernels leave them unwritten)
+__global__ __launch_bounds__(256) void k_match_export(const int32_t *__restrict__ m12,
+                                                      const int32_t *__restrict__ f1,
+                                                      const int32_t *__restrict__ counts,
+                                                      int frame_cap, int npairs,
+                                                      int32_t *__restrict__ out)
+{
+    const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (i >= (int64_t)npairs * frame_cap) return;
+    const int p = (int)(i / frame_cap), k = (int)(i - (int64_t)p * frame_cap);
+    out[i] = k < counts[f1[p]] ? m12[i] : -1;
+}
+
+int launch_match_export(hipStream_t st, const int32_t *m12, const int32_t *f1,
+                        const int32_t *counts, int frame_cap, int npairs, int32_t *out)
+{
+    const int64_t n = (int64_t)npairs * frame_cap;
+    if (n <= 0) return ORBG_OK;
+    hipLaunchKernelGGL(k_match_export, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, m12,
+                       f1, counts, frame_cap, npairs, out);
+    return hipGetLastError() == hipSuccess ? ORBG_OK : ORBG_EIO;
+}
+
 int launch_knn2(hipStream_t st, const uint8_t *q, int nq, const uint8_t *t, int nt, int32_t *out,
                 void *prof)
 {

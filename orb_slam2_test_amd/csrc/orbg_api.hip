@@ -59,6 +59,8 @@ int launch_pose_opt(hipStream_t st, const orbg_pose_edge *edges, const int32_t *
                     const orbg_pose_camera *cams, const float *tcw_in, double *q_out,
                     double *t_out, float *tcw_out, uint8_t *outlier, int32_t *ninliers,
                     int nframes, void *prof);
+int launch_match_export(hipStream_t st, const int32_t *m12, const int32_t *f1,
+                        const int32_t *counts, int frame_cap, int npairs, int32_t *out);
 int launch_knn2(hipStream_t st, const uint8_t *q, int nq, const uint8_t *t, int nt, int32_t *out,
                 void *prof);
 int launch_init_match_single(hipStream_t st, const orbg_keypoint *k1, const uint8_t *d1, int n1,
@@ -1685,6 +1687,22 @@ extern "C" int orbg_batch_summary(orbg_ctx *c, int32_t *d_out)
     if (c->last_npairs > 0)
         HIPCHK(hipMemcpyAsync(d_out + c->last_n, c->d_nm, c->last_npairs * sizeof(int32_t),
                               hipMemcpyDeviceToDevice, c->mstream));
+    HIPCHK(hipEventRecord(c->ev_mat[s], c->mstream));
+    c->mat_pending[s] = true;
+    return ORBG_OK;
+}
+
+extern "C" int orbg_batch_matches(orbg_ctx *c, int32_t *d_out, int32_t *frame_cap)
+{
+    if (!c || !c->gw || c->last_n <= 0) return set_err(ORBG_EINVAL, "no batch");
+    if (!c->last_npairs) return set_err(ORBG_EINVAL, "no match batch yet");
+    if (frame_cap) *frame_cap = c->geom.frame_cap;
+    if (!d_out) return ORBG_OK;
+    const int s = c->slot;
+    HIPCHK(hipStreamWaitEvent(c->mstream, c->ev_ext[s], 0));
+    int rc = launch_match_export(c->mstream, c->d_m12, c->d_pairs, c->d_counts,
+                                 c->geom.frame_cap, c->last_npairs, d_out);
+    if (rc) return set_err(rc, "k_match_export launch failed");
     HIPCHK(hipEventRecord(c->ev_mat[s], c->mstream));
     c->mat_pending[s] = true;
     return ORBG_OK;

@@ -3,15 +3,18 @@
 One process per GPU (torch.distributed, RCCL over xGMI between GPUs, gloo in the CPU tests).
 Rank r owns the contiguous block [lo, hi) of the sequence.  It extracts that block plus the
 frame before it, a 1-frame halo, so every pair (t-1, t) with t in [lo, hi) is matched
-locally with no exchange on the data path.  The only collective is one all_gather of the
-per-frame trajectory summary: keypoint count, and SearchForInitialization matches of
-(t-1, t).
+locally with no exchange on the data path.  The only collectives are all_gathers of the
+per-frame outputs: the trajectory summary (keypoint count, and
+SearchForInitialization matches of (t-1, t)) and, with `with_matches`, the match indices
+themselves: row t = vnMatches12 of (t-1, t) (ORBmatcher.cc:487-631), frame_cap int32, -1
+where keypoint i of frame t-1 has no match.
 
 The sequence is cyclic, as in bench.py: frame 0 pairs with frame N-1, so every frame costs
 exactly one extraction and one match.
 
 A backend maps a local batch `imgs` [n, h, w] (halo first) to (nkp[n], nmatch[n]) with
-nmatch[i] = matches of (i-1, i) for i >= 1.  `GpuBackend` runs liborbg's batched
+nmatch[i] = matches of (i-1, i) for i >= 1, and with `with_matches` also m12[n, cap] with
+row i = vnMatches12 of (i-1, i) (row 0 unused).  `GpuBackend` runs liborbg's batched
 device entry points (ORBextractor.extract_batch_device / match_batch_device).
 """
 import numpy as np
@@ -31,44 +34,87 @@ def local_indices(nframes, lo, hi):
     return np.concatenate([[(lo - 1) % nframes], np.arange(lo, hi)]).astype(np.int64)
 
 
-def gather_summary(local, world, group=None, sizes=None):
-    """all_gather a per-rank int32 tensor of shape [2, m_r] (row 0 keypoints, row 1
-    matches) into the global [2, N] summary, in rank (= frame) order.  Ranks may hold
-    different m_r, so blocks are padded to the largest before the collective.  Pass
-    `sizes` (every rank's m_r) when known to skip the size exchange and its host sync
-    (bench.py's fixed per-rank batch)."""
+def gather_rows(local, world, group=None, sizes=None):
+    """all_gather a per-rank tensor whose dim 0 holds m_r frames into the global tensor, in
+    rank (= frame) order.  Ranks may hold different m_r, so blocks are padded to the largest
+    before the collective.  Pass `sizes` (every rank's m_r) when known to skip the size
+    exchange and its host sync (bench.py's fixed per-rank batch)."""
     import torch
     import torch.distributed as dist
     if world == 1:
         return local
     if sizes is None:
-        m = torch.tensor([local.shape[1]], dtype=torch.int64, device=local.device)
+        m = torch.tensor([local.shape[0]], dtype=torch.int64, device=local.device)
         st = [torch.zeros_like(m) for _ in range(world)]
         dist.all_gather(st, m, group=group)
         sizes = [int(t.item()) for t in st]
     mx = max(sizes)
-    pad = torch.zeros((2, mx), dtype=local.dtype, device=local.device)
-    pad[:, :local.shape[1]] = local
+    pad = torch.zeros((mx,) + tuple(local.shape[1:]), dtype=local.dtype, device=local.device)
+    pad[:local.shape[0]] = local
     out = [torch.zeros_like(pad) for _ in range(world)]
     dist.all_gather(out, pad, group=group)
-    return torch.cat([o[:, :n] for o, n in zip(out, sizes)], dim=1)
+    return torch.cat([o[:n] for o, n in zip(out, sizes)], dim=0)
 
 
-def run_sharded(frames, world, rank, backend, group=None, device="cpu"):
+def gather_summary(local, world, group=None, sizes=None):
+    """all_gather a per-rank int32 tensor of shape [2, m_r] (row 0 keypoints, row 1
+    matches) into the global [2, N] summary (gather_rows along the frame axis)."""
+    if world == 1:
+        return local
+    return gather_rows(local.t().contiguous(), world, group, sizes).t().contiguous()
+
+
+def run_sharded(frames, world, rank, backend, group=None, device="cpu", with_matches=False):
     """Process this rank's block of the cyclic sequence `frames` [N, h, w] with `backend`
-    and return the gathered global summary as numpy (nkp[N], nmatch[N])."""
+    and return the gathered global outputs as numpy: (nkp[N], nmatch[N]), plus m12[N, cap]
+    (row t = vnMatches12 of (t-1, t)) with `with_matches`."""
     import torch
     n = len(frames)
     lo, hi = shard(n, world, rank)
     idx = local_indices(n, lo, hi)
+    m12 = None
     if len(idx):
-        nkp, nm = backend(np.ascontiguousarray(frames[idx]))
+        r = backend(np.ascontiguousarray(frames[idx]))
+        nkp, nm = r[0], r[1]
         local = np.stack([np.asarray(nkp, np.int32)[1:], np.asarray(nm, np.int32)[1:]])
+        if with_matches:
+            m12 = np.ascontiguousarray(np.asarray(r[2], np.int32)[1:])
     else:
         local = np.zeros((2, 0), np.int32)
-    t = torch.from_numpy(local).to(device)
-    g = gather_summary(t, world, group)
-    g = g.cpu().numpy()
+    g = gather_summary(torch.from_numpy(local).to(device), world, group).cpu().numpy()
+    if not with_matches:
+        return g[0], g[1]
+    if m12 is None:  # an empty block still takes part in the collectives
+        cap = torch.zeros(1, dtype=torch.int64, device=device)
+        if world > 1:
+            import torch.distributed as dist
+            dist.all_reduce(cap, op=dist.ReduceOp.MAX, group=group)
+        m12 = np.zeros((0, int(cap.item())), np.int32)
+    elif world > 1:
+        import torch.distributed as dist
+        cap = torch.tensor([m12.shape[1]], dtype=torch.int64, device=device)
+        dist.all_reduce(cap, op=dist.ReduceOp.MAX, group=group)
+        if int(cap.item()) > m12.shape[1]:  # rows padded with -1 to the widest rank's cap
+            m12 = np.pad(m12, ((0, 0), (0, int(cap.item()) - m12.shape[1])), constant_values=-1)
+    gm = gather_rows(torch.from_numpy(m12).to(device), world, group).cpu().numpy()
+    return g[0], g[1], gm
+
+
+def run_sharded_stereo(lefts, rights, world, rank, backend, group=None, device="cpu"):
+    """Stereo frames shard with L and R of a frame on the same rank (the stereo Frame
+    constructor extracts both, Frame.cc:110-113, then ComputeStereoMatches :619-834): rank r
+    owns stereo frames [lo, hi), no halo (stereo frames are independent).  `backend` maps
+    (lefts[n], rights[n]) to (nkp_left[n], ndepth[n]); returns the gathered global
+    (nkp_left[N], ndepth[N]) as numpy."""
+    import torch
+    n = len(lefts)
+    lo, hi = shard(n, world, rank)
+    if hi > lo:
+        nkp, nd = backend(np.ascontiguousarray(lefts[lo:hi]), np.ascontiguousarray(rights[lo:hi]))
+        local = np.stack([np.asarray(nkp, np.int32), np.asarray(nd, np.int32)])
+    else:
+        local = np.zeros((2, 0), np.int32)
+    g = gather_summary(torch.from_numpy(local).to(device), world, group).cpu().numpy()
     return g[0], g[1]
 
 
@@ -76,9 +122,10 @@ class GpuBackend:
     """liborbg batch path: extract all local frames in one launch sequence, then match the
     consecutive pairs (i-1, i) on the device; only the per-frame summary leaves HBM."""
 
-    def __init__(self, extractor, window=100, nnratio=0.9, check_ori=True):
+    def __init__(self, extractor, window=100, nnratio=0.9, check_ori=True, with_matches=False):
         self.ext = extractor
         self.window, self.nnratio, self.check_ori = window, nnratio, check_ori
+        self.with_matches = with_matches
 
     def __call__(self, imgs):
         import torch
@@ -101,9 +148,17 @@ class GpuBackend:
             self.ext.match_batch_device(np.arange(n - 1), np.arange(1, n), self.window,
                                         self.nnratio, self.check_ori)
         self.ext.ctx.batch_summary(summary.data_ptr())
-        self.ext.ctx.sync()  # the summary is written on liborbg's match stream
+        if self.with_matches:
+            cap = self.ext.ctx.batch_matches(None) if n > 1 else 0
+            dm = torch.full((n, max(cap, 1)), -1, dtype=torch.int32, device="cuda")
+            if n > 1:
+                self.ext.ctx.batch_matches(dm[1:].data_ptr())
+        self.ext.ctx.sync()  # the summary / matches are written on liborbg's match stream
         s = summary.cpu().numpy()
         nkp = s[:n].copy()
         if n > 1:
             nm[1:] = s[n:2 * n - 1]
+        if self.with_matches:
+            m12 = dm.cpu().numpy()
+            return nkp, nm, m12
         return nkp, nm

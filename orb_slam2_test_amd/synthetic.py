@@ -78,6 +78,29 @@ def sequence(n, h, w, seed=DEFAULT_SEED, max_step=8, noise=2):
     return out
 
 
+def sequence_block(n_total, lo, hi, h, w, seed=DEFAULT_SEED, max_step=8, noise=2):
+    """Frames [(lo - 1) mod n_total, lo, ..., hi - 1] -- a rank's block of the cyclic
+    batched-sequence partition plus its 1-frame halo (sequence.local_indices) -- of an
+    n_total-frame sequence panning over one canvas like sequence().  Each frame's pixel
+    jitter comes from its own generator (seed, t), so a rank materialises only its block."""
+    from .sequence import local_indices
+    rng = np.random.Generator(np.random.PCG64(seed + 1))
+    steps = rng.integers(-max_step, max_step + 1, size=(n_total, 2))
+    steps[0] = 0
+    pos = np.cumsum(steps, axis=0)
+    pos -= pos.min(axis=0)
+    base = canvas(h + int(pos[:, 0].max()) + 1, w + int(pos[:, 1].max()) + 1, seed)
+    idx = local_indices(n_total, lo, hi)
+    out = np.empty((len(idx), h, w), np.uint8)
+    for j, t in enumerate(idx):
+        y, x = pos[t]
+        crop = base[y:y + h, x:x + w]
+        jr = np.random.Generator(np.random.PCG64([seed + 7, int(t)]))
+        jitter = jr.integers(-noise, noise + 1, size=(h, w)).astype(np.float32)
+        out[j] = np.clip(np.rint(crop + jitter), 0, 255).astype(np.uint8)
+    return out
+
+
 def stereo_pair(h, w, seed=DEFAULT_SEED, noise=2, d_min=4.0, d_max=60.0, n_objects=6):
     """A rectified synthetic stereo pair (left, right) u8 and the true disparity map.
 

@@ -76,3 +76,112 @@ def test_sharded_sequence_matches_single_process(oracle, world):
     for rank, nkp, nm in res:
         assert np.array_equal(nkp, ref_nkp), rank
         assert np.array_equal(nm, ref_nm), rank
+
+
+def _oracle_pairs(O, p, imgs, window=100, nnratio=0.9):
+    """Per-frame (nkp, nmatch, vnMatches12) of consecutive pairs (i-1, i), as
+    orc_frames_batch computes them (SearchForInitialization with prevMatched = the keypoints
+    of frame i-1, bounds = the image), row 0 unused; rows padded with -1 to CAP."""
+    n, h, w = imgs.shape
+    ex = [O.extract(p, im) for im in imgs]
+    nkp = np.array([len(e["kps"]) for e in ex], np.int32)
+    nm = np.zeros(n, np.int32)
+    m12 = np.full((n, CAP), -1, np.int32)
+    for i in range(1, n):
+        a, b = ex[i - 1], ex[i]
+        prev = np.ascontiguousarray(np.stack([a["kps"]["x"], a["kps"]["y"]], 1))
+        k, m, _ = O.search_for_initialization(a["kps"], a["desc"], b["kps"], b["desc"], prev,
+                                              (0, w, 0, h), window, nnratio, True)
+        nm[i] = k
+        m12[i, :len(m)] = m
+    return nkp, nm, m12
+
+
+CAP = 2 * 500 + 256
+
+
+def _worker_matches(rank, world, port, frames, q):
+    import torch.distributed as dist
+    from oracle import pyoracle as O
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        p = O.params(nfeatures=500)
+        nkp, nm, m12 = sequence.run_sharded(frames, world, rank,
+                                            lambda imgs: _oracle_pairs(O, p, imgs),
+                                            with_matches=True)
+        q.put((rank, nkp.tolist(), nm.tolist(), m12.tolist()))
+    finally:
+        dist.destroy_process_group()
+
+
+def _worker_stereo(rank, world, port, lefts, rights, q):
+    import torch.distributed as dist
+    from oracle import pyoracle as O
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        nkp, nd = sequence.run_sharded_stereo(lefts, rights, world, rank,
+                                              lambda L, R: _oracle_stereo(O, L, R))
+        q.put((rank, nkp.tolist(), nd.tolist()))
+    finally:
+        dist.destroy_process_group()
+
+
+def _oracle_stereo(O, lefts, rights):
+    p = O.params(nfeatures=500)
+    nkp, nd = [], []
+    for L, R in zip(lefts, rights):
+        el = O.extract(p, L, with_pyramid=True)
+        er = O.extract(p, R, with_pyramid=True)
+        h, w = L.shape
+        ur, depth = O.stereo_matches(p, el, er, w, h, synthetic.KITTI_BF,
+                                     synthetic.KITTI_BF / synthetic.KITTI_FX)
+        nkp.append(len(el["kps"]))
+        nd.append(int((depth[:len(el["kps"])] > 0).sum()))
+    return np.array(nkp, np.int32), np.array(nd, np.int32)
+
+
+def _spawn(target, world, *args):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=target, args=(r, world, port) + args + (q,)) for r in range(world)]
+    for pr in procs:
+        pr.start()
+    res = [q.get(timeout=300) for _ in range(world)]
+    for pr in procs:
+        pr.join(timeout=60)
+        assert pr.exitcode == 0
+    return res
+
+
+def test_sharded_match_indices_equal_single_process(oracle):
+    """the gathered per-frame vnMatches12 rows equal the single-process ones
+    (world 2, block + 1-frame halo, cyclic)."""
+    frames = synthetic.sequence(5, H, W, seed=synthetic.DEFAULT_SEED + 9)
+    p = oracle.params(nfeatures=500)
+    # single process over the cyclic sequence: frame t pairs with t-1 (frame 0 with N-1)
+    cyc = np.concatenate([frames[-1:], frames])
+    ref_nkp, ref_nm, ref_m12 = _oracle_pairs(oracle, p, cyc)
+    ref_nkp, ref_nm, ref_m12 = ref_nkp[1:], ref_nm[1:], ref_m12[1:]
+    assert ref_nm.sum() > 0
+    for rank, nkp, nm, m12 in _spawn(_worker_matches, 2, frames):
+        assert np.array_equal(nkp, ref_nkp), rank
+        assert np.array_equal(nm, ref_nm), rank
+        assert np.array_equal(np.asarray(m12), ref_m12), rank
+        # the indices are the matches the counts count
+        assert np.array_equal((np.asarray(m12) >= 0).sum(1), ref_nm)
+
+
+def test_sharded_stereo_equals_single_process(oracle):
+    """Stereo frames shard with L and R on the same rank (Frame.cc:110-113): per-frame
+    (left keypoints, valid depths) gathered over world 2 equal one process doing all."""
+    lefts, rights, _ = synthetic.stereo_sequence(3, H, W, seed=synthetic.DEFAULT_SEED + 11)
+    ref_nkp, ref_nd = _oracle_stereo(oracle, lefts, rights)
+    assert ref_nd.sum() > 0
+    for rank, nkp, nd in _spawn(_worker_stereo, 2, lefts, rights):
+        assert np.array_equal(nkp, ref_nkp), rank
+        assert np.array_equal(nd, ref_nd), rank

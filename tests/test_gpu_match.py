@@ -208,3 +208,37 @@ def test_sharded_sequence_gpu(oracle):
             nm.append(m[1:])
         assert np.array_equal(np.concatenate(nkp), ref_nkp), world
         assert np.array_equal(np.concatenate(nm), ref_nm), world
+
+
+def test_sharded_sequence_gpu_match_indices(oracle):
+    """SURVEY 8e's per-frame gather payload: the vnMatches12 rows exported by
+    orbg_batch_matches (every pair of a batch, -1 past the first frame's keypoints) for each
+    shard (block + 1-frame halo) equal the oracle's SearchForInitialization output of the
+    whole cyclic sequence, row for row."""
+    from orb_slam2_test_amd import ORBextractor, sequence, synthetic
+    n, h, w = 5, 376, 1241
+    frames = synthetic.sequence_block(n, 0, n, h, w, seed=synthetic.DEFAULT_SEED + 13)
+    # frames = [halo (frame n-1), 0 .. n-1]: the single-process reference over the cycle
+    p = oracle.params(nfeatures=2000)
+    ex = [oracle.extract(p, im) for im in frames]
+    ref = {}
+    for t in range(1, n + 1):
+        a, b = ex[t - 1], ex[t]
+        prev = np.ascontiguousarray(np.stack([a["kps"]["x"], a["kps"]["y"]], 1))
+        k, m, _ = oracle.search_for_initialization(a["kps"], a["desc"], b["kps"], b["desc"],
+                                                   prev, (0, w, 0, h), 100, 0.9, True)
+        ref[t - 1] = (k, m)  # global frame t - 1 (row of pair (t-2, t-1))
+    be = sequence.GpuBackend(ORBextractor(2000, 1.2, 8, 20, 7, max_batch=n + 1),
+                             with_matches=True)
+    glob = frames[1:]
+    for world in (1, 2):
+        for r in range(world):
+            lo, hi = sequence.shard(n, world, r)
+            k, nm, m12 = be(glob[sequence.local_indices(n, lo, hi)])
+            for i, t in enumerate(range(lo, hi)):
+                rk, rm = ref[t]
+                row = m12[i + 1]
+                assert nm[i + 1] == rk, (world, t)
+                assert np.array_equal(row[:len(rm)], rm), (world, t)
+                assert (row[len(rm):] == -1).all(), (world, t)
+                assert (row >= 0).sum() == rk
