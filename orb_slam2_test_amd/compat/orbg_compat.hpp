@@ -19,7 +19,10 @@
 //   ORB_SLAM2::ORBextractor (only when OpenCV headers are present)
 //       the reference's exact cv::InputArray / std::vector<cv::KeyPoint> / cv::OutputArray
 //       signatures, so Tracking.cc and Frame.cc compile unchanged.  This
-//       image has no OpenCV, so that block is not compiled here.
+//       image has no OpenCV: tests/test_compat_ref.py compiles and runs that block against
+//       tests/compat_stub/, a test-only stand-in of the cv:: subset it uses.
+//   orbg_reference.hpp: ORBmatcher / Optimizer call sites over the reference's own Frame,
+//       KeyFrame and MapPoint classes.
 //
 // Errors: the C ABI returns negative errno codes; this layer throws orbg_compat::Error
 // (std::runtime_error) with orbg_last_error()'s message.  There is no CPU fallback: without
@@ -284,15 +287,19 @@ namespace ORB_SLAM2 {
 
 // Drop-in for include/ORBextractor.h: same public surface, backed by liborbg.
 class ORBextractor {
+    class LazyPyramid;
+
 public:
     enum { HARRIS_SCORE = 0, FAST_SCORE = 1 };
 
     ORBextractor(int nfeatures, float scaleFactor, int nlevels, int iniThFAST, int minThFAST)
-        : ext_(nfeatures, scaleFactor, nlevels, iniThFAST, minThFAST)
+        : mvImagePyramid(this), ext_(nfeatures, scaleFactor, nlevels, iniThFAST, minThFAST),
+          levels_(nlevels), fresh_(nlevels, false)
     {
-        mvImagePyramid.resize(nlevels);
     }
     ~ORBextractor() {}
+    ORBextractor(const ORBextractor &) = delete;
+    ORBextractor &operator=(const ORBextractor &) = delete;
 
     void operator()(cv::InputArray image, cv::InputArray mask,
                     std::vector<cv::KeyPoint> &keypoints, cv::OutputArray descriptors)
@@ -314,11 +321,8 @@ public:
             descriptors.create(n, 32, CV_8U);
             std::memcpy(descriptors.getMat().data, desc.data(), desc.size());
         }
-        for (int l = 0; l < ext_.GetLevels(); l++) {
-            int w = 0, h = 0;
-            std::vector<uint8_t> lv = ext_.ImagePyramidLevel(l, &w, &h);
-            mvImagePyramid[l] = cv::Mat(h, w, CV_8U, lv.data()).clone();
-        }
+        // the pyramid stays in HBM: only stereo callers read it (Frame.cc:626, 738)
+        fresh_.assign(fresh_.size(), false);
     }
 
     int inline GetLevels() { return ext_.GetLevels(); }
@@ -331,10 +335,38 @@ public:
         return ext_.GetInverseScaleSigmaSquares();
     }
 
-    std::vector<cv::Mat> mvImagePyramid;
+private:
+    // mvImagePyramid[l]: level l of the last operator() call, downloaded from HBM on its first
+    // access after that call (std::vector<cv::Mat>'s indexing and size in the reference)
+    class LazyPyramid {
+    public:
+        explicit LazyPyramid(ORBextractor *o) : o_(o) {}
+        cv::Mat &operator[](size_t l) { return o_->level(l); }
+        const cv::Mat &operator[](size_t l) const { return o_->level(l); }
+        size_t size() const { return o_->levels_.size(); }
+
+    private:
+        ORBextractor *o_;
+    };
+
+public:
+    LazyPyramid mvImagePyramid;
 
 private:
+    cv::Mat &level(size_t l) const
+    {
+        if (!fresh_[l]) {
+            int w = 0, h = 0;
+            std::vector<uint8_t> lv = ext_.ImagePyramidLevel((int)l, &w, &h);
+            levels_[l] = cv::Mat(h, w, CV_8U, lv.data()).clone();
+            fresh_[l] = true;
+        }
+        return levels_[l];
+    }
+
     orbg_compat::Extractor ext_;
+    mutable std::vector<cv::Mat> levels_;
+    mutable std::vector<bool> fresh_;
 };
 
 }  // namespace ORB_SLAM2

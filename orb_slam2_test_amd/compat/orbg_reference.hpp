@@ -1,0 +1,505 @@
+// orbg_reference.hpp -- the reference-facing drop-in layer: the ORB_SLAM2 call sites of the
+// hot path (ORBmatcher, Optimizer) over liborbg's C ABI, written against the reference's
+// own classes.
+//
+// Every function is a template over the reference types (ORB_SLAM2::Frame, KeyFrame,
+// MapPoint) and touches only the members the reference functions it replaces touch, with
+// the same names, so ORBmatcher.cc / Optimizer.cc keep their signatures and forward to it
+// (INTEGRATION.md 3-4):
+//
+//   int ORBmatcher::SearchForInitialization(Frame &F1, Frame &F2,
+//           vector<cv::Point2f> &vbPrevMatched, vector<int> &vnMatches12, int windowSize)
+//   { return orbg_compat::ref::SearchForInitialization(ctx, mfNNratio, mbCheckOrientation,
+//                                                      F1, F2, vbPrevMatched, vnMatches12,
+//                                                      windowSize); }
+//
+// The cv:: surface used is the stable OpenCV core subset (Mat::rows/cols/at/ptr/eye/clone,
+// KeyPoint, Point2f); tests/compat_stub/ holds a test-only stand-in of exactly that subset so
+// this header is compiled and run in this repository's tests (tests/test_compat_ref.py),
+// where OpenCV is absent.
+//
+//   SearchForInitialization ......... ORBmatcher.cc:487-631 (include/ORBmatcher.h:47)
+//   SearchByProjection (last frame) .. ORBmatcher.cc:1503-1667 (ORBmatcher.h:62)
+//   SearchByProjection (local map) ... ORBmatcher.cc:59-154 (ORBmatcher.h:51)
+//   DescriptorDistance ............... ORBmatcher.cc:1846-1862 (ORBmatcher.h:128)
+//   PoseOptimization ................. Optimizer.cc:356-631 (include/Optimizer.h:49)
+//   LocalBundleAdjustment window ..... Optimizer.cc:633-851: the vertex / edge set g2o builds
+//                                      (LbaWindow), and BlockSolver<6,3>::buildSystem's block
+//                                      layout of the linearised system (block_solver.hpp:
+//                                      502-560, G2oBlockSystem)
+#pragma once
+
+#include <algorithm>
+#include <cmath>
+#include <cstring>
+#include <list>
+#include <map>
+#include <set>
+#include <type_traits>
+#include <vector>
+
+#include "orbg_compat.hpp"
+
+namespace orbg_compat {
+namespace ref {
+
+// The context behind ORBmatcher / Optimizer call sites, which the reference constructs
+// freely (ORBmatcher matcher(0.9, true) on the stack): one per process, device 0, default
+// parameters (scale factor 1.2, 8 levels: the ORBextractor settings the tracking matchers'
+// scale tables must agree with).  Created on first use.
+inline orbg_ctx *default_ctx()
+{
+    struct Holder {
+        orbg_ctx *c = nullptr;
+        Holder()
+        {
+            orbg_params p;
+            orbg_params_default(&p);
+            check(orbg_create(0, &p, &c), "orbg_create");
+        }
+        ~Holder() { orbg_destroy(c); }
+    };
+    static Holder h;
+    return h.c;
+}
+
+// cv::KeyPoint -> orbg_keypoint (field by field, the ABI's layout is its own)
+template <class KP>
+inline orbg_keypoint to_orbg(const KP &k)
+{
+    orbg_keypoint o;
+    o.x = k.pt.x;
+    o.y = k.pt.y;
+    o.size = k.size;
+    o.angle = k.angle;
+    o.response = k.response;
+    o.octave = k.octave;
+    o.class_id = k.class_id;
+    return o;
+}
+
+template <class KPV>
+inline std::vector<orbg_keypoint> keys_of(const KPV &v)
+{
+    std::vector<orbg_keypoint> out(v.size());
+    for (size_t i = 0; i < v.size(); i++) out[i] = to_orbg(v[i]);
+    return out;
+}
+
+// N x 32 CV_8U descriptor matrix (any row step) -> contiguous rows
+template <class Mat>
+inline std::vector<uint8_t> rows32(const Mat &m, int n)
+{
+    std::vector<uint8_t> out((size_t)n * 32);
+    for (int i = 0; i < n; i++) std::memcpy(&out[(size_t)i * 32], m.template ptr<uint8_t>(i), 32);
+    return out;
+}
+
+// Frame::mnMinX .. mnMaxY (static members of the reference's Frame)
+template <class FrameT>
+inline orbg_bounds bounds_of(const FrameT &)
+{
+    return orbg_bounds{FrameT::mnMinX, FrameT::mnMaxX, FrameT::mnMinY, FrameT::mnMaxY};
+}
+
+// rows 0..2 of a 4x4 CV_32F pose (Frame::mTcw, KeyFrame::GetPose())
+template <class Mat>
+inline void pose12(const Mat &T, float out[12])
+{
+    for (int r = 0; r < 3; r++)
+        for (int c = 0; c < 4; c++) out[4 * r + c] = T.template at<float>(r, c);
+}
+
+inline int DescriptorDistance(const uint8_t *a, const uint8_t *b)
+{
+    return orbg_descriptor_distance(a, b);
+}
+
+// ORBmatcher(nnratio, checkOri).SearchForInitialization(F1, F2, vbPrevMatched,
+// vnMatches12, windowSize): vbPrevMatched is updated for the matched keypoints of F1 and
+// vnMatches12 resized to F1's keypoints, as the reference does.
+template <class FrameT, class Point2fT>
+int SearchForInitialization(orbg_ctx *ctx, float nnratio, bool checkOri, FrameT &F1, FrameT &F2,
+                            std::vector<Point2fT> &vbPrevMatched, std::vector<int> &vnMatches12,
+                            int windowSize = 10)
+{
+    const int n1 = (int)F1.mvKeysUn.size(), n2 = (int)F2.mvKeysUn.size();
+    const std::vector<orbg_keypoint> k1 = keys_of(F1.mvKeysUn), k2 = keys_of(F2.mvKeysUn);
+    const std::vector<uint8_t> d1 = rows32(F1.mDescriptors, n1), d2 = rows32(F2.mDescriptors, n2);
+    std::vector<float> prev((size_t)2 * n1);
+    for (int i = 0; i < n1; i++) {
+        prev[2 * i] = vbPrevMatched[i].x;
+        prev[2 * i + 1] = vbPrevMatched[i].y;
+    }
+    const orbg_bounds b = bounds_of(F2);
+    std::vector<int32_t> m12(n1 > 0 ? n1 : 1);
+    int nm = 0;
+    check(orbg_search_for_initialization(ctx, k1.data(), d1.data(), n1, k2.data(), d2.data(), n2,
+                                         &b, prev.data(), m12.data(), windowSize, nnratio,
+                                         checkOri ? 1 : 0, &nm),
+          "orbg_search_for_initialization");
+    vnMatches12.assign(m12.begin(), m12.begin() + n1);
+    for (int i = 0; i < n1; i++) {
+        vbPrevMatched[i].x = prev[2 * i];
+        vbPrevMatched[i].y = prev[2 * i + 1];
+    }
+    return nm;
+}
+
+// mvpMapPoints[i] && mvpMapPoints[i]->Observations() > 0, the "taken" test both
+// SearchByProjection loops apply to the current frame's slots on entry
+template <class FrameT>
+inline std::vector<uint8_t> taken_of(const FrameT &F)
+{
+    std::vector<uint8_t> t(F.mvpMapPoints.size());
+    for (size_t i = 0; i < t.size(); i++)
+        t[i] = F.mvpMapPoints[i] && F.mvpMapPoints[i]->Observations() > 0;
+    return t;
+}
+
+template <class MapPointT>
+inline void mp_desc(const MapPointT *pMP, uint8_t out[32])
+{
+    std::memcpy(out, pMP->GetDescriptor().template ptr<uint8_t>(0), 32);
+}
+
+// ORBmatcher(nnratio, checkOri).SearchByProjection(CurrentFrame, LastFrame, th, bMono)
+// (Tracking::TrackWithMotionModel): writes CurrentFrame.mvpMapPoints.
+template <class FrameT>
+int SearchByProjection(orbg_ctx *ctx, bool checkOri, FrameT &CurrentFrame, const FrameT &LastFrame,
+                       float th, bool bMono)
+{
+    const int n = (int)CurrentFrame.mvKeysUn.size(), np = (int)LastFrame.mvpMapPoints.size();
+    const std::vector<orbg_keypoint> k = keys_of(CurrentFrame.mvKeysUn);
+    const std::vector<uint8_t> d = rows32(CurrentFrame.mDescriptors, n);
+    const std::vector<uint8_t> taken = taken_of(CurrentFrame);
+    std::vector<orbg_lastframe_point> pts(np > 0 ? np : 1);
+    std::vector<uint8_t> pdesc((size_t)(np > 0 ? np : 1) * 32, 0);
+    for (int i = 0; i < np; i++) {
+        orbg_lastframe_point &p = pts[i];
+        std::memset(&p, 0, sizeof(p));
+        const auto *pMP = LastFrame.mvpMapPoints[i];
+        p.octave = LastFrame.mvKeys[i].octave;
+        p.angle = LastFrame.mvKeysUn[i].angle;
+        if (!pMP) continue;
+        const auto X = pMP->GetWorldPos();
+        p.x = X.template at<float>(0);
+        p.y = X.template at<float>(1);
+        p.z = X.template at<float>(2);
+        p.flags = (!LastFrame.mvbOutlier[i] ? ORBG_MP_VALID : 0) |
+                  (pMP->Observations() > 0 ? ORBG_MP_HAS_OBS : 0);
+        mp_desc(pMP, &pdesc[(size_t)i * 32]);
+    }
+    orbg_track_camera cam;
+    std::memset(&cam, 0, sizeof(cam));
+    pose12(CurrentFrame.mTcw, cam.Tcw);
+    pose12(LastFrame.mTcw, cam.Tlw);
+    cam.fx = FrameT::fx;
+    cam.fy = FrameT::fy;
+    cam.cx = FrameT::cx;
+    cam.cy = FrameT::cy;
+    cam.bf = CurrentFrame.mbf;
+    cam.b = CurrentFrame.mb;
+    cam.mono = bMono ? 1 : 0;
+    const orbg_bounds b = bounds_of(CurrentFrame);
+    std::vector<int32_t> match(n > 0 ? n : 1);
+    int nm = 0;
+    check(orbg_search_by_projection_lastframe(ctx, k.data(), d.data(), CurrentFrame.mvuRight.data(),
+                                              n, taken.data(), &b, pts.data(), pdesc.data(), np,
+                                              &cam, th, checkOri ? 1 : 0, match.data(), &nm),
+          "orbg_search_by_projection_lastframe");
+    for (int i = 0; i < n; i++) {
+        if (match[i] >= 0)
+            CurrentFrame.mvpMapPoints[i] = LastFrame.mvpMapPoints[match[i]];
+        else if (match[i] == -2)
+            CurrentFrame.mvpMapPoints[i] = nullptr;  // rotation-consistency filter
+    }
+    return nm;
+}
+
+// ORBmatcher(nnratio).SearchByProjection(F, vpMapPoints, th) (Tracking::SearchLocalPoints;
+// the projections come from Frame::isInFrustum's mTrackProj* fields): writes
+// F.mvpMapPoints.
+template <class FrameT, class MapPointT>
+int SearchByProjection(orbg_ctx *ctx, float nnratio, FrameT &F,
+                       const std::vector<MapPointT *> &vpMapPoints, float th = 3)
+{
+    const int n = (int)F.mvKeysUn.size(), nm_in = (int)vpMapPoints.size();
+    const std::vector<orbg_keypoint> k = keys_of(F.mvKeysUn);
+    const std::vector<uint8_t> d = rows32(F.mDescriptors, n);
+    const std::vector<uint8_t> taken = taken_of(F);
+    std::vector<orbg_map_projection> mps(nm_in > 0 ? nm_in : 1);
+    std::vector<uint8_t> mdesc((size_t)(nm_in > 0 ? nm_in : 1) * 32, 0);
+    for (int j = 0; j < nm_in; j++) {
+        const MapPointT *pMP = vpMapPoints[j];
+        orbg_map_projection &m = mps[j];
+        std::memset(&m, 0, sizeof(m));
+        if (!pMP) continue;
+        m.u = pMP->mTrackProjX;
+        m.v = pMP->mTrackProjY;
+        m.ur = pMP->mTrackProjXR;
+        m.level = pMP->mnTrackScaleLevel;
+        m.view_cos = pMP->mTrackViewCos;
+        m.flags = (pMP->mbTrackInView && !pMP->isBad() ? ORBG_MP_VALID : 0) |
+                  (pMP->Observations() > 0 ? ORBG_MP_HAS_OBS : 0);
+        if (m.flags & ORBG_MP_VALID) mp_desc(pMP, &mdesc[(size_t)j * 32]);
+    }
+    const orbg_bounds b = bounds_of(F);
+    std::vector<int32_t> match(n > 0 ? n : 1);
+    int nm = 0;
+    check(orbg_search_by_projection_local(ctx, k.data(), d.data(), F.mvuRight.data(), n,
+                                          taken.data(), &b, mps.data(), mdesc.data(), nm_in, th,
+                                          nnratio, match.data(), &nm),
+          "orbg_search_by_projection_local");
+    for (int i = 0; i < n; i++)
+        if (match[i] >= 0) F.mvpMapPoints[i] = vpMapPoints[match[i]];
+    return nm;
+}
+
+// Optimizer::PoseOptimization(pFrame): one edge per keypoint with a MapPoint (index order),
+// stereo when mvuRight[i] >= 0 (Optimizer.cc:381-460); writes pFrame->SetPose(Tcw) and
+// pFrame->mvbOutlier, returns nInitialCorrespondences - nBad.
+template <class FrameT>
+int PoseOptimization(orbg_ctx *ctx, FrameT *pFrame)
+{
+    typedef typename std::decay<decltype(pFrame->mTcw)>::type MatT;
+    const int N = (int)pFrame->mvpMapPoints.size();
+    std::vector<orbg_pose_edge> edges;
+    std::vector<int> idx;
+    edges.reserve(N);
+    for (int i = 0; i < N; i++) {
+        const auto *pMP = pFrame->mvpMapPoints[i];
+        if (!pMP) continue;
+        pFrame->mvbOutlier[i] = false;
+        const auto &kpUn = pFrame->mvKeysUn[i];
+        const auto X = pMP->GetWorldPos();
+        orbg_pose_edge e;
+        e.obs[0] = kpUn.pt.x;
+        e.obs[1] = kpUn.pt.y;
+        e.obs[2] = pFrame->mvuRight[i];
+        e.xw[0] = X.template at<float>(0);
+        e.xw[1] = X.template at<float>(1);
+        e.xw[2] = X.template at<float>(2);
+        e.inv_sigma2 = pFrame->mvInvLevelSigma2[kpUn.octave];
+        e.stereo = pFrame->mvuRight[i] >= 0 ? 1 : 0;
+        edges.push_back(e);
+        idx.push_back(i);
+    }
+    orbg_pose_camera cam{FrameT::fx, FrameT::fy, FrameT::cx, FrameT::cy, pFrame->mbf, 0.f};
+    float tcw[12], tout[12];
+    pose12(pFrame->mTcw, tcw);
+    double q[4], t[3];
+    std::vector<uint8_t> outl(edges.size() + 1);
+    int ninl = 0;
+    check(orbg_pose_optimization(ctx, edges.data(), (int)edges.size(), &cam, tcw, q, t, tout,
+                                 outl.data(), &ninl),
+          "orbg_pose_optimization");
+    if ((int)edges.size() < 3) return 0;  // Optimizer.cc:463-464: pose untouched
+    MatT pose = MatT::eye(4, 4, 5 /* CV_32F */);
+    for (int r = 0; r < 3; r++)
+        for (int c = 0; c < 4; c++) pose.template at<float>(r, c) = tout[4 * r + c];
+    pFrame->SetPose(pose);
+    for (size_t k = 0; k < idx.size(); k++) pFrame->mvbOutlier[idx[k]] = outl[k] != 0;
+    return ninl;
+}
+
+// ---------------------------------------------------------------------------------------
+// Local bundle adjustment
+// ---------------------------------------------------------------------------------------
+
+// Converter::toSE3Quat (Converter.cc:47-60): SE3Quat(Matrix3d R, Vector3d t), i.e. Eigen's
+// Quaterniond(R) (trace branch, else the largest diagonal) then normalizeRotation
+// (se3quat.h:280-285).  Host arithmetic, the same as oracle/pose_oracle.c's pin.
+inline orbg_pose se3quat_of(const float T[12], int fixed)
+{
+    double R[3][3], q[4];
+    orbg_pose p;
+    std::memset(&p, 0, sizeof(p));
+    for (int i = 0; i < 3; i++) {
+        for (int j = 0; j < 3; j++) R[i][j] = T[4 * i + j];
+        p.t[i] = T[4 * i + 3];
+    }
+    const double tr = R[0][0] + R[1][1] + R[2][2];
+    if (tr > 0) {
+        double s = std::sqrt(tr + 1.0);
+        q[3] = 0.5 * s;
+        s = 0.5 / s;
+        q[0] = (R[2][1] - R[1][2]) * s;
+        q[1] = (R[0][2] - R[2][0]) * s;
+        q[2] = (R[1][0] - R[0][1]) * s;
+    } else {
+        int i = 0;
+        if (R[1][1] > R[0][0]) i = 1;
+        if (R[2][2] > R[i][i]) i = 2;
+        const int j = (i + 1) % 3, k = (j + 1) % 3;
+        double s = std::sqrt(R[i][i] - R[j][j] - R[k][k] + 1.0);
+        q[i] = 0.5 * s;
+        s = 0.5 / s;
+        q[3] = (R[k][j] - R[j][k]) * s;
+        q[j] = (R[j][i] + R[i][j]) * s;
+        q[k] = (R[k][i] + R[i][k]) * s;
+    }
+    if (q[3] < 0)
+        for (double &v : q) v = -v;
+    const double nq = std::sqrt(q[0] * q[0] + q[1] * q[1] + q[2] * q[2] + q[3] * q[3]);
+    for (int c = 0; c < 4; c++) p.q[c] = q[c] / nq;
+    p.fixed = fixed;
+    return p;
+}
+
+// The vertices and edges Optimizer::LocalBundleAdjustment puts into g2o (Optimizer.cc:
+// 662-851) as liborbg's SoA: poses = lLocalKeyFrames (fixed iff mnId == 0) then
+// lFixedCameras (fixed); points = lLocalMapPoints (xyz); one edge per observation of a local
+// map point by a local or fixed key frame that is not bad, mono when mvuRight < 0 (Huber
+// delta sqrt(5.991)) else stereo (sqrt(7.815)), information = mvInvLevelSigma2[octave].
+template <class KeyFrameT, class MapPointT>
+struct LbaWindow {
+    std::vector<orbg_pose> poses;
+    std::vector<double> points;  // 3 per point
+    std::vector<orbg_edge> edges;
+    std::vector<KeyFrameT *> kfs;   // pose index -> key frame
+    std::vector<MapPointT *> mps;   // point index -> map point
+    std::vector<size_t> edge_obs;   // edge -> keypoint index in its key frame
+};
+
+template <class KeyFrameT, class MapPointT>
+LbaWindow<KeyFrameT, MapPointT> build_lba_window(const std::list<KeyFrameT *> &lLocalKeyFrames,
+                                                 const std::list<KeyFrameT *> &lFixedCameras,
+                                                 const std::list<MapPointT *> &lLocalMapPoints)
+{
+    LbaWindow<KeyFrameT, MapPointT> w;
+    std::map<const KeyFrameT *, int> pose_of;
+    auto add_kf = [&](KeyFrameT *pKF, int fixed) {
+        float T[12];
+        pose12(pKF->GetPose(), T);
+        pose_of[pKF] = (int)w.poses.size();
+        w.poses.push_back(se3quat_of(T, fixed));
+        w.kfs.push_back(pKF);
+    };
+    for (KeyFrameT *pKFi : lLocalKeyFrames) add_kf(pKFi, pKFi->mnId == 0 ? 1 : 0);
+    for (KeyFrameT *pKFi : lFixedCameras) add_kf(pKFi, 1);
+    const double thHuberMono = std::sqrt(5.991), thHuberStereo = std::sqrt(7.815);
+    for (MapPointT *pMP : lLocalMapPoints) {
+        const int pt = (int)w.mps.size();
+        const auto X = pMP->GetWorldPos();
+        for (int c = 0; c < 3; c++) w.points.push_back(X.template at<float>(c));
+        w.mps.push_back(pMP);
+        const auto observations = pMP->GetObservations();
+        for (const auto &obs : observations) {
+            KeyFrameT *pKFi = obs.first;
+            if (pKFi->isBad()) continue;
+            auto it = pose_of.find(pKFi);
+            if (it == pose_of.end()) continue;
+            const size_t k = obs.second;
+            const auto &kpUn = pKFi->mvKeysUn[k];
+            orbg_edge e;
+            std::memset(&e, 0, sizeof(e));
+            e.point = pt;
+            e.pose = it->second;
+            e.stereo = pKFi->mvuRight[k] < 0 ? 0 : 1;
+            e.robust = 1;
+            e.active = 1;
+            e.obs[0] = kpUn.pt.x;
+            e.obs[1] = kpUn.pt.y;
+            e.obs[2] = e.stereo ? pKFi->mvuRight[k] : 0.0;
+            e.inv_sigma2 = pKFi->mvInvLevelSigma2[kpUn.octave];
+            e.fx = pKFi->fx;
+            e.fy = pKFi->fy;
+            e.cx = pKFi->cx;
+            e.cy = pKFi->cy;
+            e.bf = pKFi->mbf;
+            e.huber_delta = e.stereo ? thHuberStereo : thHuberMono;
+            w.edges.push_back(e);
+            w.edge_obs.push_back(k);
+        }
+    }
+    return w;
+}
+
+// BlockSolver<6,3>::buildSystem's layout (block_solver.hpp:502-560).  g2o numbers the
+// hessian blocks in vertex-id order (SparseOptimizer::buildIndexMapping sorts the active
+// vertices by id): key frames are vertex mnId, map points mnId + maxKFid + 1, so the free
+// poses come first by KeyFrame::mnId, then the points by MapPoint::mnId.  Blocks are Eigen's
+// column-major 6x6 / 3x3 / 6x3; b = [b_pose (6 each) | b_point (3 each)] in hessian order
+// with g2o's sign (b -= J^T Omega e).  Hpl holds one 6x3 block per (pose, point) hessian
+// pair with an active edge, the sum of its edges' J_pose^T W J_point.  active_robust_chi2
+// is SparseOptimizer::activeRobustChi2 after computeActiveErrors (sparse_optimizer.cpp:
+// 100-112).
+struct G2oBlockSystem {
+    std::vector<int> pose_hidx;          // pose -> hessian index, -1 for fixed poses
+    std::vector<int> point_hidx;         // point -> hessian index (counted from the points)
+    std::vector<double> Hpp;             // [free pose][36] column-major, hessian order
+    std::vector<double> Hll;             // [point][9] column-major, hessian order
+    std::map<std::pair<int, int>, std::vector<double>> Hpl;  // (pose hidx, point hidx) -> 18
+    std::vector<double> b;               // 6 * free poses + 3 * points
+    double active_robust_chi2 = 0;
+};
+
+template <class Window>
+G2oBlockSystem linearize_lba_window(orbg_ctx *ctx, const Window &w)
+{
+    const int np = (int)w.poses.size(), nx = (int)(w.points.size() / 3);
+    BASystem s = linearize_local_ba(ctx, w.poses, w.points, w.edges);
+    G2oBlockSystem g;
+    g.pose_hidx.assign(np, -1);
+    g.point_hidx.assign(nx, -1);
+    {
+        std::vector<std::pair<decltype(w.kfs[0]->mnId), int>> ids;
+        for (int i = 0; i < np; i++)
+            if (!w.poses[i].fixed) ids.emplace_back(w.kfs[i]->mnId, i);
+        std::sort(ids.begin(), ids.end());
+        for (size_t k = 0; k < ids.size(); k++) g.pose_hidx[ids[k].second] = (int)k;
+    }
+    {
+        std::vector<std::pair<decltype(w.mps[0]->mnId), int>> ids;
+        for (int j = 0; j < nx; j++) ids.emplace_back(w.mps[j]->mnId, j);
+        std::sort(ids.begin(), ids.end());
+        for (size_t k = 0; k < ids.size(); k++) g.point_hidx[ids[k].second] = (int)k;
+    }
+    int nfree = 0;
+    for (int i = 0; i < np; i++) nfree += g.pose_hidx[i] >= 0;
+    g.Hpp.assign((size_t)nfree * 36, 0.0);
+    g.Hll.assign((size_t)nx * 9, 0.0);
+    g.b.assign((size_t)6 * nfree + 3 * nx, 0.0);
+    for (int i = 0; i < np; i++) {
+        const int h = g.pose_hidx[i];
+        if (h < 0) continue;
+        for (int r = 0; r < 6; r++) {
+            for (int c = 0; c < 6; c++)
+                g.Hpp[(size_t)h * 36 + c * 6 + r] = s.hpose[(size_t)i * 36 + r * 6 + c];
+            g.b[(size_t)6 * h + r] = s.bpose[(size_t)i * 6 + r];
+        }
+    }
+    for (int j = 0; j < nx; j++) {
+        const int h = g.point_hidx[j];
+        for (int r = 0; r < 3; r++) {
+            for (int c = 0; c < 3; c++)
+                g.Hll[(size_t)h * 9 + c * 3 + r] = s.hpoint[(size_t)j * 9 + r * 3 + c];
+            g.b[(size_t)6 * nfree + 3 * h + r] = s.bpoint[(size_t)j * 3 + r];
+        }
+    }
+    for (size_t e = 0; e < w.edges.size(); e++) {
+        const orbg_edge &E = w.edges[e];
+        if (!E.active) continue;
+        const orbg_edge_out &o = s.edges[e];
+        // RobustKernelHuber::robustify (robust_kernel_impl.cpp:78-91); dsqr is a float
+        // member there, so delta^2 is rounded to float
+        if (E.robust) {
+            const double dsqr = (float)(E.huber_delta * E.huber_delta);
+            g.active_robust_chi2 +=
+                o.chi2 <= dsqr ? o.chi2 : 2 * std::sqrt(o.chi2) * E.huber_delta - dsqr;
+        } else {
+            g.active_robust_chi2 += o.chi2;
+        }
+        const int h = g.pose_hidx[E.pose];
+        if (h < 0) continue;
+        std::vector<double> &blk = g.Hpl[std::make_pair(h, g.point_hidx[E.point])];
+        if (blk.empty()) blk.assign(18, 0.0);
+        for (int r = 0; r < 6; r++)  // (pose row r, point col c) = hpl[c][r]
+            for (int c = 0; c < 3; c++) blk[c * 6 + r] += o.hpl[c][r];
+    }
+    return g;
+}
+
+}  // namespace ref
+}  // namespace orbg_compat

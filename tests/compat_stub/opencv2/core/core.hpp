@@ -1,0 +1,122 @@
+// TEST-ONLY stand-in for the OpenCV core subset that orb_slam2_test_amd/compat/*.hpp use
+// (cv::Mat rows/cols/step/data/type/at/ptr/clone/eye/create/release, _InputArray /
+// _OutputArray, KeyPoint, Point2f, CV_Assert), so tests/test_compat_ref.py can compile and
+// run the OpenCV-facing drop-in layer where OpenCV is absent.  Not OpenCV: semantics are
+// those of the subset only (dense, continuous, 1-channel 8U / 32F matrices).
+#pragma once
+
+#include <cassert>
+#include <cstddef>
+#include <cstdint>
+#include <cstring>
+#include <memory>
+#include <stdexcept>
+#include <vector>
+
+#define CV_8U 0
+#define CV_8UC1 0
+#define CV_32F 5
+#define CV_Assert(expr) do { if (!(expr)) throw std::runtime_error("CV_Assert: " #expr); } while (0)
+
+namespace cv {
+
+struct Point2f {
+    float x = 0.f, y = 0.f;
+    Point2f() {}
+    Point2f(float a, float b) : x(a), y(b) {}
+};
+
+struct KeyPoint {
+    Point2f pt;
+    float size = 0.f, angle = -1.f, response = 0.f;
+    int octave = 0, class_id = -1;
+    KeyPoint() {}
+    KeyPoint(float x, float y, float s, float a = -1.f, float r = 0.f, int o = 0, int c = -1)
+        : pt(x, y), size(s), angle(a), response(r), octave(o), class_id(c) {}
+};
+
+class Mat {
+public:
+    int rows = 0, cols = 0;
+    size_t step[2] = {0, 0};
+    uint8_t *data = nullptr;
+
+    Mat() {}
+    Mat(int r, int c, int type) { create(r, c, type); }
+    Mat(int r, int c, int type, void *ext) : rows(r), cols(c), type_(type)
+    {
+        step[1] = esize();
+        step[0] = (size_t)c * step[1];
+        data = (uint8_t *)ext;
+    }
+    static Mat eye(int r, int c, int type)
+    {
+        Mat m(r, c, type);
+        for (int i = 0; i < r && i < c; i++) {
+            if (type == CV_32F) m.at<float>(i, i) = 1.f;
+            else m.at<uint8_t>(i, i) = 1;
+        }
+        return m;
+    }
+    void create(int r, int c, int type)
+    {
+        rows = r;
+        cols = c;
+        type_ = type;
+        step[1] = esize();
+        step[0] = (size_t)c * step[1];
+        buf_ = std::make_shared<std::vector<uint8_t>>((size_t)r * step[0], 0);
+        data = buf_->data();
+    }
+    void release()
+    {
+        buf_.reset();
+        data = nullptr;
+        rows = cols = 0;
+    }
+    Mat clone() const
+    {
+        Mat m(rows, cols, type_);
+        for (int r = 0; r < rows; r++) std::memcpy(m.ptr<uint8_t>(r), ptr<uint8_t>(r), m.step[0]);
+        return m;
+    }
+    bool empty() const { return data == nullptr || rows * cols == 0; }
+    int type() const { return type_; }
+    template <class T> T *ptr(int r) { return (T *)(data + (size_t)r * step[0]); }
+    template <class T> const T *ptr(int r) const { return (const T *)(data + (size_t)r * step[0]); }
+    template <class T> T &at(int r, int c) { return ptr<T>(r)[c]; }
+    template <class T> const T &at(int r, int c) const { return ptr<T>(r)[c]; }
+    // one index: element i of a row or column vector
+    template <class T> T &at(int i) { return cols == 1 ? at<T>(i, 0) : at<T>(0, i); }
+    template <class T> const T &at(int i) const { return cols == 1 ? at<T>(i, 0) : at<T>(0, i); }
+
+private:
+    int type_ = 0;
+    std::shared_ptr<std::vector<uint8_t>> buf_;
+    size_t esize() const { return type_ == CV_32F ? 4 : 1; }
+};
+
+class _InputArray {
+public:
+    _InputArray(const Mat &m) : m_(&m) {}
+    Mat getMat() const { return *m_; }
+    bool empty() const { return m_->empty(); }
+
+private:
+    const Mat *m_;
+};
+typedef const _InputArray &InputArray;
+
+class _OutputArray {
+public:
+    _OutputArray(Mat &m) : m_(&m) {}
+    void create(int r, int c, int type) const { m_->create(r, c, type); }
+    Mat getMat() const { return *m_; }
+    void release() const { m_->release(); }
+
+private:
+    Mat *m_;
+};
+typedef const _OutputArray &OutputArray;
+
+}  // namespace cv
