@@ -415,6 +415,11 @@ int orbg_ba_linearize_device(orbg_ctx *ctx, const orbg_pose *d_poses, int npose,
                              orbg_edge_out *d_eout, double *d_hpose, double *d_bpose,
                              double *d_hpoint, double *d_bpoint);
 
+/* Whether orbg_ba_linearize_device stores the per-edge Jacobians eout.jp / eout.jt (g2o's
+ * _jacobianOplusXi / Xj; default on).  Off, those fields are left as they are and every
+ * other output is unchanged: the blocks, H_pl and orbg_ba_schur_solve do not read them. */
+int orbg_ba_set_jacobians(orbg_ctx *ctx, int enable);
+
 /* g2o BlockSolver<6,3>::solve with the Schur complement (Thirdparty/g2o/g2o/core/
  * block_solver.hpp:354-486) for one LocalBundleAdjustment window, after setLambda(lambda):
  * inputs are orbg_ba_linearize's outputs (eout[e].hpl = H_pl^T of edge e) for the same

@@ -179,6 +179,7 @@ def lib():
         "orbg_bow_transform_batch_device": (i32, [vp, vp, vp, vp, i32, i32, i32, vp, vp, vp, vp,
                                                   vp, vp, vp, vp, vp]),
         "orbg_ba_linearize": (i32, [vp, vp, i32, vp, i32, vp, i32, vp, vp, vp, vp, vp]),
+        "orbg_ba_set_jacobians": (i32, [vp, i32]),
         "orbg_ba_linearize_device": (i32, [vp, vp, i32, vp, i32, vp, i32, vp, vp, vp, vp, vp, vp,
                                            vp, vp, vp]),
     }

@@ -43,6 +43,10 @@ __device__ __forceinline__ void quat_rotate(const double q[4], const double v[3]
 #define BA_ROW 8    // doubles per pose row
 #define BA_PROW 12  // doubles per edge share of its point block
 
+// JAC: store g2o's per-edge Jacobians (eout.jp / eout.jt, _jacobianOplusXi / Xj).  Nothing
+// downstream reads them (the blocks, H_pl and the Schur step use the registers), so callers
+// that do not keep them skip 216 of the 696 bytes stored per edge (orbg_ba_set_jacobians).
+template <bool JAC>
 __global__ __launch_bounds__(256) void k_ba_edges(const orbg_pose *__restrict__ poses,
                                                   const double *__restrict__ points,
                                                   const orbg_edge *__restrict__ edges, int nedge,
@@ -57,7 +61,15 @@ __global__ __launch_bounds__(256) void k_ba_edges(const orbg_pose *__restrict__ 
     double *row = rows + (size_t)i * 3 * BA_ROW;
     double *pr = prow + (size_t)i * BA_PROW;
     if (!e.active) {
-        memset(o, 0, sizeof(*o));
+        if (JAC) {
+            memset(o, 0, sizeof(*o));
+        } else {
+            for (int k = 0; k < 3; k++) o->err[k] = 0;
+            o->chi2 = 0;
+            o->rho1 = 0;
+            for (int r = 0; r < 3; r++)
+                for (int c = 0; c < 6; c++) o->hpl[r][c] = 0;
+        }
         for (int k = 0; k < 3 * BA_ROW; k++) row[k] = 0;
         for (int k = 0; k < BA_PROW; k++) pr[k] = 0;
         return;
@@ -146,10 +158,12 @@ __global__ __launch_bounds__(256) void k_ba_edges(const orbg_pose *__restrict__ 
     for (int k = 0; k < 3; k++) o->err[k] = err[k];
     o->chi2 = chi2;
     o->rho1 = rho1;
-    for (int k = 0; k < 3; k++)
-        for (int c = 0; c < 3; c++) o->jp[k][c] = jp[k][c];
-    for (int k = 0; k < 3; k++)
-        for (int c = 0; c < 6; c++) o->jt[k][c] = jt[k][c];
+    if (JAC) {
+        for (int k = 0; k < 3; k++)
+            for (int c = 0; c < 3; c++) o->jp[k][c] = jp[k][c];
+        for (int k = 0; k < 3; k++)
+            for (int c = 0; c < 6; c++) o->jt[k][c] = jt[k][c];
+    }
     // point (vertex 0) block
     double wr[3];
 #pragma unroll
@@ -347,14 +361,19 @@ int launch_ba_device(hipStream_t st, const orbg_pose *poses, int npose, const do
                      int npoint, const orbg_edge *edges, int nedge, const int32_t *pose_off,
                      const int32_t *pose_edges, const int32_t *point_off,
                      const int32_t *point_edges, orbg_edge_out *eout, double *hpose,
-                     double *bpose, double *hpoint, double *bpoint, double *rows, void *prof)
+                     double *bpose, double *hpoint, double *bpoint, double *rows, void *prof,
+                     bool jacobians)
 {
     double *prow = (double *)((uint8_t *)rows + al((size_t)(nedge > 0 ? nedge : 1) * 3 * BA_ROW * 8));
     if (nedge) {
         hipEvent_t a = nullptr;
         prof_begin(prof, st, "ba_edges", &a);
-        hipLaunchKernelGGL(k_ba_edges, dim3((nedge + 255) / 256), dim3(256), 0, st, poses, points,
-                           edges, nedge, eout, rows, prow);
+        if (jacobians)
+            hipLaunchKernelGGL(k_ba_edges<true>, dim3((nedge + 255) / 256), dim3(256), 0, st, poses,
+                               points, edges, nedge, eout, rows, prow);
+        else
+            hipLaunchKernelGGL(k_ba_edges<false>, dim3((nedge + 255) / 256), dim3(256), 0, st, poses,
+                               points, edges, nedge, eout, rows, prow);
         prof_end(prof, st, "ba_edges", a);
     }
     if (npoint) {
@@ -436,7 +455,7 @@ int launch_ba(hipStream_t st, const orbg_pose *poses, int npose, const double *p
     if (nedge) CK(hipMemcpyAsync(d_qe, point_edges, nedge * 4, hipMemcpyHostToDevice, st));
     const int rc = launch_ba_device(st, d_pose, npose, d_pts, npoint, d_edges, nedge, d_off, d_pe,
                                     d_qoff, d_qe, d_eout, d_hpose, d_bpose, d_hpt, d_bpt, d_rows,
-                                    prof);
+                                    prof, true);
     if (rc) return rc;
     if (eout && nedge)
         CK(hipMemcpyAsync(eout, d_eout, nedge * sizeof(orbg_edge_out), hipMemcpyDeviceToHost, st));

@@ -95,9 +95,10 @@ class DeviceLBA:
     with every array in HBM -- the per-iteration work of g2o's computeActiveErrors +
     buildSystem."""
 
-    def __init__(self, poses, points, edges, device=0):
+    def __init__(self, poses, points, edges, device=0, jacobians=True):
         import torch
         self.ctx = _ctx(device)
+        self.jacobians = bool(jacobians)  # eout.jp / jt stored (orbg_ba_set_jacobians)
         self.np, self.nq, self.ne = len(poses), len(points), len(edges)
         off, pe = vertex_csr(edges, "pose", self.np)
         qoff, qe = vertex_csr(edges, "point", self.nq)
@@ -120,6 +121,8 @@ class DeviceLBA:
 
     def linearize(self):
         p = lambda t: L.C.c_void_p(t.data_ptr())  # noqa: E731
+        L.check(L.lib().orbg_ba_set_jacobians(self.ctx.handle, 1 if self.jacobians else 0),
+                "orbg_ba_set_jacobians")
         L.check(L.lib().orbg_ba_linearize_device(
             self.ctx.handle, p(self.d_poses), self.np, p(self.d_points), self.nq, p(self.d_edges),
             self.ne, p(self.d_off), p(self.d_pe), p(self.d_qoff), p(self.d_qe), p(self.d_eout),

@@ -23,6 +23,8 @@ sys.path.insert(0, ROOT)
 
 HBM_PEAK_GBS = 8000.0
 EDGE_ALGO_BYTES = 108  # per-edge algorithmic bytes
+F64_MFMA_PEAK_TFLOPS = 78.6  # MI355X FP64 matrix, AMD spec (the guide lists no FP64 row)
+PMC_BA = "r02_ba_pmc_kernels.json"  # tools/pmc_kernels.py over tools/r02_ba_profile.sh
 
 
 def main():
@@ -32,6 +34,8 @@ def main():
     ap.add_argument("--iters", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--jacobians", action="store_true",
+                    help="also store g2o's per-edge Jacobians eout.jp / jt (orbg_ba_set_jacobians)")
     args = ap.parse_args()
 
     import torch
@@ -42,7 +46,7 @@ def main():
 
     base = [S.ba_window(seed=500 + i) for i in range(args.distinct)]
     poses, pts, edges = concat_windows([base[i % args.distinct] for i in range(args.windows)])
-    lba = DeviceLBA(poses, pts, edges)
+    lba = DeviceLBA(poses, pts, edges, jacobians=args.jacobians)
     for _ in range(args.warmup):
         lba.linearize()
     lba.ctx.sync()
@@ -64,7 +68,8 @@ def main():
         "dtype": "f64", "data": "synthetic",
         "config": {"workload": "configs[4]: %d KITTI00-like LBA windows (20 KFs, 6000 points)"
                                % args.windows, "edges": ne, "poses": len(poses),
-                   "points": len(pts), "stereo_frac": round(float(np.mean(edges["stereo"])), 3)},
+                   "points": len(pts), "stereo_frac": round(float(np.mean(edges["stereo"])), 3),
+                   "edge_jacobians_stored": bool(args.jacobians)},
         "ms_per_iter": round(dt / args.iters * 1e3, 4),
         "kernels": {k: {"ms_per_iter": round(v[0] / args.iters, 4),
                         "avg_launch_ms": round(v[0] / max(v[1], 1), 5)} for k, v in kern.items()},
@@ -77,6 +82,33 @@ def main():
                            "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": None,
                            "algo_bytes_per_launch": ne * EDGE_ALGO_BYTES,
                            "avg_launch_ms": round(ms, 5)}
+    pk = {}
+    pmc = os.path.join(ROOT, "profiles", PMC_BA)
+    if os.path.exists(pmc):
+        with open(pmc) as f:
+            pk = json.load(f)
+    if "roofline" in out:
+        out["roofline"]["traffic"] = pk.get("ba_edges", {}).get("hbm_bytes_per_launch")
+        out["roofline"]["pmc_source"] = os.path.relpath(pmc, ROOT) if pk else None
+    if "ba_pose_mfma" in kern:
+        # MFMAs issued: per slice of <= 64 edges of a free pose, 4 per 16 rows (3 per edge)
+        nmfma = 0
+        fixed = poses["fixed"] != 0
+        cnt = np.bincount(edges["pose"], minlength=len(poses))
+        for pidx in np.nonzero(~fixed)[0]:
+            n = int(cnt[pidx])
+            for s0 in range(0, n, 64):
+                nmfma += 4 * ((3 * min(64, n - s0) + 15) // 16)
+        ms = kern["ba_pose_mfma"][0] / max(kern["ba_pose_mfma"][1], 1)
+        tf = nmfma * 16 * 16 * 4 * 2 / (ms * 1e-3) / 1e12
+        out["mfma"] = {"kernel": "ba_pose_mfma", "instr": "v_mfma_f64_16x16x4f64",
+                       "mfma_per_launch": nmfma, "issued_tflops": round(tf, 2),
+                       "peak_tflops": F64_MFMA_PEAK_TFLOPS,
+                       "issued_frac": round(tf / F64_MFMA_PEAK_TFLOPS, 4),
+                       "mfma_frac": pk.get("ba_pose_mfma", {}).get("mfma_frac"),
+                       "note": "issued = every MFMA the kernel issues (7x7 of each 16x16 tile is "
+                               "used); mfma_frac = SQ_VALU_MFMA_BUSY_CYCLES / (1024 SIMDs x "
+                               "GPU cycles) from the committed PMC pass"}
     if not args.no_cpu:
         from oracle import pyoracle as O
         p, q, e = base[0]
