@@ -36,6 +36,8 @@ HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
 PYR_BYTES = 1444097          # all 8 levels at 1241x376
 FRAME_ALGO_BYTES = 2701578   # extract 2,533,578 + match 168,000
 STEREO_FRAME_ALGO_BYTES = 5235156  # 2 x extract + match
+EXTRACT_FRAME_ALGO_BYTES = 2533578  # configs[1] / C2: ORBextractor only
+METRIC_EXTRACT = "frames/sec ORBextractor only, 1241×376 2000feat 8lvl (configs[1], C2)"
 
 
 PMC_MONO = "r02_pmc_kernels.json"       # tools/r02_profile.sh r02 (bench.py)
@@ -114,6 +116,29 @@ def cpu_baseline_stereo(lefts, rights, threads, nframes, nframes_1core=8):
                                                              nframes_1core, dt1))}
 
 
+def cpu_baseline_extract(frames, threads, nframes, nframes_1core=48):
+    """oracle/ ORBextractor only (C2) on host threads (ctypes calls release the GIL)."""
+    from concurrent.futures import ThreadPoolExecutor
+    from oracle import pyoracle as O
+    p = O.params(nfeatures=NFEAT, nlevels=NLEV)
+
+    def run(n, th):
+        t0 = time.perf_counter()
+        with ThreadPoolExecutor(th) as pool:
+            list(pool.map(lambda i: O.extract(p, frames[i % len(frames)]), range(n)))
+        return time.perf_counter() - t0
+
+    dt = run(nframes, threads)
+    dt1 = run(nframes_1core, 1)
+    ncpu, model = host_cpu()
+    return {"value": round(nframes / dt, 3), "unit": "frames/s", "cores": threads,
+            "kind": "port", "value_1core": round(nframes_1core / dt1, 3),
+            "host_logical_cpus": ncpu, "host_cpu_model": model,
+            "sample": ("%d synthetic 1241x376 frames (ORBextractor 2000 feat/8 lvl), oracle/ C "
+                       "restatement -O3, %d threads, %.1f s wall; 1 thread: %d frames, %.1f s"
+                       % (nframes, threads, dt, nframes_1core, dt1))}
+
+
 def host_cpu():
     """The GPU box's host: logical CPUs (std::thread::hardware_concurrency) and the model
     name lscpu prints (/proc/cpuinfo)."""
@@ -170,6 +195,8 @@ def main():
                          "of step k, orbg_set_pipeline); 0: one batch after the other")
     ap.add_argument("--stereo", action="store_true",
                     help="configs[3]: stereo frames (extract L+R + ComputeStereoMatches)")
+    ap.add_argument("--extract-only", action="store_true",
+                    help="configs[1] (C2): ORBextractor only, no matching")
     args = ap.parse_args()
 
     import torch
@@ -193,6 +220,8 @@ def main():
         # [r*B, (r+1)*B) of one cyclic B*world-frame sequence and extracts them plus the frame
         # before the block (1-frame halo), so its B pairs (t-1, t) match with no exchange
         frames = synthetic.sequence_block(B * world, rank * B, (rank + 1) * B, H, W)
+        if args.extract_only:  # no pairs: the halo frame is not needed
+            frames = np.ascontiguousarray(frames[1:])
     nimg = len(frames)
     d_frames = torch.from_numpy(frames).to("cuda")
     torch.cuda.synchronize()
@@ -225,6 +254,9 @@ def main():
                 sequence.gather_summary(ssum.view(2, B), world, sizes=[B] * world)
             return
         nonlocal m12
+        if args.extract_only:
+            ext.extract_batch_device(d_frames.data_ptr(), nimg, W, H)
+            return
         ext.extract_batch_device(d_frames.data_ptr(), nimg, W, H)
         ext.match_batch_device(f1, f2, 100, 0.9, True)
         ext.ctx.batch_summary(summary.data_ptr())
@@ -274,6 +306,8 @@ def main():
                 ext.ctx.sync()
                 ext.stereo_batch_device(sl, sr, synthetic.KITTI_BF,
                                         synthetic.KITTI_BF / synthetic.KITTI_FX)
+            elif args.extract_only:
+                ext.extract_batch_device(d_frames.data_ptr(), nimg, W, H)
             else:
                 ext.extract_batch_device(d_frames.data_ptr(), nimg, W, H)
                 ext.ctx.sync()
@@ -326,8 +360,12 @@ def main():
                     "algo_bytes_per_launch": ks["algo_bytes_per_launch"],
                     "avg_launch_ms": ks["avg_launch_ms"],
                     "timing": "serial pass (orbg_set_serial), HIP events on the launch stream"}
-        fab = STEREO_FRAME_ALGO_BYTES if args.stereo else FRAME_ALGO_BYTES
-        if args.stereo:
+        fab = (STEREO_FRAME_ALGO_BYTES if args.stereo else
+               EXTRACT_FRAME_ALGO_BYTES if args.extract_only else FRAME_ALGO_BYTES)
+        if args.extract_only:
+            workload = ("configs[1] (C2) synthetic 1241x376, 2000 feat, 8 lvl: ORBextractor "
+                        "only (frames [r*B, (r+1)*B) of the sequence, no matching)")
+        elif args.stereo:
             workload = ("configs[3] KITTI00-shaped stereo 1241x376 L+R, 2000 feat/eye, 8 lvl: "
                         "ORBextractor x2 + Frame::ComputeStereoMatches (bf=386.1448, "
                         "mb=bf/fx)")
@@ -335,7 +373,8 @@ def main():
             workload = ("C3 KITTI03-shaped mono 1241x376, 2000 feat, 8 lvl: ORBextractor + "
                         "Hamming knn2 (t vs t-1) + SearchForInitialization(w=100, 0.9, checkOri)")
         out = {
-            "metric": METRIC_STEREO if args.stereo else METRIC, "value": round(value, 2),
+            "metric": (METRIC_STEREO if args.stereo else
+                       METRIC_EXTRACT if args.extract_only else METRIC), "value": round(value, 2),
             "unit": "stereo frames/s" if args.stereo else "frames/s", "n_gpus": world,
             "steps": args.steps, "warmup": args.warmup,
             "ms_per_step": round(elapsed / args.steps * 1e3, 4), "higher_is_better": True,
@@ -358,6 +397,9 @@ def main():
         if world == 1 and not args.no_cpu and args.stereo:
             out["cpu_baseline"] = cpu_baseline_stereo(lefts, rights, args.cpu_threads,
                                                       args.cpu_frames or 32 * args.cpu_threads)
+        elif world == 1 and not args.no_cpu and args.extract_only:
+            out["cpu_baseline"] = cpu_baseline_extract(frames, args.cpu_threads,
+                                                       args.cpu_frames or 256 * args.cpu_threads)
         elif world == 1 and not args.no_cpu:
             n = args.cpu_frames or 256 * args.cpu_threads
             out["cpu_baseline"] = cpu_baseline(frames, args.cpu_threads, n)
