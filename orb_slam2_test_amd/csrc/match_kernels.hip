@@ -197,27 +197,199 @@ __device__ __forceinline__ void knn2_block(const uint8_t *__restrict__ q, int nq
     }
 }
 
-__global__ __launch_bounds__(256) void k_knn2_single(const uint8_t *q, int nq, const uint8_t *t,
-                                                     int nt, int32_t *out)
+// knn2 on the fp4 matrix cores (default).  Same keys as knn2_block, at twice the i8 rate:
+// v_mfma_scale_f32_32x32x64_f8f6f4 with e2m1 operands runs K = 64 in the cycles the i8 form
+// needs for K = 32, so K = 256 is four MFMAs instead of eight.  Every bit becomes +-1.0 in
+// e2m1 (0x2 = +1, 0xA = -1): train (A) b=1 -> -1, query (B) b=1 -> +1 (b=0 the opposite), so
+// one product is -1 where the bits agree and +1 where they differ; the E8M0 scale 2^12 on A
+// makes the dot product 4096 (d - (256 - d)) = 8192 d - 2^20, and the C input (train index)
+// is added as before.  Every partial sum is an integer below 2^22 in magnitude, exact in
+// the f32 accumulator whatever the summation order, so the f32 key equals the i8 kernel's
+// i32 key value; past-nt rows carry 2^30 (rounded sums stay >= 2^30 - 2^20, above every
+// real key).  k order (A and B alike): step s, lane half h -> descriptor dword 2s + h; VGPR
+// q, nibble j -> bit 4j + q of that dword.
+typedef int knn_v8i __attribute__((ext_vector_type(8)));
+typedef float knn_v16f __attribute__((ext_vector_type(16)));
+#define KNN4_ROWB 144  // expanded train row: 128 B + 16 B pad (16 lanes' b128 reads: 64 banks)
+#define KNN4_SCALE_A (127 + 12)  // E8M0 2^12
+#define KNN4_SCALE_B 127         // E8M0 1.0
+
+// e2m1 nibbles of bits q, q+4, .., q+28 of x: b=1 -> 0xA (-1.0), b=0 -> 0x2 (+1.0)
+__device__ __forceinline__ uint32_t knn4_neg(uint32_t x, int q)
+{
+    return (((x >> q) & 0x11111111u) << 3) | 0x22222222u;
+}
+// b=1 -> 0x2 (+1.0), b=0 -> 0xA (-1.0)
+__device__ __forceinline__ uint32_t knn4_pos(uint32_t x, int q)
+{
+    return knn4_neg(x, q) ^ 0x88888888u;
+}
+
+__device__ __forceinline__ void knn2_block_fp4(const uint8_t *__restrict__ q, int nq,
+                                               const uint8_t *__restrict__ t, int nt,
+                                               int32_t *__restrict__ out, int qbase)
+{
+    __shared__ __attribute__((aligned(16))) uint8_t tile[2][64 * KNN4_ROWB];
+    const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+    const int col = lane & 31, h = lane >> 5;
+    // B fragments: query qbase + 64 wv + 32 u + col, step s: dword 2s + h
+    knn_v8i bq[2][4];
+#pragma unroll
+    for (int u = 0; u < 2; u++) {
+        const int qi = qbase + wv * 64 + u * 32 + col;
+        uint32_t x[4] = {0, 0, 0, 0};
+        if (qi < nq) {
+            const uint32_t *p = (const uint32_t *)(q + (size_t)qi * 32);
+#pragma unroll
+            for (int s = 0; s < 4; s++) x[s] = p[2 * s + h];
+        }
+#pragma unroll
+        for (int s = 0; s < 4; s++) {
+#pragma unroll
+            for (int qd = 0; qd < 4; qd++) {
+                bq[u][s][qd] = (int)knn4_pos(x[s], qd);
+                bq[u][s][qd + 4] = 0;  // e2m1 uses the first four VGPRs only
+            }
+        }
+    }
+    float k1[2] = {__builtin_huge_valf(), __builtin_huge_valf()};
+    float k2[2] = {__builtin_huge_valf(), __builtin_huge_valf()};
+
+    // expansion of stage s0 (64 rows) into buffer bf: thread -> rows (tid >> 3) and
+    // (tid >> 3) + 32, dword tid & 7 -> 16 bytes at row offset 16 * dword
+    const int er = tid >> 3, esd = tid & 7;
+    auto fetch1 = [&](int row) -> uint32_t {
+        return ((const uint32_t *)(t + (size_t)min(row, nt - 1) * 32))[esd];
+    };
+    auto expand1 = [&](uint32_t x, uint8_t *dst) {
+        uint4 w;
+        w.x = knn4_neg(x, 0); w.y = knn4_neg(x, 1);
+        w.z = knn4_neg(x, 2); w.w = knn4_neg(x, 3);
+        *(uint4 *)dst = w;
+    };
+    auto expand = [&](uint32_t x0, uint32_t x1, int bf) {
+        expand1(x0, tile[bf] + er * KNN4_ROWB + esd * 16);
+        expand1(x1, tile[bf] + (er + 32) * KNN4_ROWB + esd * 16);
+    };
+    uint32_t xr0 = 0, xr1 = 0;
+    if (nt > 0) {
+        expand(fetch1(er), fetch1(er + 32), 0);
+        xr0 = fetch1(64 + er);
+        xr1 = fetch1(96 + er);
+    }
+    knn_v16f pacc[2];
+    bool pend = false;
+    auto epilogue = [&]() {
+#pragma unroll
+        for (int r = 0; r < 16; r++) {
+#pragma unroll
+            for (int u = 0; u < 2; u++) {
+                // k1 <= k2: the new second key is med3(k1, k2, key), then the new minimum
+                k2[u] = __builtin_amdgcn_fmed3f(k1[u], k2[u], pacc[u][r]);
+                k1[u] = fminf(k1[u], pacc[u][r]);
+            }
+        }
+    };
+    for (int s0 = 0, bf = 0; s0 < nt; s0 += 64, bf ^= 1) {
+        __syncthreads();
+        if (s0 + 64 < nt) {
+            expand(xr0, xr1, bf ^ 1);
+            xr0 = fetch1(s0 + 128 + er);
+            xr1 = fetch1(s0 + 160 + er);
+        }
+#pragma unroll
+        for (int sub = 0; sub < 2; sub++) {
+            const int tb = s0 + 32 * sub;
+            if (tb >= nt) break;
+            knn_v16f ctag;
+            const float tbh = (float)(tb + 4 * h);
+#pragma unroll
+            for (int r = 0; r < 16; r++) ctag[r] = tbh + (float)((r & 3) + 8 * (r >> 2));
+            if (tb + 32 > nt) {  // last subtile: rows past nt get keys above every real one
+#pragma unroll
+                for (int r = 0; r < 16; r++)
+                    if (ctag[r] >= (float)nt) ctag[r] = (float)KNN_NONE;
+            }
+            knn_v16f acc[2];
+            const uint8_t *arow = tile[bf] + (32 * sub + col) * KNN4_ROWB + h * 16;
+#pragma unroll
+            for (int s = 0; s < 4; s++) {
+                const knn_v4i a4 = *(const knn_v4i *)(arow + s * 32);
+                const knn_v8i a = {a4[0], a4[1], a4[2], a4[3], 0, 0, 0, 0};
+                acc[0] = __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(
+                    a, bq[0][s], s ? acc[0] : ctag, 4, 4, 0, KNN4_SCALE_A, 0, KNN4_SCALE_B);
+                acc[1] = __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(
+                    a, bq[1][s], s ? acc[1] : ctag, 4, 4, 0, KNN4_SCALE_A, 0, KNN4_SCALE_B);
+            }
+            if (pend) epilogue();
+            pacc[0] = acc[0];
+            pacc[1] = acc[1];
+            pend = true;
+        }
+    }
+    if (pend) epilogue();
+    const float none = (float)(KNN_NONE - (1 << 20));
+#pragma unroll
+    for (int u = 0; u < 2; u++) {
+        const float o1 = __shfl_xor(k1[u], 32, 64), o2 = __shfl_xor(k2[u], 32, 64);
+        const float b1 = fminf(k1[u], o1);
+        const float b2 = fminf(fminf(k2[u], o2), fmaxf(k1[u], o1));
+        const int qi = qbase + wv * 64 + u * 32 + col;
+        if (h == 0 && qi < nq) {
+            const bool v1 = b1 < none, v2 = b2 < none;
+            const int e1 = v1 ? (int)b1 + (1 << 20) : 0, e2 = v2 ? (int)b2 + (1 << 20) : 0;
+            out[(size_t)qi * 3 + 0] = v1 ? (e1 & (KNN_MAX_TRAIN - 1)) : -1;
+            out[(size_t)qi * 3 + 1] = v1 ? (e1 >> 13) : INT_MAX;
+            out[(size_t)qi * 3 + 2] = v2 ? (e2 >> 13) : INT_MAX;
+        }
+    }
+}
+
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4, 8))) void k_knn2_single(
+    const uint8_t *q, int nq, const uint8_t *t, int nt, int32_t *out)
+{
+    knn2_block_fp4(q, nq, t, nt, out, blockIdx.x * 256);
+}
+__global__ __launch_bounds__(256) void k_knn2_single_i8(const uint8_t *q, int nq, const uint8_t *t,
+                                                        int nt, int32_t *out)
 {
     knn2_block(q, nq, t, nt, out, blockIdx.x * 256);
 }
 
-// batch: queries = F2 (current) keypoints of pair p, train = F1 (previous)
-__global__ __launch_bounds__(256) void k_knn2_pairs(const uint8_t *desc, const int32_t *counts,
-                                                    int fc, const int32_t *f1, const int32_t *f2,
-                                                    int32_t *out)
+// batch: queries = F2 (current) keypoints of pair p, train = F1 (previous).  1-D grid of nbx
+// blocks per pair, remapped so one pair's blocks share an XCD (and the L2 copy of the train
+// descriptors they all stream)
+#define KNN2_PAIRS_BODY(BLOCK)                                                                 \
+    const int nbx = (fc + 255) >> 8;                                                           \
+    const int id = xcd_remap(blockIdx.x, gridDim.x);                                           \
+    const int p = id / nbx, bx = id - p * nbx;                                                 \
+    const int a = f1[p], b = f2[p];                                                            \
+    const int nq = counts[b], nt = counts[a];                                                  \
+    if (bx * 256 >= nq) return;                                                                \
+    BLOCK(desc + (size_t)b * fc * 32, nq, desc + (size_t)a * fc * 32, nt,                      \
+          out + (size_t)p * fc * 3, bx * 256);
+// fp4: 128 VGPRs (4 waves per SIMD; two dwords spill outside the train loop)
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4, 8))) void k_knn2_pairs(
+    const uint8_t *desc, const int32_t *counts, int fc, const int32_t *f1, const int32_t *f2,
+    int32_t *out)
 {
-    // 1-D grid of nbx blocks per pair, remapped so one pair's blocks share an XCD (and
-    // the L2 copy of the train descriptors they all stream)
-    const int nbx = (fc + 255) >> 8;
-    const int id = xcd_remap(blockIdx.x, gridDim.x);
-    const int p = id / nbx, bx = id - p * nbx;
-    const int a = f1[p], b = f2[p];
-    const int nq = counts[b], nt = counts[a];
-    if (bx * 256 >= nq) return;
-    knn2_block(desc + (size_t)b * fc * 32, nq, desc + (size_t)a * fc * 32, nt,
-               out + (size_t)p * fc * 3, bx * 256);
+    KNN2_PAIRS_BODY(knn2_block_fp4)
+}
+__global__ __launch_bounds__(256) void k_knn2_pairs_i8(const uint8_t *desc, const int32_t *counts,
+                                                       int fc, const int32_t *f1,
+                                                       const int32_t *f2, int32_t *out)
+{
+    KNN2_PAIRS_BODY(knn2_block)
+}
+
+// ORBG_KNN_I8=1 selects the i8 MFMA kernel (developer A/B; same results)
+static bool knn_fp4()
+{
+    static const int v = [] {
+        const char *e = getenv("ORBG_KNN_I8");
+        return e && atoi(e) ? 0 : 1;
+    }();
+    return v != 0;
 }
 
 // ---------------------------------------------------------------------------
@@ -805,8 +977,8 @@ int launch_knn2(hipStream_t st, const uint8_t *q, int nq, const uint8_t *t, int 
 {
     if (nt >= KNN_MAX_TRAIN) return ORBG_ENOTSUP;  // caller chunks the train set
     PL(prof, st, "knn2",
-       hipLaunchKernelGGL(k_knn2_single, dim3((nq + 255) / 256), dim3(256), 0, st, q, nq, t, nt,
-                          out));
+       hipLaunchKernelGGL(knn_fp4() ? k_knn2_single : k_knn2_single_i8,
+                          dim3((nq + 255) / 256), dim3(256), 0, st, q, nq, t, nt, out));
     return hipGetLastError() == hipSuccess ? ORBG_OK : ORBG_EIO;
 }
 
@@ -829,8 +1001,9 @@ int launch_match_pairs(hipStream_t st, hipStream_t aux, hipEvent_t evf, hipEvent
     if (hipEventRecord(evf, st) != hipSuccess || hipStreamWaitEvent(aux, evf, 0) != hipSuccess)
         return ORBG_EIO;
     PL(prof, aux, "knn2",
-       hipLaunchKernelGGL(k_knn2_pairs, dim3((fc + 255) / 256 * npairs), dim3(256), 0, aux, desc,
-                          counts, fc, d_f1, d_f2, knn));
+       hipLaunchKernelGGL(knn_fp4() ? k_knn2_pairs : k_knn2_pairs_i8,
+                          dim3((fc + 255) / 256 * npairs), dim3(256), 0, aux, desc, counts, fc,
+                          d_f1, d_f2, knn));
     if (hipEventRecord(evj, aux) != hipSuccess) return ORBG_EIO;
     PL(prof, st, "init_resolve",
        hipLaunchKernelGGL(k_init_resolve_pairs, dim3(npairs), dim3(RESOLVE_T),
