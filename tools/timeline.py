@@ -13,7 +13,8 @@ for r in csv.DictReader(open(sys.argv[1])):
 rows.sort()
 # step starts: every 7th k_resize (7 pyramid levels per batch; pipelined batches let the
 # next batch's resizes start before this batch's orient_desc)
-starts = [s for i, s in enumerate([r[0] for r in rows if r[2] == "k_resize"]) if i % 7 == 0]
+pyr = [r[0] for r in rows if r[2] == "k_pyramid"]  # one launch per batch (all levels)
+starts = pyr if pyr else [s for i, s in enumerate([r[0] for r in rows if r[2] == "k_resize"]) if i % 7 == 0]
 nshow = int(sys.argv[2]) if len(sys.argv) > 2 else 2
 for k in range(max(0, len(starts) - 1 - nshow), len(starts) - 1):
     t0, t1 = starts[k], starts[k + 1]
