@@ -200,6 +200,8 @@ int orc_search_by_projection_local(const orc_keypoint *kps, const uint8_t *desc,
                                    float th, float nnratio, int32_t *match);
 
 /* ---- Optimizer::PoseOptimization (pose_oracle.c) ---- */
+/* LM's pow(2 rho - 1, 3) as the once-rounded exact cube (optimization_algorithm_levenberg.cpp:135) */
+double orc_lm_cube(double t);
 /* one EdgeSE3ProjectXYZOnlyPose (stereo = 0) / EdgeStereoSE3ProjectXYZOnlyPose (1) */
 typedef struct {
     float obs[3];       /* kpUn.pt.x, kpUn.pt.y, mvuRight[i] */

@@ -20,7 +20,8 @@
  *     lower triangle, zero pivots left unscaled, D^-1 skipped below DBL_MIN) with
  *     sequential inner products; solves forward / diagonal / backward in index order;
  *   - SE3Quat::exp uses a pinned sin/cos (orb_oracle.c pinned_sincos) and theta^3 as
- *     theta*theta*theta; LM's pow(2 rho - 1, 3) as t*t*t;
+ *     theta*theta*theta; LM's pow(2 rho - 1, 3) (optimization_algorithm_levenberg.cpp:135,
+ *     libm pow under C++11) as the rounded exact cube orc_lm_cube;
  *   - Quaterniond(R) is Eigen's matrix-to-quaternion (trace branch, else largest diagonal).
  */
 #include "orb_oracle.h"
@@ -28,6 +29,21 @@
 #include <float.h>
 #include <math.h>
 #include <stdlib.h>
+
+/* g2o's pow(2 rho - 1, 3) (optimization_algorithm_levenberg.cpp:135): glibc's pow is
+ * correctly rounded on all but astronomically rare inputs, and t*t*t is not (two roundings,
+ * up to ~1 ulp off), so the cube is formed exactly as a double-double and rounded once:
+ * t^2 = h + l (fma), h t = ph + pl (fma), t^3 = ph + (pl + l t).  The kernel
+ * (pose_kernels.hip) evaluates the same expression; tests/test_oracle_kats.py checks it
+ * against the host libm's pow(t, 3.0). */
+double orc_lm_cube(double t)
+{
+    const double h = t * t;
+    const double l = fma(t, t, -h);
+    const double ph = h * t;
+    const double pl = fma(h, t, -ph);
+    return ph + (pl + l * t);
+}
 #include <string.h>
 
 void orc_pinned_sincos_d(double x, double *s, double *c);
@@ -457,8 +473,7 @@ static int po_optimize(double q[4], double t[3], const orc_pose_edge *edges, int
             scale += 1e-3;
             rho /= scale;
             if (rho > 0 && isfinite(tempChi)) {
-                const double tt = 2 * rho - 1;
-                double alpha = 1. - tt * tt * tt;
+                double alpha = 1. - orc_lm_cube(2 * rho - 1);
                 alpha = fmin(alpha, 2. / 3.);
                 const double sf = fmax(1. / 3., alpha);
                 lambda *= sf;

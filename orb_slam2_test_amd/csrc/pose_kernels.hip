@@ -34,6 +34,17 @@ void prof_end(void *prof, hipStream_t s, const char *n, hipEvent_t a);
 #define PO_NV 28  // robust chi2, 21 lower-triangle H entries, 6 b entries
 
 // ---- SE3Quat (q = x, y, z, w), Eigen's formulas (see oracle/pose_oracle.c) ----
+// g2o's pow(2 rho - 1, 3) (optimization_algorithm_levenberg.cpp:135, libm pow): the exact
+// cube as a double-double, rounded once (oracle/pose_oracle.c orc_lm_cube, same expression)
+__device__ __forceinline__ double lm_cube(double t)
+{
+    const double h = t * t;
+    const double l = __builtin_fma(t, t, -h);
+    const double ph = h * t;
+    const double pl = __builtin_fma(h, t, -ph);
+    return ph + (pl + l * t);
+}
+
 __device__ __forceinline__ void q_rotate(const double q[4], const double v[3], double out[3])
 {
     double uv[3] = {q[1] * v[2] - q[2] * v[1], q[2] * v[0] - q[0] * v[2],
@@ -499,8 +510,7 @@ __global__ __launch_bounds__(PO_T) void k_pose_opt(const orbg_pose_edge *__restr
                         scale += 1e-3;
                         rho /= scale;
                         if (rho > 0 && isfinite(tempChi)) {
-                            const double t3 = 2 * rho - 1;
-                            double alpha = 1. - t3 * t3 * t3;
+                            double alpha = 1. - lm_cube(2 * rho - 1);
                             alpha = fmin(alpha, 2. / 3.);
                             const double sf = fmax(1. / 3., alpha);
                             lambda *= sf;
