@@ -29,12 +29,14 @@
 namespace orbg {
 
 // LDS per wave (fc2_* offsets in OrbgGeom, host plan):
-//   tA [H][P]     window row r at byte r * P + 1 + x (x window-local), i.e. dword j holds
+//   tA [H][2P]    window row r at byte r * 2P + 1 + x (x window-local), i.e. dword j holds
 //                 window bytes 4j-1 .. 4j+2; a unit (ry, gg) = detection pixels
 //                 x = 3 + 4gg .. 6 + 4gg of row 3 + ry, and its circle is dwords gg .. gg+2
 //                 of rows ry .. ry+6
-//   tB [H][P]     tA shifted by 2 bytes (tB byte k = tA byte k + 2): pixels 2-3 of a unit
-//                 sit where pixels 0-1 sit in tA
+//   tB            tA shifted by 2 bytes (tB byte k = tA byte k + 2): pixels 2-3 of a unit
+//                 sit where pixels 0-1 sit in tA; row r of tB is at byte r * 2P + P, between
+//                 rows r and r + 1 of tA, so the tile rows are 2P apart (for P = 48, 24 banks:
+//                 the pretest's 8 rows x 8 units of a wave read 64 distinct banks)
 //   sc [RH+2][P]  u8 scores at sc[ry + 1][4 + 4gg + i], zero border
 //   list u16      pretest survivors: ry << 8 | gg << 2 | half << 1 | dark
 #ifndef FC2_CPW
@@ -59,10 +61,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(FC2_WPE, 8)
     int c_count)
 {
     constexpr int P = 4 * P4;
+    constexpr int RS = 2 * P, RS4 = 2 * P4;  // tile row stride (bytes, dwords)
     extern __shared__ __attribute__((aligned(16))) uint32_t fc2_lds[];
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
     uint8_t *tA = (uint8_t *)fc2_lds + wv * g->fc2_wave_bytes;
-    uint8_t *tB = tA + g->fc2_tileb_off;
+    uint8_t *tB = tA + P;
     uint8_t *sc = tA + g->fc2_sc_off;
     uint16_t *list = (uint16_t *)(tA + g->fc2_list_off);
     const int total = c_count * nframes;
@@ -118,17 +121,20 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(FC2_WPE, 8)
     auto put = [&](const Fc2Cell &k, int i, uint4 q, uint2 q2, uint32_t sh) {
         const int mdiv = (65536 + k.NC - 1) / k.NC;
         const int r = (i * mdiv) >> 16, cc = i - r * k.NC;
-        const int to = r * P + 16 * cc;
+        const int to = r * RS + 16 * cc;
         const uint32_t d[6] = {q.x, q.y, q.z, q.w, q2.x, q2.y};
         uint32_t A[5], Bw[4];
 #pragma unroll
         for (int j = 0; j < 5; j++) A[j] = __builtin_amdgcn_alignbyte(d[j + 1], d[j], sh);
 #pragma unroll
         for (int j = 0; j < 4; j++) Bw[j] = __builtin_amdgcn_alignbyte(A[j + 1], A[j], 2);
-        *(uint2 *)(tA + to) = make_uint2(A[0], A[1]);
-        *(uint2 *)(tA + to + 8) = make_uint2(A[2], A[3]);
-        *(uint2 *)(tB + to) = make_uint2(Bw[0], Bw[1]);
-        *(uint2 *)(tB + to + 8) = make_uint2(Bw[2], Bw[3]);
+        *(uint4 *)(tA + to) = make_uint4(A[0], A[1], A[2], A[3]);  // RS: multiple of 16
+        if constexpr (P % 16 == 0) {
+            *(uint4 *)(tB + to) = make_uint4(Bw[0], Bw[1], Bw[2], Bw[3]);
+        } else {
+            *(uint2 *)(tB + to) = make_uint2(Bw[0], Bw[1]);
+            *(uint2 *)(tB + to + 8) = make_uint2(Bw[2], Bw[3]);
+        }
     };
 
 #pragma unroll 1
@@ -184,8 +190,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(FC2_WPE, 8)
     {
         const v2s vth1 = (v2s){(short)(thi + 1), (short)(thi + 1)};
         // tile offset of unit (ry, gg) kept incrementally (no per-iteration multiply)
-        int toff = ry0 * P + 4 * gg0;
-        const int tstep = rstep * P + 4 * gstep, twrap = P - 4 * RG;
+        int toff = ry0 * RS + 4 * gg0;
+        const int tstep = rstep * RS + 4 * gstep, twrap = RS - 4 * RG;
         for (int u0 = 0, ry = ry0, gg = gg0; u0 < nunits; u0 += 64) {
             const int u = u0 + lane;
             // per pair: bright / dark survivors as the sign bits (15, 31) of a packed word,
@@ -197,8 +203,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(FC2_WPE, 8)
 #pragma unroll
                 for (int k = 0; k < 3; k++) {
                     r0[k] = p[k];
-                    r3[k] = p[3 * P4 + k];
-                    r6[k] = p[6 * P4 + k];
+                    r3[k] = p[3 * RS4 + k];
+                    r6[k] = p[6 * RS4 + k];
                 }
                 const int valid = RW - 4 * gg;  // pixels of the unit inside the region (>= 1)
                 const uint32_t invA = valid > 1 ? 0u : 0x80000000u;
@@ -264,13 +270,13 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(FC2_WPE, 8)
         }
         const int ry = e >> 8, gg = (e >> 2) & 63, half = (e >> 1) & 1;
         const uint32_t flip = (e & 1) ? 0xFFFFFFFFu : 0u;  // dark: complemented bytes
-        const uint32_t *p = (const uint32_t *)((half ? tB : tA) + ry * P + 4 * gg);
+        const uint32_t *p = (const uint32_t *)(tA + half * P + ry * RS + 4 * gg);
         Rows7 R;
 #pragma unroll
         for (int r = 0; r < 7; r++) {
-            R.w[r][0] = p[r * P4] ^ flip;
-            R.w[r][1] = p[r * P4 + 1] ^ flip;
-            R.w[r][2] = p[r * P4 + 2] ^ flip;
+            R.w[r][0] = p[r * RS4] ^ flip;
+            R.w[r][1] = p[r * RS4 + 1] ^ flip;
+            R.w[r][2] = p[r * RS4 + 2] ^ flip;
         }
         const v2s s = fast_score_side<0>(R);
         const uint32_t s0 = (uint16_t)s.x >= (uint32_t)thi ? (uint16_t)s.x : 0u;
@@ -377,12 +383,12 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(FC2_WPE, 8)
         wave_sync_lds();
         for (int u = lane, ry = ry0, gg = gg0; u < nunits; u += 64) {
             Rows7 R;
-            const uint32_t *p = (const uint32_t *)(tA + ry * P + 4 * gg);
+            const uint32_t *p = (const uint32_t *)(tA + ry * RS + 4 * gg);
 #pragma unroll
             for (int r = 0; r < 7; r++) {
-                R.w[r][0] = p[r * P4];
-                R.w[r][1] = p[r * P4 + 1];
-                R.w[r][2] = p[r * P4 + 2];
+                R.w[r][0] = p[r * RS4];
+                R.w[r][1] = p[r * RS4 + 1];
+                R.w[r][2] = p[r * RS4 + 2];
             }
             const v2s sa = fast_score_pair<0>(R);
             const v2s sb = fast_score_pair<2>(R);

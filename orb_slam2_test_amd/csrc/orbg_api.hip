@@ -868,8 +868,8 @@ static int plan(orbg_ctx *c, int w, int h, int batch)
             return set_err(ORBG_ENOTSUP, "FAST cell %dx%d needs %d LDS bytes per wave", wmax,
                            hmax, G.fc_wave_bytes);
         // k_fast2 (fast_kernels.hip): compile-time pitch P4 >= 4 * ceil((RG + 3) / 4) (its
-        // 16-byte window chunks) among the instantiated ones; layout tA | tB (hmax rows each)
-        // | scores (hmax - 4 rows) | list (2 entries per unit).  Preferred: the most
+        // 16-byte window chunks) among the instantiated ones; layout tA / tB (hmax rows each,
+        // interleaved: row stride 2 * P) | scores (hmax - 4 rows) | list (2 entries per unit).  Preferred: the most
         // workgroups per CU by LDS (capped at 6: the VGPR bound), then the bank-spread cost.
         G.fc2_p4 = 0;
         if (c->fast_v2) {
@@ -886,7 +886,7 @@ static int plan(orbg_ctx *c, int w, int h, int batch)
                     for (int k = 0; k < 3; k++) {
                         int hist[64] = {0}, mx = 0;
                         for (int lane = 0; lane < 64; lane++) {
-                            const int b = ((lane / r) * wd + lane % r + k) & 63;
+                            const int b = ((lane / r) * 2 * wd + lane % r + k) & 63;
                             mx = std::max(mx, ++hist[b]);
                         }
                         cost += mx;
@@ -899,7 +899,7 @@ static int plan(orbg_ctx *c, int w, int h, int batch)
             }
             if (G.fc2_p4) {
                 const int P2 = 4 * G.fc2_p4;
-                G.fc2_tileb_off = hmax * P2;
+                G.fc2_tileb_off = P2;  // tB rows interleaved with tA's (row stride 2 * P2)
                 G.fc2_sc_off = 2 * hmax * P2;
                 G.fc2_list_off = G.fc2_sc_off + (std::max(hmax - 6, 0) + 2) * P2;
                 G.fc2_list_cap = 2 * max_units;
