@@ -4,7 +4,7 @@
 #include <stdint.h>
 
 // One k_octree_lds launch covers levels level0 .. level0 + gridDim.x - 1.  Dynamic LDS =
-// kcap * 6 + uni_bytes + acap2 * 2 (octree_kernels.hip OctLdsView).
+// kcap * 7 + uni_bytes + acap2 * 4 (octree_kernels.hip OctLdsView).
 struct OctLdsDims {
     int32_t level0;
     int32_t kcap;       // candidates per level this launch can hold (multiple of 64)
@@ -23,5 +23,5 @@ struct OctLdsHdr {
 
 static inline size_t oct_lds_bytes(const OctLdsDims &d)
 {
-    return (size_t)d.kcap * 6 + (size_t)d.uni_bytes + (size_t)d.acap2 * 2;
+    return (size_t)d.kcap * 7 + (size_t)d.uni_bytes + (size_t)d.acap2 * 4;
 }

@@ -29,13 +29,18 @@ namespace orbg {
 #define OCT_BSHIFT 18      // code >> 18 = root (4 bits) + digits 0..4
 
 // LDS: a static header plus a dynamic area sized per launch (OctLdsDims, host
-// octree_lds_bytes): codes[kcap] u32 | sidx[kcap] u16 | uni | aux[acap2] u16, where uni is
-// the bucket counters (nbw u32, two u16 counters each) during the sort and afterwards the
-// two list buffers + the phase-2 sort keys (3 x acap u64).  A launch whose levels need
-// little LDS runs several workgroups per CU.
+// octree_lds_bytes): codes[kcap] u32 | sidx[kcap] u16 | resp[kcap] u8 | uni | aux[acap2] u16
+// | coff[acap2] u16, where uni is the bucket counters (nbw u32, two u16 counters each) during
+// the sort and afterwards the two list buffers + the phase-2 sort keys (3 x acap u64); resp
+// is each candidate's FAST response and coff the cells' first candidate index, so the
+// candidates never go through global scratch: the scatter and the winners re-read the
+// cell lists (cell_kp, L2-resident).  A launch whose levels need little LDS runs several
+// workgroups per CU.
 struct OctLdsView {
     uint32_t *codes;
     uint16_t *sidx;
+    uint8_t *resp;
+    uint16_t *coff;
     uint32_t *bcnt;
     unsigned long long *list0, *list1;
     __device__ unsigned long long *list(int k) const { return k ? list1 : list0; }
@@ -163,8 +168,7 @@ __device__ __forceinline__ void oct_children(uint32_t *codes, uint16_t *sidx,
 // n <= D.kcap (k_octree takes the rest, same threshold)
 __global__ __launch_bounds__(OCT_T) void k_octree_lds(
     const OrbgGeom *__restrict__ g, const int32_t *__restrict__ cell_cnt,
-    const uint2 *__restrict__ cell_kp, uint32_t *__restrict__ keys_all,
-    uint32_t *__restrict__ scratch_all, uint32_t *__restrict__ lvl_kp,
+    const uint2 *__restrict__ cell_kp, uint32_t *__restrict__ lvl_kp,
     int32_t *__restrict__ lvl_cnt, int32_t *__restrict__ err_flag, OctLdsDims D)
 {
     __shared__ OctLdsHdr S;
@@ -176,17 +180,18 @@ __global__ __launch_bounds__(OCT_T) void k_octree_lds(
         p += (size_t)D.kcap * 4;
         V.sidx = (uint16_t *)p;
         p += (size_t)D.kcap * 2;
+        V.resp = p;
+        p += (size_t)D.kcap;  // kcap: multiple of 64, so uni stays 8-byte aligned
         V.bcnt = (uint32_t *)p;
         V.list0 = (unsigned long long *)p;
         V.list1 = V.list0 + D.acap;
         V.sortv = V.list1 + D.acap;
         p += D.uni_bytes;
         V.aux = (uint16_t *)p;
+        V.coff = V.aux + D.acap2;
     }
     const int l = D.level0 + blockIdx.y, f = blockIdx.x, tid = threadIdx.x;
     const OrbgLevel &lv = g->lv[l];
-    const int64_t kbase = (int64_t)f * g->keys_frame + lv.key_off;
-    uint32_t *kglob = keys_all + kbase;
     const int N = lv.nfeat, nIni = lv.nini;
 
     // ---- candidate count; larger levels (or > ALIVE-1 cells) belong to k_octree ----
@@ -199,19 +204,19 @@ __global__ __launch_bounds__(OCT_T) void k_octree_lds(
         const int c = c0 + tid;
         int tot;
         const int off = oct_scan(c < ncells ? ccount[c] : 0, &tot, S.red) + n;
-        if (c < ncells) V.aux[c] = (uint16_t)min(off, 65535);
+        if (c < ncells) V.aux[c] = V.coff[c] = (uint16_t)min(off, 65535);
         n += tot;
     }
     if (n > D.kcap) return;
-    if (tid == 0) V.aux[ncells] = (uint16_t)n;
+    if (tid == 0) V.aux[ncells] = V.coff[ncells] = (uint16_t)n;
     for (int i = tid; i < D.nbw; i += OCT_T) V.bcnt[i] = 0;
     __syncthreads();
 
-    // ---- gather (vToDistributeKeys order: cell-major, FAST order inside a cell) +
-    //      bucket histogram: one wave per cell (lane = slot), four cells' loads in flight;
-    //      each candidate's path code also goes to global scratch for the scatter ----
-    uint32_t *cscr = scratch_all + 2 * kbase;  // flattened path codes
-    {
+    // ---- bucket histogram over the candidates (vToDistributeKeys order: cell-major, FAST
+    //      order inside a cell; candidate k = coff[c] + slot), responses to LDS: one wave per
+    //      cell (lane = slot), four cells' loads in flight.  per_cell(fn) walks the cell lists;
+    //      the scatter walks them again (the lists are L2-resident by then) ----
+    auto per_cell = [&](auto &&fn) {
         const int lane = tid & 63, wv = tid >> 6;
         constexpr int NW = OCT_T / 64;
         for (int c0 = wv; c0 < ncells; c0 += 4 * NW) {
@@ -224,31 +229,27 @@ __global__ __launch_bounds__(OCT_T) void k_octree_lds(
                 k[u] = 0;
                 e[u] = make_uint2(0, 0);
                 if (c < ncells) {
-                    const int lo = V.aux[c];
-                    cnt[u] = (int)V.aux[c + 1] - lo;
+                    const int lo = V.coff[c];
+                    cnt[u] = (int)V.coff[c + 1] - lo;
                     k[u] = lo + lane;
                     if (lane < cnt[u]) e[u] = ckp[(int64_t)c * g->cell_cap + lane];
                 }
             }
 #pragma unroll
             for (int u = 0; u < 4; u++) {
-                if (lane < cnt[u]) {
-                    kglob[k[u]] = e[u].x;
-                    cscr[k[u]] = e[u].y;
-                    const uint32_t b = e[u].y >> OCT_BSHIFT;
-                    atomicAdd(&V.bcnt[b >> 1], 1u << (16 * (b & 1)));
-                }
+                if (lane < cnt[u]) fn(k[u], e[u]);
                 for (int kl = lane + 64; kl < cnt[u]; kl += 64) {  // cells with > 64 corners
                     const int c = c0 + u * NW;
-                    const uint2 x = ckp[(int64_t)c * g->cell_cap + kl];
-                    kglob[k[u] - lane + kl] = x.x;
-                    cscr[k[u] - lane + kl] = x.y;
-                    const uint32_t b = x.y >> OCT_BSHIFT;
-                    atomicAdd(&V.bcnt[b >> 1], 1u << (16 * (b & 1)));
+                    fn(k[u] - lane + kl, ckp[(int64_t)c * g->cell_cap + kl]);
                 }
             }
         }
-    }
+    };
+    per_cell([&](int k, uint2 e) {
+        V.resp[k] = (uint8_t)orbg_ps(e.x);
+        const uint32_t b = e.y >> OCT_BSHIFT;
+        atomicAdd(&V.bcnt[b >> 1], 1u << (16 * (b & 1)));
+    });
     __syncthreads();
     if (g->dbg == 1) return;
     // ---- exclusive scan of the nini * 1024 u16 bucket counters (2 * nini per thread) ----
@@ -267,26 +268,14 @@ __global__ __launch_bounds__(OCT_T) void k_octree_lds(
         }
     }
     __syncthreads();
-    // ---- scatter into bucket order (unordered inside a bucket), codes read back flat ----
-    for (int k0 = tid; k0 < n; k0 += 4 * OCT_T) {
-        uint32_t code[4];
-#pragma unroll
-        for (int u = 0; u < 4; u++) {
-            const int k = k0 + u * OCT_T;
-            code[u] = k < n ? cscr[k] : 0u;
-        }
-#pragma unroll
-        for (int u = 0; u < 4; u++) {
-            const int k = k0 + u * OCT_T;
-            if (k < n) {
-                const uint32_t b = code[u] >> OCT_BSHIFT;
-                const uint32_t old = atomicAdd(&V.bcnt[b >> 1], 1u << (16 * (b & 1)));
-                const int slot = (int)((old >> (16 * (b & 1))) & 0xFFFF);
-                V.codes[slot] = code[u];
-                V.sidx[slot] = (uint16_t)k;
-            }
-        }
-    }
+    // ---- scatter into bucket order (unordered inside a bucket) ----
+    per_cell([&](int k, uint2 e) {
+        const uint32_t code = e.y, b = code >> OCT_BSHIFT;
+        const uint32_t old = atomicAdd(&V.bcnt[b >> 1], 1u << (16 * (b & 1)));
+        const int slot = (int)((old >> (16 * (b & 1))) & 0xFFFF);
+        V.codes[slot] = code;
+        V.sidx[slot] = (uint16_t)k;
+    });
     __syncthreads();
     if (g->dbg == 2) return;
 
@@ -556,25 +545,26 @@ __global__ __launch_bounds__(OCT_T) void k_octree_lds(
         best[i] = 0;
     }
     __syncthreads();
-    for (int p0 = tid; p0 < n; p0 += 4 * OCT_T) {
-        uint32_t key[4], pos[4], idx[4];
-#pragma unroll
-        for (int u = 0; u < 4; u++) {
-            const int p = p0 + u * OCT_T;
-            idx[u] = p < n ? V.sidx[p] : 0;
-            pos[u] = p < n ? V.codes[p] : 0;
-        }
-#pragma unroll
-        for (int u = 0; u < 4; u++) key[u] = kglob[idx[u]];
-#pragma unroll
-        for (int u = 0; u < 4; u++)
-            if (p0 + u * OCT_T < n)
-                atomicMax(&best[pos[u]], ((uint32_t)orbg_ps(key[u]) << 24) | (0xFFFFFFu - idx[u]));
+    for (int p = tid; p < n; p += OCT_T) {
+        const uint32_t idx = V.sidx[p], pos = V.codes[p];
+        atomicMax(&best[pos], ((uint32_t)V.resp[idx] << 24) | (0xFFFFFFu - idx));
     }
     __syncthreads();
+    // winners: candidate index -> its cell (last c with coff[c] <= idx) -> the cell list entry
     uint32_t *out = lvl_kp + (int64_t)f * g->out_frame + lv.out_off;
     const int nout = min(alive, lv.out_cap);
-    for (int i = tid; i < nout; i += OCT_T) out[i] = kglob[0xFFFFFFu - (best[i] & 0xFFFFFFu)];
+    for (int i = tid; i < nout; i += OCT_T) {
+        const int idx = (int)(0xFFFFFFu - (best[i] & 0xFFFFFFu));
+        int a = 0, z = ncells;  // coff[a] <= idx < coff[z]
+        while (z - a > 1) {
+            const int m = (a + z) >> 1;
+            if ((int)V.coff[m] <= idx)
+                a = m;
+            else
+                z = m;
+        }
+        out[i] = ckp[(int64_t)a * g->cell_cap + (idx - (int)V.coff[a])].x;
+    }
     if (tid == 0) {
         lvl_cnt[(int64_t)f * g->L + l] = nout;
         if (alive > lv.out_cap) {

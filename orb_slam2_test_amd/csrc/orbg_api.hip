@@ -34,7 +34,7 @@ __global__ void k_octree(const OrbgGeom *, const int32_t *, const uint2 *, uint3
                          uint32_t *, uint32_t *, uint8_t *, int4 *, uint32_t *, int32_t *,
                          int32_t *);
 __global__ void k_octree_lds(const OrbgGeom *, const int32_t *, const uint2 *, uint32_t *,
-                             uint32_t *, uint32_t *, int32_t *, int32_t *, OctLdsDims);
+                             int32_t *, int32_t *, OctLdsDims);
 // fast_kernels.hip
 bool fast2_pitch_ok(int p4);
 __global__ void k_pyramid(PyrArgs, const uint4 *, const int4 *, const int2 *, const uint8_t *,
@@ -933,8 +933,8 @@ static int plan(orbg_ctx *c, int w, int h, int batch)
             d.nbw = 512 * roots;
             d.uni_bytes = std::max(d.nbw * 4, 3 * d.acap * 8);
             if (budget) {
-                const int room = kcap_or_budget - d.uni_bytes - 2 * d.acap2;
-                d.kcap = std::min(OCT_KEY_CAP, std::max(0, room / 6) & ~63);
+                const int room = kcap_or_budget - d.uni_bytes - 4 * d.acap2;
+                d.kcap = std::min(OCT_KEY_CAP, std::max(0, room / 7) & ~63);
             } else {
                 d.kcap = kcap_or_budget;
             }
@@ -1361,13 +1361,13 @@ static int launch_extract_pipe(orbg_ctx *c, const uint8_t *d_imgs, int B, int pi
     PROF_LAUNCH(c, "octree",
                 hipLaunchKernelGGL(k_octree_lds, dim3(B, 1), dim3(512),
                                    oct_lds_bytes(c->oct_dims[0]), st, c->d_geom, c->d_cell_cnt,
-                                   c->d_cell_kp, c->d_keys, c->d_act, c->d_lvl_kp, c->d_lvl_cnt,
+                                   c->d_cell_kp, c->d_lvl_kp, c->d_lvl_cnt,
                                    c->d_err, c->oct_dims[0]));
     if (G.L > 1)
         PROF_LAUNCH(c, "octree",
                     hipLaunchKernelGGL(k_octree_lds, dim3(B, G.L - 1), dim3(512),
                                        oct_lds_bytes(c->oct_dims[1]), st, c->d_geom,
-                                       c->d_cell_cnt, c->d_cell_kp, c->d_keys, c->d_act,
+                                       c->d_cell_cnt, c->d_cell_kp,
                                        c->d_lvl_kp, c->d_lvl_cnt, c->d_err, c->oct_dims[1]));
     PROF_LAUNCH(c, "octree_big",
                 hipLaunchKernelGGL(k_octree, dim3(G.L, B), dim3(ORBG_OCT_THREADS), 0, st,
@@ -1452,7 +1452,7 @@ static int launch_extract(orbg_ctx *c, const uint8_t *d_imgs, int B, int pitch, 
         PROF_LAUNCH(c, "octree",
                     hipLaunchKernelGGL(k_octree_lds, dim3(B, 1), dim3(512),
                                        oct_lds_bytes(c->oct_dims[0]), st, c->d_geom,
-                                       c->d_cell_cnt, c->d_cell_kp, c->d_keys, c->d_act,
+                                       c->d_cell_cnt, c->d_cell_kp,
                                        c->d_lvl_kp, c->d_lvl_cnt, c->d_err, c->oct_dims[0]));
         if (oct_mode == 2 && G.L > 1) {
             // levels 1.. need their FAST cells (launched on the extraction stream under fast0)
@@ -1463,7 +1463,7 @@ static int launch_extract(orbg_ctx *c, const uint8_t *d_imgs, int B, int pitch, 
             PROF_LAUNCH(c, "octree",
                         hipLaunchKernelGGL(k_octree_lds, dim3(B, G.L - 1), dim3(512),
                                            oct_lds_bytes(c->oct_dims[1]), st, c->d_geom,
-                                           c->d_cell_cnt, c->d_cell_kp, c->d_keys, c->d_act,
+                                           c->d_cell_cnt, c->d_cell_kp,
                                            c->d_lvl_kp, c->d_lvl_cnt, c->d_err, c->oct_dims[1]));
         }
         if (blur0)
@@ -1481,7 +1481,7 @@ static int launch_extract(orbg_ctx *c, const uint8_t *d_imgs, int B, int pitch, 
         PROF_LAUNCH(c, "octree",
                     hipLaunchKernelGGL(k_octree_lds, dim3(B, G.L - 1), dim3(512),
                                        oct_lds_bytes(c->oct_dims[1]), st, c->d_geom,
-                                       c->d_cell_cnt, c->d_cell_kp, c->d_keys, c->d_act,
+                                       c->d_cell_cnt, c->d_cell_kp,
                                        c->d_lvl_kp, c->d_lvl_cnt, c->d_err, c->oct_dims[1]));
     if (oct_mode) HIPCHK(hipStreamWaitEvent(st, c->ev_oct, 0));
     PROF_LAUNCH(c, "octree_big",
