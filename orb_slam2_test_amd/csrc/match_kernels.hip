@@ -202,11 +202,12 @@ __device__ __forceinline__ void knn2_block(const uint8_t *__restrict__ q, int nq
 // needs for K = 32, so K = 256 is four MFMAs instead of eight.  Every bit becomes +-1.0 in
 // e2m1 (0x2 = +1, 0xA = -1): train (A) b=1 -> -1, query (B) b=1 -> +1 (b=0 the opposite), so
 // one product is -1 where the bits agree and +1 where they differ; the E8M0 scale 2^12 on A
-// makes the dot product 4096 (d - (256 - d)) = 8192 d - 2^20, and the C input (train index)
-// is added as before.  Every partial sum is an integer below 2^22 in magnitude, exact in
-// the f32 accumulator whatever the summation order, so the f32 key equals the i8 kernel's
-// i32 key value; past-nt rows carry 2^30 (rounded sums stay >= 2^30 - 2^20, above every
-// real key).  k order (A and B alike): step s, lane half h -> descriptor dword 2s + h; VGPR
+// makes the dot product 4096 (d - (256 - d)) = 8192 d - 2^20, and the C input is the train
+// index + 2^20, so the key is 8192 d + index >= 0.  Every partial sum is an integer below
+// 2^22 in magnitude, exact in the f32 accumulator whatever the summation order; a
+// non-negative f32 orders like its bit pattern, so the top-2 runs on the u32 bits (integer
+// min / med3: no NaN canonicalisation).  Past-nt rows carry 2^30 (rounded sums stay
+// >= 2^30 - 2^20, above every real key).  k order (A and B alike): step s, lane half h -> descriptor dword 2s + h; VGPR
 // q, nibble j -> bit 4j + q of that dword.
 typedef int knn_v8i __attribute__((ext_vector_type(8)));
 typedef float knn_v16f __attribute__((ext_vector_type(16)));
@@ -252,8 +253,7 @@ __device__ __forceinline__ void knn2_block_fp4(const uint8_t *__restrict__ q, in
             }
         }
     }
-    float k1[2] = {__builtin_huge_valf(), __builtin_huge_valf()};
-    float k2[2] = {__builtin_huge_valf(), __builtin_huge_valf()};
+    uint32_t k1[2] = {UINT_MAX, UINT_MAX}, k2[2] = {UINT_MAX, UINT_MAX};
 
     // expansion of stage s0 (64 rows) into buffer bf: thread -> rows (tid >> 3) and
     // (tid >> 3) + 32, dword tid & 7 -> 16 bytes at row offset 16 * dword
@@ -277,19 +277,46 @@ __device__ __forceinline__ void knn2_block_fp4(const uint8_t *__restrict__ q, in
         xr0 = fetch1(64 + er);
         xr1 = fetch1(96 + er);
     }
-    knn_v16f pacc[2];
-    bool pend = false;
-    auto epilogue = [&]() {
+    // two accumulator sets, one per 32-row subtile of a stage: the top-2 epilogue of one set
+    // runs while the MFMAs of the other are in flight (no accumulator copies)
+    knn_v16f accA[2], accB[2];
+    auto epilogue = [&](const knn_v16f (&acc)[2]) {
 #pragma unroll
         for (int r = 0; r < 16; r++) {
 #pragma unroll
             for (int u = 0; u < 2; u++) {
                 // k1 <= k2: the new second key is med3(k1, k2, key), then the new minimum
-                k2[u] = __builtin_amdgcn_fmed3f(k1[u], k2[u], pacc[u][r]);
-                k1[u] = fminf(k1[u], pacc[u][r]);
+                // (via a scalar: __builtin_bit_cast of an ext_vector element lvalue reads
+                // element 0 under this clang)
+                const float kf = acc[u][r];
+                const uint32_t key = __float_as_uint(kf);
+                k2[u] = min(k2[u], max(k1[u], key));
+                k1[u] = min(k1[u], key);
             }
         }
     };
+    auto subtile = [&](int tb, int bf, int sub, knn_v16f (&acc)[2]) {
+        knn_v16f ctag;
+        const float tbh = (float)(tb + 4 * h + (1 << 20));
+#pragma unroll
+        for (int r = 0; r < 16; r++) ctag[r] = tbh + (float)((r & 3) + 8 * (r >> 2));
+        if (tb + 32 > nt) {  // last subtile: rows past nt get keys above every real one
+#pragma unroll
+            for (int r = 0; r < 16; r++)
+                if (ctag[r] >= (float)(nt + (1 << 20))) ctag[r] = (float)KNN_NONE;
+        }
+        const uint8_t *arow = tile[bf] + (32 * sub + col) * KNN4_ROWB + h * 16;
+#pragma unroll
+        for (int s = 0; s < 4; s++) {
+            const knn_v4i a4 = *(const knn_v4i *)(arow + s * 32);
+            const knn_v8i a = {a4[0], a4[1], a4[2], a4[3], 0, 0, 0, 0};
+            acc[0] = __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(
+                a, bq[0][s], s ? acc[0] : ctag, 4, 4, 0, KNN4_SCALE_A, 0, KNN4_SCALE_B);
+            acc[1] = __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(
+                a, bq[1][s], s ? acc[1] : ctag, 4, 4, 0, KNN4_SCALE_A, 0, KNN4_SCALE_B);
+        }
+    };
+    bool pendB = false;
     for (int s0 = 0, bf = 0; s0 < nt; s0 += 64, bf ^= 1) {
         __syncthreads();
         if (s0 + 64 < nt) {
@@ -297,47 +324,25 @@ __device__ __forceinline__ void knn2_block_fp4(const uint8_t *__restrict__ q, in
             xr0 = fetch1(s0 + 128 + er);
             xr1 = fetch1(s0 + 160 + er);
         }
-#pragma unroll
-        for (int sub = 0; sub < 2; sub++) {
-            const int tb = s0 + 32 * sub;
-            if (tb >= nt) break;
-            knn_v16f ctag;
-            const float tbh = (float)(tb + 4 * h);
-#pragma unroll
-            for (int r = 0; r < 16; r++) ctag[r] = tbh + (float)((r & 3) + 8 * (r >> 2));
-            if (tb + 32 > nt) {  // last subtile: rows past nt get keys above every real one
-#pragma unroll
-                for (int r = 0; r < 16; r++)
-                    if (ctag[r] >= (float)nt) ctag[r] = (float)KNN_NONE;
-            }
-            knn_v16f acc[2];
-            const uint8_t *arow = tile[bf] + (32 * sub + col) * KNN4_ROWB + h * 16;
-#pragma unroll
-            for (int s = 0; s < 4; s++) {
-                const knn_v4i a4 = *(const knn_v4i *)(arow + s * 32);
-                const knn_v8i a = {a4[0], a4[1], a4[2], a4[3], 0, 0, 0, 0};
-                acc[0] = __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(
-                    a, bq[0][s], s ? acc[0] : ctag, 4, 4, 0, KNN4_SCALE_A, 0, KNN4_SCALE_B);
-                acc[1] = __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(
-                    a, bq[1][s], s ? acc[1] : ctag, 4, 4, 0, KNN4_SCALE_A, 0, KNN4_SCALE_B);
-            }
-            if (pend) epilogue();
-            pacc[0] = acc[0];
-            pacc[1] = acc[1];
-            pend = true;
-        }
+        subtile(s0, bf, 0, accA);
+        if (pendB) epilogue(accB);
+        pendB = s0 + 32 < nt;
+        if (pendB) subtile(s0 + 32, bf, 1, accB);
+        epilogue(accA);
     }
-    if (pend) epilogue();
-    const float none = (float)(KNN_NONE - (1 << 20));
+    if (pendB) epilogue(accB);
+    const uint32_t none = 0x4E000000u;  // bits of 2^29: real keys < 2^22, past-nt >= 2^30 - 2^20
 #pragma unroll
     for (int u = 0; u < 2; u++) {
-        const float o1 = __shfl_xor(k1[u], 32, 64), o2 = __shfl_xor(k2[u], 32, 64);
-        const float b1 = fminf(k1[u], o1);
-        const float b2 = fminf(fminf(k2[u], o2), fmaxf(k1[u], o1));
+        const uint32_t o1 = (uint32_t)__shfl_xor((int)k1[u], 32, 64);
+        const uint32_t o2 = (uint32_t)__shfl_xor((int)k2[u], 32, 64);
+        const uint32_t b1 = min(k1[u], o1);
+        const uint32_t b2 = min(min(k2[u], o2), max(k1[u], o1));
         const int qi = qbase + wv * 64 + u * 32 + col;
         if (h == 0 && qi < nq) {
             const bool v1 = b1 < none, v2 = b2 < none;
-            const int e1 = v1 ? (int)b1 + (1 << 20) : 0, e2 = v2 ? (int)b2 + (1 << 20) : 0;
+            const int e1 = v1 ? (int)__builtin_bit_cast(float, b1) : 0;
+            const int e2 = v2 ? (int)__builtin_bit_cast(float, b2) : 0;
             out[(size_t)qi * 3 + 0] = v1 ? (e1 & (KNN_MAX_TRAIN - 1)) : -1;
             out[(size_t)qi * 3 + 1] = v1 ? (e1 >> 13) : INT_MAX;
             out[(size_t)qi * 3 + 2] = v2 ? (e2 >> 13) : INT_MAX;
