@@ -714,6 +714,7 @@ __global__ __launch_bounds__(256) void k_blur(const OrbgGeom *__restrict__ g,
     };
     const uint32_t k0 = g->gk[0], k1 = g->gk[1], k2 = g->gk[2], k3 = g->gk[3], k4 = g->gk[4],
                    k5 = g->gk[5], k6 = g->gk[6];
+    const uint32_t ksum = k0 + k1 + k2 + k3 + k4 + k5 + k6;
     // row pass weights: output x = 4j+i of a row needs tile bytes 4j+1+i .. 4j+7+i, i.e. the
     // aligned dwords W0..W2 = bytes 4j .. 4j+11 against the 7 weights placed at byte 1+i
     const uint32_t K00 = k0 << 8 | k1 << 16 | k2 << 24, K01 = k3 | k4 << 8 | k5 << 16 | k6 << 24;
@@ -760,6 +761,12 @@ __global__ __launch_bounds__(256) void k_blur(const OrbgGeom *__restrict__ g,
         __syncthreads();
         // column pass: outputs o = 4rg .. 4rg+3 from tile rows o .. o+6, i.e. row pairs
         // 2rg .. 2rg+4; four v_dot2_u32_u16 per output (sums <= 257 * 65535 fit 32 bits)
+        // weights summing to 256 (the >= 3.4.9 table): S + 2^15 < 2^24, so the output byte is
+        // byte 2 of the sum with the rounding term as the dot2 chain's initial value -- no
+        // saturation, four outputs packed by two v_perm; the legacy table (sum 257) keeps
+        // the saturating path
+        const bool norm256 = ksum == 256u;
+        const uint32_t c0 = norm256 ? (1u << 15) : 0u;
         uint32_t acc[4][4];
         {
             uint4 P[5];
@@ -775,12 +782,12 @@ __global__ __launch_bounds__(256) void k_blur(const OrbgGeom *__restrict__ g,
                     const int m = o >> 1;  // first pair of output 4rg+o: 2rg + m
                     uint32_t a2;
                     if ((o & 1) == 0) {
-                        a2 = udot2_u32(col(m), E0, 0u);
+                        a2 = udot2_u32(col(m), E0, c0);
                         a2 = udot2_u32(col(m + 1), E1, a2);
                         a2 = udot2_u32(col(m + 2), E2, a2);
                         a2 = udot2_u32(col(m + 3), E3, a2);
                     } else {
-                        a2 = udot2_u32(col(m), O0, 0u);
+                        a2 = udot2_u32(col(m), O0, c0);
                         a2 = udot2_u32(col(m + 1), O1, a2);
                         a2 = udot2_u32(col(m + 2), O2, a2);
                         a2 = udot2_u32(col(m + 3), O3, a2);
@@ -793,9 +800,17 @@ __global__ __launch_bounds__(256) void k_blur(const OrbgGeom *__restrict__ g,
         for (int o = 0; o < 4; o++) {
             const int gy = ty0 + 4 * rg + o;
             if (gy >= H || gx >= W) continue;
-            uint32_t word = 0;
+            uint32_t word;
+            if (norm256) {
+                // bytes 2 of acc[o][0..3]: perm(b, a) picks byte 2 of a (sel 2) and of b (sel 6)
+                const uint32_t lo = __builtin_amdgcn_perm(acc[o][1], acc[o][0], 0x0c0c0602u);
+                const uint32_t hi = __builtin_amdgcn_perm(acc[o][3], acc[o][2], 0x06020c0cu);
+                word = lo | hi;
+            } else {
+                word = 0;
 #pragma unroll
-            for (int bc = 0; bc < 4; bc++) word |= min((acc[o][bc] + (1u << 15)) >> 16, 255u) << (8 * bc);
+                for (int bc = 0; bc < 4; bc++) word |= min((acc[o][bc] + (1u << 15)) >> 16, 255u) << (8 * bc);
+            }
             uint8_t *d = dst + (int64_t)gy * lv.pitch + gx;
             if (gx + 4 <= W) {
                 *(uint32_t *)d = word;  // pitch is a multiple of 64, gx of 4: aligned

@@ -39,6 +39,14 @@ __global__ void k_octree_lds(const OrbgGeom *, const int32_t *, const uint2 *, u
 bool fast2_pitch_ok(int p4);
 __global__ void k_pyramid(PyrArgs, const uint4 *, const int4 *, const int2 *, const uint8_t *,
                           int64_t, int, const uint8_t *, uint8_t *, int);
+// blur_kernels.hip
+int blur2_seg();
+int blur2_neg();
+int blur2_tw();
+hipError_t launch_blur2(hipStream_t st, const OrbgGeom *g, const int32_t *task_base,
+                        const int32_t *edge_base, int edges, const uint8_t *img0, int64_t img_fs,
+                        int img_pitch, const uint8_t *pyr, uint8_t *blur, int t_begin,
+                        int t_count, int l_begin, int l_end, int nframes);
 hipError_t launch_fast2(int p4, size_t lds, hipStream_t st, const OrbgGeom *g,
                         const OrbgCell *cells, const uint8_t *img0, int64_t img_fs,
                         int img_pitch, const uint8_t *pyr, const uint32_t *ctab,
@@ -233,6 +241,7 @@ struct orbg_ctx {
     int blur0_mode = 0;  // measured: 2.013 vs 2.025 ms per 256 frames with it on
     int fast0_mode = 1;  // level-0 FAST cells on `ostream` beside the resize chain (ORBG_FAST0)
     int fast_v2 = 1;     // k_fast2 (fast_kernels.hip) where its pitch fits, else k_fast_cells (ORBG_FAST_V=1)
+    int blur_v2 = 1;     // k_blur2 (blur_kernels.hip), else k_blur (ORBG_BLUR_V=1)
     // Pipelined batches (orbg_set_pipeline): the front of a batch (pyramid, FAST cells,
     // GaussianBlur: image work) runs on `stream`, its back (quadtree, orientation +
     // descriptors, stereo: keypoint work) on `ostream`, so the front of batch k+1 overlaps
@@ -260,7 +269,7 @@ struct orbg_ctx {
     int gw = 0, gh = 0, gbatch = 0;
     OrbgGeom geom{};
     std::vector<OrbgCell> cells;
-    std::vector<int32_t> tile_base;
+    std::vector<int32_t> tile_base;  // k_blur region bases, k_blur2 tiles, k_blur2_edge tasks (L + 1 each)
     int total_tiles = 0;
     OctLdsDims oct_dims[2] = {};
     // device
@@ -644,7 +653,8 @@ static int plan(orbg_ctx *c, int w, int h, int batch)
     }
     int64_t pyr_off = 0, blur_off = 0;
     int key_off = 0, node_off = 0, out_off = 0, tiles = 0;
-    std::vector<int32_t> tile_base;
+    std::vector<int32_t> tile_base, blur2_base, edge_base;
+    int blur2_tasks = 0, edge_tasks = 0;
     for (int l = 0; l < G.L; l++) {
         OrbgLevel &L = G.lv[l];
         L.w = lw[l];
@@ -754,6 +764,10 @@ static int plan(orbg_ctx *c, int w, int h, int batch)
         blur_off += (int64_t)L.pitch * L.h;
         tile_base.push_back(tiles);
         tiles += ((L.w + 127) / 128) * ((L.h + 32 * ORBG_BLUR_NB - 1) / (32 * ORBG_BLUR_NB));  // k_blur regions
+        blur2_base.push_back(blur2_tasks);  // k_blur2 (blur_kernels.hip): 244 x SEG wave tiles
+        blur2_tasks += ((L.w + blur2_tw() - 1) / blur2_tw()) * ((L.h + blur2_seg() - 1) / blur2_seg());
+        edge_base.push_back(edge_tasks);  // k_blur2_edge: row-end column groups per segment
+        edge_tasks += blur2_neg() * ((L.h + blur2_seg() - 1) / blur2_seg());
         // resize coefficient tables (cv::resize, INTER_LINEAR)
         if (l > 0) {
             const int sw = lw[l - 1], sh = lh[l - 1], dw = lw[l], dh = lh[l];
@@ -819,6 +833,12 @@ static int plan(orbg_ctx *c, int w, int h, int batch)
         }
     }
     tile_base.push_back(tiles);
+    blur2_base.push_back(blur2_tasks);
+    edge_base.push_back(edge_tasks);
+    // d_tile_base = k_blur region bases (L + 1), k_blur2 task bases (L + 1), k_blur2_edge
+    // task bases (L + 1)
+    tile_base.insert(tile_base.end(), blur2_base.begin(), blur2_base.end());
+    tile_base.insert(tile_base.end(), edge_base.begin(), edge_base.end());
     G.ncells = (int)cells.size();
     G.cell_cap = cell_cap;
     {
@@ -1123,6 +1143,8 @@ extern "C" int orbg_create(int device, const orbg_params *p, orbg_ctx **out)
         c->fast0_mode = f0 ? atoi(f0) : 1;
         const char *fv = getenv("ORBG_FAST_V");
         c->fast_v2 = fv ? (atoi(fv) >= 2) : 1;
+        const char *bv = getenv("ORBG_BLUR_V");
+        c->blur_v2 = bv ? (atoi(bv) >= 2) : 1;
         const char *b0 = getenv("ORBG_BLUR0");
         c->blur0_mode = b0 ? atoi(b0) : 0;
         const char *bp = getenv("ORBG_BACK_PRIO");  // developer A/B: normal | high (default)
@@ -1275,6 +1297,30 @@ static hipError_t launch_pyramid(orbg_ctx *c, hipStream_t st, const uint8_t *d_i
     return hipGetLastError();
 }
 
+// GaussianBlur of levels [l0, l1) of every frame on `st`: k_blur2 (one wave per 256 x SEG
+// output tile, blur_kernels.hip), or k_blur (ORBG_BLUR_V=1)
+static hipError_t launch_blur_levels(orbg_ctx *c, hipStream_t st, const uint8_t *d_imgs, int B,
+                                     int pitch, int64_t fs, int l0, int l1)
+{
+    const int L = c->geom.L;
+    if (c->blur_v2 && c->geom.lv[L - 1].w >= 16) {  // k_blur2 loads 16-byte row windows
+        const int32_t *b2 = c->tile_base.data() + L + 1, *eb = b2 + L + 1;
+        hipError_t e = hipSuccess;
+        PROF_LAUNCH(c, "blur",
+                    e = launch_blur2(st, c->d_geom, c->d_tile_base + L + 1,
+                                     c->d_tile_base + 2 * (L + 1), eb[l1] - eb[l0], d_imgs, fs,
+                                     pitch, c->d_pyr, c->d_blur, b2[l0], b2[l1] - b2[l0], l0, l1,
+                                     B));
+        return e;
+    }
+    const int t0 = c->tile_base[l0], t1 = c->tile_base[l1];
+    PROF_LAUNCH(c, "blur",
+                hipLaunchKernelGGL(k_blur, dim3((t1 - t0) * B), dim3(256), 0, st, c->d_geom,
+                                   c->d_tile_base, d_imgs, fs, pitch, c->d_pyr, c->d_blur, t0,
+                                   t1 - t0));
+    return hipGetLastError();
+}
+
 // FAST cells [cb, cb + cn) of every frame on `st` (k_fast2 where the plan picked a pitch)
 static hipError_t launch_fast_cells(orbg_ctx *c, hipStream_t st, const uint8_t *d_imgs, int B,
                                     int pitch, int64_t fs, int cb, int cn)
@@ -1315,7 +1361,7 @@ static int launch_extract_pipe(orbg_ctx *c, const uint8_t *d_imgs, int B, int pi
             c->back_pending[s] = false;
         }
         const bool side = c->fstream && G.L > 1;
-        const int n0 = side ? G.lv[1].cell_base : 0, tb1 = side ? c->tile_base[1] : 0;
+        const int n0 = side ? G.lv[1].cell_base : 0;
         if (side) {
             // level 0 beside the pyramid: FAST cells, then its GaussianBlur
             HIPCHK(hipEventRecord(c->ev_pfork[s], st));
@@ -1324,10 +1370,7 @@ static int launch_extract_pipe(orbg_ctx *c, const uint8_t *d_imgs, int B, int pi
                 hipStream_t st = c->fstream;  // PROF_LAUNCH records on `st`
                 HIPCHK(launch_fast_cells(c, st, d_imgs, B, pitch, fs, 0, n0));
                 HIPCHK(hipEventRecord(c->ev_f0[s], st));
-                PROF_LAUNCH(c, "blur",
-                            hipLaunchKernelGGL(k_blur, dim3(tb1 * B), dim3(256), 0, st, c->d_geom,
-                                               c->d_tile_base, d_imgs, fs, pitch, c->d_pyr,
-                                               c->d_blur, 0, tb1));
+                HIPCHK(launch_blur_levels(c, st, d_imgs, B, pitch, fs, 0, 1));
                 HIPCHK(hipEventRecord(c->ev_b0[s], st));
             }
         }
@@ -1338,21 +1381,14 @@ static int launch_extract_pipe(orbg_ctx *c, const uint8_t *d_imgs, int B, int pi
         if (bside) {
             HIPCHK(hipEventRecord(c->ev_pyr[s], st));
             HIPCHK(hipStreamWaitEvent(c->fstream, c->ev_pyr[s], 0));
-            hipStream_t st = c->fstream;  // PROF_LAUNCH records on `st`
-            PROF_LAUNCH(c, "blur",
-                        hipLaunchKernelGGL(k_blur, dim3((c->total_tiles - tb1) * B), dim3(256), 0,
-                                           st, c->d_geom, c->d_tile_base, d_imgs, fs, pitch,
-                                           c->d_pyr, c->d_blur, tb1, c->total_tiles - tb1));
+            hipStream_t st = c->fstream;
+            HIPCHK(launch_blur_levels(c, st, d_imgs, B, pitch, fs, side ? 1 : 0, G.L));
             HIPCHK(hipEventRecord(c->ev_b0[s], st));
         }
         HIPCHK(launch_fast_cells(c, st, d_imgs, B, pitch, fs, n0, G.ncells - n0));
         if (side) HIPCHK(hipStreamWaitEvent(st, c->ev_f0[s], 0));
         HIPCHK(hipEventRecord(c->ev_cells[s], st));
-        if (!bside)
-            PROF_LAUNCH(c, "blur",
-                        hipLaunchKernelGGL(k_blur, dim3((c->total_tiles - tb1) * B), dim3(256), 0,
-                                           st, c->d_geom, c->d_tile_base, d_imgs, fs, pitch,
-                                           c->d_pyr, c->d_blur, tb1, c->total_tiles - tb1));
+        if (!bside) HIPCHK(launch_blur_levels(c, st, d_imgs, B, pitch, fs, side ? 1 : 0, G.L));
         if (side) HIPCHK(hipStreamWaitEvent(st, c->ev_b0[s], 0));
         HIPCHK(hipEventRecord(c->ev_front[s], st));
     }
@@ -1427,7 +1463,6 @@ static int launch_extract(orbg_ctx *c, const uint8_t *d_imgs, int B, int pitch, 
     const int n0 = G.L > 1 ? G.lv[1].cell_base : G.ncells;
     // blur0: the level-0 GaussianBlur follows them there (ORBG_BLUR0)
     const bool blur0 = fast0 && c->blur0_mode;
-    const int tb1 = c->tile_base[1], tb0 = blur0 ? tb1 : 0;
     auto launch_fast = [&](hipStream_t q, int cb, int cn) {
         return launch_fast_cells(c, q, d_imgs, B, pitch, fs, cb, cn);
     };
@@ -1466,17 +1501,10 @@ static int launch_extract(orbg_ctx *c, const uint8_t *d_imgs, int B, int pitch, 
                                            c->d_cell_cnt, c->d_cell_kp,
                                            c->d_lvl_kp, c->d_lvl_cnt, c->d_err, c->oct_dims[1]));
         }
-        if (blur0)
-            PROF_LAUNCH(c, "blur",
-                        hipLaunchKernelGGL(k_blur, dim3(tb1 * B), dim3(256), 0, st, c->d_geom,
-                                           c->d_tile_base, d_imgs, fs, pitch, c->d_pyr,
-                                           c->d_blur, 0, tb1));
+        if (blur0) HIPCHK(launch_blur_levels(c, st, d_imgs, B, pitch, fs, 0, 1));
         if (oct_mode) HIPCHK(hipEventRecord(c->ev_oct, st));
     }
-    PROF_LAUNCH(c, "blur",
-                hipLaunchKernelGGL(k_blur, dim3((c->total_tiles - tb0) * B), dim3(256), 0, st,
-                                   c->d_geom, c->d_tile_base, d_imgs, fs, pitch, c->d_pyr,
-                                   c->d_blur, tb0, c->total_tiles - tb0));
+    HIPCHK(launch_blur_levels(c, st, d_imgs, B, pitch, fs, blur0 ? 1 : 0, G.L));
     if (oct_mode != 2 && G.L > 1)
         PROF_LAUNCH(c, "octree",
                     hipLaunchKernelGGL(k_octree_lds, dim3(B, G.L - 1), dim3(512),

@@ -16,7 +16,7 @@ from collections import defaultdict
 
 # rocprof kernel name -> bench.py kernel key
 NAMES = {
-    "k_resize": "resize", "k_fast_cells": "fast_cells", "k_blur": "blur",
+    "k_resize": "resize", "k_fast_cells": "fast_cells", "k_blur": "blur", "k_blur2": "blur", "k_blur2_edge": "blur",
     "k_octree_lds": "octree", "k_octree": "octree_big", "k_orient_desc": "orient_desc",
     "k_knn2_pairs": "knn2", "k_knn2_pairs_i8": "knn2", "k_init_cands_pairs": "init_cands",
     "k_init_resolve_pairs": "init_resolve",
