@@ -242,7 +242,12 @@ __global__ __launch_bounds__(256) void k_blur2(
     constexpr int PF = ORBG_BLUR2_ROWPF;
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
     // the first edge_waves waves are the row-end lanes (dispatched first, short), then tiles
+#ifdef ORBG_BLUR2_EDGE_LAST  // developer A/B: edge waves after the tile waves
+    const int wraw0 = blockIdx.x * 4 + wv, ntw = (int)gridDim.x * 4 - edge_waves;
+    const int wraw = wraw0 >= ntw ? wraw0 - ntw : wraw0 + edge_waves;
+#else
     const int wraw = blockIdx.x * 4 + wv;
+#endif
     if (wraw < edge_waves) {
 #ifdef ORBG_BLUR2_EDGE_NOP  // developer what-if: edge waves launched but idle (wrong results)
         return;
@@ -251,7 +256,7 @@ __global__ __launch_bounds__(256) void k_blur2(
                         nframes, wraw * 64 + lane);
         return;
     }
-    const int nb = gridDim.x - edge_waves / 4, bt = blockIdx.x - edge_waves / 4;
+    const int nb = gridDim.x - edge_waves / 4, bt = wraw / 4 - edge_waves / 4;
     const int wid = __builtin_amdgcn_readfirstlane(xcd_remap(bt, nb) * 4 + wv);
     if (wid >= t_count * nframes) return;  // wave-uniform
     const Blur2Weights k(g);
