@@ -41,12 +41,10 @@ __global__ void k_pyramid(PyrArgs, const uint4 *, const int4 *, const int2 *, co
                           int64_t, int, const uint8_t *, uint8_t *, int);
 // blur_kernels.hip
 int blur2_seg();
-int blur2_neg();
 int blur2_tw();
 hipError_t launch_blur2(hipStream_t st, const OrbgGeom *g, const int32_t *task_base,
-                        const int32_t *edge_base, int edges, const uint8_t *img0, int64_t img_fs,
-                        int img_pitch, const uint8_t *pyr, uint8_t *blur, int t_begin,
-                        int t_count, int l_begin, int l_end, int nframes);
+                        const uint8_t *img0, int64_t img_fs, int img_pitch, const uint8_t *pyr,
+                        uint8_t *blur, int t_begin, int t_count, int nframes);
 hipError_t launch_fast2(int p4, size_t lds, hipStream_t st, const OrbgGeom *g,
                         const OrbgCell *cells, const uint8_t *img0, int64_t img_fs,
                         int img_pitch, const uint8_t *pyr, const uint32_t *ctab,
@@ -269,7 +267,7 @@ struct orbg_ctx {
     int gw = 0, gh = 0, gbatch = 0;
     OrbgGeom geom{};
     std::vector<OrbgCell> cells;
-    std::vector<int32_t> tile_base;  // k_blur region bases, k_blur2 tiles, k_blur2_edge tasks (L + 1 each)
+    std::vector<int32_t> tile_base;  // k_blur region bases, then k_blur2 tile bases (L + 1 each)
     int total_tiles = 0;
     OctLdsDims oct_dims[2] = {};
     // device
@@ -653,8 +651,8 @@ static int plan(orbg_ctx *c, int w, int h, int batch)
     }
     int64_t pyr_off = 0, blur_off = 0;
     int key_off = 0, node_off = 0, out_off = 0, tiles = 0;
-    std::vector<int32_t> tile_base, blur2_base, edge_base;
-    int blur2_tasks = 0, edge_tasks = 0;
+    std::vector<int32_t> tile_base, blur2_base;
+    int blur2_tasks = 0;
     for (int l = 0; l < G.L; l++) {
         OrbgLevel &L = G.lv[l];
         L.w = lw[l];
@@ -766,8 +764,6 @@ static int plan(orbg_ctx *c, int w, int h, int batch)
         tiles += ((L.w + 127) / 128) * ((L.h + 32 * ORBG_BLUR_NB - 1) / (32 * ORBG_BLUR_NB));  // k_blur regions
         blur2_base.push_back(blur2_tasks);  // k_blur2 (blur_kernels.hip): 244 x SEG wave tiles
         blur2_tasks += ((L.w + blur2_tw() - 1) / blur2_tw()) * ((L.h + blur2_seg() - 1) / blur2_seg());
-        edge_base.push_back(edge_tasks);  // k_blur2_edge: row-end column groups per segment
-        edge_tasks += blur2_neg() * ((L.h + blur2_seg() - 1) / blur2_seg());
         // resize coefficient tables (cv::resize, INTER_LINEAR)
         if (l > 0) {
             const int sw = lw[l - 1], sh = lh[l - 1], dw = lw[l], dh = lh[l];
@@ -834,11 +830,8 @@ static int plan(orbg_ctx *c, int w, int h, int batch)
     }
     tile_base.push_back(tiles);
     blur2_base.push_back(blur2_tasks);
-    edge_base.push_back(edge_tasks);
-    // d_tile_base = k_blur region bases (L + 1), k_blur2 task bases (L + 1), k_blur2_edge
-    // task bases (L + 1)
+    // d_tile_base = k_blur region bases (L + 1), then k_blur2 tile bases (L + 1)
     tile_base.insert(tile_base.end(), blur2_base.begin(), blur2_base.end());
-    tile_base.insert(tile_base.end(), edge_base.begin(), edge_base.end());
     G.ncells = (int)cells.size();
     G.cell_cap = cell_cap;
     {
@@ -1303,14 +1296,12 @@ static hipError_t launch_blur_levels(orbg_ctx *c, hipStream_t st, const uint8_t 
                                      int pitch, int64_t fs, int l0, int l1)
 {
     const int L = c->geom.L;
-    if (c->blur_v2 && c->geom.lv[L - 1].w >= 16) {  // k_blur2 loads 16-byte row windows
-        const int32_t *b2 = c->tile_base.data() + L + 1, *eb = b2 + L + 1;
+    if (c->blur_v2 && c->geom.lv[L - 1].w >= 8) {  // k_blur2's row-end permutes need W >= 8
+        const int32_t *b2 = c->tile_base.data() + L + 1;
         hipError_t e = hipSuccess;
         PROF_LAUNCH(c, "blur",
-                    e = launch_blur2(st, c->d_geom, c->d_tile_base + L + 1,
-                                     c->d_tile_base + 2 * (L + 1), eb[l1] - eb[l0], d_imgs, fs,
-                                     pitch, c->d_pyr, c->d_blur, b2[l0], b2[l1] - b2[l0], l0, l1,
-                                     B));
+                    e = launch_blur2(st, c->d_geom, c->d_tile_base + L + 1, d_imgs, fs, pitch,
+                                     c->d_pyr, c->d_blur, b2[l0], b2[l1] - b2[l0], B));
         return e;
     }
     const int t0 = c->tile_base[l0], t1 = c->tile_base[l1];
