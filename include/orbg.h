@@ -129,6 +129,12 @@ int orbg_extract(orbg_ctx *ctx, const uint8_t *img, int w, int h, size_t step,
 /* mvImagePyramid[level] of frame `frame` of the last extraction (host copy). */
 int orbg_get_level(orbg_ctx *ctx, int frame, int level, uint8_t *dst, size_t dst_step, int *lw,
                    int *lh);
+/* The GaussianBlur(7x7, sigma 2, REFLECT_101) of pyramid level `level` of frame `frame` of the
+ * last extraction: the image computeOrbDescriptor samples (ORBextractor.cc:1375-1377, a local
+ * cv::Mat there, no public member).  Parity / debugging accessor; same contract as
+ * orbg_get_level. */
+int orbg_get_blurred_level(orbg_ctx *ctx, int frame, int level, uint8_t *dst, size_t dst_step,
+                           int *lw, int *lh);
 
 /* ---------------- batched, device-resident ---------------- */
 /* d_imgs: device pointer, nframes images of w x h, row pitch `step`, frame pitch

@@ -131,6 +131,7 @@ def lib():
         "orbg_get_pattern": (i32, [vp]),
         "orbg_extract": (i32, [vp, vp, i32, i32, sz, vp, vp, i32, P(i32)]),
         "orbg_get_level": (i32, [vp, i32, i32, vp, sz, P(i32), P(i32)]),
+        "orbg_get_blurred_level": (i32, [vp, i32, i32, vp, sz, P(i32), P(i32)]),
         "orbg_extract_batch_device": (i32, [vp, vp, i32, i32, i32, sz, sz]),
         "orbg_batch_outputs": (i32, [vp, P(vp), P(vp), P(vp), P(C.c_int32)]),
         "orbg_download_frame": (i32, [vp, i32, vp, vp, i32, P(i32)]),

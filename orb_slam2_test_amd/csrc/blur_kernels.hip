@@ -168,15 +168,27 @@ __global__ __launch_bounds__(256) void k_blur2(
     }
     // bounds-checked loads over the level of this frame: offsets past its last byte (the
     // caller's image may end there) read 0, offsets before its first byte wrap and read 0
+    const int nrec = (H - 1) * pitch + W;
     const __amdgpu_buffer_rsrc_t rsrc = __builtin_amdgcn_make_buffer_rsrc(
-        (void *)src, (short)0, (H - 1) * pitch + W, 0x00020000);
+        (void *)src, (short)0, nrec, 0x00020000);
     const int sh0 = (int)((uintptr_t)src & 3);
     uint32_t ring[PF], rsh[PF];
     auto issue = [&](int i) {
         const int y = b2_reflect101(min(y0 - 3 + i, H + 2), H);
         const int rowoff = y * pitch;
         const int sh = __builtin_amdgcn_readfirstlane((rowoff + sh0) & 3);
-        ring[i % PF] = __builtin_amdgcn_raw_buffer_load_b32(rsrc, rowoff - sh + gx - 4, 0, 0);
+        const int o = rowoff - sh + gx - 4;
+        uint32_t v;
+        if (o + 4 > nrec && o < nrec) {
+            // the dword holding the level's last byte: a dword load straddling the range end
+            // reads 0 as a whole, so this one lane reads its in-range bytes one by one
+            v = 0;
+            for (int b = 0; b < 4 && o + b < nrec; b++)
+                v |= (uint32_t)__builtin_amdgcn_raw_buffer_load_b8(rsrc, o + b, 0, 0) << (8 * b);
+        } else {
+            v = __builtin_amdgcn_raw_buffer_load_b32(rsrc, o, 0, 0);
+        }
+        ring[i % PF] = v;
         rsh[i % PF] = (uint32_t)sh;
     };
 #pragma unroll

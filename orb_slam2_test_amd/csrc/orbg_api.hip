@@ -1679,6 +1679,26 @@ extern "C" int orbg_get_level(orbg_ctx *c, int frame, int level, uint8_t *dst, s
     return ORBG_OK;
 }
 
+// the GaussianBlur of a pyramid level of the last batch (ORBextractor.cc:1375-1377: the
+// image computeOrbDescriptor samples); a parity / debugging accessor, no reference member
+extern "C" int orbg_get_blurred_level(orbg_ctx *c, int frame, int level, uint8_t *dst,
+                                      size_t dst_step, int *lw, int *lh)
+{
+    if (!c || !c->gw) return set_err(ORBG_EINVAL, "nothing extracted yet");
+    if (level < 0 || level >= c->geom.L || frame < 0 || frame >= c->last_n)
+        return set_err(ORBG_EINVAL, "bad level/frame");
+    const OrbgLevel &L = c->geom.lv[level];
+    if (lw) *lw = L.w;
+    if (lh) *lh = L.h;
+    if (!dst) return ORBG_OK;
+    if (dst_step < (size_t)L.w) return set_err(ORBG_EINVAL, "dst_step too small");
+    int rc = sync_all(c);
+    if (rc) return rc;
+    HIPCHK(hipMemcpy2D(dst, dst_step, c->d_blur + frame * c->geom.blur_frame + L.blur_off,
+                       L.pitch, L.w, L.h, hipMemcpyDeviceToHost));
+    return ORBG_OK;
+}
+
 extern "C" int orbg_sync(orbg_ctx *c)
 {
     if (!c) return set_err(ORBG_EINVAL, "ctx is NULL");

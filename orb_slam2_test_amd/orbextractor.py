@@ -109,12 +109,20 @@ class ORBextractor:
         return self._pyr_cache
 
     def get_level(self, frame, level):
+        return self._level("orbg_get_level", frame, level)
+
+    def get_blurred_level(self, frame, level):
+        """The GaussianBlur of pyramid level `level` (the image rBRIEF samples,
+        ORBextractor.cc:1375-1377); a parity accessor (orbg_get_blurred_level)."""
+        return self._level("orbg_get_blurred_level", frame, level)
+
+    def _level(self, fn, frame, level):
         lw, lh = C.c_int(), C.c_int()
-        L.check(L.lib().orbg_get_level(self.ctx.handle, frame, level, None, 0, C.byref(lw),
-                                       C.byref(lh)), "orbg_get_level")
+        f = getattr(L.lib(), fn)
+        L.check(f(self.ctx.handle, frame, level, None, 0, C.byref(lw), C.byref(lh)), fn)
         out = np.zeros((lh.value, lw.value), np.uint8)
-        L.check(L.lib().orbg_get_level(self.ctx.handle, frame, level, L.ptr(out), lw.value,
-                                       C.byref(lw), C.byref(lh)), "orbg_get_level")
+        L.check(f(self.ctx.handle, frame, level, L.ptr(out), lw.value, C.byref(lw),
+                  C.byref(lh)), fn)
         return out
 
     # --- batched, device-resident ---
