@@ -211,6 +211,9 @@ __device__ __forceinline__ void knn2_block(const uint8_t *__restrict__ q, int nq
 // q, nibble j -> bit 4j + q of that dword.
 typedef int knn_v8i __attribute__((ext_vector_type(8)));
 typedef float knn_v16f __attribute__((ext_vector_type(16)));
+#ifndef ORBG_KNN_MED3
+#define ORBG_KNN_MED3 1
+#endif
 #define KNN4_ROWB 144  // expanded train row: 128 B + 16 B pad (16 lanes' b128 reads: 64 banks)
 #define KNN4_SCALE_A (127 + 12)  // E8M0 2^12
 #define KNN4_SCALE_B 127         // E8M0 1.0
@@ -290,8 +293,17 @@ __device__ __forceinline__ void knn2_block_fp4(const uint8_t *__restrict__ q, in
                 // element 0 under this clang)
                 const float kf = acc[u][r];
                 const uint32_t key = __float_as_uint(kf);
+#if ORBG_KNN_MED3
+                // the min reads the MFMA result first (the compiler places the MFMA -> VALU
+                // wait states there); v_med3_u32 of (k1, k2, key) with k1 <= k2 is the new
+                // second key -- one op where the compiler's min/max form takes two
+                const uint32_t k1o = k1[u];
+                k1[u] = min(k1o, key);
+                asm volatile("v_med3_u32 %0, %1, %2, %3" : "=v"(k2[u]) : "v"(k1o), "v"(k2[u]), "v"(key));
+#else
                 k2[u] = min(k2[u], max(k1[u], key));
                 k1[u] = min(k1[u], key);
+#endif
             }
         }
     };
