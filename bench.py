@@ -41,7 +41,7 @@ METRIC_EXTRACT = "frames/sec ORBextractor only, 1241×376 2000feat 8lvl (configs
 
 
 PMC_MONO = "r02f_pmc_kernels.json"      # tools/r02_profile.sh (bench.py), copied from its run dir
-PMC_STEREO = "r02_stereo_pmc_kernels.json"  # tools/r02_profile.sh r02s --stereo
+PMC_STEREO = "r02f_stereo_pmc_kernels.json"  # tools/r02_profile.sh <tag> --stereo
 
 
 def kernel_algo_bytes(name, B, npairs, ncand, nkp, launches_per_step):

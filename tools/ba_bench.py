@@ -24,7 +24,7 @@ sys.path.insert(0, ROOT)
 HBM_PEAK_GBS = 8000.0
 EDGE_ALGO_BYTES = 108  # per-edge algorithmic bytes
 F64_MFMA_PEAK_TFLOPS = 78.6  # MI355X FP64 matrix, AMD spec (the guide lists no FP64 row)
-PMC_BA = "r02_ba_pmc_kernels.json"  # tools/pmc_kernels.py over tools/r02_ba_profile.sh
+PMC_BA = "r02f_ba_pmc_kernels.json"  # tools/pmc_kernels.py over tools/r02_ba_profile.sh
 
 
 def main():
