@@ -229,7 +229,7 @@ struct orbg_ctx {
     // pipelined front, level 0 (FAST cells + GaussianBlur need only the input images) on
     // `fstream` beside the pyramid (ORBG_SIDE: 0 off, 1 normal priority, 2 high)
     hipStream_t fstream = nullptr;
-    int side_mode = 2;
+    int side_mode = 1;
     hipEvent_t ev_f0[2] = {nullptr, nullptr}, ev_b0[2] = {nullptr, nullptr},
                ev_pfork[2] = {nullptr, nullptr}, ev_pyr[2] = {nullptr, nullptr};
     bool blur_side = false;  // ORBG_BLUR_SIDE
@@ -1153,7 +1153,7 @@ extern "C" int orbg_create(int device, const orbg_params *p, orbg_ctx **out)
     }
     {
         const char *e = getenv("ORBG_SIDE");
-        c->side_mode = e ? atoi(e) : 2;
+        c->side_mode = e ? atoi(e) : 1;  // normal priority: 1.596 vs 1.605 ms (high) after k_blur2
         if (c->side_mode && hipStreamCreateWithPriority(&c->fstream, hipStreamNonBlocking,
                                                         c->side_mode >= 2 ? prio_hi : 0) != hipSuccess) {
             c->fstream = nullptr;
