@@ -134,21 +134,34 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(ORBG_OD_WPE
     }
     const uint32_t okmask = (uint32_t)__ballot(my_ok);
     // lane-constant (row, 16-byte chunk) of the patch / neighbourhood words this lane loads
-    int pr[2], pc[2];
+    // (the loads of lanes past the last word re-read the last word: unconditional loads keep
+    // the pipelined loops below free of exec branches, so their vmcnt waits stay partial)
+    int pr[2], pc[2], par[2], pac[2];
 #pragma unroll
     for (int k = 0; k < 2; k++) {
-        const int w = lane + 64 * k;
+        const int w = min(lane + 64 * k, OD_SPAN * 3 - 1);
         pr[k] = w / 3;
         pc[k] = w - pr[k] * 3;
+        const int wa = min(lane + 64 * k, OD_TABW - 1);
+        par[k] = wa / 3;
+        pac[k] = wa - par[k] * 3;
     }
 
+    if (!okmask) return;  // wave-uniform: no keypoint in this wave's slots
+    // Empty slots borrow the first filled slot's key (their results are dropped), so every
+    // slot's loads below are unconditional and the unrolled slot loops have no branches
+    // around them: each vmcnt wait then covers exactly the current slot's loads.
+    const int jfirst = __builtin_ctz(okmask);
+    const uint32_t kl_l = my_ok ? kl : (uint32_t)__builtin_amdgcn_readlane((int)kl, jfirst);
+    const int lev_l = my_ok ? my_lev : __builtin_amdgcn_readlane(my_lev, jfirst);
+
     // ---- A: IC_Angle moments (ORBextractor.cc:83-111), slot j's sums kept by lane j ----
-    int M01 = 0, M10 = 0;
-#pragma unroll 1
-    for (int j = 0; j < OD_KPW; j++) {
-        if (!((okmask >> j) & 1u)) continue;  // wave-uniform
-        const int lev = __builtin_amdgcn_readlane(my_lev, j);
-        const uint32_t key = (uint32_t)__builtin_amdgcn_readlane((int)kl, j);
+    // Software-pipelined over the slots: the patch loads of slot j + 1 are in flight while
+    // slot j's moments are summed (the kernel is bound by the latency of these scattered row
+    // loads, not by issue); two register buffers alternate.
+    auto load_patch = [&](int j, uint4 (&wd)[2], int (&sh)[2]) {
+        const int lev = __builtin_amdgcn_readlane(lev_l, j);
+        const uint32_t key = (uint32_t)__builtin_amdgcn_readlane((int)kl_l, j);
         const int x = orbg_px(key) + ORBG_MIN_BORDER, y = orbg_py(key) + ORBG_MIN_BORDER;
         const uint8_t *im;
         int pitch;
@@ -162,45 +175,51 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(ORBG_OD_WPE
         const uint8_t *ctr = im + (int64_t)y * pitch + x;
         // 16 bytes per lane from each row's 4-byte-aligned start (the level-0 pitch may be
         // odd, so the alignment is per row)
-        uint4 wd[2];
-        int sh[2];
 #pragma unroll
         for (int k = 0; k < 2; k++) {
-            wd[k] = make_uint4(0, 0, 0, 0);
-            sh[k] = 0;
-            if (lane + 64 * k < OD_TABW) {
-                // pointer arithmetic (not an integer round trip): global_, not flat_, loads
-                const uint8_t *pa = ctr + (int64_t)(pr[k] - ORBG_HALF_PATCH) * pitch - ORBG_HALF_PATCH;
-                sh[k] = (int)((uintptr_t)pa & 3);
-                wd[k] = *(const uint4 *)(pa - sh[k] + 16 * pc[k]);
-            }
+            // pointer arithmetic (not an integer round trip): global_, not flat_, loads
+            const uint8_t *pa = ctr + (int64_t)(par[k] - ORBG_HALF_PATCH) * pitch - ORBG_HALF_PATCH;
+            sh[k] = (int)((uintptr_t)pa & 3);
+            wd[k] = *(const uint4 *)(pa - sh[k] + 16 * pac[k]);
         }
-        int m01 = 0, m10 = 0;
+    };
+    int M01 = 0, M10 = 0;
+    {
+        uint4 wbuf[2][2];
+        int sbuf[2][2];
+        load_patch(0, wbuf[0], sbuf[0]);
 #pragma unroll
-        for (int k = 0; k < 2; k++) {
-            const int w = lane + 64 * k;
-            if (w < OD_TABW) {
-                const int v = pr[k] - ORBG_HALF_PATCH;
-                const uint4 tw = tab[(sh[k] * OD_TABW + w) * 2];
-                const uint4 to = tab[(sh[k] * OD_TABW + w) * 2 + 1];
-                uint32_t su = 0, sv = 0;
-                su = __builtin_amdgcn_udot4(wd[k].x, tw.x, su, false);
-                su = __builtin_amdgcn_udot4(wd[k].y, tw.y, su, false);
-                su = __builtin_amdgcn_udot4(wd[k].z, tw.z, su, false);
-                su = __builtin_amdgcn_udot4(wd[k].w, tw.w, su, false);
-                sv = __builtin_amdgcn_udot4(wd[k].x, to.x, sv, false);
-                sv = __builtin_amdgcn_udot4(wd[k].y, to.y, sv, false);
-                sv = __builtin_amdgcn_udot4(wd[k].z, to.z, sv, false);
-                sv = __builtin_amdgcn_udot4(wd[k].w, to.w, sv, false);
-                m10 += (int)su - ORBG_HALF_PATCH * (int)sv;
-                m01 += v * (int)sv;
+        for (int j = 0; j < OD_KPW; j++) {
+            if (j + 1 < OD_KPW) load_patch(j + 1, wbuf[(j + 1) & 1], sbuf[(j + 1) & 1]);
+            const uint4(&wd)[2] = wbuf[j & 1];
+            const int(&sh)[2] = sbuf[j & 1];
+            int m01 = 0, m10 = 0;
+#pragma unroll
+            for (int k = 0; k < 2; k++) {
+                const int w = lane + 64 * k;
+                if (w < OD_TABW) {
+                    const int v = par[k] - ORBG_HALF_PATCH;
+                    const uint4 tw = tab[(sh[k] * OD_TABW + w) * 2];
+                    const uint4 to = tab[(sh[k] * OD_TABW + w) * 2 + 1];
+                    uint32_t su = 0, sv = 0;
+                    su = __builtin_amdgcn_udot4(wd[k].x, tw.x, su, false);
+                    su = __builtin_amdgcn_udot4(wd[k].y, tw.y, su, false);
+                    su = __builtin_amdgcn_udot4(wd[k].z, tw.z, su, false);
+                    su = __builtin_amdgcn_udot4(wd[k].w, tw.w, su, false);
+                    sv = __builtin_amdgcn_udot4(wd[k].x, to.x, sv, false);
+                    sv = __builtin_amdgcn_udot4(wd[k].y, to.y, sv, false);
+                    sv = __builtin_amdgcn_udot4(wd[k].z, to.z, sv, false);
+                    sv = __builtin_amdgcn_udot4(wd[k].w, to.w, sv, false);
+                    m10 += (int)su - ORBG_HALF_PATCH * (int)sv;
+                    m01 += v * (int)sv;
+                }
             }
-        }
-        m01 = wave_sum(m01);
-        m10 = wave_sum(m10);
-        if (lane == j) {
-            M01 = m01;
-            M10 = m10;
+            m01 = wave_sum(m01);
+            m10 = wave_sum(m10);
+            if (lane == j) {
+                M01 = m01;
+                M10 = m10;
+            }
         }
     }
 
@@ -242,63 +261,73 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(ORBG_OD_WPE
     for (int t = 0; t < 4; t++) pat[t] = ((const int *)od_pattern_i8)[lane + 64 * t];
     const bool bfma = g->brief_fma != 0;
     uint8_t *bp = (uint8_t *)bpatch[wv];
-#pragma unroll 1
-    for (int j = 0; j < OD_KPW; j++) {
-        if (!((okmask >> j) & 1u)) continue;  // wave-uniform
-        const int lev = __builtin_amdgcn_readlane(my_lev, j);
-        const uint32_t key = (uint32_t)__builtin_amdgcn_readlane((int)kl, j);
+    // pipelined like phase A: slot j + 1's neighbourhood loads are issued right after slot j
+    // is staged, and land while slot j's samples are read
+    struct Nbhd {
+        uint4 v0, v1;
+        int sh;
+    };
+    auto load_nbhd = [&](int j) -> Nbhd {
+        const int lev = __builtin_amdgcn_readlane(lev_l, j);
+        const uint32_t key = (uint32_t)__builtin_amdgcn_readlane((int)kl_l, j);
         const int x = orbg_px(key) + ORBG_MIN_BORDER, y = orbg_py(key) + ORBG_MIN_BORDER;
         const OrbgLevel &lv = g->lv[lev];
         const int bpitch = lv.pitch;
         const uint8_t *bl0 = blur + f * g->blur_frame + lv.blur_off +
                              (int64_t)(y - OD_R) * bpitch + (x - OD_R);
-        const int bsh = (int)((uintptr_t)bl0 & 3);
-        const uint8_t *bw = bl0 - bsh;
-        uint4 bv[2];
+        Nbhd n;
+        n.sh = (int)((uintptr_t)bl0 & 3);
+        const uint8_t *bw = bl0 - n.sh;
+        n.v0 = *(const uint4 *)(bw + (int64_t)pr[0] * bpitch + 16 * pc[0]);
+        n.v1 = *(const uint4 *)(bw + (int64_t)pr[1] * bpitch + 16 * pc[1]);
+        return n;
+    };
+    Nbhd nbh[2];
+    nbh[0] = load_nbhd(0);
 #pragma unroll
-        for (int k = 0; k < 2; k++) {
-            bv[k] = make_uint4(0, 0, 0, 0);
-            if (lane + 64 * k < OD_SPAN * 3)
-                bv[k] = *(const uint4 *)(bw + (int64_t)pr[k] * bpitch + 16 * pc[k]);
-        }
+    for (int j = 0; j < OD_KPW; j++) {
         wave_sync_lds();  // the previous slot's sample reads are done
-#pragma unroll
-        for (int k = 0; k < 2; k++)
-            if (lane + 64 * k < OD_SPAN * 3) *(uint4 *)(bp + pr[k] * OD_ROWB + 16 * pc[k]) = bv[k];
+        *(uint4 *)(bp + pr[0] * OD_ROWB + 16 * pc[0]) = nbh[j & 1].v0;
+        *(uint4 *)(bp + pr[1] * OD_ROWB + 16 * pc[1]) = nbh[j & 1].v1;  // clamped lanes: same word twice
         wave_sync_lds();
+        const int cur_bsh = nbh[j & 1].sh;
+        if (j + 1 < OD_KPW) nbh[(j + 1) & 1] = load_nbhd(j + 1);
         const float a = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, a_l), j));
         const float b = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, b_l), j));
-        const uint8_t *bl = bp + OD_R * OD_ROWB + bsh + OD_R;  // centre
+        const uint8_t *bl = bp + OD_R * OD_ROWB + cur_bsh + OD_R;  // centre
         // opaque per slot: keeps the offset decode inside the loop (hoisted, the 16 floats
         // stay live through phase C and push the kernel past 64 VGPRs)
         int pt[4] = {pat[0], pat[1], pat[2], pat[3]};
         asm volatile("" : "+v"(pt[0]), "+v"(pt[1]), "+v"(pt[2]), "+v"(pt[3]));
-        uint32_t word = 0;
+        // all 8 sample offsets first (branch-free in bfma), then the 8 LDS reads in flight
+        // together, then the 4 ballots
+        int off[8];
 #pragma unroll
         for (int t = 0; t < 4; t++) {
-            int val[2];
 #pragma unroll
             for (int s = 0; s < 2; s++) {
                 const float px = (float)(int8_t)(pt[t] >> (16 * s));
                 const float py = (float)(int8_t)(pt[t] >> (16 * s + 8));
-                float ry, rx;
-                if (bfma) {
-                    ry = fmaf(px, b, py * a);
-                    rx = fmaf(px, a, -(py * b));
-                } else {
-                    const float t0 = px * b, t1 = py * a, t2 = px * a, t3 = py * b;
-                    ry = t0 + t1;
-                    rx = t2 - t3;
-                }
-                val[s] = bl[cv_round(ry) * OD_ROWB + cv_round(rx)];
+                const float t0 = px * b, t1 = py * a, t2 = px * a, t3 = py * b;
+                const float ry = bfma ? fmaf(px, b, t1) : t0 + t1;
+                const float rx = bfma ? fmaf(px, a, -t3) : t2 - t3;
+                off[2 * t + s] = cv_round(ry) * OD_ROWB + cv_round(rx);
             }
+        }
+        int val[8];
+#pragma unroll
+        for (int i = 0; i < 8; i++) val[i] = bl[off[i]];
+        uint32_t word = 0;
+#pragma unroll
+        for (int t = 0; t < 4; t++) {
             // bit L of ballot t = test 64t + L = descriptor bit 64t + L; dword d of the
             // descriptor is half (d & 1) of ballot d >> 1
-            const unsigned long long m = __ballot(val[0] < val[1]);
+            const unsigned long long m = __ballot(val[2 * t] < val[2 * t + 1]);
             if ((lane >> 1) == t) word = (uint32_t)(m >> (32 * (lane & 1)));
         }
         const int i = __builtin_amdgcn_readlane(my_i, j);
-        if (lane < 8) ((uint32_t *)(desc + ((int64_t)f * g->frame_cap + i) * 32))[lane] = word;
+        if (((okmask >> j) & 1u) && lane < 8)
+            ((uint32_t *)(desc + ((int64_t)f * g->frame_cap + i) * 32))[lane] = word;
     }
 }
 
