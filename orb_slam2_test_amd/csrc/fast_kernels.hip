@@ -239,8 +239,21 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(FC2_WPE, 8)
                 (top ? nboth : nlist) += __popcll(m);
             };
             const bool bothA = ab && ad, bothB = bb && bd;
-            append((ab | ad) && !bothA, false, ab ? 0 : 1);  // pixels 0-1
-            append((bb | bd) && !bothB, false, bb ? 2 : 3);  // pixels 2-3
+            // the common entries of pixels 0-1 and 2-3 in one append: a lane's entries follow
+            // those of every lower lane, its pair-0-1 entry before its pair-2-3 entry; a lane
+            // without an entry writes the spare slot past the list (lcap), so both stores are
+            // unconditional (no exec-mask branches)
+            {
+                const bool fA = (ab | ad) && !bothA, fB = (bb | bd) && !bothB;
+                const unsigned long long mA = __ballot(fA), mB = __ballot(fB);
+                const int below =
+                    __builtin_amdgcn_mbcnt_hi((uint32_t)(mA >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)mA, 0)) +
+                    __builtin_amdgcn_mbcnt_hi((uint32_t)(mB >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)mB, 0));
+                const int pa = nlist + below;
+                list[fA ? pa : lcap] = (uint16_t)(e | (ab ? 0 : 1));
+                list[fB ? pa + (int)fA : lcap] = (uint16_t)(e | (bb ? 2 : 3));
+                nlist += __popcll(mA) + __popcll(mB);
+            }
             if (__ballot(bothA || bothB)) {
                 append(bothA, true, 0);
                 append(bothB, true, 2);

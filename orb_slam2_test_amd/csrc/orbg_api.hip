@@ -916,7 +916,7 @@ static int plan(orbg_ctx *c, int w, int h, int batch)
                 G.fc2_sc_off = 2 * hmax * P2;
                 G.fc2_list_off = G.fc2_sc_off + (std::max(hmax - 6, 0) + 2) * P2;
                 G.fc2_list_cap = 2 * max_units;
-                G.fc2_wave_bytes = (G.fc2_list_off + 2 * G.fc2_list_cap + 15) & ~15;
+                G.fc2_wave_bytes = (G.fc2_list_off + 2 * G.fc2_list_cap + 2 + 15) & ~15;  // + k_fast2's spare entry
                 if (4 * G.fc2_wave_bytes > 160 * 1024) G.fc2_p4 = 0;
             }
         }
