@@ -172,6 +172,12 @@ __global__ __launch_bounds__(256) void k_blur2(
     const __amdgpu_buffer_rsrc_t rsrc = __builtin_amdgcn_make_buffer_rsrc(
         (void *)src, (short)0, nrec, 0x00020000);
     const int sh0 = (int)((uintptr_t)src & 3);
+    bool strad_wave;
+    {
+        const int ro = (H - 1) * pitch;
+        const int ol = ro - ((ro + sh0) & 3) + gx - 4;
+        strad_wave = __ballot(ol + 4 > nrec && ol < nrec) != 0;
+    }
     uint32_t ring[PF], rsh[PF];
     auto issue = [&](int i) {
         const int y = b2_reflect101(min(y0 - 3 + i, H + 2), H);
@@ -179,14 +185,19 @@ __global__ __launch_bounds__(256) void k_blur2(
         const int sh = __builtin_amdgcn_readfirstlane((rowoff + sh0) & 3);
         const int o = rowoff - sh + gx - 4;
         uint32_t v;
-        if (o + 4 > nrec && o < nrec) {
-            // the dword holding the level's last byte: a dword load straddling the range end
-            // reads 0 as a whole, so this one lane reads its in-range bytes one by one
-            v = 0;
-            for (int b = 0; b < 4 && o + b < nrec; b++)
-                v |= (uint32_t)__builtin_amdgcn_raw_buffer_load_b8(rsrc, o + b, 0, 0) << (8 * b);
-        } else {
-            v = __builtin_amdgcn_raw_buffer_load_b32(rsrc, o, 0, 0);
+        // only the level's last row can hold that dword (a tile row reads < 256 + 8 bytes,
+        // less than pitch + W), and only in waves where some lane's last-row dword does
+        // (wave-uniform test): every other row is one load with no exec-mask branches
+        v = __builtin_amdgcn_raw_buffer_load_b32(rsrc, o, 0, 0);
+        if (strad_wave && y == H - 1) {  // wave-uniform
+            if (o + 4 > nrec && o < nrec) {
+                // the dword holding the level's last byte: a dword load straddling the range
+                // end reads 0 as a whole, so this one lane reads its in-range bytes one by one
+                uint32_t vb = 0;
+                for (int b = 0; b < 4 && o + b < nrec; b++)
+                    vb |= (uint32_t)__builtin_amdgcn_raw_buffer_load_b8(rsrc, o + b, 0, 0) << (8 * b);
+                v = vb;
+            }
         }
         ring[i % PF] = v;
         rsh[i % PF] = (uint32_t)sh;
