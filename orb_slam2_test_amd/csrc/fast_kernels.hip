@@ -274,13 +274,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(FC2_WPE, 8)
     // ---- one side of one pixel pair per lane task: tasks [0, nlist) are the bottom entries,
     // then two per top entry (bright, dark) ----
     for (int j = lane; j < nlist + 2 * nboth; j += 64) {
-        int e;
-        if (j < nlist) {
-            e = list[j];
-        } else {
-            const int t = j - nlist;
-            e = list[lcap - 1 - (t >> 1)] | (t & 1);
-        }
+        // branch-free (selects, one LDS read): no exec-mask juggling per task
+        const int t = j - nlist;
+        const bool top = t >= 0;
+        const int e = list[top ? lcap - 1 - (t >> 1) : j] | (top ? (t & 1) : 0);
         const int ry = e >> 8, gg = (e >> 2) & 63, half = (e >> 1) & 1;
         const uint32_t flip = (e & 1) ? 0xFFFFFFFFu : 0u;  // dark: complemented bytes
         const uint32_t *p = (const uint32_t *)(tA + half * P + ry * RS + 4 * gg);
