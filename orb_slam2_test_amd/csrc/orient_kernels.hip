@@ -78,6 +78,10 @@ struct OrbgKeypointDev {
 #define ORBG_OD_WPE 8  // min waves per SIMD (VGPR budget)
 #endif
 #define OD_TABW ORBG_OD_TABW    // IC_Angle lanes: 31 patch rows x 3 16-byte chunks
+#ifndef ORBG_OD_PFD
+#define ORBG_OD_PFD 1  // slots whose loads are in flight ahead of the one being summed / sampled
+#endif
+#define OD_PFD ORBG_OD_PFD
 static_assert(OD_KPW >= 1 && OD_KPW <= 32, "one slot per lane, okmask is 32 bits");
 
 // IC_Angle byte tables (host-built, orbg_api.hip make_od_tab): entry (sh, w) for the patch
@@ -185,14 +189,16 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(ORBG_OD_WPE
     };
     int M01 = 0, M10 = 0;
     {
-        uint4 wbuf[2][2];
-        int sbuf[2][2];
-        load_patch(0, wbuf[0], sbuf[0]);
+        uint4 wbuf[OD_PFD + 1][2];
+        int sbuf[OD_PFD + 1][2];
+#pragma unroll
+        for (int j = 0; j < OD_PFD; j++) load_patch(j, wbuf[j], sbuf[j]);
 #pragma unroll
         for (int j = 0; j < OD_KPW; j++) {
-            if (j + 1 < OD_KPW) load_patch(j + 1, wbuf[(j + 1) & 1], sbuf[(j + 1) & 1]);
-            const uint4(&wd)[2] = wbuf[j & 1];
-            const int(&sh)[2] = sbuf[j & 1];
+            if (j + OD_PFD < OD_KPW)
+                load_patch(j + OD_PFD, wbuf[(j + OD_PFD) % (OD_PFD + 1)], sbuf[(j + OD_PFD) % (OD_PFD + 1)]);
+            const uint4(&wd)[2] = wbuf[j % (OD_PFD + 1)];
+            const int(&sh)[2] = sbuf[j % (OD_PFD + 1)];
             int m01 = 0, m10 = 0;
 #pragma unroll
             for (int k = 0; k < 2; k++) {
@@ -282,16 +288,17 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(ORBG_OD_WPE
         n.v1 = *(const uint4 *)(bw + (int64_t)pr[1] * bpitch + 16 * pc[1]);
         return n;
     };
-    Nbhd nbh[2];
-    nbh[0] = load_nbhd(0);
+    Nbhd nbh[OD_PFD + 1];
+#pragma unroll
+    for (int j = 0; j < OD_PFD; j++) nbh[j] = load_nbhd(j);
 #pragma unroll
     for (int j = 0; j < OD_KPW; j++) {
         wave_sync_lds();  // the previous slot's sample reads are done
-        *(uint4 *)(bp + pr[0] * OD_ROWB + 16 * pc[0]) = nbh[j & 1].v0;
-        *(uint4 *)(bp + pr[1] * OD_ROWB + 16 * pc[1]) = nbh[j & 1].v1;  // clamped lanes: same word twice
+        *(uint4 *)(bp + pr[0] * OD_ROWB + 16 * pc[0]) = nbh[j % (OD_PFD + 1)].v0;
+        *(uint4 *)(bp + pr[1] * OD_ROWB + 16 * pc[1]) = nbh[j % (OD_PFD + 1)].v1;  // clamped lanes: same word twice
         wave_sync_lds();
-        const int cur_bsh = nbh[j & 1].sh;
-        if (j + 1 < OD_KPW) nbh[(j + 1) & 1] = load_nbhd(j + 1);
+        const int cur_bsh = nbh[j % (OD_PFD + 1)].sh;
+        if (j + OD_PFD < OD_KPW) nbh[(j + OD_PFD) % (OD_PFD + 1)] = load_nbhd(j + OD_PFD);
         const float a = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, a_l), j));
         const float b = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, b_l), j));
         const uint8_t *bl = bp + OD_R * OD_ROWB + cur_bsh + OD_R;  // centre
