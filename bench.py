@@ -185,7 +185,10 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--batch", type=int, default=256, help="frames per GPU per step")
+    ap.add_argument("--batch", type=int, default=None,
+                    help="frames (stereo: L/R pairs) per GPU per step; default 512 (stereo 256 "
+                         "pairs = 512 images): +3.3%% frames/s over 256, the fixed cost of a "
+                         "step's dependent launches spread over twice the frames")
     ap.add_argument("--cpu-threads", type=int, default=int(os.environ.get("OMP_NUM_THREADS", "16")))
     ap.add_argument("--cpu-frames", type=int, default=0, help="0: 256 x threads (~10-20 s)")
     ap.add_argument("--no-cpu", action="store_true")
@@ -210,7 +213,7 @@ def main():
     if world > 1:
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
 
-    B = args.batch
+    B = args.batch or (256 if args.stereo else 512)
     if args.stereo:
         lefts, rights, _ = synthetic.stereo_sequence(B, H, W, seed=synthetic.DEFAULT_SEED + 1000 * rank)
         frames = np.empty((2 * B, H, W), np.uint8)
@@ -378,6 +381,7 @@ def main():
             "unit": "stereo frames/s" if args.stereo else "frames/s", "n_gpus": world,
             "steps": args.steps, "warmup": args.warmup,
             "ms_per_step": round(elapsed / args.steps * 1e3, 4), "higher_is_better": True,
+            "ms_per_256_frames": round(elapsed / args.steps * 1e3 * 256 / B, 4),
             "scaling": "weak", "vs_baseline": None, "dtype": "u8", "data": "synthetic",
             "config": {
                 "workload": workload,

@@ -71,11 +71,12 @@ __device__ __forceinline__ h2 as_h2(v2s v) { return __builtin_bit_cast(h2, v); }
 __device__ __forceinline__ v2s as_v2s(h2 v) { return __builtin_bit_cast(v2s, v); }
 
 // circle (dx, dy) of makeOffsets(16); row index = 3 + dy, byte offset = 4 + dx (+ pixel i)
-template <int I>
+// C: byte offset of pixel 0 in the 12-byte row window (4: k_fast_cells' tiles, 3: k_fast2's)
+template <int I, int C = 4>
 __device__ __forceinline__ v2s fast_score_pair(const Rows7 &R)
 {
-#define GB(row, dx) as_h2(gather2<4 + (dx) + I>(R.w[row][0], R.w[row][1], R.w[row][2]))
-    const v2s v = gather2<4 + I>(R.w[3][0], R.w[3][1], R.w[3][2]);
+#define GB(row, dx) as_h2(gather2<C + (dx) + I>(R.w[row][0], R.w[row][1], R.w[row][2]))
+    const v2s v = gather2<C + I>(R.w[3][0], R.w[3][1], R.w[3][2]);
     h2 x[16];
     x[0] = GB(6, 0);
     x[1] = GB(6, 1);
@@ -123,11 +124,11 @@ __device__ __forceinline__ v2s fast_score_pair(const Rows7 &R)
 // l_j = min(x[j .. j+7]) built from pairs and quads (8 + 8 ops) -- 36 packed ops per side
 // instead of 40.  A pixel is never a corner on both sides at one threshold (9 + 9 > 16
 // circle pixels), so the side below threshold contributes nothing: its true score is < th.
-template <int I>
+template <int I, int C = 4>
 __device__ __forceinline__ v2s fast_score_side(const Rows7 &R)
 {
-#define GB(row, dx) as_h2(gather2<4 + (dx) + I>(R.w[row][0], R.w[row][1], R.w[row][2]))
-    const v2s v = gather2<4 + I>(R.w[3][0], R.w[3][1], R.w[3][2]);
+#define GB(row, dx) as_h2(gather2<C + (dx) + I>(R.w[row][0], R.w[row][1], R.w[row][2]))
+    const v2s v = gather2<C + I>(R.w[3][0], R.w[3][1], R.w[3][2]);
     h2 x[16];
     x[0] = GB(6, 0);
     x[1] = GB(6, 1);

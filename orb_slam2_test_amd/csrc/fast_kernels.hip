@@ -29,10 +29,11 @@
 namespace orbg {
 
 // LDS per wave (fc2_* offsets in OrbgGeom, host plan):
-//   tA [H][2P]    window row r at byte r * 2P + 1 + x (x window-local), i.e. dword j holds
-//                 window bytes 4j-1 .. 4j+2; a unit (ry, gg) = detection pixels
-//                 x = 3 + 4gg .. 6 + 4gg of row 3 + ry, and its circle is dwords gg .. gg+2
-//                 of rows ry .. ry+6
+//   tA [H][2P]    window row r at byte r * 2P + x (x window-local), i.e. dword j holds
+//                 window bytes 4j .. 4j+3; a unit (ry, gg) = detection pixels
+//                 x = 3 + 4gg .. 6 + 4gg of row 3 + ry (bytes 3 .. 6 of dwords gg ..), and
+//                 the circle of its pixel pair 0-1 is dwords gg, gg+1 of rows ry .. ry+6
+//                 (14 dwords per scored pair side; the compass pretest reads 7 per unit)
 //   tB            tA shifted by 2 bytes (tB byte k = tA byte k + 2): pixels 2-3 of a unit
 //                 sit where pixels 0-1 sit in tA; row r of tB is at byte r * 2P + P, between
 //                 rows r and r + 1 of tA, so the tile rows are 2P apart (for P = 48, 24 banks:
@@ -107,14 +108,14 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(FC2_WPE, 8)
         k.nch = k.H * k.NC;
         return k;
     };
-    // Window chunk i = (row r, chunk cc): tile dwords 4cc .. 4cc+3 = window bytes 16cc-1 ..
-    // 16cc+14, from 6 aligned dwords + v_alignbyte.  The window sits >= 13 px inside the level
+    // Window chunk i = (row r, chunk cc): tile dwords 4cc .. 4cc+3 = window bytes 16cc ..
+    // 16cc+15, from 6 aligned dwords + v_alignbyte.  The window sits >= 13 px inside the level
     // and every row has >= 16 rows below it, so the aligned over-read stays in the image.
     auto chunk_src = [&](const Fc2Cell &k, int i, uint32_t &sh) {
         const int mdiv = (65536 + k.NC - 1) / k.NC;  // i / NC == (i * mdiv) >> 16, i < 1024
         const int r = (i * mdiv) >> 16, cc = i - r * k.NC;
         // pointer arithmetic (no integer round trip): global_, not flat_, loads
-        const uint8_t *src = k.base + (int64_t)r * k.pitch + 16 * cc - 1;
+        const uint8_t *src = k.base + (int64_t)r * k.pitch + 16 * cc;
         sh = (uint32_t)((uintptr_t)src & 3u);
         return (const uint32_t *)(src - sh);
     };
@@ -211,11 +212,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(FC2_WPE, 8)
                 const uint32_t invB = valid > 3 ? 0u : (valid > 2 ? 0x80000000u : 0x80008000u);
                 auto pretest = [&](auto I, uint32_t inv, uint32_t &pb_, uint32_t &pd_) {
                     constexpr int i = decltype(I)::value;
-                    const v2s v = gather2<4 + i>(r3[0], r3[1], r3[2]);
-                    const v2s c0 = gather2<4 + i>(r6[0], r6[1], r6[2]);
-                    const v2s c4 = gather2<7 + i>(r3[0], r3[1], r3[2]);
-                    const v2s c8 = gather2<4 + i>(r0[0], r0[1], r0[2]);
-                    const v2s c12 = gather2<1 + i>(r3[0], r3[1], r3[2]);
+                    const v2s v = gather2<3 + i>(r3[0], r3[1], r3[2]);
+                    const v2s c0 = gather2<3 + i>(r6[0], r6[1], r6[2]);
+                    const v2s c4 = gather2<6 + i>(r3[0], r3[1], r3[2]);
+                    const v2s c8 = gather2<3 + i>(r0[0], r0[1], r0[2]);
+                    const v2s c12 = gather2<0 + i>(r3[0], r3[1], r3[2]);
                     const v2s mb = pmin(pmax(c0, c8), pmax(c4, c12));
                     const v2s md = pmax(pmin(c0, c8), pmin(c4, c12));
                     // lane >= 0 <=> pass: mb - (v + th + 1) and (v - th - 1) - md
@@ -288,7 +289,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(FC2_WPE, 8)
             R.w[r][1] = p[r * RS4 + 1] ^ flip;
             R.w[r][2] = p[r * RS4 + 2] ^ flip;
         }
-        const v2s s = fast_score_side<0>(R);
+        const v2s s = fast_score_side<0, 3>(R);
         const uint32_t s0 = (uint16_t)s.x >= (uint32_t)thi ? (uint16_t)s.x : 0u;
         uint32_t s1 = (uint16_t)s.y >= (uint32_t)thi ? (uint16_t)s.y : 0u;
         if (RW - 4 * gg < 2 * half + 2) s1 = 0;  // pixel i + 1 past the region
@@ -400,8 +401,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(FC2_WPE, 8)
                 R.w[r][1] = p[r * RS4 + 1];
                 R.w[r][2] = p[r * RS4 + 2];
             }
-            const v2s sa = fast_score_pair<0>(R);
-            const v2s sb = fast_score_pair<2>(R);
+            const v2s sa = fast_score_pair<0, 3>(R);
+            const v2s sb = fast_score_pair<2, 3>(R);
             uint32_t word = (uint32_t)(uint16_t)sa.x | ((uint32_t)(uint16_t)sa.y << 8) |
                             ((uint32_t)(uint16_t)sb.x << 16) | ((uint32_t)(uint16_t)sb.y << 24);
             const int valid = min(RW - 4 * gg, 4);
