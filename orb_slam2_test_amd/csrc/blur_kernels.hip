@@ -178,67 +178,79 @@ __global__ __launch_bounds__(256) void k_blur2(
         const int ol = ro - ((ro + sh0) & 3) + gx - 4;
         strad_wave = __ballot(ol + 4 > nrec && ol < nrec) != 0;
     }
-    uint32_t ring[PF], rsh[PF];
-    auto issue = [&](int i) {
-        const int y = b2_reflect101(min(y0 - 3 + i, H + 2), H);
-        const int rowoff = y * pitch;
-        const int sh = __builtin_amdgcn_readfirstlane((rowoff + sh0) & 3);
-        const int o = rowoff - sh + gx - 4;
-        uint32_t v;
-        // only the level's last row can hold that dword (a tile row reads < 256 + 8 bytes,
-        // less than pitch + W), and only in waves where some lane's last-row dword does
-        // (wave-uniform test): every other row is one load with no exec-mask branches
-        v = __builtin_amdgcn_raw_buffer_load_b32(rsrc, o, 0, 0);
-        if (strad_wave && y == H - 1) {  // wave-uniform
-            if (o + 4 > nrec && o < nrec) {
-                // the dword holding the level's last byte: a dword load straddling the range
-                // end reads 0 as a whole, so this one lane reads its in-range bytes one by one
-                uint32_t vb = 0;
-                for (int b = 0; b < 4 && o + b < nrec; b++)
-                    vb |= (uint32_t)__builtin_amdgcn_raw_buffer_load_b8(rsrc, o + b, 0, 0) << (8 * b);
-                v = vb;
-            }
-        }
-        ring[i % PF] = v;
-        rsh[i % PF] = (uint32_t)sh;
-    };
-#pragma unroll
-    for (int i = 0; i < PF; i++) issue(i);
-    blur2_column<SEG>(
-        k,
-        [&](int i, uint32_t &w0, uint32_t &w1, uint32_t &w2) {
-            const uint32_t d0 = ring[i % PF], sh = rsh[i % PF];
-            if (i + PF < SEG + 6) issue(i + PF);
-            // wave_shl1 (DPP 0x130): lane j reads lane j + 1
-            const uint32_t d1 = __builtin_amdgcn_mov_dpp(d0, 0x130, 0xF, 0xF, true);
-            const uint32_t d2 = __builtin_amdgcn_mov_dpp(d1, 0x130, 0xF, 0xF, true);
-            const uint32_t d3 = __builtin_amdgcn_mov_dpp(d2, 0x130, 0xF, 0xF, true);
-            w0 = __builtin_amdgcn_alignbyte(d1, d0, sh);
-            w1 = __builtin_amdgcn_alignbyte(d2, d1, sh);
-            w2 = __builtin_amdgcn_alignbyte(d3, d2, sh);
-            if (left_wave) {  // x = -4 .. -1 -> 4, 3, 2, 1
-                const uint32_t r = __builtin_amdgcn_perm(w2, w1, 0x01020304u);
-                w0 = is_left ? r : w0;
-            }
-            if (right_wave) {
-                const uint32_t v1 = __builtin_amdgcn_perm(w1, w0, sel1);
-                const uint32_t v2 = pair_lo ? __builtin_amdgcn_perm(w1, w0, sel2)
-                                            : __builtin_amdgcn_perm(w2, w1, sel2);
-                w1 = v1;
-                w2 = v2;
-            }
-        },
-        [&](int o, uint32_t word) {
-            const int gy = y0 + o;
-            if (gy < H && owner) {  // gy: wave-uniform
-                uint8_t *d = dst + (int64_t)gy * lv.pitch + gx;
-                if (gx + 4 <= W) {
-                    *(uint32_t *)d = word;  // pitch is a multiple of 64, gx of 4: aligned
-                } else {
-                    for (int c = 0; c < 4 && gx + c < W; c++) d[c] = (uint8_t)(word >> (8 * c));
+    // stores: buffer stores over the blurred level incl. its row padding; lanes that store
+    // nothing (past the tile or the level width) and rows past the level get an offset past
+    // the range, which the hardware drops -- no exec-mask branches per row.  A lane whose
+    // 4 columns pass W writes the rest of its dword into the row padding (pitch >= W
+    // rounded up to 64; the padding is never read).
+    const __amdgpu_buffer_rsrc_t drsrc = __builtin_amdgcn_make_buffer_rsrc(
+        (void *)dst, (short)0, H * lv.pitch, 0x00020000);
+    const int lane_off = owner ? gx : (1 << 30);
+    // interior tiles (every source row inside the level, the last one above the level's last
+    // row) need no REFLECT_101 row index and no straddle test: the row offset is affine in i
+    const bool interior = y0 >= 3 && y0 + SEG + 3 < H;
+    auto run = [&](auto INTERIOR) {
+        constexpr bool inner = decltype(INTERIOR)::value;
+        uint32_t ring[PF], rsh[PF];
+        auto issue = [&](int i) {
+            const int y = inner ? y0 - 3 + i : b2_reflect101(min(y0 - 3 + i, H + 2), H);
+            const int rowoff = y * pitch;
+            const int sh = __builtin_amdgcn_readfirstlane((rowoff + sh0) & 3);
+            const int o = rowoff - sh + gx - 4;
+            uint32_t v;
+            // only the level's last row can hold that dword (a tile row reads < 256 + 8
+            // bytes, less than pitch + W), and only in waves where some lane's last-row dword
+            // does (wave-uniform test): every other row is one load with no exec-mask branches
+            v = __builtin_amdgcn_raw_buffer_load_b32(rsrc, o, 0, 0);
+            if (!inner && strad_wave && y == H - 1) {  // wave-uniform
+                if (o + 4 > nrec && o < nrec) {
+                    // the dword holding the level's last byte: a dword load straddling the
+                    // range end reads 0 as a whole, so this one lane reads its in-range bytes
+                    // one by one
+                    uint32_t vb = 0;
+                    for (int b = 0; b < 4 && o + b < nrec; b++)
+                        vb |= (uint32_t)__builtin_amdgcn_raw_buffer_load_b8(rsrc, o + b, 0, 0) << (8 * b);
+                    v = vb;
                 }
             }
-        });
+            ring[i % PF] = v;
+            rsh[i % PF] = (uint32_t)sh;
+        };
+#pragma unroll
+        for (int i = 0; i < PF; i++) issue(i);
+        blur2_column<SEG>(
+            k,
+            [&](int i, uint32_t &w0, uint32_t &w1, uint32_t &w2) {
+                const uint32_t d0 = ring[i % PF], sh = rsh[i % PF];
+                if (i + PF < SEG + 6) issue(i + PF);
+                // wave_shl1 (DPP 0x130): lane j reads lane j + 1
+                const uint32_t d1 = __builtin_amdgcn_mov_dpp(d0, 0x130, 0xF, 0xF, true);
+                const uint32_t d2 = __builtin_amdgcn_mov_dpp(d1, 0x130, 0xF, 0xF, true);
+                const uint32_t d3 = __builtin_amdgcn_mov_dpp(d2, 0x130, 0xF, 0xF, true);
+                w0 = __builtin_amdgcn_alignbyte(d1, d0, sh);
+                w1 = __builtin_amdgcn_alignbyte(d2, d1, sh);
+                w2 = __builtin_amdgcn_alignbyte(d3, d2, sh);
+                if (left_wave) {  // x = -4 .. -1 -> 4, 3, 2, 1
+                    const uint32_t r = __builtin_amdgcn_perm(w2, w1, 0x01020304u);
+                    w0 = is_left ? r : w0;
+                }
+                if (right_wave) {
+                    const uint32_t v1 = __builtin_amdgcn_perm(w1, w0, sel1);
+                    const uint32_t v2 = pair_lo ? __builtin_amdgcn_perm(w1, w0, sel2)
+                                                : __builtin_amdgcn_perm(w2, w1, sel2);
+                    w1 = v1;
+                    w2 = v2;
+                }
+            },
+            [&](int o, uint32_t word) {
+                __builtin_amdgcn_raw_buffer_store_b32(word, drsrc, lane_off + (y0 + o) * lv.pitch,
+                                                      0, 0);
+            });
+    };
+    if (interior)
+        run(std::true_type{});
+    else
+        run(std::false_type{});
 }
 
 int blur2_seg() { return ORBG_BLUR2_SEG; }
