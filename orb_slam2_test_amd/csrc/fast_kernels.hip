@@ -138,6 +138,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(FC2_WPE, 8)
         }
     };
 
+    // launch constants read once (scalar loads after the LDS fences would wait on the LDS
+    // queue too: both count in lgkmcnt)
+    const int dbg = g->dbg, thi = g->ini_th, tlo = g->min_th;
+    const int lcap = g->fc2_list_cap;  // pretest list entries (2 per unit of the largest cell)
+    const int ncells = g->ncells, cell_cap = g->cell_cap;
 #pragma unroll 1
     for (int kc = 0; kc < FC2_CPW; kc++) {
     const int cid = cid0 + kc;
@@ -174,12 +179,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(FC2_WPE, 8)
         for (int i = lane; i < nz; i += 64) z[i] = make_uint2(0, 0);
     }
     wave_sync_lds();
-    if (g->dbg == 11) continue;
+    if (dbg == 11) continue;
 
     // unit u = ry * RG + gg walked as u = lane + 64 k: (ry, gg) advance by (64 / RG, 64 % RG)
     const int rstep = RG > 0 ? 64 / RG : 0, gstep = RG > 0 ? 64 - rstep * RG : 0;
     const int ry0 = RG > 0 ? lane / RG : 0, gg0 = lane - ry0 * RG;
-    const int thi = g->ini_th, tlo = g->min_th;
 
     // ---- compass pretest at iniThFAST (necessary for a 9-arc: some adjacent compass pair
     // (0,4), (4,8), (8,12), (12,0) is on the arc's side), bright and dark apart:
@@ -187,7 +191,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(FC2_WPE, 8)
     // Survivors (pair, side) are ballot-compacted into one list; order is irrelevant (the
     // scores go to their place in sc) ----
     int nlist = 0, nboth = 0;
-    const int lcap = g->fc2_list_cap;  // entries (2 per unit of the largest cell)
     {
         const v2s vth1 = (v2s){(short)(thi + 1), (short)(thi + 1)};
         // tile offset of unit (ry, gg) kept incrementally (no per-iteration multiply)
@@ -270,7 +273,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(FC2_WPE, 8)
         }
     }
     wave_sync_lds();
-    if (g->dbg == 14) continue;
+    if (dbg == 14) continue;
 
     // ---- one side of one pixel pair per lane task: tasks [0, nlist) are the bottom entries,
     // then two per top entry (bright, dark) ----
@@ -298,7 +301,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(FC2_WPE, 8)
                               __HIP_MEMORY_SCOPE_WAVEFRONT);
     }
     wave_sync_lds();
-    if (g->dbg == 12) continue;
+    if (dbg == 12) continue;
 
     // ---- NMS (cell-local) + raster-order compaction, as k_fast_cells ----
     // cv::FAST keeps p iff s_p > every neighbour's score, a neighbour that is not a corner
@@ -333,8 +336,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(FC2_WPE, 8)
         if (valid < 4) kb &= (1u << valid) - 1u;
         return kb;
     };
-    const int64_t slot = (int64_t)f * g->ncells + c;
-    uint2 *out = cell_kp + slot * g->cell_cap;
+    const int64_t slot = (int64_t)f * ncells + c;
+    uint2 *out = cell_kp + slot * cell_cap;
     int run = 0;
     auto emit = [&](uint32_t kb, int ry, int gg) {
         const int n = __popc(kb);
@@ -387,7 +390,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(FC2_WPE, 8)
         }
         emit(kb, ry, gg);
     }
-    if (g->dbg == 13) continue;
+    if (dbg == 13) continue;
     if (run == 0) {
         // an empty cell retries at minThFAST (ORBextractor.cc:1069-1075): every unit scored
         // on both sides (the window tiles are intact), then NMS at minThFAST

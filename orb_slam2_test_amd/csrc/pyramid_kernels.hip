@@ -64,9 +64,11 @@ __device__ __forceinline__ void pyr_hrow(uint4 raw, uint32_t o, const PyrOct &t,
 __device__ __forceinline__ uint4 pyr_load(const uint8_t *p, const uint8_t *end, bool guard,
                                           uint32_t &o)
 {
-    const uintptr_t pa = (uintptr_t)p;
-    o = (uint32_t)pa & 3u;
-    const uint8_t *a = (const uint8_t *)(pa & ~(uintptr_t)3);
+    o = (uint32_t)(uintptr_t)p & 3u;
+    // pointer arithmetic, not an integer round trip: the compiler keeps the global address
+    // space (global_load, not flat_load: a flat load also counts in lgkmcnt, so every scalar
+    // ytab load's wait would drain the prefetched rows)
+    const uint8_t *a = p - o;
     if (guard && a + 16 > end) {
         uint32_t w[4] = {0, 0, 0, 0};
         for (int b = 0; b < 16; b++)
