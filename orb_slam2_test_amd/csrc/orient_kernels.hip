@@ -158,6 +158,27 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(ORBG_OD_WPE
     const int jfirst = __builtin_ctz(okmask);
     const uint32_t kl_l = my_ok ? kl : (uint32_t)__builtin_amdgcn_readlane((int)kl, jfirst);
     const int lev_l = my_ok ? my_lev : __builtin_amdgcn_readlane(my_lev, jfirst);
+    // per-slot addresses, lane j = slot j, computed once: the slot loops take them by
+    // v_readlane instead of scalar loads of the level records (which, after the LDS fences,
+    // would be reissued per slot and wait on the LDS queue: both count in lgkmcnt)
+    int ppitch_l, bpitch_l;
+    int64_t poff_l, boff_l;  // patch centre (from img0 / pyr), neighbourhood top-left (blur)
+    {
+        const OrbgLevel &lv = g->lv[lev_l];
+        const int x = orbg_px(kl_l) + ORBG_MIN_BORDER, y = orbg_py(kl_l) + ORBG_MIN_BORDER;
+        bpitch_l = lv.pitch;
+        ppitch_l = lev_l == 0 ? img_pitch : bpitch_l;
+        poff_l = (lev_l == 0 ? (int64_t)f * img_fs : (int64_t)f * g->pyr_frame + lv.pyr_off) +
+                 (int64_t)y * ppitch_l + x;
+        boff_l = (int64_t)f * g->blur_frame + lv.blur_off + (int64_t)(y - OD_R) * bpitch_l +
+                 (x - OD_R);
+    }
+    const int64_t drow0 = (int64_t)f * g->frame_cap;  // this frame's first output row
+    auto readlane64 = [](int64_t v, int j) -> int64_t {
+        const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)v, j);
+        const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(v >> 32), j);
+        return (int64_t)((uint64_t)hi << 32 | lo);
+    };
 
     // ---- A: IC_Angle moments (ORBextractor.cc:83-111), slot j's sums kept by lane j ----
     // Software-pipelined over the slots: the patch loads of slot j + 1 are in flight while
@@ -165,18 +186,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(ORBG_OD_WPE
     // loads, not by issue); two register buffers alternate.
     auto load_patch = [&](int j, uint4 (&wd)[2], int (&sh)[2]) {
         const int lev = __builtin_amdgcn_readlane(lev_l, j);
-        const uint32_t key = (uint32_t)__builtin_amdgcn_readlane((int)kl_l, j);
-        const int x = orbg_px(key) + ORBG_MIN_BORDER, y = orbg_py(key) + ORBG_MIN_BORDER;
-        const uint8_t *im;
-        int pitch;
-        if (lev == 0) {
-            im = img0 + f * img_fs;
-            pitch = img_pitch;
-        } else {
-            im = pyr + f * g->pyr_frame + g->lv[lev].pyr_off;
-            pitch = g->lv[lev].pitch;
-        }
-        const uint8_t *ctr = im + (int64_t)y * pitch + x;
+        const int pitch = __builtin_amdgcn_readlane(ppitch_l, j);
+        const uint8_t *ctr = (lev == 0 ? img0 : pyr) + readlane64(poff_l, j);
         // 16 bytes per lane from each row's 4-byte-aligned start (the level-0 pitch may be
         // odd, so the alignment is per row)
 #pragma unroll
@@ -274,13 +285,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(ORBG_OD_WPE
         int sh;
     };
     auto load_nbhd = [&](int j) -> Nbhd {
-        const int lev = __builtin_amdgcn_readlane(lev_l, j);
-        const uint32_t key = (uint32_t)__builtin_amdgcn_readlane((int)kl_l, j);
-        const int x = orbg_px(key) + ORBG_MIN_BORDER, y = orbg_py(key) + ORBG_MIN_BORDER;
-        const OrbgLevel &lv = g->lv[lev];
-        const int bpitch = lv.pitch;
-        const uint8_t *bl0 = blur + f * g->blur_frame + lv.blur_off +
-                             (int64_t)(y - OD_R) * bpitch + (x - OD_R);
+        const int bpitch = __builtin_amdgcn_readlane(bpitch_l, j);
+        const uint8_t *bl0 = blur + readlane64(boff_l, j);
         Nbhd n;
         n.sh = (int)((uintptr_t)bl0 & 3);
         const uint8_t *bw = bl0 - n.sh;
@@ -334,7 +340,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(ORBG_OD_WPE
         }
         const int i = __builtin_amdgcn_readlane(my_i, j);
         if (((okmask >> j) & 1u) && lane < 8)
-            ((uint32_t *)(desc + ((int64_t)f * g->frame_cap + i) * 32))[lane] = word;
+            ((uint32_t *)(desc + (drow0 + i) * 32))[lane] = word;
     }
 }
 
