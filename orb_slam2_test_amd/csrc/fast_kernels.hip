@@ -200,9 +200,12 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(FC2_WPE, 8)
             const int u = u0 + lane;
             // per pair: bright / dark survivors as the sign bits (15, 31) of a packed word,
             // 0 = none; pixels outside the region are forced to fail
+            // every lane runs the test (lanes past the last unit read unit 0's words and
+            // are forced to fail): no exec-mask branch per 64 units
             uint32_t ab = 0, ad = 0, bb = 0, bd = 0;
-            if (u < nunits) {
-                const uint32_t *p = (const uint32_t *)(tA + toff);
+            const bool in = u < nunits;
+            {
+                const uint32_t *p = (const uint32_t *)(tA + (in ? toff : 0));
                 uint32_t r0[3], r3[3], r6[3];
 #pragma unroll
                 for (int k = 0; k < 3; k++) {
@@ -210,8 +213,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(FC2_WPE, 8)
                     r3[k] = p[3 * RS4 + k];
                     r6[k] = p[6 * RS4 + k];
                 }
-                const int valid = RW - 4 * gg;  // pixels of the unit inside the region (>= 1)
-                const uint32_t invA = valid > 1 ? 0u : 0x80000000u;
+                const int valid = in ? RW - 4 * gg : 0;  // pixels of the unit inside the region
+                const uint32_t invA = valid > 1 ? 0u : (valid > 0 ? 0x80000000u : 0x80008000u);
                 const uint32_t invB = valid > 3 ? 0u : (valid > 2 ? 0x80000000u : 0x80008000u);
                 auto pretest = [&](auto I, uint32_t inv, uint32_t &pb_, uint32_t &pd_) {
                     constexpr int i = decltype(I)::value;
