@@ -311,12 +311,12 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(FC2_WPE, 8)
     // at the cell threshold th counting as 0; with s_p >= max(th, 1) that is exactly
     //   max(raw 8-neighbour scores) < max(th, s_p).
     const v2s one = (v2s){1, 1};
-    auto keep_bits = [&](int ry, int gg, int th) -> uint32_t {
+    auto keep_bits = [&](int ry, int gg, int th, bool may_be_empty) -> uint32_t {
         const v2s t1v = (v2s){(short)max(th, 1), (short)max(th, 1)};
         const v2s thv = (v2s){(short)th, (short)th};
         const uint32_t *m = (const uint32_t *)(sc + ry * P + 4 * gg);
         const uint32_t c1 = m[P4 + 1];
-        if (c1 == 0) return 0u;  // a unit with no scored pixel keeps nothing
+        if (may_be_empty && c1 == 0) return 0u;  // a unit with no scored pixel keeps nothing
         const uint32_t u0 = m[0], u1 = m[1], u2 = m[2];
         const uint32_t c0 = m[P4], c2 = m[P4 + 2];
         const uint32_t d0 = m[2 * P4], d1 = m[2 * P4 + 1], d2 = m[2 * P4 + 2];
@@ -366,8 +366,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(FC2_WPE, 8)
     uint16_t *plist = list;
     int npass = 0;
     for (int u0 = 0, ry = ry0, gg = gg0; u0 < nunits; u0 += 64) {
-        const bool corner =
-            u0 + lane < nunits && *(const uint32_t *)(sc + (ry + 1) * P + 4 * gg + 4) != 0;
+        const bool in = u0 + lane < nunits;  // the read is unconditional (no exec branch)
+        const uint32_t sw = *(const uint32_t *)(sc + (in ? (ry + 1) * P + 4 * gg + 4 : 0));
+        const bool corner = in && sw != 0;
         const unsigned long long m = __ballot(corner);
         const int below = __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32),
                                                     __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0));
@@ -383,14 +384,12 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(FC2_WPE, 8)
     wave_sync_lds();
     for (int j0 = 0; j0 < npass; j0 += 64) {
         const int j = j0 + lane;
-        int ry = 0, gg = 0;
-        uint32_t kb = 0;
-        if (j < npass) {
-            const int e = plist[j];
-            ry = e >> 8;
-            gg = e & 0xFF;
-            kb = keep_bits(ry, gg, thi);
-        }
+        // branch-free: lanes past the list redo the last entry and keep nothing (every
+        // listed unit has a scored pixel, so no empty-unit exit either)
+        const int e = plist[min(j, npass - 1)];
+        const int ry = e >> 8, gg = e & 0xFF;
+        const uint32_t kb0 = keep_bits(ry, gg, thi, false);
+        const uint32_t kb = j < npass ? kb0 : 0u;
         emit(kb, ry, gg);
     }
     if (dbg == 13) continue;
@@ -423,7 +422,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(FC2_WPE, 8)
         }
         wave_sync_lds();
         for (int u0 = 0, ry = ry0, gg = gg0; u0 < nunits; u0 += 64) {
-            const uint32_t kb = u0 + lane < nunits ? keep_bits(ry, gg, tlo) : 0u;
+            const uint32_t kb = u0 + lane < nunits ? keep_bits(ry, gg, tlo, true) : 0u;
             emit(kb, ry, gg);
             ry += rstep;
             gg += gstep;
