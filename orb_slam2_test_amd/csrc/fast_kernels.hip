@@ -163,16 +163,15 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(FC2_WPE, 8)
             uint32_t sh[2];
 #pragma unroll
             for (int u = 0; u < 2; u++) {
-                const int i = i0 + 64 * u + lane;
-                const uint32_t *aw = chunk_src(cur, i < cur.nch ? i : 0, sh[u]);
+                // lanes past the last chunk redo it (the same bytes to the same place): the
+                // stores below need no exec-mask branch
+                const int i = min(i0 + 64 * u + lane, cur.nch - 1);
+                const uint32_t *aw = chunk_src(cur, i, sh[u]);
                 q[u] = *(const uint4 *)aw;  // unconditional: both in flight
                 q2[u] = *(const uint2 *)(aw + 4);
             }
 #pragma unroll
-            for (int u = 0; u < 2; u++) {
-                const int i = i0 + 64 * u + lane;
-                if (i < cur.nch) put(cur, i, q[u], q2[u], sh[u]);
-            }
+            for (int u = 0; u < 2; u++) put(cur, min(i0 + 64 * u + lane, cur.nch - 1), q[u], q2[u], sh[u]);
         }
         uint2 *z = (uint2 *)sc;
         const int nz = (RH + 2) * (P / 8);
