@@ -340,6 +340,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(FC2_WPE, 8)
     };
     const int64_t slot = (int64_t)f * ncells + c;
     uint2 *out = cell_kp + slot * cell_cap;
+    const __amdgpu_buffer_rsrc_t orsrc =
+        __builtin_amdgcn_make_buffer_rsrc((void *)out, (short)0, cell_cap * 8, 0x00020000);
     int run = 0;
     auto emit = [&](uint32_t kb, int ry, int gg) {
         const int n = __popc(kb);
@@ -350,14 +352,18 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(FC2_WPE, 8)
         uint32_t cx[4];
 #pragma unroll
         for (int i = 0; i < 4; i++) cx[i] = (uint32_t)__shfl((int)xs_l, (4 * gg + i) & 63, 64);
-        if (kb) {
-            int off = run + incl - n;
-            const uint32_t c1 = *(const uint32_t *)(sc + (ry + 1) * P + 4 * gg + 4);
-            const int xx = xo + 4 * gg, y = yo + ry;
+        // four unconditional buffer stores: a pixel that is not kept gets an offset past the
+        // cell's range, which the hardware drops (no exec-mask branch per pixel)
+        const int off = run + incl - n;
+        const uint32_t c1 = *(const uint32_t *)(sc + (ry + 1) * P + 4 * gg + 4);
+        const int xx = xo + 4 * gg, y = yo + ry;
 #pragma unroll
-            for (int i = 0; i < 4; i++)
-                if (kb & (1u << i))
-                    out[off++] = make_uint2(orbg_pack(xx + i, y, (c1 >> (8 * i)) & 0xFF), cx[i] | cy);
+        for (int i = 0; i < 4; i++) {
+            const int pos = off + __popc(kb & ((1u << i) - 1u));
+            typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
+            const u32x2 rec = {orbg_pack(xx + i, y, (c1 >> (8 * i)) & 0xFF), cx[i] | cy};
+            __builtin_amdgcn_raw_buffer_store_b64(rec, orsrc, (kb >> i & 1u) ? pos * 8 : (1 << 30),
+                                                  0, 0);
         }
         run += tot;
     };
