@@ -38,7 +38,7 @@ namespace orbg {
 //                 sit where pixels 0-1 sit in tA; row r of tB is at byte r * 2P + P, between
 //                 rows r and r + 1 of tA, so the tile rows are 2P apart (for P = 48, 24 banks:
 //                 the pretest's 8 rows x 8 units of a wave read 64 distinct banks)
-//   sc [RH+2][P]  u8 scores at sc[ry + 1][4 + 4gg + i], zero border
+//   sc [RH+2][SP] u8 scores at sc[ry + 1][4 + 4gg + i], zero border (SP = P - 8 >= 4 RG + 8)
 //   list u16      pretest survivors: ry << 8 | gg << 2 | half << 1 | dark
 #ifndef FC2_CPW
 #define FC2_CPW 2  // consecutive cells per wave (shared halo lines in L1, fewer workgroups)
@@ -51,7 +51,7 @@ struct Fc2Cell {
 };
 
 #ifndef FC2_WPE
-#define FC2_WPE 6  // min waves per SIMD the register allocation targets (79 VGPRs, no spill; 4 -> 6 measured -1.3% per step)
+#define FC2_WPE 7  // min waves per SIMD the register allocation targets (72 VGPRs, 12 B spill; 6 -> 7 with the 7-WG LDS plan: -0.3% per step)
 #endif
 template <int P4>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(FC2_WPE, 8))) void k_fast2(
@@ -62,6 +62,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(FC2_WPE, 8)
     int c_count)
 {
     constexpr int P = 4 * P4;
+    constexpr int SP4 = P4 - 2, SP = 4 * SP4;  // score rows: RG + 2 dwords <= P4 - 2 (host plan)
     constexpr int RS = 2 * P, RS4 = 2 * P4;  // tile row stride (bytes, dwords)
     extern __shared__ __attribute__((aligned(16))) uint32_t fc2_lds[];
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
@@ -174,7 +175,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(FC2_WPE, 8)
             for (int u = 0; u < 2; u++) put(cur, min(i0 + 64 * u + lane, cur.nch - 1), q[u], q2[u], sh[u]);
         }
         uint2 *z = (uint2 *)sc;
-        const int nz = (RH + 2) * (P / 8);
+        const int nz = (RH + 2) * (SP / 8);
         for (int i = lane; i < nz; i += 64) z[i] = make_uint2(0, 0);
     }
     wave_sync_lds();
@@ -298,7 +299,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(FC2_WPE, 8)
         const uint32_t s0 = (uint16_t)s.x >= (uint32_t)thi ? (uint16_t)s.x : 0u;
         uint32_t s1 = (uint16_t)s.y >= (uint32_t)thi ? (uint16_t)s.y : 0u;
         if (RW - 4 * gg < 2 * half + 2) s1 = 0;  // pixel i + 1 past the region
-        __hip_atomic_fetch_or((uint32_t *)(sc + (ry + 1) * P + 4 * gg + 4),
+        __hip_atomic_fetch_or((uint32_t *)(sc + (ry + 1) * SP + 4 * gg + 4),
                               (s0 | s1 << 8) << (16 * half), __ATOMIC_RELAXED,
                               __HIP_MEMORY_SCOPE_WAVEFRONT);
     }
@@ -313,12 +314,12 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(FC2_WPE, 8)
     auto keep_bits = [&](int ry, int gg, int th, bool may_be_empty) -> uint32_t {
         const v2s t1v = (v2s){(short)max(th, 1), (short)max(th, 1)};
         const v2s thv = (v2s){(short)th, (short)th};
-        const uint32_t *m = (const uint32_t *)(sc + ry * P + 4 * gg);
-        const uint32_t c1 = m[P4 + 1];
+        const uint32_t *m = (const uint32_t *)(sc + ry * SP + 4 * gg);
+        const uint32_t c1 = m[SP4 + 1];
         if (may_be_empty && c1 == 0) return 0u;  // a unit with no scored pixel keeps nothing
         const uint32_t u0 = m[0], u1 = m[1], u2 = m[2];
-        const uint32_t c0 = m[P4], c2 = m[P4 + 2];
-        const uint32_t d0 = m[2 * P4], d1 = m[2 * P4 + 1], d2 = m[2 * P4 + 2];
+        const uint32_t c0 = m[SP4], c2 = m[SP4 + 2];
+        const uint32_t d0 = m[2 * SP4], d1 = m[2 * SP4 + 1], d2 = m[2 * SP4 + 2];
         v2s mA = pmax(pmax(gather2<3>(u0, u1, u2), gather2<4>(u0, u1, u2)), gather2<5>(u0, u1, u2));
         mA = pmax(mA, pmax(pmax(gather2<3>(d0, d1, d2), gather2<4>(d0, d1, d2)),
                            gather2<5>(d0, d1, d2)));
@@ -355,7 +356,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(FC2_WPE, 8)
         // four unconditional buffer stores: a pixel that is not kept gets an offset past the
         // cell's range, which the hardware drops (no exec-mask branch per pixel)
         const int off = run + incl - n;
-        const uint32_t c1 = *(const uint32_t *)(sc + (ry + 1) * P + 4 * gg + 4);
+        const uint32_t c1 = *(const uint32_t *)(sc + (ry + 1) * SP + 4 * gg + 4);
         const int xx = xo + 4 * gg, y = yo + ry;
 #pragma unroll
         for (int i = 0; i < 4; i++) {
@@ -372,7 +373,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(FC2_WPE, 8)
     int npass = 0;
     for (int u0 = 0, ry = ry0, gg = gg0; u0 < nunits; u0 += 64) {
         const bool in = u0 + lane < nunits;  // the read is unconditional (no exec branch)
-        const uint32_t sw = *(const uint32_t *)(sc + (in ? (ry + 1) * P + 4 * gg + 4 : 0));
+        const uint32_t sw = *(const uint32_t *)(sc + (in ? (ry + 1) * SP + 4 * gg + 4 : 0));
         const bool corner = in && sw != 0;
         const unsigned long long m = __ballot(corner);
         const int below = __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32),
@@ -417,7 +418,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(FC2_WPE, 8)
                             ((uint32_t)(uint16_t)sb.x << 16) | ((uint32_t)(uint16_t)sb.y << 24);
             const int valid = min(RW - 4 * gg, 4);
             if (valid < 4) word &= (1u << (8 * valid)) - 1u;
-            *(uint32_t *)(sc + (ry + 1) * P + 4 * gg + 4) = word;
+            *(uint32_t *)(sc + (ry + 1) * SP + 4 * gg + 4) = word;
             ry += rstep;
             gg += gstep;
             if (gg >= RG) {

@@ -882,18 +882,19 @@ static int plan(orbg_ctx *c, int w, int h, int batch)
                            hmax, G.fc_wave_bytes);
         // k_fast2 (fast_kernels.hip): compile-time pitch P4 >= 4 * ceil((RG + 3) / 4) (its
         // 16-byte window chunks) among the instantiated ones; layout tA / tB (hmax rows each,
-        // interleaved: row stride 2 * P) | scores (hmax - 4 rows) | list (2 entries per unit).  Preferred: the most
-        // workgroups per CU by LDS (capped at 6: the VGPR bound), then the bank-spread cost.
+        // interleaved: row stride 2 * P) | scores (hmax - 4 rows of P - 8 bytes) | list (2 entries per unit).  Preferred: the most
+        // workgroups per CU by LDS, then the bank-spread cost.
         G.fc2_p4 = 0;
         if (c->fast_v2) {
-            const int need = 4 * ((rg + 3 + 3) / 4);
+            // tile rows: 4 * ceil-ish((rg + 6) / 4) dwords; score rows (P4 - 2 dwords) hold rg + 2
+            const int need = std::max(4 * ((rg + 3 + 3) / 4), rg + 4);
             int best_c = 1 << 30, best_wg = 0;
             for (int wd = need; wd <= 32; wd++) {
                 if (!fast2_pitch_ok(wd)) continue;
                 const int P2 = 4 * wd;
-                const int wb = (2 * hmax * P2 + (std::max(hmax - 6, 0) + 2) * P2 +
-                                4 * max_units + 15) & ~15;
-                const int wgs = std::min(6, 163840 / (4 * wb));
+                const int wb = (2 * hmax * P2 + (std::max(hmax - 6, 0) + 2) * (P2 - 8) +
+                                4 * max_units + 2 + 15) & ~15;
+                const int wgs = std::min(8, 163840 / (4 * wb));
                 int cost = 0;
                 for (int r : rgs)
                     for (int k = 0; k < 3; k++) {
@@ -914,7 +915,7 @@ static int plan(orbg_ctx *c, int w, int h, int batch)
                 const int P2 = 4 * G.fc2_p4;
                 G.fc2_tileb_off = P2;  // tB rows interleaved with tA's (row stride 2 * P2)
                 G.fc2_sc_off = 2 * hmax * P2;
-                G.fc2_list_off = G.fc2_sc_off + (std::max(hmax - 6, 0) + 2) * P2;
+                G.fc2_list_off = G.fc2_sc_off + (std::max(hmax - 6, 0) + 2) * (P2 - 8);  // score rows: P2 - 8 bytes
                 G.fc2_list_cap = 2 * max_units;
                 G.fc2_wave_bytes = (G.fc2_list_off + 2 * G.fc2_list_cap + 2 + 15) & ~15;  // + k_fast2's spare entry
                 if (4 * G.fc2_wave_bytes > 160 * 1024) G.fc2_p4 = 0;
