@@ -33,7 +33,7 @@ namespace orbg {
 #define ORBG_BLUR2_SEG 32  // output rows per wave
 #endif
 #ifndef ORBG_BLUR2_ROWPF
-#define ORBG_BLUR2_ROWPF 6  // source rows in flight per lane (6: -1.7% serial vs 8, 12: +2%)
+#define ORBG_BLUR2_ROWPF 4  // source rows in flight per lane (vs 8: 4 -2.5%, 6 -1.7%, 12 +2% serial)
 #endif
 
 __device__ __forceinline__ uint32_t b2_udot2(uint32_t a, uint32_t b, uint32_t c)
