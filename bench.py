@@ -40,8 +40,8 @@ EXTRACT_FRAME_ALGO_BYTES = 2533578  # configs[1] / C2: ORBextractor only
 METRIC_EXTRACT = "frames/sec ORBextractor only, 1241×376 2000feat 8lvl (configs[1], C2)"
 
 
-PMC_MONO = "r02h_pmc_kernels.json"      # tools/r02_profile.sh (bench.py), copied from its run dir
-PMC_STEREO = "r02h_stereo_pmc_kernels.json"  # tools/r02_profile.sh <tag> --stereo
+PMC_MONO = "r02i_pmc_kernels.json"      # tools/r02_profile.sh (bench.py), copied from its run dir
+PMC_STEREO = "r02i_stereo_pmc_kernels.json"  # tools/r02_profile.sh <tag> --stereo
 
 
 def kernel_algo_bytes(name, B, npairs, ncand, nkp, launches_per_step):
