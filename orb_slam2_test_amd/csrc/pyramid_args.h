@@ -6,7 +6,9 @@
 #define PYR_ROWS 8   // output rows per work item (one lane)
 #define PYR_COLS 8   // output columns per work item
 #define PYR_NS 11    // max source rows per item: floor(7 * 1.2) + 1 + 2 (host checks)
+#ifndef PYR_PF
 #define PYR_PF 4     // source rows in flight ahead of the one being summed
+#endif
 
 // per output column octet: 5 x uint4
 //   [0] {sx0 = source column of the octet's first output column, scalar-column mask, 0, 0}
