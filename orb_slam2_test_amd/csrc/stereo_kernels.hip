@@ -236,7 +236,8 @@ __device__ __forceinline__ void stereo_sad_one(const StereoGeom &G,
         const int y = yl - ST_W + r;
         const uint8_t *src = c < 4 ? IL + (int64_t)y * lp + xl - ST_W
                                    : IR + (int64_t)y * rp + xr - 2 * ST_W;
-        const uintptr_t a = (uintptr_t)src & ~(uintptr_t)3;
+        // pointer arithmetic, not an integer round trip: a global_, not a flat_, load
+        const uint8_t *a = src - ((uintptr_t)src & 3);
         const uint32_t v = ((const uint32_t *)a)[c < 4 ? c : c - 4];
         if (c < 4)
             stL[r * 4 + c] = v;

@@ -380,7 +380,9 @@ __global__ __launch_bounds__(TRK_RT) void k_track_resolve(TrackArgs A)
     float *kang = (float *)(push + A.qc);
     uint8_t *taken = (uint8_t *)(kang + A.fc);
     int8_t *koct = (int8_t *)(taken + A.fc);
-    int32_t *owner = (int32_t *)(((uintptr_t)(koct + A.fc) + 3) & ~(uintptr_t)3);
+    // offset arithmetic on the LDS base (an integer round trip of the pointer would lose the
+    // address space and make every owner[] access a flat one)
+    int32_t *owner = (int32_t *)(trs + (((int)((uint8_t *)(koct + A.fc) - trs) + 3) & ~3));
     const uint8_t *t0 = A.taken0 ? A.taken0 + (size_t)f * A.fc : nullptr;
     const orbg_keypoint *kps = A.kps + (size_t)f * A.fc;
     for (int i = tid; i < n; i += TRK_RT) {
