@@ -2,13 +2,16 @@
 """bench.py -- frames/s of ORB extract + match at 1241x376, 2000 features, 8 levels.
 
 A step = one pass of the hot path over one batch of B synthetic frames per GPU, resident
-in HBM before the timed region:
+in HBM before the timed region (sequence.BenchStep, which the -m gpu parity tests run
+unchanged):
   ORBextractor::operator() on every frame (pyramid, FAST cells, quadtree, blur,
   IC_Angle + rBRIEF) and, for every frame t, the matcher between t-1 and t
   (all-pairs Hamming knn2 + SearchForInitialization(window 100, nnratio 0.9, checkOri)).
+The steps cycle through --blocks distinct resident blocks of the sequence, so a step never
+re-reads the frames the step before it read.
 Multi-GPU (torch.distributed.run, one process per GPU): frames are sharded (each rank
-owns its own block of the sequence, weak scaling); the only collective is an RCCL
-all_gather of the per-frame trajectory summary (keypoint and match counts) per step.
+owns its own blocks of the sequence, weak scaling); the only collectives are RCCL
+all_gathers of the per-frame outputs (keypoint and match counts, vnMatches12 rows) per step.
 
 Prints ONE JSON line on rank 0 (contract in the task statement):
   value = all ranks' frames / max-over-ranks wall time of K steps,
@@ -109,7 +112,8 @@ def cpu_baseline_stereo(lefts, rights, threads, nframes, nframes_1core=8):
     ncpu, model = host_cpu()
     return {"value": round(nframes / dt, 3), "unit": "stereo frames/s", "cores": threads,
             "kind": "port", "value_1core": round(nframes_1core / dt1, 3),
-            "host_logical_cpus": ncpu, "host_cpu_model": model,
+            "host_logical_cpus": ncpu, "host_affinity_cpus": len(os.sched_getaffinity(0)),
+            "host_cpu_model": model,
             "sample": ("%d synthetic 1241x376 stereo frames (extract L+R 2000 feat/8 lvl + "
                        "ComputeStereoMatches), oracle/ C restatement -O3, %d threads, %.1f s "
                        "wall; 1 thread: %d frames, %.1f s" % (nframes, threads, dt,
@@ -133,10 +137,23 @@ def cpu_baseline_extract(frames, threads, nframes, nframes_1core=48):
     ncpu, model = host_cpu()
     return {"value": round(nframes / dt, 3), "unit": "frames/s", "cores": threads,
             "kind": "port", "value_1core": round(nframes_1core / dt1, 3),
-            "host_logical_cpus": ncpu, "host_cpu_model": model,
+            "host_logical_cpus": ncpu, "host_affinity_cpus": len(os.sched_getaffinity(0)),
+            "host_cpu_model": model,
             "sample": ("%d synthetic 1241x376 frames (ORBextractor 2000 feat/8 lvl), oracle/ C "
                        "restatement -O3, %d threads, %.1f s wall; 1 thread: %d frames, %.1f s"
                        % (nframes, threads, dt, nframes_1core, dt1))}
+
+
+def cpu_share():
+    """Host threads for the CPU baseline: the CPUs this process may run on
+    (os.sched_getaffinity), capped at the lease's CPU share when the environment states one
+    (OMP_NUM_THREADS: 16 on a 1-GPU box of this pool, whose sched_getaffinity shows the
+    whole machine)."""
+    n = len(os.sched_getaffinity(0))
+    share = os.environ.get("OMP_NUM_THREADS")
+    if share and share.isdigit() and int(share) > 0:
+        n = min(n, int(share))
+    return max(1, n)
 
 
 def host_cpu():
@@ -173,7 +190,8 @@ def cpu_baseline(frames, threads, nframes, nframes_1core=32):
     ncpu, model = host_cpu()
     return {"value": round(nframes / dt, 3), "unit": "frames/s", "cores": threads,
             "kind": "port", "value_1core": round(nframes_1core / dt1, 3),
-            "host_logical_cpus": ncpu, "host_cpu_model": model,
+            "host_logical_cpus": ncpu, "host_affinity_cpus": len(os.sched_getaffinity(0)),
+            "host_cpu_model": model,
             "sample": ("%d synthetic 1241x376 frames (extract 2000 feat/8 lvl + knn2 + "
                        "SearchForInitialization vs t-1), oracle/ C restatement -O3, %d pthreads, "
                        "%.1f s wall; 1 thread: %d frames, %.1f s"
@@ -189,7 +207,13 @@ def main():
                     help="frames (stereo: L/R pairs) per GPU per step; default 512 (stereo 256 "
                          "pairs = 512 images): +3.3%% frames/s over 256, the fixed cost of a "
                          "step's dependent launches spread over twice the frames")
-    ap.add_argument("--cpu-threads", type=int, default=int(os.environ.get("OMP_NUM_THREADS", "16")))
+    ap.add_argument("--blocks", type=int, default=4,
+                    help="distinct resident input blocks the steps cycle through (4 x 239 MB "
+                         "> the 256 MB Infinity Cache: every step reads new frames); 1 = the "
+                         "same block every step (round 2's bench)")
+    ap.add_argument("--cpu-threads", type=int, default=0,
+                    help="0: the host CPUs this process may run on (os.sched_getaffinity), "
+                         "capped at the lease's CPU share (OMP_NUM_THREADS, 16 on a 1-GPU box)")
     ap.add_argument("--cpu-frames", type=int, default=0, help="0: 256 x threads (~10-20 s)")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-kernel-timing", action="store_true")
@@ -210,23 +234,39 @@ def main():
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     torch.cuda.set_device(local)
+    dist_info = {"world_size": 1, "backend": None}
     if world > 1:
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        # what the collectives really run on (RCCL reports itself as "nccl" on ROCm)
+        dist_info = {"world_size": dist.get_world_size(), "backend": dist.get_backend(),
+                     "rccl": torch.cuda.nccl.version() if hasattr(torch.cuda, "nccl") else None}
+    if not args.cpu_threads:
+        args.cpu_threads = cpu_share()
 
     B = args.batch or (256 if args.stereo else 512)
+    # Streamed input: the step cycles through `nblocks` distinct resident blocks of the
+    # sequence (nblocks x 239 MB > the 256 MB Infinity Cache at the defaults), so every step
+    # reads frames the previous steps did not (no cross-step cache reuse of the input).
+    nblocks = max(1, args.blocks)
     if args.stereo:
-        lefts, rights, _ = synthetic.stereo_sequence(B, H, W, seed=synthetic.DEFAULT_SEED + 1000 * rank)
-        frames = np.empty((2 * B, H, W), np.uint8)
-        frames[0::2], frames[1::2] = lefts, rights
+        lefts, rights, _ = synthetic.stereo_sequence(nblocks * B, H, W,
+                                                     seed=synthetic.DEFAULT_SEED + 1000 * rank)
+        blocks = []
+        for k in range(nblocks):
+            fr = np.empty((2 * B, H, W), np.uint8)
+            fr[0::2], fr[1::2] = lefts[k * B:(k + 1) * B], rights[k * B:(k + 1) * B]
+            blocks.append(fr)
     else:
-        # batched-sequence partition (sequence.run_sharded): rank r owns frames
-        # [r*B, (r+1)*B) of one cyclic B*world-frame sequence and extracts them plus the frame
-        # before the block (1-frame halo), so its B pairs (t-1, t) match with no exchange
-        frames = synthetic.sequence_block(B * world, rank * B, (rank + 1) * B, H, W)
+        # batched-sequence partition (sequence.run_sharded): rank r's block k
+        # holds frames [(k world + r) B, (k world + r + 1) B) of one cyclic sequence plus the
+        # frame before it (1-frame halo), so its B pairs (t-1, t) match with no exchange
+        n_total, ranges = synthetic.bench_block_ranges(B, world, rank, nblocks)
+        blocks = synthetic.sequence_blocks(n_total, ranges, H, W)
         if args.extract_only:  # no pairs: the halo frame is not needed
-            frames = np.ascontiguousarray(frames[1:])
+            blocks = [np.ascontiguousarray(b[1:]) for b in blocks]
+    frames = blocks[0]
     nimg = len(frames)
-    d_frames = torch.from_numpy(frames).to("cuda")
+    d_blocks = [torch.from_numpy(b).to("cuda") for b in blocks]
     torch.cuda.synchronize()
     ext = ORBextractor(NFEAT, 1.2, NLEV, 20, 7, device=local, max_batch=nimg)
     # one non-null torch stream for everything: liborbg's kernels, the summary and RCCL
@@ -235,42 +275,15 @@ def main():
     torch.cuda.set_stream(stream)
     ext.ctx.set_stream(stream.cuda_stream)
     ext.ctx.set_pipeline(bool(args.pipeline))
-    f1 = np.arange(B, dtype=np.int32)        # local frame i (0 = the halo) ...
-    f2 = np.arange(1, B + 1, dtype=np.int32)  # ... matched to frame i + 1
-    summary = torch.zeros(2 * B + 1, dtype=torch.int32, device="cuda")
-    m12 = None
-    # matching of step k (and its summary + gather) runs on liborbg's match stream while the
-    # extraction of step k+1 runs on `stream` (two output slots inside liborbg)
-    mstream = torch.cuda.ExternalStream(ext.ctx.match_stream())
+    mode = "stereo" if args.stereo else "extract" if args.extract_only else "mono"
+    bstep = sequence.BenchStep(ext, B, mode, world=world)
     torch.cuda.synchronize()
-
-    sl, sr = np.arange(B) * 2, np.arange(B) * 2 + 1
-    ssum = torch.zeros(2 * B, dtype=torch.int32, device="cuda")
+    it = [0]
 
     def step():
-        if args.stereo:
-            ext.extract_batch_device(d_frames.data_ptr(), nimg, W, H)
-            ext.stereo_batch_device(sl, sr, synthetic.KITTI_BF,
-                                    synthetic.KITTI_BF / synthetic.KITTI_FX)
-            ext.ctx.stereo_summary(ssum.data_ptr())
-            if world > 1:  # per-frame (keypoints, depths) of every rank (RCCL all_gather)
-                sequence.gather_summary(ssum.view(2, B), world, sizes=[B] * world)
-            return
-        nonlocal m12
-        if args.extract_only:
-            ext.extract_batch_device(d_frames.data_ptr(), nimg, W, H)
-            return
-        ext.extract_batch_device(d_frames.data_ptr(), nimg, W, H)
-        ext.match_batch_device(f1, f2, 100, 0.9, True)
-        ext.ctx.batch_summary(summary.data_ptr())
-        if m12 is None:
-            m12 = torch.empty((B, ext.ctx.batch_matches(None)), dtype=torch.int32, device="cuda")
-        ext.ctx.batch_matches(m12.data_ptr())  # vnMatches12 rows of the B pairs
-        if world > 1:  # per-frame outputs of every rank (RCCL all_gather)
-            with torch.cuda.stream(mstream):
-                local = torch.stack([summary[1:B + 1], summary[B + 1:]])
-                sequence.gather_summary(local, world, sizes=[B] * world)
-                sequence.gather_rows(m12, world, sizes=[B] * world)
+        d = d_blocks[it[0] % nblocks]
+        it[0] += 1
+        bstep(d.data_ptr(), W, H)
 
     for _ in range(args.warmup):
         step()
@@ -304,17 +317,16 @@ def main():
         ext.ctx.set_serial(True)
 
         def step_serial():
+            d = d_blocks[it[0] % nblocks]
+            it[0] += 1
+            ext.extract_batch_device(d.data_ptr(), nimg, W, H)
             if args.stereo:
-                ext.extract_batch_device(d_frames.data_ptr(), nimg, W, H)
                 ext.ctx.sync()
-                ext.stereo_batch_device(sl, sr, synthetic.KITTI_BF,
+                ext.stereo_batch_device(bstep.sl, bstep.sr, synthetic.KITTI_BF,
                                         synthetic.KITTI_BF / synthetic.KITTI_FX)
-            elif args.extract_only:
-                ext.extract_batch_device(d_frames.data_ptr(), nimg, W, H)
-            else:
-                ext.extract_batch_device(d_frames.data_ptr(), nimg, W, H)
+            elif not args.extract_only:
                 ext.ctx.sync()
-                ext.match_batch_device(f1, f2, 100, 0.9, True)
+                ext.match_batch_device(bstep.f1, bstep.f2, 100, 0.9, True)
             ext.ctx.sync()
 
         step_serial()
@@ -387,9 +399,16 @@ def main():
                 "workload": workload,
                 "frames_per_gpu_per_step": B, "global_batch": B * world, "width": W,
                 "pipelined_batches": bool(args.pipeline),
+                "input_blocks": nblocks,
+                "input_reuse": ("none within %d steps: the step cycles through %d resident "
+                                "blocks of %.0f MB (%.0f MB in all, > the 256 MB Infinity "
+                                "Cache)" % (nblocks, nblocks, nimg * W * H / 1e6,
+                                            nblocks * nimg * W * H / 1e6)
+                                if nblocks > 1 else "the same resident block every step"),
                 "height": H, "nfeatures": NFEAT, "nlevels": NLEV,
                 "parallelism": "frames sharded over %d GPU(s), RCCL all_gather of per-frame "
                                "summary" % world},
+            "dist": dist_info,
             "roofline": roof,
             "pipeline_roofline": {"algo_bytes_per_frame": fab,
                                   "achieved_GBps": round(value * fab / 1e9, 1),

@@ -174,9 +174,11 @@ int orbg_download_matches(orbg_ctx *ctx, int pair, int32_t *knn, int32_t *matche
  * last batch: row-band descriptor match, 11x11 SAD refinement at the keypoint's level,
  * parabola, median cut.  bf = Frame::mbf; min_z = Frame::mb, which the reference reads before
  * assigning it (Frame.cc:661 vs :148) -- pass bf / fx, the value assigned right after
- * (min_z <= 0: no maximum disparity).  Runs on the context stream (it reads this batch's
- * pyramid).  Results per pair over the left frame's keypoints: mvuRight, mvDepth (-1 where
- * unmatched) and the number of depths. */
+ * (min_z <= 0: no maximum disparity).  Runs where the batch's keypoint half ran (it reads
+ * this batch's pyramid): the context stream, or with pipelined batches the internal back
+ * stream.  Results per pair over the left frame's keypoints: mvuRight, mvDepth (-1 where
+ * unmatched) and the number of depths; device readers order themselves after the match
+ * stream via orbg_stereo_summary, or call orbg_sync. */
 int orbg_stereo_batch_device(orbg_ctx *ctx, const int32_t *left, const int32_t *right,
                              int npairs, float bf, float min_z);
 int orbg_stereo_outputs(orbg_ctx *ctx, float **d_uright /* [npairs][frame_cap] */,
@@ -190,8 +192,10 @@ int orbg_stereo_frame(orbg_ctx *ctx, const uint8_t *left, const uint8_t *right, 
                       size_t step, float bf, float min_z, orbg_keypoint *kps_l, uint8_t *desc_l,
                       int cap_l, int *n_l, orbg_keypoint *kps_r, uint8_t *desc_r, int cap_r,
                       int *n_r, float *uright, float *depth);
-/* per-pair summary on the context stream into a device buffer: d_out[p] = keypoints of the
- * left frame of pair p, d_out[npairs + p] = keypoints with a depth */
+/* per-pair summary of the last stereo batch, written on the match stream (orbg_match_stream,
+ * ordered after the stereo pass, as orbg_batch_summary) into a device buffer: order readers
+ * after the match stream, or orbg_sync.  d_out[p] = keypoints of the left frame of pair p,
+ * d_out[npairs + p] = keypoints with a depth */
 int orbg_stereo_summary(orbg_ctx *ctx, int32_t *d_out);
 /* copies cap entries of pair `pair` (synchronises) */
 int orbg_download_stereo(orbg_ctx *ctx, int pair, float *uright, float *depth, int cap,
@@ -231,6 +235,16 @@ int orbg_set_serial(orbg_ctx *ctx, int enable);
  * d_out[nframes + p] = SearchForInitialization matches of pair p (p < npairs of the last
  * orbg_match_batch_device, 0 if none) */
 int orbg_batch_summary(orbg_ctx *ctx, int32_t *d_out);
+/* Caller reads of the last batch's device outputs (orbg_batch_outputs, and
+ * orbg_stereo_outputs after a stereo pass) on a caller stream (NULL: the match stream), for
+ * pipelined batches where they are written on internal streams:
+ *   orbg_batch_acquire: `stream` waits until those outputs are written;
+ *   orbg_batch_release: every read enqueued on `stream` so far finishes before liborbg
+ *   overwrites those outputs (the extraction that reuses the output slot, the next stereo
+ *   pass wait for it).
+ * Enqueue only; no host synchronisation. */
+int orbg_batch_acquire(orbg_ctx *ctx, void *stream);
+int orbg_batch_release(orbg_ctx *ctx, void *stream);
 /* vnMatches12 of every pair of the last orbg_match_batch_device (ORBmatcher.cc:487-631's
  * output; the batched-sequence gather of SURVEY 8e), written on the match stream into a
  * device buffer: d_out[p * frame_cap + i] = index in frame f2[p] matched to keypoint i of

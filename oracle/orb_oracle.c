@@ -1132,6 +1132,11 @@ typedef struct {
     int w, h, f0, f1, nframes, window;
     float nnratio;
     int32_t *nkp, *nmatch;
+    /* optional full outputs (orc_frames_full), frame f at f * cap_out */
+    int cap_out;
+    orc_keypoint *kps_out;
+    uint8_t *desc_out;
+    int32_t *knn_out, *m12_out;
 } frames_job;
 
 static void *frames_worker(void *arg)
@@ -1168,6 +1173,23 @@ static void *frames_worker(void *arg)
             j->nkp[f] = n[cur];
         if (j->nmatch)
             j->nmatch[f] = nm;
+        if (j->cap_out > 0) {
+            const size_t o = (size_t)f * j->cap_out;
+            const int nc = n[cur] < j->cap_out ? n[cur] : j->cap_out;
+            const int np = n[pv] < j->cap_out ? n[pv] : j->cap_out;
+            if (j->kps_out)
+                memcpy(j->kps_out + o, k[cur], sizeof(orc_keypoint) * nc);
+            if (j->desc_out)
+                memcpy(j->desc_out + o * 32, d[cur], (size_t)nc * 32);
+            if (j->knn_out)
+                for (int i = 0; i < nc; i++) {
+                    j->knn_out[(o + i) * 3] = bi[i];
+                    j->knn_out[(o + i) * 3 + 1] = bi[cap + i];
+                    j->knn_out[(o + i) * 3 + 2] = bi[2 * cap + i];
+                }
+            if (j->m12_out)
+                memcpy(j->m12_out + o, bi + 3 * cap, sizeof(int32_t) * np);
+        }
         cur ^= 1;
     }
     for (int s = 0; s < 2; s++) {
@@ -1179,8 +1201,10 @@ static void *frames_worker(void *arg)
     return NULL;
 }
 
-int orc_frames_batch(const orc_params *p, const uint8_t *imgs, int nframes, int w, int h,
-                     int nthreads, int window, float nnratio, int32_t *nkp, int32_t *nmatch)
+int orc_frames_full(const orc_params *p, const uint8_t *imgs, int nframes, int w, int h,
+                    int nthreads, int window, float nnratio, int32_t *nkp, int32_t *nmatch,
+                    int cap_out, orc_keypoint *kps_out, uint8_t *desc_out, int32_t *knn_out,
+                    int32_t *m12_out)
 {
     if (nframes <= 0)
         return 0;
@@ -1204,9 +1228,21 @@ int orc_frames_batch(const orc_params *p, const uint8_t *imgs, int nframes, int 
         jobs[t].nnratio = nnratio;
         jobs[t].nkp = nkp;
         jobs[t].nmatch = nmatch;
+        jobs[t].cap_out = cap_out;
+        jobs[t].kps_out = kps_out;
+        jobs[t].desc_out = desc_out;
+        jobs[t].knn_out = knn_out;
+        jobs[t].m12_out = m12_out;
         pthread_create(&th[t], NULL, frames_worker, &jobs[t]);
     }
     for (int t = 0; t < nthreads; t++)
         pthread_join(th[t], NULL);
     return nframes;
+}
+
+int orc_frames_batch(const orc_params *p, const uint8_t *imgs, int nframes, int w, int h,
+                     int nthreads, int window, float nnratio, int32_t *nkp, int32_t *nmatch)
+{
+    return orc_frames_full(p, imgs, nframes, w, h, nthreads, window, nnratio, nkp, nmatch, 0,
+                           NULL, NULL, NULL, NULL);
 }

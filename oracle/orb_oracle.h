@@ -132,6 +132,14 @@ long orc_extract_batch(const orc_params *p, const uint8_t *imgs, int nframes, in
 /* frames = extract(t) + knn2(t, t-1) + SearchForInitialization(t-1 -> t); pthreads */
 int orc_frames_batch(const orc_params *p, const uint8_t *imgs, int nframes, int w, int h,
                      int nthreads, int window, float nnratio, int32_t *nkp, int32_t *nmatch);
+/* orc_frames_batch with every output kept: frame f's keypoints / descriptors at
+ * f * cap_out (nkp[f] of them), its knn2 triples {best idx, best, second} over frame f-1
+ * (cyclic) at (f * cap_out + i) * 3, and vnMatches12 of the pair (f-1, f) over frame f-1's
+ * keypoints at f * cap_out (nkp[f-1] of them).  Any output pointer may be NULL. */
+int orc_frames_full(const orc_params *p, const uint8_t *imgs, int nframes, int w, int h,
+                    int nthreads, int window, float nnratio, int32_t *nkp, int32_t *nmatch,
+                    int cap_out, orc_keypoint *kps_out, uint8_t *desc_out, int32_t *knn_out,
+                    int32_t *m12_out);
 
 /* ---- matcher ---- */
 int orc_descriptor_distance(const uint8_t *a, const uint8_t *b);

@@ -140,6 +140,8 @@ def lib():
                                                     C.c_int]
         L.orc_frames_batch.argtypes = [P(Params), vp, C.c_int, C.c_int, C.c_int, C.c_int,
                                        C.c_int, C.c_float, vp, vp]
+        L.orc_frames_full.argtypes = [P(Params), vp, C.c_int, C.c_int, C.c_int, C.c_int,
+                                      C.c_int, C.c_float, vp, vp, C.c_int, vp, vp, vp, vp]
         L.orc_extract_batch.argtypes = [P(Params), vp, C.c_int, C.c_int, C.c_int, C.c_int, vp]
         L.orc_extract_batch.restype = C.c_long
         L.orc_ba_linearize.argtypes = [vp, C.c_int, vp, C.c_int, vp, C.c_int, vp, vp, vp, vp, vp]
@@ -378,6 +380,28 @@ def frames_batch(p, imgs, nthreads=1, window=100, nnratio=0.9):
     lib().orc_frames_batch(C.byref(p), _p(imgs), nf, w, h, nthreads, window, nnratio, _p(nkp),
                            _p(nm))
     return nkp, nm
+
+
+def frames_full(p, imgs, nthreads=1, window=100, nnratio=0.9):
+    """The bench unit on every frame of `imgs`, every output kept (orc_frames_full): frame f
+    is extracted and matched against frame f-1 (cyclic: frame 0 against the last).  Returns
+    (nkp[f], nmatches[f], kps[f] (list of KP_DTYPE arrays), desc[f], knn[f] (nkp[f] x 3:
+    best idx, best, second over frame f-1), m12[f] (vnMatches12 of pair (f-1, f), nkp[f-1]
+    entries))."""
+    imgs = np.ascontiguousarray(imgs, np.uint8)
+    nf, h, w = imgs.shape
+    cap = 2 * p.nfeatures + 256
+    nkp = np.zeros(nf, np.int32)
+    nm = np.zeros(nf, np.int32)
+    kps = np.zeros((nf, cap), KP_DTYPE)
+    desc = np.zeros((nf, cap, 32), np.uint8)
+    knn = np.zeros((nf, cap, 3), np.int32)
+    m12 = np.zeros((nf, cap), np.int32)
+    lib().orc_frames_full(C.byref(p), _p(imgs), nf, w, h, nthreads, window, nnratio, _p(nkp),
+                          _p(nm), cap, _p(kps), _p(desc), _p(knn), _p(m12))
+    return (nkp, nm, [kps[f, :nkp[f]] for f in range(nf)], [desc[f, :nkp[f]] for f in range(nf)],
+            [knn[f, :nkp[f]] for f in range(nf)],
+            [m12[f, :nkp[(f - 1) % nf]] for f in range(nf)])
 
 
 def ba_linearize(poses, points, edges):

@@ -147,6 +147,8 @@ def lib():
         "orbg_get_pipeline": (i32, [vp]),
         "orbg_batch_summary": (i32, [vp, vp]),
         "orbg_batch_matches": (i32, [vp, vp, vp]),
+        "orbg_batch_acquire": (i32, [vp, vp]),
+        "orbg_batch_release": (i32, [vp, vp]),
         "orbg_stereo_batch_device": (i32, [vp, vp, vp, i32, f32, f32]),
         "orbg_stereo_outputs": (i32, [vp, vp, vp, vp, vp]),
         "orbg_stereo_summary": (i32, [vp, vp]),
@@ -310,6 +312,18 @@ class Context:
         check(self._L.orbg_batch_matches(self.handle, C.c_void_p(d_out_ptr) if d_out_ptr else None,
                                          C.byref(fc)), "orbg_batch_matches")
         return fc.value
+
+    def batch_acquire(self, stream_ptr=None):
+        """Make `stream` (None: the match stream) wait until the last batch's device
+        outputs (and stereo outputs) are written (orbg_batch_acquire)."""
+        check(self._L.orbg_batch_acquire(self.handle, C.c_void_p(stream_ptr) if stream_ptr else None),
+              "orbg_batch_acquire")
+
+    def batch_release(self, stream_ptr=None):
+        """Reads of those outputs enqueued on `stream` so far finish before liborbg
+        overwrites them (orbg_batch_release)."""
+        check(self._L.orbg_batch_release(self.handle, C.c_void_p(stream_ptr) if stream_ptr else None),
+              "orbg_batch_release")
 
     def batch_summary(self, d_out_ptr):
         check(self._L.orbg_batch_summary(self.handle, C.c_void_p(d_out_ptr)), "orbg_batch_summary")

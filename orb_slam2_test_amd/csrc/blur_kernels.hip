@@ -1,7 +1,8 @@
 // blur_kernels.hip -- k_blur2: GaussianBlur(7x7, sigma 2, BORDER_REFLECT_101) of every pyramid
 // level (ORBextractor.cc:1375-1377, cv::GaussianBlur 8U bit-exact fixed point:
-// out = sat((sum_v k_v * sum_h k_h * p + 2^15) >> 16)), same bytes as k_blur
-// (extract_kernels.hip), without LDS and without workgroup barriers.
+// out = sat((sum_v k_v * sum_h k_h * p + 2^15) >> 16)), without LDS and without workgroup
+// barriers.  Levels are >= 62 px wide (the plan refuses a level narrower than one 30-px cell
+// plus the borders), so the row-end permutes always have the 8 bytes they assume.
 //
 // One wave owns a 244-column x SEG-row output tile of one (frame, level); lane j owns columns
 // gx .. gx+3 (gx = tile x + 4j; lanes 61..63 only supply data) and walks the SEG + 6 source
@@ -61,7 +62,7 @@ struct Blur2Weights {
                        k4 = g->gk[4], k5 = g->gk[5];
         k6 = g->gk[6];
         norm256 = k0 + k1 + k2 + k3 + k4 + k5 + k6 == 256u;
-        // row pass weight words (as k_blur): output x = gx + i needs window bytes 1+i .. 7+i
+        // row pass weight words: output x = gx + i needs window bytes 1+i .. 7+i
         K00 = k0 << 8 | k1 << 16 | k2 << 24;
         K01 = k3 | k4 << 8 | k5 << 16 | k6 << 24;
         K10 = k0 << 16 | k1 << 24;

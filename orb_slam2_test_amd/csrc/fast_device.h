@@ -1,5 +1,5 @@
-// fast_device.h -- FAST-9 device helpers shared by k_fast_cells (extract_kernels.hip) and
-// k_fast2 (fast_kernels.hip): packed u16 pixel-pair gathers and the cornerScore<16> arc
+// fast_device.h -- FAST-9 device helpers of k_fast2 (fast_kernels.hip): packed u16
+// pixel-pair gathers and the cornerScore<16> arc
 // extremes (cv::FAST TYPE_9_16).
 #pragma once
 

@@ -1,7 +1,7 @@
 // fast_kernels.hip -- k_fast2: the FAST part of ComputeKeyPointsOctTree (ORBextractor.cc:
 // 966-1094: 30-px cells, cv::FAST(window, iniThFAST, NMS), minThFAST retry of empty cells,
-// kp.pt += (j * wCell, i * hCell)) for gfx950.  Same outputs, bit for bit, as k_fast_cells
-// (extract_kernels.hip), which stays as the fallback for LDS pitches not instantiated here.
+// kp.pt += (j * wCell, i * hCell)) for gfx950.  Every cell window of the reference's 30-px
+// grid (< 66 x 66 px) fits one of the instantiated LDS pitches.
 //
 // The kernel is VALU-issue bound (round-2 counters: ~70% of SIMD cycles issue VALU), so this
 // version cuts instructions:
@@ -306,7 +306,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(FC2_WPE, 8)
     wave_sync_lds();
     if (dbg == 12) continue;
 
-    // ---- NMS (cell-local) + raster-order compaction, as k_fast_cells ----
+    // ---- NMS (cell-local) + raster-order compaction ----
     // cv::FAST keeps p iff s_p > every neighbour's score, a neighbour that is not a corner
     // at the cell threshold th counting as 0; with s_p >= max(th, 1) that is exactly
     //   max(raw 8-neighbour scores) < max(th, s_p).
@@ -442,7 +442,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(FC2_WPE, 8)
     }  // cells of this wave
 }
 
-// instantiated LDS pitches (dwords); the host plan picks one, else k_fast_cells
+// instantiated LDS pitches (dwords); the host plan picks one
 #define ORBG_FAST2_PITCHES(X) X(12) X(14) X(16) X(18) X(20) X(22) X(24) X(26) X(28) X(32)
 
 bool fast2_pitch_ok(int p4)

@@ -2,8 +2,8 @@
 //
 //   k_knn2_*          brute-force 2-NN over ORBmatcher::DescriptorDistance
 //                     (ORBmatcher.cc:1846-1862; best/second update rule :541-556) on the
-//                     matrix cores: bits expanded to +-1 i8, v_mfma_i32_32x32x32_i8 dot
-//                     products (= 256 - 2 x distance), top-2 keys per query.
+//                     matrix cores: bits expanded to +-1.0 e2m1, v_mfma_scale_f32_32x32x64_f8f6f4
+//                     dot products (affine in the distance), top-2 keys per query.
 //   k_init_cands      SearchForInitialization's data-parallel part (ORBmatcher.cc:508-545):
 //                     per level-0 query, the window candidates of F2.GetFeaturesInArea
 //                     (Frame.cc:421-504) with their distances, kept as the K smallest
@@ -34,17 +34,9 @@ bool prof_skip_name(const char *n);
 #define TH_LOW 50
 #define HISTO_LENGTH 30
 
-// knn2 on the matrix cores.  Every descriptor bit b becomes an i8: +-64 (train, A operand:
-// b=1 -> +64) or -+64 (query, B operand: b=1 -> -64), so one product is -4096 where the bits
-// agree and +4096 where they differ, and the 256-bit dot product is
-// 4096 * (d - (256 - d)) = 8192 d - 2^20, exact in the i32 accumulator of
-// v_mfma_i32_32x32x32_i8 (eight MFMAs, K = 256, per 32 x 32 block of DescriptorDistance
-// values).  The MFMA's C input carries the train index (< 8192) in the 13 free low bits, so
-// the accumulator IS the key  d << 13 | index  (offset by -2^20): no VALU work to form it.
-// A = 32 train descriptors (expanded once per tile into LDS, shared by the four waves), B =
-// 32 query descriptors (expanded once into registers).  The MFMA's k order is irrelevant as
-// long as A and B use the same bit -> (step, lane half, element) assignment: step s, half h,
-// dword q holds bit plane 4h+q of descriptor dword s (bits 4h+q, +8, +16, +24), one per byte.
+// knn2 on the matrix cores: every 256-bit DescriptorDistance of a 32 x 32 block of (train,
+// query) pairs is one MFMA dot product of +-1 bit vectors, offset so that the accumulator IS
+// the key  d << 13 | train index  (k_knn2_* below; the train index fits the 13 low bits).
 //
 // best/second (ORBmatcher.cc:541-556's strict-< scan in train order): the smallest key is
 // (min distance, first index); the distance of the second smallest key is the multiset
@@ -53,17 +45,8 @@ bool prof_skip_name(const char *n);
 typedef int knn_v4i __attribute__((ext_vector_type(4)));
 typedef int knn_v16i __attribute__((ext_vector_type(16)));
 
-#define KNN_ROWB 272         // expanded train row: 256 B + 16 B pad (rows 4 banks apart)
 #define KNN_MAX_TRAIN 8192   // train index in the 13 low key bits
 #define KNN_NONE 0x40000000  // C tag of the rows past nt: keys above any real one
-
-// bytes of bit plane p of x (bytes 0..3 take bits p, p+8, p+16, p+24) through a 2-entry LUT
-__device__ __forceinline__ uint32_t knn_plane(uint32_t x, int p, uint32_t lut)
-{
-    return __builtin_amdgcn_perm(0u, lut, (x >> p) & 0x01010101u);
-}
-#define KNN_LUT_A 0x000040C0u  // train: 0 -> -64, 1 -> +64
-#define KNN_LUT_B 0x0000C040u  // query: 0 -> +64, 1 -> -64
 
 // key is read straight out of the MFMA result, so everything here stays compiler-visible (the
 // compiler places the MFMA -> VALU wait states; it does not for inline asm).  Three VOP2
@@ -74,132 +57,9 @@ __device__ __forceinline__ void knn_key_update(int key, int &k1, int &k2)
     k1 = min(k1, key);
 }
 
-// one 256-thread block: queries q[qbase .. qbase + 256) (64 per wave, two 32-query tiles),
-// all nt (< KNN_MAX_TRAIN) train descriptors in stages of 64 rows (two 32-row subtiles, one
-// barrier per stage).  Software-pipelined: the top-2 epilogue of subtile i runs beside the
-// MFMAs of subtile i+1 (two accumulator sets), so the matrix pipe and the VALU overlap
-// inside one wave.
-__device__ __forceinline__ void knn2_block(const uint8_t *__restrict__ q, int nq,
-                                           const uint8_t *__restrict__ t, int nt,
-                                           int32_t *__restrict__ out, int qbase)
-{
-    __shared__ __attribute__((aligned(16))) uint8_t tile[2][64 * KNN_ROWB];
-    const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
-    const int col = lane & 31, h = lane >> 5;
-    // B fragments: query qbase + 64 wv + 32 u + col, step s: planes 4h .. 4h+3 of dword s
-    knn_v4i bq[2][8];
-#pragma unroll
-    for (int u = 0; u < 2; u++) {
-        const int qi = qbase + wv * 64 + u * 32 + col;
-        uint32_t x[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-        if (qi < nq) {
-            const uint4 *p = (const uint4 *)(q + (size_t)qi * 32);
-            const uint4 a = p[0], c = p[1];
-            x[0] = a.x; x[1] = a.y; x[2] = a.z; x[3] = a.w;
-            x[4] = c.x; x[5] = c.y; x[6] = c.z; x[7] = c.w;
-        }
-#pragma unroll
-        for (int st = 0; st < 8; st++)
-#pragma unroll
-            for (int qd = 0; qd < 4; qd++) bq[u][st][qd] = (int)knn_plane(x[st], 4 * h + qd, KNN_LUT_B);
-    }
-    // C/D map: register r of lane holds row (r & 3) + 8 (r >> 2) + 4h, column col.  The C
-    // input (ctag) is the train index of the row, KNN_NONE past nt; built per subtile from
-    // one VGPR (tb + 4h) plus inline constants, so it is live only into the first MFMA
-    int k1[2] = {INT_MAX, INT_MAX}, k2[2] = {INT_MAX, INT_MAX};
-
-    // expansion of stage s0 (64 rows) into buffer bf: thread -> rows (tid >> 3) and
-    // (tid >> 3) + 32, dword tid & 7; the raw dwords are fetched one stage ahead
-    const int er = tid >> 3, esd = tid & 7;
-    // branch-free (clamped row; rows past nt carry KNN_NONE tags), so the load stays in
-    // flight until the next stage's expand instead of being waited for at a branch join
-    auto fetch1 = [&](int row) -> uint32_t {
-        return ((const uint32_t *)(t + (size_t)min(row, nt - 1) * 32))[esd];
-    };
-    auto expand1 = [&](uint32_t x, uint8_t *dst) {
-        uint4 lo, hi;
-        lo.x = knn_plane(x, 0, KNN_LUT_A); lo.y = knn_plane(x, 1, KNN_LUT_A);
-        lo.z = knn_plane(x, 2, KNN_LUT_A); lo.w = knn_plane(x, 3, KNN_LUT_A);
-        hi.x = knn_plane(x, 4, KNN_LUT_A); hi.y = knn_plane(x, 5, KNN_LUT_A);
-        hi.z = knn_plane(x, 6, KNN_LUT_A); hi.w = knn_plane(x, 7, KNN_LUT_A);
-        ((uint4 *)dst)[0] = lo;
-        ((uint4 *)dst)[1] = hi;
-    };
-    auto expand = [&](uint32_t x0, uint32_t x1, int bf) {
-        expand1(x0, tile[bf] + er * KNN_ROWB + esd * 32);
-        expand1(x1, tile[bf] + (er + 32) * KNN_ROWB + esd * 32);
-    };
-    uint32_t xr0 = 0, xr1 = 0;
-    if (nt > 0) {
-        expand(fetch1(er), fetch1(er + 32), 0);
-        xr0 = fetch1(64 + er);
-        xr1 = fetch1(96 + er);
-    }
-    knn_v16i pacc[2];  // previous subtile's accumulators, epilogue pending
-    bool pend = false;
-    auto epilogue = [&]() {
-#pragma unroll
-        for (int r = 0; r < 16; r++) {
-            knn_key_update(pacc[0][r], k1[0], k2[0]);
-            knn_key_update(pacc[1][r], k1[1], k2[1]);
-        }
-    };
-    for (int s0 = 0, bf = 0; s0 < nt; s0 += 64, bf ^= 1) {
-        __syncthreads();
-        if (s0 + 64 < nt) {
-            expand(xr0, xr1, bf ^ 1);
-            xr0 = fetch1(s0 + 128 + er);
-            xr1 = fetch1(s0 + 160 + er);
-        }
-#pragma unroll
-        for (int sub = 0; sub < 2; sub++) {
-            const int tb = s0 + 32 * sub;
-            if (tb >= nt) break;
-            knn_v16i ctag;
-            const int tbh = tb + 4 * h;
-#pragma unroll
-            for (int r = 0; r < 16; r++) ctag[r] = tbh + (r & 3) + 8 * (r >> 2);
-            if (tb + 32 > nt) {  // last subtile: rows past nt get keys above every real one
-#pragma unroll
-                for (int r = 0; r < 16; r++)
-                    if (ctag[r] >= nt) ctag[r] = KNN_NONE;
-            }
-            knn_v16i acc[2];
-            const uint8_t *arow = tile[bf] + (32 * sub + col) * KNN_ROWB + h * 16;
-#pragma unroll
-            for (int st = 0; st < 8; st++) {
-                const knn_v4i a = *(const knn_v4i *)(arow + st * 32);
-                acc[0] = __builtin_amdgcn_mfma_i32_32x32x32_i8(a, bq[0][st], st ? acc[0] : ctag, 0, 0, 0);
-                acc[1] = __builtin_amdgcn_mfma_i32_32x32x32_i8(a, bq[1][st], st ? acc[1] : ctag, 0, 0, 0);
-            }
-            if (pend) epilogue();
-            pacc[0] = acc[0];
-            pacc[1] = acc[1];
-            pend = true;
-        }
-    }
-    if (pend) epilogue();
-    // lanes col and col + 32 hold the two row halves of the same queries; keys are
-    // 8192 d - 2^20 + index, anything at or above KNN_NONE - 2^20 is no train row
-#pragma unroll
-    for (int u = 0; u < 2; u++) {
-        const int o1 = __shfl_xor(k1[u], 32, 64), o2 = __shfl_xor(k2[u], 32, 64);
-        const int b1 = min(k1[u], o1);
-        const int b2 = min(min(k2[u], o2), max(k1[u], o1));
-        const int qi = qbase + wv * 64 + u * 32 + col;
-        if (h == 0 && qi < nq) {
-            const bool v1 = b1 < KNN_NONE - (1 << 20), v2 = b2 < KNN_NONE - (1 << 20);
-            const int e1 = b1 + (1 << 20), e2 = b2 + (1 << 20);
-            out[(size_t)qi * 3 + 0] = v1 ? (e1 & (KNN_MAX_TRAIN - 1)) : -1;
-            out[(size_t)qi * 3 + 1] = v1 ? (e1 >> 13) : INT_MAX;
-            out[(size_t)qi * 3 + 2] = v2 ? (e2 >> 13) : INT_MAX;
-        }
-    }
-}
-
-// knn2 on the fp4 matrix cores (default).  Same keys as knn2_block, at twice the i8 rate:
-// v_mfma_scale_f32_32x32x64_f8f6f4 with e2m1 operands runs K = 64 in the cycles the i8 form
-// needs for K = 32, so K = 256 is four MFMAs instead of eight.  Every bit becomes +-1.0 in
+// knn2 on the fp4 matrix cores: v_mfma_scale_f32_32x32x64_f8f6f4 with e2m1 operands runs
+// K = 64 in the cycles the i8 form needs for K = 32, so K = 256 is four MFMAs (round 1's i8
+// v_mfma_i32_32x32x32_i8 form needed eight; removed in round 3).  Every bit becomes +-1.0 in
 // e2m1 (0x2 = +1, 0xA = -1): train (A) b=1 -> -1, query (B) b=1 -> +1 (b=0 the opposite), so
 // one product is -1 where the bits agree and +1 where they differ; the E8M0 scale 2^12 on A
 // makes the dot product 4096 (d - (256 - d)) = 8192 d - 2^20, and the C input is the train
@@ -367,11 +227,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4, 8))) voi
 {
     knn2_block_fp4(q, nq, t, nt, out, blockIdx.x * 256);
 }
-__global__ __launch_bounds__(256) void k_knn2_single_i8(const uint8_t *q, int nq, const uint8_t *t,
-                                                        int nt, int32_t *out)
-{
-    knn2_block(q, nq, t, nt, out, blockIdx.x * 256);
-}
 
 // batch: queries = F2 (current) keypoints of pair p, train = F1 (previous).  1-D grid of nbx
 // blocks per pair, remapped so one pair's blocks share an XCD (and the L2 copy of the train
@@ -391,22 +246,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4, 8))) voi
     int32_t *out)
 {
     KNN2_PAIRS_BODY(knn2_block_fp4)
-}
-__global__ __launch_bounds__(256) void k_knn2_pairs_i8(const uint8_t *desc, const int32_t *counts,
-                                                       int fc, const int32_t *f1,
-                                                       const int32_t *f2, int32_t *out)
-{
-    KNN2_PAIRS_BODY(knn2_block)
-}
-
-// ORBG_KNN_I8=1 selects the i8 MFMA kernel (developer A/B; same results)
-static bool knn_fp4()
-{
-    static const int v = [] {
-        const char *e = getenv("ORBG_KNN_I8");
-        return e && atoi(e) ? 0 : 1;
-    }();
-    return v != 0;
 }
 
 // ---------------------------------------------------------------------------
@@ -994,7 +833,7 @@ int launch_knn2(hipStream_t st, const uint8_t *q, int nq, const uint8_t *t, int 
 {
     if (nt >= KNN_MAX_TRAIN) return ORBG_ENOTSUP;  // caller chunks the train set
     PL(prof, st, "knn2",
-       hipLaunchKernelGGL(knn_fp4() ? k_knn2_single : k_knn2_single_i8,
+       hipLaunchKernelGGL(k_knn2_single,
                           dim3((nq + 255) / 256), dim3(256), 0, st, q, nq, t, nt, out));
     return hipGetLastError() == hipSuccess ? ORBG_OK : ORBG_EIO;
 }
@@ -1013,12 +852,12 @@ int launch_match_pairs(hipStream_t st, hipStream_t aux, hipEvent_t evf, hipEvent
                           dim3(256), 2 * cap0 * sizeof(F2Key), st, kps, desc, counts, fc, d_f1, d_f2,
                           w, h, window, (unsigned long long *)topk, topk_n, cap0));
     // knn2 (VALU bound) on `aux` beside init_resolve (one sequential workgroup per pair);
-    // serial == 1 (developer timing, ORBG_DBG=40) keeps it on `st`
+    // serial == 1 (orbg_set_serial: isolated kernel timing) keeps it on `st`
     if (serial) aux = st;
     if (hipEventRecord(evf, st) != hipSuccess || hipStreamWaitEvent(aux, evf, 0) != hipSuccess)
         return ORBG_EIO;
     PL(prof, aux, "knn2",
-       hipLaunchKernelGGL(knn_fp4() ? k_knn2_pairs : k_knn2_pairs_i8,
+       hipLaunchKernelGGL(k_knn2_pairs,
                           dim3((fc + 255) / 256 * npairs), dim3(256), 0, aux, desc, counts, fc,
                           d_f1, d_f2, knn));
     if (hipEventRecord(evj, aux) != hipSuccess) return ORBG_EIO;

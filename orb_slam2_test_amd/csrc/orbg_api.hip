@@ -5,6 +5,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <atomic>
 #include <cmath>
 #include <cstdarg>
 #include <cstdio>
@@ -26,10 +27,6 @@
 namespace orbg {
 __global__ void k_resize(const uint8_t *, int64_t, int, int, uint8_t *, int64_t, int, int, int,
                          const int2 *, const int2 *, int, int);
-__global__ void k_fast_cells(const OrbgGeom *, const OrbgCell *, const uint8_t *, int64_t, int,
-                             const uint8_t *, const uint32_t *, int32_t *, uint2 *, int, int, int);
-__global__ void k_blur(const OrbgGeom *, const int32_t *, const uint8_t *, int64_t, int,
-                       const uint8_t *, uint8_t *, int, int);
 __global__ void k_octree(const OrbgGeom *, const int32_t *, const uint2 *, uint32_t *,
                          uint32_t *, uint32_t *, uint8_t *, int4 *, uint32_t *, int32_t *,
                          int32_t *);
@@ -191,16 +188,22 @@ struct Prof {
 }  // namespace orbg
 
 // events on `st`, the stream the kernel is launched on (a local in every caller)
-// Developer what-if knob ORBG_SKIP=<names>: launches whose profile name is listed are not
-// issued (their consumers read the previous batch's buffers), so a bench run shows what a
-// kernel costs inside the overlapped pipeline.  Wrong results; never set in production.
-static int g_extract_batches = 0;  // batches issued (ORBG_SKIP_AFTER)
+// Developer what-if knob ORBG_SKIP=<names> (developer builds only, `make DEV=1` defines
+// ORBG_DEV_KNOBS): launches whose profile name is listed are not issued (their consumers
+// read the previous batch's buffers), so a bench run shows what a kernel costs inside the
+// overlapped pipeline.  Wrong results: a production build compiles it out and orbg_create
+// warns when the variable is set.
+#ifdef ORBG_DEV_KNOBS
+static std::atomic<int> g_extract_batches{0};  // batches issued, all contexts (ORBG_SKIP_AFTER)
 static bool prof_skip(const char *name)
 {
     static const char *skip = getenv("ORBG_SKIP");
     static const int after = getenv("ORBG_SKIP_AFTER") ? atoi(getenv("ORBG_SKIP_AFTER")) : 0;
-    return skip && strstr(skip, name) && g_extract_batches > after;
+    return skip && strstr(skip, name) && g_extract_batches.load() > after;
 }
+#else
+static inline bool prof_skip(const char *) { return false; }
+#endif
 #define PROF_LAUNCH(ctxp, name, ...)                                                       \
     do {                                                                                   \
         if (prof_skip(name)) break;                                                        \
@@ -238,8 +241,6 @@ struct orbg_ctx {
     int oct_mode = 0;
     int blur0_mode = 0;  // measured: 2.013 vs 2.025 ms per 256 frames with it on
     int fast0_mode = 1;  // level-0 FAST cells on `ostream` beside the resize chain (ORBG_FAST0)
-    int fast_v2 = 1;     // k_fast2 (fast_kernels.hip) where its pitch fits, else k_fast_cells (ORBG_FAST_V=1)
-    int blur_v2 = 1;     // k_blur2 (blur_kernels.hip), else k_blur (ORBG_BLUR_V=1)
     // Pipelined batches (orbg_set_pipeline): the front of a batch (pyramid, FAST cells,
     // GaussianBlur: image work) runs on `stream`, its back (quadtree, orientation +
     // descriptors, stereo: keypoint work) on `ostream`, so the front of batch k+1 overlaps
@@ -248,6 +249,17 @@ struct orbg_ctx {
     // whole front written (on `stream`), ev_back[s] = slot s's last back reader done (on
     // `ostream`); the front into slot s waits for ev_back[s].
     int pipelined = 0;
+    bool last_piped = false;  // the last batch took the pipelined path (back_stream)
+    // stereo summary (orbg_stereo_summary) on the match stream: ev_sback = stereo outputs
+    // written (back stream), ev_ssum = the summary's reads done (match stream; the next
+    // stereo batch waits for it before overwriting d_snvalid / d_spairs)
+    hipEvent_t ev_sback = nullptr, ev_ssum = nullptr;
+    bool ssum_pending = false;
+    // caller reads of the outputs (orbg_batch_acquire / orbg_batch_release): ev_rel[s] = the
+    // caller's reads of output slot s issued so far, ev_srel = of the stereo outputs; the
+    // slot's next extraction / the next stereo pass waits for them
+    hipEvent_t ev_rel[2] = {nullptr, nullptr}, ev_srel = nullptr;
+    bool rel_pending[2] = {false, false}, srel_pending = false;
     hipEvent_t ev_cells[2] = {nullptr, nullptr}, ev_front[2] = {nullptr, nullptr};
     hipEvent_t ev_back[2] = {nullptr, nullptr};
     bool back_pending[2] = {false, false};
@@ -267,8 +279,7 @@ struct orbg_ctx {
     int gw = 0, gh = 0, gbatch = 0;
     OrbgGeom geom{};
     std::vector<OrbgCell> cells;
-    std::vector<int32_t> tile_base;  // k_blur region bases, then k_blur2 tile bases (L + 1 each)
-    int total_tiles = 0;
+    std::vector<int32_t> tile_base;  // k_blur2 tile bases (L + 1)
     OctLdsDims oct_dims[2] = {};
     // device
     OrbgGeom *d_geom = nullptr;
@@ -404,6 +415,9 @@ static void free_plan(orbg_ctx *c)
         if (q) hipStreamSynchronize(q);
     c->mat_pending[0] = c->mat_pending[1] = false;
     c->back_pending[0] = c->back_pending[1] = false;
+    for (hipEvent_t e : {c->ev_rel[0], c->ev_rel[1], c->ev_srel, c->ev_ssum})
+        if (e) hipEventSynchronize(e);  // caller streams may still read the outputs
+    c->rel_pending[0] = c->rel_pending[1] = c->srel_pending = c->ssum_pending = false;
     void *ptrs[] = {c->d_geom, c->d_cells, c->d_tile_base, c->d_rtab, c->d_ctab, c->d_odtab,
                     c->pyr_slot[0], c->pyr_slot[1], c->blur_slot[0], c->blur_slot[1],
                     c->cnt_slot[0], c->cnt_slot[1], c->ckp_slot[0], c->ckp_slot[1], c->d_keys, c->d_knode, c->d_act, c->d_qk,
@@ -632,7 +646,16 @@ static int plan(orbg_ctx *c, int w, int h, int batch)
     G.min_th = std::min(std::max(p.min_th_fast, 0), 255);
     G.brief_fma = p.brief_fma;
     G.sincos_mode = p.sincos_mode;
-    G.dbg = getenv("ORBG_DBG") ? atoi(getenv("ORBG_DBG")) : 0;
+#ifdef ORBG_DEV_KNOBS
+    G.dbg = getenv("ORBG_DBG") ? atoi(getenv("ORBG_DBG")) : 0;  // phase-stop timing knob
+#else
+    G.dbg = 0;
+#endif
+    // error-path fault injection (tests): k_octree, the fallback for levels past
+    // k_octree_lds' capacity, refuses every level, so such a level overflows and the batch's
+    // sticky error flag fails the next check with ORBG_ENOTSUP (never a silent short output)
+    if (const char *fi = getenv("ORBG_FAULT_INJECT"))
+        if (!strcmp(fi, "octree_overflow")) G.dbg = 91;
     for (int i = 0; i < 7; i++) G.gk[i] = p.gauss_k[i];
     for (int i = 0; i < 16; i++) G.umax[i] = c->umax[i];
     std::vector<OrbgCell> cells;
@@ -650,7 +673,7 @@ static int plan(orbg_ctx *c, int w, int h, int batch)
             return set_err(ORBG_ENOTSUP, "level %d too large (%dx%d)", l, lw[l], lh[l]);
     }
     int64_t pyr_off = 0, blur_off = 0;
-    int key_off = 0, node_off = 0, out_off = 0, tiles = 0;
+    int key_off = 0, node_off = 0, out_off = 0;
     std::vector<int32_t> tile_base, blur2_base;
     int blur2_tasks = 0;
     for (int l = 0; l < G.L; l++) {
@@ -760,8 +783,6 @@ static int plan(orbg_ctx *c, int w, int h, int batch)
         }
         L.blur_off = blur_off;
         blur_off += (int64_t)L.pitch * L.h;
-        tile_base.push_back(tiles);
-        tiles += ((L.w + 127) / 128) * ((L.h + 32 * ORBG_BLUR_NB - 1) / (32 * ORBG_BLUR_NB));  // k_blur regions
         blur2_base.push_back(blur2_tasks);  // k_blur2 (blur_kernels.hip): 244 x SEG wave tiles
         blur2_tasks += ((L.w + blur2_tw() - 1) / blur2_tw()) * ((L.h + blur2_seg() - 1) / blur2_seg());
         // resize coefficient tables (cv::resize, INTER_LINEAR)
@@ -828,10 +849,9 @@ static int plan(orbg_ctx *c, int w, int h, int batch)
                                rows, L.rz_pitch);
         }
     }
-    tile_base.push_back(tiles);
     blur2_base.push_back(blur2_tasks);
-    // d_tile_base = k_blur region bases (L + 1), then k_blur2 tile bases (L + 1)
-    tile_base.insert(tile_base.end(), blur2_base.begin(), blur2_base.end());
+    // d_tile_base = k_blur2 tile bases (L + 1)
+    tile_base = blur2_base;
     G.ncells = (int)cells.size();
     G.cell_cap = cell_cap;
     {
@@ -841,51 +861,23 @@ static int plan(orbg_ctx *c, int w, int h, int batch)
             hmax = std::max(hmax, (int)cl.h);
         }
         const int rg = std::max(wmax - 6 + 3, 0) / 4;
-        // LDS row pitch (dwords) >= RG + 3; pick the one whose raster unit -> (row, group)
-        // mapping spreads a wave's 64 dword reads best over the 64 LDS banks, summed over
-        // the cells' distinct group counts (ds_read cost ~ worst bank multiplicity)
+        // 4-pixel unit groups per row of the cells (bank-spread cost of the LDS pitch)
         std::vector<int> rgs;
         for (const OrbgCell &cl : cells) {
             const int r = std::max((int)cl.w - 6 + 3, 0) / 4;
             if (r > 0 && std::find(rgs.begin(), rgs.end(), r) == rgs.end()) rgs.push_back(r);
         }
-        int best_w = rg + 3, best_cost = 1 << 30;
-        const int rows_per_wave = hmax + std::max(hmax - 6, 0) + 2;
-        for (int wd = rg + 3; wd <= rg + 3 + 64; wd++) {
-            if (wd > rg + 3 && rows_per_wave * 4 * wd > 16 * 1024) break;  // 4 waves <= 64 KB
-            int cost = 0;
-            for (int r : rgs)
-                for (int k = 0; k < 3; k++) {
-                    int hist[64] = {0}, mx = 0;
-                    for (int lane = 0; lane < 64; lane++) {
-                        const int b = ((lane / r) * wd + lane % r + k) & 63;
-                        mx = std::max(mx, ++hist[b]);
-                    }
-                    cost += mx;
-                }
-            if (cost < best_cost) {
-                best_cost = cost;
-                best_w = wd;
-            }
-        }
-        G.fc_pitch = 4 * best_w;  // dwords 0..RG+1 of the window / score rows, + slack
-        G.fc_tile_rows = hmax;
         // pretest survivor lists: two of one u16 (row << 8 | group) per unit of the largest cell
         int max_units = 0;
         for (const OrbgCell &cl : cells)
             max_units = std::max(max_units, std::max((int)cl.h - 6, 0) *
                                                 ((std::max((int)cl.w - 6, 0) + 3) / 4));
-        G.fc_list_off = (hmax + std::max(hmax - 6, 0) + 2) * G.fc_pitch;
-        G.fc_wave_bytes = (G.fc_list_off + 4 * max_units + 15) & ~15;
-        if (4 * G.fc_wave_bytes > 64 * 1024)
-            return set_err(ORBG_ENOTSUP, "FAST cell %dx%d needs %d LDS bytes per wave", wmax,
-                           hmax, G.fc_wave_bytes);
         // k_fast2 (fast_kernels.hip): compile-time pitch P4 >= 4 * ceil((RG + 3) / 4) (its
         // 16-byte window chunks) among the instantiated ones; layout tA / tB (hmax rows each,
         // interleaved: row stride 2 * P) | scores (hmax - 4 rows of P - 8 bytes) | list (2 entries per unit).  Preferred: the most
         // workgroups per CU by LDS, then the bank-spread cost.
         G.fc2_p4 = 0;
-        if (c->fast_v2) {
+        {
             // tile rows: 4 * ceil-ish((rg + 6) / 4) dwords; score rows (P4 - 2 dwords) hold rg + 2
             const int need = std::max(4 * ((rg + 3 + 3) / 4), rg + 4);
             int best_c = 1 << 30, best_wg = 0;
@@ -921,6 +913,9 @@ static int plan(orbg_ctx *c, int w, int h, int batch)
                 if (4 * G.fc2_wave_bytes > 160 * 1024) G.fc2_p4 = 0;
             }
         }
+        // every cell window the reference's 30-px grid makes (< 66 x 66) fits a pitch
+        if (!G.fc2_p4)
+            return set_err(ORBG_ENOTSUP, "FAST cell %dx%d fits no k_fast2 LDS pitch", wmax, hmax);
     }
     for (int l = 0; l < G.L; l++) {
         G.lv[l].key_off = key_off;
@@ -1061,7 +1056,6 @@ static int plan(orbg_ctx *c, int w, int h, int batch)
     c->geom = G;
     c->cells = cells;
     c->tile_base = tile_base;
-    c->total_tiles = tiles;
     c->gw = w;
     c->gh = h;
     c->gbatch = want_batch;
@@ -1090,7 +1084,8 @@ extern "C" int orbg_create(int device, const orbg_params *p, orbg_ctx **out)
         if (prm.gauss_k[i] < 0) return set_err(ORBG_EINVAL, "gauss_k[%d] < 0", i);
         ksum += prm.gauss_k[i];
     }
-    // 16-bit row sums in k_blur: sum(k) * 255 must fit (both OpenCV tables: 256, 257)
+    // 16-bit row sums in k_blur2's packed row pairs: sum(k) * 255 must fit (both OpenCV
+    // tables: 256, 257)
     if (ksum > 257) return set_err(ORBG_EINVAL, "gauss_k sums to %d (> 257)", ksum);
     if (ksum == 0) {
         const int32_t k[7] = {18, 34, 48, 56, 48, 34, 18};
@@ -1135,10 +1130,6 @@ extern "C" int orbg_create(int device, const orbg_params *p, orbg_ctx **out)
         c->oct_mode = e ? atoi(e) : 1;
         const char *f0 = getenv("ORBG_FAST0");
         c->fast0_mode = f0 ? atoi(f0) : 1;
-        const char *fv = getenv("ORBG_FAST_V");
-        c->fast_v2 = fv ? (atoi(fv) >= 2) : 1;
-        const char *bv = getenv("ORBG_BLUR_V");
-        c->blur_v2 = bv ? (atoi(bv) >= 2) : 1;
         const char *b0 = getenv("ORBG_BLUR0");
         c->blur0_mode = b0 ? atoi(b0) : 0;
         const char *bp = getenv("ORBG_BACK_PRIO");  // developer A/B: normal | high (default)
@@ -1184,7 +1175,21 @@ extern "C" int orbg_create(int device, const orbg_params *p, orbg_ctx **out)
         hipEventCreateWithFlags(&c->ev_front[i], hipEventDisableTiming);
         hipEventCreateWithFlags(&c->ev_back[i], hipEventDisableTiming);
     }
+    hipEventCreateWithFlags(&c->ev_sback, hipEventDisableTiming);
+    hipEventCreateWithFlags(&c->ev_ssum, hipEventDisableTiming);
+    hipEventCreateWithFlags(&c->ev_rel[0], hipEventDisableTiming);
+    hipEventCreateWithFlags(&c->ev_rel[1], hipEventDisableTiming);
+    hipEventCreateWithFlags(&c->ev_srel, hipEventDisableTiming);
     if (const char *e = getenv("ORBG_PIPELINE")) c->pipelined = atoi(e) && c->ostream;
+#ifdef ORBG_DEV_KNOBS
+    if (getenv("ORBG_SKIP") || getenv("ORBG_DBG"))
+        fprintf(stderr, "liborbg (developer build): ORBG_SKIP / ORBG_DBG set -- launches are "
+                        "skipped or cut short, outputs are WRONG\n");
+#else
+    if (getenv("ORBG_SKIP") || getenv("ORBG_DBG"))
+        fprintf(stderr, "liborbg: ORBG_SKIP / ORBG_DBG ignored (developer builds only, make "
+                        "DEV=1)\n");
+#endif
     *out = c;
     return ORBG_OK;
 }
@@ -1221,6 +1226,8 @@ extern "C" void orbg_destroy(orbg_ctx *c)
     if (c->fstream) hipStreamDestroy(c->fstream);
     if (c->ev_fast) hipEventDestroy(c->ev_fast);
     if (c->ev_oct) hipEventDestroy(c->ev_oct);
+    for (hipEvent_t e : {c->ev_sback, c->ev_ssum, c->ev_rel[0], c->ev_rel[1], c->ev_srel})
+        if (e) hipEventDestroy(e);
     if (c->mstream) hipStreamDestroy(c->mstream);
     if (c->own_stream) hipStreamDestroy(c->own_stream);
     delete c;
@@ -1282,7 +1289,7 @@ static hipError_t launch_pyramid(orbg_ctx *c, hipStream_t st, const uint8_t *d_i
         const int64_t sfs = (l == 1) ? fs : G.pyr_frame;
         const int spitch = (l == 1) ? pitch : P.pitch;
         dim3 grid((L.w + 255) / 256, (L.h + 16 * ORBG_RZ_NT - 1) / (16 * ORBG_RZ_NT), B);
-        PROF_LAUNCH(c, "resize",
+        PROF_LAUNCH(c, "resize_chain",
                     hipLaunchKernelGGL(k_resize, grid, dim3(256), L.rz_pitch * L.rz_rows, st,
                                        src, sfs, spitch, P.w, c->d_pyr + L.pyr_off, G.pyr_frame,
                                        L.pitch, L.w, L.h, c->d_rtab + L.xtab_off,
@@ -1291,47 +1298,30 @@ static hipError_t launch_pyramid(orbg_ctx *c, hipStream_t st, const uint8_t *d_i
     return hipGetLastError();
 }
 
-// GaussianBlur of levels [l0, l1) of every frame on `st`: k_blur2 (one wave per 256 x SEG
-// output tile, blur_kernels.hip), or k_blur (ORBG_BLUR_V=1)
+// GaussianBlur of levels [l0, l1) of every frame on `st`: k_blur2 (one wave per 244 x SEG
+// output tile, blur_kernels.hip)
 static hipError_t launch_blur_levels(orbg_ctx *c, hipStream_t st, const uint8_t *d_imgs, int B,
                                      int pitch, int64_t fs, int l0, int l1)
 {
-    const int L = c->geom.L;
-    if (c->blur_v2 && c->geom.lv[L - 1].w >= 8) {  // k_blur2's row-end permutes need W >= 8
-        const int32_t *b2 = c->tile_base.data() + L + 1;
-        hipError_t e = hipSuccess;
-        PROF_LAUNCH(c, "blur",
-                    e = launch_blur2(st, c->d_geom, c->d_tile_base + L + 1, d_imgs, fs, pitch,
-                                     c->d_pyr, c->d_blur, b2[l0], b2[l1] - b2[l0], B));
-        return e;
-    }
-    const int t0 = c->tile_base[l0], t1 = c->tile_base[l1];
+    const int32_t *b2 = c->tile_base.data();
+    hipError_t e = hipSuccess;
     PROF_LAUNCH(c, "blur",
-                hipLaunchKernelGGL(k_blur, dim3((t1 - t0) * B), dim3(256), 0, st, c->d_geom,
-                                   c->d_tile_base, d_imgs, fs, pitch, c->d_pyr, c->d_blur, t0,
-                                   t1 - t0));
-    return hipGetLastError();
+                e = launch_blur2(st, c->d_geom, c->d_tile_base, d_imgs, fs, pitch, c->d_pyr,
+                                 c->d_blur, b2[l0], b2[l1] - b2[l0], B));
+    return e;
 }
 
-// FAST cells [cb, cb + cn) of every frame on `st` (k_fast2 where the plan picked a pitch)
+// FAST cells [cb, cb + cn) of every frame on `st` (k_fast2, fast_kernels.hip)
 static hipError_t launch_fast_cells(orbg_ctx *c, hipStream_t st, const uint8_t *d_imgs, int B,
                                     int pitch, int64_t fs, int cb, int cn)
 {
     const OrbgGeom &G = c->geom;
-    if (G.fc2_p4) {
-        hipError_t e = hipSuccess;
-        PROF_LAUNCH(c, "fast_cells",
-                    e = launch_fast2(G.fc2_p4, 4 * G.fc2_wave_bytes, st, c->d_geom, c->d_cells,
-                                     d_imgs, fs, pitch, c->d_pyr, c->d_ctab, c->d_cell_cnt,
-                                     c->d_cell_kp, B, cb, cn));
-        return e;
-    }
+    hipError_t e = hipSuccess;
     PROF_LAUNCH(c, "fast_cells",
-                hipLaunchKernelGGL(k_fast_cells, dim3((cn * B + 3) / 4), dim3(256),
-                                   4 * G.fc_wave_bytes, st, c->d_geom, c->d_cells, d_imgs, fs,
-                                   pitch, c->d_pyr, c->d_ctab, c->d_cell_cnt, c->d_cell_kp, B,
-                                   cb, cn));
-    return hipGetLastError();
+                e = launch_fast2(G.fc2_p4, 4 * G.fc2_wave_bytes, st, c->d_geom, c->d_cells, d_imgs,
+                                 fs, pitch, c->d_pyr, c->d_ctab, c->d_cell_cnt, c->d_cell_kp, B,
+                                 cb, cn));
+    return e;
 }
 
 // Pipelined batch into slot s (orbg_set_pipeline).  Front on `stream`: resize chain, FAST
@@ -1407,6 +1397,10 @@ static int launch_extract_pipe(orbg_ctx *c, const uint8_t *d_imgs, int B, int pi
         HIPCHK(hipStreamWaitEvent(st, c->ev_mat[s], 0));
         c->mat_pending[s] = false;
     }
+    if (c->rel_pending[s]) {  // ... and so may the caller (orbg_batch_release)
+        HIPCHK(hipStreamWaitEvent(st, c->ev_rel[s], 0));
+        c->rel_pending[s] = false;
+    }
     c->slot = s;
     c->d_kps = c->kps_slot[s];
     c->d_desc = c->desc_slot[s];
@@ -1428,8 +1422,10 @@ static int launch_extract_pipe(orbg_ctx *c, const uint8_t *d_imgs, int B, int pi
     return ORBG_OK;
 }
 
-// stream the last batch's per-frame outputs are written on (and stereo runs on)
-static hipStream_t back_stream(orbg_ctx *c) { return c->pipelined ? c->ostream : c->stream; }
+// stream the last batch's per-frame outputs were written on (and stereo runs on): the back
+// stream only if that batch actually took the pipelined path (orbg_set_serial on a
+// pipelined context runs everything on the context stream)
+static hipStream_t back_stream(orbg_ctx *c) { return c->last_piped ? c->ostream : c->stream; }
 
 static int launch_extract(orbg_ctx *c, const uint8_t *d_imgs, int B, int pitch, int64_t fs)
 {
@@ -1438,7 +1434,9 @@ static int launch_extract(orbg_ctx *c, const uint8_t *d_imgs, int B, int pitch, 
     // the match / stereo outputs of the previous batch are stale from here on
     c->last_npairs = 0;
     c->last_nstereo = 0;
+#ifdef ORBG_DEV_KNOBS
     g_extract_batches++;
+#endif
     // d_err is not cleared here: it is sticky until check_err reads it
     // this batch's slot: intermediates (pyramid, blur, FAST cells) and per-frame outputs
     const int s = c->slot ^ 1;
@@ -1446,7 +1444,8 @@ static int launch_extract(orbg_ctx *c, const uint8_t *d_imgs, int B, int pitch, 
     c->d_blur = c->blur_slot[s];
     c->d_cell_cnt = c->cnt_slot[s];
     c->d_cell_kp = c->ckp_slot[s];
-    if (c->pipelined && !c->serial) return launch_extract_pipe(c, d_imgs, B, pitch, fs, s);
+    c->last_piped = c->pipelined && !c->serial;
+    if (c->last_piped) return launch_extract_pipe(c, d_imgs, B, pitch, fs, s);
     // serial (orbg_set_serial): every kernel on the caller's stream, one after the other
     const int oct_mode = c->serial ? 0 : c->oct_mode;
     // fast0: the level-0 FAST cells and quadtree need only the input images, so they run on
@@ -1515,6 +1514,10 @@ static int launch_extract(orbg_ctx *c, const uint8_t *d_imgs, int B, int pitch, 
         HIPCHK(hipStreamWaitEvent(st, c->ev_mat[s], 0));
         c->mat_pending[s] = false;
     }
+    if (c->rel_pending[s]) {
+        HIPCHK(hipStreamWaitEvent(st, c->ev_rel[s], 0));
+        c->rel_pending[s] = false;
+    }
     c->slot = s;
     c->d_kps = c->kps_slot[s];
     c->d_desc = c->desc_slot[s];
@@ -1541,6 +1544,11 @@ static int sync_all(orbg_ctx *c)
     HIPCHK(hipStreamSynchronize(c->mstream));
     if (c->ostream) HIPCHK(hipStreamSynchronize(c->ostream));
     c->mat_pending[0] = c->mat_pending[1] = false;
+    for (int i = 0; i < 2; i++)
+        if (c->rel_pending[i]) HIPCHK(hipEventSynchronize(c->ev_rel[i]));
+    if (c->srel_pending) HIPCHK(hipEventSynchronize(c->ev_srel));
+    if (c->ssum_pending) HIPCHK(hipEventSynchronize(c->ev_ssum));
+    c->rel_pending[0] = c->rel_pending[1] = c->srel_pending = c->ssum_pending = false;
     return ORBG_OK;
 }
 
@@ -1775,6 +1783,29 @@ extern "C" int orbg_batch_summary(orbg_ctx *c, int32_t *d_out)
     return ORBG_OK;
 }
 
+extern "C" int orbg_batch_acquire(orbg_ctx *c, void *stream)
+{
+    if (!c || !c->gw || c->last_n <= 0) return set_err(ORBG_EINVAL, "no batch");
+    const hipStream_t q = stream ? (hipStream_t)stream : c->mstream;
+    HIPCHK(hipStreamWaitEvent(q, c->ev_ext[c->slot], 0));
+    if (c->last_nstereo) HIPCHK(hipStreamWaitEvent(q, c->ev_sback, 0));
+    return ORBG_OK;
+}
+
+extern "C" int orbg_batch_release(orbg_ctx *c, void *stream)
+{
+    if (!c || !c->gw || c->last_n <= 0) return set_err(ORBG_EINVAL, "no batch");
+    const hipStream_t q = stream ? (hipStream_t)stream : c->mstream;
+    const int s = c->slot;
+    HIPCHK(hipEventRecord(c->ev_rel[s], q));
+    c->rel_pending[s] = true;
+    if (c->last_nstereo) {
+        HIPCHK(hipEventRecord(c->ev_srel, q));
+        c->srel_pending = true;
+    }
+    return ORBG_OK;
+}
+
 extern "C" int orbg_batch_matches(orbg_ctx *c, int32_t *d_out, int32_t *frame_cap)
 {
     if (!c || !c->gw || c->last_n <= 0) return set_err(ORBG_EINVAL, "no batch");
@@ -1904,7 +1935,8 @@ extern "C" int orbg_match_batch_device(orbg_ctx *c, const int32_t *f1, const int
                                 c->d_desc, c->d_kps, c->d_counts, (int)fc, c->d_pairs,
                                 c->d_pairs + c->pair_cap, npairs, c->geom.w, c->geom.h, window,
                                 nnratio, check_ori, c->d_knn, c->d_m12, c->d_nm, c->d_topk,
-                                c->d_topk_n, &c->prof, c->geom.dbg == 40, c->geom.lv[0].out_cap);
+                                c->d_topk_n, &c->prof, c->serial || c->geom.dbg == 40,
+                                c->geom.lv[0].out_cap);
     if (rc) return rc;
     HIPCHK(hipEventRecord(c->ev_mat[s], c->mstream));
     c->mat_pending[s] = true;
@@ -1949,21 +1981,35 @@ extern "C" int orbg_stereo_batch_device(orbg_ctx *c, const int32_t *left, const 
     // next extraction overwrites); the pair lists are uploaded only when they change
     std::vector<int32_t> hp(left, left + npairs);
     hp.insert(hp.end(), right, right + npairs);
+    const hipStream_t bs = back_stream(c);
     if (hp != c->h_spairs) {
-        HIPCHK(hipStreamSynchronize(back_stream(c)));  // a previous stereo pass may read them
+        HIPCHK(hipStreamSynchronize(bs));  // a previous stereo pass may read them
+        if (c->ssum_pending) HIPCHK(hipStreamSynchronize(c->mstream));  // ... or its summary
+        if (c->srel_pending) HIPCHK(hipEventSynchronize(c->ev_srel));   // ... or the caller
+        c->ssum_pending = c->srel_pending = false;
         HIPCHK(hipMemcpy(c->d_spairs, left, npairs * sizeof(int32_t), hipMemcpyHostToDevice));
         HIPCHK(hipMemcpy(c->d_spairs + c->stereo_cap, right, npairs * sizeof(int32_t),
                          hipMemcpyHostToDevice));
         c->h_spairs.swap(hp);
     }
+    // the previous batch's summary (match stream) reads d_snvalid, which this pass rewrites
+    if (c->ssum_pending) {
+        HIPCHK(hipStreamWaitEvent(bs, c->ev_ssum, 0));
+        c->ssum_pending = false;
+    }
+    if (c->srel_pending) {  // the caller's reads of the previous stereo outputs
+        HIPCHK(hipStreamWaitEvent(bs, c->ev_srel, 0));
+        c->srel_pending = false;
+    }
     // pipelined: on the back stream after the batch's descriptors; the slot's next front
     // waits for it (ev_back)
-    int rc = launch_stereo(back_stream(c), c->geom, c->d_kps, c->d_desc, c->d_counts, c->d_spairs,
+    int rc = launch_stereo(bs, c->geom, c->d_kps, c->d_desc, c->d_counts, c->d_spairs,
                            c->d_spairs + c->stereo_cap, npairs, c->last_img, c->last_fs,
                            c->last_pitch, c->d_pyr, bf, min_z, c->d_sscr, c->d_uright,
                            c->d_depth, c->d_snvalid, &c->prof);
     if (rc) return set_err(rc, "stereo launch failed (level-0 height > 4096?)");
-    if (c->pipelined) HIPCHK(hipEventRecord(c->ev_back[c->slot], c->ostream));
+    if (c->last_piped) HIPCHK(hipEventRecord(c->ev_back[c->slot], c->ostream));
+    HIPCHK(hipEventRecord(c->ev_sback, bs));
     c->last_nstereo = npairs;
     return ORBG_OK;
 }
@@ -1983,10 +2029,19 @@ __global__ void k_stereo_summary(const int32_t *__restrict__ counts,
 extern "C" int orbg_stereo_summary(orbg_ctx *c, int32_t *d_out)
 {
     if (!c || !c->last_nstereo || !d_out) return set_err(ORBG_EINVAL, "no stereo batch yet");
+    // on the match stream, as orbg_batch_summary: after the stereo pass (ev_sback); the
+    // extraction that next rewrites this output slot waits for it (ev_mat), the next stereo
+    // pass too (ev_ssum)
+    const int s = c->slot;
+    HIPCHK(hipStreamWaitEvent(c->mstream, c->ev_sback, 0));
     hipLaunchKernelGGL(k_stereo_summary, dim3((c->last_nstereo + 255) / 256), dim3(256), 0,
-                       back_stream(c), c->d_counts, c->d_spairs, c->d_snvalid, c->last_nstereo,
+                       c->mstream, c->d_counts, c->d_spairs, c->d_snvalid, c->last_nstereo,
                        d_out);
     HIPCHK(hipGetLastError());
+    HIPCHK(hipEventRecord(c->ev_mat[s], c->mstream));
+    c->mat_pending[s] = true;
+    HIPCHK(hipEventRecord(c->ev_ssum, c->mstream));
+    c->ssum_pending = true;
     return ORBG_OK;
 }
 

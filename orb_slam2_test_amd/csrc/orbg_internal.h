@@ -32,7 +32,6 @@
 #ifndef ORBG_RZ_FILL
 #define ORBG_RZ_FILL 5           // k_resize: staged 16-byte chunks per thread
 #endif
-#define ORBG_BLUR_NB 4           // k_blur: 32-row output bands per workgroup
 #ifndef ORBG_OD_KPW
 #define ORBG_OD_KPW 8            // k_orient_desc: quadtree output slots per wave
 #endif
@@ -74,11 +73,7 @@ struct OrbgGeom {
     int32_t brief_fma;
     int32_t sincos_mode;          // rBRIEF cos/sin: 0 glibc cosf/sinf restated, 1 pinned double
     int32_t dbg;                  // developer timing knob (ORBG_DBG env), 0 in production
-    int32_t fc_pitch;             // k_fast_cells LDS row pitch (bytes)
-    int32_t fc_tile_rows;         // max FAST window height
-    int32_t fc_wave_bytes;        // LDS bytes per wave (window + score tiles + unit list)
-    int32_t fc_list_off;          // byte offset of the pretest unit list in a wave's LDS
-    int32_t fc2_p4;               // k_fast2 LDS row pitch (dwords, a template instance; 0: k_fast_cells)
+    int32_t fc2_p4;               // k_fast2 LDS row pitch (dwords, a template instance)
     int32_t fc2_wave_bytes;       // k_fast2 LDS bytes per wave
     int32_t fc2_tileb_off, fc2_sc_off, fc2_list_off;  // k_fast2 regions within a wave's LDS
     int32_t fc2_list_cap;         // k_fast2 pretest list entries per wave

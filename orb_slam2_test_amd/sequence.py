@@ -162,3 +162,71 @@ class GpuBackend:
             m12 = dm.cpu().numpy()
             return nkp, nm, m12
         return nkp, nm
+
+
+class BenchStep:
+    """One step of the batched-sequence mode on one rank, exactly as bench.py times it.
+
+    mode "mono" (C3): ORBextractor on the B + 1 resident frames of a block (halo first),
+    then knn2 + SearchForInitialization(window, nnratio, checkOri) of the B pairs (i, i + 1)
+    (ORBmatcher.cc:487-631), the per-frame summary (keypoints of frames 1..B, matches of the
+    pairs) and the vnMatches12 rows, all on liborbg's match stream, and with world > 1
+    their RCCL all_gathers there.
+    mode "extract" (C2): ORBextractor on the B frames of a block only.
+    mode "stereo" (C4): ORBextractor on B left/right pairs (2B images, L and R
+    interleaved), Frame::ComputeStereoMatches of every pair (Frame.cc:619-834), the stereo
+    summary on the match stream and its all_gather.
+
+    `capture(step)`, when set (tests), runs on the match stream after the step's outputs
+    are written (orbg_batch_acquire) and before liborbg may reuse them
+    (orbg_batch_release); the bench leaves it unset."""
+
+    def __init__(self, ext, B, mode="mono", world=1, window=100, nnratio=0.9, check_ori=True,
+                 bf=None, min_z=None):
+        import torch
+        from . import synthetic
+        if mode not in ("mono", "extract", "stereo"):
+            raise ValueError(mode)
+        self.ext, self.B, self.mode, self.world = ext, B, mode, world
+        self.window, self.nnratio, self.check_ori = window, nnratio, check_ori
+        self.bf = synthetic.KITTI_BF if bf is None else bf
+        self.min_z = synthetic.KITTI_BF / synthetic.KITTI_FX if min_z is None else min_z
+        self.nimg = {"mono": B + 1, "extract": B, "stereo": 2 * B}[mode]
+        self.f1 = np.arange(B, dtype=np.int32)        # local frame i (0 = the halo) ...
+        self.f2 = np.arange(1, B + 1, dtype=np.int32)  # ... matched to frame i + 1
+        self.sl, self.sr = np.arange(B, dtype=np.int32) * 2, np.arange(B, dtype=np.int32) * 2 + 1
+        self.summary = torch.zeros(2 * B + 1, dtype=torch.int32, device="cuda")
+        self.ssum = torch.zeros(2 * B, dtype=torch.int32, device="cuda")
+        self.m12 = None
+        self.mstream = torch.cuda.ExternalStream(ext.ctx.match_stream())
+        self.capture = None
+        self.gathered = None
+
+    def __call__(self, d_frames_ptr, w, h):
+        import torch
+        ext, B = self.ext, self.B
+        ext.extract_batch_device(d_frames_ptr, self.nimg, w, h)
+        if self.mode == "stereo":
+            ext.stereo_batch_device(self.sl, self.sr, self.bf, self.min_z)
+            ext.ctx.stereo_summary(self.ssum.data_ptr())
+            if self.world > 1:  # per-frame (keypoints, depths) of every rank
+                with torch.cuda.stream(self.mstream):
+                    self.gathered = gather_summary(self.ssum.view(2, B), self.world,
+                                                   sizes=[B] * self.world)
+        elif self.mode == "mono":
+            ext.match_batch_device(self.f1, self.f2, self.window, self.nnratio, self.check_ori)
+            ext.ctx.batch_summary(self.summary.data_ptr())
+            if self.m12 is None:
+                self.m12 = torch.empty((B, ext.ctx.batch_matches(None)), dtype=torch.int32,
+                                       device="cuda")
+            ext.ctx.batch_matches(self.m12.data_ptr())  # vnMatches12 rows of the B pairs
+            if self.world > 1:
+                with torch.cuda.stream(self.mstream):
+                    local = torch.stack([self.summary[1:B + 1], self.summary[B + 1:]])
+                    self.gathered = (gather_summary(local, self.world, sizes=[B] * self.world),
+                                     gather_rows(self.m12, self.world, sizes=[B] * self.world))
+        if self.capture is not None:
+            ext.ctx.batch_acquire(self.mstream.cuda_stream)
+            with torch.cuda.stream(self.mstream):
+                self.capture(self)
+            ext.ctx.batch_release(self.mstream.cuda_stream)

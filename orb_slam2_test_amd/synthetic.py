@@ -101,6 +101,39 @@ def sequence_block(n_total, lo, hi, h, w, seed=DEFAULT_SEED, max_step=8, noise=2
     return out
 
 
+def sequence_blocks(n_total, ranges, h, w, seed=DEFAULT_SEED, max_step=8, noise=2):
+    """sequence_block for several blocks [(lo, hi), ...] of one n_total-frame sequence,
+    with the canvas built once: a list of [hi - lo + 1, h, w] arrays (halo first)."""
+    from .sequence import local_indices
+    rng = np.random.Generator(np.random.PCG64(seed + 1))
+    steps = rng.integers(-max_step, max_step + 1, size=(n_total, 2))
+    steps[0] = 0
+    pos = np.cumsum(steps, axis=0)
+    pos -= pos.min(axis=0)
+    base = canvas(h + int(pos[:, 0].max()) + 1, w + int(pos[:, 1].max()) + 1, seed)
+    blocks = []
+    for lo, hi in ranges:
+        idx = local_indices(n_total, lo, hi)
+        out = np.empty((len(idx), h, w), np.uint8)
+        for j, t in enumerate(idx):
+            y, x = pos[t]
+            crop = base[y:y + h, x:x + w]
+            jr = np.random.Generator(np.random.PCG64([seed + 7, int(t)]))
+            jitter = jr.integers(-noise, noise + 1, size=(h, w)).astype(np.float32)
+            out[j] = np.clip(np.rint(crop + jitter), 0, 255).astype(np.uint8)
+        blocks.append(out)
+    return blocks
+
+
+def bench_block_ranges(B, world, rank, nblocks):
+    """The blocks bench.py streams through on rank `rank`: block k = frames
+    [(k world + rank) B, (k world + rank + 1) B) of one cyclic nblocks * world * B-frame
+    sequence, so consecutive steps read different frames (different HBM) and every rank's
+    block k is disjoint from every other rank's.  Returns (n_total, [(lo, hi), ...])."""
+    n_total = nblocks * world * B
+    return n_total, [((k * world + rank) * B, (k * world + rank + 1) * B) for k in range(nblocks)]
+
+
 def stereo_pair(h, w, seed=DEFAULT_SEED, noise=2, d_min=4.0, d_max=60.0, n_objects=6):
     """A rectified synthetic stereo pair (left, right) u8 and the true disparity map.
 

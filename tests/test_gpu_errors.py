@@ -4,7 +4,8 @@ short results.
 - A quadtree level that overflows a capacity zeroes that level's keypoints on the device.
   The flag is sticky: it survives later batches until orbg_sync / orbg_check_errors /
   orbg_batch_stats / orbg_download_frame reads it, and then the call fails with
-  ORBG_ENOTSUP.  The overflow is forced with the fault-injection knob ORBG_DBG=91 (k_octree,
+  ORBG_ENOTSUP.  The overflow is forced with the fault-injection knob
+  ORBG_FAULT_INJECT=octree_overflow (k_octree,
   the fallback for levels past k_octree_lds' 16,384-candidate capacity, is disabled), on a
   pure-noise frame whose level 0 has more candidates than that.
 - Match outputs belong to the batch they were computed on: after a new extraction (same or
@@ -28,17 +29,17 @@ W, H = 1241, 376
 
 @contextlib.contextmanager
 def knob(value):
-    """ORBG_DBG is read when a context plans its buffers (its first extraction at a size),
-    so the planning call must run inside this block."""
-    old = os.environ.get("ORBG_DBG")
-    os.environ["ORBG_DBG"] = value
+    """ORBG_FAULT_INJECT is read when a context plans its buffers (its first extraction at a
+    size), so the planning call must run inside this block."""
+    old = os.environ.get("ORBG_FAULT_INJECT")
+    os.environ["ORBG_FAULT_INJECT"] = value
     try:
         yield
     finally:
         if old is None:
-            del os.environ["ORBG_DBG"]
+            del os.environ["ORBG_FAULT_INJECT"]
         else:
-            os.environ["ORBG_DBG"] = old
+            os.environ["ORBG_FAULT_INJECT"] = old
 
 
 def test_pure_noise_level0_needs_the_fallback():
@@ -53,7 +54,7 @@ def test_batched_overflow_is_sticky_and_fails_loudly():
     frames = np.stack([S.frame(H, W, seed=3), S.pure_noise(H, W), S.frame(H, W, seed=4)])
     d = torch.from_numpy(frames).cuda()
     ext = ORBextractor(2000, 1.2, 8, 20, 7, max_batch=3)
-    with knob("91"):
+    with knob("octree_overflow"):
         ext.extract_batch_device(d.data_ptr(), 3, W, H)
     # a second, clean batch on top does not wipe the first batch's flag
     clean = torch.from_numpy(np.ascontiguousarray(frames[[0, 2, 0]])).cuda()
@@ -84,7 +85,7 @@ def test_batched_overflow_is_sticky_and_fails_loudly():
 
 def test_host_entry_overflow_fails():
     ext = ORBextractor(2000, 1.2, 8, 20, 7)
-    with knob("91"), pytest.raises(_lib.OrbgError) as ei:
+    with knob("octree_overflow"), pytest.raises(_lib.OrbgError) as ei:
         ext(S.pure_noise(H, W))
     assert ei.value.code == _lib.ORBG_ENOTSUP
     # the same context keeps working on frames inside k_octree_lds' capacity

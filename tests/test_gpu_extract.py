@@ -159,3 +159,48 @@ def test_batch_padded_pitch(oracle):
         r = oracle.extract(p, frames[f])
         assert np.array_equal(k, r["kps"]) and np.array_equal(desc, r["desc"])
         assert np.array_equal(ext.get_level(f, 0), frames[f])
+
+
+def _extract_with(oracle, img, sf, nl, nfeat=2000, env=None):
+    """ORBextractor(nfeat, sf, nl, 20, 7) vs the oracle; returns the kernel names that ran."""
+    import os
+    old = {k: os.environ.get(k) for k in (env or {})}
+    os.environ.update(env or {})
+    try:
+        ext = ORBextractor(nfeat, sf, nl, 20, 7)
+        ext.ctx.profile(True)
+        kps, desc = ext(img)
+        names = set(ext.ctx.profile_read())
+        pyr = ext.mvImagePyramid
+    finally:
+        for k, v in old.items():
+            if v is None:
+                os.environ.pop(k, None)
+            else:
+                os.environ[k] = v
+    p = oracle.params(nfeatures=nfeat, scale_factor=sf, nlevels=nl)
+    ref = oracle.extract(p, img, with_pyramid=True)
+    for l in range(nl):
+        assert np.array_equal(pyr[l], ref["pyramid"][l]), f"level {l}"
+    assert np.array_equal(kps, ref["kps"]) and np.array_equal(desc, ref["desc"])
+    ext.close()
+    return names
+
+
+@pytest.mark.parametrize("sf,nl", [(1.5, 5), (1.7, 4)])
+def test_resize_chain_scale_factors(oracle, kitti_seq, sf, nl):
+    """Scale factors past k_pyramid's band plan (> 11 source rows per 8 output rows) build the
+    pyramid with the k_resize chain (one launch per level); bit-exact all the same."""
+    names = _extract_with(oracle, kitti_seq[0], sf, nl)
+    assert "resize_chain" in names and "resize" not in names
+
+
+def test_resize_chain_forced_at_1_2(oracle, kitti_seq):
+    """ORBG_PYR=0 forces the k_resize chain at the reference's 1.2 (KITTI and TUM shapes)."""
+    names = _extract_with(oracle, kitti_seq[2], 1.2, 8, env={"ORBG_PYR": "0"})
+    assert "resize_chain" in names and "resize" not in names
+    names = _extract_with(oracle, S.frame(480, 640, seed=5), 1.2, 8, nfeat=1000,
+                          env={"ORBG_PYR": "0"})
+    assert "resize_chain" in names
+    names = _extract_with(oracle, kitti_seq[2], 1.2, 8)
+    assert "resize" in names and "resize_chain" not in names
