@@ -43,12 +43,15 @@ EXTRACT_FRAME_ALGO_BYTES = 2533578  # configs[1] / C2: ORBextractor only
 METRIC_EXTRACT = "frames/sec ORBextractor only, 1241×376 2000feat 8lvl (configs[1], C2)"
 
 
-PMC_MONO = "r02i_pmc_kernels.json"      # tools/r02_profile.sh (bench.py), copied from its run dir
-PMC_STEREO = "r02i_stereo_pmc_kernels.json"  # tools/r02_profile.sh <tag> --stereo
+# serial-pass PMC profiles of the bench lines (tools/round_prof.sh), copied from the run dirs
+PMC_MONO = "r03c_pmc_kernels.json"
+PMC_STEREO = "r03c_stereo_pmc_kernels.json"
 
 
-def kernel_algo_bytes(name, B, npairs, ncand, nkp, launches_per_step):
-    """Algorithmic bytes of one launch of `name` (see DESIGN.md 'Kernels')."""
+def kernel_algo_bytes(name, B, npairs, ncand, nkp, launches_per_step, ndepth=0):
+    """Algorithmic bytes of one launch of `name` (see DESIGN.md 'Kernels').  B images, npairs
+    frame pairs, ncand FAST candidates and nkp keypoints over the batch, ndepth stereo
+    matches (keypoints with a depth) over the batch."""
     lv = level_sizes()
     if name == "resize":
         tot = B * sum(lv[l - 1][0] * lv[l - 1][1] + lv[l][0] * lv[l][1] for l in range(1, NLEV))
@@ -72,9 +75,35 @@ def kernel_algo_bytes(name, B, npairs, ncand, nkp, launches_per_step):
     elif name == "stereo_match":
         kp = nkp / max(B, 1)
         tot = npairs * (2 * kp * (32 + 28) + kp * 8)  # both frames' kps + desc, uR + depth
+    elif name == "stereo_rows":
+        # right keypoints' (y, octave) in; row offsets (H + 1) and the row lists (u16 per
+        # listed row: a keypoint of octave l spans ~4 scale_l + 2 rows) out
+        kp = nkp / max(B, 1)
+        fpl = features_per_level()
+        sc = [1.2 ** l for l in range(NLEV)]
+        rows = sum(f * (4 * s + 2) for f, s in zip(fpl, sc)) / sum(fpl)
+        tot = npairs * (kp * 8 + (H + 1) * 4 + kp * rows * 2)
+    elif name == "stereo_sad":
+        # per match: the 11x11 left patch and the 11 x 21 right strip at the keypoint's level,
+        # (uR, depth, SAD) out
+        tot = ndepth * (11 * 11 + 11 * 21 + 12)
+    elif name == "stereo_median":
+        tot = ndepth * (4 + 8)  # SADs in, cleared (uR, depth) out
     else:
         return None
     return tot / max(launches_per_step, 1)
+
+
+def features_per_level():
+    """mnFeaturesPerLevel at 2000 features, 8 levels, 1.2 (ORBextractor.cc:466-476)."""
+    f = np.float32(1.0) / np.float32(1.2)
+    d = np.float32(NFEAT) * (np.float32(1) - f) / (np.float32(1) - np.float32(f ** NLEV))
+    out, s = [], 0
+    for _ in range(NLEV - 1):
+        out.append(int(np.rint(d)))
+        s += out[-1]
+        d = np.float32(d * f)
+    return out + [max(NFEAT - s, 0)]
 
 
 def level_sizes():
@@ -220,6 +249,9 @@ def main():
     ap.add_argument("--pipeline", type=int, default=int(os.environ.get("ORBG_PIPELINE", "1")),
                     help="1: pipelined batches (image half of step k+1 beside the keypoint half "
                          "of step k, orbg_set_pipeline); 0: one batch after the other")
+    ap.add_argument("--serial", action="store_true",
+                    help="run the timed steps serially (orbg_set_serial), as the roofline's "
+                         "kernel-timing pass does: for PMC collection, not a bench line")
     ap.add_argument("--stereo", action="store_true",
                     help="configs[3]: stereo frames (extract L+R + ComputeStereoMatches)")
     ap.add_argument("--extract-only", action="store_true",
@@ -275,6 +307,8 @@ def main():
     torch.cuda.set_stream(stream)
     ext.ctx.set_stream(stream.cuda_stream)
     ext.ctx.set_pipeline(bool(args.pipeline))
+    if args.serial:  # PMC runs (tools/round_prof.sh): one dispatch per kernel and step
+        ext.ctx.set_serial(True)
     mode = "stereo" if args.stereo else "extract" if args.extract_only else "mono"
     bstep = sequence.BenchStep(ext, B, mode, world=world)
     torch.cuda.synchronize()
@@ -289,6 +323,7 @@ def main():
         step()
     torch.cuda.synchronize()
     ncand, nkp = ext.ctx.batch_stats()
+    ndepth = int(bstep.ssum[B:].sum().item()) if args.stereo else 0
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
@@ -345,31 +380,37 @@ def main():
     value = frames_total / elapsed
     out = None
     if rank == 0:
+        # PMC figures from the committed serial-pass profile of this workload
+        # (tools/round_prof.sh -> tools/pmc_kernels.py): HBM bytes per launch and the
+        # fractions of the chip's VALU issue / LDS cycles each kernel used
+        pmc = os.path.join(ROOT, "profiles", PMC_STEREO if args.stereo else PMC_MONO)
+        pmc_all = {}
+        if os.path.exists(pmc) and not args.extract_only:
+            with open(pmc) as f:
+                pmc_all = json.load(f)
         kstats = {}
         for name, (ms, n) in kern.items():
             lps = n / max(args.steps, 1)
             avg = ms / max(n, 1)
-            ab = kernel_algo_bytes(name, nimg, B, ncand, nkp, lps)
+            ab = kernel_algo_bytes(name, nimg, B, ncand, nkp, lps, ndepth)
             kstats[name] = {"ms_per_step": round(ms / args.steps, 4), "launches_per_step": lps,
                             "avg_launch_ms": round(avg, 5),
                             "algo_bytes_per_launch": None if ab is None else int(ab),
-                            "achieved_GBps": None if ab is None else round(ab / (avg * 1e-3) / 1e9, 1)}
+                            "achieved_GBps": None if ab is None else round(ab / (avg * 1e-3) / 1e9, 1),
+                            "hbm_bytes_per_launch": pmc_all.get(name, {}).get("hbm_bytes_per_launch")}
         roof = None
         if kstats:
             dom = max(kstats, key=lambda k: kstats[k]["ms_per_step"])
             ks = kstats[dom]
             ach = ks["achieved_GBps"]
-            # PMC figures of the same kernel from the committed profile of this workload
-            # (tools/r02_profile.sh -> tools/pmc_kernels.py): HBM bytes per launch and the
-            # fractions of the chip's VALU issue / LDS cycles it used
-            pk = {}
-            pmc = os.path.join(ROOT, "profiles", PMC_STEREO if args.stereo else PMC_MONO)
-            if os.path.exists(pmc):
-                with open(pmc) as f:
-                    pk = json.load(f).get(dom, {})
+            pk = pmc_all.get(dom, {})
             roof = {"kernel": dom, "bound": "hbm", "achieved": ach, "peak": HBM_PEAK_GBS,
                     "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBS, 4) if ach else None,
                     "traffic": pk.get("hbm_bytes_per_launch"),
+                    "traffic_over_algo": (round(pk["hbm_bytes_per_launch"] /
+                                                ks["algo_bytes_per_launch"], 3)
+                                          if pk.get("hbm_bytes_per_launch") and
+                                          ks["algo_bytes_per_launch"] else None),
                     "valu_frac": pk.get("valu_frac"), "lds_frac": pk.get("lds_frac"),
                     "pmc_source": os.path.relpath(pmc, ROOT) if pk else None,
                     "algo_bytes_per_launch": ks["algo_bytes_per_launch"],
@@ -398,7 +439,8 @@ def main():
             "config": {
                 "workload": workload,
                 "frames_per_gpu_per_step": B, "global_batch": B * world, "width": W,
-                "pipelined_batches": bool(args.pipeline),
+                "pipelined_batches": bool(args.pipeline) and not args.serial,
+                "serial_pass_only": bool(args.serial),
                 "input_blocks": nblocks,
                 "input_reuse": ("none within %d steps: the step cycles through %d resident "
                                 "blocks of %.0f MB (%.0f MB in all, > the 256 MB Infinity "

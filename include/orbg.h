@@ -435,6 +435,27 @@ int orbg_ba_linearize_device(orbg_ctx *ctx, const orbg_pose *d_poses, int npose,
                              orbg_edge_out *d_eout, double *d_hpose, double *d_bpose,
                              double *d_hpoint, double *d_bpoint);
 
+/* g2o's per-trial error pass for the two LBA edge types: SparseOptimizer::
+ * computeActiveErrors (Thirdparty/g2o/g2o/core/sparse_optimizer.cpp:61-76, computeError
+ * types_six_dof_expmap.h:90-95, 122-127) and the terms activeRobustChi2 sums (:100-114,
+ * RobustKernelHuber::robustify robust_kernel_impl.cpp:78-91), plus isDepthPositive
+ * (types_six_dof_expmap.h:97-101, 129-133) for LocalBundleAdjustment's outlier test
+ * (Optimizer.cc:871-901).  The LM calls this after every trial update, buildSystem
+ * (orbg_ba_linearize) once per iteration.  For every edge given, active or not:
+ *   err[3e .. 3e+2] the error (third entry 0 for mono; NULL: not stored),
+ *   chi2[e] = e^T Omega e, rho0[e] = Huber rho[0](chi2) if edges[e].robust else chi2 (NULL:
+ *   not stored), depth_ok[e] = camera-frame depth > 0 (NULL: not stored);
+ * *active_robust_chi2 (NULL: not computed) = the sum of rho0 over the active edges in the
+ * order given (pass them in g2o's _activeEdges order).  Host arrays. */
+int orbg_ba_errors(orbg_ctx *ctx, const orbg_pose *poses, int npose, const double *points,
+                   int npoint, const orbg_edge *edges, int nedge, double *err, double *chi2,
+                   double *rho0, uint8_t *depth_ok, double *active_robust_chi2);
+/* Device-resident form (no sum): every pointer device memory, enqueued on the context
+ * stream; d_chi2 required, d_err / d_rho0 / d_depth_ok may be NULL. */
+int orbg_ba_errors_device(orbg_ctx *ctx, const orbg_pose *d_poses, const double *d_points,
+                          const orbg_edge *d_edges, int nedge, double *d_err, double *d_chi2,
+                          double *d_rho0, uint8_t *d_depth_ok);
+
 /* Whether orbg_ba_linearize_device stores the per-edge Jacobians eout.jp / eout.jt (g2o's
  * _jacobianOplusXi / Xj; default on).  Off, those fields are left as they are and every
  * other output is unchanged: the blocks, H_pl and orbg_ba_schur_solve do not read them. */

@@ -231,6 +231,44 @@ void orc_ba_linearize(const orc_pose *poses, int npose, const double *points, in
     }
 }
 
+/* SparseOptimizer::computeActiveErrors (sparse_optimizer.cpp:61-76: e->computeError() per
+ * edge), the robustified chi2 activeRobustChi2 sums (:100-114; RobustKernelHuber::robustify,
+ * robust_kernel_impl.cpp:78-91, with its float dsqr member, robust_kernel_impl.h:84) and
+ * isDepthPositive (types_six_dof_expmap.h:97-101, 129-133), for every edge given.  Returns the
+ * sum of the robust chi2 over the active edges in edge order.  Any output may be NULL. */
+double orc_ba_errors(const orc_pose *poses, const double *points, const orc_edge *edges,
+                     int nedge, double *err, double *chi2, double *rho0, uint8_t *depth_ok)
+{
+    double total = 0;
+    for (int i = 0; i < nedge; i++) {
+        const orc_edge *e = &edges[i];
+        double ev[3], xc[3];
+        edge_error(&poses[e->pose], points + 3 * (size_t)e->point, e, ev, xc);
+        const int D = e->stereo ? 3 : 2;
+        double c = 0;
+        for (int k = 0; k < D; k++)
+            c += ev[k] * (e->inv_sigma2 * ev[k]);
+        double r = c;
+        if (e->robust) {
+            const float dsqr = (float)(e->huber_delta * e->huber_delta);
+            if (!(c <= dsqr))
+                r = 2 * sqrt(c) * e->huber_delta - dsqr;
+        }
+        if (err)
+            for (int k = 0; k < 3; k++)
+                err[3 * (size_t)i + k] = ev[k];
+        if (chi2)
+            chi2[i] = c;
+        if (rho0)
+            rho0[i] = r;
+        if (depth_ok)
+            depth_ok[i] = xc[2] > 0.0;
+        if (e->active)
+            total += r;
+    }
+    return total;
+}
+
 /* SE3Quat::exp(update) * T applied in rotation-matrix form (se3quat.h:223-257) */
 static void oplus_pose(const double R[3][3], const double t[3], const double upd[6],
                        double R2[3][3], double t2[3])

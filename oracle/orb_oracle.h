@@ -299,6 +299,8 @@ typedef struct {
 void orc_ba_linearize(const orc_pose *poses, int npose, const double *points, int npoint,
                       const orc_edge *edges, int nedge, orc_edge_out *eout, double *hpose,
                       double *bpose, double *hpoint, double *bpoint);
+double orc_ba_errors(const orc_pose *poses, const double *points, const orc_edge *edges,
+                     int nedge, double *err, double *chi2, double *rho0, uint8_t *depth_ok);
 /* BlockSolver_6_3::solve with the Schur complement (block_solver.hpp:354-486) after
  * setLambda(lambda): inputs are orc_ba_linearize's outputs (hpl = A^T W B per edge).
  * dx_pose[npose*6] (0 for fixed poses), dx_point[npoint*3] (0 for points without an

@@ -146,6 +146,8 @@ def lib():
         L.orc_extract_batch.restype = C.c_long
         L.orc_ba_linearize.argtypes = [vp, C.c_int, vp, C.c_int, vp, C.c_int, vp, vp, vp, vp, vp]
         L.orc_ba_numeric_jacobian.argtypes = [vp, vp, vp, vp, vp]
+        L.orc_ba_errors.argtypes = [vp, vp, vp, C.c_int, vp, vp, vp, vp]
+        L.orc_ba_errors.restype = C.c_double
         L.orc_ba_schur_solve.argtypes = [vp, C.c_int, C.c_int, vp, C.c_int, vp, vp, vp, vp, vp,
                                          C.c_double, vp, vp]
         L.orc_stereo_matches.argtypes = [P(Params), vp, vp, C.c_int, vp, vp, C.c_int, vp, vp,
@@ -417,6 +419,22 @@ def ba_linearize(poses, points, edges):
     lib().orc_ba_linearize(_p(poses), npose, _p(points), npoint, _p(edges), nedge, _p(eout),
                            _p(hpose), _p(bpose), _p(hpoint), _p(bpoint))
     return eout, hpose, bpose, hpoint, bpoint
+
+
+def ba_errors(poses, points, edges):
+    """computeActiveErrors + activeRobustChi2 + isDepthPositive restated (orc_ba_errors):
+    returns (err (n, 3), chi2 (n,), rho0 (n,), depth_ok (n,) bool, active robust chi2 sum)."""
+    poses = np.ascontiguousarray(poses, POSE_DTYPE)
+    points = np.ascontiguousarray(points, np.float64)
+    edges = np.ascontiguousarray(edges, EDGE_DTYPE)
+    n = len(edges)
+    err = np.zeros((max(n, 1), 3))
+    chi2 = np.zeros(max(n, 1))
+    rho0 = np.zeros(max(n, 1))
+    dok = np.zeros(max(n, 1), np.uint8)
+    tot = lib().orc_ba_errors(_p(poses), _p(points), _p(edges), n, _p(err), _p(chi2), _p(rho0),
+                              _p(dok))
+    return err[:n], chi2[:n], rho0[:n], dok[:n].astype(bool), tot
 
 
 def ba_numeric_jacobian(pose, xyz, edge):

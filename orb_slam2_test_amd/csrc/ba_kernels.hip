@@ -33,6 +33,87 @@ __device__ __forceinline__ void quat_rotate(const double q[4], const double v[3]
     o[2] = v[2] + q[3] * uv[2] + (q[0] * uv[1] - q[1] * uv[0]);
 }
 
+// computeError (types_six_dof_expmap.h:90-95, 122-127): Xc = q X + t, then the mono
+// projection in double, or the stereo cam_project with its float invz and float bf
+// (types_six_dof_expmap.cpp:150-157); err[2] = 0 for a mono edge
+__device__ __forceinline__ void ba_edge_error(const orbg_pose &P, const double X[3],
+                                              const orbg_edge &e, double xc[3], double err[3])
+{
+    quat_rotate(P.q, X, xc);
+    xc[0] += P.t[0];
+    xc[1] += P.t[1];
+    xc[2] += P.t[2];
+    const double x = xc[0], y = xc[1], z = xc[2];
+    err[2] = 0;
+    if (!e.stereo) {
+        err[0] = e.obs[0] - ((x / z) * e.fx + e.cx);
+        err[1] = e.obs[1] - ((y / z) * e.fy + e.cy);
+    } else {
+        const float invz = (float)(1.0f / z);
+        const float bf = (float)e.bf;
+        const double u = x * invz * e.fx + e.cx;
+        const double v = y * invz * e.fy + e.cy;
+        err[0] = e.obs[0] - u;
+        err[1] = e.obs[1] - v;
+        err[2] = e.obs[2] - (u - (double)(bf * invz));
+    }
+}
+
+// ---------------------------------------------------------------------------
+// k_ba_errors: g2o's per-trial error pass (SparseOptimizer::computeActiveErrors,
+// sparse_optimizer.cpp:61-76) and the terms activeRobustChi2 sums (:100-114): thread per
+// edge, every edge given (active or not); err / rho0 / depth_ok may be NULL.
+//   chi2 = e^T Omega e (base_edge.h:58-61), rho0 = RobustKernelHuber::robustify's rho[0]
+//   with its float dsqr (robust_kernel_impl.cpp:78-91) or chi2 without a kernel,
+//   depth_ok = isDepthPositive (types_six_dof_expmap.h:97-101, 129-133).
+// 28 B out per edge (err as f64 x 3 only on request).
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void k_ba_errors(const orbg_pose *__restrict__ poses,
+                                                   const double *__restrict__ points,
+                                                   const orbg_edge *__restrict__ edges, int nedge,
+                                                   double *__restrict__ err_out,
+                                                   double *__restrict__ chi2_out,
+                                                   double *__restrict__ rho0_out,
+                                                   uint8_t *__restrict__ depth_ok)
+{
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= nedge) return;
+    const orbg_edge &e = edges[i];
+    const int ip = e.pose, iq = e.point;
+    const orbg_pose P = poses[ip];
+    const double X[3] = {points[3 * iq], points[3 * iq + 1], points[3 * iq + 2]};
+    double xc[3], err[3];
+    ba_edge_error(P, X, e, xc, err);
+    const double info = e.inv_sigma2;
+    double chi2 = 0;
+#pragma unroll
+    for (int k = 0; k < 3; k++) chi2 += err[k] * (info * err[k]);  // mono: + exact 0
+    double rho0 = chi2;
+    if (e.robust) {
+        const float dsqr = (float)(e.huber_delta * e.huber_delta);
+        if (!(chi2 <= dsqr)) rho0 = 2 * sqrt(chi2) * e.huber_delta - dsqr;
+    }
+    chi2_out[i] = chi2;
+    if (rho0_out) rho0_out[i] = rho0;
+    if (depth_ok) depth_ok[i] = xc[2] > 0.0;
+    if (err_out)
+#pragma unroll
+        for (int k = 0; k < 3; k++) err_out[3 * (size_t)i + k] = err[k];
+}
+
+int launch_ba_errors(hipStream_t st, const orbg_pose *poses, const double *points,
+                     const orbg_edge *edges, int nedge, double *err, double *chi2, double *rho0,
+                     uint8_t *depth_ok, void *prof)
+{
+    if (nedge <= 0) return 0;
+    hipEvent_t a = nullptr;
+    prof_begin(prof, st, "ba_errors", &a);
+    hipLaunchKernelGGL(k_ba_errors, dim3((nedge + 255) / 256), dim3(256), 0, st, poses, points,
+                       edges, nedge, err, chi2, rho0, depth_ok);
+    prof_end(prof, st, "ba_errors", a);
+    return hipGetLastError() == hipSuccess ? 0 : -5;
+}
+
 // ---------------------------------------------------------------------------
 // k_ba_edges: thread per edge.  Per-edge outputs go straight to global (no 400-byte live
 // struct); point blocks are accumulated with fp64 atomics (a point has ~4-5 observations,
@@ -76,27 +157,11 @@ __global__ __launch_bounds__(256) void k_ba_edges(const orbg_pose *__restrict__ 
     }
     const orbg_pose P = poses[e.pose];
     const double X[3] = {points[3 * e.point], points[3 * e.point + 1], points[3 * e.point + 2]};
-    double xc[3];
-    quat_rotate(P.q, X, xc);
-    xc[0] += P.t[0];
-    xc[1] += P.t[1];
-    xc[2] += P.t[2];
+    double xc[3], err[3];
+    ba_edge_error(P, X, e, xc, err);
     const double x = xc[0], y = xc[1], z = xc[2], z_2 = z * z;
     const double fx = e.fx, fy = e.fy;
     const int D = e.stereo ? 3 : 2;
-    double err[3] = {0, 0, 0};
-    if (!e.stereo) {
-        err[0] = e.obs[0] - ((x / z) * fx + e.cx);
-        err[1] = e.obs[1] - ((y / z) * fy + e.cy);
-    } else {
-        const float invz = (float)(1.0f / z);
-        const float bf = (float)e.bf;
-        const double u = x * invz * fx + e.cx;
-        const double v = y * invz * fy + e.cy;
-        err[0] = e.obs[0] - u;
-        err[1] = e.obs[1] - v;
-        err[2] = e.obs[2] - (u - (double)(bf * invz));
-    }
     // rotation matrix (Eigen toRotationMatrix)
     const double *q = P.q;
     const double tx = 2 * q[0], ty = 2 * q[1], tz = 2 * q[2];

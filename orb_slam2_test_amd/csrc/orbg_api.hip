@@ -92,6 +92,9 @@ int launch_stereo(hipStream_t st, const OrbgGeom &g, const orbg_keypoint *kps,
                   int img_pitch, const uint8_t *pyr, float bf, float min_z, void *scratch,
                   float *uright, float *depth, int32_t *nvalid, void *prof);
 size_t ba_scratch_bytes(int npose, int npoint, int nedge);
+int launch_ba_errors(hipStream_t st, const orbg_pose *poses, const double *points,
+                     const orbg_edge *edges, int nedge, double *err, double *chi2, double *rho0,
+                     uint8_t *depth_ok, void *prof);
 }  // namespace orbg
 
 using namespace orbg;
@@ -2252,6 +2255,15 @@ extern "C" int orbg_search_for_initialization(orbg_ctx *c, const orbg_keypoint *
 // ---------------------------------------------------------------------------
 // local BA
 // ---------------------------------------------------------------------------
+static int ba_check_edges(const orbg_edge *edges, int nedge, int npose, int npoint)
+{
+    for (int i = 0; i < nedge; i++)
+        if (edges[i].pose < 0 || edges[i].pose >= npose || edges[i].point < 0 ||
+            edges[i].point >= npoint)
+            return set_err(ORBG_EINVAL, "edge %d references a missing vertex", i);
+    return ORBG_OK;
+}
+
 extern "C" int orbg_ba_linearize(orbg_ctx *c, const orbg_pose *poses, int npose,
                                  const double *points, int npoint, const orbg_edge *edges,
                                  int nedge, orbg_edge_out *eout, double *hpose, double *bpose,
@@ -2259,10 +2271,7 @@ extern "C" int orbg_ba_linearize(orbg_ctx *c, const orbg_pose *poses, int npose,
 {
     if (!c) return set_err(ORBG_EINVAL, "ctx is NULL");
     if (npose < 0 || npoint < 0 || nedge < 0) return set_err(ORBG_EINVAL, "negative size");
-    for (int i = 0; i < nedge; i++)
-        if (edges[i].pose < 0 || edges[i].pose >= npose || edges[i].point < 0 ||
-            edges[i].point >= npoint)
-            return set_err(ORBG_EINVAL, "edge %d references a missing vertex", i);
+    if (int rc0 = ba_check_edges(edges, nedge, npose, npoint)) return rc0;
     HIPCHK(hipSetDevice(c->device));
     // edge lists per pose and per point (CSR): MFMA pose blocks, summed point blocks
     std::vector<int32_t> off(npose + 1, 0), pe(nedge > 0 ? nedge : 1);
@@ -2289,6 +2298,83 @@ extern "C" int orbg_ba_linearize(orbg_ctx *c, const orbg_pose *poses, int npose,
     if (rc) return rc;
     HIPCHK(hipStreamSynchronize(c->stream));
     c->prof.collect();
+    return ORBG_OK;
+}
+
+extern "C" int orbg_ba_errors(orbg_ctx *c, const orbg_pose *poses, int npose, const double *points,
+                              int npoint, const orbg_edge *edges, int nedge, double *err,
+                              double *chi2, double *rho0, uint8_t *depth_ok,
+                              double *active_robust_chi2)
+{
+    if (!c) return set_err(ORBG_EINVAL, "ctx is NULL");
+    if (npose < 0 || npoint < 0 || nedge < 0) return set_err(ORBG_EINVAL, "negative size");
+    if (nedge && (!poses || !points || !edges)) return set_err(ORBG_EINVAL, "NULL array");
+    int rc = ba_check_edges(edges, nedge, npose, npoint);
+    if (rc) return rc;
+    if (active_robust_chi2) *active_robust_chi2 = 0;
+    if (nedge == 0) return ORBG_OK;
+    HIPCHK(hipSetDevice(c->device));
+    const size_t ne = (size_t)nedge;
+    size_t o = 0;
+    const size_t opo = o;
+    o += al256((size_t)npose * sizeof(orbg_pose));
+    const size_t opt = o;
+    o += al256((size_t)npoint * 24);
+    const size_t oed = o;
+    o += al256(ne * sizeof(orbg_edge));
+    const size_t oer = o;  // outputs: err, chi2, rho0, depth_ok (one D2H copy)
+    o += al256(ne * 24);
+    const size_t och = o;
+    o += al256(ne * 8);
+    const size_t orh = o;
+    o += al256(ne * 8);
+    const size_t odk = o;
+    o += al256(ne);
+    void *sp;
+    if ((rc = scratch(c, o, &sp))) return rc;
+    uint8_t *b = (uint8_t *)sp;
+    HIPCHK(hipMemcpyAsync(b + opo, poses, (size_t)npose * sizeof(orbg_pose), hipMemcpyHostToDevice,
+                          c->stream));
+    HIPCHK(hipMemcpyAsync(b + opt, points, (size_t)npoint * 24, hipMemcpyHostToDevice, c->stream));
+    HIPCHK(hipMemcpyAsync(b + oed, edges, ne * sizeof(orbg_edge), hipMemcpyHostToDevice, c->stream));
+    if ((rc = launch_ba_errors(c->stream, (const orbg_pose *)(b + opo), (const double *)(b + opt),
+                               (const orbg_edge *)(b + oed), nedge, (double *)(b + oer),
+                               (double *)(b + och), (double *)(b + orh), b + odk, &c->prof)))
+        return set_err(ORBG_EIO, "k_ba_errors launch failed");
+    std::vector<uint8_t> h(o - oer);
+    HIPCHK(hipMemcpyAsync(h.data(), b + oer, h.size(), hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(hipStreamSynchronize(c->stream));
+    c->prof.collect();
+    const double *herr = (const double *)h.data(), *hchi = (const double *)(h.data() + och - oer),
+                 *hrho = (const double *)(h.data() + orh - oer);
+    const uint8_t *hdk = h.data() + odk - oer;
+    if (err) std::memcpy(err, herr, ne * 24);
+    if (chi2) std::memcpy(chi2, hchi, ne * 8);
+    if (rho0) std::memcpy(rho0, hrho, ne * 8);
+    if (depth_ok) std::memcpy(depth_ok, hdk, ne);
+    if (active_robust_chi2) {
+        // activeRobustChi2's sum, in the caller's edge order (sparse_optimizer.cpp:100-114)
+        double t = 0;
+        for (int i = 0; i < nedge; i++)
+            if (edges[i].active) t += hrho[i];
+        *active_robust_chi2 = t;
+    }
+    return ORBG_OK;
+}
+
+extern "C" int orbg_ba_errors_device(orbg_ctx *c, const orbg_pose *d_poses,
+                                     const double *d_points, const orbg_edge *d_edges, int nedge,
+                                     double *d_err, double *d_chi2, double *d_rho0,
+                                     uint8_t *d_depth_ok)
+{
+    if (!c) return set_err(ORBG_EINVAL, "ctx is NULL");
+    if (nedge < 0) return set_err(ORBG_EINVAL, "negative size");
+    if (nedge && (!d_poses || !d_points || !d_edges || !d_chi2))
+        return set_err(ORBG_EINVAL, "NULL device array");
+    HIPCHK(hipSetDevice(c->device));
+    if (launch_ba_errors(c->stream, d_poses, d_points, d_edges, nedge, d_err, d_chi2, d_rho0,
+                         d_depth_ok, &c->prof))
+        return set_err(ORBG_EIO, "k_ba_errors launch failed");
     return ORBG_OK;
 }
 

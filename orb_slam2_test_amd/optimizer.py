@@ -41,6 +41,26 @@ def linearize_local_ba(poses, points, edges, device=0, with_edges=True):
     return eout, hpose, bpose, hpoint, bpoint
 
 
+def ba_errors(poses, points, edges, device=0):
+    """g2o's per-trial error pass (computeActiveErrors + activeRobustChi2 terms +
+    isDepthPositive, sparse_optimizer.cpp:61-114, orbg_ba_errors) for the LBA edges.
+    Returns (err (n, 3), chi2 (n,), rho0 (n,), depth_ok (n,) bool, active robust chi2 sum in
+    edge order)."""
+    poses = np.ascontiguousarray(poses, L.POSE_DTYPE)
+    points = np.ascontiguousarray(points, np.float64).reshape(-1, 3)
+    edges = np.ascontiguousarray(edges, L.EDGE_DTYPE)
+    n = len(edges)
+    err = np.zeros((max(n, 1), 3))
+    chi2 = np.zeros(max(n, 1))
+    rho0 = np.zeros(max(n, 1))
+    dok = np.zeros(max(n, 1), np.uint8)
+    tot = ctypes.c_double()
+    L.check(L.lib().orbg_ba_errors(_ctx(device).handle, L.ptr(poses), len(poses), L.ptr(points),
+                                   len(points), L.ptr(edges), n, L.ptr(err), L.ptr(chi2),
+                                   L.ptr(rho0), L.ptr(dok), ctypes.byref(tot)), "orbg_ba_errors")
+    return err[:n], chi2[:n], rho0[:n], dok[:n].astype(bool), tot.value
+
+
 def ba_schur_solve(poses, npoint, edges, eout, hpose, bpose, hpoint, bpoint, lam, device=0):
     """g2o BlockSolver<6,3>::solve (block_solver.hpp:354-486) after setLambda(lam), on
     linearize_local_ba's outputs.  Returns (ok, dx_pose (npose, 6), dx_point (npoint, 3))."""

@@ -1,9 +1,9 @@
 #!/bin/bash
 # Interleaved A/B of library variants with the serial per-kernel times (bench.py's HIP-event
 # pass) beside the pipelined ms_per_step:
-#   gpurun -- bash tools/r02_abk.sh <tag> <rounds> <variant|default> ...
+#   gpurun -- bash tools/ab.sh <tag> <rounds> <variant|default> ...
 set -e -o pipefail
-O=gpurun_out/${1:-r02abk}
+O=gpurun_out/${1:-abk}
 R=${2:-2}
 shift 2
 mkdir -p $O

@@ -1,6 +1,11 @@
 #!/usr/bin/env python3
-"""Per-kernel PMC summary (profiles/pmc_kernels*.json) from rocprofv3 --pmc passes, each in
-its own run directory (tools/r02_profile.sh).  Counters are averaged per dispatch.
+"""Per-kernel PMC summary (profiles/*pmc_kernels.json) from rocprofv3 --pmc passes, each in
+its own run directory (tools/profile.sh).  Counters are averaged per dispatch; with the
+number of steps the profiled run issued (argument 3, > 0) the per-step sums are given too.
+bench.py's roofline prices one launch of its serial pass (orbg_set_serial: one dispatch per
+kernel and step, except octree's two by design), so the PMC run is that serial pass
+(tools/round_prof.sh) and hbm_bytes_per_launch is directly comparable with
+algo_bytes_per_launch.
 
 - hbm_bytes_per_launch = 2 * FETCH_SIZE + WRITE_SIZE (KiB counters; the gfx950 FETCH_SIZE
   halving of MI355X_MICROARCH.md 'HBM'; Infinity-Cache hits count as fetched).
@@ -12,7 +17,7 @@ its own run directory (tools/r02_profile.sh).  Counters are averaged per dispatc
 - lds_frac = SQ_LDS_IDX_ACTIVE / (256 CUs * cycles): fraction of the LDS array cycles.
 - mfma_frac = SQ_VALU_MFMA_BUSY_CYCLES / (1024 SIMDs * cycles).
 
-usage: pmc_kernels.py <dir with pmc*/run_counter_collection.csv> <out.json>
+usage: pmc_kernels.py <dir with pmc*/run_counter_collection.csv> <out.json> [steps]
 """
 import csv
 import glob
@@ -25,7 +30,8 @@ sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
 from kernel_keys import key  # noqa: E402
 
 
-def main(d, out):
+def main(d, out, steps="0"):
+    steps = int(steps)
     acc = defaultdict(lambda: defaultdict(list))
     for path in glob.glob(os.path.join(d, "*", "run_counter_collection.csv")):
         for r in csv.DictReader(open(path)):
@@ -40,6 +46,12 @@ def main(d, out):
             e["fetch_size_raw_bytes"] = int(a["FETCH_SIZE"] * 1024)
             e["write_size_bytes"] = int(a["WRITE_SIZE"] * 1024)
             e["hbm_bytes_per_launch"] = int((2 * a["FETCH_SIZE"] + a["WRITE_SIZE"]) * 1024)
+            if steps > 0:
+                nd = len(c["FETCH_SIZE"])
+                e["steps"] = steps
+                e["dispatches_per_step"] = round(nd / steps, 3)
+                e["hbm_bytes_per_step"] = int((2 * sum(c["FETCH_SIZE"]) + sum(c["WRITE_SIZE"]))
+                                              * 1024 / steps)
         wc = a.get("SQ_WAVE_CYCLES")
         if wc:
             for n in ("SQ_WAIT_INST_ANY", "SQ_WAIT_ANY", "SQ_ACTIVE_INST_ANY"):

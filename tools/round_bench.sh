@@ -1,9 +1,9 @@
 #!/bin/bash
-# Round-end measurement set (one gpurun call): the -m gpu suite, every bench line with its
-# CPU baseline, the BA / single-frame / C1 benches, then the kernel trace + PMC profile.
-#   gpurun --timeout 1200 -- bash tools/r02_final.sh <tag>
+# Round-end measurement set, part 1 (one gpurun call): the -m gpu suite, every bench line with its
+# CPU baseline, the BA / single-frame / C1 benches (part 2, the profiles: tools/round_prof.sh).
+#   gpurun --timeout 1200 -- bash tools/round_bench.sh <tag>
 set -e -o pipefail
-TAG=${1:-r02final}
+TAG=${1:-r03final}
 O=gpurun_out/$TAG
 mkdir -p $O
 echo "[final] pytest -m gpu"
@@ -27,6 +27,4 @@ timeout -k 10 200 python tools/single_frame_bench.py 200 640 480 1000 >> $O/sing
 echo "[final] C1"
 timeout -k 10 300 python tools/c1_bench.py 16 > $O/c1.json 2> $O/c1.err
 cat $O/c1.json
-echo "[final] profile"
-timeout -k 10 600 bash tools/r02_profile.sh ${TAG}_prof > $O/profile.log 2>&1 || { tail -20 $O/profile.log; exit 1; }
 echo "[final] done"
