@@ -387,6 +387,19 @@ int orbg_pose_optimization_batch_device(orbg_ctx *ctx, const orbg_pose_edge *edg
                                         double *q_out, double *t_out, float *tcw_out,
                                         uint8_t *outlier, int32_t *ninliers, int nframes);
 
+/* The per-frame pose of the batched-sequence mode (SURVEY.md 8e "pose/trajectory stub"):
+ * Optimizer::PoseOptimization (src/Optimizer.cc:356-631) of frame f2[p] of every pair of the
+ * last orbg_match_batch_device, with that call's SearchForInitialization matches as the map
+ * points: F1 keypoint i matched to F2 keypoint j gives one mono edge, obs = F2 keypoint j,
+ * Xw = F1 keypoint i back-projected at `depth` in F1's camera ((x - cx) z / fx,
+ * (y - cy) z / fy, z), Omega = mvInvLevelSigma2[octave of j]; edges in F2 index order (the
+ * reference's loop over pFrame's keypoints); initial pose identity (F1's camera = world).
+ * Outputs per pair on the match stream (device memory): d_q[4p..4p+3] the SE3Quat rotation
+ * (x, y, z, w), d_t[3p..3p+2] its translation (F2's pose relative to F1) and d_ninliers[p]
+ * (PoseOptimization's return value). */
+int orbg_match_pose_batch_device(orbg_ctx *ctx, const orbg_pose_camera *cam, float depth,
+                                 double *d_q, double *d_t, int32_t *d_ninliers);
+
 /* ---------------- local BA linearisation ---------------- */
 typedef struct {
     double q[4]; /* SE3Quat rotation, Eigen coeffs order (x, y, z, w), normalised */

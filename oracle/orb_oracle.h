@@ -230,6 +230,9 @@ int orc_pose_optimization(const orc_pose_edge *edges, int n, const orc_pose_cam 
                           const float Tcw_in[12], double q_out[4], double t_out[3],
                           float Tcw_out[12], uint8_t *outlier);
 void orc_se3_from_tcw(const float Tcw[12], double q[4], double t[3]);
+int orc_match_pose(const orc_keypoint *k1, int n1, const orc_keypoint *k2, int n2,
+                   const int32_t *m12, const orc_pose_cam *cam, float depth,
+                   const float *inv_sigma2, double q[4], double t[3]);
 void orc_se3_to_tcw(const double q[4], const double t[3], float Tcw[12]);
 void orc_se3_oplus(double q[4], double t[3], const double upd[6]);
 int orc_ldlt_solve6(const double H[6][6], const double b[6], double x[6]);

@@ -587,3 +587,47 @@ int orc_pose_optimization(const orc_pose_edge *edges, int n, const orc_pose_cam 
     free(act);
     return n - nBad;
 }
+
+/* The batched-sequence mode's per-frame pose (the "trajectory stub" of SURVEY.md 8e;
+ * liborbg's orbg_match_pose_batch_device): Optimizer::PoseOptimization (Optimizer.cc:356-631)
+ * of frame 2 with SearchForInitialization's vnMatches12 (m12[i] = j) as its map points.  F1
+ * keypoint i matched to F2 keypoint j gives the mono edge obs = (x2_j, y2_j), Xw = F1 keypoint
+ * i back-projected at `depth` in F1's camera ((x1 - cx) * z / fx, (y1 - cy) * z / fy, z, in
+ * float), Omega = inv_sigma2[octave of j]; edges in F2 index order (PoseOptimization's loop
+ * over pFrame's keypoints, Optimizer.cc:381); initial pose identity (F1 = world).  Returns
+ * the inlier count; q / t = F2's pose relative to F1. */
+int orc_match_pose(const orc_keypoint *k1, int n1, const orc_keypoint *k2, int n2,
+                   const int32_t *m12, const orc_pose_cam *cam, float depth,
+                   const float *inv_sigma2, double q[4], double t[3])
+{
+    int *inv = (int *)malloc(sizeof(int) * (size_t)(n2 > 0 ? n2 : 1));
+    for (int j = 0; j < n2; j++)
+        inv[j] = -1;
+    for (int i = 0; i < n1; i++)
+        if (m12[i] >= 0 && m12[i] < n2)
+            inv[m12[i]] = i;
+    orc_pose_edge *e = (orc_pose_edge *)malloc(sizeof(orc_pose_edge) * (size_t)(n2 > 0 ? n2 : 1));
+    int n = 0;
+    for (int j = 0; j < n2; j++) {
+        const int i = inv[j];
+        if (i < 0)
+            continue;
+        orc_pose_edge *E = &e[n++];
+        E->obs[0] = k2[j].x;
+        E->obs[1] = k2[j].y;
+        E->obs[2] = -1.f;
+        E->xw[0] = (k1[i].x - cam->cx) * depth / cam->fx;
+        E->xw[1] = (k1[i].y - cam->cy) * depth / cam->fy;
+        E->xw[2] = depth;
+        E->inv_sigma2 = inv_sigma2[k2[j].octave];
+        E->stereo = 0;
+    }
+    const float T0[12] = {1, 0, 0, 0, 0, 1, 0, 0, 0, 0, 1, 0};
+    float To[12];
+    uint8_t *out = (uint8_t *)malloc((size_t)(n > 0 ? n : 1));
+    const int ninl = orc_pose_optimization(e, n, cam, T0, q, t, To, out);
+    free(out);
+    free(e);
+    free(inv);
+    return ninl;
+}

@@ -155,6 +155,7 @@ def lib():
         L.orc_track_direction.argtypes = [vp, vp, vp]
         L.orc_pose_optimization.argtypes = [vp, C.c_int, vp, vp, vp, vp, vp, vp]
         L.orc_se3_from_tcw.argtypes = [vp, vp, vp]
+        L.orc_match_pose.argtypes = [vp, C.c_int, vp, C.c_int, vp, vp, C.c_float, vp, vp, vp]
         L.orc_search_by_projection_lastframe.argtypes = [vp, vp, vp, C.c_int, vp, vp, vp, vp,
                                                          vp, C.c_int, vp, C.c_float, C.c_int,
                                                          vp]
@@ -435,6 +436,32 @@ def ba_errors(poses, points, edges):
     tot = lib().orc_ba_errors(_p(poses), _p(points), _p(edges), n, _p(err), _p(chi2), _p(rho0),
                               _p(dok))
     return err[:n], chi2[:n], rho0[:n], dok[:n].astype(bool), tot
+
+
+def match_pose(p, kps1, kps2, m12, cam, depth):
+    """The batched-sequence per-frame pose (orc_match_pose): PoseOptimization of frame 2 over
+    vnMatches12 with F1's keypoints back-projected at `depth`.  cam = (fx, fy, cx, cy, bf).
+    Returns (ninliers, q (x, y, z, w), t)."""
+    k1 = np.ascontiguousarray(kps1, KP_DTYPE)
+    k2 = np.ascontiguousarray(kps2, KP_DTYPE)
+    m = np.ascontiguousarray(m12, np.int32)
+    c = PoseCam(*[float(np.float32(v)) for v in cam], 0.0)
+    inv2 = np.ascontiguousarray(np.asarray(p.inv_sigma2[:p.nlevels], np.float32))
+    q = np.zeros(4)
+    t = np.zeros(3)
+    n = lib().orc_match_pose(_p(k1), len(k1), _p(k2), len(k2), _p(m), C.byref(c),
+                             float(depth), _p(inv2), _p(q), _p(t))
+    return n, q, t
+
+
+def se3_from_tcw(Tcw):
+    """Converter::toSE3Quat restated (orc_se3_from_tcw): rows 0..2 of a float pose ->
+    (q (x, y, z, w) normalised, t)."""
+    T = np.ascontiguousarray(np.asarray(Tcw, np.float32).reshape(-1)[:12])
+    q = np.zeros(4)
+    t = np.zeros(3)
+    lib().orc_se3_from_tcw(_p(T), _p(q), _p(t))
+    return q, t
 
 
 def ba_numeric_jacobian(pose, xyz, edge):

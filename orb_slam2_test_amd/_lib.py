@@ -148,6 +148,7 @@ def lib():
         "orbg_batch_summary": (i32, [vp, vp]),
         "orbg_batch_matches": (i32, [vp, vp, vp]),
         "orbg_batch_acquire": (i32, [vp, vp]),
+        "orbg_match_pose_batch_device": (i32, [vp, P(PoseCamera), f32, vp, vp, vp]),
         "orbg_batch_release": (i32, [vp, vp]),
         "orbg_stereo_batch_device": (i32, [vp, vp, vp, i32, f32, f32]),
         "orbg_stereo_outputs": (i32, [vp, vp, vp, vp, vp]),

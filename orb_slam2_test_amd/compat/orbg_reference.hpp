@@ -44,9 +44,13 @@ namespace orbg_compat {
 namespace ref {
 
 // The context behind ORBmatcher / Optimizer call sites, which the reference constructs
-// freely (ORBmatcher matcher(0.9, true) on the stack): one per process, device 0, default
-// parameters (scale factor 1.2, 8 levels: the ORBextractor settings the tracking matchers'
-// scale tables must agree with).  Created on first use.
+// freely (ORBmatcher matcher(0.9, true) on the stack): ONE PER CALLING THREAD, device 0,
+// default parameters (scale factor 1.2, 8 levels: the ORBextractor settings the tracking
+// matchers' scale tables must agree with), created on the thread's first use and destroyed
+// at its exit.  The reference calls the matchers and PoseOptimization on the Tracking thread
+// while LocalMapping runs LocalBundleAdjustment (System.cc:117, LocalMapping.cc:99), and a
+// liborbg context is not thread-safe (include/orbg.h), so each thread gets its own context
+// (its own streams, planning state and scratch); distinct contexts run concurrently.
 inline orbg_ctx *default_ctx()
 {
     struct Holder {
@@ -59,7 +63,7 @@ inline orbg_ctx *default_ctx()
         }
         ~Holder() { orbg_destroy(c); }
     };
-    static Holder h;
+    static thread_local Holder h;
     return h.c;
 }
 
@@ -350,8 +354,11 @@ inline orbg_pose se3quat_of(const float T[12], int fixed)
 // The vertices and edges Optimizer::LocalBundleAdjustment puts into g2o (Optimizer.cc:
 // 662-851) as liborbg's SoA: poses = lLocalKeyFrames (fixed iff mnId == 0) then
 // lFixedCameras (fixed); points = lLocalMapPoints (xyz); one edge per observation of a local
-// map point by a local or fixed key frame that is not bad, mono when mvuRight < 0 (Huber
-// delta sqrt(5.991)) else stereo (sqrt(7.815)), information = mvInvLevelSigma2[octave].
+// map point by a local or fixed key frame that is not bad, in the map point's observation
+// order (std::map<KeyFrame*, size_t>), mono when mvuRight < 0 (Huber delta (float)sqrt(5.991))
+// else stereo ((float)sqrt(7.815)), information = mvInvLevelSigma2[octave].  (The reference
+// adds an edge for every observing key frame that is not bad, Optimizer.cc:783-848; its
+// lFixedCameras hold all of them, :672-686, so the "in the window" test never drops one there.)
 template <class KeyFrameT, class MapPointT>
 struct LbaWindow {
     std::vector<orbg_pose> poses;
@@ -378,7 +385,8 @@ LbaWindow<KeyFrameT, MapPointT> build_lba_window(const std::list<KeyFrameT *> &l
     };
     for (KeyFrameT *pKFi : lLocalKeyFrames) add_kf(pKFi, pKFi->mnId == 0 ? 1 : 0);
     for (KeyFrameT *pKFi : lFixedCameras) add_kf(pKFi, 1);
-    const double thHuberMono = std::sqrt(5.991), thHuberStereo = std::sqrt(7.815);
+    // float in the reference (Optimizer.cc:758-759), then RobustKernelHuber::setDelta(double)
+    const float thHuberMono = std::sqrt(5.991), thHuberStereo = std::sqrt(7.815);
     for (MapPointT *pMP : lLocalMapPoints) {
         const int pt = (int)w.mps.size();
         const auto X = pMP->GetWorldPos();

@@ -62,6 +62,12 @@ int launch_pose_opt(hipStream_t st, const orbg_pose_edge *edges, const int32_t *
                     const orbg_pose_camera *cams, const float *tcw_in, double *q_out,
                     double *t_out, float *tcw_out, uint8_t *outlier, int32_t *ninliers,
                     int nframes, void *prof);
+int launch_match_pose(hipStream_t st, const orbg_keypoint *kps, const int32_t *counts, int fc,
+                      const int32_t *f1, const int32_t *f2, const int32_t *m12, int npairs,
+                      const orbg_pose_camera &cam, float depth, const float *inv_sigma2, int nlev,
+                      orbg_pose_edge *edges, int32_t *ecount, orbg_pose_camera *cams,
+                      float *tcw0, float *tcw_out, uint8_t *outlier, double *q_out,
+                      double *t_out, int32_t *ninliers, void *prof);
 int launch_match_export(hipStream_t st, const int32_t *m12, const int32_t *f1,
                         const int32_t *counts, int frame_cap, int npairs, int32_t *out);
 int launch_knn2(hipStream_t st, const uint8_t *q, int nq, const uint8_t *t, int nt, int32_t *out,
@@ -349,6 +355,9 @@ struct orbg_ctx {
     // tracking matchers: K-lists of the queries
     void *d_trk = nullptr;
     size_t trk_bytes = 0;
+    // batched-sequence pose stub (orbg_match_pose_batch_device): edges, counts, cameras, poses
+    void *d_mpose = nullptr;
+    size_t mpose_bytes = 0;
     Prof prof;
 };
 
@@ -1209,6 +1218,7 @@ extern "C" void orbg_destroy(orbg_ctx *c)
     if (c->d_img) hipFree(c->d_img);
     if (c->d_scr) hipFree(c->d_scr);
     if (c->d_trk) hipFree(c->d_trk);
+    if (c->d_mpose) hipFree(c->d_mpose);
     if (c->aux_stream) hipStreamSynchronize(c->aux_stream);
     if (c->ostream) hipStreamSynchronize(c->ostream);
     if (c->mstream) hipStreamSynchronize(c->mstream);
@@ -1944,6 +1954,54 @@ extern "C" int orbg_match_batch_device(orbg_ctx *c, const int32_t *f1, const int
     HIPCHK(hipEventRecord(c->ev_mat[s], c->mstream));
     c->mat_pending[s] = true;
     c->last_npairs = npairs;
+    return ORBG_OK;
+}
+
+extern "C" int orbg_match_pose_batch_device(orbg_ctx *c, const orbg_pose_camera *cam,
+                                            float depth, double *d_q, double *d_t,
+                                            int32_t *d_ninliers)
+{
+    if (!c || !c->gw || c->last_n <= 0) return set_err(ORBG_EINVAL, "no batch extracted");
+    if (!c->last_npairs) return set_err(ORBG_EINVAL, "no match batch yet");
+    if (!cam || !d_q || !d_t || !d_ninliers) return set_err(ORBG_EINVAL, "NULL argument");
+    if (!(depth > 0) || !(cam->fx > 0) || !(cam->fy > 0))
+        return set_err(ORBG_EINVAL, "depth, fx, fy must be > 0");
+    HIPCHK(hipSetDevice(c->device));
+    const int P = c->last_npairs;
+    const size_t fc = (size_t)c->geom.frame_cap;
+    size_t o = 0;
+    const size_t oe = o;
+    o += al256((size_t)P * fc * sizeof(orbg_pose_edge));
+    const size_t on = o;
+    o += al256((size_t)P * 4);
+    const size_t oc = o;
+    o += al256((size_t)P * sizeof(orbg_pose_camera));
+    const size_t ot0 = o;
+    o += al256((size_t)P * 48);
+    const size_t ot1 = o;
+    o += al256((size_t)P * 48);
+    const size_t ool = o;
+    o += al256((size_t)P * fc);
+    if (c->mpose_bytes < o) {
+        HIPCHK(hipStreamSynchronize(c->mstream));  // a previous pass may still read it
+        if (c->d_mpose) hipFree(c->d_mpose);
+        c->d_mpose = nullptr;
+        c->mpose_bytes = 0;
+        if (hipMalloc(&c->d_mpose, o) != hipSuccess)
+            return set_err(ORBG_ENOMEM, "pose scratch %zu bytes", o);
+        c->mpose_bytes = o;
+    }
+    uint8_t *b = (uint8_t *)c->d_mpose;
+    const int s = c->slot;
+    HIPCHK(hipStreamWaitEvent(c->mstream, c->ev_ext[s], 0));  // (the matching already does)
+    const int rc = launch_match_pose(
+        c->mstream, c->d_kps, c->d_counts, (int)fc, c->d_pairs, c->d_pairs + c->pair_cap,
+        c->d_m12, P, *cam, depth, c->inv_sigma2, c->p.nlevels, (orbg_pose_edge *)(b + oe),
+        (int32_t *)(b + on), (orbg_pose_camera *)(b + oc), (float *)(b + ot0),
+        (float *)(b + ot1), b + ool, d_q, d_t, d_ninliers, &c->prof);
+    if (rc) return set_err(rc, "pose stub launch failed");
+    HIPCHK(hipEventRecord(c->ev_mat[s], c->mstream));
+    c->mat_pending[s] = true;
     return ORBG_OK;
 }
 

@@ -30,6 +30,10 @@ namespace orbg {
 void prof_begin(void *prof, hipStream_t s, const char *n, hipEvent_t *a);
 void prof_end(void *prof, hipStream_t s, const char *n, hipEvent_t a);
 
+struct PoseInvSigma2 {
+    float v[16];
+};
+
 #define PO_T 256
 #define PO_NV 28  // robust chi2, 21 lower-triangle H entries, 6 b entries
 
@@ -586,6 +590,92 @@ __global__ __launch_bounds__(PO_T) void k_pose_opt(const orbg_pose_edge *__restr
         }
         ninliers[f] = n - nBad;
     }
+}
+
+// ---- the batched-sequence trajectory stub: PoseOptimization edges from the matches ----
+// One workgroup per frame pair p (F1 = f1[p], F2 = f2[p]): SearchForInitialization's
+// vnMatches12 (m12[p][i] = F2 index matched to F1 keypoint i) inverted in LDS, then one mono
+// edge per matched F2 keypoint j in index order (PoseOptimization's loop over pFrame,
+// Optimizer.cc:381): obs = F2 keypoint j, Xw = F1 keypoint back-projected at `depth` in F1's
+// camera (float, oracle/pose_oracle.c orc_match_pose), Omega = mvInvLevelSigma2[octave j].
+// Also the pair's camera and identity initial pose for k_pose_opt.
+__global__ __launch_bounds__(256) void k_match_pose_edges(
+    const orbg_keypoint *__restrict__ kps, const int32_t *__restrict__ counts, int fc,
+    const int32_t *__restrict__ f1, const int32_t *__restrict__ f2,
+    const int32_t *__restrict__ m12, orbg_pose_camera cam, float depth, PoseInvSigma2 inv2,
+    orbg_pose_edge *__restrict__ edges, int32_t *__restrict__ ecount,
+    orbg_pose_camera *__restrict__ cams, float *__restrict__ tcw0)
+{
+    extern __shared__ int pinv[];  // fc entries
+    __shared__ int wsum[4];
+    const int p = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+    const int a = f1[p], b = f2[p];
+    const int n1 = counts[a], n2 = counts[b];
+    const orbg_keypoint *k1 = kps + (size_t)a * fc, *k2 = kps + (size_t)b * fc;
+    for (int j = tid; j < n2; j += 256) pinv[j] = -1;
+    __syncthreads();
+    for (int i = tid; i < n1; i += 256) {
+        const int j = m12[(size_t)p * fc + i];
+        if (j >= 0 && j < n2) pinv[j] = i;
+    }
+    __syncthreads();
+    orbg_pose_edge *E = edges + (size_t)p * fc;
+    int run = 0;
+    for (int j0 = 0; j0 < n2; j0 += 256) {
+        const int j = j0 + tid;
+        const int i = j < n2 ? pinv[j] : -1;
+        const int f = i >= 0;
+        const int incl = wave_incl_scan(f);
+        if (lane == 63) wsum[wv] = incl;
+        __syncthreads();
+        int before = run, tot = run;
+        for (int w = 0; w < 4; w++) {
+            before += w < wv ? wsum[w] : 0;
+            tot += wsum[w];
+        }
+        if (f) {
+            const orbg_keypoint kq = k2[j], kr = k1[i];
+            orbg_pose_edge e;
+            e.obs[0] = kq.x;
+            e.obs[1] = kq.y;
+            e.obs[2] = -1.f;
+            e.xw[0] = (kr.x - cam.cx) * depth / cam.fx;
+            e.xw[1] = (kr.y - cam.cy) * depth / cam.fy;
+            e.xw[2] = depth;
+            e.inv_sigma2 = inv2.v[kq.octave];
+            e.stereo = 0;
+            E[before + incl - 1] = e;
+        }
+        run = tot;
+        __syncthreads();
+    }
+    if (tid == 0) {
+        ecount[p] = run;
+        cams[p] = cam;
+    }
+    if (tid < 12) tcw0[12 * (size_t)p + tid] = (tid % 5 == 0) ? 1.f : 0.f;  // [I | 0]
+}
+
+int launch_pose_opt(hipStream_t st, const orbg_pose_edge *edges, const int32_t *counts, int cap,
+                    const orbg_pose_camera *cams, const float *tcw_in, double *q_out,
+                    double *t_out, float *tcw_out, uint8_t *outlier, int32_t *ninliers,
+                    int nframes, void *prof);
+
+int launch_match_pose(hipStream_t st, const orbg_keypoint *kps, const int32_t *counts, int fc,
+                      const int32_t *f1, const int32_t *f2, const int32_t *m12, int npairs,
+                      const orbg_pose_camera &cam, float depth, const float *inv_sigma2, int nlev,
+                      orbg_pose_edge *edges, int32_t *ecount, orbg_pose_camera *cams,
+                      float *tcw0, float *tcw_out, uint8_t *outlier, double *q_out,
+                      double *t_out, int32_t *ninliers, void *prof)
+{
+    if (npairs <= 0) return ORBG_OK;
+    PoseInvSigma2 inv2{};
+    for (int l = 0; l < nlev && l < 16; l++) inv2.v[l] = inv_sigma2[l];
+    hipLaunchKernelGGL(k_match_pose_edges, dim3(npairs), dim3(256), (size_t)fc * 4, st, kps,
+                       counts, fc, f1, f2, m12, cam, depth, inv2, edges, ecount, cams, tcw0);
+    if (hipGetLastError() != hipSuccess) return ORBG_EIO;
+    return launch_pose_opt(st, edges, ecount, fc, cams, tcw0, q_out, t_out, tcw_out, outlier,
+                           ninliers, npairs, prof);
 }
 
 int launch_pose_opt(hipStream_t st, const orbg_pose_edge *edges, const int32_t *counts, int cap,

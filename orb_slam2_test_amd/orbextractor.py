@@ -159,6 +159,17 @@ class ORBextractor:
                                                 1 if check_ori else 0),
                 "orbg_match_batch_device")
 
+    def match_pose_batch_device(self, cam, depth, d_q, d_t, d_ninliers):
+        """PoseOptimization of frame f2[p] over the last match batch's matches (F1 keypoints
+        back-projected at `depth`; orbg_match_pose_batch_device), on the match stream.
+        cam = (fx, fy, cx, cy, bf); d_q [P][4] / d_t [P][3] float64, d_ninliers [P] int32
+        device pointers."""
+        c = L.PoseCamera(*[float(v) for v in cam], 0.0)
+        L.check(L.lib().orbg_match_pose_batch_device(self.ctx.handle, C.byref(c), float(depth),
+                                                     C.c_void_p(d_q), C.c_void_p(d_t),
+                                                     C.c_void_p(d_ninliers)),
+                "orbg_match_pose_batch_device")
+
     def match_outputs(self):
         k, m, n, fc = C.c_void_p(), C.c_void_p(), C.c_void_p(), C.c_int32()
         L.check(L.lib().orbg_match_outputs(self.ctx.handle, C.byref(k), C.byref(m), C.byref(n),

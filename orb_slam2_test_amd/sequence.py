@@ -13,11 +13,19 @@ The sequence is cyclic, as in bench.py: frame 0 pairs with frame N-1, so every f
 exactly one extraction and one match.
 
 A backend maps a local batch `imgs` [n, h, w] (halo first) to (nkp[n], nmatch[n]) with
-nmatch[i] = matches of (i-1, i) for i >= 1, and with `with_matches` also m12[n, cap] with
-row i = vnMatches12 of (i-1, i) (row 0 unused).  `GpuBackend` runs liborbg's batched
-device entry points (ORBextractor.extract_batch_device / match_batch_device).
+nmatch[i] = matches of (i-1, i) for i >= 1, with `with_matches` also m12[n, cap] with
+row i = vnMatches12 of (i-1, i) (row 0 unused), and with `with_pose` also pose[n, 8]: row i
+= the pose stub of frame i (PoseOptimization over the matches of (i-1, i), frame i-1's
+keypoints back-projected at POSE_DEPTH: SE3Quat q (x, y, z, w), t, inlier count; row 0
+unused) -- the "pose/trajectory stub" SURVEY.md 8e gathers beside the counts and indices.
+`GpuBackend` runs liborbg's batched device entry points (ORBextractor.extract_batch_device /
+match_batch_device / match_pose_batch_device).
 """
 import numpy as np
+
+# the pose stub's scene depth (m) and camera (KITTI00-02.yaml intrinsics, mbf)
+POSE_DEPTH = 10.0
+POSE_CAM = (718.856, 718.856, 607.1928, 185.2157, 386.1448)
 
 
 def shard(nframes, world, rank):
@@ -64,40 +72,49 @@ def gather_summary(local, world, group=None, sizes=None):
     return gather_rows(local.t().contiguous(), world, group, sizes).t().contiguous()
 
 
-def run_sharded(frames, world, rank, backend, group=None, device="cpu", with_matches=False):
+def run_sharded(frames, world, rank, backend, group=None, device="cpu", with_matches=False,
+                with_pose=False):
     """Process this rank's block of the cyclic sequence `frames` [N, h, w] with `backend`
-    and return the gathered global outputs as numpy: (nkp[N], nmatch[N]), plus m12[N, cap]
-    (row t = vnMatches12 of (t-1, t)) with `with_matches`."""
+    and return the gathered global outputs as numpy: (nkp[N], nmatch[N]), then m12[N, cap]
+    (row t = vnMatches12 of (t-1, t)) with `with_matches`, then pose[N, 8] (row t = frame t's
+    pose stub) with `with_pose`."""
     import torch
     n = len(frames)
     lo, hi = shard(n, world, rank)
     idx = local_indices(n, lo, hi)
-    m12 = None
+    m12 = pose = None
     if len(idx):
         r = backend(np.ascontiguousarray(frames[idx]))
         nkp, nm = r[0], r[1]
         local = np.stack([np.asarray(nkp, np.int32)[1:], np.asarray(nm, np.int32)[1:]])
+        k = 2
         if with_matches:
-            m12 = np.ascontiguousarray(np.asarray(r[2], np.int32)[1:])
+            m12 = np.ascontiguousarray(np.asarray(r[k], np.int32)[1:])
+            k += 1
+        if with_pose:
+            pose = np.ascontiguousarray(np.asarray(r[k], np.float64)[1:])
     else:
         local = np.zeros((2, 0), np.int32)
+        pose = np.zeros((0, 8))
     g = gather_summary(torch.from_numpy(local).to(device), world, group).cpu().numpy()
-    if not with_matches:
-        return g[0], g[1]
-    if m12 is None:  # an empty block still takes part in the collectives
-        cap = torch.zeros(1, dtype=torch.int64, device=device)
-        if world > 1:
+    out = [g[0], g[1]]
+    if with_matches:
+        if m12 is None:  # an empty block still takes part in the collectives
+            cap = torch.zeros(1, dtype=torch.int64, device=device)
+            if world > 1:
+                import torch.distributed as dist
+                dist.all_reduce(cap, op=dist.ReduceOp.MAX, group=group)
+            m12 = np.zeros((0, int(cap.item())), np.int32)
+        elif world > 1:
             import torch.distributed as dist
+            cap = torch.tensor([m12.shape[1]], dtype=torch.int64, device=device)
             dist.all_reduce(cap, op=dist.ReduceOp.MAX, group=group)
-        m12 = np.zeros((0, int(cap.item())), np.int32)
-    elif world > 1:
-        import torch.distributed as dist
-        cap = torch.tensor([m12.shape[1]], dtype=torch.int64, device=device)
-        dist.all_reduce(cap, op=dist.ReduceOp.MAX, group=group)
-        if int(cap.item()) > m12.shape[1]:  # rows padded with -1 to the widest rank's cap
-            m12 = np.pad(m12, ((0, 0), (0, int(cap.item()) - m12.shape[1])), constant_values=-1)
-    gm = gather_rows(torch.from_numpy(m12).to(device), world, group).cpu().numpy()
-    return g[0], g[1], gm
+            if int(cap.item()) > m12.shape[1]:  # rows padded with -1 to the widest rank's cap
+                m12 = np.pad(m12, ((0, 0), (0, int(cap.item()) - m12.shape[1])), constant_values=-1)
+        out.append(gather_rows(torch.from_numpy(m12).to(device), world, group).cpu().numpy())
+    if with_pose:
+        out.append(gather_rows(torch.from_numpy(pose).to(device), world, group).cpu().numpy())
+    return tuple(out)
 
 
 def run_sharded_stereo(lefts, rights, world, rank, backend, group=None, device="cpu"):
@@ -120,12 +137,14 @@ def run_sharded_stereo(lefts, rights, world, rank, backend, group=None, device="
 
 class GpuBackend:
     """liborbg batch path: extract all local frames in one launch sequence, then match the
-    consecutive pairs (i-1, i) on the device; only the per-frame summary leaves HBM."""
+    consecutive pairs (i-1, i) on the device (and with `with_pose` run the pose stub on
+    them); only the per-frame outputs leave HBM."""
 
-    def __init__(self, extractor, window=100, nnratio=0.9, check_ori=True, with_matches=False):
+    def __init__(self, extractor, window=100, nnratio=0.9, check_ori=True, with_matches=False,
+                 with_pose=False):
         self.ext = extractor
         self.window, self.nnratio, self.check_ori = window, nnratio, check_ori
-        self.with_matches = with_matches
+        self.with_matches, self.with_pose = with_matches, with_pose
 
     def __call__(self, imgs):
         import torch
@@ -147,21 +166,34 @@ class GpuBackend:
         if n > 1:
             self.ext.match_batch_device(np.arange(n - 1), np.arange(1, n), self.window,
                                         self.nnratio, self.check_ori)
+        if self.with_pose and n > 1:
+            dq = torch.zeros((n - 1, 4), dtype=torch.float64, device="cuda")
+            dt = torch.zeros((n - 1, 3), dtype=torch.float64, device="cuda")
+            dn = torch.zeros(n - 1, dtype=torch.int32, device="cuda")
+            self.ext.match_pose_batch_device(POSE_CAM, POSE_DEPTH, dq.data_ptr(), dt.data_ptr(),
+                                             dn.data_ptr())
         self.ext.ctx.batch_summary(summary.data_ptr())
         if self.with_matches:
             cap = self.ext.ctx.batch_matches(None) if n > 1 else 0
             dm = torch.full((n, max(cap, 1)), -1, dtype=torch.int32, device="cuda")
             if n > 1:
                 self.ext.ctx.batch_matches(dm[1:].data_ptr())
-        self.ext.ctx.sync()  # the summary / matches are written on liborbg's match stream
+        self.ext.ctx.sync()  # the summary / matches / poses are written on the match stream
         s = summary.cpu().numpy()
         nkp = s[:n].copy()
         if n > 1:
             nm[1:] = s[n:2 * n - 1]
+        out = [nkp, nm]
         if self.with_matches:
-            m12 = dm.cpu().numpy()
-            return nkp, nm, m12
-        return nkp, nm
+            out.append(dm.cpu().numpy())
+        if self.with_pose:
+            pose = np.zeros((n, 8))
+            if n > 1:
+                pose[1:, :4] = dq.cpu().numpy()
+                pose[1:, 4:7] = dt.cpu().numpy()
+                pose[1:, 7] = dn.cpu().numpy()
+            out.append(pose)
+        return tuple(out)
 
 
 class BenchStep:

@@ -3,12 +3,22 @@
 // orbg_reference.hpp) driven the way Tracking.cc / Optimizer.cc call it, on stand-ins of the
 // reference's Frame / KeyFrame / MapPoint (same member names and types) and the test-only
 // cv:: subset in tests/compat_stub/.  Built by tests/test_compat_ref.py (CPU: it compiles);
-// run there on the GPU.  usage: compat_ref_selftest img1.raw img2.raw w h
+// run there on the GPU.
+//   compat_ref_selftest img1.raw img2.raw w h   the call sites, serially, then the Tracking
+//                                               thread's and LocalMapping thread's calls
+//                                               concurrently (one liborbg context per thread)
+//   compat_ref_selftest lba <dir>               build_lba_window + linearize_lba_window on a
+//                                               scene read from <dir>, outputs written there
+//                                               (tests/test_compat_ref.py checks them against
+//                                               an independent window and the oracle)
 #include <cmath>
 #include <cstdio>
+#include <cstring>
 #include <fstream>
 #include <list>
 #include <map>
+#include <string>
+#include <thread>
 #include <vector>
 
 #include <opencv2/core/core.hpp>
@@ -62,8 +72,9 @@ struct KeyFrame {  // include/KeyFrame.h
     std::vector<cv::KeyPoint> mvKeysUn;
     std::vector<float> mvuRight, mvInvLevelSigma2;
     cv::Mat Tcw;
+    bool bad = false;
     cv::Mat GetPose() const { return Tcw.clone(); }
-    bool isBad() const { return false; }
+    bool isBad() const { return bad; }
 };
 
 static std::vector<uint8_t> read_raw(const char *path, size_t n)
@@ -74,8 +85,112 @@ static std::vector<uint8_t> read_raw(const char *path, size_t n)
     return b;
 }
 
+template <class T>
+static std::vector<T> read_vec(const std::string &path)
+{
+    std::ifstream f(path, std::ios::binary | std::ios::ate);
+    const size_t n = (size_t)f.tellg();
+    std::vector<T> v(n / sizeof(T));
+    f.seekg(0);
+    f.read((char *)v.data(), (std::streamsize)(v.size() * sizeof(T)));
+    return v;
+}
+
+template <class T>
+static void write_vec(const std::string &path, const T *p, size_t n)
+{
+    std::ofstream f(path, std::ios::binary);
+    f.write((const char *)p, (std::streamsize)(n * sizeof(T)));
+}
+
+// A LocalBundleAdjustment scene from <dir> (tests/test_compat_ref.py):
+//   lba_meta.i32 {nkf, K, nmp, nobs}; lba_kf.f64 nkf x {mnId, fx, fy, cx, cy, mbf, bad,
+//   list (1 local, 0 fixed, -1 neither), Tcw rows 0..2 (12)}; lba_kp.f32 nkf x K x {x, y, octave, uRight};
+//   lba_inv2.f32 mvInvLevelSigma2 (8); lba_mp.f64 nmp x {mnId, X, Y, Z};
+//   lba_obs.i32 nobs x {map point, key frame, keypoint}.
+// Key frames live in one array, so a map point's std::map<KeyFrame*, size_t> is in array
+// order.  lLocalKeyFrames / lFixedCameras are the local / non-local key frames in array order,
+// lLocalMapPoints all map points in order.
+static int lba_scene(const std::string &dir)
+{
+    const std::vector<int32_t> meta = read_vec<int32_t>(dir + "/lba_meta.i32");
+    REQUIRE(meta.size() == 4);
+    const int nkf = meta[0], K = meta[1], nmp = meta[2], nobs = meta[3];
+    const std::vector<double> kfd = read_vec<double>(dir + "/lba_kf.f64");
+    const std::vector<float> kpd = read_vec<float>(dir + "/lba_kp.f32");
+    const std::vector<float> inv2 = read_vec<float>(dir + "/lba_inv2.f32");
+    const std::vector<double> mpd = read_vec<double>(dir + "/lba_mp.f64");
+    const std::vector<int32_t> obs = read_vec<int32_t>(dir + "/lba_obs.i32");
+    REQUIRE((int)kfd.size() == 20 * nkf && (int)kpd.size() == 4 * K * nkf);
+    REQUIRE((int)mpd.size() == 4 * nmp && (int)obs.size() == 3 * nobs);
+    std::vector<KeyFrame> kfs(nkf);
+    std::list<KeyFrame *> local, fixed;
+    for (int i = 0; i < nkf; i++) {
+        const double *r = &kfd[20 * (size_t)i];
+        KeyFrame &k = kfs[i];
+        k.mnId = (long unsigned)r[0];
+        k.fx = (float)r[1];
+        k.fy = (float)r[2];
+        k.cx = (float)r[3];
+        k.cy = (float)r[4];
+        k.mbf = (float)r[5];
+        k.bad = r[6] != 0;
+        k.Tcw = cv::Mat::eye(4, 4, CV_32F);
+        for (int a = 0; a < 3; a++)
+            for (int c = 0; c < 4; c++) k.Tcw.at<float>(a, c) = (float)r[8 + 4 * a + c];
+        k.mvInvLevelSigma2 = inv2;
+        for (int j = 0; j < K; j++) {
+            const float *q = &kpd[4 * ((size_t)i * K + j)];
+            cv::KeyPoint kp;
+            kp.pt.x = q[0];
+            kp.pt.y = q[1];
+            kp.octave = (int)q[2];
+            k.mvKeysUn.push_back(kp);
+            k.mvuRight.push_back(q[3]);
+        }
+        if (r[7] > 0) local.push_back(&k);       // lLocalKeyFrames
+        else if (r[7] == 0) fixed.push_back(&k);  // lFixedCameras (< 0: in neither list)
+    }
+    std::vector<MapPoint> mps(nmp);
+    std::list<MapPoint *> points;
+    for (int j = 0; j < nmp; j++) {
+        mps[j].mnId = (long unsigned)mpd[4 * (size_t)j];
+        mps[j].pos = cv::Mat(3, 1, CV_32F);
+        for (int c = 0; c < 3; c++) mps[j].pos.at<float>(c) = (float)mpd[4 * (size_t)j + 1 + c];
+        points.push_back(&mps[j]);
+    }
+    for (int o = 0; o < nobs; o++) mps[obs[3 * o]].obs[&kfs[obs[3 * o + 1]]] = (size_t)obs[3 * o + 2];
+    const auto win = orbg_compat::ref::build_lba_window(local, fixed, points);
+    const auto sys = orbg_compat::ref::linearize_lba_window(orbg_compat::ref::default_ctx(), win);
+    write_vec(dir + "/win_poses.bin", win.poses.data(), win.poses.size());
+    write_vec(dir + "/win_points.f64", win.points.data(), win.points.size());
+    write_vec(dir + "/win_edges.bin", win.edges.data(), win.edges.size());
+    std::vector<int32_t> kfidx, mpidx;
+    for (KeyFrame *k : win.kfs) kfidx.push_back((int32_t)(k - kfs.data()));
+    for (MapPoint *m : win.mps) mpidx.push_back((int32_t)(m - mps.data()));
+    write_vec(dir + "/win_kf.i32", kfidx.data(), kfidx.size());
+    write_vec(dir + "/win_mp.i32", mpidx.data(), mpidx.size());
+    write_vec(dir + "/g2o_pose_hidx.i32", sys.pose_hidx.data(), sys.pose_hidx.size());
+    write_vec(dir + "/g2o_point_hidx.i32", sys.point_hidx.data(), sys.point_hidx.size());
+    write_vec(dir + "/g2o_Hpp.f64", sys.Hpp.data(), sys.Hpp.size());
+    write_vec(dir + "/g2o_Hll.f64", sys.Hll.data(), sys.Hll.size());
+    write_vec(dir + "/g2o_b.f64", sys.b.data(), sys.b.size());
+    std::vector<double> hpl;  // (pose hidx, point hidx, 18 column-major 6x3) per block
+    for (const auto &kv : sys.Hpl) {
+        hpl.push_back(kv.first.first);
+        hpl.push_back(kv.first.second);
+        hpl.insert(hpl.end(), kv.second.begin(), kv.second.end());
+    }
+    write_vec(dir + "/g2o_Hpl.f64", hpl.data(), hpl.size());
+    write_vec(dir + "/g2o_chi2.f64", &sys.active_robust_chi2, 1);
+    std::printf("lba ok: %zu poses, %zu points, %zu edges\n", win.poses.size(),
+                win.points.size() / 3, win.edges.size());
+    return 0;
+}
+
 int main(int argc, char **argv)
 {
+    if (argc == 3 && std::string(argv[1]) == "lba") return lba_scene(argv[2]);
     if (argc < 5) return 2;
     const int w = atoi(argv[3]), h = atoi(argv[4]);
     std::vector<uint8_t> im1 = read_raw(argv[1], (size_t)w * h), im2 = read_raw(argv[2], (size_t)w * h);
@@ -223,6 +338,49 @@ int main(int argc, char **argv)
     double bn = 0;
     for (double v : sys.b) bn += v * v;
     REQUIRE(bn > 0 && std::isfinite(bn));
+
+    // ---- the reference's threads: Tracking (SearchByProjection + PoseOptimization on the
+    // current frame) and LocalMapping (LocalBundleAdjustment's linearisation) at the same
+    // time (System.cc:117, LocalMapping.cc:99), each through its own thread's default_ctx();
+    // every result equals the serial run's ----
+    std::vector<MapPoint *> serial_mp = F2.mvpMapPoints;
+    const cv::Mat serial_pose = F2.mTcw.clone();
+    orbg_ctx *ctx_track = nullptr, *ctx_map = nullptr;
+    for (int round = 0; round < 4; round++) {
+        Frame F2t = F2;
+        F2t.mvpMapPoints.assign(F2t.N, nullptr);
+        F2t.mvbOutlier.assign(F2t.N, false);
+        F2t.mTcw = cv::Mat::eye(4, 4, CV_32F);
+        int tproj = -1, tinl = -1;
+        orbg_compat::ref::G2oBlockSystem tsys;
+        std::thread tracking([&] {
+            orbg_ctx *c = orbg_compat::ref::default_ctx();
+            ctx_track = c;
+            tproj = orbg_compat::ref::SearchByProjection(c, true, F2t, F1, 15.f, true);
+            tinl = orbg_compat::ref::PoseOptimization(c, &F2t);
+        });
+        std::thread mapping([&] {
+            orbg_ctx *c = orbg_compat::ref::default_ctx();
+            ctx_map = c;
+            tsys = orbg_compat::ref::linearize_lba_window(c, win);
+        });
+        tracking.join();
+        mapping.join();
+        REQUIRE(ctx_track != ctx_map && ctx_track != ctx && ctx_map != ctx);
+        REQUIRE(tproj == nproj && tinl == ninl);
+        REQUIRE(F2t.mvpMapPoints == serial_mp);
+        for (int r = 0; r < 3; r++)
+            for (int c = 0; c < 4; c++) REQUIRE(F2t.mTcw.at<float>(r, c) == serial_pose.at<float>(r, c));
+        REQUIRE(tsys.pose_hidx == sys.pose_hidx && tsys.point_hidx == sys.point_hidx);
+        REQUIRE(tsys.Hll == sys.Hll && tsys.Hpl == sys.Hpl);  // per point / per edge: exact
+        REQUIRE(tsys.active_robust_chi2 == sys.active_robust_chi2);
+        for (size_t k = 0; k < sys.Hpp.size(); k++)  // MFMA slice sums: any order, 1e-9
+            REQUIRE(std::fabs(tsys.Hpp[k] - sys.Hpp[k]) <= 1e-9 * (std::fabs(sys.Hpp[k]) + 1e-12));
+        for (size_t k = 0; k < sys.b.size(); k++)
+            REQUIRE(std::fabs(tsys.b[k] - sys.b[k]) <= 1e-9 * (std::fabs(sys.b[k]) + 1e-12));
+    }
+    std::printf("threads ok: Tracking and LocalMapping calls concurrent on their own contexts\n");
+
     std::printf("compat_ref ok: %d + %d keypoints, SearchForInitialization %d, SearchByProjection %d, "
                 "PoseOptimization inliers %d, LBA edges %zu, chi2 %.6g\n",
                 F1.N, F2.N, nsfi, nproj, ninl, win.edges.size(), sys.active_robust_chi2);

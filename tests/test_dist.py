@@ -78,15 +78,17 @@ def test_sharded_sequence_matches_single_process(oracle, world):
         assert np.array_equal(nm, ref_nm), rank
 
 
-def _oracle_pairs(O, p, imgs, window=100, nnratio=0.9):
-    """Per-frame (nkp, nmatch, vnMatches12) of consecutive pairs (i-1, i), as
+def _oracle_pairs(O, p, imgs, window=100, nnratio=0.9, with_pose=False):
+    """Per-frame (nkp, nmatch, vnMatches12[, pose]) of consecutive pairs (i-1, i), as
     orc_frames_batch computes them (SearchForInitialization with prevMatched = the keypoints
-    of frame i-1, bounds = the image), row 0 unused; rows padded with -1 to CAP."""
+    of frame i-1, bounds = the image), row 0 unused; rows padded with -1 to CAP; pose row i =
+    the pose stub of frame i (orc_match_pose: q, t, inliers)."""
     n, h, w = imgs.shape
     ex = [O.extract(p, im) for im in imgs]
     nkp = np.array([len(e["kps"]) for e in ex], np.int32)
     nm = np.zeros(n, np.int32)
     m12 = np.full((n, CAP), -1, np.int32)
+    pose = np.zeros((n, 8))
     for i in range(1, n):
         a, b = ex[i - 1], ex[i]
         prev = np.ascontiguousarray(np.stack([a["kps"]["x"], a["kps"]["y"]], 1))
@@ -94,7 +96,11 @@ def _oracle_pairs(O, p, imgs, window=100, nnratio=0.9):
                                               (0, w, 0, h), window, nnratio, True)
         nm[i] = k
         m12[i, :len(m)] = m
-    return nkp, nm, m12
+        if with_pose:
+            ni, q, t = O.match_pose(p, a["kps"], b["kps"], m, sequence.POSE_CAM,
+                                    sequence.POSE_DEPTH)
+            pose[i, :4], pose[i, 4:7], pose[i, 7] = q, t, ni
+    return (nkp, nm, m12, pose) if with_pose else (nkp, nm, m12)
 
 
 CAP = 2 * 500 + 256
@@ -112,6 +118,22 @@ def _worker_matches(rank, world, port, frames, q):
                                             lambda imgs: _oracle_pairs(O, p, imgs),
                                             with_matches=True)
         q.put((rank, nkp.tolist(), nm.tolist(), m12.tolist()))
+    finally:
+        dist.destroy_process_group()
+
+
+def _worker_pose(rank, world, port, frames, q):
+    import torch.distributed as dist
+    from oracle import pyoracle as O
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        p = O.params(nfeatures=500)
+        nkp, nm, m12, pose = sequence.run_sharded(
+            frames, world, rank, lambda imgs: _oracle_pairs(O, p, imgs, with_pose=True),
+            with_matches=True, with_pose=True)
+        q.put((rank, nkp.tolist(), nm.tolist(), m12.tolist(), pose.tolist()))
     finally:
         dist.destroy_process_group()
 
@@ -185,3 +207,22 @@ def test_sharded_stereo_equals_single_process(oracle):
     for rank, nkp, nd in _spawn(_worker_stereo, 2, lefts, rights):
         assert np.array_equal(nkp, ref_nkp), rank
         assert np.array_equal(nd, ref_nd), rank
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_sharded_pose_stub_equals_single_process(oracle, world):
+    """SURVEY 8e's pose/trajectory stub travels in the gather beside the counts and the
+    vnMatches12 rows: every rank's gathered pose rows (SE3Quat, translation, inliers of
+    PoseOptimization over the matches of (t-1, t)) equal one process doing the whole cyclic
+    sequence, bit for bit."""
+    frames = synthetic.sequence(5, H, W, seed=synthetic.DEFAULT_SEED + 19)
+    p = oracle.params(nfeatures=500)
+    cyc = np.concatenate([frames[-1:], frames])
+    ref = _oracle_pairs(oracle, p, cyc, with_pose=True)
+    ref_nkp, ref_nm, ref_m12, ref_pose = [r[1:] for r in ref]
+    assert (ref_pose[:, 7] > 20).sum() >= 3
+    for rank, nkp, nm, m12, pose in _spawn(_worker_pose, world, frames):
+        assert np.array_equal(nkp, ref_nkp), rank
+        assert np.array_equal(nm, ref_nm), rank
+        assert np.array_equal(np.asarray(m12), ref_m12), rank
+        assert np.array_equal(np.asarray(pose), ref_pose), rank
