@@ -439,8 +439,10 @@ int orbg_ba_linearize(orbg_ctx *ctx, const orbg_pose *poses, int npose, const do
 /* Device-resident variant (batched LBA windows): every pointer is device memory, enqueued
  * on the context stream.  pose_off[npose+1] / pose_edges[nedge] and point_off[npoint+1] /
  * point_edges[nedge] list each vertex's edges (CSR, built once per window: the graph does
- * not change across LM iterations).  d_eout is required; outputs are overwritten.  Pose
- * blocks H_pp | b_p are accumulated with MFMA f64, point blocks summed per point. */
+ * not change across LM iterations; a point's edges in ascending edge order).  d_eout is
+ * required; its hpl (and, per orbg_ba_set_edge_errors / _jacobians, the error terms and
+ * Jacobians) are overwritten.  Point blocks are summed per point by one thread per point
+ * over its edges; pose blocks H_pp | b_p are accumulated with MFMA f64. */
 int orbg_ba_linearize_device(orbg_ctx *ctx, const orbg_pose *d_poses, int npose,
                              const double *d_points, int npoint, const orbg_edge *d_edges,
                              int nedge, const int32_t *d_pose_off, const int32_t *d_pose_edges,
@@ -473,6 +475,12 @@ int orbg_ba_errors_device(orbg_ctx *ctx, const orbg_pose *d_poses, const double 
  * _jacobianOplusXi / Xj; default on).  Off, those fields are left as they are and every
  * other output is unchanged: the blocks, H_pl and orbg_ba_schur_solve do not read them. */
 int orbg_ba_set_jacobians(orbg_ctx *ctx, int enable);
+/* Whether orbg_ba_linearize_device stores the per-edge error terms eout.err / chi2 / rho1
+ * (default on).  Off, they are left as they are and every other output is unchanged: g2o's
+ * LM takes them from the per-trial error pass instead (orbg_ba_errors / _device, which the
+ * outlier test of Optimizer.cc:871-901 reads too), so buildSystem's pass writes only H_pl
+ * and the blocks. */
+int orbg_ba_set_edge_errors(orbg_ctx *ctx, int enable);
 
 /* g2o BlockSolver<6,3>::solve with the Schur complement (Thirdparty/g2o/g2o/core/
  * block_solver.hpp:354-486) for one LocalBundleAdjustment window, after setLambda(lambda):

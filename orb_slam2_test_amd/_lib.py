@@ -184,6 +184,7 @@ def lib():
                                                   vp, vp, vp, vp, vp]),
         "orbg_ba_linearize": (i32, [vp, vp, i32, vp, i32, vp, i32, vp, vp, vp, vp, vp]),
         "orbg_ba_set_jacobians": (i32, [vp, i32]),
+        "orbg_ba_set_edge_errors": (i32, [vp, i32]),
         "orbg_ba_errors": (i32, [vp, vp, i32, vp, i32, vp, i32, vp, vp, vp, vp, P(C.c_double)]),
         "orbg_ba_errors_device": (i32, [vp, vp, vp, vp, i32, vp, vp, vp, vp]),
         "orbg_ba_linearize_device": (i32, [vp, vp, i32, vp, i32, vp, i32, vp, vp, vp, vp, vp, vp,

@@ -1,15 +1,15 @@
 // ba_kernels.hip -- per-edge arithmetic of Optimizer::LocalBundleAdjustment on gfx950.
 //
-// k_ba_edges: one thread per edge, fp64 throughout (world coordinates reach hundreds of
-// metres on KITTI; obs - proj cancels, SURVEY.md 7 hard part 5):
+// k_ba_edges: one thread per point over its edges, fp64 throughout (world coordinates reach
+// hundreds of metres on KITTI; obs - proj cancels, SURVEY.md 7 hard part 5):
 //   EdgeSE3ProjectXYZ / EdgeStereoSE3ProjectXYZ::computeError  types_six_dof_expmap.h:90-95,122-127
 //   cam_project (stereo: float invz, float bf)                 types_six_dof_expmap.cpp:141-157
 //   linearizeOplus                                             types_six_dof_expmap.cpp:103-139,188-234
 //   chi2, Huber rho' (float dsqr)                              base_edge.h:58-61, robust_kernel_impl.cpp:65-91
 //   constructQuadraticForm: H_pp += A^T W A, b_p += A^T w_r,   base_binary_edge.hpp:55-120
 //       H_ll += B^T W B, b_l += B^T w_r, H_pl = A^T W B
-// Point blocks are summed per point over its edge list (k_ba_point_blocks, no atomics);
-// pose blocks by k_ba_pose_mfma (MFMA f64 over slices of each pose's edge rows).
+// Point blocks are summed per point over its edge list in k_ba_edges itself (no atomics);
+// pose blocks by k_ba_pose_mfma (MFMA f64 over slices of each pose's edges, rows recomputed).
 #include <hip/hip_runtime.h>
 
 #include <cstring>
@@ -20,6 +20,14 @@ namespace orbg {
 
 void prof_begin(void *prof, hipStream_t s, const char *n, hipEvent_t *a);
 void prof_end(void *prof, hipStream_t s, const char *n, hipEvent_t a);
+
+// LDS written by some lanes of a wave, then read by others (the hardware keeps one wave's
+// LDS ops in order; the fence keeps the compiler from reordering them)
+__device__ __forceinline__ void wave_sync_lds_ba()
+{
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+}
 
 __device__ __forceinline__ void quat_rotate(const double q[4], const double v[3], double o[3])
 {
@@ -115,53 +123,24 @@ int launch_ba_errors(hipStream_t st, const orbg_pose *poses, const double *point
 }
 
 // ---------------------------------------------------------------------------
-// k_ba_edges: thread per edge.  Per-edge outputs go straight to global (no 400-byte live
-// struct); point blocks are accumulated with fp64 atomics (a point has ~4-5 observations,
-// so contention is low); the pose side is left to k_ba_pose_mfma through three rows per
-// edge: rows[e][k] = {J_pose[k][0..5], -e[k], w} (w = rho' * invSigma2; mono edges have a
-// zero third row, inactive edges zero rows).
+// The linearisation of one edge (linearizeOplus types_six_dof_expmap.cpp:103-139 / 188-234,
+// chi2 + Huber rho' base_edge.h:58-61, robust_kernel_impl.cpp:78-91), everything in
+// registers; the third row of a mono edge is zero (adding it adds exact zeros, so the fixed
+// 3-row loops give the same bits as the oracle's 2-row ones).
 // ---------------------------------------------------------------------------
-#define BA_ROW 8    // doubles per pose row
-#define BA_PROW 12  // doubles per edge share of its point block
+struct BaLin {
+    double err[3], jp[3][3], jt[3][6], chi2, rho1, w, info;
+    int D;
+};
 
-// JAC: store g2o's per-edge Jacobians (eout.jp / eout.jt, _jacobianOplusXi / Xj).  Nothing
-// downstream reads them (the blocks, H_pl and the Schur step use the registers), so callers
-// that do not keep them skip 216 of the 696 bytes stored per edge (orbg_ba_set_jacobians).
-template <bool JAC>
-__global__ __launch_bounds__(256) void k_ba_edges(const orbg_pose *__restrict__ poses,
-                                                  const double *__restrict__ points,
-                                                  const orbg_edge *__restrict__ edges, int nedge,
-                                                  orbg_edge_out *__restrict__ eout,
-                                                  double *__restrict__ rows,
-                                                  double *__restrict__ prow)
+__device__ __forceinline__ void ba_linearize_edge(const orbg_pose &P, const double X[3],
+                                                  const orbg_edge &e, BaLin &L)
 {
-    const int i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= nedge) return;
-    const orbg_edge e = edges[i];
-    orbg_edge_out *o = eout + i;
-    double *row = rows + (size_t)i * 3 * BA_ROW;
-    double *pr = prow + (size_t)i * BA_PROW;
-    if (!e.active) {
-        if (JAC) {
-            memset(o, 0, sizeof(*o));
-        } else {
-            for (int k = 0; k < 3; k++) o->err[k] = 0;
-            o->chi2 = 0;
-            o->rho1 = 0;
-            for (int r = 0; r < 3; r++)
-                for (int c = 0; c < 6; c++) o->hpl[r][c] = 0;
-        }
-        for (int k = 0; k < 3 * BA_ROW; k++) row[k] = 0;
-        for (int k = 0; k < BA_PROW; k++) pr[k] = 0;
-        return;
-    }
-    const orbg_pose P = poses[e.pose];
-    const double X[3] = {points[3 * e.point], points[3 * e.point + 1], points[3 * e.point + 2]};
-    double xc[3], err[3];
-    ba_edge_error(P, X, e, xc, err);
+    double xc[3];
+    ba_edge_error(P, X, e, xc, L.err);
     const double x = xc[0], y = xc[1], z = xc[2], z_2 = z * z;
     const double fx = e.fx, fy = e.fy;
-    const int D = e.stereo ? 3 : 2;
+    L.D = e.stereo ? 3 : 2;
     // rotation matrix (Eigen toRotationMatrix)
     const double *q = P.q;
     const double tx = 2 * q[0], ty = 2 * q[1], tz = 2 * q[2];
@@ -171,140 +150,270 @@ __global__ __launch_bounds__(256) void k_ba_edges(const orbg_pose *__restrict__ 
     const double R[3][3] = {{1 - (tyy + tzz), txy - twz, txz + twy},
                             {txy + twz, 1 - (txx + tzz), tyz - twx},
                             {txz - twy, tyz + twx, 1 - (txx + tyy)}};
-    double jp[3][3] = {{0, 0, 0}, {0, 0, 0}, {0, 0, 0}};
     if (!e.stereo) {
         const double t02 = -x / z * fx, t12 = -y / z * fy;
+#pragma unroll
         for (int c = 0; c < 3; c++) {
-            jp[0][c] = -1. / z * (fx * R[0][c] + t02 * R[2][c]);
-            jp[1][c] = -1. / z * (fy * R[1][c] + t12 * R[2][c]);
+            L.jp[0][c] = -1. / z * (fx * R[0][c] + t02 * R[2][c]);
+            L.jp[1][c] = -1. / z * (fy * R[1][c] + t12 * R[2][c]);
+            L.jp[2][c] = 0;
         }
     } else {
+#pragma unroll
         for (int c = 0; c < 3; c++) {
-            jp[0][c] = -fx * R[0][c] / z + fx * x * R[2][c] / z_2;
-            jp[1][c] = -fy * R[1][c] / z + fy * y * R[2][c] / z_2;
-            jp[2][c] = jp[0][c] - e.bf * R[2][c] / z_2;
+            L.jp[0][c] = -fx * R[0][c] / z + fx * x * R[2][c] / z_2;
+            L.jp[1][c] = -fy * R[1][c] / z + fy * y * R[2][c] / z_2;
+            L.jp[2][c] = L.jp[0][c] - e.bf * R[2][c] / z_2;
         }
     }
-    double jt[3][6];
-    jt[0][0] = x * y / z_2 * fx;
-    jt[0][1] = -(1 + (x * x / z_2)) * fx;
-    jt[0][2] = y / z * fx;
-    jt[0][3] = -1. / z * fx;
-    jt[0][4] = 0;
-    jt[0][5] = x / z_2 * fx;
-    jt[1][0] = (1 + y * y / z_2) * fy;
-    jt[1][1] = -x * y / z_2 * fy;
-    jt[1][2] = -x / z * fy;
-    jt[1][3] = 0;
-    jt[1][4] = -1. / z * fy;
-    jt[1][5] = y / z_2 * fy;
+    L.jt[0][0] = x * y / z_2 * fx;
+    L.jt[0][1] = -(1 + (x * x / z_2)) * fx;
+    L.jt[0][2] = y / z * fx;
+    L.jt[0][3] = -1. / z * fx;
+    L.jt[0][4] = 0;
+    L.jt[0][5] = x / z_2 * fx;
+    L.jt[1][0] = (1 + y * y / z_2) * fy;
+    L.jt[1][1] = -x * y / z_2 * fy;
+    L.jt[1][2] = -x / z * fy;
+    L.jt[1][3] = 0;
+    L.jt[1][4] = -1. / z * fy;
+    L.jt[1][5] = y / z_2 * fy;
     if (e.stereo) {
-        jt[2][0] = jt[0][0] - e.bf * y / z_2;
-        jt[2][1] = jt[0][1] + e.bf * x / z_2;
-        jt[2][2] = jt[0][2];
-        jt[2][3] = jt[0][3];
-        jt[2][4] = 0;
-        jt[2][5] = jt[0][5] - e.bf / z_2;
+        L.jt[2][0] = L.jt[0][0] - e.bf * y / z_2;
+        L.jt[2][1] = L.jt[0][1] + e.bf * x / z_2;
+        L.jt[2][2] = L.jt[0][2];
+        L.jt[2][3] = L.jt[0][3];
+        L.jt[2][4] = 0;
+        L.jt[2][5] = L.jt[0][5] - e.bf / z_2;
     } else {
-        for (int c = 0; c < 6; c++) jt[2][c] = 0;
+#pragma unroll
+        for (int c = 0; c < 6; c++) L.jt[2][c] = 0;
     }
-    const double info = e.inv_sigma2;
-    // fixed trip counts (the third row of a mono edge is zero: adding it adds exact zeros)
-    // keep every array in registers
+    L.info = e.inv_sigma2;
     double chi2 = 0;
 #pragma unroll
-    for (int k = 0; k < 3; k++) chi2 += err[k] * (info * err[k]);
+    for (int k = 0; k < 3; k++) chi2 += L.err[k] * (L.info * L.err[k]);
     double rho1 = 1.0;
     if (e.robust) {
         const float dsqr = (float)(e.huber_delta * e.huber_delta);
         if (!(chi2 <= dsqr)) rho1 = e.huber_delta / sqrt(chi2);
     }
-    const double w = rho1 * info;
-    for (int k = 0; k < 3; k++) o->err[k] = err[k];
-    o->chi2 = chi2;
-    o->rho1 = rho1;
-    if (JAC) {
-        for (int k = 0; k < 3; k++)
-            for (int c = 0; c < 3; c++) o->jp[k][c] = jp[k][c];
-        for (int k = 0; k < 3; k++)
-            for (int c = 0; c < 6; c++) o->jt[k][c] = jt[k][c];
-    }
-    // point (vertex 0) block
-    double wr[3];
+    L.chi2 = chi2;
+    L.rho1 = rho1;
+    L.w = rho1 * L.info;
+}
+
+// per-edge outputs: field pointers with a stride in doubles per edge (the orbg_edge_out
+// records of the ABI, stride 50, or separate arrays); NULL = not stored
+struct BaEdgeOut {
+    double *err, *chi2, *rho1, *jp, *jt, *hpl;
+    int stride;
+};
+
+// ---------------------------------------------------------------------------
+// k_ba_edges: one thread per SLOT of the point-major edge order (CSR point_off / point_edges,
+// a point's edges contiguous in ascending edge index), so every lane linearises exactly one
+// edge (no per-lane loop over a point's edges: the wave's lanes do equal work).  Each lane
+// writes its edge's H_pl = J_point^T W J_pose (base_binary_edge.hpp:105-117: the block the
+// Schur step reads) plus the optional error terms / Jacobians, and stages its share of the
+// point block H_ll | b_l in LDS; the lane holding a point's first slot then sums the shares
+// in edge order (the oracle's order, same bits) and stores the block.  A point whose slots
+// run past the workgroup's 256 is finished by fp64 atomics of the per-workgroup partial sums
+// onto the zeroed block (two partials for any point with <= 256 edges: exact in either
+// order).  The pose blocks are k_ba_pose_mfma's, which recomputes the pose rows it needs.
+// ---------------------------------------------------------------------------
+#define BA_EDGES_TPB 256
+
+__global__ __launch_bounds__(BA_EDGES_TPB) void k_ba_edges(const orbg_pose *__restrict__ poses,
+                                                          const double *__restrict__ points,
+                                                          const orbg_edge *__restrict__ edges,
+                                                          int nslot,
+                                                          const int32_t *__restrict__ point_off,
+                                                          const int32_t *__restrict__ point_edges,
+                                                          BaEdgeOut o, double *__restrict__ hpoint,
+                                                          double *__restrict__ bpoint)
+{
+    __shared__ double part[12][BA_EDGES_TPB];  // H_ll row-major (9), b_l (3) per slot
+    const int t = threadIdx.x;
+    const int base = blockIdx.x * BA_EDGES_TPB;
+    const int a = base + t;
+    const int bend = min(base + BA_EDGES_TPB, nslot);
+    int q = -1;
+    {
+        double c[12];
 #pragma unroll
-    for (int k = 0; k < 3; k++) wr[k] = -info * err[k] * rho1;
-    // this edge's share of the point block (k_ba_point_blocks adds a point's edges in list
-    // order: no atomics, deterministic): pr = {H_ll row-major (9), b_l (3)}
+        for (int k = 0; k < 12; k++) c[k] = 0;
+        if (a < nslot) {
+            const int ei = point_edges[a];
+            const orbg_edge e = edges[ei];
+            const size_t ob = (size_t)ei * o.stride;
+            q = e.point;
+            if (!e.active) {  // setLevel(1): no contribution, outputs zero
+                if (o.hpl)
 #pragma unroll
-    for (int r = 0; r < 3; r++) {
-        double acc = 0;
+                    for (int k = 0; k < 18; k += 2)
+                        *(double2 *)(o.hpl + ob + k) = make_double2(0.0, 0.0);
+                if (o.err)
 #pragma unroll
-        for (int k = 0; k < 3; k++) acc += jp[k][r] * wr[k];
-        pr[9 + r] = acc;
+                    for (int k = 0; k < 3; k++) o.err[ob + k] = 0;
+                if (o.chi2) o.chi2[ob] = 0;
+                if (o.rho1) o.rho1[ob] = 0;
+                if (o.jp)
 #pragma unroll
-        for (int c = 0; c < 3; c++) {
-            double a2 = 0;
+                    for (int k = 0; k < 9; k++) o.jp[ob + k] = 0;
+                if (o.jt)
 #pragma unroll
-            for (int k = 0; k < 3; k++) a2 += jp[k][r] * w * jp[k][c];
-            pr[r * 3 + c] = a2;
+                    for (int k = 0; k < 18; k++) o.jt[ob + k] = 0;
+            } else {
+                const orbg_pose P = poses[e.pose];
+                const double X[3] = {points[3 * (size_t)q], points[3 * (size_t)q + 1],
+                                     points[3 * (size_t)q + 2]};
+                BaLin L;
+                ba_linearize_edge(P, X, e, L);
+                double wr[3];
+#pragma unroll
+                for (int k = 0; k < 3; k++) wr[k] = -L.info * L.err[k] * L.rho1;
+#pragma unroll
+                for (int r = 0; r < 3; r++) {
+                    double bs = 0;
+#pragma unroll
+                    for (int k = 0; k < 3; k++) bs += L.jp[k][r] * wr[k];
+                    c[9 + r] = bs;
+#pragma unroll
+                    for (int cc = 0; cc < 3; cc++) {
+                        double hs = 0;
+#pragma unroll
+                        for (int k = 0; k < 3; k++) hs += L.jp[k][r] * L.w * L.jp[k][cc];
+                        c[r * 3 + cc] = hs;
+                    }
+                }
+                if (o.hpl) {
+                    double h[18];
+#pragma unroll
+                    for (int r = 0; r < 3; r++)
+#pragma unroll
+                        for (int cc = 0; cc < 6; cc++) {
+                            double v = 0;
+                            if (!P.fixed)
+#pragma unroll
+                                for (int k = 0; k < 3; k++) v += L.jp[k][r] * L.w * L.jt[k][cc];
+                            h[r * 6 + cc] = v;
+                        }
+#pragma unroll
+                    for (int k = 0; k < 18; k += 2)
+                        *(double2 *)(o.hpl + ob + k) = make_double2(h[k], h[k + 1]);
+                }
+                if (o.err)
+#pragma unroll
+                    for (int k = 0; k < 3; k++) o.err[ob + k] = L.err[k];
+                if (o.chi2) o.chi2[ob] = L.chi2;
+                if (o.rho1) o.rho1[ob] = L.rho1;
+                if (o.jp)
+#pragma unroll
+                    for (int k = 0; k < 9; k++) o.jp[ob + k] = L.jp[k / 3][k % 3];
+                if (o.jt)
+#pragma unroll
+                    for (int k = 0; k < 18; k++) o.jt[ob + k] = L.jt[k / 6][k % 6];
+            }
         }
+#pragma unroll
+        for (int k = 0; k < 12; k++) part[k][t] = c[k];
     }
-    // H_pl = J_point^T W J_pose (stored per edge, base_binary_edge.hpp:105-117)
+    __syncthreads();
+    if (a >= nslot) return;
+    const int qs = point_off[q], qe = point_off[q + 1];
+    if (a != qs && t != 0) return;  // not the first slot of its point in this workgroup
+    const int end = min(qe, bend) - base;
+    double acc[12];
 #pragma unroll
-    for (int r = 0; r < 3; r++)
+    for (int k = 0; k < 12; k++) acc[k] = 0;
+    for (int j = t; j < end; j++)
 #pragma unroll
-        for (int c = 0; c < 6; c++) {
-            double a2 = 0;
-            if (!P.fixed)
+        for (int k = 0; k < 12; k++) acc[k] += part[k][j];
+    double *hq = hpoint + 9 * (size_t)q, *bq = bpoint + 3 * (size_t)q;
+    if (qs < base || qe > bend) {  // the point's slots span workgroups: partial sums
 #pragma unroll
-                for (int k = 0; k < 3; k++) a2 += jp[k][r] * w * jt[k][c];
-            o->hpl[r][c] = a2;
-        }
-    // pose rows for k_ba_pose_mfma
+        for (int k = 0; k < 9; k++) atomicAdd(hq + k, acc[k]);
 #pragma unroll
-    for (int k = 0; k < 3; k++) {
-        const bool on = k < D;
-        for (int c = 0; c < 6; c++) row[k * BA_ROW + c] = on ? jt[k][c] : 0.0;
-        row[k * BA_ROW + 6] = on ? -err[k] : 0.0;
-        row[k * BA_ROW + 7] = on ? w : 0.0;
+        for (int k = 0; k < 3; k++) atomicAdd(bq + k, acc[9 + k]);
+    } else {
+#pragma unroll
+        for (int k = 0; k < 9; k++) hq[k] = acc[k];
+#pragma unroll
+        for (int k = 0; k < 3; k++) bq[k] = acc[9 + k];
     }
 }
 
 // ---------------------------------------------------------------------------
-// k_ba_pose_mfma: one wave per pose.  With v_r = [J_pose row | -e] (7 wide) and weight w_r
-// over the pose's rows r (3 per edge, from the pose's edge list),
+// k_ba_pose_mfma: one wave per 64-edge slice of one pose's edge list.  Lane l recomputes edge
+// l's three pose rows v_r = [J_pose row | -e] (7 wide) and weight w_r = rho' invSigma2 (zero
+// rows for the third row of mono edges and for inactive edges) into LDS, then
 //     C = sum_r (w_r v_r)^T v_r   gives  H_pp = C[0:6][0:6],  b_p = C[0:6][6]
-// (constructQuadraticForm's A^T W A and A^T omega_r, omega_r = -rho' Omega e), accumulated
-// in fp64 by v_mfma_f64_16x16x4_f64: each instruction folds 4 rows, A[i][k] = w v[i] and
-// B[k][j] = v[j] padded from 7 to 16.  Fixed poses get no block (g2o skips them).
+// (constructQuadraticForm's A^T W A and A^T omega_r, omega_r = -rho' Omega e), accumulated in
+// fp64 by v_mfma_f64_16x16x4_f64: each instruction folds 4 rows, A[i][k] = w v[i] and
+// B[k][j] = v[j] padded from 7 to 16.  Slices of one pose add by fp64 atomics.  Fixed poses
+// get no block (g2o skips them).
 // ---------------------------------------------------------------------------
 typedef double v4d __attribute__((ext_vector_type(4)));
 
-#define BA_SLICE 64  // edges per wave: a pose's rows are split over waves, blocks add up
+#define BA_SLICE 64  // edges per wave
+#define BA_ROW 8     // doubles per staged pose row: J_pose (6), -e, w
 
 __global__ __launch_bounds__(256) void k_ba_pose_mfma(const orbg_pose *__restrict__ poses,
-                                                      int npose,
+                                                      const double *__restrict__ points,
+                                                      const orbg_edge *__restrict__ edges,
                                                       const int32_t *__restrict__ pose_off,
                                                       const int32_t *__restrict__ pose_edges,
                                                       const int32_t *__restrict__ slice_off,
                                                       const int32_t *__restrict__ slice_pose,
-                                                      int nslice,
-                                                      const double *__restrict__ rows,
-                                                      double *__restrict__ hpose,
+                                                      int nslice, double *__restrict__ hpose,
                                                       double *__restrict__ bpose)
 {
-    const int lane = threadIdx.x & 63;
-    const int sl = blockIdx.x * 4 + (threadIdx.x >> 6);
-    if (sl >= nslice) return;
+    __shared__ double rows_lds[4][3 * BA_SLICE * BA_ROW];  // 12 KB per wave
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    const int sl = blockIdx.x * 4 + wv;
+    if (sl >= nslice) return;    // wave-uniform; no workgroup barrier below
     const int p = slice_pose[sl];
     if (p < 0) return;           // past the last slice (table filled with -1)
-    if (poses[p].fixed) return;  // stays zero (memset): g2o builds no block for it
+    const orbg_pose P = poses[p];
+    if (P.fixed) return;         // stays zero (memset): g2o builds no block for it
     double *H = hpose + 36 * (size_t)p, *bv = bpose + 6 * (size_t)p;
-    // this wave = slice (sl - slice_off[p]) of pose p: edges [e0, e0 + ne) of its list
     const int e0p = pose_off[p], nep = pose_off[p + 1] - e0p;
     const int ks = sl - slice_off[p];
     const int e0 = e0p + ks * BA_SLICE;
     const int ne = min(BA_SLICE, nep - ks * BA_SLICE);
+    double *rl = rows_lds[wv];
+    {
+        // lane l: edge l of the slice -> rows 3l .. 3l+2
+        double v[3][BA_ROW];
+#pragma unroll
+        for (int k = 0; k < 3; k++)
+#pragma unroll
+            for (int c = 0; c < BA_ROW; c++) v[k][c] = 0;
+        if (lane < ne) {
+            const orbg_edge e = edges[pose_edges[e0 + lane]];
+            if (e.active) {
+                const double X[3] = {points[3 * (size_t)e.point], points[3 * (size_t)e.point + 1],
+                                     points[3 * (size_t)e.point + 2]};
+                BaLin L;
+                ba_linearize_edge(P, X, e, L);
+#pragma unroll
+                for (int k = 0; k < 3; k++) {
+                    const bool on = k < L.D;
+#pragma unroll
+                    for (int c = 0; c < 6; c++) v[k][c] = on ? L.jt[k][c] : 0.0;
+                    v[k][6] = on ? -L.err[k] : 0.0;
+                    v[k][7] = on ? L.w : 0.0;
+                }
+            }
+        }
+#pragma unroll
+        for (int k = 0; k < 3; k++)
+#pragma unroll
+            for (int c = 0; c < BA_ROW; c += 2)
+                *(double2 *)(rl + (3 * lane + k) * BA_ROW + c) = make_double2(v[k][c], v[k][c + 1]);
+    }
+    wave_sync_lds_ba();
     const int nrow = 3 * ne;
     const int i = lane & 15, k = lane >> 4;  // A: (row i of the 16x4 tile, k); B: (k, column i)
     const int col = i < 7 ? i : 7;           // padded columns read the weight and are zeroed
@@ -312,15 +421,11 @@ __global__ __launch_bounds__(256) void k_ba_pose_mfma(const orbg_pose *__restric
     for (int r0 = 0; r0 < nrow; r0 += 4 * 4) {
         double va[4], vb[4];
 #pragma unroll
-        for (int u = 0; u < 4; u++) {  // four MFMA steps' loads in flight
-            const int r = r0 + 4 * u + k;
-            double v = 0, w = 0;
-            if (r < nrow) {
-                const double *rw = rows + ((size_t)pose_edges[e0 + r / 3] * 3 + r % 3) * BA_ROW;
-                v = rw[col];
-                w = rw[7];
-            }
-            vb[u] = i < 7 ? v : 0.0;
+        for (int u = 0; u < 4; u++) {
+            const int r = min(r0 + 4 * u + k, 3 * BA_SLICE - 1);  // rows past nrow are zero rows or
+            const double vv = rl[r * BA_ROW + col];               // beyond: weight zeroed below
+            const double w = r0 + 4 * u + k < nrow ? rl[r * BA_ROW + 7] : 0.0;
+            vb[u] = i < 7 ? vv : 0.0;
             va[u] = vb[u] * w;
         }
 #pragma unroll
@@ -335,34 +440,6 @@ __global__ __launch_bounds__(256) void k_ba_pose_mfma(const orbg_pose *__restric
         if (row < 6 && j < 6) atomicAdd(&H[row * 6 + j], C[v]);
         if (row < 6 && j == 6) atomicAdd(&bv[row], C[v]);
     }
-}
-
-// k_ba_point_blocks: thread per point, sums its edges' shares in list order
-__global__ __launch_bounds__(256) void k_ba_point_blocks(int npoint,
-                                                         const int32_t *__restrict__ point_off,
-                                                         const int32_t *__restrict__ point_edges,
-                                                         const double *__restrict__ prow,
-                                                         double *__restrict__ hpoint,
-                                                         double *__restrict__ bpoint)
-{
-    const int q = blockIdx.x * blockDim.x + threadIdx.x;
-    if (q >= npoint) return;
-    double acc[BA_PROW];
-#pragma unroll
-    for (int k = 0; k < BA_PROW; k++) acc[k] = 0;
-    for (int a = point_off[q]; a < point_off[q + 1]; a++) {
-        const double2 *pr = (const double2 *)(prow + (size_t)point_edges[a] * BA_PROW);
-#pragma unroll
-        for (int k = 0; k < BA_PROW / 2; k++) {
-            const double2 v = pr[k];
-            acc[2 * k] += v.x;
-            acc[2 * k + 1] += v.y;
-        }
-    }
-#pragma unroll
-    for (int k = 0; k < 9; k++) hpoint[9 * (size_t)q + k] = acc[k];
-#pragma unroll
-    for (int k = 0; k < 3; k++) bpoint[3 * (size_t)q + k] = acc[9 + k];
 }
 
 // slice -> pose table: pose p owns ceil(edges_p / BA_SLICE) consecutive slices
@@ -401,13 +478,11 @@ __global__ __launch_bounds__(256) void k_ba_slices(const int32_t *__restrict__ p
 
 static size_t al(size_t x) { return (x + 255) & ~(size_t)255; }
 
-// rows + slice tables (upper bound: one slice per pose plus one per BA_SLICE edges)
+// slice tables (upper bound: one slice per pose plus one per BA_SLICE edges)
 size_t ba_rows_bytes(int nedge, int npose)
 {
     const size_t ns = (size_t)(npose > 0 ? npose : 1) + (size_t)(nedge > 0 ? nedge : 1) / BA_SLICE;
-    return al((size_t)(nedge > 0 ? nedge : 1) * 3 * BA_ROW * 8) +
-           al((size_t)(nedge > 0 ? nedge : 1) * BA_PROW * 8) + al((npose + 1) * 4) +
-           al(ns * 4) + 256;
+    return al((npose + 1) * 4) + al(ns * 4) + 256;
 }
 
 size_t ba_scratch_bytes(int npose, int npoint, int nedge)
@@ -420,37 +495,51 @@ size_t ba_scratch_bytes(int npose, int npoint, int nedge)
            ba_rows_bytes(nedge, npose);
 }
 
+// the orbg_edge_out records (include/orbg.h) as strided fields
+static BaEdgeOut eout_fields(orbg_edge_out *eout, bool jacobians, bool errors)
+{
+    BaEdgeOut o{};
+    if (!eout) return o;
+    o.stride = (int)(sizeof(orbg_edge_out) / sizeof(double));
+    o.hpl = &eout[0].hpl[0][0];
+    if (errors) {
+        o.err = &eout[0].err[0];
+        o.chi2 = &eout[0].chi2;
+        o.rho1 = &eout[0].rho1;
+    }
+    if (jacobians) {
+        o.jp = &eout[0].jp[0][0];
+        o.jt = &eout[0].jt[0][0];
+    }
+    return o;
+}
 
-// device-resident linearisation: every pointer is device memory; rows = ba_rows_bytes(nedge)
+// device-resident linearisation: every pointer is device memory; scratch = ba_rows_bytes
 int launch_ba_device(hipStream_t st, const orbg_pose *poses, int npose, const double *points,
                      int npoint, const orbg_edge *edges, int nedge, const int32_t *pose_off,
                      const int32_t *pose_edges, const int32_t *point_off,
                      const int32_t *point_edges, orbg_edge_out *eout, double *hpose,
-                     double *bpose, double *hpoint, double *bpoint, double *rows, void *prof,
-                     bool jacobians)
+                     double *bpose, double *hpoint, double *bpoint, double *scr, void *prof,
+                     bool jacobians, bool errors)
 {
-    double *prow = (double *)((uint8_t *)rows + al((size_t)(nedge > 0 ? nedge : 1) * 3 * BA_ROW * 8));
+    if (npoint) {
+        // points without edges keep zero blocks; points spanning workgroups are summed onto
+        // zero by atomics
+        if (hipMemsetAsync(hpoint, 0, (size_t)npoint * 9 * 8, st) != hipSuccess ||
+            hipMemsetAsync(bpoint, 0, (size_t)npoint * 3 * 8, st) != hipSuccess)
+            return -5;
+    }
     if (nedge) {
         hipEvent_t a = nullptr;
         prof_begin(prof, st, "ba_edges", &a);
-        if (jacobians)
-            hipLaunchKernelGGL(k_ba_edges<true>, dim3((nedge + 255) / 256), dim3(256), 0, st, poses,
-                               points, edges, nedge, eout, rows, prow);
-        else
-            hipLaunchKernelGGL(k_ba_edges<false>, dim3((nedge + 255) / 256), dim3(256), 0, st, poses,
-                               points, edges, nedge, eout, rows, prow);
+        hipLaunchKernelGGL(k_ba_edges, dim3((nedge + BA_EDGES_TPB - 1) / BA_EDGES_TPB),
+                           dim3(BA_EDGES_TPB), 0, st, poses, points, edges, nedge, point_off,
+                           point_edges, eout_fields(eout, jacobians, errors), hpoint, bpoint);
         prof_end(prof, st, "ba_edges", a);
     }
-    if (npoint) {
-        hipEvent_t a = nullptr;
-        prof_begin(prof, st, "ba_point_blocks", &a);
-        hipLaunchKernelGGL(k_ba_point_blocks, dim3((npoint + 255) / 256), dim3(256), 0, st,
-                           npoint, point_off, point_edges, prow, hpoint, bpoint);
-        prof_end(prof, st, "ba_point_blocks", a);
-    }
     if (npose) {
-        // scratch after rows and point shares: slice_off[npose+1], slice_pose[max], nslice
-        uint8_t *t = (uint8_t *)prow + al((size_t)(nedge > 0 ? nedge : 1) * BA_PROW * 8);
+        // scratch: slice_off[npose+1], slice_pose[max], nslice
+        uint8_t *t = (uint8_t *)scr;
         int32_t *slice_off = (int32_t *)t;
         t += al((npose + 1) * 4);
         int32_t *slice_pose = (int32_t *)t;
@@ -467,7 +556,7 @@ int launch_ba_device(hipStream_t st, const orbg_pose *poses, int npose, const do
         prof_begin(prof, st, "ba_pose_mfma", &a);
         // the grid covers the bound; waves past the actual slice count exit at once
         hipLaunchKernelGGL(k_ba_pose_mfma, dim3((max_slices + 3) / 4), dim3(256), 0, st, poses,
-                           npose, pose_off, pose_edges, slice_off, slice_pose, max_slices, rows,
+                           points, edges, pose_off, pose_edges, slice_off, slice_pose, max_slices,
                            hpose, bpose);
         prof_end(prof, st, "ba_pose_mfma", a);
     }
@@ -520,7 +609,7 @@ int launch_ba(hipStream_t st, const orbg_pose *poses, int npose, const double *p
     if (nedge) CK(hipMemcpyAsync(d_qe, point_edges, nedge * 4, hipMemcpyHostToDevice, st));
     const int rc = launch_ba_device(st, d_pose, npose, d_pts, npoint, d_edges, nedge, d_off, d_pe,
                                     d_qoff, d_qe, d_eout, d_hpose, d_bpose, d_hpt, d_bpt, d_rows,
-                                    prof, true);
+                                    prof, true, true);
     if (rc) return rc;
     if (eout && nedge)
         CK(hipMemcpyAsync(eout, d_eout, nedge * sizeof(orbg_edge_out), hipMemcpyDeviceToHost, st));

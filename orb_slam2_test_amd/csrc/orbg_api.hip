@@ -87,8 +87,8 @@ int launch_ba_device(hipStream_t st, const orbg_pose *poses, int npose, const do
                      int npoint, const orbg_edge *edges, int nedge, const int32_t *pose_off,
                      const int32_t *pose_edges, const int32_t *point_off,
                      const int32_t *point_edges, orbg_edge_out *eout, double *hpose,
-                     double *bpose, double *hpoint, double *bpoint, double *rows, void *prof,
-                     bool jacobians);
+                     double *bpose, double *hpoint, double *bpoint, double *scr, void *prof,
+                     bool jacobians, bool errors);
 size_t ba_rows_bytes(int nedge, int npose);
 // stereo_kernels.hip
 size_t stereo_scratch_bytes(int npairs, int frame_cap);
@@ -247,6 +247,7 @@ struct orbg_ctx {
     bool blur_side = false;  // ORBG_BLUR_SIDE
     bool serial = false;     // orbg_set_serial: no stream overlap (isolated kernel timing)
     bool ba_jacobians = true;  // orbg_ba_set_jacobians
+    bool ba_edge_errors = true;  // orbg_ba_set_edge_errors
     int oct_mode = 0;
     int blur0_mode = 0;  // measured: 2.013 vs 2.025 ms per 256 frames with it on
     int fast0_mode = 1;  // level-0 FAST cells on `ostream` beside the resize chain (ORBG_FAST0)
@@ -2443,6 +2444,13 @@ extern "C" int orbg_ba_set_jacobians(orbg_ctx *c, int enable)
     return ORBG_OK;
 }
 
+extern "C" int orbg_ba_set_edge_errors(orbg_ctx *c, int enable)
+{
+    if (!c) return set_err(ORBG_EINVAL, "ctx is NULL");
+    c->ba_edge_errors = enable != 0;
+    return ORBG_OK;
+}
+
 extern "C" int orbg_ba_linearize_device(orbg_ctx *c, const orbg_pose *d_poses, int npose,
                                         const double *d_points, int npoint,
                                         const orbg_edge *d_edges, int nedge,
@@ -2464,7 +2472,8 @@ extern "C" int orbg_ba_linearize_device(orbg_ctx *c, const orbg_pose *d_poses, i
     if (rc) return rc;
     rc = launch_ba_device(c->stream, d_poses, npose, d_points, npoint, d_edges, nedge, d_pose_off,
                           d_pose_edges, d_point_off, d_point_edges, d_eout, d_hpose, d_bpose,
-                          d_hpoint, d_bpoint, (double *)s, &c->prof, c->ba_jacobians);
+                          d_hpoint, d_bpoint, (double *)s, &c->prof, c->ba_jacobians,
+                          c->ba_edge_errors);
     if (rc) return set_err(ORBG_EIO, "BA kernel launch failed");
     return ORBG_OK;
 }

@@ -18,6 +18,22 @@ __device__ __forceinline__ int wave_incl_scan(int x)
     return x;
 }
 
+// inclusive wave64 prefix sum by DPP (row_shr 1..3 from the inputs, row_shr 4 / 8 with bank
+// masks, row_bcast 15 / 31 with row masks): seven adds, no LDS round trips (__shfl_up is a
+// ds_bpermute).  Integer adds, exact.
+__device__ __forceinline__ int wave_incl_scan_dpp(int x)
+{
+    int y = x;
+    y += __builtin_amdgcn_update_dpp(0, x, 0x111, 0xf, 0xf, true);  // row_shr:1
+    y += __builtin_amdgcn_update_dpp(0, x, 0x112, 0xf, 0xf, true);  // row_shr:2
+    y += __builtin_amdgcn_update_dpp(0, x, 0x113, 0xf, 0xf, true);  // row_shr:3
+    y += __builtin_amdgcn_update_dpp(0, y, 0x114, 0xf, 0xe, true);  // row_shr:4, banks 1-3
+    y += __builtin_amdgcn_update_dpp(0, y, 0x118, 0xf, 0xc, true);  // row_shr:8, banks 2-3
+    y += __builtin_amdgcn_update_dpp(0, y, 0x142, 0xa, 0xf, false); // row_bcast:15, rows 1, 3
+    y += __builtin_amdgcn_update_dpp(0, y, 0x143, 0xc, 0xf, false); // row_bcast:31, rows 2, 3
+    return y;
+}
+
 // inclusive wave prefix of small counts 0 <= x < 8 from three ballots (no shuffles);
 // *total = wave total
 __device__ __forceinline__ int wave_incl_scan_small(int x, int *total)

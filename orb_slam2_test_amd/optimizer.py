@@ -115,10 +115,11 @@ class DeviceLBA:
     with every array in HBM -- the per-iteration work of g2o's computeActiveErrors +
     buildSystem."""
 
-    def __init__(self, poses, points, edges, device=0, jacobians=True):
+    def __init__(self, poses, points, edges, device=0, jacobians=True, edge_errors=True):
         import torch
         self.ctx = _ctx(device)
         self.jacobians = bool(jacobians)  # eout.jp / jt stored (orbg_ba_set_jacobians)
+        self.edge_errors = bool(edge_errors)  # eout.err / chi2 / rho1 (orbg_ba_set_edge_errors)
         self.np, self.nq, self.ne = len(poses), len(points), len(edges)
         off, pe = vertex_csr(edges, "pose", self.np)
         qoff, qe = vertex_csr(edges, "point", self.nq)
@@ -137,17 +138,29 @@ class DeviceLBA:
         self.d_bpose = torch.zeros((self.np, 6), dtype=torch.float64, device=dev)
         self.d_hpoint = torch.zeros((self.nq, 3, 3), dtype=torch.float64, device=dev)
         self.d_bpoint = torch.zeros((self.nq, 3), dtype=torch.float64, device=dev)
+        self.d_chi2 = torch.zeros(max(self.ne, 1), dtype=torch.float64, device=dev)
+        self.d_rho0 = torch.zeros(max(self.ne, 1), dtype=torch.float64, device=dev)
         torch.cuda.synchronize(dev)
 
     def linearize(self):
         p = lambda t: L.C.c_void_p(t.data_ptr())  # noqa: E731
         L.check(L.lib().orbg_ba_set_jacobians(self.ctx.handle, 1 if self.jacobians else 0),
                 "orbg_ba_set_jacobians")
+        L.check(L.lib().orbg_ba_set_edge_errors(self.ctx.handle, 1 if self.edge_errors else 0),
+                "orbg_ba_set_edge_errors")
         L.check(L.lib().orbg_ba_linearize_device(
             self.ctx.handle, p(self.d_poses), self.np, p(self.d_points), self.nq, p(self.d_edges),
             self.ne, p(self.d_off), p(self.d_pe), p(self.d_qoff), p(self.d_qe), p(self.d_eout),
             p(self.d_hpose),
             p(self.d_bpose), p(self.d_hpoint), p(self.d_bpoint)), "orbg_ba_linearize_device")
+
+    def errors(self):
+        """The per-trial error pass (orbg_ba_errors_device): chi2 and the robust term of every
+        edge into self.d_chi2 / self.d_rho0."""
+        p = lambda t: L.C.c_void_p(t.data_ptr())  # noqa: E731
+        L.check(L.lib().orbg_ba_errors_device(self.ctx.handle, p(self.d_poses), p(self.d_points),
+                                              p(self.d_edges), self.ne, None, p(self.d_chi2),
+                                              p(self.d_rho0), None), "orbg_ba_errors_device")
 
     def download(self):
         self.ctx.sync()

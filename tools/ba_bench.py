@@ -3,10 +3,14 @@
 
 One "iteration" = g2o's computeActiveErrors + buildSystem arithmetic for every edge of W
 independent LBA windows (10 local + 10 fixed KFs, 6000 points, ~27k edges, 60% stereo,
-KITTI intrinsics), HBM-resident, through orbg_ba_linearize_device: k_ba_edges (thread per
-edge, fp64) + k_ba_pose_mfma (MFMA f64 pose blocks).  Prints one JSON line with edges/s,
-per-kernel HIP-event times, the HBM roofline of k_ba_edges (108 algorithmic
-bytes per edge) and the oracle (fp64 C restatement) on one window on one host core.
+KITTI intrinsics), HBM-resident: orbg_ba_linearize_device -- k_ba_edges (thread per point
+over its edges, fp64: H_pl per edge, the point blocks) + k_ba_pose_mfma (MFMA f64 pose
+blocks, rows recomputed) -- and the error pass orbg_ba_errors_device (k_ba_errors: chi2 and
+the robust term per edge).  Prints one JSON line with edges/s, per-kernel HIP-event times,
+the HBM roofline of k_ba_edges (108 algorithmic bytes per edge; beside it the
+bytes the ABI makes unavoidable: the 112-byte edge record in, H_pl's 144 bytes out, the
+point's 24 + 96 bytes per edge share) and the oracle (fp64 C restatement) on one window on
+one host core.
 
     python tools/ba_bench.py [--windows 64] [--iters 20] [--warmup 3]
 """
@@ -24,7 +28,7 @@ sys.path.insert(0, ROOT)
 HBM_PEAK_GBS = 8000.0
 EDGE_ALGO_BYTES = 108  # per-edge algorithmic bytes
 F64_MFMA_PEAK_TFLOPS = 78.6  # MI355X FP64 matrix, AMD spec (the guide lists no FP64 row)
-PMC_BA = "r02f_ba_pmc_kernels.json"  # tools/pmc_kernels.py over tools/r02_ba_profile.sh
+PMC_BA = "r03_ba_pmc_kernels.json"  # tools/profile.sh <tag> tools/ba_bench.py
 
 
 def main():
@@ -36,6 +40,9 @@ def main():
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--jacobians", action="store_true",
                     help="also store g2o's per-edge Jacobians eout.jp / jt (orbg_ba_set_jacobians)")
+    ap.add_argument("--edge-errors", action="store_true",
+                    help="also store eout.err / chi2 / rho1 in the linearisation pass "
+                         "(orbg_ba_set_edge_errors; the iteration's error pass provides them)")
     args = ap.parse_args()
 
     import torch
@@ -46,16 +53,21 @@ def main():
 
     base = [S.ba_window(seed=500 + i) for i in range(args.distinct)]
     poses, pts, edges = concat_windows([base[i % args.distinct] for i in range(args.windows)])
-    lba = DeviceLBA(poses, pts, edges, jacobians=args.jacobians)
-    for _ in range(args.warmup):
+    lba = DeviceLBA(poses, pts, edges, jacobians=args.jacobians, edge_errors=args.edge_errors)
+
+    def iteration():
         lba.linearize()
+        lba.errors()
+
+    for _ in range(args.warmup):
+        iteration()
     lba.ctx.sync()
     lba.ctx.profile(True)
     lba.ctx.profile_reset()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for _ in range(args.iters):
-        lba.linearize()
+        iteration()
     lba.ctx.sync()
     torch.cuda.synchronize()
     dt = time.perf_counter() - t0
@@ -69,7 +81,10 @@ def main():
         "config": {"workload": "configs[4]: %d KITTI00-like LBA windows (20 KFs, 6000 points)"
                                % args.windows, "edges": ne, "poses": len(poses),
                    "points": len(pts), "stereo_frac": round(float(np.mean(edges["stereo"])), 3),
-                   "edge_jacobians_stored": bool(args.jacobians)},
+                   "edge_jacobians_stored": bool(args.jacobians),
+                   "edge_errors_stored": bool(args.edge_errors),
+                   "iteration": "orbg_ba_linearize_device (buildSystem) + orbg_ba_errors_device "
+                                "(computeActiveErrors)"},
         "ms_per_iter": round(dt / args.iters * 1e3, 4),
         "kernels": {k: {"ms_per_iter": round(v[0] / args.iters, 4),
                         "avg_launch_ms": round(v[0] / max(v[1], 1), 5)} for k, v in kern.items()},
@@ -77,10 +92,16 @@ def main():
     if "ba_edges" in kern:
         ms = kern["ba_edges"][0] / max(kern["ba_edges"][1], 1)
         ach = ne * EDGE_ALGO_BYTES / (ms * 1e-3) / 1e9
+        # the bytes the ABI makes unavoidable: the edge record and its CSR slot in, H_pl out
+        # (g2o's _Hpl, read by the Schur step: not in SURVEY 8d's 108 B), the point in and its
+        # H_ll | b_l out
+        abi = ne * (112 + 4 + 144) + len(pts) * (24 + 4 + 96)
         out["roofline"] = {"kernel": "ba_edges", "bound": "hbm", "achieved": round(ach, 1),
                            "peak": HBM_PEAK_GBS, "unit": "GB/s",
                            "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": None,
                            "algo_bytes_per_launch": ne * EDGE_ALGO_BYTES,
+                           "abi_min_bytes_per_launch": abi,
+                           "abi_min_achieved": round(abi / (ms * 1e-3) / 1e9, 1),
                            "avg_launch_ms": round(ms, 5)}
     pk = {}
     pmc = os.path.join(ROOT, "profiles", PMC_BA)
@@ -88,7 +109,11 @@ def main():
         with open(pmc) as f:
             pk = json.load(f)
     if "roofline" in out:
-        out["roofline"]["traffic"] = pk.get("ba_edges", {}).get("hbm_bytes_per_launch")
+        tr = pk.get("ba_edges", {}).get("hbm_bytes_per_launch")
+        out["roofline"]["traffic"] = tr
+        if tr:
+            out["roofline"]["traffic_over_algo"] = round(tr / out["roofline"]["algo_bytes_per_launch"], 3)
+            out["roofline"]["traffic_over_abi_min"] = round(tr / out["roofline"]["abi_min_bytes_per_launch"], 3)
         out["roofline"]["pmc_source"] = os.path.relpath(pmc, ROOT) if pk else None
     if "ba_pose_mfma" in kern:
         # MFMAs issued: per slice of <= 64 edges of a free pose, 4 per 16 rows (3 per edge)
