@@ -116,6 +116,24 @@ __device__ __forceinline__ v2s fast_score_pair(const Rows7 &R)
     return pmax(M - one, zero);  // u8 score, 0 = none
 }
 
+// bytes OFF + s and OFF + s + 1 of the 12-byte window {w0, w1, w2}, s = 0 or 2 per lane,
+// as two zero-extended u16 lanes: one v_perm_b32 whose selector is sel[OFF] = the s = 0
+// selector + (s, s) in its two index bytes (the caller adds s once per task).  OFF <= 4
+// picks from w0:w1 (bytes OFF + s + 1 <= 7), OFF >= 5 from w1:w2 (bytes 5 .. 9).
+template <int OFF>
+__device__ __forceinline__ constexpr uint32_t gather2_rt_sel()
+{
+    static_assert(OFF >= 0 && OFF <= 6, "window");
+    return OFF <= 4 ? (0x0c000c00u | (uint32_t)(OFF + 1) << 16 | (uint32_t)OFF)
+                    : (0x0c000c00u | (uint32_t)(OFF - 3) << 16 | (uint32_t)(OFF - 4));
+}
+template <int OFF>
+__device__ __forceinline__ v2s gather2_rt(uint32_t w0, uint32_t w1, uint32_t w2, uint32_t sel)
+{
+    const uint32_t r = OFF <= 4 ? __builtin_amdgcn_perm(w1, w0, sel) : __builtin_amdgcn_perm(w2, w1, sel);
+    return __builtin_bit_cast(v2s, r);
+}
+
 // One side of the score of two pixels, the bright side: M = max_k min(x[k .. k+8]) - v, u8
 // score max(M - 1, 0).  The dark side is the bright side of the complemented pixels
 // (255 - x and 255 - v: v - min_k max(x[k .. k+8]) = max_k min(255 - x) - (255 - v)), so
@@ -158,6 +176,53 @@ __device__ __forceinline__ v2s fast_score_side(const Rows7 &R)
     for (int j = 0; j < 8; j++)  // even k = 2j: min(l_{k+1}, max(x_k, x_{k+9}))
         m[j] = hmin3(q[j], q[(j + 2) & 7],
                      __builtin_elementwise_maximum(x[2 * j], x[(2 * j + 9) & 15]));
+    const h2 amax = __builtin_elementwise_maximum(
+        hmax3(hmax3(m[0], m[1], m[2]), hmax3(m[3], m[4], m[5]), m[6]), m[7]);
+    const v2s zero = (v2s){0, 0}, one = (v2s){1, 1};
+    return pmax(as_v2s(amax) - v - one, zero);
+}
+
+// fast_score_side of pixel pair s / 2 (s = 0: pixels 0-1, s = 2: pixels 2-3) of the unit whose
+// rows R hold window bytes 0 .. 11 (pixel 0 at byte 3), s per lane: the seven selectors
+// gather2_rt_sel<0..6>() + (s, s) are built once per task.
+__device__ __forceinline__ v2s fast_score_side_rt(const Rows7 &R, uint32_t sadd)
+{
+    uint32_t sel[7];
+    sel[0] = gather2_rt_sel<0>() + sadd;
+    sel[1] = gather2_rt_sel<1>() + sadd;
+    sel[2] = gather2_rt_sel<2>() + sadd;
+    sel[3] = gather2_rt_sel<3>() + sadd;
+    sel[4] = gather2_rt_sel<4>() + sadd;
+    sel[5] = gather2_rt_sel<5>() + sadd;
+    sel[6] = gather2_rt_sel<6>() + sadd;
+#define GB(row, dx) as_h2(gather2_rt<3 + (dx)>(R.w[row][0], R.w[row][1], R.w[row][2], sel[3 + (dx)]))
+    const v2s v = gather2_rt<3>(R.w[3][0], R.w[3][1], R.w[3][2], sel[3]);
+    h2 x[16];
+    x[0] = GB(6, 0);
+    x[1] = GB(6, 1);
+    x[2] = GB(5, 2);
+    x[3] = GB(4, 3);
+    x[4] = GB(3, 3);
+    x[5] = GB(2, 3);
+    x[6] = GB(1, 2);
+    x[7] = GB(0, 1);
+    x[8] = GB(0, 0);
+    x[9] = GB(0, -1);
+    x[10] = GB(1, -2);
+    x[11] = GB(2, -3);
+    x[12] = GB(3, -3);
+    x[13] = GB(4, -3);
+    x[14] = GB(5, -2);
+    x[15] = GB(6, -1);
+#undef GB
+    h2 p[8], q[8], m[8];
+#pragma unroll
+    for (int j = 0; j < 8; j++) p[j] = __builtin_elementwise_minimum(x[2 * j + 1], x[(2 * j + 2) & 15]);
+#pragma unroll
+    for (int j = 0; j < 8; j++) q[j] = __builtin_elementwise_minimum(p[j], p[(j + 1) & 7]);
+#pragma unroll
+    for (int j = 0; j < 8; j++)
+        m[j] = hmin3(q[j], q[(j + 2) & 7], __builtin_elementwise_maximum(x[2 * j], x[(2 * j + 9) & 15]));
     const h2 amax = __builtin_elementwise_maximum(
         hmax3(hmax3(m[0], m[1], m[2]), hmax3(m[3], m[4], m[5]), m[6]), m[7]);
     const v2s zero = (v2s){0, 0}, one = (v2s){1, 1};

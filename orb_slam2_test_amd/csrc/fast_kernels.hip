@@ -7,9 +7,9 @@
 // version cuts instructions:
 //   - the LDS row pitch is a template parameter: every row offset of the 7-row circle reads
 //     is an immediate of the ds_read, no address arithmetic per row;
-//   - the window is staged once per 16-byte chunk with a fixed (row, chunk) per lane, plus a
-//     copy shifted by 2 bytes, so pixel pairs 2-3 of a 4-pixel unit are read exactly like
-//     pairs 0-1 (one code path for both);
+//   - the window is staged once per 16-byte chunk with a fixed (row, chunk) per lane; both
+//     pixel pairs of a 4-pixel unit are gathered from the unit's three row dwords, pair 2-3
+//     by v_perm selectors shifted 2 bytes per lane (one code path for both);
 //   - the compass pretest keeps the bright and dark verdicts apart, and each listed entry
 //     scores ONE side of one pixel pair (a pixel is never a corner on both sides at one
 //     threshold: 9 + 9 > 16 circle pixels): the dark side is the bright side of the
@@ -29,15 +29,12 @@
 namespace orbg {
 
 // LDS per wave (fc2_* offsets in OrbgGeom, host plan):
-//   tA [H][2P]    window row r at byte r * 2P + x (x window-local), i.e. dword j holds
+//   tA [H][P]     window row r at byte r * P + x (x window-local), i.e. dword j holds
 //                 window bytes 4j .. 4j+3; a unit (ry, gg) = detection pixels
 //                 x = 3 + 4gg .. 6 + 4gg of row 3 + ry (bytes 3 .. 6 of dwords gg ..), and
-//                 the circle of its pixel pair 0-1 is dwords gg, gg+1 of rows ry .. ry+6
-//                 (14 dwords per scored pair side; the compass pretest reads 7 per unit)
-//   tB            tA shifted by 2 bytes (tB byte k = tA byte k + 2): pixels 2-3 of a unit
-//                 sit where pixels 0-1 sit in tA; row r of tB is at byte r * 2P + P, between
-//                 rows r and r + 1 of tA, so the tile rows are 2P apart (for P = 48, 24 banks:
-//                 the pretest's 8 rows x 8 units of a wave read 64 distinct banks)
+//                 the circle of either pixel pair is within dwords gg .. gg+2 of rows
+//                 ry .. ry+6 (21 dwords per scored pair side; the compass pretest reads 9
+//                 per unit); the host picks P for the pretest's bank spread
 //   sc [RH+2][SP] u8 scores at sc[ry + 1][4 + 4gg + i], zero border (SP = P - 8 >= 4 RG + 8)
 //   list u16      pretest survivors: ry << 8 | gg << 2 | half << 1 | dark
 #ifndef FC2_CPW
@@ -63,11 +60,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(FC2_WPE, 8)
 {
     constexpr int P = 4 * P4;
     constexpr int SP4 = P4 - 2, SP = 4 * SP4;  // score rows: RG + 2 dwords <= P4 - 2 (host plan)
-    constexpr int RS = 2 * P, RS4 = 2 * P4;  // tile row stride (bytes, dwords)
+    constexpr int RS = P, RS4 = P4;  // tile row stride (bytes, dwords)
     extern __shared__ __attribute__((aligned(16))) uint32_t fc2_lds[];
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
     uint8_t *tA = (uint8_t *)fc2_lds + wv * g->fc2_wave_bytes;
-    uint8_t *tB = tA + P;
     uint8_t *sc = tA + g->fc2_sc_off;
     uint16_t *list = (uint16_t *)(tA + g->fc2_list_off);
     const int total = c_count * nframes;
@@ -105,7 +101,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(FC2_WPE, 8)
         k.yo = y0 - ORBG_MIN_BORDER + 3;
         k.xs = g->lv[l].xs_off + k.xo;
         k.ys = g->lv[l].ys_off + k.yo;
-        k.NC = (k.RG + 3 + 3) >> 2;  // tile dwords 0 .. RG+2 (tB needs tA dword RG+2)
+        k.NC = (k.RG + 2 + 3) >> 2;  // tile dwords 0 .. RG+1
         k.nch = k.H * k.NC;
         return k;
     };
@@ -120,22 +116,19 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(FC2_WPE, 8)
         sh = (uint32_t)((uintptr_t)src & 3u);
         return (const uint32_t *)(src - sh);
     };
-    auto put = [&](const Fc2Cell &k, int i, uint4 q, uint2 q2, uint32_t sh) {
+    auto put = [&](const Fc2Cell &k, int i, uint4 q, uint32_t q4, uint32_t sh) {
         const int mdiv = (65536 + k.NC - 1) / k.NC;
         const int r = (i * mdiv) >> 16, cc = i - r * k.NC;
         const int to = r * RS + 16 * cc;
-        const uint32_t d[6] = {q.x, q.y, q.z, q.w, q2.x, q2.y};
-        uint32_t A[5], Bw[4];
+        const uint32_t d[5] = {q.x, q.y, q.z, q.w, q4};
+        uint32_t A[4];
 #pragma unroll
-        for (int j = 0; j < 5; j++) A[j] = __builtin_amdgcn_alignbyte(d[j + 1], d[j], sh);
-#pragma unroll
-        for (int j = 0; j < 4; j++) Bw[j] = __builtin_amdgcn_alignbyte(A[j + 1], A[j], 2);
-        *(uint4 *)(tA + to) = make_uint4(A[0], A[1], A[2], A[3]);  // RS: multiple of 16
+        for (int j = 0; j < 4; j++) A[j] = __builtin_amdgcn_alignbyte(d[j + 1], d[j], sh);
         if constexpr (P % 16 == 0) {
-            *(uint4 *)(tB + to) = make_uint4(Bw[0], Bw[1], Bw[2], Bw[3]);
-        } else {
-            *(uint2 *)(tB + to) = make_uint2(Bw[0], Bw[1]);
-            *(uint2 *)(tB + to + 8) = make_uint2(Bw[2], Bw[3]);
+            *(uint4 *)(tA + to) = make_uint4(A[0], A[1], A[2], A[3]);
+        } else {  // rows 8-byte aligned
+            *(uint2 *)(tA + to) = make_uint2(A[0], A[1]);
+            *(uint2 *)(tA + to + 8) = make_uint2(A[2], A[3]);
         }
     };
 
@@ -152,15 +145,15 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(FC2_WPE, 8)
     const int f = cur.f, c = cur.c, RW = cur.RW, RH = cur.RH, RG = cur.RG, nunits = cur.nunits;
     const int xo = cur.xo, yo = cur.yo;
     // quadtree path codes of the cell's columns / rows (one per lane), issued early
-    const uint32_t xs_l = lane < RW ? ctab[cur.xs + lane] : 0u;
-    const uint32_t ys_l = lane < RH ? ctab[cur.ys + lane] : 0u;
-    // ---- window -> tA / tB: all of a lane's chunk loads in flight before the first store
+    uint32_t xs_l = lane < RW ? ctab[cur.xs + lane] : 0u;
+    uint32_t ys_l = lane < RH ? ctab[cur.ys + lane] : 0u;
+    // ---- window -> tA: all of a lane's chunk loads in flight before the first store
     // (the previous cell's reads of the tiles are done: a wave's LDS ops complete in order) ----
     wave_sync_lds();
     {
         for (int i0 = 0; i0 < cur.nch; i0 += 2 * 64) {
             uint4 q[2];
-            uint2 q2[2];
+            uint32_t q4[2];
             uint32_t sh[2];
 #pragma unroll
             for (int u = 0; u < 2; u++) {
@@ -169,10 +162,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(FC2_WPE, 8)
                 const int i = min(i0 + 64 * u + lane, cur.nch - 1);
                 const uint32_t *aw = chunk_src(cur, i, sh[u]);
                 q[u] = *(const uint4 *)aw;  // unconditional: both in flight
-                q2[u] = *(const uint2 *)(aw + 4);
+                q4[u] = aw[4];
             }
 #pragma unroll
-            for (int u = 0; u < 2; u++) put(cur, min(i0 + 64 * u + lane, cur.nch - 1), q[u], q2[u], sh[u]);
+            for (int u = 0; u < 2; u++) put(cur, min(i0 + 64 * u + lane, cur.nch - 1), q[u], q4[u], sh[u]);
         }
         uint2 *z = (uint2 *)sc;
         const int nz = (RH + 2) * (SP / 8);
@@ -287,7 +280,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(FC2_WPE, 8)
         const int e = list[top ? lcap - 1 - (t >> 1) : j] | (top ? (t & 1) : 0);
         const int ry = e >> 8, gg = (e >> 2) & 63, half = (e >> 1) & 1;
         const uint32_t flip = (e & 1) ? 0xFFFFFFFFu : 0u;  // dark: complemented bytes
-        const uint32_t *p = (const uint32_t *)(tA + half * P + ry * RS + 4 * gg);
+        const uint32_t *p = (const uint32_t *)(tA + ry * RS + 4 * gg);
         Rows7 R;
 #pragma unroll
         for (int r = 0; r < 7; r++) {
@@ -295,7 +288,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(FC2_WPE, 8)
             R.w[r][1] = p[r * RS4 + 1] ^ flip;
             R.w[r][2] = p[r * RS4 + 2] ^ flip;
         }
-        const v2s s = fast_score_side<0, 3>(R);
+        const v2s s = fast_score_side_rt(R, half ? 0x00020002u : 0u);
         const uint32_t s0 = (uint16_t)s.x >= (uint32_t)thi ? (uint16_t)s.x : 0u;
         uint32_t s1 = (uint16_t)s.y >= (uint32_t)thi ? (uint16_t)s.y : 0u;
         if (RW - 4 * gg < 2 * half + 2) s1 = 0;  // pixel i + 1 past the region
@@ -404,18 +397,30 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(FC2_WPE, 8)
         // on both sides (the window tiles are intact), then NMS at minThFAST
         wave_sync_lds();
         for (int u = lane, ry = ry0, gg = gg0; u < nunits; u += 64) {
-            Rows7 R;
+            // the four (pixel pair, side) scores of the unit one at a time, each from the
+            // tile re-read (the dark side = the bright side of the complemented bytes): max
+            // over sides of max(M_side - 1, 0) = cornerScore's max(M - 1, 0).  A rare path:
+            // re-reading keeps its register use below the main loops'.
             const uint32_t *p = (const uint32_t *)(tA + ry * RS + 4 * gg);
+            v2s sp0 = (v2s){0, 0}, sp1 = (v2s){0, 0};
+#pragma unroll 1
+            for (int t = 0; t < 4; t++) {
+                const uint32_t flip = (t & 1) ? 0xFFFFFFFFu : 0u;
+                Rows7 R;
 #pragma unroll
-            for (int r = 0; r < 7; r++) {
-                R.w[r][0] = p[r * RS4];
-                R.w[r][1] = p[r * RS4 + 1];
-                R.w[r][2] = p[r * RS4 + 2];
+                for (int r = 0; r < 7; r++) {
+                    R.w[r][0] = p[r * RS4] ^ flip;
+                    R.w[r][1] = p[r * RS4 + 1] ^ flip;
+                    R.w[r][2] = p[r * RS4 + 2] ^ flip;
+                }
+                const v2s sc2 = fast_score_side_rt(R, (t & 2) ? 0x00020002u : 0u);
+                if (t & 2)
+                    sp1 = pmax(sp1, sc2);
+                else
+                    sp0 = pmax(sp0, sc2);
             }
-            const v2s sa = fast_score_pair<0, 3>(R);
-            const v2s sb = fast_score_pair<2, 3>(R);
-            uint32_t word = (uint32_t)(uint16_t)sa.x | ((uint32_t)(uint16_t)sa.y << 8) |
-                            ((uint32_t)(uint16_t)sb.x << 16) | ((uint32_t)(uint16_t)sb.y << 24);
+            uint32_t word = (uint32_t)(uint16_t)sp0.x | ((uint32_t)(uint16_t)sp0.y << 8) |
+                            ((uint32_t)(uint16_t)sp1.x << 16) | ((uint32_t)(uint16_t)sp1.y << 24);
             const int valid = min(RW - 4 * gg, 4);
             if (valid < 4) word &= (1u << (8 * valid)) - 1u;
             *(uint32_t *)(sc + (ry + 1) * SP + 4 * gg + 4) = word;
@@ -426,6 +431,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(FC2_WPE, 8)
                 ry++;
             }
         }
+        // the path codes again (re-read, not kept live through the scoring above)
+        xs_l = lane < RW ? ctab[cur.xs + lane] : 0u;
+        ys_l = lane < RH ? ctab[cur.ys + lane] : 0u;
         wave_sync_lds();
         for (int u0 = 0, ry = ry0, gg = gg0; u0 < nunits; u0 += 64) {
             const uint32_t kb = u0 + lane < nunits ? keep_bits(ry, gg, tlo, true) : 0u;

@@ -886,9 +886,9 @@ static int plan(orbg_ctx *c, int w, int h, int batch)
             max_units = std::max(max_units, std::max((int)cl.h - 6, 0) *
                                                 ((std::max((int)cl.w - 6, 0) + 3) / 4));
         // k_fast2 (fast_kernels.hip): compile-time pitch P4 >= 4 * ceil((RG + 3) / 4) (its
-        // 16-byte window chunks) among the instantiated ones; layout tA / tB (hmax rows each,
-        // interleaved: row stride 2 * P) | scores (hmax - 4 rows of P - 8 bytes) | list (2 entries per unit).  Preferred: the most
-        // workgroups per CU by LDS, then the bank-spread cost.
+        // 16-byte window chunks) among the instantiated ones; layout tA (hmax rows of P) |
+        // scores (hmax - 4 rows of P - 8 bytes) | list (2 entries per unit).  Preferred: the
+        // most workgroups per CU by LDS, then the bank-spread cost.
         G.fc2_p4 = 0;
         {
             // tile rows: 4 * ceil-ish((rg + 6) / 4) dwords; score rows (P4 - 2 dwords) hold rg + 2
@@ -897,19 +897,20 @@ static int plan(orbg_ctx *c, int w, int h, int batch)
             for (int wd = need; wd <= 32; wd++) {
                 if (!fast2_pitch_ok(wd)) continue;
                 const int P2 = 4 * wd;
-                const int wb = (2 * hmax * P2 + (std::max(hmax - 6, 0) + 2) * (P2 - 8) +
+                const int wb = (hmax * P2 + (std::max(hmax - 6, 0) + 2) * (P2 - 8) +
                                 4 * max_units + 2 + 15) & ~15;
                 const int wgs = std::min(8, 163840 / (4 * wb));
                 int cost = 0;
                 for (int r : rgs)
-                    for (int k = 0; k < 3; k++) {
-                        int hist[64] = {0}, mx = 0;
-                        for (int lane = 0; lane < 64; lane++) {
-                            const int b = ((lane / r) * 2 * wd + lane % r + k) & 63;
-                            mx = std::max(mx, ++hist[b]);
+                    for (int k = 0; k < 3; k++)
+                        for (int h = 0; h < 64; h += 32) {  // ds_read_b32: lane groups of 32, 32 banks
+                            int hist[32] = {0}, mx = 0;
+                            for (int lane = h; lane < h + 32; lane++) {
+                                const int b = ((lane / r) * wd + lane % r + k) & 31;
+                                mx = std::max(mx, ++hist[b]);
+                            }
+                            cost += mx;
                         }
-                        cost += mx;
-                    }
                 if (wgs > best_wg || (wgs == best_wg && cost < best_c)) {
                     best_wg = wgs;
                     best_c = cost;
@@ -918,8 +919,7 @@ static int plan(orbg_ctx *c, int w, int h, int batch)
             }
             if (G.fc2_p4) {
                 const int P2 = 4 * G.fc2_p4;
-                G.fc2_tileb_off = P2;  // tB rows interleaved with tA's (row stride 2 * P2)
-                G.fc2_sc_off = 2 * hmax * P2;
+                G.fc2_sc_off = hmax * P2;
                 G.fc2_list_off = G.fc2_sc_off + (std::max(hmax - 6, 0) + 2) * (P2 - 8);  // score rows: P2 - 8 bytes
                 G.fc2_list_cap = 2 * max_units;
                 G.fc2_wave_bytes = (G.fc2_list_off + 2 * G.fc2_list_cap + 2 + 15) & ~15;  // + k_fast2's spare entry

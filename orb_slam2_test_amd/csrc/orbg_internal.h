@@ -75,7 +75,7 @@ struct OrbgGeom {
     int32_t dbg;                  // developer timing knob (ORBG_DBG env), 0 in production
     int32_t fc2_p4;               // k_fast2 LDS row pitch (dwords, a template instance)
     int32_t fc2_wave_bytes;       // k_fast2 LDS bytes per wave
-    int32_t fc2_tileb_off, fc2_sc_off, fc2_list_off;  // k_fast2 regions within a wave's LDS
+    int32_t fc2_sc_off, fc2_list_off;  // k_fast2 regions within a wave's LDS
     int32_t fc2_list_cap;         // k_fast2 pretest list entries per wave
     int32_t gk[7];
     int64_t pyr_frame;            // bytes per frame of d_pyr
