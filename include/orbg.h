@@ -450,6 +450,19 @@ int orbg_ba_linearize_device(orbg_ctx *ctx, const orbg_pose *d_poses, int npose,
                              orbg_edge_out *d_eout, double *d_hpose, double *d_bpose,
                              double *d_hpoint, double *d_bpoint);
 
+/* buildSystem alone, for an LM iteration kept in HBM: as orbg_ba_linearize_device, but
+ * H_pl goes to d_hpl[18e .. 18e+17] (edge e's 3x6 block, row-major, the _Hpl block
+ * constructQuadraticForm adds, base_binary_edge.hpp:105-117) instead of the 400-byte
+ * orbg_edge_out records, and no per-edge Jacobian or error term is stored (the LM's error
+ * pass, orbg_ba_errors_device, provides them): per edge 144 bytes out instead of a strided
+ * record.  Same blocks and the same H_pl bits as orbg_ba_linearize_device. */
+int orbg_ba_build_system_device(orbg_ctx *ctx, const orbg_pose *d_poses, int npose,
+                                const double *d_points, int npoint, const orbg_edge *d_edges,
+                                int nedge, const int32_t *d_pose_off, const int32_t *d_pose_edges,
+                                const int32_t *d_point_off, const int32_t *d_point_edges,
+                                double *d_hpl, double *d_hpose, double *d_bpose,
+                                double *d_hpoint, double *d_bpoint);
+
 /* g2o's per-trial error pass for the two LBA edge types: SparseOptimizer::
  * computeActiveErrors (Thirdparty/g2o/g2o/core/sparse_optimizer.cpp:61-76, computeError
  * types_six_dof_expmap.h:90-95, 122-127) and the terms activeRobustChi2 sums (:100-114,

@@ -189,6 +189,8 @@ def lib():
         "orbg_ba_errors_device": (i32, [vp, vp, vp, vp, i32, vp, vp, vp, vp]),
         "orbg_ba_linearize_device": (i32, [vp, vp, i32, vp, i32, vp, i32, vp, vp, vp, vp, vp, vp,
                                            vp, vp, vp]),
+        "orbg_ba_build_system_device": (i32, [vp, vp, i32, vp, i32, vp, i32, vp, vp, vp, vp, vp,
+                                              vp, vp, vp, vp]),
     }
     for name, (res, args) in sig.items():
         fn = getattr(L, name)

@@ -514,14 +514,22 @@ static BaEdgeOut eout_fields(orbg_edge_out *eout, bool jacobians, bool errors)
     return o;
 }
 
-// device-resident linearisation: every pointer is device memory; scratch = ba_rows_bytes
+// device-resident linearisation: every pointer is device memory; scratch = ba_rows_bytes.
+// hpl != NULL: H_pl goes there as [nedge][3][6] (orbg_ba_build_system_device) and eout is
+// not used.
 int launch_ba_device(hipStream_t st, const orbg_pose *poses, int npose, const double *points,
                      int npoint, const orbg_edge *edges, int nedge, const int32_t *pose_off,
                      const int32_t *pose_edges, const int32_t *point_off,
                      const int32_t *point_edges, orbg_edge_out *eout, double *hpose,
                      double *bpose, double *hpoint, double *bpoint, double *scr, void *prof,
-                     bool jacobians, bool errors)
+                     bool jacobians, bool errors, double *hpl)
 {
+    BaEdgeOut o = eout_fields(eout, jacobians, errors);
+    if (hpl) {
+        o = BaEdgeOut{};
+        o.hpl = hpl;
+        o.stride = 18;
+    }
     if (npoint) {
         // points without edges keep zero blocks; points spanning workgroups are summed onto
         // zero by atomics
@@ -534,7 +542,7 @@ int launch_ba_device(hipStream_t st, const orbg_pose *poses, int npose, const do
         prof_begin(prof, st, "ba_edges", &a);
         hipLaunchKernelGGL(k_ba_edges, dim3((nedge + BA_EDGES_TPB - 1) / BA_EDGES_TPB),
                            dim3(BA_EDGES_TPB), 0, st, poses, points, edges, nedge, point_off,
-                           point_edges, eout_fields(eout, jacobians, errors), hpoint, bpoint);
+                           point_edges, o, hpoint, bpoint);
         prof_end(prof, st, "ba_edges", a);
     }
     if (npose) {
@@ -609,7 +617,7 @@ int launch_ba(hipStream_t st, const orbg_pose *poses, int npose, const double *p
     if (nedge) CK(hipMemcpyAsync(d_qe, point_edges, nedge * 4, hipMemcpyHostToDevice, st));
     const int rc = launch_ba_device(st, d_pose, npose, d_pts, npoint, d_edges, nedge, d_off, d_pe,
                                     d_qoff, d_qe, d_eout, d_hpose, d_bpose, d_hpt, d_bpt, d_rows,
-                                    prof, true, true);
+                                    prof, true, true, nullptr);
     if (rc) return rc;
     if (eout && nedge)
         CK(hipMemcpyAsync(eout, d_eout, nedge * sizeof(orbg_edge_out), hipMemcpyDeviceToHost, st));

@@ -50,14 +50,10 @@ struct Rows7 {
     uint32_t w[7][3];
 };
 
-// Score of two pixels from the 16 circle pixels x[k] alone (no per-pixel differences):
-// with d = v - x,  max_arc min d = v - min_k A_k  and  min_arc max d = v - max_k a_k,
-// A_k / a_k = max / min of x over the 9-arc starting at k, so
-//   M = max(v - min_k A_k, max_k a_k - v),   score = max(M - 1, 0).
 // Arc extrema use gfx950's 3-input packed v_pk_maximum3_f16 / v_pk_minimum3_f16: the u16
 // lanes (values 0..255) are read as f16 bit patterns, i.e. +0 and positive denormals,
 // whose IEEE order is the integer order (f16 denormals are preserved; nothing is
-// computed in f16, only ordered).  3-arcs t_k = ext(x[k..k+2]), 9-arcs ext(t_k, t_k+3, t_k+6).
+// computed in f16, only ordered).
 typedef _Float16 h2 __attribute__((ext_vector_type(2)));
 __device__ __forceinline__ h2 hmax3(h2 a, h2 b, h2 c)
 {
@@ -69,52 +65,6 @@ __device__ __forceinline__ h2 hmin3(h2 a, h2 b, h2 c)
 }
 __device__ __forceinline__ h2 as_h2(v2s v) { return __builtin_bit_cast(h2, v); }
 __device__ __forceinline__ v2s as_v2s(h2 v) { return __builtin_bit_cast(v2s, v); }
-
-// circle (dx, dy) of makeOffsets(16); row index = 3 + dy, byte offset = 4 + dx (+ pixel i)
-// C: byte offset of pixel 0 in the 12-byte row window (4: k_fast_cells' tiles, 3: k_fast2's)
-template <int I, int C = 4>
-__device__ __forceinline__ v2s fast_score_pair(const Rows7 &R)
-{
-#define GB(row, dx) as_h2(gather2<C + (dx) + I>(R.w[row][0], R.w[row][1], R.w[row][2]))
-    const v2s v = gather2<C + I>(R.w[3][0], R.w[3][1], R.w[3][2]);
-    h2 x[16];
-    x[0] = GB(6, 0);
-    x[1] = GB(6, 1);
-    x[2] = GB(5, 2);
-    x[3] = GB(4, 3);
-    x[4] = GB(3, 3);
-    x[5] = GB(2, 3);
-    x[6] = GB(1, 2);
-    x[7] = GB(0, 1);
-    x[8] = GB(0, 0);
-    x[9] = GB(0, -1);
-    x[10] = GB(1, -2);
-    x[11] = GB(2, -3);
-    x[12] = GB(3, -3);
-    x[13] = GB(4, -3);
-    x[14] = GB(5, -2);
-    x[15] = GB(6, -1);
-#undef GB
-    // one side at a time keeps x[16] + 16 temporaries live, not 48
-    h2 t[16], A[16];
-#pragma unroll
-    for (int k = 0; k < 16; k++) t[k] = hmax3(x[k], x[(k + 1) & 15], x[(k + 2) & 15]);
-#pragma unroll
-    for (int k = 0; k < 16; k++) A[k] = hmax3(t[k], t[(k + 3) & 15], t[(k + 6) & 15]);
-    const h2 Amin = __builtin_elementwise_minimum(
-        hmin3(hmin3(A[0], A[1], A[2]), hmin3(A[3], A[4], A[5]), hmin3(A[6], A[7], A[8])),
-        hmin3(hmin3(A[9], A[10], A[11]), hmin3(A[12], A[13], A[14]), A[15]));
-#pragma unroll
-    for (int k = 0; k < 16; k++) t[k] = hmin3(x[k], x[(k + 1) & 15], x[(k + 2) & 15]);
-#pragma unroll
-    for (int k = 0; k < 16; k++) A[k] = hmin3(t[k], t[(k + 3) & 15], t[(k + 6) & 15]);
-    const h2 amax = __builtin_elementwise_maximum(
-        hmax3(hmax3(A[0], A[1], A[2]), hmax3(A[3], A[4], A[5]), hmax3(A[6], A[7], A[8])),
-        hmax3(hmax3(A[9], A[10], A[11]), hmax3(A[12], A[13], A[14]), A[15]));
-    const v2s zero = (v2s){0, 0}, one = (v2s){1, 1};
-    const v2s M = pmax(v - as_v2s(Amin), as_v2s(amax) - v);
-    return pmax(M - one, zero);  // u8 score, 0 = none
-}
 
 // bytes OFF + s and OFF + s + 1 of the 12-byte window {w0, w1, w2}, s = 0 or 2 per lane,
 // as two zero-extended u16 lanes: one v_perm_b32 whose selector is sel[OFF] = the s = 0
@@ -142,49 +92,10 @@ __device__ __forceinline__ v2s gather2_rt(uint32_t w0, uint32_t w1, uint32_t w2,
 // l_j = min(x[j .. j+7]) built from pairs and quads (8 + 8 ops) -- 36 packed ops per side
 // instead of 40.  A pixel is never a corner on both sides at one threshold (9 + 9 > 16
 // circle pixels), so the side below threshold contributes nothing: its true score is < th.
-template <int I, int C = 4>
-__device__ __forceinline__ v2s fast_score_side(const Rows7 &R)
-{
-#define GB(row, dx) as_h2(gather2<C + (dx) + I>(R.w[row][0], R.w[row][1], R.w[row][2]))
-    const v2s v = gather2<C + I>(R.w[3][0], R.w[3][1], R.w[3][2]);
-    h2 x[16];
-    x[0] = GB(6, 0);
-    x[1] = GB(6, 1);
-    x[2] = GB(5, 2);
-    x[3] = GB(4, 3);
-    x[4] = GB(3, 3);
-    x[5] = GB(2, 3);
-    x[6] = GB(1, 2);
-    x[7] = GB(0, 1);
-    x[8] = GB(0, 0);
-    x[9] = GB(0, -1);
-    x[10] = GB(1, -2);
-    x[11] = GB(2, -3);
-    x[12] = GB(3, -3);
-    x[13] = GB(4, -3);
-    x[14] = GB(5, -2);
-    x[15] = GB(6, -1);
-#undef GB
-    h2 p[8], q[8], m[8];
-#pragma unroll
-    for (int j = 0; j < 8; j++)  // odd start 2j+1: min(x[2j+1], x[2j+2])
-        p[j] = __builtin_elementwise_minimum(x[2 * j + 1], x[(2 * j + 2) & 15]);
-#pragma unroll
-    for (int j = 0; j < 8; j++)  // x[2j+1 .. 2j+4]
-        q[j] = __builtin_elementwise_minimum(p[j], p[(j + 1) & 7]);
-#pragma unroll
-    for (int j = 0; j < 8; j++)  // even k = 2j: min(l_{k+1}, max(x_k, x_{k+9}))
-        m[j] = hmin3(q[j], q[(j + 2) & 7],
-                     __builtin_elementwise_maximum(x[2 * j], x[(2 * j + 9) & 15]));
-    const h2 amax = __builtin_elementwise_maximum(
-        hmax3(hmax3(m[0], m[1], m[2]), hmax3(m[3], m[4], m[5]), m[6]), m[7]);
-    const v2s zero = (v2s){0, 0}, one = (v2s){1, 1};
-    return pmax(as_v2s(amax) - v - one, zero);
-}
-
-// fast_score_side of pixel pair s / 2 (s = 0: pixels 0-1, s = 2: pixels 2-3) of the unit whose
-// rows R hold window bytes 0 .. 11 (pixel 0 at byte 3), s per lane: the seven selectors
-// gather2_rt_sel<0..6>() + (s, s) are built once per task.
+// Pixel pair s / 2 (s = 0: pixels 0-1, s = 2: pixels 2-3) of the unit whose rows R hold
+// window bytes 0 .. 11 (pixel 0 at byte 3), s per lane: the seven selectors
+// gather2_rt_sel<0..6>() + (s, s) are built once per task.  circle (dx, dy) of
+// makeOffsets(16): row index = 3 + dy, byte offset = 3 + dx (+ pixel i).
 __device__ __forceinline__ v2s fast_score_side_rt(const Rows7 &R, uint32_t sadd)
 {
     uint32_t sel[7];

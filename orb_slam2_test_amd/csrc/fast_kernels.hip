@@ -29,14 +29,20 @@
 namespace orbg {
 
 // LDS per wave (fc2_* offsets in OrbgGeom, host plan):
-//   tA [H][P]     window row r at byte r * P + x (x window-local), i.e. dword j holds
+//   tA [H][2P]    window row r at byte r * 2P + x (x window-local), i.e. dword j holds
 //                 window bytes 4j .. 4j+3; a unit (ry, gg) = detection pixels
 //                 x = 3 + 4gg .. 6 + 4gg of row 3 + ry (bytes 3 .. 6 of dwords gg ..), and
 //                 the circle of either pixel pair is within dwords gg .. gg+2 of rows
 //                 ry .. ry+6 (21 dwords per scored pair side; the compass pretest reads 9
-//                 per unit); the host picks P for the pretest's bank spread
-//   sc [RH+2][SP] u8 scores at sc[ry + 1][4 + 4gg + i], zero border (SP = P - 8 >= 4 RG + 8)
+//                 per unit); the row stride 2P (24 dwords for P = 48) puts the 8 x 8 units
+//                 of a pretest wave (and of the NMS scan) on 64 distinct banks
+//   sc [RH+2][2P] u8 scores at sc[ry + 1][4 + 4gg + i], zero border, rows interleaved with
+//                 the window rows (sc row r = bytes P .. 2P - 9 of tile row stride r; 4 RG + 8
+//                 <= P - 8 bytes used)
 //   list u16      pretest survivors: ry << 8 | gg << 2 | half << 1 | dark
+#ifndef ORBG_FC2_IL
+#define ORBG_FC2_IL 0  // 1: score rows interleaved with the tile rows (row stride 2P); A/B
+#endif
 #ifndef FC2_CPW
 #define FC2_CPW 2  // consecutive cells per wave (shared halo lines in L1, fewer workgroups)
 #endif
@@ -59,8 +65,14 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(FC2_WPE, 8)
     int c_count)
 {
     constexpr int P = 4 * P4;
-    constexpr int SP4 = P4 - 2, SP = 4 * SP4;  // score rows: RG + 2 dwords <= P4 - 2 (host plan)
-    constexpr int RS = P, RS4 = P4;  // tile row stride (bytes, dwords)
+#if ORBG_FC2_IL
+    constexpr int RS = 2 * P, RS4 = 2 * P4;  // tile row stride (bytes, dwords)
+    constexpr int SP4 = RS4, SP = RS;         // score row stride: the tile's (interleaved)
+#else
+    constexpr int RS = P, RS4 = P4;           // tile row stride (bytes, dwords)
+    constexpr int SP4 = P4 - 2, SP = 4 * SP4;  // score rows apart: RG + 2 dwords <= P4 - 2
+#endif
+    constexpr int ZR = (P - 8) / 8;           // score row bytes in use (RG + 2 dwords <= P4 - 2), as uint2
     extern __shared__ __attribute__((aligned(16))) uint32_t fc2_lds[];
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
     uint8_t *tA = (uint8_t *)fc2_lds + wv * g->fc2_wave_bytes;
@@ -167,9 +179,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(FC2_WPE, 8)
 #pragma unroll
             for (int u = 0; u < 2; u++) put(cur, min(i0 + 64 * u + lane, cur.nch - 1), q[u], q4[u], sh[u]);
         }
-        uint2 *z = (uint2 *)sc;
-        const int nz = (RH + 2) * (SP / 8);
-        for (int i = lane; i < nz; i += 64) z[i] = make_uint2(0, 0);
+        const int nz = (RH + 2) * ZR;
+        for (int i = lane; i < nz; i += 64) {
+            const int r = i / ZR;
+            *(uint2 *)(sc + r * SP + 8 * (i - r * ZR)) = make_uint2(0, 0);
+        }
     }
     wave_sync_lds();
     if (dbg == 11) continue;
@@ -192,9 +206,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(FC2_WPE, 8)
         for (int u0 = 0, ry = ry0, gg = gg0; u0 < nunits; u0 += 64) {
             const int u = u0 + lane;
             // per pair: bright / dark survivors as the sign bits (15, 31) of a packed word,
-            // 0 = none; pixels outside the region are forced to fail
-            // every lane runs the test (lanes past the last unit read unit 0's words and
-            // are forced to fail): no exec-mask branch per 64 units
+            // 0 = none.  Every lane runs the test (lanes past the last unit read unit 0's
+            // words; their entries are dropped below): no exec-mask branch per 64 units.
+            // Pixels of the last unit column past the region are tested like the others (the
+            // window tile holds bytes there): the scoring loop zeroes their scores
             uint32_t ab = 0, ad = 0, bb = 0, bd = 0;
             const bool in = u < nunits;
             {
@@ -206,10 +221,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(FC2_WPE, 8)
                     r3[k] = p[3 * RS4 + k];
                     r6[k] = p[6 * RS4 + k];
                 }
-                const int valid = in ? RW - 4 * gg : 0;  // pixels of the unit inside the region
-                const uint32_t invA = valid > 1 ? 0u : (valid > 0 ? 0x80000000u : 0x80008000u);
-                const uint32_t invB = valid > 3 ? 0u : (valid > 2 ? 0x80000000u : 0x80008000u);
-                auto pretest = [&](auto I, uint32_t inv, uint32_t &pb_, uint32_t &pd_) {
+                auto pretest = [&](auto I, uint32_t &pb_, uint32_t &pd_) {
                     constexpr int i = decltype(I)::value;
                     const v2s v = gather2<3 + i>(r3[0], r3[1], r3[2]);
                     const v2s c0 = gather2<3 + i>(r6[0], r6[1], r6[2]);
@@ -221,11 +233,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(FC2_WPE, 8)
                     // lane >= 0 <=> pass: mb - (v + th + 1) and (v - th - 1) - md
                     const uint32_t wb = __builtin_bit_cast(uint32_t, (v2s)(mb - (v + vth1)));
                     const uint32_t wd = __builtin_bit_cast(uint32_t, (v2s)((v - vth1) - md));
-                    pb_ = ~(wb | inv) & 0x80008000u;
-                    pd_ = ~(wd | inv) & 0x80008000u;
+                    pb_ = ~wb & 0x80008000u;
+                    pd_ = ~wd & 0x80008000u;
                 };
-                pretest(std::integral_constant<int, 0>{}, invA, ab, ad);
-                pretest(std::integral_constant<int, 2>{}, invB, bb, bd);
+                pretest(std::integral_constant<int, 0>{}, ab, ad);
+                pretest(std::integral_constant<int, 2>{}, bb, bd);
             }
             const uint16_t e = (uint16_t)(ry << 8 | gg << 2);
             // one entry per pair with a survivor, from the bottom of the list (side: bright
@@ -238,13 +250,13 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(FC2_WPE, 8)
                 if (flag) list[top ? lcap - 1 - (nboth + below) : nlist + below] = (uint16_t)(e | tag);
                 (top ? nboth : nlist) += __popcll(m);
             };
-            const bool bothA = ab && ad, bothB = bb && bd;
+            const bool bothA = in && ab && ad, bothB = in && bb && bd;
             // the common entries of pixels 0-1 and 2-3 in one append: a lane's entries follow
             // those of every lower lane, its pair-0-1 entry before its pair-2-3 entry; a lane
             // without an entry writes the spare slot past the list (lcap), so both stores are
             // unconditional (no exec-mask branches)
             {
-                const bool fA = (ab | ad) && !bothA, fB = (bb | bd) && !bothB;
+                const bool fA = in && (ab | ad) && !bothA, fB = in && (bb | bd) && !bothB;
                 const unsigned long long mA = __ballot(fA), mB = __ballot(fB);
                 const int below =
                     __builtin_amdgcn_mbcnt_hi((uint32_t)(mA >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)mA, 0)) +
@@ -289,9 +301,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(FC2_WPE, 8)
             R.w[r][2] = p[r * RS4 + 2] ^ flip;
         }
         const v2s s = fast_score_side_rt(R, half ? 0x00020002u : 0u);
-        const uint32_t s0 = (uint16_t)s.x >= (uint32_t)thi ? (uint16_t)s.x : 0u;
         uint32_t s1 = (uint16_t)s.y >= (uint32_t)thi ? (uint16_t)s.y : 0u;
-        if (RW - 4 * gg < 2 * half + 2) s1 = 0;  // pixel i + 1 past the region
+        uint32_t s0 = (uint16_t)s.x >= (uint32_t)thi ? (uint16_t)s.x : 0u;
+        const int valid = RW - 4 * gg - 2 * half;  // pixels of the pair inside the region
+        if (valid < 2) s1 = 0;
+        if (valid < 1) s0 = 0;
         __hip_atomic_fetch_or((uint32_t *)(sc + (ry + 1) * SP + 4 * gg + 4),
                               (s0 | s1 << 8) << (16 * half), __ATOMIC_RELAXED,
                               __HIP_MEMORY_SCOPE_WAVEFRONT);
@@ -401,11 +415,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(FC2_WPE, 8)
             // tile re-read (the dark side = the bright side of the complemented bytes): max
             // over sides of max(M_side - 1, 0) = cornerScore's max(M - 1, 0).  A rare path:
             // re-reading keeps its register use below the main loops'.
-            const uint32_t *p = (const uint32_t *)(tA + ry * RS + 4 * gg);
             v2s sp0 = (v2s){0, 0}, sp1 = (v2s){0, 0};
 #pragma unroll 1
             for (int t = 0; t < 4; t++) {
                 const uint32_t flip = (t & 1) ? 0xFFFFFFFFu : 0u;
+                const uint32_t *p = (const uint32_t *)(tA + ry * RS + 4 * gg);
                 Rows7 R;
 #pragma unroll
                 for (int r = 0; r < 7; r++) {

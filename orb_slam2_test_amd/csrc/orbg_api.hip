@@ -88,7 +88,7 @@ int launch_ba_device(hipStream_t st, const orbg_pose *poses, int npose, const do
                      const int32_t *pose_edges, const int32_t *point_off,
                      const int32_t *point_edges, orbg_edge_out *eout, double *hpose,
                      double *bpose, double *hpoint, double *bpoint, double *scr, void *prof,
-                     bool jacobians, bool errors);
+                     bool jacobians, bool errors, double *hpl);
 size_t ba_rows_bytes(int nedge, int npose);
 // stereo_kernels.hip
 size_t stereo_scratch_bytes(int npairs, int frame_cap);
@@ -645,6 +645,10 @@ static bool make_pyr_tables(const OrbgGeom &G, const std::vector<int2> &rtab, in
 }
 
 // Build the geometry for an image size and allocate HBM for `batch` frames.
+#ifndef ORBG_FC2_IL
+#define ORBG_FC2_IL 0  // k_fast2 LDS layout variant (fast_kernels.hip); A/B builds only
+#endif
+
 static int plan(orbg_ctx *c, int w, int h, int batch)
 {
     if (c->gw == w && c->gh == h && c->gbatch >= batch) return ORBG_OK;
@@ -886,9 +890,9 @@ static int plan(orbg_ctx *c, int w, int h, int batch)
             max_units = std::max(max_units, std::max((int)cl.h - 6, 0) *
                                                 ((std::max((int)cl.w - 6, 0) + 3) / 4));
         // k_fast2 (fast_kernels.hip): compile-time pitch P4 >= 4 * ceil((RG + 3) / 4) (its
-        // 16-byte window chunks) among the instantiated ones; layout tA (hmax rows of P) |
-        // scores (hmax - 4 rows of P - 8 bytes) | list (2 entries per unit).  Preferred: the
-        // most workgroups per CU by LDS, then the bank-spread cost.
+        // 16-byte window chunks) among the instantiated ones; layout tA (hmax rows, stride
+        // 2P, the score rows in the second half of each stride) | list (2 entries per unit).
+        // Preferred: the most workgroups per CU by LDS, then the bank-spread cost.
         G.fc2_p4 = 0;
         {
             // tile rows: 4 * ceil-ish((rg + 6) / 4) dwords; score rows (P4 - 2 dwords) hold rg + 2
@@ -897,8 +901,12 @@ static int plan(orbg_ctx *c, int w, int h, int batch)
             for (int wd = need; wd <= 32; wd++) {
                 if (!fast2_pitch_ok(wd)) continue;
                 const int P2 = 4 * wd;
+#if ORBG_FC2_IL
+                const int wb = (2 * hmax * P2 + 4 * max_units + 2 + 15) & ~15;
+#else
                 const int wb = (hmax * P2 + (std::max(hmax - 6, 0) + 2) * (P2 - 8) +
                                 4 * max_units + 2 + 15) & ~15;
+#endif
                 const int wgs = std::min(8, 163840 / (4 * wb));
                 int cost = 0;
                 for (int r : rgs)
@@ -906,7 +914,7 @@ static int plan(orbg_ctx *c, int w, int h, int batch)
                         for (int h = 0; h < 64; h += 32) {  // ds_read_b32: lane groups of 32, 32 banks
                             int hist[32] = {0}, mx = 0;
                             for (int lane = h; lane < h + 32; lane++) {
-                                const int b = ((lane / r) * wd + lane % r + k) & 31;
+                                const int b = ((lane / r) * (ORBG_FC2_IL ? 2 : 1) * wd + lane % r + k) & 31;
                                 mx = std::max(mx, ++hist[b]);
                             }
                             cost += mx;
@@ -919,10 +927,18 @@ static int plan(orbg_ctx *c, int w, int h, int batch)
             }
             if (G.fc2_p4) {
                 const int P2 = 4 * G.fc2_p4;
+#if ORBG_FC2_IL
+                G.fc2_sc_off = P2;  // score rows interleaved with the tile rows
+                G.fc2_list_off = 2 * hmax * P2;
+#else
                 G.fc2_sc_off = hmax * P2;
                 G.fc2_list_off = G.fc2_sc_off + (std::max(hmax - 6, 0) + 2) * (P2 - 8);  // score rows: P2 - 8 bytes
+#endif
                 G.fc2_list_cap = 2 * max_units;
                 G.fc2_wave_bytes = (G.fc2_list_off + 2 * G.fc2_list_cap + 2 + 15) & ~15;  // + k_fast2's spare entry
+#ifdef ORBG_FC2_MIN_WAVE_BYTES  // developer A/B: LDS per wave padded (caps workgroups per CU)
+                G.fc2_wave_bytes = std::max(G.fc2_wave_bytes, ORBG_FC2_MIN_WAVE_BYTES);
+#endif
                 if (4 * G.fc2_wave_bytes > 160 * 1024) G.fc2_p4 = 0;
             }
         }
@@ -2473,7 +2489,33 @@ extern "C" int orbg_ba_linearize_device(orbg_ctx *c, const orbg_pose *d_poses, i
     rc = launch_ba_device(c->stream, d_poses, npose, d_points, npoint, d_edges, nedge, d_pose_off,
                           d_pose_edges, d_point_off, d_point_edges, d_eout, d_hpose, d_bpose,
                           d_hpoint, d_bpoint, (double *)s, &c->prof, c->ba_jacobians,
-                          c->ba_edge_errors);
+                          c->ba_edge_errors, nullptr);
+    if (rc) return set_err(ORBG_EIO, "BA kernel launch failed");
+    return ORBG_OK;
+}
+
+extern "C" int orbg_ba_build_system_device(orbg_ctx *c, const orbg_pose *d_poses, int npose,
+                                           const double *d_points, int npoint,
+                                           const orbg_edge *d_edges, int nedge,
+                                           const int32_t *d_pose_off, const int32_t *d_pose_edges,
+                                           const int32_t *d_point_off,
+                                           const int32_t *d_point_edges, double *d_hpl,
+                                           double *d_hpose, double *d_bpose, double *d_hpoint,
+                                           double *d_bpoint)
+{
+    if (!c) return set_err(ORBG_EINVAL, "ctx is NULL");
+    if (npose < 0 || npoint < 0 || nedge < 0) return set_err(ORBG_EINVAL, "negative size");
+    if ((nedge && (!d_edges || !d_hpl)) || (npose && (!d_poses || !d_pose_off || !d_pose_edges ||
+                                                      !d_hpose || !d_bpose)) ||
+        (npoint && (!d_points || !d_hpoint || !d_bpoint || !d_point_off || !d_point_edges)))
+        return set_err(ORBG_EINVAL, "NULL device array");
+    HIPCHK(hipSetDevice(c->device));
+    void *s;
+    int rc = scratch(c, ba_rows_bytes(nedge, npose), &s);
+    if (rc) return rc;
+    rc = launch_ba_device(c->stream, d_poses, npose, d_points, npoint, d_edges, nedge, d_pose_off,
+                          d_pose_edges, d_point_off, d_point_edges, nullptr, d_hpose, d_bpose,
+                          d_hpoint, d_bpoint, (double *)s, &c->prof, false, false, d_hpl);
     if (rc) return set_err(ORBG_EIO, "BA kernel launch failed");
     return ORBG_OK;
 }

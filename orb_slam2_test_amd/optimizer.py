@@ -154,6 +154,22 @@ class DeviceLBA:
             p(self.d_hpose),
             p(self.d_bpose), p(self.d_hpoint), p(self.d_bpoint)), "orbg_ba_linearize_device")
 
+    def build_system(self):
+        """buildSystem alone (orbg_ba_build_system_device): the vertex blocks and H_pl into the
+        compact self.d_hpl [nedge][3][6], no per-edge Jacobian / error record (the error pass
+        supplies those): the per-iteration pair of a device-resident LM is build_system() +
+        errors()."""
+        import torch
+        if getattr(self, "d_hpl", None) is None:
+            self.d_hpl = torch.zeros((max(self.ne, 1), 3, 6), dtype=torch.float64,
+                                     device=self.d_hpose.device)
+        p = lambda t: L.C.c_void_p(t.data_ptr())  # noqa: E731
+        L.check(L.lib().orbg_ba_build_system_device(
+            self.ctx.handle, p(self.d_poses), self.np, p(self.d_points), self.nq, p(self.d_edges),
+            self.ne, p(self.d_off), p(self.d_pe), p(self.d_qoff), p(self.d_qe), p(self.d_hpl),
+            p(self.d_hpose), p(self.d_bpose), p(self.d_hpoint), p(self.d_bpoint)),
+            "orbg_ba_build_system_device")
+
     def errors(self):
         """The per-trial error pass (orbg_ba_errors_device): chi2 and the robust term of every
         edge into self.d_chi2 / self.d_rho0."""

@@ -40,6 +40,10 @@ def main():
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--jacobians", action="store_true",
                     help="also store g2o's per-edge Jacobians eout.jp / jt (orbg_ba_set_jacobians)")
+    ap.add_argument("--records", action="store_true",
+                    help="buildSystem through orbg_ba_linearize_device (H_pl inside the 400-byte "
+                         "orbg_edge_out records) instead of orbg_ba_build_system_device (compact "
+                         "H_pl)")
     ap.add_argument("--edge-errors", action="store_true",
                     help="also store eout.err / chi2 / rho1 in the linearisation pass "
                          "(orbg_ba_set_edge_errors; the iteration's error pass provides them)")
@@ -56,7 +60,10 @@ def main():
     lba = DeviceLBA(poses, pts, edges, jacobians=args.jacobians, edge_errors=args.edge_errors)
 
     def iteration():
-        lba.linearize()
+        if args.records or args.jacobians or args.edge_errors:
+            lba.linearize()
+        else:
+            lba.build_system()
         lba.errors()
 
     for _ in range(args.warmup):
@@ -83,8 +90,10 @@ def main():
                    "points": len(pts), "stereo_frac": round(float(np.mean(edges["stereo"])), 3),
                    "edge_jacobians_stored": bool(args.jacobians),
                    "edge_errors_stored": bool(args.edge_errors),
-                   "iteration": "orbg_ba_linearize_device (buildSystem) + orbg_ba_errors_device "
-                                "(computeActiveErrors)"},
+                   "iteration": ("orbg_ba_linearize_device" if (args.records or args.jacobians
+                                                                 or args.edge_errors)
+                                 else "orbg_ba_build_system_device") +
+                                " (buildSystem) + orbg_ba_errors_device (computeActiveErrors)"},
         "ms_per_iter": round(dt / args.iters * 1e3, 4),
         "kernels": {k: {"ms_per_iter": round(v[0] / args.iters, 4),
                         "avg_launch_ms": round(v[0] / max(v[1], 1), 5)} for k, v in kern.items()},
@@ -95,7 +104,8 @@ def main():
         # the bytes the ABI makes unavoidable: the edge record and its CSR slot in, H_pl out
         # (g2o's _Hpl, read by the Schur step: not in SURVEY 8d's 108 B), the point in and its
         # H_ll | b_l out
-        abi = ne * (112 + 4 + 144) + len(pts) * (24 + 4 + 96)
+        from orb_slam2_test_amd import _lib as LB
+        abi = ne * (LB.EDGE_DTYPE.itemsize + 4 + 144) + len(pts) * (24 + 4 + 96)
         out["roofline"] = {"kernel": "ba_edges", "bound": "hbm", "achieved": round(ach, 1),
                            "peak": HBM_PEAK_GBS, "unit": "GB/s",
                            "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": None,
