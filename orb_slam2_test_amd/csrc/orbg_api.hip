@@ -48,9 +48,11 @@ hipError_t launch_fast2(int p4, size_t lds, hipStream_t st, const OrbgGeom *g,
                         int32_t *cell_cnt, uint2 *cell_kp, int nframes, int c_begin,
                         int c_count);
 struct OrbgKeypointDev;
-__global__ void k_orient_desc(const OrbgGeom *, const uint8_t *, int64_t, int, const uint8_t *,
-                              const uint8_t *, const uint4 *, const uint32_t *, const int32_t *,
-                              OrbgKeypointDev *, uint8_t *, int32_t *);
+hipError_t launch_orient_desc(bool bfma, dim3 grid, hipStream_t st, const OrbgGeom *g,
+                              const uint8_t *img0, int64_t img_fs, int img_pitch,
+                              const uint8_t *pyr, const uint8_t *blur, const uint4 *odtab,
+                              const uint32_t *lvl_kp, const int32_t *lvl_cnt,
+                              OrbgKeypointDev *kps, uint8_t *desc, int32_t *counts);
 // match_kernels.hip
 int launch_match_pairs(hipStream_t st, hipStream_t aux, hipEvent_t evf, hipEvent_t evj,
                        const uint8_t *desc, const orbg_keypoint *kps,
@@ -490,7 +492,7 @@ static void free_plan(orbg_ctx *c)
     c->gw = c->gh = c->gbatch = 0;
 }
 
-// k_orient_desc's IC_Angle byte tables, [sh 0..3][w 0..92][weights, ones]: lane w holds
+// k_orient_desc's IC_Angle byte tables, [sh 0..3][weights, ones][w 0..92]: lane w holds
 // bytes 16c .. 16c+15 (c = w % 3) of patch row r = w / 3 read from sh bytes before the row
 // start, i.e. column u = 16c + b - sh - 15; inside the circle (|u| <= umax[|r - 15|],
 // ORBextractor.cc:92-104) the weight byte is u + 15 and the one byte 1, else both 0.
@@ -509,8 +511,10 @@ static std::vector<uint4> make_od_tab(const int32_t *umax)
                     on[b >> 2] |= 1u << (8 * (b & 3));
                 }
             }
-            t[(sh * ORBG_OD_TABW + w) * 2] = make_uint4(wt[0], wt[1], wt[2], wt[3]);
-            t[(sh * ORBG_OD_TABW + w) * 2 + 1] = make_uint4(on[0], on[1], on[2], on[3]);
+            // [sh][weights | ones][w]: a wave's lanes (consecutive w) read consecutive 16-byte
+            // entries, conflict-free ds_read_b128
+            t[(sh * 2) * ORBG_OD_TABW + w] = make_uint4(wt[0], wt[1], wt[2], wt[3]);
+            t[(sh * 2 + 1) * ORBG_OD_TABW + w] = make_uint4(on[0], on[1], on[2], on[3]);
         }
     return t;
 }
@@ -1436,9 +1440,9 @@ static int launch_extract_pipe(orbg_ctx *c, const uint8_t *d_imgs, int B, int pi
     c->d_desc = c->desc_slot[s];
     c->d_counts = c->counts_slot[s];
     PROF_LAUNCH(c, "orient_desc",
-                hipLaunchKernelGGL(k_orient_desc,
+                launch_orient_desc(G.brief_fma != 0,
                                    dim3((G.out_frame + 4 * ORBG_OD_KPW - 1) / (4 * ORBG_OD_KPW) * B),
-                                   dim3(256), 0, st, c->d_geom, d_imgs, fs, pitch, c->d_pyr,
+                                   st, c->d_geom, d_imgs, fs, pitch, c->d_pyr,
                                    c->d_blur, c->d_odtab, c->d_lvl_kp, c->d_lvl_cnt,
                                    (OrbgKeypointDev *)c->d_kps, c->d_desc, c->d_counts));
     HIPCHK(hipEventRecord(c->ev_ext[s], st));
@@ -1553,9 +1557,9 @@ static int launch_extract(orbg_ctx *c, const uint8_t *d_imgs, int B, int pitch, 
     c->d_desc = c->desc_slot[s];
     c->d_counts = c->counts_slot[s];
     PROF_LAUNCH(c, "orient_desc",
-                hipLaunchKernelGGL(k_orient_desc,
+                launch_orient_desc(G.brief_fma != 0,
                                    dim3((G.out_frame + 4 * ORBG_OD_KPW - 1) / (4 * ORBG_OD_KPW) * B),
-                                   dim3(256), 0, st, c->d_geom, d_imgs, fs, pitch, c->d_pyr,
+                                   st, c->d_geom, d_imgs, fs, pitch, c->d_pyr,
                                    c->d_blur, c->d_odtab, c->d_lvl_kp, c->d_lvl_cnt, (OrbgKeypointDev *)c->d_kps,
                                    c->d_desc, c->d_counts));
     HIPCHK(hipEventRecord(c->ev_ext[s], st));

@@ -19,7 +19,6 @@ __device__ __attribute__((aligned(16))) int8_t od_pattern_i8[1024] = {
 #undef ORBG_PAIR
 };
 
-__device__ __forceinline__ int cv_round(float v) { return __float2int_rn(v); }
 
 // cv::fastAtan2 (OpenCV 3.4 atan_f32), degrees in [0, 360]
 __device__ __forceinline__ float fast_atan2(float y, float x)
@@ -90,7 +89,9 @@ static_assert(OD_KPW >= 1 && OD_KPW <= 32, "one slot per lane, okmask is 32 bits
 // IC_Angle byte tables (host-built, orbg_api.hip make_od_tab): entry (sh, w) for the patch
 // row r = w / 3, chunk c = w % 3 loaded from the 4-byte-aligned address sh bytes before the
 // row start: byte b is column u = 16c + b - sh - 15, weight u + 15 and one when
-// |u| <= umax[|r - 15|], else 0.  [sh][w][0] = weights, [sh][w][1] = ones.
+// |u| <= umax[|r - 15|], else 0.  [sh][0][w] = weights, [sh][1][w] = ones.
+// BFMA: the rBRIEF rotation x*b + y*a with one FMA (brief_fma pin) or two roundings (default)
+template <bool BFMA>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(ORBG_OD_WPE, 8))) void k_orient_desc(
     const OrbgGeom *__restrict__ g, const uint8_t *__restrict__ img0, int64_t img_fs,
     int img_pitch, const uint8_t *__restrict__ pyr, const uint8_t *__restrict__ blur,
@@ -241,8 +242,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(ORBG_OD_WPE
                 const int w = lane + 64 * k;
                 if (w < OD_TABW) {
                     const int v = par[k] - ORBG_HALF_PATCH;
-                    const uint4 tw = tab[(sh[k] * OD_TABW + w) * 2];
-                    const uint4 to = tab[(sh[k] * OD_TABW + w) * 2 + 1];
+                    const uint4 tw = tab[(2 * sh[k]) * OD_TABW + w];
+                    const uint4 to = tab[(2 * sh[k] + 1) * OD_TABW + w];
                     uint32_t su = 0, sv = 0;
                     su = __builtin_amdgcn_udot4(wd[k].x, tw.x, su, false);
                     su = __builtin_amdgcn_udot4(wd[k].y, tw.y, su, false);
@@ -323,7 +324,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(ORBG_OD_WPE
     int pat[4];
 #pragma unroll
     for (int t = 0; t < 4; t++) pat[t] = ((const int *)od_pattern_i8)[lane + 64 * t];
-    const bool bfma = g->brief_fma != 0;
     uint8_t *bp = (uint8_t *)bpatch[wv];
     // pipelined like phase A: slot j + 1's neighbourhood loads are issued right after slot j
     // is staged, and land while slot j's samples are read
@@ -354,13 +354,20 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(ORBG_OD_WPE
         if (j + OD_PFD < OD_KPW) nbh[(j + OD_PFD) % (OD_PFD + 1)] = load_nbhd(j + OD_PFD);
         const float a = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, a_l), j));
         const float b = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, b_l), j));
-        const uint8_t *bl = bp + OD_R * OD_ROWB + cur_bsh + OD_R;  // centre
+        // cvRound (round half to even) by the 1.5 * 2^23 shift: the float sum rounds r to an
+        // integer, ties to even, so bits(r + M) = 0x4B400000 + cvRound(r) for |r| < 2^22 and its
+        // low 24 bits are 2^22 + cvRound(r); one v_mad_u32_u24 then gives
+        // 48 (2^22 + ry) + bits(rx + M) = ry * 48 + rx + MK (mod 2^32), and the centre's byte
+        // index minus MK turns that into the sample's index in the staged neighbourhood
+        constexpr float M = 12582912.0f;
+        constexpr uint32_t MK = (uint32_t)OD_ROWB * 0x400000u + 0x4B400000u;
+        const uint32_t cbase = (uint32_t)(OD_R * OD_ROWB + cur_bsh + OD_R) - MK;
         // opaque per slot: keeps the offset decode inside the loop (hoisted, the 16 floats
         // stay live through phase C and push the kernel past 64 VGPRs)
         int pt[4] = {pat[0], pat[1], pat[2], pat[3]};
         asm volatile("" : "+v"(pt[0]), "+v"(pt[1]), "+v"(pt[2]), "+v"(pt[3]));
-        // all 8 sample offsets first (branch-free in bfma), then the 8 LDS reads in flight
-        // together, then the 4 ballots
+        // all 8 sample offsets first, then the 8 LDS reads in flight together, then the 4
+        // ballots
         int off[8];
 #pragma unroll
         for (int t = 0; t < 4; t++) {
@@ -369,14 +376,16 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(ORBG_OD_WPE
                 const float px = (float)(int8_t)(pt[t] >> (16 * s));
                 const float py = (float)(int8_t)(pt[t] >> (16 * s + 8));
                 const float t0 = px * b, t1 = py * a, t2 = px * a, t3 = py * b;
-                const float ry = bfma ? fmaf(px, b, t1) : t0 + t1;
-                const float rx = bfma ? fmaf(px, a, -t3) : t2 - t3;
-                off[2 * t + s] = cv_round(ry) * OD_ROWB + cv_round(rx);
+                const float ry = BFMA ? fmaf(px, b, t1) : t0 + t1;
+                const float rx = BFMA ? fmaf(px, a, -t3) : t2 - t3;
+                const uint32_t iy = __builtin_bit_cast(uint32_t, ry + M);
+                const uint32_t ix = __builtin_bit_cast(uint32_t, rx + M);
+                off[2 * t + s] = (int)((iy & 0xFFFFFFu) * (uint32_t)OD_ROWB + ix + cbase);
             }
         }
         int val[8];
 #pragma unroll
-        for (int i = 0; i < 8; i++) val[i] = bl[off[i]];
+        for (int i = 0; i < 8; i++) val[i] = bp[off[i]];
         uint32_t word = 0;
 #pragma unroll
         for (int t = 0; t < 4; t++) {
@@ -389,6 +398,21 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(ORBG_OD_WPE
         if (((okmask >> j) & 1u) && lane < 8)
             ((uint32_t *)(desc + (drow0 + i) * 32))[lane] = word;
     }
+}
+
+hipError_t launch_orient_desc(bool bfma, dim3 grid, hipStream_t st, const OrbgGeom *g,
+                              const uint8_t *img0, int64_t img_fs, int img_pitch,
+                              const uint8_t *pyr, const uint8_t *blur, const uint4 *odtab,
+                              const uint32_t *lvl_kp, const int32_t *lvl_cnt,
+                              OrbgKeypointDev *kps, uint8_t *desc, int32_t *counts)
+{
+    if (bfma)
+        hipLaunchKernelGGL(k_orient_desc<true>, grid, dim3(256), 0, st, g, img0, img_fs,
+                           img_pitch, pyr, blur, odtab, lvl_kp, lvl_cnt, kps, desc, counts);
+    else
+        hipLaunchKernelGGL(k_orient_desc<false>, grid, dim3(256), 0, st, g, img0, img_fs,
+                           img_pitch, pyr, blur, odtab, lvl_kp, lvl_cnt, kps, desc, counts);
+    return hipGetLastError();
 }
 
 }  // namespace orbg
