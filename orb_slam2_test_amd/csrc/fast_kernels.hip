@@ -41,7 +41,7 @@ namespace orbg {
 //                 <= P - 8 bytes used)
 //   list u16      pretest survivors: ry << 8 | gg << 2 | half << 1 | dark
 #ifndef ORBG_FC2_IL
-#define ORBG_FC2_IL 0  // 1: score rows interleaved with the tile rows (row stride 2P); A/B
+#define ORBG_FC2_IL 1  // score rows interleaved with the tile rows (row stride 2P; 0: apart, +0.6% per step)
 #endif
 #ifndef FC2_CPW
 #define FC2_CPW 2  // consecutive cells per wave (shared halo lines in L1, fewer workgroups)

@@ -650,7 +650,7 @@ static bool make_pyr_tables(const OrbgGeom &G, const std::vector<int2> &rtab, in
 
 // Build the geometry for an image size and allocate HBM for `batch` frames.
 #ifndef ORBG_FC2_IL
-#define ORBG_FC2_IL 0  // k_fast2 LDS layout variant (fast_kernels.hip); A/B builds only
+#define ORBG_FC2_IL 1  // k_fast2 LDS layout (fast_kernels.hip): score rows interleaved with the tile rows
 #endif
 
 static int plan(orbg_ctx *c, int w, int h, int batch)

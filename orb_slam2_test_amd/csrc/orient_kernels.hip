@@ -78,12 +78,9 @@ struct OrbgKeypointDev {
 #endif
 #define OD_TABW ORBG_OD_TABW    // IC_Angle lanes: 31 patch rows x 3 16-byte chunks
 #ifndef ORBG_OD_PFD
-#define ORBG_OD_PFD 1  // slots whose loads are in flight ahead of the one being summed / sampled
+#define ORBG_OD_PFD 2  // slots whose loads are in flight ahead of the one being summed / sampled (1: -0.4% per step)
 #endif
 #define OD_PFD ORBG_OD_PFD
-#ifndef ORBG_OD_RS
-#define ORBG_OD_RS 0  // 1: IC_Angle slot sums by reduce-scatter (0: one wave sum per slot); A/B
-#endif
 static_assert(OD_KPW >= 1 && OD_KPW <= 32, "one slot per lane, okmask is 32 bits");
 
 // IC_Angle byte tables (host-built, orbg_api.hip make_od_tab): entry (sh, w) for the patch
@@ -202,29 +199,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(ORBG_OD_WPE
             wd[k] = *(const uint4 *)(pa - sh[k] + 16 * pac[k]);
         }
     };
-    // Slot sums by a reduce-scatter over four slots at a time (instead of one wave sum per
-    // slot and moment): permlane32 / permlane16 swaps halve the slots per lane group twice,
-    // then a DPP sum inside each 16-lane row; row r then holds slot 4h + r's totals and lane
-    // 4h + r fetches them by ds_bpermute.  Integer sums: any order gives the same bits.
-    static_assert(OD_KPW == 8, "the reduce-scatter handles two halves of four slots");
     int M01 = 0, M10 = 0;
-    int pm01[4], pm10[4];  // the current half's per-lane partial moments
-    auto row_sum = [](int x) {
-        x += __builtin_amdgcn_update_dpp(0, x, 0xb1, 0xf, 0xf, false);   // quad_perm [1,0,3,2]
-        x += __builtin_amdgcn_update_dpp(0, x, 0x4e, 0xf, 0xf, false);   // quad_perm [2,3,0,1]
-        x += __builtin_amdgcn_update_dpp(0, x, 0x124, 0xf, 0xf, false);  // row_ror:4
-        x += __builtin_amdgcn_update_dpp(0, x, 0x128, 0xf, 0xf, false);  // row_ror:8
-        return x;
-    };
-    auto scatter4 = [&](const int (&v)[4]) -> int {
-        // lanes < 32: slots 0, 1 (+ the upper half's partials); lanes >= 32: slots 2, 3
-        const auto s02 = __builtin_amdgcn_permlane32_swap(v[0], v[2], false, false);
-        const auto s13 = __builtin_amdgcn_permlane32_swap(v[1], v[3], false, false);
-        const int t0 = (int)s02[0] + (int)s02[1], t1 = (int)s13[0] + (int)s13[1];
-        // rows 0..3 of the wave: slots 0, 1, 2, 3
-        const auto u = __builtin_amdgcn_permlane16_swap(t0, t1, false, false);
-        return row_sum((int)u[0] + (int)u[1]);
-    };
     {
         uint4 wbuf[OD_PFD + 1][2];
         int sbuf[OD_PFD + 1][2];
@@ -257,28 +232,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(ORBG_OD_WPE
                     m01 += v * (int)sv;
                 }
             }
-#if !ORBG_OD_RS
             m01 = wave_sum(m01);
             m10 = wave_sum(m10);
             if (lane == j) {
                 M01 = m01;
                 M10 = m10;
-            }
-            if (false) {
-#else
-            pm01[j & 3] = m01;
-            pm10[j & 3] = m10;
-            if ((j & 3) == 3) {
-#endif
-                const int r01 = scatter4(pm01), r10 = scatter4(pm10);
-                // lane 4h + r <- row r (lane 16 r)
-                const int src = ((lane - 4 * (j >> 2)) & 3) * 16 * 4;
-                const int g01 = __builtin_amdgcn_ds_bpermute(src, r01);
-                const int g10 = __builtin_amdgcn_ds_bpermute(src, r10);
-                if ((lane >> 2) == (j >> 2)) {
-                    M01 = g01;
-                    M10 = g10;
-                }
             }
         }
     }
