@@ -463,6 +463,33 @@ int orbg_ba_build_system_device(orbg_ctx *ctx, const orbg_pose *d_poses, int npo
                                 double *d_hpl, double *d_hpose, double *d_bpose,
                                 double *d_hpoint, double *d_bpoint);
 
+/* A device-resident LBA graph: the edge set of g2o's SparseOptimizer for one or many windows
+ * (Optimizer.cc:662-851 builds it; optimize(5), the outlier pass and optimize(10) at
+ * :857-905 rebuild the system over it every LM iteration).  Created once from host edges,
+ * kept in HBM packed: 24 bytes per edge (vertices, type / robust / active flags, f32
+ * observations) plus deduplicated camera and (inv_sigma2, huber_delta) tables and the
+ * per-vertex edge lists, so an iteration reads a quarter of orbg_edge's bytes.  ORB-SLAM2's
+ * observations are cv::KeyPoint floats: a graph needs every observation f32-exact (the mono
+ * third entry is ignored), at most 256 distinct (fx, fy, cx, cy, bf) and 65536 distinct
+ * (inv_sigma2, huber_delta); otherwise ORBG_ENOTSUP, and the record entry points apply.
+ * Results are bit-identical to orbg_ba_build_system_device / orbg_ba_errors_device on the
+ * same edges.  A graph belongs to the device of the context that created it. */
+typedef struct orbg_ba_graph orbg_ba_graph;
+int orbg_ba_graph_create(orbg_ctx *ctx, const orbg_edge *edges, int nedge, int npose,
+                         int npoint, orbg_ba_graph **out);
+int orbg_ba_graph_destroy(orbg_ba_graph *graph);
+/* setLevel(1) / setLevel(0) of the outlier pass (Optimizer.cc:871-901): active[e] (host,
+ * 0 or 1) for every edge, in the order given at creation; ordered on the context stream. */
+int orbg_ba_graph_set_active(orbg_ctx *ctx, orbg_ba_graph *graph, const uint8_t *active);
+/* buildSystem over the graph: outputs as orbg_ba_build_system_device (d_hpl [nedge][3][6]). */
+int orbg_ba_graph_build_system(orbg_ctx *ctx, orbg_ba_graph *graph, const orbg_pose *d_poses,
+                               const double *d_points, double *d_hpl, double *d_hpose,
+                               double *d_bpose, double *d_hpoint, double *d_bpoint);
+/* computeActiveErrors over the graph: outputs as orbg_ba_errors_device. */
+int orbg_ba_graph_errors(orbg_ctx *ctx, orbg_ba_graph *graph, const orbg_pose *d_poses,
+                         const double *d_points, double *d_err, double *d_chi2, double *d_rho0,
+                         uint8_t *d_depth_ok);
+
 /* g2o's per-trial error pass for the two LBA edge types: SparseOptimizer::
  * computeActiveErrors (Thirdparty/g2o/g2o/core/sparse_optimizer.cpp:61-76, computeError
  * types_six_dof_expmap.h:90-95, 122-127) and the terms activeRobustChi2 sums (:100-114,

@@ -191,8 +191,15 @@ def lib():
                                            vp, vp, vp]),
         "orbg_ba_build_system_device": (i32, [vp, vp, i32, vp, i32, vp, i32, vp, vp, vp, vp, vp,
                                               vp, vp, vp, vp]),
+        "orbg_ba_graph_create": (i32, [vp, vp, i32, i32, i32, P(vp)]),
+        "orbg_ba_graph_destroy": (i32, [vp]),
+        "orbg_ba_graph_set_active": (i32, [vp, vp, vp]),
+        "orbg_ba_graph_build_system": (i32, [vp, vp, vp, vp, vp, vp, vp, vp, vp]),
+        "orbg_ba_graph_errors": (i32, [vp, vp, vp, vp, vp, vp, vp, vp]),
     }
     for name, (res, args) in sig.items():
+        if os.environ.get("ORBG_LIB_VARIANT") and not hasattr(L, name):
+            continue  # developer A/B of an older build: entry points it predates stay unbound
         fn = getattr(L, name)
         fn.restype = res
         fn.argtypes = args

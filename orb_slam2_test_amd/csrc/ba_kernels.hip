@@ -15,6 +15,7 @@
 #include <cstring>
 
 #include "../../include/orbg.h"
+#include "orbg_internal.h"
 
 namespace orbg {
 
@@ -68,6 +69,47 @@ __device__ __forceinline__ void ba_edge_error(const orbg_pose &P, const double X
 }
 
 // ---------------------------------------------------------------------------
+// Edge sources: the kernels read an edge as an orbg_edge value, either from the ABI's
+// 104-byte records or from an orbg_ba_graph's 24-byte packed edges, whose camera and
+// (information, Huber delta) values sit in small deduplicated tables (an ORB-SLAM2 window has
+// one camera and one pair per octave and edge type; the observations are float keypoint
+// coordinates, exact in f32).  Same doubles either way, so the same bits out.
+// ---------------------------------------------------------------------------
+struct BaEdgeRecords {
+    const orbg_edge *e;
+    __device__ __forceinline__ orbg_edge operator()(int i) const { return e[i]; }
+};
+struct BaEdgePacked {
+    const BaPackedEdge *e;
+    const BaCam *cam;
+    const BaInfo *info;
+    __device__ __forceinline__ orbg_edge operator()(int i) const
+    {
+        const BaPackedEdge p = e[i];
+        orbg_edge r;
+        r.point = p.point;
+        r.pose = p.pose;
+        r.stereo = (int)(p.flags & 1u);
+        r.robust = (int)((p.flags >> 1) & 1u);
+        r.active = (int)((p.flags >> 2) & 1u);
+        r.pad = 0;
+        r.obs[0] = (double)p.obs[0];
+        r.obs[1] = (double)p.obs[1];
+        r.obs[2] = (double)p.obs[2];
+        const BaCam c = cam[(p.flags >> 8) & 0xFFu];
+        r.fx = c.fx;
+        r.fy = c.fy;
+        r.cx = c.cx;
+        r.cy = c.cy;
+        r.bf = c.bf;
+        const BaInfo f = info[p.flags >> 16];
+        r.inv_sigma2 = f.inv_sigma2;
+        r.huber_delta = f.huber_delta;
+        return r;
+    }
+};
+
+// ---------------------------------------------------------------------------
 // k_ba_errors: g2o's per-trial error pass (SparseOptimizer::computeActiveErrors,
 // sparse_optimizer.cpp:61-76) and the terms activeRobustChi2 sums (:100-114): thread per
 // edge, every edge given (active or not); err / rho0 / depth_ok may be NULL.
@@ -76,9 +118,10 @@ __device__ __forceinline__ void ba_edge_error(const orbg_pose &P, const double X
 //   depth_ok = isDepthPositive (types_six_dof_expmap.h:97-101, 129-133).
 // 28 B out per edge (err as f64 x 3 only on request).
 // ---------------------------------------------------------------------------
+template <class ES>
 __global__ __launch_bounds__(256) void k_ba_errors(const orbg_pose *__restrict__ poses,
                                                    const double *__restrict__ points,
-                                                   const orbg_edge *__restrict__ edges, int nedge,
+                                                   const ES edges, int nedge,
                                                    double *__restrict__ err_out,
                                                    double *__restrict__ chi2_out,
                                                    double *__restrict__ rho0_out,
@@ -86,7 +129,7 @@ __global__ __launch_bounds__(256) void k_ba_errors(const orbg_pose *__restrict__
 {
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= nedge) return;
-    const orbg_edge &e = edges[i];
+    const orbg_edge e = edges(i);
     const int ip = e.pose, iq = e.point;
     const orbg_pose P = poses[ip];
     const double X[3] = {points[3 * iq], points[3 * iq + 1], points[3 * iq + 2]};
@@ -109,17 +152,35 @@ __global__ __launch_bounds__(256) void k_ba_errors(const orbg_pose *__restrict__
         for (int k = 0; k < 3; k++) err_out[3 * (size_t)i + k] = err[k];
 }
 
-int launch_ba_errors(hipStream_t st, const orbg_pose *poses, const double *points,
-                     const orbg_edge *edges, int nedge, double *err, double *chi2, double *rho0,
-                     uint8_t *depth_ok, void *prof)
+template <class ES>
+static int launch_ba_errors_t(hipStream_t st, const orbg_pose *poses, const double *points,
+                              ES edges, int nedge, double *err, double *chi2, double *rho0,
+                              uint8_t *depth_ok, void *prof)
 {
     if (nedge <= 0) return 0;
     hipEvent_t a = nullptr;
     prof_begin(prof, st, "ba_errors", &a);
-    hipLaunchKernelGGL(k_ba_errors, dim3((nedge + 255) / 256), dim3(256), 0, st, poses, points,
-                       edges, nedge, err, chi2, rho0, depth_ok);
+    hipLaunchKernelGGL(k_ba_errors<ES>, dim3((nedge + 255) / 256), dim3(256), 0, st, poses,
+                       points, edges, nedge, err, chi2, rho0, depth_ok);
     prof_end(prof, st, "ba_errors", a);
     return hipGetLastError() == hipSuccess ? 0 : -5;
+}
+
+int launch_ba_errors(hipStream_t st, const orbg_pose *poses, const double *points,
+                     const orbg_edge *edges, int nedge, double *err, double *chi2, double *rho0,
+                     uint8_t *depth_ok, void *prof)
+{
+    return launch_ba_errors_t(st, poses, points, BaEdgeRecords{edges}, nedge, err, chi2, rho0,
+                              depth_ok, prof);
+}
+
+int launch_ba_errors_packed(hipStream_t st, const orbg_pose *poses, const double *points,
+                            const BaPackedEdge *edges, const BaCam *cam, const BaInfo *info,
+                            int nedge, double *err, double *chi2, double *rho0,
+                            uint8_t *depth_ok, void *prof)
+{
+    return launch_ba_errors_t(st, poses, points, BaEdgePacked{edges, cam, info}, nedge, err,
+                              chi2, rho0, depth_ok, prof);
 }
 
 // ---------------------------------------------------------------------------
@@ -224,9 +285,10 @@ struct BaEdgeOut {
 // ---------------------------------------------------------------------------
 #define BA_EDGES_TPB 256
 
+template <class ES>
 __global__ __launch_bounds__(BA_EDGES_TPB) void k_ba_edges(const orbg_pose *__restrict__ poses,
                                                           const double *__restrict__ points,
-                                                          const orbg_edge *__restrict__ edges,
+                                                          const ES edges,
                                                           int nslot,
                                                           const int32_t *__restrict__ point_off,
                                                           const int32_t *__restrict__ point_edges,
@@ -245,7 +307,7 @@ __global__ __launch_bounds__(BA_EDGES_TPB) void k_ba_edges(const orbg_pose *__re
         for (int k = 0; k < 12; k++) c[k] = 0;
         if (a < nslot) {
             const int ei = point_edges[a];
-            const orbg_edge e = edges[ei];
+            const orbg_edge e = edges(ei);
             const size_t ob = (size_t)ei * o.stride;
             q = e.point;
             if (!e.active) {  // setLevel(1): no contribution, outputs zero
@@ -359,9 +421,10 @@ typedef double v4d __attribute__((ext_vector_type(4)));
 #define BA_SLICE 64  // edges per wave
 #define BA_ROW 8     // doubles per staged pose row: J_pose (6), -e, w
 
+template <class ES>
 __global__ __launch_bounds__(256) void k_ba_pose_mfma(const orbg_pose *__restrict__ poses,
                                                       const double *__restrict__ points,
-                                                      const orbg_edge *__restrict__ edges,
+                                                      const ES edges,
                                                       const int32_t *__restrict__ pose_off,
                                                       const int32_t *__restrict__ pose_edges,
                                                       const int32_t *__restrict__ slice_off,
@@ -391,7 +454,7 @@ __global__ __launch_bounds__(256) void k_ba_pose_mfma(const orbg_pose *__restric
 #pragma unroll
             for (int c = 0; c < BA_ROW; c++) v[k][c] = 0;
         if (lane < ne) {
-            const orbg_edge e = edges[pose_edges[e0 + lane]];
+            const orbg_edge e = edges(pose_edges[e0 + lane]);
             if (e.active) {
                 const double X[3] = {points[3 * (size_t)e.point], points[3 * (size_t)e.point + 1],
                                      points[3 * (size_t)e.point + 2]};
@@ -517,12 +580,14 @@ static BaEdgeOut eout_fields(orbg_edge_out *eout, bool jacobians, bool errors)
 // device-resident linearisation: every pointer is device memory; scratch = ba_rows_bytes.
 // hpl != NULL: H_pl goes there as [nedge][3][6] (orbg_ba_build_system_device) and eout is
 // not used.
-int launch_ba_device(hipStream_t st, const orbg_pose *poses, int npose, const double *points,
-                     int npoint, const orbg_edge *edges, int nedge, const int32_t *pose_off,
-                     const int32_t *pose_edges, const int32_t *point_off,
-                     const int32_t *point_edges, orbg_edge_out *eout, double *hpose,
-                     double *bpose, double *hpoint, double *bpoint, double *scr, void *prof,
-                     bool jacobians, bool errors, double *hpl)
+template <class ES>
+static int launch_ba_device_t(hipStream_t st, const orbg_pose *poses, int npose,
+                              const double *points, int npoint, ES edges, int nedge,
+                              const int32_t *pose_off, const int32_t *pose_edges,
+                              const int32_t *point_off, const int32_t *point_edges,
+                              orbg_edge_out *eout, double *hpose, double *bpose, double *hpoint,
+                              double *bpoint, double *scr, void *prof, bool jacobians,
+                              bool errors, double *hpl)
 {
     BaEdgeOut o = eout_fields(eout, jacobians, errors);
     if (hpl) {
@@ -540,7 +605,7 @@ int launch_ba_device(hipStream_t st, const orbg_pose *poses, int npose, const do
     if (nedge) {
         hipEvent_t a = nullptr;
         prof_begin(prof, st, "ba_edges", &a);
-        hipLaunchKernelGGL(k_ba_edges, dim3((nedge + BA_EDGES_TPB - 1) / BA_EDGES_TPB),
+        hipLaunchKernelGGL(k_ba_edges<ES>, dim3((nedge + BA_EDGES_TPB - 1) / BA_EDGES_TPB),
                            dim3(BA_EDGES_TPB), 0, st, poses, points, edges, nedge, point_off,
                            point_edges, o, hpoint, bpoint);
         prof_end(prof, st, "ba_edges", a);
@@ -563,12 +628,37 @@ int launch_ba_device(hipStream_t st, const orbg_pose *poses, int npose, const do
         hipEvent_t a = nullptr;
         prof_begin(prof, st, "ba_pose_mfma", &a);
         // the grid covers the bound; waves past the actual slice count exit at once
-        hipLaunchKernelGGL(k_ba_pose_mfma, dim3((max_slices + 3) / 4), dim3(256), 0, st, poses,
+        hipLaunchKernelGGL(k_ba_pose_mfma<ES>, dim3((max_slices + 3) / 4), dim3(256), 0, st, poses,
                            points, edges, pose_off, pose_edges, slice_off, slice_pose, max_slices,
                            hpose, bpose);
         prof_end(prof, st, "ba_pose_mfma", a);
     }
     return hipGetLastError() == hipSuccess ? 0 : -5;
+}
+
+int launch_ba_device(hipStream_t st, const orbg_pose *poses, int npose, const double *points,
+                     int npoint, const orbg_edge *edges, int nedge, const int32_t *pose_off,
+                     const int32_t *pose_edges, const int32_t *point_off,
+                     const int32_t *point_edges, orbg_edge_out *eout, double *hpose,
+                     double *bpose, double *hpoint, double *bpoint, double *scr, void *prof,
+                     bool jacobians, bool errors, double *hpl)
+{
+    return launch_ba_device_t(st, poses, npose, points, npoint, BaEdgeRecords{edges}, nedge,
+                              pose_off, pose_edges, point_off, point_edges, eout, hpose, bpose,
+                              hpoint, bpoint, scr, prof, jacobians, errors, hpl);
+}
+
+// an orbg_ba_graph's buildSystem: H_pl compact, no per-edge record
+int launch_ba_graph(hipStream_t st, const orbg_pose *poses, int npose, const double *points,
+                    int npoint, const BaPackedEdge *edges, const BaCam *cam, const BaInfo *info,
+                    int nedge, const int32_t *pose_off, const int32_t *pose_edges,
+                    const int32_t *point_off, const int32_t *point_edges, double *hpl,
+                    double *hpose, double *bpose, double *hpoint, double *bpoint, double *scr,
+                    void *prof)
+{
+    return launch_ba_device_t(st, poses, npose, points, npoint, BaEdgePacked{edges, cam, info},
+                              nedge, pose_off, pose_edges, point_off, point_edges, nullptr,
+                              hpose, bpose, hpoint, bpoint, scr, prof, false, false, hpl);
 }
 
 // host arrays in/out: upload, build nothing on the device but the blocks, download

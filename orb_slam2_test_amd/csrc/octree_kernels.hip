@@ -20,6 +20,10 @@
 
 #pragma clang fp contract(off)
 
+#ifndef ORBG_OCT_PRIO
+#define ORBG_OCT_PRIO 2  // wave priority (s_setprio) of k_octree_lds (0: -1% per step)
+#endif
+
 namespace orbg {
 
 #define OCT_T 512
@@ -190,6 +194,11 @@ __global__ __launch_bounds__(OCT_T) void k_octree_lds(
         V.aux = (uint16_t *)p;
         V.coff = V.aux + D.acap2;
     }
+#if ORBG_OCT_PRIO
+    // the keypoint half's stream is the pipelined step's critical path, and this kernel is a
+    // latency-bound chain of barriers sharing the SIMDs with VALU-heavy waves: issue first
+    __builtin_amdgcn_s_setprio(ORBG_OCT_PRIO);
+#endif
     const int l = D.level0 + blockIdx.y, f = blockIdx.x, tid = threadIdx.x;
     const OrbgLevel &lv = g->lv[l];
     const int N = lv.nfeat, nIni = lv.nini;

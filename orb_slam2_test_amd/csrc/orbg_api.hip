@@ -12,6 +12,8 @@
 #include <cstdlib>
 #include <cstring>
 #include <string>
+#include <array>
+#include <map>
 #include <vector>
 
 #include "../../include/orbg.h"
@@ -103,6 +105,16 @@ size_t ba_scratch_bytes(int npose, int npoint, int nedge);
 int launch_ba_errors(hipStream_t st, const orbg_pose *poses, const double *points,
                      const orbg_edge *edges, int nedge, double *err, double *chi2, double *rho0,
                      uint8_t *depth_ok, void *prof);
+int launch_ba_errors_packed(hipStream_t st, const orbg_pose *poses, const double *points,
+                            const BaPackedEdge *edges, const BaCam *cam, const BaInfo *info,
+                            int nedge, double *err, double *chi2, double *rho0,
+                            uint8_t *depth_ok, void *prof);
+int launch_ba_graph(hipStream_t st, const orbg_pose *poses, int npose, const double *points,
+                    int npoint, const BaPackedEdge *edges, const BaCam *cam, const BaInfo *info,
+                    int nedge, const int32_t *pose_off, const int32_t *pose_edges,
+                    const int32_t *point_off, const int32_t *point_edges, double *hpl,
+                    double *hpose, double *bpose, double *hpoint, double *bpoint, double *scr,
+                    void *prof);
 }  // namespace orbg
 
 using namespace orbg;
@@ -2521,6 +2533,187 @@ extern "C" int orbg_ba_build_system_device(orbg_ctx *c, const orbg_pose *d_poses
                           d_pose_edges, d_point_off, d_point_edges, nullptr, d_hpose, d_bpose,
                           d_hpoint, d_bpoint, (double *)s, &c->prof, false, false, d_hpl);
     if (rc) return set_err(ORBG_EIO, "BA kernel launch failed");
+    return ORBG_OK;
+}
+
+// ---------------------------------------------------------------------------
+// orbg_ba_graph: a device-resident LBA edge set, packed (orbg_internal.h BaPackedEdge)
+// ---------------------------------------------------------------------------
+struct orbg_ba_graph {
+    int device = 0, nedge = 0, npose = 0, npoint = 0;
+    std::vector<BaPackedEdge> h;  // host copy (orbg_ba_graph_set_active rewrites the flags)
+    BaPackedEdge *d_edges = nullptr;
+    BaCam *d_cam = nullptr;
+    BaInfo *d_info = nullptr;
+    int32_t *d_off = nullptr, *d_pe = nullptr, *d_qoff = nullptr, *d_qe = nullptr;
+};
+
+static void ba_graph_free(orbg_ba_graph *g)
+{
+    if (!g) return;
+    hipSetDevice(g->device);
+    for (void *p : {(void *)g->d_edges, (void *)g->d_cam, (void *)g->d_info, (void *)g->d_off,
+                    (void *)g->d_pe, (void *)g->d_qoff, (void *)g->d_qe})
+        if (p) hipFree(p);
+    delete g;
+}
+
+extern "C" int orbg_ba_graph_create(orbg_ctx *c, const orbg_edge *edges, int nedge, int npose,
+                                    int npoint, orbg_ba_graph **out)
+{
+    if (!c || !out) return set_err(ORBG_EINVAL, "ctx / out is NULL");
+    *out = nullptr;
+    if (npose < 0 || npoint < 0 || nedge < 0) return set_err(ORBG_EINVAL, "negative size");
+    if (nedge && !edges) return set_err(ORBG_EINVAL, "edges is NULL");
+    if (int rc0 = ba_check_edges(edges, nedge, npose, npoint)) return rc0;
+    // dedup the camera and (information, Huber delta) values by their bits; the observations
+    // must survive the f32 store exactly (the mono third entry is never read: stored as 0)
+    std::map<std::array<uint64_t, 5>, int> cams;
+    std::map<std::array<uint64_t, 2>, int> infos;
+    std::vector<BaCam> hc;
+    std::vector<BaInfo> hi;
+    std::vector<BaPackedEdge> h((size_t)(nedge > 0 ? nedge : 1));
+    auto bits = [](double v) {
+        uint64_t u;
+        memcpy(&u, &v, 8);
+        return u;
+    };
+    for (int i = 0; i < nedge; i++) {
+        const orbg_edge &e = edges[i];
+        const std::array<uint64_t, 5> ck = {bits(e.fx), bits(e.fy), bits(e.cx), bits(e.cy), bits(e.bf)};
+        auto ci = cams.find(ck);
+        if (ci == cams.end()) {
+            if ((int)hc.size() >= ORBG_BA_MAX_CAMS)
+                return set_err(ORBG_ENOTSUP, "more than %d distinct cameras", ORBG_BA_MAX_CAMS);
+            ci = cams.emplace(ck, (int)hc.size()).first;
+            hc.push_back(BaCam{e.fx, e.fy, e.cx, e.cy, e.bf});
+        }
+        const std::array<uint64_t, 2> ik = {bits(e.inv_sigma2), bits(e.huber_delta)};
+        auto ii = infos.find(ik);
+        if (ii == infos.end()) {
+            if ((int)hi.size() >= ORBG_BA_MAX_INFOS)
+                return set_err(ORBG_ENOTSUP, "more than %d distinct (inv_sigma2, huber_delta)",
+                               ORBG_BA_MAX_INFOS);
+            ii = infos.emplace(ik, (int)hi.size()).first;
+            hi.push_back(BaInfo{e.inv_sigma2, e.huber_delta});
+        }
+        BaPackedEdge &p = h[i];
+        p.point = e.point;
+        p.pose = e.pose;
+        p.flags = (e.stereo ? 1u : 0u) | (e.robust ? 2u : 0u) | (e.active ? 4u : 0u) |
+                  (uint32_t)ci->second << 8 | (uint32_t)ii->second << 16;
+        const int nobs = e.stereo ? 3 : 2;
+        for (int k = 0; k < 3; k++) {
+            const double v = k < nobs ? e.obs[k] : 0.0;
+            p.obs[k] = (float)v;
+            if ((double)p.obs[k] != v)
+                return set_err(ORBG_ENOTSUP, "edge %d observation %d is not f32-exact", i, k);
+        }
+    }
+    // per-vertex edge lists (CSR), as orbg_ba_linearize
+    std::vector<int32_t> off(npose + 1, 0), pe(nedge > 0 ? nedge : 1);
+    std::vector<int32_t> qoff(npoint + 1, 0), qe(nedge > 0 ? nedge : 1);
+    for (int i = 0; i < nedge; i++) {
+        off[edges[i].pose + 1]++;
+        qoff[edges[i].point + 1]++;
+    }
+    for (int p = 0; p < npose; p++) off[p + 1] += off[p];
+    for (int q = 0; q < npoint; q++) qoff[q + 1] += qoff[q];
+    {
+        std::vector<int32_t> fill(off.begin(), off.end() - 1), qfill(qoff.begin(), qoff.end() - 1);
+        for (int i = 0; i < nedge; i++) {
+            pe[fill[edges[i].pose]++] = i;
+            qe[qfill[edges[i].point]++] = i;
+        }
+    }
+    HIPCHK(hipSetDevice(c->device));
+    orbg_ba_graph *g = new orbg_ba_graph;
+    g->device = c->device;
+    g->nedge = nedge;
+    g->npose = npose;
+    g->npoint = npoint;
+    int rc = 0;
+    if ((rc = dalloc(&g->d_edges, h.size())) || (rc = dalloc(&g->d_cam, hc.size())) ||
+        (rc = dalloc(&g->d_info, hi.size())) || (rc = dalloc(&g->d_off, off.size())) ||
+        (rc = dalloc(&g->d_pe, pe.size())) || (rc = dalloc(&g->d_qoff, qoff.size())) ||
+        (rc = dalloc(&g->d_qe, qe.size()))) {
+        ba_graph_free(g);
+        return rc;
+    }
+    auto up = [&](void *d, const void *src, size_t n) {
+        return n ? hipMemcpyAsync(d, src, n, hipMemcpyHostToDevice, c->stream) : hipSuccess;
+    };
+    if (up(g->d_edges, h.data(), (size_t)nedge * sizeof(BaPackedEdge)) != hipSuccess ||
+        up(g->d_cam, hc.data(), hc.size() * sizeof(BaCam)) != hipSuccess ||
+        up(g->d_info, hi.data(), hi.size() * sizeof(BaInfo)) != hipSuccess ||
+        up(g->d_off, off.data(), off.size() * 4) != hipSuccess ||
+        up(g->d_pe, pe.data(), (size_t)nedge * 4) != hipSuccess ||
+        up(g->d_qoff, qoff.data(), qoff.size() * 4) != hipSuccess ||
+        up(g->d_qe, qe.data(), (size_t)nedge * 4) != hipSuccess ||
+        hipStreamSynchronize(c->stream) != hipSuccess) {
+        ba_graph_free(g);
+        return set_err(ORBG_EIO, "graph upload failed");
+    }
+    g->h = std::move(h);
+    *out = g;
+    return ORBG_OK;
+}
+
+extern "C" int orbg_ba_graph_destroy(orbg_ba_graph *g)
+{
+    ba_graph_free(g);
+    return ORBG_OK;
+}
+
+extern "C" int orbg_ba_graph_set_active(orbg_ctx *c, orbg_ba_graph *g, const uint8_t *active)
+{
+    if (!c || !g) return set_err(ORBG_EINVAL, "ctx / graph is NULL");
+    if (g->nedge && !active) return set_err(ORBG_EINVAL, "active is NULL");
+    if (g->device != c->device) return set_err(ORBG_EINVAL, "graph of another device");
+    for (int i = 0; i < g->nedge; i++)
+        g->h[i].flags = (g->h[i].flags & ~4u) | (active[i] ? 4u : 0u);
+    HIPCHK(hipSetDevice(c->device));
+    if (g->nedge) {
+        // the stream may still read the previous flags: upload in order on it, and keep the
+        // host copy alive until it is done
+        HIPCHK(hipMemcpyAsync(g->d_edges, g->h.data(), (size_t)g->nedge * sizeof(BaPackedEdge),
+                              hipMemcpyHostToDevice, c->stream));
+        HIPCHK(hipStreamSynchronize(c->stream));
+    }
+    return ORBG_OK;
+}
+
+extern "C" int orbg_ba_graph_build_system(orbg_ctx *c, orbg_ba_graph *g, const orbg_pose *d_poses,
+                                          const double *d_points, double *d_hpl, double *d_hpose,
+                                          double *d_bpose, double *d_hpoint, double *d_bpoint)
+{
+    if (!c || !g) return set_err(ORBG_EINVAL, "ctx / graph is NULL");
+    if (g->device != c->device) return set_err(ORBG_EINVAL, "graph of another device");
+    if ((g->nedge && !d_hpl) || (g->npose && (!d_poses || !d_hpose || !d_bpose)) ||
+        (g->npoint && (!d_points || !d_hpoint || !d_bpoint)))
+        return set_err(ORBG_EINVAL, "NULL device array");
+    HIPCHK(hipSetDevice(c->device));
+    void *s;
+    int rc = scratch(c, ba_rows_bytes(g->nedge, g->npose), &s);
+    if (rc) return rc;
+    rc = launch_ba_graph(c->stream, d_poses, g->npose, d_points, g->npoint, g->d_edges, g->d_cam,
+                         g->d_info, g->nedge, g->d_off, g->d_pe, g->d_qoff, g->d_qe, d_hpl,
+                         d_hpose, d_bpose, d_hpoint, d_bpoint, (double *)s, &c->prof);
+    if (rc) return set_err(ORBG_EIO, "BA kernel launch failed");
+    return ORBG_OK;
+}
+
+extern "C" int orbg_ba_graph_errors(orbg_ctx *c, orbg_ba_graph *g, const orbg_pose *d_poses,
+                                    const double *d_points, double *d_err, double *d_chi2,
+                                    double *d_rho0, uint8_t *d_depth_ok)
+{
+    if (!c || !g) return set_err(ORBG_EINVAL, "ctx / graph is NULL");
+    if (g->device != c->device) return set_err(ORBG_EINVAL, "graph of another device");
+    if (g->nedge && (!d_poses || !d_points || !d_chi2)) return set_err(ORBG_EINVAL, "NULL device array");
+    HIPCHK(hipSetDevice(c->device));
+    if (launch_ba_errors_packed(c->stream, d_poses, d_points, g->d_edges, g->d_cam, g->d_info,
+                                g->nedge, d_err, d_chi2, d_rho0, d_depth_ok, &c->prof))
+        return set_err(ORBG_EIO, "BA error kernel launch failed");
     return ORBG_OK;
 }
 

@@ -26,6 +26,23 @@
 #define ORBG_GRID_COLS 64        // Frame.h:38
 #define ORBG_GRID_ROWS 48        // Frame.h:37
 #define ORBG_MATCH_TOPK 8
+// orbg_ba_graph's packed LBA edge (24 B instead of orbg_edge's 104): flags bit 0 stereo,
+// 1 robust, 2 active, bits 8..15 camera index, 16..31 (information, Huber) index; the
+// observations are f32 (ORB-SLAM2's are cv::KeyPoint floats: exact)
+struct BaPackedEdge {
+    int32_t point, pose;
+    uint32_t flags;
+    float obs[3];
+};
+struct BaCam {
+    double fx, fy, cx, cy, bf;
+};
+struct BaInfo {
+    double inv_sigma2, huber_delta;
+};
+#define ORBG_BA_MAX_CAMS 256
+#define ORBG_BA_MAX_INFOS 65536
+
 #ifndef ORBG_RZ_NT
 #define ORBG_RZ_NT 1             // k_resize: 16-row output tiles per workgroup (more: the prefetched chunks cost occupancy, measured slower)
 #endif

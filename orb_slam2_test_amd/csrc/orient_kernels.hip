@@ -77,6 +77,9 @@ struct OrbgKeypointDev {
 #define ORBG_OD_WPE 8  // min waves per SIMD (VGPR budget)
 #endif
 #define OD_TABW ORBG_OD_TABW    // IC_Angle lanes: 31 patch rows x 3 16-byte chunks
+#ifndef ORBG_OD_PRIO
+#define ORBG_OD_PRIO 1  // wave priority (s_setprio) of k_orient_desc (with k_octree_lds at 2: -1% per step)
+#endif
 #ifndef ORBG_OD_PFD
 #define ORBG_OD_PFD 2  // slots whose loads are in flight ahead of the one being summed / sampled (1: -0.4% per step)
 #endif
@@ -96,6 +99,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(ORBG_OD_WPE
     const int32_t *__restrict__ lvl_cnt, OrbgKeypointDev *__restrict__ kps,
     uint8_t *__restrict__ desc, int32_t *__restrict__ counts)
 {
+#if ORBG_OD_PRIO
+    __builtin_amdgcn_s_setprio(ORBG_OD_PRIO);  // on the pipelined step's critical path (A/B)
+#endif
     __shared__ uint4 bpatch[4][OD_SPAN * OD_ROWB / 16];
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
 #if ORBG_OD_LDSTAB

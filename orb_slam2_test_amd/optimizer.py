@@ -115,9 +115,18 @@ class DeviceLBA:
     with every array in HBM -- the per-iteration work of g2o's computeActiveErrors +
     buildSystem."""
 
-    def __init__(self, poses, points, edges, device=0, jacobians=True, edge_errors=True):
+    def __init__(self, poses, points, edges, device=0, jacobians=True, edge_errors=True,
+                 graph=False):
         import torch
         self.ctx = _ctx(device)
+        self.graph = None  # orbg_ba_graph (packed edges in HBM): build_system / errors use it
+        if graph:
+            e = np.ascontiguousarray(edges, L.EDGE_DTYPE)
+            h = L.C.c_void_p()
+            L.check(L.lib().orbg_ba_graph_create(self.ctx.handle, e.ctypes.data, len(e), len(poses),
+                                                 len(points), L.C.byref(h)),
+                    "orbg_ba_graph_create")
+            self.graph = h
         self.jacobians = bool(jacobians)  # eout.jp / jt stored (orbg_ba_set_jacobians)
         self.edge_errors = bool(edge_errors)  # eout.err / chi2 / rho1 (orbg_ba_set_edge_errors)
         self.np, self.nq, self.ne = len(poses), len(points), len(edges)
@@ -164,6 +173,12 @@ class DeviceLBA:
             self.d_hpl = torch.zeros((max(self.ne, 1), 3, 6), dtype=torch.float64,
                                      device=self.d_hpose.device)
         p = lambda t: L.C.c_void_p(t.data_ptr())  # noqa: E731
+        if self.graph is not None:
+            L.check(L.lib().orbg_ba_graph_build_system(
+                self.ctx.handle, self.graph, p(self.d_poses), p(self.d_points), p(self.d_hpl),
+                p(self.d_hpose), p(self.d_bpose), p(self.d_hpoint), p(self.d_bpoint)),
+                "orbg_ba_graph_build_system")
+            return
         L.check(L.lib().orbg_ba_build_system_device(
             self.ctx.handle, p(self.d_poses), self.np, p(self.d_points), self.nq, p(self.d_edges),
             self.ne, p(self.d_off), p(self.d_pe), p(self.d_qoff), p(self.d_qe), p(self.d_hpl),
@@ -174,9 +189,27 @@ class DeviceLBA:
         """The per-trial error pass (orbg_ba_errors_device): chi2 and the robust term of every
         edge into self.d_chi2 / self.d_rho0."""
         p = lambda t: L.C.c_void_p(t.data_ptr())  # noqa: E731
+        if self.graph is not None:
+            L.check(L.lib().orbg_ba_graph_errors(self.ctx.handle, self.graph, p(self.d_poses),
+                                                 p(self.d_points), None, p(self.d_chi2),
+                                                 p(self.d_rho0), None), "orbg_ba_graph_errors")
+            return
         L.check(L.lib().orbg_ba_errors_device(self.ctx.handle, p(self.d_poses), p(self.d_points),
                                               p(self.d_edges), self.ne, None, p(self.d_chi2),
                                               p(self.d_rho0), None), "orbg_ba_errors_device")
+
+    def set_active(self, active):
+        """The outlier pass's setLevel (Optimizer.cc:871-901) on the graph: active[e] per edge."""
+        a = np.ascontiguousarray(np.asarray(active) != 0, np.uint8)
+        if self.graph is None:
+            raise ValueError("set_active needs a DeviceLBA built with graph=True")
+        L.check(L.lib().orbg_ba_graph_set_active(self.ctx.handle, self.graph, a.ctypes.data),
+                "orbg_ba_graph_set_active")
+
+    def __del__(self):
+        if getattr(self, "graph", None) is not None:
+            L.lib().orbg_ba_graph_destroy(self.graph)
+            self.graph = None
 
     def download(self):
         self.ctx.sync()

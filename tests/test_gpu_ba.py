@@ -163,6 +163,48 @@ def test_build_system_compact_h_pl(oracle):
     assert rel(hpl, reo["hpl"]) < RTOL
 
 
+def test_graph_packed_equals_records(oracle):
+    """orbg_ba_graph (packed 24-byte edges + deduplicated camera / information tables): the
+    same blocks, H_pl, chi2 and rho bits as the record entry points, also after the outlier
+    pass's set_active, and chi2 / rho equal to the oracle's."""
+    from orb_slam2_test_amd.optimizer import DeviceLBA
+    poses, pts, edges = concat_windows([S.ba_window(n_points=400, seed=120 + i) for i in range(3)])
+    edges["active"][::11] = 0
+    a = DeviceLBA(poses, pts, edges)
+    g = DeviceLBA(poses, pts, edges, graph=True)
+
+    def run(x):
+        x.build_system()
+        x.errors()
+        x.ctx.sync()
+        return [t.cpu().numpy() for t in (x.d_hpl, x.d_hpose, x.d_bpose, x.d_hpoint, x.d_bpoint,
+                                          x.d_chi2, x.d_rho0)]
+
+    for u, v in zip(run(a), run(g)):
+        assert np.array_equal(u, v)
+    r = oracle.ba_errors(poses, pts, edges)
+    chi2 = g.d_chi2.cpu().numpy()[:len(edges)]
+    assert np.array_equal(chi2, r[1])
+    # the outlier pass: a different active set on the graph == records rebuilt with it
+    act = (np.arange(len(edges)) % 5 != 0).astype(np.uint8)
+    g.set_active(act)
+    e2 = edges.copy()
+    e2["active"] = act
+    b = DeviceLBA(poses, pts, e2)
+    for u, v in zip(run(b), run(g)):
+        assert np.array_equal(u, v)
+
+
+def test_graph_rejects_non_f32_observations():
+    """A graph stores f32 observations: an edge whose observation is not f32-exact is
+    refused (ORBG_ENOTSUP), the record entry points stay available for it."""
+    from orb_slam2_test_amd.optimizer import DeviceLBA
+    poses, pts, edges = S.ba_window(n_points=100, seed=7)
+    edges["obs"][3, 0] += 1e-9
+    with pytest.raises(Exception, match="f32-exact"):
+        DeviceLBA(poses, pts, edges, graph=True)
+
+
 @pytest.mark.parametrize("seed,n_points,lam_scale", [(3, 800, 1e-3), (4, 6000, 1e-5),
                                                      (5, 300, 10.0)])
 def test_schur_solve_matches_oracle(oracle, seed, n_points, lam_scale):

@@ -40,6 +40,9 @@ def main():
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--jacobians", action="store_true",
                     help="also store g2o's per-edge Jacobians eout.jp / jt (orbg_ba_set_jacobians)")
+    ap.add_argument("--no-graph", action="store_true",
+                    help="orbg_ba_build_system_device / orbg_ba_errors_device on the 104-byte edge "
+                         "records instead of an orbg_ba_graph (packed 24-byte edges)")
     ap.add_argument("--records", action="store_true",
                     help="buildSystem through orbg_ba_linearize_device (H_pl inside the 400-byte "
                          "orbg_edge_out records) instead of orbg_ba_build_system_device (compact "
@@ -57,10 +60,13 @@ def main():
 
     base = [S.ba_window(seed=500 + i) for i in range(args.distinct)]
     poses, pts, edges = concat_windows([base[i % args.distinct] for i in range(args.windows)])
-    lba = DeviceLBA(poses, pts, edges, jacobians=args.jacobians, edge_errors=args.edge_errors)
+    use_records = args.records or args.jacobians or args.edge_errors
+    use_graph = not (use_records or args.no_graph)
+    lba = DeviceLBA(poses, pts, edges, jacobians=args.jacobians, edge_errors=args.edge_errors,
+                    graph=use_graph)
 
     def iteration():
-        if args.records or args.jacobians or args.edge_errors:
+        if use_records:
             lba.linearize()
         else:
             lba.build_system()
@@ -90,10 +96,11 @@ def main():
                    "points": len(pts), "stereo_frac": round(float(np.mean(edges["stereo"])), 3),
                    "edge_jacobians_stored": bool(args.jacobians),
                    "edge_errors_stored": bool(args.edge_errors),
-                   "iteration": ("orbg_ba_linearize_device" if (args.records or args.jacobians
-                                                                 or args.edge_errors)
-                                 else "orbg_ba_build_system_device") +
-                                " (buildSystem) + orbg_ba_errors_device (computeActiveErrors)"},
+                   "iteration": ("orbg_ba_linearize_device + orbg_ba_errors_device" if use_records
+                                 else "orbg_ba_graph_build_system + orbg_ba_graph_errors (packed "
+                                      "24-byte edges)" if use_graph
+                                 else "orbg_ba_build_system_device + orbg_ba_errors_device") +
+                                " (buildSystem + computeActiveErrors)"},
         "ms_per_iter": round(dt / args.iters * 1e3, 4),
         "kernels": {k: {"ms_per_iter": round(v[0] / args.iters, 4),
                         "avg_launch_ms": round(v[0] / max(v[1], 1), 5)} for k, v in kern.items()},
@@ -105,7 +112,9 @@ def main():
         # (g2o's _Hpl, read by the Schur step: not in SURVEY 8d's 108 B), the point in and its
         # H_ll | b_l out
         from orb_slam2_test_amd import _lib as LB
-        abi = ne * (LB.EDGE_DTYPE.itemsize + 4 + 144) + len(pts) * (24 + 4 + 96)
+        # the edge as the iteration reads it (24-byte packed edge of a graph, or the record)
+        ebytes = 24 if use_graph else LB.EDGE_DTYPE.itemsize
+        abi = ne * (ebytes + 4 + 144) + len(pts) * (24 + 4 + 96)
         out["roofline"] = {"kernel": "ba_edges", "bound": "hbm", "achieved": round(ach, 1),
                            "peak": HBM_PEAK_GBS, "unit": "GB/s",
                            "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": None,
