@@ -32,6 +32,9 @@ namespace orbg {
 void prof_begin(void *prof, hipStream_t s, const char *n, hipEvent_t *a);
 void prof_end(void *prof, hipStream_t s, const char *n, hipEvent_t a);
 
+#ifndef ORBG_ST_XCD
+#define ORBG_ST_XCD 1  // XCD-aware pair mapping of k_stereo_match / k_stereo_sad (0: A/B)
+#endif
 #define ST_TH_HIGH 100
 #define ST_TH_ORB ((100 + 50) / 2)
 #define ST_W 5
@@ -171,11 +174,15 @@ __global__ __launch_bounds__(256) void k_stereo_match(StereoGeom G,
                                                      const int16_t *__restrict__ row_list,
                                                      int32_t *__restrict__ best_r)
 {
-    const int p = blockIdx.y;
+    // XCD-aware: the workgroups of one pair run on one XCD, so the right frame's keypoint and
+    // descriptor rows they share are fetched into one L2 (not once per XCD)
+    const int id = ORBG_ST_XCD ? xcd_remap(blockIdx.x + gridDim.x * blockIdx.y, gridDim.x * gridDim.y)
+                               : (int)(blockIdx.x + gridDim.x * blockIdx.y);
+    const int p = id / gridDim.x, bx = id - p * gridDim.x;
     const int lane = threadIdx.x & 63;
     const int fl = left[p], fr = right[p];
     const int nl = counts[fl];
-    for (int iL = blockIdx.x * 4 + (threadIdx.x >> 6); iL < nl; iL += ST_WAVES)
+    for (int iL = bx * 4 + (threadIdx.x >> 6); iL < nl; iL += ST_WAVES)
         stereo_match_one(G, kps, desc, fl, fr, iL, lane, p, row_off, row_list,
                          best_r + (size_t)p * G.fc);
 }
@@ -306,11 +313,15 @@ __global__ __launch_bounds__(256) void k_stereo_sad(StereoGeom G,
     __shared__ int sad[4][2 * ST_L + 1];
     __shared__ uint32_t stage[4][11 * 4 + 11 * 7];
     __shared__ int shl[4][11], shr[4][11];
-    const int p = blockIdx.y;
+    // XCD-aware: a pair's workgroups on one XCD, so the pyramid rows their patches and strips
+    // share come into one L2
+    const int id = ORBG_ST_XCD ? xcd_remap(blockIdx.x + gridDim.x * blockIdx.y, gridDim.x * gridDim.y)
+                               : (int)(blockIdx.x + gridDim.x * blockIdx.y);
+    const int p = id / gridDim.x, bx = id - p * gridDim.x;
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
     const int fl = left[p], fr = right[p];
     const int nl = counts[fl];
-    for (int iL = blockIdx.x * 4 + wv; iL < nl; iL += ST_WAVES) {
+    for (int iL = bx * 4 + wv; iL < nl; iL += ST_WAVES) {
         stereo_sad_one(G, kps, best_r, img0, img_fs, img_pitch, pyr, pyr_frame, uright, depth,
                        sad_out, p, fl, fr, iL, lane, sad[wv], stage[wv], shl[wv], shr[wv]);
         wave_sync_lds();  // the next keypoint reuses this wave's LDS
