@@ -233,9 +233,10 @@ def main():
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--batch", type=int, default=None,
-                    help="frames (stereo: L/R pairs) per GPU per step; default 512 (stereo 256 "
-                         "pairs = 512 images): +3.3%% frames/s over 256, the fixed cost of a "
-                         "step's dependent launches spread over twice the frames")
+                    help="frames (stereo: L/R pairs) per GPU per step; default "
+                         "sequence.BENCH_BATCH: 1024 (stereo 512 pairs = 1024 images), the fixed "
+                         "cost of a step's dependent launches spread over more frames (512: "
+                         "-2.5%%, 2048: -1%% frames/s)")
     ap.add_argument("--blocks", type=int, default=4,
                     help="distinct resident input blocks the steps cycle through (4 x 239 MB "
                          "> the 256 MB Infinity Cache: every step reads new frames); 1 = the "
@@ -275,7 +276,8 @@ def main():
     if not args.cpu_threads:
         args.cpu_threads = cpu_share()
 
-    B = args.batch or (256 if args.stereo else 512)
+    B = args.batch or sequence.BENCH_BATCH["stereo" if args.stereo else
+                                           "extract" if args.extract_only else "mono"]
     # Streamed input: the step cycles through `nblocks` distinct resident blocks of the
     # sequence (nblocks x 239 MB > the 256 MB Infinity Cache at the defaults), so every step
     # reads frames the previous steps did not (no cross-step cache reuse of the input).

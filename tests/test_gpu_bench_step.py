@@ -7,12 +7,12 @@ step's outputs on the match stream while later steps are already in flight
 (orbg_batch_acquire / orbg_batch_release).  Every frame of every step is compared with the
 oracle (oracle/, the C restatement, threaded over the host's CPU share):
 
-  C3 (mono, B = 512 + the halo frame): keypoints (all 7 cv::KeyPoint fields), descriptors,
+  C3 (mono, B = 1024 + the halo frame): keypoints (all 7 cv::KeyPoint fields), descriptors,
      knn2 {best index, best, second} of every F2 keypoint, vnMatches12 of every pair, and
      the per-frame summary (keypoints, SearchForInitialization matches)
      -- ORBextractor.cc:1330-1397, ORBmatcher.cc:487-631 / 541-556;
-  C2 (extract only, B = 512): keypoints and descriptors;
-  C4 (stereo, B = 256 L/R pairs = 512 images): both images' keypoints and descriptors,
+  C2 (extract only, B = 1024): keypoints and descriptors;
+  C4 (stereo, B = 512 L/R pairs = 1024 images): both images' keypoints and descriptors,
      mvuRight / mvDepth of every pair and the stereo summary -- Frame.cc:619-834.
 """
 import ctypes as C
@@ -86,7 +86,7 @@ def _frames_host(cap, nimg):
 
 @pytest.fixture(scope="module")
 def mono_blocks():
-    n_total, ranges = S.bench_block_ranges(512, 1, 0, NBLOCKS)
+    n_total, ranges = S.bench_block_ranges(sequence.BENCH_BATCH["mono"], 1, 0, NBLOCKS)
     return S.sequence_blocks(n_total, ranges, H, W)
 
 
@@ -98,7 +98,7 @@ def mono_ref(oracle, mono_blocks):
 
 
 def test_bench_step_c3_mono_every_frame(mono_blocks, mono_ref):
-    B = 512
+    B = sequence.BENCH_BATCH["mono"]
     nimg = B + 1
     ext, bstep = _runner(B, "mono", nimg)
     caps = []
@@ -155,7 +155,7 @@ def test_bench_step_c3_mono_every_frame(mono_blocks, mono_ref):
 
 
 def test_bench_step_c2_extract_only_every_frame(oracle, mono_blocks, mono_ref):
-    B = 512
+    B = sequence.BENCH_BATCH["extract"]
     blocks = [np.ascontiguousarray(b[1:]) for b in mono_blocks]  # bench --extract-only
     ext, bstep = _runner(B, "extract", B)
     caps = []
@@ -180,7 +180,7 @@ def test_bench_step_c2_extract_only_every_frame(oracle, mono_blocks, mono_ref):
 
 def test_bench_step_c4_stereo_every_pair(oracle):
     from concurrent.futures import ThreadPoolExecutor
-    B = 256
+    B = sequence.BENCH_BATCH["stereo"]
     nb = 2
     lefts, rights, _ = S.stereo_sequence(nb * B, H, W, seed=S.DEFAULT_SEED)  # bench rank 0
     blocks = []

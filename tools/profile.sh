@@ -31,7 +31,7 @@ i=0
 for P in "$P1" "$P2" "FETCH_SIZE" "WRITE_SIZE"; do
     i=$((i + 1))
     echo "[profile] pmc pass $i: $P"
-    timeout -s KILL 150 rocprofv3 --pmc $P -d "$O/pmc$i" -o run --output-format csv \
+    timeout -s KILL 240 rocprofv3 --pmc $P -d "$O/pmc$i" -o run --output-format csv \
         -- python3 "$R/$SCRIPT" "$@" $PMC_ARGS > "$O/pmc$i.log" 2>&1
 done
 python3 "$R/tools/pmc_kernels.py" "$O" "$O/pmc_kernels.json" ${PMC_STEPS:-0}
