@@ -248,7 +248,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(ORBG_OD_WPE
     }
 
     if (g->dbg == 21) {  // developer phase timing (ORBG_DBG, dev builds): stop after A
-        if (lane == 0) counts[f] = M01 + M10;
+        // keep the sums live without a store per wave to one address (that alone would
+        // serialise): lane j's sums into its own slot's descriptor row
+        if (my_ok) ((int *)(desc + (drow0 + my_i) * 32))[0] = M01 + M10;
         return;
     }
     // ---- B: angle = fastAtan2(m_01, m_10) (:110), cos / sin of it (:121-122), and the
