@@ -195,6 +195,32 @@ def test_graph_packed_equals_records(oracle):
         assert np.array_equal(u, v)
 
 
+def test_graph_several_cameras_and_informations(oracle):
+    """The graph's camera / information tables with several entries (windows of different
+    calibrations, per-edge information and Huber deltas off the octave table): the same bits
+    as the record path."""
+    from orb_slam2_test_amd.optimizer import DeviceLBA
+    wins = [S.ba_window(n_points=300, seed=140 + i) for i in range(3)]
+    for i, (_, _, e) in enumerate(wins):
+        e["fx"] += 3.0 * i
+        e["cy"] -= 1.5 * i
+        e["bf"] *= 1.0 + 0.1 * i
+    poses, pts, edges = concat_windows(wins)
+    edges["inv_sigma2"][::13] *= 0.5
+    edges["huber_delta"][::17] = 2.0
+    a = DeviceLBA(poses, pts, edges)
+    g = DeviceLBA(poses, pts, edges, graph=True)
+    for x in (a, g):
+        x.build_system()
+        x.errors()
+        x.ctx.sync()
+    for u, v in zip((a.d_hpl, a.d_hpose, a.d_bpose, a.d_hpoint, a.d_bpoint, a.d_chi2, a.d_rho0),
+                    (g.d_hpl, g.d_hpose, g.d_bpose, g.d_hpoint, g.d_bpoint, g.d_chi2, g.d_rho0)):
+        assert np.array_equal(u.cpu().numpy(), v.cpu().numpy())
+    r = oracle.ba_errors(poses, pts, edges)
+    assert np.array_equal(g.d_chi2.cpu().numpy()[:len(edges)], r[1])
+
+
 def test_graph_rejects_non_f32_observations():
     """A graph stores f32 observations: an edge whose observation is not f32-exact is
     refused (ORBG_ENOTSUP), the record entry points stay available for it."""
