@@ -51,20 +51,43 @@ namespace ref {
 // while LocalMapping runs LocalBundleAdjustment (System.cc:117, LocalMapping.cc:99), and a
 // liborbg context is not thread-safe (include/orbg.h), so each thread gets its own context
 // (its own streams, planning state and scratch); distinct contexts run concurrently.
-inline orbg_ctx *default_ctx()
+//
+// ctx_for_scale(sf, nl) is the calling thread's context for other pyramid settings (created
+// on first use per (sf, nl), kept until thread exit); default_ctx() is ctx_for_scale(1.2, 8).
+inline orbg_ctx *ctx_for_scale(float scale_factor, int nlevels)
 {
     struct Holder {
+        float sf;
+        int nl;
         orbg_ctx *c = nullptr;
-        Holder()
+        Holder(float sf_, int nl_) : sf(sf_), nl(nl_)
         {
             orbg_params p;
             orbg_params_default(&p);
+            p.scale_factor = sf;
+            p.nlevels = nl;
             check(orbg_create(0, &p, &c), "orbg_create");
         }
         ~Holder() { orbg_destroy(c); }
+        Holder(const Holder &) = delete;
+        Holder &operator=(const Holder &) = delete;
     };
-    static thread_local Holder h;
-    return h.c;
+    static thread_local std::list<Holder> held;  // list: a context's address never moves
+    for (const Holder &h : held)
+        if (h.sf == scale_factor && h.nl == nlevels) return h.c;
+    held.emplace_back(scale_factor, nlevels);
+    return held.back().c;
+}
+
+inline orbg_ctx *default_ctx() { return ctx_for_scale(1.2f, 8); }
+
+// The calling thread's context for a Frame's / KeyFrame's own pyramid (mfScaleFactor,
+// mnScaleLevels): the matchers size their search radii from the frame's mvScaleFactors
+// (ORBmatcher.cc:86,117,1570,1724), which the context's scale tables restate.
+template <class FrameT>
+inline orbg_ctx *ctx_for(const FrameT &F)
+{
+    return ctx_for_scale(F.mfScaleFactor, F.mnScaleLevels);
 }
 
 // cv::KeyPoint -> orbg_keypoint (field by field, the ABI's layout is its own)

@@ -61,6 +61,8 @@ struct Frame {  // include/Frame.h
     std::vector<MapPoint *> mvpMapPoints;
     std::vector<bool> mvbOutlier;
     float mbf = 0, mb = 0;
+    int mnScaleLevels = 8;
+    float mfScaleFactor = 1.2f;
     void SetPose(cv::Mat T) { mTcw = T.clone(); }
 };
 float Frame::fx, Frame::fy, Frame::cx, Frame::cy, Frame::mnMinX, Frame::mnMaxX, Frame::mnMinY,
@@ -229,6 +231,20 @@ int main(int argc, char **argv)
         F->mb = F->mbf / Frame::fx;
     }
     orbg_ctx *ctx = orbg_compat::ref::default_ctx();
+    {   // a frame's own pyramid settings pick the thread's context with those scale tables
+        REQUIRE(orbg_compat::ref::ctx_for(F1) == ctx);
+        Frame F5;
+        F5.mfScaleFactor = 1.25f;
+        F5.mnScaleLevels = 6;
+        orbg_ctx *c5 = orbg_compat::ref::ctx_for(F5);
+        REQUIRE(c5 != ctx && orbg_compat::ref::ctx_for(F5) == c5);
+        int32_t nl = 0;
+        float sf = 0, sc[8] = {0};
+        REQUIRE(orbg_get_scale_tables(c5, &nl, &sf, sc, nullptr, nullptr, nullptr, nullptr,
+                                      nullptr) == ORBG_OK);
+        REQUIRE(nl == 6 && sf == 1.25f && sc[0] == 1.f && sc[1] == 1.25f);
+        REQUIRE(std::fabs(sc[5] - (float)std::pow(1.25, 5)) <= 1e-5f * sc[5]);
+    }
 
     // ---- ORBmatcher(0.9, true).SearchForInitialization (Tracking::MonocularInitialization) ----
     std::vector<cv::Point2f> prev(F1.N);
