@@ -195,6 +195,19 @@ def test_resize_chain_scale_factors(oracle, kitti_seq, sf, nl):
     assert "resize_chain" in names and "resize" not in names
 
 
+@pytest.mark.parametrize("sf,nl", [(1.1, 8), (1.25, 8), (1.3, 6)])
+def test_other_scale_factors(oracle, kitti_seq, sf, nl):
+    """ORBextractor.scaleFactor / nLevels other than the shipped 1.2 / 8 (ORBextractor.cc:
+    432-470 tables, :1400-1443 pyramid): bit-exact whichever pyramid kernel the plan takes."""
+    names = _extract_with(oracle, kitti_seq[1], sf, nl)
+    assert ("resize" in names) != ("resize_chain" in names)
+
+
+def test_euroc_752x480_1200(oracle):
+    """EuRoC's settings (Examples/Monocular/EuRoC.yaml: 752 x 480, 1200 features)."""
+    assert_same(oracle, S.frame(480, 752, seed=77), nfeat=1200)
+
+
 def test_resize_chain_forced_at_1_2(oracle, kitti_seq):
     """ORBG_PYR=0 forces the k_resize chain at the reference's 1.2 (KITTI and TUM shapes)."""
     names = _extract_with(oracle, kitti_seq[2], 1.2, 8, env={"ORBG_PYR": "0"})
