@@ -116,53 +116,15 @@ __global__ __launch_bounds__(ST_ROWS_T) void k_stereo_rows(StereoGeom G,
 }
 
 // ---- descriptor match ---------------------------------------------------------------
-// one wave per left keypoint at a time, lanes over the row's candidates (all loads in
-// flight), then a wave minimum of (dist << 16 | iR) -- the lexicographic (distance, index)
-// minimum.  ST_WAVES waves per pair walk the left keypoints.
+// 16 lanes per left keypoint over the row's candidates, then a 16-lane minimum of
+// (dist << 16 | iR) -- the lexicographic (distance, index) minimum.  ST_WAVES waves per pair
+// walk the left keypoints.
 #define ST_WAVES 512
 
-__device__ __forceinline__ void stereo_match_one(const StereoGeom &G,
-                                                 const orbg_keypoint *__restrict__ kps,
-                                                 const uint8_t *__restrict__ desc, int fl,
-                                                 int fr, int iL, int lane, int p,
-                                                 const int32_t *__restrict__ row_off,
-                                                 const int16_t *__restrict__ row_list,
-                                                 int32_t *__restrict__ out)
-{
-    const orbg_keypoint kl = kps[(size_t)fl * G.fc + iL];
-    const int row = (int)kl.y;
-    const float minU = kl.x - G.max_d, maxU = kl.x - 0.0f;
-    int c0 = 0, c1 = 0;
-    if (row >= 0 && row < G.h && !(maxU < 0)) {
-        const int32_t *off = row_off + (size_t)p * (ST_MAX_ROWS + 1);
-        c0 = off[row];
-        c1 = min(off[row + 1], G.list_cap);
-    }
-    const uint4 *q = (const uint4 *)(desc + ((size_t)fl * G.fc + iL) * 32);
-    const orbg_keypoint *kr = kps + (size_t)fr * G.fc;
-    const uint8_t *dr = desc + (size_t)fr * G.fc * 32;
-    const int16_t *list = row_list + (size_t)p * G.list_cap;
-    uint32_t best = 0xFFFFFFFFu;
-    for (int c = c0 + lane; c < c1; c += 64) {
-        const int iR = list[c];
-        const orbg_keypoint k = kr[iR];
-        if (k.octave < kl.octave - 1 || k.octave > kl.octave + 1) continue;
-        if (!(k.x >= minU && k.x <= maxU)) continue;
-        const uint4 *d = (const uint4 *)(dr + (size_t)iR * 32);
-        const uint4 d0 = d[0], d1 = d[1], q0 = q[0], q1 = q[1];
-        const uint32_t dist = __popc(q0.x ^ d0.x) + __popc(q0.y ^ d0.y) + __popc(q0.z ^ d0.z) +
-                              __popc(q0.w ^ d0.w) + __popc(q1.x ^ d1.x) + __popc(q1.y ^ d1.y) +
-                              __popc(q1.z ^ d1.z) + __popc(q1.w ^ d1.w);
-        best = min(best, (dist << 16) | (uint32_t)iR);
-    }
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) best = min(best, (uint32_t)__shfl_xor((int)best, o, 64));
-    if (lane == 0) {
-        const int bestDist = best == 0xFFFFFFFFu ? ST_TH_HIGH : (int)(best >> 16);
-        // the reference keeps a candidate only below TH_HIGH, then needs < (TH_HIGH+TH_LOW)/2
-        out[iL] = (bestDist < ST_TH_HIGH && bestDist < ST_TH_ORB) ? (int)(best & 0xFFFF) : -1;
-    }
-}
+// A wave matches ST_MG left keypoints at once (iL = base + j * ST_WAVES), 16 lanes each: the
+// dependent chain (left keypoint -> row offsets -> row list -> right keypoint -> descriptor)
+// is paid once per batch instead of once per keypoint.
+#define ST_MG 4
 
 __global__ __launch_bounds__(256) void k_stereo_match(StereoGeom G,
                                                      const orbg_keypoint *__restrict__ kps,
@@ -174,17 +136,54 @@ __global__ __launch_bounds__(256) void k_stereo_match(StereoGeom G,
                                                      const int16_t *__restrict__ row_list,
                                                      int32_t *__restrict__ best_r)
 {
+    static_assert(ST_MG == 4, "16 lanes per keypoint");
     // XCD-aware: the workgroups of one pair run on one XCD, so the right frame's keypoint and
     // descriptor rows they share are fetched into one L2 (not once per XCD)
     const int id = ORBG_ST_XCD ? xcd_remap(blockIdx.x + gridDim.x * blockIdx.y, gridDim.x * gridDim.y)
                                : (int)(blockIdx.x + gridDim.x * blockIdx.y);
     const int p = id / gridDim.x, bx = id - p * gridDim.x;
-    const int lane = threadIdx.x & 63;
+    const int lane = threadIdx.x & 63, j = lane >> 4, q16 = lane & 15;
     const int fl = left[p], fr = right[p];
     const int nl = counts[fl];
-    for (int iL = bx * 4 + (threadIdx.x >> 6); iL < nl; iL += ST_WAVES)
-        stereo_match_one(G, kps, desc, fl, fr, iL, lane, p, row_off, row_list,
-                         best_r + (size_t)p * G.fc);
+    const int32_t *off = row_off + (size_t)p * (ST_MAX_ROWS + 1);
+    const orbg_keypoint *kr = kps + (size_t)fr * G.fc;
+    const uint8_t *dr = desc + (size_t)fr * G.fc * 32;
+    const int16_t *list = row_list + (size_t)p * G.list_cap;
+    int32_t *out = best_r + (size_t)p * G.fc;
+    for (int base = bx * 4 + (threadIdx.x >> 6); base < nl; base += ST_MG * ST_WAVES) {
+        const int iL = base + j * ST_WAVES;
+        const bool have = iL < nl;
+        const orbg_keypoint kl = kps[(size_t)fl * G.fc + (have ? iL : base)];
+        const int row = (int)kl.y;
+        const float minU = kl.x - G.max_d, maxU = kl.x - 0.0f;
+        int c0 = 0, c1 = 0;
+        if (have && row >= 0 && row < G.h && !(maxU < 0)) {
+            c0 = off[row];
+            c1 = min(off[row + 1], G.list_cap);
+        }
+        const uint4 *qd = (const uint4 *)(desc + ((size_t)fl * G.fc + (have ? iL : base)) * 32);
+        const uint4 q0 = qd[0], q1 = qd[1];
+        uint32_t best = 0xFFFFFFFFu;
+        for (int c = c0 + q16; c < c1; c += 16) {
+            const int iR = list[c];
+            const orbg_keypoint k = kr[iR];
+            if (k.octave < kl.octave - 1 || k.octave > kl.octave + 1) continue;
+            if (!(k.x >= minU && k.x <= maxU)) continue;
+            const uint4 *d = (const uint4 *)(dr + (size_t)iR * 32);
+            const uint4 d0 = d[0], d1 = d[1];
+            const uint32_t dist = __popc(q0.x ^ d0.x) + __popc(q0.y ^ d0.y) + __popc(q0.z ^ d0.z) +
+                                  __popc(q0.w ^ d0.w) + __popc(q1.x ^ d1.x) + __popc(q1.y ^ d1.y) +
+                                  __popc(q1.z ^ d1.z) + __popc(q1.w ^ d1.w);
+            best = min(best, (dist << 16) | (uint32_t)iR);
+        }
+#pragma unroll
+        for (int o = 8; o > 0; o >>= 1) best = min(best, (uint32_t)__shfl_xor((int)best, o, 64));
+        if (q16 == 0 && have) {
+            const int bestDist = best == 0xFFFFFFFFu ? ST_TH_HIGH : (int)(best >> 16);
+            // the reference keeps a candidate only below TH_HIGH, then needs < (TH_HIGH+TH_LOW)/2
+            out[iL] = (bestDist < ST_TH_HIGH && bestDist < ST_TH_ORB) ? (int)(best & 0xFFFF) : -1;
+        }
+    }
 }
 
 // ---- SAD refinement -----------------------------------------------------------------
