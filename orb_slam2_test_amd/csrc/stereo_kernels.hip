@@ -124,7 +124,10 @@ __global__ __launch_bounds__(ST_ROWS_T) void k_stereo_rows(StereoGeom G,
 // A wave matches ST_MG left keypoints at once (iL = base + j * ST_WAVES), 16 lanes each: the
 // dependent chain (left keypoint -> row offsets -> row list -> right keypoint -> descriptor)
 // is paid once per batch instead of once per keypoint.
-#define ST_MG 4
+#ifndef ST_MG
+#define ST_MG 4  // keypoints per wave batch (2: -, 8: - per A/B)
+#endif
+#define ST_LPK (64 / ST_MG)  // lanes per keypoint
 
 __global__ __launch_bounds__(256) void k_stereo_match(StereoGeom G,
                                                      const orbg_keypoint *__restrict__ kps,
@@ -136,13 +139,13 @@ __global__ __launch_bounds__(256) void k_stereo_match(StereoGeom G,
                                                      const int16_t *__restrict__ row_list,
                                                      int32_t *__restrict__ best_r)
 {
-    static_assert(ST_MG == 4, "16 lanes per keypoint");
+    static_assert(ST_MG == 2 || ST_MG == 4 || ST_MG == 8, "lanes per keypoint: 32, 16 or 8");
     // XCD-aware: the workgroups of one pair run on one XCD, so the right frame's keypoint and
     // descriptor rows they share are fetched into one L2 (not once per XCD)
     const int id = ORBG_ST_XCD ? xcd_remap(blockIdx.x + gridDim.x * blockIdx.y, gridDim.x * gridDim.y)
                                : (int)(blockIdx.x + gridDim.x * blockIdx.y);
     const int p = id / gridDim.x, bx = id - p * gridDim.x;
-    const int lane = threadIdx.x & 63, j = lane >> 4, q16 = lane & 15;
+    const int lane = threadIdx.x & 63, j = lane / ST_LPK, q16 = lane % ST_LPK;
     const int fl = left[p], fr = right[p];
     const int nl = counts[fl];
     const int32_t *off = row_off + (size_t)p * (ST_MAX_ROWS + 1);
@@ -164,7 +167,7 @@ __global__ __launch_bounds__(256) void k_stereo_match(StereoGeom G,
         const uint4 *qd = (const uint4 *)(desc + ((size_t)fl * G.fc + (have ? iL : base)) * 32);
         const uint4 q0 = qd[0], q1 = qd[1];
         uint32_t best = 0xFFFFFFFFu;
-        for (int c = c0 + q16; c < c1; c += 16) {
+        for (int c = c0 + q16; c < c1; c += ST_LPK) {
             const int iR = list[c];
             const orbg_keypoint k = kr[iR];
             if (k.octave < kl.octave - 1 || k.octave > kl.octave + 1) continue;
@@ -177,7 +180,7 @@ __global__ __launch_bounds__(256) void k_stereo_match(StereoGeom G,
             best = min(best, (dist << 16) | (uint32_t)iR);
         }
 #pragma unroll
-        for (int o = 8; o > 0; o >>= 1) best = min(best, (uint32_t)__shfl_xor((int)best, o, 64));
+        for (int o = ST_LPK / 2; o > 0; o >>= 1) best = min(best, (uint32_t)__shfl_xor((int)best, o, 64));
         if (q16 == 0 && have) {
             const int bestDist = best == 0xFFFFFFFFu ? ST_TH_HIGH : (int)(best >> 16);
             // the reference keeps a candidate only below TH_HIGH, then needs < (TH_HIGH+TH_LOW)/2
