@@ -125,7 +125,7 @@ __global__ __launch_bounds__(ST_ROWS_T) void k_stereo_rows(StereoGeom G,
 // dependent chain (left keypoint -> row offsets -> row list -> right keypoint -> descriptor)
 // is paid once per batch instead of once per keypoint.
 #ifndef ST_MG
-#define ST_MG 4  // keypoints per wave batch (2: -, 8: - per A/B)
+#define ST_MG 4  // keypoints per wave batch (measured: 2 -> 0.371 ms, 8 -> 0.444 against 0.327)
 #endif
 #define ST_LPK (64 / ST_MG)  // lanes per keypoint
 
