@@ -238,7 +238,7 @@ def main():
                          "cost of a step's dependent launches spread over more frames (512: "
                          "-2.5%%, 2048: -1%% frames/s)")
     ap.add_argument("--blocks", type=int, default=4,
-                    help="distinct resident input blocks the steps cycle through (4 x 239 MB "
+                    help="distinct resident input blocks the steps cycle through (4 x 478 MB "
                          "> the 256 MB Infinity Cache: every step reads new frames); 1 = the "
                          "same block every step (round 2's bench)")
     ap.add_argument("--cpu-threads", type=int, default=0,
@@ -279,7 +279,7 @@ def main():
     B = args.batch or sequence.BENCH_BATCH["stereo" if args.stereo else
                                            "extract" if args.extract_only else "mono"]
     # Streamed input: the step cycles through `nblocks` distinct resident blocks of the
-    # sequence (nblocks x 239 MB > the 256 MB Infinity Cache at the defaults), so every step
+    # sequence (nblocks x 478 MB > the 256 MB Infinity Cache at the defaults), so every step
     # reads frames the previous steps did not (no cross-step cache reuse of the input).
     nblocks = max(1, args.blocks)
     if args.stereo:
