@@ -35,6 +35,12 @@ void prof_end(void *prof, hipStream_t s, const char *n, hipEvent_t a);
 #ifndef ORBG_ST_XCD
 #define ORBG_ST_XCD 1  // XCD-aware pair mapping of k_stereo_match / k_stereo_sad (0: A/B)
 #endif
+#ifndef ORBG_ST_SADW
+#define ORBG_ST_SADW 1  // k_stereo_sad rows read as dwords, v_sad_u16 (0: byte reads, A/B)
+#endif
+#ifndef ORBG_ST_STG16
+#define ORBG_ST_STG16 0  // k_stereo_sad staging: 16-byte loads on 33 lanes (0: dword per lane)
+#endif
 #define ST_TH_HIGH 100
 #define ST_TH_ORB ((100 + 50) / 2)
 #define ST_W 5
@@ -240,6 +246,26 @@ __device__ __forceinline__ void stereo_sad_one(const StereoGeom &G,
     // stage the 11x11 left patch (columns xl-5..xl+5) and the 11x21 right strip (xr-10..xr+10)
     // as 4 / 7 aligned dwords per row (per-row alignment: the level-0 pitch may be odd)
     uint32_t *stL = stagew, *stR = stagew + 11 * 4;
+#if ORBG_ST_STG16
+    // one 16-byte load per lane, 33 lanes: (row, part) = left dwords 0-3, right dwords 0-3,
+    // right dwords 3-6 (dword 3 stored twice, the same value)
+    if (lane < 33) {
+        const int r = lane / 3, c = lane - 3 * r;
+        const int y = yl - ST_W + r;
+        const uint8_t *src = c == 0 ? IL + (int64_t)y * lp + xl - ST_W
+                                    : IR + (int64_t)y * rp + xr - 2 * ST_W;
+        const int sh = (int)((uintptr_t)src & 3);
+        const int d0 = c == 2 ? 3 : 0;
+        const uint4 v = *(const uint4 *)((const uint32_t *)(src - sh) + d0);
+        uint32_t *dst = (c == 0 ? stL + r * 4 : stR + r * 7) + d0;
+        dst[0] = v.x;
+        dst[1] = v.y;
+        dst[2] = v.z;
+        dst[3] = v.w;
+        if (c == 0) shlw[r] = sh;
+        if (c == 1) shrw[r] = sh;
+    }
+#else
     for (int t = lane; t < 11 * 11; t += 64) {
         const int r = t / 11, c = t - r * 11;  // c < 4: left dword, else right dword c - 4
         const int y = yl - ST_W + r;
@@ -255,6 +281,7 @@ __device__ __forceinline__ void stereo_sad_one(const StereoGeom &G,
         if (c == 0) shlw[r] = (int)((uintptr_t)src & 3);
         if (c == 4) shrw[r] = (int)((uintptr_t)src & 3);
     }
+#endif
     if (lane < 2 * ST_L + 1) sadw[lane] = 0;
     wave_sync_lds();
     const uint8_t *bL = (const uint8_t *)stL, *bR = (const uint8_t *)stR;
@@ -263,12 +290,44 @@ __device__ __forceinline__ void stereo_sad_one(const StereoGeom &G,
     for (int t = lane; t < (2 * ST_L + 1) * (2 * ST_W + 1); t += 64) {
         const int inc = t / (2 * ST_W + 1) - ST_L, dy = t % (2 * ST_W + 1);
         const int cr = bR[ST_W * 28 + shrw[ST_W] + 2 * ST_W + inc];
+#if ORBG_ST_SADW
+        // |(a - cl) - (b - cr)| = |(a + cr) - (b + cl)|: the row's 11 bytes as dwords (4 LDS
+        // reads per side instead of 11 byte reads: the byte reads made k_stereo_sad LDS-bound),
+        // aligned by v_alignbyte, two pixels per v_sad_u16 on u16 lanes (a + cr <= 510: the
+        // 32-bit add of (cr, cr) cannot carry between the lanes); byte 11 is not in the row
+        const int ls = shlw[dy];
+        const int s = shrw[dy] + ST_L + inc;  // right row byte offset, 0 .. 13
+        const uint32_t *la = stL + dy * 4, *ra = stR + dy * 7 + (s >> 2);
+        uint32_t Lw[4], Rw[4];
+#pragma unroll
+        for (int k = 0; k < 4; k++) {
+            Lw[k] = la[k];
+            Rw[k] = ra[k];
+        }
+        const uint32_t cr2 = (uint32_t)cr * 0x10001u, cl2 = (uint32_t)cl * 0x10001u;
+        uint32_t sacc = 0;
+#pragma unroll
+        for (int j = 0; j < 3; j++) {
+            const uint32_t A = __builtin_amdgcn_alignbyte(Lw[j + 1], Lw[j], ls);
+            const uint32_t B = __builtin_amdgcn_alignbyte(Rw[j + 1], Rw[j], s & 3);
+            sacc = __builtin_amdgcn_sad_u16(__builtin_amdgcn_perm(A, A, 0x0c010c00u) + cr2,
+                                            __builtin_amdgcn_perm(B, B, 0x0c010c00u) + cl2, sacc);
+            if (j < 2)
+                sacc = __builtin_amdgcn_sad_u16(__builtin_amdgcn_perm(A, A, 0x0c030c02u) + cr2,
+                                                __builtin_amdgcn_perm(B, B, 0x0c030c02u) + cl2, sacc);
+            else  // byte 10 only
+                sacc = __builtin_amdgcn_sad_u16(__builtin_amdgcn_perm(A, A, 0x0c0c0c02u) + (uint32_t)cr,
+                                                __builtin_amdgcn_perm(B, B, 0x0c0c0c02u) + (uint32_t)cl, sacc);
+        }
+        atomicAdd(&sadw[inc + ST_L], (int)sacc);
+#else
         const uint8_t *a = bL + dy * 16 + shlw[dy];
         const uint8_t *b = bR + dy * 28 + shrw[dy] + ST_L + inc;
         int s = 0;
 #pragma unroll
         for (int dx = 0; dx < 2 * ST_W + 1; dx++) s += abs((a[dx] - cl) - (b[dx] - cr));
         atomicAdd(&sadw[inc + ST_L], s);
+#endif
     }
     wave_sync_lds();
     if (lane != 0) return;
