@@ -39,7 +39,7 @@ void prof_end(void *prof, hipStream_t s, const char *n, hipEvent_t a);
 #define ORBG_ST_SADW 1  // k_stereo_sad rows read as dwords, v_sad_u16 (0: byte reads, A/B)
 #endif
 #ifndef ORBG_ST_STG16
-#define ORBG_ST_STG16 0  // k_stereo_sad staging: 16-byte loads on 33 lanes (0: dword per lane)
+#define ORBG_ST_STG16 1  // k_stereo_sad staging: 16-byte loads on 33 lanes (0: dword per lane, +17% stereo_sad)
 #endif
 #define ST_TH_HIGH 100
 #define ST_TH_ORB ((100 + 50) / 2)
