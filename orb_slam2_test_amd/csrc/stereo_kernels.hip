@@ -126,6 +126,9 @@ __global__ __launch_bounds__(ST_ROWS_T) void k_stereo_rows(StereoGeom G,
 // (dist << 16 | iR) -- the lexicographic (distance, index) minimum.  ST_WAVES waves per pair
 // walk the left keypoints.
 #define ST_WAVES 512
+#ifndef ST_SAD_WAVES
+#define ST_SAD_WAVES ST_WAVES  // waves per pair of k_stereo_sad
+#endif
 
 // A wave matches ST_MG left keypoints at once (iL = base + j * ST_WAVES), 16 lanes each: the
 // dependent chain (left keypoint -> row offsets -> row list -> right keypoint -> descriptor)
@@ -382,7 +385,7 @@ __global__ __launch_bounds__(256) void k_stereo_sad(StereoGeom G,
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
     const int fl = left[p], fr = right[p];
     const int nl = counts[fl];
-    for (int iL = bx * 4 + wv; iL < nl; iL += ST_WAVES) {
+    for (int iL = bx * 4 + wv; iL < nl; iL += ST_SAD_WAVES) {
         stereo_sad_one(G, kps, best_r, img0, img_fs, img_pitch, pyr, pyr_frame, uright, depth,
                        sad_out, p, fl, fr, iL, lane, sad[wv], stage[wv], shl[wv], shr[wv]);
         wave_sync_lds();  // the next keypoint reuses this wave's LDS
@@ -515,7 +518,7 @@ int launch_stereo(hipStream_t st, const OrbgGeom &g, const orbg_keypoint *kps,
                        desc, counts, d_left, d_right, row_off, row_list, best_r);
     prof_end(prof, st, "stereo_match", a);
     prof_begin(prof, st, "stereo_sad", &a);
-    hipLaunchKernelGGL(k_stereo_sad, dim3(ST_WAVES / 4, npairs), dim3(256), 0, st, G, kps,
+    hipLaunchKernelGGL(k_stereo_sad, dim3(ST_SAD_WAVES / 4, npairs), dim3(256), 0, st, G, kps,
                        counts, d_left, d_right, best_r, img0, img_fs, img_pitch, pyr,
                        g.pyr_frame, uright, depth, sad);
     prof_end(prof, st, "stereo_sad", a);
