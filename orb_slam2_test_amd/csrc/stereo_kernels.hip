@@ -126,8 +126,11 @@ __global__ __launch_bounds__(ST_ROWS_T) void k_stereo_rows(StereoGeom G,
 // (dist << 16 | iR) -- the lexicographic (distance, index) minimum.  ST_WAVES waves per pair
 // walk the left keypoints.
 #define ST_WAVES 512
+#ifndef ST_MATCH_WAVES
+#define ST_MATCH_WAVES ST_WAVES  // waves per pair of k_stereo_match
+#endif
 #ifndef ST_SAD_WAVES
-#define ST_SAD_WAVES ST_WAVES  // waves per pair of k_stereo_sad
+#define ST_SAD_WAVES 256  // waves per pair of k_stereo_sad (512: +3%, 128: tie, 64: +1.5%)
 #endif
 
 // A wave matches ST_MG left keypoints at once (iL = base + j * ST_WAVES), 16 lanes each: the
@@ -162,8 +165,8 @@ __global__ __launch_bounds__(256) void k_stereo_match(StereoGeom G,
     const uint8_t *dr = desc + (size_t)fr * G.fc * 32;
     const int16_t *list = row_list + (size_t)p * G.list_cap;
     int32_t *out = best_r + (size_t)p * G.fc;
-    for (int base = bx * 4 + (threadIdx.x >> 6); base < nl; base += ST_MG * ST_WAVES) {
-        const int iL = base + j * ST_WAVES;
+    for (int base = bx * 4 + (threadIdx.x >> 6); base < nl; base += ST_MG * ST_MATCH_WAVES) {
+        const int iL = base + j * ST_MATCH_WAVES;
         const bool have = iL < nl;
         const orbg_keypoint kl = kps[(size_t)fl * G.fc + (have ? iL : base)];
         const int row = (int)kl.y;
@@ -514,7 +517,7 @@ int launch_stereo(hipStream_t st, const OrbgGeom &g, const orbg_keypoint *kps,
                        d_right, row_off, row_list);
     prof_end(prof, st, "stereo_rows", a);
     prof_begin(prof, st, "stereo_match", &a);
-    hipLaunchKernelGGL(k_stereo_match, dim3(ST_WAVES / 4, npairs), dim3(256), 0, st, G, kps,
+    hipLaunchKernelGGL(k_stereo_match, dim3(ST_MATCH_WAVES / 4, npairs), dim3(256), 0, st, G, kps,
                        desc, counts, d_left, d_right, row_off, row_list, best_r);
     prof_end(prof, st, "stereo_match", a);
     prof_begin(prof, st, "stereo_sad", &a);
