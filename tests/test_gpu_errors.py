@@ -110,6 +110,7 @@ def test_stale_match_outputs_rejected():
             call()
         assert ei.value.code == _lib.ORBG_EINVAL
     summary = torch.full((8,), -7, dtype=torch.int32, device="cuda")
+    torch.cuda.synchronize()  # the fill (torch's stream) before the summary (context stream)
     ext.ctx.batch_summary(summary.data_ptr())
     ext.ctx.sync()
     s = summary.cpu().numpy()

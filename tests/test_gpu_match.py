@@ -184,6 +184,7 @@ def test_batch_match_device(oracle):
         assert np.array_equal(m12[:len(ka)], rm12)
     # the summary used by the bench's RCCL gather
     out = torch.zeros(2 * B, dtype=torch.int32, device="cuda")
+    torch.cuda.synchronize()  # the fill (torch's stream) before the summary (context stream)
     ext.ctx.batch_summary(out.data_ptr())
     ext.ctx.sync()
     s = out.cpu().numpy()

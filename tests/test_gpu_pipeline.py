@@ -61,6 +61,9 @@ def _run(frames_list, B, pipelined):
             "m12": torch.zeros((B - 1) * fc, dtype=torch.int32, device="cuda"),
             "summary": torch.zeros(2 * B, dtype=torch.int32, device="cuda"),
         }
+        # the zero fills run on torch's stream, and the context's streams are non-blocking
+        # (no implicit order with it): finish them before the match-stream copies
+        torch.cuda.current_stream().synchronize()
         ms = ext.ctx.match_stream()
         # on the match stream after this batch's matching, before orbg_batch_summary
         # records the slot's "no longer read" event
