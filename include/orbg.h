@@ -231,7 +231,9 @@ int orbg_get_pipeline(const orbg_ctx *ctx);
  * Synchronises. */
 int orbg_set_serial(orbg_ctx *ctx, int enable);
 /* per-frame trajectory summary of the last batch, written on the match stream into a
- * device buffer (order readers after orbg_match_stream, or orbg_sync): d_out[f] = keypoints of frame f (f < nframes), then
+ * device buffer (order readers after orbg_match_stream, or orbg_sync; the context's streams
+ * are non-blocking, so work the caller queued on d_out, e.g. a fill on another stream, must
+ * be complete first): d_out[f] = keypoints of frame f (f < nframes), then
  * d_out[nframes + p] = SearchForInitialization matches of pair p (p < npairs of the last
  * orbg_match_batch_device, 0 if none) */
 int orbg_batch_summary(orbg_ctx *ctx, int32_t *d_out);
