@@ -257,6 +257,10 @@ def main():
                     help="configs[3]: stereo frames (extract L+R + ComputeStereoMatches)")
     ap.add_argument("--extract-only", action="store_true",
                     help="configs[1] (C2): ORBextractor only, no matching")
+    ap.add_argument("--with-pose", action="store_true",
+                    help="mono: the full batched-sequence step, with the pose/trajectory stub "
+                         "of every pair (orbg_match_pose_batch_device) gathered beside the "
+                         "summary and vnMatches12 rows (SURVEY.md 8e); not the headline metric")
     args = ap.parse_args()
 
     import torch
@@ -312,7 +316,7 @@ def main():
     if args.serial:  # PMC runs (tools/round_prof.sh): one dispatch per kernel and step
         ext.ctx.set_serial(True)
     mode = "stereo" if args.stereo else "extract" if args.extract_only else "mono"
-    bstep = sequence.BenchStep(ext, B, mode, world=world)
+    bstep = sequence.BenchStep(ext, B, mode, world=world, with_pose=args.with_pose)
     torch.cuda.synchronize()
     it = [0]
 
@@ -430,6 +434,9 @@ def main():
         else:
             workload = ("C3 KITTI03-shaped mono 1241x376, 2000 feat, 8 lvl: ORBextractor + "
                         "Hamming knn2 (t vs t-1) + SearchForInitialization(w=100, 0.9, checkOri)")
+            if args.with_pose:
+                workload += (" + pose stub (PoseOptimization over the matches, 10 m "
+                             "back-projection) gathered with the summary")
         out = {
             "metric": (METRIC_STEREO if args.stereo else
                        METRIC_EXTRACT if args.extract_only else METRIC), "value": round(value, 2),

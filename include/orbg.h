@@ -230,10 +230,15 @@ int orbg_get_pipeline(const orbg_ctx *ctx);
  * internal streams), so per-kernel event times are the kernels' own.  Outputs unchanged.
  * Synchronises. */
 int orbg_set_serial(orbg_ctx *ctx, int enable);
-/* per-frame trajectory summary of the last batch, written on the match stream into a
- * device buffer (order readers after orbg_match_stream, or orbg_sync; the context's streams
- * are non-blocking, so work the caller queued on d_out, e.g. a fill on another stream, must
- * be complete first): d_out[f] = keypoints of frame f (f < nframes), then
+/* Caller buffers written on the match stream (orbg_batch_summary, orbg_batch_matches,
+ * orbg_match_pose_batch_device, orbg_stereo_summary) are stream-ordered on the writer side:
+ * at entry each records an event on the context stream (orbg_set_stream) and the match
+ * stream waits for it, so work the caller queued on the context stream before the call (a
+ * fill of d_out, an upload) completes before liborbg writes.  Work on any OTHER stream must
+ * be ordered by the caller.  Readers order themselves after orbg_match_stream, or orbg_sync.
+ *
+ * per-frame trajectory summary of the last batch, written on the match stream into a
+ * device buffer: d_out[f] = keypoints of frame f (f < nframes), then
  * d_out[nframes + p] = SearchForInitialization matches of pair p (p < npairs of the last
  * orbg_match_batch_device, 0 if none) */
 int orbg_batch_summary(orbg_ctx *ctx, int32_t *d_out);
@@ -243,7 +248,8 @@ int orbg_batch_summary(orbg_ctx *ctx, int32_t *d_out);
  *   orbg_batch_acquire: `stream` waits until those outputs are written;
  *   orbg_batch_release: every read enqueued on `stream` so far finishes before liborbg
  *   overwrites those outputs (the extraction that reuses the output slot, the next stereo
- *   pass wait for it).
+ *   pass wait for it).  Releases on several reader streams of one batch chain: each waits
+ *   for the previous release, so the slot waits for every reader.
  * Enqueue only; no host synchronisation. */
 int orbg_batch_acquire(orbg_ctx *ctx, void *stream);
 int orbg_batch_release(orbg_ctx *ctx, void *stream);

@@ -44,6 +44,12 @@ int blur2_tw();
 hipError_t launch_blur2(hipStream_t st, const OrbgGeom *g, const int32_t *task_base,
                         const uint8_t *img0, int64_t img_fs, int img_pitch, const uint8_t *pyr,
                         uint8_t *blur, int t_begin, int t_count, int nframes);
+// fast_rows_kernels.hip
+int fast_rows_wave_bytes();
+hipError_t launch_fast_rows(hipStream_t st, const OrbgGeom *g, const OrbgFastTile *tiles,
+                            const uint8_t *img0, int64_t img_fs, int img_pitch,
+                            const uint8_t *pyr, const uint32_t *ctab, int32_t *cell_cnt,
+                            uint2 *cell_kp, int nframes, int t_begin, int t_count);
 hipError_t launch_fast2(int p4, size_t lds, hipStream_t st, const OrbgGeom *g,
                         const OrbgCell *cells, const uint8_t *img0, int64_t img_fs,
                         int img_pitch, const uint8_t *pyr, const uint32_t *ctab,
@@ -284,6 +290,11 @@ struct orbg_ctx {
     // slot's next extraction / the next stereo pass waits for them
     hipEvent_t ev_rel[2] = {nullptr, nullptr}, ev_srel = nullptr;
     bool rel_pending[2] = {false, false}, srel_pending = false;
+    // entry points that write caller buffers on `mstream` (orbg_batch_summary /
+    // orbg_batch_matches / orbg_match_pose_batch_device / orbg_stereo_summary) first order
+    // `mstream` after the work queued on the context stream so far (ev_caller): a fill the
+    // caller queued there before the call can never land after liborbg's write
+    hipEvent_t ev_caller = nullptr;
     hipEvent_t ev_cells[2] = {nullptr, nullptr}, ev_front[2] = {nullptr, nullptr};
     hipEvent_t ev_back[2] = {nullptr, nullptr};
     bool back_pending[2] = {false, false};
@@ -304,6 +315,13 @@ struct orbg_ctx {
     OrbgGeom geom{};
     std::vector<OrbgCell> cells;
     std::vector<int32_t> tile_base;  // k_blur2 tile bases (L + 1)
+    // k_fast_rows strips (fast_rows_kernels.hip): fr_ok = every level's cells fit a strip
+    // (wCell <= 32); ftile_base[l] = first strip of level l (L + 1 entries); fr_mode 0 forces
+    // k_fast2 (ORBG_FAST_ROWS=0, developer A/B)
+    OrbgFastTile *d_ftiles = nullptr;
+    std::vector<int32_t> ftile_base;
+    bool fr_ok = false;
+    int fr_mode = 0;  // k_fast_rows opt-in (ORBG_FAST_ROWS=1) until it beats k_fast2
     OctLdsDims oct_dims[2] = {};
     // device
     OrbgGeom *d_geom = nullptr;
@@ -445,7 +463,7 @@ static void free_plan(orbg_ctx *c)
     for (hipEvent_t e : {c->ev_rel[0], c->ev_rel[1], c->ev_srel, c->ev_ssum})
         if (e) hipEventSynchronize(e);  // caller streams may still read the outputs
     c->rel_pending[0] = c->rel_pending[1] = c->srel_pending = c->ssum_pending = false;
-    void *ptrs[] = {c->d_geom, c->d_cells, c->d_tile_base, c->d_rtab, c->d_ctab, c->d_odtab,
+    void *ptrs[] = {c->d_geom, c->d_cells, c->d_ftiles, c->d_tile_base, c->d_rtab, c->d_ctab, c->d_odtab,
                     c->pyr_slot[0], c->pyr_slot[1], c->blur_slot[0], c->blur_slot[1],
                     c->cnt_slot[0], c->cnt_slot[1], c->ckp_slot[0], c->ckp_slot[1], c->d_keys, c->d_knode, c->d_act, c->d_qk,
                     c->d_nodes, c->d_lvl_kp, c->d_lvl_cnt, c->kps_slot[0], c->kps_slot[1],
@@ -457,6 +475,9 @@ static void free_plan(orbg_ctx *c)
         if (q) hipFree(q);
     c->d_geom = nullptr;
     c->d_cells = nullptr;
+    c->d_ftiles = nullptr;
+    c->ftile_base.clear();
+    c->fr_ok = false;
     c->d_tile_base = nullptr;
     c->d_rtab = nullptr;
     c->d_ptab = nullptr;
@@ -887,6 +908,42 @@ static int plan(orbg_ctx *c, int w, int h, int batch)
     tile_base = blur2_base;
     G.ncells = (int)cells.size();
     G.cell_cap = cell_cap;
+    // k_fast_rows strips: consecutive cells of one cell row, at most 8 and 256 px of region
+    // (lane l owns strip pixels 4l .. 4l+3); every level needs wCell <= 32 (a cell's bits of a
+    // strip row fit one funnel-shifted dword), else the plan keeps k_fast2
+    std::vector<OrbgFastTile> ftiles;
+    std::vector<int32_t> ftile_base;
+    bool fr_ok = true;
+    for (int l = 0; l < G.L && fr_ok; l++) {
+        const OrbgLevel &L = G.lv[l];
+        if (L.wcell > 32) fr_ok = false;
+        ftile_base.push_back((int)ftiles.size());
+        const int cpt = std::min(8, 256 / std::max(L.wcell, 1));
+        for (int a = L.cell_base; a < L.cell_base + L.ncells && fr_ok;) {
+            int b = a;
+            int tw = 0;
+            while (b < L.cell_base + L.ncells && b - a < cpt && cells[b].ci == cells[a].ci) {
+                tw += cells[b].w - 6;
+                b++;
+            }
+            OrbgFastTile t{};
+            t.level = (int16_t)l;
+            t.ncell = (int16_t)(b - a);
+            t.c0 = a;
+            t.x0 = cells[a].x0;
+            t.y0 = cells[a].y0;
+            t.h = cells[a].h;
+            t.tw = (int16_t)tw;
+            if (tw > 256 || cells[a].h < 7 || cells[a].h - 6 > 64) fr_ok = false;  // region rows: one path code per lane
+            for (int k = a; k < b; k++)
+                if (cells[k].h != cells[a].h || cells[k].y0 != cells[a].y0 ||
+                    cells[k].x0 != cells[a].x0 + (k - a) * L.wcell || (k + 1 < b && cells[k].w != L.wcell + 6))
+                    fr_ok = false;
+            ftiles.push_back(t);
+            a = b;
+        }
+    }
+    ftile_base.push_back((int)ftiles.size());
     {
         int wmax = 0, hmax = 0;
         for (const OrbgCell &cl : cells) {
@@ -1024,6 +1081,10 @@ static int plan(orbg_ctx *c, int w, int h, int batch)
     const std::vector<uint4> odtab = make_od_tab(G.umax);
     const size_t B = (size_t)want_batch;
     int rc;
+    if (fr_ok && (rc = dalloc(&c->d_ftiles, ftiles.size()))) {
+        free_plan(c);
+        return rc;
+    }
     if ((rc = dalloc(&c->d_geom, 1)) || (rc = dalloc(&c->d_cells, cells.size())) ||
         (rc = dalloc(&c->d_ctab, ctab.size())) || (rc = dalloc(&c->d_odtab, odtab.size())) ||
         (rc = dalloc(&c->d_tile_base, tile_base.size())) || (rc = dalloc(&c->d_rtab, rtab.size())) ||
@@ -1057,6 +1118,9 @@ static int plan(orbg_ctx *c, int w, int h, int batch)
     HIPCHK(hipMemcpy(c->d_geom, &G, sizeof(G), hipMemcpyHostToDevice));
     HIPCHK(hipMemcpy(c->d_cells, cells.data(), cells.size() * sizeof(OrbgCell),
                      hipMemcpyHostToDevice));
+    if (fr_ok)
+        HIPCHK(hipMemcpy(c->d_ftiles, ftiles.data(), ftiles.size() * sizeof(OrbgFastTile),
+                         hipMemcpyHostToDevice));
     HIPCHK(hipMemcpy(c->d_tile_base, tile_base.data(), tile_base.size() * sizeof(int32_t),
                      hipMemcpyHostToDevice));
     if (!rtab.empty())
@@ -1101,6 +1165,8 @@ static int plan(orbg_ctx *c, int w, int h, int batch)
     c->geom = G;
     c->cells = cells;
     c->tile_base = tile_base;
+    c->fr_ok = fr_ok;
+    c->ftile_base = fr_ok ? ftile_base : std::vector<int32_t>();
     c->gw = w;
     c->gh = h;
     c->gbatch = want_batch;
@@ -1225,7 +1291,9 @@ extern "C" int orbg_create(int device, const orbg_params *p, orbg_ctx **out)
     hipEventCreateWithFlags(&c->ev_rel[0], hipEventDisableTiming);
     hipEventCreateWithFlags(&c->ev_rel[1], hipEventDisableTiming);
     hipEventCreateWithFlags(&c->ev_srel, hipEventDisableTiming);
+    hipEventCreateWithFlags(&c->ev_caller, hipEventDisableTiming);
     if (const char *e = getenv("ORBG_PIPELINE")) c->pipelined = atoi(e) && c->ostream;
+    if (const char *e = getenv("ORBG_FAST_ROWS")) c->fr_mode = atoi(e);
 #ifdef ORBG_DEV_KNOBS
     if (getenv("ORBG_SKIP") || getenv("ORBG_DBG"))
         fprintf(stderr, "liborbg (developer build): ORBG_SKIP / ORBG_DBG set -- launches are "
@@ -1235,6 +1303,11 @@ extern "C" int orbg_create(int device, const orbg_params *p, orbg_ctx **out)
         fprintf(stderr, "liborbg: ORBG_SKIP / ORBG_DBG ignored (developer builds only, make "
                         "DEV=1)\n");
 #endif
+    if (const char *fi = getenv("ORBG_FAULT_INJECT"))
+        fprintf(stderr, "liborbg: ORBG_FAULT_INJECT=%s set -- %s\n", fi,
+                strcmp(fi, "octree_overflow") ? "unknown value, ignored"
+                                              : "every quadtree level overflows, extractions fail "
+                                                "with ORBG_ENOTSUP (error-path tests only)");
     *out = c;
     return ORBG_OK;
 }
@@ -1272,7 +1345,8 @@ extern "C" void orbg_destroy(orbg_ctx *c)
     if (c->fstream) hipStreamDestroy(c->fstream);
     if (c->ev_fast) hipEventDestroy(c->ev_fast);
     if (c->ev_oct) hipEventDestroy(c->ev_oct);
-    for (hipEvent_t e : {c->ev_sback, c->ev_ssum, c->ev_rel[0], c->ev_rel[1], c->ev_srel})
+    for (hipEvent_t e : {c->ev_sback, c->ev_ssum, c->ev_rel[0], c->ev_rel[1], c->ev_srel,
+                         c->ev_caller})
         if (e) hipEventDestroy(e);
     if (c->mstream) hipStreamDestroy(c->mstream);
     if (c->own_stream) hipStreamDestroy(c->own_stream);
@@ -1357,12 +1431,24 @@ static hipError_t launch_blur_levels(orbg_ctx *c, hipStream_t st, const uint8_t 
     return e;
 }
 
-// FAST cells [cb, cb + cn) of every frame on `st` (k_fast2, fast_kernels.hip)
+// FAST cells [cb, cb + cn) of every frame on `st`: k_fast_rows over the strips of those
+// levels (fast_rows_kernels.hip), k_fast2 (one wave per cell, fast_kernels.hip) when the plan has
+// no strips or ORBG_FAST_ROWS=0.  cb and cb + cn are level boundaries (a level's cell_base).
 static hipError_t launch_fast_cells(orbg_ctx *c, hipStream_t st, const uint8_t *d_imgs, int B,
                                     int pitch, int64_t fs, int cb, int cn)
 {
     const OrbgGeom &G = c->geom;
     hipError_t e = hipSuccess;
+    if (c->fr_ok && c->fr_mode) {
+        int l0 = 0, l1 = G.L;
+        while (l0 < G.L && G.lv[l0].cell_base < cb) l0++;
+        while (l1 > l0 && G.lv[l1 - 1].cell_base >= cb + cn) l1--;
+        const int t0 = c->ftile_base[l0], t1 = c->ftile_base[l1];
+        PROF_LAUNCH(c, "fast_cells",
+                    e = launch_fast_rows(st, c->d_geom, c->d_ftiles, d_imgs, fs, pitch, c->d_pyr,
+                                         c->d_ctab, c->d_cell_cnt, c->d_cell_kp, B, t0, t1 - t0));
+        return e;
+    }
     PROF_LAUNCH(c, "fast_cells",
                 e = launch_fast2(G.fc2_p4, 4 * G.fc2_wave_bytes, st, c->d_geom, c->d_cells, d_imgs,
                                  fs, pitch, c->d_pyr, c->d_ctab, c->d_cell_cnt, c->d_cell_kp, B,
@@ -1814,10 +1900,19 @@ extern "C" int orbg_batch_stats(orbg_ctx *c, int64_t *ncand, int64_t *nkp)
     return ORBG_OK;
 }
 
+// `mstream` after everything queued on the context stream so far (ev_caller)
+static hipError_t order_after_caller(orbg_ctx *c)
+{
+    hipError_t e = hipEventRecord(c->ev_caller, c->stream);
+    if (e != hipSuccess) return e;
+    return hipStreamWaitEvent(c->mstream, c->ev_caller, 0);
+}
+
 extern "C" int orbg_batch_summary(orbg_ctx *c, int32_t *d_out)
 {
     if (!c || !c->gw || c->last_n <= 0 || !d_out) return set_err(ORBG_EINVAL, "no batch");
     const int s = c->slot;
+    HIPCHK(order_after_caller(c));
     HIPCHK(hipStreamWaitEvent(c->mstream, c->ev_ext[s], 0));
     HIPCHK(hipMemcpyAsync(d_out, c->d_counts, c->last_n * sizeof(int32_t),
                           hipMemcpyDeviceToDevice, c->mstream));
@@ -1843,9 +1938,13 @@ extern "C" int orbg_batch_release(orbg_ctx *c, void *stream)
     if (!c || !c->gw || c->last_n <= 0) return set_err(ORBG_EINVAL, "no batch");
     const hipStream_t q = stream ? (hipStream_t)stream : c->mstream;
     const int s = c->slot;
+    // a second reader stream of the same batch: chain the releases (q waits for the earlier
+    // release's reads, then the one event covers both)
+    if (c->rel_pending[s]) HIPCHK(hipStreamWaitEvent(q, c->ev_rel[s], 0));
     HIPCHK(hipEventRecord(c->ev_rel[s], q));
     c->rel_pending[s] = true;
     if (c->last_nstereo) {
+        if (c->srel_pending) HIPCHK(hipStreamWaitEvent(q, c->ev_srel, 0));
         HIPCHK(hipEventRecord(c->ev_srel, q));
         c->srel_pending = true;
     }
@@ -1859,6 +1958,7 @@ extern "C" int orbg_batch_matches(orbg_ctx *c, int32_t *d_out, int32_t *frame_ca
     if (frame_cap) *frame_cap = c->geom.frame_cap;
     if (!d_out) return ORBG_OK;
     const int s = c->slot;
+    HIPCHK(order_after_caller(c));
     HIPCHK(hipStreamWaitEvent(c->mstream, c->ev_ext[s], 0));
     int rc = launch_match_export(c->mstream, c->d_m12, c->d_pairs, c->d_counts,
                                  c->geom.frame_cap, c->last_npairs, d_out);
@@ -2026,6 +2126,7 @@ extern "C" int orbg_match_pose_batch_device(orbg_ctx *c, const orbg_pose_camera 
     }
     uint8_t *b = (uint8_t *)c->d_mpose;
     const int s = c->slot;
+    HIPCHK(order_after_caller(c));  // d_q / d_t / d_ninliers are the caller's
     HIPCHK(hipStreamWaitEvent(c->mstream, c->ev_ext[s], 0));  // (the matching already does)
     const int rc = launch_match_pose(
         c->mstream, c->d_kps, c->d_counts, (int)fc, c->d_pairs, c->d_pairs + c->pair_cap,
@@ -2127,6 +2228,7 @@ extern "C" int orbg_stereo_summary(orbg_ctx *c, int32_t *d_out)
     // extraction that next rewrites this output slot waits for it (ev_mat), the next stereo
     // pass too (ev_ssum)
     const int s = c->slot;
+    HIPCHK(order_after_caller(c));
     HIPCHK(hipStreamWaitEvent(c->mstream, c->ev_sback, 0));
     hipLaunchKernelGGL(k_stereo_summary, dim3((c->last_nstereo + 255) / 256), dim3(256), 0,
                        c->mstream, c->d_counts, c->d_spairs, c->d_snvalid, c->last_nstereo,

@@ -109,6 +109,14 @@ struct OrbgCell {
     int16_t ci, cj;   // cell row / col (for pt += j*wCell, i*hCell)
 };
 
+// k_fast_rows strip: up to 8 consecutive cells of one cell row of one level (host plan)
+struct OrbgFastTile {
+    int16_t level, ncell;
+    int32_t c0;       // global index of the first cell (a cell row's cells are consecutive)
+    int16_t x0, y0;   // window top-left of the first cell (level coords)
+    int16_t h, tw;    // window rows (region rows + 6), region width (sum of the cells')
+};
+
 static inline __host__ __device__ uint32_t orbg_pack(int x, int y, int s)
 {
     return (uint32_t)x | ((uint32_t)y << 12) | ((uint32_t)s << 24);

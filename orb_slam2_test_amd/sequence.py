@@ -214,12 +214,22 @@ class BenchStep:
     interleaved), Frame::ComputeStereoMatches of every pair (Frame.cc:619-834), the stereo
     summary on the match stream and its all_gather.
 
+    `with_pose` (mono): also the pose/trajectory stub of every pair (orbg_match_pose_batch_device,
+    PoseOptimization over the pair's matches, Optimizer.cc:356-631) into `pose` [B, 8] = (q
+    x y z w, t, inliers), gathered beside the summary and the rows with world > 1 (SURVEY.md
+    8e's third per-frame payload, as run_sharded(with_pose=True)).  BASELINE.json's headline
+    metric is extract + match, so bench.py times it without the stub by default
+    (`bench.py --with-pose` times the full sequence step).
+
+    `group` is the process group of the gathers (None: the default group; the 2-process
+    one-GPU tests run them over gloo).
+
     `capture(step)`, when set (tests), runs on the match stream after the step's outputs
     are written (orbg_batch_acquire) and before liborbg may reuse them
     (orbg_batch_release); the bench leaves it unset."""
 
     def __init__(self, ext, B, mode="mono", world=1, window=100, nnratio=0.9, check_ori=True,
-                 bf=None, min_z=None):
+                 bf=None, min_z=None, with_pose=False, group=None):
         import torch
         from . import synthetic
         if mode not in ("mono", "extract", "stereo"):
@@ -235,6 +245,13 @@ class BenchStep:
         self.summary = torch.zeros(2 * B + 1, dtype=torch.int32, device="cuda")
         self.ssum = torch.zeros(2 * B, dtype=torch.int32, device="cuda")
         self.m12 = None
+        self.with_pose = with_pose and mode == "mono"
+        self.group = group
+        if self.with_pose:
+            self.dq = torch.zeros((B, 4), dtype=torch.float64, device="cuda")
+            self.dt = torch.zeros((B, 3), dtype=torch.float64, device="cuda")
+            self.dn = torch.zeros(B, dtype=torch.int32, device="cuda")
+        self.pose = None
         self.mstream = torch.cuda.ExternalStream(ext.ctx.match_stream())
         self.capture = None
         self.gathered = None
@@ -248,7 +265,7 @@ class BenchStep:
             ext.ctx.stereo_summary(self.ssum.data_ptr())
             if self.world > 1:  # per-frame (keypoints, depths) of every rank
                 with torch.cuda.stream(self.mstream):
-                    self.gathered = gather_summary(self.ssum.view(2, B), self.world,
+                    self.gathered = gather_summary(self.ssum.view(2, B), self.world, self.group,
                                                    sizes=[B] * self.world)
         elif self.mode == "mono":
             ext.match_batch_device(self.f1, self.f2, self.window, self.nnratio, self.check_ori)
@@ -257,11 +274,20 @@ class BenchStep:
                 self.m12 = torch.empty((B, ext.ctx.batch_matches(None)), dtype=torch.int32,
                                        device="cuda")
             ext.ctx.batch_matches(self.m12.data_ptr())  # vnMatches12 rows of the B pairs
+            if self.with_pose:  # pose stub of frame i + 1 from the matches of (i, i + 1)
+                ext.match_pose_batch_device(POSE_CAM, POSE_DEPTH, self.dq.data_ptr(),
+                                            self.dt.data_ptr(), self.dn.data_ptr())
+                with torch.cuda.stream(self.mstream):  # written there (orbg.h)
+                    self.pose = torch.cat([self.dq, self.dt, self.dn.double()[:, None]], 1)
             if self.world > 1:
                 with torch.cuda.stream(self.mstream):
+                    sizes = [B] * self.world
                     local = torch.stack([self.summary[1:B + 1], self.summary[B + 1:]])
-                    self.gathered = (gather_summary(local, self.world, sizes=[B] * self.world),
-                                     gather_rows(self.m12, self.world, sizes=[B] * self.world))
+                    g = [gather_summary(local, self.world, self.group, sizes=sizes),
+                         gather_rows(self.m12, self.world, self.group, sizes=sizes)]
+                    if self.with_pose:
+                        g.append(gather_rows(self.pose, self.world, self.group, sizes=sizes))
+                    self.gathered = tuple(g)
         if self.capture is not None:
             ext.ctx.batch_acquire(self.mstream.cuda_stream)
             with torch.cuda.stream(self.mstream):
