@@ -185,13 +185,15 @@ __global__ __launch_bounds__(256) void k_fast_rows(
         for (int y0g = 0; y0g < RH; y0g += FR_G) {
             int nlist = 0, nboth = 0;
             const int ss_g = ss_next;  // score slot of region row y0g
+            // fully unrolled (the load ring's slots must be static: a dynamic index would cost
+            // a register array in scratch, a rolled loop collapses the ring to one row in flight)
 #pragma unroll
             for (int u = 0; u < FR_G; u++) {
                 const int y = y0g + u;
-                if (y >= RH) break;  // wave-uniform
-                // window row y + 6 arrives (its load slot is static: (y + 6) % 4 == (u + 2) % 4)
+                // window row y + 6 arrives (its load slot is static: (y + 6) % 4 == (u + 2) % 4);
+                // past the last region row the loads are clamped re-reads and no row is tested
                 const int k = (u + 2) % FR_PF;
-                wave_sync_lds();
+                if (y >= RH) continue;  // wave-uniform
                 put(k);
                 issue(y + 6 + FR_PF, k);
                 wave_sync_lds();
