@@ -36,6 +36,8 @@
  *   orbg_bow_transform .............. TemplatedVocabulary::transform(features, BowVector,
  *                                     FeatureVector, levelsup) as Frame::ComputeBoW calls it
  *                                     TemplatedVocabulary.h:1126-1189, 1220-1259; Frame.cc:532-539
+ *   orbg_search_by_bow .............. ORBmatcher::SearchByBoW(KeyFrame*, Frame&, ...)
+ *                                     src/ORBmatcher.cc:195-348 (Tracking.cc:1069, 2009)
  *   orbg_ba_linearize ............... g2o computeActiveErrors + BlockSolver::buildSystem arithmetic
  *                                     for EdgeSE3ProjectXYZ / EdgeStereoSE3ProjectXYZ inside
  *                                     Optimizer::LocalBundleAdjustment  src/Optimizer.cc:633-979
@@ -480,14 +482,24 @@ int orbg_ba_build_system_device(orbg_ctx *ctx, const orbg_pose *d_poses, int npo
  * observations are cv::KeyPoint floats: a graph needs every observation f32-exact (the mono
  * third entry is ignored), at most 256 distinct (fx, fy, cx, cy, bf) and 65536 distinct
  * (inv_sigma2, huber_delta); otherwise ORBG_ENOTSUP, and the record entry points apply.
- * Results are bit-identical to orbg_ba_build_system_device / orbg_ba_errors_device on the
- * same edges.  A graph belongs to the device of the context that created it. */
+ * Per-edge outputs (H_pl, errors) are bit-identical to orbg_ba_build_system_device /
+ * orbg_ba_errors_device on the same edges.  Block sums are deterministic here: every point
+ * block is summed over its edges in edge order (a point whose edges straddle two 256-edge
+ * workgroups is summed by a follow-up pass, no atomics), the oracle's order; a pose block is
+ * the sum over its 64-edge slices in slice order (each slice an MFMA f64 accumulation).  The
+ * record entry points sum a straddling point as two partials and pose slices by fp64
+ * atomics, so those blocks agree with the graph's to rounding, not bit for bit.  The graph
+ * keeps its slice tables, special-point list and pose partials (built once), so a build is
+ * four launches (edges, special points, pose slices, pose reduction) with no zero fills.  A graph belongs to the device of the context that
+ * created it. */
 typedef struct orbg_ba_graph orbg_ba_graph;
 int orbg_ba_graph_create(orbg_ctx *ctx, const orbg_edge *edges, int nedge, int npose,
                          int npoint, orbg_ba_graph **out);
 int orbg_ba_graph_destroy(orbg_ba_graph *graph);
 /* setLevel(1) / setLevel(0) of the outlier pass (Optimizer.cc:871-901): active[e] (host,
- * 0 or 1) for every edge, in the order given at creation; ordered on the context stream. */
+ * 0 or 1) for every edge, in the order given at creation; ordered on the context stream
+ * (uploaded from pinned staging: no host synchronisation beyond waiting for the previous
+ * call's upload). */
 int orbg_ba_graph_set_active(orbg_ctx *ctx, orbg_ba_graph *graph, const uint8_t *active);
 /* buildSystem over the graph: outputs as orbg_ba_build_system_device (d_hpl [nedge][3][6]). */
 int orbg_ba_graph_build_system(orbg_ctx *ctx, orbg_ba_graph *graph, const orbg_pose *d_poses,
@@ -593,6 +605,43 @@ int orbg_bow_transform_batch_device(orbg_ctx *ctx, const orbg_vocab *v, const ui
                                     int32_t *bow_words, double *bow_weights, int32_t *nbow,
                                     int32_t *fv_nodes, int32_t *fv_off, int32_t *fv_feats,
                                     int32_t *nfv, int32_t *word_of, int32_t *node_of);
+
+/* ---------------- ORBmatcher::SearchByBoW(KeyFrame*, Frame&) ---------------- */
+/* One side of SearchByBoW pairs, device memory, in orbg_bow_transform_batch_device's layout
+ * (frame f's rows at + f * cap, fv_off at + f * (cap + 1)): descriptors [cap][32], keypoints
+ * [cap] (only .angle is read: the KeyFrame's mvKeysUn, the Frame's mvKeys), counts[f] = N,
+ * the FeatureVector (fv_nodes / fv_off / fv_feats / nfv) and, on the KeyFrame side, valid
+ * [cap] = "pMP && !pMP->isBad()" of mvpMapPoints (NULL: every feature has a good MapPoint;
+ * ignored on the Frame side). */
+typedef struct {
+    const uint8_t *desc;
+    const orbg_keypoint *kps;
+    const int32_t *counts;
+    const int32_t *fv_nodes, *fv_off, *fv_feats, *nfv;
+    const uint8_t *valid;
+} orbg_bow_frames;
+/* ORBmatcher::SearchByBoW(KeyFrame *pKF, Frame &F, vector<MapPoint*> &vpMapPointMatches)
+ * (src/ORBmatcher.cc:195-348; Tracking::TrackReferenceKeyFrame Tracking.cc:1069,
+ * Relocalization :2009) for pairs p: KeyFrame kf_index[p] of `kf`, Frame f_index[p] of `f`
+ * (device int arrays; the two sides may be the same batch).  match[p * cap + i] = the KeyFrame
+ * feature whose MapPoint matched F's feature i (vpMapPointMatches[i] =
+ * pKF->GetMapPointMatches()[match]), -1 if NULL, for i < N of the frame; nmatch[p] = the
+ * return value.  nnratio = mfNNratio, check_ori = mbCheckOrientation.  On the match stream
+ * (orbg_match_stream), ordered after the context stream (as orbg_batch_summary). */
+int orbg_search_by_bow_batch_device(orbg_ctx *ctx, const orbg_bow_frames *kf,
+                                    const orbg_bow_frames *f, int cap, const int32_t *d_kf_index,
+                                    const int32_t *d_f_index, int npairs, float nnratio,
+                                    int check_ori, int32_t *d_match, int32_t *d_nmatch);
+/* The same for one pair from host arrays: the KeyFrame's n_kf descriptors, mvKeysUn angles
+ * (kf_angle), valid flags (NULL: all) and FeatureVector; the Frame's n_f descriptors, mvKeys
+ * angles and FeatureVector.  match[n_f] as above; *nmatches = the return value. */
+int orbg_search_by_bow(orbg_ctx *ctx, const uint8_t *kf_desc, const float *kf_angle,
+                       const uint8_t *kf_valid, int n_kf, const int32_t *kf_fv_nodes,
+                       const int32_t *kf_fv_off, const int32_t *kf_fv_feats, int kf_nfv,
+                       const uint8_t *f_desc, const float *f_angle, int n_f,
+                       const int32_t *f_fv_nodes, const int32_t *f_fv_off,
+                       const int32_t *f_fv_feats, int f_nfv, float nnratio, int check_ori,
+                       int32_t *match, int *nmatches);
 
 #ifdef __cplusplus
 }

@@ -144,3 +144,88 @@ int orc_bow_transform(const orc_vocab *v, const uint8_t *desc, int n, int levels
     free(pn);
     return m;
 }
+
+/*
+ * ORBmatcher::SearchByBoW(KeyFrame *pKF, Frame &F, vector<MapPoint*> &vpMapPointMatches)
+ * (src/ORBmatcher.cc:195-348; callers Tracking::TrackReferenceKeyFrame Tracking.cc:1069 and
+ * Tracking::Relocalization :2009).  The two FeatureVectors (ascending node ids, per node the
+ * feature indices in feature order) are walked as the reference walks its std::maps: equal
+ * ids are matched, the smaller side jumps to lower_bound of the other's id -- a merge join.
+ * Per common node, in the KF node's feature order: a KF feature whose MapPoint is NULL or bad
+ * (kf_valid[i] == 0) is skipped; otherwise best / second over the node's F features not yet
+ * matched in this call (bestDist1 = bestDist2 = 256, strict <, the first best wins ties); a
+ * match needs bestDist1 <= TH_LOW and (float)bestDist1 < nnratio * (float)bestDist2.  With
+ * check_ori the rotation kp.angle (KF mvKeysUn) - F.mvKeys[best].angle bins as
+ * SearchForInitialization's, and every match outside ComputeThreeMaxima's bins is dropped.
+ * match[i] (F feature i) = the KF feature index whose MapPoint matched it, -1 if none.
+ */
+#define BOW_TH_LOW 50
+
+int orc_search_by_bow(const uint8_t *kf_desc, const float *kf_angle, const uint8_t *kf_valid,
+                      int n_kf, const int32_t *kf_nodes, const int32_t *kf_off,
+                      const int32_t *kf_feats, int kf_nfv, const uint8_t *f_desc,
+                      const float *f_angle, int n_f, const int32_t *f_nodes, const int32_t *f_off,
+                      const int32_t *f_feats, int f_nfv, float nnratio, int check_ori,
+                      int32_t *match)
+{
+    (void)n_kf;
+    for (int i = 0; i < n_f; i++) match[i] = -1;
+    int *bins = (int *)malloc(sizeof(int) * (n_f > 0 ? n_f : 1));
+    int hsize[30] = {0};
+    const float factor = 1.0f / 30;
+    int nmatches = 0;
+    int a = 0, b = 0;
+    while (a < kf_nfv && b < f_nfv) {
+        if (kf_nodes[a] == f_nodes[b]) {
+            for (int ik = kf_off[a]; ik < kf_off[a + 1]; ik++) {
+                const int realKF = kf_feats[ik];
+                if (!kf_valid[realKF]) continue;
+                const uint8_t *dKF = kf_desc + (size_t)realKF * 32;
+                int best1 = 256, bestIdx = -1, best2 = 256;
+                for (int jf = f_off[b]; jf < f_off[b + 1]; jf++) {
+                    const int realF = f_feats[jf];
+                    if (match[realF] >= 0) continue;
+                    const int d = orc_descriptor_distance(dKF, f_desc + (size_t)realF * 32);
+                    if (d < best1) {
+                        best2 = best1;
+                        best1 = d;
+                        bestIdx = realF;
+                    } else if (d < best2) {
+                        best2 = d;
+                    }
+                }
+                if (best1 <= BOW_TH_LOW && (float)best1 < nnratio * (float)best2) {
+                    match[bestIdx] = realKF;
+                    if (check_ori) {
+                        float rot = kf_angle[realKF] - f_angle[bestIdx];
+                        if (rot < 0.0)
+                            rot += 360.0f;
+                        int bin = (int)roundf(rot * factor);
+                        if (bin == 30)
+                            bin = 0;
+                        bins[bestIdx] = bin;
+                        hsize[bin]++;
+                    }
+                    nmatches++;
+                }
+            }
+            a++;
+            b++;
+        } else if (kf_nodes[a] < f_nodes[b]) {
+            a++;
+        } else {
+            b++;
+        }
+    }
+    if (check_ori) {
+        int ind1 = -1, ind2 = -1, ind3 = -1;
+        orc_three_maxima(hsize, &ind1, &ind2, &ind3);
+        for (int i = 0; i < n_f; i++)
+            if (match[i] >= 0 && bins[i] != ind1 && bins[i] != ind2 && bins[i] != ind3) {
+                match[i] = -1;
+                nmatches--;
+            }
+    }
+    free(bins);
+    return nmatches;
+}

@@ -256,6 +256,14 @@ void orc_bow_word(const orc_vocab *v, const uint8_t *feat, int levelsup, int32_t
 int orc_bow_transform(const orc_vocab *v, const uint8_t *desc, int n, int levelsup,
                       int32_t *bow_words, double *bow_weights, int *nbow, int32_t *fv_nodes,
                       int32_t *fv_off, int32_t *fv_feats, int *nfv);
+/* ORBmatcher::SearchByBoW(KeyFrame*, Frame&, ...) (ORBmatcher.cc:195-348), bow_oracle.c */
+int orc_search_by_bow(const uint8_t *kf_desc, const float *kf_angle, const uint8_t *kf_valid,
+                      int n_kf, const int32_t *kf_nodes, const int32_t *kf_off,
+                      const int32_t *kf_feats, int kf_nfv, const uint8_t *f_desc,
+                      const float *f_angle, int n_f, const int32_t *f_nodes, const int32_t *f_off,
+                      const int32_t *f_feats, int f_nfv, float nnratio, int check_ori,
+                      int32_t *match);
+void orc_three_maxima(const int *hsize, int *ind1, int *ind2, int *ind3);
 
 /* ---- Frame::ComputeStereoMatches (stereo_oracle.c) ----
  * kl/dl: left keypoints (mvKeys) + descriptors, kr/dr: right.  pyr_l / pyr_r: the two

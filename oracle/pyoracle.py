@@ -165,6 +165,9 @@ def lib():
                                         vp, vp, P(C.c_int)]
         L.orc_bow_word.argtypes = [P(OrcVocab), vp, C.c_int, P(C.c_int32), P(C.c_double),
                                    P(C.c_int32)]
+        L.orc_search_by_bow.restype = C.c_int
+        L.orc_search_by_bow.argtypes = [vp, vp, vp, C.c_int, vp, vp, vp, C.c_int, vp, vp, C.c_int,
+                                        vp, vp, vp, C.c_int, C.c_float, C.c_int, vp]
         _lib = L
     return _lib
 
@@ -549,3 +552,24 @@ def bow_transform(voc, desc, levelsup):
                             _p(vn), _p(vo), _p(vf), C.byref(nf))
     nb, nf = nb.value, nf.value
     return bw[:nb], bx[:nb], vn[:nf], vo[:nf + 1], vf[:vo[nf]]
+
+
+def search_by_bow(kf_desc, kf_angle, kf_valid, kf_fv, f_desc, f_angle, f_fv, nnratio=0.75,
+                  check_ori=True):
+    """ORBmatcher::SearchByBoW(KeyFrame*, Frame&, ...) restated (orc_search_by_bow,
+    bow_oracle.c).  kf_fv / f_fv = (fv_nodes, fv_off, fv_feats) as bow_transform returns them;
+    kf_valid[i] = pMP && !pMP->isBad() (None: all).  Returns (nmatches, match[n_f]) with
+    match[i] = the KF feature whose MapPoint matched F's feature i, -1 if none."""
+    kd = np.ascontiguousarray(kf_desc, np.uint8).reshape(-1, 32)
+    fd = np.ascontiguousarray(f_desc, np.uint8).reshape(-1, 32)
+    ka = np.ascontiguousarray(kf_angle, np.float32)
+    fa = np.ascontiguousarray(f_angle, np.float32)
+    kv = (np.ones(len(kd), np.uint8) if kf_valid is None
+          else np.ascontiguousarray(kf_valid, np.uint8))
+    kn, ko, kfe = [np.ascontiguousarray(a, np.int32) for a in kf_fv]
+    fn, fo, ffe = [np.ascontiguousarray(a, np.int32) for a in f_fv]
+    match = np.zeros(max(len(fd), 1), np.int32)
+    n = lib().orc_search_by_bow(_p(kd), _p(ka), _p(kv), len(kd), _p(kn), _p(ko), _p(kfe), len(kn),
+                                _p(fd), _p(fa), len(fd), _p(fn), _p(fo), _p(ffe), len(fn),
+                                float(nnratio), int(bool(check_ori)), _p(match))
+    return n, match[:len(fd)].copy()

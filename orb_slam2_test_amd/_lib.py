@@ -99,6 +99,13 @@ class OrbgError(RuntimeError):
         self.code = code
 
 
+class BowFrames(C.Structure):
+    """orbg_bow_frames (include/orbg.h): one side of SearchByBoW pairs, device pointers."""
+    _fields_ = [("desc", C.c_void_p), ("kps", C.c_void_p), ("counts", C.c_void_p),
+                ("fv_nodes", C.c_void_p), ("fv_off", C.c_void_p), ("fv_feats", C.c_void_p),
+                ("nfv", C.c_void_p), ("valid", C.c_void_p)]
+
+
 _lib = None
 
 
@@ -182,6 +189,10 @@ def lib():
         "orbg_bow_transform": (i32, [vp, vp, vp, i32, i32, vp, vp, P(i32), vp, vp, vp, P(i32)]),
         "orbg_bow_transform_batch_device": (i32, [vp, vp, vp, vp, i32, i32, i32, vp, vp, vp, vp,
                                                   vp, vp, vp, vp, vp]),
+        "orbg_search_by_bow": (i32, [vp, vp, vp, vp, i32, vp, vp, vp, i32, vp, vp, i32, vp, vp, vp,
+                                     i32, f32, i32, vp, P(i32)]),
+        "orbg_search_by_bow_batch_device": (i32, [vp, P(BowFrames), P(BowFrames), i32, vp, vp, i32,
+                                                  f32, i32, vp, vp]),
         "orbg_ba_linearize": (i32, [vp, vp, i32, vp, i32, vp, i32, vp, vp, vp, vp, vp]),
         "orbg_ba_set_jacobians": (i32, [vp, i32]),
         "orbg_ba_set_edge_errors": (i32, [vp, i32]),

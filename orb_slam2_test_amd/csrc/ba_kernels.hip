@@ -264,6 +264,29 @@ __device__ __forceinline__ void ba_linearize_edge(const orbg_pose &P, const doub
     L.w = rho1 * L.info;
 }
 
+// an active edge's share of its point block (base_binary_edge.hpp:55-120): c[0..8] =
+// J_point^T W J_point row-major, c[9..11] = J_point^T (-rho' Omega e)
+__device__ __forceinline__ void ba_point_share(const BaLin &L, double c[12])
+{
+    double wr[3];
+#pragma unroll
+    for (int k = 0; k < 3; k++) wr[k] = -L.info * L.err[k] * L.rho1;
+#pragma unroll
+    for (int r = 0; r < 3; r++) {
+        double bs = 0;
+#pragma unroll
+        for (int k = 0; k < 3; k++) bs += L.jp[k][r] * wr[k];
+        c[9 + r] = bs;
+#pragma unroll
+        for (int cc = 0; cc < 3; cc++) {
+            double hs = 0;
+#pragma unroll
+            for (int k = 0; k < 3; k++) hs += L.jp[k][r] * L.w * L.jp[k][cc];
+            c[r * 3 + cc] = hs;
+        }
+    }
+}
+
 // per-edge outputs: field pointers with a stride in doubles per edge (the orbg_edge_out
 // records of the ABI, stride 50, or separate arrays); NULL = not stored
 struct BaEdgeOut {
@@ -283,9 +306,9 @@ struct BaEdgeOut {
 // onto the zeroed block (two partials for any point with <= 256 edges: exact in either
 // order).  The pose blocks are k_ba_pose_mfma's, which recomputes the pose rows it needs.
 // ---------------------------------------------------------------------------
-#define BA_EDGES_TPB 256
+#define BA_EDGES_TPB ORBG_BA_EDGES_TPB
 
-template <class ES>
+template <class ES, bool GRAPH>
 __global__ __launch_bounds__(BA_EDGES_TPB) void k_ba_edges(const orbg_pose *__restrict__ poses,
                                                           const double *__restrict__ points,
                                                           const ES edges,
@@ -332,23 +355,7 @@ __global__ __launch_bounds__(BA_EDGES_TPB) void k_ba_edges(const orbg_pose *__re
                                      points[3 * (size_t)q + 2]};
                 BaLin L;
                 ba_linearize_edge(P, X, e, L);
-                double wr[3];
-#pragma unroll
-                for (int k = 0; k < 3; k++) wr[k] = -L.info * L.err[k] * L.rho1;
-#pragma unroll
-                for (int r = 0; r < 3; r++) {
-                    double bs = 0;
-#pragma unroll
-                    for (int k = 0; k < 3; k++) bs += L.jp[k][r] * wr[k];
-                    c[9 + r] = bs;
-#pragma unroll
-                    for (int cc = 0; cc < 3; cc++) {
-                        double hs = 0;
-#pragma unroll
-                        for (int k = 0; k < 3; k++) hs += L.jp[k][r] * L.w * L.jp[k][cc];
-                        c[r * 3 + cc] = hs;
-                    }
-                }
+                ba_point_share(L, c);
                 if (o.hpl) {
                     double h[18];
 #pragma unroll
@@ -393,6 +400,7 @@ __global__ __launch_bounds__(BA_EDGES_TPB) void k_ba_edges(const orbg_pose *__re
 #pragma unroll
         for (int k = 0; k < 12; k++) acc[k] += part[k][j];
     double *hq = hpoint + 9 * (size_t)q, *bq = bpoint + 3 * (size_t)q;
+    if (GRAPH && (qs < base || qe > bend)) return;  // k_ba_special sums it in edge order
     if (qs < base || qe > bend) {  // the point's slots span workgroups: partial sums
 #pragma unroll
         for (int k = 0; k < 9; k++) atomicAdd(hq + k, acc[k]);
@@ -418,36 +426,20 @@ __global__ __launch_bounds__(BA_EDGES_TPB) void k_ba_edges(const orbg_pose *__re
 // ---------------------------------------------------------------------------
 typedef double v4d __attribute__((ext_vector_type(4)));
 
-#define BA_SLICE 64  // edges per wave
+#define BA_SLICE ORBG_BA_SLICE  // edges per wave
 #define BA_ROW 8     // doubles per staged pose row: J_pose (6), -e, w
 
+// One 64-edge slice into LDS rows (lane l: edge l -> rows 3l .. 3l+2: J_pose row, -e, w; zero
+// rows for the third row of a mono edge and for inactive edges or lanes past the slice), then
+// C += sum_r (w_r v_r)^T v_r by v_mfma_f64_16x16x4f64 (A[i][k] = w v[i], B[k][j] = v[j], 7
+// columns padded to 16)
 template <class ES>
-__global__ __launch_bounds__(256) void k_ba_pose_mfma(const orbg_pose *__restrict__ poses,
-                                                      const double *__restrict__ points,
-                                                      const ES edges,
-                                                      const int32_t *__restrict__ pose_off,
-                                                      const int32_t *__restrict__ pose_edges,
-                                                      const int32_t *__restrict__ slice_off,
-                                                      const int32_t *__restrict__ slice_pose,
-                                                      int nslice, double *__restrict__ hpose,
-                                                      double *__restrict__ bpose)
+__device__ __forceinline__ void ba_pose_slice(const orbg_pose &P, const double *__restrict__ points,
+                                              const ES &edges,
+                                              const int32_t *__restrict__ pose_edges, int e0,
+                                              int ne, double *rl, int lane, v4d &C)
 {
-    __shared__ double rows_lds[4][3 * BA_SLICE * BA_ROW];  // 12 KB per wave
-    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-    const int sl = blockIdx.x * 4 + wv;
-    if (sl >= nslice) return;    // wave-uniform; no workgroup barrier below
-    const int p = slice_pose[sl];
-    if (p < 0) return;           // past the last slice (table filled with -1)
-    const orbg_pose P = poses[p];
-    if (P.fixed) return;         // stays zero (memset): g2o builds no block for it
-    double *H = hpose + 36 * (size_t)p, *bv = bpose + 6 * (size_t)p;
-    const int e0p = pose_off[p], nep = pose_off[p + 1] - e0p;
-    const int ks = sl - slice_off[p];
-    const int e0 = e0p + ks * BA_SLICE;
-    const int ne = min(BA_SLICE, nep - ks * BA_SLICE);
-    double *rl = rows_lds[wv];
     {
-        // lane l: edge l of the slice -> rows 3l .. 3l+2
         double v[3][BA_ROW];
 #pragma unroll
         for (int k = 0; k < 3; k++)
@@ -470,6 +462,7 @@ __global__ __launch_bounds__(256) void k_ba_pose_mfma(const orbg_pose *__restric
                 }
             }
         }
+        wave_sync_lds_ba();  // the previous slice's reads of rl are done (in-order LDS)
 #pragma unroll
         for (int k = 0; k < 3; k++)
 #pragma unroll
@@ -480,7 +473,6 @@ __global__ __launch_bounds__(256) void k_ba_pose_mfma(const orbg_pose *__restric
     const int nrow = 3 * ne;
     const int i = lane & 15, k = lane >> 4;  // A: (row i of the 16x4 tile, k); B: (k, column i)
     const int col = i < 7 ? i : 7;           // padded columns read the weight and are zeroed
-    v4d C = {0, 0, 0, 0};
     for (int r0 = 0; r0 < nrow; r0 += 4 * 4) {
         double va[4], vb[4];
 #pragma unroll
@@ -494,6 +486,35 @@ __global__ __launch_bounds__(256) void k_ba_pose_mfma(const orbg_pose *__restric
 #pragma unroll
         for (int u = 0; u < 4; u++) C = __builtin_amdgcn_mfma_f64_16x16x4f64(va[u], vb[u], C, 0, 0, 0);
     }
+}
+
+// record path: one wave per slice, the slices of one pose added by fp64 atomics onto the
+// zeroed blocks.  Fixed poses get no block (g2o skips them).
+template <class ES>
+__global__ __launch_bounds__(256) void k_ba_pose_mfma(const orbg_pose *__restrict__ poses,
+                                                      const double *__restrict__ points,
+                                                      const ES edges,
+                                                      const int32_t *__restrict__ pose_off,
+                                                      const int32_t *__restrict__ pose_edges,
+                                                      const int32_t *__restrict__ slice_off,
+                                                      const int32_t *__restrict__ slice_pose,
+                                                      int nslice, double *__restrict__ hpose,
+                                                      double *__restrict__ bpose)
+{
+    __shared__ double rows_lds[4][3 * BA_SLICE * BA_ROW];  // 12 KB per wave
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    const int sl = blockIdx.x * 4 + wv;
+    if (sl >= nslice) return;    // wave-uniform; no workgroup barrier below
+    const int p = slice_pose[sl];
+    if (p < 0) return;           // past the last slice (table filled with -1)
+    const orbg_pose P = poses[p];
+    if (P.fixed) return;         // stays zero (memset)
+    double *H = hpose + 36 * (size_t)p, *bv = bpose + 6 * (size_t)p;
+    const int e0p = pose_off[p], nep = pose_off[p + 1] - e0p;
+    const int ks = sl - slice_off[p];
+    v4d C = {0, 0, 0, 0};
+    ba_pose_slice(P, points, edges, pose_edges, e0p + ks * BA_SLICE,
+                  min(BA_SLICE, nep - ks * BA_SLICE), rows_lds[wv], lane, C);
     // D layout of v_mfma_f64_16x16x4f64 (measured): lane holds column j = lane % 16 of rows
     // lane / 16 + 4 v, v = 0..3
     const int j = lane & 15;
@@ -503,6 +524,109 @@ __global__ __launch_bounds__(256) void k_ba_pose_mfma(const orbg_pose *__restric
         if (row < 6 && j < 6) atomicAdd(&H[row * 6 + j], C[v]);
         if (row < 6 && j == 6) atomicAdd(&bv[row], C[v]);
     }
+}
+
+// graph path, pass 1: one wave per slice (the graph's slice tables, built once), the
+// slice's [H | b] partial (6 x 7) stored -- no fills, no atomics
+template <class ES>
+__global__ __launch_bounds__(256) void k_ba_pose_slices(const orbg_pose *__restrict__ poses,
+                                                        const double *__restrict__ points,
+                                                        const ES edges,
+                                                        const int32_t *__restrict__ pose_off,
+                                                        const int32_t *__restrict__ pose_edges,
+                                                        const int32_t *__restrict__ slice_off,
+                                                        const int32_t *__restrict__ slice_pose,
+                                                        int nslice, double *__restrict__ part)
+{
+    __shared__ double rows_lds[4][3 * BA_SLICE * BA_ROW];  // 12 KB per wave
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    const int sl = blockIdx.x * 4 + wv;
+    if (sl >= nslice) return;  // wave-uniform; no workgroup barrier below
+    const int p = slice_pose[sl];
+    const orbg_pose P = poses[p];
+    if (P.fixed) return;       // pass 2 writes the zero block
+    const int e0p = pose_off[p], nep = pose_off[p + 1] - e0p;
+    const int ks = sl - slice_off[p];
+    v4d C = {0, 0, 0, 0};
+    ba_pose_slice(P, points, edges, pose_edges, e0p + ks * BA_SLICE,
+                  min(BA_SLICE, nep - ks * BA_SLICE), rows_lds[wv], lane, C);
+    const int j = lane & 15;
+#pragma unroll
+    for (int v = 0; v < 4; v++) {
+        const int row = (lane >> 4) + 4 * v;
+        if (row < 6 && j < 7) part[42 * (size_t)sl + row * 7 + j] = C[v];
+    }
+}
+
+// graph path, pass 2: thread per (pose, block entry): the slice partials summed in slice order
+// (the next launch: stream order makes pass 1's stores visible), zero for fixed poses and poses
+// without edges; every block written, the same bits every build
+__global__ __launch_bounds__(256) void k_ba_pose_reduce(const orbg_pose *__restrict__ poses,
+                                                        int npose,
+                                                        const int32_t *__restrict__ slice_off,
+                                                        const double *__restrict__ part,
+                                                        double *__restrict__ hpose,
+                                                        double *__restrict__ bpose)
+{
+    const int t = blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= 42 * npose) return;
+    const int p = t / 42, e = t - 42 * p;
+    double acc = 0;
+    if (!poses[p].fixed)
+        for (int s = slice_off[p]; s < slice_off[p + 1]; s++) acc += part[42 * (size_t)s + e];
+    const int row = e / 7, col = e - 7 * row;
+    if (col < 6)
+        hpose[36 * (size_t)p + row * 6 + col] = acc;
+    else
+        bpose[6 * (size_t)p + row] = acc;
+}
+
+// orbg_ba_graph's special points, one wave each: points whose slots span two k_ba_edges
+// workgroups (their block summed here in edge order, the oracle's, instead of two partials)
+// and points without edges (zero block).  Lane l computes edge l's share (chunks of 64),
+// lanes 0..11 sum one block entry each over the edges in order.
+template <class ES>
+__global__ __launch_bounds__(256) void k_ba_special(const orbg_pose *__restrict__ poses,
+                                                    const double *__restrict__ points,
+                                                    const ES edges,
+                                                    const int32_t *__restrict__ point_off,
+                                                    const int32_t *__restrict__ point_edges,
+                                                    const int32_t *__restrict__ special, int nsp,
+                                                    double *__restrict__ hpoint,
+                                                    double *__restrict__ bpoint)
+{
+    __shared__ double sh[4][12][64];
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    const int i = blockIdx.x * 4 + wv;
+    if (i >= nsp) return;  // wave-uniform; no workgroup barrier below
+    const int q = special[i];
+    const double X[3] = {points[3 * (size_t)q], points[3 * (size_t)q + 1], points[3 * (size_t)q + 2]};
+    const int a0 = point_off[q], a1 = point_off[q + 1];
+    double acc = 0;  // lanes 0..11: entry `lane` of [H_ll | b_l]
+    for (int c0 = a0; c0 < a1; c0 += 64) {
+        double c[12];
+#pragma unroll
+        for (int k = 0; k < 12; k++) c[k] = 0;
+        if (c0 + lane < a1) {
+            const orbg_edge e = edges(point_edges[c0 + lane]);
+            if (e.active) {
+                BaLin L;
+                ba_linearize_edge(poses[e.pose], X, e, L);
+                ba_point_share(L, c);
+            }
+        }
+        wave_sync_lds_ba();
+#pragma unroll
+        for (int k = 0; k < 12; k++) sh[wv][k][lane] = c[k];
+        wave_sync_lds_ba();
+        const int n = min(64, a1 - c0);
+        if (lane < 12)
+            for (int j = 0; j < n; j++) acc += sh[wv][lane][j];
+    }
+    if (lane < 9)
+        hpoint[9 * (size_t)q + lane] = acc;
+    else if (lane < 12)
+        bpoint[3 * (size_t)q + lane - 9] = acc;
 }
 
 // slice -> pose table: pose p owns ceil(edges_p / BA_SLICE) consecutive slices
@@ -605,7 +729,7 @@ static int launch_ba_device_t(hipStream_t st, const orbg_pose *poses, int npose,
     if (nedge) {
         hipEvent_t a = nullptr;
         prof_begin(prof, st, "ba_edges", &a);
-        hipLaunchKernelGGL(k_ba_edges<ES>, dim3((nedge + BA_EDGES_TPB - 1) / BA_EDGES_TPB),
+        hipLaunchKernelGGL((k_ba_edges<ES, false>), dim3((nedge + BA_EDGES_TPB - 1) / BA_EDGES_TPB),
                            dim3(BA_EDGES_TPB), 0, st, poses, points, edges, nedge, point_off,
                            point_edges, o, hpoint, bpoint);
         prof_end(prof, st, "ba_edges", a);
@@ -628,9 +752,9 @@ static int launch_ba_device_t(hipStream_t st, const orbg_pose *poses, int npose,
         hipEvent_t a = nullptr;
         prof_begin(prof, st, "ba_pose_mfma", &a);
         // the grid covers the bound; waves past the actual slice count exit at once
-        hipLaunchKernelGGL(k_ba_pose_mfma<ES>, dim3((max_slices + 3) / 4), dim3(256), 0, st, poses,
-                           points, edges, pose_off, pose_edges, slice_off, slice_pose, max_slices,
-                           hpose, bpose);
+        hipLaunchKernelGGL(k_ba_pose_mfma<ES>, dim3((max_slices + 3) / 4), dim3(256), 0, st,
+                           poses, points, edges, pose_off, pose_edges, slice_off, slice_pose,
+                           max_slices, hpose, bpose);
         prof_end(prof, st, "ba_pose_mfma", a);
     }
     return hipGetLastError() == hipSuccess ? 0 : -5;
@@ -648,17 +772,49 @@ int launch_ba_device(hipStream_t st, const orbg_pose *poses, int npose, const do
                               hpoint, bpoint, scr, prof, jacobians, errors, hpl);
 }
 
-// an orbg_ba_graph's buildSystem: H_pl compact, no per-edge record
+// an orbg_ba_graph's buildSystem: H_pl compact, no per-edge record, and the structure
+// precomputed once per graph (BaGraphDev): the exact slice tables, the special vertices, the
+// pose partials and arrival counters -- no zero fills, no slice-table kernel, no atomics on
+// the blocks per build
 int launch_ba_graph(hipStream_t st, const orbg_pose *poses, int npose, const double *points,
                     int npoint, const BaPackedEdge *edges, const BaCam *cam, const BaInfo *info,
                     int nedge, const int32_t *pose_off, const int32_t *pose_edges,
-                    const int32_t *point_off, const int32_t *point_edges, double *hpl,
-                    double *hpose, double *bpose, double *hpoint, double *bpoint, double *scr,
+                    const int32_t *point_off, const int32_t *point_edges, const BaGraphDev &gd,
+                    double *hpl, double *hpose, double *bpose, double *hpoint, double *bpoint,
                     void *prof)
 {
-    return launch_ba_device_t(st, poses, npose, points, npoint, BaEdgePacked{edges, cam, info},
-                              nedge, pose_off, pose_edges, point_off, point_edges, nullptr,
-                              hpose, bpose, hpoint, bpoint, scr, prof, false, false, hpl);
+    const BaEdgePacked es{edges, cam, info};
+    BaEdgeOut o{};
+    o.hpl = hpl;
+    o.stride = 18;
+    if (nedge) {
+        hipEvent_t a = nullptr;
+        prof_begin(prof, st, "ba_edges", &a);
+        hipLaunchKernelGGL((k_ba_edges<BaEdgePacked, true>),
+                           dim3((nedge + BA_EDGES_TPB - 1) / BA_EDGES_TPB), dim3(BA_EDGES_TPB), 0,
+                           st, poses, points, es, nedge, point_off, point_edges, o, hpoint, bpoint);
+        prof_end(prof, st, "ba_edges", a);
+    }
+    if (gd.nspecial) {
+        hipEvent_t a = nullptr;
+        prof_begin(prof, st, "ba_special", &a);
+        hipLaunchKernelGGL(k_ba_special<BaEdgePacked>, dim3((gd.nspecial + 3) / 4), dim3(256), 0,
+                           st, poses, points, es, point_off, point_edges, gd.special, gd.nspecial,
+                           hpoint, bpoint);
+        prof_end(prof, st, "ba_special", a);
+    }
+    if (npose) {
+        hipEvent_t a = nullptr;
+        prof_begin(prof, st, "ba_pose_mfma", &a);
+        if (gd.nslice)
+            hipLaunchKernelGGL(k_ba_pose_slices<BaEdgePacked>, dim3((gd.nslice + 3) / 4), dim3(256),
+                               0, st, poses, points, es, pose_off, pose_edges, gd.slice_off,
+                               gd.slice_pose, gd.nslice, gd.part);
+        hipLaunchKernelGGL(k_ba_pose_reduce, dim3((42 * npose + 255) / 256), dim3(256), 0, st,
+                           poses, npose, gd.slice_off, gd.part, hpose, bpose);
+        prof_end(prof, st, "ba_pose_mfma", a);
+    }
+    return hipGetLastError() == hipSuccess ? 0 : -5;
 }
 
 // host arrays in/out: upload, build nothing on the device but the blocks, download

@@ -1,0 +1,247 @@
+// bow_match_kernels.hip -- k_bow_match: ORBmatcher::SearchByBoW(KeyFrame *pKF, Frame &F,
+// vector<MapPoint*> &vpMapPointMatches) (src/ORBmatcher.cc:195-348) for gfx950, one workgroup
+// per (KF, F) pair.  Callers: Tracking::TrackReferenceKeyFrame (Tracking.cc:1069) and
+// Tracking::Relocalization (:2009), over the FeatureVectors DBoW2's transform builds
+// (orbg_bow_transform_batch_device, bow_kernels.hip).
+//
+// The reference walks both FeatureVectors (std::map NodeId -> feature indices) in id order and
+// matches features that share a node; a feature of F lives in exactly one node, so nodes are
+// independent and only the order WITHIN a node matters (an F feature taken by an earlier KF
+// feature of the node is skipped).  Here:
+//   join     the KF node ids, 64 per wave, each lane binary-searching F's sorted node ids in
+//            HBM; common (KF node, F node) pairs are appended to an LDS list (any order);
+//   node     a wave per common node: lane l holds F candidate l (+ 64, + 128 ...) of the node,
+//            its descriptor in registers and a "taken" bit; the node's KF features run in the
+//            reference's order (a KF feature without a valid MapPoint skipped, wave-uniform),
+//            the KF descriptor in scalar registers; per lane the Hamming distance (8 xor +
+//            8 bcnt), then two wave-wide min reductions: (distance, position) for the best --
+//            the first position wins ties, as the reference's strict < -- and the second best
+//            (the winner's own second, everyone else's best).  TH_LOW and the float nnratio
+//            test, then the winner lane marks its candidate taken, writes the match and adds
+//            the rotation bin to an LDS histogram;
+//   rotation ComputeThreeMaxima (ORBmatcher.cc:1800-1841) by one lane, then every match
+//            outside the three bins dropped (its bin recomputed from the two angles).
+#include <hip/hip_runtime.h>
+
+#include "../../include/orbg.h"
+#include "orbg_internal.h"
+#include "orbg_device.h"
+
+#pragma clang fp contract(off)
+
+namespace orbg {
+
+#define BM_HISTO 30
+#define BM_TH_LOW 50
+#define BM_LIST 1024  // common nodes per pair held in LDS (a FeatureVector has <= cap nodes)
+
+struct BowMatchSide {
+    const uint8_t *desc;
+    const orbg_keypoint *kps;
+    const int32_t *counts, *fv_nodes, *fv_off, *fv_feats, *nfv;
+    const uint8_t *valid;
+};
+
+__device__ __forceinline__ unsigned wave_min_u32(unsigned v)
+{
+    // butterfly over the wave with DPP row ops and the 32-lane swap; result in every lane
+    v = min(v, (unsigned)__builtin_amdgcn_update_dpp(0, (int)v, 0xb1, 0xf, 0xf, false));  // quad_perm 1,0,3,2
+    v = min(v, (unsigned)__builtin_amdgcn_update_dpp(0, (int)v, 0x4e, 0xf, 0xf, false));  // quad_perm 2,3,0,1
+    v = min(v, (unsigned)__builtin_amdgcn_update_dpp(0, (int)v, 0x124, 0xf, 0xf, false)); // row_ror 4
+    v = min(v, (unsigned)__builtin_amdgcn_update_dpp(0, (int)v, 0x128, 0xf, 0xf, false)); // row_ror 8
+    const unsigned r0 = (unsigned)__builtin_amdgcn_readlane((int)v, 0);
+    const unsigned r1 = (unsigned)__builtin_amdgcn_readlane((int)v, 16);
+    const unsigned r2 = (unsigned)__builtin_amdgcn_readlane((int)v, 32);
+    const unsigned r3 = (unsigned)__builtin_amdgcn_readlane((int)v, 48);
+    return min(min(r0, r1), min(r2, r3));
+}
+
+__device__ __forceinline__ int bm_rot_bin(float a_kf, float a_f)
+{
+    // ORBmatcher.cc:291-297 (rot < 0.0 in double as the reference compares, then float)
+    const float factor = 1.0f / BM_HISTO;
+    float rot = a_kf - a_f;
+    if (rot < 0.0) rot += 360.0f;
+    int bin = (int)roundf(rot * factor);
+    if (bin == BM_HISTO) bin = 0;
+    return bin;
+}
+
+__global__ __launch_bounds__(256) void k_bow_match(BowMatchSide K, BowMatchSide F, int cap,
+                                                   const int32_t *__restrict__ kf_index,
+                                                   const int32_t *__restrict__ f_index,
+                                                   float nnratio, int check_ori,
+                                                   int32_t *__restrict__ match,
+                                                   int32_t *__restrict__ nmatch)
+{
+    __shared__ int2 common[BM_LIST];
+    __shared__ int ncommon, nm, removed, hist[BM_HISTO], ind[3];
+    const int p = blockIdx.x;
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    const int kf = kf_index[p], fr = f_index[p];
+    const int nk_nodes = K.nfv[kf], nf_nodes = F.nfv[fr];
+    const int n_f = F.counts[fr];
+    const int32_t *kn = K.fv_nodes + (size_t)kf * cap, *ko = K.fv_off + (size_t)kf * (cap + 1),
+                  *kfe = K.fv_feats + (size_t)kf * cap;
+    const int32_t *fn = F.fv_nodes + (size_t)fr * cap, *fo = F.fv_off + (size_t)fr * (cap + 1),
+                  *ffe = F.fv_feats + (size_t)fr * cap;
+    const uint8_t *kdesc = K.desc + (size_t)kf * cap * 32, *fdesc = F.desc + (size_t)fr * cap * 32;
+    const orbg_keypoint *kkp = K.kps + (size_t)kf * cap, *fkp = F.kps + (size_t)fr * cap;
+    const uint8_t *kval = K.valid ? K.valid + (size_t)kf * cap : nullptr;
+    int32_t *out = match + (size_t)p * cap;
+    if (threadIdx.x == 0) {
+        ncommon = 0;
+        nm = 0;
+        removed = 0;
+    }
+    if (threadIdx.x < BM_HISTO) hist[threadIdx.x] = 0;
+    for (int i = threadIdx.x; i < n_f; i += blockDim.x) out[i] = -1;
+    __syncthreads();
+    // ---- join: KF node j looks its id up in F's sorted node ids ----
+    for (int j = threadIdx.x; j < nk_nodes; j += blockDim.x) {
+        const int id = kn[j];
+        int lo = 0, hi = nf_nodes;  // first F node with id >= kn[j]
+        while (lo < hi) {
+            const int mid = (lo + hi) >> 1;
+            if (fn[mid] < id)
+                lo = mid + 1;
+            else
+                hi = mid;
+        }
+        if (lo < nf_nodes && fn[lo] == id) {
+            const int k = atomicAdd(&ncommon, 1);
+            if (k < BM_LIST) common[k] = make_int2(j, lo);
+        }
+    }
+    __syncthreads();
+    const int nc = min(ncommon, BM_LIST);
+    // ---- a wave per common node ----
+    int wave_nm = 0;
+    for (int c = wv; c < nc; c += (int)(blockDim.x >> 6)) {
+        const int2 jb = common[c];
+        const int k0 = ko[jb.x], k1 = ko[jb.x + 1];
+        const int f0 = fo[jb.y], nF = fo[jb.y + 1] - f0;
+        const int nchunk = (nF + 63) >> 6;
+        uint32_t cd0[8], cd1[8];  // candidates lane and lane + 64 (larger nodes: re-read)
+        int ci0 = -1, ci1 = -1;
+        if (lane < nF) ci0 = ffe[f0 + lane];
+        if (lane + 64 < nF) ci1 = ffe[f0 + lane + 64];
+#pragma unroll
+        for (int w = 0; w < 8; w++) {
+            cd0[w] = ci0 >= 0 ? ((const uint32_t *)(fdesc + (size_t)ci0 * 32))[w] : 0u;
+            cd1[w] = ci1 >= 0 ? ((const uint32_t *)(fdesc + (size_t)ci1 * 32))[w] : 0u;
+        }
+        uint32_t taken = 0;  // bit k: candidate lane + 64 k already matched
+        for (int ik = k0; ik < k1; ik++) {
+            const int rk = __builtin_amdgcn_readfirstlane(kfe[ik]);
+            if (kval && !kval[rk]) continue;  // pMP NULL or bad: wave-uniform skip
+            uint32_t kd[8];
+#pragma unroll
+            for (int w = 0; w < 8; w++)
+                kd[w] = __builtin_amdgcn_readfirstlane(((const uint32_t *)(kdesc + (size_t)rk * 32))[w]);
+            unsigned b1 = 256, b2 = 256, pos1 = 0xFFFF;
+            for (int ch = 0; ch < nchunk; ch++) {  // in position order: strict < keeps the first
+                const int pos = ch * 64 + lane;
+                if (pos >= nF || (taken >> ch & 1u)) continue;
+                unsigned d = 0;
+                if (ch == 0) {
+#pragma unroll
+                    for (int w = 0; w < 8; w++) d += __popc(kd[w] ^ cd0[w]);
+                } else if (ch == 1) {
+#pragma unroll
+                    for (int w = 0; w < 8; w++) d += __popc(kd[w] ^ cd1[w]);
+                } else {
+                    const uint32_t *q = (const uint32_t *)(fdesc + (size_t)ffe[f0 + pos] * 32);
+#pragma unroll
+                    for (int w = 0; w < 8; w++) d += __popc(kd[w] ^ q[w]);
+                }
+                if (d < b1) {
+                    b2 = b1;
+                    b1 = d;
+                    pos1 = (unsigned)pos;
+                } else if (d < b2) {
+                    b2 = d;
+                }
+            }
+            const unsigned key = b1 << 16 | pos1;
+            const unsigned best = wave_min_u32(key);
+            const unsigned best1 = best >> 16, bpos = best & 0xFFFFu;
+            const bool winner = key == best && best1 < 256;
+            const unsigned best2 = wave_min_u32(winner ? b2 : b1);
+            if (best1 <= BM_TH_LOW && (float)best1 < nnratio * (float)best2) {
+                wave_nm++;
+                if (winner) {
+                    taken |= 1u << (bpos >> 6);
+                    const int rf = ffe[f0 + (int)bpos];
+                    out[rf] = rk;
+                    if (check_ori) atomicAdd(&hist[bm_rot_bin(kkp[rk].angle, fkp[rf].angle)], 1);
+                }
+            }
+        }
+    }
+    if (lane == 0 && wave_nm) atomicAdd(&nm, wave_nm);
+    __syncthreads();
+    if (check_ori) {
+        if (threadIdx.x == 0) {
+            // ComputeThreeMaxima (ORBmatcher.cc:1800-1841)
+            int max1 = 0, max2 = 0, max3 = 0, i1 = -1, i2 = -1, i3 = -1;
+            for (int i = 0; i < BM_HISTO; i++) {
+                const int s = hist[i];
+                if (s > max1) {
+                    max3 = max2;
+                    max2 = max1;
+                    max1 = s;
+                    i3 = i2;
+                    i2 = i1;
+                    i1 = i;
+                } else if (s > max2) {
+                    max3 = max2;
+                    max2 = s;
+                    i3 = i2;
+                    i2 = i;
+                } else if (s > max3) {
+                    max3 = s;
+                    i3 = i;
+                }
+            }
+            if (max2 < 0.1f * (float)max1) {
+                i2 = -1;
+                i3 = -1;
+            } else if (max3 < 0.1f * (float)max1) {
+                i3 = -1;
+            }
+            ind[0] = i1;
+            ind[1] = i2;
+            ind[2] = i3;
+        }
+        __syncthreads();
+        int rm = 0;
+        for (int i = threadIdx.x; i < n_f; i += blockDim.x) {
+            const int m = out[i];
+            if (m < 0) continue;
+            const int bin = bm_rot_bin(kkp[m].angle, fkp[i].angle);
+            if (bin != ind[0] && bin != ind[1] && bin != ind[2]) {
+                out[i] = -1;
+                rm++;
+            }
+        }
+        if (rm) atomicAdd(&removed, rm);
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) nmatch[p] = nm - removed;
+}
+
+int launch_bow_match(hipStream_t st, const orbg_bow_frames &kf, const orbg_bow_frames &f, int cap,
+                     const int32_t *kf_index, const int32_t *f_index, int npairs, float nnratio,
+                     int check_ori, int32_t *match, int32_t *nmatch)
+{
+    if (npairs <= 0) return 0;
+    const BowMatchSide K{kf.desc, kf.kps, kf.counts, kf.fv_nodes, kf.fv_off, kf.fv_feats, kf.nfv,
+                         kf.valid};
+    const BowMatchSide F{f.desc, f.kps, f.counts, f.fv_nodes, f.fv_off, f.fv_feats, f.nfv, nullptr};
+    hipLaunchKernelGGL(k_bow_match, dim3(npairs), dim3(256), 0, st, K, F, cap, kf_index, f_index,
+                       nnratio, check_ori, match, nmatch);
+    return hipGetLastError() == hipSuccess ? 0 : -5;
+}
+
+}  // namespace orbg

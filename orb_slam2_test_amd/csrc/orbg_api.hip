@@ -36,8 +36,9 @@ __global__ void k_octree_lds(const OrbgGeom *, const int32_t *, const uint2 *, u
                              int32_t *, int32_t *, OctLdsDims);
 // fast_kernels.hip
 bool fast2_pitch_ok(int p4);
-__global__ void k_pyramid(PyrArgs, const uint4 *, const int4 *, const int2 *, const uint8_t *,
-                          int64_t, int, const uint8_t *, uint8_t *, int);
+__global__ void k_pyramid(PyrArgs, const OrbgGeom *, const uint4 *, const int4 *, const int4 *,
+                          const uint8_t *, int64_t, int, const uint8_t *, uint8_t *, uint8_t *,
+                          int);
 // blur_kernels.hip
 int blur2_seg();
 int blur2_tw();
@@ -87,6 +88,10 @@ int launch_init_match_single(hipStream_t st, const orbg_keypoint *k1, const uint
                              orbg_bounds b, float *prev, int32_t *m12, int32_t *nm, int window,
                              float nnratio, int check_ori, uint32_t *topk, int32_t *topk_n,
                              void *prof);
+// bow_match_kernels.hip
+int launch_bow_match(hipStream_t st, const orbg_bow_frames &kf, const orbg_bow_frames &f, int cap,
+                     const int32_t *kf_index, const int32_t *f_index, int npairs, float nnratio,
+                     int check_ori, int32_t *match, int32_t *nmatch);
 // ba_kernels.hip
 int launch_ba(hipStream_t st, const orbg_pose *poses, int npose, const double *points,
               int npoint, const orbg_edge *edges, int nedge, const int32_t *pose_off,
@@ -118,8 +123,8 @@ int launch_ba_errors_packed(hipStream_t st, const orbg_pose *poses, const double
 int launch_ba_graph(hipStream_t st, const orbg_pose *poses, int npose, const double *points,
                     int npoint, const BaPackedEdge *edges, const BaCam *cam, const BaInfo *info,
                     int nedge, const int32_t *pose_off, const int32_t *pose_edges,
-                    const int32_t *point_off, const int32_t *point_edges, double *hpl,
-                    double *hpose, double *bpose, double *hpoint, double *bpoint, double *scr,
+                    const int32_t *point_off, const int32_t *point_edges, const BaGraphDev &gd,
+                    double *hpl, double *hpose, double *bpose, double *hpoint, double *bpoint,
                     void *prof);
 }  // namespace orbg
 
@@ -332,7 +337,7 @@ struct orbg_ctx {
     // = the plan passed k_pyramid's checks (else the k_resize chain)
     uint4 *d_ptab = nullptr;
     int4 *d_ytab4 = nullptr;
-    int2 *d_bands = nullptr;
+    int4 *d_bands = nullptr;
     PyrArgs pyr_args{};
     bool pyr_ok = false;
     int pyr_wg = 512;  // k_pyramid workgroup size (ORBG_PYR_WG)
@@ -586,7 +591,7 @@ static int stage(orbg_ctx *c, size_t bytes, uint8_t **out)
 // PYR_NS source rows per 8 output rows); the k_resize chain then builds the pyramid.
 static bool make_pyr_tables(const OrbgGeom &G, const std::vector<int2> &rtab, int nband,
                             std::vector<uint4> &ptab, std::vector<int4> &ytab,
-                            std::vector<int2> &bands, PyrArgs &A)
+                            std::vector<int4> &bands, PyrArgs &A, int fuse_blur)
 {
     if (G.L < 2 || G.L > 16 || nband < 1) return false;
     A = PyrArgs{};
@@ -654,14 +659,29 @@ static bool make_pyr_tables(const OrbgGeom &G, const std::vector<int2> &rtab, in
             ytab.push_back(make_int4(sy0 | sy1 << 16, b0 << 8, b1 << 8, b0 | b1 << 16));
         }
     }
-    // bands: own rows split evenly per level; the rows a band computes are its own rows plus
-    // the source rows of what it computes one level up (top-down closure)
-    bands.assign((size_t)nband * G.L, make_int2(0, 0));
+    // bands: own rows split evenly per level; the rows a band computes are its own rows (with
+    // the fused blur, +-3 rows: the blur of its own rows reads them, REFLECT_101 inside the
+    // level) plus the source rows of what it computes one level up (top-down closure)
+    A.fuse_blur = fuse_blur;
+    A.w0 = G.lv[0].w;
+    A.h0 = G.lv[0].h;
+    A.bpitch0 = G.lv[0].pitch;
+    A.blur_frame = G.blur_frame;
+    A.blur_off0 = G.lv[0].blur_off;
+    for (int l = 1; l < G.L; l++) A.lv[l].blur_off = G.lv[l].blur_off;
+    bands.assign((size_t)nband * G.L, make_int4(0, 0, 0, 0));
     for (int b = 0; b < nband; b++) {
+        bands[(size_t)b * G.L] = make_int4(0, 0, (int)((int64_t)G.lv[0].h * b / nband),
+                                           (int)((int64_t)G.lv[0].h * (b + 1) / nband));
         int lo = 0, hi = 0;  // computed rows of level l + 1
         for (int l = G.L - 1; l >= 1; l--) {
             const OrbgLevel &L = G.lv[l];
-            int olo = (int)((int64_t)L.h * b / nband), ohi = (int)((int64_t)L.h * (b + 1) / nband);
+            const int own_lo = (int)((int64_t)L.h * b / nband), own_hi = (int)((int64_t)L.h * (b + 1) / nband);
+            int olo = own_lo, ohi = own_hi;
+            if (fuse_blur && own_hi > own_lo) {
+                olo = std::max(own_lo - 3, 0);
+                ohi = std::min(own_hi + 3, L.h);
+            }
             if (l < G.L - 1 && hi > lo) {
                 const int2 *yt = rtab.data() + G.lv[l + 1].ytab_off;
                 const int slo = yt[lo].x & 0xFFFF, shi = (yt[hi - 1].x >> 16) + 1;
@@ -673,7 +693,7 @@ static bool make_pyr_tables(const OrbgGeom &G, const std::vector<int2> &rtab, in
                     ohi = shi;
                 }
             }
-            bands[(size_t)b * G.L + l] = make_int2(olo, ohi);
+            bands[(size_t)b * G.L + l] = make_int4(olo, ohi, own_lo, own_hi);
             lo = olo;
             hi = ohi;
         }
@@ -1135,9 +1155,13 @@ static int plan(orbg_ctx *c, int w, int h, int batch)
         const char *e = getenv("ORBG_PYR"), *nb = getenv("ORBG_PYR_NB");
         std::vector<uint4> pt;
         std::vector<int4> yt4;
-        std::vector<int2> bd;
+        std::vector<int4> bd;
         PyrArgs A{};
-        c->pyr_ok = (!e || atoi(e)) && make_pyr_tables(G, rtab, nb ? atoi(nb) : 4, pt, yt4, bd, A);
+        // ORBG_PYR_BLUR (A/B): 0 k_blur2 launches, 1 every level blurred inside k_pyramid,
+        // 2 levels >= 1 inside k_pyramid and level 0 by k_blur2 (beside it on the side stream)
+        const char *fb = getenv("ORBG_PYR_BLUR");
+        c->pyr_ok = (!e || atoi(e)) && make_pyr_tables(G, rtab, nb ? atoi(nb) : 4, pt, yt4, bd, A,
+                                                       fb ? atoi(fb) : 0);
         if (c->pyr_ok) {
             if ((rc = dalloc(&c->d_ptab, pt.size())) || (rc = dalloc(&c->d_ytab4, yt4.size())) ||
                 (rc = dalloc(&c->d_bands, bd.size()))) {
@@ -1146,7 +1170,7 @@ static int plan(orbg_ctx *c, int w, int h, int batch)
             }
             HIPCHK(hipMemcpy(c->d_ptab, pt.data(), pt.size() * sizeof(uint4), hipMemcpyHostToDevice));
             HIPCHK(hipMemcpy(c->d_ytab4, yt4.data(), yt4.size() * sizeof(int4), hipMemcpyHostToDevice));
-            HIPCHK(hipMemcpy(c->d_bands, bd.data(), bd.size() * sizeof(int2), hipMemcpyHostToDevice));
+            HIPCHK(hipMemcpy(c->d_bands, bd.data(), bd.size() * sizeof(int4), hipMemcpyHostToDevice));
             c->pyr_args = A;
             const char *wg = getenv("ORBG_PYR_WG");
             c->pyr_wg = wg ? std::min(std::max(atoi(wg) / 64 * 64, 64), 1024) : 512;
@@ -1399,8 +1423,8 @@ static hipError_t launch_pyramid(orbg_ctx *c, hipStream_t st, const uint8_t *d_i
         const uint8_t *img_end = d_imgs + (int64_t)(B - 1) * fs + (int64_t)(L0.h - 1) * pitch + L0.w;
         PROF_LAUNCH(c, "resize",
                     hipLaunchKernelGGL(k_pyramid, dim3(c->pyr_args.nband * B), dim3(c->pyr_wg), 0, st,
-                                       c->pyr_args, c->d_ptab, c->d_ytab4, c->d_bands, d_imgs, fs,
-                                       pitch, img_end, c->d_pyr, B));
+                                       c->pyr_args, c->d_geom, c->d_ptab, c->d_ytab4, c->d_bands,
+                                       d_imgs, fs, pitch, img_end, c->d_pyr, c->d_blur, B));
         return hipGetLastError();
     }
     for (int l = 1; l < G.L; l++) {
@@ -1476,6 +1500,9 @@ static int launch_extract_pipe(orbg_ctx *c, const uint8_t *d_imgs, int B, int pi
         }
         const bool side = c->fstream && G.L > 1;
         const int n0 = side ? G.lv[1].cell_base : 0;
+        // fused: k_pyramid blurs levels >= 1 itself (fuse_blur 2) or every level (1)
+        const int fz = c->pyr_ok ? c->pyr_args.fuse_blur : 0;
+        const bool fused = fz != 0;
         if (side) {
             // level 0 beside the pyramid: FAST cells, then its GaussianBlur
             HIPCHK(hipEventRecord(c->ev_pfork[s], st));
@@ -1484,14 +1511,14 @@ static int launch_extract_pipe(orbg_ctx *c, const uint8_t *d_imgs, int B, int pi
                 hipStream_t st = c->fstream;  // PROF_LAUNCH records on `st`
                 HIPCHK(launch_fast_cells(c, st, d_imgs, B, pitch, fs, 0, n0));
                 HIPCHK(hipEventRecord(c->ev_f0[s], st));
-                HIPCHK(launch_blur_levels(c, st, d_imgs, B, pitch, fs, 0, 1));
+                if (fz != 1) HIPCHK(launch_blur_levels(c, st, d_imgs, B, pitch, fs, 0, 1));
                 HIPCHK(hipEventRecord(c->ev_b0[s], st));
             }
         }
         HIPCHK(launch_pyramid(c, st, d_imgs, B, pitch, fs));
         // blur_side: levels 1.. of the GaussianBlur on the side stream too, beside the FAST
         // cells of levels 1.. (both need only the pyramid)
-        const bool bside = side && c->blur_side;
+        const bool bside = side && c->blur_side && !fused;
         if (bside) {
             HIPCHK(hipEventRecord(c->ev_pyr[s], st));
             HIPCHK(hipStreamWaitEvent(c->fstream, c->ev_pyr[s], 0));
@@ -1502,7 +1529,8 @@ static int launch_extract_pipe(orbg_ctx *c, const uint8_t *d_imgs, int B, int pi
         HIPCHK(launch_fast_cells(c, st, d_imgs, B, pitch, fs, n0, G.ncells - n0));
         if (side) HIPCHK(hipStreamWaitEvent(st, c->ev_f0[s], 0));
         HIPCHK(hipEventRecord(c->ev_cells[s], st));
-        if (!bside) HIPCHK(launch_blur_levels(c, st, d_imgs, B, pitch, fs, side ? 1 : 0, G.L));
+        if (!bside && !fused) HIPCHK(launch_blur_levels(c, st, d_imgs, B, pitch, fs, side ? 1 : 0, G.L));
+        if (!side && fz == 2) HIPCHK(launch_blur_levels(c, st, d_imgs, B, pitch, fs, 0, 1));
         if (side) HIPCHK(hipStreamWaitEvent(st, c->ev_b0[s], 0));
         HIPCHK(hipEventRecord(c->ev_front[s], st));
     }
@@ -1584,8 +1612,11 @@ static int launch_extract(orbg_ctx *c, const uint8_t *d_imgs, int B, int pitch, 
     // the quadtree stream beside the resize chain (latency-bound small launches)
     const bool fast0 = c->fast0_mode && oct_mode && G.L > 1;
     const int n0 = G.L > 1 ? G.lv[1].cell_base : G.ncells;
+    // fused: k_pyramid blurs levels >= 1 itself (fuse_blur 2) or every level (1)
+    const int fz = c->pyr_ok ? c->pyr_args.fuse_blur : 0;
+    const bool fused = fz != 0;
     // blur0: the level-0 GaussianBlur follows them there (ORBG_BLUR0)
-    const bool blur0 = fast0 && c->blur0_mode;
+    const bool blur0 = fast0 && c->blur0_mode && fz != 1;
     auto launch_fast = [&](hipStream_t q, int cb, int cn) {
         return launch_fast_cells(c, q, d_imgs, B, pitch, fs, cb, cn);
     };
@@ -1627,7 +1658,8 @@ static int launch_extract(orbg_ctx *c, const uint8_t *d_imgs, int B, int pitch, 
         if (blur0) HIPCHK(launch_blur_levels(c, st, d_imgs, B, pitch, fs, 0, 1));
         if (oct_mode) HIPCHK(hipEventRecord(c->ev_oct, st));
     }
-    HIPCHK(launch_blur_levels(c, st, d_imgs, B, pitch, fs, blur0 ? 1 : 0, G.L));
+    if (!fused) HIPCHK(launch_blur_levels(c, st, d_imgs, B, pitch, fs, blur0 ? 1 : 0, G.L));
+    else if (fz == 2 && !blur0) HIPCHK(launch_blur_levels(c, st, d_imgs, B, pitch, fs, 0, 1));
     if (oct_mode != 2 && G.L > 1)
         PROF_LAUNCH(c, "octree",
                     hipLaunchKernelGGL(k_octree_lds, dim3(B, G.L - 1), dim3(512),
@@ -2644,18 +2676,33 @@ extern "C" int orbg_ba_build_system_device(orbg_ctx *c, const orbg_pose *d_poses
 struct orbg_ba_graph {
     int device = 0, nedge = 0, npose = 0, npoint = 0;
     std::vector<BaPackedEdge> h;  // host copy (orbg_ba_graph_set_active rewrites the flags)
+    // orbg_ba_graph_set_active uploads from pinned staging with no host synchronisation; the
+    // next call waits for the previous upload (ev_up) before rewriting the staging buffer
+    BaPackedEdge *h_pin = nullptr;
+    hipEvent_t ev_up = nullptr;
+    bool up_pending = false;
     BaPackedEdge *d_edges = nullptr;
     BaCam *d_cam = nullptr;
     BaInfo *d_info = nullptr;
     int32_t *d_off = nullptr, *d_pe = nullptr, *d_qoff = nullptr, *d_qe = nullptr;
+    // the build's precomputed structure (BaGraphDev, orbg_internal.h)
+    int32_t *d_special = nullptr, *d_slice_off = nullptr, *d_slice_pose = nullptr;
+    double *d_part = nullptr;
+    BaGraphDev gd{};
 };
 
 static void ba_graph_free(orbg_ba_graph *g)
 {
     if (!g) return;
     hipSetDevice(g->device);
+    if (g->ev_up) {
+        if (g->up_pending) hipEventSynchronize(g->ev_up);
+        hipEventDestroy(g->ev_up);
+    }
+    if (g->h_pin) hipHostFree(g->h_pin);
     for (void *p : {(void *)g->d_edges, (void *)g->d_cam, (void *)g->d_info, (void *)g->d_off,
-                    (void *)g->d_pe, (void *)g->d_qoff, (void *)g->d_qe})
+                    (void *)g->d_pe, (void *)g->d_qoff, (void *)g->d_qe, (void *)g->d_special,
+                    (void *)g->d_slice_off, (void *)g->d_slice_pose, (void *)g->d_part})
         if (p) hipFree(p);
     delete g;
 }
@@ -2728,6 +2775,20 @@ extern "C" int orbg_ba_graph_create(orbg_ctx *c, const orbg_edge *edges, int ned
             qe[qfill[edges[i].point]++] = i;
         }
     }
+    // pose slices (ORBG_BA_SLICE edges of one pose each)
+    std::vector<int32_t> soff(npose + 1, 0), spose;
+    for (int p = 0; p < npose; p++) {
+        const int n = (off[p + 1] - off[p] + ORBG_BA_SLICE - 1) / ORBG_BA_SLICE;
+        soff[p + 1] = soff[p] + n;
+        for (int k = 0; k < n; k++) spose.push_back(p);
+    }
+    const size_t nsl = spose.size();
+    // special points: their point-major slots span two k_ba_edges workgroups, or no edge
+    std::vector<int32_t> special;
+    for (int q = 0; q < npoint; q++)
+        if (qoff[q + 1] == qoff[q] ||
+            qoff[q] / ORBG_BA_EDGES_TPB != (qoff[q + 1] - 1) / ORBG_BA_EDGES_TPB)
+            special.push_back(q);
     HIPCHK(hipSetDevice(c->device));
     orbg_ba_graph *g = new orbg_ba_graph;
     g->device = c->device;
@@ -2738,10 +2799,20 @@ extern "C" int orbg_ba_graph_create(orbg_ctx *c, const orbg_edge *edges, int ned
     if ((rc = dalloc(&g->d_edges, h.size())) || (rc = dalloc(&g->d_cam, hc.size())) ||
         (rc = dalloc(&g->d_info, hi.size())) || (rc = dalloc(&g->d_off, off.size())) ||
         (rc = dalloc(&g->d_pe, pe.size())) || (rc = dalloc(&g->d_qoff, qoff.size())) ||
-        (rc = dalloc(&g->d_qe, qe.size()))) {
+        (rc = dalloc(&g->d_qe, qe.size())) ||
+        (rc = dalloc(&g->d_special, std::max<size_t>(special.size(), 1))) ||
+        (rc = dalloc(&g->d_slice_off, soff.size())) ||
+        (rc = dalloc(&g->d_slice_pose, std::max<size_t>(nsl, 1))) ||
+        (rc = dalloc(&g->d_part, std::max<size_t>(nsl, 1) * 42))) {
         ba_graph_free(g);
         return rc;
     }
+    g->gd.special = g->d_special;
+    g->gd.nspecial = (int)special.size();
+    g->gd.slice_off = g->d_slice_off;
+    g->gd.slice_pose = g->d_slice_pose;
+    g->gd.nslice = (int)nsl;
+    g->gd.part = g->d_part;
     auto up = [&](void *d, const void *src, size_t n) {
         return n ? hipMemcpyAsync(d, src, n, hipMemcpyHostToDevice, c->stream) : hipSuccess;
     };
@@ -2752,6 +2823,9 @@ extern "C" int orbg_ba_graph_create(orbg_ctx *c, const orbg_edge *edges, int ned
         up(g->d_pe, pe.data(), (size_t)nedge * 4) != hipSuccess ||
         up(g->d_qoff, qoff.data(), qoff.size() * 4) != hipSuccess ||
         up(g->d_qe, qe.data(), (size_t)nedge * 4) != hipSuccess ||
+        up(g->d_special, special.data(), special.size() * 4) != hipSuccess ||
+        up(g->d_slice_off, soff.data(), soff.size() * 4) != hipSuccess ||
+        up(g->d_slice_pose, spose.data(), nsl * 4) != hipSuccess ||
         hipStreamSynchronize(c->stream) != hipSuccess) {
         ba_graph_free(g);
         return set_err(ORBG_EIO, "graph upload failed");
@@ -2776,11 +2850,20 @@ extern "C" int orbg_ba_graph_set_active(orbg_ctx *c, orbg_ba_graph *g, const uin
         g->h[i].flags = (g->h[i].flags & ~4u) | (active[i] ? 4u : 0u);
     HIPCHK(hipSetDevice(c->device));
     if (g->nedge) {
-        // the stream may still read the previous flags: upload in order on it, and keep the
-        // host copy alive until it is done
-        HIPCHK(hipMemcpyAsync(g->d_edges, g->h.data(), (size_t)g->nedge * sizeof(BaPackedEdge),
+        // in stream order after the builds that read the previous flags, from pinned staging:
+        // no host synchronisation (only the previous upload's, before the staging is rewritten)
+        if (!g->h_pin) {
+            if (hipHostMalloc((void **)&g->h_pin, (size_t)g->nedge * sizeof(BaPackedEdge),
+                              hipHostMallocDefault) != hipSuccess)
+                return set_err(ORBG_ENOMEM, "pinned staging of %d edges", g->nedge);
+            HIPCHK(hipEventCreateWithFlags(&g->ev_up, hipEventDisableTiming));
+        }
+        if (g->up_pending) HIPCHK(hipEventSynchronize(g->ev_up));
+        memcpy(g->h_pin, g->h.data(), (size_t)g->nedge * sizeof(BaPackedEdge));
+        HIPCHK(hipMemcpyAsync(g->d_edges, g->h_pin, (size_t)g->nedge * sizeof(BaPackedEdge),
                               hipMemcpyHostToDevice, c->stream));
-        HIPCHK(hipStreamSynchronize(c->stream));
+        HIPCHK(hipEventRecord(g->ev_up, c->stream));
+        g->up_pending = true;
     }
     return ORBG_OK;
 }
@@ -2795,12 +2878,10 @@ extern "C" int orbg_ba_graph_build_system(orbg_ctx *c, orbg_ba_graph *g, const o
         (g->npoint && (!d_points || !d_hpoint || !d_bpoint)))
         return set_err(ORBG_EINVAL, "NULL device array");
     HIPCHK(hipSetDevice(c->device));
-    void *s;
-    int rc = scratch(c, ba_rows_bytes(g->nedge, g->npose), &s);
-    if (rc) return rc;
-    rc = launch_ba_graph(c->stream, d_poses, g->npose, d_points, g->npoint, g->d_edges, g->d_cam,
-                         g->d_info, g->nedge, g->d_off, g->d_pe, g->d_qoff, g->d_qe, d_hpl,
-                         d_hpose, d_bpose, d_hpoint, d_bpoint, (double *)s, &c->prof);
+    const int rc = launch_ba_graph(c->stream, d_poses, g->npose, d_points, g->npoint, g->d_edges,
+                                   g->d_cam, g->d_info, g->nedge, g->d_off, g->d_pe, g->d_qoff,
+                                   g->d_qe, g->gd, d_hpl, d_hpose, d_bpose, d_hpoint, d_bpoint,
+                                   &c->prof);
     if (rc) return set_err(ORBG_EIO, "BA kernel launch failed");
     return ORBG_OK;
 }
@@ -3475,5 +3556,127 @@ extern "C" int orbg_bow_transform(orbg_ctx *c, const orbg_vocab *v, const uint8_
     c->prof.collect();
     *nbow = nb;
     *nfv = nf;
+    return ORBG_OK;
+}
+
+// ---------------------------------------------------------------------------
+// ORBmatcher::SearchByBoW(KeyFrame*, Frame&) (bow_match_kernels.hip)
+// ---------------------------------------------------------------------------
+extern "C" int orbg_search_by_bow_batch_device(orbg_ctx *c, const orbg_bow_frames *kf,
+                                               const orbg_bow_frames *f, int cap,
+                                               const int32_t *d_kf_index, const int32_t *d_f_index,
+                                               int npairs, float nnratio, int check_ori,
+                                               int32_t *d_match, int32_t *d_nmatch)
+{
+    if (!c || !kf || !f) return set_err(ORBG_EINVAL, "NULL argument");
+    if (npairs < 0 || cap <= 0 || cap > 8192) return set_err(ORBG_EINVAL, "bad npairs / cap");
+    if (npairs == 0) return ORBG_OK;
+    if (!d_kf_index || !d_f_index || !d_match || !d_nmatch || !kf->desc || !kf->kps ||
+        !kf->fv_nodes || !kf->fv_off || !kf->fv_feats || !kf->nfv || !f->desc || !f->kps ||
+        !f->counts || !f->fv_nodes || !f->fv_off || !f->fv_feats || !f->nfv)
+        return set_err(ORBG_EINVAL, "NULL device array");
+    HIPCHK(hipSetDevice(c->device));
+    HIPCHK(order_after_caller(c));
+    hipStream_t st = c->mstream;  // PROF_LAUNCH records on `st`
+    int rc = 0;
+    PROF_LAUNCH(c, "bow_match",
+                rc = launch_bow_match(st, *kf, *f, cap, d_kf_index, d_f_index, npairs, nnratio,
+                                      check_ori, d_match, d_nmatch));
+    if (rc) return set_err(ORBG_EIO, "k_bow_match launch failed");
+    return ORBG_OK;
+}
+
+extern "C" int orbg_search_by_bow(orbg_ctx *c, const uint8_t *kf_desc, const float *kf_angle,
+                                  const uint8_t *kf_valid, int n_kf, const int32_t *kf_fv_nodes,
+                                  const int32_t *kf_fv_off, const int32_t *kf_fv_feats, int kf_nfv,
+                                  const uint8_t *f_desc, const float *f_angle, int n_f,
+                                  const int32_t *f_fv_nodes, const int32_t *f_fv_off,
+                                  const int32_t *f_fv_feats, int f_nfv, float nnratio,
+                                  int check_ori, int32_t *match, int *nmatches)
+{
+    if (!c || !match || !nmatches) return set_err(ORBG_EINVAL, "NULL argument");
+    if (n_kf < 0 || n_f < 0 || kf_nfv < 0 || f_nfv < 0 || kf_nfv > std::max(n_kf, 0) ||
+        f_nfv > std::max(n_f, 0))
+        return set_err(ORBG_EINVAL, "bad sizes");
+    if ((n_kf && (!kf_desc || !kf_angle)) || (n_f && (!f_desc || !f_angle)) ||
+        (kf_nfv && (!kf_fv_nodes || !kf_fv_off || !kf_fv_feats)) ||
+        (f_nfv && (!f_fv_nodes || !f_fv_off || !f_fv_feats)))
+        return set_err(ORBG_EINVAL, "NULL input array");
+    *nmatches = 0;
+    for (int i = 0; i < n_f; i++) match[i] = -1;
+    if (!n_f || !n_kf || !kf_nfv || !f_nfv) return ORBG_OK;
+    for (int j = 0; j < kf_nfv; j++)
+        for (int k = kf_fv_off[j]; k < kf_fv_off[j + 1]; k++)
+            if (kf_fv_feats[k] < 0 || kf_fv_feats[k] >= n_kf)
+                return set_err(ORBG_EINVAL, "KF feature index out of range");
+    for (int j = 0; j < f_nfv; j++)
+        for (int k = f_fv_off[j]; k < f_fv_off[j + 1]; k++)
+            if (f_fv_feats[k] < 0 || f_fv_feats[k] >= n_f)
+                return set_err(ORBG_EINVAL, "F feature index out of range");
+    HIPCHK(hipSetDevice(c->device));
+    // one buffer: two frames (KF = 0, F = 1) at cap = max(n_kf, n_f)
+    const int cap = std::max(n_kf, n_f);
+    if (cap > 8192) return set_err(ORBG_ENOTSUP, "more than 8192 features");
+    const size_t cp = (size_t)cap;
+    size_t o = 0;
+    auto take = [&](size_t bytes) {
+        const size_t r = o;
+        o += al256(bytes);
+        return r;
+    };
+    const size_t o_desc = take(2 * cp * 32), o_kps = take(2 * cp * sizeof(orbg_keypoint)),
+                 o_cnt = take(2 * 4), o_nodes = take(2 * cp * 4), o_off = take(2 * (cp + 1) * 4),
+                 o_feats = take(2 * cp * 4), o_nfv = take(2 * 4), o_val = take(2 * cp),
+                 o_idx = take(2 * 4), o_match = take(cp * 4), o_nm = take(4);
+    uint8_t *hs;
+    int rc = stage(c, o, &hs);
+    if (rc) return rc;
+    HIPCHK(hipStreamSynchronize(c->stream));
+    memset(hs, 0, o);
+    memcpy(hs + o_desc, kf_desc, (size_t)n_kf * 32);
+    memcpy(hs + o_desc + cp * 32, f_desc, (size_t)n_f * 32);
+    orbg_keypoint *hk = (orbg_keypoint *)(hs + o_kps);
+    for (int i = 0; i < n_kf; i++) hk[i].angle = kf_angle[i];
+    for (int i = 0; i < n_f; i++) hk[cp + i].angle = f_angle[i];
+    int32_t *hc = (int32_t *)(hs + o_cnt);
+    hc[0] = n_kf;
+    hc[1] = n_f;
+    memcpy(hs + o_nodes, kf_fv_nodes, (size_t)kf_nfv * 4);
+    memcpy(hs + o_nodes + cp * 4, f_fv_nodes, (size_t)f_nfv * 4);
+    memcpy(hs + o_off, kf_fv_off, (size_t)(kf_nfv + 1) * 4);
+    memcpy(hs + o_off + (cp + 1) * 4, f_fv_off, (size_t)(f_nfv + 1) * 4);
+    memcpy(hs + o_feats, kf_fv_feats, (size_t)kf_fv_off[kf_nfv] * 4);
+    memcpy(hs + o_feats + cp * 4, f_fv_feats, (size_t)f_fv_off[f_nfv] * 4);
+    int32_t *hn = (int32_t *)(hs + o_nfv);
+    hn[0] = kf_nfv;
+    hn[1] = f_nfv;
+    if (kf_valid)
+        memcpy(hs + o_val, kf_valid, (size_t)n_kf);
+    else
+        memset(hs + o_val, 1, (size_t)n_kf);
+    int32_t *hi = (int32_t *)(hs + o_idx);
+    hi[0] = 0;
+    hi[1] = 1;
+    void *d;
+    if ((rc = scratch(c, o, &d))) return rc;
+    uint8_t *db = (uint8_t *)d;
+    HIPCHK(hipMemcpyAsync(db, hs, o, hipMemcpyHostToDevice, c->stream));
+    orbg_bow_frames K{}, F{};
+    K.desc = F.desc = db + o_desc;
+    K.kps = F.kps = (const orbg_keypoint *)(db + o_kps);
+    K.counts = F.counts = (const int32_t *)(db + o_cnt);
+    K.fv_nodes = F.fv_nodes = (const int32_t *)(db + o_nodes);
+    K.fv_off = F.fv_off = (const int32_t *)(db + o_off);
+    K.fv_feats = F.fv_feats = (const int32_t *)(db + o_feats);
+    K.nfv = F.nfv = (const int32_t *)(db + o_nfv);
+    K.valid = db + o_val;
+    const int32_t *di = (const int32_t *)(db + o_idx);
+    rc = launch_bow_match(c->stream, K, F, cap, di, di + 1, 1, nnratio, check_ori,
+                          (int32_t *)(db + o_match), (int32_t *)(db + o_nm));
+    if (rc) return set_err(ORBG_EIO, "k_bow_match launch failed");
+    HIPCHK(hipMemcpyAsync(hs + o_match, db + o_match, cp * 4 + 256, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(hipStreamSynchronize(c->stream));
+    memcpy(match, hs + o_match, (size_t)n_f * 4);
+    memcpy(nmatches, hs + o_nm, 4);
     return ORBG_OK;
 }

@@ -40,6 +40,18 @@ struct BaCam {
 struct BaInfo {
     double inv_sigma2, huber_delta;
 };
+// an orbg_ba_graph's device-side structure (ba_kernels.hip launch_ba_graph), built once at
+// orbg_ba_graph_create: special = the points whose k_ba_edges slots span two workgroups or
+// that have no edge; the pose slices of ORBG_BA_SLICE edges and their partial sums
+#define ORBG_BA_SLICE 64
+#define ORBG_BA_EDGES_TPB 256
+struct BaGraphDev {
+    const int32_t *special;   // special points (above)
+    int32_t nspecial;
+    const int32_t *slice_off, *slice_pose;  // pose p owns slices slice_off[p] .. [p+1]-1
+    int32_t nslice;
+    double *part;             // [nslice][42] pose-block partials
+};
 #define ORBG_BA_MAX_CAMS 256
 #define ORBG_BA_MAX_INFOS 65536
 

@@ -6,6 +6,9 @@
 #define PYR_ROWS 8   // output rows per work item (one lane)
 #define PYR_COLS 8   // output columns per work item
 #define PYR_NS 11    // max source rows per item: floor(7 * 1.2) + 1 + 2 (host checks)
+#ifndef PYR_BLUR_SEG
+#define PYR_BLUR_SEG 16  // k_pyramid's fused GaussianBlur: output rows per wave tile
+#endif
 #ifndef PYR_PF
 #define PYR_PF 4     // source rows in flight ahead of the one being summed
 #endif
@@ -28,10 +31,17 @@ struct PyrLevelArgs {
     int32_t clamp_row;            // first output row with sy0 == sy1 (dh if none)
     int32_t guard_row;            // level 1: first output row reading the caller's last row
     int32_t pad;
+    int64_t blur_off;             // byte offset of the level in a frame's blurred pyramid
 };
 
+// bands[b * L + l] = {first, end} rows of level l (l >= 1) band b computes (its own rows, the
+// rows its higher levels read and, with fuse_blur, the +-3 rows its own blurred rows read),
+// {own first, own end} rows of level l whose GaussianBlur band b writes (level 0 too)
 struct PyrArgs {
     int32_t L, nband;
     int64_t pyr_frame;
+    int32_t fuse_blur;            // GaussianBlur in the same launch: 1 every level, 2 levels >= 1
+    int32_t w0, h0, bpitch0;      // level 0 size and its blurred row pitch
+    int64_t blur_frame, blur_off0;
     PyrLevelArgs lv[16];
 };

@@ -21,6 +21,7 @@
 #include <hip/hip_runtime.h>
 
 #include "orbg_device.h"
+#include "blur_device.h"
 #include "pyramid_args.h"
 
 #pragma clang fp contract(off)
@@ -189,70 +190,98 @@ __device__ __forceinline__ void pyr_fix(const uint8_t *src, int spitch, uint8_t 
 }
 
 // grid: nband * nframes workgroups (XCD-remapped: a frame's bands share an L2); levels
-// [1, L) in order.  bands[b * L + l] = {first, end} rows of level l this band computes.
-// Per level: fast wave items (row group of PYR_ROWS rows x chunk of 64 octets), then the
-// fix-up rows (one lane per (row, octet)): the octets from P.fix_oct on (FixedPtCast
-// columns, a partial last octet) for every row, every octet of the sy0 == sy1 rows from
-// P.clamp_row on, and for the caller image every octet of the rows whose fast loads could
-// pass the buffer (from P.guard_row on, last frame only).
-__global__ __launch_bounds__(1024) void k_pyramid(PyrArgs A, const uint4 *__restrict__ ptab,
+// [1, L) in order, one phase per level with a workgroup barrier after it.  Phase p computes
+// level p + 1's rows of the band: fast wave items (row group of PYR_ROWS rows x chunk of 64
+// octets), then the fix-up rows (one lane per (row, octet)): the octets from P.fix_oct on
+// (FixedPtCast columns, a partial last octet) for every row, every octet of the sy0 == sy1 rows
+// from P.clamp_row on, and for the caller image every octet of the rows whose fast loads could
+// pass the buffer (from P.guard_row on, last frame only).  With A.fuse_blur the same phase also
+// blurs level p's own rows (k_blur2's wave tiles, blur_device.h): level p is complete in this
+// workgroup (level 0 is the caller's image), still in L2, and no second kernel re-reads the
+// pyramid from HBM to blur it (ORBextractor.cc:1375-1377 after :1400-1443).
+__global__ __launch_bounds__(1024) void k_pyramid(PyrArgs A, const OrbgGeom *__restrict__ g,
+                                                 const uint4 *__restrict__ ptab,
                                                  const int4 *__restrict__ ytab_all,
-                                                 const int2 *__restrict__ bands,
+                                                 const int4 *__restrict__ bands,
                                                  const uint8_t *__restrict__ img0,
                                                  int64_t img_fs, int img_pitch,
                                                  const uint8_t *img_end, uint8_t *pyr,
-                                                 int nframes)
+                                                 uint8_t *blur, int nframes)
 {
     const int id = xcd_remap(blockIdx.x, gridDim.x);
     const int f = id / A.nband, band = id - f * A.nband;
     const int lane = threadIdx.x & 63;
     const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int nw = blockDim.x >> 6;
     uint8_t *fpyr = pyr + (int64_t)f * A.pyr_frame;
-    for (int l = 1; l < A.L; l++) {
-        const PyrLevelArgs &P = A.lv[l];
-        const bool lvl1 = l == 1;
-        const uint8_t *src = lvl1 ? img0 + (int64_t)f * img_fs : fpyr + P.src_off;
-        const int spitch = lvl1 ? img_pitch : P.spitch;
-        uint8_t *dst = fpyr + P.dst_off;
-        const int2 cr = bands[band * A.L + l];
-        const int4 *ytab = ytab_all + P.ytab_off;
-        const uint4 *ptab_l = ptab + P.ptab_off;
-        // rows [cr.x, fast_end) go through the fast path (the caller image's last frame
-        // stops before its guarded rows)
-        const int fast_end = (lvl1 && f == nframes - 1) ? min(cr.y, P.guard_row) : cr.y;
-        const int ngroups = max(fast_end - cr.x, 0) / PYR_ROWS + ((max(fast_end - cr.x, 0) % PYR_ROWS) != 0);
-        const int nchunk = (P.fix_oct + 63) >> 6;
-        const int items = ngroups * nchunk;
-        const int nw = blockDim.x >> 6;
-        for (int it = wv; it < items; it += nw) {
-            const int g = it / nchunk, cc = it - g * nchunk;
-            const int q = 64 * cc + lane;
-            const int y0 = cr.x + g * PYR_ROWS, n = min(PYR_ROWS, fast_end - y0);
-            pyr_wave_item(src, spitch, dst, P.dpitch, ytab, ptab_l + 5 * min(q, P.fix_oct - 1),
-                          q * PYR_COLS, q < P.fix_oct, y0, n);
-        }
-        // fix-up: (row, octet) pairs
-        {
-            const int nrow = cr.y - cr.x, nfo = P.noct - P.fix_oct;
-            const int clamp0 = max(P.clamp_row, cr.x), guard0 = max(fast_end, cr.x);
-            const int nclamp = max(cr.y - clamp0, 0), nguard = max(cr.y - guard0, 0);
-            const int n1 = nrow * nfo;                       // FixedPtCast / partial octets
-            const int n2 = n1 + nclamp * P.fix_oct;          // sy0 == sy1 rows
-            const int n3 = n2 + (guard0 < clamp0 ? min(nguard, clamp0 - guard0) : 0) * P.fix_oct;
-            for (int i = threadIdx.x; i < n3; i += blockDim.x) {
-                int dy, q;
-                if (i < n1) {
-                    dy = cr.x + i / nfo;
-                    q = P.fix_oct + i % nfo;
-                } else if (i < n2) {
-                    dy = clamp0 + (i - n1) / P.fix_oct;
-                    q = (i - n1) % P.fix_oct;
-                } else {
-                    dy = guard0 + (i - n2) / P.fix_oct;
-                    q = (i - n2) % P.fix_oct;
+    for (int ph = 0; ph < A.L; ph++) {
+        const int l = ph + 1;
+        if (l < A.L) {
+            const PyrLevelArgs &P = A.lv[l];
+            const bool lvl1 = l == 1;
+            const uint8_t *src = lvl1 ? img0 + (int64_t)f * img_fs : fpyr + P.src_off;
+            const int spitch = lvl1 ? img_pitch : P.spitch;
+            uint8_t *dst = fpyr + P.dst_off;
+            const int4 cr = bands[band * A.L + l];
+            const int4 *ytab = ytab_all + P.ytab_off;
+            const uint4 *ptab_l = ptab + P.ptab_off;
+            // rows [cr.x, fast_end) go through the fast path (the caller image's last frame
+            // stops before its guarded rows)
+            const int fast_end = (lvl1 && f == nframes - 1) ? min(cr.y, P.guard_row) : cr.y;
+            const int ngroups = max(fast_end - cr.x, 0) / PYR_ROWS + ((max(fast_end - cr.x, 0) % PYR_ROWS) != 0);
+            const int nchunk = (P.fix_oct + 63) >> 6;
+            const int items = ngroups * nchunk;
+            for (int it = wv; it < items; it += nw) {
+                const int gi = it / nchunk, cc = it - gi * nchunk;
+                const int q = 64 * cc + lane;
+                const int y0 = cr.x + gi * PYR_ROWS, n = min(PYR_ROWS, fast_end - y0);
+                pyr_wave_item(src, spitch, dst, P.dpitch, ytab, ptab_l + 5 * min(q, P.fix_oct - 1),
+                              q * PYR_COLS, q < P.fix_oct, y0, n);
+            }
+            // fix-up: (row, octet) pairs
+            {
+                const int nrow = cr.y - cr.x, nfo = P.noct - P.fix_oct;
+                const int clamp0 = max(P.clamp_row, cr.x), guard0 = max(fast_end, cr.x);
+                const int nclamp = max(cr.y - clamp0, 0), nguard = max(cr.y - guard0, 0);
+                const int n1 = nrow * nfo;                       // FixedPtCast / partial octets
+                const int n2 = n1 + nclamp * P.fix_oct;          // sy0 == sy1 rows
+                const int n3 = n2 + (guard0 < clamp0 ? min(nguard, clamp0 - guard0) : 0) * P.fix_oct;
+                for (int i = threadIdx.x; i < n3; i += blockDim.x) {
+                    int dy, q;
+                    if (i < n1) {
+                        dy = cr.x + i / nfo;
+                        q = P.fix_oct + i % nfo;
+                    } else if (i < n2) {
+                        dy = clamp0 + (i - n1) / P.fix_oct;
+                        q = (i - n1) % P.fix_oct;
+                    } else {
+                        dy = guard0 + (i - n2) / P.fix_oct;
+                        q = (i - n2) % P.fix_oct;
+                    }
+                    pyr_fix(src, spitch, dst, P.dpitch, P.dw, ytab, ptab_l + 5 * q, q * PYR_COLS,
+                            dy, img_end, lvl1);
                 }
-                pyr_fix(src, spitch, dst, P.dpitch, P.dw, ytab, ptab_l + 5 * q, q * PYR_COLS, dy,
-                        img_end, lvl1);
+            }
+        }
+        if (A.fuse_blur == 1 || (A.fuse_blur == 2 && ph > 0)) {
+            // GaussianBlur of level ph's own rows of this band (every source row it reads is
+            // the band's: computed in the phase before, the barrier orders it)
+            const int4 bo = bands[band * A.L + ph];
+            const bool l0 = ph == 0;
+            const int W = l0 ? A.w0 : A.lv[ph].dw, H = l0 ? A.h0 : A.lv[ph].dh;
+            const uint8_t *bsrc = l0 ? img0 + (int64_t)f * img_fs : fpyr + A.lv[ph].dst_off;
+            const int bp = l0 ? img_pitch : A.lv[ph].dpitch;
+            const int dp = l0 ? A.bpitch0 : A.lv[ph].dpitch;
+            uint8_t *bdst = blur + (int64_t)f * A.blur_frame + (l0 ? A.blur_off0 : A.lv[ph].blur_off);
+            const int ntx = (W + BLUR2_TW - 1) / BLUR2_TW;
+            const int nseg = (max(bo.w - bo.z, 0) + PYR_BLUR_SEG - 1) / PYR_BLUR_SEG;
+            if (nseg > 0) {
+                const Blur2Weights kw(g);
+                for (int it = wv; it < ntx * nseg; it += nw) {
+                    const int sg = it / ntx, tx = it - sg * ntx;
+                    blur2_tile<PYR_BLUR_SEG>(kw, bsrc, bp, W, H, bdst, dp, tx,
+                                             bo.z + sg * PYR_BLUR_SEG, bo.w, lane);
+                }
             }
         }
         // level l is complete in this workgroup before level l + 1 reads it (same CU: the

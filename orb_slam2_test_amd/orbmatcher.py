@@ -7,6 +7,7 @@ Reference: include/ORBmatcher.h:40-193, src/ORBmatcher.cc.
     d = ORBmatcher.DescriptorDistance(a, b)
     n, match = m.SearchByProjection(CurrentFrame, LastFrame, th, bMono)   # motion model
     n, match = m.SearchByProjection(F, vpMapPoints, th)                   # local map
+    n, match = m.SearchByBoW(pKF, F)                                      # reference KF / reloc
 
 ``Frame`` here carries just what the matcher reads from ORB_SLAM2::Frame
 (mvKeysUn, mDescriptors and the image bounds mnMinX/mnMaxX/mnMinY/mnMaxY that define
@@ -54,6 +55,12 @@ class Frame:
     # LastFrame.mvpMapPoints as LF_DTYPE records (+ their descriptors), one per keypoint
     points: np.ndarray = None
     point_desc: np.ndarray = None
+    # SearchByBoW: mvKeys (distorted keypoints; None = mvKeysUn), mFeatVec as the
+    # (fv_nodes, fv_off, fv_feats) arrays Vocabulary.transform_arrays returns, and on a
+    # KeyFrame map_valid[i] = "mvpMapPoints[i] && !mvpMapPoints[i]->isBad()" (None = all)
+    mvKeys: np.ndarray = None
+    mFeatVec: tuple = None
+    map_valid: np.ndarray = None
 
     @classmethod
     def from_extraction(cls, keypoints, descriptors, width, height):
@@ -107,6 +114,28 @@ class ORBmatcher:
             self.mfNNratio, 1 if self.mbCheckOrientation else 0, C.byref(nm)),
             "orbg_search_for_initialization")
         return nm.value, m12
+
+    def SearchByBoW(self, pKF, F):
+        """SearchByBoW(KeyFrame *pKF, Frame &F, vector<MapPoint*> &vpMapPointMatches)
+        (ORBmatcher.cc:195-348).  pKF and F are Frames carrying mFeatVec (pKF also map_valid).
+        Returns (nmatches, match): match[i] = the KeyFrame feature whose MapPoint is
+        vpMapPointMatches[i], -1 for NULL."""
+        def side(fr, keys):
+            d = np.ascontiguousarray(fr.mDescriptors, np.uint8).reshape(-1, 32)
+            a = np.ascontiguousarray(keys["angle"], np.float32)
+            nodes, off, feats = [np.ascontiguousarray(x, np.int32) for x in fr.mFeatVec]
+            return d, a, nodes, off, feats
+        kd, ka, kn, ko, kf = side(pKF, pKF.mvKeysUn)
+        fd, fa, fn, fo, ff = side(F, F.mvKeys if F.mvKeys is not None else F.mvKeysUn)
+        kv = None if pKF.map_valid is None else np.ascontiguousarray(pKF.map_valid, np.uint8)
+        match = np.full(max(len(fd), 1), -1, np.int32)
+        nm = C.c_int()
+        L.check(L.lib().orbg_search_by_bow(
+            _ctx(self.device).handle, L.ptr(kd), L.ptr(ka), L.ptr(kv), len(kd), L.ptr(kn),
+            L.ptr(ko), L.ptr(kf), len(kn), L.ptr(fd), L.ptr(fa), len(fd), L.ptr(fn), L.ptr(fo),
+            L.ptr(ff), len(fn), self.mfNNratio, 1 if self.mbCheckOrientation else 0,
+            L.ptr(match), C.byref(nm)), "orbg_search_by_bow")
+        return nm.value, match[:len(fd)]
 
     def hamming_knn2(self, query_desc, train_desc):
         """Brute-force 2-NN: (best_idx, best_dist, second_dist) per query row."""

@@ -163,16 +163,11 @@ def test_build_system_compact_h_pl(oracle):
     assert rel(hpl, reo["hpl"]) < RTOL
 
 
-def test_graph_packed_equals_records(oracle):
-    """orbg_ba_graph (packed 24-byte edges + deduplicated camera / information tables): the
-    same blocks, H_pl, chi2 and rho bits as the record entry points, also after the outlier
-    pass's set_active, and chi2 / rho equal to the oracle's."""
-    from orb_slam2_test_amd.optimizer import DeviceLBA
-    poses, pts, edges = concat_windows([S.ba_window(n_points=400, seed=120 + i) for i in range(3)])
-    edges["active"][::11] = 0
-    a = DeviceLBA(poses, pts, edges)
-    g = DeviceLBA(poses, pts, edges, graph=True)
-
+def _graph_vs_records(oracle, a, g, poses, pts, edges):
+    """H_pl, chi2, rho: the same bits on both paths.  Blocks: the graph's point blocks are the
+    oracle's sequential edge-order sums bit for bit (no atomics anywhere, a straddling point
+    summed by k_ba_special); pose blocks (slice sums in slice order) and the record path's
+    atomics agree to rounding."""
     def run(x):
         x.build_system()
         x.errors()
@@ -180,25 +175,52 @@ def test_graph_packed_equals_records(oracle):
         return [t.cpu().numpy() for t in (x.d_hpl, x.d_hpose, x.d_bpose, x.d_hpoint, x.d_bpoint,
                                           x.d_chi2, x.d_rho0)]
 
-    for u, v in zip(run(a), run(g)):
+    ra, rg = run(a), run(g)
+    for k in (0, 5, 6):
+        assert np.array_equal(ra[k], rg[k]), k
+    for k in (1, 2, 3, 4):
+        assert rel(rg[k], ra[k]) < 1e-12, k
+    _, rhp, rbp, rhq, rbq = oracle.ba_linearize(poses, pts, edges)
+    npt, npo = len(pts), len(poses)
+    assert np.array_equal(rg[3].reshape(-1)[:9 * npt], rhq.reshape(-1)), "graph H_ll != oracle"
+    assert np.array_equal(rg[4].reshape(-1)[:3 * npt], rbq.reshape(-1)), "graph b_l != oracle"
+    assert rel(rg[1].reshape(-1)[:36 * npo], rhp.reshape(-1)) < RTOL
+    assert rel(rg[2].reshape(-1)[:6 * npo], rbp.reshape(-1)) < RTOL
+    # deterministic: a second build gives the same bits
+    rg2 = run(g)
+    for u, v in zip(rg, rg2):
         assert np.array_equal(u, v)
+    return rg
+
+
+def test_graph_packed_equals_records(oracle):
+    """orbg_ba_graph (packed 24-byte edges + deduplicated camera / information tables): the
+    same H_pl, chi2 and rho bits as the record entry points, also after the outlier pass's
+    set_active, chi2 / rho equal to the oracle's, point blocks equal to the oracle's."""
+    from orb_slam2_test_amd.optimizer import DeviceLBA
+    poses, pts, edges = concat_windows([S.ba_window(n_points=400, seed=120 + i) for i in range(3)])
+    edges["active"][::11] = 0
+    a = DeviceLBA(poses, pts, edges)
+    g = DeviceLBA(poses, pts, edges, graph=True)
+    _graph_vs_records(oracle, a, g, poses, pts, edges)
     r = oracle.ba_errors(poses, pts, edges)
     chi2 = g.d_chi2.cpu().numpy()[:len(edges)]
     assert np.array_equal(chi2, r[1])
-    # the outlier pass: a different active set on the graph == records rebuilt with it
+    # the outlier pass: a different active set on the graph == records rebuilt with it (twice
+    # in a row: the second upload waits only for the first)
+    g.set_active(np.ones(len(edges), np.uint8))
     act = (np.arange(len(edges)) % 5 != 0).astype(np.uint8)
     g.set_active(act)
     e2 = edges.copy()
     e2["active"] = act
     b = DeviceLBA(poses, pts, e2)
-    for u, v in zip(run(b), run(g)):
-        assert np.array_equal(u, v)
+    _graph_vs_records(oracle, b, g, poses, pts, e2)
 
 
 def test_graph_several_cameras_and_informations(oracle):
     """The graph's camera / information tables with several entries (windows of different
-    calibrations, per-edge information and Huber deltas off the octave table): the same bits
-    as the record path."""
+    calibrations, per-edge information and Huber deltas off the octave table): the same
+    per-edge bits as the record path, point blocks equal to the oracle's."""
     from orb_slam2_test_amd.optimizer import DeviceLBA
     wins = [S.ba_window(n_points=300, seed=140 + i) for i in range(3)]
     for i, (_, _, e) in enumerate(wins):
@@ -210,15 +232,35 @@ def test_graph_several_cameras_and_informations(oracle):
     edges["huber_delta"][::17] = 2.0
     a = DeviceLBA(poses, pts, edges)
     g = DeviceLBA(poses, pts, edges, graph=True)
-    for x in (a, g):
-        x.build_system()
-        x.errors()
-        x.ctx.sync()
-    for u, v in zip((a.d_hpl, a.d_hpose, a.d_bpose, a.d_hpoint, a.d_bpoint, a.d_chi2, a.d_rho0),
-                    (g.d_hpl, g.d_hpose, g.d_bpose, g.d_hpoint, g.d_bpoint, g.d_chi2, g.d_rho0)):
-        assert np.array_equal(u.cpu().numpy(), v.cpu().numpy())
+    _graph_vs_records(oracle, a, g, poses, pts, edges)
     r = oracle.ba_errors(poses, pts, edges)
     assert np.array_equal(g.d_chi2.cpu().numpy()[:len(edges)], r[1])
+
+
+def test_graph_writes_every_block_without_fills(oracle):
+    """A graph build writes every vertex block itself (no zero fills): output buffers full of
+    NaN before the build, a point and a pose without edges (zero blocks), fixed poses (zero
+    blocks: g2o builds none), straddling points; point blocks equal to the oracle's bits."""
+    import torch
+    from orb_slam2_test_amd.optimizer import DeviceLBA
+    poses, pts, edges = concat_windows([S.ba_window(n_points=500, seed=150 + i) for i in range(2)])
+    poses = np.concatenate([poses, poses[:1]])       # a pose without edges
+    pts = np.concatenate([pts, pts[:2]])              # two points without edges
+    g = DeviceLBA(poses, pts, edges, graph=True)
+    for t in (g.d_hpose, g.d_bpose, g.d_hpoint, g.d_bpoint):
+        t.fill_(float("nan"))
+    torch.cuda.synchronize()
+    g.build_system()
+    g.ctx.sync()
+    hp, bp = g.d_hpose.cpu().numpy(), g.d_bpose.cpu().numpy()
+    hq, bq = g.d_hpoint.cpu().numpy(), g.d_bpoint.cpu().numpy()
+    assert not any(np.isnan(x).any() for x in (hp, bp, hq, bq))
+    assert not hp[-1].any() and not bp[-1].any() and not hq[-2:].any() and not bq[-2:].any()
+    fixed = poses["fixed"] != 0
+    assert fixed.any() and not hp[fixed].any() and not bp[fixed].any()
+    _, rhp, rbp, rhq, rbq = oracle.ba_linearize(poses, pts, edges)
+    assert np.array_equal(hq, rhq) and np.array_equal(bq, rbq)
+    assert rel(hp, rhp) < RTOL and rel(bp, rbp) < RTOL
 
 
 def test_graph_rejects_non_f32_observations():

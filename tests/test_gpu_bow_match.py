@@ -1,0 +1,154 @@
+"""GPU: ORBmatcher::SearchByBoW(KeyFrame*, Frame&, vector<MapPoint*>&)
+(src/ORBmatcher.cc:195-348; Tracking::TrackReferenceKeyFrame Tracking.cc:1069,
+Relocalization :2009) through the C ABI (k_bow_match, bow_match_kernels.hip) vs the CPU
+oracle (oracle/bow_oracle.c orc_search_by_bow), bit for bit: every match index and nmatches.
+
+Cases: the synthetic rule cases of tests/test_oracle_bow_match.py; real ORB features of
+consecutive synthetic KITTI frames with FeatureVectors from DBoW2's transform over a synthetic
+k = 10, L = 6 vocabulary (ORBvoc.txt's shape; the real file is a missing blob) at levelsup 4
+(ComputeBoW's) and at levelsup 6 (every feature in the root node: one node of ~2000 F
+features, the kernel's > 128-candidate path); invalid MapPoints; empty inputs; and the
+batched device entry over a batch of frames, frame t's reference KeyFrame = frame t - 1.
+"""
+import numpy as np
+import pytest
+
+from orb_slam2_test_amd import ORBVocabulary, synthetic as S
+from orb_slam2_test_amd import _lib as L
+from orb_slam2_test_amd.orbmatcher import Frame, ORBmatcher
+
+from test_oracle_bow_match import _case
+
+pytestmark = pytest.mark.gpu
+
+H, W = 376, 1241
+
+
+def _frame(desc, angles, fv, valid=None):
+    kp = np.zeros(len(desc), L.KP_DTYPE)
+    kp["angle"] = angles
+    return Frame(kp, np.ascontiguousarray(desc, np.uint8), mFeatVec=fv, map_valid=valid)
+
+
+@pytest.mark.parametrize("seed", range(6))
+@pytest.mark.parametrize("nnratio,check_ori", [(0.75, True), (0.7, False)])
+def test_rule_cases(oracle, seed, nnratio, check_ori):
+    kd, ka, kv, kfv, fd, fa, ffv = _case(seed)
+    m = ORBmatcher(nnratio, check_ori)
+    n, got = m.SearchByBoW(_frame(kd, ka, kfv, kv), _frame(fd, fa, ffv))
+    rn, ref = oracle.search_by_bow(kd, ka, kv, kfv, fd, fa, ffv, nnratio, check_ori)
+    assert n == rn and np.array_equal(got, ref)
+    assert rn > 5
+
+
+@pytest.fixture(scope="module")
+def kitti(oracle):
+    p = oracle.params(nfeatures=2000)
+    seq = S.sequence(4, H, W, seed=S.DEFAULT_SEED + 41)
+    ex = [oracle.extract(p, seq[t]) for t in range(4)]
+    voc = S.vocabulary(10, 6, seed=S.DEFAULT_SEED + 2)
+    gv = ORBVocabulary.from_tree(voc["k"], voc["L"], voc["scoring"], voc["weighting"],
+                                 voc["parent"], voc["is_leaf"], voc["desc"], voc["weight"])
+    return ex, gv
+
+
+@pytest.mark.parametrize("levelsup", [4, 6])
+def test_kitti_frames(oracle, kitti, levelsup):
+    ex, gv = kitti
+    rng = np.random.default_rng(levelsup)
+    m = ORBmatcher(0.7, True)
+    for t in range(1, 4):
+        a, b = ex[t - 1], ex[t]
+        kfv = gv.transform_arrays(a["desc"], levelsup)[2:]
+        ffv = gv.transform_arrays(b["desc"], levelsup)[2:]
+        valid = (rng.random(len(a["kps"])) > 0.1).astype(np.uint8)
+        kf = _frame(a["desc"], a["kps"]["angle"], kfv, valid)
+        fr = _frame(b["desc"], b["kps"]["angle"], ffv)
+        n, got = m.SearchByBoW(kf, fr)
+        rn, ref = oracle.search_by_bow(a["desc"], a["kps"]["angle"], valid, kfv, b["desc"],
+                                       b["kps"]["angle"], ffv, 0.7, True)
+        assert n == rn and np.array_equal(got, ref), t
+        assert rn > 100, (t, rn)
+        if levelsup == 6:
+            assert len(ffv[0]) == 1 and ffv[1][1] > 128  # one root node, > 128 candidates
+
+
+def test_empty_inputs(oracle):
+    kd, ka, kv, kfv, fd, fa, ffv = _case(3)
+    m = ORBmatcher(0.75, True)
+    empty = (np.zeros(0, np.int32), np.zeros(1, np.int32), np.zeros(0, np.int32))
+    n, got = m.SearchByBoW(_frame(kd, ka, empty), _frame(fd, fa, ffv))
+    assert n == 0 and (got == -1).all() and len(got) == len(fd)
+    n, got = m.SearchByBoW(_frame(kd, ka, kfv, np.zeros(len(kd), np.uint8)), _frame(fd, fa, ffv))
+    assert n == 0 and (got == -1).all()
+    n, got = m.SearchByBoW(_frame(kd, ka, kfv), _frame(fd[:0], fa[:0], empty))
+    assert n == 0 and len(got) == 0
+
+
+def test_batch_device_pairs(oracle, kitti):
+    """orbg_search_by_bow_batch_device over a device batch (the bow transform batch layout):
+    pairs (t - 1, t) and a frame against itself, every pair equal to the oracle."""
+    import ctypes as C
+    import torch
+    from orb_slam2_test_amd.orbmatcher import _ctx
+    ex, gv = kitti
+    B = len(ex)
+    cap = max(len(e["kps"]) for e in ex)
+    hd = np.zeros((B, cap, 32), np.uint8)
+    hk = np.zeros((B, cap), L.KP_DTYPE)
+    cnt = np.array([len(e["kps"]) for e in ex], np.int32)
+    valid = np.zeros((B, cap), np.uint8)
+    rng = np.random.default_rng(9)
+    for f, e in enumerate(ex):
+        hd[f, :cnt[f]] = e["desc"]
+        hk[f, :cnt[f]] = e["kps"]
+        valid[f, :cnt[f]] = rng.random(cnt[f]) > 0.1
+    dev = "cuda"
+    t_d = torch.from_numpy(hd.reshape(-1)).to(dev)
+    t_k = torch.from_numpy(hk.view(np.uint8).reshape(-1)).to(dev)
+    t_c = torch.from_numpy(cnt).to(dev)
+    t_v = torch.from_numpy(valid.reshape(-1)).to(dev)
+    out = {k: torch.zeros((B * cap,), dtype=torch.int32, device=dev)
+           for k in ("bow_words", "fv_nodes", "fv_feats")}
+    out["bow_weights"] = torch.zeros((B * cap,), dtype=torch.float64, device=dev)
+    out["fv_off"] = torch.zeros((B * (cap + 1),), dtype=torch.int32, device=dev)
+    out["nbow"] = torch.zeros(B, dtype=torch.int32, device=dev)
+    out["nfv"] = torch.zeros(B, dtype=torch.int32, device=dev)
+    torch.cuda.synchronize()
+    ctx = _ctx(0)
+    gv.transform_batch_device(t_d.data_ptr(), t_c.data_ptr(), cap, B, 4,
+                              {k: v.data_ptr() for k, v in out.items()}, ctx)
+    kf_i = np.array([0, 1, 2, 3], np.int32)
+    f_i = np.array([1, 2, 3, 3], np.int32)
+    P = len(kf_i)
+    t_ki, t_fi = torch.from_numpy(kf_i).to(dev), torch.from_numpy(f_i).to(dev)
+    t_m = torch.full((P * cap,), -9, dtype=torch.int32, device=dev)
+    t_n = torch.full((P,), -9, dtype=torch.int32, device=dev)
+    torch.cuda.synchronize()
+    side = dict(desc=t_d.data_ptr(), kps=t_k.data_ptr(), counts=t_c.data_ptr(),
+                fv_nodes=out["fv_nodes"].data_ptr(), fv_off=out["fv_off"].data_ptr(),
+                fv_feats=out["fv_feats"].data_ptr(), nfv=out["nfv"].data_ptr())
+    K = L.BowFrames(valid=t_v.data_ptr(), **side)
+    F = L.BowFrames(valid=None, **side)
+    L.check(L.lib().orbg_search_by_bow_batch_device(ctx.handle, C.byref(K), C.byref(F), cap,
+                                                    C.c_void_p(t_ki.data_ptr()),
+                                                    C.c_void_p(t_fi.data_ptr()), P, 0.75, 1,
+                                                    C.c_void_p(t_m.data_ptr()),
+                                                    C.c_void_p(t_n.data_ptr())),
+            "orbg_search_by_bow_batch_device")
+    ctx.sync()
+    hm, hn = t_m.cpu().numpy().reshape(P, cap), t_n.cpu().numpy()
+    h = {k: v.cpu().numpy() for k, v in out.items()}
+
+    def fv(f):
+        nf = h["nfv"][f]
+        vo = h["fv_off"][f * (cap + 1):f * (cap + 1) + nf + 1]
+        return (h["fv_nodes"][f * cap:f * cap + nf], vo, h["fv_feats"][f * cap:f * cap + vo[-1]])
+
+    for p in range(P):
+        a, b = kf_i[p], f_i[p]
+        rn, ref = oracle.search_by_bow(hd[a, :cnt[a]], hk[a, :cnt[a]]["angle"], valid[a, :cnt[a]],
+                                       fv(a), hd[b, :cnt[b]], hk[b, :cnt[b]]["angle"], fv(b),
+                                       0.75, True)
+        assert hn[p] == rn and np.array_equal(hm[p, :cnt[b]], ref), p
+        assert rn > 100
