@@ -281,7 +281,7 @@ __global__ __launch_bounds__(ORBG_OCT_THREADS) void k_octree(
     const uint2 *__restrict__ cell_kp, uint32_t *__restrict__ keys_all,
     uint32_t *__restrict__ knode_all, uint32_t *__restrict__ act_all,
     uint8_t *__restrict__ qk_all, int4 *__restrict__ nodes_all, uint32_t *__restrict__ lvl_kp,
-    int32_t *__restrict__ lvl_cnt, int32_t *__restrict__ err_flag)
+    uint16_t *__restrict__ lvl_idx, int32_t *__restrict__ lvl_cnt, int32_t *__restrict__ err_flag)
 {
     __shared__ OctShared S;
     const int l = blockIdx.x, f = blockIdx.y, tid = threadIdx.x;
@@ -733,10 +733,12 @@ __global__ __launch_bounds__(ORBG_OCT_THREADS) void k_octree(
     }
     __syncthreads();
     uint32_t *out = lvl_kp + (int64_t)f * g->out_frame + lv.out_off;
+    uint16_t *oidx = lvl_idx + (int64_t)f * g->out_frame + lv.out_off;
     const int nout = min(alive, lv.out_cap);
-    for (int i = tid; i < nout; i += nthr) {
+    for (int i = tid; i < nout; i += nthr) {  // slots in list order (k_octree_lds: tile order)
         const uint32_t k = 0xFFFFFFu - (S.u.best[i] & 0xFFFFFFu);
         out[i] = keys[k];
+        oidx[i] = (uint16_t)i;
     }
     if (tid == 0) {
         lvl_cnt[(int64_t)f * g->L + l] = nout;

@@ -12,6 +12,7 @@ struct OctLdsDims {
     int32_t acap2;      // aux entries: max(acap, cells + 1)
     int32_t nbw;        // bucket counter words: 512 * max roots (two u16 counters per word)
     int32_t uni_bytes;  // max(nbw * 4, 3 * acap * 8)
+    int32_t tile_sort;  // winners to slots in (32-row x 128-column tile) order (ORBG_OD_SORT)
 };
 
 // static LDS header of k_octree_lds

@@ -173,7 +173,8 @@ __device__ __forceinline__ void oct_children(uint32_t *codes, uint16_t *sidx,
 __global__ __launch_bounds__(OCT_T) void k_octree_lds(
     const OrbgGeom *__restrict__ g, const int32_t *__restrict__ cell_cnt,
     const uint2 *__restrict__ cell_kp, uint32_t *__restrict__ lvl_kp,
-    int32_t *__restrict__ lvl_cnt, int32_t *__restrict__ err_flag, OctLdsDims D)
+    uint16_t *__restrict__ lvl_idx, int32_t *__restrict__ lvl_cnt, int32_t *__restrict__ err_flag,
+    OctLdsDims D)
 {
     __shared__ OctLdsHdr S;
     extern __shared__ __attribute__((aligned(16))) uint8_t oct_dyn[];
@@ -559,9 +560,26 @@ __global__ __launch_bounds__(OCT_T) void k_octree_lds(
         atomicMax(&best[pos], ((uint32_t)V.resp[idx] << 24) | (0xFFFFFFu - idx));
     }
     __syncthreads();
-    // winners: candidate index -> its cell (last c with coff[c] <= idx) -> the cell list entry
+    // winners: candidate index -> its cell (last c with coff[c] <= idx) -> the cell list entry.
+    // Slot order: winner i (the reference's list order, the output row) goes to the slot its
+    // image tile's counting sort gives it, with lvl_idx[slot] = i, so k_orient_desc's waves get
+    // keypoints whose patches share cache lines; identity when D.tile_sort = 0.  The codes
+    // array (dead here) holds the keys, sidx (dead) the tile counters.
     uint32_t *out = lvl_kp + (int64_t)f * g->out_frame + lv.out_off;
+    uint16_t *oidx = lvl_idx + (int64_t)f * g->out_frame + lv.out_off;
     const int nout = min(alive, lv.out_cap);
+    uint32_t *tcnt = (uint32_t *)V.sidx;
+    const bool tsort = D.tile_sort && D.kcap >= 64;  // kcap / 2 >= 1 tile counter
+    int xs = 7, ys = 5, ntx = 0, nbins = 0;
+    if (tsort) {
+        for (;; xs++, ys++) {
+            ntx = (lv.w >> xs) + 1;
+            nbins = ntx * ((lv.h >> ys) + 1);
+            if (nbins <= D.kcap / 2) break;
+        }
+        for (int t = tid; t < nbins; t += OCT_T) tcnt[t] = 0;
+        __syncthreads();
+    }
     for (int i = tid; i < nout; i += OCT_T) {
         const int idx = (int)(0xFFFFFFu - (best[i] & 0xFFFFFFu));
         int a = 0, z = ncells;  // coff[a] <= idx < coff[z]
@@ -572,7 +590,37 @@ __global__ __launch_bounds__(OCT_T) void k_octree_lds(
             else
                 z = m;
         }
-        out[i] = ckp[(int64_t)a * g->cell_cap + (idx - (int)V.coff[a])].x;
+        const uint32_t key = ckp[(int64_t)a * g->cell_cap + (idx - (int)V.coff[a])].x;
+        if (tsort) {
+            V.codes[i] = key;
+            atomicAdd(&tcnt[(orbg_py(key) >> ys) * ntx + (orbg_px(key) >> xs)], 1u);
+        } else {
+            out[i] = key;
+            oidx[i] = (uint16_t)i;
+        }
+    }
+    if (tsort) {
+        __syncthreads();
+        // exclusive scan of the tile counters: thread t owns a run of consecutive tiles
+        const int per = (nbins + OCT_T - 1) / OCT_T, t0 = min(tid * per, nbins),
+                  t1 = min(t0 + per, nbins);
+        int sum = 0;
+        for (int t = t0; t < t1; t++) sum += (int)tcnt[t];
+        int tot;
+        int run = oct_scan(sum, &tot, S.red);
+        for (int t = t0; t < t1; t++) {
+            const int c = (int)tcnt[t];
+            tcnt[t] = (uint32_t)run;
+            run += c;
+        }
+        __syncthreads();
+        for (int i = tid; i < nout; i += OCT_T) {
+            const uint32_t key = V.codes[i];
+            const int slot =
+                (int)atomicAdd(&tcnt[(orbg_py(key) >> ys) * ntx + (orbg_px(key) >> xs)], 1u);
+            out[slot] = key;
+            oidx[slot] = (uint16_t)i;
+        }
     }
     if (tid == 0) {
         lvl_cnt[(int64_t)f * g->L + l] = nout;

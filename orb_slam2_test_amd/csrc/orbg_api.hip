@@ -30,10 +30,10 @@ namespace orbg {
 __global__ void k_resize(const uint8_t *, int64_t, int, int, uint8_t *, int64_t, int, int, int,
                          const int2 *, const int2 *, int, int);
 __global__ void k_octree(const OrbgGeom *, const int32_t *, const uint2 *, uint32_t *,
-                         uint32_t *, uint32_t *, uint8_t *, int4 *, uint32_t *, int32_t *,
-                         int32_t *);
+                         uint32_t *, uint32_t *, uint8_t *, int4 *, uint32_t *, uint16_t *,
+                         int32_t *, int32_t *);
 __global__ void k_octree_lds(const OrbgGeom *, const int32_t *, const uint2 *, uint32_t *,
-                             int32_t *, int32_t *, OctLdsDims);
+                             uint16_t *, int32_t *, int32_t *, OctLdsDims);
 // fast_kernels.hip
 bool fast2_pitch_ok(int p4);
 __global__ void k_pyramid(PyrArgs, const OrbgGeom *, const uint4 *, const int4 *, const int4 *,
@@ -60,8 +60,9 @@ struct OrbgKeypointDev;
 hipError_t launch_orient_desc(bool bfma, dim3 grid, hipStream_t st, const OrbgGeom *g,
                               const uint8_t *img0, int64_t img_fs, int img_pitch,
                               const uint8_t *pyr, const uint8_t *blur, const uint4 *odtab,
-                              const uint32_t *lvl_kp, const int32_t *lvl_cnt,
-                              OrbgKeypointDev *kps, uint8_t *desc, int32_t *counts);
+                              const uint32_t *lvl_kp, const uint16_t *lvl_idx,
+                              const int32_t *lvl_cnt, OrbgKeypointDev *kps, uint8_t *desc,
+                              int32_t *counts);
 // match_kernels.hip
 int launch_match_pairs(hipStream_t st, hipStream_t aux, hipEvent_t evf, hipEvent_t evj,
                        const uint8_t *desc, const orbg_keypoint *kps,
@@ -345,6 +346,8 @@ struct orbg_ctx {
     uint4 *d_odtab = nullptr;    // k_orient_desc IC_Angle byte tables (make_od_tab)
     uint8_t *d_img = nullptr;
     size_t img_bytes = 0;
+    uint8_t *d_pack = nullptr;  // orbg_download_frame: error word, count, kps, desc
+    size_t pack_bytes = 0;
     uint8_t *d_pyr = nullptr, *d_blur = nullptr;  // = pyr_slot[slot], blur_slot[slot]
     int32_t *d_cell_cnt = nullptr;                 // = cnt_slot[slot]
     uint2 *d_cell_kp = nullptr;                    // = ckp_slot[slot]
@@ -355,6 +358,7 @@ struct orbg_ctx {
     uint8_t *d_qk = nullptr;
     int4 *d_nodes = nullptr;
     uint32_t *d_lvl_kp = nullptr;
+    uint16_t *d_lvl_idx = nullptr;  // slot -> winner list position (octree -> orient)
     int32_t *d_lvl_cnt = nullptr;
     orbg_keypoint *d_kps = nullptr;  // = kps_slot[slot]
     uint8_t *d_desc = nullptr;        // = desc_slot[slot]
@@ -471,7 +475,7 @@ static void free_plan(orbg_ctx *c)
     void *ptrs[] = {c->d_geom, c->d_cells, c->d_ftiles, c->d_tile_base, c->d_rtab, c->d_ctab, c->d_odtab,
                     c->pyr_slot[0], c->pyr_slot[1], c->blur_slot[0], c->blur_slot[1],
                     c->cnt_slot[0], c->cnt_slot[1], c->ckp_slot[0], c->ckp_slot[1], c->d_keys, c->d_knode, c->d_act, c->d_qk,
-                    c->d_nodes, c->d_lvl_kp, c->d_lvl_cnt, c->kps_slot[0], c->kps_slot[1],
+                    c->d_nodes, c->d_lvl_kp, c->d_lvl_idx, c->d_lvl_cnt, c->kps_slot[0], c->kps_slot[1],
                     c->desc_slot[0], c->desc_slot[1], c->counts_slot[0], c->counts_slot[1],
                     c->d_err, c->d_knn, c->d_m12, c->d_nm, c->d_topk, c->d_topk_n, c->d_pairs,
                     c->d_spairs, c->d_uright, c->d_depth, c->d_snvalid, c->d_sscr,
@@ -503,6 +507,7 @@ static void free_plan(orbg_ctx *c)
     c->d_qk = nullptr;
     c->d_nodes = nullptr;
     c->d_lvl_kp = nullptr;
+    c->d_lvl_idx = nullptr;
     c->d_lvl_cnt = nullptr;
     c->d_kps = nullptr;
     c->d_desc = nullptr;
@@ -1063,6 +1068,7 @@ static int plan(orbg_ctx *c, int w, int h, int batch)
             d.acap2 = (std::max(d.acap, cells) + 7) & ~7;
             d.nbw = 512 * roots;
             d.uni_bytes = std::max(d.nbw * 4, 3 * d.acap * 8);
+            d.tile_sort = getenv("ORBG_OD_SORT") ? atoi(getenv("ORBG_OD_SORT")) != 0 : 0;  // measured: no gain
             if (budget) {
                 const int room = kcap_or_budget - d.uni_bytes - 4 * d.acap2;
                 d.kcap = std::min(OCT_KEY_CAP, std::max(0, room / 7) & ~63);
@@ -1118,6 +1124,7 @@ static int plan(orbg_ctx *c, int w, int h, int batch)
         (rc = dalloc(&c->d_keys, B * G.keys_frame)) || (rc = dalloc(&c->d_knode, B * G.keys_frame)) ||
         (rc = dalloc(&c->d_act, 2 * B * G.keys_frame)) || (rc = dalloc(&c->d_qk, B * G.keys_frame)) ||
         (rc = dalloc(&c->d_nodes, B * G.nodes_frame)) || (rc = dalloc(&c->d_lvl_kp, B * G.out_frame)) ||
+        (rc = dalloc(&c->d_lvl_idx, B * G.out_frame)) ||
         (rc = dalloc(&c->d_lvl_cnt, B * G.L)) ||
         (rc = dalloc(&c->kps_slot[0], B * G.frame_cap)) ||
         (rc = dalloc(&c->kps_slot[1], B * G.frame_cap)) ||
@@ -1346,6 +1353,7 @@ extern "C" void orbg_destroy(orbg_ctx *c)
     for (hipEvent_t e : c->prof.pool) hipEventDestroy(e);
     free_plan(c);
     if (c->d_img) hipFree(c->d_img);
+    if (c->d_pack) hipFree(c->d_pack);
     if (c->d_scr) hipFree(c->d_scr);
     if (c->d_trk) hipFree(c->d_trk);
     if (c->d_mpose) hipFree(c->d_mpose);
@@ -1539,18 +1547,18 @@ static int launch_extract_pipe(orbg_ctx *c, const uint8_t *d_imgs, int B, int pi
     PROF_LAUNCH(c, "octree",
                 hipLaunchKernelGGL(k_octree_lds, dim3(B, 1), dim3(512),
                                    oct_lds_bytes(c->oct_dims[0]), st, c->d_geom, c->d_cell_cnt,
-                                   c->d_cell_kp, c->d_lvl_kp, c->d_lvl_cnt,
+                                   c->d_cell_kp, c->d_lvl_kp, c->d_lvl_idx, c->d_lvl_cnt,
                                    c->d_err, c->oct_dims[0]));
     if (G.L > 1)
         PROF_LAUNCH(c, "octree",
                     hipLaunchKernelGGL(k_octree_lds, dim3(B, G.L - 1), dim3(512),
                                        oct_lds_bytes(c->oct_dims[1]), st, c->d_geom,
                                        c->d_cell_cnt, c->d_cell_kp,
-                                       c->d_lvl_kp, c->d_lvl_cnt, c->d_err, c->oct_dims[1]));
+                                       c->d_lvl_kp, c->d_lvl_idx, c->d_lvl_cnt, c->d_err, c->oct_dims[1]));
     PROF_LAUNCH(c, "octree_big",
                 hipLaunchKernelGGL(k_octree, dim3(G.L, B), dim3(ORBG_OCT_THREADS), 0, st,
                                    c->d_geom, c->d_cell_cnt, c->d_cell_kp, c->d_keys, c->d_knode,
-                                   c->d_act, c->d_qk, c->d_nodes, c->d_lvl_kp, c->d_lvl_cnt,
+                                   c->d_act, c->d_qk, c->d_nodes, c->d_lvl_kp, c->d_lvl_idx, c->d_lvl_cnt,
                                    c->d_err));
     HIPCHK(hipStreamWaitEvent(st, c->ev_front[s], 0));
     if (c->mat_pending[s]) {  // the matching of the batch before last reads output slot s
@@ -1569,7 +1577,7 @@ static int launch_extract_pipe(orbg_ctx *c, const uint8_t *d_imgs, int B, int pi
                 launch_orient_desc(G.brief_fma != 0,
                                    dim3((G.out_frame + 4 * ORBG_OD_KPW - 1) / (4 * ORBG_OD_KPW) * B),
                                    st, c->d_geom, d_imgs, fs, pitch, c->d_pyr,
-                                   c->d_blur, c->d_odtab, c->d_lvl_kp, c->d_lvl_cnt,
+                                   c->d_blur, c->d_odtab, c->d_lvl_kp, c->d_lvl_idx, c->d_lvl_cnt,
                                    (OrbgKeypointDev *)c->d_kps, c->d_desc, c->d_counts));
     HIPCHK(hipEventRecord(c->ev_ext[s], st));
     HIPCHK(hipEventRecord(c->ev_back[s], st));
@@ -1642,7 +1650,7 @@ static int launch_extract(orbg_ctx *c, const uint8_t *d_imgs, int B, int pitch, 
                     hipLaunchKernelGGL(k_octree_lds, dim3(B, 1), dim3(512),
                                        oct_lds_bytes(c->oct_dims[0]), st, c->d_geom,
                                        c->d_cell_cnt, c->d_cell_kp,
-                                       c->d_lvl_kp, c->d_lvl_cnt, c->d_err, c->oct_dims[0]));
+                                       c->d_lvl_kp, c->d_lvl_idx, c->d_lvl_cnt, c->d_err, c->oct_dims[0]));
         if (oct_mode == 2 && G.L > 1) {
             // levels 1.. need their FAST cells (launched on the extraction stream under fast0)
             if (fast0) {
@@ -1653,7 +1661,7 @@ static int launch_extract(orbg_ctx *c, const uint8_t *d_imgs, int B, int pitch, 
                         hipLaunchKernelGGL(k_octree_lds, dim3(B, G.L - 1), dim3(512),
                                            oct_lds_bytes(c->oct_dims[1]), st, c->d_geom,
                                            c->d_cell_cnt, c->d_cell_kp,
-                                           c->d_lvl_kp, c->d_lvl_cnt, c->d_err, c->oct_dims[1]));
+                                           c->d_lvl_kp, c->d_lvl_idx, c->d_lvl_cnt, c->d_err, c->oct_dims[1]));
         }
         if (blur0) HIPCHK(launch_blur_levels(c, st, d_imgs, B, pitch, fs, 0, 1));
         if (oct_mode) HIPCHK(hipEventRecord(c->ev_oct, st));
@@ -1665,12 +1673,12 @@ static int launch_extract(orbg_ctx *c, const uint8_t *d_imgs, int B, int pitch, 
                     hipLaunchKernelGGL(k_octree_lds, dim3(B, G.L - 1), dim3(512),
                                        oct_lds_bytes(c->oct_dims[1]), st, c->d_geom,
                                        c->d_cell_cnt, c->d_cell_kp,
-                                       c->d_lvl_kp, c->d_lvl_cnt, c->d_err, c->oct_dims[1]));
+                                       c->d_lvl_kp, c->d_lvl_idx, c->d_lvl_cnt, c->d_err, c->oct_dims[1]));
     if (oct_mode) HIPCHK(hipStreamWaitEvent(st, c->ev_oct, 0));
     PROF_LAUNCH(c, "octree_big",
                 hipLaunchKernelGGL(k_octree, dim3(G.L, B), dim3(ORBG_OCT_THREADS), 0, st,
                                    c->d_geom, c->d_cell_cnt, c->d_cell_kp, c->d_keys, c->d_knode,
-                                   c->d_act, c->d_qk, c->d_nodes, c->d_lvl_kp, c->d_lvl_cnt,
+                                   c->d_act, c->d_qk, c->d_nodes, c->d_lvl_kp, c->d_lvl_idx, c->d_lvl_cnt,
                                    c->d_err));
     // per-frame outputs go to the other slot; wait until its last reader (matching of the
     // batch before last) is done
@@ -1690,7 +1698,7 @@ static int launch_extract(orbg_ctx *c, const uint8_t *d_imgs, int B, int pitch, 
                 launch_orient_desc(G.brief_fma != 0,
                                    dim3((G.out_frame + 4 * ORBG_OD_KPW - 1) / (4 * ORBG_OD_KPW) * B),
                                    st, c->d_geom, d_imgs, fs, pitch, c->d_pyr,
-                                   c->d_blur, c->d_odtab, c->d_lvl_kp, c->d_lvl_cnt, (OrbgKeypointDev *)c->d_kps,
+                                   c->d_blur, c->d_odtab, c->d_lvl_kp, c->d_lvl_idx, c->d_lvl_cnt, (OrbgKeypointDev *)c->d_kps,
                                    c->d_desc, c->d_counts));
     HIPCHK(hipEventRecord(c->ev_ext[s], st));
     HIPCHK(hipGetLastError());
@@ -1765,29 +1773,62 @@ extern "C" int orbg_batch_outputs(orbg_ctx *c, orbg_keypoint **d_kps, uint8_t **
     return ORBG_OK;
 }
 
+// One frame's outputs gathered into one device block for a single DMA: [0..4) the sticky
+// error word and the count, then the frame's keypoints and descriptors (count entries).
+__global__ void k_pack_frame(const int32_t *__restrict__ err, const int32_t *__restrict__ counts,
+                             const uint32_t *__restrict__ kps, const uint32_t *__restrict__ desc,
+                             int frame, size_t fc, size_t okp, size_t ods,
+                             uint32_t *__restrict__ pack)
+{
+    const int n = counts[frame];
+    const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const size_t kw = sizeof(orbg_keypoint) / 4, nk = (size_t)n * kw, nd = (size_t)n * 8;
+    if (i < 4) pack[i] = i < 2 ? (uint32_t)err[i] : i == 2 ? (uint32_t)n : 0u;
+    if (i < nk) pack[okp / 4 + i] = kps[(size_t)frame * fc * kw + i];
+    if (i < nd) pack[ods / 4 + i] = desc[(size_t)frame * fc * 8 + i];
+}
+
 extern "C" int orbg_download_frame(orbg_ctx *c, int frame, orbg_keypoint *kps, uint8_t *desc,
                                    int cap, int *n_out)
 {
     if (!c || !c->gw || frame < 0 || frame >= c->last_n)
         return set_err(ORBG_EINVAL, "bad frame index");
-    int rc = check_err(c);
-    if (rc) return rc;
-    // count, keypoints and descriptors of the whole frame slot in one pinned round trip
+    static_assert(sizeof(orbg_keypoint) % 4 == 0, "keypoint records are whole words");
+    // the error word, count, keypoints and descriptors in one pinned round trip: a packing
+    // kernel behind the frame's last writer (the back stream), one DMA, then the streams are
+    // drained as check_err does, so the error word covers every batch since the last read
     const size_t fc = (size_t)c->geom.frame_cap;
     const size_t okp = 256, ods = okp + ((fc * sizeof(orbg_keypoint) + 255) & ~(size_t)255);
+    const size_t bytes = ods + fc * 32;
+    int rc;
+    if (c->pack_bytes < bytes) {
+        if ((rc = sync_all(c))) return rc;
+        if (c->d_pack) hipFree(c->d_pack);
+        c->d_pack = nullptr;
+        c->pack_bytes = 0;
+        if ((rc = dalloc(&c->d_pack, bytes))) return rc;
+        c->pack_bytes = bytes;
+    }
     uint8_t *hs;
-    if ((rc = stage(c, ods + fc * 32, &hs))) return rc;
+    if ((rc = stage(c, bytes, &hs))) return rc;
     hipStream_t st = back_stream(c);
-    HIPCHK(hipMemcpyAsync(hs, c->d_counts + frame, sizeof(int32_t), hipMemcpyDeviceToHost, st));
-    if (kps)
-        HIPCHK(hipMemcpyAsync(hs + okp, c->d_kps + frame * fc, fc * sizeof(orbg_keypoint),
-                              hipMemcpyDeviceToHost, st));
-    if (desc)
-        HIPCHK(hipMemcpyAsync(hs + ods, c->d_desc + frame * fc * 32, fc * 32,
-                              hipMemcpyDeviceToHost, st));
-    HIPCHK(hipStreamSynchronize(st));
-    int32_t n = 0;
-    std::memcpy(&n, hs, sizeof(n));
+    const size_t words = std::max(fc * (sizeof(orbg_keypoint) / 4), fc * 8);
+    hipLaunchKernelGGL(k_pack_frame, dim3((unsigned)((words + 255) / 256)), dim3(256), 0, st,
+                       c->d_err, c->d_counts, (const uint32_t *)c->d_kps,
+                       (const uint32_t *)c->d_desc, frame, fc, okp, ods, (uint32_t *)c->d_pack);
+    HIPCHK(hipGetLastError());
+    HIPCHK(hipMemcpyAsync(hs, c->d_pack, bytes, hipMemcpyDeviceToHost, st));
+    if ((rc = sync_all(c))) return rc;
+    c->prof.collect();
+    int32_t hdr[3];
+    std::memcpy(hdr, hs, sizeof(hdr));
+    if (hdr[0]) {  // check_err's reset and error
+        const int32_t e0[2] = {0, INT32_MAX};
+        HIPCHK(hipMemcpy(c->d_err, e0, sizeof(e0), hipMemcpyHostToDevice));
+        return set_err(ORBG_ENOTSUP, "quadtree capacity exceeded (flags 0x%x, first frame %d of "
+                                     "a batch since the last check)", hdr[0], hdr[1]);
+    }
+    const int32_t n = hdr[2];
     if (n_out) *n_out = n;
     if (n > cap) return set_err(ORBG_ERANGE, "capacity %d < %d keypoints", cap, n);
     if (kps && n) std::memcpy(kps, hs + okp, n * sizeof(orbg_keypoint));

@@ -96,7 +96,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(ORBG_OD_WPE
     const OrbgGeom *__restrict__ g, const uint8_t *__restrict__ img0, int64_t img_fs,
     int img_pitch, const uint8_t *__restrict__ pyr, const uint8_t *__restrict__ blur,
     const uint4 *__restrict__ odtab, const uint32_t *__restrict__ lvl_kp,
-    const int32_t *__restrict__ lvl_cnt, OrbgKeypointDev *__restrict__ kps,
+    const uint16_t *__restrict__ lvl_idx, const int32_t *__restrict__ lvl_cnt,
+    OrbgKeypointDev *__restrict__ kps,
     uint8_t *__restrict__ desc, int32_t *__restrict__ counts)
 {
 #if ORBG_OD_PRIO
@@ -123,7 +124,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(ORBG_OD_WPE
         for (int l = 0; l < L; l++) total += lc[l];
         counts[f] = total;
     }
-    // lane j < OD_KPW: slot s0 + j -> quadtree key, level, output row; okmask bit j
+    // lane j < OD_KPW: slot s0 + j -> quadtree key, level, output row (the winner's list
+    // position lvl_idx: the octree put the slots in image-tile order); okmask bit j
     // (wave-uniform) = the slot holds a keypoint
     uint32_t kl = 0u;
     int my_lev = 0, my_i = 0, my_ok = 0;
@@ -139,7 +141,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(ORBG_OD_WPE
                 kl = lvl_kp[(int64_t)f * OF + slot];
                 my_ok = 1;
                 my_lev = level;
-                my_i = before + pos;
+                my_i = before + lvl_idx[(int64_t)f * OF + slot];
             }
         }
     }
@@ -369,15 +371,18 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(ORBG_OD_WPE
 hipError_t launch_orient_desc(bool bfma, dim3 grid, hipStream_t st, const OrbgGeom *g,
                               const uint8_t *img0, int64_t img_fs, int img_pitch,
                               const uint8_t *pyr, const uint8_t *blur, const uint4 *odtab,
-                              const uint32_t *lvl_kp, const int32_t *lvl_cnt,
-                              OrbgKeypointDev *kps, uint8_t *desc, int32_t *counts)
+                              const uint32_t *lvl_kp, const uint16_t *lvl_idx,
+                              const int32_t *lvl_cnt, OrbgKeypointDev *kps, uint8_t *desc,
+                              int32_t *counts)
 {
     if (bfma)
         hipLaunchKernelGGL(k_orient_desc<true>, grid, dim3(256), 0, st, g, img0, img_fs,
-                           img_pitch, pyr, blur, odtab, lvl_kp, lvl_cnt, kps, desc, counts);
+                           img_pitch, pyr, blur, odtab, lvl_kp, lvl_idx, lvl_cnt, kps, desc,
+                           counts);
     else
         hipLaunchKernelGGL(k_orient_desc<false>, grid, dim3(256), 0, st, g, img0, img_fs,
-                           img_pitch, pyr, blur, odtab, lvl_kp, lvl_cnt, kps, desc, counts);
+                           img_pitch, pyr, blur, odtab, lvl_kp, lvl_idx, lvl_cnt, kps, desc,
+                           counts);
     return hipGetLastError();
 }
 

@@ -30,12 +30,13 @@ def main():
     # warm-up (plans the buffers, loads the code objects)
     for t in range(3):
         ext(frames[t])
-    lat = []
+    lat, lext = [], []
     t_all = time.perf_counter()
     kprev, dprev = ext(frames[0])
     for t in range(1, n + 1):
         t0 = time.perf_counter()
         k, d = ext(frames[t % len(frames)])
+        lext.append(time.perf_counter() - t0)
         F1 = Frame.from_extraction(kprev, dprev, w, h)
         F2 = Frame.from_extraction(k, d, w, h)
         pm = np.ascontiguousarray(np.stack([kprev["x"], kprev["y"]], 1).astype(np.float32))
@@ -44,6 +45,7 @@ def main():
         kprev, dprev = k, d
     gpu_total = time.perf_counter() - t_all
     lat = np.array(lat) * 1e3
+    lext = np.array(lext) * 1e3
     # oracle, one thread, same per-frame work
     p = O.params(nfeatures=nf)
     no = max(8, min(40, n // 5))
@@ -64,6 +66,8 @@ def main():
         "image": [w, h], "nfeatures": nf, "frames": n,
         "gpu_ms_per_frame": {"mean": round(float(lat.mean()), 3), "p50": round(float(np.median(lat)), 3),
                              "p90": round(float(np.percentile(lat, 90)), 3)},
+        "gpu_extract_ms_per_frame": {"mean": round(float(lext.mean()), 3),
+                                     "p50": round(float(np.median(lext)), 3)},
         "gpu_frames_per_s": round(n / gpu_total, 1),
         "cpu_oracle_1thread_ms_per_frame": {"mean": round(float(olat.mean()), 3),
                                             "p50": round(float(np.median(olat)), 3)},
