@@ -764,10 +764,9 @@ __global__ __launch_bounds__(RESOLVE_T) void k_init_resolve_single(
     const orbg_keypoint *k1, const uint8_t *d1, int n1, const orbg_keypoint *k2,
     const uint8_t *d2, int n2, orbg_bounds b, float *prev, int window, float nnratio,
     int check_ori, const unsigned long long *topk, const int32_t *topn, int32_t *m12,
-    int32_t *nm)
+    int32_t *nm, int cap)
 {
     extern __shared__ __attribute__((aligned(16))) uint8_t rs_lds[];
-    const int cap = max(n1, n2);
     ResolveShared S = resolve_layout(rs_lds, cap);
     init_resolve_block(S, cap, k1, d1, n1, k2, d2, n2, b, prev, 2, window, nnratio, check_ori, topk,
                        topn, m12, nm, prev);
@@ -870,11 +869,15 @@ int launch_match_pairs(hipStream_t st, hipStream_t aux, hipEvent_t evf, hipEvent
     return hipGetLastError() == hipSuccess ? ORBG_OK : ORBG_EIO;
 }
 
+// cap: 1 + the last level-0 index of either frame (every query / candidate index the
+// search can touch: it reads level-0 keypoints only, ORBmatcher.cc:509-512, 1 <= cap <=
+// max(n1, n2)); queries past it get no candidates and vnMatches12 = -1
 int launch_init_match_single(hipStream_t st, const orbg_keypoint *k1, const uint8_t *d1, int n1,
                              const orbg_keypoint *k2, const uint8_t *d2, int n2, orbg_bounds b,
                              float *prev, int32_t *m12, int32_t *nm, int window, float nnratio,
-                             int check_ori, uint32_t *topk, int32_t *topk_n, void *prof)
+                             int check_ori, uint32_t *topk, int32_t *topk_n, void *prof, int cap)
 {
+    const int nq = std::min(n1, cap), n2c = std::min(n2, cap);  // indices below cap
     if (n1 > RESOLVE_N2_CAP || n2 > RESOLVE_N2_CAP || n2 > INIT_F2_CAP) return ORBG_ENOTSUP;
     static bool attr = false;  // > 64 KB of dynamic LDS at the 4608-keypoint bound
     if (!attr) {
@@ -885,14 +888,14 @@ int launch_init_match_single(hipStream_t st, const orbg_keypoint *k1, const uint
         attr = true;
     }
     PL(prof, st, "init_cands",
-       hipLaunchKernelGGL(k_init_cands_single, dim3((n1 + 4 * INIT_QPW - 1) / (4 * INIT_QPW)),
-                          dim3(256), 2 * (size_t)std::max(n2, 1) * sizeof(F2Key), st, k1, d1, n1, k2,
-                          d2, n2, b, prev, window, (unsigned long long *)topk, topk_n));
+       hipLaunchKernelGGL(k_init_cands_single, dim3((nq + 4 * INIT_QPW - 1) / (4 * INIT_QPW)),
+                          dim3(256), 2 * (size_t)std::max(n2c, 1) * sizeof(F2Key), st, k1, d1, nq, k2,
+                          d2, n2c, b, prev, window, (unsigned long long *)topk, topk_n));
     PL(prof, st, "init_resolve",
        hipLaunchKernelGGL(k_init_resolve_single, dim3(1), dim3(RESOLVE_T),
-                          resolve_lds_bytes(std::max(std::max(n1, n2), 1)), st, k1, d1, n1, k2, d2, n2,
-                          b, prev, window, nnratio, check_ori, (const unsigned long long *)topk,
-                          topk_n, m12, nm));
+                          resolve_lds_bytes(cap), st, k1, d1, n1, k2, d2, n2, b, prev, window,
+                          nnratio, check_ori, (const unsigned long long *)topk, topk_n, m12, nm,
+                          cap));
     return hipGetLastError() == hipSuccess ? ORBG_OK : ORBG_EIO;
 }
 

@@ -88,7 +88,7 @@ int launch_init_match_single(hipStream_t st, const orbg_keypoint *k1, const uint
                              const orbg_keypoint *k2, const uint8_t *d2, int n2,
                              orbg_bounds b, float *prev, int32_t *m12, int32_t *nm, int window,
                              float nnratio, int check_ori, uint32_t *topk, int32_t *topk_n,
-                             void *prof);
+                             void *prof, int cap);
 // bow_match_kernels.hip
 int launch_bow_match(hipStream_t st, const orbg_bow_frames &kf, const orbg_bow_frames &f, int cap,
                      const int32_t *kf_index, const int32_t *f_index, int npairs, float nnratio,
@@ -707,6 +707,9 @@ static bool make_pyr_tables(const OrbgGeom &G, const std::vector<int2> &rtab, in
 }
 
 // Build the geometry for an image size and allocate HBM for `batch` frames.
+#ifndef ORBG_SIDE_BLUR_B
+#define ORBG_SIDE_BLUR_B 8  // batches up to this size blur on the quadtree stream (launch_extract)
+#endif
 #ifndef ORBG_FC2_IL
 #define ORBG_FC2_IL 1  // k_fast2 LDS layout (fast_kernels.hip): score rows interleaved with the tile rows
 #endif
@@ -1167,8 +1170,12 @@ static int plan(orbg_ctx *c, int w, int h, int batch)
         // ORBG_PYR_BLUR (A/B): 0 k_blur2 launches, 1 every level blurred inside k_pyramid,
         // 2 levels >= 1 inside k_pyramid and level 0 by k_blur2 (beside it on the side stream)
         const char *fb = getenv("ORBG_PYR_BLUR");
-        c->pyr_ok = (!e || atoi(e)) && make_pyr_tables(G, rtab, nb ? atoi(nb) : 4, pt, yt4, bd, A,
-                                                       fb ? atoi(fb) : 0);
+        // bands per frame: 4 fill the chip at bench batches; a small batch (the single-frame
+        // drop-in) takes 16, the B = 1 optimum (profiles/r04k_single_frame_nband.txt: 4 bands
+        // 0.247 ms per extraction, 16 0.229, 32 0.230, 48 0.233)
+        const int nb_def = want_batch <= ORBG_SIDE_BLUR_B ? 16 : 4;
+        c->pyr_ok = (!e || atoi(e)) && make_pyr_tables(G, rtab, nb ? atoi(nb) : nb_def, pt, yt4, bd,
+                                                       A, fb ? atoi(fb) : 0);
         if (c->pyr_ok) {
             if ((rc = dalloc(&c->d_ptab, pt.size())) || (rc = dalloc(&c->d_ytab4, yt4.size())) ||
                 (rc = dalloc(&c->d_bands, bd.size()))) {
@@ -1625,6 +1632,10 @@ static int launch_extract(orbg_ctx *c, const uint8_t *d_imgs, int B, int pitch, 
     const bool fused = fz != 0;
     // blur0: the level-0 GaussianBlur follows them there (ORBG_BLUR0)
     const bool blur0 = fast0 && c->blur0_mode && fz != 1;
+    // blur_side: small batches (the single-frame drop-in) blur every level on the quadtree
+    // stream after the level-0 quadtree, so levels 1.. go FAST -> quadtree without waiting for
+    // the blur on the extraction stream (at B = 1 the blur is ~9 us of a ~150 us chain)
+    const bool blur_side = fast0 && oct_mode == 1 && !fused && !blur0 && B <= ORBG_SIDE_BLUR_B;
     auto launch_fast = [&](hipStream_t q, int cb, int cn) {
         return launch_fast_cells(c, q, d_imgs, B, pitch, fs, cb, cn);
     };
@@ -1634,6 +1645,7 @@ static int launch_extract(orbg_ctx *c, const uint8_t *d_imgs, int B, int pitch, 
         HIPCHK(launch_fast(c->ostream, 0, n0));
     }
     HIPCHK(launch_pyramid(c, st, d_imgs, B, pitch, fs));
+    if (blur_side) HIPCHK(hipEventRecord(c->ev_fast, st));  // pyramid written: the side blur
     if (fast0) {
         HIPCHK(launch_fast(st, n0, G.ncells - n0));
     } else {
@@ -1664,9 +1676,14 @@ static int launch_extract(orbg_ctx *c, const uint8_t *d_imgs, int B, int pitch, 
                                            c->d_lvl_kp, c->d_lvl_idx, c->d_lvl_cnt, c->d_err, c->oct_dims[1]));
         }
         if (blur0) HIPCHK(launch_blur_levels(c, st, d_imgs, B, pitch, fs, 0, 1));
+        if (blur_side) {
+            HIPCHK(hipStreamWaitEvent(st, c->ev_fast, 0));
+            HIPCHK(launch_blur_levels(c, st, d_imgs, B, pitch, fs, 0, G.L));
+        }
         if (oct_mode) HIPCHK(hipEventRecord(c->ev_oct, st));
     }
-    if (!fused) HIPCHK(launch_blur_levels(c, st, d_imgs, B, pitch, fs, blur0 ? 1 : 0, G.L));
+    if (!fused && !blur_side)
+        HIPCHK(launch_blur_levels(c, st, d_imgs, B, pitch, fs, blur0 ? 1 : 0, G.L));
     else if (fz == 2 && !blur0) HIPCHK(launch_blur_levels(c, st, d_imgs, B, pitch, fs, 0, 1));
     if (oct_mode != 2 && G.L > 1)
         PROF_LAUNCH(c, "octree",
@@ -2501,11 +2518,26 @@ extern "C" int orbg_search_for_initialization(orbg_ctx *c, const orbg_keypoint *
     }
     std::memcpy(hs + opv, prev_xy, m1 * 8);
     HIPCHK(hipMemcpyAsync(b, hs, om, hipMemcpyHostToDevice, c->stream));
+    // the search reads level-0 keypoints only (ORBmatcher.cc:509-512): the kernels work on
+    // indices up to the last level-0 keypoint of either frame (the level-major extractor
+    // order puts them first; any order is handled)
+    int last0 = 0;
+    for (int i = n1 - 1; i >= 0; i--)
+        if (kps1[i].octave == 0) {
+            last0 = std::max(last0, i + 1);
+            break;
+        }
+    for (int i = n2 - 1; i >= 0; i--)
+        if (kps2[i].octave == 0) {
+            last0 = std::max(last0, i + 1);
+            break;
+        }
     rc = launch_init_match_single(c->stream, (const orbg_keypoint *)(b + ok1), b + od1, n1,
                                   (const orbg_keypoint *)(b + ok2), b + od2, n2, *bounds2,
                                   (float *)(b + opv), (int32_t *)(b + om),
                                   (int32_t *)(b + om + m1 * 4), window, nnratio, check_ori,
-                                  (uint32_t *)(b + otk), (int32_t *)(b + otn), &c->prof);
+                                  (uint32_t *)(b + otk), (int32_t *)(b + otn), &c->prof,
+                                  std::max(last0, 1));
     if (rc) return rc;
     int32_t nm = 0;
     HIPCHK(hipMemcpyAsync(hs + opv, b + opv, otk - opv, hipMemcpyDeviceToHost, c->stream));
