@@ -8,6 +8,13 @@
 //       writes kps0/kps1 (28-B cv::KeyPoint records), desc0/desc1 (N x 32),
 //       m12 (int32 per F1 keypoint), knn (int32 triples per F2 keypoint), nm.txt,
 //       stereo_ur / stereo_depth (StereoFrame of frame0 as left, frame1 as right)
+//   compat_selftest bench <w> <h> <frames.raw> <nimages> <nframes> <nfeatures>
+//       the monocular per-frame loop of Tracking.cc as C++ drives it (Frame ctor ->
+//       ExtractORB, then MonocularInitialization's SearchForInitialization against the
+//       previous frame), host images in, host vectors out; one JSON line of per-frame
+//       latency percentiles (the Python mirror's interpreter overhead excluded)
+#include <algorithm>
+#include <chrono>
 #include <cstdio>
 #include <cstdlib>
 #include <fstream>
@@ -33,6 +40,62 @@ static void write_file(const std::string &p, const std::vector<T> &v)
     f.write((const char *)v.data(), (std::streamsize)(v.size() * sizeof(T)));
 }
 
+static int bench(char **argv)
+{
+    using clk = std::chrono::steady_clock;
+    const int w = std::atoi(argv[2]), h = std::atoi(argv[3]);
+    const int nimg = std::atoi(argv[5]), nframes = std::atoi(argv[6]), nfeat = std::atoi(argv[7]);
+    const size_t px = (size_t)w * h;
+    std::vector<uint8_t> imgs = read_file(argv[4], px * (size_t)nimg);
+    orbg_compat::Extractor ext(nfeat, 1.2f, 8, 20, 7);
+    orbg_compat::Matcher matcher(0.9f, true, ext.context());
+    std::vector<orbg_keypoint> kp[2];
+    std::vector<uint8_t> ds[2];
+    std::vector<float> prev;
+    std::vector<int> m12;
+    std::vector<double> lat, lext;
+    int n[2] = {0, 0};
+    long matches = 0;
+    for (int t = -3; t < nframes; t++) {  // three warm-up frames
+        const int cur = (t + 3) & 1, old = cur ^ 1;
+        const auto t0 = clk::now();
+        n[cur] = ext(imgs.data() + px * (size_t)(((t % nimg) + nimg) % nimg), w, h, (size_t)w,
+                     kp[cur], ds[cur]);
+        const auto t1 = clk::now();
+        if (t > -3) {
+            prev.resize(2 * (size_t)n[old]);
+            for (int i = 0; i < n[old]; i++) {
+                prev[2 * i] = kp[old][i].x;
+                prev[2 * i + 1] = kp[old][i].y;
+            }
+            orbg_compat::FrameView F1{kp[old].data(), ds[old].data(), n[old],
+                                      {0.f, (float)w, 0.f, (float)h}};
+            orbg_compat::FrameView F2{kp[cur].data(), ds[cur].data(), n[cur],
+                                      {0.f, (float)w, 0.f, (float)h}};
+            matches += matcher.SearchForInitialization(F1, F2, prev, m12, 100);
+        }
+        const auto t2 = clk::now();
+        if (t >= 0) {
+            lat.push_back(std::chrono::duration<double, std::milli>(t2 - t0).count());
+            lext.push_back(std::chrono::duration<double, std::milli>(t1 - t0).count());
+        }
+    }
+    auto pct = [](std::vector<double> v, double q) {
+        std::sort(v.begin(), v.end());
+        return v[std::min(v.size() - 1, (size_t)(q * (double)v.size()))];
+    };
+    double mean = 0;
+    for (double v : lat) mean += v;
+    mean /= (double)std::max<size_t>(lat.size(), 1);
+    std::printf("{\"frames\": %d, \"ms_per_frame\": {\"mean\": %.4f, \"p50\": %.4f, "
+                "\"p90\": %.4f}, \"extract_ms_per_frame\": {\"p50\": %.4f}, "
+                "\"match_ms_per_frame\": {\"p50\": %.4f}, \"frames_per_s\": %.1f, "
+                "\"matches_per_frame\": %.1f}\n",
+                nframes, mean, pct(lat, 0.5), pct(lat, 0.9), pct(lext, 0.5),
+                pct(lat, 0.5) - pct(lext, 0.5), 1e3 / mean, (double)matches / (nframes + 2));
+    return 0;
+}
+
 int main(int argc, char **argv)
 {
     if (argc >= 2 && std::string(argv[1]) == "nogpu") {
@@ -45,6 +108,7 @@ int main(int argc, char **argv)
             return err.code == ORBG_EIO ? 0 : 2;
         }
     }
+    if (argc >= 8 && std::string(argv[1]) == "bench") return bench(argv);
     if (argc < 8 || std::string(argv[1]) != "run") {
         std::cerr << "usage: compat_selftest nogpu | run w h f0 f1 outdir nfeatures\n";
         return 2;

@@ -781,9 +781,42 @@ int launch_ba_graph(hipStream_t st, const orbg_pose *poses, int npose, const dou
                     int nedge, const int32_t *pose_off, const int32_t *pose_edges,
                     const int32_t *point_off, const int32_t *point_edges, const BaGraphDev &gd,
                     double *hpl, double *hpose, double *bpose, double *hpoint, double *bpoint,
-                    void *prof)
+                    void *prof, hipStream_t st2, hipEvent_t evf, hipEvent_t evj, int overlap)
 {
     const BaEdgePacked es{edges, cam, info};
+    // the pose blocks and the special points read only the graph and the estimate, like the
+    // edge pass: with st2, overlap 1 runs the pose blocks beside it, 2 the special points (fork
+    // after the caller's work on st, join back into st before return).  Measured: the edge
+    // pass fills the chip, so neither gains (profiles/r04n_ba_overlap_ab.txt); default 0
+    hipStream_t sp = st, ss = st;
+    if (st2 && overlap == 2 && gd.nspecial && nedge) {
+        // the special points beside the edge pass (a few hundred latency-bound waves)
+        if (hipEventRecord(evf, st) != hipSuccess || hipStreamWaitEvent(st2, evf, 0) != hipSuccess)
+            return -5;
+        ss = st2;
+        hipEvent_t a = nullptr;
+        prof_begin(prof, ss, "ba_special", &a);
+        hipLaunchKernelGGL(k_ba_special<BaEdgePacked>, dim3((gd.nspecial + 3) / 4), dim3(256), 0,
+                           ss, poses, points, es, point_off, point_edges, gd.special, gd.nspecial,
+                           hpoint, bpoint);
+        prof_end(prof, ss, "ba_special", a);
+        if (hipEventRecord(evj, ss) != hipSuccess) return -5;
+    }
+    if (st2 && overlap == 1 && npose && nedge) {
+        if (hipEventRecord(evf, st) != hipSuccess || hipStreamWaitEvent(st2, evf, 0) != hipSuccess)
+            return -5;
+        sp = st2;
+        hipEvent_t a = nullptr;
+        prof_begin(prof, sp, "ba_pose_mfma", &a);
+        if (gd.nslice)
+            hipLaunchKernelGGL(k_ba_pose_slices<BaEdgePacked>, dim3((gd.nslice + 3) / 4), dim3(256),
+                               0, sp, poses, points, es, pose_off, pose_edges, gd.slice_off,
+                               gd.slice_pose, gd.nslice, gd.part);
+        hipLaunchKernelGGL(k_ba_pose_reduce, dim3((42 * npose + 255) / 256), dim3(256), 0, sp,
+                           poses, npose, gd.slice_off, gd.part, hpose, bpose);
+        prof_end(prof, sp, "ba_pose_mfma", a);
+        if (hipEventRecord(evj, sp) != hipSuccess) return -5;
+    }
     BaEdgeOut o{};
     o.hpl = hpl;
     o.stride = 18;
@@ -795,7 +828,7 @@ int launch_ba_graph(hipStream_t st, const orbg_pose *poses, int npose, const dou
                            st, poses, points, es, nedge, point_off, point_edges, o, hpoint, bpoint);
         prof_end(prof, st, "ba_edges", a);
     }
-    if (gd.nspecial) {
+    if (gd.nspecial && ss == st) {
         hipEvent_t a = nullptr;
         prof_begin(prof, st, "ba_special", &a);
         hipLaunchKernelGGL(k_ba_special<BaEdgePacked>, dim3((gd.nspecial + 3) / 4), dim3(256), 0,
@@ -803,7 +836,7 @@ int launch_ba_graph(hipStream_t st, const orbg_pose *poses, int npose, const dou
                            hpoint, bpoint);
         prof_end(prof, st, "ba_special", a);
     }
-    if (npose) {
+    if (npose && sp == st) {
         hipEvent_t a = nullptr;
         prof_begin(prof, st, "ba_pose_mfma", &a);
         if (gd.nslice)
@@ -814,6 +847,7 @@ int launch_ba_graph(hipStream_t st, const orbg_pose *poses, int npose, const dou
                            poses, npose, gd.slice_off, gd.part, hpose, bpose);
         prof_end(prof, st, "ba_pose_mfma", a);
     }
+    if ((sp != st || ss != st) && hipStreamWaitEvent(st, evj, 0) != hipSuccess) return -5;
     return hipGetLastError() == hipSuccess ? 0 : -5;
 }
 

@@ -24,6 +24,13 @@ tail -c 400 $O/ba.json
 echo "[final] single frame (KITTI, TUM)"
 timeout -k 10 200 python tools/single_frame_bench.py 200 > $O/single.jsonl 2> $O/single.err
 timeout -k 10 200 python tools/single_frame_bench.py 200 640 480 1000 >> $O/single.jsonl 2>> $O/single.err
+echo "[final] single frame, C++ drop-in loop (compat_selftest bench)"
+python tools/single_frame_bench.py --write-frames /tmp/sf.raw 16
+timeout -k 10 120 orb_slam2_test_amd/lib/compat_selftest bench 1241 376 /tmp/sf.raw 16 500 2000 > $O/single_cpp.json
+cat $O/single_cpp.json
+echo "[final] SearchByBoW"
+timeout -k 10 200 python tools/bow_match_bench.py > $O/bow_match.json 2> $O/bow_match.err
+tail -c 300 $O/bow_match.json
 echo "[final] C1"
 timeout -k 10 300 python tools/c1_bench.py 16 > $O/c1.json 2> $O/c1.err
 cat $O/c1.json

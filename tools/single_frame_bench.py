@@ -7,6 +7,10 @@ orbg_search_for_initialization).  Timed per frame, next to the oracle (the C res
 on one host thread doing the same per-frame work.
 
 usage: single_frame_bench.py [nframes] [w h nfeatures]  -> one JSON line
+       single_frame_bench.py --write-frames <path> [nimages] [w h]
+           (no GPU call) writes the same synthetic frames as raw bytes for the C++ loop,
+           orb_slam2_test_amd/lib/compat_selftest bench <w> <h> <path> <nimages> <nframes>
+           <nfeatures> (the drop-in as C++ drives it, no interpreter in the loop)
 """
 import json
 import os
@@ -18,7 +22,18 @@ import numpy as np
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
 
+def write_frames():
+    path = sys.argv[2]
+    nimg = int(sys.argv[3]) if len(sys.argv) > 3 else 16
+    w, h = (int(v) for v in sys.argv[4:6]) if len(sys.argv) > 5 else (1241, 376)
+    from orb_slam2_test_amd import synthetic as S
+    frames = S.sequence(nimg, h, w, seed=S.DEFAULT_SEED + 77)
+    np.ascontiguousarray(np.stack(frames), np.uint8).tofile(path)
+
+
 def main():
+    if len(sys.argv) > 2 and sys.argv[1] == "--write-frames":
+        return write_frames()
     n = int(sys.argv[1]) if len(sys.argv) > 1 else 200
     w, h, nf = (int(v) for v in sys.argv[2:5]) if len(sys.argv) > 4 else (1241, 376, 2000)
     from orb_slam2_test_amd import ORBextractor, ORBmatcher, Frame, synthetic as S
