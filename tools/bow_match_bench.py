@@ -136,13 +136,17 @@ def main():
 
         args_l = [(frames[t][1], frames[t][0]["angle"], hv[t, :len(frames[t][0])], fv(t),
                    frames[t + 1][1], frames[t + 1][0]["angle"], fv(t + 1)) for t in range(n)]
+        # the n pairs repeated for about 3 s of CPU work (one pair takes ~0.25 ms)
         t0 = time.perf_counter()
-        for a in args_l:
-            O.search_by_bow(*a, nnratio=0.7, check_ori=True)
+        reps = 0
+        while time.perf_counter() - t0 < 3.0:
+            for a in args_l:
+                O.search_by_bow(*a, nnratio=0.7, check_ori=True)
+            reps += 1
         cdt = time.perf_counter() - t0
-        res["cpu_baseline"] = {"value": round(n / cdt, 1), "unit": "pairs/s", "cores": 1,
-                               "kind": "port", "sample": "%d pairs, oracle/ C restatement -O3, "
-                               "one thread, %.3f s" % (n, cdt)}
+        res["cpu_baseline"] = {"value": round(n * reps / cdt, 1), "unit": "pairs/s", "cores": 1,
+                               "kind": "port", "sample": "%d pairs x %d passes, oracle/ C "
+                               "restatement -O3, one thread, %.2f s" % (n, reps, cdt)}
     print(json.dumps(res), flush=True)
 
 
