@@ -33,7 +33,8 @@ namespace orbg {
 
 #define BM_HISTO 30
 #define BM_TH_LOW 50
-#define BM_LIST 1024  // common nodes per pair held in LDS (a FeatureVector has <= cap nodes)
+#define BM_LIST 1024  // common nodes per pass held in LDS (KeyFrame nodes joined BM_LIST at a time)
+#define BM_MAX_NODE 4096  // Frame features per node the taken mask covers (64 chunks of 64)
 
 struct BowMatchSide {
     const uint8_t *desc;
@@ -90,15 +91,20 @@ __global__ __launch_bounds__(256) void k_bow_match(BowMatchSide K, BowMatchSide 
     const uint8_t *kval = K.valid ? K.valid + (size_t)kf * cap : nullptr;
     int32_t *out = match + (size_t)p * cap;
     if (threadIdx.x == 0) {
-        ncommon = 0;
         nm = 0;
         removed = 0;
     }
     if (threadIdx.x < BM_HISTO) hist[threadIdx.x] = 0;
     for (int i = threadIdx.x; i < n_f; i += blockDim.x) out[i] = -1;
+    int wave_nm = 0;
+    // Nodes are independent (a feature sits in one node of its FeatureVector, so two nodes
+    // share no candidate and no KeyFrame feature): any node order gives the reference's
+    // matches, and the KeyFrame nodes are joined BM_LIST at a time.
+    for (int j0 = 0; j0 < nk_nodes; j0 += BM_LIST) {
+    if (threadIdx.x == 0) ncommon = 0;
     __syncthreads();
     // ---- join: KF node j looks its id up in F's sorted node ids ----
-    for (int j = threadIdx.x; j < nk_nodes; j += blockDim.x) {
+    for (int j = j0 + (int)threadIdx.x; j < min(nk_nodes, j0 + BM_LIST); j += blockDim.x) {
         const int id = kn[j];
         int lo = 0, hi = nf_nodes;  // first F node with id >= kn[j]
         while (lo < hi) {
@@ -110,13 +116,12 @@ __global__ __launch_bounds__(256) void k_bow_match(BowMatchSide K, BowMatchSide 
         }
         if (lo < nf_nodes && fn[lo] == id) {
             const int k = atomicAdd(&ncommon, 1);
-            if (k < BM_LIST) common[k] = make_int2(j, lo);
+            common[k] = make_int2(j, lo);  // k < BM_LIST: at most BM_LIST KF nodes per pass
         }
     }
     __syncthreads();
-    const int nc = min(ncommon, BM_LIST);
+    const int nc = ncommon;
     // ---- a wave per common node ----
-    int wave_nm = 0;
     for (int c = wv; c < nc; c += (int)(blockDim.x >> 6)) {
         const int2 jb = common[c];
         const int k0 = ko[jb.x], k1 = ko[jb.x + 1];
@@ -131,7 +136,7 @@ __global__ __launch_bounds__(256) void k_bow_match(BowMatchSide K, BowMatchSide 
             cd0[w] = ci0 >= 0 ? ((const uint32_t *)(fdesc + (size_t)ci0 * 32))[w] : 0u;
             cd1[w] = ci1 >= 0 ? ((const uint32_t *)(fdesc + (size_t)ci1 * 32))[w] : 0u;
         }
-        uint32_t taken = 0;  // bit k: candidate lane + 64 k already matched
+        uint64_t taken = 0;  // bit k: candidate lane + 64 k already matched (nF <= BM_MAX_NODE)
         for (int ik = k0; ik < k1; ik++) {
             const int rk = __builtin_amdgcn_readfirstlane(kfe[ik]);
             if (kval && !kval[rk]) continue;  // pMP NULL or bad: wave-uniform skip
@@ -171,13 +176,15 @@ __global__ __launch_bounds__(256) void k_bow_match(BowMatchSide K, BowMatchSide 
             if (best1 <= BM_TH_LOW && (float)best1 < nnratio * (float)best2) {
                 wave_nm++;
                 if (winner) {
-                    taken |= 1u << (bpos >> 6);
+                    taken |= 1ull << (bpos >> 6);
                     const int rf = ffe[f0 + (int)bpos];
                     out[rf] = rk;
                     if (check_ori) atomicAdd(&hist[bm_rot_bin(kkp[rk].angle, fkp[rf].angle)], 1);
                 }
             }
         }
+    }
+    __syncthreads();  // the common list is rebuilt by the next pass
     }
     if (lane == 0 && wave_nm) atomicAdd(&nm, wave_nm);
     __syncthreads();
@@ -236,6 +243,7 @@ int launch_bow_match(hipStream_t st, const orbg_bow_frames &kf, const orbg_bow_f
                      int check_ori, int32_t *match, int32_t *nmatch)
 {
     if (npairs <= 0) return 0;
+    if (cap > BM_MAX_NODE) return -95;  // ORBG_ENOTSUP: a node could exceed the taken mask
     const BowMatchSide K{kf.desc, kf.kps, kf.counts, kf.fv_nodes, kf.fv_off, kf.fv_feats, kf.nfv,
                          kf.valid};
     const BowMatchSide F{f.desc, f.kps, f.counts, f.fv_nodes, f.fv_off, f.fv_feats, f.nfv, nullptr};

@@ -29,6 +29,10 @@ namespace orbg {
 #define OCT_T 512
 #define OCT_CODE_DEPTH 14
 
+#ifndef OCT_PC
+#define OCT_PC 4  // cells per wave with their candidate loads in flight (per_cell)
+#endif
+
 #define OCT_NBUCKET 16384  // counting-sort buckets: root (4 bits) + first 5 quadtree digits
 #define OCT_BSHIFT 18      // code >> 18 = root (4 bits) + digits 0..4
 
@@ -224,16 +228,16 @@ __global__ __launch_bounds__(OCT_T) void k_octree_lds(
 
     // ---- bucket histogram over the candidates (vToDistributeKeys order: cell-major, FAST
     //      order inside a cell; candidate k = coff[c] + slot), responses to LDS: one wave per
-    //      cell (lane = slot), four cells' loads in flight.  per_cell(fn) walks the cell lists;
+    //      cell (lane = slot), OCT_PC cells' loads in flight.  per_cell(fn) walks the cell lists;
     //      the scatter walks them again (the lists are L2-resident by then) ----
     auto per_cell = [&](auto &&fn) {
         const int lane = tid & 63, wv = tid >> 6;
         constexpr int NW = OCT_T / 64;
-        for (int c0 = wv; c0 < ncells; c0 += 4 * NW) {
-            uint2 e[4];
-            int k[4], cnt[4];
+        for (int c0 = wv; c0 < ncells; c0 += OCT_PC * NW) {
+            uint2 e[OCT_PC];
+            int k[OCT_PC], cnt[OCT_PC];
 #pragma unroll
-            for (int u = 0; u < 4; u++) {
+            for (int u = 0; u < OCT_PC; u++) {
                 const int c = c0 + u * NW;
                 cnt[u] = 0;
                 k[u] = 0;
@@ -246,7 +250,7 @@ __global__ __launch_bounds__(OCT_T) void k_octree_lds(
                 }
             }
 #pragma unroll
-            for (int u = 0; u < 4; u++) {
+            for (int u = 0; u < OCT_PC; u++) {
                 if (lane < cnt[u]) fn(k[u], e[u]);
                 for (int kl = lane + 64; kl < cnt[u]; kl += 64) {  // cells with > 64 corners
                     const int c = c0 + u * NW;
@@ -261,7 +265,13 @@ __global__ __launch_bounds__(OCT_T) void k_octree_lds(
         atomicAdd(&V.bcnt[b >> 1], 1u << (16 * (b & 1)));
     });
     __syncthreads();
-    if (g->dbg == 1) return;
+    // developer phase stops (ORBG_DBG 1-4, developer builds only): the level is left empty
+    auto dbg_stop = [&](int d) {
+        if (g->dbg != d) return false;
+        if (tid == 0) lvl_cnt[(int64_t)f * g->L + l] = 0;
+        return true;
+    };
+    if (dbg_stop(1)) return;
     // ---- exclusive scan of the nini * 1024 u16 bucket counters (2 * nini per thread) ----
     {
         const int PER = D.nbw / OCT_T;  // words per thread (= roots)
@@ -287,7 +297,7 @@ __global__ __launch_bounds__(OCT_T) void k_octree_lds(
         V.sidx[slot] = (uint16_t)k;
     });
     __syncthreads();
-    if (g->dbg == 2) return;
+    if (dbg_stop(2)) return;
 
     // ---- roots (:705-739): contiguous by the top 4 code bits ----
     if (tid <= nIni) S.rootlo[tid] = 0;
@@ -410,6 +420,7 @@ __global__ __launch_bounds__(OCT_T) void k_octree_lds(
         }
     }
 
+    if (dbg_stop(3)) return;
     // ================= phase 2 rounds (:859-924) =================
     if (S.s_phase2 && !S.s_err) {
         while (true) {
@@ -536,6 +547,7 @@ __global__ __launch_bounds__(OCT_T) void k_octree_lds(
         }
     }
 
+    if (dbg_stop(4)) return;
     // ================= best key per node, list order (:932-948) =================
     const int alive = S.s_alive, cur = S.s_cur;
     if (S.s_err) {

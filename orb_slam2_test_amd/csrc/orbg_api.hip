@@ -3661,6 +3661,7 @@ extern "C" int orbg_search_by_bow_batch_device(orbg_ctx *c, const orbg_bow_frame
     PROF_LAUNCH(c, "bow_match",
                 rc = launch_bow_match(st, *kf, *f, cap, d_kf_index, d_f_index, npairs, nnratio,
                                       check_ori, d_match, d_nmatch));
+    if (rc == ORBG_ENOTSUP) return set_err(ORBG_ENOTSUP, "SearchByBoW: more than 4096 features per frame");
     if (rc) return set_err(ORBG_EIO, "k_bow_match launch failed");
     return ORBG_OK;
 }
@@ -3752,6 +3753,7 @@ extern "C" int orbg_search_by_bow(orbg_ctx *c, const uint8_t *kf_desc, const flo
     const int32_t *di = (const int32_t *)(db + o_idx);
     rc = launch_bow_match(c->stream, K, F, cap, di, di + 1, 1, nnratio, check_ori,
                           (int32_t *)(db + o_match), (int32_t *)(db + o_nm));
+    if (rc == ORBG_ENOTSUP) return set_err(ORBG_ENOTSUP, "SearchByBoW: more than 4096 features per frame");
     if (rc) return set_err(ORBG_EIO, "k_bow_match launch failed");
     HIPCHK(hipMemcpyAsync(hs + o_match, db + o_match, cp * 4 + 256, hipMemcpyDeviceToHost, c->stream));
     HIPCHK(hipStreamSynchronize(c->stream));

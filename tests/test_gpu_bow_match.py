@@ -6,8 +6,9 @@ oracle (oracle/bow_oracle.c orc_search_by_bow), bit for bit: every match index a
 Cases: the synthetic rule cases of tests/test_oracle_bow_match.py; real ORB features of
 consecutive synthetic KITTI frames with FeatureVectors from DBoW2's transform over a synthetic
 k = 10, L = 6 vocabulary (ORBvoc.txt's shape; the real file is a missing blob) at levelsup 4
-(ComputeBoW's) and at levelsup 6 (every feature in the root node: one node of ~2000 F
-features, the kernel's > 128-candidate path); invalid MapPoints; empty inputs; and the
+(ComputeBoW's), at levelsup 6 (every feature in the root node: one node of ~2000 F
+features, the kernel's > 128-candidate path) and at levelsup 1 (> 1024 nodes per frame:
+several node-join passes); invalid MapPoints; empty inputs; and the
 batched device entry over a batch of frames, frame t's reference KeyFrame = frame t - 1.
 """
 import numpy as np
@@ -52,7 +53,7 @@ def kitti(oracle):
     return ex, gv
 
 
-@pytest.mark.parametrize("levelsup", [4, 6])
+@pytest.mark.parametrize("levelsup", [4, 6, 1])
 def test_kitti_frames(oracle, kitti, levelsup):
     ex, gv = kitti
     rng = np.random.default_rng(levelsup)
@@ -68,9 +69,11 @@ def test_kitti_frames(oracle, kitti, levelsup):
         rn, ref = oracle.search_by_bow(a["desc"], a["kps"]["angle"], valid, kfv, b["desc"],
                                        b["kps"]["angle"], ffv, 0.7, True)
         assert n == rn and np.array_equal(got, ref), t
-        assert rn > 100, (t, rn)
+        assert rn > (0 if levelsup == 1 else 100), (t, rn)
         if levelsup == 6:
             assert len(ffv[0]) == 1 and ffv[1][1] > 128  # one root node, > 128 candidates
+        if levelsup == 1:
+            assert len(kfv[0]) > 1024  # more KeyFrame nodes than one join pass holds
 
 
 def test_empty_inputs(oracle):
