@@ -529,27 +529,22 @@ __global__ __launch_bounds__(256) void k_ba_pose_mfma(const orbg_pose *__restric
 // graph path, pass 1: one wave per slice (the graph's slice tables, built once), the
 // slice's [H | b] partial (6 x 7) stored -- no fills, no atomics
 template <class ES>
-__global__ __launch_bounds__(256) void k_ba_pose_slices(const orbg_pose *__restrict__ poses,
-                                                        const double *__restrict__ points,
-                                                        const ES edges,
-                                                        const int32_t *__restrict__ pose_off,
-                                                        const int32_t *__restrict__ pose_edges,
-                                                        const int32_t *__restrict__ slice_off,
-                                                        const int32_t *__restrict__ slice_pose,
-                                                        int nslice, double *__restrict__ part)
+__device__ __forceinline__ void ba_slice_part(const orbg_pose *__restrict__ poses,
+                                              const double *__restrict__ points, const ES &edges,
+                                              const int32_t *__restrict__ pose_off,
+                                              const int32_t *__restrict__ pose_edges,
+                                              const int32_t *__restrict__ slice_off,
+                                              const int32_t *__restrict__ slice_pose, int sl,
+                                              double *__restrict__ part, double *rows, int lane)
 {
-    __shared__ double rows_lds[4][3 * BA_SLICE * BA_ROW];  // 12 KB per wave
-    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-    const int sl = blockIdx.x * 4 + wv;
-    if (sl >= nslice) return;  // wave-uniform; no workgroup barrier below
     const int p = slice_pose[sl];
     const orbg_pose P = poses[p];
-    if (P.fixed) return;       // pass 2 writes the zero block
+    if (P.fixed) return;  // pass 2 writes the zero block
     const int e0p = pose_off[p], nep = pose_off[p + 1] - e0p;
     const int ks = sl - slice_off[p];
     v4d C = {0, 0, 0, 0};
     ba_pose_slice(P, points, edges, pose_edges, e0p + ks * BA_SLICE,
-                  min(BA_SLICE, nep - ks * BA_SLICE), rows_lds[wv], lane, C);
+                  min(BA_SLICE, nep - ks * BA_SLICE), rows, lane, C);
     const int j = lane & 15;
 #pragma unroll
     for (int v = 0; v < 4; v++) {
@@ -586,20 +581,15 @@ __global__ __launch_bounds__(256) void k_ba_pose_reduce(const orbg_pose *__restr
 // and points without edges (zero block).  Lane l computes edge l's share (chunks of 64),
 // lanes 0..11 sum one block entry each over the edges in order.
 template <class ES>
-__global__ __launch_bounds__(256) void k_ba_special(const orbg_pose *__restrict__ poses,
-                                                    const double *__restrict__ points,
-                                                    const ES edges,
-                                                    const int32_t *__restrict__ point_off,
-                                                    const int32_t *__restrict__ point_edges,
-                                                    const int32_t *__restrict__ special, int nsp,
-                                                    double *__restrict__ hpoint,
-                                                    double *__restrict__ bpoint)
+__device__ __forceinline__ void ba_special_point(const orbg_pose *__restrict__ poses,
+                                                 const double *__restrict__ points,
+                                                 const ES &edges,
+                                                 const int32_t *__restrict__ point_off,
+                                                 const int32_t *__restrict__ point_edges, int q,
+                                                 double *__restrict__ hpoint,
+                                                 double *__restrict__ bpoint, double (*sh)[64],
+                                                 int lane)
 {
-    __shared__ double sh[4][12][64];
-    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-    const int i = blockIdx.x * 4 + wv;
-    if (i >= nsp) return;  // wave-uniform; no workgroup barrier below
-    const int q = special[i];
     const double X[3] = {points[3 * (size_t)q], points[3 * (size_t)q + 1], points[3 * (size_t)q + 2]};
     const int a0 = point_off[q], a1 = point_off[q + 1];
     double acc = 0;  // lanes 0..11: entry `lane` of [H_ll | b_l]
@@ -617,16 +607,44 @@ __global__ __launch_bounds__(256) void k_ba_special(const orbg_pose *__restrict_
         }
         wave_sync_lds_ba();
 #pragma unroll
-        for (int k = 0; k < 12; k++) sh[wv][k][lane] = c[k];
+        for (int k = 0; k < 12; k++) sh[k][lane] = c[k];
         wave_sync_lds_ba();
         const int n = min(64, a1 - c0);
         if (lane < 12)
-            for (int j = 0; j < n; j++) acc += sh[wv][lane][j];
+            for (int j = 0; j < n; j++) acc += sh[lane][j];
     }
     if (lane < 9)
         hpoint[9 * (size_t)q + lane] = acc;
     else if (lane < 12)
         bpoint[3 * (size_t)q + lane - 9] = acc;
+}
+
+// graph path, pass 1: one launch, a wave per task -- the special points first (waves
+// [0, 4 * nb_special): their chains of 64-edge chunks are the longest), then one wave per
+// 64-edge slice of a pose (MFMA f64 partial of [H_pp | b_p]).  Both read only the graph and
+// the estimate; merging them hides the special points' latency behind the slices.
+template <class ES>
+__global__ __launch_bounds__(256) void k_ba_slices_special(
+    const orbg_pose *__restrict__ poses, const double *__restrict__ points, const ES edges,
+    const int32_t *__restrict__ pose_off, const int32_t *__restrict__ pose_edges,
+    const int32_t *__restrict__ slice_off, const int32_t *__restrict__ slice_pose, int nslice,
+    double *__restrict__ part, const int32_t *__restrict__ point_off,
+    const int32_t *__restrict__ point_edges, const int32_t *__restrict__ special, int nsp,
+    int nb_special, double *__restrict__ hpoint, double *__restrict__ bpoint)
+{
+    __shared__ double rows_lds[4][3 * BA_SLICE * BA_ROW];  // 12 KB per wave (special: 6 KB)
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    if ((int)blockIdx.x < nb_special) {
+        const int i = blockIdx.x * 4 + wv;
+        if (i >= nsp) return;  // wave-uniform; no workgroup barrier in either path
+        ba_special_point(poses, points, edges, point_off, point_edges, special[i], hpoint, bpoint,
+                         (double(*)[64])rows_lds[wv], lane);
+        return;
+    }
+    const int sl = ((int)blockIdx.x - nb_special) * 4 + wv;
+    if (sl >= nslice) return;
+    ba_slice_part(poses, points, edges, pose_off, pose_edges, slice_off, slice_pose, sl, part,
+                  rows_lds[wv], lane);
 }
 
 // slice -> pose table: pose p owns ceil(edges_p / BA_SLICE) consecutive slices
@@ -772,51 +790,19 @@ int launch_ba_device(hipStream_t st, const orbg_pose *poses, int npose, const do
                               hpoint, bpoint, scr, prof, jacobians, errors, hpl);
 }
 
-// an orbg_ba_graph's buildSystem: H_pl compact, no per-edge record, and the structure
 // precomputed once per graph (BaGraphDev): the exact slice tables, the special vertices, the
-// pose partials and arrival counters -- no zero fills, no slice-table kernel, no atomics on
-// the blocks per build
+// pose partials -- no zero fills, no slice-table kernel, no atomics on the blocks per build.
+// Three launches: the edge pass, the special points + pose slices, the pose reduce.  (Round 4
+// measured the pose blocks or the special points on a second stream beside the edge pass:
+// slower, the edge pass fills the chip; profiles/r04n_ba_overlap_ab.txt.)
 int launch_ba_graph(hipStream_t st, const orbg_pose *poses, int npose, const double *points,
                     int npoint, const BaPackedEdge *edges, const BaCam *cam, const BaInfo *info,
                     int nedge, const int32_t *pose_off, const int32_t *pose_edges,
                     const int32_t *point_off, const int32_t *point_edges, const BaGraphDev &gd,
                     double *hpl, double *hpose, double *bpose, double *hpoint, double *bpoint,
-                    void *prof, hipStream_t st2, hipEvent_t evf, hipEvent_t evj, int overlap)
+                    void *prof)
 {
     const BaEdgePacked es{edges, cam, info};
-    // the pose blocks and the special points read only the graph and the estimate, like the
-    // edge pass: with st2, overlap 1 runs the pose blocks beside it, 2 the special points (fork
-    // after the caller's work on st, join back into st before return).  Measured: the edge
-    // pass fills the chip, so neither gains (profiles/r04n_ba_overlap_ab.txt); default 0
-    hipStream_t sp = st, ss = st;
-    if (st2 && overlap == 2 && gd.nspecial && nedge) {
-        // the special points beside the edge pass (a few hundred latency-bound waves)
-        if (hipEventRecord(evf, st) != hipSuccess || hipStreamWaitEvent(st2, evf, 0) != hipSuccess)
-            return -5;
-        ss = st2;
-        hipEvent_t a = nullptr;
-        prof_begin(prof, ss, "ba_special", &a);
-        hipLaunchKernelGGL(k_ba_special<BaEdgePacked>, dim3((gd.nspecial + 3) / 4), dim3(256), 0,
-                           ss, poses, points, es, point_off, point_edges, gd.special, gd.nspecial,
-                           hpoint, bpoint);
-        prof_end(prof, ss, "ba_special", a);
-        if (hipEventRecord(evj, ss) != hipSuccess) return -5;
-    }
-    if (st2 && overlap == 1 && npose && nedge) {
-        if (hipEventRecord(evf, st) != hipSuccess || hipStreamWaitEvent(st2, evf, 0) != hipSuccess)
-            return -5;
-        sp = st2;
-        hipEvent_t a = nullptr;
-        prof_begin(prof, sp, "ba_pose_mfma", &a);
-        if (gd.nslice)
-            hipLaunchKernelGGL(k_ba_pose_slices<BaEdgePacked>, dim3((gd.nslice + 3) / 4), dim3(256),
-                               0, sp, poses, points, es, pose_off, pose_edges, gd.slice_off,
-                               gd.slice_pose, gd.nslice, gd.part);
-        hipLaunchKernelGGL(k_ba_pose_reduce, dim3((42 * npose + 255) / 256), dim3(256), 0, sp,
-                           poses, npose, gd.slice_off, gd.part, hpose, bpose);
-        prof_end(prof, sp, "ba_pose_mfma", a);
-        if (hipEventRecord(evj, sp) != hipSuccess) return -5;
-    }
     BaEdgeOut o{};
     o.hpl = hpl;
     o.stride = 18;
@@ -828,26 +814,23 @@ int launch_ba_graph(hipStream_t st, const orbg_pose *poses, int npose, const dou
                            st, poses, points, es, nedge, point_off, point_edges, o, hpoint, bpoint);
         prof_end(prof, st, "ba_edges", a);
     }
-    if (gd.nspecial && ss == st) {
-        hipEvent_t a = nullptr;
-        prof_begin(prof, st, "ba_special", &a);
-        hipLaunchKernelGGL(k_ba_special<BaEdgePacked>, dim3((gd.nspecial + 3) / 4), dim3(256), 0,
-                           st, poses, points, es, point_off, point_edges, gd.special, gd.nspecial,
-                           hpoint, bpoint);
-        prof_end(prof, st, "ba_special", a);
-    }
-    if (npose && sp == st) {
+    const int nb_special = (gd.nspecial + 3) / 4, nb_slice = npose ? (gd.nslice + 3) / 4 : 0;
+    if (nb_special + nb_slice) {
         hipEvent_t a = nullptr;
         prof_begin(prof, st, "ba_pose_mfma", &a);
-        if (gd.nslice)
-            hipLaunchKernelGGL(k_ba_pose_slices<BaEdgePacked>, dim3((gd.nslice + 3) / 4), dim3(256),
-                               0, st, poses, points, es, pose_off, pose_edges, gd.slice_off,
-                               gd.slice_pose, gd.nslice, gd.part);
-        hipLaunchKernelGGL(k_ba_pose_reduce, dim3((42 * npose + 255) / 256), dim3(256), 0, st,
-                           poses, npose, gd.slice_off, gd.part, hpose, bpose);
+        hipLaunchKernelGGL(k_ba_slices_special<BaEdgePacked>, dim3(nb_special + nb_slice),
+                           dim3(256), 0, st, poses, points, es, pose_off, pose_edges,
+                           gd.slice_off, gd.slice_pose, npose ? gd.nslice : 0, gd.part, point_off,
+                           point_edges, gd.special, gd.nspecial, nb_special, hpoint, bpoint);
         prof_end(prof, st, "ba_pose_mfma", a);
     }
-    if ((sp != st || ss != st) && hipStreamWaitEvent(st, evj, 0) != hipSuccess) return -5;
+    if (npose) {
+        hipEvent_t a = nullptr;
+        prof_begin(prof, st, "ba_pose_reduce", &a);
+        hipLaunchKernelGGL(k_ba_pose_reduce, dim3((42 * npose + 255) / 256), dim3(256), 0, st,
+                           poses, npose, gd.slice_off, gd.part, hpose, bpose);
+        prof_end(prof, st, "ba_pose_reduce", a);
+    }
     return hipGetLastError() == hipSuccess ? 0 : -5;
 }
 

@@ -126,7 +126,7 @@ int launch_ba_graph(hipStream_t st, const orbg_pose *poses, int npose, const dou
                     int nedge, const int32_t *pose_off, const int32_t *pose_edges,
                     const int32_t *point_off, const int32_t *point_edges, const BaGraphDev &gd,
                     double *hpl, double *hpose, double *bpose, double *hpoint, double *bpoint,
-                    void *prof, hipStream_t st2, hipEvent_t evf, hipEvent_t evj, int overlap);
+                    void *prof);
 }  // namespace orbg
 
 using namespace orbg;
@@ -301,8 +301,6 @@ struct orbg_ctx {
     // `mstream` after the work queued on the context stream so far (ev_caller): a fill the
     // caller queued there before the call can never land after liborbg's write
     hipEvent_t ev_caller = nullptr;
-    hipEvent_t ev_bafork = nullptr, ev_bajoin = nullptr;  // BA graph build: pose blocks on aux_stream
-    int ba_overlap = 0;  // ORBG_BA_OVERLAP: 1 pose blocks, 2 special points beside the edge pass (A/B)
     hipEvent_t ev_cells[2] = {nullptr, nullptr}, ev_front[2] = {nullptr, nullptr};
     hipEvent_t ev_back[2] = {nullptr, nullptr};
     bool back_pending[2] = {false, false};
@@ -1332,8 +1330,6 @@ extern "C" int orbg_create(int device, const orbg_params *p, orbg_ctx **out)
     hipEventCreateWithFlags(&c->ev_rel[1], hipEventDisableTiming);
     hipEventCreateWithFlags(&c->ev_srel, hipEventDisableTiming);
     hipEventCreateWithFlags(&c->ev_caller, hipEventDisableTiming);
-    hipEventCreateWithFlags(&c->ev_bafork, hipEventDisableTiming);
-    hipEventCreateWithFlags(&c->ev_bajoin, hipEventDisableTiming);
     if (const char *e = getenv("ORBG_PIPELINE")) c->pipelined = atoi(e) && c->ostream;
     if (const char *e = getenv("ORBG_FAST_ROWS")) c->fr_mode = atoi(e);
 #ifdef ORBG_DEV_KNOBS
@@ -1345,7 +1341,6 @@ extern "C" int orbg_create(int device, const orbg_params *p, orbg_ctx **out)
         fprintf(stderr, "liborbg: ORBG_SKIP / ORBG_DBG ignored (developer builds only, make "
                         "DEV=1)\n");
 #endif
-    if (const char *e = getenv("ORBG_BA_OVERLAP")) c->ba_overlap = atoi(e);
     if (const char *fi = getenv("ORBG_FAULT_INJECT"))
         fprintf(stderr, "liborbg: ORBG_FAULT_INJECT=%s set -- %s\n", fi,
                 strcmp(fi, "octree_overflow") ? "unknown value, ignored"
@@ -1390,7 +1385,7 @@ extern "C" void orbg_destroy(orbg_ctx *c)
     if (c->ev_fast) hipEventDestroy(c->ev_fast);
     if (c->ev_oct) hipEventDestroy(c->ev_oct);
     for (hipEvent_t e : {c->ev_sback, c->ev_ssum, c->ev_rel[0], c->ev_rel[1], c->ev_srel,
-                         c->ev_caller, c->ev_bafork, c->ev_bajoin})
+                         c->ev_caller})
         if (e) hipEventDestroy(e);
     if (c->mstream) hipStreamDestroy(c->mstream);
     if (c->own_stream) hipStreamDestroy(c->own_stream);
@@ -2959,8 +2954,7 @@ extern "C" int orbg_ba_graph_build_system(orbg_ctx *c, orbg_ba_graph *g, const o
     const int rc = launch_ba_graph(c->stream, d_poses, g->npose, d_points, g->npoint, g->d_edges,
                                    g->d_cam, g->d_info, g->nedge, g->d_off, g->d_pe, g->d_qoff,
                                    g->d_qe, g->gd, d_hpl, d_hpose, d_bpose, d_hpoint, d_bpoint,
-                                   &c->prof, c->ba_overlap ? c->aux_stream : nullptr, c->ev_bafork,
-                                   c->ev_bajoin, c->ba_overlap);
+                                   &c->prof);
     if (rc) return set_err(ORBG_EIO, "BA kernel launch failed");
     return ORBG_OK;
 }
