@@ -21,6 +21,7 @@
 //   SearchForInitialization ......... ORBmatcher.cc:487-631 (include/ORBmatcher.h:47)
 //   SearchByProjection (last frame) .. ORBmatcher.cc:1503-1667 (ORBmatcher.h:62)
 //   SearchByProjection (local map) ... ORBmatcher.cc:59-154 (ORBmatcher.h:51)
+//   SearchByBoW (KeyFrame, Frame) .... ORBmatcher.cc:195-348 (ORBmatcher.h:57)
 //   DescriptorDistance ............... ORBmatcher.cc:1846-1862 (ORBmatcher.h:128)
 //   PoseOptimization ................. Optimizer.cc:356-631 (include/Optimizer.h:49)
 //   LocalBundleAdjustment window ..... Optimizer.cc:633-851: the vertex / edge set g2o builds
@@ -280,6 +281,56 @@ int SearchByProjection(orbg_ctx *ctx, float nnratio, FrameT &F,
           "orbg_search_by_projection_local");
     for (int i = 0; i < n; i++)
         if (match[i] >= 0) F.mvpMapPoints[i] = vpMapPoints[match[i]];
+    return nm;
+}
+
+// DBoW2::FeatureVector (std::map<NodeId, std::vector<unsigned int>>, ascending ids and
+// indices) -> the ABI's CSR arrays (nodes, off[nodes + 1], feats)
+template <class FeatVecT>
+inline void flatten_fv(const FeatVecT &fv, std::vector<int32_t> &nodes, std::vector<int32_t> &off,
+                       std::vector<int32_t> &feats)
+{
+    nodes.clear();
+    feats.clear();
+    off.assign(1, 0);
+    for (const auto &e : fv) {
+        nodes.push_back((int32_t)e.first);
+        for (auto f : e.second) feats.push_back((int32_t)f);
+        off.push_back((int32_t)feats.size());
+    }
+}
+
+// ORBmatcher(nnratio, checkOri).SearchByBoW(pKF, F, vpMapPointMatches)
+// (Tracking::TrackReferenceKeyFrame Tracking.cc:1069, Relocalization :2009): both frames'
+// mFeatVec after ComputeBoW; vpMapPointMatches = F.N entries, the KeyFrame's MapPoint per
+// matched Frame feature or NULL (ORBmatcher.cc:197, 276).
+template <class KeyFrameT, class FrameT, class MapPointT>
+int SearchByBoW(orbg_ctx *ctx, float nnratio, bool checkOri, KeyFrameT *pKF, FrameT &F,
+                std::vector<MapPointT *> &vpMapPointMatches)
+{
+    const std::vector<MapPointT *> vpMPs = pKF->GetMapPointMatches();
+    const int nk = (int)pKF->mvKeysUn.size(), nf = F.N;
+    std::vector<uint8_t> valid(nk > 0 ? nk : 1, 0);
+    std::vector<float> ak(nk > 0 ? nk : 1), af(nf > 0 ? nf : 1);
+    for (int i = 0; i < nk; i++) {
+        valid[i] = vpMPs[i] && !vpMPs[i]->isBad();
+        ak[i] = pKF->mvKeysUn[i].angle;
+    }
+    for (int i = 0; i < nf; i++) af[i] = F.mvKeys[i].angle;
+    std::vector<int32_t> kn, ko, kf, fn, fo, ff;
+    flatten_fv(pKF->mFeatVec, kn, ko, kf);
+    flatten_fv(F.mFeatVec, fn, fo, ff);
+    const std::vector<uint8_t> kd = rows32(pKF->mDescriptors, nk), fd = rows32(F.mDescriptors, nf);
+    std::vector<int32_t> match(nf > 0 ? nf : 1);
+    int nm = 0;
+    check(orbg_search_by_bow(ctx, kd.data(), ak.data(), valid.data(), nk, kn.data(), ko.data(),
+                             kf.data(), (int)kn.size(), fd.data(), af.data(), nf, fn.data(),
+                             fo.data(), ff.data(), (int)fn.size(), nnratio, checkOri ? 1 : 0,
+                             match.data(), &nm),
+          "orbg_search_by_bow");
+    vpMapPointMatches.assign(nf, static_cast<MapPointT *>(nullptr));
+    for (int i = 0; i < nf; i++)
+        if (match[i] >= 0) vpMapPointMatches[i] = vpMPs[match[i]];
     return nm;
 }
 

@@ -358,11 +358,10 @@ __global__ __launch_bounds__(OCT_T) void k_octree_lds(
                         }
                     }
                 }
-                int t1, t2;
-                oct_scan(e, &t1, S.red);
-                oct_scan(m, &t2, S.red);
-                tot_e += t1;
-                nexp += t2;
+                int t;  // both totals from one scan (each < 2^16: e, m <= 4 per node)
+                oct_scan(e | (m << 16), &t, S.red);
+                tot_e += t & 0xFFFF;
+                nexp += t >> 16;
             }
             ee[ch] = e;
             spp[ch] = sp;

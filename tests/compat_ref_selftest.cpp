@@ -60,6 +60,7 @@ struct Frame {  // include/Frame.h
     cv::Mat mDescriptors, mTcw;
     std::vector<MapPoint *> mvpMapPoints;
     std::vector<bool> mvbOutlier;
+    std::map<unsigned int, std::vector<unsigned int>> mFeatVec;  // DBoW2::FeatureVector
     float mbf = 0, mb = 0;
     int mnScaleLevels = 8;
     float mfScaleFactor = 1.2f;
@@ -73,9 +74,12 @@ struct KeyFrame {  // include/KeyFrame.h
     float fx, fy, cx, cy, mbf;
     std::vector<cv::KeyPoint> mvKeysUn;
     std::vector<float> mvuRight, mvInvLevelSigma2;
-    cv::Mat Tcw;
+    cv::Mat Tcw, mDescriptors;
+    std::vector<MapPoint *> mvpMapPoints;
+    std::map<unsigned int, std::vector<unsigned int>> mFeatVec;  // DBoW2::FeatureVector
     bool bad = false;
     cv::Mat GetPose() const { return Tcw.clone(); }
+    std::vector<MapPoint *> GetMapPointMatches() const { return mvpMapPoints; }
     bool isBad() const { return bad; }
 };
 
@@ -397,8 +401,80 @@ int main(int argc, char **argv)
     }
     std::printf("threads ok: Tracking and LocalMapping calls concurrent on their own contexts\n");
 
+    // ---- ORBmatcher(0.7, true).SearchByBoW(pKF, F) (Tracking::TrackReferenceKeyFrame) ----
+    // KeyFrame = frame 1, Frame = frame 2; FeatureVectors by a fixed 128 x 64 px grid of
+    // "nodes" (a stand-in for ComputeBoW's levelsup-4 nodes); every third KeyFrame feature
+    // without a MapPoint, every seventh one bad.  With an output directory the inputs and the
+    // result are written for tests/test_compat_ref.py to replay through the oracle.
+    int nbow = 0;
+    {
+        auto node_of = [](const cv::KeyPoint &k) {
+            return (unsigned)((int)(k.pt.x / 128) + 16 * (int)(k.pt.y / 64));
+        };
+        KeyFrame RK;
+        RK.mvKeysUn = F1.mvKeysUn;
+        RK.mDescriptors = F1.mDescriptors;
+        std::vector<MapPoint> pts(F1.N);
+        RK.mvpMapPoints.assign(F1.N, nullptr);
+        for (int i = 0; i < F1.N; i++) {
+            RK.mFeatVec[node_of(F1.mvKeysUn[i])].push_back((unsigned)i);
+            if (i % 3 == 2) continue;
+            pts[i].bad = i % 7 == 3;
+            RK.mvpMapPoints[i] = &pts[i];
+        }
+        Frame FB = F2;
+        for (int i = 0; i < FB.N; i++) FB.mFeatVec[node_of(FB.mvKeys[i])].push_back((unsigned)i);
+        std::vector<MapPoint *> vpm;
+        nbow = orbg_compat::ref::SearchByBoW(ctx, 0.7f, true, &RK, FB, vpm);
+        REQUIRE((int)vpm.size() == FB.N && nbow > 50);
+        int nn = 0;
+        for (int i = 0; i < FB.N; i++) {
+            if (!vpm[i]) continue;
+            nn++;
+            const MapPoint *m = vpm[i];
+            const int k = (int)(m - pts.data());
+            REQUIRE(k >= 0 && k < F1.N && !m->bad);
+            REQUIRE(node_of(F1.mvKeysUn[k]) == node_of(FB.mvKeys[i]));
+            REQUIRE(orbg_compat::ref::DescriptorDistance(F1.mDescriptors.ptr<uint8_t>(k),
+                                                         FB.mDescriptors.ptr<uint8_t>(i)) <= 50);
+        }
+        REQUIRE(nn == nbow);
+        if (argc >= 6) {
+            const std::string o = argv[5];
+            std::vector<int32_t> kn, ko, kf, fn, fo, ff, mi(FB.N);
+            orbg_compat::ref::flatten_fv(RK.mFeatVec, kn, ko, kf);
+            orbg_compat::ref::flatten_fv(FB.mFeatVec, fn, fo, ff);
+            std::vector<uint8_t> valid(F1.N);
+            std::vector<float> ak(F1.N), af(FB.N);
+            for (int i = 0; i < F1.N; i++) {
+                valid[i] = RK.mvpMapPoints[i] && !RK.mvpMapPoints[i]->bad;
+                ak[i] = F1.mvKeysUn[i].angle;
+            }
+            for (int i = 0; i < FB.N; i++) {
+                af[i] = FB.mvKeys[i].angle;
+                mi[i] = vpm[i] ? (int32_t)(vpm[i] - pts.data()) : -1;
+            }
+            const std::vector<uint8_t> kd = orbg_compat::ref::rows32(F1.mDescriptors, F1.N),
+                                       fd = orbg_compat::ref::rows32(FB.mDescriptors, FB.N);
+            write_vec(o + "/bow_kd.u8", kd.data(), kd.size());
+            write_vec(o + "/bow_fd.u8", fd.data(), fd.size());
+            write_vec(o + "/bow_ka.f32", ak.data(), ak.size());
+            write_vec(o + "/bow_fa.f32", af.data(), af.size());
+            write_vec(o + "/bow_kv.u8", valid.data(), valid.size());
+            write_vec(o + "/bow_kn.i32", kn.data(), kn.size());
+            write_vec(o + "/bow_ko.i32", ko.data(), ko.size());
+            write_vec(o + "/bow_kf.i32", kf.data(), kf.size());
+            write_vec(o + "/bow_fn.i32", fn.data(), fn.size());
+            write_vec(o + "/bow_fo.i32", fo.data(), fo.size());
+            write_vec(o + "/bow_ff.i32", ff.data(), ff.size());
+            write_vec(o + "/bow_match.i32", mi.data(), mi.size());
+            const int32_t nbv = nbow;
+            write_vec(o + "/bow_n.i32", &nbv, 1);
+        }
+    }
+
     std::printf("compat_ref ok: %d + %d keypoints, SearchForInitialization %d, SearchByProjection %d, "
-                "PoseOptimization inliers %d, LBA edges %zu, chi2 %.6g\n",
-                F1.N, F2.N, nsfi, nproj, ninl, win.edges.size(), sys.active_robust_chi2);
+                "PoseOptimization inliers %d, LBA edges %zu, chi2 %.6g, SearchByBoW %d\n",
+                F1.N, F2.N, nsfi, nproj, ninl, win.edges.size(), sys.active_robust_chi2, nbow);
     return 0;
 }

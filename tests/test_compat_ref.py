@@ -7,7 +7,8 @@ compiles against tests/compat_stub/ (a test-only stand-in of the cv:: subset the
 CPU: the program and both headers compile (g++ -Wall -Werror).  GPU: it runs on two
 synthetic KITTI-shaped frames and checks the drop-ins against the plain-buffer layer (same
 matches, same prev positions, same H blocks) and the reference's invariants (matched map
-points within TH_HIGH, hessian blocks in vertex-id order).
+points within TH_HIGH, hessian blocks in vertex-id order), and replays its SearchByBoW call
+through the oracle (every vpMapPointMatches entry and the count).
 """
 import os
 import subprocess
@@ -42,10 +43,25 @@ def test_drop_in_layer_runs(tmp_path):
         p = tmp_path / ("f%d.raw" % i)
         np.ascontiguousarray(fr[i]).tofile(p)
         paths.append(str(p))
-    r = subprocess.run([exe, paths[0], paths[1], "1241", "376"], capture_output=True, text=True,
-                       timeout=120)
+    out = tmp_path / "out"
+    out.mkdir()
+    r = subprocess.run([exe, paths[0], paths[1], "1241", "376", str(out)], capture_output=True,
+                       text=True, timeout=120)
     assert r.returncode == 0, (r.stdout + r.stderr)[-3000:]
     assert "compat_ref ok" in r.stdout
+    # SearchByBoW through the drop-in (KeyFrame / Frame stand-ins, grid FeatureVectors):
+    # replayed through the oracle on the inputs the program wrote
+    from oracle import pyoracle as O
+
+    def rd(name, dt):
+        return np.fromfile(str(out / name), dt)
+    kd, fd = rd("bow_kd.u8", np.uint8).reshape(-1, 32), rd("bow_fd.u8", np.uint8).reshape(-1, 32)
+    kfv = (rd("bow_kn.i32", np.int32), rd("bow_ko.i32", np.int32), rd("bow_kf.i32", np.int32))
+    ffv = (rd("bow_fn.i32", np.int32), rd("bow_fo.i32", np.int32), rd("bow_ff.i32", np.int32))
+    rn, ref = O.search_by_bow(kd, rd("bow_ka.f32", np.float32), rd("bow_kv.u8", np.uint8), kfv,
+                              fd, rd("bow_fa.f32", np.float32), ffv, nnratio=0.7, check_ori=True)
+    assert int(rd("bow_n.i32", np.int32)[0]) == rn
+    assert np.array_equal(rd("bow_match.i32", np.int32), ref)
 
 
 def _lba_scene(rng):
