@@ -38,6 +38,11 @@
  *                                     TemplatedVocabulary.h:1126-1189, 1220-1259; Frame.cc:532-539
  *   orbg_search_by_bow .............. ORBmatcher::SearchByBoW(KeyFrame*, Frame&, ...)
  *                                     src/ORBmatcher.cc:195-348 (Tracking.cc:1069, 2009)
+ *   orbg_undistort_keypoints ........ Frame::UndistortKeyPoints  src/Frame.cc:542-572
+ *   orbg_compute_image_bounds ....... Frame::ComputeImageBounds  src/Frame.cc:575-611
+ *   orbg_is_in_frustum .............. Frame::isInFrustum(pMP, viewingCosLimit)  src/Frame.cc:342-409
+ *                                     (Tracking::SearchLocalPoints, Tracking.cc:1676-1691)
+ *   orbg_distinctive_descriptor ..... MapPoint::ComputeDistinctiveDescriptors  src/MapPoint.cc:342-420
  *   orbg_ba_linearize ............... g2o computeActiveErrors + BlockSolver::buildSystem arithmetic
  *                                     for EdgeSE3ProjectXYZ / EdgeStereoSE3ProjectXYZ inside
  *                                     Optimizer::LocalBundleAdjustment  src/Optimizer.cc:633-979
@@ -364,6 +369,84 @@ typedef struct {
 } orbg_track_batch;
 int orbg_search_by_projection_batch_device(orbg_ctx *ctx, int mode, const orbg_track_batch *tb,
                                            int nframes);
+
+/* ---------------- Frame / MapPoint geometry ---------------- */
+/* Frame::mK (fx, fy, cx, cy) and Frame::mDistCoef (k1, k2, p1, p2[, k3]: k3 = 0 when the
+ * settings file has none, Tracking.cc's DistCoef of 4 entries) */
+typedef struct {
+    float fx, fy, cx, cy;
+    float k1, k2, p1, p2, k3;
+} orbg_camera;
+
+/* Frame::UndistortKeyPoints (src/Frame.cc:542-572): kps_un[i] = kps[i] with pt replaced by
+ * cv::undistortPoints(pt, K, D, noArray(), K) (OpenCV 3.4: 5 fixed-point iterations in
+ * double); k1 == 0: a copy (mvKeysUn = mvKeys).  Host arrays; kps_un may alias
+ * kps. */
+int orbg_undistort_keypoints(orbg_ctx *ctx, const orbg_camera *cam, const orbg_keypoint *kps,
+                             int n, orbg_keypoint *kps_un);
+/* The same on the device for a batch: frame f's counts[f] keypoints at d_kps + f * frame_cap
+ * -> d_kps_un + f * frame_cap (entries past counts[f] untouched).  Context stream. */
+int orbg_undistort_batch_device(orbg_ctx *ctx, const orbg_camera *cam, const orbg_keypoint *d_kps,
+                                const int32_t *d_counts, int frame_cap, int nframes,
+                                orbg_keypoint *d_kps_un);
+/* Frame::ComputeImageBounds (src/Frame.cc:575-611) for a w x h image: mnMinX .. mnMaxY (the
+ * undistorted image corners when k1 != 0, else 0, w, 0, h).  Host only (four points, the
+ * expression k_undistort evaluates). */
+int orbg_compute_image_bounds(const orbg_camera *cam, int w, int h, orbg_bounds *out);
+/* Batched-sequence mode with a distorted camera (TUM / EuRoC settings): after
+ * orbg_set_camera(ctx, cam) with cam->k1 != 0, orbg_match_batch_device first undistorts the
+ * batch's keypoints on the match stream (Frame::UndistortKeyPoints, as the Frame constructor
+ * does after ExtractORB, Frame.cc:259) and SearchForInitialization (and the pose stub)
+ * read mvKeysUn with ComputeImageBounds' bounds; orbg_batch_keys_un returns the device array
+ * ([frames][frame_cap], valid after that match stream work).  cam == NULL or k1 == 0: the
+ * default (mvKeysUn = mvKeys, bounds 0, w, 0, h). */
+int orbg_set_camera(orbg_ctx *ctx, const orbg_camera *cam);
+int orbg_batch_keys_un(orbg_ctx *ctx, orbg_keypoint **d_kps_un, int32_t *frame_cap);
+
+/* What Frame::isInFrustum reads of a MapPoint: GetWorldPos(), GetNormal(), mfMinDistance,
+ * mfMaxDistance; flags: ORBG_MP_VALID = Tracking::SearchLocalPoints tests the point
+ * (!isBad() && mnLastFrameSeen != CurrentFrame.mnId, Tracking.cc:1680-1683), ORBG_MP_HAS_OBS
+ * passed through to the projection. */
+typedef struct {
+    float x, y, z;
+    float nx, ny, nz;
+    float min_dist, max_dist;
+    int32_t flags;
+} orbg_map_point;
+/* The Frame state isInFrustum reads: mTcw rows 0..2 (row-major 3x4), fx, fy, cx, cy, mbf,
+ * mfLogScaleFactor (= log(mfScaleFactor), in double then float), mnScaleLevels, mnMinX.. */
+typedef struct {
+    float Tcw[12];
+    float fx, fy, cx, cy, bf;
+    float log_scale_factor;
+    int32_t nlevels;
+    orbg_bounds bounds;
+} orbg_frustum_camera;
+/* Frame::isInFrustum(pMP, viewing_cos_limit) for n map points (host arrays): proj[i] = the
+ * mTrack* members SearchByProjection(F, vpMapPoints) reads (orbg_map_projection:
+ * mTrackProjX/Y/XR, mnTrackScaleLevel, mTrackViewCos; flags ORBG_MP_VALID = mbTrackInView,
+ * ORBG_MP_HAS_OBS passed through).  A point not in view gets only its flags written (the
+ * reference leaves the other members as they were).  *nvisible = points in view. */
+int orbg_is_in_frustum(orbg_ctx *ctx, const orbg_frustum_camera *cam, const orbg_map_point *mps,
+                       int n, float viewing_cos_limit, orbg_map_projection *proj, int *nvisible);
+/* Batched, device memory: frame f's counts[f] points at d_mps + f * cap, camera d_cams[f],
+ * projections at d_proj + f * cap, d_nvisible[f].  Context stream. */
+int orbg_is_in_frustum_batch_device(orbg_ctx *ctx, const orbg_frustum_camera *d_cams,
+                                    const orbg_map_point *d_mps, const int32_t *d_counts, int cap,
+                                    int nframes, float viewing_cos_limit,
+                                    orbg_map_projection *d_proj, int32_t *d_nvisible);
+/* MapPoint::ComputeDistinctiveDescriptors (src/MapPoint.cc:342-420) for one map point: the n
+ * observation descriptors (n x 32 bytes, in the mObservations order, bad KeyFrames left out)
+ * -> *best = BestIdx, the row with the least median distance to the others (the first on
+ * ties), -1 if n == 0. */
+int orbg_distinctive_descriptor(orbg_ctx *ctx, const uint8_t *desc, int n, int32_t *best);
+/* Batched, device memory: map point p's observations are descriptor rows
+ * d_pool[d_rows[d_off[p]] .. d_rows[d_off[p+1]-1]] (32 bytes each, e.g. the KeyFrames'
+ * mDescriptors resident in HBM); d_best[p] = BestIdx (-1: no observation) and, if d_desc is
+ * not NULL, d_desc[p * 32 ..] = that descriptor (mDescriptor).  Context stream. */
+int orbg_distinctive_descriptors_batch_device(orbg_ctx *ctx, const uint8_t *d_pool,
+                                              const int32_t *d_rows, const int32_t *d_off,
+                                              int npoints, int32_t *d_best, uint8_t *d_desc);
 
 /* ---------------- Optimizer::PoseOptimization ----------------
  * One edge per Frame keypoint with a MapPoint (index order): EdgeSE3ProjectXYZOnlyPose when

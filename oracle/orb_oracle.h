@@ -207,6 +207,51 @@ int orc_search_by_projection_local(const orc_keypoint *kps, const uint8_t *desc,
                                    const orc_map_proj *mps, const uint8_t *mdesc, int nm,
                                    float th, float nnratio, int32_t *match);
 
+/* ---- Frame / MapPoint geometry (frame_oracle.c) ---- */
+/* Frame::mK (fx, fy, cx, cy) and mDistCoef (k1, k2, p1, p2[, k3]; k3 = 0 when absent) */
+typedef struct {
+    float fx, fy, cx, cy;
+    float k1, k2, p1, p2, k3;
+} orc_camera;
+/* cv::undistortPoints(xy, out, K, D, noArray(), K) over n (x, y) pairs */
+void orc_undistort_points(const orc_camera *cam, const float *xy, int n, float *out);
+/* Frame::UndistortKeyPoints: mvKeysUn (k1 == 0: a copy) */
+void orc_undistort_keypoints(const orc_camera *cam, const orc_keypoint *kps, int n,
+                             orc_keypoint *out);
+/* Frame::ComputeImageBounds */
+void orc_image_bounds(const orc_camera *cam, int w, int h, orc_bounds *b);
+/* Frame::mfLogScaleFactor = log(mfScaleFactor) */
+float orc_log_scale_factor(float scale_factor);
+/* what Frame::isInFrustum reads of a MapPoint; flags: ORC_MP_VALID = SearchLocalPoints
+ * tests it (!isBad() && mnLastFrameSeen != frame), ORC_MP_HAS_OBS passed through */
+typedef struct {
+    float x, y, z;            /* GetWorldPos() */
+    float nx, ny, nz;         /* GetNormal() */
+    float min_dist, max_dist; /* mfMinDistance, mfMaxDistance */
+    int32_t flags;
+} orc_map_point;
+/* the Frame state isInFrustum reads: mTcw (3x4 row-major), fx.., mbf, mfLogScaleFactor,
+ * mnScaleLevels, mnMinX.. */
+typedef struct {
+    float Tcw[12];
+    float fx, fy, cx, cy, bf;
+    float log_scale_factor;
+    int32_t nlevels;
+    orc_bounds bounds;
+} orc_frustum_cam;
+/* Frame::isInFrustum(pMP, viewingCosLimit): out = the mTrack* members + flags (VALID =
+ * mbTrackInView); returns mbTrackInView */
+int orc_is_in_frustum(const orc_frustum_cam *cam, const orc_map_point *mp,
+                      float viewing_cos_limit, orc_map_proj *out);
+/* MapPoint::ComputeDistinctiveDescriptors over n observation descriptors: BestIdx (-1 if n
+ * is 0) */
+int orc_distinctive_descriptor(const uint8_t *desc, int n);
+/* loops over n points / npoints map points (observations pool[rows[off[p]..off[p+1])]) */
+int orc_is_in_frustum_n(const orc_frustum_cam *cam, const orc_map_point *mps, int n,
+                        float viewing_cos_limit, orc_map_proj *out);
+void orc_distinctive_descriptors_n(const uint8_t *pool, const int32_t *rows, const int32_t *off,
+                                   int npoints, int32_t *best);
+
 /* ---- Optimizer::PoseOptimization (pose_oracle.c) ---- */
 /* LM's pow(2 rho - 1, 3) as the once-rounded exact cube (optimization_algorithm_levenberg.cpp:135) */
 double orc_lm_cube(double t);

@@ -40,6 +40,19 @@ MP_DTYPE = np.dtype([("u", "<f4"), ("v", "<f4"), ("ur", "<f4"), ("level", "<i4")
                      ("view_cos", "<f4"), ("flags", "<i4")])
 
 
+# Frame / MapPoint geometry records (orb_oracle.h: orc_camera, orc_map_point, orc_frustum_cam)
+CAMERA_DTYPE = np.dtype([("fx", "<f4"), ("fy", "<f4"), ("cx", "<f4"), ("cy", "<f4"),
+                         ("k1", "<f4"), ("k2", "<f4"), ("p1", "<f4"), ("p2", "<f4"),
+                         ("k3", "<f4")])
+MAPPOINT_DTYPE = np.dtype([("x", "<f4"), ("y", "<f4"), ("z", "<f4"), ("nx", "<f4"),
+                           ("ny", "<f4"), ("nz", "<f4"), ("min_dist", "<f4"),
+                           ("max_dist", "<f4"), ("flags", "<i4")])
+FRUSTUM_DTYPE = np.dtype([("Tcw", "<f4", 12), ("fx", "<f4"), ("fy", "<f4"), ("cx", "<f4"),
+                          ("cy", "<f4"), ("bf", "<f4"), ("log_scale_factor", "<f4"),
+                          ("nlevels", "<i4"), ("min_x", "<f4"), ("max_x", "<f4"),
+                          ("min_y", "<f4"), ("max_y", "<f4")])
+
+
 class Params(C.Structure):
     _fields_ = [("nfeatures", C.c_int32), ("scale_factor", C.c_float), ("nlevels", C.c_int32),
                 ("ini_th_fast", C.c_int32), ("min_th_fast", C.c_int32),
@@ -168,6 +181,16 @@ def lib():
         L.orc_search_by_bow.restype = C.c_int
         L.orc_search_by_bow.argtypes = [vp, vp, vp, C.c_int, vp, vp, vp, C.c_int, vp, vp, C.c_int,
                                         vp, vp, vp, C.c_int, C.c_float, C.c_int, vp]
+        L.orc_undistort_points.argtypes = [vp, vp, C.c_int, vp]
+        L.orc_undistort_keypoints.argtypes = [vp, vp, C.c_int, vp]
+        L.orc_image_bounds.argtypes = [vp, C.c_int, C.c_int, P(Bounds)]
+        L.orc_log_scale_factor.argtypes = [C.c_float]
+        L.orc_log_scale_factor.restype = C.c_float
+        L.orc_is_in_frustum_n.argtypes = [vp, vp, C.c_int, C.c_float, vp]
+        L.orc_is_in_frustum_n.restype = C.c_int
+        L.orc_distinctive_descriptor.argtypes = [vp, C.c_int]
+        L.orc_distinctive_descriptor.restype = C.c_int
+        L.orc_distinctive_descriptors_n.argtypes = [vp, vp, vp, C.c_int, vp]
         _lib = L
     return _lib
 
@@ -573,3 +596,66 @@ def search_by_bow(kf_desc, kf_angle, kf_valid, kf_fv, f_desc, f_angle, f_fv, nnr
                                 _p(fd), _p(fa), len(fd), _p(fn), _p(fo), _p(ffe), len(fn),
                                 float(nnratio), int(bool(check_ori)), _p(match))
     return n, match[:len(fd)].copy()
+
+
+# ---- Frame / MapPoint geometry (frame_oracle.c) ----
+def camera(fx, fy, cx, cy, k1=0.0, k2=0.0, p1=0.0, p2=0.0, k3=0.0):
+    c = np.zeros((), CAMERA_DTYPE)
+    for k, v in zip(CAMERA_DTYPE.names, (fx, fy, cx, cy, k1, k2, p1, p2, k3)):
+        c[k] = v
+    return c
+
+
+def undistort_points(cam, xy):
+    """cv::undistortPoints(xy, K, D, noArray(), K): xy (n, 2) float32."""
+    cam = np.ascontiguousarray(cam, CAMERA_DTYPE)
+    xy = np.ascontiguousarray(xy, np.float32).reshape(-1, 2)
+    out = np.zeros_like(xy)
+    lib().orc_undistort_points(_p(cam), _p(xy), len(xy), _p(out))
+    return out
+
+
+def undistort_keypoints(cam, kps):
+    """Frame::UndistortKeyPoints: mvKeysUn."""
+    cam = np.ascontiguousarray(cam, CAMERA_DTYPE)
+    kps = np.ascontiguousarray(kps, KP_DTYPE)
+    out = np.zeros_like(kps)
+    lib().orc_undistort_keypoints(_p(cam), _p(kps), len(kps), _p(out))
+    return out
+
+
+def image_bounds(cam, w, h):
+    """Frame::ComputeImageBounds: (min_x, max_x, min_y, max_y)."""
+    cam = np.ascontiguousarray(cam, CAMERA_DTYPE)
+    b = Bounds()
+    lib().orc_image_bounds(_p(cam), int(w), int(h), C.byref(b))
+    return (b.min_x, b.max_x, b.min_y, b.max_y)
+
+
+def log_scale_factor(sf):
+    return lib().orc_log_scale_factor(float(sf))
+
+
+def is_in_frustum(fcam, mps, viewing_cos_limit=0.5, proj=None):
+    """Frame::isInFrustum over map points: (MP_DTYPE projections, number in view).  proj:
+    the records' values before the call (only the flags of a point out of view change)."""
+    fcam = np.ascontiguousarray(fcam, FRUSTUM_DTYPE)
+    mps = np.ascontiguousarray(mps, MAPPOINT_DTYPE)
+    out = np.zeros(len(mps), MP_DTYPE) if proj is None else np.array(proj, MP_DTYPE)
+    n = lib().orc_is_in_frustum_n(_p(fcam), _p(mps), len(mps), float(viewing_cos_limit), _p(out))
+    return out, n
+
+
+def distinctive_descriptor(desc):
+    """MapPoint::ComputeDistinctiveDescriptors over one point's observation rows: BestIdx."""
+    desc = np.ascontiguousarray(desc, np.uint8).reshape(-1, 32)
+    return lib().orc_distinctive_descriptor(_p(desc), len(desc))
+
+
+def distinctive_descriptors(pool, rows, off):
+    pool = np.ascontiguousarray(pool, np.uint8).reshape(-1, 32)
+    rows = np.ascontiguousarray(rows, np.int32)
+    off = np.ascontiguousarray(off, np.int32)
+    best = np.zeros(len(off) - 1, np.int32)
+    lib().orc_distinctive_descriptors_n(_p(pool), _p(rows), _p(off), len(off) - 1, _p(best))
+    return best

@@ -46,6 +46,19 @@ MP_DTYPE = np.dtype([("u", "<f4"), ("v", "<f4"), ("ur", "<f4"), ("level", "<i4")
                      ("view_cos", "<f4"), ("flags", "<i4")])
 
 
+# Frame / MapPoint geometry records (orbg_camera, orbg_map_point, orbg_frustum_camera)
+CAMERA_DTYPE = np.dtype([("fx", "<f4"), ("fy", "<f4"), ("cx", "<f4"), ("cy", "<f4"),
+                         ("k1", "<f4"), ("k2", "<f4"), ("p1", "<f4"), ("p2", "<f4"),
+                         ("k3", "<f4")])
+MAPPOINT_DTYPE = np.dtype([("x", "<f4"), ("y", "<f4"), ("z", "<f4"), ("nx", "<f4"),
+                           ("ny", "<f4"), ("nz", "<f4"), ("min_dist", "<f4"),
+                           ("max_dist", "<f4"), ("flags", "<i4")])
+FRUSTUM_DTYPE = np.dtype([("Tcw", "<f4", 12), ("fx", "<f4"), ("fy", "<f4"), ("cx", "<f4"),
+                          ("cy", "<f4"), ("bf", "<f4"), ("log_scale_factor", "<f4"),
+                          ("nlevels", "<i4"), ("min_x", "<f4"), ("max_x", "<f4"),
+                          ("min_y", "<f4"), ("max_y", "<f4")])
+
+
 PEDGE_DTYPE = np.dtype([("obs", "<f4", 3), ("xw", "<f4", 3), ("inv_sigma2", "<f4"),
                         ("stereo", "<i4")])
 
@@ -207,6 +220,15 @@ def lib():
         "orbg_ba_graph_set_active": (i32, [vp, vp, vp]),
         "orbg_ba_graph_build_system": (i32, [vp, vp, vp, vp, vp, vp, vp, vp, vp]),
         "orbg_ba_graph_errors": (i32, [vp, vp, vp, vp, vp, vp, vp, vp]),
+        "orbg_undistort_keypoints": (i32, [vp, vp, vp, i32, vp]),
+        "orbg_undistort_batch_device": (i32, [vp, vp, vp, vp, i32, i32, vp]),
+        "orbg_compute_image_bounds": (i32, [vp, i32, i32, P(Bounds)]),
+        "orbg_set_camera": (i32, [vp, vp]),
+        "orbg_batch_keys_un": (i32, [vp, P(vp), P(C.c_int32)]),
+        "orbg_is_in_frustum": (i32, [vp, vp, vp, i32, f32, vp, P(i32)]),
+        "orbg_is_in_frustum_batch_device": (i32, [vp, vp, vp, vp, i32, i32, f32, vp, vp]),
+        "orbg_distinctive_descriptor": (i32, [vp, vp, i32, P(C.c_int32)]),
+        "orbg_distinctive_descriptors_batch_device": (i32, [vp, vp, vp, vp, i32, vp, vp]),
     }
     for name, (res, args) in sig.items():
         if os.environ.get("ORBG_LIB_VARIANT") and not hasattr(L, name):

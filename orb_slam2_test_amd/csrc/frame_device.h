@@ -1,0 +1,45 @@
+// frame_device.h -- cv::undistortPoints(src, dst, K, D, noArray(), K) for one point, shared by
+// k_undistort (frame_kernels.hip) and the host-side Frame::ComputeImageBounds (orbg_api.hip)
+// so both run the same expression tree.  OpenCV 3.4's cvUndistortPointsInternal
+// (modules/imgproc/src/undistort.cpp) with the default criteria TermCriteria(COUNT, 5, 0.01):
+// five fixed-point iterations in double, no EPS test; K, D converted from CV_32F to double;
+// identity tilt (x0 = x), zero rational / thin-prism terms kept in the library's order;
+// RR = K * I = K, so u = fx*x + 0*y + cx, v = 0*x + fy*y + cy, w = 1 / (0*x + 0*y + 1); the
+// result rounded to float.  No FMA contraction (fp contract off here and -ffp-contract=off).
+#pragma once
+
+#pragma clang fp contract(off)
+
+#include <hip/hip_runtime.h>
+
+#include "../../include/orbg.h"
+
+namespace orbg {
+
+__host__ __device__ inline void undistort_point(const orbg_camera &c, float uf, float vf,
+                                                float *xo, float *yo)
+{
+    const double fx = c.fx, fy = c.fy, cx = c.cx, cy = c.cy;
+    const double ifx = 1. / fx, ify = 1. / fy;
+    const double k0 = c.k1, k1 = c.k2, k2 = c.p1, k3 = c.p2, k4 = c.k3;
+    const double z = 0.0;  // k[5..11]: rational and thin-prism coefficients (absent)
+    double x = uf, y = vf;
+    x = (x - cx) * ifx;
+    y = (y - cy) * ify;
+    const double x0 = x, y0 = y;
+    for (int j = 0; j < 5; j++) {
+        const double r2 = x * x + y * y;
+        const double icdist = (1 + ((z * r2 + z) * r2 + z) * r2) / (1 + ((k4 * r2 + k1) * r2 + k0) * r2);
+        const double deltaX = 2 * k2 * x * y + k3 * (r2 + 2 * x * x) + z * r2 + z * r2 * r2;
+        const double deltaY = k2 * (r2 + 2 * y * y) + 2 * k3 * x * y + z * r2 + z * r2 * r2;
+        x = (x0 - deltaX) * icdist;
+        y = (y0 - deltaY) * icdist;
+    }
+    const double xx = fx * x + 0.0 * y + cx;
+    const double yy = 0.0 * x + fy * y + cy;
+    const double ww = 1. / (0.0 * x + 0.0 * y + 1.0);
+    *xo = (float)(xx * ww);
+    *yo = (float)(yy * ww);
+}
+
+}  // namespace orbg

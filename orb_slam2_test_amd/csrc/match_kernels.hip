@@ -396,7 +396,7 @@ __global__ __launch_bounds__(256) void k_init_cands_single(
 // batch: F1 = frame f1[p] (its keypoints are vbPrevMatched), F2 = frame f2[p]
 __global__ __launch_bounds__(256) void k_init_cands_pairs(
     const orbg_keypoint *kps, const uint8_t *desc, const int32_t *counts, int fc,
-    const int32_t *f1, const int32_t *f2, int w, int h, int window, unsigned long long *topk,
+    const int32_t *f1, const int32_t *f2, orbg_bounds b, int window, unsigned long long *topk,
     int32_t *topn, int cap)
 {
     // queries are level-0 keypoints: indices below the level-0 capacity
@@ -415,7 +415,6 @@ __global__ __launch_bounds__(256) void k_init_cands_pairs(
             topn[(size_t)p * fc + i] = -1;
         return;
     }
-    orbg_bounds b{0.f, (float)w, 0.f, (float)h};
     // vbPrevMatched = F1.mvKeysUn[i].pt: read x, y straight out of the keypoint records
     init_cands_block(k1, desc + (size_t)a * fc * 32, n1, kps + (size_t)c * fc,
                      desc + (size_t)c * fc * 32, n2, b, (const float *)k1,
@@ -774,7 +773,7 @@ __global__ __launch_bounds__(RESOLVE_T) void k_init_resolve_single(
 
 __global__ __launch_bounds__(RESOLVE_T) void k_init_resolve_pairs(
     const orbg_keypoint *kps, const uint8_t *desc, const int32_t *counts, int fc,
-    const int32_t *f1, const int32_t *f2, int w, int h, int window, float nnratio,
+    const int32_t *f1, const int32_t *f2, orbg_bounds b, int window, float nnratio,
     int check_ori, const unsigned long long *topk, const int32_t *topn, int32_t *m12,
     int32_t *nm, int cap)
 {
@@ -783,7 +782,6 @@ __global__ __launch_bounds__(RESOLVE_T) void k_init_resolve_pairs(
     const int p = blockIdx.x;
     const int a = f1[p], c = f2[p];
     const orbg_keypoint *k1 = kps + (size_t)a * fc;
-    orbg_bounds b{0.f, (float)w, 0.f, (float)h};
     init_resolve_block(S, cap, k1, desc + (size_t)a * fc * 32, counts[a], kps + (size_t)c * fc,
                       desc + (size_t)c * fc * 32, counts[c], b, (const float *)k1,
                       (int)(sizeof(orbg_keypoint) / sizeof(float)), window, nnratio, check_ori,
@@ -840,7 +838,7 @@ int launch_knn2(hipStream_t st, const uint8_t *q, int nq, const uint8_t *t, int 
 int launch_match_pairs(hipStream_t st, hipStream_t aux, hipEvent_t evf, hipEvent_t evj,
                        const uint8_t *desc, const orbg_keypoint *kps,
                        const int32_t *counts, int fc, const int32_t *d_f1, const int32_t *d_f2,
-                       int npairs, int w, int h, int window, float nnratio, int check_ori,
+                       int npairs, orbg_bounds b, int window, float nnratio, int check_ori,
                        int32_t *knn, int32_t *m12, int32_t *nm, uint32_t *topk, int32_t *topk_n,
                        void *prof, int serial, int cap0)
 {
@@ -849,7 +847,7 @@ int launch_match_pairs(hipStream_t st, hipStream_t aux, hipEvent_t evf, hipEvent
     PL(prof, st, "init_cands",
        hipLaunchKernelGGL(k_init_cands_pairs, dim3((cap0 + 4 * INIT_QPW - 1) / (4 * INIT_QPW) * npairs),
                           dim3(256), 2 * cap0 * sizeof(F2Key), st, kps, desc, counts, fc, d_f1, d_f2,
-                          w, h, window, (unsigned long long *)topk, topk_n, cap0));
+                          b, window, (unsigned long long *)topk, topk_n, cap0));
     // knn2 (VALU bound) on `aux` beside init_resolve (one sequential workgroup per pair);
     // serial == 1 (orbg_set_serial: isolated kernel timing) keeps it on `st`
     if (serial) aux = st;
@@ -862,7 +860,7 @@ int launch_match_pairs(hipStream_t st, hipStream_t aux, hipEvent_t evf, hipEvent
     if (hipEventRecord(evj, aux) != hipSuccess) return ORBG_EIO;
     PL(prof, st, "init_resolve",
        hipLaunchKernelGGL(k_init_resolve_pairs, dim3(npairs), dim3(RESOLVE_T),
-                          resolve_lds_bytes(cap0), st, kps, desc, counts, fc, d_f1, d_f2, w, h,
+                          resolve_lds_bytes(cap0), st, kps, desc, counts, fc, d_f1, d_f2, b,
                           window, nnratio, check_ori, (const unsigned long long *)topk, topk_n,
                           m12, nm, cap0));
     if (hipStreamWaitEvent(st, evj, 0) != hipSuccess) return ORBG_EIO;

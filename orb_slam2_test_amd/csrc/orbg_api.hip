@@ -23,6 +23,7 @@
 #include "schur_args.h"
 #include "bow_args.h"
 #include "pyramid_args.h"
+#include "frame_device.h"
 
 #pragma clang fp contract(off)
 
@@ -67,9 +68,16 @@ hipError_t launch_orient_desc(bool bfma, dim3 grid, hipStream_t st, const OrbgGe
 int launch_match_pairs(hipStream_t st, hipStream_t aux, hipEvent_t evf, hipEvent_t evj,
                        const uint8_t *desc, const orbg_keypoint *kps,
                        const int32_t *counts, int frame_cap, const int32_t *d_f1,
-                       const int32_t *d_f2, int npairs, int w, int h, int window, float nnratio,
+                       const int32_t *d_f2, int npairs, orbg_bounds b, int window, float nnratio,
                        int check_ori, int32_t *knn, int32_t *m12, int32_t *nm, uint32_t *topk,
                        int32_t *topk_n, void *prof, int serial, int cap0);
+int launch_undistort(hipStream_t st, const orbg_camera &cam, const orbg_keypoint *kps,
+                     const int32_t *counts, int fc, int nframes, orbg_keypoint *out);
+int launch_frustum(hipStream_t st, const orbg_frustum_camera *cams, const orbg_map_point *mps,
+                   const int32_t *counts, int cap, int nframes, float cos_limit,
+                   orbg_map_projection *out, int32_t *nvisible);
+int launch_distinctive(hipStream_t st, const uint8_t *pool, const int32_t *rows,
+                       const int32_t *off, int npoints, int32_t *best, uint8_t *desc_out);
 int launch_pose_opt(hipStream_t st, const orbg_pose_edge *edges, const int32_t *counts, int cap,
                     const orbg_pose_camera *cams, const float *tcw_in, double *q_out,
                     double *t_out, float *tcw_out, uint8_t *outlier, int32_t *ninliers,
@@ -400,6 +408,13 @@ struct orbg_ctx {
     // batched-sequence pose stub (orbg_match_pose_batch_device): edges, counts, cameras, poses
     void *d_mpose = nullptr;
     size_t mpose_bytes = 0;
+    // orbg_set_camera: distorted camera of the batched-sequence mode (has_cam: k1 != 0);
+    // the batch matching undistorts into d_kps_un ([kps_un_frames][frame_cap], match stream)
+    bool has_cam = false;
+    orbg_camera cam{};
+    orbg_keypoint *d_kps_un = nullptr;
+    size_t kps_un_n = 0;
+    bool kps_un_valid = false;
     Prof prof;
 };
 
@@ -1364,6 +1379,7 @@ extern "C" void orbg_destroy(orbg_ctx *c)
     if (c->d_scr) hipFree(c->d_scr);
     if (c->d_trk) hipFree(c->d_trk);
     if (c->d_mpose) hipFree(c->d_mpose);
+    if (c->d_kps_un) hipFree(c->d_kps_un);
     if (c->aux_stream) hipStreamSynchronize(c->aux_stream);
     if (c->ostream) hipStreamSynchronize(c->ostream);
     if (c->mstream) hipStreamSynchronize(c->mstream);
@@ -2167,9 +2183,35 @@ extern "C" int orbg_match_batch_device(orbg_ctx *c, const int32_t *f1, const int
     }
     const int s = c->slot;
     HIPCHK(hipStreamWaitEvent(c->mstream, c->ev_ext[s], 0));
+    // mvKeysUn and the image bounds (Frame.cc:259, 575-611): the keypoints themselves and
+    // (0, w, 0, h) unless orbg_set_camera gave a distorted camera
+    const orbg_keypoint *kun = c->d_kps;
+    orbg_bounds b{0.f, (float)c->geom.w, 0.f, (float)c->geom.h};
+    c->kps_un_valid = false;
+    if (c->has_cam) {
+        const size_t need = (size_t)c->last_n * fc;
+        if (c->kps_un_n < need) {
+            HIPCHK(hipStreamSynchronize(c->mstream));  // an earlier match may still read it
+            if (c->d_kps_un) hipFree(c->d_kps_un);
+            c->d_kps_un = nullptr;
+            c->kps_un_n = 0;
+            int ra = dalloc(&c->d_kps_un, need);
+            if (ra) return ra;
+            c->kps_un_n = need;
+        }
+        int ru = 0;
+        hipStream_t st = c->mstream;  // PROF_LAUNCH records on `st`
+        PROF_LAUNCH(c, "undistort",
+                    ru = launch_undistort(st, c->cam, c->d_kps, c->d_counts, (int)fc, c->last_n,
+                                          c->d_kps_un));
+        if (ru) return set_err(ORBG_EIO, "k_undistort launch failed");
+        kun = c->d_kps_un;
+        orbg_compute_image_bounds(&c->cam, c->geom.w, c->geom.h, &b);
+        c->kps_un_valid = true;
+    }
     int rc = launch_match_pairs(c->mstream, c->aux_stream, c->ev_fork[1], c->ev_join[1],
-                                c->d_desc, c->d_kps, c->d_counts, (int)fc, c->d_pairs,
-                                c->d_pairs + c->pair_cap, npairs, c->geom.w, c->geom.h, window,
+                                c->d_desc, kun, c->d_counts, (int)fc, c->d_pairs,
+                                c->d_pairs + c->pair_cap, npairs, b, window,
                                 nnratio, check_ori, c->d_knn, c->d_m12, c->d_nm, c->d_topk,
                                 c->d_topk_n, &c->prof, c->serial || c->geom.dbg == 40,
                                 c->geom.lv[0].out_cap);
@@ -2219,8 +2261,8 @@ extern "C" int orbg_match_pose_batch_device(orbg_ctx *c, const orbg_pose_camera 
     HIPCHK(order_after_caller(c));  // d_q / d_t / d_ninliers are the caller's
     HIPCHK(hipStreamWaitEvent(c->mstream, c->ev_ext[s], 0));  // (the matching already does)
     const int rc = launch_match_pose(
-        c->mstream, c->d_kps, c->d_counts, (int)fc, c->d_pairs, c->d_pairs + c->pair_cap,
-        c->d_m12, P, *cam, depth, c->inv_sigma2, c->p.nlevels, (orbg_pose_edge *)(b + oe),
+        c->mstream, c->kps_un_valid ? c->d_kps_un : c->d_kps, c->d_counts, (int)fc, c->d_pairs,
+        c->d_pairs + c->pair_cap, c->d_m12, P, *cam, depth, c->inv_sigma2, c->p.nlevels, (orbg_pose_edge *)(b + oe),
         (int32_t *)(b + on), (orbg_pose_camera *)(b + oc), (float *)(b + ot0),
         (float *)(b + ot1), b + ool, d_q, d_t, d_ninliers, &c->prof);
     if (rc) return set_err(rc, "pose stub launch failed");
@@ -3753,5 +3795,228 @@ extern "C" int orbg_search_by_bow(orbg_ctx *c, const uint8_t *kf_desc, const flo
     HIPCHK(hipStreamSynchronize(c->stream));
     memcpy(match, hs + o_match, (size_t)n_f * 4);
     memcpy(nmatches, hs + o_nm, 4);
+    return ORBG_OK;
+}
+
+// ---------------------------------------------------------------------------
+// Frame / MapPoint geometry (frame_kernels.hip)
+// ---------------------------------------------------------------------------
+static bool cam_ok(const orbg_camera *cam)
+{
+    return cam && std::isfinite(cam->fx) && std::isfinite(cam->fy) && cam->fx != 0.f &&
+           cam->fy != 0.f;
+}
+
+extern "C" int orbg_compute_image_bounds(const orbg_camera *cam, int w, int h, orbg_bounds *out)
+{
+    if (!cam || !out) return set_err(ORBG_EINVAL, "NULL argument");
+    if (w < 0 || h < 0) return set_err(ORBG_EINVAL, "negative image size");
+    if (cam->k1 != 0.0f) {
+        if (!cam_ok(cam)) return set_err(ORBG_EINVAL, "fx / fy must be finite and nonzero");
+        // the corners (0,0), (cols,0), (0,rows), (cols,rows), Frame.cc:579-600
+        float o[8];
+        const float in[8] = {0.f, 0.f, (float)w, 0.f, 0.f, (float)h, (float)w, (float)h};
+        for (int i = 0; i < 4; i++) orbg::undistort_point(*cam, in[2 * i], in[2 * i + 1], &o[2 * i], &o[2 * i + 1]);
+        out->min_x = std::min(o[0], o[4]);
+        out->max_x = std::max(o[2], o[6]);
+        out->min_y = std::min(o[1], o[3]);
+        out->max_y = std::max(o[5], o[7]);
+    } else {
+        out->min_x = 0.0f;
+        out->max_x = (float)w;
+        out->min_y = 0.0f;
+        out->max_y = (float)h;
+    }
+    return ORBG_OK;
+}
+
+extern "C" int orbg_set_camera(orbg_ctx *c, const orbg_camera *cam)
+{
+    if (!c) return set_err(ORBG_EINVAL, "NULL context");
+    if (cam && cam->k1 != 0.0f && !cam_ok(cam))
+        return set_err(ORBG_EINVAL, "fx / fy must be finite and nonzero");
+    c->has_cam = cam && cam->k1 != 0.0f;
+    if (cam) c->cam = *cam;
+    return ORBG_OK;
+}
+
+extern "C" int orbg_batch_keys_un(orbg_ctx *c, orbg_keypoint **d_kps_un, int32_t *frame_cap)
+{
+    if (!c || !d_kps_un) return set_err(ORBG_EINVAL, "NULL argument");
+    if (!c->gw || c->last_n <= 0) return set_err(ORBG_EINVAL, "no batch extracted");
+    *d_kps_un = c->kps_un_valid ? c->d_kps_un : c->d_kps;
+    if (frame_cap) *frame_cap = c->geom.frame_cap;
+    return ORBG_OK;
+}
+
+extern "C" int orbg_undistort_batch_device(orbg_ctx *c, const orbg_camera *cam,
+                                           const orbg_keypoint *d_kps, const int32_t *d_counts,
+                                           int frame_cap, int nframes, orbg_keypoint *d_kps_un)
+{
+    if (!c || !cam) return set_err(ORBG_EINVAL, "NULL argument");
+    if (nframes < 0 || frame_cap < 0) return set_err(ORBG_EINVAL, "negative size");
+    if (nframes == 0 || frame_cap == 0) return ORBG_OK;
+    if (!d_kps || !d_counts || !d_kps_un) return set_err(ORBG_EINVAL, "NULL device array");
+    if (cam->k1 != 0.0f && !cam_ok(cam)) return set_err(ORBG_EINVAL, "fx / fy must be finite and nonzero");
+    HIPCHK(hipSetDevice(c->device));
+    hipStream_t st = c->stream;
+    int rc = 0;
+    PROF_LAUNCH(c, "undistort",
+                rc = launch_undistort(st, *cam, d_kps, d_counts, frame_cap, nframes, d_kps_un));
+    if (rc) return set_err(ORBG_EIO, "k_undistort launch failed");
+    return ORBG_OK;
+}
+
+extern "C" int orbg_undistort_keypoints(orbg_ctx *c, const orbg_camera *cam,
+                                        const orbg_keypoint *kps, int n, orbg_keypoint *kps_un)
+{
+    if (!c || !cam) return set_err(ORBG_EINVAL, "NULL argument");
+    if (n < 0) return set_err(ORBG_EINVAL, "negative size");
+    if (n == 0) return ORBG_OK;
+    if (!kps || !kps_un) return set_err(ORBG_EINVAL, "NULL array");
+    if (cam->k1 != 0.0f && !cam_ok(cam)) return set_err(ORBG_EINVAL, "fx / fy must be finite and nonzero");
+    HIPCHK(hipSetDevice(c->device));
+    const size_t kb = al256((size_t)n * sizeof(orbg_keypoint));
+    uint8_t *hs;
+    int rc = stage(c, 2 * kb, &hs);
+    if (rc) return rc;
+    void *d;
+    if ((rc = scratch(c, 2 * kb + 256, &d))) return rc;
+    uint8_t *db = (uint8_t *)d;
+    HIPCHK(hipStreamSynchronize(c->stream));  // the staging buffer may still feed a copy
+    memcpy(hs, kps, (size_t)n * sizeof(orbg_keypoint));
+    const int32_t cnt = n;
+    memcpy(hs + kb, &cnt, 4);
+    HIPCHK(hipMemcpyAsync(db, hs, kb + 4, hipMemcpyHostToDevice, c->stream));
+    rc = launch_undistort(c->stream, *cam, (const orbg_keypoint *)db, (const int32_t *)(db + kb),
+                          n, 1, (orbg_keypoint *)(db + kb + 256));
+    if (rc) return set_err(ORBG_EIO, "k_undistort launch failed");
+    HIPCHK(hipMemcpyAsync(hs, db + kb + 256, (size_t)n * sizeof(orbg_keypoint),
+                          hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(hipStreamSynchronize(c->stream));
+    memcpy(kps_un, hs, (size_t)n * sizeof(orbg_keypoint));
+    return ORBG_OK;
+}
+
+extern "C" int orbg_is_in_frustum_batch_device(orbg_ctx *c, const orbg_frustum_camera *d_cams,
+                                               const orbg_map_point *d_mps,
+                                               const int32_t *d_counts, int cap, int nframes,
+                                               float viewing_cos_limit,
+                                               orbg_map_projection *d_proj, int32_t *d_nvisible)
+{
+    if (!c) return set_err(ORBG_EINVAL, "NULL context");
+    if (nframes < 0 || cap < 0) return set_err(ORBG_EINVAL, "negative size");
+    if (nframes == 0 || cap == 0) return ORBG_OK;
+    if (!d_cams || !d_mps || !d_counts || !d_proj || !d_nvisible)
+        return set_err(ORBG_EINVAL, "NULL device array");
+    HIPCHK(hipSetDevice(c->device));
+    hipStream_t st = c->stream;
+    int rc = 0;
+    PROF_LAUNCH(c, "frustum",
+                rc = launch_frustum(st, d_cams, d_mps, d_counts, cap, nframes, viewing_cos_limit,
+                                    d_proj, d_nvisible));
+    if (rc) return set_err(ORBG_EIO, "k_frustum launch failed");
+    return ORBG_OK;
+}
+
+extern "C" int orbg_is_in_frustum(orbg_ctx *c, const orbg_frustum_camera *cam,
+                                  const orbg_map_point *mps, int n, float viewing_cos_limit,
+                                  orbg_map_projection *proj, int *nvisible)
+{
+    if (!c || !cam || !nvisible) return set_err(ORBG_EINVAL, "NULL argument");
+    if (n < 0) return set_err(ORBG_EINVAL, "negative size");
+    *nvisible = 0;
+    if (n == 0) return ORBG_OK;
+    if (!mps || !proj) return set_err(ORBG_EINVAL, "NULL array");
+    HIPCHK(hipSetDevice(c->device));
+    size_t o = 0;
+    auto take = [&](size_t bytes) {
+        const size_t r = o;
+        o += al256(bytes);
+        return r;
+    };
+    const size_t o_cam = take(sizeof(orbg_frustum_camera)), o_cnt = take(4),
+                 o_mp = take((size_t)n * sizeof(orbg_map_point)),
+                 o_pr = take((size_t)n * sizeof(orbg_map_projection)), o_nv = take(4);
+    uint8_t *hs;
+    int rc = stage(c, o, &hs);
+    if (rc) return rc;
+    void *d;
+    if ((rc = scratch(c, o, &d))) return rc;
+    uint8_t *db = (uint8_t *)d;
+    HIPCHK(hipStreamSynchronize(c->stream));
+    memcpy(hs + o_cam, cam, sizeof(orbg_frustum_camera));
+    const int32_t cnt = n;
+    memcpy(hs + o_cnt, &cnt, 4);
+    memcpy(hs + o_mp, mps, (size_t)n * sizeof(orbg_map_point));
+    // the projections a point not in view keeps (only its flags are written)
+    memcpy(hs + o_pr, proj, (size_t)n * sizeof(orbg_map_projection));
+    HIPCHK(hipMemcpyAsync(db, hs, o_nv, hipMemcpyHostToDevice, c->stream));
+    rc = launch_frustum(c->stream, (const orbg_frustum_camera *)(db + o_cam),
+                        (const orbg_map_point *)(db + o_mp), (const int32_t *)(db + o_cnt), n, 1,
+                        viewing_cos_limit, (orbg_map_projection *)(db + o_pr),
+                        (int32_t *)(db + o_nv));
+    if (rc) return set_err(ORBG_EIO, "k_frustum launch failed");
+    HIPCHK(hipMemcpyAsync(hs + o_pr, db + o_pr, o - o_pr, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(hipStreamSynchronize(c->stream));
+    memcpy(proj, hs + o_pr, (size_t)n * sizeof(orbg_map_projection));
+    memcpy(nvisible, hs + o_nv, 4);
+    return ORBG_OK;
+}
+
+extern "C" int orbg_distinctive_descriptors_batch_device(orbg_ctx *c, const uint8_t *d_pool,
+                                                         const int32_t *d_rows,
+                                                         const int32_t *d_off, int npoints,
+                                                         int32_t *d_best, uint8_t *d_desc)
+{
+    if (!c) return set_err(ORBG_EINVAL, "NULL context");
+    if (npoints < 0) return set_err(ORBG_EINVAL, "negative size");
+    if (npoints == 0) return ORBG_OK;
+    if (!d_pool || !d_rows || !d_off || !d_best) return set_err(ORBG_EINVAL, "NULL device array");
+    HIPCHK(hipSetDevice(c->device));
+    hipStream_t st = c->stream;
+    int rc = 0;
+    PROF_LAUNCH(c, "distinctive",
+                rc = launch_distinctive(st, d_pool, d_rows, d_off, npoints, d_best, d_desc));
+    if (rc) return set_err(ORBG_EIO, "k_distinctive launch failed");
+    return ORBG_OK;
+}
+
+extern "C" int orbg_distinctive_descriptor(orbg_ctx *c, const uint8_t *desc, int n, int32_t *best)
+{
+    if (!c || !best) return set_err(ORBG_EINVAL, "NULL argument");
+    if (n < 0) return set_err(ORBG_EINVAL, "negative size");
+    *best = -1;
+    if (n == 0) return ORBG_OK;  // observations empty: the reference returns (MapPoint.cc:356)
+    if (!desc) return set_err(ORBG_EINVAL, "NULL array");
+    HIPCHK(hipSetDevice(c->device));
+    size_t o = 0;
+    auto take = [&](size_t bytes) {
+        const size_t r = o;
+        o += al256(bytes);
+        return r;
+    };
+    const size_t o_d = take((size_t)n * 32), o_r = take((size_t)n * 4), o_off = take(8),
+                 o_b = take(4);
+    uint8_t *hs;
+    int rc = stage(c, o, &hs);
+    if (rc) return rc;
+    void *d;
+    if ((rc = scratch(c, o, &d))) return rc;
+    uint8_t *db = (uint8_t *)d;
+    HIPCHK(hipStreamSynchronize(c->stream));
+    memcpy(hs + o_d, desc, (size_t)n * 32);
+    int32_t *hr = (int32_t *)(hs + o_r);
+    for (int i = 0; i < n; i++) hr[i] = i;
+    int32_t *ho = (int32_t *)(hs + o_off);
+    ho[0] = 0;
+    ho[1] = n;
+    HIPCHK(hipMemcpyAsync(db, hs, o_b, hipMemcpyHostToDevice, c->stream));
+    rc = launch_distinctive(c->stream, db + o_d, (const int32_t *)(db + o_r),
+                            (const int32_t *)(db + o_off), 1, (int32_t *)(db + o_b), nullptr);
+    if (rc) return set_err(ORBG_EIO, "k_distinctive launch failed");
+    HIPCHK(hipMemcpyAsync(hs + o_b, db + o_b, 4, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(hipStreamSynchronize(c->stream));
+    memcpy(best, hs + o_b, 4);
     return ORBG_OK;
 }

@@ -151,6 +151,22 @@ class ORBextractor:
                                             n.value, C.byref(n)), "orbg_download_frame")
         return kps[:n.value].copy(), desc[:n.value].copy()
 
+    def set_camera(self, cam):
+        """Distorted camera of the batched-sequence mode (orbg_set_camera): the batch
+        matching then reads mvKeysUn (Frame::UndistortKeyPoints on the device) with
+        ComputeImageBounds' bounds.  cam: frame.camera(...) record, or None for the default
+        (mvKeysUn = mvKeys, bounds = image)."""
+        c = None if cam is None else np.ascontiguousarray(cam, L.CAMERA_DTYPE)
+        L.check(L.lib().orbg_set_camera(self.ctx.handle, L.ptr(c)), "orbg_set_camera")
+
+    def batch_keys_un(self):
+        """device pointer of the last match batch's mvKeysUn ([frames][frame_cap]) and
+        frame_cap (the keypoints themselves without a distorted camera)."""
+        k, fc = C.c_void_p(), C.c_int32()
+        L.check(L.lib().orbg_batch_keys_un(self.ctx.handle, C.byref(k), C.byref(fc)),
+                "orbg_batch_keys_un")
+        return k.value, fc.value
+
     def match_batch_device(self, f1, f2, window=100, nnratio=0.9, check_ori=True):
         a = np.ascontiguousarray(f1, np.int32)
         b = np.ascontiguousarray(f2, np.int32)

@@ -83,6 +83,22 @@ def main():
         ext.ctx.check_errors()
         out["gpu_frames_per_s"] = round(B * steps / dt, 1)
         out["gpu_ms_per_256_frames"] = round(dt / steps * 1e3, 4)
+        # the same with TUM1.yaml's distortion (k1..k3, p1, p2): the matching reads mvKeysUn
+        # (Frame::UndistortKeyPoints on the device, Frame.cc:259) inside ComputeImageBounds'
+        # bounds, as the reference's TUM1 run does
+        from orb_slam2_test_amd import frame as FR
+        ext.set_camera(FR.camera(517.306408, 516.469215, 318.643040, 255.313989, 0.262383,
+                                 -0.953104, -0.005358, 0.002628, 1.163314))
+        for _ in range(3):
+            step()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(steps):
+            step()
+        torch.cuda.synchronize()
+        dt = time.perf_counter() - t0
+        ext.ctx.check_errors()
+        out["gpu_tum1_distorted_frames_per_s"] = round(B * steps / dt, 1)
     print(json.dumps(out), flush=True)
 
 
