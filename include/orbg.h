@@ -43,6 +43,12 @@
  *   orbg_is_in_frustum .............. Frame::isInFrustum(pMP, viewingCosLimit)  src/Frame.cc:342-409
  *                                     (Tracking::SearchLocalPoints, Tracking.cc:1676-1691)
  *   orbg_distinctive_descriptor ..... MapPoint::ComputeDistinctiveDescriptors  src/MapPoint.cc:342-420
+ *   orbg_search_for_triangulation ... ORBmatcher::SearchForTriangulation(pKF1, pKF2, F12,
+ *                                     vMatchedPairs, bOnlyStereo)  src/ORBmatcher.cc:779-957
+ *                                     (LocalMapping::CreateNewMapPoints, LocalMapping.cc:378)
+ *   orbg_fuse ....................... ORBmatcher::Fuse(pKF, vpMapPoints, th)'s per-MapPoint search
+ *                                     src/ORBmatcher.cc:968-1069 (LocalMapping::SearchInNeighbors,
+ *                                     LocalMapping.cc:622-690)
  *   orbg_ba_linearize ............... g2o computeActiveErrors + BlockSolver::buildSystem arithmetic
  *                                     for EdgeSE3ProjectXYZ / EdgeStereoSE3ProjectXYZ inside
  *                                     Optimizer::LocalBundleAdjustment  src/Optimizer.cc:633-979
@@ -447,6 +453,80 @@ int orbg_distinctive_descriptor(orbg_ctx *ctx, const uint8_t *desc, int n, int32
 int orbg_distinctive_descriptors_batch_device(orbg_ctx *ctx, const uint8_t *d_pool,
                                               const int32_t *d_rows, const int32_t *d_off,
                                               int npoints, int32_t *d_best, uint8_t *d_desc);
+
+/* ---------------- LocalMapping matchers ---------------- */
+/* A set of KeyFrames in device memory, frame k's rows at + k * cap (fv_off at + k * (cap + 1)):
+ * mDescriptors [cap][32], mvKeysUn [cap] (x, y, angle, octave read), mvuRight [cap] (NULL: all
+ * monocular), has_mp [cap] = GetMapPoint(i) != NULL (NULL: none), counts[k] = N, and mFeatVec
+ * in orbg_bow_transform_batch_device's layout. */
+typedef struct {
+    const uint8_t *desc;
+    const orbg_keypoint *kps;
+    const float *uright;
+    const uint8_t *has_mp;
+    const int32_t *counts;
+    const int32_t *fv_nodes, *fv_off, *fv_feats, *nfv;
+} orbg_keyframes;
+/* The geometry of one SearchForTriangulation pair: F12 (row-major 3x3, LocalMapping::
+ * ComputeF12), pKF1->GetCameraCenter(), pKF2->mTcw rows 0..2 (row-major 3x4) and pKF2's
+ * fx, fy, cx, cy (the epipole, ORBmatcher.cc:800-806). */
+typedef struct {
+    float F12[9];
+    float Cw1[3];
+    float Tcw2[12];
+    float fx2, fy2, cx2, cy2;
+} orbg_triangulation_pair;
+/* ORBmatcher(nnratio, checkOri).SearchForTriangulation(pKF1, pKF2, F12, vMatchedPairs,
+ * bOnlyStereo) for pairs p: KeyFrames d_kf1[p], d_kf2[p] of `kfs`, geometry d_geo[p].
+ * d_matches12[p * cap + i] = vMatches12[i] (the pKF2 index matched to pKF1's feature i, -1;
+ * vMatchedPairs = the (i, d_matches12[i]) with d_matches12[i] >= 0 in i order) for i < N of
+ * pKF1; d_nmatches[p] = the return value.  Scale factors and sigma^2 are the context's
+ * (pKF2->mvScaleFactors / mvLevelSigma2).  Context stream.  ORBG_ENOTSUP past 65535
+ * features per frame. */
+int orbg_search_for_triangulation_batch_device(orbg_ctx *ctx, const orbg_keyframes *kfs, int cap,
+                                               const int32_t *d_kf1, const int32_t *d_kf2,
+                                               const orbg_triangulation_pair *d_geo, int npairs,
+                                               int only_stereo, int check_ori,
+                                               int32_t *d_matches12, int32_t *d_nmatches);
+/* One KeyFrame from host arrays (as orbg_keyframes, one frame; uright / has_mp may be NULL) */
+typedef struct {
+    const orbg_keypoint *kps;
+    const uint8_t *desc;
+    const float *uright;
+    const uint8_t *has_mp;
+    int32_t n;
+    const int32_t *fv_nodes, *fv_off, *fv_feats;
+    int32_t nfv;
+} orbg_keyframe;
+/* The same for one pair from host arrays: matches12[kf1->n], *nmatches. */
+int orbg_search_for_triangulation(orbg_ctx *ctx, const orbg_keyframe *kf1, const orbg_keyframe *kf2,
+                                  const orbg_triangulation_pair *geo, int only_stereo,
+                                  int check_ori, int32_t *matches12, int *nmatches);
+
+/* ORBmatcher::Fuse(pKF, vpMapPoints, th) (src/ORBmatcher.cc:968-1107) splits into a search,
+ * per MapPoint independent of the others (projection with pKF's pose, IsInImage, the
+ * [0.8 dmin, 1.2 dmax] and 60-degree gates, PredictScale, GetFeaturesInArea(u, v, th *
+ * mvScaleFactors[level]), the level window [level - 1, level], the chi-square reprojection
+ * gates 5.99 / 7.8, the least descriptor distance -- the first in GetFeaturesInArea's order),
+ * and the sequential map update of every point whose best distance is <= TH_LOW (Replace or
+ * AddObservation, :1071-1104), which the caller applies in vpMapPoints order.
+ * This is the search: best_idx[i] = the pKF feature the reference fuses point i with, -1 if
+ * none; best_dist[i] = bestDist (256: no candidate).  mps[i].flags ORBG_MP_VALID = pMP &&
+ * !isBad() && !IsInKeyFrame(pKF) when the call starts; cam = pKF's pose, fx.., mbf,
+ * mfLogScaleFactor, mnScaleLevels and mnMinX..; scale factors / inverse sigma^2 are the
+ * context's.  One KeyFrame from host arrays (kf->fv_* unused): */
+int orbg_fuse(orbg_ctx *ctx, const orbg_keyframe *kf, const orbg_frustum_camera *cam,
+              const orbg_map_point *mps, const uint8_t *mdesc, int nmp, float th,
+              int32_t *best_idx, int32_t *best_dist, int *nfused);
+/* Batched, device memory: pair p = KeyFrame d_kf[p] of `kfs` (desc, kps, uright, counts
+ * read) with camera d_cams[p] and the d_mcounts[p] MapPoints at d_mps + p * mcap (descriptors
+ * d_mdesc + p * mcap * 32); outputs at + p * mcap, d_nfused[p] = points with a target.
+ * Context stream.  ORBG_ENOTSUP past 8192 keypoints per KeyFrame (the grid lives in LDS). */
+int orbg_fuse_batch_device(orbg_ctx *ctx, const orbg_keyframes *kfs, int cap, const int32_t *d_kf,
+                           const orbg_frustum_camera *d_cams, const orbg_map_point *d_mps,
+                           const uint8_t *d_mdesc, const int32_t *d_mcounts, int mcap, int npairs,
+                           float th, int32_t *d_best_idx, int32_t *d_best_dist,
+                           int32_t *d_nfused);
 
 /* ---------------- Optimizer::PoseOptimization ----------------
  * One edge per Frame keypoint with a MapPoint (index order): EdgeSE3ProjectXYZOnlyPose when

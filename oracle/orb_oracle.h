@@ -252,6 +252,43 @@ int orc_is_in_frustum_n(const orc_frustum_cam *cam, const orc_map_point *mps, in
 void orc_distinctive_descriptors_n(const uint8_t *pool, const int32_t *rows, const int32_t *off,
                                    int npoints, int32_t *best);
 
+/* ---- LocalMapping matchers (mapping_oracle.c) ---- */
+/* one KeyFrame as SearchForTriangulation reads it */
+typedef struct {
+    const orc_keypoint *kps;  /* mvKeysUn (x, y, angle, octave) */
+    const uint8_t *desc;      /* mDescriptors */
+    const float *uright;      /* mvuRight (< 0: monocular) */
+    const uint8_t *has_mp;    /* GetMapPoint(i) != NULL */
+    int32_t n;
+    const int32_t *fv_nodes, *fv_off, *fv_feats;  /* mFeatVec */
+    int32_t nfv;
+} orc_tri_kf;
+/* F12 (row-major 3x3, LocalMapping::ComputeF12), pKF1->GetCameraCenter(), pKF2's pose rows
+ * and intrinsics */
+typedef struct {
+    float F12[9];
+    float Cw1[3];
+    float Tcw2[12];
+    float fx2, fy2, cx2, cy2;
+} orc_tri_geom;
+/* ORBmatcher(nnratio, checkOri).SearchForTriangulation: matches12[kf1->n] = vMatches12 (the
+ * KF2 index matched to each KF1 feature, -1), returns nmatches.  scale_factors / sigma2 =
+ * pKF2->mvScaleFactors / mvLevelSigma2. */
+int orc_search_for_triangulation(const orc_tri_kf *kf1, const orc_tri_kf *kf2,
+                                 const orc_tri_geom *g, const float *scale_factors,
+                                 const float *sigma2, int only_stereo, int check_ori,
+                                 int32_t *matches12);
+void orc_three_maxima(const int *hsize, int *ind1, int *ind2, int *ind3);
+/* ORBmatcher::Fuse(pKF, vpMapPoints, th)'s per-MapPoint search: kf = the KeyFrame's mvKeysUn,
+ * mDescriptors, mvuRight (n; the FeatureVector is not read), cam = its pose, intrinsics,
+ * mbf, mfLogScaleFactor, mnScaleLevels and bounds; mps[i] (flags ORC_MP_VALID: pMP &&
+ * !isBad() && !IsInKeyFrame(pKF)) with descriptor mdesc[i]; best_idx[i] = the KeyFrame
+ * feature the reference fuses the point with (bestDist <= TH_LOW), else -1; best_dist[i] =
+ * bestDist (256 when none).  Returns the number of points with a fusion target. */
+int orc_fuse_search(const orc_tri_kf *kf, const orc_frustum_cam *cam, const orc_map_point *mps,
+                    const uint8_t *mdesc, int nmp, float th, const float *scale_factors,
+                    const float *inv_sigma2, int32_t *best_idx, int32_t *best_dist);
+
 /* ---- Optimizer::PoseOptimization (pose_oracle.c) ---- */
 /* LM's pow(2 rho - 1, 3) as the once-rounded exact cube (optimization_algorithm_levenberg.cpp:135) */
 double orc_lm_cube(double t);

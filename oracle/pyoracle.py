@@ -53,6 +53,17 @@ FRUSTUM_DTYPE = np.dtype([("Tcw", "<f4", 12), ("fx", "<f4"), ("fy", "<f4"), ("cx
                           ("min_y", "<f4"), ("max_y", "<f4")])
 
 
+# SearchForTriangulation pair geometry (orb_oracle.h orc_tri_geom)
+TRI_GEOM_DTYPE = np.dtype([("F12", "<f4", 9), ("Cw1", "<f4", 3), ("Tcw2", "<f4", 12),
+                           ("fx2", "<f4"), ("fy2", "<f4"), ("cx2", "<f4"), ("cy2", "<f4")])
+
+
+class TriKF(C.Structure):
+    _fields_ = [("kps", C.c_void_p), ("desc", C.c_void_p), ("uright", C.c_void_p),
+                ("has_mp", C.c_void_p), ("n", C.c_int32), ("fv_nodes", C.c_void_p),
+                ("fv_off", C.c_void_p), ("fv_feats", C.c_void_p), ("nfv", C.c_int32)]
+
+
 class Params(C.Structure):
     _fields_ = [("nfeatures", C.c_int32), ("scale_factor", C.c_float), ("nlevels", C.c_int32),
                 ("ini_th_fast", C.c_int32), ("min_th_fast", C.c_int32),
@@ -181,6 +192,11 @@ def lib():
         L.orc_search_by_bow.restype = C.c_int
         L.orc_search_by_bow.argtypes = [vp, vp, vp, C.c_int, vp, vp, vp, C.c_int, vp, vp, C.c_int,
                                         vp, vp, vp, C.c_int, C.c_float, C.c_int, vp]
+        L.orc_search_for_triangulation.argtypes = [P(TriKF), P(TriKF), vp, vp, vp, C.c_int,
+                                                   C.c_int, vp]
+        L.orc_search_for_triangulation.restype = C.c_int
+        L.orc_fuse_search.argtypes = [P(TriKF), vp, vp, vp, C.c_int, C.c_float, vp, vp, vp, vp]
+        L.orc_fuse_search.restype = C.c_int
         L.orc_undistort_points.argtypes = [vp, vp, C.c_int, vp]
         L.orc_undistort_keypoints.argtypes = [vp, vp, C.c_int, vp]
         L.orc_image_bounds.argtypes = [vp, C.c_int, C.c_int, P(Bounds)]
@@ -659,3 +675,50 @@ def distinctive_descriptors(pool, rows, off):
     best = np.zeros(len(off) - 1, np.int32)
     lib().orc_distinctive_descriptors_n(_p(pool), _p(rows), _p(off), len(off) - 1, _p(best))
     return best
+
+
+# ---- LocalMapping matchers (mapping_oracle.c) ----
+def _tri_kf(kf, keep):
+    """kf: dict(kps, desc, uright, has_mp, fv=(nodes, off, feats)) -> TriKF (arrays kept alive
+    in `keep`)."""
+    kps = np.ascontiguousarray(kf["kps"], KP_DTYPE)
+    n = len(kps)
+    desc = np.ascontiguousarray(kf["desc"], np.uint8).reshape(-1, 32)
+    ur = kf.get("uright")
+    ur = np.full(max(n, 1), -1.0, np.float32) if ur is None else np.ascontiguousarray(ur, np.float32)
+    mp = kf.get("has_mp")
+    mp = np.zeros(max(n, 1), np.uint8) if mp is None else np.ascontiguousarray(mp, np.uint8)
+    nodes, off, feats = (np.ascontiguousarray(a, np.int32) for a in kf["fv"])
+    keep += [kps, desc, ur, mp, nodes, off, feats]
+    return TriKF(_p(kps), _p(desc), _p(ur), _p(mp), n, _p(nodes), _p(off), _p(feats), len(nodes))
+
+
+def search_for_triangulation(kf1, kf2, geom, scale_factors, sigma2, only_stereo=False,
+                             check_ori=False):
+    """ORBmatcher(0.6, check_ori).SearchForTriangulation -> (nmatches, vMatches12)."""
+    keep = []
+    a, b = _tri_kf(kf1, keep), _tri_kf(kf2, keep)
+    g = np.ascontiguousarray(geom, TRI_GEOM_DTYPE)
+    sf = np.ascontiguousarray(scale_factors, np.float32)
+    s2 = np.ascontiguousarray(sigma2, np.float32)
+    m = np.zeros(max(a.n, 1), np.int32)
+    n = lib().orc_search_for_triangulation(C.byref(a), C.byref(b), _p(g), _p(sf), _p(s2),
+                                           int(only_stereo), int(check_ori), _p(m))
+    return n, m[:a.n]
+
+
+def fuse_search(kf, fcam, mps, mdesc, th, scale_factors, inv_sigma2):
+    """ORBmatcher::Fuse(pKF, vpMapPoints, th)'s search -> (nfused, best_idx, best_dist).
+    kf: dict(kps, desc, uright) (mvKeysUn, mDescriptors, mvuRight)."""
+    keep = []
+    k = _tri_kf(dict(kf, fv=(np.zeros(0), np.zeros(1), np.zeros(0))), keep)
+    fcam = np.ascontiguousarray(fcam, FRUSTUM_DTYPE)
+    mps = np.ascontiguousarray(mps, MAPPOINT_DTYPE)
+    md = np.ascontiguousarray(mdesc, np.uint8).reshape(-1, 32)
+    sf = np.ascontiguousarray(scale_factors, np.float32)
+    isg = np.ascontiguousarray(inv_sigma2, np.float32)
+    bi = np.zeros(max(len(mps), 1), np.int32)
+    bd = np.zeros(max(len(mps), 1), np.int32)
+    n = lib().orc_fuse_search(C.byref(k), _p(fcam), _p(mps), _p(md), len(mps), float(th),
+                              _p(sf), _p(isg), _p(bi), _p(bd))
+    return n, bi[:len(mps)], bd[:len(mps)]

@@ -59,6 +59,24 @@ FRUSTUM_DTYPE = np.dtype([("Tcw", "<f4", 12), ("fx", "<f4"), ("fy", "<f4"), ("cx
                           ("min_y", "<f4"), ("max_y", "<f4")])
 
 
+TRI_GEOM_DTYPE = np.dtype([("F12", "<f4", 9), ("Cw1", "<f4", 3), ("Tcw2", "<f4", 12),
+                           ("fx2", "<f4"), ("fy2", "<f4"), ("cx2", "<f4"), ("cy2", "<f4")])
+
+
+class KeyFrames(C.Structure):
+    """orbg_keyframes (include/orbg.h): a set of KeyFrames in device memory."""
+    _fields_ = [("desc", C.c_void_p), ("kps", C.c_void_p), ("uright", C.c_void_p),
+                ("has_mp", C.c_void_p), ("counts", C.c_void_p), ("fv_nodes", C.c_void_p),
+                ("fv_off", C.c_void_p), ("fv_feats", C.c_void_p), ("nfv", C.c_void_p)]
+
+
+class KeyFrame(C.Structure):
+    """orbg_keyframe (include/orbg.h): one KeyFrame from host arrays."""
+    _fields_ = [("kps", C.c_void_p), ("desc", C.c_void_p), ("uright", C.c_void_p),
+                ("has_mp", C.c_void_p), ("n", C.c_int32), ("fv_nodes", C.c_void_p),
+                ("fv_off", C.c_void_p), ("fv_feats", C.c_void_p), ("nfv", C.c_int32)]
+
+
 PEDGE_DTYPE = np.dtype([("obs", "<f4", 3), ("xw", "<f4", 3), ("inv_sigma2", "<f4"),
                         ("stereo", "<i4")])
 
@@ -220,6 +238,13 @@ def lib():
         "orbg_ba_graph_set_active": (i32, [vp, vp, vp]),
         "orbg_ba_graph_build_system": (i32, [vp, vp, vp, vp, vp, vp, vp, vp, vp]),
         "orbg_ba_graph_errors": (i32, [vp, vp, vp, vp, vp, vp, vp, vp]),
+        "orbg_search_for_triangulation": (i32, [vp, P(KeyFrame), P(KeyFrame), vp, i32, i32, vp,
+                                                P(i32)]),
+        "orbg_search_for_triangulation_batch_device": (i32, [vp, P(KeyFrames), i32, vp, vp, vp,
+                                                             i32, i32, i32, vp, vp]),
+        "orbg_fuse": (i32, [vp, P(KeyFrame), vp, vp, vp, i32, f32, vp, vp, P(i32)]),
+        "orbg_fuse_batch_device": (i32, [vp, P(KeyFrames), i32, vp, vp, vp, vp, vp, i32, i32, f32,
+                                         vp, vp, vp]),
         "orbg_undistort_keypoints": (i32, [vp, vp, vp, i32, vp]),
         "orbg_undistort_batch_device": (i32, [vp, vp, vp, vp, i32, i32, vp]),
         "orbg_compute_image_bounds": (i32, [vp, i32, i32, P(Bounds)]),

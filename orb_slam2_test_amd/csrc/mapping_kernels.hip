@@ -1,0 +1,542 @@
+// mapping_kernels.hip -- LocalMapping's per-keyframe Hamming matchers for gfx950.
+//
+//   k_fuse        ORBmatcher::Fuse(pKF, vpMapPoints, th)'s per-MapPoint search (src/ORBmatcher.cc:
+//                 968-1069; LocalMapping::SearchInNeighbors, LocalMapping.cc:622-690), one
+//                 workgroup per (KeyFrame, MapPoint list) pair: the KeyFrame's grid
+//                 (Frame::AssignFeaturesToGrid, PosInGrid) counting-sorted into LDS, then a thread
+//                 per MapPoint: projection, IsInImage, the scale-invariance and viewing-angle
+//                 gates, PredictScale, GetFeaturesInArea's cells, the level window and the
+//                 chi-square reprojection gates, best distance by the 64-bit key (distance,
+//                 grid cell, index): the first candidate of the least distance in the
+//                 reference's enumeration (cell major, ascending index inside a cell), its
+//                 strict <.  Returns bestIdx per point (-1 unless bestDist <= TH_LOW): the
+//                 caller's sequential map update (Replace / AddObservation) applies it.
+//   k_tri_match   ORBmatcher::SearchForTriangulation(pKF1, pKF2, F12, vMatchedPairs,
+//                 bOnlyStereo) (src/ORBmatcher.cc:779-957; LocalMapping::CreateNewMapPoints,
+//                 LocalMapping.cc:305-378), one 256-thread workgroup per (KF1, KF2) pair.
+//
+// The reference walks both FeatureVectors in node order and, for every KF1 feature without a
+// MapPoint, scans the shared node's KF2 features: a candidate passes when it has no MapPoint
+// (vbMatched2 is never set, :810, so KF1 features do not compete), its distance is <= TH_LOW,
+// it is away from the epipole (both monocular) and CheckDistEpipolarLine holds; it replaces
+// the best on dist <= bestDist, so the result is the LAST passing candidate of the least
+// distance.  Every KF1 feature is therefore independent:
+//   join      KF1 node ids joined with KF2's by binary search into an LDS list (as k_bow_match);
+//   node      a wave per common node: lane l holds KF2 candidate l (and l + 64) with its
+//             descriptor, position, octave thresholds and flags in registers; each KF1 feature
+//             of the node is broadcast through scalar registers, its epipolar line (a, b, c)
+//             computed once (wave-uniform), every lane tests its candidate, and one wave-wide
+//             max of (51 - dist) << 16 | position gives the least distance, last position;
+//   rotation  ComputeThreeMaxima over an LDS histogram when checkOri (CreateNewMapPoints uses
+//             ORBmatcher(0.6, false): off), then the matches outside the three bins dropped.
+// Float pins as the oracle (oracle/mapping_oracle.c): C2 = R2w*Cw+t2w by cv::gemm's double
+// work type, the epipolar test's float dsqr compared with 3.84 * sigma2 in double; no FMA.
+#include <hip/hip_runtime.h>
+
+#include "../../include/orbg.h"
+#include "orbg_device.h"
+#include "orbg_internal.h"
+
+#pragma clang fp contract(off)
+
+namespace orbg {
+
+#define TM_HISTO 30
+#define TM_TH_LOW 50
+#define TM_LIST 1024  // common nodes per pass held in LDS
+
+struct TriTables {
+    float scale[ORBG_MAX_LEVELS];   // pKF2->mvScaleFactors
+    double epi_th[ORBG_MAX_LEVELS]; // 3.84 * mvLevelSigma2 (double, as the reference compares)
+};
+
+__device__ __forceinline__ unsigned wave_max_u32(unsigned v)
+{
+    v = max(v, (unsigned)__builtin_amdgcn_update_dpp(0, (int)v, 0xb1, 0xf, 0xf, false));  // quad_perm 1,0,3,2
+    v = max(v, (unsigned)__builtin_amdgcn_update_dpp(0, (int)v, 0x4e, 0xf, 0xf, false));  // quad_perm 2,3,0,1
+    v = max(v, (unsigned)__builtin_amdgcn_update_dpp(0, (int)v, 0x124, 0xf, 0xf, false)); // row_ror 4
+    v = max(v, (unsigned)__builtin_amdgcn_update_dpp(0, (int)v, 0x128, 0xf, 0xf, false)); // row_ror 8
+    const unsigned r0 = (unsigned)__builtin_amdgcn_readlane((int)v, 0);
+    const unsigned r1 = (unsigned)__builtin_amdgcn_readlane((int)v, 16);
+    const unsigned r2 = (unsigned)__builtin_amdgcn_readlane((int)v, 32);
+    const unsigned r3 = (unsigned)__builtin_amdgcn_readlane((int)v, 48);
+    return max(max(r0, r1), max(r2, r3));
+}
+
+__device__ __forceinline__ int tm_rot_bin(float a1, float a2)
+{
+    const float factor = 1.0f / TM_HISTO;
+    float rot = a1 - a2;
+    if (rot < 0.0) rot += 360.0f;
+    int bin = (int)roundf(rot * factor);
+    if (bin == TM_HISTO) bin = 0;
+    return bin;
+}
+
+// one KF2 candidate as a lane holds it
+struct TriCand {
+    uint32_t d[8];
+    float x, y;
+    double th;      // 3.84 * sigma2[octave]
+    int idx;        // -1: no candidate (past the node) or unusable (MapPoint / not stereo)
+    bool stereo;
+    bool epi_far;   // away from the epipole (the monocular pair test)
+};
+
+__device__ __forceinline__ void tri_load(TriCand &c, const orbg_keyframes &K, int kf2, int cap,
+                                         int f2, int pos, int nF, float ex, float ey,
+                                         const TriTables &T, int only_stereo)
+{
+    c.idx = -1;
+#pragma unroll
+    for (int w = 0; w < 8; w++) c.d[w] = 0u;
+    c.x = c.y = 0.f;
+    c.th = 0.0;
+    c.stereo = false;
+    c.epi_far = false;
+    if (pos >= nF) return;
+    const int idx = K.fv_feats[(size_t)kf2 * cap + f2 + pos];
+    const size_t g = (size_t)kf2 * cap + idx;
+    if (K.has_mp && K.has_mp[g]) return;
+    const bool st = K.uright ? K.uright[g] >= 0 : false;
+    if (only_stereo && !st) return;
+    const orbg_keypoint kp = K.kps[g];
+    const uint4 *p = (const uint4 *)(K.desc + g * 32);
+    const uint4 a = p[0], b = p[1];
+    c.d[0] = a.x; c.d[1] = a.y; c.d[2] = a.z; c.d[3] = a.w;
+    c.d[4] = b.x; c.d[5] = b.y; c.d[6] = b.z; c.d[7] = b.w;
+    c.x = kp.x;
+    c.y = kp.y;
+    c.th = T.epi_th[kp.octave];
+    const float distex = ex - kp.x, distey = ey - kp.y;
+    c.epi_far = !(distex * distex + distey * distey < 100 * T.scale[kp.octave]);
+    c.stereo = st;
+    c.idx = idx;
+}
+
+// key of a passing candidate: (51 - dist) << 16 | position (wave max = least distance, last
+// position); 0 = does not pass
+__device__ __forceinline__ unsigned tri_key(const TriCand &c, const uint32_t q[8], bool stereo1,
+                                            float a, float b, float cc, float den, int pos)
+{
+    if (c.idx < 0) return 0u;
+    int dist = 0;
+#pragma unroll
+    for (int w = 0; w < 8; w++) dist += __popc(q[w] ^ c.d[w]);
+    if (dist > TM_TH_LOW) return 0u;
+    if (!stereo1 && !c.stereo && !c.epi_far) return 0u;
+    // CheckDistEpipolarLine (ORBmatcher.cc:165-182)
+    if (den == 0) return 0u;
+    const float num = a * c.x + b * c.y + cc;
+    const float dsqr = num * num / den;
+    if (!((double)dsqr < c.th)) return 0u;
+    return ((unsigned)(51 - dist) << 16) | (unsigned)pos;
+}
+
+__global__ __launch_bounds__(256) void k_tri_match(orbg_keyframes K, int cap,
+                                                   const int32_t *__restrict__ kf1_index,
+                                                   const int32_t *__restrict__ kf2_index,
+                                                   const orbg_triangulation_pair *__restrict__ geo,
+                                                   TriTables T, int only_stereo, int check_ori,
+                                                   int32_t *__restrict__ match,
+                                                   int32_t *__restrict__ nmatch)
+{
+    __shared__ int2 common[TM_LIST];
+    __shared__ int ncommon, nm, removed, hist[TM_HISTO], ind[3];
+    const int p = blockIdx.x;
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    const int k1 = kf1_index[p], k2 = kf2_index[p];
+    const int n1 = K.counts[k1];
+    const int nn1 = K.nfv[k1], nn2 = K.nfv[k2];
+    const int32_t *n1ids = K.fv_nodes + (size_t)k1 * cap, *o1 = K.fv_off + (size_t)k1 * (cap + 1),
+                  *fe1 = K.fv_feats + (size_t)k1 * cap;
+    const int32_t *n2ids = K.fv_nodes + (size_t)k2 * cap, *o2 = K.fv_off + (size_t)k2 * (cap + 1);
+    const orbg_keypoint *kp1 = K.kps + (size_t)k1 * cap, *kp2 = K.kps + (size_t)k2 * cap;
+    const uint8_t *desc1 = K.desc + (size_t)k1 * cap * 32;
+    int32_t *out = match + (size_t)p * cap;
+    // the epipole (ORBmatcher.cc:800-806): C2 = R2w*Cw+t2w, cv::gemm small-matrix pin
+    const orbg_triangulation_pair &G = geo[p];
+    float C2[3];
+#pragma unroll
+    for (int r = 0; r < 3; r++) {
+        double t = 0.0;
+#pragma unroll
+        for (int k = 0; k < 3; k++) t += (double)G.Tcw2[4 * r + k] * (double)G.Cw1[k];
+        t *= 1.0;
+        t += (double)G.Tcw2[4 * r + 3];
+        C2[r] = (float)t;
+    }
+    const float invz = 1.0f / C2[2];
+    const float ex = G.fx2 * C2[0] * invz + G.cx2;
+    const float ey = G.fy2 * C2[1] * invz + G.cy2;
+    float F[9];
+#pragma unroll
+    for (int i = 0; i < 9; i++) F[i] = G.F12[i];
+
+    if (threadIdx.x == 0) {
+        nm = 0;
+        removed = 0;
+    }
+    if (threadIdx.x < TM_HISTO) hist[threadIdx.x] = 0;
+    for (int i = threadIdx.x; i < n1; i += blockDim.x) out[i] = -1;
+    int wave_nm = 0;
+    for (int j0 = 0; j0 < nn1; j0 += TM_LIST) {
+        if (threadIdx.x == 0) ncommon = 0;
+        __syncthreads();
+        for (int j = j0 + (int)threadIdx.x; j < min(nn1, j0 + TM_LIST); j += blockDim.x) {
+            const int id = n1ids[j];
+            int lo = 0, hi = nn2;
+            while (lo < hi) {
+                const int mid = (lo + hi) >> 1;
+                if (n2ids[mid] < id)
+                    lo = mid + 1;
+                else
+                    hi = mid;
+            }
+            if (lo < nn2 && n2ids[lo] == id) common[atomicAdd(&ncommon, 1)] = make_int2(j, lo);
+        }
+        __syncthreads();
+        const int nc = ncommon;
+        for (int c = wv; c < nc; c += (int)(blockDim.x >> 6)) {
+            const int2 jb = common[c];
+            const int a0 = o1[jb.x], a1 = o1[jb.x + 1];
+            const int f2 = o2[jb.y], nF = o2[jb.y + 1] - f2;
+            TriCand c0, c1;
+            tri_load(c0, K, k2, cap, f2, lane, nF, ex, ey, T, only_stereo);
+            tri_load(c1, K, k2, cap, f2, lane + 64, nF, ex, ey, T, only_stereo);
+            for (int ia = a0; ia < a1; ia++) {
+                const int idx1 = __builtin_amdgcn_readfirstlane(fe1[ia]);
+                const size_t g1 = (size_t)k1 * cap + idx1;
+                if (K.has_mp && K.has_mp[g1]) continue;  // pMP1: wave-uniform skip
+                const bool st1 = K.uright ? K.uright[g1] >= 0 : false;
+                if (only_stereo && !st1) continue;
+                uint32_t q[8];
+#pragma unroll
+                for (int w = 0; w < 8; w++)
+                    q[w] = __builtin_amdgcn_readfirstlane(((const uint32_t *)(desc1 + (size_t)idx1 * 32))[w]);
+                const orbg_keypoint k = kp1[idx1];
+                // epipolar line l = x1' F12 (ORBmatcher.cc:168-170), wave-uniform
+                const float a = k.x * F[0] + k.y * F[3] + F[6];
+                const float b = k.x * F[1] + k.y * F[4] + F[7];
+                const float cc = k.x * F[2] + k.y * F[5] + F[8];
+                const float den = a * a + b * b;
+                unsigned key = max(tri_key(c0, q, st1, a, b, cc, den, lane),
+                                   tri_key(c1, q, st1, a, b, cc, den, lane + 64));
+                for (int ch = 2; ch * 64 < nF; ch++) {  // nodes past 128 candidates: re-read
+                    TriCand cx;
+                    tri_load(cx, K, k2, cap, f2, ch * 64 + lane, nF, ex, ey, T, only_stereo);
+                    key = max(key, tri_key(cx, q, st1, a, b, cc, den, ch * 64 + lane));
+                }
+                const unsigned best = wave_max_u32(key);
+                if (best) {
+                    wave_nm++;
+                    if (lane == 0) {
+                        const int idx2 = K.fv_feats[(size_t)k2 * cap + f2 + (int)(best & 0xFFFFu)];
+                        out[idx1] = idx2;
+                        if (check_ori) atomicAdd(&hist[tm_rot_bin(k.angle, kp2[idx2].angle)], 1);
+                    }
+                }
+            }
+        }
+        __syncthreads();
+    }
+    if (lane == 0 && wave_nm) atomicAdd(&nm, wave_nm);
+    __syncthreads();
+    if (check_ori) {
+        if (threadIdx.x == 0) {
+            // ComputeThreeMaxima (ORBmatcher.cc:1800-1841)
+            int max1 = 0, max2 = 0, max3 = 0, i1 = -1, i2 = -1, i3 = -1;
+            for (int i = 0; i < TM_HISTO; i++) {
+                const int s = hist[i];
+                if (s > max1) {
+                    max3 = max2;
+                    max2 = max1;
+                    max1 = s;
+                    i3 = i2;
+                    i2 = i1;
+                    i1 = i;
+                } else if (s > max2) {
+                    max3 = max2;
+                    max2 = s;
+                    i3 = i2;
+                    i2 = i;
+                } else if (s > max3) {
+                    max3 = s;
+                    i3 = i;
+                }
+            }
+            if (max2 < 0.1f * (float)max1) {
+                i2 = -1;
+                i3 = -1;
+            } else if (max3 < 0.1f * (float)max1) {
+                i3 = -1;
+            }
+            ind[0] = i1;
+            ind[1] = i2;
+            ind[2] = i3;
+        }
+        __syncthreads();
+        int rm = 0;
+        for (int i = threadIdx.x; i < n1; i += blockDim.x) {
+            const int m = out[i];
+            if (m < 0) continue;
+            const int bin = tm_rot_bin(kp1[i].angle, kp2[m].angle);
+            if (bin != ind[0] && bin != ind[1] && bin != ind[2]) {
+                out[i] = -1;
+                rm++;
+            }
+        }
+        if (rm) atomicAdd(&removed, rm);
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) nmatch[p] = nm - removed;
+}
+
+// ---------------------------------------------------------------------------
+// Fuse
+// ---------------------------------------------------------------------------
+struct FuseTables {
+    float scale[ORBG_MAX_LEVELS];      // pKF->mvScaleFactors
+    float inv_sigma2[ORBG_MAX_LEVELS]; // pKF->mvInvLevelSigma2
+};
+
+struct FuseKey {  // a grid entry in LDS
+    float x, y;
+    int io;  // index << 4 | octave
+};
+
+#define FU_CELLS (ORBG_GRID_COLS * ORBG_GRID_ROWS)
+static_assert(FU_CELLS == 256 * 12, "k_fuse's scan gives 12 grid cells to each of 256 threads");
+
+__global__ __launch_bounds__(256) void k_fuse(orbg_keyframes K, int cap,
+                                              const int32_t *__restrict__ kf_index,
+                                              const orbg_frustum_camera *__restrict__ cams,
+                                              const orbg_map_point *__restrict__ mps,
+                                              const uint8_t *__restrict__ mdesc,
+                                              const int32_t *__restrict__ mcounts, int mcap,
+                                              float th, FuseTables T,
+                                              int32_t *__restrict__ best_idx,
+                                              int32_t *__restrict__ best_dist,
+                                              int32_t *__restrict__ nfused)
+{
+    extern __shared__ __attribute__((aligned(16))) uint8_t fu_lds[];
+    int *cstart = (int *)fu_lds;                         // FU_CELLS + 1
+    FuseKey *keys = (FuseKey *)(fu_lds + (FU_CELLS + 4) * 4);
+    __shared__ int nf_total;
+    const int p = blockIdx.x, tid = threadIdx.x;
+    const int kf = kf_index[p];
+    const int n = K.counts[kf];
+    const orbg_frustum_camera C = cams[p];
+    const orbg_keypoint *kps = K.kps + (size_t)kf * cap;
+    // ---- the KeyFrame grid (Frame.cc:273-274, 292-307, PosInGrid :510-520) ----
+    const float inv_w = (float)ORBG_GRID_COLS / (float)(C.bounds.max_x - C.bounds.min_x);
+    const float inv_h = (float)ORBG_GRID_ROWS / (float)(C.bounds.max_y - C.bounds.min_y);
+    for (int c = tid; c <= FU_CELLS; c += 256) cstart[c] = 0;
+    if (tid == 0) nf_total = 0;
+    __syncthreads();
+    for (int i = tid; i < n; i += 256) {
+        const orbg_keypoint kp = kps[i];
+        const int px = (int)roundf((kp.x - C.bounds.min_x) * inv_w);
+        const int py = (int)roundf((kp.y - C.bounds.min_y) * inv_h);
+        if (px < 0 || px >= ORBG_GRID_COLS || py < 0 || py >= ORBG_GRID_ROWS) continue;
+        atomicAdd(&cstart[px * ORBG_GRID_ROWS + py + 1], 1);
+    }
+    __syncthreads();
+    // exclusive starts: 12 cells per thread, then a block scan of the thread totals
+    {
+        __shared__ int part[256];
+        const int c0 = tid * 12;
+        int loc = 0;
+        for (int c = c0; c < c0 + 12; c++) loc += cstart[c + 1];
+        part[tid] = loc;
+        __syncthreads();
+        for (int o = 1; o < 256; o <<= 1) {
+            const int v = tid >= o ? part[tid - o] : 0;
+            __syncthreads();
+            part[tid] += v;
+            __syncthreads();
+        }
+        int run = tid ? part[tid - 1] : 0;
+        for (int c = c0; c < c0 + 12; c++) {
+            const int v = cstart[c + 1];
+            cstart[c + 1] = run + v;
+            run += v;
+        }
+    }
+    __syncthreads();
+    // scatter: cstart[c] (the start of cell c) is the cell's cursor, so afterwards it holds
+    // the cell's end and the start is cstart[c - 1]; the order inside a cell is irrelevant
+    // (the selection key carries the index)
+    for (int i = tid; i < n; i += 256) {
+        const orbg_keypoint kp = kps[i];
+        const int px = (int)roundf((kp.x - C.bounds.min_x) * inv_w);
+        const int py = (int)roundf((kp.y - C.bounds.min_y) * inv_h);
+        if (px < 0 || px >= ORBG_GRID_COLS || py < 0 || py >= ORBG_GRID_ROWS) continue;
+        const int slot = atomicAdd(&cstart[px * ORBG_GRID_ROWS + py], 1);
+        keys[slot] = FuseKey{kp.x, kp.y, i << 4 | (kp.octave & 15)};
+    }
+    __syncthreads();
+    int fused = 0;
+    const int nm = mcounts[p];
+    const float tcw0 = C.Tcw[3], tcw1 = C.Tcw[7], tcw2 = C.Tcw[11];
+    // KeyFrame::GetCameraCenter: Ow = -Rwc*tcw (cv::gemm pin)
+    float Ow[3];
+#pragma unroll
+    for (int r = 0; r < 3; r++) {
+        double t = 0.0;
+        t += (double)C.Tcw[r] * (double)tcw0;
+        t += (double)C.Tcw[4 + r] * (double)tcw1;
+        t += (double)C.Tcw[8 + r] * (double)tcw2;
+        Ow[r] = (float)(t * -1.0);
+    }
+    for (int i = tid; i < nm; i += 256) {
+        const size_t o = (size_t)p * mcap + i;
+        int bidx = -1, bdist = 256;
+        const orbg_map_point mp = mps[o];
+        do {
+            if (!(mp.flags & ORBG_MP_VALID)) break;
+            const float P[3] = {mp.x, mp.y, mp.z};
+            float Pc[3];
+            const float tc[3] = {tcw0, tcw1, tcw2};
+#pragma unroll
+            for (int r = 0; r < 3; r++) {
+                double t = 0.0;
+#pragma unroll
+                for (int k = 0; k < 3; k++) t += (double)C.Tcw[4 * r + k] * (double)P[k];
+                t *= 1.0;
+                t += (double)tc[r];
+                Pc[r] = (float)t;
+            }
+            if (Pc[2] < 0.0f) break;
+            const float invz = 1 / Pc[2];
+            const float x = Pc[0] * invz, y = Pc[1] * invz;
+            const float u = C.fx * x + C.cx, v = C.fy * y + C.cy;
+            if (!(u >= C.bounds.min_x && u < C.bounds.max_x && v >= C.bounds.min_y &&
+                  v < C.bounds.max_y))
+                break;
+            const float ur = u - C.bf * invz;
+            const float maxDistance = 1.2f * mp.max_dist, minDistance = 0.8f * mp.min_dist;
+            const float PO0 = P[0] - Ow[0], PO1 = P[1] - Ow[1], PO2 = P[2] - Ow[2];
+            double s = 0.0;
+            s += (double)PO0 * (double)PO0;
+            s += (double)PO1 * (double)PO1;
+            s += (double)PO2 * (double)PO2;
+            const float dist3D = (float)sqrt(s);
+            if (dist3D < minDistance || dist3D > maxDistance) break;
+            double dot = 0.0;
+            dot += (double)PO0 * (double)mp.nx;
+            dot += (double)PO1 * (double)mp.ny;
+            dot += (double)PO2 * (double)mp.nz;
+            if (dot < 0.5 * (double)dist3D) break;
+            const float ratio = mp.max_dist / dist3D;
+            int lvl = (int)ceil(log((double)ratio) / (double)C.log_scale_factor);
+            if (lvl < 0)
+                lvl = 0;
+            else if (lvl >= C.nlevels)
+                lvl = C.nlevels - 1;
+            const float r = th * T.scale[lvl];
+            // GetFeaturesInArea's cells (KeyFrame.cc:755-769)
+            const int cx0 = max(0, (int)floorf((u - C.bounds.min_x - r) * inv_w));
+            if (cx0 >= ORBG_GRID_COLS) break;
+            const int cx1 = min(ORBG_GRID_COLS - 1, (int)ceilf((u - C.bounds.min_x + r) * inv_w));
+            if (cx1 < 0) break;
+            const int cy0 = max(0, (int)floorf((v - C.bounds.min_y - r) * inv_h));
+            if (cy0 >= ORBG_GRID_ROWS) break;
+            const int cy1 = min(ORBG_GRID_ROWS - 1, (int)ceilf((v - C.bounds.min_y + r) * inv_h));
+            if (cy1 < 0) break;
+            uint32_t q[8];
+            {
+                const uint4 *dp = (const uint4 *)(mdesc + o * 32);
+                const uint4 a = dp[0], b = dp[1];
+                q[0] = a.x; q[1] = a.y; q[2] = a.z; q[3] = a.w;
+                q[4] = b.x; q[5] = b.y; q[6] = b.z; q[7] = b.w;
+            }
+            unsigned long long best = ~0ull;
+            for (int ix = cx0; ix <= cx1; ix++)
+                for (int iy = cy0; iy <= cy1; iy++) {
+                    const int c = ix * ORBG_GRID_ROWS + iy;
+                    // after the scatter cstart[c] = end of cell c: the start is cstart[c - 1]
+                    const int j0 = c ? cstart[c - 1] : 0, j1 = cstart[c];
+                    for (int j = j0; j < j1; j++) {
+                        const FuseKey e = keys[j];
+                        if (!(fabsf(e.x - u) < r && fabsf(e.y - v) < r)) continue;
+                        const int kl = e.io & 15, idx = e.io >> 4;
+                        if (kl < lvl - 1 || kl > lvl) continue;
+                        const float kr = K.uright ? K.uright[(size_t)kf * cap + idx] : -1.0f;
+                        if (kr >= 0) {
+                            const float ex = u - e.x, ey = v - e.y, er = ur - kr;
+                            const float e2 = ex * ex + ey * ey + er * er;
+                            if ((double)(e2 * T.inv_sigma2[kl]) > 7.8) continue;
+                        } else {
+                            const float ex = u - e.x, ey = v - e.y;
+                            const float e2 = ex * ex + ey * ey;
+                            if ((double)(e2 * T.inv_sigma2[kl]) > 5.99) continue;
+                        }
+                        const uint4 *kd = (const uint4 *)(K.desc + ((size_t)kf * cap + idx) * 32);
+                        const uint4 a = kd[0], b = kd[1];
+                        const int d = __popc(q[0] ^ a.x) + __popc(q[1] ^ a.y) + __popc(q[2] ^ a.z) +
+                                      __popc(q[3] ^ a.w) + __popc(q[4] ^ b.x) + __popc(q[5] ^ b.y) +
+                                      __popc(q[6] ^ b.z) + __popc(q[7] ^ b.w);
+                        const unsigned long long key = ((unsigned long long)d << 40) |
+                                                       ((unsigned long long)c << 20) | (unsigned)idx;
+                        best = key < best ? key : best;
+                    }
+                }
+            if (best == ~0ull) break;
+            bdist = (int)(best >> 40);
+            if (bdist <= TM_TH_LOW) {
+                bidx = (int)(best & 0xFFFFFu);
+                fused++;
+            }
+        } while (0);
+        best_idx[o] = bidx;
+        best_dist[o] = bdist;
+    }
+    if (fused) atomicAdd(&nf_total, fused);
+    __syncthreads();
+    if (tid == 0) nfused[p] = nf_total;
+}
+
+int launch_fuse(hipStream_t st, const orbg_keyframes &K, int cap, const int32_t *kf,
+                const orbg_frustum_camera *cams, const orbg_map_point *mps, const uint8_t *mdesc,
+                const int32_t *mcounts, int mcap, int npairs, float th, const float *scale,
+                const float *inv_sigma2, int nlevels, int32_t *best_idx, int32_t *best_dist,
+                int32_t *nfused)
+{
+    if (npairs <= 0) return 0;
+    if (cap > 8192) return -95;  // the grid's entries in LDS
+    FuseTables T{};
+    for (int l = 0; l < ORBG_MAX_LEVELS; l++) {
+        const int s = l < nlevels ? l : nlevels - 1;
+        T.scale[l] = scale[s];
+        T.inv_sigma2[l] = inv_sigma2[s];
+    }
+    const size_t lds = (FU_CELLS + 4) * 4 + (size_t)cap * sizeof(FuseKey);
+    if (lds > 64 * 1024 &&
+        hipFuncSetAttribute((const void *)k_fuse, hipFuncAttributeMaxDynamicSharedMemorySize,
+                            (int)lds) != hipSuccess)
+        return -5;
+    hipLaunchKernelGGL(k_fuse, dim3(npairs), dim3(256), lds, st, K, cap, kf, cams, mps, mdesc,
+                       mcounts, mcap, th, T, best_idx, best_dist, nfused);
+    return hipGetLastError() == hipSuccess ? 0 : -5;
+}
+
+int launch_tri_match(hipStream_t st, const orbg_keyframes &K, int cap, const int32_t *kf1,
+                     const int32_t *kf2, const orbg_triangulation_pair *geo, int npairs,
+                     const float *scale, const float *sigma2, int nlevels, int only_stereo,
+                     int check_ori, int32_t *match, int32_t *nmatch)
+{
+    if (npairs <= 0) return 0;
+    if (cap > 65535) return -95;  // positions in the key's low 16 bits
+    TriTables T{};
+    for (int l = 0; l < ORBG_MAX_LEVELS; l++) {
+        const int s = l < nlevels ? l : nlevels - 1;
+        T.scale[l] = scale[s];
+        T.epi_th[l] = 3.84 * (double)sigma2[s];
+    }
+    hipLaunchKernelGGL(k_tri_match, dim3(npairs), dim3(256), 0, st, K, cap, kf1, kf2, geo, T,
+                       only_stereo, check_ori, match, nmatch);
+    return hipGetLastError() == hipSuccess ? 0 : -5;
+}
+
+}  // namespace orbg

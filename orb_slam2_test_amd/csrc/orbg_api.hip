@@ -76,6 +76,15 @@ int launch_undistort(hipStream_t st, const orbg_camera &cam, const orbg_keypoint
 int launch_frustum(hipStream_t st, const orbg_frustum_camera *cams, const orbg_map_point *mps,
                    const int32_t *counts, int cap, int nframes, float cos_limit,
                    orbg_map_projection *out, int32_t *nvisible);
+int launch_tri_match(hipStream_t st, const orbg_keyframes &K, int cap, const int32_t *kf1,
+                     const int32_t *kf2, const orbg_triangulation_pair *geo, int npairs,
+                     const float *scale, const float *sigma2, int nlevels, int only_stereo,
+                     int check_ori, int32_t *match, int32_t *nmatch);
+int launch_fuse(hipStream_t st, const orbg_keyframes &K, int cap, const int32_t *kf,
+                const orbg_frustum_camera *cams, const orbg_map_point *mps, const uint8_t *mdesc,
+                const int32_t *mcounts, int mcap, int npairs, float th, const float *scale,
+                const float *inv_sigma2, int nlevels, int32_t *best_idx, int32_t *best_dist,
+                int32_t *nfused);
 int launch_distinctive(hipStream_t st, const uint8_t *pool, const int32_t *rows,
                        const int32_t *off, int npoints, int32_t *best, uint8_t *desc_out);
 int launch_pose_opt(hipStream_t st, const orbg_pose_edge *edges, const int32_t *counts, int cap,
@@ -4018,5 +4027,207 @@ extern "C" int orbg_distinctive_descriptor(orbg_ctx *c, const uint8_t *desc, int
     HIPCHK(hipMemcpyAsync(hs + o_b, db + o_b, 4, hipMemcpyDeviceToHost, c->stream));
     HIPCHK(hipStreamSynchronize(c->stream));
     memcpy(best, hs + o_b, 4);
+    return ORBG_OK;
+}
+
+// ---------------------------------------------------------------------------
+// LocalMapping matchers (mapping_kernels.hip)
+// ---------------------------------------------------------------------------
+extern "C" int orbg_search_for_triangulation_batch_device(
+    orbg_ctx *c, const orbg_keyframes *kfs, int cap, const int32_t *d_kf1, const int32_t *d_kf2,
+    const orbg_triangulation_pair *d_geo, int npairs, int only_stereo, int check_ori,
+    int32_t *d_matches12, int32_t *d_nmatches)
+{
+    if (!c || !kfs) return set_err(ORBG_EINVAL, "NULL argument");
+    if (npairs < 0 || cap <= 0) return set_err(ORBG_EINVAL, "bad npairs / cap");
+    if (npairs == 0) return ORBG_OK;
+    if (!d_kf1 || !d_kf2 || !d_geo || !d_matches12 || !d_nmatches || !kfs->desc || !kfs->kps ||
+        !kfs->counts || !kfs->fv_nodes || !kfs->fv_off || !kfs->fv_feats || !kfs->nfv)
+        return set_err(ORBG_EINVAL, "NULL device array");
+    HIPCHK(hipSetDevice(c->device));
+    hipStream_t st = c->stream;
+    int rc = 0;
+    PROF_LAUNCH(c, "tri_match",
+                rc = launch_tri_match(st, *kfs, cap, d_kf1, d_kf2, d_geo, npairs, c->scale,
+                                      c->sigma2, c->p.nlevels, only_stereo, check_ori,
+                                      d_matches12, d_nmatches));
+    if (rc == -95) return set_err(ORBG_ENOTSUP, "SearchForTriangulation: more than 65535 features");
+    if (rc) return set_err(ORBG_EIO, "k_tri_match launch failed");
+    return ORBG_OK;
+}
+
+static int kf_check(const orbg_keyframe *k)
+{
+    if (!k || k->n < 0 || k->nfv < 0 || k->nfv > std::max(k->n, 0)) return 0;
+    if (k->n && (!k->kps || !k->desc)) return 0;
+    if (k->nfv && (!k->fv_nodes || !k->fv_off || !k->fv_feats)) return 0;
+    for (int j = 0; j < k->nfv; j++)
+        for (int i = k->fv_off[j]; i < k->fv_off[j + 1]; i++)
+            if (k->fv_feats[i] < 0 || k->fv_feats[i] >= k->n) return 0;
+    for (int i = 0; i < k->n; i++)
+        if (k->kps[i].octave < 0 || k->kps[i].octave >= ORBG_MAX_LEVELS) return 0;
+    return 1;
+}
+
+extern "C" int orbg_search_for_triangulation(orbg_ctx *c, const orbg_keyframe *kf1,
+                                             const orbg_keyframe *kf2,
+                                             const orbg_triangulation_pair *geo, int only_stereo,
+                                             int check_ori, int32_t *matches12, int *nmatches)
+{
+    if (!c || !geo || !nmatches) return set_err(ORBG_EINVAL, "NULL argument");
+    if (!kf_check(kf1) || !kf_check(kf2)) return set_err(ORBG_EINVAL, "bad KeyFrame arrays");
+    if (kf1->n && !matches12) return set_err(ORBG_EINVAL, "NULL matches12");
+    *nmatches = 0;
+    for (int i = 0; i < kf1->n; i++) matches12[i] = -1;
+    if (!kf1->n || !kf2->n || !kf1->nfv || !kf2->nfv) return ORBG_OK;
+    HIPCHK(hipSetDevice(c->device));
+    const int cap = std::max(kf1->n, kf2->n);
+    if (cap > 65535) return set_err(ORBG_ENOTSUP, "more than 65535 features");
+    const size_t cp = (size_t)cap;
+    size_t o = 0;
+    auto take = [&](size_t bytes) {
+        const size_t r = o;
+        o += al256(bytes);
+        return r;
+    };
+    const size_t o_desc = take(2 * cp * 32), o_kps = take(2 * cp * sizeof(orbg_keypoint)),
+                 o_ur = take(2 * cp * 4), o_mp = take(2 * cp), o_cnt = take(8),
+                 o_nodes = take(2 * cp * 4), o_off = take(2 * (cp + 1) * 4),
+                 o_feats = take(2 * cp * 4), o_nfv = take(8), o_idx = take(8),
+                 o_geo = take(sizeof(orbg_triangulation_pair)), o_m = take(cp * 4), o_nm = take(4);
+    uint8_t *hs;
+    int rc = stage(c, o, &hs);
+    if (rc) return rc;
+    void *d;
+    if ((rc = scratch(c, o, &d))) return rc;
+    uint8_t *db = (uint8_t *)d;
+    HIPCHK(hipStreamSynchronize(c->stream));
+    memset(hs, 0, o_m);
+    const orbg_keyframe *ks[2] = {kf1, kf2};
+    for (int s = 0; s < 2; s++) {
+        const orbg_keyframe *k = ks[s];
+        memcpy(hs + o_desc + s * cp * 32, k->desc, (size_t)k->n * 32);
+        memcpy(hs + o_kps + s * cp * sizeof(orbg_keypoint), k->kps, (size_t)k->n * sizeof(orbg_keypoint));
+        float *ur = (float *)(hs + o_ur) + s * cp;
+        for (int i = 0; i < k->n; i++) ur[i] = k->uright ? k->uright[i] : -1.0f;
+        if (k->has_mp) memcpy(hs + o_mp + s * cp, k->has_mp, (size_t)k->n);
+        ((int32_t *)(hs + o_cnt))[s] = k->n;
+        memcpy(hs + o_nodes + s * cp * 4, k->fv_nodes, (size_t)k->nfv * 4);
+        memcpy(hs + o_off + s * (cp + 1) * 4, k->fv_off, (size_t)(k->nfv + 1) * 4);
+        memcpy(hs + o_feats + s * cp * 4, k->fv_feats, (size_t)k->fv_off[k->nfv] * 4);
+        ((int32_t *)(hs + o_nfv))[s] = k->nfv;
+        ((int32_t *)(hs + o_idx))[s] = s;
+    }
+    memcpy(hs + o_geo, geo, sizeof(orbg_triangulation_pair));
+    HIPCHK(hipMemcpyAsync(db, hs, o_m, hipMemcpyHostToDevice, c->stream));
+    orbg_keyframes K{};
+    K.desc = db + o_desc;
+    K.kps = (const orbg_keypoint *)(db + o_kps);
+    K.uright = (const float *)(db + o_ur);
+    K.has_mp = db + o_mp;
+    K.counts = (const int32_t *)(db + o_cnt);
+    K.fv_nodes = (const int32_t *)(db + o_nodes);
+    K.fv_off = (const int32_t *)(db + o_off);
+    K.fv_feats = (const int32_t *)(db + o_feats);
+    K.nfv = (const int32_t *)(db + o_nfv);
+    const int32_t *di = (const int32_t *)(db + o_idx);
+    rc = launch_tri_match(c->stream, K, cap, di, di + 1, (const orbg_triangulation_pair *)(db + o_geo),
+                          1, c->scale, c->sigma2, c->p.nlevels, only_stereo, check_ori,
+                          (int32_t *)(db + o_m), (int32_t *)(db + o_nm));
+    if (rc) return set_err(ORBG_EIO, "k_tri_match launch failed");
+    HIPCHK(hipMemcpyAsync(hs + o_m, db + o_m, o - o_m, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(hipStreamSynchronize(c->stream));
+    memcpy(matches12, hs + o_m, (size_t)kf1->n * 4);
+    memcpy(nmatches, hs + o_nm, 4);
+    return ORBG_OK;
+}
+
+extern "C" int orbg_fuse_batch_device(orbg_ctx *c, const orbg_keyframes *kfs, int cap,
+                                      const int32_t *d_kf, const orbg_frustum_camera *d_cams,
+                                      const orbg_map_point *d_mps, const uint8_t *d_mdesc,
+                                      const int32_t *d_mcounts, int mcap, int npairs, float th,
+                                      int32_t *d_best_idx, int32_t *d_best_dist,
+                                      int32_t *d_nfused)
+{
+    if (!c || !kfs) return set_err(ORBG_EINVAL, "NULL argument");
+    if (npairs < 0 || cap <= 0 || mcap < 0) return set_err(ORBG_EINVAL, "bad sizes");
+    if (npairs == 0 || mcap == 0) return ORBG_OK;
+    if (!d_kf || !d_cams || !d_mps || !d_mdesc || !d_mcounts || !d_best_idx || !d_best_dist ||
+        !d_nfused || !kfs->desc || !kfs->kps || !kfs->counts)
+        return set_err(ORBG_EINVAL, "NULL device array");
+    HIPCHK(hipSetDevice(c->device));
+    hipStream_t st = c->stream;
+    int rc = 0;
+    PROF_LAUNCH(c, "fuse",
+                rc = launch_fuse(st, *kfs, cap, d_kf, d_cams, d_mps, d_mdesc, d_mcounts, mcap,
+                                 npairs, th, c->scale, c->inv_sigma2, c->p.nlevels, d_best_idx,
+                                 d_best_dist, d_nfused));
+    if (rc == -95) return set_err(ORBG_ENOTSUP, "Fuse: more than 8192 keypoints per KeyFrame");
+    if (rc) return set_err(ORBG_EIO, "k_fuse launch failed");
+    return ORBG_OK;
+}
+
+extern "C" int orbg_fuse(orbg_ctx *c, const orbg_keyframe *kf, const orbg_frustum_camera *cam,
+                         const orbg_map_point *mps, const uint8_t *mdesc, int nmp, float th,
+                         int32_t *best_idx, int32_t *best_dist, int *nfused)
+{
+    if (!c || !kf || !cam || !nfused) return set_err(ORBG_EINVAL, "NULL argument");
+    if (nmp < 0 || kf->n < 0) return set_err(ORBG_EINVAL, "negative size");
+    if (kf->n && (!kf->kps || !kf->desc)) return set_err(ORBG_EINVAL, "NULL KeyFrame array");
+    if (nmp && (!mps || !mdesc || !best_idx || !best_dist)) return set_err(ORBG_EINVAL, "NULL array");
+    for (int i = 0; i < kf->n; i++)
+        if (kf->kps[i].octave < 0 || kf->kps[i].octave >= ORBG_MAX_LEVELS)
+            return set_err(ORBG_EINVAL, "keypoint octave out of range");
+    *nfused = 0;
+    if (nmp == 0) return ORBG_OK;
+    HIPCHK(hipSetDevice(c->device));
+    const int cap = std::max(kf->n, 1);
+    if (cap > 8192) return set_err(ORBG_ENOTSUP, "more than 8192 keypoints");
+    const size_t cp = (size_t)cap, nm = (size_t)nmp;
+    size_t o = 0;
+    auto take = [&](size_t bytes) {
+        const size_t r = o;
+        o += al256(bytes);
+        return r;
+    };
+    const size_t o_desc = take(cp * 32), o_kps = take(cp * sizeof(orbg_keypoint)),
+                 o_ur = take(cp * 4), o_cnt = take(4), o_idx = take(4),
+                 o_cam = take(sizeof(orbg_frustum_camera)), o_mp = take(nm * sizeof(orbg_map_point)),
+                 o_md = take(nm * 32), o_mc = take(4), o_bi = take(nm * 4), o_bd = take(nm * 4),
+                 o_nf = take(4);
+    uint8_t *hs;
+    int rc = stage(c, o, &hs);
+    if (rc) return rc;
+    void *d;
+    if ((rc = scratch(c, o, &d))) return rc;
+    uint8_t *db = (uint8_t *)d;
+    HIPCHK(hipStreamSynchronize(c->stream));
+    memcpy(hs + o_desc, kf->desc, (size_t)kf->n * 32);
+    memcpy(hs + o_kps, kf->kps, (size_t)kf->n * sizeof(orbg_keypoint));
+    float *ur = (float *)(hs + o_ur);
+    for (int i = 0; i < kf->n; i++) ur[i] = kf->uright ? kf->uright[i] : -1.0f;
+    ((int32_t *)(hs + o_cnt))[0] = kf->n;
+    ((int32_t *)(hs + o_idx))[0] = 0;
+    memcpy(hs + o_cam, cam, sizeof(orbg_frustum_camera));
+    memcpy(hs + o_mp, mps, nm * sizeof(orbg_map_point));
+    memcpy(hs + o_md, mdesc, nm * 32);
+    ((int32_t *)(hs + o_mc))[0] = nmp;
+    HIPCHK(hipMemcpyAsync(db, hs, o_bi, hipMemcpyHostToDevice, c->stream));
+    orbg_keyframes K{};
+    K.desc = db + o_desc;
+    K.kps = (const orbg_keypoint *)(db + o_kps);
+    K.uright = (const float *)(db + o_ur);
+    K.counts = (const int32_t *)(db + o_cnt);
+    rc = launch_fuse(c->stream, K, cap, (const int32_t *)(db + o_idx),
+                     (const orbg_frustum_camera *)(db + o_cam), (const orbg_map_point *)(db + o_mp),
+                     db + o_md, (const int32_t *)(db + o_mc), nmp, 1, th, c->scale, c->inv_sigma2,
+                     c->p.nlevels, (int32_t *)(db + o_bi), (int32_t *)(db + o_bd),
+                     (int32_t *)(db + o_nf));
+    if (rc) return set_err(ORBG_EIO, "k_fuse launch failed");
+    HIPCHK(hipMemcpyAsync(hs + o_bi, db + o_bi, o - o_bi, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(hipStreamSynchronize(c->stream));
+    memcpy(best_idx, hs + o_bi, nm * 4);
+    memcpy(best_dist, hs + o_bd, nm * 4);
+    memcpy(nfused, hs + o_nf, 4);
     return ORBG_OK;
 }

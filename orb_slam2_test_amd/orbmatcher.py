@@ -8,6 +8,8 @@ Reference: include/ORBmatcher.h:40-193, src/ORBmatcher.cc.
     n, match = m.SearchByProjection(CurrentFrame, LastFrame, th, bMono)   # motion model
     n, match = m.SearchByProjection(F, vpMapPoints, th)                   # local map
     n, match = m.SearchByBoW(pKF, F)                                      # reference KF / reloc
+    n, vMatches12 = m.SearchForTriangulation(pKF1, pKF2, F12, bOnlyStereo) # LocalMapping
+    n, best_idx, best_dist = m.Fuse(pKF, fcam, map_points, map_desc, th)   # its search
 
 ``Frame`` here carries just what the matcher reads from ORB_SLAM2::Frame
 (mvKeysUn, mDescriptors and the image bounds mnMinX/mnMaxX/mnMinY/mnMaxY that define
@@ -61,6 +63,8 @@ class Frame:
     mvKeys: np.ndarray = None
     mFeatVec: tuple = None
     map_valid: np.ndarray = None
+    # SearchForTriangulation: GetMapPoint(i) != NULL, (N,) uint8 or None (none)
+    has_mp: np.ndarray = None
 
     @classmethod
     def from_extraction(cls, keypoints, descriptors, width, height):
@@ -180,3 +184,57 @@ class ORBmatcher:
                 1 if self.mbCheckOrientation else 0, L.ptr(match), C.byref(nm)),
                 "orbg_search_by_projection_lastframe")
         return nm.value, match
+
+    def SearchForTriangulation(self, pKF1, pKF2, geom, bOnlyStereo=False):
+        """ORBmatcher::SearchForTriangulation(pKF1, pKF2, F12, vMatchedPairs, bOnlyStereo)
+        (src/ORBmatcher.cc:779-957).  pKF1 / pKF2: Frames with mvKeysUn, mDescriptors,
+        mFeatVec, mvuRight (None: monocular) and has_mp (GetMapPoint(i) != NULL, None: none);
+        geom: a TRI_GEOM_DTYPE record (F12, pKF1's camera centre, pKF2's pose and
+        intrinsics).  Returns (nmatches, vMatches12); vMatchedPairs = the (i, vMatches12[i])
+        with vMatches12[i] >= 0."""
+        keep = []
+
+        def side(fr):
+            kps = np.ascontiguousarray(fr.mvKeysUn, L.KP_DTYPE)
+            desc = np.ascontiguousarray(fr.mDescriptors, np.uint8)
+            ur = None if fr.mvuRight is None else np.ascontiguousarray(fr.mvuRight, np.float32)
+            mp = None if fr.has_mp is None else np.ascontiguousarray(fr.has_mp, np.uint8)
+            nodes, off, feats = (np.ascontiguousarray(a, np.int32) for a in fr.mFeatVec)
+            keep.extend([kps, desc, ur, mp, nodes, off, feats])
+            return L.KeyFrame(L.ptr(kps), L.ptr(desc), L.ptr(ur), L.ptr(mp), len(kps),
+                              L.ptr(nodes), L.ptr(off), L.ptr(feats), len(nodes))
+
+        a, b = side(pKF1), side(pKF2)
+        g = np.ascontiguousarray(geom, L.TRI_GEOM_DTYPE)
+        m = np.zeros(max(a.n, 1), np.int32)
+        n = C.c_int()
+        L.check(L.lib().orbg_search_for_triangulation(_ctx(self.device).handle, C.byref(a),
+                                                      C.byref(b), L.ptr(g),
+                                                      1 if bOnlyStereo else 0,
+                                                      1 if self.mbCheckOrientation else 0,
+                                                      L.ptr(m), C.byref(n)),
+                "orbg_search_for_triangulation")
+        return n.value, m[:a.n].copy()
+
+    def Fuse(self, pKF, fcam, map_points, map_desc, th=3.0):
+        """ORBmatcher::Fuse(pKF, vpMapPoints, th)'s search (src/ORBmatcher.cc:968-1069):
+        pKF a Frame with mvKeysUn / mDescriptors / mvuRight, fcam its FRUSTUM_DTYPE state
+        (pose, intrinsics, mbf, mfLogScaleFactor, mnScaleLevels, bounds), map_points
+        MAPPOINT_DTYPE records (flags MP_VALID = pMP && !isBad() && !IsInKeyFrame(pKF)) with
+        map_desc their descriptors.  Returns (nfused, best_idx, best_dist): the reference
+        fuses point i with pKF's feature best_idx[i] (>= 0); the Replace / AddObservation
+        update is the caller's, in vpMapPoints order."""
+        kps = np.ascontiguousarray(pKF.mvKeysUn, L.KP_DTYPE)
+        desc = np.ascontiguousarray(pKF.mDescriptors, np.uint8)
+        ur = None if pKF.mvuRight is None else np.ascontiguousarray(pKF.mvuRight, np.float32)
+        kf = L.KeyFrame(L.ptr(kps), L.ptr(desc), L.ptr(ur), None, len(kps), None, None, None, 0)
+        fc = np.ascontiguousarray(fcam, L.FRUSTUM_DTYPE)
+        mps = np.ascontiguousarray(map_points, L.MAPPOINT_DTYPE)
+        md = np.ascontiguousarray(map_desc, np.uint8).reshape(-1, 32)
+        bi = np.zeros(max(len(mps), 1), np.int32)
+        bd = np.zeros(max(len(mps), 1), np.int32)
+        n = C.c_int()
+        L.check(L.lib().orbg_fuse(_ctx(self.device).handle, C.byref(kf), L.ptr(fc), L.ptr(mps),
+                                  L.ptr(md), len(mps), float(th), L.ptr(bi), L.ptr(bd),
+                                  C.byref(n)), "orbg_fuse")
+        return n.value, bi[:len(mps)].copy(), bd[:len(mps)].copy()

@@ -1,0 +1,150 @@
+"""GPU: ORBmatcher::SearchForTriangulation (src/ORBmatcher.cc:779-957; LocalMapping::
+CreateNewMapPoints, LocalMapping.cc:305-378) through the C ABI (k_tri_match,
+csrc/mapping_kernels.hip) vs the CPU oracle (oracle/mapping_oracle.c, pinned against a
+pure-Python restatement in tests/test_oracle_mapping.py), bit for bit: vMatches12 and nmatches.
+
+Cases: generated KeyFrame pairs (two cameras over one point set, F12 as ComputeF12) with
+bOnlyStereo / checkOri both ways; KF2 features on the epipole of a forward motion (the
+monocular epipole test); few large nodes (> 128 candidates: the kernel's re-read path); more
+than 1024 nodes (several join passes); empty KeyFrames; and the batched device entry over a
+set of KeyFrames, each paired with several neighbours (CreateNewMapPoints' loop).
+"""
+import numpy as np
+import pytest
+
+from orb_slam2_test_amd import _lib as L
+from orb_slam2_test_amd.orbmatcher import Frame, ORBmatcher, _ctx
+
+import test_oracle_mapping as T
+
+pytestmark = pytest.mark.gpu
+
+
+def _frame(kf):
+    return Frame(kf["kps"], kf["desc"], mvuRight=kf.get("uright"), mFeatVec=kf["fv"],
+                 has_mp=kf.get("has_mp"))
+
+
+def _tables(oracle):
+    """mvScaleFactors / mvLevelSigma2 as the ORBextractor ctor builds them (the context's)"""
+    p = oracle.params(nfeatures=2000, scale_factor=1.2, nlevels=8)
+    return (np.array(p.scale[:8], np.float32), np.array(p.sigma2[:8], np.float32))
+
+
+def _check(oracle, kf1, kf2, g, only_stereo, check_ori, min_matches=1):
+    sf, s2 = _tables(oracle)
+    m = ORBmatcher(0.6, check_ori)
+    n, got = m.SearchForTriangulation(_frame(kf1), _frame(kf2), g, only_stereo)
+    rn, ref = oracle.search_for_triangulation(kf1, kf2, g, sf, s2, only_stereo, check_ori)
+    assert n == rn and np.array_equal(got, ref)
+    assert rn >= min_matches
+    return rn
+
+
+@pytest.mark.parametrize("seed", range(4))
+@pytest.mark.parametrize("only_stereo,check_ori", [(False, False), (True, False), (False, True),
+                                                   (True, True)])
+def test_pairs(oracle, seed, only_stereo, check_ori):
+    kf1, kf2, g, _, _ = T.tri_case(L.KP_DTYPE, L.TRI_GEOM_DTYPE, seed, n=2000,
+                                   forward=seed == 3)
+    _check(oracle, kf1, kf2, g, only_stereo, check_ori, 50)
+
+
+def test_epipole_rejection(oracle):
+    kf1, kf2, g, _, _ = T.tri_case(L.KP_DTYPE, L.TRI_GEOM_DTYPE, 6, n=1500, forward=True)
+    Tm = g["Tcw2"].reshape(3, 4).astype(np.float64)
+    C2 = Tm[:, :3] @ g["Cw1"].astype(np.float64) + Tm[:, 3]
+    ex, ey = 718.856 * C2[0] / C2[2] + 607.1928, 718.856 * C2[1] / C2[2] + 185.2157
+    rng = np.random.default_rng(3)
+    kf2["kps"]["x"][:300] = ex + rng.uniform(-0.3, 0.3, 300)
+    kf2["kps"]["y"][:300] = ey + rng.uniform(-0.3, 0.3, 300)
+    kf2["kps"]["octave"][:300] = rng.integers(5, 8, 300)
+    mono1 = dict(kf1, uright=np.full(1500, -1.0, np.float32))
+    mono2 = dict(kf2, uright=np.full(1500, -1.0, np.float32))
+    nm = _check(oracle, mono1, mono2, g, False, False, 20)
+    ns = _check(oracle, dict(kf1, uright=np.full(1500, 3.0, np.float32)), mono2, g, False, False)
+    assert nm < ns
+
+
+@pytest.mark.parametrize("nnodes", [3, 1500])
+def test_node_sizes(oracle, nnodes):
+    # 3 nodes: ~500 candidates per node (chunks past 128 re-read); 1500 nodes: > 1024 node
+    # join passes
+    kf1, kf2, g, _, _ = T.tri_case(L.KP_DTYPE, L.TRI_GEOM_DTYPE, 11, n=3000, nnodes=nnodes)
+    _check(oracle, kf1, kf2, g, False, True, 20)
+
+
+def test_empty(oracle):
+    kf1, kf2, g, _, _ = T.tri_case(L.KP_DTYPE, L.TRI_GEOM_DTYPE, 1, n=100)
+    e = dict(kps=kf2["kps"][:0], desc=kf2["desc"][:0],
+             fv=(np.zeros(0, np.int32), np.zeros(1, np.int32), np.zeros(0, np.int32)))
+    m = ORBmatcher(0.6, False)
+    n, got = m.SearchForTriangulation(_frame(kf1), _frame(e), g)
+    assert n == 0 and np.all(got == -1) and len(got) == 100
+    n, got = m.SearchForTriangulation(_frame(e), _frame(kf2), g)
+    assert n == 0 and len(got) == 0
+
+
+def test_batch_device(oracle):
+    """5 generated KeyFrame pairs in one orbg_keyframes set (slots 2p, 2p + 1), matched as
+    generated plus the cross pairs (2p, 2p - 1) (CreateNewMapPoints pairs a new KeyFrame with
+    each covisible one; a cross pair finds few matches), all in HBM."""
+    import ctypes as C
+    import torch
+    cap = 2048
+    kfs, pairs, geos = [], [], []
+    for q in range(5):
+        kf1, kf2, g, _, _ = T.tri_case(L.KP_DTYPE, L.TRI_GEOM_DTYPE, 200 + q, n=1200 + 150 * q,
+                                       forward=q == 4)
+        kfs += [kf1, kf2]
+        pairs.append((2 * q, 2 * q + 1))
+        geos.append(g)
+        if q:
+            pairs.append((2 * q, 2 * q - 1))
+            geos.append(g)
+    nk = len(kfs)
+    sf, s2 = _tables(oracle)
+    # device arrays
+    desc = np.zeros((nk, cap, 32), np.uint8)
+    kps = np.zeros((nk, cap), L.KP_DTYPE)
+    ur = np.zeros((nk, cap), np.float32)
+    mp = np.zeros((nk, cap), np.uint8)
+    cnt = np.zeros(nk, np.int32)
+    nodes = np.zeros((nk, cap), np.int32)
+    off = np.zeros((nk, cap + 1), np.int32)
+    feats = np.zeros((nk, cap), np.int32)
+    nfv = np.zeros(nk, np.int32)
+    for k, kf in enumerate(kfs):
+        n = len(kf["kps"])
+        desc[k, :n], kps[k, :n], ur[k, :n], mp[k, :n], cnt[k] = kf["desc"], kf["kps"], kf["uright"], kf["has_mp"], n
+        fn, fo, ff = kf["fv"]
+        nodes[k, :len(fn)], off[k, :len(fo)], feats[k, :len(ff)], nfv[k] = fn, fo, ff, len(fn)
+    dev = {k: torch.from_numpy(np.ascontiguousarray(v).view(np.uint8).reshape(-1).copy()).cuda()
+           for k, v in dict(desc=desc, kps=kps, ur=ur, mp=mp, cnt=cnt, nodes=nodes, off=off,
+                            feats=feats, nfv=nfv).items()}
+    K = L.KeyFrames(dev["desc"].data_ptr(), dev["kps"].data_ptr(), dev["ur"].data_ptr(),
+                    dev["mp"].data_ptr(), dev["cnt"].data_ptr(), dev["nodes"].data_ptr(),
+                    dev["off"].data_ptr(), dev["feats"].data_ptr(), dev["nfv"].data_ptr())
+    P = len(pairs)
+    i1 = torch.tensor([p[0] for p in pairs], dtype=torch.int32, device="cuda")
+    i2 = torch.tensor([p[1] for p in pairs], dtype=torch.int32, device="cuda")
+    G = np.array([g for g in geos], L.TRI_GEOM_DTYPE)
+    dg = torch.from_numpy(G.view(np.uint8).copy()).cuda()
+    dm = torch.full((P * cap,), -9, dtype=torch.int32, device="cuda")
+    dn = torch.zeros(P, dtype=torch.int32, device="cuda")
+    ctx = _ctx()
+    torch.cuda.synchronize()
+    L.check(L.lib().orbg_search_for_triangulation_batch_device(
+        ctx.handle, C.byref(K), cap, i1.data_ptr(), i2.data_ptr(), dg.data_ptr(), P, 0, 1,
+        dm.data_ptr(), dn.data_ptr()), "tri batch")
+    ctx.sync()
+    got = dm.cpu().numpy().reshape(P, cap)
+    gn = dn.cpu().numpy()
+    tot = 0
+    for p, (a, b) in enumerate(pairs):
+        rn, ref = oracle.search_for_triangulation(kfs[a], kfs[b], geos[p], sf, s2, False, True)
+        n1 = len(kfs[a]["kps"])
+        assert gn[p] == rn and np.array_equal(got[p, :n1], ref)
+        assert np.all(got[p, n1:] == -9)  # past N of pKF1: untouched
+        tot += rn
+    assert tot > 0
