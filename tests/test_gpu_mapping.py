@@ -148,3 +148,82 @@ def test_batch_device(oracle):
         assert np.all(got[p, n1:] == -9)  # past N of pKF1: untouched
         tot += rn
     assert tot > 0
+
+
+# ------------------------------------------------------------------------ Fuse
+@pytest.mark.parametrize("seed,th", [(0, 3.0), (1, 3.0), (2, 5.0), (3, 1.0)])
+def test_fuse_search(oracle, seed, th):
+    """ORBmatcher::Fuse(pKF, vpMapPoints, th)'s search (k_fuse) vs the oracle: bestIdx and
+    bestDist of every map point, incl. descriptor ties broken by GetFeaturesInArea's order."""
+    kf, fcam, mps, mdesc = T.fuse_case(L, seed, n=2000, nmp=3000)
+    sf, isg = T._fuse_tables(oracle)
+    m = ORBmatcher(0.6, True)
+    n, bi, bd = m.Fuse(Frame(kf["kps"], kf["desc"], mvuRight=kf["uright"]), fcam, mps, mdesc, th)
+    rn, rbi, rbd = oracle.fuse_search(kf, fcam.view(oracle.FRUSTUM_DTYPE),
+                                      mps.view(oracle.MAPPOINT_DTYPE), mdesc, th, sf, isg)
+    assert n == rn and np.array_equal(bi, rbi) and np.array_equal(bd, rbd)
+    assert rn > 100
+    # monocular KeyFrame (mvuRight all -1): the 5.99 gate only
+    mono = dict(kf, uright=np.full(len(kf["kps"]), -1.0, np.float32))
+    n2, bi2, bd2 = m.Fuse(Frame(mono["kps"], mono["desc"]), fcam, mps, mdesc, th)
+    rn2, rbi2, rbd2 = oracle.fuse_search(mono, fcam.view(oracle.FRUSTUM_DTYPE),
+                                         mps.view(oracle.MAPPOINT_DTYPE), mdesc, th, sf, isg)
+    assert n2 == rn2 and np.array_equal(bi2, rbi2) and np.array_equal(bd2, rbd2)
+
+
+def test_fuse_empty():
+    kf, fcam, mps, mdesc = T.fuse_case(L, 4, n=50, nmp=20)
+    m = ORBmatcher()
+    n, bi, bd = m.Fuse(Frame(kf["kps"], kf["desc"], mvuRight=kf["uright"]), fcam, mps[:0], mdesc[:0])
+    assert n == 0 and len(bi) == 0
+    e = kf["kps"][:0]
+    n, bi, bd = m.Fuse(Frame(e, kf["desc"][:0]), fcam, mps, mdesc)
+    assert n == 0 and np.all(bi == -1) and np.all(bd == 256)
+
+
+def test_fuse_batch_device(oracle):
+    """SearchInNeighbors' shape: one KeyFrame's map points fused into each of 6 neighbours (and
+    back), all in HBM."""
+    import ctypes as C
+    import torch
+    P, cap, mcap = 6, 2500, 2000
+    sf, isg = T._fuse_tables(oracle)
+    cases = [T.fuse_case(L, 40 + p, n=1800 + 100 * (p % 3), nmp=1200 + 150 * p) for p in range(P)]
+    desc = np.zeros((P, cap, 32), np.uint8)
+    kps = np.zeros((P, cap), L.KP_DTYPE)
+    ur = np.zeros((P, cap), np.float32)
+    cnt = np.zeros(P, np.int32)
+    cams = np.zeros(P, L.FRUSTUM_DTYPE)
+    mps = np.zeros((P, mcap), L.MAPPOINT_DTYPE)
+    md = np.zeros((P, mcap, 32), np.uint8)
+    mc = np.zeros(P, np.int32)
+    for p, (kf, fc, mp, mdsc) in enumerate(cases):
+        n = len(kf["kps"])
+        desc[p, :n], kps[p, :n], ur[p, :n], cnt[p] = kf["desc"], kf["kps"], kf["uright"], n
+        cams[p] = fc
+        mps[p, :len(mp)], md[p, :len(mp)], mc[p] = mp, mdsc, len(mp)
+    t = {k: torch.from_numpy(np.ascontiguousarray(v).view(np.uint8).reshape(-1).copy()).cuda()
+         for k, v in dict(desc=desc, kps=kps, ur=ur, cnt=cnt, cams=cams, mps=mps, md=md,
+                          mc=mc).items()}
+    K = L.KeyFrames(t["desc"].data_ptr(), t["kps"].data_ptr(), t["ur"].data_ptr(), None,
+                    t["cnt"].data_ptr(), None, None, None, None)
+    kfi = torch.arange(P, dtype=torch.int32, device="cuda")
+    bi = torch.full((P * mcap,), -9, dtype=torch.int32, device="cuda")
+    bd = torch.full((P * mcap,), -9, dtype=torch.int32, device="cuda")
+    nf = torch.zeros(P, dtype=torch.int32, device="cuda")
+    ctx = _ctx()
+    torch.cuda.synchronize()
+    L.check(L.lib().orbg_fuse_batch_device(ctx.handle, C.byref(K), cap, kfi.data_ptr(),
+                                           t["cams"].data_ptr(), t["mps"].data_ptr(),
+                                           t["md"].data_ptr(), t["mc"].data_ptr(), mcap, P, 3.0,
+                                           bi.data_ptr(), bd.data_ptr(), nf.data_ptr()), "fuse")
+    ctx.sync()
+    gbi = bi.cpu().numpy().reshape(P, mcap)
+    gbd = bd.cpu().numpy().reshape(P, mcap)
+    gnf = nf.cpu().numpy()
+    for p, (kf, fc, mp, mdsc) in enumerate(cases):
+        rn, rbi, rbd = oracle.fuse_search(kf, fc.view(oracle.FRUSTUM_DTYPE),
+                                          mp.view(oracle.MAPPOINT_DTYPE), mdsc, 3.0, sf, isg)
+        k = len(mp)
+        assert gnf[p] == rn and np.array_equal(gbi[p, :k], rbi) and np.array_equal(gbd[p, :k], rbd)
+        assert np.all(gbi[p, k:] == -9)

@@ -245,3 +245,157 @@ def test_triangulation_empty(oracle):
     e = dict(kps=kf2["kps"][:0], desc=kf2["desc"][:0], fv=(np.zeros(0), np.zeros(1), np.zeros(0)))
     n, m = oracle.search_for_triangulation(kf1, e, g, sf, s2)
     assert n == 0 and np.all(m == -1)
+
+
+# ------------------------------------------------------------------------ Fuse
+def fuse_case(mod, seed, n=2000, nmp=1500, w=1241, h=376, ties=True):
+    """A KeyFrame (mvKeysUn, mDescriptors, mvuRight, its FRUSTUM_DTYPE state) and nmp map
+    points: most project next to one of its keypoints with a noisy copy of its descriptor
+    (fusion targets), some carry a descriptor equal to several nearby keypoints' (ties broken
+    by GetFeaturesInArea's order), the rest are far / behind / out of range / unrelated."""
+    rng = np.random.default_rng(seed)
+    fx, fy, cx, cy = KITTI_K
+    R = _rot(rng, 0.2)
+    Ow = rng.uniform(-30, 30, 3)
+    t = -R @ Ow
+    Tcw = np.concatenate([R, t[:, None]], 1).astype(np.float32)
+    p = None
+    sf = (np.float32(1.2) ** np.arange(8)).astype(np.float32)
+    kp = np.zeros(n, mod.KP_DTYPE)
+    kp["x"], kp["y"] = rng.uniform(0, w, n), rng.uniform(0, h, n)
+    kp["octave"] = rng.integers(0, 8, n)
+    kp["angle"], kp["size"], kp["response"] = rng.uniform(0, 360, n), 31, 20
+    desc = rng.integers(0, 256, (n, 32), dtype=np.uint8)
+    z = rng.uniform(3, 50, n)
+    ur = np.where(rng.random(n) < 0.5, kp["x"] - BF / z, -1).astype(np.float32)
+    # map points: seeded from keypoints (true position + noise), some far off
+    src = rng.integers(0, n, nmp)
+    zz = z[src] * rng.uniform(0.97, 1.03, nmp)
+    uu = kp["x"][src] + rng.normal(0, 1.2, nmp) * sf[kp["octave"][src]]
+    vv = kp["y"][src] + rng.normal(0, 1.2, nmp) * sf[kp["octave"][src]]
+    far = rng.random(nmp) < 0.15
+    uu[far] = rng.uniform(-300, w + 300, far.sum())
+    zz[rng.random(nmp) < 0.05] *= -1
+    pc = np.stack([(uu - cx) * zz / fx, (vv - cy) * zz / fy, zz], 1)
+    pw = (R.T @ (pc - t).T).T
+    mps = np.zeros(nmp, mod.MAPPOINT_DTYPE)
+    mps["x"], mps["y"], mps["z"] = pw[:, 0], pw[:, 1], pw[:, 2]
+    d = pw - Ow
+    dist = np.linalg.norm(d, axis=1)
+    nrm = d / dist[:, None] + rng.normal(0, 0.4, (nmp, 3))
+    nrm /= np.linalg.norm(nrm, axis=1, keepdims=True)
+    mps["nx"], mps["ny"], mps["nz"] = nrm[:, 0], nrm[:, 1], nrm[:, 2]
+    # distances consistent with the source keypoint's octave (PredictScale lands near it)
+    lvl = kp["octave"][src]
+    mps["max_dist"] = dist * (np.float32(1.2) ** lvl) * rng.uniform(0.9, 1.1, nmp)
+    mps["min_dist"] = mps["max_dist"] / np.float32(1.2) ** 7 * rng.uniform(0.5, 2.0, nmp)
+    mps["flags"] = np.where(rng.random(nmp) < 0.92, 1, 0)
+    mdesc = desc[src] ^ np.packbits(rng.random((nmp, 256)) < rng.uniform(0.0, 0.25, (nmp, 1)), axis=1)
+    mdesc[rng.random(nmp) < 0.1] = rng.integers(0, 256, 32, dtype=np.uint8)
+    if ties:
+        # clusters of keypoints with one descriptor next to a point: equal distances
+        for j in range(0, min(nmp, 200), 4):
+            s = src[j]
+            near = np.argsort(np.hypot(kp["x"] - kp["x"][s], kp["y"] - kp["y"][s]))[:4]
+            desc[near] = desc[s]
+            kp["octave"][near] = kp["octave"][s]
+            mdesc[j] = desc[s]
+    fcam = np.zeros((), mod.FRUSTUM_DTYPE)
+    fcam["Tcw"] = Tcw.reshape(12)
+    for k, val in zip(("fx", "fy", "cx", "cy", "bf", "log_scale_factor"),
+                      (fx, fy, cx, cy, BF, np.float32(np.log(np.float64(np.float32(1.2)))))):
+        fcam[k] = val
+    fcam["nlevels"] = 8
+    fcam["min_x"], fcam["max_x"], fcam["min_y"], fcam["max_y"] = 0.0, float(w), 0.0, float(h)
+    del p
+    return dict(kps=kp, desc=desc, uright=ur), fcam, mps, mdesc
+
+
+def py_fuse(kf, fcam, mps, mdesc, th, sf, isg):
+    """pure-Python restatement of Fuse's search over the reference grid and order."""
+    f32 = np.float32
+    T = fcam["Tcw"].reshape(3, 4)
+    b = (f32(fcam["min_x"]), f32(fcam["max_x"]), f32(fcam["min_y"]), f32(fcam["max_y"]))
+    iw = f32(64) / f32(b[1] - b[0])
+    ih = f32(48) / f32(b[3] - b[2])
+    kps = kf["kps"]
+    grid = {}
+    for i in range(len(kps)):
+        px = int(np.round(f32(kps["x"][i] - b[0]) * iw))
+        py = int(np.round(f32(kps["y"][i] - b[2]) * ih))
+        if 0 <= px < 64 and 0 <= py < 48:
+            grid.setdefault((px, py), []).append(i)
+    Ow = [f32(sum(float(T[k, r]) * float(T[k, 3]) for k in range(3)) * -1.0) for r in range(3)]
+    bits_k = np.unpackbits(kf["desc"], axis=1)
+    bits_m = np.unpackbits(np.ascontiguousarray(mdesc, np.uint8), axis=1)
+    bi = np.full(len(mps), -1, np.int32)
+    bd = np.full(len(mps), 256, np.int32)
+    for i, mp in enumerate(mps):
+        if not mp["flags"] & 1:
+            continue
+        P = [f32(mp["x"]), f32(mp["y"]), f32(mp["z"])]
+        Pc = [f32(sum(float(T[r, k]) * float(P[k]) for k in range(3)) * 1.0 + float(T[r, 3]))
+              for r in range(3)]
+        if Pc[2] < 0:
+            continue
+        invz = f32(1) / Pc[2]
+        u = f32(fcam["fx"]) * (Pc[0] * invz) + f32(fcam["cx"])
+        v = f32(fcam["fy"]) * (Pc[1] * invz) + f32(fcam["cy"])
+        if not (u >= b[0] and u < b[1] and v >= b[2] and v < b[3]):
+            continue
+        ur = u - f32(fcam["bf"]) * invz
+        PO = [P[k] - Ow[k] for k in range(3)]
+        d3 = f32(np.sqrt(sum(float(x) * float(x) for x in PO)))
+        if d3 < f32(0.8) * mp["min_dist"] or d3 > f32(1.2) * mp["max_dist"]:
+            continue
+        dot = float(PO[0]) * float(mp["nx"]) + float(PO[1]) * float(mp["ny"]) + float(PO[2]) * float(mp["nz"])
+        if dot < 0.5 * float(d3):
+            continue
+        lvl = int(np.ceil(np.log(float(mp["max_dist"] / d3)) / float(fcam["log_scale_factor"])))
+        lvl = min(max(lvl, 0), int(fcam["nlevels"]) - 1)
+        r = f32(th) * sf[lvl]
+        cx0 = max(0, int(np.floor((u - b[0] - r) * iw)))
+        cx1 = min(63, int(np.ceil((u - b[0] + r) * iw)))
+        cy0 = max(0, int(np.floor((v - b[2] - r) * ih)))
+        cy1 = min(47, int(np.ceil((v - b[2] + r) * ih)))
+        if cx0 >= 64 or cx1 < 0 or cy0 >= 48 or cy1 < 0:
+            continue
+        best, bidx = 256, -1
+        for ix in range(cx0, cx1 + 1):
+            for iy in range(cy0, cy1 + 1):
+                for idx in grid.get((ix, iy), []):
+                    k = kps[idx]
+                    if not (abs(f32(k["x"] - u)) < r and abs(f32(k["y"] - v)) < r):
+                        continue
+                    if k["octave"] < lvl - 1 or k["octave"] > lvl:
+                        continue
+                    ex, ey = u - k["x"], v - k["y"]
+                    if kf["uright"][idx] >= 0:
+                        er = ur - kf["uright"][idx]
+                        if float((ex * ex + ey * ey + er * er) * isg[k["octave"]]) > 7.8:
+                            continue
+                    elif float((ex * ex + ey * ey) * isg[k["octave"]]) > 5.99:
+                        continue
+                    dist = int((bits_m[i] != bits_k[idx]).sum())
+                    if dist < best:
+                        best, bidx = dist, idx
+        bd[i] = best
+        if best <= 50:
+            bi[i] = bidx
+    return int((bi >= 0).sum()), bi, bd
+
+
+def _fuse_tables(oracle):
+    p = oracle.params(nfeatures=2000, scale_factor=1.2, nlevels=8)
+    return np.array(p.scale[:8], np.float32), np.array(p.inv_sigma2[:8], np.float32)
+
+
+@pytest.mark.parametrize("seed", range(3))
+def test_fuse_equals_python(oracle, seed):
+    kf, fcam, mps, mdesc = fuse_case(oracle, seed, n=1200, nmp=500)
+    sf, isg = _fuse_tables(oracle)
+    th = 3.0 if seed else 5.0
+    n, bi, bd = oracle.fuse_search(kf, fcam, mps, mdesc, th, sf, isg)
+    rn, rbi, rbd = py_fuse(kf, fcam, mps, mdesc, th, sf, isg)
+    assert n == rn and np.array_equal(bi, rbi) and np.array_equal(bd, rbd)
+    assert n > 50 and (bd < 256).sum() > n  # targets, and candidates past TH_LOW
