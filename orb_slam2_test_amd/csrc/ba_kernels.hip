@@ -427,6 +427,9 @@ __global__ __launch_bounds__(BA_EDGES_TPB) void k_ba_edges(const orbg_pose *__re
 typedef double v4d __attribute__((ext_vector_type(4)));
 
 #define BA_SLICE ORBG_BA_SLICE  // edges per wave
+#ifndef ORBG_BA_POSE_WG
+#define ORBG_BA_POSE_WG 0  // 1: graph path with a workgroup per pose, no partials / reduce launch (measured slower: 0.100 vs 0.073 + 0.011 ms; r04s_ba_pose_wg_ab.txt)
+#endif
 #define BA_ROW 8     // doubles per staged pose row: J_pose (6), -e, w
 
 // One 64-edge slice into LDS rows (lane l: edge l -> rows 3l .. 3l+2: J_pose row, -e, w; zero
@@ -567,8 +570,19 @@ __global__ __launch_bounds__(256) void k_ba_pose_reduce(const orbg_pose *__restr
     if (t >= 42 * npose) return;
     const int p = t / 42, e = t - 42 * p;
     double acc = 0;
-    if (!poses[p].fixed)
-        for (int s = slice_off[p]; s < slice_off[p + 1]; s++) acc += part[42 * (size_t)s + e];
+    if (!poses[p].fixed) {
+        // eight independent loads in flight, added in slice order (the same bits as one by one)
+        const int s1 = slice_off[p + 1];
+        int s = slice_off[p];
+        for (; s + 8 <= s1; s += 8) {
+            double v[8];
+#pragma unroll
+            for (int u = 0; u < 8; u++) v[u] = part[42 * (size_t)(s + u) + e];
+#pragma unroll
+            for (int u = 0; u < 8; u++) acc += v[u];
+        }
+        for (; s < s1; s++) acc += part[42 * (size_t)s + e];
+    }
     const int row = e / 7, col = e - 7 * row;
     if (col < 6)
         hpose[36 * (size_t)p + row * 6 + col] = acc;
@@ -630,7 +644,8 @@ __global__ __launch_bounds__(256) void k_ba_slices_special(
     const int32_t *__restrict__ slice_off, const int32_t *__restrict__ slice_pose, int nslice,
     double *__restrict__ part, const int32_t *__restrict__ point_off,
     const int32_t *__restrict__ point_edges, const int32_t *__restrict__ special, int nsp,
-    int nb_special, double *__restrict__ hpoint, double *__restrict__ bpoint)
+    int nb_special, double *__restrict__ hpoint, double *__restrict__ bpoint, int npose,
+    double *__restrict__ hpose, double *__restrict__ bpose)
 {
     __shared__ double rows_lds[4][3 * BA_SLICE * BA_ROW];  // 12 KB per wave (special: 6 KB)
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
@@ -641,10 +656,48 @@ __global__ __launch_bounds__(256) void k_ba_slices_special(
                          (double(*)[64])rows_lds[wv], lane);
         return;
     }
+#if ORBG_BA_POSE_WG
+    // a workgroup per pose: wave w accumulates the pose's slices w, w + 4, ... in its MFMA
+    // tile, the four tiles are added in wave order through LDS and the block stored -- no
+    // partials, no reduce launch; every pose block written (zero for fixed / edgeless poses)
+    __shared__ double tiles[4][42];
+    const int p = (int)blockIdx.x - nb_special;
+    if (p >= npose) return;  // workgroup-uniform
+    const orbg_pose P = poses[p];
+    v4d C = {0, 0, 0, 0};
+    if (!P.fixed) {
+        const int e0p = pose_off[p], nep = pose_off[p + 1] - e0p;
+        const int ns = (nep + BA_SLICE - 1) / BA_SLICE;
+        for (int ks = wv; ks < ns; ks += 4)
+            ba_pose_slice(P, points, edges, pose_edges, e0p + ks * BA_SLICE,
+                          min(BA_SLICE, nep - ks * BA_SLICE), rows_lds[wv], lane, C);
+    }
+    const int j = lane & 15;
+#pragma unroll
+    for (int v = 0; v < 4; v++) {
+        const int row = (lane >> 4) + 4 * v;
+        if (row < 6 && j < 7) tiles[wv][row * 7 + j] = C[v];
+    }
+    __syncthreads();
+    if (threadIdx.x < 42) {
+        const int e = threadIdx.x;
+        const double acc = ((tiles[0][e] + tiles[1][e]) + tiles[2][e]) + tiles[3][e];
+        const int row = e / 7, col = e - 7 * row;
+        if (col < 6)
+            hpose[36 * (size_t)p + row * 6 + col] = acc;
+        else
+            bpose[6 * (size_t)p + row] = acc;
+    }
+    (void)slice_off;
+    (void)slice_pose;
+    (void)nslice;
+    (void)part;
+#else
     const int sl = ((int)blockIdx.x - nb_special) * 4 + wv;
     if (sl >= nslice) return;
     ba_slice_part(poses, points, edges, pose_off, pose_edges, slice_off, slice_pose, sl, part,
                   rows_lds[wv], lane);
+#endif
 }
 
 // slice -> pose table: pose p owns ceil(edges_p / BA_SLICE) consecutive slices
@@ -814,17 +867,23 @@ int launch_ba_graph(hipStream_t st, const orbg_pose *poses, int npose, const dou
                            st, poses, points, es, nedge, point_off, point_edges, o, hpoint, bpoint);
         prof_end(prof, st, "ba_edges", a);
     }
-    const int nb_special = (gd.nspecial + 3) / 4, nb_slice = npose ? (gd.nslice + 3) / 4 : 0;
+    const int nb_special = (gd.nspecial + 3) / 4;
+#if ORBG_BA_POSE_WG
+    const int nb_slice = npose;  // a workgroup per pose
+#else
+    const int nb_slice = npose ? (gd.nslice + 3) / 4 : 0;
+#endif
     if (nb_special + nb_slice) {
         hipEvent_t a = nullptr;
         prof_begin(prof, st, "ba_pose_mfma", &a);
         hipLaunchKernelGGL(k_ba_slices_special<BaEdgePacked>, dim3(nb_special + nb_slice),
                            dim3(256), 0, st, poses, points, es, pose_off, pose_edges,
                            gd.slice_off, gd.slice_pose, npose ? gd.nslice : 0, gd.part, point_off,
-                           point_edges, gd.special, gd.nspecial, nb_special, hpoint, bpoint);
+                           point_edges, gd.special, gd.nspecial, nb_special, hpoint, bpoint,
+                           npose, hpose, bpose);
         prof_end(prof, st, "ba_pose_mfma", a);
     }
-    if (npose) {
+    if (npose && !ORBG_BA_POSE_WG) {
         hipEvent_t a = nullptr;
         prof_begin(prof, st, "ba_pose_reduce", &a);
         hipLaunchKernelGGL(k_ba_pose_reduce, dim3((42 * npose + 255) / 256), dim3(256), 0, st,
