@@ -513,8 +513,11 @@ int orbg_search_for_triangulation(orbg_ctx *ctx, const orbg_keyframe *kf1, const
  * This is the search: best_idx[i] = the pKF feature the reference fuses point i with, -1 if
  * none; best_dist[i] = bestDist (256: no candidate).  mps[i].flags ORBG_MP_VALID = pMP &&
  * !isBad() && !IsInKeyFrame(pKF) when the call starts; cam = pKF's pose, fx.., mbf,
- * mfLogScaleFactor, mnScaleLevels and mnMinX..; scale factors / inverse sigma^2 are the
- * context's.  One KeyFrame from host arrays (kf->fv_* unused): */
+ * mfLogScaleFactor, mnScaleLevels and the Frame's (float) image bounds the KeyFrame's grid was
+ * built with: the grid and its cell sizes use them, IsInImage and GetFeaturesInArea's cell
+ * range the KeyFrame's int mnMinX .. mnMaxY, their truncation (KeyFrame.h:288-291,
+ * KeyFrame.cc:51).  Scale factors / inverse sigma^2 are the context's.  One KeyFrame from host
+ * arrays (kf->fv_* unused): */
 int orbg_fuse(orbg_ctx *ctx, const orbg_keyframe *kf, const orbg_frustum_camera *cam,
               const orbg_map_point *mps, const uint8_t *mdesc, int nmp, float th,
               int32_t *best_idx, int32_t *best_dist, int *nfused);

@@ -152,8 +152,16 @@ int orc_fuse_search(const orc_tri_kf *kf, const orc_frustum_cam *cam, const orc_
                     const uint8_t *mdesc, int nmp, float th, const float *scale_factors,
                     const float *inv_sigma2, int32_t *best_idx, int32_t *best_dist)
 {
+    /* the KeyFrame's grid is the Frame's (mGrid and mfGridElementWidthInv copied from the
+     * Frame, float bounds), its mnMinX .. mnMaxY are ints (KeyFrame.h:288-291, the Frame's
+     * truncated, KeyFrame.cc:51): IsInImage and GetFeaturesInArea's cell range use those */
     ogrid g;
     orc_grid_build(&g, kf->kps, kf->n, &cam->bounds);
+    ogrid gk = g;
+    const float kminx = (float)(int)cam->bounds.min_x, kmaxx = (float)(int)cam->bounds.max_x;
+    const float kminy = (float)(int)cam->bounds.min_y, kmaxy = (float)(int)cam->bounds.max_y;
+    gk.b.min_x = kminx;
+    gk.b.min_y = kminy;
     int *cand = (int *)malloc(sizeof(int) * (kf->n > 0 ? kf->n : 1));
     const float tcw[3] = {cam->Tcw[3], cam->Tcw[7], cam->Tcw[11]};
     float Ow[3];
@@ -176,8 +184,7 @@ int orc_fuse_search(const orc_tri_kf *kf, const orc_frustum_cam *cam, const orc_
         const float u = cam->fx * x + cam->cx;
         const float v = cam->fy * y + cam->cy;
         /* KeyFrame::IsInImage (KeyFrame.cc:792-795) */
-        if (!(u >= cam->bounds.min_x && u < cam->bounds.max_x && v >= cam->bounds.min_y &&
-              v < cam->bounds.max_y))
+        if (!(u >= kminx && u < kmaxx && v >= kminy && v < kmaxy))
             continue;
         const float ur = u - cam->bf * invz;
         const float maxDistance = 1.2f * mp->max_dist;
@@ -203,7 +210,7 @@ int orc_fuse_search(const orc_tri_kf *kf, const orc_frustum_cam *cam, const orc_
             nPredictedLevel = cam->nlevels - 1;
         const float radius = th * scale_factors[nPredictedLevel];
         /* KeyFrame::GetFeaturesInArea(u, v, radius): Frame's with no level test */
-        const int nc = orc_features_in_area(&g, kf->kps, u, v, radius, -1, -1, cand);
+        const int nc = orc_features_in_area(&gk, kf->kps, u, v, radius, -1, -1, cand);
         if (nc == 0)
             continue;
         const uint8_t *dMP = mdesc + (size_t)i * 32;

@@ -24,6 +24,12 @@
 //   SearchByBoW (KeyFrame, Frame) .... ORBmatcher.cc:195-348 (ORBmatcher.h:57)
 //   DescriptorDistance ............... ORBmatcher.cc:1846-1862 (ORBmatcher.h:128)
 //   PoseOptimization ................. Optimizer.cc:356-631 (include/Optimizer.h:49)
+//   UndistortKeyPoints .............. Frame.cc:542-572 (Frame.h:142)
+//   ComputeImageBounds .............. Frame.cc:575-611
+//   isInFrustum (SearchLocalPoints) . Frame.cc:342-409, Tracking.cc:1676-1691
+//   SearchForTriangulation .......... ORBmatcher.cc:779-957 (ORBmatcher.h:72)
+//   Fuse(pKF, vpMapPoints, th) ...... ORBmatcher.cc:968-1107 (ORBmatcher.h:80)
+//   ComputeDistinctiveDescriptors ... MapPoint.cc:342-420 (the BestIdx over vDescriptors)
 //   LocalBundleAdjustment window ..... Optimizer.cc:633-851: the vertex / edge set g2o builds
 //                                      (LbaWindow), and BlockSolver<6,3>::buildSystem's block
 //                                      layout of the linearised system (block_solver.hpp:
@@ -581,6 +587,282 @@ G2oBlockSystem linearize_lba_window(orbg_ctx *ctx, const Window &w)
             for (int c = 0; c < 3; c++) blk[c * 6 + r] += o.hpl[c][r];
     }
     return g;
+}
+
+// ---------------------------------------------------------------------------
+// Frame geometry
+// ---------------------------------------------------------------------------
+// Frame::mK (3x3 CV_32F) + mDistCoef (4x1 or 5x1 CV_32F) -> orbg_camera
+template <class Mat>
+inline orbg_camera camera_of(const Mat &K, const Mat &D)
+{
+    orbg_camera c;
+    c.fx = K.template at<float>(0, 0);
+    c.fy = K.template at<float>(1, 1);
+    c.cx = K.template at<float>(0, 2);
+    c.cy = K.template at<float>(1, 2);
+    c.k1 = D.template at<float>(0);
+    c.k2 = D.template at<float>(1);
+    c.p1 = D.template at<float>(2);
+    c.p2 = D.template at<float>(3);
+    c.k3 = D.rows * D.cols > 4 ? D.template at<float>(4) : 0.f;
+    return c;
+}
+
+// Frame::UndistortKeyPoints(): F.mvKeysUn from F.mvKeys (k1 == 0: a copy)
+template <class FrameT>
+void UndistortKeyPoints(orbg_ctx *ctx, FrameT &F)
+{
+    if (F.mDistCoef.template at<float>(0) == 0.0) {
+        F.mvKeysUn = F.mvKeys;
+        return;
+    }
+    const orbg_camera cam = camera_of(F.mK, F.mDistCoef);
+    const int n = (int)F.mvKeys.size();
+    std::vector<orbg_keypoint> k = keys_of(F.mvKeys), u(n > 0 ? n : 1);
+    check(orbg_undistort_keypoints(ctx, &cam, k.data(), n, u.data()), "orbg_undistort_keypoints");
+    F.mvKeysUn.resize(n);
+    for (int i = 0; i < n; i++) {
+        auto kp = F.mvKeys[i];
+        kp.pt.x = u[i].x;
+        kp.pt.y = u[i].y;
+        F.mvKeysUn[i] = kp;
+    }
+}
+
+// Frame::ComputeImageBounds(imLeft): the static mnMinX .. mnMaxY
+template <class FrameT, class Mat>
+void ComputeImageBounds(FrameT &F, const Mat &imLeft)
+{
+    const orbg_camera cam = camera_of(F.mK, F.mDistCoef);
+    orbg_bounds b;
+    check(orbg_compute_image_bounds(&cam, imLeft.cols, imLeft.rows, &b), "orbg_compute_image_bounds");
+    FrameT::mnMinX = b.min_x;
+    FrameT::mnMaxX = b.max_x;
+    FrameT::mnMinY = b.min_y;
+    FrameT::mnMaxY = b.max_y;
+}
+
+// The isInFrustum loop of Tracking::SearchLocalPoints (Tracking.cc:1676-1691) over
+// Frame::isInFrustum(pMP, viewingCosLimit): the points not seen by this frame and not bad are
+// tested; mbTrackInView / mTrack* are written as isInFrustum writes them (a point out of view
+// gets mbTrackInView = false only) and IncreaseVisible() is called for those in view.  Returns
+// nToMatch.  PredictScale needs MapPoint::mfMinDistance / mfMaxDistance (protected in
+// MapPoint.h): the drop-in reads them through two getters a maintainer adds beside
+// GetMinDistanceInvariance (GetMinDistance / GetMaxDistance).
+template <class FrameT, class MapPointT>
+int SearchLocalPointsInFrustum(orbg_ctx *ctx, FrameT &F, const std::vector<MapPointT *> &vpLocal,
+                               float viewingCosLimit = 0.5f)
+{
+    const int n = (int)vpLocal.size();
+    std::vector<orbg_map_point> mp(n > 0 ? n : 1);
+    std::vector<orbg_map_projection> pr(n > 0 ? n : 1);
+    for (int i = 0; i < n; i++) {
+        MapPointT *p = vpLocal[i];
+        orbg_map_point &m = mp[i];
+        std::memset(&m, 0, sizeof(m));
+        const bool test = p->mnLastFrameSeen != F.mnId && !p->isBad();
+        if (test) {
+            const auto X = p->GetWorldPos(), Pn = p->GetNormal();
+            m.x = X.template at<float>(0);
+            m.y = X.template at<float>(1);
+            m.z = X.template at<float>(2);
+            m.nx = Pn.template at<float>(0);
+            m.ny = Pn.template at<float>(1);
+            m.nz = Pn.template at<float>(2);
+            m.min_dist = p->GetMinDistance();
+            m.max_dist = p->GetMaxDistance();
+            m.flags = ORBG_MP_VALID;
+        }
+        pr[i] = orbg_map_projection{p->mTrackProjX, p->mTrackProjY, p->mTrackProjXR,
+                                    p->mnTrackScaleLevel, p->mTrackViewCos, 0};
+    }
+    orbg_frustum_camera fc;
+    std::memset(&fc, 0, sizeof(fc));
+    pose12(F.mTcw, fc.Tcw);
+    fc.fx = FrameT::fx;
+    fc.fy = FrameT::fy;
+    fc.cx = FrameT::cx;
+    fc.cy = FrameT::cy;
+    fc.bf = F.mbf;
+    fc.log_scale_factor = F.mfLogScaleFactor;
+    fc.nlevels = F.mnScaleLevels;
+    fc.bounds = bounds_of(F);
+    int nvis = 0;
+    check(orbg_is_in_frustum(ctx, &fc, mp.data(), n, viewingCosLimit, pr.data(), &nvis),
+          "orbg_is_in_frustum");
+    for (int i = 0; i < n; i++) {
+        if (!(mp[i].flags & ORBG_MP_VALID)) continue;  // not tested: untouched
+        MapPointT *p = vpLocal[i];
+        p->mbTrackInView = (pr[i].flags & ORBG_MP_VALID) != 0;
+        if (!p->mbTrackInView) continue;
+        p->mTrackProjX = pr[i].u;
+        p->mTrackProjY = pr[i].v;
+        p->mTrackProjXR = pr[i].ur;
+        p->mnTrackScaleLevel = pr[i].level;
+        p->mTrackViewCos = pr[i].view_cos;
+        p->IncreaseVisible();
+    }
+    return nvis;
+}
+
+// ---------------------------------------------------------------------------
+// LocalMapping matchers
+// ---------------------------------------------------------------------------
+template <class KeyFrameT>
+struct KfArrays {  // one KeyFrame flattened for orbg_keyframe (kept alive by the caller)
+    std::vector<orbg_keypoint> k;
+    std::vector<uint8_t> d, mp;
+    std::vector<float> ur;
+    std::vector<int32_t> nodes, off, feats;
+    orbg_keyframe view(bool with_fv) const
+    {
+        orbg_keyframe v;
+        v.kps = k.data();
+        v.desc = d.data();
+        v.uright = ur.data();
+        v.has_mp = mp.data();
+        v.n = (int32_t)k.size();
+        v.fv_nodes = with_fv ? nodes.data() : nullptr;
+        v.fv_off = with_fv ? off.data() : nullptr;
+        v.fv_feats = with_fv ? feats.data() : nullptr;
+        v.nfv = with_fv ? (int32_t)nodes.size() : 0;
+        return v;
+    }
+};
+
+template <class KeyFrameT>
+KfArrays<KeyFrameT> kf_arrays(KeyFrameT *pKF, bool with_fv)
+{
+    KfArrays<KeyFrameT> a;
+    const int n = (int)pKF->mvKeysUn.size();
+    a.k = keys_of(pKF->mvKeysUn);
+    a.d = rows32(pKF->mDescriptors, n);
+    a.ur.assign(pKF->mvuRight.begin(), pKF->mvuRight.end());
+    a.mp.resize(n);
+    for (int i = 0; i < n; i++) a.mp[i] = pKF->GetMapPoint((size_t)i) != nullptr;
+    if (with_fv) flatten_fv(pKF->mFeatVec, a.nodes, a.off, a.feats);
+    return a;
+}
+
+// ORBmatcher(nnratio, checkOri).SearchForTriangulation(pKF1, pKF2, F12, vMatchedPairs,
+// bOnlyStereo) (LocalMapping::CreateNewMapPoints): both mFeatVec after ComputeBoW.
+template <class KeyFrameT, class Mat>
+int SearchForTriangulation(orbg_ctx *ctx, bool checkOri, KeyFrameT *pKF1, KeyFrameT *pKF2,
+                           const Mat &F12, std::vector<std::pair<size_t, size_t>> &vMatchedPairs,
+                           const bool bOnlyStereo)
+{
+    const KfArrays<KeyFrameT> a1 = kf_arrays(pKF1, true), a2 = kf_arrays(pKF2, true);
+    const orbg_keyframe k1 = a1.view(true), k2 = a2.view(true);
+    orbg_triangulation_pair g;
+    for (int r = 0; r < 3; r++)
+        for (int c = 0; c < 3; c++) g.F12[3 * r + c] = F12.template at<float>(r, c);
+    const auto Cw = pKF1->GetCameraCenter(), R2w = pKF2->GetRotation(), t2w = pKF2->GetTranslation();
+    for (int r = 0; r < 3; r++) {
+        g.Cw1[r] = Cw.template at<float>(r);
+        for (int c = 0; c < 3; c++) g.Tcw2[4 * r + c] = R2w.template at<float>(r, c);
+        g.Tcw2[4 * r + 3] = t2w.template at<float>(r);
+    }
+    g.fx2 = pKF2->fx;
+    g.fy2 = pKF2->fy;
+    g.cx2 = pKF2->cx;
+    g.cy2 = pKF2->cy;
+    std::vector<int32_t> m12(k1.n > 0 ? k1.n : 1);
+    int n = 0;
+    check(orbg_search_for_triangulation(ctx, &k1, &k2, &g, bOnlyStereo ? 1 : 0, checkOri ? 1 : 0,
+                                        m12.data(), &n),
+          "orbg_search_for_triangulation");
+    vMatchedPairs.clear();
+    vMatchedPairs.reserve(n);
+    for (int i = 0; i < k1.n; i++)
+        if (m12[i] >= 0) vMatchedPairs.push_back(std::make_pair((size_t)i, (size_t)m12[i]));
+    return n;
+}
+
+// ORBmatcher::Fuse(pKF, vpMapPoints, th) (LocalMapping::SearchInNeighbors): the per-point
+// search on the device, then the reference's map update in vpMapPoints order, each point
+// re-checked as the reference's loop checks it at that moment (ORBmatcher.cc:986-987) -- an
+// earlier Replace can make a later point bad or put it in pKF.  Returns nFused.  FrameT gives
+// the Frame's static (float) image bounds the KeyFrame's grid was built with (KeyFrame.cc:
+// 35-67 copies mGrid and mfGridElementWidthInv; its int mnMinX .. are their truncation).
+template <class FrameT, class KeyFrameT, class MapPointT>
+int Fuse(orbg_ctx *ctx, KeyFrameT *pKF, const std::vector<MapPointT *> &vpMapPoints,
+         const float th = 3.0f)
+{
+    const int n = (int)vpMapPoints.size();
+    const KfArrays<KeyFrameT> a = kf_arrays(pKF, false);
+    const orbg_keyframe kf = a.view(false);
+    std::vector<orbg_map_point> mp(n > 0 ? n : 1);
+    std::vector<uint8_t> md((size_t)(n > 0 ? n : 1) * 32, 0);
+    for (int i = 0; i < n; i++) {
+        MapPointT *p = vpMapPoints[i];
+        orbg_map_point &m = mp[i];
+        std::memset(&m, 0, sizeof(m));
+        if (!p || p->isBad() || p->IsInKeyFrame(pKF)) continue;
+        const auto X = p->GetWorldPos(), Pn = p->GetNormal();
+        m.x = X.template at<float>(0);
+        m.y = X.template at<float>(1);
+        m.z = X.template at<float>(2);
+        m.nx = Pn.template at<float>(0);
+        m.ny = Pn.template at<float>(1);
+        m.nz = Pn.template at<float>(2);
+        m.min_dist = p->GetMinDistance();
+        m.max_dist = p->GetMaxDistance();
+        m.flags = ORBG_MP_VALID;
+        mp_desc(p, &md[(size_t)i * 32]);
+    }
+    orbg_frustum_camera fc;
+    std::memset(&fc, 0, sizeof(fc));
+    const auto R = pKF->GetRotation(), t = pKF->GetTranslation();
+    for (int r = 0; r < 3; r++) {
+        for (int c = 0; c < 3; c++) fc.Tcw[4 * r + c] = R.template at<float>(r, c);
+        fc.Tcw[4 * r + 3] = t.template at<float>(r);
+    }
+    fc.fx = pKF->fx;
+    fc.fy = pKF->fy;
+    fc.cx = pKF->cx;
+    fc.cy = pKF->cy;
+    fc.bf = pKF->mbf;
+    fc.log_scale_factor = pKF->mfLogScaleFactor;
+    fc.nlevels = pKF->mnScaleLevels;
+    fc.bounds = orbg_bounds{FrameT::mnMinX, FrameT::mnMaxX, FrameT::mnMinY, FrameT::mnMaxY};
+    std::vector<int32_t> best(n > 0 ? n : 1), dist(n > 0 ? n : 1);
+    int ncand = 0;
+    check(orbg_fuse(ctx, &kf, &fc, mp.data(), md.data(), n, th, best.data(), dist.data(), &ncand),
+          "orbg_fuse");
+    int nFused = 0;
+    for (int i = 0; i < n; i++) {
+        MapPointT *pMP = vpMapPoints[i];
+        if (best[i] < 0 || !pMP || pMP->isBad() || pMP->IsInKeyFrame(pKF)) continue;
+        MapPointT *pMPinKF = pKF->GetMapPoint((size_t)best[i]);
+        if (pMPinKF) {
+            if (!pMPinKF->isBad()) {
+                if (pMPinKF->Observations() > pMP->Observations())
+                    pMP->Replace(pMPinKF);
+                else
+                    pMPinKF->Replace(pMP);
+            }
+        } else {
+            pMP->AddObservation(pKF, (size_t)best[i]);
+            pKF->AddMapPoint(pMP, (size_t)best[i]);
+        }
+        nFused++;
+    }
+    return nFused;
+}
+
+// MapPoint::ComputeDistinctiveDescriptors(): BestIdx over the observations' descriptor rows
+// vDescriptors (1 x 32 CV_8U each, in the mObservations order with bad KeyFrames left out);
+// the caller sets mDescriptor = vDescriptors[BestIdx].clone() (-1: none, the reference returns)
+template <class Mat>
+int DistinctiveDescriptorIndex(orbg_ctx *ctx, const std::vector<Mat> &vDescriptors)
+{
+    const int n = (int)vDescriptors.size();
+    std::vector<uint8_t> d((size_t)(n > 0 ? n : 1) * 32);
+    for (int i = 0; i < n; i++) std::memcpy(&d[(size_t)i * 32], vDescriptors[i].template ptr<uint8_t>(0), 32);
+    int32_t best = -1;
+    check(orbg_distinctive_descriptor(ctx, d.data(), n, &best), "orbg_distinctive_descriptor");
+    return best;
 }
 
 }  // namespace ref

@@ -376,6 +376,11 @@ __global__ __launch_bounds__(256) void k_fuse(orbg_keyframes K, int cap,
         keys[slot] = FuseKey{kp.x, kp.y, i << 4 | (kp.octave & 15)};
     }
     __syncthreads();
+    // KeyFrame::mnMinX .. mnMaxY are ints, the Frame's truncated (KeyFrame.h:288-291,
+    // KeyFrame.cc:51): IsInImage and GetFeaturesInArea's cell range use them, the grid (and
+    // its inverse cell sizes) is the Frame's
+    const float kminx = (float)(int)C.bounds.min_x, kmaxx = (float)(int)C.bounds.max_x;
+    const float kminy = (float)(int)C.bounds.min_y, kmaxy = (float)(int)C.bounds.max_y;
     int fused = 0;
     const int nm = mcounts[p];
     const float tcw0 = C.Tcw[3], tcw1 = C.Tcw[7], tcw2 = C.Tcw[11];
@@ -411,9 +416,7 @@ __global__ __launch_bounds__(256) void k_fuse(orbg_keyframes K, int cap,
             const float invz = 1 / Pc[2];
             const float x = Pc[0] * invz, y = Pc[1] * invz;
             const float u = C.fx * x + C.cx, v = C.fy * y + C.cy;
-            if (!(u >= C.bounds.min_x && u < C.bounds.max_x && v >= C.bounds.min_y &&
-                  v < C.bounds.max_y))
-                break;
+            if (!(u >= kminx && u < kmaxx && v >= kminy && v < kmaxy)) break;
             const float ur = u - C.bf * invz;
             const float maxDistance = 1.2f * mp.max_dist, minDistance = 0.8f * mp.min_dist;
             const float PO0 = P[0] - Ow[0], PO1 = P[1] - Ow[1], PO2 = P[2] - Ow[2];
@@ -436,13 +439,13 @@ __global__ __launch_bounds__(256) void k_fuse(orbg_keyframes K, int cap,
                 lvl = C.nlevels - 1;
             const float r = th * T.scale[lvl];
             // GetFeaturesInArea's cells (KeyFrame.cc:755-769)
-            const int cx0 = max(0, (int)floorf((u - C.bounds.min_x - r) * inv_w));
+            const int cx0 = max(0, (int)floorf((u - kminx - r) * inv_w));
             if (cx0 >= ORBG_GRID_COLS) break;
-            const int cx1 = min(ORBG_GRID_COLS - 1, (int)ceilf((u - C.bounds.min_x + r) * inv_w));
+            const int cx1 = min(ORBG_GRID_COLS - 1, (int)ceilf((u - kminx + r) * inv_w));
             if (cx1 < 0) break;
-            const int cy0 = max(0, (int)floorf((v - C.bounds.min_y - r) * inv_h));
+            const int cy0 = max(0, (int)floorf((v - kminy - r) * inv_h));
             if (cy0 >= ORBG_GRID_ROWS) break;
-            const int cy1 = min(ORBG_GRID_ROWS - 1, (int)ceilf((v - C.bounds.min_y + r) * inv_h));
+            const int cy1 = min(ORBG_GRID_ROWS - 1, (int)ceilf((v - kminy + r) * inv_h));
             if (cy1 < 0) break;
             uint32_t q[8];
             {

@@ -13,6 +13,7 @@
 //                                               an independent window and the oracle)
 #include <cmath>
 #include <cstdio>
+#include <algorithm>
 #include <cstring>
 #include <fstream>
 #include <list>
@@ -38,18 +39,29 @@ struct KeyFrame;
 
 struct MapPoint {  // include/MapPoint.h members the hot path reads
     long unsigned int mnId = 0;
-    cv::Mat pos, desc;
+    cv::Mat pos, desc, normal;
     bool bad = false;
     bool mbTrackInView = false;
     float mTrackProjX = 0, mTrackProjY = 0, mTrackProjXR = -1;
     int mnTrackScaleLevel = 0;
     float mTrackViewCos = 1;
+    long unsigned int mnLastFrameSeen = 0;
+    int nvisible = 0;
+    float min_d = 0, max_d = 0;  // mfMinDistance / mfMaxDistance (protected in MapPoint.h)
     std::map<KeyFrame *, size_t> obs;
     cv::Mat GetWorldPos() const { return pos.clone(); }
     cv::Mat GetDescriptor() const { return desc.clone(); }
+    cv::Mat GetNormal() const { return normal.clone(); }
     int Observations() const { return (int)obs.size(); }
     bool isBad() const { return bad; }
     std::map<KeyFrame *, size_t> GetObservations() const { return obs; }
+    // the two getters the isInFrustum / Fuse drop-ins need
+    float GetMinDistance() const { return min_d; }
+    float GetMaxDistance() const { return max_d; }
+    void IncreaseVisible(int n = 1) { nvisible += n; }
+    bool IsInKeyFrame(KeyFrame *k) const { return obs.count(k) != 0; }
+    void AddObservation(KeyFrame *k, size_t idx) { obs[k] = idx; }
+    void Replace(MapPoint *p);  // MapPoint.cc:196-240, below KeyFrame
 };
 
 struct Frame {  // include/Frame.h
@@ -64,6 +76,9 @@ struct Frame {  // include/Frame.h
     float mbf = 0, mb = 0;
     int mnScaleLevels = 8;
     float mfScaleFactor = 1.2f;
+    float mfLogScaleFactor = (float)std::log((double)1.2f);
+    long unsigned int mnId = 0;
+    cv::Mat mK, mDistCoef;
     void SetPose(cv::Mat T) { mTcw = T.clone(); }
 };
 float Frame::fx, Frame::fy, Frame::cx, Frame::cy, Frame::mnMinX, Frame::mnMaxX, Frame::mnMinY,
@@ -78,10 +93,54 @@ struct KeyFrame {  // include/KeyFrame.h
     std::vector<MapPoint *> mvpMapPoints;
     std::map<unsigned int, std::vector<unsigned int>> mFeatVec;  // DBoW2::FeatureVector
     bool bad = false;
+    int mnScaleLevels = 8;
+    float mfLogScaleFactor = (float)std::log((double)1.2f);
+    int mnMinX = 0, mnMinY = 0, mnMaxX = 0, mnMaxY = 0;
     cv::Mat GetPose() const { return Tcw.clone(); }
     std::vector<MapPoint *> GetMapPointMatches() const { return mvpMapPoints; }
     bool isBad() const { return bad; }
+    MapPoint *GetMapPoint(size_t i) const { return mvpMapPoints[i]; }
+    void AddMapPoint(MapPoint *p, size_t i) { mvpMapPoints[i] = p; }
+    cv::Mat GetRotation() const
+    {
+        cv::Mat R(3, 3, CV_32F);
+        for (int r = 0; r < 3; r++)
+            for (int c = 0; c < 3; c++) R.at<float>(r, c) = Tcw.at<float>(r, c);
+        return R;
+    }
+    cv::Mat GetTranslation() const
+    {
+        cv::Mat t(3, 1, CV_32F);
+        for (int r = 0; r < 3; r++) t.at<float>(r) = Tcw.at<float>(r, 3);
+        return t;
+    }
+    cv::Mat GetCameraCenter() const  // Ow = -Rcw^T tcw
+    {
+        cv::Mat O(3, 1, CV_32F);
+        for (int r = 0; r < 3; r++) {
+            double a = 0;
+            for (int k = 0; k < 3; k++) a += (double)Tcw.at<float>(k, r) * Tcw.at<float>(k, 3);
+            O.at<float>(r) = (float)-a;
+        }
+        return O;
+    }
 };
+
+void MapPoint::Replace(MapPoint *p)
+{
+    if (p == this) return;
+    for (auto &o : obs) {
+        KeyFrame *k = o.first;
+        if (!p->IsInKeyFrame(k)) {
+            k->mvpMapPoints[o.second] = p;
+            p->AddObservation(k, o.second);
+        } else {
+            k->mvpMapPoints[o.second] = nullptr;
+        }
+    }
+    obs.clear();
+    bad = true;
+}
 
 static std::vector<uint8_t> read_raw(const char *path, size_t n)
 {
@@ -473,8 +532,255 @@ int main(int argc, char **argv)
         }
     }
 
+    // ---- Frame::UndistortKeyPoints + ComputeImageBounds with TUM1.yaml's camera ----
+    {
+        Frame FU = F1;
+        FU.mK = cv::Mat::eye(3, 3, CV_32F);
+        FU.mK.at<float>(0, 0) = 517.306408f;
+        FU.mK.at<float>(1, 1) = 516.469215f;
+        FU.mK.at<float>(0, 2) = 318.643040f;
+        FU.mK.at<float>(1, 2) = 255.313989f;
+        FU.mDistCoef = cv::Mat(5, 1, CV_32F);
+        const float dc[5] = {0.262383f, -0.953104f, -0.005358f, 0.002628f, 1.163314f};
+        for (int i = 0; i < 5; i++) FU.mDistCoef.at<float>(i) = dc[i];
+        orbg_compat::ref::UndistortKeyPoints(ctx, FU);
+        REQUIRE(FU.mvKeysUn.size() == FU.mvKeys.size());
+        int moved = 0;
+        for (int i = 0; i < FU.N; i++) {
+            REQUIRE(FU.mvKeysUn[i].octave == FU.mvKeys[i].octave && FU.mvKeysUn[i].angle == FU.mvKeys[i].angle);
+            moved += FU.mvKeysUn[i].pt.x != FU.mvKeys[i].pt.x;
+        }
+        REQUIRE(moved > FU.N / 2);
+        const float saved[4] = {Frame::mnMinX, Frame::mnMaxX, Frame::mnMinY, Frame::mnMaxY};
+        cv::Mat im(480, 640, CV_8U);
+        orbg_compat::ref::ComputeImageBounds(FU, im);
+        const float bnd[4] = {Frame::mnMinX, Frame::mnMaxX, Frame::mnMinY, Frame::mnMaxY};
+        REQUIRE(bnd[0] > 0 && bnd[1] < 640 && bnd[2] > 0 && bnd[3] < 480);
+        Frame::mnMinX = saved[0];
+        Frame::mnMaxX = saved[1];
+        Frame::mnMinY = saved[2];
+        Frame::mnMaxY = saved[3];
+        // k1 == 0: a copy (Frame.cc:544-548)
+        Frame FZ = F1;
+        FZ.mK = FU.mK;
+        FZ.mDistCoef = cv::Mat(4, 1, CV_32F);
+        FZ.mvKeysUn.clear();
+        orbg_compat::ref::UndistortKeyPoints(ctx, FZ);
+        REQUIRE(FZ.mvKeysUn.size() == FZ.mvKeys.size() && FZ.mvKeysUn[3].pt.x == FZ.mvKeys[3].pt.x);
+        if (argc >= 6) {
+            const std::string o = argv[5];
+            std::vector<float> kin, kout;
+            for (int i = 0; i < FU.N; i++) {
+                kin.push_back(FU.mvKeys[i].pt.x);
+                kin.push_back(FU.mvKeys[i].pt.y);
+                kout.push_back(FU.mvKeysUn[i].pt.x);
+                kout.push_back(FU.mvKeysUn[i].pt.y);
+            }
+            write_vec(o + "/und_in.f32", kin.data(), kin.size());
+            write_vec(o + "/und_out.f32", kout.data(), kout.size());
+            write_vec(o + "/und_bounds.f32", bnd, 4);
+        }
+    }
+
+    // ---- Tracking::SearchLocalPoints' isInFrustum loop over F2 (identity pose) ----
+    int nfrustum = 0;
+    {
+        std::vector<MapPoint *> local;
+        for (int i = 0; i < F1.N; i++) {
+            MapPoint &mp = mps[i];
+            mp.normal = cv::Mat(3, 1, CV_32F);
+            const float nz = 1.f / std::sqrt(1.f + mp.pos.at<float>(0) * mp.pos.at<float>(0) / 100.f +
+                                              mp.pos.at<float>(1) * mp.pos.at<float>(1) / 100.f);
+            mp.normal.at<float>(0) = mp.pos.at<float>(0) / 10.f * nz;
+            mp.normal.at<float>(1) = mp.pos.at<float>(1) / 10.f * nz;
+            mp.normal.at<float>(2) = nz;
+            // the scale-invariance range of the keypoint's level: ratio 0.97 * 1.2^octave
+            const double dist = std::sqrt((double)mp.pos.at<float>(0) * mp.pos.at<float>(0) +
+                                          (double)mp.pos.at<float>(1) * mp.pos.at<float>(1) + 100.0);
+            mp.max_d = (float)(dist * 0.97 * std::pow(1.2, (double)F1.mvKeysUn[i].octave));
+            mp.min_d = mp.max_d / std::pow(1.2f, 7.f);
+            mp.mnLastFrameSeen = (i % 5 == 0) ? 42 : 0;  // already matched in frame 42
+            mp.mbTrackInView = true;
+            mp.nvisible = 0;
+            local.push_back(&mp);
+        }
+        Frame FL = F2;
+        FL.mnId = 42;
+        FL.mTcw = cv::Mat::eye(4, 4, CV_32F);
+        nfrustum = orbg_compat::ref::SearchLocalPointsInFrustum(ctx, FL, local, 0.5f);
+        int nview = 0;
+        for (int i = 0; i < F1.N; i++) {
+            const MapPoint &mp = mps[i];
+            if (i % 5 == 0) {  // skipped: untouched
+                REQUIRE(mp.mbTrackInView && mp.nvisible == 0);
+                continue;
+            }
+            if (!mp.mbTrackInView) continue;
+            nview++;
+            REQUIRE(mp.nvisible == 1);
+            // the projection of a point back-projected from F1's keypoint at 10 m
+            REQUIRE(std::fabs(mp.mTrackProjX - F1.mvKeysUn[i].pt.x) < 0.01f);
+            REQUIRE(std::fabs(mp.mTrackProjY - F1.mvKeysUn[i].pt.y) < 0.01f);
+            REQUIRE(mp.mnTrackScaleLevel == F1.mvKeysUn[i].octave);
+        }
+        REQUIRE(nview == nfrustum && nfrustum > F1.N / 2);
+    }
+
+    // ---- LocalMapping: SearchForTriangulation(KA, KB) and Fuse(KB, KA's points) ----
+    int ntri = 0, nfused = 0;
+    {
+        auto node_of = [](const cv::KeyPoint &k) {
+            return (unsigned)((int)(k.pt.x / 128) + 16 * (int)(k.pt.y / 64));
+        };
+        KeyFrame KA, KB;
+        for (KeyFrame *k : {&KA, &KB}) {
+            const Frame &Fs = k == &KA ? F1 : F2;
+            k->fx = k->fy = Frame::fx;
+            k->cx = Frame::cx;
+            k->cy = Frame::cy;
+            k->mbf = F1.mbf;
+            k->mvKeysUn = Fs.mvKeysUn;
+            k->mDescriptors = Fs.mDescriptors;
+            k->mvuRight.assign(Fs.N, -1.f);
+            for (int i = 0; i < Fs.N; i += 4) k->mvuRight[i] = Fs.mvKeysUn[i].pt.x - 30.f;
+            k->mvpMapPoints.assign(Fs.N, nullptr);
+            k->mvInvLevelSigma2 = inv2;
+            for (int i = 0; i < Fs.N; i++) k->mFeatVec[node_of(Fs.mvKeysUn[i])].push_back((unsigned)i);
+            k->mnMinX = 0;
+            k->mnMaxX = w;
+            k->mnMinY = 0;
+            k->mnMaxY = h;
+            k->Tcw = cv::Mat::eye(4, 4, CV_32F);
+        }
+        KB.Tcw.at<float>(0, 3) = -0.5f;  // KB half a metre to the right of KA
+        // F12 of the pure x translation (t12 = (0.5, 0, 0), R12 = I): K^-T [t]x K^-1 up to
+        // scale: the epipolar lines are the image rows
+        cv::Mat F12 = cv::Mat(3, 3, CV_32F);
+        const float f = Frame::fx, cy = Frame::cy;
+        const float Fv[9] = {0, 0, 0, 0, 0, -1.f / f, 0, 1.f / f, 0};
+        for (int r = 0; r < 3; r++)
+            for (int c = 0; c < 3; c++) F12.at<float>(r, c) = Fv[3 * r + c];
+        (void)cy;
+        std::vector<std::pair<size_t, size_t>> pairs;
+        ntri = orbg_compat::ref::SearchForTriangulation(ctx, false, &KA, &KB, F12, pairs, false);
+        REQUIRE((int)pairs.size() == ntri);
+        for (size_t i = 1; i < pairs.size(); i++) REQUIRE(pairs[i].first > pairs[i - 1].first);
+        for (auto &pr : pairs) {
+            REQUIRE(node_of(F1.mvKeysUn[pr.first]) == node_of(F2.mvKeysUn[pr.second]));
+            REQUIRE(orbg_descriptor_distance(F1.mDescriptors.ptr<uint8_t>((int)pr.first),
+                                             F2.mDescriptors.ptr<uint8_t>((int)pr.second)) <= 50);
+        }
+        if (argc >= 6) {  // replayed through the oracle by tests/test_compat_ref.py
+            const std::string o = argv[5];
+            std::vector<int32_t> an, ao, af, bn, bo, bf, res;
+            orbg_compat::ref::flatten_fv(KA.mFeatVec, an, ao, af);
+            orbg_compat::ref::flatten_fv(KB.mFeatVec, bn, bo, bf);
+            for (auto &pr : pairs) {
+                res.push_back((int32_t)pr.first);
+                res.push_back((int32_t)pr.second);
+            }
+            write_vec(o + "/tri_an.i32", an.data(), an.size());
+            write_vec(o + "/tri_ao.i32", ao.data(), ao.size());
+            write_vec(o + "/tri_af.i32", af.data(), af.size());
+            write_vec(o + "/tri_bn.i32", bn.data(), bn.size());
+            write_vec(o + "/tri_bo.i32", bo.data(), bo.size());
+            write_vec(o + "/tri_bf.i32", bf.data(), bf.size());
+            write_vec(o + "/tri_aur.f32", KA.mvuRight.data(), KA.mvuRight.size());
+            write_vec(o + "/tri_bur.f32", KB.mvuRight.data(), KB.mvuRight.size());
+            write_vec(o + "/tri_F12.f32", Fv, 9);
+            write_vec(o + "/tri_pairs.i32", res.data(), res.size());
+            const std::vector<orbg_keypoint> ak = orbg_compat::ref::keys_of(KA.mvKeysUn),
+                                             bk = orbg_compat::ref::keys_of(KB.mvKeysUn);
+            write_vec(o + "/tri_akp.bin", ak.data(), ak.size());
+            write_vec(o + "/tri_bkp.bin", bk.data(), bk.size());
+            float geo[28];
+            for (int i = 0; i < 9; i++) geo[i] = Fv[i];
+            const cv::Mat Cw = KA.GetCameraCenter();
+            for (int r = 0; r < 3; r++) geo[9 + r] = Cw.at<float>(r);
+            for (int r = 0; r < 3; r++)
+                for (int c = 0; c < 4; c++) geo[12 + 4 * r + c] = KB.Tcw.at<float>(r, c);
+            geo[24] = KB.fx;
+            geo[25] = KB.fy;
+            geo[26] = KB.cx;
+            geo[27] = KB.cy;
+            write_vec(o + "/tri_geom.f32", geo, 28);
+        }
+        // Fuse KA's map points (F1's keypoints at 10 m, KA = world) into KC, a second KeyFrame
+        // of frame 1 at the same pose: every point projects onto its own keypoint.  Every
+        // third KC feature already holds a point of its own (with two observations: it wins
+        // the Replace), the monocular slots pass the 5.99 gate, the stereo ones (uR 8.6 px
+        // off the projection) fail 7.8
+        KeyFrame KC = KA;
+        KC.mvpMapPoints.assign(F1.N, nullptr);
+        KeyFrame KD = KA;
+        std::vector<MapPoint> own(F1.N);
+        for (int i = 0; i < F1.N; i += 3) {
+            own[i].pos = mps[i].pos.clone();
+            own[i].obs[&KC] = (size_t)i;
+            own[i].obs[&KD] = (size_t)i;
+            KC.mvpMapPoints[i] = &own[i];
+        }
+        std::vector<MapPoint *> vp;
+        for (int i = 0; i < F1.N; i++) {
+            mps[i].obs.clear();
+            mps[i].obs[&KA] = (size_t)i;
+            mps[i].bad = false;
+            vp.push_back(&mps[i]);
+        }
+        vp.push_back(nullptr);        // a NULL entry: skipped
+        vp.push_back(&mps[1]);        // a repeat: in KC after its first fusion, skipped
+        nfused = orbg_compat::ref::Fuse<Frame>(ctx, &KC, vp, 3.0f);
+        int nadd = 0, nrep = 0, nmono = 0;
+        for (int i = 0; i < F1.N; i++) {
+            const bool mono = KC.mvuRight[i] < 0;
+            nmono += mono;
+            const MapPoint &mp = mps[i];
+            if (i % 3 == 0 && mono) {  // own[i] (2 observations) > mps[i] (1): mps[i] replaced
+                REQUIRE(mp.bad && KC.mvpMapPoints[i] == &own[i] && own[i].IsInKeyFrame(&KA));
+                nrep++;
+            } else if (mono) {         // AddObservation + AddMapPoint
+                REQUIRE(!mp.bad && KC.mvpMapPoints[i] == &mps[i] && mp.IsInKeyFrame(&KC));
+                nadd++;
+            } else if (KC.mvKeysUn[i].octave < 7) {
+                // stereo: its own keypoint fails the gate (e2 >= 74 * invSigma2 > 7.8); the
+                // point may still fuse with a neighbour (the same corner a level up / down)
+                REQUIRE(KC.mvpMapPoints[i] != &mps[i]);
+            }
+        }
+        REQUIRE(nfused >= nadd + nrep && nadd > 100 && nrep > 50);
+        for (int i = 0; i < F1.N; i++)  // every KC slot holds a live point or none
+            REQUIRE(!KC.mvpMapPoints[i] || !KC.mvpMapPoints[i]->bad);
+    }
+
+    // ---- MapPoint::ComputeDistinctiveDescriptors' BestIdx ----
+    {
+        std::vector<cv::Mat> vd;
+        for (int i = 0; i < 9; i++) {
+            cv::Mat d(1, 32, CV_8U);
+            std::memcpy(d.data, F1.mDescriptors.ptr<uint8_t>(i % 3 == 0 ? 7 : i), 32);
+            vd.push_back(d);
+        }
+        const int best = orbg_compat::ref::DistinctiveDescriptorIndex(ctx, vd);
+        // brute force: least median of each row's sorted distances, the first row on ties
+        int bm = 1 << 30, bi = -1;
+        for (int i = 0; i < 9; i++) {
+            std::vector<int> row;
+            for (int j = 0; j < 9; j++)
+                row.push_back(orbg_descriptor_distance(vd[i].data, vd[j].data));
+            std::sort(row.begin(), row.end());
+            if (row[4] < bm) {
+                bm = row[4];
+                bi = i;
+            }
+        }
+        REQUIRE(best == bi && best == 0);
+        REQUIRE(orbg_compat::ref::DistinctiveDescriptorIndex(ctx, std::vector<cv::Mat>()) == -1);
+    }
+
     std::printf("compat_ref ok: %d + %d keypoints, SearchForInitialization %d, SearchByProjection %d, "
-                "PoseOptimization inliers %d, LBA edges %zu, chi2 %.6g, SearchByBoW %d\n",
-                F1.N, F2.N, nsfi, nproj, ninl, win.edges.size(), sys.active_robust_chi2, nbow);
+                "PoseOptimization inliers %d, LBA edges %zu, chi2 %.6g, SearchByBoW %d, "
+                "isInFrustum %d, SearchForTriangulation %d, Fuse %d\n",
+                F1.N, F2.N, nsfi, nproj, ninl, win.edges.size(), sys.active_robust_chi2, nbow,
+                nfrustum, ntri, nfused);
     return 0;
 }

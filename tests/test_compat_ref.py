@@ -7,8 +7,10 @@ compiles against tests/compat_stub/ (a test-only stand-in of the cv:: subset the
 CPU: the program and both headers compile (g++ -Wall -Werror).  GPU: it runs on two
 synthetic KITTI-shaped frames and checks the drop-ins against the plain-buffer layer (same
 matches, same prev positions, same H blocks) and the reference's invariants (matched map
-points within TH_HIGH, hessian blocks in vertex-id order), and replays its SearchByBoW call
-through the oracle (every vpMapPointMatches entry and the count).
+points within TH_HIGH, hessian blocks in vertex-id order), and replays its SearchByBoW,
+UndistortKeyPoints / ComputeImageBounds and SearchForTriangulation calls through the oracle;
+the isInFrustum loop of SearchLocalPoints, Fuse with its sequential map update (Replace /
+AddObservation, re-checks) and ComputeDistinctiveDescriptors are checked in the program.
 """
 import os
 import subprocess
@@ -62,6 +64,30 @@ def test_drop_in_layer_runs(tmp_path):
                               fd, rd("bow_fa.f32", np.float32), ffv, nnratio=0.7, check_ori=True)
     assert int(rd("bow_n.i32", np.int32)[0]) == rn
     assert np.array_equal(rd("bow_match.i32", np.int32), ref)
+    # Frame::UndistortKeyPoints / ComputeImageBounds (TUM1.yaml's camera) through the drop-in
+    cam = O.camera(517.306408, 516.469215, 318.643040, 255.313989, 0.262383, -0.953104,
+                   -0.005358, 0.002628, 1.163314)
+    und_in = rd("und_in.f32", np.float32).reshape(-1, 2)
+    assert np.array_equal(rd("und_out.f32", np.float32).reshape(-1, 2),
+                          O.undistort_points(cam, und_in))
+    assert tuple(rd("und_bounds.f32", np.float32)) == O.image_bounds(cam, 640, 480)
+    # SearchForTriangulation(KA, KB, F12) through the drop-in, replayed on its inputs
+    akp, bkp = rd("tri_akp.bin", O.KP_DTYPE), rd("tri_bkp.bin", O.KP_DTYPE)
+    kfa = dict(kps=akp, desc=kd, uright=rd("tri_aur.f32", np.float32),
+               fv=(rd("tri_an.i32", np.int32), rd("tri_ao.i32", np.int32), rd("tri_af.i32", np.int32)))
+    kfb = dict(kps=bkp, desc=fd, uright=rd("tri_bur.f32", np.float32),
+               fv=(rd("tri_bn.i32", np.int32), rd("tri_bo.i32", np.int32), rd("tri_bf.i32", np.int32)))
+    geo = np.zeros((), O.TRI_GEOM_DTYPE)
+    gv = rd("tri_geom.f32", np.float32)
+    geo["F12"], geo["Cw1"], geo["Tcw2"] = gv[:9], gv[9:12], gv[12:24]
+    geo["fx2"], geo["fy2"], geo["cx2"], geo["cy2"] = gv[24:28]
+    p = O.params(nfeatures=2000)
+    tn, tm = O.search_for_triangulation(kfa, kfb, geo, np.array(p.scale[:8], np.float32),
+                                        np.array(p.sigma2[:8], np.float32), False, False)
+    pairs = rd("tri_pairs.i32", np.int32).reshape(-1, 2)
+    assert len(pairs) == tn and tn > 20
+    assert np.array_equal(pairs[:, 0], np.nonzero(tm >= 0)[0])
+    assert np.array_equal(pairs[:, 1], tm[tm >= 0])
 
 
 def _lba_scene(rng):

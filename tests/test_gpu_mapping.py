@@ -171,6 +171,19 @@ def test_fuse_search(oracle, seed, th):
     assert n2 == rn2 and np.array_equal(bi2, rbi2) and np.array_equal(bd2, rbd2)
 
 
+def test_fuse_fractional_bounds(oracle):
+    """a distorted camera's fractional bounds: IsInImage / the cell range on the KeyFrame's int
+    bounds, the grid on the Frame's float ones (KeyFrame.h:288-291)"""
+    b = (10.80118465423584, 1230.0478515625, 14.668615341186523, 370.3118896484375)
+    kf, fcam, mps, mdesc = T.fuse_case(L, 12, n=2000, nmp=3000, bounds=b)
+    sf, isg = T._fuse_tables(oracle)
+    n, bi, bd = ORBmatcher().Fuse(Frame(kf["kps"], kf["desc"], mvuRight=kf["uright"]), fcam, mps,
+                                  mdesc, 3.0)
+    rn, rbi, rbd = oracle.fuse_search(kf, fcam.view(oracle.FRUSTUM_DTYPE),
+                                      mps.view(oracle.MAPPOINT_DTYPE), mdesc, 3.0, sf, isg)
+    assert n == rn and np.array_equal(bi, rbi) and np.array_equal(bd, rbd) and rn > 100
+
+
 def test_fuse_empty():
     kf, fcam, mps, mdesc = T.fuse_case(L, 4, n=50, nmp=20)
     m = ORBmatcher()

@@ -248,7 +248,7 @@ def test_triangulation_empty(oracle):
 
 
 # ------------------------------------------------------------------------ Fuse
-def fuse_case(mod, seed, n=2000, nmp=1500, w=1241, h=376, ties=True):
+def fuse_case(mod, seed, n=2000, nmp=1500, w=1241, h=376, ties=True, bounds=None):
     """A KeyFrame (mvKeysUn, mDescriptors, mvuRight, its FRUSTUM_DTYPE state) and nmp map
     points: most project next to one of its keypoints with a noisy copy of its descriptor
     (fusion targets), some carry a descriptor equal to several nearby keypoints' (ties broken
@@ -306,7 +306,7 @@ def fuse_case(mod, seed, n=2000, nmp=1500, w=1241, h=376, ties=True):
                       (fx, fy, cx, cy, BF, np.float32(np.log(np.float64(np.float32(1.2)))))):
         fcam[k] = val
     fcam["nlevels"] = 8
-    fcam["min_x"], fcam["max_x"], fcam["min_y"], fcam["max_y"] = 0.0, float(w), 0.0, float(h)
+    fcam["min_x"], fcam["max_x"], fcam["min_y"], fcam["max_y"] = bounds or (0.0, float(w), 0.0, float(h))
     del p
     return dict(kps=kp, desc=desc, uright=ur), fcam, mps, mdesc
 
@@ -325,6 +325,7 @@ def py_fuse(kf, fcam, mps, mdesc, th, sf, isg):
         py = int(np.round(f32(kps["y"][i] - b[2]) * ih))
         if 0 <= px < 64 and 0 <= py < 48:
             grid.setdefault((px, py), []).append(i)
+    kb = tuple(f32(int(x)) for x in b)  # KeyFrame's int mnMinX .. (KeyFrame.h:288-291)
     Ow = [f32(sum(float(T[k, r]) * float(T[k, 3]) for k in range(3)) * -1.0) for r in range(3)]
     bits_k = np.unpackbits(kf["desc"], axis=1)
     bits_m = np.unpackbits(np.ascontiguousarray(mdesc, np.uint8), axis=1)
@@ -341,7 +342,7 @@ def py_fuse(kf, fcam, mps, mdesc, th, sf, isg):
         invz = f32(1) / Pc[2]
         u = f32(fcam["fx"]) * (Pc[0] * invz) + f32(fcam["cx"])
         v = f32(fcam["fy"]) * (Pc[1] * invz) + f32(fcam["cy"])
-        if not (u >= b[0] and u < b[1] and v >= b[2] and v < b[3]):
+        if not (u >= kb[0] and u < kb[1] and v >= kb[2] and v < kb[3]):
             continue
         ur = u - f32(fcam["bf"]) * invz
         PO = [P[k] - Ow[k] for k in range(3)]
@@ -354,10 +355,10 @@ def py_fuse(kf, fcam, mps, mdesc, th, sf, isg):
         lvl = int(np.ceil(np.log(float(mp["max_dist"] / d3)) / float(fcam["log_scale_factor"])))
         lvl = min(max(lvl, 0), int(fcam["nlevels"]) - 1)
         r = f32(th) * sf[lvl]
-        cx0 = max(0, int(np.floor((u - b[0] - r) * iw)))
-        cx1 = min(63, int(np.ceil((u - b[0] + r) * iw)))
-        cy0 = max(0, int(np.floor((v - b[2] - r) * ih)))
-        cy1 = min(47, int(np.ceil((v - b[2] + r) * ih)))
+        cx0 = max(0, int(np.floor((u - kb[0] - r) * iw)))
+        cx1 = min(63, int(np.ceil((u - kb[0] + r) * iw)))
+        cy0 = max(0, int(np.floor((v - kb[2] - r) * ih)))
+        cy1 = min(47, int(np.ceil((v - kb[2] + r) * ih)))
         if cx0 >= 64 or cx1 < 0 or cy0 >= 48 or cy1 < 0:
             continue
         best, bidx = 256, -1
@@ -399,3 +400,15 @@ def test_fuse_equals_python(oracle, seed):
     rn, rbi, rbd = py_fuse(kf, fcam, mps, mdesc, th, sf, isg)
     assert n == rn and np.array_equal(bi, rbi) and np.array_equal(bd, rbd)
     assert n > 50 and (bd < 256).sum() > n  # targets, and candidates past TH_LOW
+
+
+def test_fuse_fractional_bounds(oracle):
+    """undistorted-camera bounds (TUM1's, fractional): the KeyFrame tests IsInImage and
+    GetFeaturesInArea's cells against its int mnMinX .. (the Frame's truncated) while its grid
+    is the Frame's float one"""
+    b = (10.80118465423584, 1230.0478515625, 14.668615341186523, 370.3118896484375)
+    kf, fcam, mps, mdesc = fuse_case(oracle, 11, n=1200, nmp=600, bounds=b)
+    sf, isg = _fuse_tables(oracle)
+    n, bi, bd = oracle.fuse_search(kf, fcam, mps, mdesc, 3.0, sf, isg)
+    rn, rbi, rbd = py_fuse(kf, fcam, mps, mdesc, 3.0, sf, isg)
+    assert n == rn and np.array_equal(bi, rbi) and np.array_equal(bd, rbd) and n > 50
