@@ -38,6 +38,8 @@
  *                                     TemplatedVocabulary.h:1126-1189, 1220-1259; Frame.cc:532-539
  *   orbg_search_by_bow .............. ORBmatcher::SearchByBoW(KeyFrame*, Frame&, ...)
  *                                     src/ORBmatcher.cc:195-348 (Tracking.cc:1069, 2009)
+ *   orbg_search_by_bow_kf ........... ORBmatcher::SearchByBoW(KeyFrame*, KeyFrame*, vpMatches12)
+ *                                     src/ORBmatcher.cc:634-769 (LoopClosing.cc:485)
  *   orbg_undistort_keypoints ........ Frame::UndistortKeyPoints  src/Frame.cc:542-572
  *   orbg_compute_image_bounds ....... Frame::ComputeImageBounds  src/Frame.cc:575-611
  *   orbg_is_in_frustum .............. Frame::isInFrustum(pMP, viewingCosLimit)  src/Frame.cc:342-409
@@ -808,6 +810,29 @@ int orbg_search_by_bow(orbg_ctx *ctx, const uint8_t *kf_desc, const float *kf_an
                        const int32_t *f_fv_nodes, const int32_t *f_fv_off,
                        const int32_t *f_fv_feats, int f_nfv, float nnratio, int check_ori,
                        int32_t *match, int *nmatches);
+
+/* ORBmatcher(nnratio, checkOri).SearchByBoW(KeyFrame *pKF1, KeyFrame *pKF2, vpMatches12)
+ * (src/ORBmatcher.cc:634-769; LoopClosing::ComputeSim3, LoopClosing.cc:485): pKF1's features with a good MapPoint
+ * (valid1 = pMP && !isBad(), NULL: all) against pKF2's of the same node with a good MapPoint
+ * (valid2) not yet matched; bestDist1 < TH_LOW (strict, unlike the KeyFrame-Frame form's
+ * <=), the float ratio test, the rotation histogram over mvKeysUn angles.  match12[n1] = the
+ * pKF2 feature matched to pKF1's feature i (vpMatches12[i] = pKF2->GetMapPointMatches()[
+ * match12[i]]), -1 if NULL; *nmatches = the return value.  Host arrays: */
+int orbg_search_by_bow_kf(orbg_ctx *ctx, const uint8_t *desc1, const float *angle1,
+                          const uint8_t *valid1, int n1, const int32_t *fv_nodes1,
+                          const int32_t *fv_off1, const int32_t *fv_feats1, int nfv1,
+                          const uint8_t *desc2, const float *angle2, const uint8_t *valid2,
+                          int n2, const int32_t *fv_nodes2, const int32_t *fv_off2,
+                          const int32_t *fv_feats2, int nfv2, float nnratio, int check_ori,
+                          int32_t *match12, int *nmatches);
+/* Batched, device memory (orbg_bow_frames layout, the .valid arrays of both sides read):
+ * d_match12[p * cap + i] for i < N of pKF1 = d_kf1_index[p]; on the match stream, ordered after
+ * the context stream (as orbg_search_by_bow_batch_device). */
+int orbg_search_by_bow_kf_batch_device(orbg_ctx *ctx, const orbg_bow_frames *kf1,
+                                       const orbg_bow_frames *kf2, int cap,
+                                       const int32_t *d_kf1_index, const int32_t *d_kf2_index,
+                                       int npairs, float nnratio, int check_ori,
+                                       int32_t *d_match12, int32_t *d_nmatch);
 
 #ifdef __cplusplus
 }

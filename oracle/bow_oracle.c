@@ -229,3 +229,81 @@ int orc_search_by_bow(const uint8_t *kf_desc, const float *kf_angle, const uint8
     free(bins);
     return nmatches;
 }
+
+/* ORBmatcher::SearchByBoW(KeyFrame *pKF1, KeyFrame *pKF2, vector<MapPoint*> &vpMatches12)
+ * (src/ORBmatcher.cc:634-769): KF1 features with a good MapPoint (valid1) against the KF2
+ * features of the same node with a good MapPoint (valid2) not yet matched (vbMatched2);
+ * best / second by strict <, accepted when bestDist1 < TH_LOW (strict, unlike the
+ * KeyFrame-Frame form's <=) and the float ratio test; rotation histogram over
+ * mvKeysUn[idx1].angle - mvKeysUn[idx2].angle.  match12[n1] = the KF2 feature matched to KF1
+ * feature i (vpMatches12[i] = vpMapPoints2[match12[i]]), -1 if NULL. */
+int orc_search_by_bow_kf(const uint8_t *desc1, const float *angle1, const uint8_t *valid1,
+                         int n1, const int32_t *nodes1, const int32_t *off1,
+                         const int32_t *feats1, int nfv1, const uint8_t *desc2,
+                         const float *angle2, const uint8_t *valid2, int n2,
+                         const int32_t *nodes2, const int32_t *off2, const int32_t *feats2,
+                         int nfv2, float nnratio, int check_ori, int32_t *match12)
+{
+    for (int i = 0; i < n1; i++) match12[i] = -1;
+    uint8_t *matched2 = (uint8_t *)calloc(n2 > 0 ? n2 : 1, 1);
+    int *bins = (int *)malloc(sizeof(int) * (n1 > 0 ? n1 : 1));
+    int hsize[30] = {0};
+    const float factor = 1.0f / 30;
+    int nmatches = 0;
+    int a = 0, b = 0;
+    while (a < nfv1 && b < nfv2) {
+        if (nodes1[a] == nodes2[b]) {
+            for (int i1 = off1[a]; i1 < off1[a + 1]; i1++) {
+                const int idx1 = feats1[i1];
+                if (!valid1[idx1]) continue;
+                const uint8_t *d1 = desc1 + (size_t)idx1 * 32;
+                int best1 = 256, bestIdx2 = -1, best2 = 256;
+                for (int i2 = off2[b]; i2 < off2[b + 1]; i2++) {
+                    const int idx2 = feats2[i2];
+                    if (matched2[idx2] || !valid2[idx2]) continue;
+                    const int d = orc_descriptor_distance(d1, desc2 + (size_t)idx2 * 32);
+                    if (d < best1) {
+                        best2 = best1;
+                        best1 = d;
+                        bestIdx2 = idx2;
+                    } else if (d < best2) {
+                        best2 = d;
+                    }
+                }
+                if (best1 < BOW_TH_LOW && (float)best1 < nnratio * (float)best2) {
+                    match12[idx1] = bestIdx2;
+                    matched2[bestIdx2] = 1;
+                    if (check_ori) {
+                        float rot = angle1[idx1] - angle2[bestIdx2];
+                        if (rot < 0.0)
+                            rot += 360.0f;
+                        int bin = (int)roundf(rot * factor);
+                        if (bin == 30)
+                            bin = 0;
+                        bins[idx1] = bin;
+                        hsize[bin]++;
+                    }
+                    nmatches++;
+                }
+            }
+            a++;
+            b++;
+        } else if (nodes1[a] < nodes2[b]) {
+            a++;
+        } else {
+            b++;
+        }
+    }
+    if (check_ori) {
+        int ind1 = -1, ind2 = -1, ind3 = -1;
+        orc_three_maxima(hsize, &ind1, &ind2, &ind3);
+        for (int i = 0; i < n1; i++)
+            if (match12[i] >= 0 && bins[i] != ind1 && bins[i] != ind2 && bins[i] != ind3) {
+                match12[i] = -1;
+                nmatches--;
+            }
+    }
+    free(bins);
+    free(matched2);
+    return nmatches;
+}

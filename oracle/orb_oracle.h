@@ -345,6 +345,13 @@ int orc_search_by_bow(const uint8_t *kf_desc, const float *kf_angle, const uint8
                       const float *f_angle, int n_f, const int32_t *f_nodes, const int32_t *f_off,
                       const int32_t *f_feats, int f_nfv, float nnratio, int check_ori,
                       int32_t *match);
+/* ORBmatcher::SearchByBoW(KeyFrame*, KeyFrame*, vpMatches12): match12[n1] = KF2 index or -1 */
+int orc_search_by_bow_kf(const uint8_t *desc1, const float *angle1, const uint8_t *valid1,
+                         int n1, const int32_t *nodes1, const int32_t *off1,
+                         const int32_t *feats1, int nfv1, const uint8_t *desc2,
+                         const float *angle2, const uint8_t *valid2, int n2,
+                         const int32_t *nodes2, const int32_t *off2, const int32_t *feats2,
+                         int nfv2, float nnratio, int check_ori, int32_t *match12);
 void orc_three_maxima(const int *hsize, int *ind1, int *ind2, int *ind3);
 
 /* ---- Frame::ComputeStereoMatches (stereo_oracle.c) ----

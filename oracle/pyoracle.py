@@ -197,6 +197,9 @@ def lib():
         L.orc_search_for_triangulation.restype = C.c_int
         L.orc_fuse_search.argtypes = [P(TriKF), vp, vp, vp, C.c_int, C.c_float, vp, vp, vp, vp]
         L.orc_fuse_search.restype = C.c_int
+        L.orc_search_by_bow_kf.restype = C.c_int
+        L.orc_search_by_bow_kf.argtypes = [vp, vp, vp, C.c_int, vp, vp, vp, C.c_int, vp, vp, vp,
+                                           C.c_int, vp, vp, vp, C.c_int, C.c_float, C.c_int, vp]
         L.orc_undistort_points.argtypes = [vp, vp, C.c_int, vp]
         L.orc_undistort_keypoints.argtypes = [vp, vp, C.c_int, vp]
         L.orc_image_bounds.argtypes = [vp, C.c_int, C.c_int, P(Bounds)]
@@ -612,6 +615,26 @@ def search_by_bow(kf_desc, kf_angle, kf_valid, kf_fv, f_desc, f_angle, f_fv, nnr
                                 _p(fd), _p(fa), len(fd), _p(fn), _p(fo), _p(ffe), len(fn),
                                 float(nnratio), int(bool(check_ori)), _p(match))
     return n, match[:len(fd)].copy()
+
+
+def search_by_bow_kf(desc1, angle1, valid1, fv1, desc2, angle2, valid2, fv2, nnratio=0.75,
+                     check_ori=True):
+    """ORBmatcher::SearchByBoW(KeyFrame*, KeyFrame*, vpMatches12) restated
+    (orc_search_by_bow_kf): valid = pMP && !pMP->isBad() per side (None: all).  Returns
+    (nmatches, match12[n1]) with match12[i] = the KF2 feature matched to KF1 feature i, -1."""
+    d1 = np.ascontiguousarray(desc1, np.uint8).reshape(-1, 32)
+    d2 = np.ascontiguousarray(desc2, np.uint8).reshape(-1, 32)
+    a1 = np.ascontiguousarray(angle1, np.float32)
+    a2 = np.ascontiguousarray(angle2, np.float32)
+    v1 = np.ones(len(d1), np.uint8) if valid1 is None else np.ascontiguousarray(valid1, np.uint8)
+    v2 = np.ones(len(d2), np.uint8) if valid2 is None else np.ascontiguousarray(valid2, np.uint8)
+    n1, o1, f1 = [np.ascontiguousarray(a, np.int32) for a in fv1]
+    n2, o2, f2 = [np.ascontiguousarray(a, np.int32) for a in fv2]
+    m = np.zeros(max(len(d1), 1), np.int32)
+    n = lib().orc_search_by_bow_kf(_p(d1), _p(a1), _p(v1), len(d1), _p(n1), _p(o1), _p(f1),
+                                   len(n1), _p(d2), _p(a2), _p(v2), len(d2), _p(n2), _p(o2),
+                                   _p(f2), len(n2), float(nnratio), int(bool(check_ori)), _p(m))
+    return n, m[:len(d1)].copy()
 
 
 # ---- Frame / MapPoint geometry (frame_oracle.c) ----

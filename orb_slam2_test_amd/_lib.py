@@ -242,6 +242,10 @@ def lib():
                                                 P(i32)]),
         "orbg_search_for_triangulation_batch_device": (i32, [vp, P(KeyFrames), i32, vp, vp, vp,
                                                              i32, i32, i32, vp, vp]),
+        "orbg_search_by_bow_kf": (i32, [vp, vp, vp, vp, i32, vp, vp, vp, i32, vp, vp, vp, i32, vp, vp,
+                                        vp, i32, f32, i32, vp, P(i32)]),
+        "orbg_search_by_bow_kf_batch_device": (i32, [vp, P(BowFrames), P(BowFrames), i32, vp, vp,
+                                                     i32, f32, i32, vp, vp]),
         "orbg_fuse": (i32, [vp, P(KeyFrame), vp, vp, vp, i32, f32, vp, vp, P(i32)]),
         "orbg_fuse_batch_device": (i32, [vp, P(KeyFrames), i32, vp, vp, vp, vp, vp, i32, i32, f32,
                                          vp, vp, vp]),

@@ -22,6 +22,7 @@
 //   SearchByProjection (last frame) .. ORBmatcher.cc:1503-1667 (ORBmatcher.h:62)
 //   SearchByProjection (local map) ... ORBmatcher.cc:59-154 (ORBmatcher.h:51)
 //   SearchByBoW (KeyFrame, Frame) .... ORBmatcher.cc:195-348 (ORBmatcher.h:57)
+//   SearchByBoW (KeyFrame, KeyFrame) . ORBmatcher.cc:634-769 (ORBmatcher.h:58)
 //   DescriptorDistance ............... ORBmatcher.cc:1846-1862 (ORBmatcher.h:128)
 //   PoseOptimization ................. Optimizer.cc:356-631 (include/Optimizer.h:49)
 //   UndistortKeyPoints .............. Frame.cc:542-572 (Frame.h:142)
@@ -337,6 +338,42 @@ int SearchByBoW(orbg_ctx *ctx, float nnratio, bool checkOri, KeyFrameT *pKF, Fra
     vpMapPointMatches.assign(nf, static_cast<MapPointT *>(nullptr));
     for (int i = 0; i < nf; i++)
         if (match[i] >= 0) vpMapPointMatches[i] = vpMPs[match[i]];
+    return nm;
+}
+
+// ORBmatcher(nnratio, checkOri).SearchByBoW(pKF1, pKF2, vpMatches12) (LoopClosing::
+// ComputeSim3, LoopClosing.cc:485): vpMatches12 = pKF1's N entries, pKF2's MapPoint per
+// matched pKF1 feature or NULL.
+template <class KeyFrameT, class MapPointT>
+int SearchByBoW(orbg_ctx *ctx, float nnratio, bool checkOri, KeyFrameT *pKF1, KeyFrameT *pKF2,
+                std::vector<MapPointT *> &vpMatches12)
+{
+    const std::vector<MapPointT *> vp1 = pKF1->GetMapPointMatches(), vp2 = pKF2->GetMapPointMatches();
+    const int n1 = (int)pKF1->mvKeysUn.size(), n2 = (int)pKF2->mvKeysUn.size();
+    std::vector<uint8_t> v1(n1 > 0 ? n1 : 1, 0), v2(n2 > 0 ? n2 : 1, 0);
+    std::vector<float> a1(n1 > 0 ? n1 : 1), a2(n2 > 0 ? n2 : 1);
+    for (int i = 0; i < n1; i++) {
+        v1[i] = vp1[i] && !vp1[i]->isBad();
+        a1[i] = pKF1->mvKeysUn[i].angle;
+    }
+    for (int i = 0; i < n2; i++) {
+        v2[i] = vp2[i] && !vp2[i]->isBad();
+        a2[i] = pKF2->mvKeysUn[i].angle;
+    }
+    std::vector<int32_t> n1v, o1, f1, n2v, o2, f2;
+    flatten_fv(pKF1->mFeatVec, n1v, o1, f1);
+    flatten_fv(pKF2->mFeatVec, n2v, o2, f2);
+    const std::vector<uint8_t> d1 = rows32(pKF1->mDescriptors, n1), d2 = rows32(pKF2->mDescriptors, n2);
+    std::vector<int32_t> m12(n1 > 0 ? n1 : 1);
+    int nm = 0;
+    check(orbg_search_by_bow_kf(ctx, d1.data(), a1.data(), v1.data(), n1, n1v.data(), o1.data(),
+                                f1.data(), (int)n1v.size(), d2.data(), a2.data(), v2.data(), n2,
+                                n2v.data(), o2.data(), f2.data(), (int)n2v.size(), nnratio,
+                                checkOri ? 1 : 0, m12.data(), &nm),
+          "orbg_search_by_bow_kf");
+    vpMatches12.assign(n1, static_cast<MapPointT *>(nullptr));
+    for (int i = 0; i < n1; i++)
+        if (m12[i] >= 0) vpMatches12[i] = vp2[m12[i]];
     return nm;
 }
 

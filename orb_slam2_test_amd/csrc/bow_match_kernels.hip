@@ -1,6 +1,7 @@
 // bow_match_kernels.hip -- k_bow_match: ORBmatcher::SearchByBoW(KeyFrame *pKF, Frame &F,
 // vector<MapPoint*> &vpMapPointMatches) (src/ORBmatcher.cc:195-348) for gfx950, one workgroup
-// per (KF, F) pair.  Callers: Tracking::TrackReferenceKeyFrame (Tracking.cc:1069) and
+// per (KF, F) pair; k_bow_match<true> is the KeyFrame-KeyFrame form SearchByBoW(pKF1, pKF2,
+// vpMatches12) (:634-769: KF2's MapPoint flags, strict < TH_LOW, output at the KF1 index).  Callers: Tracking::TrackReferenceKeyFrame (Tracking.cc:1069) and
 // Tracking::Relocalization (:2009), over the FeatureVectors DBoW2's transform builds
 // (orbg_bow_transform_batch_device, bow_kernels.hip).
 //
@@ -68,6 +69,10 @@ __device__ __forceinline__ int bm_rot_bin(float a_kf, float a_f)
     return bin;
 }
 
+// KFKF: ORBmatcher::SearchByBoW(KeyFrame *pKF1, KeyFrame *pKF2, vpMatches12)
+// (ORBmatcher.cc:634-769) -- K = pKF1, F = pKF2 with its MapPoint flags (F.valid), accepted on
+// bestDist1 < TH_LOW (strict), the match written at the KF1 index (match[idx1] = idx2)
+template <bool KFKF>
 __global__ __launch_bounds__(256) void k_bow_match(BowMatchSide K, BowMatchSide F, int cap,
                                                    const int32_t *__restrict__ kf_index,
                                                    const int32_t *__restrict__ f_index,
@@ -82,6 +87,7 @@ __global__ __launch_bounds__(256) void k_bow_match(BowMatchSide K, BowMatchSide 
     const int kf = kf_index[p], fr = f_index[p];
     const int nk_nodes = K.nfv[kf], nf_nodes = F.nfv[fr];
     const int n_f = F.counts[fr];
+    const int n_out = KFKF ? K.counts[kf] : n_f;  // output rows: KF1 (KFKF) or F features
     const int32_t *kn = K.fv_nodes + (size_t)kf * cap, *ko = K.fv_off + (size_t)kf * (cap + 1),
                   *kfe = K.fv_feats + (size_t)kf * cap;
     const int32_t *fn = F.fv_nodes + (size_t)fr * cap, *fo = F.fv_off + (size_t)fr * (cap + 1),
@@ -89,13 +95,14 @@ __global__ __launch_bounds__(256) void k_bow_match(BowMatchSide K, BowMatchSide 
     const uint8_t *kdesc = K.desc + (size_t)kf * cap * 32, *fdesc = F.desc + (size_t)fr * cap * 32;
     const orbg_keypoint *kkp = K.kps + (size_t)kf * cap, *fkp = F.kps + (size_t)fr * cap;
     const uint8_t *kval = K.valid ? K.valid + (size_t)kf * cap : nullptr;
+    const uint8_t *fval = (KFKF && F.valid) ? F.valid + (size_t)fr * cap : nullptr;
     int32_t *out = match + (size_t)p * cap;
     if (threadIdx.x == 0) {
         nm = 0;
         removed = 0;
     }
     if (threadIdx.x < BM_HISTO) hist[threadIdx.x] = 0;
-    for (int i = threadIdx.x; i < n_f; i += blockDim.x) out[i] = -1;
+    for (int i = threadIdx.x; i < n_out; i += blockDim.x) out[i] = -1;
     int wave_nm = 0;
     // Nodes are independent (a feature sits in one node of its FeatureVector, so two nodes
     // share no candidate and no KeyFrame feature): any node order gives the reference's
@@ -131,6 +138,8 @@ __global__ __launch_bounds__(256) void k_bow_match(BowMatchSide K, BowMatchSide 
         int ci0 = -1, ci1 = -1;
         if (lane < nF) ci0 = ffe[f0 + lane];
         if (lane + 64 < nF) ci1 = ffe[f0 + lane + 64];
+        // KFKF: a KF2 feature without a good MapPoint is no candidate (ORBmatcher.cc:695-699)
+        const bool ok0 = !fval || (ci0 >= 0 && fval[ci0]), ok1 = !fval || (ci1 >= 0 && fval[ci1]);
 #pragma unroll
         for (int w = 0; w < 8; w++) {
             cd0[w] = ci0 >= 0 ? ((const uint32_t *)(fdesc + (size_t)ci0 * 32))[w] : 0u;
@@ -148,6 +157,8 @@ __global__ __launch_bounds__(256) void k_bow_match(BowMatchSide K, BowMatchSide 
             for (int ch = 0; ch < nchunk; ch++) {  // in position order: strict < keeps the first
                 const int pos = ch * 64 + lane;
                 if (pos >= nF || (taken >> ch & 1u)) continue;
+                if (KFKF && fval && !(ch == 0 ? ok0 : ch == 1 ? ok1 : fval[ffe[f0 + pos]] != 0))
+                    continue;
                 unsigned d = 0;
                 if (ch == 0) {
 #pragma unroll
@@ -173,12 +184,16 @@ __global__ __launch_bounds__(256) void k_bow_match(BowMatchSide K, BowMatchSide 
             const unsigned best1 = best >> 16, bpos = best & 0xFFFFu;
             const bool winner = key == best && best1 < 256;
             const unsigned best2 = wave_min_u32(winner ? b2 : b1);
-            if (best1 <= BM_TH_LOW && (float)best1 < nnratio * (float)best2) {
+            if ((KFKF ? best1 < BM_TH_LOW : best1 <= BM_TH_LOW) &&
+                (float)best1 < nnratio * (float)best2) {
                 wave_nm++;
                 if (winner) {
                     taken |= 1ull << (bpos >> 6);
                     const int rf = ffe[f0 + (int)bpos];
-                    out[rf] = rk;
+                    if (KFKF)
+                        out[rk] = rf;
+                    else
+                        out[rf] = rk;
                     if (check_ori) atomicAdd(&hist[bm_rot_bin(kkp[rk].angle, fkp[rf].angle)], 1);
                 }
             }
@@ -223,10 +238,11 @@ __global__ __launch_bounds__(256) void k_bow_match(BowMatchSide K, BowMatchSide 
         }
         __syncthreads();
         int rm = 0;
-        for (int i = threadIdx.x; i < n_f; i += blockDim.x) {
+        for (int i = threadIdx.x; i < n_out; i += blockDim.x) {
             const int m = out[i];
             if (m < 0) continue;
-            const int bin = bm_rot_bin(kkp[m].angle, fkp[i].angle);
+            const int bin = KFKF ? bm_rot_bin(kkp[i].angle, fkp[m].angle)
+                                 : bm_rot_bin(kkp[m].angle, fkp[i].angle);
             if (bin != ind[0] && bin != ind[1] && bin != ind[2]) {
                 out[i] = -1;
                 rm++;
@@ -240,15 +256,20 @@ __global__ __launch_bounds__(256) void k_bow_match(BowMatchSide K, BowMatchSide 
 
 int launch_bow_match(hipStream_t st, const orbg_bow_frames &kf, const orbg_bow_frames &f, int cap,
                      const int32_t *kf_index, const int32_t *f_index, int npairs, float nnratio,
-                     int check_ori, int32_t *match, int32_t *nmatch)
+                     int check_ori, int32_t *match, int32_t *nmatch, bool kfkf)
 {
     if (npairs <= 0) return 0;
     if (cap > BM_MAX_NODE) return -95;  // ORBG_ENOTSUP: a node could exceed the taken mask
     const BowMatchSide K{kf.desc, kf.kps, kf.counts, kf.fv_nodes, kf.fv_off, kf.fv_feats, kf.nfv,
                          kf.valid};
-    const BowMatchSide F{f.desc, f.kps, f.counts, f.fv_nodes, f.fv_off, f.fv_feats, f.nfv, nullptr};
-    hipLaunchKernelGGL(k_bow_match, dim3(npairs), dim3(256), 0, st, K, F, cap, kf_index, f_index,
-                       nnratio, check_ori, match, nmatch);
+    const BowMatchSide F{f.desc, f.kps, f.counts, f.fv_nodes, f.fv_off, f.fv_feats, f.nfv,
+                         kfkf ? f.valid : nullptr};
+    if (kfkf)
+        hipLaunchKernelGGL(k_bow_match<true>, dim3(npairs), dim3(256), 0, st, K, F, cap, kf_index,
+                           f_index, nnratio, check_ori, match, nmatch);
+    else
+        hipLaunchKernelGGL(k_bow_match<false>, dim3(npairs), dim3(256), 0, st, K, F, cap, kf_index,
+                           f_index, nnratio, check_ori, match, nmatch);
     return hipGetLastError() == hipSuccess ? 0 : -5;
 }
 

@@ -109,7 +109,7 @@ int launch_init_match_single(hipStream_t st, const orbg_keypoint *k1, const uint
 // bow_match_kernels.hip
 int launch_bow_match(hipStream_t st, const orbg_bow_frames &kf, const orbg_bow_frames &f, int cap,
                      const int32_t *kf_index, const int32_t *f_index, int npairs, float nnratio,
-                     int check_ori, int32_t *match, int32_t *nmatch);
+                     int check_ori, int32_t *match, int32_t *nmatch, bool kfkf = false);
 // ba_kernels.hip
 int launch_ba(hipStream_t st, const orbg_pose *poses, int npose, const double *points,
               int npoint, const orbg_edge *edges, int nedge, const int32_t *pose_off,
@@ -3686,6 +3686,32 @@ extern "C" int orbg_bow_transform(orbg_ctx *c, const orbg_vocab *v, const uint8_
 // ---------------------------------------------------------------------------
 // ORBmatcher::SearchByBoW(KeyFrame*, Frame&) (bow_match_kernels.hip)
 // ---------------------------------------------------------------------------
+extern "C" int orbg_search_by_bow_kf_batch_device(orbg_ctx *c, const orbg_bow_frames *kf1,
+                                                  const orbg_bow_frames *kf2, int cap,
+                                                  const int32_t *d_kf1_index,
+                                                  const int32_t *d_kf2_index, int npairs,
+                                                  float nnratio, int check_ori,
+                                                  int32_t *d_match12, int32_t *d_nmatch)
+{
+    if (!c || !kf1 || !kf2) return set_err(ORBG_EINVAL, "NULL argument");
+    if (npairs < 0 || cap <= 0 || cap > 8192) return set_err(ORBG_EINVAL, "bad npairs / cap");
+    if (npairs == 0) return ORBG_OK;
+    if (!d_kf1_index || !d_kf2_index || !d_match12 || !d_nmatch || !kf1->desc || !kf1->kps ||
+        !kf1->counts || !kf1->fv_nodes || !kf1->fv_off || !kf1->fv_feats || !kf1->nfv ||
+        !kf2->desc || !kf2->kps || !kf2->fv_nodes || !kf2->fv_off || !kf2->fv_feats || !kf2->nfv)
+        return set_err(ORBG_EINVAL, "NULL device array");
+    HIPCHK(hipSetDevice(c->device));
+    HIPCHK(order_after_caller(c));
+    hipStream_t st = c->mstream;  // PROF_LAUNCH records on `st`
+    int rc = 0;
+    PROF_LAUNCH(c, "bow_match_kf",
+                rc = launch_bow_match(st, *kf1, *kf2, cap, d_kf1_index, d_kf2_index, npairs,
+                                      nnratio, check_ori, d_match12, d_nmatch, true));
+    if (rc == ORBG_ENOTSUP) return set_err(ORBG_ENOTSUP, "SearchByBoW: more than 4096 features per frame");
+    if (rc) return set_err(ORBG_EIO, "k_bow_match launch failed");
+    return ORBG_OK;
+}
+
 extern "C" int orbg_search_by_bow_batch_device(orbg_ctx *c, const orbg_bow_frames *kf,
                                                const orbg_bow_frames *f, int cap,
                                                const int32_t *d_kf_index, const int32_t *d_f_index,
@@ -3711,14 +3737,16 @@ extern "C" int orbg_search_by_bow_batch_device(orbg_ctx *c, const orbg_bow_frame
     return ORBG_OK;
 }
 
-extern "C" int orbg_search_by_bow(orbg_ctx *c, const uint8_t *kf_desc, const float *kf_angle,
+static int search_by_bow_host(orbg_ctx *c, const uint8_t *kf_desc, const float *kf_angle,
                                   const uint8_t *kf_valid, int n_kf, const int32_t *kf_fv_nodes,
                                   const int32_t *kf_fv_off, const int32_t *kf_fv_feats, int kf_nfv,
-                                  const uint8_t *f_desc, const float *f_angle, int n_f,
+                                  const uint8_t *f_desc, const float *f_angle,
+                                  const uint8_t *f_valid, int n_f,
                                   const int32_t *f_fv_nodes, const int32_t *f_fv_off,
                                   const int32_t *f_fv_feats, int f_nfv, float nnratio,
-                                  int check_ori, int32_t *match, int *nmatches)
+                                  int check_ori, int32_t *match, int *nmatches, bool kfkf)
 {
+    const int n_out = kfkf ? n_kf : n_f;  // KeyFrame-KeyFrame: vpMatches12 over pKF1
     if (!c || !match || !nmatches) return set_err(ORBG_EINVAL, "NULL argument");
     if (n_kf < 0 || n_f < 0 || kf_nfv < 0 || f_nfv < 0 || kf_nfv > std::max(n_kf, 0) ||
         f_nfv > std::max(n_f, 0))
@@ -3728,7 +3756,7 @@ extern "C" int orbg_search_by_bow(orbg_ctx *c, const uint8_t *kf_desc, const flo
         (f_nfv && (!f_fv_nodes || !f_fv_off || !f_fv_feats)))
         return set_err(ORBG_EINVAL, "NULL input array");
     *nmatches = 0;
-    for (int i = 0; i < n_f; i++) match[i] = -1;
+    for (int i = 0; i < n_out; i++) match[i] = -1;
     if (!n_f || !n_kf || !kf_nfv || !f_nfv) return ORBG_OK;
     for (int j = 0; j < kf_nfv; j++)
         for (int k = kf_fv_off[j]; k < kf_fv_off[j + 1]; k++)
@@ -3779,6 +3807,10 @@ extern "C" int orbg_search_by_bow(orbg_ctx *c, const uint8_t *kf_desc, const flo
         memcpy(hs + o_val, kf_valid, (size_t)n_kf);
     else
         memset(hs + o_val, 1, (size_t)n_kf);
+    if (f_valid)
+        memcpy(hs + o_val + cp, f_valid, (size_t)n_f);
+    else
+        memset(hs + o_val + cp, 1, (size_t)n_f);
     int32_t *hi = (int32_t *)(hs + o_idx);
     hi[0] = 0;
     hi[1] = 1;
@@ -3794,17 +3826,45 @@ extern "C" int orbg_search_by_bow(orbg_ctx *c, const uint8_t *kf_desc, const flo
     K.fv_off = F.fv_off = (const int32_t *)(db + o_off);
     K.fv_feats = F.fv_feats = (const int32_t *)(db + o_feats);
     K.nfv = F.nfv = (const int32_t *)(db + o_nfv);
-    K.valid = db + o_val;
+    K.valid = F.valid = db + o_val;  // frame 0 (KF / pKF1) and frame 1 (F / pKF2) at + cap
     const int32_t *di = (const int32_t *)(db + o_idx);
     rc = launch_bow_match(c->stream, K, F, cap, di, di + 1, 1, nnratio, check_ori,
-                          (int32_t *)(db + o_match), (int32_t *)(db + o_nm));
+                          (int32_t *)(db + o_match), (int32_t *)(db + o_nm), kfkf);
     if (rc == ORBG_ENOTSUP) return set_err(ORBG_ENOTSUP, "SearchByBoW: more than 4096 features per frame");
     if (rc) return set_err(ORBG_EIO, "k_bow_match launch failed");
     HIPCHK(hipMemcpyAsync(hs + o_match, db + o_match, cp * 4 + 256, hipMemcpyDeviceToHost, c->stream));
     HIPCHK(hipStreamSynchronize(c->stream));
-    memcpy(match, hs + o_match, (size_t)n_f * 4);
+    memcpy(match, hs + o_match, (size_t)n_out * 4);
     memcpy(nmatches, hs + o_nm, 4);
     return ORBG_OK;
+}
+
+extern "C" int orbg_search_by_bow(orbg_ctx *c, const uint8_t *kf_desc, const float *kf_angle,
+                                  const uint8_t *kf_valid, int n_kf, const int32_t *kf_fv_nodes,
+                                  const int32_t *kf_fv_off, const int32_t *kf_fv_feats, int kf_nfv,
+                                  const uint8_t *f_desc, const float *f_angle, int n_f,
+                                  const int32_t *f_fv_nodes, const int32_t *f_fv_off,
+                                  const int32_t *f_fv_feats, int f_nfv, float nnratio,
+                                  int check_ori, int32_t *match, int *nmatches)
+{
+    return search_by_bow_host(c, kf_desc, kf_angle, kf_valid, n_kf, kf_fv_nodes, kf_fv_off,
+                              kf_fv_feats, kf_nfv, f_desc, f_angle, nullptr, n_f, f_fv_nodes,
+                              f_fv_off, f_fv_feats, f_nfv, nnratio, check_ori, match, nmatches,
+                              false);
+}
+
+extern "C" int orbg_search_by_bow_kf(orbg_ctx *c, const uint8_t *desc1, const float *angle1,
+                                     const uint8_t *valid1, int n1, const int32_t *fv_nodes1,
+                                     const int32_t *fv_off1, const int32_t *fv_feats1, int nfv1,
+                                     const uint8_t *desc2, const float *angle2,
+                                     const uint8_t *valid2, int n2, const int32_t *fv_nodes2,
+                                     const int32_t *fv_off2, const int32_t *fv_feats2, int nfv2,
+                                     float nnratio, int check_ori, int32_t *match12,
+                                     int *nmatches)
+{
+    return search_by_bow_host(c, desc1, angle1, valid1, n1, fv_nodes1, fv_off1, fv_feats1, nfv1,
+                              desc2, angle2, valid2, n2, fv_nodes2, fv_off2, fv_feats2, nfv2,
+                              nnratio, check_ori, match12, nmatches, true);
 }
 
 // ---------------------------------------------------------------------------

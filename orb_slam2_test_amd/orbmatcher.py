@@ -8,6 +8,7 @@ Reference: include/ORBmatcher.h:40-193, src/ORBmatcher.cc.
     n, match = m.SearchByProjection(CurrentFrame, LastFrame, th, bMono)   # motion model
     n, match = m.SearchByProjection(F, vpMapPoints, th)                   # local map
     n, match = m.SearchByBoW(pKF, F)                                      # reference KF / reloc
+    n, match12 = m.SearchByBoW_KF(pKF1, pKF2)                             # loop closing
     n, vMatches12 = m.SearchForTriangulation(pKF1, pKF2, F12, bOnlyStereo) # LocalMapping
     n, best_idx, best_dist = m.Fuse(pKF, fcam, map_points, map_desc, th)   # its search
 
@@ -238,3 +239,25 @@ class ORBmatcher:
                                   L.ptr(md), len(mps), float(th), L.ptr(bi), L.ptr(bd),
                                   C.byref(n)), "orbg_fuse")
         return n.value, bi[:len(mps)].copy(), bd[:len(mps)].copy()
+
+    def SearchByBoW_KF(self, pKF1, pKF2):
+        """ORBmatcher::SearchByBoW(KeyFrame *pKF1, KeyFrame *pKF2, vpMatches12)
+        (src/ORBmatcher.cc:634-769): both KeyFrames with mvKeysUn, mDescriptors, mFeatVec and
+        map_valid (pMP && !isBad(), None: all).  Returns (nmatches, match12) with match12[i]
+        the pKF2 feature matched to pKF1's feature i (vpMatches12[i] = its MapPoint), -1."""
+        def side(fr):
+            d = np.ascontiguousarray(fr.mDescriptors, np.uint8)
+            a = np.ascontiguousarray(fr.mvKeysUn["angle"], np.float32)
+            v = None if fr.map_valid is None else np.ascontiguousarray(fr.map_valid, np.uint8)
+            nodes, off, feats = (np.ascontiguousarray(x, np.int32) for x in fr.mFeatVec)
+            return d, a, v, nodes, off, feats
+        d1, a1, v1, n1, o1, f1 = side(pKF1)
+        d2, a2, v2, n2, o2, f2 = side(pKF2)
+        m = np.zeros(max(len(d1), 1), np.int32)
+        n = C.c_int()
+        L.check(L.lib().orbg_search_by_bow_kf(
+            _ctx(self.device).handle, L.ptr(d1), L.ptr(a1), L.ptr(v1), len(d1), L.ptr(n1),
+            L.ptr(o1), L.ptr(f1), len(n1), L.ptr(d2), L.ptr(a2), L.ptr(v2), len(d2), L.ptr(n2),
+            L.ptr(o2), L.ptr(f2), len(n2), float(self.mfNNratio),
+            1 if self.mbCheckOrientation else 0, L.ptr(m), C.byref(n)), "orbg_search_by_bow_kf")
+        return n.value, m[:len(d1)].copy()

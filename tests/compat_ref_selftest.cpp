@@ -18,6 +18,7 @@
 #include <fstream>
 #include <list>
 #include <map>
+#include <set>
 #include <string>
 #include <thread>
 #include <vector>
@@ -498,6 +499,34 @@ int main(int argc, char **argv)
                                                          FB.mDescriptors.ptr<uint8_t>(i)) <= 50);
         }
         REQUIRE(nn == nbow);
+        {   // SearchByBoW(KeyFrame, KeyFrame) (LoopClosing::ComputeSim3): frame 2 as a KeyFrame
+            KeyFrame RK2;
+            RK2.mvKeysUn = F2.mvKeysUn;
+            RK2.mDescriptors = F2.mDescriptors;
+            std::vector<MapPoint> pts2(F2.N);
+            RK2.mvpMapPoints.assign(F2.N, nullptr);
+            for (int i = 0; i < F2.N; i++) {
+                RK2.mFeatVec[node_of(F2.mvKeysUn[i])].push_back((unsigned)i);
+                if (i % 4 == 1) continue;
+                RK2.mvpMapPoints[i] = &pts2[i];
+            }
+            std::vector<MapPoint *> v12;
+            const int nkk = orbg_compat::ref::SearchByBoW(ctx, 0.75f, true, &RK, &RK2, v12);
+            REQUIRE((int)v12.size() == F1.N && nkk > 50);
+            int nk = 0;
+            std::set<const MapPoint *> seen;
+            for (int i = 0; i < F1.N; i++) {
+                if (!v12[i]) continue;
+                nk++;
+                const int k2 = (int)(v12[i] - pts2.data());
+                REQUIRE(k2 >= 0 && k2 < F2.N && k2 % 4 != 1);
+                REQUIRE(RK.mvpMapPoints[i] && !RK.mvpMapPoints[i]->bad);
+                REQUIRE(seen.insert(v12[i]).second);  // vbMatched2: each KF2 point once
+                REQUIRE(orbg_compat::ref::DescriptorDistance(F1.mDescriptors.ptr<uint8_t>(i),
+                                                             F2.mDescriptors.ptr<uint8_t>(k2)) < 50);
+            }
+            REQUIRE(nk == nkk);
+        }
         if (argc >= 6) {
             const std::string o = argv[5];
             std::vector<int32_t> kn, ko, kf, fn, fo, ff, mi(FB.N);

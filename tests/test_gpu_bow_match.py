@@ -18,7 +18,7 @@ from orb_slam2_test_amd import ORBVocabulary, synthetic as S
 from orb_slam2_test_amd import _lib as L
 from orb_slam2_test_amd.orbmatcher import Frame, ORBmatcher
 
-from test_oracle_bow_match import _case
+from test_oracle_bow_match import _case, kf_case
 
 pytestmark = pytest.mark.gpu
 
@@ -155,3 +155,53 @@ def test_batch_device_pairs(oracle, kitti):
                                        0.75, True)
         assert hn[p] == rn and np.array_equal(hm[p, :cnt[b]], ref), p
         assert rn > 100
+    # SearchByBoW(KeyFrame, KeyFrame) over the same batch: both sides' MapPoint flags
+    F2 = L.BowFrames(valid=t_v.data_ptr(), **side)
+    t_m.fill_(-9)
+    t_n.fill_(-9)
+    torch.cuda.synchronize()
+    L.check(L.lib().orbg_search_by_bow_kf_batch_device(ctx.handle, C.byref(K), C.byref(F2), cap,
+                                                       C.c_void_p(t_ki.data_ptr()),
+                                                       C.c_void_p(t_fi.data_ptr()), P, 0.75, 1,
+                                                       C.c_void_p(t_m.data_ptr()),
+                                                       C.c_void_p(t_n.data_ptr())),
+            "orbg_search_by_bow_kf_batch_device")
+    ctx.sync()
+    hm, hn = t_m.cpu().numpy().reshape(P, cap), t_n.cpu().numpy()
+    for p in range(P):
+        a, b = kf_i[p], f_i[p]
+        rn, ref = oracle.search_by_bow_kf(hd[a, :cnt[a]], hk[a, :cnt[a]]["angle"], valid[a, :cnt[a]],
+                                          fv(a), hd[b, :cnt[b]], hk[b, :cnt[b]]["angle"],
+                                          valid[b, :cnt[b]], fv(b), 0.75, True)
+        assert hn[p] == rn and np.array_equal(hm[p, :cnt[a]], ref), p
+        assert np.all(hm[p, cnt[a]:] == -9)
+        assert rn > 100
+
+
+# ------------------------------------------- SearchByBoW(KeyFrame*, KeyFrame*, vpMatches12)
+@pytest.mark.parametrize("seed", range(6))
+@pytest.mark.parametrize("nnratio,check_ori", [(0.75, True), (0.6, False)])
+def test_kf_rule_cases(oracle, seed, nnratio, check_ori):
+    d1, a1, v1, fv1, d2, a2, v2, fv2 = kf_case(seed)
+    m = ORBmatcher(nnratio, check_ori)
+    n, got = m.SearchByBoW_KF(_frame(d1, a1, fv1, v1), _frame(d2, a2, fv2, v2))
+    rn, ref = oracle.search_by_bow_kf(d1, a1, v1, fv1, d2, a2, v2, fv2, nnratio, check_ori)
+    assert n == rn and np.array_equal(got, ref) and rn > 0
+
+
+@pytest.mark.parametrize("levelsup", [4, 6])
+def test_kf_kitti(oracle, kitti, levelsup):
+    ex, gv = kitti
+    rng = np.random.default_rng(100 + levelsup)
+    m = ORBmatcher(0.75, True)
+    for t in range(1, 4):
+        a, b = ex[t - 1], ex[t]
+        fv1 = gv.transform_arrays(a["desc"], levelsup)[2:]
+        fv2 = gv.transform_arrays(b["desc"], levelsup)[2:]
+        v1 = (rng.random(len(a["kps"])) > 0.1).astype(np.uint8)
+        v2 = (rng.random(len(b["kps"])) > 0.3).astype(np.uint8)
+        n, got = m.SearchByBoW_KF(_frame(a["desc"], a["kps"]["angle"], fv1, v1),
+                                  _frame(b["desc"], b["kps"]["angle"], fv2, v2))
+        rn, ref = oracle.search_by_bow_kf(a["desc"], a["kps"]["angle"], v1, fv1, b["desc"],
+                                          b["kps"]["angle"], v2, fv2, 0.75, True)
+        assert n == rn and np.array_equal(got, ref) and rn > 100, t

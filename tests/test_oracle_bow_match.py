@@ -182,3 +182,110 @@ def test_rotation_filter_drops_minor_bins(oracle):
                                     nnratio=0.75, check_ori=False)
     assert n_all == n and n_ori == n - 3
     assert (m_ori[:3] == -1).all() and (m_ori[3:] == np.arange(3, n)).all()
+
+
+# ------------------------------------------- SearchByBoW(KeyFrame*, KeyFrame*, vpMatches12)
+def py_search_by_bow_kf(d1, a1, v1, fv1, d2, a2, v2, fv2, nnratio, check_ori):
+    """ORBmatcher.cc:634-769 line by line: KF1's good MapPoints against KF2's (vbMatched2,
+    strict < TH_LOW)."""
+    n1_, o1_, f1_ = fv1
+    n2_, o2_, f2_ = fv2
+    m1 = {int(n1_[j]): [int(x) for x in f1_[o1_[j]:o1_[j + 1]]] for j in range(len(n1_))}
+    m2 = {int(n2_[j]): [int(x) for x in f2_[o2_[j]:o2_[j + 1]]] for j in range(len(n2_))}
+    k1, k2 = sorted(m1), sorted(m2)
+    match = [-1] * len(d1)
+    matched2 = [False] * len(d2)
+    hist = [[] for _ in range(30)]
+    factor = np.float32(1.0) / np.float32(30)
+    nm = 0
+    a = b = 0
+    while a < len(k1) and b < len(k2):
+        if k1[a] == k2[b]:
+            for i1 in m1[k1[a]]:
+                if not v1[i1]:
+                    continue
+                b1, bi, b2 = 256, -1, 256
+                for i2 in m2[k2[b]]:
+                    if matched2[i2] or not v2[i2]:
+                        continue
+                    d = _dist(d1[i1], d2[i2])
+                    if d < b1:
+                        b2, b1, bi = b1, d, i2
+                    elif d < b2:
+                        b2 = d
+                if b1 < TH_LOW and np.float32(b1) < np.float32(nnratio) * np.float32(b2):
+                    match[i1] = bi
+                    matched2[bi] = True
+                    if check_ori:
+                        rot = np.float32(a1[i1]) - np.float32(a2[bi])
+                        if rot < 0.0:
+                            rot = np.float32(rot + np.float32(360.0))
+                        x = float(np.float32(rot * factor))
+                        bb = int(math.floor(x + 0.5))
+                        hist[0 if bb == 30 else bb].append(i1)
+                    nm += 1
+            a += 1
+            b += 1
+        elif k1[a] < k2[b]:
+            a += 1
+        else:
+            b += 1
+    if check_ori:
+        s_ = [len(h) for h in hist]
+        mx1 = mx2 = mx3 = 0
+        j1 = j2 = j3 = -1
+        for i in range(30):
+            if s_[i] > mx1:
+                mx3, mx2, mx1, j3, j2, j1 = mx2, mx1, s_[i], j2, j1, i
+            elif s_[i] > mx2:
+                mx3, mx2, j3, j2 = mx2, s_[i], j2, i
+            elif s_[i] > mx3:
+                mx3, j3 = s_[i], i
+        if mx2 < np.float32(0.1) * np.float32(mx1):
+            j2 = j3 = -1
+        elif mx3 < np.float32(0.1) * np.float32(mx1):
+            j3 = -1
+        for i in range(30):
+            if i not in (j1, j2, j3):
+                for j in hist[i]:
+                    match[j] = -1
+                    nm -= 1
+    return nm, np.array(match, np.int32)
+
+
+def kf_case(seed):
+    """a KeyFrame-KeyFrame pair: _case's KF as KF1, its F side as KF2 with MapPoint flags"""
+    kd, ka, kv, kfv, fd, fa, ffv = _case(seed)
+    rng = np.random.default_rng(seed + 100)
+    fv_ = (rng.random(len(fd)) > 0.2).astype(np.uint8)
+    return kd, ka, kv, kfv, fd, fa, fv_, ffv
+
+
+@pytest.mark.parametrize("seed", range(12))
+@pytest.mark.parametrize("nnratio,check_ori", [(0.75, True), (0.6, False), (0.9, True)])
+def test_kf_oracle_equals_python_restatement(oracle, seed, nnratio, check_ori):
+    c = kf_case(seed)
+    got = oracle.search_by_bow_kf(*c, nnratio=nnratio, check_ori=check_ori)
+    ref = py_search_by_bow_kf(*c, nnratio=nnratio, check_ori=check_ori)
+    assert got[0] == ref[0] and np.array_equal(got[1], ref[1])
+    assert got[0] > 0
+
+
+def test_kf_known_answers(oracle):
+    """KF-KF rules: strict < TH_LOW (50 rejected, 49 taken), KF2 features without a good
+    MapPoint are no candidates, a taken KF2 feature is skipped by the next KF1 feature."""
+    rng = np.random.default_rng(3)
+    d2 = rng.integers(0, 256, (5, 32), dtype=np.uint8)
+    d1 = np.stack([_flip(d2[0], 50, rng), _flip(d2[0], 49, rng), d2[1], d2[2], d2[2]])
+    for i, j in ((0, 1), (0, 2), (0, 3), (0, 4), (1, 1), (1, 2), (1, 3), (1, 4)):
+        assert _dist(d1[i], d2[j]) > 80
+    v1 = np.ones(5, np.uint8)
+    v2 = np.array([1, 0, 1, 1, 1], np.uint8)   # KF2 feature 1: no good MapPoint
+    fv1 = (np.array([4], np.int32), np.array([0, 5], np.int32), np.arange(5, dtype=np.int32))
+    fv2 = (np.array([4], np.int32), np.array([0, 5], np.int32), np.arange(5, dtype=np.int32))
+    z1, z2 = np.zeros(5, np.float32), np.zeros(5, np.float32)
+    n, m = oracle.search_by_bow_kf(d1, z1, v1, fv1, d2, z2, v2, fv2, 0.75, True)
+    # 0: 50 bits (rejected); 1: 49 bits -> KF2 0; 2: KF2 1 invalid, the rest far -> none;
+    # 3: KF2 2 exactly; 4: KF2 2 taken, the rest far -> none
+    assert m.tolist() == [-1, 0, -1, 2, -1] and n == 2
+    assert py_search_by_bow_kf(d1, z1, v1, fv1, d2, z2, v2, fv2, 0.75, True)[0] == 2
