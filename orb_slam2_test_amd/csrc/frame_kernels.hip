@@ -13,7 +13,10 @@
 //                   distance matrix is one Hamming distance per lane (row i's descriptor
 //                   broadcast through scalar registers), its median the k-th smallest across
 //                   the lanes by a 9-step binary search over [0, 256] with ballot counts (no
-//                   LDS, no sort); the least median wins, the first row on ties.
+//                   LDS, no sort); the least median wins, the first row on ties.  Up to 32
+//                   observations the wave splits into 16- or 32-lane groups that each hold
+//                   every observation and take one row per iteration (four or two rows at
+//                   once, the search on the group's ballot bits).
 //
 // Float / double pins as the oracle (oracle/frame_oracle.c): cv::gemm's small-matrix path
 // with a double work type for Rcw*P+tcw and -Rcw.t()*tcw, cv::norm / Mat::dot in double,
@@ -166,6 +169,9 @@ int launch_frustum(hipStream_t st, const orbg_frustum_camera *cams, const orbg_m
 // ComputeDistinctiveDescriptors
 // ---------------------------------------------------------------------------
 #define DD_WAVES 4
+#ifndef ORBG_DD_GROUPS
+#define ORBG_DD_GROUPS 1  // N <= 32: 16- / 32-lane groups, two or four rows per iteration (0: a row per iteration)
+#endif
 #define DD_CHUNKS 8  // observations kept as per-lane distances per row: 512
 
 __device__ __forceinline__ void load_desc(const uint8_t *__restrict__ pool, int row, uint32_t d[8])
@@ -191,13 +197,67 @@ __global__ __launch_bounds__(64 * DD_WAVES) void k_distinctive(
         return;
     }
     const int32_t *R = rows + o0;
+    const int k = (N - 1) >> 1;  // vDists[0.5*(N-1)]: (size_t)(0.5 * (N - 1)) = (N - 1) / 2
+#if ORBG_DD_GROUPS
+    if (N <= 32) {
+        // G-lane groups (G = 16 or 32), one row per group: every group holds all N
+        // observations (lane l: observation l % G), group g takes row i0 + g of each
+        // iteration, its median by the ballot search restricted to the group's bits
+        const int G = N <= 16 ? 16 : 32, R_ = 64 / G;
+        const int g = lane / G, j = lane - g * G;
+        uint32_t mine[8];
+        if (j < N) load_desc(pool, R[j], mine);
+        else
+#pragma unroll
+            for (int w = 0; w < 8; w++) mine[w] = 0;
+        const unsigned long long gmask = (G == 64 ? ~0ull : ((1ull << G) - 1ull)) << (g * G);
+        int best_median = 0x7fffffff, best = 0;
+        for (int i0 = 0; i0 < N; i0 += R_) {
+            const int r = i0 + g;  // this group's row (past N: a dead row, not compared)
+            const int src = g * G + min(r, N - 1);
+            uint32_t q[8];
+#pragma unroll
+            for (int w = 0; w < 8; w++) q[w] = (uint32_t)__shfl((int)mine[w], src, 64);
+            int d = 0x7fff;
+            if (j < N) {
+                d = 0;
+#pragma unroll
+                for (int w = 0; w < 8; w++) d += __popc(q[w] ^ mine[w]);
+            }
+            int lo = 0, hi = 256;  // group-uniform
+#pragma unroll
+            for (int it = 0; it < 9; it++) {
+                const int mid = (lo + hi) >> 1;
+                const int cnt = __popcll(__ballot(d <= mid) & gmask);
+                const bool up = cnt >= k + 1;
+                hi = up ? mid : hi;
+                lo = up ? lo : mid + 1;
+            }
+            // rows i0 .. i0 + R_ - 1 in order: strict <, the first row wins ties
+            for (int gg = 0; gg < R_; gg++) {
+                const int rr = i0 + gg;
+                if (rr >= N) break;
+                const int m = __builtin_amdgcn_readlane(lo, gg * G);
+                if (m < best_median) {
+                    best_median = m;
+                    best = rr;
+                }
+            }
+        }
+        if (lane == 0) best_out[p] = best;
+        if (desc_out && lane < 2) {
+            const int rb = R[best];
+            ((uint4 *)(desc_out + (size_t)p * 32))[lane] = ((const uint4 *)(pool + (size_t)rb * 32))[lane];
+        }
+        return;
+    }
+#endif
     // observations 0..63 register-resident, one per lane
     uint32_t mine[8];
     if (lane < N) load_desc(pool, R[lane], mine);
     else
 #pragma unroll
         for (int w = 0; w < 8; w++) mine[w] = 0;
-    const int k = (N - 1) >> 1;  // vDists[0.5*(N-1)]: (size_t)(0.5 * (N - 1)) = (N - 1) / 2
     int best_median = 0x7fffffff, best = 0;
     for (int i = 0; i < N; i++) {
         // row i's descriptor, wave-uniform (scalar registers)
