@@ -49,6 +49,7 @@
  *                                     vMatchedPairs, bOnlyStereo)  src/ORBmatcher.cc:779-957
  *                                     (LocalMapping::CreateNewMapPoints, LocalMapping.cc:378)
  *   orbg_fuse ....................... ORBmatcher::Fuse(pKF, vpMapPoints, th)'s per-MapPoint search
+ *   orbg_fuse_sim3 .................. ORBmatcher::Fuse(pKF, Scw, vpPoints, th, vpReplacePoint)'s search
  *                                     src/ORBmatcher.cc:968-1069 (LocalMapping::SearchInNeighbors,
  *                                     LocalMapping.cc:622-690)
  *   orbg_ba_linearize ............... g2o computeActiveErrors + BlockSolver::buildSystem arithmetic
@@ -532,6 +533,25 @@ int orbg_fuse_batch_device(orbg_ctx *ctx, const orbg_keyframes *kfs, int cap, co
                            const uint8_t *d_mdesc, const int32_t *d_mcounts, int mcap, int npairs,
                            float th, int32_t *d_best_idx, int32_t *d_best_dist,
                            int32_t *d_nfused);
+/* ORBmatcher::Fuse(pKF, Scw, vpPoints, th, vpReplacePoint) (src/ORBmatcher.cc:1133-1258;
+ * caller LoopClosing::SearchAndFuse, LoopClosing.cc:944-980, th 4): the same split.  cam->Tcw
+ * holds Scw's rows 0..2 (s*Rcw | s*tcw, Converter::toCvMat of the corrected g2o::Sim3); the
+ * kernel decomposes it as the reference does (scw = sqrt of row 0's double dot product, Rcw |
+ * tcw = Scw / scw with the float alpha 1 / scw, :1143-1148; Ow = -Rcw^T tcw), then projects
+ * and gates exactly as orbg_fuse but ranks the candidates by descriptor distance alone (no
+ * reprojection gate; kf->uright and cam->bf unused).  mps[i].flags ORBG_MP_VALID = !isBad() &&
+ * not in pKF->GetMapPoints() at the call's start.  Outputs as orbg_fuse; the caller then
+ * walks vpPoints in order: best_idx[i] >= 0 -> pKF's MapPoint at best_idx[i], if any and not
+ * bad, becomes vpReplacePoint[i], else AddObservation / AddMapPoint (:1239-1254). */
+int orbg_fuse_sim3(orbg_ctx *ctx, const orbg_keyframe *kf, const orbg_frustum_camera *cam,
+                   const orbg_map_point *mps, const uint8_t *mdesc, int nmp, float th,
+                   int32_t *best_idx, int32_t *best_dist, int *nfused);
+/* Batched, device memory, as orbg_fuse_batch_device (kfs->uright may be NULL). */
+int orbg_fuse_sim3_batch_device(orbg_ctx *ctx, const orbg_keyframes *kfs, int cap,
+                                const int32_t *d_kf, const orbg_frustum_camera *d_cams,
+                                const orbg_map_point *d_mps, const uint8_t *d_mdesc,
+                                const int32_t *d_mcounts, int mcap, int npairs, float th,
+                                int32_t *d_best_idx, int32_t *d_best_dist, int32_t *d_nfused);
 
 /* ---------------- Optimizer::PoseOptimization ----------------
  * One edge per Frame keypoint with a MapPoint (index order): EdgeSE3ProjectXYZOnlyPose when

@@ -145,13 +145,30 @@ int orc_search_for_triangulation(const orc_tri_kf *kf1, const orc_tri_kf *kf2,
     return nmatches;
 }
 
-/* ORBmatcher::Fuse(pKF, vpMapPoints, th), the per-MapPoint search (ORBmatcher.cc:968-1069):
- * best_idx[i] = bestIdx when bestDist <= TH_LOW (the reference then fuses), else -1;
- * best_dist[i] = bestDist (256: no candidate passed or the point was skipped). */
-int orc_fuse_search(const orc_tri_kf *kf, const orc_frustum_cam *cam, const orc_map_point *mps,
-                    const uint8_t *mdesc, int nmp, float th, const float *scale_factors,
-                    const float *inv_sigma2, int32_t *best_idx, int32_t *best_dist)
+/* The Sim3 decomposition at the top of ORBmatcher::Fuse(pKF, Scw, ...) (ORBmatcher.cc:
+ * 1143-1148): scw = sqrt(sRcw.row(0).dot(sRcw.row(0))) -- Mat::dot of floats sums double
+ * products (the dot pin of isInFrustum) and the float scw is the double root rounded; Rcw =
+ * sRcw / scw and tcw = t / scw are Mat / double, i.e. convertTo with the float alpha
+ * (float)(1 / scw) and shift 0: each element x * alpha rounded once (+ 0.0f). */
+void orc_sim3_decompose(const float *Scw, float *Tcw)
 {
+    double d = 0.0;
+    for (int k = 0; k < 3; k++)
+        d += (double)Scw[k] * (double)Scw[k];
+    const float scw = (float)sqrt(d);
+    const float a = (float)(1.0 / (double)scw);
+    for (int k = 0; k < 12; k++)
+        Tcw[k] = Scw[k] * a + 0.0f;
+}
+
+static int fuse_search(const orc_tri_kf *kf, const orc_frustum_cam *cam0, const orc_map_point *mps,
+                       const uint8_t *mdesc, int nmp, float th, const float *scale_factors,
+                       const float *inv_sigma2, int sim3, int32_t *best_idx, int32_t *best_dist)
+{
+    orc_frustum_cam camd = *cam0;
+    const orc_frustum_cam *cam = &camd;
+    if (sim3)
+        orc_sim3_decompose(cam0->Tcw, camd.Tcw);
     /* the KeyFrame's grid is the Frame's (mGrid and mfGridElementWidthInv copied from the
      * Frame, float bounds), its mnMinX .. mnMaxY are ints (KeyFrame.h:288-291, the Frame's
      * truncated, KeyFrame.cc:51): IsInImage and GetFeaturesInArea's cell range use those */
@@ -221,7 +238,9 @@ int orc_fuse_search(const orc_tri_kf *kf, const orc_frustum_cam *cam, const orc_
             const int kpLevel = kp->octave;
             if (kpLevel < nPredictedLevel - 1 || kpLevel > nPredictedLevel)
                 continue;
-            if (kf->uright[idx] >= 0) {
+            if (sim3) {
+                /* the Sim3 variant has no reprojection gate (ORBmatcher.cc:1218-1236) */
+            } else if (kf->uright[idx] >= 0) {
                 const float ex = u - kp->x, ey = v - kp->y, er = ur - kf->uright[idx];
                 const float e2 = ex * ex + ey * ey + er * er;
                 if ((double)(e2 * inv_sigma2[kpLevel]) > 7.8)
@@ -247,4 +266,27 @@ int orc_fuse_search(const orc_tri_kf *kf, const orc_frustum_cam *cam, const orc_
     free(cand);
     orc_grid_free(&g);
     return nfused;
+}
+
+/* ORBmatcher::Fuse(pKF, vpMapPoints, th), the per-MapPoint search (ORBmatcher.cc:968-1069):
+ * best_idx[i] = bestIdx when bestDist <= TH_LOW (the reference then fuses), else -1;
+ * best_dist[i] = bestDist (256: no candidate passed or the point was skipped). */
+int orc_fuse_search(const orc_tri_kf *kf, const orc_frustum_cam *cam, const orc_map_point *mps,
+                    const uint8_t *mdesc, int nmp, float th, const float *scale_factors,
+                    const float *inv_sigma2, int32_t *best_idx, int32_t *best_dist)
+{
+    return fuse_search(kf, cam, mps, mdesc, nmp, th, scale_factors, inv_sigma2, 0, best_idx,
+                       best_dist);
+}
+
+/* ORBmatcher::Fuse(pKF, Scw, vpPoints, th, vpReplacePoint)'s search (ORBmatcher.cc:1133-1238,
+ * LoopClosing::SearchAndFuse): cam->Tcw holds Scw's rows 0..2 (sR | t), decomposed as above;
+ * the projection, IsInImage, distance, angle and scale gates are Fuse's, the candidates are
+ * ranked by descriptor distance alone (no reprojection gate, mvuRight unused).  Same outputs;
+ * the replace / add update (:1239-1254) is the caller's, in vpPoints order. */
+int orc_fuse_sim3_search(const orc_tri_kf *kf, const orc_frustum_cam *cam,
+                         const orc_map_point *mps, const uint8_t *mdesc, int nmp, float th,
+                         const float *scale_factors, int32_t *best_idx, int32_t *best_dist)
+{
+    return fuse_search(kf, cam, mps, mdesc, nmp, th, scale_factors, NULL, 1, best_idx, best_dist);
 }

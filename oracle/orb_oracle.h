@@ -288,6 +288,12 @@ void orc_three_maxima(const int *hsize, int *ind1, int *ind2, int *ind3);
 int orc_fuse_search(const orc_tri_kf *kf, const orc_frustum_cam *cam, const orc_map_point *mps,
                     const uint8_t *mdesc, int nmp, float th, const float *scale_factors,
                     const float *inv_sigma2, int32_t *best_idx, int32_t *best_dist);
+/* ORBmatcher::Fuse(pKF, Scw, vpPoints, th, vpReplacePoint)'s search (ORBmatcher.cc:1133-1238):
+ * cam->Tcw = Scw's rows 0..2, decomposed by orc_sim3_decompose; no reprojection gate. */
+void orc_sim3_decompose(const float *Scw, float *Tcw);
+int orc_fuse_sim3_search(const orc_tri_kf *kf, const orc_frustum_cam *cam,
+                         const orc_map_point *mps, const uint8_t *mdesc, int nmp, float th,
+                         const float *scale_factors, int32_t *best_idx, int32_t *best_dist);
 
 /* ---- Optimizer::PoseOptimization (pose_oracle.c) ---- */
 /* LM's pow(2 rho - 1, 3) as the once-rounded exact cube (optimization_algorithm_levenberg.cpp:135) */

@@ -197,6 +197,10 @@ def lib():
         L.orc_search_for_triangulation.restype = C.c_int
         L.orc_fuse_search.argtypes = [P(TriKF), vp, vp, vp, C.c_int, C.c_float, vp, vp, vp, vp]
         L.orc_fuse_search.restype = C.c_int
+        L.orc_fuse_sim3_search.argtypes = [P(TriKF), vp, vp, vp, C.c_int, C.c_float, vp, vp, vp]
+        L.orc_fuse_sim3_search.restype = C.c_int
+        L.orc_sim3_decompose.argtypes = [vp, vp]
+        L.orc_sim3_decompose.restype = None
         L.orc_search_by_bow_kf.restype = C.c_int
         L.orc_search_by_bow_kf.argtypes = [vp, vp, vp, C.c_int, vp, vp, vp, C.c_int, vp, vp, vp,
                                            C.c_int, vp, vp, vp, C.c_int, C.c_float, C.c_int, vp]
@@ -744,4 +748,31 @@ def fuse_search(kf, fcam, mps, mdesc, th, scale_factors, inv_sigma2):
     bd = np.zeros(max(len(mps), 1), np.int32)
     n = lib().orc_fuse_search(C.byref(k), _p(fcam), _p(mps), _p(md), len(mps), float(th),
                               _p(sf), _p(isg), _p(bi), _p(bd))
+    return n, bi[:len(mps)], bd[:len(mps)]
+
+
+def sim3_decompose(Scw):
+    """Rcw | tcw (3x4 float32) of Fuse(pKF, Scw, ...)'s decomposition (ORBmatcher.cc:1143-1148)."""
+    S = np.ascontiguousarray(np.asarray(Scw, np.float32).reshape(-1)[:12])
+    T = np.zeros(12, np.float32)
+    lib().orc_sim3_decompose(_p(S), _p(T))
+    return T.reshape(3, 4)
+
+
+def fuse_sim3_search(kf, fcam, mps, mdesc, th, scale_factors):
+    """ORBmatcher::Fuse(pKF, Scw, vpPoints, th, vpReplacePoint)'s search -> (nfused, best_idx,
+    best_dist); fcam["Tcw"] holds Scw's rows 0..2.  kf: dict(kps, desc)."""
+    keep = []
+    kf = dict(kf, fv=(np.zeros(0), np.zeros(1), np.zeros(0)))
+    if kf.get("uright") is None:
+        kf["uright"] = np.full(len(kf["kps"]), -1, np.float32)
+    k = _tri_kf(kf, keep)
+    fcam = np.ascontiguousarray(fcam, FRUSTUM_DTYPE)
+    mps = np.ascontiguousarray(mps, MAPPOINT_DTYPE)
+    md = np.ascontiguousarray(mdesc, np.uint8).reshape(-1, 32)
+    sf = np.ascontiguousarray(scale_factors, np.float32)
+    bi = np.zeros(max(len(mps), 1), np.int32)
+    bd = np.zeros(max(len(mps), 1), np.int32)
+    n = lib().orc_fuse_sim3_search(C.byref(k), _p(fcam), _p(mps), _p(md), len(mps), float(th),
+                                   _p(sf), _p(bi), _p(bd))
     return n, bi[:len(mps)], bd[:len(mps)]

@@ -249,6 +249,9 @@ def lib():
         "orbg_fuse": (i32, [vp, P(KeyFrame), vp, vp, vp, i32, f32, vp, vp, P(i32)]),
         "orbg_fuse_batch_device": (i32, [vp, P(KeyFrames), i32, vp, vp, vp, vp, vp, i32, i32, f32,
                                          vp, vp, vp]),
+        "orbg_fuse_sim3": (i32, [vp, P(KeyFrame), vp, vp, vp, i32, f32, vp, vp, P(i32)]),
+        "orbg_fuse_sim3_batch_device": (i32, [vp, P(KeyFrames), i32, vp, vp, vp, vp, vp, i32, i32, f32,
+                                         vp, vp, vp]),
         "orbg_undistort_keypoints": (i32, [vp, vp, vp, i32, vp]),
         "orbg_undistort_batch_device": (i32, [vp, vp, vp, vp, i32, i32, vp]),
         "orbg_compute_image_bounds": (i32, [vp, i32, i32, P(Bounds)]),

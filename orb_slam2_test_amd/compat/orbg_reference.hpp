@@ -29,7 +29,8 @@
 //   ComputeImageBounds .............. Frame.cc:575-611
 //   isInFrustum (SearchLocalPoints) . Frame.cc:342-409, Tracking.cc:1676-1691
 //   SearchForTriangulation .......... ORBmatcher.cc:779-957 (ORBmatcher.h:72)
-//   Fuse(pKF, vpMapPoints, th) ...... ORBmatcher.cc:968-1107 (ORBmatcher.h:80)
+//   Fuse(pKF, vpMapPoints, th) ...... ORBmatcher.cc:968-1107 (ORBmatcher.h:153)
+//   Fuse(pKF, Scw, vpPoints, th, vpReplacePoint) ORBmatcher.cc:1133-1258 (ORBmatcher.h:162)
 //   ComputeDistinctiveDescriptors ... MapPoint.cc:342-420 (the BestIdx over vDescriptors)
 //   LocalBundleAdjustment window ..... Optimizer.cc:633-851: the vertex / edge set g2o builds
 //                                      (LbaWindow), and BlockSolver<6,3>::buildSystem's block
@@ -879,6 +880,72 @@ int Fuse(orbg_ctx *ctx, KeyFrameT *pKF, const std::vector<MapPointT *> &vpMapPoi
                 else
                     pMPinKF->Replace(pMP);
             }
+        } else {
+            pMP->AddObservation(pKF, (size_t)best[i]);
+            pKF->AddMapPoint(pMP, (size_t)best[i]);
+        }
+        nFused++;
+    }
+    return nFused;
+}
+
+// ORBmatcher::Fuse(pKF, Scw, vpPoints, th, vpReplacePoint) (LoopClosing::SearchAndFuse,
+// th 4): the search on the device (Scw decomposed there as the reference does), then the
+// reference's loop in vpPoints order (ORBmatcher.cc:1239-1254): a KeyFrame MapPoint at the
+// best feature, if not bad, goes to vpReplacePoint[i], else pMP is added.  The skip test
+// (isBad, already in pKF->GetMapPoints() when the call starts) cannot change inside the loop
+// (AddObservation / AddMapPoint make nothing bad and spAlreadyFound is a snapshot), so it is
+// taken once.  Returns nFused.
+template <class FrameT, class KeyFrameT, class MapPointT, class Mat>
+int Fuse(orbg_ctx *ctx, KeyFrameT *pKF, const Mat &Scw, const std::vector<MapPointT *> &vpPoints,
+         float th, std::vector<MapPointT *> &vpReplacePoint)
+{
+    const int n = (int)vpPoints.size();
+    const KfArrays<KeyFrameT> a = kf_arrays(pKF, false);
+    const orbg_keyframe kf = a.view(false);
+    const auto spAlreadyFound = pKF->GetMapPoints();
+    std::vector<orbg_map_point> mp(n > 0 ? n : 1);
+    std::vector<uint8_t> md((size_t)(n > 0 ? n : 1) * 32, 0);
+    for (int i = 0; i < n; i++) {
+        MapPointT *p = vpPoints[i];
+        orbg_map_point &m = mp[i];
+        std::memset(&m, 0, sizeof(m));
+        if (p->isBad() || spAlreadyFound.count(p)) continue;
+        const auto X = p->GetWorldPos(), Pn = p->GetNormal();
+        m.x = X.template at<float>(0);
+        m.y = X.template at<float>(1);
+        m.z = X.template at<float>(2);
+        m.nx = Pn.template at<float>(0);
+        m.ny = Pn.template at<float>(1);
+        m.nz = Pn.template at<float>(2);
+        m.min_dist = p->GetMinDistance();
+        m.max_dist = p->GetMaxDistance();
+        m.flags = ORBG_MP_VALID;
+        mp_desc(p, &md[(size_t)i * 32]);
+    }
+    orbg_frustum_camera fc;
+    std::memset(&fc, 0, sizeof(fc));
+    for (int r = 0; r < 3; r++)
+        for (int c = 0; c < 4; c++) fc.Tcw[4 * r + c] = Scw.template at<float>(r, c);
+    fc.fx = pKF->fx;
+    fc.fy = pKF->fy;
+    fc.cx = pKF->cx;
+    fc.cy = pKF->cy;
+    fc.log_scale_factor = pKF->mfLogScaleFactor;
+    fc.nlevels = pKF->mnScaleLevels;
+    fc.bounds = orbg_bounds{FrameT::mnMinX, FrameT::mnMaxX, FrameT::mnMinY, FrameT::mnMaxY};
+    std::vector<int32_t> best(n > 0 ? n : 1), dist(n > 0 ? n : 1);
+    int ncand = 0;
+    check(orbg_fuse_sim3(ctx, &kf, &fc, mp.data(), md.data(), n, th, best.data(), dist.data(),
+                         &ncand),
+          "orbg_fuse_sim3");
+    int nFused = 0;
+    for (int i = 0; i < n; i++) {
+        if (best[i] < 0) continue;
+        MapPointT *pMP = vpPoints[i];
+        MapPointT *pMPinKF = pKF->GetMapPoint((size_t)best[i]);
+        if (pMPinKF) {
+            if (!pMPinKF->isBad()) vpReplacePoint[i] = pMPinKF;
         } else {
             pMP->AddObservation(pKF, (size_t)best[i]);
             pKF->AddMapPoint(pMP, (size_t)best[i]);

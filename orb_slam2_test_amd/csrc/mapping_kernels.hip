@@ -308,6 +308,24 @@ struct FuseKey {  // a grid entry in LDS
 #define FU_CELLS (ORBG_GRID_COLS * ORBG_GRID_ROWS)
 static_assert(FU_CELLS == 256 * 12, "k_fuse's scan gives 12 grid cells to each of 256 threads");
 
+// Fuse(pKF, Scw, ...)'s decomposition (ORBmatcher.cc:1143-1148): scw = the double root of
+// row 0's double dot product, rounded to float; Rcw | tcw = Scw * (float)(1 / scw), rounded
+// once per element (Mat / double is convertTo with a float alpha and shift 0)
+__device__ inline void sim3_decompose(const float *S, float *T)
+{
+    double d = 0.0;
+#pragma unroll
+    for (int k = 0; k < 3; k++) d += (double)S[k] * (double)S[k];
+    const float scw = (float)sqrt(d);
+    const float a = (float)(1.0 / (double)scw);
+#pragma unroll
+    for (int k = 0; k < 12; k++) T[k] = __fadd_rn(__fmul_rn(S[k], a), 0.0f);
+}
+
+// SIM3 = false: Fuse(pKF, vpMapPoints, th) (:968-1069).  SIM3 = true: Fuse(pKF, Scw, vpPoints,
+// th, vpReplacePoint) (:1133-1238): cams[p].Tcw holds Scw's rows 0..2, and the candidates
+// are ranked by descriptor distance alone (no reprojection gate, no mvuRight)
+template <bool SIM3>
 __global__ __launch_bounds__(256) void k_fuse(orbg_keyframes K, int cap,
                                               const int32_t *__restrict__ kf_index,
                                               const orbg_frustum_camera *__restrict__ cams,
@@ -383,15 +401,23 @@ __global__ __launch_bounds__(256) void k_fuse(orbg_keyframes K, int cap,
     const float kminy = (float)(int)C.bounds.min_y, kmaxy = (float)(int)C.bounds.max_y;
     int fused = 0;
     const int nm = mcounts[p];
-    const float tcw0 = C.Tcw[3], tcw1 = C.Tcw[7], tcw2 = C.Tcw[11];
-    // KeyFrame::GetCameraCenter: Ow = -Rwc*tcw (cv::gemm pin)
+    float Tw[12];
+    if (SIM3) {
+        sim3_decompose(C.Tcw, Tw);
+    } else {
+#pragma unroll
+        for (int k = 0; k < 12; k++) Tw[k] = C.Tcw[k];
+    }
+    const float tcw0 = Tw[3], tcw1 = Tw[7], tcw2 = Tw[11];
+    // KeyFrame::GetCameraCenter: Ow = -Rwc*tcw (cv::gemm pin); the Sim3 variant's
+    // Ow = -Rcw.t()*tcw is the same sums
     float Ow[3];
 #pragma unroll
     for (int r = 0; r < 3; r++) {
         double t = 0.0;
-        t += (double)C.Tcw[r] * (double)tcw0;
-        t += (double)C.Tcw[4 + r] * (double)tcw1;
-        t += (double)C.Tcw[8 + r] * (double)tcw2;
+        t += (double)Tw[r] * (double)tcw0;
+        t += (double)Tw[4 + r] * (double)tcw1;
+        t += (double)Tw[8 + r] * (double)tcw2;
         Ow[r] = (float)(t * -1.0);
     }
     for (int i = tid; i < nm; i += 256) {
@@ -407,7 +433,7 @@ __global__ __launch_bounds__(256) void k_fuse(orbg_keyframes K, int cap,
             for (int r = 0; r < 3; r++) {
                 double t = 0.0;
 #pragma unroll
-                for (int k = 0; k < 3; k++) t += (double)C.Tcw[4 * r + k] * (double)P[k];
+                for (int k = 0; k < 3; k++) t += (double)Tw[4 * r + k] * (double)P[k];
                 t *= 1.0;
                 t += (double)tc[r];
                 Pc[r] = (float)t;
@@ -465,8 +491,10 @@ __global__ __launch_bounds__(256) void k_fuse(orbg_keyframes K, int cap,
                         if (!(fabsf(e.x - u) < r && fabsf(e.y - v) < r)) continue;
                         const int kl = e.io & 15, idx = e.io >> 4;
                         if (kl < lvl - 1 || kl > lvl) continue;
-                        const float kr = K.uright ? K.uright[(size_t)kf * cap + idx] : -1.0f;
-                        if (kr >= 0) {
+                        const float kr = !SIM3 && K.uright ? K.uright[(size_t)kf * cap + idx] : -1.0f;
+                        if (SIM3) {
+                            // ranked by descriptor distance alone (ORBmatcher.cc:1218-1236)
+                        } else if (kr >= 0) {
                             const float ex = u - e.x, ey = v - e.y, er = ur - kr;
                             const float e2 = ex * ex + ey * ey + er * er;
                             if ((double)(e2 * T.inv_sigma2[kl]) > 7.8) continue;
@@ -503,8 +531,8 @@ __global__ __launch_bounds__(256) void k_fuse(orbg_keyframes K, int cap,
 int launch_fuse(hipStream_t st, const orbg_keyframes &K, int cap, const int32_t *kf,
                 const orbg_frustum_camera *cams, const orbg_map_point *mps, const uint8_t *mdesc,
                 const int32_t *mcounts, int mcap, int npairs, float th, const float *scale,
-                const float *inv_sigma2, int nlevels, int32_t *best_idx, int32_t *best_dist,
-                int32_t *nfused)
+                const float *inv_sigma2, int nlevels, int sim3, int32_t *best_idx,
+                int32_t *best_dist, int32_t *nfused)
 {
     if (npairs <= 0) return 0;
     if (cap > 8192) return -95;  // the grid's entries in LDS
@@ -515,12 +543,17 @@ int launch_fuse(hipStream_t st, const orbg_keyframes &K, int cap, const int32_t 
         T.inv_sigma2[l] = inv_sigma2[s];
     }
     const size_t lds = (FU_CELLS + 4) * 4 + (size_t)cap * sizeof(FuseKey);
+    const void *fn = sim3 ? (const void *)k_fuse<true> : (const void *)k_fuse<false>;
     if (lds > 64 * 1024 &&
-        hipFuncSetAttribute((const void *)k_fuse, hipFuncAttributeMaxDynamicSharedMemorySize,
-                            (int)lds) != hipSuccess)
+        hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) !=
+            hipSuccess)
         return -5;
-    hipLaunchKernelGGL(k_fuse, dim3(npairs), dim3(256), lds, st, K, cap, kf, cams, mps, mdesc,
-                       mcounts, mcap, th, T, best_idx, best_dist, nfused);
+    if (sim3)
+        hipLaunchKernelGGL(k_fuse<true>, dim3(npairs), dim3(256), lds, st, K, cap, kf, cams, mps,
+                           mdesc, mcounts, mcap, th, T, best_idx, best_dist, nfused);
+    else
+        hipLaunchKernelGGL(k_fuse<false>, dim3(npairs), dim3(256), lds, st, K, cap, kf, cams,
+                           mps, mdesc, mcounts, mcap, th, T, best_idx, best_dist, nfused);
     return hipGetLastError() == hipSuccess ? 0 : -5;
 }
 

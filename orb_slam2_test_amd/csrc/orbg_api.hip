@@ -83,8 +83,8 @@ int launch_tri_match(hipStream_t st, const orbg_keyframes &K, int cap, const int
 int launch_fuse(hipStream_t st, const orbg_keyframes &K, int cap, const int32_t *kf,
                 const orbg_frustum_camera *cams, const orbg_map_point *mps, const uint8_t *mdesc,
                 const int32_t *mcounts, int mcap, int npairs, float th, const float *scale,
-                const float *inv_sigma2, int nlevels, int32_t *best_idx, int32_t *best_dist,
-                int32_t *nfused);
+                const float *inv_sigma2, int nlevels, int sim3, int32_t *best_idx,
+                int32_t *best_dist, int32_t *nfused);
 int launch_distinctive(hipStream_t st, const uint8_t *pool, const int32_t *rows,
                        const int32_t *off, int npoints, int32_t *best, uint8_t *desc_out);
 int launch_pose_opt(hipStream_t st, const orbg_pose_edge *edges, const int32_t *counts, int cap,
@@ -4202,12 +4202,11 @@ extern "C" int orbg_search_for_triangulation(orbg_ctx *c, const orbg_keyframe *k
     return ORBG_OK;
 }
 
-extern "C" int orbg_fuse_batch_device(orbg_ctx *c, const orbg_keyframes *kfs, int cap,
-                                      const int32_t *d_kf, const orbg_frustum_camera *d_cams,
-                                      const orbg_map_point *d_mps, const uint8_t *d_mdesc,
-                                      const int32_t *d_mcounts, int mcap, int npairs, float th,
-                                      int32_t *d_best_idx, int32_t *d_best_dist,
-                                      int32_t *d_nfused)
+static int fuse_batch(orbg_ctx *c, const orbg_keyframes *kfs, int cap, const int32_t *d_kf,
+                      const orbg_frustum_camera *d_cams, const orbg_map_point *d_mps,
+                      const uint8_t *d_mdesc, const int32_t *d_mcounts, int mcap, int npairs,
+                      float th, int sim3, int32_t *d_best_idx, int32_t *d_best_dist,
+                      int32_t *d_nfused)
 {
     if (!c || !kfs) return set_err(ORBG_EINVAL, "NULL argument");
     if (npairs < 0 || cap <= 0 || mcap < 0) return set_err(ORBG_EINVAL, "bad sizes");
@@ -4218,18 +4217,40 @@ extern "C" int orbg_fuse_batch_device(orbg_ctx *c, const orbg_keyframes *kfs, in
     HIPCHK(hipSetDevice(c->device));
     hipStream_t st = c->stream;
     int rc = 0;
-    PROF_LAUNCH(c, "fuse",
+    PROF_LAUNCH(c, sim3 ? "fuse_sim3" : "fuse",
                 rc = launch_fuse(st, *kfs, cap, d_kf, d_cams, d_mps, d_mdesc, d_mcounts, mcap,
-                                 npairs, th, c->scale, c->inv_sigma2, c->p.nlevels, d_best_idx,
-                                 d_best_dist, d_nfused));
+                                 npairs, th, c->scale, c->inv_sigma2, c->p.nlevels, sim3,
+                                 d_best_idx, d_best_dist, d_nfused));
     if (rc == -95) return set_err(ORBG_ENOTSUP, "Fuse: more than 8192 keypoints per KeyFrame");
     if (rc) return set_err(ORBG_EIO, "k_fuse launch failed");
     return ORBG_OK;
 }
 
-extern "C" int orbg_fuse(orbg_ctx *c, const orbg_keyframe *kf, const orbg_frustum_camera *cam,
-                         const orbg_map_point *mps, const uint8_t *mdesc, int nmp, float th,
-                         int32_t *best_idx, int32_t *best_dist, int *nfused)
+extern "C" int orbg_fuse_batch_device(orbg_ctx *c, const orbg_keyframes *kfs, int cap,
+                                      const int32_t *d_kf, const orbg_frustum_camera *d_cams,
+                                      const orbg_map_point *d_mps, const uint8_t *d_mdesc,
+                                      const int32_t *d_mcounts, int mcap, int npairs, float th,
+                                      int32_t *d_best_idx, int32_t *d_best_dist,
+                                      int32_t *d_nfused)
+{
+    return fuse_batch(c, kfs, cap, d_kf, d_cams, d_mps, d_mdesc, d_mcounts, mcap, npairs, th, 0,
+                      d_best_idx, d_best_dist, d_nfused);
+}
+
+extern "C" int orbg_fuse_sim3_batch_device(orbg_ctx *c, const orbg_keyframes *kfs, int cap,
+                                           const int32_t *d_kf, const orbg_frustum_camera *d_cams,
+                                           const orbg_map_point *d_mps, const uint8_t *d_mdesc,
+                                           const int32_t *d_mcounts, int mcap, int npairs,
+                                           float th, int32_t *d_best_idx, int32_t *d_best_dist,
+                                           int32_t *d_nfused)
+{
+    return fuse_batch(c, kfs, cap, d_kf, d_cams, d_mps, d_mdesc, d_mcounts, mcap, npairs, th, 1,
+                      d_best_idx, d_best_dist, d_nfused);
+}
+
+static int fuse_host(orbg_ctx *c, const orbg_keyframe *kf, const orbg_frustum_camera *cam,
+                     const orbg_map_point *mps, const uint8_t *mdesc, int nmp, float th, int sim3,
+                     int32_t *best_idx, int32_t *best_dist, int *nfused)
 {
     if (!c || !kf || !cam || !nfused) return set_err(ORBG_EINVAL, "NULL argument");
     if (nmp < 0 || kf->n < 0) return set_err(ORBG_EINVAL, "negative size");
@@ -4281,7 +4302,7 @@ extern "C" int orbg_fuse(orbg_ctx *c, const orbg_keyframe *kf, const orbg_frustu
     rc = launch_fuse(c->stream, K, cap, (const int32_t *)(db + o_idx),
                      (const orbg_frustum_camera *)(db + o_cam), (const orbg_map_point *)(db + o_mp),
                      db + o_md, (const int32_t *)(db + o_mc), nmp, 1, th, c->scale, c->inv_sigma2,
-                     c->p.nlevels, (int32_t *)(db + o_bi), (int32_t *)(db + o_bd),
+                     c->p.nlevels, sim3, (int32_t *)(db + o_bi), (int32_t *)(db + o_bd),
                      (int32_t *)(db + o_nf));
     if (rc) return set_err(ORBG_EIO, "k_fuse launch failed");
     HIPCHK(hipMemcpyAsync(hs + o_bi, db + o_bi, o - o_bi, hipMemcpyDeviceToHost, c->stream));
@@ -4290,4 +4311,18 @@ extern "C" int orbg_fuse(orbg_ctx *c, const orbg_keyframe *kf, const orbg_frustu
     memcpy(best_dist, hs + o_bd, nm * 4);
     memcpy(nfused, hs + o_nf, 4);
     return ORBG_OK;
+}
+
+extern "C" int orbg_fuse(orbg_ctx *c, const orbg_keyframe *kf, const orbg_frustum_camera *cam,
+                         const orbg_map_point *mps, const uint8_t *mdesc, int nmp, float th,
+                         int32_t *best_idx, int32_t *best_dist, int *nfused)
+{
+    return fuse_host(c, kf, cam, mps, mdesc, nmp, th, 0, best_idx, best_dist, nfused);
+}
+
+extern "C" int orbg_fuse_sim3(orbg_ctx *c, const orbg_keyframe *kf, const orbg_frustum_camera *cam,
+                              const orbg_map_point *mps, const uint8_t *mdesc, int nmp, float th,
+                              int32_t *best_idx, int32_t *best_dist, int *nfused)
+{
+    return fuse_host(c, kf, cam, mps, mdesc, nmp, th, 1, best_idx, best_dist, nfused);
 }

@@ -240,6 +240,27 @@ class ORBmatcher:
                                   C.byref(n)), "orbg_fuse")
         return n.value, bi[:len(mps)].copy(), bd[:len(mps)].copy()
 
+    def FuseSim3(self, pKF, fcam, points, points_desc, th=4.0):
+        """ORBmatcher::Fuse(pKF, Scw, vpPoints, th, vpReplacePoint)'s search
+        (src/ORBmatcher.cc:1133-1238; LoopClosing::SearchAndFuse, th 4): fcam["Tcw"] holds
+        Scw's rows 0..2 (decomposed on the device as the reference does), points
+        MAPPOINT_DTYPE records (flags MP_VALID = !isBad() and not already in pKF), no
+        reprojection gate.  Returns (nfused, best_idx, best_dist); the caller fills
+        vpReplacePoint / adds observations in vpPoints order."""
+        kps = np.ascontiguousarray(pKF.mvKeysUn, L.KP_DTYPE)
+        desc = np.ascontiguousarray(pKF.mDescriptors, np.uint8)
+        kf = L.KeyFrame(L.ptr(kps), L.ptr(desc), None, None, len(kps), None, None, None, 0)
+        fc = np.ascontiguousarray(fcam, L.FRUSTUM_DTYPE)
+        mps = np.ascontiguousarray(points, L.MAPPOINT_DTYPE)
+        md = np.ascontiguousarray(points_desc, np.uint8).reshape(-1, 32)
+        bi = np.zeros(max(len(mps), 1), np.int32)
+        bd = np.zeros(max(len(mps), 1), np.int32)
+        n = C.c_int()
+        L.check(L.lib().orbg_fuse_sim3(_ctx(self.device).handle, C.byref(kf), L.ptr(fc),
+                                       L.ptr(mps), L.ptr(md), len(mps), float(th), L.ptr(bi),
+                                       L.ptr(bd), C.byref(n)), "orbg_fuse_sim3")
+        return n.value, bi[:len(mps)].copy(), bd[:len(mps)].copy()
+
     def SearchByBoW_KF(self, pKF1, pKF2):
         """ORBmatcher::SearchByBoW(KeyFrame *pKF1, KeyFrame *pKF2, vpMatches12)
         (src/ORBmatcher.cc:634-769): both KeyFrames with mvKeysUn, mDescriptors, mFeatVec and

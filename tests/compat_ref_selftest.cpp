@@ -99,6 +99,13 @@ struct KeyFrame {  // include/KeyFrame.h
     int mnMinX = 0, mnMinY = 0, mnMaxX = 0, mnMaxY = 0;
     cv::Mat GetPose() const { return Tcw.clone(); }
     std::vector<MapPoint *> GetMapPointMatches() const { return mvpMapPoints; }
+    std::set<MapPoint *> GetMapPoints() const  // KeyFrame.cc: the non-NULL, non-bad slots
+    {
+        std::set<MapPoint *> s;
+        for (MapPoint *p : mvpMapPoints)
+            if (p && !p->isBad()) s.insert(p);
+        return s;
+    }
     bool isBad() const { return bad; }
     MapPoint *GetMapPoint(size_t i) const { return mvpMapPoints[i]; }
     void AddMapPoint(MapPoint *p, size_t i) { mvpMapPoints[i] = p; }
@@ -656,7 +663,7 @@ int main(int argc, char **argv)
     }
 
     // ---- LocalMapping: SearchForTriangulation(KA, KB) and Fuse(KB, KA's points) ----
-    int ntri = 0, nfused = 0;
+    int ntri = 0, nfused = 0, nfused3 = 0;
     {
         auto node_of = [](const cv::KeyPoint &k) {
             return (unsigned)((int)(k.pt.x / 128) + 16 * (int)(k.pt.y / 64));
@@ -779,6 +786,46 @@ int main(int argc, char **argv)
         REQUIRE(nfused >= nadd + nrep && nadd > 100 && nrep > 50);
         for (int i = 0; i < F1.N; i++)  // every KC slot holds a live point or none
             REQUIRE(!KC.mvpMapPoints[i] || !KC.mvpMapPoints[i]->bad);
+
+        // Fuse(KE, Scw, points, 4, vpReplacePoint) (LoopClosing::SearchAndFuse): KE at KA's
+        // pose, Scw = 2 [I | 0] (a loop correction of scale 2: decomposed to exactly KA's
+        // pose).  Every third KE slot holds a point of its own -> replacement candidates; the
+        // others are added; stereo slots too (no reprojection gate).  own2[0] is already in
+        // KE: skipped.
+        KeyFrame KE = KA;
+        KE.mvpMapPoints.assign(F1.N, nullptr);
+        std::vector<MapPoint> own2(F1.N), pts(F1.N);
+        for (int i = 0; i < F1.N; i += 3) {
+            own2[i].pos = mps[i].pos.clone();
+            own2[i].obs[&KE] = (size_t)i;
+            KE.mvpMapPoints[i] = &own2[i];
+        }
+        std::vector<MapPoint *> vq;
+        for (int i = 0; i < F1.N; i++) {
+            pts[i] = mps[i];
+            pts[i].obs.clear();
+            pts[i].obs[&KA] = (size_t)i;
+            pts[i].bad = false;
+            vq.push_back(&pts[i]);
+        }
+        vq.push_back(&own2[0]);
+        cv::Mat Scw = cv::Mat::eye(4, 4, CV_32F);
+        for (int r = 0; r < 3; r++) Scw.at<float>(r, r) = 2.0f;
+        std::vector<MapPoint *> vrep(vq.size(), nullptr);
+        nfused3 = orbg_compat::ref::Fuse<Frame>(ctx, &KE, Scw, vq, 4.0f, vrep);
+        int nadd3 = 0, nrep3 = 0, nst = 0;
+        for (int i = 0; i < F1.N; i++) {
+            if (vrep[i]) {
+                REQUIRE(vrep[i] != &pts[i] && !pts[i].IsInKeyFrame(&KE));
+                nrep3 += vrep[i] == &own2[i];
+            } else if (pts[i].IsInKeyFrame(&KE)) {
+                REQUIRE(KE.mvpMapPoints[pts[i].obs[&KE]] == &pts[i]);
+                nadd3++;
+                nst += KE.mvuRight[pts[i].obs[&KE]] >= 0;
+            }
+        }
+        REQUIRE(vrep[F1.N] == nullptr && !own2[0].bad);
+        REQUIRE(nrep3 > F1.N / 4 && nadd3 > F1.N / 2 && nst > 50 && nfused3 >= nrep3 + nadd3);
     }
 
     // ---- MapPoint::ComputeDistinctiveDescriptors' BestIdx ----
@@ -808,8 +855,8 @@ int main(int argc, char **argv)
 
     std::printf("compat_ref ok: %d + %d keypoints, SearchForInitialization %d, SearchByProjection %d, "
                 "PoseOptimization inliers %d, LBA edges %zu, chi2 %.6g, SearchByBoW %d, "
-                "isInFrustum %d, SearchForTriangulation %d, Fuse %d\n",
+                "isInFrustum %d, SearchForTriangulation %d, Fuse %d, Fuse(Sim3) %d\n",
                 F1.N, F2.N, nsfi, nproj, ninl, win.edges.size(), sys.active_robust_chi2, nbow,
-                nfrustum, ntri, nfused);
+                nfrustum, ntri, nfused, nfused3);
     return 0;
 }

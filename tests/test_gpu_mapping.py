@@ -240,3 +240,77 @@ def test_fuse_batch_device(oracle):
         k = len(mp)
         assert gnf[p] == rn and np.array_equal(gbi[p, :k], rbi) and np.array_equal(gbd[p, :k], rbd)
         assert np.all(gbi[p, k:] == -9)
+
+
+# ------------------------------------------------------------------------ Fuse (Sim3)
+@pytest.mark.parametrize("seed,scale,bounds", [
+    (30, 1.0, None), (31, 0.37, None), (32, 2.9, None),
+    (33, 1.7, (10.80118465423584, 1230.0478515625, 14.668615341186523, 370.3118896484375))])
+def test_fuse_sim3_search(oracle, seed, scale, bounds):
+    """ORBmatcher::Fuse(pKF, Scw, vpPoints, 4, vpReplacePoint)'s search (k_fuse<true>) vs the
+    oracle: the Sim3 decomposed on the device, no reprojection gate, ties in grid order."""
+    kf, fcam, mps, mdesc = T.fuse_case(L, seed, n=2000, nmp=3000, scale=scale, bounds=bounds)
+    sf, _ = T._fuse_tables(oracle)
+    n, bi, bd = ORBmatcher().FuseSim3(Frame(kf["kps"], kf["desc"]), fcam, mps, mdesc, 4.0)
+    rn, rbi, rbd = oracle.fuse_sim3_search(kf, fcam.view(oracle.FRUSTUM_DTYPE),
+                                           mps.view(oracle.MAPPOINT_DTYPE), mdesc, 4.0, sf)
+    assert n == rn and np.array_equal(bi, rbi) and np.array_equal(bd, rbd)
+    assert rn > 100
+
+
+def test_fuse_sim3_empty():
+    kf, fcam, mps, mdesc = T.fuse_case(L, 5, n=50, nmp=20, scale=2.0)
+    m = ORBmatcher()
+    n, bi, bd = m.FuseSim3(Frame(kf["kps"], kf["desc"]), fcam, mps[:0], mdesc[:0])
+    assert n == 0 and len(bi) == 0
+    n, bi, bd = m.FuseSim3(Frame(kf["kps"][:0], kf["desc"][:0]), fcam, mps, mdesc)
+    assert n == 0 and np.all(bi == -1) and np.all(bd == 256)
+
+
+def test_fuse_sim3_batch_device(oracle):
+    """LoopClosing::SearchAndFuse's shape: the loop's map points fused into each KeyFrame of
+    the corrected neighbourhood, one Sim3 per KeyFrame, all in HBM (no mvuRight array)."""
+    import ctypes as C
+    import torch
+    P, cap, mcap = 5, 2200, 2400
+    sf, _ = T._fuse_tables(oracle)
+    cases = [T.fuse_case(L, 60 + p, n=1700 + 100 * p, nmp=1500 + 200 * p, scale=0.5 + 0.4 * p)
+             for p in range(P)]
+    desc = np.zeros((P, cap, 32), np.uint8)
+    kps = np.zeros((P, cap), L.KP_DTYPE)
+    cnt = np.zeros(P, np.int32)
+    cams = np.zeros(P, L.FRUSTUM_DTYPE)
+    mps = np.zeros((P, mcap), L.MAPPOINT_DTYPE)
+    md = np.zeros((P, mcap, 32), np.uint8)
+    mc = np.zeros(P, np.int32)
+    for p, (kf, fc, mp, mdsc) in enumerate(cases):
+        n = len(kf["kps"])
+        desc[p, :n], kps[p, :n], cnt[p] = kf["desc"], kf["kps"], n
+        cams[p] = fc
+        mps[p, :len(mp)], md[p, :len(mp)], mc[p] = mp, mdsc, len(mp)
+    t = {k: torch.from_numpy(np.ascontiguousarray(v).view(np.uint8).reshape(-1).copy()).cuda()
+         for k, v in dict(desc=desc, kps=kps, cnt=cnt, cams=cams, mps=mps, md=md,
+                          mc=mc).items()}
+    K = L.KeyFrames(t["desc"].data_ptr(), t["kps"].data_ptr(), None, None,
+                    t["cnt"].data_ptr(), None, None, None, None)
+    kfi = torch.arange(P, dtype=torch.int32, device="cuda")
+    bi = torch.full((P * mcap,), -9, dtype=torch.int32, device="cuda")
+    bd = torch.full((P * mcap,), -9, dtype=torch.int32, device="cuda")
+    nf = torch.zeros(P, dtype=torch.int32, device="cuda")
+    ctx = _ctx()
+    torch.cuda.synchronize()
+    L.check(L.lib().orbg_fuse_sim3_batch_device(ctx.handle, C.byref(K), cap, kfi.data_ptr(),
+                                                t["cams"].data_ptr(), t["mps"].data_ptr(),
+                                                t["md"].data_ptr(), t["mc"].data_ptr(), mcap, P,
+                                                4.0, bi.data_ptr(), bd.data_ptr(),
+                                                nf.data_ptr()), "fuse_sim3")
+    ctx.sync()
+    gbi = bi.cpu().numpy().reshape(P, mcap)
+    gbd = bd.cpu().numpy().reshape(P, mcap)
+    gnf = nf.cpu().numpy()
+    for p, (kf, fc, mp, mdsc) in enumerate(cases):
+        rn, rbi, rbd = oracle.fuse_sim3_search(kf, fc.view(oracle.FRUSTUM_DTYPE),
+                                               mp.view(oracle.MAPPOINT_DTYPE), mdsc, 4.0, sf)
+        k = len(mp)
+        assert gnf[p] == rn and np.array_equal(gbi[p, :k], rbi) and np.array_equal(gbd[p, :k], rbd)
+        assert np.all(gbi[p, k:] == -9) and rn > 100

@@ -248,7 +248,7 @@ def test_triangulation_empty(oracle):
 
 
 # ------------------------------------------------------------------------ Fuse
-def fuse_case(mod, seed, n=2000, nmp=1500, w=1241, h=376, ties=True, bounds=None):
+def fuse_case(mod, seed, n=2000, nmp=1500, w=1241, h=376, ties=True, bounds=None, scale=None):
     """A KeyFrame (mvKeysUn, mDescriptors, mvuRight, its FRUSTUM_DTYPE state) and nmp map
     points: most project next to one of its keypoints with a noisy copy of its descriptor
     (fusion targets), some carry a descriptor equal to several nearby keypoints' (ties broken
@@ -301,7 +301,8 @@ def fuse_case(mod, seed, n=2000, nmp=1500, w=1241, h=376, ties=True, bounds=None
             kp["octave"][near] = kp["octave"][s]
             mdesc[j] = desc[s]
     fcam = np.zeros((), mod.FRUSTUM_DTYPE)
-    fcam["Tcw"] = Tcw.reshape(12)
+    # LoopClosing's Scw = Converter::toCvMat(g2o::Sim3): s * R and the scaled translation
+    fcam["Tcw"] = (Tcw if scale is None else (np.float64(scale) * Tcw).astype(np.float32)).reshape(12)
     for k, val in zip(("fx", "fy", "cx", "cy", "bf", "log_scale_factor"),
                       (fx, fy, cx, cy, BF, np.float32(np.log(np.float64(np.float32(1.2)))))):
         fcam[k] = val
@@ -311,10 +312,24 @@ def fuse_case(mod, seed, n=2000, nmp=1500, w=1241, h=376, ties=True, bounds=None
     return dict(kps=kp, desc=desc, uright=ur), fcam, mps, mdesc
 
 
-def py_fuse(kf, fcam, mps, mdesc, th, sf, isg):
-    """pure-Python restatement of Fuse's search over the reference grid and order."""
+def py_sim3_decompose(S):
+    """Fuse(pKF, Scw, ...)'s scw = sqrt(row0 . row0) (double products), Rcw | tcw = Scw / scw
+    (float alpha = 1 / scw, one rounding per element)."""
+    S = np.asarray(S, np.float32).reshape(3, 4)
+    d = 0.0
+    for k in range(3):
+        d += float(S[0, k]) * float(S[0, k])
+    scw = np.float32(np.sqrt(d))
+    a = np.float32(1.0 / float(scw))
+    return (S * a).astype(np.float32)
+
+
+def py_fuse(kf, fcam, mps, mdesc, th, sf, isg, sim3=False):
+    """pure-Python restatement of Fuse's search over the reference grid and order; sim3: the
+    Fuse(pKF, Scw, vpPoints, th, vpReplacePoint) variant (Scw decomposed, no reprojection
+    gate, ORBmatcher.cc:1133-1238)."""
     f32 = np.float32
-    T = fcam["Tcw"].reshape(3, 4)
+    T = py_sim3_decompose(fcam["Tcw"]) if sim3 else fcam["Tcw"].reshape(3, 4)
     b = (f32(fcam["min_x"]), f32(fcam["max_x"]), f32(fcam["min_y"]), f32(fcam["max_y"]))
     iw = f32(64) / f32(b[1] - b[0])
     ih = f32(48) / f32(b[3] - b[2])
@@ -371,7 +386,9 @@ def py_fuse(kf, fcam, mps, mdesc, th, sf, isg):
                     if k["octave"] < lvl - 1 or k["octave"] > lvl:
                         continue
                     ex, ey = u - k["x"], v - k["y"]
-                    if kf["uright"][idx] >= 0:
+                    if sim3:
+                        pass
+                    elif kf["uright"][idx] >= 0:
                         er = ur - kf["uright"][idx]
                         if float((ex * ex + ey * ey + er * er) * isg[k["octave"]]) > 7.8:
                             continue
@@ -412,3 +429,30 @@ def test_fuse_fractional_bounds(oracle):
     n, bi, bd = oracle.fuse_search(kf, fcam, mps, mdesc, 3.0, sf, isg)
     rn, rbi, rbd = py_fuse(kf, fcam, mps, mdesc, 3.0, sf, isg)
     assert n == rn and np.array_equal(bi, rbi) and np.array_equal(bd, rbd) and n > 50
+
+
+@pytest.mark.parametrize("seed,scale", [(20, 1.0), (21, 0.37), (22, 2.9)])
+def test_fuse_sim3_equals_python(oracle, seed, scale):
+    """Fuse(pKF, Scw, vpPoints, th = 4, vpReplacePoint) (LoopClosing::SearchAndFuse): the Sim3
+    decomposition and the search without the reprojection gate, C vs Python"""
+    kf, fcam, mps, mdesc = fuse_case(oracle, seed, n=1200, nmp=500, scale=scale)
+    sf, isg = _fuse_tables(oracle)
+    assert np.array_equal(oracle.sim3_decompose(fcam["Tcw"]), py_sim3_decompose(fcam["Tcw"]))
+    n, bi, bd = oracle.fuse_sim3_search(kf, fcam, mps, mdesc, 4.0, sf)
+    rn, rbi, rbd = py_fuse(kf, fcam, mps, mdesc, 4.0, sf, isg, sim3=True)
+    assert n == rn and np.array_equal(bi, rbi) and np.array_equal(bd, rbd)
+    assert n > 50 and (bd < 256).sum() > n
+    # without the reprojection gate at least as many points find a target as in Fuse(pKF, ...)
+    f1 = fcam.copy()
+    f1["Tcw"] = py_sim3_decompose(fcam["Tcw"]).reshape(12)
+    n1, _, _ = oracle.fuse_search(kf, f1, mps, mdesc, 4.0, sf, isg)
+    assert n >= n1
+
+
+def test_sim3_decompose_known():
+    """scale 2 of an exact rotation: Rcw and tcw come back exactly (power-of-two alpha)"""
+    from oracle import pyoracle as O
+    R = np.array([[0, -1, 0], [1, 0, 0], [0, 0, 1]], np.float32)
+    S = np.concatenate([2 * R, np.array([[2.0], [-4.0], [6.0]], np.float32)], 1)
+    T = O.sim3_decompose(S)
+    assert np.array_equal(T[:, :3], R) and np.array_equal(T[:, 3], [1, -2, 3])

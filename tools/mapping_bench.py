@@ -13,6 +13,9 @@ oracle (oracle/mapping_oracle.c) on one host core over a bounded sample:
              (KeyFrame, 2000 MapPoints) pairs per launch: map points/s.  Bytes: per KeyFrame
              the keypoints, descriptors and mvuRight (64 B per keypoint); per MapPoint its
              record and descriptor (68 B) and bestIdx / bestDist (8 B).
+  fuse_sim3  ORBmatcher::Fuse(pKF, Scw, vpPoints, th = 4, vpReplacePoint)'s search
+             (LoopClosing::SearchAndFuse): the same shape with one Sim3 per KeyFrame (no
+             mvuRight: 60 B per keypoint).
 
     python tools/mapping_bench.py [--steps 20] [--warmup 3] [--no-cpu] [--only NAME]
 """
@@ -142,59 +145,79 @@ def main():
                                  "%.2f s" % (calls, cdt)}
         print(json.dumps(r), flush=True)
 
-    if args.only in ("", "fuse"):
-        NQ, REP, cap, mcap = 32, 8, 2048, 2000
-        cases = [T.fuse_case(L, 700 + q, n=2000, nmp=mcap) for q in range(NQ)]
-        desc = np.zeros((NQ, cap, 32), np.uint8)
-        kps = np.zeros((NQ, cap), L.KP_DTYPE)
-        ur = np.zeros((NQ, cap), np.float32)
-        cnt = np.zeros(NQ, np.int32)
-        P = NQ * REP
-        cams = np.zeros(P, L.FRUSTUM_DTYPE)
-        mps = np.zeros((P, mcap), L.MAPPOINT_DTYPE)
-        md = np.zeros((P, mcap, 32), np.uint8)
-        mc = np.full(P, mcap, np.int32)
-        for j, (kf, fc, m, mdsc) in enumerate(cases):
-            desc[j, :2000], kps[j, :2000], ur[j, :2000], cnt[j] = kf["desc"], kf["kps"], kf["uright"], 2000
-        for p in range(P):
-            kf, fc, m, mdsc = cases[p % NQ]
-            cams[p], mps[p], md[p] = fc, m, mdsc
-        t = {k: dev(v) for k, v in dict(desc=desc, kps=kps, ur=ur, cnt=cnt, cams=cams, mps=mps,
-                                        md=md, mc=mc).items()}
-        K = L.KeyFrames(t["desc"].data_ptr(), t["kps"].data_ptr(), t["ur"].data_ptr(), None,
-                        t["cnt"].data_ptr(), None, None, None, None)
-        kfi = torch.from_numpy((np.arange(P) % NQ).astype(np.int32)).cuda()
-        bi = torch.empty(P * mcap, dtype=torch.int32, device="cuda")
-        bd = torch.empty(P * mcap, dtype=torch.int32, device="cuda")
-        nf = torch.empty(P, dtype=torch.int32, device="cuda")
+    for sim3 in (False, True):
+        if args.only not in ("", "fuse_sim3" if sim3 else "fuse"):
+            continue
+        fuse_line(args, L, T, O, ctx, h, sim3)
 
-        def run():
-            L.check(L.lib().orbg_fuse_batch_device(h, C.byref(K), cap, kfi.data_ptr(),
-                                                   t["cams"].data_ptr(), t["mps"].data_ptr(),
-                                                   t["md"].data_ptr(), t["mc"].data_ptr(), mcap,
-                                                   P, 3.0, bi.data_ptr(), bd.data_ptr(),
-                                                   nf.data_ptr()), "fuse")
-        s_step, avg = timed(ctx, "fuse", run, args.steps, args.warmup)
-        algo = P * (2000 * 64 + mcap * 76)
-        r = line("ORBmatcher::Fuse(pKF, vpMapPoints) search: map points/s (SearchInNeighbors)",
-                 "points/s", P * mcap, s_step, avg, algo,
-                 "%d (KeyFrame of 2000 keypoints, 2000 MapPoints) pairs, th 3" % P,
-                 {"dtype": "f32/f64", "fused_per_pair": round(float(nf.cpu().numpy().mean()), 1)})
-        if O is not None:
-            p = O.params(nfeatures=2000)
-            sf, isg = np.array(p.scale[:8], np.float32), np.array(p.inv_sigma2[:8], np.float32)
-            t0 = time.perf_counter()
-            calls = 0
-            while time.perf_counter() - t0 < 3.0:
-                kf, fc, m, mdsc = cases[calls % NQ]
-                O.fuse_search(kf, fc.view(O.FRUSTUM_DTYPE), m.view(O.MAPPOINT_DTYPE), mdsc, 3.0,
-                              sf, isg)
-                calls += 1
-            cdt = time.perf_counter() - t0
-            r["cpu_baseline"] = {"value": round(calls * mcap / cdt, 1), "unit": "points/s",
-                                 "cores": 1, "kind": "port", "sample": "%d x %d map points, "
-                                 "oracle -O3, one thread, %.2f s" % (calls, mcap, cdt)}
-        print(json.dumps(r), flush=True)
+
+def fuse_line(args, L, T, O, ctx, h, sim3):
+    import torch
+    NQ, REP, cap, mcap = 32, 8, 2048, 2000
+    cases = [T.fuse_case(L, 700 + q, n=2000, nmp=mcap, scale=(0.6 + 0.05 * q) if sim3 else None)
+             for q in range(NQ)]
+    desc = np.zeros((NQ, cap, 32), np.uint8)
+    kps = np.zeros((NQ, cap), L.KP_DTYPE)
+    ur = np.zeros((NQ, cap), np.float32)
+    cnt = np.zeros(NQ, np.int32)
+    P = NQ * REP
+    cams = np.zeros(P, L.FRUSTUM_DTYPE)
+    mps = np.zeros((P, mcap), L.MAPPOINT_DTYPE)
+    md = np.zeros((P, mcap, 32), np.uint8)
+    mc = np.full(P, mcap, np.int32)
+    for j, (kf, fc, m, mdsc) in enumerate(cases):
+        desc[j, :2000], kps[j, :2000], ur[j, :2000], cnt[j] = kf["desc"], kf["kps"], kf["uright"], 2000
+    for p in range(P):
+        kf, fc, m, mdsc = cases[p % NQ]
+        cams[p], mps[p], md[p] = fc, m, mdsc
+    t = {k: dev(v) for k, v in dict(desc=desc, kps=kps, ur=ur, cnt=cnt, cams=cams, mps=mps,
+                                    md=md, mc=mc).items()}
+    K = L.KeyFrames(t["desc"].data_ptr(), t["kps"].data_ptr(), t["ur"].data_ptr(), None,
+                    t["cnt"].data_ptr(), None, None, None, None)
+    kfi = torch.from_numpy((np.arange(P) % NQ).astype(np.int32)).cuda()
+    bi = torch.empty(P * mcap, dtype=torch.int32, device="cuda")
+    bd = torch.empty(P * mcap, dtype=torch.int32, device="cuda")
+    nf = torch.empty(P, dtype=torch.int32, device="cuda")
+
+    fn = L.lib().orbg_fuse_sim3_batch_device if sim3 else L.lib().orbg_fuse_batch_device
+    th = 4.0 if sim3 else 3.0
+
+    def run():
+        L.check(fn(h, C.byref(K), cap, kfi.data_ptr(), t["cams"].data_ptr(),
+                   t["mps"].data_ptr(), t["md"].data_ptr(), t["mc"].data_ptr(), mcap, P, th,
+                   bi.data_ptr(), bd.data_ptr(), nf.data_ptr()), "fuse")
+    s_step, avg = timed(ctx, "fuse_sim3" if sim3 else "fuse", run, args.steps, args.warmup)
+    # per KeyFrame its keypoints and descriptors (+ mvuRight unless Sim3); per MapPoint
+    # its record, descriptor and bestIdx / bestDist
+    algo = P * (2000 * (60 if sim3 else 64) + mcap * 76)
+    if sim3:
+        title = ("ORBmatcher::Fuse(pKF, Scw, vpPoints, th, vpReplacePoint) search: map "
+                 "points/s (LoopClosing::SearchAndFuse)")
+        wl = "%d (KeyFrame of 2000 keypoints, 2000 loop MapPoints, Sim3 scale 0.6-2.15) pairs, th 4" % P
+    else:
+        title = "ORBmatcher::Fuse(pKF, vpMapPoints) search: map points/s (SearchInNeighbors)"
+        wl = "%d (KeyFrame of 2000 keypoints, 2000 MapPoints) pairs, th 3" % P
+    r = line(title, "points/s", P * mcap, s_step, avg, algo, wl,
+             {"dtype": "f32/f64", "fused_per_pair": round(float(nf.cpu().numpy().mean()), 1)})
+    if O is not None:
+        p = O.params(nfeatures=2000)
+        sf, isg = np.array(p.scale[:8], np.float32), np.array(p.inv_sigma2[:8], np.float32)
+        t0 = time.perf_counter()
+        calls = 0
+        while time.perf_counter() - t0 < 3.0:
+            kf, fc, m, mdsc = cases[calls % NQ]
+            if sim3:
+                O.fuse_sim3_search(kf, fc.view(O.FRUSTUM_DTYPE), m.view(O.MAPPOINT_DTYPE),
+                                   mdsc, th, sf)
+            else:
+                O.fuse_search(kf, fc.view(O.FRUSTUM_DTYPE), m.view(O.MAPPOINT_DTYPE), mdsc,
+                              th, sf, isg)
+            calls += 1
+        cdt = time.perf_counter() - t0
+        r["cpu_baseline"] = {"value": round(calls * mcap / cdt, 1), "unit": "points/s",
+                             "cores": 1, "kind": "port", "sample": "%d x %d map points, "
+                             "oracle -O3, one thread, %.2f s" % (calls, mcap, cdt)}
+    print(json.dumps(r), flush=True)
 
 
 if __name__ == "__main__":
