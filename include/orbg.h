@@ -50,6 +50,8 @@
  *                                     (LocalMapping::CreateNewMapPoints, LocalMapping.cc:378)
  *   orbg_fuse ....................... ORBmatcher::Fuse(pKF, vpMapPoints, th)'s per-MapPoint search
  *   orbg_fuse_sim3 .................. ORBmatcher::Fuse(pKF, Scw, vpPoints, th, vpReplacePoint)'s search
+ *   orbg_search_by_projection_reloc . ORBmatcher::SearchByProjection(CurrentFrame, pKF, sAlreadyFound, th, ORBdist)
+ *   orbg_search_by_projection_sim3 .. ORBmatcher::SearchByProjection(pKF, Scw, vpPoints, vpMatched, th)
  *                                     src/ORBmatcher.cc:968-1069 (LocalMapping::SearchInNeighbors,
  *                                     LocalMapping.cc:622-690)
  *   orbg_ba_linearize ............... g2o computeActiveErrors + BlockSolver::buildSystem arithmetic
@@ -353,11 +355,15 @@ int orbg_search_by_projection_local(orbg_ctx *ctx, const orbg_keypoint *kps,
                                     const orbg_map_projection *mps, const uint8_t *mdesc, int nm,
                                     float th, float nnratio, int32_t *match, int *nmatches);
 
-/* Batched, device-resident form of both (mode ORBG_TRACK_LASTFRAME / ORBG_TRACK_LOCAL):
- * every pointer is device memory, frame f's arrays at f * frame_cap (keypoint side) and
+/* Batched, device-resident form of both (mode ORBG_TRACK_LASTFRAME / ORBG_TRACK_LOCAL) and
+ * of the relocalization / loop searches below (ORBG_TRACK_RELOC / ORBG_TRACK_LOOP): every
+ * pointer is device memory, frame f's arrays at f * frame_cap (keypoint side) and
  * f * query_cap (query side); enqueued on the context stream. */
 #define ORBG_TRACK_LASTFRAME 0
 #define ORBG_TRACK_LOCAL 1
+#define ORBG_TRACK_RELOC 2
+#define ORBG_TRACK_LOOP 3
+struct orbg_frustum_camera;
 typedef struct {
     const orbg_keypoint *kps;    /* [B][frame_cap] */
     const uint8_t *desc;         /* [B][frame_cap][32] */
@@ -366,7 +372,8 @@ typedef struct {
     const int32_t *counts;       /* [B] */
     const orbg_bounds *bounds;   /* [B] */
     int32_t frame_cap;
-    const void *queries;         /* [B][query_cap] orbg_lastframe_point / orbg_map_projection */
+    const void *queries;         /* [B][query_cap] orbg_lastframe_point / orbg_map_projection /
+                                    orbg_reloc_point / orbg_map_point, by mode */
     const uint8_t *qdesc;        /* [B][query_cap][32] */
     const int32_t *qcounts;      /* [B] */
     int32_t query_cap;
@@ -375,6 +382,8 @@ typedef struct {
     int32_t check_ori;
     int32_t *match;              /* [B][frame_cap] out */
     int32_t *nmatches;           /* [B] out */
+    const struct orbg_frustum_camera *fcams;  /* [B], relocalization / loop modes */
+    int32_t orb_dist;            /* relocalization: ORBdist */
 } orbg_track_batch;
 int orbg_search_by_projection_batch_device(orbg_ctx *ctx, int mode, const orbg_track_batch *tb,
                                            int nframes);
@@ -424,7 +433,7 @@ typedef struct {
 } orbg_map_point;
 /* The Frame state isInFrustum reads: mTcw rows 0..2 (row-major 3x4), fx, fy, cx, cy, mbf,
  * mfLogScaleFactor (= log(mfScaleFactor), in double then float), mnScaleLevels, mnMinX.. */
-typedef struct {
+typedef struct orbg_frustum_camera {
     float Tcw[12];
     float fx, fy, cx, cy, bf;
     float log_scale_factor;
@@ -552,6 +561,36 @@ int orbg_fuse_sim3_batch_device(orbg_ctx *ctx, const orbg_keyframes *kfs, int ca
                                 const orbg_map_point *d_mps, const uint8_t *d_mdesc,
                                 const int32_t *d_mcounts, int mcap, int npairs, float th,
                                 int32_t *d_best_idx, int32_t *d_best_dist, int32_t *d_nfused);
+
+/* ORBmatcher(0.75, checkOri).SearchByProjection(CurrentFrame, pKF, sAlreadyFound, th,
+ * ORBdist) (src/ORBmatcher.cc:1670-1798; Tracking::Relocalization, Tracking.cc:2120 th 10 /
+ * ORBdist 100, :2141 th 3 / 64): the CurrentFrame side is kps / desc (mvKeysUn,
+ * mDescriptors), taken0[i2] = mvpMapPoints[i2] != NULL on entry (NULL: none), cam =
+ * CurrentFrame's pose, fx.., mfLogScaleFactor, mnScaleLevels and mnMinX..; pts[i] =
+ * pKF->GetMapPointMatches()[i] with pKF->mvKeysUn[i].angle (flags ORBG_MP_VALID = pMP &&
+ * !isBad() && !sAlreadyFound.count(pMP)).  match[i2] = the pKF index written to
+ * mvpMapPoints[i2], -1 untouched, -2 set to NULL by the rotation filter. */
+typedef struct {
+    float x, y, z;            /* GetWorldPos() */
+    float min_dist, max_dist; /* mfMinDistance, mfMaxDistance */
+    float angle;              /* pKF->mvKeysUn[i].angle */
+    int32_t flags;
+} orbg_reloc_point;
+int orbg_search_by_projection_reloc(orbg_ctx *ctx, const orbg_keypoint *kps, const uint8_t *desc,
+                                    int n, const uint8_t *taken0, const orbg_frustum_camera *cam,
+                                    const orbg_reloc_point *pts, const uint8_t *pdesc, int np,
+                                    float th, int orb_dist, int check_ori, int32_t *match,
+                                    int *nmatches);
+/* ORBmatcher::SearchByProjection(pKF, Scw, vpPoints, vpMatched, th) (src/ORBmatcher.cc:
+ * 353-470; LoopClosing::ComputeSim3, LoopClosing.cc:669, th 10): kps / desc = pKF's,
+ * taken0[idx] = vpMatched[idx] != NULL on entry, cam->Tcw = Scw rows 0..2 (decomposed on the
+ * device as orbg_fuse_sim3 does), cam->bounds the Frame's float bounds (the KeyFrame's int
+ * bounds are their truncation); mps[i] = vpPoints[i] (flags ORBG_MP_VALID = !isBad() && not
+ * in vpMatched on entry).  match[idx] = the vpPoints index written to vpMatched[idx], -1. */
+int orbg_search_by_projection_sim3(orbg_ctx *ctx, const orbg_keypoint *kps, const uint8_t *desc,
+                                   int n, const uint8_t *taken0, const orbg_frustum_camera *cam,
+                                   const orbg_map_point *mps, const uint8_t *mdesc, int nm,
+                                   int th, int32_t *match, int *nmatches);
 
 /* ---------------- Optimizer::PoseOptimization ----------------
  * One edge per Frame keypoint with a MapPoint (index order): EdgeSE3ProjectXYZOnlyPose when

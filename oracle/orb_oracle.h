@@ -295,6 +295,33 @@ int orc_fuse_sim3_search(const orc_tri_kf *kf, const orc_frustum_cam *cam,
                          const orc_map_point *mps, const uint8_t *mdesc, int nmp, float th,
                          const float *scale_factors, int32_t *best_idx, int32_t *best_dist);
 
+/* loop_oracle.c.  ORBmatcher::SearchByProjection(CurrentFrame, pKF, sAlreadyFound, th,
+ * ORBdist) (ORBmatcher.cc:1670-1798): pts[i] = pKF->GetMapPointMatches()[i] (flags
+ * ORC_MP_VALID = pMP && !isBad() && !sAlreadyFound.count(pMP)), angle = pKF->mvKeysUn[i].angle;
+ * cam = CurrentFrame (mTcw, fx.., mfLogScaleFactor, mnScaleLevels, float bounds); taken0[i2]
+ * = CurrentFrame.mvpMapPoints[i2] != NULL on entry.  match[i2] = the pKF index written to
+ * mvpMapPoints[i2], -1, or -2 (NULLed by the rotation filter); returns nmatches. */
+typedef struct {
+    float x, y, z;            /* GetWorldPos() */
+    float min_dist, max_dist; /* mfMinDistance, mfMaxDistance */
+    float angle;              /* pKF->mvKeysUn[i].angle */
+    int32_t flags;
+} orc_reloc_point;
+int orc_search_by_projection_reloc(const orc_keypoint *kps, const uint8_t *desc, int n,
+                                   const uint8_t *taken0, const orc_frustum_cam *cam,
+                                   const float *scale_factors, const orc_reloc_point *pts,
+                                   const uint8_t *pdesc, int np, float th, int orb_dist,
+                                   int check_ori, int32_t *match);
+/* ORBmatcher::SearchByProjection(pKF, Scw, vpPoints, vpMatched, th) (ORBmatcher.cc:353-470):
+ * kps / desc = pKF's mvKeysUn / mDescriptors, cam->Tcw = Scw rows 0..2 (decomposed as in
+ * orc_fuse_sim3_search), cam->bounds the Frame's float bounds (the KeyFrame's int ones are
+ * their truncation); mps[i] flags ORC_MP_VALID = !isBad() && not in vpMatched on entry;
+ * taken0[idx] = vpMatched[idx] != NULL.  match[idx] = the vpPoints index written. */
+int orc_search_by_projection_sim3(const orc_keypoint *kps, const uint8_t *desc, int n,
+                                  const uint8_t *taken0, const orc_frustum_cam *cam,
+                                  const float *scale_factors, const orc_map_point *mps,
+                                  const uint8_t *mdesc, int nm, int th, int32_t *match);
+
 /* ---- Optimizer::PoseOptimization (pose_oracle.c) ---- */
 /* LM's pow(2 rho - 1, 3) as the once-rounded exact cube (optimization_algorithm_levenberg.cpp:135) */
 double orc_lm_cube(double t);

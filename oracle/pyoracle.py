@@ -47,6 +47,8 @@ CAMERA_DTYPE = np.dtype([("fx", "<f4"), ("fy", "<f4"), ("cx", "<f4"), ("cy", "<f
 MAPPOINT_DTYPE = np.dtype([("x", "<f4"), ("y", "<f4"), ("z", "<f4"), ("nx", "<f4"),
                            ("ny", "<f4"), ("nz", "<f4"), ("min_dist", "<f4"),
                            ("max_dist", "<f4"), ("flags", "<i4")])
+RELOC_DTYPE = np.dtype([("x", "<f4"), ("y", "<f4"), ("z", "<f4"), ("min_dist", "<f4"),
+                        ("max_dist", "<f4"), ("angle", "<f4"), ("flags", "<i4")])
 FRUSTUM_DTYPE = np.dtype([("Tcw", "<f4", 12), ("fx", "<f4"), ("fy", "<f4"), ("cx", "<f4"),
                           ("cy", "<f4"), ("bf", "<f4"), ("log_scale_factor", "<f4"),
                           ("nlevels", "<i4"), ("min_x", "<f4"), ("max_x", "<f4"),
@@ -200,6 +202,12 @@ def lib():
         L.orc_fuse_sim3_search.argtypes = [P(TriKF), vp, vp, vp, C.c_int, C.c_float, vp, vp, vp]
         L.orc_fuse_sim3_search.restype = C.c_int
         L.orc_sim3_decompose.argtypes = [vp, vp]
+        L.orc_search_by_projection_reloc.argtypes = [vp, vp, C.c_int, vp, vp, vp, vp, vp,
+                                                     C.c_int, C.c_float, C.c_int, C.c_int, vp]
+        L.orc_search_by_projection_reloc.restype = C.c_int
+        L.orc_search_by_projection_sim3.argtypes = [vp, vp, C.c_int, vp, vp, vp, vp, vp,
+                                                    C.c_int, C.c_int, vp]
+        L.orc_search_by_projection_sim3.restype = C.c_int
         L.orc_sim3_decompose.restype = None
         L.orc_search_by_bow_kf.restype = C.c_int
         L.orc_search_by_bow_kf.argtypes = [vp, vp, vp, C.c_int, vp, vp, vp, C.c_int, vp, vp, vp,
@@ -776,3 +784,36 @@ def fuse_sim3_search(kf, fcam, mps, mdesc, th, scale_factors):
     n = lib().orc_fuse_sim3_search(C.byref(k), _p(fcam), _p(mps), _p(md), len(mps), float(th),
                                    _p(sf), _p(bi), _p(bd))
     return n, bi[:len(mps)], bd[:len(mps)]
+
+
+def search_by_projection_reloc(kps, desc, taken0, fcam, scale_factors, pts, pdesc, th, orb_dist,
+                               check_ori=True):
+    """ORBmatcher::SearchByProjection(CurrentFrame, pKF, sAlreadyFound, th, ORBdist)
+    (oracle/loop_oracle.c).  fcam: CurrentFrame's FRUSTUM_DTYPE state; pts RELOC_DTYPE.
+    Returns (nmatches, match[n]: pKF point index written, -1, or -2 NULLed by the rotation
+    filter)."""
+    kps, desc, _, tk = _frame_args(kps, desc, None, taken0)
+    fcam = np.ascontiguousarray(fcam, FRUSTUM_DTYPE)
+    pts = np.ascontiguousarray(pts, RELOC_DTYPE)
+    pdesc = np.ascontiguousarray(pdesc, np.uint8)
+    sf = np.ascontiguousarray(scale_factors, np.float32)
+    match = np.zeros(max(len(kps), 1), np.int32)
+    n = lib().orc_search_by_projection_reloc(_p(kps), _p(desc), len(kps), _p(tk), _p(fcam),
+                                             _p(sf), _p(pts), _p(pdesc), len(pts), float(th),
+                                             int(orb_dist), 1 if check_ori else 0, _p(match))
+    return n, match[:len(kps)].copy()
+
+
+def search_by_projection_sim3(kps, desc, taken0, fcam, scale_factors, mps, mdesc, th):
+    """ORBmatcher::SearchByProjection(pKF, Scw, vpPoints, vpMatched, th) (oracle/loop_oracle.c):
+    fcam["Tcw"] = Scw rows 0..2.  Returns (nmatches, match[n]: vpPoints index written, -1)."""
+    kps, desc, _, tk = _frame_args(kps, desc, None, taken0)
+    fcam = np.ascontiguousarray(fcam, FRUSTUM_DTYPE)
+    mps = np.ascontiguousarray(mps, MAPPOINT_DTYPE)
+    mdesc = np.ascontiguousarray(mdesc, np.uint8)
+    sf = np.ascontiguousarray(scale_factors, np.float32)
+    match = np.zeros(max(len(kps), 1), np.int32)
+    n = lib().orc_search_by_projection_sim3(_p(kps), _p(desc), len(kps), _p(tk), _p(fcam),
+                                            _p(sf), _p(mps), _p(mdesc), len(mps), int(th),
+                                            _p(match))
+    return n, match[:len(kps)].copy()

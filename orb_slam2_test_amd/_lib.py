@@ -39,7 +39,7 @@ EDGE_OUT_DTYPE = np.dtype([("err", "<f8", 3), ("chi2", "<f8"), ("rho1", "<f8"),
 
 # tracking matcher records (orbg_lastframe_point, orbg_map_projection)
 MP_VALID, MP_HAS_OBS = 1, 2
-TRACK_LASTFRAME, TRACK_LOCAL = 0, 1
+TRACK_LASTFRAME, TRACK_LOCAL, TRACK_RELOC, TRACK_LOOP = 0, 1, 2, 3
 LF_DTYPE = np.dtype([("x", "<f4"), ("y", "<f4"), ("z", "<f4"), ("octave", "<i4"),
                      ("angle", "<f4"), ("flags", "<i4")])
 MP_DTYPE = np.dtype([("u", "<f4"), ("v", "<f4"), ("ur", "<f4"), ("level", "<i4"),
@@ -50,6 +50,8 @@ MP_DTYPE = np.dtype([("u", "<f4"), ("v", "<f4"), ("ur", "<f4"), ("level", "<i4")
 CAMERA_DTYPE = np.dtype([("fx", "<f4"), ("fy", "<f4"), ("cx", "<f4"), ("cy", "<f4"),
                          ("k1", "<f4"), ("k2", "<f4"), ("p1", "<f4"), ("p2", "<f4"),
                          ("k3", "<f4")])
+RELOC_DTYPE = np.dtype([("x", "<f4"), ("y", "<f4"), ("z", "<f4"), ("min_dist", "<f4"),
+                        ("max_dist", "<f4"), ("angle", "<f4"), ("flags", "<i4")])
 MAPPOINT_DTYPE = np.dtype([("x", "<f4"), ("y", "<f4"), ("z", "<f4"), ("nx", "<f4"),
                            ("ny", "<f4"), ("nz", "<f4"), ("min_dist", "<f4"),
                            ("max_dist", "<f4"), ("flags", "<i4")])
@@ -98,7 +100,8 @@ class TrackBatch(C.Structure):
                 ("frame_cap", C.c_int32), ("queries", C.c_void_p), ("qdesc", C.c_void_p),
                 ("qcounts", C.c_void_p), ("query_cap", C.c_int32), ("cams", C.c_void_p),
                 ("th", C.c_float), ("nnratio", C.c_float), ("check_ori", C.c_int32),
-                ("match", C.c_void_p), ("nmatches", C.c_void_p)]
+                ("match", C.c_void_p), ("nmatches", C.c_void_p), ("fcams", C.c_void_p),
+                ("orb_dist", C.c_int32)]
 
 
 def track_camera(Tcw, Tlw, fx, fy, cx, cy, bf, b, mono):
@@ -249,6 +252,10 @@ def lib():
         "orbg_fuse": (i32, [vp, P(KeyFrame), vp, vp, vp, i32, f32, vp, vp, P(i32)]),
         "orbg_fuse_batch_device": (i32, [vp, P(KeyFrames), i32, vp, vp, vp, vp, vp, i32, i32, f32,
                                          vp, vp, vp]),
+        "orbg_search_by_projection_reloc": (i32, [vp, vp, vp, i32, vp, vp, vp, vp, i32, f32, i32,
+                                                  i32, vp, P(i32)]),
+        "orbg_search_by_projection_sim3": (i32, [vp, vp, vp, i32, vp, vp, vp, vp, i32, i32, vp,
+                                                 P(i32)]),
         "orbg_fuse_sim3": (i32, [vp, P(KeyFrame), vp, vp, vp, i32, f32, vp, vp, P(i32)]),
         "orbg_fuse_sim3_batch_device": (i32, [vp, P(KeyFrames), i32, vp, vp, vp, vp, vp, i32, i32, f32,
                                          vp, vp, vp]),

@@ -42,4 +42,29 @@ __host__ __device__ inline void undistort_point(const orbg_camera &c, float uf, 
     *yo = (float)(yy * ww);
 }
 
+// Fuse(pKF, Scw, ...) / SearchByProjection(pKF, Scw, ...)'s decomposition (ORBmatcher.cc:
+// 1143-1148, 362-366): scw = the double root of row 0's double dot product, rounded to float;
+// Rcw | tcw = Scw * (float)(1 / scw), rounded once per element (Mat / double is convertTo
+// with a float alpha and shift 0; built with -ffp-contract=off)
+__host__ __device__ inline void sim3_decompose(const float *S, float *T)
+{
+    double d = 0.0;
+    for (int k = 0; k < 3; k++) d += (double)S[k] * (double)S[k];
+    const float scw = (float)sqrt(d);
+    const float a = (float)(1.0 / (double)scw);
+    for (int k = 0; k < 12; k++) T[k] = S[k] * a + 0.0f;
+}
+
+// MapPoint::PredictScale (MapPoint.cc:575-607)
+__host__ __device__ inline int predict_scale(float max_dist, float dist, float log_sf, int nlevels)
+{
+    const float ratio = max_dist / dist;
+    int n = (int)ceil(log((double)ratio) / (double)log_sf);
+    if (n < 0)
+        n = 0;
+    else if (n >= nlevels)
+        n = nlevels - 1;
+    return n;
+}
+
 }  // namespace orbg

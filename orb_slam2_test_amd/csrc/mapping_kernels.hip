@@ -34,6 +34,7 @@
 #include <hip/hip_runtime.h>
 
 #include "../../include/orbg.h"
+#include "frame_device.h"
 #include "orbg_device.h"
 #include "orbg_internal.h"
 
@@ -307,20 +308,6 @@ struct FuseKey {  // a grid entry in LDS
 
 #define FU_CELLS (ORBG_GRID_COLS * ORBG_GRID_ROWS)
 static_assert(FU_CELLS == 256 * 12, "k_fuse's scan gives 12 grid cells to each of 256 threads");
-
-// Fuse(pKF, Scw, ...)'s decomposition (ORBmatcher.cc:1143-1148): scw = the double root of
-// row 0's double dot product, rounded to float; Rcw | tcw = Scw * (float)(1 / scw), rounded
-// once per element (Mat / double is convertTo with a float alpha and shift 0)
-__device__ inline void sim3_decompose(const float *S, float *T)
-{
-    double d = 0.0;
-#pragma unroll
-    for (int k = 0; k < 3; k++) d += (double)S[k] * (double)S[k];
-    const float scw = (float)sqrt(d);
-    const float a = (float)(1.0 / (double)scw);
-#pragma unroll
-    for (int k = 0; k < 12; k++) T[k] = __fadd_rn(__fmul_rn(S[k], a), 0.0f);
-}
 
 // SIM3 = false: Fuse(pKF, vpMapPoints, th) (:968-1069).  SIM3 = true: Fuse(pKF, Scw, vpPoints,
 // th, vpReplacePoint) (:1133-1238): cams[p].Tcw holds Scw's rows 0..2, and the candidates

@@ -3048,6 +3048,8 @@ static int track_run(orbg_ctx *c, int mode, const orbg_track_batch *tb, int nfra
         !tb->qcounts || !tb->match || !tb->nmatches)
         return set_err(ORBG_EINVAL, "NULL device array");
     if (mode == ORBG_TRACK_LASTFRAME && !tb->cams) return set_err(ORBG_EINVAL, "cams is NULL");
+    if ((mode == ORBG_TRACK_RELOC || mode == ORBG_TRACK_LOOP) && !tb->fcams)
+        return set_err(ORBG_EINVAL, "fcams is NULL");
     const size_t tk = al256((size_t)nframes * tb->query_cap * ORBG_MATCH_TOPK * 8);
     const size_t need = tk + al256((size_t)nframes * tb->query_cap * 4);
     if (c->trk_bytes < need) {
@@ -3081,6 +3083,9 @@ static int track_run(orbg_ctx *c, int mode, const orbg_track_batch *tb, int nfra
     A.topn = (int32_t *)((uint8_t *)c->d_trk + tk);
     A.match = tb->match;
     A.nmatches = tb->nmatches;
+    A.fcams = tb->fcams;
+    A.orb_dist = tb->orb_dist;
+    if (mode == ORBG_TRACK_LOOP) A.check_ori = 0;
     const int rc = launch_track(c->stream, mode, A, nframes, &c->prof);
     if (rc == ORBG_ENOTSUP)
         return set_err(rc, "frame_cap %d / query_cap %d exceed the LDS budget", tb->frame_cap,
@@ -3093,7 +3098,7 @@ extern "C" int orbg_search_by_projection_batch_device(orbg_ctx *c, int mode,
                                                       const orbg_track_batch *tb, int nframes)
 {
     if (!c || !tb) return set_err(ORBG_EINVAL, "NULL argument");
-    if (mode != ORBG_TRACK_LASTFRAME && mode != ORBG_TRACK_LOCAL)
+    if (mode < ORBG_TRACK_LASTFRAME || mode > ORBG_TRACK_LOOP)
         return set_err(ORBG_EINVAL, "mode %d", mode);
     if (nframes <= 0) return ORBG_OK;
     HIPCHK(hipSetDevice(c->device));
@@ -3105,12 +3110,15 @@ static int track_host(orbg_ctx *c, int mode, const orbg_keypoint *kps, const uin
                       const float *uright, int n, const uint8_t *taken0, const orbg_bounds *bounds,
                       const void *q, size_t qrec, const uint8_t *qdesc, int nq,
                       const orbg_track_camera *cam, float th, float nnratio, int check_ori,
-                      int32_t *match, int *nmatches)
+                      int32_t *match, int *nmatches, const orbg_frustum_camera *fcam = nullptr,
+                      int orb_dist = 0)
 {
     if (!c || !bounds || !match || (n > 0 && (!kps || !desc)) || (nq > 0 && (!q || !qdesc)))
         return set_err(ORBG_EINVAL, "NULL argument");
     if (n < 0 || nq < 0) return set_err(ORBG_EINVAL, "negative size");
     if (mode == ORBG_TRACK_LASTFRAME && !cam) return set_err(ORBG_EINVAL, "cam is NULL");
+    if ((mode == ORBG_TRACK_RELOC || mode == ORBG_TRACK_LOOP) && !fcam)
+        return set_err(ORBG_EINVAL, "cam is NULL");
     for (int i = 0; i < n; i++) match[i] = -1;
     if (nmatches) *nmatches = 0;
     if (n == 0 || nq == 0) return ORBG_OK;
@@ -3126,6 +3134,7 @@ static int track_host(orbg_ctx *c, int mode, const orbg_keypoint *kps, const uin
     const size_t o_ur = uright ? take(fc * 4) : 0, o_tk = taken0 ? take(fc) : 0;
     const size_t o_cnt = take(8), o_b = take(sizeof(orbg_bounds)), o_q = take(qc * qrec);
     const size_t o_qd = take(qc * 32), o_cam = take(sizeof(orbg_track_camera));
+    const size_t o_fcam = take(sizeof(orbg_frustum_camera));
     const size_t o_match = take(fc * 4), o_nm = take(4);
     void *s;
     int rc = scratch(c, off, &s);
@@ -3142,6 +3151,8 @@ static int track_host(orbg_ctx *c, int mode, const orbg_keypoint *kps, const uin
     HIPCHK(hipMemcpyAsync(b + o_qd, qdesc, qc * 32, hipMemcpyHostToDevice, c->stream));
     if (cam)
         HIPCHK(hipMemcpyAsync(b + o_cam, cam, sizeof(*cam), hipMemcpyHostToDevice, c->stream));
+    if (fcam)
+        HIPCHK(hipMemcpyAsync(b + o_fcam, fcam, sizeof(*fcam), hipMemcpyHostToDevice, c->stream));
     orbg_track_batch tb{};
     tb.kps = (const orbg_keypoint *)(b + o_kps);
     tb.desc = b + o_desc;
@@ -3160,6 +3171,8 @@ static int track_host(orbg_ctx *c, int mode, const orbg_keypoint *kps, const uin
     tb.check_ori = check_ori;
     tb.match = (int32_t *)(b + o_match);
     tb.nmatches = (int32_t *)(b + o_nm);
+    tb.fcams = fcam ? (const orbg_frustum_camera *)(b + o_fcam) : nullptr;
+    tb.orb_dist = orb_dist;
     if ((rc = track_run(c, mode, &tb, 1))) return rc;
     int32_t nm = 0;
     HIPCHK(hipMemcpyAsync(match, b + o_match, fc * 4, hipMemcpyDeviceToHost, c->stream));
@@ -3194,6 +3207,31 @@ extern "C" int orbg_search_by_projection_local(orbg_ctx *c, const orbg_keypoint 
     return track_host(c, ORBG_TRACK_LOCAL, kps, desc, uright, n, taken0, bounds, mps,
                       sizeof(orbg_map_projection), mdesc, nm, nullptr, th, nnratio, 0, match,
                       nmatches);
+}
+
+extern "C" int orbg_search_by_projection_reloc(orbg_ctx *c, const orbg_keypoint *kps,
+                                               const uint8_t *desc, int n, const uint8_t *taken0,
+                                               const orbg_frustum_camera *cam,
+                                               const orbg_reloc_point *pts, const uint8_t *pdesc,
+                                               int np, float th, int orb_dist, int check_ori,
+                                               int32_t *match, int *nmatches)
+{
+    if (!cam) return set_err(ORBG_EINVAL, "NULL argument");
+    return track_host(c, ORBG_TRACK_RELOC, kps, desc, nullptr, n, taken0, &cam->bounds, pts,
+                      sizeof(orbg_reloc_point), pdesc, np, nullptr, th, 0.f, check_ori, match,
+                      nmatches, cam, orb_dist);
+}
+
+extern "C" int orbg_search_by_projection_sim3(orbg_ctx *c, const orbg_keypoint *kps,
+                                              const uint8_t *desc, int n, const uint8_t *taken0,
+                                              const orbg_frustum_camera *cam,
+                                              const orbg_map_point *mps, const uint8_t *mdesc,
+                                              int nm, int th, int32_t *match, int *nmatches)
+{
+    if (!cam) return set_err(ORBG_EINVAL, "NULL argument");
+    return track_host(c, ORBG_TRACK_LOOP, kps, desc, nullptr, n, taken0, &cam->bounds, mps,
+                      sizeof(orbg_map_point), mdesc, nm, nullptr, (float)th, 0.f, 0, match,
+                      nmatches, cam, 0);
 }
 
 // ---------------------------------------------------------------------------

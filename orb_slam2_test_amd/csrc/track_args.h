@@ -29,9 +29,11 @@ struct TrackArgs {
     int32_t *topn;              // [B][qc]  candidates (-1: query skipped before the search)
     int32_t *match;             // [B][fc]  query index per keypoint, -1
     int32_t *nmatches;          // [B]
+    const orbg_frustum_camera *fcams;  // [B] (relocalization / loop searches)
+    int orb_dist;               // relocalization: ORBdist
 };
 
-enum { TRK_LASTFRAME = 0, TRK_LOCAL = 1 };
+enum { TRK_LASTFRAME = 0, TRK_LOCAL = 1, TRK_RELOC = 2, TRK_LOOP = 3 };
 
 int launch_track(hipStream_t st, int mode, const TrackArgs &A, int nframes, void *prof);
 

@@ -4,6 +4,13 @@
 //       (ORBmatcher.cc:1503-1667; Tracking::TrackWithMotionModel)
 //   ORBmatcher::SearchByProjection(F, vpMapPoints, th)
 //       (ORBmatcher.cc:59-146, RadiusByViewingCos :148-154; Tracking::SearchLocalPoints)
+//   ORBmatcher::SearchByProjection(CurrentFrame, pKF, sAlreadyFound, th, ORBdist)
+//       (ORBmatcher.cc:1670-1798; Tracking::Relocalization)                  [TRK_RELOC]
+//   ORBmatcher::SearchByProjection(pKF, Scw, vpPoints, vpMatched, th)
+//       (ORBmatcher.cc:353-470; LoopClosing::ComputeSim3)                     [TRK_LOOP]
+// The last two write every pick (mvpMapPoints[i2] / vpMatched[idx] != NULL is the skip), so
+// their queries always take; RELOC keeps the rotation histogram, LOOP is TH_LOW on a
+// KeyFrame (int bounds for IsInImage and the cell range, the level window after the area).
 //
 // Both are "project, window search, best Hamming distance" loops whose only order
 // dependence is the skip of a keypoint that an earlier query already took
@@ -30,6 +37,7 @@
 #include "../../include/orbg.h"
 #include "orbg_internal.h"
 #include "orbg_device.h"
+#include "frame_device.h"
 #include "match_device.h"
 #include "track_args.h"
 
@@ -41,7 +49,9 @@ void prof_begin(void *prof, hipStream_t s, const char *n, hipEvent_t *a);
 void prof_end(void *prof, hipStream_t s, const char *n, hipEvent_t a);
 
 #define TH_HIGH 100
+#define TH_LOW 50
 #define HISTO_LENGTH 30
+#define TRK_ROT(m) ((m) == TRK_LASTFRAME || (m) == TRK_RELOC)  // rotation histogram
 #define TRK_QPW 32  // queries per wave in k_track_cands (8 x 4 in 16-lane groups)
 #define TRK_NB (ORBG_MAX_LEVELS * ORBG_GRID_COLS)  // (octave, column) buckets
 
@@ -123,6 +133,80 @@ __device__ TrackQuery track_query(const TrackArgs &A, int f, int i, bool fwd, bo
         Q.ur = u - cam.bf * invzc;
         Q.ur_thr = Q.r;
         Q.has_obs = (P.flags & ORBG_MP_HAS_OBS) != 0;
+    } else if (MODE == TRK_RELOC) {
+        // ORBmatcher.cc:1689-1727 (no depth test: the reference has none)
+        const orbg_reloc_point P = ((const orbg_reloc_point *)A.q)[(size_t)f * A.qc + i];
+        if (!(P.flags & ORBG_MP_VALID)) return Q;
+        const orbg_frustum_camera &cam = A.fcams[f];
+        const float tcw[3] = {cam.Tcw[3], cam.Tcw[7], cam.Tcw[11]};
+        const float X[3] = {P.x, P.y, P.z};
+        float xc[3], Ow[3];
+        gemm3(cam.Tcw, false, X, 1.0, tcw, xc);
+        const float invzc = (float)(1.0 / (double)xc[2]);
+        const float u = cam.fx * xc[0] * invzc + cam.cx;
+        const float v = cam.fy * xc[1] * invzc + cam.cy;
+        if (u < b.min_x || u > b.max_x) return Q;
+        if (v < b.min_y || v > b.max_y) return Q;
+        gemm3(cam.Tcw, true, tcw, -1.0, nullptr, Ow);
+        const float PO0 = X[0] - Ow[0], PO1 = X[1] - Ow[1], PO2 = X[2] - Ow[2];
+        double s = 0.0;
+        s += (double)PO0 * (double)PO0;
+        s += (double)PO1 * (double)PO1;
+        s += (double)PO2 * (double)PO2;
+        const float dist3D = (float)sqrt(s);
+        const float maxDistance = 1.2f * P.max_dist, minDistance = 0.8f * P.min_dist;
+        if (dist3D < minDistance || dist3D > maxDistance) return Q;
+        const int lvl = predict_scale(P.max_dist, dist3D, cam.log_scale_factor, cam.nlevels);
+        Q.r = A.th * A.scale[lvl];
+        Q.minL = lvl - 1;
+        Q.maxL = lvl + 1;
+        Q.x = u;
+        Q.y = v;
+        Q.ur = 0.f;
+        Q.ur_thr = INFINITY;  // no stereo test
+        Q.has_obs = true;     // every pick is written: a later point skips it
+    } else if (MODE == TRK_LOOP) {
+        // ORBmatcher.cc:379-425 on pKF with the decomposed Scw
+        const orbg_map_point M = ((const orbg_map_point *)A.q)[(size_t)f * A.qc + i];
+        if (!(M.flags & ORBG_MP_VALID)) return Q;
+        const orbg_frustum_camera &cam = A.fcams[f];
+        float T[12];
+        sim3_decompose(cam.Tcw, T);
+        const float tcw[3] = {T[3], T[7], T[11]};
+        const float X[3] = {M.x, M.y, M.z};
+        float Pc[3], Ow[3];
+        gemm3(T, false, X, 1.0, tcw, Pc);
+        if (Pc[2] < 0.0f) return Q;
+        const float invz = 1 / Pc[2];
+        const float x = Pc[0] * invz, y = Pc[1] * invz;
+        const float u = cam.fx * x + cam.cx, v = cam.fy * y + cam.cy;
+        // KeyFrame::IsInImage on the KeyFrame's int bounds (KeyFrame.h:288-291)
+        const float kminx = (float)(int)b.min_x, kmaxx = (float)(int)b.max_x;
+        const float kminy = (float)(int)b.min_y, kmaxy = (float)(int)b.max_y;
+        if (!(u >= kminx && u < kmaxx && v >= kminy && v < kmaxy)) return Q;
+        gemm3(T, true, tcw, -1.0, nullptr, Ow);
+        const float PO0 = X[0] - Ow[0], PO1 = X[1] - Ow[1], PO2 = X[2] - Ow[2];
+        double s = 0.0;
+        s += (double)PO0 * (double)PO0;
+        s += (double)PO1 * (double)PO1;
+        s += (double)PO2 * (double)PO2;
+        const float dist = (float)sqrt(s);
+        const float maxDistance = 1.2f * M.max_dist, minDistance = 0.8f * M.min_dist;
+        if (dist < minDistance || dist > maxDistance) return Q;
+        double dot = 0.0;
+        dot += (double)PO0 * (double)M.nx;
+        dot += (double)PO1 * (double)M.ny;
+        dot += (double)PO2 * (double)M.nz;
+        if (dot < 0.5 * (double)dist) return Q;
+        const int lvl = predict_scale(M.max_dist, dist, cam.log_scale_factor, cam.nlevels);
+        Q.r = A.th * A.scale[lvl];
+        Q.minL = lvl - 1;  // the loop's kpLevel window, applied after GetFeaturesInArea
+        Q.maxL = lvl;
+        Q.x = u;
+        Q.y = v;
+        Q.ur = 0.f;
+        Q.ur_thr = INFINITY;
+        Q.has_obs = true;
     } else {
         // ORBmatcher.cc:63-86
         const orbg_map_projection M = ((const orbg_map_projection *)A.q)[(size_t)f * A.qc + i];
@@ -140,6 +224,15 @@ __device__ TrackQuery track_query(const TrackArgs &A, int f, int i, bool fwd, bo
     }
     Q.valid = true;
     return Q;
+}
+
+// KeyFrame::GetFeaturesInArea's cell range uses the KeyFrame's int mnMinX / mnMinY (the
+// Frame's truncated) with the Frame's cell sizes; PosInGrid stays the Frame's
+__device__ __forceinline__ GridPrm kf_window_prm(GridPrm g)
+{
+    g.min_x = (float)(int)g.min_x;
+    g.min_y = (float)(int)g.min_y;
+    return g;
 }
 
 // level / stereo filters of one keypoint (GetFeaturesInArea's bCheckLevels, :475-482, and
@@ -248,7 +341,7 @@ __global__ __launch_bounds__(256) void k_track_cands(TrackArgs A)
         for (int k = 0; k < ORBG_MATCH_TOPK; k++) loc[k] = ~0ull;
         int cnt = 0;
         if (act) {
-            const Window w = make_window(g, Q.x, Q.y, Q.r);
+            const Window w = make_window(MODE == TRK_LOOP ? kf_window_prm(g) : g, Q.x, Q.y, Q.r);
             uint32_t qd[8];
             {
                 const uint4 *p = (const uint4 *)(A.qdesc + ((size_t)f * A.qc + i) * 32);
@@ -316,7 +409,7 @@ __device__ __forceinline__ void track_rescan(const TrackArgs &A, int f, int i, c
     const int lane = threadIdx.x & 63, n = A.counts[f];
     const orbg_bounds b = A.bounds[f];
     const GridPrm g = grid_prm(b);
-    const Window w = make_window(g, Q.x, Q.y, Q.r);
+    const Window w = make_window(MODE == TRK_LOOP ? kf_window_prm(g) : g, Q.x, Q.y, Q.r);
     unsigned long long m1 = ~0ull, m2 = ~0ull;
     if (!w.empty) {
         uint32_t qd[8];
@@ -414,6 +507,13 @@ __global__ __launch_bounds__(TRK_RT) void k_track_resolve(TrackArgs A)
                 const orbg_lastframe_point P =
                     ((const orbg_lastframe_point *)A.q)[(size_t)f * A.qc + c0 + lane];
                 qi = make_int2(__float_as_int(P.angle), P.flags);
+            } else if (MODE == TRK_RELOC) {
+                const orbg_reloc_point P =
+                    ((const orbg_reloc_point *)A.q)[(size_t)f * A.qc + c0 + lane];
+                qi = make_int2(__float_as_int(P.angle), P.flags | ORBG_MP_HAS_OBS);
+            } else if (MODE == TRK_LOOP) {
+                qi.y = ((const orbg_map_point *)A.q)[(size_t)f * A.qc + c0 + lane].flags |
+                       ORBG_MP_HAS_OBS;
             } else {
                 qi.y = ((const orbg_map_projection *)A.q)[(size_t)f * A.qc + c0 + lane].flags;
             }
@@ -454,6 +554,8 @@ __global__ __launch_bounds__(TRK_RT) void k_track_resolve(TrackArgs A)
             // K-list ran out) commit in lane order, the rest go again.  Same result as the
             // in-order loop, typically in one or two rounds per chunk.
             const int need = MODE == TRK_LOCAL ? 2 : 1;
+            // the loop's acceptance (:1623 TH_HIGH, :131 TH_HIGH, :1760 ORBdist, :458 TH_LOW)
+            const int thr = MODE == TRK_RELOC ? A.orb_dist : MODE == TRK_LOOP ? TH_LOW : TH_HIGH;
             const int qidx = c0 + lane;
             const int total = lane < cn ? cnt[lane] : 0;
             const int2 qv = qin[lane];
@@ -477,7 +579,7 @@ __global__ __launch_bounds__(TRK_RT) void k_track_resolve(TrackArgs A)
                 // the loop body's decision (ORBmatcher.cc:1623-1625 / 129-139)
                 bool app = false;
                 int bestIdx = 0, bin = 0;
-                if (pend && !resc && k1 != ~0ull && (int)(k1 >> 32) <= TH_HIGH) {
+                if (pend && !resc && k1 != ~0ull && (int)(k1 >> 32) <= thr) {
                     bestIdx = (int)(k1 & 0xFFFFF);
                     app = true;
                     if (MODE == TRK_LOCAL) {
@@ -485,7 +587,7 @@ __global__ __launch_bounds__(TRK_RT) void k_track_resolve(TrackArgs A)
                         const int o2 = k2 == ~0ull ? -1 : koct[(int)(k2 & 0xFFFFF)];
                         if (koct[bestIdx] == o2 && (int)(k1 >> 32) > A.nnratio * bestDist2)
                             app = false;
-                    } else if (A.check_ori) {
+                    } else if (TRK_ROT(MODE) && A.check_ori) {
                         float rot = __int_as_float(qv.x) - kang[bestIdx];
                         if (rot < 0.0) rot += 360.0f;
                         bin = (int)roundf(rot * factor);
@@ -511,12 +613,12 @@ __global__ __launch_bounds__(TRK_RT) void k_track_resolve(TrackArgs A)
                     if (takes) taken[bestIdx] = 1;
                 }
                 const unsigned long long am = __ballot(commit && app);
-                if (MODE == TRK_LASTFRAME && A.check_ori && commit && app) {
+                if (TRK_ROT(MODE) && A.check_ori && commit && app) {
                     const int pos = __builtin_amdgcn_mbcnt_hi(
                         (uint32_t)(am >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)am, 0));
                     push[npush + pos] = bestIdx << 8 | bin;
                 }
-                npush += (MODE == TRK_LASTFRAME && A.check_ori) ? __popcll(am) : 0;
+                npush += (TRK_ROT(MODE) && A.check_ori) ? __popcll(am) : 0;
                 nmatch += __popcll(am);
                 pending &= ~below;
                 wave_sync_lds();
@@ -526,7 +628,7 @@ __global__ __launch_bounds__(TRK_RT) void k_track_resolve(TrackArgs A)
                     unsigned long long r1, r2;
                     track_rescan<MODE>(A, f, c0 + lr, Q, taken, &r1, &r2);
                     const int qy = __shfl(qv.y, lr, 64), qx = __shfl(qv.x, lr, 64);
-                    if (lane == 0 && r1 != ~0ull && (int)(r1 >> 32) <= TH_HIGH) {
+                    if (lane == 0 && r1 != ~0ull && (int)(r1 >> 32) <= thr) {
                         const int bi = (int)(r1 & 0xFFFFF);
                         bool ok = true;
                         int bn = 0;
@@ -534,7 +636,7 @@ __global__ __launch_bounds__(TRK_RT) void k_track_resolve(TrackArgs A)
                             const int bestDist2 = r2 == ~0ull ? 256 : (int)(r2 >> 32);
                             const int o2 = r2 == ~0ull ? -1 : koct[(int)(r2 & 0xFFFFF)];
                             if (koct[bi] == o2 && (int)(r1 >> 32) > A.nnratio * bestDist2) ok = false;
-                        } else if (A.check_ori) {
+                        } else if (TRK_ROT(MODE) && A.check_ori) {
                             float rot = __int_as_float(qx) - kang[bi];
                             if (rot < 0.0) rot += 360.0f;
                             bn = (int)roundf(rot * factor);
@@ -543,7 +645,7 @@ __global__ __launch_bounds__(TRK_RT) void k_track_resolve(TrackArgs A)
                         if (ok) {
                             match[bi] = max(match[bi], c0 + lr);
                             if (qy & ORBG_MP_HAS_OBS) taken[bi] = 1;
-                            if (MODE == TRK_LASTFRAME && A.check_ori) push[npush] = bi << 8 | bn;
+                            if (TRK_ROT(MODE) && A.check_ori) push[npush] = bi << 8 | bn;
                             misc[63] = 1;
                         } else {
                             misc[63] = 0;
@@ -553,7 +655,7 @@ __global__ __launch_bounds__(TRK_RT) void k_track_resolve(TrackArgs A)
                     }
                     wave_sync_lds();
                     const int ap = misc[63];
-                    npush += (MODE == TRK_LASTFRAME && A.check_ori) ? ap : 0;
+                    npush += (TRK_ROT(MODE) && A.check_ori) ? ap : 0;
                     nmatch += ap;
                     pending &= ~(1ull << lr);
                     wave_sync_lds();
@@ -568,7 +670,7 @@ __global__ __launch_bounds__(TRK_RT) void k_track_resolve(TrackArgs A)
     }
     __syncthreads();
     int nm = misc[1];
-    if (MODE == TRK_LASTFRAME && A.check_ori) {
+    if (TRK_ROT(MODE) && A.check_ori) {
         // rotation histogram of the pushes, ComputeThreeMaxima (:1800-1841), then every
         // push in a dropped bin NULLs its slot and decrements nmatches (:1651-1663)
         const int np = misc[0];
@@ -627,34 +729,34 @@ __global__ __launch_bounds__(TRK_RT) void k_track_resolve(TrackArgs A)
 size_t track_cands_lds(int fc) { return (size_t)std::max(fc, 1) * sizeof(TKey); }
 size_t track_resolve_lds_bytes(int fc, int qc) { return track_resolve_lds(fc, qc); }
 
-// mode: 0 last frame, 1 local map.  A's pointers are device pointers; nframes frames.
+template <int MODE>
+static void launch_mode(hipStream_t st, const TrackArgs &A, int nframes, int nbx, size_t l1,
+                        size_t l2, void *prof)
+{
+    hipFuncSetAttribute((const void *)k_track_cands<MODE>,
+                        hipFuncAttributeMaxDynamicSharedMemorySize, (int)l1);
+    hipFuncSetAttribute((const void *)k_track_resolve<MODE>,
+                        hipFuncAttributeMaxDynamicSharedMemorySize, (int)l2);
+    PL(prof, st, "track_cands",
+       hipLaunchKernelGGL(k_track_cands<MODE>, dim3(nbx * nframes), dim3(256), l1, st, A));
+    PL(prof, st, "track_resolve",
+       hipLaunchKernelGGL(k_track_resolve<MODE>, dim3(nframes), dim3(TRK_RT), l2, st, A));
+}
+
+// mode: TRK_LASTFRAME / TRK_LOCAL / TRK_RELOC / TRK_LOOP.  A's pointers are device pointers;
+// nframes frames.
 int launch_track(hipStream_t st, int mode, const TrackArgs &A, int nframes, void *prof)
 {
     if (A.fc > (1 << 20) || nframes <= 0) return ORBG_EINVAL;
     const size_t l1 = track_cands_lds(A.fc), l2 = track_resolve_lds(A.fc, A.qc);
     if (l1 > 160 * 1024 || l2 > 160 * 1024) return ORBG_ENOTSUP;
     const int nbx = (A.qc + 4 * TRK_QPW - 1) / (4 * TRK_QPW);
-    if (mode == TRK_LASTFRAME) {
-        hipFuncSetAttribute((const void *)k_track_cands<TRK_LASTFRAME>,
-                            hipFuncAttributeMaxDynamicSharedMemorySize, (int)l1);
-        hipFuncSetAttribute((const void *)k_track_resolve<TRK_LASTFRAME>,
-                            hipFuncAttributeMaxDynamicSharedMemorySize, (int)l2);
-        PL(prof, st, "track_cands",
-           hipLaunchKernelGGL(k_track_cands<TRK_LASTFRAME>, dim3(nbx * nframes), dim3(256), l1,
-                              st, A));
-        PL(prof, st, "track_resolve",
-           hipLaunchKernelGGL(k_track_resolve<TRK_LASTFRAME>, dim3(nframes), dim3(TRK_RT), l2, st,
-                              A));
-    } else {
-        hipFuncSetAttribute((const void *)k_track_cands<TRK_LOCAL>,
-                            hipFuncAttributeMaxDynamicSharedMemorySize, (int)l1);
-        hipFuncSetAttribute((const void *)k_track_resolve<TRK_LOCAL>,
-                            hipFuncAttributeMaxDynamicSharedMemorySize, (int)l2);
-        PL(prof, st, "track_cands",
-           hipLaunchKernelGGL(k_track_cands<TRK_LOCAL>, dim3(nbx * nframes), dim3(256), l1, st,
-                              A));
-        PL(prof, st, "track_resolve",
-           hipLaunchKernelGGL(k_track_resolve<TRK_LOCAL>, dim3(nframes), dim3(TRK_RT), l2, st, A));
+    switch (mode) {
+    case TRK_LASTFRAME: launch_mode<TRK_LASTFRAME>(st, A, nframes, nbx, l1, l2, prof); break;
+    case TRK_LOCAL: launch_mode<TRK_LOCAL>(st, A, nframes, nbx, l1, l2, prof); break;
+    case TRK_RELOC: launch_mode<TRK_RELOC>(st, A, nframes, nbx, l1, l2, prof); break;
+    case TRK_LOOP: launch_mode<TRK_LOOP>(st, A, nframes, nbx, l1, l2, prof); break;
+    default: return ORBG_EINVAL;
     }
     return hipGetLastError() == hipSuccess ? ORBG_OK : ORBG_EIO;
 }

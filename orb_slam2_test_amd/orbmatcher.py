@@ -186,6 +186,48 @@ class ORBmatcher:
                 "orbg_search_by_projection_lastframe")
         return nm.value, match
 
+    def SearchByProjection_Reloc(self, F, fcam, kf_points, kf_point_desc, th, ORBdist):
+        """SearchByProjection(CurrentFrame, pKF, sAlreadyFound, th, ORBdist)
+        (ORBmatcher.cc:1670-1798; Tracking::Relocalization): F with mvKeysUn, mDescriptors and
+        taken (mvpMapPoints[i] != NULL, None: none); fcam its FRUSTUM_DTYPE state; kf_points
+        RELOC_DTYPE records of pKF->GetMapPointMatches() (flags MP_VALID = pMP && !isBad() &&
+        not in sAlreadyFound; angle = pKF->mvKeysUn[i].angle).  Returns (nmatches, match):
+        match[i2] = the pKF index written to mvpMapPoints[i2], -1, or -2 (rotation filter)."""
+        kps = np.ascontiguousarray(F.mvKeysUn, L.KP_DTYPE)
+        desc = np.ascontiguousarray(F.mDescriptors, np.uint8)
+        tk = None if F.taken is None else np.ascontiguousarray(F.taken, np.uint8)
+        fc = np.ascontiguousarray(fcam, L.FRUSTUM_DTYPE)
+        pts = np.ascontiguousarray(kf_points, L.RELOC_DTYPE)
+        pd = np.ascontiguousarray(kf_point_desc, np.uint8).reshape(-1, 32)
+        match = np.full(max(len(kps), 1), -1, np.int32)
+        nm = C.c_int()
+        L.check(L.lib().orbg_search_by_projection_reloc(
+            _ctx(self.device).handle, L.ptr(kps), L.ptr(desc), len(kps), L.ptr(tk), L.ptr(fc),
+            L.ptr(pts), L.ptr(pd), len(pts), float(th), int(ORBdist),
+            1 if self.mbCheckOrientation else 0, L.ptr(match), C.byref(nm)),
+            "orbg_search_by_projection_reloc")
+        return nm.value, match[:len(kps)].copy()
+
+    def SearchByProjection_Sim3(self, pKF, fcam, points, points_desc, th=10):
+        """SearchByProjection(pKF, Scw, vpPoints, vpMatched, th) (ORBmatcher.cc:353-470;
+        LoopClosing::ComputeSim3): pKF with mvKeysUn, mDescriptors and taken (vpMatched[i] !=
+        NULL, None: none); fcam["Tcw"] = Scw rows 0..2 (decomposed on the device), bounds the
+        Frame's; points MAPPOINT_DTYPE (flags MP_VALID = !isBad() and not in vpMatched).
+        Returns (nmatches, match): match[idx] = the vpPoints index written to vpMatched[idx]."""
+        kps = np.ascontiguousarray(pKF.mvKeysUn, L.KP_DTYPE)
+        desc = np.ascontiguousarray(pKF.mDescriptors, np.uint8)
+        tk = None if pKF.taken is None else np.ascontiguousarray(pKF.taken, np.uint8)
+        fc = np.ascontiguousarray(fcam, L.FRUSTUM_DTYPE)
+        mps = np.ascontiguousarray(points, L.MAPPOINT_DTYPE)
+        md = np.ascontiguousarray(points_desc, np.uint8).reshape(-1, 32)
+        match = np.full(max(len(kps), 1), -1, np.int32)
+        nm = C.c_int()
+        L.check(L.lib().orbg_search_by_projection_sim3(
+            _ctx(self.device).handle, L.ptr(kps), L.ptr(desc), len(kps), L.ptr(tk), L.ptr(fc),
+            L.ptr(mps), L.ptr(md), len(mps), int(th), L.ptr(match), C.byref(nm)),
+            "orbg_search_by_projection_sim3")
+        return nm.value, match[:len(kps)].copy()
+
     def SearchForTriangulation(self, pKF1, pKF2, geom, bOnlyStereo=False):
         """ORBmatcher::SearchForTriangulation(pKF1, pKF2, F12, vMatchedPairs, bOnlyStereo)
         (src/ORBmatcher.cc:779-957).  pKF1 / pKF2: Frames with mvKeysUn, mDescriptors,

@@ -1,0 +1,136 @@
+"""GPU: the Relocalization and LoopClosing projection matchers through the C ABI
+(k_track_cands / k_track_resolve in TRK_RELOC / TRK_LOOP mode, csrc/track_kernels.hip) vs the
+CPU oracle (oracle/loop_oracle.c, pinned against the pure-Python restatements in
+tests/test_oracle_loop.py), bit for bit: the written keypoint array and nmatches.
+
+  ORBmatcher::SearchByProjection(CurrentFrame, pKF, sAlreadyFound, th, ORBdist)
+      src/ORBmatcher.cc:1670-1798 (Tracking::Relocalization, th 10 / 100 and 3 / 64)
+  ORBmatcher::SearchByProjection(pKF, Scw, vpPoints, vpMatched, th)
+      src/ORBmatcher.cc:353-470 (LoopClosing::ComputeSim3, th 10)
+
+Cases: several points competing for one keypoint (the in-order skip of written keypoints),
+keypoints written before the call, rotations outside the dominant bins, fractional
+(undistorted-camera) bounds, Sim3 scales, empty inputs, and the batched device form.
+"""
+import ctypes as C
+
+import numpy as np
+import pytest
+
+from orb_slam2_test_amd import _lib as L
+from orb_slam2_test_amd.orbmatcher import Frame, ORBmatcher, _ctx
+
+import test_oracle_loop as T
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.mark.parametrize("seed,th,orb_dist,bounds,check_ori", [
+    (0, 10, 100, None, True), (1, 3, 64, None, True), (2, 10, 100, T.FRAC, True),
+    (3, 10, 100, None, False)])
+def test_reloc(oracle, seed, th, orb_dist, bounds, check_ori):
+    f, fcam, pts, pd = T.reloc_case(L, seed, n=2000, npts=1500, bounds=bounds)
+    sf = T._sf(oracle)
+    m = ORBmatcher(0.75, check_ori)
+    n, got = m.SearchByProjection_Reloc(Frame(f["kps"], f["desc"], taken=f["taken0"]), fcam,
+                                        pts, pd, th, orb_dist)
+    rn, ref = oracle.search_by_projection_reloc(f["kps"], f["desc"], f["taken0"],
+                                                fcam.view(oracle.FRUSTUM_DTYPE), sf,
+                                                pts.view(oracle.RELOC_DTYPE), pd, th, orb_dist,
+                                                check_ori)
+    assert n == rn and np.array_equal(got, ref)
+    assert rn > 200
+
+
+@pytest.mark.parametrize("seed,scale,bounds", [(10, 1.0, None), (11, 0.45, None),
+                                               (12, 2.6, T.FRAC)])
+def test_sim3_projection(oracle, seed, scale, bounds):
+    f, fcam, mps, md = T.sim3proj_case(L, seed, n=2000, nm=1500, scale=scale, bounds=bounds)
+    sf = T._sf(oracle)
+    n, got = ORBmatcher().SearchByProjection_Sim3(Frame(f["kps"], f["desc"], taken=f["taken0"]),
+                                                  fcam, mps, md, 10)
+    rn, ref = oracle.search_by_projection_sim3(f["kps"], f["desc"], f["taken0"],
+                                               fcam.view(oracle.FRUSTUM_DTYPE), sf,
+                                               mps.view(oracle.MAPPOINT_DTYPE), md, 10)
+    assert n == rn and np.array_equal(got, ref)
+    assert rn > 200
+
+
+def test_loop_matchers_empty():
+    f, fcam, pts, pd = T.reloc_case(L, 5, n=60, npts=30)
+    m = ORBmatcher(0.75, True)
+    n, got = m.SearchByProjection_Reloc(Frame(f["kps"], f["desc"]), fcam, pts[:0], pd[:0], 10, 100)
+    assert n == 0 and np.all(got == -1)
+    n, got = m.SearchByProjection_Reloc(Frame(f["kps"][:0], f["desc"][:0]), fcam, pts, pd, 10, 100)
+    assert n == 0 and len(got) == 0
+    g, fc2, mps, md = T.sim3proj_case(L, 6, n=60, nm=30)
+    n, got = m.SearchByProjection_Sim3(Frame(g["kps"], g["desc"]), fc2, mps[:0], md[:0])
+    assert n == 0 and np.all(got == -1)
+
+
+@pytest.mark.parametrize("mode", ["reloc", "loop"])
+def test_batch_device(oracle, mode):
+    """orbg_search_by_projection_batch_device in TRK_RELOC / TRK_LOOP mode: one candidate
+    KeyFrame (or loop KeyFrame) per frame, all in HBM, equals the oracle per frame."""
+    import torch
+    B = 4
+    sf = T._sf(oracle)
+    cases = []
+    for k in range(B):
+        if mode == "reloc":
+            cases.append(T.reloc_case(L, 30 + k, n=1500 + 100 * k, npts=1000 + 150 * k))
+        else:
+            cases.append(T.sim3proj_case(L, 40 + k, n=1500 + 100 * k, nm=1000 + 150 * k,
+                                         scale=0.5 + 0.5 * k))
+    fc = max(len(c[0]["kps"]) for c in cases)
+    qc = max(len(c[2]) for c in cases)
+    qd_t = L.RELOC_DTYPE if mode == "reloc" else L.MAPPOINT_DTYPE
+    kps = np.zeros((B, fc), L.KP_DTYPE)
+    desc = np.zeros((B, fc, 32), np.uint8)
+    tk = np.zeros((B, fc), np.uint8)
+    q = np.zeros((B, qc), qd_t)
+    qd = np.zeros((B, qc, 32), np.uint8)
+    cnt = np.zeros(B, np.int32)
+    qcnt = np.zeros(B, np.int32)
+    bounds = np.zeros((B, 4), np.float32)
+    fcams = np.zeros(B, L.FRUSTUM_DTYPE)
+    refs = []
+    for b, (f, fcam, pts, pd) in enumerate(cases):
+        n, nq = len(f["kps"]), len(pts)
+        kps[b, :n], desc[b, :n], tk[b, :n] = f["kps"], f["desc"], f["taken0"]
+        q[b, :nq], qd[b, :nq] = pts, pd
+        cnt[b], qcnt[b] = n, nq
+        bounds[b] = [fcam["min_x"], fcam["max_x"], fcam["min_y"], fcam["max_y"]]
+        fcams[b] = fcam
+        if mode == "reloc":
+            refs.append(oracle.search_by_projection_reloc(
+                f["kps"], f["desc"], f["taken0"], fcam.view(oracle.FRUSTUM_DTYPE), sf,
+                pts.view(oracle.RELOC_DTYPE), pd, 10, 100, True))
+        else:
+            refs.append(oracle.search_by_projection_sim3(
+                f["kps"], f["desc"], f["taken0"], fcam.view(oracle.FRUSTUM_DTYPE), sf,
+                pts.view(oracle.MAPPOINT_DTYPE), pd, 10))
+    t = {k: torch.from_numpy(np.ascontiguousarray(v).view(np.uint8).reshape(-1).copy()).cuda()
+         for k, v in dict(kps=kps, desc=desc, tk=tk, q=q, qd=qd, cnt=cnt, qcnt=qcnt,
+                          bounds=bounds, fcams=fcams).items()}
+    match = torch.full((B * fc,), -7, dtype=torch.int32, device="cuda")
+    nm = torch.zeros(B, dtype=torch.int32, device="cuda")
+    tb = L.TrackBatch()
+    tb.kps, tb.desc, tb.uright = t["kps"].data_ptr(), t["desc"].data_ptr(), None
+    tb.taken0 = t["tk"].data_ptr()
+    tb.counts, tb.bounds, tb.frame_cap = t["cnt"].data_ptr(), t["bounds"].data_ptr(), fc
+    tb.queries, tb.qdesc = t["q"].data_ptr(), t["qd"].data_ptr()
+    tb.qcounts, tb.query_cap = t["qcnt"].data_ptr(), qc
+    tb.cams, tb.th, tb.nnratio, tb.check_ori = None, 10.0, 0.0, 1
+    tb.match, tb.nmatches = match.data_ptr(), nm.data_ptr()
+    tb.fcams, tb.orb_dist = t["fcams"].data_ptr(), 100
+    ctx = _ctx(0)
+    torch.cuda.synchronize()
+    L.check(L.lib().orbg_search_by_projection_batch_device(
+        ctx.handle, L.TRACK_RELOC if mode == "reloc" else L.TRACK_LOOP, C.byref(tb), B), "batch")
+    ctx.sync()
+    match = match.cpu().numpy().reshape(B, fc)
+    nm = nm.cpu().numpy()
+    for b in range(B):
+        rn, rm = refs[b]
+        assert nm[b] == rn and np.array_equal(match[b, :cnt[b]], rm) and rn > 100
