@@ -31,6 +31,8 @@
 //   SearchForTriangulation .......... ORBmatcher.cc:779-957 (ORBmatcher.h:72)
 //   Fuse(pKF, vpMapPoints, th) ...... ORBmatcher.cc:968-1107 (ORBmatcher.h:153)
 //   Fuse(pKF, Scw, vpPoints, th, vpReplacePoint) ORBmatcher.cc:1133-1258 (ORBmatcher.h:162)
+//   SearchByProjection(CurrentFrame, pKF, sAlreadyFound, th, ORBdist) ORBmatcher.cc:1670-1798
+//   SearchByProjection(pKF, Scw, vpPoints, vpMatched, th) ORBmatcher.cc:353-470
 //   ComputeDistinctiveDescriptors ... MapPoint.cc:342-420 (the BestIdx over vDescriptors)
 //   LocalBundleAdjustment window ..... Optimizer.cc:633-851: the vertex / edge set g2o builds
 //                                      (LbaWindow), and BlockSolver<6,3>::buildSystem's block
@@ -289,6 +291,115 @@ int SearchByProjection(orbg_ctx *ctx, float nnratio, FrameT &F,
           "orbg_search_by_projection_local");
     for (int i = 0; i < n; i++)
         if (match[i] >= 0) F.mvpMapPoints[i] = vpMapPoints[match[i]];
+    return nm;
+}
+
+// ORBmatcher(0.75, checkOri).SearchByProjection(CurrentFrame, pKF, sAlreadyFound, th,
+// ORBdist) (Tracking::Relocalization): pKF's map points projected into CurrentFrame with its
+// pose; writes CurrentFrame.mvpMapPoints (a slot NULL on entry only: the reference skips any
+// non-NULL one).
+template <class FrameT, class KeyFrameT, class MapPointT>
+int SearchByProjection(orbg_ctx *ctx, bool checkOri, FrameT &CurrentFrame, KeyFrameT *pKF,
+                       const std::set<MapPointT *> &sAlreadyFound, const float th,
+                       const int ORBdist)
+{
+    const int n = (int)CurrentFrame.mvKeysUn.size();
+    const std::vector<orbg_keypoint> k = keys_of(CurrentFrame.mvKeysUn);
+    const std::vector<uint8_t> d = rows32(CurrentFrame.mDescriptors, n);
+    std::vector<uint8_t> taken(n > 0 ? n : 1, 0);
+    for (int i = 0; i < n; i++) taken[i] = CurrentFrame.mvpMapPoints[i] != nullptr;
+    const std::vector<MapPointT *> vpMPs = pKF->GetMapPointMatches();
+    const int np = (int)vpMPs.size();
+    std::vector<orbg_reloc_point> pts(np > 0 ? np : 1);
+    std::vector<uint8_t> pdesc((size_t)(np > 0 ? np : 1) * 32, 0);
+    for (int i = 0; i < np; i++) {
+        orbg_reloc_point &p = pts[i];
+        std::memset(&p, 0, sizeof(p));
+        MapPointT *pMP = vpMPs[i];
+        if (!pMP || pMP->isBad() || sAlreadyFound.count(pMP)) continue;
+        const auto X = pMP->GetWorldPos();
+        p.x = X.template at<float>(0);
+        p.y = X.template at<float>(1);
+        p.z = X.template at<float>(2);
+        p.min_dist = pMP->GetMinDistance();
+        p.max_dist = pMP->GetMaxDistance();
+        p.angle = pKF->mvKeysUn[i].angle;
+        p.flags = ORBG_MP_VALID;
+        mp_desc(pMP, &pdesc[(size_t)i * 32]);
+    }
+    orbg_frustum_camera cam;
+    std::memset(&cam, 0, sizeof(cam));
+    pose12(CurrentFrame.mTcw, cam.Tcw);
+    cam.fx = FrameT::fx;
+    cam.fy = FrameT::fy;
+    cam.cx = FrameT::cx;
+    cam.cy = FrameT::cy;
+    cam.bf = CurrentFrame.mbf;
+    cam.log_scale_factor = CurrentFrame.mfLogScaleFactor;
+    cam.nlevels = CurrentFrame.mnScaleLevels;
+    cam.bounds = bounds_of(CurrentFrame);
+    std::vector<int32_t> match(n > 0 ? n : 1);
+    int nm = 0;
+    check(orbg_search_by_projection_reloc(ctx, k.data(), d.data(), n, taken.data(), &cam,
+                                          pts.data(), pdesc.data(), np, th, ORBdist,
+                                          checkOri ? 1 : 0, match.data(), &nm),
+          "orbg_search_by_projection_reloc");
+    for (int i = 0; i < n; i++)  // -2: written, then set to NULL by the rotation filter
+        if (match[i] >= 0) CurrentFrame.mvpMapPoints[i] = vpMPs[match[i]];
+    return nm;
+}
+
+// ORBmatcher::SearchByProjection(pKF, Scw, vpPoints, vpMatched, th) (LoopClosing::
+// ComputeSim3): writes vpMatched (the Scw decomposition happens on the device).  FrameT gives
+// the Frame's float bounds the KeyFrame's grid was built with.
+template <class FrameT, class KeyFrameT, class MapPointT, class Mat>
+int SearchByProjection(orbg_ctx *ctx, KeyFrameT *pKF, const Mat &Scw,
+                       const std::vector<MapPointT *> &vpPoints,
+                       std::vector<MapPointT *> &vpMatched, int th)
+{
+    const int n = (int)pKF->mvKeysUn.size(), nm_in = (int)vpPoints.size();
+    const std::vector<orbg_keypoint> k = keys_of(pKF->mvKeysUn);
+    const std::vector<uint8_t> d = rows32(pKF->mDescriptors, n);
+    std::set<MapPointT *> spAlreadyFound(vpMatched.begin(), vpMatched.end());
+    spAlreadyFound.erase(static_cast<MapPointT *>(nullptr));
+    std::vector<uint8_t> taken(n > 0 ? n : 1, 0);
+    for (int i = 0; i < n; i++) taken[i] = vpMatched[i] != nullptr;
+    std::vector<orbg_map_point> mps(nm_in > 0 ? nm_in : 1);
+    std::vector<uint8_t> mdesc((size_t)(nm_in > 0 ? nm_in : 1) * 32, 0);
+    for (int i = 0; i < nm_in; i++) {
+        MapPointT *p = vpPoints[i];
+        orbg_map_point &m = mps[i];
+        std::memset(&m, 0, sizeof(m));
+        if (p->isBad() || spAlreadyFound.count(p)) continue;
+        const auto X = p->GetWorldPos(), Pn = p->GetNormal();
+        m.x = X.template at<float>(0);
+        m.y = X.template at<float>(1);
+        m.z = X.template at<float>(2);
+        m.nx = Pn.template at<float>(0);
+        m.ny = Pn.template at<float>(1);
+        m.nz = Pn.template at<float>(2);
+        m.min_dist = p->GetMinDistance();
+        m.max_dist = p->GetMaxDistance();
+        m.flags = ORBG_MP_VALID;
+        mp_desc(p, &mdesc[(size_t)i * 32]);
+    }
+    orbg_frustum_camera cam;
+    std::memset(&cam, 0, sizeof(cam));
+    pose12(Scw, cam.Tcw);
+    cam.fx = pKF->fx;
+    cam.fy = pKF->fy;
+    cam.cx = pKF->cx;
+    cam.cy = pKF->cy;
+    cam.log_scale_factor = pKF->mfLogScaleFactor;
+    cam.nlevels = pKF->mnScaleLevels;
+    cam.bounds = orbg_bounds{FrameT::mnMinX, FrameT::mnMaxX, FrameT::mnMinY, FrameT::mnMaxY};
+    std::vector<int32_t> match(n > 0 ? n : 1);
+    int nm = 0;
+    check(orbg_search_by_projection_sim3(ctx, k.data(), d.data(), n, taken.data(), &cam,
+                                         mps.data(), mdesc.data(), nm_in, th, match.data(), &nm),
+          "orbg_search_by_projection_sim3");
+    for (int i = 0; i < n; i++)
+        if (match[i] >= 0) vpMatched[i] = vpPoints[match[i]];
     return nm;
 }
 

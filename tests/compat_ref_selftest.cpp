@@ -663,7 +663,7 @@ int main(int argc, char **argv)
     }
 
     // ---- LocalMapping: SearchForTriangulation(KA, KB) and Fuse(KB, KA's points) ----
-    int ntri = 0, nfused = 0, nfused3 = 0;
+    int ntri = 0, nfused = 0, nfused3 = 0, nloop = 0, nreloc = 0;
     {
         auto node_of = [](const cv::KeyPoint &k) {
             return (unsigned)((int)(k.pt.x / 128) + 16 * (int)(k.pt.y / 64));
@@ -826,6 +826,48 @@ int main(int argc, char **argv)
         }
         REQUIRE(vrep[F1.N] == nullptr && !own2[0].bad);
         REQUIRE(nrep3 > F1.N / 4 && nadd3 > F1.N / 2 && nst > 50 && nfused3 >= nrep3 + nadd3);
+
+        // LoopClosing::ComputeSim3's SearchByProjection(KE2, Scw, vpPoints, vpMatched, 10):
+        // KE2 = frame 1 at KA's pose, Scw = 2 [I | 0]: every point projects onto its own
+        // keypoint.  Every fifth slot is matched on entry (its point is then "already
+        // found" and skipped, the slot taken).
+        KeyFrame KE2 = KA;
+        std::vector<MapPoint *> vpM(F1.N, nullptr);
+        for (int i = 0; i < F1.N; i += 5) vpM[i] = &pts[i];
+        std::vector<MapPoint *> vpl;
+        for (int i = 0; i < F1.N; i++) {
+            pts[i].bad = false;
+            vpl.push_back(&pts[i]);
+        }
+        nloop = orbg_compat::ref::SearchByProjection<Frame>(ctx, &KE2, Scw, vpl, vpM, 10);
+        int nown = 0;
+        for (int i = 0; i < F1.N; i++) {
+            if (i % 5 == 0) REQUIRE(vpM[i] == &pts[i]);
+            else if (vpM[i] == &pts[i]) nown++;
+        }
+        REQUIRE(nloop >= nown && nown > (F1.N * 4 / 5) * 3 / 4);
+
+        // Tracking::Relocalization's SearchByProjection(FR, KR, sFound, 10, 100): FR = frame 1
+        // at the identity pose with every seventh slot filled, KR = a KeyFrame of frame 1 whose
+        // slots hold the points; the first 50 are in sFound.  Same pose and angles: every
+        // point lands on its own keypoint, all in rotation bin 0.
+        Frame FR = F1;
+        FR.mTcw = cv::Mat::eye(4, 4, CV_32F);
+        FR.mvpMapPoints.assign(F1.N, nullptr);
+        for (int i = 0; i < F1.N; i += 7) FR.mvpMapPoints[i] = &own2[0];
+        KeyFrame KR = KA;
+        KR.mvpMapPoints.assign(F1.N, nullptr);
+        for (int i = 0; i < F1.N; i++) KR.mvpMapPoints[i] = &pts[i];
+        std::set<MapPoint *> sFound;
+        for (int i = 0; i < 50; i++) sFound.insert(&pts[i]);
+        nreloc = orbg_compat::ref::SearchByProjection(ctx, true, FR, &KR, sFound, 10.f, 100);
+        int nself = 0;
+        for (int i = 0; i < F1.N; i++) {
+            if (i % 7 == 0) REQUIRE(FR.mvpMapPoints[i] == &own2[0]);
+            else if (FR.mvpMapPoints[i] == &pts[i]) nself++;
+            if (i < 50) REQUIRE(FR.mvpMapPoints[i] != &pts[i]);
+        }
+        REQUIRE(nreloc >= nself && nself > (F1.N - 50) * 6 / 7 * 3 / 4);
     }
 
     // ---- MapPoint::ComputeDistinctiveDescriptors' BestIdx ----
@@ -855,8 +897,9 @@ int main(int argc, char **argv)
 
     std::printf("compat_ref ok: %d + %d keypoints, SearchForInitialization %d, SearchByProjection %d, "
                 "PoseOptimization inliers %d, LBA edges %zu, chi2 %.6g, SearchByBoW %d, "
-                "isInFrustum %d, SearchForTriangulation %d, Fuse %d, Fuse(Sim3) %d\n",
+                "isInFrustum %d, SearchForTriangulation %d, Fuse %d, Fuse(Sim3) %d, "
+                "SearchByProjection(Sim3) %d, SearchByProjection(reloc) %d\n",
                 F1.N, F2.N, nsfi, nproj, ninl, win.edges.size(), sys.active_robust_chi2, nbow,
-                nfrustum, ntri, nfused, nfused3);
+                nfrustum, ntri, nfused, nfused3, nloop, nreloc);
     return 0;
 }
