@@ -52,6 +52,7 @@
  *   orbg_fuse_sim3 .................. ORBmatcher::Fuse(pKF, Scw, vpPoints, th, vpReplacePoint)'s search
  *   orbg_search_by_projection_reloc . ORBmatcher::SearchByProjection(CurrentFrame, pKF, sAlreadyFound, th, ORBdist)
  *   orbg_search_by_projection_sim3 .. ORBmatcher::SearchByProjection(pKF, Scw, vpPoints, vpMatched, th)
+ *   orbg_search_by_sim3 ............. ORBmatcher::SearchBySim3(pKF1, pKF2, vpMatches12, s12, R12, t12, th)
  *                                     src/ORBmatcher.cc:968-1069 (LocalMapping::SearchInNeighbors,
  *                                     LocalMapping.cc:622-690)
  *   orbg_ba_linearize ............... g2o computeActiveErrors + BlockSolver::buildSystem arithmetic
@@ -591,6 +592,39 @@ int orbg_search_by_projection_sim3(orbg_ctx *ctx, const orbg_keypoint *kps, cons
                                    int n, const uint8_t *taken0, const orbg_frustum_camera *cam,
                                    const orbg_map_point *mps, const uint8_t *mdesc, int nm,
                                    int th, int32_t *match, int *nmatches);
+
+/* ORBmatcher::SearchBySim3(pKF1, pKF2, vpMatches12, s12, R12, t12, th) (src/ORBmatcher.cc:
+ * 1262-1470; LoopClosing::ComputeSim3, LoopClosing.cc:594, th 7.5): pKF1's map points
+ * projected into pKF2 through the Sim3 and pKF2's into pKF1, each to its least-distance
+ * feature (TH_HIGH), kept where the two directions agree.  kf1 / kf2: mvKeysUn, mDescriptors,
+ * n (the rest unused); mp1[i] / md1 = pKF1->GetMapPointMatches()[i] (flags ORBG_MP_VALID = pMP
+ * && !isBad()), likewise mp2 / md2; matched1[i] = vpMatches12[i] != NULL, matched2[idx2] = 1
+ * for each such point's GetIndexInKeyFrame(pKF2) (NULL: none); g = the two poses, the Sim3,
+ * pKF1's intrinsics (used both ways, as the reference does), mfLogScaleFactor,
+ * mnScaleLevels and the Frame's float bounds.  matches12[i] = the pKF2 index whose MapPoint
+ * becomes vpMatches12[i], -1 (slots already set keep theirs); *nfound = nFound. */
+typedef struct {
+    float T1w[12], T2w[12];      /* pKF1 / pKF2 GetPose() rows 0..2 */
+    float R12[9], t12[3], s12;   /* the Sim3 (R12 row-major) */
+    float fx, fy, cx, cy;        /* pKF1->fx .. */
+    float log_scale_factor;
+    int32_t nlevels;
+    orbg_bounds bounds;
+} orbg_sim3_pair;
+int orbg_search_by_sim3(orbg_ctx *ctx, const orbg_keyframe *kf1, const orbg_map_point *mp1,
+                        const uint8_t *md1, const uint8_t *matched1, const orbg_keyframe *kf2,
+                        const orbg_map_point *mp2, const uint8_t *md2, const uint8_t *matched2,
+                        const orbg_sim3_pair *g, float th, int32_t *matches12, int *nfound);
+/* Batched, device memory: pair p = KeyFrames d_kf1[p], d_kf2[p] of `kfs` (desc, kps, counts
+ * read) with d_pairs[p]; map points per KeyFrame slot at d_mps + kf * cap (descriptors
+ * d_mdesc + (kf * cap) * 32); d_matched1 / d_matched2 [npairs][cap] or NULL; outputs
+ * d_matches12 + p * cap, d_nfound[p].  Context stream; ORBG_ENOTSUP past 8192 keypoints. */
+int orbg_search_by_sim3_batch_device(orbg_ctx *ctx, const orbg_keyframes *kfs, int cap,
+                                     const int32_t *d_kf1, const int32_t *d_kf2,
+                                     const orbg_sim3_pair *d_pairs, const orbg_map_point *d_mps,
+                                     const uint8_t *d_mdesc, const uint8_t *d_matched1,
+                                     const uint8_t *d_matched2, int npairs, float th,
+                                     int32_t *d_matches12, int32_t *d_nfound);
 
 /* ---------------- Optimizer::PoseOptimization ----------------
  * One edge per Frame keypoint with a MapPoint (index order): EdgeSE3ProjectXYZOnlyPose when

@@ -225,3 +225,111 @@ int orc_search_by_projection_sim3(const orc_keypoint *kps, const uint8_t *desc, 
     orc_grid_free(&g);
     return nmatches;
 }
+
+/* one direction of SearchBySim3 (ORBmatcher.cc:1293-1365 / 1366-1440): the source
+ * KeyFrame's points through its pose (Tsw) and M | tm (sR21 | t21 or sR12 | t12) into the
+ * target KeyFrame; vn[i] = the target index of the least distance (TH_HIGH), -1 */
+static void sim3_direction(const orc_keypoint *tk, const uint8_t *tdesc, int nt,
+                           const orc_map_point *mps, const uint8_t *mdesc, const uint8_t *am,
+                           int ns, const float *Tsw, const float *M, const float *tm,
+                           const orc_sim3_pair *g, float th, const float *scale_factors, int *vn)
+{
+    ogrid gr;
+    orc_grid_build(&gr, tk, nt, &g->bounds);
+    ogrid gk = gr;
+    const float kminx = (float)(int)g->bounds.min_x, kmaxx = (float)(int)g->bounds.max_x;
+    const float kminy = (float)(int)g->bounds.min_y, kmaxy = (float)(int)g->bounds.max_y;
+    gk.b.min_x = kminx;
+    gk.b.min_y = kminy;
+    const float ts[3] = {Tsw[3], Tsw[7], Tsw[11]};
+    float M4[12]; /* M as a 3x4 for orc_gemm3 */
+    for (int r = 0; r < 3; r++) {
+        for (int c = 0; c < 3; c++)
+            M4[4 * r + c] = M[3 * r + c];
+        M4[4 * r + 3] = 0.f;
+    }
+    int *cand = (int *)malloc(sizeof(int) * (nt > 0 ? nt : 1));
+    for (int i = 0; i < ns; i++) {
+        vn[i] = -1;
+        const orc_map_point *mp = &mps[i];
+        if (!(mp->flags & ORC_MP_VALID) || (am && am[i]))
+            continue;
+        const float P[3] = {mp->x, mp->y, mp->z};
+        float Pcs[3], Pc[3];
+        orc_gemm3(Tsw, 0, P, 1.0f, ts, Pcs);
+        orc_gemm3(M4, 0, Pcs, 1.0f, tm, Pc);
+        if (Pc[2] < 0.0)
+            continue;
+        const float invz = (float)(1.0 / (double)Pc[2]);
+        const float x = Pc[0] * invz;
+        const float y = Pc[1] * invz;
+        const float u = g->fx * x + g->cx;
+        const float v = g->fy * y + g->cy;
+        if (!(u >= kminx && u < kmaxx && v >= kminy && v < kmaxy))
+            continue;
+        const float maxDistance = 1.2f * mp->max_dist;
+        const float minDistance = 0.8f * mp->min_dist;
+        const float dist3D = norm3(Pc);
+        if (dist3D < minDistance || dist3D > maxDistance)
+            continue;
+        const int lvl = predict_scale(mp->max_dist, dist3D, g->log_scale_factor, g->nlevels);
+        const float radius = th * scale_factors[lvl];
+        const int nc = orc_features_in_area(&gk, tk, u, v, radius, -1, -1, cand);
+        int bestDist = 1 << 30, bestIdx = -1;
+        for (int k = 0; k < nc; k++) {
+            const int idx = cand[k];
+            const int o = tk[idx].octave;
+            if (o < lvl - 1 || o > lvl)
+                continue;
+            const int d = orc_descriptor_distance(mdesc + (size_t)i * 32, tdesc + (size_t)idx * 32);
+            if (d < bestDist) {
+                bestDist = d;
+                bestIdx = idx;
+            }
+        }
+        if (bestDist <= 100) /* TH_HIGH */
+            vn[i] = bestIdx;
+    }
+    free(cand);
+    orc_grid_free(&gr);
+}
+
+int orc_search_by_sim3(const orc_keypoint *k1, const uint8_t *d1, int n1, const orc_map_point *mp1,
+                       const uint8_t *md1, const uint8_t *matched1, const orc_keypoint *k2,
+                       const uint8_t *d2, int n2, const orc_map_point *mp2, const uint8_t *md2,
+                       const uint8_t *matched2, const orc_sim3_pair *g, float th,
+                       const float *scale_factors, int32_t *matches12)
+{
+    /* sR12 = s12*R12, sR21 = (1.0/s12)*R12.t(): Mat * scalar = convertTo with the float
+     * alpha (one rounding per element); t21 = -sR21*t12 by gemm (ORBmatcher.cc:1275-1279) */
+    float sR12[9], sR21[9], t21[3];
+    const float a = (float)(1.0 / (double)g->s12);
+    for (int r = 0; r < 3; r++)
+        for (int c = 0; c < 3; c++) {
+            sR12[3 * r + c] = g->R12[3 * r + c] * g->s12 + 0.0f;
+            sR21[3 * r + c] = g->R12[3 * c + r] * a + 0.0f;
+        }
+    for (int r = 0; r < 3; r++) {
+        double t = 0.0;
+        for (int k = 0; k < 3; k++)
+            t += (double)sR21[3 * r + k] * (double)g->t12[k];
+        t21[r] = (float)(t * -1.0);
+    }
+    int *vn1 = (int *)malloc(sizeof(int) * (n1 > 0 ? n1 : 1));
+    int *vn2 = (int *)malloc(sizeof(int) * (n2 > 0 ? n2 : 1));
+    sim3_direction(k2, d2, n2, mp1, md1, matched1, n1, g->T1w, sR21, t21, g, th, scale_factors, vn1);
+    sim3_direction(k1, d1, n1, mp2, md2, matched2, n2, g->T2w, sR12, g->t12, g, th, scale_factors,
+                   vn2);
+    int nFound = 0;
+    for (int i1 = 0; i1 < n1; i1++) {
+        matches12[i1] = -1;
+        const int idx2 = vn1[i1];
+        if (idx2 >= 0 && vn2[idx2] == i1) {
+            matches12[i1] = idx2;
+            nFound++;
+        }
+    }
+    free(vn1);
+    free(vn2);
+    return nFound;
+}

@@ -321,6 +321,24 @@ int orc_search_by_projection_sim3(const orc_keypoint *kps, const uint8_t *desc, 
                                   const uint8_t *taken0, const orc_frustum_cam *cam,
                                   const float *scale_factors, const orc_map_point *mps,
                                   const uint8_t *mdesc, int nm, int th, int32_t *match);
+/* ORBmatcher::SearchBySim3(pKF1, pKF2, vpMatches12, s12, R12, t12, th) (ORBmatcher.cc:
+ * 1262-1470): mp1[i] = pKF1->GetMapPointMatches()[i] (ORC_MP_VALID = pMP && !isBad()),
+ * matched1[i] = vpMatches12[i] != NULL, matched2[idx2] = 1 at those points' index in pKF2 (NULL:
+ * none); g = poses, Sim3, pKF1's intrinsics, mfLogScaleFactor, mnScaleLevels, float bounds.
+ * matches12[i] = the pKF2 index agreed both ways, -1; returns nFound. */
+typedef struct {
+    float T1w[12], T2w[12];
+    float R12[9], t12[3], s12;
+    float fx, fy, cx, cy;
+    float log_scale_factor;
+    int32_t nlevels;
+    orc_bounds bounds;
+} orc_sim3_pair;
+int orc_search_by_sim3(const orc_keypoint *k1, const uint8_t *d1, int n1, const orc_map_point *mp1,
+                       const uint8_t *md1, const uint8_t *matched1, const orc_keypoint *k2,
+                       const uint8_t *d2, int n2, const orc_map_point *mp2, const uint8_t *md2,
+                       const uint8_t *matched2, const orc_sim3_pair *g, float th,
+                       const float *scale_factors, int32_t *matches12);
 
 /* ---- Optimizer::PoseOptimization (pose_oracle.c) ---- */
 /* LM's pow(2 rho - 1, 3) as the once-rounded exact cube (optimization_algorithm_levenberg.cpp:135) */

@@ -49,6 +49,11 @@ MAPPOINT_DTYPE = np.dtype([("x", "<f4"), ("y", "<f4"), ("z", "<f4"), ("nx", "<f4
                            ("max_dist", "<f4"), ("flags", "<i4")])
 RELOC_DTYPE = np.dtype([("x", "<f4"), ("y", "<f4"), ("z", "<f4"), ("min_dist", "<f4"),
                         ("max_dist", "<f4"), ("angle", "<f4"), ("flags", "<i4")])
+SIM3_PAIR_DTYPE = np.dtype([("T1w", "<f4", 12), ("T2w", "<f4", 12), ("R12", "<f4", 9),
+                            ("t12", "<f4", 3), ("s12", "<f4"), ("fx", "<f4"), ("fy", "<f4"),
+                            ("cx", "<f4"), ("cy", "<f4"), ("log_scale_factor", "<f4"),
+                            ("nlevels", "<i4"), ("min_x", "<f4"), ("max_x", "<f4"),
+                            ("min_y", "<f4"), ("max_y", "<f4")])
 FRUSTUM_DTYPE = np.dtype([("Tcw", "<f4", 12), ("fx", "<f4"), ("fy", "<f4"), ("cx", "<f4"),
                           ("cy", "<f4"), ("bf", "<f4"), ("log_scale_factor", "<f4"),
                           ("nlevels", "<i4"), ("min_x", "<f4"), ("max_x", "<f4"),
@@ -208,6 +213,9 @@ def lib():
         L.orc_search_by_projection_sim3.argtypes = [vp, vp, C.c_int, vp, vp, vp, vp, vp,
                                                     C.c_int, C.c_int, vp]
         L.orc_search_by_projection_sim3.restype = C.c_int
+        L.orc_search_by_sim3.argtypes = [vp, vp, C.c_int, vp, vp, vp, vp, vp, C.c_int, vp, vp,
+                                         vp, vp, C.c_float, vp, vp]
+        L.orc_search_by_sim3.restype = C.c_int
         L.orc_sim3_decompose.restype = None
         L.orc_search_by_bow_kf.restype = C.c_int
         L.orc_search_by_bow_kf.argtypes = [vp, vp, vp, C.c_int, vp, vp, vp, C.c_int, vp, vp, vp,
@@ -817,3 +825,22 @@ def search_by_projection_sim3(kps, desc, taken0, fcam, scale_factors, mps, mdesc
                                             _p(sf), _p(mps), _p(mdesc), len(mps), int(th),
                                             _p(match))
     return n, match[:len(kps)].copy()
+
+
+def search_by_sim3(kf1, mp1, md1, matched1, kf2, mp2, md2, matched2, g, th, scale_factors):
+    """ORBmatcher::SearchBySim3 (oracle/loop_oracle.c) -> (nFound, matches12).  kf1 / kf2:
+    dict(kps, desc); mp* MAPPOINT_DTYPE per KeyFrame slot; matched* uint8 or None; g a
+    SIM3_PAIR_DTYPE record."""
+    k1, d1, _, a1 = _frame_args(kf1["kps"], kf1["desc"], None, matched1)
+    k2, d2, _, a2 = _frame_args(kf2["kps"], kf2["desc"], None, matched2)
+    mp1 = np.ascontiguousarray(mp1, MAPPOINT_DTYPE)
+    mp2 = np.ascontiguousarray(mp2, MAPPOINT_DTYPE)
+    md1 = np.ascontiguousarray(md1, np.uint8)
+    md2 = np.ascontiguousarray(md2, np.uint8)
+    g = np.ascontiguousarray(g, SIM3_PAIR_DTYPE)
+    sf = np.ascontiguousarray(scale_factors, np.float32)
+    m = np.zeros(max(len(k1), 1), np.int32)
+    n = lib().orc_search_by_sim3(_p(k1), _p(d1), len(k1), _p(mp1), _p(md1), _p(a1), _p(k2),
+                                 _p(d2), len(k2), _p(mp2), _p(md2), _p(a2), _p(g), float(th),
+                                 _p(sf), _p(m))
+    return n, m[:len(k1)].copy()

@@ -50,6 +50,11 @@ MP_DTYPE = np.dtype([("u", "<f4"), ("v", "<f4"), ("ur", "<f4"), ("level", "<i4")
 CAMERA_DTYPE = np.dtype([("fx", "<f4"), ("fy", "<f4"), ("cx", "<f4"), ("cy", "<f4"),
                          ("k1", "<f4"), ("k2", "<f4"), ("p1", "<f4"), ("p2", "<f4"),
                          ("k3", "<f4")])
+SIM3_PAIR_DTYPE = np.dtype([("T1w", "<f4", 12), ("T2w", "<f4", 12), ("R12", "<f4", 9),
+                            ("t12", "<f4", 3), ("s12", "<f4"), ("fx", "<f4"), ("fy", "<f4"),
+                            ("cx", "<f4"), ("cy", "<f4"), ("log_scale_factor", "<f4"),
+                            ("nlevels", "<i4"), ("min_x", "<f4"), ("max_x", "<f4"),
+                            ("min_y", "<f4"), ("max_y", "<f4")])
 RELOC_DTYPE = np.dtype([("x", "<f4"), ("y", "<f4"), ("z", "<f4"), ("min_dist", "<f4"),
                         ("max_dist", "<f4"), ("angle", "<f4"), ("flags", "<i4")])
 MAPPOINT_DTYPE = np.dtype([("x", "<f4"), ("y", "<f4"), ("z", "<f4"), ("nx", "<f4"),
@@ -256,6 +261,10 @@ def lib():
                                                   i32, vp, P(i32)]),
         "orbg_search_by_projection_sim3": (i32, [vp, vp, vp, i32, vp, vp, vp, vp, i32, i32, vp,
                                                  P(i32)]),
+        "orbg_search_by_sim3": (i32, [vp, P(KeyFrame), vp, vp, vp, P(KeyFrame), vp, vp, vp, vp,
+                                      f32, vp, P(i32)]),
+        "orbg_search_by_sim3_batch_device": (i32, [vp, P(KeyFrames), i32, vp, vp, vp, vp, vp, vp,
+                                                   vp, i32, f32, vp, vp]),
         "orbg_fuse_sim3": (i32, [vp, P(KeyFrame), vp, vp, vp, i32, f32, vp, vp, P(i32)]),
         "orbg_fuse_sim3_batch_device": (i32, [vp, P(KeyFrames), i32, vp, vp, vp, vp, vp, i32, i32, f32,
                                          vp, vp, vp]),

@@ -11,6 +11,9 @@
 //                 reference's enumeration (cell major, ascending index inside a cell), its
 //                 strict <.  Returns bestIdx per point (-1 unless bestDist <= TH_LOW): the
 //                 caller's sequential map update (Replace / AddObservation) applies it.
+//   k_sim3_match  ORBmatcher::SearchBySim3(pKF1, pKF2, vpMatches12, s12, R12, t12, th)
+//   k_sim3_resolve  (src/ORBmatcher.cc:1262-1470; LoopClosing::ComputeSim3): both projection
+//                 directions on the same LDS grid machinery, then the mutual check.
 //   k_tri_match   ORBmatcher::SearchForTriangulation(pKF1, pKF2, F12, vMatchedPairs,
 //                 bOnlyStereo) (src/ORBmatcher.cc:779-957; LocalMapping::CreateNewMapPoints,
 //                 LocalMapping.cc:305-378), one 256-thread workgroup per (KF1, KF2) pair.
@@ -307,42 +310,22 @@ struct FuseKey {  // a grid entry in LDS
 };
 
 #define FU_CELLS (ORBG_GRID_COLS * ORBG_GRID_ROWS)
-static_assert(FU_CELLS == 256 * 12, "k_fuse's scan gives 12 grid cells to each of 256 threads");
+static_assert(FU_CELLS == 256 * 12, "kf_grid_build's scan gives 12 grid cells to each of 256 threads");
 
-// SIM3 = false: Fuse(pKF, vpMapPoints, th) (:968-1069).  SIM3 = true: Fuse(pKF, Scw, vpPoints,
-// th, vpReplacePoint) (:1133-1238): cams[p].Tcw holds Scw's rows 0..2, and the candidates
-// are ranked by descriptor distance alone (no reprojection gate, no mvuRight)
-template <bool SIM3>
-__global__ __launch_bounds__(256) void k_fuse(orbg_keyframes K, int cap,
-                                              const int32_t *__restrict__ kf_index,
-                                              const orbg_frustum_camera *__restrict__ cams,
-                                              const orbg_map_point *__restrict__ mps,
-                                              const uint8_t *__restrict__ mdesc,
-                                              const int32_t *__restrict__ mcounts, int mcap,
-                                              float th, FuseTables T,
-                                              int32_t *__restrict__ best_idx,
-                                              int32_t *__restrict__ best_dist,
-                                              int32_t *__restrict__ nfused)
+// A KeyFrame's grid (Frame::AssignFeaturesToGrid / PosInGrid, Frame.cc:273-274, 292-307,
+// 510-520, copied into the KeyFrame) counting-sorted into LDS by all 256 threads:
+// afterwards cstart[c] is the END of cell c (its start cstart[c - 1]); the order inside a cell
+// is irrelevant (the selection keys carry the index).
+__device__ void kf_grid_build(const orbg_keypoint *__restrict__ kps, int n, const orbg_bounds &B,
+                              float inv_w, float inv_h, int *cstart, FuseKey *keys)
 {
-    extern __shared__ __attribute__((aligned(16))) uint8_t fu_lds[];
-    int *cstart = (int *)fu_lds;                         // FU_CELLS + 1
-    FuseKey *keys = (FuseKey *)(fu_lds + (FU_CELLS + 4) * 4);
-    __shared__ int nf_total;
-    const int p = blockIdx.x, tid = threadIdx.x;
-    const int kf = kf_index[p];
-    const int n = K.counts[kf];
-    const orbg_frustum_camera C = cams[p];
-    const orbg_keypoint *kps = K.kps + (size_t)kf * cap;
-    // ---- the KeyFrame grid (Frame.cc:273-274, 292-307, PosInGrid :510-520) ----
-    const float inv_w = (float)ORBG_GRID_COLS / (float)(C.bounds.max_x - C.bounds.min_x);
-    const float inv_h = (float)ORBG_GRID_ROWS / (float)(C.bounds.max_y - C.bounds.min_y);
+    const int tid = threadIdx.x;
     for (int c = tid; c <= FU_CELLS; c += 256) cstart[c] = 0;
-    if (tid == 0) nf_total = 0;
     __syncthreads();
     for (int i = tid; i < n; i += 256) {
         const orbg_keypoint kp = kps[i];
-        const int px = (int)roundf((kp.x - C.bounds.min_x) * inv_w);
-        const int py = (int)roundf((kp.y - C.bounds.min_y) * inv_h);
+        const int px = (int)roundf((kp.x - B.min_x) * inv_w);
+        const int py = (int)roundf((kp.y - B.min_y) * inv_h);
         if (px < 0 || px >= ORBG_GRID_COLS || py < 0 || py >= ORBG_GRID_ROWS) continue;
         atomicAdd(&cstart[px * ORBG_GRID_ROWS + py + 1], 1);
     }
@@ -369,18 +352,116 @@ __global__ __launch_bounds__(256) void k_fuse(orbg_keyframes K, int cap,
         }
     }
     __syncthreads();
-    // scatter: cstart[c] (the start of cell c) is the cell's cursor, so afterwards it holds
-    // the cell's end and the start is cstart[c - 1]; the order inside a cell is irrelevant
-    // (the selection key carries the index)
+    // scatter: cstart[c] (the start of cell c) is the cell's cursor
     for (int i = tid; i < n; i += 256) {
         const orbg_keypoint kp = kps[i];
-        const int px = (int)roundf((kp.x - C.bounds.min_x) * inv_w);
-        const int py = (int)roundf((kp.y - C.bounds.min_y) * inv_h);
+        const int px = (int)roundf((kp.x - B.min_x) * inv_w);
+        const int py = (int)roundf((kp.y - B.min_y) * inv_h);
         if (px < 0 || px >= ORBG_GRID_COLS || py < 0 || py >= ORBG_GRID_ROWS) continue;
         const int slot = atomicAdd(&cstart[px * ORBG_GRID_ROWS + py], 1);
         keys[slot] = FuseKey{kp.x, kp.y, i << 4 | (kp.octave & 15)};
     }
     __syncthreads();
+}
+
+// KeyFrame::GetFeaturesInArea(u, v, r) (KeyFrame.cc:750-790: the cell range on the int
+// bounds kminx / kminy with the Frame's cell sizes, |dx| < r && |dy| < r), the level window
+// [lvl - 1, lvl], gate(idx, octave, kx, ky) and the least 64-bit key (distance, cell, index):
+// the first candidate of the least distance in the reference's enumeration (strict <).
+// Returns ~0 when no candidate passes.
+template <class Gate>
+__device__ __forceinline__ unsigned long long kf_grid_best(const int *cstart, const FuseKey *keys,
+                                                           const uint8_t *__restrict__ kdesc,
+                                                           const uint32_t q[8], float u, float v,
+                                                           float r, int lvl, float kminx,
+                                                           float kminy, float inv_w, float inv_h,
+                                                           Gate gate)
+{
+    const int cx0 = max(0, (int)floorf((u - kminx - r) * inv_w));
+    if (cx0 >= ORBG_GRID_COLS) return ~0ull;
+    const int cx1 = min(ORBG_GRID_COLS - 1, (int)ceilf((u - kminx + r) * inv_w));
+    if (cx1 < 0) return ~0ull;
+    const int cy0 = max(0, (int)floorf((v - kminy - r) * inv_h));
+    if (cy0 >= ORBG_GRID_ROWS) return ~0ull;
+    const int cy1 = min(ORBG_GRID_ROWS - 1, (int)ceilf((v - kminy + r) * inv_h));
+    if (cy1 < 0) return ~0ull;
+    unsigned long long best = ~0ull;
+    for (int ix = cx0; ix <= cx1; ix++)
+        for (int iy = cy0; iy <= cy1; iy++) {
+            const int c = ix * ORBG_GRID_ROWS + iy;
+            const int j0 = c ? cstart[c - 1] : 0, j1 = cstart[c];
+            for (int j = j0; j < j1; j++) {
+                const FuseKey e = keys[j];
+                if (!(fabsf(e.x - u) < r && fabsf(e.y - v) < r)) continue;
+                const int kl = e.io & 15, idx = e.io >> 4;
+                if (kl < lvl - 1 || kl > lvl) continue;
+                if (!gate(idx, kl, e.x, e.y)) continue;
+                const uint4 *kd = (const uint4 *)(kdesc + (size_t)idx * 32);
+                const uint4 a = kd[0], b = kd[1];
+                const int d = __popc(q[0] ^ a.x) + __popc(q[1] ^ a.y) + __popc(q[2] ^ a.z) +
+                              __popc(q[3] ^ a.w) + __popc(q[4] ^ b.x) + __popc(q[5] ^ b.y) +
+                              __popc(q[6] ^ b.z) + __popc(q[7] ^ b.w);
+                const unsigned long long key = ((unsigned long long)d << 40) |
+                                               ((unsigned long long)c << 20) | (unsigned)idx;
+                best = key < best ? key : best;
+            }
+        }
+    return best;
+}
+
+__device__ __forceinline__ void load_desc8(const uint8_t *__restrict__ p, uint32_t q[8])
+{
+    const uint4 *dp = (const uint4 *)p;
+    const uint4 a = dp[0], b = dp[1];
+    q[0] = a.x; q[1] = a.y; q[2] = a.z; q[3] = a.w;
+    q[4] = b.x; q[5] = b.y; q[6] = b.z; q[7] = b.w;
+}
+
+// cv::gemm small-matrix pin: out = alpha * A x (+ c), A the 3x3 block of a 3x4 (stride 4) or
+// 3x3 (stride 3) row-major matrix, double work type, one rounding per element
+__device__ __forceinline__ void mk_gemm3(const float *A, int stride, bool trans, const float x[3],
+                                         double alpha, const float *c, float out[3])
+{
+#pragma unroll
+    for (int r = 0; r < 3; r++) {
+        double t = 0.0;
+#pragma unroll
+        for (int k = 0; k < 3; k++)
+            t += (double)(trans ? A[stride * k + r] : A[stride * r + k]) * (double)x[k];
+        t *= alpha;
+        if (c) t += (double)c[r];
+        out[r] = (float)t;
+    }
+}
+
+// SIM3 = false: Fuse(pKF, vpMapPoints, th) (:968-1069).  SIM3 = true: Fuse(pKF, Scw, vpPoints,
+// th, vpReplacePoint) (:1133-1238): cams[p].Tcw holds Scw's rows 0..2, and the candidates
+// are ranked by descriptor distance alone (no reprojection gate, no mvuRight)
+template <bool SIM3>
+__global__ __launch_bounds__(256) void k_fuse(orbg_keyframes K, int cap,
+                                              const int32_t *__restrict__ kf_index,
+                                              const orbg_frustum_camera *__restrict__ cams,
+                                              const orbg_map_point *__restrict__ mps,
+                                              const uint8_t *__restrict__ mdesc,
+                                              const int32_t *__restrict__ mcounts, int mcap,
+                                              float th, FuseTables T,
+                                              int32_t *__restrict__ best_idx,
+                                              int32_t *__restrict__ best_dist,
+                                              int32_t *__restrict__ nfused)
+{
+    extern __shared__ __attribute__((aligned(16))) uint8_t fu_lds[];
+    int *cstart = (int *)fu_lds;                         // FU_CELLS + 1
+    FuseKey *keys = (FuseKey *)(fu_lds + (FU_CELLS + 4) * 4);
+    __shared__ int nf_total;
+    const int p = blockIdx.x, tid = threadIdx.x;
+    const int kf = kf_index[p];
+    const int n = K.counts[kf];
+    const orbg_frustum_camera C = cams[p];
+    const orbg_keypoint *kps = K.kps + (size_t)kf * cap;
+    const float inv_w = (float)ORBG_GRID_COLS / (float)(C.bounds.max_x - C.bounds.min_x);
+    const float inv_h = (float)ORBG_GRID_ROWS / (float)(C.bounds.max_y - C.bounds.min_y);
+    if (tid == 0) nf_total = 0;
+    kf_grid_build(kps, n, C.bounds, inv_w, inv_h, cstart, keys);
     // KeyFrame::mnMinX .. mnMaxY are ints, the Frame's truncated (KeyFrame.h:288-291,
     // KeyFrame.cc:51): IsInImage and GetFeaturesInArea's cell range use them, the grid (and
     // its inverse cell sizes) is the Frame's
@@ -395,18 +476,13 @@ __global__ __launch_bounds__(256) void k_fuse(orbg_keyframes K, int cap,
 #pragma unroll
         for (int k = 0; k < 12; k++) Tw[k] = C.Tcw[k];
     }
-    const float tcw0 = Tw[3], tcw1 = Tw[7], tcw2 = Tw[11];
+    const float tc[3] = {Tw[3], Tw[7], Tw[11]};
     // KeyFrame::GetCameraCenter: Ow = -Rwc*tcw (cv::gemm pin); the Sim3 variant's
     // Ow = -Rcw.t()*tcw is the same sums
     float Ow[3];
-#pragma unroll
-    for (int r = 0; r < 3; r++) {
-        double t = 0.0;
-        t += (double)Tw[r] * (double)tcw0;
-        t += (double)Tw[4 + r] * (double)tcw1;
-        t += (double)Tw[8 + r] * (double)tcw2;
-        Ow[r] = (float)(t * -1.0);
-    }
+    mk_gemm3(Tw, 4, true, tc, -1.0, nullptr, Ow);
+    const uint8_t *kdesc = K.desc + (size_t)kf * cap * 32;
+    const float *kur = (!SIM3 && K.uright) ? K.uright + (size_t)kf * cap : nullptr;
     for (int i = tid; i < nm; i += 256) {
         const size_t o = (size_t)p * mcap + i;
         int bidx = -1, bdist = 256;
@@ -415,16 +491,7 @@ __global__ __launch_bounds__(256) void k_fuse(orbg_keyframes K, int cap,
             if (!(mp.flags & ORBG_MP_VALID)) break;
             const float P[3] = {mp.x, mp.y, mp.z};
             float Pc[3];
-            const float tc[3] = {tcw0, tcw1, tcw2};
-#pragma unroll
-            for (int r = 0; r < 3; r++) {
-                double t = 0.0;
-#pragma unroll
-                for (int k = 0; k < 3; k++) t += (double)Tw[4 * r + k] * (double)P[k];
-                t *= 1.0;
-                t += (double)tc[r];
-                Pc[r] = (float)t;
-            }
+            mk_gemm3(Tw, 4, false, P, 1.0, tc, Pc);
             if (Pc[2] < 0.0f) break;
             const float invz = 1 / Pc[2];
             const float x = Pc[0] * invz, y = Pc[1] * invz;
@@ -444,62 +511,25 @@ __global__ __launch_bounds__(256) void k_fuse(orbg_keyframes K, int cap,
             dot += (double)PO1 * (double)mp.ny;
             dot += (double)PO2 * (double)mp.nz;
             if (dot < 0.5 * (double)dist3D) break;
-            const float ratio = mp.max_dist / dist3D;
-            int lvl = (int)ceil(log((double)ratio) / (double)C.log_scale_factor);
-            if (lvl < 0)
-                lvl = 0;
-            else if (lvl >= C.nlevels)
-                lvl = C.nlevels - 1;
+            const int lvl = predict_scale(mp.max_dist, dist3D, C.log_scale_factor, C.nlevels);
             const float r = th * T.scale[lvl];
-            // GetFeaturesInArea's cells (KeyFrame.cc:755-769)
-            const int cx0 = max(0, (int)floorf((u - kminx - r) * inv_w));
-            if (cx0 >= ORBG_GRID_COLS) break;
-            const int cx1 = min(ORBG_GRID_COLS - 1, (int)ceilf((u - kminx + r) * inv_w));
-            if (cx1 < 0) break;
-            const int cy0 = max(0, (int)floorf((v - kminy - r) * inv_h));
-            if (cy0 >= ORBG_GRID_ROWS) break;
-            const int cy1 = min(ORBG_GRID_ROWS - 1, (int)ceilf((v - kminy + r) * inv_h));
-            if (cy1 < 0) break;
             uint32_t q[8];
-            {
-                const uint4 *dp = (const uint4 *)(mdesc + o * 32);
-                const uint4 a = dp[0], b = dp[1];
-                q[0] = a.x; q[1] = a.y; q[2] = a.z; q[3] = a.w;
-                q[4] = b.x; q[5] = b.y; q[6] = b.z; q[7] = b.w;
-            }
-            unsigned long long best = ~0ull;
-            for (int ix = cx0; ix <= cx1; ix++)
-                for (int iy = cy0; iy <= cy1; iy++) {
-                    const int c = ix * ORBG_GRID_ROWS + iy;
-                    // after the scatter cstart[c] = end of cell c: the start is cstart[c - 1]
-                    const int j0 = c ? cstart[c - 1] : 0, j1 = cstart[c];
-                    for (int j = j0; j < j1; j++) {
-                        const FuseKey e = keys[j];
-                        if (!(fabsf(e.x - u) < r && fabsf(e.y - v) < r)) continue;
-                        const int kl = e.io & 15, idx = e.io >> 4;
-                        if (kl < lvl - 1 || kl > lvl) continue;
-                        const float kr = !SIM3 && K.uright ? K.uright[(size_t)kf * cap + idx] : -1.0f;
-                        if (SIM3) {
-                            // ranked by descriptor distance alone (ORBmatcher.cc:1218-1236)
-                        } else if (kr >= 0) {
-                            const float ex = u - e.x, ey = v - e.y, er = ur - kr;
-                            const float e2 = ex * ex + ey * ey + er * er;
-                            if ((double)(e2 * T.inv_sigma2[kl]) > 7.8) continue;
-                        } else {
-                            const float ex = u - e.x, ey = v - e.y;
-                            const float e2 = ex * ex + ey * ey;
-                            if ((double)(e2 * T.inv_sigma2[kl]) > 5.99) continue;
-                        }
-                        const uint4 *kd = (const uint4 *)(K.desc + ((size_t)kf * cap + idx) * 32);
-                        const uint4 a = kd[0], b = kd[1];
-                        const int d = __popc(q[0] ^ a.x) + __popc(q[1] ^ a.y) + __popc(q[2] ^ a.z) +
-                                      __popc(q[3] ^ a.w) + __popc(q[4] ^ b.x) + __popc(q[5] ^ b.y) +
-                                      __popc(q[6] ^ b.z) + __popc(q[7] ^ b.w);
-                        const unsigned long long key = ((unsigned long long)d << 40) |
-                                                       ((unsigned long long)c << 20) | (unsigned)idx;
-                        best = key < best ? key : best;
-                    }
+            load_desc8(mdesc + o * 32, q);
+            // the chi-square reprojection gates (:1041-1063); the Sim3 variant has none
+            auto gate = [&](int idx, int kl, float kx, float ky) -> bool {
+                if (SIM3) return true;
+                const float kr = kur ? kur[idx] : -1.0f;
+                if (kr >= 0) {
+                    const float ex = u - kx, ey = v - ky, er = ur - kr;
+                    const float e2 = ex * ex + ey * ey + er * er;
+                    return !((double)(e2 * T.inv_sigma2[kl]) > 7.8);
                 }
+                const float ex = u - kx, ey = v - ky;
+                const float e2 = ex * ex + ey * ey;
+                return !((double)(e2 * T.inv_sigma2[kl]) > 5.99);
+            };
+            const unsigned long long best =
+                kf_grid_best(cstart, keys, kdesc, q, u, v, r, lvl, kminx, kminy, inv_w, inv_h, gate);
             if (best == ~0ull) break;
             bdist = (int)(best >> 40);
             if (bdist <= TM_TH_LOW) {
@@ -513,6 +543,124 @@ __global__ __launch_bounds__(256) void k_fuse(orbg_keyframes K, int cap,
     if (fused) atomicAdd(&nf_total, fused);
     __syncthreads();
     if (tid == 0) nfused[p] = nf_total;
+}
+
+// ---------------------------------------------------------------------------
+// SearchBySim3
+// ---------------------------------------------------------------------------
+// ORBmatcher::SearchBySim3(pKF1, pKF2, vpMatches12, s12, R12, t12, th) (ORBmatcher.cc:
+// 1262-1470; LoopClosing::ComputeSim3): both directions are per-point searches with no
+// shared state (each point's best over the other KeyFrame's grid, TH_HIGH), then the matches
+// that agree both ways are kept.  k_sim3_match: workgroup 2p + d = direction d of pair p
+// (d = 0: pKF1's points into pKF2 with sR21 / t21; d = 1: pKF2's into pKF1 with sR12 / t12),
+// writing vnMatch1 / vnMatch2; k_sim3_resolve: one workgroup per pair, the mutual check.
+#define SIM3_TH_HIGH 100
+
+__global__ __launch_bounds__(256) void k_sim3_match(orbg_keyframes K, int cap,
+                                                    const int32_t *__restrict__ kf1,
+                                                    const int32_t *__restrict__ kf2,
+                                                    const orbg_sim3_pair *__restrict__ pairs,
+                                                    const orbg_map_point *__restrict__ mps,
+                                                    const uint8_t *__restrict__ mdesc,
+                                                    const uint8_t *__restrict__ matched1,
+                                                    const uint8_t *__restrict__ matched2,
+                                                    float th, FuseTables T,
+                                                    int32_t *__restrict__ vn)
+{
+    extern __shared__ __attribute__((aligned(16))) uint8_t fu_lds[];
+    int *cstart = (int *)fu_lds;
+    FuseKey *keys = (FuseKey *)(fu_lds + (FU_CELLS + 4) * 4);
+    const int p = blockIdx.x >> 1, d = blockIdx.x & 1, tid = threadIdx.x;
+    const int ks = d ? kf2[p] : kf1[p], kt = d ? kf1[p] : kf2[p];  // source / target KeyFrame
+    const int ns = K.counts[ks], nt = K.counts[kt];
+    const orbg_sim3_pair G = pairs[p];
+    const float inv_w = (float)ORBG_GRID_COLS / (float)(G.bounds.max_x - G.bounds.min_x);
+    const float inv_h = (float)ORBG_GRID_ROWS / (float)(G.bounds.max_y - G.bounds.min_y);
+    kf_grid_build(K.kps + (size_t)kt * cap, nt, G.bounds, inv_w, inv_h, cstart, keys);
+    const float kminx = (float)(int)G.bounds.min_x, kmaxx = (float)(int)G.bounds.max_x;
+    const float kminy = (float)(int)G.bounds.min_y, kmaxy = (float)(int)G.bounds.max_y;
+    // sR12 = s12*R12, sR21 = (1.0/s12)*R12.t() (Mat * scalar: convertTo with the float alpha,
+    // one rounding), t21 = -sR21*t12 (gemm, alpha -1), :1275-1279
+    float M[9], tm[3];
+    if (d == 0) {
+        const float a = (float)(1.0 / (double)G.s12);
+#pragma unroll
+        for (int r = 0; r < 3; r++)
+#pragma unroll
+            for (int c = 0; c < 3; c++) M[3 * r + c] = G.R12[3 * c + r] * a + 0.0f;
+        mk_gemm3(M, 3, false, G.t12, -1.0, nullptr, tm);
+    } else {
+#pragma unroll
+        for (int k = 0; k < 9; k++) M[k] = G.R12[k] * G.s12 + 0.0f;
+#pragma unroll
+        for (int k = 0; k < 3; k++) tm[k] = G.t12[k];
+    }
+    const float *Tsw = d ? G.T2w : G.T1w;  // the source KeyFrame's pose
+    const float ts[3] = {Tsw[3], Tsw[7], Tsw[11]};
+    const uint8_t *am = d ? matched2 : matched1;
+    const uint8_t *kdesc = K.desc + (size_t)kt * cap * 32;
+    auto nogate = [](int, int, float, float) { return true; };
+    for (int i = tid; i < ns; i += 256) {
+        const size_t o = (size_t)ks * cap + i;
+        int best_i = -1;
+        const orbg_map_point mp = mps[o];
+        do {
+            // !pMP || vbAlreadyMatched || isBad (:1298-1304 / :1366-1372)
+            if (!(mp.flags & ORBG_MP_VALID)) break;
+            if (am && am[(size_t)p * cap + i]) break;
+            const float P[3] = {mp.x, mp.y, mp.z};
+            float Pcs[3], Pc[3];
+            mk_gemm3(Tsw, 4, false, P, 1.0, ts, Pcs);  // R1w*p3Dw + t1w
+            mk_gemm3(M, 3, false, Pcs, 1.0, tm, Pc);   // sR21*p3Dc1 + t21
+            if (Pc[2] < 0.0f) break;
+            const float invz = (float)(1.0 / (double)Pc[2]);
+            const float x = Pc[0] * invz, y = Pc[1] * invz;
+            const float u = G.fx * x + G.cx, v = G.fy * y + G.cy;
+            if (!(u >= kminx && u < kmaxx && v >= kminy && v < kmaxy)) break;
+            const float maxDistance = 1.2f * mp.max_dist, minDistance = 0.8f * mp.min_dist;
+            double s = 0.0;
+            s += (double)Pc[0] * (double)Pc[0];
+            s += (double)Pc[1] * (double)Pc[1];
+            s += (double)Pc[2] * (double)Pc[2];
+            const float dist3D = (float)sqrt(s);  // cv::norm(p3Dc2)
+            if (dist3D < minDistance || dist3D > maxDistance) break;
+            const int lvl = predict_scale(mp.max_dist, dist3D, G.log_scale_factor, G.nlevels);
+            const float r = th * T.scale[lvl];
+            uint32_t q[8];
+            load_desc8(mdesc + o * 32, q);
+            const unsigned long long best = kf_grid_best(cstart, keys, kdesc, q, u, v, r, lvl,
+                                                         kminx, kminy, inv_w, inv_h, nogate);
+            if (best != ~0ull && (int)(best >> 40) <= SIM3_TH_HIGH)
+                best_i = (int)(best & 0xFFFFFu);
+        } while (0);
+        vn[((size_t)p * 2 + d) * cap + i] = best_i;
+    }
+}
+
+// the mutual check (:1458-1470): vpMatches12[i1] = vpMapPoints2[idx2] when vnMatch1[i1] =
+// idx2 and vnMatch2[idx2] = i1
+__global__ __launch_bounds__(256) void k_sim3_resolve(const int32_t *__restrict__ kf1,
+                                                      const int32_t *__restrict__ counts, int cap,
+                                                      const int32_t *__restrict__ vn,
+                                                      int32_t *__restrict__ match12,
+                                                      int32_t *__restrict__ nfound)
+{
+    __shared__ int tot;
+    const int p = blockIdx.x, tid = threadIdx.x;
+    const int n1 = counts[kf1[p]];
+    if (tid == 0) tot = 0;
+    __syncthreads();
+    const int32_t *v1 = vn + (size_t)p * 2 * cap, *v2 = v1 + cap;
+    int cnt = 0;
+    for (int i = tid; i < n1; i += 256) {
+        const int i2 = v1[i];
+        const bool ok = i2 >= 0 && v2[i2] == i;
+        match12[(size_t)p * cap + i] = ok ? i2 : -1;
+        cnt += ok;
+    }
+    if (cnt) atomicAdd(&tot, cnt);
+    __syncthreads();
+    if (tid == 0) nfound[p] = tot;
 }
 
 int launch_fuse(hipStream_t st, const orbg_keyframes &K, int cap, const int32_t *kf,
@@ -541,6 +689,30 @@ int launch_fuse(hipStream_t st, const orbg_keyframes &K, int cap, const int32_t 
     else
         hipLaunchKernelGGL(k_fuse<false>, dim3(npairs), dim3(256), lds, st, K, cap, kf, cams,
                            mps, mdesc, mcounts, mcap, th, T, best_idx, best_dist, nfused);
+    return hipGetLastError() == hipSuccess ? 0 : -5;
+}
+
+// vn: scratch of npairs * 2 * cap int32 (vnMatch1 / vnMatch2 per pair)
+int launch_search_by_sim3(hipStream_t st, const orbg_keyframes &K, int cap, const int32_t *kf1,
+                          const int32_t *kf2, const orbg_sim3_pair *pairs,
+                          const orbg_map_point *mps, const uint8_t *mdesc,
+                          const uint8_t *matched1, const uint8_t *matched2, int npairs, float th,
+                          const float *scale, int nlevels, int32_t *vn, int32_t *match12,
+                          int32_t *nfound)
+{
+    if (npairs <= 0) return 0;
+    if (cap > 8192) return -95;  // the grid's entries in LDS
+    FuseTables T{};
+    for (int l = 0; l < ORBG_MAX_LEVELS; l++) T.scale[l] = scale[l < nlevels ? l : nlevels - 1];
+    const size_t lds = (FU_CELLS + 4) * 4 + (size_t)cap * sizeof(FuseKey);
+    if (lds > 64 * 1024 &&
+        hipFuncSetAttribute((const void *)k_sim3_match, hipFuncAttributeMaxDynamicSharedMemorySize,
+                            (int)lds) != hipSuccess)
+        return -5;
+    hipLaunchKernelGGL(k_sim3_match, dim3(2 * npairs), dim3(256), lds, st, K, cap, kf1, kf2,
+                       pairs, mps, mdesc, matched1, matched2, th, T, vn);
+    hipLaunchKernelGGL(k_sim3_resolve, dim3(npairs), dim3(256), 0, st, kf1, K.counts, cap, vn,
+                       match12, nfound);
     return hipGetLastError() == hipSuccess ? 0 : -5;
 }
 

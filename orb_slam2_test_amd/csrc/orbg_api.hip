@@ -85,6 +85,12 @@ int launch_fuse(hipStream_t st, const orbg_keyframes &K, int cap, const int32_t 
                 const int32_t *mcounts, int mcap, int npairs, float th, const float *scale,
                 const float *inv_sigma2, int nlevels, int sim3, int32_t *best_idx,
                 int32_t *best_dist, int32_t *nfused);
+int launch_search_by_sim3(hipStream_t st, const orbg_keyframes &K, int cap, const int32_t *kf1,
+                          const int32_t *kf2, const orbg_sim3_pair *pairs,
+                          const orbg_map_point *mps, const uint8_t *mdesc,
+                          const uint8_t *matched1, const uint8_t *matched2, int npairs, float th,
+                          const float *scale, int nlevels, int32_t *vn, int32_t *match12,
+                          int32_t *nfound);
 int launch_distinctive(hipStream_t st, const uint8_t *pool, const int32_t *rows,
                        const int32_t *off, int npoints, int32_t *best, uint8_t *desc_out);
 int launch_pose_opt(hipStream_t st, const orbg_pose_edge *edges, const int32_t *counts, int cap,
@@ -4348,6 +4354,129 @@ static int fuse_host(orbg_ctx *c, const orbg_keyframe *kf, const orbg_frustum_ca
     memcpy(best_idx, hs + o_bi, nm * 4);
     memcpy(best_dist, hs + o_bd, nm * 4);
     memcpy(nfused, hs + o_nf, 4);
+    return ORBG_OK;
+}
+
+// scratch for k_sim3_match's vnMatch1 / vnMatch2 (npairs * 2 * cap int32), kept in the
+// tracking scratch buffer (the two never run at once on a context)
+static int sim3_scratch(orbg_ctx *c, size_t need, void **out)
+{
+    if (c->trk_bytes < need) {
+        HIPCHK(hipStreamSynchronize(c->stream));
+        if (c->d_trk) hipFree(c->d_trk);
+        c->d_trk = nullptr;
+        c->trk_bytes = 0;
+        if (hipMalloc(&c->d_trk, need) != hipSuccess)
+            return set_err(ORBG_ENOMEM, "SearchBySim3 scratch %zu bytes", need);
+        c->trk_bytes = need;
+    }
+    *out = c->d_trk;
+    return ORBG_OK;
+}
+
+extern "C" int orbg_search_by_sim3_batch_device(orbg_ctx *c, const orbg_keyframes *kfs, int cap,
+                                                const int32_t *d_kf1, const int32_t *d_kf2,
+                                                const orbg_sim3_pair *d_pairs,
+                                                const orbg_map_point *d_mps,
+                                                const uint8_t *d_mdesc,
+                                                const uint8_t *d_matched1,
+                                                const uint8_t *d_matched2, int npairs, float th,
+                                                int32_t *d_matches12, int32_t *d_nfound)
+{
+    if (!c || !kfs) return set_err(ORBG_EINVAL, "NULL argument");
+    if (npairs < 0 || cap <= 0) return set_err(ORBG_EINVAL, "bad sizes");
+    if (npairs == 0) return ORBG_OK;
+    if (!d_kf1 || !d_kf2 || !d_pairs || !d_mps || !d_mdesc || !d_matches12 || !d_nfound ||
+        !kfs->desc || !kfs->kps || !kfs->counts)
+        return set_err(ORBG_EINVAL, "NULL device array");
+    if (cap > 8192) return set_err(ORBG_ENOTSUP, "SearchBySim3: more than 8192 keypoints");
+    HIPCHK(hipSetDevice(c->device));
+    hipStream_t st = c->stream;
+    void *vn;
+    int rc = sim3_scratch(c, (size_t)npairs * 2 * cap * 4, &vn);
+    if (rc) return rc;
+    PROF_LAUNCH(c, "sim3_match",
+                rc = launch_search_by_sim3(st, *kfs, cap, d_kf1, d_kf2, d_pairs, d_mps,
+                                           d_mdesc, d_matched1, d_matched2, npairs, th, c->scale,
+                                           c->p.nlevels, (int32_t *)vn, d_matches12, d_nfound));
+    if (rc) return set_err(ORBG_EIO, "k_sim3_match launch failed");
+    return ORBG_OK;
+}
+
+extern "C" int orbg_search_by_sim3(orbg_ctx *c, const orbg_keyframe *kf1, const orbg_map_point *mp1,
+                                   const uint8_t *md1, const uint8_t *matched1,
+                                   const orbg_keyframe *kf2, const orbg_map_point *mp2,
+                                   const uint8_t *md2, const uint8_t *matched2,
+                                   const orbg_sim3_pair *g, float th, int32_t *matches12,
+                                   int *nfound)
+{
+    if (!c || !kf1 || !kf2 || !g || !nfound) return set_err(ORBG_EINVAL, "NULL argument");
+    if (kf1->n < 0 || kf2->n < 0) return set_err(ORBG_EINVAL, "negative size");
+    const orbg_keyframe *kk[2] = {kf1, kf2};
+    for (int s = 0; s < 2; s++) {
+        if (kk[s]->n && (!kk[s]->kps || !kk[s]->desc)) return set_err(ORBG_EINVAL, "NULL KeyFrame array");
+        for (int i = 0; i < kk[s]->n; i++)
+            if (kk[s]->kps[i].octave < 0 || kk[s]->kps[i].octave >= ORBG_MAX_LEVELS)
+                return set_err(ORBG_EINVAL, "keypoint octave out of range");
+    }
+    if ((kf1->n && (!mp1 || !md1 || !matches12)) || (kf2->n && (!mp2 || !md2)))
+        return set_err(ORBG_EINVAL, "NULL map point array");
+    *nfound = 0;
+    for (int i = 0; i < kf1->n; i++) matches12[i] = -1;
+    if (kf1->n == 0 || kf2->n == 0) return ORBG_OK;
+    HIPCHK(hipSetDevice(c->device));
+    const int cap = std::max(kf1->n, kf2->n);
+    if (cap > 8192) return set_err(ORBG_ENOTSUP, "more than 8192 keypoints");
+    const size_t cp = (size_t)cap;
+    size_t o = 0;
+    auto take = [&](size_t bytes) {
+        const size_t r = o;
+        o += al256(bytes);
+        return r;
+    };
+    const size_t o_desc = take(2 * cp * 32), o_kps = take(2 * cp * sizeof(orbg_keypoint)),
+                 o_cnt = take(8), o_idx = take(8), o_pair = take(sizeof(orbg_sim3_pair)),
+                 o_mp = take(2 * cp * sizeof(orbg_map_point)), o_md = take(2 * cp * 32),
+                 o_am1 = take(cp), o_am2 = take(cp), o_m = take(cp * 4), o_nf = take(4);
+    uint8_t *hs;
+    int rc = stage(c, o, &hs);
+    if (rc) return rc;
+    void *d;
+    if ((rc = scratch(c, o, &d))) return rc;
+    uint8_t *db = (uint8_t *)d;
+    HIPCHK(hipStreamSynchronize(c->stream));
+    memset(hs, 0, o_m);
+    const orbg_map_point *mpp[2] = {mp1, mp2};
+    const uint8_t *mdp[2] = {md1, md2}, *amp[2] = {matched1, matched2};
+    for (int s = 0; s < 2; s++) {
+        const size_t n = (size_t)kk[s]->n;
+        memcpy(hs + o_desc + s * cp * 32, kk[s]->desc, n * 32);
+        memcpy(hs + o_kps + s * cp * sizeof(orbg_keypoint), kk[s]->kps, n * sizeof(orbg_keypoint));
+        ((int32_t *)(hs + o_cnt))[s] = kk[s]->n;
+        ((int32_t *)(hs + o_idx))[s] = s;
+        memcpy(hs + o_mp + s * cp * sizeof(orbg_map_point), mpp[s], n * sizeof(orbg_map_point));
+        memcpy(hs + o_md + s * cp * 32, mdp[s], n * 32);
+        if (amp[s]) memcpy(hs + (s ? o_am2 : o_am1), amp[s], n);
+    }
+    memcpy(hs + o_pair, g, sizeof(orbg_sim3_pair));
+    HIPCHK(hipMemcpyAsync(db, hs, o_m, hipMemcpyHostToDevice, c->stream));
+    orbg_keyframes K{};
+    K.desc = db + o_desc;
+    K.kps = (const orbg_keypoint *)(db + o_kps);
+    K.counts = (const int32_t *)(db + o_cnt);
+    void *vn;
+    if ((rc = sim3_scratch(c, cp * 2 * 4, &vn))) return rc;
+    rc = launch_search_by_sim3(c->stream, K, cap, (const int32_t *)(db + o_idx),
+                               (const int32_t *)(db + o_idx) + 1,
+                               (const orbg_sim3_pair *)(db + o_pair),
+                               (const orbg_map_point *)(db + o_mp), db + o_md, db + o_am1,
+                               db + o_am2, 1, th, c->scale, c->p.nlevels, (int32_t *)vn,
+                               (int32_t *)(db + o_m), (int32_t *)(db + o_nf));
+    if (rc) return set_err(ORBG_EIO, "k_sim3_match launch failed");
+    HIPCHK(hipMemcpyAsync(hs + o_m, db + o_m, o - o_m, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(hipStreamSynchronize(c->stream));
+    memcpy(matches12, hs + o_m, (size_t)kf1->n * 4);
+    memcpy(nfound, hs + o_nf, 4);
     return ORBG_OK;
 }
 

@@ -228,6 +228,34 @@ class ORBmatcher:
             "orbg_search_by_projection_sim3")
         return nm.value, match[:len(kps)].copy()
 
+    def SearchBySim3(self, pKF1, pKF2, mp1, md1, mp2, md2, g, th=7.5, matched1=None,
+                     matched2=None):
+        """ORBmatcher::SearchBySim3(pKF1, pKF2, vpMatches12, s12, R12, t12, th)
+        (ORBmatcher.cc:1262-1470; LoopClosing::ComputeSim3): pKF1 / pKF2 with mvKeysUn and
+        mDescriptors; mp1 / md1 MAPPOINT_DTYPE records + descriptors of
+        pKF1->GetMapPointMatches() (flags MP_VALID = pMP && !isBad()), likewise mp2 / md2;
+        g a SIM3_PAIR_DTYPE record (poses, s12 / R12 / t12, pKF1's intrinsics, bounds);
+        matched1[i] = vpMatches12[i] != NULL, matched2 their indices in pKF2.  Returns
+        (nFound, matches12): vpMatches12[i] = pKF2's MapPoint at matches12[i] (>= 0)."""
+        def side(fr):
+            k = np.ascontiguousarray(fr.mvKeysUn, L.KP_DTYPE)
+            d = np.ascontiguousarray(fr.mDescriptors, np.uint8)
+            return k, d, L.KeyFrame(L.ptr(k), L.ptr(d), None, None, len(k), None, None, None, 0)
+        k1, d1, K1 = side(pKF1)
+        k2, d2, K2 = side(pKF2)
+        a = [np.ascontiguousarray(x, L.MAPPOINT_DTYPE) for x in (mp1, mp2)]
+        b = [np.ascontiguousarray(x, np.uint8).reshape(-1, 32) for x in (md1, md2)]
+        m1 = None if matched1 is None else np.ascontiguousarray(matched1, np.uint8)
+        m2 = None if matched2 is None else np.ascontiguousarray(matched2, np.uint8)
+        gg = np.ascontiguousarray(g, L.SIM3_PAIR_DTYPE)
+        out = np.full(max(len(k1), 1), -1, np.int32)
+        n = C.c_int()
+        L.check(L.lib().orbg_search_by_sim3(
+            _ctx(self.device).handle, C.byref(K1), L.ptr(a[0]), L.ptr(b[0]), L.ptr(m1),
+            C.byref(K2), L.ptr(a[1]), L.ptr(b[1]), L.ptr(m2), L.ptr(gg), float(th), L.ptr(out),
+            C.byref(n)), "orbg_search_by_sim3")
+        return n.value, out[:len(k1)].copy()
+
     def SearchForTriangulation(self, pKF1, pKF2, geom, bOnlyStereo=False):
         """ORBmatcher::SearchForTriangulation(pKF1, pKF2, F12, vMatchedPairs, bOnlyStereo)
         (src/ORBmatcher.cc:779-957).  pKF1 / pKF2: Frames with mvKeysUn, mDescriptors,

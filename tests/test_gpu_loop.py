@@ -134,3 +134,83 @@ def test_batch_device(oracle, mode):
     for b in range(B):
         rn, rm = refs[b]
         assert nm[b] == rn and np.array_equal(match[b, :cnt[b]], rm) and rn > 100
+
+
+# ------------------------------------------------------------------ SearchBySim3
+@pytest.mark.parametrize("seed,s12,th,bounds", [(50, 1.05, 7.5, None), (51, 0.9, 7.5, T.FRAC),
+                                                (52, 1.02, 3.0, None), (53, 1.15, 7.5, None)])
+def test_search_by_sim3(oracle, seed, s12, th, bounds):
+    c = T.sim3_case(L, seed, n=2000, m=1300, s12=s12, bounds=bounds)
+    kf1, mp1, md1, a1, kf2, mp2, md2, a2, g, perm = c
+    sf = T._sf(oracle)
+    n, got = ORBmatcher().SearchBySim3(Frame(kf1["kps"], kf1["desc"]), Frame(kf2["kps"], kf2["desc"]),
+                                       mp1, md1, mp2, md2, g, th, a1, a2)
+    rn, ref = oracle.search_by_sim3(kf1, mp1.view(oracle.MAPPOINT_DTYPE), md1, a1, kf2,
+                                    mp2.view(oracle.MAPPOINT_DTYPE), md2, a2,
+                                    g.view(oracle.SIM3_PAIR_DTYPE), th, sf)
+    assert n == rn and np.array_equal(got, ref) and rn > 200
+
+
+def test_search_by_sim3_empty():
+    c = T.sim3_case(L, 54, n=80, m=40)
+    kf1, mp1, md1, a1, kf2, mp2, md2, a2, g, perm = c
+    m = ORBmatcher()
+    n, got = m.SearchBySim3(Frame(kf1["kps"], kf1["desc"]), Frame(kf2["kps"][:0], kf2["desc"][:0]),
+                            mp1, md1, mp2[:0], md2[:0], g)
+    assert n == 0 and np.all(got == -1)
+    n, got = m.SearchBySim3(Frame(kf1["kps"][:0], kf1["desc"][:0]), Frame(kf2["kps"], kf2["desc"]),
+                            mp1[:0], md1[:0], mp2, md2, g)
+    assert n == 0 and len(got) == 0
+
+
+def test_search_by_sim3_batch_device(oracle):
+    """LoopClosing::ComputeSim3's shape: the current KeyFrame against several loop
+    candidates, each with its own Sim3 and vpMatches12, all in HBM."""
+    import torch
+    P = 4
+    sf = T._sf(oracle)
+    cases = [T.sim3_case(L, 60 + p, n=1500 + 100 * p, m=900, s12=0.95 + 0.05 * p) for p in range(P)]
+    cap = max(len(c[0]["kps"]) for c in cases)
+    nk = 2 * P
+    kps = np.zeros((nk, cap), L.KP_DTYPE)
+    desc = np.zeros((nk, cap, 32), np.uint8)
+    cnt = np.zeros(nk, np.int32)
+    mps = np.zeros((nk, cap), L.MAPPOINT_DTYPE)
+    md = np.zeros((nk, cap, 32), np.uint8)
+    am1 = np.zeros((P, cap), np.uint8)
+    am2 = np.zeros((P, cap), np.uint8)
+    pairs = np.zeros(P, L.SIM3_PAIR_DTYPE)
+    refs = []
+    for p, (kf1, mp1, md1, a1, kf2, mp2, md2, a2, g, perm) in enumerate(cases):
+        for s, (kf, mp, mdd) in enumerate(((kf1, mp1, md1), (kf2, mp2, md2))):
+            n = len(kf["kps"])
+            kps[2 * p + s, :n], desc[2 * p + s, :n], cnt[2 * p + s] = kf["kps"], kf["desc"], n
+            mps[2 * p + s, :n], md[2 * p + s, :n] = mp, mdd
+        am1[p, :len(a1)], am2[p, :len(a2)] = a1, a2
+        pairs[p] = g
+        refs.append(oracle.search_by_sim3(kf1, mp1.view(oracle.MAPPOINT_DTYPE), md1, a1, kf2,
+                                          mp2.view(oracle.MAPPOINT_DTYPE), md2, a2,
+                                          g.view(oracle.SIM3_PAIR_DTYPE), 7.5, sf))
+    t = {k: torch.from_numpy(np.ascontiguousarray(v).view(np.uint8).reshape(-1).copy()).cuda()
+         for k, v in dict(kps=kps, desc=desc, cnt=cnt, mps=mps, md=md, am1=am1, am2=am2,
+                          pairs=pairs).items()}
+    K = L.KeyFrames(t["desc"].data_ptr(), t["kps"].data_ptr(), None, None, t["cnt"].data_ptr(),
+                    None, None, None, None)
+    i1 = torch.arange(0, nk, 2, dtype=torch.int32, device="cuda")
+    i2 = torch.arange(1, nk, 2, dtype=torch.int32, device="cuda")
+    out = torch.full((P * cap,), -9, dtype=torch.int32, device="cuda")
+    nf = torch.zeros(P, dtype=torch.int32, device="cuda")
+    ctx = _ctx()
+    torch.cuda.synchronize()
+    L.check(L.lib().orbg_search_by_sim3_batch_device(
+        ctx.handle, C.byref(K), cap, i1.data_ptr(), i2.data_ptr(), t["pairs"].data_ptr(),
+        t["mps"].data_ptr(), t["md"].data_ptr(), t["am1"].data_ptr(), t["am2"].data_ptr(), P, 7.5,
+        out.data_ptr(), nf.data_ptr()), "sim3 batch")
+    ctx.sync()
+    got = out.cpu().numpy().reshape(P, cap)
+    gn = nf.cpu().numpy()
+    for p in range(P):
+        rn, ref = refs[p]
+        n1 = len(cases[p][0]["kps"])
+        assert gn[p] == rn and np.array_equal(got[p, :n1], ref) and rn > 100
+        assert np.all(got[p, n1:] == -9)

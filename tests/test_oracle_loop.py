@@ -351,3 +351,140 @@ def test_loop_matchers_empty(oracle):
     n, m = oracle.search_by_projection_reloc(f["kps"][:0], f["desc"][:0], None, fcam, sf, pts,
                                              pd, 10, 100)
     assert n == 0 and len(m) == 0
+
+
+# ------------------------------------------------------------------ SearchBySim3
+def sim3_case(mod, seed, n=1500, m=900, s12=1.3, bounds=None):
+    """two KeyFrames of one scene in two map frames related by a Sim3: pKF1 sees m common
+    points at slots 0..m-1, pKF2 at a permutation of its slots; S12 = [s12 R12 | t12] maps
+    camera-2 to camera-1 coordinates.  Map point descriptors are noisy copies of their
+    keypoint's; some slots have no (or a bad) point; a few are matched before the call."""
+    rng = np.random.default_rng(seed)
+    fx, fy, cx, cy = KITTI_K
+    R12 = _rot(rng, 0.05)
+    t12 = rng.normal(0, 0.3, 3)
+    R1, R2 = _rot(rng, 0.3), _rot(rng, 0.3)
+    t1, t2 = rng.normal(0, 5, 3), rng.normal(0, 5, 3)
+    u1 = rng.uniform(5, W - 5, n)
+    v1 = rng.uniform(5, H - 5, n)
+    z1 = rng.uniform(4, 40, n)
+    pc1 = np.stack([(u1 - cx) * z1 / fx, (v1 - cy) * z1 / fy, z1], 1)
+    pc2 = ((pc1 - t12) @ R12) / s12  # R12^T (p - t12) / s12, row form
+    perm = rng.permutation(n)
+    sf = f32(1.2) ** np.arange(8)
+
+    octs = rng.integers(0, 8, n)  # one octave per scene point in both KeyFrames
+
+    def kf(pc, order, R, t):
+        k = np.zeros(n, mod.KP_DTYPE)
+        oc = octs
+        u = fx * pc[:, 0] / pc[:, 2] + cx + rng.normal(0, 0.8, n) * sf[oc]
+        v = fy * pc[:, 1] / pc[:, 2] + cy + rng.normal(0, 0.8, n) * sf[oc]
+        k["x"][order], k["y"][order], k["octave"][order] = u, v, oc
+        k["angle"], k["size"], k["response"] = rng.uniform(0, 360, n), 31, 20
+        # non-common slots (m..n-1 of pKF1's order): random points of the image
+        extra = order[m:]
+        k["x"][extra] = rng.uniform(0, W, len(extra))
+        k["y"][extra] = rng.uniform(0, H, len(extra))
+        pw = (pc - t) @ R  # R^T (pc - t)
+        mp = np.zeros(n, mod.MAPPOINT_DTYPE)
+        mp["x"][order], mp["y"][order], mp["z"][order] = pw[:, 0], pw[:, 1], pw[:, 2]
+        dist = np.linalg.norm(pc, axis=1)
+        mx = dist * f32(1.2) ** oc * rng.uniform(0.9, 1.1, n)
+        mp["max_dist"][order] = mx
+        mp["min_dist"][order] = mx / f32(1.2) ** 7 * rng.uniform(0.5, 2.0, n)
+        mp["flags"] = np.where(rng.random(n) < 0.88, 1, 0)
+        return k, mp
+
+    k1, mp1 = kf(pc1, np.arange(n), R1, t1)
+    k2, mp2 = kf(pc2, perm, R2, t2)
+    d1 = rng.integers(0, 256, (n, 32), dtype=np.uint8)
+    d2 = np.zeros_like(d1)
+    d2[perm[:m]] = d1[:m] ^ np.packbits(rng.random((m, 256)) < rng.uniform(0.0, 0.2, (m, 1)), axis=1)
+    d2[perm[m:]] = rng.integers(0, 256, (n - m, 32), dtype=np.uint8)
+    md1 = d1 ^ np.packbits(rng.random((n, 256)) < 0.05, axis=1)
+    md2 = d2 ^ np.packbits(rng.random((n, 256)) < 0.05, axis=1)
+    matched1 = (rng.random(n) < 0.05).astype(np.uint8)
+    matched2 = np.zeros(n, np.uint8)
+    common = np.nonzero(matched1[:m])[0]
+    matched2[perm[common]] = 1
+    g = np.zeros((), mod.SIM3_PAIR_DTYPE)
+    g["T1w"] = np.concatenate([R1, t1[:, None]], 1).astype(np.float32).reshape(12)
+    g["T2w"] = np.concatenate([R2, t2[:, None]], 1).astype(np.float32).reshape(12)
+    g["R12"] = R12.astype(np.float32).reshape(9)
+    g["t12"] = t12.astype(np.float32)
+    g["s12"] = s12
+    g["fx"], g["fy"], g["cx"], g["cy"] = fx, fy, cx, cy
+    g["log_scale_factor"] = f32(np.log(np.float64(f32(1.2))))
+    g["nlevels"] = 8
+    g["min_x"], g["max_x"], g["min_y"], g["max_y"] = bounds or (0.0, float(W), 0.0, float(H))
+    return (dict(kps=k1, desc=d1), mp1, md1, matched1, dict(kps=k2, desc=d2), mp2, md2,
+            matched2, g, perm)
+
+
+def py_search_by_sim3(kf1, mp1, md1, am1, kf2, mp2, md2, am2, g, th, sf):
+    b = tuple(f32(g[k]) for k in ("min_x", "max_x", "min_y", "max_y"))
+    kb = tuple(f32(int(x)) for x in b)
+    R12 = g["R12"].reshape(3, 3)
+    s12 = f32(g["s12"])
+    a = f32(1.0 / float(s12))
+    sR12 = (R12 * s12).astype(np.float32)
+    sR21 = (R12.T * a).astype(np.float32)
+    t21 = _gemm(sR21, g["t12"], -1.0, None)
+
+    def direction(tk, tdesc, mps, mdesc, am, Tsw, M, tm):
+        grid, iw, ih = _grid(tk, b)
+        T = Tsw.reshape(3, 4)
+        out = np.full(len(mps), -1, np.int32)
+        for i, mp in enumerate(mps):
+            if not mp["flags"] & 1 or (am is not None and am[i]):
+                continue
+            X = [f32(mp["x"]), f32(mp["y"]), f32(mp["z"])]
+            pcs = _gemm(T, X, 1.0, T[:, 3])
+            pc = _gemm(M, pcs, 1.0, tm)
+            if pc[2] < 0.0:
+                continue
+            invz = f32(1.0 / float(pc[2]))
+            u = f32(g["fx"]) * (pc[0] * invz) + f32(g["cx"])
+            v = f32(g["fy"]) * (pc[1] * invz) + f32(g["cy"])
+            if not (u >= kb[0] and u < kb[1] and v >= kb[2] and v < kb[3]):
+                continue
+            d3 = f32(np.sqrt(sum(float(x) * float(x) for x in pc)))
+            if d3 < f32(0.8) * mp["min_dist"] or d3 > f32(1.2) * mp["max_dist"]:
+                continue
+            lvl = _predict(mp["max_dist"], d3, g["log_scale_factor"], int(g["nlevels"]))
+            r = f32(th) * sf[lvl]
+            best, bi = 1 << 30, -1
+            for idx in _in_area(grid, iw, ih, kb[0], kb[2], tk, u, v, r, -1, -1):
+                o = int(tk["octave"][idx])
+                if o < lvl - 1 or o > lvl:
+                    continue
+                d = _ham(mdesc[i], tdesc[idx])
+                if d < best:
+                    best, bi = d, idx
+            if best <= 100:
+                out[i] = bi
+        return out
+
+    vn1 = direction(kf2["kps"], kf2["desc"], mp1, md1, am1, g["T1w"], sR21, t21)
+    vn2 = direction(kf1["kps"], kf1["desc"], mp2, md2, am2, g["T2w"], sR12, g["t12"])
+    m12 = np.full(len(mp1), -1, np.int32)
+    for i1, i2 in enumerate(vn1):
+        if i2 >= 0 and vn2[i2] == i1:
+            m12[i1] = i2
+    return int((m12 >= 0).sum()), m12
+
+
+@pytest.mark.parametrize("seed,s12,th,bounds", [(50, 1.05, 7.5, None), (51, 0.9, 7.5, FRAC),
+                                                (52, 1.02, 3.0, None), (53, 1.15, 7.5, None)])
+def test_search_by_sim3_equals_python(oracle, seed, s12, th, bounds):
+    c = sim3_case(oracle, seed, n=900, m=600, s12=s12, bounds=bounds)
+    kf1, mp1, md1, a1, kf2, mp2, md2, a2, g, perm = c
+    sf = _sf(oracle)
+    n, m = oracle.search_by_sim3(kf1, mp1, md1, a1, kf2, mp2, md2, a2, g, th, sf)
+    rn, rm = py_search_by_sim3(kf1, mp1, md1, a1, kf2, mp2, md2, a2, g, th, sf)
+    assert n == rn and np.array_equal(m, rm)
+    assert n > 100
+    ok = m >= 0
+    assert (m[ok] == perm[np.nonzero(ok)[0]]).mean() > 0.9  # mostly the true correspondences
+    assert np.all(m[a1 == 1] == -1)
