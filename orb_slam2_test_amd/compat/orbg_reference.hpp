@@ -33,6 +33,7 @@
 //   Fuse(pKF, Scw, vpPoints, th, vpReplacePoint) ORBmatcher.cc:1133-1258 (ORBmatcher.h:162)
 //   SearchByProjection(CurrentFrame, pKF, sAlreadyFound, th, ORBdist) ORBmatcher.cc:1670-1798
 //   SearchByProjection(pKF, Scw, vpPoints, vpMatched, th) ORBmatcher.cc:353-470
+//   SearchBySim3(pKF1, pKF2, vpMatches12, s12, R12, t12, th) ORBmatcher.cc:1262-1470
 //   ComputeDistinctiveDescriptors ... MapPoint.cc:342-420 (the BestIdx over vDescriptors)
 //   LocalBundleAdjustment window ..... Optimizer.cc:633-851: the vertex / edge set g2o builds
 //                                      (LbaWindow), and BlockSolver<6,3>::buildSystem's block
@@ -1064,6 +1065,75 @@ int Fuse(orbg_ctx *ctx, KeyFrameT *pKF, const Mat &Scw, const std::vector<MapPoi
         nFused++;
     }
     return nFused;
+}
+
+// ORBmatcher::SearchBySim3(pKF1, pKF2, vpMatches12, s12, R12, t12, th) (LoopClosing::
+// ComputeSim3): writes vpMatches12 where both projection directions agree.  FrameT gives the
+// Frame's float bounds.
+template <class FrameT, class KeyFrameT, class MapPointT, class Mat>
+int SearchBySim3(orbg_ctx *ctx, KeyFrameT *pKF1, KeyFrameT *pKF2,
+                 std::vector<MapPointT *> &vpMatches12, const float &s12, const Mat &R12,
+                 const Mat &t12, const float th)
+{
+    const std::vector<MapPointT *> vp1 = pKF1->GetMapPointMatches(), vp2 = pKF2->GetMapPointMatches();
+    const int n1 = (int)vp1.size(), n2 = (int)vp2.size();
+    auto side = [](const std::vector<MapPointT *> &vp, std::vector<orbg_map_point> &mp,
+                   std::vector<uint8_t> &md) {
+        const int n = (int)vp.size();
+        mp.assign(n > 0 ? n : 1, orbg_map_point{});
+        md.assign((size_t)(n > 0 ? n : 1) * 32, 0);
+        for (int i = 0; i < n; i++) {
+            MapPointT *p = vp[i];
+            if (!p || p->isBad()) continue;
+            const auto X = p->GetWorldPos();
+            orbg_map_point &m = mp[i];
+            m.x = X.template at<float>(0);
+            m.y = X.template at<float>(1);
+            m.z = X.template at<float>(2);
+            m.min_dist = p->GetMinDistance();
+            m.max_dist = p->GetMaxDistance();
+            m.flags = ORBG_MP_VALID;
+            mp_desc(p, &md[(size_t)i * 32]);
+        }
+    };
+    std::vector<orbg_map_point> mp1, mp2;
+    std::vector<uint8_t> md1, md2;
+    side(vp1, mp1, md1);
+    side(vp2, mp2, md2);
+    std::vector<uint8_t> am1(n1 > 0 ? n1 : 1, 0), am2(n2 > 0 ? n2 : 1, 0);
+    for (int i = 0; i < n1; i++) {  // vbAlreadyMatched1 / 2 (ORBmatcher.cc:1288-1297)
+        MapPointT *pMP = vpMatches12[i];
+        if (!pMP) continue;
+        am1[i] = 1;
+        const int idx2 = pMP->GetIndexInKeyFrame(pKF2);
+        if (idx2 >= 0 && idx2 < n2) am2[idx2] = 1;
+    }
+    orbg_sim3_pair g;
+    std::memset(&g, 0, sizeof(g));
+    pose12(pKF1->GetPose(), g.T1w);
+    pose12(pKF2->GetPose(), g.T2w);
+    for (int r = 0; r < 3; r++) {
+        for (int c = 0; c < 3; c++) g.R12[3 * r + c] = R12.template at<float>(r, c);
+        g.t12[r] = t12.template at<float>(r);
+    }
+    g.s12 = s12;
+    g.fx = pKF1->fx;
+    g.fy = pKF1->fy;
+    g.cx = pKF1->cx;
+    g.cy = pKF1->cy;
+    g.log_scale_factor = pKF1->mfLogScaleFactor;
+    g.nlevels = pKF1->mnScaleLevels;
+    g.bounds = orbg_bounds{FrameT::mnMinX, FrameT::mnMaxX, FrameT::mnMinY, FrameT::mnMaxY};
+    const KfArrays<KeyFrameT> a1 = kf_arrays(pKF1, false), a2 = kf_arrays(pKF2, false);
+    const orbg_keyframe k1 = a1.view(false), k2 = a2.view(false);
+    std::vector<int32_t> m12(n1 > 0 ? n1 : 1);
+    int nFound = 0;
+    check(orbg_search_by_sim3(ctx, &k1, mp1.data(), md1.data(), am1.data(), &k2, mp2.data(),
+                              md2.data(), am2.data(), &g, th, m12.data(), &nFound),
+          "orbg_search_by_sim3");
+    for (int i = 0; i < n1; i++)
+        if (m12[i] >= 0) vpMatches12[i] = vp2[m12[i]];
+    return nFound;
 }
 
 // MapPoint::ComputeDistinctiveDescriptors(): BestIdx over the observations' descriptor rows

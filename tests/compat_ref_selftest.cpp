@@ -61,6 +61,11 @@ struct MapPoint {  // include/MapPoint.h members the hot path reads
     float GetMaxDistance() const { return max_d; }
     void IncreaseVisible(int n = 1) { nvisible += n; }
     bool IsInKeyFrame(KeyFrame *k) const { return obs.count(k) != 0; }
+    int GetIndexInKeyFrame(KeyFrame *k) const
+    {
+        const auto it = obs.find(k);
+        return it == obs.end() ? -1 : (int)it->second;
+    }
     void AddObservation(KeyFrame *k, size_t idx) { obs[k] = idx; }
     void Replace(MapPoint *p);  // MapPoint.cc:196-240, below KeyFrame
 };
@@ -663,7 +668,7 @@ int main(int argc, char **argv)
     }
 
     // ---- LocalMapping: SearchForTriangulation(KA, KB) and Fuse(KB, KA's points) ----
-    int ntri = 0, nfused = 0, nfused3 = 0, nloop = 0, nreloc = 0;
+    int ntri = 0, nfused = 0, nfused3 = 0, nloop = 0, nreloc = 0, nsim3 = 0;
     {
         auto node_of = [](const cv::KeyPoint &k) {
             return (unsigned)((int)(k.pt.x / 128) + 16 * (int)(k.pt.y / 64));
@@ -868,6 +873,36 @@ int main(int argc, char **argv)
             if (i < 50) REQUIRE(FR.mvpMapPoints[i] != &pts[i]);
         }
         REQUIRE(nreloc >= nself && nself > (F1.N - 50) * 6 / 7 * 3 / 4);
+
+        // LoopClosing::ComputeSim3's SearchBySim3(KS1, KS2, vpMatches12, 1, I, 0, 7.5): two
+        // KeyFrames of frame 1 at KA's pose, each slot holding its own copy of the point:
+        // every point lands on its own keypoint both ways.  Every ninth slot is matched on
+        // entry (to its KS2 twin, observed there: vbAlreadyMatched2 through
+        // GetIndexInKeyFrame).
+        KeyFrame KS1 = KA, KS2 = KA;
+        std::vector<MapPoint> q1(F1.N), q2(F1.N);
+        for (int i = 0; i < F1.N; i++) {
+            q1[i] = pts[i];
+            q2[i] = pts[i];
+            q1[i].obs.clear();
+            q2[i].obs.clear();
+            q1[i].obs[&KS1] = (size_t)i;
+            q2[i].obs[&KS2] = (size_t)i;
+            q1[i].bad = q2[i].bad = false;
+            KS1.mvpMapPoints[i] = &q1[i];
+            KS2.mvpMapPoints[i] = &q2[i];
+        }
+        std::vector<MapPoint *> vm12(F1.N, nullptr);
+        for (int i = 0; i < F1.N; i += 9) vm12[i] = &q2[i];
+        cv::Mat R12 = cv::Mat::eye(3, 3, CV_32F), t12(3, 1, CV_32F);
+        for (int r = 0; r < 3; r++) t12.at<float>(r) = 0.f;
+        nsim3 = orbg_compat::ref::SearchBySim3<Frame>(ctx, &KS1, &KS2, vm12, 1.0f, R12, t12, 7.5f);
+        int ntwin = 0;
+        for (int i = 0; i < F1.N; i++) {
+            if (i % 9 == 0) REQUIRE(vm12[i] == &q2[i]);
+            else if (vm12[i] == &q2[i]) ntwin++;
+        }
+        REQUIRE(nsim3 >= ntwin && ntwin > F1.N * 8 / 9 * 3 / 4);
     }
 
     // ---- MapPoint::ComputeDistinctiveDescriptors' BestIdx ----
@@ -898,8 +933,8 @@ int main(int argc, char **argv)
     std::printf("compat_ref ok: %d + %d keypoints, SearchForInitialization %d, SearchByProjection %d, "
                 "PoseOptimization inliers %d, LBA edges %zu, chi2 %.6g, SearchByBoW %d, "
                 "isInFrustum %d, SearchForTriangulation %d, Fuse %d, Fuse(Sim3) %d, "
-                "SearchByProjection(Sim3) %d, SearchByProjection(reloc) %d\n",
+                "SearchByProjection(Sim3) %d, SearchByProjection(reloc) %d, SearchBySim3 %d\n",
                 F1.N, F2.N, nsfi, nproj, ninl, win.edges.size(), sys.active_robust_chi2, nbow,
-                nfrustum, ntri, nfused, nfused3, nloop, nreloc);
+                nfrustum, ntri, nfused, nfused3, nloop, nreloc, nsim3);
     return 0;
 }

@@ -31,6 +31,12 @@ cat $O/single_cpp.json
 echo "[final] SearchByBoW"
 timeout -k 10 200 python tools/bow_match_bench.py > $O/bow_match.json 2> $O/bow_match.err
 tail -c 300 $O/bow_match.json
+echo "[final] Frame / MapPoint geometry"
+timeout -k 10 300 python tools/frame_geom_bench.py > $O/frame_geom.jsonl 2> $O/frame_geom.err
+echo "[final] LocalMapping matchers"
+timeout -k 10 300 python tools/mapping_bench.py > $O/mapping.jsonl 2> $O/mapping.err
+echo "[final] Relocalization / LoopClosing matchers"
+timeout -k 10 300 python tools/loop_bench.py > $O/loop.jsonl 2> $O/loop.err
 echo "[final] C1"
 timeout -k 10 300 python tools/c1_bench.py 16 > $O/c1.json 2> $O/c1.err
 cat $O/c1.json
