@@ -52,6 +52,7 @@
  *   orbg_fuse_sim3 .................. ORBmatcher::Fuse(pKF, Scw, vpPoints, th, vpReplacePoint)'s search
  *   orbg_search_by_projection_reloc . ORBmatcher::SearchByProjection(CurrentFrame, pKF, sAlreadyFound, th, ORBdist)
  *   orbg_search_by_projection_sim3 .. ORBmatcher::SearchByProjection(pKF, Scw, vpPoints, vpMatched, th)
+ *   orbg_rgbd_stereo ................ Frame::ComputeStereoFromRGBD (+ GrabImageRGBD's depth scaling)
  *   orbg_search_by_sim3 ............. ORBmatcher::SearchBySim3(pKF1, pKF2, vpMatches12, s12, R12, t12, th)
  *                                     src/ORBmatcher.cc:968-1069 (LocalMapping::SearchInNeighbors,
  *                                     LocalMapping.cc:622-690)
@@ -408,6 +409,28 @@ int orbg_undistort_keypoints(orbg_ctx *ctx, const orbg_camera *cam, const orbg_k
 int orbg_undistort_batch_device(orbg_ctx *ctx, const orbg_camera *cam, const orbg_keypoint *d_kps,
                                 const int32_t *d_counts, int frame_cap, int nframes,
                                 orbg_keypoint *d_kps_un);
+/* Frame::ComputeStereoFromRGBD (src/Frame.cc:837-858; the RGB-D Frame constructor) after
+ * Tracking::GrabImageRGBD's depth conversion (Tracking.cc:233-234: imDepth.convertTo(CV_32F,
+ * mDepthMapFactor) when |mDepthMapFactor - 1| > 1e-5 or the image is not CV_32F).  depth:
+ * a w x h image, row pitch `pitch` bytes, ORBG_DEPTH_U16 (raw) or ORBG_DEPTH_F32; factor =
+ * mDepthMapFactor (1 / DepthMapFactor of the settings); a pixel's depth is raw * factor
+ * rounded once to float (convertTo's float alpha), or the float itself when it is F32 and
+ * factor is within 1e-5 of 1.  kps = mvKeys (their truncated (x, y) index the depth image;
+ * outside it: no depth), kps_un = mvKeysUn.  Per keypoint: d > 0 -> depth[i] = d,
+ * uright[i] = kps_un[i].x - mbf / d; else both -1. */
+#define ORBG_DEPTH_F32 0
+#define ORBG_DEPTH_U16 1
+int orbg_rgbd_stereo(orbg_ctx *ctx, const void *depth, int depth_type, float factor, int w, int h,
+                     size_t pitch, const orbg_keypoint *kps, const orbg_keypoint *kps_un, int n,
+                     float mbf, float *uright, float *depth_out);
+/* The same on the device for a batch: frame f's depth image at d_depth + f * image_stride
+ * bytes, its counts[f] keypoints at d_kps / d_kps_un + f * frame_cap, outputs at + f * frame_cap
+ * (entries past counts[f] untouched).  Context stream. */
+int orbg_rgbd_stereo_batch_device(orbg_ctx *ctx, const void *d_depth, int depth_type, float factor,
+                                  int w, int h, size_t pitch, size_t image_stride,
+                                  const orbg_keypoint *d_kps, const orbg_keypoint *d_kps_un,
+                                  const int32_t *d_counts, int frame_cap, int nframes, float mbf,
+                                  float *d_uright, float *d_depth_out);
 /* Frame::ComputeImageBounds (src/Frame.cc:575-611) for a w x h image: mnMinX .. mnMaxY (the
  * undistorted image corners when k1 != 0, else 0, w, 0, h).  Host only (four points, the
  * expression k_undistort evaluates). */

@@ -236,3 +236,29 @@ void orc_distinctive_descriptors_n(const uint8_t *pool, const int32_t *rows, con
     }
     free(buf);
 }
+
+/* Frame::ComputeStereoFromRGBD (Frame.cc:837-858) after Tracking::GrabImageRGBD's
+ * imDepth.convertTo(CV_32F, mDepthMapFactor) (Tracking.cc:233-234): the depth of a pixel is
+ * raw * factor in float (convertTo's float alpha, shift 0), or the float itself when the image
+ * is CV_32F and |factor - 1| <= 1e-5; imDepth.at<float>(v, u) truncates the keypoint's
+ * position.  u16: 1 = raw uint16 image, 0 = float. */
+void orc_rgbd_stereo(const void *depth, int u16, float factor, int w, int h, size_t pitch,
+                     const orc_keypoint *kps, const orc_keypoint *kps_un, int n, float mbf,
+                     float *uright, float *depth_out)
+{
+    const int scale = u16 || fabsf(factor - 1.0f) > 1e-5;
+    for (int i = 0; i < n; i++) {
+        uright[i] = -1.0f;
+        depth_out[i] = -1.0f;
+        const int u = (int)kps[i].x, v = (int)kps[i].y;
+        if (u < 0 || u >= w || v < 0 || v >= h)
+            continue;
+        const uint8_t *row = (const uint8_t *)depth + (size_t)v * pitch;
+        const float raw = u16 ? (float)((const uint16_t *)row)[u] : ((const float *)row)[u];
+        const float d = scale ? raw * factor : raw;
+        if (d > 0) {
+            depth_out[i] = d;
+            uright[i] = kps_un[i].x - mbf / d;
+        }
+    }
+}

@@ -321,6 +321,10 @@ int orc_search_by_projection_sim3(const orc_keypoint *kps, const uint8_t *desc, 
                                   const uint8_t *taken0, const orc_frustum_cam *cam,
                                   const float *scale_factors, const orc_map_point *mps,
                                   const uint8_t *mdesc, int nm, int th, int32_t *match);
+/* Frame::ComputeStereoFromRGBD (frame_oracle.c) */
+void orc_rgbd_stereo(const void *depth, int u16, float factor, int w, int h, size_t pitch,
+                     const orc_keypoint *kps, const orc_keypoint *kps_un, int n, float mbf,
+                     float *uright, float *depth_out);
 /* ORBmatcher::SearchBySim3(pKF1, pKF2, vpMatches12, s12, R12, t12, th) (ORBmatcher.cc:
  * 1262-1470): mp1[i] = pKF1->GetMapPointMatches()[i] (ORC_MP_VALID = pMP && !isBad()),
  * matched1[i] = vpMatches12[i] != NULL, matched2[idx2] = 1 at those points' index in pKF2 (NULL:

@@ -216,6 +216,9 @@ def lib():
         L.orc_search_by_sim3.argtypes = [vp, vp, C.c_int, vp, vp, vp, vp, vp, C.c_int, vp, vp,
                                          vp, vp, C.c_float, vp, vp]
         L.orc_search_by_sim3.restype = C.c_int
+        L.orc_rgbd_stereo.argtypes = [vp, C.c_int, C.c_float, C.c_int, C.c_int, C.c_size_t, vp,
+                                      vp, C.c_int, C.c_float, vp, vp]
+        L.orc_rgbd_stereo.restype = None
         L.orc_sim3_decompose.restype = None
         L.orc_search_by_bow_kf.restype = C.c_int
         L.orc_search_by_bow_kf.argtypes = [vp, vp, vp, C.c_int, vp, vp, vp, C.c_int, vp, vp, vp,
@@ -844,3 +847,18 @@ def search_by_sim3(kf1, mp1, md1, matched1, kf2, mp2, md2, matched2, g, th, scal
                                  _p(d2), len(k2), _p(mp2), _p(md2), _p(a2), _p(g), float(th),
                                  _p(sf), _p(m))
     return n, m[:len(k1)].copy()
+
+
+def rgbd_stereo(depth, factor, kps, kps_un, mbf):
+    """Frame::ComputeStereoFromRGBD after GrabImageRGBD's depth conversion (oracle/
+    frame_oracle.c): depth a (h, w) uint16 or float32 image -> (uright, depth) per keypoint."""
+    depth = np.ascontiguousarray(depth)
+    assert depth.dtype in (np.uint16, np.float32)
+    kps = np.ascontiguousarray(kps, KP_DTYPE)
+    kun = np.ascontiguousarray(kps_un, KP_DTYPE)
+    ur = np.zeros(max(len(kps), 1), np.float32)
+    dd = np.zeros(max(len(kps), 1), np.float32)
+    h, w = depth.shape
+    lib().orc_rgbd_stereo(_p(depth), 1 if depth.dtype == np.uint16 else 0, float(factor), w, h,
+                          depth.strides[0], _p(kps), _p(kun), len(kps), float(mbf), _p(ur), _p(dd))
+    return ur[:len(kps)].copy(), dd[:len(kps)].copy()

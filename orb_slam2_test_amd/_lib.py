@@ -40,6 +40,7 @@ EDGE_OUT_DTYPE = np.dtype([("err", "<f8", 3), ("chi2", "<f8"), ("rho1", "<f8"),
 # tracking matcher records (orbg_lastframe_point, orbg_map_projection)
 MP_VALID, MP_HAS_OBS = 1, 2
 TRACK_LASTFRAME, TRACK_LOCAL, TRACK_RELOC, TRACK_LOOP = 0, 1, 2, 3
+DEPTH_F32, DEPTH_U16 = 0, 1
 LF_DTYPE = np.dtype([("x", "<f4"), ("y", "<f4"), ("z", "<f4"), ("octave", "<i4"),
                      ("angle", "<f4"), ("flags", "<i4")])
 MP_DTYPE = np.dtype([("u", "<f4"), ("v", "<f4"), ("ur", "<f4"), ("level", "<i4"),
@@ -261,6 +262,10 @@ def lib():
                                                   i32, vp, P(i32)]),
         "orbg_search_by_projection_sim3": (i32, [vp, vp, vp, i32, vp, vp, vp, vp, i32, i32, vp,
                                                  P(i32)]),
+        "orbg_rgbd_stereo": (i32, [vp, vp, i32, f32, i32, i32, C.c_size_t, vp, vp, i32, f32, vp,
+                                   vp]),
+        "orbg_rgbd_stereo_batch_device": (i32, [vp, vp, i32, f32, i32, i32, C.c_size_t,
+                                                C.c_size_t, vp, vp, vp, i32, i32, f32, vp, vp]),
         "orbg_search_by_sim3": (i32, [vp, P(KeyFrame), vp, vp, vp, P(KeyFrame), vp, vp, vp, vp,
                                       f32, vp, P(i32)]),
         "orbg_search_by_sim3_batch_device": (i32, [vp, P(KeyFrames), i32, vp, vp, vp, vp, vp, vp,

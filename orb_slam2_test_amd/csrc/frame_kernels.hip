@@ -59,6 +59,53 @@ int launch_undistort(hipStream_t st, const orbg_camera &cam, const orbg_keypoint
 }
 
 // ---------------------------------------------------------------------------
+// ComputeStereoFromRGBD
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void k_rgbd(const uint8_t *__restrict__ depth, int u16,
+                                              int scale, float factor, int w, int h,
+                                              size_t pitch, size_t istride,
+                                              const orbg_keypoint *__restrict__ kps,
+                                              const orbg_keypoint *__restrict__ kps_un,
+                                              const int32_t *__restrict__ counts, int fc, float mbf,
+                                              float *__restrict__ uright, float *__restrict__ dout)
+{
+    const int f = blockIdx.y;
+    const int i = blockIdx.x * 256 + threadIdx.x;
+    if (i >= counts[f]) return;
+    const size_t o = (size_t)f * fc + i;
+    const orbg_keypoint kp = kps[o];
+    // imDepth.at<float>(v, u): the float position truncated to int
+    const int u = (int)kp.x, v = (int)kp.y;
+    float d = -1.0f;
+    if (u >= 0 && u < w && v >= 0 && v < h) {
+        const uint8_t *row = depth + (size_t)f * istride + (size_t)v * pitch;
+        const float raw = u16 ? (float)((const uint16_t *)row)[u] : ((const float *)row)[u];
+        d = scale ? raw * factor : raw;
+    }
+    float ur = -1.0f, dd = -1.0f;
+    if (d > 0) {  // Frame.cc:851-855
+        dd = d;
+        ur = kps_un[o].x - mbf / d;
+    }
+    uright[o] = ur;
+    dout[o] = dd;
+}
+
+int launch_rgbd(hipStream_t st, const void *depth, int u16, float factor, int w, int h,
+                size_t pitch, size_t istride, const orbg_keypoint *kps,
+                const orbg_keypoint *kps_un, const int32_t *counts, int fc, int nframes,
+                float mbf, float *uright, float *dout)
+{
+    if (nframes <= 0 || fc <= 0) return 0;
+    // Tracking.cc:233-234: converted (x * factor) unless already float with factor ~ 1
+    const int scale = u16 || (double)fabsf(factor - 1.0f) > 1e-5;
+    hipLaunchKernelGGL(k_rgbd, dim3((fc + 255) / 256, nframes), dim3(256), 0, st,
+                       (const uint8_t *)depth, u16, scale, factor, w, h, pitch, istride, kps,
+                       kps_un, counts, fc, mbf, uright, dout);
+    return hipGetLastError() == hipSuccess ? 0 : -5;
+}
+
+// ---------------------------------------------------------------------------
 // isInFrustum
 // ---------------------------------------------------------------------------
 // cv::gemm small-matrix pin (oracle orc_gemm3): (float)(alpha * op(R) x + c), double work

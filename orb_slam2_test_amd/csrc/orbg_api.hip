@@ -91,6 +91,10 @@ int launch_search_by_sim3(hipStream_t st, const orbg_keyframes &K, int cap, cons
                           const uint8_t *matched1, const uint8_t *matched2, int npairs, float th,
                           const float *scale, int nlevels, int32_t *vn, int32_t *match12,
                           int32_t *nfound);
+int launch_rgbd(hipStream_t st, const void *depth, int u16, float factor, int w, int h,
+                size_t pitch, size_t istride, const orbg_keypoint *kps,
+                const orbg_keypoint *kps_un, const int32_t *counts, int fc, int nframes,
+                float mbf, float *uright, float *dout);
 int launch_distinctive(hipStream_t st, const uint8_t *pool, const int32_t *rows,
                        const int32_t *off, int npoints, int32_t *best, uint8_t *desc_out);
 int launch_pose_opt(hipStream_t st, const orbg_pose_edge *edges, const int32_t *counts, int cap,
@@ -3977,6 +3981,80 @@ extern "C" int orbg_undistort_batch_device(orbg_ctx *c, const orbg_camera *cam,
     PROF_LAUNCH(c, "undistort",
                 rc = launch_undistort(st, *cam, d_kps, d_counts, frame_cap, nframes, d_kps_un));
     if (rc) return set_err(ORBG_EIO, "k_undistort launch failed");
+    return ORBG_OK;
+}
+
+extern "C" int orbg_rgbd_stereo_batch_device(orbg_ctx *c, const void *d_depth, int depth_type,
+                                             float factor, int w, int h, size_t pitch,
+                                             size_t image_stride, const orbg_keypoint *d_kps,
+                                             const orbg_keypoint *d_kps_un,
+                                             const int32_t *d_counts, int frame_cap, int nframes,
+                                             float mbf, float *d_uright, float *d_depth_out)
+{
+    if (!c) return set_err(ORBG_EINVAL, "NULL argument");
+    if (depth_type != ORBG_DEPTH_F32 && depth_type != ORBG_DEPTH_U16)
+        return set_err(ORBG_EINVAL, "depth_type %d", depth_type);
+    if (nframes < 0 || frame_cap < 0 || w < 0 || h < 0) return set_err(ORBG_EINVAL, "negative size");
+    if (nframes == 0 || frame_cap == 0) return ORBG_OK;
+    const size_t px = depth_type == ORBG_DEPTH_U16 ? 2 : 4;
+    if (pitch < (size_t)w * px) return set_err(ORBG_EINVAL, "pitch below the row width");
+    if (nframes > 1 && image_stride < pitch * (size_t)h)
+        return set_err(ORBG_EINVAL, "image_stride below one image");
+    if (!d_depth || !d_kps || !d_kps_un || !d_counts || !d_uright || !d_depth_out)
+        return set_err(ORBG_EINVAL, "NULL device array");
+    HIPCHK(hipSetDevice(c->device));
+    hipStream_t st = c->stream;
+    int rc = 0;
+    PROF_LAUNCH(c, "rgbd",
+                rc = launch_rgbd(st, d_depth, depth_type == ORBG_DEPTH_U16, factor, w, h, pitch,
+                                 image_stride, d_kps, d_kps_un, d_counts, frame_cap, nframes, mbf,
+                                 d_uright, d_depth_out));
+    if (rc) return set_err(ORBG_EIO, "k_rgbd launch failed");
+    return ORBG_OK;
+}
+
+extern "C" int orbg_rgbd_stereo(orbg_ctx *c, const void *depth, int depth_type, float factor,
+                                int w, int h, size_t pitch, const orbg_keypoint *kps,
+                                const orbg_keypoint *kps_un, int n, float mbf, float *uright,
+                                float *depth_out)
+{
+    if (!c) return set_err(ORBG_EINVAL, "NULL argument");
+    if (depth_type != ORBG_DEPTH_F32 && depth_type != ORBG_DEPTH_U16)
+        return set_err(ORBG_EINVAL, "depth_type %d", depth_type);
+    if (n < 0 || w < 0 || h < 0) return set_err(ORBG_EINVAL, "negative size");
+    if (n == 0) return ORBG_OK;
+    if (!depth || !kps || !kps_un || !uright || !depth_out) return set_err(ORBG_EINVAL, "NULL array");
+    const size_t px = depth_type == ORBG_DEPTH_U16 ? 2 : 4;
+    if (pitch < (size_t)w * px) return set_err(ORBG_EINVAL, "pitch below the row width");
+    HIPCHK(hipSetDevice(c->device));
+    // only the keypoints' pixels are read: upload the image rows once (w x h), packed
+    const size_t ib = al256((size_t)w * px * h), kb = al256((size_t)n * sizeof(orbg_keypoint));
+    const size_t ob = al256((size_t)n * 4);
+    const size_t o_img = 0, o_k = ib, o_ku = ib + kb, o_cnt = ib + 2 * kb, o_ur = o_cnt + 256,
+                 o_d = o_ur + ob, tot = o_d + ob;
+    uint8_t *hs;
+    int rc = stage(c, tot, &hs);
+    if (rc) return rc;
+    void *dv;
+    if ((rc = scratch(c, tot, &dv))) return rc;
+    uint8_t *db = (uint8_t *)dv;
+    HIPCHK(hipStreamSynchronize(c->stream));
+    for (int y = 0; y < h; y++)
+        memcpy(hs + o_img + (size_t)y * w * px, (const uint8_t *)depth + (size_t)y * pitch, (size_t)w * px);
+    memcpy(hs + o_k, kps, (size_t)n * sizeof(orbg_keypoint));
+    memcpy(hs + o_ku, kps_un, (size_t)n * sizeof(orbg_keypoint));
+    const int32_t cnt = n;
+    memcpy(hs + o_cnt, &cnt, 4);
+    HIPCHK(hipMemcpyAsync(db, hs, o_ur, hipMemcpyHostToDevice, c->stream));
+    rc = launch_rgbd(c->stream, db + o_img, depth_type == ORBG_DEPTH_U16, factor, w, h,
+                     (size_t)w * px, 0, (const orbg_keypoint *)(db + o_k),
+                     (const orbg_keypoint *)(db + o_ku), (const int32_t *)(db + o_cnt), n, 1, mbf,
+                     (float *)(db + o_ur), (float *)(db + o_d));
+    if (rc) return set_err(ORBG_EIO, "k_rgbd launch failed");
+    HIPCHK(hipMemcpyAsync(hs + o_ur, db + o_ur, tot - o_ur, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(hipStreamSynchronize(c->stream));
+    memcpy(uright, hs + o_ur, (size_t)n * 4);
+    memcpy(depth_out, hs + o_d, (size_t)n * 4);
     return ORBG_OK;
 }
 

@@ -48,6 +48,30 @@ def undistort_keypoints(cam, mvKeys, ctx=None):
     return out
 
 
+def compute_stereo_from_rgbd(depth, depth_map_factor, mvKeys, mvKeysUn, mbf, ctx=None):
+    """Frame::ComputeStereoFromRGBD (src/Frame.cc:837-858) with Tracking::GrabImageRGBD's
+    depth conversion (Tracking.cc:233-234): depth the (h, w) uint16 or float32 image as
+    GrabImageRGBD receives it, depth_map_factor = mDepthMapFactor (1 / the settings'
+    DepthMapFactor).  Returns (mvuRight, mvDepth), -1 where there is no depth."""
+    depth = np.ascontiguousarray(depth)
+    if depth.dtype not in (np.uint16, np.float32):
+        raise ValueError("depth must be uint16 or float32")
+    kps = np.ascontiguousarray(mvKeys, L.KP_DTYPE)
+    kun = np.ascontiguousarray(mvKeysUn, L.KP_DTYPE)
+    if len(kps) != len(kun):
+        raise ValueError("mvKeys and mvKeysUn differ in length")
+    ur = np.zeros(max(len(kps), 1), np.float32)
+    dd = np.zeros(max(len(kps), 1), np.float32)
+    h, w = depth.shape
+    c = ctx or _default_ctx()
+    L.check(L.lib().orbg_rgbd_stereo(c.handle, L.ptr(depth),
+                                     L.DEPTH_U16 if depth.dtype == np.uint16 else L.DEPTH_F32,
+                                     float(np.float32(depth_map_factor)), w, h, depth.strides[0],
+                                     L.ptr(kps), L.ptr(kun), len(kps), float(np.float32(mbf)),
+                                     L.ptr(ur), L.ptr(dd)), "orbg_rgbd_stereo")
+    return ur[:len(kps)].copy(), dd[:len(kps)].copy()
+
+
 def compute_image_bounds(cam, width, height):
     """Frame::ComputeImageBounds: (mnMinX, mnMaxX, mnMinY, mnMaxY)."""
     cam = np.ascontiguousarray(cam, L.CAMERA_DTYPE)

@@ -216,3 +216,54 @@ def test_distinctive_descriptors_batch_device(oracle):
     ok = best >= 0
     assert np.array_equal(desc[ok], pool[rows[off[:-1][ok] + best[ok]]])
     assert best[0] == -1 and best[1] == 0
+
+
+# ------------------------------------------------------------------ ComputeStereoFromRGBD
+@pytest.mark.parametrize("kind,factor", [("u16", T.TUM_DEPTH_FACTOR), ("u16", 1.0),
+                                         ("f32", 1.0), ("f32", 0.5)])
+def test_rgbd_stereo(oracle, kind, factor):
+    """Frame::ComputeStereoFromRGBD (k_rgbd) vs the oracle, bit for bit, incl. holes, NaN /
+    negative depths and keypoints on and just outside the image border"""
+    depth, kps, kun = T.rgbd_case(L, 5, kind)
+    ur, dd = FR.compute_stereo_from_rgbd(depth, factor, kps, kun, T.TUM_MBF)
+    rur, rdd = oracle.rgbd_stereo(depth, factor, kps, kun, T.TUM_MBF)
+    assert np.array_equal(ur.view(np.uint32), rur.view(np.uint32))
+    assert np.array_equal(dd.view(np.uint32), rdd.view(np.uint32))
+    assert (dd > 0).sum() > 400
+
+
+def test_rgbd_stereo_batch_device(oracle):
+    """the batched form over 3 TUM frames (raw uint16, a padded row pitch)"""
+    import ctypes as C
+    import torch
+    B, fc, w, h, pitch = 3, 1200, 640, 480, 1408
+    imgs = np.zeros((B, h, pitch // 2), np.uint16)
+    kps = np.zeros((B, fc), L.KP_DTYPE)
+    kun = np.zeros((B, fc), L.KP_DTYPE)
+    cnt = np.zeros(B, np.int32)
+    refs = []
+    for f in range(B):
+        depth, k, ku = T.rgbd_case(L, 20 + f, "u16", n=900 + 100 * f)
+        imgs[f, :, :w] = depth
+        n = len(k)
+        kps[f, :n], kun[f, :n], cnt[f] = k, ku, n
+        refs.append(oracle.rgbd_stereo(depth, T.TUM_DEPTH_FACTOR, k, ku, T.TUM_MBF))
+    t = {k: torch.from_numpy(np.ascontiguousarray(v).view(np.uint8).reshape(-1).copy()).cuda()
+         for k, v in dict(imgs=imgs, kps=kps, kun=kun, cnt=cnt).items()}
+    ur = torch.full((B * fc,), -7.0, dtype=torch.float32, device="cuda")
+    dd = torch.full((B * fc,), -7.0, dtype=torch.float32, device="cuda")
+    ctx = FR._default_ctx()
+    torch.cuda.synchronize()
+    L.check(L.lib().orbg_rgbd_stereo_batch_device(
+        ctx.handle, t["imgs"].data_ptr(), L.DEPTH_U16, float(T.TUM_DEPTH_FACTOR), w, h, pitch,
+        pitch * h, t["kps"].data_ptr(), t["kun"].data_ptr(), t["cnt"].data_ptr(), fc, B,
+        T.TUM_MBF, ur.data_ptr(), dd.data_ptr()), "rgbd batch")
+    ctx.sync()
+    gur = ur.cpu().numpy().reshape(B, fc)
+    gdd = dd.cpu().numpy().reshape(B, fc)
+    for f in range(B):
+        n = cnt[f]
+        assert np.array_equal(gur[f, :n].view(np.uint32), refs[f][0].view(np.uint32))
+        assert np.array_equal(gdd[f, :n].view(np.uint32), refs[f][1].view(np.uint32))
+        assert np.all(gur[f, n:] == -7.0)
+

@@ -280,3 +280,62 @@ def test_distinctive_pool_batch(oracle):
     best = oracle.distinctive_descriptors(pool, rows, off)
     for p in range(200):
         assert best[p] == np_distinctive(pool[rows[off[p]:off[p + 1]]])
+
+
+# ------------------------------------------------------------------ ComputeStereoFromRGBD
+TUM_MBF = 40.0  # TUM1.yaml Camera.bf
+TUM_DEPTH_FACTOR = np.float32(1.0) / np.float32(5000.0)  # 1 / DepthMapFactor
+
+
+def rgbd_case(mod, seed, kind="u16", n=1000, w=640, h=480):
+    """a depth image (TUM-style raw uint16 with holes, or float metres with holes / NaN) and
+    keypoints over the whole image incl. its last row / column and just outside it"""
+    rng = np.random.default_rng(seed)
+    if kind == "u16":
+        depth = rng.integers(500, 40000, (h, w)).astype(np.uint16)
+        depth[rng.random((h, w)) < 0.15] = 0
+    else:
+        depth = rng.uniform(0.3, 8.0, (h, w)).astype(np.float32)
+        depth[rng.random((h, w)) < 0.1] = 0
+        depth[rng.random((h, w)) < 0.02] = np.nan
+        depth[rng.random((h, w)) < 0.02] = -1.0
+    kps = np.zeros(n, mod.KP_DTYPE)
+    kps["x"] = rng.uniform(0, w, n)
+    kps["y"] = rng.uniform(0, h, n)
+    kps["x"][:4] = [w - 0.25, 0.0, w + 0.5, -1.5]
+    kps["y"][:4] = [h - 0.75, 0.0, 10.0, 10.0]
+    kps["octave"] = rng.integers(0, 8, n)
+    kun = kps.copy()
+    kun["x"] = kps["x"] + rng.normal(0, 2, n)
+    kun["y"] = kps["y"] + rng.normal(0, 2, n)
+    return depth, kps, kun
+
+
+def np_rgbd(depth, factor, kps, kun, mbf):
+    h, w = depth.shape
+    u = np.trunc(kps["x"]).astype(np.int64)
+    v = np.trunc(kps["y"]).astype(np.int64)
+    ok = (u >= 0) & (u < w) & (v >= 0) & (v < h)
+    raw = np.zeros(len(kps), np.float32)
+    raw[ok] = depth[v[ok], u[ok]].astype(np.float32)
+    scale = depth.dtype == np.uint16 or abs(float(np.float32(factor) - np.float32(1.0))) > 1e-5
+    with np.errstate(invalid="ignore"):
+        d = (raw * np.float32(factor)).astype(np.float32) if scale else raw
+        good = ok & (d > 0)
+    ur = np.full(len(kps), -1, np.float32)
+    dd = np.full(len(kps), -1, np.float32)
+    dd[good] = d[good]
+    ur[good] = kun["x"][good] - np.float32(mbf) / d[good]
+    return ur, dd
+
+
+@pytest.mark.parametrize("kind,factor", [("u16", TUM_DEPTH_FACTOR), ("u16", 1.0),
+                                         ("f32", 1.0), ("f32", 0.5)])
+def test_rgbd_stereo_equals_numpy(oracle, kind, factor):
+    depth, kps, kun = rgbd_case(oracle, 3, kind)
+    ur, dd = oracle.rgbd_stereo(depth, factor, kps, kun, TUM_MBF)
+    rur, rdd = np_rgbd(depth, factor, kps, kun, TUM_MBF)
+    assert np.array_equal(ur.view(np.uint32), rur.view(np.uint32))
+    assert np.array_equal(dd.view(np.uint32), rdd.view(np.uint32))
+    assert (dd > 0).sum() > len(kps) // 2 and (dd == -1).sum() > 20
+    assert dd[2] == -1 and dd[3] == -1  # outside the image
