@@ -6,6 +6,9 @@ CPU oracle (oracle/frame_oracle.c) on one host core over a bounded sample:
   undistort    Frame::UndistortKeyPoints (Frame.cc:542-572) with TUM1's distortion over
                B = 1024 frames x 2000 keypoints resident in HBM: keypoints/s.
                Algorithmic bytes: the 28-byte keypoint in and out (56 B per keypoint).
+  rgbd         Frame::ComputeStereoFromRGBD (Frame.cc:837-858) over B = 256 TUM frames x 1000
+               keypoints with raw uint16 depth images in HBM: keypoints/s (66 B per keypoint:
+               two keypoint records, the depth pixel, mvuRight / mvDepth out).
   frustum      Frame::isInFrustum (Frame.cc:342-409) for Tracking::SearchLocalPoints over
                B = 256 frames x 8192 local map points: map points/s.  36-byte MapPoint
                record in, 24-byte projection out (60 B per point).
@@ -119,6 +122,41 @@ def main():
             ocam = O.camera(*TUM1)
             sample = kps[0, :n].view(O.KP_DTYPE)
             v, calls, dt = cpu_rate(lambda: O.undistort_keypoints(ocam, sample), n)
+            r["cpu_baseline"] = {"value": round(v, 1), "unit": "keypoints/s", "cores": 1,
+                                 "kind": "port", "sample": "%d x %d keypoints, oracle -O3, one "
+                                 "thread, %.2f s" % (calls, n, dt)}
+        print(json.dumps(r), flush=True)
+
+    if args.only in ("", "rgbd"):
+        B, cap, n, w, hh = 256, 1024, 1000, 640, 480
+        imgs = np.zeros((B, hh, w), np.uint16)
+        kps = np.zeros((B, cap), L.KP_DTYPE)
+        kun = np.zeros((B, cap), L.KP_DTYPE)
+        cases = [T.rgbd_case(L, 70 + q, "u16", n=n) for q in range(16)]
+        for b in range(B):
+            d, k, ku = cases[b % 16]
+            imgs[b], kps[b, :n], kun[b, :n] = d, k, ku
+        counts = np.full(B, n, np.int32)
+        t = {k: torch.from_numpy(np.ascontiguousarray(v).view(np.uint8).reshape(-1).copy()).cuda()
+             for k, v in dict(imgs=imgs, kps=kps, kun=kun, cnt=counts).items()}
+        ur = torch.empty(B * cap, dtype=torch.float32, device="cuda")
+        dd = torch.empty(B * cap, dtype=torch.float32, device="cuda")
+        fac = float(T.TUM_DEPTH_FACTOR)
+
+        def run():
+            L.check(L.lib().orbg_rgbd_stereo_batch_device(
+                h, t["imgs"].data_ptr(), L.DEPTH_U16, fac, w, hh, w * 2, w * 2 * hh,
+                t["kps"].data_ptr(), t["kun"].data_ptr(), t["cnt"].data_ptr(), cap, B,
+                T.TUM_MBF, ur.data_ptr(), dd.data_ptr()), "rgbd")
+        ms, avg = timed(ctx, "rgbd", run, args.steps, args.warmup)
+        # per keypoint: mvKeys / mvKeysUn records (56 B), the depth pixel (2 B), two floats out
+        r = line("Frame::ComputeStereoFromRGBD keypoints/s (TUM1 RGB-D, raw uint16 depth)",
+                 "keypoints/s", B * n, ms, avg, B * n * 66,
+                 "B=%d frames 640x480 x %d keypoints, DepthMapFactor 5000" % (B, n),
+                 {"dtype": "f32"})
+        if O is not None:
+            d0, k0, ku0 = cases[0]
+            v, calls, dt = cpu_rate(lambda: O.rgbd_stereo(d0, fac, k0, ku0, T.TUM_MBF), n)
             r["cpu_baseline"] = {"value": round(v, 1), "unit": "keypoints/s", "cores": 1,
                                  "kind": "port", "sample": "%d x %d keypoints, oracle -O3, one "
                                  "thread, %.2f s" % (calls, n, dt)}
