@@ -34,6 +34,7 @@
 //   SearchByProjection(CurrentFrame, pKF, sAlreadyFound, th, ORBdist) ORBmatcher.cc:1670-1798
 //   SearchByProjection(pKF, Scw, vpPoints, vpMatched, th) ORBmatcher.cc:353-470
 //   SearchBySim3(pKF1, pKF2, vpMatches12, s12, R12, t12, th) ORBmatcher.cc:1262-1470
+//   Frame::ComputeStereoFromRGBD ...... Frame.cc:837-858 (+ Tracking.cc:233-234)
 //   ComputeDistinctiveDescriptors ... MapPoint.cc:342-420 (the BestIdx over vDescriptors)
 //   LocalBundleAdjustment window ..... Optimizer.cc:633-851: the vertex / edge set g2o builds
 //                                      (LbaWindow), and BlockSolver<6,3>::buildSystem's block
@@ -1134,6 +1135,24 @@ int SearchBySim3(orbg_ctx *ctx, KeyFrameT *pKF1, KeyFrameT *pKF2,
     for (int i = 0; i < n1; i++)
         if (m12[i] >= 0) vpMatches12[i] = vp2[m12[i]];
     return nFound;
+}
+
+// Frame::ComputeStereoFromRGBD(imDepth) (Frame.cc:837-858) on the depth image as
+// Tracking::GrabImageRGBD receives it (CV_16U raw or CV_32F): the convertTo(CV_32F,
+// mDepthMapFactor) of Tracking.cc:233-234 happens in liborbg, at the keypoints' pixels.
+template <class FrameT, class Mat>
+void ComputeStereoFromRGBD(orbg_ctx *ctx, FrameT &F, const Mat &imDepthRaw, float mDepthMapFactor)
+{
+    const int n = (int)F.mvKeys.size();
+    F.mvuRight.assign(n, -1.f);
+    F.mvDepth.assign(n, -1.f);
+    if (n == 0) return;
+    const std::vector<orbg_keypoint> k = keys_of(F.mvKeys), ku = keys_of(F.mvKeysUn);
+    check(orbg_rgbd_stereo(ctx, imDepthRaw.data,
+                           imDepthRaw.type() == CV_32F ? ORBG_DEPTH_F32 : ORBG_DEPTH_U16,
+                           mDepthMapFactor, imDepthRaw.cols, imDepthRaw.rows, imDepthRaw.step[0],
+                           k.data(), ku.data(), n, F.mbf, F.mvuRight.data(), F.mvDepth.data()),
+          "orbg_rgbd_stereo");
 }
 
 // MapPoint::ComputeDistinctiveDescriptors(): BestIdx over the observations' descriptor rows

@@ -74,7 +74,7 @@ struct Frame {  // include/Frame.h
     static float fx, fy, cx, cy, mnMinX, mnMaxX, mnMinY, mnMaxY;
     int N = 0;
     std::vector<cv::KeyPoint> mvKeys, mvKeysUn;
-    std::vector<float> mvuRight, mvInvLevelSigma2;
+    std::vector<float> mvuRight, mvDepth, mvInvLevelSigma2;
     cv::Mat mDescriptors, mTcw;
     std::vector<MapPoint *> mvpMapPoints;
     std::vector<bool> mvbOutlier;
@@ -905,6 +905,30 @@ int main(int argc, char **argv)
         REQUIRE(nsim3 >= ntwin && ntwin > F1.N * 8 / 9 * 3 / 4);
     }
 
+    // ---- Frame::ComputeStereoFromRGBD on a raw uint16 depth image (TUM's DepthMapFactor
+    // 5000): 10 m everywhere except a hole column block ----
+    int nrgbd = 0;
+    {
+        Frame FD = F1;
+        FD.mbf = 40.f;
+        cv::Mat dep(h, w, CV_16U);
+        for (int y = 0; y < h; y++)
+            for (int x = 0; x < w; x++) dep.at<uint16_t>(y, x) = x < 64 ? 0 : 50000;
+        const float factor = 1.0f / 5000.0f;
+        orbg_compat::ref::ComputeStereoFromRGBD(ctx, FD, dep, factor);
+        REQUIRE((int)FD.mvuRight.size() == FD.N && (int)FD.mvDepth.size() == FD.N);
+        for (int i = 0; i < FD.N; i++) {
+            if ((int)FD.mvKeys[i].pt.x < 64) {
+                REQUIRE(FD.mvDepth[i] == -1.f && FD.mvuRight[i] == -1.f);
+                continue;
+            }
+            const float d = 50000.f * factor;
+            REQUIRE(FD.mvDepth[i] == d && FD.mvuRight[i] == FD.mvKeysUn[i].pt.x - FD.mbf / d);
+            nrgbd++;
+        }
+        REQUIRE(nrgbd > FD.N / 2);
+    }
+
     // ---- MapPoint::ComputeDistinctiveDescriptors' BestIdx ----
     {
         std::vector<cv::Mat> vd;
@@ -933,8 +957,8 @@ int main(int argc, char **argv)
     std::printf("compat_ref ok: %d + %d keypoints, SearchForInitialization %d, SearchByProjection %d, "
                 "PoseOptimization inliers %d, LBA edges %zu, chi2 %.6g, SearchByBoW %d, "
                 "isInFrustum %d, SearchForTriangulation %d, Fuse %d, Fuse(Sim3) %d, "
-                "SearchByProjection(Sim3) %d, SearchByProjection(reloc) %d, SearchBySim3 %d\n",
+                "SearchByProjection(Sim3) %d, SearchByProjection(reloc) %d, SearchBySim3 %d, RGB-D %d\n",
                 F1.N, F2.N, nsfi, nproj, ninl, win.edges.size(), sys.active_robust_chi2, nbow,
-                nfrustum, ntri, nfused, nfused3, nloop, nreloc, nsim3);
+                nfrustum, ntri, nfused, nfused3, nloop, nreloc, nsim3, nrgbd);
     return 0;
 }

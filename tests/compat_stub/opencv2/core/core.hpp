@@ -1,5 +1,5 @@
 // TEST-ONLY stand-in for the OpenCV core subset that orb_slam2_test_amd/compat/*.hpp use
-// (cv::Mat rows/cols/step/data/type/at/ptr/clone/eye/create/release, _InputArray /
+// (cv::Mat rows/cols/step/data/type/at/ptr/clone/eye/create/release, 8U / 16U / 32F, _InputArray /
 // _OutputArray, KeyPoint, Point2f, CV_Assert), so tests/test_compat_ref.py can compile and
 // run the OpenCV-facing drop-in layer where OpenCV is absent.  Not OpenCV: semantics are
 // those of the subset only (dense, continuous, 1-channel 8U / 32F matrices).
@@ -15,6 +15,7 @@
 
 #define CV_8U 0
 #define CV_8UC1 0
+#define CV_16U 2
 #define CV_32F 5
 #define CV_Assert(expr) do { if (!(expr)) throw std::runtime_error("CV_Assert: " #expr); } while (0)
 
@@ -93,7 +94,7 @@ public:
 private:
     int type_ = 0;
     std::shared_ptr<std::vector<uint8_t>> buf_;
-    size_t esize() const { return type_ == CV_32F ? 4 : 1; }
+    size_t esize() const { return type_ == CV_32F ? 4 : type_ == CV_16U ? 2 : 1; }
 };
 
 class _InputArray {
