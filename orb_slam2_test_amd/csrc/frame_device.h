@@ -55,11 +55,21 @@ __host__ __device__ inline void sim3_decompose(const float *S, float *T)
     for (int k = 0; k < 12; k++) T[k] = S[k] * a + 0.0f;
 }
 
-// MapPoint::PredictScale (MapPoint.cc:575-607)
+// MapPoint::PredictScale (MapPoint.cc:575-607): ceil(log(ratio) / mfLogScaleFactor) in double.
+// Fast path: the float quotient (logf within ~1 ulp, so within 1e-6 of the exact quotient for
+// any |q| < 64) decides the ceiling whenever it is more than 1e-3 away from an integer -- the
+// double quotient is then inside the same open interval; near an integer, or non-finite, the
+// reference's double expression is evaluated.  Same result, a fraction of the FP64 issue.
 __host__ __device__ inline int predict_scale(float max_dist, float dist, float log_sf, int nlevels)
 {
     const float ratio = max_dist / dist;
-    int n = (int)ceil(log((double)ratio) / (double)log_sf);
+    const float qf = logf(ratio) / log_sf;
+    const float fl = floorf(qf);
+    int n;
+    if (fabsf(qf) < 64.0f && qf - fl > 1e-3f && qf - fl < 0.999f)
+        n = (int)fl + 1;
+    else
+        n = (int)ceil(log((double)ratio) / (double)log_sf);
     if (n < 0)
         n = 0;
     else if (n >= nlevels)

@@ -133,6 +133,18 @@ __global__ __launch_bounds__(256) void k_frustum(const orbg_frustum_camera *__re
     const int f = blockIdx.y;
     const int i = blockIdx.x * 256 + threadIdx.x;
     const int n = counts[f];
+    // mOw = -mRcw.t()*mtcw (Frame::UpdatePoseMatrices, Frame.cc:334; gemm, alpha -1): once
+    // per workgroup (it is the frame's), not per point
+    __shared__ float sOw[3];
+    if (threadIdx.x < 3) {
+        const orbg_frustum_camera &C = cams[f];
+        const int r = threadIdx.x;
+        double t = 0.0;
+#pragma unroll
+        for (int k = 0; k < 3; k++) t += (double)C.Tcw[4 * k + r] * (double)C.Tcw[4 * k + 3];
+        sOw[r] = (float)(t * -1.0);
+    }
+    __syncthreads();
     bool vis = false;
     if (i < n) {
         const orbg_frustum_camera &C = cams[f];
@@ -154,15 +166,7 @@ __global__ __launch_bounds__(256) void k_frustum(const orbg_frustum_camera *__re
                 if (v < C.bounds.min_y || v > C.bounds.max_y) break;
                 const float maxDistance = 1.2f * mp.max_dist;
                 const float minDistance = 0.8f * mp.min_dist;
-                // mOw = -mRcw.t()*mtcw (Frame::UpdatePoseMatrices, Frame.cc:334): alpha -1
-                float Ow[3];
-#pragma unroll
-                for (int r = 0; r < 3; r++) {
-                    double t = 0.0;
-#pragma unroll
-                    for (int k = 0; k < 3; k++) t += (double)C.Tcw[4 * k + r] * (double)tcw[k];
-                    Ow[r] = (float)(t * -1.0);
-                }
+                const float Ow[3] = {sOw[0], sOw[1], sOw[2]};
                 const float PO0 = P[0] - Ow[0], PO1 = P[1] - Ow[1], PO2 = P[2] - Ow[2];
                 double s = 0.0;
                 s += (double)PO0 * (double)PO0;
@@ -176,12 +180,7 @@ __global__ __launch_bounds__(256) void k_frustum(const orbg_frustum_camera *__re
                 dot += (double)PO2 * (double)mp.nz;
                 const float viewCos = (float)(dot / (double)dist);
                 if (viewCos < cos_limit) break;
-                const float ratio = mp.max_dist / dist;
-                int ns = (int)ceil(log((double)ratio) / (double)C.log_scale_factor);
-                if (ns < 0)
-                    ns = 0;
-                else if (ns >= C.nlevels)
-                    ns = C.nlevels - 1;
+                const int ns = predict_scale(mp.max_dist, dist, C.log_scale_factor, C.nlevels);
                 o.flags |= ORBG_MP_VALID;
                 o.u = u;
                 o.ur = u - C.bf * invz;
