@@ -339,3 +339,21 @@ def test_rgbd_stereo_equals_numpy(oracle, kind, factor):
     assert np.array_equal(dd.view(np.uint32), rdd.view(np.uint32))
     assert (dd > 0).sum() > len(kps) // 2 and (dd == -1).sum() > 20
     assert dd[2] == -1 and dd[3] == -1  # outside the image
+
+
+def test_predict_scale_fast_path_logic():
+    """csrc/frame_device.h predict_scale: the float quotient decides ceil(log(r) / L) unless it
+    lies within 1e-3 of an integer (then the double expression runs).  Checked here with
+    numpy's float32 log over a million ratios, dense around every level boundary 1.2^k."""
+    rng = np.random.default_rng(7)
+    L32 = np.float32(np.log(np.float64(np.float32(1.2))))
+    k = rng.integers(-3, 12, 500000)
+    near = (np.float64(1.2) ** k * (1 + rng.normal(0, 1e-6, k.size))).astype(np.float32)
+    wide = np.exp(rng.uniform(-3, 4, 500000)).astype(np.float32)
+    r = np.concatenate([near, wide, (np.float64(1.2) ** np.arange(-3, 12)).astype(np.float32)])
+    qf = np.log(r) / L32
+    fl = np.floor(qf)
+    fast = (np.abs(qf) < 64) & (qf - fl > np.float32(1e-3)) & (qf - fl < np.float32(0.999))
+    exact = np.ceil(np.log(r.astype(np.float64)) / np.float64(L32))
+    assert np.array_equal((fl + 1)[fast], exact[fast])
+    assert fast[near.size:near.size + wide.size].mean() > 0.99 and (~fast).sum() > 1000
