@@ -123,3 +123,56 @@ def test_stale_match_outputs_rejected():
     with pytest.raises(_lib.OrbgError):
         ext.match_outputs()
     ext.ctx.sync()
+
+
+def test_widening_entry_points_reject_bad_arguments():
+    """the relocalization / loop-closing / RGB-D entry points return ORBG_EINVAL (or
+    ORBG_ENOTSUP past the LDS grid's 8192 keypoints) instead of launching on bad input"""
+    import ctypes as C
+    from orb_slam2_test_amd.orbmatcher import _ctx
+    L = _lib
+    h = _ctx().handle
+    lib = L.lib()
+    # batch projection search: unknown mode, RELOC / LOOP without frustum cameras
+    d = torch.zeros(4096, dtype=torch.uint8, device="cuda")
+    tb = L.TrackBatch()
+    tb.kps = tb.desc = tb.counts = tb.bounds = tb.queries = tb.qdesc = tb.qcounts = d.data_ptr()
+    tb.match = tb.nmatches = d.data_ptr()
+    tb.frame_cap, tb.query_cap = 16, 16
+    assert lib.orbg_search_by_projection_batch_device(h, 4, C.byref(tb), 1) == L.ORBG_EINVAL
+    for mode in (L.TRACK_RELOC, L.TRACK_LOOP):
+        tb.fcams = None
+        assert lib.orbg_search_by_projection_batch_device(h, mode, C.byref(tb), 1) == L.ORBG_EINVAL
+    # host searches: NULL camera
+    kps = np.zeros(8, L.KP_DTYPE)
+    desc = np.zeros((8, 32), np.uint8)
+    m = np.zeros(8, np.int32)
+    n = C.c_int()
+    assert lib.orbg_search_by_projection_reloc(h, L.ptr(kps), L.ptr(desc), 8, None, None, None,
+                                               None, 0, 10.0, 100, 1, L.ptr(m),
+                                               C.byref(n)) == L.ORBG_EINVAL
+    assert lib.orbg_search_by_projection_sim3(h, L.ptr(kps), L.ptr(desc), 8, None, None, None,
+                                              None, 0, 10, L.ptr(m), C.byref(n)) == L.ORBG_EINVAL
+    # RGB-D: unknown depth type, a row pitch below the row
+    dep = np.zeros((4, 4), np.uint16)
+    ur = np.zeros(8, np.float32)
+    dd = np.zeros(8, np.float32)
+    assert lib.orbg_rgbd_stereo(h, L.ptr(dep), 7, 1.0, 4, 4, 8, L.ptr(kps), L.ptr(kps), 8, 40.0,
+                                L.ptr(ur), L.ptr(dd)) == L.ORBG_EINVAL
+    assert lib.orbg_rgbd_stereo(h, L.ptr(dep), L.DEPTH_U16, 1.0, 4, 4, 6, L.ptr(kps), L.ptr(kps),
+                                8, 40.0, L.ptr(ur), L.ptr(dd)) == L.ORBG_EINVAL
+    # SearchBySim3: NULL pair geometry; more keypoints than the LDS grid holds
+    kf = L.KeyFrame(L.ptr(kps), L.ptr(desc), None, None, 8, None, None, None, 0)
+    mp = np.zeros(8, L.MAPPOINT_DTYPE)
+    assert lib.orbg_search_by_sim3(h, C.byref(kf), L.ptr(mp), L.ptr(desc), None, C.byref(kf),
+                                   L.ptr(mp), L.ptr(desc), None, None, 7.5, L.ptr(m),
+                                   C.byref(n)) == L.ORBG_EINVAL
+    big = np.zeros(9000, L.KP_DTYPE)
+    bd = np.zeros((9000, 32), np.uint8)
+    bmp = np.zeros(9000, L.MAPPOINT_DTYPE)
+    bm = np.zeros(9000, np.int32)
+    kb = L.KeyFrame(L.ptr(big), L.ptr(bd), None, None, 9000, None, None, None, 0)
+    g = np.zeros(1, L.SIM3_PAIR_DTYPE)
+    assert lib.orbg_search_by_sim3(h, C.byref(kb), L.ptr(bmp), L.ptr(bd), None, C.byref(kb),
+                                   L.ptr(bmp), L.ptr(bd), None, L.ptr(g), 7.5, L.ptr(bm),
+                                   C.byref(n)) == L.ORBG_ENOTSUP
