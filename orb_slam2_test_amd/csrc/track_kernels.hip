@@ -52,7 +52,9 @@ void prof_end(void *prof, hipStream_t s, const char *n, hipEvent_t a);
 #define TH_LOW 50
 #define HISTO_LENGTH 30
 #define TRK_ROT(m) ((m) == TRK_LASTFRAME || (m) == TRK_RELOC)  // rotation histogram
+#ifndef TRK_QPW
 #define TRK_QPW 32  // queries per wave in k_track_cands (8 x 4 in 16-lane groups)
+#endif
 #define TRK_NB (ORBG_MAX_LEVELS * ORBG_GRID_COLS)  // (octave, column) buckets
 
 // cv::gemm small-matrix pin (see oracle/track_oracle.c orc_gemm3): double work type, one
