@@ -208,36 +208,60 @@ __global__ __launch_bounds__(256) void k_tri_match(orbg_keyframes K, int cap,
             TriCand c0, c1;
             tri_load(c0, K, k2, cap, f2, lane, nF, ex, ey, T, only_stereo);
             tri_load(c1, K, k2, cap, f2, lane + 64, nF, ex, ey, T, only_stereo);
-            for (int ia = a0; ia < a1; ia++) {
-                const int idx1 = __builtin_amdgcn_readfirstlane(fe1[ia]);
-                const size_t g1 = (size_t)k1 * cap + idx1;
-                if (K.has_mp && K.has_mp[g1]) continue;  // pMP1: wave-uniform skip
-                const bool st1 = K.uright ? K.uright[g1] >= 0 : false;
-                if (only_stereo && !st1) continue;
-                uint32_t q[8];
-#pragma unroll
-                for (int w = 0; w < 8; w++)
-                    q[w] = __builtin_amdgcn_readfirstlane(((const uint32_t *)(desc1 + (size_t)idx1 * 32))[w]);
-                const orbg_keypoint k = kp1[idx1];
-                // epipolar line l = x1' F12 (ORBmatcher.cc:168-170), wave-uniform
-                const float a = k.x * F[0] + k.y * F[3] + F[6];
-                const float b = k.x * F[1] + k.y * F[4] + F[7];
-                const float cc = k.x * F[2] + k.y * F[5] + F[8];
-                const float den = a * a + b * b;
-                unsigned key = max(tri_key(c0, q, st1, a, b, cc, den, lane),
-                                   tri_key(c1, q, st1, a, b, cc, den, lane + 64));
-                for (int ch = 2; ch * 64 < nF; ch++) {  // nodes past 128 candidates: re-read
-                    TriCand cx;
-                    tri_load(cx, K, k2, cap, f2, ch * 64 + lane, nF, ex, ey, T, only_stereo);
-                    key = max(key, tri_key(cx, q, st1, a, b, cc, den, ch * 64 + lane));
+            // the node's KF1 features, 64 at a time: lane l loads feature ib + l (index,
+            // MapPoint / stereo flags, descriptor, position, angle) so the serial walk below
+            // broadcasts them from registers instead of waiting on dependent global loads
+            for (int ib = a0; ib < a1; ib += 64) {
+                const int cn = min(64, a1 - ib);
+                int my_idx = 0, my_ok = 0, my_st = 0;
+                uint32_t my_q[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+                float my_x = 0.f, my_y = 0.f, my_ang = 0.f;
+                if (lane < cn) {
+                    my_idx = fe1[ib + lane];
+                    const size_t g1 = (size_t)k1 * cap + my_idx;
+                    my_st = K.uright ? K.uright[g1] >= 0 : 0;
+                    // pMP1 (ORBmatcher.cc:837-840) and the stereo-only filter
+                    my_ok = !(K.has_mp && K.has_mp[g1]) && !(only_stereo && !my_st);
+                    const uint4 *dp = (const uint4 *)(desc1 + (size_t)my_idx * 32);
+                    const uint4 qa = dp[0], qb = dp[1];
+                    my_q[0] = qa.x; my_q[1] = qa.y; my_q[2] = qa.z; my_q[3] = qa.w;
+                    my_q[4] = qb.x; my_q[5] = qb.y; my_q[6] = qb.z; my_q[7] = qb.w;
+                    const orbg_keypoint k = kp1[my_idx];
+                    my_x = k.x;
+                    my_y = k.y;
+                    my_ang = k.angle;
                 }
-                const unsigned best = wave_max_u32(key);
-                if (best) {
-                    wave_nm++;
-                    if (lane == 0) {
-                        const int idx2 = K.fv_feats[(size_t)k2 * cap + f2 + (int)(best & 0xFFFFu)];
-                        out[idx1] = idx2;
-                        if (check_ori) atomicAdd(&hist[tm_rot_bin(k.angle, kp2[idx2].angle)], 1);
+                const unsigned long long okm = __ballot(lane < cn && my_ok);
+                for (int t = 0; t < cn; t++) {
+                    if (!((okm >> t) & 1ull)) continue;  // wave-uniform skip
+                    const int idx1 = __builtin_amdgcn_readlane(my_idx, t);
+                    const bool st1 = __builtin_amdgcn_readlane(my_st, t) != 0;
+                    uint32_t q[8];
+#pragma unroll
+                    for (int w = 0; w < 8; w++) q[w] = (uint32_t)__builtin_amdgcn_readlane((int)my_q[w], t);
+                    const float kx = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(my_x), t));
+                    const float ky = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(my_y), t));
+                    // epipolar line l = x1' F12 (ORBmatcher.cc:168-170), wave-uniform
+                    const float a = kx * F[0] + ky * F[3] + F[6];
+                    const float b = kx * F[1] + ky * F[4] + F[7];
+                    const float cc = kx * F[2] + ky * F[5] + F[8];
+                    const float den = a * a + b * b;
+                    unsigned key = max(tri_key(c0, q, st1, a, b, cc, den, lane),
+                                       tri_key(c1, q, st1, a, b, cc, den, lane + 64));
+                    for (int ch = 2; ch * 64 < nF; ch++) {  // nodes past 128 candidates: re-read
+                        TriCand cx;
+                        tri_load(cx, K, k2, cap, f2, ch * 64 + lane, nF, ex, ey, T, only_stereo);
+                        key = max(key, tri_key(cx, q, st1, a, b, cc, den, ch * 64 + lane));
+                    }
+                    const unsigned best = wave_max_u32(key);
+                    const float ang = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(my_ang), t));
+                    if (best) {
+                        wave_nm++;
+                        if (lane == 0) {
+                            const int idx2 = K.fv_feats[(size_t)k2 * cap + f2 + (int)(best & 0xFFFFu)];
+                            out[idx1] = idx2;
+                            if (check_ori) atomicAdd(&hist[tm_rot_bin(ang, kp2[idx2].angle)], 1);
+                        }
                     }
                 }
             }
