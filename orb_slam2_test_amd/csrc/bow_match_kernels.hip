@@ -146,13 +146,28 @@ __global__ __launch_bounds__(256) void k_bow_match(BowMatchSide K, BowMatchSide 
             cd1[w] = ci1 >= 0 ? ((const uint32_t *)(fdesc + (size_t)ci1 * 32))[w] : 0u;
         }
         uint64_t taken = 0;  // bit k: candidate lane + 64 k already matched (nF <= BM_MAX_NODE)
-        for (int ik = k0; ik < k1; ik++) {
-            const int rk = __builtin_amdgcn_readfirstlane(kfe[ik]);
-            if (kval && !kval[rk]) continue;  // pMP NULL or bad: wave-uniform skip
+        // the node's KF features, 64 at a time: lane l loads feature ib + l (index, MapPoint
+        // flag, descriptor) so the in-order walk broadcasts them by readlane instead of
+        // waiting on dependent global loads per feature
+        for (int ib = k0; ib < k1; ib += 64) {
+        const int cn = min(64, k1 - ib);
+        int my_rk = 0, my_ok = 0;
+        uint32_t my_kd[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+        if (lane < cn) {
+            my_rk = kfe[ib + lane];
+            my_ok = !kval || kval[my_rk];  // pMP NULL or bad: skipped
+            const uint4 *dp = (const uint4 *)(kdesc + (size_t)my_rk * 32);
+            const uint4 qa = dp[0], qb = dp[1];
+            my_kd[0] = qa.x; my_kd[1] = qa.y; my_kd[2] = qa.z; my_kd[3] = qa.w;
+            my_kd[4] = qb.x; my_kd[5] = qb.y; my_kd[6] = qb.z; my_kd[7] = qb.w;
+        }
+        const unsigned long long okm = __ballot(lane < cn && my_ok);
+        for (int t = 0; t < cn; t++) {
+            if (!((okm >> t) & 1ull)) continue;  // wave-uniform skip
+            const int rk = __builtin_amdgcn_readlane(my_rk, t);
             uint32_t kd[8];
 #pragma unroll
-            for (int w = 0; w < 8; w++)
-                kd[w] = __builtin_amdgcn_readfirstlane(((const uint32_t *)(kdesc + (size_t)rk * 32))[w]);
+            for (int w = 0; w < 8; w++) kd[w] = (uint32_t)__builtin_amdgcn_readlane((int)my_kd[w], t);
             unsigned b1 = 256, b2 = 256, pos1 = 0xFFFF;
             for (int ch = 0; ch < nchunk; ch++) {  // in position order: strict < keeps the first
                 const int pos = ch * 64 + lane;
@@ -197,6 +212,7 @@ __global__ __launch_bounds__(256) void k_bow_match(BowMatchSide K, BowMatchSide 
                     if (check_ori) atomicAdd(&hist[bm_rot_bin(kkp[rk].angle, fkp[rf].angle)], 1);
                 }
             }
+        }
         }
     }
     __syncthreads();  // the common list is rebuilt by the next pass
