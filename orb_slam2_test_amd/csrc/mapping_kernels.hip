@@ -579,6 +579,9 @@ __global__ __launch_bounds__(256) void k_fuse(orbg_keyframes K, int cap,
 // (d = 0: pKF1's points into pKF2 with sR21 / t21; d = 1: pKF2's into pKF1 with sR12 / t12),
 // writing vnMatch1 / vnMatch2; k_sim3_resolve: one workgroup per pair, the mutual check.
 #define SIM3_TH_HIGH 100
+#ifndef SIM3_SPLIT
+#define SIM3_SPLIT 4
+#endif
 
 __global__ __launch_bounds__(256) void k_sim3_match(orbg_keyframes K, int cap,
                                                     const int32_t *__restrict__ kf1,
@@ -594,7 +597,10 @@ __global__ __launch_bounds__(256) void k_sim3_match(orbg_keyframes K, int cap,
     extern __shared__ __attribute__((aligned(16))) uint8_t fu_lds[];
     int *cstart = (int *)fu_lds;
     FuseKey *keys = (FuseKey *)(fu_lds + (FU_CELLS + 4) * 4);
-    const int p = blockIdx.x >> 1, d = blockIdx.x & 1, tid = threadIdx.x;
+    // workgroup = (pair, direction, split): SIM3_SPLIT workgroups share a direction's points
+    // (each builds the target grid), so a launch of 256 pairs fills the chip
+    const int p = blockIdx.x / (2 * SIM3_SPLIT), rem = blockIdx.x - p * 2 * SIM3_SPLIT;
+    const int d = rem & 1, split = rem >> 1, tid = threadIdx.x;
     const int ks = d ? kf2[p] : kf1[p], kt = d ? kf1[p] : kf2[p];  // source / target KeyFrame
     const int ns = K.counts[ks], nt = K.counts[kt];
     const orbg_sim3_pair G = pairs[p];
@@ -624,7 +630,7 @@ __global__ __launch_bounds__(256) void k_sim3_match(orbg_keyframes K, int cap,
     const uint8_t *am = d ? matched2 : matched1;
     const uint8_t *kdesc = K.desc + (size_t)kt * cap * 32;
     auto nogate = [](int, int, float, float) { return true; };
-    for (int i = tid; i < ns; i += 256) {
+    for (int i = split * 256 + tid; i < ns; i += 256 * SIM3_SPLIT) {
         const size_t o = (size_t)ks * cap + i;
         int best_i = -1;
         const orbg_map_point mp = mps[o];
@@ -733,7 +739,7 @@ int launch_search_by_sim3(hipStream_t st, const orbg_keyframes &K, int cap, cons
         hipFuncSetAttribute((const void *)k_sim3_match, hipFuncAttributeMaxDynamicSharedMemorySize,
                             (int)lds) != hipSuccess)
         return -5;
-    hipLaunchKernelGGL(k_sim3_match, dim3(2 * npairs), dim3(256), lds, st, K, cap, kf1, kf2,
+    hipLaunchKernelGGL(k_sim3_match, dim3(2 * SIM3_SPLIT * npairs), dim3(256), lds, st, K, cap, kf1, kf2,
                        pairs, mps, mdesc, matched1, matched2, th, T, vn);
     hipLaunchKernelGGL(k_sim3_resolve, dim3(npairs), dim3(256), 0, st, kf1, K.counts, cap, vn,
                        match12, nfound);
