@@ -333,6 +333,9 @@ struct FuseKey {  // a grid entry in LDS
     int io;  // index << 4 | octave
 };
 
+#ifndef FUSE_SPLIT
+#define FUSE_SPLIT 4
+#endif
 #define FU_CELLS (ORBG_GRID_COLS * ORBG_GRID_ROWS)
 static_assert(FU_CELLS == 256 * 12, "kf_grid_build's scan gives 12 grid cells to each of 256 threads");
 
@@ -477,7 +480,9 @@ __global__ __launch_bounds__(256) void k_fuse(orbg_keyframes K, int cap,
     int *cstart = (int *)fu_lds;                         // FU_CELLS + 1
     FuseKey *keys = (FuseKey *)(fu_lds + (FU_CELLS + 4) * 4);
     __shared__ int nf_total;
-    const int p = blockIdx.x, tid = threadIdx.x;
+    // FUSE_SPLIT workgroups per pair share its MapPoints (each builds the KeyFrame grid);
+    // their counts meet in nfused[p] (zeroed by the launcher)
+    const int p = blockIdx.x / FUSE_SPLIT, split = blockIdx.x - p * FUSE_SPLIT, tid = threadIdx.x;
     const int kf = kf_index[p];
     const int n = K.counts[kf];
     const orbg_frustum_camera C = cams[p];
@@ -507,7 +512,7 @@ __global__ __launch_bounds__(256) void k_fuse(orbg_keyframes K, int cap,
     mk_gemm3(Tw, 4, true, tc, -1.0, nullptr, Ow);
     const uint8_t *kdesc = K.desc + (size_t)kf * cap * 32;
     const float *kur = (!SIM3 && K.uright) ? K.uright + (size_t)kf * cap : nullptr;
-    for (int i = tid; i < nm; i += 256) {
+    for (int i = split * 256 + tid; i < nm; i += 256 * FUSE_SPLIT) {
         const size_t o = (size_t)p * mcap + i;
         int bidx = -1, bdist = 256;
         const orbg_map_point mp = mps[o];
@@ -566,7 +571,7 @@ __global__ __launch_bounds__(256) void k_fuse(orbg_keyframes K, int cap,
     }
     if (fused) atomicAdd(&nf_total, fused);
     __syncthreads();
-    if (tid == 0) nfused[p] = nf_total;
+    if (tid == 0 && nf_total) atomicAdd(&nfused[p], nf_total);
 }
 
 // ---------------------------------------------------------------------------
@@ -713,12 +718,13 @@ int launch_fuse(hipStream_t st, const orbg_keyframes &K, int cap, const int32_t 
         hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) !=
             hipSuccess)
         return -5;
+    if (hipMemsetAsync(nfused, 0, (size_t)npairs * sizeof(int32_t), st) != hipSuccess) return -5;
     if (sim3)
-        hipLaunchKernelGGL(k_fuse<true>, dim3(npairs), dim3(256), lds, st, K, cap, kf, cams, mps,
-                           mdesc, mcounts, mcap, th, T, best_idx, best_dist, nfused);
+        hipLaunchKernelGGL(k_fuse<true>, dim3(npairs * FUSE_SPLIT), dim3(256), lds, st, K, cap,
+                           kf, cams, mps, mdesc, mcounts, mcap, th, T, best_idx, best_dist, nfused);
     else
-        hipLaunchKernelGGL(k_fuse<false>, dim3(npairs), dim3(256), lds, st, K, cap, kf, cams,
-                           mps, mdesc, mcounts, mcap, th, T, best_idx, best_dist, nfused);
+        hipLaunchKernelGGL(k_fuse<false>, dim3(npairs * FUSE_SPLIT), dim3(256), lds, st, K, cap,
+                           kf, cams, mps, mdesc, mcounts, mcap, th, T, best_idx, best_dist, nfused);
     return hipGetLastError() == hipSuccess ? 0 : -5;
 }
 
