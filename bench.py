@@ -261,6 +261,9 @@ def main():
                     help="mono: the full batched-sequence step, with the pose/trajectory stub "
                          "of every pair (orbg_match_pose_batch_device) gathered beside the "
                          "summary and vnMatches12 rows (SURVEY.md 8e); not the headline metric")
+    ap.add_argument("--force-collective", action="store_true",
+                    help="run the per-step RCCL all_gathers even at world size 1 (a one-rank "
+                         "nccl process group): exercises the multi-GPU gather path on one GPU")
     args = ap.parse_args()
 
     import torch
@@ -272,7 +275,16 @@ def main():
     local = int(os.environ.get("LOCAL_RANK", "0"))
     torch.cuda.set_device(local)
     dist_info = {"world_size": 1, "backend": None}
-    if world > 1:
+    collective = world > 1 or args.force_collective
+    if collective:
+        if world == 1:  # a one-rank group outside torch.distributed.run
+            import socket
+            with socket.socket() as s:
+                s.bind(("127.0.0.1", 0))
+                port = s.getsockname()[1]
+            for k, v in (("MASTER_ADDR", "127.0.0.1"), ("MASTER_PORT", str(port)),
+                         ("RANK", "0"), ("WORLD_SIZE", "1")):
+                os.environ.setdefault(k, v)
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
         # what the collectives really run on (RCCL reports itself as "nccl" on ROCm)
         dist_info = {"world_size": dist.get_world_size(), "backend": dist.get_backend(),
@@ -316,7 +328,8 @@ def main():
     if args.serial:  # PMC runs (tools/round_prof.sh): one dispatch per kernel and step
         ext.ctx.set_serial(True)
     mode = "stereo" if args.stereo else "extract" if args.extract_only else "mono"
-    bstep = sequence.BenchStep(ext, B, mode, world=world, with_pose=args.with_pose)
+    bstep = sequence.BenchStep(ext, B, mode, world=world, with_pose=args.with_pose,
+                               collective=collective)
     torch.cuda.synchronize()
     it = [0]
 
@@ -457,8 +470,10 @@ def main():
                                             nblocks * nimg * W * H / 1e6)
                                 if nblocks > 1 else "the same resident block every step"),
                 "height": H, "nfeatures": NFEAT, "nlevels": NLEV,
-                "parallelism": "frames sharded over %d GPU(s), RCCL all_gather of per-frame "
-                               "summary" % world},
+                "parallelism": ("frames sharded over %d GPU(s), RCCL all_gather of the "
+                                "per-frame outputs per step" % world if collective else
+                                "1 GPU, no collective (the gathers run only at world > 1 or "
+                                "with --force-collective)")},
             "dist": dist_info,
             "roofline": roof,
             "pipeline_roofline": {"algo_bytes_per_frame": fab,
@@ -480,7 +495,7 @@ def main():
         else:
             out["cpu_baseline"] = None
         print(json.dumps(out), flush=True)
-    if world > 1:
+    if collective:
         dist.barrier()
         dist.destroy_process_group()
 

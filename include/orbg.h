@@ -225,7 +225,10 @@ int orbg_download_stereo(orbg_ctx *ctx, int pair, float *uright, float *depth, i
  * keypoints would be incomplete) sets a flag that stays set until read.  orbg_sync,
  * orbg_check_errors, orbg_batch_stats and orbg_download_frame drain the streams, read and
  * clear it, and return ORBG_ENOTSUP (orbg_last_error names the flags and the first frame)
- * if any batch since the last read raised one. */
+ * if any batch since the last read raised one.  The device matchers that read per-pair
+ * counts from device memory (orbg_fuse[_sim3]_batch_device, orbg_search_by_sim3_batch_device)
+ * clamp a count past its capacity (KeyFrame counts to `cap`, MapPoint counts to `mcap`) and
+ * raise flag 0x10000; the next read returns ORBG_EINVAL naming the first pair. */
 int orbg_sync(orbg_ctx *ctx);
 int orbg_check_errors(orbg_ctx *ctx);
 void *orbg_stream(orbg_ctx *ctx);       /* hipStream_t of extraction (and host-data calls) */
@@ -384,6 +387,9 @@ typedef struct {
     int32_t check_ori;
     int32_t *match;              /* [B][frame_cap] out */
     int32_t *nmatches;           /* [B] out */
+    /* appended in round 4 (ABI note): read only in the relocalization / loop
+     * modes, so a caller built against the older, shorter struct stays valid in the
+     * last-frame / local-map modes */
     const struct orbg_frustum_camera *fcams;  /* [B], relocalization / loop modes */
     int32_t orb_dist;            /* relocalization: ORBdist */
 } orbg_track_batch;
@@ -559,8 +565,9 @@ int orbg_fuse(orbg_ctx *ctx, const orbg_keyframe *kf, const orbg_frustum_camera 
               int32_t *best_idx, int32_t *best_dist, int *nfused);
 /* Batched, device memory: pair p = KeyFrame d_kf[p] of `kfs` (desc, kps, uright, counts
  * read) with camera d_cams[p] and the d_mcounts[p] MapPoints at d_mps + p * mcap (descriptors
- * d_mdesc + p * mcap * 32); outputs at + p * mcap, d_nfused[p] = points with a target.
- * Context stream.  ORBG_ENOTSUP past 8192 keypoints per KeyFrame (the grid lives in LDS). */
+ * d_mdesc + p * mcap * 32); outputs at + p * mcap, d_nfused[p] = points with a target
+ * (written even when mcap == 0: zero).  Context stream.  ORBG_ENOTSUP past 8192 keypoints per
+ * KeyFrame (the grid lives in LDS). */
 int orbg_fuse_batch_device(orbg_ctx *ctx, const orbg_keyframes *kfs, int cap, const int32_t *d_kf,
                            const orbg_frustum_camera *d_cams, const orbg_map_point *d_mps,
                            const uint8_t *d_mdesc, const int32_t *d_mcounts, int mcap, int npairs,

@@ -56,10 +56,12 @@ __host__ __device__ inline void sim3_decompose(const float *S, float *T)
 }
 
 // MapPoint::PredictScale (MapPoint.cc:575-607): ceil(log(ratio) / mfLogScaleFactor) in double.
-// Fast path: the float quotient (logf within ~1 ulp, so within 1e-6 of the exact quotient for
-// any |q| < 64) decides the ceiling whenever it is more than 1e-3 away from an integer -- the
-// double quotient is then inside the same open interval; near an integer, or non-finite, the
-// reference's double expression is evaluated.  Same result, a fraction of the FP64 issue.
+// Fast path: the float quotient (logf within ~1 ulp, then one division: a few float ulps of q,
+// i.e. about 1e-5 absolute near |q| = 64, where the ulp is 3.8e-6) decides the ceiling whenever
+// it is more than 1e-3 away from an integer -- the double quotient is then inside the same
+// open interval; near an integer, or non-finite, the reference's double expression is
+// evaluated.  Same result, a fraction of the FP64 issue (pinned on ratios up to |q| ~ 64 by
+// tests/test_oracle_frame.py).
 __host__ __device__ inline int predict_scale(float max_dist, float dist, float log_sf, int nlevels)
 {
     const float ratio = max_dist / dist;

@@ -474,7 +474,8 @@ __global__ __launch_bounds__(256) void k_fuse(orbg_keyframes K, int cap,
                                               float th, FuseTables T,
                                               int32_t *__restrict__ best_idx,
                                               int32_t *__restrict__ best_dist,
-                                              int32_t *__restrict__ nfused)
+                                              int32_t *__restrict__ nfused,
+                                              int32_t *__restrict__ err_flag)
 {
     extern __shared__ __attribute__((aligned(16))) uint8_t fu_lds[];
     int *cstart = (int *)fu_lds;                         // FU_CELLS + 1
@@ -484,7 +485,15 @@ __global__ __launch_bounds__(256) void k_fuse(orbg_keyframes K, int cap,
     // their counts meet in nfused[p] (zeroed by the launcher)
     const int p = blockIdx.x / FUSE_SPLIT, split = blockIdx.x - p * FUSE_SPLIT, tid = threadIdx.x;
     const int kf = kf_index[p];
-    const int n = K.counts[kf];
+    // counts are device data the host never sees: one past its capacity would overrun the
+    // LDS grid (cap entries) or the pair's output rows, so it is clamped and flagged
+    // (ORBG_DEVFLAG_COUNT, sticky until orbg_check_errors)
+    const int n_in = K.counts[kf], nm_in = mcounts[p];
+    const int n = min(max(n_in, 0), cap), nm = min(max(nm_in, 0), mcap);
+    if (tid == 0 && split == 0 && (n != n_in || nm != nm_in)) {
+        atomicOr(err_flag, ORBG_DEVFLAG_COUNT);
+        atomicMin(err_flag + 1, p);
+    }
     const orbg_frustum_camera C = cams[p];
     const orbg_keypoint *kps = K.kps + (size_t)kf * cap;
     const float inv_w = (float)ORBG_GRID_COLS / (float)(C.bounds.max_x - C.bounds.min_x);
@@ -497,7 +506,6 @@ __global__ __launch_bounds__(256) void k_fuse(orbg_keyframes K, int cap,
     const float kminx = (float)(int)C.bounds.min_x, kmaxx = (float)(int)C.bounds.max_x;
     const float kminy = (float)(int)C.bounds.min_y, kmaxy = (float)(int)C.bounds.max_y;
     int fused = 0;
-    const int nm = mcounts[p];
     float Tw[12];
     if (SIM3) {
         sim3_decompose(C.Tcw, Tw);
@@ -597,7 +605,8 @@ __global__ __launch_bounds__(256) void k_sim3_match(orbg_keyframes K, int cap,
                                                     const uint8_t *__restrict__ matched1,
                                                     const uint8_t *__restrict__ matched2,
                                                     float th, FuseTables T,
-                                                    int32_t *__restrict__ vn)
+                                                    int32_t *__restrict__ vn,
+                                                    int32_t *__restrict__ err_flag)
 {
     extern __shared__ __attribute__((aligned(16))) uint8_t fu_lds[];
     int *cstart = (int *)fu_lds;
@@ -607,7 +616,13 @@ __global__ __launch_bounds__(256) void k_sim3_match(orbg_keyframes K, int cap,
     const int p = blockIdx.x / (2 * SIM3_SPLIT), rem = blockIdx.x - p * 2 * SIM3_SPLIT;
     const int d = rem & 1, split = rem >> 1, tid = threadIdx.x;
     const int ks = d ? kf2[p] : kf1[p], kt = d ? kf1[p] : kf2[p];  // source / target KeyFrame
-    const int ns = K.counts[ks], nt = K.counts[kt];
+    // clamped to the capacity and flagged as in k_fuse
+    const int ns_in = K.counts[ks], nt_in = K.counts[kt];
+    const int ns = min(max(ns_in, 0), cap), nt = min(max(nt_in, 0), cap);
+    if (tid == 0 && split == 0 && (ns != ns_in || nt != nt_in)) {
+        atomicOr(err_flag, ORBG_DEVFLAG_COUNT);
+        atomicMin(err_flag + 1, p);
+    }
     const orbg_sim3_pair G = pairs[p];
     const float inv_w = (float)ORBG_GRID_COLS / (float)(G.bounds.max_x - G.bounds.min_x);
     const float inv_h = (float)ORBG_GRID_ROWS / (float)(G.bounds.max_y - G.bounds.min_y);
@@ -682,7 +697,7 @@ __global__ __launch_bounds__(256) void k_sim3_resolve(const int32_t *__restrict_
 {
     __shared__ int tot;
     const int p = blockIdx.x, tid = threadIdx.x;
-    const int n1 = counts[kf1[p]];
+    const int n1 = min(max(counts[kf1[p]], 0), cap);  // flagged by k_sim3_match
     if (tid == 0) tot = 0;
     __syncthreads();
     const int32_t *v1 = vn + (size_t)p * 2 * cap, *v2 = v1 + cap;
@@ -702,7 +717,7 @@ int launch_fuse(hipStream_t st, const orbg_keyframes &K, int cap, const int32_t 
                 const orbg_frustum_camera *cams, const orbg_map_point *mps, const uint8_t *mdesc,
                 const int32_t *mcounts, int mcap, int npairs, float th, const float *scale,
                 const float *inv_sigma2, int nlevels, int sim3, int32_t *best_idx,
-                int32_t *best_dist, int32_t *nfused)
+                int32_t *best_dist, int32_t *nfused, int32_t *err_flag)
 {
     if (npairs <= 0) return 0;
     if (cap > 8192) return -95;  // the grid's entries in LDS
@@ -721,10 +736,12 @@ int launch_fuse(hipStream_t st, const orbg_keyframes &K, int cap, const int32_t 
     if (hipMemsetAsync(nfused, 0, (size_t)npairs * sizeof(int32_t), st) != hipSuccess) return -5;
     if (sim3)
         hipLaunchKernelGGL(k_fuse<true>, dim3(npairs * FUSE_SPLIT), dim3(256), lds, st, K, cap,
-                           kf, cams, mps, mdesc, mcounts, mcap, th, T, best_idx, best_dist, nfused);
+                           kf, cams, mps, mdesc, mcounts, mcap, th, T, best_idx, best_dist, nfused,
+                           err_flag);
     else
         hipLaunchKernelGGL(k_fuse<false>, dim3(npairs * FUSE_SPLIT), dim3(256), lds, st, K, cap,
-                           kf, cams, mps, mdesc, mcounts, mcap, th, T, best_idx, best_dist, nfused);
+                           kf, cams, mps, mdesc, mcounts, mcap, th, T, best_idx, best_dist, nfused,
+                           err_flag);
     return hipGetLastError() == hipSuccess ? 0 : -5;
 }
 
@@ -734,7 +751,7 @@ int launch_search_by_sim3(hipStream_t st, const orbg_keyframes &K, int cap, cons
                           const orbg_map_point *mps, const uint8_t *mdesc,
                           const uint8_t *matched1, const uint8_t *matched2, int npairs, float th,
                           const float *scale, int nlevels, int32_t *vn, int32_t *match12,
-                          int32_t *nfound)
+                          int32_t *nfound, int32_t *err_flag)
 {
     if (npairs <= 0) return 0;
     if (cap > 8192) return -95;  // the grid's entries in LDS
@@ -746,7 +763,7 @@ int launch_search_by_sim3(hipStream_t st, const orbg_keyframes &K, int cap, cons
                             (int)lds) != hipSuccess)
         return -5;
     hipLaunchKernelGGL(k_sim3_match, dim3(2 * SIM3_SPLIT * npairs), dim3(256), lds, st, K, cap, kf1, kf2,
-                       pairs, mps, mdesc, matched1, matched2, th, T, vn);
+                       pairs, mps, mdesc, matched1, matched2, th, T, vn, err_flag);
     hipLaunchKernelGGL(k_sim3_resolve, dim3(npairs), dim3(256), 0, st, kf1, K.counts, cap, vn,
                        match12, nfound);
     return hipGetLastError() == hipSuccess ? 0 : -5;

@@ -84,13 +84,13 @@ int launch_fuse(hipStream_t st, const orbg_keyframes &K, int cap, const int32_t 
                 const orbg_frustum_camera *cams, const orbg_map_point *mps, const uint8_t *mdesc,
                 const int32_t *mcounts, int mcap, int npairs, float th, const float *scale,
                 const float *inv_sigma2, int nlevels, int sim3, int32_t *best_idx,
-                int32_t *best_dist, int32_t *nfused);
+                int32_t *best_dist, int32_t *nfused, int32_t *err_flag);
 int launch_search_by_sim3(hipStream_t st, const orbg_keyframes &K, int cap, const int32_t *kf1,
                           const int32_t *kf2, const orbg_sim3_pair *pairs,
                           const orbg_map_point *mps, const uint8_t *mdesc,
                           const uint8_t *matched1, const uint8_t *matched2, int npairs, float th,
                           const float *scale, int nlevels, int32_t *vn, int32_t *match12,
-                          int32_t *nfound);
+                          int32_t *nfound, int32_t *err_flag);
 int launch_rgbd(hipStream_t st, const void *depth, int u16, float factor, int w, int h,
                 size_t pitch, size_t istride, const orbg_keypoint *kps,
                 const orbg_keypoint *kps_un, const int32_t *counts, int fc, int nframes,
@@ -424,6 +424,8 @@ struct orbg_ctx {
     // tracking matchers: K-lists of the queries
     void *d_trk = nullptr;
     size_t trk_bytes = 0;
+    void *d_sim3 = nullptr;  // SearchBySim3's vnMatch1 / vnMatch2 scratch
+    size_t sim3_bytes = 0;
     // batched-sequence pose stub (orbg_match_pose_batch_device): edges, counts, cameras, poses
     void *d_mpose = nullptr;
     size_t mpose_bytes = 0;
@@ -1397,6 +1399,7 @@ extern "C" void orbg_destroy(orbg_ctx *c)
     if (c->d_pack) hipFree(c->d_pack);
     if (c->d_scr) hipFree(c->d_scr);
     if (c->d_trk) hipFree(c->d_trk);
+    if (c->d_sim3) hipFree(c->d_sim3);
     if (c->d_mpose) hipFree(c->d_mpose);
     if (c->d_kps_un) hipFree(c->d_kps_un);
     if (c->aux_stream) hipStreamSynchronize(c->aux_stream);
@@ -1778,7 +1781,9 @@ static int sync_all(orbg_ctx *c)
 
 // Drains every stream, then reads and clears the sticky device error word: a non-zero flag
 // means some frame since the last read lost a level (quadtree capacity exceeded) and its
-// keypoints are incomplete, so the caller gets ORBG_ENOTSUP instead of short outputs.
+// keypoints are incomplete, so the caller gets ORBG_ENOTSUP instead of short outputs; or
+// that a device matcher was handed a count past its capacity (ORBG_DEVFLAG_COUNT: clamped,
+// ORBG_EINVAL).
 static int check_err(orbg_ctx *c)
 {
     int rc = sync_all(c);
@@ -1790,6 +1795,9 @@ static int check_err(orbg_ctx *c)
     if (e[0]) {
         const int32_t e0[2] = {0, INT32_MAX};
         HIPCHK(hipMemcpy(c->d_err, e0, sizeof(e0), hipMemcpyHostToDevice));
+        if (e[0] & ORBG_DEVFLAG_COUNT)
+            return set_err(ORBG_EINVAL, "a device matcher count exceeded its capacity (clamped; "
+                                        "flags 0x%x, first pair %d since the last check)", e[0], e[1]);
         return set_err(ORBG_ENOTSUP, "quadtree capacity exceeded (flags 0x%x, first frame %d of "
                                      "a batch since the last check)", e[0], e[1]);
     }
@@ -3093,8 +3101,13 @@ static int track_run(orbg_ctx *c, int mode, const orbg_track_batch *tb, int nfra
     A.topn = (int32_t *)((uint8_t *)c->d_trk + tk);
     A.match = tb->match;
     A.nmatches = tb->nmatches;
-    A.fcams = tb->fcams;
-    A.orb_dist = tb->orb_dist;
+    // fcams / orb_dist were appended to orbg_track_batch in round 4: a caller built against
+    // the older header passes the shorter struct, so they are read only in the modes that
+    // define them (ABI notes)
+    if (mode == ORBG_TRACK_RELOC || mode == ORBG_TRACK_LOOP) {
+        A.fcams = tb->fcams;
+        A.orb_dist = tb->orb_dist;
+    }
     if (mode == ORBG_TRACK_LOOP) A.check_ori = 0;
     const int rc = launch_track(c->stream, mode, A, nframes, &c->prof);
     if (rc == ORBG_ENOTSUP)
@@ -4332,17 +4345,22 @@ static int fuse_batch(orbg_ctx *c, const orbg_keyframes *kfs, int cap, const int
 {
     if (!c || !kfs) return set_err(ORBG_EINVAL, "NULL argument");
     if (npairs < 0 || cap <= 0 || mcap < 0) return set_err(ORBG_EINVAL, "bad sizes");
-    if (npairs == 0 || mcap == 0) return ORBG_OK;
-    if (!d_kf || !d_cams || !d_mps || !d_mdesc || !d_mcounts || !d_best_idx || !d_best_dist ||
-        !d_nfused || !kfs->desc || !kfs->kps || !kfs->counts)
-        return set_err(ORBG_EINVAL, "NULL device array");
+    if (npairs == 0) return ORBG_OK;
+    if (!d_nfused) return set_err(ORBG_EINVAL, "NULL device array");
     HIPCHK(hipSetDevice(c->device));
     hipStream_t st = c->stream;
+    if (mcap == 0) {  // no MapPoints: every pair fuses nothing (orbg.h: d_nfused is written)
+        HIPCHK(hipMemsetAsync(d_nfused, 0, (size_t)npairs * sizeof(int32_t), st));
+        return ORBG_OK;
+    }
+    if (!d_kf || !d_cams || !d_mps || !d_mdesc || !d_mcounts || !d_best_idx || !d_best_dist ||
+        !kfs->desc || !kfs->kps || !kfs->counts)
+        return set_err(ORBG_EINVAL, "NULL device array");
     int rc = 0;
     PROF_LAUNCH(c, sim3 ? "fuse_sim3" : "fuse",
                 rc = launch_fuse(st, *kfs, cap, d_kf, d_cams, d_mps, d_mdesc, d_mcounts, mcap,
                                  npairs, th, c->scale, c->inv_sigma2, c->p.nlevels, sim3,
-                                 d_best_idx, d_best_dist, d_nfused));
+                                 d_best_idx, d_best_dist, d_nfused, c->d_err));
     if (rc == -95) return set_err(ORBG_ENOTSUP, "Fuse: more than 8192 keypoints per KeyFrame");
     if (rc) return set_err(ORBG_EIO, "k_fuse launch failed");
     return ORBG_OK;
@@ -4425,7 +4443,7 @@ static int fuse_host(orbg_ctx *c, const orbg_keyframe *kf, const orbg_frustum_ca
                      (const orbg_frustum_camera *)(db + o_cam), (const orbg_map_point *)(db + o_mp),
                      db + o_md, (const int32_t *)(db + o_mc), nmp, 1, th, c->scale, c->inv_sigma2,
                      c->p.nlevels, sim3, (int32_t *)(db + o_bi), (int32_t *)(db + o_bd),
-                     (int32_t *)(db + o_nf));
+                     (int32_t *)(db + o_nf), c->d_err);
     if (rc) return set_err(ORBG_EIO, "k_fuse launch failed");
     HIPCHK(hipMemcpyAsync(hs + o_bi, db + o_bi, o - o_bi, hipMemcpyDeviceToHost, c->stream));
     HIPCHK(hipStreamSynchronize(c->stream));
@@ -4435,20 +4453,21 @@ static int fuse_host(orbg_ctx *c, const orbg_keyframe *kf, const orbg_frustum_ca
     return ORBG_OK;
 }
 
-// scratch for k_sim3_match's vnMatch1 / vnMatch2 (npairs * 2 * cap int32), kept in the
-// tracking scratch buffer (the two never run at once on a context)
+// scratch for k_sim3_match's vnMatch1 / vnMatch2 (npairs * 2 * cap int32): a buffer of its
+// own (not the tracking matchers' d_trk), so neither path depends on the other's stream.
+// Growing it synchronises c->stream, the only stream its kernels are enqueued on.
 static int sim3_scratch(orbg_ctx *c, size_t need, void **out)
 {
-    if (c->trk_bytes < need) {
+    if (c->sim3_bytes < need) {
         HIPCHK(hipStreamSynchronize(c->stream));
-        if (c->d_trk) hipFree(c->d_trk);
-        c->d_trk = nullptr;
-        c->trk_bytes = 0;
-        if (hipMalloc(&c->d_trk, need) != hipSuccess)
+        if (c->d_sim3) hipFree(c->d_sim3);
+        c->d_sim3 = nullptr;
+        c->sim3_bytes = 0;
+        if (hipMalloc(&c->d_sim3, need) != hipSuccess)
             return set_err(ORBG_ENOMEM, "SearchBySim3 scratch %zu bytes", need);
-        c->trk_bytes = need;
+        c->sim3_bytes = need;
     }
-    *out = c->d_trk;
+    *out = c->d_sim3;
     return ORBG_OK;
 }
 
@@ -4476,7 +4495,8 @@ extern "C" int orbg_search_by_sim3_batch_device(orbg_ctx *c, const orbg_keyframe
     PROF_LAUNCH(c, "sim3_match",
                 rc = launch_search_by_sim3(st, *kfs, cap, d_kf1, d_kf2, d_pairs, d_mps,
                                            d_mdesc, d_matched1, d_matched2, npairs, th, c->scale,
-                                           c->p.nlevels, (int32_t *)vn, d_matches12, d_nfound));
+                                           c->p.nlevels, (int32_t *)vn, d_matches12, d_nfound,
+                                           c->d_err));
     if (rc) return set_err(ORBG_EIO, "k_sim3_match launch failed");
     return ORBG_OK;
 }
@@ -4549,7 +4569,7 @@ extern "C" int orbg_search_by_sim3(orbg_ctx *c, const orbg_keyframe *kf1, const 
                                (const orbg_sim3_pair *)(db + o_pair),
                                (const orbg_map_point *)(db + o_mp), db + o_md, db + o_am1,
                                db + o_am2, 1, th, c->scale, c->p.nlevels, (int32_t *)vn,
-                               (int32_t *)(db + o_m), (int32_t *)(db + o_nf));
+                               (int32_t *)(db + o_m), (int32_t *)(db + o_nf), c->d_err);
     if (rc) return set_err(ORBG_EIO, "k_sim3_match launch failed");
     HIPCHK(hipMemcpyAsync(hs + o_m, db + o_m, o - o_m, hipMemcpyDeviceToHost, c->stream));
     HIPCHK(hipStreamSynchronize(c->stream));

@@ -26,6 +26,9 @@
 #define ORBG_GRID_COLS 64        // Frame.h:38
 #define ORBG_GRID_ROWS 48        // Frame.h:37
 #define ORBG_MATCH_TOPK 8
+// sticky device error word, bit 16: a device matcher read a per-frame / per-pair count past
+// its capacity (clamped; orbg_check_errors reports it).  Bits 0..9: the quadtree's flags.
+#define ORBG_DEVFLAG_COUNT (1 << 16)
 // orbg_ba_graph's packed LBA edge (24 B instead of orbg_edge's 104): flags bit 0 stereo,
 // 1 robust, 2 active, bits 8..15 camera index, 16..31 (information, Huber) index; the
 // observations are f32 (ORB-SLAM2's are cv::KeyPoint floats: exact)

@@ -42,14 +42,16 @@ def local_indices(nframes, lo, hi):
     return np.concatenate([[(lo - 1) % nframes], np.arange(lo, hi)]).astype(np.int64)
 
 
-def gather_rows(local, world, group=None, sizes=None):
+def gather_rows(local, world, group=None, sizes=None, force=False):
     """all_gather a per-rank tensor whose dim 0 holds m_r frames into the global tensor, in
     rank (= frame) order.  Ranks may hold different m_r, so blocks are padded to the largest
     before the collective.  Pass `sizes` (every rank's m_r) when known to skip the size
-    exchange and its host sync (bench.py's fixed per-rank batch)."""
+    exchange and its host sync (bench.py's fixed per-rank batch).  At world 1 the local
+    tensor is returned with no collective unless `force` (bench.py --force-collective and
+    tests/test_gpu_rccl.py run the RCCL path on a one-rank group)."""
     import torch
     import torch.distributed as dist
-    if world == 1:
+    if world == 1 and not force:
         return local
     if sizes is None:
         m = torch.tensor([local.shape[0]], dtype=torch.int64, device=local.device)
@@ -64,12 +66,12 @@ def gather_rows(local, world, group=None, sizes=None):
     return torch.cat([o[:n] for o, n in zip(out, sizes)], dim=0)
 
 
-def gather_summary(local, world, group=None, sizes=None):
+def gather_summary(local, world, group=None, sizes=None, force=False):
     """all_gather a per-rank int32 tensor of shape [2, m_r] (row 0 keypoints, row 1
     matches) into the global [2, N] summary (gather_rows along the frame axis)."""
-    if world == 1:
+    if world == 1 and not force:
         return local
-    return gather_rows(local.t().contiguous(), world, group, sizes).t().contiguous()
+    return gather_rows(local.t().contiguous(), world, group, sizes, force).t().contiguous()
 
 
 def run_sharded(frames, world, rank, backend, group=None, device="cpu", with_matches=False,
@@ -222,14 +224,16 @@ class BenchStep:
     (`bench.py --with-pose` times the full sequence step).
 
     `group` is the process group of the gathers (None: the default group; the 2-process
-    one-GPU tests run them over gloo).
+    one-GPU tests run them over gloo).  The gathers run when world > 1, or with
+    `collective=True` at any world size (a one-rank RCCL group: bench.py
+    --force-collective, tests/test_gpu_rccl.py).
 
     `capture(step)`, when set (tests), runs on the match stream after the step's outputs
     are written (orbg_batch_acquire) and before liborbg may reuse them
     (orbg_batch_release); the bench leaves it unset."""
 
     def __init__(self, ext, B, mode="mono", world=1, window=100, nnratio=0.9, check_ori=True,
-                 bf=None, min_z=None, with_pose=False, group=None):
+                 bf=None, min_z=None, with_pose=False, group=None, collective=None):
         import torch
         from . import synthetic
         if mode not in ("mono", "extract", "stereo"):
@@ -247,6 +251,7 @@ class BenchStep:
         self.m12 = None
         self.with_pose = with_pose and mode == "mono"
         self.group = group
+        self.collective = world > 1 if collective is None else bool(collective)
         if self.with_pose:
             self.dq = torch.zeros((B, 4), dtype=torch.float64, device="cuda")
             self.dt = torch.zeros((B, 3), dtype=torch.float64, device="cuda")
@@ -263,10 +268,10 @@ class BenchStep:
         if self.mode == "stereo":
             ext.stereo_batch_device(self.sl, self.sr, self.bf, self.min_z)
             ext.ctx.stereo_summary(self.ssum.data_ptr())
-            if self.world > 1:  # per-frame (keypoints, depths) of every rank
+            if self.collective:  # per-frame (keypoints, depths) of every rank
                 with torch.cuda.stream(self.mstream):
                     self.gathered = gather_summary(self.ssum.view(2, B), self.world, self.group,
-                                                   sizes=[B] * self.world)
+                                                   sizes=[B] * self.world, force=True)
         elif self.mode == "mono":
             ext.match_batch_device(self.f1, self.f2, self.window, self.nnratio, self.check_ori)
             ext.ctx.batch_summary(self.summary.data_ptr())
@@ -279,14 +284,15 @@ class BenchStep:
                                             self.dt.data_ptr(), self.dn.data_ptr())
                 with torch.cuda.stream(self.mstream):  # written there (orbg.h)
                     self.pose = torch.cat([self.dq, self.dt, self.dn.double()[:, None]], 1)
-            if self.world > 1:
+            if self.collective:
                 with torch.cuda.stream(self.mstream):
                     sizes = [B] * self.world
                     local = torch.stack([self.summary[1:B + 1], self.summary[B + 1:]])
-                    g = [gather_summary(local, self.world, self.group, sizes=sizes),
-                         gather_rows(self.m12, self.world, self.group, sizes=sizes)]
+                    g = [gather_summary(local, self.world, self.group, sizes=sizes, force=True),
+                         gather_rows(self.m12, self.world, self.group, sizes=sizes, force=True)]
                     if self.with_pose:
-                        g.append(gather_rows(self.pose, self.world, self.group, sizes=sizes))
+                        g.append(gather_rows(self.pose, self.world, self.group, sizes=sizes,
+                                             force=True))
                     self.gathered = tuple(g)
         if self.capture is not None:
             ext.ctx.batch_acquire(self.mstream.cuda_stream)

@@ -176,3 +176,59 @@ def test_widening_entry_points_reject_bad_arguments():
     assert lib.orbg_search_by_sim3(h, C.byref(kb), L.ptr(bmp), L.ptr(bd), None, C.byref(kb),
                                    L.ptr(bmp), L.ptr(bd), None, L.ptr(g), 7.5, L.ptr(bm),
                                    C.byref(n)) == L.ORBG_ENOTSUP
+
+
+def test_device_matcher_counts_are_clamped_and_flagged():
+    """orbg_fuse_batch_device reads the KeyFrame and MapPoint counts from device
+    memory.  A count past `cap` / `mcap` is clamped in the kernel (no LDS or output overrun:
+    a guard region after the outputs stays untouched) and raises the sticky flag 0x10000,
+    which the next orbg_sync reports as ORBG_EINVAL; a pair with sane counts is unaffected,
+    and mcap == 0 still writes d_nfused (zero)."""
+    import ctypes as C
+    import test_oracle_mapping as T
+    from orb_slam2_test_amd.orbmatcher import _ctx
+    P, cap, mcap, guard = 2, 2048, 1500, 4096
+    cases = [T.fuse_case(_lib, 70 + p, n=1800, nmp=1400) for p in range(P)]
+    desc = np.zeros((P, cap, 32), np.uint8)
+    kps = np.zeros((P, cap), _lib.KP_DTYPE)
+    ur = np.zeros((P, cap), np.float32)
+    cams = np.zeros(P, _lib.FRUSTUM_DTYPE)
+    mps = np.zeros((P, mcap), _lib.MAPPOINT_DTYPE)
+    md = np.zeros((P, mcap, 32), np.uint8)
+    for p, (kf, fc, mp, mdsc) in enumerate(cases):
+        n = len(kf["kps"])
+        desc[p, :n], kps[p, :n], ur[p, :n] = kf["desc"], kf["kps"], kf["uright"]
+        cams[p] = fc
+        mps[p, :len(mp)], md[p, :len(mp)] = mp, mdsc
+    cnt = np.array([1800, 1 << 20], np.int32)   # pair 1's KeyFrame count is past cap
+    mc = np.array([1400, 1 << 20], np.int32)    # and its MapPoint count past mcap
+    t = {k: torch.from_numpy(np.ascontiguousarray(v).view(np.uint8).reshape(-1).copy()).cuda()
+         for k, v in dict(desc=desc, kps=kps, ur=ur, cnt=cnt, cams=cams, mps=mps, md=md,
+                          mc=mc).items()}
+    K = _lib.KeyFrames(t["desc"].data_ptr(), t["kps"].data_ptr(), t["ur"].data_ptr(), None,
+                       t["cnt"].data_ptr(), None, None, None, None)
+    kfi = torch.arange(P, dtype=torch.int32, device="cuda")
+    bi = torch.full((P * mcap + guard,), -9, dtype=torch.int32, device="cuda")
+    bd = torch.full((P * mcap + guard,), -9, dtype=torch.int32, device="cuda")
+    nf = torch.full((P,), -7, dtype=torch.int32, device="cuda")
+    ctx = _ctx()
+    torch.cuda.synchronize()
+    _lib.check(_lib.lib().orbg_fuse_batch_device(
+        ctx.handle, C.byref(K), cap, kfi.data_ptr(), t["cams"].data_ptr(), t["mps"].data_ptr(),
+        t["md"].data_ptr(), t["mc"].data_ptr(), mcap, P, 3.0, bi.data_ptr(), bd.data_ptr(),
+        nf.data_ptr()), "fuse")
+    with pytest.raises(_lib.OrbgError) as ei:
+        ctx.sync()
+    assert ei.value.code == _lib.ORBG_EINVAL and "capacity" in str(ei.value)
+    ctx.sync()  # read and cleared
+    torch.cuda.synchronize()
+    assert np.all(bi[P * mcap:].cpu().numpy() == -9) and np.all(bd[P * mcap:].cpu().numpy() == -9)
+    assert int(nf[0]) > 100  # the sane pair still fuses
+    # mcap == 0: nothing to search, d_nfused still written
+    nf.fill_(-7)
+    _lib.check(_lib.lib().orbg_fuse_batch_device(
+        ctx.handle, C.byref(K), cap, kfi.data_ptr(), t["cams"].data_ptr(), t["mps"].data_ptr(),
+        t["md"].data_ptr(), t["mc"].data_ptr(), 0, P, 3.0, bi.data_ptr(), bd.data_ptr(),
+        nf.data_ptr()), "fuse mcap 0")
+    ctx.sync()
+    assert np.all(nf.cpu().numpy() == 0)

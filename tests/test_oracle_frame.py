@@ -350,7 +350,13 @@ def test_predict_scale_fast_path_logic():
     k = rng.integers(-3, 12, 500000)
     near = (np.float64(1.2) ** k * (1 + rng.normal(0, 1e-6, k.size))).astype(np.float32)
     wide = np.exp(rng.uniform(-3, 4, 500000)).astype(np.float32)
-    r = np.concatenate([near, wide, (np.float64(1.2) ** np.arange(-3, 12)).astype(np.float32)])
+    # |q| up to the fast path's limit of 64 (the float quotient's error grows with |q|: about
+    # 1e-5 near 64, still far inside the 1e-3 margin)
+    kf = rng.integers(-64, 64, 200000)
+    far = (np.float64(1.2) ** kf * (1 + rng.normal(0, 1e-4, kf.size))).astype(np.float32)
+    big = np.exp(rng.uniform(-64, 64, 200000) * np.float64(L32)).astype(np.float32)
+    r = np.concatenate([near, wide, (np.float64(1.2) ** np.arange(-3, 12)).astype(np.float32),
+                        far, big])
     qf = np.log(r) / L32
     fl = np.floor(qf)
     fast = (np.abs(qf) < 64) & (qf - fl > np.float32(1e-3)) & (qf - fl < np.float32(0.999))
