@@ -266,6 +266,12 @@ def main():
                          "nccl process group): exercises the multi-GPU gather path on one GPU")
     args = ap.parse_args()
 
+    # stdout carries exactly the one JSON line: everything else written to fd 1 (RCCL's
+    # version banner at communicator init, library prints) goes to stderr
+    sys.stdout.flush()
+    json_fd = os.dup(1)
+    os.dup2(2, 1)
+
     import torch
     import torch.distributed as dist
     from orb_slam2_test_amd import ORBextractor, sequence, synthetic
@@ -494,7 +500,7 @@ def main():
             out["cpu_baseline"] = cpu_baseline(frames, args.cpu_threads, n)
         else:
             out["cpu_baseline"] = None
-        print(json.dumps(out), flush=True)
+        os.write(json_fd, (json.dumps(out) + "\n").encode())
     if collective:
         dist.barrier()
         dist.destroy_process_group()

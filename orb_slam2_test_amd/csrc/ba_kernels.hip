@@ -189,6 +189,9 @@ int launch_ba_errors_packed(hipStream_t st, const orbg_pose *poses, const double
 // registers; the third row of a mono edge is zero (adding it adds exact zeros, so the fixed
 // 3-row loops give the same bits as the oracle's 2-row ones).
 // ---------------------------------------------------------------------------
+#ifndef ORBG_BA_JT_RCP
+#define ORBG_BA_JT_RCP 1  // pose Jacobian by reciprocals (0: g2o's divisions, round 4)
+#endif
 struct BaLin {
     double err[3], jp[3][3], jt[3][6], chi2, rho1, w, info;
     int D;
@@ -227,6 +230,33 @@ __device__ __forceinline__ void ba_linearize_edge(const orbg_pose &P, const doub
             L.jp[2][c] = L.jp[0][c] - e.bf * R[2][c] / z_2;
         }
     }
+#if ORBG_BA_JT_RCP
+    // the pose Jacobian by two reciprocals and products instead of g2o's twelve divisions:
+    // a few ulps from the divided form (tests hold it to 1e-9 relative of the oracle's; the
+    // error, the point Jacobian and with it the point blocks keep g2o's exact expressions)
+    const double iz = 1. / z, iz2 = 1. / z_2;
+    const double xiz = x * iz, yiz = y * iz, xiz2 = x * iz2, yiz2 = y * iz2, xy2 = x * y * iz2;
+    L.jt[0][0] = xy2 * fx;
+    L.jt[0][1] = -(1 + x * xiz2) * fx;
+    L.jt[0][2] = yiz * fx;
+    L.jt[0][3] = -iz * fx;
+    L.jt[0][4] = 0;
+    L.jt[0][5] = xiz2 * fx;
+    L.jt[1][0] = (1 + y * yiz2) * fy;
+    L.jt[1][1] = -xy2 * fy;
+    L.jt[1][2] = -xiz * fy;
+    L.jt[1][3] = 0;
+    L.jt[1][4] = -iz * fy;
+    L.jt[1][5] = yiz2 * fy;
+    if (e.stereo) {
+        L.jt[2][0] = L.jt[0][0] - e.bf * yiz2;
+        L.jt[2][1] = L.jt[0][1] + e.bf * xiz2;
+        L.jt[2][2] = L.jt[0][2];
+        L.jt[2][3] = L.jt[0][3];
+        L.jt[2][4] = 0;
+        L.jt[2][5] = L.jt[0][5] - e.bf * iz2;
+    } else {
+#else
     L.jt[0][0] = x * y / z_2 * fx;
     L.jt[0][1] = -(1 + (x * x / z_2)) * fx;
     L.jt[0][2] = y / z * fx;
@@ -247,6 +277,7 @@ __device__ __forceinline__ void ba_linearize_edge(const orbg_pose &P, const doub
         L.jt[2][4] = 0;
         L.jt[2][5] = L.jt[0][5] - e.bf / z_2;
     } else {
+#endif
 #pragma unroll
         for (int c = 0; c < 6; c++) L.jt[2][c] = 0;
     }
@@ -432,6 +463,112 @@ typedef double v4d __attribute__((ext_vector_type(4)));
 #endif
 #define BA_ROW 8     // doubles per staged pose row: J_pose (6), -e, w
 
+#ifndef ORBG_BA_MFMA4
+#define ORBG_BA_MFMA4 1  // v_mfma_f64_4x4x4f64 (0: round 4's v_mfma_f64_16x16x4f64)
+#endif
+
+#if ORBG_BA_MFMA4
+// v_mfma_f64_4x4x4f64: four independent 4x4 blocks, K = 4, one f64 per lane in each operand
+// (measured, tools/microbench/mfma_f64_rate.hip: A[b][i][k] at lane 16k + 4b + i,
+// B[b][k][j] at lane 16k + 4b + j, C[b][i][j] at lane 16i + 4b + j).  The 8x8 [H | b | 0]
+// tile is the four blocks: block b = 2I + J holds rows 4I + i, columns 4J + j, so 42 of
+// the 64 lane results are H_pp | b_p (round 4's 16x16 tile used 42 of 256).  It issues a
+// quarter of the 16x16x4 instruction's FLOPs at ~7x its rate (22 vs 154 cycles per
+// instruction and SIMD, profiles/r05a_mfma_f64.txt).
+typedef double BaAcc;
+#else
+typedef v4d BaAcc;
+#endif
+
+// every (row, column, value) of the slice accumulator a lane holds
+template <class F>
+__device__ __forceinline__ void ba_acc_entries(const BaAcc &C, int lane, F f)
+{
+#if ORBG_BA_MFMA4
+    const int i = lane >> 4, b = (lane >> 2) & 3, j = lane & 3;
+    f(4 * (b >> 1) + i, 4 * (b & 1) + j, C);
+#else
+    // D layout of v_mfma_f64_16x16x4f64 (measured): lane holds column j = lane % 16 of rows
+    // lane / 16 + 4 v, v = 0..3
+    const int j = lane & 15;
+#pragma unroll
+    for (int v = 0; v < 4; v++) f((lane >> 4) + 4 * v, j, C[v]);
+#endif
+}
+
+#if ORBG_BA_MFMA4
+// One 64-edge slice: lane l linearises edge l and stages its D nonzero pose rows (D = 2 mono,
+// 3 stereo, 0 inactive: no zero rows) at row offset sum_{l' < l} D_l', each row = J_pose row
+// (6), -e, w; rows up to the next multiple of 16 are zeroed.  Then
+//     C += sum_r (w_r v_r)^T v_r   (H_pp = C[0:6][0:6], b_p = C[0:6][6])
+// by v_mfma_f64_4x4x4f64, four independent accumulators (rows r0 + 4u + k, u = 0..3, added
+// in a fixed order at the end: deterministic, the dependent-MFMA latency hidden)
+template <class ES>
+__device__ __forceinline__ void ba_pose_slice(const orbg_pose &P, const double *__restrict__ points,
+                                              const ES &edges,
+                                              const int32_t *__restrict__ pose_edges, int e0,
+                                              int ne, double *rl, int lane, BaAcc &C)
+{
+    int nr16;
+    {
+        double v[3][BA_ROW];
+#pragma unroll
+        for (int k = 0; k < 3; k++)
+#pragma unroll
+            for (int c = 0; c < BA_ROW; c++) v[k][c] = 0;
+        int D = 0;
+        if (lane < ne) {
+            const orbg_edge e = edges(pose_edges[e0 + lane]);
+            if (e.active) {
+                const double X[3] = {points[3 * (size_t)e.point], points[3 * (size_t)e.point + 1],
+                                     points[3 * (size_t)e.point + 2]};
+                BaLin L;
+                ba_linearize_edge(P, X, e, L);
+                D = L.D;
+#pragma unroll
+                for (int k = 0; k < 3; k++) {
+#pragma unroll
+                    for (int c = 0; c < 6; c++) v[k][c] = L.jt[k][c];
+                    v[k][6] = -L.err[k];
+                    v[k][7] = L.w;
+                }
+            }
+        }
+        const unsigned long long m2 = __ballot(D >= 2), m3 = __ballot(D == 3);
+        const int off =
+            2 * __builtin_amdgcn_mbcnt_hi((uint32_t)(m2 >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m2, 0)) +
+            __builtin_amdgcn_mbcnt_hi((uint32_t)(m3 >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m3, 0));
+        const int nrow = 2 * __popcll(m2) + __popcll(m3);
+        nr16 = (nrow + 15) & ~15;
+        wave_sync_lds_ba();  // the previous slice's reads of rl are done (in-order LDS)
+#pragma unroll
+        for (int k = 0; k < 3; k++)
+            if (k < D)
+#pragma unroll
+                for (int c = 0; c < BA_ROW; c += 2)
+                    *(double2 *)(rl + (off + k) * BA_ROW + c) = make_double2(v[k][c], v[k][c + 1]);
+        if (nrow + lane < nr16)
+#pragma unroll
+            for (int c = 0; c < BA_ROW; c += 2)
+                *(double2 *)(rl + (nrow + lane) * BA_ROW + c) = make_double2(0.0, 0.0);
+    }
+    wave_sync_lds_ba();
+    const int k = lane >> 4, b = (lane >> 2) & 3, t = lane & 3;
+    const int ia = 4 * (b >> 1) + t, ib = 4 * (b & 1) + t;  // column 7 is the weight slot: 0
+    double c4[4] = {0, 0, 0, 0};
+    for (int r0 = 0; r0 < nr16; r0 += 16) {
+#pragma unroll
+        for (int u = 0; u < 4; u++) {
+            const double *row = rl + (r0 + 4 * u + k) * BA_ROW;
+            const double w = row[7];
+            const double va = ia < 7 ? row[ia] : 0.0;
+            const double vb = ib < 7 ? row[ib] : 0.0;
+            c4[u] = __builtin_amdgcn_mfma_f64_4x4x4f64(va * w, vb, c4[u], 0, 0, 0);
+        }
+    }
+    C += (c4[0] + c4[1]) + (c4[2] + c4[3]);
+}
+#else
 // One 64-edge slice into LDS rows (lane l: edge l -> rows 3l .. 3l+2: J_pose row, -e, w; zero
 // rows for the third row of a mono edge and for inactive edges or lanes past the slice), then
 // C += sum_r (w_r v_r)^T v_r by v_mfma_f64_16x16x4f64 (A[i][k] = w v[i], B[k][j] = v[j], 7
@@ -440,7 +577,7 @@ template <class ES>
 __device__ __forceinline__ void ba_pose_slice(const orbg_pose &P, const double *__restrict__ points,
                                               const ES &edges,
                                               const int32_t *__restrict__ pose_edges, int e0,
-                                              int ne, double *rl, int lane, v4d &C)
+                                              int ne, double *rl, int lane, BaAcc &C)
 {
     {
         double v[3][BA_ROW];
@@ -490,6 +627,7 @@ __device__ __forceinline__ void ba_pose_slice(const orbg_pose &P, const double *
         for (int u = 0; u < 4; u++) C = __builtin_amdgcn_mfma_f64_16x16x4f64(va[u], vb[u], C, 0, 0, 0);
     }
 }
+#endif
 
 // record path: one wave per slice, the slices of one pose added by fp64 atomics onto the
 // zeroed blocks.  Fixed poses get no block (g2o skips them).
@@ -515,18 +653,13 @@ __global__ __launch_bounds__(256) void k_ba_pose_mfma(const orbg_pose *__restric
     double *H = hpose + 36 * (size_t)p, *bv = bpose + 6 * (size_t)p;
     const int e0p = pose_off[p], nep = pose_off[p + 1] - e0p;
     const int ks = sl - slice_off[p];
-    v4d C = {0, 0, 0, 0};
+    BaAcc C = {};
     ba_pose_slice(P, points, edges, pose_edges, e0p + ks * BA_SLICE,
                   min(BA_SLICE, nep - ks * BA_SLICE), rows_lds[wv], lane, C);
-    // D layout of v_mfma_f64_16x16x4f64 (measured): lane holds column j = lane % 16 of rows
-    // lane / 16 + 4 v, v = 0..3
-    const int j = lane & 15;
-#pragma unroll
-    for (int v = 0; v < 4; v++) {
-        const int row = (lane >> 4) + 4 * v;
-        if (row < 6 && j < 6) atomicAdd(&H[row * 6 + j], C[v]);
-        if (row < 6 && j == 6) atomicAdd(&bv[row], C[v]);
-    }
+    ba_acc_entries(C, lane, [&](int row, int col, double val) {
+        if (row < 6 && col < 6) atomicAdd(&H[row * 6 + col], val);
+        if (row < 6 && col == 6) atomicAdd(&bv[row], val);
+    });
 }
 
 // graph path, pass 1: one wave per slice (the graph's slice tables, built once), the
@@ -545,15 +678,12 @@ __device__ __forceinline__ void ba_slice_part(const orbg_pose *__restrict__ pose
     if (P.fixed) return;  // pass 2 writes the zero block
     const int e0p = pose_off[p], nep = pose_off[p + 1] - e0p;
     const int ks = sl - slice_off[p];
-    v4d C = {0, 0, 0, 0};
+    BaAcc C = {};
     ba_pose_slice(P, points, edges, pose_edges, e0p + ks * BA_SLICE,
                   min(BA_SLICE, nep - ks * BA_SLICE), rows, lane, C);
-    const int j = lane & 15;
-#pragma unroll
-    for (int v = 0; v < 4; v++) {
-        const int row = (lane >> 4) + 4 * v;
-        if (row < 6 && j < 7) part[42 * (size_t)sl + row * 7 + j] = C[v];
-    }
+    ba_acc_entries(C, lane, [&](int row, int col, double val) {
+        if (row < 6 && col < 7) part[42 * (size_t)sl + row * 7 + col] = val;
+    });
 }
 
 // graph path, pass 2: thread per (pose, block entry): the slice partials summed in slice order
@@ -664,7 +794,7 @@ __global__ __launch_bounds__(256) void k_ba_slices_special(
     const int p = (int)blockIdx.x - nb_special;
     if (p >= npose) return;  // workgroup-uniform
     const orbg_pose P = poses[p];
-    v4d C = {0, 0, 0, 0};
+    BaAcc C = {};
     if (!P.fixed) {
         const int e0p = pose_off[p], nep = pose_off[p + 1] - e0p;
         const int ns = (nep + BA_SLICE - 1) / BA_SLICE;
@@ -672,12 +802,9 @@ __global__ __launch_bounds__(256) void k_ba_slices_special(
             ba_pose_slice(P, points, edges, pose_edges, e0p + ks * BA_SLICE,
                           min(BA_SLICE, nep - ks * BA_SLICE), rows_lds[wv], lane, C);
     }
-    const int j = lane & 15;
-#pragma unroll
-    for (int v = 0; v < 4; v++) {
-        const int row = (lane >> 4) + 4 * v;
-        if (row < 6 && j < 7) tiles[wv][row * 7 + j] = C[v];
-    }
+    ba_acc_entries(C, lane, [&](int row, int col, double val) {
+        if (row < 6 && col < 7) tiles[wv][row * 7 + col] = val;
+    });
     __syncthreads();
     if (threadIdx.x < 42) {
         const int e = threadIdx.x;

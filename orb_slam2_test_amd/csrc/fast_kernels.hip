@@ -43,6 +43,12 @@ namespace orbg {
 #ifndef ORBG_FC2_IL
 #define ORBG_FC2_IL 1  // score rows interleaved with the tile rows (row stride 2P; 0: apart, +0.6% per step)
 #endif
+#ifndef ORBG_FC2_DBG
+#define ORBG_FC2_DBG 0  // 1: the phase-stop checks in a product build (round-4 register layout: 65 VGPRs, 7 waves/SIMD)
+#endif
+#ifndef ORBG_FC2_LATE_PC
+#define ORBG_FC2_LATE_PC 1  // path codes loaded after the scoring: 64 VGPRs, 8 waves/SIMD (0: at the cell start)
+#endif
 #ifndef FC2_CPW
 #define FC2_CPW 2  // consecutive cells per wave (shared halo lines in L1, fewer workgroups)
 #endif
@@ -146,7 +152,12 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(FC2_WPE, 8)
 
     // launch constants read once (scalar loads after the LDS fences would wait on the LDS
     // queue too: both count in lgkmcnt)
-    const int dbg = g->dbg, thi = g->ini_th, tlo = g->min_th;
+#if defined(ORBG_DEV_KNOBS) || ORBG_FC2_DBG
+    const int dbg = g->dbg;  // developer phase stops (tools/fast_phase.sh)
+#else
+    constexpr int dbg = 0;   // product build: no phase-stop checks (their masks cost registers)
+#endif
+    const int thi = g->ini_th, tlo = g->min_th;
     const int lcap = g->fc2_list_cap;  // pretest list entries (2 per unit of the largest cell)
     const int ncells = g->ncells, cell_cap = g->cell_cap;
 #pragma unroll 1
@@ -156,9 +167,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(FC2_WPE, 8)
     const Fc2Cell cur = decode(cid);
     const int f = cur.f, c = cur.c, RW = cur.RW, RH = cur.RH, RG = cur.RG, nunits = cur.nunits;
     const int xo = cur.xo, yo = cur.yo;
-    // quadtree path codes of the cell's columns / rows (one per lane), issued early
+#if !ORBG_FC2_LATE_PC
     uint32_t xs_l = lane < RW ? ctab[cur.xs + lane] : 0u;
     uint32_t ys_l = lane < RH ? ctab[cur.ys + lane] : 0u;
+#endif
     // ---- window -> tA: all of a lane's chunk loads in flight before the first store
     // (the previous cell's reads of the tiles are done: a wave's LDS ops complete in order) ----
     wave_sync_lds();
@@ -346,6 +358,12 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(FC2_WPE, 8)
         if (valid < 4) kb &= (1u << valid) - 1u;
         return kb;
     };
+    // quadtree path codes of the cell's columns / rows (one per lane): loaded after the
+    // scoring (not live through its register peak), in flight during the corner-unit pass
+#if ORBG_FC2_LATE_PC
+    uint32_t xs_l = lane < RW ? ctab[cur.xs + lane] : 0u;
+    uint32_t ys_l = lane < RH ? ctab[cur.ys + lane] : 0u;
+#endif
     const int64_t slot = (int64_t)f * ncells + c;
     uint2 *out = cell_kp + slot * cell_cap;
     const __amdgpu_buffer_rsrc_t orsrc =

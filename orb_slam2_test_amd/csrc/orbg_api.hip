@@ -513,7 +513,7 @@ static void free_plan(orbg_ctx *c)
                     c->cnt_slot[0], c->cnt_slot[1], c->ckp_slot[0], c->ckp_slot[1], c->d_keys, c->d_knode, c->d_act, c->d_qk,
                     c->d_nodes, c->d_lvl_kp, c->d_lvl_idx, c->d_lvl_cnt, c->kps_slot[0], c->kps_slot[1],
                     c->desc_slot[0], c->desc_slot[1], c->counts_slot[0], c->counts_slot[1],
-                    c->d_err, c->d_knn, c->d_m12, c->d_nm, c->d_topk, c->d_topk_n, c->d_pairs,
+                    c->d_knn, c->d_m12, c->d_nm, c->d_topk, c->d_topk_n, c->d_pairs,
                     c->d_spairs, c->d_uright, c->d_depth, c->d_snvalid, c->d_sscr,
                     c->d_ptab, c->d_ytab4, c->d_bands};
     for (void *q : ptrs)
@@ -553,7 +553,6 @@ static void free_plan(orbg_ctx *c)
         c->desc_slot[i] = nullptr;
         c->counts_slot[i] = nullptr;
     }
-    c->d_err = nullptr;
     c->d_knn = c->d_m12 = c->d_nm = nullptr;
     c->d_topk = nullptr;
     c->d_topk_n = nullptr;
@@ -1169,16 +1168,9 @@ static int plan(orbg_ctx *c, int w, int h, int batch)
         (rc = dalloc(&c->kps_slot[1], B * G.frame_cap)) ||
         (rc = dalloc(&c->desc_slot[0], B * G.frame_cap * 32)) ||
         (rc = dalloc(&c->desc_slot[1], B * G.frame_cap * 32)) ||
-        (rc = dalloc(&c->counts_slot[0], B)) || (rc = dalloc(&c->counts_slot[1], B)) ||
-        (rc = dalloc(&c->d_err, 2))) {
+        (rc = dalloc(&c->counts_slot[0], B)) || (rc = dalloc(&c->counts_slot[1], B))) {
         free_plan(c);
         return rc;
-    }
-    {
-        // sticky device error word {flags, first failing frame}: OR of every batch since it
-        // was last read (check_err), so a pipelined caller cannot lose an overflow
-        const int32_t e0[2] = {0, INT32_MAX};
-        HIPCHK(hipMemcpy(c->d_err, e0, sizeof(e0), hipMemcpyHostToDevice));
     }
     // resize tables are referenced by offset: fix up pointers through offsets at launch
     HIPCHK(hipMemcpy(c->d_geom, &G, sizeof(G), hipMemcpyHostToDevice));
@@ -1293,6 +1285,20 @@ extern "C" int orbg_create(int device, const orbg_params *p, orbg_ctx **out)
         return set_err(ORBG_EIO, "hipStreamCreate failed");
     }
     c->stream = c->own_stream;
+    // sticky device error word {flags, first failing frame / pair}: OR of every launch since
+    // it was last read (check_err), so a pipelined caller cannot lose an overflow.  It lives
+    // as long as the context (a new extraction plan keeps pending flags), and every kernel
+    // that may raise a flag -- the quadtree's and the device matchers' -- can write it.
+    {
+        const int32_t e0[2] = {0, INT32_MAX};
+        if (hipMalloc(&c->d_err, sizeof(e0)) != hipSuccess ||
+            hipMemcpy(c->d_err, e0, sizeof(e0), hipMemcpyHostToDevice) != hipSuccess) {
+            if (c->d_err) hipFree(c->d_err);
+            hipStreamDestroy(c->own_stream);
+            delete c;
+            return set_err(ORBG_ENOMEM, "device error word");
+        }
+    }
     // The matching streams run at low priority: a stream of another priority gets its own
     // hardware queue (at normal priority it can share one with the caller's stream and then
     // runs strictly after it), and the dispatcher hands the matching kernels the slots the
@@ -1400,6 +1406,7 @@ extern "C" void orbg_destroy(orbg_ctx *c)
     if (c->d_scr) hipFree(c->d_scr);
     if (c->d_trk) hipFree(c->d_trk);
     if (c->d_sim3) hipFree(c->d_sim3);
+    if (c->d_err) hipFree(c->d_err);
     if (c->d_mpose) hipFree(c->d_mpose);
     if (c->d_kps_un) hipFree(c->d_kps_un);
     if (c->aux_stream) hipStreamSynchronize(c->aux_stream);
@@ -1779,6 +1786,16 @@ static int sync_all(orbg_ctx *c)
     return ORBG_OK;
 }
 
+// the error a non-zero device error word maps to (check_err, orbg_download_frame)
+static int err_from_flags(int32_t flags, int32_t first)
+{
+    if (flags & ORBG_DEVFLAG_COUNT)
+        return set_err(ORBG_EINVAL, "a device matcher count exceeded its capacity (clamped; "
+                                    "flags 0x%x, first pair %d since the last check)", flags, first);
+    return set_err(ORBG_ENOTSUP, "quadtree capacity exceeded (flags 0x%x, first frame %d of "
+                                 "a batch since the last check)", flags, first);
+}
+
 // Drains every stream, then reads and clears the sticky device error word: a non-zero flag
 // means some frame since the last read lost a level (quadtree capacity exceeded) and its
 // keypoints are incomplete, so the caller gets ORBG_ENOTSUP instead of short outputs; or
@@ -1789,17 +1806,12 @@ static int check_err(orbg_ctx *c)
     int rc = sync_all(c);
     if (rc) return rc;
     c->prof.collect();
-    if (!c->d_err) return ORBG_OK;
     int32_t e[2] = {0, 0};
     HIPCHK(hipMemcpy(e, c->d_err, sizeof(e), hipMemcpyDeviceToHost));
     if (e[0]) {
         const int32_t e0[2] = {0, INT32_MAX};
         HIPCHK(hipMemcpy(c->d_err, e0, sizeof(e0), hipMemcpyHostToDevice));
-        if (e[0] & ORBG_DEVFLAG_COUNT)
-            return set_err(ORBG_EINVAL, "a device matcher count exceeded its capacity (clamped; "
-                                        "flags 0x%x, first pair %d since the last check)", e[0], e[1]);
-        return set_err(ORBG_ENOTSUP, "quadtree capacity exceeded (flags 0x%x, first frame %d of "
-                                     "a batch since the last check)", e[0], e[1]);
+        return err_from_flags(e[0], e[1]);
     }
     return ORBG_OK;
 }
@@ -1885,8 +1897,7 @@ extern "C" int orbg_download_frame(orbg_ctx *c, int frame, orbg_keypoint *kps, u
     if (hdr[0]) {  // check_err's reset and error
         const int32_t e0[2] = {0, INT32_MAX};
         HIPCHK(hipMemcpy(c->d_err, e0, sizeof(e0), hipMemcpyHostToDevice));
-        return set_err(ORBG_ENOTSUP, "quadtree capacity exceeded (flags 0x%x, first frame %d of "
-                                     "a batch since the last check)", hdr[0], hdr[1]);
+        return err_from_flags(hdr[0], hdr[1]);
     }
     const int32_t n = hdr[2];
     if (n_out) *n_out = n;

@@ -42,7 +42,33 @@ def local_indices(nframes, lo, hi):
     return np.concatenate([[(lo - 1) % nframes], np.arange(lo, hi)]).astype(np.int64)
 
 
-def gather_rows(local, world, group=None, sizes=None, force=False):
+class PendingGather:
+    """An all_gather in flight (async_op=True) on the process group's own stream: the stream
+    that issued it does not wait for it, so the next step's kernels on that stream are not
+    held behind the collective.  result() orders the current stream after the collective and
+    returns the rows in rank order (cast back to `dtype` when they travelled narrowed)."""
+
+    def __init__(self, work, out, sizes, dtype=None, wire_view=None):
+        self.work, self.out, self.sizes, self.dtype = work, out, sizes, dtype
+        self.wire_view = wire_view
+        self._res = None
+
+    def result(self):
+        import torch
+        if self._res is None:
+            if self.work is not None:
+                self.work.wait()
+                self.work = None
+            r = torch.cat([o[:n] for o, n in zip(self.out, self.sizes)], dim=0)
+            if self.wire_view is not None:  # bytes on the wire -> the narrowed dtype
+                r = r.view(self.wire_view)
+            self._res = r if self.dtype is None else r.to(self.dtype)
+            self.out = None
+        return self._res
+
+
+def gather_rows(local, world, group=None, sizes=None, force=False, async_op=False,
+                wire_dtype=None):
     """all_gather a per-rank tensor whose dim 0 holds m_r frames into the global tensor, in
     rank (= frame) order.  Ranks may hold different m_r, so blocks are padded to the largest
     before the collective.  Pass `sizes` (every rank's m_r) when known to skip the size
@@ -52,18 +78,28 @@ def gather_rows(local, world, group=None, sizes=None, force=False):
     import torch
     import torch.distributed as dist
     if world == 1 and not force:
-        return local
+        return PendingGather(None, [local], [local.shape[0]]) if async_op else local
     if sizes is None:
         m = torch.tensor([local.shape[0]], dtype=torch.int64, device=local.device)
         st = [torch.zeros_like(m) for _ in range(world)]
         dist.all_gather(st, m, group=group)
         sizes = [int(t.item()) for t in st]
     mx = max(sizes)
-    pad = torch.zeros((mx,) + tuple(local.shape[1:]), dtype=local.dtype, device=local.device)
-    pad[:local.shape[0]] = local
-    out = [torch.zeros_like(pad) for _ in range(world)]
-    dist.all_gather(out, pad, group=group)
-    return torch.cat([o[:n] for o, n in zip(out, sizes)], dim=0)
+    wd = local.dtype if wire_dtype is None else wire_dtype
+    if mx == local.shape[0]:  # the common case (bench.py's fixed batch): one copy / cast
+        pad = local.to(wd, copy=True)
+    else:
+        pad = torch.zeros((mx,) + tuple(local.shape[1:]), dtype=wd, device=local.device)
+        pad[:local.shape[0]] = local
+    # RCCL has no 16-bit integer collectives: a narrowed tensor travels as its bytes
+    view = wd if wd in (torch.int16, torch.uint16) else None
+    if view is not None:
+        pad = pad.view(torch.uint8)
+    out = [torch.empty_like(pad) for _ in range(world)]
+    work = dist.all_gather(out, pad, group=group, async_op=async_op)
+    res = PendingGather(work if async_op else None, out, sizes,
+                        None if wd == local.dtype else local.dtype, view)
+    return res if async_op else res.result()
 
 
 def gather_summary(local, world, group=None, sizes=None, force=False):
@@ -72,6 +108,16 @@ def gather_summary(local, world, group=None, sizes=None, force=False):
     if world == 1 and not force:
         return local
     return gather_rows(local.t().contiguous(), world, group, sizes, force).t().contiguous()
+
+
+class _PendingT:
+    """A PendingGather of a transposed [2, m] summary, transposed back on result()."""
+
+    def __init__(self, p):
+        self.p = p
+
+    def result(self):
+        return self.p.result().t().contiguous()
 
 
 def run_sharded(frames, world, rank, backend, group=None, device="cpu", with_matches=False,
@@ -252,6 +298,12 @@ class BenchStep:
         self.with_pose = with_pose and mode == "mono"
         self.group = group
         self.collective = world > 1 if collective is None else bool(collective)
+        # the gathers run async on the process group's stream (the match stream does not wait
+        # for them) and the vnMatches12 rows travel as int16 (indices < frame_cap <= 32767):
+        # ORBG_GATHER=sync32 restores round 4's blocking int32 gathers (A/B)
+        import os
+        self.gather_async = os.environ.get("ORBG_GATHER", "async16") != "sync32"
+        self._pending = None
         if self.with_pose:
             self.dq = torch.zeros((B, 4), dtype=torch.float64, device="cuda")
             self.dt = torch.zeros((B, 3), dtype=torch.float64, device="cuda")
@@ -259,7 +311,30 @@ class BenchStep:
         self.pose = None
         self.mstream = torch.cuda.ExternalStream(ext.ctx.match_stream())
         self.capture = None
-        self.gathered = None
+        self._gathered = None
+
+    @property
+    def gathered(self):
+        """The last step's gathered outputs (stereo: the [2, N] summary; mono: (summary,
+        vnMatches12 rows[, pose rows])), waiting for the collectives if they are in flight."""
+        import torch
+        if self._pending is not None:
+            with torch.cuda.stream(self.mstream):
+                g = tuple(x.result() for x in self._pending)
+            self._gathered = g[0] if self.mode == "stereo" else g
+            self._pending = None
+        return self._gathered
+
+    def _gather_rows(self, t, wire_dtype=None):
+        sizes = [self.B] * self.world
+        if not self.gather_async:
+            g = gather_rows(t, self.world, self.group, sizes=sizes, force=True)
+            return PendingGather(None, [g], [g.shape[0]])
+        return gather_rows(t, self.world, self.group, sizes=sizes, force=True, async_op=True,
+                           wire_dtype=wire_dtype)
+
+    def _gather_summary(self, t):
+        return _PendingT(self._gather_rows(t.t().contiguous()))
 
     def __call__(self, d_frames_ptr, w, h):
         import torch
@@ -270,8 +345,7 @@ class BenchStep:
             ext.ctx.stereo_summary(self.ssum.data_ptr())
             if self.collective:  # per-frame (keypoints, depths) of every rank
                 with torch.cuda.stream(self.mstream):
-                    self.gathered = gather_summary(self.ssum.view(2, B), self.world, self.group,
-                                                   sizes=[B] * self.world, force=True)
+                    self._pending = (self._gather_summary(self.ssum.view(2, B)),)
         elif self.mode == "mono":
             ext.match_batch_device(self.f1, self.f2, self.window, self.nnratio, self.check_ori)
             ext.ctx.batch_summary(self.summary.data_ptr())
@@ -286,14 +360,12 @@ class BenchStep:
                     self.pose = torch.cat([self.dq, self.dt, self.dn.double()[:, None]], 1)
             if self.collective:
                 with torch.cuda.stream(self.mstream):
-                    sizes = [B] * self.world
                     local = torch.stack([self.summary[1:B + 1], self.summary[B + 1:]])
-                    g = [gather_summary(local, self.world, self.group, sizes=sizes, force=True),
-                         gather_rows(self.m12, self.world, self.group, sizes=sizes, force=True)]
+                    g = [self._gather_summary(local),
+                         self._gather_rows(self.m12, wire_dtype=torch.int16)]
                     if self.with_pose:
-                        g.append(gather_rows(self.pose, self.world, self.group, sizes=sizes,
-                                             force=True))
-                    self.gathered = tuple(g)
+                        g.append(self._gather_rows(self.pose))
+                    self._pending = tuple(g)
         if self.capture is not None:
             ext.ctx.batch_acquire(self.mstream.cuda_stream)
             with torch.cuda.stream(self.mstream):

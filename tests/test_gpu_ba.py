@@ -327,3 +327,39 @@ def test_ba_errors_per_trial_pass(oracle):
     eo, *_ = linearize_local_ba(poses, pts, edges)
     act = edges["active"] != 0
     assert np.array_equal(eo["chi2"][act], g[1][act]) and np.array_equal(eo["err"][act], g[0][act])
+
+
+def test_graph_bench_shaped_windows(oracle):
+    """The bench's workload at full window size (tools/ba_bench.py, configs[4]): 4 KITTI-like
+    windows of 20 KeyFrames (10 fixed), 6000 points, ~27k edges each, 60% stereo, 10%
+    outliers under Huber, as one orbg_ba_graph.  Build (k_ba_edges, the MFMA f64 4x4x4 pose
+    slices, the pose reduce) + error pass vs the oracle on the same graph: chi2 / rho and the
+    point blocks bit for bit, H_pl and the pose blocks to RTOL; a second build is
+    bit-identical (deterministic sums)."""
+    from orb_slam2_test_amd.optimizer import DeviceLBA
+    poses, pts, edges = concat_windows([S.ba_window(seed=500 + i) for i in range(4)])
+    assert len(edges) > 100000 and len(pts) == 24000
+    g = DeviceLBA(poses, pts, edges, graph=True)
+
+    def run():
+        g.build_system()
+        g.errors()
+        g.ctx.sync()
+        return [t.cpu().numpy() for t in (g.d_hpl, g.d_hpose, g.d_bpose, g.d_hpoint,
+                                          g.d_bpoint, g.d_chi2, g.d_rho0)]
+
+    r1 = run()
+    reo, rhp, rbp, rhq, rbq = oracle.ba_linearize(poses, pts, edges)
+    ne, npo, npt = len(edges), len(poses), len(pts)
+    assert rel(r1[0][:ne].reshape(ne, -1), reo["hpl"].reshape(ne, -1)) < RTOL
+    assert rel(r1[1].reshape(-1)[:36 * npo], rhp.reshape(-1)) < RTOL
+    assert rel(r1[2].reshape(-1)[:6 * npo], rbp.reshape(-1)) < RTOL
+    assert np.array_equal(r1[3].reshape(-1)[:9 * npt], rhq.reshape(-1))
+    assert np.array_equal(r1[4].reshape(-1)[:3 * npt], rbq.reshape(-1))
+    r = oracle.ba_errors(poses, pts, edges)
+    assert np.array_equal(r1[5][:ne], r[1]) and np.array_equal(r1[6][:ne], r[2])
+    fixed = poses["fixed"] != 0
+    assert fixed.sum() == 40 and not r1[1][fixed].any()
+    r2 = run()
+    for u, v in zip(r1, r2):
+        assert np.array_equal(u, v)

@@ -28,7 +28,7 @@ sys.path.insert(0, ROOT)
 HBM_PEAK_GBS = 8000.0
 EDGE_ALGO_BYTES = 108  # per-edge algorithmic bytes
 F64_MFMA_PEAK_TFLOPS = 78.6  # MI355X FP64 matrix, AMD spec (the guide lists no FP64 row)
-PMC_BA = "r03f_ba_pmc_kernels.json"  # tools/profile.sh <tag> tools/ba_bench.py
+PMC_BA = "r05_ba_pmc_kernels.json"  # tools/profile.sh <tag> tools/ba_bench.py (round 5 build)
 
 
 def main():
@@ -140,24 +140,37 @@ def main():
             out["roofline"]["traffic_over_abi_min"] = round(tr / out["roofline"]["abi_min_bytes_per_launch"], 3)
         out["roofline"]["pmc_source"] = os.path.relpath(pmc, ROOT) if pk else None
     if "ba_pose_mfma" in kern:
-        # MFMAs issued: per slice of <= 64 edges of a free pose, 4 per 16 rows (3 per edge)
-        nmfma = 0
+        # MFMAs issued by the pose-slice pass (csrc/ba_kernels.hip ba_pose_slice): per slice of
+        # <= 64 edges of a free pose, the active edges' nonzero rows (2 mono, 3 stereo)
+        # compacted and padded to a multiple of 16, one v_mfma_f64_4x4x4f64 per 4 rows
+        # (4 blocks x 4x4 x K 4 = 512 FLOP).  Useful work: the 6 x 7 entries of [H_pp | b_p]
+        # of the 8 x 8 tile (42 / 64) over the rows that are not padding.
+        nmfma, rows_used = 0, 0
         fixed = poses["fixed"] != 0
-        cnt = np.bincount(edges["pose"], minlength=len(poses))
+        order = np.argsort(edges["pose"], kind="stable")
+        D = np.where(edges["active"] != 0, np.where(edges["stereo"] != 0, 3, 2), 0)[order]
+        pe = edges["pose"][order]
+        starts = np.searchsorted(pe, np.arange(len(poses) + 1))
         for pidx in np.nonzero(~fixed)[0]:
-            n = int(cnt[pidx])
-            for s0 in range(0, n, 64):
-                nmfma += 4 * ((3 * min(64, n - s0) + 15) // 16)
+            a, b = starts[pidx], starts[pidx + 1]
+            for s0 in range(a, b, 64):
+                nr = int(D[s0:min(b, s0 + 64)].sum())
+                nmfma += ((nr + 15) // 16) * 4
+                rows_used += nr
         ms = kern["ba_pose_mfma"][0] / max(kern["ba_pose_mfma"][1], 1)
-        tf = nmfma * 16 * 16 * 4 * 2 / (ms * 1e-3) / 1e12
-        out["mfma"] = {"kernel": "ba_pose_mfma", "instr": "v_mfma_f64_16x16x4f64",
-                       "mfma_per_launch": nmfma, "issued_tflops": round(tf, 2),
-                       "peak_tflops": F64_MFMA_PEAK_TFLOPS,
+        tf = nmfma * 512 / (ms * 1e-3) / 1e12
+        useful = (42.0 / 64.0) * rows_used / max(4 * nmfma, 1)
+        out["mfma"] = {"kernel": "ba_pose_mfma (k_ba_slices_special)",
+                       "instr": "v_mfma_f64_4x4x4f64", "mfma_per_launch": nmfma,
+                       "issued_tflops": round(tf, 2), "peak_tflops": F64_MFMA_PEAK_TFLOPS,
                        "issued_frac": round(tf / F64_MFMA_PEAK_TFLOPS, 4),
+                       "useful_work_frac": round(useful, 4),
+                       "useful_tflops": round(tf * useful, 2),
                        "mfma_frac": pk.get("ba_pose_mfma", {}).get("mfma_frac"),
-                       "note": "issued = every MFMA the kernel issues (7x7 of each 16x16 tile is "
-                               "used); mfma_frac = SQ_VALU_MFMA_BUSY_CYCLES / (1024 SIMDs x "
-                               "GPU cycles) from the committed PMC pass"}
+                       "note": "issued = every MFMA the pass issues; useful = the [H_pp | b_p] "
+                               "entries (42 of the 8x8 tile's 64) x the rows that are not "
+                               "padding; mfma_frac = SQ_VALU_MFMA_BUSY_CYCLES / (1024 SIMDs x "
+                               "GPU cycles) from the committed PMC pass (pmc_source)"}
     if not args.no_cpu:
         from oracle import pyoracle as O
         p, q, e = base[0]

@@ -7,6 +7,8 @@ KEYS = {
     "k_stereo_match": "stereo_match", "k_stereo_sad": "stereo_sad",
     "k_stereo_median": "stereo_median", "k_ba_edges": "ba_edges",
     "k_ba_point_blocks": "ba_point_blocks", "k_ba_pose_mfma": "ba_pose_mfma",
+    "k_ba_slices_special": "ba_pose_mfma", "k_ba_pose_reduce": "ba_pose_reduce",
+    "k_ba_errors": "ba_errors",
 }
 
 
