@@ -800,6 +800,23 @@ int orbg_ba_graph_build_system(orbg_ctx *ctx, orbg_ba_graph *graph, const orbg_p
 int orbg_ba_graph_errors(orbg_ctx *ctx, orbg_ba_graph *graph, const orbg_pose *d_poses,
                          const double *d_points, double *d_err, double *d_chi2, double *d_rho0,
                          uint8_t *d_depth_ok);
+/* g2o's BlockSolver<6,3>::solve over an orbg_ba_graph, device-resident (Thirdparty/g2o/g2o/
+ * core/block_solver.hpp:354-486 after setLambda, optimization_algorithm_levenberg.cpp:61-164):
+ * orbg_ba_graph_schur_plan builds the Schur structure once -- free poses (`fixed`: host
+ * [npose], g2o's vertex->fixed(), Optimizer.cc:714,729), the pose-pair lists of every shared
+ * landmark in landmark order, the independent dense systems (one per LBA window of the
+ * graph) -- and uploads it; orbg_ba_graph_set_active rebuilds it for the new active set.
+ * orbg_ba_graph_schur_solve then reads the graph build's device blocks (d_hpl [nedge][3][6],
+ * H_pp / b_p, H_ll / b_l) and writes the increments d_dx_pose [npose][6] (0 for fixed poses),
+ * d_dx_point [npoint][3] and *d_ok (0: a zero / non-finite LDLT pivot, increments 0), in
+ * stream order on the context stream with no host copy: build -> errors -> solve -> update
+ * is one stream.  The Schur products run on v_mfma_f64_4x4x4f64; every sum in the order
+ * oracle/ba_oracle.c orc_ba_schur_solve pins (bit-identical). */
+int orbg_ba_graph_schur_plan(orbg_ctx *ctx, orbg_ba_graph *graph, const uint8_t *fixed);
+int orbg_ba_graph_schur_solve(orbg_ctx *ctx, orbg_ba_graph *graph, double lambda,
+                              const double *d_hpl, const double *d_hpose, const double *d_bpose,
+                              const double *d_hpoint, const double *d_bpoint, double *d_dx_pose,
+                              double *d_dx_point, int32_t *d_ok);
 
 /* g2o's per-trial error pass for the two LBA edge types: SparseOptimizer::
  * computeActiveErrors (Thirdparty/g2o/g2o/core/sparse_optimizer.cpp:61-76, computeError

@@ -388,13 +388,27 @@ int orc_ldlt_dense_solve(double *A, int n, double *x)
     }
     for (int i = 0; i < n; i++)
         x[i] /= A[i * n + i];
-    for (int i = n - 1; i >= 0; i--) { /* L^T x = y */
-        double s = x[i];
-        for (int k = i + 1; k < n; k++)
-            s -= A[k * n + i] * x[k];
-        x[i] = s;
-    }
+    /* L^T x = y, column by column (k descending): element i subtracts L_ki x_k for
+     * k = n-1 down to i+1, so each finished x_k updates every lower row at once (the GPU's
+     * k_schur_ldlt runs one k per step over all rows) */
+    for (int k = n - 1; k >= 0; k--)
+        for (int i = 0; i < k; i++)
+            x[i] -= A[k * n + i] * x[k];
     return 1;
+}
+
+/* the GPU block workgroup's chain combine: a pairwise tree over 16 chains */
+#define SCHUR_CHAINS 16
+static double schur_tree16(const double v[16])
+{
+    double a[8], b[4], c[2];
+    for (int i = 0; i < 8; i++)
+        a[i] = v[2 * i] + v[2 * i + 1];
+    for (int i = 0; i < 4; i++)
+        b[i] = a[2 * i] + a[2 * i + 1];
+    for (int i = 0; i < 2; i++)
+        c[i] = b[2 * i] + b[2 * i + 1];
+    return c[0] + c[1];
 }
 
 int orc_ba_schur_solve(const orc_pose *poses, int npose, int npoint, const orc_edge *edges,
@@ -431,10 +445,22 @@ int orc_ba_schur_solve(const orc_pose *poses, int npose, int npoint, const orc_e
             lst[b + 1] = v;
         }
     const int n = 6 * nfree;
-    double *S = (double *)calloc((size_t)n * n + 1, sizeof(double));
+    /* S accumulates in SCHUR_CHAINS = 16 chains per block (the block's landmark pairs in
+     * landmark order, pair t into chain t % 16), each chain a v_mfma_f64_4x4x4f64 accumulator
+     * (one wave of the GPU's block workgroup): per pair the 3 (+1 zero pad) products fused
+     * into the chain in k order, c = fma(-BD[r][k], h2[k][c], c), the instruction's measured
+     * arithmetic (tools/microbench/mfma_f64_pin.hip: 1,280,000 of 1,280,000 lanes bit-equal
+     * to that fma chain); S = the pairwise tree of the 16 chains (schur_tree16) */
+    double *S4 = (double *)calloc(SCHUR_CHAINS * ((size_t)n * n + 1), sizeof(double));
+    double *S = S4;  /* chain 0, the result after the combine */
+    int *npair = (int *)calloc((size_t)nfree * nfree + 1, sizeof(int));
+    /* coef of free pose i: its landmark-ordered list of B D^-1 b_l terms summed as 64 lane
+     * partials (term t into partial t % 64, in order) and the xor butterfly 32 .. 1 */
+    double *cpart = (double *)calloc((size_t)n * 64 + 1, sizeof(double));
+    int *ncoef = (int *)calloc((size_t)nfree + 1, sizeof(int));
     double *coef = (double *)calloc((size_t)n + 1, sizeof(double));
     double *Dinv = (double *)malloc(sizeof(double) * 9 * (npoint > 0 ? npoint : 1));
-    /* Hschur = Hpp + lambda (diagonal blocks) */
+    /* Hschur = Hpp + lambda (diagonal blocks): chain 0's start */
     for (int i = 0; i < npose; i++) {
         if (pidx[i] < 0)
             continue;
@@ -469,24 +495,58 @@ int orc_ba_schur_solve(const orc_pose *poses, int npose, int npoint, const orc_e
             for (int r = 0; r < 6; r++)
                 for (int c = 0; c < 3; c++)
                     BD[r][c] = (h1[0][r] * Di[c] + h1[1][r] * Di[3 + c]) + h1[2][r] * Di[6 + c];
-            for (int r = 0; r < 6; r++)
-                coef[6 * i1 + r] += (h1[0][r] * db[0] + h1[1][r] * db[1]) + h1[2][r] * db[2];
+            {
+                const int t = ncoef[i1]++;
+                for (int r = 0; r < 6; r++)
+                    cpart[(6 * (size_t)i1 + r) * 64 + (t & 63)] +=
+                        (h1[0][r] * db[0] + h1[1][r] * db[1]) + h1[2][r] * db[2];
+            }
             for (int b2 = a; b2 < cnt[p + 1]; b2++) {
                 const int e2 = lst[b2], i2 = pidx[edges[e2].pose];
                 if (i2 < 0)
                     continue;
                 const double (*h2)[6] = eout[e2].hpl;
+                double *Sc = S4 + (size_t)(npair[(size_t)i1 * nfree + i2]++ % SCHUR_CHAINS) *
+                                      ((size_t)n * n + 1);
                 for (int r = 0; r < 6; r++)
-                    for (int c = 0; c < 6; c++)
-                        S[(6 * i1 + r) * n + 6 * i2 + c] -=
-                            (BD[r][0] * h2[0][c] + BD[r][1] * h2[1][c]) + BD[r][2] * h2[2][c];
+                    for (int c = 0; c < 6; c++) {
+                        double *v = &Sc[(6 * i1 + r) * n + 6 * i2 + c];
+                        for (int k = 0; k < 3; k++)
+                            *v = fma(-BD[r][k], h2[k][c], *v);
+                        *v = fma(0.0, 0.0, *v); /* the zero-padded k = 3 */
+                    }
             }
         }
+    }
+    /* the chains of every upper block combined (blocks without pairs stay 0 / Hpp + lambda:
+     * x + 0 = x) */
+    {
+        const size_t cs = (size_t)n * n + 1;
+        for (int r = 0; r < n; r++)
+            for (int c = r / 6 * 6; c < n; c++) {
+                const size_t o = (size_t)r * n + c;
+                double v[SCHUR_CHAINS];
+                for (int u = 0; u < SCHUR_CHAINS; u++)
+                    v[u] = S4[u * cs + o];
+                S[o] = schur_tree16(v);
+            }
     }
     /* symmetric: lower blocks mirror the upper ones */
     for (int r = 0; r < n; r++)
         for (int c = 0; c < r; c++)
             S[r * n + c] = S[c * n + r];
+    for (int i = 0; i < nfree; i++)
+        for (int r = 0; r < 6; r++) {
+            double v[64];
+            memcpy(v, cpart + (6 * (size_t)i + r) * 64, sizeof(v));
+            for (int off = 32; off >= 1; off >>= 1) {
+                double w[64];
+                for (int l = 0; l < 64; l++)
+                    w[l] = v[l] + v[l ^ off];
+                memcpy(v, w, sizeof(v));
+            }
+            coef[6 * i + r] = v[0];
+        }
     double *xp = (double *)calloc((size_t)n + 1, sizeof(double));
     for (int i = 0; i < npose; i++)
         if (pidx[i] >= 0)
@@ -523,7 +583,10 @@ int orc_ba_schur_solve(const orc_pose *poses, int npose, int npoint, const orc_e
     free(cnt);
     free(lst);
     free(fill);
-    free(S);
+    free(S4);
+    free(npair);
+    free(cpart);
+    free(ncoef);
     free(coef);
     free(Dinv);
     free(xp);

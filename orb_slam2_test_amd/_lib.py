@@ -247,6 +247,8 @@ def lib():
         "orbg_ba_graph_set_active": (i32, [vp, vp, vp]),
         "orbg_ba_graph_build_system": (i32, [vp, vp, vp, vp, vp, vp, vp, vp, vp]),
         "orbg_ba_graph_errors": (i32, [vp, vp, vp, vp, vp, vp, vp, vp]),
+        "orbg_ba_graph_schur_plan": (i32, [vp, vp, vp]),
+        "orbg_ba_graph_schur_solve": (i32, [vp, vp, C.c_double, vp, vp, vp, vp, vp, vp, vp, vp]),
         "orbg_search_for_triangulation": (i32, [vp, P(KeyFrame), P(KeyFrame), vp, i32, i32, vp,
                                                 P(i32)]),
         "orbg_search_for_triangulation_batch_device": (i32, [vp, P(KeyFrames), i32, vp, vp, vp,

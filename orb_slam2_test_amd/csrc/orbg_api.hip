@@ -8,6 +8,7 @@
 #include <atomic>
 #include <cmath>
 #include <cstdarg>
+#include <cstddef>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -2842,7 +2843,52 @@ struct orbg_ba_graph {
     int32_t *d_special = nullptr, *d_slice_off = nullptr, *d_slice_pose = nullptr;
     double *d_part = nullptr;
     BaGraphDev gd{};
+    // the Schur solve's structure (orbg_ba_graph_schur_plan), rebuilt by set_active
+    bool schur_planned = false;
+    std::vector<uint8_t> fixed;  // the plan's fixed-pose flags
+    uint8_t *d_schur = nullptr;  // structure + scratch (schur_layout)
+    size_t schur_bytes = 0;
+    SchurArgs sa{};
 };
+
+static size_t schur_layout(const SchurPlanHost &P, int nedge, uint8_t *base, SchurArgs &A,
+                           size_t *structure_bytes);
+static int schur_upload(const SchurPlanHost &P, const SchurArgs &A, hipStream_t st);
+
+// (re)build an orbg_ba_graph's Schur structure from its host edges and the stored fixed
+// flags, and upload it in stream order (no host synchronisation unless the buffer grows)
+static int ba_graph_schur_replan(orbg_ctx *c, orbg_ba_graph *g)
+{
+    const int ne = g->nedge;
+    std::vector<int32_t> ep(std::max(ne, 1)), eq(std::max(ne, 1));
+    std::vector<uint8_t> ea(std::max(ne, 1));
+    for (int e = 0; e < ne; e++) {
+        ep[e] = g->h[e].pose;
+        eq[e] = g->h[e].point;
+        ea[e] = (g->h[e].flags & 4u) ? 1 : 0;
+    }
+    SchurPlanHost P;
+    build_schur_plan(g->npose, g->npoint, ne, ep.data(), eq.data(), ea.data(), g->fixed.data(), P);
+    SchurArgs A{};
+    const size_t bytes = schur_layout(P, ne, nullptr, A, nullptr);
+    if (bytes > g->schur_bytes) {
+        if (g->d_schur) {
+            HIPCHK(hipStreamSynchronize(c->stream));  // a queued solve may still read it
+            hipFree(g->d_schur);
+        }
+        g->d_schur = nullptr;
+        g->schur_bytes = 0;
+        if (hipMalloc((void **)&g->d_schur, bytes) != hipSuccess)
+            return set_err(ORBG_ENOMEM, "Schur structure %zu bytes", bytes);
+        g->schur_bytes = bytes;
+    }
+    schur_layout(P, ne, g->d_schur, A, nullptr);
+    int rc = schur_upload(P, A, c->stream);
+    if (rc) return rc;
+    g->sa = A;
+    g->schur_planned = true;
+    return ORBG_OK;
+}
 
 static void ba_graph_free(orbg_ba_graph *g)
 {
@@ -2855,7 +2901,8 @@ static void ba_graph_free(orbg_ba_graph *g)
     if (g->h_pin) hipHostFree(g->h_pin);
     for (void *p : {(void *)g->d_edges, (void *)g->d_cam, (void *)g->d_info, (void *)g->d_off,
                     (void *)g->d_pe, (void *)g->d_qoff, (void *)g->d_qe, (void *)g->d_special,
-                    (void *)g->d_slice_off, (void *)g->d_slice_pose, (void *)g->d_part})
+                    (void *)g->d_slice_off, (void *)g->d_slice_pose, (void *)g->d_part,
+                    (void *)g->d_schur})
         if (p) hipFree(p);
     delete g;
 }
@@ -3018,6 +3065,47 @@ extern "C" int orbg_ba_graph_set_active(orbg_ctx *c, orbg_ba_graph *g, const uin
         HIPCHK(hipEventRecord(g->ev_up, c->stream));
         g->up_pending = true;
     }
+    if (g->schur_planned) return ba_graph_schur_replan(c, g);  // the active set shapes it
+    return ORBG_OK;
+}
+
+extern "C" int orbg_ba_graph_schur_plan(orbg_ctx *c, orbg_ba_graph *g, const uint8_t *fixed)
+{
+    if (!c || !g) return set_err(ORBG_EINVAL, "ctx / graph is NULL");
+    if (g->npose && !fixed) return set_err(ORBG_EINVAL, "fixed is NULL");
+    if (g->device != c->device) return set_err(ORBG_EINVAL, "graph of another device");
+    HIPCHK(hipSetDevice(c->device));
+    g->fixed.assign(std::max(g->npose, 1), 0);
+    for (int i = 0; i < g->npose; i++) g->fixed[i] = fixed[i] ? 1 : 0;
+    return ba_graph_schur_replan(c, g);
+}
+
+extern "C" int orbg_ba_graph_schur_solve(orbg_ctx *c, orbg_ba_graph *g, double lambda,
+                                         const double *d_hpl, const double *d_hpose,
+                                         const double *d_bpose, const double *d_hpoint,
+                                         const double *d_bpoint, double *d_dx_pose,
+                                         double *d_dx_point, int32_t *d_ok)
+{
+    if (!c || !g) return set_err(ORBG_EINVAL, "ctx / graph is NULL");
+    if (g->device != c->device) return set_err(ORBG_EINVAL, "graph of another device");
+    if (!g->schur_planned) return set_err(ORBG_EINVAL, "orbg_ba_graph_schur_plan not called");
+    if (!d_ok || (g->nedge && !d_hpl) || (g->npose && (!d_hpose || !d_bpose || !d_dx_pose)) ||
+        (g->npoint && (!d_hpoint || !d_bpoint || !d_dx_point)))
+        return set_err(ORBG_EINVAL, "NULL device array");
+    HIPCHK(hipSetDevice(c->device));
+    SchurArgs A = g->sa;
+    A.hpl = d_hpl;
+    A.hpl_stride = 18;  // the graph build's compact H_pl [nedge][3][6]
+    A.hpose = d_hpose;
+    A.bpose = d_bpose;
+    A.hpoint = d_hpoint;
+    A.bpoint = d_bpoint;
+    A.lambda = lambda;
+    A.ok = d_ok;
+    A.dx_pose = d_dx_pose;
+    A.dx_point = d_dx_point;
+    const int rc = launch_schur(c->stream, A, &c->prof);
+    if (rc) return set_err(rc, "schur launch failed");
     return ORBG_OK;
 }
 
@@ -3339,6 +3427,76 @@ extern "C" int orbg_pose_optimization(orbg_ctx *c, const orbg_pose_edge *edges, 
 // ---------------------------------------------------------------------------
 // LocalBundleAdjustment: BlockSolver<6,3>::solve (Schur complement)
 // ---------------------------------------------------------------------------
+// Device layout of a SchurPlanHost (structure) followed by the solve's scratch, from `base`
+// (nullptr: sizes only); returns the bytes.  The structure arrays are uploaded once per plan.
+static size_t schur_layout(const SchurPlanHost &P, int nedge, uint8_t *base, SchurArgs &A,
+                           size_t *structure_bytes)
+{
+    size_t off = 0;
+    auto take = [&](size_t bytes) -> uint8_t * {
+        uint8_t *q = base ? base + off : nullptr;
+        off += al256(std::max(bytes, (size_t)1));
+        return q;
+    };
+    (void)nedge;
+    A.pidx = (const int32_t *)take(P.pidx.size() * 4);
+    A.free_pose = (const int32_t *)take(P.free_pose.size() * 4);
+    A.pt_off = (const int32_t *)take(P.pt_off.size() * 4);
+    A.pt_edges = (const int32_t *)take(P.pt_edges.size() * 4);
+    A.slot_point = (const int32_t *)take(P.slot_point.size() * 4);
+    A.edge_pose = (const int32_t *)take(P.edge_pose.size() * 4);
+    A.blk_off = (const int32_t *)take(P.blk_off.size() * 4);
+    A.blk_pairs = (const int2 *)take(P.blk_pairs.size() * 8);
+    A.blk_i1 = (const int32_t *)take(P.blk_i1.size() * 4);
+    A.blk_i2 = (const int32_t *)take(P.blk_i2.size() * 4);
+    A.blk_seg = (const int32_t *)take(P.blk_seg.size() * 4);
+    A.pose_off = (const int32_t *)take(P.pose_off.size() * 4);
+    A.pose_slots = (const int32_t *)take(P.pose_slots.size() * 4);
+    A.seg_lo = (const int32_t *)take(P.seg_lo.size() * 4);
+    A.seg_soff = (const int64_t *)take(P.seg_soff.size() * 8);
+    if (structure_bytes) *structure_bytes = off;
+    const size_t nslot = (size_t)std::max(P.pt_off.back(), 1);
+    A.rec = (double *)take((nslot + 256) * 24 * 8);  // k_schur_points' records (+ a workgroup's tail)
+    A.S = (double *)take((size_t)std::max<int64_t>(P.seg_soff.back(), 1) * 8);
+    A.x = (double *)take((size_t)std::max(6 * P.nfree, 1) * 8);
+    A.nslot = P.pt_off.back();
+    A.npose = P.npose;
+    A.npoint = P.npoint;
+    A.nfree = P.nfree;
+    A.nblk = P.nblk;
+    A.nseg = P.nseg;
+    A.max_seg = P.max_seg;
+    A.s_total = P.seg_soff.back();
+    return off;
+}
+
+// the structure arrays of P to their places in A (stream-ordered copies from host memory)
+static int schur_upload(const SchurPlanHost &P, const SchurArgs &A, hipStream_t st)
+{
+    auto up = [&](const void *dst, const void *src, size_t bytes) -> int {
+        if (bytes) HIPCHK(hipMemcpyAsync((void *)dst, src, bytes, hipMemcpyHostToDevice, st));
+        return ORBG_OK;
+    };
+    int rc;
+    if ((rc = up(A.pidx, P.pidx.data(), P.pidx.size() * 4)) ||
+        (rc = up(A.free_pose, P.free_pose.data(), P.free_pose.size() * 4)) ||
+        (rc = up(A.pt_off, P.pt_off.data(), P.pt_off.size() * 4)) ||
+        (rc = up(A.pt_edges, P.pt_edges.data(), P.pt_edges.size() * 4)) ||
+        (rc = up(A.slot_point, P.slot_point.data(), P.slot_point.size() * 4)) ||
+        (rc = up(A.edge_pose, P.edge_pose.data(), P.edge_pose.size() * 4)) ||
+        (rc = up(A.blk_off, P.blk_off.data(), P.blk_off.size() * 4)) ||
+        (rc = up(A.blk_pairs, P.blk_pairs.data(), P.blk_pairs.size() * 8)) ||
+        (rc = up(A.blk_i1, P.blk_i1.data(), P.blk_i1.size() * 4)) ||
+        (rc = up(A.blk_i2, P.blk_i2.data(), P.blk_i2.size() * 4)) ||
+        (rc = up(A.blk_seg, P.blk_seg.data(), P.blk_seg.size() * 4)) ||
+        (rc = up(A.pose_off, P.pose_off.data(), P.pose_off.size() * 4)) ||
+        (rc = up(A.pose_slots, P.pose_slots.data(), P.pose_slots.size() * 4)) ||
+        (rc = up(A.seg_lo, P.seg_lo.data(), P.seg_lo.size() * 4)) ||
+        (rc = up(A.seg_soff, P.seg_soff.data(), P.seg_soff.size() * 8)))
+        return rc;
+    return ORBG_OK;
+}
+
 extern "C" int orbg_ba_schur_solve(orbg_ctx *c, const orbg_pose *poses, int npose, int npoint,
                                    const orbg_edge *edges, int nedge, const orbg_edge_out *eout,
                                    const double *hpose, const double *bpose,
@@ -3355,125 +3513,52 @@ extern "C" int orbg_ba_schur_solve(orbg_ctx *c, const orbg_pose *poses, int npos
             edges[e].point >= npoint)
             return set_err(ORBG_EINVAL, "edge %d references a missing vertex", e);
     HIPCHK(hipSetDevice(c->device));
-    // ---- host structure (the graph is fixed across LM iterations) ----
-    std::vector<int32_t> pidx(std::max(npose, 1));
-    int nfree = 0;
-    for (int i = 0; i < npose; i++) pidx[i] = poses[i].fixed ? -1 : nfree++;
-    std::vector<int32_t> pt_off(npoint + 1, 0), pt_edges, edge_pose(std::max(nedge, 1));
+    // the structure (built per call here: the graph entry points keep it across iterations)
+    std::vector<int32_t> ep(std::max(nedge, 1)), eq(std::max(nedge, 1));
+    std::vector<uint8_t> ea(std::max(nedge, 1)), fx(std::max(npose, 1));
     for (int e = 0; e < nedge; e++) {
-        edge_pose[e] = edges[e].pose;
-        if (edges[e].active) pt_off[edges[e].point + 1]++;
+        ep[e] = edges[e].pose;
+        eq[e] = edges[e].point;
+        ea[e] = edges[e].active ? 1 : 0;
     }
-    for (int i = 0; i < npoint; i++) pt_off[i + 1] += pt_off[i];
-    pt_edges.resize(std::max(pt_off[npoint], 1));
-    {
-        std::vector<int32_t> fill(pt_off.begin(), pt_off.end() - 1);
-        for (int e = 0; e < nedge; e++)
-            if (edges[e].active) pt_edges[fill[edges[e].point]++] = e;
-        for (int p = 0; p < npoint; p++)
-            std::stable_sort(pt_edges.begin() + pt_off[p], pt_edges.begin() + pt_off[p + 1],
-                             [&](int a, int b) { return edges[a].pose < edges[b].pose; });
-    }
-    // upper Schur blocks: all diagonal blocks + every pose pair sharing a landmark; pairs
-    // listed in landmark order
-    std::vector<std::vector<int2>> blists((size_t)nfree * nfree);
-    std::vector<std::vector<int32_t>> pose_lists(nfree);
-    for (int p = 0; p < npoint; p++)
-        for (int a = pt_off[p]; a < pt_off[p + 1]; a++) {
-            const int e1 = pt_edges[a], i1 = pidx[edges[e1].pose];
-            if (i1 < 0) continue;
-            pose_lists[i1].push_back(e1);
-            for (int b = a; b < pt_off[p + 1]; b++) {
-                const int e2 = pt_edges[b], i2 = pidx[edges[e2].pose];
-                if (i2 < 0) continue;
-                blists[(size_t)i1 * nfree + i2].push_back(make_int2(e1, e2));
-            }
-        }
-    std::vector<int32_t> blk_off(1, 0), blk_i1, blk_i2;
-    std::vector<int2> blk_pairs;
-    for (int i1 = 0; i1 < nfree; i1++)
-        for (int i2 = i1; i2 < nfree; i2++) {
-            const auto &l = blists[(size_t)i1 * nfree + i2];
-            if (i1 != i2 && l.empty()) continue;
-            blk_i1.push_back(i1);
-            blk_i2.push_back(i2);
-            blk_pairs.insert(blk_pairs.end(), l.begin(), l.end());
-            blk_off.push_back((int32_t)blk_pairs.size());
-        }
-    std::vector<int32_t> pose_off(nfree + 1, 0), pose_edges;
-    for (int i = 0; i < nfree; i++) {
-        pose_edges.insert(pose_edges.end(), pose_lists[i].begin(), pose_lists[i].end());
-        pose_off[i + 1] = (int32_t)pose_edges.size();
-    }
-    const int nblk = (int)blk_i1.size(), n = 6 * nfree;
-    // ---- device buffers (scratch) ----
-    size_t off = 0;
+    for (int i = 0; i < npose; i++) fx[i] = poses[i].fixed ? 1 : 0;
+    SchurPlanHost P;
+    build_schur_plan(npose, npoint, nedge, ep.data(), eq.data(), ea.data(), fx.data(), P);
+    SchurArgs A{};
+    const size_t sb = schur_layout(P, nedge, nullptr, A, nullptr);
+    size_t off = sb;
     auto take = [&](size_t bytes) {
         const size_t o = off;
         off += al256(std::max(bytes, (size_t)1));
         return o;
     };
-    const size_t o_pidx = take(pidx.size() * 4), o_ptoff = take(pt_off.size() * 4);
-    const size_t o_pte = take(pt_edges.size() * 4), o_ep = take(edge_pose.size() * 4);
-    const size_t o_boff = take(blk_off.size() * 4), o_bp = take(blk_pairs.size() * 8);
-    const size_t o_bi1 = take(blk_i1.size() * 4), o_bi2 = take(blk_i2.size() * 4);
-    const size_t o_poff = take(pose_off.size() * 4), o_pe = take(pose_edges.size() * 4);
     const size_t o_eout = take((size_t)nedge * sizeof(orbg_edge_out));
     const size_t o_hp = take((size_t)npose * 36 * 8), o_bpz = take((size_t)npose * 6 * 8);
     const size_t o_hq = take((size_t)npoint * 9 * 8), o_bq = take((size_t)npoint * 3 * 8);
-    const size_t o_dinv = take((size_t)npoint * 9 * 8), o_bd = take((size_t)nedge * 18 * 8);
-    const size_t o_cf = take((size_t)nedge * 6 * 8), o_S = take((size_t)n * n * 8);
-    const size_t o_x = take((size_t)n * 8), o_ok = take(4);
+    const size_t o_ok = take(4);
     const size_t o_dp = take((size_t)npose * 6 * 8), o_dq = take((size_t)npoint * 3 * 8);
     void *sp;
     int rc = scratch(c, off, &sp);
     if (rc) return rc;
     uint8_t *B = (uint8_t *)sp;
+    schur_layout(P, nedge, B, A, nullptr);
+    if ((rc = schur_upload(P, A, c->stream))) return rc;
     auto up = [&](size_t o, const void *src, size_t bytes) -> int {
         if (bytes) HIPCHK(hipMemcpyAsync(B + o, src, bytes, hipMemcpyHostToDevice, c->stream));
         return ORBG_OK;
     };
-    if ((rc = up(o_pidx, pidx.data(), pidx.size() * 4)) || (rc = up(o_ptoff, pt_off.data(), pt_off.size() * 4)) ||
-        (rc = up(o_pte, pt_edges.data(), pt_edges.size() * 4)) ||
-        (rc = up(o_ep, edge_pose.data(), (size_t)nedge * 4)) ||
-        (rc = up(o_boff, blk_off.data(), blk_off.size() * 4)) ||
-        (rc = up(o_bp, blk_pairs.data(), blk_pairs.size() * 8)) ||
-        (rc = up(o_bi1, blk_i1.data(), blk_i1.size() * 4)) ||
-        (rc = up(o_bi2, blk_i2.data(), blk_i2.size() * 4)) ||
-        (rc = up(o_poff, pose_off.data(), pose_off.size() * 4)) ||
-        (rc = up(o_pe, pose_edges.data(), pose_edges.size() * 4)) ||
-        (rc = up(o_eout, eout, (size_t)nedge * sizeof(orbg_edge_out))) ||
+    if ((rc = up(o_eout, eout, (size_t)nedge * sizeof(orbg_edge_out))) ||
         (rc = up(o_hp, hpose, (size_t)npose * 36 * 8)) || (rc = up(o_bpz, bpose, (size_t)npose * 6 * 8)) ||
         (rc = up(o_hq, hpoint, (size_t)npoint * 9 * 8)) || (rc = up(o_bq, bpoint, (size_t)npoint * 3 * 8)))
         return rc;
-    if (n) HIPCHK(hipMemsetAsync(B + o_S, 0, (size_t)n * n * 8, c->stream));
-    SchurArgs A{};
-    A.npose = npose;
-    A.npoint = npoint;
-    A.nfree = nfree;
-    A.n = n;
-    A.pidx = (const int32_t *)(B + o_pidx);
-    A.pt_off = (const int32_t *)(B + o_ptoff);
-    A.pt_edges = (const int32_t *)(B + o_pte);
-    A.edge_pose = (const int32_t *)(B + o_ep);
-    A.blk_off = (const int32_t *)(B + o_boff);
-    A.blk_pairs = (const int2 *)(B + o_bp);
-    A.blk_i1 = (const int32_t *)(B + o_bi1);
-    A.blk_i2 = (const int32_t *)(B + o_bi2);
-    A.nblk = nblk;
-    A.pose_off = (const int32_t *)(B + o_poff);
-    A.pose_edges = (const int32_t *)(B + o_pe);
-    A.eout = (const orbg_edge_out *)(B + o_eout);
+    static_assert(sizeof(orbg_edge_out) % 8 == 0, "edge_out records are whole doubles");
+    A.hpl = (const double *)(B + o_eout + offsetof(orbg_edge_out, hpl));
+    A.hpl_stride = (int)(sizeof(orbg_edge_out) / 8);
     A.hpose = (const double *)(B + o_hp);
     A.bpose = (const double *)(B + o_bpz);
     A.hpoint = (const double *)(B + o_hq);
     A.bpoint = (const double *)(B + o_bq);
     A.lambda = lambda;
-    A.dinv = (double *)(B + o_dinv);
-    A.bd = (double *)(B + o_bd);
-    A.cf = (double *)(B + o_cf);
-    A.S = (double *)(B + o_S);
-    A.x = (double *)(B + o_x);
     A.ok = (int32_t *)(B + o_ok);
     A.dx_pose = (double *)(B + o_dp);
     A.dx_point = (double *)(B + o_dq);

@@ -1,18 +1,28 @@
 // schur_kernels.hip -- g2o BlockSolver<6,3>::solve with the Schur complement
-// (Thirdparty/g2o/g2o/core/block_solver.hpp:354-486) for one LocalBundleAdjustment window,
-// on gfx950, fp64.  Inputs are orbg_ba_linearize's blocks (H_pp, b_p per pose; H_ll, b_l per
-// point; H_pl per edge) after setLambda(lambda); outputs the pose and point increments.
+// (Thirdparty/g2o/g2o/core/block_solver.hpp:354-486) for LocalBundleAdjustment windows, on
+// gfx950, fp64.  Inputs are the linearisation's blocks (H_pp, b_p per pose; H_ll, b_l per
+// point; H_pl per edge) after setLambda(lambda); outputs the pose and point increments.  The
+// structure is a SchurPlanHost built once per graph (schur_args.h), so an LM iteration's
+// build -> errors -> solve runs on one stream with no host copy (orbg_ba_graph_schur_solve).
 //
-//   k_schur_points   thread per landmark: D^-1 = (H_ll + lambda I)^-1 (Eigen's cofactor
-//                    3x3 inverse), D^-1 b_l, and per active edge to a free pose
-//                    B D^-1 (6x3) and B D^-1 b_l (6)
-//   k_schur_blocks   thread per (pose pair i1 <= i2, element): S = H_pp + lambda I (diagonal
-//                    blocks) minus B_i D^-1 B_j^T landmark by landmark, then b_schur
-//   k_schur_mirror   lower triangle = upper
-//   k_schur_ldlt     one workgroup: dense LDLT (no pivoting) of S and the two triangular
-//                    solves -- 6 x (free poses) unknowns, a few hundred at most
+//   k_schur_points   thread per active edge (point-major slot): D^-1 = (H_ll + lambda I)^-1
+//                    (Eigen's cofactor 3x3 inverse), D^-1 b_l, and for an edge to a free
+//                    pose B D^-1 (6x3) and B D^-1 b_l (6), stored by slot, coalesced
+//   k_schur_blocks   workgroup per upper block (i1 <= i2): S = H_pp + lambda I (diagonal
+//                    blocks) minus sum B_i D^-1 B_j^T over its landmark pairs, one
+//                    v_mfma_f64_4x4x4f64 per pair (the 6x6 block padded to the 8x8 of the
+//                    instruction's four 4x4 blocks, K = the 3 inner terms + a zero), pair t
+//                    into accumulator chain t % 16 = wave t % 16 of the workgroup, the chains
+//                    combined by a pairwise tree; written upper + mirrored into the
+//                    segment's dense system
+//   k_schur_rhs      wave per free pose: b_schur = b_p - sum B D^-1 b_l over its landmarks
+//                    (64 lane partials in list order, xor butterfly)
+//   k_schur_ldlt     workgroup per segment: right-looking dense LDLT (no pivoting; each
+//                    element's updates in k order: the left-looking oracle's bits) and the
+//                    two triangular solves column by column, in LDS when it fits
 //   k_schur_backsub  thread per landmark: x_l = D^-1 (b_l - B^T x_p)
-// Every sum runs in the order oracle/ba_oracle.c (orc_ba_schur_solve) pins, so the
+// Every sum runs in the order oracle/ba_oracle.c (orc_ba_schur_solve) pins -- including the
+// MFMA's own: a fused chain over k in order (tools/microbench/mfma_f64_pin.hip) -- so the
 // increments are bit-identical to it.
 #include <hip/hip_runtime.h>
 
@@ -30,16 +40,9 @@ namespace orbg {
 void prof_begin(void *prof, hipStream_t s, const char *n, hipEvent_t *a);
 void prof_end(void *prof, hipStream_t s, const char *n, hipEvent_t a);
 
-__global__ void k_schur_points(SchurArgs A)
+// (H_ll + lambda I)^-1 by Eigen's cofactor 3x3 inverse (orc inv3_eigen) and D^-1 b_l
+__device__ __forceinline__ void schur_dinv(const SchurArgs &A, int p, double d[9], double db[3])
 {
-    const int p = blockIdx.x * blockDim.x + threadIdx.x;
-    if (p >= A.npoint) return;
-    const int a0 = A.pt_off[p], a1 = A.pt_off[p + 1];
-    double *Di = A.dinv + 9 * (size_t)p;
-    if (a0 == a1) {
-        for (int k = 0; k < 9; k++) Di[k] = 0;
-        return;
-    }
     double m[9];
     for (int k = 0; k < 9; k++) m[k] = A.hpoint[9 * (size_t)p + k];
     m[0] += A.lambda;
@@ -51,7 +54,6 @@ __global__ void k_schur_points(SchurArgs A)
     const double c0 = COF(0, 0), c1 = COF(1, 0), c2 = COF(2, 0);
     const double det = (c0 * M(0, 0) + c1 * M(1, 0)) + c2 * M(2, 0);
     const double invdet = 1.0 / det;
-    double d[9];
     d[0] = c0 * invdet;
     d[1] = c1 * invdet;
     d[2] = c2 * invdet;
@@ -63,112 +65,209 @@ __global__ void k_schur_points(SchurArgs A)
     d[8] = COF(2, 2) * invdet;
 #undef COF
 #undef M
-    for (int k = 0; k < 9; k++) Di[k] = d[k];
     const double *bl = A.bpoint + 3 * (size_t)p;
-    double db[3];
     for (int r = 0; r < 3; r++) db[r] = (d[r * 3] * bl[0] + d[r * 3 + 1] * bl[1]) + d[r * 3 + 2] * bl[2];
-    for (int a = a0; a < a1; a++) {
+}
+
+// thread per slot (active edge, point-major): the point's D^-1 recomputed (a few dozen flops;
+// no per-point array), then for an edge to a free pose the record B D^-1 (6x3) | B D^-1 b_l
+// (6); the workgroup's 256 records are staged in LDS and stored as one contiguous 48 KB run
+#define SCHUR_REC 24
+__global__ __launch_bounds__(256) void k_schur_points(SchurArgs A)
+{
+    __shared__ double2 rec[256 * SCHUR_REC / 2];
+    const int tid = threadIdx.x, base = blockIdx.x * 256, a = base + tid;
+    if (a == 0) *A.ok = 1;  // k_schur_ldlt clears it on a bad pivot (stream order)
+    double v[SCHUR_REC];
+#pragma unroll
+    for (int k = 0; k < SCHUR_REC; k++) v[k] = 0.0;
+    if (a < A.nslot) {
         const int e = A.pt_edges[a];
-        if (A.pidx[A.edge_pose[e]] < 0) continue;
-        const double(*h)[6] = A.eout[e].hpl;  // B = h^T (6 x 3)
-        double *bd = A.bd + 18 * (size_t)e;
-        double *cf = A.cf + 6 * (size_t)e;
-        for (int r = 0; r < 6; r++) {
-            for (int c = 0; c < 3; c++)
-                bd[r * 3 + c] = (h[0][r] * d[c] + h[1][r] * d[3 + c]) + h[2][r] * d[6 + c];
-            cf[r] = (h[0][r] * db[0] + h[1][r] * db[1]) + h[2][r] * db[2];
+        if (A.pidx[A.edge_pose[e]] >= 0) {
+            double d[9], db[3];
+            schur_dinv(A, A.slot_point[a], d, db);
+            const double *h = A.hpl + (size_t)e * A.hpl_stride;  // B = h^T (6 x 3), h[k][r] = h[6k + r]
+            double hh[18];
+#pragma unroll
+            for (int k = 0; k < 18; k++) hh[k] = h[k];
+#pragma unroll
+            for (int r = 0; r < 6; r++) {
+#pragma unroll
+                for (int c = 0; c < 3; c++)
+                    v[r * 3 + c] = (hh[r] * d[c] + hh[6 + r] * d[3 + c]) + hh[12 + r] * d[6 + c];
+                v[18 + r] = (hh[r] * db[0] + hh[6 + r] * db[1]) + hh[12 + r] * db[2];
+            }
         }
     }
+#pragma unroll
+    for (int k = 0; k < SCHUR_REC; k += 2) rec[tid * (SCHUR_REC / 2) + k / 2] = make_double2(v[k], v[k + 1]);
+    __syncthreads();
+    const int nrec = min(256, A.nslot - base);
+    double2 *out = (double2 *)(A.rec + (size_t)base * SCHUR_REC);
+    for (int i = tid; i < nrec * (SCHUR_REC / 2); i += 256) out[i] = rec[i];
 }
 
-// thread per (upper block, element): blocks of the free-pose pairs (i1 <= i2) that share a
-// landmark, plus every diagonal block
-__global__ void k_schur_blocks(SchurArgs A)
+// workgroup per upper block, wave u = accumulator chain u: the block's pairs t = u, u + 16, ...
+// (landmark order) by one v_mfma_f64_4x4x4f64 each into that wave's chain (16 chains: a
+// diagonal block sums every landmark of its pose, ~3000 in a KITTI window, so its gathers
+// need that many waves in flight), the chains combined by a pairwise tree through LDS.  Operand layout of the instruction
+// (ba_kernels.hip): A[b][i][k] at lane 16k + 4b + i, B[b][k][j] at lane 16k + 4b + j,
+// C[b][i][j] at lane 16i + 4b + j; block b = 2I + J holds rows 4I + i, columns 4J + j of the
+// padded 8x8.  A = -B D^-1 of the pair's first edge (6x3, k = its column), B = H_pl of the
+// second (3x6, k = its row).
+#define SCHUR_CHAINS 16  // waves per block workgroup = accumulator chains (the oracle's)
+__global__ __launch_bounds__(64 * SCHUR_CHAINS) void k_schur_blocks(SchurArgs A)
 {
-    const int t = blockIdx.x * blockDim.x + threadIdx.x;
-    if (t >= A.nblk * 36) return;
-    const int bk = t / 36, rc = t - bk * 36, r = rc / 6, c = rc - r * 6;
-    const int i1 = A.blk_i1[bk], i2 = A.blk_i2[bk];
-    double acc = 0.0;
-    if (i1 == i2) {
-        // the pose index of free pose i1 (pidx inverse is monotone: search)
-        int pose = 0;
-        for (int q = 0; q < A.npose; q++)
-            if (A.pidx[q] == i1) pose = q;
-        acc = A.hpose[36 * (size_t)pose + rc] + (r == c ? A.lambda : 0.0);
+    __shared__ double tile[SCHUR_CHAINS][64];
+    const int lane = threadIdx.x & 63, u = threadIdx.x >> 6, bk = blockIdx.x;
+    const int i1 = A.blk_i1[bk], i2 = A.blk_i2[bk], sg = A.blk_seg[bk];
+    const int lo = A.seg_lo[sg], n = 6 * (A.seg_lo[sg + 1] - lo);
+    const int k = lane >> 4, b = (lane >> 2) & 3, t = lane & 3;
+    const int ra = 4 * (b >> 1) + t, cb = 4 * (b & 1) + t;  // A's row, B's column
+    const bool va = ra < 6 && k < 3, vb = k < 3 && cb < 6;
+    const int oa = ra * 3 + k, ob = 6 * k + cb;
+    const int ro = 4 * (b >> 1) + k, co = 4 * (b & 1) + t;  // this lane's C entry (i = lane >> 4)
+    double c = 0.0;
+    if (u == 0 && i1 == i2 && ro < 6 && co < 6)
+        c = A.hpose[36 * (size_t)A.free_pose[i1] + 6 * ro + co] + (ro == co ? A.lambda : 0.0);
+    const int p0 = A.blk_off[bk], np = A.blk_off[bk + 1] - p0;
+    const int nu = np > u ? (np - u + SCHUR_CHAINS - 1) / SCHUR_CHAINS : 0;  // p0 + u + 16 j
+    // 16 pairs per step: lane l < 16 loads pair j0 + l's ids once, the wave takes them by
+    // readlane, so all 32 operand loads of the step are in flight together
+    for (int j0 = 0; j0 < nu; j0 += 16) {
+        const int m = min(16, nu - j0);
+        int2 prl = make_int2(0, 0);
+        if (lane < m) prl = A.blk_pairs[p0 + u + SCHUR_CHAINS * (j0 + lane)];
+        double av[16], bv[16];
+#pragma unroll
+        for (int q = 0; q < 16; q++) {
+            const int s1 = __builtin_amdgcn_readlane(prl.x, q), e2 = __builtin_amdgcn_readlane(prl.y, q);
+            av[q] = (va && q < m) ? -A.rec[(size_t)s1 * SCHUR_REC + oa] : 0.0;
+            bv[q] = (vb && q < m) ? A.hpl[(size_t)e2 * A.hpl_stride + ob] : 0.0;
+        }
+#pragma unroll
+        for (int q = 0; q < 16; q++)
+            if (q < m) c = __builtin_amdgcn_mfma_f64_4x4x4f64(av[q], bv[q], c, 0, 0, 0);
     }
-    for (int k = A.blk_off[bk]; k < A.blk_off[bk + 1]; k++) {
-        const int2 pr = A.blk_pairs[k];
-        const double *bd = A.bd + 18 * (size_t)pr.x;
-        const double(*h2)[6] = A.eout[pr.y].hpl;
-        acc -= (bd[r * 3] * h2[0][c] + bd[r * 3 + 1] * h2[1][c]) + bd[r * 3 + 2] * h2[2][c];
+    tile[u][lane] = c;
+    __syncthreads();
+    if (u != 0) return;
+    // the chains' pairwise tree (oracle schur_tree16)
+    double a8[8], b4[4];
+#pragma unroll
+    for (int i = 0; i < 8; i++) a8[i] = tile[2 * i][lane] + tile[2 * i + 1][lane];
+#pragma unroll
+    for (int i = 0; i < 4; i++) b4[i] = a8[2 * i] + a8[2 * i + 1];
+    const double v = (b4[0] + b4[1]) + (b4[2] + b4[3]);
+    if (ro < 6 && co < 6) {
+        double *S = A.S + A.seg_soff[sg];
+        const int r = 6 * (i1 - lo) + ro, cc = 6 * (i2 - lo) + co;
+        if (i1 != i2 || ro <= co) S[(size_t)r * n + cc] = v;  // upper
+        if (i1 != i2 || ro < co) S[(size_t)cc * n + r] = v;   // lower = mirror of the upper
     }
-    A.S[(size_t)(6 * i1 + r) * A.n + 6 * i2 + c] = acc;
 }
 
-// b_schur = b_p - coefficients (coefficients summed per free pose in landmark order)
-__global__ void k_schur_rhs(SchurArgs A)
+// b_schur = b_p - coefficients, per free pose: the landmark-ordered B D^-1 b_l terms summed
+// as 64 lane partials (term t into partial t % 64, in order) and an xor butterfly
+__global__ __launch_bounds__(256) void k_schur_rhs(SchurArgs A)
 {
-    const int t = blockIdx.x * blockDim.x + threadIdx.x;
-    if (t >= A.n) return;
-    const int i = t / 6, r = t - i * 6;
-    int pose = 0;
-    for (int q = 0; q < A.npose; q++)
-        if (A.pidx[q] == i) pose = q;
-    double coef = 0.0;
-    for (int k = A.pose_off[i]; k < A.pose_off[i + 1]; k++) coef += A.cf[6 * (size_t)A.pose_edges[k] + r];
-    A.x[t] = A.bpose[6 * (size_t)pose + r] - coef;
+    const int lane = threadIdx.x & 63;
+    const int i = __builtin_amdgcn_readfirstlane((int)(blockIdx.x * 4 + (threadIdx.x >> 6)));
+    if (i >= A.nfree) return;
+    const int pose = A.free_pose[i], e0 = A.pose_off[i], e1 = A.pose_off[i + 1];
+    double part[6] = {0, 0, 0, 0, 0, 0};
+    // all six partials per step, four list entries per lane in flight (each partial still
+    // adds its entries t = lane, lane + 64, ... in order)
+    int t = e0 + lane;
+    for (; t + 192 < e1; t += 256) {
+        int sl[4];
+#pragma unroll
+        for (int q = 0; q < 4; q++) sl[q] = A.pose_slots[t + 64 * q];
+        double v[4][6];
+#pragma unroll
+        for (int q = 0; q < 4; q++) {
+            const double2 *cf = (const double2 *)(A.rec + (size_t)sl[q] * SCHUR_REC + 18);
+            const double2 x0 = cf[0], x1 = cf[1], x2 = cf[2];
+            v[q][0] = x0.x; v[q][1] = x0.y; v[q][2] = x1.x; v[q][3] = x1.y; v[q][4] = x2.x; v[q][5] = x2.y;
+        }
+#pragma unroll
+        for (int q = 0; q < 4; q++)
+#pragma unroll
+            for (int r = 0; r < 6; r++) part[r] += v[q][r];
+    }
+    for (; t < e1; t += 64) {
+        const double *cf = A.rec + (size_t)A.pose_slots[t] * SCHUR_REC + 18;
+#pragma unroll
+        for (int r = 0; r < 6; r++) part[r] += cf[r];
+    }
+#pragma unroll
+    for (int r = 0; r < 6; r++) {
+#pragma unroll
+        for (int off = 32; off >= 1; off >>= 1) part[r] = part[r] + __shfl_xor(part[r], off, 64);
+    }
+    if (lane < 6) {
+        double pr = part[0];
+#pragma unroll
+        for (int r = 1; r < 6; r++) pr = lane == r ? part[r] : pr;
+        A.x[6 * i + lane] = A.bpose[6 * (size_t)pose + lane] - pr;
+    }
 }
 
-__global__ void k_schur_mirror(SchurArgs A)
-{
-    const int t = blockIdx.x * blockDim.x + threadIdx.x;
-    if (t >= A.n * A.n) return;
-    const int r = t / A.n, c = t - r * A.n;
-    if (r > c) A.S[(size_t)r * A.n + c] = A.S[(size_t)c * A.n + r];
-}
-
-// dense LDLT without pivoting + solves, one 256-thread workgroup (orc_ldlt_dense_solve)
+// one workgroup per segment: right-looking LDLT of the segment's n x n system (lower
+// triangle), then L y = b (column by column), y /= d, L^T x = y (column by column, k
+// descending), in LDS when LDSM (the matrix fits), else in place in HBM
+template <bool LDSM>
 __global__ __launch_bounds__(256) void k_schur_ldlt(SchurArgs A)
 {
-    const int n = A.n, tid = threadIdx.x;
-    double *S = A.S, *x = A.x;
-    __shared__ int bad;
-    if (tid == 0) bad = 0;
+    extern __shared__ __attribute__((aligned(16))) double sl_lds[];
+    const int sg = blockIdx.x, tid = threadIdx.x;
+    const int lo = A.seg_lo[sg], n = 6 * (A.seg_lo[sg + 1] - lo);
+    if (n == 0) return;  // workgroup-uniform
+    double *Sg = A.S + A.seg_soff[sg], *xg = A.x + 6 * lo;
+    double *M = LDSM ? sl_lds : Sg, *x = LDSM ? sl_lds + (size_t)n * n : xg;
+    if (LDSM) {
+        for (int e = tid; e < n * n; e += 256) M[e] = Sg[e];
+        for (int e = tid; e < n; e += 256) x[e] = xg[e];
+    }
     __syncthreads();
+    bool bad = false;
     for (int j = 0; j < n; j++) {
-        if (tid == 0) {
-            double d = S[(size_t)j * n + j];
-            for (int k = 0; k < j; k++) d -= S[(size_t)j * n + k] * S[(size_t)j * n + k] * S[(size_t)k * n + k];
-            S[(size_t)j * n + j] = d;
-            if (d == 0.0 || !isfinite(d)) bad = 1;
+        const double d = M[(size_t)j * n + j];  // every update of step k < j is in
+        if (d == 0.0 || !isfinite(d)) {         // uniform: the oracle stops here, ok = 0
+            bad = true;
+            break;
         }
+        for (int i = j + 1 + tid; i < n; i += 256) M[(size_t)i * n + j] = M[(size_t)i * n + j] / d;
         __syncthreads();
-        if (bad) break;
-        const double d = S[(size_t)j * n + j];
-        for (int i = j + 1 + tid; i < n; i += 256) {
-            double s = S[(size_t)i * n + j];
-            for (int k = 0; k < j; k++) s -= S[(size_t)i * n + k] * S[(size_t)j * n + k] * S[(size_t)k * n + k];
-            S[(size_t)i * n + j] = s / d;
+        // trailing lower triangle: M[r][c] -= (L_rj L_cj) d_j, the oracle's
+        // A[i][k] * A[j][k] * A[k][k] at k = j, in k order for every element
+        for (int r = j + 1 + (tid >> 4); r < n; r += 16) {
+            const double lr = M[(size_t)r * n + j];
+            for (int c = j + 1 + (tid & 15); c <= r; c += 16)
+                M[(size_t)r * n + c] -= lr * M[(size_t)c * n + j] * d;
         }
         __syncthreads();
     }
-    if (tid == 0) {
-        if (!bad) {
-            for (int i = 0; i < n; i++) {
-                double s = x[i];
-                for (int k = 0; k < i; k++) s -= S[(size_t)i * n + k] * x[k];
-                x[i] = s;
-            }
-            for (int i = 0; i < n; i++) x[i] /= S[(size_t)i * n + i];
-            for (int i = n - 1; i >= 0; i--) {
-                double s = x[i];
-                for (int k = i + 1; k < n; k++) s -= S[(size_t)k * n + i] * x[k];
-                x[i] = s;
-            }
-        }
-        *A.ok = !bad;
+    if (bad) {  // uniform: every thread read the same pivot
+        if (tid == 0) *A.ok = 0;
+        return;
     }
+    // L y = b: x_i -= L_ik x_k, k ascending (the oracle's row loop, element by element)
+    for (int k = 0; k < n; k++) {
+        const double xk = x[k];
+        for (int i = k + 1 + tid; i < n; i += 256) x[i] -= M[(size_t)i * n + k] * xk;
+        __syncthreads();
+    }
+    for (int i = tid; i < n; i += 256) x[i] /= M[(size_t)i * n + i];
+    __syncthreads();
+    // L^T x = y: x_i -= L_ki x_k, k descending
+    for (int k = n - 1; k > 0; k--) {
+        const double xk = x[k];
+        for (int i = tid; i < k; i += 256) x[i] -= M[(size_t)k * n + i] * xk;
+        __syncthreads();
+    }
+    if (LDSM)
+        for (int e = tid; e < n; e += 256) xg[e] = x[e];
 }
 
 // x_l = D^-1 (b_l - B^T x_p); pose increments scattered out
@@ -193,33 +292,183 @@ __global__ void k_schur_backsub(SchurArgs A)
     for (int a = a0; a < a1; a++) {
         const int e = A.pt_edges[a], i1 = A.pidx[A.edge_pose[e]];
         if (i1 < 0) continue;
-        const double(*h)[6] = A.eout[e].hpl;
+        const double *h = A.hpl + (size_t)e * A.hpl_stride;
         for (int k = 0; k < 3; k++) {
             double s = 0;
-            for (int r = 0; r < 6; r++) s += h[k][r] * -A.x[6 * i1 + r];
+            for (int r = 0; r < 6; r++) s += h[6 * k + r] * -A.x[6 * i1 + r];
             cl[k] += s;
         }
     }
-    const double *Di = A.dinv + 9 * (size_t)p;
+    double Di[9], db[3];
+    schur_dinv(A, p, Di, db);
     for (int r = 0; r < 3; r++) xl[r] = (Di[r * 3] * cl[0] + Di[r * 3 + 1] * cl[1]) + Di[r * 3 + 2] * cl[2];
 }
 
 int launch_schur(hipStream_t st, const SchurArgs &A, void *prof)
 {
-    hipEvent_t ev = nullptr;
-    prof_begin(prof, st, "schur", &ev);
     const int T = 256;
-    hipLaunchKernelGGL(k_schur_points, dim3((A.npoint + T - 1) / T), dim3(T), 0, st, A);
-    if (A.n > 0) {
-        hipLaunchKernelGGL(k_schur_blocks, dim3((A.nblk * 36 + T - 1) / T), dim3(T), 0, st, A);
-        hipLaunchKernelGGL(k_schur_rhs, dim3((A.n + T - 1) / T), dim3(T), 0, st, A);
-        hipLaunchKernelGGL(k_schur_mirror, dim3((A.n * A.n + T - 1) / T), dim3(T), 0, st, A);
+    hipEvent_t ev = nullptr;
+    prof_begin(prof, st, "schur_points", &ev);
+    hipLaunchKernelGGL(k_schur_points, dim3((std::max(A.nslot, 1) + T - 1) / T), dim3(T), 0, st, A);
+    prof_end(prof, st, "schur_points", ev);
+    if (A.nfree > 0) {
+        // block pairs without a shared landmark are never written: zero the systems first
+        if (hipMemsetAsync(A.S, 0, sizeof(double) * (size_t)A.s_total, st) != hipSuccess)
+            return ORBG_EIO;
+        prof_begin(prof, st, "schur_blocks", &ev);
+        hipLaunchKernelGGL(k_schur_blocks, dim3(A.nblk), dim3(64 * SCHUR_CHAINS), 0, st, A);
+        prof_end(prof, st, "schur_blocks", ev);
+        prof_begin(prof, st, "schur_rhs", &ev);
+        hipLaunchKernelGGL(k_schur_rhs, dim3((A.nfree + 3) / 4), dim3(T), 0, st, A);
+        prof_end(prof, st, "schur_rhs", ev);
+        const int n = 6 * A.max_seg;
+        const size_t lds = ((size_t)n * n + n) * sizeof(double);
+        prof_begin(prof, st, "schur_ldlt", &ev);
+        if (lds <= 160 * 1024 - 64) {
+            if (lds > 64 * 1024 &&
+                hipFuncSetAttribute((const void *)k_schur_ldlt<true>,
+                                    hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) != hipSuccess)
+                return ORBG_EIO;
+            hipLaunchKernelGGL(k_schur_ldlt<true>, dim3(A.nseg), dim3(T), lds, st, A);
+        } else {
+            hipLaunchKernelGGL(k_schur_ldlt<false>, dim3(A.nseg), dim3(T), 0, st, A);
+        }
+        prof_end(prof, st, "schur_ldlt", ev);
     }
-    hipLaunchKernelGGL(k_schur_ldlt, dim3(1), dim3(256), 0, st, A);
     const int m = std::max(A.npoint, A.npose * 6);
-    hipLaunchKernelGGL(k_schur_backsub, dim3((m + T - 1) / T), dim3(T), 0, st, A);
-    prof_end(prof, st, "schur", ev);
+    prof_begin(prof, st, "schur_backsub", &ev);
+    if (m > 0) hipLaunchKernelGGL(k_schur_backsub, dim3((m + T - 1) / T), dim3(T), 0, st, A);
+    prof_end(prof, st, "schur_backsub", ev);
     return hipGetLastError() == hipSuccess ? ORBG_OK : ORBG_EIO;
+}
+
+}  // namespace orbg
+
+namespace orbg {
+
+// ---------------------------------------------------------------------------
+// host: the solve's structure (schur_args.h), in the orders orc_ba_schur_solve pins
+// ---------------------------------------------------------------------------
+void build_schur_plan(int npose, int npoint, int nedge, const int32_t *epose,
+                      const int32_t *epoint, const uint8_t *eactive, const uint8_t *fixed,
+                      SchurPlanHost &P)
+{
+    P = SchurPlanHost{};
+    P.npose = npose;
+    P.npoint = npoint;
+    P.pidx.assign(std::max(npose, 1), -1);
+    for (int i = 0; i < npose; i++)
+        if (!fixed[i]) {
+            P.pidx[i] = P.nfree++;
+            P.free_pose.push_back(i);
+        }
+    const int nfree = P.nfree;
+    if (P.free_pose.empty()) P.free_pose.push_back(0);
+    // active edges per point, ascending pose (stable: at most one edge per (pose, point))
+    P.pt_off.assign(npoint + 1, 0);
+    P.edge_pose.assign(std::max(nedge, 1), 0);
+    for (int e = 0; e < nedge; e++) {
+        P.edge_pose[e] = epose[e];
+        if (eactive[e]) P.pt_off[epoint[e] + 1]++;
+    }
+    for (int q = 0; q < npoint; q++) P.pt_off[q + 1] += P.pt_off[q];
+    P.pt_edges.assign(std::max(P.pt_off[npoint], 1), 0);
+    P.slot_point.assign(std::max(P.pt_off[npoint], 1), 0);
+    {
+        std::vector<int32_t> fill(P.pt_off.begin(), P.pt_off.end() - 1);
+        for (int e = 0; e < nedge; e++)
+            if (eactive[e]) P.pt_edges[fill[epoint[e]]++] = e;
+        for (int q = 0; q < npoint; q++) {
+            std::stable_sort(P.pt_edges.begin() + P.pt_off[q], P.pt_edges.begin() + P.pt_off[q + 1],
+                             [&](int a, int b) { return epose[a] < epose[b]; });
+            for (int a = P.pt_off[q]; a < P.pt_off[q + 1]; a++) P.slot_point[a] = q;
+        }
+    }
+    // (block, pair) in landmark order, then grouped by upper block (i1 <= i2) with a stable
+    // sort: each block's pairs keep the landmark order; the free poses' edge lists likewise
+    struct BP {
+        int64_t key;
+        int2 pr;
+    };
+    std::vector<BP> bps;
+    std::vector<int32_t> pcount(nfree + 1, 0);
+    for (int q = 0; q < npoint; q++)
+        for (int a = P.pt_off[q]; a < P.pt_off[q + 1]; a++) {
+            const int e1 = P.pt_edges[a], i1 = P.pidx[epose[e1]];
+            if (i1 < 0) continue;
+            pcount[i1 + 1]++;
+            for (int b = a; b < P.pt_off[q + 1]; b++) {
+                const int e2 = P.pt_edges[b], i2 = P.pidx[epose[e2]];
+                if (i2 < 0) continue;
+                bps.push_back(BP{(int64_t)i1 * nfree + i2, make_int2(a, e2)});
+            }
+        }
+    for (int i = 0; i < nfree; i++)  // every diagonal block exists (H_pp + lambda I)
+        bps.push_back(BP{(int64_t)i * nfree + i, make_int2(-1, -1)});
+    std::stable_sort(bps.begin(), bps.end(), [](const BP &x, const BP &y) { return x.key < y.key; });
+    P.blk_off.push_back(0);
+    for (size_t s = 0; s < bps.size();) {
+        size_t t = s;
+        while (t < bps.size() && bps[t].key == bps[s].key) t++;
+        P.blk_i1.push_back((int32_t)(bps[s].key / nfree));
+        P.blk_i2.push_back((int32_t)(bps[s].key % nfree));
+        for (size_t u = s; u < t; u++)
+            if (bps[u].pr.x >= 0) P.blk_pairs.push_back(bps[u].pr);
+        P.blk_off.push_back((int32_t)P.blk_pairs.size());
+        s = t;
+    }
+    P.nblk = (int)P.blk_i1.size();
+    if (P.blk_pairs.empty()) P.blk_pairs.push_back(make_int2(0, 0));
+    for (int i = 0; i < nfree; i++) pcount[i + 1] += pcount[i];
+    P.pose_off = pcount;
+    P.pose_slots.assign(std::max(pcount[nfree], 1), 0);
+    {
+        std::vector<int32_t> fill(pcount.begin(), pcount.end() - 1);
+        for (int q = 0; q < npoint; q++)
+            for (int a = P.pt_off[q]; a < P.pt_off[q + 1]; a++) {
+                const int e = P.pt_edges[a], i = P.pidx[epose[e]];
+                if (i >= 0) P.pose_slots[fill[i]++] = a;
+            }
+    }
+    // segments: connected free poses (union-find over the off-diagonal blocks, the root of a
+    // component its least free index), each component's [root, max] interval, overlapping
+    // intervals merged into one segment
+    std::vector<int32_t> par(std::max(nfree, 1));
+    for (int i = 0; i < nfree; i++) par[i] = i;
+    auto find = [&](int x) {
+        while (par[x] != x) x = par[x] = par[par[x]];
+        return x;
+    };
+    for (int b = 0; b < P.nblk; b++)
+        if (P.blk_i1[b] != P.blk_i2[b]) {
+            const int a = find(P.blk_i1[b]), c = find(P.blk_i2[b]);
+            if (a != c) par[std::max(a, c)] = std::min(a, c);
+        }
+    std::vector<int32_t> hi(std::max(nfree, 1), -1);
+    for (int i = 0; i < nfree; i++) {
+        const int r = find(i);
+        hi[r] = std::max(hi[r], i);
+    }
+    std::vector<int32_t> seg_of(std::max(nfree, 1), 0);
+    P.seg_lo.push_back(0);
+    for (int i = 0, end = -1; i < nfree; i++) {
+        if (find(i) == i) end = std::max(end, hi[i]);
+        seg_of[i] = (int)P.seg_lo.size() - 1;
+        if (i == end) P.seg_lo.push_back(i + 1);  // no open interval reaches past i: close
+    }
+    P.nseg = (int)P.seg_lo.size() - 1;
+    P.seg_soff.assign(P.nseg + 1, 0);
+    for (int s = 0; s < P.nseg; s++) {
+        const int64_t n = 6 * (int64_t)(P.seg_lo[s + 1] - P.seg_lo[s]);
+        P.seg_soff[s + 1] = P.seg_soff[s] + n * n;
+        P.max_seg = std::max(P.max_seg, P.seg_lo[s + 1] - P.seg_lo[s]);
+    }
+    P.blk_seg.assign(std::max(P.nblk, 1), 0);
+    for (int b = 0; b < P.nblk; b++) P.blk_seg[b] = seg_of[P.blk_i1[b]];
+    if (P.nblk == 0) {
+        P.blk_i1.push_back(0);
+        P.blk_i2.push_back(0);
+    }
 }
 
 }  // namespace orbg

@@ -206,6 +206,30 @@ class DeviceLBA:
         L.check(L.lib().orbg_ba_graph_set_active(self.ctx.handle, self.graph, a.ctypes.data),
                 "orbg_ba_graph_set_active")
 
+    def schur_plan(self, fixed):
+        """orbg_ba_graph_schur_plan: the Schur structure of the graph for the free poses
+        (fixed[i] != 0: g2o's fixed vertex), built once; set_active rebuilds it."""
+        import torch
+        if self.graph is None:
+            raise ValueError("schur_plan needs a DeviceLBA built with graph=True")
+        f = np.ascontiguousarray(np.asarray(fixed) != 0, np.uint8)
+        L.check(L.lib().orbg_ba_graph_schur_plan(self.ctx.handle, self.graph, f.ctypes.data),
+                "orbg_ba_graph_schur_plan")
+        dev = self.d_hpose.device
+        self.d_dx_pose = torch.zeros((self.np, 6), dtype=torch.float64, device=dev)
+        self.d_dx_point = torch.zeros((self.nq, 3), dtype=torch.float64, device=dev)
+        self.d_ok = torch.zeros(1, dtype=torch.int32, device=dev)
+
+    def schur_solve(self, lam):
+        """BlockSolver<6,3>::solve on the device blocks of the last build_system()
+        (orbg_ba_graph_schur_solve): increments into self.d_dx_pose / self.d_dx_point,
+        self.d_ok, on the context stream with no host copy."""
+        p = lambda t: L.C.c_void_p(t.data_ptr())  # noqa: E731
+        L.check(L.lib().orbg_ba_graph_schur_solve(
+            self.ctx.handle, self.graph, float(lam), p(self.d_hpl), p(self.d_hpose),
+            p(self.d_bpose), p(self.d_hpoint), p(self.d_bpoint), p(self.d_dx_pose),
+            p(self.d_dx_point), p(self.d_ok)), "orbg_ba_graph_schur_solve")
+
     def __del__(self):
         if getattr(self, "graph", None) is not None:
             L.lib().orbg_ba_graph_destroy(self.graph)

@@ -363,3 +363,67 @@ def test_graph_bench_shaped_windows(oracle):
     r2 = run()
     for u, v in zip(r1, r2):
         assert np.array_equal(u, v)
+
+
+def _graph_schur_vs_oracle(oracle, poses, pts, edges, lam_scale, active=None, lam_abs=None):
+    """orbg_ba_graph_schur_solve on the graph's own device blocks vs orc_ba_schur_solve fed
+    the same blocks (downloaded): increments and ok bit for bit."""
+    from orb_slam2_test_amd import _lib as L
+    from orb_slam2_test_amd.optimizer import DeviceLBA
+    g = DeviceLBA(poses, pts, edges, graph=True)
+    g.schur_plan(poses["fixed"])
+    e2 = edges
+    if active is not None:
+        g.set_active(active)
+        e2 = edges.copy()
+        e2["active"] = active
+    g.build_system()
+    g.ctx.sync()  # the build runs on liborbg's stream, not torch's
+    hp = g.d_hpose.cpu().numpy()
+    lam = lam_scale * np.abs(hp.reshape(len(poses), 36)[:, ::7]).max() if lam_abs is None else lam_abs
+    g.schur_solve(lam)
+    g.ctx.sync()
+    ne = len(edges)
+    eo = np.zeros(ne, L.EDGE_OUT_DTYPE)
+    eo["hpl"] = g.d_hpl.cpu().numpy()[:ne]
+    bp, hq, bq = g.d_bpose.cpu().numpy(), g.d_hpoint.cpu().numpy(), g.d_bpoint.cpu().numpy()
+    rok, rdxp, rdxq = oracle.ba_schur_solve(poses, len(pts), e2, eo, hp, bp, hq, bq, lam)
+    ok = int(g.d_ok.cpu().numpy()[0])
+    dxp, dxq = g.d_dx_pose.cpu().numpy(), g.d_dx_point.cpu().numpy()
+    assert ok == rok
+    # (an undamped landmark block of one mono edge is singular: inf / NaN on both sides alike)
+    assert np.array_equal(dxp, rdxp.reshape(dxp.shape), equal_nan=True)
+    assert np.array_equal(dxq, rdxq.reshape(dxq.shape), equal_nan=True)
+    return g, ok, dxp, dxq
+
+
+@pytest.mark.parametrize("seed,lam_scale", [(8, 1e-5), (9, 1e-3)])
+def test_graph_schur_solve_full_window(oracle, seed, lam_scale):
+    """The device-resident LM solve at the bench's window size (20 KFs, 6000 points): plan
+    once, build -> solve on one stream, bit-exact vs the oracle on the same blocks."""
+    poses, pts, edges = S.ba_window(seed=seed, n_points=6000)
+    _, ok, dxp, _ = _graph_schur_vs_oracle(oracle, poses, pts, edges, lam_scale)
+    assert ok and np.abs(dxp).max() > 0
+
+
+def test_graph_schur_solve_batched_windows_and_outliers(oracle):
+    """4 independent windows in one graph (4 dense systems, one workgroup each), then the
+    outlier pass's set_active (the structure is rebuilt): still bit-exact."""
+    poses, pts, edges = concat_windows([S.ba_window(seed=600 + i, n_points=2500) for i in range(4)])
+    act = (np.arange(len(edges)) % 7 != 0).astype(np.uint8)
+    for a in (None, act):
+        _, ok, _, dxq = _graph_schur_vs_oracle(oracle, poses, pts, edges, 1e-4, a)
+        assert ok and np.abs(dxq).max() > 0
+
+
+def test_graph_schur_solve_degenerate(oracle):
+    """Every pose fixed (only the landmark blocks are solved: lambda 1, as
+    test_schur_solve_degenerate; and lambda 0, singular landmark blocks) and a zero lambda with
+    free poses (ok is the oracle's)."""
+    poses, pts, edges = S.ba_window(seed=6, n_points=300)
+    pf = poses.copy()
+    pf["fixed"] = 1
+    _, _, _, dxq = _graph_schur_vs_oracle(oracle, pf, pts, edges, 0.0, lam_abs=1.0)
+    assert np.isfinite(dxq).all() and np.abs(dxq).max() > 0
+    _graph_schur_vs_oracle(oracle, pf, pts, edges, 0.0, lam_abs=0.0)
+    _graph_schur_vs_oracle(oracle, poses, pts, edges, 0.0)

@@ -50,6 +50,9 @@ def main():
     ap.add_argument("--edge-errors", action="store_true",
                     help="also store eout.err / chi2 / rho1 in the linearisation pass "
                          "(orbg_ba_set_edge_errors; the iteration's error pass provides them)")
+    ap.add_argument("--no-solve", action="store_true",
+                    help="skip the full LM iteration line (build + errors + the device-resident "
+                         "Schur solve, orbg_ba_graph_schur_solve)")
     args = ap.parse_args()
 
     import torch
@@ -171,6 +174,40 @@ def main():
                                "entries (42 of the 8x8 tile's 64) x the rows that are not "
                                "padding; mfma_frac = SQ_VALU_MFMA_BUSY_CYCLES / (1024 SIMDs x "
                                "GPU cycles) from the committed PMC pass (pmc_source)"}
+    if use_graph and not args.no_solve:
+        # g2o's whole LM iteration on the device: buildSystem + computeActiveErrors + the
+        # Schur solve (setLambda, BlockSolver<6,3>::solve), one stream, no host copy
+        lba.schur_plan(poses["fixed"])
+        lam = 1e-4 * float(np.abs(lba.d_hpose.cpu().numpy().reshape(len(poses), 36)[:, ::7]).max())
+
+        def lm_iteration():
+            lba.build_system()
+            lba.errors()
+            lba.schur_solve(lam)
+
+        for _ in range(args.warmup):
+            lm_iteration()
+        lba.ctx.sync()
+        t0 = time.perf_counter()
+        for _ in range(args.iters):
+            lm_iteration()
+        lba.ctx.sync()
+        ldt = time.perf_counter() - t0
+        lba.ctx.profile(True)
+        lba.ctx.profile_reset()
+        for _ in range(args.iters):
+            lba.schur_solve(lam)
+        lba.ctx.sync()
+        sk = lba.ctx.profile_read()
+        lba.ctx.profile(False)
+        out["lm_iteration"] = {
+            "what": "orbg_ba_graph_build_system + orbg_ba_graph_errors + orbg_ba_graph_schur_solve "
+                    "(Schur products on v_mfma_f64_4x4x4f64, one dense LDLT per window)",
+            "ms_per_iter": round(ldt / args.iters * 1e3, 4),
+            "edges_per_s": round(ne * args.iters / ldt, 1),
+            "schur_ms": round(sum(v[0] for k, v in sk.items() if k.startswith("schur")) / args.iters, 4),
+            "schur_kernels_ms": {k: round(v[0] / args.iters, 4) for k, v in sk.items()},
+            "ok": int(lba.d_ok.cpu().numpy()[0]), "lambda": lam}
     if not args.no_cpu:
         from oracle import pyoracle as O
         p, q, e = base[0]
