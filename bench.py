@@ -261,6 +261,11 @@ def main():
                     help="mono: the full batched-sequence step, with the pose/trajectory stub "
                          "of every pair (orbg_match_pose_batch_device) gathered beside the "
                          "summary and vnMatches12 rows (SURVEY.md 8e); not the headline metric")
+    ap.add_argument("--host-input", action="store_true",
+                    help="host-fed frames: the blocks sit in pinned host memory and every step's "
+                         "block is copied H2D on a copy stream (3 device staging slots) "
+                         "overlapped with the previous steps' extraction; PCIe-inclusive "
+                         "frames/s, a second line beside the device-resident headline")
     ap.add_argument("--force-collective", action="store_true",
                     help="run the per-step RCCL all_gathers even at world size 1 (a one-rank "
                          "nccl process group): exercises the multi-GPU gather path on one GPU")
@@ -344,6 +349,45 @@ def main():
         it[0] += 1
         bstep(d.data_ptr(), W, H)
 
+    h2d = None
+    if args.host_input:
+        # Frame.cc:310-316 / mono_kitti.cc:78-90 read frames from host memory: here every
+        # step's block goes H2D on its own stream into one of 3 device slots while the
+        # extraction of the steps before runs; the copy of step k + 2 waits until step k's
+        # outputs are written (orbg_batch_acquire: the last reads of its input, IC_Angle's
+        # level-0 patches, are done by then), so a slot is never overwritten while read
+        h_blocks = [torch.from_numpy(b).pin_memory() for b in blocks]
+        stage = [torch.empty_like(d_blocks[0]) for _ in range(3)]
+        cstream = torch.cuda.Stream()
+        ev_copy = [torch.cuda.Event() for _ in range(3)]
+        pend = [0]
+
+        def issue_copy(j):
+            with torch.cuda.stream(cstream):
+                stage[j % 3].copy_(h_blocks[j % nblocks], non_blocking=True)
+                ev_copy[j % 3].record(cstream)
+
+        # the H2D rate alone (the bound of a host-fed pipeline)
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for j in range(4):
+            issue_copy(j)
+        torch.cuda.synchronize()
+        h2d = 4 * h_blocks[0].numel() / (time.perf_counter() - t0) / 1e9
+        issue_copy(0)
+        issue_copy(1)
+        pend[0] = 2
+
+        def step():  # noqa: F811 -- the host-fed step replaces the resident one
+            k = it[0]
+            it[0] += 1
+            stream.wait_event(ev_copy[k % 3])
+            bstep(stage[k % 3].data_ptr(), W, H)
+            ext.ctx.batch_acquire(cstream.cuda_stream)
+            ext.ctx.batch_release(cstream.cuda_stream)
+            issue_copy(pend[0])
+            pend[0] += 1
+
     for _ in range(args.warmup):
         step()
     torch.cuda.synchronize()
@@ -373,7 +417,7 @@ def main():
     # kernels of two batches and three streams overlap, and an event pair around a kernel
     # would time its neighbours too.
     kern = {}
-    if not args.no_kernel_timing:
+    if not args.no_kernel_timing and not args.host_input:
         ext.ctx.set_serial(True)
 
         def step_serial():
@@ -456,9 +500,11 @@ def main():
             if args.with_pose:
                 workload += (" + pose stub (PoseOptimization over the matches, 10 m "
                              "back-projection) gathered with the summary")
+        metric = (METRIC_STEREO if args.stereo else METRIC_EXTRACT if args.extract_only else METRIC)
+        if args.host_input:
+            metric += " -- host-fed (pinned host frames, H2D copies overlapped, PCIe-inclusive)"
         out = {
-            "metric": (METRIC_STEREO if args.stereo else
-                       METRIC_EXTRACT if args.extract_only else METRIC), "value": round(value, 2),
+            "metric": metric, "value": round(value, 2),
             "unit": "stereo frames/s" if args.stereo else "frames/s", "n_gpus": world,
             "steps": args.steps, "warmup": args.warmup,
             "ms_per_step": round(elapsed / args.steps * 1e3, 4), "higher_is_better": True,
@@ -486,6 +532,12 @@ def main():
                                   "achieved_GBps": round(value * fab / 1e9, 1),
                                   "frac": round(value * fab / 1e9 / HBM_PEAK_GBS, 4)},
             "kernels": kstats,
+            "host_input": ({"h2d_GBps_alone": round(h2d, 2),
+                            "input_bytes_per_frame": W * H,
+                            "h2d_bound_frames_per_s": round(h2d * 1e9 / (W * H), 1),
+                            "staging": "3 device slots, copy stream, the copy of step k+2 after "
+                                       "step k's outputs (orbg_batch_acquire)"}
+                           if args.host_input else None),
             "candidates_per_image": round(ncand / nimg, 1),
             "keypoints_per_image": round(nkp / nimg, 1),
         }

@@ -279,6 +279,41 @@ int orc_search_for_triangulation(const orc_tri_kf *kf1, const orc_tri_kf *kf2,
                                  const float *sigma2, int only_stereo, int check_ori,
                                  int32_t *matches12);
 void orc_three_maxima(const int *hsize, int *ind1, int *ind2, int *ind3);
+/* LocalMapping::CreateNewMapPoints (src/LocalMapping.cc:293-560) and ComputeF12 (:690-707).
+ * A KeyFrame's pose (Tcw rows 0..2) and calibration as they read it. */
+typedef struct {
+    float Tcw[12];
+    float fx, fy, cx, cy, invfx, invfy, mb, mbf;
+} orc_kf_cam;
+/* the keypoint side: mvKeysUn, mvKeys (UnprojectStereo; NULL: mvKeysUn), mvuRight (NULL: all
+ * monocular), mvDepth */
+typedef struct {
+    const orc_keypoint *kps;
+    const orc_keypoint *kps_raw;
+    const float *uright;
+    const float *depth;
+    int32_t n;
+} orc_kf_tri;
+/* per-match outcome: the reference's `continue`s in order */
+enum {
+    ORC_TRI_NONE = 0, ORC_TRI_NEW = 1, ORC_TRI_PARALLAX = -1, ORC_TRI_W0 = -2, ORC_TRI_Z1 = -3,
+    ORC_TRI_Z2 = -4, ORC_TRI_REPROJ1 = -5, ORC_TRI_REPROJ2 = -6, ORC_TRI_DIST0 = -7,
+    ORC_TRI_SCALE = -8
+};
+/* glibc's atan2f restated (fdlibm e_atan2f.c / s_atanf.c) */
+float orc_atan2f(float y, float x);
+long orc_atan2f_check(uint32_t seed, long n);
+/* g = F12 = ComputeF12(pKF1, pKF2), pKF1->GetCameraCenter(), pKF2's Tcw and intrinsics */
+void orc_tri_geometry(const orc_kf_cam *c1, const orc_kf_cam *c2, orc_tri_geom *g);
+/* the null vector of a 4x4 float matrix (double Jacobi on A^T A), the cv::SVD stand-in */
+void orc_tri_nullvec(const float *A, double *v);
+/* the triangulation loop over matches12 (SearchForTriangulation's vMatchedPairs as vMatches12):
+ * status[i] (ORC_TRI_*) and x3d[3i..3i+2] (the new MapPoint's position when NEW, else 0) for
+ * i < k1->n; scale_factors / sigma2 = mvScaleFactors / mvLevelSigma2, scale_factor =
+ * pKF1->mfScaleFactor.  Returns the new points. */
+int orc_triangulate(const orc_kf_tri *k1, const orc_kf_tri *k2, const orc_kf_cam *c1,
+                    const orc_kf_cam *c2, const int32_t *matches12, const float *scale_factors,
+                    const float *sigma2, float scale_factor, float *x3d, int8_t *status);
 /* ORBmatcher::Fuse(pKF, vpMapPoints, th)'s per-MapPoint search: kf = the KeyFrame's mvKeysUn,
  * mDescriptors, mvuRight (n; the FeatureVector is not read), cam = its pose, intrinsics,
  * mbf, mfLogScaleFactor, mnScaleLevels and bounds; mps[i] (flags ORC_MP_VALID: pMP &&

@@ -65,6 +65,19 @@ TRI_GEOM_DTYPE = np.dtype([("F12", "<f4", 9), ("Cw1", "<f4", 3), ("Tcw2", "<f4",
                            ("fx2", "<f4"), ("fy2", "<f4"), ("cx2", "<f4"), ("cy2", "<f4")])
 
 
+# CreateNewMapPoints camera record (orb_oracle.h orc_kf_cam) and status codes (ORC_TRI_*)
+KF_CAM_DTYPE = np.dtype([("Tcw", "<f4", 12), ("fx", "<f4"), ("fy", "<f4"), ("cx", "<f4"),
+                         ("cy", "<f4"), ("invfx", "<f4"), ("invfy", "<f4"), ("mb", "<f4"),
+                         ("mbf", "<f4")])
+TRI_NONE, TRI_NEW, TRI_PARALLAX, TRI_W0, TRI_Z1, TRI_Z2 = 0, 1, -1, -2, -3, -4
+TRI_REPROJ1, TRI_REPROJ2, TRI_DIST0, TRI_SCALE = -5, -6, -7, -8
+
+
+class KFTri(C.Structure):
+    _fields_ = [("kps", C.c_void_p), ("kps_raw", C.c_void_p), ("uright", C.c_void_p),
+                ("depth", C.c_void_p), ("n", C.c_int32)]
+
+
 class TriKF(C.Structure):
     _fields_ = [("kps", C.c_void_p), ("desc", C.c_void_p), ("uright", C.c_void_p),
                 ("has_mp", C.c_void_p), ("n", C.c_int32), ("fv_nodes", C.c_void_p),
@@ -202,6 +215,14 @@ def lib():
         L.orc_search_for_triangulation.argtypes = [P(TriKF), P(TriKF), vp, vp, vp, C.c_int,
                                                    C.c_int, vp]
         L.orc_search_for_triangulation.restype = C.c_int
+        L.orc_atan2f.argtypes = [C.c_float, C.c_float]
+        L.orc_atan2f.restype = C.c_float
+        L.orc_atan2f_check.argtypes = [C.c_uint32, C.c_long]
+        L.orc_atan2f_check.restype = C.c_long
+        L.orc_tri_geometry.argtypes = [vp, vp, vp]
+        L.orc_tri_nullvec.argtypes = [vp, vp]
+        L.orc_triangulate.argtypes = [P(KFTri), P(KFTri), vp, vp, vp, vp, vp, C.c_float, vp, vp]
+        L.orc_triangulate.restype = C.c_int
         L.orc_fuse_search.argtypes = [P(TriKF), vp, vp, vp, C.c_int, C.c_float, vp, vp, vp, vp]
         L.orc_fuse_search.restype = C.c_int
         L.orc_fuse_sim3_search.argtypes = [P(TriKF), vp, vp, vp, C.c_int, C.c_float, vp, vp, vp]
@@ -751,6 +772,75 @@ def search_for_triangulation(kf1, kf2, geom, scale_factors, sigma2, only_stereo=
     n = lib().orc_search_for_triangulation(C.byref(a), C.byref(b), _p(g), _p(sf), _p(s2),
                                            int(only_stereo), int(check_ori), _p(m))
     return n, m[:a.n]
+
+
+def atan2f(y, x):
+    """glibc atan2f restated (orc_atan2f)."""
+    return lib().orc_atan2f(float(y), float(x))
+
+
+def atan2f_check(seed, n):
+    """Bit mismatches of orc_atan2f vs the host libm's atan2f over n sampled pairs."""
+    return lib().orc_atan2f_check(int(seed), int(n))
+
+
+def kf_cam(Tcw, fx, fy, cx, cy, mb=0.0, mbf=0.0):
+    """orc_kf_cam of a KeyFrame: Tcw (3x4 float32), intrinsics, invfx = 1/fx (Frame.cc
+    float division), mb, mbf."""
+    c = np.zeros((), KF_CAM_DTYPE)
+    c["Tcw"] = np.asarray(Tcw, np.float32).reshape(-1)[:12]
+    c["fx"], c["fy"], c["cx"], c["cy"] = fx, fy, cx, cy
+    c["invfx"] = np.float32(1.0) / np.float32(fx)
+    c["invfy"] = np.float32(1.0) / np.float32(fy)
+    c["mb"], c["mbf"] = mb, mbf
+    return c
+
+
+def tri_geometry(c1, c2):
+    """LocalMapping::ComputeF12(pKF1, pKF2) + the SearchForTriangulation geometry record."""
+    a = np.ascontiguousarray(c1, KF_CAM_DTYPE)
+    b = np.ascontiguousarray(c2, KF_CAM_DTYPE)
+    g = np.zeros((), TRI_GEOM_DTYPE)
+    lib().orc_tri_geometry(_p(a), _p(b), _p(g))
+    return g
+
+
+def tri_nullvec(A):
+    """The oracle's cv::SVD stand-in: null vector (double) of a 4x4 float matrix."""
+    a = np.ascontiguousarray(A, np.float32).reshape(16)
+    v = np.zeros(4, np.float64)
+    lib().orc_tri_nullvec(_p(a), _p(v))
+    return v
+
+
+def _kf_tri(kf, keep):
+    kps = np.ascontiguousarray(kf["kps"], KP_DTYPE)
+    raw = kf.get("kps_raw")
+    raw = None if raw is None else np.ascontiguousarray(raw, KP_DTYPE)
+    ur = kf.get("uright")
+    ur = None if ur is None else np.ascontiguousarray(ur, np.float32)
+    dp = kf.get("depth")
+    dp = None if dp is None else np.ascontiguousarray(dp, np.float32)
+    keep += [kps, raw, ur, dp]
+    return KFTri(_p(kps), _p(raw), _p(ur), _p(dp), len(kps))
+
+
+def triangulate(kf1, kf2, c1, c2, matches12, scale_factors, sigma2, scale_factor):
+    """CreateNewMapPoints' triangulation of the matched pairs -> (nnew, x3d[n1, 3], status[n1]).
+    kf: dict(kps = mvKeysUn, kps_raw = mvKeys, uright, depth)."""
+    keep = []
+    a, b = _kf_tri(kf1, keep), _kf_tri(kf2, keep)
+    ca = np.ascontiguousarray(c1, KF_CAM_DTYPE)
+    cb = np.ascontiguousarray(c2, KF_CAM_DTYPE)
+    m = np.ascontiguousarray(matches12, np.int32)
+    assert len(m) == a.n
+    sf = np.ascontiguousarray(scale_factors, np.float32)
+    s2 = np.ascontiguousarray(sigma2, np.float32)
+    x = np.zeros((max(a.n, 1), 3), np.float32)
+    st = np.zeros(max(a.n, 1), np.int8)
+    n = lib().orc_triangulate(C.byref(a), C.byref(b), _p(ca), _p(cb), _p(m), _p(sf), _p(s2),
+                              float(scale_factor), _p(x), _p(st))
+    return n, x[:a.n], st[:a.n]
 
 
 def fuse_search(kf, fcam, mps, mdesc, th, scale_factors, inv_sigma2):
