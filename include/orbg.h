@@ -545,6 +545,65 @@ int orbg_search_for_triangulation(orbg_ctx *ctx, const orbg_keyframe *kf1, const
                                   const orbg_triangulation_pair *geo, int only_stereo,
                                   int check_ori, int32_t *matches12, int *nmatches);
 
+/* LocalMapping::CreateNewMapPoints (src/LocalMapping.cc:293-560) around that search: the
+ * pair's geometry before it (ComputeF12, :690-707) and the triangulation of its matches after
+ * it (:395-560).  A KeyFrame's pose and calibration as they read them: mTcw rows 0..2
+ * (row-major 3x4), fx, fy, cx, cy, invfx, invfy, mb, mbf. */
+typedef struct {
+    float Tcw[12];
+    float fx, fy, cx, cy, invfx, invfy, mb, mbf;
+} orbg_kf_camera;
+/* d_geo[p] = the orbg_triangulation_pair of KeyFrames d_kf1[p] (current) and d_kf2[p]
+ * (neighbour), cameras d_cams[kf]: F12 = K1^-T [t12]x R12 K2^-1 in the reference's float
+ * evaluation (A.inv()*B as solve(), K2.inv() closed form, gemms in double), pKF1's camera
+ * centre, pKF2's pose and intrinsics.  Context stream. */
+int orbg_triangulation_geometry_batch_device(orbg_ctx *ctx, const orbg_kf_camera *d_cams,
+                                             const int32_t *d_kf1, const int32_t *d_kf2,
+                                             int npairs, orbg_triangulation_pair *d_geo);
+/* The same for one pair from host structs. */
+int orbg_triangulation_geometry(orbg_ctx *ctx, const orbg_kf_camera *cam1,
+                                const orbg_kf_camera *cam2, orbg_triangulation_pair *geo);
+/* Per-match outcome of the triangulation, the reference's `continue`s in order: */
+enum {
+    ORBG_TRI_NONE = 0,      /* no match (matches12[i] < 0) */
+    ORBG_TRI_NEW = 1,       /* a new MapPoint at x3d */
+    ORBG_TRI_PARALLAX = -1, /* no stereo and too little parallax */
+    ORBG_TRI_W0 = -2,       /* the homogeneous solution's w == 0 */
+    ORBG_TRI_Z1 = -3,       /* behind pKF1 */
+    ORBG_TRI_Z2 = -4,       /* behind pKF2 */
+    ORBG_TRI_REPROJ1 = -5,  /* chi-square gate in pKF1 (5.991 mono / 7.8 stereo) */
+    ORBG_TRI_REPROJ2 = -6,  /* ... in pKF2 */
+    ORBG_TRI_DIST0 = -7,    /* at a camera centre */
+    ORBG_TRI_SCALE = -8     /* scale inconsistency (ratioFactor = 1.5 mfScaleFactor) */
+};
+/* For pairs p (KeyFrames d_kf1[p], d_kf2[p] of `kfs`: mvKeysUn, mvuRight, counts read; mvKeys
+ * d_kps_raw + kf * cap for UnprojectStereo (NULL: mvKeysUn), mvDepth d_depth + kf * cap
+ * (read where mvuRight >= 0; required with uright), cameras d_cams[kf]) and their
+ * SearchForTriangulation output d_matches12 + p * cap: d_status[p * cap + i] (ORBG_TRI_*)
+ * and d_x3d[3 (p * cap + i) ..] (the new point when NEW, else 0) for i < N of pKF1,
+ * d_nnew[p] = new points.  The MapPoint creation itself (new MapPoint, AddObservation,
+ * ComputeDistinctiveDescriptors, UpdateNormalAndDepth, mlpRecentAddedMapPoints) is the
+ * caller's, in i order.  Scale factors / sigma^2 / mfScaleFactor are the
+ * context's.  A match past pKF2's N counts as no match.  Context stream. */
+int orbg_triangulate_batch_device(orbg_ctx *ctx, const orbg_keyframes *kfs,
+                                  const orbg_keypoint *d_kps_raw, const float *d_depth, int cap,
+                                  const orbg_kf_camera *d_cams, const int32_t *d_kf1,
+                                  const int32_t *d_kf2, const int32_t *d_matches12, int npairs,
+                                  float *d_x3d, int8_t *d_status, int32_t *d_nnew);
+/* One KeyFrame's triangulation inputs from host arrays (kps_raw / uright may be NULL; depth
+ * required with uright) */
+typedef struct {
+    const orbg_keypoint *kps;
+    const orbg_keypoint *kps_raw;
+    const float *uright;
+    const float *depth;
+    int32_t n;
+} orbg_keyframe_geo;
+/* One pair from host arrays: status[kf1->n], x3d[3 kf1->n], *nnew. */
+int orbg_triangulate(orbg_ctx *ctx, const orbg_keyframe_geo *kf1, const orbg_keyframe_geo *kf2,
+                     const orbg_kf_camera *cam1, const orbg_kf_camera *cam2,
+                     const int32_t *matches12, float *x3d, int8_t *status, int *nnew);
+
 /* ORBmatcher::Fuse(pKF, vpMapPoints, th) (src/ORBmatcher.cc:968-1107) splits into a search,
  * per MapPoint independent of the others (projection with pKF's pose, IsInImage, the
  * [0.8 dmin, 1.2 dmax] and 60-degree gates, PredictScale, GetFeaturesInArea(u, v, th *

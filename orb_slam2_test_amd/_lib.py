@@ -71,6 +71,20 @@ TRI_GEOM_DTYPE = np.dtype([("F12", "<f4", 9), ("Cw1", "<f4", 3), ("Tcw2", "<f4",
                            ("fx2", "<f4"), ("fy2", "<f4"), ("cx2", "<f4"), ("cy2", "<f4")])
 
 
+# CreateNewMapPoints (include/orbg.h orbg_kf_camera, ORBG_TRI_*)
+KF_CAMERA_DTYPE = np.dtype([("Tcw", "<f4", 12), ("fx", "<f4"), ("fy", "<f4"), ("cx", "<f4"),
+                            ("cy", "<f4"), ("invfx", "<f4"), ("invfy", "<f4"), ("mb", "<f4"),
+                            ("mbf", "<f4")])
+TRI_NONE, TRI_NEW, TRI_PARALLAX, TRI_W0, TRI_Z1, TRI_Z2 = 0, 1, -1, -2, -3, -4
+TRI_REPROJ1, TRI_REPROJ2, TRI_DIST0, TRI_SCALE = -5, -6, -7, -8
+
+
+class KeyFrameGeo(C.Structure):
+    """orbg_keyframe_geo (include/orbg.h): one KeyFrame's triangulation inputs, host arrays."""
+    _fields_ = [("kps", C.c_void_p), ("kps_raw", C.c_void_p), ("uright", C.c_void_p),
+                ("depth", C.c_void_p), ("n", C.c_int32)]
+
+
 class KeyFrames(C.Structure):
     """orbg_keyframes (include/orbg.h): a set of KeyFrames in device memory."""
     _fields_ = [("desc", C.c_void_p), ("kps", C.c_void_p), ("uright", C.c_void_p),
@@ -253,6 +267,12 @@ def lib():
                                                 P(i32)]),
         "orbg_search_for_triangulation_batch_device": (i32, [vp, P(KeyFrames), i32, vp, vp, vp,
                                                              i32, i32, i32, vp, vp]),
+        "orbg_triangulation_geometry": (i32, [vp, vp, vp, vp]),
+        "orbg_triangulation_geometry_batch_device": (i32, [vp, vp, vp, vp, i32, vp]),
+        "orbg_triangulate": (i32, [vp, P(KeyFrameGeo), P(KeyFrameGeo), vp, vp, vp, vp, vp,
+                                   P(i32)]),
+        "orbg_triangulate_batch_device": (i32, [vp, P(KeyFrames), vp, vp, i32, vp, vp, vp, vp,
+                                                i32, vp, vp, vp]),
         "orbg_search_by_bow_kf": (i32, [vp, vp, vp, vp, i32, vp, vp, vp, i32, vp, vp, vp, i32, vp, vp,
                                         vp, i32, f32, i32, vp, P(i32)]),
         "orbg_search_by_bow_kf_batch_device": (i32, [vp, P(BowFrames), P(BowFrames), i32, vp, vp,

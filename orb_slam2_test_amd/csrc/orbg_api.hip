@@ -81,6 +81,13 @@ int launch_tri_match(hipStream_t st, const orbg_keyframes &K, int cap, const int
                      const int32_t *kf2, const orbg_triangulation_pair *geo, int npairs,
                      const float *scale, const float *sigma2, int nlevels, int only_stereo,
                      int check_ori, int32_t *match, int32_t *nmatch);
+int launch_tri_geometry(hipStream_t st, const orbg_kf_camera *cams, const int32_t *kf1,
+                        const int32_t *kf2, int npairs, orbg_triangulation_pair *geo);
+int launch_triangulate(hipStream_t st, const orbg_keyframes &K, const orbg_keypoint *kps_raw,
+                       const float *depth, int cap, const orbg_kf_camera *cams, const int32_t *kf1,
+                       const int32_t *kf2, const int32_t *m12, int npairs, const float *scale,
+                       const float *sigma2, int nlevels, float scale_factor, float *x3d,
+                       int8_t *status, int32_t *nnew);
 int launch_fuse(hipStream_t st, const orbg_keyframes &K, int cap, const int32_t *kf,
                 const orbg_frustum_camera *cams, const orbg_map_point *mps, const uint8_t *mdesc,
                 const int32_t *mcounts, int mcap, int npairs, float th, const float *scale,
@@ -4430,6 +4437,153 @@ extern "C" int orbg_search_for_triangulation(orbg_ctx *c, const orbg_keyframe *k
     HIPCHK(hipStreamSynchronize(c->stream));
     memcpy(matches12, hs + o_m, (size_t)kf1->n * 4);
     memcpy(nmatches, hs + o_nm, 4);
+    return ORBG_OK;
+}
+
+extern "C" int orbg_triangulation_geometry_batch_device(orbg_ctx *c, const orbg_kf_camera *d_cams,
+                                                        const int32_t *d_kf1, const int32_t *d_kf2,
+                                                        int npairs, orbg_triangulation_pair *d_geo)
+{
+    if (!c) return set_err(ORBG_EINVAL, "NULL context");
+    if (npairs < 0) return set_err(ORBG_EINVAL, "bad npairs");
+    if (npairs == 0) return ORBG_OK;
+    if (!d_cams || !d_kf1 || !d_kf2 || !d_geo) return set_err(ORBG_EINVAL, "NULL device array");
+    HIPCHK(hipSetDevice(c->device));
+    hipStream_t st = c->stream;
+    int rc = 0;
+    PROF_LAUNCH(c, "tri_geometry",
+                rc = launch_tri_geometry(st, d_cams, d_kf1, d_kf2, npairs, d_geo));
+    if (rc) return set_err(ORBG_EIO, "k_tri_geometry launch failed");
+    return ORBG_OK;
+}
+
+extern "C" int orbg_triangulation_geometry(orbg_ctx *c, const orbg_kf_camera *cam1,
+                                           const orbg_kf_camera *cam2, orbg_triangulation_pair *geo)
+{
+    if (!c || !cam1 || !cam2 || !geo) return set_err(ORBG_EINVAL, "NULL argument");
+    HIPCHK(hipSetDevice(c->device));
+    const size_t o_cam = 0, o_idx = al256(2 * sizeof(orbg_kf_camera)), o_geo = o_idx + 256,
+                 o = o_geo + al256(sizeof(orbg_triangulation_pair));
+    uint8_t *hs;
+    int rc = stage(c, o, &hs);
+    if (rc) return rc;
+    void *d;
+    if ((rc = scratch(c, o, &d))) return rc;
+    uint8_t *db = (uint8_t *)d;
+    HIPCHK(hipStreamSynchronize(c->stream));
+    memcpy(hs + o_cam, cam1, sizeof(orbg_kf_camera));
+    memcpy(hs + o_cam + sizeof(orbg_kf_camera), cam2, sizeof(orbg_kf_camera));
+    ((int32_t *)(hs + o_idx))[0] = 0;
+    ((int32_t *)(hs + o_idx))[1] = 1;
+    HIPCHK(hipMemcpyAsync(db, hs, o_geo, hipMemcpyHostToDevice, c->stream));
+    const int32_t *di = (const int32_t *)(db + o_idx);
+    rc = launch_tri_geometry(c->stream, (const orbg_kf_camera *)(db + o_cam), di, di + 1, 1,
+                             (orbg_triangulation_pair *)(db + o_geo));
+    if (rc) return set_err(ORBG_EIO, "k_tri_geometry launch failed");
+    HIPCHK(hipMemcpyAsync(hs + o_geo, db + o_geo, sizeof(orbg_triangulation_pair),
+                          hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(hipStreamSynchronize(c->stream));
+    memcpy(geo, hs + o_geo, sizeof(orbg_triangulation_pair));
+    return ORBG_OK;
+}
+
+extern "C" int orbg_triangulate_batch_device(orbg_ctx *c, const orbg_keyframes *kfs,
+                                             const orbg_keypoint *d_kps_raw, const float *d_depth,
+                                             int cap, const orbg_kf_camera *d_cams,
+                                             const int32_t *d_kf1, const int32_t *d_kf2,
+                                             const int32_t *d_matches12, int npairs, float *d_x3d,
+                                             int8_t *d_status, int32_t *d_nnew)
+{
+    if (!c || !kfs) return set_err(ORBG_EINVAL, "NULL argument");
+    if (npairs < 0 || cap <= 0) return set_err(ORBG_EINVAL, "bad npairs / cap");
+    if (npairs == 0) return ORBG_OK;
+    if (npairs > 65535) return set_err(ORBG_ENOTSUP, "more than 65535 pairs per call");
+    if (!kfs->kps || !kfs->counts || !d_cams || !d_kf1 || !d_kf2 || !d_matches12 || !d_x3d ||
+        !d_status || !d_nnew)
+        return set_err(ORBG_EINVAL, "NULL device array");
+    if (kfs->uright && !d_depth) return set_err(ORBG_EINVAL, "mvuRight without mvDepth");
+    HIPCHK(hipSetDevice(c->device));
+    hipStream_t st = c->stream;
+    int rc = 0;
+    PROF_LAUNCH(c, "triangulate",
+                rc = launch_triangulate(st, *kfs, d_kps_raw, d_depth, cap, d_cams, d_kf1,
+                                        d_kf2, d_matches12, npairs, c->scale, c->sigma2,
+                                        c->p.nlevels, c->p.scale_factor, d_x3d, d_status, d_nnew));
+    if (rc) return set_err(ORBG_EIO, "k_triangulate launch failed");
+    return ORBG_OK;
+}
+
+extern "C" int orbg_triangulate(orbg_ctx *c, const orbg_keyframe_geo *kf1,
+                                const orbg_keyframe_geo *kf2, const orbg_kf_camera *cam1,
+                                const orbg_kf_camera *cam2, const int32_t *matches12, float *x3d,
+                                int8_t *status, int *nnew)
+{
+    if (!c || !kf1 || !kf2 || !cam1 || !cam2 || !nnew) return set_err(ORBG_EINVAL, "NULL argument");
+    const orbg_keyframe_geo *ks[2] = {kf1, kf2};
+    for (const orbg_keyframe_geo *k : ks) {
+        if (k->n < 0 || (k->n && !k->kps)) return set_err(ORBG_EINVAL, "bad KeyFrame arrays");
+        if (k->n && k->uright && !k->depth) return set_err(ORBG_EINVAL, "mvuRight without mvDepth");
+    }
+    if (kf1->n && (!matches12 || !x3d || !status)) return set_err(ORBG_EINVAL, "NULL output");
+    *nnew = 0;
+    if (!kf1->n) return ORBG_OK;
+    HIPCHK(hipSetDevice(c->device));
+    const int cap = std::max(kf1->n, kf2->n);
+    const size_t cp = (size_t)cap;
+    size_t o = 0;
+    auto take = [&](size_t bytes) {
+        const size_t r = o;
+        o += al256(bytes);
+        return r;
+    };
+    const size_t o_kps = take(2 * cp * sizeof(orbg_keypoint)),
+                 o_raw = take(2 * cp * sizeof(orbg_keypoint)), o_ur = take(2 * cp * 4),
+                 o_dp = take(2 * cp * 4), o_cnt = take(8), o_idx = take(8),
+                 o_cam = take(2 * sizeof(orbg_kf_camera)), o_m = take(cp * 4),
+                 o_x = take(cp * 12), o_st = take(cp), o_nn = take(4);
+    uint8_t *hs;
+    int rc = stage(c, o, &hs);
+    if (rc) return rc;
+    void *d;
+    if ((rc = scratch(c, o, &d))) return rc;
+    uint8_t *db = (uint8_t *)d;
+    HIPCHK(hipStreamSynchronize(c->stream));
+    memset(hs, 0, o_x);
+    for (int s = 0; s < 2; s++) {
+        const orbg_keyframe_geo *k = ks[s];
+        const size_t n = (size_t)k->n;
+        memcpy(hs + o_kps + s * cp * sizeof(orbg_keypoint), k->kps, n * sizeof(orbg_keypoint));
+        memcpy(hs + o_raw + s * cp * sizeof(orbg_keypoint), k->kps_raw ? k->kps_raw : k->kps,
+               n * sizeof(orbg_keypoint));
+        float *ur = (float *)(hs + o_ur) + s * cp, *dp = (float *)(hs + o_dp) + s * cp;
+        for (size_t i = 0; i < n; i++) {
+            ur[i] = k->uright ? k->uright[i] : -1.0f;
+            dp[i] = k->uright ? k->depth[i] : 0.0f;
+        }
+        ((int32_t *)(hs + o_cnt))[s] = k->n;
+        ((int32_t *)(hs + o_idx))[s] = s;
+    }
+    memcpy(hs + o_cam, cam1, sizeof(orbg_kf_camera));
+    memcpy(hs + o_cam + sizeof(orbg_kf_camera), cam2, sizeof(orbg_kf_camera));
+    memcpy(hs + o_m, matches12, (size_t)kf1->n * 4);
+    for (int i = kf1->n; i < cap; i++) ((int32_t *)(hs + o_m))[i] = -1;
+    HIPCHK(hipMemcpyAsync(db, hs, o_x, hipMemcpyHostToDevice, c->stream));
+    orbg_keyframes K{};
+    K.kps = (const orbg_keypoint *)(db + o_kps);
+    K.uright = (const float *)(db + o_ur);
+    K.counts = (const int32_t *)(db + o_cnt);
+    const int32_t *di = (const int32_t *)(db + o_idx);
+    rc = launch_triangulate(c->stream, K, (const orbg_keypoint *)(db + o_raw),
+                            (const float *)(db + o_dp), cap, (const orbg_kf_camera *)(db + o_cam),
+                            di, di + 1, (const int32_t *)(db + o_m), 1, c->scale, c->sigma2,
+                            c->p.nlevels, c->p.scale_factor, (float *)(db + o_x),
+                            (int8_t *)(db + o_st), (int32_t *)(db + o_nn));
+    if (rc) return set_err(ORBG_EIO, "k_triangulate launch failed");
+    HIPCHK(hipMemcpyAsync(hs + o_x, db + o_x, o - o_x, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(hipStreamSynchronize(c->stream));
+    memcpy(x3d, hs + o_x, (size_t)kf1->n * 12);
+    memcpy(status, hs + o_st, (size_t)kf1->n);
+    memcpy(nnew, hs + o_nn, 4);
     return ORBG_OK;
 }
 

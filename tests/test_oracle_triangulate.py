@@ -46,7 +46,8 @@ def _rot(rng, s):
 
 def tri_pair_case(O, seed, n=1000, baseline=1.2, stereo=0.6, w=1241, h=376, noise=0.5,
                   distort=0.02):
-    """Two KeyFrames of one camera seeing n 3-D points and a matches12 list with the cases
+    """O: a module with KP_DTYPE and KF_CAM_DTYPE / KF_CAMERA_DTYPE (the oracle or liborbg's
+    _lib).  Two KeyFrames of one camera seeing n 3-D points and a matches12 list with the cases
     CreateNewMapPoints rejects: wrong matches (reprojection), far points (parallax), points
     behind KF2, octave jumps (scale consistency), monocular and stereo features, mvKeys !=
     mvKeysUn (UnprojectStereo reads mvKeys).  Returns (kf1, kf2, c1, c2, m12, sf, s2, Xw)."""
@@ -111,9 +112,20 @@ def tri_pair_case(O, seed, n=1000, baseline=1.2, stereo=0.6, w=1241, h=376, nois
     kf1 = dict(kps=kp1, kps_raw=raw1, uright=ur1, depth=d1)
     kf2 = dict(kps=kp2, kps_raw=raw2, uright=ur2, depth=d2)
     mb = BF / fx
-    c1 = O.kf_cam(np.concatenate([R1w, t1w[:, None]], 1), fx, fy, cx, cy, mb, BF)
-    c2 = O.kf_cam(np.concatenate([R2w, t2w[:, None]], 1), fx, fy, cx, cy, mb, BF)
+    c1 = kf_cam(O, np.concatenate([R1w, t1w[:, None]], 1), fx, fy, cx, cy, mb, BF)
+    c2 = kf_cam(O, np.concatenate([R2w, t2w[:, None]], 1), fx, fy, cx, cy, mb, BF)
     return kf1, kf2, c1, c2, m12, sf, s2, Xw
+
+
+def kf_cam(O, Tcw, fx, fy, cx, cy, mb, mbf):
+    """the camera record (the oracle's KF_CAM_DTYPE or liborbg's KF_CAMERA_DTYPE: one layout)"""
+    dt = getattr(O, "KF_CAM_DTYPE", None) or O.KF_CAMERA_DTYPE
+    c = np.zeros((), dt)
+    c["Tcw"] = np.asarray(Tcw, F32).reshape(-1)[:12]
+    c["fx"], c["fy"], c["cx"], c["cy"] = fx, fy, cx, cy
+    c["invfx"], c["invfy"] = F32(1.0) / F32(fx), F32(1.0) / F32(fy)
+    c["mb"], c["mbf"] = mb, mbf
+    return c
 
 
 # ------------------------------------------------------------- pure-Python restatement

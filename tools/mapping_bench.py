@@ -16,6 +16,13 @@ oracle (oracle/mapping_oracle.c) on one host core over a bounded sample:
   fuse_sim3  ORBmatcher::Fuse(pKF, Scw, vpPoints, th = 4, vpReplacePoint)'s search
              (LoopClosing::SearchAndFuse): the same shape with one Sim3 per KeyFrame (no
              mvuRight: 60 B per keypoint).
+  triangulate  LocalMapping::CreateNewMapPoints' triangulation (csrc/triangulate_kernels.hip):
+             1024 KeyFrame pairs (64 generated pairs of 2000-feature KeyFrames, 60% stereo,
+             8% wrong matches, 10% unmatched; each 16 times) per launch: matched pairs/s.
+             Bytes per pKF1 feature: its mvKeysUn + mvKeys + mvuRight + mvDepth (64 B), the
+             vMatches12 entry (4 B), the partner's same 64 B, status + x3D (13 B) = 145 B.
+             Per-thread ALU (a 4x4 Jacobi in double, glibc atan2f / cosf), so latency- and
+             ALU-bound: the HBM fraction is low by construction.
 
     python tools/mapping_bench.py [--steps 20] [--warmup 3] [--no-cpu] [--only NAME]
 """
@@ -149,6 +156,70 @@ def main():
         if args.only not in ("", "fuse_sim3" if sim3 else "fuse"):
             continue
         fuse_line(args, L, T, O, ctx, h, sim3)
+    if args.only in ("", "triangulate"):
+        triangulate_line(args, L, O, ctx, h)
+
+
+def triangulate_line(args, L, O, ctx, h):
+    import torch
+    import test_oracle_triangulate as TT
+    NQ, REP, cap, N = 64, 16, 2048, 2000
+    cases = [TT.tri_pair_case(L, 900 + q, n=N, baseline=0.3 + 0.05 * q) for q in range(NQ)]
+    nk = 2 * NQ
+    kps = np.zeros((nk, cap), L.KP_DTYPE)
+    raw = np.zeros((nk, cap), L.KP_DTYPE)
+    ur = np.full((nk, cap), -1, np.float32)
+    dp = np.zeros((nk, cap), np.float32)
+    cnt = np.full(nk, N, np.int32)
+    cam = np.zeros(nk, L.KF_CAMERA_DTYPE)
+    for q, c in enumerate(cases):
+        for s, kf, cm in ((2 * q, c[0], c[2]), (2 * q + 1, c[1], c[3])):
+            kps[s, :N], raw[s, :N], ur[s, :N], dp[s, :N] = kf["kps"], kf["kps_raw"], kf["uright"], kf["depth"]
+            cam[s] = np.asarray(cm).view(L.KF_CAMERA_DTYPE)
+    P = NQ * REP
+    qq = np.arange(P) % NQ
+    m12 = np.full((P, cap), -1, np.int32)
+    for p in range(P):
+        m12[p, :N] = cases[qq[p]][4]
+    t = {k: dev(v) for k, v in dict(kps=kps, raw=raw, ur=ur, dp=dp, cnt=cnt, cam=cam,
+                                    m12=m12).items()}
+    K = L.KeyFrames(None, t["kps"].data_ptr(), t["ur"].data_ptr(), None, t["cnt"].data_ptr(),
+                    None, None, None, None)
+    i1 = torch.from_numpy((2 * qq).astype(np.int32)).cuda()
+    i2 = torch.from_numpy((2 * qq + 1).astype(np.int32)).cuda()
+    dx = torch.empty(P * cap * 3, dtype=torch.float32, device="cuda")
+    dst = torch.empty(P * cap, dtype=torch.int8, device="cuda")
+    dn = torch.empty(P, dtype=torch.int32, device="cuda")
+
+    def run():
+        L.check(L.lib().orbg_triangulate_batch_device(
+            h, C.byref(K), t["raw"].data_ptr(), t["dp"].data_ptr(), cap, t["cam"].data_ptr(),
+            i1.data_ptr(), i2.data_ptr(), t["m12"].data_ptr(), P, dx.data_ptr(),
+            dst.data_ptr(), dn.data_ptr()), "triangulate")
+    s_step, avg = timed(ctx, "triangulate", run, args.steps, args.warmup)
+    matched = int((m12 >= 0).sum())
+    algo = P * N * 145
+    r = line("LocalMapping::CreateNewMapPoints triangulation: matched pairs/s", "matches/s",
+             matched, s_step, avg, algo,
+             "%d KeyFrame pairs of 2000 features (60%% stereo, 8%% wrong / 10%% no match), "
+             "%d matched pairs per launch" % (P, matched),
+             {"dtype": "f32/f64", "new_points_per_pair": round(float(dn.cpu().numpy().mean()), 1),
+              "keyframe_pairs_per_s": round(P / s_step, 1)})
+    if O is not None:
+        p = O.params(nfeatures=2000)
+        sf, s2 = np.array(p.scale[:8], np.float32), np.array(p.sigma2[:8], np.float32)
+        t0 = time.perf_counter()
+        calls = done = 0
+        while time.perf_counter() - t0 < 3.0:
+            c = cases[calls % NQ]
+            O.triangulate(c[0], c[1], c[2], c[3], c[4], sf, s2, 1.2)
+            done += int((c[4] >= 0).sum())
+            calls += 1
+        cdt = time.perf_counter() - t0
+        r["cpu_baseline"] = {"value": round(done / cdt, 1), "unit": "matches/s", "cores": 1,
+                             "kind": "port", "sample": "%d KeyFrame pairs (%d matches), oracle "
+                             "-O3, one thread, %.2f s" % (calls, done, cdt)}
+    print(json.dumps(r), flush=True)
 
 
 def fuse_line(args, L, T, O, ctx, h, sim3):
