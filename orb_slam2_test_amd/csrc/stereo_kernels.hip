@@ -395,6 +395,186 @@ __global__ __launch_bounds__(256) void k_stereo_sad(StereoGeom G,
     }
 }
 
+// Batched form of the same per-keypoint work (ORBG_ST_MG4, default): the kernel is bound by
+// each keypoint's chain of dependent loads (vbest_r -> the two keypoints -> the patch and strip
+// rows), so a wave runs four keypoints of its sequence at once, 16 lanes each, and pays the
+// chain once per four.  Per keypoint: its 33 row words staged by 16 lanes (3 loads per lane),
+// then lane i < 11 of the group owns shift inc = i - 5 and sums its 11 rows in registers (no
+// LDS atomics), and the first minimum, its neighbours and the parabola are 16-lane shuffles.
+// The level table (scales, widths, pitches, offsets) is read from LDS, not from the kernel
+// arguments by a dynamic index (a dependent global load per keypoint).
+#ifndef ORBG_ST_MG4
+#define ORBG_ST_MG4 1
+#endif
+#define ST_SMG 4  // keypoints per wave
+
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8, 8))) void k_stereo_sad_mg(StereoGeom G,
+                                                      const orbg_keypoint *__restrict__ kps,
+                                                      const int32_t *__restrict__ counts,
+                                                      const int32_t *__restrict__ left,
+                                                      const int32_t *__restrict__ right,
+                                                      const int32_t *__restrict__ best_r,
+                                                      const uint8_t *__restrict__ img0,
+                                                      int64_t img_fs, int img_pitch,
+                                                      const uint8_t *__restrict__ pyr,
+                                                      int64_t pyr_frame, float *__restrict__ uright,
+                                                      float *__restrict__ depth,
+                                                      int32_t *__restrict__ sad_out)
+{
+    __shared__ uint32_t stage[4][ST_SMG][11 * 4 + 11 * 7];
+    __shared__ int shl[4][ST_SMG][11], shr[4][ST_SMG][11];
+    __shared__ float t_inv[16], t_scale[16];
+    __shared__ int t_lw[16], t_pitch[16];
+    __shared__ int64_t t_off[16];
+    if (threadIdx.x < 16) {
+        const int l = threadIdx.x;
+        t_inv[l] = G.inv_scale[l];
+        t_scale[l] = G.scale[l];
+        t_lw[l] = G.lw[l];
+        t_pitch[l] = l == 0 ? img_pitch : G.lpitch[l];
+        t_off[l] = l == 0 ? 0 : G.pyr_off[l];
+    }
+    __syncthreads();
+    const int id = ORBG_ST_XCD ? xcd_remap(blockIdx.x + gridDim.x * blockIdx.y, gridDim.x * gridDim.y)
+                               : (int)(blockIdx.x + gridDim.x * blockIdx.y);
+    const int p = id / gridDim.x, bx = id - p * gridDim.x;
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6, g = lane >> 4, l16 = lane & 15;
+    const int fl = left[p], fr = right[p];
+    const int nl = counts[fl];
+    const int i0 = bx * 4 + wv;
+    float *ur = uright + (size_t)p * G.fc, *dp = depth + (size_t)p * G.fc;
+    int32_t *so = sad_out + (size_t)p * G.fc;
+    uint32_t *stL = stage[wv][g], *stR = stage[wv][g] + 11 * 4;
+    int *shlw = shl[wv][g], *shrw = shr[wv][g];
+    const int inc = l16 - ST_L;  // lanes l16 < 11: this shift
+    for (int j0 = 0; i0 + j0 * ST_SAD_WAVES < nl; j0 += ST_SMG) {
+        const int iL = i0 + (j0 + g) * ST_SAD_WAVES;
+        const bool have = iL < nl;
+        const int iR = have ? best_r[(size_t)p * G.fc + iL] : -1;
+        if (have && l16 == 0) {
+            ur[iL] = -1.0f;
+            dp[iL] = -1.0f;
+            so[iL] = -1;
+        }
+        bool ok = iR >= 0;
+        orbg_keypoint kl{};
+        float uR0 = 0.0f;
+        if (ok) {
+            kl = kps[(size_t)fl * G.fc + iL];
+            uR0 = kps[(size_t)fr * G.fc + iR].x;
+        }
+        const int lev = ok ? kl.octave : 0;
+        const float sf = t_inv[lev];
+        const float scaleduL = roundf(kl.x * sf);
+        const float scaledvL = roundf(kl.y * sf);
+        const float scaleduR0 = roundf(uR0 * sf);
+        const float iniu = scaleduR0 + ST_L - ST_W;
+        const float endu = scaleduR0 + ST_L + ST_W + 1;
+        ok = ok && !(iniu < 0 || endu >= t_lw[lev]);
+        // rows: word w = l16 + 16 u (u = 0..2, w < 33) = (row w / 3, part w % 3)
+        if (ok) {
+            const int pitch = t_pitch[lev];
+            const uint8_t *IL = (lev == 0 ? img0 + fl * img_fs : pyr + fl * pyr_frame + t_off[lev]);
+            const uint8_t *IR = (lev == 0 ? img0 + fr * img_fs : pyr + fr * pyr_frame + t_off[lev]);
+            const int yl = (int)scaledvL, xl = (int)scaleduL, xr = (int)scaleduR0;
+            uint4 v[3];
+            int sh[3];
+#pragma unroll
+            for (int u = 0; u < 3; u++) {
+                const int w = min(l16 + 16 * u, 32);
+                const int r = w / 3, c = w - 3 * r;
+                const uint8_t *src = c == 0 ? IL + (int64_t)(yl - ST_W + r) * pitch + xl - ST_W
+                                            : IR + (int64_t)(yl - ST_W + r) * pitch + xr - 2 * ST_W;
+                sh[u] = (int)((uintptr_t)src & 3);
+                v[u] = *(const uint4 *)((const uint32_t *)(src - sh[u]) + (c == 2 ? 3 : 0));
+            }
+#pragma unroll
+            for (int u = 0; u < 3; u++) {
+                const int w = l16 + 16 * u;
+                if (w < 33) {
+                    const int r = w / 3, c = w - 3 * r;
+                    uint32_t *dst = (c == 0 ? stL + r * 4 : stR + r * 7) + (c == 2 ? 3 : 0);
+                    dst[0] = v[u].x;
+                    dst[1] = v[u].y;
+                    dst[2] = v[u].z;
+                    dst[3] = v[u].w;
+                    if (c == 0) shlw[r] = sh[u];
+                    if (c == 1) shrw[r] = sh[u];
+                }
+            }
+        }
+        wave_sync_lds();
+        int sad = INT_MAX;
+        if (ok && l16 < 2 * ST_L + 1) {
+            const uint8_t *bL = (const uint8_t *)stL, *bR = (const uint8_t *)stR;
+            const int cl = bL[ST_W * 16 + shlw[ST_W] + ST_W];
+            const int cr = bR[ST_W * 28 + shrw[ST_W] + 2 * ST_W + inc];
+            const uint32_t cr2 = (uint32_t)cr * 0x10001u, cl2 = (uint32_t)cl * 0x10001u;
+            uint32_t sacc = 0;
+#pragma unroll 1
+            for (int dy = 0; dy < 2 * ST_W + 1; dy++) {
+                const int ls = shlw[dy];
+                const int s = shrw[dy] + ST_L + inc;
+                const uint32_t *la = stL + dy * 4, *ra = stR + dy * 7 + (s >> 2);
+                uint32_t Lw[4], Rw[4];
+#pragma unroll
+                for (int k = 0; k < 4; k++) {
+                    Lw[k] = la[k];
+                    Rw[k] = ra[k];
+                }
+#pragma unroll
+                for (int j = 0; j < 3; j++) {
+                    const uint32_t A = __builtin_amdgcn_alignbyte(Lw[j + 1], Lw[j], ls);
+                    const uint32_t B = __builtin_amdgcn_alignbyte(Rw[j + 1], Rw[j], s & 3);
+                    sacc = __builtin_amdgcn_sad_u16(__builtin_amdgcn_perm(A, A, 0x0c010c00u) + cr2,
+                                                    __builtin_amdgcn_perm(B, B, 0x0c010c00u) + cl2, sacc);
+                    if (j < 2)
+                        sacc = __builtin_amdgcn_sad_u16(__builtin_amdgcn_perm(A, A, 0x0c030c02u) + cr2,
+                                                        __builtin_amdgcn_perm(B, B, 0x0c030c02u) + cl2, sacc);
+                    else
+                        sacc = __builtin_amdgcn_sad_u16(__builtin_amdgcn_perm(A, A, 0x0c0c0c02u) + (uint32_t)cr,
+                                                        __builtin_amdgcn_perm(B, B, 0x0c0c0c02u) + (uint32_t)cl, sacc);
+                }
+            }
+            sad = (int)sacc;
+        }
+        // first minimum over the group's 11 shifts: (sad, inc) lexicographic, 16-lane butterfly
+        int key_s = sad, key_i = l16;
+#pragma unroll
+        for (int m = 8; m >= 1; m >>= 1) {
+            const int os = __shfl_xor(key_s, m, 16), oi = __shfl_xor(key_i, m, 16);
+            if (os < key_s || (os == key_s && oi < key_i)) {
+                key_s = os;
+                key_i = oi;
+            }
+        }
+        const int bestinc = key_i - ST_L;
+        const int base = lane & ~15;
+        const int d1 = __shfl(sad, base + min(max(key_i - 1, 0), 15)),
+                  d3 = __shfl(sad, base + min(key_i + 1, 15));
+        if (ok && l16 == 0 && bestinc != -ST_L && bestinc != ST_L) {
+            const float dist1 = (float)d1;
+            const float dist2 = (float)key_s;
+            const float dist3 = (float)d3;
+            const float deltaR = (dist1 - dist3) / (2.0f * (dist1 + dist3 - 2.0f * dist2));
+            if (!(deltaR < -1 || deltaR > 1)) {
+                float bestuR = t_scale[lev] * ((float)scaleduR0 + (float)bestinc + deltaR);
+                float disparity = kl.x - bestuR;
+                if (disparity >= 0.0f && disparity < G.max_d) {
+                    if (disparity <= 0) {
+                        disparity = 0.01f;
+                        bestuR = (float)((double)kl.x - 0.01);
+                    }
+                    dp[iL] = G.bf / disparity;
+                    ur[iL] = bestuR;
+                    so[iL] = key_s;
+                }
+            }
+        }
+        wave_sync_lds();  // the next batch reuses this wave's LDS
+    }
+}
+
 // ---- median cut ---------------------------------------------------------------------
 __global__ __launch_bounds__(256) void k_stereo_median(StereoGeom G,
                                                       const int32_t *__restrict__ counts,
@@ -521,9 +701,10 @@ int launch_stereo(hipStream_t st, const OrbgGeom &g, const orbg_keypoint *kps,
                        desc, counts, d_left, d_right, row_off, row_list, best_r);
     prof_end(prof, st, "stereo_match", a);
     prof_begin(prof, st, "stereo_sad", &a);
-    hipLaunchKernelGGL(k_stereo_sad, dim3(ST_SAD_WAVES / 4, npairs), dim3(256), 0, st, G, kps,
-                       counts, d_left, d_right, best_r, img0, img_fs, img_pitch, pyr,
-                       g.pyr_frame, uright, depth, sad);
+    hipLaunchKernelGGL(ORBG_ST_MG4 ? k_stereo_sad_mg : k_stereo_sad,
+                       dim3(ST_SAD_WAVES / 4, npairs), dim3(256), 0, st, G, kps, counts, d_left,
+                       d_right, best_r, img0, img_fs, img_pitch, pyr, g.pyr_frame, uright, depth,
+                       sad);
     prof_end(prof, st, "stereo_sad", a);
     prof_begin(prof, st, "stereo_median", &a);
     hipLaunchKernelGGL(k_stereo_median, dim3(npairs), dim3(256), 0, st, G, counts, d_left, sad,
