@@ -353,14 +353,18 @@ def main():
     if args.host_input:
         # Frame.cc:310-316 / mono_kitti.cc:78-90 read frames from host memory: here every
         # step's block goes H2D on its own stream into one of 3 device slots while the
-        # extraction of the steps before runs; the copy of step k + 2 waits until step k's
-        # outputs are written (orbg_batch_acquire: the last reads of its input, IC_Angle's
-        # level-0 patches, are done by then), so a slot is never overwritten while read
+        # extraction of the steps before runs.  The copy into a slot is issued once the step
+        # that read it last is done (orbg_batch_acquire: the last reads of its input, IC_Angle's
+        # level-0 patches, are done when its outputs are written), gated on the host: an event
+        # on a compute stream that the host waits for after enqueuing the next step, so the
+        # copy stream never waits on a device event (a copy queued behind one ran serialised
+        # with the extraction: profiles/r05_host_input_trace.txt)
         h_blocks = [torch.from_numpy(b).pin_memory() for b in blocks]
         stage = [torch.empty_like(d_blocks[0]) for _ in range(3)]
         cstream = torch.cuda.Stream()
+        gstream = torch.cuda.Stream()
         ev_copy = [torch.cuda.Event() for _ in range(3)]
-        pend = [0]
+        ev_done = [torch.cuda.Event() for _ in range(3)]
 
         def issue_copy(j):
             with torch.cuda.stream(cstream):
@@ -374,19 +378,20 @@ def main():
             issue_copy(j)
         torch.cuda.synchronize()
         h2d = 4 * h_blocks[0].numel() / (time.perf_counter() - t0) / 1e9
-        issue_copy(0)
-        issue_copy(1)
-        pend[0] = 2
+        for j in range(3):
+            issue_copy(j)
 
         def step():  # noqa: F811 -- the host-fed step replaces the resident one
             k = it[0]
             it[0] += 1
             stream.wait_event(ev_copy[k % 3])
             bstep(stage[k % 3].data_ptr(), W, H)
-            ext.ctx.batch_acquire(cstream.cuda_stream)
-            ext.ctx.batch_release(cstream.cuda_stream)
-            issue_copy(pend[0])
-            pend[0] += 1
+            ext.ctx.batch_acquire(gstream.cuda_stream)
+            ext.ctx.batch_release(gstream.cuda_stream)
+            ev_done[k % 3].record(gstream)
+            if k >= 1:
+                ev_done[(k - 1) % 3].synchronize()  # step k - 1 no longer reads its slot
+                issue_copy(k + 2)                   # into that slot: (k + 2) % 3 == (k - 1) % 3
 
     for _ in range(args.warmup):
         step()
@@ -535,8 +540,9 @@ def main():
             "host_input": ({"h2d_GBps_alone": round(h2d, 2),
                             "input_bytes_per_frame": W * H,
                             "h2d_bound_frames_per_s": round(h2d * 1e9 / (W * H), 1),
-                            "staging": "3 device slots, copy stream, the copy of step k+2 after "
-                                       "step k's outputs (orbg_batch_acquire)"}
+                            "staging": "3 device slots, copy stream, the copy of step k+2 issued "
+                                       "once step k-1's outputs are written (host-gated "
+                                       "orbg_batch_acquire)"}
                            if args.host_input else None),
             "candidates_per_image": round(ncand / nimg, 1),
             "keypoints_per_image": round(nkp / nimg, 1),
