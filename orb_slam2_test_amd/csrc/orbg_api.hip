@@ -307,6 +307,18 @@ struct orbg_ctx {
                ev_pfork[2] = {nullptr, nullptr}, ev_pyr[2] = {nullptr, nullptr};
     bool blur_side = false;  // ORBG_BLUR_SIDE
     bool serial = false;     // orbg_set_serial: no stream overlap (isolated kernel timing)
+    // orbg_extract's single-frame hipGraphs: the whole frame (H2D of the pinned input, the
+    // extraction's launches on the context and quadtree streams, k_pack_frame, D2H of the
+    // packed outputs) captured once per output slot and image size, then replayed with one
+    // hipGraphLaunch.  ORBG_GRAPH=1|2|3 (graph_mode below); 0, the default, launches eagerly.
+    int graph_mode = 0;
+    hipGraphExec_t gexec[2] = {nullptr, nullptr};
+    uint64_t gkey[2] = {0, 0};   // (plan generation, w, h) the graph was captured for
+    int gwarm[2] = {0, 0};       // eager frames seen for gkey_next (capture after one)
+    uint64_t gkey_seen[2] = {0, 0};
+    uint64_t plan_gen = 0;
+    uint8_t *h_gin = nullptr, *h_gout = nullptr;  // pinned graph input / output
+    size_t gin_bytes = 0, gout_bytes = 0;
     bool ba_jacobians = true;  // orbg_ba_set_jacobians
     bool ba_edge_errors = true;  // orbg_ba_set_edge_errors
     int oct_mode = 0;
@@ -762,6 +774,7 @@ static int plan(orbg_ctx *c, int w, int h, int batch)
     if (c->gw == w && c->gh == h && c->gbatch >= batch) return ORBG_OK;
     const int want_batch = std::max(batch, c->gbatch);
     free_plan(c);
+    c->plan_gen++;  // captured single-frame graphs hold the old buffers
     const orbg_params &p = c->p;
     OrbgGeom G{};
     G.L = p.nlevels;
@@ -1329,6 +1342,8 @@ extern "C" int orbg_create(int device, const orbg_params *p, orbg_ctx **out)
         c->oct_mode = e ? atoi(e) : 1;
         const char *f0 = getenv("ORBG_FAST0");
         c->fast0_mode = f0 ? atoi(f0) : 1;
+        const char *gm = getenv("ORBG_GRAPH");
+        c->graph_mode = gm ? atoi(gm) : 0;
         const char *b0 = getenv("ORBG_BLUR0");
         c->blur0_mode = b0 ? atoi(b0) : 0;
         const char *bp = getenv("ORBG_BACK_PRIO");  // developer A/B: normal | high (default)
@@ -1404,6 +1419,10 @@ extern "C" void orbg_destroy(orbg_ctx *c)
 {
     if (c && c->h_stage) hipHostFree(c->h_stage);
     if (!c) return;
+    for (int i = 0; i < 2; i++)
+        if (c->gexec[i]) hipGraphExecDestroy(c->gexec[i]);
+    if (c->h_gin) hipHostFree(c->h_gin);
+    if (c->h_gout) hipHostFree(c->h_gout);
     hipSetDevice(c->device);
     if (c->stream) hipStreamSynchronize(c->stream);
     c->prof.collect();
@@ -1915,6 +1934,9 @@ extern "C" int orbg_download_frame(orbg_ctx *c, int frame, orbg_keypoint *kps, u
     return ORBG_OK;
 }
 
+static int extract_graph(orbg_ctx *c, const uint8_t *img, int w, int h, size_t step,
+                         orbg_keypoint *kps, uint8_t *desc, int cap, int *n_out);
+
 extern "C" int orbg_extract(orbg_ctx *c, const uint8_t *img, int w, int h, size_t step,
                             orbg_keypoint *kps, uint8_t *desc, int cap, int *n_out)
 {
@@ -1935,6 +1957,9 @@ extern "C" int orbg_extract(orbg_ctx *c, const uint8_t *img, int w, int h, size_
         if ((rc = dalloc(&c->d_img, bytes))) return rc;
         c->img_bytes = bytes;
     }
+    if (c->graph_mode && !c->prof.on && c->stream && !(c->pipelined && !c->serial) &&
+        !c->mat_pending[c->slot ^ 1] && !c->rel_pending[c->slot ^ 1])
+        return extract_graph(c, img, w, h, step, kps, desc, cap, n_out);
     // rows into pinned staging, one DMA (a pageable 2-D copy of an odd-width image goes row
     // by row: ~3 ms for 1241 x 376)
     uint8_t *hs;
@@ -1948,6 +1973,148 @@ extern "C" int orbg_extract(orbg_ctx *c, const uint8_t *img, int w, int h, size_
     HIPCHK(hipMemcpyAsync(c->d_img, hs, bytes, hipMemcpyHostToDevice, c->stream));
     if ((rc = launch_extract(c, c->d_img, 1, w, (int64_t)bytes))) return rc;
     return orbg_download_frame(c, 0, kps, desc, cap, n_out);
+}
+
+// the context state launch_extract leaves for a non-pipelined batch into slot s (a graph
+// replay sets it without the launches)
+static void extract_state(orbg_ctx *c, int s, const uint8_t *d_imgs, int B, int pitch, int64_t fs)
+{
+    c->last_npairs = 0;
+    c->last_nstereo = 0;
+    c->d_pyr = c->pyr_slot[s];
+    c->d_blur = c->blur_slot[s];
+    c->d_cell_cnt = c->cnt_slot[s];
+    c->d_cell_kp = c->ckp_slot[s];
+    c->last_piped = false;
+    c->slot = s;
+    c->d_kps = c->kps_slot[s];
+    c->d_desc = c->desc_slot[s];
+    c->d_counts = c->counts_slot[s];
+    c->last_img = d_imgs;
+    c->last_fs = fs;
+    c->last_pitch = pitch;
+    c->last_n = B;
+}
+
+static int pinned(uint8_t **p, size_t *have, size_t bytes)
+{
+    if (*have >= bytes) return ORBG_OK;
+    if (*p) hipHostFree(*p);
+    *p = nullptr;
+    *have = 0;
+    if (hipHostMalloc((void **)p, bytes, hipHostMallocDefault) != hipSuccess)
+        return set_err(ORBG_ENOMEM, "hipHostMalloc(%zu bytes)", bytes);
+    *have = bytes;
+    return ORBG_OK;
+}
+
+// orbg_extract through a captured hipGraph (graph_mode; plan, d_img and the caller checks done
+// by orbg_extract).  The first frame of a (slot, size) runs eagerly (module loads, attribute
+// setup happen outside any capture), the second is captured and every later one replayed.
+static int extract_graph(orbg_ctx *c, const uint8_t *img, int w, int h, size_t step,
+                         orbg_keypoint *kps, uint8_t *desc, int cap, int *n_out)
+{
+    const size_t bytes = (size_t)w * h;
+    const size_t fc = (size_t)c->geom.frame_cap;
+    const size_t okp = 256, ods = okp + ((fc * sizeof(orbg_keypoint) + 255) & ~(size_t)255);
+    const size_t obytes = ods + fc * 32;
+    int rc;
+    if (c->pack_bytes < obytes) {
+        if ((rc = sync_all(c))) return rc;
+        if (c->d_pack) hipFree(c->d_pack);
+        c->d_pack = nullptr;
+        c->pack_bytes = 0;
+        if ((rc = dalloc(&c->d_pack, obytes))) return rc;
+        c->pack_bytes = obytes;
+    }
+    if ((rc = sync_all(c))) return rc;  // the pinned buffers' previous DMAs are done
+    if (c->gin_bytes < bytes || c->gout_bytes < obytes) {
+        for (int i = 0; i < 2; i++) {  // graphs hold the old host buffers
+            if (c->gexec[i]) hipGraphExecDestroy(c->gexec[i]);
+            c->gexec[i] = nullptr;
+            c->gkey[i] = 0;
+        }
+        if ((rc = pinned(&c->h_gin, &c->gin_bytes, bytes))) return rc;
+        if ((rc = pinned(&c->h_gout, &c->gout_bytes, obytes))) return rc;
+    }
+    if (step == (size_t)w) {
+        std::memcpy(c->h_gin, img, bytes);
+    } else {
+        for (int y = 0; y < h; y++) std::memcpy(c->h_gin + (size_t)y * w, img + (size_t)y * step, w);
+    }
+    const int s = c->slot ^ 1;
+    const uint64_t key = (c->plan_gen << 40) ^ ((uint64_t)w << 20) ^ (uint64_t)h;
+    hipStream_t st = c->stream;
+    // graph_mode 1: the copies inside the graph; 2: kernels only (the copies eager around the
+    // launch); 3: as 2 with the extraction captured on the one context stream (a linear graph)
+    const bool copies_in = c->graph_mode == 1;
+    if (c->gexec[s] && c->gkey[s] == key) {
+        extract_state(c, s, c->d_img, 1, w, (int64_t)bytes);
+        if (!copies_in) HIPCHK(hipMemcpyAsync(c->d_img, c->h_gin, bytes, hipMemcpyHostToDevice, st));
+        HIPCHK(hipGraphLaunch(c->gexec[s], st));
+        if (!copies_in)
+            HIPCHK(hipMemcpyAsync(c->h_gout, c->d_pack, obytes, hipMemcpyDeviceToHost, st));
+    } else {
+        if (c->gexec[s]) hipGraphExecDestroy(c->gexec[s]);
+        c->gexec[s] = nullptr;
+        const bool capture = c->gkey_seen[s] == key;
+        c->gkey_seen[s] = key;
+        rc = ORBG_OK;
+        if (!copies_in &&
+            hipMemcpyAsync(c->d_img, c->h_gin, bytes, hipMemcpyHostToDevice, st) != hipSuccess)
+            rc = set_err(ORBG_EIO, "hipMemcpyAsync");
+        if (capture) HIPCHK(hipStreamBeginCapture(st, hipStreamCaptureModeRelaxed));
+        if (!rc && copies_in &&
+            hipMemcpyAsync(c->d_img, c->h_gin, bytes, hipMemcpyHostToDevice, st) != hipSuccess)
+            rc = set_err(ORBG_EIO, "hipMemcpyAsync");
+        const bool ser = c->serial;
+        if (c->graph_mode == 3) c->serial = true;  // one stream: launch_extract's serial layout
+        if (!rc) rc = launch_extract(c, c->d_img, 1, w, (int64_t)bytes);
+        c->serial = ser;
+        if (!rc) {
+            const size_t words = std::max(fc * (sizeof(orbg_keypoint) / 4), fc * 8);
+            hipLaunchKernelGGL(k_pack_frame, dim3((unsigned)((words + 255) / 256)), dim3(256), 0,
+                               st, c->d_err, c->d_counts, (const uint32_t *)c->d_kps,
+                               (const uint32_t *)c->d_desc, 0, fc, okp, ods, (uint32_t *)c->d_pack);
+            if (hipGetLastError() != hipSuccess ||
+                (copies_in && hipMemcpyAsync(c->h_gout, c->d_pack, obytes, hipMemcpyDeviceToHost,
+                                             st) != hipSuccess))
+                rc = set_err(ORBG_EIO, "k_pack_frame / D2H");
+        }
+        if (capture) {
+            hipGraph_t g = nullptr;
+            const hipError_t e = hipStreamEndCapture(st, &g);
+            if (!rc && e != hipSuccess) rc = set_err(ORBG_EIO, "hipStreamEndCapture: %s", hipGetErrorString(e));
+            if (!rc && hipGraphInstantiate(&c->gexec[s], g, nullptr, nullptr, 0) != hipSuccess)
+                rc = set_err(ORBG_EIO, "hipGraphInstantiate");
+            if (g) hipGraphDestroy(g);
+            if (rc) {
+                c->gexec[s] = nullptr;
+                c->graph_mode = 0;  // fall back to eager launches for good
+                return rc;
+            }
+            c->gkey[s] = key;
+            HIPCHK(hipGraphLaunch(c->gexec[s], st));
+        }
+        if (rc) return rc;
+        if (!copies_in)
+            HIPCHK(hipMemcpyAsync(c->h_gout, c->d_pack, obytes, hipMemcpyDeviceToHost, st));
+    }
+    HIPCHK(hipEventRecord(c->ev_ext[s], st));
+    if ((rc = sync_all(c))) return rc;
+    int32_t hdr[3];
+    std::memcpy(hdr, c->h_gout, sizeof(hdr));
+    if (hdr[0]) {
+        const int32_t e0[2] = {0, INT32_MAX};
+        HIPCHK(hipMemcpy(c->d_err, e0, sizeof(e0), hipMemcpyHostToDevice));
+        return err_from_flags(hdr[0], hdr[1]);
+    }
+    const int32_t n = hdr[2];
+    if (n_out) *n_out = n;
+    if (n > cap) return set_err(ORBG_ERANGE, "capacity %d < %d keypoints", cap, n);
+    if (kps && n) std::memcpy(kps, c->h_gout + okp, n * sizeof(orbg_keypoint));
+    if (desc && n) std::memcpy(desc, c->h_gout + ods, (size_t)n * 32);
+    return ORBG_OK;
 }
 
 extern "C" int orbg_get_level(orbg_ctx *c, int frame, int level, uint8_t *dst, size_t dst_step,
@@ -2572,43 +2739,10 @@ extern "C" int orbg_search_for_initialization(orbg_ctx *c, const orbg_keypoint *
     if (nmatches) *nmatches = 0;
     if (n1 == 0) return ORBG_OK;
     HIPCHK(hipSetDevice(c->device));
-    const size_t m1 = (size_t)n1, m2 = (size_t)std::max(n2, 1);
-    size_t o = 0;
-    const size_t ok1 = o;
-    o += al256(m1 * sizeof(orbg_keypoint));
-    const size_t od1 = o;
-    o += al256(m1 * 32);
-    const size_t ok2 = o;
-    o += al256(m2 * sizeof(orbg_keypoint));
-    const size_t od2 = o;
-    o += al256(m2 * 32);
-    const size_t opv = o;
-    o += al256(m1 * 8);
-    const size_t om = o;
-    o += al256(m1 * 4 + 4);
-    const size_t otk = o;
-    o += al256(m1 * 8 * ORBG_MATCH_TOPK);
-    const size_t otn = o;
-    o += al256(m1 * 4);
-    void *s;
-    int rc = scratch(c, o, &s);
-    if (rc) return rc;
-    uint8_t *b = (uint8_t *)s;
-    // inputs packed into pinned staging with the device layout, one DMA each way
-    uint8_t *hs;
-    if ((rc = stage(c, otk, &hs))) return rc;
-    HIPCHK(hipStreamSynchronize(c->stream));  // the staging buffer's previous DMA is done
-    std::memcpy(hs + ok1, kps1, m1 * sizeof(orbg_keypoint));
-    std::memcpy(hs + od1, desc1, m1 * 32);
-    if (n2) {
-        std::memcpy(hs + ok2, kps2, (size_t)n2 * sizeof(orbg_keypoint));
-        std::memcpy(hs + od2, desc2, (size_t)n2 * 32);
-    }
-    std::memcpy(hs + opv, prev_xy, m1 * 8);
-    HIPCHK(hipMemcpyAsync(b, hs, om, hipMemcpyHostToDevice, c->stream));
     // the search reads level-0 keypoints only (ORBmatcher.cc:509-512): the kernels work on
     // indices up to the last level-0 keypoint of either frame (the level-major extractor
-    // order puts them first; any order is handled)
+    // order puts them first; any order is handled), so only those rows go up and only their
+    // vbPrevMatched entries come back (the rest are not read or written)
     int last0 = 0;
     for (int i = n1 - 1; i >= 0; i--)
         if (kps1[i].octave == 0) {
@@ -2620,19 +2754,55 @@ extern "C" int orbg_search_for_initialization(orbg_ctx *c, const orbg_keypoint *
             last0 = std::max(last0, i + 1);
             break;
         }
+    last0 = std::max(last0, 1);
+    const size_t m1 = (size_t)n1, l1 = (size_t)std::min(n1, last0);
+    const size_t l2 = (size_t)std::max(std::min(n2, last0), 1);
+    size_t o = 0;
+    const size_t ok1 = o;
+    o += al256(l1 * sizeof(orbg_keypoint));
+    const size_t od1 = o;
+    o += al256(l1 * 32);
+    const size_t ok2 = o;
+    o += al256(l2 * sizeof(orbg_keypoint));
+    const size_t od2 = o;
+    o += al256(l2 * 32);
+    const size_t opv = o;
+    o += al256(l1 * 8);
+    const size_t om = o;
+    o += al256(m1 * 4 + 4);
+    const size_t otk = o;
+    o += al256(l1 * 8 * ORBG_MATCH_TOPK);
+    const size_t otn = o;
+    o += al256(l1 * 4);
+    void *s;
+    int rc = scratch(c, o, &s);
+    if (rc) return rc;
+    uint8_t *b = (uint8_t *)s;
+    // inputs packed into pinned staging with the device layout, one DMA each way
+    uint8_t *hs;
+    if ((rc = stage(c, otk, &hs))) return rc;
+    HIPCHK(hipStreamSynchronize(c->stream));  // the staging buffer's previous DMA is done
+    std::memcpy(hs + ok1, kps1, l1 * sizeof(orbg_keypoint));
+    std::memcpy(hs + od1, desc1, l1 * 32);
+    if (n2) {
+        const size_t c2 = (size_t)std::min(n2, last0);
+        std::memcpy(hs + ok2, kps2, c2 * sizeof(orbg_keypoint));
+        std::memcpy(hs + od2, desc2, c2 * 32);
+    }
+    std::memcpy(hs + opv, prev_xy, l1 * 8);
+    HIPCHK(hipMemcpyAsync(b, hs, om, hipMemcpyHostToDevice, c->stream));
     rc = launch_init_match_single(c->stream, (const orbg_keypoint *)(b + ok1), b + od1, n1,
                                   (const orbg_keypoint *)(b + ok2), b + od2, n2, *bounds2,
                                   (float *)(b + opv), (int32_t *)(b + om),
                                   (int32_t *)(b + om + m1 * 4), window, nnratio, check_ori,
-                                  (uint32_t *)(b + otk), (int32_t *)(b + otn), &c->prof,
-                                  std::max(last0, 1));
+                                  (uint32_t *)(b + otk), (int32_t *)(b + otn), &c->prof, last0);
     if (rc) return rc;
     int32_t nm = 0;
     HIPCHK(hipMemcpyAsync(hs + opv, b + opv, otk - opv, hipMemcpyDeviceToHost, c->stream));
     HIPCHK(hipStreamSynchronize(c->stream));
     std::memcpy(matches12, hs + om, m1 * 4);
     std::memcpy(&nm, hs + om + m1 * 4, 4);
-    std::memcpy(prev_xy, hs + opv, m1 * 8);
+    std::memcpy(prev_xy, hs + opv, l1 * 8);
     c->prof.collect();
     if (nmatches) *nmatches = nm;
     return ORBG_OK;

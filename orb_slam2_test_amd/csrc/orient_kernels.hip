@@ -84,6 +84,9 @@ struct OrbgKeypointDev {
 #define ORBG_OD_PFD 2  // slots whose loads are in flight ahead of the one being summed / sampled (1: -0.4% per step)
 #endif
 #define OD_PFD ORBG_OD_PFD
+#ifndef ORBG_OD_EARLYC
+#define ORBG_OD_EARLYC 0  // phase C's first neighbourhood loads (<= OD_PFD) issued during phase A's last slots (1: orient +1.3%, 2: +16%, spills; r05k A/B)
+#endif
 static_assert(OD_KPW >= 1 && OD_KPW <= 32, "one slot per lane, okmask is 32 bits");
 
 // IC_Angle byte tables (host-built, orbg_api.hip make_od_tab): entry (sh, w) for the patch
@@ -189,6 +192,23 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(ORBG_OD_WPE
         return (int64_t)((uint64_t)hi << 32 | lo);
     };
 
+    // phase C's neighbourhood loads (defined here: the first OD_PFD are issued at the end of
+    // phase A, so their latency overlaps A's last slots and phase B)
+    struct Nbhd {
+        uint4 v0, v1;
+        int sh;
+    };
+    auto load_nbhd = [&](int j) -> Nbhd {
+        const int bpitch = __builtin_amdgcn_readlane(bpitch_l, j);
+        const uint8_t *bl0 = blur + readlane64(boff_l, j);
+        Nbhd n;
+        n.sh = (int)((uintptr_t)bl0 & 3);
+        const uint8_t *bw = bl0 - n.sh;
+        n.v0 = *(const uint4 *)(bw + (int64_t)pr[0] * bpitch + 16 * pc[0]);
+        n.v1 = *(const uint4 *)(bw + (int64_t)pr[1] * bpitch + 16 * pc[1]);
+        return n;
+    };
+    Nbhd nbh[OD_PFD + 1];
     // ---- A: IC_Angle moments (ORBextractor.cc:83-111), slot j's sums kept by lane j ----
     // Software-pipelined over the slots: the patch loads of slot j + 1 are in flight while
     // slot j's moments are summed (the kernel is bound by the latency of these scattered row
@@ -217,6 +237,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(ORBG_OD_WPE
         for (int j = 0; j < OD_KPW; j++) {
             if (j + OD_PFD < OD_KPW)
                 load_patch(j + OD_PFD, wbuf[(j + OD_PFD) % (OD_PFD + 1)], sbuf[(j + OD_PFD) % (OD_PFD + 1)]);
+            // phase C's first ORBG_OD_EARLYC neighbourhoods, issued in A's last slots
+            if (j >= OD_KPW - ORBG_OD_EARLYC) nbh[j - (OD_KPW - ORBG_OD_EARLYC)] = load_nbhd(j - (OD_KPW - ORBG_OD_EARLYC));
             const uint4(&wd)[2] = wbuf[j % (OD_PFD + 1)];
             const int(&sh)[2] = sbuf[j % (OD_PFD + 1)];
             int m01 = 0, m10 = 0;
@@ -295,23 +317,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(ORBG_OD_WPE
     uint8_t *bp = (uint8_t *)bpatch[wv];
     // pipelined like phase A: slot j + 1's neighbourhood loads are issued right after slot j
     // is staged, and land while slot j's samples are read
-    struct Nbhd {
-        uint4 v0, v1;
-        int sh;
-    };
-    auto load_nbhd = [&](int j) -> Nbhd {
-        const int bpitch = __builtin_amdgcn_readlane(bpitch_l, j);
-        const uint8_t *bl0 = blur + readlane64(boff_l, j);
-        Nbhd n;
-        n.sh = (int)((uintptr_t)bl0 & 3);
-        const uint8_t *bw = bl0 - n.sh;
-        n.v0 = *(const uint4 *)(bw + (int64_t)pr[0] * bpitch + 16 * pc[0]);
-        n.v1 = *(const uint4 *)(bw + (int64_t)pr[1] * bpitch + 16 * pc[1]);
-        return n;
-    };
-    Nbhd nbh[OD_PFD + 1];
 #pragma unroll
-    for (int j = 0; j < OD_PFD; j++) nbh[j] = load_nbhd(j);
+    for (int j = ORBG_OD_EARLYC; j < OD_PFD; j++) nbh[j] = load_nbhd(j);
 #pragma unroll
     for (int j = 0; j < OD_KPW; j++) {
         wave_sync_lds();  // the previous slot's sample reads are done

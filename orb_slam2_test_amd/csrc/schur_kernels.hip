@@ -115,11 +115,20 @@ __global__ __launch_bounds__(256) void k_schur_points(SchurArgs A)
 // C[b][i][j] at lane 16i + 4b + j; block b = 2I + J holds rows 4I + i, columns 4J + j of the
 // padded 8x8.  A = -B D^-1 of the pair's first edge (6x3, k = its column), B = H_pl of the
 // second (3x6, k = its row).
-#define SCHUR_CHAINS 16  // waves per block workgroup = accumulator chains (the oracle's)
-__global__ __launch_bounds__(64 * SCHUR_CHAINS) void k_schur_blocks(SchurArgs A)
+#ifndef ORBG_SCHUR_XCD
+#define ORBG_SCHUR_XCD 1
+#endif
+#define SCHUR_CHAINS 16
+#ifndef SCHUR_BATCH
+#define SCHUR_BATCH 11  // pairs per step and chain (11: 62 VGPRs, two 16-wave workgroups per CU; 16: 82)
+#endif  // waves per block workgroup = accumulator chains (the oracle's)
+__global__ __launch_bounds__(64 * SCHUR_CHAINS) __attribute__((amdgpu_waves_per_eu(8, 8))) void k_schur_blocks(SchurArgs A)
 {
     __shared__ double tile[SCHUR_CHAINS][64];
-    const int lane = threadIdx.x & 63, u = threadIdx.x >> 6, bk = blockIdx.x;
+    // XCD-aware: consecutive blocks (one window's, sorted by segment) share an XCD's L2, so a
+    // window's records and H_pl are fetched into one L2 rather than into all eight
+    const int lane = threadIdx.x & 63, u = threadIdx.x >> 6,
+              bk = ORBG_SCHUR_XCD ? xcd_remap(blockIdx.x, gridDim.x) : (int)blockIdx.x;
     const int i1 = A.blk_i1[bk], i2 = A.blk_i2[bk], sg = A.blk_seg[bk];
     const int lo = A.seg_lo[sg], n = 6 * (A.seg_lo[sg + 1] - lo);
     const int k = lane >> 4, b = (lane >> 2) & 3, t = lane & 3;
@@ -132,22 +141,31 @@ __global__ __launch_bounds__(64 * SCHUR_CHAINS) void k_schur_blocks(SchurArgs A)
         c = A.hpose[36 * (size_t)A.free_pose[i1] + 6 * ro + co] + (ro == co ? A.lambda : 0.0);
     const int p0 = A.blk_off[bk], np = A.blk_off[bk + 1] - p0;
     const int nu = np > u ? (np - u + SCHUR_CHAINS - 1) / SCHUR_CHAINS : 0;  // p0 + u + 16 j
-    // 16 pairs per step: lane l < 16 loads pair j0 + l's ids once, the wave takes them by
-    // readlane, so all 32 operand loads of the step are in flight together
-    for (int j0 = 0; j0 < nu; j0 += 16) {
-        const int m = min(16, nu - j0);
-        int2 prl = make_int2(0, 0);
-        if (lane < m) prl = A.blk_pairs[p0 + u + SCHUR_CHAINS * (j0 + lane)];
-        double av[16], bv[16];
+    // SCHUR_BATCH pairs per step: lane l < SCHUR_BATCH holds pair j0 + l's ids, the wave takes
+    // them by readlane, so all 2 SCHUR_BATCH operand loads of the step are in flight together;
+    // the next step's ids are loaded during this step's gathers.  Every load is unconditional
+    // (clamped pair / entry, the value then selected away), so the waits before the MFMAs
+    // leave the ids of the next step in flight.
+    const int oac = va ? oa : 0, obc = vb ? ob : 0;
+    auto ids = [&](int j) -> int2 {
+        return A.blk_pairs[p0 + u + SCHUR_CHAINS * min(j + lane, nu - 1)];
+    };
+    int2 prl = nu > 0 ? ids(0) : make_int2(0, 0);
+    for (int j0 = 0; j0 < nu; j0 += SCHUR_BATCH) {
+        const int m = min(SCHUR_BATCH, nu - j0);
+        double av[SCHUR_BATCH], bv[SCHUR_BATCH];
 #pragma unroll
-        for (int q = 0; q < 16; q++) {
+        for (int q = 0; q < SCHUR_BATCH; q++) {
             const int s1 = __builtin_amdgcn_readlane(prl.x, q), e2 = __builtin_amdgcn_readlane(prl.y, q);
-            av[q] = (va && q < m) ? -A.rec[(size_t)s1 * SCHUR_REC + oa] : 0.0;
-            bv[q] = (vb && q < m) ? A.hpl[(size_t)e2 * A.hpl_stride + ob] : 0.0;
+            av[q] = A.rec[(size_t)s1 * SCHUR_REC + oac];
+            bv[q] = A.hpl[(size_t)e2 * A.hpl_stride + obc];
         }
+        const int2 nxt = j0 + SCHUR_BATCH < nu ? ids(j0 + SCHUR_BATCH) : prl;
 #pragma unroll
-        for (int q = 0; q < 16; q++)
-            if (q < m) c = __builtin_amdgcn_mfma_f64_4x4x4f64(av[q], bv[q], c, 0, 0, 0);
+        for (int q = 0; q < SCHUR_BATCH; q++)
+            if (q < m)
+                c = __builtin_amdgcn_mfma_f64_4x4x4f64(va ? -av[q] : 0.0, vb ? bv[q] : 0.0, c, 0, 0, 0);
+        prl = nxt;
     }
     tile[u][lane] = c;
     __syncthreads();

@@ -18,6 +18,9 @@ python3 -c "import json;d=json.load(open('$O/c2.json'));print(d['value'],d['ms_p
 echo "[final] bench --stereo (C4)"
 timeout -k 10 300 python bench.py --stereo > $O/stereo.json 2> $O/stereo.err
 python3 -c "import json;d=json.load(open('$O/stereo.json'));print(d['value'],d['ms_per_step'],d['cpu_baseline']['value'],d['cpu_baseline']['value_1core'])"
+echo "[final] bench --host-input (C3 fed from pinned host memory)"
+timeout -k 10 300 python bench.py --host-input --no-cpu > $O/host.json 2> $O/host.err
+python3 -c "import json;d=json.load(open('$O/host.json'));print(d['value'],d['ms_per_step'],d['host_input'])"
 echo "[final] BA (C5)"
 timeout -k 10 300 python tools/ba_bench.py > $O/ba.json 2> $O/ba.err
 tail -c 400 $O/ba.json
