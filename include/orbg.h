@@ -851,6 +851,9 @@ int orbg_ba_graph_destroy(orbg_ba_graph *graph);
  * (uploaded from pinned staging: no host synchronisation beyond waiting for the previous
  * call's upload). */
 int orbg_ba_graph_set_active(orbg_ctx *ctx, orbg_ba_graph *graph, const uint8_t *active);
+/* e->setRobustKernel(0) / the Huber kernel per edge (Optimizer.cc:884, :900 remove it from
+ * every edge after the outlier pass): robust[e] (host, 0 or 1), ordered like set_active. */
+int orbg_ba_graph_set_robust(orbg_ctx *ctx, orbg_ba_graph *graph, const uint8_t *robust);
 /* buildSystem over the graph: outputs as orbg_ba_build_system_device (d_hpl [nedge][3][6]). */
 int orbg_ba_graph_build_system(orbg_ctx *ctx, orbg_ba_graph *graph, const orbg_pose *d_poses,
                                const double *d_points, double *d_hpl, double *d_hpose,
@@ -876,6 +879,33 @@ int orbg_ba_graph_schur_solve(orbg_ctx *ctx, orbg_ba_graph *graph, double lambda
                               const double *d_hpl, const double *d_hpose, const double *d_bpose,
                               const double *d_hpoint, const double *d_bpoint, double *d_dx_pose,
                               double *d_dx_point, int32_t *d_ok);
+/* SparseOptimizer::update for LocalBundleAdjustment's vertex types (device memory, context
+ * stream): VertexSE3Expmap::oplusImpl (types_six_dof_expmap.h:73-76: estimate =
+ * SE3Quat::exp(dx) * estimate, se3quat.h:223-257; poses with `fixed` set are copied
+ * unchanged) and VertexSBAPointXYZ::oplusImpl (estimate += dx).  In place when the outputs
+ * are the inputs. */
+int orbg_ba_update_device(orbg_ctx *ctx, const orbg_pose *d_poses, int npose,
+                          const double *d_points, int npoint, const double *d_dx_pose,
+                          const double *d_dx_point, orbg_pose *d_poses_out, double *d_points_out);
+/* optimizer.optimize(iterations) of LocalBundleAdjustment (Optimizer.cc:857, :905) on an
+ * orbg_ba_graph, OptimizationAlgorithmLevenberg::solve per iteration
+ * (optimization_algorithm_levenberg.cpp:61-164: tau 1e-5, goodStep scales 1/3 and 2/3, 10
+ * trials after failure, the (iniChi - chi) * 1e3 < iniChi three-strikes stop): build ->
+ * Schur solve -> update -> error pass -> accept or pop, all on the context stream over the
+ * estimates in HBM (d_poses / d_points, updated in place); the host reads the trial's three
+ * scalars (activeRobustChi2, computeScale, the solver's ok) once per trial.  The scalars
+ * are deterministic device reductions (a fixed grid-stride + tree order; g2o sums
+ * sequentially).  orbg_ba_graph_schur_plan must have been called (it holds the fixed poses;
+ * `fixed` of d_poses must agree); the active edges are the graph's (orbg_ba_graph_set_active).
+ * report (may be NULL): iterations run, trials, chi2 before / after, the final lambda, and
+ * terminated = 1 (rho == 0 or 10 failed trials) or 2 (three iterations without a 1e-3
+ * relative decrease), 0 if every iteration ran. */
+typedef struct {
+    int32_t iterations, trials, terminated, pad;
+    double initial_chi2, final_chi2, lambda;
+} orbg_lm_report;
+int orbg_ba_graph_optimize(orbg_ctx *ctx, orbg_ba_graph *graph, orbg_pose *d_poses,
+                           double *d_points, int iterations, orbg_lm_report *report);
 
 /* g2o's per-trial error pass for the two LBA edge types: SparseOptimizer::
  * computeActiveErrors (Thirdparty/g2o/g2o/core/sparse_optimizer.cpp:61-76, computeError

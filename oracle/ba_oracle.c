@@ -15,6 +15,7 @@
  */
 #include "orb_oracle.h"
 
+#include <float.h>
 #include <math.h>
 #include <stdlib.h>
 #include <string.h>
@@ -591,4 +592,128 @@ int orc_ba_schur_solve(const orc_pose *poses, int npose, int npoint, const orc_e
     free(Dinv);
     free(xp);
     return ok;
+}
+
+/* ---- the Levenberg-Marquardt loop of LocalBundleAdjustment's optimizer.optimize(n) ----
+ * SparseOptimizer::optimize + OptimizationAlgorithmLevenberg::solve
+ * (optimization_algorithm_levenberg.cpp:61-164; tau 1e-5 :47, goodStep scales 2/3 and 1/3
+ * :48-49, maxTrialsAfterFailure 10 :51, computeLambdaInit :166-180, computeScale :182-189),
+ * SparseOptimizer::update (oplusImpl of the two vertex types, types_six_dof_expmap.h:73-76 and
+ * the point's +=), push / pop as copies.  Sums in g2o's sequential order (activeRobustChi2 over
+ * the active edges in edge order, computeScale over [free poses' increments, points'] in
+ * index order -- fixed poses and edge-less points contribute exact zeros). */
+void orc_ba_update(orc_pose *poses, int npose, double *points, int npoint, const double *dx_pose,
+                   const double *dx_point)
+{
+    for (int i = 0; i < npose; i++)
+        if (!poses[i].fixed)
+            orc_se3_oplus(poses[i].q, poses[i].t, dx_pose + 6 * (size_t)i);
+    for (size_t j = 0; j < 3 * (size_t)npoint; j++)
+        points[j] += dx_point[j];
+}
+
+int orc_ba_optimize(orc_pose *poses, int npose, double *points, int npoint, const orc_edge *edges,
+                    int nedge, int iterations, double report[6])
+{
+    const size_t np = npose > 0 ? (size_t)npose : 1, nq = npoint > 0 ? (size_t)npoint : 1;
+    const size_t ne = nedge > 0 ? (size_t)nedge : 1;
+    orc_edge_out *eo = (orc_edge_out *)calloc(ne, sizeof(orc_edge_out));
+    double *hp = (double *)calloc(np * 36, 8), *bp = (double *)calloc(np * 6, 8);
+    double *hq = (double *)calloc(nq * 9, 8), *bq = (double *)calloc(nq * 3, 8);
+    double *dxp = (double *)calloc(np * 6, 8), *dxq = (double *)calloc(nq * 3, 8);
+    orc_pose *sp = (orc_pose *)calloc(np, sizeof(orc_pose));
+    double *sq = (double *)calloc(nq * 3, 8);
+    double currentChi = 0, lambda = 0;
+    int ni = 2, nBad = 0, it = 0, trials = 0, term = 0;
+    for (it = 0; it < iterations; it++) {
+        if (it == 0)
+            currentChi = orc_ba_errors(poses, points, edges, nedge, NULL, NULL, NULL, NULL);
+        if (it == 0)
+            report[3] = currentChi;
+        const double iniChi = currentChi;
+        orc_ba_linearize(poses, npose, points, npoint, edges, nedge, eo, hp, bp, hq, bq);
+        if (it == 0) {
+            double m = 0;
+            for (int i = 0; i < npose; i++)
+                if (!poses[i].fixed)
+                    for (int j = 0; j < 6; j++)
+                        m = fmax(fabs(hp[36 * (size_t)i + 7 * j]), m);
+            for (int p = 0; p < npoint; p++)
+                for (int j = 0; j < 3; j++)
+                    m = fmax(fabs(hq[9 * (size_t)p + 4 * j]), m);
+            lambda = 1e-5 * m;
+            ni = 2;
+            nBad = 0;
+        }
+        double rho = 0;
+        int qmax = 0;
+        do {
+            memcpy(sp, poses, (size_t)npose * sizeof(orc_pose));
+            memcpy(sq, points, (size_t)npoint * 24);
+            const int ok2 = orc_ba_schur_solve(poses, npose, npoint, edges, nedge, eo, hp, bp, hq,
+                                               bq, lambda, dxp, dxq);
+            orc_ba_update(poses, npose, points, npoint, dxp, dxq);
+            double tempChi = orc_ba_errors(poses, points, edges, nedge, NULL, NULL, NULL, NULL);
+            if (!ok2)
+                tempChi = DBL_MAX;
+            rho = currentChi - tempChi;
+            double scale = 0;
+            for (int i = 0; i < npose; i++)
+                if (!poses[i].fixed)
+                    for (int j = 0; j < 6; j++) {
+                        const double x = dxp[6 * (size_t)i + j];
+                        scale += x * (lambda * x + bp[6 * (size_t)i + j]);
+                    }
+            for (size_t j = 0; j < 3 * (size_t)npoint; j++)
+                scale += dxq[j] * (lambda * dxq[j] + bq[j]);
+            scale += 1e-3;
+            rho /= scale;
+            trials++;
+            if (rho > 0 && isfinite(tempChi)) {
+                double alpha = 1. - orc_lm_cube(2 * rho - 1);
+                alpha = fmin(alpha, 2. / 3.);
+                const double sf = fmax(1. / 3., alpha);
+                lambda *= sf;
+                ni = 2;
+                currentChi = tempChi;
+            } else {
+                lambda *= ni;
+                ni *= 2;
+                memcpy(poses, sp, (size_t)npose * sizeof(orc_pose));
+                memcpy(points, sq, (size_t)npoint * 24);
+            }
+            qmax++;
+        } while (rho < 0 && qmax < 10);
+        if (qmax == 10 || rho == 0) {
+            term = 1;
+            it++;
+            break;
+        }
+        if ((iniChi - currentChi) * 1e3 < iniChi)
+            nBad++;
+        else
+            nBad = 0;
+        if (nBad >= 3) {
+            term = 2;
+            it++;
+            break;
+        }
+    }
+    if (iterations == 0)
+        report[3] = currentChi = orc_ba_errors(poses, points, edges, nedge, NULL, NULL, NULL, NULL);
+    report[0] = it;
+    report[1] = trials;
+    report[2] = term;
+    report[4] = currentChi;
+    report[5] = lambda;
+    free(eo);
+    free(hp);
+    free(bp);
+    free(hq);
+    free(bq);
+    free(dxp);
+    free(dxq);
+    free(sp);
+    free(sq);
+    return it;
 }

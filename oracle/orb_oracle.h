@@ -500,6 +500,14 @@ int orc_ba_schur_solve(const orc_pose *poses, int npose, int npoint, const orc_e
                        const double *bpose, const double *hpoint, const double *bpoint,
                        double lambda, double *dx_pose, double *dx_point);
 int orc_ldlt_dense_solve(double *A, int n, double *x);
+/* SparseOptimizer::update for the two vertex types (in place; fixed poses untouched) */
+void orc_ba_update(orc_pose *poses, int npose, double *points, int npoint, const double *dx_pose,
+                   const double *dx_point);
+/* optimizer.optimize(iterations) with OptimizationAlgorithmLevenberg (in place).  report[6] =
+ * iterations run, trials, terminated (0, 1: rho 0 / 10 failed trials, 2: three weak
+ * iterations), chi2 before, chi2 after, final lambda.  Returns the iterations run. */
+int orc_ba_optimize(orc_pose *poses, int npose, double *points, int npoint, const orc_edge *edges,
+                    int nedge, int iterations, double report[6]);
 /* central-difference Jacobian of computeError (base_binary_edge.hpp:131-205, delta 1e-9) */
 void orc_ba_numeric_jacobian(const orc_pose *pose, const double *xyz, const orc_edge *e,
                              double jp[3][3], double jt[3][6]);

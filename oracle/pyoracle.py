@@ -191,6 +191,9 @@ def lib():
         L.orc_ba_linearize.argtypes = [vp, C.c_int, vp, C.c_int, vp, C.c_int, vp, vp, vp, vp, vp]
         L.orc_ba_numeric_jacobian.argtypes = [vp, vp, vp, vp, vp]
         L.orc_ba_errors.argtypes = [vp, vp, vp, C.c_int, vp, vp, vp, vp]
+        L.orc_ba_update.argtypes = [vp, C.c_int, vp, C.c_int, vp, vp]
+        L.orc_ba_optimize.argtypes = [vp, C.c_int, vp, C.c_int, vp, C.c_int, C.c_int, vp]
+        L.orc_ba_optimize.restype = C.c_int
         L.orc_ba_errors.restype = C.c_double
         L.orc_ba_schur_solve.argtypes = [vp, C.c_int, C.c_int, vp, C.c_int, vp, vp, vp, vp, vp,
                                          C.c_double, vp, vp]
@@ -592,6 +595,30 @@ def ba_schur_solve(poses, npoint, edges, eout, hpose, bpose, hpoint, bpoint, lam
     ok = lib().orc_ba_schur_solve(_p(poses), len(poses), npoint, _p(edges), len(edges), _p(eout),
                                   _p(hp), _p(bp), _p(hq), _p(bq), float(lam), _p(dp), _p(dq))
     return bool(ok), dp[:len(poses)], dq[:npoint]
+
+
+def ba_update(poses, points, dx_pose, dx_point):
+    """SparseOptimizer::update restated (orc_ba_update): returns updated copies."""
+    poses = np.array(poses, POSE_DTYPE)
+    points = np.array(points, np.float64)
+    dp = np.ascontiguousarray(dx_pose, np.float64)
+    dq = np.ascontiguousarray(dx_point, np.float64)
+    lib().orc_ba_update(_p(poses), len(poses), _p(points), len(points), _p(dp), _p(dq))
+    return poses, points
+
+
+def ba_optimize(poses, points, edges, iterations):
+    """optimizer.optimize(iterations) with g2o's Levenberg-Marquardt restated
+    (orc_ba_optimize): returns (poses, points, report dict)."""
+    poses = np.array(poses, POSE_DTYPE)
+    points = np.array(points, np.float64)
+    edges = np.ascontiguousarray(edges, EDGE_DTYPE)
+    rep = np.zeros(6)
+    lib().orc_ba_optimize(_p(poses), len(poses), _p(points), len(points), _p(edges), len(edges),
+                          int(iterations), _p(rep))
+    return poses, points, dict(iterations=int(rep[0]), trials=int(rep[1]),
+                               terminated=int(rep[2]), initial_chi2=rep[3], final_chi2=rep[4],
+                               **{"lambda": rep[5]})
 
 
 class Vocab:

@@ -85,6 +85,13 @@ class KeyFrameGeo(C.Structure):
                 ("depth", C.c_void_p), ("n", C.c_int32)]
 
 
+class LmReport(C.Structure):
+    """orbg_lm_report (include/orbg.h)."""
+    _fields_ = [("iterations", C.c_int32), ("trials", C.c_int32), ("terminated", C.c_int32),
+                ("pad", C.c_int32), ("initial_chi2", C.c_double), ("final_chi2", C.c_double),
+                ("lam", C.c_double)]
+
+
 class KeyFrames(C.Structure):
     """orbg_keyframes (include/orbg.h): a set of KeyFrames in device memory."""
     _fields_ = [("desc", C.c_void_p), ("kps", C.c_void_p), ("uright", C.c_void_p),
@@ -263,6 +270,9 @@ def lib():
         "orbg_ba_graph_errors": (i32, [vp, vp, vp, vp, vp, vp, vp, vp]),
         "orbg_ba_graph_schur_plan": (i32, [vp, vp, vp]),
         "orbg_ba_graph_schur_solve": (i32, [vp, vp, C.c_double, vp, vp, vp, vp, vp, vp, vp, vp]),
+        "orbg_ba_graph_set_robust": (i32, [vp, vp, vp]),
+        "orbg_ba_update_device": (i32, [vp, vp, i32, vp, i32, vp, vp, vp, vp]),
+        "orbg_ba_graph_optimize": (i32, [vp, vp, vp, vp, i32, P(LmReport)]),
         "orbg_search_for_triangulation": (i32, [vp, P(KeyFrame), P(KeyFrame), vp, i32, i32, vp,
                                                 P(i32)]),
         "orbg_search_for_triangulation_batch_device": (i32, [vp, P(KeyFrames), i32, vp, vp, vp,

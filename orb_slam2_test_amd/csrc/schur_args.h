@@ -26,7 +26,7 @@ namespace orbg {
 struct SchurPlanHost {
     int npose = 0, npoint = 0, nfree = 0, nblk = 0, nseg = 0, max_seg = 0;
     std::vector<int32_t> pidx, free_pose, pt_off, pt_edges, slot_point, edge_pose, blk_off,
-        blk_i1, blk_i2, blk_seg, pose_off, pose_slots, seg_lo;
+        blk_i1, blk_i2, blk_seg, blk_order, pose_off, pose_slots, seg_lo;
     std::vector<int2> blk_pairs;
     std::vector<int64_t> seg_soff;  // [nseg + 1] doubles before each segment's dense matrix
 };
@@ -47,6 +47,7 @@ struct SchurArgs {
     const int32_t *blk_off;            // [nblk + 1] (slot1, e2) pairs per upper block, landmark order
     const int2 *blk_pairs;
     const int32_t *blk_i1, *blk_i2, *blk_seg;  // [nblk]
+    const int32_t *blk_order;          // [nblk] k_schur_blocks' dispatch order (a permutation)
     const int32_t *pose_off, *pose_slots;      // active slots per free pose, landmark order
     const int32_t *seg_lo;             // [nseg + 1] free-index range of each segment
     const int64_t *seg_soff;           // [nseg + 1] offset (doubles) of its dense matrix in S

@@ -99,6 +99,8 @@ __global__ __launch_bounds__(256) void k_schur_points(SchurArgs A)
             }
         }
     }
+    // (the record in registers, staged as double2: 150 VGPRs; writing rows straight to LDS
+    // as doubles, ~80 VGPRs, measured slower: 0.105 against 0.085 ms, r05l)
 #pragma unroll
     for (int k = 0; k < SCHUR_REC; k += 2) rec[tid * (SCHUR_REC / 2) + k / 2] = make_double2(v[k], v[k + 1]);
     __syncthreads();
@@ -128,7 +130,7 @@ __global__ __launch_bounds__(64 * SCHUR_CHAINS) __attribute__((amdgpu_waves_per_
     // XCD-aware: consecutive blocks (one window's, sorted by segment) share an XCD's L2, so a
     // window's records and H_pl are fetched into one L2 rather than into all eight
     const int lane = threadIdx.x & 63, u = threadIdx.x >> 6,
-              bk = ORBG_SCHUR_XCD ? xcd_remap(blockIdx.x, gridDim.x) : (int)blockIdx.x;
+              bk = A.blk_order[ORBG_SCHUR_XCD ? xcd_remap(blockIdx.x, gridDim.x) : (int)blockIdx.x];
     const int i1 = A.blk_i1[bk], i2 = A.blk_i2[bk], sg = A.blk_seg[bk];
     const int lo = A.seg_lo[sg], n = 6 * (A.seg_lo[sg + 1] - lo);
     const int k = lane >> 4, b = (lane >> 2) & 3, t = lane & 3;
@@ -288,6 +290,66 @@ __global__ __launch_bounds__(256) void k_schur_ldlt(SchurArgs A)
         for (int e = tid; e < n; e += 256) xg[e] = x[e];
 }
 
+// The same factorisation and solves by ONE wave per segment, the system in LDS: a 6 n_free
+// system of an LBA window (n ~ 60) gives a wave plenty of lanes per step, and a wave's LDS
+// operations complete in order, so the 2 n steps need no workgroup barriers (the 256-thread
+// form above pays two per column).  The trailing update walks the step's lower triangle
+// flattened, 64 elements per instruction; every element still takes its updates in k order.
+#ifndef ORBG_SCHUR_LDLT_WAVE
+#define ORBG_SCHUR_LDLT_WAVE 0  // measured 0.193 ms against 0.060 for the 256-thread form (r05l): off
+#endif
+__global__ __launch_bounds__(64) void k_schur_ldlt_wave(SchurArgs A)
+{
+    extern __shared__ __attribute__((aligned(16))) double sl_lds[];
+    const int sg = blockIdx.x, lane = threadIdx.x;
+    const int lo = A.seg_lo[sg], n = 6 * (A.seg_lo[sg + 1] - lo);
+    if (n == 0) return;
+    double *Sg = A.S + A.seg_soff[sg], *xg = A.x + 6 * lo;
+    double *M = sl_lds, *x = sl_lds + (size_t)n * n;
+    for (int e = lane; e < n * n; e += 64) M[e] = Sg[e];
+    for (int e = lane; e < n; e += 64) x[e] = xg[e];
+    wave_sync_lds();
+    for (int j = 0; j < n; j++) {
+        const double d = M[(size_t)j * n + j];
+        if (d == 0.0 || !isfinite(d)) {  // uniform: the oracle stops here, ok = 0
+            if (lane == 0) *A.ok = 0;
+            return;
+        }
+        for (int i = j + 1 + lane; i < n; i += 64) M[(size_t)i * n + j] = M[(size_t)i * n + j] / d;
+        wave_sync_lds();
+        // element t of the triangle r in (j, n), c in (j, r], row-major: (r, c) advanced by 64
+        const int m = n - j - 1;
+        const int tot = m * (m + 1) / 2;
+        int r = j + 1, c = j + 1 + lane;
+        while (c > r && r < n) {  // place t = lane
+            c -= r - j;
+            r++;
+        }
+        for (int t = lane; t < tot; t += 64) {
+            M[(size_t)r * n + c] -= M[(size_t)r * n + j] * M[(size_t)c * n + j] * d;
+            c += 64;
+            while (c > r && r < n) {
+                c -= r - j;
+                r++;
+            }
+        }
+        wave_sync_lds();
+    }
+    for (int k = 0; k < n; k++) {
+        const double xk = x[k];
+        for (int i = k + 1 + lane; i < n; i += 64) x[i] -= M[(size_t)i * n + k] * xk;
+        wave_sync_lds();
+    }
+    for (int i = lane; i < n; i += 64) x[i] /= M[(size_t)i * n + i];
+    wave_sync_lds();
+    for (int k = n - 1; k > 0; k--) {
+        const double xk = x[k];
+        for (int i = lane; i < k; i += 64) x[i] -= M[(size_t)k * n + i] * xk;
+        wave_sync_lds();
+    }
+    for (int e = lane; e < n; e += 64) xg[e] = x[e];
+}
+
 // x_l = D^-1 (b_l - B^T x_p); pose increments scattered out
 __global__ void k_schur_backsub(SchurArgs A)
 {
@@ -342,7 +404,13 @@ int launch_schur(hipStream_t st, const SchurArgs &A, void *prof)
         const int n = 6 * A.max_seg;
         const size_t lds = ((size_t)n * n + n) * sizeof(double);
         prof_begin(prof, st, "schur_ldlt", &ev);
-        if (lds <= 160 * 1024 - 64) {
+        if (ORBG_SCHUR_LDLT_WAVE && lds <= 160 * 1024 - 64) {
+            if (lds > 64 * 1024 &&
+                hipFuncSetAttribute((const void *)k_schur_ldlt_wave,
+                                    hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) != hipSuccess)
+                return ORBG_EIO;
+            hipLaunchKernelGGL(k_schur_ldlt_wave, dim3(A.nseg), dim3(64), lds, st, A);
+        } else if (lds <= 160 * 1024 - 64) {
             if (lds > 64 * 1024 &&
                 hipFuncSetAttribute((const void *)k_schur_ldlt<true>,
                                     hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) != hipSuccess)
@@ -483,6 +551,15 @@ void build_schur_plan(int npose, int npoint, int nedge, const int32_t *epose,
     }
     P.blk_seg.assign(std::max(P.nblk, 1), 0);
     for (int b = 0; b < P.nblk; b++) P.blk_seg[b] = seg_of[P.blk_i1[b]];
+    // dispatch order of k_schur_blocks: segment by segment (one window's blocks on one XCD),
+    // within a segment the blocks with the most pairs first (the diagonal blocks are ~4x the
+    // others: longest-first keeps them off the kernel's tail); any order gives the same bits
+    P.blk_order.resize(std::max(P.nblk, 1));
+    for (int b = 0; b < std::max(P.nblk, 1); b++) P.blk_order[b] = b;
+    std::stable_sort(P.blk_order.begin(), P.blk_order.begin() + P.nblk, [&](int a, int b) {
+        if (P.blk_seg[a] != P.blk_seg[b]) return P.blk_seg[a] < P.blk_seg[b];
+        return P.blk_off[a + 1] - P.blk_off[a] > P.blk_off[b + 1] - P.blk_off[b];
+    });
     if (P.nblk == 0) {
         P.blk_i1.push_back(0);
         P.blk_i2.push_back(0);

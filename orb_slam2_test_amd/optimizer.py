@@ -230,6 +230,44 @@ class DeviceLBA:
             p(self.d_bpose), p(self.d_hpoint), p(self.d_bpoint), p(self.d_dx_pose),
             p(self.d_dx_point), p(self.d_ok)), "orbg_ba_graph_schur_solve")
 
+    def set_robust(self, robust):
+        """setRobustKernel per edge (orbg_ba_graph_set_robust): robust[e] != 0 keeps Huber."""
+        r = np.ascontiguousarray(np.asarray(robust) != 0, np.uint8)
+        L.check(L.lib().orbg_ba_graph_set_robust(self.ctx.handle, self.graph, r.ctypes.data),
+                "orbg_ba_graph_set_robust")
+
+    def update(self):
+        """SparseOptimizer::update with the last schur_solve's increments, in place on the
+        device estimates (orbg_ba_update_device; fixed poses untouched)."""
+        p = lambda t: L.C.c_void_p(t.data_ptr())  # noqa: E731
+        L.check(L.lib().orbg_ba_update_device(
+            self.ctx.handle, p(self.d_poses), self.np, p(self.d_points), self.nq,
+            p(self.d_dx_pose), p(self.d_dx_point), p(self.d_poses), p(self.d_points)),
+            "orbg_ba_update_device")
+
+    def optimize(self, iterations):
+        """optimizer.optimize(iterations) (Optimizer.cc:857, :905) with g2o's
+        Levenberg-Marquardt on the device estimates (orbg_ba_graph_optimize): build, Schur
+        solve, update and error pass per trial on the context stream, three scalars read
+        back per trial.  Needs schur_plan(fixed).  Returns the orbg_lm_report as a dict."""
+        if self.graph is None:
+            raise ValueError("optimize needs a DeviceLBA built with graph=True")
+        rep = L.LmReport()
+        p = lambda t: L.C.c_void_p(t.data_ptr())  # noqa: E731
+        L.check(L.lib().orbg_ba_graph_optimize(self.ctx.handle, self.graph, p(self.d_poses),
+                                               p(self.d_points), int(iterations), L.C.byref(rep)),
+                "orbg_ba_graph_optimize")
+        return dict(iterations=rep.iterations, trials=rep.trials, terminated=rep.terminated,
+                    initial_chi2=rep.initial_chi2, final_chi2=rep.final_chi2,
+                    **{"lambda": rep.lam})
+
+    def estimates(self):
+        """(poses, points) of the device estimates, host copies."""
+        self.ctx.sync()
+        poses = np.frombuffer(self.d_poses.cpu().numpy().tobytes(), L.POSE_DTYPE).copy()
+        points = np.frombuffer(self.d_points.cpu().numpy().tobytes(), np.float64).reshape(-1, 3).copy()
+        return poses, points
+
     def __del__(self):
         if getattr(self, "graph", None) is not None:
             L.lib().orbg_ba_graph_destroy(self.graph)
