@@ -8,6 +8,7 @@
 #include <atomic>
 #include <cmath>
 #include <cstdarg>
+#include <cfloat>
 #include <cstddef>
 #include <cstdio>
 #include <cstdlib>
@@ -81,6 +82,13 @@ int launch_tri_match(hipStream_t st, const orbg_keyframes &K, int cap, const int
                      const int32_t *kf2, const orbg_triangulation_pair *geo, int npairs,
                      const float *scale, const float *sigma2, int nlevels, int only_stereo,
                      int check_ori, int32_t *match, int32_t *nmatch);
+int launch_ba_update(hipStream_t st, const orbg_pose *poses, int npose, const double *points,
+                     int npoint, const double *dxp, const double *dxq, orbg_pose *pout,
+                     double *qout);
+int launch_lm_reduce(hipStream_t st, int mode, int n1, int n2, double lambda, const double *a1,
+                     const double *a2, const double *b1, const double *b2,
+                     const BaPackedEdge *edges, double *part, double *out);
+int lm_reduce_groups();
 int launch_tri_geometry(hipStream_t st, const orbg_kf_camera *cams, const int32_t *kf1,
                         const int32_t *kf2, int npairs, orbg_triangulation_pair *geo);
 int launch_triangulate(hipStream_t st, const orbg_keyframes &K, const orbg_keypoint *kps_raw,
@@ -1936,6 +1944,9 @@ extern "C" int orbg_download_frame(orbg_ctx *c, int frame, orbg_keypoint *kps, u
 
 static int extract_graph(orbg_ctx *c, const uint8_t *img, int w, int h, size_t step,
                          orbg_keypoint *kps, uint8_t *desc, int cap, int *n_out);
+#ifndef ORBG_H2D_CHUNKS
+#define ORBG_H2D_CHUNKS 4  // orbg_extract's image upload bands (host copy beside the DMA)
+#endif
 
 extern "C" int orbg_extract(orbg_ctx *c, const uint8_t *img, int w, int h, size_t step,
                             orbg_keypoint *kps, uint8_t *desc, int cap, int *n_out)
@@ -1960,17 +1971,23 @@ extern "C" int orbg_extract(orbg_ctx *c, const uint8_t *img, int w, int h, size_
     if (c->graph_mode && !c->prof.on && c->stream && !(c->pipelined && !c->serial) &&
         !c->mat_pending[c->slot ^ 1] && !c->rel_pending[c->slot ^ 1])
         return extract_graph(c, img, w, h, step, kps, desc, cap, n_out);
-    // rows into pinned staging, one DMA (a pageable 2-D copy of an odd-width image goes row
-    // by row: ~3 ms for 1241 x 376)
+    // rows into pinned staging (a pageable 2-D copy of an odd-width image goes row by row:
+    // ~3 ms for 1241 x 376), in ORBG_H2D_CHUNKS bands: the DMA of band k runs while the host
+    // copies band k + 1
     uint8_t *hs;
     if ((rc = stage(c, bytes, &hs))) return rc;
     HIPCHK(hipStreamSynchronize(c->stream));  // the staging buffer's previous DMA is done
-    if (step == (size_t)w) {
-        std::memcpy(hs, img, bytes);
-    } else {
-        for (int y = 0; y < h; y++) std::memcpy(hs + (size_t)y * w, img + (size_t)y * step, w);
+    const int nch = std::max(1, std::min(ORBG_H2D_CHUNKS, h));
+    for (int k = 0; k < nch; k++) {
+        const int y0 = (int)((int64_t)h * k / nch), y1 = (int)((int64_t)h * (k + 1) / nch);
+        if (step == (size_t)w) {
+            std::memcpy(hs + (size_t)y0 * w, img + (size_t)y0 * w, (size_t)(y1 - y0) * w);
+        } else {
+            for (int y = y0; y < y1; y++) std::memcpy(hs + (size_t)y * w, img + (size_t)y * step, w);
+        }
+        HIPCHK(hipMemcpyAsync(c->d_img + (size_t)y0 * w, hs + (size_t)y0 * w, (size_t)(y1 - y0) * w,
+                              hipMemcpyHostToDevice, c->stream));
     }
-    HIPCHK(hipMemcpyAsync(c->d_img, hs, bytes, hipMemcpyHostToDevice, c->stream));
     if ((rc = launch_extract(c, c->d_img, 1, w, (int64_t)bytes))) return rc;
     return orbg_download_frame(c, 0, kps, desc, cap, n_out);
 }
@@ -3026,6 +3043,9 @@ struct orbg_ba_graph {
     uint8_t *d_schur = nullptr;  // structure + scratch (schur_layout)
     size_t schur_bytes = 0;
     SchurArgs sa{};
+    // orbg_ba_graph_optimize's workspace (allocated on first use): the system, the errors,
+    // the increments, the pushed estimates and the reductions' scalars
+    uint8_t *d_lm = nullptr;
 };
 
 static size_t schur_layout(const SchurPlanHost &P, int nedge, uint8_t *base, SchurArgs &A,
@@ -3079,7 +3099,7 @@ static void ba_graph_free(orbg_ba_graph *g)
     for (void *p : {(void *)g->d_edges, (void *)g->d_cam, (void *)g->d_info, (void *)g->d_off,
                     (void *)g->d_pe, (void *)g->d_qoff, (void *)g->d_qe, (void *)g->d_special,
                     (void *)g->d_slice_off, (void *)g->d_slice_pose, (void *)g->d_part,
-                    (void *)g->d_schur})
+                    (void *)g->d_schur, (void *)g->d_lm})
         if (p) hipFree(p);
     delete g;
 }
@@ -3218,17 +3238,17 @@ extern "C" int orbg_ba_graph_destroy(orbg_ba_graph *g)
     return ORBG_OK;
 }
 
-extern "C" int orbg_ba_graph_set_active(orbg_ctx *c, orbg_ba_graph *g, const uint8_t *active)
+// rewrite flag bit `bit` of every packed edge from v[] and upload the edges in stream order
+// after the builds that read the previous flags, from pinned staging: no host
+// synchronisation (only the previous upload's, before the staging is rewritten)
+static int ba_graph_set_flag(orbg_ctx *c, orbg_ba_graph *g, const uint8_t *v, uint32_t bit)
 {
     if (!c || !g) return set_err(ORBG_EINVAL, "ctx / graph is NULL");
-    if (g->nedge && !active) return set_err(ORBG_EINVAL, "active is NULL");
+    if (g->nedge && !v) return set_err(ORBG_EINVAL, "flag array is NULL");
     if (g->device != c->device) return set_err(ORBG_EINVAL, "graph of another device");
-    for (int i = 0; i < g->nedge; i++)
-        g->h[i].flags = (g->h[i].flags & ~4u) | (active[i] ? 4u : 0u);
+    for (int i = 0; i < g->nedge; i++) g->h[i].flags = (g->h[i].flags & ~bit) | (v[i] ? bit : 0u);
     HIPCHK(hipSetDevice(c->device));
     if (g->nedge) {
-        // in stream order after the builds that read the previous flags, from pinned staging:
-        // no host synchronisation (only the previous upload's, before the staging is rewritten)
         if (!g->h_pin) {
             if (hipHostMalloc((void **)&g->h_pin, (size_t)g->nedge * sizeof(BaPackedEdge),
                               hipHostMallocDefault) != hipSuccess)
@@ -3242,8 +3262,20 @@ extern "C" int orbg_ba_graph_set_active(orbg_ctx *c, orbg_ba_graph *g, const uin
         HIPCHK(hipEventRecord(g->ev_up, c->stream));
         g->up_pending = true;
     }
+    return ORBG_OK;
+}
+
+extern "C" int orbg_ba_graph_set_active(orbg_ctx *c, orbg_ba_graph *g, const uint8_t *active)
+{
+    int rc = ba_graph_set_flag(c, g, active, 4u);
+    if (rc) return rc;
     if (g->schur_planned) return ba_graph_schur_replan(c, g);  // the active set shapes it
     return ORBG_OK;
+}
+
+extern "C" int orbg_ba_graph_set_robust(orbg_ctx *c, orbg_ba_graph *g, const uint8_t *robust)
+{
+    return ba_graph_set_flag(c, g, robust, 2u);
 }
 
 extern "C" int orbg_ba_graph_schur_plan(orbg_ctx *c, orbg_ba_graph *g, const uint8_t *fixed)
@@ -3315,6 +3347,178 @@ extern "C" int orbg_ba_graph_errors(orbg_ctx *c, orbg_ba_graph *g, const orbg_po
     if (launch_ba_errors_packed(c->stream, d_poses, d_points, g->d_edges, g->d_cam, g->d_info,
                                 g->nedge, d_err, d_chi2, d_rho0, d_depth_ok, &c->prof))
         return set_err(ORBG_EIO, "BA error kernel launch failed");
+    return ORBG_OK;
+}
+
+// g2o's pow(2 rho - 1, 3) as the device's lm_cube (se3_device.h): the exact cube as a
+// double-double, rounded once
+static double lm_cube_host(double t)
+{
+    const double h = t * t;
+    const double l = std::fma(t, t, -h);
+    const double ph = h * t;
+    const double pl = std::fma(h, t, -ph);
+    return ph + (pl + l * t);
+}
+
+extern "C" int orbg_ba_update_device(orbg_ctx *c, const orbg_pose *d_poses, int npose,
+                                     const double *d_points, int npoint, const double *d_dx_pose,
+                                     const double *d_dx_point, orbg_pose *d_poses_out,
+                                     double *d_points_out)
+{
+    if (!c) return set_err(ORBG_EINVAL, "ctx is NULL");
+    if (npose < 0 || npoint < 0) return set_err(ORBG_EINVAL, "negative size");
+    if ((npose && (!d_poses || !d_dx_pose || !d_poses_out)) ||
+        (npoint && (!d_points || !d_dx_point || !d_points_out)))
+        return set_err(ORBG_EINVAL, "NULL device array");
+    HIPCHK(hipSetDevice(c->device));
+    if (launch_ba_update(c->stream, d_poses, npose, d_points, npoint, d_dx_pose, d_dx_point,
+                         d_poses_out, d_points_out))
+        return set_err(ORBG_EIO, "k_ba_update launch failed");
+    return ORBG_OK;
+}
+
+// g2o's SparseOptimizer::optimize(iterations) with OptimizationAlgorithmLevenberg over an
+// orbg_ba_graph, the estimates in HBM (see include/orbg.h)
+extern "C" int orbg_ba_graph_optimize(orbg_ctx *c, orbg_ba_graph *g, orbg_pose *d_poses,
+                                      double *d_points, int iterations, orbg_lm_report *rep)
+{
+    if (!c || !g) return set_err(ORBG_EINVAL, "ctx / graph is NULL");
+    if (g->device != c->device) return set_err(ORBG_EINVAL, "graph of another device");
+    if (!g->schur_planned) return set_err(ORBG_EINVAL, "orbg_ba_graph_schur_plan not called");
+    if ((g->npose && !d_poses) || (g->npoint && !d_points))
+        return set_err(ORBG_EINVAL, "NULL device array");
+    if (iterations < 0) return set_err(ORBG_EINVAL, "negative iterations");
+    HIPCHK(hipSetDevice(c->device));
+    const size_t ne = (size_t)std::max(g->nedge, 1), np = (size_t)std::max(g->npose, 1),
+                 nq = (size_t)std::max(g->npoint, 1);
+    size_t o = 0;
+    auto take = [&](size_t bytes) {
+        const size_t r = o;
+        o += al256(bytes);
+        return r;
+    };
+    const size_t o_hpl = take(ne * 18 * 8), o_hp = take(np * 36 * 8), o_bp = take(np * 6 * 8),
+                 o_hq = take(nq * 9 * 8), o_bq = take(nq * 3 * 8), o_chi = take(ne * 8),
+                 o_rho = take(ne * 8), o_dxp = take(np * 6 * 8), o_dxq = take(nq * 3 * 8),
+                 o_sp = take(np * sizeof(orbg_pose)), o_sq = take(nq * 3 * 8),
+                 o_part = take((size_t)lm_reduce_groups() * 8), o_sc = take(4 * 8);
+    if (!g->d_lm) {
+        hipError_t e = hipMalloc((void **)&g->d_lm, o);
+        if (e != hipSuccess) return set_err(ORBG_ENOMEM, "LM workspace %zu bytes", o);
+    }
+    uint8_t *b = g->d_lm;
+    double *hpl = (double *)(b + o_hpl), *hp = (double *)(b + o_hp), *bp = (double *)(b + o_bp),
+           *hq = (double *)(b + o_hq), *bq = (double *)(b + o_bq), *chi = (double *)(b + o_chi),
+           *rho = (double *)(b + o_rho), *dxp = (double *)(b + o_dxp), *dxq = (double *)(b + o_dxq),
+           *sq = (double *)(b + o_sq), *part = (double *)(b + o_part), *sc = (double *)(b + o_sc);
+    orbg_pose *sp = (orbg_pose *)(b + o_sp);
+    // sc[0] active robust chi2, sc[1] computeScale, sc[2] max |H_jj|, sc[3] the solver's ok
+    hipStream_t st = c->stream;
+    int rc;
+    auto fail = [&](int code, const char *what) { return set_err(code, "LM: %s", what); };
+    auto chi2 = [&](double *out) -> int {
+        if ((rc = orbg_ba_graph_errors(c, g, d_poses, d_points, nullptr, chi, rho, nullptr)))
+            return rc;
+        if (launch_lm_reduce(st, 0, g->nedge, 0, 0.0, rho, nullptr, nullptr, nullptr, g->d_edges,
+                             part, out))
+            return fail(ORBG_EIO, "reduction launch");
+        return ORBG_OK;
+    };
+    auto read = [&](double *h, int n) -> int {
+        HIPCHK(hipMemcpyAsync(h, sc, n * sizeof(double), hipMemcpyDeviceToHost, st));
+        HIPCHK(hipStreamSynchronize(st));
+        return ORBG_OK;
+    };
+    orbg_lm_report R{};
+    double currentChi = 0.0, lambda = 0.0, hs[4];
+    int ni = 2, nBad = 0;
+    for (int it = 0; it < iterations; it++) {
+        if (it == 0) {  // computeActiveErrors at the start (later: the last accepted trial's)
+            if ((rc = chi2(sc)) || (rc = read(hs, 1))) return rc;
+            currentChi = hs[0];
+            R.initial_chi2 = currentChi;
+        }
+        const double iniChi = currentChi;
+        if ((rc = orbg_ba_graph_build_system(c, g, d_poses, d_points, hpl, hp, bp, hq, bq))) return rc;
+        if (it == 0) {  // computeLambdaInit: tau * max |H_jj| (before any lambda)
+            if (launch_lm_reduce(st, 2, 6 * g->npose, 3 * g->npoint, 0.0, hp, hq, nullptr, nullptr,
+                                 nullptr, part, sc + 2) ||
+                (rc = read(hs, 3)))
+                return rc ? rc : fail(ORBG_EIO, "reduction launch");
+            lambda = 1e-5 * hs[2];
+            ni = 2;
+            nBad = 0;
+        }
+        double rhoLM = 0.0;
+        int qmax = 0;
+        do {
+            // push
+            if (g->npose)
+                HIPCHK(hipMemcpyAsync(sp, d_poses, (size_t)g->npose * sizeof(orbg_pose),
+                                      hipMemcpyDeviceToDevice, st));
+            if (g->npoint)
+                HIPCHK(hipMemcpyAsync(sq, d_points, (size_t)g->npoint * 24, hipMemcpyDeviceToDevice, st));
+            // setLambda + solve + update (the Schur solve adds lambda to its own copies of
+            // the diagonal: no restoreDiagonal needed)
+            if ((rc = orbg_ba_graph_schur_solve(c, g, lambda, hpl, hp, bp, hq, bq, dxp, dxq,
+                                                (int32_t *)(sc + 3))))
+                return rc;
+            if (launch_ba_update(st, d_poses, g->npose, d_points, g->npoint, dxp, dxq, d_poses,
+                                 d_points) ||
+                launch_lm_reduce(st, 1, 6 * g->npose, 3 * g->npoint, lambda, dxp, dxq, bp, bq,
+                                 nullptr, part, sc + 1))
+                return fail(ORBG_EIO, "update / reduction launch");
+            if ((rc = chi2(sc)) || (rc = read(hs, 4))) return rc;
+            double tempChi = hs[0];
+            const bool ok2 = *(const int32_t *)&hs[3] != 0;
+            if (!ok2) tempChi = DBL_MAX;
+            rhoLM = currentChi - tempChi;
+            double scale = hs[1];
+            scale += 1e-3;
+            rhoLM /= scale;
+            R.trials++;
+            if (rhoLM > 0 && std::isfinite(tempChi)) {  // the step is good
+                double alpha = 1. - lm_cube_host(2 * rhoLM - 1);
+                alpha = std::min(alpha, 2. / 3.);
+                const double scaleFactor = std::max(1. / 3., alpha);
+                lambda *= scaleFactor;
+                ni = 2;
+                currentChi = tempChi;
+            } else {  // pop
+                lambda *= ni;
+                ni *= 2;
+                if (g->npose)
+                    HIPCHK(hipMemcpyAsync(d_poses, sp, (size_t)g->npose * sizeof(orbg_pose),
+                                          hipMemcpyDeviceToDevice, st));
+                if (g->npoint)
+                    HIPCHK(hipMemcpyAsync(d_points, sq, (size_t)g->npoint * 24,
+                                          hipMemcpyDeviceToDevice, st));
+            }
+            qmax++;
+        } while (rhoLM < 0 && qmax < 10);
+        R.iterations = it + 1;
+        R.final_chi2 = currentChi;
+        R.lambda = lambda;
+        if (qmax == 10 || rhoLM == 0) {
+            R.terminated = 1;
+            break;
+        }
+        if ((iniChi - currentChi) * 1e3 < iniChi)
+            nBad++;
+        else
+            nBad = 0;
+        if (nBad >= 3) {
+            R.terminated = 2;
+            break;
+        }
+    }
+    if (iterations == 0) {
+        if ((rc = chi2(sc)) || (rc = read(hs, 1))) return rc;
+        R.initial_chi2 = R.final_chi2 = hs[0];
+    }
+    HIPCHK(hipStreamSynchronize(st));
+    if (rep) *rep = R;
     return ORBG_OK;
 }
 
@@ -3627,6 +3831,7 @@ static size_t schur_layout(const SchurPlanHost &P, int nedge, uint8_t *base, Sch
     A.blk_i1 = (const int32_t *)take(P.blk_i1.size() * 4);
     A.blk_i2 = (const int32_t *)take(P.blk_i2.size() * 4);
     A.blk_seg = (const int32_t *)take(P.blk_seg.size() * 4);
+    A.blk_order = (const int32_t *)take(P.blk_order.size() * 4);
     A.pose_off = (const int32_t *)take(P.pose_off.size() * 4);
     A.pose_slots = (const int32_t *)take(P.pose_slots.size() * 4);
     A.seg_lo = (const int32_t *)take(P.seg_lo.size() * 4);
@@ -3666,6 +3871,7 @@ static int schur_upload(const SchurPlanHost &P, const SchurArgs &A, hipStream_t 
         (rc = up(A.blk_i1, P.blk_i1.data(), P.blk_i1.size() * 4)) ||
         (rc = up(A.blk_i2, P.blk_i2.data(), P.blk_i2.size() * 4)) ||
         (rc = up(A.blk_seg, P.blk_seg.data(), P.blk_seg.size() * 4)) ||
+        (rc = up(A.blk_order, P.blk_order.data(), P.blk_order.size() * 4)) ||
         (rc = up(A.pose_off, P.pose_off.data(), P.pose_off.size() * 4)) ||
         (rc = up(A.pose_slots, P.pose_slots.data(), P.pose_slots.size() * 4)) ||
         (rc = up(A.seg_lo, P.seg_lo.data(), P.seg_lo.size() * 4)) ||
