@@ -84,6 +84,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(FC2_WPE, 8)
     uint8_t *tA = (uint8_t *)fc2_lds + wv * g->fc2_wave_bytes;
     uint8_t *sc = tA + g->fc2_sc_off;
     uint16_t *list = (uint16_t *)(tA + g->fc2_list_off);
+#if ORBG_FC2_BITMAP
+    // units with a nonzero score, marked by the scoring; 32 units per word, raster order
+    uint32_t *bmap = (uint32_t *)(tA + g->fc2_list_off + 2 * g->fc2_list_cap + 4);
+#endif
     const int total = c_count * nframes;
     // FC2_CPW consecutive cells per wave (neighbours: shared halo lines in L1 / L2)
     const int cid0 =
@@ -196,6 +200,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(FC2_WPE, 8)
             const int r = i / ZR;
             *(uint2 *)(sc + r * SP + 8 * (i - r * ZR)) = make_uint2(0, 0);
         }
+#if ORBG_FC2_BITMAP
+        for (int i = lane; i < (nunits + 31) >> 5; i += 64) bmap[i] = 0u;
+#endif
     }
     wave_sync_lds();
     if (dbg == 11) continue;
@@ -321,6 +328,13 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(FC2_WPE, 8)
         __hip_atomic_fetch_or((uint32_t *)(sc + (ry + 1) * SP + 4 * gg + 4),
                               (s0 | s1 << 8) << (16 * half), __ATOMIC_RELAXED,
                               __HIP_MEMORY_SCOPE_WAVEFRONT);
+#if ORBG_FC2_BITMAP
+        {
+            const int u = ry * RG + gg;  // unconditional: an empty task ORs 0
+            __hip_atomic_fetch_or(bmap + (u >> 5), (s0 | s1) ? 1u << (u & 31) : 0u,
+                                  __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
+        }
+#endif
     }
     wave_sync_lds();
     if (dbg == 12) continue;
@@ -396,6 +410,28 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(FC2_WPE, 8)
     // units with a corner (nonzero score word), raster order, over the dead pretest list
     uint16_t *plist = list;
     int npass = 0;
+#if ORBG_FC2_BITMAP
+    {
+        // the scoring's bitmap, four units per lane: a 3-bit scan, no pass over every unit
+        const int mdiv = (65536 + RG - 1) / max(RG, 1);  // u / RG == (u * mdiv) >> 16, u < 1024
+        for (int b0 = 0; b0 < nunits; b0 += 256) {
+            const int u4 = b0 + 4 * lane;
+            const uint32_t w = u4 < nunits ? bmap[u4 >> 5] : 0u;
+            const uint32_t nib = (w >> (u4 & 31)) & 15u;
+            const int n = __popc(nib);
+            int tot;
+            const int incl = wave_incl_scan_small(n, &tot);
+            int pos = npass + incl - n;
+#pragma unroll
+            for (int k = 0; k < 4; k++)
+                if ((nib >> k) & 1u) {
+                    const int u = u4 + k, ry = (u * mdiv) >> 16, gg = u - ry * RG;
+                    plist[pos++] = (uint16_t)(ry << 8 | gg);
+                }
+            npass += tot;
+        }
+    }
+#else
     for (int u0 = 0, ry = ry0, gg = gg0; u0 < nunits; u0 += 64) {
         const bool in = u0 + lane < nunits;  // the read is unconditional (no exec branch)
         const uint32_t sw = *(const uint32_t *)(sc + (in ? (ry + 1) * SP + 4 * gg + 4 : 0));
@@ -412,6 +448,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(FC2_WPE, 8)
             ry++;
         }
     }
+#endif
     wave_sync_lds();
     for (int j0 = 0; j0 < npass; j0 += 64) {
         const int j = j0 + lane;

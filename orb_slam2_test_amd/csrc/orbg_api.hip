@@ -1100,7 +1100,13 @@ static int plan(orbg_ctx *c, int w, int h, int batch)
                 G.fc2_list_off = G.fc2_sc_off + (std::max(hmax - 6, 0) + 2) * (P2 - 8);  // score rows: P2 - 8 bytes
 #endif
                 G.fc2_list_cap = 2 * max_units;
+#if ORBG_FC2_BITMAP
+                // + k_fast2's spare entry (4 bytes with the alignment), + the corner-unit bitmap
+                G.fc2_wave_bytes = (G.fc2_list_off + 2 * G.fc2_list_cap + 4 +
+                                    4 * ((max_units + 31) / 32) + 15) & ~15;
+#else
                 G.fc2_wave_bytes = (G.fc2_list_off + 2 * G.fc2_list_cap + 2 + 15) & ~15;  // + k_fast2's spare entry
+#endif
 #ifdef ORBG_FC2_MIN_WAVE_BYTES  // developer A/B: LDS per wave padded (caps workgroups per CU)
                 G.fc2_wave_bytes = std::max(G.fc2_wave_bytes, ORBG_FC2_MIN_WAVE_BYTES);
 #endif

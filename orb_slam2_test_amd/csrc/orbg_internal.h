@@ -26,6 +26,9 @@
 #define ORBG_GRID_COLS 64        // Frame.h:38
 #define ORBG_GRID_ROWS 48        // Frame.h:37
 #define ORBG_MATCH_TOPK 8
+#ifndef ORBG_FC2_BITMAP
+#define ORBG_FC2_BITMAP 0  // 1: k_fast2 marks corner units in an LDS bitmap while scoring (no pass over every unit); measured +0.07 ms, profiles/r05o_fast_bitmap_ab.txt
+#endif
 // sticky device error word, bit 16: a device matcher read a per-frame / per-pair count past
 // its capacity (clamped; orbg_check_errors reports it).  Bits 0..9: the quadtree's flags.
 #define ORBG_DEVFLAG_COUNT (1 << 16)
