@@ -435,6 +435,7 @@ __global__ __launch_bounds__(256) void k_init_cands_pairs(
 struct ResolveShared {
     unsigned long long (*chunk)[RESOLVE_CHUNK * ORBG_MATCH_TOPK];
     int (*chunkn)[RESOLVE_CHUNK];
+    int nbuf;  // chunk buffers: 2 (double buffer, wave 1 prefetches) or every chunk (preloaded)
     int *hsize;
     int *nmp;
     float *ang1, *ang2;
@@ -444,21 +445,40 @@ struct ResolveShared {
     int32_t *owner;  // lowest applying lane of a speculative round (64 = none)
 };
 
-#define RESOLVE_FIXED_BYTES (2 * RESOLVE_CHUNK * ORBG_MATCH_TOPK * 8 + 2 * RESOLVE_CHUNK * 4 + 32 * 4 + 16)
+#define RESOLVE_CHUNK_BYTES (RESOLVE_CHUNK * ORBG_MATCH_TOPK * 8 + RESOLVE_CHUNK * 4)
+#define RESOLVE_FIXED_BYTES (32 * 4 + 16)
 
-__host__ __device__ constexpr size_t resolve_lds_bytes(int cap)
+// Every chunk's candidate lists preloaded into LDS up front (all loads in flight at once)
+// when the level-0 capacity is at most RESOLVE_PRELOAD_CAP queries, instead of wave 1's
+// per-chunk prefetch (two dependent global round trips per chunk on the sequential walk's
+// path).  RESOLVE_PRELOAD: 0 never (default: 1 measured a tie at B = 1, 2 +5% on the batch
+// resolver, profiles/r05p_single_ab.txt), 1 the single-pair entry (B = 1), 2 also the batch.
+#ifndef RESOLVE_PRELOAD
+#define RESOLVE_PRELOAD 0
+#endif
+#define RESOLVE_PRELOAD_CAP 1024
+
+__host__ __device__ constexpr int resolve_nbuf(int cap, bool single)
 {
-    return RESOLVE_FIXED_BYTES + (size_t)cap * 8 + (((size_t)cap * 7 + 15) & ~(size_t)15) +
-           (size_t)cap * 4;
+    return (RESOLVE_PRELOAD >= (single ? 1 : 2) && cap <= RESOLVE_PRELOAD_CAP)
+               ? (cap + RESOLVE_CHUNK - 1) / RESOLVE_CHUNK > 2 ? (cap + RESOLVE_CHUNK - 1) / RESOLVE_CHUNK : 2
+               : 2;
 }
 
-__device__ __forceinline__ ResolveShared resolve_layout(uint8_t *base, int cap)
+__host__ __device__ constexpr size_t resolve_lds_bytes(int cap, int nbuf)
+{
+    return (size_t)nbuf * RESOLVE_CHUNK_BYTES + RESOLVE_FIXED_BYTES + (size_t)cap * 8 +
+           (((size_t)cap * 7 + 15) & ~(size_t)15) + (size_t)cap * 4;
+}
+
+__device__ __forceinline__ ResolveShared resolve_layout(uint8_t *base, int cap, int nbuf)
 {
     ResolveShared S;
+    S.nbuf = nbuf;
     S.chunk = (unsigned long long(*)[RESOLVE_CHUNK * ORBG_MATCH_TOPK])base;
-    base += 2 * RESOLVE_CHUNK * ORBG_MATCH_TOPK * 8;
+    base += (size_t)nbuf * RESOLVE_CHUNK * ORBG_MATCH_TOPK * 8;
     S.chunkn = (int(*)[RESOLVE_CHUNK])base;
-    base += 2 * RESOLVE_CHUNK * 4;
+    base += (size_t)nbuf * RESOLVE_CHUNK * 4;
     S.hsize = (int *)base;
     base += 32 * 4;
     S.nmp = (int *)base;
@@ -585,12 +605,14 @@ __device__ void init_resolve_block(ResolveShared &S, int cap, const orbg_keypoin
         }
     };
     // wave 1: load chunk c into buffer c & 1 (lists only when the chunk has a live query)
+    const int nchunks = (n1c + RESOLVE_CHUNK - 1) / RESOLVE_CHUNK;
+    const bool preload = S.nbuf >= nchunks && S.nbuf > 2;
     auto prefetch = [&](int c) {
         const int c0 = c * RESOLVE_CHUNK;
         if (c0 >= n1c) return;
         const int cn = min(RESOLVE_CHUNK, n1c - c0);
         const int t = lane < cn ? topn[c0 + lane] : -1;
-        S.chunkn[c & 1][lane] = t;
+        S.chunkn[c % S.nbuf][lane] = t;
         if (__ballot(t > 0) == 0ull) return;
         unsigned long long e[ORBG_MATCH_TOPK];
 #pragma unroll
@@ -599,14 +621,33 @@ __device__ void init_resolve_block(ResolveShared &S, int cap, const orbg_keypoin
             e[u] = i < cn * ORBG_MATCH_TOPK ? topk[(size_t)c0 * ORBG_MATCH_TOPK + i] : ~0ull;
         }
 #pragma unroll
-        for (int u = 0; u < ORBG_MATCH_TOPK; u++) S.chunk[c & 1][u * 64 + lane] = e[u];
+        for (int u = 0; u < ORBG_MATCH_TOPK; u++) S.chunk[c % S.nbuf][u * 64 + lane] = e[u];
     };
-    if (wv == 1) prefetch(0);
+    if (preload) {
+        // every list at once: both waves, 8 unconditional loads in flight per batch (entries
+        // past a query's count are never read)
+        unsigned long long *flat = &S.chunk[0][0];
+        const int nk = n1c * ORBG_MATCH_TOPK;
+        for (int i0 = 0; i0 < nk; i0 += 8 * RESOLVE_T) {
+            unsigned long long e[8];
+#pragma unroll
+            for (int u = 0; u < 8; u++) {
+                const int i = min(i0 + u * RESOLVE_T + tid, nk - 1);
+                e[u] = topk[i];
+            }
+#pragma unroll
+            for (int u = 0; u < 8; u++)
+                if (i0 + u * RESOLVE_T + tid < nk) flat[i0 + u * RESOLVE_T + tid] = e[u];
+        }
+        int *flatn = &S.chunkn[0][0];
+        for (int i = tid; i < nchunks * RESOLVE_CHUNK; i += RESOLVE_T) flatn[i] = i < n1c ? topn[i] : -1;
+    } else if (wv == 1) {
+        prefetch(0);
+    }
     __syncthreads();
-    const int nchunks = (n1c + RESOLVE_CHUNK - 1) / RESOLVE_CHUNK;
     for (int c = 0; c < nchunks; c++) {
         if (wv == 1) {
-            prefetch(c + 1);
+            if (!preload) prefetch(c + 1);
         } else {
             // Speculative parallel walk, one query per lane (see track_kernels.hip): each
             // pending lane picks best / second from its K-list against the current
@@ -617,8 +658,8 @@ __device__ void init_resolve_block(ResolveShared &S, int cap, const orbg_keypoin
             // keypoints are distinct, so their steals and writes are independent), the rest
             // go again.
             const int c0 = c * RESOLVE_CHUNK, cn = min(RESOLVE_CHUNK, n1c - c0);
-            const int *cnt = S.chunkn[c & 1];
-            const unsigned long long *lists = S.chunk[c & 1];
+            const int *cnt = S.chunkn[c % S.nbuf];
+            const unsigned long long *lists = S.chunk[c % S.nbuf];
             const int total = lane < cn ? cnt[lane] : 0;
             unsigned long long e[ORBG_MATCH_TOPK];
 #pragma unroll
@@ -759,16 +800,17 @@ __device__ void init_resolve_block(ResolveShared &S, int cap, const orbg_keypoin
     if (tid == 0) *nm_out = nmatches;
 }
 
+// prev_out, m12, nm may be host-mapped (the host entry's zero-copy outputs): written once each
 __global__ __launch_bounds__(RESOLVE_T) void k_init_resolve_single(
     const orbg_keypoint *k1, const uint8_t *d1, int n1, const orbg_keypoint *k2,
-    const uint8_t *d2, int n2, orbg_bounds b, float *prev, int window, float nnratio,
-    int check_ori, const unsigned long long *topk, const int32_t *topn, int32_t *m12,
-    int32_t *nm, int cap)
+    const uint8_t *d2, int n2, orbg_bounds b, const float *prev, float *prev_out, int window,
+    float nnratio, int check_ori, const unsigned long long *topk, const int32_t *topn,
+    int32_t *m12, int32_t *nm, int cap)
 {
     extern __shared__ __attribute__((aligned(16))) uint8_t rs_lds[];
-    ResolveShared S = resolve_layout(rs_lds, cap);
+    ResolveShared S = resolve_layout(rs_lds, cap, resolve_nbuf(cap, true));
     init_resolve_block(S, cap, k1, d1, n1, k2, d2, n2, b, prev, 2, window, nnratio, check_ori, topk,
-                       topn, m12, nm, prev);
+                       topn, m12, nm, prev_out);
 }
 
 __global__ __launch_bounds__(RESOLVE_T) void k_init_resolve_pairs(
@@ -778,7 +820,7 @@ __global__ __launch_bounds__(RESOLVE_T) void k_init_resolve_pairs(
     int32_t *nm, int cap)
 {
     extern __shared__ __attribute__((aligned(16))) uint8_t rs_lds[];
-    ResolveShared S = resolve_layout(rs_lds, cap);
+    ResolveShared S = resolve_layout(rs_lds, cap, resolve_nbuf(cap, false));
     const int p = blockIdx.x;
     const int a = f1[p], c = f2[p];
     const orbg_keypoint *k1 = kps + (size_t)a * fc;
@@ -858,9 +900,22 @@ int launch_match_pairs(hipStream_t st, hipStream_t aux, hipEvent_t evf, hipEvent
                           dim3((fc + 255) / 256 * npairs), dim3(256), 0, aux, desc, counts, fc,
                           d_f1, d_f2, knn));
     if (hipEventRecord(evj, aux) != hipSuccess) return ORBG_EIO;
+    if (resolve_lds_bytes(cap0, resolve_nbuf(cap0, false)) > 65536) {
+        static bool pattr = false;  // a preloaded batch resolver past 64 KB of dynamic LDS
+        if (!pattr) {
+            if (hipFuncSetAttribute((const void *)k_init_resolve_pairs,
+                                    hipFuncAttributeMaxDynamicSharedMemorySize,
+                                    (int)resolve_lds_bytes(RESOLVE_PRELOAD_CAP,
+                                                           resolve_nbuf(RESOLVE_PRELOAD_CAP, false))) !=
+                hipSuccess)
+                return ORBG_EIO;
+            pattr = true;
+        }
+    }
     PL(prof, st, "init_resolve",
        hipLaunchKernelGGL(k_init_resolve_pairs, dim3(npairs), dim3(RESOLVE_T),
-                          resolve_lds_bytes(cap0), st, kps, desc, counts, fc, d_f1, d_f2, b,
+                          resolve_lds_bytes(cap0, resolve_nbuf(cap0, false)), st, kps, desc,
+                          counts, fc, d_f1, d_f2, b,
                           window, nnratio, check_ori, (const unsigned long long *)topk, topk_n,
                           m12, nm, cap0));
     if (hipStreamWaitEvent(st, evj, 0) != hipSuccess) return ORBG_EIO;
@@ -872,7 +927,8 @@ int launch_match_pairs(hipStream_t st, hipStream_t aux, hipEvent_t evf, hipEvent
 // max(n1, n2)); queries past it get no candidates and vnMatches12 = -1
 int launch_init_match_single(hipStream_t st, const orbg_keypoint *k1, const uint8_t *d1, int n1,
                              const orbg_keypoint *k2, const uint8_t *d2, int n2, orbg_bounds b,
-                             float *prev, int32_t *m12, int32_t *nm, int window, float nnratio,
+                             const float *prev, float *prev_out, int32_t *m12, int32_t *nm,
+                             int window, float nnratio,
                              int check_ori, uint32_t *topk, int32_t *topk_n, void *prof, int cap)
 {
     const int nq = std::min(n1, cap), n2c = std::min(n2, cap);  // indices below cap
@@ -881,7 +937,10 @@ int launch_init_match_single(hipStream_t st, const orbg_keypoint *k1, const uint
     if (!attr) {
         if (hipFuncSetAttribute((const void *)k_init_resolve_single,
                                 hipFuncAttributeMaxDynamicSharedMemorySize,
-                                (int)resolve_lds_bytes(RESOLVE_N2_CAP)) != hipSuccess)
+                                (int)std::max(resolve_lds_bytes(RESOLVE_N2_CAP, 2),
+                                              resolve_lds_bytes(RESOLVE_PRELOAD_CAP,
+                                                                resolve_nbuf(RESOLVE_PRELOAD_CAP, true)))) !=
+                hipSuccess)
             return ORBG_EIO;
         attr = true;
     }
@@ -891,7 +950,8 @@ int launch_init_match_single(hipStream_t st, const orbg_keypoint *k1, const uint
                           d2, n2c, b, prev, window, (unsigned long long *)topk, topk_n));
     PL(prof, st, "init_resolve",
        hipLaunchKernelGGL(k_init_resolve_single, dim3(1), dim3(RESOLVE_T),
-                          resolve_lds_bytes(cap), st, k1, d1, n1, k2, d2, n2, b, prev, window,
+                          resolve_lds_bytes(cap, resolve_nbuf(cap, true)), st, k1, d1, n1, k2, d2,
+                          n2, b, prev, prev_out, window,
                           nnratio, check_ori, (const unsigned long long *)topk, topk_n, m12, nm,
                           cap));
     return hipGetLastError() == hipSuccess ? ORBG_OK : ORBG_EIO;

@@ -29,8 +29,12 @@ namespace orbg {
 #define OCT_T 512
 #define OCT_CODE_DEPTH 14
 
-#ifndef OCT_PC
-#define OCT_PC 4  // cells per wave with their candidate loads in flight (per_cell)
+// OCT_PC: cells per wave with their candidate loads in flight (per_cell).  Batches take 4
+// (registers: several workgroups per CU); small batches (the single-frame drop-in: one
+// workgroup per level on an idle chip, the candidate walks are chains of L2 round trips)
+// OCT_PC_SMALL.
+#ifndef OCT_PC_SMALL
+#define OCT_PC_SMALL 16
 #endif
 
 #define OCT_NBUCKET 16384  // counting-sort buckets: root (4 bits) + first 5 quadtree digits
@@ -123,6 +127,49 @@ __device__ void flip_bitonic_u64(unsigned long long *v, int n)
     }
 }
 
+// In-place ascending sort of n distinct u64 keys by rank counting: each thread holds up to
+// OCT_RANK_R keys in registers, counts the smaller keys (LDS broadcast reads: every lane reads
+// the same v[j]), then after one barrier writes each key at its rank.  Two barriers against
+// flip_bitonic_u64's log2(n) (log2(n) + 1) / 2 -- the phase-2 sort is a chain of barriers of a
+// single workgroup, the B = 1 critical path.  n <= OCT_RANK_R * OCT_T.
+#define OCT_RANK_R 4
+__device__ void rank_sort_u64(unsigned long long *v, int n)
+{
+    const int tid = threadIdx.x;
+    if (n <= OCT_T) {
+        const unsigned long long x = tid < n ? v[tid] : 0ull;
+        int c = 0;
+#pragma unroll 8
+        for (int j = 0; j < n; j++) c += v[j] < x;
+        __syncthreads();
+        if (tid < n) v[c] = x;
+    } else {
+        unsigned long long x[OCT_RANK_R];
+        int c[OCT_RANK_R];
+#pragma unroll
+        for (int k = 0; k < OCT_RANK_R; k++) {
+            const int i = tid + k * OCT_T;
+            x[k] = i < n ? v[i] : ~0ull;
+            c[k] = 0;
+        }
+#pragma unroll 4
+        for (int j = 0; j < n; j++) {
+            const unsigned long long y = v[j];
+#pragma unroll
+            for (int k = 0; k < OCT_RANK_R; k++) c[k] += y < x[k];
+        }
+        __syncthreads();
+#pragma unroll
+        for (int k = 0; k < OCT_RANK_R; k++)
+            if (tid + k * OCT_T < n) v[c[k]] = x[k];
+    }
+    __syncthreads();
+}
+
+#ifndef ORBG_OCT_RANK
+#define ORBG_OCT_RANK 1  // phase-2 sort: 1 rank counting, 0 flip bitonic
+#endif
+
 // Candidates sit in counting-sort bucket order (root + first OCT_BDEPTH digits), unordered
 // inside a bucket.  A node shallower than OCT_BDEPTH is a run of whole buckets, so its next
 // digit is already monotone; a node of depth OCT_BDEPTH is exactly one bucket and is put in
@@ -170,10 +217,27 @@ __device__ __forceinline__ void oct_children(uint32_t *codes, uint16_t *sidx,
     }
 }
 
+// phase 2: a processed parent's split points as the cut pass left them in its sort entry
+// (pos << 48 | b3 << 32 | b2 << 16 | b1); returns the parent's record
+__device__ __forceinline__ unsigned long long oct_split_points(const OctLdsView &V, int cur,
+                                                               unsigned long long w, int b[5],
+                                                               int &pos)
+{
+    pos = (int)(w >> 48);
+    const unsigned long long r = V.list(cur)[pos];
+    b[0] = rec_lo(r);
+    b[1] = (int)(w & 0xFFFF);
+    b[2] = (int)((w >> 16) & 0xFFFF);
+    b[3] = (int)((w >> 32) & 0xFFFF);
+    b[4] = rec_lo(r) + rec_cnt(r);
+    return r;
+}
+
 // frame = blockIdx.x, level = level0 + blockIdx.y (the dispatcher walks x fastest, so every
 // frame's largest level starts first and the small levels fill the tail); handles a level iff
 // its candidate count
 // n <= D.kcap (k_octree takes the rest, same threshold)
+template <int OCT_PC>
 __global__ __launch_bounds__(OCT_T) void k_octree_lds(
     const OrbgGeom *__restrict__ g, const int32_t *__restrict__ cell_cnt,
     const uint2 *__restrict__ cell_kp, uint32_t *__restrict__ lvl_kp,
@@ -445,7 +509,10 @@ __global__ __launch_bounds__(OCT_T) void k_octree_lds(
             }
             for (int i = tid; i < alive; i += OCT_T) V.aux[i] = 0;
             __syncthreads();
-            flip_bitonic_u64(V.sortv, np);
+            if (ORBG_OCT_RANK && np <= OCT_RANK_R * OCT_T)
+                rank_sort_u64(V.sortv, np);
+            else
+                flip_bitonic_u64(V.sortv, np);
             // processing order p = largest (cnt, seq) first (:872); cut at the first p with
             // alive + sum_{p' <= p} (children - 1) >= N (:917-918)
             if (tid == 0) S.s_nproc = np;
@@ -465,6 +532,11 @@ __global__ __launch_bounds__(OCT_T) void k_octree_lds(
 #pragma unroll
                         for (int q = 0; q < 4; q++) e += b[q + 1] > b[q];
                         dl = e - 1;
+                        // the sort key is dead: keep the split points for the two passes below
+                        // (this thread's own entry; b[0], b[4] are the record's range)
+                        V.sortv[np - 1 - p] = (unsigned long long)pos << 48 |
+                                              (unsigned long long)b[3] << 32 |
+                                              (unsigned long long)b[2] << 16 | (unsigned)b[1];
                     }
                     int tot;
                     const int incl = oct_scan(dl, &tot, S.red) + run + dl;
@@ -480,9 +552,8 @@ __global__ __launch_bounds__(OCT_T) void k_octree_lds(
                 const int p = p0 + tid;
                 int e = 0;
                 if (p < nproc) {
-                    const int pos = (int)(V.sortv[np - 1 - p] & 0xFFFF);
-                    int b[5];
-                    oct_children(V.codes, V.sidx, V.list(cur)[pos], b);
+                    int b[5], pos;
+                    oct_split_points(V, cur, V.sortv[np - 1 - p], b, pos);
 #pragma unroll
                     for (int q = 0; q < 4; q++) e += b[q + 1] > b[q];
                     V.aux[pos] = 1;  // processed parent
@@ -498,9 +569,8 @@ __global__ __launch_bounds__(OCT_T) void k_octree_lds(
                     int e = 0, b[5] = {0, 0, 0, 0, 0};
                     unsigned long long r = 0;
                     if (p < nproc) {
-                        const int pos = (int)(V.sortv[np - 1 - p] & 0xFFFF);
-                        r = V.list(cur)[pos];
-                        oct_children(V.codes, V.sidx, r, b);
+                        int pos;
+                        r = oct_split_points(V, cur, V.sortv[np - 1 - p], b, pos);
 #pragma unroll
                         for (int q = 0; q < 4; q++) e += b[q + 1] > b[q];
                     }
@@ -640,6 +710,29 @@ __global__ __launch_bounds__(OCT_T) void k_octree_lds(
             atomicMin(err_flag + 1, f);
         }
     }
+}
+
+// small: B <= ORBG_SIDE_BLUR_B (OCT_PC_SMALL cells in flight per wave), else 4
+hipError_t launch_octree_lds(bool small, dim3 grid, size_t lds, hipStream_t st, const OrbgGeom *g,
+                             const int32_t *cell_cnt, const uint2 *cell_kp, uint32_t *lvl_kp,
+                             uint16_t *lvl_idx, int32_t *lvl_cnt, int32_t *err_flag, OctLdsDims D)
+{
+    if (small)
+        hipLaunchKernelGGL(k_octree_lds<OCT_PC_SMALL>, grid, dim3(OCT_T), lds, st, g, cell_cnt,
+                           cell_kp, lvl_kp, lvl_idx, lvl_cnt, err_flag, D);
+    else
+        hipLaunchKernelGGL(k_octree_lds<4>, grid, dim3(OCT_T), lds, st, g, cell_cnt, cell_kp,
+                           lvl_kp, lvl_idx, lvl_cnt, err_flag, D);
+    return hipGetLastError();
+}
+
+hipError_t octree_lds_attr(int bytes)
+{
+    for (const void *k : {(const void *)k_octree_lds<4>, (const void *)k_octree_lds<OCT_PC_SMALL>}) {
+        const hipError_t e = hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, bytes);
+        if (e != hipSuccess) return e;
+    }
+    return hipSuccess;
 }
 
 }  // namespace orbg

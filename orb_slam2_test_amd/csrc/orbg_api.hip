@@ -35,8 +35,10 @@ __global__ void k_resize(const uint8_t *, int64_t, int, int, uint8_t *, int64_t,
 __global__ void k_octree(const OrbgGeom *, const int32_t *, const uint2 *, uint32_t *,
                          uint32_t *, uint32_t *, uint8_t *, int4 *, uint32_t *, uint16_t *,
                          int32_t *, int32_t *);
-__global__ void k_octree_lds(const OrbgGeom *, const int32_t *, const uint2 *, uint32_t *,
-                             uint16_t *, int32_t *, int32_t *, OctLdsDims);
+hipError_t launch_octree_lds(bool small, dim3 grid, size_t lds, hipStream_t st, const OrbgGeom *g,
+                             const int32_t *cell_cnt, const uint2 *cell_kp, uint32_t *lvl_kp,
+                             uint16_t *lvl_idx, int32_t *lvl_cnt, int32_t *err_flag, OctLdsDims D);
+hipError_t octree_lds_attr(int bytes);
 // fast_kernels.hip
 bool fast2_pitch_ok(int p4);
 __global__ void k_pyramid(PyrArgs, const OrbgGeom *, const uint4 *, const int4 *, const int4 *,
@@ -129,9 +131,9 @@ int launch_knn2(hipStream_t st, const uint8_t *q, int nq, const uint8_t *t, int 
                 void *prof);
 int launch_init_match_single(hipStream_t st, const orbg_keypoint *k1, const uint8_t *d1, int n1,
                              const orbg_keypoint *k2, const uint8_t *d2, int n2,
-                             orbg_bounds b, float *prev, int32_t *m12, int32_t *nm, int window,
-                             float nnratio, int check_ori, uint32_t *topk, int32_t *topk_n,
-                             void *prof, int cap);
+                             orbg_bounds b, const float *prev, float *prev_out, int32_t *m12,
+                             int32_t *nm, int window, float nnratio, int check_ori, uint32_t *topk,
+                             int32_t *topk_n, void *prof, int cap);
 // bow_match_kernels.hip
 int launch_bow_match(hipStream_t st, const orbg_bow_frames &kf, const orbg_bow_frames &f, int cap,
                      const int32_t *kf_index, const int32_t *f_index, int npairs, float nnratio,
@@ -314,6 +316,15 @@ struct orbg_ctx {
     hipEvent_t ev_f0[2] = {nullptr, nullptr}, ev_b0[2] = {nullptr, nullptr},
                ev_pfork[2] = {nullptr, nullptr}, ev_pyr[2] = {nullptr, nullptr};
     bool blur_side = false;  // ORBG_BLUR_SIDE
+    // non-pipelined batches (the single-frame drop-in): k_octree, the fallback quadtree for
+    // levels past k_octree_lds' capacity, on `fstream` beside the k_octree_lds launches once
+    // every level's FAST cells are written (ev_big_a: level 0 on the quadtree stream, ev_big_b:
+    // levels 1.. on the extraction stream), joined before k_orient_desc (ev_big); it only scans
+    // the cell counts unless a level overflows.  ORBG_BIG_SIDE=1 (off by default: the single
+    // frame measured 0.26 -> 0.32-0.36 ms, the level-1.. FAST launch 15 -> 51 us behind the
+    // extra stream's waits, profiles/r05q_single_ab.txt)
+    bool big_side = false;
+    hipEvent_t ev_big_a = nullptr, ev_big_b = nullptr, ev_big = nullptr;
     bool serial = false;     // orbg_set_serial: no stream overlap (isolated kernel timing)
     // orbg_extract's single-frame hipGraphs: the whole frame (H2D of the pinned input, the
     // extraction's launches on the context and quadtree streams, k_pack_frame, D2H of the
@@ -403,6 +414,14 @@ struct orbg_ctx {
     size_t img_bytes = 0;
     uint8_t *d_pack = nullptr;  // orbg_download_frame: error word, count, kps, desc
     size_t pack_bytes = 0;
+    // zero-copy host block (coherent pinned, device-mapped; ORBG_ZC, default 1): k_pack_frame
+    // stores orbg_download_frame's packed outputs straight into it, and the
+    // SearchForInitialization host entry's inputs are read from it by one copy kernel and its
+    // outputs written into it by the resolver -- kernels instead of DMA submissions, whose
+    // start latency (6-9 us each) the single-frame path otherwise waits for
+    uint8_t *h_zc = nullptr, *h_zc_dev = nullptr;
+    size_t zc_bytes = 0;
+    int zc_mode = -1;  // -1: read ORBG_ZC on first use
     uint8_t *d_pyr = nullptr, *d_blur = nullptr;  // = pyr_slot[slot], blur_slot[slot]
     int32_t *d_cell_cnt = nullptr;                 // = cnt_slot[slot]
     uint2 *d_cell_kp = nullptr;                    // = ckp_slot[slot]
@@ -651,6 +670,46 @@ static int stage(orbg_ctx *c, size_t bytes, uint8_t **out)
     }
     *out = c->h_stage;
     return ORBG_OK;
+}
+
+static bool use_zc(orbg_ctx *c)
+{
+    if (c->zc_mode < 0) {
+        const char *e = getenv("ORBG_ZC");
+        c->zc_mode = e ? atoi(e) != 0 : 1;
+    }
+    return c->zc_mode != 0;
+}
+
+// the zero-copy block (host pointer, device pointer), grown to `bytes`; the caller has drained
+// every kernel that touched it (each user ends with sync_all / a stream synchronize).  The
+// image upload stays a DMA: a k_copy16 pull of the image measured no faster (14.5 against
+// 16.4 us, the frame a tie; profiles/r05r_single_ab.txt)
+static int zc_buf(orbg_ctx *c, size_t bytes, uint8_t **h, uint8_t **d)
+{
+    if (c->zc_bytes < bytes) {
+        HIPCHK(hipStreamSynchronize(c->stream));
+        if (c->h_zc) hipHostFree(c->h_zc);
+        c->h_zc = c->h_zc_dev = nullptr;
+        c->zc_bytes = 0;
+        const size_t nb = std::max(bytes, (size_t)1 << 20);
+        if (hipHostMalloc((void **)&c->h_zc, nb, hipHostMallocCoherent) != hipSuccess)
+            return set_err(ORBG_ENOMEM, "hipHostMalloc(%zu bytes, coherent)", nb);
+        if (hipHostGetDevicePointer((void **)&c->h_zc_dev, c->h_zc, 0) != hipSuccess)
+            return set_err(ORBG_EIO, "hipHostGetDevicePointer");
+        c->zc_bytes = nb;
+    }
+    *h = c->h_zc;
+    *d = c->h_zc_dev;
+    return ORBG_OK;
+}
+
+// n16 16-byte words src -> dst (a host-mapped source: one PCIe read per word)
+__global__ void k_copy16(const uint4 *__restrict__ src, uint4 *__restrict__ dst, size_t n16)
+{
+    for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n16;
+         i += (size_t)gridDim.x * blockDim.x)
+        dst[i] = src[i];
 }
 
 // k_pyramid tables (pyramid_args.h) from the cv::resize coefficient tables of every level.
@@ -1165,9 +1224,7 @@ static int plan(orbg_ctx *c, int w, int h, int batch)
             const size_t b = oct_lds_bytes(c->oct_dims[k]);
             if (b + sizeof(OctLdsHdr) > 160 * 1024)
                 return set_err(ORBG_ENOTSUP, "k_octree_lds needs %zu LDS bytes", b);
-            if (b > 64 * 1024)
-                HIPCHK(hipFuncSetAttribute((const void *)k_octree_lds,
-                                           hipFuncAttributeMaxDynamicSharedMemorySize, (int)b));
+            if (b > 64 * 1024) HIPCHK(octree_lds_attr((int)b));
         }
     }
     G.keys_frame = key_off;
@@ -1387,6 +1444,11 @@ extern "C" int orbg_create(int device, const orbg_params *p, orbg_ctx **out)
         }
         const char *bs = getenv("ORBG_BLUR_SIDE");
         c->blur_side = bs ? atoi(bs) != 0 : false;
+        const char *bg = getenv("ORBG_BIG_SIDE");
+        c->big_side = c->fstream && (bg ? atoi(bg) != 0 : false);
+        if (c->big_side)
+            for (hipEvent_t *e : {&c->ev_big_a, &c->ev_big_b, &c->ev_big})
+                if (hipEventCreateWithFlags(e, hipEventDisableTiming) != hipSuccess) c->big_side = false;
     }
     if (hipStreamCreateWithPriority(&c->mstream, hipStreamNonBlocking, mprio) != hipSuccess) {
         hipStreamDestroy(c->aux_stream);
@@ -1444,6 +1506,7 @@ extern "C" void orbg_destroy(orbg_ctx *c)
     free_plan(c);
     if (c->d_img) hipFree(c->d_img);
     if (c->d_pack) hipFree(c->d_pack);
+    if (c->h_zc) hipHostFree(c->h_zc);
     if (c->d_scr) hipFree(c->d_scr);
     if (c->d_trk) hipFree(c->d_trk);
     if (c->d_sim3) hipFree(c->d_sim3);
@@ -1468,6 +1531,8 @@ extern "C" void orbg_destroy(orbg_ctx *c)
         for (hipEvent_t e : {c->ev_f0[i], c->ev_b0[i], c->ev_pfork[i], c->ev_pyr[i]})
             if (e) hipEventDestroy(e);
     if (c->fstream) hipStreamDestroy(c->fstream);
+    for (hipEvent_t e : {c->ev_big_a, c->ev_big_b, c->ev_big})
+        if (e) hipEventDestroy(e);
     if (c->ev_fast) hipEventDestroy(c->ev_fast);
     if (c->ev_oct) hipEventDestroy(c->ev_oct);
     for (hipEvent_t e : {c->ev_sback, c->ev_ssum, c->ev_rel[0], c->ev_rel[1], c->ev_srel,
@@ -1638,14 +1703,14 @@ static int launch_extract_pipe(orbg_ctx *c, const uint8_t *d_imgs, int B, int pi
     hipStream_t st = c->ostream;  // the back (PROF_LAUNCH records on `st`)
     HIPCHK(hipStreamWaitEvent(st, c->ev_cells[s], 0));
     PROF_LAUNCH(c, "octree",
-                hipLaunchKernelGGL(k_octree_lds, dim3(B, 1), dim3(512),
-                                   oct_lds_bytes(c->oct_dims[0]), st, c->d_geom, c->d_cell_cnt,
+                launch_octree_lds(B <= ORBG_SIDE_BLUR_B, dim3(B, 1),
+                                      oct_lds_bytes(c->oct_dims[0]), st, c->d_geom, c->d_cell_cnt,
                                    c->d_cell_kp, c->d_lvl_kp, c->d_lvl_idx, c->d_lvl_cnt,
                                    c->d_err, c->oct_dims[0]));
     if (G.L > 1)
         PROF_LAUNCH(c, "octree",
-                    hipLaunchKernelGGL(k_octree_lds, dim3(B, G.L - 1), dim3(512),
-                                       oct_lds_bytes(c->oct_dims[1]), st, c->d_geom,
+                    launch_octree_lds(B <= ORBG_SIDE_BLUR_B, dim3(B, G.L - 1),
+                                      oct_lds_bytes(c->oct_dims[1]), st, c->d_geom,
                                        c->d_cell_cnt, c->d_cell_kp,
                                        c->d_lvl_kp, c->d_lvl_idx, c->d_lvl_cnt, c->d_err, c->oct_dims[1]));
     PROF_LAUNCH(c, "octree_big",
@@ -1725,15 +1790,30 @@ static int launch_extract(orbg_ctx *c, const uint8_t *d_imgs, int B, int pitch, 
     auto launch_fast = [&](hipStream_t q, int cb, int cn) {
         return launch_fast_cells(c, q, d_imgs, B, pitch, fs, cb, cn);
     };
+    // big_side: k_octree beside the quadtree launches (needs fast0's two FAST launches)
+    const bool big_side = fast0 && c->big_side;
     if (fast0) {
         HIPCHK(hipEventRecord(c->ev_fast, st));
         HIPCHK(hipStreamWaitEvent(c->ostream, c->ev_fast, 0));
         HIPCHK(launch_fast(c->ostream, 0, n0));
+        if (big_side) HIPCHK(hipEventRecord(c->ev_big_a, c->ostream));
     }
     HIPCHK(launch_pyramid(c, st, d_imgs, B, pitch, fs));
     if (blur_side) HIPCHK(hipEventRecord(c->ev_fast, st));  // pyramid written: the side blur
     if (fast0) {
         HIPCHK(launch_fast(st, n0, G.ncells - n0));
+        if (big_side) {
+            HIPCHK(hipEventRecord(c->ev_big_b, st));
+            HIPCHK(hipStreamWaitEvent(c->fstream, c->ev_big_a, 0));
+            HIPCHK(hipStreamWaitEvent(c->fstream, c->ev_big_b, 0));
+            hipStream_t st = c->fstream;  // PROF_LAUNCH records on `st`
+            PROF_LAUNCH(c, "octree_big",
+                        hipLaunchKernelGGL(k_octree, dim3(G.L, B), dim3(ORBG_OCT_THREADS), 0, st,
+                                           c->d_geom, c->d_cell_cnt, c->d_cell_kp, c->d_keys,
+                                           c->d_knode, c->d_act, c->d_qk, c->d_nodes, c->d_lvl_kp,
+                                           c->d_lvl_idx, c->d_lvl_cnt, c->d_err));
+            HIPCHK(hipEventRecord(c->ev_big, st));
+        }
     } else {
         HIPCHK(launch_fast(st, 0, G.ncells));
         if (oct_mode) {
@@ -1745,8 +1825,8 @@ static int launch_extract(orbg_ctx *c, const uint8_t *d_imgs, int B, int pitch, 
         // PROF_LAUNCH records on `st`
         hipStream_t st = oct_mode ? c->ostream : c->stream;
         PROF_LAUNCH(c, "octree",
-                    hipLaunchKernelGGL(k_octree_lds, dim3(B, 1), dim3(512),
-                                       oct_lds_bytes(c->oct_dims[0]), st, c->d_geom,
+                    launch_octree_lds(B <= ORBG_SIDE_BLUR_B, dim3(B, 1),
+                                      oct_lds_bytes(c->oct_dims[0]), st, c->d_geom,
                                        c->d_cell_cnt, c->d_cell_kp,
                                        c->d_lvl_kp, c->d_lvl_idx, c->d_lvl_cnt, c->d_err, c->oct_dims[0]));
         if (oct_mode == 2 && G.L > 1) {
@@ -1756,8 +1836,8 @@ static int launch_extract(orbg_ctx *c, const uint8_t *d_imgs, int B, int pitch, 
                 HIPCHK(hipStreamWaitEvent(st, c->ev_fast, 0));
             }
             PROF_LAUNCH(c, "octree",
-                        hipLaunchKernelGGL(k_octree_lds, dim3(B, G.L - 1), dim3(512),
-                                           oct_lds_bytes(c->oct_dims[1]), st, c->d_geom,
+                        launch_octree_lds(B <= ORBG_SIDE_BLUR_B, dim3(B, G.L - 1),
+                                      oct_lds_bytes(c->oct_dims[1]), st, c->d_geom,
                                            c->d_cell_cnt, c->d_cell_kp,
                                            c->d_lvl_kp, c->d_lvl_idx, c->d_lvl_cnt, c->d_err, c->oct_dims[1]));
         }
@@ -1773,16 +1853,19 @@ static int launch_extract(orbg_ctx *c, const uint8_t *d_imgs, int B, int pitch, 
     else if (fz == 2 && !blur0) HIPCHK(launch_blur_levels(c, st, d_imgs, B, pitch, fs, 0, 1));
     if (oct_mode != 2 && G.L > 1)
         PROF_LAUNCH(c, "octree",
-                    hipLaunchKernelGGL(k_octree_lds, dim3(B, G.L - 1), dim3(512),
-                                       oct_lds_bytes(c->oct_dims[1]), st, c->d_geom,
+                    launch_octree_lds(B <= ORBG_SIDE_BLUR_B, dim3(B, G.L - 1),
+                                      oct_lds_bytes(c->oct_dims[1]), st, c->d_geom,
                                        c->d_cell_cnt, c->d_cell_kp,
                                        c->d_lvl_kp, c->d_lvl_idx, c->d_lvl_cnt, c->d_err, c->oct_dims[1]));
     if (oct_mode) HIPCHK(hipStreamWaitEvent(st, c->ev_oct, 0));
-    PROF_LAUNCH(c, "octree_big",
-                hipLaunchKernelGGL(k_octree, dim3(G.L, B), dim3(ORBG_OCT_THREADS), 0, st,
-                                   c->d_geom, c->d_cell_cnt, c->d_cell_kp, c->d_keys, c->d_knode,
-                                   c->d_act, c->d_qk, c->d_nodes, c->d_lvl_kp, c->d_lvl_idx, c->d_lvl_cnt,
-                                   c->d_err));
+    if (big_side)
+        HIPCHK(hipStreamWaitEvent(st, c->ev_big, 0));
+    else
+        PROF_LAUNCH(c, "octree_big",
+                    hipLaunchKernelGGL(k_octree, dim3(G.L, B), dim3(ORBG_OCT_THREADS), 0, st,
+                                       c->d_geom, c->d_cell_cnt, c->d_cell_kp, c->d_keys, c->d_knode,
+                                       c->d_act, c->d_qk, c->d_nodes, c->d_lvl_kp, c->d_lvl_idx,
+                                       c->d_lvl_cnt, c->d_err));
     // per-frame outputs go to the other slot; wait until its last reader (matching of the
     // batch before last) is done
     if (c->mat_pending[s]) {
@@ -1914,23 +1997,28 @@ extern "C" int orbg_download_frame(orbg_ctx *c, int frame, orbg_keypoint *kps, u
     const size_t okp = 256, ods = okp + ((fc * sizeof(orbg_keypoint) + 255) & ~(size_t)255);
     const size_t bytes = ods + fc * 32;
     int rc;
-    if (c->pack_bytes < bytes) {
-        if ((rc = sync_all(c))) return rc;
-        if (c->d_pack) hipFree(c->d_pack);
-        c->d_pack = nullptr;
-        c->pack_bytes = 0;
-        if ((rc = dalloc(&c->d_pack, bytes))) return rc;
-        c->pack_bytes = bytes;
+    uint8_t *hs, *dst;
+    if (use_zc(c)) {
+        if ((rc = zc_buf(c, bytes, &hs, &dst))) return rc;
+    } else {
+        if (c->pack_bytes < bytes) {
+            if ((rc = sync_all(c))) return rc;
+            if (c->d_pack) hipFree(c->d_pack);
+            c->d_pack = nullptr;
+            c->pack_bytes = 0;
+            if ((rc = dalloc(&c->d_pack, bytes))) return rc;
+            c->pack_bytes = bytes;
+        }
+        if ((rc = stage(c, bytes, &hs))) return rc;
+        dst = c->d_pack;
     }
-    uint8_t *hs;
-    if ((rc = stage(c, bytes, &hs))) return rc;
     hipStream_t st = back_stream(c);
     const size_t words = std::max(fc * (sizeof(orbg_keypoint) / 4), fc * 8);
     hipLaunchKernelGGL(k_pack_frame, dim3((unsigned)((words + 255) / 256)), dim3(256), 0, st,
                        c->d_err, c->d_counts, (const uint32_t *)c->d_kps,
-                       (const uint32_t *)c->d_desc, frame, fc, okp, ods, (uint32_t *)c->d_pack);
+                       (const uint32_t *)c->d_desc, frame, fc, okp, ods, (uint32_t *)dst);
     HIPCHK(hipGetLastError());
-    HIPCHK(hipMemcpyAsync(hs, c->d_pack, bytes, hipMemcpyDeviceToHost, st));
+    if (!use_zc(c)) HIPCHK(hipMemcpyAsync(hs, c->d_pack, bytes, hipMemcpyDeviceToHost, st));
     if ((rc = sync_all(c))) return rc;
     c->prof.collect();
     int32_t hdr[3];
@@ -2801,10 +2889,13 @@ extern "C" int orbg_search_for_initialization(orbg_ctx *c, const orbg_keypoint *
     int rc = scratch(c, o, &s);
     if (rc) return rc;
     uint8_t *b = (uint8_t *)s;
-    // inputs packed into pinned staging with the device layout, one DMA each way
-    uint8_t *hs;
-    if ((rc = stage(c, otk, &hs))) return rc;
-    HIPCHK(hipStreamSynchronize(c->stream));  // the staging buffer's previous DMA is done
+    // inputs packed into pinned staging with the device layout, one DMA each way; zero-copy:
+    // the staging is the coherent host block, uploaded by k_copy16, and the resolver writes
+    // vnMatches12, the count and vbPrevMatched straight back into it
+    const bool zc = use_zc(c);
+    uint8_t *hs, *hd = nullptr;
+    if ((rc = zc ? zc_buf(c, otk, &hs, &hd) : stage(c, otk, &hs))) return rc;
+    HIPCHK(hipStreamSynchronize(c->stream));  // the staging buffer's previous user is done
     std::memcpy(hs + ok1, kps1, l1 * sizeof(orbg_keypoint));
     std::memcpy(hs + od1, desc1, l1 * 32);
     if (n2) {
@@ -2813,15 +2904,24 @@ extern "C" int orbg_search_for_initialization(orbg_ctx *c, const orbg_keypoint *
         std::memcpy(hs + od2, desc2, c2 * 32);
     }
     std::memcpy(hs + opv, prev_xy, l1 * 8);
-    HIPCHK(hipMemcpyAsync(b, hs, om, hipMemcpyHostToDevice, c->stream));
+    if (zc) {
+        const size_t n16 = om / 16;  // om: a multiple of 256
+        hipLaunchKernelGGL(k_copy16, dim3((unsigned)std::min<size_t>((n16 + 255) / 256, 256)),
+                           dim3(256), 0, c->stream, (const uint4 *)hd, (uint4 *)b, n16);
+        HIPCHK(hipGetLastError());
+    } else {
+        HIPCHK(hipMemcpyAsync(b, hs, om, hipMemcpyHostToDevice, c->stream));
+    }
+    // outputs: device copies behind one D2H, or the host block itself (zc)
+    uint8_t *ob = zc ? hd : b;
     rc = launch_init_match_single(c->stream, (const orbg_keypoint *)(b + ok1), b + od1, n1,
                                   (const orbg_keypoint *)(b + ok2), b + od2, n2, *bounds2,
-                                  (float *)(b + opv), (int32_t *)(b + om),
-                                  (int32_t *)(b + om + m1 * 4), window, nnratio, check_ori,
+                                  (const float *)(b + opv), (float *)(ob + opv), (int32_t *)(ob + om),
+                                  (int32_t *)(ob + om + m1 * 4), window, nnratio, check_ori,
                                   (uint32_t *)(b + otk), (int32_t *)(b + otn), &c->prof, last0);
     if (rc) return rc;
     int32_t nm = 0;
-    HIPCHK(hipMemcpyAsync(hs + opv, b + opv, otk - opv, hipMemcpyDeviceToHost, c->stream));
+    if (!zc) HIPCHK(hipMemcpyAsync(hs + opv, b + opv, otk - opv, hipMemcpyDeviceToHost, c->stream));
     HIPCHK(hipStreamSynchronize(c->stream));
     std::memcpy(matches12, hs + om, m1 * 4);
     std::memcpy(&nm, hs + om + m1 * 4, 4);
