@@ -19,7 +19,9 @@
 //                              clear every match with SAD >= 1.5f * 1.4f * median
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <climits>
+#include <cstdlib>
 
 #include "../../include/orbg.h"
 #include "orbg_device.h"
@@ -199,6 +201,199 @@ __global__ __launch_bounds__(256) void k_stereo_match(StereoGeom G,
             out[iL] = (bestDist < ST_TH_HIGH && bestDist < ST_TH_ORB) ? (int)(best & 0xFFFF) : -1;
         }
     }
+}
+
+// ---- row table + descriptor match in one workgroup per pair (default) ----------------
+// k_stereo_rows + k_stereo_match's semantics with the right frame staged in LDS: the row table
+// is built in LDS (never written to HBM), the right keypoints' (x, octave) and descriptors are
+// copied in once with coalesced 16-byte loads, and the match's dependent chain (row offsets ->
+// row list -> right keypoint -> descriptor) is LDS reads only.  ST_FUSED_T threads; a pair
+// whose row lists outgrow the LDS list capacity (host: what the layout leaves) builds them in
+// its global scratch instead (same code, global reads).
+#ifndef ORBG_ST_FUSED
+#define ORBG_ST_FUSED 1  // 0: k_stereo_rows + k_stereo_match (A/B)
+#endif
+#define ST_FUSED_T 1024
+
+struct StFusedLds {
+    int lcap;  // int16 list entries in LDS
+};
+
+// LDS layout (bytes): cnt[(h + 1) ints] | rx[fc floats] | roct[fc bytes, padded to 16] |
+// rdesc[fc * 32] | list[lcap int16]
+__host__ __device__ inline size_t st_fused_head(int h, int fc)
+{
+    size_t o = ((size_t)(h + 1) * 4 + 15) & ~(size_t)15;
+    o += ((size_t)fc * 4 + 15) & ~(size_t)15;
+    o += ((size_t)fc + 15) & ~(size_t)15;
+    o += (size_t)fc * 32;
+    return o;
+}
+
+template <bool LDSLIST>
+__device__ __forceinline__ void st_fused_body(const StereoGeom &G, int p, int nr, int nl,
+                                              const orbg_keypoint *__restrict__ kr,
+                                              const orbg_keypoint *__restrict__ klf,
+                                              const uint8_t *__restrict__ dlf, int *cnt,
+                                              const float *rx, const int8_t *roct,
+                                              const uint4 *rdesc, int16_t *list, int total,
+                                              int32_t *__restrict__ out)
+{
+    const int tid = threadIdx.x, H = G.h;
+    // fill (order inside a row is free: the match takes the lexicographic minimum)
+    for (int iR = tid; iR < nr; iR += ST_FUSED_T) {
+        const float y = kr[iR].y;
+        const float r = 2.0f * G.scale[roct[iR]];
+        const int maxr = (int)ceilf(y + r), minr = (int)floorf(y - r);
+        for (int yi = max(minr, 0); yi <= min(maxr, H - 1); yi++) {
+            const int slot = atomicAdd(&cnt[yi], 1);
+            if (LDSLIST || slot < G.list_cap) list[slot] = (int16_t)iR;  // LDS: total <= lcap
+        }
+    }
+    if (!LDSLIST) __threadfence_block();
+    __syncthreads();
+    // cnt[y] is now the end of row y; row y starts at cnt[y - 1] (0 for y = 0)
+    const int lane = tid & 63, j = lane / ST_LPK, q16 = lane % ST_LPK;
+    const int wv = tid >> 6;
+    constexpr int NW = ST_FUSED_T / 64;
+    // the left keypoint and descriptor of the next batch are loaded one batch ahead (the only
+    // global reads of the loop: their latency behind this batch's LDS work)
+    float nx, ny;
+    int noct;
+    uint4 nq0, nq1;
+    auto fetch = [&](int base) {
+        const int iL = base + j * NW;
+        const int idx = iL < nl ? iL : (base < nl ? base : 0);
+        const orbg_keypoint *k = klf + idx;
+        nx = k->x;
+        ny = k->y;
+        noct = k->octave;
+        const uint4 *qd = (const uint4 *)(dlf + (size_t)idx * 32);
+        nq0 = qd[0];
+        nq1 = qd[1];
+    };
+    fetch(wv);
+    for (int base = wv; base < nl; base += ST_MG * NW) {
+        const int iL = base + j * NW;
+        const bool have = iL < nl;
+        const float klx = nx, kly = ny;
+        const int kloct = noct;
+        const uint4 q0 = nq0, q1 = nq1;
+        fetch(base + ST_MG * NW);
+        const int row = (int)kly;
+        const float minU = klx - G.max_d, maxU = klx - 0.0f;
+        int c0 = 0, c1 = 0;
+        if (have && row >= 0 && row < G.h && !(maxU < 0)) {
+            c0 = row > 0 ? cnt[row - 1] : 0;
+            c1 = LDSLIST ? cnt[row] : min(cnt[row], G.list_cap);
+        }
+        uint32_t best = 0xFFFFFFFFu;
+        for (int c = c0 + q16; c < c1; c += ST_LPK) {
+            const int iR = list[c];
+            const int oct = roct[iR];
+            if (oct < kloct - 1 || oct > kloct + 1) continue;
+            const float x = rx[iR];
+            if (!(x >= minU && x <= maxU)) continue;
+            const uint4 d0 = rdesc[2 * iR], d1 = rdesc[2 * iR + 1];
+            const uint32_t dist = __popc(q0.x ^ d0.x) + __popc(q0.y ^ d0.y) + __popc(q0.z ^ d0.z) +
+                                  __popc(q0.w ^ d0.w) + __popc(q1.x ^ d1.x) + __popc(q1.y ^ d1.y) +
+                                  __popc(q1.z ^ d1.z) + __popc(q1.w ^ d1.w);
+            best = min(best, (dist << 16) | (uint32_t)iR);
+        }
+#pragma unroll
+        for (int o = ST_LPK / 2; o > 0; o >>= 1) best = min(best, (uint32_t)__shfl_xor((int)best, o, 64));
+        if (q16 == 0 && have) {
+            const int bestDist = best == 0xFFFFFFFFu ? ST_TH_HIGH : (int)(best >> 16);
+            out[iL] = (bestDist < ST_TH_HIGH && bestDist < ST_TH_ORB) ? (int)(best & 0xFFFF) : -1;
+        }
+    }
+}
+
+__global__ __launch_bounds__(ST_FUSED_T) void k_stereo_rows_match(
+    StereoGeom G, const orbg_keypoint *__restrict__ kps, const uint8_t *__restrict__ desc,
+    const int32_t *__restrict__ counts, const int32_t *__restrict__ left,
+    const int32_t *__restrict__ right, int16_t *__restrict__ row_list, int lcap,
+    int32_t *__restrict__ best_r)
+{
+    extern __shared__ __attribute__((aligned(16))) uint8_t st_lds[];
+    const int p = blockIdx.x, tid = threadIdx.x, H = G.h, fc = G.fc;
+    const int fl = left[p], fr = right[p];
+    const int nl = counts[fl], nr = counts[fr];
+    uint8_t *b = st_lds;
+    int *cnt = (int *)b;
+    b += ((size_t)(H + 1) * 4 + 15) & ~(size_t)15;
+    float *rx = (float *)b;
+    b += ((size_t)fc * 4 + 15) & ~(size_t)15;
+    int8_t *roct = (int8_t *)b;
+    b += ((size_t)fc + 15) & ~(size_t)15;
+    uint4 *rdesc = (uint4 *)b;
+    b += (size_t)fc * 32;
+    int16_t *llist = (int16_t *)b;
+    const orbg_keypoint *kr = kps + (size_t)fr * fc;
+    for (int y = tid; y <= H; y += ST_FUSED_T) cnt[y] = 0;
+    // the right frame's descriptors: 16-byte words, coalesced
+    {
+        // four 16-byte loads in flight per thread before the LDS stores
+        const uint4 *src = (const uint4 *)(desc + (size_t)fr * fc * 32);
+        for (int i0 = 0; i0 < 2 * nr; i0 += 4 * ST_FUSED_T) {
+            uint4 v[4];
+#pragma unroll
+            for (int u = 0; u < 4; u++) {
+                const int i = i0 + u * ST_FUSED_T + tid;
+                v[u] = src[i < 2 * nr ? i : 0];
+            }
+#pragma unroll
+            for (int u = 0; u < 4; u++) {
+                const int i = i0 + u * ST_FUSED_T + tid;
+                if (i < 2 * nr) rdesc[i] = v[u];
+            }
+        }
+    }
+    __syncthreads();
+    for (int iR = tid; iR < nr; iR += ST_FUSED_T) {
+        const orbg_keypoint k = kr[iR];
+        rx[iR] = k.x;
+        roct[iR] = (int8_t)k.octave;
+        const float r = 2.0f * G.scale[k.octave];
+        const int maxr = (int)ceilf(k.y + r), minr = (int)floorf(k.y - r);
+        for (int yi = max(minr, 0); yi <= min(maxr, H - 1); yi++) atomicAdd(&cnt[yi], 1);
+    }
+    __syncthreads();
+    // exclusive scan over H rows (<= 4 per thread); cnt[y] becomes row y's fill cursor
+    __shared__ int wsum[ST_FUSED_T / 64];
+    const int per = (H + ST_FUSED_T - 1) / ST_FUSED_T;
+    int loc = 0;
+    for (int k = 0; k < per; k++) {
+        const int y = tid * per + k;
+        loc += y < H ? cnt[y] : 0;
+    }
+    const int lane = tid & 63, wv = tid >> 6;
+    const int incl = wave_incl_scan(loc);
+    if (lane == 63) wsum[wv] = incl;
+    __syncthreads();
+    int before = 0, total = 0;
+    for (int i = 0; i < ST_FUSED_T / 64; i++) {
+        before += i < wv ? wsum[i] : 0;
+        total += wsum[i];
+    }
+    int run = before + incl - loc;
+    for (int k = 0; k < per; k++) {
+        const int y = tid * per + k;
+        if (y < H) {
+            const int c = cnt[y];
+            cnt[y] = run;
+            run += c;
+        }
+    }
+    __syncthreads();
+    const orbg_keypoint *klf = kps + (size_t)fl * fc;
+    const uint8_t *dlf = desc + (size_t)fl * fc * 32;
+    int32_t *out = best_r + (size_t)p * fc;
+    if (total <= lcap)  // workgroup-uniform
+        st_fused_body<true>(G, p, nr, nl, kr, klf, dlf, cnt, rx, roct, rdesc, llist, total, out);
+    else
+        st_fused_body<false>(G, p, nr, nl, kr, klf, dlf, cnt, rx, roct, rdesc,
+                             row_list + (size_t)p * G.list_cap, total, out);
 }
 
 // ---- SAD refinement -----------------------------------------------------------------
@@ -692,14 +887,39 @@ int launch_stereo(hipStream_t st, const OrbgGeom &g, const orbg_keypoint *kps,
     s += (size_t)npairs * G.fc * 4;
     int32_t *sad = (int32_t *)s;
     hipEvent_t a = nullptr;
-    prof_begin(prof, st, "stereo_rows", &a);
-    hipLaunchKernelGGL(k_stereo_rows, dim3(npairs), dim3(ST_ROWS_T), 0, st, G, kps, counts,
-                       d_right, row_off, row_list);
-    prof_end(prof, st, "stereo_rows", a);
-    prof_begin(prof, st, "stereo_match", &a);
-    hipLaunchKernelGGL(k_stereo_match, dim3(ST_MATCH_WAVES / 4, npairs), dim3(256), 0, st, G, kps,
-                       desc, counts, d_left, d_right, row_off, row_list, best_r);
-    prof_end(prof, st, "stereo_match", a);
+    // fused rows + match: the right frame (keypoints' x / octave, descriptors) and the row
+    // lists in LDS, up to 160 KB per workgroup
+    const size_t head = st_fused_head(G.h, G.fc);
+    int lcap = (int)std::min<size_t>((size_t)G.list_cap,
+                                     head < 160 * 1024 - 1024 ? (160 * 1024 - 1024 - head) / 2 : 0);
+    // ORBG_ST_FUSED=0|1 (default ORBG_ST_FUSED); ORBG_ST_LCAP (tests): a smaller LDS list, so
+    // pairs take the fused kernel's global-list path
+    const char *ef = getenv("ORBG_ST_FUSED"), *el = getenv("ORBG_ST_LCAP");
+    const bool fused = (ef ? atoi(ef) != 0 : ORBG_ST_FUSED != 0) && lcap >= 4 * G.fc;
+    if (el) lcap = std::max(0, std::min(lcap, atoi(el)));
+    if (fused) {
+        const size_t lds = head + (size_t)lcap * 2;
+        static size_t attr = 0;
+        if (attr < lds) {
+            if (hipFuncSetAttribute((const void *)k_stereo_rows_match,
+                                    hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) != hipSuccess)
+                return ORBG_EIO;
+            attr = lds;
+        }
+        prof_begin(prof, st, "stereo_match", &a);
+        hipLaunchKernelGGL(k_stereo_rows_match, dim3(npairs), dim3(ST_FUSED_T), lds, st, G, kps,
+                           desc, counts, d_left, d_right, row_list, lcap, best_r);
+        prof_end(prof, st, "stereo_match", a);
+    } else {
+        prof_begin(prof, st, "stereo_rows", &a);
+        hipLaunchKernelGGL(k_stereo_rows, dim3(npairs), dim3(ST_ROWS_T), 0, st, G, kps, counts,
+                           d_right, row_off, row_list);
+        prof_end(prof, st, "stereo_rows", a);
+        prof_begin(prof, st, "stereo_match", &a);
+        hipLaunchKernelGGL(k_stereo_match, dim3(ST_MATCH_WAVES / 4, npairs), dim3(256), 0, st, G,
+                           kps, desc, counts, d_left, d_right, row_off, row_list, best_r);
+        prof_end(prof, st, "stereo_match", a);
+    }
     prof_begin(prof, st, "stereo_sad", &a);
     hipLaunchKernelGGL(ORBG_ST_MG4 ? k_stereo_sad_mg : k_stereo_sad,
                        dim3(ST_SAD_WAVES / 4, npairs), dim3(256), 0, st, G, kps, counts, d_left,

@@ -20,7 +20,10 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 EXE = os.path.join(ROOT, "orb_slam2_test_amd", "lib", "compat_selftest")
 
 
-def test_cpp_compat_layer_matches_oracle(oracle, tmp_path):
+@pytest.mark.parametrize("zc", ["1", "0"])
+def test_cpp_compat_layer_matches_oracle(oracle, tmp_path, zc):
+    """zc: ORBG_ZC, the zero-copy output block / SearchForInitialization staging (default 1)
+    or the DMA path it replaced"""
     import torch
     if torch.cuda.device_count() == 0:
         pytest.skip("no GPU")
@@ -31,7 +34,8 @@ def test_cpp_compat_layer_matches_oracle(oracle, tmp_path):
         seq[t].tofile(tmp_path / f"f{t}.raw")
     r = subprocess.run([EXE, "run", str(w), str(h), str(tmp_path / "f0.raw"),
                         str(tmp_path / "f1.raw"), str(tmp_path), str(nfeat)],
-                       capture_output=True, text=True, timeout=300)
+                       capture_output=True, text=True, timeout=300,
+                       env=dict(os.environ, ORBG_ZC=zc))
     assert r.returncode == 0, r.stdout + r.stderr
     p = oracle.params(nfeatures=nfeat)
     ref = [oracle.extract(p, seq[t]) for t in range(2)]

@@ -80,3 +80,14 @@ def test_stereo_frame_host_entry(oracle):
     rur, rdp = oracle.stereo_matches(p, rl, rr, 1241, 376, BF, float(np.float32(BF) / np.float32(FX)))
     assert np.array_equal(F.mvuRight, rur) and np.array_equal(F.mvDepth, rdp)
     assert F.N == len(rl["kps"])
+
+
+@pytest.mark.parametrize("env", [{"ORBG_ST_FUSED": "0"}, {"ORBG_ST_LCAP": "64"}])
+def test_match_paths(oracle, monkeypatch, env):
+    """k_stereo_rows_match (the default: right frame and row lists in LDS) against its
+    alternatives: the two-kernel k_stereo_rows + k_stereo_match (ORBG_ST_FUSED=0), and the
+    fused kernel's global-list path taken by a pair whose row lists outgrow the LDS list
+    (forced by ORBG_ST_LCAP).  Both read at launch time, so they apply to this context."""
+    for k, v in env.items():
+        monkeypatch.setenv(k, v)
+    run_pairs(oracle, [S.stereo_pair(376, 1241, seed=300 + i) for i in range(2)])
