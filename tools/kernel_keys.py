@@ -4,7 +4,8 @@ KEYS = {
     "k_blur": "blur", "k_blur2": "blur", "k_octree_lds": "octree", "k_octree": "octree_big",
     "k_orient_desc": "orient_desc", "k_knn2_pairs": "knn2", "k_knn2_pairs_i8": "knn2", "k_init_cands_pairs": "init_cands",
     "k_init_resolve_pairs": "init_resolve", "k_stereo_rows": "stereo_rows",
-    "k_stereo_match": "stereo_match", "k_stereo_sad": "stereo_sad",
+    "k_stereo_match": "stereo_match", "k_stereo_rows_match": "stereo_match",
+    "k_stereo_sad": "stereo_sad", "k_stereo_sad_mg": "stereo_sad",
     "k_stereo_median": "stereo_median", "k_ba_edges": "ba_edges",
     "k_ba_point_blocks": "ba_point_blocks", "k_ba_pose_mfma": "ba_pose_mfma",
     "k_ba_slices_special": "ba_pose_mfma", "k_ba_pose_reduce": "ba_pose_reduce",
