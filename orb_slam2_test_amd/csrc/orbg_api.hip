@@ -67,7 +67,9 @@ hipError_t launch_orient_desc(bool bfma, dim3 grid, hipStream_t st, const OrbgGe
                               const uint8_t *pyr, const uint8_t *blur, const uint4 *odtab,
                               const uint32_t *lvl_kp, const uint16_t *lvl_idx,
                               const int32_t *lvl_cnt, OrbgKeypointDev *kps, uint8_t *desc,
-                              int32_t *counts);
+                              int32_t *counts, uint8_t *hc_base = nullptr,
+                              const int32_t *hc_err = nullptr, size_t hc_okp = 0,
+                              size_t hc_ods = 0);
 // match_kernels.hip
 int launch_match_pairs(hipStream_t st, hipStream_t aux, hipEvent_t evf, hipEvent_t evj,
                        const uint8_t *desc, const orbg_keypoint *kps,
@@ -422,6 +424,10 @@ struct orbg_ctx {
     uint8_t *h_zc = nullptr, *h_zc_dev = nullptr;
     size_t zc_bytes = 0;
     int zc_mode = -1;  // -1: read ORBG_ZC on first use
+    // orbg_extract's zero-copy outputs written by k_orient_desc itself (the packed block's
+    // device pointer while launch_extract runs; null otherwise)
+    uint8_t *hc_dst = nullptr;
+    bool hc_done = false;  // the last extraction's frame 0 is already in the packed block
     uint8_t *d_pyr = nullptr, *d_blur = nullptr;  // = pyr_slot[slot], blur_slot[slot]
     int32_t *d_cell_cnt = nullptr;                 // = cnt_slot[slot]
     uint2 *d_cell_kp = nullptr;                    // = ckp_slot[slot]
@@ -670,6 +676,15 @@ static int stage(orbg_ctx *c, size_t bytes, uint8_t **out)
     }
     *out = c->h_stage;
     return ORBG_OK;
+}
+
+static bool hc_enabled()
+{
+    static const int on = [] {
+        const char *e = getenv("ORBG_HC");
+        return e ? atoi(e) : 1;
+    }();
+    return on != 0;
 }
 
 static bool use_zc(orbg_ctx *c)
@@ -1646,6 +1661,13 @@ static hipError_t launch_fast_cells(orbg_ctx *c, hipStream_t st, const uint8_t *
     return e;
 }
 
+// the packed frame block: header, keypoints at ORBG_PACK_OKP, descriptors at pack_ods
+#define ORBG_PACK_OKP ((size_t)256)
+static size_t pack_ods(int frame_cap)
+{
+    return ORBG_PACK_OKP + (((size_t)frame_cap * sizeof(orbg_keypoint) + 255) & ~(size_t)255);
+}
+
 // Pipelined batch into slot s (orbg_set_pipeline).  Front on `stream`: resize chain, FAST
 // cells of every level (one launch), GaussianBlur.  Back on `ostream` (high priority):
 // quadtree levels once the cells are written, k_octree, then orientation + descriptors once
@@ -1760,6 +1782,7 @@ static int launch_extract(orbg_ctx *c, const uint8_t *d_imgs, int B, int pitch, 
     // the match / stereo outputs of the previous batch are stale from here on
     c->last_npairs = 0;
     c->last_nstereo = 0;
+    c->hc_done = false;
 #ifdef ORBG_DEV_KNOBS
     g_extract_batches++;
 #endif
@@ -1885,7 +1908,9 @@ static int launch_extract(orbg_ctx *c, const uint8_t *d_imgs, int B, int pitch, 
                                    dim3((G.out_frame + 4 * ORBG_OD_KPW - 1) / (4 * ORBG_OD_KPW) * B),
                                    st, c->d_geom, d_imgs, fs, pitch, c->d_pyr,
                                    c->d_blur, c->d_odtab, c->d_lvl_kp, c->d_lvl_idx, c->d_lvl_cnt, (OrbgKeypointDev *)c->d_kps,
-                                   c->d_desc, c->d_counts));
+                                   c->d_desc, c->d_counts,
+                                   c->hc_dst, c->d_err, c->hc_dst ? ORBG_PACK_OKP : 0,
+                                   c->hc_dst ? pack_ods(G.frame_cap) : 0));
     HIPCHK(hipEventRecord(c->ev_ext[s], st));
     HIPCHK(hipGetLastError());
     c->last_img = d_imgs;
@@ -1994,10 +2019,13 @@ extern "C" int orbg_download_frame(orbg_ctx *c, int frame, orbg_keypoint *kps, u
     // kernel behind the frame's last writer (the back stream), one DMA, then the streams are
     // drained as check_err does, so the error word covers every batch since the last read
     const size_t fc = (size_t)c->geom.frame_cap;
-    const size_t okp = 256, ods = okp + ((fc * sizeof(orbg_keypoint) + 255) & ~(size_t)255);
+    const size_t okp = ORBG_PACK_OKP, ods = pack_ods(c->geom.frame_cap);
     const size_t bytes = ods + fc * 32;
     int rc;
     uint8_t *hs, *dst;
+    // orbg_extract's k_orient_desc already stored frame 0's outputs into the block
+    const bool packed = c->hc_done && frame == 0;
+    c->hc_done = false;
     if (use_zc(c)) {
         if ((rc = zc_buf(c, bytes, &hs, &dst))) return rc;
     } else {
@@ -2013,11 +2041,13 @@ extern "C" int orbg_download_frame(orbg_ctx *c, int frame, orbg_keypoint *kps, u
         dst = c->d_pack;
     }
     hipStream_t st = back_stream(c);
-    const size_t words = std::max(fc * (sizeof(orbg_keypoint) / 4), fc * 8);
-    hipLaunchKernelGGL(k_pack_frame, dim3((unsigned)((words + 255) / 256)), dim3(256), 0, st,
-                       c->d_err, c->d_counts, (const uint32_t *)c->d_kps,
-                       (const uint32_t *)c->d_desc, frame, fc, okp, ods, (uint32_t *)dst);
-    HIPCHK(hipGetLastError());
+    if (!packed) {
+        const size_t words = std::max(fc * (sizeof(orbg_keypoint) / 4), fc * 8);
+        hipLaunchKernelGGL(k_pack_frame, dim3((unsigned)((words + 255) / 256)), dim3(256), 0, st,
+                           c->d_err, c->d_counts, (const uint32_t *)c->d_kps,
+                           (const uint32_t *)c->d_desc, frame, fc, okp, ods, (uint32_t *)dst);
+        HIPCHK(hipGetLastError());
+    }
     if (!use_zc(c)) HIPCHK(hipMemcpyAsync(hs, c->d_pack, bytes, hipMemcpyDeviceToHost, st));
     if ((rc = sync_all(c))) return rc;
     c->prof.collect();
@@ -2082,7 +2112,18 @@ extern "C" int orbg_extract(orbg_ctx *c, const uint8_t *img, int w, int h, size_
         HIPCHK(hipMemcpyAsync(c->d_img + (size_t)y0 * w, hs + (size_t)y0 * w, (size_t)(y1 - y0) * w,
                               hipMemcpyHostToDevice, c->stream));
     }
-    if ((rc = launch_extract(c, c->d_img, 1, w, (int64_t)bytes))) return rc;
+    // zero-copy on the non-pipelined path: k_orient_desc stores the packed outputs itself
+    // (ORBG_HC=0: k_pack_frame after it, A/B)
+    uint8_t *hz = nullptr, *dz = nullptr;
+    if (use_zc(c) && !(c->pipelined && !c->serial) && hc_enabled()) {
+        const size_t pbytes = pack_ods(c->geom.frame_cap) + (size_t)c->geom.frame_cap * 32;
+        if ((rc = zc_buf(c, pbytes, &hz, &dz))) return rc;
+    }
+    c->hc_dst = dz;
+    rc = launch_extract(c, c->d_img, 1, w, (int64_t)bytes);
+    c->hc_dst = nullptr;
+    if (rc) return rc;
+    c->hc_done = dz != nullptr;
     return orbg_download_frame(c, 0, kps, desc, cap, n_out);
 }
 

@@ -94,14 +94,24 @@ static_assert(OD_KPW >= 1 && OD_KPW <= 32, "one slot per lane, okmask is 32 bits
 // row start: byte b is column u = 16c + b - sh - 15, weight u + 15 and one when
 // |u| <= umax[|r - 15|], else 0.  [sh][0][w] = weights, [sh][1][w] = ones.
 // BFMA: the rBRIEF rotation x*b + y*a with one FMA (brief_fma pin) or two roundings (default)
-template <bool BFMA>
+// HC (the single-frame drop-in, B = 1): every output is also stored into the packed host
+// block orbg_download_frame reads (k_pack_frame's layout: [0..4) the sticky error word and
+// the count, keypoints at byte hc.okp, descriptors at hc.ods), so no packing kernel and no
+// copy follow the extraction
+struct OdHostCopy {
+    uint8_t *base;
+    const int32_t *err;
+    int32_t okp, ods;
+};
+
+template <bool BFMA, bool HC>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(ORBG_OD_WPE, 8))) void k_orient_desc(
     const OrbgGeom *__restrict__ g, const uint8_t *__restrict__ img0, int64_t img_fs,
     int img_pitch, const uint8_t *__restrict__ pyr, const uint8_t *__restrict__ blur,
     const uint4 *__restrict__ odtab, const uint32_t *__restrict__ lvl_kp,
     const uint16_t *__restrict__ lvl_idx, const int32_t *__restrict__ lvl_cnt,
     OrbgKeypointDev *__restrict__ kps,
-    uint8_t *__restrict__ desc, int32_t *__restrict__ counts)
+    uint8_t *__restrict__ desc, int32_t *__restrict__ counts, OdHostCopy hc)
 {
 #if ORBG_OD_PRIO
     __builtin_amdgcn_s_setprio(ORBG_OD_PRIO);  // on the pipelined step's critical path (A/B)
@@ -126,6 +136,13 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(ORBG_OD_WPE
         int total = 0;
         for (int l = 0; l < L; l++) total += lc[l];
         counts[f] = total;
+        if (HC) {  // header: the error word (final: its writers ran before), the count
+            int32_t *hdr = (int32_t *)hc.base;
+            hdr[0] = hc.err[0];
+            hdr[1] = hc.err[1];
+            hdr[2] = total;
+            hdr[3] = 0;
+        }
     }
     // lane j < OD_KPW: slot s0 + j -> quadtree key, level, output row (the winner's list
     // position lvl_idx: the octree put the slots in image-tile order); okmask bit j
@@ -306,6 +323,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(ORBG_OD_WPE
         kp.octave = my_lev;
         kp.class_id = -1;
         kps[(int64_t)f * g->frame_cap + my_i] = kp;
+        if (HC) ((OrbgKeypointDev *)(hc.base + hc.okp))[my_i] = kp;
     }
 
     if (g->dbg == 22) return;  // developer phase timing: stop after B
@@ -370,8 +388,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(ORBG_OD_WPE
             if ((lane >> 1) == t) word = (uint32_t)(m >> (32 * (lane & 1)));
         }
         const int i = __builtin_amdgcn_readlane(my_i, j);
-        if (((okmask >> j) & 1u) && lane < 8)
+        if (((okmask >> j) & 1u) && lane < 8) {
             ((uint32_t *)(desc + (drow0 + i) * 32))[lane] = word;
+            if (HC) ((uint32_t *)(hc.base + hc.ods + (int64_t)i * 32))[lane] = word;
+        }
     }
 }
 
@@ -380,16 +400,22 @@ hipError_t launch_orient_desc(bool bfma, dim3 grid, hipStream_t st, const OrbgGe
                               const uint8_t *pyr, const uint8_t *blur, const uint4 *odtab,
                               const uint32_t *lvl_kp, const uint16_t *lvl_idx,
                               const int32_t *lvl_cnt, OrbgKeypointDev *kps, uint8_t *desc,
-                              int32_t *counts)
+                              int32_t *counts, uint8_t *hc_base, const int32_t *hc_err,
+                              size_t hc_okp, size_t hc_ods)
 {
-    if (bfma)
-        hipLaunchKernelGGL(k_orient_desc<true>, grid, dim3(256), 0, st, g, img0, img_fs,
-                           img_pitch, pyr, blur, odtab, lvl_kp, lvl_idx, lvl_cnt, kps, desc,
-                           counts);
-    else
-        hipLaunchKernelGGL(k_orient_desc<false>, grid, dim3(256), 0, st, g, img0, img_fs,
-                           img_pitch, pyr, blur, odtab, lvl_kp, lvl_idx, lvl_cnt, kps, desc,
-                           counts);
+    const OdHostCopy hc{hc_base, hc_err, (int32_t)hc_okp, (int32_t)hc_ods};
+#define OD_LAUNCH(BF, H)                                                                       \
+    hipLaunchKernelGGL((k_orient_desc<BF, H>), grid, dim3(256), 0, st, g, img0, img_fs,        \
+                       img_pitch, pyr, blur, odtab, lvl_kp, lvl_idx, lvl_cnt, kps, desc, counts, \
+                       hc)
+    if (hc_base) {
+        if (bfma) OD_LAUNCH(true, true);
+        else OD_LAUNCH(false, true);
+    } else {
+        if (bfma) OD_LAUNCH(true, false);
+        else OD_LAUNCH(false, false);
+    }
+#undef OD_LAUNCH
     return hipGetLastError();
 }
 

@@ -20,10 +20,11 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 EXE = os.path.join(ROOT, "orb_slam2_test_amd", "lib", "compat_selftest")
 
 
-@pytest.mark.parametrize("zc", ["1", "0"])
+@pytest.mark.parametrize("zc", ["1", "0", "1-nohc"])
 def test_cpp_compat_layer_matches_oracle(oracle, tmp_path, zc):
     """zc: ORBG_ZC, the zero-copy output block / SearchForInitialization staging (default 1)
-    or the DMA path it replaced"""
+    or the DMA path it replaced; "1-nohc": zero-copy with the block filled by k_pack_frame
+    (ORBG_HC=0) instead of by k_orient_desc itself"""
     import torch
     if torch.cuda.device_count() == 0:
         pytest.skip("no GPU")
@@ -35,7 +36,7 @@ def test_cpp_compat_layer_matches_oracle(oracle, tmp_path, zc):
     r = subprocess.run([EXE, "run", str(w), str(h), str(tmp_path / "f0.raw"),
                         str(tmp_path / "f1.raw"), str(tmp_path), str(nfeat)],
                        capture_output=True, text=True, timeout=300,
-                       env=dict(os.environ, ORBG_ZC=zc))
+                       env=dict(os.environ, ORBG_ZC=zc[0], ORBG_HC="0" if "nohc" in zc else "1"))
     assert r.returncode == 0, r.stdout + r.stderr
     p = oracle.params(nfeatures=nfeat)
     ref = [oracle.extract(p, seq[t]) for t in range(2)]
