@@ -494,6 +494,23 @@ __device__ __forceinline__ ResolveShared resolve_layout(uint8_t *base, int cap, 
     return S;
 }
 
+// developer builds: cycle counts of the resolver's parts (thread 0, i.e. wave 0's lane 0):
+// [0] init, [1] chunk walks (wave 0), [2] of which rescans, [3] chunk-end barriers, [4] tail,
+// [5] speculative rounds, [6] rescans, [7] resolver calls (orbg_dev_resolve_prof)
+#ifdef ORBG_DEV_KNOBS
+__device__ unsigned long long g_rprof[8];
+#define RP_NOW() __builtin_readcyclecounter()
+#define RP_ADD(k, v)                                                                         \
+    do {                                                                                     \
+        if (threadIdx.x == 0) atomicAdd(&g_rprof[k], (unsigned long long)(v));               \
+    } while (0)
+#else
+#define RP_NOW() 0ull
+#define RP_ADD(k, v) \
+    do {             \
+    } while (0)
+#endif
+
 // exact fallback: sequential-scan semantics, wave-parallel
 __device__ void rescan(const orbg_keypoint *k2, const uint8_t *d2, int n2, const GridPrm &g,
                        const Window &w, const uint32_t qd[8], const uint16_t *mdist, int *best,
@@ -542,6 +559,8 @@ __device__ void init_resolve_block(ResolveShared &S, int cap, const orbg_keypoin
 {
     const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
     const int n1c = min(n1, cap), n2c = min(n2, cap);  // indices any query / candidate can have
+    [[maybe_unused]] unsigned long long rp_t = RP_NOW();
+    RP_ADD(7, 1);
     for (int i0 = 0; i0 < n2c; i0 += 4 * RESOLVE_T) {
         float a[4];
 #pragma unroll
@@ -645,6 +664,11 @@ __device__ void init_resolve_block(ResolveShared &S, int cap, const orbg_keypoin
         prefetch(0);
     }
     __syncthreads();
+    {
+        const unsigned long long t = RP_NOW();
+        RP_ADD(0, t - rp_t);
+        rp_t = t;
+    }
     for (int c = 0; c < nchunks; c++) {
         if (wv == 1) {
             if (!preload) prefetch(c + 1);
@@ -668,6 +692,7 @@ __device__ void init_resolve_block(ResolveShared &S, int cap, const orbg_keypoin
             const int i1 = c0 + lane;
             unsigned long long pending = __ballot(total > 0);
             while (pending) {
+                RP_ADD(5, 1);
                 const bool pend = (pending >> lane) & 1ull;
                 int found = 0, bd = INT_MAX, bd2 = INT_MAX, bi = -1, lastpos = kk - 1;
 #pragma unroll
@@ -722,6 +747,8 @@ __device__ void init_resolve_block(ResolveShared &S, int cap, const orbg_keypoin
                 pending &= ~below;
                 wave_sync_lds();
                 if (lr < 64 && lr == lstar) {
+                    [[maybe_unused]] const unsigned long long rs0 = RP_NOW();
+                    RP_ADD(6, 1);
                     // K-list exhausted: exact rescan of query c0 + lr against the committed state
                     const int q1 = c0 + lr;
                     const float px = prev[(size_t)q1 * prev_stride];
@@ -736,10 +763,21 @@ __device__ void init_resolve_block(ResolveShared &S, int cap, const orbg_keypoin
                     if (lane == 0) apply(q1, bestDist, bestDist2, bestIdx2);
                     pending &= ~(1ull << lr);
                     wave_sync_lds();
+                    RP_ADD(2, RP_NOW() - rs0);
                 }
             }
         }
+        {
+            const unsigned long long t = RP_NOW();
+            RP_ADD(1, t - rp_t);
+            rp_t = t;
+        }
         __syncthreads();
+        {
+            const unsigned long long t = RP_NOW();
+            RP_ADD(3, t - rp_t);
+            rp_t = t;
+        }
     }
     int nmatches = *S.nmp;
     if (check_ori) {
@@ -798,6 +836,7 @@ __device__ void init_resolve_block(ResolveShared &S, int cap, const orbg_keypoin
         }
     }
     if (tid == 0) *nm_out = nmatches;
+    RP_ADD(4, RP_NOW() - rp_t);
 }
 
 // prev_out, m12, nm may be host-mapped (the host entry's zero-copy outputs): written once each
@@ -925,6 +964,19 @@ int launch_match_pairs(hipStream_t st, hipStream_t aux, hipEvent_t evf, hipEvent
 // cap: 1 + the last level-0 index of either frame (every query / candidate index the
 // search can touch: it reads level-0 keypoints only, ORBmatcher.cc:509-512, 1 <= cap <=
 // max(n1, n2)); queries past it get no candidates and vnMatches12 = -1
+#ifdef ORBG_DEV_KNOBS
+// developer builds: read (and with reset, clear) the resolver cycle counters
+extern "C" int orbg_dev_resolve_prof(unsigned long long out[8], int reset)
+{
+    if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_rprof), sizeof(g_rprof)) != hipSuccess) return -5;
+    if (reset) {
+        const unsigned long long z[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+        if (hipMemcpyToSymbol(HIP_SYMBOL(g_rprof), z, sizeof(z)) != hipSuccess) return -5;
+    }
+    return 0;
+}
+#endif
+
 int launch_init_match_single(hipStream_t st, const orbg_keypoint *k1, const uint8_t *d1, int n1,
                              const orbg_keypoint *k2, const uint8_t *d2, int n2, orbg_bounds b,
                              const float *prev, float *prev_out, int32_t *m12, int32_t *nm,
