@@ -669,6 +669,7 @@ __device__ void init_resolve_block(ResolveShared &S, int cap, const orbg_keypoin
         RP_ADD(0, t - rp_t);
         rp_t = t;
     }
+    int nm_reg = 0;  // wave 0: this resolver's committed-match count (lane-uniform)
     for (int c = 0; c < nchunks; c++) {
         if (wv == 1) {
             if (!preload) prefetch(c + 1);
@@ -690,16 +691,24 @@ __device__ void init_resolve_block(ResolveShared &S, int cap, const orbg_keypoin
             for (int k = 0; k < ORBG_MATCH_TOPK; k++) e[k] = lists[lane * ORBG_MATCH_TOPK + k];
             const int kk = min(total, ORBG_MATCH_TOPK);
             const int i1 = c0 + lane;
+            const float a1 = S.ang1[min(i1, cap - 1)];  // vbPrevMatched's keypoint angle
             unsigned long long pending = __ballot(total > 0);
             while (pending) {
                 RP_ADD(5, 1);
                 const bool pend = (pending >> lane) & 1ull;
                 int found = 0, bd = INT_MAX, bd2 = INT_MAX, bi = -1, lastpos = kk - 1;
+                // every list entry's vMatchedDistance read at once (indices clamped: entries
+                // past the list are read and ignored), then the in-order pick on registers --
+                // not one dependent LDS round trip per consulted entry
+                int md[ORBG_MATCH_TOPK];
+#pragma unroll
+                for (int k = 0; k < ORBG_MATCH_TOPK; k++)
+                    md[k] = S.mdist[min((int)(e[k] & 0xFFFFF), cap - 1)];
 #pragma unroll
                 for (int k = 0; k < ORBG_MATCH_TOPK; k++) {
                     if (!pend || k >= kk || found >= 2) continue;
                     const int d = (int)(e[k] >> 32), i2 = (int)(e[k] & 0xFFFFF);
-                    if ((int)S.mdist[i2] <= d) continue;
+                    if (md[k] <= d) continue;
                     if (found == 0) {
                         bd = d;
                         bi = i2;
@@ -710,13 +719,21 @@ __device__ void init_resolve_block(ResolveShared &S, int cap, const orbg_keypoin
                 }
                 const bool resc = pend && found < 2 && total > ORBG_MATCH_TOPK;
                 const bool app = pend && !resc && bd <= TH_LOW && bd < (float)bd2 * nnratio;
+                // the commit's reads of the pick, issued before the conflict check: vnMatches21
+                // changes only in commits, and committing lanes have distinct picks
+                const int bic = max(bi, 0);
+                const int m21_pre = S.m21[bic];
+                const float a2 = S.ang2[bic];
                 if (app) atomicMin(&S.owner[bi], lane);
                 wave_sync_lds();
                 bool conf = false;
+                int ow[ORBG_MATCH_TOPK];
 #pragma unroll
                 for (int k = 0; k < ORBG_MATCH_TOPK; k++)
-                    if (pend && k < kk && k <= lastpos && S.owner[(int)(e[k] & 0xFFFFF)] < lane)
-                        conf = true;
+                    ow[k] = S.owner[min((int)(e[k] & 0xFFFFF), cap - 1)];
+#pragma unroll
+                for (int k = 0; k < ORBG_MATCH_TOPK; k++)
+                    if (pend && k < kk && k <= lastpos && ow[k] < lane) conf = true;
                 const unsigned long long cm = __ballot(conf), rm = __ballot(resc);
                 const int lc = cm ? __builtin_ctzll(cm) : 64, lr = rm ? __builtin_ctzll(rm) : 64;
                 const int lstar = min(lc, lr);
@@ -725,7 +742,7 @@ __device__ void init_resolve_block(ResolveShared &S, int cap, const orbg_keypoin
                 if (app) S.owner[bi] = 64;
                 bool stole = false;
                 if (commit) {
-                    const int old = S.m21[bi];
+                    const int old = m21_pre;
                     if (old >= 0) {
                         S.m12[old] = -1;
                         stole = true;
@@ -734,7 +751,7 @@ __device__ void init_resolve_block(ResolveShared &S, int cap, const orbg_keypoin
                     S.m21[bi] = (int16_t)i1;
                     S.mdist[bi] = (uint16_t)bd;
                     if (check_ori) {
-                        float rot = S.ang1[i1] - S.ang2[bi];
+                        float rot = a1 - a2;
                         if (rot < 0.0f) rot += 360.0f;
                         int bin = (int)roundf(rot * factor);
                         if (bin == HISTO_LENGTH) bin = 0;
@@ -742,8 +759,7 @@ __device__ void init_resolve_block(ResolveShared &S, int cap, const orbg_keypoin
                         atomicAdd(&S.hsize[bin], 1);
                     }
                 }
-                const int delta = __popcll(__ballot(commit)) - __popcll(__ballot(stole));
-                if (lane == 0) *S.nmp += delta;
+                nm_reg += __popcll(__ballot(commit)) - __popcll(__ballot(stole));
                 pending &= ~below;
                 wave_sync_lds();
                 if (lr < 64 && lr == lstar) {
@@ -779,6 +795,8 @@ __device__ void init_resolve_block(ResolveShared &S, int cap, const orbg_keypoin
             rp_t = t;
         }
     }
+    if (tid == 0) *S.nmp += nm_reg;
+    __syncthreads();
     int nmatches = *S.nmp;
     if (check_ori) {
         __shared__ int ind[3];

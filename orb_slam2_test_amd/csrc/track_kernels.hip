@@ -570,10 +570,16 @@ __global__ __launch_bounds__(TRK_RT) void k_track_resolve(TrackArgs A)
                 const bool pend = (pending >> lane) & 1ull;
                 unsigned long long k1 = ~0ull, k2 = ~0ull;
                 int found = 0, lastpos = kk - 1;
+                // every entry's taken flag read at once (indices clamped, entries past the list
+                // ignored), then the in-order pick on registers
+                int tk[ORBG_MATCH_TOPK];
+#pragma unroll
+                for (int k = 0; k < ORBG_MATCH_TOPK; k++)
+                    tk[k] = taken[min((int)(e[k] & 0xFFFFF), A.fc - 1)];
 #pragma unroll
                 for (int k = 0; k < ORBG_MATCH_TOPK; k++) {
                     if (!pend || k >= kk || found >= need) continue;
-                    if (taken[(int)(e[k] & 0xFFFFF)]) continue;
+                    if (tk[k]) continue;
                     if (found == 0) k1 = e[k]; else k2 = e[k];
                     if (++found == need) lastpos = k;
                 }
@@ -600,10 +606,13 @@ __global__ __launch_bounds__(TRK_RT) void k_track_resolve(TrackArgs A)
                 if (takes) atomicMin(&owner[bestIdx], lane);
                 wave_sync_lds();
                 bool conf = false;
+                int ow[ORBG_MATCH_TOPK];
 #pragma unroll
                 for (int k = 0; k < ORBG_MATCH_TOPK; k++)
-                    if (pend && k < kk && k <= lastpos && owner[(int)(e[k] & 0xFFFFF)] < lane)
-                        conf = true;
+                    ow[k] = owner[min((int)(e[k] & 0xFFFFF), A.fc - 1)];
+#pragma unroll
+                for (int k = 0; k < ORBG_MATCH_TOPK; k++)
+                    if (pend && k < kk && k <= lastpos && ow[k] < lane) conf = true;
                 const unsigned long long cm = __ballot(conf), rm = __ballot(resc);
                 const int lc = cm ? __builtin_ctzll(cm) : 64, lr = rm ? __builtin_ctzll(rm) : 64;
                 const int lstar = min(lc, lr);
