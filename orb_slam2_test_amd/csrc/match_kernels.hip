@@ -263,6 +263,24 @@ struct F2Key {
 // one 256-thread block: load F2 level-0 keys to LDS, then each wave handles INIT_QPW queries
 // force-inlined: as a called function its pointer arguments would be generic (flat_ loads
 // and stores, which also count in lgkmcnt)
+// dynamic LDS of init_cands_block: 2 f2cap keys (16-byte padded), + f2cap descriptor rows
+// with LDSD when that fits 64 KB
+__host__ __device__ constexpr size_t init_cands_keys_bytes(int f2cap)
+{
+    return ((size_t)2 * f2cap * sizeof(F2Key) + 15) & ~(size_t)15;
+}
+#ifndef ORBG_INIT_LDSD
+#define ORBG_INIT_LDSD 1  // the single-pair entry (B = 1); 0: descriptors from global memory (A/B)
+#endif
+__host__ __device__ constexpr bool init_cands_lds(int f2cap)
+{
+    return ORBG_INIT_LDSD && init_cands_keys_bytes(f2cap) + (size_t)f2cap * 32 <= 65536;
+}
+
+// LDSD: F2's descriptors (the first f2cap rows) are staged in LDS after the keys, so the
+// candidate loop's Hamming distances read LDS instead of one dependent global load per
+// candidate (the host takes it when 2 f2cap keys + f2cap rows fit, init_cands_lds)
+template <bool LDSD>
 __device__ __forceinline__ void init_cands_block(const orbg_keypoint *__restrict__ k1,
                                  const uint8_t *__restrict__ d1, int n1,
                                  const orbg_keypoint *__restrict__ k2,
@@ -277,6 +295,7 @@ __device__ __forceinline__ void init_cands_block(const orbg_keypoint *__restrict
     // (distance, grid order, index), independent of the scan order)
     extern __shared__ __attribute__((aligned(16))) F2Key f2mem[];
     F2Key *f2raw = f2mem, *f2 = f2mem + f2cap;
+    uint4 *d2l = (uint4 *)((uint8_t *)f2mem + init_cands_keys_bytes(f2cap));  // LDSD
     __shared__ int nf2;
     __shared__ int colstart[ORBG_GRID_COLS + 1];
     const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
@@ -286,6 +305,23 @@ __device__ __forceinline__ void init_cands_block(const orbg_keypoint *__restrict
     __syncthreads();
     // batch: level-major output, every level-0 key sits below f2cap = level-0 capacity
     const int n2s = min(n2, f2cap);
+    if (LDSD) {
+        // rows 0 .. n2s-1, 16-byte words, four loads in flight per thread
+        const uint4 *src = (const uint4 *)d2;
+        for (int i0 = 0; i0 < 2 * n2s; i0 += 4 * 256) {
+            uint4 v[4];
+#pragma unroll
+            for (int u = 0; u < 4; u++) {
+                const int i = i0 + u * 256 + tid;
+                v[u] = src[i < 2 * n2s ? i : 0];
+            }
+#pragma unroll
+            for (int u = 0; u < 4; u++) {
+                const int i = i0 + u * 256 + tid;
+                if (i < 2 * n2s) d2l[i] = v[u];
+            }
+        }
+    }
     for (int i = tid; i < n2s; i += 256) {
         const orbg_keypoint kp = k2[i];
         if (kp.octave == 0) {
@@ -347,7 +383,8 @@ __device__ __forceinline__ void init_cands_block(const orbg_keypoint *__restrict
                     const F2Key fk = f2[j];
                     const int ord = cand_order(g, w, fk.x, fk.y);
                     if (ord < 0) continue;
-                    const int d = hamming8(qd, (const uint32_t *)(d2 + (size_t)fk.idx * 32));
+                    const int d = LDSD ? hamming8(qd, (const uint32_t *)(d2l + 2 * fk.idx))
+                                       : hamming8(qd, (const uint32_t *)(d2 + (size_t)fk.idx * 32));
                     unsigned long long key = ((unsigned long long)d << 32) |
                                              ((unsigned long long)ord << 20) | (unsigned)fk.idx;
                     cnt++;
@@ -384,16 +421,18 @@ __device__ __forceinline__ void init_cands_block(const orbg_keypoint *__restrict
     }
 }
 
+template <bool LDSD>
 __global__ __launch_bounds__(256) void k_init_cands_single(
     const orbg_keypoint *k1, const uint8_t *d1, int n1, const orbg_keypoint *k2,
     const uint8_t *d2, int n2, orbg_bounds b, const float *prev, int window,
     unsigned long long *topk, int32_t *topn)
 {
-    init_cands_block(k1, d1, n1, k2, d2, n2, b, prev, 2, window, topk, topn,
+    init_cands_block<LDSD>(k1, d1, n1, k2, d2, n2, b, prev, 2, window, topk, topn,
                      blockIdx.x * 4 * INIT_QPW, n2);
 }
 
 // batch: F1 = frame f1[p] (its keypoints are vbPrevMatched), F2 = frame f2[p]
+template <bool LDSD>
 __global__ __launch_bounds__(256) void k_init_cands_pairs(
     const orbg_keypoint *kps, const uint8_t *desc, const int32_t *counts, int fc,
     const int32_t *f1, const int32_t *f2, orbg_bounds b, int window, unsigned long long *topk,
@@ -416,7 +455,7 @@ __global__ __launch_bounds__(256) void k_init_cands_pairs(
         return;
     }
     // vbPrevMatched = F1.mvKeysUn[i].pt: read x, y straight out of the keypoint records
-    init_cands_block(k1, desc + (size_t)a * fc * 32, n1, kps + (size_t)c * fc,
+    init_cands_block<LDSD>(k1, desc + (size_t)a * fc * 32, n1, kps + (size_t)c * fc,
                      desc + (size_t)c * fc * 32, n2, b, (const float *)k1,
                      (int)(sizeof(orbg_keypoint) / sizeof(float)), window,
                      topk + (size_t)p * fc * ORBG_MATCH_TOPK, topn + (size_t)p * fc, qbase, cap);
@@ -944,9 +983,11 @@ int launch_match_pairs(hipStream_t st, hipStream_t aux, hipEvent_t evf, hipEvent
     // cap0 = level-0 capacity: every index SearchForInitialization touches is below it
     if (fc > RESOLVE_N2_CAP || fc > (1 << 20) || cap0 > fc) return ORBG_ENOTSUP;
     PL(prof, st, "init_cands",
-       hipLaunchKernelGGL(k_init_cands_pairs, dim3((cap0 + 4 * INIT_QPW - 1) / (4 * INIT_QPW) * npairs),
-                          dim3(256), 2 * cap0 * sizeof(F2Key), st, kps, desc, counts, fc, d_f1, d_f2,
-                          b, window, (unsigned long long *)topk, topk_n, cap0));
+       // descriptors from global memory: at batch the staging measured +3% (r05ae)
+       hipLaunchKernelGGL(k_init_cands_pairs<false>,
+                          dim3((cap0 + 4 * INIT_QPW - 1) / (4 * INIT_QPW) * npairs), dim3(256),
+                          init_cands_keys_bytes(cap0), st, kps, desc, counts, fc, d_f1, d_f2, b,
+                          window, (unsigned long long *)topk, topk_n, cap0));
     // knn2 (VALU bound) on `aux` beside init_resolve (one sequential workgroup per pair);
     // serial == 1 (orbg_set_serial: isolated kernel timing) keeps it on `st`
     if (serial) aux = st;
@@ -1015,9 +1056,17 @@ int launch_init_match_single(hipStream_t st, const orbg_keypoint *k1, const uint
         attr = true;
     }
     PL(prof, st, "init_cands",
-       hipLaunchKernelGGL(k_init_cands_single, dim3((nq + 4 * INIT_QPW - 1) / (4 * INIT_QPW)),
-                          dim3(256), 2 * (size_t)std::max(n2c, 1) * sizeof(F2Key), st, k1, d1, nq, k2,
-                          d2, n2c, b, prev, window, (unsigned long long *)topk, topk_n));
+       if (init_cands_lds(std::max(n2c, 1)))
+           hipLaunchKernelGGL(k_init_cands_single<true>,
+                              dim3((nq + 4 * INIT_QPW - 1) / (4 * INIT_QPW)), dim3(256),
+                              init_cands_keys_bytes(std::max(n2c, 1)) + (size_t)std::max(n2c, 1) * 32,
+                              st, k1, d1, nq, k2, d2, n2c, b, prev, window,
+                              (unsigned long long *)topk, topk_n);
+       else
+           hipLaunchKernelGGL(k_init_cands_single<false>,
+                              dim3((nq + 4 * INIT_QPW - 1) / (4 * INIT_QPW)), dim3(256),
+                              init_cands_keys_bytes(std::max(n2c, 1)), st, k1, d1, nq, k2, d2, n2c,
+                              b, prev, window, (unsigned long long *)topk, topk_n));
     PL(prof, st, "init_resolve",
        hipLaunchKernelGGL(k_init_resolve_single, dim3(1), dim3(RESOLVE_T),
                           resolve_lds_bytes(cap, resolve_nbuf(cap, true)), st, k1, d1, n1, k2, d2,
