@@ -276,7 +276,12 @@ __global__ __launch_bounds__(OCT_T) void k_octree_lds(
     const int32_t *ccount = cell_cnt + (int64_t)f * g->ncells + lv.cell_base;
     const uint2 *ckp = cell_kp + ((int64_t)f * g->ncells + lv.cell_base) * g->cell_cap;
     const int ncells = lv.ncells;
-    if (ncells + 1 > D.acap2) return;
+    // a level left to k_octree: noted in err_flag[2] (not an error; the single-frame path
+    // reruns a frame for which it skipped k_octree)
+    if (ncells + 1 > D.acap2) {
+        if (tid == 0) atomicOr(err_flag + 2, 1);
+        return;
+    }
     int n = 0;
     for (int c0 = 0; c0 < ncells; c0 += OCT_T) {
         const int c = c0 + tid;
@@ -285,7 +290,10 @@ __global__ __launch_bounds__(OCT_T) void k_octree_lds(
         if (c < ncells) V.aux[c] = V.coff[c] = (uint16_t)min(off, 65535);
         n += tot;
     }
-    if (n > D.kcap) return;
+    if (n > D.kcap) {
+        if (tid == 0) atomicOr(err_flag + 2, 1);
+        return;
+    }
     if (tid == 0) V.aux[ncells] = V.coff[ncells] = (uint16_t)n;
     for (int i = tid; i < D.nbw; i += OCT_T) V.bcnt[i] = 0;
     __syncthreads();

@@ -428,6 +428,9 @@ struct orbg_ctx {
     // device pointer while launch_extract runs; null otherwise)
     uint8_t *hc_dst = nullptr;
     bool hc_done = false;  // the last extraction's frame 0 is already in the packed block
+    // with hc_dst: k_octree (the fallback quadtree) not launched; a level it would have taken
+    // shows in the packed header's word 3 and the frame is extracted again with it
+    bool skip_big = false;
     uint8_t *d_pyr = nullptr, *d_blur = nullptr;  // = pyr_slot[slot], blur_slot[slot]
     int32_t *d_cell_cnt = nullptr;                 // = cnt_slot[slot]
     uint2 *d_cell_kp = nullptr;                    // = ckp_slot[slot]
@@ -676,6 +679,15 @@ static int stage(orbg_ctx *c, size_t bytes, uint8_t **out)
     }
     *out = c->h_stage;
     return ORBG_OK;
+}
+
+static bool skip_big_enabled()
+{
+    static const int on = [] {
+        const char *e = getenv("ORBG_SKIP_BIG");
+        return e ? atoi(e) : 1;
+    }();
+    return on != 0;
 }
 
 static bool hc_enabled()
@@ -1396,8 +1408,10 @@ extern "C" int orbg_create(int device, const orbg_params *p, orbg_ctx **out)
     // it was last read (check_err), so a pipelined caller cannot lose an overflow.  It lives
     // as long as the context (a new extraction plan keeps pending flags), and every kernel
     // that may raise a flag -- the quadtree's and the device matchers' -- can write it.
+    // Word [2] is not an error: k_octree_lds sets it when it leaves a level to k_octree, which
+    // the single-frame path checks when it skipped k_octree (orbg_extract).
     {
-        const int32_t e0[2] = {0, INT32_MAX};
+        const int32_t e0[4] = {0, INT32_MAX, 0, 0};
         if (hipMalloc(&c->d_err, sizeof(e0)) != hipSuccess ||
             hipMemcpy(c->d_err, e0, sizeof(e0), hipMemcpyHostToDevice) != hipSuccess) {
             if (c->d_err) hipFree(c->d_err);
@@ -1883,7 +1897,7 @@ static int launch_extract(orbg_ctx *c, const uint8_t *d_imgs, int B, int pitch, 
     if (oct_mode) HIPCHK(hipStreamWaitEvent(st, c->ev_oct, 0));
     if (big_side)
         HIPCHK(hipStreamWaitEvent(st, c->ev_big, 0));
-    else
+    else if (!c->skip_big)
         PROF_LAUNCH(c, "octree_big",
                     hipLaunchKernelGGL(k_octree, dim3(G.L, B), dim3(ORBG_OCT_THREADS), 0, st,
                                        c->d_geom, c->d_cell_cnt, c->d_cell_kp, c->d_keys, c->d_knode,
@@ -2119,10 +2133,26 @@ extern "C" int orbg_extract(orbg_ctx *c, const uint8_t *img, int w, int h, size_
         const size_t pbytes = pack_ods(c->geom.frame_cap) + (size_t)c->geom.frame_cap * 32;
         if ((rc = zc_buf(c, pbytes, &hz, &dz))) return rc;
     }
+    // optimistic: without k_octree when every level has an LDS quadtree launch (its early exits
+    // flag d_err[2]; a flagged frame is extracted again with k_octree, ORBG_SKIP_BIG=0: never)
+    const bool skip = dz && c->oct_dims[0].kcap > 0 && c->oct_dims[1].kcap > 0 && skip_big_enabled();
     c->hc_dst = dz;
+    c->skip_big = skip;
     rc = launch_extract(c, c->d_img, 1, w, (int64_t)bytes);
     c->hc_dst = nullptr;
+    c->skip_big = false;
     if (rc) return rc;
+    if (skip) {
+        if ((rc = sync_all(c))) return rc;
+        if (((const int32_t *)hz)[3]) {  // a level needed the fallback: again, with k_octree
+            const int32_t z = 0;
+            HIPCHK(hipMemcpy(c->d_err + 2, &z, sizeof(z), hipMemcpyHostToDevice));
+            c->hc_dst = dz;
+            rc = launch_extract(c, c->d_img, 1, w, (int64_t)bytes);
+            c->hc_dst = nullptr;
+            if (rc) return rc;
+        }
+    }
     c->hc_done = dz != nullptr;
     return orbg_download_frame(c, 0, kps, desc, cap, n_out);
 }

@@ -141,7 +141,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(ORBG_OD_WPE
             hdr[0] = hc.err[0];
             hdr[1] = hc.err[1];
             hdr[2] = total;
-            hdr[3] = 0;
+            hdr[3] = hc.err[2];  // a level left to k_octree (orbg_extract reruns the frame)
         }
     }
     // lane j < OD_KPW: slot s0 + j -> quadtree key, level, output row (the winner's list
