@@ -257,7 +257,12 @@ struct F2Key {
     int idx;
 };
 
-#define INIT_QPW 8   // queries per wave in k_init_cands
+#ifndef INIT_QPW
+#define INIT_QPW 8  // queries per wave in k_init_cands_pairs (4: +7% there)
+#endif
+#ifndef INIT_QPW_SINGLE
+#define INIT_QPW_SINGLE 4  // ... in k_init_cands_single (B = 1: twice the blocks, -4 us)
+#endif
 #define INIT_F2_CAP 4608  // host-data path bound (frame capacity at 4000 features)
 
 // one 256-thread block: load F2 level-0 keys to LDS, then each wave handles INIT_QPW queries
@@ -280,7 +285,7 @@ __host__ __device__ constexpr bool init_cands_lds(int f2cap)
 // LDSD: F2's descriptors (the first f2cap rows) are staged in LDS after the keys, so the
 // candidate loop's Hamming distances read LDS instead of one dependent global load per
 // candidate (the host takes it when 2 f2cap keys + f2cap rows fit, init_cands_lds)
-template <bool LDSD>
+template <bool LDSD, int QPW>
 __device__ __forceinline__ void init_cands_block(const orbg_keypoint *__restrict__ k1,
                                  const uint8_t *__restrict__ d1, int n1,
                                  const orbg_keypoint *__restrict__ k2,
@@ -355,8 +360,8 @@ __device__ __forceinline__ void init_cands_block(const orbg_keypoint *__restrict
     // 16-way split keeps every lane busy and the K-round merge is 4 shuffle steps deep)
     const float r = (float)window;
     const int grp = lane >> 4, sub = lane & 15;
-    for (int qq = 0; qq < INIT_QPW; qq += 4) {
-        const int i1 = qbase + wv * INIT_QPW + qq + grp;
+    for (int qq = 0; qq < QPW; qq += 4) {
+        const int i1 = qbase + wv * QPW + qq + grp;
         bool act = i1 < n1;
         if (act && k1[i1].octave > 0) {
             if (sub == 0) topn[i1] = -1;  // not a query
@@ -427,8 +432,8 @@ __global__ __launch_bounds__(256) void k_init_cands_single(
     const uint8_t *d2, int n2, orbg_bounds b, const float *prev, int window,
     unsigned long long *topk, int32_t *topn)
 {
-    init_cands_block<LDSD>(k1, d1, n1, k2, d2, n2, b, prev, 2, window, topk, topn,
-                     blockIdx.x * 4 * INIT_QPW, n2);
+    init_cands_block<LDSD, INIT_QPW_SINGLE>(k1, d1, n1, k2, d2, n2, b, prev, 2, window, topk, topn,
+                                            blockIdx.x * 4 * INIT_QPW_SINGLE, n2);
 }
 
 // batch: F1 = frame f1[p] (its keypoints are vbPrevMatched), F2 = frame f2[p]
@@ -455,7 +460,7 @@ __global__ __launch_bounds__(256) void k_init_cands_pairs(
         return;
     }
     // vbPrevMatched = F1.mvKeysUn[i].pt: read x, y straight out of the keypoint records
-    init_cands_block<LDSD>(k1, desc + (size_t)a * fc * 32, n1, kps + (size_t)c * fc,
+    init_cands_block<LDSD, INIT_QPW>(k1, desc + (size_t)a * fc * 32, n1, kps + (size_t)c * fc,
                      desc + (size_t)c * fc * 32, n2, b, (const float *)k1,
                      (int)(sizeof(orbg_keypoint) / sizeof(float)), window,
                      topk + (size_t)p * fc * ORBG_MATCH_TOPK, topn + (size_t)p * fc, qbase, cap);
@@ -1058,13 +1063,13 @@ int launch_init_match_single(hipStream_t st, const orbg_keypoint *k1, const uint
     PL(prof, st, "init_cands",
        if (init_cands_lds(std::max(n2c, 1)))
            hipLaunchKernelGGL(k_init_cands_single<true>,
-                              dim3((nq + 4 * INIT_QPW - 1) / (4 * INIT_QPW)), dim3(256),
+                              dim3((nq + 4 * INIT_QPW_SINGLE - 1) / (4 * INIT_QPW_SINGLE)), dim3(256),
                               init_cands_keys_bytes(std::max(n2c, 1)) + (size_t)std::max(n2c, 1) * 32,
                               st, k1, d1, nq, k2, d2, n2c, b, prev, window,
                               (unsigned long long *)topk, topk_n);
        else
            hipLaunchKernelGGL(k_init_cands_single<false>,
-                              dim3((nq + 4 * INIT_QPW - 1) / (4 * INIT_QPW)), dim3(256),
+                              dim3((nq + 4 * INIT_QPW_SINGLE - 1) / (4 * INIT_QPW_SINGLE)), dim3(256),
                               init_cands_keys_bytes(std::max(n2c, 1)), st, k1, d1, nq, k2, d2, n2c,
                               b, prev, window, (unsigned long long *)topk, topk_n));
     PL(prof, st, "init_resolve",
