@@ -277,9 +277,16 @@ __global__ __launch_bounds__(OCT_T) void k_octree_lds(
     const uint2 *ckp = cell_kp + ((int64_t)f * g->ncells + lv.cell_base) * g->cell_cap;
     const int ncells = lv.ncells;
     // a level left to k_octree: noted in err_flag[2] (not an error; the single-frame path
-    // reruns a frame for which it skipped k_octree)
+    // reruns a frame for which it skipped k_octree) and left empty, so a consumer that runs
+    // before k_octree (or without it) never reads a stale count
+    auto leave_to_fallback = [&]() {
+        if (tid == 0) {
+            atomicOr(err_flag + 2, 1);
+            lvl_cnt[(int64_t)f * g->L + l] = 0;
+        }
+    };
     if (ncells + 1 > D.acap2) {
-        if (tid == 0) atomicOr(err_flag + 2, 1);
+        leave_to_fallback();
         return;
     }
     int n = 0;
@@ -291,7 +298,7 @@ __global__ __launch_bounds__(OCT_T) void k_octree_lds(
         n += tot;
     }
     if (n > D.kcap) {
-        if (tid == 0) atomicOr(err_flag + 2, 1);
+        leave_to_fallback();
         return;
     }
     if (tid == 0) V.aux[ncells] = V.coff[ncells] = (uint16_t)n;
