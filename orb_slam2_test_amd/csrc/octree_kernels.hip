@@ -36,6 +36,9 @@ namespace orbg {
 #ifndef OCT_PC_SMALL
 #define OCT_PC_SMALL 16
 #endif
+#ifndef OCT_PC_BATCH
+#define OCT_PC_BATCH 4
+#endif
 
 #define OCT_NBUCKET 16384  // counting-sort buckets: root (4 bits) + first 5 quadtree digits
 #define OCT_BSHIFT 18      // code >> 18 = root (4 bits) + digits 0..4
@@ -727,7 +730,7 @@ __global__ __launch_bounds__(OCT_T) void k_octree_lds(
     }
 }
 
-// small: B <= ORBG_SIDE_BLUR_B (OCT_PC_SMALL cells in flight per wave), else 4
+// small: B <= ORBG_SIDE_BLUR_B (OCT_PC_SMALL cells in flight per wave), else OCT_PC_BATCH
 hipError_t launch_octree_lds(bool small, dim3 grid, size_t lds, hipStream_t st, const OrbgGeom *g,
                              const int32_t *cell_cnt, const uint2 *cell_kp, uint32_t *lvl_kp,
                              uint16_t *lvl_idx, int32_t *lvl_cnt, int32_t *err_flag, OctLdsDims D)
@@ -736,14 +739,14 @@ hipError_t launch_octree_lds(bool small, dim3 grid, size_t lds, hipStream_t st, 
         hipLaunchKernelGGL(k_octree_lds<OCT_PC_SMALL>, grid, dim3(OCT_T), lds, st, g, cell_cnt,
                            cell_kp, lvl_kp, lvl_idx, lvl_cnt, err_flag, D);
     else
-        hipLaunchKernelGGL(k_octree_lds<4>, grid, dim3(OCT_T), lds, st, g, cell_cnt, cell_kp,
+        hipLaunchKernelGGL(k_octree_lds<OCT_PC_BATCH>, grid, dim3(OCT_T), lds, st, g, cell_cnt, cell_kp,
                            lvl_kp, lvl_idx, lvl_cnt, err_flag, D);
     return hipGetLastError();
 }
 
 hipError_t octree_lds_attr(int bytes)
 {
-    for (const void *k : {(const void *)k_octree_lds<4>, (const void *)k_octree_lds<OCT_PC_SMALL>}) {
+    for (const void *k : {(const void *)k_octree_lds<OCT_PC_BATCH>, (const void *)k_octree_lds<OCT_PC_SMALL>}) {
         const hipError_t e = hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, bytes);
         if (e != hipSuccess) return e;
     }

@@ -1245,8 +1245,16 @@ static int plan(orbg_ctx *c, int w, int h, int batch)
         // rest of a CU beside one of them (it runs concurrently on the quadtree stream), at
         // most OCT_KEY_CAP candidates
         c->oct_dims[1] = dims(1, G.L, 163840 / 3 - (int)sizeof(OctLdsHdr) - 64, true);
-        c->oct_dims[0] = dims(0, 1, 163840 - (int)oct_lds_bytes(c->oct_dims[1]) -
-                                        2 * (int)sizeof(OctLdsHdr) - 128, true);
+        // ORBG_OCT_L0_WPC=n (A/B): level 0 at n workgroups per CU.  n = 2 measured -14% octree,
+        // -0.2..0.7% per step at B = 1024, but caps level 0 at ~9.3k candidates against ~7.5k on
+        // the synthetic frames, and a level past the cap costs k_octree (n = 3: 6.4 ms per 1024
+        // frames, profiles/r05am_octree_ab.txt): not the default.
+        int l0_wpc = 1;
+        if (const char *e = getenv("ORBG_OCT_L0_WPC")) l0_wpc = std::max(1, atoi(e));
+        c->oct_dims[0] = l0_wpc > 1
+                             ? dims(0, 1, 163840 / l0_wpc - (int)sizeof(OctLdsHdr) - 64, true)
+                             : dims(0, 1, 163840 - (int)oct_lds_bytes(c->oct_dims[1]) -
+                                              2 * (int)sizeof(OctLdsHdr) - 128, true);
         for (int k = 0; k < 2; k++) {
             const size_t b = oct_lds_bytes(c->oct_dims[k]);
             if (b + sizeof(OctLdsHdr) > 160 * 1024)

@@ -143,6 +143,32 @@ def test_batch_equals_single_and_oracle(oracle):
         assert np.all(np.diff(k["octave"]) >= 0)
 
 
+def test_batch_level0_kcap_and_fallback(oracle, monkeypatch):
+    """ORBG_OCT_L0_WPC=2 sizes level 0 of k_octree_lds for two workgroups per CU (a smaller
+    candidate cap than the single-frame path's); a level past it (pure noise) goes to
+    k_octree.  Same outputs as the oracle and as one workgroup per CU (ORBG_OCT_L0_WPC=1)."""
+    import torch
+    B = 12
+    frames = S.sequence(B, 376, 1241, seed=91)
+    frames[5] = S.pure_noise(376, 1241)
+    d = torch.from_numpy(frames).cuda()
+    outs = {}
+    for wpc in ("1", "2"):
+        monkeypatch.setenv("ORBG_OCT_L0_WPC", wpc)
+        ext = ORBextractor(2000, 1.2, 8, 20, 7, max_batch=B)
+        ext.extract_batch_device(d.data_ptr(), B, 1241, 376)
+        ext.ctx.sync()
+        outs[wpc] = [ext.download_frame(f) for f in range(B)]
+    p = oracle.params()
+    for f in (0, 5, B - 1):
+        r = oracle.extract(p, frames[f])
+        k, desc = outs["2"][f]
+        assert np.array_equal(k, r["kps"]) and np.array_equal(desc, r["desc"]), f
+    for f in range(B):
+        assert np.array_equal(outs["1"][f][0], outs["2"][f][0]), f
+        assert np.array_equal(outs["1"][f][1], outs["2"][f][1]), f
+
+
 def test_batch_padded_pitch(oracle):
     import torch
     B, W, H, P = 4, 1241, 376, 1280
