@@ -13,6 +13,8 @@ struct OctLdsDims {
     int32_t nbw;        // bucket counter words: 512 * max roots (two u16 counters per word)
     int32_t uni_bytes;  // max(nbw * 4, 3 * acap * 8)
     int32_t tile_sort;  // winners to slots in (32-row x 128-column tile) order (ORBG_OD_SORT)
+    int32_t kmin;       // > 0: levels with <= kmin candidates are another launch's (untouched)
+    int32_t first;      // first of a split pair: a level past kcap is the second launch's
 };
 
 // static LDS header of k_octree_lds

@@ -284,7 +284,7 @@ __global__ __launch_bounds__(OCT_T) void k_octree_lds(
     // before k_octree (or without it) never reads a stale count
     auto leave_to_fallback = [&]() {
         if (tid == 0) {
-            atomicOr(err_flag + 2, 1);
+            if (!D.first) atomicOr(err_flag + 2, 1);
             lvl_cnt[(int64_t)f * g->L + l] = 0;
         }
     };
@@ -300,6 +300,7 @@ __global__ __launch_bounds__(OCT_T) void k_octree_lds(
         if (c < ncells) V.aux[c] = V.coff[c] = (uint16_t)min(off, 65535);
         n += tot;
     }
+    if (D.kmin > 0 && n <= D.kmin) return;  // the first launch of a split pair holds it
     if (n > D.kcap) {
         leave_to_fallback();
         return;

@@ -396,7 +396,7 @@ struct orbg_ctx {
     std::vector<int32_t> ftile_base;
     bool fr_ok = false;
     int fr_mode = 0;  // k_fast_rows opt-in (ORBG_FAST_ROWS=1) until it beats k_fast2
-    OctLdsDims oct_dims[2] = {};
+    OctLdsDims oct_dims[3] = {};  // levels 0, 1.., and level 0's batch first launch (kcap 0: none)
     // device
     OrbgGeom *d_geom = nullptr;
     OrbgCell *d_cells = nullptr;
@@ -1245,21 +1245,27 @@ static int plan(orbg_ctx *c, int w, int h, int batch)
         // rest of a CU beside one of them (it runs concurrently on the quadtree stream), at
         // most OCT_KEY_CAP candidates
         c->oct_dims[1] = dims(1, G.L, 163840 / 3 - (int)sizeof(OctLdsHdr) - 64, true);
-        // ORBG_OCT_L0_WPC=n (A/B): level 0 at n workgroups per CU.  n = 2 measured -14% octree,
-        // -0.2..0.7% per step at B = 1024, but caps level 0 at ~9.3k candidates against ~7.5k on
-        // the synthetic frames, and a level past the cap costs k_octree (n = 3: 6.4 ms per 1024
-        // frames, profiles/r05am_octree_ab.txt): not the default.
-        int l0_wpc = 1;
-        if (const char *e = getenv("ORBG_OCT_L0_WPC")) l0_wpc = std::max(1, atoi(e));
-        c->oct_dims[0] = l0_wpc > 1
-                             ? dims(0, 1, 163840 / l0_wpc - (int)sizeof(OctLdsHdr) - 64, true)
-                             : dims(0, 1, 163840 - (int)oct_lds_bytes(c->oct_dims[1]) -
-                                              2 * (int)sizeof(OctLdsHdr) - 128, true);
-        for (int k = 0; k < 2; k++) {
+        // Batches (B > ORBG_SIDE_BLUR_B) split level 0 in two launches: first at two workgroups
+        // per CU (room for ~9.3k candidates; one workgroup's chain of barriers leaves a CU
+        // idle), then the frames past that cap at one workgroup per CU.  ORBG_OCT_L0_WPC=n sets
+        // the first launch's workgroups per CU (1: no split).  dims[2] first: level 0's
+        // oct_kcap (k_octree's threshold) is the second launch's.
+        const int l0_wpc = getenv("ORBG_OCT_L0_WPC") ? std::max(1, atoi(getenv("ORBG_OCT_L0_WPC"))) : 2;
+        c->oct_dims[2] = OctLdsDims{};
+        if (l0_wpc > 1) {
+            c->oct_dims[2] = dims(0, 1, 163840 / l0_wpc - (int)sizeof(OctLdsHdr) - 64, true);
+            c->oct_dims[2].first = 1;
+        }
+        c->oct_dims[0] = dims(0, 1, 163840 - (int)oct_lds_bytes(c->oct_dims[1]) -
+                                        2 * (int)sizeof(OctLdsHdr) - 128, true);
+        if (c->oct_dims[2].kcap >= c->oct_dims[0].kcap) c->oct_dims[2].kcap = 0;
+        for (int k = 0; k < 3; k++) {
             const size_t b = oct_lds_bytes(c->oct_dims[k]);
             if (b + sizeof(OctLdsHdr) > 160 * 1024)
                 return set_err(ORBG_ENOTSUP, "k_octree_lds needs %zu LDS bytes", b);
-            if (b > 64 * 1024) HIPCHK(octree_lds_attr((int)b));
+            // the attribute is per kernel, not per context: the whole CU's room, so a later
+            // context (or the split pair's smaller launch) never lowers it under another's
+            if (b > 64 * 1024) HIPCHK(octree_lds_attr(160 * 1024 - (int)sizeof(OctLdsHdr)));
         }
     }
     G.keys_frame = key_off;
@@ -1647,6 +1653,23 @@ static hipError_t launch_pyramid(orbg_ctx *c, hipStream_t st, const uint8_t *d_i
 
 // GaussianBlur of levels [l0, l1) of every frame on `st`: k_blur2 (one wave per 244 x SEG
 // output tile, blur_kernels.hip)
+// level 0 of k_octree_lds: a batch's split pair (dims[2] then the frames past its cap at
+// dims[0]), else one launch
+static hipError_t launch_octree_l0(orbg_ctx *c, int B, hipStream_t st)
+{
+    const bool small = B <= ORBG_SIDE_BLUR_B;
+    OctLdsDims big = c->oct_dims[0];
+    if (!small && c->oct_dims[2].kcap > 0) {
+        const hipError_t e = launch_octree_lds(false, dim3(B, 1), oct_lds_bytes(c->oct_dims[2]), st,
+                                               c->d_geom, c->d_cell_cnt, c->d_cell_kp, c->d_lvl_kp,
+                                               c->d_lvl_idx, c->d_lvl_cnt, c->d_err, c->oct_dims[2]);
+        if (e != hipSuccess) return e;
+        big.kmin = c->oct_dims[2].kcap;
+    }
+    return launch_octree_lds(small, dim3(B, 1), oct_lds_bytes(big), st, c->d_geom, c->d_cell_cnt,
+                             c->d_cell_kp, c->d_lvl_kp, c->d_lvl_idx, c->d_lvl_cnt, c->d_err, big);
+}
+
 static hipError_t launch_blur_levels(orbg_ctx *c, hipStream_t st, const uint8_t *d_imgs, int B,
                                      int pitch, int64_t fs, int l0, int l1)
 {
@@ -1746,11 +1769,7 @@ static int launch_extract_pipe(orbg_ctx *c, const uint8_t *d_imgs, int B, int pi
     }
     hipStream_t st = c->ostream;  // the back (PROF_LAUNCH records on `st`)
     HIPCHK(hipStreamWaitEvent(st, c->ev_cells[s], 0));
-    PROF_LAUNCH(c, "octree",
-                launch_octree_lds(B <= ORBG_SIDE_BLUR_B, dim3(B, 1),
-                                      oct_lds_bytes(c->oct_dims[0]), st, c->d_geom, c->d_cell_cnt,
-                                   c->d_cell_kp, c->d_lvl_kp, c->d_lvl_idx, c->d_lvl_cnt,
-                                   c->d_err, c->oct_dims[0]));
+    PROF_LAUNCH(c, "octree", launch_octree_l0(c, B, st));
     if (G.L > 1)
         PROF_LAUNCH(c, "octree",
                     launch_octree_lds(B <= ORBG_SIDE_BLUR_B, dim3(B, G.L - 1),
@@ -1869,11 +1888,7 @@ static int launch_extract(orbg_ctx *c, const uint8_t *d_imgs, int B, int pitch, 
     {
         // PROF_LAUNCH records on `st`
         hipStream_t st = oct_mode ? c->ostream : c->stream;
-        PROF_LAUNCH(c, "octree",
-                    launch_octree_lds(B <= ORBG_SIDE_BLUR_B, dim3(B, 1),
-                                      oct_lds_bytes(c->oct_dims[0]), st, c->d_geom,
-                                       c->d_cell_cnt, c->d_cell_kp,
-                                       c->d_lvl_kp, c->d_lvl_idx, c->d_lvl_cnt, c->d_err, c->oct_dims[0]));
+        PROF_LAUNCH(c, "octree", launch_octree_l0(c, B, st));
         if (oct_mode == 2 && G.L > 1) {
             // levels 1.. need their FAST cells (launched on the extraction stream under fast0)
             if (fast0) {

@@ -144,16 +144,17 @@ def test_batch_equals_single_and_oracle(oracle):
 
 
 def test_batch_level0_kcap_and_fallback(oracle, monkeypatch):
-    """ORBG_OCT_L0_WPC=2 sizes level 0 of k_octree_lds for two workgroups per CU (a smaller
-    candidate cap than the single-frame path's); a level past it (pure noise) goes to
-    k_octree.  Same outputs as the oracle and as one workgroup per CU (ORBG_OCT_L0_WPC=1)."""
+    """Batches (B > 8) split level 0 of k_octree_lds: a first launch at ORBG_OCT_L0_WPC
+    workgroups per CU (default 2: a smaller candidate cap), then the frames past its cap at
+    one workgroup per CU; a level past that (pure noise) goes to k_octree.  Same outputs as
+    the oracle for 2 and 3 (3: most frames take the second launch) and as no split (1)."""
     import torch
     B = 12
     frames = S.sequence(B, 376, 1241, seed=91)
     frames[5] = S.pure_noise(376, 1241)
     d = torch.from_numpy(frames).cuda()
     outs = {}
-    for wpc in ("1", "2"):
+    for wpc in ("1", "2", "3"):
         monkeypatch.setenv("ORBG_OCT_L0_WPC", wpc)
         ext = ORBextractor(2000, 1.2, 8, 20, 7, max_batch=B)
         ext.extract_batch_device(d.data_ptr(), B, 1241, 376)
@@ -164,9 +165,10 @@ def test_batch_level0_kcap_and_fallback(oracle, monkeypatch):
         r = oracle.extract(p, frames[f])
         k, desc = outs["2"][f]
         assert np.array_equal(k, r["kps"]) and np.array_equal(desc, r["desc"]), f
-    for f in range(B):
-        assert np.array_equal(outs["1"][f][0], outs["2"][f][0]), f
-        assert np.array_equal(outs["1"][f][1], outs["2"][f][1]), f
+    for w in ("2", "3"):
+        for f in range(B):
+            assert np.array_equal(outs["1"][f][0], outs[w][f][0]), (w, f)
+            assert np.array_equal(outs["1"][f][1], outs[w][f][1]), (w, f)
 
 
 def test_batch_padded_pitch(oracle):
