@@ -44,8 +44,8 @@ METRIC_EXTRACT = "frames/sec ORBextractor only, 1241×376 2000feat 8lvl (configs
 
 
 # serial-pass PMC profiles of the bench lines (tools/round_prof.sh), copied from the run dirs
-PMC_MONO = "r05final3_pmc_kernels.json"
-PMC_STEREO = "r05final3_stereo_pmc_kernels.json"
+PMC_MONO = "r05final6_pmc_kernels.json"
+PMC_STEREO = "r05final6_stereo_pmc_kernels.json"
 
 
 def kernel_algo_bytes(name, B, npairs, ncand, nkp, launches_per_step, ndepth=0):
@@ -462,6 +462,14 @@ def main():
         if os.path.exists(pmc) and not args.extract_only:
             with open(pmc) as f:
                 pmc_all = json.load(f)
+        def pmc_hbm(name, lps):
+            # per bench launch (one PROF_LAUNCH may be several dispatches: octree's level-0
+            # pair), from the PMC run's per-step sum when it has one
+            e = pmc_all.get(name, {})
+            if e.get("hbm_bytes_per_step") and lps > 0:
+                return int(e["hbm_bytes_per_step"] / lps)
+            return e.get("hbm_bytes_per_launch")
+
         kstats = {}
         for name, (ms, n) in kern.items():
             lps = n / max(args.steps, 1)
@@ -471,7 +479,7 @@ def main():
                             "avg_launch_ms": round(avg, 5),
                             "algo_bytes_per_launch": None if ab is None else int(ab),
                             "achieved_GBps": None if ab is None else round(ab / (avg * 1e-3) / 1e9, 1),
-                            "hbm_bytes_per_launch": pmc_all.get(name, {}).get("hbm_bytes_per_launch")}
+                            "hbm_bytes_per_launch": pmc_hbm(name, lps)}
         roof = None
         if kstats:
             dom = max(kstats, key=lambda k: kstats[k]["ms_per_step"])
@@ -480,10 +488,10 @@ def main():
             pk = pmc_all.get(dom, {})
             roof = {"kernel": dom, "bound": "hbm", "achieved": ach, "peak": HBM_PEAK_GBS,
                     "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBS, 4) if ach else None,
-                    "traffic": pk.get("hbm_bytes_per_launch"),
-                    "traffic_over_algo": (round(pk["hbm_bytes_per_launch"] /
+                    "traffic": ks["hbm_bytes_per_launch"],
+                    "traffic_over_algo": (round(ks["hbm_bytes_per_launch"] /
                                                 ks["algo_bytes_per_launch"], 3)
-                                          if pk.get("hbm_bytes_per_launch") and
+                                          if ks["hbm_bytes_per_launch"] and
                                           ks["algo_bytes_per_launch"] else None),
                     "valu_frac": pk.get("valu_frac"), "lds_frac": pk.get("lds_frac"),
                     "pmc_source": os.path.relpath(pmc, ROOT) if pk else None,

@@ -281,7 +281,11 @@ static bool prof_skip(const char *name)
 {
     static const char *skip = getenv("ORBG_SKIP");
     static const int after = getenv("ORBG_SKIP_AFTER") ? atoi(getenv("ORBG_SKIP_AFTER")) : 0;
-    return skip && strstr(skip, name) && g_extract_batches.load() > after;
+    if (!skip || g_extract_batches.load() <= after) return false;
+    const size_t n = strlen(name);  // whole comma-separated names ("octree" != "octree_big")
+    for (const char *p = skip; (p = strstr(p, name)); p += n)
+        if ((p == skip || p[-1] == ',') && (p[n] == 0 || p[n] == ',')) return true;
+    return false;
 }
 #else
 static inline bool prof_skip(const char *) { return false; }
