@@ -281,8 +281,12 @@ __global__ __launch_bounds__(ORBG_OCT_THREADS) void k_octree(
     const uint2 *__restrict__ cell_kp, uint32_t *__restrict__ keys_all,
     uint32_t *__restrict__ knode_all, uint32_t *__restrict__ act_all,
     uint8_t *__restrict__ qk_all, int4 *__restrict__ nodes_all, uint32_t *__restrict__ lvl_kp,
-    uint16_t *__restrict__ lvl_idx, int32_t *__restrict__ lvl_cnt, int32_t *__restrict__ err_flag)
+    uint16_t *__restrict__ lvl_idx, int32_t *__restrict__ lvl_cnt, int32_t *__restrict__ err_flag,
+    int gate)
 {
+    // gate (pipelined batches): err_flag[2] was cleared before this batch's k_octree_lds
+    // launches, which set it for every level they leave here; clear = no level to take
+    if (gate && err_flag[2] == 0) return;
     __shared__ OctShared S;
     const int l = blockIdx.x, f = blockIdx.y, tid = threadIdx.x;
     const int nthr = blockDim.x;

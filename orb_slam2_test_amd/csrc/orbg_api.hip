@@ -34,7 +34,7 @@ __global__ void k_resize(const uint8_t *, int64_t, int, int, uint8_t *, int64_t,
                          const int2 *, const int2 *, int, int);
 __global__ void k_octree(const OrbgGeom *, const int32_t *, const uint2 *, uint32_t *,
                          uint32_t *, uint32_t *, uint8_t *, int4 *, uint32_t *, uint16_t *,
-                         int32_t *, int32_t *);
+                         int32_t *, int32_t *, int);
 hipError_t launch_octree_lds(bool small, dim3 grid, size_t lds, hipStream_t st, const OrbgGeom *g,
                              const int32_t *cell_cnt, const uint2 *cell_kp, uint32_t *lvl_kp,
                              uint16_t *lvl_idx, int32_t *lvl_cnt, int32_t *err_flag, OctLdsDims D);
@@ -1657,6 +1657,17 @@ static hipError_t launch_pyramid(orbg_ctx *c, hipStream_t st, const uint8_t *d_i
 
 // GaussianBlur of levels [l0, l1) of every frame on `st`: k_blur2 (one wave per 244 x SEG
 // output tile, blur_kernels.hip)
+// ORBG_OCT_GATE=0 (A/B): k_octree's workgroups of a pipelined batch scan their level even
+// when no k_octree_lds launch left one to them
+static bool oct_gate_enabled()
+{
+    static const bool on = [] {
+        const char *e = getenv("ORBG_OCT_GATE");
+        return !e || atoi(e) != 0;
+    }();
+    return on;
+}
+
 // level 0 of k_octree_lds: a batch's split pair (dims[2] then the frames past its cap at
 // dims[0]), else one launch
 static hipError_t launch_octree_l0(orbg_ctx *c, int B, hipStream_t st)
@@ -1773,6 +1784,9 @@ static int launch_extract_pipe(orbg_ctx *c, const uint8_t *d_imgs, int B, int pi
     }
     hipStream_t st = c->ostream;  // the back (PROF_LAUNCH records on `st`)
     HIPCHK(hipStreamWaitEvent(st, c->ev_cells[s], 0));
+    // d_err[2] cleared ahead of this batch's quadtree launches: k_octree's workgroups exit at
+    // once unless one of them left a level to it (the single-frame path clears it itself)
+    HIPCHK(hipMemsetAsync(c->d_err + 2, 0, sizeof(int32_t), st));
     PROF_LAUNCH(c, "octree", launch_octree_l0(c, B, st));
     if (G.L > 1)
         PROF_LAUNCH(c, "octree",
@@ -1784,7 +1798,7 @@ static int launch_extract_pipe(orbg_ctx *c, const uint8_t *d_imgs, int B, int pi
                 hipLaunchKernelGGL(k_octree, dim3(G.L, B), dim3(ORBG_OCT_THREADS), 0, st,
                                    c->d_geom, c->d_cell_cnt, c->d_cell_kp, c->d_keys, c->d_knode,
                                    c->d_act, c->d_qk, c->d_nodes, c->d_lvl_kp, c->d_lvl_idx, c->d_lvl_cnt,
-                                   c->d_err));
+                                   c->d_err, oct_gate_enabled() ? 1 : 0));
     HIPCHK(hipStreamWaitEvent(st, c->ev_front[s], 0));
     if (c->mat_pending[s]) {  // the matching of the batch before last reads output slot s
         HIPCHK(hipStreamWaitEvent(st, c->ev_mat[s], 0));
@@ -1879,7 +1893,7 @@ static int launch_extract(orbg_ctx *c, const uint8_t *d_imgs, int B, int pitch, 
                         hipLaunchKernelGGL(k_octree, dim3(G.L, B), dim3(ORBG_OCT_THREADS), 0, st,
                                            c->d_geom, c->d_cell_cnt, c->d_cell_kp, c->d_keys,
                                            c->d_knode, c->d_act, c->d_qk, c->d_nodes, c->d_lvl_kp,
-                                           c->d_lvl_idx, c->d_lvl_cnt, c->d_err));
+                                           c->d_lvl_idx, c->d_lvl_cnt, c->d_err, 0));
             HIPCHK(hipEventRecord(c->ev_big, st));
         }
     } else {
@@ -1929,7 +1943,7 @@ static int launch_extract(orbg_ctx *c, const uint8_t *d_imgs, int B, int pitch, 
                     hipLaunchKernelGGL(k_octree, dim3(G.L, B), dim3(ORBG_OCT_THREADS), 0, st,
                                        c->d_geom, c->d_cell_cnt, c->d_cell_kp, c->d_keys, c->d_knode,
                                        c->d_act, c->d_qk, c->d_nodes, c->d_lvl_kp, c->d_lvl_idx,
-                                       c->d_lvl_cnt, c->d_err));
+                                       c->d_lvl_cnt, c->d_err, 0));
     // per-frame outputs go to the other slot; wait until its last reader (matching of the
     // batch before last) is done
     if (c->mat_pending[s]) {
