@@ -15,6 +15,7 @@ struct OctLdsDims {
     int32_t tile_sort;  // winners to slots in (32-row x 128-column tile) order (ORBG_OD_SORT)
     int32_t kmin;       // > 0: levels with <= kmin candidates are another launch's (untouched)
     int32_t first;      // first of a split pair: a level past kcap is the second launch's
+                        // (flagged in err_flag[3])
 };
 
 // static LDS header of k_octree_lds

@@ -271,6 +271,9 @@ __global__ __launch_bounds__(OCT_T) void k_octree_lds(
     // latency-bound chain of barriers sharing the SIMDs with VALU-heavy waves: issue first
     __builtin_amdgcn_s_setprio(ORBG_OCT_PRIO);
 #endif
+    // the split pair's second launch: nothing to take unless the first flagged a level
+    // (err_flag[3], cleared ahead of the pair by launch_octree_l0)
+    if (D.kmin > 0 && err_flag[3] == 0) return;
     const int l = D.level0 + blockIdx.y, f = blockIdx.x, tid = threadIdx.x;
     const OrbgLevel &lv = g->lv[l];
     const int N = lv.nfeat, nIni = lv.nini;
@@ -284,7 +287,9 @@ __global__ __launch_bounds__(OCT_T) void k_octree_lds(
     // before k_octree (or without it) never reads a stale count
     auto leave_to_fallback = [&]() {
         if (tid == 0) {
-            if (!D.first) atomicOr(err_flag + 2, 1);
+            // the split pair's first launch flags err_flag[3] (its second launch runs only
+            // when set), every other launch err_flag[2]
+            atomicOr(err_flag + (D.first ? 3 : 2), 1);
             lvl_cnt[(int64_t)f * g->L + l] = 0;
         }
     };

@@ -1675,7 +1675,11 @@ static hipError_t launch_octree_l0(orbg_ctx *c, int B, hipStream_t st)
     const bool small = B <= ORBG_SIDE_BLUR_B;
     OctLdsDims big = c->oct_dims[0];
     if (!small && c->oct_dims[2].kcap > 0) {
-        const hipError_t e = launch_octree_lds(false, dim3(B, 1), oct_lds_bytes(c->oct_dims[2]), st,
+        // d_err[3]: set by the first launch for a level it leaves to the second, which exits
+        // at once while it is clear (ORBG_OCT_GATE=0: set, the second always scans)
+        hipError_t e = hipMemsetAsync(c->d_err + 3, oct_gate_enabled() ? 0 : 1, sizeof(int32_t), st);
+        if (e != hipSuccess) return e;
+        e = launch_octree_lds(false, dim3(B, 1), oct_lds_bytes(c->oct_dims[2]), st,
                                                c->d_geom, c->d_cell_cnt, c->d_cell_kp, c->d_lvl_kp,
                                                c->d_lvl_idx, c->d_lvl_cnt, c->d_err, c->oct_dims[2]);
         if (e != hipSuccess) return e;
