@@ -285,6 +285,13 @@ int orbg_batch_matches(orbg_ctx *ctx, int32_t *d_out, int32_t *frame_cap);
 /* host-side statistics of the last batch (synchronises): FAST candidates over all
  * cells/levels/frames and output keypoints over all frames (for bandwidth accounting) */
 int orbg_batch_stats(orbg_ctx *ctx, int64_t *ncandidates, int64_t *nkeypoints);
+/* the quadtree launch plan of the last planned image size (DistributeOctTree,
+ * ORBextractor.cc:668-951): the FAST-candidate caps of level 0's split pair of k_octree_lds
+ * launches in a batch (first_cap; 0 = no split) and of its single launch (level0_cap), and of
+ * the levels-1.. launch (upper_cap); a level with more candidates goes to the k_octree
+ * fallback.  ORBG_EINVAL before any extraction. */
+int orbg_get_quadtree_caps(const orbg_ctx *ctx, int32_t *first_cap, int32_t *level0_cap,
+                           int32_t *upper_cap);
 
 /* per-kernel timing with HIP events on the context stream (for bench roofline) */
 int orbg_profile_enable(orbg_ctx *ctx, int enable);
@@ -906,6 +913,73 @@ typedef struct {
 } orbg_lm_report;
 int orbg_ba_graph_optimize(orbg_ctx *ctx, orbg_ba_graph *graph, orbg_pose *d_poses,
                            double *d_points, int iterations, orbg_lm_report *report);
+
+/* orbg_ba_graph_optimize with g2o's force-stop flag and iteration actions
+ * (SparseOptimizer::setForceStopFlag(bool*), sparse_optimizer.h:184-188, installed by
+ * LocalBundleAdjustment at Optimizer.cc:700-701 and raised by LocalMapping when Tracking
+ * inserts a key frame; SparseOptimizer::addPostIterationAction).  Every member may be NULL:
+ *   force_stop      the caller's bool (1 byte, read volatile from the host), polled where
+ *                   g2o polls terminate(): before every iteration (sparse_optimizer.cpp:376)
+ *                   and after every LM trial (optimization_algorithm_levenberg.cpp:149); a
+ *                   raised flag ends the call after the current trial with the estimates of
+ *                   that point (an accepted trial's, or the pushed state after a rejected one),
+ *                   report->terminated = 3 unless the LM itself terminated;
+ *   post_iteration  called after each iteration (postIteration(i), sparse_optimizer.cpp:413,
+ *                   the terminating one included), on the calling thread;
+ *   post_trial      called after each trial's accept / reject (before the flag is polled);
+ *   d_last_chi2     device [nedge]: every edge's chi2 from the last error pass the call ran --
+ *                   what g2o's edges hold after optimize() (the last trial's _error, accepted or
+ *                   not; LocalBundleAdjustment's outlier tests read it, Optimizer.cc:879-901).
+ *                   Not written if no iteration ran (g2o computes no error then either).
+ * The hooks run on the calling thread between trials (device work may still be queued). */
+typedef struct {
+    const volatile uint8_t *force_stop;
+    void (*post_iteration)(void *user, int iteration);
+    void (*post_trial)(void *user, int iteration, int trial);
+    void *user;
+    double *d_last_chi2;
+} orbg_lm_control;
+int orbg_ba_graph_optimize_ctl(orbg_ctx *ctx, orbg_ba_graph *graph, orbg_pose *d_poses,
+                               double *d_points, int iterations, const orbg_lm_control *control,
+                               orbg_lm_report *report);
+
+/* The optimisation of Optimizer::LocalBundleAdjustment (Optimizer.cc:853-935) on one window,
+ * host arrays in and out, everything between on the device (the window's graph, estimates and
+ * LM in HBM):
+ *   optimize(5) (:856-857) with the force-stop flag (:700-701);
+ *   bDoMore = the flag is clear (:859-864);
+ *   if bDoMore, the outlier pass (:868-901): for every edge whose map point is not bad,
+ *     setLevel(1) if chi2 > 5.991 (mono) / 7.815 (stereo) or !isDepthPositive, and
+ *     setRobustKernel(0) -- chi2 as g2o's edges hold it (the last error pass of optimize(5),
+ *     orbg_lm_control.d_last_chi2), the depth test at the current estimates; then
+ *     optimize(10) over the level-0 edges (:904-905);
+ *   the vToErase test (:907-937): erase[e] = 1 for an edge whose map point is not bad with
+ *     chi2 > threshold or !isDepthPositive -- chi2 again as g2o holds it: the last error pass
+ *     of optimize(10) for its active edges, optimize(5)'s for the edges it did not optimise
+ *     (g2o's computeActiveErrors skips level-1 edges), the depth test at the final estimates.
+ * poses [npose] / points [npoint][3] (host) are the window (build_lba_window's order) and are
+ * overwritten with the optimised estimates (Optimizer.cc:949-978 reads them).  edges as
+ * orbg_ba_graph_create (active / robust as given: the reference starts with every edge at
+ * level 0 with a Huber kernel).  control (NULL: none): force_stop is the caller's bool* (the
+ * pbStopFlag both optimize calls poll), post_iteration / post_trial run in both optimize calls
+ * (iterations counted from 0 in each), d_last_chi2 is ignored.  point_is_bad
+ * (NULL: never): pMP->isBad(), called on the calling thread at the two places the reference
+ * calls it (the outlier pass, the vToErase test).  erase [nedge] (host, required).  The caller
+ * checks the flag before calling (Optimizer.cc:853-855 returns without any write-back); a flag
+ * raised before optimize(5)'s first iteration leaves chi2 at the initial estimates' (g2o has
+ * none: its _error is uninitialised then). */
+typedef struct {
+    orbg_lm_report lm[2];  /* optimize(5), optimize(10) (zeros when not run) */
+    int32_t do_more;       /* bDoMore: the outlier pass and optimize(10) ran */
+    int32_t n_outliers;    /* edges the outlier pass set to level 1 */
+    int32_t n_erase;       /* edges with erase[e] = 1 */
+    int32_t pad;
+} orbg_lba_report;
+int orbg_local_ba_optimize(orbg_ctx *ctx, orbg_pose *poses, int npose, double *points,
+                           int npoint, const orbg_edge *edges, int nedge,
+                           const orbg_lm_control *control,
+                           int (*point_is_bad)(void *user, int point), void *user,
+                           uint8_t *erase, orbg_lba_report *report);
 
 /* g2o's per-trial error pass for the two LBA edge types: SparseOptimizer::
  * computeActiveErrors (Thirdparty/g2o/g2o/core/sparse_optimizer.cpp:61-76, computeError

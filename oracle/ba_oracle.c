@@ -612,8 +612,19 @@ void orc_ba_update(orc_pose *poses, int npose, double *points, int npoint, const
         points[j] += dx_point[j];
 }
 
-int orc_ba_optimize(orc_pose *poses, int npose, double *points, int npoint, const orc_edge *edges,
-                    int nedge, int iterations, double report[6])
+/* optimize(iterations) with g2o's force-stop flag (SparseOptimizer::setForceStopFlag,
+ * sparse_optimizer.h:184-188) restated for tests: the flag is polled where g2o polls
+ * terminate() -- before every iteration (sparse_optimizer.cpp:376, after postIteration) and
+ * after every trial (optimization_algorithm_levenberg.cpp:149).  The test's flag is raised
+ * after trial stop_trial of iteration stop_it (stop_trial -1: after iteration stop_it's
+ * postIteration; stop_it -1: never; stop_it -2: already raised before the call).
+ * last_chi2 (NULL: not kept) receives every edge's chi2 from the last error pass the call
+ * ran (g2o's edges keep the _error of the last computeActiveErrors: the last trial's, accepted
+ * or not); untouched if no iteration ran.  report[6] as orc_ba_optimize, report[2] = 3 when the
+ * flag stopped it and nothing else did. */
+int orc_ba_optimize_ctl(orc_pose *poses, int npose, double *points, int npoint,
+                        const orc_edge *edges, int nedge, int iterations, int stop_it,
+                        int stop_trial, double *last_chi2, double report[6])
 {
     const size_t np = npose > 0 ? (size_t)npose : 1, nq = npoint > 0 ? (size_t)npoint : 1;
     const size_t ne = nedge > 0 ? (size_t)nedge : 1;
@@ -621,15 +632,19 @@ int orc_ba_optimize(orc_pose *poses, int npose, double *points, int npoint, cons
     double *hp = (double *)calloc(np * 36, 8), *bp = (double *)calloc(np * 6, 8);
     double *hq = (double *)calloc(nq * 9, 8), *bq = (double *)calloc(nq * 3, 8);
     double *dxp = (double *)calloc(np * 6, 8), *dxq = (double *)calloc(nq * 3, 8);
+    double *chi = (double *)calloc(ne, 8);
     orc_pose *sp = (orc_pose *)calloc(np, sizeof(orc_pose));
     double *sq = (double *)calloc(nq * 3, 8);
     double currentChi = 0, lambda = 0;
-    int ni = 2, nBad = 0, it = 0, trials = 0, term = 0;
-    for (it = 0; it < iterations; it++) {
-        if (it == 0)
-            currentChi = orc_ba_errors(poses, points, edges, nedge, NULL, NULL, NULL, NULL);
-        if (it == 0)
+    int ni = 2, nBad = 0, it = 0, trials = 0, term = 0, ran = 0;
+    int stop = stop_it == -2;
+    report[3] = 0;
+    for (it = 0; it < iterations && !stop; it++) {
+        if (it == 0) {
+            currentChi = orc_ba_errors(poses, points, edges, nedge, NULL, chi, NULL, NULL);
             report[3] = currentChi;
+        }
+        ran = 1;
         const double iniChi = currentChi;
         orc_ba_linearize(poses, npose, points, npoint, edges, nedge, eo, hp, bp, hq, bq);
         if (it == 0) {
@@ -653,7 +668,7 @@ int orc_ba_optimize(orc_pose *poses, int npose, double *points, int npoint, cons
             const int ok2 = orc_ba_schur_solve(poses, npose, npoint, edges, nedge, eo, hp, bp, hq,
                                                bq, lambda, dxp, dxq);
             orc_ba_update(poses, npose, points, npoint, dxp, dxq);
-            double tempChi = orc_ba_errors(poses, points, edges, nedge, NULL, NULL, NULL, NULL);
+            double tempChi = orc_ba_errors(poses, points, edges, nedge, NULL, chi, NULL, NULL);
             if (!ok2)
                 tempChi = DBL_MAX;
             rho = currentChi - tempChi;
@@ -683,24 +698,36 @@ int orc_ba_optimize(orc_pose *poses, int npose, double *points, int npoint, cons
                 memcpy(points, sq, (size_t)npoint * 24);
             }
             qmax++;
-        } while (rho < 0 && qmax < 10);
+            if (it == stop_it && qmax - 1 == stop_trial)
+                stop = 1;
+        } while (rho < 0 && qmax < 10 && !stop);
+        int ok = 1;
         if (qmax == 10 || rho == 0) {
             term = 1;
-            it++;
-            break;
+            ok = 0;
+        } else {
+            if ((iniChi - currentChi) * 1e3 < iniChi)
+                nBad++;
+            else
+                nBad = 0;
+            if (nBad >= 3) {
+                term = 2;
+                ok = 0;
+            }
         }
-        if ((iniChi - currentChi) * 1e3 < iniChi)
-            nBad++;
-        else
-            nBad = 0;
-        if (nBad >= 3) {
-            term = 2;
+        if (it == stop_it && stop_trial == -1)
+            stop = 1;  /* postIteration(i) */
+        if (!ok) {
             it++;
             break;
         }
     }
-    if (iterations == 0)
+    if (!ran)
         report[3] = currentChi = orc_ba_errors(poses, points, edges, nedge, NULL, NULL, NULL, NULL);
+    else if (last_chi2)
+        memcpy(last_chi2, chi, (size_t)nedge * 8);
+    if (stop && !term)
+        term = 3;
     report[0] = it;
     report[1] = trials;
     report[2] = term;
@@ -713,7 +740,15 @@ int orc_ba_optimize(orc_pose *poses, int npose, double *points, int npoint, cons
     free(bq);
     free(dxp);
     free(dxq);
+    free(chi);
     free(sp);
     free(sq);
     return it;
+}
+
+int orc_ba_optimize(orc_pose *poses, int npose, double *points, int npoint, const orc_edge *edges,
+                    int nedge, int iterations, double report[6])
+{
+    return orc_ba_optimize_ctl(poses, npose, points, npoint, edges, nedge, iterations, -1, -1,
+                               NULL, report);
 }

@@ -508,6 +508,9 @@ void orc_ba_update(orc_pose *poses, int npose, double *points, int npoint, const
  * iterations), chi2 before, chi2 after, final lambda.  Returns the iterations run. */
 int orc_ba_optimize(orc_pose *poses, int npose, double *points, int npoint, const orc_edge *edges,
                     int nedge, int iterations, double report[6]);
+int orc_ba_optimize_ctl(orc_pose *poses, int npose, double *points, int npoint,
+                        const orc_edge *edges, int nedge, int iterations, int stop_it,
+                        int stop_trial, double *last_chi2, double report[6]);
 /* central-difference Jacobian of computeError (base_binary_edge.hpp:131-205, delta 1e-9) */
 void orc_ba_numeric_jacobian(const orc_pose *pose, const double *xyz, const orc_edge *e,
                              double jp[3][3], double jt[3][6]);

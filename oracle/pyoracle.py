@@ -194,6 +194,9 @@ def lib():
         L.orc_ba_update.argtypes = [vp, C.c_int, vp, C.c_int, vp, vp]
         L.orc_ba_optimize.argtypes = [vp, C.c_int, vp, C.c_int, vp, C.c_int, C.c_int, vp]
         L.orc_ba_optimize.restype = C.c_int
+        L.orc_ba_optimize_ctl.argtypes = [vp, C.c_int, vp, C.c_int, vp, C.c_int, C.c_int,
+                                          C.c_int, C.c_int, vp, vp]
+        L.orc_ba_optimize_ctl.restype = C.c_int
         L.orc_ba_errors.restype = C.c_double
         L.orc_ba_schur_solve.argtypes = [vp, C.c_int, C.c_int, vp, C.c_int, vp, vp, vp, vp, vp,
                                          C.c_double, vp, vp]
@@ -202,6 +205,7 @@ def lib():
         L.orc_track_direction.argtypes = [vp, vp, vp]
         L.orc_pose_optimization.argtypes = [vp, C.c_int, vp, vp, vp, vp, vp, vp]
         L.orc_se3_from_tcw.argtypes = [vp, vp, vp]
+        L.orc_se3_to_tcw.argtypes = [vp, vp, vp]
         L.orc_match_pose.argtypes = [vp, C.c_int, vp, C.c_int, vp, vp, C.c_float, vp, vp, vp]
         L.orc_search_by_projection_lastframe.argtypes = [vp, vp, vp, C.c_int, vp, vp, vp, vp,
                                                          vp, C.c_int, vp, C.c_float, C.c_int,
@@ -546,6 +550,15 @@ def match_pose(p, kps1, kps2, m12, cam, depth):
     return n, q, t
 
 
+def se3_to_tcw(q, t):
+    """Converter::toCvMat(SE3Quat) restated (orc_se3_to_tcw): rows 0..2 of the float pose."""
+    q = np.ascontiguousarray(q, np.float64)
+    t = np.ascontiguousarray(t, np.float64)
+    T = np.zeros(12, np.float32)
+    lib().orc_se3_to_tcw(_p(q), _p(t), _p(T))
+    return T
+
+
 def se3_from_tcw(Tcw):
     """Converter::toSE3Quat restated (orc_se3_from_tcw): rows 0..2 of a float pose ->
     (q (x, y, z, w) normalised, t)."""
@@ -616,6 +629,26 @@ def ba_optimize(poses, points, edges, iterations):
     rep = np.zeros(6)
     lib().orc_ba_optimize(_p(poses), len(poses), _p(points), len(points), _p(edges), len(edges),
                           int(iterations), _p(rep))
+    return poses, points, dict(iterations=int(rep[0]), trials=int(rep[1]),
+                               terminated=int(rep[2]), initial_chi2=rep[3], final_chi2=rep[4],
+                               **{"lambda": rep[5]})
+
+
+def ba_optimize_ctl(poses, points, edges, iterations, stop_it=-1, stop_trial=-1, last_chi2=None):
+    """optimize(iterations) with g2o's force-stop flag raised after trial `stop_trial` of
+    iteration `stop_it` (-1: after that iteration; stop_it -1: never, -2: before the call),
+    restated (orc_ba_optimize_ctl).  `last_chi2` (float64 [nedge], updated in place when an
+    iteration ran): the chi2 g2o's edges hold afterwards.  Returns (poses, points, report)."""
+    poses = np.array(poses, POSE_DTYPE)
+    points = np.array(points, np.float64)
+    edges = np.ascontiguousarray(edges, EDGE_DTYPE)
+    rep = np.zeros(6)
+    if last_chi2 is not None:
+        assert last_chi2.dtype == np.float64 and last_chi2.flags.c_contiguous
+        assert len(last_chi2) == len(edges)
+    lib().orc_ba_optimize_ctl(_p(poses), len(poses), _p(points), len(points), _p(edges),
+                              len(edges), int(iterations), int(stop_it), int(stop_trial),
+                              _p(last_chi2), _p(rep))
     return poses, points, dict(iterations=int(rep[0]), trials=int(rep[1]),
                                terminated=int(rep[2]), initial_chi2=rep[3], final_chi2=rep[4],
                                **{"lambda": rep[5]})

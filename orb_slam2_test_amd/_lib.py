@@ -92,6 +92,17 @@ class LmReport(C.Structure):
                 ("lam", C.c_double)]
 
 
+LM_POST_ITERATION = C.CFUNCTYPE(None, C.c_void_p, C.c_int)
+LM_POST_TRIAL = C.CFUNCTYPE(None, C.c_void_p, C.c_int, C.c_int)
+
+
+class LmControl(C.Structure):
+    """orbg_lm_control (include/orbg.h): g2o's force-stop flag and iteration actions."""
+    _fields_ = [("force_stop", C.c_void_p), ("post_iteration", LM_POST_ITERATION),
+                ("post_trial", LM_POST_TRIAL), ("user", C.c_void_p),
+                ("d_last_chi2", C.c_void_p)]
+
+
 class KeyFrames(C.Structure):
     """orbg_keyframes (include/orbg.h): a set of KeyFrames in device memory."""
     _fields_ = [("desc", C.c_void_p), ("kps", C.c_void_p), ("uright", C.c_void_p),
@@ -226,6 +237,7 @@ def lib():
         "orbg_download_stereo": (i32, [vp, i32, vp, vp, i32, vp]),
         "orbg_match_stream": (vp, [vp]),
         "orbg_batch_stats": (i32, [vp, P(C.c_int64), P(C.c_int64)]),
+        "orbg_get_quadtree_caps": (i32, [vp, P(i32), P(i32), P(i32)]),
         "orbg_profile_enable": (i32, [vp, i32]),
         "orbg_profile_read": (i32, [vp, i32, P(C.c_char_p), P(C.c_double), P(C.c_int64)]),
         "orbg_profile_reset": (i32, [vp]),
@@ -273,6 +285,7 @@ def lib():
         "orbg_ba_graph_set_robust": (i32, [vp, vp, vp]),
         "orbg_ba_update_device": (i32, [vp, vp, i32, vp, i32, vp, vp, vp, vp]),
         "orbg_ba_graph_optimize": (i32, [vp, vp, vp, vp, i32, P(LmReport)]),
+        "orbg_ba_graph_optimize_ctl": (i32, [vp, vp, vp, vp, i32, P(LmControl), P(LmReport)]),
         "orbg_search_for_triangulation": (i32, [vp, P(KeyFrame), P(KeyFrame), vp, i32, i32, vp,
                                                 P(i32)]),
         "orbg_search_for_triangulation_batch_device": (i32, [vp, P(KeyFrames), i32, vp, vp, vp,
@@ -427,6 +440,14 @@ class Context:
         a, b = C.c_int64(), C.c_int64()
         check(self._L.orbg_batch_stats(self.handle, C.byref(a), C.byref(b)), "orbg_batch_stats")
         return a.value, b.value
+
+    def quadtree_caps(self):
+        """(first_cap, level0_cap, upper_cap) of the planned image size
+        (orbg_get_quadtree_caps): the k_octree_lds candidate caps; past them, k_octree."""
+        a, b, c = C.c_int32(), C.c_int32(), C.c_int32()
+        check(self._L.orbg_get_quadtree_caps(self.handle, C.byref(a), C.byref(b), C.byref(c)),
+              "orbg_get_quadtree_caps")
+        return a.value, b.value, c.value
 
     def stereo_summary(self, d_out_ptr):
         check(self._L.orbg_stereo_summary(self.handle, C.c_void_p(d_out_ptr)),

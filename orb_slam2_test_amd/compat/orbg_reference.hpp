@@ -40,6 +40,9 @@
 //                                      (LbaWindow), and BlockSolver<6,3>::buildSystem's block
 //                                      layout of the linearised system (block_solver.hpp:
 //                                      502-560, G2oBlockSystem)
+//   LocalBundleAdjustment ............ Optimizer.cc:633-979 (include/Optimizer.h:45): the
+//                                      whole function, its LM on the device
+//                                      (orbg_local_ba_optimize), pbStopFlag honoured
 #pragma once
 
 #include <algorithm>
@@ -47,6 +50,7 @@
 #include <cstring>
 #include <list>
 #include <map>
+#include <mutex>
 #include <set>
 #include <type_traits>
 #include <vector>
@@ -738,6 +742,122 @@ G2oBlockSystem linearize_lba_window(orbg_ctx *ctx, const Window &w)
             for (int c = 0; c < 3; c++) blk[c * 6 + r] += o.hpl[c][r];
     }
     return g;
+}
+
+// Converter::toCvMat(SE3Quat) (Converter.cc:49-53, 63-71): to_homogeneous_matrix (Eigen's
+// QuaternionBase::toRotationMatrix, se3quat.h:270-278), every element cast to float -- the
+// arithmetic of oracle/pose_oracle.c orc_se3_to_tcw
+inline void tcw_of(const orbg_pose &p, float T[12])
+{
+    const double *q = p.q;
+    const double tx = 2 * q[0], ty = 2 * q[1], tz = 2 * q[2];
+    const double twx = tx * q[3], twy = ty * q[3], twz = tz * q[3];
+    const double txx = tx * q[0], txy = ty * q[0], txz = tz * q[0];
+    const double tyy = ty * q[1], tyz = tz * q[1], tzz = tz * q[2];
+    const double R[3][3] = {{1 - (tyy + tzz), txy - twz, txz + twy},
+                            {txy + twz, 1 - (txx + tzz), tyz - twx},
+                            {txz - twy, tyz + twx, 1 - (txx + tyy)}};
+    for (int i = 0; i < 3; i++) {
+        for (int j = 0; j < 3; j++) T[4 * i + j] = (float)R[i][j];
+        T[4 * i + 3] = (float)p.t[i];
+    }
+}
+
+// Optimizer::LocalBundleAdjustment(pKF, pbStopFlag, pMap) (Optimizer.cc:633-979) with the
+// optimisation on the device:
+//   the local key frames (pKF + its not-bad covisible key frames, mnBALocalForKF), local map
+//   points (mnBALocalForKF) and fixed cameras (mnBAFixedForKF) exactly as :635-683;
+//   the window (build_lba_window, :687-851); the stop check (:853-855: return, nothing
+//   written);
+//   optimize(5), the outlier pass, optimize(10) and the vToErase test in one call
+//   (orbg_local_ba_optimize: pbStopFlag polled where g2o polls terminate(), pMP->isBad()
+//   asked where the reference asks it);
+//   under pMap->mMutexMapUpdate: EraseMapPointMatch / EraseObservation of the erased
+//   observations (mono edges first, then stereo, as vToErase is filled :909-937), the local
+//   key frames' SetPose(Converter::toCvMat(SE3quat)) and the local map points' SetWorldPos +
+//   UpdateNormalAndDepth (:939-978).
+// hooks (tests: deterministic stops) are merged with pbStopFlag; report (may be NULL).
+template <class KeyFrameT, class MapT>
+void LocalBundleAdjustment(orbg_ctx *ctx, KeyFrameT *pKF, bool *pbStopFlag, MapT *pMap,
+                           const orbg_lm_control *hooks = nullptr,
+                           orbg_lba_report *report = nullptr)
+{
+    typedef typename std::remove_pointer<
+        typename decltype(pKF->GetMapPointMatches())::value_type>::type MapPointT;
+    typedef typename std::decay<decltype(pKF->GetPose())>::type MatT;
+    std::list<KeyFrameT *> lLocalKeyFrames;
+    lLocalKeyFrames.push_back(pKF);
+    pKF->mnBALocalForKF = pKF->mnId;
+    const std::vector<KeyFrameT *> vNeighKFs = pKF->GetVectorCovisibleKeyFrames();
+    for (KeyFrameT *pKFi : vNeighKFs) {
+        pKFi->mnBALocalForKF = pKF->mnId;
+        if (!pKFi->isBad()) lLocalKeyFrames.push_back(pKFi);
+    }
+    std::list<MapPointT *> lLocalMapPoints;
+    for (KeyFrameT *pKFi : lLocalKeyFrames) {
+        const std::vector<MapPointT *> vpMPs = pKFi->GetMapPointMatches();
+        for (MapPointT *pMP : vpMPs)
+            if (pMP && !pMP->isBad() && pMP->mnBALocalForKF != pKF->mnId) {
+                lLocalMapPoints.push_back(pMP);
+                pMP->mnBALocalForKF = pKF->mnId;
+            }
+    }
+    std::list<KeyFrameT *> lFixedCameras;
+    for (MapPointT *pMP : lLocalMapPoints) {
+        const auto observations = pMP->GetObservations();
+        for (const auto &obs : observations) {
+            KeyFrameT *pKFi = obs.first;
+            if (pKFi->mnBALocalForKF != pKF->mnId && pKFi->mnBAFixedForKF != pKF->mnId) {
+                pKFi->mnBAFixedForKF = pKF->mnId;
+                if (!pKFi->isBad()) lFixedCameras.push_back(pKFi);
+            }
+        }
+    }
+    auto w = build_lba_window(lLocalKeyFrames, lFixedCameras, lLocalMapPoints);
+    if (pbStopFlag && *pbStopFlag) return;
+    orbg_lm_control K;
+    std::memset(&K, 0, sizeof(K));
+    if (hooks) K = *hooks;
+    K.force_stop = reinterpret_cast<const volatile uint8_t *>(pbStopFlag);
+    K.d_last_chi2 = nullptr;
+    const size_t ne = w.edges.size();
+    std::vector<uint8_t> erase(ne + 1, 0);
+    struct Bad {
+        static int point(void *u, int pt)
+        {
+            return (*static_cast<const std::vector<MapPointT *> *>(u))[pt]->isBad() ? 1 : 0;
+        }
+    };
+    orbg_lba_report rep;
+    check(orbg_local_ba_optimize(ctx, w.poses.data(), (int)w.poses.size(), w.points.data(),
+                                 (int)(w.points.size() / 3), w.edges.data(), (int)ne, &K,
+                                 &Bad::point, &w.mps, erase.data(), &rep),
+          "orbg_local_ba_optimize");
+    if (report) *report = rep;
+    std::unique_lock<std::mutex> lock(pMap->mMutexMapUpdate);
+    for (int pass = 0; pass < 2; pass++)  // vpEdgesMono, then vpEdgesStereo
+        for (size_t e = 0; e < ne; e++) {
+            if (w.edges[e].stereo != pass || !erase[e]) continue;
+            KeyFrameT *pKFi = w.kfs[w.edges[e].pose];
+            MapPointT *pMPi = w.mps[w.edges[e].point];
+            pKFi->EraseMapPointMatch(pMPi);
+            pMPi->EraseObservation(pKFi);
+        }
+    const size_t nlocal = lLocalKeyFrames.size();  // the window's first poses
+    for (size_t i = 0; i < nlocal; i++) {
+        float T[12];
+        tcw_of(w.poses[i], T);
+        MatT pose = MatT::eye(4, 4, 5 /* CV_32F */);
+        for (int r = 0; r < 3; r++)
+            for (int c = 0; c < 4; c++) pose.template at<float>(r, c) = T[4 * r + c];
+        w.kfs[i]->SetPose(pose);
+    }
+    for (size_t j = 0; j < w.mps.size(); j++) {
+        MatT X(3, 1, 5 /* CV_32F */);
+        for (int c = 0; c < 3; c++) X.template at<float>(c) = (float)w.points[3 * j + c];
+        w.mps[j]->SetWorldPos(X);
+        w.mps[j]->UpdateNormalAndDepth();
+    }
 }
 
 // ---------------------------------------------------------------------------

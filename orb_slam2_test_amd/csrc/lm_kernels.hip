@@ -26,12 +26,13 @@ namespace orbg {
 #define LM_RG 64   // reduction workgroups
 #define LM_RT 256  // threads per reduction workgroup
 
-__global__ __launch_bounds__(256) void k_ba_update(const orbg_pose *__restrict__ poses, int npose,
-                                                   const double *__restrict__ points, int npoint,
+// pout / qout may alias poses / points (the LM updates in place, orbg.h): no __restrict__ on
+// those pairs; each thread reads its element before writing it
+__global__ __launch_bounds__(256) void k_ba_update(const orbg_pose *poses, int npose,
+                                                   const double *points, int npoint,
                                                    const double *__restrict__ dxp,
                                                    const double *__restrict__ dxq,
-                                                   orbg_pose *__restrict__ pout,
-                                                   double *__restrict__ qout)
+                                                   orbg_pose *pout, double *qout)
 {
     const int t = blockIdx.x * blockDim.x + threadIdx.x;
     if (t < npose) {

@@ -16,6 +16,9 @@ struct OctLdsDims {
     int32_t kmin;       // > 0: levels with <= kmin candidates are another launch's (untouched)
     int32_t first;      // first of a split pair: a level past kcap is the second launch's
                         // (flagged in err_flag[3])
+    int32_t keep_cnt;   // 1: a level left to k_octree keeps its lvl_cnt entry (k_octree runs
+                        // concurrently and owns it: ORBG_BIG_SIDE), 0: zeroed for a consumer
+                        // that may run without k_octree
 };
 
 // static LDS header of k_octree_lds

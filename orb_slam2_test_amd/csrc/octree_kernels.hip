@@ -290,7 +290,7 @@ __global__ __launch_bounds__(OCT_T) void k_octree_lds(
             // the split pair's first launch flags err_flag[3] (its second launch runs only
             // when set), every other launch err_flag[2]
             atomicOr(err_flag + (D.first ? 3 : 2), 1);
-            lvl_cnt[(int64_t)f * g->L + l] = 0;
+            if (!D.keep_cnt) lvl_cnt[(int64_t)f * g->L + l] = 0;
         }
     };
     if (ncells + 1 > D.acap2) {

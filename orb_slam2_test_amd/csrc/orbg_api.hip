@@ -331,6 +331,11 @@ struct orbg_ctx {
     // extra stream's waits, profiles/r05q_single_ab.txt)
     bool big_side = false;
     hipEvent_t ev_big_a = nullptr, ev_big_b = nullptr, ev_big = nullptr;
+    // ORBG_OCT_GATE (read at orbg_create, default 1): the quadtree fallback launches of a
+    // pipelined batch (the split level-0 pair's second launch, k_octree) exit at once unless an
+    // earlier launch of the batch flagged a level for them (d_err[3], d_err[2]); 0 = they
+    // always scan (A/B, and the parity test's ungated twin)
+    bool oct_gate = true;
     bool serial = false;     // orbg_set_serial: no stream overlap (isolated kernel timing)
     // orbg_extract's single-frame hipGraphs: the whole frame (H2D of the pinned input, the
     // extraction's launches on the context and quadtree streams, k_pack_frame, D2H of the
@@ -1491,6 +1496,8 @@ extern "C" int orbg_create(int device, const orbg_params *p, orbg_ctx **out)
         }
         const char *bs = getenv("ORBG_BLUR_SIDE");
         c->blur_side = bs ? atoi(bs) != 0 : false;
+        const char *og = getenv("ORBG_OCT_GATE");
+        c->oct_gate = !og || atoi(og) != 0;
         const char *bg = getenv("ORBG_BIG_SIDE");
         c->big_side = c->fstream && (bg ? atoi(bg) != 0 : false);
         if (c->big_side)
@@ -1657,36 +1664,39 @@ static hipError_t launch_pyramid(orbg_ctx *c, hipStream_t st, const uint8_t *d_i
 
 // GaussianBlur of levels [l0, l1) of every frame on `st`: k_blur2 (one wave per 244 x SEG
 // output tile, blur_kernels.hip)
-// ORBG_OCT_GATE=0 (A/B): k_octree's workgroups of a pipelined batch scan their level even
-// when no k_octree_lds launch left one to them
-static bool oct_gate_enabled()
-{
-    static const bool on = [] {
-        const char *e = getenv("ORBG_OCT_GATE");
-        return !e || atoi(e) != 0;
-    }();
-    return on;
-}
-
 // level 0 of k_octree_lds: a batch's split pair (dims[2] then the frames past its cap at
-// dims[0]), else one launch
-static hipError_t launch_octree_l0(orbg_ctx *c, int B, hipStream_t st)
+// dims[0]), else one launch.  keep_cnt: k_octree runs concurrently (big_side) and owns the
+// lvl_cnt entries of the levels left to it
+static hipError_t launch_octree_l0(orbg_ctx *c, int B, hipStream_t st, bool keep_cnt = false)
 {
     const bool small = B <= ORBG_SIDE_BLUR_B;
     OctLdsDims big = c->oct_dims[0];
+    big.keep_cnt = keep_cnt;
     if (!small && c->oct_dims[2].kcap > 0) {
         // d_err[3]: set by the first launch for a level it leaves to the second, which exits
         // at once while it is clear (ORBG_OCT_GATE=0: set, the second always scans)
-        hipError_t e = hipMemsetAsync(c->d_err + 3, oct_gate_enabled() ? 0 : 1, sizeof(int32_t), st);
+        hipError_t e = hipMemsetAsync(c->d_err + 3, c->oct_gate ? 0 : 1, sizeof(int32_t), st);
         if (e != hipSuccess) return e;
-        e = launch_octree_lds(false, dim3(B, 1), oct_lds_bytes(c->oct_dims[2]), st,
-                                               c->d_geom, c->d_cell_cnt, c->d_cell_kp, c->d_lvl_kp,
-                                               c->d_lvl_idx, c->d_lvl_cnt, c->d_err, c->oct_dims[2]);
+        OctLdsDims first = c->oct_dims[2];
+        first.keep_cnt = keep_cnt;
+        e = launch_octree_lds(false, dim3(B, 1), oct_lds_bytes(first), st, c->d_geom,
+                              c->d_cell_cnt, c->d_cell_kp, c->d_lvl_kp, c->d_lvl_idx,
+                              c->d_lvl_cnt, c->d_err, first);
         if (e != hipSuccess) return e;
         big.kmin = c->oct_dims[2].kcap;
     }
     return launch_octree_lds(small, dim3(B, 1), oct_lds_bytes(big), st, c->d_geom, c->d_cell_cnt,
                              c->d_cell_kp, c->d_lvl_kp, c->d_lvl_idx, c->d_lvl_cnt, c->d_err, big);
+}
+
+// levels 1.. of k_octree_lds in one launch (keep_cnt as launch_octree_l0)
+static hipError_t launch_octree_upper(orbg_ctx *c, int B, hipStream_t st, bool keep_cnt = false)
+{
+    OctLdsDims d = c->oct_dims[1];
+    d.keep_cnt = keep_cnt;
+    return launch_octree_lds(B <= ORBG_SIDE_BLUR_B, dim3(B, c->geom.L - 1), oct_lds_bytes(d), st,
+                             c->d_geom, c->d_cell_cnt, c->d_cell_kp, c->d_lvl_kp, c->d_lvl_idx,
+                             c->d_lvl_cnt, c->d_err, d);
 }
 
 static hipError_t launch_blur_levels(orbg_ctx *c, hipStream_t st, const uint8_t *d_imgs, int B,
@@ -1792,17 +1802,12 @@ static int launch_extract_pipe(orbg_ctx *c, const uint8_t *d_imgs, int B, int pi
     // once unless one of them left a level to it (the single-frame path clears it itself)
     HIPCHK(hipMemsetAsync(c->d_err + 2, 0, sizeof(int32_t), st));
     PROF_LAUNCH(c, "octree", launch_octree_l0(c, B, st));
-    if (G.L > 1)
-        PROF_LAUNCH(c, "octree",
-                    launch_octree_lds(B <= ORBG_SIDE_BLUR_B, dim3(B, G.L - 1),
-                                      oct_lds_bytes(c->oct_dims[1]), st, c->d_geom,
-                                       c->d_cell_cnt, c->d_cell_kp,
-                                       c->d_lvl_kp, c->d_lvl_idx, c->d_lvl_cnt, c->d_err, c->oct_dims[1]));
+    if (G.L > 1) PROF_LAUNCH(c, "octree", launch_octree_upper(c, B, st));
     PROF_LAUNCH(c, "octree_big",
                 hipLaunchKernelGGL(k_octree, dim3(G.L, B), dim3(ORBG_OCT_THREADS), 0, st,
                                    c->d_geom, c->d_cell_cnt, c->d_cell_kp, c->d_keys, c->d_knode,
                                    c->d_act, c->d_qk, c->d_nodes, c->d_lvl_kp, c->d_lvl_idx, c->d_lvl_cnt,
-                                   c->d_err, oct_gate_enabled() ? 1 : 0));
+                                   c->d_err, c->oct_gate ? 1 : 0));
     HIPCHK(hipStreamWaitEvent(st, c->ev_front[s], 0));
     if (c->mat_pending[s]) {  // the matching of the batch before last reads output slot s
         HIPCHK(hipStreamWaitEvent(st, c->ev_mat[s], 0));
@@ -1910,18 +1915,14 @@ static int launch_extract(orbg_ctx *c, const uint8_t *d_imgs, int B, int pitch, 
     {
         // PROF_LAUNCH records on `st`
         hipStream_t st = oct_mode ? c->ostream : c->stream;
-        PROF_LAUNCH(c, "octree", launch_octree_l0(c, B, st));
+        PROF_LAUNCH(c, "octree", launch_octree_l0(c, B, st, big_side));
         if (oct_mode == 2 && G.L > 1) {
             // levels 1.. need their FAST cells (launched on the extraction stream under fast0)
             if (fast0) {
                 HIPCHK(hipEventRecord(c->ev_fast, c->stream));
                 HIPCHK(hipStreamWaitEvent(st, c->ev_fast, 0));
             }
-            PROF_LAUNCH(c, "octree",
-                        launch_octree_lds(B <= ORBG_SIDE_BLUR_B, dim3(B, G.L - 1),
-                                      oct_lds_bytes(c->oct_dims[1]), st, c->d_geom,
-                                           c->d_cell_cnt, c->d_cell_kp,
-                                           c->d_lvl_kp, c->d_lvl_idx, c->d_lvl_cnt, c->d_err, c->oct_dims[1]));
+            PROF_LAUNCH(c, "octree", launch_octree_upper(c, B, st, big_side));
         }
         if (blur0) HIPCHK(launch_blur_levels(c, st, d_imgs, B, pitch, fs, 0, 1));
         if (blur_side) {
@@ -1933,12 +1934,7 @@ static int launch_extract(orbg_ctx *c, const uint8_t *d_imgs, int B, int pitch, 
     if (!fused && !blur_side)
         HIPCHK(launch_blur_levels(c, st, d_imgs, B, pitch, fs, blur0 ? 1 : 0, G.L));
     else if (fz == 2 && !blur0) HIPCHK(launch_blur_levels(c, st, d_imgs, B, pitch, fs, 0, 1));
-    if (oct_mode != 2 && G.L > 1)
-        PROF_LAUNCH(c, "octree",
-                    launch_octree_lds(B <= ORBG_SIDE_BLUR_B, dim3(B, G.L - 1),
-                                      oct_lds_bytes(c->oct_dims[1]), st, c->d_geom,
-                                       c->d_cell_cnt, c->d_cell_kp,
-                                       c->d_lvl_kp, c->d_lvl_idx, c->d_lvl_cnt, c->d_err, c->oct_dims[1]));
+    if (oct_mode != 2 && G.L > 1) PROF_LAUNCH(c, "octree", launch_octree_upper(c, B, st, big_side));
     if (oct_mode) HIPCHK(hipStreamWaitEvent(st, c->ev_oct, 0));
     if (big_side)
         HIPCHK(hipStreamWaitEvent(st, c->ev_big, 0));
@@ -2181,6 +2177,9 @@ extern "C" int orbg_extract(orbg_ctx *c, const uint8_t *img, int w, int h, size_
     // optimistic: without k_octree when every level has an LDS quadtree launch (its early exits
     // flag d_err[2]; a flagged frame is extracted again with k_octree, ORBG_SKIP_BIG=0: never)
     const bool skip = dz && c->oct_dims[0].kcap > 0 && c->oct_dims[1].kcap > 0 && skip_big_enabled();
+    // the flag is this frame's alone: an earlier batch (non-pipelined batches never clear it)
+    // or an earlier rerun frame would otherwise force a needless second extraction
+    if (skip) HIPCHK(hipMemsetAsync(c->d_err + 2, 0, sizeof(int32_t), c->stream));
     c->hc_dst = dz;
     c->skip_big = skip;
     rc = launch_extract(c, c->d_img, 1, w, (int64_t)bytes);
@@ -2427,6 +2426,17 @@ extern "C" int orbg_set_serial(orbg_ctx *c, int enable)
     if (rc) return rc;
     c->serial = enable != 0;
     c->back_pending[0] = c->back_pending[1] = false;
+    return ORBG_OK;
+}
+
+extern "C" int orbg_get_quadtree_caps(const orbg_ctx *c, int32_t *first_cap, int32_t *level0_cap,
+                                      int32_t *upper_cap)
+{
+    if (!c) return set_err(ORBG_EINVAL, "ctx is NULL");
+    if (c->gw <= 0) return set_err(ORBG_EINVAL, "no image size planned yet");
+    if (first_cap) *first_cap = c->oct_dims[2].kcap;
+    if (level0_cap) *level0_cap = c->oct_dims[0].kcap;
+    if (upper_cap) *upper_cap = c->oct_dims[1].kcap;
     return ORBG_OK;
 }
 
@@ -3605,6 +3615,15 @@ extern "C" int orbg_ba_update_device(orbg_ctx *c, const orbg_pose *d_poses, int 
 extern "C" int orbg_ba_graph_optimize(orbg_ctx *c, orbg_ba_graph *g, orbg_pose *d_poses,
                                       double *d_points, int iterations, orbg_lm_report *rep)
 {
+    return orbg_ba_graph_optimize_ctl(c, g, d_poses, d_points, iterations, nullptr, rep);
+}
+
+// ... with g2o's force-stop flag (terminate(): before each iteration, sparse_optimizer.cpp:376,
+// and after each trial, optimization_algorithm_levenberg.cpp:149) and iteration actions
+extern "C" int orbg_ba_graph_optimize_ctl(orbg_ctx *c, orbg_ba_graph *g, orbg_pose *d_poses,
+                                          double *d_points, int iterations,
+                                          const orbg_lm_control *ctl, orbg_lm_report *rep)
+{
     if (!c || !g) return set_err(ORBG_EINVAL, "ctx / graph is NULL");
     if (g->device != c->device) return set_err(ORBG_EINVAL, "graph of another device");
     if (!g->schur_planned) return set_err(ORBG_EINVAL, "orbg_ba_graph_schur_plan not called");
@@ -3653,14 +3672,19 @@ extern "C" int orbg_ba_graph_optimize(orbg_ctx *c, orbg_ba_graph *g, orbg_pose *
         return ORBG_OK;
     };
     orbg_lm_report R{};
+    const orbg_lm_control C0{};
+    const orbg_lm_control &K = ctl ? *ctl : C0;
+    auto terminate = [&]() { return K.force_stop && *K.force_stop != 0; };
     double currentChi = 0.0, lambda = 0.0, hs[4];
     int ni = 2, nBad = 0;
-    for (int it = 0; it < iterations; it++) {
+    bool ran = false;
+    for (int it = 0; it < iterations && !terminate(); it++) {
         if (it == 0) {  // computeActiveErrors at the start (later: the last accepted trial's)
             if ((rc = chi2(sc)) || (rc = read(hs, 1))) return rc;
             currentChi = hs[0];
             R.initial_chi2 = currentChi;
         }
+        ran = true;
         const double iniChi = currentChi;
         if ((rc = orbg_ba_graph_build_system(c, g, d_poses, d_points, hpl, hp, bp, hq, bq))) return rc;
         if (it == 0) {  // computeLambdaInit: tau * max |H_jj| (before any lambda)
@@ -3718,27 +3742,152 @@ extern "C" int orbg_ba_graph_optimize(orbg_ctx *c, orbg_ba_graph *g, orbg_pose *
                                           hipMemcpyDeviceToDevice, st));
             }
             qmax++;
-        } while (rhoLM < 0 && qmax < 10);
+            if (K.post_trial) K.post_trial(K.user, it, qmax - 1);
+        } while (rhoLM < 0 && qmax < 10 && !terminate());
         R.iterations = it + 1;
         R.final_chi2 = currentChi;
         R.lambda = lambda;
+        bool ok = true;  // solve() returned OK (not Terminate)
         if (qmax == 10 || rhoLM == 0) {
             R.terminated = 1;
-            break;
+            ok = false;
+        } else {
+            if ((iniChi - currentChi) * 1e3 < iniChi)
+                nBad++;
+            else
+                nBad = 0;
+            if (nBad >= 3) {
+                R.terminated = 2;
+                ok = false;
+            }
         }
-        if ((iniChi - currentChi) * 1e3 < iniChi)
-            nBad++;
-        else
-            nBad = 0;
-        if (nBad >= 3) {
-            R.terminated = 2;
-            break;
-        }
+        if (K.post_iteration) K.post_iteration(K.user, it);
+        if (!ok) break;
     }
-    if (iterations == 0) {
+    if (!ran) {  // no iteration: the report's chi2 at the given estimates (g2o computes none)
         if ((rc = chi2(sc)) || (rc = read(hs, 1))) return rc;
         R.initial_chi2 = R.final_chi2 = hs[0];
+    } else if (K.d_last_chi2 && g->nedge) {
+        HIPCHK(hipMemcpyAsync(K.d_last_chi2, chi, (size_t)g->nedge * 8, hipMemcpyDeviceToDevice, st));
     }
+    if (R.terminated == 0 && terminate()) R.terminated = 3;
+    HIPCHK(hipStreamSynchronize(st));
+    if (rep) *rep = R;
+    return ORBG_OK;
+}
+
+// Optimizer::LocalBundleAdjustment's optimisation (Optimizer.cc:853-935) on one window: see
+// include/orbg.h.  The host takes the decisions the reference takes on the host (the flag, the
+// outlier thresholds, isBad), every pass over the edges runs on the device.
+extern "C" int orbg_local_ba_optimize(orbg_ctx *c, orbg_pose *poses, int npose, double *points,
+                                      int npoint, const orbg_edge *edges, int nedge,
+                                      const orbg_lm_control *control,
+                                      int (*point_is_bad)(void *user, int point), void *user,
+                                      uint8_t *erase, orbg_lba_report *rep)
+{
+    if (!c) return set_err(ORBG_EINVAL, "ctx is NULL");
+    if (npose < 0 || npoint < 0 || nedge < 0) return set_err(ORBG_EINVAL, "negative size");
+    if ((npose && !poses) || (npoint && !points) || (nedge && (!edges || !erase)))
+        return set_err(ORBG_EINVAL, "NULL array");
+    orbg_lba_report R{};
+    if (nedge == 0) {  // initializeOptimization of an empty graph fails: nothing optimised
+        if (rep) *rep = R;
+        return ORBG_OK;
+    }
+    HIPCHK(hipSetDevice(c->device));
+    orbg_ba_graph *g = nullptr;
+    int rc = orbg_ba_graph_create(c, edges, nedge, npose, npoint, &g);
+    if (rc) return rc;
+    uint8_t *dmem = nullptr;
+    struct Guard {
+        orbg_ba_graph *g;
+        uint8_t **m;
+        ~Guard()
+        {
+            if (*m) hipFree(*m);
+            if (g) orbg_ba_graph_destroy(g);
+        }
+    } guard{g, &dmem};
+    const size_t ne = (size_t)nedge, np = (size_t)std::max(npose, 1), nq = (size_t)std::max(npoint, 1);
+    const size_t o_p = 0, o_q = al256(np * sizeof(orbg_pose)), o_c5 = o_q + al256(nq * 24),
+                 o_c10 = o_c5 + al256(ne * 8), o_ce = o_c10 + al256(ne * 8),
+                 o_dk = o_ce + al256(ne * 8), o_end = o_dk + al256(ne);
+    HIPCHK(hipMalloc((void **)&dmem, o_end));
+    orbg_pose *d_poses = (orbg_pose *)(dmem + o_p);
+    double *d_points = (double *)(dmem + o_q), *d_c5 = (double *)(dmem + o_c5),
+           *d_c10 = (double *)(dmem + o_c10), *d_ce = (double *)(dmem + o_ce);
+    uint8_t *d_dk = dmem + o_dk;
+    hipStream_t st = c->stream;
+    if (npose)
+        HIPCHK(hipMemcpyAsync(d_poses, poses, (size_t)npose * sizeof(orbg_pose), hipMemcpyHostToDevice, st));
+    if (npoint)
+        HIPCHK(hipMemcpyAsync(d_points, points, (size_t)npoint * 24, hipMemcpyHostToDevice, st));
+    std::vector<uint8_t> fixed((size_t)std::max(npose, 1), 0), active(ne), robust(ne);
+    for (int i = 0; i < npose; i++) fixed[i] = poses[i].fixed ? 1 : 0;
+    for (size_t e = 0; e < ne; e++) {
+        active[e] = edges[e].active ? 1 : 0;
+        robust[e] = edges[e].robust ? 1 : 0;
+    }
+    if ((rc = orbg_ba_graph_schur_plan(c, g, fixed.data()))) return rc;
+    // the chi2 g2o's edges would hold if optimize(5) ran no iteration: the initial estimates'
+    if ((rc = orbg_ba_graph_errors(c, g, d_poses, d_points, nullptr, d_c5, nullptr, nullptr))) return rc;
+    orbg_lm_control K{};
+    if (control) K = *control;
+    const volatile uint8_t *force_stop = K.force_stop;
+    K.d_last_chi2 = d_c5;
+    if ((rc = orbg_ba_graph_optimize_ctl(c, g, d_poses, d_points, 5, &K, &R.lm[0]))) return rc;
+    auto stopped = [&]() { return force_stop && *force_stop != 0; };
+    auto bad = [&](int pt) { return point_is_bad && point_is_bad(user, pt) != 0; };
+    auto over = [&](size_t e, double chi2) {
+        return chi2 > (edges[e].stereo ? 7.815 : 5.991);
+    };
+    std::vector<double> chi(ne), tmp(ne);
+    std::vector<uint8_t> depth(ne);
+    auto depth_now = [&]() -> int {  // isDepthPositive at the current estimates
+        int r = orbg_ba_graph_errors(c, g, d_poses, d_points, nullptr, d_ce, nullptr, d_dk);
+        if (r) return r;
+        HIPCHK(hipMemcpyAsync(depth.data(), d_dk, ne, hipMemcpyDeviceToHost, st));
+        HIPCHK(hipStreamSynchronize(st));
+        return ORBG_OK;
+    };
+    HIPCHK(hipMemcpyAsync(chi.data(), d_c5, ne * 8, hipMemcpyDeviceToHost, st));
+    R.do_more = stopped() ? 0 : 1;
+    if (R.do_more) {
+        if ((rc = depth_now())) return rc;
+        for (size_t e = 0; e < ne; e++) {
+            if (bad(edges[e].point)) continue;
+            if (over(e, chi[e]) || !depth[e]) {
+                if (active[e]) R.n_outliers++;
+                active[e] = 0;  // setLevel(1)
+            }
+            robust[e] = 0;  // setRobustKernel(0)
+        }
+        // initializeOptimization(0): the level-0 edges (set_active rebuilds the Schur plan)
+        if ((rc = orbg_ba_graph_set_active(c, g, active.data())) ||
+            (rc = orbg_ba_graph_set_robust(c, g, robust.data())))
+            return rc;
+        K.d_last_chi2 = d_c10;
+        if ((rc = orbg_ba_graph_optimize_ctl(c, g, d_poses, d_points, 10, &K, &R.lm[1]))) return rc;
+        if (R.lm[1].trials > 0) {  // g2o recomputed the active edges' errors only
+            HIPCHK(hipMemcpyAsync(tmp.data(), d_c10, ne * 8, hipMemcpyDeviceToHost, st));
+            HIPCHK(hipStreamSynchronize(st));
+            for (size_t e = 0; e < ne; e++)
+                if (active[e]) chi[e] = tmp[e];
+        }
+    }
+    if ((rc = depth_now())) return rc;
+    for (size_t e = 0; e < ne; e++) {
+        erase[e] = 0;
+        if (bad(edges[e].point)) continue;
+        if (over(e, chi[e]) || !depth[e]) {
+            erase[e] = 1;
+            R.n_erase++;
+        }
+    }
+    if (npose)
+        HIPCHK(hipMemcpyAsync(poses, d_poses, (size_t)npose * sizeof(orbg_pose), hipMemcpyDeviceToHost, st));
+    if (npoint)
+        HIPCHK(hipMemcpyAsync(points, d_points, (size_t)npoint * 24, hipMemcpyDeviceToHost, st));
     HIPCHK(hipStreamSynchronize(st));
     if (rep) *rep = R;
     return ORBG_OK;

@@ -22,10 +22,13 @@
 #include <algorithm>
 #include <climits>
 #include <cstdlib>
+#include <mutex>
 
 #include "../../include/orbg.h"
 #include "orbg_device.h"
 #include "orbg_internal.h"
+
+#define ORBG_ST_MAX_DEV 64  // devices whose k_stereo_rows_match LDS attribute is cached
 
 #pragma clang fp contract(off)
 
@@ -899,12 +902,20 @@ int launch_stereo(hipStream_t st, const OrbgGeom &g, const orbg_keypoint *kps,
     if (el) lcap = std::max(0, std::min(lcap, atoi(el)));
     if (fused) {
         const size_t lds = head + (size_t)lcap * 2;
-        static size_t attr = 0;
-        if (attr < lds) {
-            if (hipFuncSetAttribute((const void *)k_stereo_rows_match,
-                                    hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) != hipSuccess)
-                return ORBG_EIO;
-            attr = lds;
+        // the attribute is per device: cached per device under a lock (contexts on several
+        // devices, or threads, share this function)
+        static std::mutex attr_mu;
+        static size_t attr[ORBG_ST_MAX_DEV] = {};
+        int dev = 0;
+        if (hipGetDevice(&dev) != hipSuccess || dev < 0) return ORBG_EIO;
+        {
+            std::lock_guard<std::mutex> lk(attr_mu);
+            if (dev >= ORBG_ST_MAX_DEV || attr[dev] < lds) {
+                if (hipFuncSetAttribute((const void *)k_stereo_rows_match,
+                                        hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) != hipSuccess)
+                    return ORBG_EIO;
+                if (dev < ORBG_ST_MAX_DEV) attr[dev] = lds;
+            }
         }
         prof_begin(prof, st, "stereo_match", &a);
         hipLaunchKernelGGL(k_stereo_rows_match, dim3(npairs), dim3(ST_FUSED_T), lds, st, G, kps,

@@ -252,11 +252,42 @@ class DeviceLBA:
         back per trial.  Needs schur_plan(fixed).  Returns the orbg_lm_report as a dict."""
         if self.graph is None:
             raise ValueError("optimize needs a DeviceLBA built with graph=True")
+        return self.optimize_ctl(iterations)
+
+    def optimize_ctl(self, iterations, stop_flag=None, post_iteration=None, post_trial=None,
+                     last_chi2=None):
+        """optimize(iterations) with g2o's force-stop flag (orbg_ba_graph_optimize_ctl):
+        `stop_flag` a one-byte host buffer (e.g. numpy uint8 [1], or ctypes c_bool) polled
+        before every iteration and after every trial as SparseOptimizer::terminate()
+        (sparse_optimizer.cpp:376, optimization_algorithm_levenberg.cpp:149);
+        `post_iteration(it)` / `post_trial(it, trial)` Python callbacks (they may raise the
+        flag); `last_chi2` a float64 CUDA tensor [nedge] that receives the chi2 g2o's edges
+        hold afterwards (the last trial's).  Returns the report as a dict (terminated 3 =
+        stopped by the flag)."""
+        if self.graph is None:
+            raise ValueError("optimize needs a DeviceLBA built with graph=True")
         rep = L.LmReport()
+        ctl = L.LmControl()
+        if stop_flag is not None:
+            if isinstance(stop_flag, np.ndarray):
+                assert stop_flag.dtype == np.uint8 and stop_flag.size >= 1
+                ctl.force_stop = stop_flag.ctypes.data
+            else:
+                ctl.force_stop = L.C.addressof(stop_flag)
+        # keep the thunks alive for the call
+        pi = L.LM_POST_ITERATION((lambda u, it: post_iteration(it)) if post_iteration else 0)
+        pt = L.LM_POST_TRIAL((lambda u, it, tr: post_trial(it, tr)) if post_trial else 0)
+        ctl.post_iteration, ctl.post_trial = pi, pt
+        if last_chi2 is not None:
+            import torch
+            assert last_chi2.dtype == torch.float64 and last_chi2.is_cuda
+            assert last_chi2.numel() == self.ne
+            ctl.d_last_chi2 = last_chi2.data_ptr()
         p = lambda t: L.C.c_void_p(t.data_ptr())  # noqa: E731
-        L.check(L.lib().orbg_ba_graph_optimize(self.ctx.handle, self.graph, p(self.d_poses),
-                                               p(self.d_points), int(iterations), L.C.byref(rep)),
-                "orbg_ba_graph_optimize")
+        L.check(L.lib().orbg_ba_graph_optimize_ctl(self.ctx.handle, self.graph, p(self.d_poses),
+                                                   p(self.d_points), int(iterations),
+                                                   L.C.byref(ctl), L.C.byref(rep)),
+                "orbg_ba_graph_optimize_ctl")
         return dict(iterations=rep.iterations, trials=rep.trials, terminated=rep.terminated,
                     initial_chi2=rep.initial_chi2, final_chi2=rep.final_chi2,
                     **{"lambda": rep.lam})

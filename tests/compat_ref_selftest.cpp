@@ -11,6 +11,10 @@
 //                                               scene read from <dir>, outputs written there
 //                                               (tests/test_compat_ref.py checks them against
 //                                               an independent window and the oracle)
+//   compat_ref_selftest lba_full <dir>          LocalBundleAdjustment(pKF, pbStopFlag, pMap)
+//                                               on such a scene, the map state after it
+//                                               written there (tests/test_compat_ref.py replays
+//                                               Optimizer.cc:633-979 through the oracle)
 #include <cmath>
 #include <cstdio>
 #include <algorithm>
@@ -18,6 +22,7 @@
 #include <fstream>
 #include <list>
 #include <map>
+#include <mutex>
 #include <set>
 #include <string>
 #include <thread>
@@ -68,6 +73,12 @@ struct MapPoint {  // include/MapPoint.h members the hot path reads
     }
     void AddObservation(KeyFrame *k, size_t idx) { obs[k] = idx; }
     void Replace(MapPoint *p);  // MapPoint.cc:196-240, below KeyFrame
+    // what LocalBundleAdjustment touches (Optimizer.cc:658-666, 944-978)
+    long unsigned int mnBALocalForKF = 0;
+    int n_update = 0;  // UpdateNormalAndDepth calls
+    void EraseObservation(KeyFrame *k) { obs.erase(k); }
+    void SetWorldPos(const cv::Mat &X) { pos = X.clone(); }
+    void UpdateNormalAndDepth() { n_update++; }
 };
 
 struct Frame {  // include/Frame.h
@@ -104,6 +115,16 @@ struct KeyFrame {  // include/KeyFrame.h
     int mnMinX = 0, mnMinY = 0, mnMaxX = 0, mnMaxY = 0;
     cv::Mat GetPose() const { return Tcw.clone(); }
     std::vector<MapPoint *> GetMapPointMatches() const { return mvpMapPoints; }
+    // what LocalBundleAdjustment touches (Optimizer.cc:638-683, 944-966)
+    long unsigned int mnBALocalForKF = 0, mnBAFixedForKF = 0;
+    std::vector<KeyFrame *> covisible;
+    std::vector<KeyFrame *> GetVectorCovisibleKeyFrames() const { return covisible; }
+    void SetPose(const cv::Mat &T) { Tcw = T.clone(); }
+    void EraseMapPointMatch(MapPoint *p)  // KeyFrame.cc: by the point's index in this frame
+    {
+        const int idx = p->GetIndexInKeyFrame(this);
+        if (idx >= 0) mvpMapPoints[idx] = nullptr;
+    }
     std::set<MapPoint *> GetMapPoints() const  // KeyFrame.cc: the non-NULL, non-bad slots
     {
         std::set<MapPoint *> s;
@@ -154,6 +175,10 @@ void MapPoint::Replace(MapPoint *p)
     obs.clear();
     bad = true;
 }
+
+struct Map {  // include/Map.h: the mutex LocalBundleAdjustment's write-back takes
+    std::mutex mMutexMapUpdate;
+};
 
 static std::vector<uint8_t> read_raw(const char *path, size_t n)
 {
@@ -266,9 +291,136 @@ static int lba_scene(const std::string &dir)
     return 0;
 }
 
+// Optimizer::LocalBundleAdjustment(pKF, pbStopFlag, pMap) through the drop-in on a scene from
+// <dir> (the lba_* files above; key frame 0 is pKF, the other listed-local ones and the ones in
+// neither list -- bad -- are its covisible key frames in array order; observation (j, i, k)
+// puts map point j in slot k of key frame i).  lba_ctl.i32 {stop_at, bad_at}: the flag is
+// raised at the stop_at-th post-iteration action of the run (counted over both optimize
+// calls; 0: never, -1: before the call), and the map points listed in lba_badpts.i32 turn bad
+// at the bad_at-th (0: never).  Written: lba_out_tcw.f32 (nkf x 12), lba_out_pos.f32 (nmp x 3),
+// lba_out_obs.i32 (the observations left, {map point, key frame, keypoint}), lba_out_marks.i64
+// (nkf x {mnBALocalForKF, mnBAFixedForKF}, then nmp x {mnBALocalForKF, UpdateNormalAndDepth
+// calls}), lba_out_report.bin (orbg_lba_report).
+static int lba_full(const std::string &dir)
+{
+    const std::vector<int32_t> meta = read_vec<int32_t>(dir + "/lba_meta.i32");
+    REQUIRE(meta.size() == 4);
+    const int nkf = meta[0], K = meta[1], nmp = meta[2], nobs = meta[3];
+    const std::vector<double> kfd = read_vec<double>(dir + "/lba_kf.f64");
+    const std::vector<float> kpd = read_vec<float>(dir + "/lba_kp.f32");
+    const std::vector<float> inv2 = read_vec<float>(dir + "/lba_inv2.f32");
+    const std::vector<double> mpd = read_vec<double>(dir + "/lba_mp.f64");
+    const std::vector<int32_t> obs = read_vec<int32_t>(dir + "/lba_obs.i32");
+    const std::vector<int32_t> ctl = read_vec<int32_t>(dir + "/lba_ctl.i32");
+    const std::vector<int32_t> badpts = read_vec<int32_t>(dir + "/lba_badpts.i32");
+    REQUIRE(ctl.size() == 2);
+    REQUIRE((int)kfd.size() == 20 * nkf && (int)kpd.size() == 4 * K * nkf);
+    REQUIRE((int)mpd.size() == 4 * nmp && (int)obs.size() == 3 * nobs);
+    std::vector<KeyFrame> kfs(nkf);
+    for (int i = 0; i < nkf; i++) {
+        const double *r = &kfd[20 * (size_t)i];
+        KeyFrame &k = kfs[i];
+        k.mnId = (long unsigned)r[0];
+        k.fx = (float)r[1];
+        k.fy = (float)r[2];
+        k.cx = (float)r[3];
+        k.cy = (float)r[4];
+        k.mbf = (float)r[5];
+        k.bad = r[6] != 0;
+        k.Tcw = cv::Mat::eye(4, 4, CV_32F);
+        for (int a = 0; a < 3; a++)
+            for (int c = 0; c < 4; c++) k.Tcw.at<float>(a, c) = (float)r[8 + 4 * a + c];
+        k.mvInvLevelSigma2 = inv2;
+        k.mvpMapPoints.assign(K, nullptr);
+        for (int j = 0; j < K; j++) {
+            const float *q = &kpd[4 * ((size_t)i * K + j)];
+            cv::KeyPoint kp;
+            kp.pt.x = q[0];
+            kp.pt.y = q[1];
+            kp.octave = (int)q[2];
+            k.mvKeysUn.push_back(kp);
+            k.mvuRight.push_back(q[3]);
+        }
+        if (i > 0 && r[7] != 0) kfs[0].covisible.push_back(&k);  // local (1) or bad (-1)
+    }
+    std::vector<MapPoint> mps(nmp);
+    for (int j = 0; j < nmp; j++) {
+        mps[j].mnId = (long unsigned)mpd[4 * (size_t)j];
+        mps[j].pos = cv::Mat(3, 1, CV_32F);
+        for (int c = 0; c < 3; c++) mps[j].pos.at<float>(c) = (float)mpd[4 * (size_t)j + 1 + c];
+    }
+    for (int o = 0; o < nobs; o++) {
+        MapPoint &mp = mps[obs[3 * o]];
+        KeyFrame &kf = kfs[obs[3 * o + 1]];
+        mp.obs[&kf] = (size_t)obs[3 * o + 2];
+        kf.mvpMapPoints[obs[3 * o + 2]] = &mp;
+    }
+    Map map;
+    bool stop = ctl[0] < 0;
+    struct Hook {
+        bool *stop;
+        int stop_at, bad_at, calls;
+        std::vector<MapPoint> *mps;
+        const std::vector<int32_t> *bad;
+        static void post_iteration(void *u, int)
+        {
+            Hook &h = *static_cast<Hook *>(u);
+            h.calls++;
+            if (h.calls == h.stop_at) *h.stop = true;
+            if (h.calls == h.bad_at)
+                for (int j : *h.bad) (*h.mps)[j].bad = true;
+        }
+    } hook{&stop, ctl[0], ctl[1], 0, &mps, &badpts};
+    orbg_lm_control hooks;
+    std::memset(&hooks, 0, sizeof(hooks));
+    hooks.post_iteration = &Hook::post_iteration;
+    hooks.user = &hook;
+    orbg_lba_report rep;
+    std::memset(&rep, 0, sizeof(rep));
+    orbg_compat::ref::LocalBundleAdjustment(orbg_compat::ref::default_ctx(), &kfs[0], &stop, &map,
+                                            &hooks, &rep);
+    std::vector<float> tcw, pos;
+    std::vector<int32_t> left;
+    std::vector<int64_t> marks;
+    for (int i = 0; i < nkf; i++) {
+        for (int a = 0; a < 3; a++)
+            for (int c = 0; c < 4; c++) tcw.push_back(kfs[i].Tcw.at<float>(a, c));
+        marks.push_back((int64_t)kfs[i].mnBALocalForKF);
+        marks.push_back((int64_t)kfs[i].mnBAFixedForKF);
+    }
+    for (int j = 0; j < nmp; j++) {
+        for (int c = 0; c < 3; c++) pos.push_back(mps[j].pos.at<float>(c));
+        for (const auto &o : mps[j].obs) {
+            const int i = (int)(o.first - kfs.data());
+            REQUIRE(kfs[i].mvpMapPoints[o.second] == &mps[j]);  // both sides erased together
+            left.push_back(j);
+            left.push_back(i);
+            left.push_back((int32_t)o.second);
+        }
+        marks.push_back((int64_t)mps[j].mnBALocalForKF);
+        marks.push_back((int64_t)mps[j].n_update);
+    }
+    for (int i = 0; i < nkf; i++)  // an erased match leaves no slot behind
+        for (int k = 0; k < K; k++) {
+            MapPoint *p = kfs[i].mvpMapPoints[k];
+            REQUIRE(!p || p->obs.count(&kfs[i]));
+        }
+    write_vec(dir + "/lba_out_tcw.f32", tcw.data(), tcw.size());
+    write_vec(dir + "/lba_out_pos.f32", pos.data(), pos.size());
+    write_vec(dir + "/lba_out_obs.i32", left.data(), left.size());
+    write_vec(dir + "/lba_out_marks.i64", marks.data(), marks.size());
+    write_vec(dir + "/lba_out_report.bin", (const uint8_t *)&rep, sizeof(rep));
+    std::printf("lba_full ok: optimize(5) %d it / %d trials, optimize(10) %d it, do_more %d, "
+                "%d outliers, %d erased, %d post-iteration calls\n",
+                rep.lm[0].iterations, rep.lm[0].trials, rep.lm[1].iterations, rep.do_more,
+                rep.n_outliers, rep.n_erase, hook.calls);
+    return 0;
+}
+
 int main(int argc, char **argv)
 {
     if (argc == 3 && std::string(argv[1]) == "lba") return lba_scene(argv[2]);
+    if (argc == 3 && std::string(argv[1]) == "lba_full") return lba_full(argv[2]);
     if (argc < 5) return 2;
     const int w = atoi(argv[3]), h = atoi(argv[4]);
     std::vector<uint8_t> im1 = read_raw(argv[1], (size_t)w * h), im2 = read_raw(argv[2], (size_t)w * h);

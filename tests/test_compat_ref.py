@@ -253,3 +253,190 @@ def test_lba_window_against_an_independent_window_and_the_oracle(tmp_path, oracl
     chi = float(np.fromfile(d / "g2o_chi2.f64")[0])
     assert abs(chi - rho0.sum()) <= 1e-9 * abs(rho0.sum())
     assert nf == 3
+
+
+def _ref_lba_lists(sc):
+    """Optimizer::LocalBundleAdjustment's lists (Optimizer.cc:635-683) for the lba_full scene:
+    pKF = key frame 0, its covisible key frames = the other local (1) and bad (-1) ones in array
+    order; a map point's observations in key-frame array order (std::map<KeyFrame*, size_t>
+    over one array).  Returns (local kfs, local map points, fixed cameras, the key frames whose
+    mnBALocalForKF / mnBAFixedForKF get set)."""
+    kf, obs = sc["kf"], sc["obs"]
+    slots, observers = {}, {}
+    for j, i, k in obs:
+        slots.setdefault(int(i), {})[int(k)] = int(j)
+        observers.setdefault(int(j), set()).add(int(i))
+    covis = [i for i in range(1, len(kf)) if kf[i, 7] != 0]
+    local = [0] + [i for i in covis if not kf[i, 6]]
+    marked_local = set([0] + covis)
+    lmps, seen = [], set()
+    for i in local:
+        for k in sorted(slots.get(i, {})):
+            j = slots[i][k]
+            if j not in seen:
+                seen.add(j)
+                lmps.append(j)
+    fixed, marked_fixed = [], set()
+    for j in lmps:
+        for i in sorted(observers[j]):
+            if i not in marked_local and i not in marked_fixed:
+                marked_fixed.add(i)
+                if not kf[i, 6]:
+                    fixed.append(i)
+    return local, lmps, fixed, marked_local, marked_fixed
+
+
+def _ref_lba_window(oracle, sc, local, lmps, fixed):
+    from orb_slam2_test_amd import _lib
+    kf, kp = sc["kf"], sc["kp"]
+    order = local + fixed
+    pose_of = {i: n for n, i in enumerate(order)}
+    poses = np.zeros(len(order), _lib.POSE_DTYPE)
+    for n, i in enumerate(order):
+        q, t = oracle.se3_from_tcw(kf[i, 8:].astype(np.float32))
+        poses[n]["q"], poses[n]["t"] = q, t
+        poses[n]["fixed"] = 1 if (i in fixed or kf[i, 0] == 0) else 0
+    points = sc["mp"][lmps, 1:].astype(np.float32).astype(np.float64)
+    edges = []
+    for pj, j in enumerate(lmps):
+        for (_, i, k) in sorted([tuple(o) for o in sc["obs"] if o[0] == j], key=lambda o: o[1]):
+            if kf[i, 6] or i not in pose_of:
+                continue
+            e = np.zeros((), _lib.EDGE_DTYPE)
+            e["point"], e["pose"] = pj, pose_of[i]
+            st = kp[i, k, 3] >= 0
+            e["stereo"], e["robust"], e["active"] = int(st), 1, 1
+            e["obs"][0], e["obs"][1] = kp[i, k, 0], kp[i, k, 1]
+            e["obs"][2] = kp[i, k, 3] if st else 0.0
+            e["inv_sigma2"] = sc["inv2"][int(kp[i, k, 2])]
+            e["fx"], e["fy"], e["cx"], e["cy"], e["bf"] = [np.float32(v) for v in kf[i, 1:6]]
+            e["huber_delta"] = np.float32(np.sqrt(7.815 if st else 5.991))
+            edges.append((e, i, k))
+    return order, poses, points, edges
+
+
+def _ref_lba_run(oracle, poses, points, edges, stop_at, bad_at, bad_window_pts):
+    """Optimizer.cc:853-937 restated over the oracle's LM (orc_ba_optimize_ctl): the
+    force-stop flag raised at the stop_at-th post-iteration action, map points turning bad at
+    the bad_at-th; g2o's edges keep the chi2 of their last error pass.  Returns (poses,
+    points, erase flags, report dict)."""
+    e0 = np.array([e for e, _, _ in edges])
+    thr = np.where(e0["stereo"] != 0, 7.815, 5.991)
+    chi = oracle.ba_errors(poses, points, e0)[1].copy()
+    s1 = stop_at - 1 if stop_at >= 1 else -1
+    p, q, r5 = oracle.ba_optimize_ctl(poses, points, e0, 5, stop_it=s1, last_chi2=chi)
+    it5 = r5["iterations"]
+    do_more = not (1 <= stop_at <= it5)
+    bad = np.zeros(len(e0), bool)
+    if 1 <= bad_at <= it5:
+        bad = np.isin(e0["point"], bad_window_pts)
+    r10 = None
+    n_out = 0
+    if do_more:
+        dok = oracle.ba_errors(p, q, e0)[3]
+        out = ~bad & ((chi > thr) | ~dok)
+        n_out = int(out.sum())
+        e2 = e0.copy()
+        e2["active"] = np.where(out, 0, 1)
+        e2["robust"] = np.where(bad, 1, 0)
+        c10 = chi.copy()
+        s2 = stop_at - 1 - it5 if stop_at > it5 else -1
+        p, q, r10 = oracle.ba_optimize_ctl(p, q, e2, 10, stop_it=s2, last_chi2=c10)
+        chi = np.where(e2["active"] != 0, c10, chi)
+        if 1 <= bad_at <= it5 + r10["iterations"]:
+            bad = np.isin(e0["point"], bad_window_pts)
+    dok = oracle.ba_errors(p, q, e0)[3]
+    erase = ~bad & ((chi > thr) | ~dok)
+    return p, q, erase, dict(r5=r5, r10=r10, do_more=do_more, n_out=n_out)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("stop_at,bad_at", [(0, 0), (3, 0), (8, 0), (-1, 0), (0, 1)])
+def test_local_bundle_adjustment_drop_in(tmp_path, oracle, stop_at, bad_at):
+    """Optimizer::LocalBundleAdjustment(pKF, pbStopFlag, pMap) through the compiled drop-in
+    (orbg_reference.hpp -> orbg_local_ba_optimize: the LM on the device) against the
+    reference's sequence replayed through the oracle (Optimizer.cc:633-979): the local / fixed
+    lists and their marks, optimize(5) -> the pbStopFlag check -> the outlier pass (setLevel(1),
+    setRobustKernel(0), pMP->isBad() skipped) -> optimize(10) -> vToErase -> the erased
+    observations and the write-back (SetPose(toCvMat(SE3Quat)) of the local key frames,
+    SetWorldPos + UpdateNormalAndDepth of the local map points).  The flag is raised after
+    post-iteration action stop_at (3: inside optimize(5), so bDoMore is false; 8: inside
+    optimize(10); -1: before the call, which returns at :853-855 with nothing written);
+    bad_at 1: map points turn bad after the first iteration."""
+    from orb_slam2_test_amd import _lib
+    exe = os.path.join(LIB, "compat_ref_selftest")
+    sc = _lba_scene(np.random.default_rng(2031))
+    d = tmp_path
+    np.array([len(sc["kf"]), sc["K"], len(sc["mp"]), len(sc["obs"])], np.int32).tofile(d / "lba_meta.i32")
+    sc["kf"].astype(np.float64).tofile(d / "lba_kf.f64")
+    sc["kp"].astype(np.float32).tofile(d / "lba_kp.f32")
+    sc["inv2"].tofile(d / "lba_inv2.f32")
+    sc["mp"].astype(np.float64).tofile(d / "lba_mp.f64")
+    sc["obs"].astype(np.int32).tofile(d / "lba_obs.i32")
+    local, lmps, fixed, mloc, mfix = _ref_lba_lists(sc)
+    badpts = np.array(lmps[::17][:6], np.int32)
+    np.array([stop_at, bad_at], np.int32).tofile(d / "lba_ctl.i32")
+    badpts.tofile(d / "lba_badpts.i32")
+    r = subprocess.run([exe, "lba_full", str(d)], capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0, (r.stdout + r.stderr)[-3000:]
+    nkf, nmp = len(sc["kf"]), len(sc["mp"])
+    tcw = np.fromfile(d / "lba_out_tcw.f32", np.float32).reshape(nkf, 12)
+    pos = np.fromfile(d / "lba_out_pos.f32", np.float32).reshape(nmp, 3)
+    left = {tuple(o) for o in np.fromfile(d / "lba_out_obs.i32", np.int32).reshape(-1, 3)}
+    marks = np.fromfile(d / "lba_out_marks.i64", np.int64)
+    kmarks, pmarks = marks[:2 * nkf].reshape(nkf, 2), marks[2 * nkf:].reshape(nmp, 2)
+    pid = int(sc["kf"][0, 0])
+    assert [i for i in range(nkf) if kmarks[i, 0] == pid] == sorted(mloc)
+    assert [i for i in range(nkf) if kmarks[i, 1] == pid] == sorted(mfix)
+    assert [j for j in range(nmp) if pmarks[j, 0] == pid] == sorted(lmps)
+    assert len(fixed) >= 1 and len(local) == 4
+    orig = {tuple(o) for o in sc["obs"]}
+    if stop_at == -1:  # Optimizer.cc:853-855: return before the optimisation, nothing written
+        assert left == orig and (pmarks[:, 1] == 0).all()
+        assert np.array_equal(tcw, sc["kf"][:, 8:].astype(np.float32))
+        assert np.array_equal(pos, sc["mp"][:, 1:].astype(np.float32))
+        return
+    rep = np.frombuffer((d / "lba_out_report.bin").read_bytes(), np.uint8)
+    assert len(rep) == 96  # orbg_lba_report: 2 x orbg_lm_report (40 B) + 4 int32
+    lm = np.frombuffer(rep[:80].tobytes(), np.int32).reshape(2, 10)
+    tail = np.frombuffer(rep[80:96].tobytes(), np.int32)
+    order, poses, points, edges = _ref_lba_window(oracle, sc, local, lmps, fixed)
+    win_bad = [lmps.index(j) for j in badpts]
+    rp, rq, erase, exp = _ref_lba_run(oracle, poses, points, edges, stop_at, bad_at, win_bad)
+    assert lm[0, 0] == exp["r5"]["iterations"] and lm[0, 1] == exp["r5"]["trials"]
+    assert lm[0, 2] == exp["r5"]["terminated"]
+    assert tail[0] == int(exp["do_more"]) and tail[1] == exp["n_out"]
+    if exp["do_more"]:
+        assert lm[1, 0] == exp["r10"]["iterations"] and lm[1, 1] == exp["r10"]["trials"]
+        assert lm[1, 2] == exp["r10"]["terminated"]
+    else:
+        assert lm[1, 0] == 0 and lm[1, 1] == 0
+    if stop_at == 3:
+        assert not exp["do_more"] and exp["r5"]["iterations"] == 3
+    if stop_at == 8:
+        assert exp["do_more"] and exp["r5"]["iterations"] == 5 and exp["r10"]["iterations"] == 3
+    # the erased observations: exactly the replay's vToErase
+    erased = {(j, i, k) for (e, i, k), x in zip(edges, erase) if x
+              for j in [lmps[int(e["point"])]]}
+    assert tail[2] == len(erased)
+    assert left == orig - erased
+    if stop_at == 0:
+        assert 0 < len(erased) < len(edges) and exp["n_out"] > 0
+    if bad_at:
+        be = {(lmps[int(e["point"])], i, k) for e, i, k in edges if int(e["point"]) in win_bad}
+        assert be and not (be & erased)
+    # write-back: local key frames and local map points, to the device LM's rounding (the
+    # same decisions; estimates within 1e-6 as tests/test_gpu_ba.py's LM comparisons)
+    for n, i in enumerate(order):
+        want = oracle.se3_to_tcw(rp[n]["q"], rp[n]["t"]) if n < len(local) \
+            else sc["kf"][i, 8:].astype(np.float32)
+        assert np.allclose(tcw[i], want, rtol=1e-5, atol=1e-5), (n, i)
+    for i in range(nkf):
+        if i not in order:
+            assert np.array_equal(tcw[i], sc["kf"][i, 8:].astype(np.float32))
+    want_pos = sc["mp"][:, 1:].astype(np.float32).copy()
+    want_pos[lmps] = rq.astype(np.float32)
+    assert np.allclose(pos, want_pos, rtol=1e-5, atol=1e-4)
+    assert [j for j in range(nmp) if pmarks[j, 1] == 1] == sorted(lmps)
+    moved = np.abs(pos[lmps] - sc["mp"][lmps, 1:].astype(np.float32)).max()
+    assert moved > 1e-3

@@ -517,3 +517,71 @@ def test_optimize_zero_iterations_and_no_free_pose(oracle):
     allfixed = poses.copy()
     allfixed["fixed"] = 1
     _lm_compare(oracle, allfixed, pts, edges, 3)
+
+
+@pytest.mark.parametrize("stop_it,stop_trial", [(-2, -1), (1, -1), (0, 0), (8, 1), (4, -1)])
+def test_optimize_force_stop_flag(oracle, stop_it, stop_trial):
+    """g2o's force-stop flag (SparseOptimizer::setForceStopFlag, polled by terminate() before
+    every iteration, sparse_optimizer.cpp:376, and after every LM trial,
+    optimization_algorithm_levenberg.cpp:149) on the device LM (orbg_ba_graph_optimize_ctl):
+    the flag raised by a post-iteration / post-trial action at (stop_it, stop_trial) stops the
+    device where the restated LM (orc_ba_optimize_ctl) stops: same iterations, trials,
+    terminated (3 = the flag), estimates to rounding, and the per-edge chi2 g2o's edges hold
+    afterwards (the last error pass's).  (-2: raised before the call: nothing runs.)  The
+    window's iteration 0 rejects its first trial and iteration 8 its first three, so (0, 0)
+    and (8, 1) stop the trial loop on a rejected trial: the pushed state is restored and the
+    edges keep the rejected trial's chi2, as g2o's do."""
+    import torch
+    from orb_slam2_test_amd.optimizer import DeviceLBA
+    from test_oracle_lm import _perturbed
+    poses, pts, edges = _perturbed(47, 1500, 2e-2, 0.5)
+    g = DeviceLBA(poses, pts, edges, graph=True)
+    g.schur_plan(poses["fixed"])
+    flag = np.zeros(1, np.uint8)
+    flag[0] = 1 if stop_it == -2 else 0
+    seen = []
+
+    def post_iteration(it):
+        seen.append(("it", it))
+        if it == stop_it and stop_trial == -1:
+            flag[0] = 1
+
+    def post_trial(it, tr):
+        seen.append(("tr", it, tr))
+        if it == stop_it and tr == stop_trial:
+            flag[0] = 1
+
+    sentinel = -7.0
+    last = torch.full((len(edges),), sentinel, dtype=torch.float64, device="cuda")
+    rep = g.optimize_ctl(10, stop_flag=flag, post_iteration=post_iteration, post_trial=post_trial,
+                         last_chi2=last)
+    gp, gq = g.estimates()
+    rchi = np.full(len(edges), sentinel)
+    rp, rq, rrep = oracle.ba_optimize_ctl(poses, pts, edges, 10, stop_it=stop_it,
+                                          stop_trial=stop_trial, last_chi2=rchi)
+    for k in ("iterations", "trials", "terminated"):
+        assert rep[k] == rrep[k], (k, rep, rrep)
+    its = [s[1] for s in seen if s[0] == "it"]
+    assert its == list(range(rrep["iterations"]))
+    assert sum(1 for s in seen if s[0] == "tr") == rrep["trials"]
+    got = last.cpu().numpy()
+    if stop_it == -2:
+        assert rep["iterations"] == 0 and rep["terminated"] == 3
+        assert (got == sentinel).all() and (rchi == sentinel).all()
+        assert gp.tobytes() == np.asarray(poses).tobytes()
+        return
+    assert rep["terminated"] == 3 and rep["iterations"] == stop_it + 1
+    assert rel(gq, rq) < 1e-6 and rel(gp["t"], rp["t"]) < 1e-6
+    assert rel(got, rchi) < 1e-6 and (got != sentinel).all()
+    if (stop_it, stop_trial) == (0, 0):  # rejected: the initial estimates, the trial's chi2
+        assert rep["trials"] == 1
+        assert gp.tobytes() == np.asarray(poses).tobytes() and np.array_equal(gq, pts)
+        chi_now = oracle.ba_errors(rp, rq, edges)[1]
+        assert rel(rchi, chi_now) > 1e-3
+    if (stop_it, stop_trial) == (8, 1):
+        assert rep["trials"] == 12  # iterations 0-7: 10 trials, then two of iteration 8
+    # a stopped optimize(10) = optimize(stop_it + 1) when the stop ends an iteration
+    if stop_trial == -1:
+        fp, fq, frep = oracle.ba_optimize(poses, pts, edges, stop_it + 1)
+        assert frep["trials"] == rrep["trials"]
+        assert fp.tobytes() == rp.tobytes() and np.asarray(fq).tobytes() == np.asarray(rq).tobytes()

@@ -53,3 +53,39 @@ def test_update_small_angle_branch(oracle):
     assert np.array_equal(q, pts)
     np.testing.assert_allclose(p["t"][free], poses["t"][free] + [0.25, -0.5, 1.0], rtol=0,
                                atol=1e-12)
+
+
+def test_force_stop_flag_restated(oracle):
+    """orc_ba_optimize_ctl: g2o's force-stop flag (terminate() before each iteration,
+    sparse_optimizer.cpp:376, and after each trial, optimization_algorithm_levenberg.cpp:149).
+    Raised after iteration k it equals optimize(k + 1) bit for bit; raised before the call
+    nothing runs; the edges keep the chi2 of the last error pass -- the final estimates' after
+    an accepted trial, the rejected trial's after a rejection (iteration 0 of this window
+    rejects its first trial)."""
+    poses, pts, edges = _perturbed(47, 600, 2e-2, 0.5)
+    a = oracle.ba_optimize(poses, pts, edges, 3)
+    c = np.full(len(edges), -1.0)
+    b = oracle.ba_optimize_ctl(poses, pts, edges, 10, stop_it=2, last_chi2=c)
+    assert a[0].tobytes() == b[0].tobytes() and np.array_equal(a[1], b[1])
+    assert b[2]["terminated"] == 3 and b[2]["iterations"] == 3
+    assert a[2]["trials"] == b[2]["trials"]
+    if a[2]["trials"] == b[2]["trials"] and a[2]["final_chi2"] == b[2]["final_chi2"]:
+        assert np.array_equal(c, oracle.ba_errors(b[0], b[1], edges)[1])
+    c0 = np.full(len(edges), -1.0)
+    z = oracle.ba_optimize_ctl(poses, pts, edges, 10, stop_it=-2, last_chi2=c0)
+    assert z[2]["iterations"] == 0 and z[2]["terminated"] == 3 and (c0 == -1.0).all()
+    assert z[0].tobytes() == np.asarray(poses).tobytes()
+    full = oracle.ba_optimize(poses, pts, edges, 10)
+    if full[2]["trials"] > full[2]["iterations"]:
+        # the first rejected trial: stop right after it
+        prev = 0
+        for k in range(10):
+            t = oracle.ba_optimize(poses, pts, edges, k + 1)[2]["trials"]
+            if t - prev > 1:
+                break
+            prev = t
+        c1 = np.full(len(edges), -1.0)
+        s = oracle.ba_optimize_ctl(poses, pts, edges, 10, stop_it=k, stop_trial=0, last_chi2=c1)
+        assert s[2]["iterations"] == k + 1 and s[2]["trials"] == prev + 1
+        here = oracle.ba_errors(s[0], s[1], edges)[1]
+        assert not np.array_equal(c1, here)  # the rejected trial's chi2, not the state's
