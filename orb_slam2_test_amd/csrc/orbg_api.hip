@@ -4196,6 +4196,7 @@ static size_t schur_layout(const SchurPlanHost &P, int nedge, uint8_t *base, Sch
     A.pt_off = (const int32_t *)take(P.pt_off.size() * 4);
     A.pt_edges = (const int32_t *)take(P.pt_edges.size() * 4);
     A.slot_point = (const int32_t *)take(P.slot_point.size() * 4);
+    A.slot_fidx = (const int32_t *)take(P.slot_fidx.size() * 4);
     A.edge_pose = (const int32_t *)take(P.edge_pose.size() * 4);
     A.blk_off = (const int32_t *)take(P.blk_off.size() * 4);
     A.blk_pairs = (const int2 *)take(P.blk_pairs.size() * 8);
@@ -4236,6 +4237,7 @@ static int schur_upload(const SchurPlanHost &P, const SchurArgs &A, hipStream_t 
         (rc = up(A.pt_off, P.pt_off.data(), P.pt_off.size() * 4)) ||
         (rc = up(A.pt_edges, P.pt_edges.data(), P.pt_edges.size() * 4)) ||
         (rc = up(A.slot_point, P.slot_point.data(), P.slot_point.size() * 4)) ||
+        (rc = up(A.slot_fidx, P.slot_fidx.data(), P.slot_fidx.size() * 4)) ||
         (rc = up(A.edge_pose, P.edge_pose.data(), P.edge_pose.size() * 4)) ||
         (rc = up(A.blk_off, P.blk_off.data(), P.blk_off.size() * 4)) ||
         (rc = up(A.blk_pairs, P.blk_pairs.data(), P.blk_pairs.size() * 8)) ||

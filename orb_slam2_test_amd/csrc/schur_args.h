@@ -25,8 +25,8 @@ namespace orbg {
 //     per-segment LDLT gives the same bits as one dense LDLT of the whole system.
 struct SchurPlanHost {
     int npose = 0, npoint = 0, nfree = 0, nblk = 0, nseg = 0, max_seg = 0;
-    std::vector<int32_t> pidx, free_pose, pt_off, pt_edges, slot_point, edge_pose, blk_off,
-        blk_i1, blk_i2, blk_seg, blk_order, pose_off, pose_slots, seg_lo;
+    std::vector<int32_t> pidx, free_pose, pt_off, pt_edges, slot_point, slot_fidx, edge_pose,
+        blk_off, blk_i1, blk_i2, blk_seg, blk_order, pose_off, pose_slots, seg_lo;
     std::vector<int2> blk_pairs;
     std::vector<int64_t> seg_soff;  // [nseg + 1] doubles before each segment's dense matrix
 };
@@ -42,6 +42,7 @@ struct SchurArgs {
     const int32_t *free_pose;          // [nfree] its pose
     const int32_t *pt_off, *pt_edges;  // active edges per point, ascending pose (CSR)
     const int32_t *slot_point;         // [nslot] the point of each slot of pt_edges
+    const int32_t *slot_fidx;          // [nslot] free index of the slot's pose, or -1 (fixed)
     int nslot;                         // = pt_off[npoint]
     const int32_t *edge_pose;          // [nedge] pose of each edge
     const int32_t *blk_off;            // [nblk + 1] (slot1, e2) pairs per upper block, landmark order

@@ -28,6 +28,7 @@
 
 #include <algorithm>
 #include <cmath>
+#include <cstdlib>
 
 #include "../../include/orbg.h"
 #include "orbg_device.h"
@@ -78,12 +79,16 @@ __global__ __launch_bounds__(256) void k_schur_points(SchurArgs A)
     __shared__ double2 rec[256 * SCHUR_REC / 2];
     const int tid = threadIdx.x, base = blockIdx.x * 256, a = base + tid;
     if (a == 0) *A.ok = 1;  // k_schur_ldlt clears it on a bad pivot (stream order)
+    // the dense systems zeroed here (block pairs without a shared landmark are never written
+    // by k_schur_blocks): no separate fill launch
+    for (int64_t z = a; z < A.s_total; z += (int64_t)gridDim.x * 256) A.S[z] = 0.0;
     double v[SCHUR_REC];
 #pragma unroll
     for (int k = 0; k < SCHUR_REC; k++) v[k] = 0.0;
-    if (a < A.nslot) {
+    const int fi = a < A.nslot ? A.slot_fidx[a] : -1;
+    if (fi >= 0) {
         const int e = A.pt_edges[a];
-        if (A.pidx[A.edge_pose[e]] >= 0) {
+        {
             double d[9], db[3];
             schur_dinv(A, A.slot_point[a], d, db);
             const double *h = A.hpl + (size_t)e * A.hpl_stride;  // B = h^T (6 x 3), h[k][r] = h[6k + r]
@@ -103,10 +108,19 @@ __global__ __launch_bounds__(256) void k_schur_points(SchurArgs A)
     // as doubles, ~80 VGPRs, measured slower: 0.105 against 0.085 ms, r05l)
 #pragma unroll
     for (int k = 0; k < SCHUR_REC; k += 2) rec[tid * (SCHUR_REC / 2) + k / 2] = make_double2(v[k], v[k + 1]);
+    // records of edges to fixed poses are never read (k_schur_blocks / k_schur_rhs take free
+    // poses' slots only): not stored
+    __shared__ uint8_t keep[256];
+#ifdef SCHUR_KEEP_ALL  // A/B: every record stored
+    keep[tid] = 1;
+#else
+    keep[tid] = fi >= 0;
+#endif
     __syncthreads();
     const int nrec = min(256, A.nslot - base);
     double2 *out = (double2 *)(A.rec + (size_t)base * SCHUR_REC);
-    for (int i = tid; i < nrec * (SCHUR_REC / 2); i += 256) out[i] = rec[i];
+    for (int i = tid; i < nrec * (SCHUR_REC / 2); i += 256)
+        if (keep[i / (SCHUR_REC / 2)]) out[i] = rec[i];
 }
 
 // workgroup per upper block, wave u = accumulator chain u: the block's pairs t = u, u + 16, ...
@@ -187,12 +201,99 @@ __global__ __launch_bounds__(64 * SCHUR_CHAINS) __attribute__((amdgpu_waves_per_
     }
 }
 
+// k_schur_blocks with its operands staged: the same chains, pairs and MFMAs (so the same
+// bits), but a batch's SCHUR_SBATCH B D^-1 records (the first 18 doubles of a slot's record)
+// and H_pl blocks (18 doubles) are fetched as whole 16-byte pieces -- 9 per block, one per
+// lane, 2 x 9 x SCHUR_SBATCH pieces in ceil(18 SCHUR_SBATCH / 64) load instructions -- into
+// the wave's own LDS region, and the MFMA operands are read from there.  The gather version
+// issues two 64-lane loads of 8 bytes per pair (each touching a 192- and a 144-byte block);
+// this one about a quarter as many vector-memory instructions, with the next batch's pieces
+// in flight (registers) while the current batch's MFMAs run.
+#ifndef SCHUR_SBATCH
+#define SCHUR_SBATCH 7  // pairs per batch: 2 x 9 x 7 = 126 pieces = 2 loads of 64 lanes (14: 4 loads, +5%; 21: +16%, r06c)
+#endif
+#define SCHUR_SPIECES (2 * 9 * SCHUR_SBATCH)
+#define SCHUR_SLOADS ((SCHUR_SPIECES + 63) / 64)
+__global__ __launch_bounds__(64 * SCHUR_CHAINS) __attribute__((amdgpu_waves_per_eu(8, 8))) void k_schur_blocks_lds(SchurArgs A)
+{
+    __shared__ double tile[SCHUR_CHAINS][64];
+    __shared__ double2 stage[SCHUR_CHAINS][SCHUR_SPIECES];
+    const int lane = threadIdx.x & 63, u = threadIdx.x >> 6,
+              bk = A.blk_order[ORBG_SCHUR_XCD ? xcd_remap(blockIdx.x, gridDim.x) : (int)blockIdx.x];
+    const int i1 = A.blk_i1[bk], i2 = A.blk_i2[bk], sg = A.blk_seg[bk];
+    const int lo = A.seg_lo[sg], n = 6 * (A.seg_lo[sg + 1] - lo);
+    const int k = lane >> 4, b = (lane >> 2) & 3, t = lane & 3;
+    const int ra = 4 * (b >> 1) + t, cb = 4 * (b & 1) + t;  // A's row, B's column
+    const bool va = ra < 6 && k < 3, vb = k < 3 && cb < 6;
+    const int oa = va ? ra * 3 + k : 0, ob = vb ? 6 * k + cb : 0;
+    const int ro = 4 * (b >> 1) + k, co = 4 * (b & 1) + t;  // this lane's C entry (i = lane >> 4)
+    double c = 0.0;
+    if (u == 0 && i1 == i2 && ro < 6 && co < 6)
+        c = A.hpose[36 * (size_t)A.free_pose[i1] + 6 * ro + co] + (ro == co ? A.lambda : 0.0);
+    const int p0 = A.blk_off[bk], np = A.blk_off[bk + 1] - p0;
+    const int nu = np > u ? (np - u + SCHUR_CHAINS - 1) / SCHUR_CHAINS : 0;  // p0 + u + 16 j
+    // piece c of a batch: c < 9 B: the A block of pair c / 9, else the B block of pair
+    // (c - 9 B) / 9; piece c % 9 of it (16 bytes).  Pairs past the chain's end are clamped
+    // (the MFMA skips them).
+    const double2 *recp = (const double2 *)A.rec, *hplp = (const double2 *)A.hpl;
+    const int hstride2 = A.hpl_stride / 2;  // 16-byte pieces per H_pl row (hpl_stride even)
+    auto fetch = [&](int j0, double2 (&v)[SCHUR_SLOADS]) {
+        // this lane's pairs' ids: lane q < SCHUR_SBATCH holds pair j0 + q
+        const int2 id = nu > 0 ? A.blk_pairs[p0 + u + SCHUR_CHAINS * min(j0 + min(lane, SCHUR_SBATCH - 1), nu - 1)]
+                               : make_int2(0, 0);
+#pragma unroll
+        for (int i = 0; i < SCHUR_SLOADS; i++) {
+            const int pc = lane + 64 * i;
+            const bool isb = pc >= 9 * SCHUR_SBATCH;
+            const int rel = isb ? pc - 9 * SCHUR_SBATCH : pc;
+            const int q = min(rel / 9, SCHUR_SBATCH - 1), part = rel - 9 * (rel / 9);
+            const int s1 = __shfl(id.x, q, 64), e2 = __shfl(id.y, q, 64);
+            const double2 *src = isb ? hplp + (size_t)e2 * hstride2 + part
+                                     : recp + (size_t)s1 * (SCHUR_REC / 2) + part;
+            v[i] = (pc < SCHUR_SPIECES) ? *src : make_double2(0.0, 0.0);
+        }
+    };
+    double2 cur[SCHUR_SLOADS];
+    if (nu > 0) fetch(0, cur);
+    const double *sd = (const double *)stage[u];
+    for (int j0 = 0; j0 < nu; j0 += SCHUR_SBATCH) {
+        const int m = min(SCHUR_SBATCH, nu - j0);
+#pragma unroll
+        for (int i = 0; i < SCHUR_SLOADS; i++) {
+            const int pc = lane + 64 * i;
+            if (pc < SCHUR_SPIECES) stage[u][pc] = cur[i];
+        }
+        wave_sync_lds();
+        if (j0 + SCHUR_SBATCH < nu) fetch(j0 + SCHUR_SBATCH, cur);  // in flight during the MFMAs
+#pragma unroll
+        for (int q = 0; q < SCHUR_SBATCH; q++)
+            if (q < m) {
+                const double av = sd[18 * q + oa], bv = sd[18 * (SCHUR_SBATCH + q) + ob];
+                c = __builtin_amdgcn_mfma_f64_4x4x4f64(va ? -av : 0.0, vb ? bv : 0.0, c, 0, 0, 0);
+            }
+        wave_sync_lds();  // every lane's reads of this batch before the next batch's writes
+    }
+    tile[u][lane] = c;
+    __syncthreads();
+    if (u != 0) return;
+    double a8[8], b4[4];
+#pragma unroll
+    for (int i = 0; i < 8; i++) a8[i] = tile[2 * i][lane] + tile[2 * i + 1][lane];
+#pragma unroll
+    for (int i = 0; i < 4; i++) b4[i] = a8[2 * i] + a8[2 * i + 1];
+    const double v = (b4[0] + b4[1]) + (b4[2] + b4[3]);
+    if (ro < 6 && co < 6) {
+        double *S = A.S + A.seg_soff[sg];
+        const int r = 6 * (i1 - lo) + ro, cc = 6 * (i2 - lo) + co;
+        if (i1 != i2 || ro <= co) S[(size_t)r * n + cc] = v;
+        if (i1 != i2 || ro < co) S[(size_t)cc * n + r] = v;
+    }
+}
+
 // b_schur = b_p - coefficients, per free pose: the landmark-ordered B D^-1 b_l terms summed
 // as 64 lane partials (term t into partial t % 64, in order) and an xor butterfly
-__global__ __launch_bounds__(256) void k_schur_rhs(SchurArgs A)
+__device__ __forceinline__ void schur_rhs_wave(const SchurArgs &A, int i, int lane)
 {
-    const int lane = threadIdx.x & 63;
-    const int i = __builtin_amdgcn_readfirstlane((int)(blockIdx.x * 4 + (threadIdx.x >> 6)));
     if (i >= A.nfree) return;
     const int pose = A.free_pose[i], e0 = A.pose_off[i], e1 = A.pose_off[i + 1];
     double part[6] = {0, 0, 0, 0, 0, 0};
@@ -233,6 +334,12 @@ __global__ __launch_bounds__(256) void k_schur_rhs(SchurArgs A)
     }
 }
 
+__global__ __launch_bounds__(256) void k_schur_rhs(SchurArgs A)
+{
+    const int i = __builtin_amdgcn_readfirstlane((int)(blockIdx.x * 4 + (threadIdx.x >> 6)));
+    schur_rhs_wave(A, i, threadIdx.x & 63);
+}
+
 // one workgroup per segment: right-looking LDLT of the segment's n x n system (lower
 // triangle), then L y = b (column by column), y /= d, L^T x = y (column by column, k
 // descending), in LDS when LDSM (the matrix fits), else in place in HBM
@@ -260,7 +367,9 @@ __global__ __launch_bounds__(256) void k_schur_ldlt(SchurArgs A)
         for (int i = j + 1 + tid; i < n; i += 256) M[(size_t)i * n + j] = M[(size_t)i * n + j] / d;
         __syncthreads();
         // trailing lower triangle: M[r][c] -= (L_rj L_cj) d_j, the oracle's
-        // A[i][k] * A[j][k] * A[k][k] at k = j, in k order for every element
+        // A[i][k] * A[j][k] * A[k][k] at k = j, in k order for every element.  (One barrier
+        // per column, each update dividing its two column entries itself, measured slower:
+        // 0.071 against 0.061 ms, r06f: the f64 divisions)
         for (int r = j + 1 + (tid >> 4); r < n; r += 16) {
             const double lr = M[(size_t)r * n + j];
             for (int c = j + 1 + (tid & 15); c <= r; c += 16)
@@ -270,6 +379,25 @@ __global__ __launch_bounds__(256) void k_schur_ldlt(SchurArgs A)
     }
     if (bad) {  // uniform: every thread read the same pivot
         if (tid == 0) *A.ok = 0;
+        return;
+    }
+    if (LDSM) {
+        // the triangular solves by one wave (2 n dependent steps: a wave's LDS operations
+        // complete in order, so no workgroup barrier per step)
+        if (tid >= 64) return;
+        for (int k = 0; k < n; k++) {
+            const double xk = x[k];
+            for (int i = k + 1 + tid; i < n; i += 64) x[i] -= M[(size_t)i * n + k] * xk;
+            wave_sync_lds();
+        }
+        for (int i = tid; i < n; i += 64) x[i] /= M[(size_t)i * n + i];
+        wave_sync_lds();
+        for (int k = n - 1; k > 0; k--) {
+            const double xk = x[k];
+            for (int i = tid; i < k; i += 64) x[i] -= M[(size_t)k * n + i] * xk;
+            wave_sync_lds();
+        }
+        for (int e = tid; e < n; e += 64) xg[e] = x[e];
         return;
     }
     // L y = b: x_i -= L_ik x_k, k ascending (the oracle's row loop, element by element)
@@ -296,7 +424,7 @@ __global__ __launch_bounds__(256) void k_schur_ldlt(SchurArgs A)
 // form above pays two per column).  The trailing update walks the step's lower triangle
 // flattened, 64 elements per instruction; every element still takes its updates in k order.
 #ifndef ORBG_SCHUR_LDLT_WAVE
-#define ORBG_SCHUR_LDLT_WAVE 0  // measured 0.193 ms against 0.060 for the 256-thread form (r05l): off
+#define ORBG_SCHUR_LDLT_WAVE 0  // one wave per segment: the 8 x 8 lane grid measured 0.116 ms (r06g), the round-5 flattened walk 0.193, against 0.060 for the 256-thread form
 #endif
 __global__ __launch_bounds__(64) void k_schur_ldlt_wave(SchurArgs A)
 {
@@ -317,21 +445,13 @@ __global__ __launch_bounds__(64) void k_schur_ldlt_wave(SchurArgs A)
         }
         for (int i = j + 1 + lane; i < n; i += 64) M[(size_t)i * n + j] = M[(size_t)i * n + j] / d;
         wave_sync_lds();
-        // element t of the triangle r in (j, n), c in (j, r], row-major: (r, c) advanced by 64
-        const int m = n - j - 1;
-        const int tot = m * (m + 1) / 2;
-        int r = j + 1, c = j + 1 + lane;
-        while (c > r && r < n) {  // place t = lane
-            c -= r - j;
-            r++;
-        }
-        for (int t = lane; t < tot; t += 64) {
-            M[(size_t)r * n + c] -= M[(size_t)r * n + j] * M[(size_t)c * n + j] * d;
-            c += 64;
-            while (c > r && r < n) {
-                c -= r - j;
-                r++;
-            }
+        // the trailing lower triangle on an 8 x 8 lane grid (rows j+1+(lane>>3) step 8,
+        // columns j+1+(lane&7) step 8; the round-5 flattened walk measured 0.193 ms)
+        for (int r = j + 1 + (lane >> 3); r < n; r += 8) {
+            const double lr = M[(size_t)r * n + j];
+#pragma unroll 2
+            for (int c = j + 1 + (lane & 7); c <= r; c += 8)
+                M[(size_t)r * n + c] -= lr * M[(size_t)c * n + j] * d;
         }
         wave_sync_lds();
     }
@@ -370,6 +490,7 @@ __global__ void k_schur_backsub(SchurArgs A)
     const double *bl = A.bpoint + 3 * (size_t)p;
     double cl[3] = {bl[0], bl[1], bl[2]};
     for (int a = a0; a < a1; a++) {
+        // (slot_fidx here instead of pidx[edge_pose[e]] measured 0.0625 against 0.0597 ms, r06f)
         const int e = A.pt_edges[a], i1 = A.pidx[A.edge_pose[e]];
         if (i1 < 0) continue;
         const double *h = A.hpl + (size_t)e * A.hpl_stride;
@@ -392,11 +513,15 @@ int launch_schur(hipStream_t st, const SchurArgs &A, void *prof)
     hipLaunchKernelGGL(k_schur_points, dim3((std::max(A.nslot, 1) + T - 1) / T), dim3(T), 0, st, A);
     prof_end(prof, st, "schur_points", ev);
     if (A.nfree > 0) {
-        // block pairs without a shared landmark are never written: zero the systems first
-        if (hipMemsetAsync(A.S, 0, sizeof(double) * (size_t)A.s_total, st) != hipSuccess)
-            return ORBG_EIO;
         prof_begin(prof, st, "schur_blocks", &ev);
-        hipLaunchKernelGGL(k_schur_blocks, dim3(A.nblk), dim3(64 * SCHUR_CHAINS), 0, st, A);
+        // ORBG_SCHUR_STAGE=0: the per-pair gather form (A/B); staging needs 16-byte H_pl rows
+        static const int stage_env = getenv("ORBG_SCHUR_STAGE") ? atoi(getenv("ORBG_SCHUR_STAGE")) : 1;
+        // (b_schur folded into this launch as trailing workgroups measured slower: 0.24 ms
+        // against 0.110 + 0.028, r06e)
+        if (stage_env && (A.hpl_stride % 2) == 0)
+            hipLaunchKernelGGL(k_schur_blocks_lds, dim3(A.nblk), dim3(64 * SCHUR_CHAINS), 0, st, A);
+        else
+            hipLaunchKernelGGL(k_schur_blocks, dim3(A.nblk), dim3(64 * SCHUR_CHAINS), 0, st, A);
         prof_end(prof, st, "schur_blocks", ev);
         prof_begin(prof, st, "schur_rhs", &ev);
         hipLaunchKernelGGL(k_schur_rhs, dim3((A.nfree + 3) / 4), dim3(T), 0, st, A);
@@ -404,7 +529,9 @@ int launch_schur(hipStream_t st, const SchurArgs &A, void *prof)
         const int n = 6 * A.max_seg;
         const size_t lds = ((size_t)n * n + n) * sizeof(double);
         prof_begin(prof, st, "schur_ldlt", &ev);
-        if (ORBG_SCHUR_LDLT_WAVE && lds <= 160 * 1024 - 64) {
+        static const int ldlt_wave = getenv("ORBG_SCHUR_LDLT_WAVE") ? atoi(getenv("ORBG_SCHUR_LDLT_WAVE"))
+                                                                    : ORBG_SCHUR_LDLT_WAVE;
+        if (ldlt_wave && lds <= 160 * 1024 - 64) {
             if (lds > 64 * 1024 &&
                 hipFuncSetAttribute((const void *)k_schur_ldlt_wave,
                                     hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) != hipSuccess)
@@ -470,6 +597,8 @@ void build_schur_plan(int npose, int npoint, int nedge, const int32_t *epose,
             for (int a = P.pt_off[q]; a < P.pt_off[q + 1]; a++) P.slot_point[a] = q;
         }
     }
+    P.slot_fidx.assign(P.pt_edges.size(), -1);
+    for (int a = 0; a < P.pt_off[npoint]; a++) P.slot_fidx[a] = P.pidx[epose[P.pt_edges[a]]];
     // (block, pair) in landmark order, then grouped by upper block (i1 <= i2) with a stable
     // sort: each block's pairs keep the landmark order; the free poses' edge lists likewise
     struct BP {

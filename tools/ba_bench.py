@@ -31,6 +31,70 @@ F64_MFMA_PEAK_TFLOPS = 78.6  # MI355X FP64 matrix, AMD spec (the guide lists no 
 PMC_BA = "r05_ba_pmc_kernels.json"  # tools/profile.sh <tag> tools/ba_bench.py (round 5 build)
 
 
+def schur_roofline(poses, edges, sk, iters, pk):
+    """The Schur solve's kernels against their bounds (csrc/schur_kernels.hip):
+    - k_schur_blocks: one v_mfma_f64_4x4x4f64 per (e1, e2) pair of free-pose edges of one
+      landmark (a <= b in the landmark's edge list): pairs = sum over points of f (f + 1) / 2,
+      f = the point's active edges to free poses.  Issued 512 FLOP per MFMA (4 blocks x 4x4x4
+      x 2); useful 216 (the 6x3 x 3x6 product, 2 FLOP per multiply-add).  Algorithmic bytes
+      per pair: the pair's B D^-1 (6x3 f64, 144 B) and H_pl (3x6 f64, 144 B), each read once
+      per pair as the kernel does (no reuse across pairs is assumed); the dense system's
+      writes (36 f64 per upper block, mirrored) are added per launch.
+    - k_schur_points: per active edge slot to a free pose, H_pl (144 B) + the point's H_ll | b_l
+      (96 B) in and the 24-f64 record (192 B) out.
+    mfma_frac / traffic from the committed PMC pass when it holds the kernel (pmc_source)."""
+    fixed = poses["fixed"] != 0
+    act = edges["active"] != 0
+    free_e = act & ~fixed[edges["pose"]]
+    f = np.bincount(edges["point"][free_e], minlength=1).astype(np.int64)
+    pairs = int((f * (f + 1) // 2).sum())
+    nfree = int((~fixed).sum())
+    nslot_free = int(free_e.sum())
+    out = {"pairs_per_launch": pairs, "free_poses": nfree, "free_slots": nslot_free}
+
+    def avg(k):
+        v = sk.get(k)
+        return v[0] / max(v[1], 1) if v else None
+
+    ms = avg("schur_blocks")
+    if ms:
+        # upper blocks: the diagonal ones + the distinct free-pose pairs sharing a landmark
+        # (an upper bound on the block count is enough for the write term: 36 f64 x 2 each)
+        flop_issued = pairs * 512
+        flop_useful = pairs * 216
+        byts = pairs * 288
+        out["schur_blocks"] = {
+            "avg_launch_ms": round(ms, 5),
+            "mfma_per_launch": pairs,
+            "issued_tflops": round(flop_issued / (ms * 1e-3) / 1e12, 3),
+            "useful_tflops": round(flop_useful / (ms * 1e-3) / 1e12, 3),
+            "peak_tflops": F64_MFMA_PEAK_TFLOPS,
+            "useful_frac_of_peak": round(flop_useful / (ms * 1e-3) / 1e12 / F64_MFMA_PEAK_TFLOPS, 4),
+            "useful_work_per_mfma": round(216 / 512, 4),
+            "algo_bytes_per_launch": byts,
+            "achieved_gbs": round(byts / (ms * 1e-3) / 1e9, 1),
+            "hbm_frac": round(byts / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
+            "pairs_per_s": round(pairs / (ms * 1e-3), 1),
+            "mfma_frac": pk.get("schur_blocks", {}).get("mfma_frac"),
+            "traffic": pk.get("schur_blocks", {}).get("hbm_bytes_per_launch"),
+        }
+    ms = avg("schur_points")
+    if ms:
+        byts = nslot_free * (144 + 96 + 192)
+        out["schur_points"] = {
+            "avg_launch_ms": round(ms, 5), "algo_bytes_per_launch": byts,
+            "achieved_gbs": round(byts / (ms * 1e-3) / 1e9, 1),
+            "hbm_frac": round(byts / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
+            "traffic": pk.get("schur_points", {}).get("hbm_bytes_per_launch")}
+    for k in ("schur_rhs", "schur_ldlt", "schur_backsub"):
+        ms = avg(k)
+        if ms:
+            out[k] = {"avg_launch_ms": round(ms, 5),
+                      "traffic": pk.get(k, {}).get("hbm_bytes_per_launch"),
+                      "wait_inst_any_frac": pk.get(k, {}).get("wait_inst_any_frac")}
+    return out
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--windows", type=int, default=64)
@@ -208,6 +272,7 @@ def main():
             "schur_ms": round(sum(v[0] for k, v in sk.items() if k.startswith("schur")) / args.iters, 4),
             "schur_kernels_ms": {k: round(v[0] / args.iters, 4) for k, v in sk.items()},
             "ok": int(lba.d_ok.cpu().numpy()[0]), "lambda": lam}
+        out["schur_roofline"] = schur_roofline(poses, edges, sk, args.iters, pk)
         # optimizer.optimize(5) end to end (orbg_ba_graph_optimize): per trial the build, the
         # Schur solve, the update, the error pass and the three scalars read back, from the
         # same starting estimates each run
