@@ -28,7 +28,7 @@ sys.path.insert(0, ROOT)
 HBM_PEAK_GBS = 8000.0
 EDGE_ALGO_BYTES = 108  # per-edge algorithmic bytes
 F64_MFMA_PEAK_TFLOPS = 78.6  # MI355X FP64 matrix, AMD spec (the guide lists no FP64 row)
-PMC_BA = "r05_ba_pmc_kernels.json"  # tools/profile.sh <tag> tools/ba_bench.py (round 5 build)
+PMC_BA = "r06_ba_pmc_kernels.json"  # tools/profile.sh r06_ba tools/ba_bench.py (round 6 build)
 
 
 def schur_roofline(poses, edges, sk, iters, pk):

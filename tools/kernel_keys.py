@@ -10,7 +10,8 @@ KEYS = {
     "k_ba_point_blocks": "ba_point_blocks", "k_ba_pose_mfma": "ba_pose_mfma",
     "k_ba_slices_special": "ba_pose_mfma", "k_ba_pose_reduce": "ba_pose_reduce",
     "k_ba_errors": "ba_errors", "k_ba_errors_packed": "ba_errors",
-    "k_schur_points": "schur_points", "k_schur_blocks": "schur_blocks", "k_schur_rhs": "schur_rhs",
+    "k_schur_points": "schur_points", "k_schur_blocks": "schur_blocks",
+    "k_schur_blocks_lds": "schur_blocks", "k_schur_rhs": "schur_rhs",
     "k_schur_ldlt": "schur_ldlt", "k_schur_ldlt_wave": "schur_ldlt",
     "k_schur_backsub": "schur_backsub", "k_ba_update": "ba_update", "k_lm_partial": "lm_reduce",
     "k_lm_final": "lm_reduce",
