@@ -48,17 +48,21 @@ PMC_MONO = "r05final8_pmc_kernels.json"
 PMC_STEREO = "r05final8_stereo_pmc_kernels.json"
 
 
-def kernel_algo_bytes(name, B, npairs, ncand, nkp, launches_per_step, ndepth=0):
+def kernel_algo_bytes(name, B, npairs, ncand, nkp, launches_per_step, ndepth=0, blur_plan=None):
     """Algorithmic bytes of one launch of `name` (see DESIGN.md 'Kernels').  B images, npairs
     frame pairs, ncand FAST candidates and nkp keypoints over the batch, ndepth stereo
-    matches (keypoints with a depth) over the batch."""
+    matches (keypoints with a depth) over the batch.  blur_plan = orbg_get_blur_plan's (fused,
+    interior px, border px) per frame: with the GaussianBlur fused into the FAST cells,
+    fast_cells also writes the interior's blurred bytes and "blur" (k_blur_border) reads and
+    writes only the border's."""
     lv = level_sizes()
+    fused, inner, border = blur_plan if blur_plan else (False, 0, PYR_BYTES)
     if name == "resize":
         tot = B * sum(lv[l - 1][0] * lv[l - 1][1] + lv[l][0] * lv[l][1] for l in range(1, NLEV))
     elif name == "fast_cells":
-        tot = B * PYR_BYTES + 8 * ncand
+        tot = B * PYR_BYTES + 8 * ncand + (B * inner if fused else 0)
     elif name == "blur":
-        tot = 2 * B * PYR_BYTES
+        tot = 2 * B * (border if fused else PYR_BYTES)
     elif name == "octree":
         tot = 8 * ncand + 4 * nkp
     elif name == "orient_desc":
@@ -479,11 +483,12 @@ def main():
                 return int(e["hbm_bytes_per_step"] / lps)
             return e.get("hbm_bytes_per_launch")
 
+        blur_plan = ext.ctx.blur_plan()
         kstats = {}
         for name, (ms, n) in kern.items():
             lps = n / max(args.steps, 1)
             avg = ms / max(n, 1)
-            ab = kernel_algo_bytes(name, nimg, B, ncand, nkp, lps, ndepth)
+            ab = kernel_algo_bytes(name, nimg, B, ncand, nkp, lps, ndepth, blur_plan)
             kstats[name] = {"ms_per_step": round(ms / args.steps, 4), "launches_per_step": lps,
                             "avg_launch_ms": round(avg, 5),
                             "algo_bytes_per_launch": None if ab is None else int(ab),
@@ -561,6 +566,9 @@ def main():
                                        "once step k-1's outputs are written (host-gated "
                                        "orbg_batch_acquire)"}
                            if args.host_input else None),
+            "blur_plan": {"fused_into_fast_cells": blur_plan[0],
+                          "interior_px_per_image": blur_plan[1],
+                          "border_px_per_image": blur_plan[2]},
             "candidates_per_image": round(ncand / nimg, 1),
             "keypoints_per_image": round(nkp / nimg, 1),
         }

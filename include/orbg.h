@@ -292,6 +292,13 @@ int orbg_batch_stats(orbg_ctx *ctx, int64_t *ncandidates, int64_t *nkeypoints);
  * fallback.  ORBG_EINVAL before any extraction. */
 int orbg_get_quadtree_caps(const orbg_ctx *ctx, int32_t *first_cap, int32_t *level0_cap,
                            int32_t *upper_cap);
+/* the GaussianBlur plan of the last planned image size (ORBextractor.cc:1375-1377): *fused =
+ * 1 when the FAST cells blur their detection regions from the window tiles they stage (the
+ * pixels of every level's rectangle of regions, *interior_px per frame) and a border pass
+ * blurs the rest (*border_px per frame); 0 when one blur pass covers every level.  Any
+ * pointer may be NULL.  ORBG_EINVAL before any extraction. */
+int orbg_get_blur_plan(const orbg_ctx *ctx, int32_t *fused, int64_t *interior_px,
+                       int64_t *border_px);
 
 /* per-kernel timing with HIP events on the context stream (for bench roofline) */
 int orbg_profile_enable(orbg_ctx *ctx, int enable);

@@ -23,6 +23,7 @@
 #include "orbg_internal.h"
 #include "orbg_device.h"
 #include "fast_device.h"
+#include "blur_device.h"
 
 #pragma clang fp contract(off)
 
@@ -57,18 +58,23 @@ namespace orbg {
 struct Fc2Cell {
     const uint8_t *base;  // window top-left
     int pitch, f, c, W, H, RW, RH, RG, nunits, xo, yo, NC, nch, xs, ys;
+    // fused GaussianBlur (blur != nullptr): the region's level origin, its blurred plane
+    uint8_t *bdst;
+    int X0, Y0, bpitch, bplane;
 };
 
 #ifndef FC2_WPE
 #define FC2_WPE 7  // min waves per SIMD the register allocation targets (72 VGPRs, 12 B spill; 6 -> 7 with the 7-WG LDS plan: -0.3% per step)
 #endif
-template <int P4>
+// FB: the fused GaussianBlur phase (opt-in, ORBG_FAST_BLUR=1) compiled in; the default
+// instantiation (FB = false) keeps the 64-VGPR / 8-waves register budget
+template <int P4, bool FB>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(FC2_WPE, 8))) void k_fast2(
     const OrbgGeom *__restrict__ g, const OrbgCell *__restrict__ cells,
     const uint8_t *__restrict__ img0, int64_t img_fs, int img_pitch,
     const uint8_t *__restrict__ pyr, const uint32_t *__restrict__ ctab,
-    int32_t *__restrict__ cell_cnt, uint2 *__restrict__ cell_kp, int nframes, int c_begin,
-    int c_count)
+    int32_t *__restrict__ cell_cnt, uint2 *__restrict__ cell_kp, uint8_t *__restrict__ blur,
+    int nframes, int c_begin, int c_count)
 {
     constexpr int P = 4 * P4;
 #if ORBG_FC2_IL
@@ -124,6 +130,18 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(FC2_WPE, 8)
         k.xs = g->lv[l].xs_off + k.xo;
         k.ys = g->lv[l].ys_off + k.yo;
         k.NC = (k.RG + 2 + 3) >> 2;  // tile dwords 0 .. RG+1
+        k.X0 = x0 + 3;
+        k.Y0 = y0 + 3;
+        if (FB) {
+            // the fused blur's last output dword starts below X0 + RW; its 7-tap sources reach
+            // 3 bytes past it: window bytes up to 4 ceil((X0 + RW) / 4) + 2 - x0 (the plan
+            // checked the pitch holds them)
+            const int nb = 4 * ((k.X0 + k.RW + 3) >> 2) + 3 - x0;
+            k.NC = max(k.NC, (nb + 15) >> 4);
+            k.bdst = blur + k.f * g->blur_frame + g->lv[l].blur_off;
+            k.bpitch = g->lv[l].pitch;
+            k.bplane = g->lv[l].h * k.bpitch;
+        }
         k.nch = k.H * k.NC;
         return k;
     };
@@ -206,6 +224,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(FC2_WPE, 8)
     }
     wave_sync_lds();
     if (dbg == 11) continue;
+
 
     // unit u = ry * RG + gg walked as u = lane + 64 k: (ry, gg) advance by (64 / RG, 64 % RG)
     const int rstep = RG > 0 ? 64 / RG : 0, gstep = RG > 0 ? 64 - rstep * RG : 0;
@@ -515,6 +534,54 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(FC2_WPE, 8)
             }
         }
     }
+    // ---- fused GaussianBlur 7x7 (ORBextractor.cc:1375-1377; k_blur2's arithmetic,
+    // blur2_column) of the cell's detection region from the window tile (intact: the
+    // phases above write only the score rows and the lists): output dwords
+    // (level x = 4q, q in [ceil(X0 / 4), ceil((X0 + RW) / 4))) x 4-row segments, a task per
+    // lane; the region rows' 7-row sources are window rows, the columns' 7-tap sources window
+    // bytes (the tile holds them, decode()).  Cells tile the level's rectangle [16, bx1) x
+    // [16, by1) with disjoint dwords; k_blur_border does the rest ----
+    if constexpr (FB) {
+        const Blur2Weights bw(g);
+        const int qa = (cur.X0 + 3) >> 2, nq = ((cur.X0 + RW + 3) >> 2) - qa;
+        const int ntask = nq * ((RH + 3) >> 2);
+        const int ob0 = 4 * qa - cur.X0 - 1;  // tile byte of column 4 qa - 4: -1 .. 2
+        const uint32_t bsh = (uint32_t)(ob0 & 3);
+        const int qdiv = (65536 + nq - 1) / max(nq, 1);  // t / nq == (t * qdiv) >> 16, t < 1024
+        const __amdgpu_buffer_rsrc_t brs =
+            __builtin_amdgcn_make_buffer_rsrc((void *)cur.bdst, (short)0, cur.bplane, 0x00020000);
+        auto seg = [&](auto NORM) {
+            for (int t = lane; t < ntask; t += 64) {
+                const int sg = (t * qdiv) >> 16, q = t - sg * nq;
+                const int ob = ob0 + 4 * q, di = (ob - (int)bsh) >> 2;  // di >= -1
+                const uint32_t *rowp = (const uint32_t *)tA + 4 * sg * RS4 + max(di, 0);
+                const int soff = (cur.Y0 + 4 * sg) * cur.bpitch + 4 * (qa + q);
+                blur2_column<4, decltype(NORM)::value>(
+                    bw,
+                    [&](int i, uint32_t &w0, uint32_t &w1, uint32_t &w2) {
+                        // one row's loads at a time (hoisting all ten rows' LDS reads took
+                        // the kernel past 64 VGPRs, i.e. below 8 waves per SIMD)
+                        __builtin_amdgcn_sched_barrier(0);
+                        const uint32_t *pr = rowp + i * RS4;
+                        // di = -1: dword -1 feeds only byte 0 of w0 (column gx - 4, weight 0)
+                        const uint32_t d0 = di >= 0 ? pr[0] : 0u;
+                        const uint32_t *pq = pr + (di >= 0 ? 1 : 0);
+                        const uint32_t d1 = pq[0], d2 = pq[1], d3 = pq[2];
+                        w0 = __builtin_amdgcn_alignbyte(d1, d0, bsh);
+                        w1 = __builtin_amdgcn_alignbyte(d2, d1, bsh);
+                        w2 = __builtin_amdgcn_alignbyte(d3, d2, bsh);
+                    },
+                    [&](int o, uint32_t word) {
+                        __builtin_amdgcn_raw_buffer_store_b32(
+                            word, brs, 4 * sg + o < RH ? soff + o * cur.bpitch : (1 << 30), 0, 0);
+                    });
+            }
+        };
+        if (bw.norm256)
+            seg(std::true_type{});
+        else
+            seg(std::false_type{});
+    }
     if (lane == 0) cell_cnt[slot] = run;
     }  // cells of this wave
 }
@@ -534,25 +601,39 @@ bool fast2_pitch_ok(int p4)
     }
 }
 
+template <int P4, bool FB>
+static hipError_t launch_fast2_t(size_t lds, dim3 grid, hipStream_t st, const OrbgGeom *g,
+                                 const OrbgCell *cells, const uint8_t *img0, int64_t img_fs,
+                                 int img_pitch, const uint8_t *pyr, const uint32_t *ctab,
+                                 int32_t *cell_cnt, uint2 *cell_kp, uint8_t *blur, int nframes,
+                                 int c_begin, int c_count)
+{
+    if (lds > 64 * 1024) {
+        hipError_t e = hipFuncSetAttribute((const void *)k_fast2<P4, FB>,
+                                           hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+        if (e != hipSuccess) return e;
+    }
+    hipLaunchKernelGGL((k_fast2<P4, FB>), grid, dim3(256), lds, st, g, cells, img0, img_fs,
+                       img_pitch, pyr, ctab, cell_cnt, cell_kp, blur, nframes, c_begin, c_count);
+    return hipGetLastError();
+}
+
 hipError_t launch_fast2(int p4, size_t lds, hipStream_t st, const OrbgGeom *g,
                         const OrbgCell *cells, const uint8_t *img0, int64_t img_fs,
                         int img_pitch, const uint8_t *pyr, const uint32_t *ctab,
-                        int32_t *cell_cnt, uint2 *cell_kp, int nframes, int c_begin,
-                        int c_count)
+                        int32_t *cell_cnt, uint2 *cell_kp, uint8_t *blur, int nframes,
+                        int c_begin, int c_count)
 {
     const dim3 grid((c_count * nframes + 4 * FC2_CPW - 1) / (4 * FC2_CPW));
     switch (p4) {
 #define X(n)                                                                                  \
     case n:                                                                                   \
-        if (lds > 64 * 1024) {                                                                \
-            hipError_t e = hipFuncSetAttribute((const void *)k_fast2<n>,                      \
-                                               hipFuncAttributeMaxDynamicSharedMemorySize,    \
-                                               (int)lds);                                     \
-            if (e != hipSuccess) return e;                                                    \
-        }                                                                                     \
-        hipLaunchKernelGGL(k_fast2<n>, grid, dim3(256), lds, st, g, cells, img0, img_fs,      \
-                           img_pitch, pyr, ctab, cell_cnt, cell_kp, nframes, c_begin, c_count); \
-        return hipGetLastError();
+        if (blur) return launch_fast2_t<n, true>(lds, grid, st, g, cells, img0, img_fs,       \
+                                                 img_pitch, pyr, ctab, cell_cnt, cell_kp,     \
+                                                 blur, nframes, c_begin, c_count);            \
+        return launch_fast2_t<n, false>(lds, grid, st, g, cells, img0, img_fs, img_pitch, pyr, \
+                                        ctab, cell_cnt, cell_kp, nullptr, nframes, c_begin,   \
+                                        c_count);
         ORBG_FAST2_PITCHES(X)
 #undef X
     default:

@@ -59,8 +59,11 @@ hipError_t launch_fast_rows(hipStream_t st, const OrbgGeom *g, const OrbgFastTil
 hipError_t launch_fast2(int p4, size_t lds, hipStream_t st, const OrbgGeom *g,
                         const OrbgCell *cells, const uint8_t *img0, int64_t img_fs,
                         int img_pitch, const uint8_t *pyr, const uint32_t *ctab,
-                        int32_t *cell_cnt, uint2 *cell_kp, int nframes, int c_begin,
-                        int c_count);
+                        int32_t *cell_cnt, uint2 *cell_kp, uint8_t *blur, int nframes,
+                        int c_begin, int c_count);
+hipError_t launch_blur_border(hipStream_t st, const OrbgGeom *g, int tasks_per_frame,
+                              const uint8_t *img0, int64_t img_fs, int img_pitch,
+                              const uint8_t *pyr, uint8_t *blur, int l0, int l1, int nframes);
 struct OrbgKeypointDev;
 hipError_t launch_orient_desc(bool bfma, dim3 grid, hipStream_t st, const OrbgGeom *g,
                               const uint8_t *img0, int64_t img_fs, int img_pitch,
@@ -1212,6 +1215,59 @@ static int plan(orbg_ctx *c, int w, int h, int batch)
         if (!G.fc2_p4)
             return set_err(ORBG_ENOTSUP, "FAST cell %dx%d fits no k_fast2 LDS pitch", wmax, hmax);
     }
+    // GaussianBlur fused into k_fast2 (ORBG_FAST_BLUR=1, opt-in: measured slower, r06h --
+    // fast_cells 1.97 -> 2.78 ms and the border pass 1.21 ms against k_blur2's 0.71 ms per
+    // 1025 frames; the step is issue-bound, the pyramid re-read it saves was overlapped
+    // anyway, profiles/r06h_fast_blur_ab.txt): every level's cells tile the
+    // rectangle [16, gx1) x [16, gy1) with their detection regions, so the cells blur it
+    // (dword-aligned on the right: [16, bx1)) from the window tiles they stage anyway, and
+    // k_blur_border blurs the rest.  Needs: the regions tile the rectangle, every blurred
+    // pixel's 7 x 7 sources inside the level (no REFLECT_101 in the fused part), the tile
+    // pitch holding the window bytes the last output dword reads.  Not with the k_pyramid
+    // blur (ORBG_PYR_BLUR) or k_fast_rows.
+    G.fast_blur = 0;
+    G.bt_total = 0;
+    {
+        const char *fe = getenv("ORBG_FAST_BLUR"), *pb = getenv("ORBG_PYR_BLUR");
+        bool ok = (fe && atoi(fe) != 0) && !(pb && atoi(pb) != 0) && !(fr_ok && c->fr_mode);
+        for (int l = 0; l < G.L && ok; l++) {
+            OrbgLevel &L = G.lv[l];
+            int gx0 = 1 << 30, gy0 = 1 << 30, gx1 = 0, gy1 = 0;
+            int64_t area = 0;
+            for (int k = L.cell_base; k < L.cell_base + L.ncells && ok; k++) {
+                const OrbgCell &cl = cells[k];
+                const int X0 = cl.x0 + 3, Y0 = cl.y0 + 3, rw = cl.w - 6, rh = cl.h - 6;
+                if (rw <= 0 || rh <= 0) ok = false;
+                gx0 = std::min(gx0, X0);
+                gy0 = std::min(gy0, Y0);
+                gx1 = std::max(gx1, X0 + rw);
+                gy1 = std::max(gy1, Y0 + rh);
+                area += (int64_t)rw * rh;
+                const int nb = 4 * ((X0 + rw + 3) >> 2) + 3 - cl.x0;  // k_fast2 decode()
+                if (16 * ((nb + 15) >> 4) > 4 * G.fc2_p4) ok = false;
+            }
+            if (!ok) break;
+            if (area != (int64_t)(gx1 - gx0) * (gy1 - gy0)) ok = false;  // no gaps, no overlaps
+            L.bx0 = (gx0 + 3) & ~3;  // each cell blurs the dwords starting in its region
+            L.by0 = gy0;
+            L.bx1 = (gx1 + 3) & ~3;
+            L.by1 = gy1;
+            if (L.bx1 + 3 > L.w || L.by1 + 3 > L.h || gx0 < 3 || gy0 < 3) ok = false;
+        }
+        if (ok) {
+            int off = 0;
+            for (int l = 0; l < G.L; l++) {
+                OrbgLevel &L = G.lv[l];
+                const int nqw = (L.w + 3) / 4, sm = (L.by1 - L.by0 + 7) / 8;
+                L.bt_off = off;
+                L.bt_cnt = ((L.by0 + 7) / 8) * nqw + ((L.h - L.by1 + 7) / 8) * nqw +
+                           sm * (L.bx0 / 4) + sm * (nqw - L.bx1 / 4);
+                off += L.bt_cnt;
+            }
+            G.bt_total = off;
+            G.fast_blur = 1;
+        }
+    }
     for (int l = 0; l < G.L; l++) {
         G.lv[l].key_off = key_off;
         G.lv[l].key_cap = G.lv[l].ncells * cell_cap;
@@ -1704,6 +1760,15 @@ static hipError_t launch_blur_levels(orbg_ctx *c, hipStream_t st, const uint8_t 
 {
     const int32_t *b2 = c->tile_base.data();
     hipError_t e = hipSuccess;
+    if (l1 <= l0) return e;
+    const OrbgGeom &G = c->geom;
+    if (G.fast_blur) {  // the FAST cells blurred the interior: the rest of levels [l0, l1)
+        const int tpf = G.lv[l1 - 1].bt_off + G.lv[l1 - 1].bt_cnt - G.lv[l0].bt_off;
+        PROF_LAUNCH(c, "blur",
+                    e = launch_blur_border(st, c->d_geom, tpf, d_imgs, fs, pitch, c->d_pyr,
+                                           c->d_blur, l0, l1, B));
+        return e;
+    }
     PROF_LAUNCH(c, "blur",
                 e = launch_blur2(st, c->d_geom, c->d_tile_base, d_imgs, fs, pitch, c->d_pyr,
                                  c->d_blur, b2[l0], b2[l1] - b2[l0], B));
@@ -1730,8 +1795,8 @@ static hipError_t launch_fast_cells(orbg_ctx *c, hipStream_t st, const uint8_t *
     }
     PROF_LAUNCH(c, "fast_cells",
                 e = launch_fast2(G.fc2_p4, 4 * G.fc2_wave_bytes, st, c->d_geom, c->d_cells, d_imgs,
-                                 fs, pitch, c->d_pyr, c->d_ctab, c->d_cell_cnt, c->d_cell_kp, B,
-                                 cb, cn));
+                                 fs, pitch, c->d_pyr, c->d_ctab, c->d_cell_cnt, c->d_cell_kp,
+                                 G.fast_blur ? c->d_blur : nullptr, B, cb, cn));
     return e;
 }
 
@@ -2437,6 +2502,23 @@ extern "C" int orbg_get_quadtree_caps(const orbg_ctx *c, int32_t *first_cap, int
     if (first_cap) *first_cap = c->oct_dims[2].kcap;
     if (level0_cap) *level0_cap = c->oct_dims[0].kcap;
     if (upper_cap) *upper_cap = c->oct_dims[1].kcap;
+    return ORBG_OK;
+}
+
+extern "C" int orbg_get_blur_plan(const orbg_ctx *c, int32_t *fused, int64_t *interior_px,
+                                  int64_t *border_px)
+{
+    if (!c) return set_err(ORBG_EINVAL, "ctx is NULL");
+    if (c->gw <= 0) return set_err(ORBG_EINVAL, "no image size planned yet");
+    const OrbgGeom &G = c->geom;
+    int64_t in = 0, all = 0;
+    for (int l = 0; l < G.L; l++) {
+        all += (int64_t)G.lv[l].w * G.lv[l].h;
+        if (G.fast_blur) in += (int64_t)(G.lv[l].bx1 - G.lv[l].bx0) * (G.lv[l].by1 - G.lv[l].by0);
+    }
+    if (fused) *fused = G.fast_blur;
+    if (interior_px) *interior_px = in;
+    if (border_px) *border_px = all - in;
     return ORBG_OK;
 }
 

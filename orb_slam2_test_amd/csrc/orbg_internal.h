@@ -93,6 +93,12 @@ struct OrbgLevel {
     float scale;                  // mvScaleFactor[l]
     int32_t patch_size;           // int(PATCH_SIZE * scale)
     int32_t oct_kcap, oct_acap2;  // this level's k_octree_lds launch: candidate / cell caps
+    // GaussianBlur fused into k_fast2 (G.fast_blur): the FAST cells blur the rectangle
+    // [bx0, bx1) x [by0, by1) (their detection regions, from the first dword boundary at or
+    // after the regions' left edge 19 to the first after their right edge) from their window
+    // tiles; k_blur_border the rest of the level, bt_cnt tasks (4 columns x 8 rows) from
+    // bt_off on in a frame's task list
+    int32_t bx0, by0, bx1, by1, bt_off, bt_cnt;
 };
 
 struct OrbgGeom {
@@ -112,6 +118,8 @@ struct OrbgGeom {
     int32_t fc2_wave_bytes;       // k_fast2 LDS bytes per wave
     int32_t fc2_sc_off, fc2_list_off;  // k_fast2 regions within a wave's LDS
     int32_t fc2_list_cap;         // k_fast2 pretest list entries per wave
+    int32_t fast_blur;            // 1: k_fast2 blurs its cells' regions (OrbgLevel bx1 / by1)
+    int32_t bt_total;             // k_blur_border tasks per frame (all levels)
     int32_t gk[7];
     int64_t pyr_frame;            // bytes per frame of d_pyr
     int64_t blur_frame;

@@ -1,7 +1,7 @@
 """rocprof kernel name -> bench.py kernel key (the PROF_LAUNCH names of liborbg)."""
 KEYS = {
     "k_pyramid": "resize", "k_resize": "resize", "k_fast_cells": "fast_cells", "k_fast2": "fast_cells", "k_fast_rows": "fast_cells",
-    "k_blur": "blur", "k_blur2": "blur", "k_octree_lds": "octree", "k_octree": "octree_big",
+    "k_blur": "blur", "k_blur2": "blur", "k_blur_border": "blur", "k_octree_lds": "octree", "k_octree": "octree_big",
     "k_orient_desc": "orient_desc", "k_knn2_pairs": "knn2", "k_knn2_pairs_i8": "knn2", "k_init_cands_pairs": "init_cands",
     "k_init_resolve_pairs": "init_resolve", "k_stereo_rows": "stereo_rows",
     "k_stereo_match": "stereo_match", "k_stereo_rows_match": "stereo_match",
