@@ -73,21 +73,30 @@ __device__ __forceinline__ int rec_cnt(unsigned long long r) { return (int)((r >
 __device__ __forceinline__ int rec_seq(unsigned long long r) { return (int)((r >> 32) & 0xFFFF); }
 __device__ __forceinline__ int rec_depth(unsigned long long r) { return (int)((r >> 48) & 0xFF); }
 
-// exclusive block scan for OCT_T threads (8 waves); sh: 16 ints; two barriers
-__device__ int oct_scan(int v, int *total, int *sh)
+// exclusive block scan for OCT_T threads (8 waves); sh: 16 ints, used as two halves in turn
+// (par, flipped by every call; every thread makes the same calls): one barrier.  A wave that
+// reaches the next-but-one scan has passed the next scan's barrier, which no wave reaches
+// before it read this scan's half, so the half is free again (ORBG_OCT_SCAN_2BAR=1: the
+// round-5 form, one half and a second barrier)
+#ifndef ORBG_OCT_SCAN_2BAR
+#define ORBG_OCT_SCAN_2BAR 0
+#endif
+__device__ int oct_scan(int v, int *total, int *sh, int &par)
 {
     const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    int *h = ORBG_OCT_SCAN_2BAR ? sh : sh + (OCT_T / 64) * par;
+    par ^= 1;
     int x = wave_incl_scan(v);
-    if (lane == 63) sh[wid] = x;
+    if (lane == 63) h[wid] = x;
     __syncthreads();
     int before = 0, tot = 0;
 #pragma unroll
     for (int i = 0; i < OCT_T / 64; i++) {
-        const int s = sh[i];
+        const int s = h[i];
         before += (i < wid) ? s : 0;
         tot += s;
     }
-    __syncthreads();
+    if (ORBG_OCT_SCAN_2BAR) __syncthreads();
     *total = tot;
     return before + x - v;
 }
@@ -274,6 +283,7 @@ __global__ __launch_bounds__(OCT_T) void k_octree_lds(
     // the split pair's second launch: nothing to take unless the first flagged a level
     // (err_flag[3], cleared ahead of the pair by launch_octree_l0)
     if (D.kmin > 0 && err_flag[3] == 0) return;
+    int spar = 0;  // oct_scan's half of S.red
     const int l = D.level0 + blockIdx.y, f = blockIdx.x, tid = threadIdx.x;
     const OrbgLevel &lv = g->lv[l];
     const int N = lv.nfeat, nIni = lv.nini;
@@ -301,7 +311,7 @@ __global__ __launch_bounds__(OCT_T) void k_octree_lds(
     for (int c0 = 0; c0 < ncells; c0 += OCT_T) {
         const int c = c0 + tid;
         int tot;
-        const int off = oct_scan(c < ncells ? ccount[c] : 0, &tot, S.red) + n;
+        const int off = oct_scan(c < ncells ? ccount[c] : 0, &tot, S.red, spar) + n;
         if (c < ncells) V.aux[c] = V.coff[c] = (uint16_t)min(off, 65535);
         n += tot;
     }
@@ -367,7 +377,7 @@ __global__ __launch_bounds__(OCT_T) void k_octree_lds(
         int sum = 0;
         for (int i = 0; i < PER; i++) sum += (int)(wb[i] & 0xFFFF) + (int)(wb[i] >> 16);
         int tot;
-        int run = oct_scan(sum, &tot, S.red);
+        int run = oct_scan(sum, &tot, S.red, spar);
         for (int i = 0; i < PER; i++) {
             const uint32_t w = wb[i];
             const int a = (int)(w & 0xFFFF), b = (int)(w >> 16);
@@ -447,7 +457,7 @@ __global__ __launch_bounds__(OCT_T) void k_octree_lds(
                     }
                 }
                 int t;  // both totals from one scan (each < 2^16: e, m <= 4 per node)
-                oct_scan(e | (m << 16), &t, S.red);
+                oct_scan(e | (m << 16), &t, S.red, spar);
                 tot_e += t & 0xFFFF;
                 nexp += t >> 16;
             }
@@ -464,7 +474,7 @@ __global__ __launch_bounds__(OCT_T) void k_octree_lds(
                 const int i = ch * OCT_T + tid;
                 const int e = ee[ch], sp = spp[ch];
                 int tot;
-                const int pre = oct_scan(e | (sp << 16), &tot, S.red) + run;
+                const int pre = oct_scan(e | (sp << 16), &tot, S.red, spar) + run;
                 const int E = pre & 0xFFFF, splits_before = pre >> 16;
                 if (i < alive) {
                     const unsigned long long r = V.list(cur)[i];
@@ -525,7 +535,7 @@ __global__ __launch_bounds__(OCT_T) void k_octree_lds(
                     fl = rec_cnt(r) > 1 && sq >= vbase && sq < vend;
                 }
                 int tot;
-                const int o = oct_scan(fl, &tot, S.red) + np;
+                const int o = oct_scan(fl, &tot, S.red, spar) + np;
                 if (fl)
                     V.sortv[o] = ((unsigned long long)rec_cnt(r) << 32) |
                                  ((unsigned long long)rec_seq(r) << 16) | (unsigned)i;
@@ -563,7 +573,7 @@ __global__ __launch_bounds__(OCT_T) void k_octree_lds(
                                               (unsigned long long)b[2] << 16 | (unsigned)b[1];
                     }
                     int tot;
-                    const int incl = oct_scan(dl, &tot, S.red) + run + dl;
+                    const int incl = oct_scan(dl, &tot, S.red, spar) + run + dl;
                     if (p < np && alive + incl >= N) atomicMin(&S.s_nproc, p + 1);
                     run += tot;
                 }
@@ -583,7 +593,7 @@ __global__ __launch_bounds__(OCT_T) void k_octree_lds(
                     V.aux[pos] = 1;  // processed parent
                 }
                 int t;
-                oct_scan(e, &t, S.red);
+                oct_scan(e, &t, S.red, spar);
                 tot_e += t;
             }
             {
@@ -599,7 +609,7 @@ __global__ __launch_bounds__(OCT_T) void k_octree_lds(
                         for (int q = 0; q < 4; q++) e += b[q + 1] > b[q];
                     }
                     int tot;
-                    const int E = oct_scan(e, &tot, S.red) + run;
+                    const int E = oct_scan(e, &tot, S.red, spar) + run;
                     if (p < nproc) {
                         const int blk = tot_e - E - e;
                         int k = 0;
@@ -619,7 +629,7 @@ __global__ __launch_bounds__(OCT_T) void k_octree_lds(
                     const int i = i0 + tid;
                     const int fl = (i < alive) ? (int)V.aux[i] : 0;
                     int tot;
-                    const int before = oct_scan(fl, &tot, S.red) + runp;
+                    const int before = oct_scan(fl, &tot, S.red, spar) + runp;
                     if (i < alive && !fl) V.list(nxt)[tot_e + i - before] = V.list(cur)[i];
                     runp += tot;
                 }
@@ -712,7 +722,7 @@ __global__ __launch_bounds__(OCT_T) void k_octree_lds(
         int sum = 0;
         for (int t = t0; t < t1; t++) sum += (int)tcnt[t];
         int tot;
-        int run = oct_scan(sum, &tot, S.red);
+        int run = oct_scan(sum, &tot, S.red, spar);
         for (int t = t0; t < t1; t++) {
             const int c = (int)tcnt[t];
             tcnt[t] = (uint32_t)run;
