@@ -84,3 +84,51 @@ def test_blur_batch_padded_pitch(oracle):
             if l == 0:
                 assert np.array_equal(pyr, frames[b, :, :w])
             assert np.array_equal(ext.get_blurred_level(b, l), oracle.gauss7(pyr)), (b, l)
+
+
+def _with_env(env, fn):
+    import os
+    old = {k: os.environ.get(k) for k in env}
+    os.environ.update(env)
+    try:
+        return fn()
+    finally:
+        for k, v in old.items():
+            if v is None:
+                os.environ.pop(k, None)
+            else:
+                os.environ[k] = v
+
+
+@pytest.mark.parametrize("h,w", [(376, 1241), (90, 257), (120, 200), (480, 640)])
+def test_blur_fused_into_fast_cells(oracle, h, w):
+    """ORBG_FAST_BLUR=1 (opt-in): the FAST cells blur their detection regions from
+    their window tiles (k_fast2<P4, true>) and k_blur_border the rest of every level: the same
+    bytes as the oracle's GaussianBlur, and the same keypoints / descriptors."""
+    nl = _levels_for(h, w)
+    img = _image(h, w, 900 + w)
+    ext = _with_env({"ORBG_FAST_BLUR": "1"}, lambda: ORBextractor(300, 1.2, nl, 20, 7))
+    _check(oracle, ext, img, nl)
+    fused, inner, border = ext.ctx.blur_plan()
+    assert fused and inner > 0 and border > 0
+    k, d = ext(img)
+    p = oracle.params(nfeatures=300, nlevels=nl)
+    r = oracle.extract(p, img)
+    assert np.array_equal(k, r["kps"]) and np.array_equal(d, r["desc"])
+
+
+def test_blur_fused_batch_padded_pitch(oracle):
+    import torch
+    B, h, w, pitch = 3, 160, 301, 307
+    frames = np.zeros((B, h, pitch), np.uint8)
+    for b in range(B):
+        frames[b, :, :w] = _image(h, w, 60 + b)
+    d = torch.from_numpy(frames).cuda()
+    nl = _levels_for(h, w)
+    ext = _with_env({"ORBG_FAST_BLUR": "1"}, lambda: ORBextractor(300, 1.2, nl, 20, 7, max_batch=B))
+    ext.extract_batch_device(d.data_ptr(), B, w, h, step=pitch, frame_stride=h * pitch)
+    ext.ctx.sync()
+    assert ext.ctx.blur_plan()[0]
+    for b in range(B):
+        for l in range(nl):
+            assert np.array_equal(ext.get_blurred_level(b, l), oracle.gauss7(ext.get_level(b, l))), (b, l)
