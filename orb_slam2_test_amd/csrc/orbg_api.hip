@@ -339,6 +339,7 @@ struct orbg_ctx {
     // earlier launch of the batch flagged a level for them (d_err[3], d_err[2]); 0 = they
     // always scan (A/B, and the parity test's ungated twin)
     bool oct_gate = true;
+    bool fast_blur_env = false;  // ORBG_FAST_BLUR (read at orbg_create): the fused blur plan
     bool serial = false;     // orbg_set_serial: no stream overlap (isolated kernel timing)
     // orbg_extract's single-frame hipGraphs: the whole frame (H2D of the pinned input, the
     // extraction's launches on the context and quadtree streams, k_pack_frame, D2H of the
@@ -1228,8 +1229,8 @@ static int plan(orbg_ctx *c, int w, int h, int batch)
     G.fast_blur = 0;
     G.bt_total = 0;
     {
-        const char *fe = getenv("ORBG_FAST_BLUR"), *pb = getenv("ORBG_PYR_BLUR");
-        bool ok = (fe && atoi(fe) != 0) && !(pb && atoi(pb) != 0) && !(fr_ok && c->fr_mode);
+        const char *pb = getenv("ORBG_PYR_BLUR");
+        bool ok = c->fast_blur_env && !(pb && atoi(pb) != 0) && !(fr_ok && c->fr_mode);
         for (int l = 0; l < G.L && ok; l++) {
             OrbgLevel &L = G.lv[l];
             int gx0 = 1 << 30, gy0 = 1 << 30, gx1 = 0, gy1 = 0;
@@ -1554,6 +1555,8 @@ extern "C" int orbg_create(int device, const orbg_params *p, orbg_ctx **out)
         c->blur_side = bs ? atoi(bs) != 0 : false;
         const char *og = getenv("ORBG_OCT_GATE");
         c->oct_gate = !og || atoi(og) != 0;
+        const char *fb = getenv("ORBG_FAST_BLUR");
+        c->fast_blur_env = fb && atoi(fb) != 0;
         const char *bg = getenv("ORBG_BIG_SIDE");
         c->big_side = c->fstream && (bg ? atoi(bg) != 0 : false);
         if (c->big_side)
