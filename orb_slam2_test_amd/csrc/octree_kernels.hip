@@ -418,16 +418,19 @@ __global__ __launch_bounds__(OCT_T) void k_octree_lds(
             if (cnt > 0) V.list(0)[a++] = rec_make(S.rootlo[r], cnt, 0, 0);
         }
         S.s_alive = a;
-        S.s_cur = 0;
-        S.s_seq = 1;  // roots never enter vSizeAndPointerToNode
         S.s_err = 0;
-        S.s_phase2 = 0;
     }
     __syncthreads();
+    // the list state is workgroup-uniform and every thread derives it from the scans' totals,
+    // so it lives in registers (no tid-0 update and barrier per pass); S.s_err collects the
+    // depth errors any thread may raise, read after each pass's barrier
+    int st_alive = S.s_alive, st_cur = 0, st_seq = 1;  // roots never enter vSizeAndPointerToNode
+    int st_vbase = 0, st_vend = 0, st_err = 0;
+    bool st_phase2 = false;
 
     // ================= phase 1 passes (:751-852) =================
     while (true) {
-        const int alive = S.s_alive, cur = S.s_cur, nxt = cur ^ 1, seq0 = S.s_seq;
+        const int alive = st_alive, cur = st_cur, nxt = cur ^ 1, seq0 = st_seq;
         // sweep 1: children of every splitting node (kept in registers for sweep 2)
         constexpr int MAXCH = ORBG_OCT_ALIVE / OCT_T;
         int bb[MAXCH][5];
@@ -498,31 +501,28 @@ __global__ __launch_bounds__(OCT_T) void k_octree_lds(
             nsplit_total = run >> 16;
         }
         const int na = tot_e + alive - nsplit_total;
-        __syncthreads();
-        if (tid == 0) {
-            S.s_alive = na;
-            S.s_cur = nxt;
-            S.s_seq = seq0 + tot_e;
-            S.s_vbase = seq0;
-            S.s_vend = seq0 + tot_e;
-            if (na > D.acap || seq0 + tot_e > 65535) S.s_err = 5;
-        }
-        __syncthreads();
-        if (S.s_err) break;
+        __syncthreads();  // this pass's list writes (and any S.s_err) before the next pass
+        st_alive = na;
+        st_cur = nxt;
+        st_seq = seq0 + tot_e;
+        st_vbase = seq0;
+        st_vend = seq0 + tot_e;
+        st_err = S.s_err;
+        if (!st_err && (na > D.acap || seq0 + tot_e > 65535)) st_err = 5;
+        if (st_err) break;
         if (na >= N || na == alive) break;   // :849-852
         if (na + nexp * 3 > N) {              // :856
-            if (tid == 0) S.s_phase2 = 1;
-            __syncthreads();
+            st_phase2 = true;
             break;
         }
     }
 
     if (dbg_stop(3)) return;
     // ================= phase 2 rounds (:859-924) =================
-    if (S.s_phase2 && !S.s_err) {
+    if (st_phase2 && !st_err) {
         while (true) {
-            const int alive = S.s_alive, cur = S.s_cur, nxt = cur ^ 1, seq0 = S.s_seq;
-            const int vbase = S.s_vbase, vend = S.s_vend;
+            const int alive = st_alive, cur = st_cur, nxt = cur ^ 1, seq0 = st_seq;
+            const int vbase = st_vbase, vend = st_vend;
             // vPrevSizeAndPointerToNode: multi-key nodes created last round -> (cnt, seq, pos)
             int np = 0;
             for (int i0 = 0; i0 < alive; i0 += OCT_T) {
@@ -635,27 +635,25 @@ __global__ __launch_bounds__(OCT_T) void k_octree_lds(
                 }
             }
             const int na = tot_e + alive - nproc;
-            __syncthreads();
-            if (tid == 0) {
-                S.s_alive = na;
-                S.s_cur = nxt;
-                S.s_seq = seq0 + tot_e;
-                S.s_vbase = seq0;
-                S.s_vend = seq0 + tot_e;
-                if (na > D.acap || seq0 + tot_e > 65535) S.s_err = 7;
-            }
-            __syncthreads();
-            if (S.s_err) break;
+            __syncthreads();  // this round's list writes (and any S.s_err) before the next
+            st_alive = na;
+            st_cur = nxt;
+            st_seq = seq0 + tot_e;
+            st_vbase = seq0;
+            st_vend = seq0 + tot_e;
+            st_err = S.s_err;
+            if (!st_err && (na > D.acap || seq0 + tot_e > 65535)) st_err = 7;
+            if (st_err) break;
             if (na >= N || na == alive) break;  // :921-922
         }
     }
 
     if (dbg_stop(4)) return;
     // ================= best key per node, list order (:932-948) =================
-    const int alive = S.s_alive, cur = S.s_cur;
-    if (S.s_err) {
+    const int alive = st_alive, cur = st_cur;
+    if (st_err) {
         if (tid == 0) {
-            atomicOr(err_flag, 1 << S.s_err);
+            atomicOr(err_flag, 1 << st_err);
             atomicMin(err_flag + 1, f);
             lvl_cnt[(int64_t)f * g->L + l] = 0;
         }
