@@ -84,6 +84,10 @@ struct OrbgKeypointDev {
 #define ORBG_OD_PFD 2  // slots whose loads are in flight ahead of the one being summed / sampled (1: -0.4% per step)
 #endif
 #define OD_PFD ORBG_OD_PFD
+#ifndef ORBG_OD_PK
+#define ORBG_OD_PK 1  // rBRIEF sample rotation on packed f32 pairs (0: scalar ops)
+#endif
+typedef float od_f2 __attribute__((ext_vector_type(2)));
 #ifndef ORBG_OD_EARLYC
 #define ORBG_OD_EARLYC 0  // phase C's first neighbourhood loads (<= OD_PFD) issued during phase A's last slots (1: orient +1.3%, 2: +16%, spills; r05k A/B)
 #endif
@@ -362,17 +366,34 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(ORBG_OD_WPE
         // all 8 sample offsets first, then the 8 LDS reads in flight together, then the 4
         // ballots
         int off[8];
+#if ORBG_OD_PK
+        // (ry, rx) as one packed pair: v_pk_mul / v_pk_add (v_pk_fma) process both lanes of a
+        // pair per instruction with the scalar ops' IEEE rounding; rx = px a + py (-b) is
+        // px a - py b exactly (negation is exact)
+        const od_f2 ba = {b, a}, anb = {a, -b}, MM = {M, M};
+#endif
 #pragma unroll
         for (int t = 0; t < 4; t++) {
 #pragma unroll
             for (int s = 0; s < 2; s++) {
                 const float px = (float)(int8_t)(pt[t] >> (16 * s));
                 const float py = (float)(int8_t)(pt[t] >> (16 * s + 8));
+#if ORBG_OD_PK
+                const od_f2 P = {px, px}, Q = {py, py};
+                const od_f2 q = Q * anb;
+                const od_f2 r = (BFMA ? __builtin_elementwise_fma(P, ba, q) : P * ba + q) + MM;
+                // the elements through float copies: __builtin_bit_cast of a vector element
+                // (r.y) reads element 0 with this clang
+                const float ryM = r.x, rxM = r.y;
+                const uint32_t iy = __builtin_bit_cast(uint32_t, ryM);
+                const uint32_t ix = __builtin_bit_cast(uint32_t, rxM);
+#else
                 const float t0 = px * b, t1 = py * a, t2 = px * a, t3 = py * b;
                 const float ry = BFMA ? fmaf(px, b, t1) : t0 + t1;
                 const float rx = BFMA ? fmaf(px, a, -t3) : t2 - t3;
                 const uint32_t iy = __builtin_bit_cast(uint32_t, ry + M);
                 const uint32_t ix = __builtin_bit_cast(uint32_t, rx + M);
+#endif
                 off[2 * t + s] = (int)((iy & 0xFFFFFFu) * (uint32_t)OD_ROWB + ix + cbase);
             }
         }
