@@ -14,6 +14,7 @@
 namespace orbg {
 
 #define BLUR2_TW 244  // output columns per wave (4 per lane; the last 3 lanes supply data)
+#define BLUR2_TW_T 240  // the same for tiled output: 15 whole 16-px tiles (lanes 60..63 supply data)
 #ifndef ORBG_BLUR2_SEG
 #define ORBG_BLUR2_SEG 32  // output rows per wave
 #endif
@@ -112,16 +113,27 @@ __device__ __forceinline__ void blur2_column(const Blur2Weights &k, Loader &&loa
 // Rows at or past `yend` are not stored (the store range ends there: k_pyramid's bands store
 // only their own rows; their source rows past yend + 3 may be another band's and are never used
 // by a stored output).
-template <int SEG>
+// TILED (k_blur2 with G.blur_tiled): `dst` is stored as 16 x 8-px tiles of 128 bytes, tile
+// (tx, ty) at ty * 8 * dpitch + tx * 128, pixel (x, y) at byte (y & 7) * 16 + (x & 15) of it --
+// the level's row-major footprint with its rows rounded up to 8 (k_orient_desc's rBRIEF
+// neighbourhood then touches one cache line per tile row of a tile instead of one or two per
+// image row).  The wave is BLUR2_TW_T = 15 tiles wide; its output rows go through `wlds` (8 x
+// 64 dwords of this wave's LDS) and every 8 rows leave as two dwordx4 stores of whole tile rows
+// (each instruction writes 8 whole 128-byte lines; dword stores into the tiles cost k_blur2
+// +79%, profiles/r06r_blur_tiled_ab.txt).  y0 is a multiple of 8; rows in [yend, yend rounded
+// up to 8) land in the last tile row's padding.
+template <int SEG, bool TILED = false>
 __device__ __forceinline__ void blur2_tile(const Blur2Weights &k, const uint8_t *src, int pitch,
                                            int W, int H, uint8_t *dst, int dpitch, int tx, int y0,
-                                           int yend, int lane)
+                                           int yend, int lane, uint32_t *wlds = nullptr)
 {
     constexpr int PF = ORBG_BLUR2_ROWPF;
-    const int gx = tx * BLUR2_TW + 4 * lane;
-    const bool owner = 4 * lane < BLUR2_TW && gx < W;
+    constexpr int TW = TILED ? BLUR2_TW_T : BLUR2_TW;
+    static_assert(!TILED || SEG % 8 == 0, "tiled output: whole tile rows per wave");
+    const int gx = tx * TW + 4 * lane;
+    const bool owner = 4 * lane < TW && gx < W;
     // row ends (REFLECT_101 at x = -1 and x = W): window byte b is column gx - 4 + b
-    const bool left_wave = tx == 0, right_wave = (tx + 1) * BLUR2_TW + 8 > W;
+    const bool left_wave = tx == 0, right_wave = (tx + 1) * TW + 8 > W;
     const bool is_left = gx == 0;
     const int m = W - gx;  // right lanes: m in 1..7 need reflected bytes inside the window
     uint32_t sel1 = 0x07060504u, sel2 = 0x07060504u;  // identity: w1, w2
@@ -156,7 +168,7 @@ __device__ __forceinline__ void blur2_tile(const Blur2Weights &k, const uint8_t 
     // 4 columns pass W writes the rest of its dword into the row padding (pitch >= W
     // rounded up to 64; the padding is never read).
     const __amdgpu_buffer_rsrc_t drsrc = __builtin_amdgcn_make_buffer_rsrc(
-        (void *)dst, (short)0, yend * dpitch, 0x00020000);
+        (void *)dst, (short)0, (TILED ? (yend + 7) & ~7 : yend) * dpitch, 0x00020000);
     const int lane_off = owner ? gx : (1 << 30);
     // interior tiles (every source row inside the level, the last one above the level's last
     // row) need no REFLECT_101 row index and no straddle test: the row offset is affine in i
@@ -215,8 +227,25 @@ __device__ __forceinline__ void blur2_tile(const Blur2Weights &k, const uint8_t 
                 }
             },
             [&](int o, uint32_t word) {
-                __builtin_amdgcn_raw_buffer_store_b32(word, drsrc, lane_off + (y0 + o) * dpitch,
-                                                      0, 0);
+                if (!TILED) {
+                    __builtin_amdgcn_raw_buffer_store_b32(word, drsrc, lane_off + (y0 + o) * dpitch,
+                                                          0, 0);
+                    return;
+                }
+                wlds[(o & 7) * 64 + lane] = word;
+                if ((o & 7) != 7) return;
+                wave_sync_lds();
+                const int tyoff = ((y0 + (o & ~7)) >> 3) * (8 * dpitch);
+#pragma unroll
+                for (int h = 0; h < 2; h++) {  // lane -> (tile t, tile row r)
+                    const int idx = lane + 64 * h, t = idx >> 3, r = idx & 7;
+                    typedef uint32_t b2_v4u __attribute__((ext_vector_type(4)));
+                    const b2_v4u v = *(const b2_v4u *)(wlds + r * 64 + 4 * t);
+                    const int x = tx * TW + 16 * t;
+                    const int off = (t < TW / 16 && x < W) ? tyoff + (x >> 4) * 128 + r * 16 : (1 << 30);
+                    __builtin_amdgcn_raw_buffer_store_b128(v, drsrc, off, 0, 0);
+                }
+                wave_sync_lds();  // the rows' reads before the next 8 rows overwrite them
             });
     };
     // (and the weight sum: legacy 257-sum tables saturate instead of taking byte 2)

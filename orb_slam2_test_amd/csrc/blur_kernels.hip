@@ -48,12 +48,17 @@ __global__ __launch_bounds__(256) void k_blur2(
     const int tt = t - task_base[l];
     const OrbgLevel &lv = g->lv[l];
     const int W = lv.w, H = lv.h;
-    const int ntx = (W + BLUR2_TW - 1) / BLUR2_TW;
+    const int TW = g->blur_tiled ? BLUR2_TW_T : BLUR2_TW;
+    const int ntx = (W + TW - 1) / TW;
     const int ty = tt / ntx, tx = tt - ty * ntx;
     const uint8_t *src = l == 0 ? img0 + f * img_fs : pyr + f * g->pyr_frame + lv.pyr_off;
     const int pitch = l == 0 ? img_pitch : lv.pitch;
     uint8_t *dst = blur + f * g->blur_frame + lv.blur_off;
-    blur2_tile<SEG>(k, src, pitch, W, H, dst, lv.pitch, tx, ty * SEG, H, lane);
+    __shared__ uint32_t rows[4][8 * 64];  // tiled output: each wave's 8 staged rows
+    if (g->blur_tiled)  // uniform
+        blur2_tile<SEG, true>(k, src, pitch, W, H, dst, lv.pitch, tx, ty * SEG, H, lane, rows[wv]);
+    else
+        blur2_tile<SEG, false>(k, src, pitch, W, H, dst, lv.pitch, tx, ty * SEG, H, lane);
 }
 
 // k_blur_border: the GaussianBlur of every pixel the fused FAST cells do not blur (k_fast2
@@ -166,7 +171,7 @@ hipError_t launch_blur_border(hipStream_t st, const OrbgGeom *g, int tasks_per_f
 }
 
 int blur2_seg() { return ORBG_BLUR2_SEG; }
-int blur2_tw() { return BLUR2_TW; }
+int blur2_tw(bool tiled) { return tiled ? BLUR2_TW_T : BLUR2_TW; }
 
 // tiles [t_begin, t_begin + t_count) of every frame
 hipError_t launch_blur2(hipStream_t st, const OrbgGeom *g, const int32_t *task_base,

@@ -46,7 +46,7 @@ __global__ void k_pyramid(PyrArgs, const OrbgGeom *, const uint4 *, const int4 *
                           int);
 // blur_kernels.hip
 int blur2_seg();
-int blur2_tw();
+int blur2_tw(bool tiled);
 hipError_t launch_blur2(hipStream_t st, const OrbgGeom *g, const int32_t *task_base,
                         const uint8_t *img0, int64_t img_fs, int img_pitch, const uint8_t *pyr,
                         uint8_t *blur, int t_begin, int t_count, int nframes);
@@ -65,7 +65,7 @@ hipError_t launch_blur_border(hipStream_t st, const OrbgGeom *g, int tasks_per_f
                               const uint8_t *img0, int64_t img_fs, int img_pitch,
                               const uint8_t *pyr, uint8_t *blur, int l0, int l1, int nframes);
 struct OrbgKeypointDev;
-hipError_t launch_orient_desc(bool bfma, dim3 grid, hipStream_t st, const OrbgGeom *g,
+hipError_t launch_orient_desc(bool bfma, bool tiled, dim3 grid, hipStream_t st, const OrbgGeom *g,
                               const uint8_t *img0, int64_t img_fs, int img_pitch,
                               const uint8_t *pyr, const uint8_t *blur, const uint4 *odtab,
                               const uint32_t *lvl_kp, const uint16_t *lvl_idx,
@@ -340,6 +340,7 @@ struct orbg_ctx {
     // always scan (A/B, and the parity test's ungated twin)
     bool oct_gate = true;
     bool fast_blur_env = false;  // ORBG_FAST_BLUR (read at orbg_create): the fused blur plan
+    bool blur_tiled_env = true;  // ORBG_BLUR_TILED (read at orbg_create; 0: row-major blur)
     bool serial = false;     // orbg_set_serial: no stream overlap (isolated kernel timing)
     // orbg_extract's single-frame hipGraphs: the whole frame (H2D of the pinned input, the
     // extraction's launches on the context and quadtree streams, k_pack_frame, D2H of the
@@ -917,6 +918,13 @@ static int plan(orbg_ctx *c, int w, int h, int batch)
         if (lw[l] - 2 * ORBG_MIN_BORDER >= 4096 || lh[l] - 2 * ORBG_MIN_BORDER >= 4096)
             return set_err(ORBG_ENOTSUP, "level %d too large (%dx%d)", l, lw[l], lh[l]);
     }
+    // tiled blurred levels (blur_device.h blur2_tile TILED; k_orient_desc's rBRIEF loads):
+    // k_blur2 must be the only writer -- the k_pyramid blur (ORBG_PYR_BLUR) and the fused
+    // FAST-cell blur (opt-in ORBG_FAST_BLUR) write row-major
+    {
+        const char *pb = getenv("ORBG_PYR_BLUR");
+        G.blur_tiled = c->blur_tiled_env && !c->fast_blur_env && !(pb && atoi(pb) != 0);
+    }
     int64_t pyr_off = 0, blur_off = 0;
     int key_off = 0, node_off = 0, out_off = 0;
     std::vector<int32_t> tile_base, blur2_base;
@@ -1026,10 +1034,11 @@ static int plan(orbg_ctx *c, int w, int h, int batch)
             L.pyr_off = pyr_off;
             pyr_off += (int64_t)L.pitch * L.h;
         }
-        L.blur_off = blur_off;
-        blur_off += (int64_t)L.pitch * L.h;
-        blur2_base.push_back(blur2_tasks);  // k_blur2 (blur_kernels.hip): 244 x SEG wave tiles
-        blur2_tasks += ((L.w + blur2_tw() - 1) / blur2_tw()) * ((L.h + blur2_seg() - 1) / blur2_seg());
+        L.blur_off = blur_off;  // rows rounded up to 8: the tiled layout's footprint
+        blur_off += (int64_t)L.pitch * ((L.h + 7) & ~7);
+        blur2_base.push_back(blur2_tasks);  // k_blur2 (blur_kernels.hip): 244 (tiled 240) x SEG wave tiles
+        const int btw = blur2_tw(G.blur_tiled != 0);
+        blur2_tasks += ((L.w + btw - 1) / btw) * ((L.h + blur2_seg() - 1) / blur2_seg());
         // resize coefficient tables (cv::resize, INTER_LINEAR)
         if (l > 0) {
             const int sw = lw[l - 1], sh = lh[l - 1], dw = lw[l], dh = lh[l];
@@ -1269,6 +1278,7 @@ static int plan(orbg_ctx *c, int w, int h, int batch)
             G.fast_blur = 1;
         }
     }
+    if (G.fast_blur && G.blur_tiled) return set_err(ORBG_EINVAL, "fused blur with tiled levels");
     for (int l = 0; l < G.L; l++) {
         G.lv[l].key_off = key_off;
         G.lv[l].key_cap = G.lv[l].ncells * cell_cap;
@@ -1557,6 +1567,8 @@ extern "C" int orbg_create(int device, const orbg_params *p, orbg_ctx **out)
         c->oct_gate = !og || atoi(og) != 0;
         const char *fb = getenv("ORBG_FAST_BLUR");
         c->fast_blur_env = fb && atoi(fb) != 0;
+        const char *bt = getenv("ORBG_BLUR_TILED");
+        c->blur_tiled_env = !bt || atoi(bt) != 0;
         const char *bg = getenv("ORBG_BIG_SIDE");
         c->big_side = c->fstream && (bg ? atoi(bg) != 0 : false);
         if (c->big_side)
@@ -1890,7 +1902,7 @@ static int launch_extract_pipe(orbg_ctx *c, const uint8_t *d_imgs, int B, int pi
     c->d_desc = c->desc_slot[s];
     c->d_counts = c->counts_slot[s];
     PROF_LAUNCH(c, "orient_desc",
-                launch_orient_desc(G.brief_fma != 0,
+                launch_orient_desc(G.brief_fma != 0, G.blur_tiled != 0,
                                    dim3((G.out_frame + 4 * ORBG_OD_KPW - 1) / (4 * ORBG_OD_KPW) * B),
                                    st, c->d_geom, d_imgs, fs, pitch, c->d_pyr,
                                    c->d_blur, c->d_odtab, c->d_lvl_kp, c->d_lvl_idx, c->d_lvl_cnt,
@@ -2027,7 +2039,7 @@ static int launch_extract(orbg_ctx *c, const uint8_t *d_imgs, int B, int pitch, 
     c->d_desc = c->desc_slot[s];
     c->d_counts = c->counts_slot[s];
     PROF_LAUNCH(c, "orient_desc",
-                launch_orient_desc(G.brief_fma != 0,
+                launch_orient_desc(G.brief_fma != 0, G.blur_tiled != 0,
                                    dim3((G.out_frame + 4 * ORBG_OD_KPW - 1) / (4 * ORBG_OD_KPW) * B),
                                    st, c->d_geom, d_imgs, fs, pitch, c->d_pyr,
                                    c->d_blur, c->d_odtab, c->d_lvl_kp, c->d_lvl_idx, c->d_lvl_cnt, (OrbgKeypointDev *)c->d_kps,
@@ -2448,8 +2460,20 @@ extern "C" int orbg_get_blurred_level(orbg_ctx *c, int frame, int level, uint8_t
     if (dst_step < (size_t)L.w) return set_err(ORBG_EINVAL, "dst_step too small");
     int rc = sync_all(c);
     if (rc) return rc;
-    HIPCHK(hipMemcpy2D(dst, dst_step, c->d_blur + frame * c->geom.blur_frame + L.blur_off,
-                       L.pitch, L.w, L.h, hipMemcpyDeviceToHost));
+    const uint8_t *src = c->d_blur + frame * c->geom.blur_frame + L.blur_off;
+    if (!c->geom.blur_tiled) {
+        HIPCHK(hipMemcpy2D(dst, dst_step, src, L.pitch, L.w, L.h, hipMemcpyDeviceToHost));
+        return ORBG_OK;
+    }
+    // tiled (blur2_tile TILED): the level's footprint, then its rows out of the tiles
+    const int h8 = (L.h + 7) & ~7;
+    std::vector<uint8_t> t((size_t)L.pitch * h8);
+    HIPCHK(hipMemcpy(t.data(), src, t.size(), hipMemcpyDeviceToHost));
+    for (int y = 0; y < L.h; y++)
+        for (int x0 = 0; x0 < L.w; x0 += 16)
+            memcpy(dst + (size_t)y * dst_step + x0,
+                   t.data() + (size_t)(y >> 3) * 8 * L.pitch + (size_t)(x0 >> 4) * 128 + (y & 7) * 16,
+                   std::min(16, L.w - x0));
     return ORBG_OK;
 }
 

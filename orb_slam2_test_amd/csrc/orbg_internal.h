@@ -120,6 +120,7 @@ struct OrbgGeom {
     int32_t fc2_list_cap;         // k_fast2 pretest list entries per wave
     int32_t fast_blur;            // 1: k_fast2 blurs its cells' regions (OrbgLevel bx1 / by1)
     int32_t bt_total;             // k_blur_border tasks per frame (all levels)
+    int32_t blur_tiled;           // 1: the blurred levels are 16 x 8-px tiles (blur2_tile TILED)
     int32_t gk[7];
     int64_t pyr_frame;            // bytes per frame of d_pyr
     int64_t blur_frame;

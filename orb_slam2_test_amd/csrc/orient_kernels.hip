@@ -69,6 +69,10 @@ struct OrbgKeypointDev {
 #define OD_R 18                 // rBRIEF sample radius bound: 13 * sqrt(2) rounded
 #define OD_SPAN (2 * OD_R + 1)  // 37 rows
 #define OD_ROWB 48              // staged row: 3 x 16 bytes (37 bytes + up to 3 of alignment)
+// tiled blurred levels (G.blur_tiled, TB): the staged row starts at the window's tile column
+// (16-px aligned) and holds bytes d .. d + 36 of it, d = window left & 15 <= 15: 52 bytes
+#define OD_ROWB_T 52
+#define OD_BPW ((OD_SPAN * OD_ROWB_T + 15) / 16)  // staged neighbourhood per wave (uint4)
 #define OD_KPW ORBG_OD_KPW      // slots per wave
 #ifndef ORBG_OD_LDSTAB
 #define ORBG_OD_LDSTAB 1
@@ -108,7 +112,7 @@ struct OdHostCopy {
     int32_t okp, ods;
 };
 
-template <bool BFMA, bool HC>
+template <bool BFMA, bool HC, bool TB>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(ORBG_OD_WPE, 8))) void k_orient_desc(
     const OrbgGeom *__restrict__ g, const uint8_t *__restrict__ img0, int64_t img_fs,
     int img_pitch, const uint8_t *__restrict__ pyr, const uint8_t *__restrict__ blur,
@@ -120,7 +124,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(ORBG_OD_WPE
 #if ORBG_OD_PRIO
     __builtin_amdgcn_s_setprio(ORBG_OD_PRIO);  // on the pipelined step's critical path (A/B)
 #endif
-    __shared__ uint4 bpatch[4][OD_SPAN * OD_ROWB / 16];
+    __shared__ uint4 bpatch[4][OD_BPW];
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
 #if ORBG_OD_LDSTAB
     __shared__ uint4 tab[4 * OD_TABW * 2];
@@ -194,8 +198,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(ORBG_OD_WPE
     // per-slot addresses, lane j = slot j, computed once: the slot loops take them by
     // v_readlane instead of scalar loads of the level records (which, after the LDS fences,
     // would be reissued per slot and wait on the LDS queue: both count in lgkmcnt)
-    int ppitch_l, bpitch_l;
-    int64_t poff_l, boff_l;  // patch centre (from img0 / pyr), neighbourhood top-left (blur)
+    int ppitch_l, bpitch_l, bxy_l = 0;
+    // patch centre (from img0 / pyr); neighbourhood top-left in the blurred level (TB: the
+    // level's first byte, and bxy_l = window top << 16 | window left)
+    int64_t poff_l, boff_l;
     {
         const OrbgLevel &lv = g->lv[lev_l];
         const int x = orbg_px(kl_l) + ORBG_MIN_BORDER, y = orbg_py(kl_l) + ORBG_MIN_BORDER;
@@ -203,8 +209,13 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(ORBG_OD_WPE
         ppitch_l = lev_l == 0 ? img_pitch : bpitch_l;
         poff_l = (lev_l == 0 ? (int64_t)f * img_fs : (int64_t)f * g->pyr_frame + lv.pyr_off) +
                  (int64_t)y * ppitch_l + x;
-        boff_l = (int64_t)f * g->blur_frame + lv.blur_off + (int64_t)(y - OD_R) * bpitch_l +
-                 (x - OD_R);
+        if (TB) {
+            boff_l = (int64_t)f * g->blur_frame + lv.blur_off;
+            bxy_l = (y - OD_R) << 16 | (x - OD_R);
+        } else {
+            boff_l = (int64_t)f * g->blur_frame + lv.blur_off + (int64_t)(y - OD_R) * bpitch_l +
+                     (x - OD_R);
+        }
     }
     const int64_t drow0 = (int64_t)f * g->frame_cap;  // this frame's first output row
     auto readlane64 = [](int64_t v, int j) -> int64_t {
@@ -215,18 +226,43 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(ORBG_OD_WPE
 
     // phase C's neighbourhood loads (defined here: the first OD_PFD are issued at the end of
     // phase A, so their latency overlaps A's last slots and phase B)
+    // Row-major blurred levels: lane (row pr, chunk pc) loads 16 bytes of the window row from
+    // its 4-byte-aligned start (sh = that alignment).  Tiled levels (TB, blur2_tile's layout:
+    // 16 x 8-px tiles of 128 bytes, tile rows 8 * pitch apart): lane (pr, pc) loads row pr of
+    // the window's tile column pc -- 16 bytes of one tile -- so the 37 rows touch about 19
+    // cache lines instead of about 50 (the loads' cost follows the lines an instruction
+    // touches, hit or miss: profiles/r06p_orient_load_exp.txt, r06q_orient_a2_ab.txt); sh = the
+    // window's column inside its first tile, and when sh >= 12 the window's last bytes lie in
+    // a fourth tile column: one more dword per row (d3, lanes < 37).
     struct Nbhd {
         uint4 v0, v1;
+        uint32_t d3;
         int sh;
+    };
+    auto tile_row = [](const uint8_t *lvb, int pitch, int y, int tcol) -> const uint8_t * {
+        return lvb + (int64_t)(y >> 3) * (8 * pitch) + tcol * 128 + (y & 7) * 16;
     };
     auto load_nbhd = [&](int j) -> Nbhd {
         const int bpitch = __builtin_amdgcn_readlane(bpitch_l, j);
         const uint8_t *bl0 = blur + readlane64(boff_l, j);
         Nbhd n;
-        n.sh = (int)((uintptr_t)bl0 & 3);
-        const uint8_t *bw = bl0 - n.sh;
-        n.v0 = *(const uint4 *)(bw + (int64_t)pr[0] * bpitch + 16 * pc[0]);
-        n.v1 = *(const uint4 *)(bw + (int64_t)pr[1] * bpitch + 16 * pc[1]);
+        if (TB) {
+            const int bxy = __builtin_amdgcn_readlane(bxy_l, j);
+            const int wx = bxy & 0xFFFF, wy = bxy >> 16;
+            n.sh = wx & 15;
+            const int tc = wx >> 4;
+            n.v0 = *(const uint4 *)tile_row(bl0, bpitch, wy + pr[0], tc + pc[0]);
+            n.v1 = *(const uint4 *)tile_row(bl0, bpitch, wy + pr[1], tc + pc[1]);
+            n.d3 = 0;
+            if (n.sh >= 12 && lane < OD_SPAN)  // wave-uniform slot test, then the 37 row lanes
+                n.d3 = *(const uint32_t *)tile_row(bl0, bpitch, wy + lane, tc + 3);
+        } else {
+            n.sh = (int)((uintptr_t)bl0 & 3);
+            const uint8_t *bw = bl0 - n.sh;
+            n.v0 = *(const uint4 *)(bw + (int64_t)pr[0] * bpitch + 16 * pc[0]);
+            n.v1 = *(const uint4 *)(bw + (int64_t)pr[1] * bpitch + 16 * pc[1]);
+            n.d3 = 0;
+        }
         return n;
     };
     Nbhd nbh[OD_PFD + 1];
@@ -343,9 +379,21 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(ORBG_OD_WPE
     for (int j = ORBG_OD_EARLYC; j < OD_PFD; j++) nbh[j] = load_nbhd(j);
 #pragma unroll
     for (int j = 0; j < OD_KPW; j++) {
+        constexpr int ROWB = TB ? OD_ROWB_T : OD_ROWB;
         wave_sync_lds();  // the previous slot's sample reads are done
-        *(uint4 *)(bp + pr[0] * OD_ROWB + 16 * pc[0]) = nbh[j % (OD_PFD + 1)].v0;
-        *(uint4 *)(bp + pr[1] * OD_ROWB + 16 * pc[1]) = nbh[j % (OD_PFD + 1)].v1;  // clamped lanes: same word twice
+        {
+            const Nbhd &n = nbh[j % (OD_PFD + 1)];
+            if (TB) {  // 52-byte rows: 4-byte aligned dword stores (ds_write2_b32)
+                uint32_t *r0 = (uint32_t *)(bp + pr[0] * ROWB + 16 * pc[0]);
+                uint32_t *r1 = (uint32_t *)(bp + pr[1] * ROWB + 16 * pc[1]);
+                r0[0] = n.v0.x, r0[1] = n.v0.y, r0[2] = n.v0.z, r0[3] = n.v0.w;
+                r1[0] = n.v1.x, r1[1] = n.v1.y, r1[2] = n.v1.z, r1[3] = n.v1.w;
+                if (n.sh >= 12 && lane < OD_SPAN) *(uint32_t *)(bp + lane * ROWB + 48) = n.d3;
+            } else {
+                *(uint4 *)(bp + pr[0] * ROWB + 16 * pc[0]) = n.v0;
+                *(uint4 *)(bp + pr[1] * ROWB + 16 * pc[1]) = n.v1;  // clamped lanes: same word twice
+            }
+        }
         wave_sync_lds();
         const int cur_bsh = nbh[j % (OD_PFD + 1)].sh;
         if (j + OD_PFD < OD_KPW) nbh[(j + OD_PFD) % (OD_PFD + 1)] = load_nbhd(j + OD_PFD);
@@ -354,11 +402,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(ORBG_OD_WPE
         // cvRound (round half to even) by the 1.5 * 2^23 shift: the float sum rounds r to an
         // integer, ties to even, so bits(r + M) = 0x4B400000 + cvRound(r) for |r| < 2^22 and its
         // low 24 bits are 2^22 + cvRound(r); one v_mad_u32_u24 then gives
-        // 48 (2^22 + ry) + bits(rx + M) = ry * 48 + rx + MK (mod 2^32), and the centre's byte
+        // ROWB (2^22 + ry) + bits(rx + M) = ry * ROWB + rx + MK (mod 2^32), and the centre's byte
         // index minus MK turns that into the sample's index in the staged neighbourhood
         constexpr float M = 12582912.0f;
-        constexpr uint32_t MK = (uint32_t)OD_ROWB * 0x400000u + 0x4B400000u;
-        const uint32_t cbase = (uint32_t)(OD_R * OD_ROWB + cur_bsh + OD_R) - MK;
+        constexpr uint32_t MK = (uint32_t)ROWB * 0x400000u + 0x4B400000u;
+        const uint32_t cbase = (uint32_t)(OD_R * ROWB + cur_bsh + OD_R) - MK;
         // opaque per slot: keeps the offset decode inside the loop (hoisted, the 16 floats
         // stay live through phase C and push the kernel past 64 VGPRs)
         int pt[4] = {pat[0], pat[1], pat[2], pat[3]};
@@ -394,7 +442,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(ORBG_OD_WPE
                 const uint32_t iy = __builtin_bit_cast(uint32_t, ry + M);
                 const uint32_t ix = __builtin_bit_cast(uint32_t, rx + M);
 #endif
-                off[2 * t + s] = (int)((iy & 0xFFFFFFu) * (uint32_t)OD_ROWB + ix + cbase);
+                off[2 * t + s] = (int)((iy & 0xFFFFFFu) * (uint32_t)ROWB + ix + cbase);
             }
         }
         int val[8];
@@ -416,7 +464,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(ORBG_OD_WPE
     }
 }
 
-hipError_t launch_orient_desc(bool bfma, dim3 grid, hipStream_t st, const OrbgGeom *g,
+hipError_t launch_orient_desc(bool bfma, bool tiled, dim3 grid, hipStream_t st, const OrbgGeom *g,
                               const uint8_t *img0, int64_t img_fs, int img_pitch,
                               const uint8_t *pyr, const uint8_t *blur, const uint4 *odtab,
                               const uint32_t *lvl_kp, const uint16_t *lvl_idx,
@@ -425,17 +473,21 @@ hipError_t launch_orient_desc(bool bfma, dim3 grid, hipStream_t st, const OrbgGe
                               size_t hc_okp, size_t hc_ods)
 {
     const OdHostCopy hc{hc_base, hc_err, (int32_t)hc_okp, (int32_t)hc_ods};
-#define OD_LAUNCH(BF, H)                                                                       \
-    hipLaunchKernelGGL((k_orient_desc<BF, H>), grid, dim3(256), 0, st, g, img0, img_fs,        \
+#define OD_LAUNCH(BF, H, T)                                                                    \
+    hipLaunchKernelGGL((k_orient_desc<BF, H, T>), grid, dim3(256), 0, st, g, img0, img_fs,     \
                        img_pitch, pyr, blur, odtab, lvl_kp, lvl_idx, lvl_cnt, kps, desc, counts, \
                        hc)
+#define OD_LAUNCH_T(BF, H)          \
+    if (tiled) OD_LAUNCH(BF, H, true); \
+    else OD_LAUNCH(BF, H, false)
     if (hc_base) {
-        if (bfma) OD_LAUNCH(true, true);
-        else OD_LAUNCH(false, true);
+        if (bfma) OD_LAUNCH_T(true, true);
+        else OD_LAUNCH_T(false, true);
     } else {
-        if (bfma) OD_LAUNCH(true, false);
-        else OD_LAUNCH(false, false);
+        if (bfma) OD_LAUNCH_T(true, false);
+        else OD_LAUNCH_T(false, false);
     }
+#undef OD_LAUNCH_T
 #undef OD_LAUNCH
     return hipGetLastError();
 }
