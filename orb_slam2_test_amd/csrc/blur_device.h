@@ -15,6 +15,11 @@ namespace orbg {
 
 #define BLUR2_TW 244  // output columns per wave (4 per lane; the last 3 lanes supply data)
 #define BLUR2_TW_T 240  // the same for tiled output: 15 whole 16-px tiles (lanes 60..63 supply data)
+// tiled output's LDS stage: 8 rows of 64 dwords, padded to 68 so the 16-byte reads of one
+// tile's 8 rows (lanes 8t .. 8t+7) fall on distinct banks (64 dwords apart they conflict 8-way)
+#ifndef BLUR2_LDS_ROW
+#define BLUR2_LDS_ROW 68
+#endif
 #ifndef ORBG_BLUR2_SEG
 #define ORBG_BLUR2_SEG 32  // output rows per wave
 #endif
@@ -118,7 +123,7 @@ __device__ __forceinline__ void blur2_column(const Blur2Weights &k, Loader &&loa
 // the level's row-major footprint with its rows rounded up to 8 (k_orient_desc's rBRIEF
 // neighbourhood then touches one cache line per tile row of a tile instead of one or two per
 // image row).  The wave is BLUR2_TW_T = 15 tiles wide; its output rows go through `wlds` (8 x
-// 64 dwords of this wave's LDS) and every 8 rows leave as two dwordx4 stores of whole tile rows
+// BLUR2_LDS_ROW dwords of this wave's LDS) and every 8 rows leave as two dwordx4 stores of whole tile rows
 // (each instruction writes 8 whole 128-byte lines; dword stores into the tiles cost k_blur2
 // +79%, profiles/r06r_blur_tiled_ab.txt).  y0 is a multiple of 8; rows in [yend, yend rounded
 // up to 8) land in the last tile row's padding.
@@ -232,7 +237,7 @@ __device__ __forceinline__ void blur2_tile(const Blur2Weights &k, const uint8_t 
                                                           0, 0);
                     return;
                 }
-                wlds[(o & 7) * 64 + lane] = word;
+                wlds[(o & 7) * BLUR2_LDS_ROW + lane] = word;
                 if ((o & 7) != 7) return;
                 wave_sync_lds();
                 const int tyoff = ((y0 + (o & ~7)) >> 3) * (8 * dpitch);
@@ -240,7 +245,7 @@ __device__ __forceinline__ void blur2_tile(const Blur2Weights &k, const uint8_t 
                 for (int h = 0; h < 2; h++) {  // lane -> (tile t, tile row r)
                     const int idx = lane + 64 * h, t = idx >> 3, r = idx & 7;
                     typedef uint32_t b2_v4u __attribute__((ext_vector_type(4)));
-                    const b2_v4u v = *(const b2_v4u *)(wlds + r * 64 + 4 * t);
+                    const b2_v4u v = *(const b2_v4u *)(wlds + r * BLUR2_LDS_ROW + 4 * t);
                     const int x = tx * TW + 16 * t;
                     const int off = (t < TW / 16 && x < W) ? tyoff + (x >> 4) * 128 + r * 16 : (1 << 30);
                     __builtin_amdgcn_raw_buffer_store_b128(v, drsrc, off, 0, 0);

@@ -54,7 +54,7 @@ __global__ __launch_bounds__(256) void k_blur2(
     const uint8_t *src = l == 0 ? img0 + f * img_fs : pyr + f * g->pyr_frame + lv.pyr_off;
     const int pitch = l == 0 ? img_pitch : lv.pitch;
     uint8_t *dst = blur + f * g->blur_frame + lv.blur_off;
-    __shared__ uint32_t rows[4][8 * 64];  // tiled output: each wave's 8 staged rows
+    __shared__ uint32_t rows[4][8 * BLUR2_LDS_ROW];  // tiled output: each wave's 8 staged rows
     if (g->blur_tiled)  // uniform
         blur2_tile<SEG, true>(k, src, pitch, W, H, dst, lv.pitch, tx, ty * SEG, H, lane, rows[wv]);
     else
