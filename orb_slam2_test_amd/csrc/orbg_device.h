@@ -7,21 +7,11 @@
 
 namespace orbg {
 
-__device__ __forceinline__ int wave_incl_scan(int x)
-{
-    const int lane = threadIdx.x & 63;
-#pragma unroll
-    for (int o = 1; o < 64; o <<= 1) {
-        int y = __shfl_up(x, o, 64);
-        if (lane >= o) x += y;
-    }
-    return x;
-}
-
 // inclusive wave64 prefix sum by DPP (row_shr 1..3 from the inputs, row_shr 4 / 8 with bank
-// masks, row_bcast 15 / 31 with row masks): seven adds, no LDS round trips (__shfl_up is a
-// ds_bpermute).  Integer adds, exact.
-__device__ __forceinline__ int wave_incl_scan_dpp(int x)
+// masks, row_bcast 15 / 31 with row masks): seven adds, no LDS round trips (a __shfl_up
+// ladder is six ds_bpermute round trips, on the critical path of every block scan: the
+// quadtree's chains of scans and barriers, the matchers' compactions).  Integer adds, exact.
+__device__ __forceinline__ int wave_incl_scan(int x)
 {
     int y = x;
     y += __builtin_amdgcn_update_dpp(0, x, 0x111, 0xf, 0xf, true);  // row_shr:1
@@ -33,6 +23,22 @@ __device__ __forceinline__ int wave_incl_scan_dpp(int x)
     y += __builtin_amdgcn_update_dpp(0, y, 0x143, 0xc, 0xf, false); // row_bcast:31, rows 2, 3
     return y;
 }
+__device__ __forceinline__ int wave_incl_scan_dpp(int x) { return wave_incl_scan(x); }
+
+// the round-5 form (a __shfl_up ladder), kept for A/B builds (-DORBG_SCAN_SHFL)
+__device__ __forceinline__ int wave_incl_scan_shfl(int x)
+{
+    const int lane = threadIdx.x & 63;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        int y = __shfl_up(x, o, 64);
+        if (lane >= o) x += y;
+    }
+    return x;
+}
+#ifdef ORBG_SCAN_SHFL
+#define wave_incl_scan wave_incl_scan_shfl
+#endif
 
 // inclusive wave prefix of small counts 0 <= x < 8 from three ballots (no shuffles);
 // *total = wave total
