@@ -31,6 +31,51 @@ void prof_begin(void *prof, hipStream_t s, const char *n, hipEvent_t *a);
 void prof_end(void *prof, hipStream_t s, const char *n, hipEvent_t a);
 bool prof_skip_name(const char *n);
 
+// reductions over a 16-lane row (the query groups of init_cands_block): every lane gets the
+// row's result by DPP row_ror 8 / 4 and quad_perm [2,3,0,1] / [1,0,3,2] (in the ALU; a
+// __shfl_xor ladder is four LDS-pipeline round trips per 32-bit step)
+#ifndef ORBG_ROW16_SHFL
+__device__ __forceinline__ int row16_sum(int x)
+{
+    x += __builtin_amdgcn_mov_dpp(x, 0x128, 0xf, 0xf, false);  // row_ror:8
+    x += __builtin_amdgcn_mov_dpp(x, 0x124, 0xf, 0xf, false);  // row_ror:4
+    x += __builtin_amdgcn_mov_dpp(x, 0x4e, 0xf, 0xf, false);   // quad_perm [2,3,0,1]
+    x += __builtin_amdgcn_mov_dpp(x, 0xb1, 0xf, 0xf, false);   // quad_perm [1,0,3,2]
+    return x;
+}
+__device__ __forceinline__ unsigned long long row16_min_u64(unsigned long long v)
+{
+    auto step = [&](auto CTRL) {
+        constexpr int c = decltype(CTRL)::value;
+        const uint32_t lo = __builtin_amdgcn_mov_dpp((int)(uint32_t)v, c, 0xf, 0xf, false);
+        const uint32_t hi = __builtin_amdgcn_mov_dpp((int)(uint32_t)(v >> 32), c, 0xf, 0xf, false);
+        const unsigned long long u = (unsigned long long)hi << 32 | lo;
+        v = u < v ? u : v;
+    };
+    step(std::integral_constant<int, 0x128>{});
+    step(std::integral_constant<int, 0x124>{});
+    step(std::integral_constant<int, 0x4e>{});
+    step(std::integral_constant<int, 0xb1>{});
+    return v;
+}
+#else  // the round-5 form, A/B builds
+__device__ __forceinline__ int row16_sum(int x)
+{
+#pragma unroll
+    for (int o = 8; o > 0; o >>= 1) x += __shfl_xor(x, o, 16);
+    return x;
+}
+__device__ __forceinline__ unsigned long long row16_min_u64(unsigned long long mn)
+{
+#pragma unroll
+    for (int o = 8; o > 0; o >>= 1) {
+        const unsigned long long u = __shfl_xor(mn, o, 16);
+        mn = u < mn ? u : mn;
+    }
+    return mn;
+}
+#endif
+
 #define TH_LOW 50
 #define HISTO_LENGTH 30
 
@@ -403,8 +448,7 @@ __device__ __forceinline__ void init_cands_block(const orbg_keypoint *__restrict
                 }
             }
         }
-#pragma unroll
-        for (int o = 8; o > 0; o >>= 1) cnt += __shfl_xor(cnt, o, 16);
+        cnt = row16_sum(cnt);
         // merge: K rounds of group-min over the lanes' sorted heads
         int head = 0;
         unsigned long long *out = topk + (size_t)i1 * ORBG_MATCH_TOPK;
@@ -413,12 +457,7 @@ __device__ __forceinline__ void init_cands_block(const orbg_keypoint *__restrict
 #pragma unroll
             for (int h = 0; h < ORBG_MATCH_TOPK; h++)
                 if (h == head) mine = loc[h];
-            unsigned long long mn = mine;
-#pragma unroll
-            for (int o = 8; o > 0; o >>= 1) {
-                const unsigned long long u = __shfl_xor(mn, o, 16);
-                mn = u < mn ? u : mn;
-            }
+            const unsigned long long mn = row16_min_u64(mine);
             if (mn != ~0ull && mine == mn) head++;  // keys are unique (index in low bits)
             if (act && sub == 0) out[k] = mn;
         }
