@@ -299,6 +299,11 @@ int orbg_get_quadtree_caps(const orbg_ctx *ctx, int32_t *first_cap, int32_t *lev
  * pointer may be NULL.  ORBG_EINVAL before any extraction. */
 int orbg_get_blur_plan(const orbg_ctx *ctx, int32_t *fused, int64_t *interior_px,
                        int64_t *border_px);
+/* the blurred levels' device layout of the last planned image size: *tiled = 1 for 16 x 8-pixel
+ * tiles of 128 bytes (k_blur2's default store form, read by the rBRIEF phase), 0 for rows
+ * (ORBG_BLUR_TILED=0 at orbg_create, or a blur written by another pass).  Internal; the
+ * accessor orbg_get_blurred_level always returns rows.  ORBG_EINVAL before any extraction. */
+int orbg_get_blur_layout(const orbg_ctx *ctx, int32_t *tiled);
 
 /* per-kernel timing with HIP events on the context stream (for bench roofline) */
 int orbg_profile_enable(orbg_ctx *ctx, int enable);

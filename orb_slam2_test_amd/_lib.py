@@ -239,6 +239,7 @@ def lib():
         "orbg_batch_stats": (i32, [vp, P(C.c_int64), P(C.c_int64)]),
         "orbg_get_quadtree_caps": (i32, [vp, P(i32), P(i32), P(i32)]),
         "orbg_get_blur_plan": (i32, [vp, P(i32), P(C.c_int64), P(C.c_int64)]),
+        "orbg_get_blur_layout": (i32, [vp, P(i32)]),
         "orbg_profile_enable": (i32, [vp, i32]),
         "orbg_profile_read": (i32, [vp, i32, P(C.c_char_p), P(C.c_double), P(C.c_int64)]),
         "orbg_profile_reset": (i32, [vp]),
@@ -457,6 +458,12 @@ class Context:
         check(self._L.orbg_get_blur_plan(self.handle, C.byref(a), C.byref(b), C.byref(c)),
               "orbg_get_blur_plan")
         return bool(a.value), b.value, c.value
+
+    def blur_tiled(self):
+        """True when the blurred levels are stored as 16 x 8-px tiles (orbg_get_blur_layout)."""
+        a = C.c_int32()
+        check(self._L.orbg_get_blur_layout(self.handle, C.byref(a)), "orbg_get_blur_layout")
+        return bool(a.value)
 
     def stereo_summary(self, d_out_ptr):
         check(self._L.orbg_stereo_summary(self.handle, C.c_void_p(d_out_ptr)),

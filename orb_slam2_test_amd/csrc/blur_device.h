@@ -156,11 +156,15 @@ __device__ __forceinline__ void blur2_tile(const Blur2Weights &k, const uint8_t 
         }
     }
     // bounds-checked loads over the level of this frame: offsets past its last byte (the
-    // caller's image may end there) read 0, offsets before its first byte wrap and read 0
+    // caller's image may end there) read 0.  The range starts at the dword holding the
+    // level's first byte (src - sh0: a batch frame of the caller's may start at any byte, and
+    // the dword straddling that start holds pixels 0 .. 3 - sh0 of row 0; a range starting at
+    // src would give it a negative offset and zeros).  Offsets below are src-relative; the
+    // loads add sh0.
     const int nrec = (H - 1) * pitch + W;
-    const __amdgpu_buffer_rsrc_t rsrc = __builtin_amdgcn_make_buffer_rsrc(
-        (void *)src, (short)0, nrec, 0x00020000);
     const int sh0 = (int)((uintptr_t)src & 3);
+    const __amdgpu_buffer_rsrc_t rsrc = __builtin_amdgcn_make_buffer_rsrc(
+        (void *)(src - sh0), (short)0, nrec + sh0, 0x00020000);
     bool strad_wave;
     {
         const int ro = (H - 1) * pitch;
@@ -190,7 +194,7 @@ __device__ __forceinline__ void blur2_tile(const Blur2Weights &k, const uint8_t 
             // only the level's last row can hold that dword (a tile row reads < 256 + 8
             // bytes, less than pitch + W), and only in waves where some lane's last-row dword
             // does (wave-uniform test): every other row is one load with no exec-mask branches
-            v = __builtin_amdgcn_raw_buffer_load_b32(rsrc, o, 0, 0);
+            v = __builtin_amdgcn_raw_buffer_load_b32(rsrc, o + sh0, 0, 0);
             if (!inner && strad_wave && y == H - 1) {  // wave-uniform
                 if (o + 4 > nrec && o < nrec) {
                     // the dword holding the level's last byte: a dword load straddling the
@@ -198,7 +202,7 @@ __device__ __forceinline__ void blur2_tile(const Blur2Weights &k, const uint8_t 
                     // one by one
                     uint32_t vb = 0;
                     for (int b = 0; b < 4 && o + b < nrec; b++)
-                        vb |= (uint32_t)__builtin_amdgcn_raw_buffer_load_b8(rsrc, o + b, 0, 0) << (8 * b);
+                        vb |= (uint32_t)__builtin_amdgcn_raw_buffer_load_b8(rsrc, o + b + sh0, 0, 0) << (8 * b);
                     v = vb;
                 }
             }

@@ -115,8 +115,12 @@ __global__ __launch_bounds__(256) void k_blur_border(
     const uint8_t *src = l == 0 ? img0 + f * img_fs : pyr + f * g->pyr_frame + lv.pyr_off;
     const int pitch = l == 0 ? img_pitch : lv.pitch;
     uint8_t *dst = blur + f * g->blur_frame + lv.blur_off;
+    // the source range starts at the dword holding the level's first byte (blur2_tile: a batch
+    // frame may start at any byte); offsets below are src-relative, the loads add sh0
     const int nrec = (H - 1) * pitch + W;
-    const __amdgpu_buffer_rsrc_t rsrc = __builtin_amdgcn_make_buffer_rsrc((void *)src, (short)0, nrec, 0x00020000);
+    const int sh0 = (int)((uintptr_t)src & 3);
+    const __amdgpu_buffer_rsrc_t rsrc =
+        __builtin_amdgcn_make_buffer_rsrc((void *)(src - sh0), (short)0, nrec + sh0, 0x00020000);
     const __amdgpu_buffer_rsrc_t drsrc = __builtin_amdgcn_make_buffer_rsrc((void *)dst, (short)0, H * lv.pitch, 0x00020000);
     const int gx = 4 * q;
     // window bytes gx - 4 .. gx + 7 inside the level with a dword of slack: aligned loads
@@ -129,7 +133,7 @@ __global__ __launch_bounds__(256) void k_blur_border(
         if (inside) {
             const int a = ro + gx - 4;
             const int sh = (int)(((uintptr_t)src + a) & 3);
-            const int aa = a - sh;
+            const int aa = a - sh + sh0;  // the range's offset of the aligned dword
             const uint32_t d0 = __builtin_amdgcn_raw_buffer_load_b32(rsrc, aa, 0, 0);
             const uint32_t d1 = __builtin_amdgcn_raw_buffer_load_b32(rsrc, aa + 4, 0, 0);
             const uint32_t d2 = __builtin_amdgcn_raw_buffer_load_b32(rsrc, aa + 8, 0, 0);
@@ -142,7 +146,7 @@ __global__ __launch_bounds__(256) void k_blur_border(
 #pragma unroll
             for (int b = 0; b < 12; b++) {
                 const int x = min(max(b2_reflect101(gx - 4 + b, W), 0), W - 1);
-                w[b >> 2] |= (uint32_t)__builtin_amdgcn_raw_buffer_load_b8(rsrc, ro + x, 0, 0) << (8 * (b & 3));
+                w[b >> 2] |= (uint32_t)__builtin_amdgcn_raw_buffer_load_b8(rsrc, ro + x + sh0, 0, 0) << (8 * (b & 3));
             }
             w0 = w[0];
             w1 = w[1];

@@ -2549,6 +2549,14 @@ extern "C" int orbg_get_blur_plan(const orbg_ctx *c, int32_t *fused, int64_t *in
     return ORBG_OK;
 }
 
+extern "C" int orbg_get_blur_layout(const orbg_ctx *c, int32_t *tiled)
+{
+    if (!c) return set_err(ORBG_EINVAL, "ctx is NULL");
+    if (c->gw <= 0) return set_err(ORBG_EINVAL, "no image size planned yet");
+    if (tiled) *tiled = c->geom.blur_tiled;
+    return ORBG_OK;
+}
+
 extern "C" int orbg_batch_stats(orbg_ctx *c, int64_t *ncand, int64_t *nkp)
 {
     if (!c || !c->gw || c->last_n <= 0) return set_err(ORBG_EINVAL, "no batch");

@@ -132,3 +132,65 @@ def test_blur_fused_batch_padded_pitch(oracle):
     for b in range(B):
         for l in range(nl):
             assert np.array_equal(ext.get_blurred_level(b, l), oracle.gauss7(ext.get_level(b, l))), (b, l)
+
+
+@pytest.mark.parametrize("h,w", [(376, 1241), (90, 257), (121, 333), (480, 640), (97, 250)])
+def test_blur_tiled_layout_equals_rows(oracle, h, w):
+    """The default tiled blurred levels (k_blur2 stores 16 x 8-px tiles through its LDS stage,
+    the rBRIEF phase reads tile rows; heights and widths off the tile grid) against
+    ORBG_BLUR_TILED=0 (rows): the same blurred bytes (the oracle's GaussianBlur) and the same
+    keypoints and descriptors as the oracle, in both layouts."""
+    nl = _levels_for(h, w)
+    img = _image(h, w, 1300 + w)
+    p = oracle.params(nfeatures=300, nlevels=nl)
+    r = oracle.extract(p, img)
+    for tiled in (True, False):
+        ext = _with_env({"ORBG_BLUR_TILED": "1" if tiled else "0"},
+                        lambda: ORBextractor(300, 1.2, nl, 20, 7))
+        _check(oracle, ext, img, nl)
+        assert ext.ctx.blur_tiled() == tiled
+        k, d = ext(img)
+        assert np.array_equal(k, r["kps"]) and np.array_equal(d, r["desc"]), tiled
+        ext.close()
+
+
+@pytest.mark.parametrize("tiled", [True, False])
+def test_blur_batch_unaligned_frames(oracle, tiled):
+    """A batch read in place with an odd pitch AND an odd height: the frames start at every
+    byte offset mod 4, so the dword holding a frame's first pixels straddles the frame start
+    (k_blur2's bounds-checked range starts at that dword).  Both blurred layouts."""
+    import torch
+    B, h, w, pitch = 4, 131, 389, 395
+    frames = np.zeros((B, h, pitch), np.uint8)
+    for b in range(B):
+        frames[b, :, :w] = _image(h, w, 80 + b)
+    d = torch.from_numpy(frames).cuda()
+    nl = _levels_for(h, w)
+    ext = _with_env({"ORBG_BLUR_TILED": "1" if tiled else "0"},
+                    lambda: ORBextractor(300, 1.2, nl, 20, 7, max_batch=B))
+    ext.extract_batch_device(d.data_ptr(), B, w, h, step=pitch, frame_stride=h * pitch)
+    ext.ctx.sync()
+    assert ext.ctx.blur_tiled() == tiled
+    for b in range(B):
+        for l in range(nl):
+            assert np.array_equal(ext.get_blurred_level(b, l), oracle.gauss7(ext.get_level(b, l))), (b, l)
+    ext.close()
+
+
+def test_blur_fused_unaligned_frames(oracle):
+    """The fused blur's border pass (k_blur_border) on frames starting at every byte mod 4."""
+    import torch
+    B, h, w, pitch = 4, 163, 301, 307
+    frames = np.zeros((B, h, pitch), np.uint8)
+    for b in range(B):
+        frames[b, :, :w] = _image(h, w, 90 + b)
+    d = torch.from_numpy(frames).cuda()
+    nl = _levels_for(h, w)
+    ext = _with_env({"ORBG_FAST_BLUR": "1"}, lambda: ORBextractor(300, 1.2, nl, 20, 7, max_batch=B))
+    ext.extract_batch_device(d.data_ptr(), B, w, h, step=pitch, frame_stride=h * pitch)
+    ext.ctx.sync()
+    assert ext.ctx.blur_plan()[0]
+    for b in range(B):
+        for l in range(nl):
+            assert np.array_equal(ext.get_blurred_level(b, l), oracle.gauss7(ext.get_level(b, l))), (b, l)
+    ext.close()
