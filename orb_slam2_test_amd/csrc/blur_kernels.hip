@@ -19,7 +19,10 @@
 //              dot2(P[o+2], (k2,k3)) + dot2(P[o+4], (k4,k5)) + k6 * s[o+6], the rounding term
 //              2^15 as the chain's start value;
 //   store      with weights summing to 256 the output is byte 2 of the sum: four pixels packed by
-//              two v_perm, one dword store (legacy 257-sum weights saturate instead).
+//              two v_perm, one dword store (legacy 257-sum weights saturate instead); with
+//              tiled output (G.blur_tiled, the default) the wave is 240 columns (15 tiles of
+//              16 x 8 px) wide and every 8 output rows go through the wave's LDS stage and
+//              leave as two dwordx4 stores of whole tile rows (blur_device.h blur2_tile).
 #include <hip/hip_runtime.h>
 
 #include "orbg_internal.h"
