@@ -388,7 +388,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(ORBG_OD_WPE
                 uint32_t *r1 = (uint32_t *)(bp + pr[1] * ROWB + 16 * pc[1]);
                 r0[0] = n.v0.x, r0[1] = n.v0.y, r0[2] = n.v0.z, r0[3] = n.v0.w;
                 r1[0] = n.v1.x, r1[1] = n.v1.y, r1[2] = n.v1.z, r1[3] = n.v1.w;
-                if (n.sh >= 12 && lane < OD_SPAN) *(uint32_t *)(bp + lane * ROWB + 48) = n.d3;
+                if (n.sh >= 12 && lane < OD_SPAN) {  // a fresh address: no VGPR held (spill)
+                    int la = lane * ROWB + 48;
+                    asm volatile("" : "+v"(la));
+                    *(uint32_t *)(bp + la) = n.d3;
+                }
             } else {
                 *(uint4 *)(bp + pr[0] * ROWB + 16 * pc[0]) = n.v0;
                 *(uint4 *)(bp + pr[1] * ROWB + 16 * pc[1]) = n.v1;  // clamped lanes: same word twice
@@ -458,8 +462,14 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(ORBG_OD_WPE
         }
         const int i = __builtin_amdgcn_readlane(my_i, j);
         if (((okmask >> j) & 1u) && lane < 8) {
-            ((uint32_t *)(desc + (drow0 + i) * 32))[lane] = word;
-            if (HC) ((uint32_t *)(hc.base + hc.ods + (int64_t)i * 32))[lane] = word;
+            // the row address is scalar and the lane's byte offset a fresh 32-bit value
+            // (global_store with saddr): a hoisted 64-bit per-lane pointer would hold two
+            // VGPRs across the slot loop -- spilled at 64, and each reload's vmcnt(0) wait
+            // drained the next slots' prefetched neighbourhoods
+            int lo = lane * 4;
+            asm volatile("" : "+v"(lo));
+            *(uint32_t *)(desc + (drow0 + i) * 32 + lo) = word;
+            if (HC) *(uint32_t *)(hc.base + hc.ods + (int64_t)i * 32 + lo) = word;
         }
     }
 }
