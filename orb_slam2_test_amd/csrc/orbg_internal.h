@@ -68,7 +68,7 @@ struct BaGraphDev {
 #define ORBG_RZ_FILL 5           // k_resize: staged 16-byte chunks per thread
 #endif
 #ifndef ORBG_OD_KPW
-#define ORBG_OD_KPW 8            // k_orient_desc: quadtree output slots per wave
+#define ORBG_OD_KPW 10           // k_orient_desc: quadtree output slots per wave (8: +1.6% orient, 12: a tie, profiles/r06aj_od_kpw_ab.txt)
 #endif
 #define ORBG_OD_TABW 93          // k_orient_desc: IC_Angle lanes (31 rows x 3 chunks)
 #define OCT_KEY_CAP 16384        // k_octree_lds handles levels with <= this many candidates
