@@ -34,7 +34,7 @@ namespace orbg {
 // workgroup per level on an idle chip, the candidate walks are chains of L2 round trips)
 // OCT_PC_SMALL.
 #ifndef OCT_PC_SMALL
-#define OCT_PC_SMALL 16
+#define OCT_PC_SMALL 8  // (16: +5 us per B = 1 extraction, profiles/r06an_single_knobs.txt)
 #endif
 #ifndef OCT_PC_BATCH
 #define OCT_PC_BATCH 4
