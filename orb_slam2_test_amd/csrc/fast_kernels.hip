@@ -53,6 +53,13 @@ namespace orbg {
 #ifndef FC2_CPW
 #define FC2_CPW 2  // consecutive cells per wave (shared halo lines in L1, fewer workgroups)
 #endif
+// small batches (B <= FC2_SMALL_B, the single-frame drop-in: an idle chip, the FAST launches on
+// the critical chain) take one cell per wave: twice the waves, half the chain (1 at B = 1:
+// extraction -6 us, profiles/r06ap_single_knobs.txt; at B = 1024 2 is as fast or faster)
+#ifndef FC2_CPW_SMALL
+#define FC2_CPW_SMALL 1
+#endif
+#define FC2_SMALL_B 8
 
 // one cell, wave-uniform (scalar registers)
 struct Fc2Cell {
@@ -74,7 +81,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(FC2_WPE, 8)
     const uint8_t *__restrict__ img0, int64_t img_fs, int img_pitch,
     const uint8_t *__restrict__ pyr, const uint32_t *__restrict__ ctab,
     int32_t *__restrict__ cell_cnt, uint2 *__restrict__ cell_kp, uint8_t *__restrict__ blur,
-    int nframes, int c_begin, int c_count)
+    int nframes, int c_begin, int c_count, int cpw)
 {
     constexpr int P = 4 * P4;
 #if ORBG_FC2_IL
@@ -95,9 +102,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(FC2_WPE, 8)
     uint32_t *bmap = (uint32_t *)(tA + g->fc2_list_off + 2 * g->fc2_list_cap + 4);
 #endif
     const int total = c_count * nframes;
-    // FC2_CPW consecutive cells per wave (neighbours: shared halo lines in L1 / L2)
+    // cpw consecutive cells per wave (neighbours: shared halo lines in L1 / L2)
     const int cid0 =
-        __builtin_amdgcn_readfirstlane((xcd_remap(blockIdx.x, gridDim.x) * 4 + wv) * FC2_CPW);
+        __builtin_amdgcn_readfirstlane((xcd_remap(blockIdx.x, gridDim.x) * 4 + wv) * cpw);
     if (cid0 >= total) return;  // wave-uniform; no workgroup barrier below
 
     // cell record + level geometry through the scalar cache
@@ -183,7 +190,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(FC2_WPE, 8)
     const int lcap = g->fc2_list_cap;  // pretest list entries (2 per unit of the largest cell)
     const int ncells = g->ncells, cell_cap = g->cell_cap;
 #pragma unroll 1
-    for (int kc = 0; kc < FC2_CPW; kc++) {
+    for (int kc = 0; kc < cpw; kc++) {
     const int cid = cid0 + kc;
     if (cid >= total) break;  // wave-uniform
     const Fc2Cell cur = decode(cid);
@@ -606,7 +613,7 @@ static hipError_t launch_fast2_t(size_t lds, dim3 grid, hipStream_t st, const Or
                                  const OrbgCell *cells, const uint8_t *img0, int64_t img_fs,
                                  int img_pitch, const uint8_t *pyr, const uint32_t *ctab,
                                  int32_t *cell_cnt, uint2 *cell_kp, uint8_t *blur, int nframes,
-                                 int c_begin, int c_count)
+                                 int c_begin, int c_count, int cpw)
 {
     if (lds > 64 * 1024) {
         hipError_t e = hipFuncSetAttribute((const void *)k_fast2<P4, FB>,
@@ -614,7 +621,7 @@ static hipError_t launch_fast2_t(size_t lds, dim3 grid, hipStream_t st, const Or
         if (e != hipSuccess) return e;
     }
     hipLaunchKernelGGL((k_fast2<P4, FB>), grid, dim3(256), lds, st, g, cells, img0, img_fs,
-                       img_pitch, pyr, ctab, cell_cnt, cell_kp, blur, nframes, c_begin, c_count);
+                       img_pitch, pyr, ctab, cell_cnt, cell_kp, blur, nframes, c_begin, c_count, cpw);
     return hipGetLastError();
 }
 
@@ -624,16 +631,17 @@ hipError_t launch_fast2(int p4, size_t lds, hipStream_t st, const OrbgGeom *g,
                         int32_t *cell_cnt, uint2 *cell_kp, uint8_t *blur, int nframes,
                         int c_begin, int c_count)
 {
-    const dim3 grid((c_count * nframes + 4 * FC2_CPW - 1) / (4 * FC2_CPW));
+    const int cpw = nframes <= FC2_SMALL_B ? FC2_CPW_SMALL : FC2_CPW;
+    const dim3 grid((c_count * nframes + 4 * cpw - 1) / (4 * cpw));
     switch (p4) {
 #define X(n)                                                                                  \
     case n:                                                                                   \
         if (blur) return launch_fast2_t<n, true>(lds, grid, st, g, cells, img0, img_fs,       \
                                                  img_pitch, pyr, ctab, cell_cnt, cell_kp,     \
-                                                 blur, nframes, c_begin, c_count);            \
+                                                 blur, nframes, c_begin, c_count, cpw);       \
         return launch_fast2_t<n, false>(lds, grid, st, g, cells, img0, img_fs, img_pitch, pyr, \
                                         ctab, cell_cnt, cell_kp, nullptr, nframes, c_begin,   \
-                                        c_count);
+                                        c_count, cpw);
         ORBG_FAST2_PITCHES(X)
 #undef X
     default:
