@@ -19,6 +19,9 @@ struct OctLdsDims {
     int32_t keep_cnt;   // 1: a level left to k_octree keeps its lvl_cnt entry (k_octree runs
                         // concurrently and owns it: ORBG_BIG_SIDE), 0: zeroed for a consumer
                         // that may run without k_octree
+    int32_t tag;        // != 0: a level left to k_octree stores tag into err_flag[4] instead of
+                        // setting err_flag[2] (the single-frame path's per-call flag: nothing
+                        // to clear ahead of the launch)
 };
 
 // static LDS header of k_octree_lds

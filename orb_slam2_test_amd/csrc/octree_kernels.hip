@@ -299,7 +299,10 @@ __global__ __launch_bounds__(OCT_T) void k_octree_lds(
         if (tid == 0) {
             // the split pair's first launch flags err_flag[3] (its second launch runs only
             // when set), every other launch err_flag[2]
-            atomicOr(err_flag + (D.first ? 3 : 2), 1);
+            if (D.tag)
+                err_flag[4] = D.tag;
+            else
+                atomicOr(err_flag + (D.first ? 3 : 2), 1);
             if (!D.keep_cnt) lvl_cnt[(int64_t)f * g->L + l] = 0;
         }
     };

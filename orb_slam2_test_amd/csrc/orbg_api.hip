@@ -72,7 +72,7 @@ hipError_t launch_orient_desc(bool bfma, bool tiled, dim3 grid, hipStream_t st, 
                               const int32_t *lvl_cnt, OrbgKeypointDev *kps, uint8_t *desc,
                               int32_t *counts, uint8_t *hc_base = nullptr,
                               const int32_t *hc_err = nullptr, size_t hc_okp = 0,
-                              size_t hc_ods = 0);
+                              size_t hc_ods = 0, int32_t hc_tag = 0);
 // match_kernels.hip
 int launch_match_pairs(hipStream_t st, hipStream_t aux, hipEvent_t evf, hipEvent_t evj,
                        const uint8_t *desc, const orbg_keypoint *kps,
@@ -334,6 +334,10 @@ struct orbg_ctx {
     // extra stream's waits, profiles/r05q_single_ab.txt)
     bool big_side = false;
     hipEvent_t ev_big_a = nullptr, ev_big_b = nullptr, ev_big = nullptr;
+    // small batches: the side blur on `fstream` right behind k_pyramid (ORBG_BLUR_Q3), joined
+    // before k_orient_desc
+    bool blur_q3 = false;
+    hipEvent_t ev_sblur = nullptr;
     // ORBG_OCT_GATE (read at orbg_create, default 1): the quadtree fallback launches of a
     // pipelined batch (the split level-0 pair's second launch, k_octree) exit at once unless an
     // earlier launch of the batch flagged a level for them (d_err[3], d_err[2]); 0 = they
@@ -437,6 +441,9 @@ struct orbg_ctx {
     // start latency (6-9 us each) the single-frame path otherwise waits for
     uint8_t *h_zc = nullptr, *h_zc_dev = nullptr;
     size_t zc_bytes = 0;
+    // orbg_extract's image in coherent host memory, pulled by k_copy16 (ORBG_IMG_PULL)
+    uint8_t *h_imz = nullptr, *h_imz_dev = nullptr;
+    size_t imz_bytes = 0;
     int zc_mode = -1;  // -1: read ORBG_ZC on first use
     // orbg_extract's zero-copy outputs written by k_orient_desc itself (the packed block's
     // device pointer while launch_extract runs; null otherwise)
@@ -445,6 +452,9 @@ struct orbg_ctx {
     // with hc_dst: k_octree (the fallback quadtree) not launched; a level it would have taken
     // shows in the packed header's word 3 and the frame is extracted again with it
     bool skip_big = false;
+    // the single-frame skip path's fallback tag (OctLdsDims::tag; 0 = off) and its counter
+    int32_t oct_tag = 0;
+    int32_t sf_seq = 0;
     uint8_t *d_pyr = nullptr, *d_blur = nullptr;  // = pyr_slot[slot], blur_slot[slot]
     int32_t *d_cell_cnt = nullptr;                 // = cnt_slot[slot]
     uint2 *d_cell_kp = nullptr;                    // = ckp_slot[slot]
@@ -704,6 +714,28 @@ static bool skip_big_enabled()
     return on != 0;
 }
 
+// the single-frame skip path's fallback note as a per-call tag in d_err[4] (no clear ahead of
+// the launch); ORBG_SF_TAG=0: d_err[2] cleared by a memset ahead of every frame (A/B)
+static bool sf_tag_enabled()
+{
+    static const int on = [] {
+        const char *e = getenv("ORBG_SF_TAG");
+        return e ? atoi(e) : 1;
+    }();
+    return on != 0;
+}
+
+// small batches: k_pyramid launched ahead of the level-0 FAST cells' cross-stream wait and
+// launch, so the critical chain's first kernel is submitted first (ORBG_PYR_FIRST=0: after, A/B)
+static bool pyr_first_enabled()
+{
+    static const int on = [] {
+        const char *e = getenv("ORBG_PYR_FIRST");
+        return e ? atoi(e) : 1;
+    }();
+    return on != 0;
+}
+
 static bool hc_enabled()
 {
     static const int on = [] {
@@ -743,6 +775,38 @@ static int zc_buf(orbg_ctx *c, size_t bytes, uint8_t **h, uint8_t **d)
     *h = c->h_zc;
     *d = c->h_zc_dev;
     return ORBG_OK;
+}
+
+// the image pull block (as zc_buf; the caller has drained the stream that reads it)
+static int imz_buf(orbg_ctx *c, size_t bytes, uint8_t **h, uint8_t **d)
+{
+    if (c->imz_bytes < bytes) {
+        if (c->h_imz) hipHostFree(c->h_imz);
+        c->h_imz = c->h_imz_dev = nullptr;
+        c->imz_bytes = 0;
+        const size_t nb = std::max(bytes, (size_t)1 << 20);
+        if (hipHostMalloc((void **)&c->h_imz, nb, hipHostMallocCoherent) != hipSuccess)
+            return set_err(ORBG_ENOMEM, "hipHostMalloc(%zu bytes, coherent)", nb);
+        if (hipHostGetDevicePointer((void **)&c->h_imz_dev, c->h_imz, 0) != hipSuccess)
+            return set_err(ORBG_EIO, "hipHostGetDevicePointer");
+        c->imz_bytes = nb;
+    }
+    *h = c->h_imz;
+    *d = c->h_imz_dev;
+    return ORBG_OK;
+}
+
+// orbg_extract's image upload: 1 = pulled from coherent host memory by k_copy16 on the
+// extraction stream (the first kernel of the chain then follows a kernel, not an SDMA
+// completion: ~13 us of queue hand-off on the single frame's critical path, r06as), 0 = the
+// staged DMA
+static bool img_pull_enabled()
+{
+    static const int on = [] {
+        const char *e = getenv("ORBG_IMG_PULL");
+        return e ? atoi(e) : 1;
+    }();
+    return on != 0;
 }
 
 // n16 16-byte words src -> dst (a host-mapped source: one PCIe read per word)
@@ -1499,9 +1563,10 @@ extern "C" int orbg_create(int device, const orbg_params *p, orbg_ctx **out)
     // as long as the context (a new extraction plan keeps pending flags), and every kernel
     // that may raise a flag -- the quadtree's and the device matchers' -- can write it.
     // Word [2] is not an error: k_octree_lds sets it when it leaves a level to k_octree, which
-    // the single-frame path checks when it skipped k_octree (orbg_extract).
+    // the pipelined batch's k_octree gate (and the single-frame path under ORBG_SF_TAG=0) reads.
+    // Word [4]: the same note as a per-call tag (the single-frame path, OctLdsDims::tag).
     {
-        const int32_t e0[4] = {0, INT32_MAX, 0, 0};
+        const int32_t e0[8] = {0, INT32_MAX, 0, 0, 0, 0, 0, 0};
         if (hipMalloc(&c->d_err, sizeof(e0)) != hipSuccess ||
             hipMemcpy(c->d_err, e0, sizeof(e0), hipMemcpyHostToDevice) != hipSuccess) {
             if (c->d_err) hipFree(c->d_err);
@@ -1569,6 +1634,11 @@ extern "C" int orbg_create(int device, const orbg_params *p, orbg_ctx **out)
         c->fast_blur_env = fb && atoi(fb) != 0;
         const char *bt = getenv("ORBG_BLUR_TILED");
         c->blur_tiled_env = !bt || atoi(bt) != 0;
+        const char *bq = getenv("ORBG_BLUR_Q3");
+        // off: 0.240 against 0.229 ms p50 single frame (r06av: a fourth busy stream past the
+        // four hardware queues shares one with another stream)
+        c->blur_q3 = c->fstream && (bq ? atoi(bq) != 0 : false) &&
+                     hipEventCreateWithFlags(&c->ev_sblur, hipEventDisableTiming) == hipSuccess;
         const char *bg = getenv("ORBG_BIG_SIDE");
         c->big_side = c->fstream && (bg ? atoi(bg) != 0 : false);
         if (c->big_side)
@@ -1631,6 +1701,7 @@ extern "C" void orbg_destroy(orbg_ctx *c)
     free_plan(c);
     if (c->d_img) hipFree(c->d_img);
     if (c->d_pack) hipFree(c->d_pack);
+    if (c->h_imz) hipHostFree(c->h_imz);
     if (c->h_zc) hipHostFree(c->h_zc);
     if (c->d_scr) hipFree(c->d_scr);
     if (c->d_trk) hipFree(c->d_trk);
@@ -1656,6 +1727,7 @@ extern "C" void orbg_destroy(orbg_ctx *c)
         for (hipEvent_t e : {c->ev_f0[i], c->ev_b0[i], c->ev_pfork[i], c->ev_pyr[i]})
             if (e) hipEventDestroy(e);
     if (c->fstream) hipStreamDestroy(c->fstream);
+    if (c->ev_sblur) hipEventDestroy(c->ev_sblur);
     for (hipEvent_t e : {c->ev_big_a, c->ev_big_b, c->ev_big})
         if (e) hipEventDestroy(e);
     if (c->ev_fast) hipEventDestroy(c->ev_fast);
@@ -1743,6 +1815,7 @@ static hipError_t launch_octree_l0(orbg_ctx *c, int B, hipStream_t st, bool keep
     const bool small = B <= ORBG_SIDE_BLUR_B;
     OctLdsDims big = c->oct_dims[0];
     big.keep_cnt = keep_cnt;
+    big.tag = c->oct_tag;
     if (!small && c->oct_dims[2].kcap > 0) {
         // d_err[3]: set by the first launch for a level it leaves to the second, which exits
         // at once while it is clear (ORBG_OCT_GATE=0: set, the second always scans)
@@ -1750,6 +1823,7 @@ static hipError_t launch_octree_l0(orbg_ctx *c, int B, hipStream_t st, bool keep
         if (e != hipSuccess) return e;
         OctLdsDims first = c->oct_dims[2];
         first.keep_cnt = keep_cnt;
+        first.tag = 0;
         e = launch_octree_lds(false, dim3(B, 1), oct_lds_bytes(first), st, c->d_geom,
                               c->d_cell_cnt, c->d_cell_kp, c->d_lvl_kp, c->d_lvl_idx,
                               c->d_lvl_cnt, c->d_err, first);
@@ -1765,6 +1839,7 @@ static hipError_t launch_octree_upper(orbg_ctx *c, int B, hipStream_t st, bool k
 {
     OctLdsDims d = c->oct_dims[1];
     d.keep_cnt = keep_cnt;
+    d.tag = c->oct_tag;
     return launch_octree_lds(B <= ORBG_SIDE_BLUR_B, dim3(B, c->geom.L - 1), oct_lds_bytes(d), st,
                              c->d_geom, c->d_cell_cnt, c->d_cell_kp, c->d_lvl_kp, c->d_lvl_idx,
                              c->d_lvl_cnt, c->d_err, d);
@@ -1963,16 +2038,30 @@ static int launch_extract(orbg_ctx *c, const uint8_t *d_imgs, int B, int pitch, 
     };
     // big_side: k_octree beside the quadtree launches (needs fast0's two FAST launches)
     const bool big_side = fast0 && c->big_side;
+    // pyr_first (small batches): the resize chain is the frame's critical path, so k_pyramid is
+    // submitted before the level-0 FAST cells' wait and launch (the wait still refers to the
+    // event recorded ahead of k_pyramid: the images only)
+    const bool pyr_first = fast0 && B <= ORBG_SIDE_BLUR_B && pyr_first_enabled();
+    // early (with pyr_first): each quadtree launch is submitted right behind its FAST launch,
+    // ahead of the side blur's wait and launch -- at B = 1 the host's launch sequence, not the
+    // GPU, paced the quadtrees' starts (r06at: 9-12 us behind their FAST cells)
+    const bool early = pyr_first && oct_mode == 1 && !big_side;
     if (fast0) {
         HIPCHK(hipEventRecord(c->ev_fast, st));
+        if (pyr_first) HIPCHK(launch_pyramid(c, st, d_imgs, B, pitch, fs));
         HIPCHK(hipStreamWaitEvent(c->ostream, c->ev_fast, 0));
         HIPCHK(launch_fast(c->ostream, 0, n0));
         if (big_side) HIPCHK(hipEventRecord(c->ev_big_a, c->ostream));
+        if (early) {
+            hipStream_t st = c->ostream;  // PROF_LAUNCH records on `st`
+            PROF_LAUNCH(c, "octree", launch_octree_l0(c, B, st, false));
+        }
     }
-    HIPCHK(launch_pyramid(c, st, d_imgs, B, pitch, fs));
+    if (!pyr_first) HIPCHK(launch_pyramid(c, st, d_imgs, B, pitch, fs));
     if (blur_side) HIPCHK(hipEventRecord(c->ev_fast, st));  // pyramid written: the side blur
     if (fast0) {
         HIPCHK(launch_fast(st, n0, G.ncells - n0));
+        if (early && G.L > 1) PROF_LAUNCH(c, "octree", launch_octree_upper(c, B, st, false));
         if (big_side) {
             HIPCHK(hipEventRecord(c->ev_big_b, st));
             HIPCHK(hipStreamWaitEvent(c->fstream, c->ev_big_a, 0));
@@ -1995,7 +2084,7 @@ static int launch_extract(orbg_ctx *c, const uint8_t *d_imgs, int B, int pitch, 
     {
         // PROF_LAUNCH records on `st`
         hipStream_t st = oct_mode ? c->ostream : c->stream;
-        PROF_LAUNCH(c, "octree", launch_octree_l0(c, B, st, big_side));
+        if (!early) PROF_LAUNCH(c, "octree", launch_octree_l0(c, B, st, big_side));
         if (oct_mode == 2 && G.L > 1) {
             // levels 1.. need their FAST cells (launched on the extraction stream under fast0)
             if (fast0) {
@@ -2005,7 +2094,13 @@ static int launch_extract(orbg_ctx *c, const uint8_t *d_imgs, int B, int pitch, 
             PROF_LAUNCH(c, "octree", launch_octree_upper(c, B, st, big_side));
         }
         if (blur0) HIPCHK(launch_blur_levels(c, st, d_imgs, B, pitch, fs, 0, 1));
-        if (blur_side) {
+        if (blur_side && c->blur_q3) {
+            // a third queue (A/B, off): the blur needs only the pyramid, so k_orient_desc's
+            // joins would be signalled well before the level-1.. quadtree ends
+            HIPCHK(hipStreamWaitEvent(c->fstream, c->ev_fast, 0));
+            HIPCHK(launch_blur_levels(c, c->fstream, d_imgs, B, pitch, fs, 0, G.L));
+            HIPCHK(hipEventRecord(c->ev_sblur, c->fstream));
+        } else if (blur_side) {
             HIPCHK(hipStreamWaitEvent(st, c->ev_fast, 0));
             HIPCHK(launch_blur_levels(c, st, d_imgs, B, pitch, fs, 0, G.L));
         }
@@ -2014,8 +2109,10 @@ static int launch_extract(orbg_ctx *c, const uint8_t *d_imgs, int B, int pitch, 
     if (!fused && !blur_side)
         HIPCHK(launch_blur_levels(c, st, d_imgs, B, pitch, fs, blur0 ? 1 : 0, G.L));
     else if (fz == 2 && !blur0) HIPCHK(launch_blur_levels(c, st, d_imgs, B, pitch, fs, 0, 1));
-    if (oct_mode != 2 && G.L > 1) PROF_LAUNCH(c, "octree", launch_octree_upper(c, B, st, big_side));
+    if (oct_mode != 2 && G.L > 1 && !early)
+        PROF_LAUNCH(c, "octree", launch_octree_upper(c, B, st, big_side));
     if (oct_mode) HIPCHK(hipStreamWaitEvent(st, c->ev_oct, 0));
+    if (blur_side && c->blur_q3) HIPCHK(hipStreamWaitEvent(st, c->ev_sblur, 0));
     if (big_side)
         HIPCHK(hipStreamWaitEvent(st, c->ev_big, 0));
     else if (!c->skip_big)
@@ -2045,7 +2142,7 @@ static int launch_extract(orbg_ctx *c, const uint8_t *d_imgs, int B, int pitch, 
                                    c->d_blur, c->d_odtab, c->d_lvl_kp, c->d_lvl_idx, c->d_lvl_cnt, (OrbgKeypointDev *)c->d_kps,
                                    c->d_desc, c->d_counts,
                                    c->hc_dst, c->d_err, c->hc_dst ? ORBG_PACK_OKP : 0,
-                                   c->hc_dst ? pack_ods(G.frame_cap) : 0));
+                                   c->hc_dst ? pack_ods(G.frame_cap) : 0, c->oct_tag));
     HIPCHK(hipEventRecord(c->ev_ext[s], st));
     HIPCHK(hipGetLastError());
     c->last_img = d_imgs;
@@ -2220,12 +2317,13 @@ extern "C" int orbg_extract(orbg_ctx *c, const uint8_t *img, int w, int h, size_
     int rc = plan(c, w, h, c->p.max_batch);
     if (rc) return rc;
     const size_t bytes = (size_t)w * h;
-    if (c->img_bytes < bytes) {
+    const size_t bytes16 = (bytes + 15) & ~(size_t)15;  // k_copy16's whole words
+    if (c->img_bytes < bytes16) {
         if (c->d_img) hipFree(c->d_img);
         c->d_img = nullptr;
         c->img_bytes = 0;
-        if ((rc = dalloc(&c->d_img, bytes))) return rc;
-        c->img_bytes = bytes;
+        if ((rc = dalloc(&c->d_img, bytes16))) return rc;
+        c->img_bytes = bytes16;
     }
     if (c->graph_mode && !c->prof.on && c->stream && !(c->pipelined && !c->serial) &&
         !c->mat_pending[c->slot ^ 1] && !c->rel_pending[c->slot ^ 1])
@@ -2234,9 +2332,25 @@ extern "C" int orbg_extract(orbg_ctx *c, const uint8_t *img, int w, int h, size_
     // ~3 ms for 1241 x 376), in ORBG_H2D_CHUNKS bands: the DMA of band k runs while the host
     // copies band k + 1
     uint8_t *hs;
-    if ((rc = stage(c, bytes, &hs))) return rc;
-    HIPCHK(hipStreamSynchronize(c->stream));  // the staging buffer's previous DMA is done
-    const int nch = std::max(1, std::min(ORBG_H2D_CHUNKS, h));
+    const bool pull = img_pull_enabled() && !c->graph_mode;
+    if (pull) {
+        uint8_t *ds;
+        HIPCHK(hipStreamSynchronize(c->stream));  // the previous pull is done
+        if ((rc = imz_buf(c, bytes16, &hs, &ds))) return rc;
+        if (step == (size_t)w) {
+            std::memcpy(hs, img, bytes);
+        } else {
+            for (int y = 0; y < h; y++) std::memcpy(hs + (size_t)y * w, img + (size_t)y * step, w);
+        }
+        const size_t n16 = bytes16 / 16;
+        hipLaunchKernelGGL(k_copy16, dim3((unsigned)std::min<size_t>((n16 + 255) / 256, 1024)),
+                           dim3(256), 0, c->stream, (const uint4 *)ds, (uint4 *)c->d_img, n16);
+        HIPCHK(hipGetLastError());
+    } else {
+        if ((rc = stage(c, bytes, &hs))) return rc;
+        HIPCHK(hipStreamSynchronize(c->stream));  // the staging buffer's previous DMA is done
+    }
+    const int nch = pull ? 0 : std::max(1, std::min(ORBG_H2D_CHUNKS, h));
     for (int k = 0; k < nch; k++) {
         const int y0 = (int)((int64_t)h * k / nch), y1 = (int)((int64_t)h * (k + 1) / nch);
         if (step == (size_t)w) {
@@ -2258,19 +2372,29 @@ extern "C" int orbg_extract(orbg_ctx *c, const uint8_t *img, int w, int h, size_
     // flag d_err[2]; a flagged frame is extracted again with k_octree, ORBG_SKIP_BIG=0: never)
     const bool skip = dz && c->oct_dims[0].kcap > 0 && c->oct_dims[1].kcap > 0 && skip_big_enabled();
     // the flag is this frame's alone: an earlier batch (non-pipelined batches never clear it)
-    // or an earlier rerun frame would otherwise force a needless second extraction
-    if (skip) HIPCHK(hipMemsetAsync(c->d_err + 2, 0, sizeof(int32_t), c->stream));
+    // or an earlier rerun frame would otherwise force a needless second extraction.  Default:
+    // a fresh tag per call, which the quadtree stores into d_err[4] and k_orient_desc compares
+    // (nothing to clear: a memset ahead of the frame cost a blit and two queue gaps on the
+    // critical chain); ORBG_SF_TAG=0: d_err[2] cleared ahead of the frame
+    const bool tag = skip && sf_tag_enabled();
+    if (tag) {
+        c->sf_seq = c->sf_seq == INT32_MAX ? 1 : c->sf_seq + 1;
+        c->oct_tag = c->sf_seq;
+    } else if (skip) {
+        HIPCHK(hipMemsetAsync(c->d_err + 2, 0, sizeof(int32_t), c->stream));
+    }
     c->hc_dst = dz;
     c->skip_big = skip;
     rc = launch_extract(c, c->d_img, 1, w, (int64_t)bytes);
     c->hc_dst = nullptr;
     c->skip_big = false;
+    c->oct_tag = 0;
     if (rc) return rc;
     if (skip) {
         if ((rc = sync_all(c))) return rc;
         if (((const int32_t *)hz)[3]) {  // a level needed the fallback: again, with k_octree
             const int32_t z = 0;
-            HIPCHK(hipMemcpy(c->d_err + 2, &z, sizeof(z), hipMemcpyHostToDevice));
+            if (!tag) HIPCHK(hipMemcpy(c->d_err + 2, &z, sizeof(z), hipMemcpyHostToDevice));
             c->hc_dst = dz;
             rc = launch_extract(c, c->d_img, 1, w, (int64_t)bytes);
             c->hc_dst = nullptr;

@@ -110,6 +110,7 @@ struct OdHostCopy {
     uint8_t *base;
     const int32_t *err;
     int32_t okp, ods;
+    int32_t tag;  // != 0: the quadtree's fallback flag is err[4] == tag (else err[2])
 };
 
 template <bool BFMA, bool HC, bool TB>
@@ -149,7 +150,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(ORBG_OD_WPE
             hdr[0] = hc.err[0];
             hdr[1] = hc.err[1];
             hdr[2] = total;
-            hdr[3] = hc.err[2];  // a level left to k_octree (orbg_extract reruns the frame)
+            // a level left to k_octree (orbg_extract reruns the frame)
+            hdr[3] = hc.tag ? (int32_t)(hc.err[4] == hc.tag) : hc.err[2];
         }
     }
     // lane j < OD_KPW: slot s0 + j -> quadtree key, level, output row (the winner's list
@@ -480,9 +482,9 @@ hipError_t launch_orient_desc(bool bfma, bool tiled, dim3 grid, hipStream_t st, 
                               const uint32_t *lvl_kp, const uint16_t *lvl_idx,
                               const int32_t *lvl_cnt, OrbgKeypointDev *kps, uint8_t *desc,
                               int32_t *counts, uint8_t *hc_base, const int32_t *hc_err,
-                              size_t hc_okp, size_t hc_ods)
+                              size_t hc_okp, size_t hc_ods, int32_t hc_tag)
 {
-    const OdHostCopy hc{hc_base, hc_err, (int32_t)hc_okp, (int32_t)hc_ods};
+    const OdHostCopy hc{hc_base, hc_err, (int32_t)hc_okp, (int32_t)hc_ods, hc_tag};
 #define OD_LAUNCH(BF, H, T)                                                                    \
     hipLaunchKernelGGL((k_orient_desc<BF, H, T>), grid, dim3(256), 0, st, g, img0, img_fs,     \
                        img_pitch, pyr, blur, odtab, lvl_kp, lvl_idx, lvl_cnt, kps, desc, counts, \
