@@ -337,6 +337,7 @@ struct orbg_ctx {
     // small batches: the side blur on `fstream` right behind k_pyramid (ORBG_BLUR_Q3), joined
     // before k_orient_desc
     bool blur_q3 = false;
+    bool sblur = true;  // ORBG_SBLUR=0: small batches blur on the extraction stream (A/B)
     hipEvent_t ev_sblur = nullptr;
     // ORBG_OCT_GATE (read at orbg_create, default 1): the quadtree fallback launches of a
     // pipelined batch (the split level-0 pair's second launch, k_octree) exit at once unless an
@@ -1634,6 +1635,8 @@ extern "C" int orbg_create(int device, const orbg_params *p, orbg_ctx **out)
         c->fast_blur_env = fb && atoi(fb) != 0;
         const char *bt = getenv("ORBG_BLUR_TILED");
         c->blur_tiled_env = !bt || atoi(bt) != 0;
+        const char *sb = getenv("ORBG_SBLUR");
+        c->sblur = !sb || atoi(sb) != 0;
         const char *bq = getenv("ORBG_BLUR_Q3");
         // off: 0.240 against 0.229 ms p50 single frame (r06av: a fourth busy stream past the
         // four hardware queues shares one with another stream)
@@ -2032,7 +2035,7 @@ static int launch_extract(orbg_ctx *c, const uint8_t *d_imgs, int B, int pitch, 
     // blur_side: small batches (the single-frame drop-in) blur every level on the quadtree
     // stream after the level-0 quadtree, so levels 1.. go FAST -> quadtree without waiting for
     // the blur on the extraction stream (at B = 1 the blur is ~9 us of a ~150 us chain)
-    const bool blur_side = fast0 && oct_mode == 1 && !fused && !blur0 && B <= ORBG_SIDE_BLUR_B;
+    const bool blur_side = fast0 && oct_mode == 1 && !fused && !blur0 && B <= ORBG_SIDE_BLUR_B && c->sblur;
     auto launch_fast = [&](hipStream_t q, int cb, int cn) {
         return launch_fast_cells(c, q, d_imgs, B, pitch, fs, cb, cn);
     };
