@@ -20,23 +20,38 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 EXE = os.path.join(ROOT, "orb_slam2_test_amd", "lib", "compat_selftest")
 
 
-@pytest.mark.parametrize("zc", ["1", "0", "1-nohc"])
+# the single-frame launch-sequence switches: each must give the same bytes
+LAUNCH_ENV = {
+    "dma": {"ORBG_IMG_PULL": "0"},    # the image by SDMA instead of k_copy16 from host memory
+    "notag": {"ORBG_SF_TAG": "0"},    # the fallback note cleared by a memset, not tagged
+    "nopf": {"ORBG_PYR_FIRST": "0"},  # the batch launch order
+}
+
+
+@pytest.mark.parametrize("zc", ["1", "0", "1-nohc", "1-dma", "1-notag", "1-nopf", "1-noise",
+                                "1-noise-notag"])
 def test_cpp_compat_layer_matches_oracle(oracle, tmp_path, zc):
     """zc: ORBG_ZC, the zero-copy output block / SearchForInitialization staging (default 1)
     or the DMA path it replaced; "1-nohc": zero-copy with the block filled by k_pack_frame
-    (ORBG_HC=0) instead of by k_orient_desc itself"""
+    (ORBG_HC=0) instead of by k_orient_desc itself; "1-dma" / "1-notag" / "1-nopf": the
+    default with one launch-sequence switch off (LAUNCH_ENV); "-noise": the second frame is
+    pure noise, whose level 0 overflows k_octree_lds, so the single-frame path extracts it
+    again with k_octree (the fallback note: per-call tag, or the memset under notag)"""
     import torch
     if torch.cuda.device_count() == 0:
         pytest.skip("no GPU")
     assert os.path.exists(EXE), "build() must produce the compat selftest"
     w, h, nfeat = 1241, 376, 2000
     seq = S.sequence(2, h, w, seed=S.DEFAULT_SEED + 77)
+    if "noise" in zc:
+        seq[1] = S.pure_noise(h, w)
     for t in range(2):
         seq[t].tofile(tmp_path / f"f{t}.raw")
     r = subprocess.run([EXE, "run", str(w), str(h), str(tmp_path / "f0.raw"),
                         str(tmp_path / "f1.raw"), str(tmp_path), str(nfeat)],
                        capture_output=True, text=True, timeout=300,
-                       env=dict(os.environ, ORBG_ZC=zc[0], ORBG_HC="0" if "nohc" in zc else "1"))
+                       env=dict(os.environ, ORBG_ZC=zc[0], ORBG_HC="0" if "nohc" in zc else "1",
+                                **LAUNCH_ENV.get(zc.split("-")[-1], {})))
     assert r.returncode == 0, r.stdout + r.stderr
     p = oracle.params(nfeatures=nfeat)
     ref = [oracle.extract(p, seq[t]) for t in range(2)]
