@@ -2265,8 +2265,19 @@ __global__ void k_pack_frame(const int32_t *__restrict__ err, const int32_t *__r
     if (i < nd) pack[ods / 4 + i] = desc[(size_t)frame * fc * 8 + i];
 }
 
+// drained: the caller (orbg_extract's optimistic path) drained every stream after the frame's
+// last launch, and k_orient_desc filled the block: no second round of synchronisations
+static int download_frame(orbg_ctx *c, int frame, orbg_keypoint *kps, uint8_t *desc, int cap,
+                          int *n_out, bool drained);
+
 extern "C" int orbg_download_frame(orbg_ctx *c, int frame, orbg_keypoint *kps, uint8_t *desc,
                                    int cap, int *n_out)
+{
+    return download_frame(c, frame, kps, desc, cap, n_out, false);
+}
+
+static int download_frame(orbg_ctx *c, int frame, orbg_keypoint *kps, uint8_t *desc, int cap,
+                          int *n_out, bool drained)
 {
     if (!c || !c->gw || frame < 0 || frame >= c->last_n)
         return set_err(ORBG_EINVAL, "bad frame index");
@@ -2305,7 +2316,7 @@ extern "C" int orbg_download_frame(orbg_ctx *c, int frame, orbg_keypoint *kps, u
         HIPCHK(hipGetLastError());
     }
     if (!use_zc(c)) HIPCHK(hipMemcpyAsync(hs, c->d_pack, bytes, hipMemcpyDeviceToHost, st));
-    if ((rc = sync_all(c))) return rc;
+    if (!(drained && packed && use_zc(c)) && (rc = sync_all(c))) return rc;
     c->prof.collect();
     int32_t hdr[3];
     std::memcpy(hdr, hs, sizeof(hdr));
@@ -2414,9 +2425,12 @@ extern "C" int orbg_extract(orbg_ctx *c, const uint8_t *img, int w, int h, size_
     c->skip_big = false;
     c->oct_tag = 0;
     if (rc) return rc;
+    bool drained = false;
     if (skip) {
         if ((rc = spin_sync(c->stream)) || (rc = sync_all(c))) return rc;
+        drained = true;
         if (((const int32_t *)hz)[3]) {  // a level needed the fallback: again, with k_octree
+            drained = false;
             const int32_t z = 0;
             if (!tag) HIPCHK(hipMemcpy(c->d_err + 2, &z, sizeof(z), hipMemcpyHostToDevice));
             c->hc_dst = dz;
@@ -2426,7 +2440,7 @@ extern "C" int orbg_extract(orbg_ctx *c, const uint8_t *img, int w, int h, size_
         }
     }
     c->hc_done = dz != nullptr;
-    return orbg_download_frame(c, 0, kps, desc, cap, n_out);
+    return download_frame(c, 0, kps, desc, cap, n_out, drained);
 }
 
 // the context state launch_extract leaves for a non-pipelined batch into slot s (a graph
