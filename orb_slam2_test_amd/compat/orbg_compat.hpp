@@ -108,6 +108,12 @@ public:
             check(rc, "orbg_extract");
             break;
         }
+        // the context's per-frame output capacity (known after the first extraction): every
+        // later frame fits it, and the resize above then value-initialises only the few
+        // entries between the last frame's count and that capacity, not up to 4096
+        int32_t fc = 0;
+        if (orbg_batch_outputs(ctx_, nullptr, nullptr, nullptr, &fc) == ORBG_OK && fc > 0)
+            cap_ = fc;
         keypoints.resize(n);
         descriptors.resize((size_t)n * 32);
         levels_valid_ = true;
@@ -308,8 +314,9 @@ public:
         if (image.empty()) return;
         cv::Mat im = image.getMat();
         CV_Assert(im.type() == CV_8UC1);
-        std::vector<orbg_keypoint> kps;
-        std::vector<uint8_t> desc;
+        // the staging vectors persist across frames (no allocation per frame)
+        std::vector<orbg_keypoint> &kps = kps_;
+        std::vector<uint8_t> &desc = desc_;
         const int n = ext_(im.data, im.cols, im.rows, im.step[0], kps, desc);
         keypoints.clear();
         keypoints.reserve(n);
@@ -336,6 +343,8 @@ public:
     }
 
 private:
+    std::vector<orbg_keypoint> kps_;
+    std::vector<uint8_t> desc_;
     // mvImagePyramid[l]: level l of the last operator() call, downloaded from HBM on its first
     // access after that call (std::vector<cv::Mat>'s indexing and size in the reference)
     class LazyPyramid {
