@@ -185,14 +185,14 @@ public:
         if (!ctx_) throw Error(ORBG_EINVAL, "Matcher needs an orbg context");
         if ((int)vbPrevMatched.size() < 2 * F1.n)
             throw Error(ORBG_EINVAL, "vbPrevMatched smaller than 2 * F1.n");
-        std::vector<int32_t> m12(F1.n);
+        static_assert(sizeof(int) == sizeof(int32_t), "vnMatches12 is written in place");
+        vnMatches12.resize(F1.n);  // every entry is written by the call
         int nm = 0;
         check(orbg_search_for_initialization(ctx_, F1.keys, F1.desc, F1.n, F2.keys, F2.desc,
                                              F2.n, &F2.bounds, vbPrevMatched.data(),
-                                             m12.data(), windowSize, nnratio_,
+                                             (int32_t *)vnMatches12.data(), windowSize, nnratio_,
                                              check_ori_ ? 1 : 0, &nm),
               "orbg_search_for_initialization");
-        vnMatches12.assign(m12.begin(), m12.end());
         return nm;
     }
 
