@@ -72,8 +72,7 @@ hipError_t launch_orient_desc(bool bfma, bool tiled, dim3 grid, hipStream_t st, 
                               const int32_t *lvl_cnt, OrbgKeypointDev *kps, uint8_t *desc,
                               int32_t *counts, uint8_t *hc_base = nullptr,
                               const int32_t *hc_err = nullptr, size_t hc_okp = 0,
-                              size_t hc_ods = 0, int32_t hc_tag = 0, int32_t hc_done_tag = 0,
-                              uint32_t *hc_cnt = nullptr);
+                              size_t hc_ods = 0, int32_t hc_tag = 0);
 // match_kernels.hip
 int launch_match_pairs(hipStream_t st, hipStream_t aux, hipEvent_t evf, hipEvent_t evj,
                        const uint8_t *desc, const orbg_keypoint *kps,
@@ -457,9 +456,6 @@ struct orbg_ctx {
     // the single-frame skip path's fallback tag (OctLdsDims::tag; 0 = off) and its counter
     int32_t oct_tag = 0;
     int32_t sf_seq = 0;
-    // the single-frame path's completion word (OdHostCopy::done_tag; 0 = off) and its counter
-    int32_t hc_done_tag = 0;
-    int32_t hc_seq = 0;
     uint8_t *d_pyr = nullptr, *d_blur = nullptr;  // = pyr_slot[slot], blur_slot[slot]
     int32_t *d_cell_cnt = nullptr;                 // = cnt_slot[slot]
     uint2 *d_cell_kp = nullptr;                    // = ckp_slot[slot]
@@ -736,18 +732,6 @@ static bool pyr_first_enabled()
 {
     static const int on = [] {
         const char *e = getenv("ORBG_PYR_FIRST");
-        return e ? atoi(e) : 1;
-    }();
-    return on != 0;
-}
-
-// the single-frame path waits for k_orient_desc's completion word in the host block (a poll of
-// host memory) instead of a blocking stream synchronisation, whose wake-up came 6-8 us after
-// the kernel (ORBG_HC_DONE=0: the synchronisation)
-static bool hc_done_enabled()
-{
-    static const int on = [] {
-        const char *e = getenv("ORBG_HC_DONE");
         return e ? atoi(e) : 1;
     }();
     return on != 0;
@@ -1582,8 +1566,6 @@ extern "C" int orbg_create(int device, const orbg_params *p, orbg_ctx **out)
     // Word [2] is not an error: k_octree_lds sets it when it leaves a level to k_octree, which
     // the pipelined batch's k_octree gate (and the single-frame path under ORBG_SF_TAG=0) reads.
     // Word [4]: the same note as a per-call tag (the single-frame path, OctLdsDims::tag).
-    // Word [5]: k_orient_desc's wave count of the single-frame completion word (zero between
-    // launches: the last wave resets it).
     {
         const int32_t e0[8] = {0, INT32_MAX, 0, 0, 0, 0, 0, 0};
         if (hipMalloc(&c->d_err, sizeof(e0)) != hipSuccess ||
@@ -2163,8 +2145,7 @@ static int launch_extract(orbg_ctx *c, const uint8_t *d_imgs, int B, int pitch, 
                                    c->d_blur, c->d_odtab, c->d_lvl_kp, c->d_lvl_idx, c->d_lvl_cnt, (OrbgKeypointDev *)c->d_kps,
                                    c->d_desc, c->d_counts,
                                    c->hc_dst, c->d_err, c->hc_dst ? ORBG_PACK_OKP : 0,
-                                   c->hc_dst ? pack_ods(G.frame_cap) : 0, c->oct_tag,
-                                   c->hc_dst ? c->hc_done_tag : 0, (uint32_t *)(c->d_err + 5)));
+                                   c->hc_dst ? pack_ods(G.frame_cap) : 0, c->oct_tag));
     HIPCHK(hipEventRecord(c->ev_ext[s], st));
     HIPCHK(hipGetLastError());
     c->last_img = d_imgs;
@@ -2439,31 +2420,14 @@ extern "C" int orbg_extract(orbg_ctx *c, const uint8_t *img, int w, int h, size_
     }
     c->hc_dst = dz;
     c->skip_big = skip;
-    const bool done_word = skip && hc_done_enabled();
-    if (done_word) {
-        c->hc_seq = c->hc_seq == INT32_MAX ? 1 : c->hc_seq + 1;
-        c->hc_done_tag = c->hc_seq;
-    }
     rc = launch_extract(c, c->d_img, 1, w, (int64_t)bytes);
     c->hc_dst = nullptr;
     c->skip_big = false;
     c->oct_tag = 0;
-    c->hc_done_tag = 0;
     if (rc) return rc;
     bool drained = false;
     if (skip) {
-        if (done_word) {
-            // the outputs are in the block once the word holds this call's tag: poll it (the
-            // kernel's own completion follows within microseconds; the next stream user waits
-            // for it); a word that never comes (a fault) ends in the synchronisation's error
-            volatile const int32_t *dw = (volatile const int32_t *)hz + 8;
-            bool seen = false;
-            for (long it = 0; it < (1L << 26) && !seen; it++) seen = *dw == c->hc_seq;
-            if (!seen && (rc = sync_all(c))) return rc;
-            std::atomic_thread_fence(std::memory_order_acquire);
-        } else if ((rc = spin_sync(c->stream)) || (rc = sync_all(c))) {
-            return rc;
-        }
+        if ((rc = spin_sync(c->stream)) || (rc = sync_all(c))) return rc;
         drained = true;
         if (((const int32_t *)hz)[3]) {  // a level needed the fallback: again, with k_octree
             drained = false;

@@ -111,36 +111,7 @@ struct OdHostCopy {
     const int32_t *err;
     int32_t okp, ods;
     int32_t tag;  // != 0: the quadtree's fallback flag is err[4] == tag (else err[2])
-    // != 0: every wave counts itself out in cnt (device memory, zero between launches) once
-    // its block stores are complete, and the grid's last wave stores done_tag into the
-    // block's word 8 -- the host polls that word instead of a stream synchronisation
-    int32_t done_tag;
-    uint32_t *cnt;
 };
-
-// a wave of the HC instantiation leaves: count it out (OdHostCopy::done_tag); every exit path
-// of the kernel calls this, so the last count always comes
-__device__ __forceinline__ void od_hc_done(const OdHostCopy &hc)
-{
-    if (!hc.done_tag) return;
-    // this wave's stores are complete before its count: the block is fine-grained host memory,
-    // which no GPU cache holds, so the stores' own completion (vmcnt 0) is all the ordering the
-    // host needs -- no cache writeback or invalidate (an agent-scope release / acquire here is
-    // an L2 writeback + invalidate per wave)
-    __atomic_signal_fence(__ATOMIC_SEQ_CST);
-    __builtin_amdgcn_s_waitcnt(0);
-    __atomic_signal_fence(__ATOMIC_SEQ_CST);
-    if ((threadIdx.x & 63) == 0) {
-        const uint32_t total = gridDim.x * (blockDim.x / 64);
-        const uint32_t prev = __hip_atomic_fetch_add(hc.cnt, 1u, __ATOMIC_RELAXED,
-                                                     __HIP_MEMORY_SCOPE_AGENT);
-        if (prev == total - 1) {
-            __hip_atomic_store(hc.cnt, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            __hip_atomic_store((int32_t *)hc.base + 8, hc.done_tag, __ATOMIC_RELAXED,
-                               __HIP_MEMORY_SCOPE_SYSTEM);
-        }
-    }
-}
 
 template <bool BFMA, bool HC, bool TB>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(ORBG_OD_WPE, 8))) void k_orient_desc(
@@ -168,10 +139,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(ORBG_OD_WPE
     const int f = id / nb, bx = id - f * nb;
     const int s0 = __builtin_amdgcn_readfirstlane((bx * 4 + wv) * OD_KPW);  // wave-uniform
     const int L = g->L, OF = g->out_frame;
-    if (s0 >= OF) {
-        if (HC) od_hc_done(hc);
-        return;
-    }
+    if (s0 >= OF) return;
     const int32_t *lc = lvl_cnt + (int64_t)f * L;
     if (s0 == 0 && lane == 0) {
         int total = 0;
@@ -222,10 +190,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(ORBG_OD_WPE
         pac[k] = wa - par[k] * 3;
     }
 
-    if (!okmask) {  // wave-uniform: no keypoint in this wave's slots
-        if (HC) od_hc_done(hc);
-        return;
-    }
+    if (!okmask) return;  // wave-uniform: no keypoint in this wave's slots
     // Empty slots borrow the first filled slot's key (their results are dropped), so every
     // slot's loads below are unconditional and the unrolled slot loops have no branches
     // around them: each vmcnt wait then covers exactly the current slot's loads.
@@ -369,7 +334,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(ORBG_OD_WPE
         // keep the sums live without a store per wave to one address (that alone would
         // serialise): lane j's sums into its own slot's descriptor row
         if (my_ok) ((int *)(desc + (drow0 + my_i) * 32))[0] = M01 + M10;
-        if (HC) od_hc_done(hc);
         return;
     }
     // ---- B: angle = fastAtan2(m_01, m_10) (:110), cos / sin of it (:121-122), and the
@@ -404,10 +368,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(ORBG_OD_WPE
         if (HC) ((OrbgKeypointDev *)(hc.base + hc.okp))[my_i] = kp;
     }
 
-    if (g->dbg == 22) {  // developer phase timing: stop after B
-        if (HC) od_hc_done(hc);
-        return;
-    }
+    if (g->dbg == 22) return;  // developer phase timing: stop after B
     // ---- C: rBRIEF (ORBextractor.cc:117-157) on the blurred level ----
     // lane L owns tests L + 64t (t = 0..3), one pattern word (x0, y0, x1, y1) each
     int pat[4];
@@ -513,7 +474,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(ORBG_OD_WPE
             if (HC) *(uint32_t *)(hc.base + hc.ods + (int64_t)i * 32 + lo) = word;
         }
     }
-    if (HC) od_hc_done(hc);
 }
 
 hipError_t launch_orient_desc(bool bfma, bool tiled, dim3 grid, hipStream_t st, const OrbgGeom *g,
@@ -522,11 +482,9 @@ hipError_t launch_orient_desc(bool bfma, bool tiled, dim3 grid, hipStream_t st, 
                               const uint32_t *lvl_kp, const uint16_t *lvl_idx,
                               const int32_t *lvl_cnt, OrbgKeypointDev *kps, uint8_t *desc,
                               int32_t *counts, uint8_t *hc_base, const int32_t *hc_err,
-                              size_t hc_okp, size_t hc_ods, int32_t hc_tag,
-                              int32_t hc_done_tag, uint32_t *hc_cnt)
+                              size_t hc_okp, size_t hc_ods, int32_t hc_tag)
 {
-    const OdHostCopy hc{hc_base, hc_err, (int32_t)hc_okp, (int32_t)hc_ods, hc_tag, hc_done_tag,
-                        hc_cnt};
+    const OdHostCopy hc{hc_base, hc_err, (int32_t)hc_okp, (int32_t)hc_ods, hc_tag};
 #define OD_LAUNCH(BF, H, T)                                                                    \
     hipLaunchKernelGGL((k_orient_desc<BF, H, T>), grid, dim3(256), 0, st, g, img0, img_fs,     \
                        img_pitch, pyr, blur, odtab, lvl_kp, lvl_idx, lvl_cnt, kps, desc, counts, \
