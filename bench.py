@@ -380,17 +380,19 @@ def main():
                 ev_copy[j % 3].record(cstream)
 
         # the H2D rate alone (the bound of a host-fed pipeline): the step's own copies (the
-        # copy stream, the 3 staging slots), after an untimed round (round 5 timed 4 cold
-        # copies and the host-fed line came out 1% above that bound)
+        # copy stream, the 3 staging slots), after an untimed round, the best of 5 rounds of 12
+        # (round 5 timed 4 cold copies, and one round of 12 in round 6 came out 2% under the
+        # host-fed line itself: the link's rate drifts from round to round)
         for j in range(3):
             issue_copy(j)
         torch.cuda.synchronize()
-        nprobe = 12
-        t0 = time.perf_counter()
-        for j in range(nprobe):
-            issue_copy(j)
-        torch.cuda.synchronize()
-        h2d = nprobe * h_blocks[0].numel() / (time.perf_counter() - t0) / 1e9
+        nprobe, h2d = 12, 0.0
+        for _ in range(5):
+            t0 = time.perf_counter()
+            for j in range(nprobe):
+                issue_copy(j)
+            torch.cuda.synchronize()
+            h2d = max(h2d, nprobe * h_blocks[0].numel() / (time.perf_counter() - t0) / 1e9)
         for j in range(3):
             issue_copy(j)
 
