@@ -26,7 +26,14 @@
 
 namespace orbg {
 
-#define OCT_T 512
+// threads per quadtree workgroup: a template parameter (NT) of the kernel and its block-wide
+// helpers; OCT_T names it inside them.  The single-frame launches take 512 (one workgroup per
+// level on an idle chip: more lanes per phase), batches OCT_T_BATCH
+#define OCT_T NT
+#ifndef OCT_T_BATCH
+#define OCT_T_BATCH 256  // batches: 0.612 -> 0.787 ms serial, but the pipelined step 5.42 -> 5.37 ms (r06bk)
+#endif
+#define OCT_T_SMALL 512
 #define OCT_CODE_DEPTH 14
 
 // OCT_PC: cells per wave with their candidate loads in flight (per_cell).  Batches take 4
@@ -81,6 +88,7 @@ __device__ __forceinline__ int rec_depth(unsigned long long r) { return (int)((r
 #ifndef ORBG_OCT_SCAN_2BAR
 #define ORBG_OCT_SCAN_2BAR 0
 #endif
+template <int NT>
 __device__ int oct_scan(int v, int *total, int *sh, int &par)
 {
     const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
@@ -103,6 +111,7 @@ __device__ int oct_scan(int v, int *total, int *sh, int &par)
 
 // In-place ascending sort of u64 v[0..n) without padding (flip bitonic; virtual +inf
 // entries at [n, pw) never move, so comparators touching them are skipped).
+template <int NT>
 __device__ void flip_bitonic_u64(unsigned long long *v, int n)
 {
     int pw = 1;
@@ -145,6 +154,7 @@ __device__ void flip_bitonic_u64(unsigned long long *v, int n)
 // flip_bitonic_u64's log2(n) (log2(n) + 1) / 2 -- the phase-2 sort is a chain of barriers of a
 // single workgroup, the B = 1 critical path.  n <= OCT_RANK_R * OCT_T.
 #define OCT_RANK_R 4
+template <int NT>
 __device__ void rank_sort_u64(unsigned long long *v, int n)
 {
     const int tid = threadIdx.x;
@@ -249,8 +259,8 @@ __device__ __forceinline__ unsigned long long oct_split_points(const OctLdsView 
 // frame's largest level starts first and the small levels fill the tail); handles a level iff
 // its candidate count
 // n <= D.kcap (k_octree takes the rest, same threshold)
-template <int OCT_PC>
-__global__ __launch_bounds__(OCT_T) void k_octree_lds(
+template <int OCT_PC, int NT>
+__global__ __launch_bounds__(NT) void k_octree_lds(
     const OrbgGeom *__restrict__ g, const int32_t *__restrict__ cell_cnt,
     const uint2 *__restrict__ cell_kp, uint32_t *__restrict__ lvl_kp,
     uint16_t *__restrict__ lvl_idx, int32_t *__restrict__ lvl_cnt, int32_t *__restrict__ err_flag,
@@ -314,7 +324,7 @@ __global__ __launch_bounds__(OCT_T) void k_octree_lds(
     for (int c0 = 0; c0 < ncells; c0 += OCT_T) {
         const int c = c0 + tid;
         int tot;
-        const int off = oct_scan(c < ncells ? ccount[c] : 0, &tot, S.red, spar) + n;
+        const int off = oct_scan<NT>(c < ncells ? ccount[c] : 0, &tot, S.red, spar) + n;
         if (c < ncells) V.aux[c] = V.coff[c] = (uint16_t)min(off, 65535);
         n += tot;
     }
@@ -380,7 +390,7 @@ __global__ __launch_bounds__(OCT_T) void k_octree_lds(
         int sum = 0;
         for (int i = 0; i < PER; i++) sum += (int)(wb[i] & 0xFFFF) + (int)(wb[i] >> 16);
         int tot;
-        int run = oct_scan(sum, &tot, S.red, spar);
+        int run = oct_scan<NT>(sum, &tot, S.red, spar);
         for (int i = 0; i < PER; i++) {
             const uint32_t w = wb[i];
             const int a = (int)(w & 0xFFFF), b = (int)(w >> 16);
@@ -463,7 +473,7 @@ __global__ __launch_bounds__(OCT_T) void k_octree_lds(
                     }
                 }
                 int t;  // both totals from one scan (each < 2^16: e, m <= 4 per node)
-                oct_scan(e | (m << 16), &t, S.red, spar);
+                oct_scan<NT>(e | (m << 16), &t, S.red, spar);
                 tot_e += t & 0xFFFF;
                 nexp += t >> 16;
             }
@@ -480,7 +490,7 @@ __global__ __launch_bounds__(OCT_T) void k_octree_lds(
                 const int i = ch * OCT_T + tid;
                 const int e = ee[ch], sp = spp[ch];
                 int tot;
-                const int pre = oct_scan(e | (sp << 16), &tot, S.red, spar) + run;
+                const int pre = oct_scan<NT>(e | (sp << 16), &tot, S.red, spar) + run;
                 const int E = pre & 0xFFFF, splits_before = pre >> 16;
                 if (i < alive) {
                     const unsigned long long r = V.list(cur)[i];
@@ -538,7 +548,7 @@ __global__ __launch_bounds__(OCT_T) void k_octree_lds(
                     fl = rec_cnt(r) > 1 && sq >= vbase && sq < vend;
                 }
                 int tot;
-                const int o = oct_scan(fl, &tot, S.red, spar) + np;
+                const int o = oct_scan<NT>(fl, &tot, S.red, spar) + np;
                 if (fl)
                     V.sortv[o] = ((unsigned long long)rec_cnt(r) << 32) |
                                  ((unsigned long long)rec_seq(r) << 16) | (unsigned)i;
@@ -547,9 +557,9 @@ __global__ __launch_bounds__(OCT_T) void k_octree_lds(
             for (int i = tid; i < alive; i += OCT_T) V.aux[i] = 0;
             __syncthreads();
             if (ORBG_OCT_RANK && np <= OCT_RANK_R * OCT_T)
-                rank_sort_u64(V.sortv, np);
+                rank_sort_u64<NT>(V.sortv, np);
             else
-                flip_bitonic_u64(V.sortv, np);
+                flip_bitonic_u64<NT>(V.sortv, np);
             // processing order p = largest (cnt, seq) first (:872); cut at the first p with
             // alive + sum_{p' <= p} (children - 1) >= N (:917-918)
             if (tid == 0) S.s_nproc = np;
@@ -576,7 +586,7 @@ __global__ __launch_bounds__(OCT_T) void k_octree_lds(
                                               (unsigned long long)b[2] << 16 | (unsigned)b[1];
                     }
                     int tot;
-                    const int incl = oct_scan(dl, &tot, S.red, spar) + run + dl;
+                    const int incl = oct_scan<NT>(dl, &tot, S.red, spar) + run + dl;
                     if (p < np && alive + incl >= N) atomicMin(&S.s_nproc, p + 1);
                     run += tot;
                 }
@@ -596,7 +606,7 @@ __global__ __launch_bounds__(OCT_T) void k_octree_lds(
                     V.aux[pos] = 1;  // processed parent
                 }
                 int t;
-                oct_scan(e, &t, S.red, spar);
+                oct_scan<NT>(e, &t, S.red, spar);
                 tot_e += t;
             }
             {
@@ -612,7 +622,7 @@ __global__ __launch_bounds__(OCT_T) void k_octree_lds(
                         for (int q = 0; q < 4; q++) e += b[q + 1] > b[q];
                     }
                     int tot;
-                    const int E = oct_scan(e, &tot, S.red, spar) + run;
+                    const int E = oct_scan<NT>(e, &tot, S.red, spar) + run;
                     if (p < nproc) {
                         const int blk = tot_e - E - e;
                         int k = 0;
@@ -632,7 +642,7 @@ __global__ __launch_bounds__(OCT_T) void k_octree_lds(
                     const int i = i0 + tid;
                     const int fl = (i < alive) ? (int)V.aux[i] : 0;
                     int tot;
-                    const int before = oct_scan(fl, &tot, S.red, spar) + runp;
+                    const int before = oct_scan<NT>(fl, &tot, S.red, spar) + runp;
                     if (i < alive && !fl) V.list(nxt)[tot_e + i - before] = V.list(cur)[i];
                     runp += tot;
                 }
@@ -723,7 +733,7 @@ __global__ __launch_bounds__(OCT_T) void k_octree_lds(
         int sum = 0;
         for (int t = t0; t < t1; t++) sum += (int)tcnt[t];
         int tot;
-        int run = oct_scan(sum, &tot, S.red, spar);
+        int run = oct_scan<NT>(sum, &tot, S.red, spar);
         for (int t = t0; t < t1; t++) {
             const int c = (int)tcnt[t];
             tcnt[t] = (uint32_t)run;
@@ -753,17 +763,18 @@ hipError_t launch_octree_lds(bool small, dim3 grid, size_t lds, hipStream_t st, 
                              uint16_t *lvl_idx, int32_t *lvl_cnt, int32_t *err_flag, OctLdsDims D)
 {
     if (small)
-        hipLaunchKernelGGL(k_octree_lds<OCT_PC_SMALL>, grid, dim3(OCT_T), lds, st, g, cell_cnt,
-                           cell_kp, lvl_kp, lvl_idx, lvl_cnt, err_flag, D);
+        hipLaunchKernelGGL((k_octree_lds<OCT_PC_SMALL, OCT_T_SMALL>), grid, dim3(OCT_T_SMALL), lds, st,
+                           g, cell_cnt, cell_kp, lvl_kp, lvl_idx, lvl_cnt, err_flag, D);
     else
-        hipLaunchKernelGGL(k_octree_lds<OCT_PC_BATCH>, grid, dim3(OCT_T), lds, st, g, cell_cnt, cell_kp,
-                           lvl_kp, lvl_idx, lvl_cnt, err_flag, D);
+        hipLaunchKernelGGL((k_octree_lds<OCT_PC_BATCH, OCT_T_BATCH>), grid, dim3(OCT_T_BATCH), lds, st,
+                           g, cell_cnt, cell_kp, lvl_kp, lvl_idx, lvl_cnt, err_flag, D);
     return hipGetLastError();
 }
 
 hipError_t octree_lds_attr(int bytes)
 {
-    for (const void *k : {(const void *)k_octree_lds<OCT_PC_BATCH>, (const void *)k_octree_lds<OCT_PC_SMALL>}) {
+    for (const void *k : {(const void *)k_octree_lds<OCT_PC_BATCH, OCT_T_BATCH>,
+                          (const void *)k_octree_lds<OCT_PC_SMALL, OCT_T_SMALL>}) {
         const hipError_t e = hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, bytes);
         if (e != hipSuccess) return e;
     }
