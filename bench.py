@@ -44,8 +44,8 @@ METRIC_EXTRACT = "frames/sec ORBextractor only, 1241×376 2000feat 8lvl (configs
 
 
 # serial-pass PMC profiles of the bench lines (tools/round_prof.sh), copied from the run dirs
-PMC_MONO = "r06d_pmc_kernels.json"
-PMC_STEREO = "r06d_stereo_pmc_kernels.json"
+PMC_MONO = "r06e_pmc_kernels.json"
+PMC_STEREO = "r06e_stereo_pmc_kernels.json"
 
 
 def kernel_algo_bytes(name, B, npairs, ncand, nkp, launches_per_step, ndepth=0, blur_plan=None):
