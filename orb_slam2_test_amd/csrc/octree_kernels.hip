@@ -31,7 +31,7 @@ namespace orbg {
 // level on an idle chip: more lanes per phase), batches OCT_T_BATCH
 #define OCT_T NT
 #ifndef OCT_T_BATCH
-#define OCT_T_BATCH 256  // batches: 0.612 -> 0.787 ms serial, but the pipelined step 5.42 -> 5.37 ms (r06bk)
+#define OCT_T_BATCH 256  // batches: 0.612 -> 0.787 ms serial, but the pipelined step 5.42 -> 5.37 ms (r06bl; 128: 5.52, r06bm)
 #endif
 #define OCT_T_SMALL 512
 #define OCT_CODE_DEPTH 14
