@@ -44,7 +44,7 @@ namespace orbg {
 #define OCT_PC_SMALL 8  // (16: +5 us per B = 1 extraction, profiles/r06an_single_knobs.txt)
 #endif
 #ifndef OCT_PC_BATCH
-#define OCT_PC_BATCH 8  // at 256 threads: 4 -> 8 step 5.340-5.352 -> 5.317-5.334 ms, serial octree 0.787 -> 0.737 (r06bn)
+#define OCT_PC_BATCH 8  // at 256 threads: 4 -> 8 step 5.340-5.352 -> 5.317-5.334 ms, serial octree 0.787 -> 0.737 (r06bn; 16: 5.39, r06bp)
 #endif
 
 #define OCT_NBUCKET 16384  // counting-sort buckets: root (4 bits) + first 5 quadtree digits
